@@ -1,0 +1,282 @@
+"""Synchronous actor-critic trainers: A2C and PPO-clip over a device-resident env bank.
+
+One *update* = collect a ``[T, N]`` rollout (batched policy inference + one env-bank kernel per step), estimate
+returns/advantages (n-step or GAE), then learn:
+  * ``a2c``: one full-batch gradient step (as the reference: ``Basic_AC/run_AC.py:250-251``);
+  * ``ppo``: ``ppo_epochs`` x ``ppo_minibatches`` clipped-surrogate steps.
+
+Reference features kept: KL-proxy + entropy regularised actor loss, per-batch advantage normalisation,
+element-wise gradient clipping, TF-semantics Adam, KL-adaptive actor lr (device-side), log10 annealing of the
+entropy/KL coefficients, the reference Logger format, EV before/after.
+
+Execution: all state lives on the device; nothing in ``collect``/``learn`` reads back to the host, so on a GPU
+the whole update is captured once as a hipGraph (``torch.cuda.CUDAGraph``) and replayed -- the host issues one
+graph launch per update. Data parallelism (sync DP over RCCL) plugs in between backward and the optimiser step
+(:mod:`..parallel.dp`); with ``overlap="lag1"`` the gradient all-reduce runs on a side stream while the next
+rollout is collected.
+
+The CNN family on GPU can instead run the hand-written HIP engine (:mod:`.engine`) which replaces autograd with
+explicit fused forward/backward kernels.
+"""
+from __future__ import annotations
+
+import math
+import os
+import time
+
+import torch
+
+from .. import _native
+from .. import envs as E
+from ..config import TrainConfig
+from ..models.policy import build_model
+from ..ops import returns as R
+from ..ops.optim import FlatParams, make_optimizer
+from ..utils.logger import Logger
+from ..utils.schedule import DeviceKLAdaptiveLR, RegularizerSchedule
+from ..utils.stats import var_accounted_for_tensor
+from . import losses as L
+from .storage import RolloutStorage
+
+KEY_ENV_BITS = 20
+
+
+class ActorCriticTrainer:
+    def __init__(self, cfg: TrainConfig, env=None, model=None, dp=None):
+        self.cfg = cfg
+        self.device = torch.device(cfg.device)
+        self.dp = dp
+        self.rank = dp.rank if dp is not None else 0
+        self.world = dp.world_size if dp is not None else 1
+        fs = 4 if "Pong" in cfg.env or "Breakout" in cfg.env else cfg.frames
+        self.env = env if env is not None else E.make(
+            cfg.env, cfg.num_envs, device=self.device, seed=cfg.seed, env_offset=self.rank * cfg.num_envs,
+            frame_stack=fs)
+        self.model = (model if model is not None else
+                      build_model(self.env, cfg.model, cfg.model_variant, seed=cfg.seed)).to(self.device)
+        self.flat = FlatParams(self.model.param_groups(), self.device)
+        if dp is not None:
+            dp.broadcast_params(self.flat)
+        self.opts = {}
+        for g in self.flat.groups:
+            if g == "critic":
+                self.opts[g] = make_optimizer(cfg.optimizer, self.flat, g, cfg.critic_lr, cfg.critic_clip_value,
+                                              cfg.max_grad_norm)
+            else:
+                self.opts[g] = make_optimizer(cfg.optimizer, self.flat, g, cfg.lr, cfg.clip_value, cfg.max_grad_norm)
+        self.actor_opt = self.opts.get("actor", self.opts.get("shared"))
+        T, N = cfg.n_steps, self.env.num_envs
+        act_shape = () if self.env.is_discrete else tuple(self.env.action_space.shape)
+        act_dtype = torch.int32 if self.env.is_discrete else torch.float32
+        self.storage = RolloutStorage(T, N, self.env.obs_shape, self.env.obs_dtype, act_shape, act_dtype,
+                                      self.device)
+        self.env.reset(out=self.storage.obs[0])
+        dev = self.device
+        self.ent_coef = torch.tensor(cfg.ent_coef, device=dev)
+        self.kl_coef = torch.tensor(cfg.kl_coef, device=dev)
+        self.lr_ctrl = DeviceKLAdaptiveLR(cfg.desired_kl, cfg.min_lr, cfg.max_lr) if cfg.kl_adaptive_lr else None
+        self.reg_sched = RegularizerSchedule() if cfg.anneal_regularizers else None
+        self.policy_seed = (cfg.seed * 7919 + 17) & 0xFFFFFFFF
+        self.update_counter = torch.zeros((), dtype=torch.int64, device=dev)
+        self.stats = {k: torch.zeros((), device=dev) for k in
+                      ("act_loss", "crit_loss", "kl", "entropy", "ev_before", "ev_after", "clipfrac")}
+        self.iteration = 0
+        self.env_steps = 0
+        self.graph = None
+        self.logger = None
+        if self.rank == 0 and cfg.outdir:
+            self.logger = Logger(cfg.outdir, legacy_step_index=cfg.legacy_step_index, metrics_path=cfg.metrics_path,
+                                 quiet=cfg.quiet)
+
+    # ------------------------------------------------------------------ rollout
+    def _keys(self):
+        return self.env.tg * (1 << KEY_ENV_BITS) + self.env.env_ids
+
+    @torch.no_grad()
+    def collect(self):
+        st, env, model = self.storage, self.env, self.model
+        for t in range(st.T):
+            obs_t = st.obs[t]
+            pi, v = model(obs_t)
+            keys = self._keys()
+            a, logp, ent = model.sample(pi, keys, self.policy_seed)
+            st.actions[t].copy_(a.view_as(st.actions[t]))
+            st.logp[t].copy_(logp)
+            st.entropy[t].copy_(ent)
+            st.values[t].copy_(v)
+            env.step(a, prev_obs=obs_t, obs_out=st.obs[t + 1])
+            st.rewards[t].copy_(env.reward)
+            st.dones[t].copy_(env.done)
+            st.truncated[t].copy_(env.truncated)
+        st.values[st.T].copy_(model.value(st.obs[st.T]))
+
+    # ------------------------------------------------------------------ returns
+    def compute_returns(self):
+        cfg, st = self.cfg, self.storage
+        dones = st.dones
+        if cfg.bootstrap_on_timeout:
+            dones = dones & (1 - st.truncated)
+        if cfg.returns == "gae":
+            ret, adv = R.gae(st.rewards, st.values, dones, cfg.gamma, cfg.gae_lambda)
+        else:
+            ret, adv = R.nstep_returns(st.rewards, st.values, dones, cfg.gamma, cfg.look_ahead)
+        return ret.reshape(-1), adv.reshape(-1)
+
+    # ------------------------------------------------------------------ learning
+    def _loss(self, obs, actions, logp_old, adv, ret, v_old=None):
+        cfg = self.cfg
+        logp, ent, v = self.model.evaluate(obs, actions)
+        if cfg.algo == "ppo":
+            a_loss, pg, kl, entm, clipfrac = L.ppo_actor_loss(logp, logp_old, adv, ent, cfg.ppo_clip, self.ent_coef,
+                                                            self.kl_coef)
+        else:
+            a_loss, pg, kl, entm = L.actor_loss(logp, logp_old, adv, ent, self.kl_coef, self.ent_coef)
+            clipfrac = torch.zeros((), device=self.device)
+        c_loss = L.value_loss(v, ret, v_old, cfg.ppo_value_clip if cfg.algo == "ppo" else None)
+        shared = "shared" in self.flat.groups
+        total = a_loss + (cfg.vf_coef * c_loss if shared else c_loss)
+        return total, a_loss, c_loss, kl, entm, clipfrac
+
+    def _apply_grads(self):
+        if self.dp is not None:
+            self.dp.allreduce_grads(self.flat)
+        for opt in self.opts.values():
+            opt.step()
+
+    def learn(self, ret, adv):
+        cfg, st = self.cfg, self.storage
+        obs, actions, logp_old = st.flat("obs"), st.flat("actions"), st.flat("logp")
+        v_old = st.flat("values")
+        self.stats["ev_before"].copy_(var_accounted_for_tensor(ret, v_old))
+        if cfg.norm_adv:
+            if self.dp is not None:
+                adv = self.dp.normalize_advantages(adv)
+            else:
+                adv = R.normalize_advantages(adv)
+        if cfg.algo == "ppo":
+            B = obs.shape[0]
+            mb = B // cfg.ppo_minibatches
+            idx = torch.arange(B, device=self.device, dtype=torch.int64)
+            for ep in range(cfg.ppo_epochs):
+                h = E.rng.hash_u32(self.policy_seed, idx, self.update_counter * 64 + ep, 7)
+                perm = torch.argsort(h)
+                for k in range(cfg.ppo_minibatches):
+                    sel = perm[k * mb:(k + 1) * mb]
+                    self.flat.zero_grad()
+                    total, a_loss, c_loss, kl, ent, cf = self._loss(obs[sel], actions[sel], logp_old[sel], adv[sel],
+                                                                    ret[sel], v_old[sel])
+                    total.backward()
+                    self._apply_grads()
+        else:
+            self.flat.zero_grad()
+            total, a_loss, c_loss, kl, ent, cf = self._loss(obs, actions, logp_old, adv, ret)
+            total.backward()
+            self._apply_grads()
+        self.stats["act_loss"].copy_(a_loss.detach())
+        self.stats["crit_loss"].copy_(c_loss.detach())
+        self.stats["entropy"].copy_(ent.detach())
+        self.stats["clipfrac"].copy_(cf.detach())
+        self.update_counter += 1
+        if self.lr_ctrl is not None or cfg.kl_coef > 0:
+            self._post_update_kl(obs, actions, logp_old, ret)
+        else:
+            self.stats["kl"].copy_(kl.detach())
+
+    @torch.no_grad()
+    def _post_update_kl(self, obs, actions, logp_old, ret):
+        """KL proxy and EV on the *updated* parameters (``Basic_AC/run_AC.py:257-258``), then the lr rule."""
+        logp, _, v = self.model.evaluate(obs, actions)
+        kl = ((logp_old - logp) ** 2).mean()
+        if self.dp is not None:
+            kl = self.dp.mean_scalar(kl)
+        self.stats["kl"].copy_(kl)
+        self.stats["ev_after"].copy_(var_accounted_for_tensor(ret, v))
+        if self.lr_ctrl is not None:
+            self.lr_ctrl.update_(self.actor_opt.lr, kl)
+
+    def update_body(self):
+        self.collect()
+        ret, adv = self.compute_returns()
+        self.learn(ret, adv)
+        self.storage.roll_over()
+
+    # ------------------------------------------------------------------ driver
+    def _can_capture(self):
+        return (self.cfg.cuda_graph and self.device.type == "cuda" and self.dp is None)
+
+    def capture(self, warmup=2):
+        """Capture one whole update (rollout + returns + learn) as a hipGraph."""
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self.update_body()
+        torch.cuda.current_stream().wait_stream(s)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.update_body()
+        return self.graph
+
+    def step(self):
+        """One update (graph replay when captured)."""
+        if self.reg_sched is not None:
+            e, k = self.reg_sched.entropy_coef(self.iteration), self.reg_sched.kl_coef(self.iteration)
+            if e is not None:
+                self.ent_coef.fill_(e)
+            if k is not None:
+                self.kl_coef.fill_(k)
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self.update_body()
+        self.iteration += 1
+        self.env_steps += self.cfg.n_steps * self.env.num_envs * self.world
+
+    def log(self, i, print_tog):
+        if self.logger is None:
+            return
+        s = {k: float(v) for k, v in self.stats.items()}
+        avg_rew, n_ep, ep_len = self.env.drain_episode_stats()
+        self.logger(i, act_loss=s["act_loss"], circ_loss=math.sqrt(max(s["crit_loss"], 0.0)), kl_dist=s["kl"],
+                    avg_rew=avg_rew, print_tog=print_tog, act_lr=self.actor_opt.get_lr(), avg_ent=s["entropy"],
+                    worker_id=self.rank, ev_before=s["ev_before"], ev_after=s["ev_after"])
+        return s
+
+    def train(self, num_updates=None, callback=None):
+        cfg = self.cfg
+        n = cfg.total_updates if num_updates is None else num_updates
+        if self._can_capture() and self.graph is None:
+            self.capture()
+        t0 = time.time()
+        history = []
+        for i in range(n):
+            self.step()
+            it = self.iteration - 1
+            if cfg.stdout_freq and it % cfg.stdout_freq == 0:
+                s = self.log(it, print_tog=not cfg.quiet)
+                if s is not None:
+                    history.append(dict(iteration=it, **s))
+                    if self.logger is not None:
+                        el = time.time() - t0
+                        self.logger.log_metrics(iteration=it, env_steps=self.env_steps,
+                                                env_steps_per_sec=self.env_steps / max(el, 1e-9), **s)
+            if self.logger is not None and cfg.flush_every and it % cfg.flush_every == cfg.flush_every // 2:
+                self.logger.flush()
+            if cfg.save_every and it % cfg.save_every == 0 and self.rank == 0 and cfg.checkpoint_dir:
+                self.save_checkpoint()
+            if callback is not None:
+                callback(self, it)
+        return history
+
+    # ------------------------------------------------------------------ checkpoints
+    def save_checkpoint(self, path=None):
+        from ..ckpt import save_trainer
+        return save_trainer(self, path)
+
+    def load_checkpoint(self, path):
+        from ..ckpt import load_trainer
+        return load_trainer(self, path)
+
+    def close(self):
+        if self.logger is not None:
+            self.logger.close()

@@ -1,0 +1,125 @@
+"""Typed training configuration + presets.
+
+The reference configures itself with argparse flags and module constants (defaults table: SURVEY §2.6). Here
+one dataclass carries everything; presets mirror the reference defaults (``basic_ac``, ``a3c``) and the
+BASELINE.json configs (``cartpole_cpu``, ``pong_a2c``, ``breakout_ppo``, ``a2c_dp8``, ``mujoco_ppo_dp8``).
+"""
+from __future__ import annotations
+
+import dataclasses
+from dataclasses import dataclass, field
+
+
+@dataclass
+class TrainConfig:
+    # -- problem ---------------------------------------------------------------------------------------------
+    env: str = "Pendulum-v0"
+    algo: str = "a2c"                 # a2c | ppo | a3c | basic_ac (reference-parity episode-batched trainer)
+    num_envs: int = 1                 # envs per rank / GPU
+    n_steps: int = 5                  # rollout length T
+    frames: int = 1                   # frame stack for vector envs (Atari envs always stack 4)
+    model: str = "auto"               # auto | mlp | cnn
+    model_variant: str = "basic"      # basic | a3c (reference divergences)
+    seed: int = 12321
+    device: str = "cpu"
+    # -- returns -----------------------------------------------------------------------------------------------
+    gamma: float = 0.99
+    returns: str = "nstep"            # nstep (PathAdv generalisation) | gae
+    look_ahead: int | None = None     # n-step truncation L (reference: 40); None = whole rollout
+    gae_lambda: float = 0.95
+    norm_adv: bool = False
+    bootstrap_on_timeout: bool = False
+    # -- losses ------------------------------------------------------------------------------------------------
+    ent_coef: float = 0.01            # reference "gamma" (Basic_AC/policies.py:38)
+    kl_coef: float = 0.0              # reference "beta" (squared log-prob drift proxy)
+    vf_coef: float = 0.5
+    # -- optimiser ---------------------------------------------------------------------------------------------
+    optimizer: str = "adam"           # adam | rmsprop
+    lr: float = 7e-4                  # shared-model lr / actor lr
+    critic_lr: float = 1e-3           # separate-critic lr (reference 0.001)
+    clip_value: float | None = None   # element-wise grad clip (reference actor: 1.0 Basic / 0.1 A3C)
+    critic_clip_value: float | None = None
+    max_grad_norm: float | None = 0.5
+    # -- reference regularisation machinery -----------------------------------------------------------------------
+    kl_adaptive_lr: bool = False
+    desired_kl: float = 0.002
+    min_lr: float = 1e-6
+    max_lr: float = 1.0
+    anneal_regularizers: bool = False  # log10 schedules of ent/kl coefs (Basic_AC/run_AC.py:181-182)
+    # -- PPO ---------------------------------------------------------------------------------------------------
+    ppo_epochs: int = 4
+    ppo_minibatches: int = 4
+    ppo_clip: float = 0.1
+    ppo_value_clip: float | None = None
+    # -- execution -----------------------------------------------------------------------------------------------
+    dtype: str = "bf16"               # compute dtype of the GPU engine (fp32 masters always)
+    engine: str = "auto"              # auto | native (hand-written HIP engine) | torch (autograd reference)
+    cuda_graph: bool = True
+    total_updates: int = 1000
+    # -- distributed -----------------------------------------------------------------------------------------------
+    dist_backend: str = "auto"        # auto -> nccl (RCCL) on GPU, gloo on CPU
+    overlap: str = "strict"           # strict | lag1 (all-reduce overlapped with next rollout, policy lag 1)
+    ps_num: int = 1                   # A3C parameter-server ranks
+    # -- reference episode-batched trainer (basic_ac) -------------------------------------------------------------
+    max_rolls: int = 7
+    max_path_length: int | None = None
+    ep_length_stop: int | None = None
+    # -- logging / checkpoints ---------------------------------------------------------------------------------------
+    outdir: str = "log.txt"
+    metrics_path: str | None = None
+    stdout_freq: int = 20
+    flush_every: int = 100
+    save_every: int = 600
+    checkpoint_dir: str = "tmp/checkpoints"
+    keep_checkpoints: int = 3
+    quiet: bool = False
+    legacy_step_index: bool = False
+    tboard: bool = False
+    mode: str = "train"               # train | debug | debug-light | debug-full
+
+    def replace(self, **kw):
+        return dataclasses.replace(self, **kw)
+
+    def to_dict(self):
+        return dataclasses.asdict(self)
+
+
+PRESETS = {
+    # Basic_AC/run_AC.py defaults
+    "basic_ac": dict(algo="basic_ac", env="Pendulum-v0", gamma=0.98, look_ahead=40, norm_adv=True, ent_coef=0.01,
+                     kl_coef=1.0, lr=0.005, critic_lr=0.001, clip_value=1.0, max_grad_norm=None,
+                     kl_adaptive_lr=True, max_lr=1.0, anneal_regularizers=True, model_variant="basic",
+                     optimizer="adam", device="cpu", cuda_graph=False),
+    # A3C/process.py defaults
+    "a3c": dict(algo="a3c", env="Pendulum-v0", gamma=0.98, look_ahead=40, norm_adv=True, ent_coef=0.01,
+                kl_coef=1.0, lr=0.005, critic_lr=0.001, clip_value=0.1, max_grad_norm=None, kl_adaptive_lr=True,
+                max_lr=0.1, anneal_regularizers=True, model_variant="a3c", optimizer="adam", device="cpu",
+                cuda_graph=False),
+    # BASELINE config 1
+    "cartpole_cpu": dict(algo="a2c", env="CartPole-v1", num_envs=1, n_steps=5, gamma=0.99, model="mlp",
+                         lr=1e-3, critic_lr=5e-3, norm_adv=True, device="cpu", cuda_graph=False,
+                         max_grad_norm=0.5),
+    # BASELINE config 2 (headline metric)
+    "pong_a2c": dict(algo="a2c", env="PongNoFrameskip-v4", num_envs=32, n_steps=5, gamma=0.99, model="cnn",
+                     optimizer="rmsprop", lr=7e-4, ent_coef=0.01, vf_coef=0.5, max_grad_norm=0.5,
+                     device="cuda", dtype="bf16"),
+    # BASELINE config 3
+    "breakout_ppo": dict(algo="ppo", env="BreakoutNoFrameskip-v4", num_envs=128, n_steps=128, gamma=0.99,
+                         returns="gae", gae_lambda=0.95, norm_adv=True, model="cnn", optimizer="adam", lr=2.5e-4,
+                         ppo_epochs=4, ppo_minibatches=4, ppo_clip=0.1, ent_coef=0.01, vf_coef=0.5,
+                         max_grad_norm=0.5, device="cuda", dtype="bf16"),
+    # BASELINE config 4
+    "a2c_dp8": dict(algo="a2c", env="PongNoFrameskip-v4", num_envs=32, n_steps=5, gamma=0.99, model="cnn",
+                    optimizer="rmsprop", lr=7e-4, max_grad_norm=0.5, device="cuda", dtype="bf16"),
+    # BASELINE config 5
+    "mujoco_ppo_dp8": dict(algo="ppo", env="HalfCheetahShape-v0", num_envs=64, n_steps=256, gamma=0.99,
+                           returns="gae", gae_lambda=0.95, norm_adv=True, model="mlp", optimizer="adam", lr=3e-4,
+                           critic_lr=1e-3, ppo_epochs=10, ppo_minibatches=32, ppo_clip=0.2, ent_coef=0.0,
+                           vf_coef=0.5, max_grad_norm=0.5, device="cuda", dtype="fp32"),
+}
+
+
+def preset(name, **overrides) -> TrainConfig:
+    kw = dict(PRESETS[name])
+    kw.update(overrides)
+    return TrainConfig(**kw)

@@ -1,0 +1,175 @@
+"""Flat parameter slabs and fused optimisers (kernel K10 of SURVEY §2.4).
+
+The reference runs ``clip_by_value`` + ``ApplyAdam`` per variable (17 variables for Pendulum,
+``Basic_AC/policies.py:79-82``). Here every parameter of a model is a *view into one contiguous fp32 slab*
+and so is its gradient; an optimiser step is ONE kernel over a slab segment:
+
+    g = clip(g, -c, c)                      (element-wise, optional; reference: +-1 Basic, +-0.1 A3C)
+    g *= min(1, max_norm / ||g||)           (optional global-norm clip; norm from a device reduction)
+    m = b1 m + (1-b1) g;  v = b2 v + (1-b2) g^2
+    p -= lr * sqrt(1-b2^t)/(1-b1^t) * m / (sqrt(v) + eps)      (TF1 AdamOptimizer "epsilon hat" form)
+
+``lr`` and the step ``t`` are device scalars, so the KL-adaptive lr controller and the schedules update them
+without a host sync and the step can be captured in a hipGraph. The flat gradient slab is also exactly the
+buffer the data-parallel engine all-reduces (one RCCL call per update, :mod:`..parallel.dp`). Optionally the
+same kernel writes a bf16 shadow copy of the parameters for the MFMA forward/backward kernels.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import _native
+
+
+class FlatParams:
+    """Re-homes ``params`` into one fp32 slab (``data``) with a matching gradient slab (``grad``).
+
+    ``groups`` maps a group name to ``(start, end)`` element offsets; params are laid out group by group.
+    """
+
+    def __init__(self, named_groups, device=None):
+        self.groups = {}
+        self.params = []
+        total = 0
+        for name, plist in named_groups.items():
+            start = total
+            for p in plist:
+                self.params.append(p)
+                total += p.numel()
+            self.groups[name] = (start, total)
+        dev = device if device is not None else (self.params[0].device if self.params else "cpu")
+        self.numel = total
+        self.data = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros(total, dtype=torch.float32, device=dev)
+        off = 0
+        self.offsets = []
+        for p in self.params:
+            n = p.numel()
+            self.data[off:off + n].copy_(p.data.reshape(-1).to(dev, torch.float32))
+            p.data = self.data[off:off + n].view(p.shape)
+            p.grad = self.grad[off:off + n].view(p.shape)
+            self.offsets.append(off)
+            off += n
+
+    def zero_grad(self):
+        self.grad.zero_()
+
+    def segment(self, name):
+        s, e = self.groups[name]
+        return self.data[s:e], self.grad[s:e]
+
+
+class FusedAdam:
+    """Adam (TF1 semantics) + optional element-wise / global-norm gradient clipping over a slab segment."""
+
+    def __init__(self, flat: FlatParams, group="shared", lr=1e-3, betas=(0.9, 0.999), eps=1e-8, clip_value=None,
+                 max_grad_norm=None, bf16_shadow=None):
+        self.flat = flat
+        self.group = group
+        s, e = flat.groups[group]
+        self.start, self.end = s, e
+        dev = flat.data.device
+        self.p, self.g = flat.data[s:e], flat.grad[s:e]
+        self.m = torch.zeros_like(self.p)
+        self.v = torch.zeros_like(self.p)
+        self.lr = torch.tensor(float(lr), dtype=torch.float32, device=dev)
+        self.t = torch.zeros((), dtype=torch.float32, device=dev)
+        self.b1, self.b2 = betas
+        self.eps = eps
+        self.clip_value = clip_value
+        self.max_grad_norm = max_grad_norm
+        self.gnorm = torch.zeros((), dtype=torch.float32, device=dev)
+        self.shadow = bf16_shadow  # optional bf16 tensor of the same numel (written by the native kernel)
+
+    def set_lr(self, lr):
+        self.lr.fill_(float(lr))
+
+    def get_lr(self):
+        return float(self.lr)
+
+    @torch.no_grad()
+    def step(self):
+        if _native.use_native(self.p):
+            self._native_step()
+        else:
+            self._torch_step()
+
+    def _native_step(self):
+        ops = _native.require()
+        if self.max_grad_norm is not None:
+            ops.sumsq(self.g, self.gnorm)
+        ops.adam_step(self.p, self.g, self.m, self.v, self.lr, self.t, self.gnorm,
+                      self.shadow if self.shadow is not None else torch.empty(0, device=self.p.device),
+                      float(self.b1), float(self.b2), float(self.eps),
+                      float(self.clip_value) if self.clip_value is not None else -1.0,
+                      float(self.max_grad_norm) if self.max_grad_norm is not None else -1.0)
+
+    def _torch_step(self):
+        g = self.g
+        if self.clip_value is not None:
+            g = torch.clamp(g, -self.clip_value, self.clip_value)
+        if self.max_grad_norm is not None:
+            n = torch.sqrt((g * g).sum())
+            self.gnorm.copy_(n * n)
+            g = g * torch.clamp(self.max_grad_norm / (n + 1e-6), max=1.0)
+        self.t += 1
+        self.m.mul_(self.b1).add_(g, alpha=1 - self.b1)
+        self.v.mul_(self.b2).addcmul_(g, g, value=1 - self.b2)
+        lr_t = self.lr * torch.sqrt(1 - self.b2 ** self.t) / (1 - self.b1 ** self.t)
+        self.p.sub_(lr_t * self.m / (torch.sqrt(self.v) + self.eps))
+        if self.shadow is not None:
+            self.shadow.copy_(self.p)
+
+    def state_dict(self):
+        return {"m": self.m, "v": self.v, "t": self.t, "lr": self.lr}
+
+    def load_state_dict(self, sd):
+        for k in ("m", "v", "t", "lr"):
+            if k in sd:
+                getattr(self, k).copy_(torch.as_tensor(sd[k]).to(getattr(self, k).device))
+
+
+class FusedRMSprop(FusedAdam):
+    """RMSprop (TF semantics: ``ms = rho ms + (1-rho) g^2; p -= lr g / sqrt(ms + eps)``), same slab mechanics.
+
+    The usual Atari A2C optimiser (alpha=0.99, eps=1e-5, lr=7e-4, global-norm clip 0.5).
+    """
+
+    def __init__(self, flat, group="shared", lr=7e-4, alpha=0.99, eps=1e-5, clip_value=None, max_grad_norm=None,
+                 bf16_shadow=None):
+        super().__init__(flat, group, lr, (0.0, alpha), eps, clip_value, max_grad_norm, bf16_shadow)
+        self.alpha = alpha
+
+    def _native_step(self):
+        ops = _native.require()
+        if self.max_grad_norm is not None:
+            ops.sumsq(self.g, self.gnorm)
+        ops.rmsprop_step(self.p, self.g, self.v, self.lr, self.gnorm,
+                         self.shadow if self.shadow is not None else torch.empty(0, device=self.p.device),
+                         float(self.alpha), float(self.eps),
+                         float(self.clip_value) if self.clip_value is not None else -1.0,
+                         float(self.max_grad_norm) if self.max_grad_norm is not None else -1.0)
+
+    def _torch_step(self):
+        g = self.g
+        if self.clip_value is not None:
+            g = torch.clamp(g, -self.clip_value, self.clip_value)
+        if self.max_grad_norm is not None:
+            n = torch.sqrt((g * g).sum())
+            self.gnorm.copy_(n * n)
+            g = g * torch.clamp(self.max_grad_norm / (n + 1e-6), max=1.0)
+        self.t += 1
+        self.v.mul_(self.alpha).addcmul_(g, g, value=1 - self.alpha)
+        self.p.sub_(self.lr * g / torch.sqrt(self.v + self.eps))
+        if self.shadow is not None:
+            self.shadow.copy_(self.p)
+
+
+def make_optimizer(name, flat, group, lr, clip_value=None, max_grad_norm=None, bf16_shadow=None):
+    if name == "adam":
+        return FusedAdam(flat, group, lr, clip_value=clip_value, max_grad_norm=max_grad_norm,
+                         bf16_shadow=bf16_shadow)
+    if name == "rmsprop":
+        return FusedRMSprop(flat, group, lr, clip_value=clip_value, max_grad_norm=max_grad_norm,
+                            bf16_shadow=bf16_shadow)
+    raise ValueError(name)

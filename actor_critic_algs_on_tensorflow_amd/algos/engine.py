@@ -1,0 +1,152 @@
+"""Native GPU engine for the Nature-CNN actor-critic: explicit forward / backward on hand-written gfx950 kernels.
+
+Autograd is replaced by a fixed schedule of launches over preallocated buffers (static addresses => the whole
+rollout step and the whole learner step are hipGraph-capturable). Per batch of B observations:
+
+forward   im2col_u8(obs)            -> col1 [B*400, 256]   (uint8 NCHW frames, /255 folded in)
+          gemm(col1, W1^T) +b relu  -> y1   [B*400, 32]    (NHWC bf16)
+          im2col_nhwc(y1)           -> col2 [B*81, 512]
+          gemm(col2, W2^T) +b relu  -> y2   [B*81, 64]
+          im2col_nhwc(y2)           -> col3 [B*49, 576]
+          gemm(col3, W3^T) +b relu  -> y3   [B*49, 64] == [B, 3136]
+          gemm(y3, Wfc)    +b relu  -> h    [B, 512]       (slab split-K for small B)
+          gemm(h, Wh)      +b       -> z    [B, A+1] fp32  (logits | value)
+loss      ac_loss(z, ...)           -> dz   [B, A+1] bf16, stats
+backward  dWh += h^T dz ; dbh += colsum(dz)
+          dh  = (dz Wh^T) * (h > 0)             (+ colsum -> dbfc)
+          dWfc += y3^T dh
+          dy3 = (dh Wfc^T) * (y3 > 0)           (+ per-channel colsum -> db3)
+          dW3 += dy3^T col3 ; dcol3 = dy3 W3 ; dy2 = col2im(dcol3) * (y2 > 0) (+ colsum -> db2)
+          dW2 += dy2^T col2 ; dcol2 = dy2 W2 ; dy1 = col2im(dcol2) * (y1 > 0) (+ colsum -> db1)
+          dW1 += dy1^T col1
+Weight gradients accumulate (split-K atomics) straight into the fp32 gradient slab of :class:`FlatParams` (zeroed
+once per learner step), which is also the buffer the data-parallel engine all-reduces. Weights are read from the
+bf16 shadow of the slab that the fused optimiser rewrites every step.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import _native
+from ..ops import gemm as G
+
+H0 = 84
+
+
+class _Bufs:
+    """Activation / gradient buffers for one batch size."""
+
+    def __init__(self, B, A1, dev, with_grad):
+        bf = torch.bfloat16
+        self.B = B
+        self.col1 = torch.empty(B * 400, 256, dtype=bf, device=dev)
+        self.y1 = torch.empty(B * 400, 32, dtype=bf, device=dev)
+        self.col2 = torch.empty(B * 81, 512, dtype=bf, device=dev)
+        self.y2 = torch.empty(B * 81, 64, dtype=bf, device=dev)
+        self.col3 = torch.empty(B * 49, 576, dtype=bf, device=dev)
+        self.y3 = torch.empty(B * 49, 64, dtype=bf, device=dev)
+        self.h = torch.empty(B, 512, dtype=bf, device=dev)
+        self.z = torch.empty(B, A1, dtype=torch.float32, device=dev)
+        if with_grad:
+            self.dz = torch.empty(B, A1, dtype=bf, device=dev)
+            self.dh = torch.empty(B, 512, dtype=bf, device=dev)
+            self.dy3 = torch.empty(B * 49, 64, dtype=bf, device=dev)
+            self.dcol3 = torch.empty(B * 49, 576, dtype=bf, device=dev)
+            self.dy2 = torch.empty(B * 81, 64, dtype=bf, device=dev)
+            self.dcol2 = torch.empty(B * 81, 512, dtype=bf, device=dev)
+            self.dy1 = torch.empty(B * 400, 32, dtype=bf, device=dev)
+            self.stats = torch.zeros(8, dtype=torch.float32, device=dev)
+
+
+class CNNEngine:
+    """Explicit forward/backward of :class:`..models.policy.CNNActorCritic` over a :class:`FlatParams` slab."""
+
+    def __init__(self, model, flat, shadow):
+        net = model.net
+        self.model = model
+        self.flat = flat
+        self.shadow = shadow
+        self.A = net.num_actions
+        self.A1 = self.A + 1
+        self.dev = flat.data.device
+        self.ws = G.GemmWorkspace(self.dev)
+        tr = net.trunk
+        assert tr.conv1.cin == 4 and tr.conv1.layout == "oihw" and tr.conv2.layout == "ohwi"
+        idx = {id(p): i for i, p in enumerate(flat.params)}
+
+        def views(p):
+            i = idx[id(p)]
+            off, n = flat.offsets[i], p.numel()
+            return (flat.data[off:off + n], flat.grad[off:off + n], shadow[off:off + n])
+
+        self.W1, self.gW1, self.sW1 = views(tr.conv1.weight)
+        self.b1, self.gb1, _ = views(tr.conv1.bias)
+        self.W2, self.gW2, self.sW2 = views(tr.conv2.weight)
+        self.b2, self.gb2, _ = views(tr.conv2.bias)
+        self.W3, self.gW3, self.sW3 = views(tr.conv3.weight)
+        self.b3, self.gb3, _ = views(tr.conv3.bias)
+        self.Wfc, self.gWfc, self.sWfc = views(tr.fc.kernel)
+        self.bfc, self.gbfc, _ = views(tr.fc.bias)
+        self.Wh, self.gWh, self.sWh = views(net.heads.kernel)
+        self.bh, self.gbh, _ = views(net.heads.bias)
+        self._bufs = {}
+
+    def bufs(self, B, with_grad=False):
+        key = (B, with_grad)
+        if key not in self._bufs:
+            self._bufs[key] = _Bufs(B, self.A1, self.dev, with_grad)
+        return self._bufs[key]
+
+    # ------------------------------------------------------------------------------------------------ forward
+    def forward(self, obs, b: _Bufs):
+        """obs uint8 [B, 4, 84, 84] -> b.z fp32 [B, A+1] (logits | value)."""
+        B = b.B
+        ws = self.ws
+        G.im2col_u8(obs, b.col1, 8, 8, 4)
+        G.gemm(b.col1, 256, True, self.sW1, 256, True, b.y1, 32, 1, B * 400, 32, 256, bias=self.b1, relu=True,
+               workspace=ws)
+        G.im2col_nhwc(b.y1, b.col2, B, 20, 20, 32, 4, 4, 2)
+        G.gemm(b.col2, 512, True, self.sW2, 512, True, b.y2, 64, 1, B * 81, 64, 512, bias=self.b2, relu=True,
+               workspace=ws)
+        G.im2col_nhwc(b.y2, b.col3, B, 9, 9, 64, 3, 3, 1)
+        G.gemm(b.col3, 576, True, self.sW3, 576, True, b.y3, 64, 1, B * 49, 64, 576, bias=self.b3, relu=True,
+               workspace=ws)
+        G.gemm(b.y3, 3136, True, self.sWfc, 512, False, b.h, 512, 1, B, 512, 3136, bias=self.bfc, relu=True,
+               workspace=ws)
+        G.gemm(b.h, 512, True, self.sWh, self.A1, False, b.z, self.A1, 0, B, self.A1, 512, bias=self.bh,
+               workspace=ws)
+        return b.z
+
+    # ------------------------------------------------------------------------------------------------ backward
+    def backward(self, b: _Bufs):
+        """Accumulates d(loss)/d(params) into the gradient slab from ``b.dz`` (written by the loss kernel)."""
+        B, A1, ws = b.B, self.A1, self.ws
+        ops = _native.require()
+        # heads
+        G.gemm(b.h, 512, False, b.dz, A1, False, self.gWh, A1, 2, 512, A1, B, workspace=ws)
+        ops.colsum_bf16(b.dz, B, A1, A1, self.gbh)
+        G.gemm(b.dz, A1, True, self.sWh, A1, True, b.dh, 512, 1, B, 512, A1, mask=b.h, ldm=512, colsum=self.gbfc,
+               workspace=ws)
+        # fc
+        G.gemm(b.y3, 3136, False, b.dh, 512, False, self.gWfc, 512, 2, 3136, 512, B, workspace=ws)
+        G.gemm(b.dh, 512, True, self.sWfc, 512, True, b.dy3, 3136, 1, B, 3136, 512, mask=b.y3, ldm=3136,
+               colsum=self.gb3, colsum_mod=64, workspace=ws)
+        # conv3
+        G.gemm(b.dy3, 64, False, b.col3, 576, False, self.gW3, 576, 2, 64, 576, B * 49, workspace=ws)
+        G.gemm(b.dy3, 64, True, self.sW3, 576, False, b.dcol3, 576, 1, B * 49, 576, 64, workspace=ws)
+        G.col2im_nhwc(b.dcol3, b.y2, b.dy2, self.gb2, B, 9, 9, 64, 3, 3, 1)
+        # conv2
+        G.gemm(b.dy2, 64, False, b.col2, 512, False, self.gW2, 512, 2, 64, 512, B * 81, workspace=ws)
+        G.gemm(b.dy2, 64, True, self.sW2, 512, False, b.dcol2, 512, 1, B * 81, 512, 64, workspace=ws)
+        G.col2im_nhwc(b.dcol2, b.y1, b.dy1, self.gb1, B, 20, 20, 32, 4, 4, 2)
+        # conv1
+        G.gemm(b.dy1, 32, False, b.col1, 256, False, self.gW1, 256, 2, 32, 256, B * 400, workspace=ws)
+
+    # ------------------------------------------------------------------------------------------------ loss
+    def loss(self, b: _Bufs, actions, logp_old, adv, ret, v_old, ent_coef, kl_coef, vf_coef, ppo_clip, v_clip):
+        B, A, A1 = b.B, self.A, self.A1
+        zl = b.z
+        _native.require().ac_loss(zl, A1, zl[:, A:], A1, actions, None, None, logp_old, adv, ret, v_old, ent_coef,
+                                  kl_coef, float(vf_coef), float(ppo_clip or 0.0), float(v_clip or 0.0), b.dz, A1,
+                                  b.dz[:, A:], A1, None, b.stats, B, A, False)
+        return b.stats

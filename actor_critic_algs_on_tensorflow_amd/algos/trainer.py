@@ -30,6 +30,7 @@ from .. import _native
 from .. import envs as E
 from ..config import TrainConfig
 from ..models.policy import build_model
+from ..ops import distributions as D
 from ..ops import returns as R
 from ..ops.optim import FlatParams, make_optimizer
 from ..utils.logger import Logger
@@ -57,13 +58,23 @@ class ActorCriticTrainer:
         self.flat = FlatParams(self.model.param_groups(), self.device)
         if dp is not None:
             dp.broadcast_params(self.flat)
+        self.engine = None
+        self.shadow = None
+        if self._want_native():
+            from .engine import CNNEngine
+            self.shadow = torch.empty(self.flat.numel, dtype=torch.bfloat16, device=self.device)
+            self.shadow.copy_(self.flat.data)
+            self.engine = CNNEngine(self.model, self.flat, self.shadow)
         self.opts = {}
         for g in self.flat.groups:
+            s, e = self.flat.groups[g]
+            sh = self.shadow[s:e] if self.shadow is not None else None
             if g == "critic":
                 self.opts[g] = make_optimizer(cfg.optimizer, self.flat, g, cfg.critic_lr, cfg.critic_clip_value,
-                                              cfg.max_grad_norm)
+                                              cfg.max_grad_norm, bf16_shadow=sh)
             else:
-                self.opts[g] = make_optimizer(cfg.optimizer, self.flat, g, cfg.lr, cfg.clip_value, cfg.max_grad_norm)
+                self.opts[g] = make_optimizer(cfg.optimizer, self.flat, g, cfg.lr, cfg.clip_value, cfg.max_grad_norm,
+                                              bf16_shadow=sh)
         self.actor_opt = self.opts.get("actor", self.opts.get("shared"))
         T, N = cfg.n_steps, self.env.num_envs
         act_shape = () if self.env.is_discrete else tuple(self.env.action_space.shape)
@@ -88,12 +99,25 @@ class ActorCriticTrainer:
             self.logger = Logger(cfg.outdir, legacy_step_index=cfg.legacy_step_index, metrics_path=cfg.metrics_path,
                                  quiet=cfg.quiet)
 
+    def _want_native(self):
+        """The hand-written HIP engine runs the CNN family on GPU (``engine="auto"|"native"``)."""
+        from ..models.policy import CNNActorCritic
+        eng = self.cfg.engine
+        if eng == "torch" or self.device.type != "cuda" or not isinstance(self.model, CNNActorCritic):
+            if eng == "native":
+                raise ValueError("engine='native' needs a CNN model on a GPU")
+            return False
+        _native.require()
+        return True
+
     # ------------------------------------------------------------------ rollout
     def _keys(self):
         return self.env.tg * (1 << KEY_ENV_BITS) + self.env.env_ids
 
     @torch.no_grad()
     def collect(self):
+        if self.engine is not None:
+            return self._collect_native()
         st, env, model = self.storage, self.env, self.model
         for t in range(st.T):
             obs_t = st.obs[t]
@@ -109,6 +133,24 @@ class ActorCriticTrainer:
             st.dones[t].copy_(env.done)
             st.truncated[t].copy_(env.truncated)
         st.values[st.T].copy_(model.value(st.obs[st.T]))
+
+    @torch.no_grad()
+    def _collect_native(self):
+        st, env, eng = self.storage, self.env, self.engine
+        A = eng.A
+        b = eng.bufs(env.num_envs)
+        ops = _native.require()
+        for t in range(st.T):
+            z = eng.forward(st.obs[t], b)
+            ops.categorical_sample(z[:, :A], self._keys(), self.policy_seed, st.actions[t], st.logp[t],
+                                   st.entropy[t])
+            st.values[t].copy_(z[:, A])
+            env.step(st.actions[t], prev_obs=st.obs[t], obs_out=st.obs[t + 1])
+            st.rewards[t].copy_(env.reward)
+            st.dones[t].copy_(env.done)
+            st.truncated[t].copy_(env.truncated)
+        z = eng.forward(st.obs[st.T], b)
+        st.values[st.T].copy_(z[:, A])
 
     # ------------------------------------------------------------------ returns
     def compute_returns(self):
@@ -137,13 +179,36 @@ class ActorCriticTrainer:
         total = a_loss + (cfg.vf_coef * c_loss if shared else c_loss)
         return total, a_loss, c_loss, kl, entm, clipfrac
 
+    _defer_allreduce = False
+
     def _apply_grads(self):
+        """All-reduce (DP) + optimiser step; inside a segmented capture the pre-graph stops before both."""
+        if self._defer_allreduce:
+            return
         if self.dp is not None:
             self.dp.allreduce_grads(self.flat)
+        self._run_optimizers()
+
+    def _run_optimizers(self):
         for opt in self.opts.values():
             opt.step()
 
+    def _learn_native(self, obs, actions, logp_old, adv, ret, v_old):
+        cfg, eng = self.cfg, self.engine
+        b = eng.bufs(obs.shape[0], with_grad=True)
+        self.flat.zero_grad()
+        eng.forward(obs, b)
+        ppo = cfg.algo == "ppo"
+        vf = cfg.vf_coef if "shared" in self.flat.groups else 1.0
+        stats = eng.loss(b, actions, logp_old, adv, ret, v_old if ppo else None, self.ent_coef, self.kl_coef, vf,
+                         cfg.ppo_clip if ppo else 0.0, cfg.ppo_value_clip if ppo else 0.0)
+        eng.backward(b)
+        self._apply_grads()
+        return stats
+
     def learn(self, ret, adv):
+        if self.engine is not None:
+            return self._learn_native_update(ret, adv)
         cfg, st = self.cfg, self.storage
         obs, actions, logp_old = st.flat("obs"), st.flat("actions"), st.flat("logp")
         v_old = st.flat("values")
@@ -183,6 +248,72 @@ class ActorCriticTrainer:
             self.stats["kl"].copy_(kl.detach())
 
     @torch.no_grad()
+    def _learn_native_update(self, ret, adv):
+        cfg, st = self.cfg, self.storage
+        obs, actions, logp_old = st.flat("obs"), st.flat("actions"), st.flat("logp")
+        v_old = st.flat("values")
+        self.stats["ev_before"].copy_(var_accounted_for_tensor(ret, v_old))
+        if cfg.norm_adv:
+            adv = self.dp.normalize_advantages(adv) if self.dp is not None else R.normalize_advantages(adv)
+        if cfg.algo == "ppo":
+            B = obs.shape[0]
+            mb = B // cfg.ppo_minibatches
+            if not hasattr(self, "_mb"):
+                dev = self.device
+                self._mb = dict(obs=torch.empty((mb,) + tuple(obs.shape[1:]), dtype=obs.dtype, device=dev),
+                                act=torch.empty(mb, dtype=actions.dtype, device=dev),
+                                logp=torch.empty(mb, device=dev), adv=torch.empty(mb, device=dev),
+                                ret=torch.empty(mb, device=dev), v=torch.empty(mb, device=dev))
+            m = self._mb
+            idx = torch.arange(B, device=self.device, dtype=torch.int64)
+            for ep in range(cfg.ppo_epochs):
+                h = E.rng.hash_u32(self.policy_seed, idx, self.update_counter * 64 + ep, 7)
+                perm = torch.argsort(h)
+                for k in range(cfg.ppo_minibatches):
+                    sel = perm[k * mb:(k + 1) * mb]
+                    torch.index_select(obs, 0, sel, out=m["obs"])
+                    torch.index_select(actions, 0, sel, out=m["act"])
+                    torch.index_select(logp_old, 0, sel, out=m["logp"])
+                    torch.index_select(adv, 0, sel, out=m["adv"])
+                    torch.index_select(ret, 0, sel, out=m["ret"])
+                    torch.index_select(v_old, 0, sel, out=m["v"])
+                    stats = self._learn_native(m["obs"], m["act"], m["logp"], m["adv"], m["ret"], m["v"])
+        else:
+            stats = self._learn_native(obs, actions, logp_old, adv.contiguous(), ret.contiguous(), v_old)
+        self._last = (stats, obs, actions, logp_old, ret)
+        if not self._defer_allreduce:
+            self._finish_learn()
+
+    def _finish_learn(self):
+        """Statistics + post-update KL / EV / adaptive lr (after the optimiser step)."""
+        if self.engine is None:
+            return
+        stats, obs, actions, logp_old, ret = self._last
+        cfg = self.cfg
+        self.stats["act_loss"].copy_(stats[5])
+        self.stats["crit_loss"].copy_(stats[3])
+        self.stats["entropy"].copy_(stats[2])
+        self.stats["clipfrac"].copy_(stats[4])
+        self.stats["kl"].copy_(stats[1])
+        self.update_counter += 1
+        if self.lr_ctrl is not None or cfg.kl_coef > 0:
+            self._post_update_kl_native(obs, actions, logp_old, ret)
+
+    @torch.no_grad()
+    def _post_update_kl_native(self, obs, actions, logp_old, ret):
+        eng = self.engine
+        b = eng.bufs(obs.shape[0], with_grad=True)
+        z = eng.forward(obs, b)
+        logp, _ = D.categorical_logp_entropy(z[:, :eng.A], actions)
+        kl = ((logp_old - logp) ** 2).mean()
+        if self.dp is not None:
+            kl = self.dp.mean_scalar(kl)
+        self.stats["kl"].copy_(kl)
+        self.stats["ev_after"].copy_(var_accounted_for_tensor(ret, z[:, eng.A]))
+        if self.lr_ctrl is not None:
+            self.lr_ctrl.update_(self.actor_opt.lr, kl)
+
+    @torch.no_grad()
     def _post_update_kl(self, obs, actions, logp_old, ret):
         """KL proxy and EV on the *updated* parameters (``Basic_AC/run_AC.py:257-258``), then the lr rule."""
         logp, _, v = self.model.evaluate(obs, actions)
@@ -201,21 +332,65 @@ class ActorCriticTrainer:
         self.storage.roll_over()
 
     # ------------------------------------------------------------------ driver
+    # An update is split in two segments around the gradient all-reduce:
+    #   pre  = rollout + returns + forward + loss + backward   (everything up to the gradient slab)
+    #   post = optimiser step(s) + statistics
+    # Without DP and for single-minibatch algorithms both segments run back to back and the whole update is ONE
+    # captured hipGraph. With DP each segment is its own graph and the RCCL all-reduce of the flat gradient slab
+    # is issued eagerly between the two replays (one collective per update). PPO (many optimiser steps per
+    # update) is captured whole only without DP.
+
     def _can_capture(self):
-        return (self.cfg.cuda_graph and self.device.type == "cuda" and self.dp is None)
+        return self.cfg.cuda_graph and self.device.type == "cuda"
+
+    def _segmented(self):
+        return self.dp is not None and self.cfg.algo != "ppo" and self.engine is not None
+
+    def update_body(self):
+        self.collect()
+        ret, adv = self.compute_returns()
+        self.learn(ret, adv)
+        self.storage.roll_over()
 
     def capture(self, warmup=2):
-        """Capture one whole update (rollout + returns + learn) as a hipGraph."""
+        """Capture the update as hipGraph(s) (see above)."""
+        if self.dp is not None and not self._segmented():
+            return None
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(warmup):
                 self.update_body()
         torch.cuda.current_stream().wait_stream(s)
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            self.update_body()
+        torch.cuda.synchronize()
+        if self._segmented():
+            self._defer_allreduce = True
+            try:
+                g1 = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g1):
+                    self._pre_segment()
+                g2 = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g2):
+                    self._post_segment()
+            finally:
+                self._defer_allreduce = False
+            self.graph = (g1, g2)
+        else:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self.update_body()
+            self.graph = (g,)
         return self.graph
+
+    def _pre_segment(self):
+        self.collect()
+        ret, adv = self.compute_returns()
+        self.learn(ret, adv)
+
+    def _post_segment(self):
+        self._run_optimizers()
+        self._finish_learn()
+        self.storage.roll_over()
 
     def step(self):
         """One update (graph replay when captured)."""
@@ -226,7 +401,12 @@ class ActorCriticTrainer:
             if k is not None:
                 self.kl_coef.fill_(k)
         if self.graph is not None:
-            self.graph.replay()
+            if len(self.graph) == 2:
+                self.graph[0].replay()
+                self.dp.allreduce_grads(self.flat)
+                self.graph[1].replay()
+            else:
+                self.graph[0].replay()
         else:
             self.update_body()
         self.iteration += 1

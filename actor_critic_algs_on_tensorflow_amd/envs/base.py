@@ -130,6 +130,8 @@ class VecEnv:
         """
         prev = self.obs if prev_obs is None else prev_obs
         out = self.obs if obs_out is None else obs_out
+        if prev.data_ptr() == out.data_ptr():
+            prev = prev.clone()   # the kernels read the old stack while writing the new one
         if _native.use_native(self.state):
             self._native_step(actions, prev, out)
         else:

@@ -57,19 +57,34 @@ class Dense(nn.Module):
 
 
 class Conv(nn.Module):
-    def __init__(self, cin, cout, k, stride, activation="relu", gain=2 ** 0.5, generator=None):
+    """VALID convolution with a selectable weight layout.
+
+    ``layout="oihw"``: ``weight [out, in, kh, kw]`` (PyTorch order; the im2col k index is (c, i, j)) -- used for
+    the first Atari conv, whose input is the uint8 frame stack with frames as channels.
+    ``layout="ohwi"``: ``weight [out, kh, kw, in]`` (k index (i, j, c)) -- used for convs over NHWC activations,
+    where 8 consecutive k are 8 consecutive channels and the engine's im2col is a 16-byte copy.
+    The forward here is the fp32 PyTorch reference of the engine's conv (``F.conv2d`` on NCHW tensors).
+    """
+
+    def __init__(self, cin, cout, k, stride, activation="relu", gain=2 ** 0.5, generator=None, layout="oihw"):
         super().__init__()
         self.cin, self.cout, self.k, self.stride = cin, cout, k, stride
         self.activation = activation
-        self.weight = nn.Parameter(torch.empty(cout, cin, k, k))
+        self.layout = layout
+        shape = (cout, cin, k, k) if layout == "oihw" else (cout, k, k, cin)
+        self.weight = nn.Parameter(torch.empty(shape))
         self.bias = nn.Parameter(torch.zeros(cout))
         with torch.no_grad():
             flat = torch.empty(cout, cin * k * k)
             I.orthogonal_(flat, gain, generator=generator)
-            self.weight.copy_(flat.view_as(self.weight))
+            w = flat.view(cout, cin, k, k)
+            self.weight.copy_(w if layout == "oihw" else w.permute(0, 2, 3, 1))
+
+    def weight_oihw(self):
+        return self.weight if self.layout == "oihw" else self.weight.permute(0, 3, 1, 2)
 
     def out_hw(self, h):
         return (h - self.k) // self.stride + 1
 
     def forward(self, x):
-        return ACTIVATIONS[self.activation](F.conv2d(x, self.weight, self.bias, stride=self.stride))
+        return ACTIVATIONS[self.activation](F.conv2d(x, self.weight_oihw(), self.bias, stride=self.stride))

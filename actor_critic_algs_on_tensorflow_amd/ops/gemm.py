@@ -1,0 +1,151 @@
+"""bf16 MFMA GEMM + convolution lowering ops (``csrc/kernels/gemm.hip``, ``conv.hip``).
+
+``gemm`` computes ``C = epilogue(alpha * A @ B)`` for strided bf16 operands stored either way round (see the
+kernel header) and is the only matrix product the native engine uses -- forward, dX and dW of every conv / dense
+layer. :func:`plan` picks the tile and the split-K factor from the problem shape so that small-batch products
+(rollout inference at 32 rows) still put >= one workgroup on most of the 256 CUs.
+
+Each function has a PyTorch reference (``*_ref``) that the GPU tests compare against in fp32.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import _native
+
+# tile id -> (BM, BN) ; must match aca_gemm_tile_dims
+TILES = {0: (64, 64), 1: (32, 64), 2: (64, 32), 3: (128, 64), 4: (32, 32)}
+BK = 64
+NUM_CUS = 256
+
+
+def _cdiv(a, b):
+    return (a + b - 1) // b
+
+
+def plan(M, N, K, atomic=False, max_splits=64, target_wgs=256):
+    """Choose ``(tile, splits)`` for an M x N x K product.
+
+    Prefer the largest tile that still yields ``target_wgs`` workgroups; when even the smallest tile leaves the
+    chip mostly idle, split K (each split keeps >= 2 k-tiles). ``atomic`` products (weight gradients) may split
+    deeper because their reduction costs nothing extra.
+    """
+    kt = _cdiv(K, BK)
+    best = None
+    for tile in (3, 0, 2, 1, 4):
+        bm, bn = TILES[tile]
+        if bm > 64 and M < 4 * bm:
+            continue
+        wgs = _cdiv(M, bm) * _cdiv(N, bn)
+        if wgs >= target_wgs:
+            return tile, 1
+        if best is None or wgs > best[1]:
+            best = (tile, wgs)
+    tile, wgs = best
+    splits = 1
+    cap = max_splits if atomic else 16
+    while wgs * splits * 2 <= 2 * target_wgs and kt // (splits * 2) >= 2 and splits * 2 <= cap:
+        splits *= 2
+    return tile, splits
+
+
+def workspace_elems(M, N, tile, splits):
+    bm, bn = TILES[tile]
+    return _cdiv(M, bm) * _cdiv(N, bn) * splits * bm * bn, _cdiv(M, bm) * _cdiv(N, bn)
+
+
+class GemmWorkspace:
+    """Slab + ticket workspace shared by the split-K products of one engine (sized on first use, then static)."""
+
+    def __init__(self, device, elems=1 << 20, tickets=1 << 14):
+        self.ws = torch.zeros(elems, dtype=torch.float32, device=device)
+        self.tickets = torch.zeros(tickets, dtype=torch.int32, device=device)
+
+    def ensure(self, elems, tiles):
+        if elems > self.ws.numel():
+            self.ws = torch.zeros(elems, dtype=torch.float32, device=self.ws.device)
+        if tiles > self.tickets.numel():
+            self.tickets = torch.zeros(tiles, dtype=torch.int32, device=self.ws.device)
+
+
+def gemm(A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha=1.0, bias=None, relu=False, mask=None, ldm=0,
+         colsum=None, tile=None, splits=None, workspace: GemmWorkspace | None = None, colsum_mod=0):
+    """Native GEMM; ``out_mode``: 0 fp32 store, 1 bf16 store, 2 fp32 atomic add (C pre-zeroed)."""
+    if tile is None or splits is None:
+        t, s = plan(M, N, K, atomic=(out_mode == 2))
+        tile = t if tile is None else tile
+        splits = s if splits is None else splits
+    ops = _native.require()
+    eff = ops.gemm_effective_splits(K, splits)
+    ws = tk = None
+    if eff > 1 and out_mode != 2:
+        if workspace is None:
+            raise ValueError("slab split-K needs a GemmWorkspace")
+        e, t = workspace_elems(M, N, tile, eff)
+        workspace.ensure(e, t)
+        ws, tk = workspace.ws, workspace.tickets
+    if colsum_mod:
+        if colsum is None:
+            raise ValueError("colsum_mod without colsum")
+    ops.gemm(A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, float(alpha), bias, bool(relu), mask, ldm,
+             colsum, tile, splits, ws, tk, int(colsum_mod))
+
+
+def _view(t, rows, cols, ld, k_contig_rows):
+    """Strided [rows, cols] view of a flat tensor with row stride ld (contiguous columns)."""
+    return torch.as_strided(t, (rows, cols), (ld, 1), t.storage_offset())
+
+
+def gemm_ref(A, lda, a_k, B, ldb, b_k, M, N, K, alpha=1.0, bias=None, relu=False, mask=None, ldm=0):
+    """fp32 PyTorch oracle of :func:`gemm` (returns the fp32 result; no store/colsum semantics)."""
+    Am = _view(A, M, K, lda, True) if a_k else _view(A, K, M, lda, False).t()
+    Bm = _view(B, N, K, ldb, True).t() if b_k else _view(B, K, N, ldb, False)
+    y = alpha * (Am.float() @ Bm.float())
+    if bias is not None:
+        y = y + bias[:N].float()
+    if relu:
+        y = torch.relu(y)
+    if mask is not None:
+        y = y * (_view(mask, M, N, ldm, True).float() > 0)
+    return y
+
+
+# ------------------------------------------------------------------------------------------------ conv lowering
+def conv_out(h, k, s):
+    return (h - k) // s + 1
+
+
+def im2col_u8(x, col, kh, kw, s, scale=1.0 / 255.0):
+    _native.require().im2col_u8(x, col, kh, kw, s, float(scale))
+
+
+def im2col_u8_ref(x, kh, kw, s, scale=1.0 / 255.0):
+    """uint8 NCHW -> [B*OH*OW, C*KH*KW] with k order (c, i, j)."""
+    B, C, H, W = x.shape
+    u = torch.nn.functional.unfold(x.float() * scale, (kh, kw), stride=s)  # [B, C*kh*kw, L]
+    return u.transpose(1, 2).reshape(-1, C * kh * kw)
+
+
+def im2col_nhwc(x, col, B, H, W, C, kh, kw, s):
+    _native.require().im2col_nhwc(x, col, B, H, W, C, kh, kw, s)
+
+
+def im2col_nhwc_ref(x, B, H, W, C, kh, kw, s):
+    """NHWC [B, H, W, C] -> [B*OH*OW, KH*KW*C] with k order (i, j, c)."""
+    xn = x.reshape(B, H, W, C).permute(0, 3, 1, 2).float()
+    u = torch.nn.functional.unfold(xn, (kh, kw), stride=s)  # [B, C*kh*kw, L], k order (c, i, j)
+    L = u.shape[-1]
+    u = u.view(B, C, kh * kw, L).permute(0, 3, 2, 1)      # [B, L, kh*kw, C]
+    return u.reshape(B * L, kh * kw * C)
+
+
+def col2im_nhwc(dcol, ymask, dx, colsum, B, H, W, C, kh, kw, s):
+    _native.require().col2im_nhwc(dcol, ymask, dx, colsum, B, H, W, C, kh, kw, s)
+
+
+def col2im_nhwc_ref(dcol, ymask, B, H, W, C, kh, kw, s):
+    OH, OW = conv_out(H, kh, s), conv_out(W, kw, s)
+    d = dcol.float().view(B, OH * OW, kh * kw, C).permute(0, 3, 2, 1).reshape(B, C * kh * kw, OH * OW)
+    x = torch.nn.functional.fold(d, (H, W), (kh, kw), stride=s)  # [B, C, H, W]
+    x = x.permute(0, 2, 3, 1).reshape(B * H * W, C)
+    return x * (ymask.float().view(B * H * W, C) > 0)

@@ -27,29 +27,30 @@ class FlatParams:
     ``groups`` maps a group name to ``(start, end)`` element offsets; params are laid out group by group.
     """
 
+    ALIGN = 64  # group starts are 256-byte aligned (vectorised optimiser / all-reduce segments)
+
     def __init__(self, named_groups, device=None):
         self.groups = {}
         self.params = []
+        self.offsets = []
         total = 0
         for name, plist in named_groups.items():
+            total = (total + self.ALIGN - 1) // self.ALIGN * self.ALIGN
             start = total
             for p in plist:
                 self.params.append(p)
+                self.offsets.append(total)
                 total += p.numel()
             self.groups[name] = (start, total)
         dev = device if device is not None else (self.params[0].device if self.params else "cpu")
         self.numel = total
         self.data = torch.zeros(total, dtype=torch.float32, device=dev)
         self.grad = torch.zeros(total, dtype=torch.float32, device=dev)
-        off = 0
-        self.offsets = []
-        for p in self.params:
+        for p, off in zip(self.params, self.offsets):
             n = p.numel()
             self.data[off:off + n].copy_(p.data.reshape(-1).to(dev, torch.float32))
             p.data = self.data[off:off + n].view(p.shape)
             p.grad = self.grad[off:off + n].view(p.shape)
-            self.offsets.append(off)
-            off += n
 
     def zero_grad(self):
         self.grad.zero_()
@@ -80,6 +81,9 @@ class FusedAdam:
         self.max_grad_norm = max_grad_norm
         self.gnorm = torch.zeros((), dtype=torch.float32, device=dev)
         self.shadow = bf16_shadow  # optional bf16 tensor of the same numel (written by the native kernel)
+        # sumsq partials + last-arriver tickets (self-cleaning, zero-initialised once)
+        self._partial = torch.zeros(1024, dtype=torch.float32, device=dev)
+        self._ticket = torch.zeros(2, dtype=torch.int32, device=dev)
 
     def set_lr(self, lr):
         self.lr.fill_(float(lr))
@@ -94,15 +98,22 @@ class FusedAdam:
         else:
             self._torch_step()
 
+    def _native_norm(self, ops):
+        if self.max_grad_norm is not None:
+            if self.clip_value is not None:
+                # the norm is taken after the element-wise clip (torch oracle order)
+                ops.sumsq(torch.clamp(self.g, -self.clip_value, self.clip_value), self._partial, self._ticket[:1],
+                          self.gnorm)
+            else:
+                ops.sumsq(self.g, self._partial, self._ticket[:1], self.gnorm)
+
     def _native_step(self):
         ops = _native.require()
-        if self.max_grad_norm is not None:
-            ops.sumsq(self.g, self.gnorm)
-        ops.adam_step(self.p, self.g, self.m, self.v, self.lr, self.t, self.gnorm,
-                      self.shadow if self.shadow is not None else torch.empty(0, device=self.p.device),
+        self._native_norm(ops)
+        ops.adam_step(self.p, self.g, self.m, self.v, self.lr, self.t, self.gnorm, self.shadow,
                       float(self.b1), float(self.b2), float(self.eps),
                       float(self.clip_value) if self.clip_value is not None else -1.0,
-                      float(self.max_grad_norm) if self.max_grad_norm is not None else -1.0)
+                      float(self.max_grad_norm) if self.max_grad_norm is not None else -1.0, self._ticket[1:])
 
     def _torch_step(self):
         g = self.g
@@ -142,10 +153,8 @@ class FusedRMSprop(FusedAdam):
 
     def _native_step(self):
         ops = _native.require()
-        if self.max_grad_norm is not None:
-            ops.sumsq(self.g, self.gnorm)
-        ops.rmsprop_step(self.p, self.g, self.v, self.lr, self.gnorm,
-                         self.shadow if self.shadow is not None else torch.empty(0, device=self.p.device),
+        self._native_norm(ops)
+        ops.rmsprop_step(self.p, self.g, self.v, self.lr, self.gnorm, self.shadow,
                          float(self.alpha), float(self.eps),
                          float(self.clip_value) if self.clip_value is not None else -1.0,
                          float(self.max_grad_norm) if self.max_grad_norm is not None else -1.0)
@@ -158,7 +167,6 @@ class FusedRMSprop(FusedAdam):
             n = torch.sqrt((g * g).sum())
             self.gnorm.copy_(n * n)
             g = g * torch.clamp(self.max_grad_norm / (n + 1e-6), max=1.0)
-        self.t += 1
         self.v.mul_(self.alpha).addcmul_(g, g, value=1 - self.alpha)
         self.p.sub_(self.lr * g / torch.sqrt(self.v + self.eps))
         if self.shadow is not None:

@@ -1,0 +1,89 @@
+"""Synchronous data parallelism over RCCL (``torch.distributed`` backend "nccl" == RCCL on ROCm) or gloo on CPU.
+
+The reference has no collective communication at all -- only the asynchronous parameter server of
+``A3C/process.py:156-214`` (reproduced in :mod:`.a3c`). This module is the BASELINE.json "sync-A2C data-parallel"
+mode: one process per GPU, each owning its own env bank (``env_offset = rank * N`` so every
+rank simulates different envs), identical parameters, and per update
+
+  * ONE all-reduce of the flat fp32 gradient slab (every parameter's gradient is a view into it, so there is no
+    bucketing bookkeeping: the whole model is one contiguous message -- 6.75 MB for the Atari CNN, one ring pass
+    over xGMI), averaged;
+  * ONE packed all-reduce of the scalar statistics that must be global (advantage sum / sum of squares / count
+    for normalisation; the KL proxy for the adaptive lr), so every rank takes bit-identical optimiser steps.
+
+Parameters are broadcast from rank 0 at start (the reference's race where every worker re-initialises the PS
+variables, SURVEY §2.9 #11, cannot happen). RCCL timeouts surface as exceptions (fail fast).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def init_from_env(backend="auto", timeout_s=300):
+    """Initialises the default process group from torchrun-style env vars; returns (rank, world, local_rank)."""
+    if not dist.is_available():
+        return 0, 1, 0
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world <= 1:
+        return 0, 1, 0
+    if not dist.is_initialized():
+        if backend == "auto":
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        kw = {}
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            kw["device_id"] = torch.device("cuda", local)
+        dist.init_process_group(backend, timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    return dist.get_rank(), dist.get_world_size(), local
+
+
+class DataParallel:
+    def __init__(self, group=None, average=True):
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world_size = dist.get_world_size(group)
+        self.average = average
+
+    # -- parameters ---------------------------------------------------------------------------------------------
+    @torch.no_grad()
+    def broadcast_params(self, flat, src=0):
+        dist.broadcast(flat.data, src=src, group=self.group)
+
+    # -- gradients ----------------------------------------------------------------------------------------------
+    @torch.no_grad()
+    def allreduce_grads(self, flat):
+        dist.all_reduce(flat.grad, op=dist.ReduceOp.SUM, group=self.group)
+        if self.average and self.world_size > 1:
+            flat.grad.mul_(1.0 / self.world_size)
+
+    # -- statistics ---------------------------------------------------------------------------------------------
+    @torch.no_grad()
+    def normalize_advantages(self, adv, eps=1e-8):
+        """Global population-std normalisation across ranks (one packed all-reduce of [sum, sumsq, n])."""
+        a = adv.float()
+        s = torch.stack([a.sum(), (a * a).sum(), torch.tensor(float(a.numel()), device=a.device)]).double()
+        dist.all_reduce(s, group=self.group)
+        mean = s[0] / s[2]
+        var = torch.clamp(s[1] / s[2] - mean * mean, min=0.0)
+        return ((a - mean.float()) / (eps + var.sqrt().float()))
+
+    @torch.no_grad()
+    def mean_scalar(self, x):
+        y = x.detach().float().reshape(1).clone()
+        dist.all_reduce(y, group=self.group)
+        return (y / self.world_size).reshape(())
+
+    @torch.no_grad()
+    def sum_tensor(self, x):
+        y = x.clone()
+        dist.all_reduce(y, group=self.group)
+        return y
+
+    def barrier(self):
+        dist.barrier(group=self.group)

@@ -1,0 +1,98 @@
+#!/usr/bin/env python3
+"""Headline benchmark: env-steps/sec (whole node) of synchronous A2C on the Atari-shaped CNN, 32 vec-envs per GPU.
+
+BASELINE.json metric "env-steps/sec (whole node) A2C Atari-CNN 32 vec-envs/GPU at 1/2/4/8 MI355X", config
+"Atari-Pong A2C, 32 synthetic 84x84x4 vec-envs, CNN+MLP bf16" (preset ``pong_a2c``: n_steps 5, RMSprop 7e-4,
+global-norm clip 0.5, entropy 0.01, value coef 0.5). One timed step = one full A2C update: 5 rollout steps of the
+32-env bank (CNN inference + categorical sampling + env physics + frame rendering/stacking) plus the bootstrap
+value, n-step returns, the learner forward/loss/backward over the 160-sample batch and the fused RMSprop update
+(and, for N > 1, the RCCL all-reduce of the flat gradient slab). Weak scaling: 32 envs per GPU.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]; N > 1 under torch.distributed.run (one rank per GPU).
+Synthetic data (the Pong-shaped env bank renders its own frames), random-init weights.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+METRIC = "env-steps/sec (whole node) A2C Atari-CNN 32 vec-envs/GPU at 1/2/4/8 MI355X"
+BASELINE_VALUE = None  # the reference publishes no number
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--envs", type=int, default=32)
+    ap.add_argument("--engine", default="auto")
+    ap.add_argument("--no-graph", action="store_true")
+    args = ap.parse_args()
+
+    from actor_critic_algs_on_tensorflow_amd import preset
+    from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
+    from actor_critic_algs_on_tensorflow_amd.parallel import dp as DP
+
+    rank, world, local = DP.init_from_env("nccl")
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dp = DP.DataParallel() if world > 1 else None
+    cfg = preset("pong_a2c", num_envs=args.envs, device=f"cuda:{local}", outdir=None, quiet=True,
+                 stdout_freq=0, save_every=0, engine=args.engine, cuda_graph=not args.no_graph)
+    tr = ActorCriticTrainer(cfg, dp=dp)
+    if cfg.cuda_graph:
+        tr.capture(warmup=2)
+    for _ in range(args.warmup):
+        tr.step()
+    torch.cuda.synchronize()
+    if dp is not None:
+        dp.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tr.step()
+    torch.cuda.synchronize()
+    if dp is not None:
+        dp.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if dp is not None:
+        t = torch.tensor([dt], device=f"cuda:{local}", dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t)
+    steps_per_update = cfg.n_steps * args.envs * world
+    value = steps_per_update * args.steps / dt
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * dt / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
+            "dtype": "bf16",
+            "data": "synthetic (Pong-shaped 84x84x4 uint8 env bank, random-init weights)",
+            "config": {"model": "Nature-CNN actor-critic (3 conv + fc512, 1.69M params)",
+                       "global_batch": steps_per_update, "seq_len": cfg.n_steps, "envs_per_gpu": args.envs,
+                       "algo": "A2C (RMSprop 7e-4, n-step returns, grad-norm 0.5)",
+                       "parallelism": f"dp{world}", "engine": "native" if tr.engine is not None else "torch",
+                       "hipgraph": bool(tr.graph)},
+        }
+        print(json.dumps(out), flush=True)
+    if dp is not None:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,496 @@
+// torch.ops.acamd.* registrations for the gfx950 kernels in csrc/kernels/*.hip.
+//
+// The kernels are compiled by hipcc without torch headers and export plain C launchers taking raw pointers and a
+// hipStream_t; this file (the only one that includes torch) validates tensors, resolves the current HIP stream of
+// torch.cuda (so ops are hipGraph-capturable) and forwards. Every op mutates its output arguments in place and
+// returns nothing: the Python layer owns all buffers (static addresses for graph capture).
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/library.h>
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+extern "C" {
+hipError_t aca_env_step_cartpole(float*, int32_t*, int64_t*, float*, float*, const int64_t*, const int32_t*,
+                                 const float*, float*, float*, uint8_t*, uint8_t*, uint32_t, int, int, int,
+                                 hipStream_t);
+hipError_t aca_env_step_pendulum(float*, int32_t*, int64_t*, float*, float*, const int64_t*, const float*, int,
+                                 const float*, float*, float*, uint8_t*, uint8_t*, uint32_t, int, int, int,
+                                 hipStream_t);
+hipError_t aca_env_step_linear(float*, int32_t*, int64_t*, float*, float*, const int64_t*, const float*,
+                               const float*, const float*, const float*, float*, float*, uint8_t*, uint8_t*,
+                               uint32_t, int, int, int, hipStream_t);
+hipError_t aca_env_step_pong(float*, int32_t*, int64_t*, float*, float*, const int64_t*, const int32_t*,
+                             const uint8_t*, uint8_t*, float*, uint8_t*, uint8_t*, uint32_t, int, int, int,
+                             hipStream_t);
+hipError_t aca_categorical_sample(const float*, int, int, int, const int64_t*, uint32_t, int32_t*, float*, float*,
+                                  hipStream_t);
+hipError_t aca_gaussian_sample(const float*, int, int, int, const float*, const int64_t*, uint32_t, float*, float*,
+                               float*, hipStream_t);
+hipError_t aca_gae(const float*, const float*, const uint8_t*, float*, float*, int, int, float, float, hipStream_t);
+hipError_t aca_nstep(const float*, const float*, const uint8_t*, float*, float*, int, int, float, int, hipStream_t);
+hipError_t aca_normalize(const float*, float*, int, float, hipStream_t);
+hipError_t aca_moments(const float*, const float*, float*, int, hipStream_t);
+hipError_t aca_sumsq(const float*, size_t, float*, int, unsigned int*, float*, hipStream_t);
+hipError_t aca_adam_step(float*, const float*, float*, float*, size_t, const float*, float*, const float*, uint16_t*,
+                         float, float, float, float, float, unsigned int*, hipStream_t);
+hipError_t aca_rmsprop_step(float*, const float*, float*, size_t, const float*, const float*, uint16_t*, float, float,
+                            float, float, hipStream_t);
+hipError_t aca_cast_bf16(const float*, uint16_t*, size_t, hipStream_t);
+hipError_t aca_gemm(const void*, int64_t, bool, const void*, int64_t, bool, void*, int64_t, int, int, int, int, float,
+                    const float*, int, const void*, int64_t, float*, int, int, float*, unsigned int*, int, hipStream_t);
+int aca_gemm_effective_splits(int, int);
+int aca_gemm_tile_dims(int, int*, int*);
+hipError_t aca_im2col_u8_nchw(const uint8_t*, uint16_t*, int, int, int, int, int, int, int, float, hipStream_t);
+hipError_t aca_im2col_nhwc(const uint16_t*, uint16_t*, int, int, int, int, int, int, int, hipStream_t);
+hipError_t aca_col2im_nhwc(const uint16_t*, const uint16_t*, uint16_t*, float*, int, int, int, int, int, int, int,
+                           hipStream_t);
+hipError_t aca_colsum_bf16(const uint16_t*, int64_t, int, int64_t, float*, hipStream_t);
+hipError_t aca_ac_loss(const float*, int64_t, const float*, int64_t, const int32_t*, const float*, const float*,
+                       const float*, const float*, const float*, const float*, const float*, const float*, float, float,
+                       float, uint16_t*, int64_t, uint16_t*, int64_t, float*, float*, int, int, int, hipStream_t);
+}
+
+namespace {
+
+using at::Tensor;
+
+hipStream_t cur_stream(const Tensor& t) { return c10::hip::getCurrentHIPStream(t.device().index()).stream(); }
+
+void check(hipError_t e, const char* what) {
+  TORCH_CHECK(e == hipSuccess, "acamd::", what, " launch failed: ", hipGetErrorString(e));
+}
+
+void need(const Tensor& t, at::ScalarType dt, const char* name) {
+  TORCH_CHECK(t.is_cuda(), "acamd: ", name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == dt, "acamd: ", name, " has dtype ", t.scalar_type(), ", expected ", dt);
+  TORCH_CHECK(t.is_contiguous(), "acamd: ", name, " must be contiguous");
+}
+
+template <typename T>
+T* ptr(const Tensor& t) { return reinterpret_cast<T*>(t.data_ptr()); }
+
+template <typename T>
+T* optr(const c10::optional<Tensor>& t) { return (t.has_value() && t->defined()) ? ptr<T>(*t) : nullptr; }
+
+// ---------------------------------------------------------------------------------------------- env banks
+void check_env(const Tensor& state, const Tensor& t, const Tensor& tg, const Tensor& ep_ret, const Tensor& ep_stats,
+               const Tensor& ids, const Tensor& reward, const Tensor& done, const Tensor& trunc) {
+  need(state, at::kFloat, "state");
+  need(t, at::kInt, "t");
+  need(tg, at::kLong, "tg");
+  need(ep_ret, at::kFloat, "ep_ret");
+  need(ep_stats, at::kFloat, "ep_stats");
+  need(ids, at::kLong, "env_ids");
+  need(reward, at::kFloat, "reward");
+  need(done, at::kByte, "done");
+  need(trunc, at::kByte, "truncated");
+}
+
+void env_step_cartpole(Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, Tensor ids, Tensor actions,
+                       Tensor prev, Tensor out, Tensor reward, Tensor done, Tensor trunc, int64_t seed,
+                       int64_t max_steps, int64_t k) {
+  check_env(state, t, tg, ep_ret, ep_stats, ids, reward, done, trunc);
+  need(actions, at::kInt, "actions");
+  need(prev, at::kFloat, "prev");
+  need(out, at::kFloat, "out");
+  const int N = state.size(0);
+  TORCH_CHECK(prev.numel() == (int64_t)N * 4 * k && out.numel() == prev.numel(), "cartpole: bad stack shape");
+  check(aca_env_step_cartpole(ptr<float>(state), ptr<int32_t>(t), ptr<int64_t>(tg), ptr<float>(ep_ret),
+                              ptr<float>(ep_stats), ptr<int64_t>(ids), ptr<int32_t>(actions), ptr<float>(prev),
+                              ptr<float>(out), ptr<float>(reward), ptr<uint8_t>(done), ptr<uint8_t>(trunc),
+                              (uint32_t)seed, (int)max_steps, (int)k, N, cur_stream(state)),
+        "env_step_cartpole");
+}
+
+void env_step_pendulum(Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, Tensor ids, Tensor actions,
+                       Tensor prev, Tensor out, Tensor reward, Tensor done, Tensor trunc, int64_t seed,
+                       int64_t max_steps, int64_t k) {
+  check_env(state, t, tg, ep_ret, ep_stats, ids, reward, done, trunc);
+  need(actions, at::kFloat, "actions");
+  need(prev, at::kFloat, "prev");
+  need(out, at::kFloat, "out");
+  const int N = state.size(0);
+  TORCH_CHECK(prev.numel() == (int64_t)N * 3 * k && out.numel() == prev.numel(), "pendulum: bad stack shape");
+  const int act_dim = actions.numel() / N;
+  check(aca_env_step_pendulum(ptr<float>(state), ptr<int32_t>(t), ptr<int64_t>(tg), ptr<float>(ep_ret),
+                              ptr<float>(ep_stats), ptr<int64_t>(ids), ptr<float>(actions), act_dim, ptr<float>(prev),
+                              ptr<float>(out), ptr<float>(reward), ptr<uint8_t>(done), ptr<uint8_t>(trunc),
+                              (uint32_t)seed, (int)max_steps, (int)k, N, cur_stream(state)),
+        "env_step_pendulum");
+}
+
+void env_step_linear(Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, Tensor ids, Tensor actions,
+                     Tensor A, Tensor B, Tensor prev, Tensor out, Tensor reward, Tensor done, Tensor trunc,
+                     int64_t seed, int64_t max_steps, int64_t k) {
+  check_env(state, t, tg, ep_ret, ep_stats, ids, reward, done, trunc);
+  need(actions, at::kFloat, "actions");
+  need(A, at::kFloat, "A");
+  need(B, at::kFloat, "B");
+  need(prev, at::kFloat, "prev");
+  need(out, at::kFloat, "out");
+  const int N = state.size(0);
+  TORCH_CHECK(state.size(1) == 17 && A.numel() == 17 * 17 && B.numel() == 17 * 6 && actions.numel() == N * 6,
+              "linear env: bad shapes");
+  TORCH_CHECK(prev.numel() == (int64_t)N * 17 * k && out.numel() == prev.numel(), "linear: bad stack shape");
+  check(aca_env_step_linear(ptr<float>(state), ptr<int32_t>(t), ptr<int64_t>(tg), ptr<float>(ep_ret),
+                            ptr<float>(ep_stats), ptr<int64_t>(ids), ptr<float>(actions), ptr<float>(A),
+                            ptr<float>(B), ptr<float>(prev), ptr<float>(out), ptr<float>(reward),
+                            ptr<uint8_t>(done), ptr<uint8_t>(trunc), (uint32_t)seed, (int)max_steps, (int)k, N,
+                            cur_stream(state)),
+        "env_step_linear");
+}
+
+void env_step_pong(Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, Tensor ids, Tensor actions,
+                   Tensor prev, Tensor out, Tensor reward, Tensor done, Tensor trunc, int64_t seed, int64_t max_steps,
+                   int64_t k) {
+  check_env(state, t, tg, ep_ret, ep_stats, ids, reward, done, trunc);
+  need(actions, at::kInt, "actions");
+  need(prev, at::kByte, "prev");
+  need(out, at::kByte, "out");
+  const int N = state.size(0);
+  TORCH_CHECK(state.size(1) == 8, "pong: state must be [N, 8]");
+  TORCH_CHECK(prev.numel() == (int64_t)N * k * 84 * 84 && out.numel() == prev.numel(), "pong: bad stack shape");
+  TORCH_CHECK(prev.data_ptr() != out.data_ptr(), "pong: prev and out must not alias");
+  check(aca_env_step_pong(ptr<float>(state), ptr<int32_t>(t), ptr<int64_t>(tg), ptr<float>(ep_ret),
+                          ptr<float>(ep_stats), ptr<int64_t>(ids), ptr<int32_t>(actions), ptr<uint8_t>(prev),
+                          ptr<uint8_t>(out), ptr<float>(reward), ptr<uint8_t>(done), ptr<uint8_t>(trunc),
+                          (uint32_t)seed, (int)max_steps, (int)k, N, cur_stream(state)),
+        "env_step_pong");
+}
+
+// ---------------------------------------------------------------------------------------------- heads
+void categorical_sample(Tensor logits, Tensor keys, int64_t seed, Tensor act, Tensor logp, Tensor ent) {
+  TORCH_CHECK(logits.is_cuda() && logits.scalar_type() == at::kFloat && logits.dim() == 2 && logits.stride(1) == 1,
+              "categorical_sample: logits must be fp32 [B, A] with unit column stride");
+  need(keys, at::kLong, "keys");
+  need(act, at::kInt, "act");
+  need(logp, at::kFloat, "logp");
+  need(ent, at::kFloat, "ent");
+  const int B = logits.size(0), A = logits.size(1);
+  TORCH_CHECK(A <= 64, "categorical_sample: at most 64 actions");
+  TORCH_CHECK(keys.numel() >= B && act.numel() >= B && logp.numel() >= B && ent.numel() >= B, "bad sizes");
+  check(aca_categorical_sample(ptr<float>(logits), (int)logits.stride(0), B, A, ptr<int64_t>(keys), (uint32_t)seed,
+                               ptr<int32_t>(act), ptr<float>(logp), ptr<float>(ent), cur_stream(logits)),
+        "categorical_sample");
+}
+
+void gaussian_sample(Tensor mu, Tensor log_std, Tensor keys, int64_t seed, Tensor act, Tensor logp, Tensor ent) {
+  TORCH_CHECK(mu.is_cuda() && mu.scalar_type() == at::kFloat && mu.dim() == 2 && mu.stride(1) == 1,
+              "gaussian_sample: mu must be fp32 [B, A] with unit column stride");
+  need(log_std, at::kFloat, "log_std");
+  need(keys, at::kLong, "keys");
+  need(act, at::kFloat, "act");
+  need(logp, at::kFloat, "logp");
+  need(ent, at::kFloat, "ent");
+  const int B = mu.size(0), A = mu.size(1);
+  TORCH_CHECK(log_std.numel() == A && act.numel() >= (int64_t)B * A, "gaussian_sample: bad sizes");
+  check(aca_gaussian_sample(ptr<float>(mu), (int)mu.stride(0), B, A, ptr<float>(log_std), ptr<int64_t>(keys),
+                            (uint32_t)seed, ptr<float>(act), ptr<float>(logp), ptr<float>(ent), cur_stream(mu)),
+        "gaussian_sample");
+}
+
+// ---------------------------------------------------------------------------------------------- returns / stats
+void check_returns(const Tensor& r, const Tensor& v, const Tensor& d, const Tensor& o1, const Tensor& o2) {
+  need(r, at::kFloat, "rewards");
+  need(v, at::kFloat, "values");
+  need(d, at::kByte, "dones");
+  need(o1, at::kFloat, "out1");
+  need(o2, at::kFloat, "out2");
+  TORCH_CHECK(r.dim() == 2 && v.dim() == 2 && v.size(0) == r.size(0) + 1 && v.size(1) == r.size(1) &&
+                  d.sizes() == r.sizes() && o1.sizes() == r.sizes() && o2.sizes() == r.sizes(),
+              "returns: expected rewards/dones [T, N], values [T+1, N]");
+}
+
+void gae(Tensor r, Tensor v, Tensor d, Tensor ret, Tensor adv, double gamma, double lam) {
+  check_returns(r, v, d, ret, adv);
+  check(aca_gae(ptr<float>(r), ptr<float>(v), ptr<uint8_t>(d), ptr<float>(ret), ptr<float>(adv), r.size(0), r.size(1),
+                (float)gamma, (float)lam, cur_stream(r)),
+        "gae");
+}
+
+void nstep_returns(Tensor r, Tensor v, Tensor d, Tensor tgt, Tensor adv, double gamma, int64_t L) {
+  check_returns(r, v, d, tgt, adv);
+  check(aca_nstep(ptr<float>(r), ptr<float>(v), ptr<uint8_t>(d), ptr<float>(tgt), ptr<float>(adv), r.size(0),
+                  r.size(1), (float)gamma, (int)L, cur_stream(r)),
+        "nstep_returns");
+}
+
+void normalize(Tensor a, Tensor out, double eps) {
+  need(a, at::kFloat, "a");
+  need(out, at::kFloat, "out");
+  TORCH_CHECK(a.numel() == out.numel(), "normalize: size mismatch");
+  check(aca_normalize(ptr<float>(a), ptr<float>(out), a.numel(), (float)eps, cur_stream(a)), "normalize");
+}
+
+void moments(Tensor x, Tensor y, Tensor out) {
+  need(x, at::kFloat, "x");
+  need(y, at::kFloat, "y");
+  need(out, at::kFloat, "out");
+  TORCH_CHECK(x.numel() == y.numel() && out.numel() >= 5, "moments: bad sizes");
+  check(aca_moments(ptr<float>(x), ptr<float>(y), ptr<float>(out), x.numel(), cur_stream(x)), "moments");
+}
+
+// ---------------------------------------------------------------------------------------------- optimisers
+void sumsq(Tensor x, Tensor partial, Tensor ticket, Tensor out) {
+  need(x, at::kFloat, "x");
+  need(partial, at::kFloat, "partial");
+  need(ticket, at::kInt, "ticket");
+  need(out, at::kFloat, "out");
+  check(aca_sumsq(ptr<float>(x), x.numel(), ptr<float>(partial), (int)partial.numel(), ptr<unsigned int>(ticket),
+                  ptr<float>(out), cur_stream(x)),
+        "sumsq");
+}
+
+void adam_step(Tensor p, Tensor g, Tensor m, Tensor v, Tensor lr, Tensor t, c10::optional<Tensor> gnorm_sq,
+               c10::optional<Tensor> shadow, double b1, double b2, double eps, double clip, double max_norm,
+               Tensor ticket) {
+  need(p, at::kFloat, "p");
+  need(g, at::kFloat, "g");
+  need(m, at::kFloat, "m");
+  need(v, at::kFloat, "v");
+  need(lr, at::kFloat, "lr");
+  need(t, at::kFloat, "t");
+  need(ticket, at::kInt, "ticket");
+  TORCH_CHECK(g.numel() == p.numel() && m.numel() == p.numel() && v.numel() == p.numel(), "adam: size mismatch");
+  if (max_norm > 0) TORCH_CHECK(gnorm_sq.has_value() && gnorm_sq->defined(), "adam: max_norm needs gnorm_sq");
+  uint16_t* sh = nullptr;
+  if (shadow.has_value() && shadow->defined() && shadow->numel() > 0) {
+    need(*shadow, at::kBFloat16, "shadow");
+    TORCH_CHECK(shadow->numel() == p.numel(), "adam: shadow size mismatch");
+    sh = ptr<uint16_t>(*shadow);
+  }
+  check(aca_adam_step(ptr<float>(p), ptr<float>(g), ptr<float>(m), ptr<float>(v), p.numel(), ptr<float>(lr),
+                      ptr<float>(t), optr<float>(gnorm_sq), sh, (float)b1, (float)b2, (float)eps, (float)clip,
+                      (float)max_norm, ptr<unsigned int>(ticket), cur_stream(p)),
+        "adam_step");
+}
+
+void rmsprop_step(Tensor p, Tensor g, Tensor v, Tensor lr, c10::optional<Tensor> gnorm_sq,
+                  c10::optional<Tensor> shadow, double alpha, double eps, double clip, double max_norm) {
+  need(p, at::kFloat, "p");
+  need(g, at::kFloat, "g");
+  need(v, at::kFloat, "v");
+  need(lr, at::kFloat, "lr");
+  TORCH_CHECK(g.numel() == p.numel() && v.numel() == p.numel(), "rmsprop: size mismatch");
+  if (max_norm > 0) TORCH_CHECK(gnorm_sq.has_value() && gnorm_sq->defined(), "rmsprop: max_norm needs gnorm_sq");
+  uint16_t* sh = nullptr;
+  if (shadow.has_value() && shadow->defined() && shadow->numel() > 0) {
+    need(*shadow, at::kBFloat16, "shadow");
+    TORCH_CHECK(shadow->numel() == p.numel(), "rmsprop: shadow size mismatch");
+    sh = ptr<uint16_t>(*shadow);
+  }
+  check(aca_rmsprop_step(ptr<float>(p), ptr<float>(g), ptr<float>(v), p.numel(), ptr<float>(lr),
+                         optr<float>(gnorm_sq), sh, (float)alpha, (float)eps, (float)clip, (float)max_norm,
+                         cur_stream(p)),
+        "rmsprop_step");
+}
+
+void cast_bf16(Tensor x, Tensor y) {
+  need(x, at::kFloat, "x");
+  need(y, at::kBFloat16, "y");
+  TORCH_CHECK(x.numel() == y.numel(), "cast_bf16: size mismatch");
+  check(aca_cast_bf16(ptr<float>(x), ptr<uint16_t>(y), x.numel(), cur_stream(x)), "cast_bf16");
+}
+
+// ---------------------------------------------------------------------------------------------- GEMM / conv
+// A/B/C/mask are addressed through data_ptr (views with offsets are fine); the caller passes leading dimensions.
+// Bounds are validated against the tensors' storage extents so a bad call fails here instead of faulting the GPU.
+void check_extent(const Tensor& t, int64_t rows, int64_t cols, int64_t ld, const char* name) {
+  TORCH_CHECK(t.is_cuda(), "gemm: ", name, " must be on the GPU");
+  if (rows <= 0 || cols <= 0) return;
+  const int64_t need_elems = (rows - 1) * ld + cols;
+  const int64_t have = (int64_t)(t.storage().nbytes() / t.element_size()) - t.storage_offset();
+  TORCH_CHECK(need_elems <= have, "gemm: ", name, " too small: needs ", need_elems, " elements, has ", have);
+}
+
+void gemm(Tensor A, int64_t lda, bool a_k, Tensor B, int64_t ldb, bool b_k, Tensor C, int64_t ldc, int64_t out_mode,
+          int64_t M, int64_t N, int64_t K, double alpha, c10::optional<Tensor> bias, bool relu,
+          c10::optional<Tensor> mask, int64_t ldm, c10::optional<Tensor> colsum, int64_t tile, int64_t splits,
+          c10::optional<Tensor> ws, c10::optional<Tensor> tickets, int64_t colsum_mod) {
+  TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "gemm: A and B must be bf16");
+  TORCH_CHECK(out_mode >= 0 && out_mode <= 2, "gemm: bad out_mode");
+  TORCH_CHECK(C.scalar_type() == (out_mode == 1 ? at::kBFloat16 : at::kFloat), "gemm: C dtype mismatch");
+  check_extent(A, a_k ? M : K, a_k ? K : M, lda, "A");
+  check_extent(B, b_k ? N : K, b_k ? K : N, ldb, "B");
+  check_extent(C, M, N, ldc, "C");
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() >= N, "gemm: bias must be fp32 [N]");
+  }
+  if (mask.has_value() && mask->defined()) {
+    TORCH_CHECK(mask->scalar_type() == at::kBFloat16, "gemm: mask must be bf16");
+    check_extent(*mask, M, N, ldm, "mask");
+  }
+  if (colsum.has_value() && colsum->defined()) {
+    TORCH_CHECK(colsum->scalar_type() == at::kFloat && colsum->numel() >= (colsum_mod > 0 ? colsum_mod : N),
+                "gemm: colsum too small");
+  }
+  float* wsp = nullptr;
+  unsigned int* tk = nullptr;
+  const int eff = aca_gemm_effective_splits((int)K, (int)splits);
+  if (eff > 1 && out_mode != 2) {
+    TORCH_CHECK(ws.has_value() && ws->defined() && tickets.has_value() && tickets->defined(),
+                "gemm: slab split-K needs ws and tickets");
+    int bm, bn;
+    aca_gemm_tile_dims((int)tile, &bm, &bn);
+    const int64_t tiles = ((M + bm - 1) / bm) * ((N + bn - 1) / bn);
+    TORCH_CHECK(ws->scalar_type() == at::kFloat && ws->numel() >= tiles * eff * bm * bn, "gemm: ws too small (need ",
+                tiles * eff * bm * bn, ")");
+    TORCH_CHECK(tickets->scalar_type() == at::kInt && tickets->numel() >= tiles, "gemm: tickets too small");
+    wsp = ptr<float>(*ws);
+    tk = ptr<unsigned int>(*tickets);
+  }
+  check(aca_gemm(A.data_ptr(), lda, a_k, B.data_ptr(), ldb, b_k, C.data_ptr(), ldc, (int)out_mode, (int)M, (int)N,
+                 (int)K, (float)alpha, optr<float>(bias), relu ? 1 : 0,
+                 (mask.has_value() && mask->defined()) ? mask->data_ptr() : nullptr, ldm, optr<float>(colsum),
+                 (int)tile, (int)splits, wsp, tk, (int)colsum_mod, cur_stream(C)),
+        "gemm");
+}
+
+int64_t gemm_effective_splits(int64_t K, int64_t splits) { return aca_gemm_effective_splits((int)K, (int)splits); }
+
+void im2col_u8(Tensor x, Tensor col, int64_t kh, int64_t kw, int64_t s, double scale) {
+  need(x, at::kByte, "x");
+  need(col, at::kBFloat16, "col");
+  TORCH_CHECK(x.dim() == 4, "im2col_u8: x must be [B, C, H, W]");
+  const int B = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int OH = (H - kh) / s + 1, OW = (W - kw) / s + 1;
+  TORCH_CHECK(col.numel() == (int64_t)B * OH * OW * C * kh * kw, "im2col_u8: col size mismatch");
+  check(aca_im2col_u8_nchw(ptr<uint8_t>(x), ptr<uint16_t>(col), B, C, H, W, kh, kw, s, (float)scale, cur_stream(x)),
+        "im2col_u8");
+}
+
+void im2col_nhwc(Tensor x, Tensor col, int64_t B, int64_t H, int64_t W, int64_t C, int64_t kh, int64_t kw,
+                 int64_t s) {
+  need(x, at::kBFloat16, "x");
+  need(col, at::kBFloat16, "col");
+  const int OH = (H - kh) / s + 1, OW = (W - kw) / s + 1;
+  TORCH_CHECK(x.numel() >= B * H * W * C, "im2col_nhwc: x too small");
+  TORCH_CHECK(col.numel() >= (int64_t)B * OH * OW * C * kh * kw, "im2col_nhwc: col too small");
+  check(aca_im2col_nhwc(ptr<uint16_t>(x), ptr<uint16_t>(col), B, C, H, W, kh, kw, s, cur_stream(x)), "im2col_nhwc");
+}
+
+void col2im_nhwc(Tensor dcol, Tensor ymask, Tensor dx, c10::optional<Tensor> colsum, int64_t B, int64_t H, int64_t W,
+                 int64_t C, int64_t kh, int64_t kw, int64_t s) {
+  need(dcol, at::kBFloat16, "dcol");
+  need(ymask, at::kBFloat16, "ymask");
+  need(dx, at::kBFloat16, "dx");
+  const int OH = (H - kh) / s + 1, OW = (W - kw) / s + 1;
+  TORCH_CHECK(dcol.numel() >= (int64_t)B * OH * OW * C * kh * kw, "col2im: dcol too small");
+  TORCH_CHECK(ymask.numel() >= B * H * W * C && dx.numel() >= B * H * W * C, "col2im: dx/ymask too small");
+  if (colsum.has_value() && colsum->defined())
+    TORCH_CHECK(colsum->scalar_type() == at::kFloat && colsum->numel() >= C, "col2im: colsum must be fp32 [C]");
+  check(aca_col2im_nhwc(ptr<uint16_t>(dcol), ptr<uint16_t>(ymask), ptr<uint16_t>(dx), optr<float>(colsum), B, C, H, W,
+                        kh, kw, s, cur_stream(dcol)),
+        "col2im_nhwc");
+}
+
+void colsum_bf16(Tensor x, int64_t M, int64_t N, int64_t ld, Tensor out) {
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16, "colsum: x must be bf16");
+  check_extent(x, M, N, ld, "x");
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.numel() >= N, "colsum: out must be fp32 [N]");
+  check(aca_colsum_bf16(ptr<uint16_t>(x), M, N, ld, ptr<float>(out), cur_stream(x)), "colsum_bf16");
+}
+
+// ---------------------------------------------------------------------------------------------- loss
+void ac_loss(Tensor logits, int64_t ldl, c10::optional<Tensor> value, int64_t ldv, c10::optional<Tensor> act_i,
+             c10::optional<Tensor> act_f, c10::optional<Tensor> log_std, Tensor logp_old, Tensor adv, Tensor ret,
+             c10::optional<Tensor> v_old, c10::optional<Tensor> ent_coef, c10::optional<Tensor> kl_coef,
+             double vf_coef, double ppo_clip, double v_clip, Tensor dlogits, int64_t lddl,
+             c10::optional<Tensor> dvalue, int64_t lddv, c10::optional<Tensor> dlog_std, Tensor stats, int64_t B,
+             int64_t A, bool gaussian) {
+  TORCH_CHECK(logits.scalar_type() == at::kFloat && dlogits.scalar_type() == at::kBFloat16, "ac_loss: dtypes");
+  check_extent(logits, B, A, ldl, "logits");
+  check_extent(dlogits, B, A, lddl, "dlogits");
+  need(logp_old, at::kFloat, "logp_old");
+  need(adv, at::kFloat, "adv");
+  need(ret, at::kFloat, "ret");
+  need(stats, at::kFloat, "stats");
+  TORCH_CHECK(logp_old.numel() >= B && adv.numel() >= B && ret.numel() >= B && stats.numel() >= 7, "ac_loss: sizes");
+  if (gaussian) {
+    TORCH_CHECK(act_f.has_value() && log_std.has_value(), "ac_loss: gaussian needs act_f and log_std");
+  } else {
+    TORCH_CHECK(act_i.has_value(), "ac_loss: categorical needs act_i");
+  }
+  if (value.has_value() && value->defined()) {
+    TORCH_CHECK(dvalue.has_value() && dvalue->defined(), "ac_loss: value needs dvalue");
+    check_extent(*value, B, 1, ldv, "value");
+    check_extent(*dvalue, B, 1, lddv, "dvalue");
+  }
+  check(aca_ac_loss(ptr<float>(logits), ldl, optr<float>(value), ldv, optr<int32_t>(act_i), optr<float>(act_f),
+                    optr<float>(log_std), ptr<float>(logp_old), ptr<float>(adv), ptr<float>(ret), optr<float>(v_old),
+                    optr<float>(ent_coef), optr<float>(kl_coef), (float)vf_coef, (float)ppo_clip, (float)v_clip,
+                    ptr<uint16_t>(dlogits), lddl, optr<uint16_t>(dvalue), lddv, optr<float>(dlog_std),
+                    ptr<float>(stats), (int)B, (int)A, gaussian ? 1 : 0, cur_stream(logits)),
+        "ac_loss");
+}
+
+int64_t ping() { return 355; }
+
+}  // namespace
+
+TORCH_LIBRARY(acamd, m) {
+  m.def("ping() -> int", &ping);
+  m.def("env_step_cartpole(Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, Tensor env_ids, "
+        "Tensor actions, Tensor prev, Tensor out, Tensor reward, Tensor done, Tensor truncated, int seed, "
+        "int max_steps, int k) -> ()");
+  m.def("env_step_pendulum(Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, Tensor env_ids, "
+        "Tensor actions, Tensor prev, Tensor out, Tensor reward, Tensor done, Tensor truncated, int seed, "
+        "int max_steps, int k) -> ()");
+  m.def("env_step_linear(Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, Tensor env_ids, "
+        "Tensor actions, Tensor A, Tensor B, Tensor prev, Tensor out, Tensor reward, Tensor done, Tensor truncated, "
+        "int seed, int max_steps, int k) -> ()");
+  m.def("env_step_pong(Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, Tensor env_ids, "
+        "Tensor actions, Tensor prev, Tensor out, Tensor reward, Tensor done, Tensor truncated, int seed, "
+        "int max_steps, int k) -> ()");
+  m.def("categorical_sample(Tensor logits, Tensor keys, int seed, Tensor act, Tensor logp, Tensor ent) -> ()");
+  m.def("gaussian_sample(Tensor mu, Tensor log_std, Tensor keys, int seed, Tensor act, Tensor logp, Tensor ent) -> ()");
+  m.def("gae(Tensor r, Tensor v, Tensor d, Tensor ret, Tensor adv, float gamma, float lam) -> ()");
+  m.def("nstep_returns(Tensor r, Tensor v, Tensor d, Tensor tgt, Tensor adv, float gamma, int L) -> ()");
+  m.def("normalize(Tensor a, Tensor out, float eps) -> ()");
+  m.def("moments(Tensor x, Tensor y, Tensor out) -> ()");
+  m.def("sumsq(Tensor x, Tensor partial, Tensor ticket, Tensor out) -> ()");
+  m.def("adam_step(Tensor p, Tensor g, Tensor m, Tensor v, Tensor lr, Tensor t, Tensor? gnorm_sq, Tensor? shadow, "
+        "float b1, float b2, float eps, float clip, float max_norm, Tensor ticket) -> ()");
+  m.def("rmsprop_step(Tensor p, Tensor g, Tensor v, Tensor lr, Tensor? gnorm_sq, Tensor? shadow, float alpha, "
+        "float eps, float clip, float max_norm) -> ()");
+  m.def("cast_bf16(Tensor x, Tensor y) -> ()");
+  m.def("gemm(Tensor A, int lda, bool a_k, Tensor B, int ldb, bool b_k, Tensor C, int ldc, int out_mode, int M, "
+        "int N, int K, float alpha, Tensor? bias, bool relu, Tensor? mask, int ldm, Tensor? colsum, int tile, "
+        "int splits, Tensor? ws, Tensor? tickets, int colsum_mod) -> ()");
+  m.def("gemm_effective_splits(int K, int splits) -> int", &gemm_effective_splits);
+  m.def("im2col_u8(Tensor x, Tensor col, int kh, int kw, int s, float scale) -> ()");
+  m.def("im2col_nhwc(Tensor x, Tensor col, int B, int H, int W, int C, int kh, int kw, int s) -> ()");
+  m.def("col2im_nhwc(Tensor dcol, Tensor ymask, Tensor dx, Tensor? colsum, int B, int H, int W, int C, int kh, "
+        "int kw, int s) -> ()");
+  m.def("colsum_bf16(Tensor x, int M, int N, int ld, Tensor out) -> ()");
+  m.def("ac_loss(Tensor logits, int ldl, Tensor? value, int ldv, Tensor? act_i, Tensor? act_f, Tensor? log_std, "
+        "Tensor logp_old, Tensor adv, Tensor ret, Tensor? v_old, Tensor? ent_coef, Tensor? kl_coef, float vf_coef, "
+        "float ppo_clip, float v_clip, Tensor dlogits, int lddl, Tensor? dvalue, int lddv, Tensor? dlog_std, "
+        "Tensor stats, int B, int A, bool gaussian) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
+  m.impl("env_step_cartpole", &env_step_cartpole);
+  m.impl("env_step_pendulum", &env_step_pendulum);
+  m.impl("env_step_linear", &env_step_linear);
+  m.impl("env_step_pong", &env_step_pong);
+  m.impl("categorical_sample", &categorical_sample);
+  m.impl("gaussian_sample", &gaussian_sample);
+  m.impl("gae", &gae);
+  m.impl("nstep_returns", &nstep_returns);
+  m.impl("normalize", &normalize);
+  m.impl("moments", &moments);
+  m.impl("sumsq", &sumsq);
+  m.impl("adam_step", &adam_step);
+  m.impl("rmsprop_step", &rmsprop_step);
+  m.impl("cast_bf16", &cast_bf16);
+  m.impl("gemm", &gemm);
+  m.impl("im2col_u8", &im2col_u8);
+  m.impl("im2col_nhwc", &im2col_nhwc);
+  m.impl("col2im_nhwc", &col2im_nhwc);
+  m.impl("colsum_bf16", &colsum_bf16);
+  m.impl("ac_loss", &ac_loss);
+}

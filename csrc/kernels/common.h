@@ -1,0 +1,130 @@
+// Shared device helpers for the gfx950 kernels of this package.
+//
+// Everything here is CDNA4-specific: 64-lane waves, bf16 MFMA fragments, wave-level shuffles over 64 lanes.
+// The kernels are plain HIP compiled by hipcc --offload-arch=gfx950; the host wrappers in each .hip file take raw
+// pointers + a hipStream_t so that only csrc/bindings.cpp has to see the (slow to compile) torch headers.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define ACA_WAVE 64
+
+namespace aca {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16;
+
+// ------------------------------------------------------------------------------------------------------------
+// Counter-based RNG. Bit-identical to actor_critic_algs_on_tensorflow_amd/envs/rng.py (lowbias32 finaliser).
+// ------------------------------------------------------------------------------------------------------------
+__host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+
+__host__ __device__ __forceinline__ uint32_t hash_u32(uint32_t seed, uint32_t env, uint32_t step, uint32_t stream) {
+  uint32_t h = mix32(seed ^ 0x9E3779B9u);
+  h = mix32(h ^ env);
+  h = mix32(h ^ (step * 0x27D4EB2Fu));
+  h = mix32(h ^ (stream * 0x165667B1u));
+  return h;
+}
+
+// [0, 1) with 24 random bits (envs)
+__device__ __forceinline__ float uniform01(uint32_t seed, uint32_t env, uint32_t step, uint32_t stream) {
+  return (float)(hash_u32(seed, env, step, stream) >> 8) * (1.0f / 16777216.0f);
+}
+
+// (0, 1) open interval (policy sampling); key = 64-bit per-row key split into (lo, hi) words
+__device__ __forceinline__ float uniform_open(uint32_t seed, int64_t key, uint32_t stream) {
+  uint32_t lo = (uint32_t)((uint64_t)key & 0xFFFFFFFFull);
+  uint32_t hi = (uint32_t)(((uint64_t)key >> 32) & 0xFFFFFFFFull);
+  uint32_t h = hash_u32(seed, lo, hi, stream);
+  return ((float)(h >> 8) + 0.5f) * (1.0f / 16777216.0f);
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// bf16 helpers (round-to-nearest-even through the compiler's cvt; NaN stays NaN)
+// ------------------------------------------------------------------------------------------------------------
+__device__ __forceinline__ float bf2f(u16 x) { return __uint_as_float(((uint32_t)x) << 16); }
+__device__ __forceinline__ u16 f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(u16, b);
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// wave / block reductions (64-lane waves)
+// ------------------------------------------------------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Block-wide sum for blockDim.x <= 1024; `sh` must hold >= 16 floats. Result valid in every thread.
+__device__ __forceinline__ float block_sum(float v, float* sh) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) sh[wid] = v;
+  __syncthreads();
+  float r = 0.f;
+  for (int i = 0; i < nw; ++i) r += sh[i];
+  return r;
+}
+
+__device__ __forceinline__ double block_sum_d(double v, double* sh) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  v = wave_sum_d(v);
+  __syncthreads();
+  if (lane == 0) sh[wid] = v;
+  __syncthreads();
+  double r = 0.0;
+  for (int i = 0; i < nw; ++i) r += sh[i];
+  return r;
+}
+
+// Last-arriver ticket (Guideline 16 counter form): every wave drains its stores, the block releases at agent
+// scope and takes a ticket; returns true in every thread of the block that arrived last. The caller then reads
+// the other blocks' results with plain loads (this function already performed the acquire).
+__device__ __forceinline__ bool last_block_arrival(unsigned int* ticket, unsigned int nblocks, int* sh_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned int t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int last = (t == nblocks - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // self-cleaning: the next launch starts from 0 again
+      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    *sh_flag = last;
+  }
+  __syncthreads();
+  return *sh_flag != 0;
+}
+
+}  // namespace aca
+
+#define ACA_LAUNCH_CHECK() \
+  do {                     \
+    (void)hipGetLastError(); \
+  } while (0)

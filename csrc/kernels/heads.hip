@@ -1,0 +1,95 @@
+// Policy heads: fused sample + log-prob + entropy, one launch per rollout step.
+//
+// categorical: logits [B, A] (fp32, row stride ldl) -> log_softmax, Gumbel-max sample with the counter-based
+//   hash (stream = action index), logp(a), entropy. One 64-lane wave per row; A <= 64 handled by one pass.
+// gaussian:    mu [B, A], log_std [A] clipped to [-2.5, 2.5] (Basic_AC/policies.py:49-58), Box-Muller sample,
+//   sum_i log N(a_i), sum_i (1/2 + 1/2 log 2pi + log sigma_i).
+// Oracles: ops/distributions.py (*_ref).
+#include "common.h"
+
+namespace aca {
+
+__global__ void __launch_bounds__(256) categorical_sample_kernel(const float* __restrict__ logits, int ldl, int B,
+                                                                 int A, const int64_t* __restrict__ keys,
+                                                                 uint32_t seed, int32_t* __restrict__ act,
+                                                                 float* __restrict__ logp, float* __restrict__ ent) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= B) return;
+  const bool on = lane < A;
+  const float z = on ? logits[(size_t)row * ldl + lane] : -INFINITY;
+  const float m = wave_max(z);
+  const float ex = on ? expf(z - m) : 0.f;
+  const float se = wave_sum(ex);
+  const float lse = m + logf(se);
+  const float lp = z - lse;  // log_softmax
+  const float h = on ? -expf(lp) * lp : 0.f;
+  const float H = wave_sum(h);
+  // Gumbel-max
+  float g = -INFINITY;
+  if (on) {
+    const float u = uniform_open(seed, keys[row], (uint32_t)lane);
+    g = z + (-logf(-logf(u)));
+  }
+  // argmax with first-index tie breaking
+  float best = g;
+  int bi = on ? lane : 1 << 30;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    float ob = __shfl_xor(best, o, 64);
+    int oi = __shfl_xor(bi, o, 64);
+    if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+  }
+  const float lpa = __shfl(lp, bi, 64);
+  if (lane == 0) {
+    act[row] = bi;
+    logp[row] = lpa;
+    ent[row] = H;
+  }
+}
+
+__global__ void gaussian_sample_kernel(const float* __restrict__ mu, int ldm, int B, int A,
+                                       const float* __restrict__ log_std, const int64_t* __restrict__ keys,
+                                       uint32_t seed, float* __restrict__ act, float* __restrict__ logp,
+                                       float* __restrict__ ent) {
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  if (row >= B) return;
+  const float HALF_LOG_2PI = 0.91893853320467274178f, TWO_PI = 6.28318530717958647692f;
+  const int64_t key = keys[row];
+  float lp = 0.f, H = 0.f;
+  for (int j = 0; j < A; ++j) {
+    const float ls = fminf(fmaxf(log_std[j], -2.5f), 2.5f);
+    const float u1 = uniform_open(seed, key, 2 * j), u2 = uniform_open(seed, key, 2 * j + 1);
+    const float eps = sqrtf(-2.0f * logf(u1)) * cosf(TWO_PI * u2);
+    const float m = mu[(size_t)row * ldm + j];
+    const float a = m + expf(ls) * eps;
+    act[(size_t)row * A + j] = a;
+    const float zz = (a - m) * expf(-ls);
+    lp += -0.5f * zz * zz - ls - HALF_LOG_2PI;
+    H += 0.5f + HALF_LOG_2PI + ls;
+  }
+  logp[row] = lp;
+  ent[row] = H;
+}
+
+}  // namespace aca
+
+extern "C" hipError_t aca_categorical_sample(const float* logits, int ldl, int B, int A, const int64_t* keys,
+                                             uint32_t seed, int32_t* act, float* logp, float* ent,
+                                             hipStream_t stream) {
+  if (B <= 0) return hipSuccess;
+  if (A > 64) return hipErrorInvalidValue;
+  const int rows_per_block = 4;
+  aca::categorical_sample_kernel<<<(B + rows_per_block - 1) / rows_per_block, 256, 0, stream>>>(
+      logits, ldl, B, A, keys, seed, act, logp, ent);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t aca_gaussian_sample(const float* mu, int ldm, int B, int A, const float* log_std,
+                                          const int64_t* keys, uint32_t seed, float* act, float* logp, float* ent,
+                                          hipStream_t stream) {
+  if (B <= 0) return hipSuccess;
+  aca::gaussian_sample_kernel<<<(B + 127) / 128, 128, 0, stream>>>(mu, ldm, B, A, log_std, keys, seed, act, logp,
+                                                                   ent);
+  return hipGetLastError();
+}

@@ -1,0 +1,171 @@
+// Fused actor-critic loss + head gradient, one launch per learner (mini)batch.
+//
+// Per row (categorical head; logits z [B, A], value v [B]):
+//   logp = log_softmax(z),  H = -sum p logp,  lpa = logp[a]
+//   A2C (reference, Basic_AC/policies.py:72-78):  L_pi = -mean(adv*lpa) + beta*mean((lpo-lpa)^2) - c_ent*mean(H)
+//   PPO-clip:  L_pi = -mean(min(r adv, clip(r, 1-e, 1+e) adv)) + beta*mean((lpo-lpa)^2) - c_ent*mean(H), r=e^(lpa-lpo)
+//   L_v = vf_coef * mean((v - R)^2)   (optionally PPO-clipped: max((v-R)^2, (v_old + clip(v - v_old) - R)^2))
+// and writes dL/dz, dL/dv as bf16 (the inputs of the backward GEMMs). Gaussian head (mu [B, A], log_std [A]):
+//   logp = sum -0.5 ((a-mu)/sigma)^2 - log sigma - log sqrt(2 pi), sigma = exp(clip(log_std, -2.5, 2.5)), H const in mu;
+//   d/dmu and d/dlog_std (zero outside the clip, Basic_AC/policies.py:50-51) -- log_std's gradient is summed over rows
+//   and added atomically into its slot of the fp32 gradient slab.
+// Coefficients (c_ent, beta) are read from device scalars (annealed by the schedules without a host sync).
+// stats[0..6] = pg, kl, entropy, value_loss (unscaled mean), clipfrac, total actor loss, mean ratio.
+// One 1024-thread workgroup: the stats reduction is deterministic.
+#include "common.h"
+
+namespace aca {
+
+struct LossArgs {
+  const float* logits; int64_t ldl;     // or mu for the gaussian head
+  const float* value; int64_t ldv;      // may be null (no critic term)
+  const int32_t* act_i;                 // categorical actions
+  const float* act_f;                   // gaussian actions [B, A]
+  const float* log_std;                 // gaussian
+  const float* logp_old;
+  const float* adv;
+  const float* ret;
+  const float* v_old;                   // may be null
+  const float* ent_coef;                // device scalar
+  const float* kl_coef;                 // device scalar
+  float vf_coef, ppo_clip, v_clip;
+  u16* dlogits; int64_t lddl;
+  u16* dvalue; int64_t lddv;
+  float* dlog_std;                      // gaussian: fp32 [A] (atomic add)
+  float* stats;
+  int B, A;
+  int gaussian;
+};
+
+__global__ void __launch_bounds__(1024) ac_loss_kernel(LossArgs a) {
+  __shared__ double sh[16];
+  __shared__ float dls[64];
+  if (threadIdx.x < 64) dls[threadIdx.x] = 0.f;
+  __syncthreads();
+  const float invB = 1.0f / (float)a.B;
+  const float c_ent = a.ent_coef ? *a.ent_coef : 0.f;
+  const float beta = a.kl_coef ? *a.kl_coef : 0.f;
+  const float HALF_LOG_2PI = 0.91893853320467274178f;
+  double s_pg = 0, s_kl = 0, s_H = 0, s_vl = 0, s_cf = 0, s_ratio = 0;
+  for (int b = threadIdx.x; b < a.B; b += blockDim.x) {
+    const float* z = a.logits + (int64_t)b * a.ldl;
+    float lpa = 0.f, H = 0.f, lse = 0.f;
+    if (!a.gaussian) {
+      float mx = -INFINITY;
+      for (int j = 0; j < a.A; ++j) mx = fmaxf(mx, z[j]);
+      float se = 0.f;
+      for (int j = 0; j < a.A; ++j) se += expf(z[j] - mx);
+      lse = mx + logf(se);
+      for (int j = 0; j < a.A; ++j) {
+        const float lz = z[j] - lse;
+        H -= expf(lz) * lz;
+      }
+      lpa = z[a.act_i[b]] - lse;
+    } else {
+      for (int j = 0; j < a.A; ++j) {
+        const float ls = fminf(fmaxf(a.log_std[j], -2.5f), 2.5f);
+        const float zz = (a.act_f[(int64_t)b * a.A + j] - z[j]) * expf(-ls);
+        lpa += -0.5f * zz * zz - ls - HALF_LOG_2PI;
+        H += 0.5f + HALF_LOG_2PI + ls;
+      }
+    }
+    const float lpo = a.logp_old[b], adv = a.adv[b];
+    float g_lpa;  // dL/dlpa (already divided by B)
+    if (a.ppo_clip > 0.f) {
+      const float ratio = expf(lpa - lpo);
+      const float s1 = ratio * adv;
+      const float rc = fminf(fmaxf(ratio, 1.0f - a.ppo_clip), 1.0f + a.ppo_clip);
+      const float s2 = rc * adv;
+      s_pg += -(double)fminf(s1, s2);
+      const bool inside = ratio >= 1.0f - a.ppo_clip && ratio <= 1.0f + a.ppo_clip;
+      g_lpa = (s1 <= s2 || inside) ? -adv * ratio * invB : 0.f;
+      s_cf += fabsf(ratio - 1.0f) > a.ppo_clip ? 1.0 : 0.0;
+      s_ratio += ratio;
+    } else {
+      s_pg += -(double)(adv * lpa);
+      g_lpa = -adv * invB;
+      s_ratio += 1.0;
+    }
+    const float dkl = lpo - lpa;
+    s_kl += (double)(dkl * dkl);
+    g_lpa += -2.0f * beta * dkl * invB;
+    s_H += H;
+    // head gradient
+    u16* dz = a.dlogits + (int64_t)b * a.lddl;
+    if (!a.gaussian) {
+      const int ab = a.act_i[b];
+      for (int j = 0; j < a.A; ++j) {
+        const float oh = (j == ab) ? 1.0f : 0.0f;
+        const float lz = z[j] - lse, pj = expf(lz);
+        const float g = g_lpa * (oh - pj) + c_ent * invB * pj * (lz + H);
+        dz[j] = f2bf(g);
+      }
+    } else {
+      for (int j = 0; j < a.A; ++j) {
+        const float ls_raw = a.log_std[j];
+        const float ls = fminf(fmaxf(ls_raw, -2.5f), 2.5f);
+        const float zz = (a.act_f[(int64_t)b * a.A + j] - z[j]) * expf(-ls);
+        // dlogp/dmu = zz / sigma ; dlogp/dls = zz^2 - 1 ; dH/dls = 1
+        dz[j] = f2bf(g_lpa * zz * expf(-ls));
+        const bool in_clip = ls_raw >= -2.5f && ls_raw <= 2.5f;
+        if (in_clip) atomicAdd(&dls[j], g_lpa * (zz * zz - 1.0f) - c_ent * invB);
+      }
+    }
+    // critic
+    if (a.value) {
+      const float v = a.value[(int64_t)b * a.ldv], R = a.ret[b];
+      float d = v - R;
+      float vl = d * d;
+      float gv = 2.0f * d;
+      if (a.v_clip > 0.f && a.v_old) {
+        const float vo = a.v_old[b];
+        const float vc = vo + fminf(fmaxf(v - vo, -a.v_clip), a.v_clip);
+        const float dc = vc - R;
+        if (dc * dc > vl) {
+          vl = dc * dc;
+          const bool inside = (v - vo) >= -a.v_clip && (v - vo) <= a.v_clip;
+          gv = inside ? 2.0f * dc : 0.f;
+        }
+      }
+      s_vl += vl;
+      a.dvalue[(int64_t)b * a.lddv] = f2bf(a.vf_coef * gv * invB);
+    }
+  }
+  s_pg = block_sum_d(s_pg, sh);
+  s_kl = block_sum_d(s_kl, sh);
+  s_H = block_sum_d(s_H, sh);
+  s_vl = block_sum_d(s_vl, sh);
+  s_cf = block_sum_d(s_cf, sh);
+  s_ratio = block_sum_d(s_ratio, sh);
+  __syncthreads();
+  if (a.gaussian && a.dlog_std && threadIdx.x < a.A) atomicAdd(&a.dlog_std[threadIdx.x], dls[threadIdx.x]);
+  if (threadIdx.x == 0) {
+    const double inv = 1.0 / a.B;
+    a.stats[0] = (float)(s_pg * inv);
+    a.stats[1] = (float)(s_kl * inv);
+    a.stats[2] = (float)(s_H * inv);
+    a.stats[3] = (float)(s_vl * inv);
+    a.stats[4] = (float)(s_cf * inv);
+    a.stats[5] = (float)(s_pg * inv + beta * s_kl * inv - c_ent * s_H * inv);
+    a.stats[6] = (float)(s_ratio * inv);
+  }
+}
+
+}  // namespace aca
+
+extern "C" hipError_t aca_ac_loss(const float* logits, int64_t ldl, const float* value, int64_t ldv,
+                                  const int32_t* act_i, const float* act_f, const float* log_std,
+                                  const float* logp_old, const float* adv, const float* ret, const float* v_old,
+                                  const float* ent_coef, const float* kl_coef, float vf_coef, float ppo_clip,
+                                  float v_clip, uint16_t* dlogits, int64_t lddl, uint16_t* dvalue, int64_t lddv,
+                                  float* dlog_std, float* stats, int B, int A, int gaussian, hipStream_t stream) {
+  if (A > 64) return hipErrorInvalidValue;
+  aca::LossArgs a;
+  a.logits = logits; a.ldl = ldl; a.value = value; a.ldv = ldv; a.act_i = act_i; a.act_f = act_f;
+  a.log_std = log_std; a.logp_old = logp_old; a.adv = adv; a.ret = ret; a.v_old = v_old; a.ent_coef = ent_coef;
+  a.kl_coef = kl_coef; a.vf_coef = vf_coef; a.ppo_clip = ppo_clip; a.v_clip = v_clip; a.dlogits = dlogits;
+  a.lddl = lddl; a.dvalue = dvalue; a.lddv = lddv; a.dlog_std = dlog_std; a.stats = stats; a.B = B; a.A = A;
+  a.gaussian = gaussian;
+  aca::ac_loss_kernel<<<1, 1024, 0, stream>>>(a);
+  return hipGetLastError();
+}

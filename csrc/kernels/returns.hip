@@ -1,0 +1,105 @@
+// Return / advantage estimators over [T, N] rollouts and small statistics (K12).
+//
+// * gae:    reverse scan per env column, A_t = delta_t + gamma*lambda*(1-d_t)*A_{t+1}; R_t = A_t + V_t.
+// * nstep:  PathAdv generalised to [T, N] (Basic_AC/run_AC.py:55-80): window [t, min(t+L, T)),
+//           discounted reward sum that stops at the first terminal transition, bootstrap gamma^(h-t) V[h] only if
+//           the window did not end in a terminal. One thread per (t, n).
+// * normalize_adv: (A - mean) / (1e-8 + std_pop) (Basic_AC/run_AC.py:241), one workgroup, fp64 sums.
+// * moments: sum, sum of squares of x and y and cross term (EV correlation Basic_AC/util.py:4-12).
+// Oracles: ops/returns.py, utils/stats.py.
+#include "common.h"
+
+namespace aca {
+
+__global__ void gae_kernel(const float* __restrict__ r, const float* __restrict__ v, const uint8_t* __restrict__ d,
+                           float* __restrict__ ret, float* __restrict__ adv, int T, int N, float gamma, float lam) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float last = 0.f;
+  for (int t = T - 1; t >= 0; --t) {
+    const size_t i = (size_t)t * N + n;
+    const float nd = d[i] ? 0.f : 1.f;
+    const float delta = r[i] + gamma * v[i + N] * nd - v[i];
+    last = delta + gamma * lam * nd * last;
+    adv[i] = last;
+    ret[i] = last + v[i];
+  }
+}
+
+__global__ void nstep_kernel(const float* __restrict__ r, const float* __restrict__ v, const uint8_t* __restrict__ d,
+                             float* __restrict__ tgt, float* __restrict__ adv, int T, int N, float gamma, int L) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= T * N) return;
+  const int t = idx / N, n = idx % N;
+  const int h = min(t + L, T);
+  float acc = 0.f, disc = 1.f;
+  bool alive = true;
+  for (int k = t; k < h; ++k) {
+    const size_t i = (size_t)k * N + n;
+    acc += disc * r[i];
+    disc *= gamma;
+    if (d[i]) { alive = false; break; }
+  }
+  if (alive) acc += disc * v[(size_t)h * N + n];
+  tgt[idx] = acc;
+  adv[idx] = acc - v[idx];
+}
+
+__global__ void __launch_bounds__(1024) normalize_kernel(const float* __restrict__ a, float* __restrict__ out, int n,
+                                                         float eps) {
+  __shared__ double sh[16];
+  double s = 0.0, s2 = 0.0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const double x = a[i];
+    s += x;
+    s2 += x * x;
+  }
+  s = block_sum_d(s, sh);
+  s2 = block_sum_d(s2, sh);
+  const double mean = s / n;
+  const double var = fmax(s2 / n - mean * mean, 0.0);
+  const float fm = (float)mean, inv = 1.0f / (eps + (float)sqrt(var));
+  for (int i = threadIdx.x; i < n; i += blockDim.x) out[i] = (a[i] - fm) * inv;
+}
+
+// out[0..4] = sum x, sum x^2, sum y, sum y^2, sum x*y  (fp64 accumulation, fp32 results)
+__global__ void __launch_bounds__(1024) moments_kernel(const float* __restrict__ x, const float* __restrict__ y,
+                                                       float* __restrict__ out, int n) {
+  __shared__ double sh[16];
+  double a = 0, b = 0, c = 0, dd = 0, e = 0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const double xi = x[i], yi = y[i];
+    a += xi; b += xi * xi; c += yi; dd += yi * yi; e += xi * yi;
+  }
+  a = block_sum_d(a, sh); b = block_sum_d(b, sh); c = block_sum_d(c, sh);
+  dd = block_sum_d(dd, sh); e = block_sum_d(e, sh);
+  if (threadIdx.x == 0) { out[0] = a; out[1] = b; out[2] = c; out[3] = dd; out[4] = e; }
+}
+
+}  // namespace aca
+
+extern "C" hipError_t aca_gae(const float* r, const float* v, const uint8_t* d, float* ret, float* adv, int T, int N,
+                              float gamma, float lam, hipStream_t stream) {
+  if (T <= 0 || N <= 0) return hipSuccess;
+  aca::gae_kernel<<<(N + 255) / 256, 256, 0, stream>>>(r, v, d, ret, adv, T, N, gamma, lam);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t aca_nstep(const float* r, const float* v, const uint8_t* d, float* tgt, float* adv, int T,
+                                int N, float gamma, int L, hipStream_t stream) {
+  if (T <= 0 || N <= 0) return hipSuccess;
+  const int tot = T * N;
+  aca::nstep_kernel<<<(tot + 255) / 256, 256, 0, stream>>>(r, v, d, tgt, adv, T, N, gamma, L);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t aca_normalize(const float* a, float* out, int n, float eps, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  aca::normalize_kernel<<<1, 1024, 0, stream>>>(a, out, n, eps);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t aca_moments(const float* x, const float* y, float* out, int n, hipStream_t stream) {
+  aca::moments_kernel<<<1, 1024, 0, stream>>>(x, y, out, n);
+  return hipGetLastError();
+}

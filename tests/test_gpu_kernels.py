@@ -1,0 +1,295 @@
+"""Numerics of every hand-written HIP kernel against its fp32 PyTorch reference (run on an MI355X).
+
+Each test calls the ``torch.ops.acamd`` op directly (the native path is required: the ``cuda`` fixture refuses to
+run without the extension) and compares with the oracle in ``ops/*`` / ``envs/*`` evaluated on the same inputs.
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _bf(x):
+    return x.to(torch.bfloat16)
+
+
+# ------------------------------------------------------------------------------------------------------ GEMM
+@pytest.mark.parametrize("a_k", [True, False])
+@pytest.mark.parametrize("b_k", [True, False])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4])
+def test_gemm_layouts_tiles(cuda, a_k, b_k, tile):
+    from actor_critic_algs_on_tensorflow_amd.ops import gemm as G
+    g = torch.Generator(device="cpu").manual_seed(tile * 7 + a_k * 2 + b_k)
+    for (M, N, K) in [(70, 45, 100), (256, 128, 320), (33, 7, 512), (513, 96, 64)]:
+        lda = (K if a_k else M) + 8
+        ldb = (K if b_k else N) + 8
+        A = _bf(torch.randn((M if a_k else K) * lda, generator=g)).to(cuda)
+        B = _bf(torch.randn((N if b_k else K) * ldb, generator=g)).to(cuda)
+        bias = torch.randn(N, generator=g).to(cuda)
+        mask = _bf(torch.randn(M * N, generator=g)).to(cuda)
+        ref = G.gemm_ref(A, lda, a_k, B, ldb, b_k, M, N, K, alpha=0.5, bias=bias, relu=True, mask=mask, ldm=N)
+        C = torch.full((M * N,), float("nan"), device=cuda)
+        colsum = torch.zeros(N, device=cuda)
+        G.gemm(A, lda, a_k, B, ldb, b_k, C, N, 0, M, N, K, alpha=0.5, bias=bias, relu=True, mask=mask, ldm=N,
+               colsum=colsum, tile=tile, splits=1)
+        scale = ref.abs().max().item() + 1e-3
+        assert (C.view(M, N) - ref).abs().max().item() <= 2e-3 * scale * math.sqrt(K / 64), (M, N, K)
+        assert torch.allclose(colsum, ref.sum(0), rtol=1e-3, atol=1e-2 * scale)
+        # bf16 output, slab split-K (deterministic last-arriver reduction)
+        ws = G.GemmWorkspace(cuda)
+        Cb = torch.empty(M * N, dtype=torch.bfloat16, device=cuda)
+        G.gemm(A, lda, a_k, B, ldb, b_k, Cb, N, 1, M, N, K, alpha=0.5, bias=bias, relu=True, mask=mask, ldm=N,
+               tile=tile, splits=4, workspace=ws)
+        assert (Cb.view(M, N).float() - ref).abs().max().item() <= 1e-2 * scale
+        assert int(ws.tickets.abs().sum()) == 0  # tickets are self-cleaning
+        # atomic split-K (weight-gradient mode)
+        Ca = torch.zeros(M * N, device=cuda)
+        G.gemm(A, lda, a_k, B, ldb, b_k, Ca, N, 2, M, N, K, alpha=0.5, tile=tile, splits=3)
+        ref2 = G.gemm_ref(A, lda, a_k, B, ldb, b_k, M, N, K, alpha=0.5)
+        assert (Ca.view(M, N) - ref2).abs().max().item() <= 2e-3 * (ref2.abs().max().item() + 1e-3) * math.sqrt(K / 64)
+
+
+def test_gemm_identity_asymmetric(cuda):
+    """A = I with an asymmetric B catches a transposed C write (guide §3)."""
+    from actor_critic_algs_on_tensorflow_amd.ops import gemm as G
+    n = 64
+    A = _bf(torch.eye(n)).to(cuda).reshape(-1)
+    Bm = torch.arange(n * n, dtype=torch.float32).view(n, n) % 17 - 8
+    for b_k in (True, False):
+        B = _bf(Bm.t().contiguous() if b_k else Bm).to(cuda).reshape(-1)
+        C = torch.zeros(n * n, device=cuda)
+        G.gemm(A, n, True, B, n, b_k, C, n, 0, n, n, n, tile=0, splits=1)
+        assert torch.equal(C.view(n, n).cpu(), Bm)
+
+
+# ------------------------------------------------------------------------------------------------------ conv lowering
+def test_im2col_col2im(cuda):
+    from actor_critic_algs_on_tensorflow_amd.ops import gemm as G
+    B = 3
+    x = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device=cuda)
+    col = torch.empty(B * 400, 256, dtype=torch.bfloat16, device=cuda)
+    G.im2col_u8(x, col, 8, 8, 4)
+    ref = G.im2col_u8_ref(x.cpu(), 8, 8, 4).to(torch.bfloat16)
+    assert torch.equal(col.cpu(), ref)
+    y = _bf(torch.randn(B * 20 * 20, 32)).to(cuda)
+    col2 = torch.empty(B * 81, 512, dtype=torch.bfloat16, device=cuda)
+    G.im2col_nhwc(y, col2, B, 20, 20, 32, 4, 4, 2)
+    assert torch.equal(col2.cpu().float(), G.im2col_nhwc_ref(y.cpu(), B, 20, 20, 32, 4, 4, 2))
+    # col2im is the adjoint of im2col (with the ReLU mask)
+    for (H, C, k, s) in [(20, 32, 4, 2), (9, 64, 3, 1)]:
+        OH = (H - k) // s + 1
+        dcol = _bf(torch.randn(B * OH * OH, k * k * C)).to(cuda)
+        ym = _bf(torch.randn(B * H * H, C)).to(cuda)
+        dx = torch.empty(B * H * H, C, dtype=torch.bfloat16, device=cuda)
+        cs = torch.zeros(C, device=cuda)
+        G.col2im_nhwc(dcol, ym, dx, cs, B, H, H, C, k, k, s)
+        ref = G.col2im_nhwc_ref(dcol.cpu(), ym.cpu(), B, H, H, C, k, k, s)
+        assert (dx.cpu().float() - ref).abs().max().item() < 0.05
+        assert torch.allclose(cs.cpu(), dx.cpu().float().sum(0), rtol=1e-3, atol=1e-2)
+
+
+# ------------------------------------------------------------------------------------------------------ env banks
+@pytest.mark.parametrize("env_id", ["PongNoFrameskip-v4", "CartPole-v1", "Pendulum-v0", "HalfCheetahShape-v0"])
+def test_env_bank_matches_oracle(cuda, env_id):
+    from actor_critic_algs_on_tensorflow_amd import envs as E
+    N = 16
+    gpu = E.make(env_id, N, device=cuda, seed=5)
+    cpu = E.make(env_id, N, device="cpu", seed=5)
+    gpu.reset()
+    cpu.reset()
+    gpu.state.copy_(cpu.state)
+    gpu.obs.copy_(cpu.obs)
+    g = torch.Generator().manual_seed(1)
+    steps = 300 if env_id.startswith("Pong") else 60
+    for t in range(steps):
+        a = cpu.sample_actions(generator=g)
+        prev_c, prev_g = cpu.obs.clone(), gpu.obs.clone()
+        oc, rc, dc, _ = cpu.step(a, prev_obs=prev_c, obs_out=cpu.obs)
+        og, rg, dg, _ = gpu.step(a.to(cuda), prev_obs=prev_g, obs_out=gpu.obs)
+        assert torch.equal(dc, dg.cpu()), (env_id, t)
+        if env_id.startswith("Pong"):
+            assert torch.equal(rc, rg.cpu()), t
+            assert torch.equal(oc, og.cpu()), t
+            assert torch.equal(cpu.state, gpu.state.cpu()), t
+        else:
+            assert torch.allclose(rc, rg.cpu(), rtol=1e-4, atol=1e-4), (env_id, t)
+            assert torch.allclose(oc, og.cpu(), rtol=1e-4, atol=1e-4), (env_id, t)
+            gpu.state.copy_(cpu.state)  # keep chaotic dynamics from drifting apart by ulps
+            gpu.obs.copy_(cpu.obs)
+    assert torch.allclose(cpu.ep_stats, gpu.ep_stats.cpu(), rtol=1e-4, atol=1e-3)
+
+
+# ------------------------------------------------------------------------------------------------------ heads / returns
+def test_categorical_and_gaussian_heads(cuda):
+    from actor_critic_algs_on_tensorflow_amd.ops import distributions as D
+    B, A = 2048, 6
+    logits = torch.randn(B, A) * 2
+    keys = torch.arange(B, dtype=torch.int64) * 7919 + (3 << 33)
+    a_r, lp_r, e_r = D.categorical_sample_ref(logits, keys, 11)
+    a_g, lp_g, e_g = D.categorical_sample(logits.to(cuda), keys.to(cuda), 11)
+    assert (a_r == a_g.cpu()).float().mean() > 0.999
+    same = a_r == a_g.cpu()
+    assert torch.allclose(lp_r[same], lp_g.cpu()[same], atol=1e-5)
+    assert torch.allclose(e_r, e_g.cpu(), atol=1e-5)
+    # empirical distribution of Gumbel-max sampling matches softmax
+    lg = torch.tensor([[0.0, 1.0, 2.0, -1.0]]).repeat(200000, 1)
+    k = torch.arange(200000, dtype=torch.int64)
+    a, _, _ = D.categorical_sample(lg.to(cuda), k.to(cuda), 3)
+    freq = torch.bincount(a.cpu().long(), minlength=4).float() / 200000
+    assert torch.allclose(freq, torch.softmax(lg[0], 0), atol=5e-3)
+    mu = torch.randn(B, 3)
+    ls = torch.tensor([0.3, -3.0, 1.0])
+    r = D.gaussian_sample_ref(mu, ls, keys, 5)
+    gq = D.gaussian_sample(mu.to(cuda), ls.to(cuda), keys.to(cuda), 5)
+    for x, y in zip(r, gq):
+        assert torch.allclose(x, y.cpu(), rtol=1e-4, atol=1e-4)
+
+
+def test_returns_kernels(cuda):
+    from actor_critic_algs_on_tensorflow_amd.ops import returns as R
+    T, N = 37, 19
+    g = torch.Generator().manual_seed(0)
+    r = torch.randn(T, N, generator=g)
+    v = torch.randn(T + 1, N, generator=g)
+    d = (torch.rand(T, N, generator=g) < 0.1).to(torch.uint8)
+    for L in (1, 5, 40):
+        a = R.nstep_returns_ref(r, v, d, 0.98, L)
+        b = R.nstep_returns(r.to(cuda), v.to(cuda), d.to(cuda), 0.98, L)
+        for x, y in zip(a, b):
+            assert torch.allclose(x, y.cpu(), atol=1e-4)
+    a = R.gae_ref(r, v, d, 0.99, 0.95)
+    b = R.gae(r.to(cuda), v.to(cuda), d.to(cuda), 0.99, 0.95)
+    for x, y in zip(a, b):
+        assert torch.allclose(x, y.cpu(), atol=1e-4)
+    adv = torch.randn(5000, generator=g) * 3 + 1
+    out = torch.empty(5000, device=cuda)
+    from actor_critic_algs_on_tensorflow_amd import _native
+    _native.require().normalize(adv.to(cuda), out, 1e-8)
+    assert torch.allclose(out.cpu(), R.normalize_advantages(adv), atol=1e-5)
+
+
+# ------------------------------------------------------------------------------------------------------ optimisers
+@pytest.mark.parametrize("name", ["adam", "rmsprop"])
+@pytest.mark.parametrize("clip,max_norm", [(None, None), (0.1, None), (None, 0.5), (1.0, 0.5)])
+def test_fused_optimizers(cuda, name, clip, max_norm):
+    from actor_critic_algs_on_tensorflow_amd.ops.optim import FlatParams, make_optimizer
+    n = 100003
+    p0 = torch.randn(n)
+    res = {}
+    for dev in ("cpu", cuda):
+        p = torch.nn.Parameter(p0.clone())
+        flat = FlatParams({"shared": [p]}, torch.device(dev))
+        sh = torch.empty(flat.numel, dtype=torch.bfloat16, device=dev)
+        opt = make_optimizer(name, flat, "shared", 1e-3, clip, max_norm, bf16_shadow=sh)
+        g = torch.Generator().manual_seed(4)
+        for _ in range(5):
+            flat.grad.copy_((torch.randn(n, generator=g) * 0.3).to(dev))
+            opt.step()
+        res[str(dev)] = (flat.data.cpu(), sh.cpu(), float(opt.t))
+    a, b = res["cpu"], res[str(cuda)]
+    assert torch.allclose(a[0], b[0], rtol=1e-5, atol=1e-6)
+    assert torch.allclose(b[1].float(), b[0], rtol=1e-2, atol=1e-3)
+    if name == "adam":
+        assert a[2] == b[2] == 5.0
+
+
+# ------------------------------------------------------------------------------------------------------ loss
+@pytest.mark.parametrize("ppo", [False, True])
+def test_ac_loss_kernel_matches_autograd(cuda, ppo):
+    from actor_critic_algs_on_tensorflow_amd import _native
+    from actor_critic_algs_on_tensorflow_amd.algos import losses as L
+    from actor_critic_algs_on_tensorflow_amd.ops import distributions as D
+    B, A = 300, 6
+    g = torch.Generator().manual_seed(2)
+    z = torch.randn(B, A + 1, generator=g)
+    act = torch.randint(0, A, (B,), generator=g, dtype=torch.int32)
+    lpo = D.categorical_logp_entropy(z[:, :A], act)[0] + 0.1 * torch.randn(B, generator=g)
+    adv = torch.randn(B, generator=g)
+    ret = torch.randn(B, generator=g)
+    ent_c, kl_c, vf = 0.01, 0.3, 0.5
+    zz = z.clone().requires_grad_(True)
+    logp, ent = D.categorical_logp_entropy(zz[:, :A], act)
+    if ppo:
+        al, pg, kl, em, cf = L.ppo_actor_loss(logp, lpo, adv, ent, 0.2, ent_c, kl_c)
+    else:
+        al, pg, kl, em = L.actor_loss(logp, lpo, adv, ent, kl_c, ent_c)
+    vl = L.value_loss(zz[:, A], ret)
+    (al + vf * vl).backward()
+    zc = z.to(cuda)
+    dz = torch.empty(B, A + 1, dtype=torch.bfloat16, device=cuda)
+    stats = torch.zeros(8, device=cuda)
+    _native.require().ac_loss(zc, A + 1, zc[:, A:], A + 1, act.to(cuda), None, None, lpo.to(cuda), adv.to(cuda),
+                              ret.to(cuda), None, torch.tensor(ent_c, device=cuda), torch.tensor(kl_c, device=cuda),
+                              vf, 0.2 if ppo else 0.0, 0.0, dz, A + 1, dz[:, A:], A + 1, None, stats, B, A, False)
+    assert torch.allclose(dz.cpu().float(), zz.grad, rtol=2e-2, atol=2e-5)
+    s = stats.cpu()
+    assert abs(s[5] - al.item()) < 1e-4 and abs(s[3] - vl.item()) < 1e-4 and abs(s[1] - kl.item()) < 1e-5
+
+
+# ------------------------------------------------------------------------------------------------------ engine
+def test_cnn_engine_matches_autograd(cuda):
+    """Full native forward + loss + backward of the Atari CNN vs fp32 autograd on the same parameters."""
+    from actor_critic_algs_on_tensorflow_amd.algos import losses as L
+    from actor_critic_algs_on_tensorflow_amd.algos.engine import CNNEngine
+    from actor_critic_algs_on_tensorflow_amd.models.policy import CNNActorCritic
+    from actor_critic_algs_on_tensorflow_amd.ops import distributions as D
+    from actor_critic_algs_on_tensorflow_amd.ops.optim import FlatParams
+    torch.manual_seed(0)
+    A, B = 6, 24
+    model = CNNActorCritic(A, generator=torch.Generator().manual_seed(3)).to(cuda)
+    with torch.no_grad():  # make the tiny head weights large enough to test the head gradient path well
+        model.net.heads.kernel.mul_(20)
+        for m in (model.net.trunk.conv1, model.net.trunk.conv2, model.net.trunk.conv3):
+            m.bias.uniform_(-0.05, 0.1)
+    flat = FlatParams(model.param_groups(), cuda)
+    shadow = flat.data.to(torch.bfloat16)
+    eng = CNNEngine(model, flat, shadow)
+    obs = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device=cuda)
+    b = eng.bufs(B, with_grad=True)
+    z = eng.forward(obs, b).clone()
+    # fp32 reference on the bf16-rounded parameters
+    ref_model = CNNActorCritic(A).to(cuda)
+    with torch.no_grad():
+        for pr, p in zip(ref_model.parameters(), model.parameters()):
+            pr.copy_(p.to(torch.bfloat16).float())
+    logits, v = ref_model(obs)
+    zr = torch.cat([logits, v[:, None]], 1)
+    assert (z - zr).abs().max().item() < 3e-2 * (zr.abs().max().item() + 1e-2)
+    act = torch.randint(0, A, (B,), device=cuda, dtype=torch.int32)
+    lpo = D.categorical_logp_entropy(zr[:, :A].detach(), act)[0]
+    adv = torch.randn(B, device=cuda)
+    ret = torch.randn(B, device=cuda)
+    ec, kc = torch.tensor(0.01, device=cuda), torch.tensor(0.0, device=cuda)
+    flat.zero_grad()
+    eng.loss(b, act, lpo, adv, ret, None, ec, kc, 0.5, 0.0, 0.0)
+    eng.backward(b)
+    logp, ent = D.categorical_logp_entropy(logits, act)
+    al, *_ = L.actor_loss(logp, lpo, adv, ent, 0.0, 0.01)
+    (al + 0.5 * L.value_loss(v, ret)).backward()
+    for (name, p), pr in zip(model.named_parameters(), ref_model.parameters()):
+        i = [id(q) for q in flat.params].index(id(p))
+        off = flat.offsets[i]
+        g = flat.grad[off:off + p.numel()].view_as(p)
+        err = (g - pr.grad).norm() / (pr.grad.norm() + 1e-12)
+        assert err < 0.05, (name, float(err))
+
+
+def test_trainer_native_graph_updates(cuda):
+    from actor_critic_algs_on_tensorflow_amd import preset
+    from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
+    for algo in ("pong_a2c", "breakout_ppo"):
+        kw = dict(num_envs=8, device="cuda:0", outdir=None, quiet=True, stdout_freq=0, save_every=0)
+        if algo == "breakout_ppo":
+            kw.update(n_steps=16, ppo_minibatches=2, ppo_epochs=2)
+        tr = ActorCriticTrainer(preset(algo, **kw))
+        assert tr.engine is not None
+        tr.capture(warmup=1)
+        p0 = tr.flat.data.clone()
+        for _ in range(5):
+            tr.step()
+        torch.cuda.synchronize()
+        assert torch.isfinite(tr.flat.data).all()
+        assert (tr.flat.data - p0).abs().max() > 0
+        assert torch.isfinite(torch.stack(list(tr.stats.values()))).all()

@@ -143,10 +143,13 @@ class CNNEngine:
         G.gemm(b.dy1, 32, False, b.col1, 256, False, self.gW1, 256, 2, 32, 256, B * 400, workspace=ws)
 
     # ------------------------------------------------------------------------------------------------ loss
-    def loss(self, b: _Bufs, actions, logp_old, adv, ret, v_old, ent_coef, kl_coef, vf_coef, ppo_clip, v_clip):
+    def loss(self, b: _Bufs, actions, logp_old, adv, ret, v_old, ent_coef, kl_coef, vf_coef, ppo_clip, v_clip,
+             stats=None):
+        """Fused loss + head gradient -> ``b.dz``; statistics [pg, kl, ent, vloss, clipfrac, actor loss, ratio]."""
         B, A, A1 = b.B, self.A, self.A1
         zl = b.z
+        out = b.stats if stats is None else stats
         _native.require().ac_loss(zl, A1, zl[:, A:], A1, actions, None, None, logp_old, adv, ret, v_old, ent_coef,
                                   kl_coef, float(vf_coef), float(ppo_clip or 0.0), float(v_clip or 0.0), b.dz, A1,
-                                  b.dz[:, A:], A1, None, b.stats, B, A, False)
-        return b.stats
+                                  b.dz[:, A:], A1, None, out, B, A, False)
+        return out

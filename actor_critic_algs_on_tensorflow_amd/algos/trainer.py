@@ -5,23 +5,23 @@ returns/advantages (n-step or GAE), then learn:
   * ``a2c``: one full-batch gradient step (as the reference: ``Basic_AC/run_AC.py:250-251``);
   * ``ppo``: ``ppo_epochs`` x ``ppo_minibatches`` clipped-surrogate steps.
 
-Reference features kept: KL-proxy + entropy regularised actor loss, per-batch advantage normalisation,
-element-wise gradient clipping, TF-semantics Adam, KL-adaptive actor lr (device-side), log10 annealing of the
-entropy/KL coefficients, the reference Logger format, EV before/after.
+Reference features kept: KL-proxy + entropy regularised actor loss (``Basic_AC/policies.py:72-78``), per-batch
+advantage normalisation (``Basic_AC/run_AC.py:241``), element-wise gradient clipping, TF-semantics Adam,
+KL-adaptive actor lr (``Basic_AC/run_AC.py:257-266``, device-side), log10 annealing of the entropy/KL coefficients
+(``Basic_AC/run_AC.py:181-182,268-275``), the reference Logger format, EV before/after.
 
-Execution: all state lives on the device; nothing in ``collect``/``learn`` reads back to the host, so on a GPU
-the whole update is captured once as a hipGraph (``torch.cuda.CUDAGraph``) and replayed -- the host issues one
-graph launch per update. Data parallelism (sync DP over RCCL) plugs in between backward and the optimiser step
-(:mod:`..parallel.dp`); with ``overlap="lag1"`` the gradient all-reduce runs on a side stream while the next
-rollout is collected.
-
-The CNN family on GPU can instead run the hand-written HIP engine (:mod:`.engine`) which replaces autograd with
-explicit fused forward/backward kernels.
+Two execution engines share this driver:
+  * ``native`` (CNN family on GPU, the default there): the hand-written HIP engine of :mod:`.engine` -- explicit
+    MFMA forward/backward, fused loss/head-gradient kernel, env kernels writing straight into the rollout slabs,
+    sampling kernel deriving its RNG keys from the env counters, optimiser zeroing the gradient slab after use.
+  * ``torch`` (everything else, and the CPU oracle): the same maths through autograd over the same flat slabs.
+Nothing in ``collect``/``learn`` reads back to the host, so on a GPU the update is captured as hipGraph(s) and
+replayed (see ``capture``). Data parallelism (sync DP over RCCL, :mod:`..parallel.dp`) all-reduces the flat
+gradient slab between backward and the optimiser step.
 """
 from __future__ import annotations
 
 import math
-import os
 import time
 
 import torch
@@ -40,6 +40,9 @@ from . import losses as L
 from .storage import RolloutStorage
 
 KEY_ENV_BITS = 20
+# layout of the device statistics buffer; slots 0..6 are written directly by the fused loss kernel
+STAT_KEYS = ("pg", "kl", "entropy", "crit_loss", "clipfrac", "act_loss", "ratio", "ev_before", "ev_after")
+LOG_KEYS = ("act_loss", "crit_loss", "kl", "entropy", "ev_before", "ev_after", "clipfrac")
 
 
 class ActorCriticTrainer:
@@ -49,7 +52,7 @@ class ActorCriticTrainer:
         self.dp = dp
         self.rank = dp.rank if dp is not None else 0
         self.world = dp.world_size if dp is not None else 1
-        fs = 4 if "Pong" in cfg.env or "Breakout" in cfg.env else cfg.frames
+        fs = 4 if ("Pong" in cfg.env or "Breakout" in cfg.env) else cfg.frames
         self.env = env if env is not None else E.make(
             cfg.env, cfg.num_envs, device=self.device, seed=cfg.seed, env_offset=self.rank * cfg.num_envs,
             frame_stack=fs)
@@ -70,11 +73,13 @@ class ActorCriticTrainer:
             s, e = self.flat.groups[g]
             sh = self.shadow[s:e] if self.shadow is not None else None
             if g == "critic":
-                self.opts[g] = make_optimizer(cfg.optimizer, self.flat, g, cfg.critic_lr, cfg.critic_clip_value,
-                                              cfg.max_grad_norm, bf16_shadow=sh)
+                opt = make_optimizer(cfg.optimizer, self.flat, g, cfg.critic_lr, cfg.critic_clip_value,
+                                     cfg.max_grad_norm, bf16_shadow=sh)
             else:
-                self.opts[g] = make_optimizer(cfg.optimizer, self.flat, g, cfg.lr, cfg.clip_value, cfg.max_grad_norm,
-                                              bf16_shadow=sh)
+                opt = make_optimizer(cfg.optimizer, self.flat, g, cfg.lr, cfg.clip_value, cfg.max_grad_norm,
+                                     bf16_shadow=sh)
+            opt.zero_grad_after = self.engine is not None
+            self.opts[g] = opt
         self.actor_opt = self.opts.get("actor", self.opts.get("shared"))
         T, N = cfg.n_steps, self.env.num_envs
         act_shape = () if self.env.is_discrete else tuple(self.env.action_space.shape)
@@ -89,11 +94,13 @@ class ActorCriticTrainer:
         self.reg_sched = RegularizerSchedule() if cfg.anneal_regularizers else None
         self.policy_seed = (cfg.seed * 7919 + 17) & 0xFFFFFFFF
         self.update_counter = torch.zeros((), dtype=torch.int64, device=dev)
-        self.stats = {k: torch.zeros((), device=dev) for k in
-                      ("act_loss", "crit_loss", "kl", "entropy", "ev_before", "ev_after", "clipfrac")}
+        self.stats_buf = torch.zeros(16, dtype=torch.float32, device=dev)
+        self.stats = {k: self.stats_buf[i] for i, k in enumerate(STAT_KEYS)}
+        self.adv_buf = torch.zeros(T * N, dtype=torch.float32, device=dev)
         self.iteration = 0
         self.env_steps = 0
         self.graph = None
+        self._defer_allreduce = False
         self.logger = None
         if self.rank == 0 and cfg.outdir:
             self.logger = Logger(cfg.outdir, legacy_step_index=cfg.legacy_step_index, metrics_path=cfg.metrics_path,
@@ -122,16 +129,13 @@ class ActorCriticTrainer:
         for t in range(st.T):
             obs_t = st.obs[t]
             pi, v = model(obs_t)
-            keys = self._keys()
-            a, logp, ent = model.sample(pi, keys, self.policy_seed)
+            a, logp, ent = model.sample(pi, self._keys(), self.policy_seed)
             st.actions[t].copy_(a.view_as(st.actions[t]))
             st.logp[t].copy_(logp)
             st.entropy[t].copy_(ent)
             st.values[t].copy_(v)
-            env.step(a, prev_obs=obs_t, obs_out=st.obs[t + 1])
-            st.rewards[t].copy_(env.reward)
-            st.dones[t].copy_(env.done)
-            st.truncated[t].copy_(env.truncated)
+            env.step(a, prev_obs=obs_t, obs_out=st.obs[t + 1], reward_out=st.rewards[t], done_out=st.dones[t],
+                     trunc_out=st.truncated[t])
         st.values[st.T].copy_(model.value(st.obs[st.T]))
 
     @torch.no_grad()
@@ -142,13 +146,11 @@ class ActorCriticTrainer:
         ops = _native.require()
         for t in range(st.T):
             z = eng.forward(st.obs[t], b)
-            ops.categorical_sample(z[:, :A], self._keys(), self.policy_seed, st.actions[t], st.logp[t],
-                                   st.entropy[t])
-            st.values[t].copy_(z[:, A])
-            env.step(st.actions[t], prev_obs=st.obs[t], obs_out=st.obs[t + 1])
-            st.rewards[t].copy_(env.reward)
-            st.dones[t].copy_(env.done)
-            st.truncated[t].copy_(env.truncated)
+            # one launch: sample + logp + entropy + value copy, RNG keys from the env counters
+            ops.categorical_sample_env(z[:, :A], env.tg, env.env_ids, KEY_ENV_BITS, self.policy_seed, st.actions[t],
+                                       st.logp[t], st.entropy[t], st.values[t])
+            env.step(st.actions[t], prev_obs=st.obs[t], obs_out=st.obs[t + 1], reward_out=st.rewards[t],
+                     done_out=st.dones[t], trunc_out=st.truncated[t])
         z = eng.forward(st.obs[st.T], b)
         st.values[st.T].copy_(z[:, A])
 
@@ -164,13 +166,27 @@ class ActorCriticTrainer:
             ret, adv = R.nstep_returns(st.rewards, st.values, dones, cfg.gamma, cfg.look_ahead)
         return ret.reshape(-1), adv.reshape(-1)
 
-    # ------------------------------------------------------------------ learning
+    def _normalize(self, adv):
+        if self.dp is not None:
+            return self.dp.normalize_advantages(adv)
+        if _native.use_native(adv):
+            _native.require().normalize(adv.contiguous(), self.adv_buf, 1e-8)
+            return self.adv_buf
+        return R.normalize_advantages(adv)
+
+    def _ev(self, target, pred, slot):
+        if _native.use_native(target):
+            _native.require().ev(target.contiguous(), pred.contiguous(), self.stats[slot].view(1))
+        else:
+            self.stats[slot].copy_(var_accounted_for_tensor(target, pred))
+
+    # ------------------------------------------------------------------ learning (autograd engine)
     def _loss(self, obs, actions, logp_old, adv, ret, v_old=None):
         cfg = self.cfg
         logp, ent, v = self.model.evaluate(obs, actions)
         if cfg.algo == "ppo":
             a_loss, pg, kl, entm, clipfrac = L.ppo_actor_loss(logp, logp_old, adv, ent, cfg.ppo_clip, self.ent_coef,
-                                                            self.kl_coef)
+                                                              self.kl_coef)
         else:
             a_loss, pg, kl, entm = L.actor_loss(logp, logp_old, adv, ent, self.kl_coef, self.ent_coef)
             clipfrac = torch.zeros((), device=self.device)
@@ -178,8 +194,6 @@ class ActorCriticTrainer:
         shared = "shared" in self.flat.groups
         total = a_loss + (cfg.vf_coef * c_loss if shared else c_loss)
         return total, a_loss, c_loss, kl, entm, clipfrac
-
-    _defer_allreduce = False
 
     def _apply_grads(self):
         """All-reduce (DP) + optimiser step; inside a segmented capture the pre-graph stops before both."""
@@ -193,18 +207,16 @@ class ActorCriticTrainer:
         for opt in self.opts.values():
             opt.step()
 
-    def _learn_native(self, obs, actions, logp_old, adv, ret, v_old):
-        cfg, eng = self.cfg, self.engine
-        b = eng.bufs(obs.shape[0], with_grad=True)
-        self.flat.zero_grad()
-        eng.forward(obs, b)
-        ppo = cfg.algo == "ppo"
-        vf = cfg.vf_coef if "shared" in self.flat.groups else 1.0
-        stats = eng.loss(b, actions, logp_old, adv, ret, v_old if ppo else None, self.ent_coef, self.kl_coef, vf,
-                         cfg.ppo_clip if ppo else 0.0, cfg.ppo_value_clip if ppo else 0.0)
-        eng.backward(b)
-        self._apply_grads()
-        return stats
+    def _minibatches(self, B):
+        """PPO minibatch index sets: a counter-hash permutation per epoch (device-side, graph-capturable)."""
+        cfg = self.cfg
+        mb = B // cfg.ppo_minibatches
+        idx = torch.arange(B, device=self.device, dtype=torch.int64)
+        for ep in range(cfg.ppo_epochs):
+            h = E.rng.hash_u32(self.policy_seed, idx, self.update_counter * 64 + ep, 7)
+            perm = torch.argsort(h)
+            for k in range(cfg.ppo_minibatches):
+                yield perm[k * mb:(k + 1) * mb]
 
     def learn(self, ret, adv):
         if self.engine is not None:
@@ -212,26 +224,16 @@ class ActorCriticTrainer:
         cfg, st = self.cfg, self.storage
         obs, actions, logp_old = st.flat("obs"), st.flat("actions"), st.flat("logp")
         v_old = st.flat("values")
-        self.stats["ev_before"].copy_(var_accounted_for_tensor(ret, v_old))
+        self._ev(ret, v_old, "ev_before")
         if cfg.norm_adv:
-            if self.dp is not None:
-                adv = self.dp.normalize_advantages(adv)
-            else:
-                adv = R.normalize_advantages(adv)
+            adv = self._normalize(adv)
         if cfg.algo == "ppo":
-            B = obs.shape[0]
-            mb = B // cfg.ppo_minibatches
-            idx = torch.arange(B, device=self.device, dtype=torch.int64)
-            for ep in range(cfg.ppo_epochs):
-                h = E.rng.hash_u32(self.policy_seed, idx, self.update_counter * 64 + ep, 7)
-                perm = torch.argsort(h)
-                for k in range(cfg.ppo_minibatches):
-                    sel = perm[k * mb:(k + 1) * mb]
-                    self.flat.zero_grad()
-                    total, a_loss, c_loss, kl, ent, cf = self._loss(obs[sel], actions[sel], logp_old[sel], adv[sel],
-                                                                    ret[sel], v_old[sel])
-                    total.backward()
-                    self._apply_grads()
+            for sel in self._minibatches(obs.shape[0]):
+                self.flat.zero_grad()
+                total, a_loss, c_loss, kl, ent, cf = self._loss(obs[sel], actions[sel], logp_old[sel], adv[sel],
+                                                                ret[sel], v_old[sel])
+                total.backward()
+                self._apply_grads()
         else:
             self.flat.zero_grad()
             total, a_loss, c_loss, kl, ent, cf = self._loss(obs, actions, logp_old, adv, ret)
@@ -241,20 +243,47 @@ class ActorCriticTrainer:
         self.stats["crit_loss"].copy_(c_loss.detach())
         self.stats["entropy"].copy_(ent.detach())
         self.stats["clipfrac"].copy_(cf.detach())
+        self.stats["kl"].copy_(kl.detach())
         self.update_counter += 1
         if self.lr_ctrl is not None or cfg.kl_coef > 0:
             self._post_update_kl(obs, actions, logp_old, ret)
-        else:
-            self.stats["kl"].copy_(kl.detach())
+
+    @torch.no_grad()
+    def _post_update_kl(self, obs, actions, logp_old, ret):
+        """KL proxy and EV on the *updated* parameters (``Basic_AC/run_AC.py:257-258``), then the lr rule."""
+        logp, _, v = self.model.evaluate(obs, actions)
+        self._kl_and_lr(logp_old, logp, ret, v)
+
+    def _kl_and_lr(self, logp_old, logp, ret, v):
+        kl = ((logp_old - logp) ** 2).mean()
+        if self.dp is not None:
+            kl = self.dp.mean_scalar(kl)
+        self.stats["kl"].copy_(kl)
+        self._ev(ret, v, "ev_after")
+        if self.lr_ctrl is not None:
+            self.lr_ctrl.update_(self.actor_opt.lr, kl)
+
+    # ------------------------------------------------------------------ learning (native engine)
+    def _learn_native(self, obs, actions, logp_old, adv, ret, v_old):
+        cfg, eng = self.cfg, self.engine
+        b = eng.bufs(obs.shape[0], with_grad=True)
+        eng.forward(obs, b)
+        ppo = cfg.algo == "ppo"
+        vf = cfg.vf_coef if "shared" in self.flat.groups else 1.0
+        # the loss kernel writes its statistics straight into stats_buf[0:7]
+        eng.loss(b, actions, logp_old, adv, ret, v_old if ppo else None, self.ent_coef, self.kl_coef, vf,
+                 cfg.ppo_clip if ppo else 0.0, cfg.ppo_value_clip if ppo else 0.0, stats=self.stats_buf)
+        eng.backward(b)   # gradient slab is clean: the optimiser zeroed it after its last use
+        self._apply_grads()
 
     @torch.no_grad()
     def _learn_native_update(self, ret, adv):
         cfg, st = self.cfg, self.storage
         obs, actions, logp_old = st.flat("obs"), st.flat("actions"), st.flat("logp")
         v_old = st.flat("values")
-        self.stats["ev_before"].copy_(var_accounted_for_tensor(ret, v_old))
+        self._ev(ret, v_old, "ev_before")
         if cfg.norm_adv:
-            adv = self.dp.normalize_advantages(adv) if self.dp is not None else R.normalize_advantages(adv)
+            adv = self._normalize(adv)
         if cfg.algo == "ppo":
             B = obs.shape[0]
             mb = B // cfg.ppo_minibatches
@@ -265,80 +294,40 @@ class ActorCriticTrainer:
                                 logp=torch.empty(mb, device=dev), adv=torch.empty(mb, device=dev),
                                 ret=torch.empty(mb, device=dev), v=torch.empty(mb, device=dev))
             m = self._mb
-            idx = torch.arange(B, device=self.device, dtype=torch.int64)
-            for ep in range(cfg.ppo_epochs):
-                h = E.rng.hash_u32(self.policy_seed, idx, self.update_counter * 64 + ep, 7)
-                perm = torch.argsort(h)
-                for k in range(cfg.ppo_minibatches):
-                    sel = perm[k * mb:(k + 1) * mb]
-                    torch.index_select(obs, 0, sel, out=m["obs"])
-                    torch.index_select(actions, 0, sel, out=m["act"])
-                    torch.index_select(logp_old, 0, sel, out=m["logp"])
-                    torch.index_select(adv, 0, sel, out=m["adv"])
-                    torch.index_select(ret, 0, sel, out=m["ret"])
-                    torch.index_select(v_old, 0, sel, out=m["v"])
-                    stats = self._learn_native(m["obs"], m["act"], m["logp"], m["adv"], m["ret"], m["v"])
+            for sel in self._minibatches(B):
+                torch.index_select(obs, 0, sel, out=m["obs"])
+                torch.index_select(actions, 0, sel, out=m["act"])
+                torch.index_select(logp_old, 0, sel, out=m["logp"])
+                torch.index_select(adv, 0, sel, out=m["adv"])
+                torch.index_select(ret, 0, sel, out=m["ret"])
+                torch.index_select(v_old, 0, sel, out=m["v"])
+                self._learn_native(m["obs"], m["act"], m["logp"], m["adv"], m["ret"], m["v"])
         else:
-            stats = self._learn_native(obs, actions, logp_old, adv.contiguous(), ret.contiguous(), v_old)
-        self._last = (stats, obs, actions, logp_old, ret)
+            self._learn_native(obs, actions, logp_old, adv.contiguous(), ret.contiguous(), v_old)
+        self._last = (obs, actions, logp_old, ret)
         if not self._defer_allreduce:
             self._finish_learn()
 
     def _finish_learn(self):
-        """Statistics + post-update KL / EV / adaptive lr (after the optimiser step)."""
+        """Post-update KL / EV / adaptive lr (after the optimiser step)."""
         if self.engine is None:
             return
-        stats, obs, actions, logp_old, ret = self._last
-        cfg = self.cfg
-        self.stats["act_loss"].copy_(stats[5])
-        self.stats["crit_loss"].copy_(stats[3])
-        self.stats["entropy"].copy_(stats[2])
-        self.stats["clipfrac"].copy_(stats[4])
-        self.stats["kl"].copy_(stats[1])
         self.update_counter += 1
-        if self.lr_ctrl is not None or cfg.kl_coef > 0:
-            self._post_update_kl_native(obs, actions, logp_old, ret)
-
-    @torch.no_grad()
-    def _post_update_kl_native(self, obs, actions, logp_old, ret):
-        eng = self.engine
-        b = eng.bufs(obs.shape[0], with_grad=True)
-        z = eng.forward(obs, b)
-        logp, _ = D.categorical_logp_entropy(z[:, :eng.A], actions)
-        kl = ((logp_old - logp) ** 2).mean()
-        if self.dp is not None:
-            kl = self.dp.mean_scalar(kl)
-        self.stats["kl"].copy_(kl)
-        self.stats["ev_after"].copy_(var_accounted_for_tensor(ret, z[:, eng.A]))
-        if self.lr_ctrl is not None:
-            self.lr_ctrl.update_(self.actor_opt.lr, kl)
-
-    @torch.no_grad()
-    def _post_update_kl(self, obs, actions, logp_old, ret):
-        """KL proxy and EV on the *updated* parameters (``Basic_AC/run_AC.py:257-258``), then the lr rule."""
-        logp, _, v = self.model.evaluate(obs, actions)
-        kl = ((logp_old - logp) ** 2).mean()
-        if self.dp is not None:
-            kl = self.dp.mean_scalar(kl)
-        self.stats["kl"].copy_(kl)
-        self.stats["ev_after"].copy_(var_accounted_for_tensor(ret, v))
-        if self.lr_ctrl is not None:
-            self.lr_ctrl.update_(self.actor_opt.lr, kl)
-
-    def update_body(self):
-        self.collect()
-        ret, adv = self.compute_returns()
-        self.learn(ret, adv)
-        self.storage.roll_over()
+        if self.lr_ctrl is not None or self.cfg.kl_coef > 0:
+            obs, actions, logp_old, ret = self._last
+            eng = self.engine
+            b = eng.bufs(obs.shape[0], with_grad=True)
+            z = eng.forward(obs, b)
+            logp, _ = D.categorical_logp_entropy(z[:, :eng.A], actions)
+            self._kl_and_lr(logp_old, logp, ret, z[:, eng.A])
 
     # ------------------------------------------------------------------ driver
     # An update is split in two segments around the gradient all-reduce:
     #   pre  = rollout + returns + forward + loss + backward   (everything up to the gradient slab)
     #   post = optimiser step(s) + statistics
-    # Without DP and for single-minibatch algorithms both segments run back to back and the whole update is ONE
-    # captured hipGraph. With DP each segment is its own graph and the RCCL all-reduce of the flat gradient slab
-    # is issued eagerly between the two replays (one collective per update). PPO (many optimiser steps per
-    # update) is captured whole only without DP.
+    # Without DP the whole update is ONE captured hipGraph. With DP (single optimiser step per update) each
+    # segment is its own graph and the RCCL all-reduce of the flat gradient slab is issued between the two replays
+    # (one collective per update). PPO with DP runs eagerly (many optimiser steps per update).
 
     def _can_capture(self):
         return self.cfg.cuda_graph and self.device.type == "cuda"
@@ -353,13 +342,13 @@ class ActorCriticTrainer:
         self.storage.roll_over()
 
     def capture(self, warmup=2):
-        """Capture the update as hipGraph(s) (see above)."""
-        if self.dp is not None and not self._segmented():
+        """Capture the update as hipGraph(s) (see above). Warm-up updates run first (GEMM autotuning, allocator)."""
+        if not self._can_capture() or (self.dp is not None and not self._segmented()):
             return None
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
-            for _ in range(warmup):
+            for _ in range(max(1, warmup)):
                 self.update_body()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
@@ -368,10 +357,14 @@ class ActorCriticTrainer:
             try:
                 g1 = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g1):
-                    self._pre_segment()
+                    self.collect()
+                    ret, adv = self.compute_returns()
+                    self.learn(ret, adv)
                 g2 = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g2):
-                    self._post_segment()
+                    self._run_optimizers()
+                    self._finish_learn()
+                    self.storage.roll_over()
             finally:
                 self._defer_allreduce = False
             self.graph = (g1, g2)
@@ -381,16 +374,6 @@ class ActorCriticTrainer:
                 self.update_body()
             self.graph = (g,)
         return self.graph
-
-    def _pre_segment(self):
-        self.collect()
-        ret, adv = self.compute_returns()
-        self.learn(ret, adv)
-
-    def _post_segment(self):
-        self._run_optimizers()
-        self._finish_learn()
-        self.storage.roll_over()
 
     def step(self):
         """One update (graph replay when captured)."""
@@ -414,12 +397,14 @@ class ActorCriticTrainer:
 
     def log(self, i, print_tog):
         if self.logger is None:
-            return
-        s = {k: float(v) for k, v in self.stats.items()}
+            return None
+        vals = self.stats_buf.detach().cpu().tolist()
+        s = {k: vals[STAT_KEYS.index(k)] for k in LOG_KEYS}
         avg_rew, n_ep, ep_len = self.env.drain_episode_stats()
         self.logger(i, act_loss=s["act_loss"], circ_loss=math.sqrt(max(s["crit_loss"], 0.0)), kl_dist=s["kl"],
                     avg_rew=avg_rew, print_tog=print_tog, act_lr=self.actor_opt.get_lr(), avg_ent=s["entropy"],
                     worker_id=self.rank, ev_before=s["ev_before"], ev_after=s["ev_after"])
+        s.update(avg_rew=avg_rew, episodes=n_ep, ep_len=ep_len)
         return s
 
     def train(self, num_updates=None, callback=None):
@@ -429,17 +414,16 @@ class ActorCriticTrainer:
             self.capture()
         t0 = time.time()
         history = []
-        for i in range(n):
+        for _ in range(n):
             self.step()
             it = self.iteration - 1
             if cfg.stdout_freq and it % cfg.stdout_freq == 0:
                 s = self.log(it, print_tog=not cfg.quiet)
                 if s is not None:
                     history.append(dict(iteration=it, **s))
-                    if self.logger is not None:
-                        el = time.time() - t0
-                        self.logger.log_metrics(iteration=it, env_steps=self.env_steps,
-                                                env_steps_per_sec=self.env_steps / max(el, 1e-9), **s)
+                    el = time.time() - t0
+                    self.logger.log_metrics(iteration=it, env_steps=self.env_steps,
+                                            env_steps_per_sec=self.env_steps / max(el, 1e-9), **s)
             if self.logger is not None and cfg.flush_every and it % cfg.flush_every == cfg.flush_every // 2:
                 self.logger.flush()
             if cfg.save_every and it % cfg.save_every == 0 and self.rank == 0 and cfg.checkpoint_dir:

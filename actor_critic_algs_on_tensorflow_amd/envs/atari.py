@@ -130,10 +130,10 @@ class PongVecEnv(VecEnv):
         img = torch.where(ball, torch.full_like(img, BALL_C), img)
         return img
 
-    def _native_step(self, actions, prev, out):
+    def _native_step(self, actions, prev, out, rew, done, trunc):
         _native.require().env_step_pong(
             self.state, self.t, self.tg, self.ep_ret, self.ep_stats, self.env_ids, actions.to(torch.int32),
-            prev, out, self.reward, self.done, self.truncated, self.seed, self.max_episode_steps, self.frame_stack)
+            prev, out, rew, done, trunc, self.seed, self.max_episode_steps, self.frame_stack)
 
 
 class BreakoutShapeVecEnv(PongVecEnv):

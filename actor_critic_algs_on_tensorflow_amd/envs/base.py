@@ -122,24 +122,30 @@ class VecEnv:
             new = torch.cat([prev[:, d:], frame.to(out.dtype)], dim=1)
         out.copy_(new)
 
-    def step(self, actions, prev_obs=None, obs_out=None):
+    def step(self, actions, prev_obs=None, obs_out=None, reward_out=None, done_out=None, trunc_out=None):
         """One env step for the whole bank.
 
         ``prev_obs`` / ``obs_out`` let a rollout read the stack from slot ``t`` and write slot ``t+1`` of its
-        buffer directly (static addresses => hipGraph-capturable). Defaults: the bank's own ``obs`` buffer.
+        buffer directly, and ``reward_out`` / ``done_out`` / ``trunc_out`` receive the transition's reward, done and
+        truncation flags (static addresses => hipGraph-capturable; on GPU the env kernel writes them in place, no
+        copies). Defaults: the bank's own buffers.
         """
         prev = self.obs if prev_obs is None else prev_obs
         out = self.obs if obs_out is None else obs_out
+        rew = self.reward if reward_out is None else reward_out
+        done = self.done if done_out is None else done_out
+        trunc = self.truncated if trunc_out is None else trunc_out
         if prev.data_ptr() == out.data_ptr():
             prev = prev.clone()   # the kernels read the old stack while writing the new one
         if _native.use_native(self.state):
-            self._native_step(actions, prev, out)
+            self._native_step(actions, prev, out, rew, done, trunc)
         else:
             self._torch_step(actions, prev, out)
-        if obs_out is not None and obs_out.data_ptr() != self.obs.data_ptr():
-            self._last_out = out
-        info = {"truncated": self.truncated, "ep_stats": self.ep_stats}
-        return out, self.reward, self.done, info
+            for src, dst in ((self.reward, rew), (self.done, done), (self.truncated, trunc)):
+                if dst.data_ptr() != src.data_ptr():
+                    dst.copy_(src)
+        info = {"truncated": trunc, "ep_stats": self.ep_stats}
+        return out, rew, done, info
 
     @torch.no_grad()
     def _torch_step(self, actions, prev, out):
@@ -164,7 +170,7 @@ class VecEnv:
         self._stack_push(f, prev, out)
         self._stack_reset(f, out, done)
 
-    def _native_step(self, actions, prev, out):
+    def _native_step(self, actions, prev, out, rew, done, trunc):
         raise NotImplementedError(f"{type(self).__name__} has no native kernel")
 
     def drain_episode_stats(self):

@@ -66,8 +66,8 @@ class MujocoShapeVecEnv(VecEnv):
     def _frame(self):
         return self.state.clone()
 
-    def _native_step(self, actions, prev, out):
+    def _native_step(self, actions, prev, out, rew, done, trunc):
         _native.require().env_step_linear(
             self.state, self.t, self.tg, self.ep_ret, self.ep_stats, self.env_ids,
             actions.reshape(self.num_envs, ACT_DIM).float().contiguous(), self.A, self.B,
-            prev, out, self.reward, self.done, self.truncated, self.seed, self.max_episode_steps, self.frame_stack)
+            prev, out, rew, done, trunc, self.seed, self.max_episode_steps, self.frame_stack)

@@ -9,6 +9,8 @@ Each function has a PyTorch reference (``*_ref``) that the GPU tests compare aga
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .. import _native
@@ -68,11 +70,77 @@ class GemmWorkspace:
             self.tickets = torch.zeros(tiles, dtype=torch.int32, device=self.ws.device)
 
 
+# ------------------------------------------------------------------------------------------------ autotuning
+# The engine issues ~20 distinct GEMM shapes, all small and latency-bound (32..64k rows); the fastest (tile,
+# split-K) pair depends on how many workgroups a shape yields against 256 CUs and how many k-tiles each serial
+# chain has to walk. Each new shape is timed once on its first (eager, never captured) call against scratch
+# outputs and the winner is cached for the process. ACAMD_GEMM_TUNE=0 falls back to the static :func:`plan`.
+_TUNED: dict = {}
+TUNE = os.environ.get("ACAMD_GEMM_TUNE", "1") == "1"
+
+
+def tuned_plans():
+    return dict(_TUNED)
+
+
+def _candidates(M, N, K, atomic):
+    kt = _cdiv(K, BK)
+    for tile, (bm, bn) in TILES.items():
+        if bm >= 2 * max(32, M) or bn >= 2 * max(32, N):
+            continue  # a tile at least twice the problem in one dimension only wastes MFMA issue
+        for s in (1, 2, 4, 8, 16, 32, 64):
+            if s > 1 and kt < 2 * s:
+                break
+            if not atomic and s > 16:
+                break
+            yield tile, s
+
+
+def _tune(key, A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha, bias, relu, mask, ldm, colsum,
+          workspace, colsum_mod):
+    ops = _native.require()
+    dev = C.device
+    need = (M - 1) * ldc + N
+    Cs = torch.zeros(need, dtype=C.dtype, device=dev)
+    cs = torch.zeros(max(N, colsum_mod or 0), dtype=torch.float32, device=dev) if colsum is not None else None
+    ws = workspace if workspace is not None else GemmWorkspace(dev)
+    best = None
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for tile, s in _candidates(M, N, K, out_mode == 2):
+        eff = ops.gemm_effective_splits(K, s)
+        wsp = tk = None
+        if eff > 1 and out_mode != 2:
+            e, t = workspace_elems(M, N, tile, eff)
+            ws.ensure(e, t)
+            wsp, tk = ws.ws, ws.tickets
+        args = (A, lda, a_k, B, ldb, b_k, Cs, ldc, out_mode, M, N, K, float(alpha), bias, bool(relu), mask, ldm, cs,
+                tile, s, wsp, tk, int(colsum_mod))
+        ops.gemm(*args)
+        ev0.record()
+        for _ in range(4):
+            ops.gemm(*args)
+        ev1.record()
+        ev1.synchronize()
+        ms = ev0.elapsed_time(ev1) / 4
+        if best is None or ms < best[0]:
+            best = (ms, tile, s)
+    _TUNED[key] = (best[1], best[2], best[0])
+    return best[1], best[2]
+
+
 def gemm(A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha=1.0, bias=None, relu=False, mask=None, ldm=0,
          colsum=None, tile=None, splits=None, workspace: GemmWorkspace | None = None, colsum_mod=0):
     """Native GEMM; ``out_mode``: 0 fp32 store, 1 bf16 store, 2 fp32 atomic add (C pre-zeroed)."""
     if tile is None or splits is None:
-        t, s = plan(M, N, K, atomic=(out_mode == 2))
+        key = (M, N, K, bool(a_k), bool(b_k), out_mode, lda % 8 == 0, ldb % 8 == 0)
+        hit = _TUNED.get(key)
+        if hit is not None:
+            t, s = hit[0], hit[1]
+        elif TUNE and C.is_cuda and not torch.cuda.is_current_stream_capturing():
+            t, s = _tune(key, A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha, bias, relu, mask, ldm,
+                         colsum, workspace, colsum_mod)
+        else:
+            t, s = plan(M, N, K, atomic=(out_mode == 2))
         tile = t if tile is None else tile
         splits = s if splits is None else splits
     ops = _native.require()

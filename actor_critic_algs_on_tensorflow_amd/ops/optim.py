@@ -84,6 +84,8 @@ class FusedAdam:
         # sumsq partials + last-arriver tickets (self-cleaning, zero-initialised once)
         self._partial = torch.zeros(1024, dtype=torch.float32, device=dev)
         self._ticket = torch.zeros(2, dtype=torch.int32, device=dev)
+        # native engine: the update kernel zeroes each gradient after reading it (saves a memset per step)
+        self.zero_grad_after = False
 
     def set_lr(self, lr):
         self.lr.fill_(float(lr))
@@ -113,7 +115,8 @@ class FusedAdam:
         ops.adam_step(self.p, self.g, self.m, self.v, self.lr, self.t, self.gnorm, self.shadow,
                       float(self.b1), float(self.b2), float(self.eps),
                       float(self.clip_value) if self.clip_value is not None else -1.0,
-                      float(self.max_grad_norm) if self.max_grad_norm is not None else -1.0, self._ticket[1:])
+                      float(self.max_grad_norm) if self.max_grad_norm is not None else -1.0, self._ticket[1:],
+                      bool(self.zero_grad_after))
 
     def _torch_step(self):
         g = self.g
@@ -157,7 +160,8 @@ class FusedRMSprop(FusedAdam):
         ops.rmsprop_step(self.p, self.g, self.v, self.lr, self.gnorm, self.shadow,
                          float(self.alpha), float(self.eps),
                          float(self.clip_value) if self.clip_value is not None else -1.0,
-                         float(self.max_grad_norm) if self.max_grad_norm is not None else -1.0)
+                         float(self.max_grad_norm) if self.max_grad_norm is not None else -1.0,
+                         bool(self.zero_grad_after))
 
     def _torch_step(self):
         g = self.g

@@ -25,8 +25,9 @@ hipError_t aca_env_step_linear(float*, int32_t*, int64_t*, float*, float*, const
 hipError_t aca_env_step_pong(float*, int32_t*, int64_t*, float*, float*, const int64_t*, const int32_t*,
                              const uint8_t*, uint8_t*, float*, uint8_t*, uint8_t*, uint32_t, int, int, int,
                              hipStream_t);
-hipError_t aca_categorical_sample(const float*, int, int, int, const int64_t*, uint32_t, int32_t*, float*, float*,
-                                  hipStream_t);
+hipError_t aca_categorical_sample(const float*, int, int, int, const int64_t*, const int64_t*, const int64_t*, int,
+                                  uint32_t, int32_t*, float*, float*, float*, hipStream_t);
+hipError_t aca_ev(const float*, const float*, float*, int, hipStream_t);
 hipError_t aca_gaussian_sample(const float*, int, int, int, const float*, const int64_t*, uint32_t, float*, float*,
                                float*, hipStream_t);
 hipError_t aca_gae(const float*, const float*, const uint8_t*, float*, float*, int, int, float, float, hipStream_t);
@@ -34,10 +35,10 @@ hipError_t aca_nstep(const float*, const float*, const uint8_t*, float*, float*,
 hipError_t aca_normalize(const float*, float*, int, float, hipStream_t);
 hipError_t aca_moments(const float*, const float*, float*, int, hipStream_t);
 hipError_t aca_sumsq(const float*, size_t, float*, int, unsigned int*, float*, hipStream_t);
-hipError_t aca_adam_step(float*, const float*, float*, float*, size_t, const float*, float*, const float*, uint16_t*,
-                         float, float, float, float, float, unsigned int*, hipStream_t);
-hipError_t aca_rmsprop_step(float*, const float*, float*, size_t, const float*, const float*, uint16_t*, float, float,
-                            float, float, hipStream_t);
+hipError_t aca_adam_step(float*, float*, float*, float*, size_t, const float*, float*, const float*, uint16_t*,
+                         float, float, float, float, float, unsigned int*, int, hipStream_t);
+hipError_t aca_rmsprop_step(float*, float*, float*, size_t, const float*, const float*, uint16_t*, float, float,
+                            float, float, int, hipStream_t);
 hipError_t aca_cast_bf16(const float*, uint16_t*, size_t, hipStream_t);
 hipError_t aca_gemm(const void*, int64_t, bool, const void*, int64_t, bool, void*, int64_t, int, int, int, int, float,
                     const float*, int, const void*, int64_t, float*, int, int, float*, unsigned int*, int, hipStream_t);
@@ -172,9 +173,36 @@ void categorical_sample(Tensor logits, Tensor keys, int64_t seed, Tensor act, Te
   const int B = logits.size(0), A = logits.size(1);
   TORCH_CHECK(A <= 64, "categorical_sample: at most 64 actions");
   TORCH_CHECK(keys.numel() >= B && act.numel() >= B && logp.numel() >= B && ent.numel() >= B, "bad sizes");
-  check(aca_categorical_sample(ptr<float>(logits), (int)logits.stride(0), B, A, ptr<int64_t>(keys), (uint32_t)seed,
-                               ptr<int32_t>(act), ptr<float>(logp), ptr<float>(ent), cur_stream(logits)),
+  check(aca_categorical_sample(ptr<float>(logits), (int)logits.stride(0), B, A, ptr<int64_t>(keys), nullptr, nullptr, 0,
+                               (uint32_t)seed, ptr<int32_t>(act), ptr<float>(logp), ptr<float>(ent), nullptr,
+                               cur_stream(logits)),
         "categorical_sample");
+}
+
+// rollout form: keys from the env bank counters, optional copy of the fused head's value column (logits[:, A])
+void categorical_sample_env(Tensor logits, Tensor tg, Tensor env_ids, int64_t key_shift, int64_t seed, Tensor act,
+                            Tensor logp, Tensor ent, c10::optional<Tensor> vout) {
+  TORCH_CHECK(logits.is_cuda() && logits.scalar_type() == at::kFloat && logits.dim() == 2 && logits.stride(1) == 1,
+              "categorical_sample_env: logits must be fp32 [B, A] with unit column stride");
+  need(tg, at::kLong, "tg");
+  need(env_ids, at::kLong, "env_ids");
+  need(act, at::kInt, "act");
+  need(logp, at::kFloat, "logp");
+  need(ent, at::kFloat, "ent");
+  const int B = logits.size(0), A = logits.size(1);
+  TORCH_CHECK(A <= 64, "categorical_sample_env: at most 64 actions");
+  TORCH_CHECK(tg.numel() >= B && env_ids.numel() >= B && act.numel() >= B && logp.numel() >= B && ent.numel() >= B,
+              "bad sizes");
+  float* vo = nullptr;
+  if (vout.has_value() && vout->defined()) {
+    need(*vout, at::kFloat, "vout");
+    TORCH_CHECK(vout->numel() >= B && logits.stride(0) > A, "vout needs a value column after the logits");
+    vo = ptr<float>(*vout);
+  }
+  check(aca_categorical_sample(ptr<float>(logits), (int)logits.stride(0), B, A, nullptr, ptr<int64_t>(tg),
+                               ptr<int64_t>(env_ids), (int)key_shift, (uint32_t)seed, ptr<int32_t>(act),
+                               ptr<float>(logp), ptr<float>(ent), vo, cur_stream(logits)),
+        "categorical_sample_env");
 }
 
 void gaussian_sample(Tensor mu, Tensor log_std, Tensor keys, int64_t seed, Tensor act, Tensor logp, Tensor ent) {
@@ -225,6 +253,14 @@ void normalize(Tensor a, Tensor out, double eps) {
   check(aca_normalize(ptr<float>(a), ptr<float>(out), a.numel(), (float)eps, cur_stream(a)), "normalize");
 }
 
+void ev(Tensor x, Tensor y, Tensor out) {
+  need(x, at::kFloat, "x");
+  need(y, at::kFloat, "y");
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.numel() >= 1, "ev: out must be fp32");
+  TORCH_CHECK(x.numel() == y.numel(), "ev: size mismatch");
+  check(aca_ev(ptr<float>(x), ptr<float>(y), ptr<float>(out), x.numel(), cur_stream(x)), "ev");
+}
+
 void moments(Tensor x, Tensor y, Tensor out) {
   need(x, at::kFloat, "x");
   need(y, at::kFloat, "y");
@@ -246,7 +282,7 @@ void sumsq(Tensor x, Tensor partial, Tensor ticket, Tensor out) {
 
 void adam_step(Tensor p, Tensor g, Tensor m, Tensor v, Tensor lr, Tensor t, c10::optional<Tensor> gnorm_sq,
                c10::optional<Tensor> shadow, double b1, double b2, double eps, double clip, double max_norm,
-               Tensor ticket) {
+               Tensor ticket, bool zero_grad) {
   need(p, at::kFloat, "p");
   need(g, at::kFloat, "g");
   need(m, at::kFloat, "m");
@@ -264,12 +300,13 @@ void adam_step(Tensor p, Tensor g, Tensor m, Tensor v, Tensor lr, Tensor t, c10:
   }
   check(aca_adam_step(ptr<float>(p), ptr<float>(g), ptr<float>(m), ptr<float>(v), p.numel(), ptr<float>(lr),
                       ptr<float>(t), optr<float>(gnorm_sq), sh, (float)b1, (float)b2, (float)eps, (float)clip,
-                      (float)max_norm, ptr<unsigned int>(ticket), cur_stream(p)),
+                      (float)max_norm, ptr<unsigned int>(ticket), zero_grad ? 1 : 0, cur_stream(p)),
         "adam_step");
 }
 
 void rmsprop_step(Tensor p, Tensor g, Tensor v, Tensor lr, c10::optional<Tensor> gnorm_sq,
-                  c10::optional<Tensor> shadow, double alpha, double eps, double clip, double max_norm) {
+                  c10::optional<Tensor> shadow, double alpha, double eps, double clip, double max_norm,
+                  bool zero_grad) {
   need(p, at::kFloat, "p");
   need(g, at::kFloat, "g");
   need(v, at::kFloat, "v");
@@ -284,7 +321,7 @@ void rmsprop_step(Tensor p, Tensor g, Tensor v, Tensor lr, c10::optional<Tensor>
   }
   check(aca_rmsprop_step(ptr<float>(p), ptr<float>(g), ptr<float>(v), p.numel(), ptr<float>(lr),
                          optr<float>(gnorm_sq), sh, (float)alpha, (float)eps, (float)clip, (float)max_norm,
-                         cur_stream(p)),
+                         zero_grad ? 1 : 0, cur_stream(p)),
         "rmsprop_step");
 }
 
@@ -446,6 +483,9 @@ TORCH_LIBRARY(acamd, m) {
         "Tensor actions, Tensor prev, Tensor out, Tensor reward, Tensor done, Tensor truncated, int seed, "
         "int max_steps, int k) -> ()");
   m.def("categorical_sample(Tensor logits, Tensor keys, int seed, Tensor act, Tensor logp, Tensor ent) -> ()");
+  m.def("categorical_sample_env(Tensor logits, Tensor tg, Tensor env_ids, int key_shift, int seed, Tensor act, "
+        "Tensor logp, Tensor ent, Tensor? vout) -> ()");
+  m.def("ev(Tensor x, Tensor y, Tensor out) -> ()");
   m.def("gaussian_sample(Tensor mu, Tensor log_std, Tensor keys, int seed, Tensor act, Tensor logp, Tensor ent) -> ()");
   m.def("gae(Tensor r, Tensor v, Tensor d, Tensor ret, Tensor adv, float gamma, float lam) -> ()");
   m.def("nstep_returns(Tensor r, Tensor v, Tensor d, Tensor tgt, Tensor adv, float gamma, int L) -> ()");
@@ -453,9 +493,9 @@ TORCH_LIBRARY(acamd, m) {
   m.def("moments(Tensor x, Tensor y, Tensor out) -> ()");
   m.def("sumsq(Tensor x, Tensor partial, Tensor ticket, Tensor out) -> ()");
   m.def("adam_step(Tensor p, Tensor g, Tensor m, Tensor v, Tensor lr, Tensor t, Tensor? gnorm_sq, Tensor? shadow, "
-        "float b1, float b2, float eps, float clip, float max_norm, Tensor ticket) -> ()");
+        "float b1, float b2, float eps, float clip, float max_norm, Tensor ticket, bool zero_grad=False) -> ()");
   m.def("rmsprop_step(Tensor p, Tensor g, Tensor v, Tensor lr, Tensor? gnorm_sq, Tensor? shadow, float alpha, "
-        "float eps, float clip, float max_norm) -> ()");
+        "float eps, float clip, float max_norm, bool zero_grad=False) -> ()");
   m.def("cast_bf16(Tensor x, Tensor y) -> ()");
   m.def("gemm(Tensor A, int lda, bool a_k, Tensor B, int ldb, bool b_k, Tensor C, int ldc, int out_mode, int M, "
         "int N, int K, float alpha, Tensor? bias, bool relu, Tensor? mask, int ldm, Tensor? colsum, int tile, "
@@ -479,6 +519,8 @@ TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
   m.impl("env_step_pong", &env_step_pong);
   m.impl("categorical_sample", &categorical_sample);
   m.impl("gaussian_sample", &gaussian_sample);
+  m.impl("categorical_sample_env", &categorical_sample_env);
+  m.impl("ev", &ev);
   m.impl("gae", &gae);
   m.impl("nstep_returns", &nstep_returns);
   m.impl("normalize", &normalize);

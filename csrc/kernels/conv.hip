@@ -33,6 +33,31 @@ __global__ void im2col_u8_nchw_kernel(const uint8_t* __restrict__ x, u16* __rest
   }
 }
 
+// fast path: KW % 4 == 0, S % 4 == 0, W % 4 == 0 -> every 8-element k chunk is two aligned 4-byte loads
+__global__ void im2col_u8_nchw_vec_kernel(const uint8_t* __restrict__ x, u16* __restrict__ col, int B, int C, int H,
+                                          int W, int KH, int KW, int S, int OH, int OW, float scale) {
+  const int K = C * KH * KW, KC = K / 8;
+  const int64_t total = (int64_t)B * OH * OW * KC;
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int kc = (int)(idx % KC);
+    const int64_t m = idx / KC;
+    const int ow = (int)(m % OW), oh = (int)((m / OW) % OH), b = (int)(m / ((int64_t)OW * OH));
+    const int k0 = kc * 8;
+    const int j0 = k0 % KW, i = (k0 / KW) % KH, c = k0 / (KW * KH);
+    const uint8_t* src = x + (((int64_t)b * C + c) * H + oh * S + i) * W + ow * S + j0;
+    const uint32_t w0 = *reinterpret_cast<const uint32_t*>(src);
+    const uint32_t w1 = *reinterpret_cast<const uint32_t*>(src + 4);
+    union { uint4 v; u16 h[8]; } o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      o.h[e] = f2bf((float)((w0 >> (8 * e)) & 0xFF) * scale);
+      o.h[4 + e] = f2bf((float)((w1 >> (8 * e)) & 0xFF) * scale);
+    }
+    reinterpret_cast<uint4*>(col)[idx] = o.v;
+  }
+}
+
 __global__ void im2col_nhwc_kernel(const u16* __restrict__ x, u16* __restrict__ col, int B, int C, int H, int W,
                                    int KH, int KW, int S, int OH, int OW) {
   const int CC = C / 8, KC = KH * KW * CC;
@@ -123,7 +148,10 @@ extern "C" hipError_t aca_im2col_u8_nchw(const uint8_t* x, uint16_t* col, int B,
   const int OH = (H - KH) / S + 1, OW = (W - KW) / S + 1;
   if ((C * KH * KW) % 8) return hipErrorInvalidValue;
   const int64_t total = (int64_t)B * OH * OW * (C * KH * KW / 8);
-  im2col_u8_nchw_kernel<<<grid_for(total, 256), 256, 0, stream>>>(x, col, B, C, H, W, KH, KW, S, OH, OW, scale);
+  if (KW % 8 == 0 && S % 4 == 0 && W % 4 == 0)
+    im2col_u8_nchw_vec_kernel<<<grid_for(total, 256), 256, 0, stream>>>(x, col, B, C, H, W, KH, KW, S, OH, OW, scale);
+  else
+    im2col_u8_nchw_kernel<<<grid_for(total, 256), 256, 0, stream>>>(x, col, B, C, H, W, KH, KW, S, OH, OW, scale);
   return hipGetLastError();
 }
 

@@ -9,10 +9,16 @@
 
 namespace aca {
 
+// keys: explicit per-row keys, or (keys == nullptr) key = tg[row] << key_shift | env_ids[row] computed here (the
+// env bank's global step counter and env id -- saves the host-side key arithmetic launches per rollout step).
+// vout (optional): vout[row] = logits[row * ldl + A], i.e. copies the value column of a fused [logits | value] head.
 __global__ void __launch_bounds__(256) categorical_sample_kernel(const float* __restrict__ logits, int ldl, int B,
                                                                  int A, const int64_t* __restrict__ keys,
+                                                                 const int64_t* __restrict__ tg,
+                                                                 const int64_t* __restrict__ env_ids, int key_shift,
                                                                  uint32_t seed, int32_t* __restrict__ act,
-                                                                 float* __restrict__ logp, float* __restrict__ ent) {
+                                                                 float* __restrict__ logp, float* __restrict__ ent,
+                                                                 float* __restrict__ vout) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (row >= B) return;
@@ -28,7 +34,8 @@ __global__ void __launch_bounds__(256) categorical_sample_kernel(const float* __
   // Gumbel-max
   float g = -INFINITY;
   if (on) {
-    const float u = uniform_open(seed, keys[row], (uint32_t)lane);
+    const int64_t key = keys ? keys[row] : (tg[row] * ((int64_t)1 << key_shift) + env_ids[row]);
+    const float u = uniform_open(seed, key, (uint32_t)lane);
     g = z + (-logf(-logf(u)));
   }
   // argmax with first-index tie breaking
@@ -45,6 +52,7 @@ __global__ void __launch_bounds__(256) categorical_sample_kernel(const float* __
     act[row] = bi;
     logp[row] = lpa;
     ent[row] = H;
+    if (vout) vout[row] = logits[(size_t)row * ldl + A];
   }
 }
 
@@ -75,13 +83,15 @@ __global__ void gaussian_sample_kernel(const float* __restrict__ mu, int ldm, in
 }  // namespace aca
 
 extern "C" hipError_t aca_categorical_sample(const float* logits, int ldl, int B, int A, const int64_t* keys,
-                                             uint32_t seed, int32_t* act, float* logp, float* ent,
+                                             const int64_t* tg, const int64_t* ids, int key_shift, uint32_t seed,
+                                             int32_t* act, float* logp, float* ent, float* vout,
                                              hipStream_t stream) {
   if (B <= 0) return hipSuccess;
   if (A > 64) return hipErrorInvalidValue;
+  if (!keys && (!tg || !ids)) return hipErrorInvalidValue;
   const int rows_per_block = 4;
   aca::categorical_sample_kernel<<<(B + rows_per_block - 1) / rows_per_block, 256, 0, stream>>>(
-      logits, ldl, B, A, keys, seed, act, logp, ent);
+      logits, ldl, B, A, keys, tg, ids, key_shift, seed, act, logp, ent, vout);
   return hipGetLastError();
 }
 

@@ -32,11 +32,11 @@ __global__ void __launch_bounds__(OPT_THREADS) sumsq_kernel(const float* __restr
   s = block_sum(s, sh);
   if (threadIdx.x == 0) partial[blockIdx.x] = s;
   if (last_block_arrival(ticket, gridDim.x, &flag)) {
-    if (threadIdx.x == 0) {
-      float tot = 0.f;
-      for (unsigned int b = 0; b < gridDim.x; ++b) tot += partial[b];
-      *out = tot;
-    }
+    // parallel, fixed-order (deterministic for a given grid) reduction of the per-block partials
+    float t = 0.f;
+    for (unsigned int b = threadIdx.x; b < gridDim.x; b += blockDim.x) t += partial[b];
+    t = block_sum(t, sh);
+    if (threadIdx.x == 0) *out = t;
   }
 }
 
@@ -47,12 +47,12 @@ __device__ __forceinline__ float grad_scale(const float* gnorm_sq, float max_nor
 }
 
 template <bool ADAM>
-__global__ void __launch_bounds__(OPT_THREADS) opt_kernel(float* __restrict__ p, const float* __restrict__ g,
+__global__ void __launch_bounds__(OPT_THREADS) opt_kernel(float* __restrict__ p, float* __restrict__ g,
                                                           float* __restrict__ m, float* __restrict__ v, size_t n,
                                                           const float* __restrict__ lr_ptr, float* __restrict__ t_ptr,
                                                           const float* __restrict__ gnorm_sq, u16* __restrict__ shadow,
                                                           float b1, float b2, float eps, float clip, float max_norm,
-                                                          unsigned int* __restrict__ ticket) {
+                                                          unsigned int* __restrict__ ticket, int zero_grad) {
   __shared__ int flag;
   const float lr = *lr_ptr;
   const float t = ADAM ? (*t_ptr + 1.0f) : 0.f;
@@ -62,6 +62,7 @@ __global__ void __launch_bounds__(OPT_THREADS) opt_kernel(float* __restrict__ p,
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += stride) {
     float gi = g[i];
+    if (zero_grad) g[i] = 0.f;  // the next learner step accumulates into a clean slab without a memset
     if (clip > 0.f) gi = fminf(fmaxf(gi, -clip), clip);
     gi *= scale;
     float vi = v[i];
@@ -110,21 +111,22 @@ extern "C" hipError_t aca_sumsq(const float* x, size_t n, float* partial, int ma
   return hipGetLastError();
 }
 
-extern "C" hipError_t aca_adam_step(float* p, const float* g, float* m, float* v, size_t n, const float* lr,
+extern "C" hipError_t aca_adam_step(float* p, float* g, float* m, float* v, size_t n, const float* lr,
                                     float* t, const float* gnorm_sq, uint16_t* shadow, float b1, float b2, float eps,
-                                    float clip, float max_norm, unsigned int* ticket, hipStream_t stream) {
+                                    float clip, float max_norm, unsigned int* ticket, int zero_grad,
+                                    hipStream_t stream) {
   if (n == 0) return hipSuccess;
   opt_kernel<true><<<opt_grid(n), OPT_THREADS, 0, stream>>>(p, g, m, v, n, lr, t, gnorm_sq, shadow, b1, b2, eps,
-                                                            clip, max_norm, ticket);
+                                                            clip, max_norm, ticket, zero_grad);
   return hipGetLastError();
 }
 
-extern "C" hipError_t aca_rmsprop_step(float* p, const float* g, float* v, size_t n, const float* lr,
+extern "C" hipError_t aca_rmsprop_step(float* p, float* g, float* v, size_t n, const float* lr,
                                        const float* gnorm_sq, uint16_t* shadow, float alpha, float eps, float clip,
-                                       float max_norm, hipStream_t stream) {
+                                       float max_norm, int zero_grad, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   opt_kernel<false><<<opt_grid(n), OPT_THREADS, 0, stream>>>(p, g, nullptr, v, n, lr, nullptr, gnorm_sq, shadow,
-                                                             0.f, alpha, eps, clip, max_norm, nullptr);
+                                                             0.f, alpha, eps, clip, max_norm, nullptr, zero_grad);
   return hipGetLastError();
 }
 

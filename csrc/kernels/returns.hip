@@ -76,7 +76,31 @@ __global__ void __launch_bounds__(1024) moments_kernel(const float* __restrict__
   if (threadIdx.x == 0) { out[0] = a; out[1] = b; out[2] = c; out[3] = dd; out[4] = e; }
 }
 
+// EV correlation of the reference (Basic_AC/util.py:4-12): mean(z(x) * z(y)), population std, written to *out.
+__global__ void __launch_bounds__(1024) ev_kernel(const float* __restrict__ x, const float* __restrict__ y,
+                                                  float* __restrict__ out, int n) {
+  __shared__ double sh[16];
+  double a = 0, b = 0, c = 0, dd = 0, e = 0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const double xi = x[i], yi = y[i];
+    a += xi; b += xi * xi; c += yi; dd += yi * yi; e += xi * yi;
+  }
+  a = block_sum_d(a, sh); b = block_sum_d(b, sh); c = block_sum_d(c, sh);
+  dd = block_sum_d(dd, sh); e = block_sum_d(e, sh);
+  if (threadIdx.x == 0) {
+    const double mx = a / n, my = c / n;
+    const double vx = b / n - mx * mx, vy = dd / n - my * my;
+    const double cov = e / n - mx * my;
+    *out = (float)(cov / sqrt(fmax(vx, 0.0) * fmax(vy, 0.0)));
+  }
+}
+
 }  // namespace aca
+
+extern "C" hipError_t aca_ev(const float* x, const float* y, float* out, int n, hipStream_t stream) {
+  aca::ev_kernel<<<1, 1024, 0, stream>>>(x, y, out, n);
+  return hipGetLastError();
+}
 
 extern "C" hipError_t aca_gae(const float* r, const float* v, const uint8_t* d, float* ret, float* adv, int T, int N,
                               float gamma, float lam, hipStream_t stream) {

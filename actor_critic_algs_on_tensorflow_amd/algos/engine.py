@@ -3,11 +3,8 @@
 Autograd is replaced by a fixed schedule of launches over preallocated buffers (static addresses => the whole
 rollout step and the whole learner step are hipGraph-capturable). Per batch of B observations:
 
-forward   im2col_u8(obs)            -> col1 [B*400, 256]   (uint8 NCHW frames, /255 folded in)
-          gemm(col1, W1^T) +b relu  -> y1   [B*400, 32]    (NHWC bf16)
-          im2col_nhwc(y1)           -> col2 [B*81, 512]
-          gemm(col2, W2^T) +b relu  -> y2   [B*81, 64]
-          im2col_nhwc(y2)           -> col3 [B*49, 576]
+forward   gemm(col1, W1^T) +b relu  -> y1   [B*400, 32]    col1 = im2col(obs uint8 NCHW)/255, k (c,i,j)
+          gemm(col2, W2^T) +b relu  -> y2   [B*81, 64]     col2 = im2col(y1 NHWC), k (i,j,c)
           gemm(col3, W3^T) +b relu  -> y3   [B*49, 64] == [B, 3136]
           gemm(y3, Wfc)    +b relu  -> h    [B, 512]       (slab split-K for small B)
           gemm(h, Wh)      +b       -> z    [B, A+1] fp32  (logits | value)
@@ -19,9 +16,12 @@ backward  dWh += h^T dz ; dbh += colsum(dz)
           dW3 += dy3^T col3 ; dcol3 = dy3 W3 ; dy2 = col2im(dcol3) * (y2 > 0) (+ colsum -> db2)
           dW2 += dy2^T col2 ; dcol2 = dy2 W2 ; dy1 = col2im(dcol2) * (y1 > 0) (+ colsum -> db1)
           dW1 += dy1^T col1
+The column matrices ``col*`` are never materialised in the default (``implicit=True``) mode: the GEMM gathers its
+k-contiguous A rows (forward) or n-contiguous B rows (weight gradient) straight from the activation image
+(implicit im2col, ``gemm_impl.h``). ``implicit=False`` runs explicit im2col kernels + plain GEMMs (A/B reference).
 Weight gradients accumulate (split-K atomics) straight into the fp32 gradient slab of :class:`FlatParams` (zeroed
-once per learner step), which is also the buffer the data-parallel engine all-reduces. Weights are read from the
-bf16 shadow of the slab that the fused optimiser rewrites every step.
+by the optimiser after use), which is also the buffer the data-parallel engine all-reduces. Weights are read from
+the bf16 shadow of the slab that the fused optimiser rewrites every step.
 """
 from __future__ import annotations
 
@@ -36,14 +36,16 @@ H0 = 84
 class _Bufs:
     """Activation / gradient buffers for one batch size."""
 
-    def __init__(self, B, A1, dev, with_grad):
+    def __init__(self, B, A1, dev, with_grad, implicit=True):
         bf = torch.bfloat16
         self.B = B
-        self.col1 = torch.empty(B * 400, 256, dtype=bf, device=dev)
+        self.obs = None
+        if not implicit:
+            self.col1 = torch.empty(B * 400, 256, dtype=bf, device=dev)
+            self.col2 = torch.empty(B * 81, 512, dtype=bf, device=dev)
+            self.col3 = torch.empty(B * 49, 576, dtype=bf, device=dev)
         self.y1 = torch.empty(B * 400, 32, dtype=bf, device=dev)
-        self.col2 = torch.empty(B * 81, 512, dtype=bf, device=dev)
         self.y2 = torch.empty(B * 81, 64, dtype=bf, device=dev)
-        self.col3 = torch.empty(B * 49, 576, dtype=bf, device=dev)
         self.y3 = torch.empty(B * 49, 64, dtype=bf, device=dev)
         self.h = torch.empty(B, 512, dtype=bf, device=dev)
         self.z = torch.empty(B, A1, dtype=torch.float32, device=dev)
@@ -61,8 +63,9 @@ class _Bufs:
 class CNNEngine:
     """Explicit forward/backward of :class:`..models.policy.CNNActorCritic` over a :class:`FlatParams` slab."""
 
-    def __init__(self, model, flat, shadow):
+    def __init__(self, model, flat, shadow, implicit=True):
         net = model.net
+        self.implicit = implicit
         self.model = model
         self.flat = flat
         self.shadow = shadow
@@ -94,7 +97,7 @@ class CNNEngine:
     def bufs(self, B, with_grad=False):
         key = (B, with_grad)
         if key not in self._bufs:
-            self._bufs[key] = _Bufs(B, self.A1, self.dev, with_grad)
+            self._bufs[key] = _Bufs(B, self.A1, self.dev, with_grad, self.implicit)
         return self._bufs[key]
 
     # ------------------------------------------------------------------------------------------------ forward
@@ -102,15 +105,24 @@ class CNNEngine:
         """obs uint8 [B, 4, 84, 84] -> b.z fp32 [B, A+1] (logits | value)."""
         B = b.B
         ws = self.ws
-        G.im2col_u8(obs, b.col1, 8, 8, 4)
-        G.gemm(b.col1, 256, True, self.sW1, 256, True, b.y1, 32, 1, B * 400, 32, 256, bias=self.b1, relu=True,
-               workspace=ws)
-        G.im2col_nhwc(b.y1, b.col2, B, 20, 20, 32, 4, 4, 2)
-        G.gemm(b.col2, 512, True, self.sW2, 512, True, b.y2, 64, 1, B * 81, 64, 512, bias=self.b2, relu=True,
-               workspace=ws)
-        G.im2col_nhwc(b.y2, b.col3, B, 9, 9, 64, 3, 3, 1)
-        G.gemm(b.col3, 576, True, self.sW3, 576, True, b.y3, 64, 1, B * 49, 64, 576, bias=self.b3, relu=True,
-               workspace=ws)
+        b.obs = obs  # the conv1 weight gradient re-gathers its columns from the frames
+        if self.implicit:
+            G.gemm(obs, 0, True, self.sW1, 256, True, b.y1, 32, 1, B * 400, 32, 256, bias=self.b1, relu=True,
+                   workspace=ws, ga=[1, B, 4, 84, 84, 8, 8, 4], ga_scale=1.0 / 255.0)
+            G.gemm(b.y1, 0, True, self.sW2, 512, True, b.y2, 64, 1, B * 81, 64, 512, bias=self.b2, relu=True,
+                   workspace=ws, ga=[2, B, 32, 20, 20, 4, 4, 2])
+            G.gemm(b.y2, 0, True, self.sW3, 576, True, b.y3, 64, 1, B * 49, 64, 576, bias=self.b3, relu=True,
+                   workspace=ws, ga=[2, B, 64, 9, 9, 3, 3, 1])
+        else:
+            G.im2col_u8(obs, b.col1, 8, 8, 4)
+            G.gemm(b.col1, 256, True, self.sW1, 256, True, b.y1, 32, 1, B * 400, 32, 256, bias=self.b1, relu=True,
+                   workspace=ws)
+            G.im2col_nhwc(b.y1, b.col2, B, 20, 20, 32, 4, 4, 2)
+            G.gemm(b.col2, 512, True, self.sW2, 512, True, b.y2, 64, 1, B * 81, 64, 512, bias=self.b2, relu=True,
+                   workspace=ws)
+            G.im2col_nhwc(b.y2, b.col3, B, 9, 9, 64, 3, 3, 1)
+            G.gemm(b.col3, 576, True, self.sW3, 576, True, b.y3, 64, 1, B * 49, 64, 576, bias=self.b3, relu=True,
+                   workspace=ws)
         G.gemm(b.y3, 3136, True, self.sWfc, 512, False, b.h, 512, 1, B, 512, 3136, bias=self.bfc, relu=True,
                workspace=ws)
         G.gemm(b.h, 512, True, self.sWh, self.A1, False, b.z, self.A1, 0, B, self.A1, 512, bias=self.bh,
@@ -131,16 +143,29 @@ class CNNEngine:
         G.gemm(b.y3, 3136, False, b.dh, 512, False, self.gWfc, 512, 2, 3136, 512, B, workspace=ws)
         G.gemm(b.dh, 512, True, self.sWfc, 512, True, b.dy3, 3136, 1, B, 3136, 512, mask=b.y3, ldm=3136,
                colsum=self.gb3, colsum_mod=64, workspace=ws)
+        imp = self.implicit
         # conv3
-        G.gemm(b.dy3, 64, False, b.col3, 576, False, self.gW3, 576, 2, 64, 576, B * 49, workspace=ws)
+        if imp:
+            G.gemm(b.dy3, 64, False, b.y2, 0, False, self.gW3, 576, 2, 64, 576, B * 49, workspace=ws,
+                   gb=[2, B, 64, 9, 9, 3, 3, 1])
+        else:
+            G.gemm(b.dy3, 64, False, b.col3, 576, False, self.gW3, 576, 2, 64, 576, B * 49, workspace=ws)
         G.gemm(b.dy3, 64, True, self.sW3, 576, False, b.dcol3, 576, 1, B * 49, 576, 64, workspace=ws)
         G.col2im_nhwc(b.dcol3, b.y2, b.dy2, self.gb2, B, 9, 9, 64, 3, 3, 1)
         # conv2
-        G.gemm(b.dy2, 64, False, b.col2, 512, False, self.gW2, 512, 2, 64, 512, B * 81, workspace=ws)
+        if imp:
+            G.gemm(b.dy2, 64, False, b.y1, 0, False, self.gW2, 512, 2, 64, 512, B * 81, workspace=ws,
+                   gb=[2, B, 32, 20, 20, 4, 4, 2])
+        else:
+            G.gemm(b.dy2, 64, False, b.col2, 512, False, self.gW2, 512, 2, 64, 512, B * 81, workspace=ws)
         G.gemm(b.dy2, 64, True, self.sW2, 512, False, b.dcol2, 512, 1, B * 81, 512, 64, workspace=ws)
         G.col2im_nhwc(b.dcol2, b.y1, b.dy1, self.gb1, B, 20, 20, 32, 4, 4, 2)
         # conv1
-        G.gemm(b.dy1, 32, False, b.col1, 256, False, self.gW1, 256, 2, 32, 256, B * 400, workspace=ws)
+        if imp:
+            G.gemm(b.dy1, 32, False, b.obs, 0, False, self.gW1, 256, 2, 32, 256, B * 400, workspace=ws,
+                   gb=[1, B, 4, 84, 84, 8, 8, 4], gb_scale=1.0 / 255.0)
+        else:
+            G.gemm(b.dy1, 32, False, b.col1, 256, False, self.gW1, 256, 2, 32, 256, B * 400, workspace=ws)
 
     # ------------------------------------------------------------------------------------------------ loss
     def loss(self, b: _Bufs, actions, logp_old, adv, ret, v_old, ent_coef, kl_coef, vf_coef, ppo_clip, v_clip,

@@ -17,7 +17,8 @@ from .. import _native
 
 # tile id -> (BM, BN) ; must match aca_gemm_tile_dims
 TILES = {0: (64, 64), 1: (32, 64), 2: (64, 32), 3: (128, 64), 4: (32, 32)}
-BK = 64
+# supported k-step depths per tile (aca_gemm_supported): deeper k-steps for the small tiles of latency-bound products
+BKS = {0: (64, 128), 1: (64, 128), 2: (64, 128), 3: (64,), 4: (64, 128, 256)}
 NUM_CUS = 256
 
 
@@ -25,14 +26,20 @@ def _cdiv(a, b):
     return (a + b - 1) // b
 
 
+def effective_splits(K, bk, splits):
+    kt = _cdiv(K, bk)
+    splits = max(1, min(splits, kt if kt > 0 else 1))
+    per = _cdiv(kt, splits) if kt > 0 else 0
+    return _cdiv(kt, per) if kt > 0 else 1
+
+
 def plan(M, N, K, atomic=False, max_splits=64, target_wgs=256):
-    """Choose ``(tile, splits)`` for an M x N x K product.
+    """Static ``(tile, bk, splits)`` heuristic (used when autotuning is off or during graph capture).
 
     Prefer the largest tile that still yields ``target_wgs`` workgroups; when even the smallest tile leaves the
-    chip mostly idle, split K (each split keeps >= 2 k-tiles). ``atomic`` products (weight gradients) may split
+    chip mostly idle, split K (each split keeps >= 2 k-steps). ``atomic`` products (weight gradients) may split
     deeper because their reduction costs nothing extra.
     """
-    kt = _cdiv(K, BK)
     best = None
     for tile in (3, 0, 2, 1, 4):
         bm, bn = TILES[tile]
@@ -40,15 +47,16 @@ def plan(M, N, K, atomic=False, max_splits=64, target_wgs=256):
             continue
         wgs = _cdiv(M, bm) * _cdiv(N, bn)
         if wgs >= target_wgs:
-            return tile, 1
+            return tile, 64, 1
         if best is None or wgs > best[1]:
             best = (tile, wgs)
     tile, wgs = best
+    kt = _cdiv(K, 64)
     splits = 1
     cap = max_splits if atomic else 16
     while wgs * splits * 2 <= 2 * target_wgs and kt // (splits * 2) >= 2 and splits * 2 <= cap:
         splits *= 2
-    return tile, splits
+    return tile, 64, splits
 
 
 def workspace_elems(M, N, tile, splits):
@@ -71,10 +79,10 @@ class GemmWorkspace:
 
 
 # ------------------------------------------------------------------------------------------------ autotuning
-# The engine issues ~20 distinct GEMM shapes, all small and latency-bound (32..64k rows); the fastest (tile,
-# split-K) pair depends on how many workgroups a shape yields against 256 CUs and how many k-tiles each serial
-# chain has to walk. Each new shape is timed once on its first (eager, never captured) call against scratch
-# outputs and the winner is cached for the process. ACAMD_GEMM_TUNE=0 falls back to the static :func:`plan`.
+# The engine issues ~20 distinct GEMM shapes, all small and latency-bound (32..64k rows); the fastest
+# (tile, k-step depth, split-K) triple depends on how many workgroups a shape yields against 256 CUs and how many
+# k-steps each serial chain has to walk. Each new shape is timed once on its first (eager, never captured) call
+# against scratch outputs and the winner is cached for the process. ACAMD_GEMM_TUNE=0 uses :func:`plan`.
 _TUNED: dict = {}
 TUNE = os.environ.get("ACAMD_GEMM_TUNE", "1") == "1"
 
@@ -84,67 +92,24 @@ def tuned_plans():
 
 
 def _candidates(M, N, K, atomic):
-    kt = _cdiv(K, BK)
     for tile, (bm, bn) in TILES.items():
         if bm >= 2 * max(32, M) or bn >= 2 * max(32, N):
             continue  # a tile at least twice the problem in one dimension only wastes MFMA issue
-        for s in (1, 2, 4, 8, 16, 32, 64):
-            if s > 1 and kt < 2 * s:
-                break
-            if not atomic and s > 16:
-                break
-            yield tile, s
+        for bk in BKS[tile]:
+            kt = _cdiv(K, bk)
+            if bk > 64 and kt < 1:
+                continue
+            for s in (1, 2, 4, 8, 16, 32, 64):
+                if s > 1 and kt < 2 * s:
+                    break
+                if not atomic and s > 16:
+                    break
+                yield tile, bk, s
 
 
-def _tune(key, A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha, bias, relu, mask, ldm, colsum,
-          workspace, colsum_mod):
-    ops = _native.require()
-    dev = C.device
-    need = (M - 1) * ldc + N
-    Cs = torch.zeros(need, dtype=C.dtype, device=dev)
-    cs = torch.zeros(max(N, colsum_mod or 0), dtype=torch.float32, device=dev) if colsum is not None else None
-    ws = workspace if workspace is not None else GemmWorkspace(dev)
-    best = None
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    for tile, s in _candidates(M, N, K, out_mode == 2):
-        eff = ops.gemm_effective_splits(K, s)
-        wsp = tk = None
-        if eff > 1 and out_mode != 2:
-            e, t = workspace_elems(M, N, tile, eff)
-            ws.ensure(e, t)
-            wsp, tk = ws.ws, ws.tickets
-        args = (A, lda, a_k, B, ldb, b_k, Cs, ldc, out_mode, M, N, K, float(alpha), bias, bool(relu), mask, ldm, cs,
-                tile, s, wsp, tk, int(colsum_mod))
-        ops.gemm(*args)
-        ev0.record()
-        for _ in range(4):
-            ops.gemm(*args)
-        ev1.record()
-        ev1.synchronize()
-        ms = ev0.elapsed_time(ev1) / 4
-        if best is None or ms < best[0]:
-            best = (ms, tile, s)
-    _TUNED[key] = (best[1], best[2], best[0])
-    return best[1], best[2]
-
-
-def gemm(A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha=1.0, bias=None, relu=False, mask=None, ldm=0,
-         colsum=None, tile=None, splits=None, workspace: GemmWorkspace | None = None, colsum_mod=0):
-    """Native GEMM; ``out_mode``: 0 fp32 store, 1 bf16 store, 2 fp32 atomic add (C pre-zeroed)."""
-    if tile is None or splits is None:
-        key = (M, N, K, bool(a_k), bool(b_k), out_mode, lda % 8 == 0, ldb % 8 == 0)
-        hit = _TUNED.get(key)
-        if hit is not None:
-            t, s = hit[0], hit[1]
-        elif TUNE and C.is_cuda and not torch.cuda.is_current_stream_capturing():
-            t, s = _tune(key, A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha, bias, relu, mask, ldm,
-                         colsum, workspace, colsum_mod)
-        else:
-            t, s = plan(M, N, K, atomic=(out_mode == 2))
-        tile = t if tile is None else tile
-        splits = s if splits is None else splits
-    ops = _native.require()
-    eff = ops.gemm_effective_splits(K, splits)
+def _run(ops, A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha, bias, relu, mask, ldm, colsum,
+         colsum_mod, tile, bk, splits, workspace, ga, ga_scale, gb, gb_scale):
+    eff = effective_splits(K, bk, splits)
     ws = tk = None
     if eff > 1 and out_mode != 2:
         if workspace is None:
@@ -152,11 +117,61 @@ def gemm(A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha=1.0, bias=No
         e, t = workspace_elems(M, N, tile, eff)
         workspace.ensure(e, t)
         ws, tk = workspace.ws, workspace.tickets
-    if colsum_mod:
-        if colsum is None:
-            raise ValueError("colsum_mod without colsum")
     ops.gemm(A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, float(alpha), bias, bool(relu), mask, ldm,
-             colsum, tile, splits, ws, tk, int(colsum_mod))
+             colsum, int(colsum_mod), tile, bk, splits, ws, tk, list(ga or []), float(ga_scale), list(gb or []),
+             float(gb_scale))
+
+
+def _tune(key, ops, A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha, bias, relu, mask, ldm, colsum,
+          colsum_mod, workspace, ga, ga_scale, gb, gb_scale):
+    dev = C.device
+    Cs = torch.zeros((M - 1) * ldc + N, dtype=C.dtype, device=dev)
+    cs = torch.zeros(max(N, colsum_mod or 0), dtype=torch.float32, device=dev) if colsum is not None else None
+    ws = workspace if workspace is not None else GemmWorkspace(dev)
+    best = None
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for tile, bk, s in _candidates(M, N, K, out_mode == 2):
+        args = (ops, A, lda, a_k, B, ldb, b_k, Cs, ldc, out_mode, M, N, K, alpha, bias, relu, mask, ldm, cs,
+                colsum_mod, tile, bk, s, ws, ga, ga_scale, gb, gb_scale)
+        _run(*args)
+        ev0.record()
+        for _ in range(4):
+            _run(*args)
+        ev1.record()
+        ev1.synchronize()
+        ms = ev0.elapsed_time(ev1) / 4
+        if best is None or ms < best[0]:
+            best = (ms, tile, bk, s)
+    _TUNED[key] = (best[1], best[2], best[3], best[0])
+    return best[1], best[2], best[3]
+
+
+def gemm(A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha=1.0, bias=None, relu=False, mask=None, ldm=0,
+         colsum=None, tile=None, splits=None, workspace: GemmWorkspace | None = None, colsum_mod=0, bk=None,
+         ga=None, ga_scale=1.0, gb=None, gb_scale=1.0):
+    """Native GEMM; ``out_mode``: 0 fp32 store, 1 bf16 store, 2 fp32 atomic add (C pre-zeroed).
+
+    ``ga`` / ``gb``: implicit-im2col gathers ``[mode, B, C, H, W, KH, KW, S]`` (mode 1 uint8 NCHW, 2 bf16 NHWC)
+    reading operand A (k-contiguous) / B (n-contiguous) straight from the activation image ``A`` / ``B``.
+    """
+    ops = _native.require()
+    if tile is None or splits is None or bk is None:
+        key = (M, N, K, bool(a_k), bool(b_k), out_mode, lda % 8 == 0, ldb % 8 == 0, tuple(ga or ()), tuple(gb or ()))
+        hit = _TUNED.get(key)
+        if hit is not None:
+            t, k, s = hit[0], hit[1], hit[2]
+        elif TUNE and C.is_cuda and not torch.cuda.is_current_stream_capturing():
+            t, k, s = _tune(key, ops, A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha, bias, relu, mask,
+                            ldm, colsum, colsum_mod, workspace, ga, ga_scale, gb, gb_scale)
+        else:
+            t, k, s = plan(M, N, K, atomic=(out_mode == 2))
+        tile = t if tile is None else tile
+        bk = k if bk is None else bk
+        splits = s if splits is None else splits
+    if colsum_mod and colsum is None:
+        raise ValueError("colsum_mod without colsum")
+    _run(ops, A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha, bias, relu, mask, ldm, colsum, colsum_mod,
+         tile, bk, splits, workspace, ga, ga_scale, gb, gb_scale)
 
 
 def _view(t, rows, cols, ld, k_contig_rows):

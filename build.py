@@ -27,7 +27,8 @@ BUILD_DIR = os.path.join(ROOT, "build")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
-KERNELS = ["env_classic", "env_atari", "heads", "returns", "optim", "gemm", "conv", "loss"]
+KERNELS = ["env_classic", "env_atari", "heads", "returns", "optim", "gemm", "gemm_plain", "gemm_conv", "conv",
+           "loss"]
 # env kernels must round exactly like the PyTorch oracles: no fma contraction
 NO_CONTRACT = {"env_classic", "env_atari"}
 
@@ -58,7 +59,7 @@ def write_ninja(verbose=False):
       f"-Wno-unused-result")
     binc = " ".join(f"-isystem {p}" for p in incs)
     w(f"bflags = -O2 -std=c++17 -fPIC -D__HIP_PLATFORM_AMD__=1 -DUSE_ROCM=1 -D_GLIBCXX_USE_CXX11_ABI={abi} "
-      f"-isystem {ROCM}/include {binc} -Wno-deprecated-declarations")
+      f"-isystem {ROCM}/include {binc} -I{ROOT}/csrc/kernels -Wno-deprecated-declarations")
     w(f"tbflags = -O2 -std=c++17 -fPIC -isystem {py_inc} -isystem {_pybind_include()} -I{ROOT}/csrc/tfbundle")
     w(f"ldflags = -shared -L{tlib} -Wl,-rpath,{tlib} -lamdhip64 -lc10 -lc10_hip -ltorch -ltorch_cpu -ltorch_hip")
     w("rule hipcc\n  command = $hipcc $kflags $extra -c $in -o $out\n  description = HIPCC $in")
@@ -67,7 +68,7 @@ def write_ninja(verbose=False):
     w("rule link\n  command = $cxx $in $ldflags -o $out\n  description = LINK $out")
     w("rule tblink\n  command = $cxx -shared $in -o $out\n  description = LINK $out")
     objs = []
-    hdr = os.path.join(ROOT, "csrc", "kernels", "common.h")
+    hdr = " ".join(os.path.join(ROOT, "csrc", "kernels", h) for h in ("common.h", "gemm_impl.h", "gemm_desc.h"))
     for k in KERNELS:
         src = os.path.join(ROOT, "csrc", "kernels", k + ".hip")
         obj = os.path.join(BUILD_DIR, k + ".o")
@@ -75,7 +76,7 @@ def write_ninja(verbose=False):
         w(f"build {obj}: hipcc {src} | {hdr}\n  extra = {extra}")
         objs.append(obj)
     bobj = os.path.join(BUILD_DIR, "bindings.o")
-    w(f"build {bobj}: cxx {os.path.join(ROOT, 'csrc', 'bindings.cpp')}")
+    w(f"build {bobj}: cxx {os.path.join(ROOT, 'csrc', 'bindings.cpp')} | {hdr}")
     objs.append(bobj)
     w(f"build {os.path.join(OUT_DIR, 'libacamd.so')}: link {' '.join(objs)}")
     # TF-bundle codec (pybind11, no torch)

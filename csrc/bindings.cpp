@@ -11,6 +11,9 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <vector>
+
+#include "gemm_desc.h"
 
 extern "C" {
 hipError_t aca_env_step_cartpole(float*, int32_t*, int64_t*, float*, float*, const int64_t*, const int32_t*,
@@ -40,10 +43,10 @@ hipError_t aca_adam_step(float*, float*, float*, float*, size_t, const float*, f
 hipError_t aca_rmsprop_step(float*, float*, float*, size_t, const float*, const float*, uint16_t*, float, float,
                             float, float, int, hipStream_t);
 hipError_t aca_cast_bf16(const float*, uint16_t*, size_t, hipStream_t);
-hipError_t aca_gemm(const void*, int64_t, bool, const void*, int64_t, bool, void*, int64_t, int, int, int, int, float,
-                    const float*, int, const void*, int64_t, float*, int, int, float*, unsigned int*, int, hipStream_t);
-int aca_gemm_effective_splits(int, int);
+hipError_t aca_gemm_run(const AcaGemmDesc*, hipStream_t);
+int aca_gemm_effective_splits(int, int, int);
 int aca_gemm_tile_dims(int, int*, int*);
+int aca_gemm_supported(int, int);
 hipError_t aca_im2col_u8_nchw(const uint8_t*, uint16_t*, int, int, int, int, int, int, int, float, hipStream_t);
 hipError_t aca_im2col_nhwc(const uint16_t*, uint16_t*, int, int, int, int, int, int, int, hipStream_t);
 hipError_t aca_col2im_nhwc(const uint16_t*, const uint16_t*, uint16_t*, float*, int, int, int, int, int, int, int,
@@ -343,15 +346,60 @@ void check_extent(const Tensor& t, int64_t rows, int64_t cols, int64_t ld, const
   TORCH_CHECK(need_elems <= have, "gemm: ", name, " too small: needs ", need_elems, " elements, has ", have);
 }
 
+// gather spec: [mode, B, C, H, W, KH, KW, S] (mode 0 = plain operand); the gather source is the operand tensor
+AcaConvGather make_gather(const Tensor& src, const std::vector<int64_t>& spec, double scale, const char* name) {
+  AcaConvGather g{};
+  g.mode = spec.empty() ? 0 : (int)spec[0];
+  if (!g.mode) return g;
+  TORCH_CHECK(spec.size() == 8, "gemm: gather spec for ", name, " must be [mode, B, C, H, W, KH, KW, S]");
+  g.src = src.data_ptr();
+  g.B = spec[1]; g.C = spec[2]; g.H = spec[3]; g.W = spec[4]; g.KH = spec[5]; g.KW = spec[6]; g.S = spec[7];
+  g.OH = (g.H - g.KH) / g.S + 1;
+  g.OW = (g.W - g.KW) / g.S + 1;
+  g.scale = (float)scale;
+  TORCH_CHECK(src.is_contiguous(), "gemm: gather source ", name, " must be contiguous");
+  TORCH_CHECK(src.numel() >= (int64_t)g.B * g.C * g.H * g.W, "gemm: gather source ", name, " too small");
+  if (g.mode == 1) {
+    TORCH_CHECK(src.scalar_type() == at::kByte, "gemm: gather mode 1 needs a uint8 source");
+    TORCH_CHECK(g.KW % 8 == 0 && g.S % 4 == 0 && g.W % 4 == 0, "gemm: gather mode 1 needs KW%8, S%4, W%4 == 0");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(g.src) % 4 == 0, "gemm: gather source must be 4-byte aligned");
+  } else if (g.mode == 2) {
+    TORCH_CHECK(src.scalar_type() == at::kBFloat16, "gemm: gather mode 2 needs a bf16 source");
+    TORCH_CHECK(g.C % 8 == 0, "gemm: gather mode 2 needs C % 8 == 0");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(g.src) % 16 == 0, "gemm: gather source must be 16-byte aligned");
+  } else {
+    TORCH_CHECK(false, "gemm: unknown gather mode ", g.mode);
+  }
+  return g;
+}
+
 void gemm(Tensor A, int64_t lda, bool a_k, Tensor B, int64_t ldb, bool b_k, Tensor C, int64_t ldc, int64_t out_mode,
           int64_t M, int64_t N, int64_t K, double alpha, c10::optional<Tensor> bias, bool relu,
-          c10::optional<Tensor> mask, int64_t ldm, c10::optional<Tensor> colsum, int64_t tile, int64_t splits,
-          c10::optional<Tensor> ws, c10::optional<Tensor> tickets, int64_t colsum_mod) {
-  TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "gemm: A and B must be bf16");
+          c10::optional<Tensor> mask, int64_t ldm, c10::optional<Tensor> colsum, int64_t colsum_mod, int64_t tile,
+          int64_t bk, int64_t splits, c10::optional<Tensor> ws, c10::optional<Tensor> tickets,
+          std::vector<int64_t> ga, double ga_scale, std::vector<int64_t> gb, double gb_scale) {
   TORCH_CHECK(out_mode >= 0 && out_mode <= 2, "gemm: bad out_mode");
+  TORCH_CHECK(aca_gemm_supported((int)tile, (int)bk), "gemm: unsupported tile ", tile, " / bk ", bk);
   TORCH_CHECK(C.scalar_type() == (out_mode == 1 ? at::kBFloat16 : at::kFloat), "gemm: C dtype mismatch");
-  check_extent(A, a_k ? M : K, a_k ? K : M, lda, "A");
-  check_extent(B, b_k ? N : K, b_k ? K : N, ldb, "B");
+  AcaGemmDesc d{};
+  d.ga = make_gather(A, ga, ga_scale, "A");
+  d.gb = make_gather(B, gb, gb_scale, "B");
+  if (d.ga.mode) {
+    TORCH_CHECK(a_k, "gemm: A gather needs a_k");
+    TORCH_CHECK(M == (int64_t)d.ga.B * d.ga.OH * d.ga.OW && K == (int64_t)d.ga.C * d.ga.KH * d.ga.KW,
+                "gemm: A gather shape does not match M/K");
+  } else {
+    TORCH_CHECK(A.scalar_type() == at::kBFloat16, "gemm: A must be bf16");
+    check_extent(A, a_k ? M : K, a_k ? K : M, lda, "A");
+  }
+  if (d.gb.mode) {
+    TORCH_CHECK(!b_k, "gemm: B gather needs !b_k");
+    TORCH_CHECK(K == (int64_t)d.gb.B * d.gb.OH * d.gb.OW && N == (int64_t)d.gb.C * d.gb.KH * d.gb.KW,
+                "gemm: B gather shape does not match K/N");
+  } else {
+    TORCH_CHECK(B.scalar_type() == at::kBFloat16, "gemm: B must be bf16");
+    check_extent(B, b_k ? N : K, b_k ? K : N, ldb, "B");
+  }
   check_extent(C, M, N, ldc, "C");
   if (bias.has_value() && bias->defined()) {
     TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() >= N, "gemm: bias must be fp32 [N]");
@@ -364,9 +412,7 @@ void gemm(Tensor A, int64_t lda, bool a_k, Tensor B, int64_t ldb, bool b_k, Tens
     TORCH_CHECK(colsum->scalar_type() == at::kFloat && colsum->numel() >= (colsum_mod > 0 ? colsum_mod : N),
                 "gemm: colsum too small");
   }
-  float* wsp = nullptr;
-  unsigned int* tk = nullptr;
-  const int eff = aca_gemm_effective_splits((int)K, (int)splits);
+  const int eff = aca_gemm_effective_splits((int)K, (int)bk, (int)splits);
   if (eff > 1 && out_mode != 2) {
     TORCH_CHECK(ws.has_value() && ws->defined() && tickets.has_value() && tickets->defined(),
                 "gemm: slab split-K needs ws and tickets");
@@ -376,17 +422,25 @@ void gemm(Tensor A, int64_t lda, bool a_k, Tensor B, int64_t ldb, bool b_k, Tens
     TORCH_CHECK(ws->scalar_type() == at::kFloat && ws->numel() >= tiles * eff * bm * bn, "gemm: ws too small (need ",
                 tiles * eff * bm * bn, ")");
     TORCH_CHECK(tickets->scalar_type() == at::kInt && tickets->numel() >= tiles, "gemm: tickets too small");
-    wsp = ptr<float>(*ws);
-    tk = ptr<unsigned int>(*tickets);
+    d.ws = ptr<float>(*ws);
+    d.tickets = ptr<unsigned int>(*tickets);
   }
-  check(aca_gemm(A.data_ptr(), lda, a_k, B.data_ptr(), ldb, b_k, C.data_ptr(), ldc, (int)out_mode, (int)M, (int)N,
-                 (int)K, (float)alpha, optr<float>(bias), relu ? 1 : 0,
-                 (mask.has_value() && mask->defined()) ? mask->data_ptr() : nullptr, ldm, optr<float>(colsum),
-                 (int)tile, (int)splits, wsp, tk, (int)colsum_mod, cur_stream(C)),
-        "gemm");
+  d.A = A.data_ptr(); d.B = B.data_ptr(); d.C = C.data_ptr();
+  d.bias = optr<float>(bias);
+  d.mask = (mask.has_value() && mask->defined()) ? mask->data_ptr() : nullptr;
+  d.colsum = optr<float>(colsum);
+  d.lda = lda; d.ldb = ldb; d.ldc = ldc; d.ldm = ldm;
+  d.M = (int)M; d.N = (int)N; d.K = (int)K;
+  d.a_k = a_k; d.b_k = b_k;
+  d.out_mode = (int)out_mode; d.relu = relu ? 1 : 0; d.colsum_mod = (int)colsum_mod;
+  d.alpha = (float)alpha;
+  d.tile = (int)tile; d.bk = (int)bk; d.splits = (int)splits;
+  check(aca_gemm_run(&d, cur_stream(C)), "gemm");
 }
 
-int64_t gemm_effective_splits(int64_t K, int64_t splits) { return aca_gemm_effective_splits((int)K, (int)splits); }
+int64_t gemm_effective_splits(int64_t K, int64_t bk, int64_t splits) {
+  return aca_gemm_effective_splits((int)K, (int)bk, (int)splits);
+}
 
 void im2col_u8(Tensor x, Tensor col, int64_t kh, int64_t kw, int64_t s, double scale) {
   need(x, at::kByte, "x");
@@ -498,9 +552,10 @@ TORCH_LIBRARY(acamd, m) {
         "float eps, float clip, float max_norm, bool zero_grad=False) -> ()");
   m.def("cast_bf16(Tensor x, Tensor y) -> ()");
   m.def("gemm(Tensor A, int lda, bool a_k, Tensor B, int ldb, bool b_k, Tensor C, int ldc, int out_mode, int M, "
-        "int N, int K, float alpha, Tensor? bias, bool relu, Tensor? mask, int ldm, Tensor? colsum, int tile, "
-        "int splits, Tensor? ws, Tensor? tickets, int colsum_mod) -> ()");
-  m.def("gemm_effective_splits(int K, int splits) -> int", &gemm_effective_splits);
+        "int N, int K, float alpha, Tensor? bias, bool relu, Tensor? mask, int ldm, Tensor? colsum, int colsum_mod, "
+        "int tile, int bk, int splits, Tensor? ws, Tensor? tickets, int[] ga, float ga_scale, int[] gb, "
+        "float gb_scale) -> ()");
+  m.def("gemm_effective_splits(int K, int bk, int splits) -> int", &gemm_effective_splits);
   m.def("im2col_u8(Tensor x, Tensor col, int kh, int kw, int s, float scale) -> ()");
   m.def("im2col_nhwc(Tensor x, Tensor col, int B, int H, int W, int C, int kh, int kw, int s) -> ()");
   m.def("col2im_nhwc(Tensor dcol, Tensor ymask, Tensor dx, Tensor? colsum, int B, int H, int W, int C, int kh, "

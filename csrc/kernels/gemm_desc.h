@@ -1,0 +1,46 @@
+// Plain-C description of one GEMM launch, shared by the HIP launchers and the torch bindings.
+#pragma once
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+// Implicit-im2col operand gather (convolution as GEMM without materialising the column matrix).
+//   mode 1: uint8 NCHW source [B, C, H, W], k order (c, i, j), values scaled by `scale` (the /255 of the frames);
+//           requires KW % 8 == 0, S % 4 == 0, W % 4 == 0 (8 k = two aligned 4-byte loads)
+//   mode 2: bf16 NHWC source [B, H, W, C], k order (i, j, c); requires C % 8 == 0 (8 k = one 16-byte load)
+// Row index m = (b, oh, ow) of the conv output, column index k as above.
+typedef struct {
+  const void* src;
+  int mode;  // 0 none, 1 u8 nchw, 2 bf16 nhwc
+  int B, C, H, W, KH, KW, S, OH, OW;
+  float scale;
+} AcaConvGather;
+
+typedef struct {
+  const void* A;
+  const void* B;
+  void* C;
+  const float* bias;
+  const void* mask;
+  float* colsum;
+  float* ws;
+  unsigned int* tickets;
+  int64_t lda, ldb, ldc, ldm;
+  int M, N, K;
+  int a_k, b_k;       // operand storage (see gemm_impl.h)
+  int out_mode;       // 0 fp32, 1 bf16, 2 fp32 atomic add
+  int relu;
+  int colsum_mod;
+  float alpha;
+  int tile;           // 0 64x64, 1 32x64, 2 64x32, 3 128x64, 4 32x32
+  int bk;             // 64 | 128 | 256
+  int splits;
+  AcaConvGather ga;   // gather for A (requires a_k)
+  AcaConvGather gb;   // gather for B (requires !b_k): B[k = conv row m][n = conv column k]
+} AcaGemmDesc;
+
+#ifdef __cplusplus
+}
+#endif

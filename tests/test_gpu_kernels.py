@@ -16,12 +16,16 @@ def _bf(x):
 
 
 # ------------------------------------------------------------------------------------------------------ GEMM
+TILE_BK = [(t, bk) for t in range(5) for bk in (64, 128, 256)
+           if bk in {0: (64, 128), 1: (64, 128), 2: (64, 128), 3: (64,), 4: (64, 128, 256)}[t]]
+
+
 @pytest.mark.parametrize("a_k", [True, False])
 @pytest.mark.parametrize("b_k", [True, False])
-@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4])
-def test_gemm_layouts_tiles(cuda, a_k, b_k, tile):
+@pytest.mark.parametrize("tile,bk", TILE_BK)
+def test_gemm_layouts_tiles(cuda, a_k, b_k, tile, bk):
     from actor_critic_algs_on_tensorflow_amd.ops import gemm as G
-    g = torch.Generator(device="cpu").manual_seed(tile * 7 + a_k * 2 + b_k)
+    g = torch.Generator(device="cpu").manual_seed(tile * 7 + a_k * 2 + b_k + bk)
     for (M, N, K) in [(70, 45, 100), (256, 128, 320), (33, 7, 512), (513, 96, 64)]:
         lda = (K if a_k else M) + 8
         ldb = (K if b_k else N) + 8
@@ -33,7 +37,7 @@ def test_gemm_layouts_tiles(cuda, a_k, b_k, tile):
         C = torch.full((M * N,), float("nan"), device=cuda)
         colsum = torch.zeros(N, device=cuda)
         G.gemm(A, lda, a_k, B, ldb, b_k, C, N, 0, M, N, K, alpha=0.5, bias=bias, relu=True, mask=mask, ldm=N,
-               colsum=colsum, tile=tile, splits=1)
+               colsum=colsum, tile=tile, splits=1, bk=bk)
         scale = ref.abs().max().item() + 1e-3
         assert (C.view(M, N) - ref).abs().max().item() <= 2e-3 * scale * math.sqrt(K / 64), (M, N, K)
         assert torch.allclose(colsum, ref.sum(0), rtol=1e-3, atol=1e-2 * scale)
@@ -41,12 +45,12 @@ def test_gemm_layouts_tiles(cuda, a_k, b_k, tile):
         ws = G.GemmWorkspace(cuda)
         Cb = torch.empty(M * N, dtype=torch.bfloat16, device=cuda)
         G.gemm(A, lda, a_k, B, ldb, b_k, Cb, N, 1, M, N, K, alpha=0.5, bias=bias, relu=True, mask=mask, ldm=N,
-               tile=tile, splits=4, workspace=ws)
+               tile=tile, splits=4, workspace=ws, bk=bk)
         assert (Cb.view(M, N).float() - ref).abs().max().item() <= 1e-2 * scale
         assert int(ws.tickets.abs().sum()) == 0  # tickets are self-cleaning
         # atomic split-K (weight-gradient mode)
         Ca = torch.zeros(M * N, device=cuda)
-        G.gemm(A, lda, a_k, B, ldb, b_k, Ca, N, 2, M, N, K, alpha=0.5, tile=tile, splits=3)
+        G.gemm(A, lda, a_k, B, ldb, b_k, Ca, N, 2, M, N, K, alpha=0.5, tile=tile, splits=3, bk=bk)
         ref2 = G.gemm_ref(A, lda, a_k, B, ldb, b_k, M, N, K, alpha=0.5)
         assert (Ca.view(M, N) - ref2).abs().max().item() <= 2e-3 * (ref2.abs().max().item() + 1e-3) * math.sqrt(K / 64)
 
@@ -60,8 +64,37 @@ def test_gemm_identity_asymmetric(cuda):
     for b_k in (True, False):
         B = _bf(Bm.t().contiguous() if b_k else Bm).to(cuda).reshape(-1)
         C = torch.zeros(n * n, device=cuda)
-        G.gemm(A, n, True, B, n, b_k, C, n, 0, n, n, n, tile=0, splits=1)
+        G.gemm(A, n, True, B, n, b_k, C, n, 0, n, n, n, tile=0, splits=1, bk=64)
         assert torch.equal(C.view(n, n).cpu(), Bm)
+
+
+@pytest.mark.parametrize("tile,bk", TILE_BK)
+def test_gemm_implicit_im2col_matches_explicit(cuda, tile, bk):
+    """The gathered (implicit-im2col) operands give bit-identical products to explicit im2col + plain GEMM."""
+    from actor_critic_algs_on_tensorflow_amd.ops import gemm as G
+    B = 3
+    x = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device=cuda)
+    y1 = _bf(torch.randn(B * 400, 32)).to(cuda)
+    W1 = _bf(torch.randn(32, 256)).to(cuda)
+    W2 = _bf(torch.randn(64, 512)).to(cuda)
+    col1 = torch.empty(B * 400, 256, dtype=torch.bfloat16, device=cuda)
+    G.im2col_u8(x, col1, 8, 8, 4)
+    col2 = torch.empty(B * 81, 512, dtype=torch.bfloat16, device=cuda)
+    G.im2col_nhwc(y1, col2, B, 20, 20, 32, 4, 4, 2)
+    for src, ga, scale, col, W, M, N, K in [(x, [1, B, 4, 84, 84, 8, 8, 4], 1 / 255, col1, W1, B * 400, 32, 256),
+                                            (y1, [2, B, 32, 20, 20, 4, 4, 2], 1.0, col2, W2, B * 81, 64, 512)]:
+        C0 = torch.empty(M, N, device=cuda)
+        C1 = torch.empty(M, N, device=cuda)
+        G.gemm(col, K, True, W, K, True, C0, N, 0, M, N, K, tile=tile, bk=bk, splits=1)
+        G.gemm(src, 0, True, W, K, True, C1, N, 0, M, N, K, tile=tile, bk=bk, splits=1, ga=ga, ga_scale=scale)
+        assert torch.equal(C0, C1)
+        # weight-gradient form: dW[n_out, k] = dY^T col, B gathered
+        dY = _bf(torch.randn(M, N)).to(cuda)
+        D0 = torch.zeros(N, K, device=cuda)
+        D1 = torch.zeros(N, K, device=cuda)
+        G.gemm(dY, N, False, col, K, False, D0, K, 2, N, K, M, tile=tile, bk=bk, splits=1)
+        G.gemm(dY, N, False, src, 0, False, D1, K, 2, N, K, M, tile=tile, bk=bk, splits=1, gb=ga, gb_scale=scale)
+        assert torch.equal(D0, D1)
 
 
 # ------------------------------------------------------------------------------------------------------ conv lowering
@@ -229,7 +262,8 @@ def test_ac_loss_kernel_matches_autograd(cuda, ppo):
 
 
 # ------------------------------------------------------------------------------------------------------ engine
-def test_cnn_engine_matches_autograd(cuda):
+@pytest.mark.parametrize("implicit", [True, False])
+def test_cnn_engine_matches_autograd(cuda, implicit):
     """Full native forward + loss + backward of the Atari CNN vs fp32 autograd on the same parameters."""
     from actor_critic_algs_on_tensorflow_amd.algos import losses as L
     from actor_critic_algs_on_tensorflow_amd.algos.engine import CNNEngine
@@ -245,7 +279,7 @@ def test_cnn_engine_matches_autograd(cuda):
             m.bias.uniform_(-0.05, 0.1)
     flat = FlatParams(model.param_groups(), cuda)
     shadow = flat.data.to(torch.bfloat16)
-    eng = CNNEngine(model, flat, shadow)
+    eng = CNNEngine(model, flat, shadow, implicit=implicit)
     obs = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device=cuda)
     b = eng.bufs(B, with_grad=True)
     z = eng.forward(obs, b).clone()

@@ -59,6 +59,22 @@ class _Bufs:
             self.dy1 = torch.empty(B * 400, 32, dtype=bf, device=dev)
             self.stats = torch.zeros(8, dtype=torch.float32, device=dev)
 
+    def rows(self, r0, n):
+        """Forward-only view of rows [r0, r0+n) (one rollout step writing into a learner-sized buffer)."""
+        v = _Bufs.__new__(_Bufs)
+        v.B = n
+        v.obs = None
+        v.y1 = self.y1[r0 * 400:(r0 + n) * 400]
+        v.y2 = self.y2[r0 * 81:(r0 + n) * 81]
+        v.y3 = self.y3[r0 * 49:(r0 + n) * 49]
+        v.h = self.h[r0:r0 + n]
+        v.z = self.z[r0:r0 + n]
+        for name in ("col1", "col2", "col3"):
+            if hasattr(self, name):
+                k = {"col1": 400, "col2": 81, "col3": 49}[name]
+                setattr(v, name, getattr(self, name)[r0 * k:(r0 + n) * k])
+        return v
+
 
 class CNNEngine:
     """Explicit forward/backward of :class:`..models.policy.CNNActorCritic` over a :class:`FlatParams` slab."""
@@ -93,6 +109,8 @@ class CNNEngine:
         self.Wh, self.gWh, self.sWh = views(net.heads.kernel)
         self.bh, self.gbh, _ = views(net.heads.bias)
         self._bufs = {}
+        self.side = torch.cuda.Stream(device=self.dev) if self.dev.type == "cuda" else None
+        self._ev = [torch.cuda.Event() for _ in range(6)] if self.side is not None else None
 
     def bufs(self, B, with_grad=False):
         key = (B, with_grad)
@@ -131,41 +149,73 @@ class CNNEngine:
 
     # ------------------------------------------------------------------------------------------------ backward
     def backward(self, b: _Bufs):
-        """Accumulates d(loss)/d(params) into the gradient slab from ``b.dz`` (written by the loss kernel)."""
+        """Accumulates d(loss)/d(params) into the gradient slab from ``b.dz`` (written by the loss kernel).
+
+        Two streams: the activation-gradient chain (dh -> dy3 -> dy2 -> dy1) runs on the current stream while
+        every weight-gradient product runs on a side stream as soon as its input gradient exists, so the
+        critical path is the dX chain plus the last dW (captured as parallel branches of the hipGraph).
+        """
         B, A1, ws = b.B, self.A1, self.ws
         ops = _native.require()
-        # heads
-        G.gemm(b.h, 512, False, b.dz, A1, False, self.gWh, A1, 2, 512, A1, B, workspace=ws)
-        ops.colsum_bf16(b.dz, B, A1, A1, self.gbh)
+        imp = self.implicit
+        main = torch.cuda.current_stream(self.dev)
+        side = self.side
+        ev = self._ev
+        ws2 = self._side_ws()
+        ev[0].record(main)
+        side.wait_event(ev[0])
+        with torch.cuda.stream(side):   # heads: dWh = h^T dz, dbh = colsum(dz)
+            G.gemm(b.h, 512, False, b.dz, A1, False, self.gWh, A1, 2, 512, A1, B, workspace=ws2)
+            ops.colsum_bf16(b.dz, B, A1, A1, self.gbh)
         G.gemm(b.dz, A1, True, self.sWh, A1, True, b.dh, 512, 1, B, 512, A1, mask=b.h, ldm=512, colsum=self.gbfc,
                workspace=ws)
-        # fc
-        G.gemm(b.y3, 3136, False, b.dh, 512, False, self.gWfc, 512, 2, 3136, 512, B, workspace=ws)
+        ev[1].record(main)
+        side.wait_event(ev[1])
+        with torch.cuda.stream(side):   # fc weight gradient
+            G.gemm(b.y3, 3136, False, b.dh, 512, False, self.gWfc, 512, 2, 3136, 512, B, workspace=ws2)
         G.gemm(b.dh, 512, True, self.sWfc, 512, True, b.dy3, 3136, 1, B, 3136, 512, mask=b.y3, ldm=3136,
                colsum=self.gb3, colsum_mod=64, workspace=ws)
-        imp = self.implicit
-        # conv3
-        if imp:
-            G.gemm(b.dy3, 64, False, b.y2, 0, False, self.gW3, 576, 2, 64, 576, B * 49, workspace=ws,
-                   gb=[2, B, 64, 9, 9, 3, 3, 1])
-        else:
-            G.gemm(b.dy3, 64, False, b.col3, 576, False, self.gW3, 576, 2, 64, 576, B * 49, workspace=ws)
-        G.gemm(b.dy3, 64, True, self.sW3, 576, False, b.dcol3, 576, 1, B * 49, 576, 64, workspace=ws)
-        G.col2im_nhwc(b.dcol3, b.y2, b.dy2, self.gb2, B, 9, 9, 64, 3, 3, 1)
-        # conv2
-        if imp:
-            G.gemm(b.dy2, 64, False, b.y1, 0, False, self.gW2, 512, 2, 64, 512, B * 81, workspace=ws,
-                   gb=[2, B, 32, 20, 20, 4, 4, 2])
-        else:
-            G.gemm(b.dy2, 64, False, b.col2, 512, False, self.gW2, 512, 2, 64, 512, B * 81, workspace=ws)
-        G.gemm(b.dy2, 64, True, self.sW2, 512, False, b.dcol2, 512, 1, B * 81, 512, 64, workspace=ws)
-        G.col2im_nhwc(b.dcol2, b.y1, b.dy1, self.gb1, B, 20, 20, 32, 4, 4, 2)
-        # conv1
+        ev[2].record(main)
+        side.wait_event(ev[2])
+        with torch.cuda.stream(side):   # conv3 weight gradient
+            if imp:
+                G.gemm(b.dy3, 64, False, b.y2, 0, False, self.gW3, 576, 2, 64, 576, B * 49, workspace=ws2,
+                       gb=[2, B, 64, 9, 9, 3, 3, 1])
+            else:
+                G.gemm(b.dy3, 64, False, b.col3, 576, False, self.gW3, 576, 2, 64, 576, B * 49, workspace=ws2)
+        G.gemm(b.dy3, 64, True, self.sW3, 576, False, self.dcol3(b), 576, 1, B * 49, 576, 64, workspace=ws)
+        G.col2im_nhwc(self.dcol3(b), b.y2, b.dy2, self.gb2, B, 9, 9, 64, 3, 3, 1)
+        ev[3].record(main)
+        side.wait_event(ev[3])
+        with torch.cuda.stream(side):   # conv2 weight gradient
+            if imp:
+                G.gemm(b.dy2, 64, False, b.y1, 0, False, self.gW2, 512, 2, 64, 512, B * 81, workspace=ws2,
+                       gb=[2, B, 32, 20, 20, 4, 4, 2])
+            else:
+                G.gemm(b.dy2, 64, False, b.col2, 512, False, self.gW2, 512, 2, 64, 512, B * 81, workspace=ws2)
+        G.gemm(b.dy2, 64, True, self.sW2, 512, False, self.dcol2(b), 512, 1, B * 81, 512, 64, workspace=ws)
+        G.col2im_nhwc(self.dcol2(b), b.y1, b.dy1, self.gb1, B, 20, 20, 32, 4, 4, 2)
+        # conv1 weight gradient (last product of the chain: on the main stream)
         if imp:
             G.gemm(b.dy1, 32, False, b.obs, 0, False, self.gW1, 256, 2, 32, 256, B * 400, workspace=ws,
                    gb=[1, B, 4, 84, 84, 8, 8, 4], gb_scale=1.0 / 255.0)
         else:
             G.gemm(b.dy1, 32, False, b.col1, 256, False, self.gW1, 256, 2, 32, 256, B * 400, workspace=ws)
+        ev[4].record(side)
+        main.wait_event(ev[4])
+
+    @staticmethod
+    def dcol3(b):
+        return b.dcol3
+
+    @staticmethod
+    def dcol2(b):
+        return b.dcol2
+
+    def _side_ws(self):
+        if not hasattr(self, "_ws2"):
+            self._ws2 = G.GemmWorkspace(self.dev)
+        return self._ws2
 
     # ------------------------------------------------------------------------------------------------ loss
     def loss(self, b: _Bufs, actions, logp_old, adv, ret, v_old, ent_coef, kl_coef, vf_coef, ppo_clip, v_clip,

@@ -138,14 +138,23 @@ class ActorCriticTrainer:
                      trunc_out=st.truncated[t])
         st.values[st.T].copy_(model.value(st.obs[st.T]))
 
+    def _reuse_acts(self):
+        """A2C takes one gradient step at the parameters that acted, so the rollout's forward activations ARE the
+        learner's forward pass: each rollout step writes them into its rows of the learner buffers and the learner
+        goes straight to loss + backward (exact; PPO re-evaluates after its first step and keeps the forward)."""
+        return self.engine is not None and self.cfg.algo == "a2c"
+
     @torch.no_grad()
     def _collect_native(self):
         st, env, eng = self.storage, self.env, self.engine
         A = eng.A
-        b = eng.bufs(env.num_envs)
+        N = env.num_envs
+        b = eng.bufs(N)
         ops = _native.require()
+        lb = eng.bufs(st.T * N, with_grad=True) if self._reuse_acts() else None
         for t in range(st.T):
-            z = eng.forward(st.obs[t], b)
+            bt = lb.rows(t * N, N) if lb is not None else b
+            z = eng.forward(st.obs[t], bt)
             # one launch: sample + logp + entropy + value copy, RNG keys from the env counters
             ops.categorical_sample_env(z[:, :A], env.tg, env.env_ids, KEY_ENV_BITS, self.policy_seed, st.actions[t],
                                        st.logp[t], st.entropy[t], st.values[t])
@@ -264,10 +273,13 @@ class ActorCriticTrainer:
             self.lr_ctrl.update_(self.actor_opt.lr, kl)
 
     # ------------------------------------------------------------------ learning (native engine)
-    def _learn_native(self, obs, actions, logp_old, adv, ret, v_old):
+    def _learn_native(self, obs, actions, logp_old, adv, ret, v_old, forward=True):
         cfg, eng = self.cfg, self.engine
         b = eng.bufs(obs.shape[0], with_grad=True)
-        eng.forward(obs, b)
+        if forward:
+            eng.forward(obs, b)
+        else:
+            b.obs = obs  # activations were written by the rollout; dW1 re-gathers the frames
         ppo = cfg.algo == "ppo"
         vf = cfg.vf_coef if "shared" in self.flat.groups else 1.0
         # the loss kernel writes its statistics straight into stats_buf[0:7]
@@ -303,7 +315,8 @@ class ActorCriticTrainer:
                 torch.index_select(v_old, 0, sel, out=m["v"])
                 self._learn_native(m["obs"], m["act"], m["logp"], m["adv"], m["ret"], m["v"])
         else:
-            self._learn_native(obs, actions, logp_old, adv.contiguous(), ret.contiguous(), v_old)
+            self._learn_native(obs, actions, logp_old, adv.contiguous(), ret.contiguous(), v_old,
+                               forward=not self._reuse_acts())
         self._last = (obs, actions, logp_old, ret)
         if not self._defer_allreduce:
             self._finish_learn()

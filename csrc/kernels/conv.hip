@@ -84,6 +84,7 @@ __global__ void __launch_bounds__(256) col2im_nhwc_kernel(const u16* __restrict_
   const int CC = C / 8;
   const int K = KH * KW * C;
   const int64_t total = (int64_t)B * H * W * CC;
+  float part[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
     const int cc = (int)(idx % CC);
@@ -113,11 +114,24 @@ __global__ void __launch_bounds__(256) col2im_nhwc_kernel(const u16* __restrict_
     for (int e = 0; e < 8; ++e) {
       const float v = bf2f(mk.h[e]) > 0.f ? acc[e] : 0.f;
       o.h[e] = f2bf(v);
-      if (colsum) atomicAdd(&csum[cc * 8 + e], bf2f(o.h[e]));
+      part[e] += bf2f(o.h[e]);
     }
     reinterpret_cast<uint4*>(dx)[idx] = o.v;
   }
   if (colsum) {
+    // lanes l, l+CC, l+2CC, ... of a wave hold the same channel chunk (CC divides 64 and the grid stride is a
+    // multiple of 64): reduce across them in registers, then one LDS atomic per channel per wave
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float v = part[e];
+      for (int o = 32; o >= CC; o >>= 1) v += __shfl_xor(v, o, 64);
+      part[e] = v;
+    }
+    const int lane = threadIdx.x & 63;
+    if (lane < CC) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) atomicAdd(&csum[lane * 8 + e], part[e]);
+    }
     __syncthreads();
     for (int c = threadIdx.x; c < C; c += blockDim.x) atomicAdd(&colsum[c], csum[c]);
   }
@@ -169,6 +183,7 @@ extern "C" hipError_t aca_col2im_nhwc(const uint16_t* dcol, const uint16_t* ymas
   const int OH = (H - KH) / S + 1, OW = (W - KW) / S + 1;
   if (C % 8) return hipErrorInvalidValue;
   const int64_t total = (int64_t)B * H * W * (C / 8);
+  if (64 % (C / 8)) return hipErrorInvalidValue;  // the wave-level channel reduction needs C/8 | 64
   col2im_nhwc_kernel<<<grid_for(total, 256), 256, C * sizeof(float), stream>>>(dcol, ymask, dx, colsum, B, C, H, W,
                                                                                KH, KW, S, OH, OW);
   return hipGetLastError();

@@ -104,8 +104,10 @@ using namespace aca;
 
 extern "C" hipError_t aca_sumsq(const float* x, size_t n, float* partial, int max_blocks, unsigned int* ticket,
                                 float* out, hipStream_t stream) {
-  int grid = (int)((n / 4 + OPT_THREADS - 1) / OPT_THREADS);
+  // one workgroup per CU at most: every workgroup pays an agent-scope release (L2 write-back) for its ticket
+  int grid = (int)((n / 4 + OPT_THREADS * 4 - 1) / (OPT_THREADS * 4));
   if (grid < 1) grid = 1;
+  if (grid > 256) grid = 256;
   if (grid > max_blocks) grid = max_blocks;
   sumsq_kernel<<<grid, OPT_THREADS, 0, stream>>>(x, n, partial, ticket, out);
   return hipGetLastError();

@@ -142,7 +142,7 @@ class ActorCriticTrainer:
         """A2C takes one gradient step at the parameters that acted, so the rollout's forward activations ARE the
         learner's forward pass: each rollout step writes them into its rows of the learner buffers and the learner
         goes straight to loss + backward (exact; PPO re-evaluates after its first step and keeps the forward)."""
-        return self.engine is not None and self.cfg.algo == "a2c"
+        return self.engine is not None and self.cfg.algo == "a2c" and self.cfg.reuse_rollout_acts
 
     @torch.no_grad()
     def _collect_native(self):

@@ -1,0 +1,1 @@
+"""Command-line entry points with the reference's flag names."""

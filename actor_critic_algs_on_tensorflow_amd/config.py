@@ -55,6 +55,7 @@ class TrainConfig:
     dtype: str = "bf16"               # compute dtype of the GPU engine (fp32 masters always)
     engine: str = "auto"              # auto | native (hand-written HIP engine) | torch (autograd reference)
     cuda_graph: bool = True
+    reuse_rollout_acts: bool = True   # native A2C: the rollout's activations are the learner's forward (exact)
     total_updates: int = 1000
     # -- distributed -----------------------------------------------------------------------------------------------
     dist_backend: str = "auto"        # auto -> nccl (RCCL) on GPU, gloo on CPU

@@ -50,6 +50,9 @@ class VecEnv:
         self.reward = torch.zeros(N, dtype=torch.float32, device=dev)
         self.done = torch.zeros(N, dtype=torch.uint8, device=dev)
         self.truncated = torch.zeros(N, dtype=torch.uint8, device=dev)
+        # gym-style single-env adapters need the terminal observation the auto-reset overwrites (oracle path only)
+        self.keep_final_obs = False
+        self.final_obs = None
 
     # -- shape info -------------------------------------------------------------------------------------------
     default_max_steps = 1000
@@ -162,6 +165,10 @@ class VecEnv:
         self.reward.copy_(rew)
         self.done.copy_(done.to(torch.uint8))
         self.truncated.copy_(trunc.to(torch.uint8))
+        if self.keep_final_obs:
+            if self.final_obs is None:
+                self.final_obs = torch.empty_like(out)
+            self._stack_push(self._frame(), prev, self.final_obs)
         # auto-reset
         self._reset_state(done)
         self.t.masked_fill_(done, 0)

@@ -1,0 +1,153 @@
+"""TF tensor-bundle codec (C++), reference checkpoint compatibility, trainer save/resume."""
+import os
+import shutil
+
+import numpy as np
+import pytest
+import torch
+
+from actor_critic_algs_on_tensorflow_amd import ckpt
+from actor_critic_algs_on_tensorflow_amd.ckpt import codec
+
+FIX = os.path.join(os.path.dirname(__file__), "fixtures", "model-Pendulum_a3c")
+
+EXPECTED = {
+    "global_actor/Variable": ((), 0), "global_actor/Variable_1": ((), 4), "global_actor/Variable_2": ((), 8),
+    "global_actor/first_layer/bias": ((128,), 12), "global_actor/first_layer/kernel": ((3, 128), 524),
+    "global_actor/log_std": ((1,), 2060), "global_actor/mu_layer/bias": ((1,), 2064),
+    "global_actor/mu_layer/kernel": ((64, 1), 2068), "global_actor/second_layer/bias": ((128,), 2324),
+    "global_actor/second_layer/kernel": ((128, 128), 2836), "global_actor/third_layer/bias": ((64,), 68372),
+    "global_actor/third_layer/kernel": ((128, 64), 68628), "global_critic/Variable": ((), 101396),
+    "global_critic/Variable_1": ((), 101400), "global_critic/first_layer/bias": ((256,), 101404),
+    "global_critic/first_layer/kernel": ((3, 256), 102428), "global_critic/second_layer/bias": ((128,), 105500),
+    "global_critic/second_layer/kernel": ((256, 128), 106012), "global_critic/third_layer/bias": ((128,), 237084),
+    "global_critic/third_layer/kernel": ((128, 128), 237596), "global_critic/value/bias": ((1,), 303132),
+    "global_critic/value/kernel": ((128, 1), 303136),
+}
+
+
+def test_crc32c_vectors():
+    assert codec.crc32c(b"123456789") == 0xE3069283
+    assert codec.crc32c(b"") == 0
+
+
+def test_demo_index_table():
+    header, entries = codec.parse_index(open(FIX + ".index", "rb").read())
+    assert header["num_shards"] == 1 and header["producer"] == 1
+    assert len(entries) == 22
+    for e in entries:
+        shape, off = EXPECTED[e["key"]]
+        assert tuple(e["shape"]) == shape and e["offset"] == off and e["dtype"] == 1
+    assert sum(e["size"] for e in entries) == os.path.getsize(FIX + ".data-00000-of-00001") == 303648
+
+
+def test_demo_values():
+    t = codec.read(FIX)
+    assert np.isclose(t["global_actor/Variable"], 0.005) and np.isclose(t["global_actor/Variable_1"], 0.01)
+    assert np.isclose(t["global_actor/Variable_2"], 1.0)
+    assert np.isclose(t["global_critic/Variable"], 0.001) and np.isclose(t["global_critic/Variable_1"], 0.001)
+    assert abs(float(t["global_actor/log_std"][0]) + 0.0305) < 1e-3
+
+
+def test_byte_identical_rewrite(tmp_path):
+    t = codec.read(FIX)
+    out = str(tmp_path / "rewrite")
+    codec.write(out, t)
+    assert open(out + ".index", "rb").read() == open(FIX + ".index", "rb").read()
+    assert open(out + ".data-00000-of-00001", "rb").read() == open(FIX + ".data-00000-of-00001", "rb").read()
+    idx = open(FIX + ".index", "rb").read()
+    _, entries = codec.parse_index(idx)
+    assert codec.build_index(entries) == idx
+
+
+def test_corruption_detected(tmp_path):
+    for part, pos in ((".data-00000-of-00001", 5000), (".index", 100)):
+        d = tmp_path / part.strip(".").replace("-", "_")
+        d.mkdir()
+        dst = str(d / "m")
+        shutil.copy(FIX + ".index", dst + ".index")
+        shutil.copy(FIX + ".data-00000-of-00001", dst + ".data-00000-of-00001")
+        b = bytearray(open(dst + part, "rb").read())
+        b[pos] ^= 0x40
+        open(dst + part, "wb").write(bytes(b))
+        with pytest.raises(ValueError):
+            codec.read(dst)
+
+
+def test_roundtrip_dtypes(tmp_path):
+    t = {"a/float": np.random.randn(3, 4).astype(np.float32), "b/int": np.arange(5, dtype=np.int32),
+         "c/u8": np.arange(7, dtype=np.uint8), "d/i64": np.array(2 ** 40, dtype=np.int64),
+         "e/f64": np.random.randn(2).astype(np.float64), "f/scalar": np.float32(3.5).reshape(())}
+    p = str(tmp_path / "x")
+    codec.write(p, t)
+    r = codec.read(p)
+    assert list(r) == sorted(t)
+    for k in t:
+        assert r[k].dtype == np.asarray(t[k]).dtype and np.array_equal(r[k], t[k])
+
+
+def test_demo_checkpoint_policy_is_trained():
+    """The reference's shipped A3C Pendulum policy swings up in this framework's Pendulum (parity of env dynamics,
+    MLP, tanh-scaled Gaussian head and the checkpoint layout): a random-init policy scores ~-1200."""
+    from actor_critic_algs_on_tensorflow_amd.api import Agent, evaluate
+    rews = evaluate(FIX, "Pendulum-v0", num_episodes=4, seed=3, verbose=False)
+    assert np.mean(rews) > -450, rews
+    ag = Agent.for_env("Pendulum-v0", family="mlp", variant="a3c", seed=3)
+    path = os.path.join(os.path.dirname(FIX), "..", "_tmp_random_policy")
+    ckpt.save_tensors(path, ckpt.reference_tensors(ag.model.actor, ag.model.critic, "a3c"))
+    try:
+        rr = evaluate(path, "Pendulum-v0", num_episodes=4, seed=3, verbose=False)
+    finally:
+        for f in (path + ".index", path + ".data-00000-of-00001"):
+            os.remove(f)
+    assert np.mean(rr) < np.mean(rews) - 300
+
+
+def test_agent_act_shapes():
+    from actor_critic_algs_on_tensorflow_amd.api import Agent
+    ag = Agent.from_checkpoint(FIX, "Pendulum-v0")
+    a, lp, ent = ag.act(np.zeros(3, np.float32))
+    assert a.shape == (1,) and np.isfinite(lp) and np.isfinite(ent)
+    a, lp, ent = ag.act(np.zeros((5, 3), np.float32))
+    assert a.shape == (5, 1) and lp.shape == (5,)
+    d, _, _ = ag.act(np.zeros((2, 3), np.float32), deterministic=True)
+    assert np.allclose(d[0], d[1])
+
+
+def test_trainer_save_resume(tmp_path):
+    from actor_critic_algs_on_tensorflow_amd import preset
+    from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
+    cfg = preset("cartpole_cpu", num_envs=4, outdir=None, quiet=True, stdout_freq=0, save_every=0,
+                 checkpoint_dir=str(tmp_path), keep_checkpoints=2)
+    tr = ActorCriticTrainer(cfg)
+    for _ in range(3):
+        tr.step()
+    p1 = tr.save_checkpoint()
+    names = codec.read(p1).keys()
+    assert "Actor/first_layer/kernel" in names and "Critic/value/bias" in names and "_acamd/iteration" in names
+    for _ in range(2):
+        tr.step()
+    ref_params = tr.flat.data.clone()
+    tr2 = ActorCriticTrainer(cfg)
+    tr2.load_checkpoint(p1)
+    assert tr2.iteration == 3
+    for _ in range(2):
+        tr2.step()
+    assert torch.allclose(tr2.flat.data, ref_params, atol=1e-6), "resume must continue bit-for-bit"
+    for _ in range(3):
+        tr.step()
+        tr.save_checkpoint()
+    assert len([f for f in os.listdir(tmp_path) if f.endswith(".index")]) == 2
+    assert ckpt.latest_checkpoint(str(tmp_path)).endswith(f"-{tr.iteration}")
+
+
+def test_cnn_checkpoint_roundtrip(tmp_path):
+    from actor_critic_algs_on_tensorflow_amd.api import Agent
+    ag = Agent.for_env("PongNoFrameskip-v4", seed=1)
+    t = ckpt.model_tensors(ag.model)
+    p = str(tmp_path / "cnn")
+    ckpt.save_tensors(p, t)
+    ag2 = Agent.for_env("PongNoFrameskip-v4", seed=2)
+    ckpt.load_model(ag2.model, codec.read(p))
+    for a, b in zip(ag.model.parameters(), ag2.model.parameters()):
+        assert torch.equal(a, b)

@@ -327,3 +327,23 @@ def test_trainer_native_graph_updates(cuda):
         assert torch.isfinite(tr.flat.data).all()
         assert (tr.flat.data - p0).abs().max() > 0
         assert torch.isfinite(torch.stack(list(tr.stats.values()))).all()
+
+
+def test_a2c_activation_reuse_is_exact(cuda):
+    """Learner on the rollout's stored activations == learner that recomputes its forward (same params)."""
+    from actor_critic_algs_on_tensorflow_amd import preset
+    from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
+    res = []
+    for reuse in (True, False):
+        cfg = preset("pong_a2c", num_envs=8, device="cuda:0", outdir=None, quiet=True, stdout_freq=0, save_every=0,
+                     cuda_graph=False, reuse_rollout_acts=reuse, optimizer="adam", max_grad_norm=None)
+        tr = ActorCriticTrainer(cfg)
+        p0 = tr.flat.data.clone()
+        tr.step()
+        torch.cuda.synchronize()
+        res.append((tr.flat.data - p0, tr.storage.actions.clone(), tr.stats_buf.clone()))
+    assert torch.equal(res[0][1], res[1][1])
+    # same loss statistics; same update up to bf16 rounding of activations recomputed with another tile plan
+    assert torch.allclose(res[0][2], res[1][2], rtol=1e-3, atol=1e-5)
+    d0, d1 = res[0][0], res[1][0]
+    assert (d0 - d1).norm() / d0.norm() < 0.05

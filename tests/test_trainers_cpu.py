@@ -1,0 +1,134 @@
+"""Algorithm smoke / learning tests and multi-process distributed tests on CPU (gloo)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from actor_critic_algs_on_tensorflow_amd import preset
+from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _quiet(**kw):
+    base = dict(outdir=None, quiet=True, stdout_freq=0, save_every=0)
+    base.update(kw)
+    return base
+
+
+def _mean_return(tr, updates):
+    tr.env.ep_stats.zero_()
+    for _ in range(updates):
+        tr.step()
+    s = tr.env.ep_stats
+    return float(s[0] / max(float(s[1]), 1.0))
+
+
+def test_cartpole_a2c_learns():
+    """BASELINE config 1 (CartPole A2C on CPU) improves well beyond a random policy (~22)."""
+    torch.manual_seed(0)
+    tr = ActorCriticTrainer(preset("cartpole_cpu", **_quiet(num_envs=16, n_steps=8, seed=3)))
+    first = _mean_return(tr, 60)
+    for _ in range(300):
+        tr.step()
+    last = _mean_return(tr, 60)
+    assert last > max(60.0, 2 * first), (first, last)
+
+
+def test_ppo_and_gaussian_paths_run():
+    for name, kw in (("breakout_ppo", dict(num_envs=4, n_steps=8, ppo_minibatches=2, ppo_epochs=2)),
+                     ("mujoco_ppo_dp8", dict(num_envs=4, n_steps=16, ppo_minibatches=2, ppo_epochs=2))):
+        tr = ActorCriticTrainer(preset(name, **_quiet(device="cpu", cuda_graph=False, **kw)))
+        p0 = tr.flat.data.clone()
+        for _ in range(2):
+            tr.step()
+        assert torch.isfinite(tr.flat.data).all() and (tr.flat.data != p0).any()
+        assert 0.0 <= float(tr.stats["clipfrac"]) <= 1.0
+
+
+def test_reference_regularisers_and_adaptive_lr():
+    cfg = preset("basic_ac", **_quiet(algo="a2c", env="CartPole-v0", n_steps=16, num_envs=2, anneal_regularizers=True))
+    tr = ActorCriticTrainer(cfg)
+    lr0 = tr.actor_opt.get_lr()
+    tr.step()
+    assert abs(float(tr.ent_coef) - 1e-2) < 1e-9 and abs(float(tr.kl_coef) - 1.0) < 1e-9
+    assert tr.actor_opt.get_lr() in (pytest.approx(lr0 * 1.5), pytest.approx(lr0 / 1.5), pytest.approx(lr0))
+    assert float(tr.stats["kl"]) >= 0 and np.isfinite(float(tr.stats["ev_after"]))
+
+
+def test_basic_ac_parity_trainer(tmp_path):
+    from actor_critic_algs_on_tensorflow_amd.api import train
+    log = tmp_path / "log.txt"
+    r = train("basic_ac", env="CartPole-v0", total_updates=3, outdir=str(log), quiet=True, save_every=2,
+              checkpoint_dir=str(tmp_path / "ck"), ep_length_stop=300)
+    assert r.iterations == 3 and r.env_steps >= 3 * 7 * 8   # each batch: >= 300 steps or MAX_ROLLS = 7 episodes
+    assert (tmp_path / "ck-CartPole-0.index").exists()
+    from actor_critic_algs_on_tensorflow_amd.ckpt import codec
+    t = codec.read(str(tmp_path / "ck-CartPole-0"))
+    # Basic_AC names: discrete actor has no log-std variable; beta, gamma, lr are Variable, _1, _2; Adam slots saved
+    assert "Actor/logits/kernel" in t and "Actor/Variable_2" in t and "Critic/Variable" in t
+    assert "Actor/first_layer/kernel/Adam" in t and "Critic/beta1_power" in t
+
+
+# ------------------------------------------------------------------------------------------------ distributed
+def _dp_worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+    from actor_critic_algs_on_tensorflow_amd.parallel.dp import DataParallel
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = preset("cartpole_cpu", **_quiet(num_envs=4, n_steps=5, seed=11, optimizer="adam", max_grad_norm=0.5))
+    tr = ActorCriticTrainer(cfg, dp=DataParallel())
+    for _ in range(3):
+        tr.step()
+    if rank == 0:
+        torch.save({"p": tr.flat.data.clone()}, os.path.join(out_dir, "dp.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_gloo_equals_single_process_union_batch(tmp_path):
+    """Sync DP over 2 ranks x 4 envs == one process over the same 8 envs (grad all-reduce + global adv norm)."""
+    mp.spawn(_dp_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    dp = torch.load(tmp_path / "dp.pt", weights_only=True)["p"]
+    cfg = preset("cartpole_cpu", **_quiet(num_envs=8, n_steps=5, seed=11, optimizer="adam", max_grad_norm=0.5))
+    single = ActorCriticTrainer(cfg)
+    for _ in range(3):
+        single.step()
+    assert torch.allclose(dp, single.flat.data, rtol=1e-4, atol=1e-6)
+
+
+def _a3c_proc(rank, world, port, d):
+    from actor_critic_algs_on_tensorflow_amd.cli import train
+    ps = 1
+    job = "ps" if rank < ps else "worker"
+    task = rank if rank < ps else rank - ps
+    out = train.main([job, str(task), "--env", "CartPole-v0", "--ps_num", str(ps), "--worker_num", str(world - ps),
+                      "--initport", str(port), "--outdir", d + "/logs", "--checkpoint_dir", d + "/ck",
+                      "--max_iters", "6", "--save_every", "3", "--quiet"])
+    torch.save({"gstep": out["global_step"], "role": out["role"],
+                "steps": [h["gstep"] for h in out.get("history", [])]}, f"{d}/r{rank}.pt")
+
+
+def test_a3c_async_parameter_server(tmp_path):
+    d = str(tmp_path)
+    mp.spawn(_a3c_proc, args=(3, _free_port(), d), nprocs=3, join=True)
+    ps = torch.load(f"{d}/r0.pt", weights_only=True)
+    w0 = torch.load(f"{d}/r1.pt", weights_only=True)
+    w1 = torch.load(f"{d}/r2.pt", weights_only=True)
+    assert ps["role"] == "ps" and ps["gstep"] >= 6
+    steps = sorted(w0["steps"] + w1["steps"])
+    assert steps == list(range(1, len(steps) + 1)), "PS serialises applies: every global step taken once"
+    assert os.path.exists(f"{d}/logs/worker_0.log") and os.path.exists(f"{d}/logs/worker_1.log")
+    from actor_critic_algs_on_tensorflow_amd import ckpt
+    latest = ckpt.latest_checkpoint(f"{d}/ck")
+    t = ckpt.load_tensors(latest)
+    assert "global_actor/logits/kernel" in t and "global_critic/Variable_1" in t

@@ -119,8 +119,17 @@ class CNNEngine:
         return self._bufs[key]
 
     # ------------------------------------------------------------------------------------------------ forward
-    def forward(self, obs, b: _Bufs):
-        """obs uint8 [B, 4, 84, 84] -> b.z fp32 [B, A+1] (logits | value)."""
+    def value(self, obs, b: _Bufs, out):
+        """Bootstrap value of ``obs`` written straight into ``out`` [B] (trunk + the value column of the head)."""
+        self.forward(obs, b, head=False)
+        A, A1 = self.A, self.A1
+        G.gemm(b.h, 512, True, self.sWh[A:], A1, False, out, 1, 0, b.B, 1, 512, bias=self.bh[A:],
+               workspace=self.ws)
+        return out
+
+    def forward(self, obs, b: _Bufs, head=True):
+        """obs uint8 [B, 4, 84, 84] -> b.z fp32 [B, A+1] (logits | value); ``head=False`` stops at ``b.h`` (the
+        rollout fuses the head into the sampling + env-step kernel)."""
         B = b.B
         ws = self.ws
         b.obs = obs  # the conv1 weight gradient re-gathers its columns from the frames
@@ -143,12 +152,13 @@ class CNNEngine:
                    workspace=ws)
         G.gemm(b.y3, 3136, True, self.sWfc, 512, False, b.h, 512, 1, B, 512, 3136, bias=self.bfc, relu=True,
                workspace=ws)
-        G.gemm(b.h, 512, True, self.sWh, self.A1, False, b.z, self.A1, 0, B, self.A1, 512, bias=self.bh,
-               workspace=ws)
+        if head:
+            G.gemm(b.h, 512, True, self.sWh, self.A1, False, b.z, self.A1, 0, B, self.A1, 512, bias=self.bh,
+                   workspace=ws)
         return b.z
 
     # ------------------------------------------------------------------------------------------------ backward
-    def backward(self, b: _Bufs):
+    def backward(self, b: _Bufs, head_bias_done=False):
         """Accumulates d(loss)/d(params) into the gradient slab from ``b.dz`` (written by the loss kernel).
 
         Two streams: the activation-gradient chain (dh -> dy3 -> dy2 -> dy1) runs on the current stream while
@@ -166,7 +176,8 @@ class CNNEngine:
         side.wait_event(ev[0])
         with torch.cuda.stream(side):   # heads: dWh = h^T dz, dbh = colsum(dz)
             G.gemm(b.h, 512, False, b.dz, A1, False, self.gWh, A1, 2, 512, A1, B, workspace=ws2)
-            ops.colsum_bf16(b.dz, B, A1, A1, self.gbh)
+            if not head_bias_done:
+                ops.colsum_bf16(b.dz, B, A1, A1, self.gbh)
         G.gemm(b.dz, A1, True, self.sWh, A1, True, b.dh, 512, 1, B, 512, A1, mask=b.h, ldm=512, colsum=self.gbfc,
                workspace=ws)
         ev[1].record(main)
@@ -219,12 +230,24 @@ class CNNEngine:
 
     # ------------------------------------------------------------------------------------------------ loss
     def loss(self, b: _Bufs, actions, logp_old, adv, ret, v_old, ent_coef, kl_coef, vf_coef, ppo_clip, v_clip,
-             stats=None):
-        """Fused loss + head gradient -> ``b.dz``; statistics [pg, kl, ent, vloss, clipfrac, actor loss, ratio]."""
+             stats=None, returns=None):
+        """Fused loss + head gradient -> ``b.dz``; statistics [pg, kl, ent, vloss, clipfrac, actor loss, ratio, ev].
+
+        ``returns`` (A2C fast path): dict(mode=1|2, rew, val, dones, L, gamma, lam, norm_adv, ret_w, adv_w) --
+        targets/advantages, EV-before and advantage normalisation are computed inside the same launch, and the
+        head-bias gradient is written by it too (the backward then skips its column-sum)."""
         B, A, A1 = b.B, self.A, self.A1
         zl = b.z
         out = b.stats if stats is None else stats
-        _native.require().ac_loss(zl, A1, zl[:, A:], A1, actions, None, None, logp_old, adv, ret, v_old, ent_coef,
-                                  kl_coef, float(vf_coef), float(ppo_clip or 0.0), float(v_clip or 0.0), b.dz, A1,
-                                  b.dz[:, A:], A1, None, out, B, A, False)
+        ops = _native.require()
+        if returns is None:
+            ops.ac_loss(zl, A1, zl[:, A:], A1, actions, None, None, logp_old, adv, ret, v_old, ent_coef, kl_coef,
+                        float(vf_coef), float(ppo_clip or 0.0), float(v_clip or 0.0), b.dz, A1, b.dz[:, A:], A1,
+                        None, out, B, A, False)
+        else:
+            r = returns
+            ops.ac_loss(zl, A1, zl[:, A:], A1, actions, None, None, logp_old, None, None, None, ent_coef, kl_coef,
+                        float(vf_coef), 0.0, 0.0, b.dz, A1, b.dz[:, A:], A1, None, out, B, A, False, r["mode"],
+                        r["rew"], r["val"], r["dones"], int(r["L"]), float(r["gamma"]), float(r["lam"]),
+                        bool(r["norm_adv"]), r["ret_w"], r["adv_w"], self.gbh)
         return out

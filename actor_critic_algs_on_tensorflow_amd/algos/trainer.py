@@ -152,19 +152,35 @@ class ActorCriticTrainer:
         b = eng.bufs(N)
         ops = _native.require()
         lb = eng.bufs(st.T * N, with_grad=True) if self._reuse_acts() else None
+        fused = isinstance(env, E.PongVecEnv)
         for t in range(st.T):
             bt = lb.rows(t * N, N) if lb is not None else b
+            if fused:
+                # conv trunk + fc, then ONE launch: policy/value head + sampling + env step (+ frame render)
+                eng.forward(st.obs[t], bt, head=False)
+                ops.env_policy_step_pong(bt.h, eng.sWh, eng.bh, bt.z, st.actions[t], st.logp[t], st.entropy[t],
+                                         st.values[t], KEY_ENV_BITS, self.policy_seed, env.state, env.t, env.tg,
+                                         env.ep_ret, env.ep_stats, env.env_ids, st.obs[t], st.obs[t + 1],
+                                         st.rewards[t], st.dones[t], st.truncated[t], env.seed,
+                                         env.max_episode_steps, env.frame_stack)
+                continue
             z = eng.forward(st.obs[t], bt)
             # one launch: sample + logp + entropy + value copy, RNG keys from the env counters
             ops.categorical_sample_env(z[:, :A], env.tg, env.env_ids, KEY_ENV_BITS, self.policy_seed, st.actions[t],
                                        st.logp[t], st.entropy[t], st.values[t])
             env.step(st.actions[t], prev_obs=st.obs[t], obs_out=st.obs[t + 1], reward_out=st.rewards[t],
                      done_out=st.dones[t], trunc_out=st.truncated[t])
-        z = eng.forward(st.obs[st.T], b)
-        st.values[st.T].copy_(z[:, A])
+        eng.value(st.obs[st.T], b, st.values[st.T])
 
     # ------------------------------------------------------------------ returns
+    def _fused_returns(self):
+        """Native A2C: returns, EV-before and advantage normalisation run inside the loss kernel."""
+        return (self._reuse_acts() and (self.dp is None or not self.cfg.norm_adv)
+                and not self.cfg.bootstrap_on_timeout and self.cfg.returns in ("nstep", "gae"))
+
     def compute_returns(self):
+        if self._fused_returns():
+            return None, None
         cfg, st = self.cfg, self.storage
         dones = st.dones
         if cfg.bootstrap_on_timeout:
@@ -289,7 +305,33 @@ class ActorCriticTrainer:
         self._apply_grads()
 
     @torch.no_grad()
+    def _learn_native_fused(self):
+        """A2C on the rollout's activations: ONE loss launch (returns + EV + adv-norm + loss + dz + head-bias grad),
+        the backward, the optimiser."""
+        cfg, st, eng = self.cfg, self.storage, self.engine
+        obs, actions, logp_old = st.flat("obs"), st.flat("actions"), st.flat("logp")
+        T, N = st.T, st.N
+        b = eng.bufs(T * N, with_grad=True)
+        b.obs = obs
+        if not hasattr(self, "_ret_w"):
+            self._ret_w = torch.zeros(T * N, device=self.device)
+            self._adv_w = torch.zeros(T * N, device=self.device)
+        vf = cfg.vf_coef if "shared" in self.flat.groups else 1.0
+        eng.loss(b, actions, logp_old, None, None, None, self.ent_coef, self.kl_coef, vf, 0.0, 0.0,
+                 stats=self.stats_buf,
+                 returns=dict(mode=1 if cfg.returns == "nstep" else 2, rew=st.rewards, val=st.values, dones=st.dones,
+                              L=T if cfg.look_ahead is None else cfg.look_ahead, gamma=cfg.gamma,
+                              lam=cfg.gae_lambda, norm_adv=cfg.norm_adv, ret_w=self._ret_w, adv_w=self._adv_w))
+        eng.backward(b, head_bias_done=True)
+        self._apply_grads()
+        self._last = (obs, actions, logp_old, self._ret_w)
+        if not self._defer_allreduce:
+            self._finish_learn()
+
+    @torch.no_grad()
     def _learn_native_update(self, ret, adv):
+        if ret is None:
+            return self._learn_native_fused()
         cfg, st = self.cfg, self.storage
         obs, actions, logp_old = st.flat("obs"), st.flat("actions"), st.flat("logp")
         v_old = st.flat("values")
@@ -325,7 +367,8 @@ class ActorCriticTrainer:
         """Post-update KL / EV / adaptive lr (after the optimiser step)."""
         if self.engine is None:
             return
-        self.update_counter += 1
+        if self.cfg.algo == "ppo":
+            self.update_counter += 1   # keys the minibatch permutations
         if self.lr_ctrl is not None or self.cfg.kl_coef > 0:
             obs, actions, logp_old, ret = self._last
             eng = self.engine

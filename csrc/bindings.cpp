@@ -28,6 +28,10 @@ hipError_t aca_env_step_linear(float*, int32_t*, int64_t*, float*, float*, const
 hipError_t aca_env_step_pong(float*, int32_t*, int64_t*, float*, float*, const int64_t*, const int32_t*,
                              const uint8_t*, uint8_t*, float*, uint8_t*, uint8_t*, uint32_t, int, int, int,
                              hipStream_t);
+hipError_t aca_env_policy_step_pong(const uint16_t*, int, const uint16_t*, const float*, int, float*, int32_t*,
+                                    float*, float*, float*, int, uint32_t, float*, int32_t*, int64_t*, float*, float*,
+                                    const int64_t*, const uint8_t*, uint8_t*, float*, uint8_t*, uint8_t*, uint32_t,
+                                    int, int, int, hipStream_t);
 hipError_t aca_categorical_sample(const float*, int, int, int, const int64_t*, const int64_t*, const int64_t*, int,
                                   uint32_t, int32_t*, float*, float*, float*, hipStream_t);
 hipError_t aca_ev(const float*, const float*, float*, int, hipStream_t);
@@ -54,7 +58,9 @@ hipError_t aca_col2im_nhwc(const uint16_t*, const uint16_t*, uint16_t*, float*, 
 hipError_t aca_colsum_bf16(const uint16_t*, int64_t, int, int64_t, float*, hipStream_t);
 hipError_t aca_ac_loss(const float*, int64_t, const float*, int64_t, const int32_t*, const float*, const float*,
                        const float*, const float*, const float*, const float*, const float*, const float*, float, float,
-                       float, uint16_t*, int64_t, uint16_t*, int64_t, float*, float*, int, int, int, hipStream_t);
+                       float, uint16_t*, int64_t, uint16_t*, int64_t, float*, float*, int, int, int, int,
+                       const float*, const float*, const uint8_t*, int, int, int, float, float, int, float*, float*,
+                       float*, int, hipStream_t);
 }
 
 namespace {
@@ -163,6 +169,40 @@ void env_step_pong(Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_s
                           ptr<uint8_t>(out), ptr<float>(reward), ptr<uint8_t>(done), ptr<uint8_t>(trunc),
                           (uint32_t)seed, (int)max_steps, (int)k, N, cur_stream(state)),
         "env_step_pong");
+}
+
+// fused rollout step: policy/value head + sampling + env step (native engine, Pong/Breakout-shaped banks)
+void env_policy_step_pong(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, Tensor logp, Tensor ent,
+                          Tensor value, int64_t key_shift, int64_t pseed, Tensor state, Tensor t, Tensor tg,
+                          Tensor ep_ret, Tensor ep_stats, Tensor ids, Tensor prev, Tensor out, Tensor reward,
+                          Tensor done, Tensor trunc, int64_t seed, int64_t max_steps, int64_t k) {
+  check_env(state, t, tg, ep_ret, ep_stats, ids, reward, done, trunc);
+  need(h, at::kBFloat16, "h");
+  need(Wh, at::kBFloat16, "Wh");
+  need(bh, at::kFloat, "bh");
+  need(z, at::kFloat, "z");
+  need(act, at::kInt, "act");
+  need(logp, at::kFloat, "logp");
+  need(ent, at::kFloat, "ent");
+  need(value, at::kFloat, "value");
+  need(prev, at::kByte, "prev");
+  need(out, at::kByte, "out");
+  const int N = state.size(0);
+  const int A1 = bh.numel(), A = A1 - 1;
+  const int hdim = h.numel() / N;
+  TORCH_CHECK(state.size(1) == 8 && h.numel() == (int64_t)N * hdim && Wh.numel() == (int64_t)hdim * A1 &&
+                  z.numel() >= (int64_t)N * A1 && act.numel() >= N && value.numel() >= N,
+              "env_policy_step_pong: bad shapes");
+  TORCH_CHECK(A1 <= 20 && hdim % 8 == 0, "env_policy_step_pong: at most 19 actions, hidden size % 8 == 0");
+  TORCH_CHECK(prev.numel() == (int64_t)N * k * 84 * 84 && out.numel() == prev.numel(), "pong: bad stack shape");
+  TORCH_CHECK(prev.data_ptr() != out.data_ptr(), "pong: prev and out must not alias");
+  check(aca_env_policy_step_pong(ptr<uint16_t>(h), hdim, ptr<uint16_t>(Wh), ptr<float>(bh), A, ptr<float>(z),
+                                 ptr<int32_t>(act), ptr<float>(logp), ptr<float>(ent), ptr<float>(value),
+                                 (int)key_shift, (uint32_t)pseed, ptr<float>(state), ptr<int32_t>(t),
+                                 ptr<int64_t>(tg), ptr<float>(ep_ret), ptr<float>(ep_stats), ptr<int64_t>(ids),
+                                 ptr<uint8_t>(prev), ptr<uint8_t>(out), ptr<float>(reward), ptr<uint8_t>(done),
+                                 ptr<uint8_t>(trunc), (uint32_t)seed, (int)max_steps, (int)k, N, cur_stream(state)),
+        "env_policy_step_pong");
 }
 
 // ---------------------------------------------------------------------------------------------- heads
@@ -487,19 +527,40 @@ void colsum_bf16(Tensor x, int64_t M, int64_t N, int64_t ld, Tensor out) {
 
 // ---------------------------------------------------------------------------------------------- loss
 void ac_loss(Tensor logits, int64_t ldl, c10::optional<Tensor> value, int64_t ldv, c10::optional<Tensor> act_i,
-             c10::optional<Tensor> act_f, c10::optional<Tensor> log_std, Tensor logp_old, Tensor adv, Tensor ret,
-             c10::optional<Tensor> v_old, c10::optional<Tensor> ent_coef, c10::optional<Tensor> kl_coef,
-             double vf_coef, double ppo_clip, double v_clip, Tensor dlogits, int64_t lddl,
-             c10::optional<Tensor> dvalue, int64_t lddv, c10::optional<Tensor> dlog_std, Tensor stats, int64_t B,
-             int64_t A, bool gaussian) {
+             c10::optional<Tensor> act_f, c10::optional<Tensor> log_std, Tensor logp_old, c10::optional<Tensor> adv,
+             c10::optional<Tensor> ret, c10::optional<Tensor> v_old, c10::optional<Tensor> ent_coef,
+             c10::optional<Tensor> kl_coef, double vf_coef, double ppo_clip, double v_clip, Tensor dlogits,
+             int64_t lddl, c10::optional<Tensor> dvalue, int64_t lddv, c10::optional<Tensor> dlog_std, Tensor stats,
+             int64_t B, int64_t A, bool gaussian, int64_t returns_mode, c10::optional<Tensor> rew,
+             c10::optional<Tensor> val, c10::optional<Tensor> dones, int64_t L, double gamma, double lam,
+             bool norm_adv, c10::optional<Tensor> ret_w, c10::optional<Tensor> adv_w, c10::optional<Tensor> dbias) {
   TORCH_CHECK(logits.scalar_type() == at::kFloat && dlogits.scalar_type() == at::kBFloat16, "ac_loss: dtypes");
   check_extent(logits, B, A, ldl, "logits");
   check_extent(dlogits, B, A, lddl, "dlogits");
   need(logp_old, at::kFloat, "logp_old");
-  need(adv, at::kFloat, "adv");
-  need(ret, at::kFloat, "ret");
   need(stats, at::kFloat, "stats");
-  TORCH_CHECK(logp_old.numel() >= B && adv.numel() >= B && ret.numel() >= B && stats.numel() >= 7, "ac_loss: sizes");
+  TORCH_CHECK(logp_old.numel() >= B && stats.numel() >= 8, "ac_loss: sizes");
+  int T = 0, N = 0;
+  if (returns_mode) {
+    TORCH_CHECK(rew.has_value() && val.has_value() && dones.has_value() && ret_w.has_value() && adv_w.has_value(),
+                "ac_loss: fused returns need rew, val, dones, ret_w, adv_w");
+    need(*rew, at::kFloat, "rew");
+    need(*val, at::kFloat, "val");
+    need(*dones, at::kByte, "dones");
+    need(*ret_w, at::kFloat, "ret_w");
+    need(*adv_w, at::kFloat, "adv_w");
+    TORCH_CHECK(rew->dim() == 2, "ac_loss: rewards must be [T, N]");
+    T = rew->size(0);
+    N = rew->size(1);
+    TORCH_CHECK((int64_t)T * N == B && val->numel() == (int64_t)(T + 1) * N && dones->numel() == B &&
+                    ret_w->numel() >= B && adv_w->numel() >= B,
+                "ac_loss: fused returns shape mismatch");
+  } else {
+    TORCH_CHECK(adv.has_value() && ret.has_value(), "ac_loss: adv and ret needed");
+    need(*adv, at::kFloat, "adv");
+    need(*ret, at::kFloat, "ret");
+    TORCH_CHECK(adv->numel() >= B && ret->numel() >= B, "ac_loss: sizes");
+  }
   if (gaussian) {
     TORCH_CHECK(act_f.has_value() && log_std.has_value(), "ac_loss: gaussian needs act_f and log_std");
   } else {
@@ -510,11 +571,18 @@ void ac_loss(Tensor logits, int64_t ldl, c10::optional<Tensor> value, int64_t ld
     check_extent(*value, B, 1, ldv, "value");
     check_extent(*dvalue, B, 1, lddv, "dvalue");
   }
+  int dbn = 0;
+  if (dbias.has_value() && dbias->defined()) {
+    TORCH_CHECK(dbias->scalar_type() == at::kFloat && dbias->numel() >= A + 1, "ac_loss: dbias must be fp32 [A+1]");
+    dbn = A + 1;
+  }
   check(aca_ac_loss(ptr<float>(logits), ldl, optr<float>(value), ldv, optr<int32_t>(act_i), optr<float>(act_f),
-                    optr<float>(log_std), ptr<float>(logp_old), ptr<float>(adv), ptr<float>(ret), optr<float>(v_old),
+                    optr<float>(log_std), ptr<float>(logp_old), optr<float>(adv), optr<float>(ret), optr<float>(v_old),
                     optr<float>(ent_coef), optr<float>(kl_coef), (float)vf_coef, (float)ppo_clip, (float)v_clip,
                     ptr<uint16_t>(dlogits), lddl, optr<uint16_t>(dvalue), lddv, optr<float>(dlog_std),
-                    ptr<float>(stats), (int)B, (int)A, gaussian ? 1 : 0, cur_stream(logits)),
+                    ptr<float>(stats), (int)B, (int)A, gaussian ? 1 : 0, (int)returns_mode, optr<float>(rew),
+                    optr<float>(val), optr<uint8_t>(dones), T, N, (int)L, (float)gamma, (float)lam, norm_adv ? 1 : 0,
+                    optr<float>(ret_w), optr<float>(adv_w), optr<float>(dbias), dbn, cur_stream(logits)),
         "ac_loss");
 }
 
@@ -535,6 +603,10 @@ TORCH_LIBRARY(acamd, m) {
         "int seed, int max_steps, int k) -> ()");
   m.def("env_step_pong(Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, Tensor env_ids, "
         "Tensor actions, Tensor prev, Tensor out, Tensor reward, Tensor done, Tensor truncated, int seed, "
+        "int max_steps, int k) -> ()");
+  m.def("env_policy_step_pong(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, Tensor logp, Tensor ent, "
+        "Tensor value, int key_shift, int pseed, Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, "
+        "Tensor env_ids, Tensor prev, Tensor out, Tensor reward, Tensor done, Tensor truncated, int seed, "
         "int max_steps, int k) -> ()");
   m.def("categorical_sample(Tensor logits, Tensor keys, int seed, Tensor act, Tensor logp, Tensor ent) -> ()");
   m.def("categorical_sample_env(Tensor logits, Tensor tg, Tensor env_ids, int key_shift, int seed, Tensor act, "
@@ -562,9 +634,11 @@ TORCH_LIBRARY(acamd, m) {
         "int kw, int s) -> ()");
   m.def("colsum_bf16(Tensor x, int M, int N, int ld, Tensor out) -> ()");
   m.def("ac_loss(Tensor logits, int ldl, Tensor? value, int ldv, Tensor? act_i, Tensor? act_f, Tensor? log_std, "
-        "Tensor logp_old, Tensor adv, Tensor ret, Tensor? v_old, Tensor? ent_coef, Tensor? kl_coef, float vf_coef, "
+        "Tensor logp_old, Tensor? adv, Tensor? ret, Tensor? v_old, Tensor? ent_coef, Tensor? kl_coef, float vf_coef, "
         "float ppo_clip, float v_clip, Tensor dlogits, int lddl, Tensor? dvalue, int lddv, Tensor? dlog_std, "
-        "Tensor stats, int B, int A, bool gaussian) -> ()");
+        "Tensor stats, int B, int A, bool gaussian, int returns_mode=0, Tensor? rew=None, Tensor? val=None, "
+        "Tensor? dones=None, int L=0, float gamma=0.99, float lam=0.95, bool norm_adv=False, Tensor? ret_w=None, "
+        "Tensor? adv_w=None, Tensor? dbias=None) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
@@ -572,6 +646,7 @@ TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
   m.impl("env_step_pendulum", &env_step_pendulum);
   m.impl("env_step_linear", &env_step_linear);
   m.impl("env_step_pong", &env_step_pong);
+  m.impl("env_policy_step_pong", &env_policy_step_pong);
   m.impl("categorical_sample", &categorical_sample);
   m.impl("gaussian_sample", &gaussian_sample);
   m.impl("categorical_sample_env", &categorical_sample_env);

@@ -31,25 +31,22 @@ __device__ __forceinline__ void serve(PongState& s, uint32_t seed, uint32_t id, 
 
 __device__ __forceinline__ float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
 
-__global__ void __launch_bounds__(256) pong_step_kernel(float* __restrict__ state, int32_t* __restrict__ tsteps,
-                                                        int64_t* __restrict__ tglob, float* __restrict__ ep_ret,
-                                                        float* __restrict__ ep_stats,
-                                                        const int64_t* __restrict__ env_ids,
-                                                        const int32_t* __restrict__ actions,
-                                                        const uint8_t* __restrict__ prev, uint8_t* __restrict__ out,
-                                                        float* __restrict__ reward, uint8_t* __restrict__ done_out,
-                                                        uint8_t* __restrict__ trunc_out, uint32_t seed, int max_steps,
-                                                        int k) {
-  const int e = blockIdx.x;
+struct PongIO {
+  float* state; int32_t* tsteps; int64_t* tglob; float* ep_ret; float* ep_stats; const int64_t* env_ids;
+  const uint8_t* prev; uint8_t* out; float* reward; uint8_t* done_out; uint8_t* trunc_out;
+  uint32_t seed; int max_steps; int k;
+};
+
+// One env step of env `e` by the whole workgroup: thread 0 runs the physics with action `a`, everyone renders.
+__device__ __forceinline__ void pong_step_block(const PongIO& io, int e, int a) {
   __shared__ PongState sh;
   __shared__ int sh_done;
   if (threadIdx.x == 0) {
-    float* sp = state + (size_t)e * 8;
+    float* sp = io.state + (size_t)e * 8;
     PongState s{sp[0], sp[1], sp[2], sp[3], sp[4], sp[5], sp[6], sp[7]};
-    const int64_t tg = tglob[e] + 1;
-    tglob[e] = tg;
-    const uint32_t id = (uint32_t)env_ids[e], st = (uint32_t)tg;
-    const int a = actions[e];
+    const int64_t tg = io.tglob[e] + 1;
+    io.tglob[e] = tg;
+    const uint32_t id = (uint32_t)io.env_ids[e], st = (uint32_t)tg;
     float dirn = 0.0f;
     if (a == 2 || a == 4) dirn = -1.0f;
     if (a == 3 || a == 5) dirn = 1.0f;
@@ -75,28 +72,28 @@ __global__ void __launch_bounds__(256) pong_step_kernel(float* __restrict__ stat
       s.sa = s.sa + (miss_o ? 1.0f : 0.0f);
       s.so = s.so + (miss_a ? 1.0f : 0.0f);
       s.bx = bx; s.by = by; s.vx = vx; s.vy = vy; s.pa = pa; s.po = po;
-      if (miss_a || miss_o) serve(s, seed, id, st, 200 + 4 * sub);
+      if (miss_a || miss_o) serve(s, io.seed, id, st, 200 + 4 * sub);
     }
     bool term = (s.sa >= WIN_SCORE) || (s.so >= WIN_SCORE);
-    int t = tsteps[e] + 1;
-    bool trunc = (t >= max_steps) && !term;
+    int t = io.tsteps[e] + 1;
+    bool trunc = (t >= io.max_steps) && !term;
     bool done = term || trunc;
-    float er = ep_ret[e] + rew;
-    reward[e] = rew;
-    done_out[e] = done;
-    trunc_out[e] = trunc;
+    float er = io.ep_ret[e] + rew;
+    io.reward[e] = rew;
+    io.done_out[e] = done;
+    io.trunc_out[e] = trunc;
     if (done) {
-      atomicAdd(&ep_stats[0], er);
-      atomicAdd(&ep_stats[1], 1.0f);
-      atomicAdd(&ep_stats[2], (float)t);
+      atomicAdd(&io.ep_stats[0], er);
+      atomicAdd(&io.ep_stats[1], 1.0f);
+      atomicAdd(&io.ep_stats[2], (float)t);
       const float mid = 0.5f * (FIELD_TOP + FIELD_BOT);
       s.pa = mid; s.po = mid; s.sa = 0.0f; s.so = 0.0f;
-      serve(s, seed, id, st, 100);
+      serve(s, io.seed, id, st, 100);
       t = 0;
       er = 0.0f;
     }
-    tsteps[e] = t;
-    ep_ret[e] = er;
+    io.tsteps[e] = t;
+    io.ep_ret[e] = er;
     sp[0] = s.bx; sp[1] = s.by; sp[2] = s.vx; sp[3] = s.vy; sp[4] = s.pa; sp[5] = s.po; sp[6] = s.sa; sp[7] = s.so;
     sh = s;
     sh_done = done;
@@ -104,10 +101,11 @@ __global__ void __launch_bounds__(256) pong_step_kernel(float* __restrict__ stat
   __syncthreads();
   const PongState s = sh;
   const bool done = sh_done != 0;
+  const int k = io.k;
   const int pa0 = (int)floorf(s.pa - PADDLE_H / 2), po0 = (int)floorf(s.po - PADDLE_H / 2);
   const int bx0 = (int)floorf(s.bx), by0 = (int)floorf(s.by);
-  const uint8_t* pv = prev + (size_t)e * k * FRAME;
-  uint8_t* ov = out + (size_t)e * k * FRAME;
+  const uint8_t* pv = io.prev + (size_t)e * k * FRAME;
+  uint8_t* ov = io.out + (size_t)e * k * FRAME;
   // shift the older frames (16-byte copies); a reset stack is rewritten below
   if (!done) {
     const uint4* src = reinterpret_cast<const uint4*>(pv + FRAME);
@@ -135,14 +133,119 @@ __global__ void __launch_bounds__(256) pong_step_kernel(float* __restrict__ stat
   }
 }
 
+__global__ void __launch_bounds__(256) pong_step_kernel(PongIO io, const int32_t* __restrict__ actions) {
+  pong_step_block(io, blockIdx.x, actions[blockIdx.x]);
+}
+
+// Rollout step of the native engine fused with the env: the policy/value head (z = h.Wh + bh, 512 -> A+1) of
+// env e, Gumbel-max sampling with the env-counter RNG key, logp / entropy / value, then the env step with the
+// sampled action -- one launch instead of head GEMM + sampling + env kernels. Wave 0 does the head.
+__global__ void __launch_bounds__(256) pong_policy_step_kernel(PongIO io, const u16* __restrict__ h, int hdim,
+                                                               const u16* __restrict__ Wh,
+                                                               const float* __restrict__ bh, int A,
+                                                               float* __restrict__ z_out, int32_t* __restrict__ act,
+                                                               float* __restrict__ logp, float* __restrict__ ent,
+                                                               float* __restrict__ vout, int key_shift,
+                                                               uint32_t pseed) {
+  const int e = blockIdx.x;
+  const int A1 = A + 1;
+  __shared__ int sh_act;
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    float acc[20];
+#pragma unroll
+    for (int j = 0; j < 20; ++j) acc[j] = 0.f;
+    for (int kb = lane * 8; kb < hdim; kb += 64 * 8) {
+      union { uint4 v; u16 x[8]; } hv;
+      hv.v = *reinterpret_cast<const uint4*>(h + (size_t)e * hdim + kb);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float hi = bf2f(hv.x[i]);
+        const u16* wr = Wh + (size_t)(kb + i) * A1;
+#pragma unroll
+        for (int j = 0; j < 20; ++j)
+          if (j < A1) acc[j] += hi * bf2f(wr[j]);
+      }
+    }
+    float zj = 0.f;
+#pragma unroll
+    for (int j = 0; j < 20; ++j) {
+      if (j < A1) {
+        const float v = wave_sum(acc[j]);
+        if (lane == j) zj = v + bh[j];
+      }
+    }
+    if (lane < A1) z_out[(size_t)e * A1 + lane] = zj;
+    const float value = __shfl(zj, A, 64);
+    // categorical head over lanes 0..A-1 (same maths as categorical_sample_kernel)
+    const bool on = lane < A;
+    const float z = on ? zj : -INFINITY;
+    const float m = wave_max(z);
+    const float ex = on ? expf(z - m) : 0.f;
+    const float lse = m + logf(wave_sum(ex));
+    const float lp = z - lse;
+    const float H = wave_sum(on ? -expf(lp) * lp : 0.f);
+    float g = -INFINITY;
+    if (on) {
+      const int64_t key = io.tglob[e] * ((int64_t)1 << key_shift) + io.env_ids[e];
+      g = z + (-logf(-logf(uniform_open(pseed, key, (uint32_t)lane))));
+    }
+    float best = g;
+    int bi = on ? lane : 1 << 30;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ob = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+    }
+    const float lpa = __shfl(lp, bi, 64);
+    if (lane == 0) {
+      act[e] = bi;
+      logp[e] = lpa;
+      ent[e] = H;
+      vout[e] = value;
+      sh_act = bi;
+    }
+  }
+  __syncthreads();
+  pong_step_block(io, e, sh_act);
+}
+
 }  // namespace aca
+
+static aca::PongIO make_pong_io(float* state, int32_t* t, int64_t* tg, float* ep_ret, float* ep_stats,
+                                const int64_t* ids, const uint8_t* prev, uint8_t* out, float* reward, uint8_t* done,
+                                uint8_t* trunc, uint32_t seed, int max_steps, int k) {
+  aca::PongIO io;
+  io.state = state; io.tsteps = t; io.tglob = tg; io.ep_ret = ep_ret; io.ep_stats = ep_stats; io.env_ids = ids;
+  io.prev = prev; io.out = out; io.reward = reward; io.done_out = done; io.trunc_out = trunc; io.seed = seed;
+  io.max_steps = max_steps; io.k = k;
+  return io;
+}
 
 extern "C" hipError_t aca_env_step_pong(float* state, int32_t* t, int64_t* tg, float* ep_ret, float* ep_stats,
                                         const int64_t* ids, const int32_t* actions, const uint8_t* prev,
                                         uint8_t* out, float* reward, uint8_t* done, uint8_t* trunc, uint32_t seed,
                                         int max_steps, int k, int N, hipStream_t stream) {
   if (N <= 0) return hipSuccess;
-  aca::pong_step_kernel<<<N, 256, 0, stream>>>(state, t, tg, ep_ret, ep_stats, ids, actions, prev, out, reward, done,
-                                               trunc, seed, max_steps, k);
+  aca::PongIO io = make_pong_io(state, t, tg, ep_ret, ep_stats, ids, prev, out, reward, done, trunc, seed, max_steps,
+                                k);
+  aca::pong_step_kernel<<<N, 256, 0, stream>>>(io, actions);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t aca_env_policy_step_pong(const uint16_t* h, int hdim, const uint16_t* Wh, const float* bh,
+                                               int A, float* z, int32_t* act, float* logp, float* ent, float* value,
+                                               int key_shift, uint32_t pseed, float* state, int32_t* t, int64_t* tg,
+                                               float* ep_ret, float* ep_stats, const int64_t* ids,
+                                               const uint8_t* prev, uint8_t* out, float* reward, uint8_t* done,
+                                               uint8_t* trunc, uint32_t seed, int max_steps, int k, int N,
+                                               hipStream_t stream) {
+  if (N <= 0) return hipSuccess;
+  if (A + 1 > 20 || A > 64 || hdim % 8) return hipErrorInvalidValue;
+  aca::PongIO io = make_pong_io(state, t, tg, ep_ret, ep_stats, ids, prev, out, reward, done, trunc, seed, max_steps,
+                                k);
+  aca::pong_policy_step_kernel<<<N, 256, 0, stream>>>(io, h, hdim, Wh, bh, A, z, act, logp, ent, value, key_shift,
+                                                      pseed);
   return hipGetLastError();
 }

@@ -12,6 +12,12 @@
 // Coefficients (c_ent, beta) are read from device scalars (annealed by the schedules without a host sync).
 // stats[0..6] = pg, kl, entropy, value_loss (unscaled mean), clipfrac, total actor loss, mean ratio.
 // One 1024-thread workgroup: the stats reduction is deterministic.
+//
+// A2C fast path (returns_mode 1 = n-step / 2 = GAE): the kernel first computes the targets and advantages of the
+// whole [T, N] rollout itself (same maths as returns.hip), the EV-before statistic (stats[7], Basic_AC/util.py:4-12)
+// and, with norm_adv, the population-std advantage normalisation (Basic_AC/run_AC.py:241) -- the returns, EV and
+// normalisation kernels of the generic path fold into this one launch. dbias (optional) receives the column sums of
+// dz = the gradient of the head bias, written directly (the gradient slab is clean).
 #include "common.h"
 
 namespace aca {
@@ -35,13 +41,78 @@ struct LossArgs {
   float* stats;
   int B, A;
   int gaussian;
+  // fused returns (A2C): rew/done [T, N], val [T+1, N]; ret/adv (global scratch [B]) are written then read back
+  int returns_mode;                     // 0: use ret/adv as given; 1: n-step (look-ahead L); 2: GAE(lambda)
+  const float* rew; const float* val; const uint8_t* dn;
+  int T, N, L;
+  float gamma, lam;
+  int norm_adv;
+  float* ret_w; float* adv_w;
+  float* dbias; int dbias_n;            // head bias gradient (A+1 columns: logits | value)
 };
 
 __global__ void __launch_bounds__(1024) ac_loss_kernel(LossArgs a) {
   __shared__ double sh[16];
   __shared__ float dls[64];
-  if (threadIdx.x < 64) dls[threadIdx.x] = 0.f;
+  __shared__ float dbs[64];
+  if (threadIdx.x < 64) { dls[threadIdx.x] = 0.f; dbs[threadIdx.x] = 0.f; }
   __syncthreads();
+  float adv_mean = 0.f, adv_inv = 1.f;
+  if (a.returns_mode) {
+    // ---- phase 0: targets / advantages of every (t, n), EV-before, normalisation constants
+    double s_r = 0, s_rr = 0, s_v = 0, s_vv = 0, s_rv = 0, s_a = 0, s_aa = 0;
+    for (int idx = threadIdx.x; idx < a.B; idx += blockDim.x) {
+      const int t = idx / a.N, n = idx - t * a.N;
+      float R;
+      if (a.returns_mode == 1) {
+        const int h = min(t + a.L, a.T);
+        float acc = 0.f, disc = 1.f;
+        bool alive = true;
+        for (int k = t; k < h; ++k) {
+          const int i = k * a.N + n;
+          acc += disc * a.rew[i];
+          disc *= a.gamma;
+          if (a.dn[i]) { alive = false; break; }
+        }
+        if (alive) acc += disc * a.val[h * a.N + n];
+        R = acc;
+      } else {
+        float last = 0.f, Rt = 0.f;
+        for (int k = a.T - 1; k >= t; --k) {
+          const int i = k * a.N + n;
+          const float nd = a.dn[i] ? 0.f : 1.f;
+          const float delta = a.rew[i] + a.gamma * a.val[i + a.N] * nd - a.val[i];
+          last = delta + a.gamma * a.lam * nd * last;
+        }
+        Rt = last + a.val[idx];
+        R = Rt;
+      }
+      const float v = a.val[idx];
+      const float A_ = R - v;
+      a.ret_w[idx] = R;
+      a.adv_w[idx] = A_;
+      s_r += R; s_rr += (double)R * R; s_v += v; s_vv += (double)v * v; s_rv += (double)R * v;
+      s_a += A_; s_aa += (double)A_ * A_;
+    }
+    s_r = block_sum_d(s_r, sh); s_rr = block_sum_d(s_rr, sh); s_v = block_sum_d(s_v, sh);
+    s_vv = block_sum_d(s_vv, sh); s_rv = block_sum_d(s_rv, sh); s_a = block_sum_d(s_a, sh);
+    s_aa = block_sum_d(s_aa, sh);
+    const double n = a.B;
+    if (threadIdx.x == 0) {
+      const double mr = s_r / n, mv = s_v / n;
+      const double vr = fmax(s_rr / n - mr * mr, 0.0), vv = fmax(s_vv / n - mv * mv, 0.0);
+      a.stats[7] = (float)((s_rv / n - mr * mv) / sqrt(vr * vv));
+    }
+    if (a.norm_adv) {
+      const double m = s_a / n;
+      const double var = fmax(s_aa / n - m * m, 0.0);
+      adv_mean = (float)m;
+      adv_inv = 1.0f / (1e-8f + (float)sqrt(var));
+    }
+    __syncthreads();  // ret_w / adv_w written above are read by other threads below
+  }
+  const float* advp = a.returns_mode ? a.adv_w : a.adv;
+  const float* retp = a.returns_mode ? a.ret_w : a.ret;
   const float invB = 1.0f / (float)a.B;
   const float c_ent = a.ent_coef ? *a.ent_coef : 0.f;
   const float beta = a.kl_coef ? *a.kl_coef : 0.f;
@@ -69,7 +140,7 @@ __global__ void __launch_bounds__(1024) ac_loss_kernel(LossArgs a) {
         H += 0.5f + HALF_LOG_2PI + ls;
       }
     }
-    const float lpo = a.logp_old[b], adv = a.adv[b];
+    const float lpo = a.logp_old[b], adv = (advp[b] - adv_mean) * adv_inv;
     float g_lpa;  // dL/dlpa (already divided by B)
     if (a.ppo_clip > 0.f) {
       const float ratio = expf(lpa - lpo);
@@ -98,7 +169,9 @@ __global__ void __launch_bounds__(1024) ac_loss_kernel(LossArgs a) {
         const float oh = (j == ab) ? 1.0f : 0.0f;
         const float lz = z[j] - lse, pj = expf(lz);
         const float g = g_lpa * (oh - pj) + c_ent * invB * pj * (lz + H);
-        dz[j] = f2bf(g);
+        const u16 gb = f2bf(g);
+        dz[j] = gb;
+        if (a.dbias) atomicAdd(&dbs[j], bf2f(gb));
       }
     } else {
       for (int j = 0; j < a.A; ++j) {
@@ -113,7 +186,7 @@ __global__ void __launch_bounds__(1024) ac_loss_kernel(LossArgs a) {
     }
     // critic
     if (a.value) {
-      const float v = a.value[(int64_t)b * a.ldv], R = a.ret[b];
+      const float v = a.value[(int64_t)b * a.ldv], R = retp[b];
       float d = v - R;
       float vl = d * d;
       float gv = 2.0f * d;
@@ -128,7 +201,9 @@ __global__ void __launch_bounds__(1024) ac_loss_kernel(LossArgs a) {
         }
       }
       s_vl += vl;
-      a.dvalue[(int64_t)b * a.lddv] = f2bf(a.vf_coef * gv * invB);
+      const u16 gvb = f2bf(a.vf_coef * gv * invB);
+      a.dvalue[(int64_t)b * a.lddv] = gvb;
+      if (a.dbias) atomicAdd(&dbs[a.A], bf2f(gvb));
     }
   }
   s_pg = block_sum_d(s_pg, sh);
@@ -139,6 +214,7 @@ __global__ void __launch_bounds__(1024) ac_loss_kernel(LossArgs a) {
   s_ratio = block_sum_d(s_ratio, sh);
   __syncthreads();
   if (a.gaussian && a.dlog_std && threadIdx.x < a.A) atomicAdd(&a.dlog_std[threadIdx.x], dls[threadIdx.x]);
+  if (a.dbias && threadIdx.x < a.dbias_n) a.dbias[threadIdx.x] += dbs[threadIdx.x];
   if (threadIdx.x == 0) {
     const double inv = 1.0 / a.B;
     a.stats[0] = (float)(s_pg * inv);
@@ -158,14 +234,20 @@ extern "C" hipError_t aca_ac_loss(const float* logits, int64_t ldl, const float*
                                   const float* logp_old, const float* adv, const float* ret, const float* v_old,
                                   const float* ent_coef, const float* kl_coef, float vf_coef, float ppo_clip,
                                   float v_clip, uint16_t* dlogits, int64_t lddl, uint16_t* dvalue, int64_t lddv,
-                                  float* dlog_std, float* stats, int B, int A, int gaussian, hipStream_t stream) {
-  if (A > 64) return hipErrorInvalidValue;
+                                  float* dlog_std, float* stats, int B, int A, int gaussian, int returns_mode,
+                                  const float* rew, const float* val, const uint8_t* dn, int T, int N, int L,
+                                  float gamma, float lam, int norm_adv, float* ret_w, float* adv_w, float* dbias,
+                                  int dbias_n, hipStream_t stream) {
+  if (A > 64 || dbias_n > 64) return hipErrorInvalidValue;
+  if (returns_mode && (T * N != B || !rew || !val || !dn || !ret_w || !adv_w)) return hipErrorInvalidValue;
   aca::LossArgs a;
   a.logits = logits; a.ldl = ldl; a.value = value; a.ldv = ldv; a.act_i = act_i; a.act_f = act_f;
   a.log_std = log_std; a.logp_old = logp_old; a.adv = adv; a.ret = ret; a.v_old = v_old; a.ent_coef = ent_coef;
   a.kl_coef = kl_coef; a.vf_coef = vf_coef; a.ppo_clip = ppo_clip; a.v_clip = v_clip; a.dlogits = dlogits;
   a.lddl = lddl; a.dvalue = dvalue; a.lddv = lddv; a.dlog_std = dlog_std; a.stats = stats; a.B = B; a.A = A;
   a.gaussian = gaussian;
+  a.returns_mode = returns_mode; a.rew = rew; a.val = val; a.dn = dn; a.T = T; a.N = N; a.L = L; a.gamma = gamma;
+  a.lam = lam; a.norm_adv = norm_adv; a.ret_w = ret_w; a.adv_w = adv_w; a.dbias = dbias; a.dbias_n = dbias_n;
   aca::ac_loss_kernel<<<1, 1024, 0, stream>>>(a);
   return hipGetLastError();
 }

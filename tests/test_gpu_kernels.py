@@ -347,3 +347,42 @@ def test_a2c_activation_reuse_is_exact(cuda):
     assert torch.allclose(res[0][2], res[1][2], rtol=1e-3, atol=1e-5)
     d0, d1 = res[0][0], res[1][0]
     assert (d0 - d1).norm() / d0.norm() < 0.05
+
+
+def test_fused_policy_env_step_matches_separate_kernels(cuda):
+    """env_policy_step_pong == head GEMM + categorical_sample_env + env_step_pong on the same inputs."""
+    from actor_critic_algs_on_tensorflow_amd import _native
+    from actor_critic_algs_on_tensorflow_amd import envs as E
+    ops = _native.require()
+    N, A = 16, 6
+    g = torch.Generator().manual_seed(5)
+    h = torch.relu(torch.randn(N, 512, generator=g)).to(torch.bfloat16).to(cuda)
+    Wh = (torch.randn(512 * (A + 1), generator=g) * 0.05).to(torch.bfloat16).to(cuda)
+    bh = torch.randn(A + 1, generator=g).to(cuda)
+    outs = []
+    for fused in (True, False):
+        env = E.make("PongNoFrameskip-v4", N, device=cuda, seed=3)
+        o0 = env.reset().clone()
+        o1 = torch.empty_like(o0)
+        act = torch.empty(N, dtype=torch.int32, device=cuda)
+        lp, en, val = (torch.empty(N, device=cuda) for _ in range(3))
+        z = torch.empty(N, A + 1, device=cuda)
+        rew = torch.empty(N, device=cuda)
+        dn, tr = (torch.empty(N, dtype=torch.uint8, device=cuda) for _ in range(2))
+        if fused:
+            ops.env_policy_step_pong(h, Wh, bh, z, act, lp, en, val, 20, 77, env.state, env.t, env.tg, env.ep_ret,
+                                     env.ep_stats, env.env_ids, o0, o1, rew, dn, tr, env.seed,
+                                     env.max_episode_steps, 4)
+        else:
+            z = (h.float() @ Wh.float().view(512, A + 1)) + bh
+            ops.categorical_sample_env(z[:, :A].contiguous(), env.tg, env.env_ids, 20, 77, act, lp, en, None)
+            val = z[:, A].clone()
+            env.step(act, prev_obs=o0, obs_out=o1, reward_out=rew, done_out=dn, trunc_out=tr)
+        outs.append((act.clone(), lp.clone(), en.clone(), val.clone(), o1.clone(), z.clone()))
+    (a0, l0, e0, v0, f0, z0), (a1, l1, e1, v1, f1, z1) = outs
+    assert torch.allclose(z0, z1, atol=2e-3)
+    same = a0 == a1
+    assert same.float().mean() >= 0.9
+    assert torch.allclose(l0[same], l1[same], atol=2e-3) and torch.allclose(e0, e1, atol=2e-3)
+    assert torch.allclose(v0, v1, atol=2e-3)
+    assert torch.equal(f0[same], f1[same])

@@ -16,7 +16,9 @@ backward  dWh += h^T dz ; dbh += colsum(dz)
           dW3 += dy3^T col3 ; dcol3 = dy3 W3 ; dy2 = col2im(dcol3) * (y2 > 0) (+ colsum -> db2)
           dW2 += dy2^T col2 ; dcol2 = dy2 W2 ; dy1 = col2im(dcol2) * (y1 > 0) (+ colsum -> db1)
           dW1 += dy1^T col1
-The column matrices ``col*`` are never materialised in the default (``implicit=True``) mode: the GEMM gathers its
+For rollout-sized batches (``fused_trunk_max_b``) conv1..conv3 run as ONE fused kernel (``cnn_fused.hip``: one env
+per workgroup, activations handed off through LDS, MFMA 16x16x32); y1/y2/y3 still land in the buffers above so the
+learner can reuse them. The column matrices ``col*`` are never materialised in the default (``implicit=True``) mode: the GEMM gathers its
 k-contiguous A rows (forward) or n-contiguous B rows (weight gradient) straight from the activation image
 (implicit im2col, ``gemm_impl.h``). ``implicit=False`` runs explicit im2col kernels + plain GEMMs (A/B reference).
 Weight gradients accumulate (split-K atomics) straight into the fp32 gradient slab of :class:`FlatParams` (zeroed
@@ -79,9 +81,11 @@ class _Bufs:
 class CNNEngine:
     """Explicit forward/backward of :class:`..models.policy.CNNActorCritic` over a :class:`FlatParams` slab."""
 
-    def __init__(self, model, flat, shadow, implicit=True):
+    def __init__(self, model, flat, shadow, implicit=True, fused_trunk_max_b=None):
         net = model.net
         self.implicit = implicit
+        # one workgroup per env: the fused trunk wins whenever the per-layer GEMMs are launch/latency bound
+        self.fused_trunk_max_b = 4096 if fused_trunk_max_b is None else fused_trunk_max_b
         self.model = model
         self.flat = flat
         self.shadow = shadow
@@ -133,7 +137,9 @@ class CNNEngine:
         B = b.B
         ws = self.ws
         b.obs = obs  # the conv1 weight gradient re-gathers its columns from the frames
-        if self.implicit:
+        if self.implicit and B <= self.fused_trunk_max_b:
+            G.cnn_trunk_fwd(obs, self.sW1, self.b1, self.sW2, self.b2, self.sW3, self.b3, b.y1, b.y2, b.y3)
+        elif self.implicit:
             G.gemm(obs, 0, True, self.sW1, 256, True, b.y1, 32, 1, B * 400, 32, 256, bias=self.b1, relu=True,
                    workspace=ws, ga=[1, B, 4, 84, 84, 8, 8, 4], ga_scale=1.0 / 255.0)
             G.gemm(b.y1, 0, True, self.sW2, 512, True, b.y2, 64, 1, B * 81, 64, 512, bias=self.b2, relu=True,

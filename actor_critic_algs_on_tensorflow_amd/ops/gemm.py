@@ -224,6 +224,11 @@ def im2col_nhwc_ref(x, B, H, W, C, kh, kw, s):
     return u.reshape(B * L, kh * kw * C)
 
 
+def cnn_trunk_fwd(obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale=1.0 / 255.0):
+    """Fused Nature-CNN conv1..conv3 (one env per workgroup, activations through LDS; ``cnn_fused.hip``)."""
+    _native.require().cnn_trunk_fwd(obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, float(scale))
+
+
 def col2im_nhwc(dcol, ymask, dx, colsum, B, H, W, C, kh, kw, s):
     _native.require().col2im_nhwc(dcol, ymask, dx, colsum, B, H, W, C, kh, kw, s)
 

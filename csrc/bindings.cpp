@@ -61,6 +61,8 @@ hipError_t aca_ac_loss(const float*, int64_t, const float*, int64_t, const int32
                        float, uint16_t*, int64_t, uint16_t*, int64_t, float*, float*, int, int, int, int,
                        const float*, const float*, const uint8_t*, int, int, int, float, float, int, float*, float*,
                        float*, int, hipStream_t);
+hipError_t aca_cnn_trunk_fwd(const uint8_t*, const uint16_t*, const float*, const uint16_t*, const float*,
+                             const uint16_t*, const float*, uint16_t*, uint16_t*, uint16_t*, int, float, hipStream_t);
 }
 
 namespace {
@@ -482,6 +484,29 @@ int64_t gemm_effective_splits(int64_t K, int64_t bk, int64_t splits) {
   return aca_gemm_effective_splits((int)K, (int)bk, (int)splits);
 }
 
+// Fused Nature-CNN trunk (conv1..conv3 of one env per workgroup, csrc/kernels/cnn_fused.hip). Shapes are fixed by
+// the kernel: obs [B, 4, 84, 84] uint8, W1 [32, 256] (OIHW), W2 [64, 512] / W3 [64, 576] (OHWI), y1 [B*400, 32],
+// y2 [B*81, 64], y3 [B*49, 64]; all 16-byte aligned (the kernel uses 16-byte vector accesses).
+void cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, Tensor y1,
+                   Tensor y2, Tensor y3, double scale) {
+  need(obs, at::kByte, "obs");
+  for (auto* w : {&W1, &W2, &W3, &y1, &y2, &y3}) need(*w, at::kBFloat16, "trunk bf16 operand");
+  for (auto* b : {&b1, &b2, &b3}) need(*b, at::kFloat, "trunk bias");
+  TORCH_CHECK(obs.numel() % (4 * 84 * 84) == 0, "cnn_trunk_fwd: obs must be [B, 4, 84, 84]");
+  const int64_t B = obs.numel() / (4 * 84 * 84);
+  TORCH_CHECK(W1.numel() == 32 * 256 && W2.numel() == 64 * 512 && W3.numel() == 64 * 576,
+              "cnn_trunk_fwd: weights must be Nature-CNN conv1..3");
+  TORCH_CHECK(b1.numel() == 32 && b2.numel() == 64 && b3.numel() == 64, "cnn_trunk_fwd: bias sizes");
+  TORCH_CHECK(y1.numel() >= B * 400 * 32 && y2.numel() >= B * 81 * 64 && y3.numel() >= B * 49 * 64,
+              "cnn_trunk_fwd: activation buffers too small");
+  for (auto* t : {&obs, &W1, &W2, &W3})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "cnn_trunk_fwd: operands must be 16B aligned");
+  check(aca_cnn_trunk_fwd(ptr<uint8_t>(obs), ptr<uint16_t>(W1), ptr<float>(b1), ptr<uint16_t>(W2), ptr<float>(b2),
+                          ptr<uint16_t>(W3), ptr<float>(b3), ptr<uint16_t>(y1), ptr<uint16_t>(y2), ptr<uint16_t>(y3),
+                          (int)B, (float)scale, cur_stream(obs)),
+        "cnn_trunk_fwd");
+}
+
 void im2col_u8(Tensor x, Tensor col, int64_t kh, int64_t kw, int64_t s, double scale) {
   need(x, at::kByte, "x");
   need(col, at::kBFloat16, "col");
@@ -628,6 +653,8 @@ TORCH_LIBRARY(acamd, m) {
         "int tile, int bk, int splits, Tensor? ws, Tensor? tickets, int[] ga, float ga_scale, int[] gb, "
         "float gb_scale) -> ()");
   m.def("gemm_effective_splits(int K, int bk, int splits) -> int", &gemm_effective_splits);
+  m.def("cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, Tensor y1, "
+        "Tensor y2, Tensor y3, float scale) -> ()");
   m.def("im2col_u8(Tensor x, Tensor col, int kh, int kw, int s, float scale) -> ()");
   m.def("im2col_nhwc(Tensor x, Tensor col, int B, int H, int W, int C, int kh, int kw, int s) -> ()");
   m.def("col2im_nhwc(Tensor dcol, Tensor ymask, Tensor dx, Tensor? colsum, int B, int H, int W, int C, int kh, "
@@ -660,6 +687,7 @@ TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
   m.impl("rmsprop_step", &rmsprop_step);
   m.impl("cast_bf16", &cast_bf16);
   m.impl("gemm", &gemm);
+  m.impl("cnn_trunk_fwd", &cnn_trunk_fwd);
   m.impl("im2col_u8", &im2col_u8);
   m.impl("im2col_nhwc", &im2col_nhwc);
   m.impl("col2im_nhwc", &col2im_nhwc);

@@ -99,6 +99,27 @@ __device__ __forceinline__ double block_sum_d(double v, double* sh) {
   return r;
 }
 
+// Block-wide sums of N doubles with ONE barrier pair (wave shuffles, then one cross-wave pass); `sh` must hold
+// 16 * N doubles. Results valid in every thread.
+template <int N>
+__device__ __forceinline__ void block_sum_multi(double (&v)[N], double* sh) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = wave_sum_d(v[i]);
+  __syncthreads();
+  if (lane == 0)
+#pragma unroll
+    for (int i = 0; i < N; ++i) sh[wid * N + i] = v[i];
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    double r = 0.0;
+    for (int w = 0; w < nw; ++w) r += sh[w * N + i];
+    v[i] = r;
+  }
+  __syncthreads();
+}
+
 // Last-arriver ticket (Guideline 16 counter form): every wave drains its stores, the block releases at agent
 // scope and takes a ticket; returns true in every thread of the block that arrived last. The caller then reads
 // the other blocks' results with plain loads (this function already performed the acquire).

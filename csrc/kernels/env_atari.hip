@@ -37,83 +37,108 @@ struct PongIO {
   uint32_t seed; int max_steps; int k;
 };
 
-// One env step of env `e` by the whole workgroup: thread 0 runs the physics with action `a`, everyone renders.
-__device__ __forceinline__ void pong_step_block(const PongIO& io, int e, int a) {
-  __shared__ PongState sh;
-  __shared__ int sh_done;
-  if (threadIdx.x == 0) {
-    float* sp = io.state + (size_t)e * 8;
-    PongState s{sp[0], sp[1], sp[2], sp[3], sp[4], sp[5], sp[6], sp[7]};
-    const int64_t tg = io.tglob[e] + 1;
-    io.tglob[e] = tg;
-    const uint32_t id = (uint32_t)io.env_ids[e], st = (uint32_t)tg;
-    float dirn = 0.0f;
-    if (a == 2 || a == 4) dirn = -1.0f;
-    if (a == 3 || a == 5) dirn = 1.0f;
-    float rew = 0.0f;
-    const float lo = FIELD_TOP + PADDLE_H / 2, hi = FIELD_BOT - PADDLE_H / 2;
-    for (int sub = 0; sub < 4; ++sub) {
-      float bx = s.bx, by = s.by, vx = s.vx, vy = s.vy, pa = s.pa, po = s.po;
-      pa = clampf(pa + dirn * AGENT_SPEED, lo, hi);
-      po = clampf(po + clampf(by + 1.0f - po, -OPP_SPEED, OPP_SPEED), lo, hi);
-      bx = bx + vx;
-      by = by + vy;
-      if (by < FIELD_TOP) { by = 2 * FIELD_TOP - by; vy = -vy; }
-      if (by > FIELD_BOT - BALL) { by = 2 * (FIELD_BOT - BALL) - by; vy = -vy; }
-      bool hit_a = (vx > 0) && (bx + BALL >= AGENT_X) && (bx + BALL - vx < AGENT_X) &&
-                   (fabsf(by + 1.0f - pa) <= PADDLE_H / 2 + 1.0f);
-      if (hit_a) { vy = clampf(vy + 0.25f * (by + 1.0f - pa), -2.0f, 2.0f); bx = AGENT_X - BALL; vx = -vx; }
-      const float edge = OPP_X + PADDLE_W;
-      bool hit_o = (vx < 0) && (bx <= edge) && (bx - vx > edge) && (fabsf(by + 1.0f - po) <= PADDLE_H / 2 + 1.0f);
-      if (hit_o) { vy = clampf(vy + 0.25f * (by + 1.0f - po), -2.0f, 2.0f); bx = edge; vx = -vx; }
-      bool miss_a = bx > (float)PW;
-      bool miss_o = bx < -BALL;
-      rew = rew + (miss_o ? 1.0f : 0.0f) - (miss_a ? 1.0f : 0.0f);
-      s.sa = s.sa + (miss_o ? 1.0f : 0.0f);
-      s.so = s.so + (miss_a ? 1.0f : 0.0f);
-      s.bx = bx; s.by = by; s.vx = vx; s.vy = vy; s.pa = pa; s.po = po;
-      if (miss_a || miss_o) serve(s, io.seed, id, st, 200 + 4 * sub);
-    }
-    bool term = (s.sa >= WIN_SCORE) || (s.so >= WIN_SCORE);
-    int t = io.tsteps[e] + 1;
-    bool trunc = (t >= io.max_steps) && !term;
-    bool done = term || trunc;
-    float er = io.ep_ret[e] + rew;
-    io.reward[e] = rew;
-    io.done_out[e] = done;
-    io.trunc_out[e] = trunc;
-    if (done) {
-      atomicAdd(&io.ep_stats[0], er);
-      atomicAdd(&io.ep_stats[1], 1.0f);
-      atomicAdd(&io.ep_stats[2], (float)t);
-      const float mid = 0.5f * (FIELD_TOP + FIELD_BOT);
-      s.pa = mid; s.po = mid; s.sa = 0.0f; s.so = 0.0f;
-      serve(s, io.seed, id, st, 100);
-      t = 0;
-      er = 0.0f;
-    }
-    io.tsteps[e] = t;
-    io.ep_ret[e] = er;
-    sp[0] = s.bx; sp[1] = s.by; sp[2] = s.vx; sp[3] = s.vy; sp[4] = s.pa; sp[5] = s.po; sp[6] = s.sa; sp[7] = s.so;
-    sh = s;
-    sh_done = done;
+// Result of advancing env `e` by one agent step (4 physics sub-steps) -- computed from global state without writing
+// anything, so the fused rollout kernel can evaluate all three paddle directions while the policy is still sampling.
+struct PongOut {
+  PongState s;
+  float rew, er;
+  int t, done, trunc;
+};
+
+__device__ __forceinline__ int pong_dir_index(int a) {  // 0: up, 1: stay, 2: down (dirn = index - 1)
+  return (a == 2 || a == 4) ? 0 : ((a == 3 || a == 5) ? 2 : 1);
+}
+
+__device__ __forceinline__ PongOut pong_advance(const PongIO& io, int e, float dirn) {
+  const float* sp = io.state + (size_t)e * 8;
+  PongState s{sp[0], sp[1], sp[2], sp[3], sp[4], sp[5], sp[6], sp[7]};
+  const int64_t tg = io.tglob[e] + 1;
+  const uint32_t id = (uint32_t)io.env_ids[e], st = (uint32_t)tg;
+  float rew = 0.0f;
+  const float lo = FIELD_TOP + PADDLE_H / 2, hi = FIELD_BOT - PADDLE_H / 2;
+  for (int sub = 0; sub < 4; ++sub) {
+    float bx = s.bx, by = s.by, vx = s.vx, vy = s.vy, pa = s.pa, po = s.po;
+    pa = clampf(pa + dirn * AGENT_SPEED, lo, hi);
+    po = clampf(po + clampf(by + 1.0f - po, -OPP_SPEED, OPP_SPEED), lo, hi);
+    bx = bx + vx;
+    by = by + vy;
+    if (by < FIELD_TOP) { by = 2 * FIELD_TOP - by; vy = -vy; }
+    if (by > FIELD_BOT - BALL) { by = 2 * (FIELD_BOT - BALL) - by; vy = -vy; }
+    bool hit_a = (vx > 0) && (bx + BALL >= AGENT_X) && (bx + BALL - vx < AGENT_X) &&
+                 (fabsf(by + 1.0f - pa) <= PADDLE_H / 2 + 1.0f);
+    if (hit_a) { vy = clampf(vy + 0.25f * (by + 1.0f - pa), -2.0f, 2.0f); bx = AGENT_X - BALL; vx = -vx; }
+    const float edge = OPP_X + PADDLE_W;
+    bool hit_o = (vx < 0) && (bx <= edge) && (bx - vx > edge) && (fabsf(by + 1.0f - po) <= PADDLE_H / 2 + 1.0f);
+    if (hit_o) { vy = clampf(vy + 0.25f * (by + 1.0f - po), -2.0f, 2.0f); bx = edge; vx = -vx; }
+    bool miss_a = bx > (float)PW;
+    bool miss_o = bx < -BALL;
+    rew = rew + (miss_o ? 1.0f : 0.0f) - (miss_a ? 1.0f : 0.0f);
+    s.sa = s.sa + (miss_o ? 1.0f : 0.0f);
+    s.so = s.so + (miss_a ? 1.0f : 0.0f);
+    s.bx = bx; s.by = by; s.vx = vx; s.vy = vy; s.pa = pa; s.po = po;
+    if (miss_a || miss_o) serve(s, io.seed, id, st, 200 + 4 * sub);
   }
-  __syncthreads();
-  const PongState s = sh;
-  const bool done = sh_done != 0;
+  PongOut r;
+  const bool term = (s.sa >= WIN_SCORE) || (s.so >= WIN_SCORE);
+  r.t = io.tsteps[e] + 1;
+  r.trunc = (r.t >= io.max_steps) && !term;
+  r.done = term || r.trunc;
+  r.rew = rew;
+  r.er = io.ep_ret[e] + rew;
+  if (r.done) {
+    const float mid = 0.5f * (FIELD_TOP + FIELD_BOT);
+    s.pa = mid; s.po = mid; s.sa = 0.0f; s.so = 0.0f;
+    serve(s, io.seed, id, st, 100);
+  }
+  r.s = s;
+  return r;
+}
+
+// Writes the chosen outcome back (one thread).
+__device__ __forceinline__ void pong_commit(const PongIO& io, int e, const PongOut& r) {
+  io.tglob[e] = io.tglob[e] + 1;
+  io.reward[e] = r.rew;
+  io.done_out[e] = r.done;
+  io.trunc_out[e] = r.trunc;
+  if (r.done) {
+    atomicAdd(&io.ep_stats[0], r.er);
+    atomicAdd(&io.ep_stats[1], 1.0f);
+    atomicAdd(&io.ep_stats[2], (float)r.t);
+  }
+  io.tsteps[e] = r.done ? 0 : r.t;
+  io.ep_ret[e] = r.done ? 0.0f : r.er;
+  float* sp = io.state + (size_t)e * 8;
+  const PongState& s = r.s;
+  sp[0] = s.bx; sp[1] = s.by; sp[2] = s.vx; sp[3] = s.vy; sp[4] = s.pa; sp[5] = s.po; sp[6] = s.sa; sp[7] = s.so;
+}
+
+// Frame-stack shift out[0..k-2] = prev[1..k-1] by threads [t0, t0 + nt): independent of the action, so the fused
+// kernel overlaps it with the policy head. All loads of a thread are issued before its stores (6 x 16 B in flight).
+__device__ __forceinline__ void pong_shift(const PongIO& io, int e, int t0, int nt) {
+  const int k = io.k;
+  const uint4* src = reinterpret_cast<const uint4*>(io.prev + (size_t)e * k * FRAME + FRAME);
+  uint4* dst = reinterpret_cast<uint4*>(io.out + (size_t)e * k * FRAME);
+  const int n16 = (k - 1) * FRAME / 16;
+  const int tid = threadIdx.x - t0;
+  for (int j0 = tid; j0 < n16; j0 += 8 * nt) {
+    uint4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (j0 + u * nt < n16) v[u] = src[j0 + u * nt];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (j0 + u * nt < n16) dst[j0 + u * nt] = v[u];
+  }
+}
+
+// Render the newest frame (441 chunks of 16 pixels); a finished env gets k copies of its first frame (Framer padding,
+// Basic_AC/run_AC.py:37-40) -- these stores overwrite the shifted frames, so call after a barrier that follows
+// pong_shift.
+__device__ __forceinline__ void pong_render(const PongIO& io, int e, const PongState& s, bool done) {
   const int k = io.k;
   const int pa0 = (int)floorf(s.pa - PADDLE_H / 2), po0 = (int)floorf(s.po - PADDLE_H / 2);
   const int bx0 = (int)floorf(s.bx), by0 = (int)floorf(s.by);
-  const uint8_t* pv = io.prev + (size_t)e * k * FRAME;
   uint8_t* ov = io.out + (size_t)e * k * FRAME;
-  // shift the older frames (16-byte copies); a reset stack is rewritten below
-  if (!done) {
-    const uint4* src = reinterpret_cast<const uint4*>(pv + FRAME);
-    uint4* dst = reinterpret_cast<uint4*>(ov);
-    const int n16 = (k - 1) * FRAME / 16;
-    for (int j = threadIdx.x; j < n16; j += blockDim.x) dst[j] = src[j];
-  }
-  // render the newest frame: 441 chunks of 16 pixels
   for (int c = threadIdx.x; c < FRAME / 16; c += blockDim.x) {
     union { uint4 v; uint8_t b[16]; } px;
 #pragma unroll
@@ -126,20 +151,33 @@ __device__ __forceinline__ void pong_step_block(const PongIO& io, int e, int a) 
       if (x >= bx0 && x < bx0 + (int)BALL && y >= by0 && y < by0 + (int)BALL) v = BALL_C;
       px.b[q] = v;
     }
-    uint4* dst = reinterpret_cast<uint4*>(ov + (size_t)(k - 1) * FRAME);
-    dst[c] = px.v;
+    reinterpret_cast<uint4*>(ov + (size_t)(k - 1) * FRAME)[c] = px.v;
     if (done)
       for (int s2 = 0; s2 < k - 1; ++s2) reinterpret_cast<uint4*>(ov + (size_t)s2 * FRAME)[c] = px.v;
   }
 }
 
+// One env step per workgroup with known actions: thread 0 runs the physics while the others shift the stack.
 __global__ void __launch_bounds__(256) pong_step_kernel(PongIO io, const int32_t* __restrict__ actions) {
-  pong_step_block(io, blockIdx.x, actions[blockIdx.x]);
+  const int e = blockIdx.x;
+  __shared__ PongOut sh;
+  if (threadIdx.x == 0) {
+    const int a = actions[e];
+    sh = pong_advance(io, e, (float)(pong_dir_index(a) - 1));
+    pong_commit(io, e, sh);
+  }
+  pong_shift(io, e, 0, blockDim.x);
+  __syncthreads();
+  const PongOut r = sh;
+  pong_render(io, e, r.s, r.done != 0);
 }
 
 // Rollout step of the native engine fused with the env: the policy/value head (z = h.Wh + bh, 512 -> A+1) of
 // env e, Gumbel-max sampling with the env-counter RNG key, logp / entropy / value, then the env step with the
-// sampled action -- one launch instead of head GEMM + sampling + env kernels. Wave 0 does the head.
+// sampled action -- one launch instead of head GEMM + sampling + env kernels. Critical path = the head only:
+// wave 0 computes the head and samples, meanwhile wave 1 (lanes 0..2) advances the physics for all three paddle
+// directions and waves 1..3 shift the frame stack; after one barrier the sampled direction's outcome is committed
+// and the newest frame rendered.
 __global__ void __launch_bounds__(256) pong_policy_step_kernel(PongIO io, const u16* __restrict__ h, int hdim,
                                                                const u16* __restrict__ Wh,
                                                                const float* __restrict__ bh, int A,
@@ -150,8 +188,10 @@ __global__ void __launch_bounds__(256) pong_policy_step_kernel(PongIO io, const 
   const int e = blockIdx.x;
   const int A1 = A + 1;
   __shared__ int sh_act;
+  __shared__ PongOut cand[3];
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
+    const int64_t key = io.tglob[e] * ((int64_t)1 << key_shift) + io.env_ids[e];  // pre-step counter
     float acc[20];
 #pragma unroll
     for (int j = 0; j < 20; ++j) acc[j] = 0.f;
@@ -186,10 +226,7 @@ __global__ void __launch_bounds__(256) pong_policy_step_kernel(PongIO io, const 
     const float lp = z - lse;
     const float H = wave_sum(on ? -expf(lp) * lp : 0.f);
     float g = -INFINITY;
-    if (on) {
-      const int64_t key = io.tglob[e] * ((int64_t)1 << key_shift) + io.env_ids[e];
-      g = z + (-logf(-logf(uniform_open(pseed, key, (uint32_t)lane))));
-    }
+    if (on) g = z + (-logf(-logf(uniform_open(pseed, key, (uint32_t)lane))));
     float best = g;
     int bi = on ? lane : 1 << 30;
 #pragma unroll
@@ -206,9 +243,14 @@ __global__ void __launch_bounds__(256) pong_policy_step_kernel(PongIO io, const 
       vout[e] = value;
       sh_act = bi;
     }
+  } else {
+    if (threadIdx.x < 64 + 3) cand[threadIdx.x - 64] = pong_advance(io, e, (float)((int)threadIdx.x - 65));
+    pong_shift(io, e, 64, blockDim.x - 64);
   }
   __syncthreads();
-  pong_step_block(io, e, sh_act);
+  const PongOut& r = cand[pong_dir_index(sh_act)];
+  if (threadIdx.x == 0) pong_commit(io, e, r);
+  pong_render(io, e, r.s, r.done != 0);
 }
 
 }  // namespace aca

@@ -52,9 +52,12 @@ struct LossArgs {
 };
 
 __global__ void __launch_bounds__(1024) ac_loss_kernel(LossArgs a) {
-  __shared__ double sh[16];
+  __shared__ double sh[16 * 8];
   __shared__ float dls[64];
   __shared__ float dbs[64];
+  float dbp[21];  // this thread's partial column sums of dz (head-bias gradient), A + 1 <= 21
+#pragma unroll
+  for (int j = 0; j < 21; ++j) dbp[j] = 0.f;
   if (threadIdx.x < 64) { dls[threadIdx.x] = 0.f; dbs[threadIdx.x] = 0.f; }
   __syncthreads();
   float adv_mean = 0.f, adv_inv = 1.f;
@@ -94,9 +97,9 @@ __global__ void __launch_bounds__(1024) ac_loss_kernel(LossArgs a) {
       s_r += R; s_rr += (double)R * R; s_v += v; s_vv += (double)v * v; s_rv += (double)R * v;
       s_a += A_; s_aa += (double)A_ * A_;
     }
-    s_r = block_sum_d(s_r, sh); s_rr = block_sum_d(s_rr, sh); s_v = block_sum_d(s_v, sh);
-    s_vv = block_sum_d(s_vv, sh); s_rv = block_sum_d(s_rv, sh); s_a = block_sum_d(s_a, sh);
-    s_aa = block_sum_d(s_aa, sh);
+    double red[7] = {s_r, s_rr, s_v, s_vv, s_rv, s_a, s_aa};
+    block_sum_multi<7>(red, sh);
+    s_r = red[0]; s_rr = red[1]; s_v = red[2]; s_vv = red[3]; s_rv = red[4]; s_a = red[5]; s_aa = red[6];
     const double n = a.B;
     if (threadIdx.x == 0) {
       const double mr = s_r / n, mv = s_v / n;
@@ -171,7 +174,9 @@ __global__ void __launch_bounds__(1024) ac_loss_kernel(LossArgs a) {
         const float g = g_lpa * (oh - pj) + c_ent * invB * pj * (lz + H);
         const u16 gb = f2bf(g);
         dz[j] = gb;
-        if (a.dbias) atomicAdd(&dbs[j], bf2f(gb));
+#pragma unroll
+        for (int q = 0; q < 21; ++q)
+          if (q == j) dbp[q] += bf2f(gb);
       }
     } else {
       for (int j = 0; j < a.A; ++j) {
@@ -203,15 +208,26 @@ __global__ void __launch_bounds__(1024) ac_loss_kernel(LossArgs a) {
       s_vl += vl;
       const u16 gvb = f2bf(a.vf_coef * gv * invB);
       a.dvalue[(int64_t)b * a.lddv] = gvb;
-      if (a.dbias) atomicAdd(&dbs[a.A], bf2f(gvb));
+#pragma unroll
+      for (int q = 0; q < 21; ++q)
+        if (q == a.A) dbp[q] += bf2f(gvb);
     }
   }
-  s_pg = block_sum_d(s_pg, sh);
-  s_kl = block_sum_d(s_kl, sh);
-  s_H = block_sum_d(s_H, sh);
-  s_vl = block_sum_d(s_vl, sh);
-  s_cf = block_sum_d(s_cf, sh);
-  s_ratio = block_sum_d(s_ratio, sh);
+  {
+    double red[6] = {s_pg, s_kl, s_H, s_vl, s_cf, s_ratio};
+    block_sum_multi<6>(red, sh);
+    s_pg = red[0]; s_kl = red[1]; s_H = red[2]; s_vl = red[3]; s_cf = red[4]; s_ratio = red[5];
+  }
+  if (a.dbias) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int q = 0; q < 21; ++q) {
+      if (q < a.dbias_n) {
+        const float v = wave_sum(dbp[q]);
+        if (lane == 0) atomicAdd(&dbs[q], v);
+      }
+    }
+  }
   __syncthreads();
   if (a.gaussian && a.dlog_std && threadIdx.x < a.A) atomicAdd(&a.dlog_std[threadIdx.x], dls[threadIdx.x]);
   if (a.dbias && threadIdx.x < a.dbias_n) a.dbias[threadIdx.x] += dbs[threadIdx.x];
@@ -238,7 +254,7 @@ extern "C" hipError_t aca_ac_loss(const float* logits, int64_t ldl, const float*
                                   const float* rew, const float* val, const uint8_t* dn, int T, int N, int L,
                                   float gamma, float lam, int norm_adv, float* ret_w, float* adv_w, float* dbias,
                                   int dbias_n, hipStream_t stream) {
-  if (A > 64 || dbias_n > 64) return hipErrorInvalidValue;
+  if (A > 64 || dbias_n > 21) return hipErrorInvalidValue;
   if (returns_mode && (T * N != B || !rew || !val || !dn || !ret_w || !adv_w)) return hipErrorInvalidValue;
   aca::LossArgs a;
   a.logits = logits; a.ldl = ldl; a.value = value; a.ldv = ldv; a.act_i = act_i; a.act_f = act_f;

@@ -262,8 +262,8 @@ def test_ac_loss_kernel_matches_autograd(cuda, ppo):
 
 
 # ------------------------------------------------------------------------------------------------------ engine
-@pytest.mark.parametrize("implicit", [True, False])
-def test_cnn_engine_matches_autograd(cuda, implicit):
+@pytest.mark.parametrize("implicit,fused", [(True, True), (True, False), (False, False)])
+def test_cnn_engine_matches_autograd(cuda, implicit, fused):
     """Full native forward + loss + backward of the Atari CNN vs fp32 autograd on the same parameters."""
     from actor_critic_algs_on_tensorflow_amd.algos import losses as L
     from actor_critic_algs_on_tensorflow_amd.algos.engine import CNNEngine
@@ -279,7 +279,7 @@ def test_cnn_engine_matches_autograd(cuda, implicit):
             m.bias.uniform_(-0.05, 0.1)
     flat = FlatParams(model.param_groups(), cuda)
     shadow = flat.data.to(torch.bfloat16)
-    eng = CNNEngine(model, flat, shadow, implicit=implicit)
+    eng = CNNEngine(model, flat, shadow, implicit=implicit, fused_trunk_max_b=None if fused else 0)
     obs = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device=cuda)
     b = eng.bufs(B, with_grad=True)
     z = eng.forward(obs, b).clone()
@@ -308,6 +308,32 @@ def test_cnn_engine_matches_autograd(cuda, implicit):
         g = flat.grad[off:off + p.numel()].view_as(p)
         err = (g - pr.grad).norm() / (pr.grad.norm() + 1e-12)
         assert err < 0.05, (name, float(err))
+
+
+def test_cnn_trunk_fused_matches_layers(cuda):
+    """Fused conv1..conv3 kernel vs an fp32 PyTorch conv stack fed the same bf16-rounded inputs per layer."""
+    from actor_critic_algs_on_tensorflow_amd.ops import gemm as G
+    import torch.nn.functional as F
+    torch.manual_seed(1)
+    B = 37
+    obs = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device=cuda)
+    W1 = (torch.randn(32, 4, 8, 8, device=cuda) * 0.05).to(torch.bfloat16)          # OIHW
+    W2 = (torch.randn(64, 4, 4, 32, device=cuda) * 0.05).to(torch.bfloat16)         # OHWI
+    W3 = (torch.randn(64, 3, 3, 64, device=cuda) * 0.05).to(torch.bfloat16)
+    b1, b2, b3 = (torch.rand(n, device=cuda) * 0.1 - 0.02 for n in (32, 64, 64))
+    y1 = torch.empty(B * 400, 32, dtype=torch.bfloat16, device=cuda)
+    y2 = torch.empty(B * 81, 64, dtype=torch.bfloat16, device=cuda)
+    y3 = torch.empty(B * 49, 64, dtype=torch.bfloat16, device=cuda)
+    G.cnn_trunk_fwd(obs, W1.reshape(32, 256), b1, W2.reshape(64, 512), b2, W3.reshape(64, 576), b3, y1, y2, y3)
+    x = (obs.float() / 255.0).to(torch.bfloat16).float()
+    r1 = F.relu(F.conv2d(x, W1.float(), b1, stride=4))                                 # [B, 32, 20, 20]
+    assert torch.allclose(y1.float().view(B, 20, 20, 32).permute(0, 3, 1, 2), r1, rtol=1e-2, atol=1e-2)
+    x2 = y1.float().view(B, 20, 20, 32).permute(0, 3, 1, 2)
+    r2 = F.relu(F.conv2d(x2, W2.float().permute(0, 3, 1, 2), b2, stride=2))
+    assert torch.allclose(y2.float().view(B, 9, 9, 64).permute(0, 3, 1, 2), r2, rtol=1e-2, atol=1e-2)
+    x3 = y2.float().view(B, 9, 9, 64).permute(0, 3, 1, 2)
+    r3 = F.relu(F.conv2d(x3, W3.float().permute(0, 3, 1, 2), b3, stride=1))
+    assert torch.allclose(y3.float().view(B, 7, 7, 64).permute(0, 3, 1, 2), r3, rtol=1e-2, atol=1e-2)
 
 
 def test_trainer_native_graph_updates(cuda):

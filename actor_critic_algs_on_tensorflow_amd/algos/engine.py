@@ -13,8 +13,10 @@ backward  dWh += h^T dz ; dbh += colsum(dz)
           dh  = (dz Wh^T) * (h > 0)             (+ colsum -> dbfc)
           dWfc += y3^T dh
           dy3 = (dh Wfc^T) * (y3 > 0)           (+ per-channel colsum -> db3)
-          dW3 += dy3^T col3 ; dcol3 = dy3 W3 ; dy2 = col2im(dcol3) * (y2 > 0) (+ colsum -> db2)
-          dW2 += dy2^T col2 ; dcol2 = dy2 W2 ; dy1 = col2im(dcol2) * (y1 > 0) (+ colsum -> db1)
+          dW3 += dy3^T col3 ; dy2 = conv_transpose(dy3, W3) * (y2 > 0)       (+ colsum -> db2)
+          dW2 += dy2^T col2 ; dy1 = conv_transpose(dy2, W2) * (y1 > 0)       (+ colsum -> db1)
+          (the transposed convs are GEMMs whose A rows are gathered from dy on the stride grid and whose B is the
+          OHWI weight read as [(i, j, o)][c]; ``tconv_dgrad=False`` materialises dcol = dy W and runs col2im)
           dW1 += dy1^T col1
 For rollout-sized batches (``fused_trunk_max_b``) conv1..conv3 run as ONE fused kernel (``cnn_fused.hip``: one env
 per workgroup, activations handed off through LDS, MFMA 16x16x32); y1/y2/y3 still land in the buffers above so the
@@ -55,9 +57,7 @@ class _Bufs:
             self.dz = torch.empty(B, A1, dtype=bf, device=dev)
             self.dh = torch.empty(B, 512, dtype=bf, device=dev)
             self.dy3 = torch.empty(B * 49, 64, dtype=bf, device=dev)
-            self.dcol3 = torch.empty(B * 49, 576, dtype=bf, device=dev)
             self.dy2 = torch.empty(B * 81, 64, dtype=bf, device=dev)
-            self.dcol2 = torch.empty(B * 81, 512, dtype=bf, device=dev)
             self.dy1 = torch.empty(B * 400, 32, dtype=bf, device=dev)
             self.stats = torch.zeros(8, dtype=torch.float32, device=dev)
 
@@ -81,9 +81,11 @@ class _Bufs:
 class CNNEngine:
     """Explicit forward/backward of :class:`..models.policy.CNNActorCritic` over a :class:`FlatParams` slab."""
 
-    def __init__(self, model, flat, shadow, implicit=True, fused_trunk_max_b=None):
+    def __init__(self, model, flat, shadow, implicit=True, fused_trunk_max_b=None, tconv_dgrad=None):
         net = model.net
         self.implicit = implicit
+        # data gradients of conv3/conv2 as transposed-conv GEMMs gathered from dy (no dcol matrix, no col2im pass)
+        self.tconv_dgrad = implicit if tconv_dgrad is None else tconv_dgrad
         # one workgroup per env: the fused trunk wins whenever the per-layer GEMMs are launch/latency bound
         self.fused_trunk_max_b = 4096 if fused_trunk_max_b is None else fused_trunk_max_b
         self.model = model
@@ -200,8 +202,12 @@ class CNNEngine:
                        gb=[2, B, 64, 9, 9, 3, 3, 1])
             else:
                 G.gemm(b.dy3, 64, False, b.col3, 576, False, self.gW3, 576, 2, 64, 576, B * 49, workspace=ws2)
-        G.gemm(b.dy3, 64, True, self.sW3, 576, False, self.dcol3(b), 576, 1, B * 49, 576, 64, workspace=ws)
-        G.col2im_nhwc(self.dcol3(b), b.y2, b.dy2, self.gb2, B, 9, 9, 64, 3, 3, 1)
+        if self.tconv_dgrad:   # dy2 = conv_transpose(dy3, W3) * (y2 > 0) as one gathered GEMM (+ colsum -> db2)
+            G.gemm(b.dy3, 0, True, self.sW3, 0, False, b.dy2, 64, 1, B * 81, 64, 576, mask=b.y2, ldm=64,
+                   colsum=self.gb2, workspace=ws, ga=[3, B, 64, 9, 9, 3, 3, 1], gb=[4, 1, 64, 1, 64, 3, 3, 1])
+        else:
+            G.gemm(b.dy3, 64, True, self.sW3, 576, False, self.dcol3(b), 576, 1, B * 49, 576, 64, workspace=ws)
+            G.col2im_nhwc(self.dcol3(b), b.y2, b.dy2, self.gb2, B, 9, 9, 64, 3, 3, 1)
         ev[3].record(main)
         side.wait_event(ev[3])
         with torch.cuda.stream(side):   # conv2 weight gradient
@@ -210,8 +216,12 @@ class CNNEngine:
                        gb=[2, B, 32, 20, 20, 4, 4, 2])
             else:
                 G.gemm(b.dy2, 64, False, b.col2, 512, False, self.gW2, 512, 2, 64, 512, B * 81, workspace=ws2)
-        G.gemm(b.dy2, 64, True, self.sW2, 512, False, self.dcol2(b), 512, 1, B * 81, 512, 64, workspace=ws)
-        G.col2im_nhwc(self.dcol2(b), b.y1, b.dy1, self.gb1, B, 20, 20, 32, 4, 4, 2)
+        if self.tconv_dgrad:   # dy1 = conv_transpose(dy2, W2) * (y1 > 0) (+ colsum -> db1)
+            G.gemm(b.dy2, 0, True, self.sW2, 0, False, b.dy1, 32, 1, B * 400, 32, 1024, mask=b.y1, ldm=32,
+                   colsum=self.gb1, workspace=ws, ga=[3, B, 64, 20, 20, 4, 4, 2], gb=[4, 1, 64, 1, 32, 4, 4, 1])
+        else:
+            G.gemm(b.dy2, 64, True, self.sW2, 512, False, self.dcol2(b), 512, 1, B * 81, 512, 64, workspace=ws)
+            G.col2im_nhwc(self.dcol2(b), b.y1, b.dy1, self.gb1, B, 20, 20, 32, 4, 4, 2)
         # conv1 weight gradient (last product of the chain: on the main stream)
         if imp:
             G.gemm(b.dy1, 32, False, b.obs, 0, False, self.gW1, 256, 2, 32, 256, B * 400, workspace=ws,
@@ -222,11 +232,15 @@ class CNNEngine:
         main.wait_event(ev[4])
 
     @staticmethod
-    def dcol3(b):
+    def dcol3(b):   # only the col2im data-gradient path materialises the column gradients
+        if not hasattr(b, "dcol3"):
+            b.dcol3 = torch.empty(b.B * 49, 576, dtype=torch.bfloat16, device=b.dy3.device)
         return b.dcol3
 
     @staticmethod
     def dcol2(b):
+        if not hasattr(b, "dcol2"):
+            b.dcol2 = torch.empty(b.B * 81, 512, dtype=torch.bfloat16, device=b.dy2.device)
         return b.dcol2
 
     def _side_ws(self):

@@ -28,6 +28,7 @@ class FlatParams:
     """
 
     ALIGN = 64  # group starts are 256-byte aligned (vectorised optimiser / all-reduce segments)
+    PARAM_ALIGN = 8  # every param starts 16-byte aligned in the bf16 shadow too (16-byte vector loads in kernels)
 
     def __init__(self, named_groups, device=None):
         self.groups = {}
@@ -38,6 +39,7 @@ class FlatParams:
             total = (total + self.ALIGN - 1) // self.ALIGN * self.ALIGN
             start = total
             for p in plist:
+                total = (total + self.PARAM_ALIGN - 1) // self.PARAM_ALIGN * self.PARAM_ALIGN
                 self.params.append(p)
                 self.offsets.append(total)
                 total += p.numel()
@@ -81,9 +83,9 @@ class FusedAdam:
         self.max_grad_norm = max_grad_norm
         self.gnorm = torch.zeros((), dtype=torch.float32, device=dev)
         self.shadow = bf16_shadow  # optional bf16 tensor of the same numel (written by the native kernel)
-        # sumsq partials + last-arriver tickets (self-cleaning, zero-initialised once)
-        self._partial = torch.zeros(1024, dtype=torch.float32, device=dev)
-        self._ticket = torch.zeros(2, dtype=torch.int32, device=dev)
+        # sumsq partials (reduced by every optimiser workgroup) + the Adam step ticket (self-cleaning)
+        self._partial = torch.zeros(256, dtype=torch.float32, device=dev)
+        self._ticket = torch.zeros(1, dtype=torch.int32, device=dev)
         # native engine: the update kernel zeroes each gradient after reading it (saves a memset per step)
         self.zero_grad_after = False
 
@@ -101,21 +103,24 @@ class FusedAdam:
             self._torch_step()
 
     def _native_norm(self, ops):
-        if self.max_grad_norm is not None:
-            if self.clip_value is not None:
-                # the norm is taken after the element-wise clip (torch oracle order)
-                ops.sumsq(torch.clamp(self.g, -self.clip_value, self.clip_value), self._partial, self._ticket[:1],
-                          self.gnorm)
-            else:
-                ops.sumsq(self.g, self._partial, self._ticket[:1], self.gnorm)
+        """Partial sums of squares of the (clipped) gradient; the update kernel reduces them to the global norm
+        (and writes it to ``self.gnorm``). Returns the partials or None without a norm clip."""
+        if self.max_grad_norm is None:
+            return None
+        if self.clip_value is not None:
+            # the norm is taken after the element-wise clip (torch oracle order)
+            ops.sumsq(torch.clamp(self.g, -self.clip_value, self.clip_value), self._partial)
+        else:
+            ops.sumsq(self.g, self._partial)
+        return self._partial
 
     def _native_step(self):
         ops = _native.require()
-        self._native_norm(ops)
-        ops.adam_step(self.p, self.g, self.m, self.v, self.lr, self.t, self.gnorm, self.shadow,
+        parts = self._native_norm(ops)
+        ops.adam_step(self.p, self.g, self.m, self.v, self.lr, self.t, parts, self.gnorm, self.shadow,
                       float(self.b1), float(self.b2), float(self.eps),
                       float(self.clip_value) if self.clip_value is not None else -1.0,
-                      float(self.max_grad_norm) if self.max_grad_norm is not None else -1.0, self._ticket[1:],
+                      float(self.max_grad_norm) if self.max_grad_norm is not None else -1.0, self._ticket,
                       bool(self.zero_grad_after))
 
     def _torch_step(self):
@@ -156,8 +161,8 @@ class FusedRMSprop(FusedAdam):
 
     def _native_step(self):
         ops = _native.require()
-        self._native_norm(ops)
-        ops.rmsprop_step(self.p, self.g, self.v, self.lr, self.gnorm, self.shadow,
+        parts = self._native_norm(ops)
+        ops.rmsprop_step(self.p, self.g, self.v, self.lr, parts, self.gnorm, self.shadow,
                          float(self.alpha), float(self.eps),
                          float(self.clip_value) if self.clip_value is not None else -1.0,
                          float(self.max_grad_norm) if self.max_grad_norm is not None else -1.0,

@@ -31,7 +31,7 @@ hipError_t aca_env_step_pong(float*, int32_t*, int64_t*, float*, float*, const i
 hipError_t aca_env_policy_step_pong(const uint16_t*, int, const uint16_t*, const float*, int, float*, int32_t*,
                                     float*, float*, float*, int, uint32_t, float*, int32_t*, int64_t*, float*, float*,
                                     const int64_t*, const uint8_t*, uint8_t*, float*, uint8_t*, uint8_t*, uint32_t,
-                                    int, int, int, hipStream_t);
+                                    int, int, int, uint64_t*, hipStream_t);
 hipError_t aca_categorical_sample(const float*, int, int, int, const int64_t*, const int64_t*, const int64_t*, int,
                                   uint32_t, int32_t*, float*, float*, float*, hipStream_t);
 hipError_t aca_ev(const float*, const float*, float*, int, hipStream_t);
@@ -41,10 +41,11 @@ hipError_t aca_gae(const float*, const float*, const uint8_t*, float*, float*, i
 hipError_t aca_nstep(const float*, const float*, const uint8_t*, float*, float*, int, int, float, int, hipStream_t);
 hipError_t aca_normalize(const float*, float*, int, float, hipStream_t);
 hipError_t aca_moments(const float*, const float*, float*, int, hipStream_t);
-hipError_t aca_sumsq(const float*, size_t, float*, int, unsigned int*, float*, hipStream_t);
-hipError_t aca_adam_step(float*, float*, float*, float*, size_t, const float*, float*, const float*, uint16_t*,
+hipError_t aca_sumsq(const float*, size_t, float*, hipStream_t);
+int aca_sumsq_parts();
+hipError_t aca_adam_step(float*, float*, float*, float*, size_t, const float*, float*, const float*, float*, uint16_t*,
                          float, float, float, float, float, unsigned int*, int, hipStream_t);
-hipError_t aca_rmsprop_step(float*, float*, float*, size_t, const float*, const float*, uint16_t*, float, float,
+hipError_t aca_rmsprop_step(float*, float*, float*, size_t, const float*, const float*, float*, uint16_t*, float, float,
                             float, float, int, hipStream_t);
 hipError_t aca_cast_bf16(const float*, uint16_t*, size_t, hipStream_t);
 hipError_t aca_gemm_run(const AcaGemmDesc*, hipStream_t);
@@ -62,7 +63,8 @@ hipError_t aca_ac_loss(const float*, int64_t, const float*, int64_t, const int32
                        const float*, const float*, const uint8_t*, int, int, int, float, float, int, float*, float*,
                        float*, int, hipStream_t);
 hipError_t aca_cnn_trunk_fwd(const uint8_t*, const uint16_t*, const float*, const uint16_t*, const float*,
-                             const uint16_t*, const float*, uint16_t*, uint16_t*, uint16_t*, int, float, hipStream_t);
+                             const uint16_t*, const float*, uint16_t*, uint16_t*, uint16_t*, int, float, uint64_t*,
+                             hipStream_t);
 }
 
 namespace {
@@ -83,6 +85,15 @@ void need(const Tensor& t, at::ScalarType dt, const char* name) {
 
 template <typename T>
 T* ptr(const Tensor& t) { return reinterpret_cast<T*>(t.data_ptr()); }
+
+// optional per-workgroup phase timestamps [nblocks, 16] int64 (diagnostics; s_memrealtime ticks at 100 MHz)
+uint64_t* stamps_ptr(const c10::optional<Tensor>& st, int64_t nblocks) {
+  if (!(st.has_value() && st->defined())) return nullptr;
+  need(*st, at::kLong, "stamps");
+  TORCH_CHECK(st->numel() >= nblocks * 16, "stamps: needs [nblocks, 16]");
+  return ptr<uint64_t>(*st);
+}
+
 
 template <typename T>
 T* optr(const c10::optional<Tensor>& t) { return (t.has_value() && t->defined()) ? ptr<T>(*t) : nullptr; }
@@ -177,7 +188,8 @@ void env_step_pong(Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_s
 void env_policy_step_pong(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, Tensor logp, Tensor ent,
                           Tensor value, int64_t key_shift, int64_t pseed, Tensor state, Tensor t, Tensor tg,
                           Tensor ep_ret, Tensor ep_stats, Tensor ids, Tensor prev, Tensor out, Tensor reward,
-                          Tensor done, Tensor trunc, int64_t seed, int64_t max_steps, int64_t k) {
+                          Tensor done, Tensor trunc, int64_t seed, int64_t max_steps, int64_t k,
+                          c10::optional<Tensor> stamps) {
   check_env(state, t, tg, ep_ret, ep_stats, ids, reward, done, trunc);
   need(h, at::kBFloat16, "h");
   need(Wh, at::kBFloat16, "Wh");
@@ -195,7 +207,8 @@ void env_policy_step_pong(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, 
   TORCH_CHECK(state.size(1) == 8 && h.numel() == (int64_t)N * hdim && Wh.numel() == (int64_t)hdim * A1 &&
                   z.numel() >= (int64_t)N * A1 && act.numel() >= N && value.numel() >= N,
               "env_policy_step_pong: bad shapes");
-  TORCH_CHECK(A1 <= 20 && hdim % 8 == 0, "env_policy_step_pong: at most 19 actions, hidden size % 8 == 0");
+  TORCH_CHECK(A1 <= 20 && hdim <= 512 && (hdim * A1) % 8 == 0 && reinterpret_cast<uintptr_t>(Wh.data_ptr()) % 16 == 0,
+              "env_policy_step_pong: at most 19 actions, hidden size <= 512, hdim*(A+1) % 8 == 0, Wh 16B aligned");
   TORCH_CHECK(prev.numel() == (int64_t)N * k * 84 * 84 && out.numel() == prev.numel(), "pong: bad stack shape");
   TORCH_CHECK(prev.data_ptr() != out.data_ptr(), "pong: prev and out must not alias");
   check(aca_env_policy_step_pong(ptr<uint16_t>(h), hdim, ptr<uint16_t>(Wh), ptr<float>(bh), A, ptr<float>(z),
@@ -203,7 +216,8 @@ void env_policy_step_pong(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, 
                                  (int)key_shift, (uint32_t)pseed, ptr<float>(state), ptr<int32_t>(t),
                                  ptr<int64_t>(tg), ptr<float>(ep_ret), ptr<float>(ep_stats), ptr<int64_t>(ids),
                                  ptr<uint8_t>(prev), ptr<uint8_t>(out), ptr<float>(reward), ptr<uint8_t>(done),
-                                 ptr<uint8_t>(trunc), (uint32_t)seed, (int)max_steps, (int)k, N, cur_stream(state)),
+                                 ptr<uint8_t>(trunc), (uint32_t)seed, (int)max_steps, (int)k, N,
+                                 stamps_ptr(stamps, N), cur_stream(state)),
         "env_policy_step_pong");
 }
 
@@ -315,19 +329,32 @@ void moments(Tensor x, Tensor y, Tensor out) {
 }
 
 // ---------------------------------------------------------------------------------------------- optimisers
-void sumsq(Tensor x, Tensor partial, Tensor ticket, Tensor out) {
+// Writes aca_sumsq_parts() partial sums of squares (unused slots zeroed); the optimisers reduce them.
+void sumsq(Tensor x, Tensor partial) {
   need(x, at::kFloat, "x");
   need(partial, at::kFloat, "partial");
-  need(ticket, at::kInt, "ticket");
-  need(out, at::kFloat, "out");
-  check(aca_sumsq(ptr<float>(x), x.numel(), ptr<float>(partial), (int)partial.numel(), ptr<unsigned int>(ticket),
-                  ptr<float>(out), cur_stream(x)),
-        "sumsq");
+  TORCH_CHECK(partial.numel() >= aca_sumsq_parts(), "sumsq: partial needs ", aca_sumsq_parts(), " slots");
+  check(aca_sumsq(ptr<float>(x), x.numel(), ptr<float>(partial), cur_stream(x)), "sumsq");
 }
 
-void adam_step(Tensor p, Tensor g, Tensor m, Tensor v, Tensor lr, Tensor t, c10::optional<Tensor> gnorm_sq,
-               c10::optional<Tensor> shadow, double b1, double b2, double eps, double clip, double max_norm,
-               Tensor ticket, bool zero_grad) {
+const float* gnorm_parts_ptr(const c10::optional<Tensor>& parts, double max_norm, const char* who) {
+  if (max_norm <= 0) return nullptr;
+  TORCH_CHECK(parts.has_value() && parts->defined(), who, ": max_norm needs the sumsq partials");
+  need(*parts, at::kFloat, "gnorm_parts");
+  TORCH_CHECK(parts->numel() >= aca_sumsq_parts(), who, ": gnorm_parts too small");
+  return ptr<float>(*parts);
+}
+
+uint16_t* shadow_ptr(const c10::optional<Tensor>& shadow, const Tensor& p, const char* who) {
+  if (!(shadow.has_value() && shadow->defined() && shadow->numel() > 0)) return nullptr;
+  need(*shadow, at::kBFloat16, "shadow");
+  TORCH_CHECK(shadow->numel() == p.numel(), who, ": shadow size mismatch");
+  return ptr<uint16_t>(*shadow);
+}
+
+void adam_step(Tensor p, Tensor g, Tensor m, Tensor v, Tensor lr, Tensor t, c10::optional<Tensor> gnorm_parts,
+               c10::optional<Tensor> gnorm_out, c10::optional<Tensor> shadow, double b1, double b2, double eps,
+               double clip, double max_norm, Tensor ticket, bool zero_grad) {
   need(p, at::kFloat, "p");
   need(g, at::kFloat, "g");
   need(m, at::kFloat, "m");
@@ -336,36 +363,24 @@ void adam_step(Tensor p, Tensor g, Tensor m, Tensor v, Tensor lr, Tensor t, c10:
   need(t, at::kFloat, "t");
   need(ticket, at::kInt, "ticket");
   TORCH_CHECK(g.numel() == p.numel() && m.numel() == p.numel() && v.numel() == p.numel(), "adam: size mismatch");
-  if (max_norm > 0) TORCH_CHECK(gnorm_sq.has_value() && gnorm_sq->defined(), "adam: max_norm needs gnorm_sq");
-  uint16_t* sh = nullptr;
-  if (shadow.has_value() && shadow->defined() && shadow->numel() > 0) {
-    need(*shadow, at::kBFloat16, "shadow");
-    TORCH_CHECK(shadow->numel() == p.numel(), "adam: shadow size mismatch");
-    sh = ptr<uint16_t>(*shadow);
-  }
   check(aca_adam_step(ptr<float>(p), ptr<float>(g), ptr<float>(m), ptr<float>(v), p.numel(), ptr<float>(lr),
-                      ptr<float>(t), optr<float>(gnorm_sq), sh, (float)b1, (float)b2, (float)eps, (float)clip,
-                      (float)max_norm, ptr<unsigned int>(ticket), zero_grad ? 1 : 0, cur_stream(p)),
+                      ptr<float>(t), gnorm_parts_ptr(gnorm_parts, max_norm, "adam"), optr<float>(gnorm_out),
+                      shadow_ptr(shadow, p, "adam"), (float)b1, (float)b2, (float)eps, (float)clip, (float)max_norm,
+                      ptr<unsigned int>(ticket), zero_grad ? 1 : 0, cur_stream(p)),
         "adam_step");
 }
 
-void rmsprop_step(Tensor p, Tensor g, Tensor v, Tensor lr, c10::optional<Tensor> gnorm_sq,
-                  c10::optional<Tensor> shadow, double alpha, double eps, double clip, double max_norm,
-                  bool zero_grad) {
+void rmsprop_step(Tensor p, Tensor g, Tensor v, Tensor lr, c10::optional<Tensor> gnorm_parts,
+                  c10::optional<Tensor> gnorm_out, c10::optional<Tensor> shadow, double alpha, double eps,
+                  double clip, double max_norm, bool zero_grad) {
   need(p, at::kFloat, "p");
   need(g, at::kFloat, "g");
   need(v, at::kFloat, "v");
   need(lr, at::kFloat, "lr");
   TORCH_CHECK(g.numel() == p.numel() && v.numel() == p.numel(), "rmsprop: size mismatch");
-  if (max_norm > 0) TORCH_CHECK(gnorm_sq.has_value() && gnorm_sq->defined(), "rmsprop: max_norm needs gnorm_sq");
-  uint16_t* sh = nullptr;
-  if (shadow.has_value() && shadow->defined() && shadow->numel() > 0) {
-    need(*shadow, at::kBFloat16, "shadow");
-    TORCH_CHECK(shadow->numel() == p.numel(), "rmsprop: shadow size mismatch");
-    sh = ptr<uint16_t>(*shadow);
-  }
   check(aca_rmsprop_step(ptr<float>(p), ptr<float>(g), ptr<float>(v), p.numel(), ptr<float>(lr),
-                         optr<float>(gnorm_sq), sh, (float)alpha, (float)eps, (float)clip, (float)max_norm,
+                         gnorm_parts_ptr(gnorm_parts, max_norm, "rmsprop"), optr<float>(gnorm_out),
+                         shadow_ptr(shadow, p, "rmsprop"), (float)alpha, (float)eps, (float)clip, (float)max_norm,
                          zero_grad ? 1 : 0, cur_stream(p)),
         "rmsprop_step");
 }
@@ -400,7 +415,14 @@ AcaConvGather make_gather(const Tensor& src, const std::vector<int64_t>& spec, d
   g.OW = (g.W - g.KW) / g.S + 1;
   g.scale = (float)scale;
   TORCH_CHECK(src.is_contiguous(), "gemm: gather source ", name, " must be contiguous");
-  TORCH_CHECK(src.numel() >= (int64_t)g.B * g.C * g.H * g.W, "gemm: gather source ", name, " too small");
+  if (g.mode == 3) {
+    TORCH_CHECK(g.OH > 0 && g.OW > 0, "gemm: gather mode 3 bad geometry");
+    TORCH_CHECK(src.numel() >= (int64_t)g.B * g.OH * g.OW * g.C, "gemm: gather source ", name, " too small");
+  } else if (g.mode == 4) {
+    TORCH_CHECK(src.numel() >= (int64_t)g.C * g.KH * g.KW * g.W, "gemm: gather source ", name, " too small");
+  } else {
+    TORCH_CHECK(src.numel() >= (int64_t)g.B * g.C * g.H * g.W, "gemm: gather source ", name, " too small");
+  }
   if (g.mode == 1) {
     TORCH_CHECK(src.scalar_type() == at::kByte, "gemm: gather mode 1 needs a uint8 source");
     TORCH_CHECK(g.KW % 8 == 0 && g.S % 4 == 0 && g.W % 4 == 0, "gemm: gather mode 1 needs KW%8, S%4, W%4 == 0");
@@ -408,6 +430,10 @@ AcaConvGather make_gather(const Tensor& src, const std::vector<int64_t>& spec, d
   } else if (g.mode == 2) {
     TORCH_CHECK(src.scalar_type() == at::kBFloat16, "gemm: gather mode 2 needs a bf16 source");
     TORCH_CHECK(g.C % 8 == 0, "gemm: gather mode 2 needs C % 8 == 0");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(g.src) % 16 == 0, "gemm: gather source must be 16-byte aligned");
+  } else if (g.mode == 3 || g.mode == 4) {
+    TORCH_CHECK(src.scalar_type() == at::kBFloat16, "gemm: gather modes 3/4 need a bf16 source");
+    TORCH_CHECK((g.mode == 3 ? g.C : g.W) % 8 == 0, "gemm: gather modes 3/4 need 8-aligned contiguous channels");
     TORCH_CHECK(reinterpret_cast<uintptr_t>(g.src) % 16 == 0, "gemm: gather source must be 16-byte aligned");
   } else {
     TORCH_CHECK(false, "gemm: unknown gather mode ", g.mode);
@@ -426,7 +452,13 @@ void gemm(Tensor A, int64_t lda, bool a_k, Tensor B, int64_t ldb, bool b_k, Tens
   AcaGemmDesc d{};
   d.ga = make_gather(A, ga, ga_scale, "A");
   d.gb = make_gather(B, gb, gb_scale, "B");
-  if (d.ga.mode) {
+  TORCH_CHECK(d.ga.mode != 4 && d.gb.mode != 3, "gemm: gather mode 3 is A-only, mode 4 is B-only");
+  TORCH_CHECK((d.ga.mode == 3) == (d.gb.mode == 4), "gemm: gather modes 3 and 4 go together (data gradient)");
+  if (d.ga.mode == 3) {
+    TORCH_CHECK(a_k, "gemm: A gather needs a_k");
+    TORCH_CHECK(M == (int64_t)d.ga.B * d.ga.H * d.ga.W && K == (int64_t)d.ga.C * d.ga.KH * d.ga.KW,
+                "gemm: transposed-conv gather shape does not match M/K");
+  } else if (d.ga.mode) {
     TORCH_CHECK(a_k, "gemm: A gather needs a_k");
     TORCH_CHECK(M == (int64_t)d.ga.B * d.ga.OH * d.ga.OW && K == (int64_t)d.ga.C * d.ga.KH * d.ga.KW,
                 "gemm: A gather shape does not match M/K");
@@ -434,7 +466,10 @@ void gemm(Tensor A, int64_t lda, bool a_k, Tensor B, int64_t ldb, bool b_k, Tens
     TORCH_CHECK(A.scalar_type() == at::kBFloat16, "gemm: A must be bf16");
     check_extent(A, a_k ? M : K, a_k ? K : M, lda, "A");
   }
-  if (d.gb.mode) {
+  if (d.gb.mode == 4) {
+    TORCH_CHECK(!b_k, "gemm: B gather needs !b_k");
+    TORCH_CHECK(K == (int64_t)d.gb.C * d.gb.KH * d.gb.KW && N == d.gb.W, "gemm: weight-transpose gather shape");
+  } else if (d.gb.mode) {
     TORCH_CHECK(!b_k, "gemm: B gather needs !b_k");
     TORCH_CHECK(K == (int64_t)d.gb.B * d.gb.OH * d.gb.OW && N == (int64_t)d.gb.C * d.gb.KH * d.gb.KW,
                 "gemm: B gather shape does not match K/N");
@@ -488,7 +523,7 @@ int64_t gemm_effective_splits(int64_t K, int64_t bk, int64_t splits) {
 // the kernel: obs [B, 4, 84, 84] uint8, W1 [32, 256] (OIHW), W2 [64, 512] / W3 [64, 576] (OHWI), y1 [B*400, 32],
 // y2 [B*81, 64], y3 [B*49, 64]; all 16-byte aligned (the kernel uses 16-byte vector accesses).
 void cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, Tensor y1,
-                   Tensor y2, Tensor y3, double scale) {
+                   Tensor y2, Tensor y3, double scale, c10::optional<Tensor> stamps) {
   need(obs, at::kByte, "obs");
   for (auto* w : {&W1, &W2, &W3, &y1, &y2, &y3}) need(*w, at::kBFloat16, "trunk bf16 operand");
   for (auto* b : {&b1, &b2, &b3}) need(*b, at::kFloat, "trunk bias");
@@ -503,7 +538,7 @@ void cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tenso
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "cnn_trunk_fwd: operands must be 16B aligned");
   check(aca_cnn_trunk_fwd(ptr<uint8_t>(obs), ptr<uint16_t>(W1), ptr<float>(b1), ptr<uint16_t>(W2), ptr<float>(b2),
                           ptr<uint16_t>(W3), ptr<float>(b3), ptr<uint16_t>(y1), ptr<uint16_t>(y2), ptr<uint16_t>(y3),
-                          (int)B, (float)scale, cur_stream(obs)),
+                          (int)B, (float)scale, stamps_ptr(stamps, B), cur_stream(obs)),
         "cnn_trunk_fwd");
 }
 
@@ -632,7 +667,7 @@ TORCH_LIBRARY(acamd, m) {
   m.def("env_policy_step_pong(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, Tensor logp, Tensor ent, "
         "Tensor value, int key_shift, int pseed, Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, "
         "Tensor env_ids, Tensor prev, Tensor out, Tensor reward, Tensor done, Tensor truncated, int seed, "
-        "int max_steps, int k) -> ()");
+        "int max_steps, int k, Tensor? stamps=None) -> ()");
   m.def("categorical_sample(Tensor logits, Tensor keys, int seed, Tensor act, Tensor logp, Tensor ent) -> ()");
   m.def("categorical_sample_env(Tensor logits, Tensor tg, Tensor env_ids, int key_shift, int seed, Tensor act, "
         "Tensor logp, Tensor ent, Tensor? vout) -> ()");
@@ -642,11 +677,12 @@ TORCH_LIBRARY(acamd, m) {
   m.def("nstep_returns(Tensor r, Tensor v, Tensor d, Tensor tgt, Tensor adv, float gamma, int L) -> ()");
   m.def("normalize(Tensor a, Tensor out, float eps) -> ()");
   m.def("moments(Tensor x, Tensor y, Tensor out) -> ()");
-  m.def("sumsq(Tensor x, Tensor partial, Tensor ticket, Tensor out) -> ()");
-  m.def("adam_step(Tensor p, Tensor g, Tensor m, Tensor v, Tensor lr, Tensor t, Tensor? gnorm_sq, Tensor? shadow, "
-        "float b1, float b2, float eps, float clip, float max_norm, Tensor ticket, bool zero_grad=False) -> ()");
-  m.def("rmsprop_step(Tensor p, Tensor g, Tensor v, Tensor lr, Tensor? gnorm_sq, Tensor? shadow, float alpha, "
-        "float eps, float clip, float max_norm, bool zero_grad=False) -> ()");
+  m.def("sumsq(Tensor x, Tensor partial) -> ()");
+  m.def("adam_step(Tensor p, Tensor g, Tensor m, Tensor v, Tensor lr, Tensor t, Tensor? gnorm_parts, "
+        "Tensor? gnorm_out, Tensor? shadow, float b1, float b2, float eps, float clip, float max_norm, Tensor ticket, "
+        "bool zero_grad=False) -> ()");
+  m.def("rmsprop_step(Tensor p, Tensor g, Tensor v, Tensor lr, Tensor? gnorm_parts, Tensor? gnorm_out, "
+        "Tensor? shadow, float alpha, float eps, float clip, float max_norm, bool zero_grad=False) -> ()");
   m.def("cast_bf16(Tensor x, Tensor y) -> ()");
   m.def("gemm(Tensor A, int lda, bool a_k, Tensor B, int ldb, bool b_k, Tensor C, int ldc, int out_mode, int M, "
         "int N, int K, float alpha, Tensor? bias, bool relu, Tensor? mask, int ldm, Tensor? colsum, int colsum_mod, "
@@ -654,7 +690,7 @@ TORCH_LIBRARY(acamd, m) {
         "float gb_scale) -> ()");
   m.def("gemm_effective_splits(int K, int bk, int splits) -> int", &gemm_effective_splits);
   m.def("cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, Tensor y1, "
-        "Tensor y2, Tensor y3, float scale) -> ()");
+        "Tensor y2, Tensor y3, float scale, Tensor? stamps=None) -> ()");
   m.def("im2col_u8(Tensor x, Tensor col, int kh, int kw, int s, float scale) -> ()");
   m.def("im2col_nhwc(Tensor x, Tensor col, int B, int H, int W, int C, int kh, int kw, int s) -> ()");
   m.def("col2im_nhwc(Tensor dcol, Tensor ymask, Tensor dx, Tensor? colsum, int B, int H, int W, int C, int kh, "

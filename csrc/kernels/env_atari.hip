@@ -31,6 +31,11 @@ __device__ __forceinline__ void serve(PongState& s, uint32_t seed, uint32_t id, 
 
 __device__ __forceinline__ float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
 
+// optional phase timestamps (s_memrealtime, 100 MHz), [gridDim.x, 16]; null in production
+__device__ __forceinline__ void stamp_if(uint64_t* st, int slot, bool who) {
+  if (st && who) st[(size_t)blockIdx.x * 16 + slot] = __builtin_amdgcn_s_memrealtime();
+}
+
 struct PongIO {
   float* state; int32_t* tsteps; int64_t* tglob; float* ep_ret; float* ep_stats; const int64_t* env_ids;
   const uint8_t* prev; uint8_t* out; float* reward; uint8_t* done_out; uint8_t* trunc_out;
@@ -172,6 +177,10 @@ __global__ void __launch_bounds__(256) pong_step_kernel(PongIO io, const int32_t
   pong_render(io, e, r.s, r.done != 0);
 }
 
+constexpr int HEAD_KPL = 8;                          // hidden units per lane: hdim <= 512
+constexpr int HEAD_CHUNKS = 20;                      // 16-byte Wh chunks per lane: hdim * (A + 1) <= 10240
+constexpr int HEAD_PASS = 8;                         // chunks in flight per lane per staging pass
+
 // Rollout step of the native engine fused with the env: the policy/value head (z = h.Wh + bh, 512 -> A+1) of
 // env e, Gumbel-max sampling with the env-counter RNG key, logp / entropy / value, then the env step with the
 // sampled action -- one launch instead of head GEMM + sampling + env kernels. Critical path = the head only:
@@ -184,29 +193,55 @@ __global__ void __launch_bounds__(256) pong_policy_step_kernel(PongIO io, const 
                                                                float* __restrict__ z_out, int32_t* __restrict__ act,
                                                                float* __restrict__ logp, float* __restrict__ ent,
                                                                float* __restrict__ vout, int key_shift,
-                                                               uint32_t pseed) {
+                                                               uint32_t pseed, uint64_t* __restrict__ stamps) {
   const int e = blockIdx.x;
   const int A1 = A + 1;
   __shared__ int sh_act;
   __shared__ PongOut cand[3];
+  __shared__ __attribute__((aligned(16))) u16 s_wh[HEAD_CHUNKS * 64 * 8];
+  stamp_if(stamps, 0, threadIdx.x == 0);
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     const int64_t key = io.tglob[e] * ((int64_t)1 << key_shift) + io.env_ids[e];  // pre-step counter
+    // Wh [hdim][A1] arrives as coalesced 16-byte chunks (all in flight together) and is re-read from LDS row-wise;
+    // lane l owns hidden units l, l + 64, ... (one coalesced 2-byte load per 64 units)
+    const int n16 = hdim * A1 / 8;
+    float hv[HEAD_KPL];
+#pragma unroll
+    for (int q = 0; q < HEAD_KPL; ++q) {
+      const int k = lane + 64 * q;
+      hv[q] = k < hdim ? bf2f(h[(size_t)e * hdim + k]) : 0.f;
+    }
+    for (int base = 0; base < n16; base += 64 * HEAD_PASS) {   // one pass for heads up to 4096 weights
+      uint4 wv[HEAD_PASS];
+#pragma unroll
+      for (int u = 0; u < HEAD_PASS; ++u) {
+        const int c = base + lane + 64 * u;
+        if (c < n16) wv[u] = reinterpret_cast<const uint4*>(Wh)[c];
+      }
+#pragma unroll
+      for (int u = 0; u < HEAD_PASS; ++u) {
+        const int c = base + lane + 64 * u;
+        if (c < n16) reinterpret_cast<uint4*>(s_wh)[c] = wv[u];
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    stamp_if(stamps, 8, lane == 0);
     float acc[20];
 #pragma unroll
     for (int j = 0; j < 20; ++j) acc[j] = 0.f;
-    for (int kb = lane * 8; kb < hdim; kb += 64 * 8) {
-      union { uint4 v; u16 x[8]; } hv;
-      hv.v = *reinterpret_cast<const uint4*>(h + (size_t)e * hdim + kb);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const float hi = bf2f(hv.x[i]);
-        const u16* wr = Wh + (size_t)(kb + i) * A1;
+    for (int q = 0; q < HEAD_KPL; ++q) {
+      const int k = lane + 64 * q;
+      if (k < hdim) {
+        const u16* wr = s_wh + k * A1;
 #pragma unroll
         for (int j = 0; j < 20; ++j)
-          if (j < A1) acc[j] += hi * bf2f(wr[j]);
+          if (j < A1) acc[j] += hv[q] * bf2f(wr[j]);
       }
     }
+    stamp_if(stamps, 9, lane == 0);
     float zj = 0.f;
 #pragma unroll
     for (int j = 0; j < 20; ++j) {
@@ -216,6 +251,7 @@ __global__ void __launch_bounds__(256) pong_policy_step_kernel(PongIO io, const 
       }
     }
     if (lane < A1) z_out[(size_t)e * A1 + lane] = zj;
+    stamp_if(stamps, 10, lane == 0);
     const float value = __shfl(zj, A, 64);
     // categorical head over lanes 0..A-1 (same maths as categorical_sample_kernel)
     const bool on = lane < A;
@@ -243,14 +279,23 @@ __global__ void __launch_bounds__(256) pong_policy_step_kernel(PongIO io, const 
       vout[e] = value;
       sh_act = bi;
     }
+    stamp_if(stamps, 1, lane == 0);
   } else {
     if (threadIdx.x < 64 + 3) cand[threadIdx.x - 64] = pong_advance(io, e, (float)((int)threadIdx.x - 65));
+    stamp_if(stamps, 2, threadIdx.x == 64);
     pong_shift(io, e, 64, blockDim.x - 64);
+    stamp_if(stamps, 3, threadIdx.x == 64);
   }
   __syncthreads();
+  stamp_if(stamps, 4, threadIdx.x == 0);
   const PongOut& r = cand[pong_dir_index(sh_act)];
   if (threadIdx.x == 0) pong_commit(io, e, r);
   pong_render(io, e, r.s, r.done != 0);
+  if (stamps) {
+    stamp_if(stamps, 5, threadIdx.x == 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp_if(stamps, 6, threadIdx.x == 0);
+  }
 }
 
 }  // namespace aca
@@ -282,12 +327,14 @@ extern "C" hipError_t aca_env_policy_step_pong(const uint16_t* h, int hdim, cons
                                                float* ep_ret, float* ep_stats, const int64_t* ids,
                                                const uint8_t* prev, uint8_t* out, float* reward, uint8_t* done,
                                                uint8_t* trunc, uint32_t seed, int max_steps, int k, int N,
-                                               hipStream_t stream) {
+                                               uint64_t* stamps, hipStream_t stream) {
   if (N <= 0) return hipSuccess;
-  if (A + 1 > 20 || A > 64 || hdim % 8) return hipErrorInvalidValue;
+  if (A + 1 > 20 || hdim > 64 * aca::HEAD_KPL || hdim * (A + 1) > aca::HEAD_CHUNKS * 64 * 8 || (hdim * (A + 1)) % 8 ||
+      reinterpret_cast<uintptr_t>(Wh) % 16)
+    return hipErrorInvalidValue;
   aca::PongIO io = make_pong_io(state, t, tg, ep_ret, ep_stats, ids, prev, out, reward, done, trunc, seed, max_steps,
                                 k);
   aca::pong_policy_step_kernel<<<N, 256, 0, stream>>>(io, h, hdim, Wh, bh, A, z, act, logp, ent, value, key_shift,
-                                                      pseed);
+                                                      pseed, stamps);
   return hipGetLastError();
 }

@@ -11,9 +11,14 @@ extern "C" {
 //           requires KW % 8 == 0, S % 4 == 0, W % 4 == 0 (8 k = two aligned 4-byte loads)
 //   mode 2: bf16 NHWC source [B, H, W, C], k order (i, j, c); requires C % 8 == 0 (8 k = one 16-byte load)
 // Row index m = (b, oh, ow) of the conv output, column index k as above.
+//   mode 3: transposed conv / data gradient: source = output gradient bf16 NHWC [B, OH, OW, C]; row m = (b, h, w) of
+//           the conv INPUT [H, W]; k order (i, j, c); zero where (h - i, w - j) is off the stride grid or outside
+//           the output; requires C % 8 == 0
+//   mode 4: (B operand) OHWI weight [C][KH][KW][W] read as B[k = (i, j, o)][n]: the transposed-conv weight operand
+//           without materialising the transpose; spec fields C = conv output channels, W = input channels
 typedef struct {
   const void* src;
-  int mode;  // 0 none, 1 u8 nchw, 2 bf16 nhwc
+  int mode;  // 0 none, 1 u8 nchw, 2 bf16 nhwc, 3 transposed-conv gather, 4 OHWI weight transpose
   int B, C, H, W, KH, KW, S, OH, OW;
   float scale;
 } AcaConvGather;

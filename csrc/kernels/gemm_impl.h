@@ -58,6 +58,28 @@ __device__ __forceinline__ uint4 load8(const u16* base, int64_t row_off, int idx
 template <int MODE>
 __device__ __forceinline__ uint4 gather8(const AcaConvGather& g, int m, int k, bool ok) {
   if (!ok) return make_uint4(0, 0, 0, 0);
+  if (MODE == 3) {
+    // transposed conv (data gradient): row m = (b, ih, iw) of the conv INPUT, k = (i, j, c) over the output-gradient
+    // channels; the source pixel is ((ih - i) / S, (iw - j) / S) when that lands on the stride grid, else zero
+    const int hw = g.H * g.W;
+    const int b = m / hw, p = m - b * hw;
+    const int ih = p / g.W, iw = p - ih * g.W;
+    const int kwc = g.KW * g.C;
+    const int i = k / kwc, r = k - i * kwc;
+    const int j = r / g.C, c = r - j * g.C;
+    const int th = ih - i, tw = iw - j;
+    if (th < 0 || tw < 0) return make_uint4(0, 0, 0, 0);
+    const int sh = th / g.S, sw = tw / g.S;
+    if (sh * g.S != th || sw * g.S != tw || sh >= g.OH || sw >= g.OW) return make_uint4(0, 0, 0, 0);
+    return *reinterpret_cast<const uint4*>(reinterpret_cast<const u16*>(g.src) +
+                                           (((int64_t)b * g.OH + sh) * g.OW + sw) * g.C + c);
+  }
+  if (MODE == 4) {
+    // OHWI conv weight read as B[k = (i, j, o)][n = input channel] (the transposed-conv operand): row m = k here
+    const int khw = g.KH * g.KW;
+    const int ij = m / g.C, o = m - ij * g.C;
+    return *reinterpret_cast<const uint4*>(reinterpret_cast<const u16*>(g.src) + ((int64_t)o * khw + ij) * g.W + k);
+  }
   const int ohw = g.OH * g.OW;
   const int b = m / ohw, p = m - b * ohw;
   const int oh = p / g.OW, ow = p - oh * g.OW;

@@ -11,7 +11,7 @@
 //   and added atomically into its slot of the fp32 gradient slab.
 // Coefficients (c_ent, beta) are read from device scalars (annealed by the schedules without a host sync).
 // stats[0..6] = pg, kl, entropy, value_loss (unscaled mean), clipfrac, total actor loss, mean ratio.
-// One 1024-thread workgroup: the stats reduction is deterministic.
+// One workgroup: the stats reduction is deterministic.
 //
 // A2C fast path (returns_mode 1 = n-step / 2 = GAE): the kernel first computes the targets and advantages of the
 // whole [T, N] rollout itself (same maths as returns.hip), the EV-before statistic (stats[7], Basic_AC/util.py:4-12)
@@ -51,15 +51,36 @@ struct LossArgs {
   float* dbias; int dbias_n;            // head bias gradient (A+1 columns: logits | value)
 };
 
-__global__ void __launch_bounds__(1024) ac_loss_kernel(LossArgs a) {
+constexpr int LOSS_THREADS = 256;
+constexpr int LOSS_STAGE = 2048;   // fused-returns rollouts up to this many rows are staged in LDS
+constexpr int CAT_MAX = 20;        // categorical heads: logits + value columns held in registers (A + 1 <= 21)
+
+// Latency structure (one workgroup, B ~ 160 rows for the bench): every global operand is loaded in ONE round
+// (rollout rewards / dones / values into LDS, each thread's logits row + action + old log-prob into registers),
+// the returns recursion and the row maths then run out of LDS/registers; global writes (dz, targets for logging)
+// are fire-and-forget.
+__global__ void __launch_bounds__(LOSS_THREADS) ac_loss_kernel(LossArgs a) {
   __shared__ double sh[16 * 8];
   __shared__ float dls[64];
   __shared__ float dbs[64];
-  float dbp[21];  // this thread's partial column sums of dz (head-bias gradient), A + 1 <= 21
+  __shared__ float s_rew[LOSS_STAGE], s_val[LOSS_STAGE + 256], s_ret[LOSS_STAGE], s_adv[LOSS_STAGE];
+  __shared__ uint8_t s_dn[LOSS_STAGE];
+  float dbp[CAT_MAX + 1];  // this thread's partial column sums of dz (head-bias gradient)
 #pragma unroll
-  for (int j = 0; j < 21; ++j) dbp[j] = 0.f;
+  for (int j = 0; j <= CAT_MAX; ++j) dbp[j] = 0.f;
   if (threadIdx.x < 64) { dls[threadIdx.x] = 0.f; dbs[threadIdx.x] = 0.f; }
+  const bool staged = a.returns_mode && a.B <= LOSS_STAGE && a.N <= 256;
+  if (staged) {
+    for (int i = threadIdx.x; i < a.B; i += blockDim.x) {
+      s_rew[i] = a.rew[i];
+      s_dn[i] = a.dn[i];
+    }
+    for (int i = threadIdx.x; i < a.B + a.N; i += blockDim.x) s_val[i] = a.val[i];
+  }
   __syncthreads();
+  const float* rew = staged ? s_rew : a.rew;
+  const uint8_t* dn = staged ? s_dn : a.dn;
+  const float* val = staged ? s_val : a.val;
   float adv_mean = 0.f, adv_inv = 1.f;
   if (a.returns_mode) {
     // ---- phase 0: targets / advantages of every (t, n), EV-before, normalisation constants
@@ -73,32 +94,33 @@ __global__ void __launch_bounds__(1024) ac_loss_kernel(LossArgs a) {
         bool alive = true;
         for (int k = t; k < h; ++k) {
           const int i = k * a.N + n;
-          acc += disc * a.rew[i];
+          acc += disc * rew[i];
           disc *= a.gamma;
-          if (a.dn[i]) { alive = false; break; }
+          if (dn[i]) { alive = false; break; }
         }
-        if (alive) acc += disc * a.val[h * a.N + n];
+        if (alive) acc += disc * val[h * a.N + n];
         R = acc;
       } else {
-        float last = 0.f, Rt = 0.f;
+        float last = 0.f;
         for (int k = a.T - 1; k >= t; --k) {
           const int i = k * a.N + n;
-          const float nd = a.dn[i] ? 0.f : 1.f;
-          const float delta = a.rew[i] + a.gamma * a.val[i + a.N] * nd - a.val[i];
+          const float nd = dn[i] ? 0.f : 1.f;
+          const float delta = rew[i] + a.gamma * val[i + a.N] * nd - val[i];
           last = delta + a.gamma * a.lam * nd * last;
         }
-        Rt = last + a.val[idx];
-        R = Rt;
+        R = last + val[idx];
       }
-      const float v = a.val[idx];
+      const float v = val[idx];
       const float A_ = R - v;
       a.ret_w[idx] = R;
       a.adv_w[idx] = A_;
+      if (staged) { s_ret[idx] = R; s_adv[idx] = A_; }
       s_r += R; s_rr += (double)R * R; s_v += v; s_vv += (double)v * v; s_rv += (double)R * v;
       s_a += A_; s_aa += (double)A_ * A_;
     }
+    if (!staged) __threadfence_block();   // global ret_w / adv_w are re-read by other threads after the barrier
     double red[7] = {s_r, s_rr, s_v, s_vv, s_rv, s_a, s_aa};
-    block_sum_multi<7>(red, sh);
+    block_sum_multi<7>(red, sh);   // ends with a barrier: s_ret / s_adv (or the global scratch) are complete
     s_r = red[0]; s_rr = red[1]; s_v = red[2]; s_vv = red[3]; s_rv = red[4]; s_a = red[5]; s_aa = red[6];
     const double n = a.B;
     if (threadIdx.x == 0) {
@@ -112,10 +134,9 @@ __global__ void __launch_bounds__(1024) ac_loss_kernel(LossArgs a) {
       adv_mean = (float)m;
       adv_inv = 1.0f / (1e-8f + (float)sqrt(var));
     }
-    __syncthreads();  // ret_w / adv_w written above are read by other threads below
   }
-  const float* advp = a.returns_mode ? a.adv_w : a.adv;
-  const float* retp = a.returns_mode ? a.ret_w : a.ret;
+  const float* advp = a.returns_mode ? (staged ? s_adv : a.adv_w) : a.adv;
+  const float* retp = a.returns_mode ? (staged ? s_ret : a.ret_w) : a.ret;
   const float invB = 1.0f / (float)a.B;
   const float c_ent = a.ent_coef ? *a.ent_coef : 0.f;
   const float beta = a.kl_coef ? *a.kl_coef : 0.f;
@@ -123,18 +144,35 @@ __global__ void __launch_bounds__(1024) ac_loss_kernel(LossArgs a) {
   double s_pg = 0, s_kl = 0, s_H = 0, s_vl = 0, s_cf = 0, s_ratio = 0;
   for (int b = threadIdx.x; b < a.B; b += blockDim.x) {
     const float* z = a.logits + (int64_t)b * a.ldl;
+    // every per-row operand is requested before any is used
+    float zr[CAT_MAX];
+    if (!a.gaussian) {
+#pragma unroll
+      for (int j = 0; j < CAT_MAX; ++j) zr[j] = j < a.A ? z[j] : -INFINITY;
+    }
+    const int ab = a.gaussian ? 0 : a.act_i[b];
+    const float lpo = a.logp_old[b];
+    const float v = a.value ? a.value[(int64_t)b * a.ldv] : 0.f;
+    const float vo = (a.value && a.v_clip > 0.f && a.v_old) ? a.v_old[b] : 0.f;
+    const float adv = (advp[b] - adv_mean) * adv_inv;
+    const float R = a.value ? retp[b] : 0.f;
     float lpa = 0.f, H = 0.f, lse = 0.f;
     if (!a.gaussian) {
       float mx = -INFINITY;
-      for (int j = 0; j < a.A; ++j) mx = fmaxf(mx, z[j]);
+#pragma unroll
+      for (int j = 0; j < CAT_MAX; ++j) mx = fmaxf(mx, zr[j]);
       float se = 0.f;
-      for (int j = 0; j < a.A; ++j) se += expf(z[j] - mx);
+#pragma unroll
+      for (int j = 0; j < CAT_MAX; ++j) se += j < a.A ? expf(zr[j] - mx) : 0.f;
       lse = mx + logf(se);
-      for (int j = 0; j < a.A; ++j) {
-        const float lz = z[j] - lse;
-        H -= expf(lz) * lz;
+#pragma unroll
+      for (int j = 0; j < CAT_MAX; ++j) {
+        if (j < a.A) {
+          const float lz = zr[j] - lse;
+          H -= expf(lz) * lz;
+          if (j == ab) lpa = lz;
+        }
       }
-      lpa = z[a.act_i[b]] - lse;
     } else {
       for (int j = 0; j < a.A; ++j) {
         const float ls = fminf(fmaxf(a.log_std[j], -2.5f), 2.5f);
@@ -143,7 +181,6 @@ __global__ void __launch_bounds__(1024) ac_loss_kernel(LossArgs a) {
         H += 0.5f + HALF_LOG_2PI + ls;
       }
     }
-    const float lpo = a.logp_old[b], adv = (advp[b] - adv_mean) * adv_inv;
     float g_lpa;  // dL/dlpa (already divided by B)
     if (a.ppo_clip > 0.f) {
       const float ratio = expf(lpa - lpo);
@@ -167,16 +204,16 @@ __global__ void __launch_bounds__(1024) ac_loss_kernel(LossArgs a) {
     // head gradient
     u16* dz = a.dlogits + (int64_t)b * a.lddl;
     if (!a.gaussian) {
-      const int ab = a.act_i[b];
-      for (int j = 0; j < a.A; ++j) {
-        const float oh = (j == ab) ? 1.0f : 0.0f;
-        const float lz = z[j] - lse, pj = expf(lz);
-        const float g = g_lpa * (oh - pj) + c_ent * invB * pj * (lz + H);
-        const u16 gb = f2bf(g);
-        dz[j] = gb;
 #pragma unroll
-        for (int q = 0; q < 21; ++q)
-          if (q == j) dbp[q] += bf2f(gb);
+      for (int j = 0; j < CAT_MAX; ++j) {
+        if (j < a.A) {
+          const float oh = (j == ab) ? 1.0f : 0.0f;
+          const float lz = zr[j] - lse, pj = expf(lz);
+          const float g = g_lpa * (oh - pj) + c_ent * invB * pj * (lz + H);
+          const u16 gb = f2bf(g);
+          dz[j] = gb;
+          dbp[j] += bf2f(gb);
+        }
       }
     } else {
       for (int j = 0; j < a.A; ++j) {
@@ -191,12 +228,10 @@ __global__ void __launch_bounds__(1024) ac_loss_kernel(LossArgs a) {
     }
     // critic
     if (a.value) {
-      const float v = a.value[(int64_t)b * a.ldv], R = retp[b];
       float d = v - R;
       float vl = d * d;
       float gv = 2.0f * d;
       if (a.v_clip > 0.f && a.v_old) {
-        const float vo = a.v_old[b];
         const float vc = vo + fminf(fmaxf(v - vo, -a.v_clip), a.v_clip);
         const float dc = vc - R;
         if (dc * dc > vl) {
@@ -208,8 +243,9 @@ __global__ void __launch_bounds__(1024) ac_loss_kernel(LossArgs a) {
       s_vl += vl;
       const u16 gvb = f2bf(a.vf_coef * gv * invB);
       a.dvalue[(int64_t)b * a.lddv] = gvb;
+      // the value column is column A of the fused head (dbias_n == A + 1)
 #pragma unroll
-      for (int q = 0; q < 21; ++q)
+      for (int q = 0; q <= CAT_MAX; ++q)
         if (q == a.A) dbp[q] += bf2f(gvb);
     }
   }
@@ -221,7 +257,7 @@ __global__ void __launch_bounds__(1024) ac_loss_kernel(LossArgs a) {
   if (a.dbias) {
     const int lane = threadIdx.x & 63;
 #pragma unroll
-    for (int q = 0; q < 21; ++q) {
+    for (int q = 0; q <= CAT_MAX; ++q) {
       if (q < a.dbias_n) {
         const float v = wave_sum(dbp[q]);
         if (lane == 0) atomicAdd(&dbs[q], v);
@@ -254,7 +290,7 @@ extern "C" hipError_t aca_ac_loss(const float* logits, int64_t ldl, const float*
                                   const float* rew, const float* val, const uint8_t* dn, int T, int N, int L,
                                   float gamma, float lam, int norm_adv, float* ret_w, float* adv_w, float* dbias,
                                   int dbias_n, hipStream_t stream) {
-  if (A > 64 || dbias_n > 21) return hipErrorInvalidValue;
+  if (A > 64 || dbias_n > aca::CAT_MAX + 1 || (!gaussian && A > aca::CAT_MAX)) return hipErrorInvalidValue;
   if (returns_mode && (T * N != B || !rew || !val || !dn || !ret_w || !adv_w)) return hipErrorInvalidValue;
   aca::LossArgs a;
   a.logits = logits; a.ldl = ldl; a.value = value; a.ldv = ldv; a.act_i = act_i; a.act_f = act_f;
@@ -264,6 +300,6 @@ extern "C" hipError_t aca_ac_loss(const float* logits, int64_t ldl, const float*
   a.gaussian = gaussian;
   a.returns_mode = returns_mode; a.rew = rew; a.val = val; a.dn = dn; a.T = T; a.N = N; a.L = L; a.gamma = gamma;
   a.lam = lam; a.norm_adv = norm_adv; a.ret_w = ret_w; a.adv_w = adv_w; a.dbias = dbias; a.dbias_n = dbias_n;
-  aca::ac_loss_kernel<<<1, 1024, 0, stream>>>(a);
+  aca::ac_loss_kernel<<<1, aca::LOSS_THREADS, 0, stream>>>(a);
   return hipGetLastError();
 }

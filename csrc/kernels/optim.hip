@@ -7,42 +7,56 @@
 // never sync with the host and the whole learner step can be captured in a hipGraph.
 //
 // The step counter t is read by every workgroup and advanced by the workgroup that finishes last (ticket), so no
-// extra launch is needed. sumsq is deterministic: per-block partials summed in block order by the last block.
+// extra launch is needed. sumsq is deterministic: it only writes per-workgroup partials (fixed slots); every optimiser
+// workgroup sums the same slots in the same order, so no in-kernel cross-workgroup hand-off (and no L2 write-back
+// fence) is needed for the global norm.
 #include "common.h"
 
 namespace aca {
 
 constexpr int OPT_THREADS = 256;
+constexpr int SUMSQ_U = 8;
+constexpr int SUMSQ_PARTS = 256;   // max sumsq workgroups = partial slots the optimiser reduces
 
 __global__ void __launch_bounds__(OPT_THREADS) sumsq_kernel(const float* __restrict__ x, size_t n,
-                                                             float* __restrict__ partial,
-                                                             unsigned int* __restrict__ ticket,
-                                                             float* __restrict__ out) {
+                                                             float* __restrict__ partial) {
   __shared__ float sh[16];
-  __shared__ int flag;
   float s = 0.f;
   const size_t n4 = n / 4;
   const float4* x4 = reinterpret_cast<const float4*>(x);
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
-    const float4 v = x4[i];
-    s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  // SUMSQ_U independent 16-byte loads in flight per thread before any use: the grid is capped at one workgroup
+  // per CU, so latency (not bandwidth) bounds a one-load-at-a-time loop
+  const size_t step = (size_t)gridDim.x * blockDim.x * SUMSQ_U;
+  for (size_t i0 = blockIdx.x * (size_t)blockDim.x * SUMSQ_U + threadIdx.x; i0 < n4; i0 += step) {
+    float4 v[SUMSQ_U];
+#pragma unroll
+    for (int u = 0; u < SUMSQ_U; ++u) {
+      const size_t i = i0 + (size_t)u * blockDim.x;
+      v[u] = i < n4 ? x4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < SUMSQ_U; ++u) s += v[u].x * v[u].x + v[u].y * v[u].y + v[u].z * v[u].z + v[u].w * v[u].w;
   }
-  if (blockIdx.x == 0)
+  if (blockIdx.x == 0) {
     for (size_t i = n4 * 4 + threadIdx.x; i < n; i += blockDim.x) s += x[i] * x[i];
+    // unused partial slots are zero, so the consumer always sums SUMSQ_PARTS entries in a fixed order
+    for (int b = gridDim.x + threadIdx.x; b < SUMSQ_PARTS; b += blockDim.x) partial[b] = 0.f;
+  }
   s = block_sum(s, sh);
   if (threadIdx.x == 0) partial[blockIdx.x] = s;
-  if (last_block_arrival(ticket, gridDim.x, &flag)) {
-    // parallel, fixed-order (deterministic for a given grid) reduction of the per-block partials
-    float t = 0.f;
-    for (unsigned int b = threadIdx.x; b < gridDim.x; b += blockDim.x) t += partial[b];
-    t = block_sum(t, sh);
-    if (threadIdx.x == 0) *out = t;
-  }
 }
 
-__device__ __forceinline__ float grad_scale(const float* gnorm_sq, float max_norm) {
+// Global squared norm from the sumsq partials, reduced by every consumer workgroup in the same fixed order
+// (deterministic, and no in-kernel cross-workgroup hand-off: the kernel boundary publishes the partials).
+__device__ __forceinline__ float partial_total(const float* __restrict__ parts, float* sh) {
+  float v = 0.f;
+  for (int i = threadIdx.x; i < SUMSQ_PARTS; i += blockDim.x) v += parts[i];
+  return block_sum(v, sh);
+}
+
+__device__ __forceinline__ float grad_scale(float gnorm_sq, float max_norm) {
   if (max_norm <= 0.f) return 1.f;
-  const float n = sqrtf(*gnorm_sq);
+  const float n = sqrtf(gnorm_sq);
   return fminf(max_norm / (n + 1e-6f), 1.0f);
 }
 
@@ -50,34 +64,66 @@ template <bool ADAM>
 __global__ void __launch_bounds__(OPT_THREADS) opt_kernel(float* __restrict__ p, float* __restrict__ g,
                                                           float* __restrict__ m, float* __restrict__ v, size_t n,
                                                           const float* __restrict__ lr_ptr, float* __restrict__ t_ptr,
-                                                          const float* __restrict__ gnorm_sq, u16* __restrict__ shadow,
+                                                          const float* __restrict__ gnorm_parts,
+                                                          float* __restrict__ gnorm_out, u16* __restrict__ shadow,
                                                           float b1, float b2, float eps, float clip, float max_norm,
                                                           unsigned int* __restrict__ ticket, int zero_grad) {
   __shared__ int flag;
+  __shared__ float shr[16];
   const float lr = *lr_ptr;
   const float t = ADAM ? (*t_ptr + 1.0f) : 0.f;
-  const float scale = grad_scale(gnorm_sq, max_norm);
+  float scale = 1.f;
+  if (gnorm_parts) {
+    const float gsq = partial_total(gnorm_parts, shr);
+    scale = grad_scale(gsq, max_norm);
+    if (gnorm_out && blockIdx.x == 0 && threadIdx.x == 0) *gnorm_out = gsq;
+  }
   float lr_t = lr;
   if (ADAM) lr_t = lr * sqrtf(1.0f - powf(b2, t)) / (1.0f - powf(b1, t));
-  const size_t stride = (size_t)gridDim.x * blockDim.x;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += stride) {
-    float gi = g[i];
-    if (zero_grad) g[i] = 0.f;  // the next learner step accumulates into a clean slab without a memset
+  auto upd = [&](float gi, float& vi, float& mi, float& pi) {
     if (clip > 0.f) gi = fminf(fmaxf(gi, -clip), clip);
     gi *= scale;
-    float vi = v[i];
     vi = b2 * vi + (1.0f - b2) * gi * gi;
-    v[i] = vi;
-    float pi = p[i];
     if (ADAM) {
-      float mi = b1 * m[i] + (1.0f - b1) * gi;
-      m[i] = mi;
+      mi = b1 * mi + (1.0f - b1) * gi;
       pi -= lr_t * mi / (sqrtf(vi) + eps);
     } else {
       pi -= lr * gi / sqrtf(vi + eps);
     }
-    p[i] = pi;
-    if (shadow) shadow[i] = f2bf(pi);
+  };
+  // float4 body: all operand loads of a thread are issued together (one memory round trip per element group)
+  const size_t n4 = n / 4;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 g4 = reinterpret_cast<const float4*>(g)[i];
+    float4 v4 = reinterpret_cast<const float4*>(v)[i];
+    float4 p4 = reinterpret_cast<const float4*>(p)[i];
+    float4 m4 = ADAM ? reinterpret_cast<const float4*>(m)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (zero_grad) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    upd(g4.x, v4.x, m4.x, p4.x);
+    upd(g4.y, v4.y, m4.y, p4.y);
+    upd(g4.z, v4.z, m4.z, p4.z);
+    upd(g4.w, v4.w, m4.w, p4.w);
+    reinterpret_cast<float4*>(v)[i] = v4;
+    if (ADAM) reinterpret_cast<float4*>(m)[i] = m4;
+    reinterpret_cast<float4*>(p)[i] = p4;
+    if (shadow) {
+      uint2 sv;
+      sv.x = (uint32_t)f2bf(p4.x) | ((uint32_t)f2bf(p4.y) << 16);
+      sv.y = (uint32_t)f2bf(p4.z) | ((uint32_t)f2bf(p4.w) << 16);
+      reinterpret_cast<uint2*>(shadow)[i] = sv;
+    }
+  }
+  if (blockIdx.x == 0) {   // scalar tail
+    for (size_t i = n4 * 4 + threadIdx.x; i < n; i += blockDim.x) {
+      float gi = g[i], vi = v[i], pi = p[i], mi = ADAM ? m[i] : 0.f;
+      if (zero_grad) g[i] = 0.f;
+      upd(gi, vi, mi, pi);
+      v[i] = vi;
+      if (ADAM) m[i] = mi;
+      p[i] = pi;
+      if (shadow) shadow[i] = f2bf(pi);
+    }
   }
   if (ADAM) {
     if (last_block_arrival(ticket, gridDim.x, &flag)) {
@@ -91,10 +137,10 @@ __global__ void cast_bf16_kernel(const float* __restrict__ x, u16* __restrict__ 
     y[i] = f2bf(x[i]);
 }
 
-static int opt_grid(size_t n) {
-  size_t b = (n + OPT_THREADS * 4 - 1) / (OPT_THREADS * 4);
+static int opt_grid(size_t n) {   // one float4 per thread (up to 16M parameters per pass)
+  size_t b = (n / 4 + OPT_THREADS - 1) / OPT_THREADS;
   if (b < 1) b = 1;
-  if (b > 2048) b = 2048;
+  if (b > 16384) b = 16384;
   return (int)b;
 }
 
@@ -102,32 +148,38 @@ static int opt_grid(size_t n) {
 
 using namespace aca;
 
-extern "C" hipError_t aca_sumsq(const float* x, size_t n, float* partial, int max_blocks, unsigned int* ticket,
-                                float* out, hipStream_t stream) {
-  // one workgroup per CU at most: every workgroup pays an agent-scope release (L2 write-back) for its ticket
-  int grid = (int)((n / 4 + OPT_THREADS * 4 - 1) / (OPT_THREADS * 4));
+extern "C" hipError_t aca_sumsq(const float* x, size_t n, float* partial, hipStream_t stream) {
+  if (reinterpret_cast<uintptr_t>(x) % 16) return hipErrorInvalidValue;
+  int grid = (int)((n / 4 + OPT_THREADS * SUMSQ_U - 1) / (OPT_THREADS * SUMSQ_U));
   if (grid < 1) grid = 1;
-  if (grid > 256) grid = 256;
-  if (grid > max_blocks) grid = max_blocks;
-  sumsq_kernel<<<grid, OPT_THREADS, 0, stream>>>(x, n, partial, ticket, out);
+  if (grid > SUMSQ_PARTS) grid = SUMSQ_PARTS;
+  sumsq_kernel<<<grid, OPT_THREADS, 0, stream>>>(x, n, partial);
   return hipGetLastError();
 }
 
+extern "C" int aca_sumsq_parts() { return SUMSQ_PARTS; }
+
 extern "C" hipError_t aca_adam_step(float* p, float* g, float* m, float* v, size_t n, const float* lr,
-                                    float* t, const float* gnorm_sq, uint16_t* shadow, float b1, float b2, float eps,
+                                    float* t, const float* gnorm_parts, float* gnorm_out, uint16_t* shadow, float b1, float b2, float eps,
                                     float clip, float max_norm, unsigned int* ticket, int zero_grad,
                                     hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  opt_kernel<true><<<opt_grid(n), OPT_THREADS, 0, stream>>>(p, g, m, v, n, lr, t, gnorm_sq, shadow, b1, b2, eps,
+  if ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(m) |
+       reinterpret_cast<uintptr_t>(v)) % 16 || reinterpret_cast<uintptr_t>(shadow) % 8)
+    return hipErrorInvalidValue;
+  opt_kernel<true><<<opt_grid(n), OPT_THREADS, 0, stream>>>(p, g, m, v, n, lr, t, gnorm_parts, gnorm_out, shadow, b1, b2, eps,
                                                             clip, max_norm, ticket, zero_grad);
   return hipGetLastError();
 }
 
 extern "C" hipError_t aca_rmsprop_step(float* p, float* g, float* v, size_t n, const float* lr,
-                                       const float* gnorm_sq, uint16_t* shadow, float alpha, float eps, float clip,
+                                       const float* gnorm_parts, float* gnorm_out, uint16_t* shadow, float alpha, float eps, float clip,
                                        float max_norm, int zero_grad, hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  opt_kernel<false><<<opt_grid(n), OPT_THREADS, 0, stream>>>(p, g, nullptr, v, n, lr, nullptr, gnorm_sq, shadow,
+  if ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(v)) % 16 ||
+      reinterpret_cast<uintptr_t>(shadow) % 8)
+    return hipErrorInvalidValue;
+  opt_kernel<false><<<opt_grid(n), OPT_THREADS, 0, stream>>>(p, g, nullptr, v, n, lr, nullptr, gnorm_parts, gnorm_out, shadow,
                                                              0.f, alpha, eps, clip, max_norm, nullptr, zero_grad);
   return hipGetLastError();
 }

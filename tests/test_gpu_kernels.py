@@ -262,8 +262,8 @@ def test_ac_loss_kernel_matches_autograd(cuda, ppo):
 
 
 # ------------------------------------------------------------------------------------------------------ engine
-@pytest.mark.parametrize("implicit,fused", [(True, True), (True, False), (False, False)])
-def test_cnn_engine_matches_autograd(cuda, implicit, fused):
+@pytest.mark.parametrize("implicit,fused,tconv", [(True, True, True), (True, False, False), (False, False, False)])
+def test_cnn_engine_matches_autograd(cuda, implicit, fused, tconv):
     """Full native forward + loss + backward of the Atari CNN vs fp32 autograd on the same parameters."""
     from actor_critic_algs_on_tensorflow_amd.algos import losses as L
     from actor_critic_algs_on_tensorflow_amd.algos.engine import CNNEngine
@@ -279,7 +279,7 @@ def test_cnn_engine_matches_autograd(cuda, implicit, fused):
             m.bias.uniform_(-0.05, 0.1)
     flat = FlatParams(model.param_groups(), cuda)
     shadow = flat.data.to(torch.bfloat16)
-    eng = CNNEngine(model, flat, shadow, implicit=implicit, fused_trunk_max_b=None if fused else 0)
+    eng = CNNEngine(model, flat, shadow, implicit=implicit, fused_trunk_max_b=None if fused else 0, tconv_dgrad=tconv)
     obs = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device=cuda)
     b = eng.bufs(B, with_grad=True)
     z = eng.forward(obs, b).clone()
@@ -334,6 +334,32 @@ def test_cnn_trunk_fused_matches_layers(cuda):
     x3 = y2.float().view(B, 9, 9, 64).permute(0, 3, 1, 2)
     r3 = F.relu(F.conv2d(x3, W3.float().permute(0, 3, 1, 2), b3, stride=1))
     assert torch.allclose(y3.float().view(B, 7, 7, 64).permute(0, 3, 1, 2), r3, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("k,s,H,Cout,Cin,B", [(3, 1, 9, 64, 64, 5), (4, 2, 20, 64, 32, 3), (8, 4, 84, 32, 8, 2)])
+def test_gemm_transposed_conv_dgrad(cuda, k, s, H, Cout, Cin, B):
+    """Data-gradient GEMM (A gathered from dy on the stride grid, B = OHWI weight read transposed) vs
+    torch conv_transpose2d, with the ReLU mask and bias-gradient column sums of the epilogue."""
+    from actor_critic_algs_on_tensorflow_amd.ops import gemm as G
+    import torch.nn.functional as F
+    torch.manual_seed(2)
+    OH = (H - k) // s + 1
+    dy = torch.randn(B, OH, OH, Cout, device=cuda).to(torch.bfloat16)
+    W = (torch.randn(Cout, k, k, Cin, device=cuda) * 0.1).to(torch.bfloat16)        # OHWI
+    ymask = (torch.rand(B * H * H, Cin, device=cuda) > 0.3).to(torch.bfloat16)
+    out = torch.empty(B * H * H, Cin, dtype=torch.bfloat16, device=cuda)
+    cs = torch.zeros(Cin, device=cuda)
+    for tile, bk in ((4, 64), (2, 128), (0, 64)):
+        cs.zero_()
+        G._native.require().gemm(dy, 0, True, W, 0, False, out, Cin, 1, B * H * H, Cin, k * k * Cout, 1.0, None,
+                                 False, ymask, Cin, cs, 0, tile, bk, 1, None, None, [3, B, Cout, H, H, k, k, s], 1.0,
+                                 [4, 1, Cout, 1, Cin, k, k, 1], 1.0)
+        ref = F.conv_transpose2d(dy.float().permute(0, 3, 1, 2), W.float().permute(0, 3, 1, 2), stride=s)
+        ref = ref[:, :, :H, :H].permute(0, 2, 3, 1).reshape(B * H * H, Cin) * ymask.float()
+        assert torch.allclose(out.float(), ref, rtol=2e-2, atol=2e-2), (tile, bk, (out.float() - ref).abs().max())
+        # column sums are taken from the fp32 values before the bf16 store
+        err = (cs - ref.sum(0)).abs()
+        assert (err <= 1e-2 * ref.abs().sum(0) + 1e-2).all(), (tile, bk, err.max())
 
 
 def test_trainer_native_graph_updates(cuda):

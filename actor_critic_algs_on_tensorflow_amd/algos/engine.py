@@ -29,6 +29,8 @@ the bf16 shadow of the slab that the fused optimiser rewrites every step.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .. import _native
@@ -88,6 +90,8 @@ class CNNEngine:
         self.tconv_dgrad = implicit if tconv_dgrad is None else tconv_dgrad
         # one workgroup per env: the fused trunk wins whenever the per-layer GEMMs are launch/latency bound
         self.fused_trunk_max_b = 4096 if fused_trunk_max_b is None else fused_trunk_max_b
+        # rollout frame-stack shift inside the fused trunk (else the env kernel shifts); A/B switch for profiling
+        self.trunk_shift = os.environ.get("ACA_TRUNK_SHIFT", "1") != "0"
         self.model = model
         self.flat = flat
         self.shadow = shadow
@@ -133,14 +137,21 @@ class CNNEngine:
                workspace=self.ws)
         return out
 
-    def forward(self, obs, b: _Bufs, head=True):
+    def forward(self, obs, b: _Bufs, head=True, shift_out=None):
         """obs uint8 [B, 4, 84, 84] -> b.z fp32 [B, A+1] (logits | value); ``head=False`` stops at ``b.h`` (the
-        rollout fuses the head into the sampling + env-step kernel)."""
+        rollout fuses the head into the sampling + env-step kernel). ``shift_out``: the next observation buffer,
+        whose frames 0..2 the fused trunk fills with frames 1..3 of ``obs``; returns True iff it did."""
         B = b.B
         ws = self.ws
         b.obs = obs  # the conv1 weight gradient re-gathers its columns from the frames
+        shifted = False
+        want_shift = shift_out is not None
         if self.implicit and B <= self.fused_trunk_max_b:
-            G.cnn_trunk_fwd(obs, self.sW1, self.b1, self.sW2, self.b2, self.sW3, self.b3, b.y1, b.y2, b.y3)
+            if not self.trunk_shift:
+                shift_out = None
+            G.cnn_trunk_fwd(obs, self.sW1, self.b1, self.sW2, self.b2, self.sW3, self.b3, b.y1, b.y2, b.y3,
+                            shift_out=shift_out)
+            shifted = shift_out is not None
         elif self.implicit:
             G.gemm(obs, 0, True, self.sW1, 256, True, b.y1, 32, 1, B * 400, 32, 256, bias=self.b1, relu=True,
                    workspace=ws, ga=[1, B, 4, 84, 84, 8, 8, 4], ga_scale=1.0 / 255.0)
@@ -163,7 +174,7 @@ class CNNEngine:
         if head:
             G.gemm(b.h, 512, True, self.sWh, self.A1, False, b.z, self.A1, 0, B, self.A1, 512, bias=self.bh,
                    workspace=ws)
-        return b.z
+        return shifted if want_shift else b.z
 
     # ------------------------------------------------------------------------------------------------ backward
     def backward(self, b: _Bufs, head_bias_done=False):

@@ -157,12 +157,13 @@ class ActorCriticTrainer:
             bt = lb.rows(t * N, N) if lb is not None else b
             if fused:
                 # conv trunk + fc, then ONE launch: policy/value head + sampling + env step (+ frame render)
-                eng.forward(st.obs[t], bt, head=False)
+                # (the fused trunk also shifts the frame stack into obs[t + 1]; the env kernel renders the newest)
+                shifted = eng.forward(st.obs[t], bt, head=False, shift_out=st.obs[t + 1])
                 ops.env_policy_step_pong(bt.h, eng.sWh, eng.bh, bt.z, st.actions[t], st.logp[t], st.entropy[t],
                                          st.values[t], KEY_ENV_BITS, self.policy_seed, env.state, env.t, env.tg,
                                          env.ep_ret, env.ep_stats, env.env_ids, st.obs[t], st.obs[t + 1],
                                          st.rewards[t], st.dones[t], st.truncated[t], env.seed,
-                                         env.max_episode_steps, env.frame_stack)
+                                         env.max_episode_steps, env.frame_stack, shifted)
                 continue
             z = eng.forward(st.obs[t], bt)
             # one launch: sample + logp + entropy + value copy, RNG keys from the env counters

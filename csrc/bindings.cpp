@@ -31,7 +31,7 @@ hipError_t aca_env_step_pong(float*, int32_t*, int64_t*, float*, float*, const i
 hipError_t aca_env_policy_step_pong(const uint16_t*, int, const uint16_t*, const float*, int, float*, int32_t*,
                                     float*, float*, float*, int, uint32_t, float*, int32_t*, int64_t*, float*, float*,
                                     const int64_t*, const uint8_t*, uint8_t*, float*, uint8_t*, uint8_t*, uint32_t,
-                                    int, int, int, uint64_t*, hipStream_t);
+                                    int, int, int, int, uint64_t*, hipStream_t);
 hipError_t aca_categorical_sample(const float*, int, int, int, const int64_t*, const int64_t*, const int64_t*, int,
                                   uint32_t, int32_t*, float*, float*, float*, hipStream_t);
 hipError_t aca_ev(const float*, const float*, float*, int, hipStream_t);
@@ -63,8 +63,8 @@ hipError_t aca_ac_loss(const float*, int64_t, const float*, int64_t, const int32
                        const float*, const float*, const uint8_t*, int, int, int, float, float, int, float*, float*,
                        float*, int, hipStream_t);
 hipError_t aca_cnn_trunk_fwd(const uint8_t*, const uint16_t*, const float*, const uint16_t*, const float*,
-                             const uint16_t*, const float*, uint16_t*, uint16_t*, uint16_t*, int, float, uint64_t*,
-                             hipStream_t);
+                             const uint16_t*, const float*, uint16_t*, uint16_t*, uint16_t*, int, float, uint8_t*,
+                             uint64_t*, hipStream_t);
 }
 
 namespace {
@@ -188,7 +188,7 @@ void env_step_pong(Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_s
 void env_policy_step_pong(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, Tensor logp, Tensor ent,
                           Tensor value, int64_t key_shift, int64_t pseed, Tensor state, Tensor t, Tensor tg,
                           Tensor ep_ret, Tensor ep_stats, Tensor ids, Tensor prev, Tensor out, Tensor reward,
-                          Tensor done, Tensor trunc, int64_t seed, int64_t max_steps, int64_t k,
+                          Tensor done, Tensor trunc, int64_t seed, int64_t max_steps, int64_t k, bool pre_shifted,
                           c10::optional<Tensor> stamps) {
   check_env(state, t, tg, ep_ret, ep_stats, ids, reward, done, trunc);
   need(h, at::kBFloat16, "h");
@@ -207,8 +207,9 @@ void env_policy_step_pong(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, 
   TORCH_CHECK(state.size(1) == 8 && h.numel() == (int64_t)N * hdim && Wh.numel() == (int64_t)hdim * A1 &&
                   z.numel() >= (int64_t)N * A1 && act.numel() >= N && value.numel() >= N,
               "env_policy_step_pong: bad shapes");
-  TORCH_CHECK(A1 <= 20 && hdim <= 512 && (hdim * A1) % 8 == 0 && reinterpret_cast<uintptr_t>(Wh.data_ptr()) % 16 == 0,
-              "env_policy_step_pong: at most 19 actions, hidden size <= 512, hdim*(A+1) % 8 == 0, Wh 16B aligned");
+  TORCH_CHECK(A1 >= 3 && A1 <= 20 && hdim == 512 && reinterpret_cast<uintptr_t>(Wh.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(h.data_ptr()) % 16 == 0,
+              "env_policy_step_pong: 2..19 actions, hidden size 512, h and Wh 16-byte aligned");
   TORCH_CHECK(prev.numel() == (int64_t)N * k * 84 * 84 && out.numel() == prev.numel(), "pong: bad stack shape");
   TORCH_CHECK(prev.data_ptr() != out.data_ptr(), "pong: prev and out must not alias");
   check(aca_env_policy_step_pong(ptr<uint16_t>(h), hdim, ptr<uint16_t>(Wh), ptr<float>(bh), A, ptr<float>(z),
@@ -216,7 +217,7 @@ void env_policy_step_pong(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, 
                                  (int)key_shift, (uint32_t)pseed, ptr<float>(state), ptr<int32_t>(t),
                                  ptr<int64_t>(tg), ptr<float>(ep_ret), ptr<float>(ep_stats), ptr<int64_t>(ids),
                                  ptr<uint8_t>(prev), ptr<uint8_t>(out), ptr<float>(reward), ptr<uint8_t>(done),
-                                 ptr<uint8_t>(trunc), (uint32_t)seed, (int)max_steps, (int)k, N,
+                                 ptr<uint8_t>(trunc), (uint32_t)seed, (int)max_steps, (int)k, N, pre_shifted ? 1 : 0,
                                  stamps_ptr(stamps, N), cur_stream(state)),
         "env_policy_step_pong");
 }
@@ -523,7 +524,8 @@ int64_t gemm_effective_splits(int64_t K, int64_t bk, int64_t splits) {
 // the kernel: obs [B, 4, 84, 84] uint8, W1 [32, 256] (OIHW), W2 [64, 512] / W3 [64, 576] (OHWI), y1 [B*400, 32],
 // y2 [B*81, 64], y3 [B*49, 64]; all 16-byte aligned (the kernel uses 16-byte vector accesses).
 void cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, Tensor y1,
-                   Tensor y2, Tensor y3, double scale, c10::optional<Tensor> stamps) {
+                   Tensor y2, Tensor y3, double scale, c10::optional<Tensor> shift_out,
+                   c10::optional<Tensor> stamps) {
   need(obs, at::kByte, "obs");
   for (auto* w : {&W1, &W2, &W3, &y1, &y2, &y3}) need(*w, at::kBFloat16, "trunk bf16 operand");
   for (auto* b : {&b1, &b2, &b3}) need(*b, at::kFloat, "trunk bias");
@@ -536,9 +538,17 @@ void cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tenso
               "cnn_trunk_fwd: activation buffers too small");
   for (auto* t : {&obs, &W1, &W2, &W3})
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "cnn_trunk_fwd: operands must be 16B aligned");
+  uint8_t* so = nullptr;
+  if (shift_out.has_value() && shift_out->defined()) {
+    need(*shift_out, at::kByte, "shift_out");
+    TORCH_CHECK(shift_out->numel() == obs.numel() && reinterpret_cast<uintptr_t>(shift_out->data_ptr()) % 16 == 0 &&
+                    shift_out->data_ptr() != obs.data_ptr(),
+                "cnn_trunk_fwd: shift_out must be a distinct, aligned [B, 4, 84, 84] uint8 buffer");
+    so = ptr<uint8_t>(*shift_out);
+  }
   check(aca_cnn_trunk_fwd(ptr<uint8_t>(obs), ptr<uint16_t>(W1), ptr<float>(b1), ptr<uint16_t>(W2), ptr<float>(b2),
                           ptr<uint16_t>(W3), ptr<float>(b3), ptr<uint16_t>(y1), ptr<uint16_t>(y2), ptr<uint16_t>(y3),
-                          (int)B, (float)scale, stamps_ptr(stamps, B), cur_stream(obs)),
+                          (int)B, (float)scale, so, stamps_ptr(stamps, B), cur_stream(obs)),
         "cnn_trunk_fwd");
 }
 
@@ -667,7 +677,7 @@ TORCH_LIBRARY(acamd, m) {
   m.def("env_policy_step_pong(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, Tensor logp, Tensor ent, "
         "Tensor value, int key_shift, int pseed, Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, "
         "Tensor env_ids, Tensor prev, Tensor out, Tensor reward, Tensor done, Tensor truncated, int seed, "
-        "int max_steps, int k, Tensor? stamps=None) -> ()");
+        "int max_steps, int k, bool pre_shifted=False, Tensor? stamps=None) -> ()");
   m.def("categorical_sample(Tensor logits, Tensor keys, int seed, Tensor act, Tensor logp, Tensor ent) -> ()");
   m.def("categorical_sample_env(Tensor logits, Tensor tg, Tensor env_ids, int key_shift, int seed, Tensor act, "
         "Tensor logp, Tensor ent, Tensor? vout) -> ()");
@@ -690,7 +700,7 @@ TORCH_LIBRARY(acamd, m) {
         "float gb_scale) -> ()");
   m.def("gemm_effective_splits(int K, int bk, int splits) -> int", &gemm_effective_splits);
   m.def("cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, Tensor y1, "
-        "Tensor y2, Tensor y3, float scale, Tensor? stamps=None) -> ()");
+        "Tensor y2, Tensor y3, float scale, Tensor? shift_out=None, Tensor? stamps=None) -> ()");
   m.def("im2col_u8(Tensor x, Tensor col, int kh, int kw, int s, float scale) -> ()");
   m.def("im2col_nhwc(Tensor x, Tensor col, int B, int H, int W, int C, int kh, int kw, int s) -> ()");
   m.def("col2im_nhwc(Tensor dcol, Tensor ymask, Tensor dx, Tensor? colsum, int B, int H, int W, int C, int kh, "

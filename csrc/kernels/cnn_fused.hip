@@ -7,6 +7,8 @@
 //                                  conv2 (K 512 = (i, j, c))                  --> y2 [81, 64]  bf16 (LDS + global)
 //                                  conv3 (K 576 = (i, j, c))                  --> y3 [49, 64]  bf16 (global)
 //
+// With `shift_out` (rollout) the kernel also writes frames 1..3 of each observation as frames 0..2 of the next
+// one -- the frame-stack shift of the env step, from registers it already holds.
 // y1 / y2 / y3 are also written to global memory: they are the learner's saved activations (the A2C learner reuses
 // the rollout's forward pass) and y3 feeds the fc GEMM. Weights are the bf16 shadow of the parameter slab in the
 // engine's layouts (W1 [32][256] OIHW, W2 [64][512] / W3 [64][576] OHWI); conv1 weights are staged in LDS, conv2/3
@@ -49,7 +51,7 @@ __global__ void __launch_bounds__(T_THREADS) cnn_trunk_fwd_kernel(
     const uint8_t* __restrict__ obs, const u16* __restrict__ W1, const float* __restrict__ b1,
     const u16* __restrict__ W2, const float* __restrict__ b2, const u16* __restrict__ W3,
     const float* __restrict__ b3, u16* __restrict__ y1g, u16* __restrict__ y2g, u16* __restrict__ y3g,
-    float scale, uint64_t* __restrict__ stamps) {
+    float scale, uint8_t* __restrict__ shift_out, uint64_t* __restrict__ stamps) {
   __shared__ __attribute__((aligned(16))) u16 s_obs[OBS_BYTES];
   __shared__ __attribute__((aligned(16))) u16 s_w1[32 * W1_LD];
   __shared__ __attribute__((aligned(16))) u16 s_y1[Y1_ROWS * Y1_LD];
@@ -94,9 +96,19 @@ __global__ void __launch_bounds__(T_THREADS) cnn_trunk_fwd_kernel(
       const int i = tid + u * T_THREADS, r = i / 32, c8 = (i % 32) * 8;
       *reinterpret_cast<uint4*>(s_w1 + r * W1_LD + c8) = vw[u];
     }
+    __syncthreads();
+    stamp(stamps, 1);
+    if (shift_out) {
+      // rollout: the next observation's frame stack starts with frames 1..3 of this one (the env step then only
+      // renders the newest frame): the bytes are still in registers; the stores drain behind conv1
+      uint4* so = reinterpret_cast<uint4*>(shift_out + (size_t)e * OBS_BYTES);
+#pragma unroll
+      for (int u = 0; u < OBS_PER; ++u) {
+        const int i = tid + u * T_THREADS;
+        if (i >= OBS_CH / 4 && i < OBS_CH) so[i - OBS_CH / 4] = vo[u];
+      }
+    }
   }
-  __syncthreads();
-  stamp(stamps, 1);
 
   // ---------------------------------------------------------------- conv1: M 400 (25 tiles), N 32 (2), K 256 (8)
   {
@@ -153,14 +165,11 @@ __global__ void __launch_bounds__(T_THREADS) cnn_trunk_fwd_kernel(
       const int i = k >> 7, j = (k >> 5) & 3, c0 = k & 31;
 #pragma unroll
       for (int mt = 0; mt < 6; ++mt) {
-        const int m = mt * 16 + l16;
-        bf16x8 a;
-        if (m < Y2_ROWS) {
-          const int oh = m / 9, ow = m - oh * 9;
-          a = *reinterpret_cast<const bf16x8*>(s_y1 + ((oh * 2 + i) * 20 + ow * 2 + j) * Y1_LD + c0);
-        } else {
-          a = __builtin_bit_cast(bf16x8, short8v{0, 0, 0, 0, 0, 0, 0, 0});
-        }
+        // rows past the 81 outputs are computed on a clamped (valid) pixel and never stored: no branch, so all
+        // 96 fragment reads of the layer stay in flight together
+        const int m = min(mt * 16 + l16, Y2_ROWS - 1);
+        const int oh = m / 9, ow = m - oh * 9;
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(s_y1 + ((oh * 2 + i) * 20 + ow * 2 + j) * Y1_LD + c0);
         acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw2[ks], acc[mt], 0, 0, 0);
       }
     }
@@ -193,14 +202,9 @@ __global__ void __launch_bounds__(T_THREADS) cnn_trunk_fwd_kernel(
       const int i = k / 192, j = (k >> 6) % 3, c0 = k & 63;
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt) {
-        const int m = mt * 16 + l16;
-        bf16x8 a;
-        if (m < Y3_ROWS) {
-          const int oh = m / 7, ow = m - oh * 7;
-          a = *reinterpret_cast<const bf16x8*>(s_y2 + ((oh + i) * 9 + ow + j) * Y2_LD + c0);
-        } else {
-          a = __builtin_bit_cast(bf16x8, short8v{0, 0, 0, 0, 0, 0, 0, 0});
-        }
+        const int m = min(mt * 16 + l16, Y3_ROWS - 1);
+        const int oh = m / 7, ow = m - oh * 7;
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(s_y2 + ((oh + i) * 9 + ow + j) * Y2_LD + c0);
         acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw3[ks], acc[mt], 0, 0, 0);
       }
     }
@@ -224,10 +228,10 @@ __global__ void __launch_bounds__(T_THREADS) cnn_trunk_fwd_kernel(
 
 extern "C" hipError_t aca_cnn_trunk_fwd(const uint8_t* obs, const uint16_t* W1, const float* b1, const uint16_t* W2,
                                         const float* b2, const uint16_t* W3, const float* b3, uint16_t* y1,
-                                        uint16_t* y2, uint16_t* y3, int B, float scale, uint64_t* stamps,
-                                        hipStream_t stream) {
+                                        uint16_t* y2, uint16_t* y3, int B, float scale, uint8_t* shift_out,
+                                        uint64_t* stamps, hipStream_t stream) {
   if (B <= 0) return hipSuccess;
   aca::cnn_trunk_fwd_kernel<<<B, aca::T_THREADS, 0, stream>>>(obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale,
-                                                               stamps);
+                                                               shift_out, stamps);
   return hipGetLastError();
 }

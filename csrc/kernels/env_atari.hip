@@ -140,25 +140,40 @@ __device__ __forceinline__ void pong_shift(const PongIO& io, int e, int t0, int 
 // Basic_AC/run_AC.py:37-40) -- these stores overwrite the shifted frames, so call after a barrier that follows
 // pong_shift.
 __device__ __forceinline__ void pong_render(const PongIO& io, int e, const PongState& s, bool done) {
+  // 4-pixel words, 21 per row: wall rows are uniform, and only the words that overlap a paddle or the ball need
+  // per-pixel tests (one 4-byte store per word, consecutive lanes -> consecutive words)
+  constexpr int WPR = PW / 4, NWORDS = PH * WPR;   // 21, 1764
   const int k = io.k;
   const int pa0 = (int)floorf(s.pa - PADDLE_H / 2), po0 = (int)floorf(s.po - PADDLE_H / 2);
   const int bx0 = (int)floorf(s.bx), by0 = (int)floorf(s.by);
-  uint8_t* ov = io.out + (size_t)e * k * FRAME;
-  for (int c = threadIdx.x; c < FRAME / 16; c += blockDim.x) {
-    union { uint4 v; uint8_t b[16]; } px;
+  uint32_t* ov = reinterpret_cast<uint32_t*>(io.out + (size_t)e * k * FRAME);
+  for (int w = threadIdx.x; w < NWORDS; w += blockDim.x) {
+    const int y = w / WPR, x0 = (w - y * WPR) * 4;
+    uint32_t word;
+    if (y < (int)FIELD_TOP || y >= (int)FIELD_BOT) {
+      word = WALL * 0x01010101u;
+    } else {
+      const bool agent = y >= pa0 && y < pa0 + (int)PADDLE_H && x0 + 4 > (int)AGENT_X &&
+                         x0 < (int)(AGENT_X + PADDLE_W);
+      const bool opp = y >= po0 && y < po0 + (int)PADDLE_H && x0 + 4 > (int)OPP_X && x0 < (int)(OPP_X + PADDLE_W);
+      const bool ball = y >= by0 && y < by0 + (int)BALL && x0 + 4 > bx0 && x0 < bx0 + (int)BALL;
+      word = BG * 0x01010101u;
+      if (agent || opp || ball) {
+        word = 0;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int p = c * 16 + q, y = p / PW, x = p % PW;
-      uint8_t v = BG;
-      if (y < (int)FIELD_TOP || y >= (int)FIELD_BOT) v = WALL;
-      if (x >= (int)AGENT_X && x < (int)(AGENT_X + PADDLE_W) && y >= pa0 && y < pa0 + (int)PADDLE_H) v = AGENT_C;
-      if (x >= (int)OPP_X && x < (int)(OPP_X + PADDLE_W) && y >= po0 && y < po0 + (int)PADDLE_H) v = OPP_C;
-      if (x >= bx0 && x < bx0 + (int)BALL && y >= by0 && y < by0 + (int)BALL) v = BALL_C;
-      px.b[q] = v;
+        for (int q = 0; q < 4; ++q) {
+          const int x = x0 + q;
+          uint32_t v = BG;
+          if (agent && x >= (int)AGENT_X && x < (int)(AGENT_X + PADDLE_W)) v = AGENT_C;
+          if (opp && x >= (int)OPP_X && x < (int)(OPP_X + PADDLE_W)) v = OPP_C;
+          if (ball && x >= bx0 && x < bx0 + (int)BALL) v = BALL_C;
+          word |= v << (8 * q);
+        }
+      }
     }
-    reinterpret_cast<uint4*>(ov + (size_t)(k - 1) * FRAME)[c] = px.v;
+    ov[(size_t)(k - 1) * NWORDS + w] = word;
     if (done)
-      for (int s2 = 0; s2 < k - 1; ++s2) reinterpret_cast<uint4*>(ov + (size_t)s2 * FRAME)[c] = px.v;
+      for (int s2 = 0; s2 < k - 1; ++s2) ov[(size_t)s2 * NWORDS + w] = word;
   }
 }
 
@@ -177,82 +192,61 @@ __global__ void __launch_bounds__(256) pong_step_kernel(PongIO io, const int32_t
   pong_render(io, e, r.s, r.done != 0);
 }
 
-constexpr int HEAD_KPL = 8;                          // hidden units per lane: hdim <= 512
-constexpr int HEAD_CHUNKS = 20;                      // 16-byte Wh chunks per lane: hdim * (A + 1) <= 10240
-constexpr int HEAD_PASS = 8;                         // chunks in flight per lane per staging pass
+constexpr int HEAD_HDIM = 512;                       // hidden width of the Nature-CNN trunk
 
 // Rollout step of the native engine fused with the env: the policy/value head (z = h.Wh + bh, 512 -> A+1) of
 // env e, Gumbel-max sampling with the env-counter RNG key, logp / entropy / value, then the env step with the
 // sampled action -- one launch instead of head GEMM + sampling + env kernels. Critical path = the head only:
 // wave 0 computes the head and samples, meanwhile wave 1 (lanes 0..2) advances the physics for all three paddle
 // directions and waves 1..3 shift the frame stack; after one barrier the sampled direction's outcome is committed
-// and the newest frame rendered.
-__global__ void __launch_bounds__(256) pong_policy_step_kernel(PongIO io, const u16* __restrict__ h, int hdim,
+// and the newest frame rendered. The head width A1 = A + 1 is a template parameter: lane l owns hidden units
+// 8l..8l+7, whose Wh rows are A1 contiguous 16-byte chunks, so the whole GEMV is register-resident with every
+// load in flight at once and no data-dependent branch (a runtime A1 turned each column into a guarded block and
+// serialised the loads and reductions).
+template <int A1>
+__global__ void __launch_bounds__(256) pong_policy_step_kernel(PongIO io, const u16* __restrict__ h,
                                                                const u16* __restrict__ Wh,
-                                                               const float* __restrict__ bh, int A,
+                                                               const float* __restrict__ bh,
                                                                float* __restrict__ z_out, int32_t* __restrict__ act,
                                                                float* __restrict__ logp, float* __restrict__ ent,
                                                                float* __restrict__ vout, int key_shift,
-                                                               uint32_t pseed, uint64_t* __restrict__ stamps) {
+                                                               uint32_t pseed, int pre_shifted,
+                                                               uint64_t* __restrict__ stamps) {
+  constexpr int A = A1 - 1;
   const int e = blockIdx.x;
-  const int A1 = A + 1;
   __shared__ int sh_act;
   __shared__ PongOut cand[3];
-  __shared__ __attribute__((aligned(16))) u16 s_wh[HEAD_CHUNKS * 64 * 8];
   stamp_if(stamps, 0, threadIdx.x == 0);
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     const int64_t key = io.tglob[e] * ((int64_t)1 << key_shift) + io.env_ids[e];  // pre-step counter
-    // Wh [hdim][A1] arrives as coalesced 16-byte chunks (all in flight together) and is re-read from LDS row-wise;
-    // lane l owns hidden units l, l + 64, ... (one coalesced 2-byte load per 64 units)
-    const int n16 = hdim * A1 / 8;
-    float hv[HEAD_KPL];
+    union { uint4 v[A1]; u16 x[8 * A1]; } w;
+    union { uint4 v; u16 x[8]; } hv;
+    hv.v = reinterpret_cast<const uint4*>(h + (size_t)e * HEAD_HDIM)[lane];
 #pragma unroll
-    for (int q = 0; q < HEAD_KPL; ++q) {
-      const int k = lane + 64 * q;
-      hv[q] = k < hdim ? bf2f(h[(size_t)e * hdim + k]) : 0.f;
-    }
-    for (int base = 0; base < n16; base += 64 * HEAD_PASS) {   // one pass for heads up to 4096 weights
-      uint4 wv[HEAD_PASS];
-#pragma unroll
-      for (int u = 0; u < HEAD_PASS; ++u) {
-        const int c = base + lane + 64 * u;
-        if (c < n16) wv[u] = reinterpret_cast<const uint4*>(Wh)[c];
-      }
-#pragma unroll
-      for (int u = 0; u < HEAD_PASS; ++u) {
-        const int c = base + lane + 64 * u;
-        if (c < n16) reinterpret_cast<uint4*>(s_wh)[c] = wv[u];
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    __builtin_amdgcn_wave_barrier();
+    for (int u = 0; u < A1; ++u) w.v[u] = reinterpret_cast<const uint4*>(Wh)[lane * A1 + u];
     stamp_if(stamps, 8, lane == 0);
-    float acc[20];
+    float acc[A1];
 #pragma unroll
-    for (int j = 0; j < 20; ++j) acc[j] = 0.f;
+    for (int j = 0; j < A1; ++j) acc[j] = 0.f;
 #pragma unroll
-    for (int q = 0; q < HEAD_KPL; ++q) {
-      const int k = lane + 64 * q;
-      if (k < hdim) {
-        const u16* wr = s_wh + k * A1;
+    for (int r = 0; r < 8; ++r) {
+      const float hr = bf2f(hv.x[r]);
 #pragma unroll
-        for (int j = 0; j < 20; ++j)
-          if (j < A1) acc[j] += hv[q] * bf2f(wr[j]);
-      }
+      for (int j = 0; j < A1; ++j) acc[j] += hr * bf2f(w.x[r * A1 + j]);
     }
     stamp_if(stamps, 9, lane == 0);
+#pragma unroll
+    for (int j = 0; j < A1; ++j) acc[j] = wave_sum(acc[j]);
     float zj = 0.f;
 #pragma unroll
-    for (int j = 0; j < 20; ++j) {
-      if (j < A1) {
-        const float v = wave_sum(acc[j]);
-        if (lane == j) zj = v + bh[j];
-      }
+    for (int j = 0; j < A1; ++j) zj = (lane == j) ? acc[j] : zj;
+    if (lane < A1) {
+      zj += bh[lane];
+      z_out[(size_t)e * A1 + lane] = zj;
     }
-    if (lane < A1) z_out[(size_t)e * A1 + lane] = zj;
     stamp_if(stamps, 10, lane == 0);
-    const float value = __shfl(zj, A, 64);
+    const float value = acc[A] + bh[A];
     // categorical head over lanes 0..A-1 (same maths as categorical_sample_kernel)
     const bool on = lane < A;
     const float z = on ? zj : -INFINITY;
@@ -283,7 +277,7 @@ __global__ void __launch_bounds__(256) pong_policy_step_kernel(PongIO io, const 
   } else {
     if (threadIdx.x < 64 + 3) cand[threadIdx.x - 64] = pong_advance(io, e, (float)((int)threadIdx.x - 65));
     stamp_if(stamps, 2, threadIdx.x == 64);
-    pong_shift(io, e, 64, blockDim.x - 64);
+    if (!pre_shifted) pong_shift(io, e, 64, blockDim.x - 64);   // else the trunk kernel already shifted the stack
     stamp_if(stamps, 3, threadIdx.x == 64);
   }
   __syncthreads();
@@ -327,14 +321,25 @@ extern "C" hipError_t aca_env_policy_step_pong(const uint16_t* h, int hdim, cons
                                                float* ep_ret, float* ep_stats, const int64_t* ids,
                                                const uint8_t* prev, uint8_t* out, float* reward, uint8_t* done,
                                                uint8_t* trunc, uint32_t seed, int max_steps, int k, int N,
-                                               uint64_t* stamps, hipStream_t stream) {
+                                               int pre_shifted, uint64_t* stamps, hipStream_t stream) {
   if (N <= 0) return hipSuccess;
-  if (A + 1 > 20 || hdim > 64 * aca::HEAD_KPL || hdim * (A + 1) > aca::HEAD_CHUNKS * 64 * 8 || (hdim * (A + 1)) % 8 ||
-      reinterpret_cast<uintptr_t>(Wh) % 16)
+  if (hdim != aca::HEAD_HDIM || reinterpret_cast<uintptr_t>(Wh) % 16 || reinterpret_cast<uintptr_t>(h) % 16)
     return hipErrorInvalidValue;
   aca::PongIO io = make_pong_io(state, t, tg, ep_ret, ep_stats, ids, prev, out, reward, done, trunc, seed, max_steps,
                                 k);
-  aca::pong_policy_step_kernel<<<N, 256, 0, stream>>>(io, h, hdim, Wh, bh, A, z, act, logp, ent, value, key_shift,
-                                                      pseed, stamps);
+  switch (A + 1) {
+#define ACA_POLICY_CASE(A1)                                                                                         \
+  case A1:                                                                                                          \
+    aca::pong_policy_step_kernel<A1><<<N, 256, 0, stream>>>(io, h, Wh, bh, z, act, logp, ent, value, key_shift,    \
+                                                            pseed, pre_shifted, stamps);                            \
+    break;
+    ACA_POLICY_CASE(3) ACA_POLICY_CASE(4) ACA_POLICY_CASE(5) ACA_POLICY_CASE(6) ACA_POLICY_CASE(7)
+    ACA_POLICY_CASE(8) ACA_POLICY_CASE(9) ACA_POLICY_CASE(10) ACA_POLICY_CASE(11) ACA_POLICY_CASE(12)
+    ACA_POLICY_CASE(13) ACA_POLICY_CASE(14) ACA_POLICY_CASE(15) ACA_POLICY_CASE(16) ACA_POLICY_CASE(17)
+    ACA_POLICY_CASE(18) ACA_POLICY_CASE(19) ACA_POLICY_CASE(20)
+#undef ACA_POLICY_CASE
+    default:
+      return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }

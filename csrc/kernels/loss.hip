@@ -59,7 +59,11 @@ constexpr int CAT_MAX = 20;        // categorical heads: logits + value columns 
 // (rollout rewards / dones / values into LDS, each thread's logits row + action + old log-prob into registers),
 // the returns recursion and the row maths then run out of LDS/registers; global writes (dz, targets for logging)
 // are fire-and-forget.
+// AC > 0: categorical head with AC actions fixed at compile time (the per-column loops lose their guards, so the
+// row's loads and exp/log chains are scheduled together); AC == 0: any head (runtime A, gaussian).
+template <int AC>
 __global__ void __launch_bounds__(LOSS_THREADS) ac_loss_kernel(LossArgs a) {
+  constexpr int NJ = AC ? AC : CAT_MAX;
   __shared__ double sh[16 * 8];
   __shared__ float dls[64];
   __shared__ float dbs[64];
@@ -148,7 +152,7 @@ __global__ void __launch_bounds__(LOSS_THREADS) ac_loss_kernel(LossArgs a) {
     float zr[CAT_MAX];
     if (!a.gaussian) {
 #pragma unroll
-      for (int j = 0; j < CAT_MAX; ++j) zr[j] = j < a.A ? z[j] : -INFINITY;
+      for (int j = 0; j < NJ; ++j) zr[j] = (AC || j < a.A) ? z[j] : -INFINITY;
     }
     const int ab = a.gaussian ? 0 : a.act_i[b];
     const float lpo = a.logp_old[b];
@@ -160,17 +164,17 @@ __global__ void __launch_bounds__(LOSS_THREADS) ac_loss_kernel(LossArgs a) {
     if (!a.gaussian) {
       float mx = -INFINITY;
 #pragma unroll
-      for (int j = 0; j < CAT_MAX; ++j) mx = fmaxf(mx, zr[j]);
+      for (int j = 0; j < NJ; ++j) mx = fmaxf(mx, zr[j]);
       float se = 0.f;
 #pragma unroll
-      for (int j = 0; j < CAT_MAX; ++j) se += j < a.A ? expf(zr[j] - mx) : 0.f;
+      for (int j = 0; j < NJ; ++j) se += (AC || j < a.A) ? expf(zr[j] - mx) : 0.f;
       lse = mx + logf(se);
 #pragma unroll
-      for (int j = 0; j < CAT_MAX; ++j) {
-        if (j < a.A) {
+      for (int j = 0; j < NJ; ++j) {
+        if (AC || j < a.A) {
           const float lz = zr[j] - lse;
           H -= expf(lz) * lz;
-          if (j == ab) lpa = lz;
+          lpa = (j == ab) ? lz : lpa;
         }
       }
     } else {
@@ -205,8 +209,8 @@ __global__ void __launch_bounds__(LOSS_THREADS) ac_loss_kernel(LossArgs a) {
     u16* dz = a.dlogits + (int64_t)b * a.lddl;
     if (!a.gaussian) {
 #pragma unroll
-      for (int j = 0; j < CAT_MAX; ++j) {
-        if (j < a.A) {
+      for (int j = 0; j < NJ; ++j) {
+        if (AC || j < a.A) {
           const float oh = (j == ab) ? 1.0f : 0.0f;
           const float lz = zr[j] - lse, pj = expf(lz);
           const float g = g_lpa * (oh - pj) + c_ent * invB * pj * (lz + H);
@@ -244,9 +248,13 @@ __global__ void __launch_bounds__(LOSS_THREADS) ac_loss_kernel(LossArgs a) {
       const u16 gvb = f2bf(a.vf_coef * gv * invB);
       a.dvalue[(int64_t)b * a.lddv] = gvb;
       // the value column is column A of the fused head (dbias_n == A + 1)
+      if (AC) {
+        dbp[AC] += bf2f(gvb);
+      } else {
 #pragma unroll
-      for (int q = 0; q <= CAT_MAX; ++q)
-        if (q == a.A) dbp[q] += bf2f(gvb);
+        for (int q = 0; q <= CAT_MAX; ++q)
+          if (q == a.A) dbp[q] += bf2f(gvb);
+      }
     }
   }
   {
@@ -300,6 +308,17 @@ extern "C" hipError_t aca_ac_loss(const float* logits, int64_t ldl, const float*
   a.gaussian = gaussian;
   a.returns_mode = returns_mode; a.rew = rew; a.val = val; a.dn = dn; a.T = T; a.N = N; a.L = L; a.gamma = gamma;
   a.lam = lam; a.norm_adv = norm_adv; a.ret_w = ret_w; a.adv_w = adv_w; a.dbias = dbias; a.dbias_n = dbias_n;
-  aca::ac_loss_kernel<<<1, aca::LOSS_THREADS, 0, stream>>>(a);
+  if (!gaussian && A >= 2 && A <= 19) {
+    switch (A) {
+#define ACA_LOSS_CASE(n) \
+  case n: aca::ac_loss_kernel<n><<<1, aca::LOSS_THREADS, 0, stream>>>(a); break;
+      ACA_LOSS_CASE(2) ACA_LOSS_CASE(3) ACA_LOSS_CASE(4) ACA_LOSS_CASE(5) ACA_LOSS_CASE(6) ACA_LOSS_CASE(7)
+      ACA_LOSS_CASE(8) ACA_LOSS_CASE(9) ACA_LOSS_CASE(10) ACA_LOSS_CASE(11) ACA_LOSS_CASE(12) ACA_LOSS_CASE(13)
+      ACA_LOSS_CASE(14) ACA_LOSS_CASE(15) ACA_LOSS_CASE(16) ACA_LOSS_CASE(17) ACA_LOSS_CASE(18) ACA_LOSS_CASE(19)
+#undef ACA_LOSS_CASE
+    }
+  } else {
+    aca::ac_loss_kernel<0><<<1, aca::LOSS_THREADS, 0, stream>>>(a);
+  }
   return hipGetLastError();
 }

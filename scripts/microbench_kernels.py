@@ -68,8 +68,9 @@ def main():
     lb = eng.bufs(N * st.T, with_grad=True)
     bt = lb.rows(0, N)
     res = {}
+    shift_scratch = st.obs[1].clone()
     trunk = lambda stamps=None: ops.cnn_trunk_fwd(st.obs[0], eng.sW1, eng.b1, eng.sW2, eng.b2, eng.sW3, eng.b3,  # noqa
-                                                  bt.y1, bt.y2, bt.y3, 1.0 / 255.0, stamps)
+                                                  bt.y1, bt.y2, bt.y3, 1.0 / 255.0, shift_scratch, stamps)
     res["trunk_chained_us"] = graph_time(trunk)
     fc = lambda: G.gemm(bt.y3, 3136, True, eng.sWfc, 512, False, bt.h, 512, 1, N, 512, 3136, bias=eng.bfc,  # noqa
                         relu=True, workspace=eng.ws)
@@ -84,7 +85,7 @@ def main():
         ops.env_policy_step_pong(bt.h, eng.sWh, eng.bh, bt.z, act, logp, ent, val, KEY_ENV_BITS, tr.policy_seed,
                                  scratch["state"], scratch["t"], scratch["tg"], scratch["ep_ret"], scratch["ep_stats"],
                                  env.env_ids, prev, out, rew, done, trunc, env.seed, env.max_episode_steps,
-                                 env.frame_stack, stamps)
+                                 env.frame_stack, True, stamps)
     res["policy_step_chained_us"] = graph_time(pstep)
     opt = tr.actor_opt
     parts = torch.zeros(256, device=eng.dev)

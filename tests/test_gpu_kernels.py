@@ -412,7 +412,7 @@ def test_fused_policy_env_step_matches_separate_kernels(cuda):
     Wh = (torch.randn(512 * (A + 1), generator=g) * 0.05).to(torch.bfloat16).to(cuda)
     bh = torch.randn(A + 1, generator=g).to(cuda)
     outs = []
-    for fused in (True, False):
+    for fused in (True, False, "pre_shifted"):
         env = E.make("PongNoFrameskip-v4", N, device=cuda, seed=3)
         o0 = env.reset().clone()
         o1 = torch.empty_like(o0)
@@ -421,7 +421,16 @@ def test_fused_policy_env_step_matches_separate_kernels(cuda):
         z = torch.empty(N, A + 1, device=cuda)
         rew = torch.empty(N, device=cuda)
         dn, tr = (torch.empty(N, dtype=torch.uint8, device=cuda) for _ in range(2))
-        if fused:
+        if fused == "pre_shifted":
+            # the fused trunk writes the shifted stack into o1, the env kernel then only renders the newest frame
+            W = [(torch.randn(n, generator=g) * 0.05).to(torch.bfloat16).to(cuda) for n in (8192, 32768, 36864)]
+            bb = [torch.zeros(n, device=cuda) for n in (32, 64, 64)]
+            ys = [torch.empty(N * r, c, dtype=torch.bfloat16, device=cuda) for r, c in ((400, 32), (81, 64), (49, 64))]
+            ops.cnn_trunk_fwd(o0, W[0], bb[0], W[1], bb[1], W[2], bb[2], ys[0], ys[1], ys[2], 1.0 / 255.0, o1)
+            ops.env_policy_step_pong(h, Wh, bh, z, act, lp, en, val, 20, 77, env.state, env.t, env.tg, env.ep_ret,
+                                     env.ep_stats, env.env_ids, o0, o1, rew, dn, tr, env.seed,
+                                     env.max_episode_steps, 4, True)
+        elif fused:
             ops.env_policy_step_pong(h, Wh, bh, z, act, lp, en, val, 20, 77, env.state, env.t, env.tg, env.ep_ret,
                                      env.ep_stats, env.env_ids, o0, o1, rew, dn, tr, env.seed,
                                      env.max_episode_steps, 4)
@@ -431,7 +440,8 @@ def test_fused_policy_env_step_matches_separate_kernels(cuda):
             val = z[:, A].clone()
             env.step(act, prev_obs=o0, obs_out=o1, reward_out=rew, done_out=dn, trunc_out=tr)
         outs.append((act.clone(), lp.clone(), en.clone(), val.clone(), o1.clone(), z.clone()))
-    (a0, l0, e0, v0, f0, z0), (a1, l1, e1, v1, f1, z1) = outs
+    (a0, l0, e0, v0, f0, z0), (a1, l1, e1, v1, f1, z1), (a2, l2, e2, v2, f2, z2) = outs
+    assert torch.equal(a0, a2) and torch.equal(f0, f2) and torch.equal(z0, z2) and torch.equal(l0, l2)
     assert torch.allclose(z0, z1, atol=2e-3)
     same = a0 == a1
     assert same.float().mean() >= 0.9

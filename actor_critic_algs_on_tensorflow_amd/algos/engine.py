@@ -92,6 +92,10 @@ class CNNEngine:
         self.fused_trunk_max_b = 4096 if fused_trunk_max_b is None else fused_trunk_max_b
         # rollout frame-stack shift inside the fused trunk (else the env kernel shifts); A/B switch for profiling
         self.trunk_shift = os.environ.get("ACA_TRUNK_SHIFT", "1") != "0"
+        # rollout fc product left as split-K partial planes, reduced by its consumer kernel (no in-launch fence)
+        self.fc_parts = os.environ.get("ACA_FC_PARTS", "1") != "0"
+        self._hpart = {}
+        self.last_fc = None
         self.model = model
         self.flat = flat
         self.shadow = shadow
@@ -129,15 +133,26 @@ class CNNEngine:
         return self._bufs[key]
 
     # ------------------------------------------------------------------------------------------------ forward
+    def hpart(self, B):
+        """fp32 [8, B, 512] split-K partial planes of the rollout fc product (GEMM out_mode 3)."""
+        if B not in self._hpart:
+            self._hpart[B] = torch.zeros(8 * B * 512, dtype=torch.float32, device=self.dev)
+        return self._hpart[B]
+
     def value(self, obs, b: _Bufs, out):
         """Bootstrap value of ``obs`` written straight into ``out`` [B] (trunk + the value column of the head)."""
+        if self.fc_parts:
+            self.forward(obs, b, head=False, fc_parts=True)
+            hp, S = self.last_fc
+            _native.require().fc_value(hp, S, self.bfc, self.sWh, self.bh, out, None)
+            return out
         self.forward(obs, b, head=False)
         A, A1 = self.A, self.A1
         G.gemm(b.h, 512, True, self.sWh[A:], A1, False, out, 1, 0, b.B, 1, 512, bias=self.bh[A:],
                workspace=self.ws)
         return out
 
-    def forward(self, obs, b: _Bufs, head=True, shift_out=None):
+    def forward(self, obs, b: _Bufs, head=True, shift_out=None, fc_parts=False):
         """obs uint8 [B, 4, 84, 84] -> b.z fp32 [B, A+1] (logits | value); ``head=False`` stops at ``b.h`` (the
         rollout fuses the head into the sampling + env-step kernel). ``shift_out``: the next observation buffer,
         whose frames 0..2 the fused trunk fills with frames 1..3 of ``obs``; returns True iff it did."""
@@ -169,6 +184,13 @@ class CNNEngine:
             G.im2col_nhwc(b.y2, b.col3, B, 9, 9, 64, 3, 3, 1)
             G.gemm(b.col3, 576, True, self.sW3, 576, True, b.y3, 64, 1, B * 49, 64, 576, bias=self.b3, relu=True,
                    workspace=ws)
+        if fc_parts and not head:
+            # partial planes only: the consumer (fused policy/env kernel or fc_value) reduces, adds the bias,
+            # applies ReLU and writes b.h
+            hp = self.hpart(B)
+            S = G.gemm(b.y3, 3136, True, self.sWfc, 512, False, hp, 512, 3, B, 512, 3136, workspace=ws)
+            self.last_fc = (hp, S)
+            return shifted if want_shift else b.z
         G.gemm(b.y3, 3136, True, self.sWfc, 512, False, b.h, 512, 1, B, 512, 3136, bias=self.bfc, relu=True,
                workspace=ws)
         if head:

@@ -158,12 +158,15 @@ class ActorCriticTrainer:
             if fused:
                 # conv trunk + fc, then ONE launch: policy/value head + sampling + env step (+ frame render)
                 # (the fused trunk also shifts the frame stack into obs[t + 1]; the env kernel renders the newest)
-                shifted = eng.forward(st.obs[t], bt, head=False, shift_out=st.obs[t + 1])
+                # (and leaves the fc product as split-K planes that the env kernel reduces into bt.h)
+                shifted = eng.forward(st.obs[t], bt, head=False, shift_out=st.obs[t + 1], fc_parts=eng.fc_parts)
+                hp, S = eng.last_fc if eng.fc_parts else (None, 0)
                 ops.env_policy_step_pong(bt.h, eng.sWh, eng.bh, bt.z, st.actions[t], st.logp[t], st.entropy[t],
                                          st.values[t], KEY_ENV_BITS, self.policy_seed, env.state, env.t, env.tg,
                                          env.ep_ret, env.ep_stats, env.env_ids, st.obs[t], st.obs[t + 1],
                                          st.rewards[t], st.dones[t], st.truncated[t], env.seed,
-                                         env.max_episode_steps, env.frame_stack, shifted)
+                                         env.max_episode_steps, env.frame_stack, shifted, hp, S,
+                                         eng.bfc if hp is not None else None)
                 continue
             z = eng.forward(st.obs[t], bt)
             # one launch: sample + logp + entropy + value copy, RNG keys from the env counters

@@ -84,6 +84,7 @@ class GemmWorkspace:
 # k-steps each serial chain has to walk. Each new shape is timed once on its first (eager, never captured) call
 # against scratch outputs and the winner is cached for the process. ACAMD_GEMM_TUNE=0 uses :func:`plan`.
 _TUNED: dict = {}
+PARTIAL_MAX_SPLITS = 8   # out_mode 3: the consumer kernels reduce at most this many partial planes
 TUNE = os.environ.get("ACAMD_GEMM_TUNE", "1") == "1"
 
 
@@ -91,7 +92,7 @@ def tuned_plans():
     return dict(_TUNED)
 
 
-def _candidates(M, N, K, atomic):
+def _candidates(M, N, K, atomic, max_splits=None):
     for tile, (bm, bn) in TILES.items():
         if bm >= 2 * max(32, M) or bn >= 2 * max(32, N):
             continue  # a tile at least twice the problem in one dimension only wastes MFMA issue
@@ -104,6 +105,8 @@ def _candidates(M, N, K, atomic):
                     break
                 if not atomic and s > 16:
                     break
+                if max_splits is not None and s > max_splits:
+                    break
                 yield tile, bk, s
 
 
@@ -111,7 +114,7 @@ def _run(ops, A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha, bias, 
          colsum_mod, tile, bk, splits, workspace, ga, ga_scale, gb, gb_scale):
     eff = effective_splits(K, bk, splits)
     ws = tk = None
-    if eff > 1 and out_mode != 2:
+    if eff > 1 and out_mode < 2:
         if workspace is None:
             raise ValueError("slab split-K needs a GemmWorkspace")
         e, t = workspace_elems(M, N, tile, eff)
@@ -120,17 +123,19 @@ def _run(ops, A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha, bias, 
     ops.gemm(A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, float(alpha), bias, bool(relu), mask, ldm,
              colsum, int(colsum_mod), tile, bk, splits, ws, tk, list(ga or []), float(ga_scale), list(gb or []),
              float(gb_scale))
+    return eff
 
 
 def _tune(key, ops, A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha, bias, relu, mask, ldm, colsum,
           colsum_mod, workspace, ga, ga_scale, gb, gb_scale):
     dev = C.device
-    Cs = torch.zeros((M - 1) * ldc + N, dtype=C.dtype, device=dev)
+    planes = PARTIAL_MAX_SPLITS if out_mode == 3 else 1
+    Cs = torch.zeros(planes * M * ldc, dtype=C.dtype, device=dev)
     cs = torch.zeros(max(N, colsum_mod or 0), dtype=torch.float32, device=dev) if colsum is not None else None
     ws = workspace if workspace is not None else GemmWorkspace(dev)
     best = None
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    for tile, bk, s in _candidates(M, N, K, out_mode == 2):
+    for tile, bk, s in _candidates(M, N, K, out_mode == 2, PARTIAL_MAX_SPLITS if out_mode == 3 else None):
         args = (ops, A, lda, a_k, B, ldb, b_k, Cs, ldc, out_mode, M, N, K, alpha, bias, relu, mask, ldm, cs,
                 colsum_mod, tile, bk, s, ws, ga, ga_scale, gb, gb_scale)
         _run(*args)
@@ -151,7 +156,8 @@ def _tune(key, ops, A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha, 
 def gemm(A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha=1.0, bias=None, relu=False, mask=None, ldm=0,
          colsum=None, tile=None, splits=None, workspace: GemmWorkspace | None = None, colsum_mod=0, bk=None,
          ga=None, ga_scale=1.0, gb=None, gb_scale=1.0):
-    """Native GEMM; ``out_mode``: 0 fp32 store, 1 bf16 store, 2 fp32 atomic add (C pre-zeroed).
+    """Native GEMM; ``out_mode``: 0 fp32 store, 1 bf16 store, 2 fp32 atomic add (C pre-zeroed), 3 fp32 split-K
+    partial planes ``C[z, M, ldc]`` (no bias/activation: the consumer reduces). Returns the effective split count.
 
     ``ga`` / ``gb``: implicit-im2col gathers ``[mode, B, C, H, W, KH, KW, S]`` (mode 1 uint8 NCHW, 2 bf16 NHWC)
     reading operand A (k-contiguous) / B (n-contiguous) straight from the activation image ``A`` / ``B``.
@@ -167,13 +173,17 @@ def gemm(A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha=1.0, bias=No
                             ldm, colsum, colsum_mod, workspace, ga, ga_scale, gb, gb_scale)
         else:
             t, k, s = plan(M, N, K, atomic=(out_mode == 2))
+            if out_mode == 3:
+                s = min(s, PARTIAL_MAX_SPLITS)
         tile = t if tile is None else tile
         bk = k if bk is None else bk
         splits = s if splits is None else splits
     if colsum_mod and colsum is None:
         raise ValueError("colsum_mod without colsum")
-    _run(ops, A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha, bias, relu, mask, ldm, colsum, colsum_mod,
-         tile, bk, splits, workspace, ga, ga_scale, gb, gb_scale)
+    if out_mode == 3 and effective_splits(K, bk, splits) > PARTIAL_MAX_SPLITS:
+        raise ValueError("out_mode 3 supports at most %d partial planes" % PARTIAL_MAX_SPLITS)
+    return _run(ops, A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha, bias, relu, mask, ldm, colsum,
+                colsum_mod, tile, bk, splits, workspace, ga, ga_scale, gb, gb_scale)
 
 
 def _view(t, rows, cols, ld, k_contig_rows):

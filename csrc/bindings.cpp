@@ -28,7 +28,10 @@ hipError_t aca_env_step_linear(float*, int32_t*, int64_t*, float*, float*, const
 hipError_t aca_env_step_pong(float*, int32_t*, int64_t*, float*, float*, const int64_t*, const int32_t*,
                              const uint8_t*, uint8_t*, float*, uint8_t*, uint8_t*, uint32_t, int, int, int,
                              hipStream_t);
-hipError_t aca_env_policy_step_pong(const uint16_t*, int, const uint16_t*, const float*, int, float*, int32_t*,
+hipError_t aca_fc_value(const float*, int, int64_t, const float*, const uint16_t*, int, const float*, float*,
+                        uint16_t*, int, hipStream_t);
+hipError_t aca_env_policy_step_pong(uint16_t*, const float*, int, int64_t, const float*, int, const uint16_t*,
+                                    const float*, int, float*, int32_t*,
                                     float*, float*, float*, int, uint32_t, float*, int32_t*, int64_t*, float*, float*,
                                     const int64_t*, const uint8_t*, uint8_t*, float*, uint8_t*, uint8_t*, uint32_t,
                                     int, int, int, int, uint64_t*, hipStream_t);
@@ -189,6 +192,7 @@ void env_policy_step_pong(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, 
                           Tensor value, int64_t key_shift, int64_t pseed, Tensor state, Tensor t, Tensor tg,
                           Tensor ep_ret, Tensor ep_stats, Tensor ids, Tensor prev, Tensor out, Tensor reward,
                           Tensor done, Tensor trunc, int64_t seed, int64_t max_steps, int64_t k, bool pre_shifted,
+                          c10::optional<Tensor> hpart, int64_t planes, c10::optional<Tensor> bfc,
                           c10::optional<Tensor> stamps) {
   check_env(state, t, tg, ep_ret, ep_stats, ids, reward, done, trunc);
   need(h, at::kBFloat16, "h");
@@ -212,7 +216,21 @@ void env_policy_step_pong(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, 
               "env_policy_step_pong: 2..19 actions, hidden size 512, h and Wh 16-byte aligned");
   TORCH_CHECK(prev.numel() == (int64_t)N * k * 84 * 84 && out.numel() == prev.numel(), "pong: bad stack shape");
   TORCH_CHECK(prev.data_ptr() != out.data_ptr(), "pong: prev and out must not alias");
-  check(aca_env_policy_step_pong(ptr<uint16_t>(h), hdim, ptr<uint16_t>(Wh), ptr<float>(bh), A, ptr<float>(z),
+  const float* hp = nullptr;
+  const float* bf = nullptr;
+  int64_t pstride = 0;
+  if (hpart.has_value() && hpart->defined()) {
+    need(*hpart, at::kFloat, "hpart");
+    TORCH_CHECK(bfc.has_value() && bfc->defined() && bfc->numel() == hdim, "env_policy_step_pong: hpart needs bfc");
+    need(*bfc, at::kFloat, "bfc");
+    TORCH_CHECK(planes >= 1 && planes <= 8 && hpart->numel() % 8 == 0, "env_policy_step_pong: 1..8 planes");
+    pstride = hpart->numel() / 8;   // buffer holds 8 planes of equal size
+    TORCH_CHECK(pstride >= (int64_t)N * hdim, "env_policy_step_pong: hpart planes too small");
+    hp = ptr<float>(*hpart);
+    bf = ptr<float>(*bfc);
+  }
+  check(aca_env_policy_step_pong(ptr<uint16_t>(h), hp, (int)planes, pstride, bf, hdim, ptr<uint16_t>(Wh),
+                                 ptr<float>(bh), A, ptr<float>(z),
                                  ptr<int32_t>(act), ptr<float>(logp), ptr<float>(ent), ptr<float>(value),
                                  (int)key_shift, (uint32_t)pseed, ptr<float>(state), ptr<int32_t>(t),
                                  ptr<int64_t>(tg), ptr<float>(ep_ret), ptr<float>(ep_stats), ptr<int64_t>(ids),
@@ -220,6 +238,29 @@ void env_policy_step_pong(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, 
                                  ptr<uint8_t>(trunc), (uint32_t)seed, (int)max_steps, (int)k, N, pre_shifted ? 1 : 0,
                                  stamps_ptr(stamps, N), cur_stream(state)),
         "env_policy_step_pong");
+}
+
+// bootstrap value from the fc partial planes (cnn_fused.hip); hpart holds 8 equal planes of [N, 512]
+void fc_value(Tensor hpart, int64_t planes, Tensor bfc, Tensor Wh, Tensor bh, Tensor out, c10::optional<Tensor> h_out) {
+  need(hpart, at::kFloat, "hpart");
+  need(bfc, at::kFloat, "bfc");
+  need(Wh, at::kBFloat16, "Wh");
+  need(bh, at::kFloat, "bh");
+  need(out, at::kFloat, "out");
+  const int N = out.numel(), A1 = bh.numel();
+  const int64_t pstride = hpart.numel() / 8;
+  TORCH_CHECK(hpart.numel() % 8 == 0 && pstride >= (int64_t)N * 512 && planes >= 1 && planes <= 8,
+              "fc_value: hpart must hold 8 planes of [N, 512]");
+  TORCH_CHECK(bfc.numel() == 512 && Wh.numel() == 512 * A1, "fc_value: bad head shapes");
+  uint16_t* ho = nullptr;
+  if (h_out.has_value() && h_out->defined()) {
+    need(*h_out, at::kBFloat16, "h_out");
+    TORCH_CHECK(h_out->numel() >= (int64_t)N * 512, "fc_value: h_out too small");
+    ho = ptr<uint16_t>(*h_out);
+  }
+  check(aca_fc_value(ptr<float>(hpart), (int)planes, pstride, ptr<float>(bfc), ptr<uint16_t>(Wh), A1, ptr<float>(bh),
+                     ptr<float>(out), ho, N, cur_stream(out)),
+        "fc_value");
 }
 
 // ---------------------------------------------------------------------------------------------- heads
@@ -415,6 +456,7 @@ AcaConvGather make_gather(const Tensor& src, const std::vector<int64_t>& spec, d
   g.OH = (g.H - g.KH) / g.S + 1;
   g.OW = (g.W - g.KW) / g.S + 1;
   g.scale = (float)scale;
+  aca_gather_prepare(&g);
   TORCH_CHECK(src.is_contiguous(), "gemm: gather source ", name, " must be contiguous");
   if (g.mode == 3) {
     TORCH_CHECK(g.OH > 0 && g.OW > 0, "gemm: gather mode 3 bad geometry");
@@ -447,7 +489,11 @@ void gemm(Tensor A, int64_t lda, bool a_k, Tensor B, int64_t ldb, bool b_k, Tens
           c10::optional<Tensor> mask, int64_t ldm, c10::optional<Tensor> colsum, int64_t colsum_mod, int64_t tile,
           int64_t bk, int64_t splits, c10::optional<Tensor> ws, c10::optional<Tensor> tickets,
           std::vector<int64_t> ga, double ga_scale, std::vector<int64_t> gb, double gb_scale) {
-  TORCH_CHECK(out_mode >= 0 && out_mode <= 2, "gemm: bad out_mode");
+  TORCH_CHECK(out_mode >= 0 && out_mode <= 3, "gemm: bad out_mode");
+  if (out_mode == 3)
+    TORCH_CHECK(!(bias.has_value() && bias->defined()) && !relu && !(mask.has_value() && mask->defined()) &&
+                    !(colsum.has_value() && colsum->defined()),
+                "gemm: out_mode 3 (partial planes) takes no bias / relu / mask / colsum");
   TORCH_CHECK(aca_gemm_supported((int)tile, (int)bk), "gemm: unsupported tile ", tile, " / bk ", bk);
   TORCH_CHECK(C.scalar_type() == (out_mode == 1 ? at::kBFloat16 : at::kFloat), "gemm: C dtype mismatch");
   AcaGemmDesc d{};
@@ -478,7 +524,8 @@ void gemm(Tensor A, int64_t lda, bool a_k, Tensor B, int64_t ldb, bool b_k, Tens
     TORCH_CHECK(B.scalar_type() == at::kBFloat16, "gemm: B must be bf16");
     check_extent(B, b_k ? N : K, b_k ? K : N, ldb, "B");
   }
-  check_extent(C, M, N, ldc, "C");
+  if (out_mode == 3) check_extent(C, aca_gemm_effective_splits((int)K, (int)bk, (int)splits) * M, N, ldc, "C");
+  else check_extent(C, M, N, ldc, "C");
   if (bias.has_value() && bias->defined()) {
     TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() >= N, "gemm: bias must be fp32 [N]");
   }
@@ -491,7 +538,7 @@ void gemm(Tensor A, int64_t lda, bool a_k, Tensor B, int64_t ldb, bool b_k, Tens
                 "gemm: colsum too small");
   }
   const int eff = aca_gemm_effective_splits((int)K, (int)bk, (int)splits);
-  if (eff > 1 && out_mode != 2) {
+  if (eff > 1 && out_mode < 2) {
     TORCH_CHECK(ws.has_value() && ws->defined() && tickets.has_value() && tickets->defined(),
                 "gemm: slab split-K needs ws and tickets");
     int bm, bn;
@@ -677,7 +724,9 @@ TORCH_LIBRARY(acamd, m) {
   m.def("env_policy_step_pong(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, Tensor logp, Tensor ent, "
         "Tensor value, int key_shift, int pseed, Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, "
         "Tensor env_ids, Tensor prev, Tensor out, Tensor reward, Tensor done, Tensor truncated, int seed, "
-        "int max_steps, int k, bool pre_shifted=False, Tensor? stamps=None) -> ()");
+        "int max_steps, int k, bool pre_shifted=False, Tensor? hpart=None, int planes=0, Tensor? bfc=None, "
+        "Tensor? stamps=None) -> ()");
+  m.def("fc_value(Tensor hpart, int planes, Tensor bfc, Tensor Wh, Tensor bh, Tensor out, Tensor? h_out) -> ()");
   m.def("categorical_sample(Tensor logits, Tensor keys, int seed, Tensor act, Tensor logp, Tensor ent) -> ()");
   m.def("categorical_sample_env(Tensor logits, Tensor tg, Tensor env_ids, int key_shift, int seed, Tensor act, "
         "Tensor logp, Tensor ent, Tensor? vout) -> ()");
@@ -734,6 +783,7 @@ TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
   m.impl("cast_bf16", &cast_bf16);
   m.impl("gemm", &gemm);
   m.impl("cnn_trunk_fwd", &cnn_trunk_fwd);
+  m.impl("fc_value", &fc_value);
   m.impl("im2col_u8", &im2col_u8);
   m.impl("im2col_nhwc", &im2col_nhwc);
   m.impl("col2im_nhwc", &col2im_nhwc);

@@ -18,6 +18,7 @@
 // the conv1 epilogue (one conversion per pixel instead of one per im2col element). Work split: conv1 -- waves take M tiles round-robin and both N tiles; conv2/3 -- wave w
 // owns output-channel tile w for every M tile, so every B fragment is loaded exactly once per workgroup.
 #include "common.h"
+#include "cnn_head.h"
 
 namespace aca {
 
@@ -224,7 +225,40 @@ __global__ void __launch_bounds__(T_THREADS) cnn_trunk_fwd_kernel(
   }
 }
 
+// Bootstrap value V(s_T) straight from the fc partial planes: one wave per env, h = relu(sum planes + bfc)
+// (bf16-rounded like the GEMM epilogue), value = h . Wh[:, A] + bh[A]. Replaces GEMM-reduce + value GEMM.
+__global__ void __launch_bounds__(256) fc_value_kernel(const float* __restrict__ hpart, int S, int64_t plane_stride,
+                                                       const float* __restrict__ bfc, const u16* __restrict__ Wh,
+                                                       int A1, const float* __restrict__ bh, float* __restrict__ out,
+                                                       u16* __restrict__ h_out, int N) {
+  const int lane = threadIdx.x & 63;
+  const int e = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (e >= N) return;
+  const int A = A1 - 1;
+  float wv[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) wv[r] = bf2f(Wh[(lane * 8 + r) * A1 + A]);
+  float hv[8];
+  fc_h_from_parts(hpart, S, plane_stride, bfc, e, lane, h_out, hv);
+  float acc = 0.f;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) acc += hv[r] * wv[r];
+  acc = wave_sum(acc);
+  if (lane == 0) out[e] = acc + bh[A];
+}
+
 }  // namespace aca
+
+extern "C" hipError_t aca_fc_value(const float* hpart, int S, int64_t plane_stride, const float* bfc,
+                                   const uint16_t* Wh, int A1, const float* bh, float* out, uint16_t* h_out, int N,
+                                   hipStream_t stream) {
+  if (N <= 0) return hipSuccess;
+  if (S < 1 || S > aca::FC_MAX_PLANES || reinterpret_cast<uintptr_t>(hpart) % 16 ||
+      reinterpret_cast<uintptr_t>(bfc) % 16 || plane_stride % 4)
+    return hipErrorInvalidValue;
+  aca::fc_value_kernel<<<(N + 3) / 4, 256, 0, stream>>>(hpart, S, plane_stride, bfc, Wh, A1, bh, out, h_out, N);
+  return hipGetLastError();
+}
 
 extern "C" hipError_t aca_cnn_trunk_fwd(const uint8_t* obs, const uint16_t* W1, const float* b1, const uint16_t* W2,
                                         const float* b2, const uint16_t* W3, const float* b3, uint16_t* y1,

@@ -1,0 +1,54 @@
+// Consumer side of the rollout's fc product (Nature-CNN hidden layer, 512 units): the fc GEMM leaves its split-K
+// partial sums as fp32 planes (GEMM out_mode 3, no in-launch reduction / fence); the kernel that needs h sums the
+// planes in plane order (deterministic), adds the bias, applies ReLU and rounds to bf16 -- exactly the GEMM
+// epilogue it replaces -- and stores the row for the learner, which reuses the rollout's activations.
+#pragma once
+#include "common.h"
+
+namespace aca {
+
+constexpr int FC_UNITS = 512;
+constexpr int FC_MAX_PLANES = 8;   // = ops/gemm.py PARTIAL_MAX_SPLITS
+
+// One wave: lane l produces hidden units 8l..8l+7 of env e into hv (bf16-rounded, as floats) and, if h_out,
+// stores them. All plane loads are issued before any is used (planes past S are loaded from the allocated
+// buffer and discarded by a select, so there is no data-dependent branch).
+__device__ __forceinline__ void fc_h_from_parts(const float* __restrict__ hpart, int S, int64_t plane_stride,
+                                                const float* __restrict__ bfc, int e, int lane,
+                                                u16* __restrict__ h_out, float (&hv)[8]) {
+  float4 p[FC_MAX_PLANES][2];
+#pragma unroll
+  for (int z = 0; z < FC_MAX_PLANES; ++z) {
+    const int zz = z < S ? z : 0;
+    const float4* src = reinterpret_cast<const float4*>(hpart + zz * plane_stride + (int64_t)e * FC_UNITS + lane * 8);
+    p[z][0] = src[0];
+    p[z][1] = src[1];
+  }
+  const float4* b4 = reinterpret_cast<const float4*>(bfc + lane * 8);
+  const float4 b0 = b4[0], b1 = b4[1];
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int z = 0; z < FC_MAX_PLANES; ++z) {
+    const bool on = z < S;   // select, not multiply: unused planes may hold anything
+    a[0] += on ? p[z][0].x : 0.f; a[1] += on ? p[z][0].y : 0.f; a[2] += on ? p[z][0].z : 0.f;
+    a[3] += on ? p[z][0].w : 0.f; a[4] += on ? p[z][1].x : 0.f; a[5] += on ? p[z][1].y : 0.f;
+    a[6] += on ? p[z][1].z : 0.f; a[7] += on ? p[z][1].w : 0.f;
+  }
+  const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+  u16 hb[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    hb[r] = f2bf(fmaxf(a[r] + bb[r], 0.f));
+    hv[r] = bf2f(hb[r]);
+  }
+  if (h_out) {
+    uint4 o;
+    o.x = hb[0] | ((uint32_t)hb[1] << 16);
+    o.y = hb[2] | ((uint32_t)hb[3] << 16);
+    o.z = hb[4] | ((uint32_t)hb[5] << 16);
+    o.w = hb[6] | ((uint32_t)hb[7] << 16);
+    reinterpret_cast<uint4*>(h_out + (int64_t)e * FC_UNITS)[lane] = o;
+  }
+}
+
+}  // namespace aca

@@ -6,6 +6,7 @@
 // first frame (Framer padding rule, Basic_AC/run_AC.py:37-40). Oracle: envs/atari.py (compiled with
 // -ffp-contract=off so the physics rounds exactly like the PyTorch oracle).
 #include "common.h"
+#include "cnn_head.h"
 
 namespace aca {
 
@@ -203,8 +204,15 @@ constexpr int HEAD_HDIM = 512;                       // hidden width of the Natu
 // 8l..8l+7, whose Wh rows are A1 contiguous 16-byte chunks, so the whole GEMV is register-resident with every
 // load in flight at once and no data-dependent branch (a runtime A1 turned each column into a guarded block and
 // serialised the loads and reductions).
+struct FcParts {        // optional: h comes from the fc GEMM's split-K partial planes (cnn_head.h)
+  const float* hpart;    // null: h is read as a finished bf16 row
+  int S;
+  int64_t plane_stride;
+  const float* bfc;
+};
+
 template <int A1>
-__global__ void __launch_bounds__(256) pong_policy_step_kernel(PongIO io, const u16* __restrict__ h,
+__global__ void __launch_bounds__(256) pong_policy_step_kernel(PongIO io, FcParts fc, u16* __restrict__ h,
                                                                const u16* __restrict__ Wh,
                                                                const float* __restrict__ bh,
                                                                float* __restrict__ z_out, int32_t* __restrict__ act,
@@ -221,17 +229,25 @@ __global__ void __launch_bounds__(256) pong_policy_step_kernel(PongIO io, const 
     const int lane = threadIdx.x;
     const int64_t key = io.tglob[e] * ((int64_t)1 << key_shift) + io.env_ids[e];  // pre-step counter
     union { uint4 v[A1]; u16 x[8 * A1]; } w;
-    union { uint4 v; u16 x[8]; } hv;
-    hv.v = reinterpret_cast<const uint4*>(h + (size_t)e * HEAD_HDIM)[lane];
 #pragma unroll
     for (int u = 0; u < A1; ++u) w.v[u] = reinterpret_cast<const uint4*>(Wh)[lane * A1 + u];
+    float hf[8];
+    if (fc.hpart) {
+      // h = relu(sum of the fc partial planes + bias), rounded to bf16 and stored for the learner
+      fc_h_from_parts(fc.hpart, fc.S, fc.plane_stride, fc.bfc, e, lane, h, hf);
+    } else {
+      union { uint4 v; u16 x[8]; } hv;
+      hv.v = reinterpret_cast<const uint4*>(h + (size_t)e * HEAD_HDIM)[lane];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) hf[r] = bf2f(hv.x[r]);
+    }
     stamp_if(stamps, 8, lane == 0);
     float acc[A1];
 #pragma unroll
     for (int j = 0; j < A1; ++j) acc[j] = 0.f;
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
-      const float hr = bf2f(hv.x[r]);
+      const float hr = hf[r];
 #pragma unroll
       for (int j = 0; j < A1; ++j) acc[j] += hr * bf2f(w.x[r * A1 + j]);
     }
@@ -315,7 +331,8 @@ extern "C" hipError_t aca_env_step_pong(float* state, int32_t* t, int64_t* tg, f
   return hipGetLastError();
 }
 
-extern "C" hipError_t aca_env_policy_step_pong(const uint16_t* h, int hdim, const uint16_t* Wh, const float* bh,
+extern "C" hipError_t aca_env_policy_step_pong(uint16_t* h, const float* hpart, int S, int64_t plane_stride,
+                                               const float* bfc, int hdim, const uint16_t* Wh, const float* bh,
                                                int A, float* z, int32_t* act, float* logp, float* ent, float* value,
                                                int key_shift, uint32_t pseed, float* state, int32_t* t, int64_t* tg,
                                                float* ep_ret, float* ep_stats, const int64_t* ids,
@@ -325,12 +342,16 @@ extern "C" hipError_t aca_env_policy_step_pong(const uint16_t* h, int hdim, cons
   if (N <= 0) return hipSuccess;
   if (hdim != aca::HEAD_HDIM || reinterpret_cast<uintptr_t>(Wh) % 16 || reinterpret_cast<uintptr_t>(h) % 16)
     return hipErrorInvalidValue;
+  if (hpart && (S < 1 || S > aca::FC_MAX_PLANES || !bfc || reinterpret_cast<uintptr_t>(hpart) % 16 ||
+                reinterpret_cast<uintptr_t>(bfc) % 16 || plane_stride % 4))
+    return hipErrorInvalidValue;
+  const aca::FcParts fc{hpart, S, plane_stride, bfc};
   aca::PongIO io = make_pong_io(state, t, tg, ep_ret, ep_stats, ids, prev, out, reward, done, trunc, seed, max_steps,
                                 k);
   switch (A + 1) {
 #define ACA_POLICY_CASE(A1)                                                                                         \
   case A1:                                                                                                          \
-    aca::pong_policy_step_kernel<A1><<<N, 256, 0, stream>>>(io, h, Wh, bh, z, act, logp, ent, value, key_shift,    \
+    aca::pong_policy_step_kernel<A1><<<N, 256, 0, stream>>>(io, fc, h, Wh, bh, z, act, logp, ent, value, key_shift,\
                                                             pseed, pre_shifted, stamps);                            \
     break;
     ACA_POLICY_CASE(3) ACA_POLICY_CASE(4) ACA_POLICY_CASE(5) ACA_POLICY_CASE(6) ACA_POLICY_CASE(7)

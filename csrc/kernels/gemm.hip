@@ -43,7 +43,8 @@ extern "C" hipError_t aca_gemm_run(const AcaGemmDesc* d, hipStream_t stream) {
   const int kt = (d->K + d->bk - 1) / d->bk;
   P.splits = aca_gemm_effective_splits(d->K, d->bk, d->splits);
   P.k_tiles_per_split = kt > 0 ? (kt + P.splits - 1) / P.splits : 0;
-  if (P.splits > 1 && d->out_mode != 2 && (d->ws == nullptr || d->tickets == nullptr)) return hipErrorInvalidValue;
+  if (P.splits > 1 && d->out_mode < 2 && (d->ws == nullptr || d->tickets == nullptr)) return hipErrorInvalidValue;
+  if (d->out_mode == 3 && (d->bias || d->relu || d->mask || d->colsum)) return hipErrorInvalidValue;
   if (d->ga.mode || d->gb.mode) return gemm_conv(P, stream);
   return gemm_plain(P, stream);
 }

@@ -16,12 +16,41 @@ extern "C" {
 //           the output; requires C % 8 == 0
 //   mode 4: (B operand) OHWI weight [C][KH][KW][W] read as B[k = (i, j, o)][n]: the transposed-conv weight operand
 //           without materialising the transpose; spec fields C = conv output channels, W = input channels
+// n / d for 0 <= n < 2^31 as (umulhi(n, m) + n) >> s (Granlund-Montgomery, computed on the host by
+// aca_fastdiv_init): the gathers decode their (b, h, w) / (i, j, c) indices without integer division sequences.
+typedef struct {
+  unsigned int m, s;
+} AcaFastDiv;
+
 typedef struct {
   const void* src;
   int mode;  // 0 none, 1 u8 nchw, 2 bf16 nhwc, 3 transposed-conv gather, 4 OHWI weight transpose
   int B, C, H, W, KH, KW, S, OH, OW;
   float scale;
+  AcaFastDiv fd_ohw, fd_ow, fd_hw, fd_w, fd_khw, fd_kw, fd_kwc, fd_c, fd_s;
 } AcaConvGather;
+
+static inline AcaFastDiv aca_fastdiv_init(unsigned int d) {
+  AcaFastDiv f;
+  unsigned int l = 0;
+  while (l < 32 && (1ull << l) < d) ++l;   // l = ceil(log2 d)
+  f.m = (unsigned int)((((unsigned long long)1 << 32) * (((unsigned long long)1 << l) - d)) / d + 1);
+  f.s = l;
+  return f;
+}
+
+// fills the fast divisors of a gather whose geometry fields are set
+static inline void aca_gather_prepare(AcaConvGather* g) {
+  g->fd_ohw = aca_fastdiv_init((unsigned int)(g->OH * g->OW > 0 ? g->OH * g->OW : 1));
+  g->fd_ow = aca_fastdiv_init((unsigned int)(g->OW > 0 ? g->OW : 1));
+  g->fd_hw = aca_fastdiv_init((unsigned int)(g->H * g->W > 0 ? g->H * g->W : 1));
+  g->fd_w = aca_fastdiv_init((unsigned int)(g->W > 0 ? g->W : 1));
+  g->fd_khw = aca_fastdiv_init((unsigned int)(g->KH * g->KW > 0 ? g->KH * g->KW : 1));
+  g->fd_kw = aca_fastdiv_init((unsigned int)(g->KW > 0 ? g->KW : 1));
+  g->fd_kwc = aca_fastdiv_init((unsigned int)(g->KW * g->C > 0 ? g->KW * g->C : 1));
+  g->fd_c = aca_fastdiv_init((unsigned int)(g->C > 0 ? g->C : 1));
+  g->fd_s = aca_fastdiv_init((unsigned int)(g->S > 0 ? g->S : 1));
+}
 
 typedef struct {
   const void* A;
@@ -35,7 +64,7 @@ typedef struct {
   int64_t lda, ldb, ldc, ldm;
   int M, N, K;
   int a_k, b_k;       // operand storage (see gemm_impl.h)
-  int out_mode;       // 0 fp32, 1 bf16, 2 fp32 atomic add
+  int out_mode;       // 0 fp32, 1 bf16, 2 fp32 atomic add, 3 fp32 split-K partial planes
   int relu;
   int colsum_mod;
   float alpha;

@@ -23,6 +23,9 @@
 //     deterministic, used for skinny forward products (M = 32 rollout rows against K = 3136).
 // Epilogue (in order): *alpha, +bias[n], relu, *(mask[m,n] > 0) (ReLU backward), store fp32 | bf16 | atomic-add
 // fp32, and optional column sums of the final values atomically added to colsum[n % colsum_mod] (bias gradients).
+// out_mode 3 ("partials"): split z stores alpha*acc into plane z of C [splits, M, ldc] with no reduction, no
+// ticket and no fence; the consumer kernel sums the planes in fixed order (deterministic) and applies bias and
+// activation itself -- the rollout's fc product, whose only consumer is the fused policy/env kernel.
 #pragma once
 #include "common.h"
 #include "gemm_desc.h"
@@ -54,58 +57,111 @@ __device__ __forceinline__ uint4 load8(const u16* base, int64_t row_off, int idx
   return pack8(tmp);
 }
 
-// implicit im2col: 8 consecutive k of conv-output row m (k % 8 == 0)
+__device__ __forceinline__ int fdiv(int n, AcaFastDiv f) {
+  return (int)((__umulhi((unsigned int)n, f.m) + (unsigned int)n) >> f.s);
+}
+
+// Implicit-im2col gathers. Each thread stages fixed (row, column-chunk) slots of every k-step, so the part of the
+// address that depends only on its fixed index is decoded ONCE before the k-loop (GCtx) and each k-step decodes
+// only the varying index, with multiply-shift division (an integer-division sequence per index was ~30x the
+// MFMA work of a tile).
+struct GCtx {
+  int64_t base;   // element offset of the fixed part
+  int p, q;       // mode 3: input-image row / column of the output pixel
+  int ok;
+};
+
+// A operand (modes 1/2/3): fixed conv row m of this chunk
 template <int MODE>
-__device__ __forceinline__ uint4 gather8(const AcaConvGather& g, int m, int k, bool ok) {
-  if (!ok) return make_uint4(0, 0, 0, 0);
+__device__ __forceinline__ GCtx gctx_a(const AcaConvGather& g, int m, bool ok) {
+  GCtx c{0, 0, 0, ok ? 1 : 0};
+  if (!ok) return c;
   if (MODE == 3) {
-    // transposed conv (data gradient): row m = (b, ih, iw) of the conv INPUT, k = (i, j, c) over the output-gradient
-    // channels; the source pixel is ((ih - i) / S, (iw - j) / S) when that lands on the stride grid, else zero
-    const int hw = g.H * g.W;
-    const int b = m / hw, p = m - b * hw;
-    const int ih = p / g.W, iw = p - ih * g.W;
-    const int kwc = g.KW * g.C;
-    const int i = k / kwc, r = k - i * kwc;
-    const int j = r / g.C, c = r - j * g.C;
-    const int th = ih - i, tw = iw - j;
-    if (th < 0 || tw < 0) return make_uint4(0, 0, 0, 0);
-    const int sh = th / g.S, sw = tw / g.S;
-    if (sh * g.S != th || sw * g.S != tw || sh >= g.OH || sw >= g.OW) return make_uint4(0, 0, 0, 0);
-    return *reinterpret_cast<const uint4*>(reinterpret_cast<const u16*>(g.src) +
-                                           (((int64_t)b * g.OH + sh) * g.OW + sw) * g.C + c);
-  }
-  if (MODE == 4) {
-    // OHWI conv weight read as B[k = (i, j, o)][n = input channel] (the transposed-conv operand): row m = k here
-    const int khw = g.KH * g.KW;
-    const int ij = m / g.C, o = m - ij * g.C;
-    return *reinterpret_cast<const uint4*>(reinterpret_cast<const u16*>(g.src) + ((int64_t)o * khw + ij) * g.W + k);
-  }
-  const int ohw = g.OH * g.OW;
-  const int b = m / ohw, p = m - b * ohw;
-  const int oh = p / g.OW, ow = p - oh * g.OW;
-  if (MODE == 1) {
-    const int khw = g.KH * g.KW;
-    const int c = k / khw, r = k - c * khw;
-    const int i = r / g.KW, j = r - i * g.KW;
-    const uint8_t* src = reinterpret_cast<const uint8_t*>(g.src) +
-                         (((int64_t)b * g.C + c) * g.H + oh * g.S + i) * g.W + ow * g.S + j;
-    const uint32_t w0 = *reinterpret_cast<const uint32_t*>(src);
-    const uint32_t w1 = *reinterpret_cast<const uint32_t*>(src + 4);
-    u16 t[8];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      t[e] = f2bf((float)((w0 >> (8 * e)) & 0xFF) * g.scale);
-      t[4 + e] = f2bf((float)((w1 >> (8 * e)) & 0xFF) * g.scale);
-    }
-    return pack8(t);
+    const int b = fdiv(m, g.fd_hw), p = m - b * g.H * g.W;
+    const int ih = fdiv(p, g.fd_w);
+    c.base = (int64_t)b * g.OH * g.OW;
+    c.p = ih;
+    c.q = p - ih * g.W;
   } else {
-    const int kwc = g.KW * g.C;
-    const int i = k / kwc, r = k - i * kwc;
-    const int j = r / g.C, c = r - j * g.C;
-    const u16* src = reinterpret_cast<const u16*>(g.src) +
-                     (((int64_t)b * g.H + oh * g.S + i) * g.W + ow * g.S + j) * g.C + c;
-    return *reinterpret_cast<const uint4*>(src);
+    const int b = fdiv(m, g.fd_ohw), p = m - b * g.OH * g.OW;
+    const int oh = fdiv(p, g.fd_ow), ow = p - oh * g.OW;
+    c.base = MODE == 1 ? (((int64_t)b * g.C) * g.H + oh * g.S) * g.W + ow * g.S
+                       : (((int64_t)b * g.H + oh * g.S) * g.W + ow * g.S) * g.C;
   }
+  return c;
+}
+
+__device__ __forceinline__ uint4 u8x8_scaled(const uint8_t* src, float scale) {
+  const uint32_t w0 = *reinterpret_cast<const uint32_t*>(src);
+  const uint32_t w1 = *reinterpret_cast<const uint32_t*>(src + 4);
+  u16 t[8];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    t[e] = f2bf((float)((w0 >> (8 * e)) & 0xFF) * scale);
+    t[4 + e] = f2bf((float)((w1 >> (8 * e)) & 0xFF) * scale);
+  }
+  return pack8(t);
+}
+
+// 8 consecutive k of the A row described by c (k % 8 == 0)
+template <int MODE>
+__device__ __forceinline__ uint4 gather_a(const AcaConvGather& g, const GCtx& c, int k, bool kok) {
+  if (!(c.ok && kok)) return make_uint4(0, 0, 0, 0);
+  if (MODE == 1) {
+    const int ci = fdiv(k, g.fd_khw), r = k - ci * g.KH * g.KW;
+    const int i = fdiv(r, g.fd_kw), j = r - i * g.KW;
+    return u8x8_scaled(reinterpret_cast<const uint8_t*>(g.src) + c.base + ((int64_t)ci * g.H + i) * g.W + j,
+                       g.scale);
+  }
+  const int i = fdiv(k, g.fd_kwc), r = k - i * g.KW * g.C;
+  const int j = fdiv(r, g.fd_c), cc = r - j * g.C;
+  if (MODE == 2)
+    return *reinterpret_cast<const uint4*>(reinterpret_cast<const u16*>(g.src) + c.base + (i * g.W + j) * g.C + cc);
+  // MODE 3: transposed conv (data gradient): source pixel ((ih - i) / S, (iw - j) / S) when on the stride grid
+  const int th = c.p - i, tw = c.q - j;
+  if (th < 0 || tw < 0) return make_uint4(0, 0, 0, 0);
+  const int sh = fdiv(th, g.fd_s), sw = fdiv(tw, g.fd_s);
+  if (sh * g.S != th || sw * g.S != tw || sh >= g.OH || sw >= g.OW) return make_uint4(0, 0, 0, 0);
+  return *reinterpret_cast<const uint4*>(reinterpret_cast<const u16*>(g.src) +
+                                         ((c.base + (int64_t)sh * g.OW + sw) * g.C + cc));
+}
+
+// B operand (modes 1/2: weight gradient, B[k = conv row][n = conv column]; mode 4: OHWI weight read as
+// B[k = (i, j, o)][n]): fixed column n of this chunk
+template <int MODE>
+__device__ __forceinline__ GCtx gctx_b(const AcaConvGather& g, int n, bool ok) {
+  GCtx c{0, 0, 0, ok ? 1 : 0};
+  if (!ok) return c;
+  if (MODE == 1) {
+    const int ci = fdiv(n, g.fd_khw), r = n - ci * g.KH * g.KW;
+    const int i = fdiv(r, g.fd_kw), j = r - i * g.KW;
+    c.base = ((int64_t)ci * g.H + i) * g.W + j;
+  } else if (MODE == 2) {
+    const int i = fdiv(n, g.fd_kwc), r = n - i * g.KW * g.C;
+    const int j = fdiv(r, g.fd_c), cc = r - j * g.C;
+    c.base = ((int64_t)i * g.W + j) * g.C + cc;
+  } else {
+    c.base = n;
+  }
+  return c;
+}
+
+template <int MODE>
+__device__ __forceinline__ uint4 gather_b(const AcaConvGather& g, const GCtx& c, int k, bool kok) {
+  if (!(c.ok && kok)) return make_uint4(0, 0, 0, 0);
+  if (MODE == 4) {
+    const int ij = fdiv(k, g.fd_c), o = k - ij * g.C;
+    return *reinterpret_cast<const uint4*>(reinterpret_cast<const u16*>(g.src) +
+                                           ((int64_t)o * g.KH * g.KW + ij) * g.W + c.base);
+  }
+  const int b = fdiv(k, g.fd_ohw), p = k - b * g.OH * g.OW;
+  const int oh = fdiv(p, g.fd_ow), ow = p - oh * g.OW;
+  if (MODE == 1) {
+    const int64_t rb = (((int64_t)b * g.C) * g.H + oh * g.S) * g.W + ow * g.S;
+    return u8x8_scaled(reinterpret_cast<const uint8_t*>(g.src) + rb + c.base, g.scale);
+  }
+  const int64_t rb = (((int64_t)b * g.H + oh * g.S) * g.W + ow * g.S) * g.C;
+  return *reinterpret_cast<const uint4*>(reinterpret_cast<const u16*>(g.src) + rb + c.base);
 }
 
 struct GemmParams {
@@ -149,6 +205,22 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmParams P) {
     for (int j = 0; j < TN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   uint4 ra[A_CHUNKS], rb[B_CHUNKS];
+  // gather contexts of this thread's fixed staging slots (decoded once)
+  GCtx actx[AG ? A_CHUNKS : 1], bctx[BG ? B_CHUNKS : 1];
+  if (AG) {
+#pragma unroll
+    for (int c = 0; c < A_CHUNKS; ++c) {
+      const int r = (tid + c * 256) / (BK / 8);
+      actx[c] = gctx_a<AG>(g.ga, m0 + r, m0 + r < g.M);
+    }
+  }
+  if (BG) {
+#pragma unroll
+    for (int c = 0; c < B_CHUNKS; ++c) {
+      const int nc = ((tid + c * 256) % (BN / 8)) * 8;
+      bctx[c] = gctx_b<BG>(g.gb, n0 + nc, n0 + nc < g.N);
+    }
+  }
 
   auto gload = [&](int kt) {
     const int k0 = kt * BK;
@@ -158,7 +230,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmParams P) {
       if (A_K) {
         const int r = ch / (BK / 8), kc = (ch % (BK / 8)) * 8;
         const int m = m0 + r;
-        if (AG) ra[c] = gather8<AG>(g.ga, m, k0 + kc, m < g.M && k0 + kc < g.K);
+        if (AG) ra[c] = gather_a<AG>(g.ga, actx[AG ? c : 0], k0 + kc, k0 + kc < g.K);
         else ra[c] = load8(Ag, (int64_t)m * g.lda, k0 + kc, g.K, m < g.M);
       } else {
         const int kr = ch / (BM / 8), mc = (ch % (BM / 8)) * 8;
@@ -176,7 +248,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmParams P) {
       } else {
         const int kr = ch / (BN / 8), nc = (ch % (BN / 8)) * 8;
         const int k = k0 + kr;
-        if (BG) rb[c] = gather8<BG>(g.gb, k, n0 + nc, k < g.K && n0 + nc < g.N);
+        if (BG) rb[c] = gather_b<BG>(g.gb, bctx[BG ? c : 0], k, k < g.K);
         else rb[c] = load8(Bg, (int64_t)k * g.ldb, n0 + nc, g.N, k < g.K);
       }
     }
@@ -247,7 +319,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmParams P) {
   }
 
   // ---------------------------------------------------------------- split-K reduction (slab flavour)
-  if (P.splits > 1 && g.out_mode != 2) {
+  if (P.splits > 1 && g.out_mode < 2) {
     float* slab = g.ws + ((size_t)tile * P.splits + z) * (BM * BN);
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -285,6 +357,10 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmParams P) {
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + wm * (BM / 2) + i * 16 + lg * 4 + r;
         if (!(n_ok && m < g.M)) continue;
+        if (g.out_mode == 3) {   // split-K partial plane z, reduced (with bias / activation) by the consumer
+          reinterpret_cast<float*>(g.C)[((int64_t)z * g.M + m) * g.ldc + n] = acc[i][j][r] * g.alpha;
+          continue;
+        }
         float v = acc[i][j][r] * g.alpha + b;
         if (g.relu) v = fmaxf(v, 0.f);
         if (mask) v = (bf2f(mask[(int64_t)m * g.ldm + n]) > 0.f) ? v : 0.f;

@@ -85,7 +85,7 @@ def main():
         ops.env_policy_step_pong(bt.h, eng.sWh, eng.bh, bt.z, act, logp, ent, val, KEY_ENV_BITS, tr.policy_seed,
                                  scratch["state"], scratch["t"], scratch["tg"], scratch["ep_ret"], scratch["ep_stats"],
                                  env.env_ids, prev, out, rew, done, trunc, env.seed, env.max_episode_steps,
-                                 env.frame_stack, True, stamps)
+                                 env.frame_stack, True, stamps=stamps)
     res["policy_step_chained_us"] = graph_time(pstep)
     opt = tr.actor_opt
     parts = torch.zeros(256, device=eng.dev)
@@ -121,6 +121,7 @@ def main():
         "drained_us": float((s[:, 6] - t0).median()),
         "end_from_first_start_us": float(s[:, 6].max() - t0.min()),
     }
+    res["tuned_gemms"] = {str(k): v for k, v in G.tuned_plans().items()}
     txt = json.dumps(res, indent=1)
     print(txt)
     if a.out:

@@ -448,3 +448,51 @@ def test_fused_policy_env_step_matches_separate_kernels(cuda):
     assert torch.allclose(l0[same], l1[same], atol=2e-3) and torch.allclose(e0, e1, atol=2e-3)
     assert torch.allclose(v0, v1, atol=2e-3)
     assert torch.equal(f0[same], f1[same])
+
+
+def test_fc_partial_planes_and_consumers(cuda):
+    """GEMM out_mode 3 (split-K partial planes) + its consumers: fc_value and the fused policy step reducing the
+    planes themselves (bias + ReLU + bf16 like the GEMM epilogue) == the finished-h path."""
+    from actor_critic_algs_on_tensorflow_amd import _native
+    from actor_critic_algs_on_tensorflow_amd import envs as E
+    from actor_critic_algs_on_tensorflow_amd.ops import gemm as G
+    ops = _native.require()
+    g = torch.Generator().manual_seed(11)
+    N, A = 32, 6
+    y3 = torch.relu(torch.randn(N, 3136, generator=g)).to(torch.bfloat16).to(cuda)
+    Wfc = (torch.randn(3136, 512, generator=g) * 0.02).to(torch.bfloat16).to(cuda)
+    bfc = (torch.randn(512, generator=g) * 0.1).to(cuda)
+    Wh = (torch.randn(512 * (A + 1), generator=g) * 0.05).to(torch.bfloat16).to(cuda)
+    bh = torch.randn(A + 1, generator=g).to(cuda)
+    ref = torch.relu(y3.float() @ Wfc.float() + bfc)
+    for tile, bk, splits in ((1, 64, 4), (4, 256, 8), (0, 128, 1)):
+        hp = torch.full((8 * N * 512,), float("nan"), device=cuda)   # unused planes must never be read as data
+        S = G.gemm(y3, 3136, True, Wfc, 512, False, hp, 512, 3, N, 512, 3136, tile=tile, bk=bk, splits=splits)
+        assert S == G.effective_splits(3136, bk, splits)
+        h_sum = torch.relu(hp.view(8, N, 512)[:S].sum(0) + bfc)
+        assert torch.allclose(h_sum, ref, rtol=1e-3, atol=1e-3)
+        val = torch.empty(N, device=cuda)
+        hout = torch.empty(N, 512, dtype=torch.bfloat16, device=cuda)
+        ops.fc_value(hp, S, bfc, Wh, bh, val, hout)
+        assert torch.allclose(hout.float(), ref, rtol=1e-2, atol=1e-2)
+        vref = hout.float() @ Wh.float().view(512, A + 1)[:, A] + bh[A]
+        assert torch.allclose(val, vref, rtol=1e-4, atol=1e-4)
+        outs = []
+        for parts in (True, False):
+            env = E.make("PongNoFrameskip-v4", N, device=cuda, seed=3)
+            o0 = env.reset().clone()
+            o1 = torch.empty_like(o0)
+            act = torch.empty(N, dtype=torch.int32, device=cuda)
+            lp, en, v = (torch.empty(N, device=cuda) for _ in range(3))
+            z = torch.empty(N, A + 1, device=cuda)
+            rew = torch.empty(N, device=cuda)
+            dn, tr = (torch.empty(N, dtype=torch.uint8, device=cuda) for _ in range(2))
+            h = torch.empty(N, 512, dtype=torch.bfloat16, device=cuda) if parts else hout.clone()
+            ops.env_policy_step_pong(h, Wh, bh, z, act, lp, en, v, 20, 77, env.state, env.t, env.tg, env.ep_ret,
+                                     env.ep_stats, env.env_ids, o0, o1, rew, dn, tr, env.seed,
+                                     env.max_episode_steps, 4, False, hp if parts else None, S if parts else 0,
+                                     bfc if parts else None)
+            outs.append((h.clone(), z.clone(), act.clone(), v.clone(), o1.clone()))
+        for a, b in zip(outs[0], outs[1]):
+            assert torch.equal(a, b)
+        assert torch.allclose(outs[0][3], val, atol=1e-5)

@@ -250,8 +250,9 @@ class CNNEngine:
             else:
                 G.gemm(b.dy2, 64, False, b.col2, 512, False, self.gW2, 512, 2, 64, 512, B * 81, workspace=ws2)
         if self.tconv_dgrad:   # dy1 = conv_transpose(dy2, W2) * (y1 > 0) (+ colsum -> db1)
-            G.gemm(b.dy2, 0, True, self.sW2, 0, False, b.dy1, 32, 1, B * 400, 32, 1024, mask=b.y1, ldm=32,
-                   colsum=self.gb1, workspace=ws, ga=[3, B, 64, 20, 20, 4, 4, 2], gb=[4, 1, 64, 1, 32, 4, 4, 1])
+            # stride 2: sub-pixel form -- rows grouped by stride phase, only the 2x2 taps on each phase's grid
+            G.gemm(b.dy2, 0, True, self.sW2, 0, False, b.dy1, 32, 1, B * 400, 32, 256, mask=b.y1, ldm=32,
+                   colsum=self.gb1, workspace=ws, ga=[5, B, 64, 20, 20, 4, 4, 2], gb=[6, 1, 64, 1, 32, 4, 4, 2])
         else:
             G.gemm(b.dy2, 64, True, self.sW2, 512, False, self.dcol2(b), 512, 1, B * 81, 512, 64, workspace=ws)
             G.col2im_nhwc(self.dcol2(b), b.y1, b.dy1, self.gb1, B, 20, 20, 32, 4, 4, 2)

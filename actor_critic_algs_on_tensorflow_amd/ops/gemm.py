@@ -92,8 +92,10 @@ def tuned_plans():
     return dict(_TUNED)
 
 
-def _candidates(M, N, K, atomic, max_splits=None):
+def _candidates(M, N, K, atomic, max_splits=None, row_block=None):
     for tile, (bm, bn) in TILES.items():
+        if row_block is not None and row_block % bm:
+            continue  # sub-pixel gathers: a tile must not straddle two stride phases
         if bm >= 2 * max(32, M) or bn >= 2 * max(32, N):
             continue  # a tile at least twice the problem in one dimension only wastes MFMA issue
         for bk in BKS[tile]:
@@ -111,7 +113,7 @@ def _candidates(M, N, K, atomic, max_splits=None):
 
 
 def _run(ops, A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha, bias, relu, mask, ldm, colsum,
-         colsum_mod, tile, bk, splits, workspace, ga, ga_scale, gb, gb_scale):
+         colsum_mod, tile, bk, splits, workspace, ga, ga_scale, gb, gb_scale, stamps=None):
     eff = effective_splits(K, bk, splits)
     ws = tk = None
     if eff > 1 and out_mode < 2:
@@ -122,8 +124,15 @@ def _run(ops, A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha, bias, 
         ws, tk = workspace.ws, workspace.tickets
     ops.gemm(A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, float(alpha), bias, bool(relu), mask, ldm,
              colsum, int(colsum_mod), tile, bk, splits, ws, tk, list(ga or []), float(ga_scale), list(gb or []),
-             float(gb_scale))
+             float(gb_scale), stamps)
     return eff
+
+
+def _row_block(ga):
+    """Rows per stride phase of a sub-pixel (mode 5) gather, else None."""
+    if ga and ga[0] == 5:
+        return ga[1] * (ga[3] // ga[7]) * (ga[4] // ga[7])
+    return None
 
 
 def _tune(key, ops, A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha, bias, relu, mask, ldm, colsum,
@@ -135,7 +144,8 @@ def _tune(key, ops, A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha, 
     ws = workspace if workspace is not None else GemmWorkspace(dev)
     best = None
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    for tile, bk, s in _candidates(M, N, K, out_mode == 2, PARTIAL_MAX_SPLITS if out_mode == 3 else None):
+    for tile, bk, s in _candidates(M, N, K, out_mode == 2, PARTIAL_MAX_SPLITS if out_mode == 3 else None,
+                                   _row_block(ga)):
         args = (ops, A, lda, a_k, B, ldb, b_k, Cs, ldc, out_mode, M, N, K, alpha, bias, relu, mask, ldm, cs,
                 colsum_mod, tile, bk, s, ws, ga, ga_scale, gb, gb_scale)
         _run(*args)
@@ -155,7 +165,7 @@ def _tune(key, ops, A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha, 
 
 def gemm(A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha=1.0, bias=None, relu=False, mask=None, ldm=0,
          colsum=None, tile=None, splits=None, workspace: GemmWorkspace | None = None, colsum_mod=0, bk=None,
-         ga=None, ga_scale=1.0, gb=None, gb_scale=1.0):
+         ga=None, ga_scale=1.0, gb=None, gb_scale=1.0, stamps=None):
     """Native GEMM; ``out_mode``: 0 fp32 store, 1 bf16 store, 2 fp32 atomic add (C pre-zeroed), 3 fp32 split-K
     partial planes ``C[z, M, ldc]`` (no bias/activation: the consumer reduces). Returns the effective split count.
 
@@ -175,6 +185,9 @@ def gemm(A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha=1.0, bias=No
             t, k, s = plan(M, N, K, atomic=(out_mode == 2))
             if out_mode == 3:
                 s = min(s, PARTIAL_MAX_SPLITS)
+            rb = _row_block(ga)
+            if rb is not None and rb % TILES[t][0]:
+                t = next(tt for tt in (2, 0, 4, 1) if rb % TILES[tt][0] == 0)
         tile = t if tile is None else tile
         bk = k if bk is None else bk
         splits = s if splits is None else splits
@@ -183,7 +196,7 @@ def gemm(A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha=1.0, bias=No
     if out_mode == 3 and effective_splits(K, bk, splits) > PARTIAL_MAX_SPLITS:
         raise ValueError("out_mode 3 supports at most %d partial planes" % PARTIAL_MAX_SPLITS)
     return _run(ops, A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha, bias, relu, mask, ldm, colsum,
-                colsum_mod, tile, bk, splits, workspace, ga, ga_scale, gb, gb_scale)
+                colsum_mod, tile, bk, splits, workspace, ga, ga_scale, gb, gb_scale, stamps)
 
 
 def _view(t, rows, cols, ld, k_contig_rows):

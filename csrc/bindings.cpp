@@ -458,10 +458,13 @@ AcaConvGather make_gather(const Tensor& src, const std::vector<int64_t>& spec, d
   g.scale = (float)scale;
   aca_gather_prepare(&g);
   TORCH_CHECK(src.is_contiguous(), "gemm: gather source ", name, " must be contiguous");
-  if (g.mode == 3) {
-    TORCH_CHECK(g.OH > 0 && g.OW > 0, "gemm: gather mode 3 bad geometry");
+  if (g.mode == 3 || g.mode == 5) {
+    TORCH_CHECK(g.OH > 0 && g.OW > 0, "gemm: gather mode 3/5 bad geometry");
+    if (g.mode == 5)
+      TORCH_CHECK(g.S > 0 && g.KH % g.S == 0 && g.KW % g.S == 0 && g.H % g.S == 0 && g.W % g.S == 0,
+                  "gemm: sub-pixel gather needs KH, KW, H, W divisible by the stride");
     TORCH_CHECK(src.numel() >= (int64_t)g.B * g.OH * g.OW * g.C, "gemm: gather source ", name, " too small");
-  } else if (g.mode == 4) {
+  } else if (g.mode == 4 || g.mode == 6) {
     TORCH_CHECK(src.numel() >= (int64_t)g.C * g.KH * g.KW * g.W, "gemm: gather source ", name, " too small");
   } else {
     TORCH_CHECK(src.numel() >= (int64_t)g.B * g.C * g.H * g.W, "gemm: gather source ", name, " too small");
@@ -474,9 +477,10 @@ AcaConvGather make_gather(const Tensor& src, const std::vector<int64_t>& spec, d
     TORCH_CHECK(src.scalar_type() == at::kBFloat16, "gemm: gather mode 2 needs a bf16 source");
     TORCH_CHECK(g.C % 8 == 0, "gemm: gather mode 2 needs C % 8 == 0");
     TORCH_CHECK(reinterpret_cast<uintptr_t>(g.src) % 16 == 0, "gemm: gather source must be 16-byte aligned");
-  } else if (g.mode == 3 || g.mode == 4) {
-    TORCH_CHECK(src.scalar_type() == at::kBFloat16, "gemm: gather modes 3/4 need a bf16 source");
-    TORCH_CHECK((g.mode == 3 ? g.C : g.W) % 8 == 0, "gemm: gather modes 3/4 need 8-aligned contiguous channels");
+  } else if (g.mode >= 3 && g.mode <= 6) {
+    TORCH_CHECK(src.scalar_type() == at::kBFloat16, "gemm: gather modes 3-6 need a bf16 source");
+    TORCH_CHECK((g.mode == 3 || g.mode == 5 ? g.C : g.W) % 8 == 0,
+                "gemm: gather modes 3-6 need 8-aligned contiguous channels");
     TORCH_CHECK(reinterpret_cast<uintptr_t>(g.src) % 16 == 0, "gemm: gather source must be 16-byte aligned");
   } else {
     TORCH_CHECK(false, "gemm: unknown gather mode ", g.mode);
@@ -488,7 +492,8 @@ void gemm(Tensor A, int64_t lda, bool a_k, Tensor B, int64_t ldb, bool b_k, Tens
           int64_t M, int64_t N, int64_t K, double alpha, c10::optional<Tensor> bias, bool relu,
           c10::optional<Tensor> mask, int64_t ldm, c10::optional<Tensor> colsum, int64_t colsum_mod, int64_t tile,
           int64_t bk, int64_t splits, c10::optional<Tensor> ws, c10::optional<Tensor> tickets,
-          std::vector<int64_t> ga, double ga_scale, std::vector<int64_t> gb, double gb_scale) {
+          std::vector<int64_t> ga, double ga_scale, std::vector<int64_t> gb, double gb_scale,
+          c10::optional<Tensor> stamps) {
   TORCH_CHECK(out_mode >= 0 && out_mode <= 3, "gemm: bad out_mode");
   if (out_mode == 3)
     TORCH_CHECK(!(bias.has_value() && bias->defined()) && !relu && !(mask.has_value() && mask->defined()) &&
@@ -499,9 +504,21 @@ void gemm(Tensor A, int64_t lda, bool a_k, Tensor B, int64_t ldb, bool b_k, Tens
   AcaGemmDesc d{};
   d.ga = make_gather(A, ga, ga_scale, "A");
   d.gb = make_gather(B, gb, gb_scale, "B");
-  TORCH_CHECK(d.ga.mode != 4 && d.gb.mode != 3, "gemm: gather mode 3 is A-only, mode 4 is B-only");
+  TORCH_CHECK(d.ga.mode != 4 && d.gb.mode != 3 && d.ga.mode != 6 && d.gb.mode != 5,
+              "gemm: gather modes 3/5 are A-only, 4/6 B-only");
   TORCH_CHECK((d.ga.mode == 3) == (d.gb.mode == 4), "gemm: gather modes 3 and 4 go together (data gradient)");
-  if (d.ga.mode == 3) {
+  TORCH_CHECK((d.ga.mode == 5) == (d.gb.mode == 6), "gemm: gather modes 5 and 6 go together (sub-pixel dgrad)");
+  if (d.ga.mode == 5) {
+    TORCH_CHECK(a_k, "gemm: A gather needs a_k");
+    TORCH_CHECK(M == (int64_t)d.ga.B * d.ga.H * d.ga.W && K == (int64_t)d.ga.C * d.ga.KHS * d.ga.KWS,
+                "gemm: sub-pixel gather shape does not match M/K");
+    TORCH_CHECK(d.gb.S == d.ga.S && d.gb.KH == d.ga.KH && d.gb.KW == d.ga.KW && d.gb.C == d.ga.C,
+                "gemm: sub-pixel A/B gather geometry mismatch");
+    int bm, bn;
+    aca_gemm_tile_dims((int)tile, &bm, &bn);
+    TORCH_CHECK(((int64_t)d.ga.B * d.ga.HS * d.ga.WS) % bm == 0, "gemm: sub-pixel rows per phase must be a multiple "
+                "of the tile height");
+  } else if (d.ga.mode == 3) {
     TORCH_CHECK(a_k, "gemm: A gather needs a_k");
     TORCH_CHECK(M == (int64_t)d.ga.B * d.ga.H * d.ga.W && K == (int64_t)d.ga.C * d.ga.KH * d.ga.KW,
                 "gemm: transposed-conv gather shape does not match M/K");
@@ -513,7 +530,10 @@ void gemm(Tensor A, int64_t lda, bool a_k, Tensor B, int64_t ldb, bool b_k, Tens
     TORCH_CHECK(A.scalar_type() == at::kBFloat16, "gemm: A must be bf16");
     check_extent(A, a_k ? M : K, a_k ? K : M, lda, "A");
   }
-  if (d.gb.mode == 4) {
+  if (d.gb.mode == 6) {
+    TORCH_CHECK(!b_k, "gemm: B gather needs !b_k");
+    TORCH_CHECK(K == (int64_t)d.gb.C * d.gb.KHS * d.gb.KWS && N == d.gb.W, "gemm: phase weight gather shape");
+  } else if (d.gb.mode == 4) {
     TORCH_CHECK(!b_k, "gemm: B gather needs !b_k");
     TORCH_CHECK(K == (int64_t)d.gb.C * d.gb.KH * d.gb.KW && N == d.gb.W, "gemm: weight-transpose gather shape");
   } else if (d.gb.mode) {
@@ -559,6 +579,14 @@ void gemm(Tensor A, int64_t lda, bool a_k, Tensor B, int64_t ldb, bool b_k, Tens
   d.a_k = a_k; d.b_k = b_k;
   d.out_mode = (int)out_mode; d.relu = relu ? 1 : 0; d.colsum_mod = (int)colsum_mod;
   d.alpha = (float)alpha;
+  if (stamps.has_value() && stamps->defined()) {   // diagnostics: [tiles * splits, 4] int64 per workgroup
+    int bm, bn;
+    aca_gemm_tile_dims((int)tile, &bm, &bn);
+    const int64_t wgs = ((M + bm - 1) / bm) * ((N + bn - 1) / bn) * aca_gemm_effective_splits((int)K, (int)bk, (int)splits);
+    need(*stamps, at::kLong, "stamps");
+    TORCH_CHECK(stamps->numel() >= wgs * 4, "gemm: stamps needs [workgroups, 4]");
+    d.stamps = ptr<unsigned long long>(*stamps);
+  }
   d.tile = (int)tile; d.bk = (int)bk; d.splits = (int)splits;
   check(aca_gemm_run(&d, cur_stream(C)), "gemm");
 }
@@ -746,7 +774,7 @@ TORCH_LIBRARY(acamd, m) {
   m.def("gemm(Tensor A, int lda, bool a_k, Tensor B, int ldb, bool b_k, Tensor C, int ldc, int out_mode, int M, "
         "int N, int K, float alpha, Tensor? bias, bool relu, Tensor? mask, int ldm, Tensor? colsum, int colsum_mod, "
         "int tile, int bk, int splits, Tensor? ws, Tensor? tickets, int[] ga, float ga_scale, int[] gb, "
-        "float gb_scale) -> ()");
+        "float gb_scale, Tensor? stamps=None) -> ()");
   m.def("gemm_effective_splits(int K, int bk, int splits) -> int", &gemm_effective_splits);
   m.def("cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, Tensor y1, "
         "Tensor y2, Tensor y3, float scale, Tensor? shift_out=None, Tensor? stamps=None) -> ()");

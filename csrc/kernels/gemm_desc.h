@@ -16,6 +16,13 @@ extern "C" {
 //           the output; requires C % 8 == 0
 //   mode 4: (B operand) OHWI weight [C][KH][KW][W] read as B[k = (i, j, o)][n]: the transposed-conv weight operand
 //           without materialising the transpose; spec fields C = conv output channels, W = input channels
+//   mode 5: sub-pixel transposed conv (stride S, KH % S == KW % S == H % S == W % S == 0): the rows are the input
+//           pixels grouped by stride phase (ph, pw), m = (((ph * S + pw) * B + b) * H/S + a) * W/S + c for pixel
+//           (a*S + ph, c*S + pw), k = (di, dj, o) over (KH/S) x (KW/S) x C: only the taps i = ph + S*di,
+//           j = pw + S*dj that land on the stride grid, so K shrinks by S^2 and no zero products are computed;
+//           the epilogue writes row m back to its natural NHWC position. Pairs with
+//   mode 6: (B operand) OHWI weight read as B[k = (di, dj, o)][n] = W[o][ph + S*di][pw + S*dj][n] for the phase of
+//           the workgroup's rows (tiles never straddle phases: (B * H/S * W/S) % BM == 0)
 // n / d for 0 <= n < 2^31 as (umulhi(n, m) + n) >> s (Granlund-Montgomery, computed on the host by
 // aca_fastdiv_init): the gathers decode their (b, h, w) / (i, j, c) indices without integer division sequences.
 typedef struct {
@@ -24,10 +31,14 @@ typedef struct {
 
 typedef struct {
   const void* src;
-  int mode;  // 0 none, 1 u8 nchw, 2 bf16 nhwc, 3 transposed-conv gather, 4 OHWI weight transpose
+  int mode;  // 0 none, 1 u8 nchw, 2 bf16 nhwc, 3 transposed-conv gather, 4 OHWI weight transpose,
+             // 5 sub-pixel transposed conv, 6 phase-selected OHWI weight
   int B, C, H, W, KH, KW, S, OH, OW;
   float scale;
   AcaFastDiv fd_ohw, fd_ow, fd_hw, fd_w, fd_khw, fd_kw, fd_kwc, fd_c, fd_s;
+  // modes 5/6 (sub-pixel): HS = H/S, WS = W/S, KHS = KH/S, KWS = KW/S
+  int HS, WS, KHS, KWS;
+  AcaFastDiv fd_phase, fd_hsws, fd_ws, fd_kwsc, fd_kws;
 } AcaConvGather;
 
 static inline AcaFastDiv aca_fastdiv_init(unsigned int d) {
@@ -50,6 +61,14 @@ static inline void aca_gather_prepare(AcaConvGather* g) {
   g->fd_kwc = aca_fastdiv_init((unsigned int)(g->KW * g->C > 0 ? g->KW * g->C : 1));
   g->fd_c = aca_fastdiv_init((unsigned int)(g->C > 0 ? g->C : 1));
   g->fd_s = aca_fastdiv_init((unsigned int)(g->S > 0 ? g->S : 1));
+  if (g->S > 0) {
+    g->HS = g->H / g->S; g->WS = g->W / g->S; g->KHS = g->KH / g->S; g->KWS = g->KW / g->S;
+    g->fd_phase = aca_fastdiv_init((unsigned int)(g->B * g->HS * g->WS > 0 ? g->B * g->HS * g->WS : 1));
+    g->fd_hsws = aca_fastdiv_init((unsigned int)(g->HS * g->WS > 0 ? g->HS * g->WS : 1));
+    g->fd_ws = aca_fastdiv_init((unsigned int)(g->WS > 0 ? g->WS : 1));
+    g->fd_kwsc = aca_fastdiv_init((unsigned int)(g->KWS * g->C > 0 ? g->KWS * g->C : 1));
+    g->fd_kws = aca_fastdiv_init((unsigned int)(g->KWS > 0 ? g->KWS : 1));
+  }
 }
 
 typedef struct {
@@ -73,6 +92,7 @@ typedef struct {
   int splits;
   AcaConvGather ga;   // gather for A (requires a_k)
   AcaConvGather gb;   // gather for B (requires !b_k): B[k = conv row m][n = conv column k]
+  unsigned long long* stamps;   // diagnostics (null in production): per workgroup [start, k-loop, epilogue, end]
 } AcaGemmDesc;
 
 #ifdef __cplusplus

@@ -46,7 +46,37 @@ __device__ __forceinline__ uint4 pack8(const u16* t) {
   return r;
 }
 
-// 8 contiguous bf16 at base[row_off + idx] (valid while idx+j < lim)
+// 64 zero bytes in global memory: out-of-range operand chunks are loaded from here, so the loaded registers need
+// no post-processing and their first use is the LDS store after the MFMAs of the current k-step (a select on the
+// loaded data made the compiler drain every load right after issuing it, i.e. no prefetch overlap)
+static __device__ __attribute__((aligned(64))) const unsigned char aca_zero_line[64] = {0};
+
+template <typename T>
+__device__ __forceinline__ const T* zero_or(bool ok, const T* p) {
+  return ok ? p : reinterpret_cast<const T*>(aca_zero_line);
+}
+
+// loads through an explicit global (address space 1) pointer: a select between two generic pointers would
+// otherwise compile to flat_load, which also counts against lgkmcnt and stalls every LDS wait of the k-loop
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) u32x4v gl_u32x4;
+typedef const __attribute__((address_space(1))) unsigned int gl_u32;
+__device__ __forceinline__ uint4 gload16(const void* p) {
+  const u32x4v v = *(gl_u32x4*)(p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint32_t gload4(const void* p) { return *(gl_u32*)(p); }
+
+// Branch-free 16-byte operand chunk (VEC operands: 16-byte aligned rows, ld % 8 == 0 and the contiguous extent
+// % 8 == 0, so a chunk is wholly inside or wholly outside). No per-chunk branch means every chunk load of a k-step
+// is in flight at once; the guarded form below made the compiler wait for each chunk before issuing the next (one
+// memory round trip per chunk).
+__device__ __forceinline__ uint4 load8v(const u16* base, int64_t row_off, int idx, int lim, bool row_ok) {
+  const bool ok = row_ok && idx < lim;
+  return gload16(zero_or(ok, base + row_off + idx));
+}
+
+// 8 contiguous bf16 at base[row_off + idx] (valid while idx+j < lim): any alignment / extent (scalar fallback)
 __device__ __forceinline__ uint4 load8(const u16* base, int64_t row_off, int idx, int lim, bool row_ok) {
   if (!row_ok) return make_uint4(0, 0, 0, 0);
   const u16* p = base + row_off + idx;
@@ -82,6 +112,13 @@ __device__ __forceinline__ GCtx gctx_a(const AcaConvGather& g, int m, bool ok) {
     c.base = (int64_t)b * g.OH * g.OW;
     c.p = ih;
     c.q = p - ih * g.W;
+  } else if (MODE == 5) {
+    const int ph_pw = fdiv(m, g.fd_phase), r = m - ph_pw * g.B * g.HS * g.WS;
+    const int b = fdiv(r, g.fd_hsws), p = r - b * g.HS * g.WS;
+    const int a = fdiv(p, g.fd_ws);
+    c.base = (int64_t)b * g.OH * g.OW;
+    c.p = a;
+    c.q = p - a * g.WS;
   } else {
     const int b = fdiv(m, g.fd_ohw), p = m - b * g.OH * g.OW;
     const int oh = fdiv(p, g.fd_ow), ow = p - oh * g.OW;
@@ -91,9 +128,13 @@ __device__ __forceinline__ GCtx gctx_a(const AcaConvGather& g, int m, bool ok) {
   return c;
 }
 
-__device__ __forceinline__ uint4 u8x8_scaled(const uint8_t* src, float scale) {
-  const uint32_t w0 = *reinterpret_cast<const uint32_t*>(src);
-  const uint32_t w1 = *reinterpret_cast<const uint32_t*>(src + 4);
+// mode-1 (uint8) chunks travel as two raw 32-bit words (x, y) and are converted when stored to LDS
+__device__ __forceinline__ uint4 u8x8_raw(const uint8_t* src) {
+  return make_uint4(gload4(src), gload4(src + 4), 0u, 0u);
+}
+
+__device__ __forceinline__ uint4 u8x8_convert(uint4 raw, float scale) {
+  const uint32_t w0 = raw.x, w1 = raw.y;
   u16 t[8];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -103,35 +144,53 @@ __device__ __forceinline__ uint4 u8x8_scaled(const uint8_t* src, float scale) {
   return pack8(t);
 }
 
-// 8 consecutive k of the A row described by c (k % 8 == 0)
+// 8 consecutive k of the A row described by c (k % 8 == 0); branch-free (see load8v)
 template <int MODE>
 __device__ __forceinline__ uint4 gather_a(const AcaConvGather& g, const GCtx& c, int k, bool kok) {
-  if (!(c.ok && kok)) return make_uint4(0, 0, 0, 0);
+  bool ok = c.ok && kok;
   if (MODE == 1) {
     const int ci = fdiv(k, g.fd_khw), r = k - ci * g.KH * g.KW;
     const int i = fdiv(r, g.fd_kw), j = r - i * g.KW;
-    return u8x8_scaled(reinterpret_cast<const uint8_t*>(g.src) + c.base + ((int64_t)ci * g.H + i) * g.W + j,
-                       g.scale);
+    const int64_t off = c.base + ((int64_t)ci * g.H + i) * g.W + j;
+    return u8x8_raw(zero_or(ok, reinterpret_cast<const uint8_t*>(g.src) + off));
+  }
+  if (MODE == 5) {
+    // k = (di, dj, o): source pixel (a - di, c - dj) of the output gradient
+    const int di = fdiv(k, g.fd_kwsc), r = k - di * g.KWS * g.C;
+    const int dj = fdiv(r, g.fd_c), cc = r - dj * g.C;
+    const int sh = c.p - di, sw = c.q - dj;
+    ok = ok && sh >= 0 && sw >= 0 && sh < g.OH && sw < g.OW;
+    const int64_t off5 = (c.base + (int64_t)sh * g.OW + sw) * g.C + cc;
+    return gload16(zero_or(ok, reinterpret_cast<const u16*>(g.src) + off5));
   }
   const int i = fdiv(k, g.fd_kwc), r = k - i * g.KW * g.C;
   const int j = fdiv(r, g.fd_c), cc = r - j * g.C;
-  if (MODE == 2)
-    return *reinterpret_cast<const uint4*>(reinterpret_cast<const u16*>(g.src) + c.base + (i * g.W + j) * g.C + cc);
-  // MODE 3: transposed conv (data gradient): source pixel ((ih - i) / S, (iw - j) / S) when on the stride grid
-  const int th = c.p - i, tw = c.q - j;
-  if (th < 0 || tw < 0) return make_uint4(0, 0, 0, 0);
-  const int sh = fdiv(th, g.fd_s), sw = fdiv(tw, g.fd_s);
-  if (sh * g.S != th || sw * g.S != tw || sh >= g.OH || sw >= g.OW) return make_uint4(0, 0, 0, 0);
-  return *reinterpret_cast<const uint4*>(reinterpret_cast<const u16*>(g.src) +
-                                         ((c.base + (int64_t)sh * g.OW + sw) * g.C + cc));
+  int64_t off;
+  if (MODE == 2) {
+    off = c.base + (i * g.W + j) * g.C + cc;
+  } else {
+    // MODE 3: transposed conv (data gradient): source pixel ((ih - i) / S, (iw - j) / S) when on the stride grid
+    const int th = c.p - i, tw = c.q - j;
+    const int sh = fdiv(max(th, 0), g.fd_s), sw = fdiv(max(tw, 0), g.fd_s);
+    ok = ok && th >= 0 && tw >= 0 && sh * g.S == th && sw * g.S == tw && sh < g.OH && sw < g.OW;
+    off = (c.base + (int64_t)sh * g.OW + sw) * g.C + cc;
+  }
+  return gload16(zero_or(ok, reinterpret_cast<const u16*>(g.src) + off));
 }
 
 // B operand (modes 1/2: weight gradient, B[k = conv row][n = conv column]; mode 4: OHWI weight read as
 // B[k = (i, j, o)][n]): fixed column n of this chunk
 template <int MODE>
-__device__ __forceinline__ GCtx gctx_b(const AcaConvGather& g, int n, bool ok) {
+__device__ __forceinline__ GCtx gctx_b(const AcaConvGather& g, int n, bool ok, int phase = 0) {
   GCtx c{0, 0, 0, ok ? 1 : 0};
   if (!ok) return c;
+  if (MODE == 6) {   // phase (ph, pw) of the workgroup's rows
+    const int ph = fdiv(phase, g.fd_s);
+    c.p = ph;
+    c.q = phase - ph * g.S;
+    c.base = n;
+    return c;
+  }
   if (MODE == 1) {
     const int ci = fdiv(n, g.fd_khw), r = n - ci * g.KH * g.KW;
     const int i = fdiv(r, g.fd_kw), j = r - i * g.KW;
@@ -148,20 +207,27 @@ __device__ __forceinline__ GCtx gctx_b(const AcaConvGather& g, int n, bool ok) {
 
 template <int MODE>
 __device__ __forceinline__ uint4 gather_b(const AcaConvGather& g, const GCtx& c, int k, bool kok) {
-  if (!(c.ok && kok)) return make_uint4(0, 0, 0, 0);
+  const bool ok = c.ok && kok;
+  if (MODE == 6) {
+    const int di = fdiv(k, g.fd_kwsc), r = k - di * g.KWS * g.C;
+    const int dj = fdiv(r, g.fd_c), o = r - dj * g.C;
+    const int i = c.p + g.S * di, j = c.q + g.S * dj;
+    const int64_t off = (((int64_t)o * g.KH + i) * g.KW + j) * g.W + c.base;
+    return gload16(zero_or(ok, reinterpret_cast<const u16*>(g.src) + off));
+  }
   if (MODE == 4) {
     const int ij = fdiv(k, g.fd_c), o = k - ij * g.C;
-    return *reinterpret_cast<const uint4*>(reinterpret_cast<const u16*>(g.src) +
-                                           ((int64_t)o * g.KH * g.KW + ij) * g.W + c.base);
+    const int64_t off = ((int64_t)o * g.KH * g.KW + ij) * g.W + c.base;
+    return gload16(zero_or(ok, reinterpret_cast<const u16*>(g.src) + off));
   }
   const int b = fdiv(k, g.fd_ohw), p = k - b * g.OH * g.OW;
   const int oh = fdiv(p, g.fd_ow), ow = p - oh * g.OW;
   if (MODE == 1) {
     const int64_t rb = (((int64_t)b * g.C) * g.H + oh * g.S) * g.W + ow * g.S;
-    return u8x8_scaled(reinterpret_cast<const uint8_t*>(g.src) + rb + c.base, g.scale);
+    return u8x8_raw(zero_or(ok, reinterpret_cast<const uint8_t*>(g.src) + rb + c.base));
   }
   const int64_t rb = (((int64_t)b * g.H + oh * g.S) * g.W + ow * g.S) * g.C;
-  return *reinterpret_cast<const uint4*>(reinterpret_cast<const u16*>(g.src) + rb + c.base);
+  return gload16(zero_or(ok, reinterpret_cast<const u16*>(g.src) + rb + c.base));
 }
 
 struct GemmParams {
@@ -170,7 +236,7 @@ struct GemmParams {
   int splits;
 };
 
-template <int BM, int BN, int BK, bool A_K, bool B_K, int AG, int BG>
+template <int BM, int BN, int BK, bool A_K, bool B_K, int AG, int BG, bool VEC>
 __global__ void __launch_bounds__(256) gemm_kernel(GemmParams P) {
   const AcaGemmDesc& g = P.d;
   constexpr int A_ELEMS = A_K ? BM * (BK + GEMM_PAD) : BK * (BM + GEMM_PAD);
@@ -198,13 +264,17 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmParams P) {
   const int kt0 = z * P.k_tiles_per_split;
   const int kt1 = min(kt0 + P.k_tiles_per_split, k_tiles_total);
 
+  unsigned long long* const st =
+      g.stamps ? g.stamps + ((size_t)blockIdx.z * gridDim.x + blockIdx.x) * 4 : nullptr;
+  if (st && tid == 0) st[0] = __builtin_amdgcn_s_memrealtime();
   floatx4 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  uint4 ra[A_CHUNKS], rb[B_CHUNKS];
+  // two register sets: the k-loop keeps two k-steps of operand loads in flight (prefetch distance 2)
+  uint4 ra0[A_CHUNKS], rb0[B_CHUNKS], ra1[A_CHUNKS], rb1[B_CHUNKS];
   // gather contexts of this thread's fixed staging slots (decoded once)
   GCtx actx[AG ? A_CHUNKS : 1], bctx[BG ? B_CHUNKS : 1];
   if (AG) {
@@ -218,11 +288,11 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmParams P) {
 #pragma unroll
     for (int c = 0; c < B_CHUNKS; ++c) {
       const int nc = ((tid + c * 256) % (BN / 8)) * 8;
-      bctx[c] = gctx_b<BG>(g.gb, n0 + nc, n0 + nc < g.N);
+      bctx[c] = gctx_b<BG>(g.gb, n0 + nc, n0 + nc < g.N, BG == 6 ? fdiv(m0, g.ga.fd_phase) : 0);
     }
   }
 
-  auto gload = [&](int kt) {
+  auto gload = [&](int kt, uint4 (&ra)[A_CHUNKS], uint4 (&rb)[B_CHUNKS]) {
     const int k0 = kt * BK;
 #pragma unroll
     for (int c = 0; c < A_CHUNKS; ++c) {
@@ -231,11 +301,13 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmParams P) {
         const int r = ch / (BK / 8), kc = (ch % (BK / 8)) * 8;
         const int m = m0 + r;
         if (AG) ra[c] = gather_a<AG>(g.ga, actx[AG ? c : 0], k0 + kc, k0 + kc < g.K);
+        else if (VEC) ra[c] = load8v(Ag, (int64_t)m * g.lda, k0 + kc, g.K, m < g.M);
         else ra[c] = load8(Ag, (int64_t)m * g.lda, k0 + kc, g.K, m < g.M);
       } else {
         const int kr = ch / (BM / 8), mc = (ch % (BM / 8)) * 8;
         const int k = k0 + kr;
-        ra[c] = load8(Ag, (int64_t)k * g.lda, m0 + mc, g.M, k < g.K);
+        ra[c] = VEC ? load8v(Ag, (int64_t)k * g.lda, m0 + mc, g.M, k < g.K)
+                    : load8(Ag, (int64_t)k * g.lda, m0 + mc, g.M, k < g.K);
       }
     }
 #pragma unroll
@@ -244,23 +316,25 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmParams P) {
       if (B_K) {
         const int r = ch / (BK / 8), kc = (ch % (BK / 8)) * 8;
         const int n = n0 + r;
-        rb[c] = load8(Bg, (int64_t)n * g.ldb, k0 + kc, g.K, n < g.N);
+        rb[c] = VEC ? load8v(Bg, (int64_t)n * g.ldb, k0 + kc, g.K, n < g.N)
+                    : load8(Bg, (int64_t)n * g.ldb, k0 + kc, g.K, n < g.N);
       } else {
         const int kr = ch / (BN / 8), nc = (ch % (BN / 8)) * 8;
         const int k = k0 + kr;
         if (BG) rb[c] = gather_b<BG>(g.gb, bctx[BG ? c : 0], k, k < g.K);
+        else if (VEC) rb[c] = load8v(Bg, (int64_t)k * g.ldb, n0 + nc, g.N, k < g.K);
         else rb[c] = load8(Bg, (int64_t)k * g.ldb, n0 + nc, g.N, k < g.K);
       }
     }
   };
-  auto sstore = [&](int buf) {
+  auto sstore = [&](int buf, const uint4 (&ra)[A_CHUNKS], const uint4 (&rb)[B_CHUNKS]) {
 #pragma unroll
     for (int c = 0; c < A_CHUNKS; ++c) {
       const int ch = tid + c * 256;
       int off;
       if (A_K) off = (ch / (BK / 8)) * (BK + GEMM_PAD) + (ch % (BK / 8)) * 8;
       else off = (ch / (BM / 8)) * (BM + GEMM_PAD) + (ch % (BM / 8)) * 8;
-      *reinterpret_cast<uint4*>(As0 + buf * A_ELEMS + off) = ra[c];
+      *reinterpret_cast<uint4*>(As0 + buf * A_ELEMS + off) = AG == 1 ? u8x8_convert(ra[c], g.ga.scale) : ra[c];
     }
 #pragma unroll
     for (int c = 0; c < B_CHUNKS; ++c) {
@@ -268,7 +342,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmParams P) {
       int off;
       if (B_K) off = (ch / (BK / 8)) * (BK + GEMM_PAD) + (ch % (BK / 8)) * 8;
       else off = (ch / (BN / 8)) * (BN + GEMM_PAD) + (ch % (BN / 8)) * 8;
-      *reinterpret_cast<uint4*>(Bs0 + buf * B_ELEMS + off) = rb[c];
+      *reinterpret_cast<uint4*>(Bs0 + buf * B_ELEMS + off) = BG == 1 ? u8x8_convert(rb[c], g.gb.scale) : rb[c];
     }
   };
 
@@ -290,34 +364,51 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmParams P) {
     }
   };
 
+  auto compute = [&](int buf) {
+    const u16* as = As0 + buf * A_ELEMS;
+    const u16* bs = Bs0 + buf * B_ELEMS;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      bf16x8 af[TM], bfr[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = frag(as, A_K, BM, wm * (BM / 2) + i * 16, ks);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = frag(bs, B_K, BN, wn * (BN / 2) + j * 16, ks);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  // Pipeline (small products are latency-bound: a k-step's MFMA work is far shorter than an L2 round trip, so
+  // with one step of prefetch every step costs a full round trip). Register set s holds k-step kt+2 while LDS
+  // buffer b holds kt and the other register set waits to be stored as kt+1: loads are issued two k-steps ahead,
+  // unconditionally (steps past the end read the zero line or a neighbouring split's data that is never stored),
+  // so the loop body has no data-dependent branch around its loads.
   if (kt0 < kt1) {
-    gload(kt0);
-    sstore(0);
+    gload(kt0, ra0, rb0);
+    gload(kt0 + 1, ra1, rb1);
+    sstore(0, ra0, rb0);
     __syncthreads();
-    for (int kt = kt0; kt < kt1; ++kt) {
-      const int buf = (kt - kt0) & 1;
-      const bool more = kt + 1 < kt1;
-      if (more) gload(kt + 1);
-      const u16* as = As0 + buf * A_ELEMS;
-      const u16* bs = Bs0 + buf * B_ELEMS;
-#pragma unroll
-      for (int ks = 0; ks < BK / 32; ++ks) {
-        bf16x8 af[TM], bfr[TN];
-#pragma unroll
-        for (int i = 0; i < TM; ++i) af[i] = frag(as, A_K, BM, wm * (BM / 2) + i * 16, ks);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) bfr[j] = frag(bs, B_K, BN, wn * (BN / 2) + j * 16, ks);
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-      }
-      if (more) sstore(buf ^ 1);
+    if (st && tid == 0) st[1] = __builtin_amdgcn_s_memrealtime();
+    // (the LDS stores are unconditional too: a store past the last k-step is never read, and a conditional one
+    // leaves loads pending on one path, which makes the compiler drain them at the loop head)
+    for (int kt = kt0; kt < kt1; kt += 2) {
+      gload(kt + 2, ra0, rb0);
+      compute(0);
+      sstore(1, ra1, rb1);
+      __syncthreads();
+      if (kt + 1 >= kt1) break;
+      gload(kt + 3, ra1, rb1);
+      compute(1);
+      sstore(0, ra0, rb0);
       __syncthreads();
     }
   }
 
+  if (st && tid == 0) st[2] = __builtin_amdgcn_s_memrealtime();
   // ---------------------------------------------------------------- split-K reduction (slab flavour)
   if (P.splits > 1 && g.out_mode < 2) {
     float* slab = g.ws + ((size_t)tile * P.splits + z) * (BM * BN);
@@ -332,24 +423,75 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmParams P) {
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-    for (int s = 0; s < P.splits; ++s) {
-      const float* sl = g.ws + ((size_t)tile * P.splits + s) * (BM * BN);
+    // slabs summed in split order, four splits' loads in flight per round (missing ones read the zero line)
+    typedef const __attribute__((address_space(1))) float gl_f32;
+    for (int s0 = 0; s0 < P.splits; s0 += 4) {
+      float v[4][TM][TN][4];
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+      for (int u = 0; u < 4; ++u) {
+        const bool on = s0 + u < P.splits;
+        const float* sl = g.ws + ((size_t)tile * P.splits + (on ? s0 + u : 0)) * (BM * BN);
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) acc[i][j][r] += sl[((i * TN + j) * 4 + r) * 256 + tid];
+          for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float* q = sl + ((i * TN + j) * 4 + r) * 256 + tid;
+              v[u][i][j][r] = *(gl_f32*)(on ? q : reinterpret_cast<const float*>(aca_zero_line));
+            }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[i][j][r] += v[u][i][j][r];
     }
   }
 
   // ---------------------------------------------------------------- epilogue
+  // output row of GEMM row m (mode 5 rows are phase-major: write each back to its NHWC pixel)
+  auto out_row = [&](int m) -> int64_t {
+    if (AG != 5) return m;
+    const AcaConvGather& a = g.ga;
+    const int ph_pw = fdiv(m, a.fd_phase), r = m - ph_pw * a.B * a.HS * a.WS;
+    const int b = fdiv(r, a.fd_hsws), p = r - b * a.HS * a.WS;
+    const int aa = fdiv(p, a.fd_ws), cc = p - aa * a.WS;
+    const int ph = fdiv(ph_pw, a.fd_s), pw = ph_pw - ph * a.S;
+    return ((int64_t)b * a.H + aa * a.S + ph) * a.W + cc * a.S + pw;
+  };
+  // bias and ReLU-backward mask operands are fetched for every output of this thread up front, branch-free (a
+  // guarded load per output element serialised TM*TN*4 memory round trips at the end of every product)
+  typedef const __attribute__((address_space(1))) u16 gl_u16;
+  typedef const __attribute__((address_space(1))) float gl_f32e;
   const u16* mask = reinterpret_cast<const u16*>(g.mask);
+  float bias_v[TN];
+  u16 mk[TM][TN][4];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = n0 + wn * (BN / 2) + j * 16 + lr16;
     const bool n_ok = n < g.N;
-    const float b = (g.bias && n_ok) ? g.bias[n] : 0.f;
+    bias_v[j] = g.bias ? *(gl_f32e*)(n_ok ? g.bias + n : reinterpret_cast<const float*>(aca_zero_line)) : 0.f;
+    if (mask) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * (BM / 2) + i * 16 + lg * 4 + r;
+          const bool ok = n_ok && m < g.M;
+          const int64_t mr = out_row(m);
+          mk[i][j][r] = *(gl_u16*)(ok ? mask + mr * g.ldm + n : reinterpret_cast<const u16*>(aca_zero_line));
+        }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn * (BN / 2) + j * 16 + lr16;
+    const bool n_ok = n < g.N;
+    const float b = bias_v[j];
     float csum = 0.f;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -363,8 +505,8 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmParams P) {
         }
         float v = acc[i][j][r] * g.alpha + b;
         if (g.relu) v = fmaxf(v, 0.f);
-        if (mask) v = (bf2f(mask[(int64_t)m * g.ldm + n]) > 0.f) ? v : 0.f;
-        const int64_t ci = (int64_t)m * g.ldc + n;
+        if (mask) v = (bf2f(mk[i][j][r]) > 0.f) ? v : 0.f;
+        const int64_t ci = out_row(m) * g.ldc + n;
         if (g.out_mode == 0) reinterpret_cast<float*>(g.C)[ci] = v;
         else if (g.out_mode == 1) reinterpret_cast<u16*>(g.C)[ci] = f2bf(v);
         else atomicAdd(reinterpret_cast<float*>(g.C) + ci, v);
@@ -377,39 +519,48 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmParams P) {
       if (lg == 0 && n_ok) atomicAdd(&g.colsum[g.colsum_mod ? n % g.colsum_mod : n], csum);
     }
   }
+  if (st) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (tid == 0) st[3] = __builtin_amdgcn_s_memrealtime();
+  }
 }
 
-template <int BM, int BN, int BK, bool A_K, bool B_K, int AG, int BG>
+template <int BM, int BN, int BK, bool A_K, bool B_K, int AG, int BG, bool VEC>
 hipError_t gemm_launch(const GemmParams& P, hipStream_t s) {
   const int tiles = ((P.d.M + BM - 1) / BM) * ((P.d.N + BN - 1) / BN);
   dim3 grid(tiles, 1, P.splits);
-  gemm_kernel<BM, BN, BK, A_K, B_K, AG, BG><<<grid, 256, 0, s>>>(P);
+  gemm_kernel<BM, BN, BK, A_K, B_K, AG, BG, VEC><<<grid, 256, 0, s>>>(P);
   return hipGetLastError();
 }
 
 // dispatch over the supported (tile, bk) pairs for one operand family
-template <bool A_K, bool B_K, int AG, int BG>
+template <bool A_K, bool B_K, int AG, int BG, bool VEC>
 hipError_t gemm_dispatch_tiles(const GemmParams& P, hipStream_t s) {
   const int t = P.d.tile, bk = P.d.bk;
   if (bk == 64) {
     switch (t) {
-      case 0: return gemm_launch<64, 64, 64, A_K, B_K, AG, BG>(P, s);
-      case 1: return gemm_launch<32, 64, 64, A_K, B_K, AG, BG>(P, s);
-      case 2: return gemm_launch<64, 32, 64, A_K, B_K, AG, BG>(P, s);
-      case 3: return gemm_launch<128, 64, 64, A_K, B_K, AG, BG>(P, s);
-      case 4: return gemm_launch<32, 32, 64, A_K, B_K, AG, BG>(P, s);
+      case 0: return gemm_launch<64, 64, 64, A_K, B_K, AG, BG, VEC>(P, s);
+      case 1: return gemm_launch<32, 64, 64, A_K, B_K, AG, BG, VEC>(P, s);
+      case 2: return gemm_launch<64, 32, 64, A_K, B_K, AG, BG, VEC>(P, s);
+      case 3: return gemm_launch<128, 64, 64, A_K, B_K, AG, BG, VEC>(P, s);
+      case 4: return gemm_launch<32, 32, 64, A_K, B_K, AG, BG, VEC>(P, s);
     }
   } else if (bk == 128) {
     switch (t) {
-      case 0: return gemm_launch<64, 64, 128, A_K, B_K, AG, BG>(P, s);
-      case 1: return gemm_launch<32, 64, 128, A_K, B_K, AG, BG>(P, s);
-      case 2: return gemm_launch<64, 32, 128, A_K, B_K, AG, BG>(P, s);
-      case 4: return gemm_launch<32, 32, 128, A_K, B_K, AG, BG>(P, s);
+      case 0: return gemm_launch<64, 64, 128, A_K, B_K, AG, BG, VEC>(P, s);
+      case 1: return gemm_launch<32, 64, 128, A_K, B_K, AG, BG, VEC>(P, s);
+      case 2: return gemm_launch<64, 32, 128, A_K, B_K, AG, BG, VEC>(P, s);
+      case 4: return gemm_launch<32, 32, 128, A_K, B_K, AG, BG, VEC>(P, s);
     }
   } else if (bk == 256) {
-    if (t == 4) return gemm_launch<32, 32, 256, A_K, B_K, AG, BG>(P, s);
+    if (t == 4) return gemm_launch<32, 32, 256, A_K, B_K, AG, BG, VEC>(P, s);
   }
   return hipErrorInvalidValue;
+}
+
+// vector-loadable plain operand: 16-byte aligned base, row stride % 8 == 0, contiguous extent % 8 == 0
+inline bool gemm_operand_vec(const void* p, int64_t ld, int contig_extent) {
+  return (reinterpret_cast<uintptr_t>(p) % 16 == 0) && (ld % 8 == 0) && (contig_extent % 8 == 0);
 }
 
 }  // namespace aca

@@ -336,8 +336,10 @@ def test_cnn_trunk_fused_matches_layers(cuda):
     assert torch.allclose(y3.float().view(B, 7, 7, 64).permute(0, 3, 1, 2), r3, rtol=1e-2, atol=1e-2)
 
 
-@pytest.mark.parametrize("k,s,H,Cout,Cin,B", [(3, 1, 9, 64, 64, 5), (4, 2, 20, 64, 32, 3), (8, 4, 84, 32, 8, 2)])
-def test_gemm_transposed_conv_dgrad(cuda, k, s, H, Cout, Cin, B):
+@pytest.mark.parametrize("k,s,H,Cout,Cin,B,subpixel", [(3, 1, 9, 64, 64, 5, False), (4, 2, 20, 64, 32, 3, False),
+                                                        (8, 4, 84, 32, 8, 2, False), (4, 2, 20, 64, 32, 160, True),
+                                                        (8, 4, 84, 32, 8, 32, True), (4, 2, 20, 64, 32, 16, True)])
+def test_gemm_transposed_conv_dgrad(cuda, k, s, H, Cout, Cin, B, subpixel):
     """Data-gradient GEMM (A gathered from dy on the stride grid, B = OHWI weight read transposed) vs
     torch conv_transpose2d, with the ReLU mask and bias-gradient column sums of the epilogue."""
     from actor_critic_algs_on_tensorflow_amd.ops import gemm as G
@@ -349,17 +351,27 @@ def test_gemm_transposed_conv_dgrad(cuda, k, s, H, Cout, Cin, B):
     ymask = (torch.rand(B * H * H, Cin, device=cuda) > 0.3).to(torch.bfloat16)
     out = torch.empty(B * H * H, Cin, dtype=torch.bfloat16, device=cuda)
     cs = torch.zeros(Cin, device=cuda)
+    ran = 0
     for tile, bk in ((4, 64), (2, 128), (0, 64)):
         cs.zero_()
-        G._native.require().gemm(dy, 0, True, W, 0, False, out, Cin, 1, B * H * H, Cin, k * k * Cout, 1.0, None,
-                                 False, ymask, Cin, cs, 0, tile, bk, 1, None, None, [3, B, Cout, H, H, k, k, s], 1.0,
-                                 [4, 1, Cout, 1, Cin, k, k, 1], 1.0)
+        if subpixel:   # rows per phase B*(H/s)^2 must be a multiple of the tile height
+            if (B * (H // s) ** 2) % G.TILES[tile][0]:
+                continue
+            G._native.require().gemm(dy, 0, True, W, 0, False, out, Cin, 1, B * H * H, Cin, (k // s) ** 2 * Cout, 1.0,
+                                     None, False, ymask, Cin, cs, 0, tile, bk, 1, None, None,
+                                     [5, B, Cout, H, H, k, k, s], 1.0, [6, 1, Cout, 1, Cin, k, k, s], 1.0)
+        else:
+            G._native.require().gemm(dy, 0, True, W, 0, False, out, Cin, 1, B * H * H, Cin, k * k * Cout, 1.0, None,
+                                     False, ymask, Cin, cs, 0, tile, bk, 1, None, None, [3, B, Cout, H, H, k, k, s],
+                                     1.0, [4, 1, Cout, 1, Cin, k, k, 1], 1.0)
         ref = F.conv_transpose2d(dy.float().permute(0, 3, 1, 2), W.float().permute(0, 3, 1, 2), stride=s)
         ref = ref[:, :, :H, :H].permute(0, 2, 3, 1).reshape(B * H * H, Cin) * ymask.float()
         assert torch.allclose(out.float(), ref, rtol=2e-2, atol=2e-2), (tile, bk, (out.float() - ref).abs().max())
         # column sums are taken from the fp32 values before the bf16 store
         err = (cs - ref.sum(0)).abs()
         assert (err <= 1e-2 * ref.abs().sum(0) + 1e-2).all(), (tile, bk, err.max())
+        ran += 1
+    assert ran > 0
 
 
 def test_trainer_native_graph_updates(cuda):

@@ -199,20 +199,38 @@ class CNNEngine:
         return shifted if want_shift else b.z
 
     # ------------------------------------------------------------------------------------------------ backward
-    def backward(self, b: _Bufs, head_bias_done=False):
+    def tail_bucket(self):
+        """(start, end) slab offsets of the parameters whose gradients are final after the ``"tail"`` backward stage
+        (fc + policy/value head: 95% of the bytes). They are contiguous at the end of the slab, so data parallelism
+        can all-reduce them while the conv backward (``"trunk"`` stage) still runs."""
+        base = self.flat.grad.data_ptr()
+        start = (self.gWfc.data_ptr() - base) // 4
+        end = (self.gbh.data_ptr() - base) // 4 + self.gbh.numel()
+        for g in (self.gW1, self.gb1, self.gW2, self.gb2, self.gW3, self.gb3):
+            assert (g.data_ptr() - base) // 4 + g.numel() <= start, "conv gradients must precede the fc/head bucket"
+        for g in (self.gbfc, self.gWh):
+            assert start <= (g.data_ptr() - base) // 4 < end
+        return start, end
+
+    def backward(self, b: _Bufs, head_bias_done=False, stage="all"):
         """Accumulates d(loss)/d(params) into the gradient slab from ``b.dz`` (written by the loss kernel).
 
         Two streams: the activation-gradient chain (dh -> dy3 -> dy2 -> dy1) runs on the current stream while
         every weight-gradient product runs on a side stream as soon as its input gradient exists, so the
         critical path is the dX chain plus the last dW (captured as parallel branches of the hipGraph).
+
+        ``stage``: ``"all"``; or ``"tail"`` (head + fc gradients, ending with both streams joined so the fc/head
+        gradient bucket is final) followed later by ``"trunk"`` (conv gradients) -- data parallelism issues the
+        all-reduce of :meth:`tail_bucket` between the two (overlapping the conv backward).
         """
         B, A1, ws = b.B, self.A1, self.ws
         ops = _native.require()
-        imp = self.implicit
         main = torch.cuda.current_stream(self.dev)
         side = self.side
         ev = self._ev
         ws2 = self._side_ws()
+        if stage == "trunk":
+            return self._backward_trunk(b, main, side, ev, ws, ws2)
         ev[0].record(main)
         side.wait_event(ev[0])
         with torch.cuda.stream(side):   # heads: dWh = h^T dz, dbh = colsum(dz)
@@ -227,6 +245,15 @@ class CNNEngine:
             G.gemm(b.y3, 3136, False, b.dh, 512, False, self.gWfc, 512, 2, 3136, 512, B, workspace=ws2)
         G.gemm(b.dh, 512, True, self.sWfc, 512, True, b.dy3, 3136, 1, B, 3136, 512, mask=b.y3, ldm=3136,
                colsum=self.gb3, colsum_mod=64, workspace=ws)
+        if stage == "tail":
+            ev[5].record(side)
+            main.wait_event(ev[5])
+            return
+        return self._backward_trunk(b, main, side, ev, ws, ws2)
+
+    def _backward_trunk(self, b, main, side, ev, ws, ws2):
+        B = b.B
+        imp = self.implicit
         ev[2].record(main)
         side.wait_event(ev[2])
         with torch.cuda.stream(side):   # conv3 weight gradient

@@ -79,6 +79,8 @@ class ActorCriticTrainer:
                 opt = make_optimizer(cfg.optimizer, self.flat, g, cfg.lr, cfg.clip_value, cfg.max_grad_norm,
                                      bf16_shadow=sh)
             opt.zero_grad_after = self.engine is not None
+            if dp is not None:
+                opt.grad_mul = dp.grad_mul   # the all-reduce leaves the sum; the update kernel averages on read
             self.opts[g] = opt
         self.actor_opt = self.opts.get("actor", self.opts.get("shared"))
         T, N = cfg.n_steps, self.env.num_envs
@@ -101,6 +103,10 @@ class ActorCriticTrainer:
         self.env_steps = 0
         self.graph = None
         self._defer_allreduce = False
+        self._bw_stage = "all"      # "tail" while capturing the first segment of the bucketed DP update
+        self._bw_pending = None
+        self._comm_grad = None      # lag-1 DP: the all-reduced copy of the previous update's gradient
+        self._comm_work = None
         self.logger = None
         if self.rank == 0 and cfg.outdir:
             self.logger = Logger(cfg.outdir, legacy_step_index=cfg.legacy_step_index, metrics_path=cfg.metrics_path,
@@ -229,7 +235,7 @@ class ActorCriticTrainer:
         if self._defer_allreduce:
             return
         if self.dp is not None:
-            self.dp.allreduce_grads(self.flat)
+            self.dp.allreduce_grads(self.flat, scale=False)
         self._run_optimizers()
 
     def _run_optimizers(self):
@@ -305,7 +311,8 @@ class ActorCriticTrainer:
         # the loss kernel writes its statistics straight into stats_buf[0:7]
         eng.loss(b, actions, logp_old, adv, ret, v_old if ppo else None, self.ent_coef, self.kl_coef, vf,
                  cfg.ppo_clip if ppo else 0.0, cfg.ppo_value_clip if ppo else 0.0, stats=self.stats_buf)
-        eng.backward(b)   # gradient slab is clean: the optimiser zeroed it after its last use
+        eng.backward(b, stage=self._bw_stage)   # gradient slab is clean: the optimiser zeroed it after its last use
+        self._bw_pending = (b, False)
         self._apply_grads()
 
     @torch.no_grad()
@@ -326,7 +333,8 @@ class ActorCriticTrainer:
                  returns=dict(mode=1 if cfg.returns == "nstep" else 2, rew=st.rewards, val=st.values, dones=st.dones,
                               L=T if cfg.look_ahead is None else cfg.look_ahead, gamma=cfg.gamma,
                               lam=cfg.gae_lambda, norm_adv=cfg.norm_adv, ret_w=self._ret_w, adv_w=self._adv_w))
-        eng.backward(b, head_bias_done=True)
+        eng.backward(b, head_bias_done=True, stage=self._bw_stage)
+        self._bw_pending = (b, True)
         self._apply_grads()
         self._last = (obs, actions, logp_old, self._ret_w)
         if not self._defer_allreduce:
@@ -382,24 +390,52 @@ class ActorCriticTrainer:
             self._kl_and_lr(logp_old, logp, ret, z[:, eng.A])
 
     # ------------------------------------------------------------------ driver
-    # An update is split in two segments around the gradient all-reduce:
-    #   pre  = rollout + returns + forward + loss + backward   (everything up to the gradient slab)
-    #   post = optimiser step(s) + statistics
-    # Without DP the whole update is ONE captured hipGraph. With DP (single optimiser step per update) each
-    # segment is its own graph and the RCCL all-reduce of the flat gradient slab is issued between the two replays
-    # (one collective per update). PPO with DP runs eagerly (many optimiser steps per update).
+    # Without DP the whole update is ONE captured hipGraph. With DP (native engine, one optimiser step per update)
+    # the update is split into captured segments around the RCCL collectives, which are issued from the host between
+    # replays (async w.r.t. the host: the stream waits, the CPU does not):
+    #   overlap="strict" (exact synchronous A2C, the default):
+    #       pre   = rollout + returns + loss + backward of the head and fc layers        (graph 1)
+    #       AR(fc/head bucket, 95% of the bytes) on the RCCL stream    || mid = conv backward (graph 2)
+    #       AR(conv bucket) ; the main stream waits for both ; post = optimiser + stats    (graph 3)
+    #   overlap="lag1" (policy lag 1, BASELINE's "all-reduce overlapped with the next rollout"):
+    #       pre   = rollout + returns + loss + full backward into the gradient slab G     (graph 1)
+    #               || AR(C) of the PREVIOUS update's gradient, issued at the end of the previous step
+    #       wait ; post = optimiser step reading C (the previous gradient) + move G -> C, G = 0   (graph 2)
+    #       AR(C) issued, overlapping the next update's rollout.
+    #     Every gradient is on-policy for its batch (computed at the parameters that acted) and applied one update
+    #     late (delayed-gradient SGD with staleness 1).
+    # PPO with DP, and configurations that need collectives inside the update (global advantage normalisation,
+    # the KL-adaptive lr), run eagerly with synchronous collectives.
 
     def _can_capture(self):
         return self.cfg.cuda_graph and self.device.type == "cuda"
 
     def _segmented(self):
-        return self.dp is not None and self.cfg.algo != "ppo" and self.engine is not None
+        cfg = self.cfg
+        return (self.dp is not None and cfg.algo == "a2c" and self.engine is not None and not cfg.norm_adv
+                and self.lr_ctrl is None and cfg.kl_coef == 0.0)
 
     def update_body(self):
         self.collect()
         ret, adv = self.compute_returns()
         self.learn(ret, adv)
         self.storage.roll_over()
+
+    def _post_body(self):
+        self._run_optimizers()
+        self._finish_learn()
+
+    def _lag1(self):
+        return self.cfg.overlap == "lag1"
+
+    def _grad_move(self):
+        """lag-1: C <- G, G <- 0 (one launch) so the next backward accumulates into a clean slab while C is
+        all-reduced and consumed by the next optimiser step."""
+        if _native.use_native(self.flat.grad):
+            _native.require().grad_move(self.flat.grad, self._comm_grad)
+        else:
+            self._comm_grad.copy_(self.flat.grad)
+            self.flat.grad.zero_()
 
     def capture(self, warmup=2):
         """Capture the update as hipGraph(s) (see above). Warm-up updates run first (GEMM autotuning, allocator)."""
@@ -415,25 +451,68 @@ class ActorCriticTrainer:
         if self._segmented():
             self._defer_allreduce = True
             try:
-                g1 = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g1):
-                    self.collect()
-                    ret, adv = self.compute_returns()
-                    self.learn(ret, adv)
-                g2 = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g2):
-                    self._run_optimizers()
-                    self._finish_learn()
-                    self.storage.roll_over()
+                if self._lag1():
+                    self._comm_grad = torch.zeros_like(self.flat.grad)
+                    for opt in self.opts.values():
+                        opt.bind_grad(self._comm_grad)
+                    g1 = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g1):
+                        self.update_body()
+                    g2 = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g2):
+                        self._post_body()
+                        self._grad_move()
+                    self.graph = ("lag1", g1, g2)
+                else:
+                    self._bw_stage = "tail"
+                    g1 = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g1):
+                        self.collect()
+                        ret, adv = self.compute_returns()
+                        self.learn(ret, adv)
+                    self._bw_stage = "all"
+                    b, hb = self._bw_pending
+                    g2 = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g2):
+                        self.engine.backward(b, head_bias_done=hb, stage="trunk")
+                    g3 = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g3):
+                        self._post_body()
+                        self.storage.roll_over()
+                    self.graph = ("strict", g1, g2, g3)
             finally:
                 self._defer_allreduce = False
-            self.graph = (g1, g2)
+                self._bw_stage = "all"
         else:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 self.update_body()
-            self.graph = (g,)
+            self.graph = ("single", g)
         return self.graph
+
+    def _replay(self):
+        kind = self.graph[0]
+        if kind == "single":
+            self.graph[1].replay()
+        elif kind == "strict":
+            _, g1, g2, g3 = self.graph
+            s, e = self.engine.tail_bucket()
+            g1.replay()
+            w_tail = self.dp.allreduce_async(self.flat.grad[s:e])   # overlaps the conv backward
+            g2.replay()
+            w_trunk = self.dp.allreduce_async(self.flat.grad[:s])
+            w_tail.wait()
+            w_trunk.wait()
+            g3.replay()
+        else:   # lag1
+            _, g1, g2 = self.graph
+            g1.replay()                       # overlaps the all-reduce of the previous gradient
+            if self._comm_work is None:       # first update: nothing to apply yet
+                self._grad_move()
+            else:
+                self._comm_work.wait()
+                g2.replay()
+            self._comm_work = self.dp.allreduce_async(self._comm_grad)
 
     def step(self):
         """One update (graph replay when captured)."""
@@ -444,16 +523,19 @@ class ActorCriticTrainer:
             if k is not None:
                 self.kl_coef.fill_(k)
         if self.graph is not None:
-            if len(self.graph) == 2:
-                self.graph[0].replay()
-                self.dp.allreduce_grads(self.flat)
-                self.graph[1].replay()
-            else:
-                self.graph[0].replay()
+            self._replay()
         else:
             self.update_body()
         self.iteration += 1
         self.env_steps += self.cfg.n_steps * self.env.num_envs * self.world
+
+    def flush_pending(self):
+        """lag-1 DP: apply the last all-reduced gradient (end of training / before a checkpoint)."""
+        if self.graph is not None and self.graph[0] == "lag1" and self._comm_work is not None:
+            self._comm_work.wait()
+            self._post_body()
+            self._comm_grad.zero_()
+            self._comm_work = None
 
     def log(self, i, print_tog):
         if self.logger is None:
@@ -490,6 +572,7 @@ class ActorCriticTrainer:
                 self.save_checkpoint()
             if callback is not None:
                 callback(self, it)
+        self.flush_pending()
         return history
 
     # ------------------------------------------------------------------ checkpoints

@@ -88,6 +88,12 @@ class FusedAdam:
         self._ticket = torch.zeros(1, dtype=torch.int32, device=dev)
         # native engine: the update kernel zeroes each gradient after reading it (saves a memset per step)
         self.zero_grad_after = False
+        # data parallelism: the slab holds the SUM over ranks; the kernel folds the 1/world average into its read
+        self.grad_mul = 1.0
+
+    def bind_grad(self, grad_slab):
+        """Read gradients from this group's segment of another slab (lag-1 DP reads the all-reduced copy)."""
+        self.g = grad_slab[self.start:self.end]
 
     def set_lr(self, lr):
         self.lr.fill_(float(lr))
@@ -105,13 +111,16 @@ class FusedAdam:
     def _native_norm(self, ops):
         """Partial sums of squares of the (clipped) gradient; the update kernel reduces them to the global norm
         (and writes it to ``self.gnorm``). Returns the partials or None without a norm clip."""
+        self._norm_mul = 1.0
         if self.max_grad_norm is None:
             return None
         if self.clip_value is not None:
             # the norm is taken after the element-wise clip (torch oracle order)
-            ops.sumsq(torch.clamp(self.g, -self.clip_value, self.clip_value), self._partial)
+            g = self.g * self.grad_mul if self.grad_mul != 1.0 else self.g
+            ops.sumsq(torch.clamp(g, -self.clip_value, self.clip_value), self._partial)
         else:
             ops.sumsq(self.g, self._partial)
+            self._norm_mul = self.grad_mul * self.grad_mul
         return self._partial
 
     def _native_step(self):
@@ -121,10 +130,10 @@ class FusedAdam:
                       float(self.b1), float(self.b2), float(self.eps),
                       float(self.clip_value) if self.clip_value is not None else -1.0,
                       float(self.max_grad_norm) if self.max_grad_norm is not None else -1.0, self._ticket,
-                      bool(self.zero_grad_after))
+                      bool(self.zero_grad_after), float(self.grad_mul), float(self._norm_mul))
 
     def _torch_step(self):
-        g = self.g
+        g = self.g * self.grad_mul if self.grad_mul != 1.0 else self.g
         if self.clip_value is not None:
             g = torch.clamp(g, -self.clip_value, self.clip_value)
         if self.max_grad_norm is not None:
@@ -166,10 +175,10 @@ class FusedRMSprop(FusedAdam):
                          float(self.alpha), float(self.eps),
                          float(self.clip_value) if self.clip_value is not None else -1.0,
                          float(self.max_grad_norm) if self.max_grad_norm is not None else -1.0,
-                         bool(self.zero_grad_after))
+                         bool(self.zero_grad_after), float(self.grad_mul), float(self._norm_mul))
 
     def _torch_step(self):
-        g = self.g
+        g = self.g * self.grad_mul if self.grad_mul != 1.0 else self.g
         if self.clip_value is not None:
             g = torch.clamp(g, -self.clip_value, self.clip_value)
         if self.max_grad_norm is not None:

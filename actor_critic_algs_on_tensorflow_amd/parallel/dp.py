@@ -56,11 +56,26 @@ class DataParallel:
         dist.broadcast(flat.data, src=src, group=self.group)
 
     # -- gradients ----------------------------------------------------------------------------------------------
+    @property
+    def grad_mul(self):
+        """Factor the optimisers fold into their gradient read (1/world when averaging): the all-reduce leaves the
+        SUM in the slab and no separate scaling pass runs."""
+        return 1.0 / self.world_size if self.average else 1.0
+
     @torch.no_grad()
-    def allreduce_grads(self, flat):
+    def allreduce_grads(self, flat, scale=True):
+        """Synchronous all-reduce of the whole gradient slab; ``scale=False`` leaves the sum (optimisers carrying
+        ``grad_mul`` average on read)."""
         dist.all_reduce(flat.grad, op=dist.ReduceOp.SUM, group=self.group)
-        if self.average and self.world_size > 1:
+        if scale and self.average and self.world_size > 1:
             flat.grad.mul_(1.0 / self.world_size)
+
+    @torch.no_grad()
+    def allreduce_async(self, buf):
+        """Issues the SUM all-reduce of ``buf`` (a contiguous slab segment) on the RCCL stream, ordered after the
+        work already queued on the current stream, and returns the work handle. ``handle.wait()`` makes the
+        *current stream* wait for it (no host block), so the caller keeps queueing compute that overlaps it."""
+        return dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
     # -- statistics ---------------------------------------------------------------------------------------------
     @torch.no_grad()

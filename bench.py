@@ -33,6 +33,10 @@ def main():
     ap.add_argument("--envs", type=int, default=32)
     ap.add_argument("--engine", default="auto")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--overlap", default="strict", choices=["strict", "lag1"],
+                    help="DP schedule: strict = exact sync A2C, fc/head gradient bucket all-reduced under the conv "
+                         "backward; lag1 = all-reduce overlapped with the next rollout, gradient applied one update "
+                         "late")
     args = ap.parse_args()
 
     from actor_critic_algs_on_tensorflow_amd import preset
@@ -45,7 +49,8 @@ def main():
     torch.cuda.set_device(local)
     dp = DP.DataParallel() if world > 1 else None
     cfg = preset("pong_a2c", num_envs=args.envs, device=f"cuda:{local}", outdir=None, quiet=True,
-                 stdout_freq=0, save_every=0, engine=args.engine, cuda_graph=not args.no_graph)
+                 stdout_freq=0, save_every=0, engine=args.engine, cuda_graph=not args.no_graph,
+                 overlap=args.overlap)
     tr = ActorCriticTrainer(cfg, dp=dp)
     if cfg.cuda_graph:
         tr.capture(warmup=2)
@@ -87,7 +92,7 @@ def main():
                        "global_batch": steps_per_update, "seq_len": cfg.n_steps, "envs_per_gpu": args.envs,
                        "algo": "A2C (RMSprop 7e-4, n-step returns, grad-norm 0.5)",
                        "parallelism": f"dp{world}", "engine": "native" if tr.engine is not None else "torch",
-                       "hipgraph": bool(tr.graph)},
+                       "hipgraph": bool(tr.graph), "dp_schedule": tr.graph[0] if tr.graph else "eager"},
         }
         print(json.dumps(out), flush=True)
     if dp is not None:

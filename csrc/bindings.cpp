@@ -47,10 +47,11 @@ hipError_t aca_moments(const float*, const float*, float*, int, hipStream_t);
 hipError_t aca_sumsq(const float*, size_t, float*, hipStream_t);
 int aca_sumsq_parts();
 hipError_t aca_adam_step(float*, float*, float*, float*, size_t, const float*, float*, const float*, float*, uint16_t*,
-                         float, float, float, float, float, unsigned int*, int, hipStream_t);
+                         float, float, float, float, float, unsigned int*, int, float, float, hipStream_t);
 hipError_t aca_rmsprop_step(float*, float*, float*, size_t, const float*, const float*, float*, uint16_t*, float, float,
-                            float, float, int, hipStream_t);
+                            float, float, int, float, float, hipStream_t);
 hipError_t aca_cast_bf16(const float*, uint16_t*, size_t, hipStream_t);
+hipError_t aca_grad_move(float*, float*, size_t, hipStream_t);
 hipError_t aca_gemm_run(const AcaGemmDesc*, hipStream_t);
 int aca_gemm_effective_splits(int, int, int);
 int aca_gemm_tile_dims(int, int*, int*);
@@ -396,7 +397,7 @@ uint16_t* shadow_ptr(const c10::optional<Tensor>& shadow, const Tensor& p, const
 
 void adam_step(Tensor p, Tensor g, Tensor m, Tensor v, Tensor lr, Tensor t, c10::optional<Tensor> gnorm_parts,
                c10::optional<Tensor> gnorm_out, c10::optional<Tensor> shadow, double b1, double b2, double eps,
-               double clip, double max_norm, Tensor ticket, bool zero_grad) {
+               double clip, double max_norm, Tensor ticket, bool zero_grad, double gmul, double norm_mul) {
   need(p, at::kFloat, "p");
   need(g, at::kFloat, "g");
   need(m, at::kFloat, "m");
@@ -408,13 +409,13 @@ void adam_step(Tensor p, Tensor g, Tensor m, Tensor v, Tensor lr, Tensor t, c10:
   check(aca_adam_step(ptr<float>(p), ptr<float>(g), ptr<float>(m), ptr<float>(v), p.numel(), ptr<float>(lr),
                       ptr<float>(t), gnorm_parts_ptr(gnorm_parts, max_norm, "adam"), optr<float>(gnorm_out),
                       shadow_ptr(shadow, p, "adam"), (float)b1, (float)b2, (float)eps, (float)clip, (float)max_norm,
-                      ptr<unsigned int>(ticket), zero_grad ? 1 : 0, cur_stream(p)),
+                      ptr<unsigned int>(ticket), zero_grad ? 1 : 0, (float)gmul, (float)norm_mul, cur_stream(p)),
         "adam_step");
 }
 
 void rmsprop_step(Tensor p, Tensor g, Tensor v, Tensor lr, c10::optional<Tensor> gnorm_parts,
                   c10::optional<Tensor> gnorm_out, c10::optional<Tensor> shadow, double alpha, double eps,
-                  double clip, double max_norm, bool zero_grad) {
+                  double clip, double max_norm, bool zero_grad, double gmul, double norm_mul) {
   need(p, at::kFloat, "p");
   need(g, at::kFloat, "g");
   need(v, at::kFloat, "v");
@@ -423,8 +424,15 @@ void rmsprop_step(Tensor p, Tensor g, Tensor v, Tensor lr, c10::optional<Tensor>
   check(aca_rmsprop_step(ptr<float>(p), ptr<float>(g), ptr<float>(v), p.numel(), ptr<float>(lr),
                          gnorm_parts_ptr(gnorm_parts, max_norm, "rmsprop"), optr<float>(gnorm_out),
                          shadow_ptr(shadow, p, "rmsprop"), (float)alpha, (float)eps, (float)clip, (float)max_norm,
-                         zero_grad ? 1 : 0, cur_stream(p)),
+                         zero_grad ? 1 : 0, (float)gmul, (float)norm_mul, cur_stream(p)),
         "rmsprop_step");
+}
+
+void grad_move(Tensor src, Tensor dst) {
+  need(src, at::kFloat, "src");
+  need(dst, at::kFloat, "dst");
+  TORCH_CHECK(src.numel() == dst.numel(), "grad_move: size mismatch");
+  check(aca_grad_move(ptr<float>(src), ptr<float>(dst), src.numel(), cur_stream(src)), "grad_move");
 }
 
 void cast_bf16(Tensor x, Tensor y) {
@@ -767,10 +775,12 @@ TORCH_LIBRARY(acamd, m) {
   m.def("sumsq(Tensor x, Tensor partial) -> ()");
   m.def("adam_step(Tensor p, Tensor g, Tensor m, Tensor v, Tensor lr, Tensor t, Tensor? gnorm_parts, "
         "Tensor? gnorm_out, Tensor? shadow, float b1, float b2, float eps, float clip, float max_norm, Tensor ticket, "
-        "bool zero_grad=False) -> ()");
+        "bool zero_grad=False, float gmul=1.0, float norm_mul=1.0) -> ()");
   m.def("rmsprop_step(Tensor p, Tensor g, Tensor v, Tensor lr, Tensor? gnorm_parts, Tensor? gnorm_out, "
-        "Tensor? shadow, float alpha, float eps, float clip, float max_norm, bool zero_grad=False) -> ()");
+        "Tensor? shadow, float alpha, float eps, float clip, float max_norm, bool zero_grad=False, float gmul=1.0, "
+        "float norm_mul=1.0) -> ()");
   m.def("cast_bf16(Tensor x, Tensor y) -> ()");
+  m.def("grad_move(Tensor src, Tensor dst) -> ()");
   m.def("gemm(Tensor A, int lda, bool a_k, Tensor B, int ldb, bool b_k, Tensor C, int ldc, int out_mode, int M, "
         "int N, int K, float alpha, Tensor? bias, bool relu, Tensor? mask, int ldm, Tensor? colsum, int colsum_mod, "
         "int tile, int bk, int splits, Tensor? ws, Tensor? tickets, int[] ga, float ga_scale, int[] gb, "
@@ -809,6 +819,7 @@ TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
   m.impl("adam_step", &adam_step);
   m.impl("rmsprop_step", &rmsprop_step);
   m.impl("cast_bf16", &cast_bf16);
+  m.impl("grad_move", &grad_move);
   m.impl("gemm", &gemm);
   m.impl("cnn_trunk_fwd", &cnn_trunk_fwd);
   m.impl("fc_value", &fc_value);

@@ -67,20 +67,22 @@ __global__ void __launch_bounds__(OPT_THREADS) opt_kernel(float* __restrict__ p,
                                                           const float* __restrict__ gnorm_parts,
                                                           float* __restrict__ gnorm_out, u16* __restrict__ shadow,
                                                           float b1, float b2, float eps, float clip, float max_norm,
-                                                          unsigned int* __restrict__ ticket, int zero_grad) {
+                                                          unsigned int* __restrict__ ticket, int zero_grad,
+                                                          float gmul, float norm_mul) {
   __shared__ int flag;
   __shared__ float shr[16];
   const float lr = *lr_ptr;
   const float t = ADAM ? (*t_ptr + 1.0f) : 0.f;
   float scale = 1.f;
   if (gnorm_parts) {
-    const float gsq = partial_total(gnorm_parts, shr);
+    const float gsq = partial_total(gnorm_parts, shr) * norm_mul;
     scale = grad_scale(gsq, max_norm);
     if (gnorm_out && blockIdx.x == 0 && threadIdx.x == 0) *gnorm_out = gsq;
   }
   float lr_t = lr;
   if (ADAM) lr_t = lr * sqrtf(1.0f - powf(b2, t)) / (1.0f - powf(b1, t));
   auto upd = [&](float gi, float& vi, float& mi, float& pi) {
+    gi *= gmul;   // data parallelism: 1/world averaging of the summed gradient, folded in (no extra pass)
     if (clip > 0.f) gi = fminf(fmaxf(gi, -clip), clip);
     gi *= scale;
     vi = b2 * vi + (1.0f - b2) * gi * gi;
@@ -132,6 +134,24 @@ __global__ void __launch_bounds__(OPT_THREADS) opt_kernel(float* __restrict__ p,
   }
 }
 
+// lag-1 data parallelism: dst <- src, src <- 0 in one pass (the next backward accumulates into a clean slab while
+// dst is all-reduced and consumed by the next optimiser step)
+__global__ void __launch_bounds__(OPT_THREADS) grad_move_kernel(float* __restrict__ src, float* __restrict__ dst,
+                                                                size_t n) {
+  const size_t n4 = n / 4;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const float4 v = reinterpret_cast<const float4*>(src)[i];
+    reinterpret_cast<float4*>(src)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    reinterpret_cast<float4*>(dst)[i] = v;
+  }
+  if (blockIdx.x == 0)
+    for (size_t i = n4 * 4 + threadIdx.x; i < n; i += blockDim.x) {
+      dst[i] = src[i];
+      src[i] = 0.f;
+    }
+}
+
 __global__ void cast_bf16_kernel(const float* __restrict__ x, u16* __restrict__ y, size_t n) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
     y[i] = f2bf(x[i]);
@@ -162,25 +182,34 @@ extern "C" int aca_sumsq_parts() { return SUMSQ_PARTS; }
 extern "C" hipError_t aca_adam_step(float* p, float* g, float* m, float* v, size_t n, const float* lr,
                                     float* t, const float* gnorm_parts, float* gnorm_out, uint16_t* shadow, float b1, float b2, float eps,
                                     float clip, float max_norm, unsigned int* ticket, int zero_grad,
-                                    hipStream_t stream) {
+                                    float gmul, float norm_mul, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   if ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(m) |
        reinterpret_cast<uintptr_t>(v)) % 16 || reinterpret_cast<uintptr_t>(shadow) % 8)
     return hipErrorInvalidValue;
   opt_kernel<true><<<opt_grid(n), OPT_THREADS, 0, stream>>>(p, g, m, v, n, lr, t, gnorm_parts, gnorm_out, shadow, b1, b2, eps,
-                                                            clip, max_norm, ticket, zero_grad);
+                                                            clip, max_norm, ticket, zero_grad, gmul, norm_mul);
   return hipGetLastError();
 }
 
 extern "C" hipError_t aca_rmsprop_step(float* p, float* g, float* v, size_t n, const float* lr,
                                        const float* gnorm_parts, float* gnorm_out, uint16_t* shadow, float alpha, float eps, float clip,
-                                       float max_norm, int zero_grad, hipStream_t stream) {
+                                       float max_norm, int zero_grad, float gmul, float norm_mul,
+                                       hipStream_t stream) {
   if (n == 0) return hipSuccess;
   if ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(v)) % 16 ||
       reinterpret_cast<uintptr_t>(shadow) % 8)
     return hipErrorInvalidValue;
   opt_kernel<false><<<opt_grid(n), OPT_THREADS, 0, stream>>>(p, g, nullptr, v, n, lr, nullptr, gnorm_parts, gnorm_out, shadow,
-                                                             0.f, alpha, eps, clip, max_norm, nullptr, zero_grad);
+                                                             0.f, alpha, eps, clip, max_norm, nullptr, zero_grad,
+                                                             gmul, norm_mul);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t aca_grad_move(float* src, float* dst, size_t n, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  if ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) % 16) return hipErrorInvalidValue;
+  grad_move_kernel<<<opt_grid(n), OPT_THREADS, 0, stream>>>(src, dst, n);
   return hipGetLastError();
 }
 

@@ -62,8 +62,12 @@ class ActorCriticTrainer:
         if dp is not None:
             dp.broadcast_params(self.flat)
         self.engine = None
+        self.mlp = None
         self.shadow = None
-        if self._want_native():
+        if self._want_native_mlp():
+            from ..ops.mlp import MLPEngine
+            self.mlp = MLPEngine(self.model, self.flat)
+        elif self._want_native():
             from .engine import CNNEngine
             self.shadow = torch.empty(self.flat.numel, dtype=torch.bfloat16, device=self.device)
             self.shadow.copy_(self.flat.data)
@@ -78,7 +82,7 @@ class ActorCriticTrainer:
             else:
                 opt = make_optimizer(cfg.optimizer, self.flat, g, cfg.lr, cfg.clip_value, cfg.max_grad_norm,
                                      bf16_shadow=sh)
-            opt.zero_grad_after = self.engine is not None
+            opt.zero_grad_after = self.engine is not None or self.mlp is not None
             if dp is not None:
                 opt.grad_mul = dp.grad_mul   # the all-reduce leaves the sum; the update kernel averages on read
             self.opts[g] = opt
@@ -123,12 +127,26 @@ class ActorCriticTrainer:
         _native.require()
         return True
 
+    def _want_native_mlp(self):
+        """The fused MLP engine (``ops/mlp.py``) runs the reference's MLP actor/critic on GPU."""
+        from ..models.policy import MLPActorCritic
+        if self.cfg.engine == "torch" or self.device.type != "cuda" or not isinstance(self.model, MLPActorCritic):
+            return False
+        if self.model.actor.ac_dim > 16 or self.env.obs_dtype != torch.float32 or len(self.env.obs_shape) != 1:
+            if self.cfg.engine == "native":
+                raise ValueError("the native MLP engine needs fp32 vector observations and at most 16 actions")
+            return False
+        _native.require()
+        return True
+
     # ------------------------------------------------------------------ rollout
     def _keys(self):
         return self.env.tg * (1 << KEY_ENV_BITS) + self.env.env_ids
 
     @torch.no_grad()
     def collect(self):
+        if self.mlp is not None:
+            return self._collect_mlp()
         if self.engine is not None:
             return self._collect_native()
         st, env, model = self.storage, self.env, self.model
@@ -143,6 +161,17 @@ class ActorCriticTrainer:
             env.step(a, prev_obs=obs_t, obs_out=st.obs[t + 1], reward_out=st.rewards[t], done_out=st.dones[t],
                      trunc_out=st.truncated[t])
         st.values[st.T].copy_(model.value(st.obs[st.T]))
+
+    @torch.no_grad()
+    def _collect_mlp(self):
+        """One launch per step for the policy (both towers + sampling) and one for the env bank."""
+        st, env, eng = self.storage, self.env, self.mlp
+        for t in range(st.T):
+            eng.policy_step(st.obs[t], st.actions[t], st.logp[t], st.entropy[t], st.values[t], env.tg, env.env_ids,
+                            KEY_ENV_BITS, self.policy_seed)
+            env.step(st.actions[t], prev_obs=st.obs[t], obs_out=st.obs[t + 1], reward_out=st.rewards[t],
+                     done_out=st.dones[t], trunc_out=st.truncated[t])
+        eng.value(st.obs[st.T], st.values[st.T])
 
     def _reuse_acts(self):
         """A2C takes one gradient step at the parameters that acted, so the rollout's forward activations ARE the
@@ -254,6 +283,8 @@ class ActorCriticTrainer:
                 yield perm[k * mb:(k + 1) * mb]
 
     def learn(self, ret, adv):
+        if self.mlp is not None:
+            return self._learn_mlp(ret, adv)
         if self.engine is not None:
             return self._learn_native_update(ret, adv)
         cfg, st = self.cfg, self.storage
@@ -297,6 +328,42 @@ class ActorCriticTrainer:
         self._ev(ret, v, "ev_after")
         if self.lr_ctrl is not None:
             self.lr_ctrl.update_(self.actor_opt.lr, kl)
+
+    # ------------------------------------------------------------------ learning (native MLP engine)
+    def _mlp_step(self, eng, B, idx, obs, actions, logp_old, adv, ret, v_old):
+        cfg = self.cfg
+        ppo = cfg.algo == "ppo"
+        used = eng.train(obs, actions, logp_old, adv, ret, self.ent_coef, self.kl_coef, B, idx=idx,
+                         v_old=v_old if ppo else None, vf_coef=1.0, ppo=ppo, ppo_clip=cfg.ppo_clip if ppo else 0.0,
+                         v_clip=(cfg.ppo_value_clip or 0.0) if ppo else 0.0, stats=self.stats_buf,
+                         clips=(cfg.clip_value, cfg.critic_clip_value), want_parts=self.dp is None)
+        for t, g in enumerate(("actor", "critic")):
+            self.opts[g].ext_parts = eng.parts[t] if used else None
+        self._apply_grads()
+
+    @torch.no_grad()
+    def _learn_mlp(self, ret, adv):
+        cfg, st, eng = self.cfg, self.storage, self.mlp
+        obs, actions, logp_old = st.flat("obs"), st.flat("actions"), st.flat("logp")
+        v_old = st.flat("values")
+        self._ev(ret, v_old, "ev_before")
+        if cfg.norm_adv:
+            adv = self._normalize(adv)
+        adv, ret = adv.contiguous(), ret.contiguous()
+        B = obs.shape[0]
+        if cfg.algo == "ppo":
+            mb = B // cfg.ppo_minibatches
+            for sel in self._minibatches(B):
+                self._mlp_step(eng, mb, sel, obs, actions, logp_old, adv, ret, v_old)
+        else:
+            self._mlp_step(eng, B, None, obs, actions, logp_old, adv, ret, v_old)
+        self.update_counter += 1
+        if self.lr_ctrl is not None or cfg.kl_coef > 0:
+            if not hasattr(self, "_eval_buf"):
+                self._eval_buf = (torch.empty(B, device=self.device), torch.empty(B, device=self.device))
+            logp, v = self._eval_buf
+            eng.evaluate(obs, actions, logp, None, v)
+            self._kl_and_lr(logp_old, logp, ret, v)
 
     # ------------------------------------------------------------------ learning (native engine)
     def _learn_native(self, obs, actions, logp_old, adv, ret, v_old, forward=True):

@@ -1,0 +1,164 @@
+"""Native engine for the reference's MLP actor-critic (kernels K01/K02/K05/K07/K08 of SURVEY §2.4, ``mlp.hip``).
+
+The reference builds its actor and critic as separate TF graphs (``Basic_AC/policies.py:33-162``,
+``A3C/policies.py:34-182``) and runs each ``Session.run`` as ~10 TF ops per layer. Here each tower is ONE workgroup
+per 16 rows with its activations in LDS, on f32 MFMA:
+
+* :meth:`MLPEngine.policy_step` -- rollout: both towers in one launch; the actor workgroups also sample the action
+  (Gaussian Box-Muller / categorical Gumbel-max, counter-based keys derived from the env counters, so the actions are
+  bit-identical to :func:`..ops.distributions.gaussian_sample_ref` draws), and write log-prob and entropy; the critic
+  workgroups write V(s).
+* :meth:`MLPEngine.train` -- learner (mini)batch: one fused launch (gathered rows -> forward -> per-row loss gradient
+  -> data-gradient chain) + one weight-gradient launch (every dW/db element written once, deterministic; per-tile
+  sums of squares for the global-norm clip; loss statistics). The optimiser step follows (:mod:`.optim`).
+* :meth:`MLPEngine.evaluate` / :meth:`value` -- log-prob / entropy of given actions and values (post-update KL proxy
+  and EV of the reference, ``Basic_AC/run_AC.py:257-258``; bootstrap values).
+
+Weights are read in place from the fp32 parameter slab (TF ``[in, out]`` kernels, so checkpoints need no
+transposes) and gradients are written straight into the gradient slab.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import _native
+
+MAXL = 5
+TOWER_WORDS = 2 + 9 * MAXL     # int64 words of one MlpTower (csrc/kernels/mlp_desc.h)
+ACT_CODES = {None: 0, "none": 0, "relu": 1, "lrelu": 2, "tanh": 3}
+BM = 16
+MAXW = 256
+PARTS = 256
+
+
+def _rup16(x):
+    return (x + 15) // 16 * 16
+
+
+class MLPEngine:
+    def __init__(self, model, flat):
+        from ..models.policy import MLPActorCritic
+        assert isinstance(model, MLPActorCritic)
+        self.model = model
+        self.flat = flat
+        self.dev = flat.data.device
+        actor, critic = model.actor, model.critic
+        self.discrete = model.discrete
+        self.D = actor.ob_dim
+        self.A = actor.ac_dim
+        self.head = 1 if self.discrete else 2
+        if self.A > 16:
+            raise ValueError("MLP engine heads support at most 16 actions")
+        out_layer = actor.logits if self.discrete else actor.mu_layer
+        self.towers = [
+            [actor.first_layer, actor.second_layer, actor.third_layer, out_layer],
+            [critic.first_layer, critic.second_layer] + ([critic.third_layer] if critic.variant == "a3c" else [])
+            + [critic.value],
+        ]
+        for tw in self.towers:
+            assert len(tw) <= MAXL and tw[0].in_features == self.D
+            for i, lay in enumerate(tw):
+                assert lay.in_features <= MAXW and lay.out_features <= MAXW
+                if i:
+                    assert lay.in_features == tw[i - 1].out_features
+        idx = {id(p): i for i, p in enumerate(flat.params)}
+
+        def views(p):
+            i = idx[id(p)]
+            off, n = flat.offsets[i], p.numel()
+            return flat.data[off:off + n], flat.grad[off:off + n]
+
+        self._views = views
+        if not self.discrete:
+            self.log_std, self.g_log_std = views(actor.log_std)
+            self.ac_scale = actor.ac_scale.to(self.dev, torch.float32).contiguous()
+        else:
+            self.log_std = self.g_log_std = self.ac_scale = None
+        self.mstats = torch.zeros(8, dtype=torch.float32, device=self.dev)
+        self.parts = [torch.zeros(PARTS, dtype=torch.float32, device=self.dev) for _ in range(2)]
+        self.items = [sum(((l.in_features + 15) // 16) * ((l.out_features + 15) // 16) for l in tw)
+                      for tw in self.towers]
+        self._descs = {}
+        self._dummy_stats = torch.zeros(16, dtype=torch.float32, device=self.dev)
+
+    # ------------------------------------------------------------------------------------------- descriptors
+    def desc(self, B=None):
+        """Device descriptor (+ training workspace for batch ``B``; ``None`` = inference only)."""
+        if B in self._descs:
+            return self._descs[B]
+        words = torch.zeros(2 * TOWER_WORDS, dtype=torch.int64)
+        ws = []
+        for t, tw in enumerate(self.towers):
+            base = t * TOWER_WORDS
+            words[base] = len(tw)
+            for l, lay in enumerate(tw):
+                W, gW = self._views(lay.kernel)
+                b, gb = self._views(lay.bias)
+                words[base + 2 + l] = lay.in_features
+                words[base + 2 + MAXL + l] = lay.out_features
+                words[base + 2 + 2 * MAXL + l] = ACT_CODES[lay.activation]
+                for j, tns in enumerate((W, b, gW, gb)):
+                    words[base + 2 + (3 + j) * MAXL + l] = tns.data_ptr()
+                if B is not None:
+                    xs = torch.zeros(B, lay.in_features, dtype=torch.float32, device=self.dev)
+                    dp = torch.zeros(B, lay.out_features, dtype=torch.float32, device=self.dev)
+                    ws += [xs, dp]
+                    words[base + 2 + 7 * MAXL + l] = xs.data_ptr()
+                    words[base + 2 + 8 * MAXL + l] = dp.data_ptr()
+        d = (words.to(self.dev), ws)
+        self._descs[B] = d
+        return d
+
+    def lds_bytes(self, mode, tw_base, ntw):
+        best = 0
+        for t in range(tw_base, tw_base + ntw):
+            n = BM * (_rup16(self.D) + 4)
+            for lay in self.towers[t]:
+                n += BM * (_rup16(lay.out_features) + 4)
+            if mode == 2:
+                n += 2 * BM * (MAXW + 4)
+            best = max(best, n)
+        return best * 4
+
+    def _fwd(self, mode, obs, B, tw_base=0, ntw=2, desc_B=None, idx=None, tg=None, env_ids=None, key_shift=0,
+             seed=0, act_out=None, logp_out=None, ent_out=None, v_out=None, act_in=None, logp_old=None, adv=None,
+             ret=None, v_old=None, ent_coef=None, kl_coef=None, vf_coef=1.0, ppo_clip=0.0, v_clip=0.0, ppo=False):
+        ops = _native.require()
+        desc, _ = self.desc(desc_B)
+        obs2 = obs.reshape(obs.shape[0], -1)
+        ops.mlp_fwd(desc, tw_base, ntw, mode, self.lds_bytes(mode, tw_base, ntw), obs2, idx, B, self.head, self.A,
+                    self.log_std, self.ac_scale, tg, env_ids, key_shift, seed, act_out, logp_out, ent_out, v_out,
+                    act_in, logp_old, adv, ret, v_old, ent_coef, kl_coef, float(vf_coef), float(ppo_clip),
+                    float(v_clip or 0.0), bool(ppo), self.g_log_std if mode == 2 else None,
+                    self.mstats if mode == 2 else None)
+
+    # ------------------------------------------------------------------------------------------- API
+    def policy_step(self, obs, act_out, logp_out, ent_out, v_out, tg, env_ids, key_shift, seed):
+        """Rollout step over the env bank: actions, log-probs, entropies and values in one launch."""
+        self._fwd(0, obs, obs.shape[0], 0, 2, tg=tg, env_ids=env_ids, key_shift=key_shift, seed=seed,
+                  act_out=act_out, logp_out=logp_out, ent_out=ent_out, v_out=v_out)
+
+    def value(self, obs, out):
+        self._fwd(1, obs, obs.shape[0], 1, 1, v_out=out)
+        return out
+
+    def evaluate(self, obs, actions, logp_out, ent_out=None, v_out=None):
+        self._fwd(1, obs, obs.shape[0], 0, 2 if v_out is not None else 1, act_in=actions, logp_out=logp_out,
+                  ent_out=ent_out, v_out=v_out)
+
+    def train(self, obs, actions, logp_old, adv, ret, ent_coef, kl_coef, B, idx=None, v_old=None, vf_coef=1.0,
+              ppo=False, ppo_clip=0.0, v_clip=0.0, stats=None, clips=(None, None), want_parts=True):
+        """One learner (mini)batch: rows ``idx`` (or the first ``B``) of the rollout -> gradients in the slab,
+        statistics into ``stats[0:7]``, sums of squares into :attr:`parts` (when ``want_parts``)."""
+        ops = _native.require()
+        self._fwd(2, obs, B, 0, 2, desc_B=B, idx=idx, act_in=actions, logp_old=logp_old, adv=adv, ret=ret,
+                  v_old=v_old, ent_coef=ent_coef, kl_coef=kl_coef, vf_coef=vf_coef, ppo_clip=ppo_clip,
+                  v_clip=v_clip, ppo=ppo)
+        desc, _ = self.desc(B)
+        nsplit = max(1, min(16, B // 1024))
+        use_parts = want_parts and nsplit == 1
+        st = stats if stats is not None else self._dummy_stats
+        ops.mlp_wgrad(desc, 2, B, nsplit, self.items[0], self.items[1], self.parts[0] if use_parts else None,
+                      self.parts[1] if use_parts else None, float(clips[0] or -1.0), float(clips[1] or -1.0),
+                      self.g_log_std, self.A, self.mstats, st, ent_coef, kl_coef)
+        return use_parts

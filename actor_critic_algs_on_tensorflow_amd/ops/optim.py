@@ -90,6 +90,8 @@ class FusedAdam:
         self.zero_grad_after = False
         # data parallelism: the slab holds the SUM over ranks; the kernel folds the 1/world average into its read
         self.grad_mul = 1.0
+        # sumsq partials already produced by the gradient kernel (MLP engine): the norm needs no extra launch
+        self.ext_parts = None
 
     def bind_grad(self, grad_slab):
         """Read gradients from this group's segment of another slab (lag-1 DP reads the all-reduced copy)."""
@@ -114,6 +116,8 @@ class FusedAdam:
         self._norm_mul = 1.0
         if self.max_grad_norm is None:
             return None
+        if self.ext_parts is not None:
+            return self.ext_parts
         if self.clip_value is not None:
             # the norm is taken after the element-wise clip (torch oracle order)
             g = self.g * self.grad_mul if self.grad_mul != 1.0 else self.g

@@ -28,7 +28,7 @@ ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
 KERNELS = ["env_classic", "env_atari", "heads", "returns", "optim", "gemm", "gemm_plain", "gemm_conv", "conv",
-           "loss", "cnn_fused"]
+           "loss", "cnn_fused", "mlp"]
 # env kernels must round exactly like the PyTorch oracles: no fma contraction
 NO_CONTRACT = {"env_classic", "env_atari"}
 
@@ -68,7 +68,7 @@ def write_ninja(verbose=False):
     w("rule link\n  command = $cxx $in $ldflags -o $out\n  description = LINK $out")
     w("rule tblink\n  command = $cxx -shared $in -o $out\n  description = LINK $out")
     objs = []
-    hdr = " ".join(os.path.join(ROOT, "csrc", "kernels", h) for h in ("common.h", "gemm_impl.h", "gemm_desc.h"))
+    hdr = " ".join(os.path.join(ROOT, "csrc", "kernels", h) for h in ("common.h", "gemm_impl.h", "gemm_desc.h", "mlp_desc.h"))
     for k in KERNELS:
         src = os.path.join(ROOT, "csrc", "kernels", k + ".hip")
         obj = os.path.join(BUILD_DIR, k + ".o")

@@ -14,8 +14,11 @@
 #include <vector>
 
 #include "gemm_desc.h"
+#include "mlp_desc.h"
 
 extern "C" {
+hipError_t aca_mlp_fwd(const aca::MlpArgs*, int, size_t, hipStream_t);
+hipError_t aca_mlp_wgrad(const aca::WgradArgs*, hipStream_t);
 hipError_t aca_env_step_cartpole(float*, int32_t*, int64_t*, float*, float*, const int64_t*, const int32_t*,
                                  const float*, float*, float*, uint8_t*, uint8_t*, uint32_t, int, int, int,
                                  hipStream_t);
@@ -428,6 +431,115 @@ void rmsprop_step(Tensor p, Tensor g, Tensor v, Tensor lr, c10::optional<Tensor>
         "rmsprop_step");
 }
 
+// ---------------------------------------------------------------------------------------------- MLP engine
+// desc: device int64 [2 * sizeof(MlpTower) / 8] built by ops/mlp.py (pointers into the parameter / gradient slabs
+// and the training workspace); lds: dynamic LDS bytes computed there for (desc, mode).
+template <typename T>
+const T* copt(const c10::optional<Tensor>& t, at::ScalarType dt, const char* name) {
+  if (!(t.has_value() && t->defined())) return nullptr;
+  need(*t, dt, name);
+  return ptr<T>(*t);
+}
+
+void mlp_fwd(Tensor desc, int64_t tw_base, int64_t ntw, int64_t mode, int64_t lds, Tensor obs,
+             c10::optional<Tensor> idx, int64_t B, int64_t head, int64_t A, c10::optional<Tensor> log_std,
+             c10::optional<Tensor> ac_scale, c10::optional<Tensor> tg, c10::optional<Tensor> env_ids,
+             int64_t key_shift, int64_t seed, c10::optional<Tensor> act_out, c10::optional<Tensor> logp_out,
+             c10::optional<Tensor> ent_out, c10::optional<Tensor> v_out, c10::optional<Tensor> act_in,
+             c10::optional<Tensor> logp_old, c10::optional<Tensor> adv, c10::optional<Tensor> ret,
+             c10::optional<Tensor> v_old, c10::optional<Tensor> ent_coef, c10::optional<Tensor> kl_coef,
+             double vf_coef, double ppo_clip, double v_clip, bool ppo, c10::optional<Tensor> g_log_std,
+             c10::optional<Tensor> mstats) {
+  need(desc, at::kLong, "desc");
+  TORCH_CHECK(desc.numel() * 8 >= (int64_t)(2 * sizeof(aca::MlpTower)), "mlp_fwd: desc too small");
+  TORCH_CHECK(obs.is_cuda() && obs.scalar_type() == at::kFloat && obs.dim() == 2 && obs.stride(1) == 1,
+              "mlp_fwd: obs must be fp32 [rows, D] with unit column stride");
+  aca::MlpArgs a{};
+  a.tw = reinterpret_cast<const aca::MlpTower*>(desc.data_ptr());
+  a.tw_base = (int)tw_base;
+  a.B = (int)B;
+  a.D = (int)obs.size(1);
+  a.obs = ptr<float>(obs);
+  a.ld_obs = obs.stride(0);
+  a.idx = copt<int64_t>(idx, at::kLong, "idx");
+  if (!a.idx) TORCH_CHECK(obs.size(0) >= B, "mlp_fwd: obs has fewer rows than B");
+  a.mode = (int)mode;
+  a.head = (int)head;
+  a.A = (int)A;
+  a.log_std = copt<float>(log_std, at::kFloat, "log_std");
+  a.ac_scale = copt<float>(ac_scale, at::kFloat, "ac_scale");
+  a.tg = copt<int64_t>(tg, at::kLong, "tg");
+  a.env_ids = copt<int64_t>(env_ids, at::kLong, "env_ids");
+  a.key_shift = (int)key_shift;
+  a.seed = (uint32_t)seed;
+  const bool gauss = head == 2;
+  if (act_out.has_value() && act_out->defined()) {
+    if (gauss) a.act_f_out = const_cast<float*>(copt<float>(act_out, at::kFloat, "act_out"));
+    else a.act_i_out = const_cast<int32_t*>(copt<int32_t>(act_out, at::kInt, "act_out"));
+  }
+  if (act_in.has_value() && act_in->defined()) {
+    if (gauss) a.act_f_in = copt<float>(act_in, at::kFloat, "act_in");
+    else a.act_i_in = copt<int32_t>(act_in, at::kInt, "act_in");
+  }
+  a.logp_out = const_cast<float*>(copt<float>(logp_out, at::kFloat, "logp_out"));
+  a.ent_out = const_cast<float*>(copt<float>(ent_out, at::kFloat, "ent_out"));
+  a.v_out = const_cast<float*>(copt<float>(v_out, at::kFloat, "v_out"));
+  a.logp_old = copt<float>(logp_old, at::kFloat, "logp_old");
+  a.adv = copt<float>(adv, at::kFloat, "adv");
+  a.ret = copt<float>(ret, at::kFloat, "ret");
+  a.v_old = copt<float>(v_old, at::kFloat, "v_old");
+  a.ent_coef = copt<float>(ent_coef, at::kFloat, "ent_coef");
+  a.kl_coef = copt<float>(kl_coef, at::kFloat, "kl_coef");
+  a.vf_coef = (float)vf_coef;
+  a.ppo_clip = (float)ppo_clip;
+  a.v_clip = (float)v_clip;
+  a.ppo = ppo ? 1 : 0;
+  a.g_log_std = const_cast<float*>(copt<float>(g_log_std, at::kFloat, "g_log_std"));
+  a.mstats = const_cast<float*>(copt<float>(mstats, at::kFloat, "mstats"));
+  a.inv_B = B > 0 ? 1.0f / (float)B : 0.f;
+  const bool policy = tw_base == 0;
+  if (policy) {
+    TORCH_CHECK(head == 1 || head == 2, "mlp_fwd: policy tower needs head 1 (categorical) or 2 (gaussian)");
+    if (gauss) TORCH_CHECK(a.log_std && a.ac_scale, "mlp_fwd: gaussian head needs log_std and ac_scale");
+    if (mode == 0) TORCH_CHECK((gauss ? (void*)a.act_f_out : (void*)a.act_i_out) && a.tg && a.env_ids,
+                               "mlp_fwd: rollout needs act_out, tg, env_ids");
+    if (mode == 1) TORCH_CHECK(gauss ? (bool)a.act_f_in : (bool)a.act_i_in, "mlp_fwd: evaluate needs act_in");
+  }
+  if (mode == 2) {
+    TORCH_CHECK(a.mstats && a.ret && a.ent_coef && a.kl_coef, "mlp_fwd: train needs mstats, ret, coefficients");
+    if (policy) TORCH_CHECK(a.logp_old && a.adv && (gauss ? (bool)a.act_f_in : (bool)a.act_i_in) &&
+                                (!gauss || a.g_log_std), "mlp_fwd: train needs actions, logp_old, adv (+ g_log_std)");
+    if (ppo && v_clip > 0) TORCH_CHECK(a.v_old, "mlp_fwd: clipped value loss needs v_old");
+  }
+  check(aca_mlp_fwd(&a, (int)ntw, (size_t)lds, cur_stream(obs)), "mlp_fwd");
+}
+
+void mlp_wgrad(Tensor desc, int64_t ntw, int64_t B, int64_t nsplit, int64_t items0, int64_t items1,
+               c10::optional<Tensor> parts0, c10::optional<Tensor> parts1, double clip0, double clip1,
+               c10::optional<Tensor> g_log_std, int64_t A, c10::optional<Tensor> mstats, c10::optional<Tensor> stats,
+               c10::optional<Tensor> ent_coef, c10::optional<Tensor> kl_coef) {
+  need(desc, at::kLong, "desc");
+  aca::WgradArgs a{};
+  a.tw = reinterpret_cast<const aca::MlpTower*>(desc.data_ptr());
+  a.ntw = (int)ntw;
+  a.B = (int)B;
+  a.nsplit = (int)nsplit;
+  a.items[0] = (int)items0;
+  a.items[1] = (int)items1;
+  a.parts[0] = const_cast<float*>(copt<float>(parts0, at::kFloat, "parts0"));
+  a.parts[1] = const_cast<float*>(copt<float>(parts1, at::kFloat, "parts1"));
+  a.clip[0] = (float)clip0;
+  a.clip[1] = (float)clip1;
+  a.g_log_std = copt<float>(g_log_std, at::kFloat, "g_log_std");
+  a.A = (int)A;
+  a.mstats = const_cast<float*>(copt<float>(mstats, at::kFloat, "mstats"));
+  a.stats = const_cast<float*>(copt<float>(stats, at::kFloat, "stats"));
+  a.ent_coef = copt<float>(ent_coef, at::kFloat, "ent_coef");
+  a.kl_coef = copt<float>(kl_coef, at::kFloat, "kl_coef");
+  if (a.stats) TORCH_CHECK(a.mstats && a.ent_coef && a.kl_coef, "mlp_wgrad: stats need mstats and coefficients");
+  check(aca_mlp_wgrad(&a, cur_stream(desc)), "mlp_wgrad");
+}
+
 void grad_move(Tensor src, Tensor dst) {
   need(src, at::kFloat, "src");
   need(dst, at::kFloat, "dst");
@@ -781,6 +893,14 @@ TORCH_LIBRARY(acamd, m) {
         "float norm_mul=1.0) -> ()");
   m.def("cast_bf16(Tensor x, Tensor y) -> ()");
   m.def("grad_move(Tensor src, Tensor dst) -> ()");
+  m.def("mlp_fwd(Tensor desc, int tw_base, int ntw, int mode, int lds, Tensor obs, Tensor? idx, int B, int head, "
+        "int A, Tensor? log_std, Tensor? ac_scale, Tensor? tg, Tensor? env_ids, int key_shift, int seed, "
+        "Tensor? act_out, Tensor? logp_out, Tensor? ent_out, Tensor? v_out, Tensor? act_in, Tensor? logp_old, "
+        "Tensor? adv, Tensor? ret, Tensor? v_old, Tensor? ent_coef, Tensor? kl_coef, float vf_coef, float ppo_clip, "
+        "float v_clip, bool ppo, Tensor? g_log_std, Tensor? mstats) -> ()");
+  m.def("mlp_wgrad(Tensor desc, int ntw, int B, int nsplit, int items0, int items1, Tensor? parts0, "
+        "Tensor? parts1, float clip0, float clip1, Tensor? g_log_std, int A, Tensor? mstats, Tensor? stats, "
+        "Tensor? ent_coef, Tensor? kl_coef) -> ()");
   m.def("gemm(Tensor A, int lda, bool a_k, Tensor B, int ldb, bool b_k, Tensor C, int ldc, int out_mode, int M, "
         "int N, int K, float alpha, Tensor? bias, bool relu, Tensor? mask, int ldm, Tensor? colsum, int colsum_mod, "
         "int tile, int bk, int splits, Tensor? ws, Tensor? tickets, int[] ga, float ga_scale, int[] gb, "
@@ -820,6 +940,8 @@ TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
   m.impl("rmsprop_step", &rmsprop_step);
   m.impl("cast_bf16", &cast_bf16);
   m.impl("grad_move", &grad_move);
+  m.impl("mlp_fwd", &mlp_fwd);
+  m.impl("mlp_wgrad", &mlp_wgrad);
   m.impl("gemm", &gemm);
   m.impl("cnn_trunk_fwd", &cnn_trunk_fwd);
   m.impl("fc_value", &fc_value);

@@ -1,0 +1,59 @@
+// Descriptors shared by the MLP engine kernels (mlp.hip) and the torch-op bindings (bindings.cpp): plain C types
+// only, so both hipcc and g++ compile this header.
+#pragma once
+#include <stdint.h>
+
+namespace aca {
+
+constexpr int MLP_MAXL = 5;
+
+// Tower descriptor, device-resident (built once per engine and batch size by ops/mlp.py, every field 64-bit so the
+// host packs it as an int64 tensor). Read with uniform (scalar) loads; a by-value kernel argument indexed by a
+// runtime layer number would be spilled to scratch instead.
+struct MlpTower {
+  int64_t nl, pad;
+  int64_t in[MLP_MAXL], out[MLP_MAXL], act[MLP_MAXL];
+  int64_t W[MLP_MAXL];        // const float* [in][out]
+  int64_t b[MLP_MAXL];
+  int64_t gW[MLP_MAXL];
+  int64_t gb[MLP_MAXL];
+  int64_t xs[MLP_MAXL];       // train workspace: layer inputs  [B][in]
+  int64_t dp[MLP_MAXL];       // train workspace: dL/d(pre-activation) [B][out]
+};
+
+struct MlpArgs {
+  const MlpTower* tw;         // [2] device: 0 = actor (policy head), 1 = critic (value)
+  int tw_base;
+  int B, D;
+  const float* obs; int64_t ld_obs;
+  const int64_t* idx;         // optional row gather (PPO minibatch)
+  int mode;                   // 0 rollout, 1 evaluate, 2 train
+  int head;                   // tower 0's head: 1 categorical, 2 gaussian
+  int A;
+  const float* log_std;
+  const float* ac_scale;
+  const int64_t* tg; const int64_t* env_ids; int key_shift; uint32_t seed;
+  int32_t* act_i_out; float* act_f_out; float* logp_out; float* ent_out; float* v_out;
+  const int32_t* act_i_in; const float* act_f_in;
+  const float* logp_old; const float* adv; const float* ret; const float* v_old;
+  const float* ent_coef; const float* kl_coef;
+  float vf_coef, ppo_clip, v_clip;
+  int ppo;
+  float* g_log_std;
+  float* mstats;              // [8] sums (atomics): pg, kl, ent, vloss, clipfrac, -, ratio
+  float inv_B;
+};
+
+struct WgradArgs {
+  const MlpTower* tw;
+  int ntw;
+  int B;
+  int nsplit;                 // > 1: the batch is split over waves, results added atomically (no sumsq)
+  float* parts[2];            // sumsq slots per tower (null: none)
+  float clip[2];              // element-wise clip applied before squaring (<= 0: none)
+  const float* g_log_std; int A;   // included in tower 0's first slot
+  float* mstats; float* stats; const float* ent_coef; const float* kl_coef;
+  int items[2];               // 16x16 tiles per tower (host-computed)
+};
+
+}  // namespace aca

@@ -268,17 +268,46 @@ class ActorCriticTrainer:
         self._run_optimizers()
 
     def _run_optimizers(self):
-        for opt in self.opts.values():
+        """Optimiser step(s). Several groups (the reference's separate actor / critic Adam) run as ONE launch, which
+        also writes the MLP engine's transposed weight shadows; otherwise one launch per group (+ a shadow pass)."""
+        opts = list(self.opts.values())
+        if len(opts) > 1 and _native.use_native(self.flat.data):
+            from ..ops.optim import FusedGroupStep
+            if not hasattr(self, "_group_step"):
+                self._group_step = None
+                if FusedGroupStep.compatible(opts):
+                    tr = None
+                    if self.mlp is not None and list(self.opts) == ["actor", "critic"]:
+                        tr = self.mlp.transposes()
+                    self._group_step = FusedGroupStep(opts, tr)
+            if self._group_step is not None:
+                self._group_step.step()
+                if self.mlp is not None and self._group_step._trans is None:
+                    self.mlp.sync_shadow()
+                return
+        for opt in opts:
             opt.step()
+        if self.mlp is not None:
+            self.mlp.sync_shadow()
+
+    def _epoch_perm(self, B, ep):
+        """Keyed pseudo-random permutation of the batch for PPO epoch ``ep`` (envs/rng.py ``prp``; one native launch
+        on GPU, key derived on the device from the update counter -> graph-capturable)."""
+        if _native.use_native(self.update_counter):
+            if not hasattr(self, "_perm_buf") or self._perm_buf.numel() != B:
+                self._perm_buf = torch.empty(B, dtype=torch.int64, device=self.device)
+            # reused across epochs: the previous epoch's consumers are already queued on the stream
+            _native.require().prp_perm(self._perm_buf, self.policy_seed, self.update_counter.view(1), ep)
+            return self._perm_buf
+        key = E.rng.minibatch_key(self.policy_seed, self.update_counter, ep)
+        return E.rng.prp(torch.arange(B, device=self.device, dtype=torch.int64), B, key)
 
     def _minibatches(self, B):
-        """PPO minibatch index sets: a counter-hash permutation per epoch (device-side, graph-capturable)."""
+        """PPO minibatch index sets: one keyed permutation of the batch per epoch, split into contiguous slices."""
         cfg = self.cfg
         mb = B // cfg.ppo_minibatches
-        idx = torch.arange(B, device=self.device, dtype=torch.int64)
         for ep in range(cfg.ppo_epochs):
-            h = E.rng.hash_u32(self.policy_seed, idx, self.update_counter * 64 + ep, 7)
-            perm = torch.argsort(h)
+            perm = self._epoch_perm(B, ep)
             for k in range(cfg.ppo_minibatches):
                 yield perm[k * mb:(k + 1) * mb]
 
@@ -330,10 +359,10 @@ class ActorCriticTrainer:
             self.lr_ctrl.update_(self.actor_opt.lr, kl)
 
     # ------------------------------------------------------------------ learning (native MLP engine)
-    def _mlp_step(self, eng, B, idx, obs, actions, logp_old, adv, ret, v_old):
+    def _mlp_step(self, eng, B, idx, obs, actions, logp_old, adv, ret, v_old, perm=None):
         cfg = self.cfg
         ppo = cfg.algo == "ppo"
-        used = eng.train(obs, actions, logp_old, adv, ret, self.ent_coef, self.kl_coef, B, idx=idx,
+        used = eng.train(obs, actions, logp_old, adv, ret, self.ent_coef, self.kl_coef, B, idx=idx, perm=perm,
                          v_old=v_old if ppo else None, vf_coef=1.0, ppo=ppo, ppo_clip=cfg.ppo_clip if ppo else 0.0,
                          v_clip=(cfg.ppo_value_clip or 0.0) if ppo else 0.0, stats=self.stats_buf,
                          clips=(cfg.clip_value, cfg.critic_clip_value), want_parts=self.dp is None)
@@ -352,9 +381,13 @@ class ActorCriticTrainer:
         adv, ret = adv.contiguous(), ret.contiguous()
         B = obs.shape[0]
         if cfg.algo == "ppo":
+            # minibatch rows come from the keyed epoch permutation computed inside the fused kernel (no index list)
             mb = B // cfg.ppo_minibatches
-            for sel in self._minibatches(B):
-                self._mlp_step(eng, mb, sel, obs, actions, logp_old, adv, ret, v_old)
+            uc = self.update_counter.view(1)
+            for ep in range(cfg.ppo_epochs):
+                for k in range(cfg.ppo_minibatches):
+                    self._mlp_step(eng, mb, None, obs, actions, logp_old, adv, ret, v_old,
+                                   perm=(uc, ep, k * mb, B, self.policy_seed))
         else:
             self._mlp_step(eng, B, None, obs, actions, logp_old, adv, ret, v_old)
         self.update_counter += 1

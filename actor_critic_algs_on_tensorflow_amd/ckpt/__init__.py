@@ -194,6 +194,8 @@ def load_trainer(trainer, path):
     # the model parameters are views into the flat slab; refresh the bf16 shadow of the native engine
     if trainer.shadow is not None:
         trainer.shadow.copy_(trainer.flat.data)
+    if getattr(trainer, "mlp", None) is not None:   # transposed weight shadows of the MLP engine
+        trainer.mlp.sync_shadow()
     for g, opt in trainer.opts.items():
         sd = {k.rsplit("/", 1)[1]: torch.as_tensor(np.array(v)) for k, v in t.items()
               if k.startswith(f"_acamd/opt/{g}/")}

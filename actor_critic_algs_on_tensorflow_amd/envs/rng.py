@@ -39,6 +39,40 @@ def uniform(seed, env, step, stream):
     return (hash_u32(seed, env, step, stream) >> 8).to(torch.float32) * (1.0 / 16777216.0)
 
 
+_PRP_MULTS = (0x9E3779B1, 0x85EBCA77, 0xC2B2AE3D)
+
+
+def minibatch_key(seed, update_counter, epoch):
+    """Key of the PPO minibatch permutation of ``epoch`` in update ``update_counter`` (a tensor, so the key is
+    derived on the device inside a captured graph). Identical to ``minibatch_key`` in csrc/kernels/common.h."""
+    uc = torch.as_tensor(update_counter, dtype=torch.int64)
+    return hash_u32(seed, (uc * 64 + epoch) & M32, 7, 11)
+
+
+def prp(i, n, key):
+    """Keyed pseudo-random permutation of ``[0, n)`` applied to the int64 tensor ``i`` (values < n): three rounds of
+    xor-key / odd multiply / xorshift, each a bijection of the k-bit domain (k = ceil(log2 n)), with cycle walking
+    back into ``[0, n)``. Bit-identical to ``prp_index`` in csrc/kernels/common.h."""
+    k = 1
+    while k < 32 and (1 << k) < n:
+        k += 1
+    mask = (1 << k) - 1
+    sh = (k + 1) >> 1
+    key = torch.as_tensor(key, dtype=torch.int64)
+    cs = [hash_u32(key, r, 0x5BD1, 3) & mask for r in range(3)]
+
+    def rounds(x):
+        for c, m in zip(cs, _PRP_MULTS):
+            x = ((x ^ c) * m) & mask
+            x = x ^ (x >> sh)
+        return x
+
+    x = rounds(torch.as_tensor(i, dtype=torch.int64))
+    while bool((x >= n).any()):
+        x = torch.where(x >= n, rounds(x), x)
+    return x
+
+
 def hash_u32_py(seed, env, step, stream):
     """Pure-Python reference (used to pin test vectors)."""
     def mix(x):

@@ -24,15 +24,18 @@ import torch
 from .. import _native
 
 MAXL = 5
-TOWER_WORDS = 2 + 9 * MAXL     # int64 words of one MlpTower (csrc/kernels/mlp_desc.h)
+TOWER_WORDS = 2 + 10 * MAXL    # int64 words of one MlpTower (csrc/kernels/mlp_desc.h)
 ACT_CODES = {None: 0, "none": 0, "relu": 1, "lrelu": 2, "tanh": 3}
 BM = 16
 MAXW = 256
 PARTS = 256
 
 
-def _rup16(x):
-    return (x + 15) // 16 * 16
+def _ld(w):
+    """LDS row stride of a width (mlp.hip ld_of: 16 * power-of-two k-groups + 4)."""
+    g = (w + 15) // 16
+    g = 1 if g <= 1 else 2 if g <= 2 else 4 if g <= 4 else 8 if g <= 8 else 16
+    return 16 * g + 4
 
 
 class MLPEngine:
@@ -59,6 +62,8 @@ class MLPEngine:
             assert len(tw) <= MAXL and tw[0].in_features == self.D
             for i, lay in enumerate(tw):
                 assert lay.in_features <= MAXW and lay.out_features <= MAXW
+                # layer widths above 32 must be multiples of 16 (vectorised data-gradient weight loads, mlp.hip)
+                assert lay.out_features <= 32 or lay.out_features % 16 == 0
                 if i:
                     assert lay.in_features == tw[i - 1].out_features
         idx = {id(p): i for i, p in enumerate(flat.params)}
@@ -80,6 +85,25 @@ class MLPEngine:
                       for tw in self.towers]
         self._descs = {}
         self._dummy_stats = torch.zeros(16, dtype=torch.float32, device=self.dev)
+        # transposed weight shadows [out][16 * ngp2(in)] (zero pad) -- the forward's B operand
+        self.wt = {}
+        for tw in self.towers:
+            for lay in tw:
+                kp = _ld(lay.in_features) - 4
+                self.wt[id(lay)] = torch.zeros(lay.out_features, kp, dtype=torch.float32, device=self.dev)
+        self.n_weights = sum(l.in_features * l.out_features for tw in self.towers for l in tw)
+        self.sync_shadow()
+
+    def transposes(self):
+        """Per tower (= optimiser group actor, critic): (W view, K, N, Wt) for the optimiser-written shadows."""
+        return [[(self._views(l.kernel)[0], l.in_features, l.out_features, self.wt[id(l)]) for l in tw]
+                for tw in self.towers]
+
+    def sync_shadow(self):
+        """Rewrites the transposed weight shadows from the fp32 slab (after every optimiser step, and whenever the
+        parameters change outside the optimiser: checkpoint load, broadcast, parameter-server pull)."""
+        desc, _ = self.desc(None)
+        _native.require().mlp_tshadow(desc, 2, self.n_weights)
 
     # ------------------------------------------------------------------------------------------- descriptors
     def desc(self, B=None):
@@ -99,9 +123,13 @@ class MLPEngine:
                 words[base + 2 + 2 * MAXL + l] = ACT_CODES[lay.activation]
                 for j, tns in enumerate((W, b, gW, gb)):
                     words[base + 2 + (3 + j) * MAXL + l] = tns.data_ptr()
+                words[base + 2 + 9 * MAXL + l] = self.wt[id(lay)].data_ptr()
                 if B is not None:
-                    xs = torch.zeros(B, lay.in_features, dtype=torch.float32, device=self.dev)
-                    dp = torch.zeros(B, lay.out_features, dtype=torch.float32, device=self.dev)
+                    # rows padded to a multiple of 128 and never written: the weight-gradient kernel reads whole
+                    # 128-row chunks unguarded
+                    Bp = (B + 127) // 128 * 128
+                    xs = torch.zeros(Bp, lay.in_features, dtype=torch.float32, device=self.dev)
+                    dp = torch.zeros(Bp, lay.out_features, dtype=torch.float32, device=self.dev)
                     ws += [xs, dp]
                     words[base + 2 + 7 * MAXL + l] = xs.data_ptr()
                     words[base + 2 + 8 * MAXL + l] = dp.data_ptr()
@@ -112,21 +140,23 @@ class MLPEngine:
     def lds_bytes(self, mode, tw_base, ntw):
         best = 0
         for t in range(tw_base, tw_base + ntw):
-            n = BM * (_rup16(self.D) + 4)
+            n = BM * _ld(self.D)
             for lay in self.towers[t]:
-                n += BM * (_rup16(lay.out_features) + 4)
+                n += BM * _ld(lay.out_features)
             if mode == 2:
                 n += 2 * BM * (MAXW + 4)
             best = max(best, n)
         return best * 4
 
-    def _fwd(self, mode, obs, B, tw_base=0, ntw=2, desc_B=None, idx=None, tg=None, env_ids=None, key_shift=0,
+    def _fwd(self, mode, obs, B, tw_base=0, ntw=2, desc_B=None, idx=None, perm=None, tg=None, env_ids=None, key_shift=0,
              seed=0, act_out=None, logp_out=None, ent_out=None, v_out=None, act_in=None, logp_old=None, adv=None,
              ret=None, v_old=None, ent_coef=None, kl_coef=None, vf_coef=1.0, ppo_clip=0.0, v_clip=0.0, ppo=False):
         ops = _native.require()
         desc, _ = self.desc(desc_B)
         obs2 = obs.reshape(obs.shape[0], -1)
-        ops.mlp_fwd(desc, tw_base, ntw, mode, self.lds_bytes(mode, tw_base, ntw), obs2, idx, B, self.head, self.A,
+        puc, pep, poff, pn, pseed = perm if perm is not None else (None, 0, 0, 0, 0)
+        ops.mlp_fwd(desc, tw_base, ntw, mode, self.lds_bytes(mode, tw_base, ntw), obs2, idx, puc, pep, poff, pn,
+                    pseed, B, self.head, self.A,
                     self.log_std, self.ac_scale, tg, env_ids, key_shift, seed, act_out, logp_out, ent_out, v_out,
                     act_in, logp_old, adv, ret, v_old, ent_coef, kl_coef, float(vf_coef), float(ppo_clip),
                     float(v_clip or 0.0), bool(ppo), self.g_log_std if mode == 2 else None,
@@ -147,15 +177,17 @@ class MLPEngine:
                   ent_out=ent_out, v_out=v_out)
 
     def train(self, obs, actions, logp_old, adv, ret, ent_coef, kl_coef, B, idx=None, v_old=None, vf_coef=1.0,
-              ppo=False, ppo_clip=0.0, v_clip=0.0, stats=None, clips=(None, None), want_parts=True):
-        """One learner (mini)batch: rows ``idx`` (or the first ``B``) of the rollout -> gradients in the slab,
-        statistics into ``stats[0:7]``, sums of squares into :attr:`parts` (when ``want_parts``)."""
+              ppo=False, ppo_clip=0.0, v_clip=0.0, stats=None, clips=(None, None), want_parts=True, perm=None):
+        """One learner (mini)batch: rows ``idx`` / ``perm`` = (update_counter, epoch, offset, n, seed) -- the rows
+        ``prp(offset + r)`` of the keyed permutation of ``[0, n)`` (envs/rng.py), computed in-kernel -- or the first
+        ``B`` rows of the rollout -> gradients in the slab, statistics into ``stats[0:7]``, sums of squares into
+        :attr:`parts` (when ``want_parts``)."""
         ops = _native.require()
-        self._fwd(2, obs, B, 0, 2, desc_B=B, idx=idx, act_in=actions, logp_old=logp_old, adv=adv, ret=ret,
+        self._fwd(2, obs, B, 0, 2, desc_B=B, idx=idx, perm=perm, act_in=actions, logp_old=logp_old, adv=adv, ret=ret,
                   v_old=v_old, ent_coef=ent_coef, kl_coef=kl_coef, vf_coef=vf_coef, ppo_clip=ppo_clip,
                   v_clip=v_clip, ppo=ppo)
         desc, _ = self.desc(B)
-        nsplit = max(1, min(16, B // 1024))
+        nsplit = max(1, min(16, B // 2048))
         use_parts = want_parts and nsplit == 1
         st = stats if stats is not None else self._dummy_stats
         ops.mlp_wgrad(desc, 2, B, nsplit, self.items[0], self.items[1], self.parts[0] if use_parts else None,

@@ -195,6 +195,70 @@ class FusedRMSprop(FusedAdam):
             self.shadow.copy_(self.p)
 
 
+class FusedGroupStep:
+    """Steps several optimisers of the same kind and hyper-parameters (e.g. the reference's separate actor and critic
+    Adam, ``Basic_AC/policies.py:79-82,142-143``) with ONE native launch (``opt_multi_kernel``): each group keeps its
+    own lr / step / clip / norm; any sum-of-squares launches they need run first."""
+
+    MAXT = 6
+
+    def __init__(self, opts, transposes=None):
+        """``transposes``: optional per-optimiser lists of (W view, K, N, Wt tensor) -- transposed fp32 shadows the
+        update writes as it goes (the MLP engine's forward operand)."""
+        self.opts = list(opts)
+        o0 = self.opts[0]
+        self.adam = not isinstance(o0, FusedRMSprop)
+        self._key = None
+        self._words = self._fvals = None
+        self._trans = None
+        if transposes is not None:
+            t = torch.zeros(len(self.opts), self.MAXT, 5, dtype=torch.int64)
+            for k, (o, lst) in enumerate(zip(self.opts, transposes)):
+                assert len(lst) <= self.MAXT
+                for e, (W, K, N, Wt) in enumerate(lst):
+                    off = (W.data_ptr() - o.p.data_ptr()) // 4
+                    assert 0 <= off and off + K * N <= o.p.numel()
+                    t[k, e] = torch.tensor([off, K, N, Wt.shape[1], Wt.data_ptr()])
+            self._trans = t
+
+    @staticmethod
+    def compatible(opts):
+        if len(opts) < 2 or len(opts) > 4:
+            return False
+        kinds = {type(o) for o in opts}
+        if len(kinds) != 1:
+            return False
+        o0 = opts[0]
+        return all((o.b1, o.b2, o.eps) == (o0.b1, o0.b2, o0.eps) for o in opts)
+
+    @torch.no_grad()
+    def step(self):
+        ops = _native.require()
+        parts = [o._native_norm(ops) for o in self.opts]
+        key = tuple((p.data_ptr() if p is not None else 0, o._norm_mul, o.grad_mul, o.g.data_ptr())
+                    for p, o in zip(parts, self.opts))
+        if key != self._key:
+            words, fvals = [], []
+            for p, o in zip(parts, self.opts):
+                shadow = o.shadow.data_ptr() if o.shadow is not None else 0
+                adam = self.adam
+                words.append([o.p.data_ptr(), o.g.data_ptr(), o.m.data_ptr() if adam else 0, o.v.data_ptr(),
+                              o.p.numel(), o.lr.data_ptr(), o.t.data_ptr() if adam else 0,
+                              p.data_ptr() if p is not None else 0, o.gnorm.data_ptr(), shadow,
+                              o._ticket.data_ptr() if adam else 0])
+                fvals.append([float(o.clip_value) if o.clip_value is not None else -1.0,
+                              float(o.max_grad_norm) if o.max_grad_norm is not None else -1.0,
+                              float(o.grad_mul), float(o._norm_mul)])
+            self._words = torch.tensor(words, dtype=torch.int64)
+            self._fvals = torch.tensor(fvals, dtype=torch.float32)
+            self._key = key
+        o0 = self.opts[0]
+        zero = all(o.zero_grad_after for o in self.opts)
+        assert zero or not any(o.zero_grad_after for o in self.opts)
+        ops.opt_multi(self._words, self._fvals, self._trans, self.adam, float(o0.b1), float(o0.b2), float(o0.eps),
+                      zero, o0.p)
+
+
 def make_optimizer(name, flat, group, lr, clip_value=None, max_grad_norm=None, bf16_shadow=None):
     if name == "adam":
         return FusedAdam(flat, group, lr, clip_value=clip_value, max_grad_norm=max_grad_norm,

@@ -17,6 +17,10 @@
 #include "mlp_desc.h"
 
 extern "C" {
+hipError_t aca_mlp_tshadow(const aca::MlpTower*, int, int, hipStream_t);
+hipError_t aca_opt_multi(const int64_t*, const float*, const int64_t*, int, int, float, float, float, int,
+                         hipStream_t);
+hipError_t aca_prp_perm(int64_t*, int, uint32_t, const int64_t*, int, hipStream_t);
 hipError_t aca_mlp_fwd(const aca::MlpArgs*, int, size_t, hipStream_t);
 hipError_t aca_mlp_wgrad(const aca::WgradArgs*, hipStream_t);
 hipError_t aca_env_step_cartpole(float*, int32_t*, int64_t*, float*, float*, const int64_t*, const int32_t*,
@@ -441,8 +445,17 @@ const T* copt(const c10::optional<Tensor>& t, at::ScalarType dt, const char* nam
   return ptr<T>(*t);
 }
 
+void prp_perm(Tensor out, int64_t seed, Tensor uc, int64_t epoch) {
+  need(out, at::kLong, "out");
+  need(uc, at::kLong, "uc");
+  check(aca_prp_perm(ptr<int64_t>(out), (int)out.numel(), (uint32_t)seed, ptr<int64_t>(uc), (int)epoch,
+                     cur_stream(out)),
+        "prp_perm");
+}
+
 void mlp_fwd(Tensor desc, int64_t tw_base, int64_t ntw, int64_t mode, int64_t lds, Tensor obs,
-             c10::optional<Tensor> idx, int64_t B, int64_t head, int64_t A, c10::optional<Tensor> log_std,
+             c10::optional<Tensor> idx, c10::optional<Tensor> perm_uc, int64_t perm_ep, int64_t perm_off,
+             int64_t perm_n, int64_t perm_seed, int64_t B, int64_t head, int64_t A, c10::optional<Tensor> log_std,
              c10::optional<Tensor> ac_scale, c10::optional<Tensor> tg, c10::optional<Tensor> env_ids,
              int64_t key_shift, int64_t seed, c10::optional<Tensor> act_out, c10::optional<Tensor> logp_out,
              c10::optional<Tensor> ent_out, c10::optional<Tensor> v_out, c10::optional<Tensor> act_in,
@@ -462,7 +475,14 @@ void mlp_fwd(Tensor desc, int64_t tw_base, int64_t ntw, int64_t mode, int64_t ld
   a.obs = ptr<float>(obs);
   a.ld_obs = obs.stride(0);
   a.idx = copt<int64_t>(idx, at::kLong, "idx");
-  if (!a.idx) TORCH_CHECK(obs.size(0) >= B, "mlp_fwd: obs has fewer rows than B");
+  a.perm_uc = copt<int64_t>(perm_uc, at::kLong, "perm_uc");
+  a.perm_ep = (int)perm_ep;
+  a.perm_off = (int)perm_off;
+  a.perm_n = (int)perm_n;
+  a.perm_seed = (uint32_t)perm_seed;
+  if (a.perm_uc) TORCH_CHECK(perm_n > 0 && perm_off + B <= perm_n && obs.size(0) >= perm_n,
+                             "mlp_fwd: minibatch permutation out of range");
+  if (!a.idx && !a.perm_uc) TORCH_CHECK(obs.size(0) >= B, "mlp_fwd: obs has fewer rows than B");
   a.mode = (int)mode;
   a.head = (int)head;
   a.A = (int)A;
@@ -514,6 +534,13 @@ void mlp_fwd(Tensor desc, int64_t tw_base, int64_t ntw, int64_t mode, int64_t ld
   check(aca_mlp_fwd(&a, (int)ntw, (size_t)lds, cur_stream(obs)), "mlp_fwd");
 }
 
+void mlp_tshadow(Tensor desc, int64_t ntw, int64_t total) {
+  need(desc, at::kLong, "desc");
+  check(aca_mlp_tshadow(reinterpret_cast<const aca::MlpTower*>(desc.data_ptr()), (int)ntw, (int)total,
+                        cur_stream(desc)),
+        "mlp_tshadow");
+}
+
 void mlp_wgrad(Tensor desc, int64_t ntw, int64_t B, int64_t nsplit, int64_t items0, int64_t items1,
                c10::optional<Tensor> parts0, c10::optional<Tensor> parts1, double clip0, double clip1,
                c10::optional<Tensor> g_log_std, int64_t A, c10::optional<Tensor> mstats, c10::optional<Tensor> stats,
@@ -538,6 +565,24 @@ void mlp_wgrad(Tensor desc, int64_t ntw, int64_t B, int64_t nsplit, int64_t item
   a.kl_coef = copt<float>(kl_coef, at::kFloat, "kl_coef");
   if (a.stats) TORCH_CHECK(a.mstats && a.ent_coef && a.kl_coef, "mlp_wgrad: stats need mstats and coefficients");
   check(aca_mlp_wgrad(&a, cur_stream(desc)), "mlp_wgrad");
+}
+
+// words: CPU int64 [nseg, 11], fvals: CPU float [nseg, 4] (built once by ops/optim.py FusedGroupStep)
+void opt_multi(Tensor words, Tensor fvals, c10::optional<Tensor> trans, bool adam, double b1, double b2, double eps,
+               bool zero_grad, Tensor stream_ref) {
+  TORCH_CHECK(!words.is_cuda() && words.scalar_type() == at::kLong && words.is_contiguous() && words.dim() == 2 &&
+                  words.size(1) == 11, "opt_multi: words must be CPU int64 [nseg, 11]");
+  TORCH_CHECK(!fvals.is_cuda() && fvals.scalar_type() == at::kFloat && fvals.is_contiguous() &&
+                  fvals.numel() == words.size(0) * 4, "opt_multi: fvals must be CPU float [nseg, 4]");
+  const int64_t* tp = nullptr;
+  if (trans.has_value() && trans->defined()) {
+    TORCH_CHECK(!trans->is_cuda() && trans->scalar_type() == at::kLong && trans->is_contiguous() &&
+                    trans->numel() == words.size(0) * 6 * 5, "opt_multi: trans must be CPU int64 [nseg, 6, 5]");
+    tp = ptr<int64_t>(*trans);
+  }
+  check(aca_opt_multi(ptr<int64_t>(words), ptr<float>(fvals), tp, (int)words.size(0), adam ? 1 : 0, (float)b1,
+                      (float)b2, (float)eps, zero_grad ? 1 : 0, cur_stream(stream_ref)),
+        "opt_multi");
 }
 
 void grad_move(Tensor src, Tensor dst) {
@@ -893,7 +938,12 @@ TORCH_LIBRARY(acamd, m) {
         "float norm_mul=1.0) -> ()");
   m.def("cast_bf16(Tensor x, Tensor y) -> ()");
   m.def("grad_move(Tensor src, Tensor dst) -> ()");
-  m.def("mlp_fwd(Tensor desc, int tw_base, int ntw, int mode, int lds, Tensor obs, Tensor? idx, int B, int head, "
+  m.def("opt_multi(Tensor words, Tensor fvals, Tensor? trans, bool adam, float b1, float b2, float eps, bool zero_grad, "
+        "Tensor stream_ref) -> ()");
+  m.def("prp_perm(Tensor out, int seed, Tensor uc, int epoch) -> ()");
+  m.def("mlp_tshadow(Tensor desc, int ntw, int total) -> ()");
+  m.def("mlp_fwd(Tensor desc, int tw_base, int ntw, int mode, int lds, Tensor obs, Tensor? idx, Tensor? perm_uc, "
+        "int perm_ep, int perm_off, int perm_n, int perm_seed, int B, int head, "
         "int A, Tensor? log_std, Tensor? ac_scale, Tensor? tg, Tensor? env_ids, int key_shift, int seed, "
         "Tensor? act_out, Tensor? logp_out, Tensor? ent_out, Tensor? v_out, Tensor? act_in, Tensor? logp_old, "
         "Tensor? adv, Tensor? ret, Tensor? v_old, Tensor? ent_coef, Tensor? kl_coef, float vf_coef, float ppo_clip, "
@@ -940,7 +990,10 @@ TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
   m.impl("rmsprop_step", &rmsprop_step);
   m.impl("cast_bf16", &cast_bf16);
   m.impl("grad_move", &grad_move);
+  m.impl("opt_multi", &opt_multi);
   m.impl("mlp_fwd", &mlp_fwd);
+  m.impl("prp_perm", &prp_perm);
+  m.impl("mlp_tshadow", &mlp_tshadow);
   m.impl("mlp_wgrad", &mlp_wgrad);
   m.impl("gemm", &gemm);
   m.impl("cnn_trunk_fwd", &cnn_trunk_fwd);

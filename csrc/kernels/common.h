@@ -48,6 +48,33 @@ __device__ __forceinline__ float uniform_open(uint32_t seed, int64_t key, uint32
   return ((float)(h >> 8) + 0.5f) * (1.0f / 16777216.0f);
 }
 
+// Keyed pseudo-random permutation of [0, n) (PPO minibatch shuffles; identical to envs/rng.py prp): three rounds
+// of xor-key / odd multiply / xorshift -- each a bijection of the k-bit domain, k = ceil(log2 n) -- with cycle
+// walking back into [0, n) (expected < 2 rounds since 2^k < 2n; exactly one when n is a power of two).
+__host__ __device__ __forceinline__ uint32_t prp_index(uint32_t i, uint32_t n, uint32_t key) {
+  uint32_t k = 1;
+  while (k < 32 && (1u << k) < n) ++k;
+  const uint32_t mask = k >= 32 ? 0xFFFFFFFFu : ((1u << k) - 1u);
+  const uint32_t sh = (k + 1) >> 1;
+  const uint32_t c0 = hash_u32(key, 0, 0x5BD1u, 3) & mask, c1 = hash_u32(key, 1, 0x5BD1u, 3) & mask,
+                 c2 = hash_u32(key, 2, 0x5BD1u, 3) & mask;
+  uint32_t x = i;
+  do {
+    x = ((x ^ c0) * 0x9E3779B1u) & mask;
+    x ^= x >> sh;
+    x = ((x ^ c1) * 0x85EBCA77u) & mask;
+    x ^= x >> sh;
+    x = ((x ^ c2) * 0xC2B2AE3Du) & mask;
+    x ^= x >> sh;
+  } while (x >= n);
+  return x;
+}
+
+// key of the minibatch permutation of PPO epoch `ep` in update `uc` (envs/rng.py minibatch_key)
+__host__ __device__ __forceinline__ uint32_t minibatch_key(uint32_t seed, int64_t uc, int ep) {
+  return hash_u32(seed, (uint32_t)((uint64_t)(uc * 64 + ep) & 0xFFFFFFFFull), 7, 11);
+}
+
 // ------------------------------------------------------------------------------------------------------------
 // bf16 helpers (round-to-nearest-even through the compiler's cvt; NaN stays NaN)
 // ------------------------------------------------------------------------------------------------------------

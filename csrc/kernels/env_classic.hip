@@ -166,56 +166,70 @@ __global__ void pendulum_step_kernel(EnvIO io, const float* __restrict__ actions
 // ------------------------------------------------------------------------------------------------ linear (MuJoCo-shape)
 constexpr int LIN_OBS = 17, LIN_ACT = 6;
 
-__global__ void linear_step_kernel(EnvIO io, const float* __restrict__ actions, const float* __restrict__ A,
-                                   const float* __restrict__ B) {
+// 32 lanes per env, lane r < 17 owns state row r: the matrix-vector products, the noise hash and the frame write are
+// spread over the lanes (each row's sum keeps the sequential column order of the oracle); lane 0 owns the scalar
+// episode bookkeeping. The env's previous state / actions are read by every lane of its group (broadcast loads).
+constexpr int LIN_LANES = 32;
+
+__global__ void __launch_bounds__(256) linear_step_kernel(EnvIO io, const float* __restrict__ actions,
+                                                          const float* __restrict__ A, const float* __restrict__ B) {
   __shared__ float sA[LIN_OBS * LIN_OBS], sB[LIN_OBS * LIN_ACT];
   for (int j = threadIdx.x; j < LIN_OBS * LIN_OBS; j += blockDim.x) sA[j] = A[j];
   for (int j = threadIdx.x; j < LIN_OBS * LIN_ACT; j += blockDim.x) sB[j] = B[j];
   __syncthreads();
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = (blockIdx.x * blockDim.x + threadIdx.x) / LIN_LANES;
+  const int r = threadIdx.x % LIN_LANES;
   const bool active = i < io.N;
+  const bool owner = active && r == 0;
   bool done = false;
   float ret = 0.f, len = 0.f;
   if (active) {
     float* s = io.state + (size_t)i * LIN_OBS;
     const int64_t tg = io.tg[i] + 1;
-    io.tg[i] = tg;
     const uint32_t id = (uint32_t)io.env_ids[i], st = (uint32_t)tg;
-    float x[LIN_OBS], a[LIN_ACT], y[LIN_OBS];
-    for (int j = 0; j < LIN_OBS; ++j) x[j] = s[j];
+    float a[LIN_ACT];
     float asq = 0.f;
     for (int j = 0; j < LIN_ACT; ++j) {
       a[j] = fminf(fmaxf(actions[(size_t)i * LIN_ACT + j], -1.0f), 1.0f);
       asq += a[j] * a[j];
     }
-    for (int r = 0; r < LIN_OBS; ++r) {
+    float y = 0.f;
+    if (r < LIN_OBS) {
       float acc = 0.f, acc2 = 0.f;
-      for (int c = 0; c < LIN_OBS; ++c) acc += x[c] * sA[r * LIN_OBS + c];
+      for (int c = 0; c < LIN_OBS; ++c) acc += s[c] * sA[r * LIN_OBS + c];
       for (int c = 0; c < LIN_ACT; ++c) acc2 += a[c] * sB[r * LIN_ACT + c];
-      float nz = uniform01(io.seed, id, st, 300 + r);
-      y[r] = acc + acc2 + (nz - 0.5f) * 0.02f;
+      const float nz = uniform01(io.seed, id, st, 300 + r);
+      y = acc + acc2 + (nz - 0.5f) * 0.02f;
     }
-    float rew = y[8] - 0.1f * asq;
-    int t = io.t[i] + 1;
-    bool trunc = t >= io.max_steps;
+    // reward reads row 8 (lane 8 of the group)
+    const float y8 = __shfl(y, (threadIdx.x & 63 & ~(LIN_LANES - 1)) + 8, 64);
+    const float rew = y8 - 0.1f * asq;
+    const int t = io.t[i] + 1;
+    const bool trunc = t >= io.max_steps;
     done = trunc;
-    float er = io.ep_ret[i] + rew;
+    const float er = io.ep_ret[i] + rew;
     ret = er;
     len = (float)t;
-    io.reward[i] = rew;
-    io.done[i] = done;
-    io.truncated[i] = trunc;
-    if (done) {
-      for (int j = 0; j < LIN_OBS; ++j) y[j] = (uniform01(io.seed, id, st, 100 + j) - 0.5f) * 0.2f;
-      t = 0;
-      er = 0.f;
+    if (done && r < LIN_OBS) y = (uniform01(io.seed, id, st, 100 + r) - 0.5f) * 0.2f;
+    if (r < LIN_OBS) {
+      s[r] = y;
+      // frame stack: shift the k-1 newest frames down, append y (reset: k copies of y)
+      const int k = io.k;
+      const float* pv = io.prev + (size_t)i * k * LIN_OBS;
+      float* o = io.out + (size_t)i * k * LIN_OBS;
+      for (int f = 0; f < k - 1; ++f) o[f * LIN_OBS + r] = done ? y : pv[(f + 1) * LIN_OBS + r];
+      o[(k - 1) * LIN_OBS + r] = y;
     }
-    for (int j = 0; j < LIN_OBS; ++j) s[j] = y[j];
-    io.t[i] = t;
-    io.ep_ret[i] = er;
-    push_frame<LIN_OBS>(io, i, y, done);
+    if (owner) {
+      io.tg[i] = tg;
+      io.reward[i] = rew;
+      io.done[i] = done;
+      io.truncated[i] = trunc;
+      io.t[i] = done ? 0 : t;
+      io.ep_ret[i] = done ? 0.f : er;
+    }
   }
-  add_ep_stats(io.ep_stats, active, done, ret, len);
+  add_ep_stats(io.ep_stats, owner, done, ret, len);
 }
 
 }  // namespace aca
@@ -259,7 +273,7 @@ extern "C" hipError_t aca_env_step_linear(float* state, int32_t* t, int64_t* tg,
                                           uint8_t* trunc, uint32_t seed, int max_steps, int k, int N,
                                           hipStream_t stream) {
   EnvIO io = make_io(state, t, tg, ep_ret, ep_stats, ids, prev, out, reward, done, trunc, seed, max_steps, k, N);
-  const int bs = 128;
-  linear_step_kernel<<<(N + bs - 1) / bs, bs, 0, stream>>>(io, actions, A, B);
+  const int bs = 256;
+  linear_step_kernel<<<(N * LIN_LANES + bs - 1) / bs, bs, 0, stream>>>(io, actions, A, B);
   return hipGetLastError();
 }

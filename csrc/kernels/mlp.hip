@@ -38,117 +38,170 @@ constexpr int MLP_PARTS = 256;      // sumsq partial slots per tower (= optim.hi
 
 enum { ACT_NONE = 0, ACT_RELU = 1, ACT_LRELU = 2, ACT_TANH = 3 };
 
+// Descriptor words -> pointers. The cast goes through the global address space so the compiler emits global_load /
+// global_store: a plain int -> generic pointer cast yields flat_* instructions, which count against lgkmcnt too, so
+// every LDS fragment read would also wait for all outstanding weight loads.
+typedef const __attribute__((address_space(1))) float gcf32;
+typedef __attribute__((address_space(1))) float gf32;
 template <typename T>
-__device__ __forceinline__ T* P_(int64_t v) { return reinterpret_cast<T*>(v); }
+__device__ __forceinline__ __attribute__((address_space(1))) T* P_(int64_t v) {
+  return (__attribute__((address_space(1))) T*)v;
+}
 
 __device__ __forceinline__ int rup16(int x) { return (x + 15) & ~15; }
-__device__ __forceinline__ int ld_of(int w) { return rup16(w) + 4; }   // padded LDS row stride
-
-__device__ __forceinline__ float act_fwd(float v, int act) {
-  switch (act) {
-    case ACT_RELU: return fmaxf(v, 0.f);
-    case ACT_LRELU: return 0.8f * fmaxf(v, 0.f) + 0.2f * v;   // (1-a) relu(x) + a x, a = 0.2 (policies.py:20-21)
-    case ACT_TANH: return tanhf(v);
-    default: return v;
-  }
+// k-groups of a width, rounded up to a power of two: the layer loops are instantiated for NG in {1, 2, 4, 8, 16} so
+// they are straight-line code (a runtime group count means a branch per group, and the waitcnt pass then drains
+// every group's loads before the next one issues)
+__device__ __forceinline__ int ngp2(int w) {
+  const int g = (w + 15) >> 4;
+  return g <= 1 ? 1 : g <= 2 ? 2 : g <= 4 ? 4 : g <= 8 ? 8 : 16;
 }
+__device__ __forceinline__ int ld_of(int w) { return 16 * ngp2(w) + 4; }   // padded LDS row stride
 
-// derivative from the activation OUTPUT y (relu/lrelu keep the sign of x; tanh' = 1 - y^2)
-__device__ __forceinline__ float act_bwd(float y, int act) {
-  switch (act) {
-    case ACT_RELU: return y > 0.f ? 1.f : 0.f;
-    case ACT_LRELU: return y > 0.f ? 1.f : 0.2f;
-    case ACT_TANH: return 1.f - y * y;
-    default: return 1.f;
-  }
+// Hidden-layer activations as one branch-free form y = v > 0 ? v : slope * v (relu: slope 0, lrelu(0.2) of
+// policies.py:20-21: 0.2, identity: 1); the tanh of the Gaussian head is applied by the head code itself (the
+// layer stores the pre-activation z), so the MFMA epilogues carry no per-activation branches.
+__device__ __forceinline__ float act_slope(int act) {
+  return act == ACT_RELU ? 0.f : act == ACT_LRELU ? 0.2f : 1.f;
 }
+__device__ __forceinline__ float act_fwd(float v, float slope) { return v > 0.f ? v : slope * v; }
+// derivative from the activation OUTPUT y (relu / lrelu / identity keep the sign of x)
+__device__ __forceinline__ float act_bwd(float y, float slope) { return y > 0.f ? 1.f : slope; }
 
 __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// Y[16][N] = act(X[16][K] W[K][N] + b) (* scale for the tanh head). X: LDS, zero-padded to rup16(K) columns.
-// Y: LDS, columns [N, rup16(N)) written as 0 (so Y is a valid zero-padded input of the next layer).
-// The tanh head stores tanh (unscaled) in Y so that act_bwd applies; the caller scales.
-__device__ void layer_fwd(const float* __restrict__ X, int ldx, int K, const float* __restrict__ W,
-                          const float* __restrict__ bias, int N, int act, float* __restrict__ Y, int ldy) {
+constexpr int MLP_MAXG = MLP_MAXW / 16;   // k-groups of the widest layer
+
+// Y[16][N] = act(X[16][K] W[K][N] + b). X: LDS, zero-padded to 16*NG columns (NG = ngp2(K)).
+// Y: LDS; every column tile up to ngp2(N) is written, columns >= N as 0 (a valid zero-padded input of the next
+// layer). For the tanh head Y holds z (the head code applies tanh and the scale).
+// B operand from the transposed shadow Wt[N][16*NG] (zero-padded rows, refreshed after every optimiser step by
+// mlp_tshadow_kernel): with the remapped k index a lane's four B values of a k-group are Wt[c][16g+4q .. +3], ONE
+// 16-byte load at a constant offset -- all NG loads of a tile are issued before its first MFMA (one L2 round trip
+// per tile, 4*NG live registers, no per-k address registers).
+template <int NG>
+__device__ void layer_fwd_t(const float* __restrict__ X, int ldx, gcf32* __restrict__ Wt, gcf32* __restrict__ bias,
+                            int N, int act, float* __restrict__ Y, int ldy) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 15, q = lane >> 4;
-  const int ntile = (N + 15) >> 4, ng = rup16(K) >> 4;
+  const int ntile = ngp2(N);
   for (int tile = wave; tile < ntile; tile += MLP_THREADS / 64) {
     const int c = tile * 16 + r;
     const bool cok = c < N;
-    const int cc = cok ? c : 0;
+    const int cc = cok ? c : N - 1;   // discarded column: any in-range row
+    const __attribute__((address_space(1))) floatx4* wrow =
+        (const __attribute__((address_space(1))) floatx4*)(Wt + (size_t)cc * (16 * NG) + 4 * q);
+    floatx4 bv[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) bv[g] = wrow[4 * g];
+    // keep every load above this point (under register pressure the scheduler would sink each load to its MFMA)
+    __builtin_amdgcn_sched_barrier(0);
     floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-    for (int g = 0; g < ng; ++g) {
-      const int k0 = 16 * g + 4 * q;
-      const float4 a4 = *reinterpret_cast<const float4*>(&X[r * ldx + k0]);
-      float bv[4];
+    // opaque zero tied to the tile: keeps the A-fragment reads inside the tile loop (hoisted, all NG of them would
+    // stay live across the loop -- 4*NG more registers for no reuse when a wave owns a single tile)
+    const int z0 = __builtin_amdgcn_readfirstlane(tile) - tile;
+    const float* Xr = X + r * ldx + 4 * q + z0;
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const bool ok = cok && (k0 + s) < K;
-        const float w = W[(size_t)(ok ? k0 + s : 0) * N + cc];
-        bv[s] = ok ? w : 0.f;
-      }
-      acc = mfma4(a4.x, bv[0], acc);
-      acc = mfma4(a4.y, bv[1], acc);
-      acc = mfma4(a4.z, bv[2], acc);
-      acc = mfma4(a4.w, bv[3], acc);
+    for (int g = 0; g < NG; ++g) {
+      const float4 a4 = *reinterpret_cast<const float4*>(&Xr[16 * g]);
+      acc = mfma4(a4.x, bv[g][0], acc);
+      acc = mfma4(a4.y, bv[g][1], acc);
+      acc = mfma4(a4.z, bv[g][2], acc);
+      acc = mfma4(a4.w, bv[g][3], acc);
+      // one A-fragment LDS read per 4 MFMAs (not all reads hoisted: that would double the live registers)
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
     }
-    const float bb = cok ? bias[cc] : 0.f;
+    const float bb = bias[cc];
+    const float slope = act_slope(act);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) Y[(4 * q + i) * ldy + c] = cok ? act_fwd(acc[i] + bb, act) : 0.f;
+    for (int i = 0; i < 4; ++i) Y[(4 * q + i) * ldy + c] = cok ? act_fwd(acc[i] + bb, slope) : 0.f;
+  }
+}
+
+__device__ __forceinline__ void layer_fwd(const float* X, int ldx, int K, gcf32* Wt, gcf32* bias, int N, int act,
+                                          float* Y, int ldy) {
+  switch (ngp2(K)) {
+    case 1: layer_fwd_t<1>(X, ldx, Wt, bias, N, act, Y, ldy); break;
+    case 2: layer_fwd_t<2>(X, ldx, Wt, bias, N, act, Y, ldy); break;
+    case 4: layer_fwd_t<4>(X, ldx, Wt, bias, N, act, Y, ldy); break;
+    case 8: layer_fwd_t<8>(X, ldx, Wt, bias, N, act, Y, ldy); break;
+    default: layer_fwd_t<16>(X, ldx, Wt, bias, N, act, Y, ldy); break;
   }
 }
 
 // dX[16][K] = dP[16][N] W[K][N]^T, then * act'(Yprev) (Yprev: LDS outputs of the previous layer, act_prev) ->
-// dPprev (LDS, zero-padded) and, when gdst != null, the global rows of the previous layer's dP.
-template <bool VEC>
-__device__ void layer_dgrad(const float* __restrict__ dP, int ldp, int N, const float* __restrict__ W, int K,
-                            const float* __restrict__ Yprev, int ldyp, int act_prev, float* __restrict__ dPprev,
-                            int lddp, float* __restrict__ gdst, int rows) {
+// dPprev (LDS; every column tile up to ngp2(K) written, columns >= K as 0) and, when gdst != null, the global rows
+// of the previous layer's dP. dP is zero-padded to 16*NG columns (NG = ngp2(N)).
+// VEC: N % 16 == 0, each k-group's B fragment is one 16-byte load of a weight row; all groups loaded up front.
+template <int NG, bool VEC>
+__device__ void layer_dgrad_t(const float* __restrict__ dP, int ldp, int N, gcf32* __restrict__ W, int K,
+                              const float* __restrict__ Yprev, int ldyp, int act_prev, float* __restrict__ dPprev,
+                              int lddp, gf32* __restrict__ gdst, int rows) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 15, q = lane >> 4;
-  const int ntile = (K + 15) >> 4, ng = rup16(N) >> 4;
+  const int ntile = ngp2(K);
   for (int tile = wave; tile < ntile; tile += MLP_THREADS / 64) {
     const int kc = tile * 16 + r;   // output column = input feature of the layer
     const bool kok = kc < K;
-    const float* wrow = W + (size_t)(kok ? kc : 0) * N;
-    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-    for (int g = 0; g < ng; ++g) {
-      const int n0 = 16 * g + 4 * q;
-      const float4 a4 = *reinterpret_cast<const float4*>(&dP[r * ldp + n0]);
-      float4 b4;
-      if (VEC) {
-        b4 = *reinterpret_cast<const float4*>(wrow + n0);
-        if (!kok) b4 = make_float4(0.f, 0.f, 0.f, 0.f);
-      } else {
-        float t[4];
+    gcf32* wrow = W + (size_t)(kok ? kc : 0) * N;
+    float4 bv[NG];
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const bool ok = kok && (n0 + s) < N;
-          const float w = wrow[ok ? n0 + s : 0];
-          t[s] = ok ? w : 0.f;
-        }
-        b4 = make_float4(t[0], t[1], t[2], t[3]);
+    for (int g = 0; g < NG; ++g) {
+      const int n0 = 16 * g + 4 * q;
+      // (kc >= K rows are discarded, n >= N meets a zero-padded dP column: clamped loads, no selects)
+      if (VEC) {
+        const int nn = N >= 16 * NG ? n0 : min(n0, N - 4);
+        const floatx4 w4 = *(const __attribute__((address_space(1))) floatx4*)(wrow + nn);
+        bv[g] = make_float4(w4[0], w4[1], w4[2], w4[3]);
+      } else {
+        bv[g] = make_float4(wrow[min(n0, N - 1)], wrow[min(n0 + 1, N - 1)], wrow[min(n0 + 2, N - 1)],
+                            wrow[min(n0 + 3, N - 1)]);
       }
-      acc = mfma4(a4.x, b4.x, acc);
-      acc = mfma4(a4.y, b4.y, acc);
-      acc = mfma4(a4.z, b4.z, acc);
-      acc = mfma4(a4.w, b4.w, acc);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    const int z0 = __builtin_amdgcn_readfirstlane(tile) - tile;
+    const float* Pr = dP + r * ldp + 4 * q + z0;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      const float4 a4 = *reinterpret_cast<const float4*>(&Pr[16 * g]);
+      acc = mfma4(a4.x, bv[g].x, acc);
+      acc = mfma4(a4.y, bv[g].y, acc);
+      acc = mfma4(a4.z, bv[g].z, acc);
+      acc = mfma4(a4.w, bv[g].w, acc);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
     }
     // C layout: col = lane&15 = kc, rows 4q + i
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = 4 * q + i;
       float v = 0.f;
-      if (kok) v = acc[i] * act_bwd(Yprev[row * ldyp + kc], act_prev);
+      if (kok) v = acc[i] * act_bwd(Yprev[row * ldyp + kc], act_slope(act_prev));
       dPprev[row * lddp + kc] = v;
       if (gdst && kok && row < rows) gdst[(size_t)row * K + kc] = v;
     }
   }
+}
+
+__device__ __forceinline__ void layer_dgrad(const float* dP, int ldp, int N, gcf32* W, int K, const float* Yprev,
+                                            int ldyp, int act_prev, float* dPprev, int lddp, gf32* gdst, int rows) {
+  const bool vec = (N & 15) == 0;
+#define ACA_DG(NG_)                                                                                      \
+  if (vec) layer_dgrad_t<NG_, true>(dP, ldp, N, W, K, Yprev, ldyp, act_prev, dPprev, lddp, gdst, rows);  \
+  else layer_dgrad_t<NG_, false>(dP, ldp, N, W, K, Yprev, ldyp, act_prev, dPprev, lddp, gdst, rows);
+  // (non-multiple-of-16 widths above 32 are rejected by the host: ops/mlp.py)
+  switch (ngp2(N)) {
+    case 1: ACA_DG(1) break;
+    case 2: ACA_DG(2) break;
+    case 4: layer_dgrad_t<4, true>(dP, ldp, N, W, K, Yprev, ldyp, act_prev, dPprev, lddp, gdst, rows); break;
+    case 8: layer_dgrad_t<8, true>(dP, ldp, N, W, K, Yprev, ldyp, act_prev, dPprev, lddp, gdst, rows); break;
+    default: layer_dgrad_t<16, true>(dP, ldp, N, W, K, Yprev, ldyp, act_prev, dPprev, lddp, gdst, rows); break;
+  }
+#undef ACA_DG
 }
 
 __device__ __forceinline__ int64_t row_key(const MlpArgs& a, int grow) {
@@ -168,25 +221,34 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
   const int rows = min(MLP_BM, a.B - row0);
   // ---- LDS layout: X0 | Y_0 .. Y_{nl-1} | dP ping-pong (train)
   const int ld0 = ld_of(a.D);
+  // (offsets recomputed from the descriptor rather than kept in per-layer pointer arrays: a runtime-indexed array
+  // of LDS pointers lives in scratch and its loads come back as generic (flat) pointers)
   float* X0 = sm;
-  float* Y[MLP_MAXL];
-  int ldy[MLP_MAXL];
-  float* p = X0 + MLP_BM * ld0;
-  for (int l = 0; l < nl; ++l) {
-    ldy[l] = ld_of((int)T.out[l]);
-    Y[l] = p;
-    p += MLP_BM * ldy[l];
+  auto ldyf = [&](int l) { return ld_of((int)T.out[l]); };
+  auto Yp = [&](int l) {
+    int off = MLP_BM * ld0;
+    for (int j = 0; j < l; ++j) off += MLP_BM * ldyf(j);
+    return sm + off;
+  };
+  float* P0 = Yp(nl);
+  float* P1 = P0 + MLP_BM * (MLP_MAXW + 4);
+  // ---- row gather: explicit index list, the keyed minibatch permutation (PPO), or identity
+  __shared__ int64_t s_grow[MLP_BM];
+  if (threadIdx.x < MLP_BM) {
+    const int lrow = min(row0 + (int)threadIdx.x, a.B - 1);
+    int64_t g = lrow;
+    if (a.idx) g = a.idx[lrow];
+    else if (a.perm_uc)
+      g = prp_index((uint32_t)(a.perm_off + lrow), (uint32_t)a.perm_n,
+                    minibatch_key(a.perm_seed, *a.perm_uc, a.perm_ep));
+    s_grow[threadIdx.x] = g;
   }
-  float* P0 = p;
-  float* P1 = p + MLP_BM * (MLP_MAXW + 4);
+  __syncthreads();
   // ---- input tile (gathered rows; padded rows / columns are zero)
   for (int e = threadIdx.x; e < MLP_BM * ld0; e += MLP_THREADS) {
     const int r = e / ld0, c = e - r * ld0;
     float v = 0.f;
-    if (r < rows && c < a.D) {
-      const int64_t gr = a.idx ? a.idx[row0 + r] : (int64_t)(row0 + r);
-      v = a.obs[gr * a.ld_obs + c];
-    }
+    if (r < rows && c < a.D) v = a.obs[s_grow[r] * a.ld_obs + c];
     X0[e] = v;
     if (a.mode == 2 && r < rows && c < a.D) P_<float>(T.xs[0])[(size_t)(row0 + r) * a.D + c] = v;
   }
@@ -195,23 +257,25 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
   const float* X = X0;
   int ldx = ld0;
   for (int l = 0; l < nl; ++l) {
-    layer_fwd(X, ldx, (int)T.in[l], P_<const float>(T.W[l]), P_<const float>(T.b[l]), (int)T.out[l], (int)T.act[l],
-              Y[l], ldy[l]);
+    float* Yl = Yp(l);
+    const int ldl = ldyf(l);
+    layer_fwd(X, ldx, (int)T.in[l], P_<const float>(T.Wt[l]), P_<const float>(T.b[l]), (int)T.out[l], (int)T.act[l],
+              Yl, ldl);
     __syncthreads();
     if (a.mode == 2 && l + 1 < nl) {   // inputs of layer l+1 for its weight gradient
       const int w = (int)T.out[l];
-      float* xs = P_<float>(T.xs[l + 1]);
+      gf32* xs = P_<float>(T.xs[l + 1]);
       for (int e = threadIdx.x; e < rows * w; e += MLP_THREADS) {
         const int r = e / w, c = e - r * w;
-        xs[(size_t)(row0 + r) * w + c] = Y[l][r * ldy[l] + c];
+        xs[(size_t)(row0 + r) * w + c] = Yl[r * ldl + c];
       }
     }
-    X = Y[l];
-    ldx = ldy[l];
+    X = Yl;
+    ldx = ldl;
   }
   const int L = nl - 1;
-  const float* Yo = Y[L];
-  const int ldo = ldy[L];
+  const float* Yo = Yp(L);
+  const int ldo = ldyf(L);
   // ---- heads: one thread per row
   const bool policy = (t == 0);
   float* dPtop = P0;
@@ -225,7 +289,7 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
     const int r = tid;
     const bool live = r < rows;
     const int lrow = row0 + r;   // batch-local row (workspace / minibatch order)
-    const int64_t grow = a.idx ? a.idx[lrow < a.B ? lrow : 0] : (int64_t)lrow;
+    const int64_t grow = s_grow[r];
     float st[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (!policy) {
       const float v = Yo[r * ldo];
@@ -252,7 +316,7 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
       const int64_t key = (a.mode == 0 && live) ? row_key(a, (int)grow) : 0;
       for (int j = 0; j < A; ++j) {
         ls[j] = fminf(fmaxf(a.log_std[j], -2.5f), 2.5f);
-        mu[j] = Yo[r * ldo + j] * a.ac_scale[j];
+        mu[j] = tanhf(Yo[r * ldo + j]) * a.ac_scale[j];
         float aj;
         if (a.mode == 0) {
           const float u1 = uniform_open(a.seed, key, 2 * j), u2 = uniform_open(a.seed, key, 2 * j + 1);
@@ -299,7 +363,7 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
         for (int j = 0; j < A; ++j) {
           const float ivar = expf(-2.f * ls[j]);
           const float d = act[j] - mu[j];
-          const float th = Yo[r * ldo + j];
+          const float th = tanhf(Yo[r * ldo + j]);
           const float dmu = g * d * ivar;
           dPtop[r * ldP + j] = live ? dmu * a.ac_scale[j] * (1.f - th * th) : 0.f;
           const float raw = a.log_std[j];
@@ -385,7 +449,7 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
   // ---- top layer dP: apply the head activation derivative (tanh applied above) and publish
   {
     const int w = (int)T.out[L];
-    float* dp = P_<float>(T.dp[L]);
+    gf32* dp = P_<float>(T.dp[L]);
     for (int e = threadIdx.x; e < rows * w; e += MLP_THREADS) {
       const int r = e / w, c = e - r * w;
       dp[(size_t)(row0 + r) * w + c] = dPtop[r * ldP + c];
@@ -396,12 +460,9 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
   float* nxt = P1;
   for (int l = L; l >= 1; --l) {
     const int N = (int)T.out[l], K = (int)T.in[l];
-    float* gdst = P_<float>(T.dp[l - 1]) + (size_t)row0 * K;
-    const float* W = P_<const float>(T.W[l]);
-    if ((N & 15) == 0)
-      layer_dgrad<true>(cur, ldP, N, W, K, Y[l - 1], ldy[l - 1], (int)T.act[l - 1], nxt, ldP, gdst, rows);
-    else
-      layer_dgrad<false>(cur, ldP, N, W, K, Y[l - 1], ldy[l - 1], (int)T.act[l - 1], nxt, ldP, gdst, rows);
+    gf32* gdst = P_<float>(T.dp[l - 1]) + (size_t)row0 * K;
+    gcf32* W = P_<const float>(T.W[l]);
+    layer_dgrad(cur, ldP, N, W, K, Yp(l - 1), ldyf(l - 1), (int)T.act[l - 1], nxt, ldP, gdst, rows);
     __syncthreads();
     float* tmp = cur;
     cur = nxt;
@@ -416,11 +477,15 @@ __device__ __forceinline__ float clipsq(float v, float c) {
   return v * v;
 }
 
+// One 4-wave workgroup per 16x16 gradient tile: the waves take interleaved 128-row chunks of the batch (all 64
+// operand loads of a chunk in flight before its MFMAs), then the four partial tiles are summed through LDS.
+constexpr int WG_CHUNK = 32;   // loads per operand per lane per chunk (128 rows)
+
 __global__ void __launch_bounds__(256) mlp_wgrad_kernel(WgradArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  const int split = gw % a.nsplit;
-  int item = gw / a.nsplit;
+  __shared__ float red[4][64][5];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int split = blockIdx.x % a.nsplit;
+  int item = blockIdx.x / a.nsplit;
   if (blockIdx.x == 0 && threadIdx.x == 0 && a.stats) {   // publish (and reset) the fused kernel's statistics
     float m[8];
     for (int k = 0; k < 8; ++k) m[k] = a.mstats[k];
@@ -450,34 +515,40 @@ __global__ void __launch_bounds__(256) mlp_wgrad_kernel(WgradArgs a) {
   const int ti = item / tn, tj = item - ti * tn;
   const int i0 = ti * 16, j0 = tj * 16;
   const int r = lane & 15, q = lane >> 4;
-  const float* X = P_<const float>(T.xs[l]);
-  const float* P = P_<const float>(T.dp[l]);
+  gcf32* X = P_<const float>(T.xs[l]);
+  gcf32* P = P_<const float>(T.dp[l]);
   const int ia = i0 + r, jb = j0 + r;
   const bool iok = ia < K, jok = jb < N;
-  // rows of this split
-  const int per = (((a.B + a.nsplit - 1) / a.nsplit) + 15) & ~15;
+  const int iac = iok ? ia : 0, jbc = jok ? jb : 0;
+  // split ranges are whole 128-row chunks; the workspace is zero-padded to a multiple of 128 rows, so a chunk is
+  // always in bounds and its pad rows contribute zero (no selects on loaded values: all 64 loads stay in flight)
+  const int per = (((a.B + a.nsplit - 1) / a.nsplit) + 127) & ~127;
   const int rb = split * per, re = min(a.B, rb + per);
   floatx4 acc = {0.f, 0.f, 0.f, 0.f};
   float bsum = 0.f;
-  const bool do_bias = (ti == 0);
-#pragma unroll 2
-  for (int g0 = rb; g0 < re; g0 += 16) {
-    float av[4], bv[4];
+  for (int c0 = rb + wave * 4 * WG_CHUNK; c0 < re; c0 += 16 * WG_CHUNK) {
+    float av[WG_CHUNK], bv[WG_CHUNK];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int row = g0 + 4 * q + s;
-      const bool rok = row < re;
-      const float xa = X[(size_t)(rok ? row : 0) * K + (iok ? ia : 0)];
-      const float pb = P[(size_t)(rok ? row : 0) * N + (jok ? jb : 0)];
-      av[s] = (rok && iok) ? xa : 0.f;
-      bv[s] = (rok && jok) ? pb : 0.f;
+    for (int u = 0; u < WG_CHUNK; ++u) {
+      const int row = c0 + 16 * (u >> 2) + 4 * q + (u & 3);
+      av[u] = X[(size_t)row * K + iac];
+      bv[u] = P[(size_t)row * N + jbc];
     }
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      acc = mfma4(av[s], bv[s], acc);
-      bsum += bv[s];
+    for (int u = 0; u < WG_CHUNK; ++u) {
+      acc = mfma4(av[u], bv[u], acc);
+      bsum += bv[u];
     }
   }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) red[wave][lane][i] = acc[i];
+  red[wave][lane][4] = bsum;
+  __syncthreads();
+  if (wave) return;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i] = red[0][lane][i] + red[1][lane][i] + red[2][lane][i] + red[3][lane][i];
+  bsum = red[0][lane][4] + red[1][lane][4] + red[2][lane][4] + red[3][lane][4];
   float ss = 0.f;
   const float c = a.clip[t];
   // C: col = lane&15 -> j, rows 4q+i -> i
@@ -485,20 +556,20 @@ __global__ void __launch_bounds__(256) mlp_wgrad_kernel(WgradArgs a) {
   for (int i = 0; i < 4; ++i) {
     const int ii = i0 + 4 * q + i, jj = j0 + r;
     if (ii < K && jj < N) {
-      float* dst = P_<float>(T.gW[l]) + (size_t)ii * N + jj;
-      if (a.nsplit > 1) atomicAdd(dst, acc[i]);
+      gf32* dst = P_<float>(T.gW[l]) + (size_t)ii * N + jj;
+      if (a.nsplit > 1) atomicAdd((float*)dst, acc[i]);
       else {
         *dst = acc[i];
         ss += clipsq(acc[i], c);
       }
     }
   }
-  if (do_bias) {
+  if (ti == 0) {
     // lanes with equal (lane & 15) hold partial column sums over rows = q (mod 4)
     bsum += __shfl_xor(bsum, 16, 64);
     bsum += __shfl_xor(bsum, 32, 64);
     if (q == 0 && jok) {
-      if (a.nsplit > 1) atomicAdd(P_<float>(T.gb[l]) + jb, bsum);
+      if (a.nsplit > 1) atomicAdd((float*)(P_<float>(T.gb[l]) + jb), bsum);
       else {
         P_<float>(T.gb[l])[jb] = bsum;
         ss += clipsq(bsum, c);
@@ -511,6 +582,25 @@ __global__ void __launch_bounds__(256) mlp_wgrad_kernel(WgradArgs a) {
     if (lane == 0) a.parts[t][local_item] = ss;
     if (local_item == 0)   // unused slots are zero: the optimiser sums all MLP_PARTS in a fixed order
       for (int k = a.items[t] + lane; k < MLP_PARTS; k += 64) a.parts[t][k] = 0.f;
+  }
+}
+
+// Wt[c][k] = W[k][c] (rows padded to 16 * ngp2(K), pad stays zero) for every layer of the launched towers: the
+// forward's B operand. One thread per weight element; runs after each optimiser step (and at engine creation).
+__global__ void __launch_bounds__(256) mlp_tshadow_kernel(const MlpTower* __restrict__ tw, int ntw, int total) {
+  int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= total) return;
+  for (int t = 0; t < ntw; ++t) {
+    const MlpTower& T = tw[t];
+    for (int l = 0; l < (int)T.nl; ++l) {
+      const int K = (int)T.in[l], N = (int)T.out[l];
+      if (e < K * N) {
+        const int k = e / N, c = e - k * N;
+        P_<float>(T.Wt[l])[(size_t)c * (16 * ngp2(K)) + k] = P_<const float>(T.W[l])[e];
+        return;
+      }
+      e -= K * N;
+    }
   }
 }
 
@@ -542,8 +632,12 @@ extern "C" hipError_t aca_mlp_wgrad(const WgradArgs* a, hipStream_t stream) {
   for (int t = 0; t < a->ntw; ++t)
     if (a->parts[t] && a->nsplit == 1 && a->items[t] > MLP_PARTS) return hipErrorInvalidValue;
   const int total = a->items[0] + (a->ntw > 1 ? a->items[1] : 0);
-  const int waves = total * a->nsplit;
-  const int wpb = 4;
-  mlp_wgrad_kernel<<<(waves + wpb - 1) / wpb, 64 * wpb, 0, stream>>>(*a);
+  mlp_wgrad_kernel<<<total * a->nsplit, 256, 0, stream>>>(*a);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t aca_mlp_tshadow(const MlpTower* tw, int ntw, int total, hipStream_t stream) {
+  if (total <= 0) return hipSuccess;
+  mlp_tshadow_kernel<<<(total + 255) / 256, 256, 0, stream>>>(tw, ntw, total);
   return hipGetLastError();
 }

@@ -19,6 +19,7 @@ struct MlpTower {
   int64_t gb[MLP_MAXL];
   int64_t xs[MLP_MAXL];       // train workspace: layer inputs  [B][in]
   int64_t dp[MLP_MAXL];       // train workspace: dL/d(pre-activation) [B][out]
+  int64_t Wt[MLP_MAXL];       // transposed weight shadow [out][16 * ngp2(in)] (forward B operand)
 };
 
 struct MlpArgs {
@@ -26,7 +27,10 @@ struct MlpArgs {
   int tw_base;
   int B, D;
   const float* obs; int64_t ld_obs;
-  const int64_t* idx;         // optional row gather (PPO minibatch)
+  const int64_t* idx;         // optional row gather (explicit index list)
+  const int64_t* perm_uc;     // optional row gather: rows prp(perm_off + r) of a keyed permutation of [0, perm_n)
+  int perm_ep, perm_off, perm_n;   // (PPO minibatch: key = minibatch_key(perm_seed, *perm_uc, perm_ep))
+  uint32_t perm_seed;
   int mode;                   // 0 rollout, 1 evaluate, 2 train
   int head;                   // tower 0's head: 1 categorical, 2 gaussian
   int A;

@@ -60,25 +60,56 @@ __device__ __forceinline__ float grad_scale(float gnorm_sq, float max_norm) {
   return fminf(max_norm / (n + 1e-6f), 1.0f);
 }
 
-template <bool ADAM>
-__global__ void __launch_bounds__(OPT_THREADS) opt_kernel(float* __restrict__ p, float* __restrict__ g,
-                                                          float* __restrict__ m, float* __restrict__ v, size_t n,
-                                                          const float* __restrict__ lr_ptr, float* __restrict__ t_ptr,
-                                                          const float* __restrict__ gnorm_parts,
-                                                          float* __restrict__ gnorm_out, u16* __restrict__ shadow,
-                                                          float b1, float b2, float eps, float clip, float max_norm,
-                                                          unsigned int* __restrict__ ticket, int zero_grad,
-                                                          float gmul, float norm_mul) {
-  __shared__ int flag;
-  __shared__ float shr[16];
-  const float lr = *lr_ptr;
-  const float t = ADAM ? (*t_ptr + 1.0f) : 0.f;
-  float scale = 1.f;
-  if (gnorm_parts) {
-    const float gsq = partial_total(gnorm_parts, shr) * norm_mul;
-    scale = grad_scale(gsq, max_norm);
-    if (gnorm_out && blockIdx.x == 0 && threadIdx.x == 0) *gnorm_out = gsq;
+// One optimiser segment (a parameter group of the flat slab) with its own lr / step / clip / norm settings.
+// Optional transposed fp32 shadows of [K][N] weight matrices inside the segment (the MLP engine's forward reads
+// Wt[N][ldt]); written by the update itself, so the shadow never needs a pass of its own.
+constexpr int OPT_MAXT = 6;
+struct OptTrans {
+  int64_t off;   // element offset of W within the segment
+  int K, N, ldt;
+  float* dst;
+};
+
+struct OptSeg {
+  float* p; float* g; float* m; float* v; size_t n;
+  const float* lr; float* t;
+  const float* parts; float* gnorm_out; u16* shadow;
+  float clip, max_norm, gmul, norm_mul;
+  unsigned int* ticket;
+  int nblocks;
+  int ntrans;
+  OptTrans tr[OPT_MAXT];
+};
+
+__device__ __forceinline__ void write_trans(const OptSeg& S, size_t i, float v) {
+  for (int e = 0; e < S.ntrans; ++e) {
+    const OptTrans& T = S.tr[e];
+    const int64_t o = (int64_t)i - T.off;
+    if (o >= 0 && o < (int64_t)T.K * T.N) {
+      const int k = (int)(o / T.N), c = (int)(o - (int64_t)k * T.N);
+      T.dst[(size_t)c * T.ldt + k] = v;
+      return;
+    }
   }
+}
+
+template <bool ADAM>
+__device__ __forceinline__ void opt_body(const OptSeg& S, float b1, float b2, float eps, int zero_grad, int vblk,
+                                         int vgrid, int* flag, float* shr) {
+  float* __restrict__ p = S.p;
+  float* __restrict__ g = S.g;
+  float* __restrict__ m = S.m;
+  float* __restrict__ v = S.v;
+  const size_t n = S.n;
+  const float lr = *S.lr;
+  const float t = ADAM ? (*S.t + 1.0f) : 0.f;
+  float scale = 1.f;
+  if (S.parts) {
+    const float gsq = partial_total(S.parts, shr) * S.norm_mul;
+    scale = grad_scale(gsq, S.max_norm);
+    if (S.gnorm_out && vblk == 0 && threadIdx.x == 0) *S.gnorm_out = gsq;
+  }
+  const float clip = S.clip, gmul = S.gmul;
   float lr_t = lr;
   if (ADAM) lr_t = lr * sqrtf(1.0f - powf(b2, t)) / (1.0f - powf(b1, t));
   auto upd = [&](float gi, float& vi, float& mi, float& pi) {
@@ -93,10 +124,11 @@ __global__ void __launch_bounds__(OPT_THREADS) opt_kernel(float* __restrict__ p,
       pi -= lr * gi / sqrtf(vi + eps);
     }
   };
+  u16* shadow = S.shadow;
   // float4 body: all operand loads of a thread are issued together (one memory round trip per element group)
   const size_t n4 = n / 4;
-  const size_t stride = (size_t)gridDim.x * blockDim.x;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += stride) {
+  const size_t stride = (size_t)vgrid * blockDim.x;
+  for (size_t i = vblk * (size_t)blockDim.x + threadIdx.x; i < n4; i += stride) {
     float4 g4 = reinterpret_cast<const float4*>(g)[i];
     float4 v4 = reinterpret_cast<const float4*>(v)[i];
     float4 p4 = reinterpret_cast<const float4*>(p)[i];
@@ -115,8 +147,14 @@ __global__ void __launch_bounds__(OPT_THREADS) opt_kernel(float* __restrict__ p,
       sv.y = (uint32_t)f2bf(p4.z) | ((uint32_t)f2bf(p4.w) << 16);
       reinterpret_cast<uint2*>(shadow)[i] = sv;
     }
+    if (S.ntrans) {
+      write_trans(S, 4 * i, p4.x);
+      write_trans(S, 4 * i + 1, p4.y);
+      write_trans(S, 4 * i + 2, p4.z);
+      write_trans(S, 4 * i + 3, p4.w);
+    }
   }
-  if (blockIdx.x == 0) {   // scalar tail
+  if (vblk == 0) {   // scalar tail
     for (size_t i = n4 * 4 + threadIdx.x; i < n; i += blockDim.x) {
       float gi = g[i], vi = v[i], pi = p[i], mi = ADAM ? m[i] : 0.f;
       if (zero_grad) g[i] = 0.f;
@@ -125,13 +163,39 @@ __global__ void __launch_bounds__(OPT_THREADS) opt_kernel(float* __restrict__ p,
       if (ADAM) m[i] = mi;
       p[i] = pi;
       if (shadow) shadow[i] = f2bf(pi);
+      if (S.ntrans) write_trans(S, i, pi);
     }
   }
   if (ADAM) {
-    if (last_block_arrival(ticket, gridDim.x, &flag)) {
-      if (threadIdx.x == 0) *t_ptr = t;
+    if (last_block_arrival(S.ticket, vgrid, flag)) {
+      if (threadIdx.x == 0) *S.t = t;
     }
   }
+}
+
+template <bool ADAM>
+__global__ void __launch_bounds__(OPT_THREADS) opt_kernel(OptSeg S, float b1, float b2, float eps, int zero_grad) {
+  __shared__ int flag;
+  __shared__ float shr[16];
+  opt_body<ADAM>(S, b1, b2, eps, zero_grad, blockIdx.x, gridDim.x, &flag, shr);
+}
+
+// Several parameter groups (e.g. the reference's separate actor and critic optimisers) in ONE launch: the grid is
+// the concatenation of the groups' grids.
+constexpr int OPT_MAXSEG = 4;
+struct OptMulti {
+  OptSeg seg[OPT_MAXSEG];
+  int nseg;
+};
+
+template <bool ADAM>
+__global__ void __launch_bounds__(OPT_THREADS) opt_multi_kernel(OptMulti M, float b1, float b2, float eps,
+                                                                int zero_grad) {
+  __shared__ int flag;
+  __shared__ float shr[16];
+  int b = blockIdx.x, k = 0;
+  while (k + 1 < M.nseg && b >= M.seg[k].nblocks) b -= M.seg[k++].nblocks;
+  opt_body<ADAM>(M.seg[k], b1, b2, eps, zero_grad, b, M.seg[k].nblocks, &flag, shr);
 }
 
 // lag-1 data parallelism: dst <- src, src <- 0 in one pass (the next backward accumulates into a clean slab while
@@ -179,16 +243,20 @@ extern "C" hipError_t aca_sumsq(const float* x, size_t n, float* partial, hipStr
 
 extern "C" int aca_sumsq_parts() { return SUMSQ_PARTS; }
 
+static bool opt_aligned(const float* p, const float* g, const float* m, const float* v, const uint16_t* shadow) {
+  return !((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(m) |
+            reinterpret_cast<uintptr_t>(v)) % 16 || reinterpret_cast<uintptr_t>(shadow) % 8);
+}
+
 extern "C" hipError_t aca_adam_step(float* p, float* g, float* m, float* v, size_t n, const float* lr,
                                     float* t, const float* gnorm_parts, float* gnorm_out, uint16_t* shadow, float b1, float b2, float eps,
                                     float clip, float max_norm, unsigned int* ticket, int zero_grad,
                                     float gmul, float norm_mul, hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  if ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(m) |
-       reinterpret_cast<uintptr_t>(v)) % 16 || reinterpret_cast<uintptr_t>(shadow) % 8)
-    return hipErrorInvalidValue;
-  opt_kernel<true><<<opt_grid(n), OPT_THREADS, 0, stream>>>(p, g, m, v, n, lr, t, gnorm_parts, gnorm_out, shadow, b1, b2, eps,
-                                                            clip, max_norm, ticket, zero_grad, gmul, norm_mul);
+  if (!opt_aligned(p, g, m, v, shadow)) return hipErrorInvalidValue;
+  OptSeg S{p, g, m, v, n, lr, t, gnorm_parts, gnorm_out, shadow, clip, max_norm, gmul, norm_mul, ticket, opt_grid(n),
+           0, {}};
+  opt_kernel<true><<<S.nblocks, OPT_THREADS, 0, stream>>>(S, b1, b2, eps, zero_grad);
   return hipGetLastError();
 }
 
@@ -197,12 +265,56 @@ extern "C" hipError_t aca_rmsprop_step(float* p, float* g, float* v, size_t n, c
                                        float max_norm, int zero_grad, float gmul, float norm_mul,
                                        hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  if ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(v)) % 16 ||
-      reinterpret_cast<uintptr_t>(shadow) % 8)
-    return hipErrorInvalidValue;
-  opt_kernel<false><<<opt_grid(n), OPT_THREADS, 0, stream>>>(p, g, nullptr, v, n, lr, nullptr, gnorm_parts, gnorm_out, shadow,
-                                                             0.f, alpha, eps, clip, max_norm, nullptr, zero_grad,
-                                                             gmul, norm_mul);
+  if (!opt_aligned(p, g, v, v, shadow)) return hipErrorInvalidValue;
+  OptSeg S{p, g, nullptr, v, n, lr, nullptr, gnorm_parts, gnorm_out, shadow, clip, max_norm, gmul, norm_mul, nullptr,
+           opt_grid(n), 0, {}};
+  opt_kernel<false><<<S.nblocks, OPT_THREADS, 0, stream>>>(S, 0.f, alpha, eps, zero_grad);
+  return hipGetLastError();
+}
+
+// Multi-group step. segs: nseg records of 16 words (see ops/optim.py FusedGroupStep): p, g, m, v, n, lr, t, parts,
+// gnorm_out, shadow, ticket (pointers / sizes as 64-bit words) and clip, max_norm, gmul, norm_mul (floats).
+extern "C" hipError_t aca_opt_multi(const int64_t* words, const float* fvals, const int64_t* trans, int nseg,
+                                    int adam, float b1, float b2, float eps, int zero_grad, hipStream_t stream) {
+  if (nseg < 1 || nseg > OPT_MAXSEG) return hipErrorInvalidValue;
+  OptMulti M{};
+  M.nseg = nseg;
+  int total = 0;
+  for (int k = 0; k < nseg; ++k) {
+    const int64_t* w = words + 11 * k;
+    const float* f = fvals + 4 * k;
+    OptSeg& S = M.seg[k];
+    S.p = reinterpret_cast<float*>(w[0]);
+    S.g = reinterpret_cast<float*>(w[1]);
+    S.m = reinterpret_cast<float*>(w[2]);
+    S.v = reinterpret_cast<float*>(w[3]);
+    S.n = (size_t)w[4];
+    S.lr = reinterpret_cast<const float*>(w[5]);
+    S.t = reinterpret_cast<float*>(w[6]);
+    S.parts = reinterpret_cast<const float*>(w[7]);
+    S.gnorm_out = reinterpret_cast<float*>(w[8]);
+    S.shadow = reinterpret_cast<u16*>(w[9]);
+    S.ticket = reinterpret_cast<unsigned int*>(w[10]);
+    S.clip = f[0];
+    S.max_norm = f[1];
+    S.gmul = f[2];
+    S.norm_mul = f[3];
+    if (S.n == 0 || !opt_aligned(S.p, S.g, adam ? S.m : S.v, S.v, S.shadow)) return hipErrorInvalidValue;
+    if (adam && (!S.m || !S.t || !S.ticket)) return hipErrorInvalidValue;
+    S.nblocks = opt_grid(S.n);
+    total += S.nblocks;
+    // trans: [nseg][OPT_MAXT][5] = (offset, K, N, ldt, dst); K == 0 ends a segment's list
+    S.ntrans = 0;
+    if (trans)
+      for (int e = 0; e < OPT_MAXT; ++e) {
+        const int64_t* tw = trans + ((int64_t)k * OPT_MAXT + e) * 5;
+        if (tw[1] <= 0) break;
+        S.tr[e] = OptTrans{tw[0], (int)tw[1], (int)tw[2], (int)tw[3], reinterpret_cast<float*>(tw[4])};
+        S.ntrans = e + 1;
+      }
+  }
+  if (adam) opt_multi_kernel<true><<<total, OPT_THREADS, 0, stream>>>(M, b1, b2, eps, zero_grad);
+  else opt_multi_kernel<false><<<total, OPT_THREADS, 0, stream>>>(M, 0.f, b2, eps, zero_grad);
   return hipGetLastError();
 }
 

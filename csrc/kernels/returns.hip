@@ -95,6 +95,13 @@ __global__ void __launch_bounds__(1024) ev_kernel(const float* __restrict__ x, c
   }
 }
 
+// PPO minibatch permutation of one epoch (csrc/kernels/common.h prp_index; oracle envs/rng.py prp)
+__global__ void prp_perm_kernel(int64_t* __restrict__ out, int n, uint32_t seed, const int64_t* __restrict__ uc,
+                                int ep) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = prp_index((uint32_t)i, (uint32_t)n, minibatch_key(seed, *uc, ep));
+}
+
 }  // namespace aca
 
 extern "C" hipError_t aca_ev(const float* x, const float* y, float* out, int n, hipStream_t stream) {
@@ -125,5 +132,12 @@ extern "C" hipError_t aca_normalize(const float* a, float* out, int n, float eps
 
 extern "C" hipError_t aca_moments(const float* x, const float* y, float* out, int n, hipStream_t stream) {
   aca::moments_kernel<<<1, 1024, 0, stream>>>(x, y, out, n);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t aca_prp_perm(int64_t* out, int n, uint32_t seed, const int64_t* uc, int ep,
+                                   hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  aca::prp_perm_kernel<<<(n + 255) / 256, 256, 0, stream>>>(out, n, seed, uc, ep);
   return hipGetLastError();
 }

@@ -170,3 +170,73 @@ def test_mlp_trainer_graph_capture(cuda, preset_name, kw):
     torch.cuda.synchronize()
     assert torch.isfinite(tr.flat.data).all() and (tr.flat.data != p0).any()
     assert torch.isfinite(tr.stats_buf).all()
+
+
+@pytest.mark.parametrize("name", ["adam", "rmsprop"])
+def test_multi_group_optimizer_matches_separate_steps(cuda, name):
+    """Actor + critic groups stepped by ONE opt_multi launch == each group stepped by its own kernel."""
+    from actor_critic_algs_on_tensorflow_amd.ops.optim import FlatParams, FusedGroupStep, make_optimizer
+    torch.manual_seed(0)
+    ps = {"actor": [torch.nn.Parameter(torch.randn(37, 5)), torch.nn.Parameter(torch.randn(7))],
+          "critic": [torch.nn.Parameter(torch.randn(129, 3))]}
+    flats = []
+    for _ in range(2):
+        f = FlatParams({k: [torch.nn.Parameter(p.detach().clone()) for p in v] for k, v in ps.items()}, cuda)
+        f.grad.copy_(torch.randn(f.numel, generator=torch.Generator().manual_seed(1)).to(cuda))
+        flats.append(f)
+    cfgs = {"actor": dict(lr=3e-3, clip_value=0.05, max_grad_norm=0.5), "critic": dict(lr=1e-2, max_grad_norm=0.3)}
+    sep = [make_optimizer(name, flats[0], g, **c) for g, c in cfgs.items()]
+    grp = [make_optimizer(name, flats[1], g, **c) for g, c in cfgs.items()]
+    for o in sep + grp:
+        o.zero_grad_after = True
+    gs = FusedGroupStep(grp)
+    for it in range(3):
+        for o in sep:
+            o.step()
+        gs.step()
+        g = torch.randn(flats[0].numel, generator=torch.Generator().manual_seed(10 + it)).to(cuda)
+        flats[0].grad.copy_(g)
+        flats[1].grad.copy_(g)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(flats[1].data, flats[0].data, rtol=0, atol=0)
+    for a, b in zip(sep, grp):
+        torch.testing.assert_close(b.v, a.v, rtol=0, atol=0)
+
+
+def test_prp_permutation_kernel_matches_oracle(cuda):
+    from actor_critic_algs_on_tensorflow_amd import _native
+    from actor_critic_algs_on_tensorflow_amd.envs import rng
+    for n, uc, ep in ((16384, 3, 2), (1000, 0, 0), (4097, 12, 9), (1, 5, 1)):
+        out = torch.empty(n, dtype=torch.int64, device=cuda)
+        ucd = torch.tensor([uc], dtype=torch.int64, device=cuda)
+        _native.require().prp_perm(out, 777, ucd, ep)
+        ref = rng.prp(torch.arange(n), n, rng.minibatch_key(777, torch.tensor(uc), ep))
+        assert torch.equal(out.cpu(), ref)
+        assert torch.equal(torch.sort(out.cpu()).values, torch.arange(n))
+
+
+def test_optimizer_writes_transposed_shadows(cuda):
+    """The multi-group optimiser keeps the MLP engine's transposed weight shadows equal to W^T after every step,
+    and checkpoint restore refreshes them."""
+    from actor_critic_algs_on_tensorflow_amd import preset
+    from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
+    tr = ActorCriticTrainer(preset("mujoco_ppo_dp8", num_envs=8, n_steps=16, ppo_epochs=1, ppo_minibatches=2,
+                                   device="cuda:0", outdir=None, quiet=True, stdout_freq=0, save_every=0,
+                                   cuda_graph=False))
+    for _ in range(2):
+        tr.step()
+    torch.cuda.synchronize()
+    assert tr._group_step is not None and tr._group_step._trans is not None
+
+    def check():
+        for tw in tr.mlp.towers:
+            for lay in tw:
+                wt = tr.mlp.wt[id(lay)]
+                K = lay.in_features
+                assert torch.equal(wt[:, :K], lay.kernel.detach().t()), lay
+                assert (wt[:, K:] == 0).all()
+    check()
+    with torch.no_grad():
+        tr.flat.data.mul_(0.5)
+    tr.mlp.sync_shadow()
+    check()

@@ -70,6 +70,13 @@ class GemmWorkspace:
     def __init__(self, device, elems=1 << 20, tickets=1 << 14):
         self.ws = torch.zeros(elems, dtype=torch.float32, device=device)
         self.tickets = torch.zeros(tickets, dtype=torch.int32, device=device)
+        self.part = torch.zeros(1 << 16, dtype=torch.float32, device=device)
+
+    def part_buf(self, elems):
+        """Per-row-tile column-sum partials (fully rewritten by every GEMM that uses them)."""
+        if elems > self.part.numel():
+            self.part = torch.zeros(elems, dtype=torch.float32, device=self.part.device)
+        return self.part
 
     def ensure(self, elems, tiles):
         if elems > self.ws.numel():
@@ -85,6 +92,7 @@ class GemmWorkspace:
 # against scratch outputs and the winner is cached for the process. ACAMD_GEMM_TUNE=0 uses :func:`plan`.
 _TUNED: dict = {}
 PARTIAL_MAX_SPLITS = 8   # out_mode 3: the consumer kernels reduce at most this many partial planes
+COLSUM_PART_MIN_TILES = int(os.environ.get("ACAMD_COLSUM_PART_MIN_TILES", "48"))
 TUNE = os.environ.get("ACAMD_GEMM_TUNE", "1") == "1"
 
 
@@ -122,9 +130,18 @@ def _run(ops, A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha, bias, 
         e, t = workspace_elems(M, N, tile, eff)
         workspace.ensure(e, t)
         ws, tk = workspace.ws, workspace.tickets
+    # bias column sums of products with many row tiles: per-tile partials + one reduce launch instead of every
+    # workgroup adding into the same few addresses (thousands of same-address atomics serialise in L2)
+    part, R = None, 0
+    if colsum is not None and eff == 1 and out_mode != 3 and workspace is not None:
+        R = (M + TILES[tile][0] - 1) // TILES[tile][0]
+        if R >= COLSUM_PART_MIN_TILES:
+            part = workspace.part_buf(R * N)
     ops.gemm(A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, float(alpha), bias, bool(relu), mask, ldm,
              colsum, int(colsum_mod), tile, bk, splits, ws, tk, list(ga or []), float(ga_scale), list(gb or []),
-             float(gb_scale), stamps)
+             float(gb_scale), stamps, part)
+    if part is not None:
+        ops.colsum_reduce(part, R, N, colsum, int(colsum_mod))
     return eff
 
 

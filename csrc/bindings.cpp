@@ -17,6 +17,7 @@
 #include "mlp_desc.h"
 
 extern "C" {
+hipError_t aca_colsum_reduce(const float*, int, int, float*, int, hipStream_t);
 hipError_t aca_mlp_tshadow(const aca::MlpTower*, int, int, hipStream_t);
 hipError_t aca_opt_multi(const int64_t*, const float*, const int64_t*, int, int, float, float, float, int,
                          hipStream_t);
@@ -658,7 +659,7 @@ void gemm(Tensor A, int64_t lda, bool a_k, Tensor B, int64_t ldb, bool b_k, Tens
           c10::optional<Tensor> mask, int64_t ldm, c10::optional<Tensor> colsum, int64_t colsum_mod, int64_t tile,
           int64_t bk, int64_t splits, c10::optional<Tensor> ws, c10::optional<Tensor> tickets,
           std::vector<int64_t> ga, double ga_scale, std::vector<int64_t> gb, double gb_scale,
-          c10::optional<Tensor> stamps) {
+          c10::optional<Tensor> stamps, c10::optional<Tensor> colsum_part) {
   TORCH_CHECK(out_mode >= 0 && out_mode <= 3, "gemm: bad out_mode");
   if (out_mode == 3)
     TORCH_CHECK(!(bias.has_value() && bias->defined()) && !relu && !(mask.has_value() && mask->defined()) &&
@@ -753,6 +754,14 @@ void gemm(Tensor A, int64_t lda, bool a_k, Tensor B, int64_t ldb, bool b_k, Tens
     d.stamps = ptr<unsigned long long>(*stamps);
   }
   d.tile = (int)tile; d.bk = (int)bk; d.splits = (int)splits;
+  if (colsum_part.has_value() && colsum_part->defined()) {
+    TORCH_CHECK(d.colsum && eff == 1 && out_mode != 3, "gemm: colsum partials need colsum and no split-K");
+    int bm, bn;
+    aca_gemm_tile_dims((int)tile, &bm, &bn);
+    need(*colsum_part, at::kFloat, "colsum_part");
+    TORCH_CHECK(colsum_part->numel() >= ((M + bm - 1) / bm) * N, "gemm: colsum_part needs [M tiles, N]");
+    d.colsum_part = ptr<float>(*colsum_part);
+  }
   check(aca_gemm_run(&d, cur_stream(C)), "gemm");
 }
 
@@ -826,6 +835,14 @@ void col2im_nhwc(Tensor dcol, Tensor ymask, Tensor dx, c10::optional<Tensor> col
   check(aca_col2im_nhwc(ptr<uint16_t>(dcol), ptr<uint16_t>(ymask), ptr<uint16_t>(dx), optr<float>(colsum), B, C, H, W,
                         kh, kw, s, cur_stream(dcol)),
         "col2im_nhwc");
+}
+
+void colsum_reduce(Tensor part, int64_t R, int64_t N, Tensor out, int64_t mod) {
+  need(part, at::kFloat, "part");
+  need(out, at::kFloat, "out");
+  TORCH_CHECK(part.numel() >= R * N && out.numel() >= (mod > 0 ? mod : N), "colsum_reduce: size mismatch");
+  check(aca_colsum_reduce(ptr<float>(part), (int)R, (int)N, ptr<float>(out), (int)mod, cur_stream(part)),
+        "colsum_reduce");
 }
 
 void colsum_bf16(Tensor x, int64_t M, int64_t N, int64_t ld, Tensor out) {
@@ -954,7 +971,8 @@ TORCH_LIBRARY(acamd, m) {
   m.def("gemm(Tensor A, int lda, bool a_k, Tensor B, int ldb, bool b_k, Tensor C, int ldc, int out_mode, int M, "
         "int N, int K, float alpha, Tensor? bias, bool relu, Tensor? mask, int ldm, Tensor? colsum, int colsum_mod, "
         "int tile, int bk, int splits, Tensor? ws, Tensor? tickets, int[] ga, float ga_scale, int[] gb, "
-        "float gb_scale, Tensor? stamps=None) -> ()");
+        "float gb_scale, Tensor? stamps=None, Tensor? colsum_part=None) -> ()");
+  m.def("colsum_reduce(Tensor part, int R, int N, Tensor out, int mod) -> ()");
   m.def("gemm_effective_splits(int K, int bk, int splits) -> int", &gemm_effective_splits);
   m.def("cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, Tensor y1, "
         "Tensor y2, Tensor y3, float scale, Tensor? shift_out=None, Tensor? stamps=None) -> ()");
@@ -1002,5 +1020,6 @@ TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
   m.impl("im2col_nhwc", &im2col_nhwc);
   m.impl("col2im_nhwc", &col2im_nhwc);
   m.impl("colsum_bf16", &colsum_bf16);
+  m.impl("colsum_reduce", &colsum_reduce);
   m.impl("ac_loss", &ac_loss);
 }

@@ -146,6 +146,29 @@ __global__ void colsum_bf16_kernel(const u16* __restrict__ x, int64_t M, int N, 
   atomicAdd(&out[n], s);
 }
 
+// out[n % mod] += sum_r part[r][n] (the GEMM's per-row-tile column-sum partials): 8 row lanes x 32 columns per
+// workgroup over 512 rows, one atomic per column per workgroup (a few dozen adds per address instead of thousands)
+__global__ void __launch_bounds__(256) colsum_reduce_kernel(const float* __restrict__ part, int R, int N,
+                                                            float* __restrict__ out, int mod) {
+  __shared__ float sh[8][33];
+  const int c = threadIdx.x & 31, rl = threadIdx.x >> 5;
+  const int n = blockIdx.y * 32 + c;
+  const int r1 = min(R, (int)(blockIdx.x + 1) * 512);
+  float s = 0.f;
+  if (n < N) {
+#pragma unroll 8
+    for (int r = blockIdx.x * 512 + rl; r < r1; r += 8) s += part[(int64_t)r * N + n];
+  }
+  sh[rl][c] = s;
+  __syncthreads();
+  if (rl == 0 && n < N) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t += sh[i][c];
+    atomicAdd(&out[mod ? n % mod : n], t);
+  }
+}
+
 static int grid_for(int64_t total, int bs) {
   int64_t g = (total + bs - 1) / bs;
   if (g > 8192) g = 8192;
@@ -194,5 +217,12 @@ extern "C" hipError_t aca_colsum_bf16(const uint16_t* x, int64_t M, int N, int64
   if (M <= 0 || N <= 0) return hipSuccess;
   dim3 grid((unsigned)(M < 256 ? M : 256), (N + 63) / 64);
   colsum_bf16_kernel<<<grid, 64, 0, stream>>>(x, M, N, ld, out);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t aca_colsum_reduce(const float* part, int R, int N, float* out, int mod, hipStream_t stream) {
+  if (R <= 0 || N <= 0) return hipSuccess;
+  dim3 grid((R + 511) / 512, (N + 31) / 32);
+  colsum_reduce_kernel<<<grid, 256, 0, stream>>>(part, R, N, out, mod);
   return hipGetLastError();
 }

@@ -93,6 +93,9 @@ typedef struct {
   AcaConvGather ga;   // gather for A (requires a_k)
   AcaConvGather gb;   // gather for B (requires !b_k): B[k = conv row m][n = conv column k]
   unsigned long long* stamps;   // diagnostics (null in production): per workgroup [start, k-loop, epilogue, end]
+  // column sums as per-row-tile partials (plain stores to colsum_part[(m0 / BM) * N + n], no atomics; reduced into
+  // colsum by aca_colsum_reduce): thousands of workgroups adding into the same few bias addresses serialise in L2
+  float* colsum_part;
 } AcaGemmDesc;
 
 #ifdef __cplusplus

@@ -487,6 +487,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmParams P) {
         }
     }
   }
+  float csums[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = n0 + wn * (BN / 2) + j * 16 + lr16;
@@ -513,11 +514,26 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmParams P) {
         csum += v;
       }
     }
-    if (g.colsum) {
-      csum += __shfl_xor(csum, 16, 64);
-      csum += __shfl_xor(csum, 32, 64);
-      if (lg == 0 && n_ok) atomicAdd(&g.colsum[g.colsum_mod ? n % g.colsum_mod : n], csum);
-    }
+    csum += __shfl_xor(csum, 16, 64);
+    csum += __shfl_xor(csum, 32, 64);
+    csums[j] = csum;
+    if (g.colsum && !g.colsum_part && lg == 0 && n_ok)
+      atomicAdd(&g.colsum[g.colsum_mod ? n % g.colsum_mod : n], csum);
+  }
+  if (g.colsum_part) {
+    // the two waves sharing these columns (wm = 0, 1) combine through LDS, then one plain store per column
+    float* csh = reinterpret_cast<float*>(smem);
+    __syncthreads();   // every wave is past its last LDS operand read
+    if (wm == 1 && lg == 0)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) csh[wn * (BN / 2) + j * 16 + lr16] = csums[j];
+    __syncthreads();
+    if (wm == 0 && lg == 0)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int nl = wn * (BN / 2) + j * 16 + lr16;
+        if (n0 + nl < g.N) g.colsum_part[(int64_t)(m0 / BM) * g.N + n0 + nl] = csums[j] + csh[nl];
+      }
   }
   if (st) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -17,6 +17,7 @@
 #include "mlp_desc.h"
 
 extern "C" {
+hipError_t aca_seg_stats(const float*, const int64_t*, int, float*, hipStream_t);
 hipError_t aca_colsum_reduce(const float*, int, int, float*, int, hipStream_t);
 hipError_t aca_mlp_tshadow(const aca::MlpTower*, int, int, hipStream_t);
 hipError_t aca_opt_multi(const int64_t*, const float*, const int64_t*, int, int, float, float, float, int,
@@ -837,6 +838,15 @@ void col2im_nhwc(Tensor dcol, Tensor ymask, Tensor dx, c10::optional<Tensor> col
         "col2im_nhwc");
 }
 
+void seg_stats(Tensor x, Tensor segs, Tensor out) {
+  need(x, at::kFloat, "x");
+  need(segs, at::kLong, "segs");
+  need(out, at::kFloat, "out");
+  const int64_t nv = segs.numel() / 2;
+  TORCH_CHECK(out.numel() >= 4 * nv, "seg_stats: out needs [nvars, 4]");
+  check(aca_seg_stats(ptr<float>(x), ptr<int64_t>(segs), (int)nv, ptr<float>(out), cur_stream(x)), "seg_stats");
+}
+
 void colsum_reduce(Tensor part, int64_t R, int64_t N, Tensor out, int64_t mod) {
   need(part, at::kFloat, "part");
   need(out, at::kFloat, "out");
@@ -973,6 +983,7 @@ TORCH_LIBRARY(acamd, m) {
         "int tile, int bk, int splits, Tensor? ws, Tensor? tickets, int[] ga, float ga_scale, int[] gb, "
         "float gb_scale, Tensor? stamps=None, Tensor? colsum_part=None) -> ()");
   m.def("colsum_reduce(Tensor part, int R, int N, Tensor out, int mod) -> ()");
+  m.def("seg_stats(Tensor x, Tensor segs, Tensor out) -> ()");
   m.def("gemm_effective_splits(int K, int bk, int splits) -> int", &gemm_effective_splits);
   m.def("cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, Tensor y1, "
         "Tensor y2, Tensor y3, float scale, Tensor? shift_out=None, Tensor? stamps=None) -> ()");
@@ -1021,5 +1032,6 @@ TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
   m.impl("col2im_nhwc", &col2im_nhwc);
   m.impl("colsum_bf16", &colsum_bf16);
   m.impl("colsum_reduce", &colsum_reduce);
+  m.impl("seg_stats", &seg_stats);
   m.impl("ac_loss", &ac_loss);
 }

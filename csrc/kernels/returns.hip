@@ -102,6 +102,48 @@ __global__ void prp_perm_kernel(int64_t* __restrict__ out, int n, uint32_t seed,
   if (i < n) out[i] = prp_index((uint32_t)i, (uint32_t)n, minibatch_key(seed, *uc, ep));
 }
 
+// Per-variable statistics of a flat fp32 parameter slab (the reference's variable_summaries, Basic_AC/policies.py:
+// 9-18): out[v] = (mean, population stddev, max, min) of x[off_v, off_v + n_v). One workgroup per
+// variable, double accumulation (single pass: E[x^2] - mean^2 in fp64 matches the two-pass fp32 form closely).
+__global__ void __launch_bounds__(256) seg_stats_kernel(const float* __restrict__ x, const int64_t* __restrict__ segs,
+                                                        float* __restrict__ out) {
+  __shared__ double shd[16 * 2];
+  __shared__ float shf[16];
+  const int v = blockIdx.x;
+  const int64_t off = segs[2 * v], n = segs[2 * v + 1];
+  double s = 0.0, ss = 0.0;
+  float mx = -INFINITY, mn = INFINITY;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const float a = x[off + i];
+    s += a;
+    ss += (double)a * a;
+    mx = fmaxf(mx, a);
+    mn = fminf(mn, a);
+  }
+  double r[2] = {s, ss};
+  block_sum_multi<2>(r, shd);
+  mx = wave_max(mx);
+  mn = -wave_max(-mn);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if (lane == 0) shf[wid] = mx;
+  __syncthreads();
+  float M = -INFINITY;
+  for (int w = 0; w < nw; ++w) M = fmaxf(M, shf[w]);
+  __syncthreads();
+  if (lane == 0) shf[wid] = mn;
+  __syncthreads();
+  float m = INFINITY;
+  for (int w = 0; w < nw; ++w) m = fminf(m, shf[w]);
+  if (threadIdx.x == 0) {
+    const double mean = n ? r[0] / n : 0.0;
+    const double var = n ? fmax(r[1] / n - mean * mean, 0.0) : 0.0;
+    out[4 * v] = (float)mean;
+    out[4 * v + 1] = (float)sqrt(var);
+    out[4 * v + 2] = M;
+    out[4 * v + 3] = m;
+  }
+}
+
 }  // namespace aca
 
 extern "C" hipError_t aca_ev(const float* x, const float* y, float* out, int n, hipStream_t stream) {
@@ -139,5 +181,11 @@ extern "C" hipError_t aca_prp_perm(int64_t* out, int n, uint32_t seed, const int
                                    hipStream_t stream) {
   if (n <= 0) return hipSuccess;
   aca::prp_perm_kernel<<<(n + 255) / 256, 256, 0, stream>>>(out, n, seed, uc, ep);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t aca_seg_stats(const float* x, const int64_t* segs, int nv, float* out, hipStream_t stream) {
+  if (nv <= 0) return hipSuccess;
+  aca::seg_stats_kernel<<<nv, 256, 0, stream>>>(x, segs, out);
   return hipGetLastError();
 }

@@ -127,6 +127,8 @@ class A3CWorker:
         self.cfg = cfg
         self.task = task
         self.is_chief = task == 0
+        # A3C/process.py:175
+        self.debug = cfg.mode == "debug-full" or (cfg.mode == "debug-light" and self.is_chief)
         self.shard = shard
         self.ps_ranks = ps_ranks
         seed = cfg.seed + task
@@ -203,6 +205,13 @@ class A3CWorker:
             ep_obs, ep_advs, ep_logps, ep_targets, ep_acs = ref.make_np(ep_obs, ep_advs, ep_logps, ep_targets, ep_acs)
             ep_advs = (ep_advs - np.mean(ep_advs)) / (1e-8 + np.std(ep_advs))
             avg_ent = tot_ent / float(len(ep_logps))
+            if self.debug and i % 50 == 13:   # A3C/process.py:250-256
+                perm = np.random.choice(len(ep_advs), size=20)
+                print("Some preds", critic.value(ep_obs[perm]))
+                print("Some target vals", ep_targets[perm])
+                print("Some logps", ep_logps[perm])
+                actor.printoo(ep_obs)
+                critic.printoo(ep_obs)
             ev_before = ref.var_accounted_for(ep_targets, critic.value(ep_obs))
             cir_loss = critic.compute_grads(ep_obs, ep_targets)
             act_loss = actor.compute_grads(ep_acs, ep_obs, ep_advs, ep_logps)

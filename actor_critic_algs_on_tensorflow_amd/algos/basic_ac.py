@@ -50,6 +50,11 @@ class BasicACTrainer:
         self.rank = 0
         self.history = []
         self.model = self._model_view()
+        self.tb = None
+        if cfg.tboard:   # Basic_AC/run_AC.py:201-202: summaries/<outdir stem>.data
+            from ..utils import tensorboard as TB
+            self.tb = TB.VariableSummaries(TB.SummaryWriter(TB.summaries_dir(cfg.outdir or "run", cfg.tb_root)),
+                                           TB.reference_summary_scopes(self.actor.net, self.critic.net))
 
     def _model_view(self):
         from ..models.policy import MLPActorCritic
@@ -90,8 +95,15 @@ class BasicACTrainer:
         ep_obs, ep_advs, ep_logps, ep_targets, ep_acs = ref.make_np(ep_obs, ep_advs, ep_logps, ep_targets, ep_acs)
         if cfg.norm_adv:
             ep_advs = (ep_advs - np.mean(ep_advs)) / (1e-8 + np.std(ep_advs))
+        if i % 50 == 13 and cfg.mode == "debug":   # Basic_AC/run_AC.py:243-247
+            perm = np.random.choice(len(ep_advs), size=20)
+            print("Some targets", ep_targets[perm])
+            print("Some preds", critic.value(ep_obs[perm]))
+            print("Some logps", ep_logps[perm])
         cir_loss, ev_before, ev_after = ref.train_ciritic(critic, None, ep_obs, ep_targets)
         act_loss = ref.train_actor(actor, None, ep_obs, ep_advs, ep_logps, ep_acs)
+        if self.tb is not None:   # every iteration, after both updates (Basic_AC/run_AC.py:253-255)
+            self.tb.write(i)
         act_lr, cur_beta, cur_gamma = actor.get_opt_param()
         kl = actor.get_kl(None, ep_logps, ep_obs, ep_acs)
         if cfg.kl_adaptive_lr:
@@ -173,3 +185,5 @@ class BasicACTrainer:
     def close(self):
         if self.logger is not None:
             self.logger.close()
+        if self.tb is not None:
+            self.tb.close()

@@ -22,6 +22,8 @@ gradient slab between backward and the optimiser step.
 from __future__ import annotations
 
 import math
+import os
+import sys
 import time
 
 import torch
@@ -36,10 +38,21 @@ from ..ops.optim import FlatParams, make_optimizer
 from ..utils.logger import Logger
 from ..utils.schedule import DeviceKLAdaptiveLR, RegularizerSchedule
 from ..utils.stats import var_accounted_for_tensor
+from ..utils.trace import PhaseTimer
 from . import losses as L
 from .storage import RolloutStorage
 
 KEY_ENV_BITS = 20
+FAULT_EXIT_CODE = 43   # exit status of a rank killed by ``fault_inject`` (SURVEY §5.3 test hook)
+
+
+def parse_fault(spec):
+    """``"rank:iteration"`` -> (rank, iteration) or None."""
+    if not spec:
+        return None
+    r, it = str(spec).split(":")
+    return int(r), int(it)
+
 # layout of the device statistics buffer; slots 0..6 are written directly by the fused loss kernel
 STAT_KEYS = ("pg", "kl", "entropy", "crit_loss", "clipfrac", "act_loss", "ratio", "ev_before", "ev_after")
 LOG_KEYS = ("act_loss", "crit_loss", "kl", "entropy", "ev_before", "ev_after", "clipfrac")
@@ -115,6 +128,13 @@ class ActorCriticTrainer:
         if self.rank == 0 and cfg.outdir:
             self.logger = Logger(cfg.outdir, legacy_step_index=cfg.legacy_step_index, metrics_path=cfg.metrics_path,
                                  quiet=cfg.quiet)
+        self.tb = None
+        if cfg.tboard and self.rank == 0:
+            from ..utils import tensorboard as TB
+            self.tb = TB.VariableSummaries(TB.SummaryWriter(TB.summaries_dir(cfg.outdir or "run", cfg.tb_root)),
+                                           self._summary_scopes(), self.flat)
+        self.timer = PhaseTimer(self.device, enabled=cfg.trace)
+        self._fault = parse_fault(cfg.fault_inject)
 
     def _want_native(self):
         """The hand-written HIP engine runs the CNN family on GPU (``engine="auto"|"native"``)."""
@@ -516,9 +536,12 @@ class ActorCriticTrainer:
                 and self.lr_ctrl is None and cfg.kl_coef == 0.0)
 
     def update_body(self):
-        self.collect()
-        ret, adv = self.compute_returns()
-        self.learn(ret, adv)
+        with self.timer.phase("rollout"):
+            self.collect()
+        with self.timer.phase("returns"):
+            ret, adv = self.compute_returns()
+        with self.timer.phase("learn"):
+            self.learn(ret, adv)
         self.storage.roll_over()
 
     def _post_body(self):
@@ -541,6 +564,13 @@ class ActorCriticTrainer:
         """Capture the update as hipGraph(s) (see above). Warm-up updates run first (GEMM autotuning, allocator)."""
         if not self._can_capture() or (self.dp is not None and not self._segmented()):
             return None
+        self.timer.suspended = True
+        try:
+            return self._capture(warmup)
+        finally:
+            self.timer.suspended = False
+
+    def _capture(self, warmup):
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -623,7 +653,8 @@ class ActorCriticTrainer:
             if k is not None:
                 self.kl_coef.fill_(k)
         if self.graph is not None:
-            self._replay()
+            with self.timer.phase("update_graph"):
+                self._replay()
         else:
             self.update_body()
         self.iteration += 1
@@ -657,6 +688,7 @@ class ActorCriticTrainer:
         t0 = time.time()
         history = []
         for _ in range(n):
+            self._maybe_fault()
             self.step()
             it = self.iteration - 1
             if cfg.stdout_freq and it % cfg.stdout_freq == 0:
@@ -664,11 +696,17 @@ class ActorCriticTrainer:
                 if s is not None:
                     history.append(dict(iteration=it, **s))
                     el = time.time() - t0
+                    extra = {"phase_ms": self.timer.summary()} if cfg.trace else {}
                     self.logger.log_metrics(iteration=it, env_steps=self.env_steps,
-                                            env_steps_per_sec=self.env_steps / max(el, 1e-9), **s)
+                                            env_steps_per_sec=self.env_steps / max(el, 1e-9), **extra, **s)
+                if self.tb is not None:
+                    self.tb.write(it, extra=self._tb_scalars(s))
+                if cfg.mode.startswith("debug") and (cfg.mode != "debug-light" or self.rank == 0):
+                    self._debug_print()
             if self.logger is not None and cfg.flush_every and it % cfg.flush_every == cfg.flush_every // 2:
                 self.logger.flush()
-            if cfg.save_every and it % cfg.save_every == 0 and self.rank == 0 and cfg.checkpoint_dir:
+            if cfg.save_every and it % cfg.save_every == 0 and cfg.checkpoint_dir and \
+                    (self.rank == 0 or self.dp is not None):   # DP: every rank takes part (env-state gather)
                 self.save_checkpoint()
             if callback is not None:
                 callback(self, it)
@@ -687,3 +725,47 @@ class ActorCriticTrainer:
     def close(self):
         if self.logger is not None:
             self.logger.close()
+        if self.tb is not None:
+            self.tb.close()
+
+    # ------------------------------------------------------------------ observability / failure hooks
+    def _maybe_fault(self):
+        """SURVEY §5.3 fault injection: ``fault_inject="rank:iteration"`` kills this process -- no cleanup, no
+        collective goodbye, as a crashed host would -- when it is about to run that iteration. The surviving ranks'
+        next collective raises (gloo: peer closed; RCCL: ``dist_timeout_s``), and ``resume="auto"`` restarts the job
+        from the newest checkpoint."""
+        if self._fault is not None and self._fault == (self.rank, self.iteration):
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(FAULT_EXIT_CODE)
+
+    def _summary_scopes(self):
+        """The reference's per-variable summary scopes (``Basic_AC/policies.py:83-85,146-149``) for the MLP family;
+        one ``ActorCritic`` scope over every parameter otherwise."""
+        from ..models.policy import MLPActorCritic
+        from ..utils.tensorboard import reference_summary_scopes
+        if isinstance(self.model, MLPActorCritic):
+            return reference_summary_scopes(self.model.actor, self.model.critic)
+        return [("ActorCritic", list(self.model.parameters()))]
+
+    def _tb_scalars(self, s):
+        if s is None:
+            vals = self.stats_buf.detach().cpu().tolist()
+            s = {k: vals[STAT_KEYS.index(k)] for k in LOG_KEYS}
+        return {"train/" + k: float(v) for k, v in s.items() if isinstance(v, (int, float))}
+
+    @torch.no_grad()
+    def _debug_print(self):
+        """``--mode debug`` (``debug-light``: rank 0 only, ``debug-full``: every rank): the reference's printer block
+        (``Basic_AC/policies.py:87-89,144-145``; ``A3C/process.py:250-256``) -- per-variable means (one statistics
+        launch over the parameter slab) and a strided sample of predicted values, log-probs and returns."""
+        from ..ops.stats import param_segments, seg_stats
+        params = list(self.model.parameters())
+        means = seg_stats(self.flat.data, param_segments(self.flat, params))[:, 0].cpu().tolist()
+        st = self.storage
+        n = st.T * self.env.num_envs
+        idx = torch.arange(20, device=st.values.device) * max(1, n // 20) % n
+        print("[rank %d] Variable data" % self.rank, [round(m, 6) for m in means])
+        print("[rank %d] Some preds" % self.rank, st.values[:st.T].reshape(-1)[idx].cpu().numpy())
+        print("[rank %d] Some logps" % self.rank, st.logp.reshape(-1)[idx].cpu().numpy())
+        print("[rank %d] Some rewards" % self.rank, st.rewards.reshape(-1)[idx].cpu().numpy(), flush=True)

@@ -56,19 +56,28 @@ def train(cfg: TrainConfig | str, **overrides) -> TrainResult:
         cfg = cfg.replace(**overrides)
     dp = None
     from .parallel import dp as DP
-    rank, world, local = DP.init_from_env(cfg.dist_backend)
+    rank, world, local = DP.init_from_env(cfg.dist_backend, timeout_s=cfg.dist_timeout_s)
     if world > 1:
         if cfg.device.startswith("cuda"):
             cfg = cfg.replace(device=f"cuda:{local}")
         dp = DP.DataParallel()
     tr = make_trainer(cfg, dp)
+    n = None
+    if cfg.resume:   # restart from the newest (or a given) checkpoint, run the remaining updates
+        if cfg.algo == "basic_ac":
+            raise ValueError("resume needs the vectorised trainers (the basic_ac parity loop keeps no resume state)")
+        from . import ckpt
+        path = ckpt.latest_checkpoint(cfg.checkpoint_dir) if cfg.resume == "auto" else cfg.resume
+        if path is not None:
+            tr.load_checkpoint(path)
+        n = max(0, cfg.total_updates - tr.iteration)
     t0 = time.time()
-    hist = tr.train()
+    hist = tr.train(n) if n is not None else tr.train()
     if cfg.device.startswith("cuda"):
         torch.cuda.synchronize()
     dt = time.time() - t0
     ck = None
-    if cfg.checkpoint_dir and cfg.save_every and getattr(tr, "rank", 0) == 0:
+    if cfg.checkpoint_dir and cfg.save_every and (getattr(tr, "rank", 0) == 0 or getattr(tr, "dp", None) is not None):
         ck = tr.save_checkpoint()
     if hasattr(tr, "close"):
         tr.close()

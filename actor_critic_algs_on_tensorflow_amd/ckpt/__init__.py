@@ -141,9 +141,42 @@ def env_prefix(env_id):
     return env_id.split("-")[0]
 
 
+def _env_state(trainer):
+    env = trainer.env
+    st = {k: getattr(env, k) for k in ("state", "t", "tg", "ep_ret")}
+    st["obs"] = trainer.storage.obs[0]
+    return st
+
+
+def _gather_env_states(trainer):
+    """-> {rank: {name: tensor}} on rank 0, None on the other ranks. With data parallelism every rank simulates its
+    own envs, so a resumable checkpoint needs all of them: one all_gather per tensor (identical shapes on every
+    rank), called collectively by all ranks."""
+    st = _env_state(trainer)
+    dp = getattr(trainer, "dp", None)
+    if dp is None or dp.world_size == 1:
+        return {0: st}
+    import torch.distributed as dist
+    got = {r: {} for r in range(dp.world_size)}
+    for k, v in st.items():
+        v = v.contiguous()
+        bufs = [torch.empty_like(v) for _ in range(dp.world_size)]
+        dist.all_gather(bufs, v, group=dp.group)
+        for r in range(dp.world_size):
+            got[r][k] = bufs[r]
+    return got if dp.rank == 0 else None
+
+
 def save_trainer(trainer, path=None):
-    """Rank-0 checkpoint of an :class:`..algos.trainer.ActorCriticTrainer` (model + optimiser + counters)."""
+    """Checkpoint of an :class:`..algos.trainer.ActorCriticTrainer` (model + optimiser + counters + env banks).
+
+    Without DP it is called on rank 0. With DP every rank must call it (the env states are gathered); rank 0
+    writes and returns the path, the others return None. Resume is exact for the strict / single-graph schedules; a
+    lag-1 DP run resumes without the in-flight delayed gradient."""
     cfg = trainer.cfg
+    envs = _gather_env_states(trainer)
+    if envs is None:
+        return None
     base = f"model-{env_prefix(cfg.env)}"
     if path is None:
         os.makedirs(cfg.checkpoint_dir, exist_ok=True)
@@ -154,10 +187,14 @@ def save_trainer(trainer, path=None):
             tensors[f"_acamd/opt/{g}/{k}"] = v.reshape(-1) if v.dim() else v
     tensors["_acamd/iteration"] = np.asarray(trainer.iteration, dtype=np.int64)
     tensors["_acamd/env_steps"] = np.asarray(trainer.env_steps, dtype=np.int64)
-    env = trainer.env
-    for k in ("state", "t", "tg", "ep_ret"):
-        tensors[f"_acamd/env/{k}"] = getattr(env, k)
-    tensors["_acamd/env/obs"] = trainer.storage.obs[0]
+    for k, v in envs[0].items():
+        tensors[f"_acamd/env/{k}"] = v
+    if len(envs) > 1:
+        for r, st in envs.items():
+            for k, v in st.items():
+                tensors[f"_acamd/env/rank{r}/{k}"] = v
+    tensors["_acamd/world_size"] = np.asarray(len(envs), dtype=np.int64)
+    tensors["_acamd/update_counter"] = trainer.update_counter
     tensors["_acamd/ent_coef"] = trainer.ent_coef
     tensors["_acamd/kl_coef"] = trainer.kl_coef
     save_tensors(path, tensors)
@@ -205,9 +242,16 @@ def load_trainer(trainer, path):
     if "_acamd/iteration" in t:
         trainer.iteration = int(t["_acamd/iteration"])
         trainer.env_steps = int(t["_acamd/env_steps"])
+        world, rank = getattr(trainer, "world", 1), getattr(trainer, "rank", 0)
+        saved = int(t["_acamd/world_size"]) if "_acamd/world_size" in t else 1
+        if saved != world:
+            raise ValueError(f"checkpoint {path} holds the env banks of {saved} rank(s); this job has {world}")
+        pre = f"_acamd/env/rank{rank}/" if saved > 1 else "_acamd/env/"
         for k in ("state", "t", "tg", "ep_ret"):
-            _assign(getattr(trainer.env, k), t[f"_acamd/env/{k}"])
-        _assign(trainer.storage.obs[0], t["_acamd/env/obs"])
+            _assign(getattr(trainer.env, k), t[pre + k])
+        _assign(trainer.storage.obs[0], t[pre + "obs"])
+        if "_acamd/update_counter" in t:
+            _assign(trainer.update_counter, t["_acamd/update_counter"])
         _assign(trainer.ent_coef, t["_acamd/ent_coef"])
         _assign(trainer.kl_coef, t["_acamd/kl_coef"])
     return trainer

@@ -75,8 +75,14 @@ class TrainConfig:
     keep_checkpoints: int = 3
     quiet: bool = False
     legacy_step_index: bool = False
-    tboard: bool = False
+    tboard: bool = False              # TensorBoard event file under summaries_dir(outdir) (utils/tensorboard.py)
+    tb_root: str = "summaries"
     mode: str = "train"               # train | debug | debug-light | debug-full
+    trace: bool = False               # per-phase timers + ROCTx ranges (utils/trace.py), reported in the metrics stream
+    # -- failure handling -------------------------------------------------------------------------------
+    fault_inject: str | None = None   # "rank:iteration": that rank dies (os._exit) when it reaches that iteration
+    resume: str | None = None         # "auto" = newest checkpoint in checkpoint_dir, or a checkpoint prefix
+    dist_timeout_s: int = 300         # collective timeout: a dead peer surfaces as an exception, not a hang
 
     def replace(self, **kw):
         return dataclasses.replace(self, **kw)

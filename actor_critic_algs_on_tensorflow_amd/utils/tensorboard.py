@@ -123,6 +123,84 @@ def variable_summary_tags(scopes):
     return out
 
 
+def summaries_dir(outdir, root="summaries"):
+    """The reference's event directory: ``summaries/<outdir up to the first '.'>.data`` (``Basic_AC/run_AC.py:202``)."""
+    return os.path.join(root, str(outdir).split(".")[0] + ".data")
+
+
+def reference_summary_scopes(actor, critic):
+    """The variable lists the reference attaches ``variable_summaries`` to, in graph order.
+
+    ``Basic_AC/run_AC.py:197-198`` builds the Critic before the Actor, and both call ``adam.compute_gradients(loss)``
+    without a ``var_list`` (``Basic_AC/policies.py:80,146``), i.e. over EVERY trainable variable that exists at that
+    point: the Critic summarises its own 8 variables (``third_layer`` included although ``value`` reads
+    ``second_layer``), the Actor summarises the Critic's 8 followed by its own (kernel/bias of the 4 dense layers, then
+    the continuous ``log_std``)."""
+    crit = []
+    for n in ("first_layer", "second_layer", "third_layer", "value"):
+        layer = getattr(critic, n, None)
+        if layer is not None:
+            crit += [layer.kernel, layer.bias]
+    act = []
+    for n in ("first_layer", "second_layer", "third_layer", "logits" if actor.discrete else "mu_layer"):
+        layer = getattr(actor, n, None)
+        if layer is not None:
+            act += [layer.kernel, layer.bias]
+    if not actor.discrete and getattr(actor, "log_std", None) is not None:
+        act.append(actor.log_std)
+    return [("Critic", crit), ("Actor", crit + act)]
+
+
+class VariableSummaries:
+    """Per-variable mean / stddev / max / min of scoped variable lists, written as one merged Event.
+
+    When every variable lives in one :class:`..ops.optim.FlatParams` slab the statistics come from ONE device
+    reduction launch and ONE device->host copy (``ops/stats.py``); otherwise (the CPU parity trainer) per tensor."""
+
+    def __init__(self, writer, scopes, flat=None):
+        self.writer = writer
+        self.tags = [t for per in variable_summary_tags([(s, len(v)) for s, v in scopes]) for t in per]
+        uniq, self.slot, seen = [], [], {}
+        for _, vs in scopes:
+            for v in vs:
+                if id(v) not in seen:
+                    seen[id(v)] = len(uniq)
+                    uniq.append(v)
+                self.slot.append(seen[id(v)])
+        self.uniq = uniq
+        self.flat, self.segs = None, None
+        if flat is not None and all(id(v) in {id(p) for p in flat.params} for v in uniq):
+            from ..ops.stats import param_segments
+            self.flat = flat
+            self.segs = param_segments(flat, uniq)
+
+    def values(self):
+        """-> dict tag -> float."""
+        if self.flat is not None:
+            from ..ops.stats import seg_stats
+            st = seg_stats(self.flat.data, self.segs).cpu().tolist()
+        else:
+            st = []
+            for v in self.uniq:
+                x = v.detach().double().reshape(-1)
+                st.append([x.mean().item(), x.var(unbiased=False).sqrt().item(), x.max().item(), x.min().item()])
+        out = {}
+        for tags, k in zip(self.tags, self.slot):
+            for tag, val in zip(tags, st[k]):
+                out[tag] = val
+        return out
+
+    def write(self, step, extra=None):
+        vals = self.values()
+        if extra:
+            vals.update(extra)
+        self.writer.add_scalars(vals, step)
+        return vals
+
+    def close(self):
+        self.writer.close()
+
+
 # ------------------------------------------------------------------------------------------------ reader (tests)
 def _read_varint(b, i):
     shift = n = 0

@@ -281,7 +281,10 @@ void append_block(std::string* file, const std::string& block, uint64_t* off, ui
 }
 
 std::string read_block(const std::string& file, uint64_t off, uint64_t size) {
-  if (off + size + 5 > file.size()) throw FormatError("block handle out of range");
+  // (no off + size + 5 sum: handles come from the file and the sum can wrap around 64 bits -- found by the ASan
+  // self-test, csrc/tfbundle/selftest.cpp)
+  if (off > file.size() || size > file.size() - off || file.size() - off - size < 5)
+    throw FormatError("block handle out of range");
   const std::string block = file.substr(off, size);
   const uint8_t type = (uint8_t)file[off + size];
   if (type != 0) throw FormatError("compressed blocks are not supported");
@@ -478,13 +481,14 @@ std::vector<Tensor> read_bundle(const std::string& prefix, bool verify_crc) {
   std::vector<Entry> entries;
   parse_index(slurp(prefix + ".index"), &h, &entries);
   if (h.endianness != 0) throw FormatError("big-endian bundles are not supported");
+  if (h.num_shards < 0 || h.num_shards > 65536) throw FormatError("bad shard count");
   std::vector<std::string> shards;
   for (int s = 0; s < std::max(1, h.num_shards); ++s) shards.push_back(slurp(data_path(prefix, s, h.num_shards)));
   std::vector<Tensor> out;
   for (const Entry& e : entries) {
     if (e.shard_id < 0 || e.shard_id >= (int)shards.size()) throw FormatError("bad shard id for " + e.key);
     const std::string& d = shards[e.shard_id];
-    if (e.offset < 0 || e.size < 0 || (uint64_t)(e.offset + e.size) > d.size())
+    if (e.offset < 0 || e.size < 0 || (uint64_t)e.offset > d.size() || (uint64_t)e.size > d.size() - (uint64_t)e.offset)
       throw FormatError("tensor " + e.key + " out of range of the data file");
     Tensor t;
     t.key = e.key;

@@ -184,8 +184,13 @@ class ActorCriticTrainer:
 
     @torch.no_grad()
     def _collect_mlp(self):
-        """One launch per step for the policy (both towers + sampling) and one for the env bank."""
+        """MuJoCo-shaped bank: ONE persistent launch for the whole rollout + one critic launch (ops/mlp.py
+        ``rollout_linear``). Otherwise one launch per step for the policy (both towers + sampling) and one for the
+        env bank."""
         st, env, eng = self.storage, self.env, self.mlp
+        if self.cfg.fused_rollout and eng.supports_fused_rollout(env):
+            eng.rollout_linear(env, st, KEY_ENV_BITS, self.policy_seed)
+            return
         for t in range(st.T):
             eng.policy_step(st.obs[t], st.actions[t], st.logp[t], st.entropy[t], st.values[t], env.tg, env.env_ids,
                             KEY_ENV_BITS, self.policy_seed)

@@ -56,6 +56,7 @@ class TrainConfig:
     engine: str = "auto"              # auto | native (hand-written HIP engine) | torch (autograd reference)
     cuda_graph: bool = True
     reuse_rollout_acts: bool = True   # native A2C: the rollout's activations are the learner's forward (exact)
+    fused_rollout: bool = True        # native MLP engine + MuJoCo-shaped bank: the whole rollout in one launch
     total_updates: int = 1000
     # -- distributed -----------------------------------------------------------------------------------------------
     dist_backend: str = "auto"        # auto -> nccl (RCCL) on GPU, gloo on CPU

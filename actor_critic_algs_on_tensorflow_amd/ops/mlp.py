@@ -13,6 +13,10 @@ per 16 rows with its activations in LDS, on f32 MFMA:
   sums of squares for the global-norm clip; loss statistics). The optimiser step follows (:mod:`.optim`).
 * :meth:`MLPEngine.evaluate` / :meth:`value` -- log-prob / entropy of given actions and values (post-update KL proxy
   and EV of the reference, ``Basic_AC/run_AC.py:257-258``; bootstrap values).
+* :meth:`MLPEngine.rollout_linear` -- the whole T-step rollout of the MuJoCo-shaped bank in ONE persistent launch
+  (actor + sampling + env dynamics + frame stack per 16-env workgroup, ``mlp_rollout_kernel``) followed by ONE
+  batched critic launch over all ``(T+1) N`` observations (the rollout's Session.run-per-step loop of
+  ``Basic_AC/run_AC.py:82-107``).
 
 Weights are read in place from the fp32 parameter slab (TF ``[in, out]`` kernels, so checkpoints need no
 transposes) and gradients are written straight into the gradient slab.
@@ -29,6 +33,8 @@ ACT_CODES = {None: 0, "none": 0, "relu": 1, "lrelu": 2, "tanh": 3}
 BM = 16
 MAXW = 256
 PARTS = 256
+MPART_W = 24    # per-workgroup partial row of the train kernel (mlp_desc.h)
+LIN_OBS, LIN_ACT = 17, 6
 
 
 def _ld(w):
@@ -84,6 +90,7 @@ class MLPEngine:
         self.items = [sum(((l.in_features + 15) // 16) * ((l.out_features + 15) // 16) for l in tw)
                       for tw in self.towers]
         self._descs = {}
+        self._mparts = {}
         self._dummy_stats = torch.zeros(16, dtype=torch.float32, device=self.dev)
         # transposed weight shadows [out][16 * ngp2(in)] (zero pad) -- the forward's B operand
         self.wt = {}
@@ -148,6 +155,13 @@ class MLPEngine:
             best = max(best, n)
         return best * 4
 
+    def _mpart(self, B):
+        """Per-workgroup partial rows of the train kernel (loss statistics + log-std gradient), summed by the
+        weight-gradient kernel -- no same-address atomics from every workgroup."""
+        if B not in self._mparts:
+            self._mparts[B] = torch.zeros((B + BM - 1) // BM * MPART_W, dtype=torch.float32, device=self.dev)
+        return self._mparts[B]
+
     def _fwd(self, mode, obs, B, tw_base=0, ntw=2, desc_B=None, idx=None, perm=None, tg=None, env_ids=None, key_shift=0,
              seed=0, act_out=None, logp_out=None, ent_out=None, v_out=None, act_in=None, logp_old=None, adv=None,
              ret=None, v_old=None, ent_coef=None, kl_coef=None, vf_coef=1.0, ppo_clip=0.0, v_clip=0.0, ppo=False):
@@ -160,7 +174,7 @@ class MLPEngine:
                     self.log_std, self.ac_scale, tg, env_ids, key_shift, seed, act_out, logp_out, ent_out, v_out,
                     act_in, logp_old, adv, ret, v_old, ent_coef, kl_coef, float(vf_coef), float(ppo_clip),
                     float(v_clip or 0.0), bool(ppo), self.g_log_std if mode == 2 else None,
-                    self.mstats if mode == 2 else None)
+                    self.mstats if mode == 2 else None, self._mpart(B) if mode == 2 else None)
 
     # ------------------------------------------------------------------------------------------- API
     def policy_step(self, obs, act_out, logp_out, ent_out, v_out, tg, env_ids, key_shift, seed):
@@ -192,5 +206,27 @@ class MLPEngine:
         st = stats if stats is not None else self._dummy_stats
         ops.mlp_wgrad(desc, 2, B, nsplit, self.items[0], self.items[1], self.parts[0] if use_parts else None,
                       self.parts[1] if use_parts else None, float(clips[0] or -1.0), float(clips[1] or -1.0),
-                      self.g_log_std, self.A, self.mstats, st, ent_coef, kl_coef)
+                      self.g_log_std, self.A, self.mstats, st, ent_coef, kl_coef, self._mpart(B), (B + BM - 1) // BM)
         return use_parts
+
+    # ------------------------------------------------------------------------------------------- fused rollout
+    def supports_fused_rollout(self, env):
+        from ..envs.mujoco import MujocoShapeVecEnv
+        return (isinstance(env, MujocoShapeVecEnv) and not self.discrete and self.A == LIN_ACT
+                and self.D == LIN_OBS * env.frame_stack)
+
+    def rollout_lds_bytes(self):
+        n = 2 * BM * _ld(self.D) + sum(BM * _ld(l.out_features) for l in self.towers[0])
+        n += LIN_OBS * LIN_OBS + LIN_OBS * LIN_ACT + BM * LIN_OBS + BM * 16
+        return 4 * n
+
+    def rollout_linear(self, env, st, key_shift, seed):
+        """T steps of policy + env for the whole bank in one launch, then V(s) of all (T+1) N observations in one
+        critic launch. Bit-identical to T x (:meth:`policy_step` + ``env.step``) + :meth:`value`."""
+        T, N = st.T, env.num_envs
+        desc, _ = self.desc(None)
+        _native.require().mlp_rollout(desc, self.rollout_lds_bytes(), st.obs, st.actions, st.logp, st.entropy,
+                                      st.rewards, st.dones, st.truncated, self.log_std, self.ac_scale, key_shift, seed,
+                                      env.state, env.t, env.tg, env.ep_ret, env.ep_stats, env.env_ids, env.A, env.B,
+                                      env.seed, env.max_episode_steps, env.frame_stack)
+        self.value(st.obs.view((T + 1) * N, -1), st.values.view(-1))

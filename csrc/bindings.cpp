@@ -25,6 +25,7 @@ hipError_t aca_opt_multi(const int64_t*, const float*, const int64_t*, int, int,
 hipError_t aca_prp_perm(int64_t*, int, uint32_t, const int64_t*, int, hipStream_t);
 hipError_t aca_mlp_fwd(const aca::MlpArgs*, int, size_t, hipStream_t);
 hipError_t aca_mlp_wgrad(const aca::WgradArgs*, hipStream_t);
+hipError_t aca_mlp_rollout(const aca::RolloutArgs*, size_t, hipStream_t);
 hipError_t aca_env_step_cartpole(float*, int32_t*, int64_t*, float*, float*, const int64_t*, const int32_t*,
                                  const float*, float*, float*, uint8_t*, uint8_t*, uint32_t, int, int, int,
                                  hipStream_t);
@@ -464,7 +465,7 @@ void mlp_fwd(Tensor desc, int64_t tw_base, int64_t ntw, int64_t mode, int64_t ld
              c10::optional<Tensor> logp_old, c10::optional<Tensor> adv, c10::optional<Tensor> ret,
              c10::optional<Tensor> v_old, c10::optional<Tensor> ent_coef, c10::optional<Tensor> kl_coef,
              double vf_coef, double ppo_clip, double v_clip, bool ppo, c10::optional<Tensor> g_log_std,
-             c10::optional<Tensor> mstats) {
+             c10::optional<Tensor> mstats, c10::optional<Tensor> mpart) {
   need(desc, at::kLong, "desc");
   TORCH_CHECK(desc.numel() * 8 >= (int64_t)(2 * sizeof(aca::MlpTower)), "mlp_fwd: desc too small");
   TORCH_CHECK(obs.is_cuda() && obs.scalar_type() == at::kFloat && obs.dim() == 2 && obs.stride(1) == 1,
@@ -518,6 +519,9 @@ void mlp_fwd(Tensor desc, int64_t tw_base, int64_t ntw, int64_t mode, int64_t ld
   a.ppo = ppo ? 1 : 0;
   a.g_log_std = const_cast<float*>(copt<float>(g_log_std, at::kFloat, "g_log_std"));
   a.mstats = const_cast<float*>(copt<float>(mstats, at::kFloat, "mstats"));
+  a.mpart = const_cast<float*>(copt<float>(mpart, at::kFloat, "mpart"));
+  if (a.mpart) TORCH_CHECK(mode == 2 && mpart->numel() >= (B + 15) / 16 * aca::MPART_W,
+                           "mlp_fwd: mpart must hold ceil(B/16) rows of ", aca::MPART_W, " (train mode)");
   a.inv_B = B > 0 ? 1.0f / (float)B : 0.f;
   const bool policy = tw_base == 0;
   if (policy) {
@@ -546,9 +550,14 @@ void mlp_tshadow(Tensor desc, int64_t ntw, int64_t total) {
 void mlp_wgrad(Tensor desc, int64_t ntw, int64_t B, int64_t nsplit, int64_t items0, int64_t items1,
                c10::optional<Tensor> parts0, c10::optional<Tensor> parts1, double clip0, double clip1,
                c10::optional<Tensor> g_log_std, int64_t A, c10::optional<Tensor> mstats, c10::optional<Tensor> stats,
-               c10::optional<Tensor> ent_coef, c10::optional<Tensor> kl_coef) {
+               c10::optional<Tensor> ent_coef, c10::optional<Tensor> kl_coef, c10::optional<Tensor> mpart,
+               int64_t mpart_rows) {
   need(desc, at::kLong, "desc");
   aca::WgradArgs a{};
+  a.mpart = copt<float>(mpart, at::kFloat, "mpart");
+  a.mpart_rows = (int)mpart_rows;
+  if (a.mpart) TORCH_CHECK(mpart_rows >= 0 && mpart->numel() >= mpart_rows * aca::MPART_W && A <= 16,
+                           "mlp_wgrad: mpart too small");
   a.tw = reinterpret_cast<const aca::MlpTower*>(desc.data_ptr());
   a.ntw = (int)ntw;
   a.B = (int)B;
@@ -559,14 +568,72 @@ void mlp_wgrad(Tensor desc, int64_t ntw, int64_t B, int64_t nsplit, int64_t item
   a.parts[1] = const_cast<float*>(copt<float>(parts1, at::kFloat, "parts1"));
   a.clip[0] = (float)clip0;
   a.clip[1] = (float)clip1;
-  a.g_log_std = copt<float>(g_log_std, at::kFloat, "g_log_std");
+  a.g_log_std = const_cast<float*>(copt<float>(g_log_std, at::kFloat, "g_log_std"));
   a.A = (int)A;
   a.mstats = const_cast<float*>(copt<float>(mstats, at::kFloat, "mstats"));
   a.stats = const_cast<float*>(copt<float>(stats, at::kFloat, "stats"));
   a.ent_coef = copt<float>(ent_coef, at::kFloat, "ent_coef");
   a.kl_coef = copt<float>(kl_coef, at::kFloat, "kl_coef");
   if (a.stats) TORCH_CHECK(a.mstats && a.ent_coef && a.kl_coef, "mlp_wgrad: stats need mstats and coefficients");
+  if (a.mpart) TORCH_CHECK(a.mstats, "mlp_wgrad: mpart needs mstats");
   check(aca_mlp_wgrad(&a, cur_stream(desc)), "mlp_wgrad");
+}
+
+void mlp_rollout(Tensor desc, int64_t lds, Tensor obs, Tensor act, Tensor logp, Tensor ent, Tensor reward,
+                 Tensor done, Tensor trunc, Tensor log_std, Tensor ac_scale, int64_t key_shift, int64_t policy_seed,
+                 Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, Tensor env_ids, Tensor lin_A,
+                 Tensor lin_B, int64_t env_seed, int64_t max_steps, int64_t k) {
+  need(desc, at::kLong, "desc");
+  TORCH_CHECK(desc.numel() * 8 >= (int64_t)sizeof(aca::MlpTower), "mlp_rollout: desc too small");
+  need(obs, at::kFloat, "obs");
+  check_env(state, t, tg, ep_ret, ep_stats, env_ids, reward, done, trunc);
+  need(act, at::kFloat, "act");
+  need(logp, at::kFloat, "logp");
+  need(ent, at::kFloat, "ent");
+  need(log_std, at::kFloat, "log_std");
+  need(ac_scale, at::kFloat, "ac_scale");
+  need(lin_A, at::kFloat, "lin_A");
+  need(lin_B, at::kFloat, "lin_B");
+  TORCH_CHECK(obs.dim() == 3, "mlp_rollout: obs must be [T+1, N, D]");
+  const int64_t T = obs.size(0) - 1, N = obs.size(1), D = obs.size(2);
+  TORCH_CHECK(T >= 1 && k >= 1 && D == 17 * k && state.numel() == N * 17, "mlp_rollout: bad obs / state shapes");
+  TORCH_CHECK(act.numel() == T * N * 6 && logp.numel() == T * N && ent.numel() == T * N && reward.numel() == T * N &&
+                  done.numel() == T * N && trunc.numel() == T * N,
+              "mlp_rollout: rollout buffers must be [T, N] / [T, N, 6]");
+  TORCH_CHECK(t.numel() == N && tg.numel() == N && ep_ret.numel() == N && env_ids.numel() == N &&
+                  ep_stats.numel() >= 3, "mlp_rollout: env bank buffers must be [N]");
+  TORCH_CHECK(log_std.numel() == 6 && ac_scale.numel() == 6 && lin_A.numel() == 17 * 17 && lin_B.numel() == 17 * 6,
+              "mlp_rollout: bad head / dynamics shapes");
+  aca::RolloutArgs a{};
+  a.tw = reinterpret_cast<const aca::MlpTower*>(desc.data_ptr());
+  a.N = (int)N;
+  a.T = (int)T;
+  a.D = (int)D;
+  a.A = 6;
+  a.head = 2;
+  a.k = (int)k;
+  a.log_std = ptr<float>(log_std);
+  a.ac_scale = ptr<float>(ac_scale);
+  a.key_shift = (int)key_shift;
+  a.policy_seed = (uint32_t)policy_seed;
+  a.obs = ptr<float>(obs);
+  a.act = ptr<float>(act);
+  a.logp = ptr<float>(logp);
+  a.ent = ptr<float>(ent);
+  a.reward = ptr<float>(reward);
+  a.done = ptr<uint8_t>(done);
+  a.trunc = ptr<uint8_t>(trunc);
+  a.state = ptr<float>(state);
+  a.t = ptr<int32_t>(t);
+  a.tg = ptr<int64_t>(tg);
+  a.ep_ret = ptr<float>(ep_ret);
+  a.ep_stats = ptr<float>(ep_stats);
+  a.env_ids = ptr<int64_t>(env_ids);
+  a.lin_A = ptr<float>(lin_A);
+  a.lin_B = ptr<float>(lin_B);
+  a.env_seed = (uint32_t)env_seed;
+  a.max_steps = (int)max_steps;
+  check(aca_mlp_rollout(&a, (size_t)lds, cur_stream(obs)), "mlp_rollout");
 }
 
 // words: CPU int64 [nseg, 11], fvals: CPU float [nseg, 4] (built once by ops/optim.py FusedGroupStep)
@@ -974,10 +1041,14 @@ TORCH_LIBRARY(acamd, m) {
         "int A, Tensor? log_std, Tensor? ac_scale, Tensor? tg, Tensor? env_ids, int key_shift, int seed, "
         "Tensor? act_out, Tensor? logp_out, Tensor? ent_out, Tensor? v_out, Tensor? act_in, Tensor? logp_old, "
         "Tensor? adv, Tensor? ret, Tensor? v_old, Tensor? ent_coef, Tensor? kl_coef, float vf_coef, float ppo_clip, "
-        "float v_clip, bool ppo, Tensor? g_log_std, Tensor? mstats) -> ()");
+        "float v_clip, bool ppo, Tensor? g_log_std, Tensor? mstats, Tensor? mpart=None) -> ()");
   m.def("mlp_wgrad(Tensor desc, int ntw, int B, int nsplit, int items0, int items1, Tensor? parts0, "
         "Tensor? parts1, float clip0, float clip1, Tensor? g_log_std, int A, Tensor? mstats, Tensor? stats, "
-        "Tensor? ent_coef, Tensor? kl_coef) -> ()");
+        "Tensor? ent_coef, Tensor? kl_coef, Tensor? mpart=None, int mpart_rows=0) -> ()");
+  m.def("mlp_rollout(Tensor desc, int lds, Tensor obs, Tensor act, Tensor logp, Tensor ent, Tensor reward, "
+        "Tensor done, Tensor truncated, Tensor log_std, Tensor ac_scale, int key_shift, int policy_seed, "
+        "Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, Tensor env_ids, Tensor lin_A, "
+        "Tensor lin_B, int env_seed, int max_steps, int k) -> ()");
   m.def("gemm(Tensor A, int lda, bool a_k, Tensor B, int ldb, bool b_k, Tensor C, int ldc, int out_mode, int M, "
         "int N, int K, float alpha, Tensor? bias, bool relu, Tensor? mask, int ldm, Tensor? colsum, int colsum_mod, "
         "int tile, int bk, int splits, Tensor? ws, Tensor? tickets, int[] ga, float ga_scale, int[] gb, "
@@ -1024,6 +1095,7 @@ TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
   m.impl("prp_perm", &prp_perm);
   m.impl("mlp_tshadow", &mlp_tshadow);
   m.impl("mlp_wgrad", &mlp_wgrad);
+  m.impl("mlp_rollout", &mlp_rollout);
   m.impl("gemm", &gemm);
   m.impl("cnn_trunk_fwd", &cnn_trunk_fwd);
   m.impl("fc_value", &fc_value);

@@ -92,6 +92,21 @@ __device__ __forceinline__ float wave_sum(float v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+
+// wave-aggregated episode statistics [sum_ret, count, sum_len] (one atomic per wave and field)
+__device__ __forceinline__ void add_ep_stats(float* ep_stats, bool active, bool done, float ret, float len) {
+  float a = (active && done) ? ret : 0.f;
+  float b = (active && done) ? 1.f : 0.f;
+  float c = (active && done) ? len : 0.f;
+  a = wave_sum(a);
+  b = wave_sum(b);
+  c = wave_sum(c);
+  if ((threadIdx.x & 63) == 0 && b > 0.f) {
+    atomicAdd(&ep_stats[0], a);
+    atomicAdd(&ep_stats[1], b);
+    atomicAdd(&ep_stats[2], c);
+  }
+}
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));

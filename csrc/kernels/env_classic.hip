@@ -27,21 +27,6 @@ struct EnvIO {
   int N;
 };
 
-// wave-aggregated episode statistics (one atomic per wave and field)
-__device__ __forceinline__ void add_ep_stats(float* ep_stats, bool active, bool done, float ret, float len) {
-  float a = (active && done) ? ret : 0.f;
-  float b = (active && done) ? 1.f : 0.f;
-  float c = (active && done) ? len : 0.f;
-  a = wave_sum(a);
-  b = wave_sum(b);
-  c = wave_sum(c);
-  if ((threadIdx.x & 63) == 0 && b > 0.f) {
-    atomicAdd(&ep_stats[0], a);
-    atomicAdd(&ep_stats[1], b);
-    atomicAdd(&ep_stats[2], c);
-  }
-}
-
 template <int D>
 __device__ __forceinline__ void push_frame(const EnvIO& io, int i, const float* frame, bool reset) {
   const int k = io.k;

@@ -434,7 +434,12 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
         float v = st[k];
 #pragma unroll
         for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 16);
-        if (r == 0 && k != 5 && (policy ? (k != 3) : (k == 3)) && v != 0.f) atomicAdd(&a.mstats[k], v * a.inv_B);
+        if (r == 0 && (policy ? (k != 3) : (k == 3))) {
+          // partial rows: every workgroup owns a row, the weight-gradient kernel sums them in a fixed order
+          // (atomics from every workgroup to one 32-byte line serialise in L2, ~12 ns each)
+          if (a.mpart) a.mpart[(size_t)blockIdx.x * MPART_W + k] = v * a.inv_B;
+          else if (k != 5 && v != 0.f) atomicAdd(&a.mstats[k], v * a.inv_B);
+        }
       }
     }
   }
@@ -444,7 +449,8 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
   if (policy && a.head == 2 && threadIdx.x < a.A) {
     float s = 0.f;
     for (int r = 0; r < MLP_BM; ++r) s += s_red[r][threadIdx.x];
-    atomicAdd(&a.g_log_std[threadIdx.x], s);
+    if (a.mpart) a.mpart[(size_t)blockIdx.x * MPART_W + 8 + threadIdx.x] = s;
+    else atomicAdd(&a.g_log_std[threadIdx.x], s);
   }
   // ---- top layer dP: apply the head activation derivative (tanh applied above) and publish
   {
@@ -483,9 +489,32 @@ constexpr int WG_CHUNK = 32;   // loads per operand per lane per chunk (128 rows
 
 __global__ void __launch_bounds__(256) mlp_wgrad_kernel(WgradArgs a) {
   __shared__ float red[4][64][5];
+  __shared__ float s_glog[MLP_MAXA];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int split = blockIdx.x % a.nsplit;
   int item = blockIdx.x / a.nsplit;
+  if (blockIdx.x == 0 && a.mpart) {   // sum the train kernel's partial rows (fixed order: deterministic)
+    if (wave == 0) {
+      float v[MPART_W];
+#pragma unroll
+      for (int c = 0; c < MPART_W; ++c) v[c] = 0.f;
+      for (int row = lane; row < a.mpart_rows; row += 64) {
+#pragma unroll
+        for (int c = 0; c < MPART_W; ++c) v[c] += a.mpart[(size_t)row * MPART_W + c];
+      }
+#pragma unroll
+      for (int c = 0; c < MPART_W; ++c) v[c] = wave_sum(v[c]);
+      if (lane == 0) {
+        for (int k = 0; k < 8; ++k) a.mstats[k] += v[k];
+        for (int j = 0; j < a.A; ++j) {
+          const float g = a.g_log_std ? a.g_log_std[j] + v[8 + j] : 0.f;
+          if (a.g_log_std) a.g_log_std[j] = g;
+          s_glog[j] = g;
+        }
+      }
+    }
+    __syncthreads();
+  }
   if (blockIdx.x == 0 && threadIdx.x == 0 && a.stats) {   // publish (and reset) the fused kernel's statistics
     float m[8];
     for (int k = 0; k < 8; ++k) m[k] = a.mstats[k];
@@ -577,7 +606,8 @@ __global__ void __launch_bounds__(256) mlp_wgrad_kernel(WgradArgs a) {
     }
   }
   if (a.nsplit == 1 && a.parts[t]) {
-    if (t == 0 && local_item == 0 && a.g_log_std && lane < a.A) ss += clipsq(a.g_log_std[lane], c);
+    if (t == 0 && local_item == 0 && a.g_log_std && lane < a.A)
+      ss += clipsq(a.mpart ? s_glog[lane] : a.g_log_std[lane], c);
     ss = wave_sum(ss);
     if (lane == 0) a.parts[t][local_item] = ss;
     if (local_item == 0)   // unused slots are zero: the optimiser sums all MLP_PARTS in a fixed order
@@ -601,6 +631,187 @@ __global__ void __launch_bounds__(256) mlp_tshadow_kernel(const MlpTower* __rest
       }
       e -= K * N;
     }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------ fused rollout
+// mlp_rollout_kernel: the whole T-step rollout of the MuJoCo-shaped linear bank in ONE launch (SURVEY §7.5 item 1,
+// "a persistent rollout kernel for the MLP configs"). One workgroup owns 16 envs for all T steps:
+//   actor forward (layer_fwd; the transposed weight shadows stay hot in this CU's L2 across steps) -> Gaussian sample /
+//   log-prob / entropy (the mode-0 head of mlp_fwd_kernel, same RNG keys) -> env step by 32-lane groups (the
+//   arithmetic of env_classic.hip linear_step_kernel, fma contraction off) -> frame-stack push straight into the LDS
+//   observation tile of the next step (double-buffered).
+// Env state, step counters and episode returns live in LDS for the whole rollout (read once, written back once); the
+// observation slab, actions, log-probs, entropies, rewards and done flags stream out. The critic's values of all
+// (T+1)*N observations are one batched mlp_fwd launch afterwards (ops/mlp.py), off this serial chain.
+constexpr int LIN_OBS = 17, LIN_ACT = 6, LIN_LANES = 32;
+
+__device__ __forceinline__ float lin_row(const float* s, const float* av, const float* sA, const float* sB, int r,
+                                         float nz) {
+#pragma clang fp contract(off)
+  float acc = 0.f, acc2 = 0.f;
+  for (int c = 0; c < LIN_OBS; ++c) acc += s[c] * sA[r * LIN_OBS + c];
+  for (int c = 0; c < LIN_ACT; ++c) acc2 += av[c] * sB[r * LIN_ACT + c];
+  return acc + acc2 + (nz - 0.5f) * 0.02f;
+}
+__device__ __forceinline__ float lin_asq(const float* av) {
+#pragma clang fp contract(off)
+  float asq = 0.f;
+  for (int j = 0; j < LIN_ACT; ++j) asq += av[j] * av[j];
+  return asq;
+}
+__device__ __forceinline__ float lin_reward(float y8, float asq) {
+#pragma clang fp contract(off)
+  return y8 - 0.1f * asq;
+}
+__device__ __forceinline__ float lin_reset(float u) {
+#pragma clang fp contract(off)
+  return (u - 0.5f) * 0.2f;
+}
+
+__global__ void __launch_bounds__(MLP_THREADS) mlp_rollout_kernel(RolloutArgs a) {
+  extern __shared__ float sm[];
+  __shared__ int64_t s_tg[MLP_BM];
+  __shared__ int s_t[MLP_BM];
+  __shared__ float s_er[MLP_BM];
+  const MlpTower& T = a.tw[0];
+  const int nl = (int)T.nl;
+  const int row0 = blockIdx.x * MLP_BM;
+  const int rows = min(MLP_BM, a.N - row0);
+  const int tid = threadIdx.x;
+  const int A = a.A, D = a.D;
+  const int ld0 = ld_of(D);
+  auto ldyf = [&](int l) { return ld_of((int)T.out[l]); };
+  auto Yp = [&](int l) {
+    int off = 2 * MLP_BM * ld0;
+    for (int j = 0; j < l; ++j) off += MLP_BM * ldyf(j);
+    return sm + off;
+  };
+  // LDS: obs tile x2 | Y_0 .. Y_{nl-1} | A | B | env state [16][17] | actions [16][16]
+  float* sA = Yp(nl);
+  float* sB = sA + LIN_OBS * LIN_OBS;
+  float* s_state = sB + LIN_OBS * LIN_ACT;
+  float* s_act = s_state + MLP_BM * LIN_OBS;
+  for (int e = tid; e < 2 * MLP_BM * ld0; e += MLP_THREADS) {   // step-0 tile (+ a zeroed second buffer)
+    const int r = e / ld0, c = e - r * ld0;
+    float v = 0.f;
+    if (r < rows && c < D) v = a.obs[(size_t)(row0 + r) * D + c];
+    sm[e] = v;
+  }
+  for (int j = tid; j < LIN_OBS * LIN_OBS; j += MLP_THREADS) sA[j] = a.lin_A[j];
+  for (int j = tid; j < LIN_OBS * LIN_ACT; j += MLP_THREADS) sB[j] = a.lin_B[j];
+  for (int e = tid; e < MLP_BM * LIN_OBS; e += MLP_THREADS)
+    s_state[e] = e / LIN_OBS < rows ? a.state[(size_t)row0 * LIN_OBS + e] : 0.f;
+  for (int e = tid; e < MLP_BM * MLP_MAXA; e += MLP_THREADS) s_act[e] = 0.f;
+  if (tid < MLP_BM) {
+    const bool live = tid < rows;
+    s_tg[tid] = live ? a.tg[row0 + tid] : 0;
+    s_t[tid] = live ? a.t[row0 + tid] : 0;
+    s_er[tid] = live ? a.ep_ret[row0 + tid] : 0.f;
+  }
+  __syncthreads();
+  for (int step = 0; step < a.T; ++step) {
+    float* Xc = sm + (step & 1) * MLP_BM * ld0;
+    float* Xn = sm + ((step & 1) ^ 1) * MLP_BM * ld0;
+    // ---- actor forward
+    const float* X = Xc;
+    int ldx = ld0;
+    for (int l = 0; l < nl; ++l) {
+      float* Yl = Yp(l);
+      const int ldl = ldyf(l);
+      layer_fwd(X, ldx, (int)T.in[l], P_<const float>(T.Wt[l]), P_<const float>(T.b[l]), (int)T.out[l],
+                (int)T.act[l], Yl, ldl);
+      __syncthreads();
+      X = Yl;
+      ldx = ldl;
+    }
+    // ---- Gaussian head: one thread per env (mlp_fwd_kernel mode 0)
+    if (tid < MLP_BM) {
+      const int r = tid;
+      const bool live = r < rows;
+      const int i = row0 + r;
+      const float* Yo = X + r * ldx;
+      const int64_t key = live ? s_tg[r] * ((int64_t)1 << a.key_shift) + a.env_ids[i] : 0;
+      float lp = 0.f, H = 0.f;
+      for (int j = 0; j < A; ++j) {
+        const float ls = fminf(fmaxf(a.log_std[j], -2.5f), 2.5f);
+        const float mu = tanhf(Yo[j]) * a.ac_scale[j];
+        const float u1 = uniform_open(a.policy_seed, key, 2 * j), u2 = uniform_open(a.policy_seed, key, 2 * j + 1);
+        const float eps = sqrtf(-2.0f * logf(u1)) * cosf(TWO_PI * u2);
+        const float aj = mu + expf(ls) * eps;
+        const float zz = (aj - mu) * expf(-ls);
+        lp += -0.5f * zz * zz - ls - HALF_LOG_2PI;
+        H += 0.5f + HALF_LOG_2PI + ls;
+        s_act[r * MLP_MAXA + j] = aj;
+        if (live) a.act[((size_t)step * a.N + i) * A + j] = aj;
+      }
+      if (live) {
+        a.logp[(size_t)step * a.N + i] = lp;
+        a.ent[(size_t)step * a.N + i] = H;
+      }
+    }
+    __syncthreads();
+    // ---- env step: 32 lanes per env, lane r < 17 owns state row r (linear_step_kernel)
+    {
+      const int e = tid / LIN_LANES, r = tid % LIN_LANES;
+      const bool active = e < rows;
+      const bool owner = active && r == 0;
+      bool done = false;
+      float ret = 0.f, len = 0.f;
+      if (active) {
+        const int i = row0 + e;
+        float* s = s_state + e * LIN_OBS;
+        const int64_t tg = s_tg[e] + 1;
+        const uint32_t id = (uint32_t)a.env_ids[i], st = (uint32_t)tg;
+        float av[LIN_ACT];
+        for (int j = 0; j < LIN_ACT; ++j) av[j] = fminf(fmaxf(s_act[e * MLP_MAXA + j], -1.0f), 1.0f);
+        const float asq = lin_asq(av);
+        float y = 0.f;
+        if (r < LIN_OBS) y = lin_row(s, av, sA, sB, r, uniform01(a.env_seed, id, st, 300 + r));
+        // reward reads row 8 (lane 8 of the group); every lane of the group has read s before lane r rewrites s[r]
+        const float y8 = __shfl(y, (tid & 63 & ~(LIN_LANES - 1)) + 8, 64);
+        const float rew = lin_reward(y8, asq);
+        const int t = s_t[e] + 1;
+        const bool trunc = t >= a.max_steps;
+        done = trunc;
+        const float er = s_er[e] + rew;
+        ret = er;
+        len = (float)t;
+        if (done && r < LIN_OBS) y = lin_reset(uniform01(a.env_seed, id, st, 100 + r));
+        if (r < LIN_OBS) {
+          s[r] = y;
+          const int k = a.k;
+          const float* pv = Xc + e * ld0;
+          float* xo = Xn + e * ld0;
+          float* go = a.obs + ((size_t)(step + 1) * a.N + i) * D;
+          for (int f = 0; f < k - 1; ++f) {
+            const float v = done ? y : pv[(f + 1) * LIN_OBS + r];
+            xo[f * LIN_OBS + r] = v;
+            go[f * LIN_OBS + r] = v;
+          }
+          xo[(k - 1) * LIN_OBS + r] = y;
+          go[(k - 1) * LIN_OBS + r] = y;
+        }
+        if (owner) {
+          const size_t o = (size_t)step * a.N + i;
+          s_tg[e] = tg;
+          a.reward[o] = rew;
+          a.done[o] = done;
+          a.trunc[o] = trunc;
+          s_t[e] = done ? 0 : t;
+          s_er[e] = done ? 0.f : er;
+        }
+      }
+      add_ep_stats(a.ep_stats, owner, done, ret, len);
+    }
+    __syncthreads();
+  }
+  // ---- env bank write-back
+  for (int e = tid; e < rows * LIN_OBS; e += MLP_THREADS) a.state[(size_t)row0 * LIN_OBS + e] = s_state[e];
+  if (tid < rows) {
+    a.tg[row0 + tid] = s_tg[tid];
+    a.t[row0 + tid] = s_t[tid];
+    a.ep_ret[row0 + tid] = s_er[tid];
   }
 }
 
@@ -639,5 +850,21 @@ extern "C" hipError_t aca_mlp_wgrad(const WgradArgs* a, hipStream_t stream) {
 extern "C" hipError_t aca_mlp_tshadow(const MlpTower* tw, int ntw, int total, hipStream_t stream) {
   if (total <= 0) return hipSuccess;
   mlp_tshadow_kernel<<<(total + 255) / 256, 256, 0, stream>>>(tw, ntw, total);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t aca_mlp_rollout(const RolloutArgs* a, size_t lds, hipStream_t stream) {
+  if (a->N <= 0 || a->T <= 0) return hipSuccess;
+  if (!a->tw || a->head != 2 || a->A != LIN_ACT || a->k < 1 || a->D != LIN_OBS * a->k || a->D > MLP_MAXW)
+    return hipErrorInvalidValue;
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_rollout_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 140 * 1024) != hipSuccess)
+      return hipErrorInvalidValue;
+    attr = true;
+  }
+  if (lds > 140 * 1024) return hipErrorInvalidValue;
+  mlp_rollout_kernel<<<(a->N + MLP_BM - 1) / MLP_BM, MLP_THREADS, lds, stream>>>(*a);
   return hipGetLastError();
 }

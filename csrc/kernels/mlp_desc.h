@@ -6,6 +6,7 @@
 namespace aca {
 
 constexpr int MLP_MAXL = 5;
+constexpr int MPART_W = 24;   // per-workgroup partial row of the train kernel: 8 loss statistics + 16 log-std grads
 
 // Tower descriptor, device-resident (built once per engine and batch size by ops/mlp.py, every field 64-bit so the
 // host packs it as an int64 tensor). Read with uniform (scalar) loads; a by-value kernel argument indexed by a
@@ -45,6 +46,7 @@ struct MlpArgs {
   int ppo;
   float* g_log_std;
   float* mstats;              // [8] sums (atomics): pg, kl, ent, vloss, clipfrac, -, ratio
+  float* mpart;               // optional [ceil(B/16)][MPART_W]: per-workgroup partials instead of the atomics above
   float inv_B;
 };
 
@@ -55,9 +57,24 @@ struct WgradArgs {
   int nsplit;                 // > 1: the batch is split over waves, results added atomically (no sumsq)
   float* parts[2];            // sumsq slots per tower (null: none)
   float clip[2];              // element-wise clip applied before squaring (<= 0: none)
-  const float* g_log_std; int A;   // included in tower 0's first slot
+  float* g_log_std; int A;         // included in tower 0's first slot (the partial rows are added here)
   float* mstats; float* stats; const float* ent_coef; const float* kl_coef;
   int items[2];               // 16x16 tiles per tower (host-computed)
+  const float* mpart; int mpart_rows;   // the train kernel's partial rows (reduced here in a fixed order)
+};
+
+// Fused rollout of the MuJoCo-shaped linear bank (mlp_rollout_kernel): T steps of actor + Gaussian sample + env step.
+struct RolloutArgs {
+  const MlpTower* tw;         // tower 0 (actor) of the engine descriptor
+  int N, T, D, A, head, k;
+  const float* log_std; const float* ac_scale;
+  int key_shift; uint32_t policy_seed;
+  float* obs;                 // [T+1][N][D]: block 0 read, blocks 1..T written
+  float* act; float* logp; float* ent;        // [T][N][A], [T][N], [T][N]
+  float* reward; uint8_t* done; uint8_t* trunc;   // [T][N]
+  float* state; int32_t* t; int64_t* tg; float* ep_ret; float* ep_stats; const int64_t* env_ids;
+  const float* lin_A; const float* lin_B;
+  uint32_t env_seed; int max_steps;
 };
 
 }  // namespace aca

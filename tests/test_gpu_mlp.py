@@ -240,3 +240,41 @@ def test_optimizer_writes_transposed_shadows(cuda):
         tr.flat.data.mul_(0.5)
     tr.mlp.sync_shadow()
     check()
+
+
+@pytest.mark.parametrize("frames,num_envs", [(1, 20), (3, 37)])
+def test_fused_rollout_matches_per_step_launches(cuda, frames, num_envs):
+    """mlp_rollout_kernel (whole T-step rollout of the MuJoCo-shaped bank in one launch + one batched critic launch)
+    == T x (policy_step launch + env_step_linear launch) + value launch: same actions, log-probs, observations,
+    rewards, resets and env bank state (episode limit 7 so resets happen inside the rollout; partial 16-env tiles)."""
+    from actor_critic_algs_on_tensorflow_amd import preset
+    from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
+    kw = dict(num_envs=num_envs, n_steps=24, frames=frames, ppo_epochs=1, ppo_minibatches=2, device="cuda:0",
+              outdir=None, quiet=True, stdout_freq=0, save_every=0, cuda_graph=False)
+    trs = [ActorCriticTrainer(preset("mujoco_ppo_dp8", fused_rollout=f, **kw)) for f in (True, False)]
+    for tr in trs:
+        assert tr.mlp is not None and tr.mlp.supports_fused_rollout(tr.env)
+        tr.env.max_episode_steps = 7
+    for _ in range(2):   # second rollout starts from the written-back env bank
+        for tr in trs:
+            tr.collect()
+        torch.cuda.synchronize()
+        a, b = (tr.storage for tr in trs)
+        for name in ("obs", "actions", "logp", "entropy", "rewards", "dones", "truncated", "values"):
+            x, y = getattr(a, name), getattr(b, name)
+            assert torch.equal(x, y), (name, (x.float() - y.float()).abs().max().item())
+        ea, eb = (tr.env for tr in trs)
+        for name in ("state", "t", "tg", "ep_ret"):
+            assert torch.equal(getattr(ea, name), getattr(eb, name)), name
+        torch.testing.assert_close(ea.ep_stats, eb.ep_stats, rtol=1e-5, atol=1e-4)
+        assert int(a.dones.sum()) > 0
+        for tr in trs:
+            tr.storage.roll_over()
+
+
+def test_seg_stats_kernel_matches_reference(cuda):
+    """Per-variable mean / std / max / min (TensorBoard variable summaries) in one launch vs float64 torch."""
+    from actor_critic_algs_on_tensorflow_amd.ops.stats import seg_stats, seg_stats_ref
+    x = torch.randn(300000, device=cuda) * 3 + 1
+    segs = torch.tensor([[0, 1], [7, 100], [1000, 65536], [70000, 229999], [5, 3]], device=cuda)
+    torch.testing.assert_close(seg_stats(x, segs), seg_stats_ref(x, segs), rtol=1e-5, atol=1e-5)

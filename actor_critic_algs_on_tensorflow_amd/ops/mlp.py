@@ -215,18 +215,28 @@ class MLPEngine:
         return (isinstance(env, MujocoShapeVecEnv) and not self.discrete and self.A == LIN_ACT
                 and self.D == LIN_OBS * env.frame_stack)
 
-    def rollout_lds_bytes(self):
+    ROLLOUT_MAX_LDS = 152 * 1024
+
+    def rollout_lds_bytes(self, wlds):
+        """Dynamic LDS of mlp_rollout_kernel (layout in mlp.hip); ``wlds`` adds the staged actor weights + biases."""
         n = 2 * BM * _ld(self.D) + sum(BM * _ld(l.out_features) for l in self.towers[0])
         n += LIN_OBS * LIN_OBS + LIN_OBS * LIN_ACT + BM * LIN_OBS + BM * 16
+        if wlds:
+            n = (n + 3) // 4 * 4 + sum(l.out_features * _ld(l.in_features) + _ld(l.out_features) - 4
+                                       for l in self.towers[0])
         return 4 * n
 
-    def rollout_linear(self, env, st, key_shift, seed):
+    def rollout_weights_in_lds(self):
+        return self.rollout_lds_bytes(True) <= self.ROLLOUT_MAX_LDS
+
+    def rollout_linear(self, env, st, key_shift, seed, stamps=None):
         """T steps of policy + env for the whole bank in one launch, then V(s) of all (T+1) N observations in one
         critic launch. Bit-identical to T x (:meth:`policy_step` + ``env.step``) + :meth:`value`."""
         T, N = st.T, env.num_envs
         desc, _ = self.desc(None)
-        _native.require().mlp_rollout(desc, self.rollout_lds_bytes(), st.obs, st.actions, st.logp, st.entropy,
+        wlds = self.rollout_weights_in_lds()
+        _native.require().mlp_rollout(desc, self.rollout_lds_bytes(wlds), st.obs, st.actions, st.logp, st.entropy,
                                       st.rewards, st.dones, st.truncated, self.log_std, self.ac_scale, key_shift, seed,
                                       env.state, env.t, env.tg, env.ep_ret, env.ep_stats, env.env_ids, env.A, env.B,
-                                      env.seed, env.max_episode_steps, env.frame_stack)
+                                      env.seed, env.max_episode_steps, env.frame_stack, wlds, stamps)
         self.value(st.obs.view((T + 1) * N, -1), st.values.view(-1))

@@ -582,7 +582,8 @@ void mlp_wgrad(Tensor desc, int64_t ntw, int64_t B, int64_t nsplit, int64_t item
 void mlp_rollout(Tensor desc, int64_t lds, Tensor obs, Tensor act, Tensor logp, Tensor ent, Tensor reward,
                  Tensor done, Tensor trunc, Tensor log_std, Tensor ac_scale, int64_t key_shift, int64_t policy_seed,
                  Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, Tensor env_ids, Tensor lin_A,
-                 Tensor lin_B, int64_t env_seed, int64_t max_steps, int64_t k) {
+                 Tensor lin_B, int64_t env_seed, int64_t max_steps, int64_t k, bool wlds,
+                 c10::optional<Tensor> stamps) {
   need(desc, at::kLong, "desc");
   TORCH_CHECK(desc.numel() * 8 >= (int64_t)sizeof(aca::MlpTower), "mlp_rollout: desc too small");
   need(obs, at::kFloat, "obs");
@@ -633,6 +634,8 @@ void mlp_rollout(Tensor desc, int64_t lds, Tensor obs, Tensor act, Tensor logp, 
   a.lin_B = ptr<float>(lin_B);
   a.env_seed = (uint32_t)env_seed;
   a.max_steps = (int)max_steps;
+  a.wlds = wlds ? 1 : 0;
+  a.stamps = reinterpret_cast<int64_t*>(stamps_ptr(stamps, 8));   // [16 steps][8 phases]
   check(aca_mlp_rollout(&a, (size_t)lds, cur_stream(obs)), "mlp_rollout");
 }
 
@@ -1048,7 +1051,7 @@ TORCH_LIBRARY(acamd, m) {
   m.def("mlp_rollout(Tensor desc, int lds, Tensor obs, Tensor act, Tensor logp, Tensor ent, Tensor reward, "
         "Tensor done, Tensor truncated, Tensor log_std, Tensor ac_scale, int key_shift, int policy_seed, "
         "Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, Tensor env_ids, Tensor lin_A, "
-        "Tensor lin_B, int env_seed, int max_steps, int k) -> ()");
+        "Tensor lin_B, int env_seed, int max_steps, int k, bool wlds, Tensor? stamps=None) -> ()");
   m.def("gemm(Tensor A, int lda, bool a_k, Tensor B, int ldb, bool b_k, Tensor C, int ldc, int out_mode, int M, "
         "int N, int K, float alpha, Tensor? bias, bool relu, Tensor? mask, int ldm, Tensor? colsum, int colsum_mod, "
         "int tile, int bk, int splits, Tensor? ws, Tensor? tickets, int[] ga, float ga_scale, int[] gb, "

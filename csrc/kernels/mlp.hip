@@ -285,6 +285,39 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
     __syncthreads();
   }
   const int tid = threadIdx.x;
+  // Gaussian policy head, phase A: one thread per (row, action component) -- mean, sample (rollout) or given action,
+  // the component's log-prob term (a per-row loop of tanh / hash / log / sqrt / cos / exp chains on 16 lanes would
+  // idle 7 of 8 waves; the per-row sums below keep the sequential order, so the results do not change)
+  __shared__ float s_hl[MLP_BM][MLP_MAXA], s_ht[MLP_BM][MLP_MAXA], s_hd[MLP_BM][MLP_MAXA];
+  __shared__ float s_g[MLP_BM];
+  const bool gauss = policy && a.head == 2;
+  if (gauss) {
+    if (tid < MLP_BM * MLP_MAXA) {
+      const int r = tid / MLP_MAXA, j = tid % MLP_MAXA;
+      if (j < a.A) {
+        const bool live = r < rows;
+        const int64_t grow = s_grow[r];
+        const float ls = fminf(fmaxf(a.log_std[j], -2.5f), 2.5f);
+        const float th = tanhf(Yo[r * ldo + j]);
+        const float mu = th * a.ac_scale[j];
+        float aj;
+        if (a.mode == 0) {
+          const int64_t key = live ? row_key(a, (int)grow) : 0;
+          const float u1 = uniform_open(a.seed, key, 2 * j), u2 = uniform_open(a.seed, key, 2 * j + 1);
+          const float eps = sqrtf(-2.0f * logf(u1)) * cosf(TWO_PI * u2);
+          aj = mu + expf(ls) * eps;
+          if (live) a.act_f_out[grow * a.A + j] = aj;
+        } else {
+          aj = live ? a.act_f_in[grow * a.A + j] : mu;
+        }
+        const float zz = (aj - mu) * expf(-ls);
+        s_hl[r][j] = -0.5f * zz * zz - ls - HALF_LOG_2PI;
+        s_ht[r][j] = th;
+        s_hd[r][j] = aj - mu;
+      }
+    }
+    __syncthreads();
+  }
   if (tid < MLP_BM) {
     const int r = tid;
     const bool live = r < rows;
@@ -309,68 +342,41 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
         dPtop[r * ldP] = a.vf_coef * a.inv_B * dv;
         st[3] = l2;
       }
-    } else if (a.head == 2) {   // diagonal Gaussian: mu = tanh(z) * scale
+    } else if (a.head == 2) {   // diagonal Gaussian: per-component terms computed above, fixed-order sums here
       const int A = a.A;
       float lp = 0.f, H = 0.f;
-      float mu[MLP_MAXA], act[MLP_MAXA], ls[MLP_MAXA];
-      const int64_t key = (a.mode == 0 && live) ? row_key(a, (int)grow) : 0;
       for (int j = 0; j < A; ++j) {
-        ls[j] = fminf(fmaxf(a.log_std[j], -2.5f), 2.5f);
-        mu[j] = tanhf(Yo[r * ldo + j]) * a.ac_scale[j];
-        float aj;
-        if (a.mode == 0) {
-          const float u1 = uniform_open(a.seed, key, 2 * j), u2 = uniform_open(a.seed, key, 2 * j + 1);
-          const float eps = sqrtf(-2.0f * logf(u1)) * cosf(TWO_PI * u2);
-          aj = mu[j] + expf(ls[j]) * eps;
-          if (live) a.act_f_out[grow * A + j] = aj;
-        } else {
-          aj = live ? a.act_f_in[grow * A + j] : mu[j];
-        }
-        act[j] = aj;
-        const float zz = (aj - mu[j]) * expf(-ls[j]);
-        lp += -0.5f * zz * zz - ls[j] - HALF_LOG_2PI;
-        H += 0.5f + HALF_LOG_2PI + ls[j];
+        lp += s_hl[r][j];
+        H += 0.5f + HALF_LOG_2PI + fminf(fmaxf(a.log_std[j], -2.5f), 2.5f);
       }
       if (live && a.mode != 2) {
         if (a.logp_out) a.logp_out[grow] = lp;
         if (a.ent_out) a.ent_out[grow] = H;
       }
-      if (a.mode == 2) {
-        float g = 0.f;
-        if (live) {
-          const float lo = a.logp_old[grow], adv = a.adv[grow];
-          const float beta = *a.kl_coef;
-          float dsurr;
-          if (a.ppo) {
-            const float ratio = expf(lp - lo);
-            const float s1 = ratio * adv;
-            const float rc = fminf(fmaxf(ratio, 1.f - a.ppo_clip), 1.f + a.ppo_clip);
-            const float s2 = rc * adv;
-            dsurr = (s1 <= s2) ? ratio * adv : 0.f;
-            st[0] = -fminf(s1, s2);
-            st[4] = fabsf(ratio - 1.f) > a.ppo_clip ? 1.f : 0.f;
-            st[6] = ratio;
-          } else {
-            dsurr = adv;
-            st[0] = -adv * lp;
-            st[6] = 1.f;
-          }
-          st[1] = (lo - lp) * (lo - lp);
-          st[2] = H;
-          g = a.inv_B * (-dsurr - 2.f * beta * (lo - lp));
+      float g = 0.f;
+      if (a.mode == 2 && live) {
+        const float lo = a.logp_old[grow], adv = a.adv[grow];
+        const float beta = *a.kl_coef;
+        float dsurr;
+        if (a.ppo) {
+          const float ratio = expf(lp - lo);
+          const float s1 = ratio * adv;
+          const float rc = fminf(fmaxf(ratio, 1.f - a.ppo_clip), 1.f + a.ppo_clip);
+          const float s2 = rc * adv;
+          dsurr = (s1 <= s2) ? ratio * adv : 0.f;
+          st[0] = -fminf(s1, s2);
+          st[4] = fabsf(ratio - 1.f) > a.ppo_clip ? 1.f : 0.f;
+          st[6] = ratio;
+        } else {
+          dsurr = adv;
+          st[0] = -adv * lp;
+          st[6] = 1.f;
         }
-        const float ce = *a.ent_coef;
-        for (int j = 0; j < A; ++j) {
-          const float ivar = expf(-2.f * ls[j]);
-          const float d = act[j] - mu[j];
-          const float th = tanhf(Yo[r * ldo + j]);
-          const float dmu = g * d * ivar;
-          dPtop[r * ldP + j] = live ? dmu * a.ac_scale[j] * (1.f - th * th) : 0.f;
-          const float raw = a.log_std[j];
-          const bool inr = raw >= -2.5f && raw <= 2.5f;
-          s_red[r][j] = (live && inr) ? g * (d * d * ivar - 1.f) - ce * a.inv_B : 0.f;
-        }
+        st[1] = (lo - lp) * (lo - lp);
+        st[2] = H;
+        g = a.inv_B * (-dsurr - 2.f * beta * (lo - lp));
       }
+      s_g[r] = g;
     } else {   // categorical logits
       const int A = a.A;
       float z[MLP_MAXA];
@@ -445,6 +451,23 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
   }
   if (a.mode != 2) return;
   __syncthreads();
+  if (gauss) {   // phase C: d(loss)/d(pre-tanh mean) and the per-row log-std gradient terms, per component
+    if (tid < MLP_BM * MLP_MAXA) {
+      const int r = tid / MLP_MAXA, j = tid % MLP_MAXA;
+      if (j < a.A) {
+        const bool live = r < rows;
+        const float raw = a.log_std[j];
+        const float ls = fminf(fmaxf(raw, -2.5f), 2.5f);
+        const float ivar = expf(-2.f * ls);
+        const float d = s_hd[r][j], th = s_ht[r][j], g = s_g[r];
+        const float dmu = g * d * ivar;
+        dPtop[r * ldP + j] = live ? dmu * a.ac_scale[j] * (1.f - th * th) : 0.f;
+        const bool inr = raw >= -2.5f && raw <= 2.5f;
+        s_red[r][j] = (live && inr) ? g * (d * d * ivar - 1.f) - (*a.ent_coef) * a.inv_B : 0.f;
+      }
+    }
+    __syncthreads();
+  }
   // log-std gradient: column sums over the tile's rows, one atomic per column
   if (policy && a.head == 2 && threadIdx.x < a.A) {
     float s = 0.f;
@@ -669,11 +692,67 @@ __device__ __forceinline__ float lin_reset(float u) {
   return (u - 0.5f) * 0.2f;
 }
 
+// Y = act(X W + b) with the transposed weights W[N][ldw] and the bias in LDS (ldw = 16*NG + 4: consecutive output
+// columns land 4 banks apart, so a 16-byte fragment read is conflict-free). No global memory at all.
+template <int NG>
+__device__ void layer_fwd_lds_t(const float* __restrict__ X, int ldx, const float* __restrict__ W, int ldw,
+                                const float* __restrict__ bias, int N, int act, float* __restrict__ Y, int ldy) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 15, q = lane >> 4;
+  const int ntile = ngp2(N);
+  for (int tile = wave; tile < ntile; tile += MLP_THREADS / 64) {
+    const int c = tile * 16 + r;
+    const bool cok = c < N;
+    const int cc = cok ? c : N - 1;
+    const float* wrow = W + cc * ldw + 4 * q;
+    floatx4 bv[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) bv[g] = *reinterpret_cast<const floatx4*>(wrow + 16 * g);
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    const float* Xr = X + r * ldx + 4 * q;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      const float4 a4 = *reinterpret_cast<const float4*>(&Xr[16 * g]);
+      acc = mfma4(a4.x, bv[g][0], acc);
+      acc = mfma4(a4.y, bv[g][1], acc);
+      acc = mfma4(a4.z, bv[g][2], acc);
+      acc = mfma4(a4.w, bv[g][3], acc);
+    }
+    const float bb = bias[cc];
+    const float slope = act_slope(act);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) Y[(4 * q + i) * ldy + c] = cok ? act_fwd(acc[i] + bb, slope) : 0.f;
+  }
+}
+
+__device__ __forceinline__ void layer_fwd_lds(const float* X, int ldx, int K, const float* W, const float* bias, int N,
+                                              int act, float* Y, int ldy) {
+  const int ldw = 16 * ngp2(K) + 4;
+  switch (ngp2(K)) {
+    case 1: layer_fwd_lds_t<1>(X, ldx, W, ldw, bias, N, act, Y, ldy); break;
+    case 2: layer_fwd_lds_t<2>(X, ldx, W, ldw, bias, N, act, Y, ldy); break;
+    case 4: layer_fwd_lds_t<4>(X, ldx, W, ldw, bias, N, act, Y, ldy); break;
+    case 8: layer_fwd_lds_t<8>(X, ldx, W, ldw, bias, N, act, Y, ldy); break;
+    default: layer_fwd_lds_t<16>(X, ldx, W, ldw, bias, N, act, Y, ldy); break;
+  }
+}
+
+// WLDS: the actor's weights and biases are staged in LDS once (the reference actor at D = 17 is ~120 KB, SURVEY
+// §2.4 K01), so the step loop issues no global loads at all. That matters beyond the load latency: on gfx9 global
+// stores count on vmcnt too, so every wait for a load issued after the previous step's stores (observations,
+// actions, rewards) would first drain those stores. The descriptor, head parameters and env ids are staged as well.
+// !WLDS (wider frame stacks): weights stream from the L2-resident transposed shadows.
+template <bool WLDS>
 __global__ void __launch_bounds__(MLP_THREADS) mlp_rollout_kernel(RolloutArgs a) {
   extern __shared__ float sm[];
   __shared__ int64_t s_tg[MLP_BM];
+  __shared__ int64_t s_ids[MLP_BM];
   __shared__ int s_t[MLP_BM];
   __shared__ float s_er[MLP_BM];
+  __shared__ float s_ls[MLP_MAXA], s_sc[MLP_MAXA];
+  __shared__ float s_hl[MLP_BM * MLP_MAXA];
+  __shared__ int s_in[MLP_MAXL], s_out[MLP_MAXL], s_actc[MLP_MAXL];
+  __shared__ int64_t s_wt[MLP_MAXL], s_b[MLP_MAXL];
   const MlpTower& T = a.tw[0];
   const int nl = (int)T.nl;
   const int row0 = blockIdx.x * MLP_BM;
@@ -681,17 +760,61 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_rollout_kernel(RolloutArgs a)
   const int tid = threadIdx.x;
   const int A = a.A, D = a.D;
   const int ld0 = ld_of(D);
-  auto ldyf = [&](int l) { return ld_of((int)T.out[l]); };
+  if (tid < nl) {
+    s_in[tid] = (int)T.in[tid];
+    s_out[tid] = (int)T.out[tid];
+    s_actc[tid] = (int)T.act[tid];
+    s_wt[tid] = T.Wt[tid];
+    s_b[tid] = T.b[tid];
+  }
+  if (tid < MLP_MAXA) {
+    s_ls[tid] = tid < A ? fminf(fmaxf(a.log_std[tid], -2.5f), 2.5f) : 0.f;
+    s_sc[tid] = tid < A ? a.ac_scale[tid] : 0.f;
+  }
+  if (tid < MLP_BM) {
+    const bool live = tid < rows;
+    s_tg[tid] = live ? a.tg[row0 + tid] : 0;
+    s_ids[tid] = live ? a.env_ids[row0 + tid] : 0;
+    s_t[tid] = live ? a.t[row0 + tid] : 0;
+    s_er[tid] = live ? a.ep_ret[row0 + tid] : 0.f;
+  }
+  __syncthreads();
+  // diagnostics: 100 MHz stamps at phase boundaries (workgroup 0, wave 0 after the barrier), steps 0..15
+  auto stamp = [&](int step, int slot) {
+    if (a.stamps && blockIdx.x == 0 && tid == 0 && step < 16) a.stamps[step * 8 + slot] = __builtin_amdgcn_s_memrealtime();
+  };
+  auto ldyf = [&](int l) { return ld_of(s_out[l]); };
   auto Yp = [&](int l) {
     int off = 2 * MLP_BM * ld0;
     for (int j = 0; j < l; ++j) off += MLP_BM * ldyf(j);
     return sm + off;
   };
-  // LDS: obs tile x2 | Y_0 .. Y_{nl-1} | A | B | env state [16][17] | actions [16][16]
+  // LDS: obs tile x2 | Y_0 .. Y_{nl-1} | A | B | env state [16][17] | actions [16][16] | (WLDS) W_l, b_l per layer
   float* sA = Yp(nl);
   float* sB = sA + LIN_OBS * LIN_OBS;
   float* s_state = sB + LIN_OBS * LIN_ACT;
   float* s_act = s_state + MLP_BM * LIN_OBS;
+  float* s_w0 = sm + (((s_act - sm) + MLP_BM * MLP_MAXA + 3) & ~3);   // 16-byte aligned (b128 reads)
+  auto Wl = [&](int l) {
+    float* p = s_w0;
+    for (int j = 0; j < l; ++j) p += s_out[j] * (16 * ngp2(s_in[j]) + 4) + 16 * ngp2(s_out[j]);
+    return p;
+  };
+  if (WLDS) {   // W_l [out][16*ngp2(in) + 4] (from the zero-padded transposed shadow), then b_l [16*ngp2(out)]
+    for (int l = 0; l < nl; ++l) {
+      const int K4 = 4 * ngp2(s_in[l]), N = s_out[l], ldw = 16 * ngp2(s_in[l]) + 4;
+      float* w = Wl(l);
+      const __attribute__((address_space(1))) floatx4* src =
+          (const __attribute__((address_space(1))) floatx4*)P_<const float>(s_wt[l]);
+      for (int e = tid; e < N * K4; e += MLP_THREADS) {
+        const int c = e / K4, k4 = e - c * K4;
+        *reinterpret_cast<floatx4*>(w + c * ldw + 4 * k4) = src[e];
+      }
+      float* b = w + N * ldw;
+      gcf32* bsrc = P_<const float>(s_b[l]);
+      for (int e = tid; e < 16 * ngp2(N); e += MLP_THREADS) b[e] = e < N ? bsrc[e] : 0.f;
+    }
+  }
   for (int e = tid; e < 2 * MLP_BM * ld0; e += MLP_THREADS) {   // step-0 tile (+ a zeroed second buffer)
     const int r = e / ld0, c = e - r * ld0;
     float v = 0.f;
@@ -703,12 +826,6 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_rollout_kernel(RolloutArgs a)
   for (int e = tid; e < MLP_BM * LIN_OBS; e += MLP_THREADS)
     s_state[e] = e / LIN_OBS < rows ? a.state[(size_t)row0 * LIN_OBS + e] : 0.f;
   for (int e = tid; e < MLP_BM * MLP_MAXA; e += MLP_THREADS) s_act[e] = 0.f;
-  if (tid < MLP_BM) {
-    const bool live = tid < rows;
-    s_tg[tid] = live ? a.tg[row0 + tid] : 0;
-    s_t[tid] = live ? a.t[row0 + tid] : 0;
-    s_er[tid] = live ? a.ep_ret[row0 + tid] : 0.f;
-  }
   __syncthreads();
   for (int step = 0; step < a.T; ++step) {
     float* Xc = sm + (step & 1) * MLP_BM * ld0;
@@ -719,38 +836,49 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_rollout_kernel(RolloutArgs a)
     for (int l = 0; l < nl; ++l) {
       float* Yl = Yp(l);
       const int ldl = ldyf(l);
-      layer_fwd(X, ldx, (int)T.in[l], P_<const float>(T.Wt[l]), P_<const float>(T.b[l]), (int)T.out[l],
-                (int)T.act[l], Yl, ldl);
+      if (WLDS) {
+        const float* w = Wl(l);
+        layer_fwd_lds(X, ldx, s_in[l], w, w + s_out[l] * (16 * ngp2(s_in[l]) + 4), s_out[l], s_actc[l], Yl, ldl);
+      } else {
+        layer_fwd(X, ldx, s_in[l], P_<const float>(s_wt[l]), P_<const float>(s_b[l]), s_out[l], s_actc[l], Yl, ldl);
+      }
       __syncthreads();
+      stamp(step, l);
       X = Yl;
       ldx = ldl;
     }
-    // ---- Gaussian head: one thread per env (mlp_fwd_kernel mode 0)
-    if (tid < MLP_BM) {
-      const int r = tid;
-      const bool live = r < rows;
-      const int i = row0 + r;
-      const float* Yo = X + r * ldx;
-      const int64_t key = live ? s_tg[r] * ((int64_t)1 << a.key_shift) + a.env_ids[i] : 0;
-      float lp = 0.f, H = 0.f;
-      for (int j = 0; j < A; ++j) {
-        const float ls = fminf(fmaxf(a.log_std[j], -2.5f), 2.5f);
-        const float mu = tanhf(Yo[j]) * a.ac_scale[j];
+    // ---- Gaussian head, one thread per (env, action component): mean, Box-Muller sample and the component's
+    // log-prob term in parallel (a serial per-env loop of hash + log/sqrt/cos/tanh/exp chains on 16 lanes would
+    // leave 7 of 8 waves idle for most of the step), then fixed-order per-env sums: bit-identical to the
+    // one-thread-per-row head of mlp_fwd_kernel mode 0
+    if (tid < MLP_BM * MLP_MAXA) {
+      const int r = tid / MLP_MAXA, j = tid % MLP_MAXA;
+      if (j < A) {
+        const bool live = r < rows;
+        const float* Yo = X + r * ldx;
+        const int64_t key = live ? s_tg[r] * ((int64_t)1 << a.key_shift) + s_ids[r] : 0;
+        const float ls = s_ls[j];
+        const float mu = tanhf(Yo[j]) * s_sc[j];
         const float u1 = uniform_open(a.policy_seed, key, 2 * j), u2 = uniform_open(a.policy_seed, key, 2 * j + 1);
         const float eps = sqrtf(-2.0f * logf(u1)) * cosf(TWO_PI * u2);
         const float aj = mu + expf(ls) * eps;
         const float zz = (aj - mu) * expf(-ls);
-        lp += -0.5f * zz * zz - ls - HALF_LOG_2PI;
-        H += 0.5f + HALF_LOG_2PI + ls;
+        s_hl[r * MLP_MAXA + j] = -0.5f * zz * zz - ls - HALF_LOG_2PI;
         s_act[r * MLP_MAXA + j] = aj;
-        if (live) a.act[((size_t)step * a.N + i) * A + j] = aj;
-      }
-      if (live) {
-        a.logp[(size_t)step * a.N + i] = lp;
-        a.ent[(size_t)step * a.N + i] = H;
+        if (live) a.act[((size_t)step * a.N + row0 + r) * A + j] = aj;
       }
     }
     __syncthreads();
+    stamp(step, 5);
+    if (tid < rows) {
+      float lp = 0.f, H = 0.f;
+      for (int j = 0; j < A; ++j) {
+        lp += s_hl[tid * MLP_MAXA + j];
+        H += 0.5f + HALF_LOG_2PI + s_ls[j];
+      }
+      a.logp[(size_t)step * a.N + row0 + tid] = lp;
+      a.ent[(size_t)step * a.N + row0 + tid] = H;
+    }
     // ---- env step: 32 lanes per env, lane r < 17 owns state row r (linear_step_kernel)
     {
       const int e = tid / LIN_LANES, r = tid % LIN_LANES;
@@ -762,7 +890,7 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_rollout_kernel(RolloutArgs a)
         const int i = row0 + e;
         float* s = s_state + e * LIN_OBS;
         const int64_t tg = s_tg[e] + 1;
-        const uint32_t id = (uint32_t)a.env_ids[i], st = (uint32_t)tg;
+        const uint32_t id = (uint32_t)s_ids[e], st = (uint32_t)tg;
         float av[LIN_ACT];
         for (int j = 0; j < LIN_ACT; ++j) av[j] = fminf(fmaxf(s_act[e * MLP_MAXA + j], -1.0f), 1.0f);
         const float asq = lin_asq(av);
@@ -805,6 +933,7 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_rollout_kernel(RolloutArgs a)
       add_ep_stats(a.ep_stats, owner, done, ret, len);
     }
     __syncthreads();
+    stamp(step, 6);
   }
   // ---- env bank write-back
   for (int e = tid; e < rows * LIN_OBS; e += MLP_THREADS) a.state[(size_t)row0 * LIN_OBS + e] = s_state[e];
@@ -853,18 +982,24 @@ extern "C" hipError_t aca_mlp_tshadow(const MlpTower* tw, int ntw, int total, hi
   return hipGetLastError();
 }
 
+constexpr size_t ROLLOUT_MAX_LDS = 152 * 1024;   // + ~0.5 KB static: within the 160 KB of a CU
+
 extern "C" hipError_t aca_mlp_rollout(const RolloutArgs* a, size_t lds, hipStream_t stream) {
   if (a->N <= 0 || a->T <= 0) return hipSuccess;
   if (!a->tw || a->head != 2 || a->A != LIN_ACT || a->k < 1 || a->D != LIN_OBS * a->k || a->D > MLP_MAXW)
     return hipErrorInvalidValue;
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_rollout_kernel),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 140 * 1024) != hipSuccess)
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_rollout_kernel<true>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, ROLLOUT_MAX_LDS) != hipSuccess ||
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_rollout_kernel<false>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, ROLLOUT_MAX_LDS) != hipSuccess)
       return hipErrorInvalidValue;
     attr = true;
   }
-  if (lds > 140 * 1024) return hipErrorInvalidValue;
-  mlp_rollout_kernel<<<(a->N + MLP_BM - 1) / MLP_BM, MLP_THREADS, lds, stream>>>(*a);
+  if (lds > ROLLOUT_MAX_LDS) return hipErrorInvalidValue;
+  const dim3 grid((a->N + MLP_BM - 1) / MLP_BM);
+  if (a->wlds) mlp_rollout_kernel<true><<<grid, MLP_THREADS, lds, stream>>>(*a);
+  else mlp_rollout_kernel<false><<<grid, MLP_THREADS, lds, stream>>>(*a);
   return hipGetLastError();
 }

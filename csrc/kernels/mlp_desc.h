@@ -75,6 +75,8 @@ struct RolloutArgs {
   float* state; int32_t* t; int64_t* tg; float* ep_ret; float* ep_stats; const int64_t* env_ids;
   const float* lin_A; const float* lin_B;
   uint32_t env_seed; int max_steps;
+  int wlds;                   // actor weights staged in LDS (host decides from the LDS budget)
+  int64_t* stamps;            // optional diagnostics: s_memrealtime per phase of the first 16 steps (workgroup 0)
 };
 
 }  // namespace aca

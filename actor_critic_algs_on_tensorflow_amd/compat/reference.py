@@ -289,6 +289,44 @@ def test_process(env_id, random_seed, stack_frames, model_path, num_episodes, an
                     animate=animate)
 
 
+# ---- reference helper names, as plain tensor functions -------------------------------------
+SCALE = 0.1   # Basic_AC/policies.py:4
+
+
+def ID_FN(x):   # Basic_AC/policies.py:5 -- identity observation scaler
+    return x
+
+
+def lrelu(x, alpha=0.2):   # Basic_AC/policies.py:28-31: (1 - a) relu(x) + a x
+    from ..models.layers import lrelu as _lrelu
+    return _lrelu(x, alpha)
+
+
+def xavier(shape, generator=None):   # TF Xavier-uniform for a [in, out] kernel
+    from ..models.init import xavier_uniform_
+    return xavier_uniform_(torch.empty(*shape), generator=generator)
+
+
+def xav(shape, generator=None):   # Basic_AC/policies.py:6-7: SCALE * Xavier-uniform
+    from ..models.init import scaled_xavier_
+    return scaled_xavier_(torch.empty(*shape), scale=SCALE, generator=generator)
+
+
+def normalized_column_initializer(std=SCALE):   # A3C/policies.py:3-10: N(0,1) columns rescaled to L2 norm ``std``
+    from ..models.init import normalized_column_
+
+    def _init(shape, generator=None):
+        return normalized_column_(torch.empty(*shape), norm=std, generator=generator)
+    return _init
+
+
+def fancy_clip(grad, clip_value_min, clip_value_max):   # Basic_AC/policies.py:23-26: clip that passes None through
+    if grad is None:
+        return None
+    return torch.clamp(grad, clip_value_min, clip_value_max)
+
+
 __all__ = ["Actor", "Critic", "GymEnv", "rollout", "train_ciritic", "train_critic", "train_actor", "get_roll_params",
            "test_process", "make_actor_critic", "Framer", "PathAdv", "LinearSchedule", "Logger",
-           "var_accounted_for", "make_np"]
+           "var_accounted_for", "make_np", "SCALE", "ID_FN", "lrelu", "xavier", "xav",
+           "normalized_column_initializer", "fancy_clip"]

@@ -10,7 +10,13 @@ ap.add_argument("--updates", type=int, default=40)
 ap.add_argument("--marker", default="pong_step_kernel")
 ap.add_argument("--per-update", type=int, default=5)
 a = ap.parse_args()
-rows = list(csv.DictReader(open(a.trace)))
+if a.trace.endswith(".db"):   # rocprofv3 >= 7 default output (rocpd SQLite): same fields as the CSV kernel trace
+    import sqlite3
+    con = sqlite3.connect(a.trace)
+    rows = [{"Kernel_Name": n, "Start_Timestamp": s, "End_Timestamp": e}
+            for n, s, e in con.execute("select name, start, end from kernels")]
+else:
+    rows = list(csv.DictReader(open(a.trace)))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 marks = [i for i, r in enumerate(rows) if a.marker in r["Kernel_Name"]]
 need = a.updates * a.per_update

@@ -232,3 +232,21 @@ def test_sampling_distributions():
     mu = torch.zeros(100000, 1)
     act, _, _ = D.gaussian_sample_ref(mu, torch.tensor([math.log(2.0)]), keys, 7)
     assert abs(act.mean()) < 0.03 and abs(act.std() - 2.0) < 0.03
+
+
+def test_reference_helper_names():
+    """C13/C14 helpers under their reference names: lrelu, xav/xavier bounds, column-normalised init, fancy_clip."""
+    import torch
+    from actor_critic_algs_on_tensorflow_amd.compat import reference as R
+    x = torch.tensor([-2.0, 0.0, 3.0])
+    assert torch.allclose(R.lrelu(x), torch.tensor([-0.4, 0.0, 3.0]))
+    assert R.ID_FN(x) is x and R.SCALE == 0.1
+    g = torch.Generator().manual_seed(0)
+    w = R.xavier((64, 128), generator=g)
+    lim = (6.0 / (64 + 128)) ** 0.5
+    assert w.abs().max() <= lim and w.abs().max() > 0.9 * lim
+    assert R.xav((64, 128), generator=g).abs().max() <= 0.1 * lim
+    c = R.normalized_column_initializer(0.1)((32, 8), generator=g)
+    assert torch.allclose(c.norm(dim=0), torch.full((8,), 0.1), atol=1e-6)
+    assert R.fancy_clip(None, -1, 1) is None
+    assert torch.equal(R.fancy_clip(torch.tensor([-3.0, 0.5, 2.0]), -1.0, 1.0), torch.tensor([-1.0, 0.5, 1.0]))

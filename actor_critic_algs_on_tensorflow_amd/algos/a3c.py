@@ -137,7 +137,7 @@ class A3CWorker:
         mpl, stop = ref.E.get_roll_params(cfg.env, "a3c")
         self.max_path_length = cfg.max_path_length or mpl
         self.ep_length_stop = cfg.ep_length_stop or stop
-        self.env = ref.GymEnv(cfg.env, seed=seed, max_episode_steps=self.max_path_length)
+        self.env = ref.GymEnv(cfg.env, seed=seed)   # env time limit kept; max_path_length bounds the loop
         self.framer = ref.Framer(cfg.frames)
         self.actor, self.critic = ref.make_actor_critic(self.env, cfg.frames, "a3c", seed=seed)
         self.actor.set_opt_param(new_lr=cfg.lr, new_beta=cfg.kl_coef, new_gamma=cfg.ent_coef)

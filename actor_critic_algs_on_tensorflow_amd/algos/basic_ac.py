@@ -34,7 +34,9 @@ class BasicACTrainer:
         mpl, stop = ref.E.get_roll_params(cfg.env, "basic")
         self.max_path_length = cfg.max_path_length or mpl
         self.ep_length_stop = cfg.ep_length_stop or stop
-        self.env = ref.GymEnv(cfg.env, seed=cfg.seed, max_episode_steps=self.max_path_length)
+        # the env keeps its own time limit (gym TimeLimit: 200 for Pendulum-v0); max_path_length only bounds the
+        # rollout loop (Basic_AC/run_AC.py:95,130-131), so a Basic Pendulum batch is 7 episodes of 200 steps
+        self.env = ref.GymEnv(cfg.env, seed=cfg.seed)
         self.framer = ref.Framer(cfg.frames)
         self.actor, self.critic = ref.make_actor_critic(self.env, cfg.frames, self.variant, seed=cfg.seed)
         self.actor.set_opt_param(new_lr=cfg.lr, new_beta=cfg.kl_coef, new_gamma=cfg.ent_coef)

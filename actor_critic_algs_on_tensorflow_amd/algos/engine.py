@@ -61,6 +61,7 @@ class _Bufs:
             self.dy3 = torch.empty(B * 49, 64, dtype=bf, device=dev)
             self.dy2 = torch.empty(B * 81, 64, dtype=bf, device=dev)
             self.dy1 = torch.empty(B * 400, 32, dtype=bf, device=dev)
+            self.biasp = torch.zeros(B, 160, dtype=torch.float32, device=dev)   # per-sample db3 | db2 | db1
             self.stats = torch.zeros(8, dtype=torch.float32, device=dev)
 
     def rows(self, r0, n):
@@ -92,6 +93,13 @@ class CNNEngine:
         self.fused_trunk_max_b = 4096 if fused_trunk_max_b is None else fused_trunk_max_b
         # rollout frame-stack shift inside the fused trunk (else the env kernel shifts); A/B switch for profiling
         self.trunk_shift = os.environ.get("ACA_TRUNK_SHIFT", "1") != "0"
+        # 1: seven row workgroups per env (224 CUs at 32 envs); 0: one workgroup per env
+        self.trunk_mode = int(os.environ.get("ACA_TRUNK_MODE", "1"))
+        # learner data-gradient chain dy3 -> dy2 -> dy1 as ONE per-sample kernel (cnn_trunk_bwd; bias gradients as
+        # per-sample partial rows reduced by the gradient finaliser) instead of two transposed-conv GEMMs
+        self.fused_bwd = implicit and os.environ.get("ACA_FUSED_BWD", "1") != "0"
+        self.fin_parts = torch.zeros(256, dtype=torch.float32, device=flat.data.device)
+        self._fin_words = {}
         # rollout fc product left as split-K partial planes, reduced by its consumer kernel (no in-launch fence)
         self.fc_parts = os.environ.get("ACA_FC_PARTS", "1") != "0"
         self._hpart = {}
@@ -165,7 +173,7 @@ class CNNEngine:
             if not self.trunk_shift:
                 shift_out = None
             G.cnn_trunk_fwd(obs, self.sW1, self.b1, self.sW2, self.b2, self.sW3, self.b3, b.y1, b.y2, b.y3,
-                            shift_out=shift_out)
+                            shift_out=shift_out, mode=self.trunk_mode)
             shifted = shift_out is not None
         elif self.implicit:
             G.gemm(obs, 0, True, self.sW1, 256, True, b.y1, 32, 1, B * 400, 32, 256, bias=self.b1, relu=True,
@@ -244,7 +252,7 @@ class CNNEngine:
         with torch.cuda.stream(side):   # fc weight gradient
             G.gemm(b.y3, 3136, False, b.dh, 512, False, self.gWfc, 512, 2, 3136, 512, B, workspace=ws2)
         G.gemm(b.dh, 512, True, self.sWfc, 512, True, b.dy3, 3136, 1, B, 3136, 512, mask=b.y3, ldm=3136,
-               colsum=self.gb3, colsum_mod=64, workspace=ws)
+               colsum=None if self.fused_bwd else self.gb3, colsum_mod=0 if self.fused_bwd else 64, workspace=ws)
         if stage == "tail":
             ev[5].record(side)
             main.wait_event(ev[5])
@@ -262,7 +270,11 @@ class CNNEngine:
                        gb=[2, B, 64, 9, 9, 3, 3, 1])
             else:
                 G.gemm(b.dy3, 64, False, b.col3, 576, False, self.gW3, 576, 2, 64, 576, B * 49, workspace=ws2)
-        if self.tconv_dgrad:   # dy2 = conv_transpose(dy3, W3) * (y2 > 0) as one gathered GEMM (+ colsum -> db2)
+        if self.fused_bwd:
+            # dy2 = tconv(dy3, W3) * (y2 > 0) and dy1 = tconv(dy2, W2) * (y1 > 0) in one per-sample launch; the
+            # bias-gradient partial rows (db3 | db2 | db1) are reduced by the finaliser
+            _native.require().cnn_trunk_bwd(b.dy3, self.sW3, b.y2, self.sW2, b.y1, b.dy2, b.dy1, b.biasp)
+        elif self.tconv_dgrad:   # dy2 = conv_transpose(dy3, W3) * (y2 > 0) as one gathered GEMM (+ colsum -> db2)
             G.gemm(b.dy3, 0, True, self.sW3, 0, False, b.dy2, 64, 1, B * 81, 64, 576, mask=b.y2, ldm=64,
                    colsum=self.gb2, workspace=ws, ga=[3, B, 64, 9, 9, 3, 3, 1], gb=[4, 1, 64, 1, 64, 3, 3, 1])
         else:
@@ -276,7 +288,9 @@ class CNNEngine:
                        gb=[2, B, 32, 20, 20, 4, 4, 2])
             else:
                 G.gemm(b.dy2, 64, False, b.col2, 512, False, self.gW2, 512, 2, 64, 512, B * 81, workspace=ws2)
-        if self.tconv_dgrad:   # dy1 = conv_transpose(dy2, W2) * (y1 > 0) (+ colsum -> db1)
+        if self.fused_bwd:
+            pass
+        elif self.tconv_dgrad:   # dy1 = conv_transpose(dy2, W2) * (y1 > 0) (+ colsum -> db1)
             # stride 2: sub-pixel form -- rows grouped by stride phase, only the 2x2 taps on each phase's grid
             G.gemm(b.dy2, 0, True, self.sW2, 0, False, b.dy1, 32, 1, B * 400, 32, 256, mask=b.y1, ldm=32,
                    colsum=self.gb1, workspace=ws, ga=[5, B, 64, 20, 20, 4, 4, 2], gb=[6, 1, 64, 1, 32, 4, 4, 2])
@@ -291,6 +305,35 @@ class CNNEngine:
             G.gemm(b.dy1, 32, False, b.col1, 256, False, self.gW1, 256, 2, 32, 256, B * 400, workspace=ws)
         ev[4].record(side)
         main.wait_event(ev[4])
+        if self.fused_bwd or self.want_parts:
+            self.finalize(b)
+
+    # ------------------------------------------------------------------------------------------------ finaliser
+    want_parts = False   # set by the trainer when the optimiser may take the finaliser's sum-of-squares partials
+
+    def finalize(self, b: _Bufs):
+        """One launch after the backward (``grad_finalize``): reduces the per-sample conv bias-gradient rows
+        (fused backward) into the slab and, with ``want_parts``, writes the global-norm partials of the whole
+        gradient (``fin_parts``) so the optimiser needs no sum-of-squares pass."""
+        key = (b.B, self.want_parts, self.fused_bwd)
+        words = self._fin_words.get(key)
+        if words is None:
+            segs = []
+            flat = self.flat
+            bias_src = {}
+            if self.fused_bwd:
+                bp = b.biasp.data_ptr()
+                bias_src = {self.gb3.data_ptr(): bp, self.gb2.data_ptr(): bp + 64 * 4, self.gb1.data_ptr(): bp + 128 * 4}
+            for p, off in zip(flat.params, flat.offsets):
+                g = flat.grad[off:off + p.numel()]
+                src = bias_src.get(g.data_ptr())
+                if src is not None:
+                    segs.append([g.data_ptr(), src, g.numel(), 160, b.B, 0])
+                elif self.want_parts:
+                    segs.append([g.data_ptr(), 0, g.numel(), 0, 0, 0])
+            words = torch.tensor(segs, dtype=torch.int64)
+            self._fin_words[key] = words
+        _native.require().grad_finalize(words, self.fin_parts)
 
     @staticmethod
     def dcol3(b):   # only the col2im data-gradient path materialises the column gradients

@@ -100,11 +100,19 @@ class ActorCriticTrainer:
                 opt.grad_mul = dp.grad_mul   # the all-reduce leaves the sum; the update kernel averages on read
             self.opts[g] = opt
         self.actor_opt = self.opts.get("actor", self.opts.get("shared"))
+        if (self.engine is not None and dp is None and len(self.opts) == 1
+                and all(o.clip_value is None for o in self.opts.values())):
+            # the engine's gradient finaliser writes the global-norm partials: no separate sum-of-squares pass
+            self.engine.want_parts = True
+            for o in self.opts.values():
+                o.ext_parts = self.engine.fin_parts
         T, N = cfg.n_steps, self.env.num_envs
         act_shape = () if self.env.is_discrete else tuple(self.env.action_space.shape)
         act_dtype = torch.int32 if self.env.is_discrete else torch.float32
         self.storage = RolloutStorage(T, N, self.env.obs_shape, self.env.obs_dtype, act_shape, act_dtype,
                                       self.device)
+        if cfg.bootstrap_on_timeout:
+            self.env.keep_final_obs = True   # the torch env step keeps the pre-reset observation (envs/base.py)
         self.env.reset(out=self.storage.obs[0])
         dev = self.device
         self.ent_coef = torch.tensor(cfg.ent_coef, device=dev)
@@ -140,7 +148,11 @@ class ActorCriticTrainer:
         """The hand-written HIP engine runs the CNN family on GPU (``engine="auto"|"native"``)."""
         from ..models.policy import CNNActorCritic
         eng = self.cfg.engine
-        if eng == "torch" or self.device.type != "cuda" or not isinstance(self.model, CNNActorCritic):
+        if self.cfg.bootstrap_on_timeout and eng == "native":
+            raise ValueError("bootstrap_on_timeout needs the terminal observation of truncated episodes, which the "
+                             "native env/rollout kernels do not keep: use engine='torch'")
+        if eng == "torch" or self.cfg.bootstrap_on_timeout or self.device.type != "cuda" or \
+                not isinstance(self.model, CNNActorCritic):
             if eng == "native":
                 raise ValueError("engine='native' needs a CNN model on a GPU")
             return False
@@ -150,7 +162,8 @@ class ActorCriticTrainer:
     def _want_native_mlp(self):
         """The fused MLP engine (``ops/mlp.py``) runs the reference's MLP actor/critic on GPU."""
         from ..models.policy import MLPActorCritic
-        if self.cfg.engine == "torch" or self.device.type != "cuda" or not isinstance(self.model, MLPActorCritic):
+        if self.cfg.engine == "torch" or self.cfg.bootstrap_on_timeout or self.device.type != "cuda" or \
+                not isinstance(self.model, MLPActorCritic):
             return False
         if self.model.actor.ac_dim > 16 or self.env.obs_dtype != torch.float32 or len(self.env.obs_shape) != 1:
             if self.cfg.engine == "native":
@@ -180,6 +193,12 @@ class ActorCriticTrainer:
             st.values[t].copy_(v)
             env.step(a, prev_obs=obs_t, obs_out=st.obs[t + 1], reward_out=st.rewards[t], done_out=st.dones[t],
                      trunc_out=st.truncated[t])
+            if self.cfg.bootstrap_on_timeout:
+                # a time-limit cut stays an episode boundary (done = 1: nothing leaks into the next episode, whose
+                # reset observation already sits in obs[t+1]); the truncated step's reward gets gamma * V(terminal
+                # observation) -- the observation the auto-reset overwrote, kept by the bank in final_obs
+                vf = model.value(env.final_obs)
+                st.rewards[t].add_(self.cfg.gamma * vf * st.truncated[t].to(vf.dtype))
         st.values[st.T].copy_(model.value(st.obs[st.T]))
 
     @torch.no_grad()
@@ -246,9 +265,7 @@ class ActorCriticTrainer:
         if self._fused_returns():
             return None, None
         cfg, st = self.cfg, self.storage
-        dones = st.dones
-        if cfg.bootstrap_on_timeout:
-            dones = dones & (1 - st.truncated)
+        dones = st.dones   # bootstrap_on_timeout: the bootstrap is already in the truncated step's reward (collect)
         if cfg.returns == "gae":
             ret, adv = R.gae(st.rewards, st.values, dones, cfg.gamma, cfg.gae_lambda)
         else:
@@ -651,17 +668,18 @@ class ActorCriticTrainer:
 
     def step(self):
         """One update (graph replay when captured)."""
-        if self.reg_sched is not None:
-            e, k = self.reg_sched.entropy_coef(self.iteration), self.reg_sched.kl_coef(self.iteration)
-            if e is not None:
-                self.ent_coef.fill_(e)
-            if k is not None:
-                self.kl_coef.fill_(k)
         if self.graph is not None:
             with self.timer.phase("update_graph"):
                 self._replay()
         else:
             self.update_body()
+        if self.reg_sched is not None:
+            # after update i, as the reference (Basic_AC/run_AC.py:268-275): a new coefficient acts from i + 1 on
+            e, k = self.reg_sched.entropy_coef(self.iteration), self.reg_sched.kl_coef(self.iteration)
+            if e is not None:
+                self.ent_coef.fill_(e)
+            if k is not None:
+                self.kl_coef.fill_(k)
         self.iteration += 1
         self.env_steps += self.cfg.n_steps * self.env.num_envs * self.world
 

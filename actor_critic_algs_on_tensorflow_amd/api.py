@@ -151,8 +151,7 @@ def evaluate(model_path, env_id, num_episodes=3, seed=12321, frames=1, animate=F
     mpl, _ = E.get_roll_params(env_id, "a3c" if (variant or "a3c") == "a3c" else "basic")
     if max_path_length is not None:
         mpl = max_path_length
-    env.max_episode_steps = mpl
-    rewards = []
+    rewards = []   # the env keeps its own time limit; mpl only bounds the loop (rollout(), run_AC.py:95)
     obs = env.reset().clone()
     for i in range(num_episodes):
         total, length = 0.0, 0
@@ -165,7 +164,7 @@ def evaluate(model_path, env_id, num_episodes=3, seed=12321, frames=1, animate=F
             total += float(r[0])
             length += 1
             obs = obs_next.clone()
-            if bool(d[0]):
+            if bool(d[0]) or length >= mpl:
                 break
         rewards.append(total)
         if verbose:

@@ -71,7 +71,7 @@ class GymEnv:
 def get_roll_params(env_id, variant="basic", seed=0):
     """-> (env, max_path_length, ep_length_stop) (``Basic_AC/run_AC.py:124-136``, ``A3C/process.py:100-109``)."""
     mpl, stop = E.get_roll_params(env_id, variant)
-    env = GymEnv(env_id, seed=seed, max_episode_steps=mpl)
+    env = GymEnv(env_id, seed=seed)   # env time limit kept; mpl only bounds the rollout loop
     print('\nMAX PATH LENGTH, EP LENGTH STEP: {}, {}\n'.format(mpl, stop))
     return env, mpl, stop
 

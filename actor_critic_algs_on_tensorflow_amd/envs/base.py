@@ -140,7 +140,7 @@ class VecEnv:
         trunc = self.truncated if trunc_out is None else trunc_out
         if prev.data_ptr() == out.data_ptr():
             prev = prev.clone()   # the kernels read the old stack while writing the new one
-        if _native.use_native(self.state):
+        if _native.use_native(self.state) and not self.keep_final_obs:   # the kernels keep no terminal obs
             self._native_step(actions, prev, out, rew, done, trunc)
         else:
             self._torch_step(actions, prev, out)

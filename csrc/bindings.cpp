@@ -79,6 +79,12 @@ hipError_t aca_ac_loss(const float*, int64_t, const float*, int64_t, const int32
 hipError_t aca_cnn_trunk_fwd(const uint8_t*, const uint16_t*, const float*, const uint16_t*, const float*,
                              const uint16_t*, const float*, uint16_t*, uint16_t*, uint16_t*, int, float, uint8_t*,
                              uint64_t*, hipStream_t);
+hipError_t aca_grad_finalize(const int64_t*, int, float*, hipStream_t);
+hipError_t aca_cnn_trunk_bwd(const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*,
+                             uint16_t*, uint16_t*, float*, int, uint64_t*, hipStream_t);
+hipError_t aca_cnn_trunk_rows(const uint8_t*, const uint16_t*, const float*, const uint16_t*, const float*,
+                              const uint16_t*, const float*, uint16_t*, uint16_t*, uint16_t*, int, float, uint8_t*,
+                              uint8_t*, uint64_t*, int, hipStream_t);
 }
 
 namespace {
@@ -843,9 +849,11 @@ int64_t gemm_effective_splits(int64_t K, int64_t bk, int64_t splits) {
 // Fused Nature-CNN trunk (conv1..conv3 of one env per workgroup, csrc/kernels/cnn_fused.hip). Shapes are fixed by
 // the kernel: obs [B, 4, 84, 84] uint8, W1 [32, 256] (OIHW), W2 [64, 512] / W3 [64, 576] (OHWI), y1 [B*400, 32],
 // y2 [B*81, 64], y3 [B*49, 64]; all 16-byte aligned (the kernel uses 16-byte vector accesses).
+// mode 0: one workgroup per env; mode 1: 7 row workgroups per env (cnn_trunk_rows_kernel). copy_out (mode 1 only):
+// also copy the whole observation there (rollover of the last observation into slot 0 of the next rollout).
 void cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, Tensor y1,
                    Tensor y2, Tensor y3, double scale, c10::optional<Tensor> shift_out,
-                   c10::optional<Tensor> stamps) {
+                   c10::optional<Tensor> stamps, int64_t mode, c10::optional<Tensor> copy_out) {
   need(obs, at::kByte, "obs");
   for (auto* w : {&W1, &W2, &W3, &y1, &y2, &y3}) need(*w, at::kBFloat16, "trunk bf16 operand");
   for (auto* b : {&b1, &b2, &b3}) need(*b, at::kFloat, "trunk bias");
@@ -866,10 +874,60 @@ void cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tenso
                 "cnn_trunk_fwd: shift_out must be a distinct, aligned [B, 4, 84, 84] uint8 buffer");
     so = ptr<uint8_t>(*shift_out);
   }
+  uint8_t* co = nullptr;
+  if (copy_out.has_value() && copy_out->defined()) {
+    TORCH_CHECK(mode >= 1, "cnn_trunk_fwd: copy_out needs a row-split mode");
+    need(*copy_out, at::kByte, "copy_out");
+    TORCH_CHECK(copy_out->numel() == obs.numel() && reinterpret_cast<uintptr_t>(copy_out->data_ptr()) % 16 == 0 &&
+                    copy_out->data_ptr() != obs.data_ptr(),
+                "cnn_trunk_fwd: copy_out must be a distinct, aligned [B, 4, 84, 84] uint8 buffer");
+    co = ptr<uint8_t>(*copy_out);
+  }
+  if (mode == 1 || mode == 2) {   // 2: the row kernel with its conv2/conv3 weight loads issued after conv1
+    check(aca_cnn_trunk_rows(ptr<uint8_t>(obs), ptr<uint16_t>(W1), ptr<float>(b1), ptr<uint16_t>(W2),
+                             ptr<float>(b2), ptr<uint16_t>(W3), ptr<float>(b3), ptr<uint16_t>(y1), ptr<uint16_t>(y2),
+                             ptr<uint16_t>(y3), (int)B, (float)scale, so, co, stamps_ptr(stamps, B * 7),
+                             mode == 2 ? 1 : 0, cur_stream(obs)),
+          "cnn_trunk_rows");
+    return;
+  }
+  TORCH_CHECK(mode == 0, "cnn_trunk_fwd: mode must be 0 or 1");
   check(aca_cnn_trunk_fwd(ptr<uint8_t>(obs), ptr<uint16_t>(W1), ptr<float>(b1), ptr<uint16_t>(W2), ptr<float>(b2),
                           ptr<uint16_t>(W3), ptr<float>(b3), ptr<uint16_t>(y1), ptr<uint16_t>(y2), ptr<uint16_t>(y3),
                           (int)B, (float)scale, so, stamps_ptr(stamps, B), cur_stream(obs)),
         "cnn_trunk_fwd");
+}
+
+// Fused data-gradient chain dy3 -> dy2 -> dy1 of the Nature-CNN trunk, one workgroup per sample
+// (cnn_fused.hip cnn_trunk_bwd_kernel): dy3 [B*49, 64] (already masked by y3 > 0), W3 [64, 576] / W2 [64, 512]
+// (OHWI bf16 shadows), masks y2 [B*81, 64] / y1 [B*400, 32]; writes dy2, dy1 (masked) and the per-sample bias
+// gradient partials biasp [B, 160] = (sum dy3 | sum dy2 | sum dy1).
+void cnn_trunk_bwd(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tensor dy2, Tensor dy1, Tensor biasp,
+                   c10::optional<Tensor> stamps) {
+  for (auto* t : {&dy3, &W3, &y2, &W2, &y1, &dy2, &dy1}) need(*t, at::kBFloat16, "trunk_bwd bf16 operand");
+  need(biasp, at::kFloat, "biasp");
+  TORCH_CHECK(dy3.numel() % (49 * 64) == 0, "cnn_trunk_bwd: dy3 must be [B*49, 64]");
+  const int64_t B = dy3.numel() / (49 * 64);
+  TORCH_CHECK(W3.numel() == 64 * 576 && W2.numel() == 64 * 512, "cnn_trunk_bwd: weights must be conv3 / conv2");
+  TORCH_CHECK(y2.numel() >= B * 81 * 64 && y1.numel() >= B * 400 * 32 && dy2.numel() >= B * 81 * 64 &&
+                  dy1.numel() >= B * 400 * 32 && biasp.numel() >= B * 160,
+              "cnn_trunk_bwd: buffers too small");
+  check(aca_cnn_trunk_bwd(ptr<uint16_t>(dy3), ptr<uint16_t>(W3), ptr<uint16_t>(y2), ptr<uint16_t>(W2),
+                          ptr<uint16_t>(y1), ptr<uint16_t>(dy2), ptr<uint16_t>(dy1), ptr<float>(biasp), (int)B,
+                          stamps_ptr(stamps, B), cur_stream(dy3)),
+        "cnn_trunk_bwd");
+}
+
+// Gradient finaliser (optim.hip grad_finalize_kernel): words = host int64 [nseg, 6] (dst, src, n, stride, S, 0)
+// device pointers; writes dst = sum of S planes for src != 0, and the SUMSQ_PARTS sum-of-squares partials.
+void grad_finalize(Tensor words, Tensor partial) {
+  TORCH_CHECK(words.device().is_cpu() && words.scalar_type() == at::kLong && words.dim() == 2 && words.size(1) == 6,
+              "grad_finalize: words must be a CPU int64 [nseg, 6] tensor");
+  need(partial, at::kFloat, "partial");
+  TORCH_CHECK(partial.numel() >= aca_sumsq_parts(), "grad_finalize: partial too small");
+  auto w = words.contiguous();
+  check(aca_grad_finalize(w.data_ptr<int64_t>(), (int)w.size(0), ptr<float>(partial), cur_stream(partial)),
+        "grad_finalize");
 }
 
 void im2col_u8(Tensor x, Tensor col, int64_t kh, int64_t kw, int64_t s, double scale) {
@@ -1060,7 +1118,11 @@ TORCH_LIBRARY(acamd, m) {
   m.def("seg_stats(Tensor x, Tensor segs, Tensor out) -> ()");
   m.def("gemm_effective_splits(int K, int bk, int splits) -> int", &gemm_effective_splits);
   m.def("cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, Tensor y1, "
-        "Tensor y2, Tensor y3, float scale, Tensor? shift_out=None, Tensor? stamps=None) -> ()");
+        "Tensor y2, Tensor y3, float scale, Tensor? shift_out=None, Tensor? stamps=None, int mode=0, "
+        "Tensor? copy_out=None) -> ()");
+  m.def("cnn_trunk_bwd(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tensor dy2, Tensor dy1, "
+        "Tensor biasp, Tensor? stamps=None) -> ()");
+  m.def("grad_finalize(Tensor words, Tensor partial) -> ()");
   m.def("im2col_u8(Tensor x, Tensor col, int kh, int kw, int s, float scale) -> ()");
   m.def("im2col_nhwc(Tensor x, Tensor col, int B, int H, int W, int C, int kh, int kw, int s) -> ()");
   m.def("col2im_nhwc(Tensor dcol, Tensor ymask, Tensor dx, Tensor? colsum, int B, int H, int W, int C, int kh, "
@@ -1102,6 +1164,8 @@ TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
   m.impl("gemm", &gemm);
   m.impl("cnn_trunk_fwd", &cnn_trunk_fwd);
   m.impl("fc_value", &fc_value);
+  m.impl("cnn_trunk_bwd", &cnn_trunk_bwd);
+  m.impl("grad_finalize", &grad_finalize);
   m.impl("im2col_u8", &im2col_u8);
   m.impl("im2col_nhwc", &im2col_nhwc);
   m.impl("col2im_nhwc", &col2im_nhwc);

@@ -225,6 +225,518 @@ __global__ void __launch_bounds__(T_THREADS) cnn_trunk_fwd_kernel(
   }
 }
 
+// ------------------------------------------------------------------------------------------------------------
+// Row-split trunk: 7 workgroups per env, workgroup r computes the receptive field of conv3 output row r only
+// (conv2 rows r..r+2, conv1 rows 2r..2r+7, input rows 8r..8r+35). The per-env kernel above keeps one CU busy per
+// env (32 of 256 CUs at the bench's 32 envs) and its layers run at one wave per SIMD; here 7x the CUs each do
+// ~1/3 of the work (the overlapping conv1/conv2 rows are recomputed: 56 conv1 rows for 20), so the step latency
+// falls to about a third. Each output row of y1 / y2 / y3 has exactly ONE owner workgroup that stores it (the
+// recomputed copies are bit-identical anyway: same operands, same MFMA order):
+//   y1 rows [ceil(20r/7), ceil(20(r+1)/7)), y2 row r (+ rows 7, 8 for r = 6), y3 row r,
+//   input rows [12r, 12r + 12) for the frame-stack outputs (shift_out: frames 1..3 -> 0..2 of the next
+//   observation; copy_out: all 4 frames, the rollover of the last observation into slot 0 of the next rollout).
+// ------------------------------------------------------------------------------------------------------------
+constexpr int TR_ROWS = 7;                 // workgroups per env (conv3 output rows)
+constexpr int TR_IN_ROWS = 36;             // staged input rows per frame
+constexpr int TR_C1_ROWS = 8;              // conv1 rows per workgroup
+constexpr int TR_C1_POS = TR_C1_ROWS * 20; // 160 = 10 M tiles
+constexpr int TR_C2_POS = 27;              // 3 conv2 rows x 9
+constexpr int TR_IN_ELEMS = 768 * 16;   // 4 x 36 x 84 = 12096 bf16, padded to 3 x 256 16-byte chunks x 2
+
+__device__ __forceinline__ int tr_y1_own_begin(int r) { return (20 * r + 6) / 7; }
+
+template <bool LATE_W>
+__global__ void __launch_bounds__(T_THREADS) cnn_trunk_rows_kernel(
+    const uint8_t* __restrict__ obs, const u16* __restrict__ W1, const float* __restrict__ b1,
+    const u16* __restrict__ W2, const float* __restrict__ b2, const u16* __restrict__ W3,
+    const float* __restrict__ b3, u16* __restrict__ y1g, u16* __restrict__ y2g, u16* __restrict__ y3g,
+    float scale, uint8_t* __restrict__ shift_out, uint8_t* __restrict__ copy_out, uint64_t* __restrict__ stamps) {
+  __shared__ __attribute__((aligned(16))) u16 s_in[TR_IN_ELEMS];
+  __shared__ __attribute__((aligned(16))) u16 s_w1[32 * W1_LD];
+  __shared__ __attribute__((aligned(16))) u16 s_y1[TR_C1_POS * Y1_LD];
+  __shared__ __attribute__((aligned(16))) u16 s_y2[TR_C2_POS * Y2_LD];
+
+  const int r = blockIdx.x % TR_ROWS, e = blockIdx.x / TR_ROWS;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int l16 = lane & 15, lg = lane >> 4;
+  const int in0 = 8 * r;                   // first staged input row
+  stamp(stamps, 0);
+
+  // ---------------------------------------------------------------- loads, oldest first in the order they are
+  // consumed (the vm counter retires in issue order): biases, the staged input rows, conv1 weight fragments, conv2
+  // weight fragments; conv3's are issued after the staging barrier. Weights go straight to registers (each B
+  // fragment is used by one wave only), the input rows through LDS (the im2col reads overlap).
+  const int n2 = wid * 16 + l16;
+  const float bias1a = b1[l16], bias1b = b1[16 + l16], bias2 = b2[n2], bias3 = b3[n2];
+  constexpr int FR_CH = TR_IN_ROWS * 84 / 16;            // 189 chunks per frame (rows of 84 B never cross frames)
+  constexpr int IN_CH = 4 * FR_CH;                        // 756
+  constexpr int IN_PER = (IN_CH + T_THREADS - 1) / T_THREADS;   // 3
+  uint4 vo[IN_PER];
+  {
+    const uint8_t* src = obs + (size_t)e * OBS_BYTES + (size_t)in0 * 84;
+#pragma unroll
+    for (int u = 0; u < IN_PER; ++u) {
+      const int i = min(tid + u * T_THREADS, IN_CH - 1);    // clamped: unconditional loads
+      const int f = i / FR_CH, c = i - f * FR_CH;
+      vo[u] = *reinterpret_cast<const uint4*>(src + (size_t)f * 84 * 84 + c * 16);
+    }
+  }
+  constexpr int W1_PER = 32 * 256 / 8 / T_THREADS;   // 4: W1 staged once through LDS (all 4 waves read it)
+  uint4 vw[W1_PER];
+#pragma unroll
+  for (int u = 0; u < W1_PER; ++u) vw[u] = reinterpret_cast<const uint4*>(W1)[tid + u * T_THREADS];
+  {
+    uint4* dst = reinterpret_cast<uint4*>(s_in);
+#pragma unroll
+    for (int u = 0; u < IN_PER; ++u) {   // branch-free (slots past IN_CH land in the pad): no block splits
+      const int i = tid + u * T_THREADS;
+      const uint2 a = u8x4_to_bf16(vo[u].x), b = u8x4_to_bf16(vo[u].y);
+      const uint2 c = u8x4_to_bf16(vo[u].z), d = u8x4_to_bf16(vo[u].w);
+      dst[2 * i] = make_uint4(a.x, a.y, b.x, b.y);
+      dst[2 * i + 1] = make_uint4(c.x, c.y, d.x, d.y);
+    }
+#pragma unroll
+    for (int u = 0; u < W1_PER; ++u) {
+      const int i = tid + u * T_THREADS, rr = i / 32, c8 = (i % 32) * 8;
+      *reinterpret_cast<uint4*>(s_w1 + rr * W1_LD + c8) = vw[u];
+    }
+    // frame-stack outputs of the owned input rows [12r, 12r + 12), straight from the registers above: the window
+    // starts 4r rows into the staged rows and spans 12 x 84 B = 63 whole 16-byte chunks (336r B = 21r chunks in),
+    // so every chunk is wholly owned or not
+    if (shift_out || copy_out) {
+#pragma unroll
+      for (int u = 0; u < IN_PER; ++u) {
+        const int i = tid + u * T_THREADS;
+        const int f = i / FR_CH, c = i - f * FR_CH;
+        const bool own = i < IN_CH && c >= 21 * r && c < 21 * r + 63;
+        const size_t goff = (size_t)e * OBS_BYTES + (size_t)in0 * 84 + c * 16;
+        if (own && copy_out) *reinterpret_cast<uint4*>(copy_out + (size_t)f * 84 * 84 + goff) = vo[u];
+        if (own && shift_out && f >= 1)
+          *reinterpret_cast<uint4*>(shift_out + (size_t)(f - 1) * 84 * 84 + goff) = vo[u];
+      }
+    }
+    __syncthreads();
+  }
+  stamp(stamps, 1);
+  // conv2 / conv3 weight fragments: issued now (the staging barrier waited for obs + W1 only), consumed after conv1
+  // (LATE_W: issued after conv1's MFMAs instead -- A/B variant, trunk mode 2)
+  bf16x8 bw2[16], bw3[18];
+  if constexpr (!LATE_W) {
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) bw2[ks] = *reinterpret_cast<const bf16x8*>(W2 + n2 * 512 + ks * 32 + lg * 8);
+#pragma unroll
+    for (int ks = 0; ks < 18; ++ks) bw3[ks] = *reinterpret_cast<const bf16x8*>(W3 + n2 * 576 + ks * 32 + lg * 8);
+  }
+
+  // ---------------------------------------------------------------- conv1: 160 positions (10 M tiles) x 32 x K 256
+  {
+    bf16x8 bw1[2][8];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks)
+        bw1[nt][ks] = *reinterpret_cast<const bf16x8*>(s_w1 + (nt * 16 + l16) * W1_LD + ks * 32 + lg * 8);
+    const float bias0 = bias1a, bias1 = bias1b;
+    // 10 M tiles over 4 waves (3, 3, 2, 2): a fixed trip count with a guard, no global stores in the loop (they
+    // would sit in the vm counter in front of the W3 fragment loads that conv2 waits for)
+#pragma unroll
+    for (int it = 0; it < 3; ++it) {
+      const int mt = wid + 4 * it;
+      if (mt >= TR_C1_POS / 16) break;
+      floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+      const int m = mt * 16 + l16;
+      const int oh = m / 20, ow = m - oh * 20;      // local conv1 row, column
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        const int k = ks * 32 + lg * 8;
+        const int c = k >> 6, i = (k >> 3) & 7;
+        const u16* p = s_in + (c * TR_IN_ROWS + oh * 4 + i) * 84 + ow * 4;
+        const uint2 lo = *reinterpret_cast<const uint2*>(p), hi = *reinterpret_cast<const uint2*>(p + 4);
+        const bf16x8 a = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw1[0][ks], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw1[1][ks], acc1, 0, 0, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = mt * 16 + lg * 4 + q;        // local position
+        const u16 v0 = f2bf(fmaxf(acc0[q] * scale + bias0, 0.f));
+        const u16 v1 = f2bf(fmaxf(acc1[q] * scale + bias1, 0.f));
+        s_y1[row * Y1_LD + l16] = v0;
+        s_y1[row * Y1_LD + 16 + l16] = v1;
+      }
+    }
+  }
+  if constexpr (LATE_W) {
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) bw2[ks] = *reinterpret_cast<const bf16x8*>(W2 + n2 * 512 + ks * 32 + lg * 8);
+#pragma unroll
+    for (int ks = 0; ks < 18; ++ks) bw3[ks] = *reinterpret_cast<const bf16x8*>(W3 + n2 * 576 + ks * 32 + lg * 8);
+  }
+  __syncthreads();
+  stamp(stamps, 2);
+  // ---------------------------------------------------------------- conv2: 27 positions (2 M tiles), N 64, K 512
+  {
+    const int n = n2;
+    const float bias = bias2;
+    floatx4 acc[2];
+    acc[0] = floatx4{0.f, 0.f, 0.f, 0.f};
+    acc[1] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) {
+      const int k = ks * 32 + lg * 8;   // (i, j, c0)
+      const int i = k >> 7, j = (k >> 5) & 3, c0 = k & 31;
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) {
+        const int m = min(mt * 16 + l16, TR_C2_POS - 1);
+        const int oh = m / 9, ow = m - oh * 9;     // local conv2 row (0..2), column
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(s_y1 + ((oh * 2 + i) * 20 + ow * 2 + j) * Y1_LD + c0);
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw2[ks], acc[mt], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = mt * 16 + lg * 4 + q;
+        if (row < TR_C2_POS) s_y2[row * Y2_LD + n] = f2bf(fmaxf(acc[mt][q] + bias, 0.f));
+      }
+    }
+  }
+  __syncthreads();
+  stamp(stamps, 3);
+  // ---------------------------------------------------------------- conv3: 7 positions (1 M tile), N 64, K 576
+  {
+    const int n = n2;
+    const float bias = bias3;
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    const int m = min(l16, 6);
+#pragma unroll
+    for (int ks = 0; ks < 18; ++ks) {
+      const int k = ks * 32 + lg * 8;
+      const int i = k / 192, j = (k >> 6) % 3, c0 = k & 63;
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(s_y2 + (i * 9 + m + j) * Y2_LD + c0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw3[ks], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = lg * 4 + q;
+      if (row < 7) y3g[((size_t)e * Y3_ROWS + r * 7 + row) * Y3_C + n] = f2bf(fmaxf(acc[q] + bias, 0.f));
+    }
+  }
+  // ---------------------------------------------------------------- owned y1 / y2 rows: LDS -> global, 16-byte rows
+  {
+    const int p1 = tr_y1_own_begin(r) * 20, p1e = tr_y1_own_begin(r + 1) * 20;   // owned conv1 pixels (global)
+    const int n1 = (p1e - p1) * 4;                                                // 16-byte chunks (4 per pixel)
+    for (int c = tid; c < n1; c += T_THREADS) {
+      const int px = p1 + (c >> 2), lp = px - 2 * r * 20, q = (c & 3) * 8;
+      *reinterpret_cast<uint4*>(y1g + ((size_t)e * Y1_ROWS + px) * Y1_C + q) =
+          *reinterpret_cast<const uint4*>(s_y1 + lp * Y1_LD + q);
+    }
+    const int n2c = ((r == TR_ROWS - 1) ? 27 : 9) * 8;   // y2 row r (and rows 7, 8 for the last workgroup)
+    if (tid < n2c) {
+      const int lp = tid >> 3, q = (tid & 7) * 8;
+      *reinterpret_cast<uint4*>(y2g + ((size_t)e * Y2_ROWS + r * 9 + lp) * Y2_C + q) =
+          *reinterpret_cast<const uint4*>(s_y2 + lp * Y2_LD + q);
+    }
+  }
+  if (stamps) {
+    stamp(stamps, 4);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp(stamps, 5);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// Fused data-gradient chain of the conv trunk, one workgroup per sample (learner backward):
+//   dy2 = conv_transpose(dy3, W3) * (y2 > 0)        M 81 positions, N 64, K 576 = (tap i j, o)
+//   dy1 = conv_transpose(dy2, W2) * (y1 > 0)        sub-pixel form: per output parity class (py, px) only the
+//                                                    2 x 2 taps on its grid, K 256 = (di, dj, o)
+// plus the per-sample bias-gradient partials  biasp[b] = [ sum_p dy3 | sum_p dy2 | sum_p dy1 ]  (64 | 64 | 32).
+// Both products are per sample (no reduction over the batch), so they run back to back out of LDS: dy3 lands in
+// a zero-bordered image (taps off the grid read zeros, no bounds tests), dy2 is written into a second zero-bordered
+// image that feeds dy1, and the weights are staged as B rows [k][n] read with the transposing ds_read_b64_tr_b16.
+// W2 is prefetched into registers while dy2 runs, so its staging costs no round trip. dy2 / dy1 leave through LDS
+// in 16-byte rows (the weight-gradient GEMMs read them); masks are applied in those passes. The bias partials
+// are summed in a fixed order (deterministic); the gradient finaliser reduces them over the batch.
+// Replaces two implicit transposed-conv GEMM launches (dy2: mode 3/4, dy1: sub-pixel mode 5/6) + their colsums.
+// ------------------------------------------------------------------------------------------------------------
+constexpr int BW_LD3 = 72;                  // W3 B-row stride (64 + 8 pad), also the image pixel stride
+constexpr int BW_LD2 = 40;                  // W2 B-row stride (32 + 8)
+constexpr int BW_P3 = 11;                   // dy3 image 7x7 + 2 zero rows/cols on each side
+constexpr int BW_P2 = 11;                   // dy2 image 9x9 + 1 zero row/col on each side
+constexpr int BW_RW = 576 * BW_LD3;         // >= 1024 * BW_LD2
+constexpr int BW_P3E = BW_P3 * BW_P3 * BW_LD3;
+constexpr int BW_M2E = 81 * 64;
+constexpr int BW_P2E = BW_P2 * BW_P2 * BW_LD3;
+static_assert(400 * 32 <= BW_P3E + BW_M2E, "dy1 staging aliases the dy3 image + y2 mask");
+static_assert(1024 * BW_LD2 <= BW_RW, "W2 rows fit the W3 region");
+
+// element e (0..7) of 8 packed bf16 as float, without taking the vector's address (that would go to scratch)
+__device__ __forceinline__ float bf_lane(const uint4& v, int e) {
+  const uint32_t w = e < 2 ? v.x : (e < 4 ? v.y : (e < 6 ? v.z : v.w));
+  return __uint_as_float((e & 1) ? (w & 0xFFFF0000u) : (w << 16));
+}
+__device__ __forceinline__ uint32_t mask_pair(uint32_t w, uint32_t m) {   // zero each bf16 of w whose mask is <= 0
+  const uint32_t lo = (__uint_as_float(m << 16) > 0.f) ? 0x0000FFFFu : 0u;
+  const uint32_t hi = (__uint_as_float(m & 0xFFFF0000u) > 0.f) ? 0xFFFF0000u : 0u;
+  return w & (lo | hi);
+}
+
+__device__ __forceinline__ bf16x8 tr_frag(const u16* rows, int ld, int col0, int lane) {
+  // B fragment (k = 8 (lane >> 4) + 0..7, n = col0 + lane & 15) from n-contiguous rows via two transposing reads
+  const int lr16 = lane & 15, lg = lane >> 4, q = lr16 >> 2, p = lr16 & 3;
+  const u16* p0 = rows + (lg * 8 + q) * ld + col0 + 4 * p;
+  const u16* p1 = rows + (lg * 8 + 4 + q) * ld + col0 + 4 * p;
+  typedef short short4x __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) short4x lds4;
+  const short4x lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(p0));
+  const short4x hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(p1));
+  const short8v v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// 8 waves (2 per SIMD: one wave per SIMD left every LDS read latency exposed); one workgroup per CU by LDS.
+constexpr int BW_T = 512;
+__global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_kernel(
+    const u16* __restrict__ dy3g, const u16* __restrict__ W3, const u16* __restrict__ y2g,
+    const u16* __restrict__ W2, const u16* __restrict__ y1g, u16* __restrict__ dy2g, u16* __restrict__ dy1g,
+    float* __restrict__ biasp, uint64_t* __restrict__ stamps) {
+  __shared__ __attribute__((aligned(16))) u16 s_w[BW_RW];
+  __shared__ __attribute__((aligned(16))) u16 s_p3m2[BW_P3E + BW_M2E];   // dy3 image + y2 mask; later dy1 staging
+  __shared__ __attribute__((aligned(16))) u16 s_p2[BW_P2E];
+  __shared__ float s_red[8 * 128 + 8 * 32];
+  u16* const s_p3 = s_p3m2;
+  u16* const s_m2 = s_p3m2 + BW_P3E;
+  u16* const s_d1 = s_p3m2;
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int l16 = lane & 15, lg = lane >> 4;
+  const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
+  stamp(stamps, 0);
+
+  // ---------------------------------------------------------------- loads: dy3 image, W3 rows, y2 mask; W2 + y1
+  // mask prefetched into registers (consumed in the dy1 phase)
+  {
+    constexpr int P3_CH = BW_P3 * BW_P3 * 9;                  // 1089 chunks (9 per 144-byte pixel)
+    constexpr int P3_PER = (P3_CH + BW_T - 1) / BW_T;          // 3
+    constexpr int W3_CH = 576 * 8, W3_PER = W3_CH / BW_T;      // 9
+    constexpr int M2_CH = 81 * 8;                              // 648
+    constexpr int M2_PER = (M2_CH + BW_T - 1) / BW_T;          // 2
+    uint4 vp[P3_PER], vw[W3_PER], vm[M2_PER];
+#pragma unroll
+    for (int u = 0; u < P3_PER; ++u) {
+      const int c = tid + u * BW_T;
+      const int px = c / 9, part = c - px * 9, pa = px / BW_P3, pb = px - pa * BW_P3;
+      const bool in = c < P3_CH && part < 8 && pa >= 2 && pa < 9 && pb >= 2 && pb < 9;
+      const int src = in ? ((b * 49 + (pa - 2) * 7 + (pb - 2)) * 64 + part * 8) : b * 49 * 64;
+      const uint4 v = *reinterpret_cast<const uint4*>(dy3g + src);
+      // per component: an aggregate select is lowered through scratch
+      vp[u] = make_uint4(in ? v.x : 0u, in ? v.y : 0u, in ? v.z : 0u, in ? v.w : 0u);
+    }
+#pragma unroll
+    for (int u = 0; u < W3_PER; ++u) {
+      // B row k = (i, j, o) <- W3[o][i][j][:] (64 contiguous channels = 8 chunks)
+      const int c = tid + u * BW_T, k = c >> 3, part = c & 7;
+      const int t = k >> 6, o = k & 63;
+      vw[u] = *reinterpret_cast<const uint4*>(W3 + o * 576 + t * 64 + part * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < M2_PER; ++u) {
+      const int c = min(tid + u * BW_T, M2_CH - 1);
+      vm[u] = *reinterpret_cast<const uint4*>(y2g + (size_t)b * 81 * 64 + c * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < P3_PER; ++u) {
+      const int c = tid + u * BW_T;
+      if (c < P3_CH) *reinterpret_cast<uint4*>(s_p3 + (c / 9) * BW_LD3 + (c % 9) * 8) = vp[u];
+    }
+#pragma unroll
+    for (int u = 0; u < W3_PER; ++u) {
+      const int c = tid + u * BW_T;
+      *reinterpret_cast<uint4*>(s_w + (c >> 3) * BW_LD3 + (c & 7) * 8) = vw[u];
+    }
+#pragma unroll
+    for (int u = 0; u < M2_PER; ++u) {
+      const int c = tid + u * BW_T;
+      if (c < M2_CH) *reinterpret_cast<uint4*>(s_m2 + c * 8) = vm[u];
+    }
+    // dy2 image: zero border and pad lanes; the interior is written by the dy2 epilogue
+    for (int c = tid; c < BW_P2 * BW_P2 * 9; c += BW_T) {
+      const int px = c / 9, part = c - px * 9, pa = px / BW_P2, pb = px - pa * BW_P2;
+      if (pa == 0 || pb == 0 || pa == BW_P2 - 1 || pb == BW_P2 - 1 || part == 8)
+        *reinterpret_cast<uint4*>(s_p2 + px * BW_LD3 + part * 8) = z4;
+    }
+  }
+  // held across the dy2 phase in named registers (hipcc left a uint4 array for this in scratch)
+  static_assert(64 * 512 / 8 / BW_T == 8, "W2 prefetch is written out for 8 chunks per thread");
+#define ACA_W2_LD(u) const uint4 vw2_##u = *reinterpret_cast<const uint4*>(W2 + (tid + (u) * BW_T) * 8);
+  ACA_W2_LD(0) ACA_W2_LD(1) ACA_W2_LD(2) ACA_W2_LD(3) ACA_W2_LD(4) ACA_W2_LD(5) ACA_W2_LD(6) ACA_W2_LD(7)
+#undef ACA_W2_LD
+  constexpr int M1_CH = 400 * 4, M1_PER = (M1_CH + BW_T - 1) / BW_T;   // 1600 -> 4
+  uint4 vm1[M1_PER];
+#pragma unroll
+  for (int u = 0; u < M1_PER; ++u) {
+    const int c = min(tid + u * BW_T, M1_CH - 1);
+    vm1[u] = *reinterpret_cast<const uint4*>(y1g + (size_t)b * 400 * 32 + c * 8);
+  }
+  __syncthreads();
+  stamp(stamps, 1);
+
+  // ---------------------------------------------------------------- dy2: wave -> (N tile wid % 4, M tiles 3 x half)
+  {
+    const int n0 = (wid & 3) * 16, mh = (wid >> 2) * 3;
+    floatx4 acc[3];
+#pragma unroll
+    for (int mt = 0; mt < 3; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 18; ++ks) {
+      const int kb = ks * 32 + lg * 8, t = kb >> 6, o0 = kb & 63, ti = t / 3, tj = t - ti * 3;
+      const bf16x8 bf = tr_frag(s_w + ks * 32 * BW_LD3, BW_LD3, n0, lane);
+#pragma unroll
+      for (int mt = 0; mt < 3; ++mt) {
+        const int m = min((mh + mt) * 16 + l16, 80);
+        const int a = m / 9, c = m - a * 9;
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(s_p3 + ((a - ti + 2) * BW_P3 + (c - tj + 2)) * BW_LD3 + o0);
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, acc[mt], 0, 0, 0);
+      }
+    }
+    const int n = n0 + l16;
+#pragma unroll
+    for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = (mh + mt) * 16 + lg * 4 + r;
+        if (m < 81) {
+          const int a = m / 9, c = m - a * 9;
+          const float v = bf2f(s_m2[m * 64 + n]) > 0.f ? acc[mt][r] : 0.f;
+          s_p2[((a + 1) * BW_P2 + (c + 1)) * BW_LD3 + n] = f2bf(v);
+        }
+      }
+  }
+  // db3 partial from the dy3 image (before it is overwritten): thread -> channel group tid % 8, fixed order
+  float part3[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int c = tid; c < 49 * 8; c += BW_T) {
+    const int px = c >> 3, g = c & 7, pa = px / 7, pb = px - pa * 7;
+    const uint4 v = *reinterpret_cast<const uint4*>(s_p3 + ((pa + 2) * BW_P3 + (pb + 2)) * BW_LD3 + g * 8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) part3[e] += bf_lane(v, e);
+  }
+  __syncthreads();   // dy2 image complete; the W3 rows and the dy3 image are dead
+  stamp(stamps, 2);
+
+  // ---------------------------------------------------------------- W2 rows in; dy2 out (16-byte rows) + db2
+  // W2 chunk c -> B row (tap, o): o = c / 64, tap = (c / 4) % 16, part = c % 4
+#define ACA_W2_ST(u)                                                                                  \
+  {                                                                                                   \
+    const int c = tid + (u) * BW_T, o = c >> 6, t = (c >> 2) & 15, part = c & 3;                     \
+    *reinterpret_cast<uint4*>(s_w + (t * 64 + o) * BW_LD2 + part * 8) = vw2_##u;                     \
+  }
+  ACA_W2_ST(0) ACA_W2_ST(1) ACA_W2_ST(2) ACA_W2_ST(3) ACA_W2_ST(4) ACA_W2_ST(5) ACA_W2_ST(6) ACA_W2_ST(7)
+#undef ACA_W2_ST
+  float part2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int c = tid; c < 81 * 8; c += BW_T) {
+    const int m = c >> 3, g = c & 7, a = m / 9, cc = m - a * 9;
+    const uint4 v = *reinterpret_cast<const uint4*>(s_p2 + ((a + 1) * BW_P2 + (cc + 1)) * BW_LD3 + g * 8);
+    *reinterpret_cast<uint4*>(dy2g + ((size_t)b * 81 + m) * 64 + g * 8) = v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) part2[e] += bf_lane(v, e);
+  }
+  // channel sums (fixed order, deterministic): lanes of one channel group (tid % 8 == g) are combined by xor
+  // shuffles inside each wave, then the 8 waves' rows are summed in wave order
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+#pragma unroll
+    for (int o = 8; o < 64; o <<= 1) {
+      part3[e] += __shfl_xor(part3[e], o, 64);
+      part2[e] += __shfl_xor(part2[e], o, 64);
+    }
+  if (lane < 8)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      s_red[wid * 128 + lane * 8 + e] = part3[e];          // channel lane * 8 + e
+      s_red[wid * 128 + 64 + lane * 8 + e] = part2[e];
+    }
+  __syncthreads();   // W2 rows + the reduction rows complete
+  if (tid < 128) {
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) v += s_red[w * 128 + tid];
+    biasp[(size_t)b * 160 + tid] = v;                      // db3 (0..63) | db2 (64..127)
+  }
+  stamp(stamps, 3);
+
+  // ---------------------------------------------------------------- dy1 (sub-pixel): wave -> (N tile wid % 2,
+  // parity class wid / 2 = (py, px): its 7 M tiles of 16 of the class's 10 x 10 outputs)
+  {
+    const int nt = wid & 1, cls = wid >> 1, py = cls >> 1, px = cls & 1;
+    floatx4 acc[7];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      const int d = ks >> 1, di = d >> 1, dj = d & 1, ob = (ks & 1) * 32;
+      const int tap = (py + 2 * di) * 4 + (px + 2 * dj);
+      const bf16x8 bf = tr_frag(s_w + (tap * 64 + ob) * BW_LD2, BW_LD2, nt * 16, lane);
+#pragma unroll
+      for (int i = 0; i < 7; ++i) {
+        const int u = min(i * 16 + l16, 99), yy = u / 10, xx = u - yy * 10;
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(
+            s_p2 + ((yy - di + 1) * BW_P2 + (xx - dj + 1)) * BW_LD3 + ob + lg * 8);
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, acc[i], 0, 0, 0);
+      }
+    }
+    // unmasked dy1 -> LDS [400][32] (the mask is applied in the 16-byte output pass)
+    const int n = nt * 16 + l16;
+#pragma unroll
+    for (int i = 0; i < 7; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int u = i * 16 + lg * 4 + r;
+        if (u < 100) {
+          const int yy = u / 10, xx = u - yy * 10;
+          s_d1[((2 * yy + py) * 20 + 2 * xx + px) * 32 + n] = f2bf(acc[i][r]);
+        }
+      }
+  }
+  __syncthreads();
+  stamp(stamps, 4);
+  // dy1 out: mask (prefetched y1 rows) applied, 16-byte stores, db1 partials (thread -> channel group tid % 4)
+  float part1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int u = 0; u < M1_PER; ++u) {
+    const int c = tid + u * BW_T;
+    if (c < M1_CH) {
+      uint4 v = *reinterpret_cast<const uint4*>(s_d1 + c * 8);
+      v.x = mask_pair(v.x, vm1[u].x);
+      v.y = mask_pair(v.y, vm1[u].y);
+      v.z = mask_pair(v.z, vm1[u].z);
+      v.w = mask_pair(v.w, vm1[u].w);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) part1[e] += bf_lane(v, e);
+      *reinterpret_cast<uint4*>(dy1g + (size_t)b * 400 * 32 + c * 8) = v;
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+#pragma unroll
+    for (int o = 4; o < 64; o <<= 1) part1[e] += __shfl_xor(part1[e], o, 64);
+  if (lane < 4)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s_red[1024 + wid * 32 + lane * 8 + e] = part1[e];   // channel lane * 8 + e
+  __syncthreads();
+  if (tid < 32) {
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) v += s_red[1024 + w * 32 + tid];
+    biasp[(size_t)b * 160 + 128 + tid] = v;
+  }
+  if (stamps) {
+    stamp(stamps, 5);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp(stamps, 6);
+  }
+}
+
 // Bootstrap value V(s_T) straight from the fc partial planes: one wave per env, h = relu(sum planes + bfc)
 // (bf16-rounded like the GEMM epilogue), value = h . Wh[:, A] + bh[A]. Replaces GEMM-reduce + value GEMM.
 __global__ void __launch_bounds__(256) fc_value_kernel(const float* __restrict__ hpart, int S, int64_t plane_stride,
@@ -267,5 +779,30 @@ extern "C" hipError_t aca_cnn_trunk_fwd(const uint8_t* obs, const uint16_t* W1, 
   if (B <= 0) return hipSuccess;
   aca::cnn_trunk_fwd_kernel<<<B, aca::T_THREADS, 0, stream>>>(obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale,
                                                                shift_out, stamps);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t aca_cnn_trunk_rows(const uint8_t* obs, const uint16_t* W1, const float* b1, const uint16_t* W2,
+                                         const float* b2, const uint16_t* W3, const float* b3, uint16_t* y1,
+                                         uint16_t* y2, uint16_t* y3, int B, float scale, uint8_t* shift_out,
+                                         uint8_t* copy_out, uint64_t* stamps, int late_w, hipStream_t stream) {
+  if (B <= 0) return hipSuccess;
+  if (late_w)
+    aca::cnn_trunk_rows_kernel<true><<<B * aca::TR_ROWS, aca::T_THREADS, 0, stream>>>(
+        obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale, shift_out, copy_out, stamps);
+  else
+    aca::cnn_trunk_rows_kernel<false><<<B * aca::TR_ROWS, aca::T_THREADS, 0, stream>>>(
+        obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale, shift_out, copy_out, stamps);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t aca_cnn_trunk_bwd(const uint16_t* dy3, const uint16_t* W3, const uint16_t* y2, const uint16_t* W2,
+                                        const uint16_t* y1, uint16_t* dy2, uint16_t* dy1, float* biasp, int B,
+                                        uint64_t* stamps, hipStream_t stream) {
+  if (B <= 0) return hipSuccess;
+  for (const void* p : {(const void*)dy3, (const void*)W3, (const void*)y2, (const void*)W2, (const void*)y1,
+                        (const void*)dy2, (const void*)dy1})
+    if (reinterpret_cast<uintptr_t>(p) % 16) return hipErrorInvalidValue;
+  aca::cnn_trunk_bwd_kernel<<<B, aca::BW_T, 0, stream>>>(dy3, W3, y2, W2, y1, dy2, dy1, biasp, stamps);
   return hipGetLastError();
 }

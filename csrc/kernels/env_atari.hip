@@ -119,21 +119,24 @@ __device__ __forceinline__ void pong_commit(const PongIO& io, int e, const PongO
 }
 
 // Frame-stack shift out[0..k-2] = prev[1..k-1] by threads [t0, t0 + nt): independent of the action, so the fused
-// kernel overlaps it with the policy head. All loads of a thread are issued before its stores (6 x 16 B in flight).
+// kernel overlaps it with the policy head. The 4 loads of a round are issued (clamped addresses, unconditional)
+// before its guarded stores. Named registers, not a guarded uint4 array: hipcc put that array in scratch (144 B/lane).
 __device__ __forceinline__ void pong_shift(const PongIO& io, int e, int t0, int nt) {
   const int k = io.k;
   const uint4* src = reinterpret_cast<const uint4*>(io.prev + (size_t)e * k * FRAME + FRAME);
   uint4* dst = reinterpret_cast<uint4*>(io.out + (size_t)e * k * FRAME);
   const int n16 = (k - 1) * FRAME / 16;
   const int tid = threadIdx.x - t0;
-  for (int j0 = tid; j0 < n16; j0 += 8 * nt) {
-    uint4 v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-      if (j0 + u * nt < n16) v[u] = src[j0 + u * nt];
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-      if (j0 + u * nt < n16) dst[j0 + u * nt] = v[u];
+  for (int j0 = tid; j0 < n16; j0 += 4 * nt) {
+    const int j1 = j0 + nt, j2 = j0 + 2 * nt, j3 = j0 + 3 * nt;
+    const uint4 v0 = src[j0];
+    const uint4 v1 = src[min(j1, n16 - 1)];
+    const uint4 v2 = src[min(j2, n16 - 1)];
+    const uint4 v3 = src[min(j3, n16 - 1)];
+    dst[j0] = v0;
+    if (j1 < n16) dst[j1] = v1;
+    if (j2 < n16) dst[j2] = v2;
+    if (j3 < n16) dst[j3] = v3;
   }
 }
 

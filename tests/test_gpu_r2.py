@@ -1,0 +1,131 @@
+"""GPU tests of the round-2 kernels (row-split trunk, ...) against the kernels / fp32 oracles they replace."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _trunk_inputs(cuda, B, seed=1):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    obs = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, generator=g).to(cuda)
+    W1 = (torch.randn(32, 256, generator=g) * 0.05).to(torch.bfloat16).to(cuda)
+    W2 = (torch.randn(64, 512, generator=g) * 0.05).to(torch.bfloat16).to(cuda)
+    W3 = (torch.randn(64, 576, generator=g) * 0.05).to(torch.bfloat16).to(cuda)
+    b1, b2, b3 = ((torch.rand(n, generator=g) * 0.1 - 0.02).to(cuda) for n in (32, 64, 64))
+    return obs, W1, b1, W2, b2, W3, b3
+
+
+@pytest.mark.parametrize("B", [1, 7, 32, 37])
+def test_trunk_rows_bitwise_equals_per_env_trunk(cuda, B):
+    """7 row workgroups per env (receptive fields recomputed, each output row stored by its owner) == the one
+    workgroup per env kernel, bit for bit, including the frame-stack shift; copy_out == the observation."""
+    from actor_critic_algs_on_tensorflow_amd.ops import gemm as G
+    obs, W1, b1, W2, b2, W3, b3 = _trunk_inputs(cuda, B)
+    outs = []
+    for mode in (0, 1, 2):
+        ys = [torch.full((B * r, c), float("nan"), dtype=torch.bfloat16, device=cuda)
+              for r, c in ((400, 32), (81, 64), (49, 64))]
+        sh = torch.full_like(obs, 7)
+        cp = torch.full_like(obs, 9) if mode >= 1 else None
+        G.cnn_trunk_fwd(obs, W1, b1, W2, b2, W3, b3, *ys, shift_out=sh, mode=mode, copy_out=cp)
+        torch.cuda.synchronize()
+        outs.append((ys, sh, cp))
+    (y0, s0, _) = outs[0]
+    for (y1, s1, c1) in outs[1:]:
+        for a, b in zip(y0, y1):
+            assert not torch.isnan(b.float()).any(), "row-split trunk left an activation row unwritten"
+            assert torch.equal(a.view(torch.int16), b.view(torch.int16))
+        assert torch.equal(s0[:, :3], s1[:, :3]) and torch.equal(s1[:, :3], obs[:, 1:])
+        assert (s1[:, 3] == 7).all(), "the newest frame slot is the env kernel's to render"
+        assert torch.equal(c1, obs)
+
+
+@pytest.mark.parametrize("B", [1, 5, 160])
+def test_trunk_bwd_matches_conv_transpose(cuda, B):
+    """Fused per-sample data-gradient chain vs fp32 torch conv_transpose2d on the same bf16 inputs: dy2 = tconv(dy3,
+    W3) * (y2 > 0), dy1 = tconv(dy2_bf16, W2) * (y1 > 0), and the per-sample bias-gradient partials."""
+    import torch.nn.functional as F
+    from actor_critic_algs_on_tensorflow_amd import _native
+    ops = _native.require()
+    g = torch.Generator(device="cpu").manual_seed(3)
+    dy3 = (torch.randn(B, 7, 7, 64, generator=g) * (torch.rand(B, 7, 7, 64, generator=g) > 0.4)).to(torch.bfloat16)
+    W3 = (torch.randn(64, 3, 3, 64, generator=g) * 0.05).to(torch.bfloat16)        # OHWI
+    W2 = (torch.randn(64, 4, 4, 32, generator=g) * 0.05).to(torch.bfloat16)
+    y2 = (torch.rand(B, 9, 9, 64, generator=g) - 0.3).clamp(min=0).to(torch.bfloat16)
+    y1 = (torch.rand(B, 20, 20, 32, generator=g) - 0.3).clamp(min=0).to(torch.bfloat16)
+    dev = [t.to(cuda) for t in (dy3, W3, y2, W2, y1)]
+    dy2 = torch.full((B * 81, 64), float("nan"), dtype=torch.bfloat16, device=cuda)
+    dy1 = torch.full((B * 400, 32), float("nan"), dtype=torch.bfloat16, device=cuda)
+    bp = torch.full((B, 160), float("nan"), device=cuda)
+    ops.cnn_trunk_bwd(dev[0].reshape(B * 49, 64), dev[1].reshape(64, 576), dev[2].reshape(B * 81, 64),
+                      dev[3].reshape(64, 512), dev[4].reshape(B * 400, 32), dy2, dy1, bp)
+    torch.cuda.synchronize()
+    r2 = F.conv_transpose2d(dy3.float().permute(0, 3, 1, 2), W3.float().permute(0, 3, 1, 2), stride=1)
+    r2 = r2.permute(0, 2, 3, 1) * (y2.float() > 0)                                     # [B, 9, 9, 64]
+    got2 = dy2.float().cpu().view(B, 9, 9, 64)
+    assert torch.allclose(got2, r2, rtol=2e-2, atol=2e-2), (got2 - r2).abs().max()
+    # dy1 from the kernel's own bf16 dy2 (the chain's rounding point)
+    r1 = F.conv_transpose2d(got2.permute(0, 3, 1, 2), W2.float().permute(0, 3, 1, 2), stride=2)
+    r1 = r1.permute(0, 2, 3, 1) * (y1.float() > 0)                                     # [B, 20, 20, 32]
+    got1 = dy1.float().cpu().view(B, 20, 20, 32)
+    assert torch.allclose(got1, r1, rtol=2e-2, atol=2e-2), (got1 - r1).abs().max()
+    bpc = bp.cpu()
+    assert torch.allclose(bpc[:, :64], dy3.float().sum((1, 2)), rtol=1e-4, atol=1e-4)
+    assert torch.allclose(bpc[:, 64:128], got2.sum((1, 2)), rtol=1e-4, atol=1e-3)
+    assert torch.allclose(bpc[:, 128:], got1.sum((1, 2)), rtol=1e-4, atol=1e-3)
+    # bitwise reproducible
+    dy1b, bpb = dy1.clone(), bp.clone()
+    ops.cnn_trunk_bwd(dev[0].reshape(B * 49, 64), dev[1].reshape(64, 576), dev[2].reshape(B * 81, 64),
+                      dev[3].reshape(64, 512), dev[4].reshape(B * 400, 32), dy2, dy1, bp)
+    torch.cuda.synchronize()
+    assert torch.equal(dy1b.view(torch.int16), dy1.view(torch.int16)) and torch.equal(bpb, bp)
+
+
+def _one_update(fused, algo="pong_a2c", **kw):
+    from actor_critic_algs_on_tensorflow_amd import preset
+    from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
+    cfg = preset(algo, num_envs=8, device="cuda:0", outdir=None, quiet=True, stdout_freq=0, save_every=0,
+                 cuda_graph=False, optimizer="adam", **kw)
+    tr = ActorCriticTrainer(cfg)
+    tr.engine.fused_bwd = fused
+    p0 = tr.flat.data.clone()
+    tr.step()
+    torch.cuda.synchronize()
+    return tr.flat.data - p0, tr.stats_buf.clone()
+
+
+@pytest.mark.parametrize("algo,kw", [("pong_a2c", {}), ("breakout_ppo", dict(n_steps=16, ppo_minibatches=2,
+                                                                              ppo_epochs=1))])
+def test_fused_backward_update_matches_gemm_backward(cuda, algo, kw):
+    """One optimiser step with the fused data-gradient kernel + finaliser == the transposed-conv GEMM backward
+    (same loss statistics, same parameter update up to bf16 rounding order)."""
+    d1, s1 = _one_update(True, algo, **kw)
+    d0, s0 = _one_update(False, algo, **kw)
+    assert torch.allclose(s0, s1, rtol=1e-3, atol=1e-5)
+    assert (d0 - d1).norm() / d0.norm() < 2e-2, float((d0 - d1).norm() / d0.norm())
+
+
+def test_grad_finalize_planes_and_norm(cuda):
+    """grad_finalize: plane sums in fixed order into dst, read-only segments untouched, sum-of-squares partials of
+    the final gradient over both kinds of segment."""
+    from actor_critic_algs_on_tensorflow_amd import _native
+    ops = _native.require()
+    g = torch.Generator(device="cpu").manual_seed(0)
+    slab = torch.randn(70001, generator=g).to(cuda)
+    planes = torch.randn(7, 1003, generator=g).to(cuda)     # 7 planes of a 1003-element gradient (stride 1003)
+    rows = torch.randn(33, 160, generator=g).to(cuda)       # per-sample rows, columns 64..127 -> a 64-element bias
+    dA, dB = slab[10:1013], slab[2000:2064]
+    ro = slab[3000:70001]
+    words = torch.tensor([[dA.data_ptr(), planes.data_ptr(), 1003, 1003, 7, 0],
+                          [dB.data_ptr(), rows.data_ptr() + 64 * 4, 64, 160, 33, 0],
+                          [ro.data_ptr(), 0, ro.numel(), 0, 0, 0]], dtype=torch.int64)
+    keep = ro.clone()
+    parts = torch.full((256,), float("nan"), device=cuda)
+    ops.grad_finalize(words, parts)
+    torch.cuda.synchronize()
+    assert torch.allclose(dA, planes.sum(0), atol=1e-5)
+    assert torch.allclose(dB, rows[:, 64:128].sum(0), atol=1e-5)
+    assert torch.equal(ro, keep)
+    tot = float(parts.double().sum())
+    ref = float(dA.double().pow(2).sum() + dB.double().pow(2).sum() + ro.double().pow(2).sum())
+    assert abs(tot - ref) <= 1e-4 * ref

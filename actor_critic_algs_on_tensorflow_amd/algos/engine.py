@@ -99,6 +99,15 @@ class CNNEngine:
         # per-sample partial rows reduced by the gradient finaliser) instead of two transposed-conv GEMMs
         self.fused_bwd = implicit and os.environ.get("ACA_FUSED_BWD", "1") != "0"
         self.fin_parts = torch.zeros(256, dtype=torch.float32, device=flat.data.device)
+        # A2C head in one launch (head_bwd: loss + dz + dh + dWh + dbh + dbfc, no GEMMs) for categorical heads of up
+        # to 7 actions and learner batches up to 1024 rows
+        self.fused_head = os.environ.get("ACA_FUSED_HEAD", "1") != "0"
+        # conv weight gradients as split-K partial planes reduced in plane order by the finaliser (deterministic);
+        # 0: split-K fp32 atomics into the slab (nondeterministic summation order)
+        self.det_wgrad = implicit and os.environ.get("ACA_DET_WGRAD", "1") != "0"
+        self.wgrad_planes = 32
+        self._planes = {}
+        self._wsplits = {}
         self._fin_words = {}
         # rollout fc product left as split-K partial planes, reduced by its consumer kernel (no in-launch fence)
         self.fc_parts = os.environ.get("ACA_FC_PARTS", "1") != "0"
@@ -220,7 +229,34 @@ class CNNEngine:
             assert start <= (g.data_ptr() - base) // 4 < end
         return start, end
 
-    def backward(self, b: _Bufs, head_bias_done=False, stage="all"):
+    def _wgrad(self, name, gview, A, lda, B_, ldb, M, N, K, ws, gb, gb_scale=1.0):
+        """Conv weight gradient dW = A^T-ish product over the batch rows (K): deterministic split-K planes reduced
+        by the finaliser (``det_wgrad``), else atomics straight into the slab."""
+        if not self.det_wgrad:
+            G.gemm(A, lda, False, B_, ldb, False, gview, N, 2, M, N, K, workspace=ws, gb=gb, gb_scale=gb_scale)
+            return
+        buf = self._planes.get(name)
+        if buf is None:
+            buf = torch.zeros(self.wgrad_planes * M * N, dtype=torch.float32, device=self.dev)
+            self._planes[name] = buf
+        S = G.gemm(A, lda, False, B_, ldb, False, buf, N, 3, M, N, K, workspace=ws, gb=gb, gb_scale=gb_scale,
+                   max_planes=self.wgrad_planes)
+        self._wsplits[name] = S
+
+    def head_ok(self, B):
+        return self.fused_head and 2 <= self.A <= 7 and B <= 512
+
+    def head_backward(self, b: _Bufs, actions, logp_old, ent_coef, kl_coef, vf_coef, stats, returns):
+        """A2C fast path: ``head_bwd`` -- returns/EV/adv-norm + loss + dz and the head's backward (dh, dWh, dbh,
+        dbfc) in one launch; :meth:`backward` then starts at the fc layer (``head_done=True``)."""
+        r = returns
+        _native.require().head_bwd(b.z, actions, logp_old, ent_coef, kl_coef, float(vf_coef), r["rew"], r["val"],
+                                   r["dones"], int(r["L"]), int(r["mode"]), bool(r["norm_adv"]), float(r["gamma"]),
+                                   float(r["lam"]), r["ret_w"], r["adv_w"], b.h, self.sWh, b.dh, self.gWh, self.gbh,
+                                   self.gbfc, stats)
+        return stats
+
+    def backward(self, b: _Bufs, head_bias_done=False, stage="all", head_done=False):
         """Accumulates d(loss)/d(params) into the gradient slab from ``b.dz`` (written by the loss kernel).
 
         Two streams: the activation-gradient chain (dh -> dy3 -> dy2 -> dy1) runs on the current stream while
@@ -239,18 +275,20 @@ class CNNEngine:
         ws2 = self._side_ws()
         if stage == "trunk":
             return self._backward_trunk(b, main, side, ev, ws, ws2)
-        ev[0].record(main)
-        side.wait_event(ev[0])
-        with torch.cuda.stream(side):   # heads: dWh = h^T dz, dbh = colsum(dz)
-            G.gemm(b.h, 512, False, b.dz, A1, False, self.gWh, A1, 2, 512, A1, B, workspace=ws2)
-            if not head_bias_done:
-                ops.colsum_bf16(b.dz, B, A1, A1, self.gbh)
-        G.gemm(b.dz, A1, True, self.sWh, A1, True, b.dh, 512, 1, B, 512, A1, mask=b.h, ldm=512, colsum=self.gbfc,
-               workspace=ws)
+        if not head_done:
+            ev[0].record(main)
+            side.wait_event(ev[0])
+            with torch.cuda.stream(side):   # heads: dWh = h^T dz, dbh = colsum(dz)
+                G.gemm(b.h, 512, False, b.dz, A1, False, self.gWh, A1, 2, 512, A1, B, workspace=ws2)
+                if not head_bias_done:
+                    ops.colsum_bf16(b.dz, B, A1, A1, self.gbh)
+            G.gemm(b.dz, A1, True, self.sWh, A1, True, b.dh, 512, 1, B, 512, A1, mask=b.h, ldm=512,
+                   colsum=self.gbfc, workspace=ws)
         ev[1].record(main)
         side.wait_event(ev[1])
-        with torch.cuda.stream(side):   # fc weight gradient
-            G.gemm(b.y3, 3136, False, b.dh, 512, False, self.gWfc, 512, 2, 3136, 512, B, workspace=ws2)
+        with torch.cuda.stream(side):   # fc weight gradient (det_wgrad: store; split-K slabs reduced in order)
+            G.gemm(b.y3, 3136, False, b.dh, 512, False, self.gWfc, 512, 0 if self.det_wgrad else 2, 3136, 512, B,
+                   workspace=ws2)
         G.gemm(b.dh, 512, True, self.sWfc, 512, True, b.dy3, 3136, 1, B, 3136, 512, mask=b.y3, ldm=3136,
                colsum=None if self.fused_bwd else self.gb3, colsum_mod=0 if self.fused_bwd else 64, workspace=ws)
         if stage == "tail":
@@ -266,8 +304,7 @@ class CNNEngine:
         side.wait_event(ev[2])
         with torch.cuda.stream(side):   # conv3 weight gradient
             if imp:
-                G.gemm(b.dy3, 64, False, b.y2, 0, False, self.gW3, 576, 2, 64, 576, B * 49, workspace=ws2,
-                       gb=[2, B, 64, 9, 9, 3, 3, 1])
+                self._wgrad("W3", self.gW3, b.dy3, 64, b.y2, 0, 64, 576, B * 49, ws2, [2, B, 64, 9, 9, 3, 3, 1])
             else:
                 G.gemm(b.dy3, 64, False, b.col3, 576, False, self.gW3, 576, 2, 64, 576, B * 49, workspace=ws2)
         if self.fused_bwd:
@@ -284,8 +321,7 @@ class CNNEngine:
         side.wait_event(ev[3])
         with torch.cuda.stream(side):   # conv2 weight gradient
             if imp:
-                G.gemm(b.dy2, 64, False, b.y1, 0, False, self.gW2, 512, 2, 64, 512, B * 81, workspace=ws2,
-                       gb=[2, B, 32, 20, 20, 4, 4, 2])
+                self._wgrad("W2", self.gW2, b.dy2, 64, b.y1, 0, 64, 512, B * 81, ws2, [2, B, 32, 20, 20, 4, 4, 2])
             else:
                 G.gemm(b.dy2, 64, False, b.col2, 512, False, self.gW2, 512, 2, 64, 512, B * 81, workspace=ws2)
         if self.fused_bwd:
@@ -299,13 +335,13 @@ class CNNEngine:
             G.col2im_nhwc(self.dcol2(b), b.y1, b.dy1, self.gb1, B, 20, 20, 32, 4, 4, 2)
         # conv1 weight gradient (last product of the chain: on the main stream)
         if imp:
-            G.gemm(b.dy1, 32, False, b.obs, 0, False, self.gW1, 256, 2, 32, 256, B * 400, workspace=ws,
-                   gb=[1, B, 4, 84, 84, 8, 8, 4], gb_scale=1.0 / 255.0)
+            self._wgrad("W1", self.gW1, b.dy1, 32, b.obs, 0, 32, 256, B * 400, ws, [1, B, 4, 84, 84, 8, 8, 4],
+                        1.0 / 255.0)
         else:
             G.gemm(b.dy1, 32, False, b.col1, 256, False, self.gW1, 256, 2, 32, 256, B * 400, workspace=ws)
         ev[4].record(side)
         main.wait_event(ev[4])
-        if self.fused_bwd or self.want_parts:
+        if self.fused_bwd or self.want_parts or self.det_wgrad:
             self.finalize(b)
 
     # ------------------------------------------------------------------------------------------------ finaliser
@@ -315,23 +351,29 @@ class CNNEngine:
         """One launch after the backward (``grad_finalize``): reduces the per-sample conv bias-gradient rows
         (fused backward) into the slab and, with ``want_parts``, writes the global-norm partials of the whole
         gradient (``fin_parts``) so the optimiser needs no sum-of-squares pass."""
-        key = (b.B, self.want_parts, self.fused_bwd)
+        planes = tuple(sorted(self._wsplits.items())) if self.det_wgrad else ()
+        key = (b.B, self.want_parts, self.fused_bwd, planes)
         words = self._fin_words.get(key)
         if words is None:
             segs = []
             flat = self.flat
-            bias_src = {}
+            src_of = {}   # gradient slot -> (source, stride, planes)
             if self.fused_bwd:
                 bp = b.biasp.data_ptr()
-                bias_src = {self.gb3.data_ptr(): bp, self.gb2.data_ptr(): bp + 64 * 4, self.gb1.data_ptr(): bp + 128 * 4}
+                src_of = {self.gb3.data_ptr(): (bp, 160, b.B), self.gb2.data_ptr(): (bp + 64 * 4, 160, b.B),
+                          self.gb1.data_ptr(): (bp + 128 * 4, 160, b.B)}
+            for name, S in planes:
+                g = {"W1": self.gW1, "W2": self.gW2, "W3": self.gW3}[name]
+                src_of[g.data_ptr()] = (self._planes[name].data_ptr(), g.numel(), S)
             for p, off in zip(flat.params, flat.offsets):
                 g = flat.grad[off:off + p.numel()]
-                src = bias_src.get(g.data_ptr())
+                src = src_of.get(g.data_ptr())
                 if src is not None:
-                    segs.append([g.data_ptr(), src, g.numel(), 160, b.B, 0])
+                    segs.append((g.data_ptr(), src[0], g.numel(), src[1], src[2]))
                 elif self.want_parts:
-                    segs.append([g.data_ptr(), 0, g.numel(), 0, 0, 0])
-            words = torch.tensor(segs, dtype=torch.int64)
+                    segs.append((g.data_ptr(), 0, g.numel(), 0, 0))
+            from ..ops.optim import finalize_jobs
+            words = finalize_jobs(segs, self.dev)
             self._fin_words[key] = words
         _native.require().grad_finalize(words, self.fin_parts)
 

@@ -470,12 +470,17 @@ class ActorCriticTrainer:
             self._ret_w = torch.zeros(T * N, device=self.device)
             self._adv_w = torch.zeros(T * N, device=self.device)
         vf = cfg.vf_coef if "shared" in self.flat.groups else 1.0
-        eng.loss(b, actions, logp_old, None, None, None, self.ent_coef, self.kl_coef, vf, 0.0, 0.0,
-                 stats=self.stats_buf,
-                 returns=dict(mode=1 if cfg.returns == "nstep" else 2, rew=st.rewards, val=st.values, dones=st.dones,
-                              L=T if cfg.look_ahead is None else cfg.look_ahead, gamma=cfg.gamma,
-                              lam=cfg.gae_lambda, norm_adv=cfg.norm_adv, ret_w=self._ret_w, adv_w=self._adv_w))
-        eng.backward(b, head_bias_done=True, stage=self._bw_stage)
+        rets = dict(mode=1 if cfg.returns == "nstep" else 2, rew=st.rewards, val=st.values, dones=st.dones,
+                    L=T if cfg.look_ahead is None else cfg.look_ahead, gamma=cfg.gamma, lam=cfg.gae_lambda,
+                    norm_adv=cfg.norm_adv, ret_w=self._ret_w, adv_w=self._adv_w)
+        if eng.head_ok(T * N):
+            # loss + dz + the head's backward (dh, dWh, dbh, dbfc) in one launch
+            eng.head_backward(b, actions, logp_old, self.ent_coef, self.kl_coef, vf, self.stats_buf, rets)
+            eng.backward(b, head_bias_done=True, stage=self._bw_stage, head_done=True)
+        else:
+            eng.loss(b, actions, logp_old, None, None, None, self.ent_coef, self.kl_coef, vf, 0.0, 0.0,
+                     stats=self.stats_buf, returns=rets)
+            eng.backward(b, head_bias_done=True, stage=self._bw_stage)
         self._bw_pending = (b, True)
         self._apply_grads()
         self._last = (obs, actions, logp_old, self._ret_w)

@@ -153,15 +153,15 @@ def _row_block(ga):
 
 
 def _tune(key, ops, A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha, bias, relu, mask, ldm, colsum,
-          colsum_mod, workspace, ga, ga_scale, gb, gb_scale):
+          colsum_mod, workspace, ga, ga_scale, gb, gb_scale, max_planes=PARTIAL_MAX_SPLITS):
     dev = C.device
-    planes = PARTIAL_MAX_SPLITS if out_mode == 3 else 1
+    planes = max_planes if out_mode == 3 else 1
     Cs = torch.zeros(planes * M * ldc, dtype=C.dtype, device=dev)
     cs = torch.zeros(max(N, colsum_mod or 0), dtype=torch.float32, device=dev) if colsum is not None else None
     ws = workspace if workspace is not None else GemmWorkspace(dev)
     best = None
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    for tile, bk, s in _candidates(M, N, K, out_mode == 2, PARTIAL_MAX_SPLITS if out_mode == 3 else None,
+    for tile, bk, s in _candidates(M, N, K, out_mode in (2, 3), max_planes if out_mode == 3 else None,
                                    _row_block(ga)):
         args = (ops, A, lda, a_k, B, ldb, b_k, Cs, ldc, out_mode, M, N, K, alpha, bias, relu, mask, ldm, cs,
                 colsum_mod, tile, bk, s, ws, ga, ga_scale, gb, gb_scale)
@@ -182,26 +182,28 @@ def _tune(key, ops, A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha, 
 
 def gemm(A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha=1.0, bias=None, relu=False, mask=None, ldm=0,
          colsum=None, tile=None, splits=None, workspace: GemmWorkspace | None = None, colsum_mod=0, bk=None,
-         ga=None, ga_scale=1.0, gb=None, gb_scale=1.0, stamps=None):
+         ga=None, ga_scale=1.0, gb=None, gb_scale=1.0, stamps=None, max_planes=PARTIAL_MAX_SPLITS):
     """Native GEMM; ``out_mode``: 0 fp32 store, 1 bf16 store, 2 fp32 atomic add (C pre-zeroed), 3 fp32 split-K
-    partial planes ``C[z, M, ldc]`` (no bias/activation: the consumer reduces). Returns the effective split count.
+    partial planes ``C[z, M, ldc]`` (no bias/activation: the consumer reduces, in plane order -- deterministic;
+    ``max_planes`` bounds the split count, C must hold that many planes). Returns the effective split count.
 
     ``ga`` / ``gb``: implicit-im2col gathers ``[mode, B, C, H, W, KH, KW, S]`` (mode 1 uint8 NCHW, 2 bf16 NHWC)
     reading operand A (k-contiguous) / B (n-contiguous) straight from the activation image ``A`` / ``B``.
     """
     ops = _native.require()
     if tile is None or splits is None or bk is None:
-        key = (M, N, K, bool(a_k), bool(b_k), out_mode, lda % 8 == 0, ldb % 8 == 0, tuple(ga or ()), tuple(gb or ()))
+        key = (M, N, K, bool(a_k), bool(b_k), out_mode, lda % 8 == 0, ldb % 8 == 0, tuple(ga or ()), tuple(gb or ()),
+               max_planes if out_mode == 3 else 0)
         hit = _TUNED.get(key)
         if hit is not None:
             t, k, s = hit[0], hit[1], hit[2]
         elif TUNE and C.is_cuda and not torch.cuda.is_current_stream_capturing():
             t, k, s = _tune(key, ops, A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha, bias, relu, mask,
-                            ldm, colsum, colsum_mod, workspace, ga, ga_scale, gb, gb_scale)
+                            ldm, colsum, colsum_mod, workspace, ga, ga_scale, gb, gb_scale, max_planes)
         else:
-            t, k, s = plan(M, N, K, atomic=(out_mode == 2))
+            t, k, s = plan(M, N, K, atomic=(out_mode in (2, 3)))
             if out_mode == 3:
-                s = min(s, PARTIAL_MAX_SPLITS)
+                s = min(s, max_planes)
             rb = _row_block(ga)
             if rb is not None and rb % TILES[t][0]:
                 t = next(tt for tt in (2, 0, 4, 1) if rb % TILES[tt][0] == 0)
@@ -210,8 +212,8 @@ def gemm(A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha=1.0, bias=No
         splits = s if splits is None else splits
     if colsum_mod and colsum is None:
         raise ValueError("colsum_mod without colsum")
-    if out_mode == 3 and effective_splits(K, bk, splits) > PARTIAL_MAX_SPLITS:
-        raise ValueError("out_mode 3 supports at most %d partial planes" % PARTIAL_MAX_SPLITS)
+    if out_mode == 3 and effective_splits(K, bk, splits) > max_planes:
+        raise ValueError("out_mode 3: more split-K planes than C holds (%d)" % max_planes)
     return _run(ops, A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha, bias, relu, mask, ldm, colsum,
                 colsum_mod, tile, bk, splits, workspace, ga, ga_scale, gb, gb_scale, stamps)
 

@@ -259,6 +259,46 @@ class FusedGroupStep:
                       zero, o0.p)
 
 
+SUMSQ_PARTS = 256   # optim.hip: partial slots of the global-norm reduction = max finaliser workgroups
+
+
+def finalize_jobs(segments, device):
+    """Job table of the gradient finaliser (``grad_finalize``): ``segments`` = [(dst_ptr, src_ptr, n, stride, S)]
+    (``src_ptr`` 0: final already, read for the norm). Plane reductions are cut into 1024-element jobs (one float4
+    per thread, a short chain of plane loads), per-sample bias rows (n <= 64) take one job each, and the read-only
+    segments share the remaining workgroups in equal multiples of 1024 elements; at most ``SUMSQ_PARTS`` jobs."""
+    plane_ch = 1024
+    while True:
+        jobs = []
+        ro = [sg for sg in segments if not sg[1]]
+        for dst, src, n, stride, S in segments:
+            if not src:
+                continue
+            if n <= 64:
+                jobs.append([dst, src, n, stride, S])
+                continue
+            for a in range(0, n, plane_ch):
+                jobs.append([dst + 4 * a, src + 4 * a, min(plane_ch, n - a), stride, S])
+        left = SUMSQ_PARTS - len(jobs)
+        total_ro = sum(sg[2] for sg in ro)
+        if left >= max(1, len(ro)) or plane_ch >= 1 << 20:
+            break
+        plane_ch *= 2
+    if ro:
+        ch = max(1024, -(-total_ro // max(1, left - len(ro))))
+        ch = -(-ch // 1024) * 1024
+        for dst, _, n, _, _ in ro:
+            for a in range(0, n, ch):
+                jobs.append([dst + 4 * a, 0, min(ch, n - a), 0, 0])
+    if len(jobs) > SUMSQ_PARTS:
+        raise ValueError("finalize_jobs: %d jobs exceed %d norm partials" % (len(jobs), SUMSQ_PARTS))
+    rows = []
+    for dst, src, n, stride, S in jobs:
+        vec = int(dst % 16 == 0 and (not src or (src % 16 == 0 and stride % 4 == 0)))
+        rows.append([dst, src, n, stride, S, vec, 0, 0])
+    return torch.tensor(rows, dtype=torch.int64).to(device)
+
+
 def make_optimizer(name, flat, group, lr, clip_value=None, max_grad_norm=None, bf16_shadow=None):
     if name == "adam":
         return FusedAdam(flat, group, lr, clip_value=clip_value, max_grad_norm=max_grad_norm,

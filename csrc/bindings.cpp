@@ -80,6 +80,10 @@ hipError_t aca_cnn_trunk_fwd(const uint8_t*, const uint16_t*, const float*, cons
                              const uint16_t*, const float*, uint16_t*, uint16_t*, uint16_t*, int, float, uint8_t*,
                              uint64_t*, hipStream_t);
 hipError_t aca_grad_finalize(const int64_t*, int, float*, hipStream_t);
+hipError_t aca_head_bwd(const float*, const int32_t*, const float*, const float*, const float*, float, const float*,
+                        const float*, const uint8_t*, int, int, int, int, int, float, float, float*, float*,
+                        const uint16_t*, const uint16_t*, uint16_t*, float*, float*, float*, float*, int,
+                        hipStream_t);
 hipError_t aca_cnn_trunk_bwd(const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*,
                              uint16_t*, uint16_t*, float*, int, uint64_t*, hipStream_t);
 hipError_t aca_cnn_trunk_rows(const uint8_t*, const uint16_t*, const float*, const uint16_t*, const float*,
@@ -918,16 +922,47 @@ void cnn_trunk_bwd(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tenso
         "cnn_trunk_bwd");
 }
 
-// Gradient finaliser (optim.hip grad_finalize_kernel): words = host int64 [nseg, 6] (dst, src, n, stride, S, 0)
-// device pointers; writes dst = sum of S planes for src != 0, and the SUMSQ_PARTS sum-of-squares partials.
-void grad_finalize(Tensor words, Tensor partial) {
-  TORCH_CHECK(words.device().is_cpu() && words.scalar_type() == at::kLong && words.dim() == 2 && words.size(1) == 6,
-              "grad_finalize: words must be a CPU int64 [nseg, 6] tensor");
+// Gradient finaliser (optim.hip grad_finalize_kernel): jobs = device int64 [njobs, 8] (dst, src, n, stride, S,
+// vec, 0, 0) built by ops/optim.py finalize_jobs; writes dst = sum of S planes where src != 0 and the
+// SUMSQ_PARTS sum-of-squares partials.
+void grad_finalize(Tensor jobs, Tensor partial) {
+  need(jobs, at::kLong, "jobs");
+  TORCH_CHECK(jobs.dim() == 2 && jobs.size(1) == 8 && jobs.is_contiguous(), "grad_finalize: jobs must be [njobs, 8]");
   need(partial, at::kFloat, "partial");
-  TORCH_CHECK(partial.numel() >= aca_sumsq_parts(), "grad_finalize: partial too small");
-  auto w = words.contiguous();
-  check(aca_grad_finalize(w.data_ptr<int64_t>(), (int)w.size(0), ptr<float>(partial), cur_stream(partial)),
+  TORCH_CHECK(partial.numel() >= aca_sumsq_parts() && jobs.size(0) <= aca_sumsq_parts(),
+              "grad_finalize: partial too small / too many jobs");
+  check(aca_grad_finalize(jobs.data_ptr<int64_t>(), (int)jobs.size(0), ptr<float>(partial), cur_stream(partial)),
         "grad_finalize");
+}
+
+// A2C learner head in one launch (loss.hip head_bwd_kernel): returns + EV + advantage normalisation + loss + dz,
+// then dh = (h > 0) * dz Wh^T, dbfc, dWh, dbh written straight into their gradient slots (deterministic).
+void head_bwd(Tensor z, Tensor act, Tensor logp_old, Tensor ent_coef, Tensor kl_coef, double vf_coef, Tensor rew,
+              Tensor val, Tensor dones, int64_t L, int64_t returns_mode, bool norm_adv, double gamma, double lam,
+              Tensor ret_w, Tensor adv_w, Tensor h, Tensor Wh, Tensor dh, Tensor gWh, Tensor gbh, Tensor gbfc,
+              Tensor stats) {
+  TORCH_CHECK(rew.dim() == 2, "head_bwd: rewards must be [T, N]");
+  const int T = rew.size(0), N = rew.size(1), B = T * N;
+  TORCH_CHECK(z.dim() == 2 && z.size(0) >= B, "head_bwd: z must be [B, A + 1]");
+  const int A = z.size(1) - 1;
+  need(z, at::kFloat, "z");
+  need(act, at::kInt, "act");
+  for (auto* t : {&logp_old, &ent_coef, &kl_coef, &rew, &val, &ret_w, &adv_w, &gWh, &gbh, &gbfc, &stats})
+    need(*t, at::kFloat, "head_bwd fp32 operand");
+  need(dones, at::kByte, "dones");
+  for (auto* t : {&h, &Wh, &dh}) need(*t, at::kBFloat16, "head_bwd bf16 operand");
+  TORCH_CHECK(z.is_contiguous() && z.stride(0) == A + 1, "head_bwd: z must be contiguous [B, A + 1]");
+  TORCH_CHECK(act.numel() >= B && logp_old.numel() >= B && val.numel() == (int64_t)(T + 1) * N &&
+                  dones.numel() == B && ret_w.numel() >= B && adv_w.numel() >= B && h.numel() >= (int64_t)B * 512 &&
+                  dh.numel() >= (int64_t)B * 512 && Wh.numel() == 512 * (A + 1) && gWh.numel() == 512 * (A + 1) &&
+                  gbh.numel() == A + 1 && gbfc.numel() == 512 && stats.numel() >= 8,
+              "head_bwd: shape mismatch");
+  check(aca_head_bwd(ptr<float>(z), ptr<int32_t>(act), ptr<float>(logp_old), ptr<float>(ent_coef),
+                     ptr<float>(kl_coef), (float)vf_coef, ptr<float>(rew), ptr<float>(val), ptr<uint8_t>(dones), T, N,
+                     (int)L, (int)returns_mode, norm_adv ? 1 : 0, (float)gamma, (float)lam, ptr<float>(ret_w),
+                     ptr<float>(adv_w), ptr<uint16_t>(h), ptr<uint16_t>(Wh), ptr<uint16_t>(dh), ptr<float>(gWh),
+                     ptr<float>(gbh), ptr<float>(gbfc), ptr<float>(stats), A, cur_stream(z)),
+        "head_bwd");
 }
 
 void im2col_u8(Tensor x, Tensor col, int64_t kh, int64_t kw, int64_t s, double scale) {
@@ -1122,7 +1157,10 @@ TORCH_LIBRARY(acamd, m) {
         "Tensor? copy_out=None) -> ()");
   m.def("cnn_trunk_bwd(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tensor dy2, Tensor dy1, "
         "Tensor biasp, Tensor? stamps=None) -> ()");
-  m.def("grad_finalize(Tensor words, Tensor partial) -> ()");
+  m.def("grad_finalize(Tensor jobs, Tensor partial) -> ()");
+  m.def("head_bwd(Tensor z, Tensor act, Tensor logp_old, Tensor ent_coef, Tensor kl_coef, float vf_coef, Tensor rew, "
+        "Tensor val, Tensor dones, int L, int returns_mode, bool norm_adv, float gamma, float lam, Tensor ret_w, "
+        "Tensor adv_w, Tensor h, Tensor Wh, Tensor dh, Tensor gWh, Tensor gbh, Tensor gbfc, Tensor stats) -> ()");
   m.def("im2col_u8(Tensor x, Tensor col, int kh, int kw, int s, float scale) -> ()");
   m.def("im2col_nhwc(Tensor x, Tensor col, int B, int H, int W, int C, int kh, int kw, int s) -> ()");
   m.def("col2im_nhwc(Tensor dcol, Tensor ymask, Tensor dx, Tensor? colsum, int B, int H, int W, int C, int kh, "
@@ -1166,6 +1204,7 @@ TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
   m.impl("fc_value", &fc_value);
   m.impl("cnn_trunk_bwd", &cnn_trunk_bwd);
   m.impl("grad_finalize", &grad_finalize);
+  m.impl("head_bwd", &head_bwd);
   m.impl("im2col_u8", &im2col_u8);
   m.impl("im2col_nhwc", &im2col_nhwc);
   m.impl("col2im_nhwc", &col2im_nhwc);

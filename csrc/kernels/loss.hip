@@ -287,7 +287,279 @@ __global__ void __launch_bounds__(LOSS_THREADS) ac_loss_kernel(LossArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------------------------------
+// A2C learner head, one launch (the rollout's activations are the forward): n-step / GAE returns, EV-before and
+// advantage normalisation, the actor-critic loss and dz = dL/d(logits | value) exactly as ac_loss_kernel's fused
+// path, then the head's backward without GEMM launches:
+//   dh[b, j]  = (h[b, j] > 0) * sum_a dz[b, a] Wh[j, a]      (bf16, the fc layer's data gradient)
+//   dbfc[j]   = sum_b dh[b, j]          dWh[j, a] = sum_b h[b, j] dz[b, a]          dbh[a] = sum_b dz[b, a]
+// written straight into their gradient-slab slots. HB_WG workgroups, each owning 64 of the 512 hidden columns;
+// every workgroup recomputes the (tiny, B-row) loss so that no cross-workgroup hand-off is needed, and workgroup 0
+// alone writes the statistics / returns / dbh. Every sum runs in a fixed order (deterministic, and the loss of
+// every workgroup is bit-identical). Head phase: wave w, lane l -> 8-column chunk l % 8 of the workgroup's 64, rows
+// w * 8 + l / 8 + 64 i (16-byte h loads and dh stores, all of a thread's rows in flight at once); per-wave column
+// sums by xor shuffles, then the 8 waves in wave order through LDS. Replaces ac_loss + the dh / dWh GEMMs.
+// ------------------------------------------------------------------------------------------------------------
+constexpr int HB_THREADS = 512;             // 2 waves per SIMD: 256 registers for the head phase's columns
+constexpr int HB_MAXB = 512;
+constexpr int HB_H = 512;
+constexpr int HB_WG = 8;                    // workgroups (64 hidden columns each)
+constexpr int HB_RPT = HB_MAXB / 64;        // row slots per thread in the head phase (8)
+
+struct HeadBwdArgs {
+  const float* z;            // [B, A1] logits | value
+  const int32_t* act;
+  const float* logp_old;
+  const float* ent_coef; const float* kl_coef;
+  float vf_coef;
+  const float* rew; const float* val; const uint8_t* dn;
+  int T, N, L, returns_mode, norm_adv;
+  float gamma, lam;
+  float* ret_w; float* adv_w;
+  const u16* h;              // [B, 512] bf16 (rollout activations)
+  const u16* Wh;             // [512, A1] bf16 shadow
+  u16* dh;                   // [B, 512] out
+  float* gWh; float* gbh; float* gbfc;
+  float* stats;
+  int B;
+};
+
+template <int AC>
+__global__ void __launch_bounds__(HB_THREADS) head_bwd_kernel(HeadBwdArgs a) {
+  constexpr int A1 = AC + 1;
+  __shared__ double sh[16 * 8];
+  __shared__ float s_dz[HB_MAXB * A1];
+  __shared__ float s_rew[HB_MAXB], s_val[HB_MAXB + 256], s_ret[HB_MAXB], s_adv[HB_MAXB];
+  __shared__ uint8_t s_dn[HB_MAXB];
+  __shared__ float s_red[8 * 64 * (A1 + 1)];    // per wave: 64 columns x (dWh | dbfc)
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int B = a.B;
+  const bool lead = blockIdx.x == 0;
+  const int col0 = blockIdx.x * 64;
+  // ---- every global operand in one round: rollout slabs into LDS, this thread's loss row and its head-phase
+  // operands (h rows, Wh columns) in registers
+  for (int i = tid; i < B; i += HB_THREADS) {
+    s_rew[i] = a.rew[i];
+    s_dn[i] = a.dn[i];
+  }
+  for (int i = tid; i < B + a.N; i += HB_THREADS) s_val[i] = a.val[i];
+  const bool row = tid < B;
+  const int rb = row ? tid : 0;
+  float zr[A1];
+#pragma unroll
+  for (int j = 0; j < A1; ++j) zr[j] = a.z[(int64_t)rb * A1 + j];
+  const int ab = a.act[rb];
+  const float lpo = a.logp_old[rb];
+  const int ck = lane & 7, rsub = wv * 8 + (lane >> 3);   // head phase: column chunk, first row
+  const int jc0 = col0 + ck * 8;                          // first of this thread's 8 columns
+  float wj[8][A1];
+#pragma unroll
+  for (int c = 0; c < 8; ++c)
+#pragma unroll
+    for (int q = 0; q < A1; ++q) wj[c][q] = bf2f(a.Wh[(jc0 + c) * A1 + q]);
+  uint4 hv[HB_RPT];
+#pragma unroll
+  for (int r = 0; r < HB_RPT; ++r) {
+    const int b = min(rsub + 64 * r, B - 1);
+    hv[r] = *reinterpret_cast<const uint4*>(a.h + (int64_t)b * HB_H + jc0);
+  }
+  const float c_ent = *a.ent_coef, beta = *a.kl_coef;
+  __syncthreads();
+  // ---- returns, EV-before, advantage statistics (same maths as ac_loss_kernel phase 0)
+  double s_r = 0, s_rr = 0, s_v = 0, s_vv = 0, s_rv = 0, s_a = 0, s_aa = 0;
+  if (row) {
+    const int idx = tid, t = idx / a.N, n = idx - t * a.N;
+    float R;
+    if (a.returns_mode == 1) {
+      const int hh = min(t + a.L, a.T);
+      float acc = 0.f, disc = 1.f;
+      bool alive = true;
+      for (int k = t; k < hh; ++k) {
+        const int i = k * a.N + n;
+        acc += disc * s_rew[i];
+        disc *= a.gamma;
+        if (s_dn[i]) { alive = false; break; }
+      }
+      if (alive) acc += disc * s_val[hh * a.N + n];
+      R = acc;
+    } else {
+      float last = 0.f;
+      for (int k = a.T - 1; k >= t; --k) {
+        const int i = k * a.N + n;
+        const float nd = s_dn[i] ? 0.f : 1.f;
+        const float delta = s_rew[i] + a.gamma * s_val[i + a.N] * nd - s_val[i];
+        last = delta + a.gamma * a.lam * nd * last;
+      }
+      R = last + s_val[idx];
+    }
+    const float v = s_val[idx], A_ = R - v;
+    if (lead) {
+      a.ret_w[idx] = R;
+      a.adv_w[idx] = A_;
+    }
+    s_ret[idx] = R;
+    s_adv[idx] = A_;
+    s_r = R; s_rr = (double)R * R; s_v = v; s_vv = (double)v * v; s_rv = (double)R * v; s_a = A_;
+    s_aa = (double)A_ * A_;
+  }
+  double red[7] = {s_r, s_rr, s_v, s_vv, s_rv, s_a, s_aa};
+  block_sum_multi<7>(red, sh);
+  const double nB = B;
+  if (lead && tid == 0) {
+    const double mr = red[0] / nB, mv = red[2] / nB;
+    const double vr = fmax(red[1] / nB - mr * mr, 0.0), vv = fmax(red[3] / nB - mv * mv, 0.0);
+    a.stats[7] = (float)((red[4] / nB - mr * mv) / sqrt(vr * vv));
+  }
+  float adv_mean = 0.f, adv_inv = 1.f;
+  if (a.norm_adv) {
+    const double m = red[5] / nB, var = fmax(red[6] / nB - m * m, 0.0);
+    adv_mean = (float)m;
+    adv_inv = 1.0f / (1e-8f + (float)sqrt(var));
+  }
+  // ---- loss + dz (A2C: PG + KL proxy + entropy; value MSE)
+  const float invB = 1.0f / (float)B;
+  double s_pg = 0, s_kl = 0, s_H = 0, s_vl = 0;
+  if (row) {
+    const float adv = (s_adv[tid] - adv_mean) * adv_inv;
+    const float R = s_ret[tid];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < AC; ++j) mx = fmaxf(mx, zr[j]);
+    float se = 0.f;
+#pragma unroll
+    for (int j = 0; j < AC; ++j) se += expf(zr[j] - mx);
+    const float lse = mx + logf(se);
+    float H = 0.f, lpa = 0.f;
+#pragma unroll
+    for (int j = 0; j < AC; ++j) {
+      const float lz = zr[j] - lse;
+      H -= expf(lz) * lz;
+      lpa = (j == ab) ? lz : lpa;
+    }
+    s_pg = -(double)(adv * lpa);
+    const float dkl = lpo - lpa;
+    s_kl = (double)(dkl * dkl);
+    s_H = H;
+    const float g_lpa = -adv * invB - 2.0f * beta * dkl * invB;
+#pragma unroll
+    for (int j = 0; j < AC; ++j) {
+      const float lz = zr[j] - lse, pj = expf(lz);
+      const float g = g_lpa * (((j == ab) ? 1.0f : 0.0f) - pj) + c_ent * invB * pj * (lz + H);
+      s_dz[tid * A1 + j] = bf2f(f2bf(g));   // the bf16 rounding the GEMM path's dz buffer applied
+    }
+    const float d = zr[AC] - R;
+    s_vl = (double)(d * d);
+    s_dz[tid * A1 + AC] = bf2f(f2bf(a.vf_coef * 2.0f * d * invB));
+  }
+  {
+    double r4[4] = {s_pg, s_kl, s_H, s_vl};
+    block_sum_multi<4>(r4, sh);   // ends with a barrier: s_dz complete
+    if (lead && tid == 0) {
+      const double inv = 1.0 / B;
+      a.stats[0] = (float)(r4[0] * inv);
+      a.stats[1] = (float)(r4[1] * inv);
+      a.stats[2] = (float)(r4[2] * inv);
+      a.stats[3] = (float)(r4[3] * inv);
+      a.stats[4] = 0.f;
+      a.stats[5] = (float)(r4[0] * inv + beta * r4[1] * inv - c_ent * r4[2] * inv);
+      a.stats[6] = 1.f;
+    }
+  }
+  // ---- head backward over this thread's rows x 8 columns
+  float dwp[8][A1], dbf[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    dbf[c] = 0.f;
+#pragma unroll
+    for (int q = 0; q < A1; ++q) dwp[c][q] = 0.f;
+  }
+#pragma unroll
+  for (int r = 0; r < HB_RPT; ++r) {
+    const int b = rsub + 64 * r;
+    if (b < B) {
+      float dzb[A1];
+#pragma unroll
+      for (int q = 0; q < A1; ++q) dzb[q] = s_dz[b * A1 + q];
+      const uint32_t hw[4] = {hv[r].x, hv[r].y, hv[r].z, hv[r].w};
+      uint32_t out[4];
+#pragma unroll
+      for (int c2 = 0; c2 < 4; ++c2) {
+        uint32_t packed = 0;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int c = 2 * c2 + e;
+          const float hf = __uint_as_float(e ? (hw[c2] & 0xFFFF0000u) : (hw[c2] << 16));
+          float sacc = 0.f;
+#pragma unroll
+          for (int q = 0; q < A1; ++q) {
+            sacc += dzb[q] * wj[c][q];
+            dwp[c][q] += hf * dzb[q];
+          }
+          const float d = hf > 0.f ? sacc : 0.f;
+          dbf[c] += d;
+          packed |= (uint32_t)f2bf(d) << (16 * e);
+        }
+        out[c2] = packed;
+      }
+      *reinterpret_cast<uint4*>(a.dh + (int64_t)b * HB_H + jc0) = make_uint4(out[0], out[1], out[2], out[3]);
+    }
+  }
+  // per-wave column sums: lanes l, l ^ 8, l ^ 16, l ^ 32 share a column chunk (xor tree, fixed order)
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+#pragma unroll
+    for (int o = 8; o < 64; o <<= 1) {
+      dbf[c] += __shfl_xor(dbf[c], o, 64);
+#pragma unroll
+      for (int q = 0; q < A1; ++q) dwp[c][q] += __shfl_xor(dwp[c][q], o, 64);
+    }
+  }
+  if (lane < 8) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      float* dstw = s_red + (wv * 64 + lane * 8 + c) * (A1 + 1);
+#pragma unroll
+      for (int q = 0; q < A1; ++q) dstw[q] = dwp[c][q];
+      dstw[A1] = dbf[c];
+    }
+  }
+  __syncthreads();
+  if (tid < 64 * (A1 + 1)) {   // (column, value) pairs: the 8 waves in wave order
+    const int cl = tid / (A1 + 1), q = tid - cl * (A1 + 1);
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) v += s_red[(w * 64 + cl) * (A1 + 1) + q];
+    if (q < A1) a.gWh[(col0 + cl) * A1 + q] = v;
+    else a.gbfc[col0 + cl] = v;
+  }
+  if (lead && tid < A1) {   // head-bias gradient: column sums of dz in row order
+    float sb = 0.f;
+    for (int bb = 0; bb < B; ++bb) sb += s_dz[bb * A1 + tid];
+    a.gbh[tid] = sb;
+  }
+}
+
 }  // namespace aca
+
+extern "C" hipError_t aca_head_bwd(const float* z, const int32_t* act, const float* logp_old, const float* ent_coef,
+                                   const float* kl_coef, float vf_coef, const float* rew, const float* val,
+                                   const uint8_t* dn, int T, int N, int L, int returns_mode, int norm_adv, float gamma,
+                                   float lam, float* ret_w, float* adv_w, const uint16_t* h, const uint16_t* Wh,
+                                   uint16_t* dh, float* gWh, float* gbh, float* gbfc, float* stats, int A,
+                                   hipStream_t stream) {
+  const int B = T * N;
+  if (B < 1 || B > aca::HB_MAXB || N > 256 || A < 2 || A > 7 || (returns_mode != 1 && returns_mode != 2))
+    return hipErrorInvalidValue;
+  aca::HeadBwdArgs a{z, act, logp_old, ent_coef, kl_coef, vf_coef, rew, val, dn, T, N, L, returns_mode, norm_adv,
+                     gamma, lam, ret_w, adv_w, h, Wh, dh, gWh, gbh, gbfc, stats, B};
+  switch (A) {
+#define ACA_HB_CASE(n) \
+  case n: aca::head_bwd_kernel<n><<<aca::HB_WG, aca::HB_THREADS, 0, stream>>>(a); break;
+    ACA_HB_CASE(2) ACA_HB_CASE(3) ACA_HB_CASE(4) ACA_HB_CASE(5) ACA_HB_CASE(6) ACA_HB_CASE(7)
+#undef ACA_HB_CASE
+  }
+  return hipGetLastError();
+}
 
 extern "C" hipError_t aca_ac_loss(const float* logits, int64_t ldl, const float* value, int64_t ldv,
                                   const int32_t* act_i, const float* act_f, const float* log_std,

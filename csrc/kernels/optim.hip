@@ -198,129 +198,107 @@ __global__ void __launch_bounds__(OPT_THREADS) opt_multi_kernel(OptMulti M, floa
   opt_body<ADAM>(M.seg[k], b1, b2, eps, zero_grad, b, M.seg[k].nblocks, &flag, shr);
 }
 
-// Gradient finaliser: the last step of a backward pass before the optimiser. Segments (concatenated into one
-// virtual index space) are either already-final gradients (src == null: read for the norm only) or reductions of
-// S partial planes in plane order -- split-K weight-gradient planes, per-sample bias-gradient rows --
-// dst[i] = sum_{z < S} src[z * stride + i]  (deterministic: fixed order, no atomics). Every workgroup writes the
-// sum of squares of its share of the final gradient into its own partial slot (SUMSQ_PARTS slots, the unused ones
-// zeroed), which the optimiser reduces in a fixed order: the global-norm clip needs no separate sumsq pass.
-struct FinSeg {
-  float* dst; const float* src; int64_t n; int64_t stride; int64_t S; int64_t vec;
-};
-constexpr int FIN_MAXSEG = 24;
-struct FinArgs {
-  FinSeg seg[FIN_MAXSEG];
-  int64_t off[FIN_MAXSEG + 1];   // prefix offsets of the segments in the virtual index space (multiples of 4)
-  int nseg;
-  int64_t chunk;                 // elements per workgroup (multiple of 4)
-};
+// Gradient finaliser: the last step of a backward pass before the optimiser. Gradient segments are either
+// already final (src == null: read for the norm only) or reductions of S partial planes in plane order -- split-K
+// weight-gradient planes, per-sample bias-gradient rows -- dst[i] = sum_{z < S} src[z * stride + i]
+// (deterministic: fixed order, no atomics). The host cuts the segments into at most SUMSQ_PARTS jobs (one per
+// workgroup, sized so that no thread walks a long dependent chain of loads); every workgroup writes the sum of
+// squares of its share of the final gradient into its own partial slot (the unused slots zeroed), which the
+// optimiser reduces in a fixed order: the global-norm clip needs no separate sum-of-squares pass.
+// Job record (8 int64 words): dst, src, n, stride, S, (unused x3). dst / src / stride are float4-aligned when the
+// job's flag word 5 is 1 (host-checked).
+constexpr int FIN_WORDS = 8;
 
-// sum of planes z = z0, z0 + dz, ... < S of element i, 16 loads in flight per round (fixed order: deterministic;
-// out-of-range slots of the last round read plane z0 and are discarded by a select)
-__device__ __forceinline__ float plane_sum(const float* __restrict__ src, int64_t stride, int64_t i, int64_t z0,
-                                           int64_t dz, int64_t S) {
-  float acc = 0.f;
-  for (int64_t z = z0; z < S; z += 16 * dz) {
-    float v[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int64_t zz = z + u * dz;
-      v[u] = src[(zz < S ? zz : z0) * stride + i];
-    }
-#pragma unroll
-    for (int u = 0; u < 16; ++u) acc += (z + u * dz < S) ? v[u] : 0.f;
-  }
-  return acc;
-}
-
-__device__ __forceinline__ float4 plane_sum4(const float* __restrict__ src, int64_t stride, int64_t i, int64_t S) {
-  float4 a[4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) a[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-  int64_t z = 0;
-  for (; z + 3 < S; z += 4) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const float4 q = *reinterpret_cast<const float4*>(src + (z + u) * stride + i);
-      a[u].x += q.x; a[u].y += q.y; a[u].z += q.z; a[u].w += q.w;
-    }
-  }
-  for (int u = 0; z < S; ++z, ++u) {
-    const float4 q = *reinterpret_cast<const float4*>(src + z * stride + i);
-    a[u & 3].x += q.x; a[u & 3].y += q.y; a[u & 3].z += q.z; a[u & 3].w += q.w;
-  }
-  return make_float4((a[0].x + a[1].x) + (a[2].x + a[3].x), (a[0].y + a[1].y) + (a[2].y + a[3].y),
-                     (a[0].z + a[1].z) + (a[2].z + a[3].z), (a[0].w + a[1].w) + (a[2].w + a[3].w));
-}
-
-__global__ void __launch_bounds__(OPT_THREADS) grad_finalize_kernel(FinArgs F, float* __restrict__ partial) {
+__global__ void __launch_bounds__(OPT_THREADS) grad_finalize_kernel(const int64_t* __restrict__ jobs, int njobs,
+                                                                    float* __restrict__ partial) {
   __shared__ float sh[16];
   __shared__ float red[OPT_THREADS];
-  const int64_t v0 = (int64_t)blockIdx.x * F.chunk, v1 = min(v0 + F.chunk, F.off[F.nseg]);
+  const int64_t* w = jobs + (int64_t)blockIdx.x * FIN_WORDS;
+  float* dst = reinterpret_cast<float*>(w[0]);
+  const float* src = reinterpret_cast<const float*>(w[1]);
+  const int n = (int)w[2], S = (int)w[4], vec = (int)w[5];
+  const int64_t stride = w[3];
+  const int tid = threadIdx.x;
   float s = 0.f;
-  for (int k = 0; k < F.nseg; ++k) {
-    const FinSeg G = F.seg[k];
-    const int64_t a = max(v0, F.off[k]) - F.off[k], e = min(min(v1, F.off[k + 1]) - F.off[k], G.n);
-    if (a >= e) continue;
-    if (G.src && G.S > 32 && e - a <= 64) {
-      // few elements, many planes (per-sample bias rows): 64 elements x 4 plane groups, combined in LDS in group
-      // order -- the planes of one element are spread over four threads instead of one long dependent chain
-      const int el = threadIdx.x & 63, pg = threadIdx.x >> 6;
-      const int64_t i = a + el;
-      const float part = i < e ? plane_sum(G.src, G.stride, i, pg, 4, G.S) : 0.f;
-      __syncthreads();
-      red[threadIdx.x] = part;
-      __syncthreads();
-      if (threadIdx.x < 64 && i < e) {
-        const float v = (red[el] + red[64 + el]) + (red[128 + el] + red[192 + el]);
-        G.dst[i] = v;
-        s += v * v;
-      }
-    } else if (!G.src && G.vec && (a & 3) == 0) {
-      // read-only float4 path (norm only): 8 independent 16-byte loads per thread in flight per round
-      const int64_t e4 = a + ((e - a) & ~(int64_t)3);
-      for (int64_t i0 = a + 4 * threadIdx.x; i0 < e4; i0 += 4 * OPT_THREADS * 8) {
+  if (!src) {
+    if (vec) {   // read-only, 8 independent 16-byte loads per thread in flight
+      const int n4 = n >> 2;
+      for (int i0 = tid; i0 < n4; i0 += OPT_THREADS * 8) {
         float4 v[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          const int64_t i = i0 + 4 * OPT_THREADS * u;
-          v[u] = *reinterpret_cast<const float4*>(G.dst + (i < e4 ? i : a));
+          const int i = i0 + OPT_THREADS * u;
+          v[u] = reinterpret_cast<const float4*>(dst)[i < n4 ? i : 0];
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u)
-          if (i0 + 4 * OPT_THREADS * u < e4) s += v[u].x * v[u].x + v[u].y * v[u].y + v[u].z * v[u].z + v[u].w * v[u].w;
+          if (i0 + OPT_THREADS * u < n4) s += v[u].x * v[u].x + v[u].y * v[u].y + v[u].z * v[u].z + v[u].w * v[u].w;
       }
-      for (int64_t i = e4 + threadIdx.x; i < e; i += OPT_THREADS) s += G.dst[i] * G.dst[i];
-    } else if (G.vec && (a & 3) == 0) {
-      // float4 path: dst / src / stride 16-byte aligned (host-checked), the range starts on a float4
-      const int64_t e4 = a + ((e - a) & ~(int64_t)3);
-      for (int64_t i = a + 4 * threadIdx.x; i < e4; i += 4 * OPT_THREADS) {
-        float4 v;
-        if (G.src) {
-          v = plane_sum4(G.src, G.stride, i, G.S);
-          *reinterpret_cast<float4*>(G.dst + i) = v;
-        } else {
-          v = *reinterpret_cast<const float4*>(G.dst + i);
-        }
-        s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
-      }
-      for (int64_t i = e4 + threadIdx.x; i < e; i += OPT_THREADS) {
-        const float v = G.src ? plane_sum(G.src, G.stride, i, 0, 1, G.S) : G.dst[i];
-        if (G.src) G.dst[i] = v;
-        s += v * v;
-      }
+      for (int i = 4 * n4 + tid; i < n; i += OPT_THREADS) s += dst[i] * dst[i];
     } else {
-      for (int64_t i = a + threadIdx.x; i < e; i += OPT_THREADS) {
-        const float v = G.src ? plane_sum(G.src, G.stride, i, 0, 1, G.S) : G.dst[i];
-        if (G.src) G.dst[i] = v;
-        s += v * v;
+      for (int i = tid; i < n; i += OPT_THREADS) s += dst[i] * dst[i];
+    }
+  } else if (n <= 64) {
+    // few elements, many planes (per-sample bias rows): 64 elements x 4 plane groups, 16 loads in flight per
+    // thread, the groups combined in LDS in group order
+    const int el = tid & 63, pg = tid >> 6;
+    float acc = 0.f;
+    if (el < n) {
+      for (int z0 = pg; z0 < S; z0 += 64) {
+        float v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const int z = z0 + 4 * u;
+          v[u] = src[(int64_t)(z < S ? z : pg) * stride + el];
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) acc += (z0 + 4 * u < S) ? v[u] : 0.f;
       }
+    }
+    red[tid] = acc;
+    __syncthreads();
+    if (tid < n) {
+      const float v = (red[tid] + red[64 + tid]) + (red[128 + tid] + red[192 + tid]);
+      dst[tid] = v;
+      s = v * v;
+    }
+  } else if (vec) {
+    // planes, float4 elements: 8 planes per round in flight, elements striding over the workgroup
+    const int n4 = n >> 2;
+    for (int i = tid; i < n4; i += OPT_THREADS) {
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int z0 = 0; z0 < S; z0 += 8) {
+        float4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int z = z0 + u < S ? z0 + u : 0;
+          v[u] = *reinterpret_cast<const float4*>(src + (int64_t)z * stride + 4 * (int64_t)i);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (z0 + u < S) { acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w; }
+      }
+      reinterpret_cast<float4*>(dst)[i] = acc;
+      s += acc.x * acc.x + acc.y * acc.y + acc.z * acc.z + acc.w * acc.w;
+    }
+    for (int i = 4 * n4 + tid; i < n; i += OPT_THREADS) {
+      float v = 0.f;
+      for (int z = 0; z < S; ++z) v += src[(int64_t)z * stride + i];
+      dst[i] = v;
+      s += v * v;
+    }
+  } else {
+    for (int i = tid; i < n; i += OPT_THREADS) {
+      float v = 0.f;
+      for (int z = 0; z < S; ++z) v += src[(int64_t)z * stride + i];
+      dst[i] = v;
+      s += v * v;
     }
   }
   if (blockIdx.x == 0)
-    for (int b = gridDim.x + threadIdx.x; b < SUMSQ_PARTS; b += blockDim.x) partial[b] = 0.f;
+    for (int b = njobs + tid; b < SUMSQ_PARTS; b += OPT_THREADS) partial[b] = 0.f;
   s = block_sum(s, sh);
-  if (threadIdx.x == 0) partial[blockIdx.x] = s;
+  if (tid == 0) partial[blockIdx.x] = s;
 }
 
 // lag-1 data parallelism: dst <- src, src <- 0 in one pass (the next backward accumulates into a clean slab while
@@ -368,34 +346,10 @@ extern "C" hipError_t aca_sumsq(const float* x, size_t n, float* partial, hipStr
 
 extern "C" int aca_sumsq_parts() { return SUMSQ_PARTS; }
 
-// segs: nseg records of 6 int64 words (dst, src, n, stride, S, unused); partial: SUMSQ_PARTS floats
-extern "C" hipError_t aca_grad_finalize(const int64_t* words, int nseg, float* partial, hipStream_t stream) {
-  if (nseg < 1 || nseg > FIN_MAXSEG) return hipErrorInvalidValue;
-  FinArgs F{};
-  F.nseg = nseg;
-  F.off[0] = 0;
-  for (int k = 0; k < nseg; ++k) {
-    const int64_t* w = words + 6 * k;
-    FinSeg& G = F.seg[k];
-    G.dst = reinterpret_cast<float*>(w[0]);
-    G.src = reinterpret_cast<const float*>(w[1]);
-    G.n = w[2];
-    G.stride = w[3];
-    G.S = w[4];
-    if (!G.dst || G.n < 0 || (G.src && G.S < 1)) return hipErrorInvalidValue;
-    G.vec = (reinterpret_cast<uintptr_t>(G.dst) % 16 == 0) &&
-            (!G.src || (reinterpret_cast<uintptr_t>(G.src) % 16 == 0 && G.stride % 4 == 0));
-    F.off[k + 1] = F.off[k] + (G.n + 3) / 4 * 4;   // segments start on float4 boundaries of the virtual space
-  }
-  const int64_t total = F.off[nseg];
-  if (total == 0) return hipSuccess;
-  // as many workgroups as the norm has partial slots, each a multiple-of-4 share (>= 1024 elements)
-  int64_t chunk = (total + SUMSQ_PARTS - 1) / SUMSQ_PARTS;
-  chunk = (chunk + 3) / 4 * 4;
-  if (chunk < 1024) chunk = 1024;
-  F.chunk = chunk;
-  const int grid = (int)((total + chunk - 1) / chunk);
-  grad_finalize_kernel<<<grid, OPT_THREADS, 0, stream>>>(F, partial);
+// jobs: device int64 [njobs, FIN_WORDS] (built by the host, ops/optim.py finalize_jobs); partial: SUMSQ_PARTS floats
+extern "C" hipError_t aca_grad_finalize(const int64_t* jobs, int njobs, float* partial, hipStream_t stream) {
+  if (njobs < 1 || njobs > SUMSQ_PARTS) return hipErrorInvalidValue;
+  grad_finalize_kernel<<<njobs, OPT_THREADS, 0, stream>>>(jobs, njobs, partial);
   return hipGetLastError();
 }
 

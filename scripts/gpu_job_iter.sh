@@ -7,6 +7,7 @@ TAG=${1:-iter}
 shift
 O=gpurun_out/$TAG
 mkdir -p $O
+python -c "from actor_critic_algs_on_tensorflow_amd import _native; _native.load(raise_on_error=True)" || exit 3
 timeout -k 10 400 python -u -m pytest tests/test_gpu_r2.py tests/test_gpu_kernels.py tests/test_gpu_dp.py -x -q --timeout 120 --timeout-method thread > $O/tests_r2.log 2>&1
 rc=$?; echo "tests_r2 rc=$rc"; tail -5 $O/tests_r2.log
 [ $rc -ne 0 ] && exit $rc

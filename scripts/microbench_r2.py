@@ -83,9 +83,11 @@ def main():
                workspace=eng.ws, ga=[5, B, 64, 20, 20, 4, 4, 2], gb=[6, 1, 64, 1, 32, 4, 4, 2])
     cands["bwd_gemms_dy2_dy1"] = gemms
     cands["finalize_engine"] = lambda: eng.finalize(lb)
-    fw = eng._fin_words[(lb.B, eng.want_parts, eng.fused_bwd)]
-    bias_w = fw[fw[:, 1] != 0].clone()
+    fw = list(eng._fin_words.values())[-1]
+    bias_w = fw[(fw[:, 1] != 0) & (fw[:, 2] <= 64)].clone()
+    plane_w = fw[(fw[:, 1] != 0) & (fw[:, 2] > 64)].clone()
     ro_w = fw[fw[:, 1] == 0].clone()
+    cands["finalize_planes_only"] = lambda: ops.grad_finalize(plane_w, eng.fin_parts)
     cands["finalize_bias_only"] = lambda: ops.grad_finalize(bias_w, eng.fin_parts)
     cands["finalize_readonly_only"] = lambda: ops.grad_finalize(ro_w, eng.fin_parts)
     cands["sumsq_slab"] = lambda: ops.sumsq(eng.flat.grad, eng.fin_parts)

@@ -81,13 +81,14 @@ def test_trunk_bwd_matches_conv_transpose(cuda, B):
     assert torch.equal(dy1b.view(torch.int16), dy1.view(torch.int16)) and torch.equal(bpb, bp)
 
 
-def _one_update(fused, algo="pong_a2c", **kw):
+def _one_update(fused, algo="pong_a2c", head=True, **kw):
     from actor_critic_algs_on_tensorflow_amd import preset
     from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
     cfg = preset(algo, num_envs=8, device="cuda:0", outdir=None, quiet=True, stdout_freq=0, save_every=0,
                  cuda_graph=False, optimizer="adam", **kw)
     tr = ActorCriticTrainer(cfg)
     tr.engine.fused_bwd = fused
+    tr.engine.fused_head = head
     p0 = tr.flat.data.clone()
     tr.step()
     torch.cuda.synchronize()
@@ -116,9 +117,10 @@ def test_grad_finalize_planes_and_norm(cuda):
     rows = torch.randn(33, 160, generator=g).to(cuda)       # per-sample rows, columns 64..127 -> a 64-element bias
     dA, dB = slab[10:1013], slab[2000:2064]
     ro = slab[3000:70001]
-    words = torch.tensor([[dA.data_ptr(), planes.data_ptr(), 1003, 1003, 7, 0],
-                          [dB.data_ptr(), rows.data_ptr() + 64 * 4, 64, 160, 33, 0],
-                          [ro.data_ptr(), 0, ro.numel(), 0, 0, 0]], dtype=torch.int64)
+    from actor_critic_algs_on_tensorflow_amd.ops.optim import finalize_jobs
+    words = finalize_jobs([(dA.data_ptr(), planes.data_ptr(), 1003, 1003, 7),
+                           (dB.data_ptr(), rows.data_ptr() + 64 * 4, 64, 160, 33),
+                           (ro.data_ptr(), 0, ro.numel(), 0, 0)], cuda)
     keep = ro.clone()
     parts = torch.full((256,), float("nan"), device=cuda)
     ops.grad_finalize(words, parts)
@@ -129,3 +131,30 @@ def test_grad_finalize_planes_and_norm(cuda):
     tot = float(parts.double().sum())
     ref = float(dA.double().pow(2).sum() + dB.double().pow(2).sum() + ro.double().pow(2).sum())
     assert abs(tot - ref) <= 1e-4 * ref
+
+
+@pytest.mark.parametrize("norm_adv,returns", [(False, "nstep"), (True, "gae")])
+def test_fused_head_matches_loss_plus_head_gemms(cuda, norm_adv, returns):
+    """head_bwd (loss + dz + dh + dWh + dbh + dbfc in one launch) == ac_loss + the dh / dWh GEMMs + colsums: same
+    statistics, same update up to summation order."""
+    d1, s1 = _one_update(True, head=True, norm_adv=norm_adv, returns=returns)
+    d0, s0 = _one_update(True, head=False, norm_adv=norm_adv, returns=returns)
+    assert torch.allclose(s0[:8], s1[:8], rtol=1e-4, atol=1e-6), (s0[:8], s1[:8])
+    assert (d0 - d1).norm() / d0.norm() < 1e-2, float((d0 - d1).norm() / d0.norm())
+
+
+def test_a2c_update_is_bitwise_deterministic(cuda):
+    """Two identical native A2C runs (graph-captured, 5 updates) end bit-identical."""
+    from actor_critic_algs_on_tensorflow_amd import preset
+    from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
+    outs = []
+    for _ in range(2):
+        cfg = preset("pong_a2c", num_envs=16, device="cuda:0", outdir=None, quiet=True, stdout_freq=0, save_every=0)
+        tr = ActorCriticTrainer(cfg)
+        tr.capture(warmup=1)
+        for _ in range(5):
+            tr.step()
+        torch.cuda.synchronize()
+        outs.append((tr.flat.data.clone(), tr.stats_buf.clone()))
+    assert torch.equal(outs[0][0], outs[1][0]), "parameters differ between identical runs"
+    assert torch.equal(outs[0][1], outs[1][1])

@@ -37,6 +37,7 @@ from .. import _native
 from ..ops import gemm as G
 
 H0 = 84
+FC_PLANES = 32   # split-K partial planes of the rollout fc product (cnn_head.h FC_MAX_PLANES)
 
 
 class _Bufs:
@@ -105,12 +106,14 @@ class CNNEngine:
         # conv weight gradients as split-K partial planes reduced in plane order by the finaliser (deterministic);
         # 0: split-K fp32 atomics into the slab (nondeterministic summation order)
         self.det_wgrad = implicit and os.environ.get("ACA_DET_WGRAD", "1") != "0"
-        self.wgrad_planes = 32
+        self.wgrad_planes = int(os.environ.get("ACA_WGRAD_PLANES", "32"))
         self._planes = {}
         self._wsplits = {}
         self._fin_words = {}
         # rollout fc product left as split-K partial planes, reduced by its consumer kernel (no in-launch fence)
         self.fc_parts = os.environ.get("ACA_FC_PARTS", "1") != "0"
+        # split-K planes the fc GEMM may use (more planes: more workgroups stream Wfc, more for the consumer to sum)
+        self.fc_max_planes = min(FC_PLANES, int(os.environ.get("ACA_FC_MAX_PLANES", "32")))
         self._hpart = {}
         self.last_fc = None
         self.model = model
@@ -151,9 +154,9 @@ class CNNEngine:
 
     # ------------------------------------------------------------------------------------------------ forward
     def hpart(self, B):
-        """fp32 [8, B, 512] split-K partial planes of the rollout fc product (GEMM out_mode 3)."""
+        """fp32 [FC_PLANES, B, 512] split-K partial planes of the rollout fc product (GEMM out_mode 3)."""
         if B not in self._hpart:
-            self._hpart[B] = torch.zeros(8 * B * 512, dtype=torch.float32, device=self.dev)
+            self._hpart[B] = torch.zeros(FC_PLANES * B * 512, dtype=torch.float32, device=self.dev)
         return self._hpart[B]
 
     def value(self, obs, b: _Bufs, out):
@@ -205,7 +208,8 @@ class CNNEngine:
             # partial planes only: the consumer (fused policy/env kernel or fc_value) reduces, adds the bias,
             # applies ReLU and writes b.h
             hp = self.hpart(B)
-            S = G.gemm(b.y3, 3136, True, self.sWfc, 512, False, hp, 512, 3, B, 512, 3136, workspace=ws)
+            S = G.gemm(b.y3, 3136, True, self.sWfc, 512, False, hp, 512, 3, B, 512, 3136, workspace=ws,
+                       max_planes=self.fc_max_planes)
             self.last_fc = (hp, S)
             return shifted if want_shift else b.z
         G.gemm(b.y3, 3136, True, self.sWfc, 512, False, b.h, 512, 1, B, 512, 3136, bias=self.bfc, relu=True,

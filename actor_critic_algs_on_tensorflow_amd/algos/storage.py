@@ -16,11 +16,43 @@ from __future__ import annotations
 import torch
 
 
+class _ObsRing:
+    """``obs[t]`` of a ring of 2T observation slots: rollout k uses slots ``phase*T .. phase*T + T`` (mod 2T), so
+    the last observation of one rollout IS the first of the next -- the rollover is a phase flip, not a copy of
+    the whole frame stack (903 KB for the bench's 32 Atari envs: a copy launch + a kernel boundary per update)."""
+
+    def __init__(self, st):
+        self.st = st
+
+    def __getitem__(self, t):
+        st = self.st
+        if not isinstance(t, int) or not 0 <= t <= st.T:
+            raise IndexError("ring observation slots take an int in [0, T]")
+        return st.slots[(st.phase * st.T + t) % (2 * st.T)]
+
+    def __len__(self):
+        return self.st.T + 1
+
+    @property
+    def dtype(self):
+        return self.st.slots.dtype
+
+    @property
+    def device(self):
+        return self.st.slots.device
+
+
 class RolloutStorage:
-    def __init__(self, T, N, obs_shape, obs_dtype, action_shape, action_dtype, device):
+    def __init__(self, T, N, obs_shape, obs_dtype, action_shape, action_dtype, device, ring=False):
         self.T, self.N = T, N
         dev = torch.device(device)
-        self.obs = torch.zeros((T + 1, N) + tuple(obs_shape), dtype=obs_dtype, device=dev)
+        self.ring = bool(ring)
+        self.phase = 0
+        if self.ring:
+            self.slots = torch.zeros((2 * T, N) + tuple(obs_shape), dtype=obs_dtype, device=dev)
+            self.obs = _ObsRing(self)
+        else:
+            self.obs = torch.zeros((T + 1, N) + tuple(obs_shape), dtype=obs_dtype, device=dev)
         self.actions = torch.zeros((T, N) + tuple(action_shape), dtype=action_dtype, device=dev)
         self.logp = torch.zeros(T, N, dtype=torch.float32, device=dev)
         self.entropy = torch.zeros(T, N, dtype=torch.float32, device=dev)
@@ -31,15 +63,22 @@ class RolloutStorage:
         self.keys = torch.zeros(T, N, dtype=torch.int64, device=dev)
 
     def flat(self, name):
+        if name == "obs" and self.ring:   # this rollout's T slots are contiguous in the ring
+            x = self.slots[self.phase * self.T:(self.phase + 1) * self.T]
+            return x.reshape((self.T * self.N,) + tuple(x.shape[2:]))
         x = getattr(self, name)
         if name in ("obs", "values"):
             x = x[:self.T]
         return x.reshape((self.T * self.N,) + tuple(x.shape[2:]))
 
     def roll_over(self):
-        """The last observation becomes the first of the next rollout."""
-        self.obs[0].copy_(self.obs[self.T])
+        """The last observation becomes the first of the next rollout (ring: flip the phase, no copy)."""
+        if self.ring:
+            self.phase ^= 1
+        else:
+            self.obs[0].copy_(self.obs[self.T])
 
     def nbytes(self):
-        return sum(t.numel() * t.element_size() for t in (self.obs, self.actions, self.logp, self.entropy,
+        obs = self.slots if self.ring else self.obs
+        return sum(t.numel() * t.element_size() for t in (obs, self.actions, self.logp, self.entropy,
                                                           self.rewards, self.dones, self.values, self.keys))

@@ -110,7 +110,7 @@ class ActorCriticTrainer:
         act_shape = () if self.env.is_discrete else tuple(self.env.action_space.shape)
         act_dtype = torch.int32 if self.env.is_discrete else torch.float32
         self.storage = RolloutStorage(T, N, self.env.obs_shape, self.env.obs_dtype, act_shape, act_dtype,
-                                      self.device)
+                                      self.device, ring=self.engine is not None)
         if cfg.bootstrap_on_timeout:
             self.env.keep_final_obs = True   # the torch env step keeps the pre-reset observation (envs/base.py)
         self.env.reset(out=self.storage.obs[0])
@@ -605,13 +605,29 @@ class ActorCriticTrainer:
                 self.update_body()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
+        st = self.storage
+        if st.ring:
+            # one graph set per ring phase (their slot addresses differ); capturing runs nothing, and each set
+            # flips the host-side phase once, so after both captures host phase == device state again
+            p0 = st.phase
+            first = self._capture_set()
+            second = self._capture_set()
+            assert st.phase == p0
+            self._graph_sets = {p0: first, 1 - p0: second}
+            self.graph = first
+            return self.graph
+        self.graph = self._capture_set()
+        return self.graph
+
+    def _capture_set(self):
         if self._segmented():
             self._defer_allreduce = True
             try:
                 if self._lag1():
-                    self._comm_grad = torch.zeros_like(self.flat.grad)
-                    for opt in self.opts.values():
-                        opt.bind_grad(self._comm_grad)
+                    if self._comm_grad is None:   # one buffer shared by both ring-phase graph sets
+                        self._comm_grad = torch.zeros_like(self.flat.grad)
+                        for opt in self.opts.values():
+                            opt.bind_grad(self._comm_grad)
                     g1 = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g1):
                         self.update_body()
@@ -619,7 +635,7 @@ class ActorCriticTrainer:
                     with torch.cuda.graph(g2):
                         self._post_body()
                         self._grad_move()
-                    self.graph = ("lag1", g1, g2)
+                    graph = ("lag1", g1, g2)
                 else:
                     self._bw_stage = "tail"
                     g1 = torch.cuda.CUDAGraph()
@@ -636,7 +652,7 @@ class ActorCriticTrainer:
                     with torch.cuda.graph(g3):
                         self._post_body()
                         self.storage.roll_over()
-                    self.graph = ("strict", g1, g2, g3)
+                    graph = ("strict", g1, g2, g3)
             finally:
                 self._defer_allreduce = False
                 self._bw_stage = "all"
@@ -644,15 +660,22 @@ class ActorCriticTrainer:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 self.update_body()
-            self.graph = ("single", g)
-        return self.graph
+            graph = ("single", g)
+        return graph
 
     def _replay(self):
-        kind = self.graph[0]
+        st = self.storage
+        graph = self._graph_sets[st.phase] if st.ring else self.graph
+        self._replay_set(graph)
+        if st.ring:
+            st.phase ^= 1   # the replayed update ended with its rollover
+
+    def _replay_set(self, graph):
+        kind = graph[0]
         if kind == "single":
-            self.graph[1].replay()
+            graph[1].replay()
         elif kind == "strict":
-            _, g1, g2, g3 = self.graph
+            _, g1, g2, g3 = graph
             s, e = self.engine.tail_bucket()
             g1.replay()
             w_tail = self.dp.allreduce_async(self.flat.grad[s:e])   # overlaps the conv backward
@@ -662,7 +685,7 @@ class ActorCriticTrainer:
             w_trunk.wait()
             g3.replay()
         else:   # lag1
-            _, g1, g2 = self.graph
+            _, g1, g2 = graph
             g1.replay()                       # overlaps the all-reduce of the previous gradient
             if self._comm_work is None:       # first update: nothing to apply yet
                 self._grad_move()

@@ -100,6 +100,39 @@ def tuned_plans():
     return dict(_TUNED)
 
 
+# Tuned plans measured on an MI355X for the engine's shapes (scripts/dump_gemm_plans.py): loaded at import so runs
+# start with the measured winners (no tuning pass, and no run-to-run plan noise); shapes not in the file are still
+# tuned on first use. ACAMD_GEMM_PLANS=0 ignores the file.
+PLANS_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_plans.json")
+
+
+def _key_from_json(k):
+    return tuple(tuple(x) if isinstance(x, list) else x for x in k)
+
+
+def load_plans(path=PLANS_FILE):
+    import json
+    if not os.path.exists(path) or os.environ.get("ACAMD_GEMM_PLANS", "1") == "0":
+        return 0
+    with open(path) as f:
+        rows = json.load(f)
+    for r in rows:
+        _TUNED.setdefault(_key_from_json(r["key"]), tuple(r["plan"]))
+    return len(rows)
+
+
+def save_plans(path=PLANS_FILE):
+    import json
+    rows = [{"key": [list(x) if isinstance(x, tuple) else x for x in k], "plan": list(v)}
+            for k, v in sorted(_TUNED.items(), key=lambda kv: str(kv[0]))]
+    with open(path, "w") as f:
+        json.dump(rows, f, indent=0)
+    return len(rows)
+
+
+load_plans()
+
+
 def _candidates(M, N, K, atomic, max_splits=None, row_block=None):
     for tile, (bm, bn) in TILES.items():
         if row_block is not None and row_block % bm:

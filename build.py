@@ -68,7 +68,8 @@ def write_ninja(verbose=False):
     w("rule link\n  command = $cxx $in $ldflags -o $out\n  description = LINK $out")
     w("rule tblink\n  command = $cxx -shared $in -o $out\n  description = LINK $out")
     objs = []
-    hdr = " ".join(os.path.join(ROOT, "csrc", "kernels", h) for h in ("common.h", "gemm_impl.h", "gemm_desc.h", "mlp_desc.h"))
+    hdr = " ".join(os.path.join(ROOT, "csrc", "kernels", h)
+                   for h in ("common.h", "gemm_impl.h", "gemm_desc.h", "mlp_desc.h", "cnn_head.h"))
     for k in KERNELS:
         src = os.path.join(ROOT, "csrc", "kernels", k + ".hip")
         obj = os.path.join(BUILD_DIR, k + ".o")

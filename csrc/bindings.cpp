@@ -83,7 +83,7 @@ hipError_t aca_grad_finalize(const int64_t*, int, float*, hipStream_t);
 hipError_t aca_head_bwd(const float*, const int32_t*, const float*, const float*, const float*, float, const float*,
                         const float*, const uint8_t*, int, int, int, int, int, float, float, float*, float*,
                         const uint16_t*, const uint16_t*, uint16_t*, float*, float*, float*, float*, int,
-                        hipStream_t);
+                        uint64_t*, hipStream_t);
 hipError_t aca_cnn_trunk_bwd(const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*,
                              uint16_t*, uint16_t*, float*, int, uint64_t*, hipStream_t);
 hipError_t aca_cnn_trunk_rows(const uint8_t*, const uint16_t*, const float*, const uint16_t*, const float*,
@@ -244,8 +244,8 @@ void env_policy_step_pong(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, 
     need(*hpart, at::kFloat, "hpart");
     TORCH_CHECK(bfc.has_value() && bfc->defined() && bfc->numel() == hdim, "env_policy_step_pong: hpart needs bfc");
     need(*bfc, at::kFloat, "bfc");
-    TORCH_CHECK(planes >= 1 && planes <= 8 && hpart->numel() % 8 == 0, "env_policy_step_pong: 1..8 planes");
-    pstride = hpart->numel() / 8;   // buffer holds 8 planes of equal size
+    TORCH_CHECK(planes >= 1 && planes <= 32 && hpart->numel() % 32 == 0, "env_policy_step_pong: 1..32 planes");
+    pstride = hpart->numel() / 32;   // buffer holds 32 planes of equal size (engine.py FC_PLANES)
     TORCH_CHECK(pstride >= (int64_t)N * hdim, "env_policy_step_pong: hpart planes too small");
     hp = ptr<float>(*hpart);
     bf = ptr<float>(*bfc);
@@ -261,7 +261,7 @@ void env_policy_step_pong(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, 
         "env_policy_step_pong");
 }
 
-// bootstrap value from the fc partial planes (cnn_fused.hip); hpart holds 8 equal planes of [N, 512]
+// bootstrap value from the fc partial planes (cnn_fused.hip); hpart holds 32 equal planes of [N, 512]
 void fc_value(Tensor hpart, int64_t planes, Tensor bfc, Tensor Wh, Tensor bh, Tensor out, c10::optional<Tensor> h_out) {
   need(hpart, at::kFloat, "hpart");
   need(bfc, at::kFloat, "bfc");
@@ -269,9 +269,9 @@ void fc_value(Tensor hpart, int64_t planes, Tensor bfc, Tensor Wh, Tensor bh, Te
   need(bh, at::kFloat, "bh");
   need(out, at::kFloat, "out");
   const int N = out.numel(), A1 = bh.numel();
-  const int64_t pstride = hpart.numel() / 8;
-  TORCH_CHECK(hpart.numel() % 8 == 0 && pstride >= (int64_t)N * 512 && planes >= 1 && planes <= 8,
-              "fc_value: hpart must hold 8 planes of [N, 512]");
+  const int64_t pstride = hpart.numel() / 32;
+  TORCH_CHECK(hpart.numel() % 32 == 0 && pstride >= (int64_t)N * 512 && planes >= 1 && planes <= 32,
+              "fc_value: hpart must hold 32 planes of [N, 512]");
   TORCH_CHECK(bfc.numel() == 512 && Wh.numel() == 512 * A1, "fc_value: bad head shapes");
   uint16_t* ho = nullptr;
   if (h_out.has_value() && h_out->defined()) {
@@ -940,7 +940,7 @@ void grad_finalize(Tensor jobs, Tensor partial) {
 void head_bwd(Tensor z, Tensor act, Tensor logp_old, Tensor ent_coef, Tensor kl_coef, double vf_coef, Tensor rew,
               Tensor val, Tensor dones, int64_t L, int64_t returns_mode, bool norm_adv, double gamma, double lam,
               Tensor ret_w, Tensor adv_w, Tensor h, Tensor Wh, Tensor dh, Tensor gWh, Tensor gbh, Tensor gbfc,
-              Tensor stats) {
+              Tensor stats, c10::optional<Tensor> stamps) {
   TORCH_CHECK(rew.dim() == 2, "head_bwd: rewards must be [T, N]");
   const int T = rew.size(0), N = rew.size(1), B = T * N;
   TORCH_CHECK(z.dim() == 2 && z.size(0) >= B, "head_bwd: z must be [B, A + 1]");
@@ -961,7 +961,7 @@ void head_bwd(Tensor z, Tensor act, Tensor logp_old, Tensor ent_coef, Tensor kl_
                      ptr<float>(kl_coef), (float)vf_coef, ptr<float>(rew), ptr<float>(val), ptr<uint8_t>(dones), T, N,
                      (int)L, (int)returns_mode, norm_adv ? 1 : 0, (float)gamma, (float)lam, ptr<float>(ret_w),
                      ptr<float>(adv_w), ptr<uint16_t>(h), ptr<uint16_t>(Wh), ptr<uint16_t>(dh), ptr<float>(gWh),
-                     ptr<float>(gbh), ptr<float>(gbfc), ptr<float>(stats), A, cur_stream(z)),
+                     ptr<float>(gbh), ptr<float>(gbfc), ptr<float>(stats), A, stamps_ptr(stamps, 8), cur_stream(z)),
         "head_bwd");
 }
 
@@ -1160,7 +1160,8 @@ TORCH_LIBRARY(acamd, m) {
   m.def("grad_finalize(Tensor jobs, Tensor partial) -> ()");
   m.def("head_bwd(Tensor z, Tensor act, Tensor logp_old, Tensor ent_coef, Tensor kl_coef, float vf_coef, Tensor rew, "
         "Tensor val, Tensor dones, int L, int returns_mode, bool norm_adv, float gamma, float lam, Tensor ret_w, "
-        "Tensor adv_w, Tensor h, Tensor Wh, Tensor dh, Tensor gWh, Tensor gbh, Tensor gbfc, Tensor stats) -> ()");
+        "Tensor adv_w, Tensor h, Tensor Wh, Tensor dh, Tensor gWh, Tensor gbh, Tensor gbfc, Tensor stats, "
+        "Tensor? stamps=None) -> ()");
   m.def("im2col_u8(Tensor x, Tensor col, int kh, int kw, int s, float scale) -> ()");
   m.def("im2col_nhwc(Tensor x, Tensor col, int B, int H, int W, int C, int kh, int kw, int s) -> ()");
   m.def("col2im_nhwc(Tensor dcol, Tensor ymask, Tensor dx, Tensor? colsum, int B, int H, int W, int C, int kh, "

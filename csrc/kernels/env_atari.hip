@@ -200,13 +200,12 @@ constexpr int HEAD_HDIM = 512;                       // hidden width of the Natu
 
 // Rollout step of the native engine fused with the env: the policy/value head (z = h.Wh + bh, 512 -> A+1) of
 // env e, Gumbel-max sampling with the env-counter RNG key, logp / entropy / value, then the env step with the
-// sampled action -- one launch instead of head GEMM + sampling + env kernels. Critical path = the head only:
-// wave 0 computes the head and samples, meanwhile wave 1 (lanes 0..2) advances the physics for all three paddle
-// directions and waves 1..3 shift the frame stack; after one barrier the sampled direction's outcome is committed
-// and the newest frame rendered. The head width A1 = A + 1 is a template parameter: lane l owns hidden units
-// 8l..8l+7, whose Wh rows are A1 contiguous 16-byte chunks, so the whole GEMV is register-resident with every
-// load in flight at once and no data-dependent branch (a runtime A1 turned each column into a guarded block and
-// serialised the loads and reductions).
+// sampled action -- one launch instead of head GEMM + sampling + env kernels. The head uses the whole workgroup:
+// thread t owns hidden units 2t, 2t+1 (reduced from the fc GEMM's split-K partial planes, every plane's load in
+// flight at once), multiplies them into its two rows of Wh (register-resident, A1 = A + 1 a template parameter so
+// the GEMV has no data-dependent branch), and the A1 partial sums meet through wave shuffles + one LDS row per
+// wave (fixed order). Meanwhile threads 64..66 advance the physics for all three paddle directions. Wave 0 then
+// samples; after one barrier the sampled direction's outcome is committed and the newest frame rendered.
 struct FcParts {        // optional: h comes from the fc GEMM's split-K partial planes (cnn_head.h)
   const float* hpart;    // null: h is read as a finished bf16 row
   int S;
@@ -224,48 +223,47 @@ __global__ void __launch_bounds__(256) pong_policy_step_kernel(PongIO io, FcPart
                                                                uint32_t pseed, int pre_shifted,
                                                                uint64_t* __restrict__ stamps) {
   constexpr int A = A1 - 1;
-  const int e = blockIdx.x;
+  const int e = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   __shared__ int sh_act;
   __shared__ PongOut cand[3];
-  stamp_if(stamps, 0, threadIdx.x == 0);
-  if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
+  __shared__ float s_acc[4][A1];
+  stamp_if(stamps, 0, tid == 0);
+  // this thread's two Wh rows (2 * A1 bf16 = A1 32-bit words at byte offset 4 * A1 * tid)
+  uint32_t wv[A1];
+#pragma unroll
+  for (int u = 0; u < A1; ++u) wv[u] = reinterpret_cast<const uint32_t*>(Wh)[A1 * tid + u];
+  float hf[2];
+  if (fc.hpart) {
+    // h = relu(sum of the fc partial planes + bias), rounded to bf16 and stored for the learner
+    fc_h2_from_parts(fc.hpart, fc.S, fc.plane_stride, fc.bfc, e, tid, h, hf);
+  } else {
+    const uint32_t hw = reinterpret_cast<const uint32_t*>(h + (size_t)e * HEAD_HDIM)[tid];
+    hf[0] = __uint_as_float(hw << 16);
+    hf[1] = __uint_as_float(hw & 0xFFFF0000u);
+  }
+  if (tid >= 64 && tid < 67) cand[tid - 64] = pong_advance(io, e, (float)(tid - 65));
+  stamp_if(stamps, 8, tid == 0);
+  float acc[A1];
+#pragma unroll
+  for (int j = 0; j < A1; ++j) {
+    // Wh[2t][j] and Wh[2t+1][j] are elements j and A1 + j of the thread's 2 * A1 bf16
+    const uint32_t w0 = wv[j >> 1], w1 = wv[(A1 + j) >> 1];
+    const float a0 = __uint_as_float((j & 1) ? (w0 & 0xFFFF0000u) : (w0 << 16));
+    const float a1 = __uint_as_float(((A1 + j) & 1) ? (w1 & 0xFFFF0000u) : (w1 << 16));
+    acc[j] = wave_sum(hf[0] * a0 + hf[1] * a1);
+  }
+  if (lane == 0)
+#pragma unroll
+    for (int j = 0; j < A1; ++j) s_acc[wid][j] = acc[j];
+  __syncthreads();
+  stamp_if(stamps, 9, tid == 0);
+  if (wid == 0) {
     const int64_t key = io.tglob[e] * ((int64_t)1 << key_shift) + io.env_ids[e];  // pre-step counter
-    union { uint4 v[A1]; u16 x[8 * A1]; } w;
-#pragma unroll
-    for (int u = 0; u < A1; ++u) w.v[u] = reinterpret_cast<const uint4*>(Wh)[lane * A1 + u];
-    float hf[8];
-    if (fc.hpart) {
-      // h = relu(sum of the fc partial planes + bias), rounded to bf16 and stored for the learner
-      fc_h_from_parts(fc.hpart, fc.S, fc.plane_stride, fc.bfc, e, lane, h, hf);
-    } else {
-      union { uint4 v; u16 x[8]; } hv;
-      hv.v = reinterpret_cast<const uint4*>(h + (size_t)e * HEAD_HDIM)[lane];
-#pragma unroll
-      for (int r = 0; r < 8; ++r) hf[r] = bf2f(hv.x[r]);
-    }
-    stamp_if(stamps, 8, lane == 0);
-    float acc[A1];
-#pragma unroll
-    for (int j = 0; j < A1; ++j) acc[j] = 0.f;
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const float hr = hf[r];
-#pragma unroll
-      for (int j = 0; j < A1; ++j) acc[j] += hr * bf2f(w.x[r * A1 + j]);
-    }
-    stamp_if(stamps, 9, lane == 0);
-#pragma unroll
-    for (int j = 0; j < A1; ++j) acc[j] = wave_sum(acc[j]);
-    float zj = 0.f;
-#pragma unroll
-    for (int j = 0; j < A1; ++j) zj = (lane == j) ? acc[j] : zj;
-    if (lane < A1) {
-      zj += bh[lane];
-      z_out[(size_t)e * A1 + lane] = zj;
-    }
+    const int jj = lane < A1 ? lane : 0;
+    float zj = ((s_acc[0][jj] + s_acc[1][jj]) + (s_acc[2][jj] + s_acc[3][jj])) + bh[jj];
+    if (lane < A1) z_out[(size_t)e * A1 + lane] = zj;
+    const float value = __shfl(zj, A, 64);
     stamp_if(stamps, 10, lane == 0);
-    const float value = acc[A] + bh[A];
     // categorical head over lanes 0..A-1 (same maths as categorical_sample_kernel)
     const bool on = lane < A;
     const float z = on ? zj : -INFINITY;
@@ -293,21 +291,20 @@ __global__ void __launch_bounds__(256) pong_policy_step_kernel(PongIO io, FcPart
       sh_act = bi;
     }
     stamp_if(stamps, 1, lane == 0);
-  } else {
-    if (threadIdx.x < 64 + 3) cand[threadIdx.x - 64] = pong_advance(io, e, (float)((int)threadIdx.x - 65));
-    stamp_if(stamps, 2, threadIdx.x == 64);
-    if (!pre_shifted) pong_shift(io, e, 64, blockDim.x - 64);   // else the trunk kernel already shifted the stack
-    stamp_if(stamps, 3, threadIdx.x == 64);
+  } else if (!pre_shifted) {
+    pong_shift(io, e, 64, blockDim.x - 64);   // else the trunk kernel already shifted the stack
   }
+  stamp_if(stamps, 2, tid == 64);
+  stamp_if(stamps, 3, tid == 64);
   __syncthreads();
-  stamp_if(stamps, 4, threadIdx.x == 0);
+  stamp_if(stamps, 4, tid == 0);
   const PongOut& r = cand[pong_dir_index(sh_act)];
-  if (threadIdx.x == 0) pong_commit(io, e, r);
+  if (tid == 0) pong_commit(io, e, r);
   pong_render(io, e, r.s, r.done != 0);
   if (stamps) {
-    stamp_if(stamps, 5, threadIdx.x == 0);
+    stamp_if(stamps, 5, tid == 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    stamp_if(stamps, 6, threadIdx.x == 0);
+    stamp_if(stamps, 6, tid == 0);
   }
 }
 

@@ -322,7 +322,12 @@ struct HeadBwdArgs {
   float* gWh; float* gbh; float* gbfc;
   float* stats;
   int B;
+  uint64_t* stamps;          // optional [HB_WG, 16] s_memrealtime phase stamps (diagnostics; null in production)
 };
+
+__device__ __forceinline__ void hb_stamp(const HeadBwdArgs& a, int slot) {
+  if (a.stamps && threadIdx.x == 0) a.stamps[(size_t)blockIdx.x * 16 + slot] = __builtin_amdgcn_s_memrealtime();
+}
 
 template <int AC>
 __global__ void __launch_bounds__(HB_THREADS) head_bwd_kernel(HeadBwdArgs a) {
@@ -336,6 +341,7 @@ __global__ void __launch_bounds__(HB_THREADS) head_bwd_kernel(HeadBwdArgs a) {
   const int B = a.B;
   const bool lead = blockIdx.x == 0;
   const int col0 = blockIdx.x * 64;
+  hb_stamp(a, 0);
   // ---- every global operand in one round: rollout slabs into LDS, this thread's loss row and its head-phase
   // operands (h rows, Wh columns) in registers
   for (int i = tid; i < B; i += HB_THREADS) {
@@ -365,6 +371,7 @@ __global__ void __launch_bounds__(HB_THREADS) head_bwd_kernel(HeadBwdArgs a) {
   }
   const float c_ent = *a.ent_coef, beta = *a.kl_coef;
   __syncthreads();
+  hb_stamp(a, 1);
   // ---- returns, EV-before, advantage statistics (same maths as ac_loss_kernel phase 0)
   double s_r = 0, s_rr = 0, s_v = 0, s_vv = 0, s_rv = 0, s_a = 0, s_aa = 0;
   if (row) {
@@ -404,6 +411,7 @@ __global__ void __launch_bounds__(HB_THREADS) head_bwd_kernel(HeadBwdArgs a) {
   }
   double red[7] = {s_r, s_rr, s_v, s_vv, s_rv, s_a, s_aa};
   block_sum_multi<7>(red, sh);
+  hb_stamp(a, 2);
   const double nB = B;
   if (lead && tid == 0) {
     const double mr = red[0] / nB, mv = red[2] / nB;
@@ -454,6 +462,7 @@ __global__ void __launch_bounds__(HB_THREADS) head_bwd_kernel(HeadBwdArgs a) {
   {
     double r4[4] = {s_pg, s_kl, s_H, s_vl};
     block_sum_multi<4>(r4, sh);   // ends with a barrier: s_dz complete
+    hb_stamp(a, 3);
     if (lead && tid == 0) {
       const double inv = 1.0 / B;
       a.stats[0] = (float)(r4[0] * inv);
@@ -514,6 +523,7 @@ __global__ void __launch_bounds__(HB_THREADS) head_bwd_kernel(HeadBwdArgs a) {
       for (int q = 0; q < A1; ++q) dwp[c][q] += __shfl_xor(dwp[c][q], o, 64);
     }
   }
+  hb_stamp(a, 4);
   if (lane < 8) {
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
@@ -537,6 +547,11 @@ __global__ void __launch_bounds__(HB_THREADS) head_bwd_kernel(HeadBwdArgs a) {
     for (int bb = 0; bb < B; ++bb) sb += s_dz[bb * A1 + tid];
     a.gbh[tid] = sb;
   }
+  if (a.stamps) {
+    hb_stamp(a, 5);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    hb_stamp(a, 6);
+  }
 }
 
 }  // namespace aca
@@ -546,12 +561,12 @@ extern "C" hipError_t aca_head_bwd(const float* z, const int32_t* act, const flo
                                    const uint8_t* dn, int T, int N, int L, int returns_mode, int norm_adv, float gamma,
                                    float lam, float* ret_w, float* adv_w, const uint16_t* h, const uint16_t* Wh,
                                    uint16_t* dh, float* gWh, float* gbh, float* gbfc, float* stats, int A,
-                                   hipStream_t stream) {
+                                   uint64_t* stamps, hipStream_t stream) {
   const int B = T * N;
   if (B < 1 || B > aca::HB_MAXB || N > 256 || A < 2 || A > 7 || (returns_mode != 1 && returns_mode != 2))
     return hipErrorInvalidValue;
   aca::HeadBwdArgs a{z, act, logp_old, ent_coef, kl_coef, vf_coef, rew, val, dn, T, N, L, returns_mode, norm_adv,
-                     gamma, lam, ret_w, adv_w, h, Wh, dh, gWh, gbh, gbfc, stats, B};
+                     gamma, lam, ret_w, adv_w, h, Wh, dh, gWh, gbh, gbfc, stats, B, stamps};
   switch (A) {
 #define ACA_HB_CASE(n) \
   case n: aca::head_bwd_kernel<n><<<aca::HB_WG, aca::HB_THREADS, 0, stream>>>(a); break;

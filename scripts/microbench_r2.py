@@ -67,7 +67,7 @@ def main():
             None, m, None))
     hp = eng.hpart(N)
     cands["fc_parts"] = lambda: G.gemm(bt.y3, 3136, True, eng.sWfc, 512, False, hp, 512, 3, N, 512, 3136,
-                                       workspace=eng.ws)
+                                       workspace=eng.ws, max_planes=32)
     # learner data-gradient chain at the bench batch (B = T * N = 160): fused per-sample kernel vs the two GEMMs
     B = lb.B
     biasp = torch.zeros(B, 160, device="cuda:0")
@@ -91,6 +91,13 @@ def main():
     cands["finalize_bias_only"] = lambda: ops.grad_finalize(bias_w, eng.fin_parts)
     cands["finalize_readonly_only"] = lambda: ops.grad_finalize(ro_w, eng.fin_parts)
     cands["sumsq_slab"] = lambda: ops.sumsq(eng.flat.grad, eng.fin_parts)
+    # fused A2C head (loss + head backward) on the rollout's buffers
+    cfg_ = tr.cfg
+    rets = dict(mode=1, rew=st.rewards, val=st.values, dones=st.dones, L=st.T, gamma=cfg_.gamma, lam=cfg_.gae_lambda,
+                norm_adv=cfg_.norm_adv, ret_w=tr._ret_w, adv_w=tr._adv_w)
+    acts, lpo = st.flat("actions"), st.flat("logp")
+    sbuf = torch.zeros(16, device="cuda:0")
+    cands["head_bwd"] = lambda: eng.head_backward(lb, acts, lpo, tr.ent_coef, tr.kl_coef, cfg_.vf_coef, sbuf, rets)
     graphs = {k: make_graph(f, a.reps) for k, f in cands.items()}
     res = {k: [] for k in graphs}
     for _ in range(a.rounds):
@@ -122,6 +129,20 @@ def main():
         ph[names[i]] = float((s2[:, i] - s2[:, i - 1]).median())
     ph["end_from_first_start_us"] = float(s2[:, 6].max() - t0)
     out["trunk_bwd_phases"] = ph
+    st3 = torch.zeros(8, 16, dtype=torch.int64, device="cuda:0")
+    r = rets
+    ops.head_bwd(lb.z, acts, lpo, tr.ent_coef, tr.kl_coef, float(cfg_.vf_coef), r["rew"], r["val"], r["dones"],
+                 int(r["L"]), 1, bool(r["norm_adv"]), float(r["gamma"]), float(r["lam"]), r["ret_w"], r["adv_w"],
+                 lb.h, eng.sWh, lb.dh, eng.gWh, eng.gbh, eng.gbfc, sbuf, st3)
+    torch.cuda.synchronize()
+    s3 = st3.cpu().double() * 10e-3
+    t0 = s3[:, 0].min()
+    names = ["entry", "loads", "returns_reduce", "loss_reduce", "head_compute", "head_reduce_store", "drained"]
+    ph = {"start_spread_us": float(s3[:, 0].max() - t0)}
+    for i in range(1, 7):
+        ph[names[i]] = float((s3[:, i] - s3[:, i - 1]).median())
+    ph["end_from_first_start_us"] = float(s3[:, 6].max() - t0)
+    out["head_bwd_phases"] = ph
     print(json.dumps(out, indent=1))
     if a.out:
         with open(a.out, "w") as f:

@@ -477,11 +477,12 @@ def test_fc_partial_planes_and_consumers(cuda):
     Wh = (torch.randn(512 * (A + 1), generator=g) * 0.05).to(torch.bfloat16).to(cuda)
     bh = torch.randn(A + 1, generator=g).to(cuda)
     ref = torch.relu(y3.float() @ Wfc.float() + bfc)
-    for tile, bk, splits in ((1, 64, 4), (4, 256, 8), (0, 128, 1)):
-        hp = torch.full((8 * N * 512,), float("nan"), device=cuda)   # unused planes must never be read as data
-        S = G.gemm(y3, 3136, True, Wfc, 512, False, hp, 512, 3, N, 512, 3136, tile=tile, bk=bk, splits=splits)
+    for tile, bk, splits in ((1, 64, 4), (4, 256, 8), (0, 128, 1), (4, 64, 32), (1, 64, 16)):
+        hp = torch.full((32 * N * 512,), float("nan"), device=cuda)   # unused planes must never be read as data
+        S = G.gemm(y3, 3136, True, Wfc, 512, False, hp, 512, 3, N, 512, 3136, tile=tile, bk=bk, splits=splits,
+                   max_planes=32)
         assert S == G.effective_splits(3136, bk, splits)
-        h_sum = torch.relu(hp.view(8, N, 512)[:S].sum(0) + bfc)
+        h_sum = torch.relu(hp.view(32, N, 512)[:S].sum(0) + bfc)
         assert torch.allclose(h_sum, ref, rtol=1e-3, atol=1e-3)
         val = torch.empty(N, device=cuda)
         hout = torch.empty(N, 512, dtype=torch.bfloat16, device=cuda)

@@ -109,6 +109,7 @@ class CNNEngine:
         self.wgrad_planes = int(os.environ.get("ACA_WGRAD_PLANES", "32"))
         self._planes = {}
         self._wsplits = {}
+        self._cur_planes = {}
         self._fin_words = {}
         # rollout fc product left as split-K partial planes, reduced by its consumer kernel (no in-launch fence)
         self.fc_parts = os.environ.get("ACA_FC_PARTS", "1") != "0"
@@ -246,6 +247,7 @@ class CNNEngine:
         S = G.gemm(A, lda, False, B_, ldb, False, buf, N, 3, M, N, K, workspace=ws, gb=gb, gb_scale=gb_scale,
                    max_planes=self.wgrad_planes)
         self._wsplits[name] = S
+        self._cur_planes[name] = S
 
     def head_ok(self, B):
         return self.fused_head and 2 <= self.A <= 7 and B <= 512
@@ -279,11 +281,16 @@ class CNNEngine:
         ws2 = self._side_ws()
         if stage == "trunk":
             return self._backward_trunk(b, main, side, ev, ws, ws2)
+        self._cur_planes = {}   # weight-gradient plane sets written by THIS backward (reduced by its finaliser)
+        head_bias_done = head_bias_done or getattr(b, "bias_done", False)
         if not head_done:
             ev[0].record(main)
             side.wait_event(ev[0])
             with torch.cuda.stream(side):   # heads: dWh = h^T dz, dbh = colsum(dz)
-                G.gemm(b.h, 512, False, b.dz, A1, False, self.gWh, A1, 2, 512, A1, B, workspace=ws2)
+                if self.det_wgrad and stage == "all":   # split-K planes, reduced in order by the finaliser
+                    self._wgrad("Wh", self.gWh, b.h, 512, b.dz, A1, 512, A1, B, ws2, None)
+                else:
+                    G.gemm(b.h, 512, False, b.dz, A1, False, self.gWh, A1, 2, 512, A1, B, workspace=ws2)
                 if not head_bias_done:
                     ops.colsum_bf16(b.dz, B, A1, A1, self.gbh)
             G.gemm(b.dz, A1, True, self.sWh, A1, True, b.dh, 512, 1, B, 512, A1, mask=b.h, ldm=512,
@@ -355,7 +362,7 @@ class CNNEngine:
         """One launch after the backward (``grad_finalize``): reduces the per-sample conv bias-gradient rows
         (fused backward) into the slab and, with ``want_parts``, writes the global-norm partials of the whole
         gradient (``fin_parts``) so the optimiser needs no sum-of-squares pass."""
-        planes = tuple(sorted(self._wsplits.items())) if self.det_wgrad else ()
+        planes = tuple(sorted(self._cur_planes.items())) if self.det_wgrad else ()
         key = (b.B, self.want_parts, self.fused_bwd, planes)
         words = self._fin_words.get(key)
         if words is None:
@@ -367,7 +374,7 @@ class CNNEngine:
                 src_of = {self.gb3.data_ptr(): (bp, 160, b.B), self.gb2.data_ptr(): (bp + 64 * 4, 160, b.B),
                           self.gb1.data_ptr(): (bp + 128 * 4, 160, b.B)}
             for name, S in planes:
-                g = {"W1": self.gW1, "W2": self.gW2, "W3": self.gW3}[name]
+                g = {"W1": self.gW1, "W2": self.gW2, "W3": self.gW3, "Wh": self.gWh}[name]
                 src_of[g.data_ptr()] = (self._planes[name].data_ptr(), g.numel(), S)
             for p, off in zip(flat.params, flat.offsets):
                 g = flat.grad[off:off + p.numel()]
@@ -411,9 +418,12 @@ class CNNEngine:
         out = b.stats if stats is None else stats
         ops = _native.require()
         if returns is None:
+            # det_wgrad: the loss kernel also writes the head-bias gradient (fixed-order sums), so the backward needs
+            # no atomic column sum
             ops.ac_loss(zl, A1, zl[:, A:], A1, actions, None, None, logp_old, adv, ret, v_old, ent_coef, kl_coef,
                         float(vf_coef), float(ppo_clip or 0.0), float(v_clip or 0.0), b.dz, A1, b.dz[:, A:], A1,
-                        None, out, B, A, False)
+                        None, out, B, A, False, dbias=self.gbh if self.det_wgrad else None)
+            b.bias_done = self.det_wgrad
         else:
             r = returns
             ops.ac_loss(zl, A1, zl[:, A:], A1, actions, None, None, logp_old, None, None, None, ent_coef, kl_coef,

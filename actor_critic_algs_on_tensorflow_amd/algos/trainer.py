@@ -58,6 +58,57 @@ STAT_KEYS = ("pg", "kl", "entropy", "crit_loss", "clipfrac", "act_loss", "ratio"
 LOG_KEYS = ("act_loss", "crit_loss", "kl", "entropy", "ev_before", "ev_after", "clipfrac")
 
 
+class SegmentRecorder:
+    """Captures one update as a chain of hipGraphs cut at the host-issued collectives.
+
+    Trainer code routes every collective through :meth:`ActorCriticTrainer._comm`; while recording, that ends the
+    current graph, stores the collective (a closure over persistent buffers, written in place) and opens the next
+    graph, so ``replay`` = graph 0, collective 0, graph 1, ... All graphs share one memory pool and always replay in
+    capture order (the condition under which pool sharing is safe). Collectives are stream-ordered, not host-
+    blocking: the host only walks the list."""
+
+    def __init__(self):
+        self.items = []
+        self.pool = torch.cuda.graph_pool_handle()
+        self._g = None
+        self._ctx = None
+
+    def start(self):
+        self._g = torch.cuda.CUDAGraph()
+        self._ctx = torch.cuda.graph(self._g, pool=self.pool)
+        self._ctx.__enter__()
+
+    def cut(self, fn):
+        self._ctx.__exit__(None, None, None)
+        self.items.append(("graph", self._g))
+        self.items.append(("host", fn))
+        self.start()
+
+    def finish(self):
+        self._ctx.__exit__(None, None, None)
+        self.items.append(("graph", self._g))
+        self._g = self._ctx = None
+
+    def abort(self):
+        if self._ctx is not None:
+            try:
+                self._ctx.__exit__(None, None, None)
+            except Exception:   # pragma: no cover - capture already invalid
+                pass
+            self._g = self._ctx = None
+
+    @property
+    def n_graphs(self):
+        return sum(1 for k, _ in self.items if k == "graph")
+
+    def replay(self):
+        for kind, obj in self.items:
+            if kind == "graph":
+                obj.replay()
+            else:
+                obj()
+
+
 class ActorCriticTrainer:
     def __init__(self, cfg: TrainConfig, env=None, model=None, dp=None):
         self.cfg = cfg
@@ -74,6 +125,9 @@ class ActorCriticTrainer:
         self.flat = FlatParams(self.model.param_groups(), self.device)
         if dp is not None:
             dp.broadcast_params(self.flat)
+            if cfg.grad_bucket_dtype == "bf16" and dp.compress is None:
+                dp.compress = "bf16"
+            dp.prepare(self.flat.grad)
         self.engine = None
         self.mlp = None
         self.shadow = None
@@ -132,6 +186,8 @@ class ActorCriticTrainer:
         self._bw_pending = None
         self._comm_grad = None      # lag-1 DP: the all-reduced copy of the previous update's gradient
         self._comm_work = None
+        self._rec = None            # SegmentRecorder while capturing a segmented (DP) update
+        self._kl_buf = torch.zeros(1, dtype=torch.float32, device=self.device) if dp is not None else None
         self.logger = None
         if self.rank == 0 and cfg.outdir:
             self.logger = Logger(cfg.outdir, legacy_step_index=cfg.legacy_step_index, metrics_path=cfg.metrics_path,
@@ -266,6 +322,26 @@ class ActorCriticTrainer:
             return None, None
         cfg, st = self.cfg, self.storage
         dones = st.dones   # bootstrap_on_timeout: the bootstrap is already in the truncated step's reward (collect)
+        self._scanned = False
+        if _native.use_native(st.rewards) and cfg.returns in ("gae", "nstep"):
+            # ONE launch: chunked scan returns + EV-before + moments (+ in-place adv normalisation on one rank; under
+            # DP the fp64 moments are all-reduced on the device and an elementwise kernel normalises)
+            T, N = st.T, st.N
+            if getattr(self, "_scan_ws", None) is None:
+                self._scan_ws = R.ScanWorkspace(self.device, T, N)
+                self._scan_ret = torch.empty(T * N, device=self.device)
+                self._scan_adv = torch.empty(T * N, device=self.device)
+            local_norm = cfg.norm_adv and self.dp is None
+            ret, adv, mom = R.returns_scan(st.rewards, st.values, dones, cfg.returns, cfg.gamma, cfg.gae_lambda,
+                                           cfg.look_ahead, norm=local_norm, ws=self._scan_ws,
+                                           ev_out=self.stats["ev_before"].view(1), ret_out=self._scan_ret,
+                                           adv_out=self._scan_adv)
+            if cfg.norm_adv and self.dp is not None:
+                dp = self.dp
+                self._comm(lambda: dp.allreduce_sum_(mom))
+                _native.require().normalize_mom(self._scan_adv, self._scan_adv, mom, 1e-8)
+            self._scanned = True
+            return self._scan_ret, self._scan_adv
         if cfg.returns == "gae":
             ret, adv = R.gae(st.rewards, st.values, dones, cfg.gamma, cfg.gae_lambda)
         else:
@@ -280,9 +356,18 @@ class ActorCriticTrainer:
             return self.adv_buf
         return R.normalize_advantages(adv)
 
+    def _pre_learn_stats(self, ret, adv, v_old):
+        """EV-before and advantage normalisation, unless the fused returns scan already produced both."""
+        if getattr(self, "_scanned", False):
+            return adv
+        self._ev(ret, v_old, "ev_before")
+        return self._normalize(adv) if self.cfg.norm_adv else adv
+
     def _ev(self, target, pred, slot):
         if _native.use_native(target):
-            _native.require().ev(target.contiguous(), pred.contiguous(), self.stats[slot].view(1))
+            ws = getattr(self, "_scan_ws", None)   # many-workgroup form when the scan workspace exists
+            _native.require().ev(target.contiguous(), pred.contiguous(), self.stats[slot].view(1),
+                                 ws.ev_part if ws is not None else None, ws.ev_ticket if ws is not None else None)
         else:
             self.stats[slot].copy_(var_accounted_for_tensor(target, pred))
 
@@ -301,12 +386,23 @@ class ActorCriticTrainer:
         total = a_loss + (cfg.vf_coef * c_loss if shared else c_loss)
         return total, a_loss, c_loss, kl, entm, clipfrac
 
+    def _comm(self, fn):
+        """Runs a collective now (eager) or, while a :class:`SegmentRecorder` is capturing, records it as a cut
+        between two graphs. ``fn`` must work in place on buffers that outlive the capture."""
+        if self._rec is None:
+            fn()
+        else:
+            self._rec.cut(fn)
+
     def _apply_grads(self):
         """All-reduce (DP) + optimiser step; inside a segmented capture the pre-graph stops before both."""
         if self._defer_allreduce:
             return
         if self.dp is not None:
-            self.dp.allreduce_grads(self.flat, scale=False)
+            dp, g = self.dp, self.flat.grad
+            dp.pack(g)                                   # bf16 buckets: captured cast into the comm buffer
+            self._comm(lambda: dp.allreduce_packed(g))
+            dp.unpack(g)
         self._run_optimizers()
 
     def _run_optimizers(self):
@@ -361,9 +457,7 @@ class ActorCriticTrainer:
         cfg, st = self.cfg, self.storage
         obs, actions, logp_old = st.flat("obs"), st.flat("actions"), st.flat("logp")
         v_old = st.flat("values")
-        self._ev(ret, v_old, "ev_before")
-        if cfg.norm_adv:
-            adv = self._normalize(adv)
+        adv = self._pre_learn_stats(ret, adv, v_old)
         if cfg.algo == "ppo":
             for sel in self._minibatches(obs.shape[0]):
                 self.flat.zero_grad()
@@ -393,8 +487,11 @@ class ActorCriticTrainer:
 
     def _kl_and_lr(self, logp_old, logp, ret, v):
         kl = ((logp_old - logp) ** 2).mean()
-        if self.dp is not None:
-            kl = self.dp.mean_scalar(kl)
+        if self.dp is not None:   # in-place device all-reduce: capturable as a segment cut
+            dp, buf = self.dp, self._kl_buf
+            buf.copy_(kl.reshape(1))
+            self._comm(lambda: dp.allreduce_sum_(buf))
+            kl = (buf / self.world).reshape(())
         self.stats["kl"].copy_(kl)
         self._ev(ret, v, "ev_after")
         if self.lr_ctrl is not None:
@@ -417,9 +514,7 @@ class ActorCriticTrainer:
         cfg, st, eng = self.cfg, self.storage, self.mlp
         obs, actions, logp_old = st.flat("obs"), st.flat("actions"), st.flat("logp")
         v_old = st.flat("values")
-        self._ev(ret, v_old, "ev_before")
-        if cfg.norm_adv:
-            adv = self._normalize(adv)
+        adv = self._pre_learn_stats(ret, adv, v_old)
         adv, ret = adv.contiguous(), ret.contiguous()
         B = obs.shape[0]
         if cfg.algo == "ppo":
@@ -494,9 +589,7 @@ class ActorCriticTrainer:
         cfg, st = self.cfg, self.storage
         obs, actions, logp_old = st.flat("obs"), st.flat("actions"), st.flat("logp")
         v_old = st.flat("values")
-        self._ev(ret, v_old, "ev_before")
-        if cfg.norm_adv:
-            adv = self._normalize(adv)
+        adv = self._pre_learn_stats(ret, adv, v_old)
         if cfg.algo == "ppo":
             B = obs.shape[0]
             mb = B // cfg.ppo_minibatches
@@ -507,14 +600,22 @@ class ActorCriticTrainer:
                                 logp=torch.empty(mb, device=dev), adv=torch.empty(mb, device=dev),
                                 ret=torch.empty(mb, device=dev), v=torch.empty(mb, device=dev))
             m = self._mb
-            for sel in self._minibatches(B):
-                torch.index_select(obs, 0, sel, out=m["obs"])
-                torch.index_select(actions, 0, sel, out=m["act"])
-                torch.index_select(logp_old, 0, sel, out=m["logp"])
-                torch.index_select(adv, 0, sel, out=m["adv"])
-                torch.index_select(ret, 0, sel, out=m["ret"])
-                torch.index_select(v_old, 0, sel, out=m["v"])
-                self._learn_native(m["obs"], m["act"], m["logp"], m["adv"], m["ret"], m["v"])
+            if actions.dtype == torch.int32:
+                # one launch per minibatch: the keyed epoch permutation evaluated in place + every row gathered
+                ops = _native.require()
+                uc = self.update_counter.view(1)
+                args = [t.contiguous() for t in (obs, actions, logp_old, adv, ret, v_old)]
+                for ep in range(cfg.ppo_epochs):
+                    for k in range(cfg.ppo_minibatches):
+                        ops.mb_gather(*args, m["obs"], m["act"], m["logp"], m["adv"], m["ret"], m["v"],
+                                      self.policy_seed, uc, ep, k * mb)
+                        self._learn_native(m["obs"], m["act"], m["logp"], m["adv"], m["ret"], m["v"])
+            else:
+                for sel in self._minibatches(B):
+                    for key, src in (("obs", obs), ("act", actions), ("logp", logp_old), ("adv", adv), ("ret", ret),
+                                     ("v", v_old)):
+                        torch.index_select(src, 0, sel, out=m[key])
+                    self._learn_native(m["obs"], m["act"], m["logp"], m["adv"], m["ret"], m["v"])
         else:
             self._learn_native(obs, actions, logp_old, adv.contiguous(), ret.contiguous(), v_old,
                                forward=not self._reuse_acts())
@@ -551,8 +652,10 @@ class ActorCriticTrainer:
     #       AR(C) issued, overlapping the next update's rollout.
     #     Every gradient is on-policy for its batch (computed at the parameters that acted) and applied one update
     #     late (delayed-gradient SGD with staleness 1).
-    # PPO with DP, and configurations that need collectives inside the update (global advantage normalisation,
-    # the KL-adaptive lr), run eagerly with synchronous collectives.
+    # Every other DP configuration (PPO minibatch steps, global advantage normalisation, the KL-adaptive lr / KL
+    # proxy, the MLP engine) is captured by a SegmentRecorder: one graph chain per update, cut at each collective
+    # (gradient all-reduce per optimiser step, the packed fp64 advantage moments, the KL scalar), every collective
+    # an in-place stream-ordered RCCL call on a persistent buffer. No DP configuration runs eagerly.
 
     def _can_capture(self):
         return self.cfg.cuda_graph and self.device.type == "cuda"
@@ -589,7 +692,7 @@ class ActorCriticTrainer:
 
     def capture(self, warmup=2):
         """Capture the update as hipGraph(s) (see above). Warm-up updates run first (GEMM autotuning, allocator)."""
-        if not self._can_capture() or (self.dp is not None and not self._segmented()):
+        if not self._can_capture():
             return None
         self.timer.suspended = True
         try:
@@ -633,8 +736,10 @@ class ActorCriticTrainer:
                         self.update_body()
                     g2 = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g2):
+                        self.dp.unpack(self._comm_grad)     # bf16 buckets: the all-reduced sum back into C
                         self._post_body()
                         self._grad_move()
+                        self.dp.pack(self._comm_grad)
                     graph = ("lag1", g1, g2)
                 else:
                     self._bw_stage = "tail"
@@ -643,19 +748,35 @@ class ActorCriticTrainer:
                         self.collect()
                         ret, adv = self.compute_returns()
                         self.learn(ret, adv)
+                        self.dp.pack(self.flat.grad, *self.engine.tail_bucket())
                     self._bw_stage = "all"
                     b, hb = self._bw_pending
                     g2 = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g2):
                         self.engine.backward(b, head_bias_done=hb, stage="trunk")
+                        self.dp.pack(self.flat.grad, 0, self.engine.tail_bucket()[0])
                     g3 = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g3):
+                        self.dp.unpack(self.flat.grad)
                         self._post_body()
                         self.storage.roll_over()
                     graph = ("strict", g1, g2, g3)
             finally:
                 self._defer_allreduce = False
                 self._bw_stage = "all"
+        elif self.dp is not None:
+            rec = SegmentRecorder()
+            self._rec = rec
+            try:
+                rec.start()
+                self.update_body()
+                rec.finish()
+            except BaseException:
+                rec.abort()
+                raise
+            finally:
+                self._rec = None
+            graph = ("segments", rec)
         else:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
@@ -674,13 +795,15 @@ class ActorCriticTrainer:
         kind = graph[0]
         if kind == "single":
             graph[1].replay()
+        elif kind == "segments":
+            graph[1].replay()
         elif kind == "strict":
             _, g1, g2, g3 = graph
             s, e = self.engine.tail_bucket()
             g1.replay()
-            w_tail = self.dp.allreduce_async(self.flat.grad[s:e])   # overlaps the conv backward
+            w_tail = self.dp.allreduce_async(self.dp.comm_view(self.flat.grad, s, e))   # overlaps the conv backward
             g2.replay()
-            w_trunk = self.dp.allreduce_async(self.flat.grad[:s])
+            w_trunk = self.dp.allreduce_async(self.dp.comm_view(self.flat.grad, 0, s))
             w_tail.wait()
             w_trunk.wait()
             g3.replay()
@@ -689,10 +812,11 @@ class ActorCriticTrainer:
             g1.replay()                       # overlaps the all-reduce of the previous gradient
             if self._comm_work is None:       # first update: nothing to apply yet
                 self._grad_move()
+                self.dp.pack(self._comm_grad)
             else:
                 self._comm_work.wait()
                 g2.replay()
-            self._comm_work = self.dp.allreduce_async(self._comm_grad)
+            self._comm_work = self.dp.allreduce_async(self.dp.comm_view(self._comm_grad))
 
     def step(self):
         """One update (graph replay when captured)."""
@@ -715,6 +839,7 @@ class ActorCriticTrainer:
         """lag-1 DP: apply the last all-reduced gradient (end of training / before a checkpoint)."""
         if self.graph is not None and self.graph[0] == "lag1" and self._comm_work is not None:
             self._comm_work.wait()
+            self.dp.unpack(self._comm_grad)
             self._post_body()
             self._comm_grad.zero_()
             self._comm_work = None

@@ -92,7 +92,9 @@ class GemmWorkspace:
 # against scratch outputs and the winner is cached for the process. ACAMD_GEMM_TUNE=0 uses :func:`plan`.
 _TUNED: dict = {}
 PARTIAL_MAX_SPLITS = 8   # out_mode 3: the consumer kernels reduce at most this many partial planes
-COLSUM_PART_MIN_TILES = int(os.environ.get("ACAMD_COLSUM_PART_MIN_TILES", "48"))
+# with >= 2 row tiles the bias column sums go through per-tile partials + one ordered reduce (deterministic; one
+# tile row adds each column once, also deterministic)
+COLSUM_PART_MIN_TILES = int(os.environ.get("ACAMD_COLSUM_PART_MIN_TILES", "2"))
 TUNE = os.environ.get("ACAMD_GEMM_TUNE", "1") == "1"
 
 
@@ -102,8 +104,10 @@ def tuned_plans():
 
 # Tuned plans measured on an MI355X for the engine's shapes (scripts/dump_gemm_plans.py): loaded at import so runs
 # start with the measured winners (no tuning pass, and no run-to-run plan noise); shapes not in the file are still
-# tuned on first use. ACAMD_GEMM_PLANS=0 ignores the file.
+# tuned on first use. ACAMD_GEMM_PLANS=0 ignores the file; ACAMD_GEMM_PLANS=<path> loads another plans file.
 PLANS_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_plans.json")
+if os.environ.get("ACAMD_GEMM_PLANS", "1") not in ("0", "1", ""):
+    PLANS_FILE = os.environ["ACAMD_GEMM_PLANS"]
 
 
 def _key_from_json(k):

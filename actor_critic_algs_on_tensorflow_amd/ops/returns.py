@@ -10,9 +10,13 @@
 * :func:`normalize_advantages` -- ``(A - mean) / (1e-8 + std)`` with the population std
   (``Basic_AC/run_AC.py:241``).
 
-On GPU each function is one HIP launch (``csrc/kernels/returns.hip``): one thread per env column runs the
-reverse scan for GAE; n-step runs one thread per (t, n) with an O(L) window. The PyTorch code below is the
-oracle those kernels are tested against.
+On GPU the trainers use :func:`returns_scan`: ONE HIP launch (``returns_scan_kernel`` in
+``csrc/kernels/returns.hip``) computes either estimator as a chunked associative reverse scan over (time chunk x
+env) -- both are affine recurrences ``x_t = a_t + c_t x_{t+1}`` -- together with the EV-before correlation, the
+moments a data-parallel run all-reduces, and (optionally) the in-place advantage normalisation. The truncated
+n-step window (``L < T``) uses its prefix-sum form (scan of the un-bootstrapped return + next-terminal index). The
+simple per-column kernels (:func:`gae`, :func:`nstep_returns`) stay as the small-T building blocks. The PyTorch
+code below is the oracle all of them are tested against.
 """
 from __future__ import annotations
 
@@ -127,3 +131,64 @@ def normalize_advantages(adv, eps=1e-8):
     """Population-std normalisation (numpy ddof=0), as ``Basic_AC/run_AC.py:241``."""
     a = adv.float()
     return (a - a.mean()) / (eps + a.std(unbiased=False))
+
+
+class ScanWorkspace:
+    """Device workspace of :func:`returns_scan` / the many-workgroup EV: per-workgroup fp64 partial moments, the
+    self-cleaning last-arriver ticket, the fp64 totals ``mom`` (``[count, sum adv, sum adv^2, sum ret, sum ret^2,
+    sum V, sum V^2, sum ret*V]``) and the truncated-window scratch. Create once, outside any graph capture."""
+
+    def __init__(self, device, T=0, N=0):
+        self.device = torch.device(device)
+        self.part = torch.zeros(256 * 8, dtype=torch.float64, device=self.device)
+        self.ticket = torch.zeros(4, dtype=torch.int32, device=self.device)
+        self.ev_ticket = torch.zeros(4, dtype=torch.int32, device=self.device)
+        self.ev_part = torch.zeros(64 * 8, dtype=torch.float64, device=self.device)
+        self.mom = torch.zeros(8, dtype=torch.float64, device=self.device)
+        self.gz = torch.zeros(max(T * N, 1), dtype=torch.float64, device=self.device)
+
+    def fit(self, T, N):
+        blocks = _native.require().returns_scan_geometry(T, N)[3]
+        if self.part.numel() < blocks * 8:
+            self.part = torch.zeros(blocks * 8, dtype=torch.float64, device=self.device)
+        if self.gz.numel() < T * N:
+            self.gz = torch.zeros(T * N, dtype=torch.float64, device=self.device)
+        return self
+
+
+def returns_scan(rews, vals, dones, mode="gae", gamma=0.99, lam=0.95, look_ahead=None, norm=False, eps=1e-8,
+                 ws: ScanWorkspace | None = None, ev_out=None, ret_out=None, adv_out=None):
+    """Fused returns + statistics. ``mode`` "gae" or "nstep" (``look_ahead`` None -> whole rollout).
+
+    Returns ``(ret, adv, mom)``: ``adv`` normalised (population std) when ``norm``; ``mom`` the fp64 totals
+    (``[count, sum adv, sum adv^2, sum ret, sum ret^2, sum V, sum V^2, sum ret*V]``, pre-normalisation) and, if
+    ``ev_out`` is given, ``ev_out[0]`` = EV correlation of (ret, V[:T]) (``Basic_AC/util.py:4-12``)."""
+    T, N = rews.shape
+    L = T if look_ahead is None else int(look_ahead)
+    if not _native.use_native(rews):
+        ret, adv = gae_ref(rews, vals, dones, gamma, lam) if mode == "gae" else \
+            nstep_returns_ref(rews, vals, dones, gamma, L)
+        v = vals[:T].double()
+        a, r = adv.double(), ret.double()
+        mom = torch.stack([torch.tensor(float(T * N), dtype=torch.float64, device=rews.device), a.sum(),
+                           (a * a).sum(), r.sum(), (r * r).sum(), v.sum(), (v * v).sum(), (r * v).sum()])
+        if ev_out is not None:
+            from ..utils.stats import var_accounted_for_tensor
+            ev_out.view(-1)[0] = var_accounted_for_tensor(ret.reshape(-1), vals[:T].reshape(-1))
+        if norm:
+            adv = normalize_advantages(adv, eps)
+        if ret_out is not None:
+            ret_out.view(T, N).copy_(ret)
+            ret = ret_out.view(T, N)
+        if adv_out is not None:
+            adv_out.view(T, N).copy_(adv)
+            adv = adv_out.view(T, N)
+        return ret, adv, mom
+    ws = (ws or ScanWorkspace(rews.device)).fit(T, N)
+    ret = ret_out.view(T, N) if ret_out is not None else torch.empty(T, N, device=rews.device)
+    adv = adv_out.view(T, N) if adv_out is not None else torch.empty(T, N, device=rews.device)
+    _native.require().returns_scan(rews.float().contiguous(), vals.float().contiguous(),
+                                   dones.to(torch.uint8).contiguous(), ret, adv, 2 if mode == "gae" else 1,
+                                   float(gamma), float(lam), L, bool(norm), float(eps), ws.part, ws.ticket, ws.mom,
+                                   ev_out, ws.gz)
+    return ret, adv, ws.mom

@@ -44,11 +44,50 @@ def init_from_env(backend="auto", timeout_s=300):
 
 
 class DataParallel:
-    def __init__(self, group=None, average=True):
+    """``compress="bf16"`` all-reduces the gradient slab as bf16 (half the xGMI bytes: 3.4 MB instead of 6.75 MB
+    for the Atari CNN): a captured cast packs the fp32 slab (or a bucket range of it) into a persistent bf16 comm
+    buffer, RCCL sums that, a captured cast unpacks it. Summation then happens in bf16 (rounding error grows with
+    the world size); the default keeps fp32 buckets."""
+
+    def __init__(self, group=None, average=True, compress=None):
         self.group = group
         self.rank = dist.get_rank(group)
         self.world_size = dist.get_world_size(group)
         self.average = average
+        if compress in ("none", "fp32"):
+            compress = None
+        if compress not in (None, "bf16"):
+            raise ValueError(f"compress must be None/'none'/'bf16', got {compress!r}")
+        self.compress = compress
+        self._cbuf = None
+
+    # -- gradient buckets (optionally bf16) ----------------------------------------------------------------------
+    def prepare(self, grad):
+        """Allocates the persistent comm buffer (call outside any graph capture)."""
+        if self.compress and (self._cbuf is None or self._cbuf.numel() != grad.numel()):
+            self._cbuf = torch.zeros(grad.numel(), dtype=torch.bfloat16, device=grad.device)
+
+    def comm_view(self, grad, s=0, e=None):
+        """The tensor the collective runs on for slab range [s, e)."""
+        if self.compress:
+            self.prepare(grad)
+            return self._cbuf[s:e]
+        return grad[s:e]
+
+    @torch.no_grad()
+    def pack(self, grad, s=0, e=None):
+        if self.compress:
+            self.comm_view(grad, s, e).copy_(grad[s:e])
+
+    @torch.no_grad()
+    def unpack(self, grad, s=0, e=None):
+        if self.compress:
+            grad[s:e].copy_(self._cbuf[s:e])
+
+    @torch.no_grad()
+    def allreduce_packed(self, grad, s=0, e=None):
+        """Synchronous (stream-ordered) SUM all-reduce of the packed range."""
+        dist.all_reduce(self.comm_view(grad, s, e), op=dist.ReduceOp.SUM, group=self.group)
 
     # -- parameters ---------------------------------------------------------------------------------------------
     @torch.no_grad()
@@ -87,6 +126,13 @@ class DataParallel:
         mean = s[0] / s[2]
         var = torch.clamp(s[1] / s[2] - mean * mean, min=0.0)
         return ((a - mean.float()) / (eps + var.sqrt().float()))
+
+    @torch.no_grad()
+    def allreduce_sum_(self, t):
+        """In-place SUM all-reduce of a small device tensor (e.g. the packed fp64 return-scan moments): no host
+        round trip, capturable."""
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        return t
 
     @torch.no_grad()
     def mean_scalar(self, x):

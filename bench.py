@@ -37,6 +37,8 @@ def main():
                     help="DP schedule: strict = exact sync A2C, fc/head gradient bucket all-reduced under the conv "
                          "backward; lag1 = all-reduce overlapped with the next rollout, gradient applied one update "
                          "late")
+    ap.add_argument("--bucket-dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="dtype of the all-reduced gradient buckets (bf16 halves the xGMI bytes)")
     args = ap.parse_args()
 
     from actor_critic_algs_on_tensorflow_amd import preset
@@ -50,7 +52,7 @@ def main():
     dp = DP.DataParallel() if world > 1 else None
     cfg = preset("pong_a2c", num_envs=args.envs, device=f"cuda:{local}", outdir=None, quiet=True,
                  stdout_freq=0, save_every=0, engine=args.engine, cuda_graph=not args.no_graph,
-                 overlap=args.overlap)
+                 overlap=args.overlap, grad_bucket_dtype=args.bucket_dtype)
     tr = ActorCriticTrainer(cfg, dp=dp)
     if cfg.cuda_graph:
         tr.capture(warmup=2)
@@ -92,9 +94,13 @@ def main():
                        "global_batch": steps_per_update, "seq_len": cfg.n_steps, "envs_per_gpu": args.envs,
                        "algo": "A2C (RMSprop 7e-4, n-step returns, grad-norm 0.5)",
                        "parallelism": f"dp{world}", "engine": "native" if tr.engine is not None else "torch",
-                       "hipgraph": bool(tr.graph), "dp_schedule": tr.graph[0] if tr.graph else "eager"},
+                       "hipgraph": bool(tr.graph), "dp_schedule": tr.graph[0] if tr.graph else "eager",
+                       "grad_bucket_dtype": args.bucket_dtype},
         }
         print(json.dumps(out), flush=True)
+        if os.environ.get("ACA_BENCH_SAVE_PLANS"):   # record the GEMM plans this run tuned (scripts/plan_search.sh)
+            from actor_critic_algs_on_tensorflow_amd.ops import gemm as G
+            G.save_plans(os.environ["ACA_BENCH_SAVE_PLANS"])
     if dp is not None:
         torch.distributed.destroy_process_group()
 

@@ -54,6 +54,15 @@ hipError_t aca_gae(const float*, const float*, const uint8_t*, float*, float*, i
 hipError_t aca_nstep(const float*, const float*, const uint8_t*, float*, float*, int, int, float, int, hipStream_t);
 hipError_t aca_normalize(const float*, float*, int, float, hipStream_t);
 hipError_t aca_moments(const float*, const float*, float*, int, hipStream_t);
+void aca_returns_scan_geometry(int, int, int*, int*, int*, int*);
+hipError_t aca_returns_scan(const float*, const float*, const uint8_t*, float*, float*, double*, double*, unsigned int*,
+                            double*, float*, int, int, int, int, int, float, float, float, hipStream_t);
+hipError_t aca_normalize_mom(const float*, float*, const double*, int, float, hipStream_t);
+int aca_ev_multi_blocks(int);
+hipError_t aca_mb_gather(const uint8_t*, int64_t, const int*, const float*, const float*, const float*, const float*,
+                         uint8_t*, int*, float*, float*, float*, float*, int, int, uint32_t, const int64_t*, int, int,
+                         hipStream_t);
+hipError_t aca_ev_multi(const float*, const float*, float*, int, double*, unsigned int*, hipStream_t);
 hipError_t aca_sumsq(const float*, size_t, float*, hipStream_t);
 int aca_sumsq_parts();
 hipError_t aca_adam_step(float*, float*, float*, float*, size_t, const float*, float*, const float*, float*, uint16_t*,
@@ -375,12 +384,97 @@ void normalize(Tensor a, Tensor out, double eps) {
   check(aca_normalize(ptr<float>(a), ptr<float>(out), a.numel(), (float)eps, cur_stream(a)), "normalize");
 }
 
-void ev(Tensor x, Tensor y, Tensor out) {
+// ev(x, y, out[, part, ticket]): with a workspace (part fp64 [>= ev_blocks(n) * 8], ticket int32 zeroed once) the
+// many-workgroup form runs; without, the one-workgroup kernel.
+void ev(Tensor x, Tensor y, Tensor out, c10::optional<Tensor> part, c10::optional<Tensor> ticket) {
   need(x, at::kFloat, "x");
   need(y, at::kFloat, "y");
   TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.numel() >= 1, "ev: out must be fp32");
   TORCH_CHECK(x.numel() == y.numel(), "ev: size mismatch");
+  if (part.has_value() && part->defined()) {
+    need(*part, at::kDouble, "part");
+    TORCH_CHECK(ticket.has_value() && ticket->is_cuda() && ticket->scalar_type() == at::kInt, "ev: ticket int32");
+    TORCH_CHECK(part->numel() >= aca_ev_multi_blocks(x.numel()) * 8, "ev: part too small");
+    check(aca_ev_multi(ptr<float>(x), ptr<float>(y), ptr<float>(out), x.numel(), ptr<double>(*part),
+                       reinterpret_cast<unsigned int*>(ticket->data_ptr<int>()), cur_stream(x)),
+          "ev_multi");
+    return;
+  }
   check(aca_ev(ptr<float>(x), ptr<float>(y), ptr<float>(out), x.numel(), cur_stream(x)), "ev");
+}
+
+int64_t ev_blocks(int64_t n) { return aca_ev_multi_blocks((int)n); }
+
+std::vector<int64_t> returns_scan_geometry(int64_t T, int64_t N) {
+  int E, CH, K, blocks;
+  aca_returns_scan_geometry((int)T, (int)N, &E, &CH, &K, &blocks);
+  return {E, CH, K, blocks};
+}
+
+// Chunked-scan returns (mode 1 n-step window L, 2 GAE) + moments + EV + optional in-place adv normalisation.
+void returns_scan(Tensor r, Tensor v, Tensor d, Tensor ret, Tensor adv, int64_t mode, double gamma, double lam,
+                  int64_t L, bool norm, double eps, Tensor part, Tensor ticket, Tensor mom,
+                  c10::optional<Tensor> ev_out, c10::optional<Tensor> gz) {
+  check_returns(r, v, d, ret, adv);
+  const int T = r.size(0), N = r.size(1);
+  TORCH_CHECK(mode == 1 || mode == 2, "returns_scan: mode 1 (n-step) or 2 (GAE)");
+  int E, CH, K, blocks;
+  aca_returns_scan_geometry(T, N, &E, &CH, &K, &blocks);
+  need(part, at::kDouble, "part");
+  need(mom, at::kDouble, "mom");
+  TORCH_CHECK(part.numel() >= (int64_t)blocks * 8 && mom.numel() >= 8, "returns_scan: workspace too small");
+  TORCH_CHECK(ticket.is_cuda() && ticket.scalar_type() == at::kInt, "returns_scan: ticket int32");
+  double* gzp = nullptr;
+  if (mode == 1 && L < T) {
+    TORCH_CHECK(gz.has_value() && gz->defined(), "returns_scan: truncated n-step needs a gz workspace");
+    need(*gz, at::kDouble, "gz");
+    TORCH_CHECK(gz->numel() >= (int64_t)T * N, "returns_scan: gz too small");
+    gzp = ptr<double>(*gz);
+  }
+  float* evp = nullptr;
+  if (ev_out.has_value() && ev_out->defined()) {
+    need(*ev_out, at::kFloat, "ev_out");
+    evp = ptr<float>(*ev_out);
+  }
+  check(aca_returns_scan(ptr<float>(r), ptr<float>(v), ptr<uint8_t>(d), ptr<float>(ret), ptr<float>(adv), gzp,
+                         ptr<double>(part), reinterpret_cast<unsigned int*>(ticket.data_ptr<int>()), ptr<double>(mom),
+                         evp, T, N, (int)mode, (int)L, norm ? 1 : 0, (float)gamma, (float)lam, (float)eps,
+                         cur_stream(r)),
+        "returns_scan");
+}
+
+// PPO minibatch k of epoch ep: rows prp_index(off + i, n, key(seed, *uc, ep)) of the rollout gathered in one launch.
+void mb_gather(Tensor obs, Tensor act, Tensor logp, Tensor adv, Tensor ret, Tensor v, Tensor o_obs, Tensor o_act,
+               Tensor o_logp, Tensor o_adv, Tensor o_ret, Tensor o_v, int64_t seed, Tensor uc, int64_t ep,
+               int64_t off) {
+  TORCH_CHECK(obs.is_cuda() && obs.is_contiguous() && obs.scalar_type() == at::kByte, "mb_gather: obs uint8");
+  TORCH_CHECK(o_obs.is_cuda() && o_obs.is_contiguous() && o_obs.scalar_type() == at::kByte, "mb_gather: o_obs");
+  need(act, at::kInt, "act");
+  need(o_act, at::kInt, "o_act");
+  for (auto* t : {&logp, &adv, &ret, &v, &o_logp, &o_adv, &o_ret, &o_v}) need(*t, at::kFloat, "mb_gather f32");
+  TORCH_CHECK(uc.is_cuda() && uc.scalar_type() == at::kLong, "mb_gather: update counter int64");
+  const int64_t n = obs.size(0), mb = o_obs.size(0);
+  const int64_t R = obs.numel() / n;
+  TORCH_CHECK(o_obs.numel() == mb * R, "mb_gather: o_obs shape");
+  TORCH_CHECK(act.numel() == n && logp.numel() == n && adv.numel() == n && ret.numel() == n && v.numel() == n,
+              "mb_gather: per-row inputs must have n rows");
+  TORCH_CHECK(o_act.numel() == mb && o_logp.numel() == mb && o_adv.numel() == mb && o_ret.numel() == mb &&
+                  o_v.numel() == mb, "mb_gather: per-row outputs must have mb rows");
+  TORCH_CHECK(off >= 0 && off + mb <= n, "mb_gather: minibatch out of range");
+  check(aca_mb_gather(obs.data_ptr<uint8_t>(), R, ptr<int>(act), ptr<float>(logp), ptr<float>(adv), ptr<float>(ret),
+                      ptr<float>(v), o_obs.data_ptr<uint8_t>(), ptr<int>(o_act), ptr<float>(o_logp),
+                      ptr<float>(o_adv), ptr<float>(o_ret), ptr<float>(o_v), (int)mb, (int)n, (uint32_t)seed,
+                      uc.data_ptr<int64_t>(), (int)ep, (int)off, cur_stream(obs)),
+        "mb_gather");
+}
+
+void normalize_mom(Tensor a, Tensor out, Tensor mom, double eps) {
+  need(a, at::kFloat, "a");
+  need(out, at::kFloat, "out");
+  need(mom, at::kDouble, "mom");
+  TORCH_CHECK(a.numel() == out.numel() && mom.numel() >= 3, "normalize_mom: bad sizes");
+  check(aca_normalize_mom(ptr<float>(a), ptr<float>(out), ptr<double>(mom), a.numel(), (float)eps, cur_stream(a)),
+        "normalize_mom");
 }
 
 void moments(Tensor x, Tensor y, Tensor out) {
@@ -1113,7 +1207,15 @@ TORCH_LIBRARY(acamd, m) {
   m.def("categorical_sample(Tensor logits, Tensor keys, int seed, Tensor act, Tensor logp, Tensor ent) -> ()");
   m.def("categorical_sample_env(Tensor logits, Tensor tg, Tensor env_ids, int key_shift, int seed, Tensor act, "
         "Tensor logp, Tensor ent, Tensor? vout) -> ()");
-  m.def("ev(Tensor x, Tensor y, Tensor out) -> ()");
+  m.def("ev(Tensor x, Tensor y, Tensor out, Tensor? part=None, Tensor? ticket=None) -> ()");
+  m.def("ev_blocks(int n) -> int", &ev_blocks);
+  m.def("returns_scan_geometry(int T, int N) -> int[]", &returns_scan_geometry);
+  m.def("returns_scan(Tensor r, Tensor v, Tensor d, Tensor ret, Tensor adv, int mode, float gamma, float lam, int L, "
+        "bool norm, float eps, Tensor part, Tensor ticket, Tensor mom, Tensor? ev_out=None, Tensor? gz=None) -> ()");
+  m.def("normalize_mom(Tensor a, Tensor out, Tensor mom, float eps) -> ()");
+  m.def("mb_gather(Tensor obs, Tensor act, Tensor logp, Tensor adv, Tensor ret, Tensor v, Tensor o_obs, "
+        "Tensor o_act, Tensor o_logp, Tensor o_adv, Tensor o_ret, Tensor o_v, int seed, Tensor uc, int ep, "
+        "int off) -> ()");
   m.def("gaussian_sample(Tensor mu, Tensor log_std, Tensor keys, int seed, Tensor act, Tensor logp, Tensor ent) -> ()");
   m.def("gae(Tensor r, Tensor v, Tensor d, Tensor ret, Tensor adv, float gamma, float lam) -> ()");
   m.def("nstep_returns(Tensor r, Tensor v, Tensor d, Tensor tgt, Tensor adv, float gamma, int L) -> ()");
@@ -1188,6 +1290,9 @@ TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
   m.impl("gae", &gae);
   m.impl("nstep_returns", &nstep_returns);
   m.impl("normalize", &normalize);
+  m.impl("returns_scan", &returns_scan);
+  m.impl("normalize_mom", &normalize_mom);
+  m.impl("mb_gather", &mb_gather);
   m.impl("moments", &moments);
   m.impl("sumsq", &sumsq);
   m.impl("adam_step", &adam_step);

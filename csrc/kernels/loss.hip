@@ -65,14 +65,16 @@ template <int AC>
 __global__ void __launch_bounds__(LOSS_THREADS) ac_loss_kernel(LossArgs a) {
   constexpr int NJ = AC ? AC : CAT_MAX;
   __shared__ double sh[16 * 8];
-  __shared__ float dls[64];
-  __shared__ float dbs[64];
+  __shared__ float dls[LOSS_THREADS / 64][CAT_MAX + 1];   // per-wave partials, summed in wave order
+  __shared__ float dbs[LOSS_THREADS / 64][CAT_MAX + 1];
+  float dlp[CAT_MAX];   // gaussian: this thread's partial d/dlog_std
   __shared__ float s_rew[LOSS_STAGE], s_val[LOSS_STAGE + 256], s_ret[LOSS_STAGE], s_adv[LOSS_STAGE];
   __shared__ uint8_t s_dn[LOSS_STAGE];
   float dbp[CAT_MAX + 1];  // this thread's partial column sums of dz (head-bias gradient)
 #pragma unroll
   for (int j = 0; j <= CAT_MAX; ++j) dbp[j] = 0.f;
-  if (threadIdx.x < 64) { dls[threadIdx.x] = 0.f; dbs[threadIdx.x] = 0.f; }
+#pragma unroll
+  for (int j = 0; j < CAT_MAX; ++j) dlp[j] = 0.f;
   const bool staged = a.returns_mode && a.B <= LOSS_STAGE && a.N <= 256;
   if (staged) {
     for (int i = threadIdx.x; i < a.B; i += blockDim.x) {
@@ -227,7 +229,9 @@ __global__ void __launch_bounds__(LOSS_THREADS) ac_loss_kernel(LossArgs a) {
         // dlogp/dmu = zz / sigma ; dlogp/dls = zz^2 - 1 ; dH/dls = 1
         dz[j] = f2bf(g_lpa * zz * expf(-ls));
         const bool in_clip = ls_raw >= -2.5f && ls_raw <= 2.5f;
-        if (in_clip) atomicAdd(&dls[j], g_lpa * (zz * zz - 1.0f) - c_ent * invB);
+#pragma unroll
+        for (int q = 0; q < CAT_MAX; ++q)   // register partial (named slot, no dynamic indexing)
+          if (q == j && in_clip) dlp[q] += g_lpa * (zz * zz - 1.0f) - c_ent * invB;
       }
     }
     // critic
@@ -262,19 +266,38 @@ __global__ void __launch_bounds__(LOSS_THREADS) ac_loss_kernel(LossArgs a) {
     block_sum_multi<6>(red, sh);
     s_pg = red[0]; s_kl = red[1]; s_H = red[2]; s_vl = red[3]; s_cf = red[4]; s_ratio = red[5];
   }
+  // head-bias and log-std gradients: wave shuffle sums, then the waves' partials added in wave order by one thread
+  // per column (fixed order: bitwise reproducible)
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   if (a.dbias) {
-    const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int q = 0; q <= CAT_MAX; ++q) {
       if (q < a.dbias_n) {
         const float v = wave_sum(dbp[q]);
-        if (lane == 0) atomicAdd(&dbs[q], v);
+        if (lane == 0) dbs[wid][q] = v;
+      }
+    }
+  }
+  if (a.gaussian && a.dlog_std) {
+#pragma unroll
+    for (int q = 0; q < CAT_MAX; ++q) {
+      if (q < a.A) {
+        const float v = wave_sum(dlp[q]);
+        if (lane == 0) dls[wid][q] = v;
       }
     }
   }
   __syncthreads();
-  if (a.gaussian && a.dlog_std && threadIdx.x < a.A) atomicAdd(&a.dlog_std[threadIdx.x], dls[threadIdx.x]);
-  if (a.dbias && threadIdx.x < a.dbias_n) a.dbias[threadIdx.x] += dbs[threadIdx.x];
+  if (a.gaussian && a.dlog_std && threadIdx.x < a.A) {
+    float t = 0.f;
+    for (int w = 0; w < LOSS_THREADS / 64; ++w) t += dls[w][threadIdx.x];
+    a.dlog_std[threadIdx.x] += t;
+  }
+  if (a.dbias && threadIdx.x < a.dbias_n) {
+    float t = 0.f;
+    for (int w = 0; w < LOSS_THREADS / 64; ++w) t += dbs[w][threadIdx.x];
+    a.dbias[threadIdx.x] += t;
+  }
   if (threadIdx.x == 0) {
     const double inv = 1.0 / a.B;
     a.stats[0] = (float)(s_pg * inv);

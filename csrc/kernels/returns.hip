@@ -102,6 +102,44 @@ __global__ void prp_perm_kernel(int64_t* __restrict__ out, int n, uint32_t seed,
   if (i < n) out[i] = prp_index((uint32_t)i, (uint32_t)n, minibatch_key(seed, *uc, ep));
 }
 
+// PPO minibatch gather of the CNN engine (replaces six index_select copies + the permutation launch
+// per minibatch): workgroup i copies batch row src = prp_index(off + i, n, key(seed, update, epoch)) -- the keyed
+// epoch permutation of envs/rng.py, computed in place -- i.e. the frame stack (R bytes, 16 B vector copies) and the
+// per-row action / logp / advantage / return / old value.
+__global__ void __launch_bounds__(256) mb_gather_kernel(const uint8_t* __restrict__ obs, int64_t R,
+                                                        const int* __restrict__ act, const float* __restrict__ logp,
+                                                        const float* __restrict__ adv, const float* __restrict__ ret,
+                                                        const float* __restrict__ v, uint8_t* __restrict__ o_obs,
+                                                        int* __restrict__ o_act, float* __restrict__ o_logp,
+                                                        float* __restrict__ o_adv, float* __restrict__ o_ret,
+                                                        float* __restrict__ o_v, int n, uint32_t seed,
+                                                        const int64_t* __restrict__ uc, int ep, int off) {
+  const int i = blockIdx.x;
+  const uint32_t src = prp_index((uint32_t)(off + i), (uint32_t)n, minibatch_key(seed, *uc, ep));
+  const uint8_t* s = obs + (size_t)src * R;
+  uint8_t* d = o_obs + (size_t)i * R;
+  if ((R & 15) == 0) {
+    const uint4* s4 = reinterpret_cast<const uint4*>(s);
+    uint4* d4 = reinterpret_cast<uint4*>(d);
+    const int n4 = (int)(R >> 4);
+    int j = threadIdx.x;
+    for (; j + 3 * 256 < n4; j += 4 * 256) {   // four 16 B loads in flight per thread
+      const uint4 a = s4[j], b = s4[j + 256], c = s4[j + 512], e = s4[j + 768];
+      d4[j] = a; d4[j + 256] = b; d4[j + 512] = c; d4[j + 768] = e;
+    }
+    for (; j < n4; j += 256) d4[j] = s4[j];
+  } else {
+    for (int64_t j = threadIdx.x; j < R; j += 256) d[j] = s[j];
+  }
+  if (threadIdx.x == 0) {
+    o_act[i] = act[src];
+    o_logp[i] = logp[src];
+    o_adv[i] = adv[src];
+    o_ret[i] = ret[src];
+    o_v[i] = v[src];
+  }
+}
+
 // Per-variable statistics of a flat fp32 parameter slab (the reference's variable_summaries, Basic_AC/policies.py:
 // 9-18): out[v] = (mean, population stddev, max, min) of x[off_v, off_v + n_v). One workgroup per
 // variable, double accumulation (single pass: E[x^2] - mean^2 in fp64 matches the two-pass fp32 form closely).
@@ -141,6 +179,224 @@ __global__ void __launch_bounds__(256) seg_stats_kernel(const float* __restrict_
     out[4 * v + 1] = (float)sqrt(var);
     out[4 * v + 2] = M;
     out[4 * v + 3] = m;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------------
+// Chunked associative return scan fused with the batch statistics (reference
+// Basic_AC/run_AC.py:63-75, 241 and Basic_AC/util.py:4-12).
+//
+// Both estimators are reverse affine recurrences x_t = a_t + c_t x_{t+1}:
+//   GAE      a_t = r_t + gamma V_{t+1} (1-d_t) - V_t,  c_t = gamma lambda (1-d_t),  x_T = 0      -> adv, ret = adv + V
+//   n-step   a_t = r_t,                              c_t = gamma (1-d_t),           x_T = V_T  -> target (L >= T)
+// A workgroup owns E env columns x CH time chunks of K steps (thread = (chunk, env), env-fastest so every time
+// step is one coalesced row segment). Pass 1 composes each chunk's affine map (fp64), a Hillis-Steele suffix scan
+// over the CH chunk maps in LDS gives every chunk its incoming carry, pass 2 replays the chunk with that carry and
+// writes the outputs. A truncated window (n-step, L < T) scans the un-bootstrapped return Gz (x_T = 0) together
+// with the next-terminal index (suffix min) and fixes each window in a third pass:
+//   target_t = Gz_t + [no terminal in [t, h)] gamma^(h-t) (V_h - Gz_h),  h = min(t + L, T), Gz_T = 0,
+// the prefix-sum form of the O(L) window of Basic_AC/run_AC.py:63-75.
+// Every workgroup reduces its moments (adv, adv^2, ret, ret^2, V, V^2, ret*V) in fixed order into its partial
+// slot; the last workgroup to arrive sums the slots in block order (bitwise reproducible), writes the totals
+// (mom[0] = count, for the DP all-reduce), the EV-before correlation, and -- if `norm` -- normalises the whole
+// advantage array in place, so returns + EV + advantage normalisation are ONE launch.
+constexpr int RS_THREADS = 256;
+constexpr int RS_MOM = 7;
+
+struct RetScanArgs {
+  const float* r;
+  const float* v;
+  const uint8_t* d;
+  float* ret;
+  float* adv;
+  double* gz;            // [T, N] (truncated n-step windows only)
+  double* part;          // [gridDim.x, 8]
+  unsigned int* ticket;  // zero before the first launch; self-cleaning
+  double* mom;           // [8]: count, then the RS_MOM sums
+  float* ev_out;         // EV(ret, V[:T]) or null
+  int T, N, E, CH, K, mode, L, norm;
+  float gamma, lam, eps;
+};
+
+__global__ void __launch_bounds__(RS_THREADS) returns_scan_kernel(RetScanArgs a) {
+  __shared__ double s_a[RS_THREADS], s_c[RS_THREADS];
+  __shared__ int s_ft[RS_THREADS];
+  __shared__ double s_red[16 * RS_MOM];
+  __shared__ double s_tot[8];
+  __shared__ int s_flag;
+  const int tid = threadIdx.x;
+  const int e = tid % a.E, ch = tid / a.E;
+  const int T = a.T, N = a.N;
+  const int n = blockIdx.x * a.E + e;
+  const bool live = n < N && ch < a.CH;
+  const int t0 = min(ch * a.K, T), t1 = min(t0 + a.K, T);
+  const bool gae = a.mode == 2;
+  const bool window = !gae && a.L < T;
+  const double g = a.gamma, gl = (double)a.gamma * (double)a.lam;
+
+  // pass 1: chunk map x_{t0} = ca + cc x_{t1}, first terminal index in the chunk
+  double ca = 0.0, cc = 1.0;
+  int ft = T;
+  if (live) {
+    for (int t = t1 - 1; t >= t0; --t) {
+      const size_t i = (size_t)t * N + n;
+      const bool dn = a.d[i] != 0;
+      const double nd = dn ? 0.0 : 1.0;
+      ft = dn ? t : ft;
+      const double x = gae ? (double)a.r[i] + g * (double)a.v[i + N] * nd - (double)a.v[i] : (double)a.r[i];
+      const double c = (gae ? gl : g) * nd;
+      ca = x + c * ca;
+      cc = c * cc;
+    }
+  }
+  // suffix scan over the chunks of each env: F_ch = f_ch o F_{ch+1}
+  s_a[tid] = ca;
+  s_c[tid] = cc;
+  s_ft[tid] = ft;
+  __syncthreads();
+  for (int off = 1; off < a.CH; off <<= 1) {
+    double na = ca, nc = cc;
+    int nf = ft;
+    if (ch + off < a.CH) {
+      const int j = tid + off * a.E;
+      na = ca + cc * s_a[j];
+      nc = cc * s_c[j];
+      nf = min(ft, s_ft[j]);
+    }
+    __syncthreads();
+    s_a[tid] = ca = na;
+    s_c[tid] = cc = nc;
+    s_ft[tid] = ft = nf;
+    __syncthreads();
+  }
+  const double init = (live && !gae && !window) ? (double)a.v[(size_t)T * N + n] : 0.0;
+  double x = init;
+  int ntc = T;
+  if (ch + 1 < a.CH) {
+    const int j = tid + a.E;
+    x = s_a[j] + s_c[j] * init;
+    ntc = s_ft[j];
+  }
+
+  // pass 2: replay the chunk from its carry
+  double m[RS_MOM];
+#pragma unroll
+  for (int k = 0; k < RS_MOM; ++k) m[k] = 0.0;
+  if (live) {
+    for (int t = t1 - 1; t >= t0; --t) {
+      const size_t i = (size_t)t * N + n;
+      const double nd = a.d[i] ? 0.0 : 1.0;
+      const double vt = a.v[i];
+      if (gae) x = (double)a.r[i] + g * (double)a.v[i + N] * nd - vt + gl * nd * x;
+      else x = (double)a.r[i] + g * nd * x;
+      if (window) {
+        a.gz[i] = x;
+        continue;
+      }
+      const double rt = gae ? x + vt : x, ad = gae ? x : x - vt;
+      const float rf = (float)rt, af = (float)ad;
+      a.ret[i] = rf;
+      a.adv[i] = af;
+      m[0] += af; m[1] += (double)af * af; m[2] += rf; m[3] += (double)rf * rf;
+      m[4] += vt; m[5] += vt * vt; m[6] += (double)rf * vt;
+    }
+  }
+  if (window) {   // uniform across the grid: every thread reaches the barrier
+    __syncthreads();   // the later chunks' Gz (same workgroup) are visible
+    if (live) {
+      int nt = ntc;
+      const double gL = pow(g, (double)a.L);
+      for (int t = t1 - 1; t >= t0; --t) {
+        const size_t i = (size_t)t * N + n;
+        nt = a.d[i] ? t : nt;
+        const int h = min(t + a.L, T);
+        double tg = a.gz[i];
+        if (nt >= h) {
+          const double gh = (h - t == a.L) ? gL : pow(g, (double)(h - t));
+          tg += gh * ((double)a.v[(size_t)h * N + n] - (h < T ? a.gz[(size_t)h * N + n] : 0.0));
+        }
+        const double vt = a.v[i];
+        const float rf = (float)tg, af = (float)(tg - vt);
+        a.ret[i] = rf;
+        a.adv[i] = af;
+        m[0] += af; m[1] += (double)af * af; m[2] += rf; m[3] += (double)rf * rf;
+        m[4] += vt; m[5] += vt * vt; m[6] += (double)rf * vt;
+      }
+    }
+  }
+  block_sum_multi<RS_MOM>(m, s_red);
+  if (tid < RS_MOM) a.part[(size_t)blockIdx.x * 8 + tid] = m[tid];
+  if (!last_block_arrival(a.ticket, gridDim.x, &s_flag)) return;
+  if (tid < RS_MOM) {
+    double s = 0.0;
+    for (unsigned b = 0; b < gridDim.x; ++b) s += a.part[(size_t)b * 8 + tid];
+    s_tot[1 + tid] = s;
+  }
+  __syncthreads();
+  const double cnt = (double)T * N;
+  const double mean = s_tot[1] / cnt;
+  const double var = fmax(s_tot[2] / cnt - mean * mean, 0.0);
+  if (tid == 0) {
+    a.mom[0] = cnt;
+    for (int k = 0; k < RS_MOM; ++k) a.mom[1 + k] = s_tot[1 + k];
+    if (a.ev_out) {
+      const double mx = s_tot[3] / cnt, my = s_tot[5] / cnt;
+      const double vx = s_tot[4] / cnt - mx * mx, vy = s_tot[6] / cnt - my * my;
+      *a.ev_out = (float)((s_tot[7] / cnt - mx * my) / sqrt(fmax(vx, 0.0) * fmax(vy, 0.0)));
+    }
+  }
+  if (a.norm) {
+    const float fm = (float)mean, inv = 1.0f / (a.eps + (float)sqrt(var));
+    const int tot = T * N;
+    if ((tot & 3) == 0 && (((uintptr_t)a.adv) & 15) == 0) {
+      float4* p = reinterpret_cast<float4*>(a.adv);
+      for (int i = tid; i < tot / 4; i += RS_THREADS) {
+        float4 q = p[i];
+        q.x = (q.x - fm) * inv; q.y = (q.y - fm) * inv; q.z = (q.z - fm) * inv; q.w = (q.w - fm) * inv;
+        p[i] = q;
+      }
+    } else {
+      for (int i = tid; i < tot; i += RS_THREADS) a.adv[i] = (a.adv[i] - fm) * inv;
+    }
+  }
+}
+
+// Advantage normalisation from all-reduced totals (data-parallel runs: mom = sum over ranks of returns_scan's
+// moments, mom[0] = global count): out = (a - mean) / (eps + std_pop). Elementwise, many workgroups.
+__global__ void normalize_mom_kernel(const float* __restrict__ a, float* __restrict__ out,
+                                     const double* __restrict__ mom, int n, float eps) {
+  const double cnt = mom[0], mean = mom[1] / cnt;
+  const double var = fmax(mom[2] / cnt - mean * mean, 0.0);
+  const float fm = (float)mean, inv = 1.0f / (eps + (float)sqrt(var));
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) out[i] = (a[i] - fm) * inv;
+}
+
+// EV correlation over many workgroups: fixed-order partial moments + last-arriver combine (the one-workgroup
+// ev_kernel above caps at one CU; this is the PPO-sized form).
+__global__ void __launch_bounds__(RS_THREADS) ev_multi_kernel(const float* __restrict__ x, const float* __restrict__ y,
+                                                              float* __restrict__ out, int n, double* part,
+                                                              unsigned int* ticket) {
+  __shared__ double sh[16 * 5];
+  __shared__ double s_tot[5];
+  __shared__ int s_flag;
+  double m[5] = {0, 0, 0, 0, 0};
+  for (int i = blockIdx.x * RS_THREADS + threadIdx.x; i < n; i += gridDim.x * RS_THREADS) {
+    const double xi = x[i], yi = y[i];
+    m[0] += xi; m[1] += xi * xi; m[2] += yi; m[3] += yi * yi; m[4] += xi * yi;
+  }
+  block_sum_multi<5>(m, sh);
+  if (threadIdx.x < 5) part[(size_t)blockIdx.x * 8 + threadIdx.x] = m[threadIdx.x];
+  if (!last_block_arrival(ticket, gridDim.x, &s_flag)) return;
+  if (threadIdx.x < 5) {
+    double s = 0.0;
+    for (unsigned b = 0; b < gridDim.x; ++b) s += part[(size_t)b * 8 + threadIdx.x];
+    s_tot[threadIdx.x] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double mx = s_tot[0] / n, my = s_tot[2] / n;
+    const double vx = s_tot[1] / n - mx * mx, vy = s_tot[3] / n - my * my;
+    *out = (float)((s_tot[4] / n - mx * my) / sqrt(fmax(vx, 0.0) * fmax(vy, 0.0)));
   }
 }
 
@@ -187,5 +443,55 @@ extern "C" hipError_t aca_prp_perm(int64_t* out, int n, uint32_t seed, const int
 extern "C" hipError_t aca_seg_stats(const float* x, const int64_t* segs, int nv, float* out, hipStream_t stream) {
   if (nv <= 0) return hipSuccess;
   aca::seg_stats_kernel<<<nv, 256, 0, stream>>>(x, segs, out);
+  return hipGetLastError();
+}
+
+// Launch geometry of returns_scan: chunk length ~4 steps, CH chunks (power of two, <= 256) per env, E = 256 / CH
+// envs per workgroup.
+extern "C" void aca_returns_scan_geometry(int T, int N, int* E, int* CH, int* K, int* blocks) {
+  int ch = 1;
+  while (ch < 256 && ch * 4 < T) ch <<= 1;
+  *CH = ch;
+  *E = aca::RS_THREADS / ch;
+  *K = (T + ch - 1) / ch;
+  *blocks = (N + *E - 1) / *E;
+}
+
+extern "C" hipError_t aca_returns_scan(const float* r, const float* v, const uint8_t* d, float* ret, float* adv,
+                                       double* gz, double* part, unsigned int* ticket, double* mom, float* ev_out,
+                                       int T, int N, int mode, int L, int norm, float gamma, float lam, float eps,
+                                       hipStream_t stream) {
+  if (T <= 0 || N <= 0) return hipSuccess;
+  aca::RetScanArgs a{r, v, d, ret, adv, gz, part, ticket, mom, ev_out, T, N, 0, 0, 0, mode, L, norm, gamma, lam, eps};
+  int blocks;
+  aca_returns_scan_geometry(T, N, &a.E, &a.CH, &a.K, &blocks);
+  aca::returns_scan_kernel<<<blocks, aca::RS_THREADS, 0, stream>>>(a);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t aca_normalize_mom(const float* a, float* out, const double* mom, int n, float eps,
+                                        hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  const int blocks = std::min((n + 255) / 256, 1024);
+  aca::normalize_mom_kernel<<<blocks, 256, 0, stream>>>(a, out, mom, n, eps);
+  return hipGetLastError();
+}
+
+extern "C" int aca_ev_multi_blocks(int n) { return std::max(1, std::min(64, (n + 2047) / 2048)); }
+
+extern "C" hipError_t aca_ev_multi(const float* x, const float* y, float* out, int n, double* part,
+                                   unsigned int* ticket, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  aca::ev_multi_kernel<<<aca_ev_multi_blocks(n), aca::RS_THREADS, 0, stream>>>(x, y, out, n, part, ticket);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t aca_mb_gather(const uint8_t* obs, int64_t R, const int* act, const float* logp, const float* adv,
+                                    const float* ret, const float* v, uint8_t* o_obs, int* o_act, float* o_logp,
+                                    float* o_adv, float* o_ret, float* o_v, int mb, int n, uint32_t seed,
+                                    const int64_t* uc, int ep, int off, hipStream_t stream) {
+  if (mb <= 0) return hipSuccess;
+  aca::mb_gather_kernel<<<mb, 256, 0, stream>>>(obs, R, act, logp, adv, ret, v, o_obs, o_act, o_logp, o_adv, o_ret,
+                                                o_v, n, seed, uc, ep, off);
   return hipGetLastError();
 }

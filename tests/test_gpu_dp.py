@@ -33,19 +33,25 @@ def _free_port():
     return p
 
 
-def _cfg(num_envs, overlap):
-    return preset("pong_a2c", num_envs=num_envs, n_steps=3, device="cuda:0", outdir=None, quiet=True, stdout_freq=0,
-                  save_every=0, overlap=overlap, seed=5)
+def _cfg(num_envs, overlap, name="pong_a2c", **kw):
+    base = dict(n_steps=3) if name == "pong_a2c" else {}
+    base.update(kw)
+    return preset(name, num_envs=num_envs, device="cuda:0", outdir=None, quiet=True, stdout_freq=0,
+                  save_every=0, overlap=overlap, seed=5, **base)
 
 
-def _run(dp, num_envs, overlap, updates=UPDATES):
+def _run(dp, num_envs, overlap, updates=UPDATES, name="pong_a2c", capture=True, **kw):
     from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
-    tr = ActorCriticTrainer(_cfg(num_envs, overlap), dp=dp)
-    assert tr.engine is not None
+    tr = ActorCriticTrainer(_cfg(num_envs, overlap, name, **kw), dp=dp)
+    assert tr.engine is not None or tr.mlp is not None
     p0 = tr.flat.data.clone()
-    tr.capture(warmup=1)
-    assert tr.graph is not None
-    kind = tr.graph[0]
+    kind = "eager"
+    if capture:
+        tr.capture(warmup=1)
+        assert tr.graph is not None, "DP update fell back to eager execution"
+        kind = tr.graph[0]
+    else:
+        tr.step()   # the same one warm-up update the capture runs
     snaps = []
     for _ in range(updates):
         tr.step()
@@ -55,37 +61,43 @@ def _run(dp, num_envs, overlap, updates=UPDATES):
     return p0, tr, kind, snaps
 
 
-def _worker(rank, world, port, out_dir, num_envs, overlap):
+def _worker(rank, world, port, out_dir, num_envs, overlap, opts=None):
     import torch.distributed as dist
     from actor_critic_algs_on_tensorflow_amd.parallel.dp import DataParallel
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    opts = dict(opts or {})
+    tag = opts.pop("tag", overlap)
     try:
-        _, tr, kind, snaps = _run(DataParallel(), num_envs, overlap)
-        torch.save({"snaps": [s.cpu() for s in snaps], "kind": kind},
-                   os.path.join(out_dir, f"{overlap}_w{world}_r{rank}.pt"))
+        _, tr, kind, snaps = _run(DataParallel(), num_envs, overlap, **opts)
+        n_graphs = tr.graph[1].n_graphs if kind == "segments" else None
+        torch.save({"snaps": [s.cpu() for s in snaps], "kind": kind, "n_graphs": n_graphs},
+                   os.path.join(out_dir, f"{tag}_w{world}_r{rank}.pt"))
         dist.barrier()
     finally:
         dist.destroy_process_group()
 
 
-def _spawn(tmp_path, world, num_envs, overlap):
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), num_envs, overlap), nprocs=world, join=True)
-    return [torch.load(tmp_path / f"{overlap}_w{world}_r{r}.pt", weights_only=True) for r in range(world)]
+def _spawn(tmp_path, world, num_envs, overlap, **opts):
+    tag = opts.get("tag", overlap)
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), num_envs, overlap, opts), nprocs=world, join=True)
+    return [torch.load(tmp_path / f"{tag}_w{world}_r{r}.pt", weights_only=True) for r in range(world)]
 
 
 def _cos(a, b):
     return float(torch.nn.functional.cosine_similarity(a.double().flatten(), b.double().flatten(), dim=0))
 
 
+@pytest.mark.parametrize("world", [2, 4])
 @pytest.mark.parametrize("overlap", ["strict", "lag1"])
-def test_dp_segments_union_equivalence(cuda, tmp_path, overlap):
-    two = _spawn(tmp_path, 2, 8, overlap)
+def test_dp_segments_union_equivalence(cuda, tmp_path, overlap, world):
+    two = _spawn(tmp_path, world, 16 // world, overlap)
     one = _spawn(tmp_path, 1, 16, overlap)
     assert two[0]["kind"] == overlap and one[0]["kind"] == overlap
-    for a, b in zip(two[0]["snaps"], two[1]["snaps"]):
-        assert torch.equal(a, b), "ranks diverged"
+    for r in range(1, world):
+        for a, b in zip(two[0]["snaps"], two[r]["snaps"]):
+            assert torch.equal(a, b), "ranks diverged"
     # per-update parameter deltas of the 2-rank run follow the 1-rank union run (bf16 MFMA, split-K atomics:
     # summation order differs, so compare directions and magnitudes, not bits)
     s2, s1 = two[0]["snaps"], one[0]["snaps"]
@@ -105,3 +117,51 @@ def test_dp_world1_strict_equals_single_graph(cuda, tmp_path):
         d_dp = one[0]["snaps"][k] - one[0]["snaps"][k - 1]
         d_sg = snaps[k].cpu() - snaps[k - 1].cpu()
         assert _cos(d_dp, d_sg) > 0.99, (k, _cos(d_dp, d_sg))
+
+
+def _deltas(snaps):
+    return [snaps[k] - snaps[k - 1] for k in range(1, len(snaps))]
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_dp_ppo_captured_as_segments_equals_eager(cuda, tmp_path, world, monkeypatch):
+    """Breakout-shaped PPO under DP (minibatch gradient all-reduces, global advantage normalisation via the packed
+    fp64 moments, KL proxy for the adaptive lr) is captured as a segment chain -- no eager fallback -- and its
+    replay is BITWISE equal to the eager DP run (deterministic PPO backward: split-K planes + ordered finaliser,
+    ordered bias sums; fixed GEMM plans so both processes run the same kernels); ranks stay bit-identical."""
+    monkeypatch.setenv("ACAMD_GEMM_TUNE", "0")
+    kw = dict(name="breakout_ppo", n_steps=8, ppo_epochs=2, ppo_minibatches=2, kl_adaptive_lr=True, kl_coef=0.05)
+    cap = _spawn(tmp_path, world, 4, "strict", tag="ppo_cap", **kw)
+    eag = _spawn(tmp_path, world, 4, "strict", tag="ppo_eager", capture=False, **kw)
+    assert cap[0]["kind"] == "segments"
+    # 4 gradient all-reduces + 1 moments all-reduce + 1 KL all-reduce -> 7 graphs
+    assert cap[0]["n_graphs"] == 7, cap[0]["n_graphs"]
+    for r in range(1, world):
+        for a, b in zip(cap[0]["snaps"], cap[r]["snaps"]):
+            assert torch.equal(a, b), "ranks diverged"
+    for k, (a, b) in enumerate(zip(cap[0]["snaps"], eag[0]["snaps"])):
+        assert torch.equal(a, b), (k, _cos(a, b))
+
+
+def test_dp_mlp_ppo_captured_as_segments(cuda, tmp_path):
+    """MuJoCo-shaped PPO on the MLP engine under DP: captured (segments), ranks identical, replay follows eager."""
+    kw = dict(name="mujoco_ppo_dp8", n_steps=16, ppo_epochs=2, ppo_minibatches=4)
+    cap = _spawn(tmp_path, 2, 8, "strict", tag="mlp_cap", **kw)
+    eag = _spawn(tmp_path, 2, 8, "strict", tag="mlp_eager", capture=False, **kw)
+    assert cap[0]["kind"] == "segments"
+    for a, b in zip(cap[0]["snaps"], cap[1]["snaps"]):
+        assert torch.equal(a, b), "ranks diverged"
+    for d_c, d_e in zip(_deltas(cap[0]["snaps"]), _deltas(eag[0]["snaps"])):
+        assert _cos(d_c, d_e) > 0.99, _cos(d_c, d_e)
+
+
+@pytest.mark.parametrize("overlap", ["strict", "lag1"])
+def test_dp_bf16_buckets_track_fp32(cuda, tmp_path, overlap):
+    """bf16 gradient buckets (half the all-reduce bytes): ranks identical, updates follow the fp32-bucket run."""
+    b16 = _spawn(tmp_path, 2, 8, overlap, tag=f"{overlap}_b16", grad_bucket_dtype="bf16")
+    f32 = _spawn(tmp_path, 2, 8, overlap, tag=f"{overlap}_f32")
+    assert b16[0]["kind"] == overlap
+    for a, b in zip(b16[0]["snaps"], b16[1]["snaps"]):
+        assert torch.equal(a, b), "ranks diverged"
+    for d_b, d_f in zip(_deltas(b16[0]["snaps"]), _deltas(f32[0]["snaps"])):
+        assert _cos(d_b, d_f) > 0.97, _cos(d_b, d_f)

@@ -158,3 +158,54 @@ def test_a2c_update_is_bitwise_deterministic(cuda):
         outs.append((tr.flat.data.clone(), tr.stats_buf.clone()))
     assert torch.equal(outs[0][0], outs[1][0]), "parameters differ between identical runs"
     assert torch.equal(outs[0][1], outs[1][1])
+
+
+def test_mb_gather_equals_index_select_of_keyed_permutation(cuda):
+    """PPO minibatch gather (one launch: keyed epoch permutation evaluated in the kernel + every row copied) ==
+    index_select with the oracle permutation (envs/rng.py prp), bit for bit."""
+    from actor_critic_algs_on_tensorflow_amd import _native
+    from actor_critic_algs_on_tensorflow_amd.envs import rng
+    ops = _native.require()
+    n, mb, seed = 1000, 250, 12345
+    g = torch.Generator(device="cpu").manual_seed(3)
+    obs = torch.randint(0, 256, (n, 4, 84, 84), dtype=torch.uint8, generator=g).to(cuda)
+    act = torch.randint(0, 6, (n,), dtype=torch.int32, generator=g).to(cuda)
+    fl = [torch.randn(n, generator=g).to(cuda) for _ in range(4)]
+    uc = torch.tensor([7], dtype=torch.int64, device=cuda)
+    for ep, k in ((0, 0), (2, 3)):
+        outs = [torch.empty(mb, 4, 84, 84, dtype=torch.uint8, device=cuda),
+                torch.empty(mb, dtype=torch.int32, device=cuda)] + [torch.empty(mb, device=cuda) for _ in range(4)]
+        ops.mb_gather(obs, act, *fl, *outs, seed, uc, ep, k * mb)
+        key = rng.minibatch_key(seed, torch.tensor(7), ep)
+        sel = rng.prp(torch.arange(k * mb, (k + 1) * mb, dtype=torch.int64), n, key).to(cuda)
+        for src, out in zip([obs, act] + fl, outs):
+            assert torch.equal(torch.index_select(src, 0, sel), out)
+
+
+@pytest.mark.parametrize("name", ["breakout_ppo", "mujoco_ppo_dp8"])
+def test_ppo_graph_replay_bitwise_equals_eager(cuda, name, monkeypatch):
+    """Single-device PPO: the captured update replays bit-for-bit what the eager update computes (same kernels,
+    deterministic reductions), over several updates with the keyed minibatch permutation and adv normalisation."""
+    monkeypatch.setattr("actor_critic_algs_on_tensorflow_amd.ops.gemm.TUNE", False)
+    from actor_critic_algs_on_tensorflow_amd import preset
+    from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
+    kw = dict(num_envs=8, n_steps=16, ppo_epochs=2, ppo_minibatches=4, device="cuda:0", outdir=None, quiet=True,
+              stdout_freq=0, save_every=0, seed=3)
+    if name == "breakout_ppo":
+        kw.update(kl_adaptive_lr=True, kl_coef=0.05)
+    runs = []
+    for capture in (True, False):
+        tr = ActorCriticTrainer(preset(name, **kw))
+        if capture:
+            tr.capture(warmup=1)
+            assert tr.graph is not None and tr.graph[0] == "single"
+        else:
+            tr.step()
+        snaps = []
+        for _ in range(3):
+            tr.step()
+            snaps.append(tr.flat.data.clone())
+        torch.cuda.synchronize()
+        runs.append(snaps)
+    for k, (a, b) in enumerate(zip(*runs)):
+        assert torch.equal(a, b), k

@@ -80,30 +80,55 @@ def test_basic_ac_parity_trainer(tmp_path):
 
 
 # ------------------------------------------------------------------------------------------------ distributed
-def _dp_worker(rank, world, port, out_dir):
+def _dp_worker(rank, world, port, out_dir, n_envs=4, extra=None):
     import torch.distributed as dist
     from actor_critic_algs_on_tensorflow_amd.parallel.dp import DataParallel
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    cfg = preset("cartpole_cpu", **_quiet(num_envs=4, n_steps=5, seed=11, optimizer="adam", max_grad_norm=0.5))
+    cfg = preset("cartpole_cpu", **_quiet(num_envs=n_envs, n_steps=5, seed=11, optimizer="adam", max_grad_norm=0.5,
+                                          **(extra or {})))
     tr = ActorCriticTrainer(cfg, dp=DataParallel())
     for _ in range(3):
         tr.step()
-    if rank == 0:
-        torch.save({"p": tr.flat.data.clone()}, os.path.join(out_dir, "dp.pt"))
+    torch.save({"p": tr.flat.data.clone(), "kl": float(tr.stats["kl"])}, os.path.join(out_dir, f"dp{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_dp_gloo_equals_single_process_union_batch(tmp_path):
-    """Sync DP over 2 ranks x 4 envs == one process over the same 8 envs (grad all-reduce + global adv norm)."""
-    mp.spawn(_dp_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
-    dp = torch.load(tmp_path / "dp.pt", weights_only=True)["p"]
+@pytest.mark.parametrize("world", [2, 4])
+def test_dp_gloo_equals_single_process_union_batch(tmp_path, world):
+    """Sync DP over W ranks x 8/W envs == one process over the same 8 envs (grad all-reduce + global adv norm via
+    the packed moments all-reduce)."""
+    mp.spawn(_dp_worker, args=(world, _free_port(), str(tmp_path), 8 // world), nprocs=world, join=True)
+    ps = [torch.load(tmp_path / f"dp{r}.pt", weights_only=True)["p"] for r in range(world)]
+    for p in ps[1:]:
+        assert torch.equal(p, ps[0]), "ranks diverged"
     cfg = preset("cartpole_cpu", **_quiet(num_envs=8, n_steps=5, seed=11, optimizer="adam", max_grad_norm=0.5))
     single = ActorCriticTrainer(cfg)
     for _ in range(3):
         single.step()
-    assert torch.allclose(dp, single.flat.data, rtol=1e-4, atol=1e-6)
+    assert torch.allclose(ps[0], single.flat.data, rtol=1e-4, atol=1e-6)
+
+
+def test_dp_gloo_world4_ppo_kl_lr_and_bf16_buckets(tmp_path):
+    """World-4 PPO (minibatch all-reduce per optimiser step, global adv norm, KL proxy all-reduced for the adaptive
+    lr): ranks stay bit-identical; bf16 gradient buckets track the fp32 run."""
+    extra = dict(algo="ppo", ppo_epochs=2, ppo_minibatches=2, kl_adaptive_lr=True, kl_coef=0.1)
+    mp.spawn(_dp_worker, args=(4, _free_port(), str(tmp_path), 2, extra), nprocs=4, join=True)
+    fp = [torch.load(tmp_path / f"dp{r}.pt", weights_only=True) for r in range(4)]
+    for d in fp[1:]:
+        assert torch.equal(d["p"], fp[0]["p"]) and d["kl"] == fp[0]["kl"]
+    (tmp_path / "b").mkdir()
+    mp.spawn(_dp_worker, args=(4, _free_port(), str(tmp_path / "b"), 2, dict(extra, grad_bucket_dtype="bf16")),
+             nprocs=4, join=True)
+    bf = [torch.load(tmp_path / "b" / f"dp{r}.pt", weights_only=True)["p"] for r in range(4)]
+    for p in bf[1:]:
+        assert torch.equal(p, bf[0])
+    cfg = preset("cartpole_cpu", **_quiet(num_envs=2, n_steps=5, seed=11, optimizer="adam", max_grad_norm=0.5))
+    p0 = ActorCriticTrainer(cfg).flat.data
+    d_fp, d_bf = fp[0]["p"] - p0, bf[0] - p0
+    cos = float(torch.nn.functional.cosine_similarity(d_fp.double(), d_bf.double(), dim=0))
+    assert cos > 0.97, cos
 
 
 def _a3c_proc(rank, world, port, d):

@@ -1,7 +1,8 @@
 """A3C-style asynchronous parameter-server training (``A3C/process.py:156-288``, ``A3C/train.py``).
 
 Reference semantics: ``ps_num`` parameter-server tasks hold the global actor/critic (and
-the shared Adam slots, because every worker's optimiser creates its slots under the same global names); each of
+the shared Adam moment slots, because every worker's optimiser creates its slots under the same global names --
+but each worker's own beta-power step count, kept per source rank on the PS); each of
 ``worker_num`` workers collects whole episodes with its LOCAL copy until >= ``ep_length_stop`` steps, computes
 actor (clip +-0.1) and critic gradients locally, applies them to the GLOBAL variables with its own learning rate,
 then copies the global variables back (``sync_w_global``). The actor apply increments ``global_step``; the chief
@@ -89,17 +90,23 @@ class ParameterServer:
         self.critic_lr = critic_lr
         self.global_step = 0
         self.workers = set(worker_ranks)
+        self.worker_t = {}   # per-worker Adam step counts (bias correction)
 
-    def apply(self, grad, actor_lr):
-        """One worker's update: critic vars with the critic lr, actor vars clipped +-0.1 with the worker's lr."""
+    def apply(self, grad, actor_lr, src=None):
+        """One worker's update: critic vars with the critic lr, actor vars clipped +-0.1 with the worker's lr.
+        The moments are shared (one set of global slot variables), but the bias-correction step count is the
+        sender's own: each reference worker builds its own Adam whose beta1/beta2 powers advance only with its
+        applies (A3C/policies.py:83-98)."""
         a = self.actor_mask
         g = grad.clone()
         g[a] = torch.clamp(g[a], -ACTOR_CLIP, ACTOR_CLIP)
         ad = self.adam
-        ad.t += 1
+        t = self.worker_t.get(src, 0) + 1
+        self.worker_t[src] = t
+        ad.t.fill_(float(t))
         ad.m.mul_(ad.b1).add_(g, alpha=1 - ad.b1)
         ad.v.mul_(ad.b2).addcmul_(g, g, value=1 - ad.b2)
-        corr = np.sqrt(1 - ad.b2 ** float(ad.t)) / (1 - ad.b1 ** float(ad.t))
+        corr = np.sqrt(1 - ad.b2 ** float(t)) / (1 - ad.b1 ** float(t))
         lr = torch.where(a, torch.tensor(float(actor_lr)), torch.tensor(float(self.critic_lr)))
         self.params.data.sub_(lr * corr * ad.m / (torch.sqrt(ad.v) + ad.eps))
         self.global_step += 1
@@ -116,14 +123,14 @@ class ParameterServer:
             if cmd == CMD_APPLY:
                 buf = torch.empty(n + 1)
                 dist.recv(buf, src=src)
-                self.apply(buf[:n], float(buf[n]))
+                self.apply(buf[:n], float(buf[n]), src)
             out = torch.cat([self.params.data, torch.tensor([float(self.global_step)])])
             dist.send(out, dst=src)
 
 
 # ------------------------------------------------------------------------------------------------ worker
 class A3CWorker:
-    def __init__(self, cfg, task, shard, ps_ranks, logfile=None):
+    def __init__(self, cfg, task, shard, ps_ranks, logfile=None, logger=None, checkpoint_basename=None):
         self.cfg = cfg
         self.task = task
         self.is_chief = task == 0
@@ -145,7 +152,8 @@ class A3CWorker:
         self.log_gamma = LinearSchedule(100, 3000, -2, -8, 100)
         self.log_beta = LinearSchedule(100, 3000, 0, -4, 100)
         self.params = [p for _, p in _param_list(self.critic.net, self.actor.net)]
-        self.logger = ref.Logger(logfile, quiet=cfg.quiet) if logfile else None
+        self.logger = logger if logger is not None else (ref.Logger(logfile, quiet=cfg.quiet) if logfile else None)
+        self.ckpt_base = checkpoint_basename or ("model-" + C.env_prefix(cfg.env))
         self.gstep = 0
         self.history = []
 
@@ -251,7 +259,7 @@ class A3CWorker:
 
     def save(self, gstep):
         os.makedirs(self.cfg.checkpoint_dir, exist_ok=True)
-        base = "model-" + C.env_prefix(self.cfg.env)
+        base = self.ckpt_base
         path = os.path.join(self.cfg.checkpoint_dir, f"{base}-{gstep}")
         t = C.reference_tensors(self.actor.net, self.critic.net, "a3c", actor_lr=self.cfg.lr,
                                 ent_coef=self.cfg.ent_coef, kl_coef=self.cfg.kl_coef, critic_lr=self.cfg.critic_lr)
@@ -261,7 +269,7 @@ class A3CWorker:
         return path
 
 
-def run(cfg, rank=None, world=None, ps_num=None, log_dir=None):
+def run(cfg, rank=None, world=None, ps_num=None, log_dir=None, logger=None, checkpoint_basename=None):
     """Entry point of one process of the A3C job (PS or worker by rank); the process group must be initialised
     (gloo) or is initialised here from the torchrun environment."""
     if not dist.is_initialized():
@@ -287,6 +295,7 @@ def run(cfg, rank=None, world=None, ps_num=None, log_dir=None):
     logfile = os.path.join(log_dir, f"worker_{task}.log") if log_dir else None
     if logfile:
         os.makedirs(log_dir, exist_ok=True)
-    w = A3CWorker(cfg, task, shard, list(range(ps_num)), logfile)
+    w = A3CWorker(cfg, task, shard, list(range(ps_num)), None if logger is not None else logfile, logger=logger,
+                  checkpoint_basename=checkpoint_basename)
     hist = w.run()
     return {"role": "worker", "task": task, "history": hist, "global_step": w.gstep}

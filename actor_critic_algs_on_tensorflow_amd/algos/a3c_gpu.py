@@ -1,0 +1,270 @@
+"""GPU-native asynchronous parameter-server training (the reference's A3C, ``A3C/process.py:156-288``, redesigned
+for MI355X: SURVEY §2.2 D03/D04/X04, §5.8).
+
+Roles (ranks ``0 .. ps_num-1`` are parameter servers, the rest workers, as :mod:`.a3c`):
+
+* **worker**: a vectorised trainer (:class:`.trainer.ActorCriticTrainer`, algo ``a2c``) that owns a device env bank
+  (``num_envs`` envs, global env ids ``task * num_envs + i``) and the device engines (native MLP / CNN engine,
+  hipGraph capture). One iteration = rollout ``[T, N]`` + returns + loss + backward exactly as the synchronous
+  trainer, but the optimiser step is replaced by the **exchange**: the gradient slab (and the worker's own
+  KL-adaptive actor lr) is pushed to every PS shard, the updated parameters and the global step are pulled back
+  (the reference's ``apply_gradients`` on the global variables + ``sync_w_global``). Under capture the exchange is a
+  segment cut (:class:`.trainer.SegmentRecorder`): rollout..backward and the post-pull work replay as graphs, the
+  exchange runs between them.
+* **parameter server**: holds a contiguous shard of the flat fp32 parameter slab and its Adam moments ON ITS
+  DEVICE, and applies each request with the fused native Adam kernel (actor segment element-clipped +-clip_value
+  with the sender's lr, critic segment with the critic lr), one request at a time -- applies are serialised, so the
+  reference's Hogwild races on the PS variables cannot happen. Adam's bias-correction step count is
+  kept PER WORKER (each reference worker builds its own Adam, whose beta powers advance only with its own applies).
+
+Transport: a gloo **control plane** (int64 headers, ``recv`` from any source, so the PS serves whichever worker
+asks first) and a **data plane** for the payloads: ``"nccl"`` = RCCL point-to-point ``send/recv`` of device
+tensors (over xGMI between GPUs of a node; needs one GPU per rank), or ``"gloo"`` = the same messages staged
+through host memory (CPU runs, several ranks sharing one GPU). Bounded staleness (stale-synchronous parallel):
+with ``max_staleness = s`` a PS defers a worker's apply while that worker is more than ``s`` applies ahead of
+the slowest live worker, so a gradient is never older than ``(W - 1) * (s + 1)`` global steps; ``s < 0`` disables
+the bound (the reference's unbounded asynchrony). Every apply is logged as (worker, pulled version, global step).
+"""
+from __future__ import annotations
+
+import time
+
+import torch
+import torch.distributed as dist
+
+from .. import envs as E
+from ..ops.optim import make_optimizer
+
+CMD_PULL, CMD_APPLY, CMD_DONE = 1, 2, 3
+
+
+def shard_ranges(flat, ps_num):
+    """Contiguous slab ranges, one per PS, cut at parameter boundaries and balanced by element count."""
+    bounds = [off + p.numel() for p, off in zip(flat.params, flat.offsets)]
+    total = flat.numel
+    cuts = [0]
+    for s in range(1, ps_num):
+        target = total * s / ps_num
+        c = min(bounds, key=lambda b: abs(b - target))
+        cuts.append(max(c, cuts[-1]))
+    cuts.append(total)
+    return [(cuts[i], cuts[i + 1]) for i in range(ps_num)]
+
+
+class _Planes:
+    """Control plane (gloo, CPU headers) + data plane (RCCL device tensors, or gloo via host staging)."""
+
+    def __init__(self, ctrl, data, data_backend, device):
+        self.ctrl, self.data, self.backend, self.device = ctrl, data, data_backend, device
+
+    def send_hdr(self, vals, dst):
+        dist.send(torch.tensor(vals, dtype=torch.int64), dst=dst, group=self.ctrl)
+
+    def recv_hdr(self, src=None):
+        h = torch.zeros(4, dtype=torch.int64)
+        s = dist.recv(h, src=src, group=self.ctrl)
+        return s, [int(x) for x in h]
+
+    def send(self, t, dst):
+        if self.backend == "nccl":
+            dist.send(t, dst=dst, group=self.data)
+        else:
+            dist.send(t.detach().to("cpu"), dst=dst, group=self.data)
+
+    def recv(self, t, src):
+        if self.backend == "nccl":
+            dist.recv(t, src=src, group=self.data)
+        else:
+            h = torch.empty(t.shape, dtype=t.dtype)
+            dist.recv(h, src=src, group=self.data)
+            t.copy_(h)
+
+
+def _build_flat(cfg, device):
+    """Model + flat slab exactly as a worker's trainer builds them (same seed -> same initial values)."""
+    from ..models.policy import build_model
+    from ..ops.optim import FlatParams
+    fs = 4 if ("Pong" in cfg.env or "Breakout" in cfg.env) else cfg.frames   # as ActorCriticTrainer
+    env = E.make(cfg.env, 1, device=device, seed=cfg.seed, frame_stack=fs)
+    model = build_model(env, cfg.model, cfg.model_variant, seed=cfg.seed).to(device)
+    return FlatParams(model.param_groups(), device)
+
+
+class DeviceParameterServer:
+    def __init__(self, cfg, sid, rng_, worker_ranks, planes, device, max_staleness=-1):
+        self.cfg, self.sid = cfg, sid
+        self.s, self.e = rng_
+        self.n = self.e - self.s
+        self.device = torch.device(device)
+        self.flat = _build_flat(cfg, self.device)
+        self.planes = planes
+        self.workers = list(worker_ranks)
+        self.live = set(self.workers)
+        self.max_staleness = max_staleness
+        # optimiser segments = (group, start, end) of this shard, with their own Adam moments
+        self.segs = []
+        for g, (gs, ge) in list(self.flat.groups.items()):
+            a, b = max(gs, self.s), min(ge, self.e)
+            if a >= b:
+                continue
+            name = f"ps{sid}_{g}"
+            self.flat.groups[name] = (a, b)
+            actor = g != "critic"
+            opt = make_optimizer("adam", self.flat, name, cfg.lr if actor else cfg.critic_lr,
+                                 cfg.clip_value if actor else cfg.critic_clip_value, cfg.max_grad_norm)
+            self.segs.append((opt, a - self.s, b - self.s, actor))
+        # per-worker Adam step counts (bias correction advances with that worker's applies only)
+        self.t = {(k, w): torch.zeros((), dtype=torch.float32, device=self.device)
+                  for k in range(len(self.segs)) for w in self.workers}
+        self.n_applies = {w: 0 for w in self.workers}
+        self.global_step = 0
+        self.log = []   # (worker rank, version the gradient was computed at, global step before the apply)
+        self._pay = {w: torch.zeros(self.n + 1, device=self.device) for w in self.workers}
+        self._rep = torch.zeros(self.n + 1, device=self.device)
+
+    # -- one apply ------------------------------------------------------------------------------------------------
+    @torch.no_grad()
+    def apply(self, w, version):
+        buf = self._pay[w]
+        for k, (opt, a, b, actor) in enumerate(self.segs):
+            opt.g = buf[a:b]
+            if actor:
+                opt.lr.copy_(buf[self.n])   # the sender's (KL-adaptive) actor lr, device to device
+            opt.t = self.t[(k, w)]
+            opt.step()
+        self.log.append((w, version, self.global_step))
+        self.global_step += 1
+        self.n_applies[w] += 1
+
+    def reply(self, w):
+        self._rep[:self.n].copy_(self.flat.data[self.s:self.e])
+        self._rep[self.n] = float(self.global_step)
+        self.planes.send(self._rep, w)
+
+    def _allowed(self, w):
+        if self.max_staleness < 0 or len(self.live) <= 1:
+            return True
+        slowest = min(self.n_applies[v] for v in self.live)
+        return self.n_applies[w] - slowest <= self.max_staleness
+
+    def serve(self):
+        pending = []   # deferred applies (stale-synchronous bound), served in arrival order once allowed
+        while self.live or pending:
+            if self.live:
+                src, (cmd, _task, version, _) = self.planes.recv_hdr()
+                if cmd == CMD_DONE:
+                    self.live.discard(src)
+                elif cmd == CMD_PULL:
+                    self.reply(src)
+                else:
+                    self.planes.recv(self._pay[src], src)
+                    pending.append((src, version))
+            progressed = True
+            while progressed:
+                progressed = False
+                for i, (w, v) in enumerate(pending):
+                    if self._allowed(w) or not self.live - {w}:
+                        pending.pop(i)
+                        self.apply(w, v)
+                        self.reply(w)
+                        progressed = True
+                        break
+            if not self.live and pending:   # every other worker finished: nothing left to wait for
+                for w, v in pending:
+                    self.apply(w, v)
+                    self.reply(w)
+                pending = []
+
+
+class GPUWorker:
+    """A vectorised device trainer whose optimiser step is the PS exchange."""
+
+    def __init__(self, cfg, task, ranges, ps_ranks, planes, device):
+        from .trainer import ActorCriticTrainer
+        self.cfg, self.task = cfg, task
+        self.ranges, self.ps_ranks, self.planes = ranges, ps_ranks, planes
+        self.device = torch.device(device)
+        wcfg = cfg.replace(algo="a2c", device=str(self.device), outdir=None if task else cfg.outdir)
+        fs = 4 if ("Pong" in cfg.env or "Breakout" in cfg.env) else cfg.frames
+        env = E.make(cfg.env, cfg.num_envs, device=self.device, seed=cfg.seed, env_offset=task * cfg.num_envs,
+                     frame_stack=fs)
+        self.tr = ActorCriticTrainer(wcfg, env=env)
+        self.tr._grad_sink = self._exchange
+        self.version = 0
+        n = [e - s for s, e in ranges]
+        self._pay = [torch.zeros(k + 1, device=self.device) for k in n]
+        self._rep = [torch.zeros(k + 1, device=self.device) for k in n]
+
+    @torch.no_grad()
+    def _exchange(self, pull_only=False):
+        tr = self.tr
+        flat = tr.flat
+        lr = tr.actor_opt.lr
+        for sid, ((s, e), r) in enumerate(zip(self.ranges, self.ps_ranks)):
+            self.planes.send_hdr([CMD_PULL if pull_only else CMD_APPLY, self.task, self.version, 0], r)
+            if not pull_only:
+                p = self._pay[sid]
+                p[:e - s].copy_(flat.grad[s:e])
+                p[e - s:].copy_(lr.reshape(1))
+                self.planes.send(p, r)
+        for sid, ((s, e), r) in enumerate(zip(self.ranges, self.ps_ranks)):
+            self.planes.recv(self._rep[sid], r)
+            flat.data[s:e].copy_(self._rep[sid][:e - s])
+        self.version = int(self._rep[0][-1])   # global step of PS 0 (host read: the exchange is synchronous)
+        return self.version
+
+    def run(self, total_updates, report_every=0):
+        """Trains until the PS global step reaches ``total_updates``. Returns the global step after each of this
+        worker's updates; with ``report_every`` also (update, global step, mean finished-episode return) rows in
+        ``self.returns`` (a host read of the env bank's episode statistics every ``report_every`` updates)."""
+        tr = self.tr
+        self._exchange(pull_only=True)   # initial sync_w_global (reference bug #12 fixed)
+        tr._after_pull()
+        if tr._can_capture():
+            tr.capture(warmup=1)
+        hist = []
+        self.returns = []
+        while self.version < total_updates:
+            tr.step()
+            hist.append(self.version)
+            if report_every and len(hist) % report_every == 0:
+                ret, n_ep, _ = tr.env.drain_episode_stats()
+                self.returns.append((len(hist), self.version, ret, n_ep))
+        for r in self.ps_ranks:
+            self.planes.send_hdr([CMD_DONE, self.task, self.version, 0], r)
+        return hist
+
+
+def run(cfg, rank=None, world=None, ps_num=None, data_backend="gloo", max_staleness=-1, device=None,
+        report_every=0):
+    """Entry point of one process of the GPU-native async job. The default process group (gloo) must exist or is
+    created from the torchrun environment; with ``data_backend="nccl"`` an RCCL group carries the payloads."""
+    if not dist.is_initialized():
+        dist.init_process_group("gloo")
+    rank = dist.get_rank() if rank is None else rank
+    world = dist.get_world_size() if world is None else world
+    ps_num = cfg.ps_num if ps_num is None else ps_num
+    assert world - ps_num >= 1, "need at least one worker rank"
+    device = torch.device(device or cfg.device)
+    if device.type == "cuda":
+        torch.cuda.set_device(device)
+    ctrl = dist.new_group(backend="gloo")
+    data = dist.new_group(backend="nccl") if data_backend == "nccl" else ctrl
+    planes = _Planes(ctrl, data, data_backend, device)
+    flat = _build_flat(cfg, torch.device("cpu"))
+    ranges = shard_ranges(flat, ps_num)
+    t0 = time.time()
+    if rank < ps_num:
+        ps = DeviceParameterServer(cfg, rank, ranges[rank], range(ps_num, world), planes, device, max_staleness)
+        ps.serve()
+        return {"role": "ps", "global_step": ps.global_step, "log": ps.log, "n_applies": ps.n_applies,
+                "adam_t": {f"{k}:{w}": float(t) for (k, w), t in ps.t.items()}, "wall_s": time.time() - t0,
+                "params": ps.flat.data[ps.s:ps.e].detach().cpu()}
+    task = rank - ps_num
+    w = GPUWorker(cfg, task, ranges, list(range(ps_num)), planes, device)
+    hist = w.run(cfg.total_updates, report_every)
+    tr = w.tr
+    ret, n_ep, _ = tr.env.drain_episode_stats()
+    return {"role": "worker", "task": task, "global_step": w.version, "history": hist, "updates": len(hist),
+            "env_steps": tr.env_steps, "wall_s": time.time() - t0, "ep_return": ret, "episodes": n_ep,
+            "returns": w.returns}

@@ -187,6 +187,7 @@ class ActorCriticTrainer:
         self._comm_grad = None      # lag-1 DP: the all-reduced copy of the previous update's gradient
         self._comm_work = None
         self._rec = None            # SegmentRecorder while capturing a segmented (DP) update
+        self._grad_sink = None      # async PS worker: replaces all-reduce + optimiser (algos/a3c_gpu.py)
         self._kl_buf = torch.zeros(1, dtype=torch.float32, device=self.device) if dp is not None else None
         self.logger = None
         if self.rank == 0 and cfg.outdir:
@@ -386,6 +387,15 @@ class ActorCriticTrainer:
         total = a_loss + (cfg.vf_coef * c_loss if shared else c_loss)
         return total, a_loss, c_loss, kl, entm, clipfrac
 
+    def _after_pull(self):
+        """Parameters were replaced from outside (PS pull): clear the gradient slab the optimiser would have
+        zeroed and refresh the engines' low-precision / transposed weight shadows."""
+        self.flat.grad.zero_()
+        if self.shadow is not None:
+            self.shadow.copy_(self.flat.data)
+        if self.mlp is not None:
+            self.mlp.sync_shadow()
+
     def _comm(self, fn):
         """Runs a collective now (eager) or, while a :class:`SegmentRecorder` is capturing, records it as a cut
         between two graphs. ``fn`` must work in place on buffers that outlive the capture."""
@@ -397,6 +407,10 @@ class ActorCriticTrainer:
     def _apply_grads(self):
         """All-reduce (DP) + optimiser step; inside a segmented capture the pre-graph stops before both."""
         if self._defer_allreduce:
+            return
+        if self._grad_sink is not None:   # async PS worker (a3c_gpu): push the gradient, pull the parameters
+            self._comm(self._grad_sink)
+            self._after_pull()
             return
         if self.dp is not None:
             dp, g = self.dp, self.flat.grad
@@ -764,7 +778,7 @@ class ActorCriticTrainer:
             finally:
                 self._defer_allreduce = False
                 self._bw_stage = "all"
-        elif self.dp is not None:
+        elif self.dp is not None or self._grad_sink is not None:
             rec = SegmentRecorder()
             self._rec = rec
             try:

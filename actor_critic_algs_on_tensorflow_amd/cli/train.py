@@ -6,6 +6,12 @@ process joins one ``torch.distributed`` gloo group: rendezvous at ``127.0.0.1:in
 ``<outdir>/worker_<task>.log``; the chief (worker 0) writes ``<checkpoint_dir>/model-<EnvPrefix>-<global_step>``.
 
 Also usable under torchrun (``--job auto``: the rank decides the role).
+
+``--device cuda`` (or ``cuda:K``; ``cuda`` alone maps each rank to GPU ``rank % device_count``) selects the
+GPU-native mode (:mod:`..algos.a3c_gpu`): workers own ``--num_envs`` device envs and the device engines, PS tasks
+keep their shard and Adam moments on the device; ``--data_plane nccl`` moves the payloads over RCCL (one GPU per
+rank), ``gloo`` stages them through host memory. ``--max_staleness s`` bounds gradient staleness (-1: unbounded,
+as the reference).
 """
 from __future__ import annotations
 
@@ -34,6 +40,11 @@ def build_parser():
     p.add_argument("--desired_kl", default=0.002, type=float)
     p.add_argument("--max_iters", default=int(1e7), type=int, help="stop at this many global steps (MAX_ITERS)")
     p.add_argument("--quiet", action="store_true")
+    p.add_argument("--device", default="cpu", help="cpu (reference-shaped episode workers) | cuda[:K] (GPU-native)")
+    p.add_argument("--num_envs", default=16, type=int, help="GPU mode: device envs per worker")
+    p.add_argument("--n_steps", default=16, type=int, help="GPU mode: rollout length per update")
+    p.add_argument("--data_plane", default="gloo", choices=["gloo", "nccl"])
+    p.add_argument("--max_staleness", default=-1, type=int)
     return p
 
 
@@ -58,7 +69,16 @@ def main(argv=None):
     task = rank if role == "ps" else rank - args.ps_num
     log = os.path.join(args.outdir, "worker_{}.log".format(task)) if role == "worker" else "N/A"
     print("Starting {} {} with log at {}".format(role, task, log), flush=True)
-    out = a3c.run(cfg, rank=rank, world=world, ps_num=args.ps_num, log_dir=args.outdir)
+    if args.device.startswith("cuda"):
+        import torch
+        from ..algos import a3c_gpu
+        dev = args.device if ":" in args.device else f"cuda:{rank % max(1, torch.cuda.device_count())}"
+        cfg = cfg.replace(device=dev, num_envs=args.num_envs, n_steps=args.n_steps, cuda_graph=True,
+                          outdir=log if role == "worker" and task == 0 else None)
+        out = a3c_gpu.run(cfg, rank=rank, world=world, ps_num=args.ps_num, data_backend=args.data_plane,
+                          max_staleness=args.max_staleness, device=dev)
+    else:
+        out = a3c.run(cfg, rank=rank, world=world, ps_num=args.ps_num, log_dir=args.outdir)
     dist.destroy_process_group()
     return out
 

@@ -6,6 +6,7 @@ accepted and ignored).
   ``sync_w_global`` (``Basic_AC/policies.py:33-120``; A3C variant ``A3C/policies.py:34-134``).
 * :class:`Critic` -- ``value`` / ``optimize`` / ``set_opt_param`` (a no-op, as in the reference: bug #6 of
   SURVEY §2.9) / ``printoo`` / ``sync_w_global`` (``Basic_AC/policies.py:123-162``).
+* :func:`process_fn` -- one PS / worker process of the async job (``A3C/process.py:156-158`` signature).
 * :func:`rollout`, :func:`train_ciritic`, :func:`train_actor`, :func:`get_roll_params`, :func:`test_process`,
   :class:`GymEnv` (a one-env gym-style adapter over the env bank), plus re-exports of ``Framer``, ``PathAdv``,
   ``LinearSchedule``, ``Logger``, ``var_accounted_for``, ``make_np``.
@@ -287,6 +288,44 @@ def test_process(env_id, random_seed, stack_frames, model_path, num_episodes, an
     from ..api import evaluate
     return evaluate(model_path, env_id, num_episodes=num_episodes, seed=random_seed, frames=stack_frames,
                     animate=animate)
+
+
+def process_fn(cluster, task_id, job, env_id, logger, save_path, stdout_freq, random_seed=12321, gamma=0.98,
+               look_ahead=40, stack_frames=3, animate=False, save_every=600, desired_kl=0.002, TB_log=False,
+               run_mode="train", checkpoint_basename="model", device="cpu", num_envs=16, n_steps=16,
+               data_plane="gloo", max_staleness=-1, max_iters=int(1e7)):
+    """``A3C/process.py:156-158``: one process of the async job, by (job, task_id) in the cluster dict
+    ``{"ps": ["host:port", ...], "worker": [...]}``. All processes join one gloo group rendezvousing at the first
+    PS address (PS tasks are ranks 0..P-1, workers P..). ``device="cpu"`` runs the reference-shaped episode
+    workers (:mod:`..algos.a3c`); ``device="cuda[:K]"`` the GPU-native mode (:mod:`..algos.a3c_gpu`: vectorised
+    device workers, device-resident PS shards, RCCL or gloo data plane). ``logger`` is the worker's Logger (None
+    for PS tasks), ``save_path`` the checkpoint directory, ``checkpoint_basename`` the file prefix. Returns the
+    role's summary dict (the reference returns nothing; a PS task returns when every worker has finished instead
+    of joining forever)."""
+    import datetime
+    import os
+
+    import torch.distributed as dist
+
+    from ..config import preset
+    num_ps, num_workers = len(cluster["ps"]), len(cluster["worker"])
+    rank = task_id if job == "ps" else num_ps + task_id
+    world = num_ps + num_workers
+    host, port = cluster["ps"][0].rsplit(":", 1)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1" if host in ("localhost", "") else host)
+    os.environ.setdefault("MASTER_PORT", port)
+    if not dist.is_initialized():
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=600))
+    cfg = preset("a3c", env=env_id, seed=random_seed, gamma=gamma, look_ahead=look_ahead, frames=stack_frames,
+                 save_every=save_every, desired_kl=desired_kl, tboard=bool(TB_log), mode=run_mode,
+                 checkpoint_dir=save_path, stdout_freq=stdout_freq, ps_num=num_ps, total_updates=int(max_iters))
+    if str(device).startswith("cuda"):
+        from ..algos import a3c_gpu
+        cfg = cfg.replace(device=device, num_envs=num_envs, n_steps=n_steps, cuda_graph=True, outdir=None)
+        return a3c_gpu.run(cfg, rank=rank, world=world, ps_num=num_ps, data_backend=data_plane,
+                           max_staleness=max_staleness, device=device)
+    from ..algos import a3c
+    return a3c.run(cfg, rank=rank, world=world, ps_num=num_ps, logger=logger, checkpoint_basename=checkpoint_basename)
 
 
 # ---- reference helper names (SURVEY §2.1 C13/C14), as plain tensor functions -------------------------------------

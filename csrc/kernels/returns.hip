@@ -350,7 +350,20 @@ __global__ void __launch_bounds__(RS_THREADS) returns_scan_kernel(RetScanArgs a)
     const int tot = T * N;
     if ((tot & 3) == 0 && (((uintptr_t)a.adv) & 15) == 0) {
       float4* p = reinterpret_cast<float4*>(a.adv);
-      for (int i = tid; i < tot / 4; i += RS_THREADS) {
+      const int n4 = tot / 4;
+      int i = tid;
+      for (; i + 7 * RS_THREADS < n4; i += 8 * RS_THREADS) {   // 8 loads in flight per thread, then 8 stores
+        float4 q[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) q[u] = p[i + u * RS_THREADS];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          q[u].x = (q[u].x - fm) * inv; q[u].y = (q[u].y - fm) * inv;
+          q[u].z = (q[u].z - fm) * inv; q[u].w = (q[u].w - fm) * inv;
+          p[i + u * RS_THREADS] = q[u];
+        }
+      }
+      for (; i < n4; i += RS_THREADS) {
         float4 q = p[i];
         q.x = (q.x - fm) * inv; q.y = (q.y - fm) * inv; q.z = (q.z - fm) * inv; q.w = (q.w - fm) * inv;
         p[i] = q;

@@ -1,0 +1,139 @@
+"""GPU-native async parameter-server mode (algos/a3c_gpu.py; reference A3C/process.py:156-288): vectorised device
+workers push gradients / pull parameters, the PS applies them serially with the fused Adam kernel and per-worker
+step counts. CPU runs (gloo, world 3 and 4) check the protocol; the GPU run shares cuda:0 between three ranks
+(gloo data plane staged through host memory -- RCCL needs one GPU per rank)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from actor_critic_algs_on_tensorflow_amd import preset
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _cfg(device, total, **kw):
+    base = dict(num_envs=4, n_steps=8, total_updates=total, outdir=None, quiet=True, stdout_freq=0, save_every=0,
+                device=device, cuda_graph=device.startswith("cuda"), seed=7)
+    base.update(kw)
+    return preset("a3c", **base)
+
+
+def _proc(rank, world, port, out, device, total, ps_num, staleness, kw):
+    import torch.distributed as dist
+    from actor_critic_algs_on_tensorflow_amd.algos import a3c_gpu
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if device.startswith("cuda"):
+        torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        res = a3c_gpu.run(_cfg(device, total, **kw), ps_num=ps_num, data_backend="gloo", max_staleness=staleness,
+                          device=device)
+        torch.save(res, os.path.join(out, f"r{rank}.pt"))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(tmp_path, world, device="cpu", total=12, ps_num=1, staleness=1, **kw):
+    mp.spawn(_proc, args=(world, _free_port(), str(tmp_path), device, total, ps_num, staleness, kw), nprocs=world,
+             join=True)
+    return [torch.load(tmp_path / f"r{r}.pt", weights_only=False) for r in range(world)]
+
+
+def _check(res, ps_num, staleness, total):
+    ps, workers = res[:ps_num], res[ps_num:]
+    W = len(workers)
+    for p in ps:
+        assert p["role"] == "ps"
+        log = p["log"]
+        # serialised global steps: every apply takes exactly the next step
+        assert [g for _, _, g in log] == list(range(len(log)))
+        assert p["global_step"] == len(log) >= total
+        # bounded staleness (stale-synchronous bound s): no gradient older than (W - 1) * (s + 1) steps
+        if staleness >= 0:
+            assert max(g - v for _, v, g in log) <= (W - 1) * (staleness + 1), log
+        # per-worker Adam step counts == that worker's applies
+        for key, t in p["adam_t"].items():
+            w = int(key.split(":")[1])
+            assert t == p["n_applies"][w], (key, t, p["n_applies"])
+        assert torch.isfinite(p["params"]).all()
+    for w in workers:
+        assert w["role"] == "worker" and w["updates"] >= 1
+    assert sum(ps[0]["n_applies"].values()) == ps[0]["global_step"]
+
+
+def test_a3c_gpu_mode_protocol_cpu(tmp_path):
+    res = _run(tmp_path, 3, staleness=1)
+    _check(res, 1, 1, 12)
+
+
+def test_a3c_gpu_mode_two_ps_shards_three_workers_cpu(tmp_path):
+    res = _run(tmp_path, 5, ps_num=2, staleness=0, total=9)
+    _check(res, 2, 0, 9)
+    n = [r["params"].numel() for r in res[:2]]
+    assert all(k > 0 for k in n)
+
+
+@pytest.mark.gpu
+def test_a3c_gpu_workers_on_device(cuda, tmp_path):
+    """Workers run the device engines (env bank + hipGraph-captured segments on cuda:0); the PS holds its slab and
+    Adam moments on the device and applies with the native fused Adam kernel."""
+    res = _run(tmp_path, 3, device="cuda:0", staleness=1, total=30)
+    _check(res, 1, 1, 30)
+
+
+def _pf_proc(rank, port, d):
+    from actor_critic_algs_on_tensorflow_amd.compat import reference as ref
+    cluster = {"ps": [f"localhost:{port}"], "worker": [f"localhost:{port + 1}", f"localhost:{port + 2}"]}
+    job, task = ("ps", 0) if rank == 0 else ("worker", rank - 1)
+    logger = ref.Logger(f"{d}/w{task}.log", quiet=True) if job == "worker" else None
+    out = ref.process_fn(cluster, task, job, "CartPole-v0", logger, f"{d}/ck", 0, random_seed=5, save_every=2,
+                         checkpoint_basename="model-CartPole", max_iters=4)
+    if logger is not None:
+        logger.close()
+    torch.save({"role": out["role"], "gstep": out["global_step"]}, f"{d}/pf{rank}.pt")
+
+
+def test_process_fn_reference_signature(tmp_path):
+    """compat.reference.process_fn(cluster, task_id, job, env_id, logger, save_path, ...) runs the async job."""
+    d = str(tmp_path)
+    mp.spawn(_pf_proc, args=(_free_port(), d), nprocs=3, join=True)
+    ps = torch.load(f"{d}/pf0.pt", weights_only=True)
+    assert ps["role"] == "ps" and ps["gstep"] >= 4
+    assert any(n.startswith("model-CartPole-") for n in os.listdir(f"{d}/ck"))
+    assert os.path.exists(f"{d}/w0.log")
+
+
+def test_cpu_ps_per_worker_adam_step_count():
+    """the CPU PS's Adam bias correction uses the SENDER's own step count (reference workers each own an
+    Adam whose beta powers advance only with their applies): worker B's first apply after two of worker A's uses
+    t = 1, i.e. the TF formula lr * sqrt(1 - b2) / (1 - b1) * m / (sqrt(v) + eps)."""
+    import numpy as np
+    from actor_critic_algs_on_tensorflow_amd.algos.a3c import ParameterServer
+
+    class _Shard:
+        sizes, is_actor = [4], [False]
+        shard_vars, shard_numel = [[0]], [4]
+
+    ps = ParameterServer(_Shard(), 0, torch.zeros(4), [1, 2], critic_lr=0.01)
+    g = torch.tensor([1.0, -2.0, 0.5, 0.0])
+    ps.apply(g, 0.0, src=1)
+    ps.apply(g, 0.0, src=1)
+    m_prev, v_prev = ps.adam.m.clone(), ps.adam.v.clone()
+    p_prev = ps.params.detach().clone()
+    ps.apply(g, 0.0, src=2)
+    b1, b2, eps = ps.adam.b1, ps.adam.b2, ps.adam.eps
+    m = b1 * m_prev + (1 - b1) * g
+    v = b2 * v_prev + (1 - b2) * g * g
+    lr_t = 0.01 * np.sqrt(1 - b2) / (1 - b1)   # t = 1 for worker 2
+    torch.testing.assert_close(ps.params.detach(), p_prev - lr_t * m / (torch.sqrt(v) + eps))
+    assert ps.worker_t == {1: 2, 2: 1} and ps.global_step == 3

@@ -85,15 +85,70 @@ def train(cfg: TrainConfig | str, **overrides) -> TrainResult:
 
 
 class Agent:
-    """A policy ready to act: wraps a model family and its device; ``act`` is batched over observations."""
+    """A policy ready to act: wraps a model family and its device; ``act`` is batched over observations.
 
-    def __init__(self, model, env_id=None, device="cpu", seed=0):
+    On a GPU (``engine="auto"|"native"``) ``act`` runs the hand-written HIP engines the trainers use: the CNN family
+    through :class:`.algos.engine.CNNEngine` (fused trunk + fc + head, bf16 MFMA) and the categorical sampling
+    kernel; the MLP family through :class:`.ops.mlp.MLPEngine` (both towers + sampling in one launch). Sampling keys
+    are ``(call counter << 20) + row``, so the native and the PyTorch paths draw the same actions from the same
+    logits. ``engine="torch"`` (and every CPU agent) runs the PyTorch modules."""
+
+    def __init__(self, model, env_id=None, device="cpu", seed=0, engine="auto"):
         self.model = model.to(device)
         self.model.eval()
         self.env_id = env_id
         self.device = torch.device(device)
         self.seed = seed
         self._ctr = 0
+        self.engine_kind = engine
+        self._eng = None
+
+    def _engine(self):
+        """Lazily builds the native engine over the model's parameters (None on CPU / engine="torch")."""
+        if self._eng is not None or self.engine_kind == "torch" or self.device.type != "cuda":
+            return self._eng
+        from .models.policy import CNNActorCritic, MLPActorCritic
+        from .ops.optim import FlatParams
+        from . import _native
+        _native.require()
+        flat = FlatParams(self.model.param_groups(), self.device)   # re-homes the parameters into one slab
+        if isinstance(self.model, CNNActorCritic):
+            from .algos.engine import CNNEngine
+            shadow = flat.data.to(torch.bfloat16)
+            self._eng = ("cnn", CNNEngine(self.model, flat, shadow), flat)
+        elif isinstance(self.model, MLPActorCritic) and self.model.actor.ac_dim <= 16:
+            from .ops.mlp import MLPEngine
+            self._eng = ("mlp", MLPEngine(self.model, flat), flat)
+        elif self.engine_kind == "native":
+            raise ValueError("no native engine for this model")
+        return self._eng
+
+    @torch.no_grad()
+    def _act_native(self, o, keys_ctr, deterministic):
+        from .ops import distributions as D
+        kind, eng, _ = self._eng
+        N = o.shape[0]
+        if kind == "cnn":
+            b = eng.bufs(N)
+            z = eng.forward(o.to(torch.uint8).contiguous(), b)
+            logits = z[:, :eng.A].contiguous()
+            if deterministic:
+                a = logits.argmax(-1).to(torch.int32)
+                logp, ent = D.categorical_logp_entropy(logits, a)
+                return a, logp, ent
+            keys = torch.arange(N, dtype=torch.int64, device=self.device) + (keys_ctr << 20)
+            return D.categorical_sample(logits, keys, self.seed)
+        if deterministic:
+            return None
+        act = torch.empty((N,) if eng.discrete else (N, eng.A), dtype=torch.int32 if eng.discrete else torch.float32,
+                          device=self.device)
+        logp = torch.empty(N, device=self.device)
+        ent = torch.empty(N, device=self.device)
+        v = torch.empty(N, device=self.device)
+        tg = torch.full((N,), keys_ctr, dtype=torch.int64, device=self.device)
+        ids = torch.arange(N, dtype=torch.int64, device=self.device)
+        eng.policy_step(o.float().contiguous(), act, logp, ent, v, tg, ids, 20, self.seed)
+        return act, logp, ent
 
     @classmethod
     def for_env(cls, env_id, family="auto", variant="basic", frames=1, device="cpu", seed=0):
@@ -124,9 +179,14 @@ class Agent:
             o = o.unsqueeze(0)
         o = o.to(self.device)
         N = o.shape[0]
-        keys = torch.arange(N, dtype=torch.int64, device=self.device) + (self._ctr << 20)
+        ctr = self._ctr
         self._ctr += 1
-        a, logp, ent, _ = self.model.act(o, keys=keys, seed=self.seed, deterministic=deterministic)
+        res = self._act_native(o, ctr, deterministic) if self._engine() is not None else None
+        if res is not None:
+            a, logp, ent = res
+        else:
+            keys = torch.arange(N, dtype=torch.int64, device=self.device) + (ctr << 20)
+            a, logp, ent, _ = self.model.act(o, keys=keys, seed=self.seed, deterministic=deterministic)
         out = (a.cpu().numpy(), logp.cpu().numpy(), ent.cpu().numpy())
         return tuple(x[0] for x in out) if single else out
 

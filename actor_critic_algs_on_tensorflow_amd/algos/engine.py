@@ -106,6 +106,8 @@ class CNNEngine:
         # A2C head in one launch (head_bwd: loss + dz + dh + dWh + dbh + dbfc, no GEMMs) for categorical heads of up
         # to 7 actions and learner batches up to 1024 rows
         self.fused_head = os.environ.get("ACA_FUSED_HEAD", "1") != "0"
+        # A2C learner on ONE stream with grouped GEMM launches instead of a side stream joined by events
+        self.grouped = os.environ.get("ACA_GROUPED", "1") != "0"
         # conv weight gradients as split-K partial planes reduced in plane order by the finaliser (deterministic);
         # 0: split-K fp32 atomics into the slab (nondeterministic summation order)
         self.det_wgrad = implicit and os.environ.get("ACA_DET_WGRAD", "1") != "0"
@@ -282,9 +284,14 @@ class CNNEngine:
         side = self.side
         ev = self._ev
         ws2 = self._side_ws()
+        grouped = self.grouped and (head_done or stage == "trunk") and self.fused_bwd and self.det_wgrad
         if stage == "trunk":
+            if grouped:
+                return self._backward_grouped(b, stage, ws, ws2)
             return self._backward_trunk(b, main, side, ev, ws, ws2)
         self._cur_planes = {}   # weight-gradient plane sets written by THIS backward (reduced by its finaliser)
+        if grouped:
+            return self._backward_grouped(b, stage, ws, ws2)
         head_bias_done = head_bias_done or getattr(b, "bias_done", False)
         if not head_done:
             ev[0].record(main)
@@ -310,6 +317,27 @@ class CNNEngine:
             main.wait_event(ev[5])
             return
         return self._backward_trunk(b, main, side, ev, ws, ws2)
+
+    def _backward_grouped(self, b, stage, ws, ws2):
+        """One stream, no cross-stream edges: the independent products of each stage run as ONE grouped launch
+        (ops.gemm.group) -- {dWfc, dy3}, then the fused dy3 -> dy2 -> dy1 kernel, then {dW3, dW2, dW1} as split-K
+        planes, then the finaliser. Inside a captured graph every event edge between streams costs several
+        microseconds of inter-queue synchronisation; here the critical path is the chain of launches itself."""
+        B = b.B
+        if stage in ("all", "tail"):
+            with G.group():
+                G.gemm(b.y3, 3136, False, b.dh, 512, False, self.gWfc, 512, 0, 3136, 512, B, workspace=ws2)
+                G.gemm(b.dh, 512, True, self.sWfc, 512, True, b.dy3, 3136, 1, B, 3136, 512, mask=b.y3, ldm=3136,
+                       workspace=ws)
+            if stage == "tail":
+                return
+        _native.require().cnn_trunk_bwd(b.dy3, self.sW3, b.y2, self.sW2, b.y1, b.dy2, b.dy1, b.biasp)
+        with G.group():
+            self._wgrad("W3", self.gW3, b.dy3, 64, b.y2, 0, 64, 576, B * 49, ws2, [2, B, 64, 9, 9, 3, 3, 1])
+            self._wgrad("W2", self.gW2, b.dy2, 64, b.y1, 0, 64, 512, B * 81, ws2, [2, B, 32, 20, 20, 4, 4, 2])
+            self._wgrad("W1", self.gW1, b.dy1, 32, b.obs, 0, 32, 256, B * 400, ws, [1, B, 4, 84, 84, 8, 8, 4],
+                        1.0 / 255.0)
+        self.finalize(b)
 
     def _backward_trunk(self, b, main, side, ev, ws, ws2):
         B = b.B

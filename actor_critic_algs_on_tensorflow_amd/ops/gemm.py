@@ -173,6 +173,8 @@ def _run(ops, A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha, bias, 
     if colsum is not None and eff == 1 and out_mode != 3 and workspace is not None:
         R = (M + TILES[tile][0] - 1) // TILES[tile][0]
         if R >= COLSUM_PART_MIN_TILES:
+            if _GROUP_DEPTH:
+                raise ValueError("gemm group: products with column-sum partials cannot be grouped")
             part = workspace.part_buf(R * N)
     ops.gemm(A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, float(alpha), bias, bool(relu), mask, ldm,
              colsum, int(colsum_mod), tile, bk, splits, ws, tk, list(ga or []), float(ga_scale), list(gb or []),
@@ -180,6 +182,39 @@ def _run(ops, A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha, bias, 
     if part is not None:
         ops.colsum_reduce(part, R, N, colsum, int(colsum_mod))
     return eff
+
+
+_GROUP_DEPTH = 0
+GROUP_STATS = {"grouped": 0, "fallback": 0}
+
+
+class group:
+    """Context manager: the :func:`gemm` calls inside (independent products, one stream) run as ONE grouped
+    launch when an instantiation covers their tile configurations (csrc/kernels/gemm_group.hip), else one launch
+    each in issue order. Products in a group must not use the column-sum partial path (its reduce launch would
+    run before the group) -- the learner's grouped products have no column sums."""
+
+    def __enter__(self):
+        global _GROUP_DEPTH
+        assert _GROUP_DEPTH == 0, "gemm groups do not nest"
+        _native.require().gemm_group_begin()
+        _GROUP_DEPTH = 1
+        return self
+
+    def __exit__(self, exc_type, exc, tb):
+        global _GROUP_DEPTH
+        _GROUP_DEPTH = 0
+        ran = _native.require().gemm_group_end() if exc_type is None else _abort_group()
+        GROUP_STATS["grouped" if ran else "fallback"] += 1
+        return False
+
+
+def _abort_group():
+    try:
+        _native.require().gemm_group_end()
+    except Exception:   # pragma: no cover - already failing
+        pass
+    return 0
 
 
 def _row_block(ga):
@@ -235,8 +270,14 @@ def gemm(A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha=1.0, bias=No
         if hit is not None:
             t, k, s = hit[0], hit[1], hit[2]
         elif TUNE and C.is_cuda and not torch.cuda.is_current_stream_capturing():
-            t, k, s = _tune(key, ops, A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha, bias, relu, mask,
-                            ldm, colsum, colsum_mod, workspace, ga, ga_scale, gb, gb_scale, max_planes)
+            if _GROUP_DEPTH:
+                ops.gemm_group_pause(True)   # trials launch directly, not into the open group
+            try:
+                t, k, s = _tune(key, ops, A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha, bias, relu,
+                                mask, ldm, colsum, colsum_mod, workspace, ga, ga_scale, gb, gb_scale, max_planes)
+            finally:
+                if _GROUP_DEPTH:
+                    ops.gemm_group_pause(False)
         else:
             t, k, s = plan(M, N, K, atomic=(out_mode in (2, 3)))
             if out_mode == 3:

@@ -59,6 +59,7 @@ hipError_t aca_returns_scan(const float*, const float*, const uint8_t*, float*, 
                             double*, float*, int, int, int, int, int, float, float, float, hipStream_t);
 hipError_t aca_normalize_mom(const float*, float*, const double*, int, float, hipStream_t);
 int aca_ev_multi_blocks(int);
+hipError_t aca_gemm_group_run(const AcaGemmDesc*, int, hipStream_t, int*);
 hipError_t aca_mb_gather(const uint8_t*, int64_t, const int*, const float*, const float*, const float*, const float*,
                          uint8_t*, int*, float*, float*, float*, float*, int, int, uint32_t, const int64_t*, int, int,
                          hipStream_t);
@@ -829,6 +830,13 @@ AcaConvGather make_gather(const Tensor& src, const std::vector<int64_t>& spec, d
   return g;
 }
 
+struct GemmGroupState {
+  bool active = false, paused = false;
+  std::vector<AcaGemmDesc> descs;
+  hipStream_t stream = nullptr;
+};
+static thread_local GemmGroupState g_gemm_group;
+
 void gemm(Tensor A, int64_t lda, bool a_k, Tensor B, int64_t ldb, bool b_k, Tensor C, int64_t ldc, int64_t out_mode,
           int64_t M, int64_t N, int64_t K, double alpha, c10::optional<Tensor> bias, bool relu,
           c10::optional<Tensor> mask, int64_t ldm, c10::optional<Tensor> colsum, int64_t colsum_mod, int64_t tile,
@@ -937,7 +945,45 @@ void gemm(Tensor A, int64_t lda, bool a_k, Tensor B, int64_t ldb, bool b_k, Tens
     TORCH_CHECK(colsum_part->numel() >= ((M + bm - 1) / bm) * N, "gemm: colsum_part needs [M tiles, N]");
     d.colsum_part = ptr<float>(*colsum_part);
   }
+  if (g_gemm_group.active) {   // grouped launch being collected: run at gemm_group_end
+    TORCH_CHECK(g_gemm_group.descs.empty() || g_gemm_group.stream == cur_stream(C),
+                "gemm group: every product must be issued on the same stream");
+    g_gemm_group.stream = cur_stream(C);
+    g_gemm_group.descs.push_back(d);
+    return;
+  }
   check(aca_gemm_run(&d, cur_stream(C)), "gemm");
+}
+
+// Grouped GEMM launches: between gemm_group_begin() and gemm_group_end() every gemm() call is collected instead of
+// launched; the end runs them as ONE grouped kernel when an instantiation covers their tile configurations
+// (csrc/kernels/gemm_group.hip), else one launch each, in issue order. Returns 1 if the grouped kernel ran.
+void gemm_group_begin() {
+  TORCH_CHECK(!g_gemm_group.active, "gemm group already open");
+  g_gemm_group.active = true;
+  g_gemm_group.descs.clear();
+}
+
+int64_t gemm_group_end() {
+  TORCH_CHECK(g_gemm_group.active, "gemm group not open");
+  g_gemm_group.active = false;
+  if (g_gemm_group.descs.empty()) return 0;
+  int grouped = 0;
+  const hipError_t err = aca_gemm_group_run(g_gemm_group.descs.data(), (int)g_gemm_group.descs.size(),
+                                            g_gemm_group.stream, &grouped);
+  g_gemm_group.descs.clear();
+  check(err, "gemm_group");
+  return grouped;
+}
+
+void gemm_group_pause(bool paused) {   // autotuning inside an open group launches its trials directly
+  if (paused && g_gemm_group.active) {
+    g_gemm_group.active = false;
+    g_gemm_group.paused = true;
+  } else if (!paused && g_gemm_group.paused) {
+    g_gemm_group.active = true;
+    g_gemm_group.paused = false;
+  }
 }
 
 int64_t gemm_effective_splits(int64_t K, int64_t bk, int64_t splits) {
@@ -1213,6 +1259,9 @@ TORCH_LIBRARY(acamd, m) {
   m.def("returns_scan(Tensor r, Tensor v, Tensor d, Tensor ret, Tensor adv, int mode, float gamma, float lam, int L, "
         "bool norm, float eps, Tensor part, Tensor ticket, Tensor mom, Tensor? ev_out=None, Tensor? gz=None) -> ()");
   m.def("normalize_mom(Tensor a, Tensor out, Tensor mom, float eps) -> ()");
+  m.def("gemm_group_begin() -> ()", &gemm_group_begin);
+  m.def("gemm_group_end() -> int", &gemm_group_end);
+  m.def("gemm_group_pause(bool paused) -> ()", &gemm_group_pause);
   m.def("mb_gather(Tensor obs, Tensor act, Tensor logp, Tensor adv, Tensor ret, Tensor v, Tensor o_obs, "
         "Tensor o_act, Tensor o_logp, Tensor o_adv, Tensor o_ret, Tensor o_v, int seed, Tensor uc, int ep, "
         "int off) -> ()");

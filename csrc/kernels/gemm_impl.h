@@ -236,19 +236,30 @@ struct GemmParams {
   int splits;
 };
 
+// LDS footprint (bf16 elements) of one tile configuration: double-buffered A and B k-step tiles
+template <int BM, int BN, int BK, bool A_K, bool B_K>
+struct GemmSmem {
+  static constexpr int A_ELEMS = A_K ? BM * (BK + GEMM_PAD) : BK * (BM + GEMM_PAD);
+  static constexpr int B_ELEMS = B_K ? BN * (BK + GEMM_PAD) : BK * (BN + GEMM_PAD);
+  static constexpr int ELEMS = 2 * (A_ELEMS + B_ELEMS);
+};
+
+// One output tile x one K split of a product: the body shared by the one-product kernel (gemm_kernel, tile =
+// blockIdx.x, z = blockIdx.z) and the grouped kernel (gemm_group_kernel: several independent products of up to two
+// tile configurations in ONE launch, so a backward pass issues its independent products without cross-stream
+// dependencies). `smem` is the caller's LDS array (>= GemmSmem::ELEMS), `ntiles` the product's tile count.
 template <int BM, int BN, int BK, bool A_K, bool B_K, int AG, int BG, bool VEC>
-__global__ void __launch_bounds__(256) gemm_kernel(GemmParams P) {
+__device__ __forceinline__ void gemm_block(const GemmParams& P, const int tile, const int z, const int ntiles,
+                                           u16* const smem, int& sh_flag) {
   const AcaGemmDesc& g = P.d;
-  constexpr int A_ELEMS = A_K ? BM * (BK + GEMM_PAD) : BK * (BM + GEMM_PAD);
-  constexpr int B_ELEMS = B_K ? BN * (BK + GEMM_PAD) : BK * (BN + GEMM_PAD);
+  constexpr int A_ELEMS = GemmSmem<BM, BN, BK, A_K, B_K>::A_ELEMS;
+  constexpr int B_ELEMS = GemmSmem<BM, BN, BK, A_K, B_K>::B_ELEMS;
   constexpr int TM = BM / 32, TN = BN / 32;   // 16x16 MFMA tiles per wave (2 x 2 waves)
   constexpr int A_CHUNKS = BM * BK / 8 / 256;  // 16-byte chunks per thread per k-step
   constexpr int B_CHUNKS = BN * BK / 8 / 256;
   static_assert(A_CHUNKS >= 1 && B_CHUNKS >= 1, "tile too small");
   static_assert(!AG || A_K, "A gather needs a k-contiguous A");
   static_assert(!BG || !B_K, "B gather needs an n-contiguous B");
-  __shared__ __attribute__((aligned(16))) u16 smem[2 * (A_ELEMS + B_ELEMS)];
-  __shared__ int sh_flag;
   u16* const As0 = smem;
   u16* const Bs0 = smem + 2 * A_ELEMS;
   const u16* Ag = reinterpret_cast<const u16*>(g.A);
@@ -257,15 +268,13 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmParams P) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int tiles_n = (g.N + BN - 1) / BN;
-  const int tile = blockIdx.x;
   const int m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
-  const int z = blockIdx.z;
   const int k_tiles_total = (g.K + BK - 1) / BK;
   const int kt0 = z * P.k_tiles_per_split;
   const int kt1 = min(kt0 + P.k_tiles_per_split, k_tiles_total);
 
   unsigned long long* const st =
-      g.stamps ? g.stamps + ((size_t)blockIdx.z * gridDim.x + blockIdx.x) * 4 : nullptr;
+      g.stamps ? g.stamps + ((size_t)z * ntiles + tile) * 4 : nullptr;
   if (st && tid == 0) st[0] = __builtin_amdgcn_s_memrealtime();
   floatx4 acc[TM][TN];
 #pragma unroll
@@ -539,6 +548,62 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmParams P) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (tid == 0) st[3] = __builtin_amdgcn_s_memrealtime();
   }
+}
+
+template <int BM, int BN, int BK, bool A_K, bool B_K, int AG, int BG, bool VEC>
+__global__ void __launch_bounds__(256) gemm_kernel(GemmParams P) {
+  __shared__ __attribute__((aligned(16))) u16 smem[GemmSmem<BM, BN, BK, A_K, B_K>::ELEMS];
+  __shared__ int sh_flag;
+  gemm_block<BM, BN, BK, A_K, B_K, AG, BG, VEC>(P, blockIdx.x, blockIdx.z, gridDim.x, smem, sh_flag);
+}
+
+// ---------------------------------------------------------------------------------------------- grouped launch
+// Up to GEMM_GROUP_MAX independent products in one launch; product k uses tile configuration CA (cfg[k] == 0) or
+// CB (cfg[k] == 1). Its workgroups are blocks [start[k], start[k + 1]) of the flat grid: tile = local % tiles[k],
+// split = local / tiles[k].
+constexpr int GEMM_GROUP_MAX = 3;
+struct GemmGroupArgs {
+  GemmParams p[GEMM_GROUP_MAX];
+  int tiles[GEMM_GROUP_MAX];
+  int start[GEMM_GROUP_MAX + 1];
+  int cfg[GEMM_GROUP_MAX];
+  int n;
+};
+
+template <int BM, int BN, int BK, bool A_K, bool B_K, int AG, int BG, bool VEC>
+struct GemmCfg {
+  static constexpr int bm = BM, bn = BN, smem = GemmSmem<BM, BN, BK, A_K, B_K>::ELEMS;
+  static __device__ __forceinline__ void run(const GemmParams& P, int tile, int z, int ntiles, u16* sm, int& f) {
+    gemm_block<BM, BN, BK, A_K, B_K, AG, BG, VEC>(P, tile, z, ntiles, sm, f);
+  }
+};
+
+template <class CA, class CB>
+__global__ void __launch_bounds__(256) gemm_group_kernel(GemmGroupArgs G) {
+  constexpr int SM = CA::smem > CB::smem ? CA::smem : CB::smem;
+  __shared__ __attribute__((aligned(16))) u16 smem[SM];
+  __shared__ int sh_flag;
+  const int b = blockIdx.x;
+  int k = 0;
+  if (G.n > 1 && b >= G.start[1]) k = 1;
+  if (G.n > 2 && b >= G.start[2]) k = 2;
+  const int local = b - G.start[k], tiles = G.tiles[k];
+  if (G.cfg[k] == 0) CA::run(G.p[k], local % tiles, local / tiles, tiles, smem, sh_flag);
+  else CB::run(G.p[k], local % tiles, local / tiles, tiles, smem, sh_flag);
+}
+
+template <class CA, class CB>
+hipError_t gemm_group_launch(GemmGroupArgs& G, hipStream_t s) {
+  int total = 0;
+  for (int k = 0; k < G.n; ++k) {
+    const int bm = G.cfg[k] == 0 ? CA::bm : CB::bm, bn = G.cfg[k] == 0 ? CA::bn : CB::bn;
+    G.tiles[k] = ((G.p[k].d.M + bm - 1) / bm) * ((G.p[k].d.N + bn - 1) / bn);
+    G.start[k] = total;
+    total += G.tiles[k] * G.p[k].splits;
+  }
+  G.start[G.n] = total;
+  gemm_group_kernel<CA, CB><<<total, 256, 0, s>>>(G);
+  return hipGetLastError();
 }
 
 template <int BM, int BN, int BK, bool A_K, bool B_K, int AG, int BG, bool VEC>

@@ -234,3 +234,57 @@ def test_agent_act_runs_native_engine(cuda, env_id):
         np.testing.assert_allclose(a1, a2, rtol=1e-4, atol=1e-4)
         np.testing.assert_allclose(lp1, lp2, rtol=1e-3, atol=1e-3)
         np.testing.assert_allclose(e1, e2, rtol=1e-3, atol=1e-3)
+
+
+def test_grouped_gemm_launch_equals_separate_launches(cuda):
+    """{dWfc, dy3} and {dW3, dW2, dW1} as ONE grouped launch each == the same products launched one by one, bit for
+    bit (same tile plans), and the grouped kernel really ran (not the per-product fallback)."""
+    from actor_critic_algs_on_tensorflow_amd.ops import gemm as G
+    B = 160
+    g = torch.Generator(device="cpu").manual_seed(9)
+
+    def bf(*shape):
+        return (torch.randn(*shape, generator=g) * 0.1).to(torch.bfloat16).to(cuda)
+
+    y3, dh, Wfc = bf(B * 49, 64), bf(B, 512), bf(3136, 512)
+    dy3m = bf(B, 3136)
+    dy2, dy1, y2, y1 = bf(B * 81, 64), bf(B * 400, 32), bf(B * 81, 64), bf(B * 400, 32)
+    obs = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, generator=g).to(cuda)
+    dy3 = bf(B * 49, 64)
+
+    def run(grouped):
+        outs = [torch.zeros(3136 * 512, device=cuda), torch.zeros(B * 3136, dtype=torch.bfloat16, device=cuda),
+                torch.zeros(32 * 64 * 576, device=cuda), torch.zeros(32 * 64 * 512, device=cuda),
+                torch.zeros(32 * 32 * 256, device=cuda)]
+        ws1, ws2 = G.GemmWorkspace(cuda), G.GemmWorkspace(cuda)
+        before = dict(G.GROUP_STATS)
+
+        def first():
+            G.gemm(y3, 3136, False, dh, 512, False, outs[0], 512, 0, 3136, 512, B, workspace=ws2, tile=4, bk=64,
+                   splits=1)
+            G.gemm(dh, 512, True, Wfc, 512, True, outs[1], 3136, 1, B, 3136, 512, mask=dy3m, ldm=3136, workspace=ws1,
+                   tile=4, bk=64, splits=1)
+
+        def second():
+            G.gemm(dy3, 64, False, y2, 0, False, outs[2], 576, 3, 64, 576, B * 49, gb=[2, B, 64, 9, 9, 3, 3, 1],
+                   tile=2, bk=64, splits=32, max_planes=32)
+            G.gemm(dy2, 64, False, y1, 0, False, outs[3], 512, 3, 64, 512, B * 81, gb=[2, B, 32, 20, 20, 4, 4, 2],
+                   tile=2, bk=64, splits=32, max_planes=32)
+            G.gemm(dy1, 32, False, obs, 0, False, outs[4], 256, 3, 32, 256, B * 400, gb=[1, B, 4, 84, 84, 8, 8, 4],
+                   gb_scale=1.0 / 255.0, tile=4, bk=256, splits=32, max_planes=32)
+
+        for fn in (first, second):
+            if grouped:
+                with G.group():
+                    fn()
+            else:
+                fn()
+        torch.cuda.synchronize()
+        ran = G.GROUP_STATS["grouped"] - before["grouped"]
+        return outs, ran
+
+    sep, _ = run(False)
+    grp, ran = run(True)
+    assert ran == 2
+    for a, b in zip(sep, grp):
+        assert torch.equal(a, b)

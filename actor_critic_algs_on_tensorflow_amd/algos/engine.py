@@ -111,7 +111,7 @@ class CNNEngine:
         # conv weight gradients as split-K partial planes reduced in plane order by the finaliser (deterministic);
         # 0: split-K fp32 atomics into the slab (nondeterministic summation order)
         self.det_wgrad = implicit and os.environ.get("ACA_DET_WGRAD", "1") != "0"
-        self.wgrad_planes = int(os.environ.get("ACA_WGRAD_PLANES", "32"))
+        self.wgrad_planes = int(os.environ.get("ACA_WGRAD_PLANES", "64"))
         self._planes = {}
         self._wsplits = {}
         self._cur_planes = {}
@@ -325,18 +325,18 @@ class CNNEngine:
         microseconds of inter-queue synchronisation; here the critical path is the chain of launches itself."""
         B = b.B
         if stage in ("all", "tail"):
-            with G.group():
-                G.gemm(b.y3, 3136, False, b.dh, 512, False, self.gWfc, 512, 0, 3136, 512, B, workspace=ws2)
+            with G.group():   # workgroups start in product order: the critical-path product first
                 G.gemm(b.dh, 512, True, self.sWfc, 512, True, b.dy3, 3136, 1, B, 3136, 512, mask=b.y3, ldm=3136,
                        workspace=ws)
+                G.gemm(b.y3, 3136, False, b.dh, 512, False, self.gWfc, 512, 0, 3136, 512, B, workspace=ws2)
             if stage == "tail":
                 return
         _native.require().cnn_trunk_bwd(b.dy3, self.sW3, b.y2, self.sW2, b.y1, b.dy2, b.dy1, b.biasp)
-        with G.group():
-            self._wgrad("W3", self.gW3, b.dy3, 64, b.y2, 0, 64, 576, B * 49, ws2, [2, B, 64, 9, 9, 3, 3, 1])
-            self._wgrad("W2", self.gW2, b.dy2, 64, b.y1, 0, 64, 512, B * 81, ws2, [2, B, 32, 20, 20, 4, 4, 2])
+        with G.group():   # the longest product (conv1, K = 400 B) first
             self._wgrad("W1", self.gW1, b.dy1, 32, b.obs, 0, 32, 256, B * 400, ws, [1, B, 4, 84, 84, 8, 8, 4],
                         1.0 / 255.0)
+            self._wgrad("W2", self.gW2, b.dy2, 64, b.y1, 0, 64, 512, B * 81, ws2, [2, B, 32, 20, 20, 4, 4, 2])
+            self._wgrad("W3", self.gW3, b.dy3, 64, b.y2, 0, 64, 576, B * 49, ws2, [2, B, 64, 9, 9, 3, 3, 1])
         self.finalize(b)
 
     def _backward_trunk(self, b, main, side, ev, ws, ws2):

@@ -26,9 +26,13 @@ struct KCfg : GemmCfg<BM, BN, BK, A_K, B_K, AG, BG, VEC> {
 using FcW32 = KCfg<32, 32, 64, false, false, 0, 0, true>;
 using FcW64x32 = KCfg<64, 32, 64, false, false, 0, 0, true>;
 using FcW64 = KCfg<64, 64, 64, false, false, 0, 0, true>;
+using FcW32k128 = KCfg<32, 32, 128, false, false, 0, 0, true>;
 using FcD32 = KCfg<32, 32, 64, true, true, 0, 0, true>;
 using FcD64 = KCfg<64, 64, 64, true, true, 0, 0, true>;
 using FcD32x64 = KCfg<32, 64, 64, true, true, 0, 0, true>;
+using FcD32x64k128 = KCfg<32, 64, 128, true, true, 0, 0, true>;
+using FcD32k128 = KCfg<32, 32, 128, true, true, 0, 0, true>;
+using FcD64x32 = KCfg<64, 32, 64, true, true, 0, 0, true>;
 // conv weight gradients: B gathered from the bf16 NHWC activations (conv2 / conv3) or the uint8 frames (conv1)
 using Wg64x32 = KCfg<64, 32, 64, false, false, 0, 2, true>;
 using Wg32x64k128 = KCfg<32, 64, 128, false, false, 0, 2, true>;
@@ -45,10 +49,12 @@ struct GroupEntry {
 template <class A, class B>
 constexpr GroupEntry entry() { return GroupEntry{A::key, B::key, &gemm_group_launch<A, B>}; }
 
+#define FC_ROW(W)                                                                                           \
+  entry<W, FcD32>(), entry<W, FcD64>(), entry<W, FcD32x64>(), entry<W, FcD32x64k128>(), entry<W, FcD32k128>(), \
+      entry<W, FcD64x32>()
+
 static const GroupEntry kGroups[] = {
-    entry<FcW32, FcD32>(),     entry<FcW32, FcD64>(),       entry<FcW32, FcD32x64>(),
-    entry<FcW64x32, FcD32>(),  entry<FcW64x32, FcD64>(),    entry<FcW64x32, FcD32x64>(),
-    entry<FcW64, FcD32>(),     entry<FcW64, FcD64>(),       entry<FcW64, FcD32x64>(),
+    FC_ROW(FcW32), FC_ROW(FcW64x32), FC_ROW(FcW64), FC_ROW(FcW32k128),
     entry<Wg64x32, Wu32k256>(), entry<Wg64x32, Wu32k128>(), entry<Wg32x64k128, Wu32k256>(),
     entry<Wg32x64k128, Wu32k128>(), entry<Wg64, Wu32k256>(), entry<Wg64, Wu32k128>(),
     entry<Wg64x32k128, Wu32k256>(), entry<Wg64x32k128, Wu32k128>(),

@@ -96,9 +96,11 @@ class CNNEngine:
         self.trunk_shift = os.environ.get("ACA_TRUNK_SHIFT", "1") != "0"
         # 1: seven row workgroups per env (224 CUs at 32 envs); 0: one workgroup per env. Row splitting buys
         # parallelism for rollout-sized batches; large learner batches already fill the chip with one workgroup per
-        # env, and the split's recomputed receptive fields only cost there (ACA_TRUNK_MODE_LARGE, B > 256)
+        # env, and the split's recomputed receptive fields only cost there (ACA_TRUNK_MODE_LARGE above
+        # ACA_TRUNK_ROWS_MAX_B envs: 7 B row workgroups stop fitting the chip in one wave)
         self.trunk_mode = int(os.environ.get("ACA_TRUNK_MODE", "1"))
         self.trunk_mode_large = int(os.environ.get("ACA_TRUNK_MODE_LARGE", "0"))
+        self.trunk_rows_max_b = int(os.environ.get("ACA_TRUNK_ROWS_MAX_B", "64"))
         # learner data-gradient chain dy3 -> dy2 -> dy1 as ONE per-sample kernel (cnn_trunk_bwd; bias gradients as
         # per-sample partial rows reduced by the gradient finaliser) instead of two transposed-conv GEMMs
         self.fused_bwd = implicit and os.environ.get("ACA_FUSED_BWD", "1") != "0"
@@ -191,7 +193,7 @@ class CNNEngine:
             if not self.trunk_shift:
                 shift_out = None
             G.cnn_trunk_fwd(obs, self.sW1, self.b1, self.sW2, self.b2, self.sW3, self.b3, b.y1, b.y2, b.y3,
-                            shift_out=shift_out, mode=self.trunk_mode if B <= 256 else self.trunk_mode_large)
+                            shift_out=shift_out, mode=self.trunk_mode if B <= self.trunk_rows_max_b else self.trunk_mode_large)
             shifted = shift_out is not None
         elif self.implicit:
             G.gemm(obs, 0, True, self.sW1, 256, True, b.y1, 32, 1, B * 400, 32, 256, bias=self.b1, relu=True,

@@ -166,23 +166,21 @@ __device__ __forceinline__ void opt_body(const OptSeg& S, float b1, float b2, fl
       if (S.ntrans) write_trans(S, i, pi);
     }
   }
-  if (ADAM && S.ticket) {   // small grids: the last block publishes t (large grids: step_inc_kernel after the launch)
-    if (last_block_arrival(S.ticket, vgrid, flag)) {
-      if (threadIdx.x == 0) *S.t = t;
+  if (ADAM) {
+    // The last workgroup to finish publishes t + 1. Only a COUNT is needed (no data hand-off), so the ticket is a
+    // relaxed atomic with no release fence: a fenced last-arriver ticket (last_block_arrival) costs every workgroup
+    // an agent-scope release -- an L2 write-back on this multi-XCD part -- which was 60 us of a 70 us step over a
+    // 1.7M-parameter slab. The barrier orders this workgroup's reads of *S.t (every wave, at its start) before its
+    // ticket, so the final write cannot overtake a reader.
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned int prev = __hip_atomic_fetch_add(S.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (prev == (unsigned int)vgrid - 1u) {
+        *S.t = t;
+        __hip_atomic_store(S.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   }
-}
-
-// Adam step counters of large segments, advanced by a one-wave launch after the update: the in-kernel last-arriver
-// ticket costs every workgroup an agent-scope release (an L2 write-back on this multi-XCD part) and a same-address
-// atomic -- for a 1.7M-parameter slab (1649 workgroups) that is 60 us of a 70 us optimiser step.
-constexpr int OPT_TICKET_MAX_BLOCKS = 32;
-struct StepPtrs {
-  float* t[4];
-  int n;
-};
-__global__ void step_inc_kernel(StepPtrs P) {
-  if (threadIdx.x < P.n) *P.t[threadIdx.x] += 1.0f;
 }
 
 template <bool ADAM>
@@ -224,7 +222,7 @@ constexpr int FIN_WORDS = 8;
 __global__ void __launch_bounds__(OPT_THREADS) grad_finalize_kernel(const int64_t* __restrict__ jobs, int njobs,
                                                                     float* __restrict__ partial) {
   __shared__ float sh[16];
-  __shared__ float red[OPT_THREADS];
+  __shared__ float red[16 * 64];
   const int64_t* w = jobs + (int64_t)blockIdx.x * FIN_WORDS;
   float* dst = reinterpret_cast<float*>(w[0]);
   const float* src = reinterpret_cast<const float*>(w[1]);
@@ -249,6 +247,41 @@ __global__ void __launch_bounds__(OPT_THREADS) grad_finalize_kernel(const int64_
       for (int i = 4 * n4 + tid; i < n; i += OPT_THREADS) s += dst[i] * dst[i];
     } else {
       for (int i = tid; i < n; i += OPT_THREADS) s += dst[i] * dst[i];
+    }
+  } else if (n <= 64 && vec && (n & 3) == 0) {
+    // few elements, many planes (per-sample bias rows, up to one per learner sample): 16 float4 columns x 16 plane
+    // groups, 16 16-byte loads in flight per thread (4x the bytes in flight of the scalar form -- this reduction is
+    // latency-bound: one workgroup walks B planes), groups combined in LDS in group order
+    const int c4 = tid & 15, pg = tid >> 4, n4 = n >> 2;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c4 < n4) {
+      for (int z0 = pg; z0 < S; z0 += 256) {
+        float4 v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const int z = z0 + 16 * u;
+          v[u] = *reinterpret_cast<const float4*>(src + (int64_t)(z < S ? z : pg) * stride + 4 * c4);
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+          if (z0 + 16 * u < S) { acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w; }
+      }
+    }
+    float* red4 = red;   // [16 groups][64 elements]
+    __syncthreads();
+    if (c4 < n4) {
+      red4[pg * 64 + 4 * c4] = acc.x;
+      red4[pg * 64 + 4 * c4 + 1] = acc.y;
+      red4[pg * 64 + 4 * c4 + 2] = acc.z;
+      red4[pg * 64 + 4 * c4 + 3] = acc.w;
+    }
+    __syncthreads();
+    if (tid < n) {
+      float v = 0.f;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) v += red4[g * 64 + tid];
+      dst[tid] = v;
+      s = v * v;
     }
   } else if (n <= 64) {
     // few elements, many planes (per-sample bias rows): 64 elements x 4 plane groups, 16 loads in flight per
@@ -378,13 +411,8 @@ extern "C" hipError_t aca_adam_step(float* p, float* g, float* m, float* v, size
   if (!opt_aligned(p, g, m, v, shadow)) return hipErrorInvalidValue;
   OptSeg S{p, g, m, v, n, lr, t, gnorm_parts, gnorm_out, shadow, clip, max_norm, gmul, norm_mul, ticket, opt_grid(n),
            0, {}};
-  const bool big = S.nblocks > OPT_TICKET_MAX_BLOCKS;
-  if (big) S.ticket = nullptr;
+  if (!ticket || !t) return hipErrorInvalidValue;
   opt_kernel<true><<<S.nblocks, OPT_THREADS, 0, stream>>>(S, b1, b2, eps, zero_grad);
-  if (big) {
-    StepPtrs P{{t, nullptr, nullptr, nullptr}, 1};
-    step_inc_kernel<<<1, 64, 0, stream>>>(P);
-  }
   return hipGetLastError();
 }
 
@@ -441,16 +469,8 @@ extern "C" hipError_t aca_opt_multi(const int64_t* words, const float* fvals, co
         S.ntrans = e + 1;
       }
   }
-  StepPtrs P{{nullptr, nullptr, nullptr, nullptr}, 0};
-  if (adam)
-    for (int k = 0; k < nseg; ++k)
-      if (M.seg[k].nblocks > OPT_TICKET_MAX_BLOCKS) {
-        P.t[P.n++] = M.seg[k].t;
-        M.seg[k].ticket = nullptr;
-      }
   if (adam) opt_multi_kernel<true><<<total, OPT_THREADS, 0, stream>>>(M, b1, b2, eps, zero_grad);
   else opt_multi_kernel<false><<<total, OPT_THREADS, 0, stream>>>(M, 0.f, b2, eps, zero_grad);
-  if (P.n) step_inc_kernel<<<1, 64, 0, stream>>>(P);
   return hipGetLastError();
 }
 

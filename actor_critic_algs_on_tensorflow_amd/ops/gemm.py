@@ -16,9 +16,12 @@ import torch
 from .. import _native
 
 # tile id -> (BM, BN) ; must match aca_gemm_tile_dims
-TILES = {0: (64, 64), 1: (32, 64), 2: (64, 32), 3: (128, 64), 4: (32, 32)}
-# supported k-step depths per tile (aca_gemm_supported): deeper k-steps for the small tiles of latency-bound products
-BKS = {0: (64, 128), 1: (64, 128), 2: (64, 128), 3: (64,), 4: (64, 128, 256)}
+TILES = {0: (64, 64), 1: (32, 64), 2: (64, 32), 3: (128, 64), 4: (32, 32), 5: (64, 256), 6: (32, 256),
+         7: (128, 128)}
+# supported k-step depths per tile (aca_gemm_supported): deeper k-steps for the small tiles of latency-bound products;
+# the wide tiles (5, 6: skinny-M weight gradients over huge K, the operand that every N tile re-reads is read 4-8x
+# less; 7: large-batch products) only with 64-deep k-steps (LDS)
+BKS = {0: (64, 128), 1: (64, 128), 2: (64, 128), 3: (64,), 4: (64, 128, 256), 5: (64,), 6: (64,), 7: (64,)}
 NUM_CUS = 256
 
 

@@ -14,13 +14,16 @@ extern "C" int aca_gemm_tile_dims(int tile, int* bm, int* bn) {
     case 2: *bm = 64; *bn = 32; break;
     case 3: *bm = 128; *bn = 64; break;
     case 4: *bm = 32; *bn = 32; break;
+    case 5: *bm = 64; *bn = 256; break;
+    case 6: *bm = 32; *bn = 256; break;
+    case 7: *bm = 128; *bn = 128; break;
     default: *bm = 64; *bn = 64; break;
   }
   return 0;
 }
 
 extern "C" int aca_gemm_supported(int tile, int bk) {
-  if (bk == 64) return tile >= 0 && tile <= 4;
+  if (bk == 64) return tile >= 0 && tile <= 7;
   if (bk == 128) return tile == 0 || tile == 1 || tile == 2 || tile == 4;
   if (bk == 256) return tile == 4;
   return 0;

@@ -625,6 +625,9 @@ hipError_t gemm_dispatch_tiles(const GemmParams& P, hipStream_t s) {
       case 2: return gemm_launch<64, 32, 64, A_K, B_K, AG, BG, VEC>(P, s);
       case 3: return gemm_launch<128, 64, 64, A_K, B_K, AG, BG, VEC>(P, s);
       case 4: return gemm_launch<32, 32, 64, A_K, B_K, AG, BG, VEC>(P, s);
+      case 5: return gemm_launch<64, 256, 64, A_K, B_K, AG, BG, VEC>(P, s);
+      case 6: return gemm_launch<32, 256, 64, A_K, B_K, AG, BG, VEC>(P, s);
+      case 7: return gemm_launch<128, 128, 64, A_K, B_K, AG, BG, VEC>(P, s);
     }
   } else if (bk == 128) {
     switch (t) {

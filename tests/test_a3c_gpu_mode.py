@@ -27,7 +27,7 @@ def _cfg(device, total, **kw):
     return preset("a3c", **base)
 
 
-def _proc(rank, world, port, out, device, total, ps_num, staleness, kw):
+def _proc(rank, world, port, out, device, total, ps_num, staleness, kw, report=0):
     import torch.distributed as dist
     from actor_critic_algs_on_tensorflow_amd.algos import a3c_gpu
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -36,16 +36,16 @@ def _proc(rank, world, port, out, device, total, ps_num, staleness, kw):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         res = a3c_gpu.run(_cfg(device, total, **kw), ps_num=ps_num, data_backend="gloo", max_staleness=staleness,
-                          device=device)
+                          device=device, report_every=report)
         torch.save(res, os.path.join(out, f"r{rank}.pt"))
         dist.barrier()
     finally:
         dist.destroy_process_group()
 
 
-def _run(tmp_path, world, device="cpu", total=12, ps_num=1, staleness=1, **kw):
-    mp.spawn(_proc, args=(world, _free_port(), str(tmp_path), device, total, ps_num, staleness, kw), nprocs=world,
-             join=True)
+def _run(tmp_path, world, device="cpu", total=12, ps_num=1, staleness=1, report=0, **kw):
+    mp.spawn(_proc, args=(world, _free_port(), str(tmp_path), device, total, ps_num, staleness, kw, report),
+             nprocs=world, join=True)
     return [torch.load(tmp_path / f"r{r}.pt", weights_only=False) for r in range(world)]
 
 
@@ -89,6 +89,20 @@ def test_a3c_gpu_workers_on_device(cuda, tmp_path):
     Adam moments on the device and applies with the native fused Adam kernel."""
     res = _run(tmp_path, 3, device="cuda:0", staleness=1, total=30)
     _check(res, 1, 1, 30)
+
+
+@pytest.mark.gpu
+def test_a3c_gpu_workers_learn_pendulum(cuda, tmp_path):
+    """Pendulum-v0 with the reference A3C preset on 2 device workers (32 envs x 16 steps per worker update):
+    measured -925 -> -253 (seed 12321) and -1337 -> -823 (seed 7) mean episode return over 3000 global steps
+    (profiles/r2_learning_curves.txt)."""
+    res = _run(tmp_path, 3, device="cuda:0", staleness=2, total=3000, report=500, num_envs=32, n_steps=16,
+               seed=12321)
+    _check(res, 1, 2, 3000)
+    for w in res[1:]:
+        rets = [r[2] for r in w["returns"]]
+        # random play scores about -1200 +- 300; the curves measured over seeds reach -250 .. -820 at 3000 steps
+        assert len(rets) >= 2 and rets[-1] > -950 and rets[-1] > rets[0] + 300, rets
 
 
 def _pf_proc(rank, port, d):

@@ -16,8 +16,12 @@ def _bf(x):
 
 
 # ------------------------------------------------------------------------------------------------------ GEMM
-TILE_BK = [(t, bk) for t in range(5) for bk in (64, 128, 256)
-           if bk in {0: (64, 128), 1: (64, 128), 2: (64, 128), 3: (64,), 4: (64, 128, 256)}[t]]
+def _tile_bk():
+    from actor_critic_algs_on_tensorflow_amd.ops.gemm import BKS   # every supported (tile, k-step) pair
+    return [(t, bk) for t in sorted(BKS) for bk in BKS[t]]
+
+
+TILE_BK = _tile_bk()
 
 
 @pytest.mark.parametrize("a_k", [True, False])

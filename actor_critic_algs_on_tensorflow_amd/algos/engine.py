@@ -94,11 +94,12 @@ class CNNEngine:
         self.fused_trunk_max_b = 4096 if fused_trunk_max_b is None else fused_trunk_max_b
         # rollout frame-stack shift inside the fused trunk (else the env kernel shifts); A/B switch for profiling
         self.trunk_shift = os.environ.get("ACA_TRUNK_SHIFT", "1") != "0"
-        # 1: seven row workgroups per env (224 CUs at 32 envs); 0: one workgroup per env. Row splitting buys
+        # 1 / 2: seven row workgroups per env (224 CUs at 32 envs; 2 issues the conv2/conv3 weight loads after conv1,
+        # leaving conv1 the registers to pipeline its LDS reads); 0: one workgroup per env. Row splitting buys
         # parallelism for rollout-sized batches; large learner batches already fill the chip with one workgroup per
         # env, and the split's recomputed receptive fields only cost there (ACA_TRUNK_MODE_LARGE above
         # ACA_TRUNK_ROWS_MAX_B envs: 7 B row workgroups stop fitting the chip in one wave)
-        self.trunk_mode = int(os.environ.get("ACA_TRUNK_MODE", "1"))
+        self.trunk_mode = int(os.environ.get("ACA_TRUNK_MODE", "2"))
         self.trunk_mode_large = int(os.environ.get("ACA_TRUNK_MODE_LARGE", "0"))
         self.trunk_rows_max_b = int(os.environ.get("ACA_TRUNK_ROWS_MAX_B", "64"))
         # learner data-gradient chain dy3 -> dy2 -> dy1 as ONE per-sample kernel (cnn_trunk_bwd; bias gradients as

@@ -100,9 +100,10 @@ __device__ __forceinline__ PongOut pong_advance(const PongIO& io, int e, float d
   return r;
 }
 
-// Writes the chosen outcome back (one thread).
-__device__ __forceinline__ void pong_commit(const PongIO& io, int e, const PongOut& r) {
-  io.tglob[e] = io.tglob[e] + 1;
+// Writes the chosen outcome back (one thread). tg_old: the env's global step counter, when the caller already holds
+// it (saves a dependent load round trip at the end of the fused step).
+__device__ __forceinline__ void pong_commit(const PongIO& io, int e, const PongOut& r, int64_t tg_old = -1) {
+  io.tglob[e] = (tg_old >= 0 ? tg_old : io.tglob[e]) + 1;
   io.reward[e] = r.rew;
   io.done_out[e] = r.done;
   io.trunc_out[e] = r.trunc;
@@ -228,6 +229,10 @@ __global__ void __launch_bounds__(256) pong_policy_step_kernel(PongIO io, FcPart
   __shared__ PongOut cand[3];
   __shared__ float s_acc[4][A1];
   stamp_if(stamps, 0, tid == 0);
+  // operands of the sampling wave and the commit, requested first (they were dependent round trips after the
+  // head's barrier): the RNG key's counters and the head bias
+  const int64_t tg0 = io.tglob[e], id0 = io.env_ids[e];
+  const float bhj = bh[lane < A1 ? lane : 0];
   // this thread's two Wh rows (2 * A1 bf16 = A1 32-bit words at byte offset 4 * A1 * tid)
   uint32_t wv[A1];
 #pragma unroll
@@ -258,9 +263,9 @@ __global__ void __launch_bounds__(256) pong_policy_step_kernel(PongIO io, FcPart
   __syncthreads();
   stamp_if(stamps, 9, tid == 0);
   if (wid == 0) {
-    const int64_t key = io.tglob[e] * ((int64_t)1 << key_shift) + io.env_ids[e];  // pre-step counter
+    const int64_t key = tg0 * ((int64_t)1 << key_shift) + id0;  // pre-step counter
     const int jj = lane < A1 ? lane : 0;
-    float zj = ((s_acc[0][jj] + s_acc[1][jj]) + (s_acc[2][jj] + s_acc[3][jj])) + bh[jj];
+    float zj = ((s_acc[0][jj] + s_acc[1][jj]) + (s_acc[2][jj] + s_acc[3][jj])) + bhj;
     if (lane < A1) z_out[(size_t)e * A1 + lane] = zj;
     const float value = __shfl(zj, A, 64);
     stamp_if(stamps, 10, lane == 0);
@@ -299,7 +304,7 @@ __global__ void __launch_bounds__(256) pong_policy_step_kernel(PongIO io, FcPart
   __syncthreads();
   stamp_if(stamps, 4, tid == 0);
   const PongOut& r = cand[pong_dir_index(sh_act)];
-  if (tid == 0) pong_commit(io, e, r);
+  if (tid == 0) pong_commit(io, e, r, tg0);
   pong_render(io, e, r.s, r.done != 0);
   if (stamps) {
     stamp_if(stamps, 5, tid == 0);

@@ -565,10 +565,11 @@ __global__ void __launch_bounds__(HB_THREADS) head_bwd_kernel(HeadBwdArgs a) {
     if (q < A1) a.gWh[(col0 + cl) * A1 + q] = v;
     else a.gbfc[col0 + cl] = v;
   }
-  if (lead && tid < A1) {   // head-bias gradient: column sums of dz in row order
+  if (lead && wv < A1) {   // head-bias gradient: column wv of dz, rows strided over a wave, xor tree (fixed order)
     float sb = 0.f;
-    for (int bb = 0; bb < B; ++bb) sb += s_dz[bb * A1 + tid];
-    a.gbh[tid] = sb;
+    for (int bb = lane; bb < B; bb += 64) sb += s_dz[bb * A1 + wv];
+    sb = wave_sum(sb);
+    if (lane == 0) a.gbh[wv] = sb;
   }
   if (a.stamps) {
     hb_stamp(a, 5);

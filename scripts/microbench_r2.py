@@ -129,6 +129,32 @@ def main():
         ph[names[i]] = float((s2[:, i] - s2[:, i - 1]).median())
     ph["end_from_first_start_us"] = float(s2[:, 6].max() - t0)
     out["trunk_bwd_phases"] = ph
+    # policy/env step phases (slots: 0 entry, 8 fc planes reduced + Wh loaded, 9 head partials, 10 logits,
+    # 1 sampled, 4 barrier, 5 committed + rendered (issued), 6 drained)
+    env = tr.env
+    eng.forward(st.obs[0], bt, head=False, shift_out=scratch, fc_parts=True)
+    hp_, S_ = eng.last_fc
+    st4 = torch.zeros(N, 16, dtype=torch.int64, device="cuda:0")
+    outs = [torch.empty_like(st.actions[0]), torch.empty_like(st.logp[0]), torch.empty_like(st.entropy[0]),
+            torch.empty_like(st.values[0]), torch.empty_like(st.rewards[0]), torch.empty_like(st.dones[0]),
+            torch.empty_like(st.truncated[0])]
+    scratch2 = scratch.clone()
+    ops.env_policy_step_pong(bt.h, eng.sWh, eng.bh, bt.z, outs[0], outs[1], outs[2], outs[3], 20, tr.policy_seed,
+                             env.state, env.t, env.tg, env.ep_ret, env.ep_stats, env.env_ids, st.obs[0], scratch2,
+                             outs[4], outs[5], outs[6], env.seed, env.max_episode_steps, env.frame_stack, True, hp_,
+                             S_, eng.bfc, st4)
+    torch.cuda.synchronize()
+    s4 = st4.cpu().double() * 10e-3
+    t0 = s4[:, 0].min()
+    seq = [(8, "fc_reduce_wh"), (9, "head_partials"), (10, "logits"), (1, "sample"), (4, "barrier"),
+           (5, "commit_render_issue"), (6, "drained")]
+    ph = {"start_spread_us": float(s4[:, 0].max() - t0)}
+    prev = 0
+    for slot, name in seq:
+        ph[name] = float((s4[:, slot] - s4[:, prev]).median())
+        prev = slot
+    ph["end_from_first_start_us"] = float(s4[:, 6].max() - t0)
+    out["policy_phases"] = ph
     st3 = torch.zeros(8, 16, dtype=torch.int64, device="cuda:0")
     r = rets
     ops.head_bwd(lb.z, acts, lpo, tr.ent_coef, tr.kl_coef, float(cfg_.vf_coef), r["rew"], r["val"], r["dones"],

@@ -332,7 +332,11 @@ class ActorCriticTrainer:
                 self._scan_ws = R.ScanWorkspace(self.device, T, N)
                 self._scan_ret = torch.empty(T * N, device=self.device)
                 self._scan_adv = torch.empty(T * N, device=self.device)
-            local_norm = cfg.norm_adv and self.dp is None
+            # native PPO: the minibatch gather normalises while it copies (no pass over the whole batch here)
+            self._norm_mom = None
+            defer = (cfg.norm_adv and self.engine is not None and cfg.algo == "ppo"
+                     and st.actions.dtype == torch.int32)
+            local_norm = cfg.norm_adv and self.dp is None and not defer
             ret, adv, mom = R.returns_scan(st.rewards, st.values, dones, cfg.returns, cfg.gamma, cfg.gae_lambda,
                                            cfg.look_ahead, norm=local_norm, ws=self._scan_ws,
                                            ev_out=self.stats["ev_before"].view(1), ret_out=self._scan_ret,
@@ -340,7 +344,10 @@ class ActorCriticTrainer:
             if cfg.norm_adv and self.dp is not None:
                 dp = self.dp
                 self._comm(lambda: dp.allreduce_sum_(mom))
-                _native.require().normalize_mom(self._scan_adv, self._scan_adv, mom, 1e-8)
+                if not defer:
+                    _native.require().normalize_mom(self._scan_adv, self._scan_adv, mom, 1e-8)
+            if defer:
+                self._norm_mom = mom
             self._scanned = True
             return self._scan_ret, self._scan_adv
         if cfg.returns == "gae":
@@ -622,7 +629,7 @@ class ActorCriticTrainer:
                 for ep in range(cfg.ppo_epochs):
                     for k in range(cfg.ppo_minibatches):
                         ops.mb_gather(*args, m["obs"], m["act"], m["logp"], m["adv"], m["ret"], m["v"],
-                                      self.policy_seed, uc, ep, k * mb)
+                                      self.policy_seed, uc, ep, k * mb, getattr(self, "_norm_mom", None), 1e-8)
                         self._learn_native(m["obs"], m["act"], m["logp"], m["adv"], m["ret"], m["v"])
             else:
                 for sel in self._minibatches(B):

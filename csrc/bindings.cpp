@@ -62,7 +62,7 @@ int aca_ev_multi_blocks(int);
 hipError_t aca_gemm_group_run(const AcaGemmDesc*, int, hipStream_t, int*);
 hipError_t aca_mb_gather(const uint8_t*, int64_t, const int*, const float*, const float*, const float*, const float*,
                          uint8_t*, int*, float*, float*, float*, float*, int, int, uint32_t, const int64_t*, int, int,
-                         hipStream_t);
+                         const double*, float, hipStream_t);
 hipError_t aca_ev_multi(const float*, const float*, float*, int, double*, unsigned int*, hipStream_t);
 hipError_t aca_sumsq(const float*, size_t, float*, hipStream_t);
 int aca_sumsq_parts();
@@ -447,7 +447,13 @@ void returns_scan(Tensor r, Tensor v, Tensor d, Tensor ret, Tensor adv, int64_t 
 // PPO minibatch k of epoch ep: rows prp_index(off + i, n, key(seed, *uc, ep)) of the rollout gathered in one launch.
 void mb_gather(Tensor obs, Tensor act, Tensor logp, Tensor adv, Tensor ret, Tensor v, Tensor o_obs, Tensor o_act,
                Tensor o_logp, Tensor o_adv, Tensor o_ret, Tensor o_v, int64_t seed, Tensor uc, int64_t ep,
-               int64_t off) {
+               int64_t off, c10::optional<Tensor> mom, double eps) {
+  const double* momp = nullptr;
+  if (mom.has_value() && mom->defined()) {
+    need(*mom, at::kDouble, "mom");
+    TORCH_CHECK(mom->numel() >= 3, "mb_gather: mom needs [count, sum, sum of squares]");
+    momp = ptr<double>(*mom);
+  }
   TORCH_CHECK(obs.is_cuda() && obs.is_contiguous() && obs.scalar_type() == at::kByte, "mb_gather: obs uint8");
   TORCH_CHECK(o_obs.is_cuda() && o_obs.is_contiguous() && o_obs.scalar_type() == at::kByte, "mb_gather: o_obs");
   need(act, at::kInt, "act");
@@ -465,7 +471,7 @@ void mb_gather(Tensor obs, Tensor act, Tensor logp, Tensor adv, Tensor ret, Tens
   check(aca_mb_gather(obs.data_ptr<uint8_t>(), R, ptr<int>(act), ptr<float>(logp), ptr<float>(adv), ptr<float>(ret),
                       ptr<float>(v), o_obs.data_ptr<uint8_t>(), ptr<int>(o_act), ptr<float>(o_logp),
                       ptr<float>(o_adv), ptr<float>(o_ret), ptr<float>(o_v), (int)mb, (int)n, (uint32_t)seed,
-                      uc.data_ptr<int64_t>(), (int)ep, (int)off, cur_stream(obs)),
+                      uc.data_ptr<int64_t>(), (int)ep, (int)off, momp, (float)eps, cur_stream(obs)),
         "mb_gather");
 }
 
@@ -1264,7 +1270,7 @@ TORCH_LIBRARY(acamd, m) {
   m.def("gemm_group_pause(bool paused) -> ()", &gemm_group_pause);
   m.def("mb_gather(Tensor obs, Tensor act, Tensor logp, Tensor adv, Tensor ret, Tensor v, Tensor o_obs, "
         "Tensor o_act, Tensor o_logp, Tensor o_adv, Tensor o_ret, Tensor o_v, int seed, Tensor uc, int ep, "
-        "int off) -> ()");
+        "int off, Tensor? mom=None, float eps=1e-8) -> ()");
   m.def("gaussian_sample(Tensor mu, Tensor log_std, Tensor keys, int seed, Tensor act, Tensor logp, Tensor ent) -> ()");
   m.def("gae(Tensor r, Tensor v, Tensor d, Tensor ret, Tensor adv, float gamma, float lam) -> ()");
   m.def("nstep_returns(Tensor r, Tensor v, Tensor d, Tensor tgt, Tensor adv, float gamma, int L) -> ()");

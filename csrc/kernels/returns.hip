@@ -113,7 +113,8 @@ __global__ void __launch_bounds__(256) mb_gather_kernel(const uint8_t* __restric
                                                         int* __restrict__ o_act, float* __restrict__ o_logp,
                                                         float* __restrict__ o_adv, float* __restrict__ o_ret,
                                                         float* __restrict__ o_v, int n, uint32_t seed,
-                                                        const int64_t* __restrict__ uc, int ep, int off) {
+                                                        const int64_t* __restrict__ uc, int ep, int off,
+                                                        const double* __restrict__ mom, float eps) {
   const int i = blockIdx.x;
   const uint32_t src = prp_index((uint32_t)(off + i), (uint32_t)n, minibatch_key(seed, *uc, ep));
   const uint8_t* s = obs + (size_t)src * R;
@@ -132,9 +133,14 @@ __global__ void __launch_bounds__(256) mb_gather_kernel(const uint8_t* __restric
     for (int64_t j = threadIdx.x; j < R; j += 256) d[j] = s[j];
   }
   if (threadIdx.x == 0) {
+    float a_ = adv[src];
+    if (mom) {   // advantage normalisation deferred from the returns scan (population std, fp64 totals)
+      const double cnt = mom[0], mean = mom[1] / cnt, var = fmax(mom[2] / cnt - mean * mean, 0.0);
+      a_ = (a_ - (float)mean) * (1.0f / (eps + (float)sqrt(var)));
+    }
     o_act[i] = act[src];
     o_logp[i] = logp[src];
-    o_adv[i] = adv[src];
+    o_adv[i] = a_;
     o_ret[i] = ret[src];
     o_v[i] = v[src];
   }
@@ -202,6 +208,7 @@ __global__ void __launch_bounds__(256) seg_stats_kernel(const float* __restrict_
 // advantage array in place, so returns + EV + advantage normalisation are ONE launch.
 constexpr int RS_THREADS = 256;
 constexpr int RS_MOM = 7;
+constexpr int RS_KREG = 8;   // chunks up to this many steps stay in registers between the passes
 
 struct RetScanArgs {
   const float* r;
@@ -225,7 +232,7 @@ __global__ void __launch_bounds__(RS_THREADS) returns_scan_kernel(RetScanArgs a)
   __shared__ double s_tot[8];
   __shared__ int s_flag;
   const int tid = threadIdx.x;
-  const int e = tid % a.E, ch = tid / a.E;
+  const int e = tid % a.E, ch = tid / a.E;   // env-fastest: every time step of a chunk is one coalesced row
   const int T = a.T, N = a.N;
   const int n = blockIdx.x * a.E + e;
   const bool live = n < N && ch < a.CH;
@@ -234,10 +241,41 @@ __global__ void __launch_bounds__(RS_THREADS) returns_scan_kernel(RetScanArgs a)
   const bool window = !gae && a.L < T;
   const double g = a.gamma, gl = (double)a.gamma * (double)a.lam;
 
+  // every operand of the thread's chunk is requested up front (chunks of <= RS_KREG steps are kept in registers
+  // for pass 2: one global round trip for the whole kernel instead of one per pass)
+  const double init = (live && !gae && !window) ? (double)a.v[(size_t)T * N + n] : 0.0;
+  const bool regs = a.K <= RS_KREG;
+  float cr[RS_KREG], cv[RS_KREG], cvn[RS_KREG];
+  uint8_t cd[RS_KREG];
+  if (regs) {
+#pragma unroll
+    for (int u = 0; u < RS_KREG; ++u) {   // u-th step from the chunk's end; clamped (unconditional) loads
+      const int t = max(t1 - 1 - u, 0);
+      const size_t i = (size_t)t * N + (live ? n : 0);
+      cr[u] = a.r[i];
+      cv[u] = a.v[i];
+      cvn[u] = a.v[i + N];
+      cd[u] = a.d[i];
+    }
+  }
   // pass 1: chunk map x_{t0} = ca + cc x_{t1}, first terminal index in the chunk
   double ca = 0.0, cc = 1.0;
   int ft = T;
-  if (live) {
+  if (live && regs) {
+#pragma unroll
+    for (int u = 0; u < RS_KREG; ++u) {
+      const int t = t1 - 1 - u;
+      if (t >= t0) {
+        const bool dn = cd[u] != 0;
+        const double nd = dn ? 0.0 : 1.0;
+        ft = dn ? t : ft;
+        const double x = gae ? (double)cr[u] + g * (double)cvn[u] * nd - (double)cv[u] : (double)cr[u];
+        const double c = (gae ? gl : g) * nd;
+        ca = x + c * ca;
+        cc = c * cc;
+      }
+    }
+  } else if (live) {
     for (int t = t1 - 1; t >= t0; --t) {
       const size_t i = (size_t)t * N + n;
       const bool dn = a.d[i] != 0;
@@ -250,39 +288,61 @@ __global__ void __launch_bounds__(RS_THREADS) returns_scan_kernel(RetScanArgs a)
     }
   }
   // suffix scan over the chunks of each env: F_ch = f_ch o F_{ch+1}
-  s_a[tid] = ca;
-  s_c[tid] = cc;
-  s_ft[tid] = ft;
-  __syncthreads();
-  for (int off = 1; off < a.CH; off <<= 1) {
-    double na = ca, nc = cc;
-    int nf = ft;
-    if (ch + off < a.CH) {
-      const int j = tid + off * a.E;
-      na = ca + cc * s_a[j];
-      nc = cc * s_c[j];
-      nf = min(ft, s_ft[j]);
-    }
-    __syncthreads();
-    s_a[tid] = ca = na;
-    s_c[tid] = cc = nc;
-    s_ft[tid] = ft = nf;
-    __syncthreads();
-  }
-  const double init = (live && !gae && !window) ? (double)a.v[(size_t)T * N + n] : 0.0;
   double x = init;
   int ntc = T;
-  if (ch + 1 < a.CH) {
-    const int j = tid + a.E;
-    x = s_a[j] + s_c[j] * init;
-    ntc = s_ft[j];
+  {
+    s_a[tid] = ca;
+    s_c[tid] = cc;
+    s_ft[tid] = ft;
+    __syncthreads();
+    for (int off = 1; off < a.CH; off <<= 1) {
+      double na = ca, nc = cc;
+      int nf = ft;
+      if (ch + off < a.CH) {
+        const int j = tid + off * a.E;
+        na = ca + cc * s_a[j];
+        nc = cc * s_c[j];
+        nf = min(ft, s_ft[j]);
+      }
+      __syncthreads();
+      s_a[tid] = ca = na;
+      s_c[tid] = cc = nc;
+      s_ft[tid] = ft = nf;
+      __syncthreads();
+    }
+    if (ch + 1 < a.CH) {
+      const int j = tid + a.E;
+      x = s_a[j] + s_c[j] * init;
+      ntc = s_ft[j];
+    }
   }
 
   // pass 2: replay the chunk from its carry
   double m[RS_MOM];
 #pragma unroll
   for (int k = 0; k < RS_MOM; ++k) m[k] = 0.0;
-  if (live) {
+  if (live && regs) {
+#pragma unroll
+    for (int u = 0; u < RS_KREG; ++u) {
+      const int t = t1 - 1 - u;
+      if (t < t0) continue;
+      const size_t i = (size_t)t * N + n;
+      const double nd = cd[u] ? 0.0 : 1.0;
+      const double vt = cv[u];
+      if (gae) x = (double)cr[u] + g * (double)cvn[u] * nd - vt + gl * nd * x;
+      else x = (double)cr[u] + g * nd * x;
+      if (window) {
+        a.gz[i] = x;
+        continue;
+      }
+      const double rt = gae ? x + vt : x, ad = gae ? x : x - vt;
+      const float rf = (float)rt, af = (float)ad;
+      a.ret[i] = rf;
+      a.adv[i] = af;
+      m[0] += af; m[1] += (double)af * af; m[2] += rf; m[3] += (double)rf * rf;
+      m[4] += vt; m[5] += vt * vt; m[6] += (double)rf * vt;
+    }
+  } else if (live) {
     for (int t = t1 - 1; t >= t0; --t) {
       const size_t i = (size_t)t * N + n;
       const double nd = a.d[i] ? 0.0 : 1.0;
@@ -459,11 +519,11 @@ extern "C" hipError_t aca_seg_stats(const float* x, const int64_t* segs, int nv,
   return hipGetLastError();
 }
 
-// Launch geometry of returns_scan: chunk length ~4 steps, CH chunks (power of two, <= 256) per env, E = 256 / CH
-// envs per workgroup.
+// Launch geometry of returns_scan: chunk length ~RS_KREG steps (kept in registers), CH chunks (power of two,
+// <= 256) per env, E = 256 / CH envs per workgroup.
 extern "C" void aca_returns_scan_geometry(int T, int N, int* E, int* CH, int* K, int* blocks) {
   int ch = 1;
-  while (ch < 256 && ch * 4 < T) ch <<= 1;
+  while (ch < 256 && ch * aca::RS_KREG < T) ch <<= 1;
   *CH = ch;
   *E = aca::RS_THREADS / ch;
   *K = (T + ch - 1) / ch;
@@ -502,9 +562,10 @@ extern "C" hipError_t aca_ev_multi(const float* x, const float* y, float* out, i
 extern "C" hipError_t aca_mb_gather(const uint8_t* obs, int64_t R, const int* act, const float* logp, const float* adv,
                                     const float* ret, const float* v, uint8_t* o_obs, int* o_act, float* o_logp,
                                     float* o_adv, float* o_ret, float* o_v, int mb, int n, uint32_t seed,
-                                    const int64_t* uc, int ep, int off, hipStream_t stream) {
+                                    const int64_t* uc, int ep, int off, const double* mom, float eps,
+                                    hipStream_t stream) {
   if (mb <= 0) return hipSuccess;
   aca::mb_gather_kernel<<<mb, 256, 0, stream>>>(obs, R, act, logp, adv, ret, v, o_obs, o_act, o_logp, o_adv, o_ret,
-                                                o_v, n, seed, uc, ep, off);
+                                                o_v, n, seed, uc, ep, off, mom, eps);
   return hipGetLastError();
 }

@@ -180,6 +180,14 @@ def test_mb_gather_equals_index_select_of_keyed_permutation(cuda):
         sel = rng.prp(torch.arange(k * mb, (k + 1) * mb, dtype=torch.int64), n, key).to(cuda)
         for src, out in zip([obs, act] + fl, outs):
             assert torch.equal(torch.index_select(src, 0, sel), out)
+        # deferred advantage normalisation (fp64 totals [count, sum, sum of squares] of the whole batch)
+        adv = fl[1].double()
+        mom = torch.stack([torch.tensor(float(n), dtype=torch.float64, device=cuda), adv.sum(), (adv * adv).sum()])
+        o_adv = torch.empty(mb, device=cuda)
+        ops.mb_gather(obs, act, *fl, outs[0], outs[1], outs[2], o_adv, outs[4], outs[5], seed, uc, ep, k * mb, mom,
+                      1e-8)
+        ref = (fl[1] - fl[1].mean()) / (1e-8 + fl[1].std(unbiased=False))
+        torch.testing.assert_close(o_adv, torch.index_select(ref, 0, sel), rtol=1e-5, atol=1e-5)
 
 
 @pytest.mark.parametrize("name", ["breakout_ppo", "mujoco_ppo_dp8"])

@@ -181,6 +181,19 @@ class CNNEngine:
                workspace=self.ws)
         return out
 
+    def fused_step_ok(self, B):
+        """The rollout step can run as ONE launch of policy/env + the next observation's row-split trunk."""
+        return (self.implicit and self.fc_parts and self.trunk_shift and self.trunk_mode in (1, 2)
+                and B <= min(self.trunk_rows_max_b, self.fused_trunk_max_b) and 2 <= self.A <= 6 and os.environ.get("ACA_FUSED_STEP", "1") != "0")
+
+    def fc_planes(self, b: _Bufs):
+        """fc product of ``b.y3`` as split-K partial planes (consumed by the fused step / value kernels)."""
+        hp = self.hpart(b.B)
+        S = G.gemm(b.y3, 3136, True, self.sWfc, 512, False, hp, 512, 3, b.B, 512, 3136, workspace=self.ws,
+                   max_planes=self.fc_max_planes)
+        self.last_fc = (hp, S)
+        return hp, S
+
     def forward(self, obs, b: _Bufs, head=True, shift_out=None, fc_parts=False):
         """obs uint8 [B, 4, 84, 84] -> b.z fp32 [B, A+1] (logits | value); ``head=False`` stops at ``b.h`` (the
         rollout fuses the head into the sampling + env-step kernel). ``shift_out``: the next observation buffer,

@@ -289,6 +289,8 @@ class ActorCriticTrainer:
         ops = _native.require()
         lb = eng.bufs(st.T * N, with_grad=True) if self._reuse_acts() else None
         fused = isinstance(env, E.PongVecEnv)
+        if fused and env.frame_stack == 4 and eng.fused_step_ok(N):
+            return self._collect_fused_steps(st, env, eng, lb, b, N)
         for t in range(st.T):
             bt = lb.rows(t * N, N) if lb is not None else b
             if fused:
@@ -311,6 +313,33 @@ class ActorCriticTrainer:
             env.step(st.actions[t], prev_obs=st.obs[t], obs_out=st.obs[t + 1], reward_out=st.rewards[t],
                      done_out=st.dones[t], trunc_out=st.truncated[t])
         eng.value(st.obs[st.T], b, st.values[st.T])
+
+    def _collect_fused_steps(self, st, env, eng, lb, b, N):
+        """Rollout as trunk(obs_0) + fc, then per step ONE launch of policy/env step t fused with the row-split trunk
+        of obs_{t+1} (``pong_fused_step``) + the fc product of obs_{t+1}; the last step's trunk is the bootstrap
+        observation's, whose value comes straight from the fc planes. The env state alternates between its two
+        parity slots (the fused kernel reads one and commits into the other)."""
+        ops = _native.require()
+        T = st.T
+        rows = (lambda t: lb.rows(t * N, N)) if lb is not None else (lambda t: b)
+        eng.forward(st.obs[0], rows(0), head=False, shift_out=st.obs[1], fc_parts=True)
+        for t in range(T):
+            hp, S = eng.last_fc
+            cur = rows(t)
+            nxt = rows(t + 1) if t + 1 < T else b
+            sn, tn, tgn, ern = env.next_state()
+            ops.pong_fused_step(cur.h, eng.sWh, eng.bh, cur.z, st.actions[t], st.logp[t], st.entropy[t],
+                                st.values[t], KEY_ENV_BITS, self.policy_seed, env.state, env.t, env.tg, env.ep_ret,
+                                sn, tn, tgn, ern, env.ep_stats, env.env_ids, st.obs[t], st.obs[t + 1],
+                                st.rewards[t], st.dones[t], st.truncated[t], env.seed, env.max_episode_steps, hp, S,
+                                eng.bfc, eng.sW1, eng.b1, eng.sW2, eng.b2, eng.sW3, eng.b3, nxt.y1, nxt.y2, nxt.y3,
+                                1.0 / 255.0, st.obs[t + 2] if t + 2 <= T else None)
+            env.flip()
+            nxt.obs = st.obs[t + 1]
+            eng.fc_planes(nxt)
+        hp, S = eng.last_fc
+        ops.fc_value(hp, S, eng.bfc, eng.sWh, eng.bh, st.values[T], None)
+        self._env_flips = T
 
     # ------------------------------------------------------------------ returns
     def _fused_returns(self):
@@ -811,6 +840,8 @@ class ActorCriticTrainer:
         self._replay_set(graph)
         if st.ring:
             st.phase ^= 1   # the replayed update ended with its rollover
+        if getattr(self, "_env_flips", 0) & 1:   # the fused rollout steps alternated the env's state slots
+            self.env.flip()
 
     def _replay_set(self, graph):
         kind = graph[0]

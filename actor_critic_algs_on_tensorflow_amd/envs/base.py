@@ -25,12 +25,28 @@ from .. import _native
 from .spaces import Box, Discrete, EnvSpec
 
 
+def _slot_property(name):
+    def get(self):
+        return self._sbuf[name][self.parity]
+
+    def set(self, value):   # in-place operators re-assign the same view; anything else is copied in
+        cur = self._sbuf[name][self.parity]
+        if value is not cur:
+            cur.copy_(value)
+    return property(get, set)
+
+
 class VecEnv:
     env_id = "base"
     observation_space = None
     action_space = None
     obs_dtype = torch.float32
     state_dim = 0
+
+    state = _slot_property("state")
+    t = _slot_property("t")
+    tg = _slot_property("tg")
+    ep_ret = _slot_property("ep_ret")
 
     def __init__(self, num_envs, device="cpu", seed=0, max_episode_steps=None, env_offset=0, frame_stack=1):
         self.num_envs = int(num_envs)
@@ -40,10 +56,16 @@ class VecEnv:
         self.env_offset = int(env_offset)
         self.frame_stack = int(frame_stack)
         N, dev = self.num_envs, self.device
-        self.state = torch.zeros(N, self.state_dim, dtype=torch.float32, device=dev)
-        self.t = torch.zeros(N, dtype=torch.int32, device=dev)           # steps in the current episode
-        self.tg = torch.zeros(N, dtype=torch.int64, device=dev)          # global step counter (RNG key)
-        self.ep_ret = torch.zeros(N, dtype=torch.float32, device=dev)    # running episode return
+        # per-env state, double-buffered: ``state`` / ``t`` / ``tg`` / ``ep_ret`` are views of slot ``parity``. Kernels
+        # that read the state in several workgroups while one of them commits the step (the fused rollout step of
+        # the CNN engine) read the current slot and write the other; :meth:`flip` then makes it current.
+        self._sbuf = {
+            "state": torch.zeros(2, N, self.state_dim, dtype=torch.float32, device=dev),
+            "t": torch.zeros(2, N, dtype=torch.int32, device=dev),        # steps in the current episode
+            "tg": torch.zeros(2, N, dtype=torch.int64, device=dev),       # global step counter (RNG key)
+            "ep_ret": torch.zeros(2, N, dtype=torch.float32, device=dev),  # running episode return
+        }
+        self.parity = 0
         self.ep_stats = torch.zeros(3, dtype=torch.float32, device=dev)  # [sum_ret, count, sum_len]
         self.env_ids = torch.arange(N, dtype=torch.int64, device=dev) + self.env_offset
         self.obs = torch.zeros((N,) + self.obs_shape, dtype=self.obs_dtype, device=dev)
@@ -53,6 +75,15 @@ class VecEnv:
         # gym-style single-env adapters need the terminal observation the auto-reset overwrites (oracle path only)
         self.keep_final_obs = False
         self.final_obs = None
+
+    def next_state(self):
+        """(state, t, tg, ep_ret) views of the non-current parity slot."""
+        q = 1 - self.parity
+        return tuple(self._sbuf[k][q] for k in ("state", "t", "tg", "ep_ret"))
+
+    def flip(self):
+        """The other parity slot becomes current (after a kernel committed the step into it)."""
+        self.parity ^= 1
 
     # -- shape info -------------------------------------------------------------------------------------------
     default_max_steps = 1000

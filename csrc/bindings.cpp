@@ -45,6 +45,12 @@ hipError_t aca_env_policy_step_pong(uint16_t*, const float*, int, int64_t, const
                                     float*, float*, float*, int, uint32_t, float*, int32_t*, int64_t*, float*, float*,
                                     const int64_t*, const uint8_t*, uint8_t*, float*, uint8_t*, uint8_t*, uint32_t,
                                     int, int, int, int, uint64_t*, hipStream_t);
+hipError_t aca_pong_fused_step(uint16_t*, const float*, int, int64_t, const float*, const uint16_t*, const float*, int,
+                               float*, int32_t*, float*, float*, float*, int, uint32_t, float*, int32_t*, int64_t*,
+                               float*, float*, int32_t*, int64_t*, float*, float*, const int64_t*, const uint8_t*,
+                               uint8_t*, float*, uint8_t*, uint8_t*, uint32_t, int, const uint16_t*, const float*,
+                               const uint16_t*, const float*, const uint16_t*, const float*, uint16_t*, uint16_t*,
+                               uint16_t*, float, uint8_t*, uint64_t*, int, hipStream_t);
 hipError_t aca_categorical_sample(const float*, int, int, int, const int64_t*, const int64_t*, const int64_t*, int,
                                   uint32_t, int32_t*, float*, float*, float*, hipStream_t);
 hipError_t aca_ev(const float*, const float*, float*, int, hipStream_t);
@@ -269,6 +275,65 @@ void env_policy_step_pong(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, 
                                  ptr<uint8_t>(trunc), (uint32_t)seed, (int)max_steps, (int)k, N, pre_shifted ? 1 : 0,
                                  stamps_ptr(stamps, N), cur_stream(state)),
         "env_policy_step_pong");
+}
+
+// Rollout step t of the Pong bank fused with the row-split trunk of the observation it produces (cnn_fused.hip
+// pong_fused_step_kernel): env state read from (state, t, tg, ep_ret), committed to the other parity buffers
+// (state_n, t_n, tg_n, ep_ret_n); prev = obs[t], out = obs[t+1] (frames 0..2 already shifted in), shift_out =
+// obs[t+2] or None; y1..y3 = the trunk activations of obs[t+1].
+void pong_fused_step(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, Tensor logp, Tensor ent, Tensor value,
+                     int64_t key_shift, int64_t pseed, Tensor state, Tensor t, Tensor tg, Tensor ep_ret,
+                     Tensor state_n, Tensor t_n, Tensor tg_n, Tensor ep_ret_n, Tensor ep_stats, Tensor ids,
+                     Tensor prev, Tensor out, Tensor reward, Tensor done, Tensor trunc, int64_t seed,
+                     int64_t max_steps, Tensor hpart, int64_t planes, Tensor bfc, Tensor W1, Tensor b1, Tensor W2,
+                     Tensor b2, Tensor W3, Tensor b3, Tensor y1, Tensor y2, Tensor y3, double scale,
+                     c10::optional<Tensor> shift_out, c10::optional<Tensor> stamps) {
+  check_env(state, t, tg, ep_ret, ep_stats, ids, reward, done, trunc);
+  check_env(state_n, t_n, tg_n, ep_ret_n, ep_stats, ids, reward, done, trunc);
+  for (auto* x : {&h, &Wh, &W1, &W2, &W3, &y1, &y2, &y3}) need(*x, at::kBFloat16, "pong_fused_step bf16");
+  for (auto* x : {&bh, &z, &logp, &ent, &value, &hpart, &bfc, &b1, &b2, &b3}) need(*x, at::kFloat, "pong_fused_step f32");
+  need(act, at::kInt, "act");
+  need(prev, at::kByte, "prev");
+  need(out, at::kByte, "out");
+  const int N = state.size(0);
+  const int A1 = bh.numel(), A = A1 - 1;
+  TORCH_CHECK(A1 >= 3 && A1 <= 7, "pong_fused_step: 2..6 actions");
+  TORCH_CHECK(state.size(1) == 8 && h.numel() == (int64_t)N * 512 && Wh.numel() == 512 * A1 &&
+                  z.numel() >= (int64_t)N * A1 && act.numel() >= N && value.numel() >= N,
+              "pong_fused_step: bad head shapes");
+  TORCH_CHECK(prev.numel() == (int64_t)N * 4 * 84 * 84 && out.numel() == prev.numel() &&
+                  prev.data_ptr() != out.data_ptr(), "pong_fused_step: frame stacks [N, 4, 84, 84], not aliased");
+  TORCH_CHECK(state.data_ptr() != state_n.data_ptr() && t.data_ptr() != t_n.data_ptr() &&
+                  tg.data_ptr() != tg_n.data_ptr() && ep_ret.data_ptr() != ep_ret_n.data_ptr(),
+              "pong_fused_step: the next-parity env state must be separate buffers");
+  TORCH_CHECK(W1.numel() == 32 * 256 && W2.numel() == 64 * 512 && W3.numel() == 64 * 576 && b1.numel() == 32 &&
+                  b2.numel() == 64 && b3.numel() == 64 && y1.numel() == (int64_t)N * 400 * 32 &&
+                  y2.numel() == (int64_t)N * 81 * 64 && y3.numel() == (int64_t)N * 49 * 64,
+              "pong_fused_step: trunk shapes");
+  for (const Tensor* x : {&prev, &out, &W1, &W2, &W3, &y1, &y2, &y3, &h, &Wh})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(x->data_ptr()) % 16 == 0, "pong_fused_step: 16-byte aligned buffers");
+  TORCH_CHECK(planes >= 1 && planes <= 32 && hpart.numel() % 32 == 0 && bfc.numel() == 512,
+              "pong_fused_step: 1..32 fc planes");
+  const int64_t pstride = hpart.numel() / 32;
+  TORCH_CHECK(pstride >= (int64_t)N * 512, "pong_fused_step: hpart planes too small");
+  uint8_t* so = nullptr;
+  if (shift_out.has_value() && shift_out->defined()) {
+    need(*shift_out, at::kByte, "shift_out");
+    TORCH_CHECK(shift_out->numel() == prev.numel() && reinterpret_cast<uintptr_t>(shift_out->data_ptr()) % 16 == 0 &&
+                    shift_out->data_ptr() != out.data_ptr(), "pong_fused_step: shift_out shape / aliasing");
+    so = shift_out->data_ptr<uint8_t>();
+  }
+  check(aca_pong_fused_step(ptr<uint16_t>(h), ptr<float>(hpart), (int)planes, pstride, ptr<float>(bfc),
+                            ptr<uint16_t>(Wh), ptr<float>(bh), A, ptr<float>(z), ptr<int32_t>(act), ptr<float>(logp),
+                            ptr<float>(ent), ptr<float>(value), (int)key_shift, (uint32_t)pseed, ptr<float>(state),
+                            ptr<int32_t>(t), ptr<int64_t>(tg), ptr<float>(ep_ret), ptr<float>(state_n),
+                            ptr<int32_t>(t_n), ptr<int64_t>(tg_n), ptr<float>(ep_ret_n), ptr<float>(ep_stats),
+                            ptr<int64_t>(ids), ptr<uint8_t>(prev), ptr<uint8_t>(out), ptr<float>(reward),
+                            ptr<uint8_t>(done), ptr<uint8_t>(trunc), (uint32_t)seed, (int)max_steps,
+                            ptr<uint16_t>(W1), ptr<float>(b1), ptr<uint16_t>(W2), ptr<float>(b2), ptr<uint16_t>(W3),
+                            ptr<float>(b3), ptr<uint16_t>(y1), ptr<uint16_t>(y2), ptr<uint16_t>(y3), (float)scale,
+                            so, stamps_ptr(stamps, N * 7), N, cur_stream(state)),
+        "pong_fused_step");
 }
 
 // bootstrap value from the fc partial planes (cnn_fused.hip); hpart holds 32 equal planes of [N, 512]
@@ -1256,6 +1321,12 @@ TORCH_LIBRARY(acamd, m) {
         "int max_steps, int k, bool pre_shifted=False, Tensor? hpart=None, int planes=0, Tensor? bfc=None, "
         "Tensor? stamps=None) -> ()");
   m.def("fc_value(Tensor hpart, int planes, Tensor bfc, Tensor Wh, Tensor bh, Tensor out, Tensor? h_out) -> ()");
+  m.def("pong_fused_step(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, Tensor logp, Tensor ent, "
+        "Tensor value, int key_shift, int pseed, Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor state_n, "
+        "Tensor t_n, Tensor tg_n, Tensor ep_ret_n, Tensor ep_stats, Tensor env_ids, Tensor prev, Tensor out, "
+        "Tensor reward, Tensor done, Tensor truncated, int seed, int max_steps, Tensor hpart, int planes, "
+        "Tensor bfc, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, Tensor y1, Tensor y2, "
+        "Tensor y3, float scale, Tensor? shift_out=None, Tensor? stamps=None) -> ()");
   m.def("categorical_sample(Tensor logits, Tensor keys, int seed, Tensor act, Tensor logp, Tensor ent) -> ()");
   m.def("categorical_sample_env(Tensor logits, Tensor tg, Tensor env_ids, int key_shift, int seed, Tensor act, "
         "Tensor logp, Tensor ent, Tensor? vout) -> ()");
@@ -1338,6 +1409,7 @@ TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
   m.impl("env_step_linear", &env_step_linear);
   m.impl("env_step_pong", &env_step_pong);
   m.impl("env_policy_step_pong", &env_policy_step_pong);
+  m.impl("pong_fused_step", &pong_fused_step);
   m.impl("categorical_sample", &categorical_sample);
   m.impl("gaussian_sample", &gaussian_sample);
   m.impl("categorical_sample_env", &categorical_sample_env);

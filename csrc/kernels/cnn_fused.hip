@@ -19,6 +19,7 @@
 // owns output-channel tile w for every M tile, so every B fragment is loaded exactly once per workgroup.
 #include "common.h"
 #include "cnn_head.h"
+#include "pong_env.h"
 
 namespace aca {
 
@@ -245,79 +246,20 @@ constexpr int TR_IN_ELEMS = 768 * 16;   // 4 x 36 x 84 = 12096 bf16, padded to 3
 
 __device__ __forceinline__ int tr_y1_own_begin(int r) { return (20 * r + 6) / 7; }
 
+// conv1 -> conv3 of row workgroup (e, r) from its staged input rows (s_in: 4 frames x 36 rows of bf16 pixel values,
+// complete) and the conv1 weights (s_w1, complete); stores the owned y1 / y2 rows and its y3 row. Shared by the
+// trunk kernel and the fused policy/env + trunk kernel.
 template <bool LATE_W>
-__global__ void __launch_bounds__(T_THREADS) cnn_trunk_rows_kernel(
-    const uint8_t* __restrict__ obs, const u16* __restrict__ W1, const float* __restrict__ b1,
-    const u16* __restrict__ W2, const float* __restrict__ b2, const u16* __restrict__ W3,
-    const float* __restrict__ b3, u16* __restrict__ y1g, u16* __restrict__ y2g, u16* __restrict__ y3g,
-    float scale, uint8_t* __restrict__ shift_out, uint8_t* __restrict__ copy_out, uint64_t* __restrict__ stamps) {
-  __shared__ __attribute__((aligned(16))) u16 s_in[TR_IN_ELEMS];
-  __shared__ __attribute__((aligned(16))) u16 s_w1[32 * W1_LD];
-  __shared__ __attribute__((aligned(16))) u16 s_y1[TR_C1_POS * Y1_LD];
-  __shared__ __attribute__((aligned(16))) u16 s_y2[TR_C2_POS * Y2_LD];
-
-  const int r = blockIdx.x % TR_ROWS, e = blockIdx.x / TR_ROWS;
+__device__ __forceinline__ void trunk_rows_compute(const u16* __restrict__ s_in, const u16* __restrict__ s_w1,
+                                                   u16* __restrict__ s_y1, u16* __restrict__ s_y2, int e, int r,
+                                                   const float bias1a, const float bias1b, const float bias2,
+                                                   const float bias3, const u16* __restrict__ W2,
+                                                   const u16* __restrict__ W3, u16* __restrict__ y1g,
+                                                   u16* __restrict__ y2g, u16* __restrict__ y3g, float scale,
+                                                   uint64_t* __restrict__ stamps) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l16 = lane & 15, lg = lane >> 4;
-  const int in0 = 8 * r;                   // first staged input row
-  stamp(stamps, 0);
-
-  // ---------------------------------------------------------------- loads, oldest first in the order they are
-  // consumed (the vm counter retires in issue order): biases, the staged input rows, conv1 weight fragments, conv2
-  // weight fragments; conv3's are issued after the staging barrier. Weights go straight to registers (each B
-  // fragment is used by one wave only), the input rows through LDS (the im2col reads overlap).
   const int n2 = wid * 16 + l16;
-  const float bias1a = b1[l16], bias1b = b1[16 + l16], bias2 = b2[n2], bias3 = b3[n2];
-  constexpr int FR_CH = TR_IN_ROWS * 84 / 16;            // 189 chunks per frame (rows of 84 B never cross frames)
-  constexpr int IN_CH = 4 * FR_CH;                        // 756
-  constexpr int IN_PER = (IN_CH + T_THREADS - 1) / T_THREADS;   // 3
-  uint4 vo[IN_PER];
-  {
-    const uint8_t* src = obs + (size_t)e * OBS_BYTES + (size_t)in0 * 84;
-#pragma unroll
-    for (int u = 0; u < IN_PER; ++u) {
-      const int i = min(tid + u * T_THREADS, IN_CH - 1);    // clamped: unconditional loads
-      const int f = i / FR_CH, c = i - f * FR_CH;
-      vo[u] = *reinterpret_cast<const uint4*>(src + (size_t)f * 84 * 84 + c * 16);
-    }
-  }
-  constexpr int W1_PER = 32 * 256 / 8 / T_THREADS;   // 4: W1 staged once through LDS (all 4 waves read it)
-  uint4 vw[W1_PER];
-#pragma unroll
-  for (int u = 0; u < W1_PER; ++u) vw[u] = reinterpret_cast<const uint4*>(W1)[tid + u * T_THREADS];
-  {
-    uint4* dst = reinterpret_cast<uint4*>(s_in);
-#pragma unroll
-    for (int u = 0; u < IN_PER; ++u) {   // branch-free (slots past IN_CH land in the pad): no block splits
-      const int i = tid + u * T_THREADS;
-      const uint2 a = u8x4_to_bf16(vo[u].x), b = u8x4_to_bf16(vo[u].y);
-      const uint2 c = u8x4_to_bf16(vo[u].z), d = u8x4_to_bf16(vo[u].w);
-      dst[2 * i] = make_uint4(a.x, a.y, b.x, b.y);
-      dst[2 * i + 1] = make_uint4(c.x, c.y, d.x, d.y);
-    }
-#pragma unroll
-    for (int u = 0; u < W1_PER; ++u) {
-      const int i = tid + u * T_THREADS, rr = i / 32, c8 = (i % 32) * 8;
-      *reinterpret_cast<uint4*>(s_w1 + rr * W1_LD + c8) = vw[u];
-    }
-    // frame-stack outputs of the owned input rows [12r, 12r + 12), straight from the registers above: the window
-    // starts 4r rows into the staged rows and spans 12 x 84 B = 63 whole 16-byte chunks (336r B = 21r chunks in),
-    // so every chunk is wholly owned or not
-    if (shift_out || copy_out) {
-#pragma unroll
-      for (int u = 0; u < IN_PER; ++u) {
-        const int i = tid + u * T_THREADS;
-        const int f = i / FR_CH, c = i - f * FR_CH;
-        const bool own = i < IN_CH && c >= 21 * r && c < 21 * r + 63;
-        const size_t goff = (size_t)e * OBS_BYTES + (size_t)in0 * 84 + c * 16;
-        if (own && copy_out) *reinterpret_cast<uint4*>(copy_out + (size_t)f * 84 * 84 + goff) = vo[u];
-        if (own && shift_out && f >= 1)
-          *reinterpret_cast<uint4*>(shift_out + (size_t)(f - 1) * 84 * 84 + goff) = vo[u];
-      }
-    }
-    __syncthreads();
-  }
-  stamp(stamps, 1);
   // conv2 / conv3 weight fragments: issued now (the staging barrier waited for obs + W1 only), consumed after conv1
   // (LATE_W: issued after conv1's MFMAs instead -- A/B variant, trunk mode 2)
   bf16x8 bw2[16], bw3[18];
@@ -444,6 +386,286 @@ __global__ void __launch_bounds__(T_THREADS) cnn_trunk_rows_kernel(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     stamp(stamps, 5);
   }
+}
+
+
+template <bool LATE_W>
+__global__ void __launch_bounds__(T_THREADS) cnn_trunk_rows_kernel(
+    const uint8_t* __restrict__ obs, const u16* __restrict__ W1, const float* __restrict__ b1,
+    const u16* __restrict__ W2, const float* __restrict__ b2, const u16* __restrict__ W3,
+    const float* __restrict__ b3, u16* __restrict__ y1g, u16* __restrict__ y2g, u16* __restrict__ y3g,
+    float scale, uint8_t* __restrict__ shift_out, uint8_t* __restrict__ copy_out, uint64_t* __restrict__ stamps) {
+  __shared__ __attribute__((aligned(16))) u16 s_in[TR_IN_ELEMS];
+  __shared__ __attribute__((aligned(16))) u16 s_w1[32 * W1_LD];
+  __shared__ __attribute__((aligned(16))) u16 s_y1[TR_C1_POS * Y1_LD];
+  __shared__ __attribute__((aligned(16))) u16 s_y2[TR_C2_POS * Y2_LD];
+
+  const int r = blockIdx.x % TR_ROWS, e = blockIdx.x / TR_ROWS;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int l16 = lane & 15, lg = lane >> 4;
+  const int in0 = 8 * r;                   // first staged input row
+  stamp(stamps, 0);
+
+  // ---------------------------------------------------------------- loads, oldest first in the order they are
+  // consumed (the vm counter retires in issue order): biases, the staged input rows, conv1 weight fragments, conv2
+  // weight fragments; conv3's are issued after the staging barrier. Weights go straight to registers (each B
+  // fragment is used by one wave only), the input rows through LDS (the im2col reads overlap).
+  const int n2 = wid * 16 + l16;
+  const float bias1a = b1[l16], bias1b = b1[16 + l16], bias2 = b2[n2], bias3 = b3[n2];
+  constexpr int FR_CH = TR_IN_ROWS * 84 / 16;            // 189 chunks per frame (rows of 84 B never cross frames)
+  constexpr int IN_CH = 4 * FR_CH;                        // 756
+  constexpr int IN_PER = (IN_CH + T_THREADS - 1) / T_THREADS;   // 3
+  uint4 vo[IN_PER];
+  {
+    const uint8_t* src = obs + (size_t)e * OBS_BYTES + (size_t)in0 * 84;
+#pragma unroll
+    for (int u = 0; u < IN_PER; ++u) {
+      const int i = min(tid + u * T_THREADS, IN_CH - 1);    // clamped: unconditional loads
+      const int f = i / FR_CH, c = i - f * FR_CH;
+      vo[u] = *reinterpret_cast<const uint4*>(src + (size_t)f * 84 * 84 + c * 16);
+    }
+  }
+  constexpr int W1_PER = 32 * 256 / 8 / T_THREADS;   // 4: W1 staged once through LDS (all 4 waves read it)
+  uint4 vw[W1_PER];
+#pragma unroll
+  for (int u = 0; u < W1_PER; ++u) vw[u] = reinterpret_cast<const uint4*>(W1)[tid + u * T_THREADS];
+  {
+    uint4* dst = reinterpret_cast<uint4*>(s_in);
+#pragma unroll
+    for (int u = 0; u < IN_PER; ++u) {   // branch-free (slots past IN_CH land in the pad): no block splits
+      const int i = tid + u * T_THREADS;
+      const uint2 a = u8x4_to_bf16(vo[u].x), b = u8x4_to_bf16(vo[u].y);
+      const uint2 c = u8x4_to_bf16(vo[u].z), d = u8x4_to_bf16(vo[u].w);
+      dst[2 * i] = make_uint4(a.x, a.y, b.x, b.y);
+      dst[2 * i + 1] = make_uint4(c.x, c.y, d.x, d.y);
+    }
+#pragma unroll
+    for (int u = 0; u < W1_PER; ++u) {
+      const int i = tid + u * T_THREADS, rr = i / 32, c8 = (i % 32) * 8;
+      *reinterpret_cast<uint4*>(s_w1 + rr * W1_LD + c8) = vw[u];
+    }
+    // frame-stack outputs of the owned input rows [12r, 12r + 12), straight from the registers above: the window
+    // starts 4r rows into the staged rows and spans 12 x 84 B = 63 whole 16-byte chunks (336r B = 21r chunks in),
+    // so every chunk is wholly owned or not
+    if (shift_out || copy_out) {
+#pragma unroll
+      for (int u = 0; u < IN_PER; ++u) {
+        const int i = tid + u * T_THREADS;
+        const int f = i / FR_CH, c = i - f * FR_CH;
+        const bool own = i < IN_CH && c >= 21 * r && c < 21 * r + 63;
+        const size_t goff = (size_t)e * OBS_BYTES + (size_t)in0 * 84 + c * 16;
+        if (own && copy_out) *reinterpret_cast<uint4*>(copy_out + (size_t)f * 84 * 84 + goff) = vo[u];
+        if (own && shift_out && f >= 1)
+          *reinterpret_cast<uint4*>(shift_out + (size_t)(f - 1) * 84 * 84 + goff) = vo[u];
+      }
+    }
+    __syncthreads();
+  }
+  stamp(stamps, 1);
+  trunk_rows_compute<LATE_W>(s_in, s_w1, s_y1, s_y2, e, r, bias1a, bias1b, bias2, bias3, W2, W3, y1g, y2g, y3g,
+                             scale, stamps);
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// Rollout step t fused with the trunk of step t + 1 (Pong-shaped bank, row-split trunk layout: workgroup (e, r)):
+//   policy/value head of env e from the fc partial planes, Gumbel-max sample, env physics (all three paddle
+//   directions evaluated while the head runs), then the NEW frame rendered straight into the staged input rows of
+//   conv row r (bf16 in LDS), the owned rows stored to the next observation (and shifted into the one after), and
+//   conv1 -> conv3 of that observation. The 7 row workgroups of an env evaluate the (tiny) head, sampling and physics
+//   redundantly -- bit-identical inputs and maths, so the same action everywhere -- and workgroup r = 0 alone
+//   writes the step's outputs. The env state is read from the current parity buffers and the committed state goes
+//   to the other parity (`nx`): no workgroup can overwrite state another one still has to read. One launch and one
+//   kernel boundary less per rollout step than policy/env kernel + trunk kernel, and the new frame never makes a
+//   global round trip before conv1.
+// ------------------------------------------------------------------------------------------------------------
+struct PongNext {   // the next parity's env state buffers (written by the committing workgroup)
+  float* state;
+  int32_t* tsteps;
+  int64_t* tglob;
+  float* ep_ret;
+};
+
+__device__ __forceinline__ void pong_commit_next(const PongIO& io, const PongNext& nx, int e, const PongOut& r,
+                                                 int64_t tg_old) {
+  nx.tglob[e] = tg_old + 1;
+  io.reward[e] = r.rew;
+  io.done_out[e] = r.done;
+  io.trunc_out[e] = r.trunc;
+  if (r.done) {
+    atomicAdd(&io.ep_stats[0], r.er);
+    atomicAdd(&io.ep_stats[1], 1.0f);
+    atomicAdd(&io.ep_stats[2], (float)r.t);
+  }
+  nx.tsteps[e] = r.done ? 0 : r.t;
+  nx.ep_ret[e] = r.done ? 0.0f : r.er;
+  float* sp = nx.state + (size_t)e * 8;
+  const PongState& q = r.s;
+  sp[0] = q.bx; sp[1] = q.by; sp[2] = q.vx; sp[3] = q.vy; sp[4] = q.pa; sp[5] = q.po; sp[6] = q.sa; sp[7] = q.so;
+}
+
+template <int A1>
+__global__ void __launch_bounds__(T_THREADS) pong_fused_step_kernel(
+    PongIO io, PongNext nx, FcParts fc, u16* __restrict__ h, const u16* __restrict__ Wh,
+    const float* __restrict__ bh, float* __restrict__ z_out, int32_t* __restrict__ act, float* __restrict__ logp,
+    float* __restrict__ ent, float* __restrict__ vout, int key_shift, uint32_t pseed, const u16* __restrict__ W1,
+    const float* __restrict__ b1, const u16* __restrict__ W2, const float* __restrict__ b2,
+    const u16* __restrict__ W3, const float* __restrict__ b3, u16* __restrict__ y1g, u16* __restrict__ y2g,
+    u16* __restrict__ y3g, float scale, uint8_t* __restrict__ shift_out, uint64_t* __restrict__ stamps) {
+  constexpr int A = A1 - 1;
+  __shared__ __attribute__((aligned(16))) u16 s_in[TR_IN_ELEMS];
+  __shared__ __attribute__((aligned(16))) u16 s_w1[32 * W1_LD];
+  __shared__ __attribute__((aligned(16))) u16 s_y1[TR_C1_POS * Y1_LD];
+  __shared__ __attribute__((aligned(16))) u16 s_y2[TR_C2_POS * Y2_LD];
+  __shared__ float s_acc[4][A1];
+  __shared__ PongOut cand[3];
+  __shared__ int sh_act;
+  const int r = blockIdx.x % TR_ROWS, e = blockIdx.x / TR_ROWS;
+  const bool lead = r == 0;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, l16 = lane & 15;
+  const int in0 = 8 * r;
+  stamp(stamps, 0);
+  // ---------------------------------------------------------------- every independent operand requested first
+  const int64_t tg0 = io.tglob[e], id0 = io.env_ids[e];
+  const float bhj = bh[lane < A1 ? lane : 0];
+  const int n2 = wid * 16 + l16;
+  const float bias1a = b1[l16], bias1b = b1[16 + l16], bias2 = b2[n2], bias3 = b3[n2];
+  uint32_t wv[A1];   // this thread's two Wh rows
+#pragma unroll
+  for (int u = 0; u < A1; ++u) wv[u] = reinterpret_cast<const uint32_t*>(Wh)[A1 * tid + u];
+  // frames 0..2 of the next observation (shifted in by the previous trunk launch): the staged rows
+  constexpr int FR_CH = TR_IN_ROWS * 84 / 16;                      // 189 chunks per frame
+  constexpr int IN3_CH = 3 * FR_CH;                                // 567
+  constexpr int IN3_PER = (IN3_CH + T_THREADS - 1) / T_THREADS;    // 3
+  uint4 vo[IN3_PER];
+  {
+    const uint8_t* src = io.out + (size_t)e * OBS_BYTES + (size_t)in0 * 84;
+#pragma unroll
+    for (int u = 0; u < IN3_PER; ++u) {
+      const int i = min(tid + u * T_THREADS, IN3_CH - 1);
+      const int f = i / FR_CH, c = i - f * FR_CH;
+      vo[u] = *reinterpret_cast<const uint4*>(src + (size_t)f * FRAME + c * 16);
+    }
+  }
+  constexpr int W1_PER = 32 * 256 / 8 / T_THREADS;   // 4
+  uint4 vw[W1_PER];
+#pragma unroll
+  for (int u = 0; u < W1_PER; ++u) vw[u] = reinterpret_cast<const uint4*>(W1)[tid + u * T_THREADS];
+  // ---------------------------------------------------------------- policy head (every row workgroup of env e)
+  float hf[2];
+  fc_h2_from_parts(fc.hpart, fc.S, fc.plane_stride, fc.bfc, e, tid, lead ? h : nullptr, hf);
+  if (tid >= 64 && tid < 67) cand[tid - 64] = pong_advance(io, e, (float)(tid - 65));
+  float acc[A1];
+#pragma unroll
+  for (int j = 0; j < A1; ++j) {
+    const uint32_t w0 = wv[j >> 1], w1 = wv[(A1 + j) >> 1];
+    const float a0 = __uint_as_float((j & 1) ? (w0 & 0xFFFF0000u) : (w0 << 16));
+    const float a1 = __uint_as_float(((A1 + j) & 1) ? (w1 & 0xFFFF0000u) : (w1 << 16));
+    acc[j] = wave_sum(hf[0] * a0 + hf[1] * a1);
+  }
+  if (lane == 0)
+#pragma unroll
+    for (int j = 0; j < A1; ++j) s_acc[wid][j] = acc[j];
+  // staging of everything that does not depend on the action: conv1 weights, frames 0..2 (bf16)
+  {
+    uint4* dst = reinterpret_cast<uint4*>(s_in);
+#pragma unroll
+    for (int u = 0; u < IN3_PER; ++u) {   // branch-free: slots past IN3_CH land in frame 3's rows (rendered later)
+      const int i = tid + u * T_THREADS;
+      const uint2 a = u8x4_to_bf16(vo[u].x), b = u8x4_to_bf16(vo[u].y);
+      const uint2 c = u8x4_to_bf16(vo[u].z), d = u8x4_to_bf16(vo[u].w);
+      dst[2 * i] = make_uint4(a.x, a.y, b.x, b.y);
+      dst[2 * i + 1] = make_uint4(c.x, c.y, d.x, d.y);
+    }
+#pragma unroll
+    for (int u = 0; u < W1_PER; ++u) {
+      const int i = tid + u * T_THREADS, rr = i / 32, c8 = (i % 32) * 8;
+      *reinterpret_cast<uint4*>(s_w1 + rr * W1_LD + c8) = vw[u];
+    }
+  }
+  __syncthreads();
+  if (wid == 0) {
+    const int64_t key = tg0 * ((int64_t)1 << key_shift) + id0;   // pre-step counter
+    const int jj = lane < A1 ? lane : 0;
+    const float zj = ((s_acc[0][jj] + s_acc[1][jj]) + (s_acc[2][jj] + s_acc[3][jj])) + bhj;
+    if (lead && lane < A1) z_out[(size_t)e * A1 + lane] = zj;
+    const float value = __shfl(zj, A, 64);
+    const bool on = lane < A;
+    const float z = on ? zj : -INFINITY;
+    const float m = wave_max(z);
+    const float ex = on ? expf(z - m) : 0.f;
+    const float lse = m + logf(wave_sum(ex));
+    const float lp = z - lse;
+    const float H = wave_sum(on ? -expf(lp) * lp : 0.f);
+    float gmb = -INFINITY;
+    if (on) gmb = z + (-logf(-logf(uniform_open(pseed, key, (uint32_t)lane))));
+    float best = gmb;
+    int bi = on ? lane : 1 << 30;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ob = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+    }
+    const float lpa = __shfl(lp, bi, 64);
+    if (lane == 0) {
+      if (lead) {
+        act[e] = bi;
+        logp[e] = lpa;
+        ent[e] = H;
+        vout[e] = value;
+      }
+      sh_act = bi;
+    }
+  }
+  __syncthreads();
+  const PongOut& res = cand[pong_dir_index(sh_act)];
+  const bool done = res.done != 0;
+  if (lead && tid == 0) pong_commit_next(io, nx, e, res, tg0);
+  // ---------------------------------------------------------------- the new frame: staged rows (all 4 frames
+  // after an episode restart), owned rows [12r, 12r + 12) to the next observation and the shifted one after it
+  {
+    constexpr int WPR = PW / 4;   // 21 words of 4 pixels per row
+    const PongGeom gm = pong_geom(res.s);
+    uint32_t* ob = reinterpret_cast<uint32_t*>(io.out + (size_t)e * OBS_BYTES);
+    uint32_t* sb = shift_out ? reinterpret_cast<uint32_t*>(shift_out + (size_t)e * OBS_BYTES) : nullptr;
+    for (int w = tid; w < TR_IN_ROWS * WPR; w += T_THREADS) {
+      const int row = w / WPR, x0 = (w - row * WPR) * 4, y = in0 + row;
+      const uint32_t word = pong_word(gm, y, x0);
+      const uint2 bw = u8x4_to_bf16(word);
+      *reinterpret_cast<uint2*>(s_in + (3 * TR_IN_ROWS + row) * 84 + x0) = bw;
+      if (done)
+#pragma unroll
+        for (int f = 0; f < 3; ++f) *reinterpret_cast<uint2*>(s_in + (f * TR_IN_ROWS + row) * 84 + x0) = bw;
+      if (y >= 12 * r && y < 12 * r + 12) {
+        const int px = (y * 84 + x0) >> 2;
+        ob[(3 * FRAME >> 2) + px] = word;
+        if (done)
+#pragma unroll
+          for (int f = 0; f < 3; ++f) ob[(f * FRAME >> 2) + px] = word;
+        if (sb) {
+          sb[(2 * FRAME >> 2) + px] = word;
+          if (done) {
+            sb[px] = word;
+            sb[(FRAME >> 2) + px] = word;
+          }
+        }
+      }
+    }
+    if (sb && !done) {   // next-next observation frames 0, 1 <- frames 1, 2 (owned 16-byte chunks, from registers)
+#pragma unroll
+      for (int u = 0; u < IN3_PER; ++u) {
+        const int i = tid + u * T_THREADS;
+        const int f = i / FR_CH, c = i - f * FR_CH;
+        if (i < IN3_CH && f >= 1 && c >= 21 * r && c < 21 * r + 63)
+          *reinterpret_cast<uint4*>(shift_out + (size_t)e * OBS_BYTES + (size_t)(f - 1) * FRAME +
+                                    (size_t)in0 * 84 + c * 16) = vo[u];
+      }
+    }
+  }
+  __syncthreads();
+  stamp(stamps, 1);
+  trunk_rows_compute<true>(s_in, s_w1, s_y1, s_y2, e, r, bias1a, bias1b, bias2, bias3, W2, W3, y1g, y2g, y3g,
+                           scale, stamps);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -804,5 +1026,36 @@ extern "C" hipError_t aca_cnn_trunk_bwd(const uint16_t* dy3, const uint16_t* W3,
                         (const void*)dy2, (const void*)dy1})
     if (reinterpret_cast<uintptr_t>(p) % 16) return hipErrorInvalidValue;
   aca::cnn_trunk_bwd_kernel<<<B, aca::BW_T, 0, stream>>>(dy3, W3, y2, W2, y1, dy2, dy1, biasp, stamps);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t aca_pong_fused_step(
+    uint16_t* h, const float* hpart, int S, int64_t plane_stride, const float* bfc, const uint16_t* Wh,
+    const float* bh, int A, float* z, int32_t* act, float* logp, float* ent, float* value, int key_shift,
+    uint32_t pseed, float* state, int32_t* t, int64_t* tg, float* ep_ret, float* state_n, int32_t* t_n,
+    int64_t* tg_n, float* ep_ret_n, float* ep_stats, const int64_t* ids, const uint8_t* prev, uint8_t* out,
+    float* reward, uint8_t* done, uint8_t* trunc, uint32_t seed, int max_steps, const uint16_t* W1, const float* b1,
+    const uint16_t* W2, const float* b2, const uint16_t* W3, const float* b3, uint16_t* y1, uint16_t* y2,
+    uint16_t* y3, float scale, uint8_t* shift_out, uint64_t* stamps, int N, hipStream_t stream) {
+  if (N <= 0) return hipSuccess;
+  aca::PongIO io;
+  io.state = state; io.tsteps = t; io.tglob = tg; io.ep_ret = ep_ret; io.ep_stats = ep_stats; io.env_ids = ids;
+  io.prev = prev; io.out = out; io.reward = reward; io.done_out = done; io.trunc_out = trunc; io.seed = seed;
+  io.max_steps = max_steps; io.k = 4;
+  aca::PongNext nx{state_n, t_n, tg_n, ep_ret_n};
+  aca::FcParts fc{hpart, S, plane_stride, bfc};
+  const int grid = N * aca::TR_ROWS;
+  switch (A + 1) {
+#define ACA_FUSED_CASE(A1)                                                                                       \
+  case A1:                                                                                                       \
+    aca::pong_fused_step_kernel<A1><<<grid, aca::T_THREADS, 0, stream>>>(                                         \
+        io, nx, fc, h, Wh, bh, z, act, logp, ent, value, key_shift, pseed, W1, b1, W2, b2, W3, b3, y1, y2, y3,    \
+        scale, shift_out, stamps);                                                                               \
+    break;
+    ACA_FUSED_CASE(3) ACA_FUSED_CASE(4) ACA_FUSED_CASE(5) ACA_FUSED_CASE(6) ACA_FUSED_CASE(7)
+#undef ACA_FUSED_CASE
+    default:
+      return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }

@@ -56,6 +56,13 @@ __device__ __forceinline__ void fc_h_from_parts(const float* __restrict__ hpart,
 // One workgroup of 256 threads: thread t produces hidden units 2t, 2t+1 of env e (8 planes' loads in flight per
 // round; slots past S read plane 0 and are discarded by a select), bf16-rounded like the GEMM epilogue; stores
 // them if h_out.
+struct FcParts {        // optional: h comes from the fc GEMM's split-K partial planes
+  const float* hpart;    // null: h is read as a finished bf16 row
+  int S;
+  int64_t plane_stride;
+  const float* bfc;
+};
+
 __device__ __forceinline__ void fc_h2_from_parts(const float* __restrict__ hpart, int S, int64_t plane_stride,
                                                  const float* __restrict__ bfc, int e, int t,
                                                  u16* __restrict__ h_out, float (&hv)[2]) {

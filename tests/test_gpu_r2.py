@@ -296,3 +296,37 @@ def test_grouped_gemm_launch_equals_separate_launches(cuda):
     assert ran == 2
     for a, b in zip(sep, grp):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("capture", [True, False])
+def test_fused_rollout_step_equals_separate_policy_and_trunk(cuda, capture, monkeypatch):
+    """The rollout step fused with the next observation's row-split trunk (pong_fused_step, env state in two parity
+    slots) reproduces the separate trunk + policy/env launches bit for bit: parameters, rollout tensors and env
+    state over several updates with episode truncations, an odd rollout length (parity flips on graph replay) and
+    graph capture or eager steps."""
+    monkeypatch.setattr("actor_critic_algs_on_tensorflow_amd.ops.gemm.TUNE", False)
+    from actor_critic_algs_on_tensorflow_amd import preset
+    from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
+    runs = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("ACA_FUSED_STEP", fused)
+        tr = ActorCriticTrainer(preset("pong_a2c", num_envs=16, n_steps=5, device="cuda:0", outdir=None, quiet=True,
+                                       stdout_freq=0, save_every=0, seed=5))
+        tr.env.max_episode_steps = 7
+        if capture:
+            tr.capture(warmup=1)
+        else:
+            tr.step()
+        snaps = []
+        for _ in range(4):
+            tr.step()
+            st = tr.storage
+            snaps.append([tr.flat.data.clone(), st.actions[:].clone(), st.rewards[:].clone(),
+                          st.values[:].clone(), st.obs[st.T].clone(), tr.env.state.clone(), tr.env.t.clone(),
+                          tr.env.tg.clone(), tr.env.ep_ret.clone(), tr.env.ep_stats.clone()])
+        torch.cuda.synchronize()
+        assert (getattr(tr, "_env_flips", 0) == 5) == (fused == "1")
+        runs.append(snaps)
+    for k, (a, b) in enumerate(zip(*runs)):
+        for j, (x, y) in enumerate(zip(a, b)):
+            assert torch.equal(x, y), (k, j)

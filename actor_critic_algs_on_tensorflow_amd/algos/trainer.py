@@ -548,10 +548,10 @@ class ActorCriticTrainer:
             self.lr_ctrl.update_(self.actor_opt.lr, kl)
 
     # ------------------------------------------------------------------ learning (native MLP engine)
-    def _mlp_step(self, eng, B, idx, obs, actions, logp_old, adv, ret, v_old, perm=None):
+    def _mlp_step(self, eng, B, idx, obs, actions, logp_old, adv, ret, v_old, perm=None, bump=None):
         cfg = self.cfg
         ppo = cfg.algo == "ppo"
-        used = eng.train(obs, actions, logp_old, adv, ret, self.ent_coef, self.kl_coef, B, idx=idx, perm=perm,
+        used = eng.train(obs, actions, logp_old, adv, ret, self.ent_coef, self.kl_coef, B, idx=idx, perm=perm, bump=bump,
                          v_old=v_old if ppo else None, vf_coef=1.0, ppo=ppo, ppo_clip=cfg.ppo_clip if ppo else 0.0,
                          v_clip=(cfg.ppo_value_clip or 0.0) if ppo else 0.0, stats=self.stats_buf,
                          clips=(cfg.clip_value, cfg.critic_clip_value), want_parts=self.dp is None)
@@ -573,11 +573,13 @@ class ActorCriticTrainer:
             uc = self.update_counter.view(1)
             for ep in range(cfg.ppo_epochs):
                 for k in range(cfg.ppo_minibatches):
+                    last = ep == cfg.ppo_epochs - 1 and k == cfg.ppo_minibatches - 1
+                    # the last minibatch's weight-gradient launch advances the update counter (no extra launch)
                     self._mlp_step(eng, mb, None, obs, actions, logp_old, adv, ret, v_old,
-                                   perm=(uc, ep, k * mb, B, self.policy_seed))
+                                   perm=(uc, ep, k * mb, B, self.policy_seed), bump=self.update_counter if last else None)
         else:
             self._mlp_step(eng, B, None, obs, actions, logp_old, adv, ret, v_old)
-        self.update_counter += 1
+            self.update_counter += 1
         if self.lr_ctrl is not None or cfg.kl_coef > 0:
             if not hasattr(self, "_eval_buf"):
                 self._eval_buf = (torch.empty(B, device=self.device), torch.empty(B, device=self.device))
@@ -655,11 +657,17 @@ class ActorCriticTrainer:
                 ops = _native.require()
                 uc = self.update_counter.view(1)
                 args = [t.contiguous() for t in (obs, actions, logp_old, adv, ret, v_old)]
+                if not hasattr(self, "_uc_ticket"):
+                    self._uc_ticket = torch.zeros(1, dtype=torch.int32, device=self.device)
                 for ep in range(cfg.ppo_epochs):
                     for k in range(cfg.ppo_minibatches):
+                        last = ep == cfg.ppo_epochs - 1 and k == cfg.ppo_minibatches - 1
+                        # the last gather also advances the update counter (its last workgroup; no extra launch)
                         ops.mb_gather(*args, m["obs"], m["act"], m["logp"], m["adv"], m["ret"], m["v"],
-                                      self.policy_seed, uc, ep, k * mb, getattr(self, "_norm_mom", None), 1e-8)
+                                      self.policy_seed, uc, ep, k * mb, getattr(self, "_norm_mom", None), 1e-8,
+                                      self._uc_ticket if last else None)
                         self._learn_native(m["obs"], m["act"], m["logp"], m["adv"], m["ret"], m["v"])
+                self._uc_bumped = True
             else:
                 for sel in self._minibatches(B):
                     for key, src in (("obs", obs), ("act", actions), ("logp", logp_old), ("adv", adv), ("ret", ret),
@@ -677,7 +685,7 @@ class ActorCriticTrainer:
         """Post-update KL / EV / adaptive lr (after the optimiser step)."""
         if self.engine is None:
             return
-        if self.cfg.algo == "ppo":
+        if self.cfg.algo == "ppo" and not getattr(self, "_uc_bumped", False):
             self.update_counter += 1   # keys the minibatch permutations
         if self.lr_ctrl is not None or self.cfg.kl_coef > 0:
             obs, actions, logp_old, ret = self._last

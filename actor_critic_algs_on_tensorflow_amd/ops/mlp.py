@@ -191,11 +191,13 @@ class MLPEngine:
                   ent_out=ent_out, v_out=v_out)
 
     def train(self, obs, actions, logp_old, adv, ret, ent_coef, kl_coef, B, idx=None, v_old=None, vf_coef=1.0,
-              ppo=False, ppo_clip=0.0, v_clip=0.0, stats=None, clips=(None, None), want_parts=True, perm=None):
+              ppo=False, ppo_clip=0.0, v_clip=0.0, stats=None, clips=(None, None), want_parts=True, perm=None,
+              bump=None):
         """One learner (mini)batch: rows ``idx`` / ``perm`` = (update_counter, epoch, offset, n, seed) -- the rows
         ``prp(offset + r)`` of the keyed permutation of ``[0, n)`` (envs/rng.py), computed in-kernel -- or the first
         ``B`` rows of the rollout -> gradients in the slab, statistics into ``stats[0:7]``, sums of squares into
-        :attr:`parts` (when ``want_parts``)."""
+        :attr:`parts` (when ``want_parts``). ``bump``: an int64 counter the weight-gradient launch advances by one
+        (the PPO update counter, after the update's last minibatch -- no separate launch)."""
         ops = _native.require()
         self._fwd(2, obs, B, 0, 2, desc_B=B, idx=idx, perm=perm, act_in=actions, logp_old=logp_old, adv=adv, ret=ret,
                   v_old=v_old, ent_coef=ent_coef, kl_coef=kl_coef, vf_coef=vf_coef, ppo_clip=ppo_clip,
@@ -206,7 +208,8 @@ class MLPEngine:
         st = stats if stats is not None else self._dummy_stats
         ops.mlp_wgrad(desc, 2, B, nsplit, self.items[0], self.items[1], self.parts[0] if use_parts else None,
                       self.parts[1] if use_parts else None, float(clips[0] or -1.0), float(clips[1] or -1.0),
-                      self.g_log_std, self.A, self.mstats, st, ent_coef, kl_coef, self._mpart(B), (B + BM - 1) // BM)
+                      self.g_log_std, self.A, self.mstats, st, ent_coef, kl_coef, self._mpart(B), (B + BM - 1) // BM,
+                      bump)
         return use_parts
 
     # ------------------------------------------------------------------------------------------- fused rollout

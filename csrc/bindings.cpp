@@ -68,7 +68,7 @@ int aca_ev_multi_blocks(int);
 hipError_t aca_gemm_group_run(const AcaGemmDesc*, int, hipStream_t, int*);
 hipError_t aca_mb_gather(const uint8_t*, int64_t, const int*, const float*, const float*, const float*, const float*,
                          uint8_t*, int*, float*, float*, float*, float*, int, int, uint32_t, const int64_t*, int, int,
-                         const double*, float, hipStream_t);
+                         const double*, float, unsigned int*, hipStream_t);
 hipError_t aca_ev_multi(const float*, const float*, float*, int, double*, unsigned int*, hipStream_t);
 hipError_t aca_sumsq(const float*, size_t, float*, hipStream_t);
 int aca_sumsq_parts();
@@ -512,8 +512,13 @@ void returns_scan(Tensor r, Tensor v, Tensor d, Tensor ret, Tensor adv, int64_t 
 // PPO minibatch k of epoch ep: rows prp_index(off + i, n, key(seed, *uc, ep)) of the rollout gathered in one launch.
 void mb_gather(Tensor obs, Tensor act, Tensor logp, Tensor adv, Tensor ret, Tensor v, Tensor o_obs, Tensor o_act,
                Tensor o_logp, Tensor o_adv, Tensor o_ret, Tensor o_v, int64_t seed, Tensor uc, int64_t ep,
-               int64_t off, c10::optional<Tensor> mom, double eps) {
+               int64_t off, c10::optional<Tensor> mom, double eps, c10::optional<Tensor> bump_ticket) {
   const double* momp = nullptr;
+  unsigned int* tk = nullptr;
+  if (bump_ticket.has_value() && bump_ticket->defined()) {
+    need(*bump_ticket, at::kInt, "bump_ticket");
+    tk = reinterpret_cast<unsigned int*>(bump_ticket->data_ptr<int32_t>());
+  }
   if (mom.has_value() && mom->defined()) {
     need(*mom, at::kDouble, "mom");
     TORCH_CHECK(mom->numel() >= 3, "mb_gather: mom needs [count, sum, sum of squares]");
@@ -536,7 +541,7 @@ void mb_gather(Tensor obs, Tensor act, Tensor logp, Tensor adv, Tensor ret, Tens
   check(aca_mb_gather(obs.data_ptr<uint8_t>(), R, ptr<int>(act), ptr<float>(logp), ptr<float>(adv), ptr<float>(ret),
                       ptr<float>(v), o_obs.data_ptr<uint8_t>(), ptr<int>(o_act), ptr<float>(o_logp),
                       ptr<float>(o_adv), ptr<float>(o_ret), ptr<float>(o_v), (int)mb, (int)n, (uint32_t)seed,
-                      uc.data_ptr<int64_t>(), (int)ep, (int)off, momp, (float)eps, cur_stream(obs)),
+                      uc.data_ptr<int64_t>(), (int)ep, (int)off, momp, (float)eps, tk, cur_stream(obs)),
         "mb_gather");
 }
 
@@ -727,9 +732,13 @@ void mlp_wgrad(Tensor desc, int64_t ntw, int64_t B, int64_t nsplit, int64_t item
                c10::optional<Tensor> parts0, c10::optional<Tensor> parts1, double clip0, double clip1,
                c10::optional<Tensor> g_log_std, int64_t A, c10::optional<Tensor> mstats, c10::optional<Tensor> stats,
                c10::optional<Tensor> ent_coef, c10::optional<Tensor> kl_coef, c10::optional<Tensor> mpart,
-               int64_t mpart_rows) {
+               int64_t mpart_rows, c10::optional<Tensor> bump) {
   need(desc, at::kLong, "desc");
   aca::WgradArgs a{};
+  if (bump.has_value() && bump->defined()) {
+    need(*bump, at::kLong, "bump");
+    a.bump = bump->data_ptr<int64_t>();
+  }
   a.mpart = copt<float>(mpart, at::kFloat, "mpart");
   a.mpart_rows = (int)mpart_rows;
   if (a.mpart) TORCH_CHECK(mpart_rows >= 0 && mpart->numel() >= mpart_rows * aca::MPART_W && A <= 16,
@@ -1341,7 +1350,7 @@ TORCH_LIBRARY(acamd, m) {
   m.def("gemm_group_pause(bool paused) -> ()", &gemm_group_pause);
   m.def("mb_gather(Tensor obs, Tensor act, Tensor logp, Tensor adv, Tensor ret, Tensor v, Tensor o_obs, "
         "Tensor o_act, Tensor o_logp, Tensor o_adv, Tensor o_ret, Tensor o_v, int seed, Tensor uc, int ep, "
-        "int off, Tensor? mom=None, float eps=1e-8) -> ()");
+        "int off, Tensor? mom=None, float eps=1e-8, Tensor? bump_ticket=None) -> ()");
   m.def("gaussian_sample(Tensor mu, Tensor log_std, Tensor keys, int seed, Tensor act, Tensor logp, Tensor ent) -> ()");
   m.def("gae(Tensor r, Tensor v, Tensor d, Tensor ret, Tensor adv, float gamma, float lam) -> ()");
   m.def("nstep_returns(Tensor r, Tensor v, Tensor d, Tensor tgt, Tensor adv, float gamma, int L) -> ()");
@@ -1368,7 +1377,7 @@ TORCH_LIBRARY(acamd, m) {
         "float v_clip, bool ppo, Tensor? g_log_std, Tensor? mstats, Tensor? mpart=None) -> ()");
   m.def("mlp_wgrad(Tensor desc, int ntw, int B, int nsplit, int items0, int items1, Tensor? parts0, "
         "Tensor? parts1, float clip0, float clip1, Tensor? g_log_std, int A, Tensor? mstats, Tensor? stats, "
-        "Tensor? ent_coef, Tensor? kl_coef, Tensor? mpart=None, int mpart_rows=0) -> ()");
+        "Tensor? ent_coef, Tensor? kl_coef, Tensor? mpart=None, int mpart_rows=0, Tensor? bump=None) -> ()");
   m.def("mlp_rollout(Tensor desc, int lds, Tensor obs, Tensor act, Tensor logp, Tensor ent, Tensor reward, "
         "Tensor done, Tensor truncated, Tensor log_std, Tensor ac_scale, int key_shift, int policy_seed, "
         "Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, Tensor env_ids, Tensor lin_A, "

@@ -545,6 +545,8 @@ __global__ void __launch_bounds__(256) mlp_wgrad_kernel(WgradArgs a) {
     for (int k = 0; k < 7; ++k) a.stats[k] = m[k];
     for (int k = 0; k < 8; ++k) a.mstats[k] = 0.f;
   }
+  // the train kernel (the counter's only reader in this minibatch) has finished: stream order
+  if (blockIdx.x == 0 && threadIdx.x == 0 && a.bump) *a.bump += 1;
   // locate (tower, layer, tile)
   int t = 0;
   if (item >= a.items[0]) {

@@ -61,6 +61,7 @@ struct WgradArgs {
   float* mstats; float* stats; const float* ent_coef; const float* kl_coef;
   int items[2];               // 16x16 tiles per tower (host-computed)
   const float* mpart; int mpart_rows;   // the train kernel's partial rows (reduced here in a fixed order)
+  int64_t* bump;              // optional counter advanced once (PPO update counter after the update's last minibatch)
 };
 
 // Fused rollout of the MuJoCo-shaped linear bank (mlp_rollout_kernel): T steps of actor + Gaussian sample + env step.

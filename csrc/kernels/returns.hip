@@ -114,9 +114,11 @@ __global__ void __launch_bounds__(256) mb_gather_kernel(const uint8_t* __restric
                                                         float* __restrict__ o_adv, float* __restrict__ o_ret,
                                                         float* __restrict__ o_v, int n, uint32_t seed,
                                                         const int64_t* __restrict__ uc, int ep, int off,
-                                                        const double* __restrict__ mom, float eps) {
+                                                        const double* __restrict__ mom, float eps,
+                                                        unsigned int* __restrict__ bump_ticket) {
   const int i = blockIdx.x;
-  const uint32_t src = prp_index((uint32_t)(off + i), (uint32_t)n, minibatch_key(seed, *uc, ep));
+  const int64_t ucv = *uc;
+  const uint32_t src = prp_index((uint32_t)(off + i), (uint32_t)n, minibatch_key(seed, ucv, ep));
   const uint8_t* s = obs + (size_t)src * R;
   uint8_t* d = o_obs + (size_t)i * R;
   if ((R & 15) == 0) {
@@ -143,6 +145,18 @@ __global__ void __launch_bounds__(256) mb_gather_kernel(const uint8_t* __restric
     o_adv[i] = a_;
     o_ret[i] = ret[src];
     o_v[i] = v[src];
+  }
+  if (bump_ticket) {
+    // last minibatch of the update: the workgroup that finishes last advances the update counter. Only a count is
+    // handed over (every workgroup read *uc before its ticket), so the ticket is relaxed, with no release fence.
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned int prev = __hip_atomic_fetch_add(bump_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (prev == gridDim.x - 1u) {
+        *const_cast<int64_t*>(uc) = ucv + 1;
+        __hip_atomic_store(bump_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
   }
 }
 
@@ -563,9 +577,9 @@ extern "C" hipError_t aca_mb_gather(const uint8_t* obs, int64_t R, const int* ac
                                     const float* ret, const float* v, uint8_t* o_obs, int* o_act, float* o_logp,
                                     float* o_adv, float* o_ret, float* o_v, int mb, int n, uint32_t seed,
                                     const int64_t* uc, int ep, int off, const double* mom, float eps,
-                                    hipStream_t stream) {
+                                    unsigned int* bump_ticket, hipStream_t stream) {
   if (mb <= 0) return hipSuccess;
   aca::mb_gather_kernel<<<mb, 256, 0, stream>>>(obs, R, act, logp, adv, ret, v, o_obs, o_act, o_logp, o_adv, o_ret,
-                                                o_v, n, seed, uc, ep, off, mom, eps);
+                                                o_v, n, seed, uc, ep, off, mom, eps, bump_ticket);
   return hipGetLastError();
 }

@@ -210,10 +210,12 @@ def test_ppo_graph_replay_bitwise_equals_eager(cuda, name, monkeypatch):
         else:
             tr.step()
         snaps = []
+        uc0 = int(tr.update_counter)
         for _ in range(3):
             tr.step()
             snaps.append(tr.flat.data.clone())
         torch.cuda.synchronize()
+        assert int(tr.update_counter) == uc0 + 3   # advanced in-kernel by the last minibatch of each update
         runs.append(snaps)
     for k, (a, b) in enumerate(zip(*runs)):
         assert torch.equal(a, b), k

@@ -115,6 +115,10 @@ class CNNEngine:
         # 0: split-K fp32 atomics into the slab (nondeterministic summation order)
         self.det_wgrad = implicit and os.environ.get("ACA_DET_WGRAD", "1") != "0"
         self.wgrad_planes = int(os.environ.get("ACA_WGRAD_PLANES", "64"))
+        # conv1 weight gradient by the per-sample kernel (conv_wgrad.hip: frames + dy1 staged once per sample) instead
+        # of the implicit-im2col GEMM, from this many learner rows up
+        self.conv1_wgrad_min_b = int(os.environ.get("ACA_CONV1_WGRAD_MIN_B", "1024"))
+        self.conv1_planes = int(os.environ.get("ACA_CONV1_PLANES", "128"))
         self._planes = {}
         self._wsplits = {}
         self._cur_planes = {}
@@ -270,6 +274,21 @@ class CNNEngine:
         self._wsplits[name] = S
         self._cur_planes[name] = S
 
+    def _wgrad_conv1(self, b, ws):
+        B = b.B
+        if not (self.det_wgrad and self.implicit and B >= self.conv1_wgrad_min_b):
+            self._wgrad("W1", self.gW1, b.dy1, 32, b.obs, 0, 32, 256, B * 400, ws, [1, B, 4, 84, 84, 8, 8, 4],
+                        1.0 / 255.0)
+            return
+        P = max(1, min(self.conv1_planes, B))
+        buf = self._planes.get("W1")
+        if buf is None or buf.numel() < P * 32 * 256:
+            buf = torch.zeros(max(P, self.wgrad_planes) * 32 * 256, dtype=torch.float32, device=self.dev)
+            self._planes["W1"] = buf
+        _native.require().conv1_wgrad(b.obs, b.dy1, buf, P, 1.0 / 255.0)
+        self._wsplits["W1"] = P
+        self._cur_planes["W1"] = P
+
     def head_ok(self, B):
         return self.fused_head and 2 <= self.A <= 7 and B <= 512
 
@@ -349,8 +368,7 @@ class CNNEngine:
                 return
         _native.require().cnn_trunk_bwd(b.dy3, self.sW3, b.y2, self.sW2, b.y1, b.dy2, b.dy1, b.biasp)
         with G.group():   # the longest product (conv1, K = 400 B) first
-            self._wgrad("W1", self.gW1, b.dy1, 32, b.obs, 0, 32, 256, B * 400, ws, [1, B, 4, 84, 84, 8, 8, 4],
-                        1.0 / 255.0)
+            self._wgrad_conv1(b, ws)
             self._wgrad("W2", self.gW2, b.dy2, 64, b.y1, 0, 64, 512, B * 81, ws2, [2, B, 32, 20, 20, 4, 4, 2])
             self._wgrad("W3", self.gW3, b.dy3, 64, b.y2, 0, 64, 576, B * 49, ws2, [2, B, 64, 9, 9, 3, 3, 1])
         self.finalize(b)
@@ -393,8 +411,7 @@ class CNNEngine:
             G.col2im_nhwc(self.dcol2(b), b.y1, b.dy1, self.gb1, B, 20, 20, 32, 4, 4, 2)
         # conv1 weight gradient (last product of the chain: on the main stream)
         if imp:
-            self._wgrad("W1", self.gW1, b.dy1, 32, b.obs, 0, 32, 256, B * 400, ws, [1, B, 4, 84, 84, 8, 8, 4],
-                        1.0 / 255.0)
+            self._wgrad_conv1(b, ws)
         else:
             G.gemm(b.dy1, 32, False, b.col1, 256, False, self.gW1, 256, 2, 32, 256, B * 400, workspace=ws)
         ev[4].record(side)

@@ -70,6 +70,7 @@ hipError_t aca_mb_gather(const uint8_t*, int64_t, const int*, const float*, cons
                          uint8_t*, int*, float*, float*, float*, float*, int, int, uint32_t, const int64_t*, int, int,
                          const double*, float, unsigned int*, hipStream_t);
 hipError_t aca_ev_multi(const float*, const float*, float*, int, double*, unsigned int*, hipStream_t);
+hipError_t aca_conv1_wgrad(const uint8_t*, const uint16_t*, float*, int, int, float, hipStream_t);
 hipError_t aca_sumsq(const float*, size_t, float*, hipStream_t);
 int aca_sumsq_parts();
 hipError_t aca_adam_step(float*, float*, float*, float*, size_t, const float*, float*, const float*, float*, uint16_t*,
@@ -507,6 +508,23 @@ void returns_scan(Tensor r, Tensor v, Tensor d, Tensor ret, Tensor adv, int64_t 
                          evp, T, N, (int)mode, (int)L, norm ? 1 : 0, (float)gamma, (float)lam, (float)eps,
                          cur_stream(r)),
         "returns_scan");
+}
+
+// conv1 weight gradient as P partial planes [P][32][256] (conv_wgrad.hip): obs uint8 [B, 4, 84, 84], dy1 bf16
+// [B * 400, 32]; plane g holds samples [g B / P, (g + 1) B / P).
+void conv1_wgrad(Tensor obs, Tensor dy1, Tensor planes, int64_t P, double scale) {
+  TORCH_CHECK(obs.is_cuda() && obs.is_contiguous() && obs.scalar_type() == at::kByte, "conv1_wgrad: obs uint8");
+  need(dy1, at::kBFloat16, "conv1_wgrad dy1");
+  need(planes, at::kFloat, "conv1_wgrad planes");
+  const int64_t B = obs.numel() / (4 * 84 * 84);
+  TORCH_CHECK(B >= 1 && obs.numel() == B * 4 * 84 * 84 && dy1.numel() == B * 400 * 32,
+              "conv1_wgrad: obs [B, 4, 84, 84] and dy1 [B * 400, 32]");
+  TORCH_CHECK(P >= 1 && P <= 1024 && planes.numel() >= P * 32 * 256, "conv1_wgrad: planes too small");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(obs.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(dy1.data_ptr()) % 16 == 0,
+              "conv1_wgrad: 16-byte aligned operands");
+  check(aca_conv1_wgrad(obs.data_ptr<uint8_t>(), ptr<uint16_t>(dy1), ptr<float>(planes), (int)B, (int)P, (float)scale,
+                        cur_stream(obs)),
+        "conv1_wgrad");
 }
 
 // PPO minibatch k of epoch ep: rows prp_index(off + i, n, key(seed, *uc, ep)) of the rollout gathered in one launch.
@@ -1348,6 +1366,7 @@ TORCH_LIBRARY(acamd, m) {
   m.def("gemm_group_begin() -> ()", &gemm_group_begin);
   m.def("gemm_group_end() -> int", &gemm_group_end);
   m.def("gemm_group_pause(bool paused) -> ()", &gemm_group_pause);
+  m.def("conv1_wgrad(Tensor obs, Tensor dy1, Tensor planes, int P, float scale) -> ()");
   m.def("mb_gather(Tensor obs, Tensor act, Tensor logp, Tensor adv, Tensor ret, Tensor v, Tensor o_obs, "
         "Tensor o_act, Tensor o_logp, Tensor o_adv, Tensor o_ret, Tensor o_v, int seed, Tensor uc, int ep, "
         "int off, Tensor? mom=None, float eps=1e-8, Tensor? bump_ticket=None) -> ()");
@@ -1429,6 +1448,7 @@ TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
   m.impl("returns_scan", &returns_scan);
   m.impl("normalize_mom", &normalize_mom);
   m.impl("mb_gather", &mb_gather);
+  m.impl("conv1_wgrad", &conv1_wgrad);
   m.impl("moments", &moments);
   m.impl("sumsq", &sumsq);
   m.impl("adam_step", &adam_step);

@@ -332,3 +332,30 @@ def test_fused_rollout_step_equals_separate_policy_and_trunk(cuda, capture, monk
     for k, (a, b) in enumerate(zip(*runs)):
         for j, (x, y) in enumerate(zip(a, b)):
             assert torch.equal(x, y), (k, j)
+
+
+@pytest.mark.parametrize("B,P", [(7, 4), (160, 64), (1024, 64)])
+def test_conv1_wgrad_planes_match_autograd(cuda, B, P):
+    """Per-sample conv1 weight gradient (conv_wgrad.hip): the plane sum == the fp32 autograd conv weight gradient of
+    obs/255 and dy1, every plane holds exactly its sample range, and two runs are bit-identical."""
+    import torch.nn.functional as F
+    from actor_critic_algs_on_tensorflow_amd import _native
+    ops = _native.require()
+    g = torch.Generator(device="cpu").manual_seed(B)
+    obs = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, generator=g).to(cuda)
+    dy1 = (torch.randn(B * 400, 32, generator=g) * 0.1).to(torch.bfloat16).to(cuda)
+    planes = torch.full((64 * 32 * 256,), float("nan"), device=cuda)
+    ops.conv1_wgrad(obs, dy1, planes, P, 1.0 / 255.0)
+    got = planes[:P * 8192].view(P, 32, 256)
+    go = dy1.float().view(B, 20, 20, 32).permute(0, 3, 1, 2)
+    ref = torch.nn.grad.conv2d_weight(obs.float() / 255.0, (32, 4, 8, 8), go, stride=4).reshape(32, 256)
+    tot = got.sum(0)
+    assert ((tot - ref).norm() / ref.norm()).item() < 1e-4
+    # plane 0 = samples [0, B // P)
+    n0 = B // P
+    if n0:
+        r0 = torch.nn.grad.conv2d_weight(obs[:n0].float() / 255.0, (32, 4, 8, 8), go[:n0], stride=4).reshape(32, 256)
+        torch.testing.assert_close(got[0], r0, rtol=1e-4, atol=1e-4)
+    again = torch.zeros_like(planes)
+    ops.conv1_wgrad(obs, dy1, again, P, 1.0 / 255.0)
+    assert torch.equal(again[:P * 8192], planes[:P * 8192])

@@ -119,6 +119,10 @@ class CNNEngine:
         # of the implicit-im2col GEMM, from this many learner rows up
         self.conv1_wgrad_min_b = int(os.environ.get("ACA_CONV1_WGRAD_MIN_B", "1024"))
         self.conv1_planes = int(os.environ.get("ACA_CONV1_PLANES", "128"))
+        # fused trunk backward as a persistent kernel (weights in registers, one workgroup per CU walking the samples)
+        # from this many learner rows up
+        self.trunk_bwd_persist_min_b = int(os.environ.get("ACA_TRUNK_BWD_PERSIST_MIN_B", "1024"))
+        self.trunk_bwd_persist = int(os.environ.get("ACA_TRUNK_BWD_PERSIST", "256"))
         self._planes = {}
         self._wsplits = {}
         self._cur_planes = {}
@@ -274,6 +278,10 @@ class CNNEngine:
         self._wsplits[name] = S
         self._cur_planes[name] = S
 
+    def _trunk_bwd(self, b):
+        persist = self.trunk_bwd_persist if b.B >= self.trunk_bwd_persist_min_b else 0
+        _native.require().cnn_trunk_bwd(b.dy3, self.sW3, b.y2, self.sW2, b.y1, b.dy2, b.dy1, b.biasp, None, persist)
+
     def _wgrad_conv1(self, b, ws):
         B = b.B
         if not (self.det_wgrad and self.implicit and B >= self.conv1_wgrad_min_b):
@@ -366,7 +374,7 @@ class CNNEngine:
                 G.gemm(b.y3, 3136, False, b.dh, 512, False, self.gWfc, 512, 0, 3136, 512, B, workspace=ws2)
             if stage == "tail":
                 return
-        _native.require().cnn_trunk_bwd(b.dy3, self.sW3, b.y2, self.sW2, b.y1, b.dy2, b.dy1, b.biasp)
+        self._trunk_bwd(b)
         with G.group():   # the longest product (conv1, K = 400 B) first
             self._wgrad_conv1(b, ws)
             self._wgrad("W2", self.gW2, b.dy2, 64, b.y1, 0, 64, 512, B * 81, ws2, [2, B, 32, 20, 20, 4, 4, 2])
@@ -386,7 +394,7 @@ class CNNEngine:
         if self.fused_bwd:
             # dy2 = tconv(dy3, W3) * (y2 > 0) and dy1 = tconv(dy2, W2) * (y1 > 0) in one per-sample launch; the
             # bias-gradient partial rows (db3 | db2 | db1) are reduced by the finaliser
-            _native.require().cnn_trunk_bwd(b.dy3, self.sW3, b.y2, self.sW2, b.y1, b.dy2, b.dy1, b.biasp)
+            self._trunk_bwd(b)
         elif self.tconv_dgrad:   # dy2 = conv_transpose(dy3, W3) * (y2 > 0) as one gathered GEMM (+ colsum -> db2)
             G.gemm(b.dy3, 0, True, self.sW3, 0, False, b.dy2, 64, 1, B * 81, 64, 576, mask=b.y2, ldm=64,
                    colsum=self.gb2, workspace=ws, ga=[3, B, 64, 9, 9, 3, 3, 1], gb=[4, 1, 64, 1, 64, 3, 3, 1])

@@ -102,7 +102,7 @@ hipError_t aca_head_bwd(const float*, const int32_t*, const float*, const float*
                         const uint16_t*, const uint16_t*, uint16_t*, float*, float*, float*, float*, int,
                         uint64_t*, hipStream_t);
 hipError_t aca_cnn_trunk_bwd(const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*,
-                             uint16_t*, uint16_t*, float*, int, uint64_t*, hipStream_t);
+                             uint16_t*, uint16_t*, float*, int, uint64_t*, int, hipStream_t);
 hipError_t aca_cnn_trunk_rows(const uint8_t*, const uint16_t*, const float*, const uint16_t*, const float*,
                               const uint16_t*, const float*, uint16_t*, uint16_t*, uint16_t*, int, float, uint8_t*,
                               uint8_t*, uint64_t*, int, hipStream_t);
@@ -1141,11 +1141,12 @@ void cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tenso
 }
 
 // Fused data-gradient chain dy3 -> dy2 -> dy1 of the Nature-CNN trunk, one workgroup per sample
-// (cnn_fused.hip cnn_trunk_bwd_kernel): dy3 [B*49, 64] (already masked by y3 > 0), W3 [64, 576] / W2 [64, 512]
+// (cnn_fused.hip cnn_trunk_bwd_kernel), or ``persist`` > 0 workgroups walking the samples with the weight fragments
+// held in registers (cnn_trunk_bwd_persist_kernel, bit-identical): dy3 [B*49, 64] (already masked by y3 > 0), W3 [64, 576] / W2 [64, 512]
 // (OHWI bf16 shadows), masks y2 [B*81, 64] / y1 [B*400, 32]; writes dy2, dy1 (masked) and the per-sample bias
 // gradient partials biasp [B, 160] = (sum dy3 | sum dy2 | sum dy1).
 void cnn_trunk_bwd(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tensor dy2, Tensor dy1, Tensor biasp,
-                   c10::optional<Tensor> stamps) {
+                   c10::optional<Tensor> stamps, int64_t persist) {
   for (auto* t : {&dy3, &W3, &y2, &W2, &y1, &dy2, &dy1}) need(*t, at::kBFloat16, "trunk_bwd bf16 operand");
   need(biasp, at::kFloat, "biasp");
   TORCH_CHECK(dy3.numel() % (49 * 64) == 0, "cnn_trunk_bwd: dy3 must be [B*49, 64]");
@@ -1156,7 +1157,7 @@ void cnn_trunk_bwd(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tenso
               "cnn_trunk_bwd: buffers too small");
   check(aca_cnn_trunk_bwd(ptr<uint16_t>(dy3), ptr<uint16_t>(W3), ptr<uint16_t>(y2), ptr<uint16_t>(W2),
                           ptr<uint16_t>(y1), ptr<uint16_t>(dy2), ptr<uint16_t>(dy1), ptr<float>(biasp), (int)B,
-                          stamps_ptr(stamps, B), cur_stream(dy3)),
+                          stamps_ptr(stamps, B), (int)persist, cur_stream(dy3)),
         "cnn_trunk_bwd");
 }
 
@@ -1412,7 +1413,7 @@ TORCH_LIBRARY(acamd, m) {
         "Tensor y2, Tensor y3, float scale, Tensor? shift_out=None, Tensor? stamps=None, int mode=0, "
         "Tensor? copy_out=None) -> ()");
   m.def("cnn_trunk_bwd(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tensor dy2, Tensor dy1, "
-        "Tensor biasp, Tensor? stamps=None) -> ()");
+        "Tensor biasp, Tensor? stamps=None, int persist=0) -> ()");
   m.def("grad_finalize(Tensor jobs, Tensor partial) -> ()");
   m.def("head_bwd(Tensor z, Tensor act, Tensor logp_old, Tensor ent_coef, Tensor kl_coef, float vf_coef, Tensor rew, "
         "Tensor val, Tensor dones, int L, int returns_mode, bool norm_adv, float gamma, float lam, Tensor ret_w, "

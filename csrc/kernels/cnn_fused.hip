@@ -959,6 +959,248 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_kernel(
   }
 }
 
+// Persistent form of the data-gradient chain above for large learner batches (PPO minibatches): one workgroup per
+// CU walks samples b = blockIdx.x, blockIdx.x + gridDim.x, ... The per-sample kernel restages W3 (74 KB) and W2
+// (64 KB) from L2 into LDS for every sample and leaves the CU idle while each sample's operands arrive; here W3's B
+// rows are staged into LDS ONCE and stay resident, and every wave extracts the 8 W2 fragments it uses (its N tile x
+// its parity class's k-steps, 32 registers) once, through a staging pass that aliases the image buffers, and keeps
+// them in registers for all of its samples; the next sample's dy3 image, y2 mask and y1 mask are loaded into
+// registers while the current one is processed. Same MFMA order per sample as the per-sample kernel: bit-identical
+// outputs.
+__global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
+    const u16* __restrict__ dy3g, const u16* __restrict__ W3, const u16* __restrict__ y2g,
+    const u16* __restrict__ W2, const u16* __restrict__ y1g, u16* __restrict__ dy2g, u16* __restrict__ dy1g,
+    float* __restrict__ biasp, int B) {
+  // staging area for the weight fragments (aliases the images: used before the sample loop only)
+  constexpr int STAGE = BW_P3E + BW_M2E + BW_P2E;   // 8712 + 5184 + 8712 u16 = 45 KB
+  __shared__ __attribute__((aligned(16))) u16 s_w3[576 * BW_LD3];   // 81 KB
+  __shared__ __attribute__((aligned(16))) u16 s_img[STAGE];
+  __shared__ float s_red[8 * 128 + 8 * 32];
+  u16* const s_p2i = s_img + BW_P3E + BW_M2E;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int l16 = lane & 15, lg = lane >> 4;
+  const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
+  static_assert(512 * BW_LD2 <= STAGE, "half of the W2 rows fit the staging area");
+
+  // ---- W3 B rows k = (t, o) <- W3[o][t][:], resident in LDS for the whole walk
+  for (int c = tid; c < 576 * 8; c += BW_T) {
+    const int k = c >> 3, part = c & 7, t = k >> 6, o = k & 63;
+    *reinterpret_cast<uint4*>(s_w3 + k * BW_LD3 + part * 8) =
+        *reinterpret_cast<const uint4*>(W3 + o * 576 + t * 64 + part * 8);
+  }
+  // ---- W2 fragments of this wave's (N tile, parity class): rows (t, o) <- W2[o][t][:], staged 512 rows at a time
+  bf16x8 w2f[8];
+  {
+    const int nt = wid & 1, cls = wid >> 1, py = cls >> 1, px = cls & 1;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      for (int c = tid; c < 512 * 4; c += BW_T) {
+        const int row = half * 512 + (c >> 2), part = c & 3, t = row >> 6, o = row & 63;
+        *reinterpret_cast<uint4*>(s_img + (c >> 2) * BW_LD2 + part * 8) =
+            *reinterpret_cast<const uint4*>(W2 + o * 512 + t * 32 + part * 8);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        const int d = ks >> 1, di = d >> 1, dj = d & 1, ob = (ks & 1) * 32;
+        const int tap = (py + 2 * di) * 4 + (px + 2 * dj);
+        if ((tap >> 3) == half) w2f[ks] = tr_frag(s_img + ((tap & 7) * 64 + ob) * BW_LD2, BW_LD2, nt * 16, lane);
+      }
+      __syncthreads();
+    }
+  }
+  // dy2 image border and pad lanes: zero once (the interior is rewritten for every sample, the border never)
+  for (int c = tid; c < BW_P2 * BW_P2 * 9; c += BW_T) {
+    const int px = c / 9, part = c - px * 9, pa = px / BW_P2, pb = px - pa * BW_P2;
+    if (pa == 0 || pb == 0 || pa == BW_P2 - 1 || pb == BW_P2 - 1 || part == 8)
+      *reinterpret_cast<uint4*>(s_p2i + px * BW_LD3 + part * 8) = z4;
+  }
+
+  constexpr int P3_CH = BW_P3 * BW_P3 * 9, P3_PER = (P3_CH + BW_T - 1) / BW_T;   // 1089 -> 3
+  constexpr int M2_CH = 81 * 8, M2_PER = (M2_CH + BW_T - 1) / BW_T;              // 648 -> 2
+  constexpr int M1_CH = 400 * 4, M1_PER = (M1_CH + BW_T - 1) / BW_T;             // 1600 -> 4
+  static_assert(P3_PER == 3 && M2_PER == 2 && M1_PER == 4, "prefetch registers are written out");
+  uint4 vp0, vp1, vp2, vm0, vm1_, m10, m11, m12, m13;   // next sample
+  auto fetch = [&](int b) {
+    uint4 v[3];
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int c = tid + u * BW_T;
+      const int px = c / 9, part = c - px * 9, pa = px / BW_P3, pb = px - pa * BW_P3;
+      const bool in = c < P3_CH && part < 8 && pa >= 2 && pa < 9 && pb >= 2 && pb < 9;
+      const int src = in ? ((b * 49 + (pa - 2) * 7 + (pb - 2)) * 64 + part * 8) : b * 49 * 64;
+      const uint4 x = *reinterpret_cast<const uint4*>(dy3g + src);
+      v[u] = make_uint4(in ? x.x : 0u, in ? x.y : 0u, in ? x.z : 0u, in ? x.w : 0u);
+    }
+    vp0 = v[0]; vp1 = v[1]; vp2 = v[2];
+    vm0 = *reinterpret_cast<const uint4*>(y2g + (size_t)b * 81 * 64 + min(tid, M2_CH - 1) * 8);
+    vm1_ = *reinterpret_cast<const uint4*>(y2g + (size_t)b * 81 * 64 + min(tid + BW_T, M2_CH - 1) * 8);
+    m10 = *reinterpret_cast<const uint4*>(y1g + (size_t)b * 400 * 32 + tid * 8);
+    m11 = *reinterpret_cast<const uint4*>(y1g + (size_t)b * 400 * 32 + (tid + BW_T) * 8);
+    m12 = *reinterpret_cast<const uint4*>(y1g + (size_t)b * 400 * 32 + (tid + 2 * BW_T) * 8);
+    m13 = *reinterpret_cast<const uint4*>(y1g + (size_t)b * 400 * 32 + min(tid + 3 * BW_T, M1_CH - 1) * 8);
+  };
+  if ((int)blockIdx.x < B) fetch(blockIdx.x);
+  for (int b = blockIdx.x; b < B; b += gridDim.x) {
+    // opaque zero (per iteration): keeps the LDS address arithmetic of the unrolled MFMA loops inside the sample
+    // loop -- hoisted out of it, the loop-invariant addresses alone took more registers than the kernel has
+    int z0;
+    asm volatile("s_mov_b32 %0, 0" : "=s"(z0));
+    u16* const s_p3 = s_img + z0;
+    u16* const s_m2 = s_img + BW_P3E + z0;
+    u16* const s_d1 = s_img + z0;
+    u16* const s_p2 = s_img + BW_P3E + BW_M2E + z0;
+    const u16* const s_w3z = s_w3 + z0;
+    const int lane = (threadIdx.x & 63) + z0, l16 = lane & 15, lg = lane >> 4;   // shadow: per-iteration values
+    // ---- this sample's dy3 image + y2 mask to LDS; y1 mask kept in registers; the next sample's loads issued
+    {
+      const uint4 vp[3] = {vp0, vp1, vp2};
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+        const int c = tid + u * BW_T;
+        if (c < P3_CH) *reinterpret_cast<uint4*>(s_p3 + (c / 9) * BW_LD3 + (c % 9) * 8) = vp[u];
+      }
+      *reinterpret_cast<uint4*>(s_m2 + tid * 8) = vm0;
+      if (tid + BW_T < M2_CH) *reinterpret_cast<uint4*>(s_m2 + (tid + BW_T) * 8) = vm1_;
+    }
+    const uint4 vm1[4] = {m10, m11, m12, m13};
+    __syncthreads();
+    if (b + (int)gridDim.x < B) fetch(b + gridDim.x);
+
+    // ---- dy2: wave -> (N tile wid % 4, M tiles 3 x half)
+    {
+      const int n0 = (wid & 3) * 16, mh = (wid >> 2) * 3;
+      floatx4 acc[3];
+#pragma unroll
+      for (int mt = 0; mt < 3; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 18; ++ks) {
+        const int kb = ks * 32 + lg * 8, t = kb >> 6, o0 = kb & 63, ti = t / 3, tj = t - ti * 3;
+        const bf16x8 bw = tr_frag(s_w3z + ks * 32 * BW_LD3, BW_LD3, n0, lane);
+#pragma unroll
+        for (int mt = 0; mt < 3; ++mt) {
+          const int m = min((mh + mt) * 16 + l16, 80);
+          const int a = m / 9, c = m - a * 9;
+          const bf16x8 af =
+              *reinterpret_cast<const bf16x8*>(s_p3 + ((a - ti + 2) * BW_P3 + (c - tj + 2)) * BW_LD3 + o0);
+          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bw, acc[mt], 0, 0, 0);
+        }
+      }
+      const int n = n0 + l16;
+#pragma unroll
+      for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = (mh + mt) * 16 + lg * 4 + r;
+          if (m < 81) {
+            const int a = m / 9, c = m - a * 9;
+            const float v = bf2f(s_m2[m * 64 + n]) > 0.f ? acc[mt][r] : 0.f;
+            s_p2[((a + 1) * BW_P2 + (c + 1)) * BW_LD3 + n] = f2bf(v);
+          }
+        }
+    }
+    float part3[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int c = tid; c < 49 * 8; c += BW_T) {
+      const int px = c >> 3, g = c & 7, pa = px / 7, pb = px - pa * 7;
+      const uint4 v = *reinterpret_cast<const uint4*>(s_p3 + ((pa + 2) * BW_P3 + (pb + 2)) * BW_LD3 + g * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) part3[e] += bf_lane(v, e);
+    }
+    __syncthreads();   // dy2 image complete; the dy3 image and the y2 mask are dead
+
+    // ---- dy2 out (16-byte rows) + db2 / db3 channel sums
+    float part2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int c = tid; c < 81 * 8; c += BW_T) {
+      const int m = c >> 3, g = c & 7, a = m / 9, cc = m - a * 9;
+      const uint4 v = *reinterpret_cast<const uint4*>(s_p2 + ((a + 1) * BW_P2 + (cc + 1)) * BW_LD3 + g * 8);
+      *reinterpret_cast<uint4*>(dy2g + ((size_t)b * 81 + m) * 64 + g * 8) = v;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) part2[e] += bf_lane(v, e);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int o = 8; o < 64; o <<= 1) {
+        part3[e] += __shfl_xor(part3[e], o, 64);
+        part2[e] += __shfl_xor(part2[e], o, 64);
+      }
+    if (lane < 8)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s_red[wid * 128 + lane * 8 + e] = part3[e];
+        s_red[wid * 128 + 64 + lane * 8 + e] = part2[e];
+      }
+
+    // ---- dy1 (sub-pixel): wave -> (N tile wid % 2, parity class wid / 2)
+    {
+      const int nt = wid & 1, cls = wid >> 1, py = cls >> 1, px = cls & 1;
+      floatx4 acc[7];
+#pragma unroll
+      for (int i = 0; i < 7; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        const int d = ks >> 1, di = d >> 1, dj = d & 1, ob = (ks & 1) * 32;
+#pragma unroll
+        for (int i = 0; i < 7; ++i) {
+          const int u = min(i * 16 + l16, 99), yy = u / 10, xx = u - yy * 10;
+          const bf16x8 af = *reinterpret_cast<const bf16x8*>(
+              s_p2 + ((yy - di + 1) * BW_P2 + (xx - dj + 1)) * BW_LD3 + ob + lg * 8);
+          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, w2f[ks], acc[i], 0, 0, 0);
+        }
+      }
+      __syncthreads();   // every wave is past its dy2-image reads of the db sums; s_red rows complete
+      if (tid < 128) {
+        float v = 0.f;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) v += s_red[w * 128 + tid];
+        biasp[(size_t)b * 160 + tid] = v;                      // db3 (0..63) | db2 (64..127)
+      }
+      const int n = nt * 16 + l16;
+#pragma unroll
+      for (int i = 0; i < 7; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int u = i * 16 + lg * 4 + r;
+          if (u < 100) {
+            const int yy = u / 10, xx = u - yy * 10;
+            s_d1[((2 * yy + py) * 20 + 2 * xx + px) * 32 + n] = f2bf(acc[i][r]);
+          }
+        }
+    }
+    __syncthreads();
+    // ---- dy1 out: y1 mask applied, 16-byte stores, db1 partials
+    float part1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int c = tid + u * BW_T;
+      if (c < M1_CH) {
+        uint4 v = *reinterpret_cast<const uint4*>(s_d1 + c * 8);
+        v.x = mask_pair(v.x, vm1[u].x);
+        v.y = mask_pair(v.y, vm1[u].y);
+        v.z = mask_pair(v.z, vm1[u].z);
+        v.w = mask_pair(v.w, vm1[u].w);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) part1[e] += bf_lane(v, e);
+        *reinterpret_cast<uint4*>(dy1g + (size_t)b * 400 * 32 + c * 8) = v;
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int o = 4; o < 64; o <<= 1) part1[e] += __shfl_xor(part1[e], o, 64);
+    if (lane < 4)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s_red[1024 + wid * 32 + lane * 8 + e] = part1[e];
+    __syncthreads();   // also: every s_d1 read is done before the next sample's dy3 image lands on it
+    if (tid < 32) {
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) v += s_red[1024 + w * 32 + tid];
+      biasp[(size_t)b * 160 + 128 + tid] = v;
+    }
+  }
+}
+
 // Bootstrap value V(s_T) straight from the fc partial planes: one wave per env, h = relu(sum planes + bfc)
 // (bf16-rounded like the GEMM epilogue), value = h . Wh[:, A] + bh[A]. Replaces GEMM-reduce + value GEMM.
 __global__ void __launch_bounds__(256) fc_value_kernel(const float* __restrict__ hpart, int S, int64_t plane_stride,
@@ -1020,12 +1262,16 @@ extern "C" hipError_t aca_cnn_trunk_rows(const uint8_t* obs, const uint16_t* W1,
 
 extern "C" hipError_t aca_cnn_trunk_bwd(const uint16_t* dy3, const uint16_t* W3, const uint16_t* y2, const uint16_t* W2,
                                         const uint16_t* y1, uint16_t* dy2, uint16_t* dy1, float* biasp, int B,
-                                        uint64_t* stamps, hipStream_t stream) {
+                                        uint64_t* stamps, int persist, hipStream_t stream) {
   if (B <= 0) return hipSuccess;
   for (const void* p : {(const void*)dy3, (const void*)W3, (const void*)y2, (const void*)W2, (const void*)y1,
                         (const void*)dy2, (const void*)dy1})
     if (reinterpret_cast<uintptr_t>(p) % 16) return hipErrorInvalidValue;
-  aca::cnn_trunk_bwd_kernel<<<B, aca::BW_T, 0, stream>>>(dy3, W3, y2, W2, y1, dy2, dy1, biasp, stamps);
+  if (persist > 0 && !stamps)
+    aca::cnn_trunk_bwd_persist_kernel<<<persist < B ? persist : B, aca::BW_T, 0, stream>>>(dy3, W3, y2, W2, y1, dy2,
+                                                                                             dy1, biasp, B);
+  else
+    aca::cnn_trunk_bwd_kernel<<<B, aca::BW_T, 0, stream>>>(dy3, W3, y2, W2, y1, dy2, dy1, biasp, stamps);
   return hipGetLastError();
 }
 

@@ -79,6 +79,16 @@ def test_trunk_bwd_matches_conv_transpose(cuda, B):
                       dev[3].reshape(64, 512), dev[4].reshape(B * 400, 32), dy2, dy1, bp)
     torch.cuda.synchronize()
     assert torch.equal(dy1b.view(torch.int16), dy1.view(torch.int16)) and torch.equal(bpb, bp)
+    # the persistent form (weights staged once, workgroups walking the samples) is bit-identical
+    dy2b = dy2.clone()
+    for persist in (3, 256):
+        dy2.fill_(float("nan")), dy1.fill_(float("nan")), bp.fill_(float("nan"))
+        ops.cnn_trunk_bwd(dev[0].reshape(B * 49, 64), dev[1].reshape(64, 576), dev[2].reshape(B * 81, 64),
+                          dev[3].reshape(64, 512), dev[4].reshape(B * 400, 32), dy2, dy1, bp, None, persist)
+        torch.cuda.synchronize()
+        assert torch.equal(dy2b.view(torch.int16), dy2.view(torch.int16)), persist
+        assert torch.equal(dy1b.view(torch.int16), dy1.view(torch.int16)), persist
+        assert torch.equal(bpb, bp), persist
 
 
 def _one_update(fused, algo="pong_a2c", head=True, **kw):

@@ -119,6 +119,9 @@ class CNNEngine:
         # of the implicit-im2col GEMM, from this many learner rows up
         self.conv1_wgrad_min_b = int(os.environ.get("ACA_CONV1_WGRAD_MIN_B", "1024"))
         self.conv1_planes = int(os.environ.get("ACA_CONV1_PLANES", "128"))
+        # conv2 / conv3 weight gradients by the per-sample NHWC kernel (conv_wgrad.hip) from this many rows up
+        self.nhwc_wgrad_min_b = int(os.environ.get("ACA_NHWC_WGRAD_MIN_B", "1024"))
+        self.nhwc_planes = int(os.environ.get("ACA_NHWC_PLANES", "64"))
         # fused trunk backward as a persistent kernel (weights in registers, one workgroup per CU walking the samples)
         # from this many learner rows up
         self.trunk_bwd_persist_min_b = int(os.environ.get("ACA_TRUNK_BWD_PERSIST_MIN_B", "1024"))
@@ -282,6 +285,27 @@ class CNNEngine:
         persist = self.trunk_bwd_persist if b.B >= self.trunk_bwd_persist_min_b else 0
         _native.require().cnn_trunk_bwd(b.dy3, self.sW3, b.y2, self.sW2, b.y1, b.dy2, b.dy1, b.biasp, None, persist)
 
+    def _wgrad_conv23(self, name, b, ws2):
+        B = b.B
+        if not (self.det_wgrad and self.implicit and B >= self.nhwc_wgrad_min_b):
+            if name == "W2":
+                self._wgrad("W2", self.gW2, b.dy2, 64, b.y1, 0, 64, 512, B * 81, ws2, [2, B, 32, 20, 20, 4, 4, 2])
+            else:
+                self._wgrad("W3", self.gW3, b.dy3, 64, b.y2, 0, 64, 576, B * 49, ws2, [2, B, 64, 9, 9, 3, 3, 1])
+            return
+        n = 512 if name == "W2" else 576
+        P = max(1, min(self.nhwc_planes, B))
+        buf = self._planes.get(name)
+        if buf is None or buf.numel() < P * 64 * n:
+            buf = torch.zeros(max(P, self.wgrad_planes) * 64 * n, dtype=torch.float32, device=self.dev)
+            self._planes[name] = buf
+        if name == "W2":
+            _native.require().conv_wgrad_nhwc(2, b.y1, b.dy2, buf, P)
+        else:
+            _native.require().conv_wgrad_nhwc(3, b.y2, b.dy3, buf, P)
+        self._wsplits[name] = P
+        self._cur_planes[name] = P
+
     def _wgrad_conv1(self, b, ws):
         B = b.B
         if not (self.det_wgrad and self.implicit and B >= self.conv1_wgrad_min_b):
@@ -377,8 +401,8 @@ class CNNEngine:
         self._trunk_bwd(b)
         with G.group():   # the longest product (conv1, K = 400 B) first
             self._wgrad_conv1(b, ws)
-            self._wgrad("W2", self.gW2, b.dy2, 64, b.y1, 0, 64, 512, B * 81, ws2, [2, B, 32, 20, 20, 4, 4, 2])
-            self._wgrad("W3", self.gW3, b.dy3, 64, b.y2, 0, 64, 576, B * 49, ws2, [2, B, 64, 9, 9, 3, 3, 1])
+            self._wgrad_conv23("W2", b, ws2)
+            self._wgrad_conv23("W3", b, ws2)
         self.finalize(b)
 
     def _backward_trunk(self, b, main, side, ev, ws, ws2):
@@ -388,7 +412,7 @@ class CNNEngine:
         side.wait_event(ev[2])
         with torch.cuda.stream(side):   # conv3 weight gradient
             if imp:
-                self._wgrad("W3", self.gW3, b.dy3, 64, b.y2, 0, 64, 576, B * 49, ws2, [2, B, 64, 9, 9, 3, 3, 1])
+                self._wgrad_conv23("W3", b, ws2)
             else:
                 G.gemm(b.dy3, 64, False, b.col3, 576, False, self.gW3, 576, 2, 64, 576, B * 49, workspace=ws2)
         if self.fused_bwd:
@@ -405,7 +429,7 @@ class CNNEngine:
         side.wait_event(ev[3])
         with torch.cuda.stream(side):   # conv2 weight gradient
             if imp:
-                self._wgrad("W2", self.gW2, b.dy2, 64, b.y1, 0, 64, 512, B * 81, ws2, [2, B, 32, 20, 20, 4, 4, 2])
+                self._wgrad_conv23("W2", b, ws2)
             else:
                 G.gemm(b.dy2, 64, False, b.col2, 512, False, self.gW2, 512, 2, 64, 512, B * 81, workspace=ws2)
         if self.fused_bwd:

@@ -180,6 +180,134 @@ __global__ void __launch_bounds__(CW_T) conv1_wgrad_kernel(const uint8_t* __rest
   }
 }
 
+
+// ------------------------------------------------------------------------------------------------------------
+// Per-sample weight gradient of a bf16 NHWC conv layer (conv2: y1 [20][20][32] -> 9x9, 4x4 stride 2; conv3: y2
+// [9][9][64] -> 7x7, 3x3 stride 1; 64 output channels, OHWI weights [64][KS KS C]), same scheme as conv1 above:
+//   dW[o][(ky, kx, c)] = sum_b sum_p dy[b][p][o] * img[b][S oy + ky][S ox + kx][c]
+// Workgroup (g, ky) owns kernel row ky (KS C columns) of plane g's samples; per sample the image and the dy rows
+// are staged in LDS once, A fragments are the dy rows (transposing reads, positions = K), and each lane points its
+// B-fragment transposing read at the 4 contiguous channels c0..c0+3 of pixel (S oy + ky, S ox + kx) of its
+// position -- no im2col. Wave w owns column tiles w, w + 8, ... and all four 16-channel output tiles, so the
+// waves' outputs are disjoint (no cross-wave reduction). Two samples in flight in registers.
+template <int H, int W, int C, int KS, int S, int OH, int OW>
+__global__ void __launch_bounds__(512) conv_wgrad_nhwc_kernel(const u16* __restrict__ img,
+                                                              const u16* __restrict__ dy,
+                                                              float* __restrict__ planes, int B, int P) {
+  constexpr int T = 512;
+  constexpr int NPOS = OH * OW, KSTEPS = (NPOS + 31) / 32, KPOS = KSTEPS * 32;
+  constexpr int NCOL = KS * KS * C, SLICE = KS * C, NT = SLICE / 16;
+  constexpr int LDI = C + 8, LDD = 72;
+  constexpr int IMG4 = H * W * C / 8, DY4 = NPOS * 8;          // 16-byte chunks per sample
+  constexpr int IPER = (IMG4 + T - 1) / T, DPER = (DY4 + T - 1) / T;
+  constexpr int NTW = (NT + 7) / 8;                            // column tiles per wave (at most)
+  static_assert(SLICE % 16 == 0 && C % 4 == 0, "tile shapes");
+  __shared__ __attribute__((aligned(16))) u16 s_img[H * W * LDI + 8];
+  __shared__ __attribute__((aligned(16))) u16 s_dy[KPOS * LDD];
+  const int g = blockIdx.x % P, ky = blockIdx.x / P;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int b0 = (int)((int64_t)g * B / P), b1 = (int)((int64_t)(g + 1) * B / P);
+  const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
+  for (int c = tid; c < (KPOS - NPOS) * (LDD / 8); c += T)
+    *reinterpret_cast<uint4*>(s_dy + NPOS * LDD + c * 8) = z4;
+  if (tid == 0) *reinterpret_cast<uint4*>(s_img + H * W * LDI) = z4;
+
+  // two register sets of up to 4 image + 2 dy chunks per thread, written out as named variables (private arrays
+  // here stayed in scratch)
+  static_assert(IPER <= 4 && DPER <= 2, "register sets hold 4 image + 2 dy chunks per thread");
+  uint4 ra0, ra1, ra2, ra3, ra4, ra5, rb0, rb1, rb2, rb3, rb4, rb5;
+#define CWN_LD1(R, k, base, lim, u) if ((u) < (lim##PER)) R##k = base[min(tid + (u) * T, lim##4 - 1)];
+#define CWN_LOAD(R, b)                                                                                   \
+  {                                                                                                      \
+    const uint4* ip = reinterpret_cast<const uint4*>(img + (size_t)(b) * H * W * C);                     \
+    const uint4* dp = reinterpret_cast<const uint4*>(dy + (size_t)(b) * NPOS * 64);                      \
+    if (0 < IPER) R##0 = ip[min(tid, IMG4 - 1)];                                                         \
+    if (1 < IPER) R##1 = ip[min(tid + T, IMG4 - 1)];                                                     \
+    if (2 < IPER) R##2 = ip[min(tid + 2 * T, IMG4 - 1)];                                                 \
+    if (3 < IPER) R##3 = ip[min(tid + 3 * T, IMG4 - 1)];                                                 \
+    if (0 < DPER) R##4 = dp[min(tid, DY4 - 1)];                                                          \
+    if (1 < DPER) R##5 = dp[min(tid + T, DY4 - 1)];                                                      \
+  }
+#define CWN_ST_I(v, u)                                                                                   \
+  if ((u) < IPER && tid + (u) * T < IMG4) {                                                              \
+    const int c = tid + (u) * T;                                                                         \
+    *reinterpret_cast<uint4*>(s_img + (c / (C / 8)) * LDI + (c % (C / 8)) * 8) = (v);                    \
+  }
+#define CWN_ST_D(v, u)                                                                                   \
+  if ((u) < DPER && tid + (u) * T < DY4) {                                                               \
+    const int c = tid + (u) * T;                                                                         \
+    *reinterpret_cast<uint4*>(s_dy + (c >> 3) * LDD + (c & 7) * 8) = (v);                                \
+  }
+#define CWN_STORE(R)                                                                                     \
+  {                                                                                                      \
+    CWN_ST_I(R##0, 0) CWN_ST_I(R##1, 1) CWN_ST_I(R##2, 2) CWN_ST_I(R##3, 3)                              \
+    CWN_ST_D(R##4, 0) CWN_ST_D(R##5, 1)                                                                  \
+  }
+  floatx4 acc[NTW][4];
+#pragma unroll
+  for (int j = 0; j < NTW; ++j)
+#pragma unroll
+    for (int m = 0; m < 4; ++m) acc[j][m] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int lr16 = lane & 15, lg = lane >> 4, q = lr16 >> 2, pq = lr16 & 3;
+#define CWN_SAMPLE()                                                                                     \
+  {                                                                                                      \
+    _Pragma("unroll") for (int ks = 0; ks < KSTEPS; ++ks) {                                              \
+      bf16x8 af[4];                                                                                      \
+      _Pragma("unroll") for (int m = 0; m < 4; ++m) af[m] = cw_tr_frag(s_dy + ks * 32 * LDD, LDD, m * 16, lane); \
+      const int pa = ks * 32 + lg * 8 + q, pb = pa + 4;                                                  \
+      const int oya = pa / OW, oyb = pb / OW;                                                            \
+      const int ba = (S * oya + ky) * W + S * (pa - oya * OW), bb = (S * oyb + ky) * W + S * (pb - oyb * OW); \
+      _Pragma("unroll") for (int j = 0; j < NTW; ++j) {                                                  \
+        const int nt = wid + 8 * j;                                                                      \
+        if (nt < NT) {                                                                                   \
+          const int n = nt * 16 + 4 * pq, kx = n / C, c0 = n - kx * C;                                   \
+          const int offa = pa < NPOS ? (ba + kx) * LDI + c0 : H * W * LDI;                               \
+          const int offb = pb < NPOS ? (bb + kx) * LDI + c0 : H * W * LDI;                               \
+          typedef short short4x __attribute__((ext_vector_type(4)));                                     \
+          typedef __attribute__((address_space(3))) short4x lds4;                                        \
+          const short4x lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(s_img + offa));             \
+          const short4x hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(s_img + offb));             \
+          const cw_short8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};                   \
+          const bf16x8 bf = __builtin_bit_cast(bf16x8, v);                                               \
+          _Pragma("unroll") for (int m = 0; m < 4; ++m)                                                  \
+            acc[j][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bf, acc[j][m], 0, 0, 0);          \
+        }                                                                                                \
+      }                                                                                                  \
+    }                                                                                                    \
+    __syncthreads();                                                                                     \
+  }
+  if (b0 < b1) CWN_LOAD(ra, b0)
+  if (b0 + 1 < b1) CWN_LOAD(rb, b0 + 1)
+  for (int b = b0; b < b1; b += 2) {
+    CWN_STORE(ra)
+    __syncthreads();
+    if (b + 2 < b1) CWN_LOAD(ra, b + 2)
+    CWN_SAMPLE()
+    if (b + 1 >= b1) break;
+    CWN_STORE(rb)
+    __syncthreads();
+    if (b + 3 < b1) CWN_LOAD(rb, b + 3)
+    CWN_SAMPLE()
+  }
+#undef CWN_LD1
+#undef CWN_LOAD
+#undef CWN_ST_I
+#undef CWN_ST_D
+#undef CWN_STORE
+#undef CWN_SAMPLE
+  float* dst = planes + (size_t)g * 64 * NCOL;
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) {
+    const int nt = wid + 8 * j;
+    if (nt < NT)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          dst[(size_t)(m * 16 + 4 * lg + i) * NCOL + ky * SLICE + nt * 16 + lr16] = acc[j][m][i];
+  }
+}
+
 }  // namespace aca
 
 // obs uint8 [B][4][84][84], dy1 bf16 [B][400][32] -> planes fp32 [P][32][256] (plane g: samples
@@ -189,5 +317,20 @@ extern "C" hipError_t aca_conv1_wgrad(const uint8_t* obs, const uint16_t* dy1, f
   if (B <= 0) return hipSuccess;
   if (P < 1 || P > 1024) return hipErrorInvalidValue;
   aca::conv1_wgrad_kernel<<<4 * P, aca::CW_T, 0, stream>>>(obs, dy1, planes, B, P, scale);
+  return hipGetLastError();
+}
+
+// conv2 (layer 2: y1 [B][20][20][32] -> dy2 [B][81][64], W2 [64][512]) / conv3 (layer 3: y2 [B][9][9][64] -> dy3
+// [B][49][64], W3 [64][576]) weight gradient as P partial planes; grid KS P (workgroup (g, ky)).
+extern "C" hipError_t aca_conv_wgrad_nhwc(int layer, const uint16_t* img, const uint16_t* dy, float* planes, int B,
+                                          int P, hipStream_t stream) {
+  if (B <= 0) return hipSuccess;
+  if (P < 1 || P > 1024) return hipErrorInvalidValue;
+  if (layer == 2)
+    aca::conv_wgrad_nhwc_kernel<20, 20, 32, 4, 2, 9, 9><<<4 * P, 512, 0, stream>>>(img, dy, planes, B, P);
+  else if (layer == 3)
+    aca::conv_wgrad_nhwc_kernel<9, 9, 64, 3, 1, 7, 7><<<3 * P, 512, 0, stream>>>(img, dy, planes, B, P);
+  else
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }

@@ -369,3 +369,26 @@ def test_conv1_wgrad_planes_match_autograd(cuda, B, P):
     again = torch.zeros_like(planes)
     ops.conv1_wgrad(obs, dy1, again, P, 1.0 / 255.0)
     assert torch.equal(again[:P * 8192], planes[:P * 8192])
+
+
+@pytest.mark.parametrize("layer,B,P", [(2, 5, 3), (2, 300, 64), (3, 9, 4), (3, 300, 64)])
+def test_conv_wgrad_nhwc_planes_match_autograd(cuda, layer, B, P):
+    """Per-sample conv2 / conv3 weight gradient (conv_wgrad.hip, no im2col): the plane sum == the fp32 autograd conv
+    weight gradient (OHWI layout), and two runs are bit-identical."""
+    from actor_critic_algs_on_tensorflow_amd import _native
+    ops = _native.require()
+    H, C, KS, S, OH = (20, 32, 4, 2, 9) if layer == 2 else (9, 64, 3, 1, 7)
+    g = torch.Generator(device="cpu").manual_seed(B + layer)
+    img = torch.rand(B, H, H, C, generator=g).to(torch.bfloat16).to(cuda)
+    dy = (torch.randn(B, OH, OH, 64, generator=g) * 0.1).to(torch.bfloat16).to(cuda)
+    n = KS * KS * C
+    planes = torch.full((P * 64 * n,), float("nan"), device=cuda)
+    ops.conv_wgrad_nhwc(layer, img.view(B * H * H, C), dy.view(B * OH * OH, 64), planes, P)
+    ref = torch.nn.grad.conv2d_weight(img.float().permute(0, 3, 1, 2), (64, C, KS, KS), dy.float().permute(0, 3, 1, 2),
+                                      stride=S)
+    ref = ref.permute(0, 2, 3, 1).reshape(64, n)
+    tot = planes.view(P, 64, n).sum(0)
+    assert ((tot - ref).norm() / ref.norm()).item() < 1e-4
+    again = torch.zeros_like(planes)
+    ops.conv_wgrad_nhwc(layer, img.view(B * H * H, C), dy.view(B * OH * OH, 64), again, P)
+    assert torch.equal(again, planes)

@@ -164,7 +164,8 @@ class MLPEngine:
 
     def _fwd(self, mode, obs, B, tw_base=0, ntw=2, desc_B=None, idx=None, perm=None, tg=None, env_ids=None, key_shift=0,
              seed=0, act_out=None, logp_out=None, ent_out=None, v_out=None, act_in=None, logp_old=None, adv=None,
-             ret=None, v_old=None, ent_coef=None, kl_coef=None, vf_coef=1.0, ppo_clip=0.0, v_clip=0.0, ppo=False):
+             ret=None, v_old=None, ent_coef=None, kl_coef=None, vf_coef=1.0, ppo_clip=0.0, v_clip=0.0, ppo=False,
+             stamps=None):
         ops = _native.require()
         desc, _ = self.desc(desc_B)
         obs2 = obs.reshape(obs.shape[0], -1)
@@ -174,7 +175,7 @@ class MLPEngine:
                     self.log_std, self.ac_scale, tg, env_ids, key_shift, seed, act_out, logp_out, ent_out, v_out,
                     act_in, logp_old, adv, ret, v_old, ent_coef, kl_coef, float(vf_coef), float(ppo_clip),
                     float(v_clip or 0.0), bool(ppo), self.g_log_std if mode == 2 else None,
-                    self.mstats if mode == 2 else None, self._mpart(B) if mode == 2 else None)
+                    self.mstats if mode == 2 else None, self._mpart(B) if mode == 2 else None, stamps)
 
     # ------------------------------------------------------------------------------------------- API
     def policy_step(self, obs, act_out, logp_out, ent_out, v_out, tg, env_ids, key_shift, seed):
@@ -192,7 +193,7 @@ class MLPEngine:
 
     def train(self, obs, actions, logp_old, adv, ret, ent_coef, kl_coef, B, idx=None, v_old=None, vf_coef=1.0,
               ppo=False, ppo_clip=0.0, v_clip=0.0, stats=None, clips=(None, None), want_parts=True, perm=None,
-              bump=None):
+              bump=None, stamps=None):
         """One learner (mini)batch: rows ``idx`` / ``perm`` = (update_counter, epoch, offset, n, seed) -- the rows
         ``prp(offset + r)`` of the keyed permutation of ``[0, n)`` (envs/rng.py), computed in-kernel -- or the first
         ``B`` rows of the rollout -> gradients in the slab, statistics into ``stats[0:7]``, sums of squares into
@@ -201,7 +202,7 @@ class MLPEngine:
         ops = _native.require()
         self._fwd(2, obs, B, 0, 2, desc_B=B, idx=idx, perm=perm, act_in=actions, logp_old=logp_old, adv=adv, ret=ret,
                   v_old=v_old, ent_coef=ent_coef, kl_coef=kl_coef, vf_coef=vf_coef, ppo_clip=ppo_clip,
-                  v_clip=v_clip, ppo=ppo)
+                  v_clip=v_clip, ppo=ppo, stamps=stamps)
         desc, _ = self.desc(B)
         nsplit = max(1, min(16, B // 2048))
         use_parts = want_parts and nsplit == 1

@@ -684,7 +684,7 @@ void mlp_fwd(Tensor desc, int64_t tw_base, int64_t ntw, int64_t mode, int64_t ld
              c10::optional<Tensor> logp_old, c10::optional<Tensor> adv, c10::optional<Tensor> ret,
              c10::optional<Tensor> v_old, c10::optional<Tensor> ent_coef, c10::optional<Tensor> kl_coef,
              double vf_coef, double ppo_clip, double v_clip, bool ppo, c10::optional<Tensor> g_log_std,
-             c10::optional<Tensor> mstats, c10::optional<Tensor> mpart) {
+             c10::optional<Tensor> mstats, c10::optional<Tensor> mpart, c10::optional<Tensor> stamps) {
   need(desc, at::kLong, "desc");
   TORCH_CHECK(desc.numel() * 8 >= (int64_t)(2 * sizeof(aca::MlpTower)), "mlp_fwd: desc too small");
   TORCH_CHECK(obs.is_cuda() && obs.scalar_type() == at::kFloat && obs.dim() == 2 && obs.stride(1) == 1,
@@ -742,6 +742,7 @@ void mlp_fwd(Tensor desc, int64_t tw_base, int64_t ntw, int64_t mode, int64_t ld
   if (a.mpart) TORCH_CHECK(mode == 2 && mpart->numel() >= (B + 15) / 16 * aca::MPART_W,
                            "mlp_fwd: mpart must hold ceil(B/16) rows of ", aca::MPART_W, " (train mode)");
   a.inv_B = B > 0 ? 1.0f / (float)B : 0.f;
+  a.stamps = reinterpret_cast<int64_t*>(stamps_ptr(stamps, 2));   // [2 towers][16 phases]
   const bool policy = tw_base == 0;
   if (policy) {
     TORCH_CHECK(head == 1 || head == 2, "mlp_fwd: policy tower needs head 1 (categorical) or 2 (gaussian)");
@@ -1415,7 +1416,7 @@ TORCH_LIBRARY(acamd, m) {
         "int A, Tensor? log_std, Tensor? ac_scale, Tensor? tg, Tensor? env_ids, int key_shift, int seed, "
         "Tensor? act_out, Tensor? logp_out, Tensor? ent_out, Tensor? v_out, Tensor? act_in, Tensor? logp_old, "
         "Tensor? adv, Tensor? ret, Tensor? v_old, Tensor? ent_coef, Tensor? kl_coef, float vf_coef, float ppo_clip, "
-        "float v_clip, bool ppo, Tensor? g_log_std, Tensor? mstats, Tensor? mpart=None) -> ()");
+        "float v_clip, bool ppo, Tensor? g_log_std, Tensor? mstats, Tensor? mpart=None, Tensor? stamps=None) -> ()");
   m.def("mlp_wgrad(Tensor desc, int ntw, int B, int nsplit, int items0, int items1, Tensor? parts0, "
         "Tensor? parts1, float clip0, float clip1, Tensor? g_log_std, int A, Tensor? mstats, Tensor? stats, "
         "Tensor? ent_coef, Tensor? kl_coef, Tensor? mpart=None, int mpart_rows=0, Tensor? bump=None) -> ()");

@@ -219,6 +219,15 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
   const int nl = (int)T.nl;
   const int row0 = blockIdx.x * MLP_BM;
   const int rows = min(MLP_BM, a.B - row0);
+  // diagnostics: s_memrealtime (100 MHz) at phase ends, thread 0 of workgroup (0, tower) after the barrier; slots 12
+  // and 13 hold s_memtime (shader clock) at the ends of the input tile and of the data-gradient chain
+  auto stamp = [&](int slot) {
+    if (a.stamps && blockIdx.x == 0 && threadIdx.x == 0) a.stamps[blockIdx.y * 16 + slot] = __builtin_amdgcn_s_memrealtime();
+  };
+  auto cstamp = [&](int slot) {
+    if (a.stamps && blockIdx.x == 0 && threadIdx.x == 0) a.stamps[blockIdx.y * 16 + slot] = __builtin_amdgcn_s_memtime();
+  };
+  stamp(0);
   // ---- LDS layout: X0 | Y_0 .. Y_{nl-1} | dP ping-pong (train)
   const int ld0 = ld_of(a.D);
   // (offsets recomputed from the descriptor rather than kept in per-layer pointer arrays: a runtime-indexed array
@@ -244,6 +253,7 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
     s_grow[threadIdx.x] = g;
   }
   __syncthreads();
+  stamp(1);
   // ---- input tile (gathered rows; padded rows / columns are zero)
   for (int e = threadIdx.x; e < MLP_BM * ld0; e += MLP_THREADS) {
     const int r = e / ld0, c = e - r * ld0;
@@ -253,6 +263,8 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
     if (a.mode == 2 && r < rows && c < a.D) P_<float>(T.xs[0])[(size_t)(row0 + r) * a.D + c] = v;
   }
   __syncthreads();
+  stamp(2);
+  cstamp(12);
   // ---- forward
   const float* X = X0;
   int ldx = ld0;
@@ -262,6 +274,7 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
     layer_fwd(X, ldx, (int)T.in[l], P_<const float>(T.Wt[l]), P_<const float>(T.b[l]), (int)T.out[l], (int)T.act[l],
               Yl, ldl);
     __syncthreads();
+    stamp(3 + l);
     if (a.mode == 2 && l + 1 < nl) {   // inputs of layer l+1 for its weight gradient
       const int w = (int)T.out[l];
       gf32* xs = P_<float>(T.xs[l + 1]);
@@ -451,6 +464,7 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
   }
   if (a.mode != 2) return;
   __syncthreads();
+  stamp(8);
   if (gauss) {   // phase C: d(loss)/d(pre-tanh mean) and the per-row log-std gradient terms, per component
     if (tid < MLP_BM * MLP_MAXA) {
       const int r = tid / MLP_MAXA, j = tid % MLP_MAXA;
@@ -475,6 +489,7 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
     if (a.mpart) a.mpart[(size_t)blockIdx.x * MPART_W + 8 + threadIdx.x] = s;
     else atomicAdd(&a.g_log_std[threadIdx.x], s);
   }
+  stamp(14);   // head phase C + log-std sums (the data-gradient layers take slots 9 ..)
   // ---- top layer dP: apply the head activation derivative (tanh applied above) and publish
   {
     const int w = (int)T.out[L];
@@ -493,10 +508,12 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
     gcf32* W = P_<const float>(T.W[l]);
     layer_dgrad(cur, ldP, N, W, K, Yp(l - 1), ldyf(l - 1), (int)T.act[l - 1], nxt, ldP, gdst, rows);
     __syncthreads();
+    stamp(9 + L - l);
     float* tmp = cur;
     cur = nxt;
     nxt = tmp;
   }
+  cstamp(13);
 }
 
 // ------------------------------------------------------------------------------------------------ weight grads

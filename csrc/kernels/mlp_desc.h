@@ -48,6 +48,7 @@ struct MlpArgs {
   float* mstats;              // [8] sums (atomics): pg, kl, ent, vloss, clipfrac, -, ratio
   float* mpart;               // optional [ceil(B/16)][MPART_W]: per-workgroup partials instead of the atomics above
   float inv_B;
+  int64_t* stamps;            // optional diagnostics: [2 towers][16] s_memrealtime at phase ends of workgroup (0, tower)
 };
 
 struct WgradArgs {

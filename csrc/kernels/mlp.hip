@@ -715,10 +715,12 @@ __device__ __forceinline__ float lin_reset(float u) {
 // columns land 4 banks apart, so a 16-byte fragment read is conflict-free). No global memory at all.
 template <int NG>
 __device__ void layer_fwd_lds_t(const float* __restrict__ X, int ldx, const float* __restrict__ W, int ldw,
-                                const float* __restrict__ bias, int N, int act, float* __restrict__ Y, int ldy) {
+                                const float* __restrict__ bias, int N, int act, float* __restrict__ Y, int ldy,
+                                int64_t* dbg) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 15, q = lane >> 4;
   const int ntile = ngp2(N);
+  if (dbg && lane == 0) dbg[wave * 8 + 0] = __builtin_amdgcn_s_memtime();
   for (int tile = wave; tile < ntile; tile += MLP_THREADS / 64) {
     const int c = tile * 16 + r;
     const bool cok = c < N;
@@ -739,20 +741,25 @@ __device__ void layer_fwd_lds_t(const float* __restrict__ X, int ldx, const floa
     }
     const float bb = bias[cc];
     const float slope = act_slope(act);
+    if (dbg && lane == 0) dbg[wave * 8 + 1] = __builtin_amdgcn_s_memtime();
 #pragma unroll
     for (int i = 0; i < 4; ++i) Y[(4 * q + i) * ldy + c] = cok ? act_fwd(acc[i] + bb, slope) : 0.f;
+    if (dbg && lane == 0) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the epilogue's LDS stores (and so the MFMA results) done
+      dbg[wave * 8 + 2] = __builtin_amdgcn_s_memtime();
+    }
   }
 }
 
 __device__ __forceinline__ void layer_fwd_lds(const float* X, int ldx, int K, const float* W, const float* bias, int N,
-                                              int act, float* Y, int ldy) {
+                                              int act, float* Y, int ldy, int64_t* dbg = nullptr) {
   const int ldw = 16 * ngp2(K) + 4;
   switch (ngp2(K)) {
-    case 1: layer_fwd_lds_t<1>(X, ldx, W, ldw, bias, N, act, Y, ldy); break;
-    case 2: layer_fwd_lds_t<2>(X, ldx, W, ldw, bias, N, act, Y, ldy); break;
-    case 4: layer_fwd_lds_t<4>(X, ldx, W, ldw, bias, N, act, Y, ldy); break;
-    case 8: layer_fwd_lds_t<8>(X, ldx, W, ldw, bias, N, act, Y, ldy); break;
-    default: layer_fwd_lds_t<16>(X, ldx, W, ldw, bias, N, act, Y, ldy); break;
+    case 1: layer_fwd_lds_t<1>(X, ldx, W, ldw, bias, N, act, Y, ldy, dbg); break;
+    case 2: layer_fwd_lds_t<2>(X, ldx, W, ldw, bias, N, act, Y, ldy, dbg); break;
+    case 4: layer_fwd_lds_t<4>(X, ldx, W, ldw, bias, N, act, Y, ldy, dbg); break;
+    case 8: layer_fwd_lds_t<8>(X, ldx, W, ldw, bias, N, act, Y, ldy, dbg); break;
+    default: layer_fwd_lds_t<16>(X, ldx, W, ldw, bias, N, act, Y, ldy, dbg); break;
   }
 }
 
@@ -857,7 +864,14 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_rollout_kernel(RolloutArgs a)
       const int ldl = ldyf(l);
       if (WLDS) {
         const float* w = Wl(l);
-        layer_fwd_lds(X, ldx, s_in[l], w, w + s_out[l] * (16 * ngp2(s_in[l]) + 4), s_out[l], s_actc[l], Yl, ldl);
+        // diagnostics: per-wave shader-clock stamps inside layer 1 of step 5 (entry, MFMAs issued, epilogue landed,
+        // after the barrier) at stamps[128 + wave * 8 + k]
+        int64_t* dbg = (a.stamps && blockIdx.x == 0 && step == 5 && l == 1) ? a.stamps + 128 : nullptr;
+        layer_fwd_lds(X, ldx, s_in[l], w, w + s_out[l] * (16 * ngp2(s_in[l]) + 4), s_out[l], s_actc[l], Yl, ldl, dbg);
+        if (dbg) {
+          __syncthreads();
+          if ((threadIdx.x & 63) == 0) dbg[(threadIdx.x >> 6) * 8 + 3] = __builtin_amdgcn_s_memtime();
+        }
       } else {
         layer_fwd(X, ldx, s_in[l], P_<const float>(s_wt[l]), P_<const float>(s_b[l]), s_out[l], s_actc[l], Yl, ldl);
       }

@@ -17,7 +17,7 @@ def main():
                  cuda_graph=False)
     tr = ActorCriticTrainer(cfg)
     eng, st, env = tr.mlp, tr.storage, tr.env
-    stamps = torch.zeros(16 * 8, dtype=torch.int64, device="cuda:0")
+    stamps = torch.zeros(16 * 8 + 64, dtype=torch.int64, device="cuda:0")
     out = {"wlds": eng.rollout_weights_in_lds(), "T": st.T, "N": env.num_envs}
     for rep in range(3):
         torch.cuda.synchronize()
@@ -25,7 +25,11 @@ def main():
         eng.rollout_linear(env, st, KEY_ENV_BITS, tr.policy_seed, stamps=stamps)
         torch.cuda.synchronize()
         out[f"host_ms_{rep}"] = round((time.perf_counter() - t0) * 1e3, 3)
-    s = stamps.view(16, 8).cpu().tolist()
+    allst = stamps.cpu().tolist()
+    s = [allst[8 * k:8 * k + 8] for k in range(16)]
+    d = [allst[128 + 8 * w:128 + 8 * w + 4] for w in range(8)]
+    t0c = min(x[0] for x in d if x[0])
+    out["layer1_step5_wave_cycles"] = {f"w{w}": [x[k] - t0c if x[k] else None for k in range(4)] for w, x in enumerate(d)}
     names = ["layer0", "layer1", "layer2", "layer3", "-", "head", "env"]
     ph = {n: [] for n in names if n != "-"}
     for k in range(1, 16):

@@ -121,7 +121,10 @@ class CNNEngine:
         self.conv1_planes = int(os.environ.get("ACA_CONV1_PLANES", "128"))
         # conv2 / conv3 weight gradients by the per-sample NHWC kernel (conv_wgrad.hip) from this many rows up
         self.nhwc_wgrad_min_b = int(os.environ.get("ACA_NHWC_WGRAD_MIN_B", "1024"))
-        self.nhwc_planes = int(os.environ.get("ACA_NHWC_PLANES", "64"))
+        self.nhwc_planes = int(os.environ.get("ACA_NHWC_PLANES", "128"))
+        # conv3's per-sample work is small (2 k-steps x 12 column tiles), so its grid (3 workgroups per plane) needs
+        # more planes than conv2 to cover the CUs
+        self.nhwc3_planes = int(os.environ.get("ACA_NHWC3_PLANES", "256"))
         # fused trunk backward as a persistent kernel (weights in registers, one workgroup per CU walking the samples)
         # from this many learner rows up
         self.trunk_bwd_persist_min_b = int(os.environ.get("ACA_TRUNK_BWD_PERSIST_MIN_B", "1024"))
@@ -294,7 +297,7 @@ class CNNEngine:
                 self._wgrad("W3", self.gW3, b.dy3, 64, b.y2, 0, 64, 576, B * 49, ws2, [2, B, 64, 9, 9, 3, 3, 1])
             return
         n = 512 if name == "W2" else 576
-        P = max(1, min(self.nhwc_planes, B))
+        P = max(1, min(self.nhwc_planes if name == "W2" else self.nhwc3_planes, B))
         buf = self._planes.get(name)
         if buf is None or buf.numel() < P * 64 * n:
             buf = torch.zeros(max(P, self.wgrad_planes) * 64 * n, dtype=torch.float32, device=self.dev)

@@ -8,13 +8,21 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 constexpr int NM = 256;
 
-template <int MODE>
+template <int MODE, bool RANDOM = false>
 __global__ void __launch_bounds__(512) probe(float* out, long long* cyc, float seed) {
   extern __shared__ float dyn[];   // MODE 7 / 8: operands at float offset 24576 (96 KB) / 2048 (8 KB) of 150 KB
   __shared__ float lds_s[MODE >= 7 ? 1 : 3 * 16 * 132 + 128 * 132 + 128];
   float* lds = MODE == 7 ? dyn + 24576 : MODE == 8 ? dyn + 2048 : lds_s;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int i = threadIdx.x; i < 3 * 16 * 132 + 128 * 132 + 128; i += 512) lds[i] = seed * (float)(i & 7) * 0.01f;
+  for (int i = threadIdx.x; i < 3 * 16 * 132 + 128 * 132 + 128; i += 512) {
+    if (RANDOM) {   // full-entropy operands (hashed), as trained weights / activations are
+      unsigned h = (unsigned)i * 2654435761u + 12345u;
+      h ^= h >> 13; h *= 0x5bd1e995u; h ^= h >> 15;
+      lds[i] = ((float)(h & 0xffffff) / 16777216.0f - 0.5f) * 0.2f;
+    } else {
+      lds[i] = seed * (float)(i & 7) * 0.01f;
+    }
+  }
   __syncthreads();
   float a = seed + lane, b = seed * 2.f - lane;
   floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, c2 = c0, c3 = c0;
@@ -117,13 +125,14 @@ int main() {
   long long* cyc;
   hipMalloc(&out, 256 * 512 * 4);
   hipMalloc(&cyc, 4096 * 8);
-  const char* names[9] = {"f32 16x16x4, 1 chain (regs)", "f32 16x16x4, 4 chains (regs)",
+  const char* names[10] = {"f32 16x16x4, 1 chain (regs)", "f32 16x16x4, 4 chains (regs)",
                           "f32 16x16x4, 1 chain, A/B from LDS", "bf16 16x16x32, 1 chain (regs)",
                           "engine LDS layer 128x128 (+barrier)", "engine layer, ~6k-cycle sleep between layers",
                           "engine layer, ~VALU gap between layers", "engine layer, operands at 96 KB of 150 KB dyn LDS",
-                          "engine layer, operands at 8 KB of 150 KB dyn LDS"};
+                          "engine layer, operands at 8 KB of 150 KB dyn LDS",
+                          "engine layer, RANDOM full-entropy operands"};
   for (int grid : {1, 64}) {
-    for (int mode = 0; mode < 9; ++mode) {
+    for (int mode = 0; mode < 10; ++mode) {
       for (int rep = 0; rep < 3; ++rep) {
         if (mode == 0) probe<0><<<grid, 512>>>(out, cyc, 1.0f);
         if (mode == 1) probe<1><<<grid, 512>>>(out, cyc, 1.0f);
@@ -134,6 +143,7 @@ int main() {
         if (mode == 6) probe<6><<<grid, 512>>>(out, cyc, 1.0f);
         if (mode == 7) probe<7><<<grid, 512, 150 * 1024>>>(out, cyc, 1.0f);
         if (mode == 8) probe<8><<<grid, 512, 150 * 1024>>>(out, cyc, 1.0f);
+        if (mode == 9) probe<4, true><<<grid, 512>>>(out, cyc, 1.0f);
       }
       hipDeviceSynchronize();
       long long h[8];
@@ -142,7 +152,7 @@ int main() {
       for (int w = 0; w < 8; ++w) mx = h[w] > mx ? h[w] : mx;
       printf("grid %3d  %-45s  max wave cycles %7lld  -> %.1f cycles per MFMA per wave, %.1f per SIMD (2 waves)\n",
              grid, names[mode], mx, (double)mx / NM, (double)mx / (2 * NM));
-      if (mode >= 4) {
+      if (mode >= 4) {  // (mode 9 is MODE 4 on random data)
         hipMemcpy(h, cyc + 1024, sizeof(h), hipMemcpyDeviceToHost);
         long long m2 = 0;
         for (int w = 0; w < 8; ++w) m2 = h[w] > m2 ? h[w] : m2;

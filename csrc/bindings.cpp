@@ -859,7 +859,7 @@ void mlp_rollout(Tensor desc, int64_t lds, Tensor obs, Tensor act, Tensor logp, 
   a.env_seed = (uint32_t)env_seed;
   a.max_steps = (int)max_steps;
   a.wlds = wlds ? 1 : 0;
-  a.stamps = reinterpret_cast<int64_t*>(stamps_ptr(stamps, 8));   // [16 steps][8 phases]
+  a.stamps = reinterpret_cast<int64_t*>(stamps_ptr(stamps, 16));   // [16 steps][8 phases] + per-wave layer stamps + flag
   check(aca_mlp_rollout(&a, (size_t)lds, cur_stream(obs)), "mlp_rollout");
 }
 

@@ -853,6 +853,8 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_rollout_kernel(RolloutArgs a)
     s_state[e] = e / LIN_OBS < rows ? a.state[(size_t)row0 * LIN_OBS + e] : 0.f;
   for (int e = tid; e < MLP_BM * MLP_MAXA; e += MLP_THREADS) s_act[e] = 0.f;
   __syncthreads();
+  // diagnostics only (stamps[255] == 1): the step loop runs the actor layers alone (no head, no env step)
+  const bool layers_only = a.stamps && a.stamps[255] == 1;
   for (int step = 0; step < a.T; ++step) {
     float* Xc = sm + (step & 1) * MLP_BM * ld0;
     float* Xn = sm + ((step & 1) ^ 1) * MLP_BM * ld0;
@@ -879,6 +881,10 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_rollout_kernel(RolloutArgs a)
       stamp(step, l);
       X = Yl;
       ldx = ldl;
+    }
+    if (layers_only) {
+      stamp(step, 6);
+      continue;
     }
     // ---- Gaussian head, one thread per (env, action component): mean, Box-Muller sample and the component's
     // log-prob term in parallel (a serial per-env loop of hash + log/sqrt/cos/tanh/exp chains on 16 lanes would

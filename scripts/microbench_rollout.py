@@ -17,7 +17,7 @@ def main():
                  cuda_graph=False)
     tr = ActorCriticTrainer(cfg)
     eng, st, env = tr.mlp, tr.storage, tr.env
-    stamps = torch.zeros(16 * 8 + 64, dtype=torch.int64, device="cuda:0")
+    stamps = torch.zeros(256, dtype=torch.int64, device="cuda:0")
     out = {"wlds": eng.rollout_weights_in_lds(), "T": st.T, "N": env.num_envs}
     for rep in range(3):
         torch.cuda.synchronize()
@@ -26,6 +26,18 @@ def main():
         torch.cuda.synchronize()
         out[f"host_ms_{rep}"] = round((time.perf_counter() - t0) * 1e3, 3)
     allst = stamps.cpu().tolist()
+    if len(sys.argv) > 1 and sys.argv[1] == "--layers-only":   # diagnostics: actor layers alone in the step loop
+        st2 = torch.zeros(256, dtype=torch.int64, device="cuda:0")
+        st2[255] = 1
+        eng.rollout_linear(env, st, KEY_ENV_BITS, tr.policy_seed, stamps=st2)
+        torch.cuda.synchronize()
+        a2 = st2.cpu().tolist()
+        d2 = [a2[128 + 8 * w:128 + 8 * w + 4] for w in range(8)]
+        t2 = min(x[0] for x in d2 if x[0])
+        out["layers_only_layer1_step5_wave_cycles"] = {f"w{w}": [x[k] - t2 if x[k] else None for k in range(4)]
+                                                       for w, x in enumerate(d2)}
+        s2 = [a2[8 * k:8 * k + 8] for k in range(16)]
+        out["layers_only_layer_us"] = [round((s2[8][i] - (s2[8][i - 1] if i else s2[7][6])) * 0.01, 2) for i in range(4)]
     s = [allst[8 * k:8 * k + 8] for k in range(16)]
     d = [allst[128 + 8 * w:128 + 8 * w + 4] for w in range(8)]
     t0c = min(x[0] for x in d if x[0])

@@ -118,6 +118,82 @@ __global__ void __launch_bounds__(512) probe(float* out, long long* cyc, float s
   if (lane == 0) cyc[blockIdx.x * 8 + wave] = t1 - t0;
 }
 
+
+__device__ __forceinline__ int ngp2(int w) {
+  const int g = (w + 15) >> 4;
+  return g <= 1 ? 1 : g <= 2 ? 2 : g <= 4 ? 4 : g <= 8 ? 8 : 16;
+}
+template <int NG>
+__device__ void layer_rt(const float* __restrict__ X, int ldx, const float* __restrict__ W, int ldw,
+                         const float* __restrict__ bias, int N, int act, float* __restrict__ Y, int ldy) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = lane & 15, q = lane >> 4;
+  const int ntile = ngp2(N);
+  for (int tile = wave; tile < ntile; tile += 8) {
+    const int c = tile * 16 + r;
+    const bool cok = c < N;
+    const int cc = cok ? c : N - 1;
+    const float* wrow = W + cc * ldw + 4 * q;
+    floatx4 bv[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) bv[g] = *reinterpret_cast<const floatx4*>(wrow + 16 * g);
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    const float* Xr = X + r * ldx + 4 * q;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      const float4 a4 = *reinterpret_cast<const float4*>(&Xr[16 * g]);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, bv[g][0], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.y, bv[g][1], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.z, bv[g][2], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.w, bv[g][3], acc, 0, 0, 0);
+    }
+    const float bb = bias[cc];
+    const float slope = act == 1 ? 0.f : act == 2 ? 0.2f : 1.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float v = acc[i] + bb;
+      Y[(4 * q + i) * ldy + c] = cok ? (v > 0.f ? v : slope * v) : 0.f;
+    }
+  }
+}
+__device__ void layer_sw(const float* X, int ldx, int K, const float* W, const float* bias, int N, int act, float* Y,
+                         int ldy) {
+  const int ldw = 16 * ngp2(K) + 4;
+  switch (ngp2(K)) {
+    case 1: layer_rt<1>(X, ldx, W, ldw, bias, N, act, Y, ldy); break;
+    case 2: layer_rt<2>(X, ldx, W, ldw, bias, N, act, Y, ldy); break;
+    case 4: layer_rt<4>(X, ldx, W, ldw, bias, N, act, Y, ldy); break;
+    case 8: layer_rt<8>(X, ldx, W, ldw, bias, N, act, Y, ldy); break;
+    default: layer_rt<16>(X, ldx, W, ldw, bias, N, act, Y, ldy); break;
+  }
+}
+// MODE 10 kernel: layers of runtime shape (K, N) = (kk, nn) through the switch, as mlp_rollout_kernel calls them
+__global__ void __launch_bounds__(512) probe_rt(float* out, long long* cyc, int kk, int nn, int nl) {
+  extern __shared__ float sm[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int ldx = 16 * ngp2(kk) + 4;
+  float* X = sm;
+  float* Y = sm + 16 * 260;
+  float* W = sm + 2 * 16 * 260;
+  float* bias = W + 256 * 260;
+  for (int i = threadIdx.x; i < 2 * 16 * 260 + 256 * 260 + 256; i += 512) {
+    unsigned h = (unsigned)i * 2654435761u + 12345u;
+    h ^= h >> 13; h *= 0x5bd1e995u; h ^= h >> 15;
+    sm[i] = ((float)(h & 0xffffff) / 16777216.0f - 0.5f) * 0.2f;
+  }
+  __syncthreads();
+  const long long t0 = __builtin_amdgcn_s_memtime();
+  for (int l = 0; l < nl; ++l) {
+    layer_sw(X, ldx, kk, W, bias, nn, 2, Y, ldx);
+    __syncthreads();
+    float* t = X; X = Y; Y = t;
+  }
+  out[threadIdx.x] = X[threadIdx.x];
+  __builtin_amdgcn_s_waitcnt(0);
+  const long long t1 = __builtin_amdgcn_s_memtime();
+  if (lane == 0) cyc[wave] = t1 - t0;
+}
+
 int main() {
   hipFuncSetAttribute(reinterpret_cast<const void*>(&probe<7>), hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
   hipFuncSetAttribute(reinterpret_cast<const void*>(&probe<8>), hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
@@ -161,5 +237,14 @@ int main() {
       }
     }
   }
+  hipFuncSetAttribute(reinterpret_cast<const void*>(&probe_rt), hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+  for (int rep = 0; rep < 3; ++rep) probe_rt<<<1, 512, 150 * 1024>>>(out, cyc, 128, 128, 8);
+  hipDeviceSynchronize();
+  long long h2[8];
+  hipMemcpy(h2, cyc, sizeof(h2), hipMemcpyDeviceToHost);
+  long long m3 = 0;
+  for (int w = 0; w < 8; ++w) m3 = h2[w] > m3 ? h2[w] : m3;
+  printf("runtime-shape layer via switch (the engine's code), 8 layers 128x128: %lld cycles = %.0f per layer\n", m3,
+         m3 / 8.0);
   return 0;
 }

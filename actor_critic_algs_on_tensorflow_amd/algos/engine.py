@@ -121,6 +121,7 @@ class CNNEngine:
         self.conv1_planes = int(os.environ.get("ACA_CONV1_PLANES", "128"))
         # conv2 / conv3 weight gradients by the per-sample NHWC kernel (conv_wgrad.hip) from this many rows up
         self.nhwc_wgrad_min_b = int(os.environ.get("ACA_NHWC_WGRAD_MIN_B", "1024"))
+        self.nhwc3_wgrad_min_b = int(os.environ.get("ACA_NHWC3_WGRAD_MIN_B", str(self.nhwc_wgrad_min_b)))
         self.nhwc_planes = int(os.environ.get("ACA_NHWC_PLANES", "128"))
         # conv3's per-sample work is small (2 k-steps x 12 column tiles), so its grid (3 workgroups per plane) needs
         # more planes than conv2 to cover the CUs
@@ -290,7 +291,8 @@ class CNNEngine:
 
     def _wgrad_conv23(self, name, b, ws2):
         B = b.B
-        if not (self.det_wgrad and self.implicit and B >= self.nhwc_wgrad_min_b):
+        min_b = self.nhwc_wgrad_min_b if name == "W2" else self.nhwc3_wgrad_min_b
+        if not (self.det_wgrad and self.implicit and B >= min_b):
             if name == "W2":
                 self._wgrad("W2", self.gW2, b.dy2, 64, b.y1, 0, 64, 512, B * 81, ws2, [2, B, 32, 20, 20, 4, 4, 2])
             else:

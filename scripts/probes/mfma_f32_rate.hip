@@ -194,7 +194,7 @@ __global__ void __launch_bounds__(512) probe_rt(float* out, long long* cyc, int 
   if (lane == 0) cyc[wave] = t1 - t0;
 }
 
-int main() {
+extern "C" int run_probe() {
   hipFuncSetAttribute(reinterpret_cast<const void*>(&probe<7>), hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
   hipFuncSetAttribute(reinterpret_cast<const void*>(&probe<8>), hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
   float* out;
@@ -248,3 +248,7 @@ int main() {
          m3 / 8.0);
   return 0;
 }
+
+#ifndef PROBE_LIB
+int main() { return run_probe(); }
+#endif

@@ -212,7 +212,7 @@ constexpr float HALF_LOG_2PI = 0.91893853320467274178f;
 constexpr float TWO_PI = 6.28318530717958647692f;
 
 __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
-  extern __shared__ float sm[];
+  extern __shared__ __attribute__((aligned(16))) float sm[];   // 16-byte base: the b128 LDS reads stay aligned
   __shared__ float s_red[MLP_BM][MLP_MAXA + 8];   // per-row partials: log-std grads + stats
   const int t = blockIdx.y + a.tw_base;
   const MlpTower& T = a.tw[t];
@@ -770,7 +770,7 @@ __device__ __forceinline__ void layer_fwd_lds(const float* X, int ldx, int K, co
 // !WLDS (wider frame stacks): weights stream from the L2-resident transposed shadows.
 template <bool WLDS>
 __global__ void __launch_bounds__(MLP_THREADS) mlp_rollout_kernel(RolloutArgs a) {
-  extern __shared__ float sm[];
+  extern __shared__ __attribute__((aligned(16))) float sm[];   // 16-byte base: the b128 LDS reads stay aligned
   __shared__ int64_t s_tg[MLP_BM];
   __shared__ int64_t s_ids[MLP_BM];
   __shared__ int s_t[MLP_BM];

@@ -78,7 +78,7 @@ __global__ void __launch_bounds__(256) col2im_nhwc_kernel(const u16* __restrict_
                                                           u16* __restrict__ dx, float* __restrict__ colsum, int B,
                                                           int C, int H, int W, int KH, int KW, int S, int OH,
                                                           int OW) {
-  extern __shared__ float csum[];  // [C]
+  extern __shared__ __attribute__((aligned(16))) float csum[];  // [C]
   for (int c = threadIdx.x; c < C; c += blockDim.x) csum[c] = 0.f;
   __syncthreads();
   const int CC = C / 8;

@@ -22,8 +22,9 @@ asks first) and a **data plane** for the payloads: ``"nccl"`` = RCCL point-to-po
 tensors (over xGMI between GPUs of a node; needs one GPU per rank), or ``"gloo"`` = the same messages staged
 through host memory (CPU runs, several ranks sharing one GPU). Bounded staleness (stale-synchronous parallel):
 with ``max_staleness = s`` a PS defers a worker's apply while that worker is more than ``s`` applies ahead of
-the slowest live worker, so a gradient is never older than ``(W - 1) * (s + 1)`` global steps; ``s < 0`` disables
-the bound (the reference's unbounded asynchrony). Every apply is logged as (worker, pulled version, global step).
+the slowest live worker. While one worker computes a gradient, another can first catch up (it may trail by up to
+``s + 1`` applies) and then run ``s + 1`` applies ahead, so a gradient is never older than ``2 (W - 1) (s + 1)``
+global steps; ``s < 0`` disables the bound (the reference's unbounded asynchrony). Every apply is logged as (worker, pulled version, global step).
 """
 from __future__ import annotations
 

@@ -16,7 +16,8 @@ import threading
 import torch
 
 _LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_C")
-LIB_PATH = os.path.join(_LIB_DIR, "libacamd.so")
+# (ACAMD_LIB: an alternative in-tree build of the same library, for A/B runs of kernel variants)
+LIB_PATH = os.environ.get("ACAMD_LIB") or os.path.join(_LIB_DIR, "libacamd.so")
 
 _lock = threading.Lock()
 _loaded = None

@@ -105,22 +105,6 @@ __device__ __forceinline__ void opt_body(const OptSeg& S, float b1, float b2, fl
   const size_t n = S.n;
   const float lr = *S.lr;
   const float t = ADAM ? (*S.t + 1.0f) : 0.f;
-  u16* shadow = S.shadow;
-  // float4 body, software-pipelined: a thread's first element group is requested BEFORE the global-norm partials
-  // are reduced (the two loads are independent, so the update waits one memory round trip instead of two), and
-  // each later group is requested before the previous one is stored
-  const size_t n4 = n / 4;
-  const size_t stride = (size_t)vgrid * blockDim.x;
-  size_t i = vblk * (size_t)blockDim.x + threadIdx.x;
-  bool have = i < n4;
-  float4 g4, v4, p4, m4;
-  auto load4 = [&](size_t j) {
-    g4 = reinterpret_cast<const float4*>(g)[j];
-    v4 = reinterpret_cast<const float4*>(v)[j];
-    p4 = reinterpret_cast<const float4*>(p)[j];
-    m4 = ADAM ? reinterpret_cast<const float4*>(m)[j] : make_float4(0.f, 0.f, 0.f, 0.f);
-  };
-  if (have) load4(i);
   float scale = 1.f;
   if (S.parts) {
     const float gsq = partial_total(S.parts, shr) * S.norm_mul;
@@ -142,31 +126,34 @@ __device__ __forceinline__ void opt_body(const OptSeg& S, float b1, float b2, fl
       pi -= lr * gi / sqrtf(vi + eps);
     }
   };
-  while (have) {
+  u16* shadow = S.shadow;
+  // float4 body: all operand loads of a thread are issued together (one memory round trip per element group)
+  const size_t n4 = n / 4;
+  const size_t stride = (size_t)vgrid * blockDim.x;
+  for (size_t i = vblk * (size_t)blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 g4 = reinterpret_cast<const float4*>(g)[i];
+    float4 v4 = reinterpret_cast<const float4*>(v)[i];
+    float4 p4 = reinterpret_cast<const float4*>(p)[i];
+    float4 m4 = ADAM ? reinterpret_cast<const float4*>(m)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
     if (zero_grad) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     upd(g4.x, v4.x, m4.x, p4.x);
     upd(g4.y, v4.y, m4.y, p4.y);
     upd(g4.z, v4.z, m4.z, p4.z);
     upd(g4.w, v4.w, m4.w, p4.w);
-    const float4 vo = v4, mo = m4, po = p4;
-    const size_t io = i;
-    i += stride;
-    have = i < n4;
-    if (have) load4(i);
-    reinterpret_cast<float4*>(v)[io] = vo;
-    if (ADAM) reinterpret_cast<float4*>(m)[io] = mo;
-    reinterpret_cast<float4*>(p)[io] = po;
+    reinterpret_cast<float4*>(v)[i] = v4;
+    if (ADAM) reinterpret_cast<float4*>(m)[i] = m4;
+    reinterpret_cast<float4*>(p)[i] = p4;
     if (shadow) {
       uint2 sv;
-      sv.x = (uint32_t)f2bf(po.x) | ((uint32_t)f2bf(po.y) << 16);
-      sv.y = (uint32_t)f2bf(po.z) | ((uint32_t)f2bf(po.w) << 16);
-      reinterpret_cast<uint2*>(shadow)[io] = sv;
+      sv.x = (uint32_t)f2bf(p4.x) | ((uint32_t)f2bf(p4.y) << 16);
+      sv.y = (uint32_t)f2bf(p4.z) | ((uint32_t)f2bf(p4.w) << 16);
+      reinterpret_cast<uint2*>(shadow)[i] = sv;
     }
     if (S.ntrans) {
-      write_trans(S, 4 * io, po.x);
-      write_trans(S, 4 * io + 1, po.y);
-      write_trans(S, 4 * io + 2, po.z);
-      write_trans(S, 4 * io + 3, po.w);
+      write_trans(S, 4 * i, p4.x);
+      write_trans(S, 4 * i + 1, p4.y);
+      write_trans(S, 4 * i + 2, p4.z);
+      write_trans(S, 4 * i + 3, p4.w);
     }
   }
   if (vblk == 0) {   // scalar tail

@@ -107,8 +107,9 @@ def test_a3c_gpu_worker_learns_pendulum(cuda, tmp_path):
     _check(res, 1, -1, 3000)
     rets = [r[2] for r in res[1]["returns"]]
     assert len(rets) >= 5, rets
-    # measured on this fixed trajectory: -1512 (first 500 updates) -> -1410 -> -1238 -> -1229 -> -1229
-    assert max(rets[2:]) > rets[0] + 200, rets
+    # measured: -1512 -> -1410 -> -1238 -> -1229 -> -1229 and, with an optimiser build that rounds differently,
+    # -1318 -> -1241 -> -1227 -> -1229 -> -1229: both settle on the same plateau from different first reports
+    assert max(rets[2:]) > rets[0] + 50 and max(rets[2:]) > -1260, rets
 
 
 def _pf_proc(rank, port, d):

@@ -826,6 +826,13 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_rollout_kernel(RolloutArgs a)
     for (int j = 0; j < l; ++j) p += s_out[j] * (16 * ngp2(s_in[j]) + 4) + 16 * ngp2(s_out[j]);
     return p;
   };
+  // per-layer LDS offsets, computed once: in the step loop each is one LDS read instead of a dependent chain of
+  // reads over the earlier layers' widths
+  __shared__ int s_yo[MLP_MAXL + 1], s_wo[MLP_MAXL];
+  if (tid == 0) {
+    for (int l = 0; l <= nl; ++l) s_yo[l] = (int)(Yp(l) - sm);
+    for (int l = 0; l < nl; ++l) s_wo[l] = (int)(Wl(l) - sm);
+  }
   if (WLDS) {   // W_l [out][16*ngp2(in) + 4] (from the zero-padded transposed shadow), then b_l [16*ngp2(out)]
     for (int l = 0; l < nl; ++l) {
       const int K4 = 4 * ngp2(s_in[l]), N = s_out[l], ldw = 16 * ngp2(s_in[l]) + 4;
@@ -862,10 +869,10 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_rollout_kernel(RolloutArgs a)
     const float* X = Xc;
     int ldx = ld0;
     for (int l = 0; l < nl; ++l) {
-      float* Yl = Yp(l);
+      float* Yl = sm + s_yo[l];
       const int ldl = ldyf(l);
       if (WLDS) {
-        const float* w = Wl(l);
+        const float* w = sm + s_wo[l];
         // diagnostics: per-wave shader-clock stamps inside layer 1 of step 5 (entry, MFMAs issued, epilogue landed,
         // after the barrier) at stamps[128 + wave * 8 + k]
         int64_t* dbg = (a.stamps && blockIdx.x == 0 && step == 5 && l == 1) ? a.stamps + 128 : nullptr;

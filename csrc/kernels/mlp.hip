@@ -241,6 +241,15 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
   };
   float* P0 = Yp(nl);
   float* P1 = P0 + MLP_BM * (MLP_MAXW + 4);
+  // per-layer LDS offsets and strides, computed once (one LDS read per use instead of a chain over the earlier
+  // layers' widths read from the descriptor)
+  __shared__ int s_yo[MLP_MAXL], s_ld[MLP_MAXL];
+  if (threadIdx.x == 64) {
+    for (int l = 0; l < nl; ++l) {
+      s_yo[l] = (int)(Yp(l) - sm);
+      s_ld[l] = ldyf(l);
+    }
+  }
   // ---- row gather: explicit index list, the keyed minibatch permutation (PPO), or identity
   __shared__ int64_t s_grow[MLP_BM];
   if (threadIdx.x < MLP_BM) {
@@ -269,8 +278,8 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
   const float* X = X0;
   int ldx = ld0;
   for (int l = 0; l < nl; ++l) {
-    float* Yl = Yp(l);
-    const int ldl = ldyf(l);
+    float* Yl = sm + s_yo[l];
+    const int ldl = s_ld[l];
     layer_fwd(X, ldx, (int)T.in[l], P_<const float>(T.Wt[l]), P_<const float>(T.b[l]), (int)T.out[l], (int)T.act[l],
               Yl, ldl);
     __syncthreads();
@@ -287,8 +296,8 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
     ldx = ldl;
   }
   const int L = nl - 1;
-  const float* Yo = Yp(L);
-  const int ldo = ldyf(L);
+  const float* Yo = sm + s_yo[L];
+  const int ldo = s_ld[L];
   // ---- heads: one thread per row
   const bool policy = (t == 0);
   float* dPtop = P0;
@@ -506,7 +515,7 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
     const int N = (int)T.out[l], K = (int)T.in[l];
     gf32* gdst = P_<float>(T.dp[l - 1]) + (size_t)row0 * K;
     gcf32* W = P_<const float>(T.W[l]);
-    layer_dgrad(cur, ldP, N, W, K, Yp(l - 1), ldyf(l - 1), (int)T.act[l - 1], nxt, ldP, gdst, rows);
+    layer_dgrad(cur, ldP, N, W, K, sm + s_yo[l - 1], s_ld[l - 1], (int)T.act[l - 1], nxt, ldP, gdst, rows);
     __syncthreads();
     stamp(9 + L - l);
     float* tmp = cur;

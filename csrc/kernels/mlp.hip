@@ -538,41 +538,56 @@ constexpr int WG_CHUNK = 32;   // loads per operand per lane per chunk (128 rows
 
 __global__ void __launch_bounds__(256) mlp_wgrad_kernel(WgradArgs a) {
   __shared__ float red[4][64][5];
-  __shared__ float s_glog[MLP_MAXA];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int split = blockIdx.x % a.nsplit;
-  int item = blockIdx.x / a.nsplit;
-  if (blockIdx.x == 0 && a.mpart) {   // sum the train kernel's partial rows (fixed order: deterministic)
-    if (wave == 0) {
-      float v[MPART_W];
+  if (blockIdx.x == gridDim.x - 1) {
+    // The bookkeeping workgroup (one past the tiles): the train kernel's partial rows summed in a fixed order
+    // (deterministic), the log-std gradient finished and its sum of squares written to its own slot, the loss
+    // statistics published, the update counter advanced. Done by a tile workgroup, this chain of dependent global
+    // round trips made that workgroup -- and so the launch -- finish last.
+    if (wave != 0) return;
+    float v[MPART_W];
 #pragma unroll
-      for (int c = 0; c < MPART_W; ++c) v[c] = 0.f;
+    for (int c = 0; c < MPART_W; ++c) v[c] = 0.f;
+    if (a.mpart) {
       for (int row = lane; row < a.mpart_rows; row += 64) {
 #pragma unroll
         for (int c = 0; c < MPART_W; ++c) v[c] += a.mpart[(size_t)row * MPART_W + c];
       }
 #pragma unroll
       for (int c = 0; c < MPART_W; ++c) v[c] = wave_sum(v[c]);
-      if (lane == 0) {
-        for (int k = 0; k < 8; ++k) a.mstats[k] += v[k];
-        for (int j = 0; j < a.A; ++j) {
-          const float g = a.g_log_std ? a.g_log_std[j] + v[8 + j] : 0.f;
-          if (a.g_log_std) a.g_log_std[j] = g;
-          s_glog[j] = g;
-        }
+    }
+    float g = 0.f;
+    if (a.g_log_std && lane < a.A) {
+      g = a.g_log_std[lane];
+      if (a.mpart) {
+        float part = 0.f;   // v[8 + lane] with compile-time indices (a runtime index would put v in scratch)
+#pragma unroll
+        for (int j = 0; j < MLP_MAXA; ++j) part = lane == j ? v[8 + j] : part;
+        g += part;
+        a.g_log_std[lane] = g;
       }
     }
-    __syncthreads();
+    if (a.g_log_std && a.nsplit == 1 && a.parts[0]) {
+      const float ss = wave_sum(lane < a.A ? clipsq(g, a.clip[0]) : 0.f);
+      if (lane == 0) a.parts[0][a.items[0]] = ss;   // the slot after tower 0's tiles (host-checked < MLP_PARTS)
+    }
+    if (lane == 0) {
+      if (a.mpart)
+        for (int k = 0; k < 8; ++k) a.mstats[k] += v[k];
+      if (a.stats) {   // publish (and reset) the fused kernel's statistics
+        float m[8];
+        for (int k = 0; k < 8; ++k) m[k] = a.mstats[k];
+        m[5] = m[0] + (*a.kl_coef) * m[1] - (*a.ent_coef) * m[2];
+        for (int k = 0; k < 7; ++k) a.stats[k] = m[k];
+        for (int k = 0; k < 8; ++k) a.mstats[k] = 0.f;
+      }
+      // the train kernel (the counter's only reader in this minibatch) has finished: stream order
+      if (a.bump) *a.bump += 1;
+    }
+    return;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0 && a.stats) {   // publish (and reset) the fused kernel's statistics
-    float m[8];
-    for (int k = 0; k < 8; ++k) m[k] = a.mstats[k];
-    m[5] = m[0] + (*a.kl_coef) * m[1] - (*a.ent_coef) * m[2];
-    for (int k = 0; k < 7; ++k) a.stats[k] = m[k];
-    for (int k = 0; k < 8; ++k) a.mstats[k] = 0.f;
-  }
-  // the train kernel (the counter's only reader in this minibatch) has finished: stream order
-  if (blockIdx.x == 0 && threadIdx.x == 0 && a.bump) *a.bump += 1;
+  const int split = blockIdx.x % a.nsplit;
+  int item = blockIdx.x / a.nsplit;
   // locate (tower, layer, tile)
   int t = 0;
   if (item >= a.items[0]) {
@@ -657,12 +672,12 @@ __global__ void __launch_bounds__(256) mlp_wgrad_kernel(WgradArgs a) {
     }
   }
   if (a.nsplit == 1 && a.parts[t]) {
-    if (t == 0 && local_item == 0 && a.g_log_std && lane < a.A)
-      ss += clipsq(a.mpart ? s_glog[lane] : a.g_log_std[lane], c);
     ss = wave_sum(ss);
     if (lane == 0) a.parts[t][local_item] = ss;
-    if (local_item == 0)   // unused slots are zero: the optimiser sums all MLP_PARTS in a fixed order
-      for (int k = a.items[t] + lane; k < MLP_PARTS; k += 64) a.parts[t][k] = 0.f;
+    if (local_item == 0) {   // unused slots are zero: the optimiser sums all MLP_PARTS in a fixed order
+      const int first = a.items[t] + (t == 0 && a.g_log_std ? 1 : 0);   // (tower 0: the log-std slot is taken)
+      for (int k = first + lane; k < MLP_PARTS; k += 64) a.parts[t][k] = 0.f;
+    }
   }
 }
 
@@ -1026,8 +1041,10 @@ extern "C" hipError_t aca_mlp_wgrad(const WgradArgs* a, hipStream_t stream) {
   if (!a->tw || a->nsplit < 1 || a->ntw < 1 || a->ntw > 2) return hipErrorInvalidValue;
   for (int t = 0; t < a->ntw; ++t)
     if (a->parts[t] && a->nsplit == 1 && a->items[t] > MLP_PARTS) return hipErrorInvalidValue;
+  if (a->g_log_std && a->parts[0] && a->nsplit == 1 && a->items[0] >= MLP_PARTS) return hipErrorInvalidValue;
   const int total = a->items[0] + (a->ntw > 1 ? a->items[1] : 0);
-  mlp_wgrad_kernel<<<total * a->nsplit, 256, 0, stream>>>(*a);
+  // + the bookkeeping workgroup (statistics, log-std gradient, update counter)
+  mlp_wgrad_kernel<<<total * a->nsplit + 1, 256, 0, stream>>>(*a);
   return hipGetLastError();
 }
 

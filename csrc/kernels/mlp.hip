@@ -250,6 +250,22 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
       s_ld[l] = ldyf(l);
     }
   }
+  // the tower descriptor's per-layer words staged in LDS once: indexed by the runtime layer number they are vector
+  // memory loads, and on gfx9 a load issued after the layer's workspace stores waits for those stores (vmcnt counts
+  // both, in order) -- each layer paid that before it could even address its weights
+  __shared__ int s_in[MLP_MAXL], s_out[MLP_MAXL], s_act[MLP_MAXL];
+  __shared__ int64_t s_Wt[MLP_MAXL], s_bb[MLP_MAXL], s_W[MLP_MAXL], s_xs[MLP_MAXL], s_dp[MLP_MAXL];
+  if (threadIdx.x >= 96 && threadIdx.x < 96 + nl) {
+    const int l = threadIdx.x - 96;
+    s_in[l] = (int)T.in[l];
+    s_out[l] = (int)T.out[l];
+    s_act[l] = (int)T.act[l];
+    s_Wt[l] = T.Wt[l];
+    s_bb[l] = T.b[l];
+    s_W[l] = T.W[l];
+    s_xs[l] = T.xs[l];
+    s_dp[l] = T.dp[l];
+  }
   // ---- row gather: explicit index list, the keyed minibatch permutation (PPO), or identity
   __shared__ int64_t s_grow[MLP_BM];
   if (threadIdx.x < MLP_BM) {
@@ -269,7 +285,7 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
     float v = 0.f;
     if (r < rows && c < a.D) v = a.obs[s_grow[r] * a.ld_obs + c];
     X0[e] = v;
-    if (a.mode == 2 && r < rows && c < a.D) P_<float>(T.xs[0])[(size_t)(row0 + r) * a.D + c] = v;
+    if (a.mode == 2 && r < rows && c < a.D) P_<float>(s_xs[0])[(size_t)(row0 + r) * a.D + c] = v;
   }
   __syncthreads();
   stamp(2);
@@ -280,13 +296,13 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
   for (int l = 0; l < nl; ++l) {
     float* Yl = sm + s_yo[l];
     const int ldl = s_ld[l];
-    layer_fwd(X, ldx, (int)T.in[l], P_<const float>(T.Wt[l]), P_<const float>(T.b[l]), (int)T.out[l], (int)T.act[l],
+    layer_fwd(X, ldx, s_in[l], P_<const float>(s_Wt[l]), P_<const float>(s_bb[l]), s_out[l], s_act[l],
               Yl, ldl);
     __syncthreads();
     stamp(3 + l);
     if (a.mode == 2 && l + 1 < nl) {   // inputs of layer l+1 for its weight gradient
-      const int w = (int)T.out[l];
-      gf32* xs = P_<float>(T.xs[l + 1]);
+      const int w = s_out[l];
+      gf32* xs = P_<float>(s_xs[l + 1]);
       for (int e = threadIdx.x; e < rows * w; e += MLP_THREADS) {
         const int r = e / w, c = e - r * w;
         xs[(size_t)(row0 + r) * w + c] = Yl[r * ldl + c];
@@ -501,8 +517,8 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
   stamp(14);   // head phase C + log-std sums (the data-gradient layers take slots 9 ..)
   // ---- top layer dP: apply the head activation derivative (tanh applied above) and publish
   {
-    const int w = (int)T.out[L];
-    gf32* dp = P_<float>(T.dp[L]);
+    const int w = s_out[L];
+    gf32* dp = P_<float>(s_dp[L]);
     for (int e = threadIdx.x; e < rows * w; e += MLP_THREADS) {
       const int r = e / w, c = e - r * w;
       dp[(size_t)(row0 + r) * w + c] = dPtop[r * ldP + c];
@@ -512,10 +528,10 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
   float* cur = P0;
   float* nxt = P1;
   for (int l = L; l >= 1; --l) {
-    const int N = (int)T.out[l], K = (int)T.in[l];
-    gf32* gdst = P_<float>(T.dp[l - 1]) + (size_t)row0 * K;
-    gcf32* W = P_<const float>(T.W[l]);
-    layer_dgrad(cur, ldP, N, W, K, sm + s_yo[l - 1], s_ld[l - 1], (int)T.act[l - 1], nxt, ldP, gdst, rows);
+    const int N = s_out[l], K = s_in[l];
+    gf32* gdst = P_<float>(s_dp[l - 1]) + (size_t)row0 * K;
+    gcf32* W = P_<const float>(s_W[l]);
+    layer_dgrad(cur, ldP, N, W, K, sm + s_yo[l - 1], s_ld[l - 1], s_act[l - 1], nxt, ldP, gdst, rows);
     __syncthreads();
     stamp(9 + L - l);
     float* tmp = cur;

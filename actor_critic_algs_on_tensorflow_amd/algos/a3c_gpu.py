@@ -18,16 +18,30 @@ Roles (ranks ``0 .. ps_num-1`` are parameter servers, the rest workers, as :mod:
   kept PER WORKER (each reference worker builds its own Adam, whose beta powers advance only with its own applies).
 
 Transport: a gloo **control plane** (int64 headers, ``recv`` from any source, so the PS serves whichever worker
-asks first) and a **data plane** for the payloads: ``"nccl"`` = RCCL point-to-point ``send/recv`` of device
-tensors (over xGMI between GPUs of a node; needs one GPU per rank), or ``"gloo"`` = the same messages staged
-through host memory (CPU runs, several ranks sharing one GPU). Bounded staleness (stale-synchronous parallel):
-with ``max_staleness = s`` a PS defers a worker's apply while that worker is more than ``s`` applies ahead of
-the slowest live worker. While one worker computes a gradient, another can first catch up (it may trail by up to
-``s + 1`` applies) and then run ``s + 1`` applies ahead, so a gradient is never older than ``2 (W - 1) (s + 1)``
-global steps; ``s < 0`` disables the bound (the reference's unbounded asynchrony). Every apply is logged as (worker, pulled version, global step).
+asks first; the PS's reply header carries the global step, so a worker never reads the device to learn it) and a
+**data plane** for the payloads: ``"nccl"`` = RCCL point-to-point ``send/recv`` of device tensors (over xGMI
+between GPUs of a node; needs one GPU per rank), or ``"gloo"`` = the same messages staged through host memory (CPU
+runs, several ranks sharing one GPU). A PS apply is ONE native launch (``opt_multi``: the shard's actor and critic
+segments with their own lr / clip / per-worker step count; the actor lr is read straight from the payload slot the
+worker filled). Bounded staleness (stale-synchronous parallel): with ``max_staleness = s`` a PS defers a worker's
+apply while that worker is more than ``s`` applies ahead of the slowest live worker. While one worker computes a
+gradient, another can first catch up (it may trail by up to ``s + 1`` applies) and then run ``s + 1`` applies
+ahead, so a gradient is never older than ``2 (W - 1) (s + 1)`` global steps; ``s < 0`` disables the bound (the
+reference's unbounded asynchrony). Every apply is logged as (worker, pulled version, global step).
+
+Chief duties and logs (``A3C/process.py:211-214,280-283``, ``A3C/train.py:39``): worker 0 writes the global
+actor/critic as a TF bundle ``<checkpoint_dir>/model-<Env>-<global step>`` every ``save_every`` global steps (the
+reference's ``CheckpointSaverHook``; reference variable names, so ``cli/test_model.py`` evaluates it) and every
+worker keeps a reference-format Logger file ``<log_dir>/worker_<task>.log``.
+
+Failure handling: a worker that dies mid-run (``fault_inject="rank:iteration"``) makes the PS's next
+control-plane receive fail -- gloo reports the closed peer, or the group timeout expires -- and the PS returns an
+``"aborted"`` summary instead of waiting forever; the surviving workers' exchange with the departed PS raises, so
+every process of the job ends.
 """
 from __future__ import annotations
 
+import os
 import time
 
 import torch
@@ -36,7 +50,12 @@ import torch.distributed as dist
 from .. import envs as E
 from ..ops.optim import make_optimizer
 
-CMD_PULL, CMD_APPLY, CMD_DONE = 1, 2, 3
+CMD_PULL, CMD_APPLY, CMD_DONE, CMD_REPLY = 1, 2, 3, 4
+PAY_ALIGN = 8   # payload slots: the actor lr sits after the gradient, padded to a 32-byte boundary
+
+
+def _pay_len(n):
+    return (n + PAY_ALIGN - 1) // PAY_ALIGN * PAY_ALIGN + PAY_ALIGN
 
 
 def shard_ranges(flat, ps_num):
@@ -111,8 +130,9 @@ class DeviceParameterServer:
             name = f"ps{sid}_{g}"
             self.flat.groups[name] = (a, b)
             actor = g != "critic"
+            # element-wise clipping only (A3C/policies.py:85): a global-norm clip would be taken per shard here
             opt = make_optimizer("adam", self.flat, name, cfg.lr if actor else cfg.critic_lr,
-                                 cfg.clip_value if actor else cfg.critic_clip_value, cfg.max_grad_norm)
+                                 cfg.clip_value if actor else cfg.critic_clip_value, None)
             self.segs.append((opt, a - self.s, b - self.s, actor))
         # per-worker Adam step counts (bias correction advances with that worker's applies only)
         self.t = {(k, w): torch.zeros((), dtype=torch.float32, device=self.device)
@@ -120,27 +140,43 @@ class DeviceParameterServer:
         self.n_applies = {w: 0 for w in self.workers}
         self.global_step = 0
         self.log = []   # (worker rank, version the gradient was computed at, global step before the apply)
-        self._pay = {w: torch.zeros(self.n + 1, device=self.device) for w in self.workers}
-        self._rep = torch.zeros(self.n + 1, device=self.device)
+        self.status = "ok"
+        self._pay = {w: torch.zeros(_pay_len(self.n), device=self.device) for w in self.workers}
+        self._steppers = {w: self._stepper(w) for w in self.workers}
+
+    def _stepper(self, w):
+        """The apply of worker ``w``'s payload: per segment a shallow view of the shard optimiser whose gradient is
+        the payload slice, whose step count is ``w``'s own and (actor segments) whose lr is the payload's lr slot --
+        all segments in ONE ``opt_multi`` launch on a GPU (moments and parameters are the shared ones)."""
+        import copy
+        from .. import _native
+        from ..ops.optim import FusedGroupStep
+        buf = self._pay[w]
+        lr_slot = buf[_pay_len(self.n) - PAY_ALIGN]
+        views = []
+        for k, (opt, a, b, actor) in enumerate(self.segs):
+            o = copy.copy(opt)
+            o.g = buf[a:b]
+            o.t = self.t[(k, w)]
+            if actor:
+                o.lr = lr_slot
+            views.append(o)
+        if _native.use_native(self.flat.data):
+            return FusedGroupStep(views).step   # opt_multi takes 1..OPT_MAXSEG segments
+        return lambda: [o.step() for o in views]
 
     # -- one apply ------------------------------------------------------------------------------------------------
     @torch.no_grad()
     def apply(self, w, version):
-        buf = self._pay[w]
-        for k, (opt, a, b, actor) in enumerate(self.segs):
-            opt.g = buf[a:b]
-            if actor:
-                opt.lr.copy_(buf[self.n])   # the sender's (KL-adaptive) actor lr, device to device
-            opt.t = self.t[(k, w)]
-            opt.step()
+        self._steppers[w]()
         self.log.append((w, version, self.global_step))
         self.global_step += 1
         self.n_applies[w] += 1
 
     def reply(self, w):
-        self._rep[:self.n].copy_(self.flat.data[self.s:self.e])
-        self._rep[self.n] = float(self.global_step)
-        self.planes.send(self._rep, w)
+        """Reply header (global step, on the control plane) + the shard's parameters (data plane)."""
+        self.planes.send_hdr([CMD_REPLY, self.sid, self.global_step, 0], w)
+        self.planes.send(self.flat.data[self.s:self.e], w)
 
     def _allowed(self, w):
         if self.max_staleness < 0 or len(self.live) <= 1:
@@ -149,6 +185,15 @@ class DeviceParameterServer:
         return self.n_applies[w] - slowest <= self.max_staleness
 
     def serve(self):
+        """Serves until every worker said DONE. A failed control-plane receive (a worker died: gloo reports the
+        closed peer, or the group timeout expired) ends the PS with ``status == "aborted"`` instead of a hang."""
+        try:
+            self._serve()
+        except RuntimeError as e:
+            self.status = "aborted"
+            self.error = repr(e)
+
+    def _serve(self):
         pending = []   # deferred applies (stale-synchronous bound), served in arrival order once allowed
         while self.live or pending:
             if self.live:
@@ -180,24 +225,35 @@ class DeviceParameterServer:
 class GPUWorker:
     """A vectorised device trainer whose optimiser step is the PS exchange."""
 
-    def __init__(self, cfg, task, ranges, ps_ranks, planes, device):
+    def __init__(self, cfg, task, ranges, ps_ranks, planes, device, log_dir=None, rank=None, logger=None,
+                 checkpoint_basename=None):
         from .trainer import ActorCriticTrainer
+        from ..utils.logger import Logger
         self.cfg, self.task = cfg, task
+        self.rank = rank if rank is not None else task
         self.ranges, self.ps_ranks, self.planes = ranges, ps_ranks, planes
         self.device = torch.device(device)
-        wcfg = cfg.replace(algo="a2c", device=str(self.device), outdir=None if task else cfg.outdir)
+        wcfg = cfg.replace(algo="a2c", device=str(self.device), outdir=None)
         fs = 4 if ("Pong" in cfg.env or "Breakout" in cfg.env) else cfg.frames
         env = E.make(cfg.env, cfg.num_envs, device=self.device, seed=cfg.seed, env_offset=task * cfg.num_envs,
                      frame_stack=fs)
         self.tr = ActorCriticTrainer(wcfg, env=env)
         self.tr._grad_sink = self._exchange
+        self.tr.worker_id = task
+        if logger is not None:   # the caller's Logger (compat.process_fn's ``logger`` argument)
+            self.tr.logger = logger
+        elif log_dir:   # A3C/train.py:39: tmp/logs/worker_<i>.log, one per worker
+            self.tr.logger = Logger(os.path.join(log_dir, f"worker_{task}.log"), quiet=cfg.quiet)
+        self.ckpt_base = checkpoint_basename
         self.version = 0
         n = [e - s for s, e in ranges]
-        self._pay = [torch.zeros(k + 1, device=self.device) for k in n]
-        self._rep = [torch.zeros(k + 1, device=self.device) for k in n]
+        self._pay = [torch.zeros(_pay_len(k), device=self.device) for k in n]
+        self.saved = []
 
     @torch.no_grad()
     def _exchange(self, pull_only=False):
+        """Push the gradient + this worker's actor lr to every shard, pull the parameters back. The global step
+        comes in the PS's reply header (host memory), so nothing here reads the device."""
         tr = self.tr
         flat = tr.flat
         lr = tr.actor_opt.lr
@@ -206,51 +262,103 @@ class GPUWorker:
             if not pull_only:
                 p = self._pay[sid]
                 p[:e - s].copy_(flat.grad[s:e])
-                p[e - s:].copy_(lr.reshape(1))
+                p[p.numel() - PAY_ALIGN:p.numel() - PAY_ALIGN + 1].copy_(lr.reshape(1))
                 self.planes.send(p, r)
+        version = 0
         for sid, ((s, e), r) in enumerate(zip(self.ranges, self.ps_ranks)):
-            self.planes.recv(self._rep[sid], r)
-            flat.data[s:e].copy_(self._rep[sid][:e - s])
-        self.version = int(self._rep[0][-1])   # global step of PS 0 (host read: the exchange is synchronous)
-        return self.version
+            _, (cmd, _sid, gstep, _) = self.planes.recv_hdr(r)
+            assert cmd == CMD_REPLY, cmd
+            self.planes.recv(flat.data[s:e], r)
+            if sid == 0:
+                version = gstep   # global step of PS 0 (the shard that also counts the actor applies)
+        self.version = version
+        return version
 
     def run(self, total_updates, report_every=0):
         """Trains until the PS global step reaches ``total_updates``. Returns the global step after each of this
         worker's updates; with ``report_every`` also (update, global step, mean finished-episode return) rows in
-        ``self.returns`` (a host read of the env bank's episode statistics every ``report_every`` updates)."""
-        tr = self.tr
+        ``self.returns`` (a host read of the env bank's episode statistics every ``report_every`` updates). Worker
+        0 (the chief) checkpoints every ``save_every`` global steps; each worker logs reference-format rows."""
+        from .trainer import FAULT_EXIT_CODE, parse_fault
+        cfg, tr = self.cfg, self.tr
+        fault = parse_fault(cfg.fault_inject)
         self._exchange(pull_only=True)   # initial sync_w_global (reference bug #12 fixed)
         tr._after_pull()
         if tr._can_capture():
             tr.capture(warmup=1)
         hist = []
         self.returns = []
+        last_mark = -1
+        i = 0
         while self.version < total_updates:
+            if fault is not None and fault == (self.rank, i):   # SURVEY §5.3 test hook: die without goodbye
+                os._exit(FAULT_EXIT_CODE)
             tr.step()
             hist.append(self.version)
             if report_every and len(hist) % report_every == 0:
                 ret, n_ep, _ = tr.env.drain_episode_stats()
                 self.returns.append((len(hist), self.version, ret, n_ep))
+            if tr.logger is not None and cfg.stdout_freq and i % cfg.stdout_freq == 0:
+                tr.log(i, print_tog=not cfg.quiet)   # A3C/process.py:280-283
+            if tr.logger is not None and cfg.flush_every and i % cfg.flush_every == cfg.flush_every // 2:
+                tr.logger.flush()
+            if self.task == 0 and cfg.save_every and cfg.checkpoint_dir:
+                mark = self.version // cfg.save_every   # CheckpointSaverHook(save_steps=save_every), chief only
+                if mark != last_mark:
+                    self.saved.append(self.save(self.version))
+                    last_mark = mark
+            i += 1
+        if self.task == 0 and cfg.save_every and cfg.checkpoint_dir:
+            self.saved.append(self.save(self.version))   # the final global parameters
         for r in self.ps_ranks:
             self.planes.send_hdr([CMD_DONE, self.task, self.version, 0], r)
+        if tr.logger is not None:
+            tr.logger.close()
         return hist
+
+    def save(self, gstep):
+        """The global actor/critic (this worker holds them right after its pull) under the reference names
+        ``global_actor/...`` / ``global_critic/...``: no Adam slots and no global step, as the reference's Saver
+        built before them."""
+        from .. import ckpt as C
+        from ..models.policy import MLPActorCritic
+        cfg, m = self.cfg, self.tr.model
+        d = cfg.checkpoint_dir
+        os.makedirs(d, exist_ok=True)
+        base = self.ckpt_base or ("model-" + C.env_prefix(cfg.env))
+        path = os.path.join(d, f"{base}-{gstep}")
+        if isinstance(m, MLPActorCritic):
+            t = C.reference_tensors(m.actor, m.critic, "a3c", actor_lr=cfg.lr, ent_coef=cfg.ent_coef,
+                                    kl_coef=cfg.kl_coef, critic_lr=cfg.critic_lr)
+        else:
+            t = C.generic_tensors(m)
+        C.save_tensors(path, t)
+        kept = C._prune(d, base, cfg.keep_checkpoints)
+        C._write_state_file(d, path, kept or [path])
+        return path
 
 
 def run(cfg, rank=None, world=None, ps_num=None, data_backend="gloo", max_staleness=-1, device=None,
-        report_every=0):
+        report_every=0, log_dir=None, logger=None, checkpoint_basename=None):
     """Entry point of one process of the GPU-native async job. The default process group (gloo) must exist or is
-    created from the torchrun environment; with ``data_backend="nccl"`` an RCCL group carries the payloads."""
+    created from the torchrun environment; with ``data_backend="nccl"`` an RCCL group carries the payloads.
+    ``log_dir``: per-worker Logger files ``worker_<task>.log`` (the reference's ``tmp/logs``)."""
+    import datetime
     if not dist.is_initialized():
         dist.init_process_group("gloo")
     rank = dist.get_rank() if rank is None else rank
     world = dist.get_world_size() if world is None else world
     ps_num = cfg.ps_num if ps_num is None else ps_num
     assert world - ps_num >= 1, "need at least one worker rank"
+    if cfg.max_grad_norm is not None:
+        raise ValueError("async PS mode clips element-wise only (A3C/policies.py:85); a global-norm clip "
+                         f"(max_grad_norm={cfg.max_grad_norm}) would be computed per PS shard: set it to None")
     device = torch.device(device or cfg.device)
     if device.type == "cuda":
         torch.cuda.set_device(device)
-    ctrl = dist.new_group(backend="gloo")
-    data = dist.new_group(backend="nccl") if data_backend == "nccl" else ctrl
+    tmo = datetime.timedelta(seconds=cfg.dist_timeout_s)
+    ctrl = dist.new_group(backend="gloo", timeout=tmo)
+    data = dist.new_group(backend="nccl", timeout=tmo) if data_backend == "nccl" else ctrl
     planes = _Planes(ctrl, data, data_backend, device)
     flat = _build_flat(cfg, torch.device("cpu"))
     ranges = shard_ranges(flat, ps_num)
@@ -258,14 +366,16 @@ def run(cfg, rank=None, world=None, ps_num=None, data_backend="gloo", max_stalen
     if rank < ps_num:
         ps = DeviceParameterServer(cfg, rank, ranges[rank], range(ps_num, world), planes, device, max_staleness)
         ps.serve()
-        return {"role": "ps", "global_step": ps.global_step, "log": ps.log, "n_applies": ps.n_applies,
+        return {"role": "ps", "status": ps.status, "error": getattr(ps, "error", None),
+                "global_step": ps.global_step, "log": ps.log, "n_applies": ps.n_applies,
                 "adam_t": {f"{k}:{w}": float(t) for (k, w), t in ps.t.items()}, "wall_s": time.time() - t0,
                 "params": ps.flat.data[ps.s:ps.e].detach().cpu()}
     task = rank - ps_num
-    w = GPUWorker(cfg, task, ranges, list(range(ps_num)), planes, device)
+    w = GPUWorker(cfg, task, ranges, list(range(ps_num)), planes, device, log_dir=log_dir, rank=rank, logger=logger,
+                  checkpoint_basename=checkpoint_basename)
     hist = w.run(cfg.total_updates, report_every)
     tr = w.tr
     ret, n_ep, _ = tr.env.drain_episode_stats()
     return {"role": "worker", "task": task, "global_step": w.version, "history": hist, "updates": len(hist),
             "env_steps": tr.env_steps, "wall_s": time.time() - t0, "ep_return": ret, "episodes": n_ep,
-            "returns": w.returns}
+            "returns": w.returns, "checkpoints": w.saved}

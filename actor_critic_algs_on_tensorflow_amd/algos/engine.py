@@ -326,8 +326,14 @@ class CNNEngine:
         self._wsplits["W1"] = P
         self._cur_planes["W1"] = P
 
-    def head_ok(self, B):
-        return self.fused_head and 2 <= self.A <= 7 and B <= 512
+    # limits of loss.hip head_bwd_kernel: B rows staged in LDS (HB_MAXB), the bootstrap row of N values after them
+    HB_MAXB, HB_MAXN = 512, 256
+
+    def head_ok(self, B, N):
+        """Gate of the fused A2C head (``head_bwd``): the same limits the kernel's launcher checks, so a config
+        outside them takes the loss + GEMM path instead of failing at launch."""
+        return (self.fused_head and 2 <= self.A <= 7 and 1 <= B <= self.HB_MAXB and 1 <= N <= self.HB_MAXN
+                and B % N == 0)
 
     def head_backward(self, b: _Bufs, actions, logp_old, ent_coef, kl_coef, vf_coef, stats, returns):
         """A2C fast path: ``head_bwd`` -- returns/EV/adv-norm + loss + dz and the head's backward (dh, dWh, dbh,
@@ -458,6 +464,20 @@ class CNNEngine:
 
     # ------------------------------------------------------------------------------------------------ finaliser
     want_parts = False   # set by the trainer when the optimiser may take the finaliser's sum-of-squares partials
+    defer_finalize = False   # set by the trainer: the finaliser runs inside the optimiser's launch (grad_finalize_opt)
+    _fin_pending = None
+
+    def take_finalize(self):
+        """The deferred finaliser job table (words, largest job) of the last backward, or None."""
+        p, self._fin_pending = self._fin_pending, None
+        return p
+
+    def flush_finalize(self):
+        """Runs a deferred finaliser as its own launch (the gradient slab is needed before an optimiser step:
+        data parallelism, the async-PS push, or a fused launch that was refused)."""
+        p = self.take_finalize()
+        if p is not None:
+            _native.require().grad_finalize(p[0], self.fin_parts)
 
     def finalize(self, b: _Bufs):
         """One launch after the backward (``grad_finalize``): reduces the per-sample conv bias-gradient rows
@@ -485,9 +505,12 @@ class CNNEngine:
                 elif self.want_parts:
                     segs.append((g.data_ptr(), 0, g.numel(), 0, 0))
             from ..ops.optim import finalize_jobs
-            words = finalize_jobs(segs, self.dev)
+            words = finalize_jobs(segs, self.dev, return_max=True)
             self._fin_words[key] = words
-        _native.require().grad_finalize(words, self.fin_parts)
+        if self.defer_finalize:
+            self._fin_pending = words
+            return
+        _native.require().grad_finalize(words[0], self.fin_parts)
 
     @staticmethod
     def dcol3(b):   # only the col2im data-gradient path materialises the column gradients

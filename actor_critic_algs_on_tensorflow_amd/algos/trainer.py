@@ -115,6 +115,7 @@ class ActorCriticTrainer:
         self.device = torch.device(cfg.device)
         self.dp = dp
         self.rank = dp.rank if dp is not None else 0
+        self.worker_id = self.rank   # Logger rows' worker column (an async PS worker sets its task id)
         self.world = dp.world_size if dp is not None else 1
         fs = 4 if ("Pong" in cfg.env or "Breakout" in cfg.env) else cfg.frames
         self.env = env if env is not None else E.make(
@@ -160,6 +161,8 @@ class ActorCriticTrainer:
             self.engine.want_parts = True
             for o in self.opts.values():
                 o.ext_parts = self.engine.fin_parts
+            # ... and the finaliser itself runs inside the optimiser's launch (grad_finalize_opt)
+            self.engine.defer_finalize = os.environ.get("ACA_FUSED_FINOPT", "1") != "0"
         T, N = cfg.n_steps, self.env.num_envs
         act_shape = () if self.env.is_discrete else tuple(self.env.action_space.shape)
         act_dtype = torch.int32 if self.env.is_discrete else torch.float32
@@ -440,10 +443,47 @@ class ActorCriticTrainer:
         else:
             self._rec.cut(fn)
 
+    def _inline_comm(self):
+        """DP collectives are recorded inside the update's hipGraph (RCCL) instead of cutting it (gloo)."""
+        return (self.dp is not None and self.dp.graph_capturable and self.cfg.dp_capture != "segments"
+                and self._grad_sink is None)
+
+    def _inline_dp_overlap(self):
+        """RCCL DP on the CNN engine: the gradient all-reduce is split into the fc/head bucket (all-reduced while
+        the conv backward runs) and the conv bucket. (Also with ``dp_capture="segments"``, where both are host
+        cuts, so the two capture modes run the same kernels and stay bitwise equal.)"""
+        return (self.engine is not None and self.dp is not None and self.dp.graph_capturable
+                and self._grad_sink is None and not self._defer_allreduce and self._bw_stage == "all")
+
+    def _backward_allreduce_overlapped(self, b, head_bias_done, head_done=False):
+        """Backward + gradient all-reduce + optimiser for RCCL data parallelism, as ONE stream-ordered sequence that
+        a hipGraph records whole (SURVEY §5.8): the head/fc backward makes the tail bucket (95 % of the bytes) final;
+        its all-reduce is issued on RCCL's stream (a forked branch of the graph) while the conv backward runs on the
+        compute stream; then the conv bucket is all-reduced and the compute stream joins both before the optimiser.
+        Nothing is issued from the host at replay time."""
+        eng, dp, g = self.engine, self.dp, self.flat.grad
+        eng.backward(b, head_bias_done=head_bias_done, stage="tail", head_done=head_done)
+        s, e = eng.tail_bucket()
+        dp.pack(g, s, e)
+        inline = self._inline_comm()
+        if inline:
+            w_tail = dp.allreduce_async(dp.comm_view(g, s, e))
+        else:
+            self._comm(lambda: dp.allreduce_packed(g, s, e))
+        eng.backward(b, head_bias_done=head_bias_done, stage="trunk")
+        dp.pack(g, 0, s)
+        self._comm(lambda: dp.allreduce_packed(g, 0, s))
+        if inline:
+            w_tail.wait()
+        dp.unpack(g)
+        self._run_optimizers()
+
     def _apply_grads(self):
         """All-reduce (DP) + optimiser step; inside a segmented capture the pre-graph stops before both."""
         if self._defer_allreduce:
             return
+        if self.engine is not None and (self._grad_sink is not None or self.dp is not None):
+            self.engine.flush_finalize()   # the slab itself is pushed / all-reduced
         if self._grad_sink is not None:   # async PS worker (a3c_gpu): push the gradient, pull the parameters
             self._comm(self._grad_sink)
             self._after_pull()
@@ -459,6 +499,11 @@ class ActorCriticTrainer:
         """Optimiser step(s). Several groups (the reference's separate actor / critic Adam) run as ONE launch, which
         also writes the MLP engine's transposed weight shadows; otherwise one launch per group (+ a shadow pass)."""
         opts = list(self.opts.values())
+        pend = self.engine.take_finalize() if self.engine is not None else None
+        if pend is not None:
+            if len(opts) == 1 and opts[0].step_finalize(pend[0], pend[1], self.engine.fin_parts):
+                return
+            _native.require().grad_finalize(pend[0], self.engine.fin_parts)
         if len(opts) > 1 and _native.use_native(self.flat.data):
             from ..ops.optim import FusedGroupStep
             if not hasattr(self, "_group_step"):
@@ -600,8 +645,10 @@ class ActorCriticTrainer:
         # the loss kernel writes its statistics straight into stats_buf[0:7]
         eng.loss(b, actions, logp_old, adv, ret, v_old if ppo else None, self.ent_coef, self.kl_coef, vf,
                  cfg.ppo_clip if ppo else 0.0, cfg.ppo_value_clip if ppo else 0.0, stats=self.stats_buf)
-        eng.backward(b, stage=self._bw_stage)   # gradient slab is clean: the optimiser zeroed it after its last use
         self._bw_pending = (b, False)
+        if self._inline_dp_overlap():
+            return self._backward_allreduce_overlapped(b, False)
+        eng.backward(b, stage=self._bw_stage)   # gradient slab is clean: the optimiser zeroed it after its last use
         self._apply_grads()
 
     @torch.no_grad()
@@ -620,16 +667,19 @@ class ActorCriticTrainer:
         rets = dict(mode=1 if cfg.returns == "nstep" else 2, rew=st.rewards, val=st.values, dones=st.dones,
                     L=T if cfg.look_ahead is None else cfg.look_ahead, gamma=cfg.gamma, lam=cfg.gae_lambda,
                     norm_adv=cfg.norm_adv, ret_w=self._ret_w, adv_w=self._adv_w)
-        if eng.head_ok(T * N):
+        head_done = eng.head_ok(T * N, N)
+        if head_done:
             # loss + dz + the head's backward (dh, dWh, dbh, dbfc) in one launch
             eng.head_backward(b, actions, logp_old, self.ent_coef, self.kl_coef, vf, self.stats_buf, rets)
-            eng.backward(b, head_bias_done=True, stage=self._bw_stage, head_done=True)
         else:
             eng.loss(b, actions, logp_old, None, None, None, self.ent_coef, self.kl_coef, vf, 0.0, 0.0,
                      stats=self.stats_buf, returns=rets)
-            eng.backward(b, head_bias_done=True, stage=self._bw_stage)
         self._bw_pending = (b, True)
-        self._apply_grads()
+        if self._inline_dp_overlap():
+            self._backward_allreduce_overlapped(b, True, head_done)
+        else:
+            eng.backward(b, head_bias_done=True, stage=self._bw_stage, head_done=head_done)
+            self._apply_grads()
         self._last = (obs, actions, logp_old, self._ret_w)
         if not self._defer_allreduce:
             self._finish_learn()
@@ -696,9 +746,13 @@ class ActorCriticTrainer:
             self._kl_and_lr(logp_old, logp, ret, z[:, eng.A])
 
     # ------------------------------------------------------------------ driver
-    # Without DP the whole update is ONE captured hipGraph. With DP (native engine, one optimiser step per update)
-    # the update is split into captured segments around the RCCL collectives, which are issued from the host between
-    # replays (async w.r.t. the host: the stream waits, the CPU does not):
+    # Without DP the whole update is ONE captured hipGraph. With RCCL data parallelism it is ONE graph too: every
+    # collective is recorded in it (RCCL calls are stream-ordered and capturable); the CNN engine's gradient
+    # all-reduce is split into the fc/head bucket, issued on RCCL's stream (a forked graph branch) while the conv
+    # backward runs, and the conv bucket (_backward_allreduce_overlapped). The host issues nothing per replay.
+    # Host-side collectives (gloo) cannot be captured, so there the update is split into captured segments around
+    # them, issued from the host between replays (async w.r.t. the host: the stream waits, the CPU does not); the
+    # same segment schedules serve RCCL lag-1 A2C, whose all-reduce spans two updates:
     #   overlap="strict" (exact synchronous A2C, the default):
     #       pre   = rollout + returns + loss + backward of the head and fc layers        (graph 1)
     #       AR(fc/head bucket, 95% of the bytes) on the RCCL stream    || mid = conv backward (graph 2)
@@ -719,7 +773,11 @@ class ActorCriticTrainer:
         return self.cfg.cuda_graph and self.device.type == "cuda"
 
     def _segmented(self):
+        """The A2C strict / lag-1 schedules with host-issued collectives between captured segments (gloo; and lag-1
+        under RCCL, whose all-reduce spans two updates). RCCL strict A2C is one graph (see _capture_set)."""
         cfg = self.cfg
+        if self._inline_comm() and not self._lag1():
+            return False
         return (self.dp is not None and cfg.algo == "a2c" and self.engine is not None and not cfg.norm_adv
                 and self.lr_ctrl is None and cfg.kl_coef == 0.0)
 
@@ -822,6 +880,13 @@ class ActorCriticTrainer:
             finally:
                 self._defer_allreduce = False
                 self._bw_stage = "all"
+        elif self._inline_comm():
+            # RCCL: every collective of the update (gradient buckets per optimiser step, the advantage moments, the
+            # KL scalar) is recorded in the graph -- one replay per update, zero host-issued collectives
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self.update_body()
+            graph = ("single", g)
         elif self.dp is not None or self._grad_sink is not None:
             rec = SegmentRecorder()
             self._rec = rec
@@ -912,7 +977,7 @@ class ActorCriticTrainer:
         avg_rew, n_ep, ep_len = self.env.drain_episode_stats()
         self.logger(i, act_loss=s["act_loss"], circ_loss=math.sqrt(max(s["crit_loss"], 0.0)), kl_dist=s["kl"],
                     avg_rew=avg_rew, print_tog=print_tog, act_lr=self.actor_opt.get_lr(), avg_ent=s["entropy"],
-                    worker_id=self.rank, ev_before=s["ev_before"], ev_after=s["ev_after"])
+                    worker_id=self.worker_id, ev_before=s["ev_before"], ev_after=s["ev_after"])
         s.update(avg_rew=avg_rew, episodes=n_ep, ep_len=ep_len)
         return s
 

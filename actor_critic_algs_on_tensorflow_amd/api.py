@@ -224,7 +224,12 @@ def evaluate(model_path, env_id, num_episodes=3, seed=12321, frames=1, animate=F
             total += float(r[0])
             length += 1
             obs = obs_next.clone()
-            if bool(d[0]) or length >= mpl:
+            if bool(d[0]):
+                break   # the bank auto-reset: obs already holds the next episode's first observation
+            if length >= mpl:
+                # cut by the loop bound without done: start the next episode fresh, as rollout() does with its
+                # env.reset() per episode (Basic_AC/run_AC.py:88)
+                obs = env.reset().clone()
                 break
         rewards.append(total)
         if verbose:

@@ -73,10 +73,9 @@ def main(argv=None):
         import torch
         from ..algos import a3c_gpu
         dev = args.device if ":" in args.device else f"cuda:{rank % max(1, torch.cuda.device_count())}"
-        cfg = cfg.replace(device=dev, num_envs=args.num_envs, n_steps=args.n_steps, cuda_graph=True,
-                          outdir=log if role == "worker" and task == 0 else None)
+        cfg = cfg.replace(device=dev, num_envs=args.num_envs, n_steps=args.n_steps, cuda_graph=True, outdir=None)
         out = a3c_gpu.run(cfg, rank=rank, world=world, ps_num=args.ps_num, data_backend=args.data_plane,
-                          max_staleness=args.max_staleness, device=dev)
+                          max_staleness=args.max_staleness, device=dev, log_dir=args.outdir)
     else:
         out = a3c.run(cfg, rank=rank, world=world, ps_num=args.ps_num, log_dir=args.outdir)
     dist.destroy_process_group()

@@ -322,8 +322,10 @@ def process_fn(cluster, task_id, job, env_id, logger, save_path, stdout_freq, ra
     if str(device).startswith("cuda"):
         from ..algos import a3c_gpu
         cfg = cfg.replace(device=device, num_envs=num_envs, n_steps=n_steps, cuda_graph=True, outdir=None)
+        # worker rows go to the caller's Logger, the chief writes checkpoints into save_path (A3C/process.py:211-214)
         return a3c_gpu.run(cfg, rank=rank, world=world, ps_num=num_ps, data_backend=data_plane,
-                           max_staleness=max_staleness, device=device)
+                           max_staleness=max_staleness, device=device, logger=logger,
+                           checkpoint_basename=checkpoint_basename)
     from ..algos import a3c
     return a3c.run(cfg, rank=rank, world=world, ps_num=num_ps, logger=logger, checkpoint_basename=checkpoint_basename)
 

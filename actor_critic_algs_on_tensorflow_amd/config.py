@@ -62,6 +62,9 @@ class TrainConfig:
     dist_backend: str = "auto"        # auto -> nccl (RCCL) on GPU, gloo on CPU
     overlap: str = "strict"           # strict | lag1 (all-reduce overlapped with next rollout, policy lag 1)
     grad_bucket_dtype: str = "fp32"   # fp32 | bf16 (all-reduce the gradient buckets as bf16: half the xGMI bytes)
+    dp_capture: str = "auto"          # auto: RCCL collectives recorded INSIDE the update's hipGraph (one graph per
+                                      # update); gloo (host-side collectives) -> a graph chain cut at each one |
+                                      # segments: force the graph chain (A/B and equivalence tests)
     ps_num: int = 1                   # A3C parameter-server ranks
     # -- reference episode-batched trainer (basic_ac) -------------------------------------------------------------
     max_rolls: int = 7

@@ -152,6 +152,22 @@ class FusedAdam:
         if self.shadow is not None:
             self.shadow.copy_(self.p)
 
+    def step_finalize(self, words, max_job_n, parts):
+        """Gradient finaliser + this update in ONE launch (``grad_finalize_opt``): the job table of the engine's
+        finaliser covers this group's whole slab range (single-group update, no data parallelism). Returns False
+        when the launch is not possible (the caller runs the finaliser and :meth:`step` instead)."""
+        if not _native.use_native(self.p) or self.clip_value is not None:
+            return False
+        if not hasattr(self, "_fin_state"):
+            self._fin_state = torch.zeros(4, dtype=torch.int32, device=self.p.device)
+        adam = not isinstance(self, FusedRMSprop)
+        b1, b2 = (self.b1, self.b2) if adam else (0.0, self.alpha)
+        return bool(_native.require().grad_finalize_opt(
+            words, int(max_job_n), parts, self.g, self.p, self.m if adam else None, self.v, self.shadow, self.lr,
+            self.t if adam else None, self.gnorm, -1.0,
+            float(self.max_grad_norm) if self.max_grad_norm is not None else -1.0, float(self.grad_mul), 1.0,
+            float(b1), float(b2), float(self.eps), adam, self._fin_state))
+
     def state_dict(self):
         return {"m": self.m, "v": self.v, "t": self.t, "lr": self.lr}
 
@@ -262,7 +278,7 @@ class FusedGroupStep:
 SUMSQ_PARTS = 256   # optim.hip: partial slots of the global-norm reduction = max finaliser workgroups
 
 
-def finalize_jobs(segments, device):
+def finalize_jobs(segments, device, return_max=False):
     """Job table of the gradient finaliser (``grad_finalize``): ``segments`` = [(dst_ptr, src_ptr, n, stride, S)]
     (``src_ptr`` 0: final already, read for the norm). Plane reductions are cut into 1024-element jobs (one float4
     per thread, a short chain of plane loads), per-sample bias rows (n <= 64) take one job each, and the read-only
@@ -296,7 +312,10 @@ def finalize_jobs(segments, device):
     for dst, src, n, stride, S in jobs:
         vec = int(dst % 16 == 0 and (not src or (src % 16 == 0 and stride % 4 == 0)))
         rows.append([dst, src, n, stride, S, vec, 0, 0])
-    return torch.tensor(rows, dtype=torch.int64).to(device)
+    words = torch.tensor(rows, dtype=torch.int64).to(device)
+    if return_max:   # the largest job (the fused finaliser + optimiser holds one job's elements in LDS)
+        return words, max(r[2] for r in rows)
+    return words
 
 
 def make_optimizer(name, flat, group, lr, clip_value=None, max_grad_norm=None, bf16_shadow=None):

@@ -60,6 +60,11 @@ class DataParallel:
             raise ValueError(f"compress must be None/'none'/'bf16', got {compress!r}")
         self.compress = compress
         self._cbuf = None
+        # RCCL ("nccl") collectives are stream-ordered and capturable: the trainer records them INSIDE its
+        # hipGraph (one graph per update, the collective as a graph node on RCCL's stream with event joins).
+        # gloo collectives run on the host, so a captured gloo update is a chain of graphs cut at each one.
+        self.backend = dist.get_backend(group)
+        self.issued = 0   # collectives issued from the host (a replayed one-graph update issues none)
 
     # -- gradient buckets (optionally bf16) ----------------------------------------------------------------------
     def prepare(self, grad):
@@ -87,6 +92,7 @@ class DataParallel:
     @torch.no_grad()
     def allreduce_packed(self, grad, s=0, e=None):
         """Synchronous (stream-ordered) SUM all-reduce of the packed range."""
+        self.issued += 1
         dist.all_reduce(self.comm_view(grad, s, e), op=dist.ReduceOp.SUM, group=self.group)
 
     # -- parameters ---------------------------------------------------------------------------------------------
@@ -95,6 +101,11 @@ class DataParallel:
         dist.broadcast(flat.data, src=src, group=self.group)
 
     # -- gradients ----------------------------------------------------------------------------------------------
+    @property
+    def graph_capturable(self):
+        """Collectives can be recorded inside a hipGraph (RCCL); gloo needs host-side cuts."""
+        return self.backend == "nccl"
+
     @property
     def grad_mul(self):
         """Factor the optimisers fold into their gradient read (1/world when averaging): the all-reduce leaves the
@@ -114,6 +125,7 @@ class DataParallel:
         """Issues the SUM all-reduce of ``buf`` (a contiguous slab segment) on the RCCL stream, ordered after the
         work already queued on the current stream, and returns the work handle. ``handle.wait()`` makes the
         *current stream* wait for it (no host block), so the caller keeps queueing compute that overlaps it."""
+        self.issued += 1
         return dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
     # -- statistics ---------------------------------------------------------------------------------------------
@@ -131,6 +143,7 @@ class DataParallel:
     def allreduce_sum_(self, t):
         """In-place SUM all-reduce of a small device tensor (e.g. the packed fp64 return-scan moments): no host
         round trip, capturable."""
+        self.issued += 1
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
         return t
 

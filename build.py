@@ -14,6 +14,7 @@ Usage: ``python build.py [-j N] [--clean] [--verbose]``.
 from __future__ import annotations
 
 import argparse
+import glob
 import os
 import shutil
 import subprocess
@@ -69,8 +70,9 @@ def write_ninja(verbose=False):
     w("rule link\n  command = $cxx $in $ldflags -o $out\n  description = LINK $out")
     w("rule tblink\n  command = $cxx -shared $in -o $out\n  description = LINK $out")
     objs = []
-    hdr = " ".join(os.path.join(ROOT, "csrc", "kernels", h)
-                   for h in ("common.h", "gemm_impl.h", "gemm_desc.h", "mlp_desc.h", "cnn_head.h"))
+    # every kernel header is an implicit dependency of every object (pong_env.h, cnn_head.h, ... are shared by
+    # several translation units; a stale object would silently diverge from the oracles)
+    hdr = " ".join(sorted(glob.glob(os.path.join(ROOT, "csrc", "kernels", "*.h"))))
     for k in KERNELS:
         src = os.path.join(ROOT, "csrc", "kernels", k + ".hip")
         obj = os.path.join(BUILD_DIR, k + ".o")

@@ -67,7 +67,7 @@ hipError_t aca_normalize_mom(const float*, float*, const double*, int, float, hi
 int aca_ev_multi_blocks(int);
 hipError_t aca_gemm_group_run(const AcaGemmDesc*, int, hipStream_t, int*);
 hipError_t aca_mb_gather(const uint8_t*, int64_t, const int*, const float*, const float*, const float*, const float*,
-                         uint8_t*, int*, float*, float*, float*, float*, int, int, uint32_t, const int64_t*, int, int,
+                         uint8_t*, int*, float*, float*, float*, float*, int, int, uint32_t, int64_t*, int, int,
                          const double*, float, unsigned int*, hipStream_t);
 hipError_t aca_ev_multi(const float*, const float*, float*, int, double*, unsigned int*, hipStream_t);
 hipError_t aca_conv1_wgrad(const uint8_t*, const uint16_t*, float*, int, int, float, hipStream_t);
@@ -98,6 +98,9 @@ hipError_t aca_cnn_trunk_fwd(const uint8_t*, const uint16_t*, const float*, cons
                              const uint16_t*, const float*, uint16_t*, uint16_t*, uint16_t*, int, float, uint8_t*,
                              uint64_t*, hipStream_t);
 hipError_t aca_grad_finalize(const int64_t*, int, float*, hipStream_t);
+hipError_t aca_grad_finalize_opt(const int64_t*, int, int, float*, float*, float*, float*, uint16_t*, const float*,
+                                 const float*, float*, float*, float, float, float, float, float, float, float, int,
+                                 unsigned int*, hipStream_t);
 hipError_t aca_head_bwd(const float*, const int32_t*, const float*, const float*, const float*, float, const float*,
                         const float*, const uint8_t*, int, int, int, int, int, float, float, float*, float*,
                         const uint16_t*, const uint16_t*, uint16_t*, float*, float*, float*, float*, int,
@@ -1195,6 +1198,46 @@ void grad_finalize(Tensor jobs, Tensor partial) {
         "grad_finalize");
 }
 
+// Finaliser + optimiser in one launch (optim.hip grad_finalize_opt_kernel): the jobs of grad_finalize, then the
+// clip + Adam (m, t given) / RMSprop (b2 = alpha) update of every job's slab range from the LDS copy. `grad` is the
+// gradient slab segment the job dst pointers point into; p / m / v / shadow are the matching parameter-side
+// segments. Returns false (nothing launched) when the job table cannot be resident at once (the caller then runs
+// the two separate launches).
+bool grad_finalize_opt(Tensor jobs, int64_t max_job_n, Tensor partial, Tensor grad, Tensor p, c10::optional<Tensor> m,
+                       Tensor v, c10::optional<Tensor> shadow, Tensor lr, c10::optional<Tensor> t,
+                       c10::optional<Tensor> gnorm_out, double clip, double max_norm, double gmul, double norm_mul,
+                       double b1, double b2, double eps, bool adam, Tensor state) {
+  need(jobs, at::kLong, "jobs");
+  TORCH_CHECK(jobs.dim() == 2 && jobs.size(1) == 8 && jobs.is_contiguous(), "grad_finalize_opt: jobs [njobs, 8]");
+  for (auto* x : {&partial, &grad, &p, &v, &lr}) need(*x, at::kFloat, "grad_finalize_opt f32 operand");
+  need(state, at::kInt, "state");
+  TORCH_CHECK(state.numel() >= 3, "grad_finalize_opt: state needs 3 words");
+  TORCH_CHECK(grad.numel() == p.numel() && v.numel() == p.numel(), "grad_finalize_opt: size mismatch");
+  TORCH_CHECK(partial.numel() >= aca_sumsq_parts() && jobs.size(0) <= aca_sumsq_parts(),
+              "grad_finalize_opt: partial too small / too many jobs");
+  float* mp = nullptr;
+  float* tp = nullptr;
+  if (adam) {
+    TORCH_CHECK(m.has_value() && t.has_value(), "grad_finalize_opt: Adam needs m and t");
+    need(*m, at::kFloat, "m");
+    need(*t, at::kFloat, "t");
+    TORCH_CHECK(m->numel() == p.numel(), "grad_finalize_opt: m size mismatch");
+    mp = ptr<float>(*m);
+    tp = ptr<float>(*t);
+  }
+  const hipError_t e = aca_grad_finalize_opt(
+      jobs.data_ptr<int64_t>(), (int)jobs.size(0), (int)max_job_n, ptr<float>(partial), ptr<float>(p), mp,
+      ptr<float>(v), shadow_ptr(shadow, p, "grad_finalize_opt"), ptr<float>(grad), ptr<float>(lr), tp,
+      optr<float>(gnorm_out), (float)clip, (float)max_norm, (float)gmul, (float)norm_mul, (float)b1, (float)b2,
+      (float)eps, adam ? 1 : 0, reinterpret_cast<unsigned int*>(state.data_ptr<int32_t>()), cur_stream(p));
+  if (e == hipErrorInvalidValue) {
+    (void)hipGetLastError();
+    return false;
+  }
+  check(e, "grad_finalize_opt");
+  return true;
+}
+
 // A2C learner head in one launch (loss.hip head_bwd_kernel): returns + EV + advantage normalisation + loss + dz,
 // then dh = (h > 0) * dz Wh^T, dbfc, dWh, dbh written straight into their gradient slots (deterministic).
 void head_bwd(Tensor z, Tensor act, Tensor logp_old, Tensor ent_coef, Tensor kl_coef, double vf_coef, Tensor rew,
@@ -1437,6 +1480,9 @@ TORCH_LIBRARY(acamd, m) {
   m.def("cnn_trunk_bwd(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tensor dy2, Tensor dy1, "
         "Tensor biasp, Tensor? stamps=None, int persist=0) -> ()");
   m.def("grad_finalize(Tensor jobs, Tensor partial) -> ()");
+  m.def("grad_finalize_opt(Tensor jobs, int max_job_n, Tensor partial, Tensor grad, Tensor p, Tensor? m, Tensor v, "
+        "Tensor? shadow, Tensor lr, Tensor? t, Tensor? gnorm_out, float clip, float max_norm, float gmul, "
+        "float norm_mul, float b1, float b2, float eps, bool adam, Tensor state) -> bool");
   m.def("head_bwd(Tensor z, Tensor act, Tensor logp_old, Tensor ent_coef, Tensor kl_coef, float vf_coef, Tensor rew, "
         "Tensor val, Tensor dones, int L, int returns_mode, bool norm_adv, float gamma, float lam, Tensor ret_w, "
         "Tensor adv_w, Tensor h, Tensor Wh, Tensor dh, Tensor gWh, Tensor gbh, Tensor gbfc, Tensor stats, "
@@ -1490,6 +1536,7 @@ TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
   m.impl("fc_value", &fc_value);
   m.impl("cnn_trunk_bwd", &cnn_trunk_bwd);
   m.impl("grad_finalize", &grad_finalize);
+  m.impl("grad_finalize_opt", &grad_finalize_opt);
   m.impl("head_bwd", &head_bwd);
   m.impl("im2col_u8", &im2col_u8);
   m.impl("im2col_nhwc", &im2col_nhwc);

@@ -113,7 +113,7 @@ __global__ void __launch_bounds__(256) mb_gather_kernel(const uint8_t* __restric
                                                         int* __restrict__ o_act, float* __restrict__ o_logp,
                                                         float* __restrict__ o_adv, float* __restrict__ o_ret,
                                                         float* __restrict__ o_v, int n, uint32_t seed,
-                                                        const int64_t* __restrict__ uc, int ep, int off,
+                                                        int64_t* uc, int ep, int off,
                                                         const double* __restrict__ mom, float eps,
                                                         unsigned int* __restrict__ bump_ticket) {
   const int i = blockIdx.x;
@@ -153,7 +153,7 @@ __global__ void __launch_bounds__(256) mb_gather_kernel(const uint8_t* __restric
     if (threadIdx.x == 0) {
       const unsigned int prev = __hip_atomic_fetch_add(bump_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (prev == gridDim.x - 1u) {
-        *const_cast<int64_t*>(uc) = ucv + 1;
+        *uc = ucv + 1;
         __hip_atomic_store(bump_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
@@ -576,7 +576,7 @@ extern "C" hipError_t aca_ev_multi(const float* x, const float* y, float* out, i
 extern "C" hipError_t aca_mb_gather(const uint8_t* obs, int64_t R, const int* act, const float* logp, const float* adv,
                                     const float* ret, const float* v, uint8_t* o_obs, int* o_act, float* o_logp,
                                     float* o_adv, float* o_ret, float* o_v, int mb, int n, uint32_t seed,
-                                    const int64_t* uc, int ep, int off, const double* mom, float eps,
+                                    int64_t* uc, int ep, int off, const double* mom, float eps,
                                     unsigned int* bump_ticket, hipStream_t stream) {
   if (mb <= 0) return hipSuccess;
   aca::mb_gather_kernel<<<mb, 256, 0, stream>>>(obs, R, act, logp, adv, ret, v, o_obs, o_act, o_logp, o_adv, o_ret,

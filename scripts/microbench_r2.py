@@ -83,7 +83,7 @@ def main():
                workspace=eng.ws, ga=[5, B, 64, 20, 20, 4, 4, 2], gb=[6, 1, 64, 1, 32, 4, 4, 2])
     cands["bwd_gemms_dy2_dy1"] = gemms
     cands["finalize_engine"] = lambda: eng.finalize(lb)
-    fw = list(eng._fin_words.values())[-1]
+    fw = list(eng._fin_words.values())[-1][0]
     bias_w = fw[(fw[:, 1] != 0) & (fw[:, 2] <= 64)].clone()
     plane_w = fw[(fw[:, 1] != 0) & (fw[:, 2] > 64)].clone()
     ro_w = fw[fw[:, 1] == 0].clone()

@@ -28,17 +28,24 @@ def _cfg(device, total, **kw):
 
 
 def _proc(rank, world, port, out, device, total, ps_num, staleness, kw, report=0):
+    import datetime
     import torch.distributed as dist
     from actor_critic_algs_on_tensorflow_amd.algos import a3c_gpu
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     if device.startswith("cuda"):
         torch.cuda.set_device(0)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    kw = dict(kw)
+    log_dir = kw.pop("_log_dir", None)
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=kw.get("dist_timeout_s", 300)))
     try:
         res = a3c_gpu.run(_cfg(device, total, **kw), ps_num=ps_num, data_backend="gloo", max_staleness=staleness,
-                          device=device, report_every=report)
+                          device=device, report_every=report, log_dir=log_dir)
         torch.save(res, os.path.join(out, f"r{rank}.pt"))
-        dist.barrier()
+        if not kw.get("fault_inject"):
+            dist.barrier()
+    except RuntimeError as e:   # a surviving worker of a job whose PS aborted
+        torch.save({"role": "worker", "error": repr(e)}, os.path.join(out, f"r{rank}.pt"))
     finally:
         dist.destroy_process_group()
 
@@ -110,6 +117,58 @@ def test_a3c_gpu_worker_learns_pendulum(cuda, tmp_path):
     # measured: -1512 -> -1410 -> -1238 -> -1229 -> -1229 and, with an optimiser build that rounds differently,
     # -1318 -> -1241 -> -1227 -> -1229 -> -1229: both settle on the same plateau from different first reports
     assert max(rets[2:]) > rets[0] + 50 and max(rets[2:]) > -1260, rets
+
+
+def test_a3c_gpu_mode_chief_checkpoints_and_worker_logs_cpu(tmp_path):
+    """A3C/process.py:211-214,280-283: the chief writes the GLOBAL actor/critic under the reference names every
+    save_every global steps (evaluable by cli/test_model.py), every worker keeps a reference-format log file."""
+    from actor_critic_algs_on_tensorflow_amd import ckpt
+    from actor_critic_algs_on_tensorflow_amd.api import evaluate
+    ck = tmp_path / "ck"
+    res = _run(tmp_path, 3, staleness=-1, total=9, save_every=4, checkpoint_dir=str(ck), stdout_freq=1,
+               flush_every=2, _log_dir=str(tmp_path / "logs"))
+    ps, w0, w1 = res
+    assert ps["status"] == "ok"
+    latest = ckpt.latest_checkpoint(str(ck))
+    assert latest is not None and latest.endswith("-%d" % w0["global_step"]), (latest, w0["global_step"])
+    t = ckpt.load_tensors(latest)
+    assert "global_actor/first_layer/kernel" in t and "global_critic/value/bias" in t
+    # the chief's final checkpoint holds the PS parameters (its last pull)
+    assert len(w0["checkpoints"]) >= 2 and not w1["checkpoints"]
+    rewards = evaluate(latest, "Pendulum-v0", num_episodes=1, verbose=False, max_path_length=20)
+    assert len(rewards) == 1
+    for task in (0, 1):
+        rows = open(tmp_path / "logs" / f"worker_{task}.log").read().splitlines()
+        assert rows[0].split()[:3] == ["step", "avg_rew", "ev_before"] and len(rows) > 1
+
+
+def test_a3c_gpu_mode_worker_death_aborts_cleanly_cpu(tmp_path):
+    """a worker dying mid-run (no DONE message) makes the PS return "aborted" instead of serving
+    forever, and the surviving worker's next exchange fails -- every process ends, nothing hangs."""
+    import multiprocessing
+    from actor_critic_algs_on_tensorflow_amd.algos.trainer import FAULT_EXIT_CODE
+    ctx = multiprocessing.get_context("spawn")
+    port = _free_port()
+    # rank 2 (worker 1) dies when it reaches its 3rd iteration
+    args = (3, port, str(tmp_path), "cpu", 40, 1, -1, dict(fault_inject="2:3", dist_timeout_s=30))
+    procs = [ctx.Process(target=_proc, args=(r,) + args) for r in range(3)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(150)
+    alive = [p.is_alive() for p in procs]
+    for p in procs:   # the exact child objects, never a pattern
+        if p.is_alive():
+            p.kill()
+    assert not any(alive), "a process of the job hung after a worker died"
+    assert procs[2].exitcode == FAULT_EXIT_CODE
+    ps = torch.load(tmp_path / "r0.pt", weights_only=False)
+    assert ps["role"] == "ps" and ps["status"] == "aborted", ps.get("status")
+    # the dead worker's applies stop at its fault; the survivor either finished the job through the PS or got an
+    # error from its exchange -- both are clean ends
+    assert ps["n_applies"][2] <= 3
+    w0 = torch.load(tmp_path / "r1.pt", weights_only=False)
+    assert "error" in w0 or w0["global_step"] >= 40
 
 
 def _pf_proc(rank, port, d):

@@ -33,3 +33,20 @@ def test_no_cuda_compat_layers():
             if pat in txt:
                 bad.append((os.path.basename(path), pat))
     assert not bad, bad
+
+
+def test_fused_head_gate_matches_kernel_limits():
+    """the Python gate of the fused A2C head (engine.head_ok) applies the same limits as the kernel's
+    launcher (loss.hip aca_head_bwd: B <= 512 rows, N <= 256 envs, 2..7 actions), so e.g. n_steps=1 with 300 envs
+    takes the loss + GEMM path instead of failing at launch."""
+    from actor_critic_algs_on_tensorflow_amd.algos.engine import CNNEngine
+    eng = CNNEngine.__new__(CNNEngine)
+    eng.fused_head, eng.A = True, 6
+    assert eng.head_ok(160, 32)
+    assert eng.head_ok(512, 256)
+    assert not eng.head_ok(300, 300)     # one step of 300 envs: N > 256
+    assert not eng.head_ok(640, 128)     # B > 512
+    eng.A = 8
+    assert not eng.head_ok(160, 32)
+    src = open(os.path.join(ROOT, "csrc", "kernels", "loss.hip")).read()
+    assert "B > aca::HB_MAXB || N > 256" in src and "constexpr int HB_MAXB = 512;" in src

@@ -165,3 +165,61 @@ def test_dp_bf16_buckets_track_fp32(cuda, tmp_path, overlap):
         assert torch.equal(a, b), "ranks diverged"
     for d_b, d_f in zip(_deltas(b16[0]["snaps"]), _deltas(f32[0]["snaps"])):
         assert _cos(d_b, d_f) > 0.97, _cos(d_b, d_f)
+
+
+# ---------------------------------------------------------------------------------------------- RCCL, in-graph
+def _rccl_worker(port, out_dir, name, kw, modes):
+    """One process, an RCCL ("nccl") group of world 1 on cuda:0: the same DP update captured with the collectives
+    INSIDE one hipGraph (``dp_capture="auto"``) and as the host-cut segment chain (``"segments"``)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ACAMD_GEMM_TUNE="0")
+    import torch.distributed as dist
+    from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
+    from actor_critic_algs_on_tensorflow_amd.parallel.dp import DataParallel
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        res = {}
+        for mode in modes:
+            dp = DataParallel()
+            assert dp.backend == "nccl"
+            tr = ActorCriticTrainer(_cfg(kw_envs(name), "strict", name, dp_capture=mode, **kw), dp=dp)
+            tr.capture(warmup=1)
+            kind = tr.graph[0]
+            n_graphs = tr.graph[1].n_graphs if kind == "segments" else 1
+            issued = dp.issued
+            snaps = []
+            for _ in range(UPDATES):
+                tr.step()
+                torch.cuda.synchronize()
+                snaps.append(tr.flat.data.cpu().clone())
+            res[mode] = {"kind": kind, "n_graphs": n_graphs, "host_collectives": dp.issued - issued,
+                         "snaps": snaps}
+        torch.save(res, os.path.join(out_dir, f"rccl_{name}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def kw_envs(name):
+    return {"pong_a2c": 16, "breakout_ppo": 4, "mujoco_ppo_dp8": 8}[name]
+
+
+@pytest.mark.parametrize("name,kw", [
+    ("pong_a2c", {}),
+    ("breakout_ppo", dict(n_steps=8, ppo_epochs=2, ppo_minibatches=2, kl_adaptive_lr=True, kl_coef=0.05)),
+    ("mujoco_ppo_dp8", dict(n_steps=16, ppo_epochs=2, ppo_minibatches=4, kl_adaptive_lr=True, kl_coef=0.05)),
+])
+def test_rccl_dp_update_is_one_graph(cuda, tmp_path, name, kw):
+    """RCCL data parallelism (world 1 here; the driver's node runs 2-8): the whole DP update -- per-minibatch
+    gradient all-reduces (CNN: fc/head bucket overlapped with the conv backward), the advantage moments, the KL
+    scalar -- is ONE captured hipGraph whose replay issues zero collectives from the host, and it is BITWISE equal
+    to the segment-chain capture of the same update (host-issued collectives between graphs)."""
+    mp.spawn(_rccl_worker, args=(_free_port(), str(tmp_path), name, dict(kw), ["auto", "segments"]), nprocs=1,
+             join=True)
+    res = torch.load(tmp_path / f"rccl_{name}.pt", weights_only=True)
+    one, seg = res["auto"], res["segments"]
+    assert one["kind"] == "single", one["kind"]
+    assert one["host_collectives"] == 0, one["host_collectives"]
+    assert seg["host_collectives"] > 0 and seg["n_graphs"] > 1
+    for k, (a, b) in enumerate(zip(one["snaps"], seg["snaps"])):
+        assert torch.equal(a, b), (k, _cos(a, b))
+    assert not torch.equal(one["snaps"][0], one["snaps"][-1])

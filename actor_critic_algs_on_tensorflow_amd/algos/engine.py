@@ -121,8 +121,11 @@ class CNNEngine:
         self.conv1_planes = int(os.environ.get("ACA_CONV1_PLANES", "128"))
         # conv2 / conv3 weight gradients by the per-sample NHWC kernel (conv_wgrad.hip) from this many rows up
         self.nhwc_wgrad_min_b = int(os.environ.get("ACA_NHWC_WGRAD_MIN_B", "1024"))
+        self.wgrad_gemm = os.environ.get("ACA_WGRAD_GEMM", "1") != "0"
         self.nhwc3_wgrad_min_b = int(os.environ.get("ACA_NHWC3_WGRAD_MIN_B", str(self.nhwc_wgrad_min_b)))
-        self.nhwc_planes = int(os.environ.get("ACA_NHWC_PLANES", "128"))
+        # (the batched-position kernel's grid is one workgroup per plane: 256 planes cover the CUs)
+        self.nhwc_planes = int(os.environ.get("ACA_NHWC_PLANES",
+                                              "256" if os.environ.get("ACA_WGRAD_GEMM", "1") != "0" else "128"))
         # conv3's per-sample work is small (2 k-steps x 12 column tiles), so its grid (3 workgroups per plane) needs
         # more planes than conv2 to cover the CUs
         self.nhwc3_planes = int(os.environ.get("ACA_NHWC3_PLANES", "256"))
@@ -304,10 +307,12 @@ class CNNEngine:
         if buf is None or buf.numel() < P * 64 * n:
             buf = torch.zeros(max(P, self.wgrad_planes) * 64 * n, dtype=torch.float32, device=self.dev)
             self._planes[name] = buf
+        # batched-position MFMA 32x32x16 kernel (default) or the per-sample kernel (ACA_WGRAD_GEMM=0)
+        fn = _native.require().conv_wgrad_gemm if self.wgrad_gemm else _native.require().conv_wgrad_nhwc
         if name == "W2":
-            _native.require().conv_wgrad_nhwc(2, b.y1, b.dy2, buf, P)
+            fn(2, b.y1, b.dy2, buf, P)
         else:
-            _native.require().conv_wgrad_nhwc(3, b.y2, b.dy3, buf, P)
+            fn(3, b.y2, b.dy3, buf, P)
         self._wsplits[name] = P
         self._cur_planes[name] = P
 

@@ -72,6 +72,7 @@ hipError_t aca_mb_gather(const uint8_t*, int64_t, const int*, const float*, cons
 hipError_t aca_ev_multi(const float*, const float*, float*, int, double*, unsigned int*, hipStream_t);
 hipError_t aca_conv1_wgrad(const uint8_t*, const uint16_t*, float*, int, int, float, hipStream_t);
 hipError_t aca_conv_wgrad_nhwc(int, const uint16_t*, const uint16_t*, float*, int, int, hipStream_t);
+hipError_t aca_conv_wgrad_gemm(int, const uint16_t*, const uint16_t*, float*, int, int, hipStream_t);
 hipError_t aca_sumsq(const float*, size_t, float*, hipStream_t);
 int aca_sumsq_parts();
 hipError_t aca_adam_step(float*, float*, float*, float*, size_t, const float*, float*, const float*, float*, uint16_t*,
@@ -548,6 +549,25 @@ void conv_wgrad_nhwc(int64_t layer, Tensor img, Tensor dy, Tensor planes, int64_
   check(aca_conv_wgrad_nhwc((int)layer, ptr<uint16_t>(img), ptr<uint16_t>(dy), ptr<float>(planes), (int)B, (int)P,
                             cur_stream(img)),
         "conv_wgrad_nhwc");
+}
+
+// Same planes from the batched-position MFMA 32x32x16 kernel (conv_wgrad.hip conv_wgrad_gemm_kernel): grid P, every
+// workgroup owns its whole plane.
+void conv_wgrad_gemm(int64_t layer, Tensor img, Tensor dy, Tensor planes, int64_t P) {
+  need(img, at::kBFloat16, "conv_wgrad_gemm img");
+  need(dy, at::kBFloat16, "conv_wgrad_gemm dy");
+  need(planes, at::kFloat, "conv_wgrad_gemm planes");
+  TORCH_CHECK(layer == 2 || layer == 3, "conv_wgrad_gemm: layer 2 or 3");
+  const int64_t img_per = layer == 2 ? 400 * 32 : 81 * 64, dy_per = layer == 2 ? 81 * 64 : 49 * 64;
+  const int64_t ncol = layer == 2 ? 512 : 576;
+  const int64_t B = dy.numel() / dy_per;
+  TORCH_CHECK(B >= 1 && dy.numel() == B * dy_per && img.numel() == B * img_per, "conv_wgrad_gemm: shapes");
+  TORCH_CHECK(P >= 1 && P <= 1024 && planes.numel() >= P * 64 * ncol, "conv_wgrad_gemm: planes too small");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(img.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(dy.data_ptr()) % 16 == 0,
+              "conv_wgrad_gemm: 16-byte aligned operands");
+  check(aca_conv_wgrad_gemm((int)layer, ptr<uint16_t>(img), ptr<uint16_t>(dy), ptr<float>(planes), (int)B, (int)P,
+                            cur_stream(img)),
+        "conv_wgrad_gemm");
 }
 
 // PPO minibatch k of epoch ep: rows prp_index(off + i, n, key(seed, *uc, ep)) of the rollout gathered in one launch.
@@ -1433,6 +1453,7 @@ TORCH_LIBRARY(acamd, m) {
   m.def("gemm_group_pause(bool paused) -> ()", &gemm_group_pause);
   m.def("conv1_wgrad(Tensor obs, Tensor dy1, Tensor planes, int P, float scale) -> ()");
   m.def("conv_wgrad_nhwc(int layer, Tensor img, Tensor dy, Tensor planes, int P) -> ()");
+  m.def("conv_wgrad_gemm(int layer, Tensor img, Tensor dy, Tensor planes, int P) -> ()");
   m.def("mb_gather(Tensor obs, Tensor act, Tensor logp, Tensor adv, Tensor ret, Tensor v, Tensor o_obs, "
         "Tensor o_act, Tensor o_logp, Tensor o_adv, Tensor o_ret, Tensor o_v, int seed, Tensor uc, int ep, "
         "int off, Tensor? mom=None, float eps=1e-8, Tensor? bump_ticket=None) -> ()");
@@ -1519,6 +1540,7 @@ TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
   m.impl("mb_gather", &mb_gather);
   m.impl("conv1_wgrad", &conv1_wgrad);
   m.impl("conv_wgrad_nhwc", &conv_wgrad_nhwc);
+  m.impl("conv_wgrad_gemm", &conv_wgrad_gemm);
   m.impl("moments", &moments);
   m.impl("sumsq", &sumsq);
   m.impl("adam_step", &adam_step);

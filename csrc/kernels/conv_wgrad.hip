@@ -308,6 +308,166 @@ __global__ void __launch_bounds__(512) conv_wgrad_nhwc_kernel(const u16* __restr
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------------------------
+// Batched-position weight gradient of a bf16 NHWC conv layer on the 32x32x16 MFMA (large learner batches):
+//   dW[o][n] = sum_P dy[P][o] * col[P][n],   P = (sample, oy, ox) over the workgroup's samples,
+//                                              n = (ky, kx, c),  col[P][n] = img[sample][S oy + ky][S ox + kx][c]
+// i.e. ONE GEMM with M = 64 output channels, N = KS KS C, K = the positions of SB samples at a time (positions of
+// consecutive samples are consecutive K rows -- no per-sample padding of the 49 / 81 positions to a k-step). The
+// per-sample kernel above multiplies 12-16 MFMAs per wave per staged sample and spends its time staging and at
+// barriers; here every workgroup owns ALL 64 x N outputs of its plane (8 waves: wave w holds m-tile w & 1 and the
+// n-tiles (w >> 1) + 4 i, 32x32 fp32 accumulators in registers), stages SB samples per LDS fill (the next fill is in
+// flight in registers meanwhile) and runs KP / 16 k-steps of 4-5 MFMAs per wave between two barriers. Both MFMA
+// operands come from K-major LDS rows through the transposing ds_read_b64_tr_b16: A = dy rows (position-major,
+// 64 channels), B = the implicit im2col -- each lane points its read at the 4 contiguous channels of its
+// (position, ky, kx, c0) pixel, no column matrix. Plane g (samples [g B / P, (g + 1) B / P)) is written once, in
+// full; the gradient finaliser reduces the P planes in plane order (deterministic, no atomics).
+// ---------------------------------------------------------------------------------------------------------------
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+template <int H, int W, int C, int KS, int S, int OH, int OW, int SB>
+__global__ void __launch_bounds__(512) conv_wgrad_gemm_kernel(const u16* __restrict__ img,
+                                                              const u16* __restrict__ dy,
+                                                              float* __restrict__ planes, int B, int P) {
+  constexpr int T = 512;
+  constexpr int NPOS = OH * OW, NCOL = KS * KS * C;
+  constexpr int GP = SB * NPOS, KST = (GP + 15) / 16, KP = KST * 16;
+  constexpr int LDI = C + 8, LDD = 72, IMG_E = H * W * LDI;
+  constexpr int NT = NCOL / 32;                         // n tiles of 32
+  constexpr int TPW = (NT + 3) / 4;                     // n tiles per wave (wave pairs share an n tile set)
+  constexpr int CPP = C / 8;                            // 16-byte chunks per pixel
+  constexpr int IMG4 = SB * H * W * CPP, DY4 = SB * NPOS * 8;
+  constexpr int IPER = (IMG4 + T - 1) / T, DPER = (DY4 + T - 1) / T;
+  static_assert(NCOL % 32 == 0 && C % 16 == 0, "tile shapes");
+  __shared__ __attribute__((aligned(16))) u16 s_img[SB * IMG_E + 8];   // + a zero chunk for padding positions
+  __shared__ __attribute__((aligned(16))) u16 s_dy[KP * LDD];
+  const int g = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int b0 = (int)((int64_t)g * B / P), b1 = (int)((int64_t)(g + 1) * B / P);
+  const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
+  // padding rows GP..KP of the dy image and the zero chunk: written once, never restaged
+  for (int c = tid; c < (KP - GP) * (LDD / 8); c += T) *reinterpret_cast<uint4*>(s_dy + GP * LDD + c * 8) = z4;
+  if (tid == 0) *reinterpret_cast<uint4*>(s_img + SB * IMG_E) = z4;
+
+  // the next fill in flight in NAMED registers (arrays of uint4 here were placed in scratch / LDS by the compiler)
+  static_assert(IPER <= 8 && DPER <= 3, "register set holds 8 image + 3 dy chunks per thread");
+  uint4 ri0 = z4, ri1 = z4, ri2 = z4, ri3 = z4, ri4 = z4, ri5 = z4, ri6 = z4, ri7 = z4, rd0 = z4, rd1 = z4, rd2 = z4;
+#define CWG_LDI(R, u)                                                                                     \
+  if ((u) < IPER) {                                                                                       \
+    const int c = min(tid + (u) * T, IMG4 - 1);                                                           \
+    const int sm = c / (H * W * CPP), r = c - sm * (H * W * CPP);                                         \
+    R = reinterpret_cast<const uint4*>(img + (size_t)min(bs + sm, b1 - 1) * H * W * C)[r];                \
+  }
+#define CWG_LDD(R, u)                                                                                     \
+  if ((u) < DPER) {                                                                                       \
+    const int c = min(tid + (u) * T, DY4 - 1);                                                            \
+    const int sm = c / (NPOS * 8), r = c - sm * (NPOS * 8);                                               \
+    const uint4 v = reinterpret_cast<const uint4*>(dy + (size_t)min(bs + sm, b1 - 1) * NPOS * 64)[r];     \
+    R = bs + sm < b1 ? v : z4;                                                                            \
+  }
+  // samples bs .. bs + SB - 1 -> registers (past b1: the image of sample b1 - 1, zero dy rows)
+#define CWG_LOAD(bs_)                                                                                     \
+  {                                                                                                       \
+    const int bs = (bs_);                                                                                 \
+    CWG_LDI(ri0, 0) CWG_LDI(ri1, 1) CWG_LDI(ri2, 2) CWG_LDI(ri3, 3)                                       \
+    CWG_LDI(ri4, 4) CWG_LDI(ri5, 5) CWG_LDI(ri6, 6) CWG_LDI(ri7, 7)                                       \
+    CWG_LDD(rd0, 0) CWG_LDD(rd1, 1) CWG_LDD(rd2, 2)                                                       \
+  }
+#define CWG_STI(R, u)                                                                                     \
+  if ((u) < IPER && tid + (u) * T < IMG4) {                                                               \
+    const int c = tid + (u) * T;                                                                          \
+    const int sm = c / (H * W * CPP), r = c - sm * (H * W * CPP);                                         \
+    const int px = r / CPP, part = r - px * CPP;                                                          \
+    *reinterpret_cast<uint4*>(s_img + sm * IMG_E + px * LDI + part * 8) = R;                              \
+  }
+#define CWG_STD(R, u)                                                                                     \
+  if ((u) < DPER && tid + (u) * T < DY4) {                                                                \
+    const int c = tid + (u) * T;                                                                          \
+    *reinterpret_cast<uint4*>(s_dy + (c >> 3) * LDD + (c & 7) * 8) = R;                                   \
+  }
+#define CWG_STORE()                                                                                       \
+  {                                                                                                       \
+    CWG_STI(ri0, 0) CWG_STI(ri1, 1) CWG_STI(ri2, 2) CWG_STI(ri3, 3)                                       \
+    CWG_STI(ri4, 4) CWG_STI(ri5, 5) CWG_STI(ri6, 6) CWG_STI(ri7, 7)                                       \
+    CWG_STD(rd0, 0) CWG_STD(rd1, 1) CWG_STD(rd2, 2)                                                       \
+  }
+
+  floatx16 acc[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+  // lane roles in the transposing reads: 16-lane group gl, lane 4q + p of the group; a group covers 16 columns
+  const int gl = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3;
+  const int mt = wid & 1, nb = wid >> 1;
+  const int acol = mt * 32 + (gl & 1) * 16 + 4 * p4;   // dy column block of this lane's A read
+  const int khalf = 8 * (gl >> 1);
+  int noff[TPW];                                        // (ky, kx, c0) pixel offset of this lane's B columns
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    const int nt = min(nb + 4 * t, NT - 1);
+    const int n0 = nt * 32 + (gl & 1) * 16 + 4 * p4;
+    const int kyx = n0 / C, c0 = n0 - kyx * C, ky = kyx / KS, kx = kyx - ky * KS;
+    noff[t] = (ky * W + kx) * LDI + c0;
+  }
+  typedef short short4x __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) short4x lds4;
+  auto pos_off = [&](int Pk) -> int {   // LDS element offset of pixel (S oy, S ox) of position Pk; padding -> zero
+    if (Pk >= GP) return SB * IMG_E;
+    const int sm = Pk / NPOS, pp = Pk - sm * NPOS, oy = pp / OW, ox = pp - oy * OW;
+    return sm * IMG_E + (S * oy * W + S * ox) * LDI;
+  };
+  const int ngroups = (b1 - b0 + SB - 1) / SB;
+  if (ngroups > 0) CWG_LOAD(b0)
+  for (int gi = 0; gi < ngroups; ++gi) {
+    CWG_STORE()
+    __syncthreads();
+    if (gi + 1 < ngroups) CWG_LOAD(b0 + (gi + 1) * SB)
+#pragma unroll 2
+    for (int ks = 0; ks < KST; ++ks) {
+      const int kb = ks * 16 + khalf;
+      const short4x a_lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(s_dy + (kb + q) * LDD + acol));
+      const short4x a_hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(s_dy + (kb + 4 + q) * LDD + acol));
+      const cw_short8 av = {a_lo[0], a_lo[1], a_lo[2], a_lo[3], a_hi[0], a_hi[1], a_hi[2], a_hi[3]};
+      const bf16x8 af = __builtin_bit_cast(bf16x8, av);
+      const int pa = pos_off(kb + q), pb = pos_off(kb + 4 + q);
+      const bool padded = kb + 4 + q >= GP;
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) {
+        if (nb + 4 * t < NT) {   // wave-uniform
+          const int oa = pa == SB * IMG_E ? pa : pa + noff[t];
+          const int ob = padded ? SB * IMG_E : pb + noff[t];
+          const short4x lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(s_img + oa));
+          const short4x hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(s_img + ob));
+          const cw_short8 bv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, __builtin_bit_cast(bf16x8, bv), acc[t], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+  }
+#undef CWG_LDI
+#undef CWG_LDD
+#undef CWG_LOAD
+#undef CWG_STI
+#undef CWG_STD
+#undef CWG_STORE
+  // plane g: [64][NCOL] fp32, each element written exactly once (zero for an empty sample range)
+  float* dst = planes + (size_t)g * 64 * NCOL;
+  const int col = lane & 31, rh = 4 * (lane >> 5);
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    const int nt = nb + 4 * t;
+    if (nt < NT)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int row = mt * 32 + (i & 3) + 8 * (i >> 2) + rh;
+        dst[(size_t)row * NCOL + nt * 32 + col] = acc[t][i];
+      }
+  }
+}
+
 }  // namespace aca
 
 // obs uint8 [B][4][84][84], dy1 bf16 [B][400][32] -> planes fp32 [P][32][256] (plane g: samples
@@ -317,6 +477,20 @@ extern "C" hipError_t aca_conv1_wgrad(const uint8_t* obs, const uint16_t* dy1, f
   if (B <= 0) return hipSuccess;
   if (P < 1 || P > 1024) return hipErrorInvalidValue;
   aca::conv1_wgrad_kernel<<<4 * P, aca::CW_T, 0, stream>>>(obs, dy1, planes, B, P, scale);
+  return hipGetLastError();
+}
+
+// Batched-position form (conv_wgrad_gemm_kernel): grid P, plane g of [64][N] per workgroup. layer 2 / 3 as below.
+extern "C" hipError_t aca_conv_wgrad_gemm(int layer, const uint16_t* img, const uint16_t* dy, float* planes, int B,
+                                          int P, hipStream_t stream) {
+  if (B <= 0) return hipSuccess;
+  if (P < 1 || P > 1024) return hipErrorInvalidValue;
+  if (layer == 2)
+    aca::conv_wgrad_gemm_kernel<20, 20, 32, 4, 2, 9, 9, 2><<<P, 512, 0, stream>>>(img, dy, planes, B, P);
+  else if (layer == 3)
+    aca::conv_wgrad_gemm_kernel<9, 9, 64, 3, 1, 7, 7, 2><<<P, 512, 0, stream>>>(img, dy, planes, B, P);
+  else
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

@@ -168,7 +168,7 @@ def test_dp_bf16_buckets_track_fp32(cuda, tmp_path, overlap):
 
 
 # ---------------------------------------------------------------------------------------------- RCCL, in-graph
-def _rccl_worker(port, out_dir, name, kw, modes):
+def _rccl_worker(_idx, port, out_dir, name, kw, modes):
     """One process, an RCCL ("nccl") group of world 1 on cuda:0: the same DP update captured with the collectives
     INSIDE one hipGraph (``dp_capture="auto"``) and as the host-cut segment chain (``"segments"``)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ACAMD_GEMM_TUNE="0")
@@ -185,7 +185,8 @@ def _rccl_worker(port, out_dir, name, kw, modes):
             tr = ActorCriticTrainer(_cfg(kw_envs(name), "strict", name, dp_capture=mode, **kw), dp=dp)
             tr.capture(warmup=1)
             kind = tr.graph[0]
-            n_graphs = tr.graph[1].n_graphs if kind == "segments" else 1
+            n_graphs = (tr.graph[1].n_graphs if kind == "segments" else
+                        len(tr.graph) - 1 if kind in ("strict", "lag1") else 1)
             issued = dp.issued
             snaps = []
             for _ in range(UPDATES):

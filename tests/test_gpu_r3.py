@@ -1,0 +1,109 @@
+"""Round-3 HIP kernels vs fp32 PyTorch references of the same op.
+
+* ``conv_wgrad_gemm`` (conv_wgrad.hip conv_wgrad_gemm_kernel): the batched-position MFMA 32x32x16 weight gradient
+  of conv2 / conv3 -- every plane == the fp32 autograd weight gradient of its sample range, planes bit-identical
+  across runs, empty sample ranges written as zeros;
+* ``grad_finalize_opt`` (optim.hip grad_finalize_opt_kernel): the finaliser + RMSprop / Adam update in one launch
+  == the finaliser launch followed by the optimiser launch, and the gradient slab is left zero.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _wgrad_ref(layer, img, dy):
+    H, C, KS, S, OH = (20, 32, 4, 2, 9) if layer == 2 else (9, 64, 3, 1, 7)
+    ref = torch.nn.grad.conv2d_weight(img.float().permute(0, 3, 1, 2), (64, C, KS, KS),
+                                      dy.float().permute(0, 3, 1, 2), stride=S)
+    return ref.permute(0, 2, 3, 1).reshape(64, KS * KS * C)
+
+
+@pytest.mark.parametrize("layer,B,P", [(2, 5, 3), (2, 7, 8), (2, 300, 64), (3, 9, 4), (3, 301, 64), (3, 4096, 256)])
+def test_conv_wgrad_gemm_planes_match_autograd(cuda, layer, B, P):
+    from actor_critic_algs_on_tensorflow_amd import _native
+    ops = _native.require()
+    H, C, KS, OH = (20, 32, 4, 9) if layer == 2 else (9, 64, 3, 7)
+    n = KS * KS * C
+    g = torch.Generator(device="cpu").manual_seed(B * 7 + layer)
+    img = torch.rand(B, H, H, C, generator=g).to(torch.bfloat16).to(cuda)
+    dy = (torch.randn(B, OH, OH, 64, generator=g) * 0.1).to(torch.bfloat16).to(cuda)
+    planes = torch.full((P * 64 * n,), float("nan"), device=cuda)
+    ops.conv_wgrad_gemm(layer, img.view(B * H * H, C), dy.view(B * OH * OH, 64), planes, P)
+    torch.cuda.synchronize()
+    pl = planes.view(P, 64, n)
+    assert torch.isfinite(pl).all()
+    # every plane is the gradient of its own sample range [g B / P, (g + 1) B / P)
+    for gi in sorted({0, P // 2, P - 1}):
+        b0, b1 = gi * B // P, (gi + 1) * B // P
+        if b1 == b0:
+            assert (pl[gi] == 0).all()
+            continue
+        r = _wgrad_ref(layer, img[b0:b1], dy[b0:b1])
+        torch.testing.assert_close(pl[gi], r, rtol=1e-4, atol=1e-4)
+    tot = pl.sum(0)
+    ref = _wgrad_ref(layer, img, dy)
+    assert ((tot - ref).norm() / ref.norm()).item() < 1e-4
+    again = torch.zeros_like(planes)
+    ops.conv_wgrad_gemm(layer, img.view(B * H * H, C), dy.view(B * OH * OH, 64), again, P)
+    assert torch.equal(again, planes)
+
+
+@pytest.mark.parametrize("adam", [False, True])
+def test_grad_finalize_opt_equals_two_launches(cuda, adam):
+    """One launch of finaliser + optimiser (grid barrier between the phases) == grad_finalize then the optimiser
+    step reading the finalised slab: same parameters / moments / bf16 shadow (bitwise), and the slab is zero."""
+    from actor_critic_algs_on_tensorflow_amd import _native
+    from actor_critic_algs_on_tensorflow_amd.ops.optim import (FlatParams, FusedAdam, FusedRMSprop,
+                                                               finalize_jobs)
+    ops = _native.require()
+    g = torch.Generator(device="cpu").manual_seed(3 + adam)
+    shapes = [(4099,), (64, 513), (33,), (257, 129)]
+    runs = []
+    for fused in (False, True):
+        torch.manual_seed(0)
+        params = [torch.nn.Parameter(torch.randn(s, generator=torch.Generator().manual_seed(i)))
+                  for i, s in enumerate(shapes)]
+        flat = FlatParams({"shared": params}, cuda)
+        shadow = torch.zeros(flat.numel, dtype=torch.bfloat16, device=cuda)
+        cls = FusedAdam if adam else FusedRMSprop
+        opt = cls(flat, "shared", 1e-3, max_grad_norm=0.5, bf16_shadow=shadow)
+        opt.zero_grad_after = True
+        # plane sources for params 1 and 3 (7 planes each); params 0 and 2 are final in the slab (read-only jobs)
+        gen = torch.Generator(device="cpu").manual_seed(11)
+        planes = {}
+        for i in (1, 3):
+            planes[i] = torch.randn(7 * params[i].numel(), generator=gen).to(cuda)
+        for step in range(3):
+            for i in (0, 2):
+                off = flat.offsets[i]
+                flat.grad[off:off + params[i].numel()] = torch.randn(params[i].numel(), generator=gen).to(cuda)
+            segs = []
+            for i, p in enumerate(params):
+                off = flat.offsets[i]
+                dst = flat.grad[off:off + p.numel()].data_ptr()
+                if i in planes:
+                    segs.append((dst, planes[i].data_ptr(), p.numel(), p.numel(), 7))
+                else:
+                    segs.append((dst, 0, p.numel(), 0, 0))
+            words, maxn = finalize_jobs(segs, cuda, return_max=True)
+            parts = torch.zeros(256, device=cuda)
+            if fused:
+                assert opt.step_finalize(words, maxn, parts)
+            else:
+                ops.grad_finalize(words, parts)
+                opt.ext_parts = parts
+                opt.step()
+            torch.cuda.synchronize()
+        st = {"p": flat.data.clone(), "v": opt.v.clone(), "shadow": shadow.clone(), "grad": flat.grad.clone()}
+        if adam:
+            st.update(m=opt.m.clone(), t=opt.t.clone())
+        if fused:
+            assert int(opt._fin_state[2]) == 0, "grid barrier timed out"
+        runs.append(st)
+    a, b = runs
+    for k in a:
+        if k == "grad":
+            continue
+        assert torch.equal(a[k], b[k]), k
+    assert (b["grad"] == 0).all() and (a["grad"] == 0).all()

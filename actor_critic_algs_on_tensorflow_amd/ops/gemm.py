@@ -266,6 +266,15 @@ def gemm(A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha=1.0, bias=No
     reading operand A (k-contiguous) / B (n-contiguous) straight from the activation image ``A`` / ``B``.
     """
     ops = _native.require()
+    if _mfma32_ok(M, N, K, out_mode, colsum, ga, gb, tile, splits, _GROUP_DEPTH):
+        s32 = 1
+        if out_mode == 3:   # partial planes: split K while the grid is short of the CUs
+            tiles = -(-M // 128) * -(-N // 128)
+            while s32 * 2 <= max_planes and tiles * s32 < 256 and K % (64 * s32 * 2) == 0 and K // (s32 * 2) >= 512:
+                s32 *= 2
+        if ops.gemm_mfma32(A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, float(alpha), bias, bool(relu), mask,
+                           ldm, s32):
+            return s32
     if tile is None or splits is None or bk is None:
         key = (M, N, K, bool(a_k), bool(b_k), out_mode, lda % 8 == 0, ldb % 8 == 0, tuple(ga or ()), tuple(gb or ()),
                max_planes if out_mode == 3 else 0)
@@ -297,6 +306,17 @@ def gemm(A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha=1.0, bias=No
         raise ValueError("out_mode 3: more split-K planes than C holds (%d)" % max_planes)
     return _run(ops, A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha, bias, relu, mask, ldm, colsum,
                 colsum_mod, tile, bk, splits, workspace, ga, ga_scale, gb, gb_scale, stamps)
+
+
+# large plain products (PPO minibatch fc layer) run on the 32x32x16-MFMA kernel (gemm_mfma32.hip) from this many
+# MACs up; ACAMD_GEMM32=0 keeps every product on the general kernel
+GEMM32 = os.environ.get("ACAMD_GEMM32", "1") != "0"
+GEMM32_MIN_MACS = int(os.environ.get("ACAMD_GEMM32_MIN_MACS", str(1 << 30)))
+
+
+def _mfma32_ok(M, N, K, out_mode, colsum, ga, gb, tile, splits, grouped):
+    return (GEMM32 and not grouped and tile is None and splits is None and not ga and not gb and colsum is None
+            and out_mode in (0, 1, 3) and M * N * K >= GEMM32_MIN_MACS and K % 64 == 0)
 
 
 def _view(t, rows, cols, ld, k_contig_rows):

@@ -73,6 +73,7 @@ hipError_t aca_ev_multi(const float*, const float*, float*, int, double*, unsign
 hipError_t aca_conv1_wgrad(const uint8_t*, const uint16_t*, float*, int, int, float, hipStream_t);
 hipError_t aca_conv_wgrad_nhwc(int, const uint16_t*, const uint16_t*, float*, int, int, hipStream_t);
 hipError_t aca_conv_wgrad_gemm(int, const uint16_t*, const uint16_t*, float*, int, int, hipStream_t);
+hipError_t aca_gemm_mfma32(const AcaGemmDesc*, hipStream_t);
 hipError_t aca_sumsq(const float*, size_t, float*, hipStream_t);
 int aca_sumsq_parts();
 hipError_t aca_adam_step(float*, float*, float*, float*, size_t, const float*, float*, const float*, float*, uint16_t*,
@@ -979,6 +980,44 @@ struct GemmGroupState {
 };
 static thread_local GemmGroupState g_gemm_group;
 
+// Large-shape GEMM on the 32x32x16 MFMA (gemm_mfma32.hip): plain bf16 operands, epilogue bias / relu / mask, store
+// fp32 | bf16 (splits 1) or fp32 split-K partial planes (out_mode 3). Returns false when the kernel does not take
+// this shape / layout (nothing launched: the caller uses the general GEMM).
+bool gemm_mfma32(Tensor A, int64_t lda, bool a_k, Tensor B, int64_t ldb, bool b_k, Tensor C, int64_t ldc,
+                 int64_t out_mode, int64_t M, int64_t N, int64_t K, double alpha, c10::optional<Tensor> bias, bool relu,
+                 c10::optional<Tensor> mask, int64_t ldm, int64_t splits) {
+  TORCH_CHECK(out_mode == 0 || out_mode == 1 || out_mode == 3, "gemm_mfma32: out_mode 0 / 1 / 3");
+  TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "gemm_mfma32: bf16 operands");
+  TORCH_CHECK(C.scalar_type() == (out_mode == 1 ? at::kBFloat16 : at::kFloat), "gemm_mfma32: C dtype mismatch");
+  TORCH_CHECK(splits >= 1 && (splits == 1 || out_mode == 3), "gemm_mfma32: split-K only as partial planes");
+  check_extent(A, a_k ? M : K, a_k ? K : M, lda, "A");
+  check_extent(B, b_k ? N : K, b_k ? K : N, ldb, "B");
+  check_extent(C, out_mode == 3 ? splits * M : M, N, ldc, "C");
+  if (bias.has_value() && bias->defined())
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() >= N, "gemm_mfma32: bias must be fp32 [N]");
+  if (mask.has_value() && mask->defined()) {
+    TORCH_CHECK(mask->scalar_type() == at::kBFloat16, "gemm_mfma32: mask must be bf16");
+    check_extent(*mask, M, N, ldm, "mask");
+  }
+  AcaGemmDesc d{};
+  d.A = A.data_ptr(); d.B = B.data_ptr(); d.C = C.data_ptr();
+  d.bias = optr<float>(bias);
+  d.mask = (mask.has_value() && mask->defined()) ? mask->data_ptr() : nullptr;
+  d.lda = lda; d.ldb = ldb; d.ldc = ldc; d.ldm = ldm;
+  d.M = (int)M; d.N = (int)N; d.K = (int)K;
+  d.a_k = a_k; d.b_k = b_k;
+  d.out_mode = (int)out_mode; d.relu = relu ? 1 : 0;
+  d.alpha = (float)alpha;
+  d.splits = (int)splits;
+  const hipError_t e = aca_gemm_mfma32(&d, cur_stream(C));
+  if (e == hipErrorInvalidValue) {
+    (void)hipGetLastError();
+    return false;
+  }
+  check(e, "gemm_mfma32");
+  return true;
+}
+
 void gemm(Tensor A, int64_t lda, bool a_k, Tensor B, int64_t ldb, bool b_k, Tensor C, int64_t ldc, int64_t out_mode,
           int64_t M, int64_t N, int64_t K, double alpha, c10::optional<Tensor> bias, bool relu,
           c10::optional<Tensor> mask, int64_t ldm, c10::optional<Tensor> colsum, int64_t colsum_mod, int64_t tile,
@@ -1454,6 +1493,8 @@ TORCH_LIBRARY(acamd, m) {
   m.def("conv1_wgrad(Tensor obs, Tensor dy1, Tensor planes, int P, float scale) -> ()");
   m.def("conv_wgrad_nhwc(int layer, Tensor img, Tensor dy, Tensor planes, int P) -> ()");
   m.def("conv_wgrad_gemm(int layer, Tensor img, Tensor dy, Tensor planes, int P) -> ()");
+  m.def("gemm_mfma32(Tensor A, int lda, bool a_k, Tensor B, int ldb, bool b_k, Tensor C, int ldc, int out_mode, "
+        "int M, int N, int K, float alpha, Tensor? bias, bool relu, Tensor? mask, int ldm, int splits) -> bool");
   m.def("mb_gather(Tensor obs, Tensor act, Tensor logp, Tensor adv, Tensor ret, Tensor v, Tensor o_obs, "
         "Tensor o_act, Tensor o_logp, Tensor o_adv, Tensor o_ret, Tensor o_v, int seed, Tensor uc, int ep, "
         "int off, Tensor? mom=None, float eps=1e-8, Tensor? bump_ticket=None) -> ()");
@@ -1541,6 +1582,7 @@ TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
   m.impl("conv1_wgrad", &conv1_wgrad);
   m.impl("conv_wgrad_nhwc", &conv_wgrad_nhwc);
   m.impl("conv_wgrad_gemm", &conv_wgrad_gemm);
+  m.impl("gemm_mfma32", &gemm_mfma32);
   m.impl("moments", &moments);
   m.impl("sumsq", &sumsq);
   m.impl("adam_step", &adam_step);

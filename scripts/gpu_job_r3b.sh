@@ -15,8 +15,10 @@ ACA_FUSED_FINOPT=0 timeout -k 10 120 python -u bench.py --steps 400 --warmup 20 
 cat $O/bench_nofuse.json
 timeout -k 10 300 python -u scripts/bench_configs.py --configs breakout_ppo > $O/br.jsonl 2> $O/br.err || { tail -5 $O/br.err; exit 1; }
 tail -n 2 $O/br.jsonl
-ACA_WGRAD_GEMM=0 timeout -k 10 300 python -u scripts/bench_configs.py --configs breakout_ppo > $O/br_old.jsonl 2> $O/br_old.err || exit 1
+ACA_WGRAD_GEMM=0 ACAMD_GEMM32=0 timeout -k 10 300 python -u scripts/bench_configs.py --configs breakout_ppo > $O/br_old.jsonl 2> $O/br_old.err || exit 1
 tail -n 2 $O/br_old.jsonl
+ACAMD_GEMM32=0 timeout -k 10 300 python -u scripts/bench_configs.py --configs breakout_ppo > $O/br_wg.jsonl 2> $O/br_wg.err || exit 1
+tail -n 2 $O/br_wg.jsonl
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; grep -E "passed|failed" $O/tests.log | tail -2; grep -E "FAILED" $O/tests.log | head -20
 [ $rc -eq 0 ] || exit $rc

@@ -107,3 +107,38 @@ def test_grad_finalize_opt_equals_two_launches(cuda, adam):
             continue
         assert torch.equal(a[k], b[k]), k
     assert (b["grad"] == 0).all() and (a["grad"] == 0).all()
+
+
+@pytest.mark.parametrize("a_k,b_k", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("M,N,K,out_mode,epi", [
+    (4096, 512, 3136, 1, "bias_relu"),     # PPO fc forward
+    (4096, 3136, 512, 1, "mask"),          # dy3 = dh Wfc^T * (y3 > 0)
+    (3136, 512, 4096, 0, None),            # dWfc (fp32 store)
+    (1000, 136, 1024, 3, None),            # partial tiles, split-K planes
+])
+def test_gemm_mfma32_matches_fp32_reference(cuda, a_k, b_k, M, N, K, out_mode, epi):
+    """The 32x32x16-MFMA GEMM (gemm_mfma32.hip) == the fp32 oracle of the same product (bf16 operands in every
+    storage orientation, bias / relu / mask epilogues, fp32 / bf16 stores, split-K partial planes)."""
+    from actor_critic_algs_on_tensorflow_amd import _native
+    from actor_critic_algs_on_tensorflow_amd.ops.gemm import gemm_ref
+    ops = _native.require()
+    g = torch.Generator(device="cpu").manual_seed(M + N + K + 2 * a_k + b_k)
+    lda = K if a_k else M
+    ldb = K if b_k else N
+    A = (torch.randn((M if a_k else K) * lda, generator=g) * 0.5).to(torch.bfloat16).to(cuda)
+    B = (torch.randn((N if b_k else K) * ldb, generator=g) * 0.5).to(torch.bfloat16).to(cuda)
+    bias = torch.randn(N, generator=g).to(cuda) if epi == "bias_relu" else None
+    mask = torch.randn(M * N, generator=g).to(torch.bfloat16).to(cuda) if epi == "mask" else None
+    splits = 4 if out_mode == 3 else 1
+    dt = torch.bfloat16 if out_mode == 1 else torch.float32
+    C = torch.full((splits * M * N,), float("nan"), dtype=dt, device=cuda)
+    ok = ops.gemm_mfma32(A, lda, a_k, B, ldb, b_k, C, N, out_mode, M, N, K, 1.0, bias, epi == "bias_relu", mask,
+                         N if mask is not None else 0, splits)
+    assert ok
+    torch.cuda.synchronize()
+    ref = gemm_ref(A, lda, a_k, B, ldb, b_k, M, N, K, 1.0, bias, epi == "bias_relu", mask, N if mask is not None else 0)
+    got = C.view(splits, M, N).float().sum(0) if out_mode == 3 else C.view(M, N).float()
+    tol = 2e-2 if out_mode == 1 else 1e-3
+    err = ((got - ref).norm() / ref.norm()).item()
+    assert err < tol, err
+    assert torch.isfinite(got).all()

@@ -43,6 +43,11 @@ from . import losses as L
 from .storage import RolloutStorage
 
 KEY_ENV_BITS = 20
+# Graph capture is thread-local: RCCL's watchdog thread polls the events of earlier (uncaptured) collectives while
+# the trainer captures an update whose collectives are recorded in the graph; in the default global mode that poll
+# is a forbidden call during capture and kills the process group (seen on MI355X: hipErrorStreamCaptureUnsupported
+# from ProcessGroupNCCL's watchdog).
+CAPTURE_MODE = "thread_local"
 FAULT_EXIT_CODE = 43   # exit status of a rank killed by ``fault_inject`` (SURVEY §5.3 test hook)
 
 
@@ -75,7 +80,7 @@ class SegmentRecorder:
 
     def start(self):
         self._g = torch.cuda.CUDAGraph()
-        self._ctx = torch.cuda.graph(self._g, pool=self.pool)
+        self._ctx = torch.cuda.graph(self._g, pool=self.pool, capture_error_mode=CAPTURE_MODE)
         self._ctx.__enter__()
 
     def cut(self, fn):
@@ -161,8 +166,10 @@ class ActorCriticTrainer:
             self.engine.want_parts = True
             for o in self.opts.values():
                 o.ext_parts = self.engine.fin_parts
-            # ... and the finaliser itself runs inside the optimiser's launch (grad_finalize_opt)
-            self.engine.defer_finalize = os.environ.get("ACA_FUSED_FINOPT", "1") != "0"
+            # opt-in: the finaliser inside the optimiser's launch (grad_finalize_opt). Measured on the headline
+            # update it is SLOWER (0.227 vs 0.199 ms per update, profiles/r3_bench_finopt_ab.txt): the in-launch grid
+            # barrier of 256 workgroups costs more than the kernel boundary and the slab pass it removes
+            self.engine.defer_finalize = os.environ.get("ACA_FUSED_FINOPT", "0") == "1"
         T, N = cfg.n_steps, self.env.num_envs
         act_shape = () if self.env.is_discrete else tuple(self.env.action_space.shape)
         act_dtype = torch.int32 if self.env.is_discrete else torch.float32
@@ -222,7 +229,9 @@ class ActorCriticTrainer:
     def _want_native_mlp(self):
         """The fused MLP engine (``ops/mlp.py``) runs the reference's MLP actor/critic on GPU."""
         from ..models.policy import MLPActorCritic
-        if self.cfg.engine == "torch" or self.cfg.bootstrap_on_timeout or self.device.type != "cuda" or \
+        # time-limit bootstrapping needs the env kernel's terminal observation (classic / MuJoCo-shaped banks)
+        boot_ok = not self.cfg.bootstrap_on_timeout or getattr(self.env, "native_final_obs", False)
+        if self.cfg.engine == "torch" or not boot_ok or self.device.type != "cuda" or \
                 not isinstance(self.model, MLPActorCritic):
             return False
         if self.model.actor.ac_dim > 16 or self.env.obs_dtype != torch.float32 or len(self.env.obs_shape) != 1:
@@ -267,15 +276,26 @@ class ActorCriticTrainer:
         ``rollout_linear``). Otherwise one launch per step for the policy (both towers + sampling) and one for the
         env bank."""
         st, env, eng = self.storage, self.env, self.mlp
-        if self.cfg.fused_rollout and eng.supports_fused_rollout(env):
+        boot = self.cfg.bootstrap_on_timeout
+        if self.cfg.fused_rollout and eng.supports_fused_rollout(env) and not boot:
             eng.rollout_linear(env, st, KEY_ENV_BITS, self.policy_seed)
             return
+        if boot and getattr(self, "_final_obs", None) is None:
+            self._final_obs = torch.zeros((st.T,) + tuple(st.obs.shape[1:]), dtype=st.obs.dtype, device=self.device)
+            self._final_v = torch.zeros(st.T * st.N, dtype=torch.float32, device=self.device)
         for t in range(st.T):
             eng.policy_step(st.obs[t], st.actions[t], st.logp[t], st.entropy[t], st.values[t], env.tg, env.env_ids,
                             KEY_ENV_BITS, self.policy_seed)
             env.step(st.actions[t], prev_obs=st.obs[t], obs_out=st.obs[t + 1], reward_out=st.rewards[t],
-                     done_out=st.dones[t], trunc_out=st.truncated[t])
+                     done_out=st.dones[t], trunc_out=st.truncated[t],
+                     final_out=self._final_obs[t] if boot else None)
         eng.value(st.obs[st.T], st.values[st.T])
+        if boot:
+            # a time-limit cut stays an episode boundary (done = 1); the truncated step's reward gets
+            # gamma * V(terminal observation): ONE critic launch over the T x N terminal stacks the env kernel wrote
+            eng.value(self._final_obs.view(st.T * st.N, -1), self._final_v)
+            st.rewards.addcmul_(self._final_v.view(st.T, st.N), st.truncated.to(torch.float32),
+                                value=self.cfg.gamma)
 
     def _reuse_acts(self):
         """A2C takes one gradient step at the parameters that acted, so the rollout's forward activations ARE the
@@ -848,10 +868,10 @@ class ActorCriticTrainer:
                         for opt in self.opts.values():
                             opt.bind_grad(self._comm_grad)
                     g1 = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g1):
+                    with torch.cuda.graph(g1, capture_error_mode=CAPTURE_MODE):
                         self.update_body()
                     g2 = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g2):
+                    with torch.cuda.graph(g2, capture_error_mode=CAPTURE_MODE):
                         self.dp.unpack(self._comm_grad)     # bf16 buckets: the all-reduced sum back into C
                         self._post_body()
                         self._grad_move()
@@ -860,7 +880,7 @@ class ActorCriticTrainer:
                 else:
                     self._bw_stage = "tail"
                     g1 = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g1):
+                    with torch.cuda.graph(g1, capture_error_mode=CAPTURE_MODE):
                         self.collect()
                         ret, adv = self.compute_returns()
                         self.learn(ret, adv)
@@ -868,11 +888,11 @@ class ActorCriticTrainer:
                     self._bw_stage = "all"
                     b, hb = self._bw_pending
                     g2 = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g2):
+                    with torch.cuda.graph(g2, capture_error_mode=CAPTURE_MODE):
                         self.engine.backward(b, head_bias_done=hb, stage="trunk")
                         self.dp.pack(self.flat.grad, 0, self.engine.tail_bucket()[0])
                     g3 = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g3):
+                    with torch.cuda.graph(g3, capture_error_mode=CAPTURE_MODE):
                         self.dp.unpack(self.flat.grad)
                         self._post_body()
                         self.storage.roll_over()
@@ -884,7 +904,7 @@ class ActorCriticTrainer:
             # RCCL: every collective of the update (gradient buckets per optimiser step, the advantage moments, the
             # KL scalar) is recorded in the graph -- one replay per update, zero host-issued collectives
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
                 self.update_body()
             graph = ("single", g)
         elif self.dp is not None or self._grad_sink is not None:
@@ -902,7 +922,7 @@ class ActorCriticTrainer:
             graph = ("segments", rec)
         else:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
                 self.update_body()
             graph = ("single", g)
         return graph
@@ -950,6 +970,8 @@ class ActorCriticTrainer:
                 self._replay()
         else:
             self.update_body()
+        if self.cfg.lr_schedule == "linear":
+            self._decay_lr(self.iteration + 1)
         if self.reg_sched is not None:
             # after update i, as the reference (Basic_AC/run_AC.py:268-275): a new coefficient acts from i + 1 on
             e, k = self.reg_sched.entropy_coef(self.iteration), self.reg_sched.kl_coef(self.iteration)
@@ -959,6 +981,15 @@ class ActorCriticTrainer:
                 self.kl_coef.fill_(k)
         self.iteration += 1
         self.env_steps += self.cfg.n_steps * self.env.num_envs * self.world
+
+    def _decay_lr(self, it):
+        """Linear lr decay (``lr_schedule="linear"``): update ``it`` runs with lr0 * (1 - it / total_updates). One
+        device scalar write per optimiser between replays (the captured update reads lr from device memory)."""
+        frac = max(0.0, 1.0 - it / max(1, self.cfg.total_updates))
+        for g, opt in self.opts.items():
+            if g == "critic" or self.lr_ctrl is None or opt is not self.actor_opt:
+                base = self.cfg.critic_lr if g == "critic" else self.cfg.lr
+                opt.lr.fill_(base * frac)
 
     def flush_pending(self):
         """lag-1 DP: apply the last all-reduced gradient (end of training / before a checkpoint)."""

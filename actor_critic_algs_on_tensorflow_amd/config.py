@@ -46,6 +46,8 @@ class TrainConfig:
     min_lr: float = 1e-6
     max_lr: float = 1.0
     anneal_regularizers: bool = False  # log10 schedules of ent/kl coefs (Basic_AC/run_AC.py:181-182)
+    lr_schedule: str = "constant"     # constant | linear (every optimiser's lr decays linearly to 0 at total_updates;
+                                      # not combined with the KL-adaptive lr, which owns the actor lr)
     # -- PPO ---------------------------------------------------------------------------------------------------
     ppo_epochs: int = 4
     ppo_minibatches: int = 4
@@ -107,6 +109,15 @@ PRESETS = {
                 kl_coef=1.0, lr=0.005, critic_lr=0.001, clip_value=0.1, max_grad_norm=None, kl_adaptive_lr=True,
                 max_lr=0.1, anneal_regularizers=True, model_variant="a3c", optimizer="adam", device="cpu",
                 cuda_graph=False),
+    # The reference's flagship task (Pendulum-v0, README.md:18,33-37) solved by PPO-clip on the reference networks:
+    # the A3C actor / critic (model_variant a3c), gamma 0.98 as the reference, one 200-step episode per
+    # env per rollout (16 envs: 3200 steps, the scale of the reference's 1200-step batches), GAE(0.95), 10 epochs x
+    # 8 minibatches, Adam 3e-4 with a 0.5 global-norm clip. Reaches a mean return above -200 within ~150k env steps
+    # (profiles/r3_pendulum_learning.txt); the reference's own single-step KL-adaptive update is preset "a3c".
+    "pendulum_ppo": dict(algo="ppo", env="Pendulum-v0", model="mlp", model_variant="a3c", num_envs=16, n_steps=200,
+                         gamma=0.98, returns="gae", gae_lambda=0.95, norm_adv=True, ppo_epochs=10, ppo_minibatches=8,
+                         ppo_clip=0.2, optimizer="adam", lr=3e-4, critic_lr=1e-3, ent_coef=0.0, kl_coef=0.0,
+                         max_grad_norm=0.5, device="cuda", dtype="fp32"),
     # BASELINE config 1
     "cartpole_cpu": dict(algo="a2c", env="CartPole-v1", num_envs=1, n_steps=5, gamma=0.99, model="mlp",
                          lr=1e-3, critic_lr=5e-3, norm_adv=True, device="cpu", cuda_graph=False,

@@ -156,13 +156,18 @@ class VecEnv:
             new = torch.cat([prev[:, d:], frame.to(out.dtype)], dim=1)
         out.copy_(new)
 
-    def step(self, actions, prev_obs=None, obs_out=None, reward_out=None, done_out=None, trunc_out=None):
+    native_final_obs = False   # env kernel writes the terminal observation (subclasses with that support)
+
+    def step(self, actions, prev_obs=None, obs_out=None, reward_out=None, done_out=None, trunc_out=None,
+             final_out=None):
         """One env step for the whole bank.
 
         ``prev_obs`` / ``obs_out`` let a rollout read the stack from slot ``t`` and write slot ``t+1`` of its
         buffer directly, and ``reward_out`` / ``done_out`` / ``trunc_out`` receive the transition's reward, done and
         truncation flags (static addresses => hipGraph-capturable; on GPU the env kernel writes them in place, no
-        copies). Defaults: the bank's own buffers.
+        copies). Defaults: the bank's own buffers. With ``keep_final_obs`` the stack holding the transition's new
+        frame before any auto-reset (the terminal observation of finished episodes) goes to ``final_out`` (default
+        ``self.final_obs``).
         """
         prev = self.obs if prev_obs is None else prev_obs
         out = self.obs if obs_out is None else obs_out
@@ -171,10 +176,19 @@ class VecEnv:
         trunc = self.truncated if trunc_out is None else trunc_out
         if prev.data_ptr() == out.data_ptr():
             prev = prev.clone()   # the kernels read the old stack while writing the new one
-        if _native.use_native(self.state) and not self.keep_final_obs:   # the kernels keep no terminal obs
+        native = _native.use_native(self.state) and (not self.keep_final_obs or self.native_final_obs)
+        if native and self.keep_final_obs:
+            if final_out is None:
+                if self.final_obs is None:
+                    self.final_obs = torch.empty_like(out)
+                final_out = self.final_obs
+            self._native_step(actions, prev, out, rew, done, trunc, final_out)
+        elif native:
             self._native_step(actions, prev, out, rew, done, trunc)
         else:
             self._torch_step(actions, prev, out)
+            if self.keep_final_obs and final_out is not None:
+                final_out.copy_(self.final_obs)
             for src, dst in ((self.reward, rew), (self.done, done), (self.truncated, trunc)):
                 if dst.data_ptr() != src.data_ptr():
                     dst.copy_(src)

@@ -62,10 +62,13 @@ class CartPoleVecEnv(VecEnv):
     def _frame(self):
         return self.state.clone()
 
-    def _native_step(self, actions, prev, out, rew, done, trunc):
+    native_final_obs = True   # the kernel can write the terminal observation (time-limit bootstrap)
+
+    def _native_step(self, actions, prev, out, rew, done, trunc, final_out=None):
         _native.require().env_step_cartpole(
             self.state, self.t, self.tg, self.ep_ret, self.ep_stats, self.env_ids, actions.to(torch.int32),
-            prev, out, rew, done, trunc, self.seed, self.max_episode_steps, self.frame_stack)
+            prev, out, rew, done, trunc, self.seed, self.max_episode_steps, self.frame_stack,
+            final_out)
 
 
 class CartPoleV0VecEnv(CartPoleVecEnv):
@@ -112,8 +115,11 @@ class PendulumVecEnv(VecEnv):
         th, thdot = self.state.unbind(1)
         return torch.stack([torch.cos(th), torch.sin(th), thdot], 1)
 
-    def _native_step(self, actions, prev, out, rew, done, trunc):
+    native_final_obs = True   # the kernel can write the terminal observation (time-limit bootstrap)
+
+    def _native_step(self, actions, prev, out, rew, done, trunc, final_out=None):
         _native.require().env_step_pendulum(
             self.state, self.t, self.tg, self.ep_ret, self.ep_stats, self.env_ids,
             actions.reshape(self.num_envs, -1).float().contiguous(),
-            prev, out, rew, done, trunc, self.seed, self.max_episode_steps, self.frame_stack)
+            prev, out, rew, done, trunc, self.seed, self.max_episode_steps, self.frame_stack,
+            final_out)

@@ -66,8 +66,11 @@ class MujocoShapeVecEnv(VecEnv):
     def _frame(self):
         return self.state.clone()
 
-    def _native_step(self, actions, prev, out, rew, done, trunc):
+    native_final_obs = True   # the kernel can write the terminal observation (time-limit bootstrap)
+
+    def _native_step(self, actions, prev, out, rew, done, trunc, final_out=None):
         _native.require().env_step_linear(
             self.state, self.t, self.tg, self.ep_ret, self.ep_stats, self.env_ids,
             actions.reshape(self.num_envs, ACT_DIM).float().contiguous(), self.A, self.B,
-            prev, out, rew, done, trunc, self.seed, self.max_episode_steps, self.frame_stack)
+            prev, out, rew, done, trunc, self.seed, self.max_episode_steps, self.frame_stack,
+            final_out)

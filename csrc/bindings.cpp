@@ -27,14 +27,14 @@ hipError_t aca_mlp_fwd(const aca::MlpArgs*, int, size_t, hipStream_t);
 hipError_t aca_mlp_wgrad(const aca::WgradArgs*, hipStream_t);
 hipError_t aca_mlp_rollout(const aca::RolloutArgs*, size_t, hipStream_t);
 hipError_t aca_env_step_cartpole(float*, int32_t*, int64_t*, float*, float*, const int64_t*, const int32_t*,
-                                 const float*, float*, float*, uint8_t*, uint8_t*, uint32_t, int, int, int,
+                                 const float*, float*, float*, uint8_t*, uint8_t*, uint32_t, int, int, int, float*,
                                  hipStream_t);
 hipError_t aca_env_step_pendulum(float*, int32_t*, int64_t*, float*, float*, const int64_t*, const float*, int,
-                                 const float*, float*, float*, uint8_t*, uint8_t*, uint32_t, int, int, int,
+                                 const float*, float*, float*, uint8_t*, uint8_t*, uint32_t, int, int, int, float*,
                                  hipStream_t);
 hipError_t aca_env_step_linear(float*, int32_t*, int64_t*, float*, float*, const int64_t*, const float*,
                                const float*, const float*, const float*, float*, float*, uint8_t*, uint8_t*,
-                               uint32_t, int, int, int, hipStream_t);
+                               uint32_t, int, int, int, float*, hipStream_t);
 hipError_t aca_env_step_pong(float*, int32_t*, int64_t*, float*, float*, const int64_t*, const int32_t*,
                              const uint8_t*, uint8_t*, float*, uint8_t*, uint8_t*, uint32_t, int, int, int,
                              hipStream_t);
@@ -159,9 +159,17 @@ void check_env(const Tensor& state, const Tensor& t, const Tensor& tg, const Ten
   need(trunc, at::kByte, "truncated");
 }
 
+// optional terminal-observation output of the classic env kernels: same [N, k*D] stack shape as `out`
+float* final_out_ptr(const c10::optional<Tensor>& f, const Tensor& out) {
+  if (!(f.has_value() && f->defined())) return nullptr;
+  need(*f, at::kFloat, "final_out");
+  TORCH_CHECK(f->numel() == out.numel(), "final_out: must match the observation stack");
+  return ptr<float>(*f);
+}
+
 void env_step_cartpole(Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, Tensor ids, Tensor actions,
                        Tensor prev, Tensor out, Tensor reward, Tensor done, Tensor trunc, int64_t seed,
-                       int64_t max_steps, int64_t k) {
+                       int64_t max_steps, int64_t k, c10::optional<Tensor> final_out) {
   check_env(state, t, tg, ep_ret, ep_stats, ids, reward, done, trunc);
   need(actions, at::kInt, "actions");
   need(prev, at::kFloat, "prev");
@@ -171,13 +179,14 @@ void env_step_cartpole(Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor 
   check(aca_env_step_cartpole(ptr<float>(state), ptr<int32_t>(t), ptr<int64_t>(tg), ptr<float>(ep_ret),
                               ptr<float>(ep_stats), ptr<int64_t>(ids), ptr<int32_t>(actions), ptr<float>(prev),
                               ptr<float>(out), ptr<float>(reward), ptr<uint8_t>(done), ptr<uint8_t>(trunc),
-                              (uint32_t)seed, (int)max_steps, (int)k, N, cur_stream(state)),
+                              (uint32_t)seed, (int)max_steps, (int)k, N, final_out_ptr(final_out, out),
+                              cur_stream(state)),
         "env_step_cartpole");
 }
 
 void env_step_pendulum(Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, Tensor ids, Tensor actions,
                        Tensor prev, Tensor out, Tensor reward, Tensor done, Tensor trunc, int64_t seed,
-                       int64_t max_steps, int64_t k) {
+                       int64_t max_steps, int64_t k, c10::optional<Tensor> final_out) {
   check_env(state, t, tg, ep_ret, ep_stats, ids, reward, done, trunc);
   need(actions, at::kFloat, "actions");
   need(prev, at::kFloat, "prev");
@@ -188,13 +197,14 @@ void env_step_pendulum(Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor 
   check(aca_env_step_pendulum(ptr<float>(state), ptr<int32_t>(t), ptr<int64_t>(tg), ptr<float>(ep_ret),
                               ptr<float>(ep_stats), ptr<int64_t>(ids), ptr<float>(actions), act_dim, ptr<float>(prev),
                               ptr<float>(out), ptr<float>(reward), ptr<uint8_t>(done), ptr<uint8_t>(trunc),
-                              (uint32_t)seed, (int)max_steps, (int)k, N, cur_stream(state)),
+                              (uint32_t)seed, (int)max_steps, (int)k, N, final_out_ptr(final_out, out),
+                              cur_stream(state)),
         "env_step_pendulum");
 }
 
 void env_step_linear(Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, Tensor ids, Tensor actions,
                      Tensor A, Tensor B, Tensor prev, Tensor out, Tensor reward, Tensor done, Tensor trunc,
-                     int64_t seed, int64_t max_steps, int64_t k) {
+                     int64_t seed, int64_t max_steps, int64_t k, c10::optional<Tensor> final_out) {
   check_env(state, t, tg, ep_ret, ep_stats, ids, reward, done, trunc);
   need(actions, at::kFloat, "actions");
   need(A, at::kFloat, "A");
@@ -209,7 +219,7 @@ void env_step_linear(Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep
                             ptr<float>(ep_stats), ptr<int64_t>(ids), ptr<float>(actions), ptr<float>(A),
                             ptr<float>(B), ptr<float>(prev), ptr<float>(out), ptr<float>(reward),
                             ptr<uint8_t>(done), ptr<uint8_t>(trunc), (uint32_t)seed, (int)max_steps, (int)k, N,
-                            cur_stream(state)),
+                            final_out_ptr(final_out, out), cur_stream(state)),
         "env_step_linear");
 }
 
@@ -1456,13 +1466,13 @@ TORCH_LIBRARY(acamd, m) {
   m.def("ping() -> int", &ping);
   m.def("env_step_cartpole(Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, Tensor env_ids, "
         "Tensor actions, Tensor prev, Tensor out, Tensor reward, Tensor done, Tensor truncated, int seed, "
-        "int max_steps, int k) -> ()");
+        "int max_steps, int k, Tensor? final_out=None) -> ()");
   m.def("env_step_pendulum(Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, Tensor env_ids, "
         "Tensor actions, Tensor prev, Tensor out, Tensor reward, Tensor done, Tensor truncated, int seed, "
-        "int max_steps, int k) -> ()");
+        "int max_steps, int k, Tensor? final_out=None) -> ()");
   m.def("env_step_linear(Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, Tensor env_ids, "
         "Tensor actions, Tensor A, Tensor B, Tensor prev, Tensor out, Tensor reward, Tensor done, Tensor truncated, "
-        "int seed, int max_steps, int k) -> ()");
+        "int seed, int max_steps, int k, Tensor? final_out=None) -> ()");
   m.def("env_step_pong(Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, Tensor env_ids, "
         "Tensor actions, Tensor prev, Tensor out, Tensor reward, Tensor done, Tensor truncated, int seed, "
         "int max_steps, int k) -> ()");

@@ -21,6 +21,8 @@ struct EnvIO {
   float* reward;
   uint8_t* done;
   uint8_t* truncated;
+  float* final_out;   // optional [N, k*D]: the stack with the transition's new frame BEFORE any auto-reset (the
+                      // terminal observation of a finished episode; time-limit bootstrapping values it)
   uint32_t seed;
   int max_steps;
   int k;
@@ -28,10 +30,10 @@ struct EnvIO {
 };
 
 template <int D>
-__device__ __forceinline__ void push_frame(const EnvIO& io, int i, const float* frame, bool reset) {
+__device__ __forceinline__ void push_frame_to(const EnvIO& io, float* dst, int i, const float* frame, bool reset) {
   const int k = io.k;
   const float* p = io.prev + (size_t)i * k * D;
-  float* o = io.out + (size_t)i * k * D;
+  float* o = dst + (size_t)i * k * D;
   if (reset) {
     for (int s = 0; s < k; ++s)
       for (int j = 0; j < D; ++j) o[s * D + j] = frame[j];
@@ -40,6 +42,11 @@ __device__ __forceinline__ void push_frame(const EnvIO& io, int i, const float* 
       for (int j = 0; j < D; ++j) o[s * D + j] = p[(s + 1) * D + j];
     for (int j = 0; j < D; ++j) o[(k - 1) * D + j] = frame[j];
   }
+}
+
+template <int D>
+__device__ __forceinline__ void push_frame(const EnvIO& io, int i, const float* frame, bool reset) {
+  push_frame_to<D>(io, io.out, i, frame, reset);
 }
 
 // ------------------------------------------------------------------------------------------------ CartPole
@@ -75,6 +82,10 @@ __global__ void cartpole_step_kernel(EnvIO io, const int32_t* __restrict__ actio
     io.reward[i] = 1.0f;
     io.done[i] = done;
     io.truncated[i] = trunc;
+    if (io.final_out) {
+      const float fin[4] = {x, x_dot, th, th_dot};
+      push_frame_to<4>(io, io.final_out, i, fin, false);
+    }
     if (done) {
       const uint32_t id = (uint32_t)io.env_ids[i], st = (uint32_t)tg;
       x = uniform01(io.seed, id, st, 100) * 0.1f - 0.05f;
@@ -131,6 +142,10 @@ __global__ void pendulum_step_kernel(EnvIO io, const float* __restrict__ actions
     io.reward[i] = rew;
     io.done[i] = done;
     io.truncated[i] = trunc;
+    if (io.final_out) {
+      const float fin[3] = {cosf(th), sinf(th), thdot};
+      push_frame_to<3>(io, io.final_out, i, fin, false);
+    }
     if (done) {
       const uint32_t id = (uint32_t)io.env_ids[i], st = (uint32_t)tg;
       th = uniform01(io.seed, id, st, 100) * TWO_PI - PI;
@@ -195,6 +210,13 @@ __global__ void __launch_bounds__(256) linear_step_kernel(EnvIO io, const float*
     const float er = io.ep_ret[i] + rew;
     ret = er;
     len = (float)t;
+    if (io.final_out && r < LIN_OBS) {   // terminal observation (before the reset below)
+      const int k = io.k;
+      const float* pv = io.prev + (size_t)i * k * LIN_OBS;
+      float* fo = io.final_out + (size_t)i * k * LIN_OBS;
+      for (int f = 0; f < k - 1; ++f) fo[f * LIN_OBS + r] = pv[(f + 1) * LIN_OBS + r];
+      fo[(k - 1) * LIN_OBS + r] = y;
+    }
     if (done && r < LIN_OBS) y = (uniform01(io.seed, id, st, 100 + r) - 0.5f) * 0.2f;
     if (r < LIN_OBS) {
       s[r] = y;
@@ -223,8 +245,9 @@ using namespace aca;
 
 static EnvIO make_io(float* state, int32_t* t, int64_t* tg, float* ep_ret, float* ep_stats, const int64_t* ids,
                      const float* prev, float* out, float* reward, uint8_t* done, uint8_t* trunc, uint32_t seed,
-                     int max_steps, int k, int N) {
+                     int max_steps, int k, int N, float* final_out = nullptr) {
   EnvIO io;
+  io.final_out = final_out;
   io.state = state; io.t = t; io.tg = tg; io.ep_ret = ep_ret; io.ep_stats = ep_stats; io.env_ids = ids;
   io.prev = prev; io.out = out; io.reward = reward; io.done = done; io.truncated = trunc; io.seed = seed;
   io.max_steps = max_steps; io.k = k; io.N = N;
@@ -234,8 +257,10 @@ static EnvIO make_io(float* state, int32_t* t, int64_t* tg, float* ep_ret, float
 extern "C" hipError_t aca_env_step_cartpole(float* state, int32_t* t, int64_t* tg, float* ep_ret, float* ep_stats,
                                             const int64_t* ids, const int32_t* actions, const float* prev,
                                             float* out, float* reward, uint8_t* done, uint8_t* trunc,
-                                            uint32_t seed, int max_steps, int k, int N, hipStream_t stream) {
-  EnvIO io = make_io(state, t, tg, ep_ret, ep_stats, ids, prev, out, reward, done, trunc, seed, max_steps, k, N);
+                                            uint32_t seed, int max_steps, int k, int N, float* final_out,
+                                            hipStream_t stream) {
+  EnvIO io = make_io(state, t, tg, ep_ret, ep_stats, ids, prev, out, reward, done, trunc, seed, max_steps, k, N,
+                     final_out);
   const int bs = 256;
   cartpole_step_kernel<<<(N + bs - 1) / bs, bs, 0, stream>>>(io, actions);
   return hipGetLastError();
@@ -245,8 +270,9 @@ extern "C" hipError_t aca_env_step_pendulum(float* state, int32_t* t, int64_t* t
                                             const int64_t* ids, const float* actions, int act_dim,
                                             const float* prev, float* out, float* reward, uint8_t* done,
                                             uint8_t* trunc, uint32_t seed, int max_steps, int k, int N,
-                                            hipStream_t stream) {
-  EnvIO io = make_io(state, t, tg, ep_ret, ep_stats, ids, prev, out, reward, done, trunc, seed, max_steps, k, N);
+                                            float* final_out, hipStream_t stream) {
+  EnvIO io = make_io(state, t, tg, ep_ret, ep_stats, ids, prev, out, reward, done, trunc, seed, max_steps, k, N,
+                     final_out);
   const int bs = 256;
   pendulum_step_kernel<<<(N + bs - 1) / bs, bs, 0, stream>>>(io, actions, act_dim);
   return hipGetLastError();
@@ -256,8 +282,9 @@ extern "C" hipError_t aca_env_step_linear(float* state, int32_t* t, int64_t* tg,
                                           const int64_t* ids, const float* actions, const float* A, const float* B,
                                           const float* prev, float* out, float* reward, uint8_t* done,
                                           uint8_t* trunc, uint32_t seed, int max_steps, int k, int N,
-                                          hipStream_t stream) {
-  EnvIO io = make_io(state, t, tg, ep_ret, ep_stats, ids, prev, out, reward, done, trunc, seed, max_steps, k, N);
+                                          float* final_out, hipStream_t stream) {
+  EnvIO io = make_io(state, t, tg, ep_ret, ep_stats, ids, prev, out, reward, done, trunc, seed, max_steps, k, N,
+                     final_out);
   const int bs = 256;
   linear_step_kernel<<<(N * LIN_LANES + bs - 1) / bs, bs, 0, stream>>>(io, actions, A, B);
   return hipGetLastError();

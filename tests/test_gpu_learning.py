@@ -61,6 +61,35 @@ def test_cartpole_native_mlp_and_torch_engines_learn_alike(cuda):
     assert abs(finals["native"] - finals["torch"]) < 200, finals
 
 
+def test_pendulum_ppo_solves_and_checkpoint_evaluates(cuda, tmp_path):
+    """the framework solves the reference's flagship task. Pendulum-v0 swing-up with the
+    reference A3C actor / critic on the native MLP engine (preset pendulum_ppo: gamma 0.98, PPO-clip, one 200-step
+    episode per env per rollout): the mean finished-episode return rises from random play (about -1200) above -400
+    -- the bar the reference's own shipped demo policy meets (tests/test_ckpt_cpu.py) -- within 100 updates (320k env
+    steps); the trained policy is saved as a TF bundle under the reference names (global_actor/..., A3C/process.py's
+    Saver) and the evaluation CLI (cli/test_model.py, README.md:33-37) scores it above -400 too."""
+    import numpy as np
+    from actor_critic_algs_on_tensorflow_amd import ckpt
+    from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
+    from actor_critic_algs_on_tensorflow_amd.cli import test_model
+    tr = ActorCriticTrainer(preset("pendulum_ppo", device="cuda:0", outdir=None, quiet=True, stdout_freq=0,
+                                   save_every=0, seed=3))
+    assert tr.mlp is not None and tr.cfg.model_variant == "a3c"
+    tr.capture(warmup=1)
+    rets = []
+    for u in range(1, 101):
+        tr.step()
+        if u % 10 == 0:
+            rets.append(tr.env.drain_episode_stats()[0])
+    assert rets[0] < -600, rets               # random-level start (the first 10 updates)
+    assert np.mean(rets[-3:]) > -400, rets    # solved: the demo checkpoint's bar
+    path = tr.save_checkpoint(str(tmp_path / "model-Pendulum-ppo-100"))
+    names = ckpt.load_tensors(path)
+    assert "global_actor/mu_layer/kernel" in names and "global_critic/value/bias" in names
+    rewards = test_model.main(["Pendulum-v0", path, "--num_episodes", "10", "--animate_not", "--seed", "77"])
+    assert np.mean(rewards) > -400, rewards
+
+
 def test_mujoco_ppo_mlp_engine_improves(cuda):
     tr, rows = _curve("mujoco_ppo_dp8", 90, 30)
     assert tr.mlp is not None

@@ -52,7 +52,8 @@ def test_conv_wgrad_gemm_planes_match_autograd(cuda, layer, B, P):
 @pytest.mark.parametrize("adam", [False, True])
 def test_grad_finalize_opt_equals_two_launches(cuda, adam):
     """One launch of finaliser + optimiser (grid barrier between the phases) == grad_finalize then the optimiser
-    step reading the finalised slab: same parameters / moments / bf16 shadow (bitwise), and the slab is zero."""
+    step reading the finalised slab: same parameters / moments / bf16 shadow (RMSprop bitwise), and the slab is
+    zero."""
     from actor_critic_algs_on_tensorflow_amd import _native
     from actor_critic_algs_on_tensorflow_amd.ops.optim import (FlatParams, FusedAdam, FusedRMSprop,
                                                                finalize_jobs)
@@ -105,7 +106,12 @@ def test_grad_finalize_opt_equals_two_launches(cuda, adam):
     for k in a:
         if k == "grad":
             continue
-        assert torch.equal(a[k], b[k]), k
+        if adam and k in ("p", "m", "v", "shadow"):
+            # the Adam update compiles with different fp contractions in the two kernels (fma placement in the
+            # moment / step expressions): the same maths to the last ulp or two; RMSprop comes out bitwise
+            torch.testing.assert_close(a[k].float(), b[k].float(), rtol=1e-6, atol=1e-7)
+        else:
+            assert torch.equal(a[k], b[k]), k
     assert (b["grad"] == 0).all() and (a["grad"] == 0).all()
 
 
@@ -142,3 +148,36 @@ def test_gemm_mfma32_matches_fp32_reference(cuda, a_k, b_k, M, N, K, out_mode, e
     err = ((got - ref).norm() / ref.norm()).item()
     assert err < tol, err
     assert torch.isfinite(got).all()
+
+
+def test_native_mlp_time_limit_bootstrap_matches_oracle(cuda):
+    """time-limit bootstrapping on the native engines. The env kernel writes the terminal
+    observation of every transition (before the auto-reset), one critic launch values them after the rollout, and
+    the truncated steps' rewards carry gamma * V(terminal observation) -- the CPU oracle of
+    test_semantics_cpu.py::test_bootstrap_on_timeout_cuts_episode_and_bootstraps_terminal_value, on the GPU."""
+    from actor_critic_algs_on_tensorflow_amd import envs as E
+    from actor_critic_algs_on_tensorflow_amd import preset
+    from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
+    gamma = 0.9
+    env = E.make("Pendulum-v0", 3, seed=5, max_episode_steps=3, device=cuda)
+    cfg = preset("basic_ac", algo="a2c", num_envs=3, n_steps=7, gamma=gamma, look_ahead=None, returns="nstep",
+                 bootstrap_on_timeout=True, norm_adv=False, kl_adaptive_lr=False, anneal_regularizers=False,
+                 device="cuda:0", cuda_graph=False, outdir=None, quiet=True, stdout_freq=0, save_every=0)
+    tr = ActorCriticTrainer(cfg, env=env)
+    assert tr.mlp is not None, "the native MLP engine must run with bootstrap_on_timeout"
+    st = tr.storage
+    tr.collect()
+    torch.cuda.synchronize()
+    twin = E.make("Pendulum-v0", 3, seed=5, max_episode_steps=3, device=cuda)
+    twin.keep_final_obs = True
+    twin.reset()
+    with torch.no_grad():
+        for t in range(7):
+            prev = twin.obs.clone()
+            _, r, d, info = twin.step(st.actions[t], prev_obs=prev)
+            boot = gamma * tr.model.value(twin.final_obs) * info["truncated"].float()
+            assert torch.equal(d, st.dones[t])
+            torch.testing.assert_close(st.rewards[t], r + boot, rtol=1e-5, atol=1e-5)
+    assert st.truncated[2].all() and st.dones[2].all() and st.truncated[5].all()
+    # the terminal stacks are the pre-reset observations: never equal to the reset observation that follows
+    assert not torch.equal(tr._final_obs[2], st.obs[3])

@@ -122,6 +122,8 @@ class CNNEngine:
         # conv2 / conv3 weight gradients by the per-sample NHWC kernel (conv_wgrad.hip) from this many rows up
         self.nhwc_wgrad_min_b = int(os.environ.get("ACA_NHWC_WGRAD_MIN_B", "1024"))
         self.wgrad_gemm = os.environ.get("ACA_WGRAD_GEMM", "1") != "0"
+        self.serial_bwd = os.environ.get("ACA_SERIAL_BWD", "0") == "1"
+        self.serial_bwd_min_b = int(os.environ.get("ACA_SERIAL_BWD_MIN_B", "1024"))
         self.nhwc3_wgrad_min_b = int(os.environ.get("ACA_NHWC3_WGRAD_MIN_B", str(self.nhwc_wgrad_min_b)))
         # (the batched-position kernel's grid is one workgroup per plane: 256 planes cover the CUs)
         self.nhwc_planes = int(os.environ.get("ACA_NHWC_PLANES",
@@ -364,7 +366,9 @@ class CNNEngine:
         B, A1, ws = b.B, self.A1, self.ws
         ops = _native.require()
         main = torch.cuda.current_stream(self.dev)
-        side = self.side
+        # serial_bwd: the weight-gradient products run on the compute stream too (large batches: the persistent
+        # trunk backward holds every CU, and a side-stream product beside it only waits for LDS room)
+        side = main if (self.serial_bwd and b.B >= self.serial_bwd_min_b) else self.side
         ev = self._ev
         ws2 = self._side_ws()
         grouped = self.grouped and (head_done or stage == "trunk") and self.fused_bwd and self.det_wgrad

@@ -308,9 +308,10 @@ def gemm(A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha=1.0, bias=No
                 colsum_mod, tile, bk, splits, workspace, ga, ga_scale, gb, gb_scale, stamps)
 
 
-# large plain products (PPO minibatch fc layer) run on the 32x32x16-MFMA kernel (gemm_mfma32.hip) from this many
-# MACs up; ACAMD_GEMM32=0 keeps every product on the general kernel
-GEMM32 = os.environ.get("ACAMD_GEMM32", "1") != "0"
+# opt-in (ACAMD_GEMM32=1): large plain products on the 32x32x16-MFMA kernel (gemm_mfma32.hip) from this many MACs
+# up. Measured standalone at the PPO fc shapes it is 10-25 % SLOWER than the general kernel with its tuned plan
+# (profiles/r3_microbench_breakout_products.json: 45 / 58 / 58 us vs 41 / 47 / 46 us), so it is off by default.
+GEMM32 = os.environ.get("ACAMD_GEMM32", "0") == "1"
 GEMM32_MIN_MACS = int(os.environ.get("ACAMD_GEMM32_MIN_MACS", str(1 << 30)))
 
 

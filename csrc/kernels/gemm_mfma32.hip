@@ -22,10 +22,12 @@ typedef short g32_short4 __attribute__((ext_vector_type(4)));
 typedef short g32_short8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) g32_short4 g32_lds4;
 
-constexpr int G32_BM = 128, G32_BN = 128, G32_BK = 64, G32_T = 512;
-constexpr int G32_KLD = G32_BK + 8;     // [row][k] LDS row (k-contiguous operand), 144 B
-constexpr int G32_MLD = G32_BM + 8;     // [k][row] LDS row (m/n-contiguous operand), 272 B
-constexpr int G32_TILE_E = G32_BM * G32_KLD > G32_BK * G32_MLD ? G32_BM * G32_KLD : G32_BK * G32_MLD;
+constexpr int G32_BN = 128, G32_BK = 64;
+constexpr int G32_KLD = G32_BK + 8;     // [row][k] LDS row (k-contiguous operand), 144 B: the 16 rows a b128 read
+                                        // group touches start 36 dwords apart -> 64 distinct banks
+constexpr int G32_MLD = 128 + 32;       // [k][row] LDS row (m/n-contiguous operand), 320 B = 80 dwords: the four
+                                        // rows of a transposing read start 16 banks apart -> no overlap
+constexpr int G32_TILE_E = 128 * G32_KLD > G32_BK * G32_MLD ? 128 * G32_KLD : G32_BK * G32_MLD;
 
 struct G32Params {
   const u16* A;
@@ -66,44 +68,55 @@ __device__ __forceinline__ bf16x8 g32_frag(const u16* tile, int row0, int k0, in
   }
 }
 
-template <bool A_K, bool B_K>
-__global__ void __launch_bounds__(G32_T) gemm_mfma32_kernel(G32Params p) {
+// BM = 128 (8 waves) or 64 (4 waves): wave w owns rows 32 (w % (BM / 32)) .. + 31 and columns 64 (w / (BM / 32))
+// .. + 63 of the BM x 128 tile. The 64-row form doubles the workgroups of products with few 128 x 128 tiles.
+template <bool A_K, bool B_K, int BM>
+__global__ void __launch_bounds__(BM * 4) gemm_mfma32_kernel(G32Params p) {
+  constexpr int G32_T = BM * 4;                    // threads
+  constexpr int CA = BM * G32_BK / 8 / G32_T;      // A staging chunks per thread (2)
+  constexpr int CB = G32_BN * G32_BK / 8 / G32_T;  // B staging chunks per thread (2 | 4)
+  constexpr int WM = BM / 32;                      // waves along m
   __shared__ __attribute__((aligned(16))) u16 s_a[2][G32_TILE_E];
   __shared__ __attribute__((aligned(16))) u16 s_b[2][G32_TILE_E];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int m0 = blockIdx.x * G32_BM, n0 = blockIdx.y * G32_BN, z = blockIdx.z;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * G32_BN, z = blockIdx.z;
   const int kbeg = z * p.k_per_split, kend = min(p.K, kbeg + p.k_per_split);
   const int nk = (kend - kbeg) / G32_BK;
-  // staging slots: 1024 16-byte chunks per operand tile, 2 per thread
-  //   k-contiguous [row][k] tile: chunk c -> row c >> 3, k 8 (c & 7);  m/n-contiguous [k][row]: k c >> 4, row 8 (c & 15)
-  uint4 ra0, ra1, rb0, rb1;
+  // staging: 16-byte chunks; k-contiguous [row][k] tile: chunk c -> row c >> 3, k 8 (c & 7); m/n-contiguous
+  // [k][row] tile: k c / (rows / 8), row 8 (c % (rows / 8)). The next k-step's chunks wait in registers.
+  uint4 ra[CA], rb[CB];
   auto load = [&](int k0) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < CA; ++u) {
       const int c = tid + u * G32_T;
-      uint4 va, vb;
-      if (A_K) va = g32_load(p.A, p.lda, m0 + (c >> 3), k0 + 8 * (c & 7), p.M, p.K);
-      else va = g32_load(p.A, p.lda, k0 + (c >> 4), m0 + 8 * (c & 15), p.K, p.M);
-      if (B_K) vb = g32_load(p.B, p.ldb, n0 + (c >> 3), k0 + 8 * (c & 7), p.N, p.K);
-      else vb = g32_load(p.B, p.ldb, k0 + (c >> 4), n0 + 8 * (c & 15), p.K, p.N);
-      if (u == 0) { ra0 = va; rb0 = vb; } else { ra1 = va; rb1 = vb; }
+      if (A_K) ra[u] = g32_load(p.A, p.lda, m0 + (c >> 3), k0 + 8 * (c & 7), p.M, p.K);
+      else ra[u] = g32_load(p.A, p.lda, k0 + c / (BM / 8), m0 + 8 * (c % (BM / 8)), p.K, p.M);
+    }
+#pragma unroll
+    for (int u = 0; u < CB; ++u) {
+      const int c = tid + u * G32_T;
+      if (B_K) rb[u] = g32_load(p.B, p.ldb, n0 + (c >> 3), k0 + 8 * (c & 7), p.N, p.K);
+      else rb[u] = g32_load(p.B, p.ldb, k0 + (c >> 4), n0 + 8 * (c & 15), p.K, p.N);
     }
   };
   auto store = [&](int buf) {
+    u16* ta = s_a[buf];
+    u16* tb = s_b[buf];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < CA; ++u) {
       const int c = tid + u * G32_T;
-      const uint4 va = u == 0 ? ra0 : ra1, vb = u == 0 ? rb0 : rb1;
-      u16* ta = s_a[buf];
-      u16* tb = s_b[buf];
-      if (A_K) *reinterpret_cast<uint4*>(ta + (c >> 3) * G32_KLD + 8 * (c & 7)) = va;
-      else *reinterpret_cast<uint4*>(ta + (c >> 4) * G32_MLD + 8 * (c & 15)) = va;
-      if (B_K) *reinterpret_cast<uint4*>(tb + (c >> 3) * G32_KLD + 8 * (c & 7)) = vb;
-      else *reinterpret_cast<uint4*>(tb + (c >> 4) * G32_MLD + 8 * (c & 15)) = vb;
+      if (A_K) *reinterpret_cast<uint4*>(ta + (c >> 3) * G32_KLD + 8 * (c & 7)) = ra[u];
+      else *reinterpret_cast<uint4*>(ta + (c / (BM / 8)) * G32_MLD + 8 * (c % (BM / 8))) = ra[u];
+    }
+#pragma unroll
+    for (int u = 0; u < CB; ++u) {
+      const int c = tid + u * G32_T;
+      if (B_K) *reinterpret_cast<uint4*>(tb + (c >> 3) * G32_KLD + 8 * (c & 7)) = rb[u];
+      else *reinterpret_cast<uint4*>(tb + (c >> 4) * G32_MLD + 8 * (c & 15)) = rb[u];
     }
   };
   // wave tile: rows wm .. wm + 31 (one 32-row A fragment), columns wn .. wn + 63 (two 32-column B fragments)
-  const int wm = (wid & 3) * 32, wn = (wid >> 2) * 64;
+  const int wm = (wid % WM) * 32, wn = (wid / WM) * 64;
   g32_floatx16 acc0, acc1;
 #pragma unroll
   for (int i = 0; i < 16; ++i) { acc0[i] = 0.f; acc1[i] = 0.f; }
@@ -184,10 +197,18 @@ extern "C" hipError_t aca_gemm_mfma32(const AcaGemmDesc* d, hipStream_t stream) 
   p.out_mode = d->out_mode;
   p.relu = d->relu;
   p.alpha = d->alpha;
-  dim3 grid((d->M + G32_BM - 1) / G32_BM, (d->N + G32_BN - 1) / G32_BN, splits);
-  if (d->a_k && d->b_k) gemm_mfma32_kernel<true, true><<<grid, G32_T, 0, stream>>>(p);
-  else if (d->a_k) gemm_mfma32_kernel<true, false><<<grid, G32_T, 0, stream>>>(p);
-  else if (d->b_k) gemm_mfma32_kernel<false, true><<<grid, G32_T, 0, stream>>>(p);
-  else gemm_mfma32_kernel<false, false><<<grid, G32_T, 0, stream>>>(p);
+  // 64-row tiles when 128 x 128 tiles would leave CUs idle (fewer than 256 workgroups)
+  const int tn = (d->N + G32_BN - 1) / G32_BN;
+  const bool small = (int64_t)((d->M + 127) / 128) * tn * splits < 256;
+  const int bm = small ? 64 : 128;
+  dim3 grid((d->M + bm - 1) / bm, tn, splits);
+#define G32_LAUNCH(AK, BK_)                                                                              \
+  if (small) gemm_mfma32_kernel<AK, BK_, 64><<<grid, 256, 0, stream>>>(p);                               \
+  else gemm_mfma32_kernel<AK, BK_, 128><<<grid, 512, 0, stream>>>(p);
+  if (d->a_k && d->b_k) { G32_LAUNCH(true, true) }
+  else if (d->a_k) { G32_LAUNCH(true, false) }
+  else if (d->b_k) { G32_LAUNCH(false, true) }
+  else { G32_LAUNCH(false, false) }
+#undef G32_LAUNCH
   return hipGetLastError();
 }

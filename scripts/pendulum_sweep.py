@@ -23,6 +23,7 @@ CONFIGS = {
     # the reference A3C hyper-parameters verbatim (lr cap 0.1)
     "cap01": dict(),
     "cap001": dict(max_lr=0.01),
+    "cap001_torch": dict(max_lr=0.01, engine="torch"),
     "cap0003": dict(max_lr=0.003),
     "cap001_n64": dict(max_lr=0.01, num_envs=64),
     "cap001_n128": dict(max_lr=0.01, num_envs=128),

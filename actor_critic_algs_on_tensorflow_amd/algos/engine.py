@@ -122,7 +122,8 @@ class CNNEngine:
         # conv2 / conv3 weight gradients by the per-sample NHWC kernel (conv_wgrad.hip) from this many rows up
         self.nhwc_wgrad_min_b = int(os.environ.get("ACA_NHWC_WGRAD_MIN_B", "1024"))
         self.wgrad_gemm = os.environ.get("ACA_WGRAD_GEMM", "1") != "0"
-        self.serial_bwd = os.environ.get("ACA_SERIAL_BWD", "0") == "1"
+        # large-batch backward on ONE stream (Breakout PPO 18.3 -> 17.0 ms per update, profiles/r3_breakout_ab.txt)
+        self.serial_bwd = os.environ.get("ACA_SERIAL_BWD", "1") == "1"
         self.serial_bwd_min_b = int(os.environ.get("ACA_SERIAL_BWD_MIN_B", "1024"))
         self.nhwc3_wgrad_min_b = int(os.environ.get("ACA_NHWC3_WGRAD_MIN_B", str(self.nhwc_wgrad_min_b)))
         # (the batched-position kernel's grid is one workgroup per plane: 256 planes cover the CUs)

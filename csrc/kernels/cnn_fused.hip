@@ -17,6 +17,8 @@
 // layer). The frames are staged as exact bf16 integers and the 1/255 scale is applied to the fp32 accumulator in
 // the conv1 epilogue (one conversion per pixel instead of one per im2col element). Work split: conv1 -- waves take M tiles round-robin and both N tiles; conv2/3 -- wave w
 // owns output-channel tile w for every M tile, so every B fragment is loaded exactly once per workgroup.
+#include <cstdlib>
+
 #include "common.h"
 #include "cnn_head.h"
 #include "pong_env.h"
@@ -249,21 +251,33 @@ __device__ __forceinline__ int tr_y1_own_begin(int r) { return (20 * r + 6) / 7;
 // conv1 -> conv3 of row workgroup (e, r) from its staged input rows (s_in: 4 frames x 36 rows of bf16 pixel values,
 // complete) and the conv1 weights (s_w1, complete); stores the owned y1 / y2 rows and its y3 row. Shared by the
 // trunk kernel and the fused policy/env + trunk kernel.
-template <bool LATE_W>
+// conv2 / conv3 B fragments of wave-column n2 = wid * 16 + (lane & 15) (16 + 18 k-steps, 16-byte loads)
+__device__ __forceinline__ void trunk_w23_load(const u16* __restrict__ W2, const u16* __restrict__ W3,
+                                               bf16x8 (&bw2)[16], bf16x8 (&bw3)[18]) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int n2 = wid * 16 + (lane & 15), lg = lane >> 4;
+#pragma unroll
+  for (int ks = 0; ks < 16; ++ks) bw2[ks] = *reinterpret_cast<const bf16x8*>(W2 + n2 * 512 + ks * 32 + lg * 8);
+#pragma unroll
+  for (int ks = 0; ks < 18; ++ks) bw3[ks] = *reinterpret_cast<const bf16x8*>(W3 + n2 * 576 + ks * 32 + lg * 8);
+}
+
+// WMODE (when the conv2 / conv3 weight fragments are requested): 0 at entry (the staging barrier waited for obs +
+// W1 only), 1 after conv1's MFMAs (trunk mode 2), 2 by the caller, before anything else of its launch (the fused
+// step: the loads overlap the policy head, the env step and the render)
+template <int WMODE>
 __device__ __forceinline__ void trunk_rows_compute(const u16* __restrict__ s_in, const u16* __restrict__ s_w1,
                                                    u16* __restrict__ s_y1, u16* __restrict__ s_y2, int e, int r,
                                                    const float bias1a, const float bias1b, const float bias2,
                                                    const float bias3, const u16* __restrict__ W2,
                                                    const u16* __restrict__ W3, u16* __restrict__ y1g,
                                                    u16* __restrict__ y2g, u16* __restrict__ y3g, float scale,
-                                                   uint64_t* __restrict__ stamps) {
+                                                   uint64_t* __restrict__ stamps, bf16x8 (&bw2)[16],
+                                                   bf16x8 (&bw3)[18]) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l16 = lane & 15, lg = lane >> 4;
   const int n2 = wid * 16 + l16;
-  // conv2 / conv3 weight fragments: issued now (the staging barrier waited for obs + W1 only), consumed after conv1
-  // (LATE_W: issued after conv1's MFMAs instead -- A/B variant, trunk mode 2)
-  bf16x8 bw2[16], bw3[18];
-  if constexpr (!LATE_W) {
+  if constexpr (WMODE == 0) {
 #pragma unroll
     for (int ks = 0; ks < 16; ++ks) bw2[ks] = *reinterpret_cast<const bf16x8*>(W2 + n2 * 512 + ks * 32 + lg * 8);
 #pragma unroll
@@ -308,7 +322,7 @@ __device__ __forceinline__ void trunk_rows_compute(const u16* __restrict__ s_in,
       }
     }
   }
-  if constexpr (LATE_W) {
+  if constexpr (WMODE == 1) {
 #pragma unroll
     for (int ks = 0; ks < 16; ++ks) bw2[ks] = *reinterpret_cast<const bf16x8*>(W2 + n2 * 512 + ks * 32 + lg * 8);
 #pragma unroll
@@ -462,8 +476,9 @@ __global__ void __launch_bounds__(T_THREADS) cnn_trunk_rows_kernel(
     __syncthreads();
   }
   stamp(stamps, 1);
-  trunk_rows_compute<LATE_W>(s_in, s_w1, s_y1, s_y2, e, r, bias1a, bias1b, bias2, bias3, W2, W3, y1g, y2g, y3g,
-                             scale, stamps);
+  bf16x8 bw2[16], bw3[18];
+  trunk_rows_compute<LATE_W ? 1 : 0>(s_in, s_w1, s_y1, s_y2, e, r, bias1a, bias1b, bias2, bias3, W2, W3, y1g, y2g,
+                                     y3g, scale, stamps, bw2, bw3);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -503,7 +518,7 @@ __device__ __forceinline__ void pong_commit_next(const PongIO& io, const PongNex
   sp[0] = q.bx; sp[1] = q.by; sp[2] = q.vx; sp[3] = q.vy; sp[4] = q.pa; sp[5] = q.po; sp[6] = q.sa; sp[7] = q.so;
 }
 
-template <int A1>
+template <int A1, bool EARLY_W>
 __global__ void __launch_bounds__(T_THREADS) pong_fused_step_kernel(
     PongIO io, PongNext nx, FcParts fc, u16* __restrict__ h, const u16* __restrict__ Wh,
     const float* __restrict__ bh, float* __restrict__ z_out, int32_t* __restrict__ act, float* __restrict__ logp,
@@ -550,6 +565,10 @@ __global__ void __launch_bounds__(T_THREADS) pong_fused_step_kernel(
   uint4 vw[W1_PER];
 #pragma unroll
   for (int u = 0; u < W1_PER; ++u) vw[u] = reinterpret_cast<const uint4*>(W1)[tid + u * T_THREADS];
+  // EARLY_W: the conv2 / conv3 weight fragments are requested now, after every load the head and the staging
+  // wait for (the vm counter retires in issue order), so they arrive while the head, env and render run
+  bf16x8 bw2[16], bw3[18];
+  if constexpr (EARLY_W) trunk_w23_load(W2, W3, bw2, bw3);
   // ---------------------------------------------------------------- policy head (every row workgroup of env e)
   float hf[2];
   fc_h2_from_parts(fc.hpart, fc.S, fc.plane_stride, fc.bfc, e, tid, lead ? h : nullptr, hf);
@@ -664,8 +683,8 @@ __global__ void __launch_bounds__(T_THREADS) pong_fused_step_kernel(
   }
   __syncthreads();
   stamp(stamps, 1);
-  trunk_rows_compute<true>(s_in, s_w1, s_y1, s_y2, e, r, bias1a, bias1b, bias2, bias3, W2, W3, y1g, y2g, y3g,
-                           scale, stamps);
+  trunk_rows_compute<EARLY_W ? 2 : 1>(s_in, s_w1, s_y1, s_y2, e, r, bias1a, bias1b, bias2, bias3, W2, W3, y1g, y2g,
+                                      y3g, scale, stamps, bw2, bw3);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -1291,12 +1310,22 @@ extern "C" hipError_t aca_pong_fused_step(
   aca::PongNext nx{state_n, t_n, tg_n, ep_ret_n};
   aca::FcParts fc{hpart, S, plane_stride, bfc};
   const int grid = N * aca::TR_ROWS;
+  // ACA_FUSED_EARLY_W=1: conv2 / conv3 weight fragments requested at kernel entry (A/B knob, read once)
+  static const bool early = [] {
+    const char* v = getenv("ACA_FUSED_EARLY_W");
+    return v && v[0] == '1';
+  }();
   switch (A + 1) {
 #define ACA_FUSED_CASE(A1)                                                                                       \
   case A1:                                                                                                       \
-    aca::pong_fused_step_kernel<A1><<<grid, aca::T_THREADS, 0, stream>>>(                                         \
-        io, nx, fc, h, Wh, bh, z, act, logp, ent, value, key_shift, pseed, W1, b1, W2, b2, W3, b3, y1, y2, y3,    \
-        scale, shift_out, stamps);                                                                               \
+    if (early)                                                                                                   \
+      aca::pong_fused_step_kernel<A1, true><<<grid, aca::T_THREADS, 0, stream>>>(                                \
+          io, nx, fc, h, Wh, bh, z, act, logp, ent, value, key_shift, pseed, W1, b1, W2, b2, W3, b3, y1, y2, y3,  \
+          scale, shift_out, stamps);                                                                             \
+    else                                                                                                         \
+      aca::pong_fused_step_kernel<A1, false><<<grid, aca::T_THREADS, 0, stream>>>(                               \
+          io, nx, fc, h, Wh, bh, z, act, logp, ent, value, key_shift, pseed, W1, b1, W2, b2, W3, b3, y1, y2, y3,  \
+          scale, shift_out, stamps);                                                                             \
     break;
     ACA_FUSED_CASE(3) ACA_FUSED_CASE(4) ACA_FUSED_CASE(5) ACA_FUSED_CASE(6) ACA_FUSED_CASE(7)
 #undef ACA_FUSED_CASE

@@ -229,6 +229,290 @@ __global__ void __launch_bounds__(T_THREADS) cnn_trunk_fwd_kernel(
 }
 
 // ------------------------------------------------------------------------------------------------------------
+// Persistent form of the per-env trunk for large learner batches (PPO minibatches, B = 4096): one workgroup per
+// CU walks samples b = blockIdx.x, blockIdx.x + gridDim.x, ... The per-env kernel above re-reads the conv2 / conv3
+// weights (136 KB) from L2 for every sample and stages each observation only after the previous sample has left
+// the CU; here every wave extracts its W2 / W3 B fragments (its output-channel tile, all k) ONCE and keeps them in
+// registers for the whole walk, and the next sample's frames are copied global -> LDS by the LDS-DMA path
+// (global_load_lds_dwordx4: no registers, tracked by the vm counter) into the second half of a double-buffered
+// uint8 staging area while the current sample is multiplied. conv1 converts its uint8 pixels to exact bf16 integers
+// on the fly. Same MFMA order and epilogues as the per-env kernel: bit-identical outputs.
+constexpr int TP_OBS_PAD = 28 * 1024;   // one observation (28224 B) padded to whole 1 KB wave copies
+
+__device__ __forceinline__ void trunk_w23_load(const u16* __restrict__ W2, const u16* __restrict__ W3,
+                                               bf16x8 (&bw2)[16], bf16x8 (&bw3)[18]);
+
+__device__ __forceinline__ void trunk_obs_dma(const uint8_t* __restrict__ src, uint8_t* dst_lds) {
+  // 28 wave-copies of 64 x 16 B: wave w copies blocks w, w + 4, ...; lanes past the observation read its last
+  // chunk again (their bytes land in the padding)
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int blk = wid; blk < TP_OBS_PAD / 1024; blk += T_THREADS / 64) {
+    const int c = min(blk * 64 + lane, OBS_BYTES / 16 - 1);
+    uint8_t* base = dst_lds + blk * 1024;   // wave-uniform LDS base (lane i lands at base + 16 i)
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint4*>(src) + c,
+                                     (__attribute__((address_space(3))) void*)(base), 16, 0, 0);
+  }
+}
+
+__global__ void __launch_bounds__(T_THREADS) cnn_trunk_fwd_persist_kernel(
+    const uint8_t* __restrict__ obs, const u16* __restrict__ W1, const float* __restrict__ b1,
+    const u16* __restrict__ W2, const float* __restrict__ b2, const u16* __restrict__ W3,
+    const float* __restrict__ b3, u16* __restrict__ y1g, u16* __restrict__ y2g, u16* __restrict__ y3g,
+    float scale, int B) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_obs8[2][TP_OBS_PAD];
+  __shared__ __attribute__((aligned(16))) u16 s_w1[32 * W1_LD];
+  __shared__ __attribute__((aligned(16))) u16 s_y1[Y1_ROWS * Y1_LD];
+  __shared__ __attribute__((aligned(16))) u16 s_y2[Y2_ROWS * Y2_LD];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int l16 = lane & 15, lg = lane >> 4;
+  const int n2 = wid * 16 + l16;
+  const int b0 = blockIdx.x;
+  if (b0 >= B) return;
+  // ---- first observation in flight, then the resident weights
+  trunk_obs_dma(obs + (size_t)b0 * OBS_BYTES, s_obs8[0]);
+  {
+    constexpr int W1_PER = 32 * 256 / 8 / T_THREADS;   // 4
+#pragma unroll
+    for (int u = 0; u < W1_PER; ++u) {
+      const int i = tid + u * T_THREADS, r = i / 32, c8 = (i % 32) * 8;
+      *reinterpret_cast<uint4*>(s_w1 + r * W1_LD + c8) = reinterpret_cast<const uint4*>(W1)[i];
+    }
+  }
+  bf16x8 bw2[16], bw3[18];
+  trunk_w23_load(W2, W3, bw2, bw3);
+  const float bias1a = b1[l16], bias1b = b1[16 + l16], bias2 = b2[n2], bias3 = b3[n2];
+  int buf = 0;
+  for (int b = b0; b < B; b += gridDim.x) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this sample's frames have landed (and the weights)
+    __syncthreads();
+    if (b + gridDim.x < B) trunk_obs_dma(obs + (size_t)(b + gridDim.x) * OBS_BYTES, s_obs8[buf ^ 1]);
+    const uint8_t* so = s_obs8[buf];
+    // ------------------------------------------------------------ conv1: M 400 (25 tiles), N 32 (2), K 256 (8)
+    {
+      bf16x8 bw[2][8];
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks)
+          bw[nt][ks] = *reinterpret_cast<const bf16x8*>(s_w1 + (nt * 16 + l16) * W1_LD + ks * 32 + lg * 8);
+      for (int mt = wid; mt < 25; mt += 4) {
+        floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+        const int m = mt * 16 + l16;
+        const int oh = m / 20, ow = m - oh * 20;
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+          const int k = ks * 32 + lg * 8;
+          const int c = k >> 6, i = (k >> 3) & 7;
+          const uint8_t* p = so + (c * 84 + oh * 4 + i) * 84 + ow * 4;   // 4-byte aligned
+          const uint32_t w0 = *reinterpret_cast<const uint32_t*>(p), w1 = *reinterpret_cast<const uint32_t*>(p + 4);
+          const uint2 lo = u8x4_to_bf16(w0), hi = u8x4_to_bf16(w1);
+          const bf16x8 a = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw[0][ks], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw[1][ks], acc1, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = mt * 16 + lg * 4 + r;
+          const u16 v0 = f2bf(fmaxf(acc0[r] * scale + bias1a, 0.f));
+          const u16 v1 = f2bf(fmaxf(acc1[r] * scale + bias1b, 0.f));
+          s_y1[row * Y1_LD + l16] = v0;
+          s_y1[row * Y1_LD + 16 + l16] = v1;
+          y1g[((size_t)b * Y1_ROWS + row) * Y1_C + l16] = v0;
+          y1g[((size_t)b * Y1_ROWS + row) * Y1_C + 16 + l16] = v1;
+        }
+      }
+    }
+    __syncthreads();
+    // ------------------------------------------------------------ conv2: M 81 (6 tiles), N 64 (wave = N tile), K 512
+    {
+      floatx4 acc[6];
+#pragma unroll
+      for (int mt = 0; mt < 6; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 16; ++ks) {
+        const int k = ks * 32 + lg * 8;
+        const int i = k >> 7, j = (k >> 5) & 3, c0 = k & 31;
+#pragma unroll
+        for (int mt = 0; mt < 6; ++mt) {
+          const int m = min(mt * 16 + l16, Y2_ROWS - 1);
+          const int oh = m / 9, ow = m - oh * 9;
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(s_y1 + ((oh * 2 + i) * 20 + ow * 2 + j) * Y1_LD + c0);
+          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw2[ks], acc[mt], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int mt = 0; mt < 6; ++mt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = mt * 16 + lg * 4 + r;
+          if (row < Y2_ROWS) {
+            const u16 v = f2bf(fmaxf(acc[mt][r] + bias2, 0.f));
+            s_y2[row * Y2_LD + n2] = v;
+            y2g[((size_t)b * Y2_ROWS + row) * Y2_C + n2] = v;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // ------------------------------------------------------------ conv3: M 49 (4 tiles), N 64 (wave = N tile), K 576
+    {
+      floatx4 acc[4];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 18; ++ks) {
+        const int k = ks * 32 + lg * 8;
+        const int i = k / 192, j = (k >> 6) % 3, c0 = k & 63;
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt) {
+          const int m = min(mt * 16 + l16, Y3_ROWS - 1);
+          const int oh = m / 7, ow = m - oh * 7;
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(s_y2 + ((oh + i) * 9 + ow + j) * Y2_LD + c0);
+          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw3[ks], acc[mt], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = mt * 16 + lg * 4 + r;
+          if (row < Y3_ROWS) y3g[((size_t)b * Y3_ROWS + row) * Y3_C + n2] = f2bf(fmaxf(acc[mt][r] + bias3, 0.f));
+        }
+      }
+    }
+    buf ^= 1;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// Per-env trunk, lean-LDS form: the observation is staged as its uint8 bytes by LDS-DMA (28 KB instead of 56 KB of
+// bf16, no staging registers) and the conv1 weight fragments come straight from L2 into registers (no 17 KB W1
+// stage), so a workgroup needs 74 KB of LDS and TWO fit a CU: while one sample waits on a barrier or a memory round
+// trip the other one's MFMAs run (the 118 KB form above runs one workgroup -- one wave per SIMD -- per CU). conv1
+// converts the pixels to exact bf16 integers on the fly; same MFMA order and epilogues: bit-identical outputs.
+__global__ void __launch_bounds__(T_THREADS) cnn_trunk_fwd_u8_kernel(
+    const uint8_t* __restrict__ obs, const u16* __restrict__ W1, const float* __restrict__ b1,
+    const u16* __restrict__ W2, const float* __restrict__ b2, const u16* __restrict__ W3,
+    const float* __restrict__ b3, u16* __restrict__ y1g, u16* __restrict__ y2g, u16* __restrict__ y3g,
+    float scale, uint8_t* __restrict__ shift_out) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_obs8[TP_OBS_PAD];
+  __shared__ __attribute__((aligned(16))) u16 s_y1[Y1_ROWS * Y1_LD];
+  __shared__ __attribute__((aligned(16))) u16 s_y2[Y2_ROWS * Y2_LD];
+  const int e = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int l16 = lane & 15, lg = lane >> 4;
+  const int n2 = wid * 16 + l16;
+  // loads in the order they are consumed (the vm counter retires in issue order): frames (LDS-DMA), conv1
+  // fragments, conv2 fragments; conv3's after conv1
+  trunk_obs_dma(obs + (size_t)e * OBS_BYTES, s_obs8);
+  bf16x8 bw[2][8];
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+      bw[nt][ks] = *reinterpret_cast<const bf16x8*>(W1 + (nt * 16 + l16) * 256 + ks * 32 + lg * 8);
+  bf16x8 bw2[16];
+#pragma unroll
+  for (int ks = 0; ks < 16; ++ks) bw2[ks] = *reinterpret_cast<const bf16x8*>(W2 + n2 * 512 + ks * 32 + lg * 8);
+  const float bias0 = b1[l16], bias1 = b1[16 + l16], bias2 = b2[n2], bias3 = b3[n2];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (shift_out) {   // rollout: frames 1..3 of this observation become frames 0..2 of the next one
+    uint4* so = reinterpret_cast<uint4*>(shift_out + (size_t)e * OBS_BYTES);
+    const uint4* si = reinterpret_cast<const uint4*>(s_obs8);
+    for (int i = OBS_BYTES / 64 + tid; i < OBS_BYTES / 16; i += T_THREADS) so[i - OBS_BYTES / 64] = si[i];
+  }
+  // ---------------------------------------------------------------- conv1: M 400 (25 tiles), N 32 (2), K 256 (8)
+  for (int mt = wid; mt < 25; mt += 4) {
+    floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    const int m = mt * 16 + l16;
+    const int oh = m / 20, ow = m - oh * 20;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      const int k = ks * 32 + lg * 8;
+      const int c = k >> 6, i = (k >> 3) & 7;
+      const uint8_t* p = s_obs8 + (c * 84 + oh * 4 + i) * 84 + ow * 4;   // 4-byte aligned
+      const uint2 lo = u8x4_to_bf16(*reinterpret_cast<const uint32_t*>(p));
+      const uint2 hi = u8x4_to_bf16(*reinterpret_cast<const uint32_t*>(p + 4));
+      const bf16x8 a = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw[0][ks], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw[1][ks], acc1, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = mt * 16 + lg * 4 + r;
+      const u16 v0 = f2bf(fmaxf(acc0[r] * scale + bias0, 0.f));
+      const u16 v1 = f2bf(fmaxf(acc1[r] * scale + bias1, 0.f));
+      s_y1[row * Y1_LD + l16] = v0;
+      s_y1[row * Y1_LD + 16 + l16] = v1;
+      y1g[((size_t)e * Y1_ROWS + row) * Y1_C + l16] = v0;
+      y1g[((size_t)e * Y1_ROWS + row) * Y1_C + 16 + l16] = v1;
+    }
+  }
+  bf16x8 bw3[18];
+#pragma unroll
+  for (int ks = 0; ks < 18; ++ks) bw3[ks] = *reinterpret_cast<const bf16x8*>(W3 + n2 * 576 + ks * 32 + lg * 8);
+  __syncthreads();
+  // ---------------------------------------------------------------- conv2: M 81 (6 tiles), N 64 (wave = N tile), K 512
+  {
+    floatx4 acc[6];
+#pragma unroll
+    for (int mt = 0; mt < 6; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) {
+      const int k = ks * 32 + lg * 8;
+      const int i = k >> 7, j = (k >> 5) & 3, c0 = k & 31;
+#pragma unroll
+      for (int mt = 0; mt < 6; ++mt) {
+        const int m = min(mt * 16 + l16, Y2_ROWS - 1);
+        const int oh = m / 9, ow = m - oh * 9;
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(s_y1 + ((oh * 2 + i) * 20 + ow * 2 + j) * Y1_LD + c0);
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw2[ks], acc[mt], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int mt = 0; mt < 6; ++mt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = mt * 16 + lg * 4 + r;
+        if (row < Y2_ROWS) {
+          const u16 v = f2bf(fmaxf(acc[mt][r] + bias2, 0.f));
+          s_y2[row * Y2_LD + n2] = v;
+          y2g[((size_t)e * Y2_ROWS + row) * Y2_C + n2] = v;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // ---------------------------------------------------------------- conv3: M 49 (4 tiles), N 64 (wave = N tile), K 576
+  {
+    floatx4 acc[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 18; ++ks) {
+      const int k = ks * 32 + lg * 8;
+      const int i = k / 192, j = (k >> 6) % 3, c0 = k & 63;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const int m = min(mt * 16 + l16, Y3_ROWS - 1);
+        const int oh = m / 7, ow = m - oh * 7;
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(s_y2 + ((oh + i) * 9 + ow + j) * Y2_LD + c0);
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw3[ks], acc[mt], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = mt * 16 + lg * 4 + r;
+        if (row < Y3_ROWS) y3g[((size_t)e * Y3_ROWS + row) * Y3_C + n2] = f2bf(fmaxf(acc[mt][r] + bias3, 0.f));
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
 // Row-split trunk: 7 workgroups per env, workgroup r computes the receptive field of conv3 output row r only
 // (conv2 rows r..r+2, conv1 rows 2r..2r+7, input rows 8r..8r+35). The per-env kernel above keeps one CU busy per
 // env (32 of 256 CUs at the bench's 32 envs) and its layers run at one wave per SIMD; here 7x the CUs each do
@@ -1260,6 +1544,30 @@ extern "C" hipError_t aca_cnn_trunk_fwd(const uint8_t* obs, const uint16_t* W1, 
                                         uint16_t* y2, uint16_t* y3, int B, float scale, uint8_t* shift_out,
                                         uint64_t* stamps, hipStream_t stream) {
   if (B <= 0) return hipSuccess;
+  // persistent walk (one workgroup per CU) for learner batches: ACA_TRUNK_FWD_PERSIST workgroups (0 = off)
+  static const int persist = [] {
+    const char* v = getenv("ACA_TRUNK_FWD_PERSIST");
+    return v ? atoi(v) : 0;   // measured slower than the per-env kernel on Breakout PPO (17.45 vs 17.18 ms)
+  }();
+  static const int persist_min_b = [] {
+    const char* v = getenv("ACA_TRUNK_FWD_PERSIST_MIN_B");
+    return v ? atoi(v) : 1024;
+  }();
+  // lean-LDS per-env form (two workgroups per CU); ACA_TRUNK_FWD_U8=0 keeps the bf16-staged form
+  static const bool u8 = [] {
+    const char* v = getenv("ACA_TRUNK_FWD_U8");
+    return !v || v[0] != '0';
+  }();
+  if (u8 && !stamps && !(persist > 0 && B >= persist_min_b && !shift_out)) {
+    aca::cnn_trunk_fwd_u8_kernel<<<B, aca::T_THREADS, 0, stream>>>(obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale,
+                                                                    shift_out);
+    return hipGetLastError();
+  }
+  if (persist > 0 && B >= persist_min_b && !shift_out && !stamps) {
+    aca::cnn_trunk_fwd_persist_kernel<<<persist < B ? persist : B, aca::T_THREADS, 0, stream>>>(
+        obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale, B);
+    return hipGetLastError();
+  }
   aca::cnn_trunk_fwd_kernel<<<B, aca::T_THREADS, 0, stream>>>(obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale,
                                                                shift_out, stamps);
   return hipGetLastError();

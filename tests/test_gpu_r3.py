@@ -181,3 +181,33 @@ def test_native_mlp_time_limit_bootstrap_matches_oracle(cuda):
     assert st.truncated[2].all() and st.dones[2].all() and st.truncated[5].all()
     # the terminal stacks are the pre-reset observations: never equal to the reset observation that follows
     assert not torch.equal(tr._final_obs[2], st.obs[3])
+
+
+def test_trunk_fwd_persistent_equals_per_env_kernel(cuda):
+    """The persistent trunk forward (cnn_fused.hip cnn_trunk_fwd_persist_kernel: one workgroup per CU walking
+    samples, W2 / W3 fragments resident in registers, the next observation copied global -> LDS by LDS-DMA as uint8)
+    is BITWISE equal to the per-env kernel (taken for batches below ACA_TRUNK_FWD_PERSIST_MIN_B = 1024): same bf16
+    integer pixels, same MFMA order. 1283 samples: the walk ends unevenly over the 256 workgroups."""
+    from actor_critic_algs_on_tensorflow_amd.ops import gemm as G
+    torch.manual_seed(4)
+    B = 1283
+    obs = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, device=cuda)
+    W1 = (torch.randn(32, 256, device=cuda) * 0.05).to(torch.bfloat16)
+    W2 = (torch.randn(64, 512, device=cuda) * 0.05).to(torch.bfloat16)
+    W3 = (torch.randn(64, 576, device=cuda) * 0.05).to(torch.bfloat16)
+    b1, b2, b3 = (torch.rand(n, device=cuda) * 0.1 - 0.02 for n in (32, 64, 64))
+
+    def run(o):
+        n = o.shape[0]
+        y1 = torch.full((n * 400, 32), float("nan"), dtype=torch.bfloat16, device=cuda)
+        y2 = torch.full((n * 81, 64), float("nan"), dtype=torch.bfloat16, device=cuda)
+        y3 = torch.full((n * 49, 64), float("nan"), dtype=torch.bfloat16, device=cuda)
+        G.cnn_trunk_fwd(o, W1, b1, W2, b2, W3, b3, y1, y2, y3, mode=0)
+        return y1, y2, y3
+
+    big = run(obs)                                   # persistent walk (B >= 1024)
+    parts = [run(obs[i:i + 700]) for i in (0, 700)]  # per-env kernel (B < 1024)
+    torch.cuda.synchronize()
+    for k in range(3):
+        ref = torch.cat([p[k] for p in parts])
+        assert torch.equal(big[k], ref), k

@@ -109,6 +109,10 @@ class CNNEngine:
         # A2C head in one launch (head_bwd: loss + dz + dh + dWh + dbh + dbfc, no GEMMs) for categorical heads of up
         # to 7 actions and learner batches up to 1024 rows
         self.fused_head = os.environ.get("ACA_FUSED_HEAD", "1") != "0"
+        # A2C head v2 (loss.hip a2c_head_kernel): bootstrap value + returns + loss + head backward in one launch of 32
+        # narrow workgroups (ACA_A2C_HEAD=0: fc_value + the 8-workgroup head_bwd kernel of round 2)
+        self.a2c_head = os.environ.get("ACA_A2C_HEAD", "1") != "0"
+        self._a2c_bar = None
         # A2C learner on ONE stream with grouped GEMM launches instead of a side stream joined by events
         self.grouped = os.environ.get("ACA_GROUPED", "1") != "0"
         # conv weight gradients as split-K partial planes reduced in plane order by the finaliser (deterministic);
@@ -343,10 +347,23 @@ class CNNEngine:
         return (self.fused_head and 2 <= self.A <= 7 and 1 <= B <= self.HB_MAXB and 1 <= N <= self.HB_MAXN
                 and B % N == 0)
 
-    def head_backward(self, b: _Bufs, actions, logp_old, ent_coef, kl_coef, vf_coef, stats, returns):
-        """A2C fast path: ``head_bwd`` -- returns/EV/adv-norm + loss + dz and the head's backward (dh, dWh, dbh,
-        dbfc) in one launch; :meth:`backward` then starts at the fc layer (``head_done=True``)."""
+    def head_backward(self, b: _Bufs, actions, logp_old, ent_coef, kl_coef, vf_coef, stats, returns, boot=None):
+        """A2C fast path: ``a2c_head`` (or round 2's ``head_bwd``) -- returns/EV/adv-norm + loss + dz and the head's
+        backward (dh, dWh, dbh, dbfc) in one launch; :meth:`backward` then starts at the fc layer (``head_done=True``).
+        ``boot`` = (fc partial planes, count) of the bootstrap observation: V(s_T) is computed in the same launch and
+        written into ``returns["val"][T]`` (the rollout then skips its ``fc_value`` launch)."""
         r = returns
+        if self.a2c_head:
+            if self._a2c_bar is None:
+                self._a2c_bar = torch.zeros(4, dtype=torch.int32, device=self.dev)
+            hp, S = boot if boot is not None else (None, 0)
+            _native.require().a2c_head(b.z, actions, logp_old, ent_coef, kl_coef, float(vf_coef), r["rew"], r["val"],
+                                       r["dones"], int(r["L"]), int(r["mode"]), bool(r["norm_adv"]), float(r["gamma"]),
+                                       float(r["lam"]), r["ret_w"], r["adv_w"], b.h, self.sWh, b.dh, self.gWh,
+                                       self.gbh, self.gbfc, stats, hp, int(S), self.bfc if hp is not None else None,
+                                       self.bh if hp is not None else None, self._a2c_bar)
+            return stats
+        assert boot is None, "the bootstrap value is fused only into a2c_head"
         _native.require().head_bwd(b.z, actions, logp_old, ent_coef, kl_coef, float(vf_coef), r["rew"], r["val"],
                                    r["dones"], int(r["L"]), int(r["mode"]), bool(r["norm_adv"]), float(r["gamma"]),
                                    float(r["lam"]), r["ret_w"], r["adv_w"], b.h, self.sWh, b.dh, self.gWh, self.gbh,

@@ -361,8 +361,17 @@ class ActorCriticTrainer:
             nxt.obs = st.obs[t + 1]
             eng.fc_planes(nxt)
         hp, S = eng.last_fc
-        ops.fc_value(hp, S, eng.bfc, eng.sWh, eng.bh, st.values[T], None)
         self._env_flips = T
+        if self._boot_in_head():
+            # V(s_T) is computed by the learner's head launch straight from these planes (no fc_value launch)
+            self._boot = (hp, S)
+            return
+        ops.fc_value(hp, S, eng.bfc, eng.sWh, eng.bh, st.values[T], None)
+
+    def _boot_in_head(self):
+        """The A2C head launch (``a2c_head``) also computes the bootstrap value V(s_T) from the last fc planes."""
+        st = self.storage
+        return (self._fused_returns() and self.engine.a2c_head and self.engine.head_ok(st.T * st.N, st.N))
 
     # ------------------------------------------------------------------ returns
     def _fused_returns(self):
@@ -690,7 +699,8 @@ class ActorCriticTrainer:
         head_done = eng.head_ok(T * N, N)
         if head_done:
             # loss + dz + the head's backward (dh, dWh, dbh, dbfc) in one launch
-            eng.head_backward(b, actions, logp_old, self.ent_coef, self.kl_coef, vf, self.stats_buf, rets)
+            boot, self._boot = getattr(self, "_boot", None), None
+            eng.head_backward(b, actions, logp_old, self.ent_coef, self.kl_coef, vf, self.stats_buf, rets, boot=boot)
         else:
             eng.loss(b, actions, logp_old, None, None, None, self.ent_coef, self.kl_coef, vf, 0.0, 0.0,
                      stats=self.stats_buf, returns=rets)

@@ -107,6 +107,10 @@ hipError_t aca_head_bwd(const float*, const int32_t*, const float*, const float*
                         const float*, const uint8_t*, int, int, int, int, int, float, float, float*, float*,
                         const uint16_t*, const uint16_t*, uint16_t*, float*, float*, float*, float*, int,
                         uint64_t*, hipStream_t);
+hipError_t aca_a2c_head(const float*, const int32_t*, const float*, const float*, const float*, float, const float*,
+                        float*, const uint8_t*, int, int, int, int, int, float, float, float*, float*,
+                        const uint16_t*, const uint16_t*, uint16_t*, float*, float*, float*, float*, int,
+                        const float*, int, int64_t, const float*, const float*, unsigned int*, uint64_t*, hipStream_t);
 hipError_t aca_cnn_trunk_bwd(const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*,
                              uint16_t*, uint16_t*, float*, int, uint64_t*, int, hipStream_t);
 hipError_t aca_cnn_trunk_rows(const uint8_t*, const uint16_t*, const float*, const uint16_t*, const float*,
@@ -1337,6 +1341,56 @@ void head_bwd(Tensor z, Tensor act, Tensor logp_old, Tensor ent_coef, Tensor kl_
         "head_bwd");
 }
 
+// A2C learner head v2 (loss.hip a2c_head_kernel): the bootstrap value V(s_T) from the rollout's last fc partial planes
+// (written into val[T]) + everything head_bwd does, in one launch of 32 narrow workgroups meeting at a bounded grid
+// barrier (bar: int32[3] zeros; bar[2] != 0 after a launch = the barrier timed out). hpart = None: val[T] is given.
+void a2c_head(Tensor z, Tensor act, Tensor logp_old, Tensor ent_coef, Tensor kl_coef, double vf_coef, Tensor rew,
+              Tensor val, Tensor dones, int64_t L, int64_t returns_mode, bool norm_adv, double gamma, double lam,
+              Tensor ret_w, Tensor adv_w, Tensor h, Tensor Wh, Tensor dh, Tensor gWh, Tensor gbh, Tensor gbfc,
+              Tensor stats, c10::optional<Tensor> hpart, int64_t planes, c10::optional<Tensor> bfc,
+              c10::optional<Tensor> bh, c10::optional<Tensor> bar, c10::optional<Tensor> stamps) {
+  TORCH_CHECK(rew.dim() == 2, "a2c_head: rewards must be [T, N]");
+  const int T = rew.size(0), N = rew.size(1), B = T * N;
+  TORCH_CHECK(z.dim() == 2 && z.size(0) >= B, "a2c_head: z must be [B, A + 1]");
+  const int A = z.size(1) - 1;
+  need(z, at::kFloat, "z");
+  need(act, at::kInt, "act");
+  for (auto* t : {&logp_old, &ent_coef, &kl_coef, &rew, &val, &ret_w, &adv_w, &gWh, &gbh, &gbfc, &stats})
+    need(*t, at::kFloat, "a2c_head fp32 operand");
+  need(dones, at::kByte, "dones");
+  for (auto* t : {&h, &Wh, &dh}) need(*t, at::kBFloat16, "a2c_head bf16 operand");
+  TORCH_CHECK(z.is_contiguous() && z.stride(0) == A + 1, "a2c_head: z must be contiguous [B, A + 1]");
+  TORCH_CHECK(act.numel() >= B && logp_old.numel() >= B && val.numel() == (int64_t)(T + 1) * N &&
+                  dones.numel() == B && ret_w.numel() >= B && adv_w.numel() >= B && h.numel() >= (int64_t)B * 512 &&
+                  dh.numel() >= (int64_t)B * 512 && Wh.numel() == 512 * (A + 1) && gWh.numel() == 512 * (A + 1) &&
+                  gbh.numel() == A + 1 && gbfc.numel() == 512 && stats.numel() >= 8,
+              "a2c_head: shape mismatch");
+  const float* hp = nullptr;
+  int64_t pstride = 0;
+  unsigned int* barp = nullptr;
+  if (hpart.has_value() && hpart->defined()) {
+    need(*hpart, at::kFloat, "hpart");
+    TORCH_CHECK(bfc.has_value() && bh.has_value() && bar.has_value(), "a2c_head: hpart needs bfc, bh and bar");
+    need(*bfc, at::kFloat, "bfc");
+    need(*bh, at::kFloat, "bh");
+    need(*bar, at::kInt, "bar");
+    pstride = hpart->numel() / 32;
+    TORCH_CHECK(hpart->numel() % 32 == 0 && pstride >= (int64_t)N * 512 && planes >= 1 && planes <= 32,
+                "a2c_head: hpart must hold 32 planes of [N, 512]");
+    TORCH_CHECK(bfc->numel() == 512 && bh->numel() == A + 1 && bar->numel() >= 3, "a2c_head: bad bootstrap operands");
+    hp = ptr<float>(*hpart);
+    barp = reinterpret_cast<unsigned int*>(bar->data_ptr<int32_t>());
+  }
+  check(aca_a2c_head(ptr<float>(z), ptr<int32_t>(act), ptr<float>(logp_old), ptr<float>(ent_coef),
+                     ptr<float>(kl_coef), (float)vf_coef, ptr<float>(rew), ptr<float>(val), ptr<uint8_t>(dones), T, N,
+                     (int)L, (int)returns_mode, norm_adv ? 1 : 0, (float)gamma, (float)lam, ptr<float>(ret_w),
+                     ptr<float>(adv_w), ptr<uint16_t>(h), ptr<uint16_t>(Wh), ptr<uint16_t>(dh), ptr<float>(gWh),
+                     ptr<float>(gbh), ptr<float>(gbfc), ptr<float>(stats), A, hp, (int)planes, pstride,
+                     hp ? ptr<float>(*bfc) : nullptr, hp ? ptr<float>(*bh) : nullptr, barp, stamps_ptr(stamps, 32),
+                     cur_stream(z)),
+        "a2c_head");
+}
+
 void im2col_u8(Tensor x, Tensor col, int64_t kh, int64_t kw, int64_t s, double scale) {
   need(x, at::kByte, "x");
   need(col, at::kBFloat16, "col");
@@ -1559,6 +1613,10 @@ TORCH_LIBRARY(acamd, m) {
         "Tensor val, Tensor dones, int L, int returns_mode, bool norm_adv, float gamma, float lam, Tensor ret_w, "
         "Tensor adv_w, Tensor h, Tensor Wh, Tensor dh, Tensor gWh, Tensor gbh, Tensor gbfc, Tensor stats, "
         "Tensor? stamps=None) -> ()");
+  m.def("a2c_head(Tensor z, Tensor act, Tensor logp_old, Tensor ent_coef, Tensor kl_coef, float vf_coef, Tensor rew, "
+        "Tensor val, Tensor dones, int L, int returns_mode, bool norm_adv, float gamma, float lam, Tensor ret_w, "
+        "Tensor adv_w, Tensor h, Tensor Wh, Tensor dh, Tensor gWh, Tensor gbh, Tensor gbfc, Tensor stats, "
+        "Tensor? hpart, int planes, Tensor? bfc, Tensor? bh, Tensor? bar, Tensor? stamps=None) -> ()");
   m.def("im2col_u8(Tensor x, Tensor col, int kh, int kw, int s, float scale) -> ()");
   m.def("im2col_nhwc(Tensor x, Tensor col, int B, int H, int W, int C, int kh, int kw, int s) -> ()");
   m.def("col2im_nhwc(Tensor dcol, Tensor ymask, Tensor dx, Tensor? colsum, int B, int H, int W, int C, int kh, "
@@ -1612,6 +1670,7 @@ TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
   m.impl("grad_finalize", &grad_finalize);
   m.impl("grad_finalize_opt", &grad_finalize_opt);
   m.impl("head_bwd", &head_bwd);
+  m.impl("a2c_head", &a2c_head);
   m.impl("im2col_u8", &im2col_u8);
   m.impl("im2col_nhwc", &im2col_nhwc);
   m.impl("col2im_nhwc", &col2im_nhwc);

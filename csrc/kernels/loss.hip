@@ -19,6 +19,7 @@
 // normalisation kernels of the generic path fold into this one launch. dbias (optional) receives the column sums of
 // dz = the gradient of the head bias, written directly (the gradient slab is clean).
 #include "common.h"
+#include "cnn_head.h"
 
 namespace aca {
 
@@ -578,6 +579,337 @@ __global__ void __launch_bounds__(HB_THREADS) head_bwd_kernel(HeadBwdArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------------------------------
+// A2C learner head v2: the bootstrap value V(s_T) + everything head_bwd_kernel does, in ONE launch of AH_WG narrow
+// workgroups (replaces fc_value_kernel + head_bwd_kernel: 2 launches, 8 wide workgroups on the critical path).
+//   phase 0: workgroup w, wave v computes V(s_T) of envs e = w + AH_WG (v + 4k) straight from the rollout's last fc
+//            partial planes (fc_h_from_parts: the same plane order and bf16 rounding as fc_value_kernel, so the values
+//            are bit-identical), stores them with agent-coherent (sc1) stores, and arrives at a grid barrier. Every
+//            operand that does not depend on V(s_T) (rewards, dones, values, logits, h columns, Wh) is requested
+//            before the wait.
+//   phase 1: returns / advantages of all B rows (each workgroup: identical code and order -> identical bits), the
+//            advantage moments (2 fp64 sums; workgroup 0 adds the EV-before sums), loss + dz (workgroup 0 alone
+//            reduces the loss statistics, writes ret/adv, stats and dbh).
+//   phase 2: the head backward for the workgroup's 16 hidden columns: thread t -> 4 columns (t & 3), rows
+//            (t >> 2) + 64 i; dh stored as bf16, dWh / dbfc partials reduced over lanes (xor tree) then waves (LDS),
+//            fixed order (deterministic, no atomics).
+// The grid barrier needs the AH_WG workgroups co-resident (32 of 256 CUs; nothing else runs in the captured
+// update); its spin is bounded and a timeout raises bar[2] instead of hanging. Cross-workgroup data (V(s_T)) moves
+// only through sc1 (agent-coherent) stores / loads ordered by s_waitcnt, so no L2 write-back / invalidate is needed.
+// ------------------------------------------------------------------------------------------------------------
+constexpr int AH_THREADS = 256;
+constexpr int AH_WG = 32;
+constexpr int AH_COLS = HB_H / AH_WG;        // 16 hidden columns per workgroup
+constexpr int AH_MAXB = 512;
+constexpr int AH_MAXN = 256;
+constexpr int AH_RPT = AH_MAXB / 64;         // row slots per thread in the head phase
+constexpr unsigned int AH_SPIN_LIMIT = 1u << 21;
+
+struct A2cHeadArgs {
+  HeadBwdArgs h;
+  const float* hpart; int S; int64_t plane_stride;   // last fc product (split-K planes) of s_T, or null: val holds V(s_T)
+  const float* bfc; const float* bh;
+  float* vboot;              // [N] = val + B (written in phase 0)
+  unsigned int* bar;         // [0] arrivals, [1] departures, [2] timeout flag
+};
+
+template <int AC>
+__global__ void __launch_bounds__(AH_THREADS) a2c_head_kernel(A2cHeadArgs args) {
+  constexpr int A1 = AC + 1;
+  const HeadBwdArgs& a = args.h;
+  __shared__ double sh[4 * 8];
+  __shared__ float s_dz[AH_MAXB * A1];
+  __shared__ float s_rew[AH_MAXB], s_val[AH_MAXB + AH_MAXN], s_ret[AH_MAXB], s_adv[AH_MAXB];
+  __shared__ uint8_t s_dn[AH_MAXB];
+  __shared__ float s_wh[AH_COLS * A1];
+  __shared__ float s_red[4 * AH_COLS * (A1 + 1)];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int B = a.B, N = a.N;
+  const bool lead = blockIdx.x == 0;
+  const int col0 = blockIdx.x * AH_COLS;
+  hb_stamp(a, 0);
+  // ---- phase 0: bootstrap values of this workgroup's envs
+  if (args.hpart) {
+    for (int e = blockIdx.x + AH_WG * wv; e < N; e += AH_WG * 4) {
+      float wvv[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) wvv[r] = bf2f(a.Wh[(lane * 8 + r) * A1 + AC]);
+      float hv[8];
+      fc_h_from_parts(args.hpart, args.S, args.plane_stride, args.bfc, e, lane, nullptr, hv);
+      float acc = 0.f;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) acc += hv[r] * wvv[r];
+      acc = wave_sum(acc);
+      if (lane == 0) __hip_atomic_store(&args.vboot[e], acc + args.bh[AC], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  // ---- operands independent of V(s_T), requested before the barrier wait
+  for (int i = tid; i < B; i += AH_THREADS) {
+    s_rew[i] = a.rew[i];
+    s_dn[i] = a.dn[i];
+    s_val[i] = a.val[i];
+  }
+  if (tid < AH_COLS * A1) s_wh[tid] = bf2f(a.Wh[col0 * A1 + tid]);   // columns col0.. are contiguous rows of Wh
+  float zr[2][A1];
+  int ab[2];
+  float lpo[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int rb = min(tid + k * AH_THREADS, B - 1);
+#pragma unroll
+    for (int j = 0; j < A1; ++j) zr[k][j] = a.z[(int64_t)rb * A1 + j];
+    ab[k] = a.act[rb];
+    lpo[k] = a.logp_old[rb];
+  }
+  const int cg = tid & 3, rl = tid >> 2;   // head phase: 4-column group, first row
+  const int jc0 = col0 + 4 * cg;
+  uint2 hv2[AH_RPT];
+#pragma unroll
+  for (int r = 0; r < AH_RPT; ++r) {
+    const int b = min(rl + 64 * r, B - 1);
+    hv2[r] = *reinterpret_cast<const uint2*>(a.h + (int64_t)b * HB_H + jc0);
+  }
+  const float c_ent = *a.ent_coef, beta = *a.kl_coef;
+  // ---- grid barrier (bootstrap values published)
+  if (args.hpart) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's sc1 value stores are acknowledged
+    __syncthreads();
+    if (tid == 0) {
+      __hip_atomic_fetch_add(&args.bar[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      unsigned int spins = 0;
+      int ok = 1;
+      while (__hip_atomic_load(&args.bar[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned int)AH_WG) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > AH_SPIN_LIMIT) { ok = 0; break; }
+      }
+      if (!ok) __hip_atomic_store(&args.bar[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    for (int i = tid; i < N; i += AH_THREADS)
+      s_val[B + i] = __hip_atomic_load(&args.vboot[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // departure: the last workgroup past the wait resets the barrier for the next launch (stream-ordered)
+    if (tid == 0) {
+      const unsigned int prev = __hip_atomic_fetch_add(&args.bar[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (prev == (unsigned int)AH_WG - 1u) {
+        __hip_atomic_store(&args.bar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&args.bar[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  } else {
+    for (int i = tid; i < N; i += AH_THREADS) s_val[B + i] = a.val[B + i];
+  }
+  __syncthreads();
+  hb_stamp(a, 1);
+  // ---- returns, advantage moments (+ EV-before sums on workgroup 0)
+  double s_r = 0, s_rr = 0, s_v = 0, s_vv = 0, s_rv = 0, s_a = 0, s_aa = 0;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int idx = tid + k * AH_THREADS;
+    if (idx < B) {
+      const int t = idx / N, n = idx - t * N;
+      float R;
+      if (a.returns_mode == 1) {
+        const int hh = min(t + a.L, a.T);
+        float acc = 0.f, disc = 1.f;
+        bool alive = true;
+        for (int q = t; q < hh; ++q) {
+          const int i = q * N + n;
+          acc += disc * s_rew[i];
+          disc *= a.gamma;
+          if (s_dn[i]) { alive = false; break; }
+        }
+        if (alive) acc += disc * s_val[hh * N + n];
+        R = acc;
+      } else {
+        float last = 0.f;
+        for (int q = a.T - 1; q >= t; --q) {
+          const int i = q * N + n;
+          const float nd = s_dn[i] ? 0.f : 1.f;
+          const float delta = s_rew[i] + a.gamma * s_val[i + N] * nd - s_val[i];
+          last = delta + a.gamma * a.lam * nd * last;
+        }
+        R = last + s_val[idx];
+      }
+      const float v = s_val[idx], A_ = R - v;
+      if (lead) {
+        a.ret_w[idx] = R;
+        a.adv_w[idx] = A_;
+      }
+      s_ret[idx] = R;
+      s_adv[idx] = A_;
+      s_r += R; s_rr += (double)R * R; s_v += v; s_vv += (double)v * v; s_rv += (double)R * v; s_a += A_;
+      s_aa += (double)A_ * A_;
+    }
+  }
+  const double nB = B;
+  float adv_mean = 0.f, adv_inv = 1.f;
+  if (lead) {
+    double red[7] = {s_a, s_aa, s_r, s_rr, s_v, s_vv, s_rv};
+    block_sum_multi<7>(red, sh);
+    if (tid == 0) {
+      const double mr = red[2] / nB, mv = red[4] / nB;
+      const double vr = fmax(red[3] / nB - mr * mr, 0.0), vv = fmax(red[5] / nB - mv * mv, 0.0);
+      a.stats[7] = (float)((red[6] / nB - mr * mv) / sqrt(vr * vv));
+    }
+    s_a = red[0];
+    s_aa = red[1];
+  } else {
+    double red[2] = {s_a, s_aa};   // the same per-value tree as the lead's: bit-identical moments
+    block_sum_multi<2>(red, sh);
+    s_a = red[0];
+    s_aa = red[1];
+  }
+  hb_stamp(a, 2);
+  if (a.norm_adv) {
+    const double m = s_a / nB, var = fmax(s_aa / nB - m * m, 0.0);
+    adv_mean = (float)m;
+    adv_inv = 1.0f / (1e-8f + (float)sqrt(var));
+  }
+  // ---- loss + dz
+  const float invB = 1.0f / (float)B;
+  double s_pg = 0, s_kl = 0, s_H = 0, s_vl = 0;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int idx = tid + k * AH_THREADS;
+    if (idx < B) {
+      const float adv = (s_adv[idx] - adv_mean) * adv_inv;
+      const float R = s_ret[idx];
+      float mx = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < AC; ++j) mx = fmaxf(mx, zr[k][j]);
+      float se = 0.f;
+#pragma unroll
+      for (int j = 0; j < AC; ++j) se += expf(zr[k][j] - mx);
+      const float lse = mx + logf(se);
+      float H = 0.f, lpa = 0.f;
+#pragma unroll
+      for (int j = 0; j < AC; ++j) {
+        const float lz = zr[k][j] - lse;
+        H -= expf(lz) * lz;
+        lpa = (j == ab[k]) ? lz : lpa;
+      }
+      s_pg += -(double)(adv * lpa);
+      const float dkl = lpo[k] - lpa;
+      s_kl += (double)(dkl * dkl);
+      s_H += H;
+      const float g_lpa = -adv * invB - 2.0f * beta * dkl * invB;
+#pragma unroll
+      for (int j = 0; j < AC; ++j) {
+        const float lz = zr[k][j] - lse, pj = expf(lz);
+        const float g = g_lpa * (((j == ab[k]) ? 1.0f : 0.0f) - pj) + c_ent * invB * pj * (lz + H);
+        s_dz[idx * A1 + j] = bf2f(f2bf(g));   // the bf16 rounding of the GEMM path's dz buffer
+      }
+      const float d = zr[k][AC] - R;
+      s_vl += (double)(d * d);
+      s_dz[idx * A1 + AC] = bf2f(f2bf(a.vf_coef * 2.0f * d * invB));
+    }
+  }
+  if (lead) {
+    double r4[4] = {s_pg, s_kl, s_H, s_vl};
+    block_sum_multi<4>(r4, sh);   // ends with a barrier: s_dz complete
+    if (tid == 0) {
+      const double inv = 1.0 / B;
+      a.stats[0] = (float)(r4[0] * inv);
+      a.stats[1] = (float)(r4[1] * inv);
+      a.stats[2] = (float)(r4[2] * inv);
+      a.stats[3] = (float)(r4[3] * inv);
+      a.stats[4] = 0.f;
+      a.stats[5] = (float)(r4[0] * inv + beta * r4[1] * inv - c_ent * r4[2] * inv);
+      a.stats[6] = 1.f;
+    }
+  } else {
+    __syncthreads();   // s_dz complete
+  }
+  hb_stamp(a, 3);
+  // ---- head backward: 4 columns x rows rl + 64 i
+  float wj[4][A1];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int q = 0; q < A1; ++q) wj[c][q] = s_wh[(4 * cg + c) * A1 + q];
+  float dwp[4][A1], dbf[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    dbf[c] = 0.f;
+#pragma unroll
+    for (int q = 0; q < A1; ++q) dwp[c][q] = 0.f;
+  }
+#pragma unroll
+  for (int r = 0; r < AH_RPT; ++r) {
+    const int b = rl + 64 * r;
+    if (b < B) {
+      float dzb[A1];
+#pragma unroll
+      for (int q = 0; q < A1; ++q) dzb[q] = s_dz[b * A1 + q];
+      const uint32_t hw[2] = {hv2[r].x, hv2[r].y};
+      uint32_t out[2];
+#pragma unroll
+      for (int c2 = 0; c2 < 2; ++c2) {
+        uint32_t packed = 0;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int c = 2 * c2 + e;
+          const float hf = __uint_as_float(e ? (hw[c2] & 0xFFFF0000u) : (hw[c2] << 16));
+          float sacc = 0.f;
+#pragma unroll
+          for (int q = 0; q < A1; ++q) {
+            sacc += dzb[q] * wj[c][q];
+            dwp[c][q] += hf * dzb[q];
+          }
+          const float d = hf > 0.f ? sacc : 0.f;
+          dbf[c] += d;
+          packed |= (uint32_t)f2bf(d) << (16 * e);
+        }
+        out[c2] = packed;
+      }
+      *reinterpret_cast<uint2*>(a.dh + (int64_t)b * HB_H + jc0) = make_uint2(out[0], out[1]);
+    }
+  }
+  // lanes sharing a column group (lane & 3) -> xor over lane bits 2..5, fixed order
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+#pragma unroll
+    for (int o = 4; o < 64; o <<= 1) {
+      dbf[c] += __shfl_xor(dbf[c], o, 64);
+#pragma unroll
+      for (int q = 0; q < A1; ++q) dwp[c][q] += __shfl_xor(dwp[c][q], o, 64);
+    }
+  }
+  hb_stamp(a, 4);
+  if (lane < 4) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      float* dstw = s_red + (wv * AH_COLS + 4 * lane + c) * (A1 + 1);
+#pragma unroll
+      for (int q = 0; q < A1; ++q) dstw[q] = dwp[c][q];
+      dstw[A1] = dbf[c];
+    }
+  }
+  __syncthreads();
+  if (tid < AH_COLS * (A1 + 1)) {   // (column, value) pairs: the 4 waves in wave order
+    const int cl = tid / (A1 + 1), q = tid - cl * (A1 + 1);
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) v += s_red[(w * AH_COLS + cl) * (A1 + 1) + q];
+    if (q < A1) a.gWh[(col0 + cl) * A1 + q] = v;
+    else a.gbfc[col0 + cl] = v;
+  }
+  if (lead) {   // head-bias gradient: column q of dz, rows strided over a wave, xor tree (fixed order)
+    for (int q = wv; q < A1; q += 4) {
+      float sb = 0.f;
+      for (int bb = lane; bb < B; bb += 64) sb += s_dz[bb * A1 + q];
+      sb = wave_sum(sb);
+      if (lane == 0) a.gbh[q] = sb;
+    }
+  }
+  if (a.stamps) {
+    hb_stamp(a, 5);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    hb_stamp(a, 6);
+  }
+}
+
 }  // namespace aca
 
 extern "C" hipError_t aca_head_bwd(const float* z, const int32_t* act, const float* logp_old, const float* ent_coef,
@@ -596,6 +928,32 @@ extern "C" hipError_t aca_head_bwd(const float* z, const int32_t* act, const flo
   case n: aca::head_bwd_kernel<n><<<aca::HB_WG, aca::HB_THREADS, 0, stream>>>(a); break;
     ACA_HB_CASE(2) ACA_HB_CASE(3) ACA_HB_CASE(4) ACA_HB_CASE(5) ACA_HB_CASE(6) ACA_HB_CASE(7)
 #undef ACA_HB_CASE
+  }
+  return hipGetLastError();
+}
+
+extern "C" hipError_t aca_a2c_head(const float* z, const int32_t* act, const float* logp_old, const float* ent_coef,
+                                   const float* kl_coef, float vf_coef, const float* rew, float* val,
+                                   const uint8_t* dn, int T, int N, int L, int returns_mode, int norm_adv, float gamma,
+                                   float lam, float* ret_w, float* adv_w, const uint16_t* h, const uint16_t* Wh,
+                                   uint16_t* dh, float* gWh, float* gbh, float* gbfc, float* stats, int A,
+                                   const float* hpart, int S, int64_t plane_stride, const float* bfc, const float* bh,
+                                   unsigned int* bar, uint64_t* stamps, hipStream_t stream) {
+  const int B = T * N;
+  if (B < 1 || B > aca::AH_MAXB || N > aca::AH_MAXN || A < 2 || A > 7 || (returns_mode != 1 && returns_mode != 2))
+    return hipErrorInvalidValue;
+  if (hpart && (S < 1 || S > aca::FC_MAX_PLANES || !bfc || !bh || !bar || reinterpret_cast<uintptr_t>(hpart) % 16 ||
+                reinterpret_cast<uintptr_t>(bfc) % 16 || plane_stride % 4))
+    return hipErrorInvalidValue;
+  aca::A2cHeadArgs a;
+  a.h = aca::HeadBwdArgs{z, act, logp_old, ent_coef, kl_coef, vf_coef, rew, val, dn, T, N, L, returns_mode, norm_adv,
+                         gamma, lam, ret_w, adv_w, h, Wh, dh, gWh, gbh, gbfc, stats, B, stamps};
+  a.hpart = hpart; a.S = S; a.plane_stride = plane_stride; a.bfc = bfc; a.bh = bh; a.vboot = val + B; a.bar = bar;
+  switch (A) {
+#define ACA_AH_CASE(n) \
+  case n: aca::a2c_head_kernel<n><<<aca::AH_WG, aca::AH_THREADS, 0, stream>>>(a); break;
+    ACA_AH_CASE(2) ACA_AH_CASE(3) ACA_AH_CASE(4) ACA_AH_CASE(5) ACA_AH_CASE(6) ACA_AH_CASE(7)
+#undef ACA_AH_CASE
   }
   return hipGetLastError();
 }

@@ -211,3 +211,88 @@ def test_trunk_fwd_persistent_equals_per_env_kernel(cuda):
     for k in range(3):
         ref = torch.cat([p[k] for p in parts])
         assert torch.equal(big[k], ref), k
+
+
+@pytest.mark.parametrize("T,N,mode,norm_adv", [(5, 32, 1, False), (5, 32, 2, True), (5, 64, 1, True),
+                                               (16, 24, 2, False)])
+def test_a2c_head_equals_fc_value_plus_head_bwd(cuda, T, N, mode, norm_adv):
+    """a2c_head (bootstrap value from the fc partial planes + returns + loss + head backward, ONE launch of 32
+    workgroups meeting at a grid barrier) == fc_value + head_bwd (round 2's two launches): V(s_T), dh, dz-derived
+    statistics, targets / advantages and dbh bit-identical for B <= 256 (same per-element arithmetic and reduction
+    trees; above, a thread holds two rows and the fp64 moments may round differently), dWh /
+    dbfc equal up to the summation order over rows; the barrier words are back to zero after every launch."""
+    from actor_critic_algs_on_tensorflow_amd import _native
+    ops = _native.require()
+    A, A1, B, S = 6, 7, T * N, 13
+    g = torch.Generator(device="cpu").manual_seed(T * 100 + N)
+    z = torch.randn(B, A1, generator=g).to(cuda)
+    act = torch.randint(0, A, (B,), dtype=torch.int32, generator=g).to(cuda)
+    lpo = (-torch.rand(B, generator=g) * 2).to(cuda)
+    rew = torch.randn(T, N, generator=g).to(cuda)
+    dones = (torch.rand(T, N, generator=g) < 0.1).to(torch.uint8).to(cuda)
+    h = torch.relu(torch.randn(B, 512, generator=g)).to(torch.bfloat16).to(cuda)
+    Wh = (0.05 * torch.randn(512, A1, generator=g)).to(torch.bfloat16).to(cuda)
+    hpart = (0.1 * torch.randn(32, N, 512, generator=g)).to(cuda)
+    bfc = (0.1 * torch.randn(512, generator=g)).to(cuda)
+    bh = torch.randn(A1, generator=g).to(cuda)
+    ent, kl = torch.tensor([0.01], device=cuda), torch.tensor([0.3], device=cuda)
+    val0 = torch.randn(T + 1, N, generator=g).to(cuda)
+
+    def outs():
+        return dict(ret=torch.zeros(B, device=cuda), adv=torch.zeros(B, device=cuda),
+                    dh=torch.zeros(B, 512, dtype=torch.bfloat16, device=cuda), gWh=torch.zeros(512 * A1, device=cuda),
+                    gbh=torch.zeros(A1, device=cuda), gbfc=torch.zeros(512, device=cuda),
+                    stats=torch.zeros(8, device=cuda))
+
+    ref, new = outs(), outs()
+    vref = val0.clone()
+    ops.fc_value(hpart, S, bfc, Wh, bh, vref[T], None)
+    ops.head_bwd(z, act, lpo, ent, kl, 0.5, rew, vref, dones, 5, mode, norm_adv, 0.99, 0.95, ref["ret"], ref["adv"],
+                 h, Wh, ref["dh"], ref["gWh"], ref["gbh"], ref["gbfc"], ref["stats"])
+    bar = torch.zeros(4, dtype=torch.int32, device=cuda)
+    for rep in range(3):   # repeated launches: the barrier resets itself
+        vnew = val0.clone()
+        vnew[T] = float("nan")
+        ops.a2c_head(z, act, lpo, ent, kl, 0.5, rew, vnew, dones, 5, mode, norm_adv, 0.99, 0.95, new["ret"],
+                     new["adv"], h, Wh, new["dh"], new["gWh"], new["gbh"], new["gbfc"], new["stats"], hpart, S, bfc, bh,
+                     bar)
+        torch.cuda.synchronize()
+        assert bar.tolist() == [0, 0, 0, 0], bar
+        assert torch.equal(vnew, vref)
+        for k in ("ret", "adv", "dh", "gbh", "stats"):
+            if B <= 256 or k in ("ret", "adv"):   # one row per thread in both kernels: identical fp64 moment trees
+                assert torch.equal(new[k], ref[k]), (k, new[k], ref[k])
+            else:
+                torch.testing.assert_close(new[k].float(), ref[k].float(), rtol=1e-2, atol=1e-5)
+        torch.testing.assert_close(new["gWh"], ref["gWh"], rtol=1e-5, atol=1e-7)
+        torch.testing.assert_close(new["gbfc"], ref["gbfc"], rtol=1e-5, atol=1e-7)
+    # without planes the kernel reads V(s_T) from val (no barrier)
+    new2 = outs()
+    ops.a2c_head(z, act, lpo, ent, kl, 0.5, rew, vref, dones, 5, mode, norm_adv, 0.99, 0.95, new2["ret"], new2["adv"],
+                 h, Wh, new2["dh"], new2["gWh"], new2["gbh"], new2["gbfc"], new2["stats"], None, 0, None, None, None)
+    for k in ("ret", "adv", "dh", "gbh", "stats", "gWh", "gbfc"):
+        assert torch.equal(new2[k], new[k]), k
+
+
+def test_a2c_update_with_fused_bootstrap_head_matches_round2_head(cuda, monkeypatch):
+    """Native Pong A2C, 3 graph-captured updates: the a2c_head path (no fc_value launch) tracks the round-2
+    fc_value + head_bwd path (same statistics; parameters equal up to the dWh / dbfc summation order)."""
+    from actor_critic_algs_on_tensorflow_amd import preset
+    from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
+    res = {}
+    for knob in ("1", "0"):
+        monkeypatch.setenv("ACA_A2C_HEAD", knob)
+        cfg = preset("pong_a2c", num_envs=32, device="cuda:0", outdir=None, quiet=True, stdout_freq=0, save_every=0)
+        tr = ActorCriticTrainer(cfg)
+        assert tr.engine.a2c_head == (knob == "1")
+        tr.capture(warmup=1)
+        p0 = tr.flat.data.clone()
+        for _ in range(3):
+            tr.step()
+        torch.cuda.synchronize()
+        assert (getattr(tr, "_boot", None) is None)
+        res[knob] = (tr.flat.data - p0, tr.stats_buf.clone(), tr.storage.values.clone())
+    d1, s1, v1 = res["1"]
+    d0, s0, v0 = res["0"]
+    assert torch.allclose(s0[:8], s1[:8], rtol=1e-3, atol=1e-5), (s0[:8], s1[:8])
+    assert (d0 - d1).norm() / d0.norm() < 1e-2, float((d0 - d1).norm() / d0.norm())

@@ -150,6 +150,14 @@ class CNNEngine:
         self.fc_max_planes = min(FC_PLANES, int(os.environ.get("ACA_FC_MAX_PLANES", "32")))
         self._hpart = {}
         self.last_fc = None
+        # fc fold (cnn_fused.hip FcFold, opt-in): the rollout's fc product computed inside the row-split trunk launch
+        # as 7 partial planes by 16 helper workgroups per conv3 row (no fc GEMM launch per rollout step); 16 or 32
+        # envs. The fused step reads one plane buffer and writes the other (ping-pong). Measured SLOWER on the
+        # headline (0.206 vs 0.193 ms per update, profiles/r3_bench_fc_fold_ab.txt): the in-launch hand-off chain
+        # (publish, fan-in wait, cross-XCD payload reads) costs ~7.5 us per launch against the 5 us GEMM it removes.
+        self.fc_fold = os.environ.get("ACA_FC_FOLD", "0") == "1"
+        self._hpart2 = {}
+        self._fold_cnt = None
         self.model = model
         self.flat = flat
         self.shadow = shadow
@@ -206,6 +214,31 @@ class CNNEngine:
                workspace=self.ws)
         return out
 
+    FOLD_PLANES = 7
+
+    def fold_ok(self, B):
+        """The row-split trunk of ``B`` observations can also compute their fc product (the launch's 7 B workgroups
+        must be co-resident: 16 or 32 envs; the launcher re-checks the occupancy and refuses otherwise)."""
+        return (self.fc_fold and self.implicit and self.fc_parts and B in (16, 32) and self.trunk_mode in (1, 2)
+                and B <= min(self.trunk_rows_max_b, self.fused_trunk_max_b))
+
+    def fold_args(self, B, parity=0):
+        """(Wfc shadow, plane buffer ``parity``, counters) for a folded trunk launch; sets :attr:`last_fc`."""
+        if self._fold_cnt is None:
+            self._fold_cnt = torch.zeros(16, dtype=torch.int32, device=self.dev)
+        if parity:
+            if B not in self._hpart2:
+                self._hpart2[B] = torch.zeros(FC_PLANES * B * 512, dtype=torch.float32, device=self.dev)
+            hp = self._hpart2[B]
+        else:
+            hp = self.hpart(B)
+        self.last_fc = (hp, self.FOLD_PLANES)
+        return self.sWfc, hp, self._fold_cnt
+
+    def fold_timed_out(self):
+        """True if a folded launch's helpers ever gave up waiting (counter word 15; the planes are then wrong)."""
+        return self._fold_cnt is not None and int(self._fold_cnt[15]) != 0
+
     def fused_step_ok(self, B):
         """The rollout step can run as ONE launch of policy/env + the next observation's row-split trunk."""
         return (self.implicit and self.fc_parts and self.trunk_shift and self.trunk_mode in (1, 2)
@@ -231,9 +264,13 @@ class CNNEngine:
         if self.implicit and B <= self.fused_trunk_max_b:
             if not self.trunk_shift:
                 shift_out = None
+            fold = self.fold_args(B) if (fc_parts and not head and self.fold_ok(B)) else None
             G.cnn_trunk_fwd(obs, self.sW1, self.b1, self.sW2, self.b2, self.sW3, self.b3, b.y1, b.y2, b.y3,
-                            shift_out=shift_out, mode=self.trunk_mode if B <= self.trunk_rows_max_b else self.trunk_mode_large)
+                            shift_out=shift_out, mode=self.trunk_mode if B <= self.trunk_rows_max_b else self.trunk_mode_large,
+                            fold=fold)
             shifted = shift_out is not None
+            if fold is not None:   # the fc product is already in the planes (last_fc set by fold_args)
+                return shifted if want_shift else b.z
         elif self.implicit:
             G.gemm(obs, 0, True, self.sW1, 256, True, b.y1, 32, 1, B * 400, 32, 256, bias=self.b1, relu=True,
                    workspace=ws, ga=[1, B, 4, 84, 84, 8, 8, 4], ga_scale=1.0 / 255.0)

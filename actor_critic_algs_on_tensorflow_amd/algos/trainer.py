@@ -351,15 +351,18 @@ class ActorCriticTrainer:
             cur = rows(t)
             nxt = rows(t + 1) if t + 1 < T else b
             sn, tn, tgn, ern = env.next_state()
+            # fc fold: this launch also computes obs_{t+1}'s fc planes, into the other plane buffer
+            fold = eng.fold_args(N, (t + 1) % 2) if eng.fold_ok(N) else (None, None, None)
             ops.pong_fused_step(cur.h, eng.sWh, eng.bh, cur.z, st.actions[t], st.logp[t], st.entropy[t],
                                 st.values[t], KEY_ENV_BITS, self.policy_seed, env.state, env.t, env.tg, env.ep_ret,
                                 sn, tn, tgn, ern, env.ep_stats, env.env_ids, st.obs[t], st.obs[t + 1],
                                 st.rewards[t], st.dones[t], st.truncated[t], env.seed, env.max_episode_steps, hp, S,
                                 eng.bfc, eng.sW1, eng.b1, eng.sW2, eng.b2, eng.sW3, eng.b3, nxt.y1, nxt.y2, nxt.y3,
-                                1.0 / 255.0, st.obs[t + 2] if t + 2 <= T else None)
+                                1.0 / 255.0, st.obs[t + 2] if t + 2 <= T else None, None, *fold)
             env.flip()
             nxt.obs = st.obs[t + 1]
-            eng.fc_planes(nxt)
+            if fold[0] is None:
+                eng.fc_planes(nxt)
         hp, S = eng.last_fc
         self._env_flips = T
         if self._boot_in_head():
@@ -622,13 +625,29 @@ class ActorCriticTrainer:
             self.lr_ctrl.update_(self.actor_opt.lr, kl)
 
     # ------------------------------------------------------------------ learning (native MLP engine)
+    def _mlp_fused_opt(self):
+        """Opt-in (ACA_MLP_FUSED_OPT=1): Adam folded into the MLP weight-gradient launch (one launch per minibatch
+        instead of two) on a single device with the reference's actor / critic Adam pair. Measured SLOWER on the
+        MuJoCo-shape PPO update (16.3 vs 14.1 ms, profiles/r3_mujoco_fused_adam_ab.txt): the in-launch grid barrier
+        over ~360 workgroups costs more than the kernel boundary and the optimiser launch it removes."""
+        if self.dp is not None or self._grad_sink is not None or self._defer_allreduce:
+            return None
+        if not hasattr(self, "_mfo"):
+            self._mfo = None
+            if os.environ.get("ACA_MLP_FUSED_OPT", "0") == "1" and list(self.opts) == ["actor", "critic"]:
+                self._mfo = self.mlp.fused_adam_words(self.opts["actor"], self.opts["critic"])
+        return self._mfo
+
     def _mlp_step(self, eng, B, idx, obs, actions, logp_old, adv, ret, v_old, perm=None, bump=None):
         cfg = self.cfg
         ppo = cfg.algo == "ppo"
+        fo = self._mlp_fused_opt()
         used = eng.train(obs, actions, logp_old, adv, ret, self.ent_coef, self.kl_coef, B, idx=idx, perm=perm, bump=bump,
                          v_old=v_old if ppo else None, vf_coef=1.0, ppo=ppo, ppo_clip=cfg.ppo_clip if ppo else 0.0,
                          v_clip=(cfg.ppo_value_clip or 0.0) if ppo else 0.0, stats=self.stats_buf,
-                         clips=(cfg.clip_value, cfg.critic_clip_value), want_parts=self.dp is None)
+                         clips=(cfg.clip_value, cfg.critic_clip_value), want_parts=self.dp is None, fused_opt=fo)
+        if fo is not None:
+            return   # the weight-gradient launch applied both Adam steps and wrote the transposed shadows
         for t, g in enumerate(("actor", "critic")):
             self.opts[g].ext_parts = eng.parts[t] if used else None
         self._apply_grads()

@@ -50,7 +50,7 @@ hipError_t aca_pong_fused_step(uint16_t*, const float*, int, int64_t, const floa
                                float*, float*, int32_t*, int64_t*, float*, float*, const int64_t*, const uint8_t*,
                                uint8_t*, float*, uint8_t*, uint8_t*, uint32_t, int, const uint16_t*, const float*,
                                const uint16_t*, const float*, const uint16_t*, const float*, uint16_t*, uint16_t*,
-                               uint16_t*, float, uint8_t*, uint64_t*, int, hipStream_t);
+                               uint16_t*, float, uint8_t*, uint64_t*, int, const uint16_t*, float*, unsigned int*, hipStream_t);
 hipError_t aca_categorical_sample(const float*, int, int, int, const int64_t*, const int64_t*, const int64_t*, int,
                                   uint32_t, int32_t*, float*, float*, float*, hipStream_t);
 hipError_t aca_ev(const float*, const float*, float*, int, hipStream_t);
@@ -115,7 +115,7 @@ hipError_t aca_cnn_trunk_bwd(const uint16_t*, const uint16_t*, const uint16_t*, 
                              uint16_t*, uint16_t*, float*, int, uint64_t*, int, hipStream_t);
 hipError_t aca_cnn_trunk_rows(const uint8_t*, const uint16_t*, const float*, const uint16_t*, const float*,
                               const uint16_t*, const float*, uint16_t*, uint16_t*, uint16_t*, int, float, uint8_t*,
-                              uint8_t*, uint64_t*, int, hipStream_t);
+                              uint8_t*, uint64_t*, int, const uint16_t*, float*, unsigned int*, hipStream_t);
 }
 
 namespace {
@@ -298,6 +298,30 @@ void env_policy_step_pong(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, 
         "env_policy_step_pong");
 }
 
+// fc fold operands (cnn_fused.hip FcFold): bf16 Wfc [3136, 512], fp32 planes >= 7 x [N, 512], int32 counters [16]
+struct FoldPtrs {
+  const uint16_t* w = nullptr;
+  float* planes = nullptr;
+  unsigned int* cnt = nullptr;
+};
+FoldPtrs fold_ptrs(const c10::optional<Tensor>& w, const c10::optional<Tensor>& planes,
+                   const c10::optional<Tensor>& cnt, int64_t N, const char* what) {
+  FoldPtrs f;
+  if (!(cnt.has_value() && cnt->defined())) return f;
+  TORCH_CHECK(w.has_value() && w->defined() && planes.has_value() && planes->defined(), what,
+              ": the fc fold needs fold_w, fold_planes and fold_cnt");
+  need(*w, at::kBFloat16, "fold_w");
+  need(*planes, at::kFloat, "fold_planes");
+  need(*cnt, at::kInt, "fold_cnt");
+  TORCH_CHECK(w->numel() == 3136 * 512 && planes->numel() >= 7 * N * 512 && cnt->numel() >= 16 &&
+                  reinterpret_cast<uintptr_t>(w->data_ptr()) % 16 == 0,
+              what, ": fold shapes (Wfc [3136, 512], planes >= 7 x [N, 512], 16 counter words)");
+  f.w = ptr<uint16_t>(*w);
+  f.planes = ptr<float>(*planes);
+  f.cnt = reinterpret_cast<unsigned int*>(cnt->data_ptr<int32_t>());
+  return f;
+}
+
 // Rollout step t of the Pong bank fused with the row-split trunk of the observation it produces (cnn_fused.hip
 // pong_fused_step_kernel): env state read from (state, t, tg, ep_ret), committed to the other parity buffers
 // (state_n, t_n, tg_n, ep_ret_n); prev = obs[t], out = obs[t+1] (frames 0..2 already shifted in), shift_out =
@@ -308,7 +332,8 @@ void pong_fused_step(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, Tenso
                      Tensor prev, Tensor out, Tensor reward, Tensor done, Tensor trunc, int64_t seed,
                      int64_t max_steps, Tensor hpart, int64_t planes, Tensor bfc, Tensor W1, Tensor b1, Tensor W2,
                      Tensor b2, Tensor W3, Tensor b3, Tensor y1, Tensor y2, Tensor y3, double scale,
-                     c10::optional<Tensor> shift_out, c10::optional<Tensor> stamps) {
+                     c10::optional<Tensor> shift_out, c10::optional<Tensor> stamps, c10::optional<Tensor> fold_w,
+                     c10::optional<Tensor> fold_planes, c10::optional<Tensor> fold_cnt) {
   check_env(state, t, tg, ep_ret, ep_stats, ids, reward, done, trunc);
   check_env(state_n, t_n, tg_n, ep_ret_n, ep_stats, ids, reward, done, trunc);
   for (auto* x : {&h, &Wh, &W1, &W2, &W3, &y1, &y2, &y3}) need(*x, at::kBFloat16, "pong_fused_step bf16");
@@ -344,6 +369,7 @@ void pong_fused_step(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, Tenso
                     shift_out->data_ptr() != out.data_ptr(), "pong_fused_step: shift_out shape / aliasing");
     so = shift_out->data_ptr<uint8_t>();
   }
+  const FoldPtrs ff = fold_ptrs(fold_w, fold_planes, fold_cnt, N, "pong_fused_step");
   check(aca_pong_fused_step(ptr<uint16_t>(h), ptr<float>(hpart), (int)planes, pstride, ptr<float>(bfc),
                             ptr<uint16_t>(Wh), ptr<float>(bh), A, ptr<float>(z), ptr<int32_t>(act), ptr<float>(logp),
                             ptr<float>(ent), ptr<float>(value), (int)key_shift, (uint32_t)pseed, ptr<float>(state),
@@ -353,7 +379,7 @@ void pong_fused_step(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, Tenso
                             ptr<uint8_t>(done), ptr<uint8_t>(trunc), (uint32_t)seed, (int)max_steps,
                             ptr<uint16_t>(W1), ptr<float>(b1), ptr<uint16_t>(W2), ptr<float>(b2), ptr<uint16_t>(W3),
                             ptr<float>(b3), ptr<uint16_t>(y1), ptr<uint16_t>(y2), ptr<uint16_t>(y3), (float)scale,
-                            so, stamps_ptr(stamps, N * 7), N, cur_stream(state)),
+                            so, stamps_ptr(stamps, N * 7), N, ff.w, ff.planes, ff.cnt, cur_stream(state)),
         "pong_fused_step");
 }
 
@@ -809,9 +835,36 @@ void mlp_wgrad(Tensor desc, int64_t ntw, int64_t B, int64_t nsplit, int64_t item
                c10::optional<Tensor> parts0, c10::optional<Tensor> parts1, double clip0, double clip1,
                c10::optional<Tensor> g_log_std, int64_t A, c10::optional<Tensor> mstats, c10::optional<Tensor> stats,
                c10::optional<Tensor> ent_coef, c10::optional<Tensor> kl_coef, c10::optional<Tensor> mpart,
-               int64_t mpart_rows, c10::optional<Tensor> bump) {
+               int64_t mpart_rows, c10::optional<Tensor> bump, c10::optional<Tensor> opt_words,
+               c10::optional<Tensor> opt_floats) {
   need(desc, at::kLong, "desc");
   aca::WgradArgs a{};
+  if (opt_words.has_value() && opt_words->defined()) {
+    // Adam folded into the launch (mlp.hip mlp_wgrad_adam_kernel): host int64 [14] = p0, m, v, lr, t, gnorm (per
+    // tower), log_std, barrier words; host float [5] = max_norm (per tower), b1, b2, eps
+    TORCH_CHECK(opt_floats.has_value() && opt_floats->defined(), "mlp_wgrad: opt_words needs opt_floats");
+    const Tensor w = opt_words->to(at::kCPU).contiguous(), f = opt_floats->to(at::kCPU).contiguous();
+    TORCH_CHECK(w.scalar_type() == at::kLong && w.numel() == 14 && f.scalar_type() == at::kFloat && f.numel() == 5,
+                "mlp_wgrad: opt_words int64[14], opt_floats float[5]");
+    const int64_t* wp = w.data_ptr<int64_t>();
+    const float* fp = f.data_ptr<float>();
+    aca::WgradOpt& o = a.opt;
+    for (int q = 0; q < 2; ++q) {
+      o.p0[q] = reinterpret_cast<float*>(wp[0 + q]);
+      o.m[q] = reinterpret_cast<float*>(wp[2 + q]);
+      o.v[q] = reinterpret_cast<float*>(wp[4 + q]);
+      o.lr[q] = reinterpret_cast<const float*>(wp[6 + q]);
+      o.t[q] = reinterpret_cast<float*>(wp[8 + q]);
+      o.gnorm[q] = reinterpret_cast<float*>(wp[10 + q]);
+      o.max_norm[q] = fp[q];
+    }
+    o.log_std = reinterpret_cast<float*>(wp[12]);
+    o.bar = reinterpret_cast<unsigned int*>(wp[13]);
+    o.b1 = fp[2];
+    o.b2 = fp[3];
+    o.eps = fp[4];
+    a.fuse = 1;
+  }
   if (bump.has_value() && bump->defined()) {
     need(*bump, at::kLong, "bump");
     a.bump = bump->data_ptr<int64_t>();
@@ -1192,7 +1245,8 @@ int64_t gemm_effective_splits(int64_t K, int64_t bk, int64_t splits) {
 // also copy the whole observation there (rollover of the last observation into slot 0 of the next rollout).
 void cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, Tensor y1,
                    Tensor y2, Tensor y3, double scale, c10::optional<Tensor> shift_out,
-                   c10::optional<Tensor> stamps, int64_t mode, c10::optional<Tensor> copy_out) {
+                   c10::optional<Tensor> stamps, int64_t mode, c10::optional<Tensor> copy_out,
+                   c10::optional<Tensor> fold_w, c10::optional<Tensor> fold_planes, c10::optional<Tensor> fold_cnt) {
   need(obs, at::kByte, "obs");
   for (auto* w : {&W1, &W2, &W3, &y1, &y2, &y3}) need(*w, at::kBFloat16, "trunk bf16 operand");
   for (auto* b : {&b1, &b2, &b3}) need(*b, at::kFloat, "trunk bias");
@@ -1222,11 +1276,13 @@ void cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tenso
                 "cnn_trunk_fwd: copy_out must be a distinct, aligned [B, 4, 84, 84] uint8 buffer");
     co = ptr<uint8_t>(*copy_out);
   }
+  const FoldPtrs ff = fold_ptrs(fold_w, fold_planes, fold_cnt, B, "cnn_trunk_fwd");
+  TORCH_CHECK(!ff.cnt || mode == 1 || mode == 2, "cnn_trunk_fwd: the fc fold needs a row-split mode");
   if (mode == 1 || mode == 2) {   // 2: the row kernel with its conv2/conv3 weight loads issued after conv1
     check(aca_cnn_trunk_rows(ptr<uint8_t>(obs), ptr<uint16_t>(W1), ptr<float>(b1), ptr<uint16_t>(W2),
                              ptr<float>(b2), ptr<uint16_t>(W3), ptr<float>(b3), ptr<uint16_t>(y1), ptr<uint16_t>(y2),
                              ptr<uint16_t>(y3), (int)B, (float)scale, so, co, stamps_ptr(stamps, B * 7),
-                             mode == 2 ? 1 : 0, cur_stream(obs)),
+                             mode == 2 ? 1 : 0, ff.w, ff.planes, ff.cnt, cur_stream(obs)),
           "cnn_trunk_rows");
     return;
   }
@@ -1541,7 +1597,8 @@ TORCH_LIBRARY(acamd, m) {
         "Tensor t_n, Tensor tg_n, Tensor ep_ret_n, Tensor ep_stats, Tensor env_ids, Tensor prev, Tensor out, "
         "Tensor reward, Tensor done, Tensor truncated, int seed, int max_steps, Tensor hpart, int planes, "
         "Tensor bfc, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, Tensor y1, Tensor y2, "
-        "Tensor y3, float scale, Tensor? shift_out=None, Tensor? stamps=None) -> ()");
+        "Tensor y3, float scale, Tensor? shift_out=None, Tensor? stamps=None, Tensor? fold_w=None, "
+        "Tensor? fold_planes=None, Tensor? fold_cnt=None) -> ()");
   m.def("categorical_sample(Tensor logits, Tensor keys, int seed, Tensor act, Tensor logp, Tensor ent) -> ()");
   m.def("categorical_sample_env(Tensor logits, Tensor tg, Tensor env_ids, int key_shift, int seed, Tensor act, "
         "Tensor logp, Tensor ent, Tensor? vout) -> ()");
@@ -1588,7 +1645,8 @@ TORCH_LIBRARY(acamd, m) {
         "float v_clip, bool ppo, Tensor? g_log_std, Tensor? mstats, Tensor? mpart=None, Tensor? stamps=None) -> ()");
   m.def("mlp_wgrad(Tensor desc, int ntw, int B, int nsplit, int items0, int items1, Tensor? parts0, "
         "Tensor? parts1, float clip0, float clip1, Tensor? g_log_std, int A, Tensor? mstats, Tensor? stats, "
-        "Tensor? ent_coef, Tensor? kl_coef, Tensor? mpart=None, int mpart_rows=0, Tensor? bump=None) -> ()");
+        "Tensor? ent_coef, Tensor? kl_coef, Tensor? mpart=None, int mpart_rows=0, Tensor? bump=None, "
+        "Tensor? opt_words=None, Tensor? opt_floats=None) -> ()");
   m.def("mlp_rollout(Tensor desc, int lds, Tensor obs, Tensor act, Tensor logp, Tensor ent, Tensor reward, "
         "Tensor done, Tensor truncated, Tensor log_std, Tensor ac_scale, int key_shift, int policy_seed, "
         "Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, Tensor env_ids, Tensor lin_A, "
@@ -1602,7 +1660,7 @@ TORCH_LIBRARY(acamd, m) {
   m.def("gemm_effective_splits(int K, int bk, int splits) -> int", &gemm_effective_splits);
   m.def("cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, Tensor y1, "
         "Tensor y2, Tensor y3, float scale, Tensor? shift_out=None, Tensor? stamps=None, int mode=0, "
-        "Tensor? copy_out=None) -> ()");
+        "Tensor? copy_out=None, Tensor? fold_w=None, Tensor? fold_planes=None, Tensor? fold_cnt=None) -> ()");
   m.def("cnn_trunk_bwd(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tensor dy2, Tensor dy1, "
         "Tensor biasp, Tensor? stamps=None, int persist=0) -> ()");
   m.def("grad_finalize(Tensor jobs, Tensor partial) -> ()");

@@ -532,6 +532,106 @@ constexpr int TR_IN_ELEMS = 768 * 16;   // 4 x 36 x 84 = 12096 bf16, padded to 3
 
 __device__ __forceinline__ int tr_y1_own_begin(int r) { return (20 * r + 6) / 7; }
 
+// ------------------------------------------------------------------------------------------------------------
+// fc fold: the rollout's fc product (y3 [N, 3136] x Wfc [3136, 512]) inside the row-split trunk launch, as 7 partial
+// planes (plane r = conv3 row r's 448 features x the matching 448 rows of Wfc). Every row workgroup (e, r) publishes
+// its conv3 row with agent-coherent (sc1) stores and arrives at the row's counter; workgroups e < FF_HELPERS of each
+// row are the row's helpers: once all N envs have arrived (bounded spin; a timeout raises cnt[15] instead of hanging)
+// helper e multiplies the N envs' row r [N x 448] (sc1 loads: other XCDs' L2s hold them dirty otherwise) by the
+// 448 x 32 Wfc slice of columns 32e .. 32e+31 -- staged into LDS by the LDS-DMA path at launch entry, so it lands
+// while conv1 runs -- with 16x16x32 bf16 MFMA and stores its [N x 32] block of plane r. Consumers sum the 7 planes
+// in plane order (FcParts, S = 7). Replaces the fc GEMM launch of every rollout step. Needs every workgroup of the
+// launch co-resident (7 N <= 224 with one workgroup per CU; the launcher checks the occupancy) and N in {16, 32}.
+// Counter words: [r] arrivals of row r, [8 + r] departures of its helpers (the last one zeroes both), [15] timeout.
+// ------------------------------------------------------------------------------------------------------------
+constexpr int FF_HELPERS = 16;                 // helper workgroups per conv3 row
+constexpr int FF_COLS = 512 / FF_HELPERS;      // 32 fc columns per helper
+constexpr int FF_K = 7 * 64;                   // 448 features per conv3 row
+constexpr unsigned int FF_SPIN_LIMIT = 1u << 21;
+
+struct FcFold {
+  const u16* Wfc;        // [3136][512] bf16 (K x N, row-major)
+  float* planes;         // plane r at planes + r * N * 512: [N][512] fp32
+  unsigned int* cnt;     // [16] counter words (zero between launches); null: no fold
+  int N;
+};
+
+// Wfc rows [448 r, 448 r + 448) x columns [32 e, 32 e + 32) -> s_wfc [448][32] bf16, 28 wave copies of 16 rows
+// (lane i -> row 16 blk + i / 4, 16-byte chunk i % 4): no registers, tracked by the vm counter
+__device__ __forceinline__ void ff_stage_w(const FcFold& ff, int e, int r, u16* s_wfc) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int blk = wid; blk < FF_K / 16; blk += T_THREADS / 64) {
+    const int row = blk * 16 + (lane >> 2), ch = lane & 3;
+    const u16* src = ff.Wfc + (size_t)(r * FF_K + row) * 512 + e * FF_COLS + ch * 8;
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint4*>(src),
+                                     (__attribute__((address_space(3))) void*)(s_wfc + blk * 16 * FF_COLS), 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ uint4 ld_b128_sc1(const void* p) {   // agent-coherent 16-byte load (caller waits vmcnt)
+  uint4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+
+__device__ __forceinline__ bf16x8 ff_tr_frag(const u16* rows, int ld, int col0, int lane) {
+  // B fragment (k = 8 (lane >> 4) + 0..7, n = col0 + lane & 15) from n-contiguous rows via two transposing reads
+  const int lr16 = lane & 15, lg = lane >> 4, q = lr16 >> 2, p = lr16 & 3;
+  typedef short short4f __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) short4f lds4f;
+  const short4f lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4f*)(rows + (lg * 8 + q) * ld + col0 + 4 * p));
+  const short4f hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4f*)(rows + (lg * 8 + 4 + q) * ld + col0 + 4 * p));
+  const short8v v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// After workgroup (e, r) published its conv3 row (sc1 stores issued): arrive; helpers wait for the row and multiply.
+__device__ void ff_arrive_and_help(const FcFold& ff, int e, int r, const u16* __restrict__ s_wfc,
+                                   const u16* __restrict__ y3g) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's row stores acknowledged, its W slice copies landed
+  __syncthreads();
+  if (tid == 0) __hip_atomic_fetch_add(&ff.cnt[r], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (e >= FF_HELPERS) return;
+  if (tid == 0) {
+    unsigned int spins = 0;
+    while (__hip_atomic_load(&ff.cnt[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned int)ff.N) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > FF_SPIN_LIMIT) {
+        __hip_atomic_store(&ff.cnt[15], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  const int mtiles = ff.N >> 4;
+  if (wid < 2 * mtiles) {   // wave -> (env tile mt, column tile nt) of the helper's [N x 32] block
+    const int mt = wid % mtiles, nt = wid / mtiles;
+    const int l16 = lane & 15, lg = lane >> 4;
+    const u16* arow = y3g + ((size_t)(16 * mt + l16) * Y3_ROWS + r * 7) * Y3_C + lg * 8;
+    uint4 af[FF_K / 32];
+#pragma unroll
+    for (int ks = 0; ks < FF_K / 32; ++ks) af[ks] = ld_b128_sc1(arow + ks * 32);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < FF_K / 32; ++ks)
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[ks]),
+                                                    ff_tr_frag(s_wfc + ks * 32 * FF_COLS, FF_COLS, nt * 16, lane),
+                                                    acc, 0, 0, 0);
+    float* dst = ff.planes + (size_t)r * ff.N * 512 + (size_t)(16 * mt + 4 * lg) * 512 + e * FF_COLS + nt * 16 + l16;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dst[(size_t)i * 512] = acc[i];
+  }
+  if (tid == 0) {   // departure: the row's last helper zeroes its counters for the next launch (stream-ordered)
+    const unsigned int prev = __hip_atomic_fetch_add(&ff.cnt[8 + r], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == (unsigned int)FF_HELPERS - 1u) {
+      __hip_atomic_store(&ff.cnt[r], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&ff.cnt[8 + r], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // conv1 -> conv3 of row workgroup (e, r) from its staged input rows (s_in: 4 frames x 36 rows of bf16 pixel values,
 // complete) and the conv1 weights (s_w1, complete); stores the owned y1 / y2 rows and its y3 row. Shared by the
 // trunk kernel and the fused policy/env + trunk kernel.
@@ -557,7 +657,8 @@ __device__ __forceinline__ void trunk_rows_compute(const u16* __restrict__ s_in,
                                                    const u16* __restrict__ W3, u16* __restrict__ y1g,
                                                    u16* __restrict__ y2g, u16* __restrict__ y3g, float scale,
                                                    uint64_t* __restrict__ stamps, bf16x8 (&bw2)[16],
-                                                   bf16x8 (&bw3)[18]) {
+                                                   bf16x8 (&bw3)[18], const FcFold& ff, u16* __restrict__ s_y3,
+                                                   const u16* __restrict__ s_wfc) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l16 = lane & 15, lg = lane >> 4;
   const int n2 = wid * 16 + l16;
@@ -660,7 +761,11 @@ __device__ __forceinline__ void trunk_rows_compute(const u16* __restrict__ s_in,
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int row = lg * 4 + q;
-      if (row < 7) y3g[((size_t)e * Y3_ROWS + r * 7 + row) * Y3_C + n] = f2bf(fmaxf(acc[q] + bias, 0.f));
+      const u16 v = f2bf(fmaxf(acc[q] + bias, 0.f));
+      if (row < 7) {
+        if (ff.cnt) s_y3[row * Y3_C + n] = v;   // published below as whole words with sc1 stores
+        else y3g[((size_t)e * Y3_ROWS + r * 7 + row) * Y3_C + n] = v;
+      }
     }
   }
   // ---------------------------------------------------------------- owned y1 / y2 rows: LDS -> global, 16-byte rows
@@ -679,6 +784,13 @@ __device__ __forceinline__ void trunk_rows_compute(const u16* __restrict__ s_in,
           *reinterpret_cast<const uint4*>(s_y2 + lp * Y2_LD + q);
     }
   }
+  if (ff.cnt) {
+    __syncthreads();   // s_y3 complete
+    if (tid < FF_K / 2)
+      __hip_atomic_store(reinterpret_cast<uint32_t*>(y3g + ((size_t)e * Y3_ROWS + r * 7) * Y3_C) + tid,
+                         reinterpret_cast<const uint32_t*>(s_y3)[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ff_arrive_and_help(ff, e, r, s_wfc, y3g);
+  }
   if (stamps) {
     stamp(stamps, 4);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -692,11 +804,14 @@ __global__ void __launch_bounds__(T_THREADS) cnn_trunk_rows_kernel(
     const uint8_t* __restrict__ obs, const u16* __restrict__ W1, const float* __restrict__ b1,
     const u16* __restrict__ W2, const float* __restrict__ b2, const u16* __restrict__ W3,
     const float* __restrict__ b3, u16* __restrict__ y1g, u16* __restrict__ y2g, u16* __restrict__ y3g,
-    float scale, uint8_t* __restrict__ shift_out, uint8_t* __restrict__ copy_out, uint64_t* __restrict__ stamps) {
+    float scale, uint8_t* __restrict__ shift_out, uint8_t* __restrict__ copy_out, uint64_t* __restrict__ stamps,
+    FcFold ff) {
   __shared__ __attribute__((aligned(16))) u16 s_in[TR_IN_ELEMS];
   __shared__ __attribute__((aligned(16))) u16 s_w1[32 * W1_LD];
   __shared__ __attribute__((aligned(16))) u16 s_y1[TR_C1_POS * Y1_LD];
   __shared__ __attribute__((aligned(16))) u16 s_y2[TR_C2_POS * Y2_LD];
+  __shared__ __attribute__((aligned(16))) u16 s_y3[7 * Y3_C];
+  __shared__ __attribute__((aligned(16))) u16 s_wfc[FF_K * FF_COLS];
 
   const int r = blockIdx.x % TR_ROWS, e = blockIdx.x / TR_ROWS;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -727,6 +842,7 @@ __global__ void __launch_bounds__(T_THREADS) cnn_trunk_rows_kernel(
   uint4 vw[W1_PER];
 #pragma unroll
   for (int u = 0; u < W1_PER; ++u) vw[u] = reinterpret_cast<const uint4*>(W1)[tid + u * T_THREADS];
+  if (ff.cnt && e < FF_HELPERS) ff_stage_w(ff, e, r, s_wfc);   // behind the staging loads in the vm queue
   {
     uint4* dst = reinterpret_cast<uint4*>(s_in);
 #pragma unroll
@@ -762,7 +878,7 @@ __global__ void __launch_bounds__(T_THREADS) cnn_trunk_rows_kernel(
   stamp(stamps, 1);
   bf16x8 bw2[16], bw3[18];
   trunk_rows_compute<LATE_W ? 1 : 0>(s_in, s_w1, s_y1, s_y2, e, r, bias1a, bias1b, bias2, bias3, W2, W3, y1g, y2g,
-                                     y3g, scale, stamps, bw2, bw3);
+                                     y3g, scale, stamps, bw2, bw3, ff, s_y3, s_wfc);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -809,12 +925,14 @@ __global__ void __launch_bounds__(T_THREADS) pong_fused_step_kernel(
     float* __restrict__ ent, float* __restrict__ vout, int key_shift, uint32_t pseed, const u16* __restrict__ W1,
     const float* __restrict__ b1, const u16* __restrict__ W2, const float* __restrict__ b2,
     const u16* __restrict__ W3, const float* __restrict__ b3, u16* __restrict__ y1g, u16* __restrict__ y2g,
-    u16* __restrict__ y3g, float scale, uint8_t* __restrict__ shift_out, uint64_t* __restrict__ stamps) {
+    u16* __restrict__ y3g, float scale, uint8_t* __restrict__ shift_out, uint64_t* __restrict__ stamps, FcFold ff) {
   constexpr int A = A1 - 1;
   __shared__ __attribute__((aligned(16))) u16 s_in[TR_IN_ELEMS];
   __shared__ __attribute__((aligned(16))) u16 s_w1[32 * W1_LD];
   __shared__ __attribute__((aligned(16))) u16 s_y1[TR_C1_POS * Y1_LD];
   __shared__ __attribute__((aligned(16))) u16 s_y2[TR_C2_POS * Y2_LD];
+  __shared__ __attribute__((aligned(16))) u16 s_y3[7 * Y3_C];
+  __shared__ __attribute__((aligned(16))) u16 s_wfc[FF_K * FF_COLS];
   __shared__ float s_acc[4][A1];
   __shared__ PongOut cand[3];
   __shared__ int sh_act;
@@ -853,6 +971,7 @@ __global__ void __launch_bounds__(T_THREADS) pong_fused_step_kernel(
   // wait for (the vm counter retires in issue order), so they arrive while the head, env and render run
   bf16x8 bw2[16], bw3[18];
   if constexpr (EARLY_W) trunk_w23_load(W2, W3, bw2, bw3);
+  if (ff.cnt && e < FF_HELPERS) ff_stage_w(ff, e, r, s_wfc);   // lands while the head, env and conv1 run
   // ---------------------------------------------------------------- policy head (every row workgroup of env e)
   float hf[2];
   fc_h2_from_parts(fc.hpart, fc.S, fc.plane_stride, fc.bfc, e, tid, lead ? h : nullptr, hf);
@@ -968,7 +1087,7 @@ __global__ void __launch_bounds__(T_THREADS) pong_fused_step_kernel(
   __syncthreads();
   stamp(stamps, 1);
   trunk_rows_compute<EARLY_W ? 2 : 1>(s_in, s_w1, s_y1, s_y2, e, r, bias1a, bias1b, bias2, bias3, W2, W3, y1g, y2g,
-                                      y3g, scale, stamps, bw2, bw3);
+                                      y3g, scale, stamps, bw2, bw3, ff, s_y3, s_wfc);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -1573,17 +1692,37 @@ extern "C" hipError_t aca_cnn_trunk_fwd(const uint8_t* obs, const uint16_t* W1, 
   return hipGetLastError();
 }
 
+namespace aca {
+// The fold's helpers spin on their row's arrivals: every workgroup of the launch must be resident at once. N in
+// {16, 32} and (occupancy per CU) x (CUs) >= 7 N, evaluated once per kernel.
+inline bool ff_coresident(const void* kernel, int N) {
+  if (N != 16 && N != 32) return false;
+  int dev = 0, cus = 0, per = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, T_THREADS, 0) != hipSuccess)
+    return false;
+  return (int64_t)per * cus >= (int64_t)N * TR_ROWS;
+}
+}  // namespace aca
+
 extern "C" hipError_t aca_cnn_trunk_rows(const uint8_t* obs, const uint16_t* W1, const float* b1, const uint16_t* W2,
                                          const float* b2, const uint16_t* W3, const float* b3, uint16_t* y1,
                                          uint16_t* y2, uint16_t* y3, int B, float scale, uint8_t* shift_out,
-                                         uint8_t* copy_out, uint64_t* stamps, int late_w, hipStream_t stream) {
+                                         uint8_t* copy_out, uint64_t* stamps, int late_w, const uint16_t* ff_w,
+                                         float* ff_planes, unsigned int* ff_cnt, hipStream_t stream) {
   if (B <= 0) return hipSuccess;
+  aca::FcFold ff{ff_w, ff_planes, ff_cnt, B};
+  if (ff_cnt) {
+    const void* k = late_w ? (const void*)aca::cnn_trunk_rows_kernel<true> : (const void*)aca::cnn_trunk_rows_kernel<false>;
+    if (!ff_w || !ff_planes || !aca::ff_coresident(k, B)) return hipErrorInvalidValue;
+  }
   if (late_w)
     aca::cnn_trunk_rows_kernel<true><<<B * aca::TR_ROWS, aca::T_THREADS, 0, stream>>>(
-        obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale, shift_out, copy_out, stamps);
+        obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale, shift_out, copy_out, stamps, ff);
   else
     aca::cnn_trunk_rows_kernel<false><<<B * aca::TR_ROWS, aca::T_THREADS, 0, stream>>>(
-        obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale, shift_out, copy_out, stamps);
+        obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale, shift_out, copy_out, stamps, ff);
   return hipGetLastError();
 }
 
@@ -1609,8 +1748,10 @@ extern "C" hipError_t aca_pong_fused_step(
     int64_t* tg_n, float* ep_ret_n, float* ep_stats, const int64_t* ids, const uint8_t* prev, uint8_t* out,
     float* reward, uint8_t* done, uint8_t* trunc, uint32_t seed, int max_steps, const uint16_t* W1, const float* b1,
     const uint16_t* W2, const float* b2, const uint16_t* W3, const float* b3, uint16_t* y1, uint16_t* y2,
-    uint16_t* y3, float scale, uint8_t* shift_out, uint64_t* stamps, int N, hipStream_t stream) {
+    uint16_t* y3, float scale, uint8_t* shift_out, uint64_t* stamps, int N, const uint16_t* ff_w, float* ff_planes,
+    unsigned int* ff_cnt, hipStream_t stream) {
   if (N <= 0) return hipSuccess;
+  aca::FcFold ff{ff_w, ff_planes, ff_cnt, N};
   aca::PongIO io;
   io.state = state; io.tsteps = t; io.tglob = tg; io.ep_ret = ep_ret; io.ep_stats = ep_stats; io.env_ids = ids;
   io.prev = prev; io.out = out; io.reward = reward; io.done_out = done; io.trunc_out = trunc; io.seed = seed;
@@ -1623,17 +1764,28 @@ extern "C" hipError_t aca_pong_fused_step(
     const char* v = getenv("ACA_FUSED_EARLY_W");
     return v && v[0] == '1';
   }();
+  if (ff_cnt) {
+    const void* k = nullptr;
+    switch (A + 1) {
+#define ACA_FUSED_K(A1) \
+  case A1: k = early ? (const void*)aca::pong_fused_step_kernel<A1, true> : (const void*)aca::pong_fused_step_kernel<A1, false>; break;
+      ACA_FUSED_K(3) ACA_FUSED_K(4) ACA_FUSED_K(5) ACA_FUSED_K(6) ACA_FUSED_K(7)
+#undef ACA_FUSED_K
+      default: return hipErrorInvalidValue;
+    }
+    if (!ff_w || !ff_planes || ff_planes == hpart || !aca::ff_coresident(k, N)) return hipErrorInvalidValue;
+  }
   switch (A + 1) {
 #define ACA_FUSED_CASE(A1)                                                                                       \
   case A1:                                                                                                       \
     if (early)                                                                                                   \
       aca::pong_fused_step_kernel<A1, true><<<grid, aca::T_THREADS, 0, stream>>>(                                \
           io, nx, fc, h, Wh, bh, z, act, logp, ent, value, key_shift, pseed, W1, b1, W2, b2, W3, b3, y1, y2, y3,  \
-          scale, shift_out, stamps);                                                                             \
+          scale, shift_out, stamps, ff);                                                                         \
     else                                                                                                         \
       aca::pong_fused_step_kernel<A1, false><<<grid, aca::T_THREADS, 0, stream>>>(                               \
           io, nx, fc, h, Wh, bh, z, act, logp, ent, value, key_shift, pseed, W1, b1, W2, b2, W3, b3, y1, y2, y3,  \
-          scale, shift_out, stamps);                                                                             \
+          scale, shift_out, stamps, ff);                                                                         \
     break;
     ACA_FUSED_CASE(3) ACA_FUSED_CASE(4) ACA_FUSED_CASE(5) ACA_FUSED_CASE(6) ACA_FUSED_CASE(7)
 #undef ACA_FUSED_CASE

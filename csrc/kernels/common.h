@@ -119,6 +119,14 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 }
 
 // Block-wide sum for blockDim.x <= 1024; `sh` must hold >= 16 floats. Result valid in every thread.
+// global-norm clip factor min(1, max_norm / (||g|| + 1e-6)) (TF clip_by_global_norm form; <= 0: no clip). Shared by
+// the optimisers (optim.hip) and the MLP weight-gradient launch with Adam folded in (mlp.hip).
+__device__ __forceinline__ float grad_scale(float gnorm_sq, float max_norm) {
+  if (max_norm <= 0.f) return 1.f;
+  const float n = sqrtf(gnorm_sq);
+  return fminf(max_norm / (n + 1e-6f), 1.0f);
+}
+
 __device__ __forceinline__ float block_sum(float v, float* sh) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
   v = wave_sum(v);

@@ -588,8 +588,8 @@ __global__ void __launch_bounds__(HB_THREADS) head_bwd_kernel(HeadBwdArgs a) {
 //            operand that does not depend on V(s_T) (rewards, dones, values, logits, h columns, Wh) is requested
 //            before the wait.
 //   phase 1: returns / advantages of all B rows (each workgroup: identical code and order -> identical bits), the
-//            advantage moments (2 fp64 sums; workgroup 0 adds the EV-before sums), loss + dz (workgroup 0 alone
-//            reduces the loss statistics, writes ret/adv, stats and dbh).
+//            advantage moments (2 fp64 sums), loss + dz. Side duties, one per workgroup so that no workgroup carries
+//            them all: 0 writes ret / adv, 1 the EV-before sums (stats[7]), 2 the loss statistics, 3 dbh.
 //   phase 2: the head backward for the workgroup's 16 hidden columns: thread t -> 4 columns (t & 3), rows
 //            (t >> 2) + 64 i; dh stored as bf16, dWh / dbfc partials reduced over lanes (xor tree) then waves (LDS),
 //            fixed order (deterministic, no atomics).
@@ -625,7 +625,9 @@ __global__ void __launch_bounds__(AH_THREADS) a2c_head_kernel(A2cHeadArgs args) 
   __shared__ float s_red[4 * AH_COLS * (A1 + 1)];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int B = a.B, N = a.N;
-  const bool lead = blockIdx.x == 0;
+  // side duties spread over workgroups 0..3 (one extra reduction each instead of all on one straggler):
+  // 0 targets / advantages out, 1 EV-before, 2 loss statistics, 3 head-bias gradient
+  const bool lead = blockIdx.x == 0, ev_wg = blockIdx.x == 1, st_wg = blockIdx.x == 2, bh_wg = blockIdx.x == 3;
   const int col0 = blockIdx.x * AH_COLS;
   hb_stamp(a, 0);
   // ---- phase 0: bootstrap values of this workgroup's envs
@@ -744,7 +746,7 @@ __global__ void __launch_bounds__(AH_THREADS) a2c_head_kernel(A2cHeadArgs args) 
   }
   const double nB = B;
   float adv_mean = 0.f, adv_inv = 1.f;
-  if (lead) {
+  if (ev_wg) {
     double red[7] = {s_a, s_aa, s_r, s_rr, s_v, s_vv, s_rv};
     block_sum_multi<7>(red, sh);
     if (tid == 0) {
@@ -805,7 +807,7 @@ __global__ void __launch_bounds__(AH_THREADS) a2c_head_kernel(A2cHeadArgs args) 
       s_dz[idx * A1 + AC] = bf2f(f2bf(a.vf_coef * 2.0f * d * invB));
     }
   }
-  if (lead) {
+  if (st_wg) {
     double r4[4] = {s_pg, s_kl, s_H, s_vl};
     block_sum_multi<4>(r4, sh);   // ends with a barrier: s_dz complete
     if (tid == 0) {
@@ -895,7 +897,7 @@ __global__ void __launch_bounds__(AH_THREADS) a2c_head_kernel(A2cHeadArgs args) 
     if (q < A1) a.gWh[(col0 + cl) * A1 + q] = v;
     else a.gbfc[col0 + cl] = v;
   }
-  if (lead) {   // head-bias gradient: column q of dz, rows strided over a wave, xor tree (fixed order)
+  if (bh_wg) {   // head-bias gradient: column q of dz, rows strided over a wave, xor tree (fixed order)
     for (int q = wv; q < A1; q += 4) {
       float sb = 0.f;
       for (int bb = lane; bb < B; bb += 64) sb += s_dz[bb * A1 + q];

@@ -54,11 +54,6 @@ __device__ __forceinline__ float partial_total(const float* __restrict__ parts, 
   return block_sum(v, sh);
 }
 
-__device__ __forceinline__ float grad_scale(float gnorm_sq, float max_norm) {
-  if (max_norm <= 0.f) return 1.f;
-  const float n = sqrtf(gnorm_sq);
-  return fminf(max_norm / (n + 1e-6f), 1.0f);
-}
 
 // One optimiser segment (a parameter group of the flat slab) with its own lr / step / clip / norm settings.
 // Optional transposed fp32 shadows of [K][N] weight matrices inside the segment (the MLP engine's forward reads

@@ -296,3 +296,110 @@ def test_a2c_update_with_fused_bootstrap_head_matches_round2_head(cuda, monkeypa
     d0, s0, v0 = res["0"]
     assert torch.allclose(s0[:8], s1[:8], rtol=1e-3, atol=1e-5), (s0[:8], s1[:8])
     assert (d0 - d1).norm() / d0.norm() < 1e-2, float((d0 - d1).norm() / d0.norm())
+
+
+@pytest.mark.parametrize("N", [16, 32])
+def test_fc_fold_planes_match_fp32_product(cuda, N):
+    """fc fold (cnn_fused.hip FcFold): the row-split trunk launch also computes the fc product as 7 partial planes
+    (plane r = conv3 row r of every env x the matching 448 rows of Wfc, 16 helper workgroups per row meeting the row's
+    other workgroups at a counter). y1 / y2 / y3 stay bit-identical to the unfolded launch, every plane matches the
+    fp32 product of the same bf16 operands, repeated launches give identical planes (no races), and the counter words
+    are back to zero with no helper timeout."""
+    from actor_critic_algs_on_tensorflow_amd import _native
+    ops = _native.require()
+    g = torch.Generator(device="cpu").manual_seed(N)
+    obs = torch.randint(0, 256, (N, 4, 84, 84), dtype=torch.uint8, generator=g).to(cuda)
+    W1 = (0.05 * torch.randn(32, 256, generator=g)).to(torch.bfloat16).to(cuda)
+    W2 = (0.05 * torch.randn(64, 512, generator=g)).to(torch.bfloat16).to(cuda)
+    W3 = (0.05 * torch.randn(64, 576, generator=g)).to(torch.bfloat16).to(cuda)
+    b1, b2, b3 = [(0.1 * torch.randn(n, generator=g)).to(cuda) for n in (32, 64, 64)]
+    Wfc = (0.02 * torch.randn(3136, 512, generator=g)).to(torch.bfloat16).to(cuda)
+
+    def acts():
+        return (torch.zeros(N * 400 * 32, dtype=torch.bfloat16, device=cuda),
+                torch.zeros(N * 81 * 64, dtype=torch.bfloat16, device=cuda),
+                torch.zeros(N * 49 * 64, dtype=torch.bfloat16, device=cuda))
+
+    ref = acts()
+    ops.cnn_trunk_fwd(obs, W1, b1, W2, b2, W3, b3, *ref, 1.0 / 255.0, None, None, 2, None)
+    cnt = torch.zeros(16, dtype=torch.int32, device=cuda)
+    planes = torch.full((32 * N * 512,), float("nan"), device=cuda)
+    got = acts()
+    first = None
+    for rep in range(5):
+        ops.cnn_trunk_fwd(obs, W1, b1, W2, b2, W3, b3, *got, 1.0 / 255.0, None, None, 2, None, Wfc, planes, cnt)
+        torch.cuda.synchronize()
+        assert cnt.tolist() == [0] * 16, cnt
+        for x, y in zip(got, ref):
+            assert torch.equal(x, y)
+        p = planes[:7 * N * 512].view(7, N, 512).clone()
+        if first is None:
+            first = p
+        assert torch.equal(p, first), rep
+    y3 = ref[2].float().view(N, 7, 448)
+    for r in range(7):
+        want = y3[:, r] @ Wfc[r * 448:(r + 1) * 448].float()
+        torch.testing.assert_close(first[r], want, rtol=1e-4, atol=1e-4)
+    h = first.sum(0)
+    torch.testing.assert_close(h, ref[2].float().view(N, 3136) @ Wfc.float(), rtol=1e-4, atol=1e-3)
+
+
+def test_a2c_with_fc_fold_tracks_gemm_fc(cuda, monkeypatch):
+    """Native Pong A2C (32 envs, graph-captured): the folded fc product (no fc GEMM launches) tracks the split-K GEMM
+    path over 3 updates (same loss statistics within rounding; the plane sums differ in order only), and the helpers
+    never timed out."""
+    from actor_critic_algs_on_tensorflow_amd import preset
+    from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
+    res = {}
+    for knob in ("1", "0"):
+        monkeypatch.setenv("ACA_FC_FOLD", knob)
+        cfg = preset("pong_a2c", num_envs=32, device="cuda:0", outdir=None, quiet=True, stdout_freq=0, save_every=0)
+        tr = ActorCriticTrainer(cfg)
+        assert tr.engine.fold_ok(32) == (knob == "1")
+        tr.capture(warmup=1)
+        p0 = tr.flat.data.clone()
+        tr.step()
+        torch.cuda.synchronize()
+        assert not tr.engine.fold_timed_out()
+        res[knob] = (tr.flat.data - p0, tr.stats_buf.clone())
+    (d1, s1), (d0, s0) = res["1"], res["0"]
+    # losses / entropy / ratio agree to rounding; EV-before (stats[7]) of a random-init critic is ~1e-3 noise
+    assert torch.allclose(s0[:7], s1[:7], rtol=1e-2, atol=1e-3), (s0[:8], s1[:8])
+    assert (d0 - d1).norm() / d0.norm() < 5e-2, float((d0 - d1).norm() / d0.norm())
+
+
+@pytest.mark.parametrize("name,kw", [("mujoco_ppo_dp8", dict(num_envs=16, n_steps=64, ppo_epochs=2, ppo_minibatches=4)),
+                                     ("cartpole_cpu", dict(num_envs=64, n_steps=5, device="cuda:0", cuda_graph=True))])
+def test_mlp_wgrad_with_fused_adam_is_bitwise_the_two_launch_update(cuda, name, kw, monkeypatch):
+    """MLP engine: Adam folded into the weight-gradient launch (mlp_wgrad_adam_kernel: grid barrier on the sum-of-
+    squares slots, each tile workgroup updating its own tile + transposed shadow) == weight-gradient launch +
+    opt_multi: Adam step counts and the untouched gradient slab exactly, parameters / moments / global norms / the
+    transposed shadows to float rounding (same operation order; the compiler's fp contraction differs between the two
+    kernels), over several graph-replayed updates (PPO with the Gaussian head and log-std, A2C with the categorical
+    head). Each path alone is bitwise deterministic (test_ppo_graph_replay_bitwise_equals_eager)."""
+    from actor_critic_algs_on_tensorflow_amd import preset
+    from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
+    runs = []
+    for knob in ("1", "0"):
+        monkeypatch.setenv("ACA_MLP_FUSED_OPT", knob)
+        base = dict(outdir=None, quiet=True, stdout_freq=0, save_every=0, seed=4)
+        base.update(kw)
+        tr = ActorCriticTrainer(preset(name, **base))
+        assert tr.mlp is not None
+        tr.capture(warmup=1)
+        assert (tr._mlp_fused_opt() is not None) == (knob == "1")
+        for _ in range(3):
+            tr.step()
+        torch.cuda.synchronize()
+        if knob == "1":
+            assert not tr.mlp.fused_opt_timed_out()
+        o = tr.opts
+        runs.append([tr.flat.data.clone(), tr.flat.grad.clone()] +
+                    [x.clone() for g in ("actor", "critic") for x in (o[g].m, o[g].v, o[g].t, o[g].gnorm)] +
+                    [tr.mlp.wt[id(lay)].clone() for tw in tr.mlp.towers for lay in tw])
+    exact = {1, 4, 8}   # gradient slab, actor / critic step counts
+    for j, (x, y) in enumerate(zip(*runs)):
+        if j in exact:
+            assert torch.equal(x, y), j
+        else:
+            torch.testing.assert_close(x, y, rtol=2e-4, atol=1e-6, msg=lambda m: f"item {j}: {m}")

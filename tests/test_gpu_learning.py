@@ -3,8 +3,8 @@ its training curve, Basic_AC/run_AC.py:277-280 / Basic_AC/util.py:64-106).
 
 * native Pong A2C (bf16 CNN engine, the headline config, graph-captured): the fraction of points won rises from
   the random policy's level by a fixed margin within a bounded number of updates;
-* CartPole on the fused MLP engine and on the torch/autograd engine: both reach the same solved level;
-* MuJoCo-shape PPO on the MLP engine improves its episode return;
+* CartPole on the fused MLP engine and on the torch/autograd engine: both reach the 500-step cap and stay there;
+* MuJoCo-shape PPO on the MLP engine learns and holds >= 0.9 of its peak over the last third of 300 updates;
 * engine-vs-autograd gradients at the production batch sizes (B = 160 A2C learner, B = 4096 PPO minibatch) with
   the autotuned GEMM plans.
 Thresholds come from measured curves (scripts/learn_curve.py on an MI355X; profiles/r2_learning_curves.txt)."""
@@ -49,16 +49,18 @@ def test_native_pong_a2c_learns(cuda):
 
 
 def test_cartpole_native_mlp_and_torch_engines_learn_alike(cuda):
+    """A2C on CartPole-v1 (64 envs x 5 steps) reaches the 500-step cap and STAYS there on both engines. With the
+    preset's lr (1e-3 actor / 5e-3 critic) the policy solves and collapses again (one seed fell to 9-step episodes,
+    profiles/r3_learning_stability.txt); actor 3e-4 / critic 1e-3 with linear lr decay over the run stayed at 500 on
+    all 3 measured seeds x 2 engines. Bar: the mean of the last 3 reports (the final 1200 updates) > 400."""
     finals = {}
     for eng in ("native", "torch"):
-        tr, rows = _curve("cartpole_cpu", 3000, 300, device="cuda:0", num_envs=64, cuda_graph=True, engine=eng)
+        tr, rows = _curve("cartpole_cpu", 4000, 400, device="cuda:0", num_envs=64, cuda_graph=True, engine=eng,
+                          lr=3e-4, critic_lr=1e-3, lr_schedule="linear", total_updates=4000)
         assert (tr.mlp is not None) == (eng == "native")
-        # the peak over the run: A2C on CartPole can collapse after solving it, and where (and whether) it does
-        # depends on last-ulp rounding (an optimiser variant with a different fp contraction -- same math -- turned
-        # a run that ends above 300 into one that peaks and then collapses)
-        finals[eng] = max(r["ret"] for r in rows[1:])
-        assert rows[0]["ret"] < 100 and finals[eng] > 300, (eng, rows)
-    assert abs(finals["native"] - finals["torch"]) < 200, finals
+        finals[eng] = sum(r["ret"] for r in rows[-3:]) / 3
+        assert rows[0]["ret"] < 100 and finals[eng] > 400, (eng, rows)
+    assert abs(finals["native"] - finals["torch"]) < 100, finals
 
 
 def test_pendulum_ppo_solves_and_checkpoint_evaluates(cuda, tmp_path):
@@ -90,10 +92,18 @@ def test_pendulum_ppo_solves_and_checkpoint_evaluates(cuda, tmp_path):
     assert np.mean(rewards) > -400, rewards
 
 
-def test_mujoco_ppo_mlp_engine_improves(cuda):
-    tr, rows = _curve("mujoco_ppo_dp8", 90, 30)
+def test_mujoco_ppo_mlp_engine_learns_and_does_not_decay(cuda):
+    """MuJoCo-shape PPO on the MLP engine (64 envs x 256 steps, 10 epochs x 32 minibatches) over 300 updates: the
+    return rises from its start and the last third of the run holds >= 0.9 of the peak. The preset's constant 3e-4
+    peaks near update 90 and then decays (462 -> 338 by update 300, profiles/r2_learning_curves.txt); actor 1e-4 with
+    linear lr decay held on all 3 measured seeds (peak 443-453, last third 432-449; profiles/r3_learning_stability.txt)."""
+    tr, rows = _curve("mujoco_ppo_dp8", 300, 30, lr=1e-4, critic_lr=1e-3, lr_schedule="linear", total_updates=300)
     assert tr.mlp is not None
-    assert rows[-1]["ret"] > rows[0]["ret"] + 100, rows
+    rets = [r["ret"] for r in rows]
+    peak = max(rets)
+    assert peak > rets[0] + 150, rets
+    last_third = rets[-(len(rets) // 3):]
+    assert sum(last_third) / len(last_third) >= 0.9 * peak, rets
 
 
 @pytest.mark.parametrize("B,ppo", [(160, False), (4096, True)])

@@ -427,6 +427,9 @@ class CNNEngine:
         ev = self._ev
         ws2 = self._side_ws()
         grouped = self.grouped and (head_done or stage == "trunk") and self.fused_bwd and self.det_wgrad
+        # every gradient element of this backward is STORED (fused head, dWfc out_mode 0, conv planes and bias rows
+        # through the finaliser): the optimiser may skip zeroing the slab (trainer._run_optimizers)
+        self.last_bwd_stores_all = grouped and head_done and stage == "all"
         if stage == "trunk":
             if grouped:
                 return self._backward_grouped(b, stage, ws, ws2)

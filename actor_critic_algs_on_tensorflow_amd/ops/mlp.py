@@ -237,7 +237,8 @@ class MLPEngine:
                 if not (lo <= q.data_ptr() and q.data_ptr() + 4 * q.numel() <= hi):
                     return None
         if not hasattr(self, "_fo_bar"):
-            self._fo_bar = torch.zeros(4, dtype=torch.int32, device=self.dev)
+            # mlp.hip WGO_BAR_WORDS: sharded arrival counters, top counter, release flags, departures, timeout flag
+            self._fo_bar = torch.zeros(19 * 32, dtype=torch.int32, device=self.dev)
         words = torch.tensor([a.p.data_ptr(), c.p.data_ptr(), a.m.data_ptr(), c.m.data_ptr(), a.v.data_ptr(),
                               c.v.data_ptr(), a.lr.data_ptr(), c.lr.data_ptr(), a.t.data_ptr(), c.t.data_ptr(),
                               a.gnorm.data_ptr(), c.gnorm.data_ptr(),
@@ -249,7 +250,7 @@ class MLPEngine:
         return words, floats
 
     def fused_opt_timed_out(self):
-        return hasattr(self, "_fo_bar") and int(self._fo_bar[2]) != 0
+        return hasattr(self, "_fo_bar") and int(self._fo_bar[18 * 32]) != 0
 
     # ------------------------------------------------------------------------------------------- fused rollout
     def supports_fused_rollout(self, env):

@@ -1623,26 +1623,26 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
   }
 }
 
-// Bootstrap value V(s_T) straight from the fc partial planes: one wave per env, h = relu(sum planes + bfc)
-// (bf16-rounded like the GEMM epilogue), value = h . Wh[:, A] + bh[A]. Replaces GEMM-reduce + value GEMM.
+// Bootstrap value V(s_T) straight from the fc partial planes: one workgroup per env, thread t -> hidden units 2t,
+// 2t + 1 (fc_h2_from_parts: every plane's load of a round in flight, planes summed in order, bias + ReLU + bf16
+// rounding as the GEMM epilogue), value = h . Wh[:, A] + bh[A] reduced per wave (xor tree) then over the 4 waves in
+// order -- the same arithmetic as loss.hip a2c_head_kernel's bootstrap phase, so both give bit-identical values.
+// Replaces GEMM-reduce + value GEMM.
 __global__ void __launch_bounds__(256) fc_value_kernel(const float* __restrict__ hpart, int S, int64_t plane_stride,
                                                        const float* __restrict__ bfc, const u16* __restrict__ Wh,
                                                        int A1, const float* __restrict__ bh, float* __restrict__ out,
                                                        u16* __restrict__ h_out, int N) {
-  const int lane = threadIdx.x & 63;
-  const int e = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (e >= N) return;
+  __shared__ float s_vw[4];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int e = blockIdx.x;
   const int A = A1 - 1;
-  float wv[8];
-#pragma unroll
-  for (int r = 0; r < 8; ++r) wv[r] = bf2f(Wh[(lane * 8 + r) * A1 + A]);
-  float hv[8];
-  fc_h_from_parts(hpart, S, plane_stride, bfc, e, lane, h_out, hv);
-  float acc = 0.f;
-#pragma unroll
-  for (int r = 0; r < 8; ++r) acc += hv[r] * wv[r];
-  acc = wave_sum(acc);
-  if (lane == 0) out[e] = acc + bh[A];
+  const float w0 = bf2f(Wh[(2 * tid) * A1 + A]), w1 = bf2f(Wh[(2 * tid + 1) * A1 + A]);
+  float hv[2];
+  fc_h2_from_parts<32>(hpart, S, plane_stride, bfc, e, tid, h_out, hv);
+  const float part = wave_sum(hv[0] * w0 + hv[1] * w1);
+  if (lane == 0) s_vw[wv] = part;
+  __syncthreads();
+  if (tid == 0) out[e] = ((s_vw[0] + s_vw[1]) + (s_vw[2] + s_vw[3])) + bh[A];
 }
 
 }  // namespace aca
@@ -1654,7 +1654,7 @@ extern "C" hipError_t aca_fc_value(const float* hpart, int S, int64_t plane_stri
   if (S < 1 || S > aca::FC_MAX_PLANES || reinterpret_cast<uintptr_t>(hpart) % 16 ||
       reinterpret_cast<uintptr_t>(bfc) % 16 || plane_stride % 4)
     return hipErrorInvalidValue;
-  aca::fc_value_kernel<<<(N + 3) / 4, 256, 0, stream>>>(hpart, S, plane_stride, bfc, Wh, A1, bh, out, h_out, N);
+  aca::fc_value_kernel<<<N, 256, 0, stream>>>(hpart, S, plane_stride, bfc, Wh, A1, bh, out, h_out, N);
   return hipGetLastError();
 }
 

@@ -582,9 +582,10 @@ __global__ void __launch_bounds__(HB_THREADS) head_bwd_kernel(HeadBwdArgs a) {
 // ------------------------------------------------------------------------------------------------------------
 // A2C learner head v2: the bootstrap value V(s_T) + everything head_bwd_kernel does, in ONE launch of AH_WG narrow
 // workgroups (replaces fc_value_kernel + head_bwd_kernel: 2 launches, 8 wide workgroups on the critical path).
-//   phase 0: workgroup w, wave v computes V(s_T) of envs e = w + AH_WG (v + 4k) straight from the rollout's last fc
-//            partial planes (fc_h_from_parts: the same plane order and bf16 rounding as fc_value_kernel, so the values
-//            are bit-identical), stores them with agent-coherent (sc1) stores, and arrives at a grid barrier. Every
+//   phase 0: workgroup w computes V(s_T) of envs e = w + AH_WG k straight from the rollout's last fc partial planes
+//            (fc_h2_from_parts: the rollout step's plane order and bf16 rounding of h; the value's dot product is
+//            reduced per wave then across waves), stores them with agent-coherent (sc1) stores, and arrives at a
+//            grid barrier. Every
 //            operand that does not depend on V(s_T) (rewards, dones, values, logits, h columns, Wh) is requested
 //            before the wait.
 //   phase 1: returns / advantages of all B rows (each workgroup: identical code and order -> identical bits), the
@@ -630,19 +631,22 @@ __global__ void __launch_bounds__(AH_THREADS) a2c_head_kernel(A2cHeadArgs args) 
   const bool lead = blockIdx.x == 0, ev_wg = blockIdx.x == 1, st_wg = blockIdx.x == 2, bh_wg = blockIdx.x == 3;
   const int col0 = blockIdx.x * AH_COLS;
   hb_stamp(a, 0);
-  // ---- phase 0: bootstrap values of this workgroup's envs
+  // ---- phase 0: bootstrap values of this workgroup's envs: the whole workgroup per env (thread t: hidden units
+  // 2t, 2t + 1, every plane's load in flight at once -- fc_h2_from_parts, the fused rollout step's reduction), then
+  // h . Wh[:, A] reduced in a fixed order (xor tree per wave, waves in order)
   if (args.hpart) {
-    for (int e = blockIdx.x + AH_WG * wv; e < N; e += AH_WG * 4) {
-      float wvv[8];
-#pragma unroll
-      for (int r = 0; r < 8; ++r) wvv[r] = bf2f(a.Wh[(lane * 8 + r) * A1 + AC]);
-      float hv[8];
-      fc_h_from_parts(args.hpart, args.S, args.plane_stride, args.bfc, e, lane, nullptr, hv);
-      float acc = 0.f;
-#pragma unroll
-      for (int r = 0; r < 8; ++r) acc += hv[r] * wvv[r];
-      acc = wave_sum(acc);
-      if (lane == 0) __hip_atomic_store(&args.vboot[e], acc + args.bh[AC], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __shared__ float s_vw[4];
+    const float w0 = bf2f(a.Wh[(2 * tid) * A1 + AC]), w1 = bf2f(a.Wh[(2 * tid + 1) * A1 + AC]);
+    for (int e = blockIdx.x; e < N; e += AH_WG) {
+      float hv[2];
+      fc_h2_from_parts<32>(args.hpart, args.S, args.plane_stride, args.bfc, e, tid, nullptr, hv);
+      const float part = wave_sum(hv[0] * w0 + hv[1] * w1);
+      if (lane == 0) s_vw[wv] = part;
+      __syncthreads();
+      if (tid == 0)
+        __hip_atomic_store(&args.vboot[e], ((s_vw[0] + s_vw[1]) + (s_vw[2] + s_vw[3])) + args.bh[AC],
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
     }
   }
   // ---- operands independent of V(s_T), requested before the barrier wait

@@ -708,6 +708,11 @@ __global__ void __launch_bounds__(256) mlp_wgrad_kernel(WgradArgs a) {
 // optimiser, so the end states match). Adam's step counts are read before the barrier and advanced by workgroup 0
 // after it. The barrier needs every workgroup co-resident (~360 small workgroups; the launcher checks).
 constexpr unsigned int WGO_SPIN_LIMIT = 1u << 21;
+// barrier words (uint32), every counter / flag on a 128-byte line of its own: shard arrivals [x * LINE], top
+// counter, shard release flags [GO + x * LINE], departures, timeout flag; WGO_BAR_WORDS in total (host: mlp.py)
+constexpr unsigned int WGO_SHARDS = 8, WGO_LINE = 32;
+constexpr unsigned int WGO_TOP = 8 * WGO_LINE, WGO_GO = 9 * WGO_LINE, WGO_DEP = 17 * WGO_LINE, WGO_ERR = 18 * WGO_LINE;
+constexpr unsigned int WGO_BAR_WORDS = 19 * WGO_LINE;
 
 __device__ __forceinline__ float wgo_ld(const float* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -854,17 +859,33 @@ __global__ void __launch_bounds__(256) mlp_wgrad_adam_kernel(WgradArgs a) {
       }
     }
   }
-  // ---- grid barrier: every sum-of-squares slot published
+  // ---- grid barrier, sharded by blockIdx % 8 (the XCD under round-robin placement: speed only, any sharding is
+  // correct): a shard's arrivals go to its own counter line; the shard's last arriver (told by the returned count)
+  // adds to the top counter; the last shard's leader raises every shard's release flag; each workgroup polls only its
+  // shard's flag. Every sum-of-squares slot was stored sc1 and acknowledged before its workgroup's arrival.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (tid == 0) {
-    __hip_atomic_fetch_add(&O.bar[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    unsigned int spins = 0;
-    while (__hip_atomic_load(&O.bar[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gridDim.x) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > WGO_SPIN_LIMIT) {
-        __hip_atomic_store(&O.bar[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
+  {
+    const unsigned int G = gridDim.x, x = blockIdx.x & (WGO_SHARDS - 1);
+    const unsigned int nsh = G < WGO_SHARDS ? G : WGO_SHARDS;
+    const unsigned int nx = (G - x + WGO_SHARDS - 1) / WGO_SHARDS;
+    if (tid == 0) {
+      const unsigned int prev =
+          __hip_atomic_fetch_add(&O.bar[x * WGO_LINE], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (prev == nx - 1u) {
+        const unsigned int done =
+            __hip_atomic_fetch_add(&O.bar[WGO_TOP], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (done == nsh - 1u)
+          for (unsigned int y = 0; y < nsh; ++y)
+            __hip_atomic_store(&O.bar[WGO_GO + y * WGO_LINE], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      unsigned int spins = 0;
+      while (__hip_atomic_load(&O.bar[WGO_GO + x * WGO_LINE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > WGO_SPIN_LIMIT) {
+          __hip_atomic_store(&O.bar[WGO_ERR], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
       }
     }
   }
@@ -930,10 +951,14 @@ __global__ void __launch_bounds__(256) mlp_wgrad_adam_kernel(WgradArgs a) {
   if (tid == 0) {
     if (blockIdx.x == 0)
       for (int q = 0; q < ntw; ++q) *O.t[q] = tnew[q];
-    const unsigned int prev = __hip_atomic_fetch_add(&O.bar[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == gridDim.x - 1u) {
-      __hip_atomic_store(&O.bar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&O.bar[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned int prev = __hip_atomic_fetch_add(&O.bar[WGO_DEP], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == gridDim.x - 1u) {   // every workgroup is past its poll: reset the shard counters, top, flags
+      for (unsigned int y = 0; y < WGO_SHARDS; ++y) {
+        __hip_atomic_store(&O.bar[y * WGO_LINE], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&O.bar[WGO_GO + y * WGO_LINE], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __hip_atomic_store(&O.bar[WGO_TOP], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&O.bar[WGO_DEP], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }

@@ -319,19 +319,22 @@ __device__ __forceinline__ float fin_job(const int64_t* __restrict__ w, float* _
       s = v * v;
     }
   } else if (vec) {
-    // planes, float4 elements: 8 planes per round in flight, elements striding over the workgroup
+    // planes, float4 elements: 16 planes per round in flight (the rounds are dependent memory round trips: 4 of
+    // them for the headline's 64 weight-gradient planes, not 8), elements striding over the workgroup; the adds run
+    // in plane order whatever the round size
+    constexpr int RND = 16;
     const int n4 = n >> 2;
     for (int i = tid; i < n4; i += OPT_THREADS) {
       float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-      for (int z0 = 0; z0 < S; z0 += 8) {
-        float4 v[8];
+      for (int z0 = 0; z0 < S; z0 += RND) {
+        float4 v[RND];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < RND; ++u) {
           const int z = z0 + u < S ? z0 + u : 0;
           v[u] = *reinterpret_cast<const float4*>(src + (int64_t)z * stride + 4 * (int64_t)i);
         }
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
+        for (int u = 0; u < RND; ++u)
           if (z0 + u < S) { acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w; }
       }
       if constexpr (FUSED) reinterpret_cast<float4*>(out)[i] = acc; else reinterpret_cast<float4*>(dst)[i] = acc;

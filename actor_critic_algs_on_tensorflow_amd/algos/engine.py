@@ -252,13 +252,23 @@ class CNNEngine:
         self.last_fc = (hp, S)
         return hp, S
 
-    def forward(self, obs, b: _Bufs, head=True, shift_out=None, fc_parts=False):
+    def obs_index_ok(self, B):
+        """A learner batch of ``B`` rows can read its observations through an index (PPO minibatch gathered by
+        index, ``mb_gather`` index mode): the per-env lean-LDS trunk kernel and the per-sample conv1 weight-gradient
+        kernel are the only readers of the frames then (ACA_MB_INDEX=0: copy the minibatch's observations)."""
+        return (os.environ.get("ACA_MB_INDEX", "1") != "0" and self.implicit and self.det_wgrad
+                and B <= self.fused_trunk_max_b and B > self.trunk_rows_max_b and self.trunk_mode_large == 0
+                and B >= self.conv1_wgrad_min_b and os.environ.get("ACA_TRUNK_FWD_U8", "1") != "0")
+
+    def forward(self, obs, b: _Bufs, head=True, shift_out=None, fc_parts=False, obs_idx=None):
         """obs uint8 [B, 4, 84, 84] -> b.z fp32 [B, A+1] (logits | value); ``head=False`` stops at ``b.h`` (the
         rollout fuses the head into the sampling + env-step kernel). ``shift_out``: the next observation buffer,
         whose frames 0..2 the fused trunk fills with frames 1..3 of ``obs``; returns True iff it did."""
         B = b.B
         ws = self.ws
         b.obs = obs  # the conv1 weight gradient re-gathers its columns from the frames
+        b.obs_idx = obs_idx   # None, or: sample r is row obs_idx[r] of obs
+        assert obs_idx is None or (self.obs_index_ok(B) and obs_idx.numel() == B and shift_out is None)
         shifted = False
         want_shift = shift_out is not None
         if self.implicit and B <= self.fused_trunk_max_b:
@@ -267,7 +277,7 @@ class CNNEngine:
             fold = self.fold_args(B) if (fc_parts and not head and self.fold_ok(B)) else None
             G.cnn_trunk_fwd(obs, self.sW1, self.b1, self.sW2, self.b2, self.sW3, self.b3, b.y1, b.y2, b.y3,
                             shift_out=shift_out, mode=self.trunk_mode if B <= self.trunk_rows_max_b else self.trunk_mode_large,
-                            fold=fold)
+                            fold=fold, obs_idx=obs_idx)
             shifted = shift_out is not None
             if fold is not None:   # the fc product is already in the planes (last_fc set by fold_args)
                 return shifted if want_shift else b.z
@@ -371,7 +381,7 @@ class CNNEngine:
         if buf is None or buf.numel() < P * 32 * 256:
             buf = torch.zeros(max(P, self.wgrad_planes) * 32 * 256, dtype=torch.float32, device=self.dev)
             self._planes["W1"] = buf
-        _native.require().conv1_wgrad(b.obs, b.dy1, buf, P, 1.0 / 255.0)
+        _native.require().conv1_wgrad(b.obs, b.dy1, buf, P, 1.0 / 255.0, getattr(b, "obs_idx", None))
         self._wsplits["W1"] = P
         self._cur_planes["W1"] = P
 

@@ -688,11 +688,11 @@ class ActorCriticTrainer:
             self._kl_and_lr(logp_old, logp, ret, v)
 
     # ------------------------------------------------------------------ learning (native engine)
-    def _learn_native(self, obs, actions, logp_old, adv, ret, v_old, forward=True):
+    def _learn_native(self, obs, actions, logp_old, adv, ret, v_old, forward=True, obs_idx=None):
         cfg, eng = self.cfg, self.engine
-        b = eng.bufs(obs.shape[0], with_grad=True)
+        b = eng.bufs(obs.shape[0] if obs_idx is None else obs_idx.numel(), with_grad=True)
         if forward:
-            eng.forward(obs, b)
+            eng.forward(obs, b, obs_idx=obs_idx)
         else:
             b.obs = obs  # activations were written by the rollout; dW1 re-gathers the frames
         ppo = cfg.algo == "ppo"
@@ -765,14 +765,22 @@ class ActorCriticTrainer:
                 args = [t.contiguous() for t in (obs, actions, logp_old, adv, ret, v_old)]
                 if not hasattr(self, "_uc_ticket"):
                     self._uc_ticket = torch.zeros(1, dtype=torch.int32, device=self.device)
+                # index mode: the minibatch's observations are read in place through their row indices (no copy)
+                by_index = self.engine.obs_index_ok(mb) and args[0].is_contiguous()
+                if by_index and "idx" not in m:
+                    m["idx"] = torch.empty(mb, dtype=torch.int64, device=self.device)
                 for ep in range(cfg.ppo_epochs):
                     for k in range(cfg.ppo_minibatches):
                         last = ep == cfg.ppo_epochs - 1 and k == cfg.ppo_minibatches - 1
                         # the last gather also advances the update counter (its last workgroup; no extra launch)
-                        ops.mb_gather(*args, m["obs"], m["act"], m["logp"], m["adv"], m["ret"], m["v"],
-                                      self.policy_seed, uc, ep, k * mb, getattr(self, "_norm_mom", None), 1e-8,
-                                      self._uc_ticket if last else None)
-                        self._learn_native(m["obs"], m["act"], m["logp"], m["adv"], m["ret"], m["v"])
+                        ops.mb_gather(*args, None if by_index else m["obs"], m["act"], m["logp"], m["adv"], m["ret"],
+                                      m["v"], self.policy_seed, uc, ep, k * mb, getattr(self, "_norm_mom", None), 1e-8,
+                                      self._uc_ticket if last else None, m["idx"] if by_index else None)
+                        if by_index:
+                            self._learn_native(args[0], m["act"], m["logp"], m["adv"], m["ret"], m["v"],
+                                               obs_idx=m["idx"])
+                        else:
+                            self._learn_native(m["obs"], m["act"], m["logp"], m["adv"], m["ret"], m["v"])
                 self._uc_bumped = True
             else:
                 for sel in self._minibatches(B):

@@ -369,15 +369,16 @@ def im2col_nhwc_ref(x, B, H, W, C, kh, kw, s):
 
 
 def cnn_trunk_fwd(obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale=1.0 / 255.0, shift_out=None, mode=1,
-                  copy_out=None, fold=None):
+                  copy_out=None, fold=None, obs_idx=None):
     """Fused Nature-CNN conv1..conv3, activations through LDS (``cnn_fused.hip``). ``mode`` 1: seven workgroups per
     env, one per conv3 output row (its receptive field recomputed); 0: one workgroup per env.
     ``shift_out``: also write frames 1..3 of every observation as frames 0..2 of this buffer (frame-stack shift);
     ``copy_out`` (mode 1): also copy the whole observation there. ``fold`` = (Wfc, planes, counters): the row
-    workgroups also compute the fc product as 7 partial planes (``FcFold``, 16 or 32 observations)."""
+    workgroups also compute the fc product as 7 partial planes (``FcFold``, 16 or 32 observations). ``obs_idx``
+    (int64 [B], mode 0): sample b is row ``obs_idx[b]`` of ``obs`` (a PPO minibatch gathered by index)."""
     fw, fp, fc = fold if fold is not None else (None, None, None)
     _native.require().cnn_trunk_fwd(obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, float(scale), shift_out, None,
-                                    int(mode), copy_out, fw, fp, fc)
+                                    int(mode), copy_out, fw, fp, fc, obs_idx)
 
 
 def col2im_nhwc(dcol, ymask, dx, colsum, B, H, W, C, kh, kw, s):

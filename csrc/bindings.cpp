@@ -68,9 +68,9 @@ int aca_ev_multi_blocks(int);
 hipError_t aca_gemm_group_run(const AcaGemmDesc*, int, hipStream_t, int*);
 hipError_t aca_mb_gather(const uint8_t*, int64_t, const int*, const float*, const float*, const float*, const float*,
                          uint8_t*, int*, float*, float*, float*, float*, int, int, uint32_t, int64_t*, int, int,
-                         const double*, float, unsigned int*, hipStream_t);
+                         const double*, float, unsigned int*, int64_t*, hipStream_t);
 hipError_t aca_ev_multi(const float*, const float*, float*, int, double*, unsigned int*, hipStream_t);
-hipError_t aca_conv1_wgrad(const uint8_t*, const uint16_t*, float*, int, int, float, hipStream_t);
+hipError_t aca_conv1_wgrad(const uint8_t*, const uint16_t*, float*, int, int, float, const int64_t*, hipStream_t);
 hipError_t aca_conv_wgrad_nhwc(int, const uint16_t*, const uint16_t*, float*, int, int, hipStream_t);
 hipError_t aca_conv_wgrad_gemm(int, const uint16_t*, const uint16_t*, float*, int, int, hipStream_t);
 hipError_t aca_gemm_mfma32(const AcaGemmDesc*, hipStream_t);
@@ -98,7 +98,7 @@ hipError_t aca_ac_loss(const float*, int64_t, const float*, int64_t, const int32
                        float*, int, hipStream_t);
 hipError_t aca_cnn_trunk_fwd(const uint8_t*, const uint16_t*, const float*, const uint16_t*, const float*,
                              const uint16_t*, const float*, uint16_t*, uint16_t*, uint16_t*, int, float, uint8_t*,
-                             uint64_t*, hipStream_t);
+                             uint64_t*, const int64_t*, hipStream_t);
 hipError_t aca_grad_finalize(const int64_t*, int, float*, hipStream_t);
 hipError_t aca_grad_finalize_opt(const int64_t*, int, int, float*, float*, float*, float*, uint16_t*, const float*,
                                  const float*, float*, float*, float, float, float, float, float, float, float, int,
@@ -558,18 +558,26 @@ void returns_scan(Tensor r, Tensor v, Tensor d, Tensor ret, Tensor adv, int64_t 
 
 // conv1 weight gradient as P partial planes [P][32][256] (conv_wgrad.hip): obs uint8 [B, 4, 84, 84], dy1 bf16
 // [B * 400, 32]; plane g holds samples [g B / P, (g + 1) B / P).
-void conv1_wgrad(Tensor obs, Tensor dy1, Tensor planes, int64_t P, double scale) {
+// obs_idx (optional int64 [B]): sample b's frames are row obs_idx[b] of obs (a PPO minibatch gathered by index)
+void conv1_wgrad(Tensor obs, Tensor dy1, Tensor planes, int64_t P, double scale, c10::optional<Tensor> obs_idx) {
   TORCH_CHECK(obs.is_cuda() && obs.is_contiguous() && obs.scalar_type() == at::kByte, "conv1_wgrad: obs uint8");
   need(dy1, at::kBFloat16, "conv1_wgrad dy1");
   need(planes, at::kFloat, "conv1_wgrad planes");
-  const int64_t B = obs.numel() / (4 * 84 * 84);
-  TORCH_CHECK(B >= 1 && obs.numel() == B * 4 * 84 * 84 && dy1.numel() == B * 400 * 32,
-              "conv1_wgrad: obs [B, 4, 84, 84] and dy1 [B * 400, 32]");
+  const int64_t rows = obs.numel() / (4 * 84 * 84);
+  TORCH_CHECK(rows >= 1 && obs.numel() == rows * 4 * 84 * 84, "conv1_wgrad: obs [n, 4, 84, 84]");
+  const int64_t* idx = nullptr;
+  int64_t B = rows;
+  if (obs_idx.has_value() && obs_idx->defined()) {
+    need(*obs_idx, at::kLong, "obs_idx");
+    B = obs_idx->numel();
+    idx = obs_idx->data_ptr<int64_t>();
+  }
+  TORCH_CHECK(B >= 1 && dy1.numel() == B * 400 * 32, "conv1_wgrad: dy1 [B * 400, 32]");
   TORCH_CHECK(P >= 1 && P <= 1024 && planes.numel() >= P * 32 * 256, "conv1_wgrad: planes too small");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(obs.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(dy1.data_ptr()) % 16 == 0,
               "conv1_wgrad: 16-byte aligned operands");
   check(aca_conv1_wgrad(obs.data_ptr<uint8_t>(), ptr<uint16_t>(dy1), ptr<float>(planes), (int)B, (int)P, (float)scale,
-                        cur_stream(obs)),
+                        idx, cur_stream(obs)),
         "conv1_wgrad");
 }
 
@@ -612,9 +620,12 @@ void conv_wgrad_gemm(int64_t layer, Tensor img, Tensor dy, Tensor planes, int64_
 }
 
 // PPO minibatch k of epoch ep: rows prp_index(off + i, n, key(seed, *uc, ep)) of the rollout gathered in one launch.
-void mb_gather(Tensor obs, Tensor act, Tensor logp, Tensor adv, Tensor ret, Tensor v, Tensor o_obs, Tensor o_act,
-               Tensor o_logp, Tensor o_adv, Tensor o_ret, Tensor o_v, int64_t seed, Tensor uc, int64_t ep,
-               int64_t off, c10::optional<Tensor> mom, double eps, c10::optional<Tensor> bump_ticket) {
+// o_obs None + o_idx (int64 [mb]): index mode -- the source row of every minibatch row is written instead of a copy
+// of its observation (the minibatch's trunk forward and conv1 weight gradient read through it)
+void mb_gather(Tensor obs, Tensor act, Tensor logp, Tensor adv, Tensor ret, Tensor v, c10::optional<Tensor> o_obs_opt,
+               Tensor o_act, Tensor o_logp, Tensor o_adv, Tensor o_ret, Tensor o_v, int64_t seed, Tensor uc,
+               int64_t ep, int64_t off, c10::optional<Tensor> mom, double eps, c10::optional<Tensor> bump_ticket,
+               c10::optional<Tensor> o_idx) {
   const double* momp = nullptr;
   unsigned int* tk = nullptr;
   if (bump_ticket.has_value() && bump_ticket->defined()) {
@@ -627,23 +638,37 @@ void mb_gather(Tensor obs, Tensor act, Tensor logp, Tensor adv, Tensor ret, Tens
     momp = ptr<double>(*mom);
   }
   TORCH_CHECK(obs.is_cuda() && obs.is_contiguous() && obs.scalar_type() == at::kByte, "mb_gather: obs uint8");
-  TORCH_CHECK(o_obs.is_cuda() && o_obs.is_contiguous() && o_obs.scalar_type() == at::kByte, "mb_gather: o_obs");
+  const bool by_index = o_idx.has_value() && o_idx->defined();
+  TORCH_CHECK(by_index != (o_obs_opt.has_value() && o_obs_opt->defined()), "mb_gather: exactly one of o_obs, o_idx");
+  int64_t* idxp = nullptr;
+  uint8_t* oobs = nullptr;
+  int64_t mb = 0;
+  if (by_index) {
+    need(*o_idx, at::kLong, "o_idx");
+    idxp = o_idx->data_ptr<int64_t>();
+    mb = o_idx->numel();
+  } else {
+    const Tensor& o_obs = *o_obs_opt;
+    TORCH_CHECK(o_obs.is_cuda() && o_obs.is_contiguous() && o_obs.scalar_type() == at::kByte, "mb_gather: o_obs");
+    oobs = o_obs.data_ptr<uint8_t>();
+    mb = o_obs.size(0);
+  }
   need(act, at::kInt, "act");
   need(o_act, at::kInt, "o_act");
   for (auto* t : {&logp, &adv, &ret, &v, &o_logp, &o_adv, &o_ret, &o_v}) need(*t, at::kFloat, "mb_gather f32");
   TORCH_CHECK(uc.is_cuda() && uc.scalar_type() == at::kLong, "mb_gather: update counter int64");
-  const int64_t n = obs.size(0), mb = o_obs.size(0);
+  const int64_t n = obs.size(0);
   const int64_t R = obs.numel() / n;
-  TORCH_CHECK(o_obs.numel() == mb * R, "mb_gather: o_obs shape");
+  TORCH_CHECK(by_index || o_obs_opt->numel() == mb * R, "mb_gather: o_obs shape");
   TORCH_CHECK(act.numel() == n && logp.numel() == n && adv.numel() == n && ret.numel() == n && v.numel() == n,
               "mb_gather: per-row inputs must have n rows");
   TORCH_CHECK(o_act.numel() == mb && o_logp.numel() == mb && o_adv.numel() == mb && o_ret.numel() == mb &&
                   o_v.numel() == mb, "mb_gather: per-row outputs must have mb rows");
   TORCH_CHECK(off >= 0 && off + mb <= n, "mb_gather: minibatch out of range");
   check(aca_mb_gather(obs.data_ptr<uint8_t>(), R, ptr<int>(act), ptr<float>(logp), ptr<float>(adv), ptr<float>(ret),
-                      ptr<float>(v), o_obs.data_ptr<uint8_t>(), ptr<int>(o_act), ptr<float>(o_logp),
+                      ptr<float>(v), oobs, ptr<int>(o_act), ptr<float>(o_logp),
                       ptr<float>(o_adv), ptr<float>(o_ret), ptr<float>(o_v), (int)mb, (int)n, (uint32_t)seed,
-                      uc.data_ptr<int64_t>(), (int)ep, (int)off, momp, (float)eps, tk, cur_stream(obs)),
+                      uc.data_ptr<int64_t>(), (int)ep, (int)off, momp, (float)eps, tk, idxp, cur_stream(obs)),
         "mb_gather");
 }
 
@@ -1246,12 +1271,20 @@ int64_t gemm_effective_splits(int64_t K, int64_t bk, int64_t splits) {
 void cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, Tensor y1,
                    Tensor y2, Tensor y3, double scale, c10::optional<Tensor> shift_out,
                    c10::optional<Tensor> stamps, int64_t mode, c10::optional<Tensor> copy_out,
-                   c10::optional<Tensor> fold_w, c10::optional<Tensor> fold_planes, c10::optional<Tensor> fold_cnt) {
+                   c10::optional<Tensor> fold_w, c10::optional<Tensor> fold_planes, c10::optional<Tensor> fold_cnt,
+                   c10::optional<Tensor> obs_idx) {
   need(obs, at::kByte, "obs");
   for (auto* w : {&W1, &W2, &W3, &y1, &y2, &y3}) need(*w, at::kBFloat16, "trunk bf16 operand");
   for (auto* b : {&b1, &b2, &b3}) need(*b, at::kFloat, "trunk bias");
   TORCH_CHECK(obs.numel() % (4 * 84 * 84) == 0, "cnn_trunk_fwd: obs must be [B, 4, 84, 84]");
-  const int64_t B = obs.numel() / (4 * 84 * 84);
+  int64_t B = obs.numel() / (4 * 84 * 84);
+  const int64_t* idxp = nullptr;
+  if (obs_idx.has_value() && obs_idx->defined()) {   // sample b = row obs_idx[b] of obs (per-env mode 0 only)
+    need(*obs_idx, at::kLong, "obs_idx");
+    TORCH_CHECK(mode == 0, "cnn_trunk_fwd: obs_idx needs the per-env mode");
+    B = obs_idx->numel();
+    idxp = obs_idx->data_ptr<int64_t>();
+  }
   TORCH_CHECK(W1.numel() == 32 * 256 && W2.numel() == 64 * 512 && W3.numel() == 64 * 576,
               "cnn_trunk_fwd: weights must be Nature-CNN conv1..3");
   TORCH_CHECK(b1.numel() == 32 && b2.numel() == 64 && b3.numel() == 64, "cnn_trunk_fwd: bias sizes");
@@ -1289,7 +1322,7 @@ void cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tenso
   TORCH_CHECK(mode == 0, "cnn_trunk_fwd: mode must be 0 or 1");
   check(aca_cnn_trunk_fwd(ptr<uint8_t>(obs), ptr<uint16_t>(W1), ptr<float>(b1), ptr<uint16_t>(W2), ptr<float>(b2),
                           ptr<uint16_t>(W3), ptr<float>(b3), ptr<uint16_t>(y1), ptr<uint16_t>(y2), ptr<uint16_t>(y3),
-                          (int)B, (float)scale, so, stamps_ptr(stamps, B), cur_stream(obs)),
+                          (int)B, (float)scale, so, stamps_ptr(stamps, B), idxp, cur_stream(obs)),
         "cnn_trunk_fwd");
 }
 
@@ -1611,14 +1644,14 @@ TORCH_LIBRARY(acamd, m) {
   m.def("gemm_group_begin() -> ()", &gemm_group_begin);
   m.def("gemm_group_end() -> int", &gemm_group_end);
   m.def("gemm_group_pause(bool paused) -> ()", &gemm_group_pause);
-  m.def("conv1_wgrad(Tensor obs, Tensor dy1, Tensor planes, int P, float scale) -> ()");
+  m.def("conv1_wgrad(Tensor obs, Tensor dy1, Tensor planes, int P, float scale, Tensor? obs_idx=None) -> ()");
   m.def("conv_wgrad_nhwc(int layer, Tensor img, Tensor dy, Tensor planes, int P) -> ()");
   m.def("conv_wgrad_gemm(int layer, Tensor img, Tensor dy, Tensor planes, int P) -> ()");
   m.def("gemm_mfma32(Tensor A, int lda, bool a_k, Tensor B, int ldb, bool b_k, Tensor C, int ldc, int out_mode, "
         "int M, int N, int K, float alpha, Tensor? bias, bool relu, Tensor? mask, int ldm, int splits) -> bool");
-  m.def("mb_gather(Tensor obs, Tensor act, Tensor logp, Tensor adv, Tensor ret, Tensor v, Tensor o_obs, "
+  m.def("mb_gather(Tensor obs, Tensor act, Tensor logp, Tensor adv, Tensor ret, Tensor v, Tensor? o_obs, "
         "Tensor o_act, Tensor o_logp, Tensor o_adv, Tensor o_ret, Tensor o_v, int seed, Tensor uc, int ep, "
-        "int off, Tensor? mom=None, float eps=1e-8, Tensor? bump_ticket=None) -> ()");
+        "int off, Tensor? mom=None, float eps=1e-8, Tensor? bump_ticket=None, Tensor? o_idx=None) -> ()");
   m.def("gaussian_sample(Tensor mu, Tensor log_std, Tensor keys, int seed, Tensor act, Tensor logp, Tensor ent) -> ()");
   m.def("gae(Tensor r, Tensor v, Tensor d, Tensor ret, Tensor adv, float gamma, float lam) -> ()");
   m.def("nstep_returns(Tensor r, Tensor v, Tensor d, Tensor tgt, Tensor adv, float gamma, int L) -> ()");
@@ -1660,7 +1693,8 @@ TORCH_LIBRARY(acamd, m) {
   m.def("gemm_effective_splits(int K, int bk, int splits) -> int", &gemm_effective_splits);
   m.def("cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, Tensor y1, "
         "Tensor y2, Tensor y3, float scale, Tensor? shift_out=None, Tensor? stamps=None, int mode=0, "
-        "Tensor? copy_out=None, Tensor? fold_w=None, Tensor? fold_planes=None, Tensor? fold_cnt=None) -> ()");
+        "Tensor? copy_out=None, Tensor? fold_w=None, Tensor? fold_planes=None, Tensor? fold_cnt=None, "
+        "Tensor? obs_idx=None) -> ()");
   m.def("cnn_trunk_bwd(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tensor dy2, Tensor dy1, "
         "Tensor biasp, Tensor? stamps=None, int persist=0) -> ()");
   m.def("grad_finalize(Tensor jobs, Tensor partial) -> ()");

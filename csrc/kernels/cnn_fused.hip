@@ -243,10 +243,10 @@ __device__ __forceinline__ void trunk_w23_load(const u16* __restrict__ W2, const
                                                bf16x8 (&bw2)[16], bf16x8 (&bw3)[18]);
 
 __device__ __forceinline__ void trunk_obs_dma(const uint8_t* __restrict__ src, uint8_t* dst_lds) {
-  // 28 wave-copies of 64 x 16 B: wave w copies blocks w, w + 4, ...; lanes past the observation read its last
-  // chunk again (their bytes land in the padding)
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  for (int blk = wid; blk < TP_OBS_PAD / 1024; blk += T_THREADS / 64) {
+  // 28 wave-copies of 64 x 16 B: wave w copies blocks w, w + (waves), ...; lanes past the observation read its
+  // last chunk again (their bytes land in the padding)
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int blk = wid; blk < TP_OBS_PAD / 1024; blk += nw) {
     const int c = min(blk * 64 + lane, OBS_BYTES / 16 - 1);
     uint8_t* base = dst_lds + blk * 1024;   // wave-uniform LDS base (lane i lands at base + 16 i)
     __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint4*>(src) + c,
@@ -390,21 +390,28 @@ __global__ void __launch_bounds__(T_THREADS) cnn_trunk_fwd_persist_kernel(
 // stage), so a workgroup needs 74 KB of LDS and TWO fit a CU: while one sample waits on a barrier or a memory round
 // trip the other one's MFMAs run (the 118 KB form above runs one workgroup -- one wave per SIMD -- per CU). conv1
 // converts the pixels to exact bf16 integers on the fly; same MFMA order and epilogues: bit-identical outputs.
-__global__ void __launch_bounds__(T_THREADS) cnn_trunk_fwd_u8_kernel(
+// NW = 4 waves (two workgroups per CU: learner batches) or 8 (one workgroup per CU, each layer's tiles spread over
+// twice the waves: rollout batches below the CU count, where half the CUs would idle anyway). With 8 waves, waves
+// w and w + 4 share an output-channel tile of conv2 / conv3 and split its position tiles; same MFMA order per output
+// tile either way: bit-identical results.
+template <int NW>
+__global__ void __launch_bounds__(NW * 64) cnn_trunk_fwd_u8_kernel(
     const uint8_t* __restrict__ obs, const u16* __restrict__ W1, const float* __restrict__ b1,
     const u16* __restrict__ W2, const float* __restrict__ b2, const u16* __restrict__ W3,
     const float* __restrict__ b3, u16* __restrict__ y1g, u16* __restrict__ y2g, u16* __restrict__ y3g,
-    float scale, uint8_t* __restrict__ shift_out) {
+    float scale, uint8_t* __restrict__ shift_out, const int64_t* __restrict__ obs_idx) {
   __shared__ __attribute__((aligned(16))) uint8_t s_obs8[TP_OBS_PAD];
   __shared__ __attribute__((aligned(16))) u16 s_y1[Y1_ROWS * Y1_LD];
   __shared__ __attribute__((aligned(16))) u16 s_y2[Y2_ROWS * Y2_LD];
   const int e = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l16 = lane & 15, lg = lane >> 4;
-  const int n2 = wid * 16 + l16;
+  const int nw4 = wid & 3, half = wid >> 2;   // output-channel tile; position-tile half (NW = 8)
+  const int n2 = nw4 * 16 + l16;
   // loads in the order they are consumed (the vm counter retires in issue order): frames (LDS-DMA), conv1
   // fragments, conv2 fragments; conv3's after conv1
-  trunk_obs_dma(obs + (size_t)e * OBS_BYTES, s_obs8);
+  // obs_idx (PPO minibatch in index mode): sample e is row obs_idx[e] of the rollout's observations
+  trunk_obs_dma(obs + (size_t)(obs_idx ? obs_idx[e] : e) * OBS_BYTES, s_obs8);
   bf16x8 bw[2][8];
 #pragma unroll
   for (int nt = 0; nt < 2; ++nt)
@@ -420,10 +427,10 @@ __global__ void __launch_bounds__(T_THREADS) cnn_trunk_fwd_u8_kernel(
   if (shift_out) {   // rollout: frames 1..3 of this observation become frames 0..2 of the next one
     uint4* so = reinterpret_cast<uint4*>(shift_out + (size_t)e * OBS_BYTES);
     const uint4* si = reinterpret_cast<const uint4*>(s_obs8);
-    for (int i = OBS_BYTES / 64 + tid; i < OBS_BYTES / 16; i += T_THREADS) so[i - OBS_BYTES / 64] = si[i];
+    for (int i = OBS_BYTES / 64 + tid; i < OBS_BYTES / 16; i += NW * 64) so[i - OBS_BYTES / 64] = si[i];
   }
   // ---------------------------------------------------------------- conv1: M 400 (25 tiles), N 32 (2), K 256 (8)
-  for (int mt = wid; mt < 25; mt += 4) {
+  for (int mt = wid; mt < 25; mt += NW) {
     floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
     const int m = mt * 16 + l16;
     const int oh = m / 20, ow = m - oh * 20;
@@ -455,26 +462,28 @@ __global__ void __launch_bounds__(T_THREADS) cnn_trunk_fwd_u8_kernel(
   __syncthreads();
   // ---------------------------------------------------------------- conv2: M 81 (6 tiles), N 64 (wave = N tile), K 512
   {
-    floatx4 acc[6];
+    constexpr int M2 = NW == 8 ? 3 : 6;   // position tiles of this wave (NW = 8: half 0 -> 0..2, half 1 -> 3..5)
+    const int mt0 = NW == 8 ? 3 * half : 0;
+    floatx4 acc[M2];
 #pragma unroll
-    for (int mt = 0; mt < 6; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int mt = 0; mt < M2; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < 16; ++ks) {
       const int k = ks * 32 + lg * 8;
       const int i = k >> 7, j = (k >> 5) & 3, c0 = k & 31;
 #pragma unroll
-      for (int mt = 0; mt < 6; ++mt) {
-        const int m = min(mt * 16 + l16, Y2_ROWS - 1);
+      for (int mt = 0; mt < M2; ++mt) {
+        const int m = min((mt0 + mt) * 16 + l16, Y2_ROWS - 1);
         const int oh = m / 9, ow = m - oh * 9;
         const bf16x8 a = *reinterpret_cast<const bf16x8*>(s_y1 + ((oh * 2 + i) * 20 + ow * 2 + j) * Y1_LD + c0);
         acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw2[ks], acc[mt], 0, 0, 0);
       }
     }
 #pragma unroll
-    for (int mt = 0; mt < 6; ++mt) {
+    for (int mt = 0; mt < M2; ++mt) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = mt * 16 + lg * 4 + r;
+        const int row = (mt0 + mt) * 16 + lg * 4 + r;
         if (row < Y2_ROWS) {
           const u16 v = f2bf(fmaxf(acc[mt][r] + bias2, 0.f));
           s_y2[row * Y2_LD + n2] = v;
@@ -486,26 +495,28 @@ __global__ void __launch_bounds__(T_THREADS) cnn_trunk_fwd_u8_kernel(
   __syncthreads();
   // ---------------------------------------------------------------- conv3: M 49 (4 tiles), N 64 (wave = N tile), K 576
   {
-    floatx4 acc[4];
+    constexpr int M3 = NW == 8 ? 2 : 4;
+    const int mt0 = NW == 8 ? 2 * half : 0;
+    floatx4 acc[M3];
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int mt = 0; mt < M3; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < 18; ++ks) {
       const int k = ks * 32 + lg * 8;
       const int i = k / 192, j = (k >> 6) % 3, c0 = k & 63;
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        const int m = min(mt * 16 + l16, Y3_ROWS - 1);
+      for (int mt = 0; mt < M3; ++mt) {
+        const int m = min((mt0 + mt) * 16 + l16, Y3_ROWS - 1);
         const int oh = m / 7, ow = m - oh * 7;
         const bf16x8 a = *reinterpret_cast<const bf16x8*>(s_y2 + ((oh + i) * 9 + ow + j) * Y2_LD + c0);
         acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw3[ks], acc[mt], 0, 0, 0);
       }
     }
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
+    for (int mt = 0; mt < M3; ++mt) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = mt * 16 + lg * 4 + r;
+        const int row = (mt0 + mt) * 16 + lg * 4 + r;
         if (row < Y3_ROWS) y3g[((size_t)e * Y3_ROWS + row) * Y3_C + n2] = f2bf(fmaxf(acc[mt][r] + bias3, 0.f));
       }
     }
@@ -1661,7 +1672,7 @@ extern "C" hipError_t aca_fc_value(const float* hpart, int S, int64_t plane_stri
 extern "C" hipError_t aca_cnn_trunk_fwd(const uint8_t* obs, const uint16_t* W1, const float* b1, const uint16_t* W2,
                                         const float* b2, const uint16_t* W3, const float* b3, uint16_t* y1,
                                         uint16_t* y2, uint16_t* y3, int B, float scale, uint8_t* shift_out,
-                                        uint64_t* stamps, hipStream_t stream) {
+                                        uint64_t* stamps, const int64_t* obs_idx, hipStream_t stream) {
   if (B <= 0) return hipSuccess;
   // persistent walk (one workgroup per CU) for learner batches: ACA_TRUNK_FWD_PERSIST workgroups (0 = off)
   static const int persist = [] {
@@ -1677,9 +1688,20 @@ extern "C" hipError_t aca_cnn_trunk_fwd(const uint8_t* obs, const uint16_t* W1, 
     const char* v = getenv("ACA_TRUNK_FWD_U8");
     return !v || v[0] != '0';
   }();
-  if (u8 && !stamps && !(persist > 0 && B >= persist_min_b && !shift_out)) {
-    aca::cnn_trunk_fwd_u8_kernel<<<B, aca::T_THREADS, 0, stream>>>(obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale,
-                                                                    shift_out);
+  // obs_idx (gathered rows): only the lean-LDS per-env kernel reads through the index
+  if (obs_idx && !(u8 && !stamps)) return hipErrorInvalidValue;
+  // 8-wave workgroups while the batch leaves CUs idle (one env per CU), 4-wave ones (two per CU) above
+  static const int wide_max_b = [] {
+    const char* v = getenv("ACA_TRUNK_FWD_WIDE_MAX_B");
+    return v ? atoi(v) : 256;
+  }();
+  if (u8 && !stamps && (obs_idx || !(persist > 0 && B >= persist_min_b && !shift_out))) {
+    if (B <= wide_max_b)
+      aca::cnn_trunk_fwd_u8_kernel<8><<<B, 512, 0, stream>>>(obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale,
+                                                            shift_out, obs_idx);
+    else
+      aca::cnn_trunk_fwd_u8_kernel<4><<<B, 256, 0, stream>>>(obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale,
+                                                            shift_out, obs_idx);
     return hipGetLastError();
   }
   if (persist > 0 && B >= persist_min_b && !shift_out && !stamps) {

@@ -54,7 +54,8 @@ __device__ __forceinline__ uint2 cw_u8x4(uint32_t w) {
 
 __global__ void __launch_bounds__(CW_T) conv1_wgrad_kernel(const uint8_t* __restrict__ obs,
                                                           const u16* __restrict__ dy1, float* __restrict__ planes,
-                                                          int B, int P, float scale) {
+                                                          int B, int P, float scale,
+                                                          const int64_t* __restrict__ obs_idx) {
   __shared__ __attribute__((aligned(16))) float red[4 * 8 * 4 * 64];      // the waves' partial slices (32 KB)
   __shared__ __attribute__((aligned(16))) u16 s_dy[CW_POS * CW_LDY];
   __shared__ __attribute__((aligned(16))) u16 s_fb[CW_FR + 8];            // frame as exact bf16 + a zero chunk
@@ -72,7 +73,7 @@ __global__ void __launch_bounds__(CW_T) conv1_wgrad_kernel(const uint8_t* __rest
 #define CW_SET(S) uint4 S##f0, S##d0, S##d1, S##d2, S##d3;
 #define CW_LOAD(S, b)                                                                                    \
   {                                                                                                      \
-    const uint4* f = reinterpret_cast<const uint4*>(obs + ((size_t)(b) * 4 + ch) * CW_FR);               \
+    const uint4* f = reinterpret_cast<const uint4*>(obs + ((size_t)(obs_idx ? obs_idx[b] : (b)) * 4 + ch) * CW_FR); \
     const uint4* d = reinterpret_cast<const uint4*>(dy1 + (size_t)(b) * 400 * 32);                       \
     S##f0 = f[min(tid, CW_FR4 - 1)];                                                                     \
     S##d0 = d[tid]; S##d1 = d[tid + CW_T]; S##d2 = d[tid + 2 * CW_T];                                    \
@@ -473,10 +474,10 @@ __global__ void __launch_bounds__(512) conv_wgrad_gemm_kernel(const u16* __restr
 // obs uint8 [B][4][84][84], dy1 bf16 [B][400][32] -> planes fp32 [P][32][256] (plane g: samples
 // [g B / P, (g + 1) B / P)); grid 4 P. Shapes and alignment are checked by the binding.
 extern "C" hipError_t aca_conv1_wgrad(const uint8_t* obs, const uint16_t* dy1, float* planes, int B, int P,
-                                      float scale, hipStream_t stream) {
+                                      float scale, const int64_t* obs_idx, hipStream_t stream) {
   if (B <= 0) return hipSuccess;
   if (P < 1 || P > 1024) return hipErrorInvalidValue;
-  aca::conv1_wgrad_kernel<<<4 * P, aca::CW_T, 0, stream>>>(obs, dy1, planes, B, P, scale);
+  aca::conv1_wgrad_kernel<<<4 * P, aca::CW_T, 0, stream>>>(obs, dy1, planes, B, P, scale, obs_idx);
   return hipGetLastError();
 }
 

@@ -52,7 +52,12 @@ struct LossArgs {
   float* dbias; int dbias_n;            // head bias gradient (A+1 columns: logits | value)
 };
 
-constexpr int LOSS_THREADS = 256;
+// threads of ac_loss_kernel: the categorical specialisations run 16 waves (a B = 4096 PPO minibatch is 4 row
+// iterations per thread, not 16 -- each iteration is a dependent memory round trip); the generic form (runtime A,
+// Gaussian head) keeps 4 waves and the widest categorical heads 8, where their per-thread column arrays fit the
+// register file without spilling
+template <int AC>
+constexpr int loss_threads() { return AC == 0 ? 256 : (AC <= 16 ? 1024 : 512); }
 constexpr int LOSS_STAGE = 2048;   // fused-returns rollouts up to this many rows are staged in LDS
 constexpr int CAT_MAX = 20;        // categorical heads: logits + value columns held in registers (A + 1 <= 21)
 
@@ -63,7 +68,8 @@ constexpr int CAT_MAX = 20;        // categorical heads: logits + value columns 
 // AC > 0: categorical head with AC actions fixed at compile time (the per-column loops lose their guards, so the
 // row's loads and exp/log chains are scheduled together); AC == 0: any head (runtime A, gaussian).
 template <int AC>
-__global__ void __launch_bounds__(LOSS_THREADS) ac_loss_kernel(LossArgs a) {
+__global__ void __launch_bounds__(loss_threads<AC>()) ac_loss_kernel(LossArgs a) {
+  constexpr int LOSS_THREADS = loss_threads<AC>();
   constexpr int NJ = AC ? AC : CAT_MAX;
   __shared__ double sh[16 * 8];
   __shared__ float dls[LOSS_THREADS / 64][CAT_MAX + 1];   // per-wave partials, summed in wave order
@@ -986,14 +992,14 @@ extern "C" hipError_t aca_ac_loss(const float* logits, int64_t ldl, const float*
   if (!gaussian && A >= 2 && A <= 19) {
     switch (A) {
 #define ACA_LOSS_CASE(n) \
-  case n: aca::ac_loss_kernel<n><<<1, aca::LOSS_THREADS, 0, stream>>>(a); break;
+  case n: aca::ac_loss_kernel<n><<<1, aca::loss_threads<n>(), 0, stream>>>(a); break;
       ACA_LOSS_CASE(2) ACA_LOSS_CASE(3) ACA_LOSS_CASE(4) ACA_LOSS_CASE(5) ACA_LOSS_CASE(6) ACA_LOSS_CASE(7)
       ACA_LOSS_CASE(8) ACA_LOSS_CASE(9) ACA_LOSS_CASE(10) ACA_LOSS_CASE(11) ACA_LOSS_CASE(12) ACA_LOSS_CASE(13)
       ACA_LOSS_CASE(14) ACA_LOSS_CASE(15) ACA_LOSS_CASE(16) ACA_LOSS_CASE(17) ACA_LOSS_CASE(18) ACA_LOSS_CASE(19)
 #undef ACA_LOSS_CASE
     }
   } else {
-    aca::ac_loss_kernel<0><<<1, aca::LOSS_THREADS, 0, stream>>>(a);
+    aca::ac_loss_kernel<0><<<1, aca::loss_threads<0>(), 0, stream>>>(a);
   }
   return hipGetLastError();
 }

@@ -115,9 +115,30 @@ __global__ void __launch_bounds__(256) mb_gather_kernel(const uint8_t* __restric
                                                         float* __restrict__ o_v, int n, uint32_t seed,
                                                         int64_t* uc, int ep, int off,
                                                         const double* __restrict__ mom, float eps,
-                                                        unsigned int* __restrict__ bump_ticket) {
-  const int i = blockIdx.x;
+                                                        unsigned int* __restrict__ bump_ticket,
+                                                        int64_t* __restrict__ o_idx, int mb) {
   const int64_t ucv = *uc;
+  if (o_idx) {
+    // index mode (o_obs null): one thread per row writes the source row index instead of copying the observation;
+    // the minibatch's trunk forward and conv1 weight gradient read obs[o_idx[i]] directly (one 28 KB copy per row
+    // less)
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < mb) {
+      const uint32_t src = prp_index((uint32_t)(off + i), (uint32_t)n, minibatch_key(seed, ucv, ep));
+      float a_ = adv[src];
+      if (mom) {
+        const double cnt = mom[0], mean = mom[1] / cnt, var = fmax(mom[2] / cnt - mean * mean, 0.0);
+        a_ = (a_ - (float)mean) * (1.0f / (eps + (float)sqrt(var)));
+      }
+      o_idx[i] = src;
+      o_act[i] = act[src];
+      o_logp[i] = logp[src];
+      o_adv[i] = a_;
+      o_ret[i] = ret[src];
+      o_v[i] = v[src];
+    }
+  } else {
+  const int i = blockIdx.x;
   const uint32_t src = prp_index((uint32_t)(off + i), (uint32_t)n, minibatch_key(seed, ucv, ep));
   const uint8_t* s = obs + (size_t)src * R;
   uint8_t* d = o_obs + (size_t)i * R;
@@ -145,6 +166,7 @@ __global__ void __launch_bounds__(256) mb_gather_kernel(const uint8_t* __restric
     o_adv[i] = a_;
     o_ret[i] = ret[src];
     o_v[i] = v[src];
+  }
   }
   if (bump_ticket) {
     // last minibatch of the update: the workgroup that finishes last advances the update counter. Only a count is
@@ -577,9 +599,15 @@ extern "C" hipError_t aca_mb_gather(const uint8_t* obs, int64_t R, const int* ac
                                     const float* ret, const float* v, uint8_t* o_obs, int* o_act, float* o_logp,
                                     float* o_adv, float* o_ret, float* o_v, int mb, int n, uint32_t seed,
                                     int64_t* uc, int ep, int off, const double* mom, float eps,
-                                    unsigned int* bump_ticket, hipStream_t stream) {
+                                    unsigned int* bump_ticket, int64_t* o_idx, hipStream_t stream) {
   if (mb <= 0) return hipSuccess;
-  aca::mb_gather_kernel<<<mb, 256, 0, stream>>>(obs, R, act, logp, adv, ret, v, o_obs, o_act, o_logp, o_adv, o_ret,
-                                                o_v, n, seed, uc, ep, off, mom, eps, bump_ticket);
+  if (!o_idx && !o_obs) return hipErrorInvalidValue;
+  if (o_idx)
+    aca::mb_gather_kernel<<<(mb + 255) / 256, 256, 0, stream>>>(obs, R, act, logp, adv, ret, v, nullptr, o_act,
+                                                                 o_logp, o_adv, o_ret, o_v, n, seed, uc, ep, off, mom,
+                                                                 eps, bump_ticket, o_idx, mb);
+  else
+    aca::mb_gather_kernel<<<mb, 256, 0, stream>>>(obs, R, act, logp, adv, ret, v, o_obs, o_act, o_logp, o_adv, o_ret,
+                                                  o_v, n, seed, uc, ep, off, mom, eps, bump_ticket, nullptr, mb);
   return hipGetLastError();
 }

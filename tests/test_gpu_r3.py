@@ -412,3 +412,73 @@ def test_mlp_wgrad_with_fused_adam_is_bitwise_the_two_launch_update(cuda, name, 
             assert torch.equal(x, y), j
         else:
             torch.testing.assert_close(x, y, rtol=2e-4, atol=1e-6, msg=lambda m: f"item {j}: {m}")
+
+
+def test_ppo_minibatch_by_index_is_bitwise_the_copied_minibatch(cuda, monkeypatch):
+    """PPO on the CNN engine with minibatches gathered BY INDEX (mb_gather index mode: the trunk forward and the
+    conv1 weight gradient read obs[idx[r]] in place, no 28 KB copy per row) == the copied minibatches, bit for bit:
+    parameters and statistics over 2 graph-replayed updates (16 envs x 128 steps, 2 minibatches of 1024)."""
+    monkeypatch.setattr("actor_critic_algs_on_tensorflow_amd.ops.gemm.TUNE", False)
+    from actor_critic_algs_on_tensorflow_amd import preset
+    from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
+    runs = []
+    for knob in ("1", "0"):
+        monkeypatch.setenv("ACA_MB_INDEX", knob)
+        tr = ActorCriticTrainer(preset("breakout_ppo", num_envs=16, n_steps=128, ppo_epochs=2, ppo_minibatches=2,
+                                       device="cuda:0", outdir=None, quiet=True, stdout_freq=0, save_every=0, seed=9))
+        assert tr.engine.obs_index_ok(1024) == (knob == "1")
+        tr.capture(warmup=1)
+        for _ in range(2):
+            tr.step()
+        torch.cuda.synchronize()
+        runs.append((tr.flat.data.clone(), tr.stats_buf.clone()))
+    assert torch.equal(runs[0][0], runs[1][0])
+    assert torch.equal(runs[0][1], runs[1][1])
+
+
+def test_mb_gather_index_mode_equals_copy_mode(cuda):
+    """mb_gather index mode writes the same keyed-permutation rows the copy mode copies, and the same scalars."""
+    from actor_critic_algs_on_tensorflow_amd import _native
+    ops = _native.require()
+    n, mb, seed = 700, 300, 4242
+    g = torch.Generator(device="cpu").manual_seed(5)
+    obs = torch.randint(0, 256, (n, 4, 84, 84), dtype=torch.uint8, generator=g).to(cuda)
+    act = torch.randint(0, 6, (n,), dtype=torch.int32, generator=g).to(cuda)
+    fl = [torch.randn(n, generator=g).to(cuda) for _ in range(4)]
+    uc = torch.tensor([3], dtype=torch.int64, device=cuda)
+    outs_c = [torch.empty(mb, 4, 84, 84, dtype=torch.uint8, device=cuda), torch.empty(mb, dtype=torch.int32,
+                                                                                      device=cuda)]
+    outs_c += [torch.empty(mb, device=cuda) for _ in range(4)]
+    outs_i = [torch.empty(mb, dtype=torch.int32, device=cuda)] + [torch.empty(mb, device=cuda) for _ in range(4)]
+    idx = torch.empty(mb, dtype=torch.int64, device=cuda)
+    ops.mb_gather(obs, act, *fl, *outs_c, seed, uc, 1, 400)
+    ops.mb_gather(obs, act, *fl, None, *outs_i, seed, uc, 1, 400, None, 1e-8, None, idx)
+    assert torch.equal(obs[idx], outs_c[0])
+    for a, b in zip(outs_c[1:], outs_i):
+        assert torch.equal(a, b)
+
+
+def test_trunk_fwd_8wave_equals_4wave_kernel(cuda):
+    """The per-env lean-LDS trunk forward runs 8-wave workgroups for batches up to ACA_TRUNK_FWD_WIDE_MAX_B (256:
+    the rollout's 128 envs, one env per CU) and 4-wave ones above (two per CU): the same per-tile MFMA order, so the
+    first 200 samples of a 300-sample launch (4 waves) equal a 200-sample launch (8 waves) bit for bit."""
+    from actor_critic_algs_on_tensorflow_amd import _native
+    ops = _native.require()
+    g = torch.Generator(device="cpu").manual_seed(11)
+    obs = torch.randint(0, 256, (300, 4, 84, 84), dtype=torch.uint8, generator=g).to(cuda)
+    W1 = (0.05 * torch.randn(32, 256, generator=g)).to(torch.bfloat16).to(cuda)
+    W2 = (0.05 * torch.randn(64, 512, generator=g)).to(torch.bfloat16).to(cuda)
+    W3 = (0.05 * torch.randn(64, 576, generator=g)).to(torch.bfloat16).to(cuda)
+    b1, b2, b3 = [(0.1 * torch.randn(n, generator=g)).to(cuda) for n in (32, 64, 64)]
+
+    def run(B):
+        y = (torch.zeros(B * 400 * 32, dtype=torch.bfloat16, device=cuda),
+             torch.zeros(B * 81 * 64, dtype=torch.bfloat16, device=cuda),
+             torch.zeros(B * 49 * 64, dtype=torch.bfloat16, device=cuda))
+        ops.cnn_trunk_fwd(obs[:B], W1, b1, W2, b2, W3, b3, *y, 1.0 / 255.0, None, None, 0, None)
+        torch.cuda.synchronize()
+        return y
+
+    wide, narrow = run(200), run(300)
+    for a, b in zip(wide, narrow):
+        assert torch.equal(a, b[:a.numel()])

@@ -85,7 +85,8 @@ class FusedAdam:
         self.shadow = bf16_shadow  # optional bf16 tensor of the same numel (written by the native kernel)
         # sumsq partials (reduced by every optimiser workgroup) + the Adam step ticket (self-cleaning)
         self._partial = torch.zeros(256, dtype=torch.float32, device=dev)
-        self._ticket = torch.zeros(1, dtype=torch.int32, device=dev)
+        # (optim.hip: 8 shard counters + a top counter, one per 128-byte line)
+        self._ticket = torch.zeros(9 * 32, dtype=torch.int32, device=dev)
         # native engine: the update kernel zeroes each gradient after reading it (saves a memset per step)
         self.zero_grad_after = False
         # data parallelism: the slab holds the SUM over ranks; the kernel folds the 1/world average into its read

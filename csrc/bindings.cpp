@@ -723,6 +723,7 @@ void adam_step(Tensor p, Tensor g, Tensor m, Tensor v, Tensor lr, Tensor t, c10:
   need(lr, at::kFloat, "lr");
   need(t, at::kFloat, "t");
   need(ticket, at::kInt, "ticket");
+  TORCH_CHECK(ticket.numel() >= 9 * 32, "adam_step: the step ticket needs 9 x 32 words (8 shards + top)");
   TORCH_CHECK(g.numel() == p.numel() && m.numel() == p.numel() && v.numel() == p.numel(), "adam: size mismatch");
   check(aca_adam_step(ptr<float>(p), ptr<float>(g), ptr<float>(m), ptr<float>(v), p.numel(), ptr<float>(lr),
                       ptr<float>(t), gnorm_parts_ptr(gnorm_parts, max_norm, "adam"), optr<float>(gnorm_out),

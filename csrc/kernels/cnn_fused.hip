@@ -1690,10 +1690,12 @@ extern "C" hipError_t aca_cnn_trunk_fwd(const uint8_t* obs, const uint16_t* W1, 
   }();
   // obs_idx (gathered rows): only the lean-LDS per-env kernel reads through the index
   if (obs_idx && !(u8 && !stamps)) return hipErrorInvalidValue;
-  // 8-wave workgroups while the batch leaves CUs idle (one env per CU), 4-wave ones (two per CU) above
+  // opt-in (ACA_TRUNK_FWD_WIDE_MAX_B=256): 8-wave workgroups while the batch leaves CUs idle. Measured SLOWER on the
+  // Breakout rollout (18.7 vs 15.8 us per 128-env step, 16.35 vs 15.86 ms per update, profiles/r3_breakout_ab2.txt):
+  // the 4-wave form's two-workgroups-per-CU placement already spreads 128 envs, and the extra waves add barrier time
   static const int wide_max_b = [] {
     const char* v = getenv("ACA_TRUNK_FWD_WIDE_MAX_B");
-    return v ? atoi(v) : 256;
+    return v ? atoi(v) : 0;
   }();
   if (u8 && !stamps && (obs_idx || !(persist > 0 && B >= persist_min_b && !shift_out))) {
     if (B <= wide_max_b)

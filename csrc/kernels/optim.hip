@@ -15,6 +15,7 @@
 namespace aca {
 
 constexpr int OPT_THREADS = 256;
+constexpr unsigned int OPT_TK_LINE = 32;   // Adam step ticket: 9 counters, one per 128-byte line (ops/optim.py)
 constexpr int SUMSQ_U = 8;
 constexpr int SUMSQ_PARTS = 256;   // max sumsq workgroups = partial slots the optimiser reduces
 
@@ -169,12 +170,24 @@ __device__ __forceinline__ void opt_body(const OptSeg& S, float b1, float b2, fl
     // an agent-scope release -- an L2 write-back on this multi-XCD part -- which was 60 us of a 70 us step over a
     // 1.7M-parameter slab. The barrier orders this workgroup's reads of *S.t (every wave, at its start) before its
     // ticket, so the final write cannot overtake a reader.
+    // The ticket is sharded by workgroup % 8 (each shard counter on its own 128-byte line): one counter took ~12 ns
+    // per arrival serialised in memory -- ~20 us over the 1650 workgroups of a 1.7M-parameter Adam step. A shard's
+    // last arriver (told by the returned count) resets its counter and adds to the top counter; the last shard
+    // publishes t + 1 and resets the top. Words: [x * OPT_TK_LINE] shards, [8 * OPT_TK_LINE] top.
     __syncthreads();
     if (threadIdx.x == 0) {
-      const unsigned int prev = __hip_atomic_fetch_add(S.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (prev == (unsigned int)vgrid - 1u) {
-        *S.t = t;
-        __hip_atomic_store(S.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned int x = (unsigned int)vblk & 7u, G = (unsigned int)vgrid;
+      const unsigned int nsh = G < 8u ? G : 8u, nx = (G - x + 7u) / 8u;
+      const unsigned int prev =
+          __hip_atomic_fetch_add(S.ticket + x * OPT_TK_LINE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (prev == nx - 1u) {
+        __hip_atomic_store(S.ticket + x * OPT_TK_LINE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned int done =
+            __hip_atomic_fetch_add(S.ticket + 8 * OPT_TK_LINE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (done == nsh - 1u) {
+          *S.t = t;
+          __hip_atomic_store(S.ticket + 8 * OPT_TK_LINE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
     }
   }

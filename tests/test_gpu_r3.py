@@ -459,9 +459,9 @@ def test_mb_gather_index_mode_equals_copy_mode(cuda):
 
 
 def test_trunk_fwd_8wave_equals_4wave_kernel(cuda):
-    """The per-env lean-LDS trunk forward runs 8-wave workgroups for batches up to ACA_TRUNK_FWD_WIDE_MAX_B (256:
-    the rollout's 128 envs, one env per CU) and 4-wave ones above (two per CU): the same per-tile MFMA order, so the
-    first 200 samples of a 300-sample launch (4 waves) equal a 200-sample launch (8 waves) bit for bit."""
+    """The per-env lean-LDS trunk forward's opt-in 8-wave form (batches up to ACA_TRUNK_FWD_WIDE_MAX_B) and its
+    4-wave form share the per-tile MFMA order: the first 200 samples of a 300-sample launch equal a 200-sample launch
+    bit for bit (whichever form the process's knob selects for each; the GPU job sets 256 to cover both)."""
     from actor_critic_algs_on_tensorflow_amd import _native
     ops = _native.require()
     g = torch.Generator(device="cpu").manual_seed(11)

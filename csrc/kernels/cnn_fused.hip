@@ -689,13 +689,9 @@ __device__ __forceinline__ void trunk_rows_compute(const u16* __restrict__ s_in,
       for (int ks = 0; ks < 8; ++ks)
         bw1[nt][ks] = *reinterpret_cast<const bf16x8*>(s_w1 + (nt * 16 + l16) * W1_LD + ks * 32 + lg * 8);
     const float bias0 = bias1a, bias1 = bias1b;
-    // 10 M tiles over 4 waves (3, 3, 2, 2): a fixed trip count with a guard, no global stores in the loop (they
-    // would sit in the vm counter in front of the W3 fragment loads that conv2 waits for)
-#pragma unroll
-    for (int it = 0; it < 3; ++it) {
-      const int mt = wid + 4 * it;
-      if (mt >= TR_C1_POS / 16) break;
-      floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    // im2col A fragments of M tile mt: 8 k-steps, lane (l16, lg) reads one 8-pixel patch row (16 bytes, 8-byte
+    // aligned: two 8-byte halves)
+    auto c1_load = [&](int mt, bf16x8 (&a)[8]) {
       const int m = mt * 16 + l16;
       const int oh = m / 20, ow = m - oh * 20;      // local conv1 row, column
 #pragma unroll
@@ -704,9 +700,26 @@ __device__ __forceinline__ void trunk_rows_compute(const u16* __restrict__ s_in,
         const int c = k >> 6, i = (k >> 3) & 7;
         const u16* p = s_in + (c * TR_IN_ROWS + oh * 4 + i) * 84 + ow * 4;
         const uint2 lo = *reinterpret_cast<const uint2*>(p), hi = *reinterpret_cast<const uint2*>(p + 4);
-        const bf16x8 a = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw1[0][ks], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw1[1][ks], acc1, 0, 0, 0);
+        a[ks] = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+      }
+    };
+    // 10 M tiles over 4 waves (3, 3, 2, 2): a fixed trip count with a guard, no global stores in the loop (they
+    // would sit in the vm counter in front of the W3 fragment loads that conv2 waits for). The next tile's A
+    // fragments are read while this tile's MFMAs run (two register buffers): read one k-step ahead, as the
+    // compiler schedules it on its own, every MFMA pair waited out an LDS round trip.
+    bf16x8 abuf[2][8];
+    c1_load(wid, abuf[0]);
+#pragma unroll
+    for (int it = 0; it < 3; ++it) {
+      const int mt = wid + 4 * it;
+      if (mt >= TR_C1_POS / 16) break;
+      if (it < 2 && mt + 4 < TR_C1_POS / 16) c1_load(mt + 4, abuf[(it + 1) & 1]);
+      const bf16x8 (&a)[8] = abuf[it & 1];
+      floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks], bw1[0][ks], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks], bw1[1][ks], acc1, 0, 0, 0);
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -733,17 +746,31 @@ __device__ __forceinline__ void trunk_rows_compute(const u16* __restrict__ s_in,
     floatx4 acc[2];
     acc[0] = floatx4{0.f, 0.f, 0.f, 0.f};
     acc[1] = floatx4{0.f, 0.f, 0.f, 0.f};
+    // A fragments in chunks of 4 k-steps x 2 M tiles, the next chunk read while this one's MFMAs run (the W2 / W3
+    // fragments hold 136 registers, so not all 32 A fragments at once)
+    auto c2_load = [&](int ks0, bf16x8 (&a)[4][2]) {
 #pragma unroll
-    for (int ks = 0; ks < 16; ++ks) {
-      const int k = ks * 32 + lg * 8;   // (i, j, c0)
-      const int i = k >> 7, j = (k >> 5) & 3, c0 = k & 31;
+      for (int u = 0; u < 4; ++u) {
+        const int k = (ks0 + u) * 32 + lg * 8;   // (i, j, c0)
+        const int i = k >> 7, j = (k >> 5) & 3, c0 = k & 31;
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
-        const int m = min(mt * 16 + l16, TR_C2_POS - 1);
-        const int oh = m / 9, ow = m - oh * 9;     // local conv2 row (0..2), column
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(s_y1 + ((oh * 2 + i) * 20 + ow * 2 + j) * Y1_LD + c0);
-        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw2[ks], acc[mt], 0, 0, 0);
+        for (int mt = 0; mt < 2; ++mt) {
+          const int m = min(mt * 16 + l16, TR_C2_POS - 1);
+          const int oh = m / 9, ow = m - oh * 9;     // local conv2 row (0..2), column
+          a[u][mt] = *reinterpret_cast<const bf16x8*>(s_y1 + ((oh * 2 + i) * 20 + ow * 2 + j) * Y1_LD + c0);
+        }
       }
+    };
+    bf16x8 a2[2][4][2];
+    c2_load(0, a2[0]);
+#pragma unroll
+    for (int ch = 0; ch < 4; ++ch) {
+      if (ch < 3) c2_load(4 * (ch + 1), a2[(ch + 1) & 1]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt)
+          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2[ch & 1][u][mt], bw2[4 * ch + u], acc[mt], 0, 0, 0);
     }
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
@@ -762,13 +789,15 @@ __device__ __forceinline__ void trunk_rows_compute(const u16* __restrict__ s_in,
     const float bias = bias3;
     floatx4 acc = {0.f, 0.f, 0.f, 0.f};
     const int m = min(l16, 6);
+    bf16x8 a3[18];   // all A fragments read up front (W2's registers are free by now)
 #pragma unroll
     for (int ks = 0; ks < 18; ++ks) {
       const int k = ks * 32 + lg * 8;
       const int i = k / 192, j = (k >> 6) % 3, c0 = k & 63;
-      const bf16x8 a = *reinterpret_cast<const bf16x8*>(s_y2 + (i * 9 + m + j) * Y2_LD + c0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw3[ks], acc, 0, 0, 0);
+      a3[ks] = *reinterpret_cast<const bf16x8*>(s_y2 + (i * 9 + m + j) * Y2_LD + c0);
     }
+#pragma unroll
+    for (int ks = 0; ks < 18; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a3[ks], bw3[ks], acc, 0, 0, 0);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int row = lg * 4 + q;

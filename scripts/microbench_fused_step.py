@@ -73,6 +73,10 @@ def main():
         res.append(stamps)
     out["pong_fused_step"] = phases(res[-1], [(1, "head_env_render_staged"), (2, "conv1"), (3, "conv2"),
                                               (4, "conv3_issue"), (5, "drained")])
+    st = res[-1].cpu().double() * 10e-3
+    if bool((st[:, 6:10] != 0).any()):   # probe builds: wave 0's conv1 sub-phases (slots 6..9) from slot 1
+        out["pong_fused_step_conv1_wave0"] = {f"slot{k}": float((st[:, k] - st[:, 1]).median()) for k in range(6, 10)
+                                               if bool((st[:, k] != 0).all())}
     print(json.dumps(out, indent=1))
     if a.out:
         with open(a.out, "w") as f:

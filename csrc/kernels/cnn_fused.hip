@@ -958,7 +958,7 @@ __device__ __forceinline__ void pong_commit_next(const PongIO& io, const PongNex
   sp[0] = q.bx; sp[1] = q.by; sp[2] = q.vx; sp[3] = q.vy; sp[4] = q.pa; sp[5] = q.po; sp[6] = q.sa; sp[7] = q.so;
 }
 
-template <int A1, bool EARLY_W>
+template <int A1, int WPOS>
 __global__ void __launch_bounds__(T_THREADS) pong_fused_step_kernel(
     PongIO io, PongNext nx, FcParts fc, u16* __restrict__ h, const u16* __restrict__ Wh,
     const float* __restrict__ bh, float* __restrict__ z_out, int32_t* __restrict__ act, float* __restrict__ logp,
@@ -1007,10 +1007,15 @@ __global__ void __launch_bounds__(T_THREADS) pong_fused_step_kernel(
   uint4 vw[W1_PER];
 #pragma unroll
   for (int u = 0; u < W1_PER; ++u) vw[u] = reinterpret_cast<const uint4*>(W1)[tid + u * T_THREADS];
-  // EARLY_W: the conv2 / conv3 weight fragments are requested now, after every load the head and the staging
-  // wait for (the vm counter retires in issue order), so they arrive while the head, env and render run
+  // Where the conv2 / conv3 weight fragments (136 KB per workgroup: every workgroup pulls all of W2 / W3 from L2,
+  // ~2.3 us per step at the rate 224 workgroups get) are requested: WPOS 0 after conv1's MFMAs (trunk_rows_compute;
+  // default), 1 here, after every load the head and the staging wait for, 2 once the head's plane loads are consumed
+  // (below). The vm counter retires in issue order, so at 1 the head's fc-plane loads wait behind them; at 2 nothing
+  // waits on the vm counter before conv2, and conv1 drops from 3.9 to 1.4 us -- but the render's stores queue behind
+  // the fragment loads and the head/env/render phase grows from 6.0 to 8.8 us: the L2 -> CU transfer is on the
+  // critical path wherever it sits (profiles/r3_fused_step_wpos_ab.txt). Both measured slower than 0.
   bf16x8 bw2[16], bw3[18];
-  if constexpr (EARLY_W) trunk_w23_load(W2, W3, bw2, bw3);
+  if constexpr (WPOS == 1) trunk_w23_load(W2, W3, bw2, bw3);
   if (ff.cnt && e < FF_HELPERS) ff_stage_w(ff, e, r, s_wfc);   // lands while the head, env and conv1 run
   // ---------------------------------------------------------------- policy head (every row workgroup of env e)
   float hf[2];
@@ -1045,6 +1050,7 @@ __global__ void __launch_bounds__(T_THREADS) pong_fused_step_kernel(
     }
   }
   __syncthreads();
+  if constexpr (WPOS == 2) trunk_w23_load(W2, W3, bw2, bw3);
   if (wid == 0) {
     const int64_t key = tg0 * ((int64_t)1 << key_shift) + id0;   // pre-step counter
     const int jj = lane < A1 ? lane : 0;
@@ -1126,7 +1132,7 @@ __global__ void __launch_bounds__(T_THREADS) pong_fused_step_kernel(
   }
   __syncthreads();
   stamp(stamps, 1);
-  trunk_rows_compute<EARLY_W ? 2 : 1>(s_in, s_w1, s_y1, s_y2, e, r, bias1a, bias1b, bias2, bias3, W2, W3, y1g, y2g,
+  trunk_rows_compute<WPOS != 0 ? 2 : 1>(s_in, s_w1, s_y1, s_y2, e, r, bias1a, bias1b, bias2, bias3, W2, W3, y1g, y2g,
                                       y3g, scale, stamps, bw2, bw3, ff, s_y3, s_wfc);
 }
 
@@ -1812,16 +1818,21 @@ extern "C" hipError_t aca_pong_fused_step(
   aca::PongNext nx{state_n, t_n, tg_n, ep_ret_n};
   aca::FcParts fc{hpart, S, plane_stride, bfc};
   const int grid = N * aca::TR_ROWS;
-  // ACA_FUSED_EARLY_W=1: conv2 / conv3 weight fragments requested at kernel entry (A/B knob, read once)
-  static const bool early = [] {
-    const char* v = getenv("ACA_FUSED_EARLY_W");
-    return v && v[0] == '1';
+  // ACA_FUSED_WPOS (read once): where the conv2 / conv3 weight fragments are requested -- 0 after conv1's MFMAs
+  // (default), 1 at kernel entry, 2 after the policy head (see pong_fused_step_kernel; both measured slower)
+  static const int wpos = [] {
+    const char* v = getenv("ACA_FUSED_WPOS");
+    return v && (v[0] == '1' || v[0] == '2') ? v[0] - '0' : 0;
   }();
   if (ff_cnt) {
     const void* k = nullptr;
     switch (A + 1) {
 #define ACA_FUSED_K(A1) \
-  case A1: k = early ? (const void*)aca::pong_fused_step_kernel<A1, true> : (const void*)aca::pong_fused_step_kernel<A1, false>; break;
+  case A1:                                                                                                       \
+    k = wpos == 2 ? (const void*)aca::pong_fused_step_kernel<A1, 2>                                              \
+                  : (wpos == 1 ? (const void*)aca::pong_fused_step_kernel<A1, 1>                                 \
+                               : (const void*)aca::pong_fused_step_kernel<A1, 0>);                               \
+    break;
       ACA_FUSED_K(3) ACA_FUSED_K(4) ACA_FUSED_K(5) ACA_FUSED_K(6) ACA_FUSED_K(7)
 #undef ACA_FUSED_K
       default: return hipErrorInvalidValue;
@@ -1831,12 +1842,16 @@ extern "C" hipError_t aca_pong_fused_step(
   switch (A + 1) {
 #define ACA_FUSED_CASE(A1)                                                                                       \
   case A1:                                                                                                       \
-    if (early)                                                                                                   \
-      aca::pong_fused_step_kernel<A1, true><<<grid, aca::T_THREADS, 0, stream>>>(                                \
+    if (wpos == 2)                                                                                               \
+      aca::pong_fused_step_kernel<A1, 2><<<grid, aca::T_THREADS, 0, stream>>>(                                   \
+          io, nx, fc, h, Wh, bh, z, act, logp, ent, value, key_shift, pseed, W1, b1, W2, b2, W3, b3, y1, y2, y3,  \
+          scale, shift_out, stamps, ff);                                                                         \
+    else if (wpos == 1)                                                                                          \
+      aca::pong_fused_step_kernel<A1, 1><<<grid, aca::T_THREADS, 0, stream>>>(                                   \
           io, nx, fc, h, Wh, bh, z, act, logp, ent, value, key_shift, pseed, W1, b1, W2, b2, W3, b3, y1, y2, y3,  \
           scale, shift_out, stamps, ff);                                                                         \
     else                                                                                                         \
-      aca::pong_fused_step_kernel<A1, false><<<grid, aca::T_THREADS, 0, stream>>>(                               \
+      aca::pong_fused_step_kernel<A1, 0><<<grid, aca::T_THREADS, 0, stream>>>(                                   \
           io, nx, fc, h, Wh, bh, z, act, logp, ent, value, key_shift, pseed, W1, b1, W2, b2, W3, b3, y1, y2, y3,  \
           scale, shift_out, stamps, ff);                                                                         \
     break;

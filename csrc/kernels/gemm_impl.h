@@ -35,7 +35,11 @@ namespace aca {
 typedef short short4v __attribute__((ext_vector_type(4)));
 typedef short short8v __attribute__((ext_vector_type(8)));
 
-constexpr int GEMM_PAD = 8;  // 16 bytes per LDS row
+// LDS row padding (bf16 elements). k-contiguous tiles (read by ds_read_b128, whose lane groups are
+// {0-3,12-15,20-27} / {4-11,16-19,28-31} per 32 lanes, bank = dword % 64): a 16-byte pad gives a 2-way conflict on
+// every fragment read at any BK, a 32-byte pad none. m/n-contiguous tiles (ds_read_b64_tr_b16) keep 16 bytes.
+constexpr int GEMM_PAD_K = 16;
+constexpr int GEMM_PAD = 8;
 
 __device__ __forceinline__ uint4 pack8(const u16* t) {
   uint4 r;
@@ -239,8 +243,8 @@ struct GemmParams {
 // LDS footprint (bf16 elements) of one tile configuration: double-buffered A and B k-step tiles
 template <int BM, int BN, int BK, bool A_K, bool B_K>
 struct GemmSmem {
-  static constexpr int A_ELEMS = A_K ? BM * (BK + GEMM_PAD) : BK * (BM + GEMM_PAD);
-  static constexpr int B_ELEMS = B_K ? BN * (BK + GEMM_PAD) : BK * (BN + GEMM_PAD);
+  static constexpr int A_ELEMS = A_K ? BM * (BK + GEMM_PAD_K) : BK * (BM + GEMM_PAD);
+  static constexpr int B_ELEMS = B_K ? BN * (BK + GEMM_PAD_K) : BK * (BN + GEMM_PAD);
   static constexpr int ELEMS = 2 * (A_ELEMS + B_ELEMS);
 };
 
@@ -341,7 +345,7 @@ __device__ __forceinline__ void gemm_block(const GemmParams& P, const int tile, 
     for (int c = 0; c < A_CHUNKS; ++c) {
       const int ch = tid + c * 256;
       int off;
-      if (A_K) off = (ch / (BK / 8)) * (BK + GEMM_PAD) + (ch % (BK / 8)) * 8;
+      if (A_K) off = (ch / (BK / 8)) * (BK + GEMM_PAD_K) + (ch % (BK / 8)) * 8;
       else off = (ch / (BM / 8)) * (BM + GEMM_PAD) + (ch % (BM / 8)) * 8;
       *reinterpret_cast<uint4*>(As0 + buf * A_ELEMS + off) = AG == 1 ? u8x8_convert(ra[c], g.ga.scale) : ra[c];
     }
@@ -349,7 +353,7 @@ __device__ __forceinline__ void gemm_block(const GemmParams& P, const int tile, 
     for (int c = 0; c < B_CHUNKS; ++c) {
       const int ch = tid + c * 256;
       int off;
-      if (B_K) off = (ch / (BK / 8)) * (BK + GEMM_PAD) + (ch % (BK / 8)) * 8;
+      if (B_K) off = (ch / (BK / 8)) * (BK + GEMM_PAD_K) + (ch % (BK / 8)) * 8;
       else off = (ch / (BN / 8)) * (BN + GEMM_PAD) + (ch % (BN / 8)) * 8;
       *reinterpret_cast<uint4*>(Bs0 + buf * B_ELEMS + off) = BG == 1 ? u8x8_convert(rb[c], g.gb.scale) : rb[c];
     }
@@ -361,7 +365,7 @@ __device__ __forceinline__ void gemm_block(const GemmParams& P, const int tile, 
 
   auto frag = [&](const u16* base, bool kc, int ld_dim, int rowbase, int ks) -> bf16x8 {
     if (kc) {
-      return *reinterpret_cast<const bf16x8*>(base + (rowbase + lr16) * (BK + GEMM_PAD) + ks * 32 + lg * 8);
+      return *reinterpret_cast<const bf16x8*>(base + (rowbase + lr16) * (BK + GEMM_PAD_K) + ks * 32 + lg * 8);
     } else {
       const int kb = ks * 32 + lg * 8;
       const u16* p0 = base + (kb + q) * (ld_dim + GEMM_PAD) + rowbase + 4 * p;

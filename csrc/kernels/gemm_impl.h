@@ -27,6 +27,8 @@
 // ticket and no fence; the consumer kernel sums the planes in fixed order (deterministic) and applies bias and
 // activation itself -- the rollout's fc product, whose only consumer is the fused policy/env kernel.
 #pragma once
+#include <type_traits>
+
 #include "common.h"
 #include "gemm_desc.h"
 
@@ -35,11 +37,22 @@ namespace aca {
 typedef short short4v __attribute__((ext_vector_type(4)));
 typedef short short8v __attribute__((ext_vector_type(8)));
 
-// LDS row padding (bf16 elements). k-contiguous tiles (read by ds_read_b128, whose lane groups are
-// {0-3,12-15,20-27} / {4-11,16-19,28-31} per 32 lanes, bank = dword % 64): a 16-byte pad gives a 2-way conflict on
-// every fragment read at any BK, a 32-byte pad none. m/n-contiguous tiles (ds_read_b64_tr_b16) keep 16 bytes.
+// LDS layouts. k-contiguous tiles (read by ds_read_b128, whose lane groups are {0-3,12-15,20-27} /
+// {4-11,16-19,28-31} per 32 lanes, bank = dword % 64) pad each row by 32 bytes: a 16-byte pad gave a 2-way
+// conflict on every fragment read at any BK. m/n-contiguous tiles (rows of W = BM or BN elements, read by
+// ds_read_b64_tr_b16: a 32-lane group reads k rows {r..r+3, r+8..r+11} x 32 bytes) are unpadded with the 16-byte
+// chunk index XOR-swizzled by the row (gemm_tr_swz): no pad can separate rows r and r + 8 (2-way on every read);
+// the swizzle makes both the transposed reads and the 16-byte staging stores conflict-free for W = 32..256.
 constexpr int GEMM_PAD_K = 16;
-constexpr int GEMM_PAD = 8;
+constexpr int GEMM_PAD = 0;
+
+template <int W>
+__device__ __forceinline__ int gemm_tr_swz(int row) {
+  static_assert(W == 32 || W == 64 || W == 128 || W == 256, "swizzle defined for 32..256-wide tiles");
+  if constexpr (W == 32) return ((row >> 3) & 1) << 1;
+  else if constexpr (W == 64) return (((row >> 1) & 1) << 1) ^ (((row >> 3) & 1) << 2);
+  else return ((row & 1) << 1) ^ (((row >> 1) & 1) << 2) ^ (((row >> 3) & 1) << 3);
+}
 
 __device__ __forceinline__ uint4 pack8(const u16* t) {
   uint4 r;
@@ -346,7 +359,10 @@ __device__ __forceinline__ void gemm_block(const GemmParams& P, const int tile, 
       const int ch = tid + c * 256;
       int off;
       if (A_K) off = (ch / (BK / 8)) * (BK + GEMM_PAD_K) + (ch % (BK / 8)) * 8;
-      else off = (ch / (BM / 8)) * (BM + GEMM_PAD) + (ch % (BM / 8)) * 8;
+      else {
+        const int kr = ch / (BM / 8);
+        off = kr * (BM + GEMM_PAD) + ((ch % (BM / 8)) ^ gemm_tr_swz<BM>(kr)) * 8;
+      }
       *reinterpret_cast<uint4*>(As0 + buf * A_ELEMS + off) = AG == 1 ? u8x8_convert(ra[c], g.ga.scale) : ra[c];
     }
 #pragma unroll
@@ -354,7 +370,10 @@ __device__ __forceinline__ void gemm_block(const GemmParams& P, const int tile, 
       const int ch = tid + c * 256;
       int off;
       if (B_K) off = (ch / (BK / 8)) * (BK + GEMM_PAD_K) + (ch % (BK / 8)) * 8;
-      else off = (ch / (BN / 8)) * (BN + GEMM_PAD) + (ch % (BN / 8)) * 8;
+      else {
+        const int kr = ch / (BN / 8);
+        off = kr * (BN + GEMM_PAD) + ((ch % (BN / 8)) ^ gemm_tr_swz<BN>(kr)) * 8;
+      }
       *reinterpret_cast<uint4*>(Bs0 + buf * B_ELEMS + off) = BG == 1 ? u8x8_convert(rb[c], g.gb.scale) : rb[c];
     }
   };
@@ -363,13 +382,18 @@ __device__ __forceinline__ void gemm_block(const GemmParams& P, const int tile, 
   const int q = lr16 >> 2, p = lr16 & 3;        // transposed-read address roles (lane 4q+p of each 16-lane group)
   typedef __attribute__((address_space(3))) short4v lds_s4;
 
-  auto frag = [&](const u16* base, bool kc, int ld_dim, int rowbase, int ks) -> bf16x8 {
+  // m/n-contiguous operand: element (k, col) of a W-wide tile at row k, 16-byte chunk (col / 8) ^ swz(k)
+  auto tr_addr = [&](const u16* base, auto wtag, int k, int col) -> const u16* {
+    constexpr int W = decltype(wtag)::value;
+    return base + k * (W + GEMM_PAD) + (((col >> 3) ^ gemm_tr_swz<W>(k)) << 3) + (col & 7);
+  };
+  auto frag = [&](const u16* base, bool kc, auto wtag, int rowbase, int ks) -> bf16x8 {
     if (kc) {
       return *reinterpret_cast<const bf16x8*>(base + (rowbase + lr16) * (BK + GEMM_PAD_K) + ks * 32 + lg * 8);
     } else {
       const int kb = ks * 32 + lg * 8;
-      const u16* p0 = base + (kb + q) * (ld_dim + GEMM_PAD) + rowbase + 4 * p;
-      const u16* p1 = base + (kb + 4 + q) * (ld_dim + GEMM_PAD) + rowbase + 4 * p;
+      const u16* p0 = tr_addr(base, wtag, kb + q, rowbase + 4 * p);
+      const u16* p1 = tr_addr(base, wtag, kb + 4 + q, rowbase + 4 * p);
       const short4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(p0));
       const short4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(p1));
       const short8v v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -384,9 +408,11 @@ __device__ __forceinline__ void gemm_block(const GemmParams& P, const int tile, 
     for (int ks = 0; ks < BK / 32; ++ks) {
       bf16x8 af[TM], bfr[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = frag(as, A_K, BM, wm * (BM / 2) + i * 16, ks);
+      for (int i = 0; i < TM; ++i)
+        af[i] = frag(as, A_K, std::integral_constant<int, BM>{}, wm * (BM / 2) + i * 16, ks);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bfr[j] = frag(bs, B_K, BN, wn * (BN / 2) + j * 16, ks);
+      for (int j = 0; j < TN; ++j)
+        bfr[j] = frag(bs, B_K, std::integral_constant<int, BN>{}, wn * (BN / 2) + j * 16, ks);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll

@@ -102,6 +102,10 @@ class CNNEngine:
         self.trunk_mode = int(os.environ.get("ACA_TRUNK_MODE", "2"))
         self.trunk_mode_large = int(os.environ.get("ACA_TRUNK_MODE_LARGE", "0"))
         self.trunk_rows_max_b = int(os.environ.get("ACA_TRUNK_ROWS_MAX_B", "64"))
+        # batches from this size up compute the policy/value head with head_fwd (0 = never, the default: the kernel
+        # is 8.3 vs ~15.5 us for the GEMM at B = 4096, but Breakout PPO A/B runs were within the GEMM autotuner's
+        # run-to-run noise, profiles/r3_head_fwd_ab.txt)
+        self.head_fwd_min_b = int(os.environ.get("ACA_HEAD_FWD_MIN_B", "0")) or (1 << 62)
         # learner data-gradient chain dy3 -> dy2 -> dy1 as ONE per-sample kernel (cnn_trunk_bwd; bias gradients as
         # per-sample partial rows reduced by the gradient finaliser) instead of two transposed-conv GEMMs
         self.fused_bwd = implicit and os.environ.get("ACA_FUSED_BWD", "1") != "0"
@@ -309,9 +313,17 @@ class CNNEngine:
         G.gemm(b.y3, 3136, True, self.sWfc, 512, False, b.h, 512, 1, B, 512, 3136, bias=self.bfc, relu=True,
                workspace=ws)
         if head:
-            G.gemm(b.h, 512, True, self.sWh, self.A1, False, b.z, self.A1, 0, B, self.A1, 512, bias=self.bh,
-                   workspace=ws)
+            if self.head_fwd_ok(B):   # large learner batches: dedicated N = A + 1 kernel (heads.hip head_fwd)
+                _native.require().head_fwd(b.h, self.sWh, self.bh, b.z)
+            else:
+                G.gemm(b.h, 512, True, self.sWh, self.A1, False, b.z, self.A1, 0, B, self.A1, 512, bias=self.bh,
+                       workspace=ws)
         return shifted if want_shift else b.z
+
+    def head_fwd_ok(self, B):
+        """z = h Wh + bh by ``head_fwd`` (8 lanes per row, Wh in LDS) instead of the generic GEMM, whose few
+        workgroups walk every k-step of the unaligned [512, A+1] operand (~15 us at B = 4096)."""
+        return self.dev.type == "cuda" and 2 <= self.A1 <= 8 and B >= self.head_fwd_min_b
 
     # ------------------------------------------------------------------------------------------------ backward
     def tail_bucket(self):

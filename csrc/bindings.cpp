@@ -91,6 +91,7 @@ hipError_t aca_im2col_nhwc(const uint16_t*, uint16_t*, int, int, int, int, int, 
 hipError_t aca_col2im_nhwc(const uint16_t*, const uint16_t*, uint16_t*, float*, int, int, int, int, int, int, int,
                            hipStream_t);
 hipError_t aca_colsum_bf16(const uint16_t*, int64_t, int, int64_t, float*, hipStream_t);
+hipError_t aca_head_fwd(const uint16_t*, const uint16_t*, const float*, float*, int, int, hipStream_t);
 hipError_t aca_ac_loss(const float*, int64_t, const float*, int64_t, const int32_t*, const float*, const float*,
                        const float*, const float*, const float*, const float*, const float*, const float*, float, float,
                        float, uint16_t*, int64_t, uint16_t*, int64_t, float*, float*, int, int, int, int,
@@ -1541,6 +1542,24 @@ void colsum_bf16(Tensor x, int64_t M, int64_t N, int64_t ld, Tensor out) {
   check(aca_colsum_bf16(ptr<uint16_t>(x), M, N, ld, ptr<float>(out), cur_stream(x)), "colsum_bf16");
 }
 
+// z [B, A1] fp32 = bh + h [B, 512] bf16 . Wh [512, A1] bf16 (large learner batches; heads.hip head_fwd_kernel)
+void head_fwd(Tensor h, Tensor Wh, Tensor bh, Tensor z) {
+  TORCH_CHECK(h.scalar_type() == at::kBFloat16 && h.is_contiguous() && h.dim() == 2 && h.size(1) == 512,
+              "head_fwd: h must be contiguous bf16 [B, 512]");
+  const int64_t B = h.size(0), A1 = bh.numel();
+  TORCH_CHECK(A1 >= 2 && A1 <= 8, "head_fwd: 2 <= A + 1 <= 8");
+  TORCH_CHECK(Wh.scalar_type() == at::kBFloat16 && Wh.is_contiguous() && Wh.numel() == 512 * A1,
+              "head_fwd: Wh must be contiguous bf16 [512, A1]");
+  TORCH_CHECK(bh.scalar_type() == at::kFloat && bh.is_contiguous(), "head_fwd: bh must be fp32");
+  TORCH_CHECK(z.scalar_type() == at::kFloat && z.is_contiguous() && z.numel() >= B * A1,
+              "head_fwd: z must be contiguous fp32 [B, A1]");
+  TORCH_CHECK(h.device() == Wh.device() && h.device() == bh.device() && h.device() == z.device(),
+              "head_fwd: one device");
+  check(aca_head_fwd(ptr<uint16_t>(h), ptr<uint16_t>(Wh), ptr<float>(bh), ptr<float>(z), (int)B, (int)A1,
+                     cur_stream(h)),
+        "head_fwd");
+}
+
 // ---------------------------------------------------------------------------------------------- loss
 void ac_loss(Tensor logits, int64_t ldl, c10::optional<Tensor> value, int64_t ldv, c10::optional<Tensor> act_i,
              c10::optional<Tensor> act_f, c10::optional<Tensor> log_std, Tensor logp_old, c10::optional<Tensor> adv,
@@ -1715,6 +1734,7 @@ TORCH_LIBRARY(acamd, m) {
   m.def("col2im_nhwc(Tensor dcol, Tensor ymask, Tensor dx, Tensor? colsum, int B, int H, int W, int C, int kh, "
         "int kw, int s) -> ()");
   m.def("colsum_bf16(Tensor x, int M, int N, int ld, Tensor out) -> ()");
+  m.def("head_fwd(Tensor h, Tensor Wh, Tensor bh, Tensor z) -> ()");
   m.def("ac_loss(Tensor logits, int ldl, Tensor? value, int ldv, Tensor? act_i, Tensor? act_f, Tensor? log_std, "
         "Tensor logp_old, Tensor? adv, Tensor? ret, Tensor? v_old, Tensor? ent_coef, Tensor? kl_coef, float vf_coef, "
         "float ppo_clip, float v_clip, Tensor dlogits, int lddl, Tensor? dvalue, int lddv, Tensor? dlog_std, "
@@ -1768,6 +1788,7 @@ TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
   m.impl("im2col_nhwc", &im2col_nhwc);
   m.impl("col2im_nhwc", &col2im_nhwc);
   m.impl("colsum_bf16", &colsum_bf16);
+  m.impl("head_fwd", &head_fwd);
   m.impl("colsum_reduce", &colsum_reduce);
   m.impl("seg_stats", &seg_stats);
   m.impl("ac_loss", &ac_loss);

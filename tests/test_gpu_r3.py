@@ -482,3 +482,43 @@ def test_trunk_fwd_8wave_equals_4wave_kernel(cuda):
     wide, narrow = run(200), run(300)
     for a, b in zip(wide, narrow):
         assert torch.equal(a, b[:a.numel()])
+
+
+@pytest.mark.parametrize("B,A1", [(1, 2), (33, 5), (4096, 5), (1000, 7), (64, 8)])
+def test_head_fwd_matches_fp32(cuda, B, A1):
+    """heads.hip head_fwd (large-batch policy/value head, 8 lanes per row, Wh staged in LDS) == the fp32 product of
+    the same bf16 operands, and repeat launches are bit-identical."""
+    from actor_critic_algs_on_tensorflow_amd import _native
+    ops = _native.require()
+    g = torch.Generator(device="cpu").manual_seed(B + A1)
+    h = torch.relu(torch.randn(B, 512, generator=g)).to(torch.bfloat16).to(cuda)
+    Wh = (0.05 * torch.randn(512, A1, generator=g)).to(torch.bfloat16).to(cuda)
+    bh = torch.randn(A1, generator=g).to(cuda)
+    z = torch.full((B, A1), float("nan"), device=cuda)
+    ops.head_fwd(h, Wh, bh, z)
+    z2 = torch.empty_like(z)
+    ops.head_fwd(h, Wh, bh, z2)
+    torch.cuda.synchronize()
+    ref = h.double() @ Wh.double() + bh.double()
+    torch.testing.assert_close(z.double(), ref, rtol=1e-5, atol=1e-4)
+    assert torch.equal(z, z2)
+
+
+def test_ppo_learner_forward_head_fwd_equals_gemm_path(cuda, monkeypatch):
+    """The CNN engine's large-batch head (head_fwd) and the GEMM path give the same logits / values to fp32
+    rounding on a PPO-sized batch."""
+    from actor_critic_algs_on_tensorflow_amd import preset
+    from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
+    tr = ActorCriticTrainer(preset("breakout_ppo", num_envs=16, n_steps=64, device="cuda:0", outdir=None, quiet=True,
+                                   stdout_freq=0, save_every=0, cuda_graph=False))
+    eng = tr.engine
+    obs = torch.randint(0, 256, (1024, 4, 84, 84), dtype=torch.uint8, device=cuda)
+    b = eng.bufs(1024)
+    eng.head_fwd_min_b = 512   # opt-in (ACA_HEAD_FWD_MIN_B)
+    assert eng.head_fwd_ok(1024)
+    z_new = eng.forward(obs, b).clone()
+    eng.head_fwd_min_b = 1 << 62
+    assert not eng.head_fwd_ok(1024)
+    z_gemm = eng.forward(obs, b).clone()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(z_new, z_gemm, rtol=1e-4, atol=1e-4)

@@ -17,6 +17,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="pong_a2c,breakout_ppo")
     ap.add_argument("--rounds", type=int, default=3, help="tune each shape this many times, keep the fastest plan")
+    ap.add_argument("--out", default=None, help="write here instead of the package's plans file")
+    ap.add_argument("--keep-existing", action="store_true",
+                    help="shapes already in the package's plans file keep their plan (only new shapes are added)")
     a = ap.parse_args()
     best = {}
     for _ in range(a.rounds):
@@ -33,8 +36,14 @@ def main():
                 best[k] = v
     G._TUNED.clear()
     G._TUNED.update(best)
-    n = G.save_plans()
-    print("wrote", n, "plans to", G.PLANS_FILE)
+    if a.keep_existing:
+        import json
+        with open(G.PLANS_FILE) as f:
+            for r in json.load(f):
+                G._TUNED[G._key_from_json(r["key"])] = tuple(r["plan"])
+    out = a.out or G.PLANS_FILE
+    n = G.save_plans(out)
+    print("wrote", n, "plans to", out)
 
 
 if __name__ == "__main__":

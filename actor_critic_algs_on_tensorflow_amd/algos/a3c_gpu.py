@@ -58,6 +58,10 @@ def _pay_len(n):
     return (n + PAY_ALIGN - 1) // PAY_ALIGN * PAY_ALIGN + PAY_ALIGN
 
 
+class _PeerLost(Exception):
+    """A control-plane receive on the PS failed: a worker departed (closed peer or group timeout)."""
+
+
 def shard_ranges(flat, ps_num):
     """Contiguous slab ranges, one per PS, cut at parameter boundaries and balanced by element count."""
     bounds = [off + p.numel() for p, off in zip(flat.params, flat.offsets)]
@@ -186,18 +190,26 @@ class DeviceParameterServer:
 
     def serve(self):
         """Serves until every worker said DONE. A failed control-plane receive (a worker died: gloo reports the
-        closed peer, or the group timeout expired) ends the PS with ``status == "aborted"`` instead of a hang."""
+        closed peer, or the group timeout expired) ends the PS with ``status == "aborted"`` instead of a hang. Only
+        that receive is treated as a departure: a failure of the apply (optimiser launch) or of the reply
+        propagates, so a kernel error on the PS is never reported as a worker death."""
         try:
             self._serve()
-        except RuntimeError as e:
+        except _PeerLost as e:
             self.status = "aborted"
-            self.error = repr(e)
+            self.error = repr(e.__cause__)
+
+    def _recv_hdr(self):
+        try:
+            return self.planes.recv_hdr()
+        except RuntimeError as e:   # gloo: peer closed / timeout (DistBackendError is a RuntimeError)
+            raise _PeerLost() from e
 
     def _serve(self):
         pending = []   # deferred applies (stale-synchronous bound), served in arrival order once allowed
         while self.live or pending:
             if self.live:
-                src, (cmd, _task, version, _) = self.planes.recv_hdr()
+                src, (cmd, _task, version, _) = self._recv_hdr()
                 if cmd == CMD_DONE:
                     self.live.discard(src)
                 elif cmd == CMD_PULL:
@@ -290,16 +302,34 @@ class GPUWorker:
         self.returns = []
         last_mark = -1
         i = 0
+        # the env bank's episode counters are drained ONCE per iteration in which any consumer reads them, into one
+        # accumulator per consumer, so the `returns` rows and the worker log each see every finished episode
+        acc = {"report": [0.0, 0, 0.0], "log": [0.0, 0, 0.0]}
+
+        def take(key):
+            s, n, ln = acc[key]
+            acc[key] = [0.0, 0, 0.0]
+            return (s / n if n else float("nan")), n, (ln / n if n else float("nan"))
+
         while self.version < total_updates:
             if fault is not None and fault == (self.rank, i):   # SURVEY §5.3 test hook: die without goodbye
                 os._exit(FAULT_EXIT_CODE)
             tr.step()
             hist.append(self.version)
-            if report_every and len(hist) % report_every == 0:
-                ret, n_ep, _ = tr.env.drain_episode_stats()
+            rep_due = bool(report_every) and len(hist) % report_every == 0
+            log_due = tr.logger is not None and bool(cfg.stdout_freq) and i % cfg.stdout_freq == 0
+            if rep_due or log_due:
+                ret, n_ep, ln = tr.env.drain_episode_stats()
+                for a in acc.values():
+                    if n_ep:
+                        a[0] += ret * n_ep
+                        a[1] += n_ep
+                        a[2] += ln * n_ep
+            if rep_due:
+                ret, n_ep, _ = take("report")
                 self.returns.append((len(hist), self.version, ret, n_ep))
-            if tr.logger is not None and cfg.stdout_freq and i % cfg.stdout_freq == 0:
-                tr.log(i, print_tog=not cfg.quiet)   # A3C/process.py:280-283
+            if log_due:
+                tr.log(i, print_tog=not cfg.quiet, ep_stats=take("log"))   # A3C/process.py:280-283
             if tr.logger is not None and cfg.flush_every and i % cfg.flush_every == cfg.flush_every // 2:
                 tr.logger.flush()
             if self.task == 0 and cfg.save_every and cfg.checkpoint_dir:
@@ -353,6 +383,9 @@ def run(cfg, rank=None, world=None, ps_num=None, data_backend="gloo", max_stalen
     if cfg.max_grad_norm is not None:
         raise ValueError("async PS mode clips element-wise only (A3C/policies.py:85); a global-norm clip "
                          f"(max_grad_norm={cfg.max_grad_norm}) would be computed per PS shard: set it to None")
+    if cfg.lr_schedule != "constant":
+        raise ValueError("async PS mode: the critic lr lives in the PS shard optimisers, which do not decay it; "
+                         "lr_schedule must be 'constant'")
     device = torch.device(device or cfg.device)
     if device.type == "cuda":
         torch.cuda.set_device(device)

@@ -29,8 +29,6 @@ the bf16 shadow of the slab that the fused optimiser rewrites every step.
 """
 from __future__ import annotations
 
-import os
-
 import torch
 
 from .. import _native
@@ -85,83 +83,64 @@ class _Bufs:
 class CNNEngine:
     """Explicit forward/backward of :class:`..models.policy.CNNActorCritic` over a :class:`FlatParams` slab."""
 
-    def __init__(self, model, flat, shadow, implicit=True, fused_trunk_max_b=None, tconv_dgrad=None):
+    def __init__(self, model, flat, shadow, implicit=True, fused_trunk_max_b=None, tconv_dgrad=None, opts=None):
+        from ..config import EngineOpts
         net = model.net
+        o = self.opts = opts if opts is not None else EngineOpts()
         self.implicit = implicit
         # data gradients of conv3/conv2 as transposed-conv GEMMs gathered from dy (no dcol matrix, no col2im pass)
         self.tconv_dgrad = implicit if tconv_dgrad is None else tconv_dgrad
         # one workgroup per env: the fused trunk wins whenever the per-layer GEMMs are launch/latency bound
         self.fused_trunk_max_b = 4096 if fused_trunk_max_b is None else fused_trunk_max_b
-        # rollout frame-stack shift inside the fused trunk (else the env kernel shifts); A/B switch for profiling
-        self.trunk_shift = os.environ.get("ACA_TRUNK_SHIFT", "1") != "0"
-        # 1 / 2: seven row workgroups per env (224 CUs at 32 envs; 2 issues the conv2/conv3 weight loads after conv1,
-        # leaving conv1 the registers to pipeline its LDS reads); 0: one workgroup per env. Row splitting buys
-        # parallelism for rollout-sized batches; large learner batches already fill the chip with one workgroup per
-        # env, and the split's recomputed receptive fields only cost there (ACA_TRUNK_MODE_LARGE above
-        # ACA_TRUNK_ROWS_MAX_B envs: 7 B row workgroups stop fitting the chip in one wave)
-        self.trunk_mode = int(os.environ.get("ACA_TRUNK_MODE", "2"))
-        self.trunk_mode_large = int(os.environ.get("ACA_TRUNK_MODE_LARGE", "0"))
-        self.trunk_rows_max_b = int(os.environ.get("ACA_TRUNK_ROWS_MAX_B", "64"))
-        # batches from this size up compute the policy/value head with head_fwd (0 = never, the default: the kernel
-        # is 8.3 vs ~15.5 us for the GEMM at B = 4096, but Breakout PPO A/B runs were within the GEMM autotuner's
-        # run-to-run noise, profiles/r3_head_fwd_ab.txt)
-        self.head_fwd_min_b = int(os.environ.get("ACA_HEAD_FWD_MIN_B", "0")) or (1 << 62)
+        # rollout batches up to trunk_rows_max_b envs: seven row workgroups per env (224 CUs at 32 envs; late_w
+        # issues the conv2/conv3 weight loads after conv1, leaving conv1 the registers to pipeline its LDS reads).
+        # Larger batches already fill the chip with one workgroup per env (mode 0), where the split's recomputed
+        # receptive fields only cost
+        self.trunk_mode = 2 if o.trunk_late_w else 1
+        self.trunk_rows_max_b = o.trunk_rows_max_b
         # learner data-gradient chain dy3 -> dy2 -> dy1 as ONE per-sample kernel (cnn_trunk_bwd; bias gradients as
         # per-sample partial rows reduced by the gradient finaliser) instead of two transposed-conv GEMMs
-        self.fused_bwd = implicit and os.environ.get("ACA_FUSED_BWD", "1") != "0"
+        self.fused_bwd = implicit and o.fused_bwd
         self.fin_parts = torch.zeros(256, dtype=torch.float32, device=flat.data.device)
         # A2C head in one launch (head_bwd: loss + dz + dh + dWh + dbh + dbfc, no GEMMs) for categorical heads of up
         # to 7 actions and learner batches up to 1024 rows
-        self.fused_head = os.environ.get("ACA_FUSED_HEAD", "1") != "0"
+        self.fused_head = o.fused_head
         # A2C head v2 (loss.hip a2c_head_kernel): bootstrap value + returns + loss + head backward in one launch of 32
-        # narrow workgroups (ACA_A2C_HEAD=0: fc_value + the 8-workgroup head_bwd kernel of round 2)
-        self.a2c_head = os.environ.get("ACA_A2C_HEAD", "1") != "0"
+        # narrow workgroups (off: fc_value + the 8-workgroup head_bwd kernel of round 2)
+        self.a2c_head = o.a2c_head
         self._a2c_bar = None
         # A2C learner on ONE stream with grouped GEMM launches instead of a side stream joined by events
-        self.grouped = os.environ.get("ACA_GROUPED", "1") != "0"
+        self.grouped = o.grouped
         # conv weight gradients as split-K partial planes reduced in plane order by the finaliser (deterministic);
-        # 0: split-K fp32 atomics into the slab (nondeterministic summation order)
-        self.det_wgrad = implicit and os.environ.get("ACA_DET_WGRAD", "1") != "0"
-        self.wgrad_planes = int(os.environ.get("ACA_WGRAD_PLANES", "64"))
+        # off: split-K fp32 atomics into the slab (nondeterministic summation order)
+        self.det_wgrad = implicit and o.det_wgrad
+        self.wgrad_planes = o.wgrad_planes
         # conv1 weight gradient by the per-sample kernel (conv_wgrad.hip: frames + dy1 staged once per sample) instead
         # of the implicit-im2col GEMM, from this many learner rows up
-        self.conv1_wgrad_min_b = int(os.environ.get("ACA_CONV1_WGRAD_MIN_B", "1024"))
-        self.conv1_planes = int(os.environ.get("ACA_CONV1_PLANES", "128"))
-        # conv2 / conv3 weight gradients by the per-sample NHWC kernel (conv_wgrad.hip) from this many rows up
-        self.nhwc_wgrad_min_b = int(os.environ.get("ACA_NHWC_WGRAD_MIN_B", "1024"))
-        self.wgrad_gemm = os.environ.get("ACA_WGRAD_GEMM", "1") != "0"
+        self.conv1_wgrad_min_b = o.conv1_wgrad_min_b
+        self.conv1_planes = o.conv1_planes
+        # conv2 / conv3 weight gradients by the batched-position MFMA kernel (wgrad_gemm) or the per-sample NHWC
+        # kernel (conv_wgrad.hip) from this many rows up; one workgroup per plane: 256 planes cover the CUs
+        self.nhwc_wgrad_min_b = o.nhwc_wgrad_min_b
+        self.wgrad_gemm = o.wgrad_gemm
+        self.nhwc_planes = o.nhwc_planes
+        self.nhwc3_planes = o.nhwc_planes
         # large-batch backward on ONE stream (Breakout PPO 18.3 -> 17.0 ms per update, profiles/r3_breakout_ab.txt)
-        self.serial_bwd = os.environ.get("ACA_SERIAL_BWD", "1") == "1"
-        self.serial_bwd_min_b = int(os.environ.get("ACA_SERIAL_BWD_MIN_B", "1024"))
-        self.nhwc3_wgrad_min_b = int(os.environ.get("ACA_NHWC3_WGRAD_MIN_B", str(self.nhwc_wgrad_min_b)))
-        # (the batched-position kernel's grid is one workgroup per plane: 256 planes cover the CUs)
-        self.nhwc_planes = int(os.environ.get("ACA_NHWC_PLANES",
-                                              "256" if os.environ.get("ACA_WGRAD_GEMM", "1") != "0" else "128"))
-        # conv3's per-sample work is small (2 k-steps x 12 column tiles), so its grid (3 workgroups per plane) needs
-        # more planes than conv2 to cover the CUs
-        self.nhwc3_planes = int(os.environ.get("ACA_NHWC3_PLANES", "256"))
+        self.serial_bwd_min_b = o.serial_bwd_min_b
         # fused trunk backward as a persistent kernel (weights in registers, one workgroup per CU walking the samples)
         # from this many learner rows up
-        self.trunk_bwd_persist_min_b = int(os.environ.get("ACA_TRUNK_BWD_PERSIST_MIN_B", "1024"))
-        self.trunk_bwd_persist = int(os.environ.get("ACA_TRUNK_BWD_PERSIST", "256"))
+        self.trunk_bwd_persist_min_b = o.trunk_bwd_persist_min_b
+        self.trunk_bwd_persist = o.trunk_bwd_persist
         self._planes = {}
         self._wsplits = {}
         self._cur_planes = {}
         self._fin_words = {}
         # rollout fc product left as split-K partial planes, reduced by its consumer kernel (no in-launch fence)
-        self.fc_parts = os.environ.get("ACA_FC_PARTS", "1") != "0"
+        self.fc_parts = True
         # split-K planes the fc GEMM may use (more planes: more workgroups stream Wfc, more for the consumer to sum)
-        self.fc_max_planes = min(FC_PLANES, int(os.environ.get("ACA_FC_MAX_PLANES", "32")))
+        self.fc_max_planes = min(FC_PLANES, o.fc_max_planes)
         self._hpart = {}
         self.last_fc = None
-        # fc fold (cnn_fused.hip FcFold, opt-in): the rollout's fc product computed inside the row-split trunk launch
-        # as 7 partial planes by 16 helper workgroups per conv3 row (no fc GEMM launch per rollout step); 16 or 32
-        # envs. The fused step reads one plane buffer and writes the other (ping-pong). Measured SLOWER on the
-        # headline (0.206 vs 0.193 ms per update, profiles/r3_bench_fc_fold_ab.txt): the in-launch hand-off chain
-        # (publish, fan-in wait, cross-XCD payload reads) costs ~7.5 us per launch against the 5 us GEMM it removes.
-        self.fc_fold = os.environ.get("ACA_FC_FOLD", "0") == "1"
-        self._hpart2 = {}
-        self._fold_cnt = None
         self.model = model
         self.flat = flat
         self.shadow = shadow
@@ -218,35 +197,21 @@ class CNNEngine:
                workspace=self.ws)
         return out
 
-    FOLD_PLANES = 7
+    def a2c_head_timed_out(self):
+        """True if an ``a2c_head`` launch's bounded in-launch hand-off ever gave up waiting (word 2 of its barrier
+        block, sticky): V(s_T) may then have been read before it was written, so the returns, advantages and
+        gradients of that update are wrong. One host read (syncs); the trainer checks it at log / checkpoint time
+        and after the capture warm-up."""
+        return self._a2c_bar is not None and int(self._a2c_bar[2]) != 0
 
-    def fold_ok(self, B):
-        """The row-split trunk of ``B`` observations can also compute their fc product (the launch's 7 B workgroups
-        must be co-resident: 16 or 32 envs; the launcher re-checks the occupancy and refuses otherwise)."""
-        return (self.fc_fold and self.implicit and self.fc_parts and B in (16, 32) and self.trunk_mode in (1, 2)
-                and B <= min(self.trunk_rows_max_b, self.fused_trunk_max_b))
-
-    def fold_args(self, B, parity=0):
-        """(Wfc shadow, plane buffer ``parity``, counters) for a folded trunk launch; sets :attr:`last_fc`."""
-        if self._fold_cnt is None:
-            self._fold_cnt = torch.zeros(16, dtype=torch.int32, device=self.dev)
-        if parity:
-            if B not in self._hpart2:
-                self._hpart2[B] = torch.zeros(FC_PLANES * B * 512, dtype=torch.float32, device=self.dev)
-            hp = self._hpart2[B]
-        else:
-            hp = self.hpart(B)
-        self.last_fc = (hp, self.FOLD_PLANES)
-        return self.sWfc, hp, self._fold_cnt
-
-    def fold_timed_out(self):
-        """True if a folded launch's helpers ever gave up waiting (counter word 15; the planes are then wrong)."""
-        return self._fold_cnt is not None and int(self._fold_cnt[15]) != 0
+    def health_errors(self):
+        """Names of the in-launch hand-offs that timed out since the engine was built (empty = healthy)."""
+        return ["a2c_head bootstrap-value hand-off"] if self.a2c_head_timed_out() else []
 
     def fused_step_ok(self, B):
         """The rollout step can run as ONE launch of policy/env + the next observation's row-split trunk."""
-        return (self.implicit and self.fc_parts and self.trunk_shift and self.trunk_mode in (1, 2)
-                and B <= min(self.trunk_rows_max_b, self.fused_trunk_max_b) and 2 <= self.A <= 6 and os.environ.get("ACA_FUSED_STEP", "1") != "0")
+        return (self.opts.fused_step and self.implicit and B <= min(self.trunk_rows_max_b, self.fused_trunk_max_b)
+                and 2 <= self.A <= 6)
 
     def fc_planes(self, b: _Bufs):
         """fc product of ``b.y3`` as split-K partial planes (consumed by the fused step / value kernels)."""
@@ -259,10 +224,10 @@ class CNNEngine:
     def obs_index_ok(self, B):
         """A learner batch of ``B`` rows can read its observations through an index (PPO minibatch gathered by
         index, ``mb_gather`` index mode): the per-env lean-LDS trunk kernel and the per-sample conv1 weight-gradient
-        kernel are the only readers of the frames then (ACA_MB_INDEX=0: copy the minibatch's observations)."""
-        return (os.environ.get("ACA_MB_INDEX", "1") != "0" and self.implicit and self.det_wgrad
-                and B <= self.fused_trunk_max_b and B > self.trunk_rows_max_b and self.trunk_mode_large == 0
-                and B >= self.conv1_wgrad_min_b and os.environ.get("ACA_TRUNK_FWD_U8", "1") != "0")
+        kernel are the only readers of the frames then (``EngineOpts.mb_index`` off: copy the minibatch's
+        observations)."""
+        return (self.opts.mb_index and self.implicit and self.det_wgrad and B <= self.fused_trunk_max_b
+                and B > self.trunk_rows_max_b and B >= self.conv1_wgrad_min_b)
 
     def forward(self, obs, b: _Bufs, head=True, shift_out=None, fc_parts=False, obs_idx=None):
         """obs uint8 [B, 4, 84, 84] -> b.z fp32 [B, A+1] (logits | value); ``head=False`` stops at ``b.h`` (the
@@ -276,15 +241,10 @@ class CNNEngine:
         shifted = False
         want_shift = shift_out is not None
         if self.implicit and B <= self.fused_trunk_max_b:
-            if not self.trunk_shift:
-                shift_out = None
-            fold = self.fold_args(B) if (fc_parts and not head and self.fold_ok(B)) else None
             G.cnn_trunk_fwd(obs, self.sW1, self.b1, self.sW2, self.b2, self.sW3, self.b3, b.y1, b.y2, b.y3,
-                            shift_out=shift_out, mode=self.trunk_mode if B <= self.trunk_rows_max_b else self.trunk_mode_large,
-                            fold=fold, obs_idx=obs_idx)
+                            shift_out=shift_out, mode=self.trunk_mode if B <= self.trunk_rows_max_b else 0,
+                            obs_idx=obs_idx)
             shifted = shift_out is not None
-            if fold is not None:   # the fc product is already in the planes (last_fc set by fold_args)
-                return shifted if want_shift else b.z
         elif self.implicit:
             G.gemm(obs, 0, True, self.sW1, 256, True, b.y1, 32, 1, B * 400, 32, 256, bias=self.b1, relu=True,
                    workspace=ws, ga=[1, B, 4, 84, 84, 8, 8, 4], ga_scale=1.0 / 255.0)
@@ -313,17 +273,9 @@ class CNNEngine:
         G.gemm(b.y3, 3136, True, self.sWfc, 512, False, b.h, 512, 1, B, 512, 3136, bias=self.bfc, relu=True,
                workspace=ws)
         if head:
-            if self.head_fwd_ok(B):   # large learner batches: dedicated N = A + 1 kernel (heads.hip head_fwd)
-                _native.require().head_fwd(b.h, self.sWh, self.bh, b.z)
-            else:
-                G.gemm(b.h, 512, True, self.sWh, self.A1, False, b.z, self.A1, 0, B, self.A1, 512, bias=self.bh,
-                       workspace=ws)
+            G.gemm(b.h, 512, True, self.sWh, self.A1, False, b.z, self.A1, 0, B, self.A1, 512, bias=self.bh,
+                   workspace=ws)
         return shifted if want_shift else b.z
-
-    def head_fwd_ok(self, B):
-        """z = h Wh + bh by ``head_fwd`` (8 lanes per row, Wh in LDS) instead of the generic GEMM, whose few
-        workgroups walk every k-step of the unaligned [512, A+1] operand (~15 us at B = 4096)."""
-        return self.dev.type == "cuda" and 2 <= self.A1 <= 8 and B >= self.head_fwd_min_b
 
     # ------------------------------------------------------------------------------------------------ backward
     def tail_bucket(self):
@@ -360,7 +312,7 @@ class CNNEngine:
 
     def _wgrad_conv23(self, name, b, ws2):
         B = b.B
-        min_b = self.nhwc_wgrad_min_b if name == "W2" else self.nhwc3_wgrad_min_b
+        min_b = self.nhwc_wgrad_min_b
         if not (self.det_wgrad and self.implicit and B >= min_b):
             if name == "W2":
                 self._wgrad("W2", self.gW2, b.dy2, 64, b.y1, 0, 64, 512, B * 81, ws2, [2, B, 32, 20, 20, 4, 4, 2])
@@ -373,7 +325,7 @@ class CNNEngine:
         if buf is None or buf.numel() < P * 64 * n:
             buf = torch.zeros(max(P, self.wgrad_planes) * 64 * n, dtype=torch.float32, device=self.dev)
             self._planes[name] = buf
-        # batched-position MFMA 32x32x16 kernel (default) or the per-sample kernel (ACA_WGRAD_GEMM=0)
+        # batched-position MFMA 32x32x16 kernel (default) or the per-sample kernel (EngineOpts.wgrad_gemm off)
         fn = _native.require().conv_wgrad_gemm if self.wgrad_gemm else _native.require().conv_wgrad_nhwc
         if name == "W2":
             fn(2, b.y1, b.dy2, buf, P)
@@ -445,7 +397,7 @@ class CNNEngine:
         main = torch.cuda.current_stream(self.dev)
         # serial_bwd: the weight-gradient products run on the compute stream too (large batches: the persistent
         # trunk backward holds every CU, and a side-stream product beside it only waits for LDS room)
-        side = main if (self.serial_bwd and b.B >= self.serial_bwd_min_b) else self.side
+        side = main if b.B >= self.serial_bwd_min_b else self.side
         ev = self._ev
         ws2 = self._side_ws()
         grouped = self.grouped and (head_done or stage == "trunk") and self.fused_bwd and self.det_wgrad
@@ -553,20 +505,6 @@ class CNNEngine:
 
     # ------------------------------------------------------------------------------------------------ finaliser
     want_parts = False   # set by the trainer when the optimiser may take the finaliser's sum-of-squares partials
-    defer_finalize = False   # set by the trainer: the finaliser runs inside the optimiser's launch (grad_finalize_opt)
-    _fin_pending = None
-
-    def take_finalize(self):
-        """The deferred finaliser job table (words, largest job) of the last backward, or None."""
-        p, self._fin_pending = self._fin_pending, None
-        return p
-
-    def flush_finalize(self):
-        """Runs a deferred finaliser as its own launch (the gradient slab is needed before an optimiser step:
-        data parallelism, the async-PS push, or a fused launch that was refused)."""
-        p = self.take_finalize()
-        if p is not None:
-            _native.require().grad_finalize(p[0], self.fin_parts)
 
     def finalize(self, b: _Bufs):
         """One launch after the backward (``grad_finalize``): reduces the per-sample conv bias-gradient rows
@@ -596,9 +534,6 @@ class CNNEngine:
             from ..ops.optim import finalize_jobs
             words = finalize_jobs(segs, self.dev, return_max=True)
             self._fin_words[key] = words
-        if self.defer_finalize:
-            self._fin_pending = words
-            return
         _native.require().grad_finalize(words[0], self.fin_parts)
 
     @staticmethod

@@ -144,7 +144,7 @@ class ActorCriticTrainer:
             from .engine import CNNEngine
             self.shadow = torch.empty(self.flat.numel, dtype=torch.bfloat16, device=self.device)
             self.shadow.copy_(self.flat.data)
-            self.engine = CNNEngine(self.model, self.flat, self.shadow)
+            self.engine = CNNEngine(self.model, self.flat, self.shadow, opts=cfg.engine_opts)
         self.opts = {}
         for g in self.flat.groups:
             s, e = self.flat.groups[g]
@@ -166,10 +166,6 @@ class ActorCriticTrainer:
             self.engine.want_parts = True
             for o in self.opts.values():
                 o.ext_parts = self.engine.fin_parts
-            # opt-in: the finaliser inside the optimiser's launch (grad_finalize_opt). Measured on the headline
-            # update it is SLOWER (0.227 vs 0.199 ms per update, profiles/r3_bench_finopt_ab.txt): the in-launch grid
-            # barrier of 256 workgroups costs more than the kernel boundary and the slab pass it removes
-            self.engine.defer_finalize = os.environ.get("ACA_FUSED_FINOPT", "0") == "1"
         T, N = cfg.n_steps, self.env.num_envs
         act_shape = () if self.env.is_discrete else tuple(self.env.action_space.shape)
         act_dtype = torch.int32 if self.env.is_discrete else torch.float32
@@ -351,18 +347,15 @@ class ActorCriticTrainer:
             cur = rows(t)
             nxt = rows(t + 1) if t + 1 < T else b
             sn, tn, tgn, ern = env.next_state()
-            # fc fold: this launch also computes obs_{t+1}'s fc planes, into the other plane buffer
-            fold = eng.fold_args(N, (t + 1) % 2) if eng.fold_ok(N) else (None, None, None)
             ops.pong_fused_step(cur.h, eng.sWh, eng.bh, cur.z, st.actions[t], st.logp[t], st.entropy[t],
                                 st.values[t], KEY_ENV_BITS, self.policy_seed, env.state, env.t, env.tg, env.ep_ret,
                                 sn, tn, tgn, ern, env.ep_stats, env.env_ids, st.obs[t], st.obs[t + 1],
                                 st.rewards[t], st.dones[t], st.truncated[t], env.seed, env.max_episode_steps, hp, S,
                                 eng.bfc, eng.sW1, eng.b1, eng.sW2, eng.b2, eng.sW3, eng.b3, nxt.y1, nxt.y2, nxt.y3,
-                                1.0 / 255.0, st.obs[t + 2] if t + 2 <= T else None, None, *fold)
+                                1.0 / 255.0, st.obs[t + 2] if t + 2 <= T else None, None)
             env.flip()
             nxt.obs = st.obs[t + 1]
-            if fold[0] is None:
-                eng.fc_planes(nxt)
+            eng.fc_planes(nxt)
         hp, S = eng.last_fc
         self._env_flips = T
         if self._boot_in_head():
@@ -514,8 +507,6 @@ class ActorCriticTrainer:
         """All-reduce (DP) + optimiser step; inside a segmented capture the pre-graph stops before both."""
         if self._defer_allreduce:
             return
-        if self.engine is not None and (self._grad_sink is not None or self.dp is not None):
-            self.engine.flush_finalize()   # the slab itself is pushed / all-reduced
         if self._grad_sink is not None:   # async PS worker (a3c_gpu): push the gradient, pull the parameters
             self._comm(self._grad_sink)
             self._after_pull()
@@ -531,11 +522,6 @@ class ActorCriticTrainer:
         """Optimiser step(s). Several groups (the reference's separate actor / critic Adam) run as ONE launch, which
         also writes the MLP engine's transposed weight shadows; otherwise one launch per group (+ a shadow pass)."""
         opts = list(self.opts.values())
-        pend = self.engine.take_finalize() if self.engine is not None else None
-        if pend is not None:
-            if len(opts) == 1 and opts[0].step_finalize(pend[0], pend[1], self.engine.fin_parts):
-                return
-            _native.require().grad_finalize(pend[0], self.engine.fin_parts)
         if len(opts) > 1 and _native.use_native(self.flat.data):
             from ..ops.optim import FusedGroupStep
             if not hasattr(self, "_group_step"):
@@ -632,29 +618,13 @@ class ActorCriticTrainer:
             self.lr_ctrl.update_(self.actor_opt.lr, kl)
 
     # ------------------------------------------------------------------ learning (native MLP engine)
-    def _mlp_fused_opt(self):
-        """Opt-in (ACA_MLP_FUSED_OPT=1): Adam folded into the MLP weight-gradient launch (one launch per minibatch
-        instead of two) on a single device with the reference's actor / critic Adam pair. Measured SLOWER on the
-        MuJoCo-shape PPO update (16.3 vs 14.1 ms, profiles/r3_mujoco_fused_adam_ab.txt): the in-launch grid barrier
-        over ~360 workgroups costs more than the kernel boundary and the optimiser launch it removes."""
-        if self.dp is not None or self._grad_sink is not None or self._defer_allreduce:
-            return None
-        if not hasattr(self, "_mfo"):
-            self._mfo = None
-            if os.environ.get("ACA_MLP_FUSED_OPT", "0") == "1" and list(self.opts) == ["actor", "critic"]:
-                self._mfo = self.mlp.fused_adam_words(self.opts["actor"], self.opts["critic"])
-        return self._mfo
-
     def _mlp_step(self, eng, B, idx, obs, actions, logp_old, adv, ret, v_old, perm=None, bump=None):
         cfg = self.cfg
         ppo = cfg.algo == "ppo"
-        fo = self._mlp_fused_opt()
         used = eng.train(obs, actions, logp_old, adv, ret, self.ent_coef, self.kl_coef, B, idx=idx, perm=perm, bump=bump,
                          v_old=v_old if ppo else None, vf_coef=1.0, ppo=ppo, ppo_clip=cfg.ppo_clip if ppo else 0.0,
                          v_clip=(cfg.ppo_value_clip or 0.0) if ppo else 0.0, stats=self.stats_buf,
-                         clips=(cfg.clip_value, cfg.critic_clip_value), want_parts=self.dp is None, fused_opt=fo)
-        if fo is not None:
-            return   # the weight-gradient launch applied both Adam steps and wrote the transposed shadows
+                         clips=(cfg.clip_value, cfg.critic_clip_value), want_parts=self.dp is None)
         for t, g in enumerate(("actor", "critic")):
             self.opts[g].ext_parts = eng.parts[t] if used else None
         self._apply_grads()
@@ -888,6 +858,7 @@ class ActorCriticTrainer:
                 self.update_body()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
+        self.check_health()
         st = self.storage
         if st.ring:
             # one graph set per ring phase (their slot addresses differ); capturing runs nothing, and each set
@@ -1044,17 +1015,30 @@ class ActorCriticTrainer:
             self._comm_grad.zero_()
             self._comm_work = None
 
-    def log(self, i, print_tog):
+    def log(self, i, print_tog, ep_stats=None):
+        """One Logger row. ``ep_stats`` = (mean return, episodes, mean length) already drained by the caller (the
+        async worker shares one drain between its consumers); else the env bank's counters are drained here."""
         if self.logger is None:
             return None
+        self.check_health()
         vals = self.stats_buf.detach().cpu().tolist()
         s = {k: vals[STAT_KEYS.index(k)] for k in LOG_KEYS}
-        avg_rew, n_ep, ep_len = self.env.drain_episode_stats()
+        avg_rew, n_ep, ep_len = ep_stats if ep_stats is not None else self.env.drain_episode_stats()
         self.logger(i, act_loss=s["act_loss"], circ_loss=math.sqrt(max(s["crit_loss"], 0.0)), kl_dist=s["kl"],
                     avg_rew=avg_rew, print_tog=print_tog, act_lr=self.actor_opt.get_lr(), avg_ent=s["entropy"],
                     worker_id=self.worker_id, ev_before=s["ev_before"], ev_after=s["ev_after"])
         s.update(avg_rew=avg_rew, episodes=n_ep, ep_len=ep_len)
         return s
+
+    def check_health(self):
+        """Raises if a native in-launch hand-off timed out (its outputs, and so this update's gradients, would be
+        corrupt). One host read; called at log / checkpoint time, after the capture warm-up and at the end of
+        ``train``."""
+        if self.engine is not None:
+            errs = self.engine.health_errors()
+            if errs:
+                raise RuntimeError("native engine hand-off timed out (" + ", ".join(errs) + "): the affected "
+                                   "updates trained on incomplete data")
 
     def train(self, num_updates=None, callback=None):
         cfg = self.cfg
@@ -1087,10 +1071,12 @@ class ActorCriticTrainer:
             if callback is not None:
                 callback(self, it)
         self.flush_pending()
+        self.check_health()
         return history
 
     # ------------------------------------------------------------------ checkpoints
     def save_checkpoint(self, path=None):
+        self.check_health()
         from ..ckpt import save_trainer
         return save_trainer(self, path)
 

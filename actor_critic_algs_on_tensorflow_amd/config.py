@@ -11,6 +11,55 @@ from dataclasses import dataclass, field
 
 
 @dataclass
+class EngineOpts:
+    """Kernel selection of the native CNN engine (``algos/engine.py``). Every switch is a path that is tested and
+    measured (the A/B evidence sits next to each default in ``profiles/``); the defaults are the fastest measured
+    configuration on MI355X. ``TrainConfig.engine_opts`` carries one; plain dicts are accepted and converted."""
+    # -- rollout -------------------------------------------------------------------------------------------------
+    fused_step: bool = True           # Pong bank: policy/env step t fused with the row-split trunk of obs t+1
+    trunk_rows_max_b: int = 64        # row-split trunk (7 workgroups per env) up to this many envs, per-env above
+    trunk_late_w: bool = True         # row-split trunk: conv2/conv3 weight fragments requested after conv1's MFMAs
+    fc_max_planes: int = 32           # split-K partial planes of the rollout fc product (consumer-reduced)
+    # -- learner -------------------------------------------------------------------------------------------------
+    a2c_head: bool = True             # A2C: V(s_T) + returns + loss + head backward in one launch (loss.hip a2c_head)
+    fused_head: bool = True           # A2C: loss + head backward in one launch (round-2 head_bwd) when a2c_head is off
+    grouped: bool = True              # independent backward products as ONE grouped GEMM launch (no side stream)
+    det_wgrad: bool = True            # weight gradients as split-K planes reduced in fixed order (bitwise determinism)
+    fused_bwd: bool = True            # dy3 -> dy2 -> dy1 in one per-sample kernel (cnn_trunk_bwd)
+    mb_index: bool = True             # PPO minibatches read their observations in place through a row index
+    wgrad_gemm: bool = True           # conv2/conv3 weight gradients: batched-position MFMA kernel (else per-sample)
+    serial_bwd_min_b: int = 1024      # learner batches from this size run the backward on one stream
+    conv1_wgrad_min_b: int = 1024     # per-sample conv1 weight-gradient kernel from this many rows (else GEMM)
+    nhwc_wgrad_min_b: int = 1024      # conv2/conv3 weight-gradient kernels from this many rows (else GEMM)
+    trunk_bwd_persist_min_b: int = 1024   # persistent trunk backward (weights in registers) from this many rows
+    trunk_bwd_persist: int = 256      # its workgroups
+    wgrad_planes: int = 64            # split-K planes of the GEMM weight gradients
+    conv1_planes: int = 128           # planes of the per-sample conv1 weight gradient
+    nhwc_planes: int = 256            # planes of the conv2 / conv3 weight-gradient kernels
+
+    def replace(self, **kw):
+        return dataclasses.replace(self, **kw)
+
+
+# string-valued TrainConfig fields and the values they accept (validated in __post_init__)
+CHOICES = {
+    "algo": {"a2c", "ppo", "a3c", "basic_ac"},
+    "model": {"auto", "mlp", "cnn"},
+    "model_variant": {"basic", "a3c"},
+    "returns": {"nstep", "gae"},
+    "optimizer": {"adam", "rmsprop"},
+    "lr_schedule": {"constant", "linear"},
+    "dtype": {"bf16", "fp32"},
+    "engine": {"auto", "native", "torch"},
+    "dist_backend": {"auto", "nccl", "gloo"},
+    "overlap": {"strict", "lag1"},
+    "grad_bucket_dtype": {"fp32", "bf16"},
+    "dp_capture": {"auto", "segments"},
+    "mode": {"train", "debug", "debug-light", "debug-full"},
+}
+
+
+@dataclass
 class TrainConfig:
     # -- problem ---------------------------------------------------------------------------------------------
     env: str = "Pendulum-v0"
@@ -59,6 +108,7 @@ class TrainConfig:
     cuda_graph: bool = True
     reuse_rollout_acts: bool = True   # native A2C: the rollout's activations are the learner's forward (exact)
     fused_rollout: bool = True        # native MLP engine + MuJoCo-shaped bank: the whole rollout in one launch
+    engine_opts: EngineOpts = field(default_factory=EngineOpts)   # kernel selection of the native CNN engine
     total_updates: int = 1000
     # -- distributed -----------------------------------------------------------------------------------------------
     dist_backend: str = "auto"        # auto -> nccl (RCCL) on GPU, gloo on CPU
@@ -90,6 +140,17 @@ class TrainConfig:
     fault_inject: str | None = None   # "rank:iteration": that rank dies (os._exit) when it reaches that iteration
     resume: str | None = None         # "auto" = newest checkpoint in checkpoint_dir, or a checkpoint prefix
     dist_timeout_s: int = 300         # collective timeout: a dead peer surfaces as an exception, not a hang
+
+    def __post_init__(self):
+        for name, allowed in CHOICES.items():
+            v = getattr(self, name)
+            if v not in allowed:
+                raise ValueError(f"TrainConfig.{name}={v!r}: expected one of {sorted(allowed)}")
+        if self.lr_schedule == "linear" and self.kl_adaptive_lr:
+            raise ValueError("lr_schedule='linear' with kl_adaptive_lr=True: the KL controller owns the actor lr, so "
+                             "only the critic would decay; pick one")
+        if not isinstance(self.engine_opts, EngineOpts):
+            self.engine_opts = EngineOpts(**dict(self.engine_opts or {}))
 
     def replace(self, **kw):
         return dataclasses.replace(self, **kw)

@@ -97,7 +97,7 @@ _TUNED: dict = {}
 PARTIAL_MAX_SPLITS = 8   # out_mode 3: the consumer kernels reduce at most this many partial planes
 # with >= 2 row tiles the bias column sums go through per-tile partials + one ordered reduce (deterministic; one
 # tile row adds each column once, also deterministic)
-COLSUM_PART_MIN_TILES = int(os.environ.get("ACAMD_COLSUM_PART_MIN_TILES", "2"))
+COLSUM_PART_MIN_TILES = 2
 TUNE = os.environ.get("ACAMD_GEMM_TUNE", "1") == "1"
 
 
@@ -266,15 +266,6 @@ def gemm(A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha=1.0, bias=No
     reading operand A (k-contiguous) / B (n-contiguous) straight from the activation image ``A`` / ``B``.
     """
     ops = _native.require()
-    if _mfma32_ok(M, N, K, out_mode, colsum, ga, gb, tile, splits, _GROUP_DEPTH):
-        s32 = 1
-        if out_mode == 3:   # partial planes: split K while the grid is short of the CUs
-            tiles = -(-M // 128) * -(-N // 128)
-            while s32 * 2 <= max_planes and tiles * s32 < 256 and K % (64 * s32 * 2) == 0 and K // (s32 * 2) >= 512:
-                s32 *= 2
-        if ops.gemm_mfma32(A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, float(alpha), bias, bool(relu), mask,
-                           ldm, s32):
-            return s32
     if tile is None or splits is None or bk is None:
         key = (M, N, K, bool(a_k), bool(b_k), out_mode, lda % 8 == 0, ldb % 8 == 0, tuple(ga or ()), tuple(gb or ()),
                max_planes if out_mode == 3 else 0)
@@ -306,18 +297,6 @@ def gemm(A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha=1.0, bias=No
         raise ValueError("out_mode 3: more split-K planes than C holds (%d)" % max_planes)
     return _run(ops, A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha, bias, relu, mask, ldm, colsum,
                 colsum_mod, tile, bk, splits, workspace, ga, ga_scale, gb, gb_scale, stamps)
-
-
-# opt-in (ACAMD_GEMM32=1): large plain products on the 32x32x16-MFMA kernel (gemm_mfma32.hip) from this many MACs
-# up. Measured standalone at the PPO fc shapes it is 10-25 % SLOWER than the general kernel with its tuned plan
-# (profiles/r3_microbench_breakout_products.json: 45 / 58 / 58 us vs 41 / 47 / 46 us), so it is off by default.
-GEMM32 = os.environ.get("ACAMD_GEMM32", "0") == "1"
-GEMM32_MIN_MACS = int(os.environ.get("ACAMD_GEMM32_MIN_MACS", str(1 << 30)))
-
-
-def _mfma32_ok(M, N, K, out_mode, colsum, ga, gb, tile, splits, grouped):
-    return (GEMM32 and not grouped and tile is None and splits is None and not ga and not gb and colsum is None
-            and out_mode in (0, 1, 3) and M * N * K >= GEMM32_MIN_MACS and K % 64 == 0)
 
 
 def _view(t, rows, cols, ld, k_contig_rows):
@@ -369,16 +348,14 @@ def im2col_nhwc_ref(x, B, H, W, C, kh, kw, s):
 
 
 def cnn_trunk_fwd(obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale=1.0 / 255.0, shift_out=None, mode=1,
-                  copy_out=None, fold=None, obs_idx=None):
+                  copy_out=None, obs_idx=None):
     """Fused Nature-CNN conv1..conv3, activations through LDS (``cnn_fused.hip``). ``mode`` 1: seven workgroups per
     env, one per conv3 output row (its receptive field recomputed); 0: one workgroup per env.
     ``shift_out``: also write frames 1..3 of every observation as frames 0..2 of this buffer (frame-stack shift);
-    ``copy_out`` (mode 1): also copy the whole observation there. ``fold`` = (Wfc, planes, counters): the row
-    workgroups also compute the fc product as 7 partial planes (``FcFold``, 16 or 32 observations). ``obs_idx``
-    (int64 [B], mode 0): sample b is row ``obs_idx[b]`` of ``obs`` (a PPO minibatch gathered by index)."""
-    fw, fp, fc = fold if fold is not None else (None, None, None)
+    ``copy_out`` (mode 1): also copy the whole observation there. ``obs_idx`` (int64 [B], mode 0): sample b is row
+    ``obs_idx[b]`` of ``obs`` (a PPO minibatch gathered by index)."""
     _native.require().cnn_trunk_fwd(obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, float(scale), shift_out, None,
-                                    int(mode), copy_out, fw, fp, fc, obs_idx)
+                                    int(mode), copy_out, obs_idx)
 
 
 def col2im_nhwc(dcol, ymask, dx, colsum, B, H, W, C, kh, kw, s):

@@ -193,14 +193,12 @@ class MLPEngine:
 
     def train(self, obs, actions, logp_old, adv, ret, ent_coef, kl_coef, B, idx=None, v_old=None, vf_coef=1.0,
               ppo=False, ppo_clip=0.0, v_clip=0.0, stats=None, clips=(None, None), want_parts=True, perm=None,
-              bump=None, stamps=None, fused_opt=None):
+              bump=None, stamps=None):
         """One learner (mini)batch: rows ``idx`` / ``perm`` = (update_counter, epoch, offset, n, seed) -- the rows
         ``prp(offset + r)`` of the keyed permutation of ``[0, n)`` (envs/rng.py), computed in-kernel -- or the first
         ``B`` rows of the rollout -> gradients in the slab, statistics into ``stats[0:7]``, sums of squares into
         :attr:`parts` (when ``want_parts``). ``bump``: an int64 counter the weight-gradient launch advances by one
-        (the PPO update counter, after the update's last minibatch -- no separate launch). ``fused_opt`` = (int64[14],
-        float[5]) host words of :func:`fused_adam_words`: the weight-gradient launch also applies the actor / critic
-        Adam steps (``mlp_wgrad_adam_kernel``) -- no optimiser launch, the gradient never reaches the slab."""
+        (the PPO update counter, after the update's last minibatch -- no separate launch)."""
         ops = _native.require()
         self._fwd(2, obs, B, 0, 2, desc_B=B, idx=idx, perm=perm, act_in=actions, logp_old=logp_old, adv=adv, ret=ret,
                   v_old=v_old, ent_coef=ent_coef, kl_coef=kl_coef, vf_coef=vf_coef, ppo_clip=ppo_clip,
@@ -212,45 +210,8 @@ class MLPEngine:
         ops.mlp_wgrad(desc, 2, B, nsplit, self.items[0], self.items[1], self.parts[0] if use_parts else None,
                       self.parts[1] if use_parts else None, float(clips[0] or -1.0), float(clips[1] or -1.0),
                       self.g_log_std, self.A, self.mstats, st, ent_coef, kl_coef, self._mpart(B), (B + BM - 1) // BM,
-                      bump, *(fused_opt if fused_opt is not None else (None, None)))
+                      bump)
         return use_parts
-
-    def fused_adam_words(self, actor_opt, critic_opt):
-        """Host descriptor of the Adam steps folded into the weight-gradient launch, or None when the optimisers do not
-        qualify: two FusedAdam groups with equal betas / eps, no gradient multiplier or bf16 shadow, and every element
-        of the actor group a tower-0 weight / bias or the log-std, of the critic group a tower-1 weight / bias."""
-        from .optim import FusedAdam
-        a, c = actor_opt, critic_opt
-        if not (isinstance(a, FusedAdam) and isinstance(c, FusedAdam)):
-            return None
-        if (a.b1, a.b2, a.eps) != (c.b1, c.b2, c.eps) or a.grad_mul != 1.0 or c.grad_mul != 1.0:
-            return None
-        if a.shadow is not None or c.shadow is not None:
-            return None
-        for o, tw, extra in ((a, self.towers[0], self.log_std), (c, self.towers[1], None)):
-            # every tower weight / bias (+ the log-std) must lie in the group's segment. Other elements of the
-            # segment (slab alignment padding; the reference Basic_AC critic's unused third layer) never receive an
-            # engine gradient: with zero gradient and zero moments Adam leaves them unchanged, so skipping them matches
-            # the unfused optimiser exactly
-            lo, hi = o.p.data_ptr(), o.p.data_ptr() + 4 * o.p.numel()
-            for q in [t for lay in tw for t in (lay.kernel, lay.bias)] + ([extra] if extra is not None else []):
-                if not (lo <= q.data_ptr() and q.data_ptr() + 4 * q.numel() <= hi):
-                    return None
-        if not hasattr(self, "_fo_bar"):
-            # mlp.hip WGO_BAR_WORDS: sharded arrival counters, top counter, release flags, departures, timeout flag
-            self._fo_bar = torch.zeros(19 * 32, dtype=torch.int32, device=self.dev)
-        words = torch.tensor([a.p.data_ptr(), c.p.data_ptr(), a.m.data_ptr(), c.m.data_ptr(), a.v.data_ptr(),
-                              c.v.data_ptr(), a.lr.data_ptr(), c.lr.data_ptr(), a.t.data_ptr(), c.t.data_ptr(),
-                              a.gnorm.data_ptr(), c.gnorm.data_ptr(),
-                              self.log_std.data_ptr() if self.log_std is not None else 0, self._fo_bar.data_ptr()],
-                             dtype=torch.int64)
-        floats = torch.tensor([float(a.max_grad_norm) if a.max_grad_norm is not None else -1.0,
-                               float(c.max_grad_norm) if c.max_grad_norm is not None else -1.0,
-                               float(a.b1), float(a.b2), float(a.eps)], dtype=torch.float32)
-        return words, floats
-
-    def fused_opt_timed_out(self):
-        return hasattr(self, "_fo_bar") and int(self._fo_bar[18 * 32]) != 0
 
     # ------------------------------------------------------------------------------------------- fused rollout
     def supports_fused_rollout(self, env):

@@ -153,22 +153,6 @@ class FusedAdam:
         if self.shadow is not None:
             self.shadow.copy_(self.p)
 
-    def step_finalize(self, words, max_job_n, parts):
-        """Gradient finaliser + this update in ONE launch (``grad_finalize_opt``): the job table of the engine's
-        finaliser covers this group's whole slab range (single-group update, no data parallelism). Returns False
-        when the launch is not possible (the caller runs the finaliser and :meth:`step` instead)."""
-        if not _native.use_native(self.p) or self.clip_value is not None:
-            return False
-        if not hasattr(self, "_fin_state"):
-            self._fin_state = torch.zeros(4, dtype=torch.int32, device=self.p.device)
-        adam = not isinstance(self, FusedRMSprop)
-        b1, b2 = (self.b1, self.b2) if adam else (0.0, self.alpha)
-        return bool(_native.require().grad_finalize_opt(
-            words, int(max_job_n), parts, self.g, self.p, self.m if adam else None, self.v, self.shadow, self.lr,
-            self.t if adam else None, self.gnorm, -1.0,
-            float(self.max_grad_norm) if self.max_grad_norm is not None else -1.0, float(self.grad_mul), 1.0,
-            float(b1), float(b2), float(self.eps), adam, self._fin_state))
-
     def state_dict(self):
         return {"m": self.m, "v": self.v, "t": self.t, "lr": self.lr}
 

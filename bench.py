@@ -22,7 +22,12 @@ import time
 import torch
 
 METRIC = "env-steps/sec (whole node) A2C Atari-CNN 32 vec-envs/GPU at 1/2/4/8 MI355X"
-BASELINE_VALUE = None  # the reference publishes no number
+# The reference publishes no number. vs_baseline is taken against the MEASURED reference-style loop
+# (SURVEY §6.3): the same model and algorithm in the reference's architecture -- one env per process, batch-1
+# inference every step, CPU learner -- run with this repo's code (scripts/baseline_reference_loop.py,
+# profiles/r4_reference_style_baseline.jsonl, BASELINE.md "Measured reference-style baseline").
+BASELINE_VALUE = 63.08
+BASELINE_WHAT = "reference-style loop (1 env, batch-1 inference, CPU; this repo's code), 63.08 env-steps/s"
 
 
 def main():
@@ -87,7 +92,8 @@ def main():
             "ms_per_step": round(1000.0 * dt / args.steps, 4),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
+            "vs_baseline": round(value / BASELINE_VALUE, 1) if BASELINE_VALUE else None,
+            "baseline": BASELINE_WHAT,
             "dtype": "bf16",
             "data": "synthetic (Pong-shaped 84x84x4 uint8 env bank, random-init weights)",
             "config": {"model": "Nature-CNN actor-critic (3 conv + fc512, 1.69M params)",

@@ -29,7 +29,7 @@ ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
 KERNELS = ["env_classic", "env_atari", "heads", "returns", "optim", "gemm", "gemm_plain", "gemm_conv", "gemm_group",
-           "gemm_mfma32", "conv", "conv_wgrad",
+           "conv", "conv_wgrad",
            "loss", "cnn_fused", "mlp"]
 # env kernels must round exactly like the PyTorch oracles: no fma contraction
 NO_CONTRACT = {"env_classic", "env_atari"}

@@ -50,7 +50,7 @@ hipError_t aca_pong_fused_step(uint16_t*, const float*, int, int64_t, const floa
                                float*, float*, int32_t*, int64_t*, float*, float*, const int64_t*, const uint8_t*,
                                uint8_t*, float*, uint8_t*, uint8_t*, uint32_t, int, const uint16_t*, const float*,
                                const uint16_t*, const float*, const uint16_t*, const float*, uint16_t*, uint16_t*,
-                               uint16_t*, float, uint8_t*, uint64_t*, int, const uint16_t*, float*, unsigned int*, hipStream_t);
+                               uint16_t*, float, uint8_t*, uint64_t*, int, hipStream_t);
 hipError_t aca_categorical_sample(const float*, int, int, int, const int64_t*, const int64_t*, const int64_t*, int,
                                   uint32_t, int32_t*, float*, float*, float*, hipStream_t);
 hipError_t aca_ev(const float*, const float*, float*, int, hipStream_t);
@@ -73,7 +73,6 @@ hipError_t aca_ev_multi(const float*, const float*, float*, int, double*, unsign
 hipError_t aca_conv1_wgrad(const uint8_t*, const uint16_t*, float*, int, int, float, const int64_t*, hipStream_t);
 hipError_t aca_conv_wgrad_nhwc(int, const uint16_t*, const uint16_t*, float*, int, int, hipStream_t);
 hipError_t aca_conv_wgrad_gemm(int, const uint16_t*, const uint16_t*, float*, int, int, hipStream_t);
-hipError_t aca_gemm_mfma32(const AcaGemmDesc*, hipStream_t);
 hipError_t aca_sumsq(const float*, size_t, float*, hipStream_t);
 int aca_sumsq_parts();
 hipError_t aca_adam_step(float*, float*, float*, float*, size_t, const float*, float*, const float*, float*, uint16_t*,
@@ -91,7 +90,6 @@ hipError_t aca_im2col_nhwc(const uint16_t*, uint16_t*, int, int, int, int, int, 
 hipError_t aca_col2im_nhwc(const uint16_t*, const uint16_t*, uint16_t*, float*, int, int, int, int, int, int, int,
                            hipStream_t);
 hipError_t aca_colsum_bf16(const uint16_t*, int64_t, int, int64_t, float*, hipStream_t);
-hipError_t aca_head_fwd(const uint16_t*, const uint16_t*, const float*, float*, int, int, hipStream_t);
 hipError_t aca_ac_loss(const float*, int64_t, const float*, int64_t, const int32_t*, const float*, const float*,
                        const float*, const float*, const float*, const float*, const float*, const float*, float, float,
                        float, uint16_t*, int64_t, uint16_t*, int64_t, float*, float*, int, int, int, int,
@@ -101,9 +99,6 @@ hipError_t aca_cnn_trunk_fwd(const uint8_t*, const uint16_t*, const float*, cons
                              const uint16_t*, const float*, uint16_t*, uint16_t*, uint16_t*, int, float, uint8_t*,
                              uint64_t*, const int64_t*, hipStream_t);
 hipError_t aca_grad_finalize(const int64_t*, int, float*, hipStream_t);
-hipError_t aca_grad_finalize_opt(const int64_t*, int, int, float*, float*, float*, float*, uint16_t*, const float*,
-                                 const float*, float*, float*, float, float, float, float, float, float, float, int,
-                                 unsigned int*, hipStream_t);
 hipError_t aca_head_bwd(const float*, const int32_t*, const float*, const float*, const float*, float, const float*,
                         const float*, const uint8_t*, int, int, int, int, int, float, float, float*, float*,
                         const uint16_t*, const uint16_t*, uint16_t*, float*, float*, float*, float*, int,
@@ -116,7 +111,7 @@ hipError_t aca_cnn_trunk_bwd(const uint16_t*, const uint16_t*, const uint16_t*, 
                              uint16_t*, uint16_t*, float*, int, uint64_t*, int, hipStream_t);
 hipError_t aca_cnn_trunk_rows(const uint8_t*, const uint16_t*, const float*, const uint16_t*, const float*,
                               const uint16_t*, const float*, uint16_t*, uint16_t*, uint16_t*, int, float, uint8_t*,
-                              uint8_t*, uint64_t*, int, const uint16_t*, float*, unsigned int*, hipStream_t);
+                              uint8_t*, uint64_t*, int, hipStream_t);
 }
 
 namespace {
@@ -299,30 +294,6 @@ void env_policy_step_pong(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, 
         "env_policy_step_pong");
 }
 
-// fc fold operands (cnn_fused.hip FcFold): bf16 Wfc [3136, 512], fp32 planes >= 7 x [N, 512], int32 counters [16]
-struct FoldPtrs {
-  const uint16_t* w = nullptr;
-  float* planes = nullptr;
-  unsigned int* cnt = nullptr;
-};
-FoldPtrs fold_ptrs(const c10::optional<Tensor>& w, const c10::optional<Tensor>& planes,
-                   const c10::optional<Tensor>& cnt, int64_t N, const char* what) {
-  FoldPtrs f;
-  if (!(cnt.has_value() && cnt->defined())) return f;
-  TORCH_CHECK(w.has_value() && w->defined() && planes.has_value() && planes->defined(), what,
-              ": the fc fold needs fold_w, fold_planes and fold_cnt");
-  need(*w, at::kBFloat16, "fold_w");
-  need(*planes, at::kFloat, "fold_planes");
-  need(*cnt, at::kInt, "fold_cnt");
-  TORCH_CHECK(w->numel() == 3136 * 512 && planes->numel() >= 7 * N * 512 && cnt->numel() >= 16 &&
-                  reinterpret_cast<uintptr_t>(w->data_ptr()) % 16 == 0,
-              what, ": fold shapes (Wfc [3136, 512], planes >= 7 x [N, 512], 16 counter words)");
-  f.w = ptr<uint16_t>(*w);
-  f.planes = ptr<float>(*planes);
-  f.cnt = reinterpret_cast<unsigned int*>(cnt->data_ptr<int32_t>());
-  return f;
-}
-
 // Rollout step t of the Pong bank fused with the row-split trunk of the observation it produces (cnn_fused.hip
 // pong_fused_step_kernel): env state read from (state, t, tg, ep_ret), committed to the other parity buffers
 // (state_n, t_n, tg_n, ep_ret_n); prev = obs[t], out = obs[t+1] (frames 0..2 already shifted in), shift_out =
@@ -333,8 +304,7 @@ void pong_fused_step(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, Tenso
                      Tensor prev, Tensor out, Tensor reward, Tensor done, Tensor trunc, int64_t seed,
                      int64_t max_steps, Tensor hpart, int64_t planes, Tensor bfc, Tensor W1, Tensor b1, Tensor W2,
                      Tensor b2, Tensor W3, Tensor b3, Tensor y1, Tensor y2, Tensor y3, double scale,
-                     c10::optional<Tensor> shift_out, c10::optional<Tensor> stamps, c10::optional<Tensor> fold_w,
-                     c10::optional<Tensor> fold_planes, c10::optional<Tensor> fold_cnt) {
+                     c10::optional<Tensor> shift_out, c10::optional<Tensor> stamps) {
   check_env(state, t, tg, ep_ret, ep_stats, ids, reward, done, trunc);
   check_env(state_n, t_n, tg_n, ep_ret_n, ep_stats, ids, reward, done, trunc);
   for (auto* x : {&h, &Wh, &W1, &W2, &W3, &y1, &y2, &y3}) need(*x, at::kBFloat16, "pong_fused_step bf16");
@@ -370,7 +340,6 @@ void pong_fused_step(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, Tenso
                     shift_out->data_ptr() != out.data_ptr(), "pong_fused_step: shift_out shape / aliasing");
     so = shift_out->data_ptr<uint8_t>();
   }
-  const FoldPtrs ff = fold_ptrs(fold_w, fold_planes, fold_cnt, N, "pong_fused_step");
   check(aca_pong_fused_step(ptr<uint16_t>(h), ptr<float>(hpart), (int)planes, pstride, ptr<float>(bfc),
                             ptr<uint16_t>(Wh), ptr<float>(bh), A, ptr<float>(z), ptr<int32_t>(act), ptr<float>(logp),
                             ptr<float>(ent), ptr<float>(value), (int)key_shift, (uint32_t)pseed, ptr<float>(state),
@@ -380,7 +349,7 @@ void pong_fused_step(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, Tenso
                             ptr<uint8_t>(done), ptr<uint8_t>(trunc), (uint32_t)seed, (int)max_steps,
                             ptr<uint16_t>(W1), ptr<float>(b1), ptr<uint16_t>(W2), ptr<float>(b2), ptr<uint16_t>(W3),
                             ptr<float>(b3), ptr<uint16_t>(y1), ptr<uint16_t>(y2), ptr<uint16_t>(y3), (float)scale,
-                            so, stamps_ptr(stamps, N * 7), N, ff.w, ff.planes, ff.cnt, cur_stream(state)),
+                            so, stamps_ptr(stamps, N * 7), N, cur_stream(state)),
         "pong_fused_step");
 }
 
@@ -862,36 +831,9 @@ void mlp_wgrad(Tensor desc, int64_t ntw, int64_t B, int64_t nsplit, int64_t item
                c10::optional<Tensor> parts0, c10::optional<Tensor> parts1, double clip0, double clip1,
                c10::optional<Tensor> g_log_std, int64_t A, c10::optional<Tensor> mstats, c10::optional<Tensor> stats,
                c10::optional<Tensor> ent_coef, c10::optional<Tensor> kl_coef, c10::optional<Tensor> mpart,
-               int64_t mpart_rows, c10::optional<Tensor> bump, c10::optional<Tensor> opt_words,
-               c10::optional<Tensor> opt_floats) {
+               int64_t mpart_rows, c10::optional<Tensor> bump) {
   need(desc, at::kLong, "desc");
   aca::WgradArgs a{};
-  if (opt_words.has_value() && opt_words->defined()) {
-    // Adam folded into the launch (mlp.hip mlp_wgrad_adam_kernel): host int64 [14] = p0, m, v, lr, t, gnorm (per
-    // tower), log_std, barrier words; host float [5] = max_norm (per tower), b1, b2, eps
-    TORCH_CHECK(opt_floats.has_value() && opt_floats->defined(), "mlp_wgrad: opt_words needs opt_floats");
-    const Tensor w = opt_words->to(at::kCPU).contiguous(), f = opt_floats->to(at::kCPU).contiguous();
-    TORCH_CHECK(w.scalar_type() == at::kLong && w.numel() == 14 && f.scalar_type() == at::kFloat && f.numel() == 5,
-                "mlp_wgrad: opt_words int64[14], opt_floats float[5]");
-    const int64_t* wp = w.data_ptr<int64_t>();
-    const float* fp = f.data_ptr<float>();
-    aca::WgradOpt& o = a.opt;
-    for (int q = 0; q < 2; ++q) {
-      o.p0[q] = reinterpret_cast<float*>(wp[0 + q]);
-      o.m[q] = reinterpret_cast<float*>(wp[2 + q]);
-      o.v[q] = reinterpret_cast<float*>(wp[4 + q]);
-      o.lr[q] = reinterpret_cast<const float*>(wp[6 + q]);
-      o.t[q] = reinterpret_cast<float*>(wp[8 + q]);
-      o.gnorm[q] = reinterpret_cast<float*>(wp[10 + q]);
-      o.max_norm[q] = fp[q];
-    }
-    o.log_std = reinterpret_cast<float*>(wp[12]);
-    o.bar = reinterpret_cast<unsigned int*>(wp[13]);
-    o.b1 = fp[2];
-    o.b2 = fp[3];
-    o.eps = fp[4];
-    a.fuse = 1;
-  }
   if (bump.has_value() && bump->defined()) {
     need(*bump, at::kLong, "bump");
     a.bump = bump->data_ptr<int64_t>();
@@ -1074,44 +1016,6 @@ struct GemmGroupState {
 };
 static thread_local GemmGroupState g_gemm_group;
 
-// Large-shape GEMM on the 32x32x16 MFMA (gemm_mfma32.hip): plain bf16 operands, epilogue bias / relu / mask, store
-// fp32 | bf16 (splits 1) or fp32 split-K partial planes (out_mode 3). Returns false when the kernel does not take
-// this shape / layout (nothing launched: the caller uses the general GEMM).
-bool gemm_mfma32(Tensor A, int64_t lda, bool a_k, Tensor B, int64_t ldb, bool b_k, Tensor C, int64_t ldc,
-                 int64_t out_mode, int64_t M, int64_t N, int64_t K, double alpha, c10::optional<Tensor> bias, bool relu,
-                 c10::optional<Tensor> mask, int64_t ldm, int64_t splits) {
-  TORCH_CHECK(out_mode == 0 || out_mode == 1 || out_mode == 3, "gemm_mfma32: out_mode 0 / 1 / 3");
-  TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "gemm_mfma32: bf16 operands");
-  TORCH_CHECK(C.scalar_type() == (out_mode == 1 ? at::kBFloat16 : at::kFloat), "gemm_mfma32: C dtype mismatch");
-  TORCH_CHECK(splits >= 1 && (splits == 1 || out_mode == 3), "gemm_mfma32: split-K only as partial planes");
-  check_extent(A, a_k ? M : K, a_k ? K : M, lda, "A");
-  check_extent(B, b_k ? N : K, b_k ? K : N, ldb, "B");
-  check_extent(C, out_mode == 3 ? splits * M : M, N, ldc, "C");
-  if (bias.has_value() && bias->defined())
-    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() >= N, "gemm_mfma32: bias must be fp32 [N]");
-  if (mask.has_value() && mask->defined()) {
-    TORCH_CHECK(mask->scalar_type() == at::kBFloat16, "gemm_mfma32: mask must be bf16");
-    check_extent(*mask, M, N, ldm, "mask");
-  }
-  AcaGemmDesc d{};
-  d.A = A.data_ptr(); d.B = B.data_ptr(); d.C = C.data_ptr();
-  d.bias = optr<float>(bias);
-  d.mask = (mask.has_value() && mask->defined()) ? mask->data_ptr() : nullptr;
-  d.lda = lda; d.ldb = ldb; d.ldc = ldc; d.ldm = ldm;
-  d.M = (int)M; d.N = (int)N; d.K = (int)K;
-  d.a_k = a_k; d.b_k = b_k;
-  d.out_mode = (int)out_mode; d.relu = relu ? 1 : 0;
-  d.alpha = (float)alpha;
-  d.splits = (int)splits;
-  const hipError_t e = aca_gemm_mfma32(&d, cur_stream(C));
-  if (e == hipErrorInvalidValue) {
-    (void)hipGetLastError();
-    return false;
-  }
-  check(e, "gemm_mfma32");
-  return true;
-}
-
 void gemm(Tensor A, int64_t lda, bool a_k, Tensor B, int64_t ldb, bool b_k, Tensor C, int64_t ldc, int64_t out_mode,
           int64_t M, int64_t N, int64_t K, double alpha, c10::optional<Tensor> bias, bool relu,
           c10::optional<Tensor> mask, int64_t ldm, c10::optional<Tensor> colsum, int64_t colsum_mod, int64_t tile,
@@ -1273,7 +1177,6 @@ int64_t gemm_effective_splits(int64_t K, int64_t bk, int64_t splits) {
 void cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, Tensor y1,
                    Tensor y2, Tensor y3, double scale, c10::optional<Tensor> shift_out,
                    c10::optional<Tensor> stamps, int64_t mode, c10::optional<Tensor> copy_out,
-                   c10::optional<Tensor> fold_w, c10::optional<Tensor> fold_planes, c10::optional<Tensor> fold_cnt,
                    c10::optional<Tensor> obs_idx) {
   need(obs, at::kByte, "obs");
   for (auto* w : {&W1, &W2, &W3, &y1, &y2, &y3}) need(*w, at::kBFloat16, "trunk bf16 operand");
@@ -1311,13 +1214,11 @@ void cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tenso
                 "cnn_trunk_fwd: copy_out must be a distinct, aligned [B, 4, 84, 84] uint8 buffer");
     co = ptr<uint8_t>(*copy_out);
   }
-  const FoldPtrs ff = fold_ptrs(fold_w, fold_planes, fold_cnt, B, "cnn_trunk_fwd");
-  TORCH_CHECK(!ff.cnt || mode == 1 || mode == 2, "cnn_trunk_fwd: the fc fold needs a row-split mode");
   if (mode == 1 || mode == 2) {   // 2: the row kernel with its conv2/conv3 weight loads issued after conv1
     check(aca_cnn_trunk_rows(ptr<uint8_t>(obs), ptr<uint16_t>(W1), ptr<float>(b1), ptr<uint16_t>(W2),
                              ptr<float>(b2), ptr<uint16_t>(W3), ptr<float>(b3), ptr<uint16_t>(y1), ptr<uint16_t>(y2),
                              ptr<uint16_t>(y3), (int)B, (float)scale, so, co, stamps_ptr(stamps, B * 7),
-                             mode == 2 ? 1 : 0, ff.w, ff.planes, ff.cnt, cur_stream(obs)),
+                             mode == 2 ? 1 : 0, cur_stream(obs)),
           "cnn_trunk_rows");
     return;
   }
@@ -1360,46 +1261,6 @@ void grad_finalize(Tensor jobs, Tensor partial) {
               "grad_finalize: partial too small / too many jobs");
   check(aca_grad_finalize(jobs.data_ptr<int64_t>(), (int)jobs.size(0), ptr<float>(partial), cur_stream(partial)),
         "grad_finalize");
-}
-
-// Finaliser + optimiser in one launch (optim.hip grad_finalize_opt_kernel): the jobs of grad_finalize, then the
-// clip + Adam (m, t given) / RMSprop (b2 = alpha) update of every job's slab range from the LDS copy. `grad` is the
-// gradient slab segment the job dst pointers point into; p / m / v / shadow are the matching parameter-side
-// segments. Returns false (nothing launched) when the job table cannot be resident at once (the caller then runs
-// the two separate launches).
-bool grad_finalize_opt(Tensor jobs, int64_t max_job_n, Tensor partial, Tensor grad, Tensor p, c10::optional<Tensor> m,
-                       Tensor v, c10::optional<Tensor> shadow, Tensor lr, c10::optional<Tensor> t,
-                       c10::optional<Tensor> gnorm_out, double clip, double max_norm, double gmul, double norm_mul,
-                       double b1, double b2, double eps, bool adam, Tensor state) {
-  need(jobs, at::kLong, "jobs");
-  TORCH_CHECK(jobs.dim() == 2 && jobs.size(1) == 8 && jobs.is_contiguous(), "grad_finalize_opt: jobs [njobs, 8]");
-  for (auto* x : {&partial, &grad, &p, &v, &lr}) need(*x, at::kFloat, "grad_finalize_opt f32 operand");
-  need(state, at::kInt, "state");
-  TORCH_CHECK(state.numel() >= 3, "grad_finalize_opt: state needs 3 words");
-  TORCH_CHECK(grad.numel() == p.numel() && v.numel() == p.numel(), "grad_finalize_opt: size mismatch");
-  TORCH_CHECK(partial.numel() >= aca_sumsq_parts() && jobs.size(0) <= aca_sumsq_parts(),
-              "grad_finalize_opt: partial too small / too many jobs");
-  float* mp = nullptr;
-  float* tp = nullptr;
-  if (adam) {
-    TORCH_CHECK(m.has_value() && t.has_value(), "grad_finalize_opt: Adam needs m and t");
-    need(*m, at::kFloat, "m");
-    need(*t, at::kFloat, "t");
-    TORCH_CHECK(m->numel() == p.numel(), "grad_finalize_opt: m size mismatch");
-    mp = ptr<float>(*m);
-    tp = ptr<float>(*t);
-  }
-  const hipError_t e = aca_grad_finalize_opt(
-      jobs.data_ptr<int64_t>(), (int)jobs.size(0), (int)max_job_n, ptr<float>(partial), ptr<float>(p), mp,
-      ptr<float>(v), shadow_ptr(shadow, p, "grad_finalize_opt"), ptr<float>(grad), ptr<float>(lr), tp,
-      optr<float>(gnorm_out), (float)clip, (float)max_norm, (float)gmul, (float)norm_mul, (float)b1, (float)b2,
-      (float)eps, adam ? 1 : 0, reinterpret_cast<unsigned int*>(state.data_ptr<int32_t>()), cur_stream(p));
-  if (e == hipErrorInvalidValue) {
-    (void)hipGetLastError();
-    return false;
-  }
-  check(e, "grad_finalize_opt");
-  return true;
 }
 
 // A2C learner head in one launch (loss.hip head_bwd_kernel): returns + EV + advantage normalisation + loss + dz,
@@ -1542,24 +1403,6 @@ void colsum_bf16(Tensor x, int64_t M, int64_t N, int64_t ld, Tensor out) {
   check(aca_colsum_bf16(ptr<uint16_t>(x), M, N, ld, ptr<float>(out), cur_stream(x)), "colsum_bf16");
 }
 
-// z [B, A1] fp32 = bh + h [B, 512] bf16 . Wh [512, A1] bf16 (large learner batches; heads.hip head_fwd_kernel)
-void head_fwd(Tensor h, Tensor Wh, Tensor bh, Tensor z) {
-  TORCH_CHECK(h.scalar_type() == at::kBFloat16 && h.is_contiguous() && h.dim() == 2 && h.size(1) == 512,
-              "head_fwd: h must be contiguous bf16 [B, 512]");
-  const int64_t B = h.size(0), A1 = bh.numel();
-  TORCH_CHECK(A1 >= 2 && A1 <= 8, "head_fwd: 2 <= A + 1 <= 8");
-  TORCH_CHECK(Wh.scalar_type() == at::kBFloat16 && Wh.is_contiguous() && Wh.numel() == 512 * A1,
-              "head_fwd: Wh must be contiguous bf16 [512, A1]");
-  TORCH_CHECK(bh.scalar_type() == at::kFloat && bh.is_contiguous(), "head_fwd: bh must be fp32");
-  TORCH_CHECK(z.scalar_type() == at::kFloat && z.is_contiguous() && z.numel() >= B * A1,
-              "head_fwd: z must be contiguous fp32 [B, A1]");
-  TORCH_CHECK(h.device() == Wh.device() && h.device() == bh.device() && h.device() == z.device(),
-              "head_fwd: one device");
-  check(aca_head_fwd(ptr<uint16_t>(h), ptr<uint16_t>(Wh), ptr<float>(bh), ptr<float>(z), (int)B, (int)A1,
-                     cur_stream(h)),
-        "head_fwd");
-}
-
 // ---------------------------------------------------------------------------------------------- loss
 void ac_loss(Tensor logits, int64_t ldl, c10::optional<Tensor> value, int64_t ldv, c10::optional<Tensor> act_i,
              c10::optional<Tensor> act_f, c10::optional<Tensor> log_std, Tensor logp_old, c10::optional<Tensor> adv,
@@ -1650,8 +1493,7 @@ TORCH_LIBRARY(acamd, m) {
         "Tensor t_n, Tensor tg_n, Tensor ep_ret_n, Tensor ep_stats, Tensor env_ids, Tensor prev, Tensor out, "
         "Tensor reward, Tensor done, Tensor truncated, int seed, int max_steps, Tensor hpart, int planes, "
         "Tensor bfc, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, Tensor y1, Tensor y2, "
-        "Tensor y3, float scale, Tensor? shift_out=None, Tensor? stamps=None, Tensor? fold_w=None, "
-        "Tensor? fold_planes=None, Tensor? fold_cnt=None) -> ()");
+        "Tensor y3, float scale, Tensor? shift_out=None, Tensor? stamps=None) -> ()");
   m.def("categorical_sample(Tensor logits, Tensor keys, int seed, Tensor act, Tensor logp, Tensor ent) -> ()");
   m.def("categorical_sample_env(Tensor logits, Tensor tg, Tensor env_ids, int key_shift, int seed, Tensor act, "
         "Tensor logp, Tensor ent, Tensor? vout) -> ()");
@@ -1667,8 +1509,6 @@ TORCH_LIBRARY(acamd, m) {
   m.def("conv1_wgrad(Tensor obs, Tensor dy1, Tensor planes, int P, float scale, Tensor? obs_idx=None) -> ()");
   m.def("conv_wgrad_nhwc(int layer, Tensor img, Tensor dy, Tensor planes, int P) -> ()");
   m.def("conv_wgrad_gemm(int layer, Tensor img, Tensor dy, Tensor planes, int P) -> ()");
-  m.def("gemm_mfma32(Tensor A, int lda, bool a_k, Tensor B, int ldb, bool b_k, Tensor C, int ldc, int out_mode, "
-        "int M, int N, int K, float alpha, Tensor? bias, bool relu, Tensor? mask, int ldm, int splits) -> bool");
   m.def("mb_gather(Tensor obs, Tensor act, Tensor logp, Tensor adv, Tensor ret, Tensor v, Tensor? o_obs, "
         "Tensor o_act, Tensor o_logp, Tensor o_adv, Tensor o_ret, Tensor o_v, int seed, Tensor uc, int ep, "
         "int off, Tensor? mom=None, float eps=1e-8, Tensor? bump_ticket=None, Tensor? o_idx=None) -> ()");
@@ -1698,8 +1538,7 @@ TORCH_LIBRARY(acamd, m) {
         "float v_clip, bool ppo, Tensor? g_log_std, Tensor? mstats, Tensor? mpart=None, Tensor? stamps=None) -> ()");
   m.def("mlp_wgrad(Tensor desc, int ntw, int B, int nsplit, int items0, int items1, Tensor? parts0, "
         "Tensor? parts1, float clip0, float clip1, Tensor? g_log_std, int A, Tensor? mstats, Tensor? stats, "
-        "Tensor? ent_coef, Tensor? kl_coef, Tensor? mpart=None, int mpart_rows=0, Tensor? bump=None, "
-        "Tensor? opt_words=None, Tensor? opt_floats=None) -> ()");
+        "Tensor? ent_coef, Tensor? kl_coef, Tensor? mpart=None, int mpart_rows=0, Tensor? bump=None) -> ()");
   m.def("mlp_rollout(Tensor desc, int lds, Tensor obs, Tensor act, Tensor logp, Tensor ent, Tensor reward, "
         "Tensor done, Tensor truncated, Tensor log_std, Tensor ac_scale, int key_shift, int policy_seed, "
         "Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, Tensor env_ids, Tensor lin_A, "
@@ -1713,14 +1552,10 @@ TORCH_LIBRARY(acamd, m) {
   m.def("gemm_effective_splits(int K, int bk, int splits) -> int", &gemm_effective_splits);
   m.def("cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, Tensor y1, "
         "Tensor y2, Tensor y3, float scale, Tensor? shift_out=None, Tensor? stamps=None, int mode=0, "
-        "Tensor? copy_out=None, Tensor? fold_w=None, Tensor? fold_planes=None, Tensor? fold_cnt=None, "
-        "Tensor? obs_idx=None) -> ()");
+        "Tensor? copy_out=None, Tensor? obs_idx=None) -> ()");
   m.def("cnn_trunk_bwd(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tensor dy2, Tensor dy1, "
         "Tensor biasp, Tensor? stamps=None, int persist=0) -> ()");
   m.def("grad_finalize(Tensor jobs, Tensor partial) -> ()");
-  m.def("grad_finalize_opt(Tensor jobs, int max_job_n, Tensor partial, Tensor grad, Tensor p, Tensor? m, Tensor v, "
-        "Tensor? shadow, Tensor lr, Tensor? t, Tensor? gnorm_out, float clip, float max_norm, float gmul, "
-        "float norm_mul, float b1, float b2, float eps, bool adam, Tensor state) -> bool");
   m.def("head_bwd(Tensor z, Tensor act, Tensor logp_old, Tensor ent_coef, Tensor kl_coef, float vf_coef, Tensor rew, "
         "Tensor val, Tensor dones, int L, int returns_mode, bool norm_adv, float gamma, float lam, Tensor ret_w, "
         "Tensor adv_w, Tensor h, Tensor Wh, Tensor dh, Tensor gWh, Tensor gbh, Tensor gbfc, Tensor stats, "
@@ -1734,7 +1569,6 @@ TORCH_LIBRARY(acamd, m) {
   m.def("col2im_nhwc(Tensor dcol, Tensor ymask, Tensor dx, Tensor? colsum, int B, int H, int W, int C, int kh, "
         "int kw, int s) -> ()");
   m.def("colsum_bf16(Tensor x, int M, int N, int ld, Tensor out) -> ()");
-  m.def("head_fwd(Tensor h, Tensor Wh, Tensor bh, Tensor z) -> ()");
   m.def("ac_loss(Tensor logits, int ldl, Tensor? value, int ldv, Tensor? act_i, Tensor? act_f, Tensor? log_std, "
         "Tensor logp_old, Tensor? adv, Tensor? ret, Tensor? v_old, Tensor? ent_coef, Tensor? kl_coef, float vf_coef, "
         "float ppo_clip, float v_clip, Tensor dlogits, int lddl, Tensor? dvalue, int lddv, Tensor? dlog_std, "
@@ -1763,7 +1597,6 @@ TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
   m.impl("conv1_wgrad", &conv1_wgrad);
   m.impl("conv_wgrad_nhwc", &conv_wgrad_nhwc);
   m.impl("conv_wgrad_gemm", &conv_wgrad_gemm);
-  m.impl("gemm_mfma32", &gemm_mfma32);
   m.impl("moments", &moments);
   m.impl("sumsq", &sumsq);
   m.impl("adam_step", &adam_step);
@@ -1781,14 +1614,12 @@ TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
   m.impl("fc_value", &fc_value);
   m.impl("cnn_trunk_bwd", &cnn_trunk_bwd);
   m.impl("grad_finalize", &grad_finalize);
-  m.impl("grad_finalize_opt", &grad_finalize_opt);
   m.impl("head_bwd", &head_bwd);
   m.impl("a2c_head", &a2c_head);
   m.impl("im2col_u8", &im2col_u8);
   m.impl("im2col_nhwc", &im2col_nhwc);
   m.impl("col2im_nhwc", &col2im_nhwc);
   m.impl("colsum_bf16", &colsum_bf16);
-  m.impl("head_fwd", &head_fwd);
   m.impl("colsum_reduce", &colsum_reduce);
   m.impl("seg_stats", &seg_stats);
   m.impl("ac_loss", &ac_loss);

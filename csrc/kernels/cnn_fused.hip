@@ -229,18 +229,9 @@ __global__ void __launch_bounds__(T_THREADS) cnn_trunk_fwd_kernel(
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// Persistent form of the per-env trunk for large learner batches (PPO minibatches, B = 4096): one workgroup per
-// CU walks samples b = blockIdx.x, blockIdx.x + gridDim.x, ... The per-env kernel above re-reads the conv2 / conv3
-// weights (136 KB) from L2 for every sample and stages each observation only after the previous sample has left
-// the CU; here every wave extracts its W2 / W3 B fragments (its output-channel tile, all k) ONCE and keeps them in
-// registers for the whole walk, and the next sample's frames are copied global -> LDS by the LDS-DMA path
-// (global_load_lds_dwordx4: no registers, tracked by the vm counter) into the second half of a double-buffered
-// uint8 staging area while the current sample is multiplied. conv1 converts its uint8 pixels to exact bf16 integers
-// on the fly. Same MFMA order and epilogues as the per-env kernel: bit-identical outputs.
+// One observation copied global -> LDS by the LDS-DMA path (global_load_lds_dwordx4: no registers, tracked by the vm
+// counter), padded to whole 1 KB wave copies.
 constexpr int TP_OBS_PAD = 28 * 1024;   // one observation (28224 B) padded to whole 1 KB wave copies
-
-__device__ __forceinline__ void trunk_w23_load(const u16* __restrict__ W2, const u16* __restrict__ W3,
-                                               bf16x8 (&bw2)[16], bf16x8 (&bw3)[18]);
 
 __device__ __forceinline__ void trunk_obs_dma(const uint8_t* __restrict__ src, uint8_t* dst_lds) {
   // 28 wave-copies of 64 x 16 B: wave w copies blocks w, w + (waves), ...; lanes past the observation read its
@@ -251,136 +242,6 @@ __device__ __forceinline__ void trunk_obs_dma(const uint8_t* __restrict__ src, u
     uint8_t* base = dst_lds + blk * 1024;   // wave-uniform LDS base (lane i lands at base + 16 i)
     __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint4*>(src) + c,
                                      (__attribute__((address_space(3))) void*)(base), 16, 0, 0);
-  }
-}
-
-__global__ void __launch_bounds__(T_THREADS) cnn_trunk_fwd_persist_kernel(
-    const uint8_t* __restrict__ obs, const u16* __restrict__ W1, const float* __restrict__ b1,
-    const u16* __restrict__ W2, const float* __restrict__ b2, const u16* __restrict__ W3,
-    const float* __restrict__ b3, u16* __restrict__ y1g, u16* __restrict__ y2g, u16* __restrict__ y3g,
-    float scale, int B) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_obs8[2][TP_OBS_PAD];
-  __shared__ __attribute__((aligned(16))) u16 s_w1[32 * W1_LD];
-  __shared__ __attribute__((aligned(16))) u16 s_y1[Y1_ROWS * Y1_LD];
-  __shared__ __attribute__((aligned(16))) u16 s_y2[Y2_ROWS * Y2_LD];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int l16 = lane & 15, lg = lane >> 4;
-  const int n2 = wid * 16 + l16;
-  const int b0 = blockIdx.x;
-  if (b0 >= B) return;
-  // ---- first observation in flight, then the resident weights
-  trunk_obs_dma(obs + (size_t)b0 * OBS_BYTES, s_obs8[0]);
-  {
-    constexpr int W1_PER = 32 * 256 / 8 / T_THREADS;   // 4
-#pragma unroll
-    for (int u = 0; u < W1_PER; ++u) {
-      const int i = tid + u * T_THREADS, r = i / 32, c8 = (i % 32) * 8;
-      *reinterpret_cast<uint4*>(s_w1 + r * W1_LD + c8) = reinterpret_cast<const uint4*>(W1)[i];
-    }
-  }
-  bf16x8 bw2[16], bw3[18];
-  trunk_w23_load(W2, W3, bw2, bw3);
-  const float bias1a = b1[l16], bias1b = b1[16 + l16], bias2 = b2[n2], bias3 = b3[n2];
-  int buf = 0;
-  for (int b = b0; b < B; b += gridDim.x) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this sample's frames have landed (and the weights)
-    __syncthreads();
-    if (b + gridDim.x < B) trunk_obs_dma(obs + (size_t)(b + gridDim.x) * OBS_BYTES, s_obs8[buf ^ 1]);
-    const uint8_t* so = s_obs8[buf];
-    // ------------------------------------------------------------ conv1: M 400 (25 tiles), N 32 (2), K 256 (8)
-    {
-      bf16x8 bw[2][8];
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-        for (int ks = 0; ks < 8; ++ks)
-          bw[nt][ks] = *reinterpret_cast<const bf16x8*>(s_w1 + (nt * 16 + l16) * W1_LD + ks * 32 + lg * 8);
-      for (int mt = wid; mt < 25; mt += 4) {
-        floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-        const int m = mt * 16 + l16;
-        const int oh = m / 20, ow = m - oh * 20;
-#pragma unroll
-        for (int ks = 0; ks < 8; ++ks) {
-          const int k = ks * 32 + lg * 8;
-          const int c = k >> 6, i = (k >> 3) & 7;
-          const uint8_t* p = so + (c * 84 + oh * 4 + i) * 84 + ow * 4;   // 4-byte aligned
-          const uint32_t w0 = *reinterpret_cast<const uint32_t*>(p), w1 = *reinterpret_cast<const uint32_t*>(p + 4);
-          const uint2 lo = u8x4_to_bf16(w0), hi = u8x4_to_bf16(w1);
-          const bf16x8 a = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw[0][ks], acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw[1][ks], acc1, 0, 0, 0);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = mt * 16 + lg * 4 + r;
-          const u16 v0 = f2bf(fmaxf(acc0[r] * scale + bias1a, 0.f));
-          const u16 v1 = f2bf(fmaxf(acc1[r] * scale + bias1b, 0.f));
-          s_y1[row * Y1_LD + l16] = v0;
-          s_y1[row * Y1_LD + 16 + l16] = v1;
-          y1g[((size_t)b * Y1_ROWS + row) * Y1_C + l16] = v0;
-          y1g[((size_t)b * Y1_ROWS + row) * Y1_C + 16 + l16] = v1;
-        }
-      }
-    }
-    __syncthreads();
-    // ------------------------------------------------------------ conv2: M 81 (6 tiles), N 64 (wave = N tile), K 512
-    {
-      floatx4 acc[6];
-#pragma unroll
-      for (int mt = 0; mt < 6; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < 16; ++ks) {
-        const int k = ks * 32 + lg * 8;
-        const int i = k >> 7, j = (k >> 5) & 3, c0 = k & 31;
-#pragma unroll
-        for (int mt = 0; mt < 6; ++mt) {
-          const int m = min(mt * 16 + l16, Y2_ROWS - 1);
-          const int oh = m / 9, ow = m - oh * 9;
-          const bf16x8 a = *reinterpret_cast<const bf16x8*>(s_y1 + ((oh * 2 + i) * 20 + ow * 2 + j) * Y1_LD + c0);
-          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw2[ks], acc[mt], 0, 0, 0);
-        }
-      }
-#pragma unroll
-      for (int mt = 0; mt < 6; ++mt) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = mt * 16 + lg * 4 + r;
-          if (row < Y2_ROWS) {
-            const u16 v = f2bf(fmaxf(acc[mt][r] + bias2, 0.f));
-            s_y2[row * Y2_LD + n2] = v;
-            y2g[((size_t)b * Y2_ROWS + row) * Y2_C + n2] = v;
-          }
-        }
-      }
-    }
-    __syncthreads();
-    // ------------------------------------------------------------ conv3: M 49 (4 tiles), N 64 (wave = N tile), K 576
-    {
-      floatx4 acc[4];
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < 18; ++ks) {
-        const int k = ks * 32 + lg * 8;
-        const int i = k / 192, j = (k >> 6) % 3, c0 = k & 63;
-#pragma unroll
-        for (int mt = 0; mt < 4; ++mt) {
-          const int m = min(mt * 16 + l16, Y3_ROWS - 1);
-          const int oh = m / 7, ow = m - oh * 7;
-          const bf16x8 a = *reinterpret_cast<const bf16x8*>(s_y2 + ((oh + i) * 9 + ow + j) * Y2_LD + c0);
-          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw3[ks], acc[mt], 0, 0, 0);
-        }
-      }
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = mt * 16 + lg * 4 + r;
-          if (row < Y3_ROWS) y3g[((size_t)b * Y3_ROWS + row) * Y3_C + n2] = f2bf(fmaxf(acc[mt][r] + bias3, 0.f));
-        }
-      }
-    }
-    buf ^= 1;
   }
 }
 
@@ -543,123 +404,11 @@ constexpr int TR_IN_ELEMS = 768 * 16;   // 4 x 36 x 84 = 12096 bf16, padded to 3
 
 __device__ __forceinline__ int tr_y1_own_begin(int r) { return (20 * r + 6) / 7; }
 
-// ------------------------------------------------------------------------------------------------------------
-// fc fold: the rollout's fc product (y3 [N, 3136] x Wfc [3136, 512]) inside the row-split trunk launch, as 7 partial
-// planes (plane r = conv3 row r's 448 features x the matching 448 rows of Wfc). Every row workgroup (e, r) publishes
-// its conv3 row with agent-coherent (sc1) stores and arrives at the row's counter; workgroups e < FF_HELPERS of each
-// row are the row's helpers: once all N envs have arrived (bounded spin; a timeout raises cnt[15] instead of hanging)
-// helper e multiplies the N envs' row r [N x 448] (sc1 loads: other XCDs' L2s hold them dirty otherwise) by the
-// 448 x 32 Wfc slice of columns 32e .. 32e+31 -- staged into LDS by the LDS-DMA path at launch entry, so it lands
-// while conv1 runs -- with 16x16x32 bf16 MFMA and stores its [N x 32] block of plane r. Consumers sum the 7 planes
-// in plane order (FcParts, S = 7). Replaces the fc GEMM launch of every rollout step. Needs every workgroup of the
-// launch co-resident (7 N <= 224 with one workgroup per CU; the launcher checks the occupancy) and N in {16, 32}.
-// Counter words: [r] arrivals of row r, [8 + r] departures of its helpers (the last one zeroes both), [15] timeout.
-// ------------------------------------------------------------------------------------------------------------
-constexpr int FF_HELPERS = 16;                 // helper workgroups per conv3 row
-constexpr int FF_COLS = 512 / FF_HELPERS;      // 32 fc columns per helper
-constexpr int FF_K = 7 * 64;                   // 448 features per conv3 row
-constexpr unsigned int FF_SPIN_LIMIT = 1u << 21;
-
-struct FcFold {
-  const u16* Wfc;        // [3136][512] bf16 (K x N, row-major)
-  float* planes;         // plane r at planes + r * N * 512: [N][512] fp32
-  unsigned int* cnt;     // [16] counter words (zero between launches); null: no fold
-  int N;
-};
-
-// Wfc rows [448 r, 448 r + 448) x columns [32 e, 32 e + 32) -> s_wfc [448][32] bf16, 28 wave copies of 16 rows
-// (lane i -> row 16 blk + i / 4, 16-byte chunk i % 4): no registers, tracked by the vm counter
-__device__ __forceinline__ void ff_stage_w(const FcFold& ff, int e, int r, u16* s_wfc) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  for (int blk = wid; blk < FF_K / 16; blk += T_THREADS / 64) {
-    const int row = blk * 16 + (lane >> 2), ch = lane & 3;
-    const u16* src = ff.Wfc + (size_t)(r * FF_K + row) * 512 + e * FF_COLS + ch * 8;
-    __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint4*>(src),
-                                     (__attribute__((address_space(3))) void*)(s_wfc + blk * 16 * FF_COLS), 16, 0, 0);
-  }
-}
-
-__device__ __forceinline__ uint4 ld_b128_sc1(const void* p) {   // agent-coherent 16-byte load (caller waits vmcnt)
-  uint4 v;
-  asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
-  return v;
-}
-
-__device__ __forceinline__ bf16x8 ff_tr_frag(const u16* rows, int ld, int col0, int lane) {
-  // B fragment (k = 8 (lane >> 4) + 0..7, n = col0 + lane & 15) from n-contiguous rows via two transposing reads
-  const int lr16 = lane & 15, lg = lane >> 4, q = lr16 >> 2, p = lr16 & 3;
-  typedef short short4f __attribute__((ext_vector_type(4)));
-  typedef __attribute__((address_space(3))) short4f lds4f;
-  const short4f lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4f*)(rows + (lg * 8 + q) * ld + col0 + 4 * p));
-  const short4f hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4f*)(rows + (lg * 8 + 4 + q) * ld + col0 + 4 * p));
-  const short8v v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8, v);
-}
-
-// After workgroup (e, r) published its conv3 row (sc1 stores issued): arrive; helpers wait for the row and multiply.
-__device__ void ff_arrive_and_help(const FcFold& ff, int e, int r, const u16* __restrict__ s_wfc,
-                                   const u16* __restrict__ y3g) {
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's row stores acknowledged, its W slice copies landed
-  __syncthreads();
-  if (tid == 0) __hip_atomic_fetch_add(&ff.cnt[r], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (e >= FF_HELPERS) return;
-  if (tid == 0) {
-    unsigned int spins = 0;
-    while (__hip_atomic_load(&ff.cnt[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned int)ff.N) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > FF_SPIN_LIMIT) {
-        __hip_atomic_store(&ff.cnt[15], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-  }
-  __syncthreads();
-  const int mtiles = ff.N >> 4;
-  if (wid < 2 * mtiles) {   // wave -> (env tile mt, column tile nt) of the helper's [N x 32] block
-    const int mt = wid % mtiles, nt = wid / mtiles;
-    const int l16 = lane & 15, lg = lane >> 4;
-    const u16* arow = y3g + ((size_t)(16 * mt + l16) * Y3_ROWS + r * 7) * Y3_C + lg * 8;
-    uint4 af[FF_K / 32];
-#pragma unroll
-    for (int ks = 0; ks < FF_K / 32; ++ks) af[ks] = ld_b128_sc1(arow + ks * 32);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < FF_K / 32; ++ks)
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[ks]),
-                                                    ff_tr_frag(s_wfc + ks * 32 * FF_COLS, FF_COLS, nt * 16, lane),
-                                                    acc, 0, 0, 0);
-    float* dst = ff.planes + (size_t)r * ff.N * 512 + (size_t)(16 * mt + 4 * lg) * 512 + e * FF_COLS + nt * 16 + l16;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) dst[(size_t)i * 512] = acc[i];
-  }
-  if (tid == 0) {   // departure: the row's last helper zeroes its counters for the next launch (stream-ordered)
-    const unsigned int prev = __hip_atomic_fetch_add(&ff.cnt[8 + r], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == (unsigned int)FF_HELPERS - 1u) {
-      __hip_atomic_store(&ff.cnt[r], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&ff.cnt[8 + r], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
 // conv1 -> conv3 of row workgroup (e, r) from its staged input rows (s_in: 4 frames x 36 rows of bf16 pixel values,
 // complete) and the conv1 weights (s_w1, complete); stores the owned y1 / y2 rows and its y3 row. Shared by the
 // trunk kernel and the fused policy/env + trunk kernel.
-// conv2 / conv3 B fragments of wave-column n2 = wid * 16 + (lane & 15) (16 + 18 k-steps, 16-byte loads)
-__device__ __forceinline__ void trunk_w23_load(const u16* __restrict__ W2, const u16* __restrict__ W3,
-                                               bf16x8 (&bw2)[16], bf16x8 (&bw3)[18]) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int n2 = wid * 16 + (lane & 15), lg = lane >> 4;
-#pragma unroll
-  for (int ks = 0; ks < 16; ++ks) bw2[ks] = *reinterpret_cast<const bf16x8*>(W2 + n2 * 512 + ks * 32 + lg * 8);
-#pragma unroll
-  for (int ks = 0; ks < 18; ++ks) bw3[ks] = *reinterpret_cast<const bf16x8*>(W3 + n2 * 576 + ks * 32 + lg * 8);
-}
-
 // WMODE (when the conv2 / conv3 weight fragments are requested): 0 at entry (the staging barrier waited for obs +
-// W1 only), 1 after conv1's MFMAs (trunk mode 2), 2 by the caller, before anything else of its launch (the fused
-// step: the loads overlap the policy head, the env step and the render)
+// W1 only), 1 after conv1's MFMAs (trunk mode 2, and the fused step)
 template <int WMODE>
 __device__ __forceinline__ void trunk_rows_compute(const u16* __restrict__ s_in, const u16* __restrict__ s_w1,
                                                    u16* __restrict__ s_y1, u16* __restrict__ s_y2, int e, int r,
@@ -668,8 +417,7 @@ __device__ __forceinline__ void trunk_rows_compute(const u16* __restrict__ s_in,
                                                    const u16* __restrict__ W3, u16* __restrict__ y1g,
                                                    u16* __restrict__ y2g, u16* __restrict__ y3g, float scale,
                                                    uint64_t* __restrict__ stamps, bf16x8 (&bw2)[16],
-                                                   bf16x8 (&bw3)[18], const FcFold& ff, u16* __restrict__ s_y3,
-                                                   const u16* __restrict__ s_wfc) {
+                                                   bf16x8 (&bw3)[18]) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l16 = lane & 15, lg = lane >> 4;
   const int n2 = wid * 16 + l16;
@@ -802,10 +550,7 @@ __device__ __forceinline__ void trunk_rows_compute(const u16* __restrict__ s_in,
     for (int q = 0; q < 4; ++q) {
       const int row = lg * 4 + q;
       const u16 v = f2bf(fmaxf(acc[q] + bias, 0.f));
-      if (row < 7) {
-        if (ff.cnt) s_y3[row * Y3_C + n] = v;   // published below as whole words with sc1 stores
-        else y3g[((size_t)e * Y3_ROWS + r * 7 + row) * Y3_C + n] = v;
-      }
+      if (row < 7) y3g[((size_t)e * Y3_ROWS + r * 7 + row) * Y3_C + n] = v;
     }
   }
   // ---------------------------------------------------------------- owned y1 / y2 rows: LDS -> global, 16-byte rows
@@ -824,13 +569,6 @@ __device__ __forceinline__ void trunk_rows_compute(const u16* __restrict__ s_in,
           *reinterpret_cast<const uint4*>(s_y2 + lp * Y2_LD + q);
     }
   }
-  if (ff.cnt) {
-    __syncthreads();   // s_y3 complete
-    if (tid < FF_K / 2)
-      __hip_atomic_store(reinterpret_cast<uint32_t*>(y3g + ((size_t)e * Y3_ROWS + r * 7) * Y3_C) + tid,
-                         reinterpret_cast<const uint32_t*>(s_y3)[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    ff_arrive_and_help(ff, e, r, s_wfc, y3g);
-  }
   if (stamps) {
     stamp(stamps, 4);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -844,14 +582,11 @@ __global__ void __launch_bounds__(T_THREADS) cnn_trunk_rows_kernel(
     const uint8_t* __restrict__ obs, const u16* __restrict__ W1, const float* __restrict__ b1,
     const u16* __restrict__ W2, const float* __restrict__ b2, const u16* __restrict__ W3,
     const float* __restrict__ b3, u16* __restrict__ y1g, u16* __restrict__ y2g, u16* __restrict__ y3g,
-    float scale, uint8_t* __restrict__ shift_out, uint8_t* __restrict__ copy_out, uint64_t* __restrict__ stamps,
-    FcFold ff) {
+    float scale, uint8_t* __restrict__ shift_out, uint8_t* __restrict__ copy_out, uint64_t* __restrict__ stamps) {
   __shared__ __attribute__((aligned(16))) u16 s_in[TR_IN_ELEMS];
   __shared__ __attribute__((aligned(16))) u16 s_w1[32 * W1_LD];
   __shared__ __attribute__((aligned(16))) u16 s_y1[TR_C1_POS * Y1_LD];
   __shared__ __attribute__((aligned(16))) u16 s_y2[TR_C2_POS * Y2_LD];
-  __shared__ __attribute__((aligned(16))) u16 s_y3[7 * Y3_C];
-  __shared__ __attribute__((aligned(16))) u16 s_wfc[FF_K * FF_COLS];
 
   const int r = blockIdx.x % TR_ROWS, e = blockIdx.x / TR_ROWS;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -882,7 +617,6 @@ __global__ void __launch_bounds__(T_THREADS) cnn_trunk_rows_kernel(
   uint4 vw[W1_PER];
 #pragma unroll
   for (int u = 0; u < W1_PER; ++u) vw[u] = reinterpret_cast<const uint4*>(W1)[tid + u * T_THREADS];
-  if (ff.cnt && e < FF_HELPERS) ff_stage_w(ff, e, r, s_wfc);   // behind the staging loads in the vm queue
   {
     uint4* dst = reinterpret_cast<uint4*>(s_in);
 #pragma unroll
@@ -918,7 +652,7 @@ __global__ void __launch_bounds__(T_THREADS) cnn_trunk_rows_kernel(
   stamp(stamps, 1);
   bf16x8 bw2[16], bw3[18];
   trunk_rows_compute<LATE_W ? 1 : 0>(s_in, s_w1, s_y1, s_y2, e, r, bias1a, bias1b, bias2, bias3, W2, W3, y1g, y2g,
-                                     y3g, scale, stamps, bw2, bw3, ff, s_y3, s_wfc);
+                                     y3g, scale, stamps, bw2, bw3);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -958,21 +692,19 @@ __device__ __forceinline__ void pong_commit_next(const PongIO& io, const PongNex
   sp[0] = q.bx; sp[1] = q.by; sp[2] = q.vx; sp[3] = q.vy; sp[4] = q.pa; sp[5] = q.po; sp[6] = q.sa; sp[7] = q.so;
 }
 
-template <int A1, int WPOS>
+template <int A1>
 __global__ void __launch_bounds__(T_THREADS) pong_fused_step_kernel(
     PongIO io, PongNext nx, FcParts fc, u16* __restrict__ h, const u16* __restrict__ Wh,
     const float* __restrict__ bh, float* __restrict__ z_out, int32_t* __restrict__ act, float* __restrict__ logp,
     float* __restrict__ ent, float* __restrict__ vout, int key_shift, uint32_t pseed, const u16* __restrict__ W1,
     const float* __restrict__ b1, const u16* __restrict__ W2, const float* __restrict__ b2,
     const u16* __restrict__ W3, const float* __restrict__ b3, u16* __restrict__ y1g, u16* __restrict__ y2g,
-    u16* __restrict__ y3g, float scale, uint8_t* __restrict__ shift_out, uint64_t* __restrict__ stamps, FcFold ff) {
+    u16* __restrict__ y3g, float scale, uint8_t* __restrict__ shift_out, uint64_t* __restrict__ stamps) {
   constexpr int A = A1 - 1;
   __shared__ __attribute__((aligned(16))) u16 s_in[TR_IN_ELEMS];
   __shared__ __attribute__((aligned(16))) u16 s_w1[32 * W1_LD];
   __shared__ __attribute__((aligned(16))) u16 s_y1[TR_C1_POS * Y1_LD];
   __shared__ __attribute__((aligned(16))) u16 s_y2[TR_C2_POS * Y2_LD];
-  __shared__ __attribute__((aligned(16))) u16 s_y3[7 * Y3_C];
-  __shared__ __attribute__((aligned(16))) u16 s_wfc[FF_K * FF_COLS];
   __shared__ float s_acc[4][A1];
   __shared__ PongOut cand[3];
   __shared__ int sh_act;
@@ -1007,16 +739,11 @@ __global__ void __launch_bounds__(T_THREADS) pong_fused_step_kernel(
   uint4 vw[W1_PER];
 #pragma unroll
   for (int u = 0; u < W1_PER; ++u) vw[u] = reinterpret_cast<const uint4*>(W1)[tid + u * T_THREADS];
-  // Where the conv2 / conv3 weight fragments (136 KB per workgroup: every workgroup pulls all of W2 / W3 from L2,
-  // ~2.3 us per step at the rate 224 workgroups get) are requested: WPOS 0 after conv1's MFMAs (trunk_rows_compute;
-  // default), 1 here, after every load the head and the staging wait for, 2 once the head's plane loads are consumed
-  // (below). The vm counter retires in issue order, so at 1 the head's fc-plane loads wait behind them; at 2 nothing
-  // waits on the vm counter before conv2, and conv1 drops from 3.9 to 1.4 us -- but the render's stores queue behind
-  // the fragment loads and the head/env/render phase grows from 6.0 to 8.8 us: the L2 -> CU transfer is on the
-  // critical path wherever it sits (profiles/r3_fused_step_wpos_ab.txt). Both measured slower than 0.
+  // The conv2 / conv3 weight fragments (136 KB per workgroup) are requested after conv1's MFMAs (trunk_rows_compute
+  // WMODE 1). Requesting them at kernel entry or after the policy head measured slower: the vm counter retires in
+  // issue order, so the head's fc-plane loads or the render's stores queue behind them
+  // (profiles/r3_fused_step_wpos_ab.txt).
   bf16x8 bw2[16], bw3[18];
-  if constexpr (WPOS == 1) trunk_w23_load(W2, W3, bw2, bw3);
-  if (ff.cnt && e < FF_HELPERS) ff_stage_w(ff, e, r, s_wfc);   // lands while the head, env and conv1 run
   // ---------------------------------------------------------------- policy head (every row workgroup of env e)
   float hf[2];
   fc_h2_from_parts(fc.hpart, fc.S, fc.plane_stride, fc.bfc, e, tid, lead ? h : nullptr, hf);
@@ -1050,7 +777,6 @@ __global__ void __launch_bounds__(T_THREADS) pong_fused_step_kernel(
     }
   }
   __syncthreads();
-  if constexpr (WPOS == 2) trunk_w23_load(W2, W3, bw2, bw3);
   if (wid == 0) {
     const int64_t key = tg0 * ((int64_t)1 << key_shift) + id0;   // pre-step counter
     const int jj = lane < A1 ? lane : 0;
@@ -1132,8 +858,8 @@ __global__ void __launch_bounds__(T_THREADS) pong_fused_step_kernel(
   }
   __syncthreads();
   stamp(stamps, 1);
-  trunk_rows_compute<WPOS != 0 ? 2 : 1>(s_in, s_w1, s_y1, s_y2, e, r, bias1a, bias1b, bias2, bias3, W2, W3, y1g, y2g,
-                                      y3g, scale, stamps, bw2, bw3, ff, s_y3, s_wfc);
+  trunk_rows_compute<1>(s_in, s_w1, s_y1, s_y2, e, r, bias1a, bias1b, bias2, bias3, W2, W3, y1g, y2g, y3g, scale,
+                        stamps, bw2, bw3);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -1709,79 +1435,31 @@ extern "C" hipError_t aca_cnn_trunk_fwd(const uint8_t* obs, const uint16_t* W1, 
                                         uint16_t* y2, uint16_t* y3, int B, float scale, uint8_t* shift_out,
                                         uint64_t* stamps, const int64_t* obs_idx, hipStream_t stream) {
   if (B <= 0) return hipSuccess;
-  // persistent walk (one workgroup per CU) for learner batches: ACA_TRUNK_FWD_PERSIST workgroups (0 = off)
-  static const int persist = [] {
-    const char* v = getenv("ACA_TRUNK_FWD_PERSIST");
-    return v ? atoi(v) : 0;   // measured slower than the per-env kernel on Breakout PPO (17.45 vs 17.18 ms)
-  }();
-  static const int persist_min_b = [] {
-    const char* v = getenv("ACA_TRUNK_FWD_PERSIST_MIN_B");
-    return v ? atoi(v) : 1024;
-  }();
-  // lean-LDS per-env form (two workgroups per CU); ACA_TRUNK_FWD_U8=0 keeps the bf16-staged form
-  static const bool u8 = [] {
-    const char* v = getenv("ACA_TRUNK_FWD_U8");
-    return !v || v[0] != '0';
-  }();
-  // obs_idx (gathered rows): only the lean-LDS per-env kernel reads through the index
-  if (obs_idx && !(u8 && !stamps)) return hipErrorInvalidValue;
-  // opt-in (ACA_TRUNK_FWD_WIDE_MAX_B=256): 8-wave workgroups while the batch leaves CUs idle. Measured SLOWER on the
-  // Breakout rollout (18.7 vs 15.8 us per 128-env step, 16.35 vs 15.86 ms per update, profiles/r3_breakout_ab2.txt):
-  // the 4-wave form's two-workgroups-per-CU placement already spreads 128 envs, and the extra waves add barrier time
-  static const int wide_max_b = [] {
-    const char* v = getenv("ACA_TRUNK_FWD_WIDE_MAX_B");
-    return v ? atoi(v) : 0;
-  }();
-  if (u8 && !stamps && (obs_idx || !(persist > 0 && B >= persist_min_b && !shift_out))) {
-    if (B <= wide_max_b)
-      aca::cnn_trunk_fwd_u8_kernel<8><<<B, 512, 0, stream>>>(obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale,
-                                                            shift_out, obs_idx);
-    else
-      aca::cnn_trunk_fwd_u8_kernel<4><<<B, 256, 0, stream>>>(obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale,
-                                                            shift_out, obs_idx);
+  // the lean-LDS per-env form (two workgroups per CU) unless phase stamps are asked for: those live in the
+  // bf16-staged per-env kernel (diagnostic builds, scripts/microbench_*.py). Only the lean form reads through
+  // an index (obs_idx: gathered minibatch rows).
+  if (!stamps) {
+    aca::cnn_trunk_fwd_u8_kernel<4><<<B, 256, 0, stream>>>(obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale, shift_out,
+                                                          obs_idx);
     return hipGetLastError();
   }
-  if (persist > 0 && B >= persist_min_b && !shift_out && !stamps) {
-    aca::cnn_trunk_fwd_persist_kernel<<<persist < B ? persist : B, aca::T_THREADS, 0, stream>>>(
-        obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale, B);
-    return hipGetLastError();
-  }
+  if (obs_idx) return hipErrorInvalidValue;
   aca::cnn_trunk_fwd_kernel<<<B, aca::T_THREADS, 0, stream>>>(obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale,
                                                                shift_out, stamps);
   return hipGetLastError();
 }
 
-namespace aca {
-// The fold's helpers spin on their row's arrivals: every workgroup of the launch must be resident at once. N in
-// {16, 32} and (occupancy per CU) x (CUs) >= 7 N, evaluated once per kernel.
-inline bool ff_coresident(const void* kernel, int N) {
-  if (N != 16 && N != 32) return false;
-  int dev = 0, cus = 0, per = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, T_THREADS, 0) != hipSuccess)
-    return false;
-  return (int64_t)per * cus >= (int64_t)N * TR_ROWS;
-}
-}  // namespace aca
-
 extern "C" hipError_t aca_cnn_trunk_rows(const uint8_t* obs, const uint16_t* W1, const float* b1, const uint16_t* W2,
                                          const float* b2, const uint16_t* W3, const float* b3, uint16_t* y1,
                                          uint16_t* y2, uint16_t* y3, int B, float scale, uint8_t* shift_out,
-                                         uint8_t* copy_out, uint64_t* stamps, int late_w, const uint16_t* ff_w,
-                                         float* ff_planes, unsigned int* ff_cnt, hipStream_t stream) {
+                                         uint8_t* copy_out, uint64_t* stamps, int late_w, hipStream_t stream) {
   if (B <= 0) return hipSuccess;
-  aca::FcFold ff{ff_w, ff_planes, ff_cnt, B};
-  if (ff_cnt) {
-    const void* k = late_w ? (const void*)aca::cnn_trunk_rows_kernel<true> : (const void*)aca::cnn_trunk_rows_kernel<false>;
-    if (!ff_w || !ff_planes || !aca::ff_coresident(k, B)) return hipErrorInvalidValue;
-  }
   if (late_w)
     aca::cnn_trunk_rows_kernel<true><<<B * aca::TR_ROWS, aca::T_THREADS, 0, stream>>>(
-        obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale, shift_out, copy_out, stamps, ff);
+        obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale, shift_out, copy_out, stamps);
   else
     aca::cnn_trunk_rows_kernel<false><<<B * aca::TR_ROWS, aca::T_THREADS, 0, stream>>>(
-        obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale, shift_out, copy_out, stamps, ff);
+        obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale, shift_out, copy_out, stamps);
   return hipGetLastError();
 }
 
@@ -1807,10 +1485,8 @@ extern "C" hipError_t aca_pong_fused_step(
     int64_t* tg_n, float* ep_ret_n, float* ep_stats, const int64_t* ids, const uint8_t* prev, uint8_t* out,
     float* reward, uint8_t* done, uint8_t* trunc, uint32_t seed, int max_steps, const uint16_t* W1, const float* b1,
     const uint16_t* W2, const float* b2, const uint16_t* W3, const float* b3, uint16_t* y1, uint16_t* y2,
-    uint16_t* y3, float scale, uint8_t* shift_out, uint64_t* stamps, int N, const uint16_t* ff_w, float* ff_planes,
-    unsigned int* ff_cnt, hipStream_t stream) {
+    uint16_t* y3, float scale, uint8_t* shift_out, uint64_t* stamps, int N, hipStream_t stream) {
   if (N <= 0) return hipSuccess;
-  aca::FcFold ff{ff_w, ff_planes, ff_cnt, N};
   aca::PongIO io;
   io.state = state; io.tsteps = t; io.tglob = tg; io.ep_ret = ep_ret; io.ep_stats = ep_stats; io.env_ids = ids;
   io.prev = prev; io.out = out; io.reward = reward; io.done_out = done; io.trunc_out = trunc; io.seed = seed;
@@ -1818,42 +1494,12 @@ extern "C" hipError_t aca_pong_fused_step(
   aca::PongNext nx{state_n, t_n, tg_n, ep_ret_n};
   aca::FcParts fc{hpart, S, plane_stride, bfc};
   const int grid = N * aca::TR_ROWS;
-  // ACA_FUSED_WPOS (read once): where the conv2 / conv3 weight fragments are requested -- 0 after conv1's MFMAs
-  // (default), 1 at kernel entry, 2 after the policy head (see pong_fused_step_kernel; both measured slower)
-  static const int wpos = [] {
-    const char* v = getenv("ACA_FUSED_WPOS");
-    return v && (v[0] == '1' || v[0] == '2') ? v[0] - '0' : 0;
-  }();
-  if (ff_cnt) {
-    const void* k = nullptr;
-    switch (A + 1) {
-#define ACA_FUSED_K(A1) \
-  case A1:                                                                                                       \
-    k = wpos == 2 ? (const void*)aca::pong_fused_step_kernel<A1, 2>                                              \
-                  : (wpos == 1 ? (const void*)aca::pong_fused_step_kernel<A1, 1>                                 \
-                               : (const void*)aca::pong_fused_step_kernel<A1, 0>);                               \
-    break;
-      ACA_FUSED_K(3) ACA_FUSED_K(4) ACA_FUSED_K(5) ACA_FUSED_K(6) ACA_FUSED_K(7)
-#undef ACA_FUSED_K
-      default: return hipErrorInvalidValue;
-    }
-    if (!ff_w || !ff_planes || ff_planes == hpart || !aca::ff_coresident(k, N)) return hipErrorInvalidValue;
-  }
   switch (A + 1) {
 #define ACA_FUSED_CASE(A1)                                                                                       \
   case A1:                                                                                                       \
-    if (wpos == 2)                                                                                               \
-      aca::pong_fused_step_kernel<A1, 2><<<grid, aca::T_THREADS, 0, stream>>>(                                   \
-          io, nx, fc, h, Wh, bh, z, act, logp, ent, value, key_shift, pseed, W1, b1, W2, b2, W3, b3, y1, y2, y3,  \
-          scale, shift_out, stamps, ff);                                                                         \
-    else if (wpos == 1)                                                                                          \
-      aca::pong_fused_step_kernel<A1, 1><<<grid, aca::T_THREADS, 0, stream>>>(                                   \
-          io, nx, fc, h, Wh, bh, z, act, logp, ent, value, key_shift, pseed, W1, b1, W2, b2, W3, b3, y1, y2, y3,  \
-          scale, shift_out, stamps, ff);                                                                         \
-    else                                                                                                         \
-      aca::pong_fused_step_kernel<A1, 0><<<grid, aca::T_THREADS, 0, stream>>>(                                   \
-          io, nx, fc, h, Wh, bh, z, act, logp, ent, value, key_shift, pseed, W1, b1, W2, b2, W3, b3, y1, y2, y3,  \
-          scale, shift_out, stamps, ff);                                                                         \
+    aca::pong_fused_step_kernel<A1><<<grid, aca::T_THREADS, 0, stream>>>(                                        \
+        io, nx, fc, h, Wh, bh, z, act, logp, ent, value, key_shift, pseed, W1, b1, W2, b2, W3, b3, y1, y2, y3,    \
+        scale, shift_out, stamps);                                                                               \
     break;
     ACA_FUSED_CASE(3) ACA_FUSED_CASE(4) ACA_FUSED_CASE(5) ACA_FUSED_CASE(6) ACA_FUSED_CASE(7)
 #undef ACA_FUSED_CASE

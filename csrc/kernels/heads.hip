@@ -80,67 +80,7 @@ __global__ void gaussian_sample_kernel(const float* __restrict__ mu, int ldm, in
   ent[row] = H;
 }
 
-// Policy/value head of a large learner batch (PPO minibatches, B in the thousands):
-//   z[b][j] = bh[j] + sum_k h[b][k] Wh[k][j]        h bf16 [B][512], Wh bf16 [512][A1] (ld A1), z fp32 [B][A1]
-// The generic GEMM runs this N = A1 <= 8 product in few workgroups that walk every k-step of an unaligned
-// [512][A1] operand (~15 us at B = 4096); here 8 lanes share a row, each reading 8 interleaved 16-byte chunks of it
-// (8 consecutive lanes cover 128 contiguous bytes), with Wh staged once per workgroup in LDS as fp32. Lane sums are
-// combined in a fixed xor tree: deterministic, not bit-equal to the MFMA order of the GEMM path.
-constexpr int HF_ROWS = 32;   // rows per 256-thread workgroup
-
-template <int A1>
-__global__ void __launch_bounds__(256) head_fwd_kernel(const u16* __restrict__ h, const u16* __restrict__ Wh,
-                                                       const float* __restrict__ bh, float* __restrict__ z, int B) {
-  __shared__ float s_w[512 * A1];
-  for (int i = threadIdx.x; i < 512 * A1; i += 256) s_w[i] = bf2f(Wh[i]);
-  const int g = threadIdx.x >> 3, t = threadIdx.x & 7;
-  const int row = blockIdx.x * HF_ROWS + g;
-  uint4 v[8];
-  const uint4* hp = reinterpret_cast<const uint4*>(h + (size_t)min(row, B - 1) * 512);
-#pragma unroll
-  for (int c = 0; c < 8; ++c) v[c] = hp[c * 8 + t];   // chunk c * 8 + t: k = 64 c + 8 t + e
-  __syncthreads();
-  float acc[A1];
-#pragma unroll
-  for (int j = 0; j < A1; ++j) acc[j] = 0.f;
-#pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    const uint32_t w[4] = {v[c].x, v[c].y, v[c].z, v[c].w};
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float x = __uint_as_float((e & 1) ? (w[e >> 1] & 0xFFFF0000u) : (w[e >> 1] << 16));
-      const float* wr = s_w + (64 * c + 8 * t + e) * A1;
-#pragma unroll
-      for (int j = 0; j < A1; ++j) acc[j] += x * wr[j];
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < A1; ++j) {
-    acc[j] += __shfl_xor(acc[j], 1, 64);
-    acc[j] += __shfl_xor(acc[j], 2, 64);
-    acc[j] += __shfl_xor(acc[j], 4, 64);
-  }
-  if (t == 0 && row < B)
-#pragma unroll
-    for (int j = 0; j < A1; ++j) z[(size_t)row * A1 + j] = acc[j] + bh[j];
-}
-
 }  // namespace aca
-
-extern "C" hipError_t aca_head_fwd(const uint16_t* h, const uint16_t* Wh, const float* bh, float* z, int B, int A1,
-                                   hipStream_t stream) {
-  if (B <= 0) return hipSuccess;
-  if ((reinterpret_cast<uintptr_t>(h) & 15) != 0) return hipErrorInvalidValue;
-  const int grid = (B + aca::HF_ROWS - 1) / aca::HF_ROWS;
-  switch (A1) {
-#define ACA_HF(N) \
-  case N: aca::head_fwd_kernel<N><<<grid, 256, 0, stream>>>(h, Wh, bh, z, B); break;
-    ACA_HF(2) ACA_HF(3) ACA_HF(4) ACA_HF(5) ACA_HF(6) ACA_HF(7) ACA_HF(8)
-#undef ACA_HF
-    default: return hipErrorInvalidValue;
-  }
-  return hipGetLastError();
-}
 
 extern "C" hipError_t aca_categorical_sample(const float* logits, int ldl, int B, int A, const int64_t* keys,
                                              const int64_t* tg, const int64_t* ids, int key_shift, uint32_t seed,

@@ -697,272 +697,6 @@ __global__ void __launch_bounds__(256) mlp_wgrad_kernel(WgradArgs a) {
   }
 }
 
-// ------------------------------------------------------------------------------------------------ wgrad + Adam
-// mlp_wgrad_adam_kernel: the weight-gradient launch above with the optimiser step folded in (one launch per PPO
-// minibatch instead of wgrad + opt_multi). Same tiles, same bookkeeping workgroup; then every workgroup meets the
-// others at a grid barrier (the sum-of-squares slots are the only cross-workgroup data: sc1 stores / loads, no L2
-// write-back), reduces its tower's global norm exactly as opt_multi does (block_sum over the 256 slots: bit-identical
-// scale), and applies clip + Adam to the elements it owns -- wave 0 of a tile workgroup holds its 16x16 dW tile (and
-// the tile row's bias sums) in registers, the bookkeeping workgroup the log-std gradient -- writing p, m, v and the
-// transposed forward shadow Wt. The gradient never reaches the slab (the unfused path leaves it zeroed by the
-// optimiser, so the end states match). Adam's step counts are read before the barrier and advanced by workgroup 0
-// after it. The barrier needs every workgroup co-resident (~360 small workgroups; the launcher checks).
-constexpr unsigned int WGO_SPIN_LIMIT = 1u << 21;
-// barrier words (uint32), every counter / flag on a 128-byte line of its own: shard arrivals [x * LINE], top
-// counter, shard release flags [GO + x * LINE], departures, timeout flag; WGO_BAR_WORDS in total (host: mlp.py)
-constexpr unsigned int WGO_SHARDS = 8, WGO_LINE = 32;
-constexpr unsigned int WGO_TOP = 8 * WGO_LINE, WGO_GO = 9 * WGO_LINE, WGO_DEP = 17 * WGO_LINE, WGO_ERR = 18 * WGO_LINE;
-constexpr unsigned int WGO_BAR_WORDS = 19 * WGO_LINE;
-
-__device__ __forceinline__ float wgo_ld(const float* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void wgo_st(float* p, float v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// clip + (global-norm) scale + Adam, the operation order of optim.hip opt_body (gmul = 1); the compiler's fp
-// contraction may still round the last bit differently in the two kernels
-__device__ __forceinline__ void wgo_adam(float gi, float clip, float scale, float b1, float b2, float eps, float lr_t,
-                                         float& pi, float& mi, float& vi) {
-  if (clip > 0.f) gi = fminf(fmaxf(gi, -clip), clip);
-  gi *= scale;
-  vi = b2 * vi + (1.0f - b2) * gi * gi;
-  mi = b1 * mi + (1.0f - b1) * gi;
-  pi -= lr_t * mi / (sqrtf(vi) + eps);
-}
-
-__global__ void __launch_bounds__(256) mlp_wgrad_adam_kernel(WgradArgs a) {
-  __shared__ float red[4][64][5];
-  __shared__ float shr[16];
-  const WgradOpt& O = a.opt;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int ntw = a.ntw;
-  // operands read before the barrier (workgroup 0 rewrites the step counts after it)
-  float tnew[2] = {0.f, 0.f}, lrv[2] = {0.f, 0.f};
-  for (int q = 0; q < ntw; ++q) {
-    tnew[q] = *O.t[q] + 1.0f;
-    lrv[q] = *O.lr[q];
-  }
-  const bool book = blockIdx.x == gridDim.x - 1;
-  int t = 0, l = 0, K = 0, N = 0, i0 = 0, j0 = 0, ti = 0;
-  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-  float bsum = 0.f, g_ls = 0.f;
-  if (book) {
-    if (wave == 0) {
-      float v[MPART_W];
-#pragma unroll
-      for (int c = 0; c < MPART_W; ++c) v[c] = 0.f;
-      if (a.mpart) {
-        for (int row = lane; row < a.mpart_rows; row += 64) {
-#pragma unroll
-          for (int c = 0; c < MPART_W; ++c) v[c] += a.mpart[(size_t)row * MPART_W + c];
-        }
-#pragma unroll
-        for (int c = 0; c < MPART_W; ++c) v[c] = wave_sum(v[c]);
-      }
-      if (a.g_log_std && lane < a.A) {
-        float g = a.g_log_std[lane];
-        if (a.mpart) {
-          float part = 0.f;
-#pragma unroll
-          for (int j = 0; j < MLP_MAXA; ++j) part = lane == j ? v[8 + j] : part;
-          g += part;
-        }
-        g_ls = g;
-        a.g_log_std[lane] = 0.f;   // the unfused optimiser leaves the gradient slab zeroed
-      }
-      if (a.g_log_std && a.parts[0]) {
-        const float ss = wave_sum(lane < a.A ? clipsq(g_ls, a.clip[0]) : 0.f);
-        if (lane == 0) wgo_st(&a.parts[0][a.items[0]], ss);
-      }
-      if (lane == 0) {
-        if (a.mpart)
-          for (int k = 0; k < 8; ++k) a.mstats[k] += v[k];
-        if (a.stats) {
-          float m[8];
-          for (int k = 0; k < 8; ++k) m[k] = a.mstats[k];
-          m[5] = m[0] + (*a.kl_coef) * m[1] - (*a.ent_coef) * m[2];
-          for (int k = 0; k < 7; ++k) a.stats[k] = m[k];
-          for (int k = 0; k < 8; ++k) a.mstats[k] = 0.f;
-        }
-        if (a.bump) *a.bump += 1;
-      }
-    }
-  } else {
-    int item = blockIdx.x;
-    if (item >= a.items[0]) {
-      item -= a.items[0];
-      t = 1;
-    }
-    const int local_item = item;
-    const MlpTower& T = a.tw[t];
-    const int nl = (int)T.nl;
-    for (l = 0; l < nl; ++l) {
-      const int n = (((int)T.in[l] + 15) >> 4) * (((int)T.out[l] + 15) >> 4);
-      if (item < n) break;
-      item -= n;
-    }
-    K = (int)T.in[l];
-    N = (int)T.out[l];
-    const int tn = (N + 15) >> 4;
-    ti = item / tn;
-    const int tj = item - ti * tn;
-    i0 = ti * 16;
-    j0 = tj * 16;
-    const int r = lane & 15, q = lane >> 4;
-    gcf32* X = P_<const float>(T.xs[l]);
-    gcf32* P = P_<const float>(T.dp[l]);
-    const int iac = i0 + r < K ? i0 + r : 0, jbc = j0 + r < N ? j0 + r : 0;
-    for (int c0 = wave * 4 * WG_CHUNK; c0 < a.B; c0 += 16 * WG_CHUNK) {
-      float av[WG_CHUNK], bv[WG_CHUNK];
-#pragma unroll
-      for (int u = 0; u < WG_CHUNK; ++u) {
-        const int row = c0 + 16 * (u >> 2) + 4 * q + (u & 3);
-        av[u] = X[(size_t)row * K + iac];
-        bv[u] = P[(size_t)row * N + jbc];
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int u = 0; u < WG_CHUNK; ++u) {
-        acc = mfma4(av[u], bv[u], acc);
-        bsum += bv[u];
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) red[wave][lane][i] = acc[i];
-    red[wave][lane][4] = bsum;
-    __syncthreads();
-    if (wave == 0) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) acc[i] = red[0][lane][i] + red[1][lane][i] + red[2][lane][i] + red[3][lane][i];
-      bsum = red[0][lane][4] + red[1][lane][4] + red[2][lane][4] + red[3][lane][4];
-      float ss = 0.f;
-      const float c = a.clip[t];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int ii = i0 + 4 * q + i, jj = j0 + r;
-        if (ii < K && jj < N) ss += clipsq(acc[i], c);
-      }
-      if (ti == 0) {
-        bsum += __shfl_xor(bsum, 16, 64);
-        bsum += __shfl_xor(bsum, 32, 64);
-        if (q == 0 && j0 + r < N) ss += clipsq(bsum, c);
-      }
-      if (a.parts[t]) {
-        ss = wave_sum(ss);
-        if (lane == 0) wgo_st(&a.parts[t][local_item], ss);
-        if (local_item == 0) {
-          const int first = a.items[t] + (t == 0 && a.g_log_std ? 1 : 0);
-          for (int k = first + lane; k < MLP_PARTS; k += 64) wgo_st(&a.parts[t][k], 0.f);
-        }
-      }
-    }
-  }
-  // ---- grid barrier, sharded by blockIdx % 8 (the XCD under round-robin placement: speed only, any sharding is
-  // correct): a shard's arrivals go to its own counter line; the shard's last arriver (told by the returned count)
-  // adds to the top counter; the last shard's leader raises every shard's release flag; each workgroup polls only its
-  // shard's flag. Every sum-of-squares slot was stored sc1 and acknowledged before its workgroup's arrival.
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  {
-    const unsigned int G = gridDim.x, x = blockIdx.x & (WGO_SHARDS - 1);
-    const unsigned int nsh = G < WGO_SHARDS ? G : WGO_SHARDS;
-    const unsigned int nx = (G - x + WGO_SHARDS - 1) / WGO_SHARDS;
-    if (tid == 0) {
-      const unsigned int prev =
-          __hip_atomic_fetch_add(&O.bar[x * WGO_LINE], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (prev == nx - 1u) {
-        const unsigned int done =
-            __hip_atomic_fetch_add(&O.bar[WGO_TOP], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (done == nsh - 1u)
-          for (unsigned int y = 0; y < nsh; ++y)
-            __hip_atomic_store(&O.bar[WGO_GO + y * WGO_LINE], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      unsigned int spins = 0;
-      while (__hip_atomic_load(&O.bar[WGO_GO + x * WGO_LINE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++spins > WGO_SPIN_LIMIT) {
-          __hip_atomic_store(&O.bar[WGO_ERR], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-      }
-    }
-  }
-  __syncthreads();
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  // ---- global norms: opt_multi's partial_total (one slot per thread, block_sum) -> identical bits
-  float scale[2] = {1.f, 1.f};
-  for (int q = 0; q < ntw; ++q) {
-    if (!(a.parts[q] && O.max_norm[q] > 0.f)) continue;
-    if (!(blockIdx.x == 0 || (book ? q == 0 : q == t))) continue;
-    float v = 0.f;
-    for (int i = tid; i < MLP_PARTS; i += 256) v += wgo_ld(&a.parts[q][i]);
-    const float gsq = block_sum(v, shr);
-    scale[q] = grad_scale(gsq, O.max_norm[q]);
-    if (blockIdx.x == 0 && tid == 0 && O.gnorm[q]) *O.gnorm[q] = gsq;
-  }
-  // ---- Adam on the elements this workgroup owns
-  const float b1 = O.b1, b2 = O.b2, eps = O.eps;
-  if (book) {
-    if (wave == 0 && a.g_log_std && O.log_std && lane < a.A) {
-      const float lr_t = lrv[0] * sqrtf(1.0f - powf(b2, tnew[0])) / (1.0f - powf(b1, tnew[0]));
-      const size_t o = (size_t)(O.log_std - O.p0[0]) + lane;
-      float pi = O.log_std[lane], mi = O.m[0][o], vi = O.v[0][o];
-      wgo_adam(g_ls, a.clip[0], scale[0], b1, b2, eps, lr_t, pi, mi, vi);
-      O.log_std[lane] = pi;
-      O.m[0][o] = mi;
-      O.v[0][o] = vi;
-    }
-  } else if (wave == 0) {
-    const MlpTower& T = a.tw[t];
-    const int r = lane & 15, q = lane >> 4;
-    const float lr_t = lrv[t] * sqrtf(1.0f - powf(b2, tnew[t])) / (1.0f - powf(b1, tnew[t]));
-    const float c = a.clip[t];
-    gf32* W = P_<float>(T.W[l]);
-    gf32* Wt = P_<float>(T.Wt[l]);
-    const int ldt = 16 * ngp2(K);
-    const size_t wo = (size_t)((T.W[l] - reinterpret_cast<int64_t>(O.p0[t])) / 4);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int ii = i0 + 4 * q + i, jj = j0 + r;
-      if (ii < K && jj < N) {
-        const size_t e = (size_t)ii * N + jj;
-        float pi = W[e], mi = O.m[t][wo + e], vi = O.v[t][wo + e];
-        wgo_adam(acc[i], c, scale[t], b1, b2, eps, lr_t, pi, mi, vi);
-        W[e] = pi;
-        O.m[t][wo + e] = mi;
-        O.v[t][wo + e] = vi;
-        Wt[(size_t)jj * ldt + ii] = pi;
-      }
-    }
-    if (ti == 0 && q == 0 && j0 + r < N) {
-      gf32* bp = P_<float>(T.b[l]);
-      const size_t bo = (size_t)((T.b[l] - reinterpret_cast<int64_t>(O.p0[t])) / 4) + j0 + r;
-      float pi = bp[j0 + r], mi = O.m[t][bo], vi = O.v[t][bo];
-      wgo_adam(bsum, c, scale[t], b1, b2, eps, lr_t, pi, mi, vi);
-      bp[j0 + r] = pi;
-      O.m[t][bo] = mi;
-      O.v[t][bo] = vi;
-    }
-  }
-  // ---- departure: workgroup 0 advances the step counts (every workgroup read them before the barrier); the last
-  // workgroup out resets the barrier for the next launch (stream-ordered)
-  if (tid == 0) {
-    if (blockIdx.x == 0)
-      for (int q = 0; q < ntw; ++q) *O.t[q] = tnew[q];
-    const unsigned int prev = __hip_atomic_fetch_add(&O.bar[WGO_DEP], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == gridDim.x - 1u) {   // every workgroup is past its poll: reset the shard counters, top, flags
-      for (unsigned int y = 0; y < WGO_SHARDS; ++y) {
-        __hip_atomic_store(&O.bar[y * WGO_LINE], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&O.bar[WGO_GO + y * WGO_LINE], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      __hip_atomic_store(&O.bar[WGO_TOP], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&O.bar[WGO_DEP], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
 // Wt[c][k] = W[k][c] (rows padded to 16 * ngp2(K), pad stays zero) for every layer of the launched towers: the
 // forward's B operand. One thread per weight element; runs after each optimiser step (and at engine creation).
 __global__ void __launch_bounds__(256) mlp_tshadow_kernel(const MlpTower* __restrict__ tw, int ntw, int total) {
@@ -1325,24 +1059,6 @@ extern "C" hipError_t aca_mlp_wgrad(const WgradArgs* a, hipStream_t stream) {
     if (a->parts[t] && a->nsplit == 1 && a->items[t] > MLP_PARTS) return hipErrorInvalidValue;
   if (a->g_log_std && a->parts[0] && a->nsplit == 1 && a->items[0] >= MLP_PARTS) return hipErrorInvalidValue;
   const int total = a->items[0] + (a->ntw > 1 ? a->items[1] : 0);
-  if (a->fuse) {
-    // every workgroup co-resident for the grid barrier (checked once per process against the occupancy)
-    static int cap = [] {
-      int dev = 0, cus = 0, per = 0;
-      if (hipGetDevice(&dev) != hipSuccess ||
-          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-          hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&mlp_wgrad_adam_kernel), 256,
-                                                       0) != hipSuccess)
-        return 0;
-      return per * cus;
-    }();
-    const WgradOpt& O = a->opt;
-    if (a->nsplit != 1 || total + 1 > cap || !O.bar || !O.p0[0] || !O.m[0] || !O.v[0] || !O.lr[0] || !O.t[0] ||
-        (a->ntw > 1 && (!O.p0[1] || !O.m[1] || !O.v[1] || !O.lr[1] || !O.t[1])) || (a->g_log_std && !O.log_std))
-      return hipErrorInvalidValue;
-    mlp_wgrad_adam_kernel<<<total + 1, 256, 0, stream>>>(*a);
-    return hipGetLastError();
-  }
   // + the bookkeeping workgroup (statistics, log-std gradient, update counter)
   mlp_wgrad_kernel<<<total * a->nsplit + 1, 256, 0, stream>>>(*a);
   return hipGetLastError();

@@ -51,17 +51,6 @@ struct MlpArgs {
   int64_t* stamps;            // optional diagnostics: [2 towers][16] s_memrealtime at phase ends of workgroup (0, tower)
 };
 
-// Adam fused into the weight-gradient launch (mlp_wgrad_adam_kernel): per tower = optimiser group (actor | critic).
-struct WgradOpt {
-  float* p0[2];               // first parameter of the group's slab segment (m / v are indexed from it)
-  float* m[2]; float* v[2];   // the group's Adam moments
-  const float* lr[2]; float* t[2]; float* gnorm[2];   // device scalars: lr, step count, global-norm output
-  float max_norm[2];          // <= 0: no global-norm clip
-  float* log_std;             // the actor's log-std parameter (tower 0's group), null if none
-  float b1, b2, eps;
-  unsigned int* bar;          // [4] grid barrier words (zero between launches)
-};
-
 struct WgradArgs {
   const MlpTower* tw;
   int ntw;
@@ -74,8 +63,6 @@ struct WgradArgs {
   int items[2];               // 16x16 tiles per tower (host-computed)
   const float* mpart; int mpart_rows;   // the train kernel's partial rows (reduced here in a fixed order)
   int64_t* bump;              // optional counter advanced once (PPO update counter after the update's last minibatch)
-  int fuse;                   // 1: mlp_wgrad_adam_kernel (the gradient never reaches the slab; Adam applied in-launch)
-  WgradOpt opt;
 };
 
 // Fused rollout of the MuJoCo-shaped linear bank (mlp_rollout_kernel): T steps of actor + Gaussian sample + env step.

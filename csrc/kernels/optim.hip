@@ -382,126 +382,6 @@ __global__ void __launch_bounds__(OPT_THREADS) grad_finalize_kernel(const int64_
   if (threadIdx.x == 0) partial[blockIdx.x] = s;
 }
 
-// ---------------------------------------------------------------------------------------------------------------
-// Finaliser + optimiser in ONE launch (single-group update, no data parallelism): workgroup j finalises job j into
-// LDS (plane reductions in fixed order, read-only segments read and zeroed), publishes its sum-of-squares partial,
-// and meets every other workgroup at a grid barrier; each then reduces the same partials in the same order (the
-// global norm, deterministic), and applies the clip + Adam / RMSprop update to ITS job's elements from the LDS copy.
-// Versus finaliser + optimiser launches this drops the gradient's write + re-read + zeroing pass over the slab and
-// a kernel boundary. Plane-reduced gradients never touch the slab (it stays zero between updates).
-// The barrier needs every workgroup resident at once: the host launches at most (CUs x resident blocks per CU)
-// jobs (checked with the occupancy API). Its spin is bounded: if it ever times out the workgroup records the
-// failure in `err` and skips its update (no hang; the caller checks `err`).
-// State words: [0] arrivals, [1] departures (the last one resets both), [2] error flag.
-constexpr int FINOPT_MAXN = 12288;   // elements per job held in LDS (48 KB)
-constexpr unsigned int FINOPT_SPIN_LIMIT = 1u << 22;
-
-template <bool ADAM>
-__global__ void __launch_bounds__(OPT_THREADS) grad_finalize_opt_kernel(const int64_t* __restrict__ jobs, int njobs,
-                                                                        float* __restrict__ partial, OptSeg S,
-                                                                        const float* __restrict__ gbase, float b1,
-                                                                        float b2, float eps,
-                                                                        unsigned int* __restrict__ state) {
-  __shared__ float sh[16];
-  __shared__ float red[16 * 64];
-  __shared__ __attribute__((aligned(16))) float s_g[FINOPT_MAXN];
-  __shared__ int s_ok;
-  const int64_t* w = jobs + (int64_t)blockIdx.x * FIN_WORDS;
-  const int tid = threadIdx.x;
-  // operands of phase 2 that do not depend on the barrier, requested first
-  const float lr = *S.lr;
-  const float t = ADAM ? (*S.t + 1.0f) : 0.f;
-  float s = fin_job<true>(w, s_g, red);
-  s = block_sum(s, sh);
-  if (tid == 0) {
-    __hip_atomic_store(&partial[blockIdx.x], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_fetch_add(&state[0], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    unsigned int spins = 0;
-    int ok = 1;
-    while (__hip_atomic_load(&state[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < (unsigned int)njobs) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > FINOPT_SPIN_LIMIT) { ok = 0; break; }
-    }
-    if (!ok) __hip_atomic_store(&state[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_ok = ok;
-  }
-  __syncthreads();
-  const bool ok = s_ok != 0;
-  if (ok) {
-    // global norm: every workgroup sums the same njobs partials in the same order
-    float v = 0.f;
-    for (int i = tid; i < njobs; i += OPT_THREADS)
-      v += __hip_atomic_load(&partial[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const float gsq = block_sum(v, sh) * S.norm_mul;
-    const float scale = S.parts ? grad_scale(gsq, S.max_norm) : 1.0f;
-    if (S.gnorm_out && blockIdx.x == 0 && tid == 0) *S.gnorm_out = gsq;
-    const float clip = S.clip, gmul = S.gmul;
-    float lr_t = lr;
-    if (ADAM) lr_t = lr * sqrtf(1.0f - powf(b2, t)) / (1.0f - powf(b1, t));
-    const float* dstp = reinterpret_cast<const float*>(w[0]);
-    const int n = (int)w[2];
-    const size_t off = (size_t)(dstp - gbase);   // element offset of the job in the segment
-    float* __restrict__ p = S.p + off;
-    float* __restrict__ vv = S.v + off;
-    float* __restrict__ m = ADAM ? S.m + off : nullptr;
-    u16* shadow = S.shadow ? S.shadow + off : nullptr;
-    auto upd = [&](float gi, float& vi, float& mi, float& pi) {
-      gi *= gmul;
-      if (clip > 0.f) gi = fminf(fmaxf(gi, -clip), clip);
-      gi *= scale;
-      vi = b2 * vi + (1.0f - b2) * gi * gi;
-      if (ADAM) {
-        mi = b1 * mi + (1.0f - b1) * gi;
-        pi -= lr_t * mi / (sqrtf(vi) + eps);
-      } else {
-        pi -= lr * gi / sqrtf(vi + eps);
-      }
-    };
-    if ((int)w[5] && (n & 3) == 0) {   // float4 (the job's slab range is 16-byte aligned: host-checked flag)
-      const int n4 = n >> 2;
-      for (int i = tid; i < n4; i += OPT_THREADS) {
-        const float4 g4 = reinterpret_cast<const float4*>(s_g)[i];
-        float4 v4 = reinterpret_cast<const float4*>(vv)[i];
-        float4 p4 = reinterpret_cast<const float4*>(p)[i];
-        float4 m4 = ADAM ? reinterpret_cast<const float4*>(m)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-        upd(g4.x, v4.x, m4.x, p4.x);
-        upd(g4.y, v4.y, m4.y, p4.y);
-        upd(g4.z, v4.z, m4.z, p4.z);
-        upd(g4.w, v4.w, m4.w, p4.w);
-        reinterpret_cast<float4*>(vv)[i] = v4;
-        if (ADAM) reinterpret_cast<float4*>(m)[i] = m4;
-        reinterpret_cast<float4*>(p)[i] = p4;
-        if (shadow) {
-          uint2 sv;
-          sv.x = (uint32_t)f2bf(p4.x) | ((uint32_t)f2bf(p4.y) << 16);
-          sv.y = (uint32_t)f2bf(p4.z) | ((uint32_t)f2bf(p4.w) << 16);
-          reinterpret_cast<uint2*>(shadow)[i] = sv;
-        }
-      }
-    } else {
-      for (int i = tid; i < n; i += OPT_THREADS) {
-        float vi = vv[i], pi = p[i], mi = ADAM ? m[i] : 0.f;
-        upd(s_g[i], vi, mi, pi);
-        vv[i] = vi;
-        if (ADAM) m[i] = mi;
-        p[i] = pi;
-        if (shadow) shadow[i] = f2bf(pi);
-      }
-    }
-  }
-  // departure ticket: the last workgroup out resets the barrier (and advances Adam's step count); a relaxed count
-  // is enough -- nothing is handed over through it, and the next launch is ordered after this one by the stream
-  __syncthreads();
-  if (tid == 0) {
-    const unsigned int prev = __hip_atomic_fetch_add(&state[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == (unsigned int)njobs - 1u) {
-      if (ADAM && ok) *S.t = t;
-      __hip_atomic_store(&state[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&state[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
 // lag-1 data parallelism: dst <- src, src <- 0 in one pass (the next backward accumulates into a clean slab while
 // dst is all-reduced and consumed by the next optimiser step)
 __global__ void __launch_bounds__(OPT_THREADS) grad_move_kernel(float* __restrict__ src, float* __restrict__ dst,
@@ -551,42 +431,6 @@ extern "C" int aca_sumsq_parts() { return SUMSQ_PARTS; }
 extern "C" hipError_t aca_grad_finalize(const int64_t* jobs, int njobs, float* partial, hipStream_t stream) {
   if (njobs < 1 || njobs > SUMSQ_PARTS) return hipErrorInvalidValue;
   grad_finalize_kernel<<<njobs, OPT_THREADS, 0, stream>>>(jobs, njobs, partial);
-  return hipGetLastError();
-}
-
-// Fused finaliser + optimiser (see grad_finalize_opt_kernel). `jobs` as aca_grad_finalize; the segment S covers the
-// slab range of every job (element offsets relative to `gbase`, the gradient base); state: 3 zeroed uint32 words.
-// Returns hipErrorInvalidValue when the jobs cannot all be resident at once (the caller falls back).
-extern "C" hipError_t aca_grad_finalize_opt(const int64_t* jobs, int njobs, int max_job_n, float* partial, float* p,
-                                            float* m, float* v, uint16_t* shadow, const float* gbase, const float* lr,
-                                            float* t, float* gnorm_out, float clip, float max_norm, float gmul,
-                                            float norm_mul, float b1, float b2, float eps, int adam,
-                                            unsigned int* state, hipStream_t stream) {
-  if (njobs < 1 || njobs > SUMSQ_PARTS || max_job_n > FINOPT_MAXN) return hipErrorInvalidValue;
-  static int resident = -1;
-  if (resident < 0) {
-    int dev = 0, cus = 0, per = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      return hipErrorInvalidValue;
-    hipError_t e = adam ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, grad_finalize_opt_kernel<true>,
-                                                                      OPT_THREADS, 0)
-                        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, grad_finalize_opt_kernel<false>,
-                                                                      OPT_THREADS, 0);
-    if (e != hipSuccess) return e;
-    resident = cus * per;
-  }
-  if (njobs > resident) return hipErrorInvalidValue;
-  if (adam && !t) return hipErrorInvalidValue;
-  OptSeg S{p, nullptr, m, v, 0, lr, t, partial, gnorm_out, shadow, clip, max_norm, gmul, norm_mul, nullptr, njobs,
-           0, {}};
-  if (max_norm <= 0.f) S.parts = nullptr;
-  if (adam)
-    grad_finalize_opt_kernel<true><<<njobs, OPT_THREADS, 0, stream>>>(jobs, njobs, partial, S, gbase, b1, b2, eps,
-                                                                     state);
-  else
-    grad_finalize_opt_kernel<false><<<njobs, OPT_THREADS, 0, stream>>>(jobs, njobs, partial, S, gbase, 0.f, b2, eps,
-                                                                      state);
   return hipGetLastError();
 }
 

@@ -215,12 +215,9 @@ def test_prp_permutation_kernel_matches_oracle(cuda):
         assert torch.equal(torch.sort(out.cpu()).values, torch.arange(n))
 
 
-@pytest.mark.parametrize("fused", ["1", "0"])
-def test_optimizer_writes_transposed_shadows(cuda, fused, monkeypatch):
-    """The optimiser keeps the MLP engine's transposed weight shadows equal to W^T after every step -- Adam folded
-    into the weight-gradient launch (fused = 1) or the multi-group optimiser launch (0) -- and checkpoint restore
-    refreshes them."""
-    monkeypatch.setenv("ACA_MLP_FUSED_OPT", fused)
+def test_optimizer_writes_transposed_shadows(cuda):
+    """The multi-group optimiser launch keeps the MLP engine's transposed weight shadows equal to W^T after every
+    step, and checkpoint restore refreshes them."""
     from actor_critic_algs_on_tensorflow_amd import preset
     from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
     tr = ActorCriticTrainer(preset("mujoco_ppo_dp8", num_envs=8, n_steps=16, ppo_epochs=1, ppo_minibatches=2,
@@ -229,10 +226,7 @@ def test_optimizer_writes_transposed_shadows(cuda, fused, monkeypatch):
     for _ in range(2):
         tr.step()
     torch.cuda.synchronize()
-    if fused == "1":
-        assert tr._mlp_fused_opt() is not None and getattr(tr, "_group_step", None) is None
-    else:
-        assert tr._group_step is not None and tr._group_step._trans is not None
+    assert tr._group_step is not None and tr._group_step._trans is not None
 
     def check():
         for tw in tr.mlp.towers:

@@ -321,9 +321,8 @@ def test_fused_rollout_step_equals_separate_policy_and_trunk(cuda, capture, monk
     from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
     runs = []
     for fused in ("1", "0"):
-        monkeypatch.setenv("ACA_FUSED_STEP", fused)
         tr = ActorCriticTrainer(preset("pong_a2c", num_envs=16, n_steps=5, device="cuda:0", outdir=None, quiet=True,
-                                       stdout_freq=0, save_every=0, seed=5))
+                                       stdout_freq=0, save_every=0, seed=5, engine_opts=dict(fused_step=fused == "1")))
         tr.env.max_episode_steps = 7
         if capture:
             tr.capture(warmup=1)

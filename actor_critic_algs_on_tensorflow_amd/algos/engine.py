@@ -141,6 +141,8 @@ class CNNEngine:
         self.fc_max_planes = min(FC_PLANES, o.fc_max_planes)
         self._hpart = {}
         self.last_fc = None
+        self._head_planes = {}   # plane sets written by ppo_head, merged into the next backward's finaliser jobs
+        self._ph = {}
         self.model = model
         self.flat = flat
         self.shadow = shadow
@@ -349,6 +351,36 @@ class CNNEngine:
         self._wsplits["W1"] = P
         self._cur_planes["W1"] = P
 
+    def ppo_head_ok(self, B):
+        """The large-batch head launch (``ppo_head.hip``) can take a learner batch of ``B`` rows: categorical head of
+        2..7 actions, the grouped deterministic backward that starts at the fc layer."""
+        return (self.opts.ppo_head and self.dev.type == "cuda" and 3 <= self.A1 <= 8 and self.grouped
+                and self.fused_bwd and self.det_wgrad and B >= 1)
+
+    def ppo_head(self, b: _Bufs, actions, logp_old, adv, ret, v_old, ent_coef, kl_coef, vf_coef, ppo_clip, v_clip,
+                 stats, z_out=None):
+        """z = h Wh + bh, the clipped-surrogate (or A2C) + value loss, dz, dh and the head's weight / bias gradient
+        planes in ONE launch (replaces the head GEMM, the loss launch, the dWh / dh GEMMs and the bias column sums).
+        ``b.h`` must hold the fc activations (``forward(head=False)``); :meth:`backward` then starts at the fc layer
+        (``head_done=True``) and its finaliser reduces the head planes."""
+        B, A1 = b.B, self.A1
+        ops = _native.require()
+        ph = self._ph.get(B)
+        if ph is None:
+            P = int(ops.ppo_head_planes(B))
+            dev = self.dev
+            ph = dict(P=P, Wh=torch.zeros(P * 512 * A1, device=dev), bh=torch.zeros(P * A1, device=dev),
+                      bfc=torch.zeros(P * 512, device=dev), st=torch.zeros(P * 6, dtype=torch.float64, device=dev),
+                      ticket=torch.zeros(1, dtype=torch.int32, device=dev))
+            self._ph[B] = ph
+        ops.ppo_head(b.h, self.sWh, self.bh, actions, logp_old, adv, ret, v_old if v_clip else None, ent_coef,
+                     kl_coef, float(vf_coef), float(ppo_clip or 0.0), float(v_clip or 0.0), b.dh, z_out, ph["Wh"],
+                     ph["bh"], ph["bfc"], ph["st"], ph["ticket"], stats)
+        for name in ("Wh", "bh", "bfc"):
+            self._planes["ph_" + name] = ph[name]
+        self._head_planes = {"ph_Wh": ph["P"], "ph_bh": ph["P"], "ph_bfc": ph["P"]}
+        return stats
+
     # limits of loss.hip head_bwd_kernel: B rows staged in LDS (HB_MAXB), the bootstrap row of N values after them
     HB_MAXB, HB_MAXN = 512, 256
 
@@ -408,7 +440,9 @@ class CNNEngine:
             if grouped:
                 return self._backward_grouped(b, stage, ws, ws2)
             return self._backward_trunk(b, main, side, ev, ws, ws2)
-        self._cur_planes = {}   # weight-gradient plane sets written by THIS backward (reduced by its finaliser)
+        # weight-gradient plane sets written by THIS backward (reduced by its finaliser), plus the head's planes when
+        # ppo_head ran just before it
+        self._cur_planes, self._head_planes = dict(self._head_planes) if head_done else {}, {}
         if grouped:
             return self._backward_grouped(b, stage, ws, ws2)
         head_bias_done = head_bias_done or getattr(b, "bias_done", False)
@@ -522,7 +556,8 @@ class CNNEngine:
                 src_of = {self.gb3.data_ptr(): (bp, 160, b.B), self.gb2.data_ptr(): (bp + 64 * 4, 160, b.B),
                           self.gb1.data_ptr(): (bp + 128 * 4, 160, b.B)}
             for name, S in planes:
-                g = {"W1": self.gW1, "W2": self.gW2, "W3": self.gW3, "Wh": self.gWh}[name]
+                g = {"W1": self.gW1, "W2": self.gW2, "W3": self.gW3, "Wh": self.gWh, "ph_Wh": self.gWh,
+                     "ph_bh": self.gbh, "ph_bfc": self.gbfc}[name]
                 src_of[g.data_ptr()] = (self._planes[name].data_ptr(), g.numel(), S)
             for p, off in zip(flat.params, flat.offsets):
                 g = flat.grad[off:off + p.numel()]

@@ -661,12 +661,22 @@ class ActorCriticTrainer:
     def _learn_native(self, obs, actions, logp_old, adv, ret, v_old, forward=True, obs_idx=None):
         cfg, eng = self.cfg, self.engine
         b = eng.bufs(obs.shape[0] if obs_idx is None else obs_idx.numel(), with_grad=True)
+        ppo = cfg.algo == "ppo"
+        vf = cfg.vf_coef if "shared" in self.flat.groups else 1.0
+        if (forward and self.dp is None and self._grad_sink is None and self._bw_stage == "all"
+                and actions.dtype == torch.int32 and eng.ppo_head_ok(b.B)):
+            # ONE head launch (z, loss, dz, dh, head gradient planes); the backward starts at the fc layer
+            eng.forward(obs, b, head=False, obs_idx=obs_idx)
+            eng.ppo_head(b, actions, logp_old, adv, ret, v_old, self.ent_coef, self.kl_coef, vf,
+                         cfg.ppo_clip if ppo else 0.0, (cfg.ppo_value_clip or 0.0) if ppo else 0.0, self.stats_buf)
+            self._bw_pending = (b, True)
+            eng.backward(b, head_bias_done=True, stage="all", head_done=True)
+            self._apply_grads()
+            return
         if forward:
             eng.forward(obs, b, obs_idx=obs_idx)
         else:
             b.obs = obs  # activations were written by the rollout; dW1 re-gathers the frames
-        ppo = cfg.algo == "ppo"
-        vf = cfg.vf_coef if "shared" in self.flat.groups else 1.0
         # the loss kernel writes its statistics straight into stats_buf[0:7]
         eng.loss(b, actions, logp_old, adv, ret, v_old if ppo else None, self.ent_coef, self.kl_coef, vf,
                  cfg.ppo_clip if ppo else 0.0, cfg.ppo_value_clip if ppo else 0.0, stats=self.stats_buf)

@@ -30,7 +30,7 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
 KERNELS = ["env_classic", "env_atari", "heads", "returns", "optim", "gemm", "gemm_plain", "gemm_conv", "gemm_group",
            "conv", "conv_wgrad",
-           "loss", "cnn_fused", "mlp"]
+           "loss", "cnn_fused", "mlp", "ppo_head"]
 # env kernels must round exactly like the PyTorch oracles: no fma contraction
 NO_CONTRACT = {"env_classic", "env_atari"}
 

@@ -15,6 +15,7 @@
 
 #include "gemm_desc.h"
 #include "mlp_desc.h"
+#include "ppo_head.h"
 
 extern "C" {
 hipError_t aca_seg_stats(const float*, const int64_t*, int, float*, hipStream_t);
@@ -25,6 +26,8 @@ hipError_t aca_opt_multi(const int64_t*, const float*, const int64_t*, int, int,
 hipError_t aca_prp_perm(int64_t*, int, uint32_t, const int64_t*, int, hipStream_t);
 hipError_t aca_mlp_fwd(const aca::MlpArgs*, int, size_t, hipStream_t);
 hipError_t aca_mlp_wgrad(const aca::WgradArgs*, hipStream_t);
+hipError_t aca_ppo_head(const aca::PpoHeadArgs*, int, hipStream_t);
+int aca_ppo_head_planes(int);
 hipError_t aca_mlp_rollout(const aca::RolloutArgs*, size_t, hipStream_t);
 hipError_t aca_env_step_cartpole(float*, int32_t*, int64_t*, float*, float*, const int64_t*, const int32_t*,
                                  const float*, float*, float*, uint8_t*, uint8_t*, uint32_t, int, int, int, float*,
@@ -726,6 +729,62 @@ const T* copt(const c10::optional<Tensor>& t, at::ScalarType dt, const char* nam
   need(*t, dt, name);
   return ptr<T>(*t);
 }
+
+// Large-batch learner head (ppo_head.hip): z = h Wh + bh, the PPO-clip / A2C loss, dz, dh = (h > 0) dz Wh^T and
+// per-workgroup partial planes of dWh [P, 512 * A1], dbh [P, A1], dbfc [P, 512] (P = ppo_head_planes(B), reduced in
+// plane order by the gradient finaliser); stats[0..6] written by the last workgroup (pstats: double [P, 6] scratch,
+// ticket: int32 zero-initialised, self-cleaning).
+void ppo_head(Tensor h, Tensor Wh, Tensor bh, Tensor act, Tensor logp_old, Tensor adv, Tensor ret,
+              c10::optional<Tensor> v_old, Tensor ent_coef, Tensor kl_coef, double vf_coef, double ppo_clip,
+              double v_clip, Tensor dh, c10::optional<Tensor> z_out, Tensor pWh, Tensor pbh, Tensor pbfc,
+              Tensor pstats, Tensor ticket, Tensor stats) {
+  need(h, at::kBFloat16, "h");
+  need(Wh, at::kBFloat16, "Wh");
+  need(dh, at::kBFloat16, "dh");
+  for (auto* x : {&bh, &logp_old, &adv, &ret, &ent_coef, &kl_coef, &pWh, &pbh, &pbfc, &stats})
+    need(*x, at::kFloat, "ppo_head f32 operand");
+  need(act, at::kInt, "act");
+  need(pstats, at::kDouble, "pstats");
+  need(ticket, at::kInt, "ticket");
+  const int64_t B = act.numel(), A1 = bh.numel();
+  TORCH_CHECK(A1 >= 3 && A1 <= 8, "ppo_head: 2..7 actions + value");
+  TORCH_CHECK(h.is_contiguous() && h.numel() == B * 512 && dh.is_contiguous() && dh.numel() == B * 512,
+              "ppo_head: h / dh must be contiguous [B, 512]");
+  TORCH_CHECK(Wh.is_contiguous() && Wh.numel() == 512 * A1, "ppo_head: Wh must be contiguous [512, A1]");
+  TORCH_CHECK(logp_old.numel() >= B && adv.numel() >= B && ret.numel() >= B, "ppo_head: row operands too small");
+  const int64_t P = aca_ppo_head_planes((int)B);
+  TORCH_CHECK(pWh.numel() >= P * 512 * A1 && pbh.numel() >= P * A1 && pbfc.numel() >= P * 512 &&
+                  pstats.numel() >= P * aca::PH_NSTAT && ticket.numel() >= 1 && stats.numel() >= 7,
+              "ppo_head: plane / scratch buffers too small");
+  aca::PpoHeadArgs a{};
+  a.h = ptr<uint16_t>(h);
+  a.Wh = ptr<uint16_t>(Wh);
+  a.bh = ptr<float>(bh);
+  a.act = ptr<int32_t>(act);
+  a.logp_old = ptr<float>(logp_old);
+  a.adv = ptr<float>(adv);
+  a.ret = ptr<float>(ret);
+  a.v_old = copt<float>(v_old, at::kFloat, "v_old");
+  TORCH_CHECK(v_clip <= 0.0 || a.v_old, "ppo_head: value clipping needs v_old");
+  a.ent_coef = ptr<float>(ent_coef);
+  a.kl_coef = ptr<float>(kl_coef);
+  a.vf_coef = (float)vf_coef;
+  a.ppo_clip = (float)ppo_clip;
+  a.v_clip = (float)v_clip;
+  a.dh = ptr<uint16_t>(dh);
+  a.z_out = const_cast<float*>(copt<float>(z_out, at::kFloat, "z_out"));
+  if (a.z_out) TORCH_CHECK(z_out->numel() >= B * A1, "ppo_head: z_out too small");
+  a.pWh = ptr<float>(pWh);
+  a.pbh = ptr<float>(pbh);
+  a.pbfc = ptr<float>(pbfc);
+  a.pstats = ptr<double>(pstats);
+  a.ticket = reinterpret_cast<unsigned int*>(ptr<int32_t>(ticket));
+  a.stats = ptr<float>(stats);
+  a.B = (int)B;
+  check(aca_ppo_head(&a, (int)A1, cur_stream(h)), "ppo_head");
+}
+
+int64_t ppo_head_planes(int64_t B) { return aca_ppo_head_planes((int)B); }
 
 void prp_perm(Tensor out, int64_t seed, Tensor uc, int64_t epoch) {
   need(out, at::kLong, "out");
@@ -1556,6 +1615,10 @@ TORCH_LIBRARY(acamd, m) {
   m.def("cnn_trunk_bwd(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tensor dy2, Tensor dy1, "
         "Tensor biasp, Tensor? stamps=None, int persist=0) -> ()");
   m.def("grad_finalize(Tensor jobs, Tensor partial) -> ()");
+  m.def("ppo_head(Tensor h, Tensor Wh, Tensor bh, Tensor act, Tensor logp_old, Tensor adv, Tensor ret, Tensor? v_old, "
+        "Tensor ent_coef, Tensor kl_coef, float vf_coef, float ppo_clip, float v_clip, Tensor dh, Tensor? z_out, "
+        "Tensor pWh, Tensor pbh, Tensor pbfc, Tensor pstats, Tensor ticket, Tensor stats) -> ()");
+  m.def("ppo_head_planes(int B) -> int", &ppo_head_planes);
   m.def("head_bwd(Tensor z, Tensor act, Tensor logp_old, Tensor ent_coef, Tensor kl_coef, float vf_coef, Tensor rew, "
         "Tensor val, Tensor dones, int L, int returns_mode, bool norm_adv, float gamma, float lam, Tensor ret_w, "
         "Tensor adv_w, Tensor h, Tensor Wh, Tensor dh, Tensor gWh, Tensor gbh, Tensor gbfc, Tensor stats, "
@@ -1614,6 +1677,7 @@ TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
   m.impl("fc_value", &fc_value);
   m.impl("cnn_trunk_bwd", &cnn_trunk_bwd);
   m.impl("grad_finalize", &grad_finalize);
+  m.impl("ppo_head", &ppo_head);
   m.impl("head_bwd", &head_bwd);
   m.impl("a2c_head", &a2c_head);
   m.impl("im2col_u8", &im2col_u8);

@@ -215,6 +215,12 @@ class CNNEngine:
         return (self.opts.fused_step and self.implicit and B <= min(self.trunk_rows_max_b, self.fused_trunk_max_b)
                 and 2 <= self.A <= 6)
 
+    def fused_env_step_ok(self, B):
+        """Banks too large for the row-split trunk: ONE per-env launch of policy/env + the next observation's trunk
+        (``pong_fused_env_step``) per rollout step."""
+        return (self.opts.fused_step and self.implicit and self.trunk_rows_max_b < B <= self.fused_trunk_max_b
+                and 2 <= self.A <= 6)
+
     def fc_planes(self, b: _Bufs):
         """fc product of ``b.y3`` as split-K partial planes (consumed by the fused step / value kernels)."""
         hp = self.hpart(b.B)

@@ -310,6 +310,8 @@ class ActorCriticTrainer:
         fused = isinstance(env, E.PongVecEnv)
         if fused and env.frame_stack == 4 and eng.fused_step_ok(N):
             return self._collect_fused_steps(st, env, eng, lb, b, N)
+        if fused and env.frame_stack == 4 and eng.fused_env_step_ok(N):
+            return self._collect_fused_env_steps(st, env, eng, lb, b, N)
         for t in range(st.T):
             bt = lb.rows(t * N, N) if lb is not None else b
             if fused:
@@ -360,6 +362,32 @@ class ActorCriticTrainer:
         self._env_flips = T
         if self._boot_in_head():
             # V(s_T) is computed by the learner's head launch straight from these planes (no fc_value launch)
+            self._boot = (hp, S)
+            return
+        ops.fc_value(hp, S, eng.bfc, eng.sWh, eng.bh, st.values[T], None)
+
+    def _collect_fused_env_steps(self, st, env, eng, lb, b, N):
+        """Large banks (per-env trunk): trunk(obs_0) + fc, then per step ONE launch of policy/env step t fused with
+        the per-env trunk of obs_{t+1} (``pong_fused_env_step``) + the fc product of obs_{t+1}; the last step's
+        trunk is the bootstrap observation's, whose value comes straight from the fc planes."""
+        ops = _native.require()
+        T = st.T
+        rows = (lambda t: lb.rows(t * N, N)) if lb is not None else (lambda t: b)
+        eng.forward(st.obs[0], rows(0), head=False, shift_out=st.obs[1], fc_parts=True)
+        for t in range(T):
+            hp, S = eng.last_fc
+            cur = rows(t)
+            nxt = rows(t + 1) if t + 1 < T else b
+            ops.pong_fused_env_step(cur.h, eng.sWh, eng.bh, cur.z, st.actions[t], st.logp[t], st.entropy[t],
+                                    st.values[t], KEY_ENV_BITS, self.policy_seed, env.state, env.t, env.tg,
+                                    env.ep_ret, env.ep_stats, env.env_ids, st.obs[t + 1], st.rewards[t], st.dones[t],
+                                    st.truncated[t], env.seed, env.max_episode_steps, hp, S, eng.bfc, eng.sW1,
+                                    eng.b1, eng.sW2, eng.b2, eng.sW3, eng.b3, nxt.y1, nxt.y2, nxt.y3, 1.0 / 255.0,
+                                    st.obs[t + 2] if t + 2 <= T else None)
+            nxt.obs = st.obs[t + 1]
+            eng.fc_planes(nxt)
+        hp, S = eng.last_fc
+        if self._boot_in_head():
             self._boot = (hp, S)
             return
         ops.fc_value(hp, S, eng.bfc, eng.sWh, eng.bh, st.values[T], None)

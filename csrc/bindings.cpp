@@ -54,6 +54,12 @@ hipError_t aca_pong_fused_step(uint16_t*, const float*, int, int64_t, const floa
                                uint8_t*, float*, uint8_t*, uint8_t*, uint32_t, int, const uint16_t*, const float*,
                                const uint16_t*, const float*, const uint16_t*, const float*, uint16_t*, uint16_t*,
                                uint16_t*, float, uint8_t*, uint64_t*, int, hipStream_t);
+hipError_t aca_pong_fused_env_step(uint16_t*, const float*, int, int64_t, const float*, const uint16_t*, const float*,
+                                   int, float*, int32_t*, float*, float*, float*, int, uint32_t, float*, int32_t*,
+                                   int64_t*, float*, float*, const int64_t*, uint8_t*, float*, uint8_t*, uint8_t*,
+                                   uint32_t, int, const uint16_t*, const float*, const uint16_t*, const float*,
+                                   const uint16_t*, const float*, uint16_t*, uint16_t*, uint16_t*, float, uint8_t*, int,
+                                   hipStream_t);
 hipError_t aca_categorical_sample(const float*, int, int, int, const int64_t*, const int64_t*, const int64_t*, int,
                                   uint32_t, int32_t*, float*, float*, float*, hipStream_t);
 hipError_t aca_ev(const float*, const float*, float*, int, hipStream_t);
@@ -354,6 +360,58 @@ void pong_fused_step(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, Tenso
                             ptr<float>(b3), ptr<uint16_t>(y1), ptr<uint16_t>(y2), ptr<uint16_t>(y3), (float)scale,
                             so, stamps_ptr(stamps, N * 7), N, cur_stream(state)),
         "pong_fused_step");
+}
+
+// Per-env fused rollout step (cnn_fused.hip pong_fused_env_step_kernel): policy/env step t of env e (fc planes of
+// obs t -> h, head, sample, physics, commit into (state, t, tg, ep_ret)) + the new frame rendered into obs t+1 (out,
+// frames 0..2 already shifted in) + frames 1..3 of obs t+1 shifted into shift_out (obs t+2, or None) + conv1..conv3
+// of obs t+1 into y1..y3. One workgroup per env.
+void pong_fused_env_step(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, Tensor logp, Tensor ent, Tensor value,
+                         int64_t key_shift, int64_t pseed, Tensor state, Tensor t, Tensor tg, Tensor ep_ret,
+                         Tensor ep_stats, Tensor ids, Tensor out, Tensor reward, Tensor done, Tensor trunc,
+                         int64_t seed, int64_t max_steps, Tensor hpart, int64_t planes, Tensor bfc, Tensor W1,
+                         Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, Tensor y1, Tensor y2, Tensor y3,
+                         double scale, c10::optional<Tensor> shift_out) {
+  check_env(state, t, tg, ep_ret, ep_stats, ids, reward, done, trunc);
+  for (auto* x : {&h, &Wh, &W1, &W2, &W3, &y1, &y2, &y3}) need(*x, at::kBFloat16, "pong_fused_env_step bf16");
+  for (auto* x : {&bh, &z, &logp, &ent, &value, &hpart, &bfc, &b1, &b2, &b3})
+    need(*x, at::kFloat, "pong_fused_env_step f32");
+  need(act, at::kInt, "act");
+  need(out, at::kByte, "out");
+  const int N = state.size(0);
+  const int A1 = bh.numel();
+  TORCH_CHECK(A1 >= 3 && A1 <= 7, "pong_fused_env_step: 2..6 actions");
+  TORCH_CHECK(state.size(1) == 8 && h.numel() == (int64_t)N * 512 && Wh.numel() == 512 * A1 &&
+                  z.numel() >= (int64_t)N * A1 && act.numel() >= N && value.numel() >= N,
+              "pong_fused_env_step: bad head shapes");
+  TORCH_CHECK(out.numel() == (int64_t)N * 4 * 84 * 84, "pong_fused_env_step: frame stack [N, 4, 84, 84]");
+  TORCH_CHECK(W1.numel() == 32 * 256 && W2.numel() == 64 * 512 && W3.numel() == 64 * 576 && b1.numel() == 32 &&
+                  b2.numel() == 64 && b3.numel() == 64 && y1.numel() == (int64_t)N * 400 * 32 &&
+                  y2.numel() == (int64_t)N * 81 * 64 && y3.numel() == (int64_t)N * 49 * 64,
+              "pong_fused_env_step: trunk shapes");
+  for (const Tensor* x : {&out, &W1, &W2, &W3, &y1, &y2, &y3, &h, &Wh, &hpart, &bfc})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(x->data_ptr()) % 16 == 0, "pong_fused_env_step: 16-byte aligned buffers");
+  TORCH_CHECK(planes >= 1 && planes <= 32 && hpart.numel() % 32 == 0 && bfc.numel() == 512,
+              "pong_fused_env_step: 1..32 fc planes");
+  const int64_t pstride = hpart.numel() / 32;
+  TORCH_CHECK(pstride >= (int64_t)N * 512, "pong_fused_env_step: hpart planes too small");
+  uint8_t* so = nullptr;
+  if (shift_out.has_value() && shift_out->defined()) {
+    need(*shift_out, at::kByte, "shift_out");
+    TORCH_CHECK(shift_out->numel() == out.numel() && reinterpret_cast<uintptr_t>(shift_out->data_ptr()) % 16 == 0 &&
+                    shift_out->data_ptr() != out.data_ptr(), "pong_fused_env_step: shift_out shape / aliasing");
+    so = shift_out->data_ptr<uint8_t>();
+  }
+  check(aca_pong_fused_env_step(ptr<uint16_t>(h), ptr<float>(hpart), (int)planes, pstride, ptr<float>(bfc),
+                                ptr<uint16_t>(Wh), ptr<float>(bh), A1 - 1, ptr<float>(z), ptr<int32_t>(act),
+                                ptr<float>(logp), ptr<float>(ent), ptr<float>(value), (int)key_shift, (uint32_t)pseed,
+                                ptr<float>(state), ptr<int32_t>(t), ptr<int64_t>(tg), ptr<float>(ep_ret),
+                                ptr<float>(ep_stats), ptr<int64_t>(ids), ptr<uint8_t>(out), ptr<float>(reward),
+                                ptr<uint8_t>(done), ptr<uint8_t>(trunc), (uint32_t)seed, (int)max_steps,
+                                ptr<uint16_t>(W1), ptr<float>(b1), ptr<uint16_t>(W2), ptr<float>(b2),
+                                ptr<uint16_t>(W3), ptr<float>(b3), ptr<uint16_t>(y1), ptr<uint16_t>(y2),
+                                ptr<uint16_t>(y3), (float)scale, so, N, cur_stream(state)),
+        "pong_fused_env_step");
 }
 
 // bootstrap value from the fc partial planes (cnn_fused.hip); hpart holds 32 equal planes of [N, 512]
@@ -1553,6 +1611,11 @@ TORCH_LIBRARY(acamd, m) {
         "Tensor reward, Tensor done, Tensor truncated, int seed, int max_steps, Tensor hpart, int planes, "
         "Tensor bfc, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, Tensor y1, Tensor y2, "
         "Tensor y3, float scale, Tensor? shift_out=None, Tensor? stamps=None) -> ()");
+  m.def("pong_fused_env_step(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, Tensor logp, Tensor ent, "
+        "Tensor value, int key_shift, int pseed, Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, "
+        "Tensor env_ids, Tensor out, Tensor reward, Tensor done, Tensor truncated, int seed, int max_steps, "
+        "Tensor hpart, int planes, Tensor bfc, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, "
+        "Tensor y1, Tensor y2, Tensor y3, float scale, Tensor? shift_out=None) -> ()");
   m.def("categorical_sample(Tensor logits, Tensor keys, int seed, Tensor act, Tensor logp, Tensor ent) -> ()");
   m.def("categorical_sample_env(Tensor logits, Tensor tg, Tensor env_ids, int key_shift, int seed, Tensor act, "
         "Tensor logp, Tensor ent, Tensor? vout) -> ()");
@@ -1678,6 +1741,7 @@ TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
   m.impl("cnn_trunk_bwd", &cnn_trunk_bwd);
   m.impl("grad_finalize", &grad_finalize);
   m.impl("ppo_head", &ppo_head);
+  m.impl("pong_fused_env_step", &pong_fused_env_step);
   m.impl("head_bwd", &head_bwd);
   m.impl("a2c_head", &a2c_head);
   m.impl("im2col_u8", &im2col_u8);

@@ -251,45 +251,19 @@ __device__ __forceinline__ void trunk_obs_dma(const uint8_t* __restrict__ src, u
 // stage), so a workgroup needs 74 KB of LDS and TWO fit a CU: while one sample waits on a barrier or a memory round
 // trip the other one's MFMAs run (the 118 KB form above runs one workgroup -- one wave per SIMD -- per CU). conv1
 // converts the pixels to exact bf16 integers on the fly; same MFMA order and epilogues: bit-identical outputs.
-// NW = 4 waves (two workgroups per CU: learner batches) or 8 (one workgroup per CU, each layer's tiles spread over
-// twice the waves: rollout batches below the CU count, where half the CUs would idle anyway). With 8 waves, waves
-// w and w + 4 share an output-channel tile of conv2 / conv3 and split its position tiles; same MFMA order per output
-// tile either way: bit-identical results.
-template <int NW>
-__global__ void __launch_bounds__(NW * 64) cnn_trunk_fwd_u8_kernel(
-    const uint8_t* __restrict__ obs, const u16* __restrict__ W1, const float* __restrict__ b1,
-    const u16* __restrict__ W2, const float* __restrict__ b2, const u16* __restrict__ W3,
-    const float* __restrict__ b3, u16* __restrict__ y1g, u16* __restrict__ y2g, u16* __restrict__ y3g,
-    float scale, uint8_t* __restrict__ shift_out, const int64_t* __restrict__ obs_idx) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_obs8[TP_OBS_PAD];
-  __shared__ __attribute__((aligned(16))) u16 s_y1[Y1_ROWS * Y1_LD];
-  __shared__ __attribute__((aligned(16))) u16 s_y2[Y2_ROWS * Y2_LD];
-  const int e = blockIdx.x;
+// The conv chain is a device function shared with the per-env fused rollout step (pong_fused_env_step_kernel).
+// ------------------------------------------------------------------------------------------------------------
+// conv1 -> conv2 -> conv3 of env e from its staged uint8 observation (s_obs8, complete behind a barrier); bw / bw2:
+// this wave's conv1 / conv2 weight fragments (already in registers), W3's are loaded after conv1.
+__device__ __forceinline__ void trunk_env_convs(const uint8_t* __restrict__ s_obs8, u16* __restrict__ s_y1,
+                                                u16* __restrict__ s_y2, int e, const bf16x8 (&bw)[2][8],
+                                                const bf16x8 (&bw2)[16], const u16* __restrict__ W3, float bias0,
+                                                float bias1, float bias2, float bias3, u16* __restrict__ y1g,
+                                                u16* __restrict__ y2g, u16* __restrict__ y3g, float scale) {
+  constexpr int NW = 4;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l16 = lane & 15, lg = lane >> 4;
-  const int nw4 = wid & 3, half = wid >> 2;   // output-channel tile; position-tile half (NW = 8)
-  const int n2 = nw4 * 16 + l16;
-  // loads in the order they are consumed (the vm counter retires in issue order): frames (LDS-DMA), conv1
-  // fragments, conv2 fragments; conv3's after conv1
-  // obs_idx (PPO minibatch in index mode): sample e is row obs_idx[e] of the rollout's observations
-  trunk_obs_dma(obs + (size_t)(obs_idx ? obs_idx[e] : e) * OBS_BYTES, s_obs8);
-  bf16x8 bw[2][8];
-#pragma unroll
-  for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks)
-      bw[nt][ks] = *reinterpret_cast<const bf16x8*>(W1 + (nt * 16 + l16) * 256 + ks * 32 + lg * 8);
-  bf16x8 bw2[16];
-#pragma unroll
-  for (int ks = 0; ks < 16; ++ks) bw2[ks] = *reinterpret_cast<const bf16x8*>(W2 + n2 * 512 + ks * 32 + lg * 8);
-  const float bias0 = b1[l16], bias1 = b1[16 + l16], bias2 = b2[n2], bias3 = b3[n2];
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (shift_out) {   // rollout: frames 1..3 of this observation become frames 0..2 of the next one
-    uint4* so = reinterpret_cast<uint4*>(shift_out + (size_t)e * OBS_BYTES);
-    const uint4* si = reinterpret_cast<const uint4*>(s_obs8);
-    for (int i = OBS_BYTES / 64 + tid; i < OBS_BYTES / 16; i += NW * 64) so[i - OBS_BYTES / 64] = si[i];
-  }
+  const int n2 = wid * 16 + l16;
   // ---------------------------------------------------------------- conv1: M 400 (25 tiles), N 32 (2), K 256 (8)
   for (int mt = wid; mt < 25; mt += NW) {
     floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
@@ -323,28 +297,26 @@ __global__ void __launch_bounds__(NW * 64) cnn_trunk_fwd_u8_kernel(
   __syncthreads();
   // ---------------------------------------------------------------- conv2: M 81 (6 tiles), N 64 (wave = N tile), K 512
   {
-    constexpr int M2 = NW == 8 ? 3 : 6;   // position tiles of this wave (NW = 8: half 0 -> 0..2, half 1 -> 3..5)
-    const int mt0 = NW == 8 ? 3 * half : 0;
-    floatx4 acc[M2];
+    floatx4 acc[6];
 #pragma unroll
-    for (int mt = 0; mt < M2; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int mt = 0; mt < 6; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < 16; ++ks) {
       const int k = ks * 32 + lg * 8;
       const int i = k >> 7, j = (k >> 5) & 3, c0 = k & 31;
 #pragma unroll
-      for (int mt = 0; mt < M2; ++mt) {
-        const int m = min((mt0 + mt) * 16 + l16, Y2_ROWS - 1);
+      for (int mt = 0; mt < 6; ++mt) {
+        const int m = min(mt * 16 + l16, Y2_ROWS - 1);
         const int oh = m / 9, ow = m - oh * 9;
         const bf16x8 a = *reinterpret_cast<const bf16x8*>(s_y1 + ((oh * 2 + i) * 20 + ow * 2 + j) * Y1_LD + c0);
         acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw2[ks], acc[mt], 0, 0, 0);
       }
     }
 #pragma unroll
-    for (int mt = 0; mt < M2; ++mt) {
+    for (int mt = 0; mt < 6; ++mt) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = (mt0 + mt) * 16 + lg * 4 + r;
+        const int row = mt * 16 + lg * 4 + r;
         if (row < Y2_ROWS) {
           const u16 v = f2bf(fmaxf(acc[mt][r] + bias2, 0.f));
           s_y2[row * Y2_LD + n2] = v;
@@ -356,32 +328,73 @@ __global__ void __launch_bounds__(NW * 64) cnn_trunk_fwd_u8_kernel(
   __syncthreads();
   // ---------------------------------------------------------------- conv3: M 49 (4 tiles), N 64 (wave = N tile), K 576
   {
-    constexpr int M3 = NW == 8 ? 2 : 4;
-    const int mt0 = NW == 8 ? 2 * half : 0;
-    floatx4 acc[M3];
+    floatx4 acc[4];
 #pragma unroll
-    for (int mt = 0; mt < M3; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int mt = 0; mt < 4; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < 18; ++ks) {
       const int k = ks * 32 + lg * 8;
       const int i = k / 192, j = (k >> 6) % 3, c0 = k & 63;
 #pragma unroll
-      for (int mt = 0; mt < M3; ++mt) {
-        const int m = min((mt0 + mt) * 16 + l16, Y3_ROWS - 1);
+      for (int mt = 0; mt < 4; ++mt) {
+        const int m = min(mt * 16 + l16, Y3_ROWS - 1);
         const int oh = m / 7, ow = m - oh * 7;
         const bf16x8 a = *reinterpret_cast<const bf16x8*>(s_y2 + ((oh + i) * 9 + ow + j) * Y2_LD + c0);
         acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw3[ks], acc[mt], 0, 0, 0);
       }
     }
 #pragma unroll
-    for (int mt = 0; mt < M3; ++mt) {
+    for (int mt = 0; mt < 4; ++mt) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = (mt0 + mt) * 16 + lg * 4 + r;
+        const int row = mt * 16 + lg * 4 + r;
         if (row < Y3_ROWS) y3g[((size_t)e * Y3_ROWS + row) * Y3_C + n2] = f2bf(fmaxf(acc[mt][r] + bias3, 0.f));
       }
     }
   }
+}
+
+// conv1 / conv2 weight fragments of this wave (output-channel tile wid for conv2)
+__device__ __forceinline__ void trunk_env_w12(const u16* __restrict__ W1, const u16* __restrict__ W2,
+                                              bf16x8 (&bw)[2][8], bf16x8 (&bw2)[16]) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, l16 = lane & 15, lg = lane >> 4;
+  const int n2 = wid * 16 + l16;
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+      bw[nt][ks] = *reinterpret_cast<const bf16x8*>(W1 + (nt * 16 + l16) * 256 + ks * 32 + lg * 8);
+#pragma unroll
+  for (int ks = 0; ks < 16; ++ks) bw2[ks] = *reinterpret_cast<const bf16x8*>(W2 + n2 * 512 + ks * 32 + lg * 8);
+}
+
+__global__ void __launch_bounds__(256) cnn_trunk_fwd_u8_kernel(
+    const uint8_t* __restrict__ obs, const u16* __restrict__ W1, const float* __restrict__ b1,
+    const u16* __restrict__ W2, const float* __restrict__ b2, const u16* __restrict__ W3,
+    const float* __restrict__ b3, u16* __restrict__ y1g, u16* __restrict__ y2g, u16* __restrict__ y3g,
+    float scale, uint8_t* __restrict__ shift_out, const int64_t* __restrict__ obs_idx) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_obs8[TP_OBS_PAD];
+  __shared__ __attribute__((aligned(16))) u16 s_y1[Y1_ROWS * Y1_LD];
+  __shared__ __attribute__((aligned(16))) u16 s_y2[Y2_ROWS * Y2_LD];
+  const int e = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int l16 = lane & 15;
+  const int n2 = wid * 16 + l16;
+  // loads in the order they are consumed (the vm counter retires in issue order): frames (LDS-DMA), conv1
+  // fragments, conv2 fragments; conv3's after conv1
+  // obs_idx (PPO minibatch in index mode): sample e is row obs_idx[e] of the rollout's observations
+  trunk_obs_dma(obs + (size_t)(obs_idx ? obs_idx[e] : e) * OBS_BYTES, s_obs8);
+  bf16x8 bw[2][8], bw2[16];
+  trunk_env_w12(W1, W2, bw, bw2);
+  const float bias0 = b1[l16], bias1 = b1[16 + l16], bias2 = b2[n2], bias3 = b3[n2];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (shift_out) {   // rollout: frames 1..3 of this observation become frames 0..2 of the next one
+    uint4* so = reinterpret_cast<uint4*>(shift_out + (size_t)e * OBS_BYTES);
+    const uint4* si = reinterpret_cast<const uint4*>(s_obs8);
+    for (int i = OBS_BYTES / 64 + tid; i < OBS_BYTES / 16; i += 256) so[i - OBS_BYTES / 64] = si[i];
+  }
+  trunk_env_convs(s_obs8, s_y1, s_y2, e, bw, bw2, W3, bias0, bias1, bias2, bias3, y1g, y2g, y3g, scale);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -860,6 +873,127 @@ __global__ void __launch_bounds__(T_THREADS) pong_fused_step_kernel(
   stamp(stamps, 1);
   trunk_rows_compute<1>(s_in, s_w1, s_y1, s_y2, e, r, bias1a, bias1b, bias2, bias3, W2, W3, y1g, y2g, y3g, scale,
                         stamps, bw2, bw3);
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// Rollout step t fused with the trunk of step t + 1, per-env layout (one workgroup per env: the large banks,
+// Breakout-shape PPO at 128 envs, where 7 row workgroups per env would not fit the chip in one wave):
+//   every load first -- the next observation's frames (LDS-DMA: frames 0..2 were shifted in by the previous launch),
+//   the conv1 / conv2 weight fragments, the head's Wh rows, the fc partial planes of obs t --; then h (planes summed
+//   in order + bias + ReLU), the policy/value head, Gumbel-max sampling, the env physics (all three paddle directions
+//   evaluated while the head runs) and the commit; the new frame is rendered straight into the staged uint8 image
+//   (all 4 frames after an episode restart) and to obs t+1 in memory; frames 1..3 of obs t+1 go to obs t+2 (shift);
+//   then conv1 -> conv3 of obs t+1 (trunk_env_convs, bit-identical to the per-env trunk kernel).
+// One launch instead of the trunk kernel + the policy/env kernel of the unfused step, and the new frame never makes a
+// global round trip before conv1.
+// ------------------------------------------------------------------------------------------------------------
+template <int A1>
+__global__ void __launch_bounds__(256) pong_fused_env_step_kernel(
+    PongIO io, FcParts fc, u16* __restrict__ h, const u16* __restrict__ Wh, const float* __restrict__ bh,
+    float* __restrict__ z_out, int32_t* __restrict__ act, float* __restrict__ logp, float* __restrict__ ent,
+    float* __restrict__ vout, int key_shift, uint32_t pseed, const u16* __restrict__ W1,
+    const float* __restrict__ b1, const u16* __restrict__ W2, const float* __restrict__ b2,
+    const u16* __restrict__ W3, const float* __restrict__ b3, u16* __restrict__ y1g, u16* __restrict__ y2g,
+    u16* __restrict__ y3g, float scale, uint8_t* __restrict__ shift_out) {
+  constexpr int A = A1 - 1;
+  __shared__ __attribute__((aligned(16))) uint8_t s_obs8[TP_OBS_PAD];
+  __shared__ __attribute__((aligned(16))) u16 s_y1[Y1_ROWS * Y1_LD];
+  __shared__ __attribute__((aligned(16))) u16 s_y2[Y2_ROWS * Y2_LD];
+  __shared__ float s_acc[4][A1];
+  __shared__ PongOut cand[3];
+  __shared__ int sh_act;
+  const int e = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, l16 = lane & 15;
+  const int n2 = wid * 16 + l16;
+  // ---------------------------------------------------------------- every independent operand requested first
+  trunk_obs_dma(io.out + (size_t)e * OBS_BYTES, s_obs8);   // obs t+1: frames 0..2 valid, frame 3 rendered below
+  const int64_t tg0 = io.tglob[e], id0 = io.env_ids[e];
+  const float bhj = bh[lane < A1 ? lane : 0];
+  uint32_t wv[A1];   // this thread's two Wh rows
+#pragma unroll
+  for (int u = 0; u < A1; ++u) wv[u] = reinterpret_cast<const uint32_t*>(Wh)[A1 * tid + u];
+  bf16x8 bw[2][8], bw2[16];
+  trunk_env_w12(W1, W2, bw, bw2);
+  const float bias0 = b1[l16], bias1 = b1[16 + l16], bias2 = b2[n2], bias3 = b3[n2];
+  // ---------------------------------------------------------------- policy head of obs t
+  float hf[2];
+  fc_h2_from_parts(fc.hpart, fc.S, fc.plane_stride, fc.bfc, e, tid, h, hf);
+  if (tid >= 64 && tid < 67) cand[tid - 64] = pong_advance(io, e, (float)(tid - 65));
+  float accj[A1];
+#pragma unroll
+  for (int j = 0; j < A1; ++j) {
+    const uint32_t w0 = wv[j >> 1], w1 = wv[(A1 + j) >> 1];
+    const float a0 = __uint_as_float((j & 1) ? (w0 & 0xFFFF0000u) : (w0 << 16));
+    const float a1 = __uint_as_float(((A1 + j) & 1) ? (w1 & 0xFFFF0000u) : (w1 << 16));
+    accj[j] = wave_sum(hf[0] * a0 + hf[1] * a1);
+  }
+  if (lane == 0)
+#pragma unroll
+    for (int j = 0; j < A1; ++j) s_acc[wid][j] = accj[j];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the staged frames have landed (and every fragment)
+  __syncthreads();
+  if (wid == 0) {
+    const int64_t key = tg0 * ((int64_t)1 << key_shift) + id0;   // pre-step counter
+    const int jj = lane < A1 ? lane : 0;
+    const float zj = ((s_acc[0][jj] + s_acc[1][jj]) + (s_acc[2][jj] + s_acc[3][jj])) + bhj;
+    if (lane < A1) z_out[(size_t)e * A1 + lane] = zj;
+    const float value = __shfl(zj, A, 64);
+    const bool on = lane < A;
+    const float z = on ? zj : -INFINITY;
+    const float m = wave_max(z);
+    const float ex = on ? expf(z - m) : 0.f;
+    const float lse = m + logf(wave_sum(ex));
+    const float lp = z - lse;
+    const float H = wave_sum(on ? -expf(lp) * lp : 0.f);
+    float gmb = -INFINITY;
+    if (on) gmb = z + (-logf(-logf(uniform_open(pseed, key, (uint32_t)lane))));
+    float best = gmb;
+    int bi = on ? lane : 1 << 30;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ob = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+    }
+    const float lpa = __shfl(lp, bi, 64);
+    if (lane == 0) {
+      act[e] = bi;
+      logp[e] = lpa;
+      ent[e] = H;
+      vout[e] = value;
+      sh_act = bi;
+    }
+  }
+  __syncthreads();
+  const PongOut& res = cand[pong_dir_index(sh_act)];
+  const bool done = res.done != 0;
+  if (tid == 0) pong_commit(io, e, res, tg0);
+  // ---------------------------------------------------------------- the new frame: staged image + obs t+1 in memory
+  {
+    constexpr int WPR = PW / 4, NWORDS = PH * WPR;   // 21, 1764
+    const PongGeom gm = pong_geom(res.s);
+    uint32_t* ob = reinterpret_cast<uint32_t*>(io.out + (size_t)e * OBS_BYTES);
+    uint32_t* sw = reinterpret_cast<uint32_t*>(s_obs8);
+    for (int w = tid; w < NWORDS; w += 256) {
+      const int y = w / WPR, x0 = (w - y * WPR) * 4;
+      const uint32_t word = pong_word(gm, y, x0);
+      sw[3 * NWORDS + w] = word;
+      ob[3 * NWORDS + w] = word;
+      if (done)
+#pragma unroll
+        for (int f = 0; f < 3; ++f) {
+          sw[f * NWORDS + w] = word;
+          ob[f * NWORDS + w] = word;
+        }
+    }
+  }
+  __syncthreads();
+  if (shift_out) {   // frames 1..3 of obs t+1 become frames 0..2 of obs t+2
+    uint4* so = reinterpret_cast<uint4*>(shift_out + (size_t)e * OBS_BYTES);
+    const uint4* si = reinterpret_cast<const uint4*>(s_obs8);
+    for (int i = OBS_BYTES / 64 + tid; i < OBS_BYTES / 16; i += 256) so[i - OBS_BYTES / 64] = si[i];
+  }
+  trunk_env_convs(s_obs8, s_y1, s_y2, e, bw, bw2, W3, bias0, bias1, bias2, bias3, y1g, y2g, y3g, scale);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -1439,7 +1573,7 @@ extern "C" hipError_t aca_cnn_trunk_fwd(const uint8_t* obs, const uint16_t* W1, 
   // bf16-staged per-env kernel (diagnostic builds, scripts/microbench_*.py). Only the lean form reads through
   // an index (obs_idx: gathered minibatch rows).
   if (!stamps) {
-    aca::cnn_trunk_fwd_u8_kernel<4><<<B, 256, 0, stream>>>(obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale, shift_out,
+    aca::cnn_trunk_fwd_u8_kernel<<<B, 256, 0, stream>>>(obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale, shift_out,
                                                           obs_idx);
     return hipGetLastError();
   }
@@ -1503,6 +1637,35 @@ extern "C" hipError_t aca_pong_fused_step(
     break;
     ACA_FUSED_CASE(3) ACA_FUSED_CASE(4) ACA_FUSED_CASE(5) ACA_FUSED_CASE(6) ACA_FUSED_CASE(7)
 #undef ACA_FUSED_CASE
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+extern "C" hipError_t aca_pong_fused_env_step(
+    uint16_t* h, const float* hpart, int S, int64_t plane_stride, const float* bfc, const uint16_t* Wh,
+    const float* bh, int A, float* z, int32_t* act, float* logp, float* ent, float* value, int key_shift,
+    uint32_t pseed, float* state, int32_t* t, int64_t* tg, float* ep_ret, float* ep_stats, const int64_t* ids,
+    uint8_t* out, float* reward, uint8_t* done, uint8_t* trunc, uint32_t seed, int max_steps, const uint16_t* W1,
+    const float* b1, const uint16_t* W2, const float* b2, const uint16_t* W3, const float* b3, uint16_t* y1,
+    uint16_t* y2, uint16_t* y3, float scale, uint8_t* shift_out, int N, hipStream_t stream) {
+  if (N <= 0) return hipSuccess;
+  if (S < 1 || S > aca::FC_MAX_PLANES) return hipErrorInvalidValue;
+  aca::PongIO io;
+  io.state = state; io.tsteps = t; io.tglob = tg; io.ep_ret = ep_ret; io.ep_stats = ep_stats; io.env_ids = ids;
+  io.prev = out; io.out = out; io.reward = reward; io.done_out = done; io.trunc_out = trunc; io.seed = seed;
+  io.max_steps = max_steps; io.k = 4;
+  aca::FcParts fc{hpart, S, plane_stride, bfc};
+  switch (A + 1) {
+#define ACA_FES_CASE(A1)                                                                                         \
+  case A1:                                                                                                       \
+    aca::pong_fused_env_step_kernel<A1><<<N, 256, 0, stream>>>(io, fc, h, Wh, bh, z, act, logp, ent, value,     \
+                                                               key_shift, pseed, W1, b1, W2, b2, W3, b3, y1, y2, \
+                                                               y3, scale, shift_out);                            \
+    break;
+    ACA_FES_CASE(3) ACA_FES_CASE(4) ACA_FES_CASE(5) ACA_FES_CASE(6) ACA_FES_CASE(7)
+#undef ACA_FES_CASE
     default:
       return hipErrorInvalidValue;
   }

@@ -23,13 +23,25 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 
-def run(name, updates, warmup, engine, device):
+def run(name, updates, warmup, engine, device, dp_world1=False):
     from actor_critic_algs_on_tensorflow_amd import preset
     from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
     dev = device if name != "cartpole_cpu" or device == "cpu" else device
     cfg = preset(name, device=dev, outdir=None, quiet=True, stdout_freq=0, save_every=0, engine=engine,
                  cuda_graph=dev.startswith("cuda"))
-    tr = ActorCriticTrainer(cfg)
+    dp = None
+    if dp_world1:
+        # the data-parallel update at world size 1 (RCCL on a GPU): every collective of the DP schedule is issued
+        # (recorded in the update's graph), so the trace shows what the collectives cost on top of the compute
+        import torch.distributed as dist
+        from actor_critic_algs_on_tensorflow_amd.parallel import dp as DP
+        if not dist.is_initialized():
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29531")
+            kw = dict(device_id=torch.device(dev)) if dev.startswith("cuda") else {}
+            dist.init_process_group("nccl" if dev.startswith("cuda") else "gloo", rank=0, world_size=1, **kw)
+        dp = DP.DataParallel()
+    tr = ActorCriticTrainer(cfg, dp=dp)
     cuda = dev.startswith("cuda")
     if cuda:
         tr.capture(warmup=2)
@@ -47,7 +59,7 @@ def run(name, updates, warmup, engine, device):
     return {"config": name, "env_steps_per_s": round(steps / dt, 1), "ms_per_update": round(1e3 * dt / updates, 4),
             "updates": updates, "envs": tr.env.num_envs, "n_steps": cfg.n_steps, "algo": cfg.algo,
             "engine": "native-cnn" if tr.engine is not None else ("native-mlp" if tr.mlp is not None else "torch"),
-            "hipgraph": bool(tr.graph), "device": dev,
+            "hipgraph": bool(tr.graph), "device": dev, "dp_world1": bool(dp_world1),
             "ppo": {"epochs": cfg.ppo_epochs, "minibatches": cfg.ppo_minibatches} if cfg.algo == "ppo" else None}
 
 
@@ -58,9 +70,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--engine", default="auto")
     ap.add_argument("--device", default="cuda:0" if torch.cuda.is_available() else "cpu")
+    ap.add_argument("--dp-world1", action="store_true", help="run the data-parallel schedule at world size 1")
     args = ap.parse_args()
     for name in args.configs.split(","):
-        print(json.dumps(run(name, args.updates, args.warmup, args.engine, args.device)), flush=True)
+        print(json.dumps(run(name, args.updates, args.warmup, args.engine, args.device, args.dp_world1)), flush=True)
 
 
 if __name__ == "__main__":

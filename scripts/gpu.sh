@@ -26,7 +26,7 @@ SQ="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VAL
 prog() {   # NAME -> program, trace marker, kernels per update, updates summarised
   case $1 in
     pong) echo "pong_fused_step 5 30 $PONG" ;;
-    breakout) echo "pong_policy_step 128 1 $BR" ;;
+    breakout) echo "pong_fused_env_step 128 1 $BR" ;;
     mujoco) echo "mlp_rollout 1 1 $MJ" ;;
     *) echo "unknown program $1" >&2; return 1 ;;
   esac

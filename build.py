@@ -28,7 +28,7 @@ BUILD_DIR = os.path.join(ROOT, "build")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
-KERNELS = ["env_classic", "env_atari", "heads", "returns", "optim", "gemm", "gemm_plain", "gemm_conv", "gemm_group",
+KERNELS = ["env_classic", "env_atari", "heads", "returns", "optim", "gemm", "gemm_plain", "gemm_conv", "gemm_group", "gemm_big",
            "conv", "conv_wgrad",
            "loss", "cnn_fused", "mlp", "ppo_head"]
 # env kernels must round exactly like the PyTorch oracles: no fma contraction

@@ -82,6 +82,8 @@ hipError_t aca_ev_multi(const float*, const float*, float*, int, double*, unsign
 hipError_t aca_conv1_wgrad(const uint8_t*, const uint16_t*, float*, int, int, float, const int64_t*, hipStream_t);
 hipError_t aca_conv_wgrad_nhwc(int, const uint16_t*, const uint16_t*, float*, int, int, hipStream_t);
 hipError_t aca_conv_wgrad_gemm(int, const uint16_t*, const uint16_t*, float*, int, int, hipStream_t);
+hipError_t aca_gemm_big(const AcaGemmDesc*, hipStream_t);
+int64_t aca_gemm_big_ws(int, int, int);
 hipError_t aca_sumsq(const float*, size_t, float*, hipStream_t);
 int aca_sumsq_parts();
 hipError_t aca_adam_step(float*, float*, float*, float*, size_t, const float*, float*, const float*, float*, uint16_t*,
@@ -1133,6 +1135,54 @@ struct GemmGroupState {
 };
 static thread_local GemmGroupState g_gemm_group;
 
+// Large plain bf16 products on 128 x 128 tiles of the 32x32x16 MFMA with LDS-DMA staging (gemm_big.hip): epilogue
+// alpha / bias / relu / mask, store fp32 (out_mode 0) or bf16 (1); splits > 1: slab split-K (ws >= gemm_big_ws
+// floats, tickets >= tiles int32 zeros, self-cleaning), reduced in split order by the last-arriving split.
+void gemm_big(Tensor A, int64_t lda, bool a_k, Tensor B, int64_t ldb, bool b_k, Tensor C, int64_t ldc,
+              int64_t out_mode, int64_t M, int64_t N, int64_t K, double alpha, c10::optional<Tensor> bias, bool relu,
+              c10::optional<Tensor> mask, int64_t ldm, int64_t splits, c10::optional<Tensor> ws,
+              c10::optional<Tensor> tickets) {
+  TORCH_CHECK(out_mode == 0 || out_mode == 1, "gemm_big: out_mode 0 / 1");
+  TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "gemm_big: bf16 operands");
+  TORCH_CHECK(C.scalar_type() == (out_mode == 1 ? at::kBFloat16 : at::kFloat), "gemm_big: C dtype mismatch");
+  check_extent(A, a_k ? M : K, a_k ? K : M, lda, "A");
+  check_extent(B, b_k ? N : K, b_k ? K : N, ldb, "B");
+  check_extent(C, M, N, ldc, "C");
+  AcaGemmDesc d{};
+  d.A = A.data_ptr();
+  d.B = B.data_ptr();
+  d.C = C.data_ptr();
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() >= N, "gemm_big: bias must be fp32 [N]");
+    d.bias = ptr<float>(*bias);
+  }
+  if (mask.has_value() && mask->defined()) {
+    TORCH_CHECK(mask->scalar_type() == at::kBFloat16, "gemm_big: mask must be bf16");
+    check_extent(*mask, M, N, ldm, "mask");
+    d.mask = mask->data_ptr();
+  }
+  if (splits > 1) {
+    TORCH_CHECK(ws.has_value() && ws->defined() && tickets.has_value() && tickets->defined(),
+                "gemm_big: split-K needs ws and tickets");
+    TORCH_CHECK(ws->scalar_type() == at::kFloat && ws->numel() >= aca_gemm_big_ws((int)M, (int)N, (int)splits),
+                "gemm_big: ws too small");
+    TORCH_CHECK(tickets->scalar_type() == at::kInt &&
+                    tickets->numel() >= ((M + 127) / 128) * ((N + 127) / 128), "gemm_big: tickets too small");
+    d.ws = ptr<float>(*ws);
+    d.tickets = reinterpret_cast<unsigned int*>(tickets->data_ptr<int32_t>());
+  }
+  d.lda = lda; d.ldb = ldb; d.ldc = ldc; d.ldm = ldm;
+  d.M = (int)M; d.N = (int)N; d.K = (int)K;
+  d.a_k = a_k; d.b_k = b_k;
+  d.out_mode = (int)out_mode;
+  d.relu = relu;
+  d.alpha = (float)alpha;
+  d.splits = (int)splits;
+  check(aca_gemm_big(&d, cur_stream(C)), "gemm_big");
+}
+
+int64_t gemm_big_ws(int64_t M, int64_t N, int64_t splits) { return aca_gemm_big_ws((int)M, (int)N, (int)splits); }
+
 void gemm(Tensor A, int64_t lda, bool a_k, Tensor B, int64_t ldb, bool b_k, Tensor C, int64_t ldc, int64_t out_mode,
           int64_t M, int64_t N, int64_t K, double alpha, c10::optional<Tensor> bias, bool relu,
           c10::optional<Tensor> mask, int64_t ldm, c10::optional<Tensor> colsum, int64_t colsum_mod, int64_t tile,
@@ -1670,6 +1720,10 @@ TORCH_LIBRARY(acamd, m) {
         "int tile, int bk, int splits, Tensor? ws, Tensor? tickets, int[] ga, float ga_scale, int[] gb, "
         "float gb_scale, Tensor? stamps=None, Tensor? colsum_part=None) -> ()");
   m.def("colsum_reduce(Tensor part, int R, int N, Tensor out, int mod) -> ()");
+  m.def("gemm_big(Tensor A, int lda, bool a_k, Tensor B, int ldb, bool b_k, Tensor C, int ldc, int out_mode, int M, "
+        "int N, int K, float alpha, Tensor? bias, bool relu, Tensor? mask, int ldm, int splits, Tensor? ws=None, "
+        "Tensor? tickets=None) -> ()");
+  m.def("gemm_big_ws(int M, int N, int splits) -> int", &gemm_big_ws);
   m.def("seg_stats(Tensor x, Tensor segs, Tensor out) -> ()");
   m.def("gemm_effective_splits(int K, int bk, int splits) -> int", &gemm_effective_splits);
   m.def("cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, Tensor y1, "
@@ -1741,6 +1795,7 @@ TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
   m.impl("cnn_trunk_bwd", &cnn_trunk_bwd);
   m.impl("grad_finalize", &grad_finalize);
   m.impl("ppo_head", &ppo_head);
+  m.impl("gemm_big", &gemm_big);
   m.impl("pong_fused_env_step", &pong_fused_env_step);
   m.impl("head_bwd", &head_bwd);
   m.impl("a2c_head", &a2c_head);

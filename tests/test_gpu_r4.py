@@ -144,3 +144,43 @@ def test_fused_env_step_equals_separate_trunk_and_policy(cuda, preset_name, capt
     for k, (a, b) in enumerate(zip(*runs)):
         for j, (x, y) in enumerate(zip(a, b)):
             assert torch.equal(x, y), (k, j)
+
+
+@pytest.mark.parametrize("a_k,b_k,M,N,K,out_mode,epi,splits", [
+    (True, False, 4096, 512, 3136, 1, "bias_relu", 1),     # PPO fc forward: h = relu(y3 Wfc + bfc)
+    (True, False, 4096, 512, 3072, 1, "bias_relu", 2),     # ... split-K slabs (3072 = 48 k-steps)
+    (False, False, 3136, 512, 4096, 0, None, 2),           # dWfc = y3^T dh (fp32, partial M tile)
+    (True, True, 4096, 3136, 512, 1, "mask", 1),           # dy3 = (dh Wfc^T) * (y3 > 0) (partial N tile)
+    (False, True, 200, 136, 256, 0, None, 4),              # both partial tiles, 4 splits
+])
+def test_gemm_big_matches_fp32_reference(cuda, a_k, b_k, M, N, K, out_mode, epi, splits):
+    """gemm_big.hip (128 x 128 tiles of the 32x32x16 MFMA, LDS-DMA 3-stage ring, swizzled images) == the fp32
+    product of the same bf16 operands in every storage orientation; split-K slabs reduced by the last arriver; a
+    second launch is bitwise identical (fixed split order)."""
+    from actor_critic_algs_on_tensorflow_amd import _native
+    from actor_critic_algs_on_tensorflow_amd.ops.gemm import gemm_ref
+    ops = _native.require()
+    g = torch.Generator(device="cpu").manual_seed(M + N + K + 2 * a_k + b_k + splits)
+    lda = K if a_k else M
+    ldb = K if b_k else N
+    A = (torch.randn((M if a_k else K) * lda, generator=g) * 0.5).to(torch.bfloat16).to(cuda)
+    B = (torch.randn((N if b_k else K) * ldb, generator=g) * 0.5).to(torch.bfloat16).to(cuda)
+    bias = torch.randn(N, generator=g).to(cuda) if epi == "bias_relu" else None
+    mask = torch.randn(M * N, generator=g).to(torch.bfloat16).to(cuda) if epi == "mask" else None
+    dt = torch.bfloat16 if out_mode == 1 else torch.float32
+    ws = torch.zeros(max(1, int(ops.gemm_big_ws(M, N, splits))), device=cuda)
+    tickets = torch.zeros(((M + 127) // 128) * ((N + 127) // 128), dtype=torch.int32, device=cuda)
+    outs = []
+    for _ in range(2):
+        C = torch.full((M * N,), float("nan"), dtype=dt, device=cuda)
+        ops.gemm_big(A, lda, a_k, B, ldb, b_k, C, N, out_mode, M, N, K, 1.0, bias, epi == "bias_relu", mask,
+                     N if mask is not None else 0, splits, ws, tickets)
+        torch.cuda.synchronize()
+        outs.append(C)
+    assert torch.equal(outs[0], outs[1])
+    assert (tickets == 0).all()
+    ref = gemm_ref(A, lda, a_k, B, ldb, b_k, M, N, K, 1.0, bias, epi == "bias_relu", mask, N if mask is not None else 0)
+    got = outs[0].view(M, N).float()
+    assert torch.isfinite(got).all()
+    err = ((got - ref).norm() / ref.norm()).item()
+    assert err < (1e-2 if out_mode == 1 else 1e-5), err

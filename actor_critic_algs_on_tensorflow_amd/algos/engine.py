@@ -150,6 +150,7 @@ class CNNEngine:
         self.A1 = self.A + 1
         self.dev = flat.data.device
         self.ws = G.GemmWorkspace(self.dev)
+        self.big_ws = G.GemmBigWorkspace(self.dev) if self.dev.type == "cuda" else None
         tr = net.trunk
         assert tr.conv1.cin == 4 and tr.conv1.layout == "oihw" and tr.conv2.layout == "ohwi"
         idx = {id(p): i for i, p in enumerate(flat.params)}
@@ -278,8 +279,12 @@ class CNNEngine:
                        max_planes=self.fc_max_planes)
             self.last_fc = (hp, S)
             return shifted if want_shift else b.z
-        G.gemm(b.y3, 3136, True, self.sWfc, 512, False, b.h, 512, 1, B, 512, 3136, bias=self.bfc, relu=True,
-               workspace=ws)
+        if self.big_gemm_ok(B):   # 128 x 128 tiles, 2 splits: 256 workgroups at B = 4096
+            G.gemm_big(b.y3, 3136, True, self.sWfc, 512, False, b.h, 512, 1, B, 512, 3136, bias=self.bfc, relu=True,
+                       splits=2, workspace=self.big_ws)
+        else:
+            G.gemm(b.y3, 3136, True, self.sWfc, 512, False, b.h, 512, 1, B, 512, 3136, bias=self.bfc, relu=True,
+                   workspace=ws)
         if head:
             G.gemm(b.h, 512, True, self.sWh, self.A1, False, b.z, self.A1, 0, B, self.A1, 512, bias=self.bh,
                    workspace=ws)
@@ -477,13 +482,25 @@ class CNNEngine:
             return
         return self._backward_trunk(b, main, side, ev, ws, ws2)
 
+    def big_gemm_ok(self, B):
+        """The fc products of a ``B``-row learner batch run on gemm_big.hip (large tiles, LDS-DMA ring)."""
+        return self.big_ws is not None and 0 < self.opts.big_gemm_min_b <= B and B % 64 == 0
+
     def _backward_grouped(self, b, stage, ws, ws2):
         """One stream, no cross-stream edges: the independent products of each stage run as ONE grouped launch
         (ops.gemm.group) -- {dWfc, dy3}, then the fused dy3 -> dy2 -> dy1 kernel, then {dW3, dW2, dW1} as split-K
         planes, then the finaliser. Inside a captured graph every event edge between streams costs several
         microseconds of inter-queue synchronisation; here the critical path is the chain of launches itself."""
         B = b.B
-        if stage in ("all", "tail"):
+        if stage in ("all", "tail") and self.big_gemm_ok(B):
+            # dy3 = (dh Wfc^T) * (y3 > 0) [B, 3136] (K 512: no split), dWfc = y3^T dh [3136, 512] (K = B: 2 splits)
+            G.gemm_big(b.dh, 512, True, self.sWfc, 512, True, b.dy3, 3136, 1, B, 3136, 512, mask=b.y3, ldm=3136,
+                       workspace=self.big_ws)
+            G.gemm_big(b.y3, 3136, False, b.dh, 512, False, self.gWfc, 512, 0, 3136, 512, B, splits=2,
+                       workspace=self.big_ws)
+            if stage == "tail":
+                return
+        elif stage in ("all", "tail"):
             with G.group():   # workgroups start in product order: the critical-path product first
                 G.gemm(b.dh, 512, True, self.sWfc, 512, True, b.dy3, 3136, 1, B, 3136, 512, mask=b.y3, ldm=3136,
                        workspace=ws)

@@ -299,6 +299,39 @@ def gemm(A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha=1.0, bias=No
                 colsum_mod, tile, bk, splits, workspace, ga, ga_scale, gb, gb_scale, stamps)
 
 
+# gemm_big launch variant: bit 0 XCD-grouped workgroup order, bits 1-2 LDS ring depth - 2
+GEMM_BIG_VARIANT = 2
+
+
+class GemmBigWorkspace:
+    """Split-K slabs + self-cleaning tickets of :func:`gemm_big` (grown outside graph capture, shared by the
+    stream-ordered launches of one engine)."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.ws = torch.zeros(1, dtype=torch.float32, device=self.device)
+        self.tickets = torch.zeros(1, dtype=torch.int32, device=self.device)
+
+    def fit(self, M, N, splits):
+        need = int(_native.require().gemm_big_ws(M, N, splits))
+        if self.ws.numel() < need:
+            self.ws = torch.zeros(need, dtype=torch.float32, device=self.device)
+        tiles = -(-M // 128) * -(-N // 128)
+        if self.tickets.numel() < tiles:
+            self.tickets = torch.zeros(tiles, dtype=torch.int32, device=self.device)
+        return self
+
+
+def gemm_big(A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha=1.0, bias=None, relu=False, mask=None,
+             ldm=0, splits=1, workspace=None, variant=GEMM_BIG_VARIANT, stamps=None):
+    """Large plain bf16 product on the 128 x 128 / 32x32x16-MFMA kernel with LDS-DMA staging (``gemm_big.hip``):
+    out_mode 0 fp32 / 1 bf16 store, bias / relu / mask epilogue, slab split-K (deterministic). K % 64 == 0."""
+    ws = workspace.fit(M, N, splits) if splits > 1 else None
+    _native.require().gemm_big(A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, float(alpha), bias, bool(relu),
+                               mask, ldm, splits, ws.ws if ws else None, ws.tickets if ws else None, stamps,
+                               int(variant))
+
+
 def _view(t, rows, cols, ld, k_contig_rows):
     """Strided [rows, cols] view of a flat tensor with row stride ld (contiguous columns)."""
     return torch.as_strided(t, (rows, cols), (ld, 1), t.storage_offset())

@@ -1141,8 +1141,9 @@ static thread_local GemmGroupState g_gemm_group;
 void gemm_big(Tensor A, int64_t lda, bool a_k, Tensor B, int64_t ldb, bool b_k, Tensor C, int64_t ldc,
               int64_t out_mode, int64_t M, int64_t N, int64_t K, double alpha, c10::optional<Tensor> bias, bool relu,
               c10::optional<Tensor> mask, int64_t ldm, int64_t splits, c10::optional<Tensor> ws,
-              c10::optional<Tensor> tickets) {
+              c10::optional<Tensor> tickets, c10::optional<Tensor> stamps, int64_t variant) {
   TORCH_CHECK(out_mode == 0 || out_mode == 1, "gemm_big: out_mode 0 / 1");
+  TORCH_CHECK(variant >= 0 && variant < 8, "gemm_big: variant 0..7");
   TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "gemm_big: bf16 operands");
   TORCH_CHECK(C.scalar_type() == (out_mode == 1 ? at::kBFloat16 : at::kFloat), "gemm_big: C dtype mismatch");
   check_extent(A, a_k ? M : K, a_k ? K : M, lda, "A");
@@ -1178,6 +1179,12 @@ void gemm_big(Tensor A, int64_t lda, bool a_k, Tensor B, int64_t ldb, bool b_k, 
   d.relu = relu;
   d.alpha = (float)alpha;
   d.splits = (int)splits;
+  d.tile = (int)variant;
+  if (stamps.has_value() && stamps->defined()) {
+    const int64_t grid = ((M + 127) / 128) * ((N + 127) / 128) * std::max<int64_t>(splits, 1);
+    TORCH_CHECK(stamps->scalar_type() == at::kLong && stamps->numel() >= grid * 4, "gemm_big: stamps [grid, 4] int64");
+    d.stamps = reinterpret_cast<unsigned long long*>(stamps->data_ptr<int64_t>());
+  }
   check(aca_gemm_big(&d, cur_stream(C)), "gemm_big");
 }
 
@@ -1722,7 +1729,7 @@ TORCH_LIBRARY(acamd, m) {
   m.def("colsum_reduce(Tensor part, int R, int N, Tensor out, int mod) -> ()");
   m.def("gemm_big(Tensor A, int lda, bool a_k, Tensor B, int ldb, bool b_k, Tensor C, int ldc, int out_mode, int M, "
         "int N, int K, float alpha, Tensor? bias, bool relu, Tensor? mask, int ldm, int splits, Tensor? ws=None, "
-        "Tensor? tickets=None) -> ()");
+        "Tensor? tickets=None, Tensor? stamps=None, int variant=0) -> ()");
   m.def("gemm_big_ws(int M, int N, int splits) -> int", &gemm_big_ws);
   m.def("seg_stats(Tensor x, Tensor segs, Tensor out) -> ()");
   m.def("gemm_effective_splits(int K, int bk, int splits) -> int", &gemm_effective_splits);

@@ -170,6 +170,20 @@ __device__ __forceinline__ void block_sum_multi(double (&v)[N], double* sh) {
   __syncthreads();
 }
 
+// Fixed-order sum of per-workgroup records (N doubles each, `stride` apart) read by the last-arriving workgroup:
+// every thread takes a strided subset (independent loads in flight), then block_sum_multi. A one-thread walk is one
+// dependent cross-XCD load per record (~0.2 us each). `sh` as for block_sum_multi; results valid in every thread.
+template <int N>
+__device__ __forceinline__ void grid_records_sum(const double* part, int stride, unsigned nrec, double (&v)[N],
+                                                 double* sh) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = 0.0;
+  for (unsigned r = threadIdx.x; r < nrec; r += blockDim.x)
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] += part[(size_t)r * stride + i];
+  block_sum_multi<N>(v, sh);
+}
+
 // Last-arriver ticket (Guideline 16 counter form): every wave drains its stores, the block releases at agent
 // scope and takes a ticket; returns true in every thread of the block that arrived last. The caller then reads
 // the other blocks' results with plain loads (this function already performed the acquire).

@@ -21,17 +21,19 @@
 //   * split-K over the grid: each split writes its fp32 partial tile to a slab, the last-arriving split (agent-scope
 //     release / acquire ticket) sums the slabs in split order and runs the epilogue (deterministic).
 // Epilogue: *alpha, +bias[n], relu, *(mask[m][n] > 0), store fp32 | bf16.
-// Requirements (host-checked): plain bf16 operands, 16-byte aligned, lda / ldb % 8 == 0, K % 64 == 0 with every split
-// a whole number of k-steps, the m/n-contiguous extents % 8 == 0.
+// Requirements (host-checked): plain bf16 operands, 16-byte aligned, lda / ldb % 8 == 0, K % 64 == 0 (splits take
+// ceil(K / 64 / splits) k-steps each, the last one the rest), the m/n-contiguous extents % 8 == 0.
 #include "common.h"
 #include "gemm_desc.h"
 
 namespace aca {
 
-constexpr int GB_BM = 128, GB_BN = 128, GB_BK = 64, GB_T = 256, GB_STAGES = 3;
+constexpr int GB_BM = 128, GB_BN = 128, GB_BK = 64, GB_T = 256;
 constexpr int GB_TILE = 128 * 64;                      // bf16 elements of one operand stage (16 KB)
-constexpr int GB_LDS = GB_STAGES * 2 * GB_TILE + 64;   // + the last-arriver flag (one __shared__ array: a second
-                                                       // object makes hipcc wait vmcnt(0) before ds_reads)
+// ring of ST stages + the last-arriver flag (one __shared__ array: a second object makes hipcc wait vmcnt(0) before
+// ds_reads)
+template <int ST>
+constexpr int gb_lds() { return ST * 2 * GB_TILE + 64; }
 
 typedef float gb_f32x16 __attribute__((ext_vector_type(16)));
 typedef short gb_s4 __attribute__((ext_vector_type(4)));
@@ -89,14 +91,21 @@ __device__ __forceinline__ bf16x8 gb_frag_mn(const u16* __restrict__ t, int base
 struct GbParams {
   AcaGemmDesc d;
   int tiles_n, splits, ksteps_per_split;
+  int xcd;   // XCD-grouped workgroup order (grid % 8 == 0)
 };
 
-template <bool A_K, bool B_K>
+template <bool A_K, bool B_K, int ST>
 __global__ void __launch_bounds__(GB_T) gemm_big_kernel(GbParams P) {
-  __shared__ __attribute__((aligned(16))) u16 smem[GB_LDS];
+  __shared__ __attribute__((aligned(16))) u16 smem[gb_lds<ST>()];
   const AcaGemmDesc& d = P.d;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int tile = blockIdx.x / P.splits, z = blockIdx.x - tile * P.splits;
+  unsigned long long* st = d.stamps ? d.stamps + (size_t)blockIdx.x * 4 : nullptr;
+  if (st && tid == 0) st[0] = __builtin_amdgcn_s_memrealtime();
+  // workgroups are dealt round-robin over the 8 XCDs (each its own L2): give every XCD a contiguous run of tiles, so
+  // the n-tiles sharing an A row block (and the splits of a tile) meet in one L2
+  int bid = blockIdx.x;
+  if (P.xcd) bid = (bid & 7) * (int)(gridDim.x >> 3) + (bid >> 3);
+  const int tile = bid / P.splits, z = bid - tile * P.splits;
   const int m0 = (tile / P.tiles_n) * GB_BM, n0 = (tile % P.tiles_n) * GB_BN;
   const int ks0 = z * P.ksteps_per_split;
   const int nk = min(P.ksteps_per_split, d.K / GB_BK - ks0);
@@ -105,7 +114,7 @@ __global__ void __launch_bounds__(GB_T) gemm_big_kernel(GbParams P) {
   auto stA = [&](int s) { return smem + s * 2 * GB_TILE; };
   auto stB = [&](int s) { return smem + s * 2 * GB_TILE + GB_TILE; };
   auto issue = [&](int kt) {
-    const int s = kt % GB_STAGES, k0 = (ks0 + kt) * GB_BK;
+    const int s = kt % ST, k0 = (ks0 + kt) * GB_BK;
     gb_stage<A_K>(Ag, d.lda, m0, d.M, k0, stA(s));
     gb_stage<B_K>(Bg, d.ldb, n0, d.N, k0, stB(s));
   };
@@ -117,18 +126,28 @@ __global__ void __launch_bounds__(GB_T) gemm_big_kernel(GbParams P) {
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-  if (nk > 0) issue(0);
-  if (nk > 1) issue(1);
+#pragma unroll
+  for (int q = 0; q < ST - 1; ++q)
+    if (q < nk) issue(q);
   for (int kt = 0; kt < nk; ++kt) {
-    // this wave's copies of k-step kt have landed (kt + 1's 8 may still fly), every wave's LDS reads of the stage
-    // the next issue overwrites are done; the barrier publishes both
-    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // this wave's copies of k-step kt have landed (the newer k-steps' 8 each may still fly), every wave's LDS reads
+    // of the stage the next issue overwrites are done; the barrier publishes both
+    const int newer = min(ST - 2, nk - 1 - kt);
+    if constexpr (ST >= 4) {
+      if (newer >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else if (newer == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if constexpr (ST == 3) {
+      if (newer >= 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (kt + 2 < nk) issue(kt + 2);
-    const u16* ta = stA(kt % GB_STAGES);
-    const u16* tb = stB(kt % GB_STAGES);
+    if (kt + ST - 1 < nk) issue(kt + ST - 1);
+    const u16* ta = stA(kt % ST);
+    const u16* tb = stB(kt % ST);
     // every fragment of the k-step requested before the first MFMA (the LDS reads of later 16-deep slices overlap
     // the MFMAs of earlier ones; the compiler counts lgkmcnt down slice by slice)
     bf16x8 af[GB_BK / 16][2], bfr[GB_BK / 16][2];
@@ -149,6 +168,7 @@ __global__ void __launch_bounds__(GB_T) gemm_big_kernel(GbParams P) {
         for (int j = 0; j < 2; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
   }
+  if (st && tid == 0) st[1] = __builtin_amdgcn_s_memrealtime();
   // ---------------------------------------------------------------- split-K: slabs + last arriver, in split order
   if (P.splits > 1) {
     float* slab = d.ws + ((size_t)tile * P.splits + z) * (GB_BM * GB_BN);
@@ -158,7 +178,7 @@ __global__ void __launch_bounds__(GB_T) gemm_big_kernel(GbParams P) {
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) slab[((i * 2 + j) * 16 + r) * GB_T + tid] = acc[i][j][r];
-    int* flag = reinterpret_cast<int*>(smem + GB_STAGES * 2 * GB_TILE);
+    int* flag = reinterpret_cast<int*>(smem + ST * 2 * GB_TILE);
     if (!last_block_arrival(&d.tickets[tile], P.splits, flag)) return;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -176,6 +196,7 @@ __global__ void __launch_bounds__(GB_T) gemm_big_kernel(GbParams P) {
           for (int r = 0; r < 16; ++r) acc[i][j][r] += sl[((i * 2 + j) * 16 + r) * GB_T + tid];
     }
   }
+  if (st && tid == 0) st[2] = __builtin_amdgcn_s_memrealtime();
   // ---------------------------------------------------------------- epilogue
   // bias and mask operands fetched for every output of this thread up front, from clamped (always valid) addresses:
   // a guarded load per output would be one dependent memory round trip each
@@ -214,6 +235,10 @@ __global__ void __launch_bounds__(GB_T) gemm_big_kernel(GbParams P) {
       }
     }
   }
+  if (st) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (tid == 0) st[3] = __builtin_amdgcn_s_memrealtime();
+  }
 }
 
 }  // namespace aca
@@ -233,7 +258,8 @@ extern "C" hipError_t aca_gemm_big(const AcaGemmDesc* d, hipStream_t stream) {
   if (d->out_mode != 0 && d->out_mode != 1) return hipErrorInvalidValue;
   const int splits = d->splits < 1 ? 1 : d->splits;
   const int ksteps = d->K / GB_BK;
-  if (d->K % GB_BK || ksteps % splits) return hipErrorInvalidValue;
+  const int per = (ksteps + splits - 1) / splits;   // the last split may be shorter; every split gets >= 1 k-step
+  if (d->K % GB_BK || ksteps < 1 || per * (splits - 1) >= ksteps) return hipErrorInvalidValue;
   if ((d->lda % 8) || (d->ldb % 8) || (reinterpret_cast<uintptr_t>(d->A) % 16) ||
       (reinterpret_cast<uintptr_t>(d->B) % 16))
     return hipErrorInvalidValue;
@@ -243,12 +269,20 @@ extern "C" hipError_t aca_gemm_big(const AcaGemmDesc* d, hipStream_t stream) {
   P.d = *d;
   P.tiles_n = (d->N + GB_BN - 1) / GB_BN;
   P.splits = splits;
-  P.ksteps_per_split = ksteps / splits;
+  P.ksteps_per_split = per;
   const int tiles = ((d->M + GB_BM - 1) / GB_BM) * P.tiles_n;
   const dim3 grid(tiles * splits);
-  if (d->a_k && d->b_k) gemm_big_kernel<true, true><<<grid, GB_T, 0, stream>>>(P);
-  else if (d->a_k) gemm_big_kernel<true, false><<<grid, GB_T, 0, stream>>>(P);
-  else if (d->b_k) gemm_big_kernel<false, true><<<grid, GB_T, 0, stream>>>(P);
-  else gemm_big_kernel<false, false><<<grid, GB_T, 0, stream>>>(P);
+  // d->tile: variant bits (bit 0 XCD-grouped order, bits 1-2 ring depth - 2)
+  P.xcd = (d->tile & 1) && (grid.x % 8 == 0);
+  const int st = 2 + ((d->tile >> 1) & 3);
+#define GB_LAUNCH(S)                                                                        \
+  if (d->a_k && d->b_k) gemm_big_kernel<true, true, S><<<grid, GB_T, 0, stream>>>(P);       \
+  else if (d->a_k) gemm_big_kernel<true, false, S><<<grid, GB_T, 0, stream>>>(P);           \
+  else if (d->b_k) gemm_big_kernel<false, true, S><<<grid, GB_T, 0, stream>>>(P);           \
+  else gemm_big_kernel<false, false, S><<<grid, GB_T, 0, stream>>>(P);
+  if (st == 2) { GB_LAUNCH(2) }
+  else if (st == 3) { GB_LAUNCH(3) }
+  else { GB_LAUNCH(4) }
+#undef GB_LAUNCH
   return hipGetLastError();
 }

@@ -17,7 +17,8 @@
 // The cross-row sums are deterministic: each workgroup writes its partial dWh / dbh / dbfc as one plane (rows of
 // the workgroup summed in a fixed order, waves combined in wave order through LDS) -- the engine's gradient
 // finaliser reduces the planes in plane order -- and its loss statistics (fp64) as one record; the last-arriving
-// workgroup (agent-scope release / acquire ticket, common.h last_block_arrival) sums the records in workgroup order.
+// workgroup (agent-scope release / acquire ticket, common.h last_block_arrival) sums the records in a fixed order
+// (common.h grid_records_sum).
 #include "common.h"
 #include "ppo_head.h"
 
@@ -29,6 +30,7 @@ __global__ void __launch_bounds__(PH_THREADS) ppo_head_kernel(PpoHeadArgs p) {
   __shared__ float s_red[PH_THREADS / 64][PH_H * A1];   // per-wave dWh partials (wave-ordered combine)
   __shared__ float s_rb[PH_THREADS / 64][PH_H];          // per-wave dbfc partials
   __shared__ double s_st[PH_THREADS / 64][PH_NSTAT + A1];
+  __shared__ double s_sum[16 * PH_NSTAT];                 // last workgroup: statistics reduction
   __shared__ int sh_flag;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wg = blockIdx.x;
@@ -204,12 +206,14 @@ __global__ void __launch_bounds__(PH_THREADS) ppo_head_kernel(PpoHeadArgs p) {
                                             s_st[2][PH_NSTAT + tid]) + s_st[3][PH_NSTAT + tid]);
   if (tid < PH_NSTAT)
     p.pstats[(size_t)wg * PH_NSTAT + tid] = ((s_st[0][tid] + s_st[1][tid]) + s_st[2][tid]) + s_st[3][tid];
-  // ---- statistics: the last workgroup sums the records in workgroup order
+  // ---- statistics: the last workgroup sums the records (fixed order)
   if (!last_block_arrival(p.ticket, gridDim.x, &sh_flag)) return;
-  if (tid < PH_NSTAT) {
-    double t = 0.0;
-    for (int w = 0; w < (int)gridDim.x; ++w) t += p.pstats[(size_t)w * PH_NSTAT + tid];
-    s_st[0][tid] = t;
+  {
+    double t[PH_NSTAT];
+    grid_records_sum<PH_NSTAT>(p.pstats, PH_NSTAT, gridDim.x, t, s_sum);
+    if (tid == 0)
+#pragma unroll
+      for (int q = 0; q < PH_NSTAT; ++q) s_st[0][q] = t[q];
   }
   __syncthreads();
   if (tid == 0) {

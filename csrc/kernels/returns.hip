@@ -423,10 +423,12 @@ __global__ void __launch_bounds__(RS_THREADS) returns_scan_kernel(RetScanArgs a)
   block_sum_multi<RS_MOM>(m, s_red);
   if (tid < RS_MOM) a.part[(size_t)blockIdx.x * 8 + tid] = m[tid];
   if (!last_block_arrival(a.ticket, gridDim.x, &s_flag)) return;
-  if (tid < RS_MOM) {
-    double s = 0.0;
-    for (unsigned b = 0; b < gridDim.x; ++b) s += a.part[(size_t)b * 8 + tid];
-    s_tot[1 + tid] = s;
+  {
+    double s[RS_MOM];
+    grid_records_sum<RS_MOM>(a.part, 8, gridDim.x, s, s_red);
+    if (tid == 0)
+#pragma unroll
+      for (int k = 0; k < RS_MOM; ++k) s_tot[1 + k] = s[k];
   }
   __syncthreads();
   const double cnt = (double)T * N;
@@ -496,10 +498,12 @@ __global__ void __launch_bounds__(RS_THREADS) ev_multi_kernel(const float* __res
   block_sum_multi<5>(m, sh);
   if (threadIdx.x < 5) part[(size_t)blockIdx.x * 8 + threadIdx.x] = m[threadIdx.x];
   if (!last_block_arrival(ticket, gridDim.x, &s_flag)) return;
-  if (threadIdx.x < 5) {
-    double s = 0.0;
-    for (unsigned b = 0; b < gridDim.x; ++b) s += part[(size_t)b * 8 + threadIdx.x];
-    s_tot[threadIdx.x] = s;
+  {
+    double s[5];
+    grid_records_sum<5>(part, 8, gridDim.x, s, sh);
+    if (threadIdx.x == 0)
+#pragma unroll
+      for (int k = 0; k < 5; ++k) s_tot[k] = s[k];
   }
   __syncthreads();
   if (threadIdx.x == 0) {

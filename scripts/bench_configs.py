@@ -2,7 +2,7 @@
 """Throughput of every BASELINE.json config on one device (env-steps/s, ms per update), one JSON line per config.
 
     python scripts/bench_configs.py [--configs pong_a2c,breakout_ppo,mujoco_ppo_dp8,cartpole_cpu] [--updates K]
-                                    [--warmup W] [--engine auto|torch] [--device cuda:0]
+                                    [--warmup W] [--engine auto|torch] [--device cuda:0] [--engine-opts JSON]
 
 Each config runs with its preset (config.py PRESETS): same model, env bank, rollout length, optimiser and PPO
 epochs/minibatches as BASELINE.json names; synthetic envs and random-init weights. The update is captured as a
@@ -23,12 +23,15 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 
-def run(name, updates, warmup, engine, device, dp_world1=False):
+def run(name, updates, warmup, engine, device, dp_world1=False, engine_opts=None):
     from actor_critic_algs_on_tensorflow_amd import preset
     from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
     dev = device if name != "cartpole_cpu" or device == "cpu" else device
     cfg = preset(name, device=dev, outdir=None, quiet=True, stdout_freq=0, save_every=0, engine=engine,
                  cuda_graph=dev.startswith("cuda"))
+    if engine_opts:
+        import dataclasses
+        cfg.engine_opts = dataclasses.replace(cfg.engine_opts, **engine_opts)
     dp = None
     if dp_world1:
         # the data-parallel update at world size 1 (RCCL on a GPU): every collective of the DP schedule is issued
@@ -60,6 +63,7 @@ def run(name, updates, warmup, engine, device, dp_world1=False):
             "updates": updates, "envs": tr.env.num_envs, "n_steps": cfg.n_steps, "algo": cfg.algo,
             "engine": "native-cnn" if tr.engine is not None else ("native-mlp" if tr.mlp is not None else "torch"),
             "hipgraph": bool(tr.graph), "device": dev, "dp_world1": bool(dp_world1),
+            "engine_opts": engine_opts or {},
             "ppo": {"epochs": cfg.ppo_epochs, "minibatches": cfg.ppo_minibatches} if cfg.algo == "ppo" else None}
 
 
@@ -71,9 +75,11 @@ def main():
     ap.add_argument("--engine", default="auto")
     ap.add_argument("--device", default="cuda:0" if torch.cuda.is_available() else "cpu")
     ap.add_argument("--dp-world1", action="store_true", help="run the data-parallel schedule at world size 1")
+    ap.add_argument("--engine-opts", default="", help='JSON EngineOpts overrides, e.g. \'{"ppo_head": false}\'')
     args = ap.parse_args()
+    opts = json.loads(args.engine_opts) if args.engine_opts else None
     for name in args.configs.split(","):
-        print(json.dumps(run(name, args.updates, args.warmup, args.engine, args.device, args.dp_world1)), flush=True)
+        print(json.dumps(run(name, args.updates, args.warmup, args.engine, args.device, args.dp_world1, opts)), flush=True)
 
 
 if __name__ == "__main__":

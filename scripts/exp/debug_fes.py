@@ -1,4 +1,7 @@
 """Compare one rollout of the per-env fused step against the unfused per-env trunk + policy/env launches."""
+import os
+import sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch
 from actor_critic_algs_on_tensorflow_amd import preset
 from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer

@@ -195,6 +195,10 @@ class ActorCriticTrainer:
         self._rec = None            # SegmentRecorder while capturing a segmented (DP) update
         self._grad_sink = None      # async PS worker: replaces all-reduce + optimiser (algos/a3c_gpu.py)
         self._kl_buf = torch.zeros(1, dtype=torch.float32, device=self.device) if dp is not None else None
+        # deferred post-update KL [sum over ranks, ranks that wrote it] (_kl_deferred); re-pointed into the returns
+        # scan's moment buffer once that exists, so it travels in the same all-reduce
+        self._kl_tail = torch.zeros(2, dtype=torch.float64, device=self.device) if dp is not None else None
+        self._kl_defer_on = True
         self.logger = None
         if self.rank == 0 and cfg.outdir:
             self.logger = Logger(cfg.outdir, legacy_step_index=cfg.legacy_step_index, metrics_path=cfg.metrics_path,
@@ -415,6 +419,8 @@ class ActorCriticTrainer:
             T, N = st.T, st.N
             if getattr(self, "_scan_ws", None) is None:
                 self._scan_ws = R.ScanWorkspace(self.device, T, N)
+                if self._kl_tail is not None:
+                    self._kl_tail = self._scan_ws.mom[8:10]
                 self._scan_ret = torch.empty(T * N, device=self.device)
                 self._scan_adv = torch.empty(T * N, device=self.device)
             # native PPO: the minibatch gather normalises while it copies (no pass over the whole batch here)
@@ -428,7 +434,8 @@ class ActorCriticTrainer:
                                            adv_out=self._scan_adv)
             if cfg.norm_adv and self.dp is not None:
                 dp = self.dp
-                self._comm(lambda: dp.allreduce_sum_(mom))
+                self._comm(lambda: dp.allreduce_sum_(mom))   # moments [0:8] + the deferred KL [8:10]
+                self._settle_kl()
                 if not defer:
                     _native.require().normalize_mom(self._scan_adv, self._scan_adv, mom, 1e-8)
             if defer:
@@ -443,7 +450,9 @@ class ActorCriticTrainer:
 
     def _normalize(self, adv):
         if self.dp is not None:
-            return self.dp.normalize_advantages(adv)
+            out = self.dp.normalize_advantages(adv, extra=self._kl_tail if self._kl_deferred() else None)
+            self._settle_kl()
+            return out
         if _native.use_native(adv):
             _native.require().normalize(adv.contiguous(), self.adv_buf, 1e-8)
             return self.adv_buf
@@ -633,8 +642,43 @@ class ActorCriticTrainer:
         logp, _, v = self.model.evaluate(obs, actions)
         self._kl_and_lr(logp_old, logp, ret, v)
 
+    def _kl_deferred(self):
+        """DP with global advantage normalisation: the post-update KL proxy is not all-reduced on its own but rides
+        in the NEXT update's advantage-moments all-reduce (one packed fp64 collective per update for both, SURVEY
+        §5.8). The KL-adaptive lr rule then runs right after that all-reduce -- before the next update's first
+        optimiser step, the first place the rule's result is used, so the lr sequence is unchanged. Until then
+        ``stats["kl"]`` holds this rank's KL; :meth:`flush_kl` settles a pending KL (checkpoints, end of train)."""
+        return (self.dp is not None and self.cfg.norm_adv and self._kl_defer_on and not self._fused_returns()
+                and (self.lr_ctrl is not None or self.cfg.kl_coef > 0))
+
+    def _settle_kl(self):
+        """Consumes the all-reduced deferred KL slot (no-op on the device when nothing was pending)."""
+        if not self._kl_deferred():
+            return
+        t = self._kl_tail
+        valid = t[1] > 0
+        kl = (t[0] / torch.clamp(t[1], min=1.0)).float()
+        self.stats["kl"].copy_(torch.where(valid, kl, self.stats["kl"]))
+        if self.lr_ctrl is not None:
+            self.lr_ctrl.update_(self.actor_opt.lr, kl, valid)
+        t.zero_()
+
+    @torch.no_grad()
+    def flush_kl(self):
+        """Settles a KL still waiting for the next moments all-reduce: one standalone all-reduce of the 2-slot
+        tail. Collective: every rank calls it at the same point (save_checkpoint and the end of train do)."""
+        if not self._kl_deferred():
+            return
+        self.dp.allreduce_sum_(self._kl_tail)
+        self._settle_kl()
+
     def _kl_and_lr(self, logp_old, logp, ret, v):
         kl = ((logp_old - logp) ** 2).mean()
+        if self._kl_deferred():
+            self._kl_tail.copy_(torch.stack([kl.double(), torch.ones((), dtype=torch.float64, device=kl.device)]))
+            self.stats["kl"].copy_(kl)   # this rank's value until the next moments all-reduce
+            self._ev(ret, v, "ev_after")
+            return
         if self.dp is not None:   # in-place device all-reduce: capturable as a segment cut
             dp, buf = self.dp, self._kl_buf
             buf.copy_(kl.reshape(1))
@@ -836,10 +880,14 @@ class ActorCriticTrainer:
     #       AR(C) issued, overlapping the next update's rollout.
     #     Every gradient is on-policy for its batch (computed at the parameters that acted) and applied one update
     #     late (delayed-gradient SGD with staleness 1).
-    # Every other DP configuration (PPO minibatch steps, global advantage normalisation, the KL-adaptive lr / KL
-    # proxy, the MLP engine) is captured by a SegmentRecorder: one graph chain per update, cut at each collective
-    # (gradient all-reduce per optimiser step, the packed fp64 advantage moments, the KL scalar), every collective
-    # an in-place stream-ordered RCCL call on a persistent buffer. No DP configuration runs eagerly.
+    # Capture selection (_capture_set, in this order):
+    #   * the gloo / lag-1 A2C segment schedules above (_segmented);
+    #   * RCCL (_inline_comm), every other algorithm and engine (PPO minibatch steps, global advantage moments, the
+    #     KL-adaptive lr / KL proxy, the MLP engine): ONE graph per update with every collective recorded in it;
+    #   * gloo DP outside the A2C schedules, or a gradient sink (A3C worker): a SegmentRecorder -- one graph chain
+    #     per update cut at each host-issued collective;
+    #   * no DP: one graph.
+    # No DP configuration runs eagerly.
 
     def _can_capture(self):
         return self.cfg.cuda_graph and self.device.type == "cuda"
@@ -1109,12 +1157,14 @@ class ActorCriticTrainer:
             if callback is not None:
                 callback(self, it)
         self.flush_pending()
+        self.flush_kl()
         self.check_health()
         return history
 
     # ------------------------------------------------------------------ checkpoints
     def save_checkpoint(self, path=None):
         self.check_health()
+        self.flush_kl()
         from ..ckpt import save_trainer
         return save_trainer(self, path)
 

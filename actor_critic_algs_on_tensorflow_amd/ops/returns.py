@@ -144,7 +144,8 @@ class ScanWorkspace:
         self.ticket = torch.zeros(4, dtype=torch.int32, device=self.device)
         self.ev_ticket = torch.zeros(4, dtype=torch.int32, device=self.device)
         self.ev_part = torch.zeros(64 * 8, dtype=torch.float64, device=self.device)
-        self.mom = torch.zeros(8, dtype=torch.float64, device=self.device)
+        # [0:8] the moments; [8:10] a slot the trainer packs into the same all-reduce (its deferred KL)
+        self.mom = torch.zeros(10, dtype=torch.float64, device=self.device)
         self.gz = torch.zeros(max(T * N, 1), dtype=torch.float64, device=self.device)
 
     def fit(self, T, N):

@@ -130,11 +130,17 @@ class DataParallel:
 
     # -- statistics ---------------------------------------------------------------------------------------------
     @torch.no_grad()
-    def normalize_advantages(self, adv, eps=1e-8):
-        """Global population-std normalisation across ranks (one packed all-reduce of [sum, sumsq, n])."""
+    def normalize_advantages(self, adv, eps=1e-8, extra=None):
+        """Global population-std normalisation across ranks (one packed all-reduce of [sum, sumsq, n]). ``extra``:
+        a small fp64 tensor summed in the same collective (written back in place; e.g. the deferred KL slot)."""
         a = adv.float()
         s = torch.stack([a.sum(), (a * a).sum(), torch.tensor(float(a.numel()), device=a.device)]).double()
+        if extra is not None:
+            s = torch.cat([s, extra.reshape(-1)])
+        self.issued += 1
         dist.all_reduce(s, group=self.group)
+        if extra is not None:
+            extra.copy_(s[3:].reshape(extra.shape))
         mean = s[0] / s[2]
         var = torch.clamp(s[1] / s[2] - mean * mean, min=0.0)
         return ((a - mean.float()) / (eps + var.sqrt().float()))

@@ -71,10 +71,13 @@ class DeviceKLAdaptiveLR(KLAdaptiveLR):
     """
 
     @torch.no_grad()
-    def update_(self, lr: torch.Tensor, kl: torch.Tensor) -> torch.Tensor:
+    def update_(self, lr: torch.Tensor, kl: torch.Tensor, valid: torch.Tensor | None = None) -> torch.Tensor:
+        """``valid`` (0-d bool tensor): apply the rule only where it is true (a deferred KL that may be absent)."""
         up = torch.clamp(lr * self.factor, max=self.max_lr)
         down = torch.clamp(lr / self.factor, min=self.min_lr)
         new = torch.where(kl < self.desired_kl / 4, up, torch.where(kl > self.desired_kl * 4, down, lr))
+        if valid is not None:
+            new = torch.where(valid, new, lr)
         lr.copy_(new)
         return lr
 

@@ -80,7 +80,7 @@ def test_basic_ac_parity_trainer(tmp_path):
 
 
 # ------------------------------------------------------------------------------------------------ distributed
-def _dp_worker(rank, world, port, out_dir, n_envs=4, extra=None):
+def _dp_worker(rank, world, port, out_dir, n_envs=4, extra=None, updates=3, kl_defer=True):
     import torch.distributed as dist
     from actor_critic_algs_on_tensorflow_amd.parallel.dp import DataParallel
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -88,9 +88,15 @@ def _dp_worker(rank, world, port, out_dir, n_envs=4, extra=None):
     cfg = preset("cartpole_cpu", **_quiet(num_envs=n_envs, n_steps=5, seed=11, optimizer="adam", max_grad_norm=0.5,
                                           **(extra or {})))
     tr = ActorCriticTrainer(cfg, dp=DataParallel())
-    for _ in range(3):
+    tr._kl_defer_on = kl_defer
+    lrs = []
+    for _ in range(updates):
         tr.step()
-    torch.save({"p": tr.flat.data.clone(), "kl": float(tr.stats["kl"])}, os.path.join(out_dir, f"dp{rank}.pt"))
+        lrs.append(float(tr.actor_opt.get_lr()))
+    issued = tr.dp.issued
+    tr.flush_kl()   # a deferred KL (DP + norm_adv) is settled here, as at a checkpoint / the end of train()
+    torch.save({"p": tr.flat.data.clone(), "kl": float(tr.stats["kl"]), "lr": float(tr.actor_opt.get_lr()),
+                "lrs": lrs, "issued": issued}, os.path.join(out_dir, f"dp{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -129,6 +135,26 @@ def test_dp_gloo_world4_ppo_kl_lr_and_bf16_buckets(tmp_path):
     d_fp, d_bf = fp[0]["p"] - p0, bf[0] - p0
     cos = float(torch.nn.functional.cosine_similarity(d_fp.double(), d_bf.double(), dim=0))
     assert cos > 0.97, cos
+
+
+def test_dp_gloo_kl_rides_in_moments_allreduce(tmp_path):
+    """DP + global adv norm + KL-adaptive lr: the post-update KL is packed into the next update's moments
+    all-reduce (one non-gradient collective per update instead of two). Same parameters, lr sequence (shifted by
+    one update: applied before the next optimiser step instead of after this one) and settled KL as the
+    standalone-collective schedule."""
+    extra = dict(algo="ppo", ppo_epochs=2, ppo_minibatches=2, kl_adaptive_lr=True, desired_kl=1e-4, lr=3e-3)
+    out = {}
+    for defer in (True, False):
+        d = tmp_path / str(defer)
+        d.mkdir()
+        mp.spawn(_dp_worker, args=(2, _free_port(), str(d), 2, extra, 6, defer), nprocs=2, join=True)
+        out[defer] = [torch.load(d / f"dp{r}.pt", weights_only=True) for r in range(2)]
+    a, b = out[True][0], out[False][0]
+    assert torch.equal(a["p"], b["p"]) and a["lr"] == b["lr"] and a["kl"] == pytest.approx(b["kl"], rel=1e-6)
+    assert a["lrs"][1:] == b["lrs"][:-1], (a["lrs"], b["lrs"])
+    assert len(set(b["lrs"])) > 1, "the lr rule never fired: the comparison is vacuous"
+    assert b["issued"] - a["issued"] == 6, (a["issued"], b["issued"])   # one KL collective per update saved
+    assert torch.equal(out[True][1]["p"], a["p"]) and out[True][1]["kl"] == a["kl"]
 
 
 def _a3c_proc(rank, world, port, d):

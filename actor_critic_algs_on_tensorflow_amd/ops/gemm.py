@@ -299,8 +299,9 @@ def gemm(A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha=1.0, bias=No
                 colsum_mod, tile, bk, splits, workspace, ga, ga_scale, gb, gb_scale, stamps)
 
 
-# gemm_big launch variant: bit 0 XCD-grouped workgroup order, bits 1-2 LDS ring depth - 2
-GEMM_BIG_VARIANT = 2
+# gemm_big launch variant: bit 0 XCD-grouped workgroup order, bits 1-2 LDS ring depth - 2 (2: 64 KB LDS, two
+# workgroups per CU -- measured fastest on all three fc products), bit 3 scalar bf16 epilogue
+GEMM_BIG_VARIANT = 1
 
 
 class GemmBigWorkspace:

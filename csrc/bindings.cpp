@@ -1143,7 +1143,7 @@ void gemm_big(Tensor A, int64_t lda, bool a_k, Tensor B, int64_t ldb, bool b_k, 
               c10::optional<Tensor> mask, int64_t ldm, int64_t splits, c10::optional<Tensor> ws,
               c10::optional<Tensor> tickets, c10::optional<Tensor> stamps, int64_t variant) {
   TORCH_CHECK(out_mode == 0 || out_mode == 1, "gemm_big: out_mode 0 / 1");
-  TORCH_CHECK(variant >= 0 && variant < 8, "gemm_big: variant 0..7");
+  TORCH_CHECK(variant >= 0 && variant < 16, "gemm_big: variant 0..15");
   TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "gemm_big: bf16 operands");
   TORCH_CHECK(C.scalar_type() == (out_mode == 1 ? at::kBFloat16 : at::kFloat), "gemm_big: C dtype mismatch");
   check_extent(A, a_k ? M : K, a_k ? K : M, lda, "A");
@@ -1182,7 +1182,7 @@ void gemm_big(Tensor A, int64_t lda, bool a_k, Tensor B, int64_t ldb, bool b_k, 
   d.tile = (int)variant;
   if (stamps.has_value() && stamps->defined()) {
     const int64_t grid = ((M + 127) / 128) * ((N + 127) / 128) * std::max<int64_t>(splits, 1);
-    TORCH_CHECK(stamps->scalar_type() == at::kLong && stamps->numel() >= grid * 4, "gemm_big: stamps [grid, 4] int64");
+    TORCH_CHECK(stamps->scalar_type() == at::kLong && stamps->numel() >= grid * 8, "gemm_big: stamps [grid, 8] int64");
     d.stamps = reinterpret_cast<unsigned long long*>(stamps->data_ptr<int64_t>());
   }
   check(aca_gemm_big(&d, cur_stream(C)), "gemm_big");

@@ -91,7 +91,8 @@ __device__ __forceinline__ bf16x8 gb_frag_mn(const u16* __restrict__ t, int base
 struct GbParams {
   AcaGemmDesc d;
   int tiles_n, splits, ksteps_per_split;
-  int xcd;   // XCD-grouped workgroup order (grid % 8 == 0)
+  int xcd;       // XCD-grouped workgroup order (grid % 8 == 0)
+  int vec_epi;   // bf16 output staged through LDS, 16-byte mask loads / C stores (N, ldc, ldm % 8 == 0, aligned)
 };
 
 template <bool A_K, bool B_K, int ST>
@@ -99,8 +100,13 @@ __global__ void __launch_bounds__(GB_T) gemm_big_kernel(GbParams P) {
   __shared__ __attribute__((aligned(16))) u16 smem[gb_lds<ST>()];
   const AcaGemmDesc& d = P.d;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  unsigned long long* st = d.stamps ? d.stamps + (size_t)blockIdx.x * 4 : nullptr;
-  if (st && tid == 0) st[0] = __builtin_amdgcn_s_memrealtime();
+  // diagnostics: [start, k-loop done, split reduce done, end, HW_ID, XCC_ID] per workgroup (vector stores)
+  unsigned long long* st = d.stamps ? d.stamps + (size_t)blockIdx.x * 8 : nullptr;
+  if (st && tid == 0) {
+    st[0] = __builtin_amdgcn_s_memrealtime();
+    st[4] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+    st[5] = (unsigned)__builtin_amdgcn_s_getreg((15 << 11) | 20);
+  }
   // workgroups are dealt round-robin over the 8 XCDs (each its own L2): give every XCD a contiguous run of tiles, so
   // the n-tiles sharing an A row block (and the splits of a tile) meet in one L2
   int bid = blockIdx.x;
@@ -198,9 +204,62 @@ __global__ void __launch_bounds__(GB_T) gemm_big_kernel(GbParams P) {
   }
   if (st && tid == 0) st[2] = __builtin_amdgcn_s_memrealtime();
   // ---------------------------------------------------------------- epilogue
+  const u16* mask = reinterpret_cast<const u16*>(d.mask);
+  if (d.out_mode == 1 && P.vec_epi) {
+    // bf16 tile staged through LDS ([128][136]: the two 32-lane halves of a ds_write_b16 land in disjoint banks,
+    // every 16-lane ds_read_b128 phase reads one conflict-free 256-byte row), then whole 16-byte mask loads and C
+    // stores (8 per thread instead of 64 two-byte ones: full cache lines)
+    constexpr int LDC = GB_BN + 8;
+    const int er = tid >> 4, ec = (tid & 15) * 8;
+    uint4 mv[8];
+    if (mask) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {   // issued first: their latency hides behind the LDS staging
+        const int m = min(m0 + q * 16 + er, d.M - 1), n = min(n0 + ec, d.N - 8);
+        mv[q] = *reinterpret_cast<const uint4*>(mask + (int64_t)m * d.ldm + n);
+      }
+    }
+    float bv[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) bv[j] = d.bias ? d.bias[min(n0 + wn + 32 * j + (lane & 31), d.N - 1)] : 0.f;
+    __syncthreads();   // every wave is past its last ring read
+    u16* sc = smem;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float v = acc[i][j][r] * d.alpha + bv[j];
+          if (d.relu) v = fmaxf(v, 0.f);
+          const int row = wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          sc[row * LDC + wn + 32 * j + (lane & 31)] = f2bf(v);
+        }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int row = q * 16 + er, m = m0 + row, n = n0 + ec;
+      uint4 v = *reinterpret_cast<const uint4*>(sc + row * LDC + ec);
+      if (mask) {
+        uint32_t* w = reinterpret_cast<uint32_t*>(&v);
+        const uint32_t* mw = reinterpret_cast<const uint32_t*>(&mv[q]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t lo = (mw[e] << 16), hi = (mw[e] & 0xFFFF0000u);
+          const uint32_t keep = (__uint_as_float(lo) > 0.f ? 0x0000FFFFu : 0u) | (__uint_as_float(hi) > 0.f ? 0xFFFF0000u : 0u);
+          w[e] &= keep;
+        }
+      }
+      if (m < d.M && n < d.N) *reinterpret_cast<uint4*>(reinterpret_cast<u16*>(d.C) + (int64_t)m * d.ldc + n) = v;
+    }
+    if (st) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (tid == 0) st[3] = __builtin_amdgcn_s_memrealtime();
+    }
+    return;
+  }
   // bias and mask operands fetched for every output of this thread up front, from clamped (always valid) addresses:
   // a guarded load per output would be one dependent memory round trip each
-  const u16* mask = reinterpret_cast<const u16*>(d.mask);
   float bv[2];
   u16 mk[2][2][16];
 #pragma unroll
@@ -272,8 +331,10 @@ extern "C" hipError_t aca_gemm_big(const AcaGemmDesc* d, hipStream_t stream) {
   P.ksteps_per_split = per;
   const int tiles = ((d->M + GB_BM - 1) / GB_BM) * P.tiles_n;
   const dim3 grid(tiles * splits);
-  // d->tile: variant bits (bit 0 XCD-grouped order, bits 1-2 ring depth - 2)
+  // d->tile: variant bits (bit 0 XCD-grouped order, bits 1-2 ring depth - 2, bit 3 scalar bf16 epilogue)
   P.xcd = (d->tile & 1) && (grid.x % 8 == 0);
+  P.vec_epi = d->out_mode == 1 && d->N % 8 == 0 && d->ldc % 8 == 0 && reinterpret_cast<uintptr_t>(d->C) % 16 == 0 &&
+              (!d->mask || (d->ldm % 8 == 0 && reinterpret_cast<uintptr_t>(d->mask) % 16 == 0)) && !(d->tile & 8);
   const int st = 2 + ((d->tile >> 1) & 3);
 #define GB_LAUNCH(S)                                                                        \
   if (d->a_k && d->b_k) gemm_big_kernel<true, true, S><<<grid, GB_T, 0, stream>>>(P);       \

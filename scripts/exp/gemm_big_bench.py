@@ -58,31 +58,37 @@ def main():
         print(f"{name}: general gemm {t_gen:.1f} us ({flop / t_gen / 1e6:.0f} TF/s)  torch {t_ref:.1f} us "
               f"({flop / t_ref / 1e6:.0f} TF/s)", flush=True)
         best = None
-        for s in (1, 2, 4):
-            for v in (0, 1, 2, 3, 4, 5):
+        for s in (1, 2):
+            for v in (0, 1, 5, 9):
                 try:
                     t = timeit(lambda: big(v, s))
                 except RuntimeError as e:
                     print(f"  v{v} s{s}: {e}")
                     continue
-                print(f"  gemm_big v{v} (xcd {v & 1}, ring {2 + (v >> 1)}) splits {s}: {t:.1f} us "
+                print(f"  gemm_big v{v} (xcd {v & 1}, ring {2 + ((v >> 1) & 3)}, scalar-epi {v >> 3}) splits {s}: {t:.1f} us "
                       f"({flop / t / 1e6:.0f} TF/s)", flush=True)
                 if best is None or t < best[0]:
                     best = (t, v, s)
         t, v, s = best
         grid = -(-M // 128) * -(-N // 128) * s
-        st = torch.zeros(grid, 4, dtype=torch.int64, device=dev)
+        st = torch.zeros(grid, 8, dtype=torch.int64, device=dev)
         big(v, s)
         big(v, s, st)
         torch.cuda.synchronize()
-        x = st.cpu().double() * 10e-3   # 100 MHz realtime counter -> us
+        raw = st.cpu()
+        x = raw[:, :4].double() * 10e-3   # 100 MHz realtime counter -> us
         t0 = x[:, 0].min()
-        loop = (x[:, 1] - x[:, 0]).mean().item()
-        red = (x[:, 2] - x[:, 1]).mean().item()
-        epi = (x[:, 3] - x[:, 2]).mean().item()
+        loop = x[:, 1] - x[:, 0]
+        q = torch.quantile(loop, torch.tensor([0.0, 0.5, 0.9, 1.0], dtype=torch.float64)).tolist()
+        fin = x[:, 3] > 0   # split-K: only the last arriver reaches the epilogue
+        epi = (x[fin, 3] - x[fin, 1]).mean().item()
+        hw, xcc = raw[:, 4], raw[:, 5]
+        cu = (xcc & 0xF) * 256 + ((hw >> 13) & 7) * 32 + ((hw >> 12) & 1) * 16 + ((hw >> 8) & 0xF)
+        _, counts = torch.unique(cu, return_counts=True)
         print(f"  best v{v} s{s} {t:.1f} us; stamps (grid {grid}): start spread {(x[:, 0].max() - t0).item():.1f} us, "
-              f"loop {loop:.1f}, split-reduce {red:.1f}, epilogue {epi:.1f}, span {(x[:, 3].max() - t0).item():.1f} us",
-              flush=True)
+              f"loop min/med/p90/max {q[0]:.1f}/{q[1]:.1f}/{q[2]:.1f}/{q[3]:.1f}, reduce+epilogue {epi:.1f}, "
+              f"span {(x[fin, 3].max() - t0).item():.1f} us; {len(counts)} distinct CUs, max {int(counts.max())} "
+              f"workgroups on one CU, starts after t0+5us: {int(((x[:, 0] - t0) > 5).sum())}", flush=True)
 
 
 if __name__ == "__main__":

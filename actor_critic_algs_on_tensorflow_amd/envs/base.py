@@ -214,8 +214,9 @@ class VecEnv:
             if self.final_obs is None:
                 self.final_obs = torch.empty_like(out)
             self._stack_push(self._frame(), prev, self.final_obs)
-        # auto-reset
-        self._reset_state(done)
+        # auto-reset (on the host, skipped when no env finished: the counter RNG consumes no state)
+        if done.device.type != "cpu" or bool(done.any()):
+            self._reset_state(done)
         self.t.masked_fill_(done, 0)
         self.ep_ret.masked_fill_(done, 0.0)
         f = self._frame()

@@ -72,19 +72,24 @@ def nstep_returns_ref(rews, vals, dones, gamma, look_ahead):
     r = rews.double()
     v = vals.double()
     d = dones.to(torch.bool)
-    tgt = torch.zeros(T, N, dtype=torch.float64, device=rews.device)
-    for t in range(T):
-        acc = torch.zeros(N, dtype=torch.float64, device=rews.device)
-        alive = torch.ones(N, dtype=torch.bool, device=rews.device)
-        disc = 1.0
-        h_end = min(t + look_ahead, T)
-        for k in range(t, h_end):
-            acc = acc + torch.where(alive, disc * r[k], torch.zeros_like(acc))
-            alive = alive & ~d[k]
-            disc *= gamma
-        # bootstrap with V[h_end] only if no terminal transition inside the window
-        acc = acc + torch.where(alive, (gamma ** (h_end - t)) * v[h_end], torch.zeros_like(acc))
-        tgt[t] = acc
+    L = max(1, min(int(look_ahead), T))
+    # every start t at once, one window offset j per pass (L passes instead of T * L): the same per-t summation
+    # order and the same Python-float discount products as a per-t loop, so the values are bitwise those of it
+    acc = torch.zeros(T, N, dtype=torch.float64, device=rews.device)
+    alive = torch.ones(T, N, dtype=torch.bool, device=rews.device)
+    zero = torch.zeros((), dtype=torch.float64, device=rews.device)
+    disc = 1.0
+    for j in range(L):
+        n = T - j                     # starts t < T - j still have step t + j inside the rollout
+        acc[:n] = acc[:n] + torch.where(alive[:n], disc * r[j:], zero)
+        alive[:n] = alive[:n] & ~d[j:]
+        disc *= gamma
+    # bootstrap with V[h_end], h_end = min(t + L, T), only if no terminal transition inside the window
+    t_idx = torch.arange(T, device=rews.device)
+    h_end = torch.clamp(t_idx + L, max=T)
+    pw = torch.tensor([gamma ** e for e in range(L + 1)], dtype=torch.float64, device=rews.device)
+    boot = pw[h_end - t_idx][:, None] * v[h_end]
+    tgt = acc + torch.where(alive, boot, zero)
     adv = tgt - v[:T]
     return tgt.float(), adv.float()
 

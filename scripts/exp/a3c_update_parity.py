@@ -63,11 +63,11 @@ def flat_oracle_grad(oa, grads):
                       g["log_std"]]).detach()
 
 
-def run(updates=3, num_envs=6, verbose=True):
+def run(updates=3, num_envs=6, verbose=True, seed=5, schedule=True):
     """-> one dict per update: gradient relative error, max parameter difference, KL and lr (ours, oracle)."""
     rows = []
     log = print if verbose else (lambda *x, **k: None)
-    cfg = preset("a3c", algo="a2c", num_envs=num_envs, n_steps=200, seed=5, device="cpu", cuda_graph=False,
+    cfg = preset("a3c", algo="a2c", num_envs=num_envs, n_steps=200, seed=seed, device="cpu", cuda_graph=False,
                  outdir=None, quiet=True, stdout_freq=0, save_every=0)
     tr = ActorCriticTrainer(cfg)
     # the oracle keeps its own Adam moments across updates, started in step with ours
@@ -132,6 +132,13 @@ def run(updates=3, num_envs=6, verbose=True):
         rows.append(dict(grad_rel=rel, param_max=float(d.max()), kl=(float(tr.stats["kl"]), kl),
                          lr=(float(tr.actor_opt.get_lr()), aopt.lr), logp_consistency=float((lp.detach() - LP).abs().max()),
                          target_max=float((ret.reshape(T, N) - tgt).abs().max())))
+        if schedule and tr.reg_sched is not None:   # what step() does after the update (Basic_AC/run_AC.py:268-275)
+            e, k = tr.reg_sched.entropy_coef(tr.iteration), tr.reg_sched.kl_coef(tr.iteration)
+            if e is not None:
+                tr.ent_coef.fill_(e)
+            if k is not None:
+                tr.kl_coef.fill_(k)
+        tr.iteration += 1
         g_ent, beta = float(tr.ent_coef), float(tr.kl_coef)
     return rows
 
@@ -139,9 +146,11 @@ def run(updates=3, num_envs=6, verbose=True):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--updates", type=int, default=3)
+    ap.add_argument("--seed", type=int, default=5)
+    ap.add_argument("--no-schedule", action="store_true")
     a = ap.parse_args()
     torch.set_num_threads(4)
-    run(a.updates)
+    run(a.updates, seed=a.seed, schedule=not a.no_schedule)
 
 
 if __name__ == "__main__":

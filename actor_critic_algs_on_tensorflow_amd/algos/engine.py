@@ -271,6 +271,12 @@ class CNNEngine:
             G.im2col_nhwc(b.y2, b.col3, B, 9, 9, 64, 3, 3, 1)
             G.gemm(b.col3, 576, True, self.sW3, 576, True, b.y3, 64, 1, B * 49, 64, 576, bias=self.b3, relu=True,
                    workspace=ws)
+        if fc_parts and not head and self.big_gemm_ok(B):
+            # learner batch: the two split-K planes of the large-tile product, reduced (+ bias, ReLU) by ppo_head
+            hp = self._big_planes("hfc", 2 * B * 512)
+            G.gemm_big(b.y3, 3136, True, self.sWfc, 512, False, hp, 512, 3, B, 512, 3136, splits=2)
+            self.last_fc = (hp, 2)
+            return shifted if want_shift else b.z
         if fc_parts and not head:
             # partial planes only: the consumer (fused policy/env kernel or fc_value) reduces, adds the bias,
             # applies ReLU and writes b.h
@@ -368,12 +374,21 @@ class CNNEngine:
         return (self.opts.ppo_head and self.dev.type == "cuda" and 3 <= self.A1 <= 8 and self.grouped
                 and self.fused_bwd and self.det_wgrad and B >= 1)
 
+    def _big_planes(self, name, n):
+        buf = self._planes.get(name)
+        if buf is None or buf.numel() < n:
+            buf = torch.zeros(n, dtype=torch.float32, device=self.dev)
+            self._planes[name] = buf
+        return buf
+
     def ppo_head(self, b: _Bufs, actions, logp_old, adv, ret, v_old, ent_coef, kl_coef, vf_coef, ppo_clip, v_clip,
-                 stats, z_out=None):
+                 stats, z_out=None, fc=None):
         """z = h Wh + bh, the clipped-surrogate (or A2C) + value loss, dz, dh and the head's weight / bias gradient
         planes in ONE launch (replaces the head GEMM, the loss launch, the dWh / dh GEMMs and the bias column sums).
         ``b.h`` must hold the fc activations (``forward(head=False)``); :meth:`backward` then starts at the fc layer
-        (``head_done=True``) and its finaliser reduces the head planes."""
+        (``head_done=True``) and its finaliser reduces the head planes. ``fc`` = (partial planes, count) of the fc
+        product (``forward(head=False, fc_parts=True)`` at learner batch sizes): the head reduces them into h itself
+        (``b.h`` is then not written)."""
         B, A1 = b.B, self.A1
         ops = _native.require()
         ph = self._ph.get(B)
@@ -386,7 +401,8 @@ class CNNEngine:
             self._ph[B] = ph
         ops.ppo_head(b.h, self.sWh, self.bh, actions, logp_old, adv, ret, v_old if v_clip else None, ent_coef,
                      kl_coef, float(vf_coef), float(ppo_clip or 0.0), float(v_clip or 0.0), b.dh, z_out, ph["Wh"],
-                     ph["bh"], ph["bfc"], ph["st"], ph["ticket"], stats)
+                     ph["bh"], ph["bfc"], ph["st"], ph["ticket"], stats, fc[0] if fc else None, fc[1] if fc else 0,
+                     self.bfc if fc else None)
         for name in ("Wh", "bh", "bfc"):
             self._planes["ph_" + name] = ph[name]
         self._head_planes = {"ph_Wh": ph["P"], "ph_bh": ph["P"], "ph_bfc": ph["P"]}
@@ -493,11 +509,18 @@ class CNNEngine:
         microseconds of inter-queue synchronisation; here the critical path is the chain of launches itself."""
         B = b.B
         if stage in ("all", "tail") and self.big_gemm_ok(B):
-            # dy3 = (dh Wfc^T) * (y3 > 0) [B, 3136] (K 512: no split), dWfc = y3^T dh [3136, 512] (K = B: 2 splits)
+            # dy3 = (dh Wfc^T) * (y3 > 0) [B, 3136] (K 512: no split), dWfc = y3^T dh [3136, 512] (K = B: 2 splits;
+            # whole backward: as two partial planes the finaliser reduces, else stored through the split-K slabs so
+            # the fc/head bucket is final at the end of the "tail" stage)
             G.gemm_big(b.dh, 512, True, self.sWfc, 512, True, b.dy3, 3136, 1, B, 3136, 512, mask=b.y3, ldm=3136,
                        workspace=self.big_ws)
-            G.gemm_big(b.y3, 3136, False, b.dh, 512, False, self.gWfc, 512, 0, 3136, 512, B, splits=2,
-                       workspace=self.big_ws)
+            if stage == "all" and self.det_wgrad:
+                buf = self._big_planes("Wfc", 2 * 3136 * 512)
+                G.gemm_big(b.y3, 3136, False, b.dh, 512, False, buf, 512, 3, 3136, 512, B, splits=2)
+                self._cur_planes["Wfc"] = 2
+            else:
+                G.gemm_big(b.y3, 3136, False, b.dh, 512, False, self.gWfc, 512, 0, 3136, 512, B, splits=2,
+                           workspace=self.big_ws)
             if stage == "tail":
                 return
         elif stage in ("all", "tail"):
@@ -580,7 +603,7 @@ class CNNEngine:
                           self.gb1.data_ptr(): (bp + 128 * 4, 160, b.B)}
             for name, S in planes:
                 g = {"W1": self.gW1, "W2": self.gW2, "W3": self.gW3, "Wh": self.gWh, "ph_Wh": self.gWh,
-                     "ph_bh": self.gbh, "ph_bfc": self.gbfc}[name]
+                     "ph_bh": self.gbh, "ph_bfc": self.gbfc, "Wfc": self.gWfc}[name]
                 src_of[g.data_ptr()] = (self._planes[name].data_ptr(), g.numel(), S)
             for p, off in zip(flat.params, flat.offsets):
                 g = flat.grad[off:off + p.numel()]

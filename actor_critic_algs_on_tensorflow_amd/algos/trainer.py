@@ -738,9 +738,11 @@ class ActorCriticTrainer:
         if (forward and self.dp is None and self._grad_sink is None and self._bw_stage == "all"
                 and actions.dtype == torch.int32 and eng.ppo_head_ok(b.B)):
             # ONE head launch (z, loss, dz, dh, head gradient planes); the backward starts at the fc layer
-            eng.forward(obs, b, head=False, obs_idx=obs_idx)
+            planes = eng.big_gemm_ok(b.B)   # the fc product's split-K planes go straight to the head launch
+            eng.forward(obs, b, head=False, obs_idx=obs_idx, fc_parts=planes)
             eng.ppo_head(b, actions, logp_old, adv, ret, v_old, self.ent_coef, self.kl_coef, vf,
-                         cfg.ppo_clip if ppo else 0.0, (cfg.ppo_value_clip or 0.0) if ppo else 0.0, self.stats_buf)
+                         cfg.ppo_clip if ppo else 0.0, (cfg.ppo_value_clip or 0.0) if ppo else 0.0, self.stats_buf,
+                         fc=eng.last_fc if planes else None)
             self._bw_pending = (b, True)
             eng.backward(b, head_bias_done=True, stage="all", head_done=True)
             self._apply_grads()

@@ -326,8 +326,9 @@ class GemmBigWorkspace:
 def gemm_big(A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, alpha=1.0, bias=None, relu=False, mask=None,
              ldm=0, splits=1, workspace=None, variant=GEMM_BIG_VARIANT, stamps=None):
     """Large plain bf16 product on the 128 x 128 / 32x32x16-MFMA kernel with LDS-DMA staging (``gemm_big.hip``):
-    out_mode 0 fp32 / 1 bf16 store, bias / relu / mask epilogue, slab split-K (deterministic). K % 64 == 0."""
-    ws = workspace.fit(M, N, splits) if splits > 1 else None
+    out_mode 0 fp32 / 1 bf16 store, bias / relu / mask epilogue, slab split-K (deterministic); out_mode 3: the
+    ``splits`` fp32 partial planes ``C[z, M, ldc]`` for a consumer that reduces them (no epilogue). K % 64 == 0."""
+    ws = workspace.fit(M, N, splits) if splits > 1 and out_mode != 3 else None
     _native.require().gemm_big(A, lda, a_k, B, ldb, b_k, C, ldc, out_mode, M, N, K, float(alpha), bias, bool(relu),
                                mask, ldm, splits, ws.ws if ws else None, ws.tickets if ws else None, stamps,
                                int(variant))

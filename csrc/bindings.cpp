@@ -797,7 +797,8 @@ const T* copt(const c10::optional<Tensor>& t, at::ScalarType dt, const char* nam
 void ppo_head(Tensor h, Tensor Wh, Tensor bh, Tensor act, Tensor logp_old, Tensor adv, Tensor ret,
               c10::optional<Tensor> v_old, Tensor ent_coef, Tensor kl_coef, double vf_coef, double ppo_clip,
               double v_clip, Tensor dh, c10::optional<Tensor> z_out, Tensor pWh, Tensor pbh, Tensor pbfc,
-              Tensor pstats, Tensor ticket, Tensor stats) {
+              Tensor pstats, Tensor ticket, Tensor stats, c10::optional<Tensor> hp, int64_t hp_planes,
+              c10::optional<Tensor> hbias) {
   need(h, at::kBFloat16, "h");
   need(Wh, at::kBFloat16, "Wh");
   need(dh, at::kBFloat16, "dh");
@@ -841,6 +842,17 @@ void ppo_head(Tensor h, Tensor Wh, Tensor bh, Tensor act, Tensor logp_old, Tenso
   a.ticket = reinterpret_cast<unsigned int*>(ptr<int32_t>(ticket));
   a.stats = ptr<float>(stats);
   a.B = (int)B;
+  if (hp.has_value() && hp->defined()) {
+    need(*hp, at::kFloat, "hp");
+    TORCH_CHECK(hp_planes >= 1 && hp_planes <= 4 && hp->numel() >= hp_planes * B * 512,
+                "ppo_head: hp must hold hp_planes (1..4) planes of [B, 512]");
+    TORCH_CHECK(hbias.has_value() && hbias->defined() && hbias->scalar_type() == at::kFloat && hbias->numel() >= 512,
+                "ppo_head: hp needs the fp32 fc bias");
+    a.hp = ptr<float>(*hp);
+    a.hbias = ptr<float>(*hbias);
+    a.hp_stride = B * 512;
+    a.hp_planes = (int)hp_planes;
+  }
   check(aca_ppo_head(&a, (int)A1, cur_stream(h)), "ppo_head");
 }
 
@@ -1142,13 +1154,19 @@ void gemm_big(Tensor A, int64_t lda, bool a_k, Tensor B, int64_t ldb, bool b_k, 
               int64_t out_mode, int64_t M, int64_t N, int64_t K, double alpha, c10::optional<Tensor> bias, bool relu,
               c10::optional<Tensor> mask, int64_t ldm, int64_t splits, c10::optional<Tensor> ws,
               c10::optional<Tensor> tickets, c10::optional<Tensor> stamps, int64_t variant) {
-  TORCH_CHECK(out_mode == 0 || out_mode == 1, "gemm_big: out_mode 0 / 1");
+  TORCH_CHECK(out_mode == 0 || out_mode == 1 || out_mode == 3, "gemm_big: out_mode 0 / 1 / 3 (partial planes)");
   TORCH_CHECK(variant >= 0 && variant < 16, "gemm_big: variant 0..15");
   TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16, "gemm_big: bf16 operands");
   TORCH_CHECK(C.scalar_type() == (out_mode == 1 ? at::kBFloat16 : at::kFloat), "gemm_big: C dtype mismatch");
   check_extent(A, a_k ? M : K, a_k ? K : M, lda, "A");
   check_extent(B, b_k ? N : K, b_k ? K : N, ldb, "B");
   check_extent(C, M, N, ldc, "C");
+  if (out_mode == 3) {
+    TORCH_CHECK(C.is_contiguous() && C.numel() >= std::max<int64_t>(splits, 1) * M * ldc,
+                "gemm_big: out_mode 3 needs splits planes of [M, ldc]");
+    TORCH_CHECK(!(bias.has_value() && bias->defined()) && !relu && !(mask.has_value() && mask->defined()) &&
+                    alpha == 1.0, "gemm_big: partial planes take no epilogue");
+  }
   AcaGemmDesc d{};
   d.A = A.data_ptr();
   d.B = B.data_ptr();
@@ -1162,7 +1180,7 @@ void gemm_big(Tensor A, int64_t lda, bool a_k, Tensor B, int64_t ldb, bool b_k, 
     check_extent(*mask, M, N, ldm, "mask");
     d.mask = mask->data_ptr();
   }
-  if (splits > 1) {
+  if (splits > 1 && out_mode != 3) {
     TORCH_CHECK(ws.has_value() && ws->defined() && tickets.has_value() && tickets->defined(),
                 "gemm_big: split-K needs ws and tickets");
     TORCH_CHECK(ws->scalar_type() == at::kFloat && ws->numel() >= aca_gemm_big_ws((int)M, (int)N, (int)splits),
@@ -1741,7 +1759,8 @@ TORCH_LIBRARY(acamd, m) {
   m.def("grad_finalize(Tensor jobs, Tensor partial) -> ()");
   m.def("ppo_head(Tensor h, Tensor Wh, Tensor bh, Tensor act, Tensor logp_old, Tensor adv, Tensor ret, Tensor? v_old, "
         "Tensor ent_coef, Tensor kl_coef, float vf_coef, float ppo_clip, float v_clip, Tensor dh, Tensor? z_out, "
-        "Tensor pWh, Tensor pbh, Tensor pbfc, Tensor pstats, Tensor ticket, Tensor stats) -> ()");
+        "Tensor pWh, Tensor pbh, Tensor pbfc, Tensor pstats, Tensor ticket, Tensor stats, Tensor? hp=None, "
+        "int hp_planes=0, Tensor? hbias=None) -> ()");
   m.def("ppo_head_planes(int B) -> int", &ppo_head_planes);
   m.def("head_bwd(Tensor z, Tensor act, Tensor logp_old, Tensor ent_coef, Tensor kl_coef, float vf_coef, Tensor rew, "
         "Tensor val, Tensor dones, int L, int returns_mode, bool norm_adv, float gamma, float lam, Tensor ret_w, "

@@ -20,7 +20,8 @@
 //     k-rows of a ds_read_b64_tr_b16 group in four different 64-byte bank quarters;
 //   * split-K over the grid: each split writes its fp32 partial tile to a slab, the last-arriving split (agent-scope
 //     release / acquire ticket) sums the slabs in split order and runs the epilogue (deterministic).
-// Epilogue: *alpha, +bias[n], relu, *(mask[m][n] > 0), store fp32 | bf16.
+// Epilogue: *alpha, +bias[n], relu, *(mask[m][n] > 0), store fp32 | bf16; or out_mode 3: each split stores its fp32
+// partial tile into its own plane and the consumer reduces (no in-launch reduction).
 // Requirements (host-checked): plain bf16 operands, 16-byte aligned, lda / ldb % 8 == 0, K % 64 == 0 (splits take
 // ceil(K / 64 / splits) k-steps each, the last one the rest), the m/n-contiguous extents % 8 == 0.
 #include "common.h"
@@ -175,6 +176,29 @@ __global__ void __launch_bounds__(GB_T) gemm_big_kernel(GbParams P) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
   }
   if (st && tid == 0) st[1] = __builtin_amdgcn_s_memrealtime();
+  // ---------------------------------------------------------------- partial planes (out_mode 3): no reduction here
+  if (d.out_mode == 3) {
+    // split z stores its fp32 tile into plane z of C ([splits][M][ldc]); the consumer sums the planes in order
+    // (the gradient finaliser, or the PPO head for the fc activations): no slab round trip, no agent-scope
+    // release / acquire (an L2 write-back + invalidate per arrival on a multi-XCD part)
+    float* Cz = reinterpret_cast<float*>(d.C) + (size_t)z * d.M * d.ldc;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wn + 32 * j + (lane & 31);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          if (m < d.M && n < d.N) Cz[(int64_t)m * d.ldc + n] = acc[i][j][r];
+        }
+    }
+    if (st) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (tid == 0) st[3] = __builtin_amdgcn_s_memrealtime();
+    }
+    return;
+  }
   // ---------------------------------------------------------------- split-K: slabs + last arriver, in split order
   if (P.splits > 1) {
     float* slab = d.ws + ((size_t)tile * P.splits + z) * (GB_BM * GB_BN);
@@ -314,7 +338,8 @@ extern "C" int64_t aca_gemm_big_ws(int M, int N, int splits) {
 extern "C" hipError_t aca_gemm_big(const AcaGemmDesc* d, hipStream_t stream) {
   if (d->M <= 0 || d->N <= 0) return hipSuccess;
   if (d->ga.mode || d->gb.mode || d->colsum || d->colsum_part) return hipErrorInvalidValue;
-  if (d->out_mode != 0 && d->out_mode != 1) return hipErrorInvalidValue;
+  if (d->out_mode != 0 && d->out_mode != 1 && d->out_mode != 3) return hipErrorInvalidValue;
+  if (d->out_mode == 3 && (d->bias || d->relu || d->mask || d->alpha != 1.0f)) return hipErrorInvalidValue;
   const int splits = d->splits < 1 ? 1 : d->splits;
   const int ksteps = d->K / GB_BK;
   const int per = (ksteps + splits - 1) / splits;   // the last split may be shorter; every split gets >= 1 k-step
@@ -323,7 +348,7 @@ extern "C" hipError_t aca_gemm_big(const AcaGemmDesc* d, hipStream_t stream) {
       (reinterpret_cast<uintptr_t>(d->B) % 16))
     return hipErrorInvalidValue;
   if ((!d->a_k && d->M % 8) || (!d->b_k && d->N % 8)) return hipErrorInvalidValue;
-  if (splits > 1 && (!d->ws || !d->tickets)) return hipErrorInvalidValue;
+  if (splits > 1 && d->out_mode != 3 && (!d->ws || !d->tickets)) return hipErrorInvalidValue;
   GbParams P;
   P.d = *d;
   P.tiles_n = (d->N + GB_BN - 1) / GB_BN;

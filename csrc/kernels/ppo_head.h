@@ -11,7 +11,11 @@ constexpr int PH_H = 512;
 constexpr int PH_NSTAT = 6;   // pg, kl, entropy, value loss, clip count, ratio
 
 struct PpoHeadArgs {
-  const uint16_t* h;            // [B, 512] bf16
+  const uint16_t* h;            // [B, 512] bf16 (unless hp)
+  const float* hp;              // optional: fc split-K partial planes [hp_planes][B, 512] fp32; h = bf16(relu(sum + hbias))
+  const float* hbias;           // [512] fc bias (with hp)
+  int64_t hp_stride;            // floats between planes
+  int hp_planes;                // 1..4
   const uint16_t* Wh;           // [512, A1] bf16 (k-major, TF [in, out] layout)
   const float* bh;         // [A1]
   const int32_t* act;      // [B]

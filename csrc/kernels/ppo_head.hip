@@ -52,11 +52,47 @@ __global__ void __launch_bounds__(PH_THREADS) ppo_head_kernel(PpoHeadArgs p) {
   uint4 hraw[PH_ROWS_PER_WAVE];
   int32_t ab[PH_ROWS_PER_WAVE];
   float lpo[PH_ROWS_PER_WAVE], adv[PH_ROWS_PER_WAVE], R[PH_ROWS_PER_WAVE], vo[PH_ROWS_PER_WAVE];
+  if (p.hp) {
+    // h from the fc product's split-K partial planes: sum in plane order, + bias, ReLU, bf16 -- the epilogue the
+    // fc GEMM would have run (bitwise the same h), without its cross-workgroup reduction
+    float hb[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) hb[e] = p.hbias[k0 + e];
+#pragma unroll
+    for (int i = 0; i < PH_ROWS_PER_WAVE; ++i) {
+      const int b = wg * PH_ROWS + wid * PH_ROWS_PER_WAVE + i;
+      const int bc = b < p.B ? b : p.B - 1;
+      float4 q[4][2];
+#pragma unroll
+      for (int z = 0; z < 4; ++z)
+        if (z < p.hp_planes) {
+          const float4* src = reinterpret_cast<const float4*>(p.hp + z * p.hp_stride + (size_t)bc * PH_H + k0);
+          q[z][0] = src[0];
+          q[z][1] = src[1];
+        }
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = 0.f;
+#pragma unroll
+      for (int z = 0; z < 4; ++z)
+        if (z < p.hp_planes) {
+          v[0] += q[z][0].x; v[1] += q[z][0].y; v[2] += q[z][0].z; v[3] += q[z][0].w;
+          v[4] += q[z][1].x; v[5] += q[z][1].y; v[6] += q[z][1].z; v[7] += q[z][1].w;
+        }
+      u16 hb16[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) hb16[e] = f2bf(fmaxf(v[e] * 1.0f + hb[e], 0.f));
+      hraw[i].x = hb16[0] | ((uint32_t)hb16[1] << 16);
+      hraw[i].y = hb16[2] | ((uint32_t)hb16[3] << 16);
+      hraw[i].z = hb16[4] | ((uint32_t)hb16[5] << 16);
+      hraw[i].w = hb16[6] | ((uint32_t)hb16[7] << 16);
+    }
+  }
 #pragma unroll
   for (int i = 0; i < PH_ROWS_PER_WAVE; ++i) {
     const int b = wg * PH_ROWS + wid * PH_ROWS_PER_WAVE + i;
     const int bc = b < p.B ? b : p.B - 1;   // clamped: unconditional loads, contributions masked below
-    hraw[i] = *reinterpret_cast<const uint4*>(p.h + (size_t)bc * PH_H + k0);
+    if (!p.hp) hraw[i] = *reinterpret_cast<const uint4*>(p.h + (size_t)bc * PH_H + k0);
     ab[i] = p.act[bc];
     lpo[i] = p.logp_old[bc];
     adv[i] = p.adv[bc];
@@ -236,7 +272,11 @@ extern "C" int aca_ppo_head_planes(int B) { return (B + aca::PH_ROWS - 1) / aca:
 
 extern "C" hipError_t aca_ppo_head(const aca::PpoHeadArgs* a, int A1, hipStream_t stream) {
   if (a->B <= 0) return hipSuccess;
-  if (reinterpret_cast<uintptr_t>(a->h) % 16 || reinterpret_cast<uintptr_t>(a->dh) % 16) return hipErrorInvalidValue;
+  if ((!a->hp && reinterpret_cast<uintptr_t>(a->h) % 16) || reinterpret_cast<uintptr_t>(a->dh) % 16)
+    return hipErrorInvalidValue;
+  if (a->hp && (reinterpret_cast<uintptr_t>(a->hp) % 16 || a->hp_stride % 4 || a->hp_planes < 1 || a->hp_planes > 4 ||
+                !a->hbias))
+    return hipErrorInvalidValue;
   const int grid = aca_ppo_head_planes(a->B);
   switch (A1) {
 #define ACA_PH(N) \

@@ -184,3 +184,66 @@ def test_gemm_big_matches_fp32_reference(cuda, a_k, b_k, M, N, K, out_mode, epi,
     assert torch.isfinite(got).all()
     err = ((got - ref).norm() / ref.norm()).item()
     assert err < (1e-2 if out_mode == 1 else 1e-5), err
+
+
+@pytest.mark.parametrize("a_k,b_k,M,N,K", [(True, False, 4096, 512, 3136), (False, False, 3136, 512, 4096),
+                                           (False, True, 200, 136, 256)])
+def test_gemm_big_partial_planes_sum_to_the_slab_reduction(cuda, a_k, b_k, M, N, K):
+    """out_mode 3: each split stores its fp32 tile into its own plane (no slab, no ticket); summing the planes in
+    split order reproduces the last-arriver slab reduction bit for bit."""
+    from actor_critic_algs_on_tensorflow_amd import _native
+    ops = _native.require()
+    g = torch.Generator(device="cpu").manual_seed(M + K)
+    lda, ldb = (K if a_k else M), (K if b_k else N)
+    A = (torch.randn((M if a_k else K) * lda, generator=g) * 0.5).to(torch.bfloat16).to(cuda)
+    B = (torch.randn((N if b_k else K) * ldb, generator=g) * 0.5).to(torch.bfloat16).to(cuda)
+    ws = torch.zeros(int(ops.gemm_big_ws(M, N, 2)), device=cuda)
+    tickets = torch.zeros(((M + 127) // 128) * ((N + 127) // 128), dtype=torch.int32, device=cuda)
+    C = torch.full((M * N,), float("nan"), device=cuda)
+    ops.gemm_big(A, lda, a_k, B, ldb, b_k, C, N, 0, M, N, K, 1.0, None, False, None, 0, 2, ws, tickets)
+    P = torch.full((2 * M * N,), float("nan"), device=cuda)
+    ops.gemm_big(A, lda, a_k, B, ldb, b_k, P, N, 3, M, N, K, 1.0, None, False, None, 0, 2, None, None)
+    torch.cuda.synchronize()
+    p = P.view(2, M * N)
+    assert torch.isfinite(p).all()
+    assert torch.equal(p[0] + p[1], C)
+
+
+def test_ppo_head_from_fc_planes_equals_stored_h(cuda):
+    """The learner head fed the fc product's two split-K planes (sum + bias + ReLU + bf16 inside the head launch)
+    == the head fed h stored by the fc product's own epilogue: every output bitwise."""
+    from actor_critic_algs_on_tensorflow_amd import _native
+    ops = _native.require()
+    B, A1 = 4096, 5
+    g = torch.Generator(device="cpu").manual_seed(11)
+    y3 = torch.relu(torch.randn(B * 3136, generator=g)).to(torch.bfloat16).to(cuda)
+    Wfc = (0.02 * torch.randn(3136 * 512, generator=g)).to(torch.bfloat16).to(cuda)
+    bfc = (0.1 * torch.randn(512, generator=g)).to(cuda)
+    Wh = (0.05 * torch.randn(512, A1, generator=g)).to(torch.bfloat16).to(cuda)
+    bh = (0.1 * torch.randn(A1, generator=g)).to(cuda)
+    act = torch.randint(0, A1 - 1, (B,), dtype=torch.int32, generator=g).to(cuda)
+    lpo = (-torch.rand(B, generator=g) * 2).to(cuda)
+    adv, ret = torch.randn(B, generator=g).to(cuda), torch.randn(B, generator=g).to(cuda)
+    ent, kl = torch.tensor([0.01], device=cuda), torch.tensor([0.3], device=cuda)
+    h = torch.empty(B, 512, dtype=torch.bfloat16, device=cuda)
+    ws = torch.zeros(int(ops.gemm_big_ws(B, 512, 2)), device=cuda)
+    tickets = torch.zeros((B // 128) * 4, dtype=torch.int32, device=cuda)
+    ops.gemm_big(y3, 3136, True, Wfc, 512, False, h, 512, 1, B, 512, 3136, 1.0, bfc, True, None, 0, 2, ws, tickets)
+    hp = torch.empty(2 * B * 512, device=cuda)
+    ops.gemm_big(y3, 3136, True, Wfc, 512, False, hp, 512, 3, B, 512, 3136, 1.0, None, False, None, 0, 2, None, None)
+    P = int(ops.ppo_head_planes(B))
+    outs = []
+    for planes in (False, True):
+        o = dict(dh=torch.empty(B, 512, dtype=torch.bfloat16, device=cuda), z=torch.empty(B, A1, device=cuda),
+                 pWh=torch.empty(P * 512 * A1, device=cuda), pbh=torch.empty(P * A1, device=cuda),
+                 pbfc=torch.empty(P * 512, device=cuda), st=torch.zeros(P * 6, dtype=torch.float64, device=cuda),
+                 stats=torch.zeros(8, device=cuda))
+        ticket = torch.zeros(1, dtype=torch.int32, device=cuda)
+        hin = torch.full_like(h, float("nan")) if planes else h   # the planes path must not read h
+        ops.ppo_head(hin, Wh, bh, act, lpo, adv, ret, None, ent, kl, 0.5, 0.1, 0.0, o["dh"], o["z"], o["pWh"],
+                     o["pbh"], o["pbfc"], o["st"], ticket, o["stats"], hp if planes else None, 2 if planes else 0,
+                     bfc if planes else None)
+        torch.cuda.synchronize()
+        outs.append(o)
+    for k in outs[0]:
+        assert torch.equal(outs[0][k], outs[1][k]), k

@@ -1298,7 +1298,12 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_kernel(
 __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
     const u16* __restrict__ dy3g, const u16* __restrict__ W3, const u16* __restrict__ y2g,
     const u16* __restrict__ W2, const u16* __restrict__ y1g, u16* __restrict__ dy2g, u16* __restrict__ dy1g,
-    float* __restrict__ biasp, int B) {
+    float* __restrict__ biasp, int B, uint64_t* __restrict__ stamps) {
+  // diagnostics: phase stamps of the first two samples of every workgroup ([blockIdx][16]: 8 per sample)
+  auto pst = [&](int it, int k) {
+    if (stamps && it < 2 && threadIdx.x == 0)
+      stamps[(size_t)blockIdx.x * 16 + it * 8 + k] = __builtin_amdgcn_s_memrealtime();
+  };
   // staging area for the weight fragments (aliases the images: used before the sample loop only)
   constexpr int STAGE = BW_P3E + BW_M2E + BW_P2E;   // 8712 + 5184 + 8712 u16 = 45 KB
   __shared__ __attribute__((aligned(16))) u16 s_w3[576 * BW_LD3];   // 81 KB
@@ -1369,7 +1374,8 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
     m13 = *reinterpret_cast<const uint4*>(y1g + (size_t)b * 400 * 32 + min(tid + 3 * BW_T, M1_CH - 1) * 8);
   };
   if ((int)blockIdx.x < B) fetch(blockIdx.x);
-  for (int b = blockIdx.x; b < B; b += gridDim.x) {
+  for (int b = blockIdx.x, it = 0; b < B; b += gridDim.x, ++it) {
+    pst(it, 0);
     // opaque zero (per iteration): keeps the LDS address arithmetic of the unrolled MFMA loops inside the sample
     // loop -- hoisted out of it, the loop-invariant addresses alone took more registers than the kernel has
     int z0;
@@ -1393,6 +1399,7 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
     }
     const uint4 vm1[4] = {m10, m11, m12, m13};
     __syncthreads();
+    pst(it, 1);
     if (b + (int)gridDim.x < B) fetch(b + gridDim.x);
 
     // ---- dy2: wave -> (N tile wid % 4, M tiles 3 x half)
@@ -1435,6 +1442,7 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
       for (int e = 0; e < 8; ++e) part3[e] += bf_lane(v, e);
     }
     __syncthreads();   // dy2 image complete; the dy3 image and the y2 mask are dead
+    pst(it, 2);
 
     // ---- dy2 out (16-byte rows) + db2 / db3 channel sums
     float part2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -1476,6 +1484,7 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
           acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, w2f[ks], acc[i], 0, 0, 0);
         }
       }
+      pst(it, 3);
       __syncthreads();   // every wave is past its dy2-image reads of the db sums; s_red rows complete
       if (tid < 128) {
         float v = 0.f;
@@ -1496,6 +1505,7 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
         }
     }
     __syncthreads();
+    pst(it, 4);
     // ---- dy1 out: y1 mask applied, 16-byte stores, db1 partials
     float part1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -1526,6 +1536,7 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
       for (int w = 0; w < 8; ++w) v += s_red[1024 + w * 32 + tid];
       biasp[(size_t)b * 160 + 128 + tid] = v;
     }
+    pst(it, 5);
   }
 }
 
@@ -1604,9 +1615,9 @@ extern "C" hipError_t aca_cnn_trunk_bwd(const uint16_t* dy3, const uint16_t* W3,
   for (const void* p : {(const void*)dy3, (const void*)W3, (const void*)y2, (const void*)W2, (const void*)y1,
                         (const void*)dy2, (const void*)dy1})
     if (reinterpret_cast<uintptr_t>(p) % 16) return hipErrorInvalidValue;
-  if (persist > 0 && !stamps)
+  if (persist > 0)
     aca::cnn_trunk_bwd_persist_kernel<<<persist < B ? persist : B, aca::BW_T, 0, stream>>>(dy3, W3, y2, W2, y1, dy2,
-                                                                                             dy1, biasp, B);
+                                                                                             dy1, biasp, B, stamps);
   else
     aca::cnn_trunk_bwd_kernel<<<B, aca::BW_T, 0, stream>>>(dy3, W3, y2, W2, y1, dy2, dy1, biasp, stamps);
   return hipGetLastError();

@@ -5,4 +5,5 @@ timeout -k 10 300 python -u scripts/bench_configs.py --configs breakout_ppo --up
 timeout -k 10 300 python -u scripts/bench_configs.py --configs breakout_ppo --updates 5 --warmup 2 --engine-opts '{"trunk_rows_max_b": 128}' && \
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/tr -o run -- python3 scripts/bench_configs.py --configs breakout_ppo --updates 2 --warmup 1 > $O/tr.log 2>&1 && \
 python3 scripts/trace_summary.py $(find $O/tr -name "*kernel_trace.csv") --updates 1 --marker pong_fused_env_step --per-update 128 > $O/breakout_trace_summary.txt && head -30 $O/breakout_trace_summary.txt && \
-find $O/tr -name "*.csv" -size +6M -delete
+find $O/tr -name "*.csv" -size +6M -delete &&
+timeout -k 10 120 python -u scripts/exp/trunk_bwd_phases.py

@@ -265,26 +265,27 @@ SUMSQ_PARTS = 256   # optim.hip: partial slots of the global-norm reduction = ma
 
 def finalize_jobs(segments, device, return_max=False):
     """Job table of the gradient finaliser (``grad_finalize``): ``segments`` = [(dst_ptr, src_ptr, n, stride, S)]
-    (``src_ptr`` 0: final already, read for the norm). Plane reductions are cut into 1024-element jobs (one float4
-    per thread, a short chain of plane loads), per-sample bias rows (n <= 64) take one job each, and the read-only
-    segments share the remaining workgroups in equal multiples of 1024 elements; at most ``SUMSQ_PARTS`` jobs."""
-    plane_ch = 1024
+    (``src_ptr`` 0: final already, read for the norm). Plane reductions are cut into jobs of about equal load count
+    (``n * S`` spread over the workgroups: 1024-element jobs for the many-plane conv gradients, long jobs for a
+    two-plane fc gradient of 1.6 M elements, which at 1024 elements per job would not fit the job budget), per-sample
+    bias rows (n <= 64) take one job each, and the read-only segments share the remaining workgroups in equal
+    multiples of 1024 elements; at most ``SUMSQ_PARTS`` jobs."""
+    small = [sg for sg in segments if sg[1] and sg[2] <= 64]
+    big = [sg for sg in segments if sg[1] and sg[2] > 64]
+    ro = [sg for sg in segments if not sg[1]]
+    budget = max(1, SUMSQ_PARTS - len(small) - max(1, len(ro)))
+    target = max(1024.0, sum(n * S for _, _, n, _, S in big) / budget)   # plane loads per job
     while True:
-        jobs = []
-        ro = [sg for sg in segments if not sg[1]]
-        for dst, src, n, stride, S in segments:
-            if not src:
-                continue
-            if n <= 64:
-                jobs.append([dst, src, n, stride, S])
-                continue
-            for a in range(0, n, plane_ch):
-                jobs.append([dst + 4 * a, src + 4 * a, min(plane_ch, n - a), stride, S])
+        jobs = [[dst, src, n, stride, S] for dst, src, n, stride, S in small]
+        for dst, src, n, stride, S in big:
+            ch = max(1024, -(-int(target // max(1, S)) // 1024) * 1024)
+            for a in range(0, n, ch):
+                jobs.append([dst + 4 * a, src + 4 * a, min(ch, n - a), stride, S])
         left = SUMSQ_PARTS - len(jobs)
         total_ro = sum(sg[2] for sg in ro)
-        if left >= max(1, len(ro)) or plane_ch >= 1 << 20:
+        if left >= max(1, len(ro)) or target > 1 << 40:
             break
-        plane_ch *= 2
+        target *= 1.25
     if ro:
         ch = max(1024, -(-total_ro // max(1, left - len(ro))))
         ch = -(-ch // 1024) * 1024

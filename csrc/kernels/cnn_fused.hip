@@ -1010,16 +1010,40 @@ __global__ void __launch_bounds__(256) pong_fused_env_step_kernel(
 // are summed in a fixed order (deterministic); the gradient finaliser reduces them over the batch.
 // Replaces two implicit transposed-conv GEMM launches (dy2: mode 3/4, dy1: sub-pixel mode 5/6) + their colsums.
 // ------------------------------------------------------------------------------------------------------------
-constexpr int BW_LD3 = 72;                  // W3 B-row stride (64 + 8 pad), also the image pixel stride
-constexpr int BW_LD2 = 40;                  // W2 B-row stride (32 + 8)
-constexpr int BW_P3 = 11;                   // dy3 image 7x7 + 2 zero rows/cols on each side
-constexpr int BW_P2 = 11;                   // dy2 image 9x9 + 1 zero row/col on each side
-constexpr int BW_RW = 576 * BW_LD3;         // >= 1024 * BW_LD2
-constexpr int BW_P3E = BW_P3 * BW_P3 * BW_LD3;
+// LDS layouts, conflict-free for every fragment read (tests/test_lds_layouts_cpu.py models them):
+//  * the A operands of the 16x16x32 MFMA are pixel rows of zero-bordered images: lane l reads 16 bytes of output
+//    position m0 + (l & 15) at channel chunk (l >> 4). A ds_read_b128 lane group holds 8 positions at one chunk
+//    and 8 at the next; with a 160-byte pixel stride (10 bank quads) those land in 16 distinct quads whenever the
+//    8 positions of each chunk are distinct mod 8, which holds when the image width == the output width mod 8:
+//    dy3 image 17 wide for the 9-wide dy2 output (17 = 9 + 8), dy2 image 18 wide for the 10-wide sub-pixel
+//    classes of dy1 (18 = 10 + 8). (The previous 144-byte stride over 11-wide images: 2.6-2.7 cycles per read.)
+//  * the B operands are weight rows read by ds_read_b64_tr_b16 (8 rows x 16 columns per 32-lane group): W3 rows of
+//    64 and W2 rows of 32 elements unpadded, each row's 16-byte chunks XOR-swizzled (bw_sw3 / bw_sw2), so the 8
+//    rows of a group cover all 64 banks (unswizzled padded rows: 2 cycles per read instead of 1).
+constexpr int BW_LDW3 = 64;                 // W3 B rows [576][64], chunks ^ bw_sw3(row)
+constexpr int BW_LDW2 = 32;                 // W2 B rows [1024][32], chunks ^ bw_sw2(row)
+constexpr int BW_PS = 80;                   // image pixel stride (64 channels + 16 unused)
+constexpr int BW_P3H = 11, BW_P3W = 17;     // dy3 image: 7x7 at (2, 2), zero border
+constexpr int BW_P2H = 11, BW_P2W = 18;     // dy2 image: 9x9 at (1, 1), zero border
+constexpr int BW_RW = 576 * BW_LDW3;        // >= 1024 * BW_LDW2
+constexpr int BW_P3E = BW_P3H * BW_P3W * BW_PS;
 constexpr int BW_M2E = 81 * 64;
-constexpr int BW_P2E = BW_P2 * BW_P2 * BW_LD3;
+constexpr int BW_P2E = BW_P2H * BW_P2W * BW_PS;
 static_assert(400 * 32 <= BW_P3E + BW_M2E, "dy1 staging aliases the dy3 image + y2 mask");
-static_assert(1024 * BW_LD2 <= BW_RW, "W2 rows fit the W3 region");
+static_assert(1024 * BW_LDW2 <= BW_RW, "W2 rows fit the W3 region");
+static_assert(BW_P3W % 8 == 9 % 8 && BW_P2W % 8 == 10 % 8 && BW_PS == 80, "conflict-free image geometry");
+__device__ __forceinline__ int bw_sw3(int r) { return (((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2); }
+__device__ __forceinline__ int bw_sw2(int r) { return ((r >> 3) & 1) << 1; }
+// zero the border pixels of an H x W image (interior rows / cols [LO, LO + N)), the 8 data chunks of each pixel
+template <int H, int W, int LO, int N, int NT>
+__device__ __forceinline__ void bw_zero_border(u16* img) {
+  const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
+  for (int c = threadIdx.x; c < H * W * 8; c += NT) {
+    const int px = c >> 3, part = c & 7, pa = px / W, pb = px - pa * W;
+    if (pa < LO || pa >= LO + N || pb < LO || pb >= LO + N)
+      *reinterpret_cast<uint4*>(img + px * BW_PS + part * 8) = z4;
+  }
+}
 
 // element e (0..7) of 8 packed bf16 as float, without taking the vector's address (that would go to scratch)
 __device__ __forceinline__ float bf_lane(const uint4& v, int e) {
@@ -1030,6 +1054,22 @@ __device__ __forceinline__ uint32_t mask_pair(uint32_t w, uint32_t m) {   // zer
   const uint32_t lo = (__uint_as_float(m << 16) > 0.f) ? 0x0000FFFFu : 0u;
   const uint32_t hi = (__uint_as_float(m & 0xFFFF0000u) > 0.f) ? 0xFFFF0000u : 0u;
   return w & (lo | hi);
+}
+
+// tr_frag over XOR-swizzled rows (SW 3: bw_sw3, 2: bw_sw2); `rows` at a row index that is a multiple of 16
+template <int SW>
+__device__ __forceinline__ bf16x8 tr_frag_sw(const u16* rows, int ld, int col0, int lane) {
+  const int lr16 = lane & 15, lg = lane >> 4, q = lr16 >> 2, p = lr16 & 3;
+  const int r0 = lg * 8 + q, r1 = r0 + 4, col = col0 + 4 * p;
+  const int s0 = SW == 3 ? bw_sw3(r0) : bw_sw2(r0), s1 = SW == 3 ? bw_sw3(r1) : bw_sw2(r1);
+  const u16* p0 = rows + r0 * ld + ((((col >> 3) ^ s0) << 3) | (col & 7));
+  const u16* p1 = rows + r1 * ld + ((((col >> 3) ^ s1) << 3) | (col & 7));
+  typedef short short4x __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) short4x lds4;
+  const short4x lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(p0));
+  const short4x hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(p1));
+  const short8v v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
 }
 
 __device__ __forceinline__ bf16x8 tr_frag(const u16* rows, int ld, int col0, int lane) {
@@ -1061,28 +1101,17 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_kernel(
   const int b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l16 = lane & 15, lg = lane >> 4;
-  const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
   stamp(stamps, 0);
 
   // ---------------------------------------------------------------- loads: dy3 image, W3 rows, y2 mask; W2 + y1
   // mask prefetched into registers (consumed in the dy1 phase)
   {
-    constexpr int P3_CH = BW_P3 * BW_P3 * 9;                  // 1089 chunks (9 per 144-byte pixel)
-    constexpr int P3_PER = (P3_CH + BW_T - 1) / BW_T;          // 3
     constexpr int W3_CH = 576 * 8, W3_PER = W3_CH / BW_T;      // 9
     constexpr int M2_CH = 81 * 8;                              // 648
     constexpr int M2_PER = (M2_CH + BW_T - 1) / BW_T;          // 2
-    uint4 vp[P3_PER], vw[W3_PER], vm[M2_PER];
-#pragma unroll
-    for (int u = 0; u < P3_PER; ++u) {
-      const int c = tid + u * BW_T;
-      const int px = c / 9, part = c - px * 9, pa = px / BW_P3, pb = px - pa * BW_P3;
-      const bool in = c < P3_CH && part < 8 && pa >= 2 && pa < 9 && pb >= 2 && pb < 9;
-      const int src = in ? ((b * 49 + (pa - 2) * 7 + (pb - 2)) * 64 + part * 8) : b * 49 * 64;
-      const uint4 v = *reinterpret_cast<const uint4*>(dy3g + src);
-      // per component: an aggregate select is lowered through scratch
-      vp[u] = make_uint4(in ? v.x : 0u, in ? v.y : 0u, in ? v.z : 0u, in ? v.w : 0u);
-    }
+    uint4 vw[W3_PER], vm[M2_PER];
+    // dy3: 49 pixels x 8 chunks = 392 <= BW_T, one 16-byte load per thread (the border is zeroed below)
+    const uint4 vp = *reinterpret_cast<const uint4*>(dy3g + (size_t)b * 49 * 64 + min(tid, 391) * 8);
 #pragma unroll
     for (int u = 0; u < W3_PER; ++u) {
       // B row k = (i, j, o) <- W3[o][i][j][:] (64 contiguous channels = 8 chunks)
@@ -1095,27 +1124,23 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_kernel(
       const int c = min(tid + u * BW_T, M2_CH - 1);
       vm[u] = *reinterpret_cast<const uint4*>(y2g + (size_t)b * 81 * 64 + c * 8);
     }
-#pragma unroll
-    for (int u = 0; u < P3_PER; ++u) {
-      const int c = tid + u * BW_T;
-      if (c < P3_CH) *reinterpret_cast<uint4*>(s_p3 + (c / 9) * BW_LD3 + (c % 9) * 8) = vp[u];
+    if (tid < 392) {
+      const int px = tid >> 3, pa = px / 7, pb = px - pa * 7;
+      *reinterpret_cast<uint4*>(s_p3 + ((pa + 2) * BW_P3W + pb + 2) * BW_PS + (tid & 7) * 8) = vp;
     }
+    bw_zero_border<BW_P3H, BW_P3W, 2, 7, BW_T>(s_p3);
 #pragma unroll
     for (int u = 0; u < W3_PER; ++u) {
-      const int c = tid + u * BW_T;
-      *reinterpret_cast<uint4*>(s_w + (c >> 3) * BW_LD3 + (c & 7) * 8) = vw[u];
+      const int c = tid + u * BW_T, k = c >> 3;
+      *reinterpret_cast<uint4*>(s_w + k * BW_LDW3 + (((c & 7) ^ bw_sw3(k)) << 3)) = vw[u];
     }
 #pragma unroll
     for (int u = 0; u < M2_PER; ++u) {
       const int c = tid + u * BW_T;
       if (c < M2_CH) *reinterpret_cast<uint4*>(s_m2 + c * 8) = vm[u];
     }
-    // dy2 image: zero border and pad lanes; the interior is written by the dy2 epilogue
-    for (int c = tid; c < BW_P2 * BW_P2 * 9; c += BW_T) {
-      const int px = c / 9, part = c - px * 9, pa = px / BW_P2, pb = px - pa * BW_P2;
-      if (pa == 0 || pb == 0 || pa == BW_P2 - 1 || pb == BW_P2 - 1 || part == 8)
-        *reinterpret_cast<uint4*>(s_p2 + px * BW_LD3 + part * 8) = z4;
-    }
+    // dy2 image: zero border; the interior is written by the dy2 epilogue
+    bw_zero_border<BW_P2H, BW_P2W, 1, 9, BW_T>(s_p2);
   }
   // held across the dy2 phase in named registers (hipcc left a uint4 array for this in scratch)
   static_assert(64 * 512 / 8 / BW_T == 8, "W2 prefetch is written out for 8 chunks per thread");
@@ -1141,12 +1166,12 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_kernel(
 #pragma unroll
     for (int ks = 0; ks < 18; ++ks) {
       const int kb = ks * 32 + lg * 8, t = kb >> 6, o0 = kb & 63, ti = t / 3, tj = t - ti * 3;
-      const bf16x8 bf = tr_frag(s_w + ks * 32 * BW_LD3, BW_LD3, n0, lane);
+      const bf16x8 bf = tr_frag_sw<3>(s_w + ks * 32 * BW_LDW3, BW_LDW3, n0, lane);
 #pragma unroll
       for (int mt = 0; mt < 3; ++mt) {
         const int m = min((mh + mt) * 16 + l16, 80);
         const int a = m / 9, c = m - a * 9;
-        const bf16x8 af = *reinterpret_cast<const bf16x8*>(s_p3 + ((a - ti + 2) * BW_P3 + (c - tj + 2)) * BW_LD3 + o0);
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(s_p3 + ((a - ti + 2) * BW_P3W + (c - tj + 2)) * BW_PS + o0);
         acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, acc[mt], 0, 0, 0);
       }
     }
@@ -1159,7 +1184,7 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_kernel(
         if (m < 81) {
           const int a = m / 9, c = m - a * 9;
           const float v = bf2f(s_m2[m * 64 + n]) > 0.f ? acc[mt][r] : 0.f;
-          s_p2[((a + 1) * BW_P2 + (c + 1)) * BW_LD3 + n] = f2bf(v);
+          s_p2[((a + 1) * BW_P2W + (c + 1)) * BW_PS + n] = f2bf(v);
         }
       }
   }
@@ -1167,7 +1192,7 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_kernel(
   float part3[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int c = tid; c < 49 * 8; c += BW_T) {
     const int px = c >> 3, g = c & 7, pa = px / 7, pb = px - pa * 7;
-    const uint4 v = *reinterpret_cast<const uint4*>(s_p3 + ((pa + 2) * BW_P3 + (pb + 2)) * BW_LD3 + g * 8);
+    const uint4 v = *reinterpret_cast<const uint4*>(s_p3 + ((pa + 2) * BW_P3W + (pb + 2)) * BW_PS + g * 8);
 #pragma unroll
     for (int e = 0; e < 8; ++e) part3[e] += bf_lane(v, e);
   }
@@ -1179,14 +1204,14 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_kernel(
 #define ACA_W2_ST(u)                                                                                  \
   {                                                                                                   \
     const int c = tid + (u) * BW_T, o = c >> 6, t = (c >> 2) & 15, part = c & 3;                     \
-    *reinterpret_cast<uint4*>(s_w + (t * 64 + o) * BW_LD2 + part * 8) = vw2_##u;                     \
+    *reinterpret_cast<uint4*>(s_w + (t * 64 + o) * BW_LDW2 + ((part ^ bw_sw2(t * 64 + o)) << 3)) = vw2_##u; \
   }
   ACA_W2_ST(0) ACA_W2_ST(1) ACA_W2_ST(2) ACA_W2_ST(3) ACA_W2_ST(4) ACA_W2_ST(5) ACA_W2_ST(6) ACA_W2_ST(7)
 #undef ACA_W2_ST
   float part2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int c = tid; c < 81 * 8; c += BW_T) {
     const int m = c >> 3, g = c & 7, a = m / 9, cc = m - a * 9;
-    const uint4 v = *reinterpret_cast<const uint4*>(s_p2 + ((a + 1) * BW_P2 + (cc + 1)) * BW_LD3 + g * 8);
+    const uint4 v = *reinterpret_cast<const uint4*>(s_p2 + ((a + 1) * BW_P2W + (cc + 1)) * BW_PS + g * 8);
     *reinterpret_cast<uint4*>(dy2g + ((size_t)b * 81 + m) * 64 + g * 8) = v;
 #pragma unroll
     for (int e = 0; e < 8; ++e) part2[e] += bf_lane(v, e);
@@ -1226,12 +1251,12 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_kernel(
     for (int ks = 0; ks < 8; ++ks) {
       const int d = ks >> 1, di = d >> 1, dj = d & 1, ob = (ks & 1) * 32;
       const int tap = (py + 2 * di) * 4 + (px + 2 * dj);
-      const bf16x8 bf = tr_frag(s_w + (tap * 64 + ob) * BW_LD2, BW_LD2, nt * 16, lane);
+      const bf16x8 bf = tr_frag_sw<2>(s_w + (tap * 64 + ob) * BW_LDW2, BW_LDW2, nt * 16, lane);
 #pragma unroll
       for (int i = 0; i < 7; ++i) {
         const int u = min(i * 16 + l16, 99), yy = u / 10, xx = u - yy * 10;
         const bf16x8 af = *reinterpret_cast<const bf16x8*>(
-            s_p2 + ((yy - di + 1) * BW_P2 + (xx - dj + 1)) * BW_LD3 + ob + lg * 8);
+            s_p2 + ((yy - di + 1) * BW_P2W + (xx - dj + 1)) * BW_PS + ob + lg * 8);
         acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, acc[i], 0, 0, 0);
       }
     }
@@ -1305,20 +1330,19 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
       stamps[(size_t)blockIdx.x * 16 + it * 8 + k] = __builtin_amdgcn_s_memrealtime();
   };
   // staging area for the weight fragments (aliases the images: used before the sample loop only)
-  constexpr int STAGE = BW_P3E + BW_M2E + BW_P2E;   // 8712 + 5184 + 8712 u16 = 45 KB
-  __shared__ __attribute__((aligned(16))) u16 s_w3[576 * BW_LD3];   // 81 KB
+  constexpr int STAGE = BW_P3E + BW_M2E + BW_P2E;   // 14960 + 5184 + 15840 u16 = 70 KB
+  __shared__ __attribute__((aligned(16))) u16 s_w3[576 * BW_LDW3];   // 72 KB
   __shared__ __attribute__((aligned(16))) u16 s_img[STAGE];
   __shared__ float s_red[8 * 128 + 8 * 32];
   u16* const s_p2i = s_img + BW_P3E + BW_M2E;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l16 = lane & 15, lg = lane >> 4;
-  const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
-  static_assert(512 * BW_LD2 <= STAGE, "half of the W2 rows fit the staging area");
+  static_assert(512 * BW_LDW2 <= STAGE, "half of the W2 rows fit the staging area");
 
   // ---- W3 B rows k = (t, o) <- W3[o][t][:], resident in LDS for the whole walk
   for (int c = tid; c < 576 * 8; c += BW_T) {
     const int k = c >> 3, part = c & 7, t = k >> 6, o = k & 63;
-    *reinterpret_cast<uint4*>(s_w3 + k * BW_LD3 + part * 8) =
+    *reinterpret_cast<uint4*>(s_w3 + k * BW_LDW3 + ((part ^ bw_sw3(k)) << 3)) =
         *reinterpret_cast<const uint4*>(W3 + o * 576 + t * 64 + part * 8);
   }
   // ---- W2 fragments of this wave's (N tile, parity class): rows (t, o) <- W2[o][t][:], staged 512 rows at a time
@@ -1329,7 +1353,7 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
     for (int half = 0; half < 2; ++half) {
       for (int c = tid; c < 512 * 4; c += BW_T) {
         const int row = half * 512 + (c >> 2), part = c & 3, t = row >> 6, o = row & 63;
-        *reinterpret_cast<uint4*>(s_img + (c >> 2) * BW_LD2 + part * 8) =
+        *reinterpret_cast<uint4*>(s_img + (c >> 2) * BW_LDW2 + ((part ^ bw_sw2(c >> 2)) << 3)) =
             *reinterpret_cast<const uint4*>(W2 + o * 512 + t * 32 + part * 8);
       }
       __syncthreads();
@@ -1337,35 +1361,22 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
       for (int ks = 0; ks < 8; ++ks) {
         const int d = ks >> 1, di = d >> 1, dj = d & 1, ob = (ks & 1) * 32;
         const int tap = (py + 2 * di) * 4 + (px + 2 * dj);
-        if ((tap >> 3) == half) w2f[ks] = tr_frag(s_img + ((tap & 7) * 64 + ob) * BW_LD2, BW_LD2, nt * 16, lane);
+        if ((tap >> 3) == half)
+          w2f[ks] = tr_frag_sw<2>(s_img + ((tap & 7) * 64 + ob) * BW_LDW2, BW_LDW2, nt * 16, lane);
       }
       __syncthreads();
     }
   }
-  // dy2 image border and pad lanes: zero once (the interior is rewritten for every sample, the border never)
-  for (int c = tid; c < BW_P2 * BW_P2 * 9; c += BW_T) {
-    const int px = c / 9, part = c - px * 9, pa = px / BW_P2, pb = px - pa * BW_P2;
-    if (pa == 0 || pb == 0 || pa == BW_P2 - 1 || pb == BW_P2 - 1 || part == 8)
-      *reinterpret_cast<uint4*>(s_p2i + px * BW_LD3 + part * 8) = z4;
-  }
+  // dy2 image border: zero once (the interior is rewritten for every sample, the border never)
+  bw_zero_border<BW_P2H, BW_P2W, 1, 9, BW_T>(s_p2i);
 
-  constexpr int P3_CH = BW_P3 * BW_P3 * 9, P3_PER = (P3_CH + BW_T - 1) / BW_T;   // 1089 -> 3
   constexpr int M2_CH = 81 * 8, M2_PER = (M2_CH + BW_T - 1) / BW_T;              // 648 -> 2
   constexpr int M1_CH = 400 * 4, M1_PER = (M1_CH + BW_T - 1) / BW_T;             // 1600 -> 4
-  static_assert(P3_PER == 3 && M2_PER == 2 && M1_PER == 4, "prefetch registers are written out");
-  uint4 vp0, vp1, vp2, vm0, vm1_, m10, m11, m12, m13;   // next sample
+  static_assert(M2_PER == 2 && M1_PER == 4, "prefetch registers are written out");
+  uint4 vp0, vm0, vm1_, m10, m11, m12, m13;   // next sample
   auto fetch = [&](int b) {
-    uint4 v[3];
-#pragma unroll
-    for (int u = 0; u < 3; ++u) {
-      const int c = tid + u * BW_T;
-      const int px = c / 9, part = c - px * 9, pa = px / BW_P3, pb = px - pa * BW_P3;
-      const bool in = c < P3_CH && part < 8 && pa >= 2 && pa < 9 && pb >= 2 && pb < 9;
-      const int src = in ? ((b * 49 + (pa - 2) * 7 + (pb - 2)) * 64 + part * 8) : b * 49 * 64;
-      const uint4 x = *reinterpret_cast<const uint4*>(dy3g + src);
-      v[u] = make_uint4(in ? x.x : 0u, in ? x.y : 0u, in ? x.z : 0u, in ? x.w : 0u);
-    }
-    vp0 = v[0]; vp1 = v[1]; vp2 = v[2];
+    // dy3: 49 pixels x 8 chunks = 392 <= BW_T: one 16-byte load per thread
+    vp0 = *reinterpret_cast<const uint4*>(dy3g + (size_t)b * 49 * 64 + min(tid, 391) * 8);
     vm0 = *reinterpret_cast<const uint4*>(y2g + (size_t)b * 81 * 64 + min(tid, M2_CH - 1) * 8);
     vm1_ = *reinterpret_cast<const uint4*>(y2g + (size_t)b * 81 * 64 + min(tid + BW_T, M2_CH - 1) * 8);
     m10 = *reinterpret_cast<const uint4*>(y1g + (size_t)b * 400 * 32 + tid * 8);
@@ -1386,14 +1397,14 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
     u16* const s_p2 = s_img + BW_P3E + BW_M2E + z0;
     const u16* const s_w3z = s_w3 + z0;
     const int lane = (threadIdx.x & 63) + z0, l16 = lane & 15, lg = lane >> 4;   // shadow: per-iteration values
-    // ---- this sample's dy3 image + y2 mask to LDS; y1 mask kept in registers; the next sample's loads issued
+    // ---- this sample's dy3 image + y2 mask to LDS (the border re-zeroed: the previous sample's dy1 staging
+    // aliased it); y1 mask kept in registers; the next sample's loads issued
     {
-      const uint4 vp[3] = {vp0, vp1, vp2};
-#pragma unroll
-      for (int u = 0; u < 3; ++u) {
-        const int c = tid + u * BW_T;
-        if (c < P3_CH) *reinterpret_cast<uint4*>(s_p3 + (c / 9) * BW_LD3 + (c % 9) * 8) = vp[u];
+      if (tid < 392) {
+        const int px = tid >> 3, pa = px / 7, pb = px - pa * 7;
+        *reinterpret_cast<uint4*>(s_p3 + ((pa + 2) * BW_P3W + pb + 2) * BW_PS + (tid & 7) * 8) = vp0;
       }
+      bw_zero_border<BW_P3H, BW_P3W, 2, 7, BW_T>(s_p3);
       *reinterpret_cast<uint4*>(s_m2 + tid * 8) = vm0;
       if (tid + BW_T < M2_CH) *reinterpret_cast<uint4*>(s_m2 + (tid + BW_T) * 8) = vm1_;
     }
@@ -1411,13 +1422,13 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
 #pragma unroll
       for (int ks = 0; ks < 18; ++ks) {
         const int kb = ks * 32 + lg * 8, t = kb >> 6, o0 = kb & 63, ti = t / 3, tj = t - ti * 3;
-        const bf16x8 bw = tr_frag(s_w3z + ks * 32 * BW_LD3, BW_LD3, n0, lane);
+        const bf16x8 bw = tr_frag_sw<3>(s_w3z + ks * 32 * BW_LDW3, BW_LDW3, n0, lane);
 #pragma unroll
         for (int mt = 0; mt < 3; ++mt) {
           const int m = min((mh + mt) * 16 + l16, 80);
           const int a = m / 9, c = m - a * 9;
           const bf16x8 af =
-              *reinterpret_cast<const bf16x8*>(s_p3 + ((a - ti + 2) * BW_P3 + (c - tj + 2)) * BW_LD3 + o0);
+              *reinterpret_cast<const bf16x8*>(s_p3 + ((a - ti + 2) * BW_P3W + (c - tj + 2)) * BW_PS + o0);
           acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bw, acc[mt], 0, 0, 0);
         }
       }
@@ -1430,14 +1441,14 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
           if (m < 81) {
             const int a = m / 9, c = m - a * 9;
             const float v = bf2f(s_m2[m * 64 + n]) > 0.f ? acc[mt][r] : 0.f;
-            s_p2[((a + 1) * BW_P2 + (c + 1)) * BW_LD3 + n] = f2bf(v);
+            s_p2[((a + 1) * BW_P2W + (c + 1)) * BW_PS + n] = f2bf(v);
           }
         }
     }
     float part3[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int c = tid; c < 49 * 8; c += BW_T) {
       const int px = c >> 3, g = c & 7, pa = px / 7, pb = px - pa * 7;
-      const uint4 v = *reinterpret_cast<const uint4*>(s_p3 + ((pa + 2) * BW_P3 + (pb + 2)) * BW_LD3 + g * 8);
+      const uint4 v = *reinterpret_cast<const uint4*>(s_p3 + ((pa + 2) * BW_P3W + (pb + 2)) * BW_PS + g * 8);
 #pragma unroll
       for (int e = 0; e < 8; ++e) part3[e] += bf_lane(v, e);
     }
@@ -1448,7 +1459,7 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
     float part2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int c = tid; c < 81 * 8; c += BW_T) {
       const int m = c >> 3, g = c & 7, a = m / 9, cc = m - a * 9;
-      const uint4 v = *reinterpret_cast<const uint4*>(s_p2 + ((a + 1) * BW_P2 + (cc + 1)) * BW_LD3 + g * 8);
+      const uint4 v = *reinterpret_cast<const uint4*>(s_p2 + ((a + 1) * BW_P2W + (cc + 1)) * BW_PS + g * 8);
       *reinterpret_cast<uint4*>(dy2g + ((size_t)b * 81 + m) * 64 + g * 8) = v;
 #pragma unroll
       for (int e = 0; e < 8; ++e) part2[e] += bf_lane(v, e);
@@ -1480,7 +1491,7 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
         for (int i = 0; i < 7; ++i) {
           const int u = min(i * 16 + l16, 99), yy = u / 10, xx = u - yy * 10;
           const bf16x8 af = *reinterpret_cast<const bf16x8*>(
-              s_p2 + ((yy - di + 1) * BW_P2 + (xx - dj + 1)) * BW_LD3 + ob + lg * 8);
+              s_p2 + ((yy - di + 1) * BW_P2W + (xx - dj + 1)) * BW_PS + ob + lg * 8);
           acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, w2f[ks], acc[i], 0, 0, 0);
         }
       }

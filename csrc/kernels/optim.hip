@@ -331,6 +331,40 @@ __device__ __forceinline__ float fin_job(const int64_t* __restrict__ w, float* _
       if constexpr (FUSED) out[tid] = v; else dst[tid] = v;
       s = v * v;
     }
+  } else if (vec && S <= 4) {
+    // few planes of many elements (a two-split fc weight gradient): 8 float4 elements x S planes per thread in
+    // flight per round (one element at a time would be a dependent round trip per 2 loads); plane order per element
+    const int n4 = n >> 2;
+    const float4* s4 = reinterpret_cast<const float4*>(src);
+    const int64_t st4 = stride >> 2;
+    for (int i0 = tid; i0 < n4; i0 += OPT_THREADS * 8) {
+      float4 v[4][8];
+#pragma unroll
+      for (int z = 0; z < 4; ++z)
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int i = i0 + OPT_THREADS * u;
+          if (z < S) v[z][u] = s4[z * st4 + (i < n4 ? i : 0)];
+        }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + OPT_THREADS * u;
+        if (i < n4) {
+          float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+          for (int z = 0; z < 4; ++z)
+            if (z < S) { acc.x += v[z][u].x; acc.y += v[z][u].y; acc.z += v[z][u].z; acc.w += v[z][u].w; }
+          if constexpr (FUSED) reinterpret_cast<float4*>(out)[i] = acc; else reinterpret_cast<float4*>(dst)[i] = acc;
+          s += acc.x * acc.x + acc.y * acc.y + acc.z * acc.z + acc.w * acc.w;
+        }
+      }
+    }
+    for (int i = 4 * n4 + tid; i < n; i += OPT_THREADS) {
+      float v = 0.f;
+      for (int z = 0; z < S; ++z) v += src[(int64_t)z * stride + i];
+      if constexpr (FUSED) out[i] = v; else dst[i] = v;
+      s += v * v;
+    }
   } else if (vec) {
     // planes, float4 elements: 16 planes per round in flight (the rounds are dependent memory round trips: 4 of
     // them for the headline's 64 weight-gradient planes, not 8), elements striding over the workgroup; the adds run

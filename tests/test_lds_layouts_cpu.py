@@ -102,3 +102,68 @@ def test_transposed_tiles_conflict_free(w, bk):
     # the swizzle is a permutation of each row's chunks (no two columns share a slot)
     for k in range(bk):
         assert sorted(c ^ tr_swz(w, k) for c in range(per_row)) == list(range(per_row))
+
+
+# ---------------------------------------------------------------------------------------------- trunk backward
+CNN = os.path.join(os.path.dirname(__file__), "..", "csrc", "kernels", "cnn_fused.hip")
+GTR = [list(range(32)), list(range(32, 64))]
+
+
+def _bw_consts():
+    src = open(CNN).read()
+    c = {k: int(re.search(r"\b%s = (\d+)" % k, src).group(1)) for k in
+         ("BW_LDW3", "BW_LDW2", "BW_PS", "BW_P3W", "BW_P2W")}
+    assert "(((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2)" in src and "return ((r >> 3) & 1) << 1;" in src
+    return c
+
+
+def test_trunk_bwd_image_reads_are_conflict_free():
+    """cnn_trunk_bwd(_persist): the A fragments of dy2 (dy3 image, 9-wide output) and dy1 (dy2 image, 10-wide
+    sub-pixel classes) read at one LDS cycle per lane group under the model."""
+    c = _bw_consts()
+    ps = c["BW_PS"] * 2   # bytes per pixel
+    for wid in range(8):
+        mh = (wid >> 2) * 3
+        for ks in range(18):
+            for mt in range(3):
+                addr = []
+                for lane in range(64):
+                    l16, lg = lane & 15, lane >> 4
+                    kb = ks * 32 + lg * 8
+                    t, o0 = kb >> 6, kb & 63
+                    ti, tj = t // 3, t % 3
+                    m = min((mh + mt) * 16 + l16, 80)
+                    a, cc = m // 9, m % 9
+                    addr.append(((a - ti + 2) * c["BW_P3W"] + (cc - tj + 2)) * ps + o0 * 2)
+                assert cycles([[addr[l] for l in g] for g in G128], 4, 64) == 4, (wid, ks, mt)
+    for ks in range(8):
+        d = ks >> 1
+        di, dj, ob = d >> 1, d & 1, (ks & 1) * 32
+        for i in range(7):
+            addr = []
+            for lane in range(64):
+                l16, lg = lane & 15, lane >> 4
+                u = min(i * 16 + l16, 99)
+                yy, xx = u // 10, u % 10
+                addr.append(((yy - di + 1) * c["BW_P2W"] + (xx - dj + 1)) * ps + (ob + lg * 8) * 2)
+            assert cycles([[addr[l] for l in g] for g in G128], 4, 64) == 4, (ks, i)
+
+
+def test_trunk_bwd_weight_reads_are_conflict_free():
+    """W3 / W2 B rows, unpadded with XOR-swizzled 16-byte chunks: every ds_read_b64_tr_b16 of tr_frag_sw at one
+    LDS cycle per 32-lane group."""
+    c = _bw_consts()
+    sw3 = lambda r: (((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2)
+    sw2 = lambda r: ((r >> 3) & 1) << 1
+    for ld, sw, col0s, row0s in ((c["BW_LDW3"], sw3, (0, 16, 32, 48), [ks * 32 for ks in range(18)]),
+                                 (c["BW_LDW2"], sw2, (0, 16), [t * 64 + ob for t in range(16) for ob in (0, 32)])):
+        for col0 in col0s:
+            for row0 in row0s:
+                for half in (0, 4):
+                    addr = []
+                    for lane in range(64):
+                        lr16, lg = lane & 15, lane >> 4
+                        q, p = lr16 >> 2, lr16 & 3
+                        r, col = row0 + lg * 8 + half + q, col0 + 4 * p
+                        addr.append((r * ld + (((col >> 3) ^ sw(r)) << 3) + (col & 7)) * 2)
+                    assert cycles([[addr[l] for l in g] for g in GTR], 2, 64) == 2, (ld, col0, row0, half)

@@ -1432,6 +1432,7 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
           acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bw, acc[mt], 0, 0, 0);
         }
       }
+      pst(it, 6);
       const int n = n0 + l16;
 #pragma unroll
       for (int mt = 0; mt < 3; ++mt)
@@ -1452,6 +1453,7 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
 #pragma unroll
       for (int e = 0; e < 8; ++e) part3[e] += bf_lane(v, e);
     }
+    pst(it, 7);
     __syncthreads();   // dy2 image complete; the dy3 image and the y2 mask are dead
     pst(it, 2);
 

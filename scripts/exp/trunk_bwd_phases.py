@@ -48,6 +48,9 @@ def main():
             d = x[:, it * 8 + k + 1] - x[:, it * 8 + k]
             ph[n] = round(float(d.median()), 3)
         ph["total"] = round(float((x[:, it * 8 + 5] - x[:, it * 8]).median()), 3)
+        ph["  of which dy2 mfma loop"] = round(float((x[:, it * 8 + 6] - x[:, it * 8 + 1]).median()), 3)
+        ph["  of which dy2 epilogue+db3"] = round(float((x[:, it * 8 + 7] - x[:, it * 8 + 6]).median()), 3)
+        ph["  of which barrier wait"] = round(float((x[:, it * 8 + 2] - x[:, it * 8 + 7]).median()), 3)
         out[f"sample{it}"] = ph
     out["loop_gap_us"] = round(float((x[:, 8] - x[:, 5]).median()), 3)
     out["start_spread_us"] = round(float(x[:, 0].max() - x[:, 0].min()), 3)

@@ -235,7 +235,15 @@ class FusedGroupStep:
     @torch.no_grad()
     def step(self):
         ops = _native.require()
-        parts = [o._native_norm(ops) for o in self.opts]
+        plain = [o for o in self.opts if o.max_grad_norm is not None and o.ext_parts is None and o.clip_value is None]
+        if len(plain) > 1:
+            # the groups' plain sums of squares (data parallelism: no engine-written partials) in ONE launch
+            ops.sumsq_multi([o.g for o in plain], [o._partial for o in plain])
+            for o in plain:
+                o._norm_mul = o.grad_mul * o.grad_mul
+            parts = [o._partial if o in plain else o._native_norm(ops) for o in self.opts]
+        else:
+            parts = [o._native_norm(ops) for o in self.opts]
         key = tuple((p.data_ptr() if p is not None else 0, o._norm_mul, o.grad_mul, o.g.data_ptr())
                     for p, o in zip(parts, self.opts))
         if key != self._key:

@@ -85,6 +85,7 @@ hipError_t aca_conv_wgrad_gemm(int, const uint16_t*, const uint16_t*, float*, in
 hipError_t aca_gemm_big(const AcaGemmDesc*, hipStream_t);
 int64_t aca_gemm_big_ws(int, int, int);
 hipError_t aca_sumsq(const float*, size_t, float*, hipStream_t);
+hipError_t aca_sumsq_multi(const float* const*, const size_t*, float* const*, int, hipStream_t);
 int aca_sumsq_parts();
 hipError_t aca_adam_step(float*, float*, float*, float*, size_t, const float*, float*, const float*, float*, uint16_t*,
                          float, float, float, float, float, unsigned int*, int, float, float, hipStream_t);
@@ -729,6 +730,23 @@ void sumsq(Tensor x, Tensor partial) {
   need(partial, at::kFloat, "partial");
   TORCH_CHECK(partial.numel() >= aca_sumsq_parts(), "sumsq: partial needs ", aca_sumsq_parts(), " slots");
   check(aca_sumsq(ptr<float>(x), x.numel(), ptr<float>(partial), cur_stream(x)), "sumsq");
+}
+
+// several sums of squares (one partial set each) in one launch: the per-group norms of a multi-group optimiser step
+void sumsq_multi(std::vector<Tensor> xs, std::vector<Tensor> partials) {
+  TORCH_CHECK(!xs.empty() && xs.size() <= 4 && xs.size() == partials.size(), "sumsq_multi: 1..4 (x, partial) pairs");
+  const float* xp[4];
+  float* pp[4];
+  size_t ns[4];
+  for (size_t g = 0; g < xs.size(); ++g) {
+    need(xs[g], at::kFloat, "x");
+    need(partials[g], at::kFloat, "partial");
+    TORCH_CHECK(partials[g].numel() >= aca_sumsq_parts(), "sumsq_multi: partial needs ", aca_sumsq_parts(), " slots");
+    xp[g] = ptr<float>(xs[g]);
+    pp[g] = ptr<float>(partials[g]);
+    ns[g] = xs[g].numel();
+  }
+  check(aca_sumsq_multi(xp, ns, pp, (int)xs.size(), cur_stream(xs[0])), "sumsq_multi");
 }
 
 const float* gnorm_parts_ptr(const c10::optional<Tensor>& parts, double max_norm, const char* who) {
@@ -1715,6 +1733,7 @@ TORCH_LIBRARY(acamd, m) {
   m.def("normalize(Tensor a, Tensor out, float eps) -> ()");
   m.def("moments(Tensor x, Tensor y, Tensor out) -> ()");
   m.def("sumsq(Tensor x, Tensor partial) -> ()");
+  m.def("sumsq_multi(Tensor[] xs, Tensor[] partials) -> ()");
   m.def("adam_step(Tensor p, Tensor g, Tensor m, Tensor v, Tensor lr, Tensor t, Tensor? gnorm_parts, "
         "Tensor? gnorm_out, Tensor? shadow, float b1, float b2, float eps, float clip, float max_norm, Tensor ticket, "
         "bool zero_grad=False, float gmul=1.0, float norm_mul=1.0) -> ()");
@@ -1805,6 +1824,7 @@ TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
   m.impl("conv_wgrad_gemm", &conv_wgrad_gemm);
   m.impl("moments", &moments);
   m.impl("sumsq", &sumsq);
+  m.impl("sumsq_multi", &sumsq_multi);
   m.impl("adam_step", &adam_step);
   m.impl("rmsprop_step", &rmsprop_step);
   m.impl("cast_bf16", &cast_bf16);

@@ -19,16 +19,17 @@ constexpr unsigned int OPT_TK_LINE = 32;   // Adam step ticket: 9 counters, one 
 constexpr int SUMSQ_U = 8;
 constexpr int SUMSQ_PARTS = 256;   // max sumsq workgroups = partial slots the optimiser reduces
 
-__global__ void __launch_bounds__(OPT_THREADS) sumsq_kernel(const float* __restrict__ x, size_t n,
-                                                             float* __restrict__ partial) {
-  __shared__ float sh[16];
+// Partial sums of squares of x over `nblk` workgroups (this one: `bid`), one partial slot each; slot `nblk` .. are
+// zeroed by workgroup 0 so the consumer always sums SUMSQ_PARTS entries in a fixed order.
+__device__ __forceinline__ void sumsq_body(const float* __restrict__ x, size_t n, float* __restrict__ partial,
+                                           int nblk, int bid, float* sh) {
   float s = 0.f;
   const size_t n4 = n / 4;
   const float4* x4 = reinterpret_cast<const float4*>(x);
   // SUMSQ_U independent 16-byte loads in flight per thread before any use: the grid is capped at one workgroup
   // per CU, so latency (not bandwidth) bounds a one-load-at-a-time loop
-  const size_t step = (size_t)gridDim.x * blockDim.x * SUMSQ_U;
-  for (size_t i0 = blockIdx.x * (size_t)blockDim.x * SUMSQ_U + threadIdx.x; i0 < n4; i0 += step) {
+  const size_t step = (size_t)nblk * blockDim.x * SUMSQ_U;
+  for (size_t i0 = bid * (size_t)blockDim.x * SUMSQ_U + threadIdx.x; i0 < n4; i0 += step) {
     float4 v[SUMSQ_U];
 #pragma unroll
     for (int u = 0; u < SUMSQ_U; ++u) {
@@ -38,13 +39,33 @@ __global__ void __launch_bounds__(OPT_THREADS) sumsq_kernel(const float* __restr
 #pragma unroll
     for (int u = 0; u < SUMSQ_U; ++u) s += v[u].x * v[u].x + v[u].y * v[u].y + v[u].z * v[u].z + v[u].w * v[u].w;
   }
-  if (blockIdx.x == 0) {
+  if (bid == 0) {
     for (size_t i = n4 * 4 + threadIdx.x; i < n; i += blockDim.x) s += x[i] * x[i];
-    // unused partial slots are zero, so the consumer always sums SUMSQ_PARTS entries in a fixed order
-    for (int b = gridDim.x + threadIdx.x; b < SUMSQ_PARTS; b += blockDim.x) partial[b] = 0.f;
+    for (int b = nblk + threadIdx.x; b < SUMSQ_PARTS; b += blockDim.x) partial[b] = 0.f;
   }
   s = block_sum(s, sh);
-  if (threadIdx.x == 0) partial[blockIdx.x] = s;
+  if (threadIdx.x == 0) partial[bid] = s;
+}
+
+__global__ void __launch_bounds__(OPT_THREADS) sumsq_kernel(const float* __restrict__ x, size_t n,
+                                                             float* __restrict__ partial) {
+  __shared__ float sh[16];
+  sumsq_body(x, n, partial, gridDim.x, blockIdx.x, sh);
+}
+
+// Several independent sums of squares in ONE launch (the separate actor / critic norms of a data-parallel MLP
+// update): blockIdx.y = segment, each with the workgroup count a single sumsq launch would use (same partials).
+struct SumsqSegs {
+  const float* x[4];
+  float* partial[4];
+  size_t n[4];
+  int nblk[4];
+};
+__global__ void __launch_bounds__(OPT_THREADS) sumsq_multi_kernel(SumsqSegs a) {
+  __shared__ float sh[16];
+  const int g = blockIdx.y;
+  if ((int)blockIdx.x >= a.nblk[g]) return;
+  sumsq_body(a.x[g], a.n[g], a.partial[g], a.nblk[g], blockIdx.x, sh);
 }
 
 // Global squared norm from the sumsq partials, reduced by every consumer workgroup in the same fixed order
@@ -460,6 +481,26 @@ extern "C" hipError_t aca_sumsq(const float* x, size_t n, float* partial, hipStr
 }
 
 extern "C" int aca_sumsq_parts() { return SUMSQ_PARTS; }
+
+extern "C" hipError_t aca_sumsq_multi(const float* const* xs, const size_t* ns, float* const* partials, int nseg,
+                                      hipStream_t stream) {
+  if (nseg < 1 || nseg > 4) return hipErrorInvalidValue;
+  SumsqSegs a{};
+  int gx = 1;
+  for (int g = 0; g < nseg; ++g) {
+    if (reinterpret_cast<uintptr_t>(xs[g]) % 16) return hipErrorInvalidValue;
+    int grid = (int)((ns[g] / 4 + OPT_THREADS * SUMSQ_U - 1) / (OPT_THREADS * SUMSQ_U));
+    if (grid < 1) grid = 1;
+    if (grid > SUMSQ_PARTS) grid = SUMSQ_PARTS;
+    a.x[g] = xs[g];
+    a.n[g] = ns[g];
+    a.partial[g] = partials[g];
+    a.nblk[g] = grid;
+    gx = grid > gx ? grid : gx;
+  }
+  sumsq_multi_kernel<<<dim3(gx, nseg), OPT_THREADS, 0, stream>>>(a);
+  return hipGetLastError();
+}
 
 // jobs: device int64 [njobs, FIN_WORDS] (built by the host, ops/optim.py finalize_jobs); partial: SUMSQ_PARTS floats
 extern "C" hipError_t aca_grad_finalize(const int64_t* jobs, int njobs, float* partial, hipStream_t stream) {

@@ -247,3 +247,22 @@ def test_ppo_head_from_fc_planes_equals_stored_h(cuda):
         outs.append(o)
     for k in outs[0]:
         assert torch.equal(outs[0][k], outs[1][k]), k
+
+
+def test_sumsq_multi_equals_separate_launches(cuda):
+    """One launch for several groups' sums of squares (data-parallel multi-group optimiser step) writes exactly the
+    partials of one sumsq launch per group."""
+    from actor_critic_algs_on_tensorflow_amd import _native
+    ops = _native.require()
+    g = torch.Generator(device="cpu").manual_seed(4)
+    xs = [torch.randn(n, generator=g).to(cuda) for n in (37, 25347, 50561, 4 * 1024 * 1024 + 3)]
+    P = int(ops.sumsq_parts()) if hasattr(ops, "sumsq_parts") else 256
+    sep = [torch.full((P,), float("nan"), device=cuda) for _ in xs]
+    mul = [torch.full((P,), float("nan"), device=cuda) for _ in xs]
+    for x, p in zip(xs, sep):
+        ops.sumsq(x, p)
+    ops.sumsq_multi(xs, mul)
+    torch.cuda.synchronize()
+    for a, b, x in zip(sep, mul, xs):
+        assert torch.equal(a, b)
+        assert abs(float(b.double().sum()) - float((x.double() ** 2).sum())) <= 1e-4 * float((x.double() ** 2).sum())

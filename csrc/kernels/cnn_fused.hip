@@ -233,6 +233,18 @@ __global__ void __launch_bounds__(T_THREADS) cnn_trunk_fwd_kernel(
 // counter), padded to whole 1 KB wave copies.
 constexpr int TP_OBS_PAD = 28 * 1024;   // one observation (28224 B) padded to whole 1 KB wave copies
 
+// Per-env activation images in LDS (trunk_env_convs), conflict-free for the conv2 / conv3 A-fragment reads: a
+// ds_read_b128 lane group holds 8 output positions at one channel chunk and 8 at the next; with the pixel strides
+// Y1_LD = 40 (5 bank quads) / Y2_LD = 80 (10) they land in 16 distinct quads when the image's row pitch satisfies
+// pitch * stride == output width * stride (mod 16 quads) for the stride-2 (conv2) / stride-1 (conv3) walk: y1 rows of
+// 25 pixels for the 9-wide conv2 output (2 x 25 = 2 x 9 + 32), y2 rows of 15 for the 7-wide conv3 output
+// (15 = 7 + 8) (tests/test_lds_layouts_cpu.py). Tight 20 / 9 pitches: 1.8 / 1.75 LDS cycles per read. y2 lives in
+// the staged observation's bytes (dead after conv1), which keeps two workgroups per CU.
+constexpr int E1_W = 25, E2_W = 15;
+constexpr int E1_ELEMS = 20 * E1_W * Y1_LD;   // 20000 u16 = 40 KB
+constexpr int E2_ELEMS = 9 * E2_W * Y2_LD;    // 10800 u16 = 21.6 KB
+static_assert(E2_ELEMS * 2 <= TP_OBS_PAD, "y2 image aliases the staged observation");
+
 __device__ __forceinline__ void trunk_obs_dma(const uint8_t* __restrict__ src, uint8_t* dst_lds) {
   // 28 wave-copies of 64 x 16 B: wave w copies blocks w, w + (waves), ...; lanes past the observation read its
   // last chunk again (their bytes land in the padding)
@@ -285,8 +297,9 @@ __device__ __forceinline__ void trunk_env_convs(const uint8_t* __restrict__ s_ob
       const int row = mt * 16 + lg * 4 + r;
       const u16 v0 = f2bf(fmaxf(acc0[r] * scale + bias0, 0.f));
       const u16 v1 = f2bf(fmaxf(acc1[r] * scale + bias1, 0.f));
-      s_y1[row * Y1_LD + l16] = v0;
-      s_y1[row * Y1_LD + 16 + l16] = v1;
+      const int px1 = (row / 20) * E1_W + row % 20;
+      s_y1[px1 * Y1_LD + l16] = v0;
+      s_y1[px1 * Y1_LD + 16 + l16] = v1;
       y1g[((size_t)e * Y1_ROWS + row) * Y1_C + l16] = v0;
       y1g[((size_t)e * Y1_ROWS + row) * Y1_C + 16 + l16] = v1;
     }
@@ -308,7 +321,7 @@ __device__ __forceinline__ void trunk_env_convs(const uint8_t* __restrict__ s_ob
       for (int mt = 0; mt < 6; ++mt) {
         const int m = min(mt * 16 + l16, Y2_ROWS - 1);
         const int oh = m / 9, ow = m - oh * 9;
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(s_y1 + ((oh * 2 + i) * 20 + ow * 2 + j) * Y1_LD + c0);
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(s_y1 + ((oh * 2 + i) * E1_W + ow * 2 + j) * Y1_LD + c0);
         acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw2[ks], acc[mt], 0, 0, 0);
       }
     }
@@ -319,7 +332,7 @@ __device__ __forceinline__ void trunk_env_convs(const uint8_t* __restrict__ s_ob
         const int row = mt * 16 + lg * 4 + r;
         if (row < Y2_ROWS) {
           const u16 v = f2bf(fmaxf(acc[mt][r] + bias2, 0.f));
-          s_y2[row * Y2_LD + n2] = v;
+          s_y2[((row / 9) * E2_W + row % 9) * Y2_LD + n2] = v;
           y2g[((size_t)e * Y2_ROWS + row) * Y2_C + n2] = v;
         }
       }
@@ -339,7 +352,7 @@ __device__ __forceinline__ void trunk_env_convs(const uint8_t* __restrict__ s_ob
       for (int mt = 0; mt < 4; ++mt) {
         const int m = min(mt * 16 + l16, Y3_ROWS - 1);
         const int oh = m / 7, ow = m - oh * 7;
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(s_y2 + ((oh + i) * 9 + ow + j) * Y2_LD + c0);
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(s_y2 + ((oh + i) * E2_W + ow + j) * Y2_LD + c0);
         acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw3[ks], acc[mt], 0, 0, 0);
       }
     }
@@ -373,9 +386,9 @@ __global__ void __launch_bounds__(256) cnn_trunk_fwd_u8_kernel(
     const u16* __restrict__ W2, const float* __restrict__ b2, const u16* __restrict__ W3,
     const float* __restrict__ b3, u16* __restrict__ y1g, u16* __restrict__ y2g, u16* __restrict__ y3g,
     float scale, uint8_t* __restrict__ shift_out, const int64_t* __restrict__ obs_idx) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_obs8[TP_OBS_PAD];
-  __shared__ __attribute__((aligned(16))) u16 s_y1[Y1_ROWS * Y1_LD];
-  __shared__ __attribute__((aligned(16))) u16 s_y2[Y2_ROWS * Y2_LD];
+  __shared__ __attribute__((aligned(16))) uint8_t s_obs8[TP_OBS_PAD];   // later the y2 image
+  __shared__ __attribute__((aligned(16))) u16 s_y1[E1_ELEMS];
+  u16* const s_y2 = reinterpret_cast<u16*>(s_obs8);
   const int e = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l16 = lane & 15;
@@ -896,9 +909,9 @@ __global__ void __launch_bounds__(256) pong_fused_env_step_kernel(
     const u16* __restrict__ W3, const float* __restrict__ b3, u16* __restrict__ y1g, u16* __restrict__ y2g,
     u16* __restrict__ y3g, float scale, uint8_t* __restrict__ shift_out) {
   constexpr int A = A1 - 1;
-  __shared__ __attribute__((aligned(16))) uint8_t s_obs8[TP_OBS_PAD];
-  __shared__ __attribute__((aligned(16))) u16 s_y1[Y1_ROWS * Y1_LD];
-  __shared__ __attribute__((aligned(16))) u16 s_y2[Y2_ROWS * Y2_LD];
+  __shared__ __attribute__((aligned(16))) uint8_t s_obs8[TP_OBS_PAD];   // later the y2 image
+  __shared__ __attribute__((aligned(16))) u16 s_y1[E1_ELEMS];
+  u16* const s_y2 = reinterpret_cast<u16*>(s_obs8);
   __shared__ float s_acc[4][A1];
   __shared__ PongOut cand[3];
   __shared__ int sh_act;

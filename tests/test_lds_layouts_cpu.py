@@ -167,3 +167,36 @@ def test_trunk_bwd_weight_reads_are_conflict_free():
                         r, col = row0 + lg * 8 + half + q, col0 + 4 * p
                         addr.append((r * ld + (((col >> 3) ^ sw(r)) << 3) + (col & 7)) * 2)
                     assert cycles([[addr[l] for l in g] for g in GTR], 2, 64) == 2, (ld, col0, row0, half)
+
+
+def test_per_env_trunk_forward_reads_are_conflict_free():
+    """trunk_env_convs (per-env trunk forward and the fused rollout step): the conv2 A fragments over the y1 image
+    (pixel stride Y1_LD, row pitch E1_W) and the conv3 ones over the y2 image (Y2_LD, E2_W) at one LDS cycle per
+    lane group."""
+    src = open(CNN).read()
+    y1_ld, y2_ld = (int(v) for v in re.search(r"constexpr int Y1_LD = (\d+), Y2_LD = (\d+);", src).groups())
+    e1_w, e2_w = (int(v) for v in re.search(r"constexpr int E1_W = (\d+), E2_W = (\d+);", src).groups())
+    body = src[src.index("void trunk_env_convs("):src.index("// conv1 / conv2 weight fragments of this wave")]
+    assert "((oh * 2 + i) * E1_W + ow * 2 + j) * Y1_LD + c0" in body and "((oh + i) * E2_W + ow + j) * Y2_LD + c0" in body
+    for ks in range(16):
+        for mt in range(6):
+            addr = []
+            for lane in range(64):
+                l16, lg = lane & 15, lane >> 4
+                k = ks * 32 + lg * 8
+                i, j, c0 = k >> 7, (k >> 5) & 3, k & 31
+                m = min(mt * 16 + l16, 80)
+                oh, ow = m // 9, m % 9
+                addr.append((((oh * 2 + i) * e1_w + ow * 2 + j) * y1_ld + c0) * 2)
+            assert cycles([[addr[l] for l in g] for g in G128], 4, 64) == 4, ("conv2", ks, mt)
+    for ks in range(18):
+        for mt in range(4):
+            addr = []
+            for lane in range(64):
+                l16, lg = lane & 15, lane >> 4
+                k = ks * 32 + lg * 8
+                i, j, c0 = k // 192, (k >> 6) % 3, k & 63
+                m = min(mt * 16 + l16, 48)
+                oh, ow = m // 7, m % 7
+                addr.append((((oh + i) * e2_w + ow + j) * y2_ld + c0) * 2)
+            assert cycles([[addr[l] for l in g] for g in G128], 4, 64) == 4, ("conv3", ks, mt)

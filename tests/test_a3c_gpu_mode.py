@@ -103,18 +103,19 @@ def test_a3c_gpu_workers_on_device(cuda, tmp_path):
 @pytest.mark.gpu
 def test_a3c_gpu_worker_learns_cartpole(cuda, tmp_path):
     """The reference's own update (preset a3c: one element-clipped Adam step per batch with the KL-adaptive actor
-    lr) trained THROUGH the device parameter server: CartPole-v0 (the reference's other env, its discrete head),
-    32 envs x 16 steps per worker update, the lr capped at 0.01. One worker makes the run deterministic (serial
-    applies, deterministic kernels). The mean episode length (= return; random play lasts about 20 steps) reaches
-    140 (measured on an MI355X: 92 -> 104 -> 141 -> 147 at 400 / 800 / 1200 / 1600 worker updates).
+    lr, capped at the reference's 0.1, A3C/process.py:12) trained THROUGH the device parameter server: CartPole-v0
+    (the reference's other env, its discrete head), 32 envs x 16 steps per worker update. One worker makes the run
+    deterministic (serial applies, deterministic kernels). The mean episode length (= return; random play lasts
+    about 20 steps) must reach 140.
 
-    Pendulum with this update: with the reference's lr cap of 0.1 (A3C/process.py:12) the KL controller drives the
-    lr to the cap, the tanh mean saturates and the log-std leaves its clip window -- the KL proxy reads exactly 0, no
-    gradient remains, and the run sits at random level (-1230, the round-2 plateau); capped at 0.01 it crawls (-1110
-    after 1500 updates on the native engine, profiles/r3_pendulum_learning.txt). The framework's Pendulum solve is
-    test_gpu_learning.py::test_pendulum_ppo_solves_and_checkpoint_evaluates (PPO on the reference networks)."""
+    Pendulum with this update at the reference geometry is seed-dependent in the reference's own algorithm: an
+    independent plain-PyTorch oracle of the worker update (scripts/exp/a3c_oracle.py) reaches -121 / -185 on two of
+    four seeds and stalls on the other two, and this framework's update equals the oracle's to 1e-6 per update
+    (tests/test_a3c_update_parity_cpu.py; profiles/r4_a3c_parity_and_seeds.txt has the per-seed curves). The
+    framework's reliable Pendulum solve is test_gpu_learning.py::test_pendulum_ppo_solves_and_checkpoint_evaluates
+    (PPO on the reference networks)."""
     res = _run(tmp_path, 2, device="cuda:0", staleness=-1, total=2000, report=400, num_envs=32, n_steps=16,
-               seed=12321, max_lr=0.01, env="CartPole-v0")
+               seed=12321, max_lr=0.1, env="CartPole-v0")
     _check(res, 1, -1, 2000)
     rets = [r[2] for r in res[1]["returns"]]
     assert len(rets) >= 4, rets

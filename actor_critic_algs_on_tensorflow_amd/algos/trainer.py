@@ -387,7 +387,7 @@ class ActorCriticTrainer:
                                     env.ep_ret, env.ep_stats, env.env_ids, st.obs[t + 1], st.rewards[t], st.dones[t],
                                     st.truncated[t], env.seed, env.max_episode_steps, hp, S, eng.bfc, eng.sW1,
                                     eng.b1, eng.sW2, eng.b2, eng.sW3, eng.b3, nxt.y1, nxt.y2, nxt.y3, 1.0 / 255.0,
-                                    st.obs[t + 2] if t + 2 <= T else None, int(self.cfg.engine_opts.fused_env_waves))
+                                    st.obs[t + 2] if t + 2 <= T else None)
             nxt.obs = st.obs[t + 1]
             eng.fc_planes(nxt)
         hp, S = eng.last_fc

@@ -18,7 +18,6 @@ class EngineOpts:
     # -- rollout -------------------------------------------------------------------------------------------------
     fused_step: bool = True           # Pong bank: policy/env step t fused with the row-split trunk of obs t+1
     trunk_rows_max_b: int = 64        # row-split trunk (7 workgroups per env) up to this many envs, per-env above
-    fused_env_waves: int = 0          # per-env fused rollout step: 0 auto (8 waves while <= 256 envs), 4 or 8
     trunk_late_w: bool = True         # row-split trunk: conv2/conv3 weight fragments requested after conv1's MFMAs
     fc_max_planes: int = 32           # split-K partial planes of the rollout fc product (consumer-reduced)
     # -- learner -------------------------------------------------------------------------------------------------
@@ -39,10 +38,6 @@ class EngineOpts:
     wgrad_planes: int = 64            # split-K planes of the GEMM weight gradients
     conv1_planes: int = 128           # planes of the per-sample conv1 weight gradient
     nhwc_planes: int = 256            # planes of the conv2 / conv3 weight-gradient kernels
-
-    def __post_init__(self):
-        if self.fused_env_waves not in (0, 4, 8):
-            raise ValueError(f"EngineOpts.fused_env_waves must be 0 (auto), 4 or 8, got {self.fused_env_waves!r}")
 
     def replace(self, **kw):
         return dataclasses.replace(self, **kw)

@@ -59,7 +59,7 @@ hipError_t aca_pong_fused_env_step(uint16_t*, const float*, int, int64_t, const 
                                    int64_t*, float*, float*, const int64_t*, uint8_t*, float*, uint8_t*, uint8_t*,
                                    uint32_t, int, const uint16_t*, const float*, const uint16_t*, const float*,
                                    const uint16_t*, const float*, uint16_t*, uint16_t*, uint16_t*, float, uint8_t*, int,
-                                   int, hipStream_t);
+                                   hipStream_t);
 hipError_t aca_categorical_sample(const float*, int, int, int, const int64_t*, const int64_t*, const int64_t*, int,
                                   uint32_t, int32_t*, float*, float*, float*, hipStream_t);
 hipError_t aca_ev(const float*, const float*, float*, int, hipStream_t);
@@ -374,9 +374,8 @@ void pong_fused_env_step(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, T
                          Tensor ep_stats, Tensor ids, Tensor out, Tensor reward, Tensor done, Tensor trunc,
                          int64_t seed, int64_t max_steps, Tensor hpart, int64_t planes, Tensor bfc, Tensor W1,
                          Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, Tensor y1, Tensor y2, Tensor y3,
-                         double scale, c10::optional<Tensor> shift_out, int64_t waves) {
+                         double scale, c10::optional<Tensor> shift_out) {
   check_env(state, t, tg, ep_ret, ep_stats, ids, reward, done, trunc);
-  TORCH_CHECK(waves == 0 || waves == 4 || waves == 8, "pong_fused_env_step: waves 0 (auto) / 4 / 8");
   for (auto* x : {&h, &Wh, &W1, &W2, &W3, &y1, &y2, &y3}) need(*x, at::kBFloat16, "pong_fused_env_step bf16");
   for (auto* x : {&bh, &z, &logp, &ent, &value, &hpart, &bfc, &b1, &b2, &b3})
     need(*x, at::kFloat, "pong_fused_env_step f32");
@@ -414,7 +413,7 @@ void pong_fused_env_step(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, T
                                 ptr<uint8_t>(done), ptr<uint8_t>(trunc), (uint32_t)seed, (int)max_steps,
                                 ptr<uint16_t>(W1), ptr<float>(b1), ptr<uint16_t>(W2), ptr<float>(b2),
                                 ptr<uint16_t>(W3), ptr<float>(b3), ptr<uint16_t>(y1), ptr<uint16_t>(y2),
-                                ptr<uint16_t>(y3), (float)scale, so, N, (int)waves, cur_stream(state)),
+                                ptr<uint16_t>(y3), (float)scale, so, N, cur_stream(state)),
         "pong_fused_env_step");
 }
 
@@ -1709,7 +1708,7 @@ TORCH_LIBRARY(acamd, m) {
         "Tensor value, int key_shift, int pseed, Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, "
         "Tensor env_ids, Tensor out, Tensor reward, Tensor done, Tensor truncated, int seed, int max_steps, "
         "Tensor hpart, int planes, Tensor bfc, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, "
-        "Tensor y1, Tensor y2, Tensor y3, float scale, Tensor? shift_out=None, int waves=0) -> ()");
+        "Tensor y1, Tensor y2, Tensor y3, float scale, Tensor? shift_out=None) -> ()");
   m.def("categorical_sample(Tensor logits, Tensor keys, int seed, Tensor act, Tensor logp, Tensor ent) -> ()");
   m.def("categorical_sample_env(Tensor logits, Tensor tg, Tensor env_ids, int key_shift, int seed, Tensor act, "
         "Tensor logp, Tensor ent, Tensor? vout) -> ()");

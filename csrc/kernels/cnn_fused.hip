@@ -267,19 +267,15 @@ __device__ __forceinline__ void trunk_obs_dma(const uint8_t* __restrict__ src, u
 // ------------------------------------------------------------------------------------------------------------
 // conv1 -> conv2 -> conv3 of env e from its staged uint8 observation (s_obs8, complete behind a barrier); bw / bw2:
 // this wave's conv1 / conv2 weight fragments (already in registers), W3's are loaded after conv1.
-template <int NW>
 __device__ __forceinline__ void trunk_env_convs(const uint8_t* __restrict__ s_obs8, u16* __restrict__ s_y1,
                                                 u16* __restrict__ s_y2, int e, const bf16x8 (&bw)[2][8],
                                                 const bf16x8 (&bw2)[16], const u16* __restrict__ W3, float bias0,
                                                 float bias1, float bias2, float bias3, u16* __restrict__ y1g,
                                                 u16* __restrict__ y2g, u16* __restrict__ y3g, float scale) {
-  // NW = 4: wave w = output-channel tile w of conv2 / conv3 over every M tile; NW = 8 (the rollout's 8-wave form):
-  // waves w and w + 4 share channel tile w & 3 and split the M tiles (same per-tile MFMA order: bit-identical)
-  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
-  constexpr int MT2 = NW == 4 ? 6 : 3, MT3 = NW == 4 ? 4 : 2;
+  constexpr int NW = 4;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l16 = lane & 15, lg = lane >> 4;
-  const int n2 = (wid & 3) * 16 + l16, mh = wid >> 2;
+  const int n2 = wid * 16 + l16;
   // ---------------------------------------------------------------- conv1: M 400 (25 tiles), N 32 (2), K 256 (8)
   for (int mt = wid; mt < 25; mt += NW) {
     floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
@@ -314,29 +310,28 @@ __device__ __forceinline__ void trunk_env_convs(const uint8_t* __restrict__ s_ob
   __syncthreads();
   // ---------------------------------------------------------------- conv2: M 81 (6 tiles), N 64 (wave = N tile), K 512
   {
-    floatx4 acc[MT2];
+    floatx4 acc[6];
 #pragma unroll
-    for (int q = 0; q < MT2; ++q) acc[q] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int mt = 0; mt < 6; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < 16; ++ks) {
       const int k = ks * 32 + lg * 8;
       const int i = k >> 7, j = (k >> 5) & 3, c0 = k & 31;
 #pragma unroll
-      for (int q = 0; q < MT2; ++q) {
-        const int mt = mh * MT2 + q;
+      for (int mt = 0; mt < 6; ++mt) {
         const int m = min(mt * 16 + l16, Y2_ROWS - 1);
         const int oh = m / 9, ow = m - oh * 9;
         const bf16x8 a = *reinterpret_cast<const bf16x8*>(s_y1 + ((oh * 2 + i) * E1_W + ow * 2 + j) * Y1_LD + c0);
-        acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw2[ks], acc[q], 0, 0, 0);
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw2[ks], acc[mt], 0, 0, 0);
       }
     }
 #pragma unroll
-    for (int q = 0; q < MT2; ++q) {
+    for (int mt = 0; mt < 6; ++mt) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = (mh * MT2 + q) * 16 + lg * 4 + r;
+        const int row = mt * 16 + lg * 4 + r;
         if (row < Y2_ROWS) {
-          const u16 v = f2bf(fmaxf(acc[q][r] + bias2, 0.f));
+          const u16 v = f2bf(fmaxf(acc[mt][r] + bias2, 0.f));
           s_y2[((row / 9) * E2_W + row % 9) * Y2_LD + n2] = v;
           y2g[((size_t)e * Y2_ROWS + row) * Y2_C + n2] = v;
         }
@@ -346,28 +341,27 @@ __device__ __forceinline__ void trunk_env_convs(const uint8_t* __restrict__ s_ob
   __syncthreads();
   // ---------------------------------------------------------------- conv3: M 49 (4 tiles), N 64 (wave = N tile), K 576
   {
-    floatx4 acc[MT3];
+    floatx4 acc[4];
 #pragma unroll
-    for (int q = 0; q < MT3; ++q) acc[q] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int mt = 0; mt < 4; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < 18; ++ks) {
       const int k = ks * 32 + lg * 8;
       const int i = k / 192, j = (k >> 6) % 3, c0 = k & 63;
 #pragma unroll
-      for (int q = 0; q < MT3; ++q) {
-        const int mt = mh * MT3 + q;
+      for (int mt = 0; mt < 4; ++mt) {
         const int m = min(mt * 16 + l16, Y3_ROWS - 1);
         const int oh = m / 7, ow = m - oh * 7;
         const bf16x8 a = *reinterpret_cast<const bf16x8*>(s_y2 + ((oh + i) * E2_W + ow + j) * Y2_LD + c0);
-        acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw3[ks], acc[q], 0, 0, 0);
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw3[ks], acc[mt], 0, 0, 0);
       }
     }
 #pragma unroll
-    for (int q = 0; q < MT3; ++q) {
+    for (int mt = 0; mt < 4; ++mt) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = (mh * MT3 + q) * 16 + lg * 4 + r;
-        if (row < Y3_ROWS) y3g[((size_t)e * Y3_ROWS + row) * Y3_C + n2] = f2bf(fmaxf(acc[q][r] + bias3, 0.f));
+        const int row = mt * 16 + lg * 4 + r;
+        if (row < Y3_ROWS) y3g[((size_t)e * Y3_ROWS + row) * Y3_C + n2] = f2bf(fmaxf(acc[mt][r] + bias3, 0.f));
       }
     }
   }
@@ -377,7 +371,7 @@ __device__ __forceinline__ void trunk_env_convs(const uint8_t* __restrict__ s_ob
 __device__ __forceinline__ void trunk_env_w12(const u16* __restrict__ W1, const u16* __restrict__ W2,
                                               bf16x8 (&bw)[2][8], bf16x8 (&bw2)[16]) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, l16 = lane & 15, lg = lane >> 4;
-  const int n2 = (wid & 3) * 16 + l16;   // 8-wave form: waves w and w + 4 hold the same channel tile
+  const int n2 = wid * 16 + l16;
 #pragma unroll
   for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
@@ -413,7 +407,7 @@ __global__ void __launch_bounds__(256) cnn_trunk_fwd_u8_kernel(
     const uint4* si = reinterpret_cast<const uint4*>(s_obs8);
     for (int i = OBS_BYTES / 64 + tid; i < OBS_BYTES / 16; i += 256) so[i - OBS_BYTES / 64] = si[i];
   }
-  trunk_env_convs<4>(s_obs8, s_y1, s_y2, e, bw, bw2, W3, bias0, bias1, bias2, bias3, y1g, y2g, y3g, scale);
+  trunk_env_convs(s_obs8, s_y1, s_y2, e, bw, bw2, W3, bias0, bias1, bias2, bias3, y1g, y2g, y3g, scale);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -906,10 +900,8 @@ __global__ void __launch_bounds__(T_THREADS) pong_fused_step_kernel(
 // One launch instead of the trunk kernel + the policy/env kernel of the unfused step, and the new frame never makes a
 // global round trip before conv1.
 // ------------------------------------------------------------------------------------------------------------
-// NT = 512 (8 waves; banks of at most one env per CU): the head runs on waves 0-3 as in the 4-wave form, the conv
-// chain on all 8 (trunk_env_convs<8>), so a lone workgroup on its CU has two waves per SIMD to hide latency.
-template <int A1, int NT>
-__global__ void __launch_bounds__(NT) pong_fused_env_step_kernel(
+template <int A1>
+__global__ void __launch_bounds__(256) pong_fused_env_step_kernel(
     PongIO io, FcParts fc, u16* __restrict__ h, const u16* __restrict__ Wh, const float* __restrict__ bh,
     float* __restrict__ z_out, int32_t* __restrict__ act, float* __restrict__ logp, float* __restrict__ ent,
     float* __restrict__ vout, int key_shift, uint32_t pseed, const u16* __restrict__ W1,
@@ -925,35 +917,32 @@ __global__ void __launch_bounds__(NT) pong_fused_env_step_kernel(
   __shared__ int sh_act;
   const int e = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, l16 = lane & 15;
-  const int n2 = (wid & 3) * 16 + l16;
-  const bool head = tid < 256;   // the policy head: hidden units 2t, 2t + 1 of threads 0..255
+  const int n2 = wid * 16 + l16;
   // ---------------------------------------------------------------- every independent operand requested first
   trunk_obs_dma(io.out + (size_t)e * OBS_BYTES, s_obs8);   // obs t+1: frames 0..2 valid, frame 3 rendered below
   const int64_t tg0 = io.tglob[e], id0 = io.env_ids[e];
   const float bhj = bh[lane < A1 ? lane : 0];
   uint32_t wv[A1];   // this thread's two Wh rows
 #pragma unroll
-  for (int u = 0; u < A1; ++u) wv[u] = reinterpret_cast<const uint32_t*>(Wh)[A1 * (head ? tid : 0) + u];
+  for (int u = 0; u < A1; ++u) wv[u] = reinterpret_cast<const uint32_t*>(Wh)[A1 * tid + u];
   bf16x8 bw[2][8], bw2[16];
   trunk_env_w12(W1, W2, bw, bw2);
   const float bias0 = b1[l16], bias1 = b1[16 + l16], bias2 = b2[n2], bias3 = b3[n2];
   // ---------------------------------------------------------------- policy head of obs t
-  if (head) {
-    float hf[2];
-    fc_h2_from_parts(fc.hpart, fc.S, fc.plane_stride, fc.bfc, e, tid, h, hf);
-    if (tid >= 64 && tid < 67) cand[tid - 64] = pong_advance(io, e, (float)(tid - 65));
-    float accj[A1];
+  float hf[2];
+  fc_h2_from_parts(fc.hpart, fc.S, fc.plane_stride, fc.bfc, e, tid, h, hf);
+  if (tid >= 64 && tid < 67) cand[tid - 64] = pong_advance(io, e, (float)(tid - 65));
+  float accj[A1];
 #pragma unroll
-    for (int j = 0; j < A1; ++j) {
-      const uint32_t w0 = wv[j >> 1], w1 = wv[(A1 + j) >> 1];
-      const float a0 = __uint_as_float((j & 1) ? (w0 & 0xFFFF0000u) : (w0 << 16));
-      const float a1 = __uint_as_float(((A1 + j) & 1) ? (w1 & 0xFFFF0000u) : (w1 << 16));
-      accj[j] = wave_sum(hf[0] * a0 + hf[1] * a1);
-    }
-    if (lane == 0)
-#pragma unroll
-      for (int j = 0; j < A1; ++j) s_acc[wid][j] = accj[j];
+  for (int j = 0; j < A1; ++j) {
+    const uint32_t w0 = wv[j >> 1], w1 = wv[(A1 + j) >> 1];
+    const float a0 = __uint_as_float((j & 1) ? (w0 & 0xFFFF0000u) : (w0 << 16));
+    const float a1 = __uint_as_float(((A1 + j) & 1) ? (w1 & 0xFFFF0000u) : (w1 << 16));
+    accj[j] = wave_sum(hf[0] * a0 + hf[1] * a1);
   }
+  if (lane == 0)
+#pragma unroll
+    for (int j = 0; j < A1; ++j) s_acc[wid][j] = accj[j];
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the staged frames have landed (and every fragment)
   __syncthreads();
   if (wid == 0) {
@@ -998,7 +987,7 @@ __global__ void __launch_bounds__(NT) pong_fused_env_step_kernel(
     const PongGeom gm = pong_geom(res.s);
     uint32_t* ob = reinterpret_cast<uint32_t*>(io.out + (size_t)e * OBS_BYTES);
     uint32_t* sw = reinterpret_cast<uint32_t*>(s_obs8);
-    for (int w = tid; w < NWORDS; w += NT) {
+    for (int w = tid; w < NWORDS; w += 256) {
       const int y = w / WPR, x0 = (w - y * WPR) * 4;
       const uint32_t word = pong_word(gm, y, x0);
       sw[3 * NWORDS + w] = word;
@@ -1015,9 +1004,9 @@ __global__ void __launch_bounds__(NT) pong_fused_env_step_kernel(
   if (shift_out) {   // frames 1..3 of obs t+1 become frames 0..2 of obs t+2
     uint4* so = reinterpret_cast<uint4*>(shift_out + (size_t)e * OBS_BYTES);
     const uint4* si = reinterpret_cast<const uint4*>(s_obs8);
-    for (int i = OBS_BYTES / 64 + tid; i < OBS_BYTES / 16; i += NT) so[i - OBS_BYTES / 64] = si[i];
+    for (int i = OBS_BYTES / 64 + tid; i < OBS_BYTES / 16; i += 256) so[i - OBS_BYTES / 64] = si[i];
   }
-  trunk_env_convs<NT / 64>(s_obs8, s_y1, s_y2, e, bw, bw2, W3, bias0, bias1, bias2, bias3, y1g, y2g, y3g, scale);
+  trunk_env_convs(s_obs8, s_y1, s_y2, e, bw, bw2, W3, bias0, bias1, bias2, bias3, y1g, y2g, y3g, scale);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -1697,12 +1686,9 @@ extern "C" hipError_t aca_pong_fused_env_step(
     uint32_t pseed, float* state, int32_t* t, int64_t* tg, float* ep_ret, float* ep_stats, const int64_t* ids,
     uint8_t* out, float* reward, uint8_t* done, uint8_t* trunc, uint32_t seed, int max_steps, const uint16_t* W1,
     const float* b1, const uint16_t* W2, const float* b2, const uint16_t* W3, const float* b3, uint16_t* y1,
-    uint16_t* y2, uint16_t* y3, float scale, uint8_t* shift_out, int N, int waves, hipStream_t stream) {
+    uint16_t* y2, uint16_t* y3, float scale, uint8_t* shift_out, int N, hipStream_t stream) {
   if (N <= 0) return hipSuccess;
   if (S < 1 || S > aca::FC_MAX_PLANES) return hipErrorInvalidValue;
-  // 8 waves while the bank leaves CUs idle (one workgroup per CU at most), else 4 (two workgroups per CU)
-  if (waves == 0) waves = N <= 256 ? 8 : 4;
-  if (waves != 4 && waves != 8) return hipErrorInvalidValue;
   aca::PongIO io;
   io.state = state; io.tsteps = t; io.tglob = tg; io.ep_ret = ep_ret; io.ep_stats = ep_stats; io.env_ids = ids;
   io.prev = out; io.out = out; io.reward = reward; io.done_out = done; io.trunc_out = trunc; io.seed = seed;
@@ -1711,14 +1697,9 @@ extern "C" hipError_t aca_pong_fused_env_step(
   switch (A + 1) {
 #define ACA_FES_CASE(A1)                                                                                         \
   case A1:                                                                                                       \
-    if (waves == 8)                                                                                              \
-      aca::pong_fused_env_step_kernel<A1, 512><<<N, 512, 0, stream>>>(io, fc, h, Wh, bh, z, act, logp, ent,      \
-                                                                     value, key_shift, pseed, W1, b1, W2, b2, W3, \
-                                                                     b3, y1, y2, y3, scale, shift_out);          \
-    else                                                                                                         \
-      aca::pong_fused_env_step_kernel<A1, 256><<<N, 256, 0, stream>>>(io, fc, h, Wh, bh, z, act, logp, ent,      \
-                                                                     value, key_shift, pseed, W1, b1, W2, b2, W3, \
-                                                                     b3, y1, y2, y3, scale, shift_out);          \
+    aca::pong_fused_env_step_kernel<A1><<<N, 256, 0, stream>>>(io, fc, h, Wh, bh, z, act, logp, ent, value,     \
+                                                               key_shift, pseed, W1, b1, W2, b2, W3, b3, y1, y2, \
+                                                               y3, scale, shift_out);                            \
     break;
     ACA_FES_CASE(3) ACA_FES_CASE(4) ACA_FES_CASE(5) ACA_FES_CASE(6) ACA_FES_CASE(7)
 #undef ACA_FES_CASE

@@ -112,14 +112,12 @@ def test_ppo_update_through_ppo_head_tracks_generic_head(cuda, monkeypatch):
     assert ((d1 - d0).norm() / d0.norm()).item() < 5e-2
 
 
-@pytest.mark.parametrize("preset_name,capture,waves", [("pong_a2c", True, 0), ("breakout_ppo", False, 0),
-                                                       ("breakout_ppo", True, 0), ("breakout_ppo", True, 4)])
-def test_fused_env_step_equals_separate_trunk_and_policy(cuda, preset_name, capture, waves, monkeypatch):
+@pytest.mark.parametrize("preset_name,capture", [("pong_a2c", True), ("breakout_ppo", False), ("breakout_ppo", True)])
+def test_fused_env_step_equals_separate_trunk_and_policy(cuda, preset_name, capture, monkeypatch):
     """Large banks (72 envs > the row-split limit): the per-env fused rollout step (pong_fused_env_step: policy/env
     step t + render + shift + the trunk of obs t+1 in one launch) reproduces the separate per-env trunk + policy/env
     launches bit for bit -- parameters, rollout tensors and env state over several updates with episode
-    truncations, A2C (learner reuses the rollout activations) and PPO, graph-captured or eager; the 8-wave launch
-    (auto at <= 256 envs) and the 4-wave one."""
+    truncations, A2C (learner reuses the rollout activations) and PPO, graph-captured or eager."""
     monkeypatch.setattr("actor_critic_algs_on_tensorflow_amd.ops.gemm.TUNE", False)
     from actor_critic_algs_on_tensorflow_amd import preset
     from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
@@ -127,8 +125,7 @@ def test_fused_env_step_equals_separate_trunk_and_policy(cuda, preset_name, capt
     for fused in (True, False):
         kw = dict(n_steps=5) if preset_name == "pong_a2c" else dict(n_steps=8, ppo_epochs=1, ppo_minibatches=2)
         tr = ActorCriticTrainer(preset(preset_name, num_envs=72, device="cuda:0", outdir=None, quiet=True,
-                                       stdout_freq=0, save_every=0, seed=5,
-                                       engine_opts=dict(fused_step=fused, fused_env_waves=waves), **kw))
+                                       stdout_freq=0, save_every=0, seed=5, engine_opts=dict(fused_step=fused), **kw))
         assert tr.engine.fused_env_step_ok(72) == fused
         tr.env.max_episode_steps = 7
         if capture:

@@ -1,0 +1,4 @@
+set -o pipefail
+timeout -k 10 600 python -u -m pytest tests/test_gpu_r4.py -x -q --timeout 120 --timeout-method thread && \
+timeout -k 10 300 python -u scripts/bench_configs.py --configs breakout_ppo --updates 5 --warmup 2 && \
+timeout -k 10 300 python -u scripts/bench_configs.py --configs breakout_ppo --updates 5 --warmup 2 --engine-opts '{"fused_env_waves": 4}'

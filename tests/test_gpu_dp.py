@@ -126,7 +126,8 @@ def _deltas(snaps):
 @pytest.mark.parametrize("world", [2, 4])
 def test_dp_ppo_captured_as_segments_equals_eager(cuda, tmp_path, world, monkeypatch):
     """Breakout-shaped PPO under DP (minibatch gradient all-reduces, global advantage normalisation via the packed
-    fp64 moments, KL proxy for the adaptive lr) is captured as a segment chain -- no eager fallback -- and its
+    fp64 moments, which also carry the KL proxy for the adaptive lr) is captured as a segment chain -- no eager
+    fallback -- and its
     replay is BITWISE equal to the eager DP run (deterministic PPO backward: split-K planes + ordered finaliser,
     ordered bias sums; fixed GEMM plans so both processes run the same kernels); ranks stay bit-identical."""
     monkeypatch.setenv("ACAMD_GEMM_TUNE", "0")
@@ -134,8 +135,8 @@ def test_dp_ppo_captured_as_segments_equals_eager(cuda, tmp_path, world, monkeyp
     cap = _spawn(tmp_path, world, 4, "strict", tag="ppo_cap", **kw)
     eag = _spawn(tmp_path, world, 4, "strict", tag="ppo_eager", capture=False, **kw)
     assert cap[0]["kind"] == "segments"
-    # 4 gradient all-reduces + 1 moments all-reduce + 1 KL all-reduce -> 7 graphs
-    assert cap[0]["n_graphs"] == 7, cap[0]["n_graphs"]
+    # 4 gradient all-reduces + 1 packed all-reduce of the advantage moments and the previous update's KL -> 6 graphs
+    assert cap[0]["n_graphs"] == 6, cap[0]["n_graphs"]
     for r in range(1, world):
         for a, b in zip(cap[0]["snaps"], cap[r]["snaps"]):
             assert torch.equal(a, b), "ranks diverged"

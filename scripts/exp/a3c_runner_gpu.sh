@@ -2,13 +2,13 @@
 # the reference A3C runner topology (A3C/runner.sh: 1 PS + 3 workers) on Pendulum-v0 at the
 # reference geometry -- each worker update is 6 whole 200-step episodes (1200 steps), L = 40, lr cap 0.1 -- with the
 # GPU-native workers sharing one GPU (gloo control plane), the chief checkpointing every 600 global steps; the
-# latest chief checkpoint scored by the eval CLI. Usage: bash scripts/gpu.sh TAG cmd=scripts/exp/a3c_runner_gpu.sh
+# latest chief checkpoint scored by the eval CLI. Usage: SEED=3 bash scripts/exp/a3c_runner_gpu.sh
 set -o pipefail
-O=gpurun_out/a3c_runner
-mkdir -p $O/logs $O/ck
 ITERS=${ITERS:-3000}
 SEED=${SEED:-12321}
 PORT=${PORT:-29631}
+O=gpurun_out/a3c_runner/seed$SEED
+mkdir -p $O/logs $O/ck
 common="--worker_num 3 --ps_num 1 --initport $PORT --max_iters $ITERS --outdir $O/logs --checkpoint_dir $O/ck \
   --device cuda:0 --num_envs 6 --n_steps 200 --seed $SEED --save_every 600 --stdout_freq 100"
 timeout -k 10 800 python -u -m actor_critic_algs_on_tensorflow_amd.cli.train ps 0 $common --quiet > $O/ps0.out 2>&1 &

@@ -373,9 +373,12 @@ class ActorCriticTrainer:
     def _collect_fused_env_steps(self, st, env, eng, lb, b, N):
         """Large banks (per-env trunk): trunk(obs_0) + fc, then per step ONE launch of policy/env step t fused with
         the per-env trunk of obs_{t+1} (``pong_fused_env_step``) + the fc product of obs_{t+1}; the last step's
-        trunk is the bootstrap observation's, whose value comes straight from the fc planes."""
+        trunk is the bootstrap observation's, whose value comes straight from the fc planes. With
+        ``EngineOpts.fused_env_split`` two workgroups per env share each step (the conv rows split in halves) and the
+        env state alternates between its parity slots, as in the row-split step."""
         ops = _native.require()
         T = st.T
+        split = eng.opts.fused_env_split
         rows = (lambda t: lb.rows(t * N, N)) if lb is not None else (lambda t: b)
         eng.forward(st.obs[0], rows(0), head=False, shift_out=st.obs[1], fc_parts=True)
         for t in range(T):
@@ -387,9 +390,13 @@ class ActorCriticTrainer:
                                     env.ep_ret, env.ep_stats, env.env_ids, st.obs[t + 1], st.rewards[t], st.dones[t],
                                     st.truncated[t], env.seed, env.max_episode_steps, hp, S, eng.bfc, eng.sW1,
                                     eng.b1, eng.sW2, eng.b2, eng.sW3, eng.b3, nxt.y1, nxt.y2, nxt.y3, 1.0 / 255.0,
-                                    st.obs[t + 2] if t + 2 <= T else None)
+                                    st.obs[t + 2] if t + 2 <= T else None,
+                                    list(env.next_state()) if split else None)
+            if split:
+                env.flip()
             nxt.obs = st.obs[t + 1]
             eng.fc_planes(nxt)
+        self._env_flips = T if split else 0
         hp, S = eng.last_fc
         if self._boot_in_head():
             self._boot = (hp, S)

@@ -19,6 +19,7 @@ class EngineOpts:
     fused_step: bool = True           # Pong bank: policy/env step t fused with the row-split trunk of obs t+1
     trunk_rows_max_b: int = 64        # row-split trunk (7 workgroups per env) up to this many envs, per-env above
     trunk_late_w: bool = True         # row-split trunk: conv2/conv3 weight fragments requested after conv1's MFMAs
+    fused_env_split: bool = True      # per-env fused step (banks above trunk_rows_max_b): two workgroups per env
     fc_max_planes: int = 32           # split-K partial planes of the rollout fc product (consumer-reduced)
     # -- learner -------------------------------------------------------------------------------------------------
     a2c_head: bool = True             # A2C: V(s_T) + returns + loss + head backward in one launch (loss.hip a2c_head)

@@ -58,8 +58,8 @@ hipError_t aca_pong_fused_env_step(uint16_t*, const float*, int, int64_t, const 
                                    int, float*, int32_t*, float*, float*, float*, int, uint32_t, float*, int32_t*,
                                    int64_t*, float*, float*, const int64_t*, uint8_t*, float*, uint8_t*, uint8_t*,
                                    uint32_t, int, const uint16_t*, const float*, const uint16_t*, const float*,
-                                   const uint16_t*, const float*, uint16_t*, uint16_t*, uint16_t*, float, uint8_t*, int,
-                                   hipStream_t);
+                                   const uint16_t*, const float*, uint16_t*, uint16_t*, uint16_t*, float, uint8_t*,
+                                   float*, int32_t*, int64_t*, float*, uint64_t*, int, hipStream_t);
 hipError_t aca_categorical_sample(const float*, int, int, int, const int64_t*, const int64_t*, const int64_t*, int,
                                   uint32_t, int32_t*, float*, float*, float*, hipStream_t);
 hipError_t aca_ev(const float*, const float*, float*, int, hipStream_t);
@@ -368,14 +368,27 @@ void pong_fused_step(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, Tenso
 // Per-env fused rollout step (cnn_fused.hip pong_fused_env_step_kernel): policy/env step t of env e (fc planes of
 // obs t -> h, head, sample, physics, commit into (state, t, tg, ep_ret)) + the new frame rendered into obs t+1 (out,
 // frames 0..2 already shifted in) + frames 1..3 of obs t+1 shifted into shift_out (obs t+2, or None) + conv1..conv3
-// of obs t+1 into y1..y3. One workgroup per env.
+// of obs t+1 into y1..y3. One workgroup per env; with next_state = [state_n, t_n, tg_n, ep_ret_n] (the other parity's
+// env state) two workgroups per env, the state committed there (the caller flips parity after the launch).
 void pong_fused_env_step(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, Tensor logp, Tensor ent, Tensor value,
                          int64_t key_shift, int64_t pseed, Tensor state, Tensor t, Tensor tg, Tensor ep_ret,
                          Tensor ep_stats, Tensor ids, Tensor out, Tensor reward, Tensor done, Tensor trunc,
                          int64_t seed, int64_t max_steps, Tensor hpart, int64_t planes, Tensor bfc, Tensor W1,
                          Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, Tensor y1, Tensor y2, Tensor y3,
-                         double scale, c10::optional<Tensor> shift_out) {
+                         double scale, c10::optional<Tensor> shift_out, c10::optional<std::vector<Tensor>> next_state,
+                         c10::optional<Tensor> stamps) {
   check_env(state, t, tg, ep_ret, ep_stats, ids, reward, done, trunc);
+  float* sn = nullptr; int32_t* tn = nullptr; int64_t* tgn = nullptr; float* ern = nullptr;
+  if (next_state.has_value()) {
+    const auto& v = *next_state;
+    TORCH_CHECK(v.size() == 4, "pong_fused_env_step: next_state = [state, t, tg, ep_ret]");
+    check_env(v[0], v[1], v[2], v[3], ep_stats, ids, reward, done, trunc);
+    TORCH_CHECK(v[0].sizes() == state.sizes() && v[0].data_ptr() != state.data_ptr() &&
+                    v[1].data_ptr() != t.data_ptr() && v[2].data_ptr() != tg.data_ptr() &&
+                    v[3].data_ptr() != ep_ret.data_ptr(),
+                "pong_fused_env_step: the next-parity env state must be separate buffers of the same shape");
+    sn = ptr<float>(v[0]); tn = ptr<int32_t>(v[1]); tgn = ptr<int64_t>(v[2]); ern = ptr<float>(v[3]);
+  }
   for (auto* x : {&h, &Wh, &W1, &W2, &W3, &y1, &y2, &y3}) need(*x, at::kBFloat16, "pong_fused_env_step bf16");
   for (auto* x : {&bh, &z, &logp, &ent, &value, &hpart, &bfc, &b1, &b2, &b3})
     need(*x, at::kFloat, "pong_fused_env_step f32");
@@ -413,7 +426,8 @@ void pong_fused_env_step(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, T
                                 ptr<uint8_t>(done), ptr<uint8_t>(trunc), (uint32_t)seed, (int)max_steps,
                                 ptr<uint16_t>(W1), ptr<float>(b1), ptr<uint16_t>(W2), ptr<float>(b2),
                                 ptr<uint16_t>(W3), ptr<float>(b3), ptr<uint16_t>(y1), ptr<uint16_t>(y2),
-                                ptr<uint16_t>(y3), (float)scale, so, N, cur_stream(state)),
+                                ptr<uint16_t>(y3), (float)scale, so, sn, tn, tgn, ern, stamps_ptr(stamps, sn ? 2 * N : N),
+                                N, cur_stream(state)),
         "pong_fused_env_step");
 }
 
@@ -1708,7 +1722,7 @@ TORCH_LIBRARY(acamd, m) {
         "Tensor value, int key_shift, int pseed, Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, "
         "Tensor env_ids, Tensor out, Tensor reward, Tensor done, Tensor truncated, int seed, int max_steps, "
         "Tensor hpart, int planes, Tensor bfc, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, "
-        "Tensor y1, Tensor y2, Tensor y3, float scale, Tensor? shift_out=None) -> ()");
+        "Tensor y1, Tensor y2, Tensor y3, float scale, Tensor? shift_out=None, Tensor[]? next_state=None, Tensor? stamps=None) -> ()");
   m.def("categorical_sample(Tensor logits, Tensor keys, int seed, Tensor act, Tensor logp, Tensor ent) -> ()");
   m.def("categorical_sample_env(Tensor logits, Tensor tg, Tensor env_ids, int key_shift, int seed, Tensor act, "
         "Tensor logp, Tensor ent, Tensor? vout) -> ()");

@@ -265,22 +265,49 @@ __device__ __forceinline__ void trunk_obs_dma(const uint8_t* __restrict__ src, u
 // converts the pixels to exact bf16 integers on the fly; same MFMA order and epilogues: bit-identical outputs.
 // The conv chain is a device function shared with the per-env fused rollout step (pong_fused_env_step_kernel).
 // ------------------------------------------------------------------------------------------------------------
-// conv1 -> conv2 -> conv3 of env e from its staged uint8 observation (s_obs8, complete behind a barrier); bw / bw2:
-// this wave's conv1 / conv2 weight fragments (already in registers), W3's are loaded after conv1.
+// Output rows computed / stored by part PART of an env's trunk: -1 the whole env (one workgroup per env), 0 / 1 the
+// two halves of the split rollout step (pong_fused_env_step_kernel<A1, 2>): conv3 rows [c3a, c3b), the conv2 / conv1 /
+// input rows of their receptive field (recomputed by both halves where they overlap), and the rows each half OWNS
+// (stores) -- every y1 / y2 row and every input row of the next observation has exactly one owner.
+template <int PART>
+struct EnvRows {
+  static constexpr int c3a = PART == 1 ? 4 : 0, c3b = PART == 0 ? 4 : 7;
+  static constexpr int c2a = c3a, c2b = c3b + 2;          // conv2 rows [c2a, c2b)
+  static constexpr int c1a = 2 * c2a, c1b = 2 * c2b + 2;  // conv1 rows [c1a, c1b)
+  static constexpr int ia = 4 * c1a, ib = 4 * c1b + 4;    // input rows [ia, ib)
+  static constexpr int o1a = PART == 1 ? 10 : 0, o1b = PART == 0 ? 10 : 20;   // owned y1 rows
+  static constexpr int o2a = PART == 1 ? 4 : 0, o2b = PART == 0 ? 4 : 9;      // owned y2 rows
+  static constexpr int oia = PART == 1 ? 40 : 0, oib = PART == 0 ? 40 : 84;   // owned input rows (16-byte aligned)
+  static constexpr int P1 = (c1b - c1a) * 20, T1 = (P1 + 15) / 16;   // conv1 positions / M tiles
+  static constexpr int P2 = (c2b - c2a) * 9, T2 = (P2 + 15) / 16;
+  static constexpr int P3 = (c3b - c3a) * 7, T3 = (P3 + 15) / 16;
+  static_assert(c1b <= 20 && ib <= 84 && oia * 84 % 16 == 0, "row ranges");
+};
+static_assert(EnvRows<-1>::P1 == 400 && EnvRows<-1>::P2 == 81 && EnvRows<-1>::P3 == 49, "whole env");
+static_assert(EnvRows<0>::T1 == 18 && EnvRows<1>::T1 == 15 && EnvRows<0>::ib == 60 && EnvRows<1>::ia == 32, "halves");
+constexpr int E1P_ELEMS = 14 * E1_W * Y1_LD;   // the y1 image of a half (at most 14 conv1 rows): 28 KB
+
+// conv1 -> conv2 -> conv3 of env e (part PART) from its staged uint8 observation (s_obs8, complete behind a barrier;
+// image rows are global, the y1 / y2 images hold the part's rows from c1a / c2a); bw / bw2: this wave's conv1 / conv2
+// weight fragments (already in registers), W3's are loaded after conv1. Every output's MFMA order is the same in
+// every part: the halves are bit-identical to the whole-env form.
+template <int PART>
 __device__ __forceinline__ void trunk_env_convs(const uint8_t* __restrict__ s_obs8, u16* __restrict__ s_y1,
                                                 u16* __restrict__ s_y2, int e, const bf16x8 (&bw)[2][8],
                                                 const bf16x8 (&bw2)[16], const u16* __restrict__ W3, float bias0,
                                                 float bias1, float bias2, float bias3, u16* __restrict__ y1g,
-                                                u16* __restrict__ y2g, u16* __restrict__ y3g, float scale) {
+                                                u16* __restrict__ y2g, u16* __restrict__ y3g, float scale,
+                                                uint64_t* __restrict__ stamps = nullptr) {
+  using R = EnvRows<PART>;
   constexpr int NW = 4;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l16 = lane & 15, lg = lane >> 4;
   const int n2 = wid * 16 + l16;
-  // ---------------------------------------------------------------- conv1: M 400 (25 tiles), N 32 (2), K 256 (8)
-  for (int mt = wid; mt < 25; mt += NW) {
+  // ---------------------------------------------------------------- conv1: M P1 (T1 tiles), N 32 (2), K 256 (8)
+  for (int mt = wid; mt < R::T1; mt += NW) {
     floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-    const int m = mt * 16 + l16;
-    const int oh = m / 20, ow = m - oh * 20;
+    const int m = min(mt * 16 + l16, R::P1 - 1);
+    const int oh = R::c1a + m / 20, ow = m % 20;   // global conv1 row
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) {
       const int k = ks * 32 + lg * 8;
@@ -294,91 +321,132 @@ __device__ __forceinline__ void trunk_env_convs(const uint8_t* __restrict__ s_ob
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int row = mt * 16 + lg * 4 + r;
-      const u16 v0 = f2bf(fmaxf(acc0[r] * scale + bias0, 0.f));
-      const u16 v1 = f2bf(fmaxf(acc1[r] * scale + bias1, 0.f));
-      const int px1 = (row / 20) * E1_W + row % 20;
-      s_y1[px1 * Y1_LD + l16] = v0;
-      s_y1[px1 * Y1_LD + 16 + l16] = v1;
-      y1g[((size_t)e * Y1_ROWS + row) * Y1_C + l16] = v0;
-      y1g[((size_t)e * Y1_ROWS + row) * Y1_C + 16 + l16] = v1;
+      const int row = mt * 16 + lg * 4 + r;   // local position
+      if (R::P1 % 16 == 0 || row < R::P1) {
+        const u16 v0 = f2bf(fmaxf(acc0[r] * scale + bias0, 0.f));
+        const u16 v1 = f2bf(fmaxf(acc1[r] * scale + bias1, 0.f));
+        const int lr = row / 20, col = row % 20;
+        const int px1 = lr * E1_W + col;
+        s_y1[px1 * Y1_LD + l16] = v0;
+        s_y1[px1 * Y1_LD + 16 + l16] = v1;
+        if (PART < 0 || (R::c1a + lr >= R::o1a && R::c1a + lr < R::o1b)) {
+          const size_t g = (size_t)e * Y1_ROWS + R::c1a * 20 + row;
+          y1g[g * Y1_C + l16] = v0;
+          y1g[g * Y1_C + 16 + l16] = v1;
+        }
+      }
     }
   }
   bf16x8 bw3[18];
 #pragma unroll
   for (int ks = 0; ks < 18; ++ks) bw3[ks] = *reinterpret_cast<const bf16x8*>(W3 + n2 * 576 + ks * 32 + lg * 8);
   __syncthreads();
-  // ---------------------------------------------------------------- conv2: M 81 (6 tiles), N 64 (wave = N tile), K 512
+  stamp(stamps, 5);
+  // ---------------------------------------------------------------- conv2: M P2 (T2 tiles), N 64 (wave = N tile), K 512
   {
-    floatx4 acc[6];
+    floatx4 acc[R::T2];
 #pragma unroll
-    for (int mt = 0; mt < 6; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int mt = 0; mt < R::T2; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < 16; ++ks) {
       const int k = ks * 32 + lg * 8;
       const int i = k >> 7, j = (k >> 5) & 3, c0 = k & 31;
 #pragma unroll
-      for (int mt = 0; mt < 6; ++mt) {
-        const int m = min(mt * 16 + l16, Y2_ROWS - 1);
-        const int oh = m / 9, ow = m - oh * 9;
+      for (int mt = 0; mt < R::T2; ++mt) {
+        const int m = min(mt * 16 + l16, R::P2 - 1);
+        const int oh = m / 9, ow = m - oh * 9;   // local conv2 row (its y1 rows start at local 2 * oh)
         const bf16x8 a = *reinterpret_cast<const bf16x8*>(s_y1 + ((oh * 2 + i) * E1_W + ow * 2 + j) * Y1_LD + c0);
         acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw2[ks], acc[mt], 0, 0, 0);
       }
     }
 #pragma unroll
-    for (int mt = 0; mt < 6; ++mt) {
+    for (int mt = 0; mt < R::T2; ++mt) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = mt * 16 + lg * 4 + r;
-        if (row < Y2_ROWS) {
+        if (row < R::P2) {
           const u16 v = f2bf(fmaxf(acc[mt][r] + bias2, 0.f));
-          s_y2[((row / 9) * E2_W + row % 9) * Y2_LD + n2] = v;
-          y2g[((size_t)e * Y2_ROWS + row) * Y2_C + n2] = v;
+          const int lr = row / 9;
+          s_y2[(lr * E2_W + row % 9) * Y2_LD + n2] = v;
+          if (PART < 0 || (R::c2a + lr >= R::o2a && R::c2a + lr < R::o2b))
+            y2g[((size_t)e * Y2_ROWS + R::c2a * 9 + row) * Y2_C + n2] = v;
         }
       }
     }
   }
   __syncthreads();
-  // ---------------------------------------------------------------- conv3: M 49 (4 tiles), N 64 (wave = N tile), K 576
+  stamp(stamps, 6);
+  // ---------------------------------------------------------------- conv3: M P3 (T3 tiles), N 64 (wave = N tile), K 576
   {
-    floatx4 acc[4];
+    floatx4 acc[R::T3];
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int mt = 0; mt < R::T3; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < 18; ++ks) {
       const int k = ks * 32 + lg * 8;
       const int i = k / 192, j = (k >> 6) % 3, c0 = k & 63;
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        const int m = min(mt * 16 + l16, Y3_ROWS - 1);
-        const int oh = m / 7, ow = m - oh * 7;
+      for (int mt = 0; mt < R::T3; ++mt) {
+        const int m = min(mt * 16 + l16, R::P3 - 1);
+        const int oh = m / 7, ow = m - oh * 7;   // local conv3 row = local y2 row
         const bf16x8 a = *reinterpret_cast<const bf16x8*>(s_y2 + ((oh + i) * E2_W + ow + j) * Y2_LD + c0);
         acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw3[ks], acc[mt], 0, 0, 0);
       }
     }
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
+    for (int mt = 0; mt < R::T3; ++mt) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = mt * 16 + lg * 4 + r;
-        if (row < Y3_ROWS) y3g[((size_t)e * Y3_ROWS + row) * Y3_C + n2] = f2bf(fmaxf(acc[mt][r] + bias3, 0.f));
+        if (row < R::P3)
+          y3g[((size_t)e * Y3_ROWS + R::c3a * 7 + row) * Y3_C + n2] = f2bf(fmaxf(acc[mt][r] + bias3, 0.f));
       }
     }
   }
+  stamp(stamps, 7);
+}
+
+// W1 [32][256] bf16 (16 KB) copied global -> LDS by the LDS-DMA path, each 512-byte row's 16-byte chunks
+// XOR-swizzled by (row & 15) so the fragment reads (16 rows at one column per lane group) are conflict-free; lane i
+// of a wave copy lands at base + 16 i, so the swizzle is applied to the SOURCE chunk it fetches.
+__device__ __forceinline__ void w1_lds_dma(const u16* __restrict__ W1, u16* dst_lds) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int blk = wid; blk < 16; blk += nw) {
+    const int q = blk * 64 + lane, row = q >> 5, lc = (q & 31) ^ (row & 15);
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint4*>(W1) + row * 32 + lc,
+                                     (__attribute__((address_space(3))) void*)(dst_lds + blk * 512), 16, 0, 0);
+  }
+}
+__device__ __forceinline__ void w1_frags_from_lds(const u16* __restrict__ s_w, bf16x8 (&bw)[2][8]) {
+  const int lane = threadIdx.x & 63, l16 = lane & 15, lg = lane >> 4;
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      const int row = nt * 16 + l16, pc = (ks * 4 + lg) ^ (row & 15);
+      bw[nt][ks] = *reinterpret_cast<const bf16x8*>(s_w + row * 256 + pc * 8);
+    }
 }
 
 // conv1 / conv2 weight fragments of this wave (output-channel tile wid for conv2)
-__device__ __forceinline__ void trunk_env_w12(const u16* __restrict__ W1, const u16* __restrict__ W2,
-                                              bf16x8 (&bw)[2][8], bf16x8 (&bw2)[16]) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, l16 = lane & 15, lg = lane >> 4;
-  const int n2 = wid * 16 + l16;
+__device__ __forceinline__ void trunk_env_w1(const u16* __restrict__ W1, bf16x8 (&bw)[2][8]) {
+  const int lane = threadIdx.x & 63, l16 = lane & 15, lg = lane >> 4;
 #pragma unroll
   for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks)
       bw[nt][ks] = *reinterpret_cast<const bf16x8*>(W1 + (nt * 16 + l16) * 256 + ks * 32 + lg * 8);
+}
+__device__ __forceinline__ void trunk_env_w2(const u16* __restrict__ W2, bf16x8 (&bw2)[16]) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, l16 = lane & 15, lg = lane >> 4;
+  const int n2 = wid * 16 + l16;
 #pragma unroll
   for (int ks = 0; ks < 16; ++ks) bw2[ks] = *reinterpret_cast<const bf16x8*>(W2 + n2 * 512 + ks * 32 + lg * 8);
+}
+__device__ __forceinline__ void trunk_env_w12(const u16* __restrict__ W1, const u16* __restrict__ W2,
+                                              bf16x8 (&bw)[2][8], bf16x8 (&bw2)[16]) {
+  trunk_env_w1(W1, bw);
+  trunk_env_w2(W2, bw2);
 }
 
 __global__ void __launch_bounds__(256) cnn_trunk_fwd_u8_kernel(
@@ -407,7 +475,7 @@ __global__ void __launch_bounds__(256) cnn_trunk_fwd_u8_kernel(
     const uint4* si = reinterpret_cast<const uint4*>(s_obs8);
     for (int i = OBS_BYTES / 64 + tid; i < OBS_BYTES / 16; i += 256) so[i - OBS_BYTES / 64] = si[i];
   }
-  trunk_env_convs(s_obs8, s_y1, s_y2, e, bw, bw2, W3, bias0, bias1, bias2, bias3, y1g, y2g, y3g, scale);
+  trunk_env_convs<-1>(s_obs8, s_y1, s_y2, e, bw, bw2, W3, bias0, bias1, bias2, bias3, y1g, y2g, y3g, scale);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -900,38 +968,48 @@ __global__ void __launch_bounds__(T_THREADS) pong_fused_step_kernel(
 // One launch instead of the trunk kernel + the policy/env kernel of the unfused step, and the new frame never makes a
 // global round trip before conv1.
 // ------------------------------------------------------------------------------------------------------------
-template <int A1>
-__global__ void __launch_bounds__(256) pong_fused_env_step_kernel(
-    PongIO io, FcParts fc, u16* __restrict__ h, const u16* __restrict__ Wh, const float* __restrict__ bh,
-    float* __restrict__ z_out, int32_t* __restrict__ act, float* __restrict__ logp, float* __restrict__ ent,
-    float* __restrict__ vout, int key_shift, uint32_t pseed, const u16* __restrict__ W1,
-    const float* __restrict__ b1, const u16* __restrict__ W2, const float* __restrict__ b2,
-    const u16* __restrict__ W3, const float* __restrict__ b3, u16* __restrict__ y1g, u16* __restrict__ y2g,
-    u16* __restrict__ y3g, float scale, uint8_t* __restrict__ shift_out) {
+// The body of one (env, part) workgroup; PART -1: the whole env (one workgroup per env, commits into io), 0 / 1:
+// the halves of the split step (two workgroups per env: at 128 envs the whole-env form leaves half the CUs idle
+// for the ~22 us of the step). Both halves evaluate the head, sampling and physics redundantly (bit-identical inputs
+// and maths, so the same action), half 0 alone writes the step's outputs and commits the env state into the other
+// parity (nx: the halves read the current one), each half renders the input rows it needs and stores the rows it
+// owns, and runs the conv chain of its rows (trunk_env_convs<PART>).
+template <int A1, int PART>
+__device__ __forceinline__ void env_step_body(
+    uint8_t* __restrict__ s_obs8, u16* __restrict__ s_y1, float (*s_acc)[A1], PongOut* cand, int* sh_act,
+    const PongIO& io, const PongNext& nx, const FcParts& fc, int e, u16* __restrict__ h,
+    const u16* __restrict__ Wh, const float* __restrict__ bh, float* __restrict__ z_out, int32_t* __restrict__ act,
+    float* __restrict__ logp, float* __restrict__ ent, float* __restrict__ vout, int key_shift, uint32_t pseed,
+    const u16* __restrict__ W1, const float* __restrict__ b1, const u16* __restrict__ W2,
+    const float* __restrict__ b2, const u16* __restrict__ W3, const float* __restrict__ b3, u16* __restrict__ y1g,
+    u16* __restrict__ y2g, u16* __restrict__ y3g, float scale, uint8_t* __restrict__ shift_out,
+    uint64_t* __restrict__ stamps) {
+  using R = EnvRows<PART>;
   constexpr int A = A1 - 1;
-  __shared__ __attribute__((aligned(16))) uint8_t s_obs8[TP_OBS_PAD];   // later the y2 image
-  __shared__ __attribute__((aligned(16))) u16 s_y1[E1_ELEMS];
+  constexpr bool lead = PART <= 0;
   u16* const s_y2 = reinterpret_cast<u16*>(s_obs8);
-  __shared__ float s_acc[4][A1];
-  __shared__ PongOut cand[3];
-  __shared__ int sh_act;
-  const int e = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, l16 = lane & 15;
   const int n2 = wid * 16 + l16;
-  // ---------------------------------------------------------------- every independent operand requested first
-  trunk_obs_dma(io.out + (size_t)e * OBS_BYTES, s_obs8);   // obs t+1: frames 0..2 valid, frame 3 rendered below
+  stamp(stamps, 0);
+  // ---------------------------------------------------------------- loads, in the order they are needed (the vm
+  // counter retires in issue order): the head's operands (Wh rows, fc planes of obs t, env state), then the next
+  // observation's frames (LDS-DMA: frames 0..2 were shifted in by the previous launch) and the conv1 fragments;
+  // the conv2 fragments after the render (they land while conv1 runs), conv3's after conv1
   const int64_t tg0 = io.tglob[e], id0 = io.env_ids[e];
   const float bhj = bh[lane < A1 ? lane : 0];
   uint32_t wv[A1];   // this thread's two Wh rows
 #pragma unroll
   for (int u = 0; u < A1; ++u) wv[u] = reinterpret_cast<const uint32_t*>(Wh)[A1 * tid + u];
+  FcH2<16> fch;
+  fch.issue(fc.hpart, fc.S, fc.plane_stride, fc.bfc, e, tid);
+  if (tid >= 64 && tid < 67) cand[tid - 64] = pong_advance(io, e, (float)(tid - 65));
+  trunk_obs_dma(io.out + (size_t)e * OBS_BYTES, s_obs8);   // obs t+1: frames 0..2 valid, frame 3 rendered below
+  w1_lds_dma(W1, s_y1);   // W1 once per workgroup (16 KB; the y1 image is written only from conv1's epilogue on)
   bf16x8 bw[2][8], bw2[16];
-  trunk_env_w12(W1, W2, bw, bw2);
   const float bias0 = b1[l16], bias1 = b1[16 + l16], bias2 = b2[n2], bias3 = b3[n2];
   // ---------------------------------------------------------------- policy head of obs t
   float hf[2];
-  fc_h2_from_parts(fc.hpart, fc.S, fc.plane_stride, fc.bfc, e, tid, h, hf);
-  if (tid >= 64 && tid < 67) cand[tid - 64] = pong_advance(io, e, (float)(tid - 65));
+  fch.finish(fc.hpart, fc.S, fc.plane_stride, e, tid, lead ? h : nullptr, hf);
   float accj[A1];
 #pragma unroll
   for (int j = 0; j < A1; ++j) {
@@ -943,13 +1021,13 @@ __global__ void __launch_bounds__(256) pong_fused_env_step_kernel(
   if (lane == 0)
 #pragma unroll
     for (int j = 0; j < A1; ++j) s_acc[wid][j] = accj[j];
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the staged frames have landed (and every fragment)
   __syncthreads();
+  stamp(stamps, 1);
   if (wid == 0) {
     const int64_t key = tg0 * ((int64_t)1 << key_shift) + id0;   // pre-step counter
     const int jj = lane < A1 ? lane : 0;
     const float zj = ((s_acc[0][jj] + s_acc[1][jj]) + (s_acc[2][jj] + s_acc[3][jj])) + bhj;
-    if (lane < A1) z_out[(size_t)e * A1 + lane] = zj;
+    if (lead && lane < A1) z_out[(size_t)e * A1 + lane] = zj;
     const float value = __shfl(zj, A, 64);
     const bool on = lane < A;
     const float z = on ? zj : -INFINITY;
@@ -970,43 +1048,99 @@ __global__ void __launch_bounds__(256) pong_fused_env_step_kernel(
     }
     const float lpa = __shfl(lp, bi, 64);
     if (lane == 0) {
-      act[e] = bi;
-      logp[e] = lpa;
-      ent[e] = H;
-      vout[e] = value;
-      sh_act = bi;
+      if (lead) {
+        act[e] = bi;
+        logp[e] = lpa;
+        ent[e] = H;
+        vout[e] = value;
+      }
+      *sh_act = bi;
     }
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the staged frames and W1 have landed
   __syncthreads();
-  const PongOut& res = cand[pong_dir_index(sh_act)];
+  stamp(stamps, 2);
+  w1_frags_from_lds(s_y1, bw);   // read before the next barrier: conv1's epilogue overwrites them
+  const PongOut& res = cand[pong_dir_index(*sh_act)];
   const bool done = res.done != 0;
-  if (tid == 0) pong_commit(io, e, res, tg0);
-  // ---------------------------------------------------------------- the new frame: staged image + obs t+1 in memory
+  if (tid == 0) {
+    if constexpr (PART < 0) pong_commit(io, e, res, tg0);
+    else if constexpr (PART == 0) pong_commit_next(io, nx, e, res, tg0);
+  }
+  // ---------------------------------------------------------------- the new frame: the part's rows of the staged
+  // image (all 4 frames after an episode restart), its owned rows of obs t+1 in memory
   {
     constexpr int WPR = PW / 4, NWORDS = PH * WPR;   // 21, 1764
     const PongGeom gm = pong_geom(res.s);
     uint32_t* ob = reinterpret_cast<uint32_t*>(io.out + (size_t)e * OBS_BYTES);
     uint32_t* sw = reinterpret_cast<uint32_t*>(s_obs8);
-    for (int w = tid; w < NWORDS; w += 256) {
+    for (int w = R::ia * WPR + tid; w < R::ib * WPR; w += 256) {
       const int y = w / WPR, x0 = (w - y * WPR) * 4;
       const uint32_t word = pong_word(gm, y, x0);
+      const bool own = PART < 0 || (y >= R::oia && y < R::oib);
       sw[3 * NWORDS + w] = word;
-      ob[3 * NWORDS + w] = word;
+      if (own) ob[3 * NWORDS + w] = word;
       if (done)
 #pragma unroll
         for (int f = 0; f < 3; ++f) {
           sw[f * NWORDS + w] = word;
-          ob[f * NWORDS + w] = word;
+          if (own) ob[f * NWORDS + w] = word;
         }
     }
   }
   __syncthreads();
-  if (shift_out) {   // frames 1..3 of obs t+1 become frames 0..2 of obs t+2
+  stamp(stamps, 3);
+  if (shift_out) {   // frames 1..3 of obs t+1 become frames 0..2 of obs t+2 (the owned rows of each frame)
     uint4* so = reinterpret_cast<uint4*>(shift_out + (size_t)e * OBS_BYTES);
     const uint4* si = reinterpret_cast<const uint4*>(s_obs8);
-    for (int i = OBS_BYTES / 64 + tid; i < OBS_BYTES / 16; i += 256) so[i - OBS_BYTES / 64] = si[i];
+    constexpr int FC = FRAME / 16, C0 = R::oia * 84 / 16, NC = (R::oib - R::oia) * 84 / 16;   // chunks
+    for (int i = tid; i < 3 * NC; i += 256) {
+      const int f = i / NC, c = C0 + i - f * NC;
+      so[f * FC + c] = si[(f + 1) * FC + c];
+    }
   }
-  trunk_env_convs(s_obs8, s_y1, s_y2, e, bw, bw2, W3, bias0, bias1, bias2, bias3, y1g, y2g, y3g, scale);
+  trunk_env_w2(W2, bw2);
+  stamp(stamps, 4);
+  trunk_env_convs<PART>(s_obs8, s_y1, s_y2, e, bw, bw2, W3, bias0, bias1, bias2, bias3, y1g, y2g, y3g, scale,
+                        stamps);
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// Rollout step t fused with the trunk of step t + 1, per-env layout (the large banks, Breakout-shape PPO at 128
+// envs, where 7 row workgroups per env would not fit the chip in one wave): SPLIT 1 -- one workgroup per env,
+// SPLIT 2 -- two per env (env_step_body PART 0 / 1; the env state alternates parity slots as in the row-split step):
+//   every load first -- the next observation's frames (LDS-DMA: frames 0..2 were shifted in by the previous launch),
+//   the conv1 / conv2 weight fragments, the head's Wh rows, the fc partial planes of obs t --; then h (planes summed
+//   in order + bias + ReLU), the policy/value head, Gumbel-max sampling, the env physics (all three paddle directions
+//   evaluated while the head runs) and the commit; the new frame is rendered straight into the staged uint8 image
+//   (all 4 frames after an episode restart) and to obs t+1 in memory; frames 1..3 of obs t+1 go to obs t+2 (shift);
+//   then conv1 -> conv3 of obs t+1 (trunk_env_convs, bit-identical to the per-env trunk kernel).
+// One launch instead of the trunk kernel + the policy/env kernel of the unfused step, and the new frame never makes a
+// global round trip before conv1.
+// ------------------------------------------------------------------------------------------------------------
+template <int A1, int SPLIT>
+__global__ void __launch_bounds__(256) pong_fused_env_step_kernel(
+    PongIO io, PongNext nx, FcParts fc, u16* __restrict__ h, const u16* __restrict__ Wh, const float* __restrict__ bh,
+    float* __restrict__ z_out, int32_t* __restrict__ act, float* __restrict__ logp, float* __restrict__ ent,
+    float* __restrict__ vout, int key_shift, uint32_t pseed, const u16* __restrict__ W1,
+    const float* __restrict__ b1, const u16* __restrict__ W2, const float* __restrict__ b2,
+    const u16* __restrict__ W3, const float* __restrict__ b3, u16* __restrict__ y1g, u16* __restrict__ y2g,
+    u16* __restrict__ y3g, float scale, uint8_t* __restrict__ shift_out, uint64_t* __restrict__ stamps) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_obs8[TP_OBS_PAD];   // later the y2 image
+  __shared__ __attribute__((aligned(16))) u16 s_y1[SPLIT == 1 ? E1_ELEMS : E1P_ELEMS];
+  __shared__ float s_acc[4][A1];
+  __shared__ PongOut cand[3];
+  __shared__ int sh_act;
+#define ACA_ENV_BODY(PART, E)                                                                                    \
+  env_step_body<A1, PART>(s_obs8, s_y1, s_acc, cand, &sh_act, io, nx, fc, E, h, Wh, bh, z_out, act, logp, ent,    \
+                          vout, key_shift, pseed, W1, b1, W2, b2, W3, b3, y1g, y2g, y3g, scale, shift_out, stamps)
+  if constexpr (SPLIT == 1) {
+    ACA_ENV_BODY(-1, blockIdx.x);
+  } else {
+    if (blockIdx.x & 1) ACA_ENV_BODY(1, blockIdx.x >> 1);
+    else ACA_ENV_BODY(0, blockIdx.x >> 1);
+  }
+#undef ACA_ENV_BODY
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -1686,9 +1820,14 @@ extern "C" hipError_t aca_pong_fused_env_step(
     uint32_t pseed, float* state, int32_t* t, int64_t* tg, float* ep_ret, float* ep_stats, const int64_t* ids,
     uint8_t* out, float* reward, uint8_t* done, uint8_t* trunc, uint32_t seed, int max_steps, const uint16_t* W1,
     const float* b1, const uint16_t* W2, const float* b2, const uint16_t* W3, const float* b3, uint16_t* y1,
-    uint16_t* y2, uint16_t* y3, float scale, uint8_t* shift_out, int N, hipStream_t stream) {
+    uint16_t* y2, uint16_t* y3, float scale, uint8_t* shift_out, float* state_n, int32_t* t_n, int64_t* tg_n,
+    float* ep_ret_n, uint64_t* stamps, int N, hipStream_t stream) {
+  // state_n .. ep_ret_n: the other parity's env state -> two workgroups per env (commit there); null -> one
   if (N <= 0) return hipSuccess;
   if (S < 1 || S > aca::FC_MAX_PLANES) return hipErrorInvalidValue;
+  const bool split = state_n != nullptr;
+  if (split && (!t_n || !tg_n || !ep_ret_n)) return hipErrorInvalidValue;
+  aca::PongNext nx{state_n, t_n, tg_n, ep_ret_n};
   aca::PongIO io;
   io.state = state; io.tsteps = t; io.tglob = tg; io.ep_ret = ep_ret; io.ep_stats = ep_stats; io.env_ids = ids;
   io.prev = out; io.out = out; io.reward = reward; io.done_out = done; io.trunc_out = trunc; io.seed = seed;
@@ -1697,9 +1836,14 @@ extern "C" hipError_t aca_pong_fused_env_step(
   switch (A + 1) {
 #define ACA_FES_CASE(A1)                                                                                         \
   case A1:                                                                                                       \
-    aca::pong_fused_env_step_kernel<A1><<<N, 256, 0, stream>>>(io, fc, h, Wh, bh, z, act, logp, ent, value,     \
-                                                               key_shift, pseed, W1, b1, W2, b2, W3, b3, y1, y2, \
-                                                               y3, scale, shift_out);                            \
+    if (split)                                                                                                   \
+      aca::pong_fused_env_step_kernel<A1, 2><<<2 * N, 256, 0, stream>>>(                                         \
+          io, nx, fc, h, Wh, bh, z, act, logp, ent, value, key_shift, pseed, W1, b1, W2, b2, W3, b3, y1, y2, y3,  \
+          scale, shift_out, stamps);                                                                             \
+    else                                                                                                         \
+      aca::pong_fused_env_step_kernel<A1, 1><<<N, 256, 0, stream>>>(                                             \
+          io, nx, fc, h, Wh, bh, z, act, logp, ent, value, key_shift, pseed, W1, b1, W2, b2, W3, b3, y1, y2, y3,  \
+          scale, shift_out, stamps);                                                                             \
     break;
     ACA_FES_CASE(3) ACA_FES_CASE(4) ACA_FES_CASE(5) ACA_FES_CASE(6) ACA_FES_CASE(7)
 #undef ACA_FES_CASE

@@ -117,15 +117,18 @@ def test_fused_env_step_equals_separate_trunk_and_policy(cuda, preset_name, capt
     """Large banks (72 envs > the row-split limit): the per-env fused rollout step (pong_fused_env_step: policy/env
     step t + render + shift + the trunk of obs t+1 in one launch) reproduces the separate per-env trunk + policy/env
     launches bit for bit -- parameters, rollout tensors and env state over several updates with episode
-    truncations, A2C (learner reuses the rollout activations) and PPO, graph-captured or eager."""
+    truncations, A2C (learner reuses the rollout activations) and PPO, graph-captured or eager -- in both its forms:
+    two workgroups per env (the conv rows split in halves, the env state alternating parity slots; T = 5 leaves the
+    parity flipped at every update) and one."""
     monkeypatch.setattr("actor_critic_algs_on_tensorflow_amd.ops.gemm.TUNE", False)
     from actor_critic_algs_on_tensorflow_amd import preset
     from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
     runs = []
-    for fused in (True, False):
+    for fused, split in ((True, True), (True, False), (False, False)):
         kw = dict(n_steps=5) if preset_name == "pong_a2c" else dict(n_steps=8, ppo_epochs=1, ppo_minibatches=2)
         tr = ActorCriticTrainer(preset(preset_name, num_envs=72, device="cuda:0", outdir=None, quiet=True,
-                                       stdout_freq=0, save_every=0, seed=5, engine_opts=dict(fused_step=fused), **kw))
+                                       stdout_freq=0, save_every=0, seed=5,
+                                       engine_opts=dict(fused_step=fused, fused_env_split=split), **kw))
         assert tr.engine.fused_env_step_ok(72) == fused
         tr.env.max_episode_steps = 7
         if capture:
@@ -141,9 +144,10 @@ def test_fused_env_step_equals_separate_trunk_and_policy(cuda, preset_name, capt
                           tr.env.t.clone(), tr.env.tg.clone(), tr.env.ep_ret.clone(), tr.env.ep_stats.clone()])
         torch.cuda.synchronize()
         runs.append(snaps)
-    for k, (a, b) in enumerate(zip(*runs)):
-        for j, (x, y) in enumerate(zip(a, b)):
-            assert torch.equal(x, y), (k, j)
+    for other in runs[1:]:
+        for k, (a, b) in enumerate(zip(runs[0], other)):
+            for j, (x, y) in enumerate(zip(a, b)):
+                assert torch.equal(x, y), (k, j)
 
 
 @pytest.mark.parametrize("a_k,b_k,M,N,K,out_mode,epi,splits", [

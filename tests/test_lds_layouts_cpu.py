@@ -200,3 +200,26 @@ def test_per_env_trunk_forward_reads_are_conflict_free():
                 oh, ow = m // 7, m % 7
                 addr.append((((oh + i) * e2_w + ow + j) * y2_ld + c0) * 2)
             assert cycles([[addr[l] for l in g] for g in G128], 4, 64) == 4, ("conv3", ks, mt)
+
+
+def test_w1_lds_image_is_a_permutation_and_fragment_reads_are_conflict_free():
+    """w1_lds_dma / w1_frags_from_lds (cnn_fused.hip, the fused rollout step): W1's 16-byte chunks land XOR-swizzled
+    by (row & 15) -- every chunk exactly once -- and the conv1 fragment reads (16 rows at one column per lane group)
+    take one LDS cycle per group."""
+    src = open(CNN).read()
+    assert "lc = (q & 31) ^ (row & 15);" in src and "pc = (ks * 4 + lg) ^ (row & 15);" in src
+    placed = {}
+    for q in range(1024):                 # LDS chunk q <- source chunk row * 32 + lc
+        row, lc = q >> 5, (q & 31) ^ ((q >> 5) & 15)
+        placed[row * 32 + lc] = q
+    assert sorted(placed) == list(range(1024))
+    for nt in range(2):
+        for ks in range(8):
+            addr = []
+            for lane in range(64):
+                l16, lg = lane & 15, lane >> 4
+                row = nt * 16 + l16
+                pc = (ks * 4 + lg) ^ (row & 15)
+                assert placed[row * 32 + ks * 4 + lg] == row * 32 + pc
+                addr.append((row * 256 + pc * 8) * 2)
+            assert cycles([[addr[l] for l in g] for g in G128], 4, 64) == 4, (nt, ks)

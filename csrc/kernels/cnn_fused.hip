@@ -257,6 +257,24 @@ __device__ __forceinline__ void trunk_obs_dma(const uint8_t* __restrict__ src, u
   }
 }
 
+// Frames 0..2, input rows [IA, IB) of one observation to the same offsets of the LDS image (the rollout step renders
+// frame 3 itself): per frame ceil((IB - IA) * 84 / 1024) wave copies, the lanes past a frame's range masked off
+// (their slots would be the next frame's first rows).
+template <int IA, int IB>
+__device__ __forceinline__ void obs_rows_dma(const uint8_t* __restrict__ src, uint8_t* dst_lds) {
+  constexpr int NCH = (IB - IA) * 84 / 16, NCOPY = (NCH + 63) / 64, C0 = IA * 84 / 16;
+  static_assert(IA * 84 % 16 == 0 && (IB - IA) * 84 % 16 == 0, "16-byte rows ranges");
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int k = wid; k < 3 * NCOPY; k += nw) {
+    const int f = k / NCOPY, blk = k - f * NCOPY;
+    const int c = f * (FRAME / 16) + C0 + blk * 64 + lane;
+    uint8_t* base = dst_lds + f * FRAME + IA * 84 + blk * 1024;
+    if (blk * 64 + lane < NCH)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint4*>(src) + c,
+                                       (__attribute__((address_space(3))) void*)(base), 16, 0, 0);
+  }
+}
+
 // ------------------------------------------------------------------------------------------------------------
 // Per-env trunk, lean-LDS form: the observation is staged as its uint8 bytes by LDS-DMA (28 KB instead of 56 KB of
 // bf16, no staging registers) and the conv1 weight fragments come straight from L2 into registers (no 17 KB W1
@@ -271,7 +289,7 @@ __device__ __forceinline__ void trunk_obs_dma(const uint8_t* __restrict__ src, u
 // (stores) -- every y1 / y2 row and every input row of the next observation has exactly one owner.
 template <int PART>
 struct EnvRows {
-  static constexpr int c3a = PART == 1 ? 4 : 0, c3b = PART == 0 ? 4 : 7;
+  static constexpr int c3a = PART == 1 ? 3 : 0, c3b = PART == 0 ? 3 : 7;   // half 0 (it also commits) the smaller
   static constexpr int c2a = c3a, c2b = c3b + 2;          // conv2 rows [c2a, c2b)
   static constexpr int c1a = 2 * c2a, c1b = 2 * c2b + 2;  // conv1 rows [c1a, c1b)
   static constexpr int ia = 4 * c1a, ib = 4 * c1b + 4;    // input rows [ia, ib)
@@ -284,7 +302,10 @@ struct EnvRows {
   static_assert(c1b <= 20 && ib <= 84 && oia * 84 % 16 == 0, "row ranges");
 };
 static_assert(EnvRows<-1>::P1 == 400 && EnvRows<-1>::P2 == 81 && EnvRows<-1>::P3 == 49, "whole env");
-static_assert(EnvRows<0>::T1 == 18 && EnvRows<1>::T1 == 15 && EnvRows<0>::ib == 60 && EnvRows<1>::ia == 32, "halves");
+static_assert(EnvRows<0>::T1 == 15 && EnvRows<1>::T1 == 18 && EnvRows<0>::ib == 52 && EnvRows<1>::ia == 24 &&
+              EnvRows<0>::c1b >= EnvRows<0>::o1b && EnvRows<1>::c1a <= EnvRows<1>::o1a &&
+              EnvRows<0>::c2b >= EnvRows<0>::o2b && EnvRows<1>::c2a <= EnvRows<1>::o2a &&
+              EnvRows<0>::ib >= EnvRows<0>::oib && EnvRows<1>::ia <= EnvRows<1>::oia, "halves own what they compute");
 constexpr int E1P_ELEMS = 14 * E1_W * Y1_LD;   // the y1 image of a half (at most 14 conv1 rows): 28 KB
 
 // conv1 -> conv2 -> conv3 of env e (part PART) from its staged uint8 observation (s_obs8, complete behind a barrier;
@@ -995,6 +1016,9 @@ __device__ __forceinline__ void env_step_body(
   // counter retires in issue order): the head's operands (Wh rows, fc planes of obs t, env state), then the next
   // observation's frames (LDS-DMA: frames 0..2 were shifted in by the previous launch) and the conv1 fragments;
   // the conv2 fragments after the render (they land while conv1 runs), conv3's after conv1
+  const bool phys = tid >= 64 && tid < 67;   // the three paddle directions' physics candidates
+  PongIn pin;
+  if (phys) pin = pong_load(io, e);
   const int64_t tg0 = io.tglob[e], id0 = io.env_ids[e];
   const float bhj = bh[lane < A1 ? lane : 0];
   uint32_t wv[A1];   // this thread's two Wh rows
@@ -1002,14 +1026,16 @@ __device__ __forceinline__ void env_step_body(
   for (int u = 0; u < A1; ++u) wv[u] = reinterpret_cast<const uint32_t*>(Wh)[A1 * tid + u];
   FcH2<16> fch;
   fch.issue(fc.hpart, fc.S, fc.plane_stride, fc.bfc, e, tid);
-  if (tid >= 64 && tid < 67) cand[tid - 64] = pong_advance(io, e, (float)(tid - 65));
-  trunk_obs_dma(io.out + (size_t)e * OBS_BYTES, s_obs8);   // obs t+1: frames 0..2 valid, frame 3 rendered below
+  obs_rows_dma<R::ia, R::ib>(io.out + (size_t)e * OBS_BYTES, s_obs8);   // obs t+1 frames 0..2 (3 is rendered)
   w1_lds_dma(W1, s_y1);   // W1 once per workgroup (16 KB; the y1 image is written only from conv1's epilogue on)
   bf16x8 bw[2][8], bw2[16];
   const float bias0 = b1[l16], bias1 = b1[16 + l16], bias2 = b2[n2], bias3 = b3[n2];
+  if (phys) cand[tid - 64] = pong_advance_in(io, pin, (float)(tid - 65));
+  if (stamps && tid == 64) stamps[(size_t)blockIdx.x * 16 + 10] = __builtin_amdgcn_s_memrealtime();
   // ---------------------------------------------------------------- policy head of obs t
   float hf[2];
   fch.finish(fc.hpart, fc.S, fc.plane_stride, e, tid, lead ? h : nullptr, hf);
+  stamp(stamps, 8);
   float accj[A1];
 #pragma unroll
   for (int j = 0; j < A1; ++j) {
@@ -1021,8 +1047,11 @@ __device__ __forceinline__ void env_step_body(
   if (lane == 0)
 #pragma unroll
     for (int j = 0; j < A1; ++j) s_acc[wid][j] = accj[j];
+  stamp(stamps, 9);
   __syncthreads();
   stamp(stamps, 1);
+  // the staged frames and W1 have landed (waited for before the sampling wave's output stores join the vm counter)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (wid == 0) {
     const int64_t key = tg0 * ((int64_t)1 << key_shift) + id0;   // pre-step counter
     const int jj = lane < A1 ? lane : 0;
@@ -1057,10 +1086,10 @@ __device__ __forceinline__ void env_step_body(
       *sh_act = bi;
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the staged frames and W1 have landed
   __syncthreads();
   stamp(stamps, 2);
   w1_frags_from_lds(s_y1, bw);   // read before the next barrier: conv1's epilogue overwrites them
+  trunk_env_w2(W2, bw2);         // lands during the render and conv1
   const PongOut& res = cand[pong_dir_index(*sh_act)];
   const bool done = res.done != 0;
   if (tid == 0) {
@@ -1099,7 +1128,6 @@ __device__ __forceinline__ void env_step_body(
       so[f * FC + c] = si[(f + 1) * FC + c];
     }
   }
-  trunk_env_w2(W2, bw2);
   stamp(stamps, 4);
   trunk_env_convs<PART>(s_obs8, s_y1, s_y2, e, bw, bw2, W3, bias0, bias1, bias2, bias3, y1g, y2g, y3g, scale,
                         stamps);

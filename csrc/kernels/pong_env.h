@@ -52,12 +52,27 @@ __device__ __forceinline__ int pong_dir_index(int a) {  // 0: up, 1: stay, 2: do
   return (a == 2 || a == 4) ? 0 : ((a == 3 || a == 5) ? 2 : 1);
 }
 
-__device__ __forceinline__ PongOut pong_advance(const PongIO& io, int e, float dirn) {
-#pragma clang fp contract(off)   // rounds exactly like the PyTorch oracle, whatever the including file's flags
+// The env's state as advance reads it: loaded by pong_load so that a kernel can request it before its other loads and
+// run the physics later (pong_advance_in), without a round trip in between.
+struct PongIn {
+  PongState s;
+  int64_t tg;
+  int64_t id;
+  int32_t t;
+  float ep_ret;
+};
+
+__device__ __forceinline__ PongIn pong_load(const PongIO& io, int e) {
   const float* sp = io.state + (size_t)e * 8;
-  PongState s{sp[0], sp[1], sp[2], sp[3], sp[4], sp[5], sp[6], sp[7]};
-  const int64_t tg = io.tglob[e] + 1;
-  const uint32_t id = (uint32_t)io.env_ids[e], st = (uint32_t)tg;
+  return PongIn{PongState{sp[0], sp[1], sp[2], sp[3], sp[4], sp[5], sp[6], sp[7]}, io.tglob[e], io.env_ids[e],
+                io.tsteps[e], io.ep_ret[e]};
+}
+
+__device__ __forceinline__ PongOut pong_advance_in(const PongIO& io, const PongIn& in, float dirn) {
+#pragma clang fp contract(off)   // rounds exactly like the PyTorch oracle, whatever the including file's flags
+  PongState s = in.s;
+  const int64_t tg = in.tg + 1;
+  const uint32_t id = (uint32_t)in.id, st = (uint32_t)tg;
   float rew = 0.0f;
   const float lo = FIELD_TOP + PADDLE_H / 2, hi = FIELD_BOT - PADDLE_H / 2;
   for (int sub = 0; sub < 4; ++sub) {
@@ -84,11 +99,11 @@ __device__ __forceinline__ PongOut pong_advance(const PongIO& io, int e, float d
   }
   PongOut r;
   const bool term = (s.sa >= WIN_SCORE) || (s.so >= WIN_SCORE);
-  r.t = io.tsteps[e] + 1;
+  r.t = in.t + 1;
   r.trunc = (r.t >= io.max_steps) && !term;
   r.done = term || r.trunc;
   r.rew = rew;
-  r.er = io.ep_ret[e] + rew;
+  r.er = in.ep_ret + rew;
   if (r.done) {
     const float mid = 0.5f * (FIELD_TOP + FIELD_BOT);
     s.pa = mid; s.po = mid; s.sa = 0.0f; s.so = 0.0f;
@@ -96,6 +111,10 @@ __device__ __forceinline__ PongOut pong_advance(const PongIO& io, int e, float d
   }
   r.s = s;
   return r;
+}
+
+__device__ __forceinline__ PongOut pong_advance(const PongIO& io, int e, float dirn) {
+  return pong_advance_in(io, pong_load(io, e), dirn);
 }
 
 // Writes the chosen outcome back (one thread). tg_old: the env's global step counter, when the caller already holds

@@ -55,6 +55,9 @@ def main():
         for name, y in parts:
             ph = {n: round(float((y[:, k + 1] - y[:, k]).median()), 2) for k, n in enumerate(NAMES)}
             ph["total (first stamp .. last)"] = round(float((y[:, 7] - y[:, 0]).median()), 2)
+            ph["  start -> fc planes summed (wave 0)"] = round(float((y[:, 8] - y[:, 0]).median()), 2)
+            ph["  start -> head partials written (wave 0)"] = round(float((y[:, 9] - y[:, 0]).median()), 2)
+            ph["  start -> physics candidates (wave 1)"] = round(float((y[:, 10] - y[:, 0]).median()), 2)
             res[name] = ph
         res["start spread us"] = round(float(x[:, 0].max() - x[:, 0].min()), 2)
         res["end spread us (last - first end)"] = round(float(x[:, 7].max() - x[:, 7].min()), 2)

@@ -251,8 +251,8 @@ class CNNEngine:
         want_shift = shift_out is not None
         if self.implicit and B <= self.fused_trunk_max_b:
             G.cnn_trunk_fwd(obs, self.sW1, self.b1, self.sW2, self.b2, self.sW3, self.b3, b.y1, b.y2, b.y3,
-                            shift_out=shift_out, mode=self.trunk_mode if B <= self.trunk_rows_max_b else 0,
-                            obs_idx=obs_idx)
+                            shift_out=shift_out, mode=self.trunk_mode if B <= self.trunk_rows_max_b else
+                            (3 if self.opts.trunk_fwd_staged else 0), obs_idx=obs_idx)
             shifted = shift_out is not None
         elif self.implicit:
             G.gemm(obs, 0, True, self.sW1, 256, True, b.y1, 32, 1, B * 400, 32, 256, bias=self.b1, relu=True,

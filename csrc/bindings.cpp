@@ -110,6 +110,9 @@ hipError_t aca_ac_loss(const float*, int64_t, const float*, int64_t, const int32
 hipError_t aca_cnn_trunk_fwd(const uint8_t*, const uint16_t*, const float*, const uint16_t*, const float*,
                              const uint16_t*, const float*, uint16_t*, uint16_t*, uint16_t*, int, float, uint8_t*,
                              uint64_t*, const int64_t*, hipStream_t);
+hipError_t aca_cnn_trunk_fwd_s16(const uint8_t*, const uint16_t*, const float*, const uint16_t*, const float*,
+                                 const uint16_t*, const float*, uint16_t*, uint16_t*, uint16_t*, int, float, uint8_t*,
+                                 const int64_t*, hipStream_t);
 hipError_t aca_grad_finalize(const int64_t*, int, float*, hipStream_t);
 hipError_t aca_head_bwd(const float*, const int32_t*, const float*, const float*, const float*, float, const float*,
                         const float*, const uint8_t*, int, int, int, int, int, float, float, float*, float*,
@@ -1410,7 +1413,7 @@ void cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tenso
   const int64_t* idxp = nullptr;
   if (obs_idx.has_value() && obs_idx->defined()) {   // sample b = row obs_idx[b] of obs (per-env mode 0 only)
     need(*obs_idx, at::kLong, "obs_idx");
-    TORCH_CHECK(mode == 0, "cnn_trunk_fwd: obs_idx needs the per-env mode");
+    TORCH_CHECK(mode == 0 || mode == 3, "cnn_trunk_fwd: obs_idx needs a per-env mode");
     B = obs_idx->numel();
     idxp = obs_idx->data_ptr<int64_t>();
   }
@@ -1419,7 +1422,7 @@ void cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tenso
   TORCH_CHECK(b1.numel() == 32 && b2.numel() == 64 && b3.numel() == 64, "cnn_trunk_fwd: bias sizes");
   TORCH_CHECK(y1.numel() >= B * 400 * 32 && y2.numel() >= B * 81 * 64 && y3.numel() >= B * 49 * 64,
               "cnn_trunk_fwd: activation buffers too small");
-  for (auto* t : {&obs, &W1, &W2, &W3})
+  for (auto* t : {&obs, &W1, &W2, &W3, &y1, &y2, &y3})
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "cnn_trunk_fwd: operands must be 16B aligned");
   uint8_t* so = nullptr;
   if (shift_out.has_value() && shift_out->defined()) {
@@ -1446,7 +1449,15 @@ void cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tenso
           "cnn_trunk_rows");
     return;
   }
-  TORCH_CHECK(mode == 0, "cnn_trunk_fwd: mode must be 0 or 1");
+  if (mode == 3) {   // the per-env bf16-staged kernel (one byte conversion per pixel; the learner's minibatch trunk)
+    TORCH_CHECK(!stamps.has_value() || !stamps->defined(), "cnn_trunk_fwd: mode 3 has no phase stamps");
+    check(aca_cnn_trunk_fwd_s16(ptr<uint8_t>(obs), ptr<uint16_t>(W1), ptr<float>(b1), ptr<uint16_t>(W2),
+                                ptr<float>(b2), ptr<uint16_t>(W3), ptr<float>(b3), ptr<uint16_t>(y1),
+                                ptr<uint16_t>(y2), ptr<uint16_t>(y3), (int)B, (float)scale, so, idxp, cur_stream(obs)),
+          "cnn_trunk_fwd_s16");
+    return;
+  }
+  TORCH_CHECK(mode == 0, "cnn_trunk_fwd: mode must be 0..3");
   check(aca_cnn_trunk_fwd(ptr<uint8_t>(obs), ptr<uint16_t>(W1), ptr<float>(b1), ptr<uint16_t>(W2), ptr<float>(b2),
                           ptr<uint16_t>(W3), ptr<float>(b3), ptr<uint16_t>(y1), ptr<uint16_t>(y2), ptr<uint16_t>(y3),
                           (int)B, (float)scale, so, stamps_ptr(stamps, B), idxp, cur_stream(obs)),

@@ -500,6 +500,171 @@ __global__ void __launch_bounds__(256) cnn_trunk_fwd_u8_kernel(
 }
 
 // ------------------------------------------------------------------------------------------------------------
+// Per-env trunk, bf16-staged form (the learner's minibatch forward): the lean form above converts every observation
+// byte to bf16 in conv1's inner loop, ~3.6 times per byte (the 8x8 / stride-4 windows overlap) -- conv1 is then
+// vector-issue bound (2.4k VALU vs 0.27k MFMA instructions per wave, profiles/r4_trunk_mix.txt). Here the bytes are
+// converted ONCE into a bf16 image (56 KB: still two workgroups per CU), conv1's outputs wait in registers until
+// every wave is done with the image, and y1 (unpadded 20 x 20 x 64 B, columns even-then-odd, chunk XOR-swizzled:
+// e1t_addr) + y2 (padded, conflict-free) then reuse its bytes. y1 / y2 / y3 leave through LDS as 16-byte rows.
+// Same MFMA order per output as every other trunk form: bit-identical activations.
+// ------------------------------------------------------------------------------------------------------------
+constexpr int E1T_ELEMS = 20 * 20 * Y1_C;   // 12800 u16
+__device__ __forceinline__ int e1t_addr(int h, int w, int ch) {
+  return (h * 20 + (w & 1) * 10 + (w >> 1)) * Y1_C + (((ch >> 3) ^ (((h >> 1) & 1) << 1)) << 3) + (ch & 7);
+}
+constexpr int OB16_ELEMS = 4 * 84 * 84;     // 28224 u16
+static_assert(E1T_ELEMS + E2_ELEMS <= OB16_ELEMS && Y3_ROWS * Y3_C <= E1T_ELEMS, "y1 + y2 (+ y3) reuse the image");
+
+__global__ void __launch_bounds__(256) cnn_trunk_fwd_s16_kernel(
+    const uint8_t* __restrict__ obs, const u16* __restrict__ W1, const float* __restrict__ b1,
+    const u16* __restrict__ W2, const float* __restrict__ b2, const u16* __restrict__ W3,
+    const float* __restrict__ b3, u16* __restrict__ y1g, u16* __restrict__ y2g, u16* __restrict__ y3g,
+    float scale, uint8_t* __restrict__ shift_out, const int64_t* __restrict__ obs_idx) {
+  __shared__ __attribute__((aligned(16))) u16 s_img[OB16_ELEMS];
+  u16* const s_y1 = s_img;               // after conv1
+  u16* const s_y2 = s_img + E1T_ELEMS;   // after conv1
+  u16* const s_y3 = s_img;               // after conv2 (y1 dead)
+  const int e = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int l16 = lane & 15, lg = lane >> 4;
+  const int n2 = wid * 16 + l16;
+  // ---------------------------------------------------------------- loads: observation bytes, conv1 fragments
+  constexpr int NCH = OBS_BYTES / 16, PER = (NCH + 255) / 256;   // 1764 chunks, 7 per thread
+  const uint4* src = reinterpret_cast<const uint4*>(obs + (size_t)(obs_idx ? obs_idx[e] : e) * OBS_BYTES);
+  uint4 v[PER];
+#pragma unroll
+  for (int u = 0; u < PER; ++u) v[u] = src[min(tid + u * 256, NCH - 1)];
+  bf16x8 bw[2][8];
+  trunk_env_w1(W1, bw);
+  const float bias0 = b1[l16], bias1 = b1[16 + l16], bias2 = b2[n2], bias3 = b3[n2];
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int i = tid + u * 256;
+    if (i < NCH) {
+      const uint2 a = u8x4_to_bf16(v[u].x), b = u8x4_to_bf16(v[u].y);
+      const uint2 c = u8x4_to_bf16(v[u].z), d = u8x4_to_bf16(v[u].w);
+      uint4* dst = reinterpret_cast<uint4*>(s_img) + 2 * i;
+      dst[0] = make_uint4(a.x, a.y, b.x, b.y);
+      dst[1] = make_uint4(c.x, c.y, d.x, d.y);
+      if (shift_out && i >= NCH / 4)   // rollout: frames 1..3 become frames 0..2 of the next observation
+        reinterpret_cast<uint4*>(shift_out + (size_t)e * OBS_BYTES)[i - NCH / 4] = v[u];
+    }
+  }
+  __syncthreads();
+  // ---------------------------------------------------------------- conv1: M 400 (25 tiles), N 32 (2), K 256 (8);
+  // the outputs stay in registers (bf16 pairs) until every wave is done reading the image
+  constexpr int MT1 = 7;   // tiles per wave (wave w: w, w + 4, ...; 7, 6, 6, 6)
+  uint32_t yr[MT1][4];
+#pragma unroll
+  for (int q = 0; q < MT1; ++q) {
+    const int mt = wid + 4 * q;
+    if (mt < 25) {
+      floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+      const int m = mt * 16 + l16;
+      const int oh = m / 20, ow = m - oh * 20;
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        const int k = ks * 32 + lg * 8;
+        const int c = k >> 6, i = (k >> 3) & 7;
+        const u16* p = s_img + (c * 84 + oh * 4 + i) * 84 + ow * 4;   // 8-byte aligned
+        const uint2 lo = *reinterpret_cast<const uint2*>(p), hi = *reinterpret_cast<const uint2*>(p + 4);
+        const bf16x8 a = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw[0][ks], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw[1][ks], acc1, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        yr[q][r] = (uint32_t)f2bf(fmaxf(acc0[r] * scale + bias0, 0.f)) |
+                   ((uint32_t)f2bf(fmaxf(acc1[r] * scale + bias1, 0.f)) << 16);
+    }
+  }
+  bf16x8 bw2[16];
+  trunk_env_w2(W2, bw2);
+  __syncthreads();   // the image is dead
+#pragma unroll
+  for (int q = 0; q < MT1; ++q) {
+    const int mt = wid + 4 * q;
+    if (mt < 25)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = mt * 16 + lg * 4 + r, h = row / 20, w = row - h * 20;
+        s_y1[e1t_addr(h, w, l16)] = (u16)(yr[q][r] & 0xFFFFu);
+        s_y1[e1t_addr(h, w, 16 + l16)] = (u16)(yr[q][r] >> 16);
+      }
+  }
+  __syncthreads();
+  // y1 -> global as 16-byte chunks (pixel p, channel chunk cq) while conv2 runs
+  for (int i = tid; i < Y1_ROWS * 4; i += 256) {
+    const int p = i >> 2, cq = i & 3, h = p / 20, w = p - h * 20;
+    *reinterpret_cast<uint4*>(y1g + ((size_t)e * Y1_ROWS + p) * Y1_C + cq * 8) =
+        *reinterpret_cast<const uint4*>(s_y1 + e1t_addr(h, w, cq * 8));
+  }
+  // ---------------------------------------------------------------- conv2: M 81 (6 tiles), N 64 (wave = N tile), K 512
+  {
+    floatx4 acc[6];
+#pragma unroll
+    for (int mt = 0; mt < 6; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) {
+      const int k = ks * 32 + lg * 8;
+      const int i = k >> 7, j = (k >> 5) & 3, c0 = k & 31;
+#pragma unroll
+      for (int mt = 0; mt < 6; ++mt) {
+        const int m = min(mt * 16 + l16, Y2_ROWS - 1);
+        const int oh = m / 9, ow = m - oh * 9;
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(s_y1 + e1t_addr(oh * 2 + i, ow * 2 + j, c0));
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw2[ks], acc[mt], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int mt = 0; mt < 6; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = mt * 16 + lg * 4 + r;
+        if (row < Y2_ROWS)
+          s_y2[((row / 9) * E2_W + row % 9) * Y2_LD + n2] = f2bf(fmaxf(acc[mt][r] + bias2, 0.f));
+      }
+  }
+  bf16x8 bw3[18];
+#pragma unroll
+  for (int ks = 0; ks < 18; ++ks) bw3[ks] = *reinterpret_cast<const bf16x8*>(W3 + n2 * 576 + ks * 32 + lg * 8);
+  __syncthreads();   // y2 complete; y1 dead (its global copy read it before the barrier)
+  for (int i = tid; i < Y2_ROWS * 8; i += 256) {
+    const int p = i >> 3, cq = i & 7;
+    *reinterpret_cast<uint4*>(y2g + ((size_t)e * Y2_ROWS + p) * Y2_C + cq * 8) =
+        *reinterpret_cast<const uint4*>(s_y2 + ((p / 9) * E2_W + p % 9) * Y2_LD + cq * 8);
+  }
+  // ---------------------------------------------------------------- conv3: M 49 (4 tiles), N 64 (wave = N tile), K 576
+  {
+    floatx4 acc[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 18; ++ks) {
+      const int k = ks * 32 + lg * 8;
+      const int i = k / 192, j = (k >> 6) % 3, c0 = k & 63;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const int m = min(mt * 16 + l16, Y3_ROWS - 1);
+        const int oh = m / 7, ow = m - oh * 7;
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(s_y2 + ((oh + i) * E2_W + ow + j) * Y2_LD + c0);
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw3[ks], acc[mt], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = mt * 16 + lg * 4 + r;
+        if (row < Y3_ROWS) s_y3[row * Y3_C + n2] = f2bf(fmaxf(acc[mt][r] + bias3, 0.f));
+      }
+  }
+  __syncthreads();
+  for (int i = tid; i < Y3_ROWS * 8; i += 256)
+    reinterpret_cast<uint4*>(y3g + (size_t)e * Y3_ROWS * Y3_C)[i] = reinterpret_cast<const uint4*>(s_y3)[i];
+}
+
+// ------------------------------------------------------------------------------------------------------------
 // Row-split trunk: 7 workgroups per env, workgroup r computes the receptive field of conv3 output row r only
 // (conv2 rows r..r+2, conv1 rows 2r..2r+7, input rows 8r..8r+35). The per-env kernel above keeps one CU busy per
 // env (32 of 256 CUs at the bench's 32 envs) and its layers run at one wave per SIMD; here 7x the CUs each do
@@ -1779,6 +1944,16 @@ extern "C" hipError_t aca_cnn_trunk_fwd(const uint8_t* obs, const uint16_t* W1, 
   if (obs_idx) return hipErrorInvalidValue;
   aca::cnn_trunk_fwd_kernel<<<B, aca::T_THREADS, 0, stream>>>(obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale,
                                                                shift_out, stamps);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t aca_cnn_trunk_fwd_s16(const uint8_t* obs, const uint16_t* W1, const float* b1,
+                                            const uint16_t* W2, const float* b2, const uint16_t* W3, const float* b3,
+                                            uint16_t* y1, uint16_t* y2, uint16_t* y3, int B, float scale,
+                                            uint8_t* shift_out, const int64_t* obs_idx, hipStream_t stream) {
+  if (B <= 0) return hipSuccess;
+  aca::cnn_trunk_fwd_s16_kernel<<<B, 256, 0, stream>>>(obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale, shift_out,
+                                                        obs_idx);
   return hipGetLastError();
 }
 

@@ -270,3 +270,37 @@ def test_sumsq_multi_equals_separate_launches(cuda):
     for a, b, x in zip(sep, mul, xs):
         assert torch.equal(a, b)
         assert abs(float(b.double().sum()) - float((x.double() ** 2).sum())) <= 1e-4 * float((x.double() ** 2).sum())
+
+
+def test_trunk_fwd_bf16_staged_by_index_equals_lean_form(cuda):
+    """cnn_trunk_fwd mode 3 (cnn_trunk_fwd_s16_kernel: bytes converted once into a bf16 image, y1/y2/y3 out through
+    LDS as 16-byte rows) reading a PPO minibatch through an index == the lean per-env form (mode 0) bit for bit, and
+    both match the fp32 torch convolutions of the same bf16 operands."""
+    import torch.nn.functional as F
+    from actor_critic_algs_on_tensorflow_amd.ops import gemm as G
+    g = torch.Generator(device="cpu").manual_seed(11)
+    R, B = 300, 257
+    obs = torch.randint(0, 256, (R, 4, 84, 84), dtype=torch.uint8, generator=g).to(cuda)
+    idx = torch.randint(0, R, (B,), generator=g).to(cuda)
+    W1 = (torch.randn(32, 256, generator=g) * 0.05).to(torch.bfloat16).to(cuda)
+    W2 = (torch.randn(64, 512, generator=g) * 0.05).to(torch.bfloat16).to(cuda)
+    W3 = (torch.randn(64, 576, generator=g) * 0.05).to(torch.bfloat16).to(cuda)
+    b1, b2, b3 = ((torch.rand(n, generator=g) * 0.1 - 0.02).to(cuda) for n in (32, 64, 64))
+    outs = []
+    for mode in (0, 3):
+        ys = [torch.full((B * r, c), float("nan"), dtype=torch.bfloat16, device=cuda)
+              for r, c in ((400, 32), (81, 64), (49, 64))]
+        G.cnn_trunk_fwd(obs, W1, b1, W2, b2, W3, b3, *ys, mode=mode, obs_idx=idx)
+        outs.append(ys)
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert torch.equal(a.view(torch.int16), b.view(torch.int16))
+    x = obs[idx].float() / 255.0
+    w1 = W1.float().view(32, 4, 8, 8)
+    y1 = F.relu(F.conv2d(x, w1, b1, stride=4)).to(torch.bfloat16)
+    w2 = W2.float().view(64, 4, 4, 32).permute(0, 3, 1, 2)
+    y2 = F.relu(F.conv2d(y1.float(), w2, b2, stride=2)).to(torch.bfloat16)
+    w3 = W3.float().view(64, 3, 3, 64).permute(0, 3, 1, 2)
+    y3 = F.relu(F.conv2d(y2.float(), w3, b3, stride=1))
+    got = outs[1][2].float().view(B, 7, 7, 64).permute(0, 3, 1, 2)
+    assert torch.allclose(got, y3, rtol=2e-2, atol=2e-2), (got - y3).abs().max()

@@ -688,7 +688,8 @@ __device__ __forceinline__ int tr_y1_own_begin(int r) { return (20 * r + 6) / 7;
 // complete) and the conv1 weights (s_w1, complete); stores the owned y1 / y2 rows and its y3 row. Shared by the
 // trunk kernel and the fused policy/env + trunk kernel.
 // WMODE (when the conv2 / conv3 weight fragments are requested): 0 at entry (the staging barrier waited for obs +
-// W1 only), 1 after conv1's MFMAs (trunk mode 2, and the fused step)
+// W1 only), 1 after conv1's MFMAs (trunk mode 2), 2 W2 at entry and W3 after conv1's MFMAs, 3 W2 already requested
+// by the caller and W3 after conv1's MFMAs (the fused step: W2's 64 KB per workgroup lands during the render)
 template <int WMODE>
 __device__ __forceinline__ void trunk_rows_compute(const u16* __restrict__ s_in, const u16* __restrict__ s_w1,
                                                    u16* __restrict__ s_y1, u16* __restrict__ s_y2, int e, int r,
@@ -701,9 +702,11 @@ __device__ __forceinline__ void trunk_rows_compute(const u16* __restrict__ s_in,
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l16 = lane & 15, lg = lane >> 4;
   const int n2 = wid * 16 + l16;
-  if constexpr (WMODE == 0) {
+  if constexpr (WMODE == 0 || WMODE == 2) {
 #pragma unroll
     for (int ks = 0; ks < 16; ++ks) bw2[ks] = *reinterpret_cast<const bf16x8*>(W2 + n2 * 512 + ks * 32 + lg * 8);
+  }
+  if constexpr (WMODE == 0) {
 #pragma unroll
     for (int ks = 0; ks < 18; ++ks) bw3[ks] = *reinterpret_cast<const bf16x8*>(W3 + n2 * 576 + ks * 32 + lg * 8);
   }
@@ -759,9 +762,12 @@ __device__ __forceinline__ void trunk_rows_compute(const u16* __restrict__ s_in,
       }
     }
   }
+  stamp(stamps, 10);
   if constexpr (WMODE == 1) {
 #pragma unroll
     for (int ks = 0; ks < 16; ++ks) bw2[ks] = *reinterpret_cast<const bf16x8*>(W2 + n2 * 512 + ks * 32 + lg * 8);
+  }
+  if constexpr (WMODE >= 1) {
 #pragma unroll
     for (int ks = 0; ks < 18; ++ks) bw3[ks] = *reinterpret_cast<const bf16x8*>(W3 + n2 * 576 + ks * 32 + lg * 8);
   }
@@ -993,14 +999,21 @@ __global__ void __launch_bounds__(T_THREADS) pong_fused_step_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, l16 = lane & 15;
   const int in0 = 8 * r;
   stamp(stamps, 0);
-  // ---------------------------------------------------------------- every independent operand requested first
+  // ---------------------------------------------------------------- every independent operand requested first, the
+  // head's first (env state, Wh rows, fc planes of obs t: the vm counter retires in issue order, so the sampling
+  // waits on them only), then the staged input rows and W1
+  const bool phys = tid >= 64 && tid < 67;   // the three paddle directions' physics candidates
+  PongIn pin;
+  if (phys) pin = pong_load(io, e);
   const int64_t tg0 = io.tglob[e], id0 = io.env_ids[e];
   const float bhj = bh[lane < A1 ? lane : 0];
-  const int n2 = wid * 16 + l16;
-  const float bias1a = b1[l16], bias1b = b1[16 + l16], bias2 = b2[n2], bias3 = b3[n2];
   uint32_t wv[A1];   // this thread's two Wh rows
 #pragma unroll
   for (int u = 0; u < A1; ++u) wv[u] = reinterpret_cast<const uint32_t*>(Wh)[A1 * tid + u];
+  FcH2<16> fch;
+  fch.issue(fc.hpart, fc.S, fc.plane_stride, fc.bfc, e, tid);
+  const int n2 = wid * 16 + l16;
+  const float bias1a = b1[l16], bias1b = b1[16 + l16], bias2 = b2[n2], bias3 = b3[n2];
   // frames 0..2 of the next observation (shifted in by the previous trunk launch): the staged rows
   constexpr int FR_CH = TR_IN_ROWS * 84 / 16;                      // 189 chunks per frame
   constexpr int IN3_CH = 3 * FR_CH;                                // 567
@@ -1026,8 +1039,8 @@ __global__ void __launch_bounds__(T_THREADS) pong_fused_step_kernel(
   bf16x8 bw2[16], bw3[18];
   // ---------------------------------------------------------------- policy head (every row workgroup of env e)
   float hf[2];
-  fc_h2_from_parts(fc.hpart, fc.S, fc.plane_stride, fc.bfc, e, tid, lead ? h : nullptr, hf);
-  if (tid >= 64 && tid < 67) cand[tid - 64] = pong_advance(io, e, (float)(tid - 65));
+  if (phys) cand[tid - 64] = pong_advance_in(io, pin, (float)(tid - 65));
+  fch.finish(fc.hpart, fc.S, fc.plane_stride, e, tid, lead ? h : nullptr, hf);
   float acc[A1];
 #pragma unroll
   for (int j = 0; j < A1; ++j) {
@@ -1057,30 +1070,16 @@ __global__ void __launch_bounds__(T_THREADS) pong_fused_step_kernel(
     }
   }
   __syncthreads();
+  stamp(stamps, 8);
   if (wid == 0) {
     const int64_t key = tg0 * ((int64_t)1 << key_shift) + id0;   // pre-step counter
     const int jj = lane < A1 ? lane : 0;
     const float zj = ((s_acc[0][jj] + s_acc[1][jj]) + (s_acc[2][jj] + s_acc[3][jj])) + bhj;
     if (lead && lane < A1) z_out[(size_t)e * A1 + lane] = zj;
-    const float value = __shfl(zj, A, 64);
-    const bool on = lane < A;
-    const float z = on ? zj : -INFINITY;
-    const float m = wave_max(z);
-    const float ex = on ? expf(z - m) : 0.f;
-    const float lse = m + logf(wave_sum(ex));
-    const float lp = z - lse;
-    const float H = wave_sum(on ? -expf(lp) * lp : 0.f);
-    float gmb = -INFINITY;
-    if (on) gmb = z + (-logf(-logf(uniform_open(pseed, key, (uint32_t)lane))));
-    float best = gmb;
-    int bi = on ? lane : 1 << 30;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float ob = __shfl_xor(best, o, 64);
-      const int oi = __shfl_xor(bi, o, 64);
-      if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
-    }
-    const float lpa = __shfl(lp, bi, 64);
+    const float value = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(zj), A));
+    const CatSample cs = cat_sample<8>(zj, A, lane, pseed, key);   // A1 <= 7
+    const int bi = cs.act;
+    const float lpa = cs.lpa, H = cs.H;
     if (lane == 0) {
       if (lead) {
         act[e] = bi;
@@ -1092,6 +1091,10 @@ __global__ void __launch_bounds__(T_THREADS) pong_fused_step_kernel(
     }
   }
   __syncthreads();
+  stamp(stamps, 9);
+#pragma unroll
+  for (int ks = 0; ks < 16; ++ks)   // conv2's fragments, landing during the render (trunk_rows_compute WMODE 3)
+    bw2[ks] = *reinterpret_cast<const bf16x8*>(W2 + n2 * 512 + ks * 32 + (lane >> 4) * 8);
   const PongOut& res = cand[pong_dir_index(sh_act)];
   const bool done = res.done != 0;
   if (lead && tid == 0) pong_commit_next(io, nx, e, res, tg0);
@@ -1138,7 +1141,7 @@ __global__ void __launch_bounds__(T_THREADS) pong_fused_step_kernel(
   }
   __syncthreads();
   stamp(stamps, 1);
-  trunk_rows_compute<1>(s_in, s_w1, s_y1, s_y2, e, r, bias1a, bias1b, bias2, bias3, W2, W3, y1g, y2g, y3g, scale,
+  trunk_rows_compute<3>(s_in, s_w1, s_y1, s_y2, e, r, bias1a, bias1b, bias2, bias3, W2, W3, y1g, y2g, y3g, scale,
                         stamps, bw2, bw3);
 }
 
@@ -1222,25 +1225,10 @@ __device__ __forceinline__ void env_step_body(
     const int jj = lane < A1 ? lane : 0;
     const float zj = ((s_acc[0][jj] + s_acc[1][jj]) + (s_acc[2][jj] + s_acc[3][jj])) + bhj;
     if (lead && lane < A1) z_out[(size_t)e * A1 + lane] = zj;
-    const float value = __shfl(zj, A, 64);
-    const bool on = lane < A;
-    const float z = on ? zj : -INFINITY;
-    const float m = wave_max(z);
-    const float ex = on ? expf(z - m) : 0.f;
-    const float lse = m + logf(wave_sum(ex));
-    const float lp = z - lse;
-    const float H = wave_sum(on ? -expf(lp) * lp : 0.f);
-    float gmb = -INFINITY;
-    if (on) gmb = z + (-logf(-logf(uniform_open(pseed, key, (uint32_t)lane))));
-    float best = gmb;
-    int bi = on ? lane : 1 << 30;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float ob = __shfl_xor(best, o, 64);
-      const int oi = __shfl_xor(bi, o, 64);
-      if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
-    }
-    const float lpa = __shfl(lp, bi, 64);
+    const float value = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(zj), A));
+    const CatSample cs = cat_sample<8>(zj, A, lane, pseed, key);   // A1 <= 7
+    const int bi = cs.act;
+    const float lpa = cs.lpa, H = cs.H;
     if (lane == 0) {
       if (lead) {
         act[e] = bi;

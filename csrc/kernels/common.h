@@ -112,6 +112,82 @@ __device__ __forceinline__ float wave_max(float v) {
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
   return v;
 }
+// ------------------------------------------------------------------------------------------------------------
+// Categorical head of one wave: lanes 0..A-1 hold the logits (z), the log-softmax, entropy and a Gumbel-max sample
+// (first-index tie break) come back in every lane. W = 64: xor butterflies over the whole wave; W = 8 (A <= 8): the
+// same trees' last three rounds only -- lanes >= A hold the neutral element (0 for sums, -inf / index 2^30 for the
+// max and the argmax), so the 64-lane tree's first three rounds leave lanes 0..7 at (v + 0) and the results are
+// bit-identical -- with the xor-2 / xor-1 rounds as quad-permute DPP moves instead of LDS-crossbar permutes (the
+// 64-lane form is a chain of 32 ds_bpermute round trips, ~1 us of the fused rollout step's sampling wave).
+// ------------------------------------------------------------------------------------------------------------
+__device__ __forceinline__ float dpp_xor1(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float dpp_xor2(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
+}
+__device__ __forceinline__ int dpp_xor1i(int v) { return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false); }
+__device__ __forceinline__ int dpp_xor2i(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false); }
+
+template <int W>
+__device__ __forceinline__ float red_sum(float v) {
+  if constexpr (W == 64) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+  } else {
+    static_assert(W == 8, "8 or 64 lanes");
+    v = v + 0.0f;   // the first three rounds of the 64-lane tree (+0 partners): canonicalises -0
+    v += __shfl_xor(v, 4, 64);
+    v += dpp_xor2(v);
+    v += dpp_xor1(v);
+    return v;
+  }
+}
+template <int W>
+__device__ __forceinline__ float red_max(float v) {
+  if constexpr (W == 64) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+  } else {
+    v = fmaxf(v, __shfl_xor(v, 4, 64));
+    v = fmaxf(v, dpp_xor2(v));
+    return fmaxf(v, dpp_xor1(v));
+  }
+}
+__device__ __forceinline__ void argmax_step(float& best, int& bi, float ob, int oi) {
+  if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+}
+
+struct CatSample {
+  int act;     // sampled action (Gumbel-max)
+  float lpa;   // its log-probability
+  float H;     // entropy
+};
+template <int W>
+__device__ __forceinline__ CatSample cat_sample(float zin, int A, int lane, uint32_t seed, int64_t key) {
+  const bool on = lane < A;
+  const float z = on ? zin : -INFINITY;
+  const float m = red_max<W>(z);
+  const float ex = on ? expf(z - m) : 0.f;
+  const float lse = m + logf(red_sum<W>(ex));
+  const float lp = z - lse;
+  const float H = red_sum<W>(on ? -expf(lp) * lp : 0.f);
+  float best = -INFINITY;
+  if (on) best = z + (-logf(-logf(uniform_open(seed, key, (uint32_t)lane))));
+  int bi = on ? lane : 1 << 30;
+  if constexpr (W == 64) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) argmax_step(best, bi, __shfl_xor(best, o, 64), __shfl_xor(bi, o, 64));
+  } else {
+    argmax_step(best, bi, __shfl_xor(best, 4, 64), __shfl_xor(bi, 4, 64));
+    argmax_step(best, bi, dpp_xor2(best), dpp_xor2i(bi));
+    argmax_step(best, bi, dpp_xor1(best), dpp_xor1i(bi));
+  }
+  return CatSample{bi, __shfl(lp, bi, 64), H};
+}
+
 __device__ __forceinline__ double wave_sum_d(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -60,6 +60,7 @@ hipError_t aca_pong_fused_env_step(uint16_t*, const float*, int, int64_t, const 
                                    uint32_t, int, const uint16_t*, const float*, const uint16_t*, const float*,
                                    const uint16_t*, const float*, uint16_t*, uint16_t*, uint16_t*, float, uint8_t*,
                                    float*, int32_t*, int64_t*, float*, uint64_t*, int, hipStream_t);
+hipError_t aca_wave_reduce_check(const float*, float*, int, hipStream_t);
 hipError_t aca_categorical_sample(const float*, int, int, int, const int64_t*, const int64_t*, const int64_t*, int,
                                   uint32_t, int32_t*, float*, float*, float*, hipStream_t);
 hipError_t aca_ev(const float*, const float*, float*, int, hipStream_t);
@@ -458,6 +459,14 @@ void fc_value(Tensor hpart, int64_t planes, Tensor bfc, Tensor Wh, Tensor bh, Te
 }
 
 // ---------------------------------------------------------------------------------------------- heads
+// diagnostics: x [rows, 64] fp32 -> out [rows, 4, 64] (heads.hip wave_reduce_check_kernel)
+void wave_reduce_check(Tensor x, Tensor out) {
+  need(x, at::kFloat, "x");
+  need(out, at::kFloat, "out");
+  TORCH_CHECK(x.numel() % 64 == 0 && out.numel() == x.numel() * 4, "wave_reduce_check: x [rows, 64], out [rows, 4, 64]");
+  check(aca_wave_reduce_check(ptr<float>(x), ptr<float>(out), (int)(x.numel() / 64), cur_stream(x)), "wave_reduce_check");
+}
+
 void categorical_sample(Tensor logits, Tensor keys, int64_t seed, Tensor act, Tensor logp, Tensor ent) {
   TORCH_CHECK(logits.is_cuda() && logits.scalar_type() == at::kFloat && logits.dim() == 2 && logits.stride(1) == 1,
               "categorical_sample: logits must be fp32 [B, A] with unit column stride");
@@ -1735,6 +1744,7 @@ TORCH_LIBRARY(acamd, m) {
         "Tensor hpart, int planes, Tensor bfc, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, "
         "Tensor y1, Tensor y2, Tensor y3, float scale, Tensor? shift_out=None, Tensor[]? next_state=None, Tensor? stamps=None) -> ()");
   m.def("categorical_sample(Tensor logits, Tensor keys, int seed, Tensor act, Tensor logp, Tensor ent) -> ()");
+  m.def("wave_reduce_check(Tensor x, Tensor out) -> ()");
   m.def("categorical_sample_env(Tensor logits, Tensor tg, Tensor env_ids, int key_shift, int seed, Tensor act, "
         "Tensor logp, Tensor ent, Tensor? vout) -> ()");
   m.def("ev(Tensor x, Tensor y, Tensor out, Tensor? part=None, Tensor? ticket=None) -> ()");
@@ -1868,6 +1878,7 @@ TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
   m.impl("ppo_head", &ppo_head);
   m.impl("gemm_big", &gemm_big);
   m.impl("pong_fused_env_step", &pong_fused_env_step);
+  m.impl("wave_reduce_check", &wave_reduce_check);
   m.impl("head_bwd", &head_bwd);
   m.impl("a2c_head", &a2c_head);
   m.impl("im2col_u8", &im2col_u8);

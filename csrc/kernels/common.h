@@ -87,7 +87,43 @@ __device__ __forceinline__ u16 f2bf(float f) {
 // ------------------------------------------------------------------------------------------------------------
 // wave / block reductions (64-lane waves)
 // ------------------------------------------------------------------------------------------------------------
+// The xor butterfly (round o pairs lane i with lane i ^ o, o = 32 .. 1), every round a register move instead of an
+// LDS-crossbar permute: xor 32 / 16 by v_permlane32_swap / v_permlane16_swap (+ a select of the half that holds the
+// partner), xor 8 by DPP row_ror:8, xor 4 by DPP row_shl:4 / row_shr:4 (+ select), xor 2 / 1 by quad-permute DPP.
+// Same pairing and operand order as the ds_bpermute form (wave_sum_ref): bit-identical results in every lane
+// (tests/test_gpu_r4.py checks both on random data).
+__device__ __forceinline__ float xor32f(float v) {
+  const auto p = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
+  return __int_as_float((threadIdx.x & 32) ? p[0] : p[1]);
+}
+__device__ __forceinline__ float xor16f(float v) {
+  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_int(v), __float_as_int(v), false, false);
+  return __int_as_float((threadIdx.x & 16) ? p[0] : p[1]);
+}
+__device__ __forceinline__ float xor8f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xF, 0xF, false));   // row_ror:8
+}
+__device__ __forceinline__ float xor4f(float v) {
+  const int up = __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x104, 0xF, 0xF, false);   // row_shl:4 (i + 4)
+  const int dn = __builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x114, 0xF, 0xF, false);   // row_shr:4 (i - 4)
+  return __int_as_float((threadIdx.x & 4) ? dn : up);
+}
+__device__ __forceinline__ float xor2f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float xor1f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
 __device__ __forceinline__ float wave_sum(float v) {
+  v += xor32f(v);
+  v += xor16f(v);
+  v += xor8f(v);
+  v += xor4f(v);
+  v += xor2f(v);
+  v += xor1f(v);
+  return v;
+}
+__device__ __forceinline__ float wave_sum_ref(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
@@ -108,52 +144,50 @@ __device__ __forceinline__ void add_ep_stats(float* ep_stats, bool active, bool 
   }
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  v = fmaxf(v, xor32f(v));
+  v = fmaxf(v, xor16f(v));
+  v = fmaxf(v, xor8f(v));
+  v = fmaxf(v, xor4f(v));
+  v = fmaxf(v, xor2f(v));
+  return fmaxf(v, xor1f(v));
 }
 // ------------------------------------------------------------------------------------------------------------
 // Categorical head of one wave: lanes 0..A-1 hold the logits (z), the log-softmax, entropy and a Gumbel-max sample
 // (first-index tie break) come back in every lane. W = 64: xor butterflies over the whole wave; W = 8 (A <= 8): the
 // same trees' last three rounds only -- lanes >= A hold the neutral element (0 for sums, -inf / index 2^30 for the
 // max and the argmax), so the 64-lane tree's first three rounds leave lanes 0..7 at (v + 0) and the results are
-// bit-identical -- with the xor-2 / xor-1 rounds as quad-permute DPP moves instead of LDS-crossbar permutes (the
-// 64-lane form is a chain of 32 ds_bpermute round trips, ~1 us of the fused rollout step's sampling wave).
+// bit-identical -- every round a register move (the ds_bpermute form was a chain of 32 LDS-crossbar round trips,
+// ~1 us of the fused rollout step's sampling wave).
 // ------------------------------------------------------------------------------------------------------------
-__device__ __forceinline__ float dpp_xor1(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+__device__ __forceinline__ int xor4i(int v) {
+  const int up = __builtin_amdgcn_update_dpp(0, v, 0x104, 0xF, 0xF, false);
+  const int dn = __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);
+  return (threadIdx.x & 4) ? dn : up;
 }
-__device__ __forceinline__ float dpp_xor2(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
-}
-__device__ __forceinline__ int dpp_xor1i(int v) { return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false); }
-__device__ __forceinline__ int dpp_xor2i(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false); }
+__device__ __forceinline__ int xor2i(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false); }
+__device__ __forceinline__ int xor1i(int v) { return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false); }
 
 template <int W>
 __device__ __forceinline__ float red_sum(float v) {
   if constexpr (W == 64) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    return wave_sum(v);
   } else {
     static_assert(W == 8, "8 or 64 lanes");
     v = v + 0.0f;   // the first three rounds of the 64-lane tree (+0 partners): canonicalises -0
-    v += __shfl_xor(v, 4, 64);
-    v += dpp_xor2(v);
-    v += dpp_xor1(v);
+    v += xor4f(v);
+    v += xor2f(v);
+    v += xor1f(v);
     return v;
   }
 }
 template <int W>
 __device__ __forceinline__ float red_max(float v) {
   if constexpr (W == 64) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-    return v;
+    return wave_max(v);
   } else {
-    v = fmaxf(v, __shfl_xor(v, 4, 64));
-    v = fmaxf(v, dpp_xor2(v));
-    return fmaxf(v, dpp_xor1(v));
+    v = fmaxf(v, xor4f(v));
+    v = fmaxf(v, xor2f(v));
+    return fmaxf(v, xor1f(v));
   }
 }
 __device__ __forceinline__ void argmax_step(float& best, int& bi, float ob, int oi) {
@@ -181,9 +215,9 @@ __device__ __forceinline__ CatSample cat_sample(float zin, int A, int lane, uint
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) argmax_step(best, bi, __shfl_xor(best, o, 64), __shfl_xor(bi, o, 64));
   } else {
-    argmax_step(best, bi, __shfl_xor(best, 4, 64), __shfl_xor(bi, 4, 64));
-    argmax_step(best, bi, dpp_xor2(best), dpp_xor2i(bi));
-    argmax_step(best, bi, dpp_xor1(best), dpp_xor1i(bi));
+    argmax_step(best, bi, xor4f(best), xor4i(bi));
+    argmax_step(best, bi, xor2f(best), xor2i(bi));
+    argmax_step(best, bi, xor1f(best), xor1i(bi));
   }
   return CatSample{bi, __shfl(lp, bi, 64), H};
 }

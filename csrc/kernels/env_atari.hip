@@ -90,27 +90,12 @@ __global__ void __launch_bounds__(256) pong_policy_step_kernel(PongIO io, FcPart
     const int jj = lane < A1 ? lane : 0;
     float zj = ((s_acc[0][jj] + s_acc[1][jj]) + (s_acc[2][jj] + s_acc[3][jj])) + bhj;
     if (lane < A1) z_out[(size_t)e * A1 + lane] = zj;
-    const float value = __shfl(zj, A, 64);
+    const float value = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(zj), A));
     stamp_if(stamps, 10, lane == 0);
-    // categorical head over lanes 0..A-1 (same maths as categorical_sample_kernel)
-    const bool on = lane < A;
-    const float z = on ? zj : -INFINITY;
-    const float m = wave_max(z);
-    const float ex = on ? expf(z - m) : 0.f;
-    const float lse = m + logf(wave_sum(ex));
-    const float lp = z - lse;
-    const float H = wave_sum(on ? -expf(lp) * lp : 0.f);
-    float g = -INFINITY;
-    if (on) g = z + (-logf(-logf(uniform_open(pseed, key, (uint32_t)lane))));
-    float best = g;
-    int bi = on ? lane : 1 << 30;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float ob = __shfl_xor(best, o, 64);
-      const int oi = __shfl_xor(bi, o, 64);
-      if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
-    }
-    const float lpa = __shfl(lp, bi, 64);
+    // categorical head over lanes 0..A-1 (same maths as categorical_sample_kernel; A1 <= 7: the 8-lane trees)
+    const CatSample cs = cat_sample<8>(zj, A, lane, pseed, key);
+    const int bi = cs.act;
+    const float lpa = cs.lpa, H = cs.H;
     if (lane == 0) {
       act[e] = bi;
       logp[e] = lpa;

@@ -23,31 +23,13 @@ __global__ void __launch_bounds__(256) categorical_sample_kernel(const float* __
   const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (row >= B) return;
   const bool on = lane < A;
-  const float z = on ? logits[(size_t)row * ldl + lane] : -INFINITY;
-  const float m = wave_max(z);
-  const float ex = on ? expf(z - m) : 0.f;
-  const float se = wave_sum(ex);
-  const float lse = m + logf(se);
-  const float lp = z - lse;  // log_softmax
-  const float h = on ? -expf(lp) * lp : 0.f;
-  const float H = wave_sum(h);
-  // Gumbel-max
-  float g = -INFINITY;
-  if (on) {
-    const int64_t key = keys ? keys[row] : (tg[row] * ((int64_t)1 << key_shift) + env_ids[row]);
-    const float u = uniform_open(seed, key, (uint32_t)lane);
-    g = z + (-logf(-logf(u)));
-  }
-  // argmax with first-index tie breaking
-  float best = g;
-  int bi = on ? lane : 1 << 30;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    float ob = __shfl_xor(best, o, 64);
-    int oi = __shfl_xor(bi, o, 64);
-    if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
-  }
-  const float lpa = __shfl(lp, bi, 64);
+  const float z = on ? logits[(size_t)row * ldl + lane] : 0.f;
+  const int64_t key = keys ? keys[row] : (tg[row] * ((int64_t)1 << key_shift) + env_ids[row]);
+  // log_softmax, entropy, Gumbel-max with first-index tie breaking (common.h cat_sample: 8-lane trees for A <= 8,
+  // bit-identical to the 64-lane ones)
+  const CatSample cs = A <= 8 ? cat_sample<8>(z, A, lane, seed, key) : cat_sample<64>(z, A, lane, seed, key);
+  const int bi = cs.act;
+  const float lpa = cs.lpa, H = cs.H;
   if (lane == 0) {
     act[row] = bi;
     logp[row] = lpa;
@@ -81,6 +63,28 @@ __global__ void gaussian_sample_kernel(const float* __restrict__ mu, int ldm, in
 }
 
 }  // namespace aca
+
+// Diagnostics (tests/test_gpu_r4.py): every lane's result of the register-move wave reductions next to the
+// ds_bpermute reference forms -- out [rows, 4, 64]: wave_sum, wave_sum_ref, wave_max, max via __shfl_xor.
+__global__ void wave_reduce_check_kernel(const float* __restrict__ x, float* __restrict__ out, int rows) {
+  const int lane = threadIdx.x & 63, row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float v = x[(size_t)row * 64 + lane];
+  float m = v;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  float* o = out + (size_t)row * 256;
+  o[lane] = aca::wave_sum(v);
+  o[64 + lane] = aca::wave_sum_ref(v);
+  o[128 + lane] = aca::wave_max(v);
+  o[192 + lane] = m;
+}
+
+extern "C" hipError_t aca_wave_reduce_check(const float* x, float* out, int rows, hipStream_t stream) {
+  if (rows <= 0) return hipSuccess;
+  wave_reduce_check_kernel<<<(rows + 3) / 4, 256, 0, stream>>>(x, out, rows);
+  return hipGetLastError();
+}
 
 extern "C" hipError_t aca_categorical_sample(const float* logits, int ldl, int B, int A, const int64_t* keys,
                                              const int64_t* tg, const int64_t* ids, int key_shift, uint32_t seed,

@@ -304,3 +304,25 @@ def test_trunk_fwd_bf16_staged_by_index_equals_lean_form(cuda):
     y3 = F.relu(F.conv2d(y2.float(), w3, b3, stride=1))
     got = outs[1][2].float().view(B, 7, 7, 64).permute(0, 3, 1, 2)
     assert torch.allclose(got, y3, rtol=2e-2, atol=2e-2), (got - y3).abs().max()
+
+
+def test_register_move_wave_reductions_are_bit_identical_to_bpermute(cuda):
+    """common.h wave_sum / wave_max (permlane32/16 swaps, DPP row_ror:8, row_shl/shr:4, quad permutes) == the
+    ds_bpermute xor butterflies bit for bit in every lane, on random data with signed zeros and infinities mixed in."""
+    from actor_critic_algs_on_tensorflow_amd import _native
+    ops = _native.require()
+    g = torch.Generator(device="cpu").manual_seed(5)
+    x = torch.randn(4096, 64, generator=g) * torch.exp(torch.randn(4096, 64, generator=g) * 4)
+    x[::7, ::5] = -0.0
+    x[::11, 3] = float("inf")
+    x[::13, 9] = float("-inf")
+    x = x.to(cuda)
+    out = torch.empty(4096, 4, 64, device=cuda)
+    ops.wave_reduce_check(x, out)
+    torch.cuda.synchronize()
+    a = out.view(torch.int32)
+    assert torch.equal(a[:, 0], a[:, 1]), "wave_sum"
+    assert torch.equal(a[:, 2], a[:, 3]), "wave_max"
+    fin = torch.isfinite(out[:, 1]).all(dim=1)
+    ref = x.double().sum(dim=1)
+    assert torch.allclose(out[fin, 1, 0].double(), ref[fin], rtol=1e-4, atol=1e-3 * x.abs().max().item())

@@ -1550,8 +1550,8 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_kernel(
   for (int e = 0; e < 8; ++e)
 #pragma unroll
     for (int o = 8; o < 64; o <<= 1) {
-      part3[e] += __shfl_xor(part3[e], o, 64);
-      part2[e] += __shfl_xor(part2[e], o, 64);
+      part3[e] += lane_xor(part3[e], o);
+      part2[e] += lane_xor(part2[e], o);
     }
   if (lane < 8)
 #pragma unroll
@@ -1622,7 +1622,7 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_kernel(
 #pragma unroll
   for (int e = 0; e < 8; ++e)
 #pragma unroll
-    for (int o = 4; o < 64; o <<= 1) part1[e] += __shfl_xor(part1[e], o, 64);
+    for (int o = 4; o < 64; o <<= 1) part1[e] += lane_xor(part1[e], o);
   if (lane < 4)
 #pragma unroll
     for (int e = 0; e < 8; ++e) s_red[1024 + wid * 32 + lane * 8 + e] = part1[e];   // channel lane * 8 + e
@@ -1747,18 +1747,30 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
       floatx4 acc[3];
 #pragma unroll
       for (int mt = 0; mt < 3; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
+      // operands of k-step ks + 1 read while ks's MFMAs run (two register buffers): left to the compiler, every
+      // MFMA waited out the LDS read issued just before it
+      int pix[3];
+#pragma unroll
+      for (int mt = 0; mt < 3; ++mt) {
+        const int m = min((mh + mt) * 16 + l16, 80);
+        const int a = m / 9, c = m - a * 9;
+        pix[mt] = (a + 2) * BW_P3W + (c + 2);
+      }
+      bf16x8 af[2][3], bwf[2];
+      auto ld2 = [&](int ks, int buf) {
+        const int kb = ks * 32 + lg * 8, t = kb >> 6, o0 = kb & 63, ti = t / 3, tj = t - ti * 3;
+        bwf[buf] = tr_frag_sw<3>(s_w3z + ks * 32 * BW_LDW3, BW_LDW3, n0, lane);
+#pragma unroll
+        for (int mt = 0; mt < 3; ++mt)
+          af[buf][mt] = *reinterpret_cast<const bf16x8*>(s_p3 + (pix[mt] - ti * BW_P3W - tj) * BW_PS + o0);
+      };
+      ld2(0, 0);
 #pragma unroll
       for (int ks = 0; ks < 18; ++ks) {
-        const int kb = ks * 32 + lg * 8, t = kb >> 6, o0 = kb & 63, ti = t / 3, tj = t - ti * 3;
-        const bf16x8 bw = tr_frag_sw<3>(s_w3z + ks * 32 * BW_LDW3, BW_LDW3, n0, lane);
+        if (ks + 1 < 18) ld2(ks + 1, (ks + 1) & 1);
 #pragma unroll
-        for (int mt = 0; mt < 3; ++mt) {
-          const int m = min((mh + mt) * 16 + l16, 80);
-          const int a = m / 9, c = m - a * 9;
-          const bf16x8 af =
-              *reinterpret_cast<const bf16x8*>(s_p3 + ((a - ti + 2) * BW_P3W + (c - tj + 2)) * BW_PS + o0);
-          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bw, acc[mt], 0, 0, 0);
-        }
+        for (int mt = 0; mt < 3; ++mt)
+          acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks & 1][mt], bwf[ks & 1], acc[mt], 0, 0, 0);
       }
       pst(it, 6);
       const int n = n0 + l16;
@@ -1798,8 +1810,8 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
     for (int e = 0; e < 8; ++e)
 #pragma unroll
       for (int o = 8; o < 64; o <<= 1) {
-        part3[e] += __shfl_xor(part3[e], o, 64);
-        part2[e] += __shfl_xor(part2[e], o, 64);
+        part3[e] += lane_xor(part3[e], o);
+        part2[e] += lane_xor(part2[e], o);
       }
     if (lane < 8)
 #pragma unroll
@@ -1814,16 +1826,26 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
       floatx4 acc[7];
 #pragma unroll
       for (int i = 0; i < 7; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+      int pix1[7];
 #pragma unroll
-      for (int ks = 0; ks < 8; ++ks) {
+      for (int i = 0; i < 7; ++i) {
+        const int u = min(i * 16 + l16, 99), yy = u / 10, xx = u - yy * 10;
+        pix1[i] = (yy + 1) * BW_P2W + (xx + 1);
+      }
+      bf16x8 a1[2][7];   // k-step ks + 1's A fragments read while ks's MFMAs run
+      auto ld1 = [&](int ks, int buf) {
         const int d = ks >> 1, di = d >> 1, dj = d & 1, ob = (ks & 1) * 32;
 #pragma unroll
-        for (int i = 0; i < 7; ++i) {
-          const int u = min(i * 16 + l16, 99), yy = u / 10, xx = u - yy * 10;
-          const bf16x8 af = *reinterpret_cast<const bf16x8*>(
-              s_p2 + ((yy - di + 1) * BW_P2W + (xx - dj + 1)) * BW_PS + ob + lg * 8);
-          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, w2f[ks], acc[i], 0, 0, 0);
-        }
+        for (int i = 0; i < 7; ++i)
+          a1[buf][i] = *reinterpret_cast<const bf16x8*>(s_p2 + (pix1[i] - di * BW_P2W - dj) * BW_PS + ob + lg * 8);
+      };
+      ld1(0, 0);
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        if (ks + 1 < 8) ld1(ks + 1, (ks + 1) & 1);
+#pragma unroll
+        for (int i = 0; i < 7; ++i)
+          acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[ks & 1][i], w2f[ks], acc[i], 0, 0, 0);
       }
       pst(it, 3);
       __syncthreads();   // every wave is past its dy2-image reads of the db sums; s_red rows complete
@@ -1866,7 +1888,7 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
 #pragma unroll
     for (int e = 0; e < 8; ++e)
 #pragma unroll
-      for (int o = 4; o < 64; o <<= 1) part1[e] += __shfl_xor(part1[e], o, 64);
+      for (int o = 4; o < 64; o <<= 1) part1[e] += lane_xor(part1[e], o);
     if (lane < 4)
 #pragma unroll
       for (int e = 0; e < 8; ++e) s_red[1024 + wid * 32 + lane * 8 + e] = part1[e];

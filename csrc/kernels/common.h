@@ -114,6 +114,18 @@ __device__ __forceinline__ float xor2f(float v) {
 __device__ __forceinline__ float xor1f(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
 }
+// partner value of lane i ^ o (o a compile-time power of two after unrolling): the register move for it
+__device__ __forceinline__ float lane_xor(float v, int o) {
+  switch (o) {
+    case 32: return xor32f(v);
+    case 16: return xor16f(v);
+    case 8: return xor8f(v);
+    case 4: return xor4f(v);
+    case 2: return xor2f(v);
+    case 1: return xor1f(v);
+    default: return __shfl_xor(v, o, 64);
+  }
+}
 __device__ __forceinline__ float wave_sum(float v) {
   v += xor32f(v);
   v += xor16f(v);

@@ -124,7 +124,8 @@ __global__ void __launch_bounds__(256) col2im_nhwc_kernel(const u16* __restrict_
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       float v = part[e];
-      for (int o = 32; o >= CC; o >>= 1) v += __shfl_xor(v, o, 64);
+#pragma unroll
+      for (int o = 32; o >= CC; o >>= 1) v += lane_xor(v, o);
       part[e] = v;
     }
     const int lane = threadIdx.x & 63;

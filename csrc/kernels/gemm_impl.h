@@ -553,8 +553,8 @@ __device__ __forceinline__ void gemm_block(const GemmParams& P, const int tile, 
         csum += v;
       }
     }
-    csum += __shfl_xor(csum, 16, 64);
-    csum += __shfl_xor(csum, 32, 64);
+    csum += lane_xor(csum, 16);
+    csum += lane_xor(csum, 32);
     csums[j] = csum;
     if (g.colsum && !g.colsum_part && lg == 0 && n_ok)
       atomicAdd(&g.colsum[g.colsum_mod ? n % g.colsum_mod : n], csum);

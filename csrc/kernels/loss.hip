@@ -548,9 +548,9 @@ __global__ void __launch_bounds__(HB_THREADS) head_bwd_kernel(HeadBwdArgs a) {
   for (int c = 0; c < 8; ++c) {
 #pragma unroll
     for (int o = 8; o < 64; o <<= 1) {
-      dbf[c] += __shfl_xor(dbf[c], o, 64);
+      dbf[c] += lane_xor(dbf[c], o);
 #pragma unroll
-      for (int q = 0; q < A1; ++q) dwp[c][q] += __shfl_xor(dwp[c][q], o, 64);
+      for (int q = 0; q < A1; ++q) dwp[c][q] += lane_xor(dwp[c][q], o);
     }
   }
   hb_stamp(a, 4);
@@ -883,9 +883,9 @@ __global__ void __launch_bounds__(AH_THREADS) a2c_head_kernel(A2cHeadArgs args) 
   for (int c = 0; c < 4; ++c) {
 #pragma unroll
     for (int o = 4; o < 64; o <<= 1) {
-      dbf[c] += __shfl_xor(dbf[c], o, 64);
+      dbf[c] += lane_xor(dbf[c], o);
 #pragma unroll
-      for (int q = 0; q < A1; ++q) dwp[c][q] += __shfl_xor(dwp[c][q], o, 64);
+      for (int q = 0; q < A1; ++q) dwp[c][q] += lane_xor(dwp[c][q], o);
     }
   }
   hb_stamp(a, 4);

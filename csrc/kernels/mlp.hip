@@ -477,7 +477,7 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
       for (int k = 0; k < 8; ++k) {
         float v = st[k];
 #pragma unroll
-        for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 16);
+        for (int o = 8; o > 0; o >>= 1) v += lane_xor(v, o);
         if (r == 0 && (policy ? (k != 3) : (k == 3))) {
           // partial rows: every workgroup owns a row, the weight-gradient kernel sums them in a fixed order
           // (atomics from every workgroup to one 32-byte line serialise in L2, ~12 ns each)
@@ -677,8 +677,8 @@ __global__ void __launch_bounds__(256) mlp_wgrad_kernel(WgradArgs a) {
   }
   if (ti == 0) {
     // lanes with equal (lane & 15) hold partial column sums over rows = q (mod 4)
-    bsum += __shfl_xor(bsum, 16, 64);
-    bsum += __shfl_xor(bsum, 32, 64);
+    bsum += lane_xor(bsum, 16);
+    bsum += lane_xor(bsum, 32);
     if (q == 0 && jok) {
       if (a.nsplit > 1) atomicAdd((float*)(P_<float>(T.gb[l]) + jb), bsum);
       else {

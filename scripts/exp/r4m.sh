@@ -1,7 +1,7 @@
 # Instruction mix / stall breakdown of the PPO-learner trunk kernels (scripts/exp/trunk_mix.py): three PMC passes.
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r4m
+O=gpurun_out/${TAG:-r4m}
 mkdir -p $O
 P1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAVE_CYCLES"
 P2="SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_BUSY_CYCLES"

@@ -26,7 +26,7 @@ def main():
     dy2, dy1 = torch.empty_like(y2), torch.empty_like(y1)
     biasp = torch.empty(B * 160, device=dev)
     for _ in range(10):
-        G.cnn_trunk_fwd(obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, mode=0)
+        G.cnn_trunk_fwd(obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, mode=int(os.environ.get("TRUNK_MODE", "3")))
     for _ in range(10):
         ops.cnn_trunk_bwd(dy3, W3.view(-1), y2, W2.view(-1), y1, dy2, dy1, biasp, None, 256)
     torch.cuda.synchronize()

@@ -576,7 +576,10 @@ class ActorCriticTrainer:
                         tr = self.mlp.transposes()
                     self._group_step = FusedGroupStep(opts, tr)
             if self._group_step is not None:
-                self._group_step.step()
+                t_off = getattr(self, "_t_off", None)
+                self._group_step.step(t_off=t_off)
+                if t_off is not None:
+                    self._t_offs_used += 1
                 if self.mlp is not None and self._group_step._trans is None:
                     self.mlp.sync_shadow()
                 return
@@ -720,12 +723,21 @@ class ActorCriticTrainer:
             # minibatch rows come from the keyed epoch permutation computed inside the fused kernel (no index list)
             mb = B // cfg.ppo_minibatches
             uc = self.update_counter.view(1)
+            # the grouped Adam launches of this update know their step (t + j + 1 for minibatch j): no per-launch
+            # step ticket, the counters advance once after the loop
+            offsets = self.cfg.engine_opts.adam_step_offsets and self.dp is None
+            self._t_offs_used = 0
             for ep in range(cfg.ppo_epochs):
                 for k in range(cfg.ppo_minibatches):
                     last = ep == cfg.ppo_epochs - 1 and k == cfg.ppo_minibatches - 1
+                    self._t_off = ep * cfg.ppo_minibatches + k if offsets else None
                     # the last minibatch's weight-gradient launch advances the update counter (no extra launch)
                     self._mlp_step(eng, mb, None, obs, actions, logp_old, adv, ret, v_old,
                                    perm=(uc, ep, k * mb, B, self.policy_seed), bump=self.update_counter if last else None)
+            self._t_off = None
+            if self._t_offs_used:
+                assert self._t_offs_used == cfg.ppo_epochs * cfg.ppo_minibatches
+                self._group_step.advance(self._t_offs_used)
         else:
             self._mlp_step(eng, B, None, obs, actions, logp_old, adv, ret, v_old)
             self.update_counter += 1

@@ -21,6 +21,7 @@ class EngineOpts:
     trunk_late_w: bool = True         # row-split trunk: conv2/conv3 weight fragments requested after conv1's MFMAs
     fused_env_split: bool = True      # per-env fused step (banks above trunk_rows_max_b): two workgroups per env
     trunk_fwd_staged: bool = True     # per-env trunk forward: bytes converted once into a bf16 LDS image (mode 3)
+    adam_step_offsets: bool = True    # MLP PPO: grouped Adam launches take their step from the minibatch index (no ticket)
     fc_max_planes: int = 32           # split-K partial planes of the rollout fc product (consumer-reduced)
     # -- learner -------------------------------------------------------------------------------------------------
     a2c_head: bool = True             # A2C: V(s_T) + returns + loss + head backward in one launch (loss.hip a2c_head)

@@ -233,7 +233,9 @@ class FusedGroupStep:
         return all((o.b1, o.b2, o.eps) == (o0.b1, o0.b2, o0.eps) for o in opts)
 
     @torch.no_grad()
-    def step(self):
+    def step(self, t_off=None):
+        """``t_off`` (Adam): this step is step ``t + t_off + 1`` of a sequence whose counters the caller advances
+        afterwards (:meth:`advance`) -- the launch skips the step ticket (one agent-scope atomic chain per launch)."""
         ops = _native.require()
         plain = [o for o in self.opts if o.max_grad_norm is not None and o.ext_parts is None and o.clip_value is None]
         if len(plain) > 1:
@@ -265,7 +267,14 @@ class FusedGroupStep:
         zero = all(o.zero_grad_after for o in self.opts)
         assert zero or not any(o.zero_grad_after for o in self.opts)
         ops.opt_multi(self._words, self._fvals, self._trans, self.adam, float(o0.b1), float(o0.b2), float(o0.eps),
-                      zero, o0.p)
+                      zero, o0.p, -1 if (t_off is None or not self.adam) else int(t_off))
+
+    def advance(self, n):
+        """After ``n`` steps taken with ``t_off`` = 0 .. n-1: the Adam step counters move by ``n`` (one device add
+        per group)."""
+        if self.adam:
+            for o in self.opts:
+                o.t.add_(float(n))
 
 
 SUMSQ_PARTS = 256   # optim.hip: partial slots of the global-norm reduction = max finaliser workgroups

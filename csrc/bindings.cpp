@@ -21,7 +21,7 @@ extern "C" {
 hipError_t aca_seg_stats(const float*, const int64_t*, int, float*, hipStream_t);
 hipError_t aca_colsum_reduce(const float*, int, int, float*, int, hipStream_t);
 hipError_t aca_mlp_tshadow(const aca::MlpTower*, int, int, hipStream_t);
-hipError_t aca_opt_multi(const int64_t*, const float*, const int64_t*, int, int, float, float, float, int,
+hipError_t aca_opt_multi(const int64_t*, const float*, const int64_t*, int, int, float, float, float, int, int,
                          hipStream_t);
 hipError_t aca_prp_perm(int64_t*, int, uint32_t, const int64_t*, int, hipStream_t);
 hipError_t aca_mlp_fwd(const aca::MlpArgs*, int, size_t, hipStream_t);
@@ -1100,7 +1100,7 @@ void mlp_rollout(Tensor desc, int64_t lds, Tensor obs, Tensor act, Tensor logp, 
 
 // words: CPU int64 [nseg, 11], fvals: CPU float [nseg, 4] (built once by ops/optim.py FusedGroupStep)
 void opt_multi(Tensor words, Tensor fvals, c10::optional<Tensor> trans, bool adam, double b1, double b2, double eps,
-               bool zero_grad, Tensor stream_ref) {
+               bool zero_grad, Tensor stream_ref, int64_t t_off) {
   TORCH_CHECK(!words.is_cuda() && words.scalar_type() == at::kLong && words.is_contiguous() && words.dim() == 2 &&
                   words.size(1) == 11, "opt_multi: words must be CPU int64 [nseg, 11]");
   TORCH_CHECK(!fvals.is_cuda() && fvals.scalar_type() == at::kFloat && fvals.is_contiguous() &&
@@ -1112,7 +1112,7 @@ void opt_multi(Tensor words, Tensor fvals, c10::optional<Tensor> trans, bool ada
     tp = ptr<int64_t>(*trans);
   }
   check(aca_opt_multi(ptr<int64_t>(words), ptr<float>(fvals), tp, (int)words.size(0), adam ? 1 : 0, (float)b1,
-                      (float)b2, (float)eps, zero_grad ? 1 : 0, cur_stream(stream_ref)),
+                      (float)b2, (float)eps, zero_grad ? 1 : 0, (int)t_off, cur_stream(stream_ref)),
         "opt_multi");
 }
 
@@ -1778,7 +1778,7 @@ TORCH_LIBRARY(acamd, m) {
   m.def("cast_bf16(Tensor x, Tensor y) -> ()");
   m.def("grad_move(Tensor src, Tensor dst) -> ()");
   m.def("opt_multi(Tensor words, Tensor fvals, Tensor? trans, bool adam, float b1, float b2, float eps, bool zero_grad, "
-        "Tensor stream_ref) -> ()");
+        "Tensor stream_ref, int t_off=-1) -> ()");
   m.def("prp_perm(Tensor out, int seed, Tensor uc, int epoch) -> ()");
   m.def("mlp_tshadow(Tensor desc, int ntw, int total) -> ()");
   m.def("mlp_fwd(Tensor desc, int tw_base, int ntw, int mode, int lds, Tensor obs, Tensor? idx, Tensor? perm_uc, "

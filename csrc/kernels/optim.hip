@@ -96,6 +96,9 @@ struct OptSeg {
   int nblocks;
   int ntrans;
   OptTrans tr[OPT_MAXT];
+  // >= 0: this launch is Adam step *t + t_off + 1 of a captured sequence whose counter the host advances once per
+  // update (the launch-time step is known), so no workgroup publishes t + 1 and the ticket is skipped; -1: ticket
+  int t_off = -1;
 };
 
 __device__ __forceinline__ void write_trans(const OptSeg& S, size_t i, float v) {
@@ -121,7 +124,7 @@ __device__ __forceinline__ void opt_body(const OptSeg& S, float b1, float b2, fl
   float* __restrict__ v = S.v;
   const size_t n = S.n;
   const float lr = *S.lr;
-  const float t = ADAM ? (*S.t + 1.0f) : 0.f;
+  const float t = ADAM ? (*S.t + 1.0f + (S.t_off > 0 ? (float)S.t_off : 0.f)) : 0.f;
   float scale = 1.f;
   if (S.parts) {
     const float gsq = partial_total(S.parts, shr) * S.norm_mul;
@@ -185,7 +188,7 @@ __device__ __forceinline__ void opt_body(const OptSeg& S, float b1, float b2, fl
       if (S.ntrans) write_trans(S, i, pi);
     }
   }
-  if (ADAM) {
+  if (ADAM && S.t_off < 0) {
     // The last workgroup to finish publishes t + 1. Only a COUNT is needed (no data hand-off), so the ticket is a
     // relaxed atomic with no release fence: a fenced last-arriver ticket (last_block_arrival) costs every workgroup
     // an agent-scope release -- an L2 write-back on this multi-XCD part -- which was 60 us of a 70 us step over a
@@ -542,7 +545,8 @@ extern "C" hipError_t aca_rmsprop_step(float* p, float* g, float* v, size_t n, c
 // Multi-group step. segs: nseg records of 16 words (see ops/optim.py FusedGroupStep): p, g, m, v, n, lr, t, parts,
 // gnorm_out, shadow, ticket (pointers / sizes as 64-bit words) and clip, max_norm, gmul, norm_mul (floats).
 extern "C" hipError_t aca_opt_multi(const int64_t* words, const float* fvals, const int64_t* trans, int nseg,
-                                    int adam, float b1, float b2, float eps, int zero_grad, hipStream_t stream) {
+                                    int adam, float b1, float b2, float eps, int zero_grad, int t_off,
+                                    hipStream_t stream) {
   if (nseg < 1 || nseg > OPT_MAXSEG) return hipErrorInvalidValue;
   OptMulti M{};
   M.nseg = nseg;
@@ -566,6 +570,7 @@ extern "C" hipError_t aca_opt_multi(const int64_t* words, const float* fvals, co
     S.max_norm = f[1];
     S.gmul = f[2];
     S.norm_mul = f[3];
+    S.t_off = t_off < 0 ? -1 : t_off;
     if (S.n == 0 || !opt_aligned(S.p, S.g, adam ? S.m : S.v, S.v, S.shadow)) return hipErrorInvalidValue;
     if (adam && (!S.m || !S.t || !S.ticket)) return hipErrorInvalidValue;
     S.nblocks = opt_grid(S.n);

@@ -326,3 +326,28 @@ def test_register_move_wave_reductions_are_bit_identical_to_bpermute(cuda):
     fin = torch.isfinite(out[:, 1]).all(dim=1)
     ref = x.double().sum(dim=1)
     assert torch.allclose(out[fin, 1, 0].double(), ref[fin], rtol=1e-4, atol=1e-3 * x.abs().max().item())
+
+
+def test_mlp_ppo_adam_step_offsets_equal_ticket(cuda):
+    """MuJoCo-shape PPO (MLP engine, separate actor / critic Adam in one opt_multi launch per minibatch): the grouped
+    Adam launches taking their step from the minibatch index (no per-launch step ticket, counters advanced once per
+    update) == the ticket form bit for bit -- parameters, Adam moments and step counters over captured updates."""
+    from actor_critic_algs_on_tensorflow_amd import preset
+    from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
+    runs = []
+    for offsets in (True, False):
+        tr = ActorCriticTrainer(preset("mujoco_ppo_dp8", num_envs=16, n_steps=32, ppo_epochs=2, ppo_minibatches=4,
+                                       device="cuda:0", outdir=None, quiet=True, stdout_freq=0, save_every=0, seed=2,
+                                       engine_opts=dict(adam_step_offsets=offsets)))
+        tr.capture(warmup=1)
+        for _ in range(3):
+            tr.step()
+        torch.cuda.synchronize()
+        state = [tr.flat.data.clone()]
+        for o in tr.opts.values():
+            state += [o.m.clone(), o.v.clone(), o.t.clone()]
+        runs.append(state)
+        t = float(list(tr.opts.values())[0].t)
+        assert t >= 3 * 8 and t % 8 == 0, t   # whole updates of 2 x 4 minibatch steps
+    for k, (a, b) in enumerate(zip(*runs)):
+        assert torch.equal(a, b), k

@@ -1,0 +1,79 @@
+// L2 -> CU streaming rate probe: every workgroup (one per CU, 256 threads) reads the SAME L2-resident buffer REPS
+// times, fully coalesced 16-byte loads (a wave load = 1 KB contiguous), U loads in flight per thread; variants:
+// plain global_load_dwordx4 into registers, and LDS-DMA (global_load_lds_dwordx4). Prints bytes per clock per CU
+// (clock from s_memtime deltas over s_memrealtime) for 1 and all 256 CUs.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <vector>
+
+template <int U, bool DMA>
+__global__ void __launch_bounds__(256) probe(const uint4* __restrict__ buf, int n16, int reps, float* sink,
+                                             unsigned long long* clk) {
+  __shared__ __attribute__((aligned(16))) uint4 lds[U * 256];
+  const int tid = threadIdx.x;
+  unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+  uint4 acc = make_uint4(0, 0, 0, 0);
+  for (int r = 0; r < reps; ++r) {
+    for (int i0 = 0; i0 < n16; i0 += 256 * U) {
+      if constexpr (DMA) {
+        const int lane = tid & 63, wid = tid >> 6;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int i = i0 + u * 256 + wid * 64 + lane;
+          __builtin_amdgcn_global_load_lds(buf + (i < n16 ? i : 0),
+                                           (__attribute__((address_space(3))) void*)(lds + u * 256 + wid * 64), 16,
+                                           0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else {
+        uint4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int i = i0 + u * 256 + tid;
+          v[u] = buf[i < n16 ? i : 0];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) { acc.x ^= v[u].x; acc.y ^= v[u].y; acc.z ^= v[u].z; acc.w ^= v[u].w; }
+      }
+    }
+  }
+  unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+  if (tid == 0) { clk[blockIdx.x * 2] = t1 - t0; clk[blockIdx.x * 2 + 1] = r1 - r0; }
+  if (acc.x == 0x12345678u && acc.y == 1u) sink[0] = 1.f;   // keep the loads
+  if constexpr (DMA) { if (tid == 0 && lds[1].x == 0x12345678u) sink[1] = 1.f; }
+}
+
+template <int U, bool DMA>
+void run(const uint4* d, int n16, int reps, float* sink, unsigned long long* clk, int grid) {
+  probe<U, DMA><<<grid, 256>>>(d, n16, 1, sink, clk);   // warm L2
+  hipDeviceSynchronize();
+  probe<U, DMA><<<grid, 256>>>(d, n16, reps, sink, clk);
+  hipDeviceSynchronize();
+  std::vector<unsigned long long> h(2 * grid);
+  hipMemcpy(h.data(), clk, 16 * grid, hipMemcpyDeviceToHost);
+  double cyc = 0, us = 0;
+  for (int b = 0; b < grid; ++b) { cyc += h[2 * b]; us += h[2 * b + 1] * 0.01; }
+  cyc /= grid; us /= grid;
+  const double bytes = (double)n16 * 16 * reps;
+  printf("%-5s U=%2d grid=%3d buf=%4d KB: %.1f B/clk/CU (shader clock %.2f GHz), %.1f GB/s per CU, %.2f TB/s total\n",
+         DMA ? "dma" : "load", U, grid, n16 * 16 / 1024, bytes / cyc, cyc / us / 1e3, bytes / us / 1e3,
+         bytes / us / 1e6 * grid);
+}
+
+int main() {
+  const int n16 = 256 * 1024 / 16;   // 256 KB, L2-resident
+  uint4* d; float* sink; unsigned long long* clk;
+  hipMalloc(&d, n16 * 16); hipMalloc(&sink, 64); hipMalloc(&clk, 16 * 256);
+  hipMemset(d, 1, n16 * 16);
+  for (int grid : {1, 256}) {
+    run<4, false>(d, n16, 20, sink, clk, grid);
+    run<8, false>(d, n16, 20, sink, clk, grid);
+    run<16, false>(d, n16, 20, sink, clk, grid);
+    run<4, true>(d, n16, 20, sink, clk, grid);
+    run<8, true>(d, n16, 20, sink, clk, grid);
+  }
+  hipFree(d); hipFree(sink); hipFree(clk);
+  return 0;
+}

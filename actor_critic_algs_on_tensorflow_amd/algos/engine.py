@@ -171,8 +171,39 @@ class CNNEngine:
         self.Wh, self.gWh, self.sWh = views(net.heads.kernel)
         self.bh, self.gbh, _ = views(net.heads.bias)
         self._bufs = {}
+        # fragment-ordered bf16 copies of the conv weights (ops/optim.py frag_order), rewritten by the optimiser step
+        # itself (FusedAdam.set_frag): the fused trunk kernels' weight loads read 1 KB per wave contiguously instead
+        # of 16 rows x 64 bytes (profiles/r4_l2_stream_probe.txt: 16 vs ~60 B/clk/CU from L2)
+        self.frag = None
+        if o.frag_weights and self.dev.type == "cuda" and implicit:
+            self.frag = [torch.empty(n, dtype=torch.bfloat16, device=self.dev) for n in (32 * 256, 64 * 512, 64 * 576)]
+            self.sync_frag()
         self.side = torch.cuda.Stream(device=self.dev) if self.dev.type == "cuda" else None
         self._ev = [torch.cuda.Event() for _ in range(6)] if self.side is not None else None
+
+    _FRAG_SHAPES = ((32, 256), (64, 512), (64, 576))
+
+    def frag_entries(self):
+        """(fp32 W view, rows, cols, fragment-ordered bf16 copy) of conv1..3 for the optimiser (``set_frag``)."""
+        if self.frag is None:
+            return []
+        return [(W, K, N, F) for W, (K, N), F in zip((self.W1, self.W2, self.W3), self._FRAG_SHAPES, self.frag)]
+
+    @torch.no_grad()
+    def sync_frag(self):
+        """Rebuild the fragment-ordered copies from the bf16 shadow (parameters changed outside the optimiser:
+        construction, checkpoint load, parameter-server pull)."""
+        if self.frag is None:
+            return
+        from ..ops.optim import frag_order
+        for S, (K, N), F in zip((self.sW1, self.sW2, self.sW3), self._FRAG_SHAPES, self.frag):
+            F.copy_(frag_order(S, K, N))
+
+    def trunk_w(self):
+        """(W1, W2, W3) operands of the fused trunk kernels and whether they are fragment-ordered."""
+        if self.frag is not None:
+            return (*self.frag, True)
+        return (self.sW1, self.sW2, self.sW3, False)
 
     def bufs(self, B, with_grad=False):
         key = (B, with_grad)
@@ -250,9 +281,14 @@ class CNNEngine:
         shifted = False
         want_shift = shift_out is not None
         if self.implicit and B <= self.fused_trunk_max_b:
-            G.cnn_trunk_fwd(obs, self.sW1, self.b1, self.sW2, self.b2, self.sW3, self.b3, b.y1, b.y2, b.y3,
-                            shift_out=shift_out, mode=self.trunk_mode if B <= self.trunk_rows_max_b else
-                            (3 if self.opts.trunk_fwd_staged else 0), obs_idx=obs_idx)
+            if B > self.trunk_rows_max_b and self.opts.trunk_fwd_staged and self.frag is not None:
+                F1, F2, F3 = self.frag   # mode 5: the bf16-staged kernel on the fragment-ordered weights
+                G.cnn_trunk_fwd(obs, F1, self.b1, F2, self.b2, F3, self.b3, b.y1, b.y2, b.y3, shift_out=shift_out,
+                                mode=5, obs_idx=obs_idx)
+            else:
+                G.cnn_trunk_fwd(obs, self.sW1, self.b1, self.sW2, self.b2, self.sW3, self.b3, b.y1, b.y2, b.y3,
+                                shift_out=shift_out, mode=self.trunk_mode if B <= self.trunk_rows_max_b else
+                                (3 if self.opts.trunk_fwd_staged else 0), obs_idx=obs_idx)
             shifted = shift_out is not None
         elif self.implicit:
             G.gemm(obs, 0, True, self.sW1, 256, True, b.y1, 32, 1, B * 400, 32, 256, bias=self.b1, relu=True,

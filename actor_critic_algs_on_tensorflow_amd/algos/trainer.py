@@ -159,6 +159,13 @@ class ActorCriticTrainer:
             if dp is not None:
                 opt.grad_mul = dp.grad_mul   # the all-reduce leaves the sum; the update kernel averages on read
             self.opts[g] = opt
+        if self.engine is not None and self.engine.frag is not None:
+            # the group holding the conv weights also rewrites their fragment-ordered copies in its update
+            ent = self.engine.frag_entries()
+            owner = [o for o in self.opts.values()
+                     if all(0 <= W.data_ptr() - o.p.data_ptr() < o.p.numel() * 4 for W, _, _, _ in ent)]
+            assert len(owner) == 1, "the conv weights must live in one optimiser group"
+            owner[0].set_frag(ent)
         self.actor_opt = self.opts.get("actor", self.opts.get("shared"))
         if (self.engine is not None and dp is None and len(self.opts) == 1
                 and all(o.clip_value is None for o in self.opts.values())):
@@ -347,6 +354,7 @@ class ActorCriticTrainer:
         ops = _native.require()
         T = st.T
         rows = (lambda t: lb.rows(t * N, N)) if lb is not None else (lambda t: b)
+        _, W2, W3, frag = eng.trunk_w()   # conv2 / conv3 operands (fragment-ordered copies when kept)
         eng.forward(st.obs[0], rows(0), head=False, shift_out=st.obs[1], fc_parts=True)
         for t in range(T):
             hp, S = eng.last_fc
@@ -357,8 +365,8 @@ class ActorCriticTrainer:
                                 st.values[t], KEY_ENV_BITS, self.policy_seed, env.state, env.t, env.tg, env.ep_ret,
                                 sn, tn, tgn, ern, env.ep_stats, env.env_ids, st.obs[t], st.obs[t + 1],
                                 st.rewards[t], st.dones[t], st.truncated[t], env.seed, env.max_episode_steps, hp, S,
-                                eng.bfc, eng.sW1, eng.b1, eng.sW2, eng.b2, eng.sW3, eng.b3, nxt.y1, nxt.y2, nxt.y3,
-                                1.0 / 255.0, st.obs[t + 2] if t + 2 <= T else None, None)
+                                eng.bfc, eng.sW1, eng.b1, W2, eng.b2, W3, eng.b3, nxt.y1, nxt.y2, nxt.y3,
+                                1.0 / 255.0, st.obs[t + 2] if t + 2 <= T else None, None, frag)
             env.flip()
             nxt.obs = st.obs[t + 1]
             eng.fc_planes(nxt)
@@ -379,6 +387,7 @@ class ActorCriticTrainer:
         ops = _native.require()
         T = st.T
         split = eng.opts.fused_env_split
+        _, W2, W3, frag = eng.trunk_w()
         rows = (lambda t: lb.rows(t * N, N)) if lb is not None else (lambda t: b)
         eng.forward(st.obs[0], rows(0), head=False, shift_out=st.obs[1], fc_parts=True)
         for t in range(T):
@@ -389,9 +398,9 @@ class ActorCriticTrainer:
                                     st.values[t], KEY_ENV_BITS, self.policy_seed, env.state, env.t, env.tg,
                                     env.ep_ret, env.ep_stats, env.env_ids, st.obs[t + 1], st.rewards[t], st.dones[t],
                                     st.truncated[t], env.seed, env.max_episode_steps, hp, S, eng.bfc, eng.sW1,
-                                    eng.b1, eng.sW2, eng.b2, eng.sW3, eng.b3, nxt.y1, nxt.y2, nxt.y3, 1.0 / 255.0,
+                                    eng.b1, W2, eng.b2, W3, eng.b3, nxt.y1, nxt.y2, nxt.y3, 1.0 / 255.0,
                                     st.obs[t + 2] if t + 2 <= T else None,
-                                    list(env.next_state()) if split else None)
+                                    list(env.next_state()) if split else None, None, frag)
             if split:
                 env.flip()
             nxt.obs = st.obs[t + 1]
@@ -501,6 +510,8 @@ class ActorCriticTrainer:
         self.flat.grad.zero_()
         if self.shadow is not None:
             self.shadow.copy_(self.flat.data)
+        if self.engine is not None:
+            self.engine.sync_frag()
         if self.mlp is not None:
             self.mlp.sync_shadow()
 

@@ -231,6 +231,8 @@ def load_trainer(trainer, path):
     # the model parameters are views into the flat slab; refresh the bf16 shadow of the native engine
     if trainer.shadow is not None:
         trainer.shadow.copy_(trainer.flat.data)
+        if getattr(trainer, "engine", None) is not None:   # the engine's fragment-ordered conv weight copies
+            trainer.engine.sync_frag()
     if getattr(trainer, "mlp", None) is not None:   # transposed weight shadows of the MLP engine
         trainer.mlp.sync_shadow()
     for g, opt in trainer.opts.items():

@@ -22,6 +22,8 @@ class EngineOpts:
     fused_env_split: bool = True      # per-env fused step (banks above trunk_rows_max_b): two workgroups per env
     trunk_fwd_staged: bool = True     # per-env trunk forward: bytes converted once into a bf16 LDS image (mode 3)
     adam_step_offsets: bool = True    # MLP PPO: grouped Adam launches take their step from the minibatch index (no ticket)
+    frag_weights: bool = True         # conv weights also kept fragment-ordered (written by the optimiser step): the
+                                      # MFMA weight loads become one contiguous 1 KB read per wave
     fc_max_planes: int = 32           # split-K partial planes of the rollout fc product (consumer-reduced)
     # -- learner -------------------------------------------------------------------------------------------------
     a2c_head: bool = True             # A2C: V(s_T) + returns + loss + head backward in one launch (loss.hip a2c_head)

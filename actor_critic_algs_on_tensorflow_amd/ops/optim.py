@@ -93,10 +93,33 @@ class FusedAdam:
         self.grad_mul = 1.0
         # sumsq partials already produced by the gradient kernel (MLP engine): the norm needs no extra launch
         self.ext_parts = None
+        # fragment-ordered bf16 copies of some weights, written by the update (set_frag)
+        self.frag = []
+        self._frag_table = None
 
     def bind_grad(self, grad_slab):
         """Read gradients from this group's segment of another slab (lag-1 DP reads the all-reduced copy)."""
         self.g = grad_slab[self.start:self.end]
+
+    def set_frag(self, entries):
+        """Fragment-ordered bf16 weight copies the update writes as it goes (``optim.hip`` OptTrans with ldt < 0):
+        ``entries`` = [(W fp32 view into this group, K rows, N cols, dst bf16 [K * N])]; the CNN engine's MFMA
+        kernels read them as one contiguous 1 KB load per wave fragment (``cnn_fused.hip`` frag_w1..3)."""
+        self.frag = list(entries)
+        self._frag_table = None
+        if not self.frag:
+            return
+        t = torch.zeros(6, 5, dtype=torch.int64)
+        for e, (W, K, N, dst) in enumerate(self.frag):
+            off = (W.data_ptr() - self.p.data_ptr()) // 4
+            assert 0 <= off and off + K * N <= self.p.numel() and W.numel() == K * N
+            assert K % 16 == 0 and N % 32 == 0 and dst.dtype == torch.bfloat16 and dst.numel() == K * N
+            t[e] = torch.tensor([off, K, N, -1, dst.data_ptr()])
+        self._frag_table = t
+
+    def _torch_frag(self):
+        for W, K, N, dst in getattr(self, "frag", ()):
+            dst.copy_(frag_order(W, K, N))
 
     def set_lr(self, lr):
         self.lr.fill_(float(lr))
@@ -135,7 +158,8 @@ class FusedAdam:
                       float(self.b1), float(self.b2), float(self.eps),
                       float(self.clip_value) if self.clip_value is not None else -1.0,
                       float(self.max_grad_norm) if self.max_grad_norm is not None else -1.0, self._ticket,
-                      bool(self.zero_grad_after), float(self.grad_mul), float(self._norm_mul))
+                      bool(self.zero_grad_after), float(self.grad_mul), float(self._norm_mul),
+                      getattr(self, "_frag_table", None))
 
     def _torch_step(self):
         g = self.g * self.grad_mul if self.grad_mul != 1.0 else self.g
@@ -152,6 +176,7 @@ class FusedAdam:
         self.p.sub_(lr_t * self.m / (torch.sqrt(self.v) + self.eps))
         if self.shadow is not None:
             self.shadow.copy_(self.p)
+        self._torch_frag()
 
     def state_dict(self):
         return {"m": self.m, "v": self.v, "t": self.t, "lr": self.lr}
@@ -180,7 +205,8 @@ class FusedRMSprop(FusedAdam):
                          float(self.alpha), float(self.eps),
                          float(self.clip_value) if self.clip_value is not None else -1.0,
                          float(self.max_grad_norm) if self.max_grad_norm is not None else -1.0,
-                         bool(self.zero_grad_after), float(self.grad_mul), float(self._norm_mul))
+                         bool(self.zero_grad_after), float(self.grad_mul), float(self._norm_mul),
+                         getattr(self, "_frag_table", None))
 
     def _torch_step(self):
         g = self.g * self.grad_mul if self.grad_mul != 1.0 else self.g
@@ -194,6 +220,7 @@ class FusedRMSprop(FusedAdam):
         self.p.sub_(self.lr * g / torch.sqrt(self.v + self.eps))
         if self.shadow is not None:
             self.shadow.copy_(self.p)
+        self._torch_frag()
 
 
 class FusedGroupStep:
@@ -212,14 +239,19 @@ class FusedGroupStep:
         self._key = None
         self._words = self._fvals = None
         self._trans = None
-        if transposes is not None:
+        frag = [getattr(o, "_frag_table", None) for o in self.opts]
+        if transposes is not None or any(f is not None for f in frag):
             t = torch.zeros(len(self.opts), self.MAXT, 5, dtype=torch.int64)
-            for k, (o, lst) in enumerate(zip(self.opts, transposes)):
-                assert len(lst) <= self.MAXT
+            for k, o in enumerate(self.opts):
+                lst = transposes[k] if transposes is not None else []
+                nf = len(o.frag) if frag[k] is not None else 0
+                assert len(lst) + nf <= self.MAXT
                 for e, (W, K, N, Wt) in enumerate(lst):
                     off = (W.data_ptr() - o.p.data_ptr()) // 4
                     assert 0 <= off and off + K * N <= o.p.numel()
                     t[k, e] = torch.tensor([off, K, N, Wt.shape[1], Wt.data_ptr()])
+                if nf:
+                    t[k, len(lst):len(lst) + nf] = frag[k][:nf]
             self._trans = t
 
     @staticmethod
@@ -275,6 +307,12 @@ class FusedGroupStep:
         if self.adam:
             for o in self.opts:
                 o.t.add_(float(n))
+
+
+def frag_order(W, K, N):
+    """bf16 fragment-ordered copy of the row-major [K][N] weight ``W`` (``optim.hip`` OptTrans, ldt < 0): MFMA
+    fragment (16-row tile, 32-wide k-step) of lane ``lg * 16 + row16`` at ((tile * N / 32 + kstep) * 64 + lane) * 8."""
+    return W.reshape(K // 16, 16, N // 32, 4, 8).permute(0, 2, 3, 1, 4).reshape(-1).to(torch.bfloat16)
 
 
 SUMSQ_PARTS = 256   # optim.hip: partial slots of the global-norm reduction = max finaliser workgroups

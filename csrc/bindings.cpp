@@ -53,13 +53,13 @@ hipError_t aca_pong_fused_step(uint16_t*, const float*, int, int64_t, const floa
                                float*, float*, int32_t*, int64_t*, float*, float*, const int64_t*, const uint8_t*,
                                uint8_t*, float*, uint8_t*, uint8_t*, uint32_t, int, const uint16_t*, const float*,
                                const uint16_t*, const float*, const uint16_t*, const float*, uint16_t*, uint16_t*,
-                               uint16_t*, float, uint8_t*, uint64_t*, int, hipStream_t);
+                               uint16_t*, float, uint8_t*, uint64_t*, int, int, hipStream_t);
 hipError_t aca_pong_fused_env_step(uint16_t*, const float*, int, int64_t, const float*, const uint16_t*, const float*,
                                    int, float*, int32_t*, float*, float*, float*, int, uint32_t, float*, int32_t*,
                                    int64_t*, float*, float*, const int64_t*, uint8_t*, float*, uint8_t*, uint8_t*,
                                    uint32_t, int, const uint16_t*, const float*, const uint16_t*, const float*,
                                    const uint16_t*, const float*, uint16_t*, uint16_t*, uint16_t*, float, uint8_t*,
-                                   float*, int32_t*, int64_t*, float*, uint64_t*, int, hipStream_t);
+                                   float*, int32_t*, int64_t*, float*, uint64_t*, int, int, hipStream_t);
 hipError_t aca_wave_reduce_check(const float*, float*, int, hipStream_t);
 hipError_t aca_categorical_sample(const float*, int, int, int, const int64_t*, const int64_t*, const int64_t*, int,
                                   uint32_t, int32_t*, float*, float*, float*, hipStream_t);
@@ -89,9 +89,10 @@ hipError_t aca_sumsq(const float*, size_t, float*, hipStream_t);
 hipError_t aca_sumsq_multi(const float* const*, const size_t*, float* const*, int, hipStream_t);
 int aca_sumsq_parts();
 hipError_t aca_adam_step(float*, float*, float*, float*, size_t, const float*, float*, const float*, float*, uint16_t*,
-                         float, float, float, float, float, unsigned int*, int, float, float, hipStream_t);
+                         float, float, float, float, float, unsigned int*, int, float, float, const int64_t*,
+                         hipStream_t);
 hipError_t aca_rmsprop_step(float*, float*, float*, size_t, const float*, const float*, float*, uint16_t*, float, float,
-                            float, float, int, float, float, hipStream_t);
+                            float, float, int, float, float, const int64_t*, hipStream_t);
 hipError_t aca_cast_bf16(const float*, uint16_t*, size_t, hipStream_t);
 hipError_t aca_grad_move(float*, float*, size_t, hipStream_t);
 hipError_t aca_gemm_run(const AcaGemmDesc*, hipStream_t);
@@ -113,7 +114,7 @@ hipError_t aca_cnn_trunk_fwd(const uint8_t*, const uint16_t*, const float*, cons
                              uint64_t*, const int64_t*, hipStream_t);
 hipError_t aca_cnn_trunk_fwd_s16(const uint8_t*, const uint16_t*, const float*, const uint16_t*, const float*,
                                  const uint16_t*, const float*, uint16_t*, uint16_t*, uint16_t*, int, float, uint8_t*,
-                                 const int64_t*, hipStream_t);
+                                 const int64_t*, int, hipStream_t);
 hipError_t aca_grad_finalize(const int64_t*, int, float*, hipStream_t);
 hipError_t aca_head_bwd(const float*, const int32_t*, const float*, const float*, const float*, float, const float*,
                         const float*, const uint8_t*, int, int, int, int, int, float, float, float*, float*,
@@ -320,7 +321,8 @@ void pong_fused_step(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, Tenso
                      Tensor prev, Tensor out, Tensor reward, Tensor done, Tensor trunc, int64_t seed,
                      int64_t max_steps, Tensor hpart, int64_t planes, Tensor bfc, Tensor W1, Tensor b1, Tensor W2,
                      Tensor b2, Tensor W3, Tensor b3, Tensor y1, Tensor y2, Tensor y3, double scale,
-                     c10::optional<Tensor> shift_out, c10::optional<Tensor> stamps) {
+                     c10::optional<Tensor> shift_out, c10::optional<Tensor> stamps, bool frag) {
+  // frag: W2 / W3 are the fragment-ordered copies (ops/optim.py frag_order); W1 row-major
   check_env(state, t, tg, ep_ret, ep_stats, ids, reward, done, trunc);
   check_env(state_n, t_n, tg_n, ep_ret_n, ep_stats, ids, reward, done, trunc);
   for (auto* x : {&h, &Wh, &W1, &W2, &W3, &y1, &y2, &y3}) need(*x, at::kBFloat16, "pong_fused_step bf16");
@@ -365,7 +367,7 @@ void pong_fused_step(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, Tenso
                             ptr<uint8_t>(done), ptr<uint8_t>(trunc), (uint32_t)seed, (int)max_steps,
                             ptr<uint16_t>(W1), ptr<float>(b1), ptr<uint16_t>(W2), ptr<float>(b2), ptr<uint16_t>(W3),
                             ptr<float>(b3), ptr<uint16_t>(y1), ptr<uint16_t>(y2), ptr<uint16_t>(y3), (float)scale,
-                            so, stamps_ptr(stamps, N * 7), N, cur_stream(state)),
+                            so, stamps_ptr(stamps, N * 7), frag ? 1 : 0, N, cur_stream(state)),
         "pong_fused_step");
 }
 
@@ -380,7 +382,8 @@ void pong_fused_env_step(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, T
                          int64_t seed, int64_t max_steps, Tensor hpart, int64_t planes, Tensor bfc, Tensor W1,
                          Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, Tensor y1, Tensor y2, Tensor y3,
                          double scale, c10::optional<Tensor> shift_out, c10::optional<std::vector<Tensor>> next_state,
-                         c10::optional<Tensor> stamps) {
+                         c10::optional<Tensor> stamps, bool frag) {
+  // frag: W2 / W3 are the fragment-ordered copies (ops/optim.py frag_order); W1 row-major
   check_env(state, t, tg, ep_ret, ep_stats, ids, reward, done, trunc);
   float* sn = nullptr; int32_t* tn = nullptr; int64_t* tgn = nullptr; float* ern = nullptr;
   if (next_state.has_value()) {
@@ -431,7 +434,7 @@ void pong_fused_env_step(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, T
                                 ptr<uint16_t>(W1), ptr<float>(b1), ptr<uint16_t>(W2), ptr<float>(b2),
                                 ptr<uint16_t>(W3), ptr<float>(b3), ptr<uint16_t>(y1), ptr<uint16_t>(y2),
                                 ptr<uint16_t>(y3), (float)scale, so, sn, tn, tgn, ern, stamps_ptr(stamps, sn ? 2 * N : N),
-                                N, cur_stream(state)),
+                                frag ? 1 : 0, N, cur_stream(state)),
         "pong_fused_env_step");
 }
 
@@ -790,9 +793,18 @@ uint16_t* shadow_ptr(const c10::optional<Tensor>& shadow, const Tensor& p, const
   return ptr<uint16_t>(*shadow);
 }
 
+// trans: optional CPU int64 [6, 5] table of weight copies the update writes as it goes (optim.hip OptTrans)
+static const int64_t* trans_table(const c10::optional<Tensor>& trans, const char* who) {
+  if (!(trans.has_value() && trans->defined())) return nullptr;
+  TORCH_CHECK(!trans->is_cuda() && trans->scalar_type() == at::kLong && trans->is_contiguous() &&
+                  trans->numel() == 6 * 5, who, ": trans must be CPU int64 [6, 5]");
+  return ptr<int64_t>(*trans);
+}
+
 void adam_step(Tensor p, Tensor g, Tensor m, Tensor v, Tensor lr, Tensor t, c10::optional<Tensor> gnorm_parts,
                c10::optional<Tensor> gnorm_out, c10::optional<Tensor> shadow, double b1, double b2, double eps,
-               double clip, double max_norm, Tensor ticket, bool zero_grad, double gmul, double norm_mul) {
+               double clip, double max_norm, Tensor ticket, bool zero_grad, double gmul, double norm_mul,
+               c10::optional<Tensor> trans) {
   need(p, at::kFloat, "p");
   need(g, at::kFloat, "g");
   need(m, at::kFloat, "m");
@@ -805,13 +817,15 @@ void adam_step(Tensor p, Tensor g, Tensor m, Tensor v, Tensor lr, Tensor t, c10:
   check(aca_adam_step(ptr<float>(p), ptr<float>(g), ptr<float>(m), ptr<float>(v), p.numel(), ptr<float>(lr),
                       ptr<float>(t), gnorm_parts_ptr(gnorm_parts, max_norm, "adam"), optr<float>(gnorm_out),
                       shadow_ptr(shadow, p, "adam"), (float)b1, (float)b2, (float)eps, (float)clip, (float)max_norm,
-                      ptr<unsigned int>(ticket), zero_grad ? 1 : 0, (float)gmul, (float)norm_mul, cur_stream(p)),
+                      ptr<unsigned int>(ticket), zero_grad ? 1 : 0, (float)gmul, (float)norm_mul,
+                      trans_table(trans, "adam_step"), cur_stream(p)),
         "adam_step");
 }
 
 void rmsprop_step(Tensor p, Tensor g, Tensor v, Tensor lr, c10::optional<Tensor> gnorm_parts,
                   c10::optional<Tensor> gnorm_out, c10::optional<Tensor> shadow, double alpha, double eps,
-                  double clip, double max_norm, bool zero_grad, double gmul, double norm_mul) {
+                  double clip, double max_norm, bool zero_grad, double gmul, double norm_mul,
+                  c10::optional<Tensor> trans) {
   need(p, at::kFloat, "p");
   need(g, at::kFloat, "g");
   need(v, at::kFloat, "v");
@@ -820,7 +834,8 @@ void rmsprop_step(Tensor p, Tensor g, Tensor v, Tensor lr, c10::optional<Tensor>
   check(aca_rmsprop_step(ptr<float>(p), ptr<float>(g), ptr<float>(v), p.numel(), ptr<float>(lr),
                          gnorm_parts_ptr(gnorm_parts, max_norm, "rmsprop"), optr<float>(gnorm_out),
                          shadow_ptr(shadow, p, "rmsprop"), (float)alpha, (float)eps, (float)clip, (float)max_norm,
-                         zero_grad ? 1 : 0, (float)gmul, (float)norm_mul, cur_stream(p)),
+                         zero_grad ? 1 : 0, (float)gmul, (float)norm_mul, trans_table(trans, "rmsprop_step"),
+                         cur_stream(p)),
         "rmsprop_step");
 }
 
@@ -1422,7 +1437,7 @@ void cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tenso
   const int64_t* idxp = nullptr;
   if (obs_idx.has_value() && obs_idx->defined()) {   // sample b = row obs_idx[b] of obs (per-env mode 0 only)
     need(*obs_idx, at::kLong, "obs_idx");
-    TORCH_CHECK(mode == 0 || mode == 3, "cnn_trunk_fwd: obs_idx needs a per-env mode");
+    TORCH_CHECK(mode == 0 || mode == 3 || mode == 5, "cnn_trunk_fwd: obs_idx needs a per-env mode");
     B = obs_idx->numel();
     idxp = obs_idx->data_ptr<int64_t>();
   }
@@ -1458,15 +1473,17 @@ void cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tenso
           "cnn_trunk_rows");
     return;
   }
-  if (mode == 3) {   // the per-env bf16-staged kernel (one byte conversion per pixel; the learner's minibatch trunk)
+  if (mode == 3 || mode == 5) {   // the per-env bf16-staged kernel (one byte conversion per pixel); mode 5: W1..W3
+    // are the fragment-ordered copies (frag_weights)
     TORCH_CHECK(!stamps.has_value() || !stamps->defined(), "cnn_trunk_fwd: mode 3 has no phase stamps");
     check(aca_cnn_trunk_fwd_s16(ptr<uint8_t>(obs), ptr<uint16_t>(W1), ptr<float>(b1), ptr<uint16_t>(W2),
                                 ptr<float>(b2), ptr<uint16_t>(W3), ptr<float>(b3), ptr<uint16_t>(y1),
-                                ptr<uint16_t>(y2), ptr<uint16_t>(y3), (int)B, (float)scale, so, idxp, cur_stream(obs)),
+                                ptr<uint16_t>(y2), ptr<uint16_t>(y3), (int)B, (float)scale, so, idxp,
+                                mode == 5 ? 1 : 0, cur_stream(obs)),
           "cnn_trunk_fwd_s16");
     return;
   }
-  TORCH_CHECK(mode == 0, "cnn_trunk_fwd: mode must be 0..3");
+  TORCH_CHECK(mode == 0, "cnn_trunk_fwd: mode must be 0..3 or 5");
   check(aca_cnn_trunk_fwd(ptr<uint8_t>(obs), ptr<uint16_t>(W1), ptr<float>(b1), ptr<uint16_t>(W2), ptr<float>(b2),
                           ptr<uint16_t>(W3), ptr<float>(b3), ptr<uint16_t>(y1), ptr<uint16_t>(y2), ptr<uint16_t>(y3),
                           (int)B, (float)scale, so, stamps_ptr(stamps, B), idxp, cur_stream(obs)),
@@ -1737,12 +1754,13 @@ TORCH_LIBRARY(acamd, m) {
         "Tensor t_n, Tensor tg_n, Tensor ep_ret_n, Tensor ep_stats, Tensor env_ids, Tensor prev, Tensor out, "
         "Tensor reward, Tensor done, Tensor truncated, int seed, int max_steps, Tensor hpart, int planes, "
         "Tensor bfc, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, Tensor y1, Tensor y2, "
-        "Tensor y3, float scale, Tensor? shift_out=None, Tensor? stamps=None) -> ()");
+        "Tensor y3, float scale, Tensor? shift_out=None, Tensor? stamps=None, bool frag=False) -> ()");
   m.def("pong_fused_env_step(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, Tensor logp, Tensor ent, "
         "Tensor value, int key_shift, int pseed, Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, "
         "Tensor env_ids, Tensor out, Tensor reward, Tensor done, Tensor truncated, int seed, int max_steps, "
         "Tensor hpart, int planes, Tensor bfc, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, "
-        "Tensor y1, Tensor y2, Tensor y3, float scale, Tensor? shift_out=None, Tensor[]? next_state=None, Tensor? stamps=None) -> ()");
+        "Tensor y1, Tensor y2, Tensor y3, float scale, Tensor? shift_out=None, Tensor[]? next_state=None, "
+        "Tensor? stamps=None, bool frag=False) -> ()");
   m.def("categorical_sample(Tensor logits, Tensor keys, int seed, Tensor act, Tensor logp, Tensor ent) -> ()");
   m.def("wave_reduce_check(Tensor x, Tensor out) -> ()");
   m.def("categorical_sample_env(Tensor logits, Tensor tg, Tensor env_ids, int key_shift, int seed, Tensor act, "
@@ -1771,10 +1789,10 @@ TORCH_LIBRARY(acamd, m) {
   m.def("sumsq_multi(Tensor[] xs, Tensor[] partials) -> ()");
   m.def("adam_step(Tensor p, Tensor g, Tensor m, Tensor v, Tensor lr, Tensor t, Tensor? gnorm_parts, "
         "Tensor? gnorm_out, Tensor? shadow, float b1, float b2, float eps, float clip, float max_norm, Tensor ticket, "
-        "bool zero_grad=False, float gmul=1.0, float norm_mul=1.0) -> ()");
+        "bool zero_grad=False, float gmul=1.0, float norm_mul=1.0, Tensor? trans=None) -> ()");
   m.def("rmsprop_step(Tensor p, Tensor g, Tensor v, Tensor lr, Tensor? gnorm_parts, Tensor? gnorm_out, "
         "Tensor? shadow, float alpha, float eps, float clip, float max_norm, bool zero_grad=False, float gmul=1.0, "
-        "float norm_mul=1.0) -> ()");
+        "float norm_mul=1.0, Tensor? trans=None) -> ()");
   m.def("cast_bf16(Tensor x, Tensor y) -> ()");
   m.def("grad_move(Tensor src, Tensor dst) -> ()");
   m.def("opt_multi(Tensor words, Tensor fvals, Tensor? trans, bool adam, float b1, float b2, float eps, bool zero_grad, "

@@ -282,6 +282,66 @@ __device__ __forceinline__ void obs_rows_dma(const uint8_t* __restrict__ src, ui
 // trip the other one's MFMAs run (the 118 KB form above runs one workgroup -- one wave per SIMD -- per CU). conv1
 // converts the pixels to exact bf16 integers on the fly; same MFMA order and epilogues: bit-identical outputs.
 // The conv chain is a device function shared with the per-env fused rollout step (pong_fused_env_step_kernel).
+// conv1 / conv2 weight fragments of this wave (output-channel tile wid for conv2)
+__device__ __forceinline__ void trunk_env_w1(const u16* __restrict__ W1, bf16x8 (&bw)[2][8]) {
+  const int lane = threadIdx.x & 63, l16 = lane & 15, lg = lane >> 4;
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+      bw[nt][ks] = *reinterpret_cast<const bf16x8*>(W1 + (nt * 16 + l16) * 256 + ks * 32 + lg * 8);
+}
+__device__ __forceinline__ void trunk_env_w2(const u16* __restrict__ W2, bf16x8 (&bw2)[16]) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, l16 = lane & 15, lg = lane >> 4;
+  const int n2 = wid * 16 + l16;
+#pragma unroll
+  for (int ks = 0; ks < 16; ++ks) bw2[ks] = *reinterpret_cast<const bf16x8*>(W2 + n2 * 512 + ks * 32 + lg * 8);
+}
+__device__ __forceinline__ void trunk_env_w12(const u16* __restrict__ W1, const u16* __restrict__ W2,
+                                              bf16x8 (&bw)[2][8], bf16x8 (&bw2)[16]) {
+  trunk_env_w1(W1, bw);
+  trunk_env_w2(W2, bw2);
+}
+
+// Fragment-ordered weight copies (written by the optimiser step, optim.hip OptTrans): fragment (tile, k-step) of lane l at ((tile * KS + ks) * 64 +
+// l) * 8 -- a wave's fragment load is ONE contiguous 1 KB read. The row-major fragment loads above touch 16 rows x
+// 64 bytes per wave instruction, which the L2 -> CU path serves at 16 B/clk/CU against ~60 for whole-line wave loads
+// (profiles/r4_l2_stream_probe.txt).
+__device__ __forceinline__ void frag_w1(const u16* __restrict__ F1, bf16x8 (&bw)[2][8]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) bw[nt][ks] = *reinterpret_cast<const bf16x8*>(F1 + ((nt * 8 + ks) * 64 + lane) * 8);
+}
+__device__ __forceinline__ void frag_w2(const u16* __restrict__ F2, bf16x8 (&bw2)[16]) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int ks = 0; ks < 16; ++ks) bw2[ks] = *reinterpret_cast<const bf16x8*>(F2 + ((wid * 16 + ks) * 64 + lane) * 8);
+}
+__device__ __forceinline__ void frag_w3(const u16* __restrict__ F3, bf16x8 (&bw3)[18]) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int ks = 0; ks < 18; ++ks) bw3[ks] = *reinterpret_cast<const bf16x8*>(F3 + ((wid * 18 + ks) * 64 + lane) * 8);
+}
+
+// conv2 / conv3 fragments of this wave from the row-major weights or (FRAG) their fragment-ordered copies
+template <bool FRAG>
+__device__ __forceinline__ void load_w2(const u16* __restrict__ W2, bf16x8 (&bw2)[16]) {
+  if constexpr (FRAG) frag_w2(W2, bw2);
+  else trunk_env_w2(W2, bw2);
+}
+template <bool FRAG>
+__device__ __forceinline__ void load_w3(const u16* __restrict__ W3, bf16x8 (&bw3)[18]) {
+  if constexpr (FRAG) {
+    frag_w3(W3, bw3);
+  } else {
+    const int lane = threadIdx.x & 63, n2 = (threadIdx.x >> 6) * 16 + (lane & 15), lg = lane >> 4;
+#pragma unroll
+    for (int ks = 0; ks < 18; ++ks) bw3[ks] = *reinterpret_cast<const bf16x8*>(W3 + n2 * 576 + ks * 32 + lg * 8);
+  }
+}
+
 // ------------------------------------------------------------------------------------------------------------
 // Output rows computed / stored by part PART of an env's trunk: -1 the whole env (one workgroup per env), 0 / 1 the
 // two halves of the split rollout step (pong_fused_env_step_kernel<A1, 2>): conv3 rows [c3a, c3b), the conv2 / conv1 /
@@ -312,7 +372,7 @@ constexpr int E1P_ELEMS = 14 * E1_W * Y1_LD;   // the y1 image of a half (at mos
 // image rows are global, the y1 / y2 images hold the part's rows from c1a / c2a); bw / bw2: this wave's conv1 / conv2
 // weight fragments (already in registers), W3's are loaded after conv1. Every output's MFMA order is the same in
 // every part: the halves are bit-identical to the whole-env form.
-template <int PART>
+template <int PART, bool FRAG = false>
 __device__ __forceinline__ void trunk_env_convs(const uint8_t* __restrict__ s_obs8, u16* __restrict__ s_y1,
                                                 u16* __restrict__ s_y2, int e, const bf16x8 (&bw)[2][8],
                                                 const bf16x8 (&bw2)[16], const u16* __restrict__ W3, float bias0,
@@ -359,8 +419,7 @@ __device__ __forceinline__ void trunk_env_convs(const uint8_t* __restrict__ s_ob
     }
   }
   bf16x8 bw3[18];
-#pragma unroll
-  for (int ks = 0; ks < 18; ++ks) bw3[ks] = *reinterpret_cast<const bf16x8*>(W3 + n2 * 576 + ks * 32 + lg * 8);
+  load_w3<FRAG>(W3, bw3);
   __syncthreads();
   stamp(stamps, 5);
   // ---------------------------------------------------------------- conv2: M P2 (T2 tiles), N 64 (wave = N tile), K 512
@@ -449,27 +508,6 @@ __device__ __forceinline__ void w1_frags_from_lds(const u16* __restrict__ s_w, b
     }
 }
 
-// conv1 / conv2 weight fragments of this wave (output-channel tile wid for conv2)
-__device__ __forceinline__ void trunk_env_w1(const u16* __restrict__ W1, bf16x8 (&bw)[2][8]) {
-  const int lane = threadIdx.x & 63, l16 = lane & 15, lg = lane >> 4;
-#pragma unroll
-  for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks)
-      bw[nt][ks] = *reinterpret_cast<const bf16x8*>(W1 + (nt * 16 + l16) * 256 + ks * 32 + lg * 8);
-}
-__device__ __forceinline__ void trunk_env_w2(const u16* __restrict__ W2, bf16x8 (&bw2)[16]) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, l16 = lane & 15, lg = lane >> 4;
-  const int n2 = wid * 16 + l16;
-#pragma unroll
-  for (int ks = 0; ks < 16; ++ks) bw2[ks] = *reinterpret_cast<const bf16x8*>(W2 + n2 * 512 + ks * 32 + lg * 8);
-}
-__device__ __forceinline__ void trunk_env_w12(const u16* __restrict__ W1, const u16* __restrict__ W2,
-                                              bf16x8 (&bw)[2][8], bf16x8 (&bw2)[16]) {
-  trunk_env_w1(W1, bw);
-  trunk_env_w2(W2, bw2);
-}
-
 __global__ void __launch_bounds__(256) cnn_trunk_fwd_u8_kernel(
     const uint8_t* __restrict__ obs, const u16* __restrict__ W1, const float* __restrict__ b1,
     const u16* __restrict__ W2, const float* __restrict__ b2, const u16* __restrict__ W3,
@@ -515,6 +553,7 @@ __device__ __forceinline__ int e1t_addr(int h, int w, int ch) {
 constexpr int OB16_ELEMS = 4 * 84 * 84;     // 28224 u16
 static_assert(E1T_ELEMS + E2_ELEMS <= OB16_ELEMS && Y3_ROWS * Y3_C <= E1T_ELEMS, "y1 + y2 (+ y3) reuse the image");
 
+template <bool FRAG>
 __global__ void __launch_bounds__(256) cnn_trunk_fwd_s16_kernel(
     const uint8_t* __restrict__ obs, const u16* __restrict__ W1, const float* __restrict__ b1,
     const u16* __restrict__ W2, const float* __restrict__ b2, const u16* __restrict__ W3,
@@ -535,7 +574,8 @@ __global__ void __launch_bounds__(256) cnn_trunk_fwd_s16_kernel(
 #pragma unroll
   for (int u = 0; u < PER; ++u) v[u] = src[min(tid + u * 256, NCH - 1)];
   bf16x8 bw[2][8];
-  trunk_env_w1(W1, bw);
+  if constexpr (FRAG) frag_w1(W1, bw);
+  else trunk_env_w1(W1, bw);
   const float bias0 = b1[l16], bias1 = b1[16 + l16], bias2 = b2[n2], bias3 = b3[n2];
 #pragma unroll
   for (int u = 0; u < PER; ++u) {
@@ -579,7 +619,7 @@ __global__ void __launch_bounds__(256) cnn_trunk_fwd_s16_kernel(
     }
   }
   bf16x8 bw2[16];
-  trunk_env_w2(W2, bw2);
+  load_w2<FRAG>(W2, bw2);
   __syncthreads();   // the image is dead
 #pragma unroll
   for (int q = 0; q < MT1; ++q) {
@@ -626,8 +666,7 @@ __global__ void __launch_bounds__(256) cnn_trunk_fwd_s16_kernel(
       }
   }
   bf16x8 bw3[18];
-#pragma unroll
-  for (int ks = 0; ks < 18; ++ks) bw3[ks] = *reinterpret_cast<const bf16x8*>(W3 + n2 * 576 + ks * 32 + lg * 8);
+  load_w3<FRAG>(W3, bw3);
   __syncthreads();   // y2 complete; y1 dead (its global copy read it before the barrier)
   for (int i = tid; i < Y2_ROWS * 8; i += 256) {
     const int p = i >> 3, cq = i & 7;
@@ -690,7 +729,7 @@ __device__ __forceinline__ int tr_y1_own_begin(int r) { return (20 * r + 6) / 7;
 // WMODE (when the conv2 / conv3 weight fragments are requested): 0 at entry (the staging barrier waited for obs +
 // W1 only), 1 after conv1's MFMAs (trunk mode 2), 2 W2 at entry and W3 after conv1's MFMAs, 3 W2 already requested
 // by the caller and W3 after conv1's MFMAs (the fused step: W2's 64 KB per workgroup lands during the render)
-template <int WMODE>
+template <int WMODE, bool FRAG = false>
 __device__ __forceinline__ void trunk_rows_compute(const u16* __restrict__ s_in, const u16* __restrict__ s_w1,
                                                    u16* __restrict__ s_y1, u16* __restrict__ s_y2, int e, int r,
                                                    const float bias1a, const float bias1b, const float bias2,
@@ -703,12 +742,10 @@ __device__ __forceinline__ void trunk_rows_compute(const u16* __restrict__ s_in,
   const int l16 = lane & 15, lg = lane >> 4;
   const int n2 = wid * 16 + l16;
   if constexpr (WMODE == 0 || WMODE == 2) {
-#pragma unroll
-    for (int ks = 0; ks < 16; ++ks) bw2[ks] = *reinterpret_cast<const bf16x8*>(W2 + n2 * 512 + ks * 32 + lg * 8);
+    load_w2<FRAG>(W2, bw2);
   }
   if constexpr (WMODE == 0) {
-#pragma unroll
-    for (int ks = 0; ks < 18; ++ks) bw3[ks] = *reinterpret_cast<const bf16x8*>(W3 + n2 * 576 + ks * 32 + lg * 8);
+    load_w3<FRAG>(W3, bw3);
   }
 
   // ---------------------------------------------------------------- conv1: 160 positions (10 M tiles) x 32 x K 256
@@ -764,12 +801,10 @@ __device__ __forceinline__ void trunk_rows_compute(const u16* __restrict__ s_in,
   }
   stamp(stamps, 10);
   if constexpr (WMODE == 1) {
-#pragma unroll
-    for (int ks = 0; ks < 16; ++ks) bw2[ks] = *reinterpret_cast<const bf16x8*>(W2 + n2 * 512 + ks * 32 + lg * 8);
+    load_w2<FRAG>(W2, bw2);
   }
   if constexpr (WMODE >= 1) {
-#pragma unroll
-    for (int ks = 0; ks < 18; ++ks) bw3[ks] = *reinterpret_cast<const bf16x8*>(W3 + n2 * 576 + ks * 32 + lg * 8);
+    load_w3<FRAG>(W3, bw3);
   }
   __syncthreads();
   stamp(stamps, 2);
@@ -978,7 +1013,7 @@ __device__ __forceinline__ void pong_commit_next(const PongIO& io, const PongNex
   sp[0] = q.bx; sp[1] = q.by; sp[2] = q.vx; sp[3] = q.vy; sp[4] = q.pa; sp[5] = q.po; sp[6] = q.sa; sp[7] = q.so;
 }
 
-template <int A1>
+template <int A1, bool FRAG>
 __global__ void __launch_bounds__(T_THREADS) pong_fused_step_kernel(
     PongIO io, PongNext nx, FcParts fc, u16* __restrict__ h, const u16* __restrict__ Wh,
     const float* __restrict__ bh, float* __restrict__ z_out, int32_t* __restrict__ act, float* __restrict__ logp,
@@ -1092,9 +1127,7 @@ __global__ void __launch_bounds__(T_THREADS) pong_fused_step_kernel(
   }
   __syncthreads();
   stamp(stamps, 9);
-#pragma unroll
-  for (int ks = 0; ks < 16; ++ks)   // conv2's fragments, landing during the render (trunk_rows_compute WMODE 3)
-    bw2[ks] = *reinterpret_cast<const bf16x8*>(W2 + n2 * 512 + ks * 32 + (lane >> 4) * 8);
+  load_w2<FRAG>(W2, bw2);   // conv2's fragments, landing during the render (trunk_rows_compute WMODE 3)
   const PongOut& res = cand[pong_dir_index(sh_act)];
   const bool done = res.done != 0;
   if (lead && tid == 0) pong_commit_next(io, nx, e, res, tg0);
@@ -1141,8 +1174,8 @@ __global__ void __launch_bounds__(T_THREADS) pong_fused_step_kernel(
   }
   __syncthreads();
   stamp(stamps, 1);
-  trunk_rows_compute<3>(s_in, s_w1, s_y1, s_y2, e, r, bias1a, bias1b, bias2, bias3, W2, W3, y1g, y2g, y3g, scale,
-                        stamps, bw2, bw3);
+  trunk_rows_compute<3, FRAG>(s_in, s_w1, s_y1, s_y2, e, r, bias1a, bias1b, bias2, bias3, W2, W3, y1g, y2g, y3g,
+                              scale, stamps, bw2, bw3);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -1163,7 +1196,7 @@ __global__ void __launch_bounds__(T_THREADS) pong_fused_step_kernel(
 // and maths, so the same action), half 0 alone writes the step's outputs and commits the env state into the other
 // parity (nx: the halves read the current one), each half renders the input rows it needs and stores the rows it
 // owns, and runs the conv chain of its rows (trunk_env_convs<PART>).
-template <int A1, int PART>
+template <int A1, int PART, bool FRAG>
 __device__ __forceinline__ void env_step_body(
     uint8_t* __restrict__ s_obs8, u16* __restrict__ s_y1, float (*s_acc)[A1], PongOut* cand, int* sh_act,
     const PongIO& io, const PongNext& nx, const FcParts& fc, int e, u16* __restrict__ h,
@@ -1242,7 +1275,7 @@ __device__ __forceinline__ void env_step_body(
   __syncthreads();
   stamp(stamps, 2);
   w1_frags_from_lds(s_y1, bw);   // read before the next barrier: conv1's epilogue overwrites them
-  trunk_env_w2(W2, bw2);         // lands during the render and conv1
+  load_w2<FRAG>(W2, bw2);        // lands during the render and conv1
   const PongOut& res = cand[pong_dir_index(*sh_act)];
   const bool done = res.done != 0;
   if (tid == 0) {
@@ -1282,8 +1315,8 @@ __device__ __forceinline__ void env_step_body(
     }
   }
   stamp(stamps, 4);
-  trunk_env_convs<PART>(s_obs8, s_y1, s_y2, e, bw, bw2, W3, bias0, bias1, bias2, bias3, y1g, y2g, y3g, scale,
-                        stamps);
+  trunk_env_convs<PART, FRAG>(s_obs8, s_y1, s_y2, e, bw, bw2, W3, bias0, bias1, bias2, bias3, y1g, y2g, y3g, scale,
+                              stamps);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -1299,7 +1332,7 @@ __device__ __forceinline__ void env_step_body(
 // One launch instead of the trunk kernel + the policy/env kernel of the unfused step, and the new frame never makes a
 // global round trip before conv1.
 // ------------------------------------------------------------------------------------------------------------
-template <int A1, int SPLIT>
+template <int A1, int SPLIT, bool FRAG>
 __global__ void __launch_bounds__(256) pong_fused_env_step_kernel(
     PongIO io, PongNext nx, FcParts fc, u16* __restrict__ h, const u16* __restrict__ Wh, const float* __restrict__ bh,
     float* __restrict__ z_out, int32_t* __restrict__ act, float* __restrict__ logp, float* __restrict__ ent,
@@ -1313,8 +1346,8 @@ __global__ void __launch_bounds__(256) pong_fused_env_step_kernel(
   __shared__ PongOut cand[3];
   __shared__ int sh_act;
 #define ACA_ENV_BODY(PART, E)                                                                                    \
-  env_step_body<A1, PART>(s_obs8, s_y1, s_acc, cand, &sh_act, io, nx, fc, E, h, Wh, bh, z_out, act, logp, ent,    \
-                          vout, key_shift, pseed, W1, b1, W2, b2, W3, b3, y1g, y2g, y3g, scale, shift_out, stamps)
+  env_step_body<A1, PART, FRAG>(s_obs8, s_y1, s_acc, cand, &sh_act, io, nx, fc, E, h, Wh, bh, z_out, act, logp,     \
+                                ent, vout, key_shift, pseed, W1, b1, W2, b2, W3, b3, y1g, y2g, y3g, scale, shift_out, stamps)
   if constexpr (SPLIT == 1) {
     ACA_ENV_BODY(-1, blockIdx.x);
   } else {
@@ -1960,10 +1993,15 @@ extern "C" hipError_t aca_cnn_trunk_fwd(const uint8_t* obs, const uint16_t* W1, 
 extern "C" hipError_t aca_cnn_trunk_fwd_s16(const uint8_t* obs, const uint16_t* W1, const float* b1,
                                             const uint16_t* W2, const float* b2, const uint16_t* W3, const float* b3,
                                             uint16_t* y1, uint16_t* y2, uint16_t* y3, int B, float scale,
-                                            uint8_t* shift_out, const int64_t* obs_idx, hipStream_t stream) {
+                                            uint8_t* shift_out, const int64_t* obs_idx, int frag,
+                                            hipStream_t stream) {
   if (B <= 0) return hipSuccess;
-  aca::cnn_trunk_fwd_s16_kernel<<<B, 256, 0, stream>>>(obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale, shift_out,
-                                                        obs_idx);
+  if (frag)
+    aca::cnn_trunk_fwd_s16_kernel<true><<<B, 256, 0, stream>>>(obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale,
+                                                                shift_out, obs_idx);
+  else
+    aca::cnn_trunk_fwd_s16_kernel<false><<<B, 256, 0, stream>>>(obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale,
+                                                                 shift_out, obs_idx);
   return hipGetLastError();
 }
 
@@ -2003,7 +2041,8 @@ extern "C" hipError_t aca_pong_fused_step(
     int64_t* tg_n, float* ep_ret_n, float* ep_stats, const int64_t* ids, const uint8_t* prev, uint8_t* out,
     float* reward, uint8_t* done, uint8_t* trunc, uint32_t seed, int max_steps, const uint16_t* W1, const float* b1,
     const uint16_t* W2, const float* b2, const uint16_t* W3, const float* b3, uint16_t* y1, uint16_t* y2,
-    uint16_t* y3, float scale, uint8_t* shift_out, uint64_t* stamps, int N, hipStream_t stream) {
+    uint16_t* y3, float scale, uint8_t* shift_out, uint64_t* stamps, int frag, int N, hipStream_t stream) {
+  // frag: W2 / W3 are the fragment-ordered copies (W1 stays row-major: the kernel stages it through LDS)
   if (N <= 0) return hipSuccess;
   aca::PongIO io;
   io.state = state; io.tsteps = t; io.tglob = tg; io.ep_ret = ep_ret; io.ep_stats = ep_stats; io.env_ids = ids;
@@ -2015,9 +2054,14 @@ extern "C" hipError_t aca_pong_fused_step(
   switch (A + 1) {
 #define ACA_FUSED_CASE(A1)                                                                                       \
   case A1:                                                                                                       \
-    aca::pong_fused_step_kernel<A1><<<grid, aca::T_THREADS, 0, stream>>>(                                        \
-        io, nx, fc, h, Wh, bh, z, act, logp, ent, value, key_shift, pseed, W1, b1, W2, b2, W3, b3, y1, y2, y3,    \
-        scale, shift_out, stamps);                                                                               \
+    if (frag)                                                                                                    \
+      aca::pong_fused_step_kernel<A1, true><<<grid, aca::T_THREADS, 0, stream>>>(                                \
+          io, nx, fc, h, Wh, bh, z, act, logp, ent, value, key_shift, pseed, W1, b1, W2, b2, W3, b3, y1, y2, y3,  \
+          scale, shift_out, stamps);                                                                             \
+    else                                                                                                         \
+      aca::pong_fused_step_kernel<A1, false><<<grid, aca::T_THREADS, 0, stream>>>(                               \
+          io, nx, fc, h, Wh, bh, z, act, logp, ent, value, key_shift, pseed, W1, b1, W2, b2, W3, b3, y1, y2, y3,  \
+          scale, shift_out, stamps);                                                                             \
     break;
     ACA_FUSED_CASE(3) ACA_FUSED_CASE(4) ACA_FUSED_CASE(5) ACA_FUSED_CASE(6) ACA_FUSED_CASE(7)
 #undef ACA_FUSED_CASE
@@ -2034,8 +2078,9 @@ extern "C" hipError_t aca_pong_fused_env_step(
     uint8_t* out, float* reward, uint8_t* done, uint8_t* trunc, uint32_t seed, int max_steps, const uint16_t* W1,
     const float* b1, const uint16_t* W2, const float* b2, const uint16_t* W3, const float* b3, uint16_t* y1,
     uint16_t* y2, uint16_t* y3, float scale, uint8_t* shift_out, float* state_n, int32_t* t_n, int64_t* tg_n,
-    float* ep_ret_n, uint64_t* stamps, int N, hipStream_t stream) {
-  // state_n .. ep_ret_n: the other parity's env state -> two workgroups per env (commit there); null -> one
+    float* ep_ret_n, uint64_t* stamps, int frag, int N, hipStream_t stream) {
+  // state_n .. ep_ret_n: the other parity's env state -> two workgroups per env (commit there); null -> one.
+  // frag: W2 / W3 are the fragment-ordered copies (W1 stays row-major: LDS-DMA staged)
   if (N <= 0) return hipSuccess;
   if (S < 1 || S > aca::FC_MAX_PLANES) return hipErrorInvalidValue;
   const bool split = state_n != nullptr;
@@ -2046,20 +2091,21 @@ extern "C" hipError_t aca_pong_fused_env_step(
   io.prev = out; io.out = out; io.reward = reward; io.done_out = done; io.trunc_out = trunc; io.seed = seed;
   io.max_steps = max_steps; io.k = 4;
   aca::FcParts fc{hpart, S, plane_stride, bfc};
+#define ACA_FES_LAUNCH(A1, SPLIT, FRAG, GRID)                                                                   \
+  aca::pong_fused_env_step_kernel<A1, SPLIT, FRAG><<<GRID, 256, 0, stream>>>(                                    \
+      io, nx, fc, h, Wh, bh, z, act, logp, ent, value, key_shift, pseed, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale, \
+      shift_out, stamps);
   switch (A + 1) {
 #define ACA_FES_CASE(A1)                                                                                         \
   case A1:                                                                                                       \
-    if (split)                                                                                                   \
-      aca::pong_fused_env_step_kernel<A1, 2><<<2 * N, 256, 0, stream>>>(                                         \
-          io, nx, fc, h, Wh, bh, z, act, logp, ent, value, key_shift, pseed, W1, b1, W2, b2, W3, b3, y1, y2, y3,  \
-          scale, shift_out, stamps);                                                                             \
-    else                                                                                                         \
-      aca::pong_fused_env_step_kernel<A1, 1><<<N, 256, 0, stream>>>(                                             \
-          io, nx, fc, h, Wh, bh, z, act, logp, ent, value, key_shift, pseed, W1, b1, W2, b2, W3, b3, y1, y2, y3,  \
-          scale, shift_out, stamps);                                                                             \
+    if (split && frag) ACA_FES_LAUNCH(A1, 2, true, 2 * N)                                                      \
+    else if (split) ACA_FES_LAUNCH(A1, 2, false, 2 * N)                                                          \
+    else if (frag) ACA_FES_LAUNCH(A1, 1, true, N)                                                                \
+    else ACA_FES_LAUNCH(A1, 1, false, N)                                                                         \
     break;
     ACA_FES_CASE(3) ACA_FES_CASE(4) ACA_FES_CASE(5) ACA_FES_CASE(6) ACA_FES_CASE(7)
 #undef ACA_FES_CASE
+#undef ACA_FES_LAUNCH
     default:
       return hipErrorInvalidValue;
   }

@@ -81,6 +81,9 @@ __device__ __forceinline__ float partial_total(const float* __restrict__ parts, 
 // Optional transposed fp32 shadows of [K][N] weight matrices inside the segment (the MLP engine's forward reads
 // Wt[N][ldt]); written by the update itself, so the shadow never needs a pass of its own.
 constexpr int OPT_MAXT = 6;
+// ldt < 0: a FRAGMENT-ORDERED bf16 copy of the row-major [K][N] weight (the CNN engine's MFMA weight operands,
+// cnn_fused.hip frag_w1..3): element (k, c) goes to u16 ((((k / 16) * (N / 32) + c / 32) * 64 + (c / 8 % 4) * 16 +
+// k % 16) * 8 + c % 8), so a wave's 16-byte-per-lane fragment load is one contiguous 1 KB read.
 struct OptTrans {
   int64_t off;   // element offset of W within the segment
   int K, N, ldt;
@@ -109,7 +112,12 @@ __device__ __forceinline__ void write_trans(const OptSeg& S, size_t i, float v) 
       // 32-bit division (a 64-bit one is a ~100-instruction software sequence per element)
       const uint32_t ou = (uint32_t)o, n = (uint32_t)T.N;
       const uint32_t k = ou / n, c = ou - k * n;
-      T.dst[(size_t)c * T.ldt + k] = v;
+      if (T.ldt < 0) {
+        const uint32_t f = (((k >> 4) * (n >> 5) + (c >> 5)) * 64u + ((c >> 3) & 3u) * 16u + (k & 15u)) * 8u + (c & 7u);
+        reinterpret_cast<u16*>(T.dst)[f] = f2bf(v);
+      } else {
+        T.dst[(size_t)c * T.ldt + k] = v;
+      }
       return;
     }
   }
@@ -512,6 +520,20 @@ extern "C" hipError_t aca_grad_finalize(const int64_t* jobs, int njobs, float* p
   return hipGetLastError();
 }
 
+// trans: host table [OPT_MAXT][5] = (offset, K, N, ldt, dst) of one segment; K == 0 ends the list
+static bool opt_load_trans(OptSeg& S, const int64_t* tw0) {
+  S.ntrans = 0;
+  if (!tw0) return true;
+  for (int e = 0; e < OPT_MAXT; ++e) {
+    const int64_t* tw = tw0 + (int64_t)e * 5;
+    if (tw[1] <= 0) break;
+    if (tw[3] < 0 && (tw[1] % 16 || tw[2] % 32)) return false;   // fragment order: 16-row tiles, 32-wide k-steps
+    S.tr[e] = OptTrans{tw[0], (int)tw[1], (int)tw[2], (int)tw[3], reinterpret_cast<float*>(tw[4])};
+    S.ntrans = e + 1;
+  }
+  return true;
+}
+
 static bool opt_aligned(const float* p, const float* g, const float* m, const float* v, const uint16_t* shadow) {
   return !((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(m) |
             reinterpret_cast<uintptr_t>(v)) % 16 || reinterpret_cast<uintptr_t>(shadow) % 8);
@@ -520,12 +542,13 @@ static bool opt_aligned(const float* p, const float* g, const float* m, const fl
 extern "C" hipError_t aca_adam_step(float* p, float* g, float* m, float* v, size_t n, const float* lr,
                                     float* t, const float* gnorm_parts, float* gnorm_out, uint16_t* shadow, float b1, float b2, float eps,
                                     float clip, float max_norm, unsigned int* ticket, int zero_grad,
-                                    float gmul, float norm_mul, hipStream_t stream) {
+                                    float gmul, float norm_mul, const int64_t* trans, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   if (!opt_aligned(p, g, m, v, shadow)) return hipErrorInvalidValue;
   OptSeg S{p, g, m, v, n, lr, t, gnorm_parts, gnorm_out, shadow, clip, max_norm, gmul, norm_mul, ticket, opt_grid(n),
            0, {}};
   if (!ticket || !t) return hipErrorInvalidValue;
+  if (!opt_load_trans(S, trans)) return hipErrorInvalidValue;
   opt_kernel<true><<<S.nblocks, OPT_THREADS, 0, stream>>>(S, b1, b2, eps, zero_grad);
   return hipGetLastError();
 }
@@ -533,11 +556,12 @@ extern "C" hipError_t aca_adam_step(float* p, float* g, float* m, float* v, size
 extern "C" hipError_t aca_rmsprop_step(float* p, float* g, float* v, size_t n, const float* lr,
                                        const float* gnorm_parts, float* gnorm_out, uint16_t* shadow, float alpha, float eps, float clip,
                                        float max_norm, int zero_grad, float gmul, float norm_mul,
-                                       hipStream_t stream) {
+                                       const int64_t* trans, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   if (!opt_aligned(p, g, v, v, shadow)) return hipErrorInvalidValue;
   OptSeg S{p, g, nullptr, v, n, lr, nullptr, gnorm_parts, gnorm_out, shadow, clip, max_norm, gmul, norm_mul, nullptr,
            opt_grid(n), 0, {}};
+  if (!opt_load_trans(S, trans)) return hipErrorInvalidValue;
   opt_kernel<false><<<S.nblocks, OPT_THREADS, 0, stream>>>(S, 0.f, alpha, eps, zero_grad);
   return hipGetLastError();
 }
@@ -575,15 +599,8 @@ extern "C" hipError_t aca_opt_multi(const int64_t* words, const float* fvals, co
     if (adam && (!S.m || !S.t || !S.ticket)) return hipErrorInvalidValue;
     S.nblocks = opt_grid(S.n);
     total += S.nblocks;
-    // trans: [nseg][OPT_MAXT][5] = (offset, K, N, ldt, dst); K == 0 ends a segment's list
-    S.ntrans = 0;
-    if (trans)
-      for (int e = 0; e < OPT_MAXT; ++e) {
-        const int64_t* tw = trans + ((int64_t)k * OPT_MAXT + e) * 5;
-        if (tw[1] <= 0) break;
-        S.tr[e] = OptTrans{tw[0], (int)tw[1], (int)tw[2], (int)tw[3], reinterpret_cast<float*>(tw[4])};
-        S.ntrans = e + 1;
-      }
+    // trans: [nseg][OPT_MAXT][5]
+    if (!opt_load_trans(S, trans ? trans + (int64_t)k * OPT_MAXT * 5 : nullptr)) return hipErrorInvalidValue;
   }
   if (adam) opt_multi_kernel<true><<<total, OPT_THREADS, 0, stream>>>(M, b1, b2, eps, zero_grad);
   else opt_multi_kernel<false><<<total, OPT_THREADS, 0, stream>>>(M, 0.f, b2, eps, zero_grad);

@@ -1,6 +1,7 @@
 """A/B of the per-env trunk forward forms at the PPO learner batch (B = 4096 through an index, as the minibatch
 forward reads them): mode 0 (lean, bytes converted in conv1's loop) vs mode 3 (bf16-staged). Event-timed, 20
-launches each after warm-up. GPU only."""
+launches each after warm-up; mode 5 = mode 3 reading fragment-ordered weight copies (one contiguous 1 KB read per
+wave fragment load), checked bitwise against mode 3. GPU only."""
 import json
 import os
 import sys
@@ -20,10 +21,19 @@ def main():
     W1, W2, W3 = bf(32, 256), bf(64, 512), bf(64, 576)
     b1, b2, b3 = (torch.zeros(n, device=dev) for n in (32, 64, 64))
     ys = [torch.empty(B * r, c, dtype=torch.bfloat16, device=dev) for r, c in ((400, 32), (81, 64), (49, 64))]
-    out = {}
+    # fragment order: [tile][k-step][lane = lg*16 + row16][8 elements]
+    F1 = W1.view(2, 16, 8, 4, 8).permute(0, 2, 3, 1, 4).contiguous()
+    F2 = W2.view(4, 16, 16, 4, 8).permute(0, 2, 3, 1, 4).contiguous()
+    F3 = W3.view(4, 16, 18, 4, 8).permute(0, 2, 3, 1, 4).contiguous()
+    G.cnn_trunk_fwd(obs, W1, b1, W2, b2, W3, b3, *ys, mode=3, obs_idx=idx)
+    ref = [y.clone() for y in ys]
+    G.cnn_trunk_fwd(obs, F1, b1, F2, b2, F3, b3, *ys, mode=5, obs_idx=idx)
+    torch.cuda.synchronize()
+    out = {"frag_bitwise": all(torch.equal(a, b) for a, b in zip(ref, ys))}
     for rep in range(2):
-        for mode in (0, 3):
-            run = lambda: G.cnn_trunk_fwd(obs, W1, b1, W2, b2, W3, b3, *ys, mode=mode, obs_idx=idx)
+        for mode in (0, 3, 5):
+            w = (F1, F2, F3) if mode == 5 else (W1, W2, W3)
+            run = lambda: G.cnn_trunk_fwd(obs, w[0], b1, w[1], b2, w[2], b3, *ys, mode=mode, obs_idx=idx)
             for _ in range(3):
                 run()
             torch.cuda.synchronize()

@@ -274,8 +274,9 @@ def test_sumsq_multi_equals_separate_launches(cuda):
 
 def test_trunk_fwd_bf16_staged_by_index_equals_lean_form(cuda):
     """cnn_trunk_fwd mode 3 (cnn_trunk_fwd_s16_kernel: bytes converted once into a bf16 image, y1/y2/y3 out through
-    LDS as 16-byte rows) reading a PPO minibatch through an index == the lean per-env form (mode 0) bit for bit, and
-    both match the fp32 torch convolutions of the same bf16 operands."""
+    LDS as 16-byte rows) reading a PPO minibatch through an index == the lean per-env form (mode 0) bit for bit, as
+    does mode 5 (the same kernel on fragment-ordered weight copies), and they match the fp32 torch convolutions of
+    the same bf16 operands."""
     import torch.nn.functional as F
     from actor_critic_algs_on_tensorflow_amd.ops import gemm as G
     g = torch.Generator(device="cpu").manual_seed(11)
@@ -286,15 +287,19 @@ def test_trunk_fwd_bf16_staged_by_index_equals_lean_form(cuda):
     W2 = (torch.randn(64, 512, generator=g) * 0.05).to(torch.bfloat16).to(cuda)
     W3 = (torch.randn(64, 576, generator=g) * 0.05).to(torch.bfloat16).to(cuda)
     b1, b2, b3 = ((torch.rand(n, generator=g) * 0.1 - 0.02).to(cuda) for n in (32, 64, 64))
+    from actor_critic_algs_on_tensorflow_amd.ops.optim import frag_order
+    F1, F2, F3 = (frag_order(W, *W.shape) for W in (W1, W2, W3))
     outs = []
-    for mode in (0, 3):
+    for mode in (0, 3, 5):   # 5: the staged kernel reading the fragment-ordered weight copies
         ys = [torch.full((B * r, c), float("nan"), dtype=torch.bfloat16, device=cuda)
               for r, c in ((400, 32), (81, 64), (49, 64))]
-        G.cnn_trunk_fwd(obs, W1, b1, W2, b2, W3, b3, *ys, mode=mode, obs_idx=idx)
+        w = (F1, F2, F3) if mode == 5 else (W1, W2, W3)
+        G.cnn_trunk_fwd(obs, w[0], b1, w[1], b2, w[2], b3, *ys, mode=mode, obs_idx=idx)
         outs.append(ys)
     torch.cuda.synchronize()
-    for a, b in zip(*outs):
-        assert torch.equal(a.view(torch.int16), b.view(torch.int16))
+    for other in outs[1:]:
+        for a, b in zip(outs[0], other):
+            assert torch.equal(a.view(torch.int16), b.view(torch.int16))
     x = obs[idx].float() / 255.0
     w1 = W1.float().view(32, 4, 8, 8)
     y1 = F.relu(F.conv2d(x, w1, b1, stride=4)).to(torch.bfloat16)
@@ -351,3 +356,36 @@ def test_mlp_ppo_adam_step_offsets_equal_ticket(cuda):
         assert t >= 3 * 8 and t % 8 == 0, t   # whole updates of 2 x 4 minibatch steps
     for k, (a, b) in enumerate(zip(*runs)):
         assert torch.equal(a, b), k
+
+
+@pytest.mark.parametrize("preset_name,envs", [("pong_a2c", 32), ("breakout_ppo", 72)])
+def test_fragment_ordered_weights_equal_row_major(cuda, preset_name, envs, monkeypatch):
+    """EngineOpts.frag_weights: the conv weights' fragment-ordered bf16 copies, rewritten by the optimiser step itself
+    (RMSprop for A2C, Adam for PPO) and read by the rollout step kernels (row-split at 32 envs, per-env split at 72)
+    and the learner's staged trunk forward, give the same training bit for bit as the row-major weights -- and after
+    the updates the copies equal frag_order(bf16 shadow) exactly (no stale copy)."""
+    monkeypatch.setattr("actor_critic_algs_on_tensorflow_amd.ops.gemm.TUNE", False)
+    from actor_critic_algs_on_tensorflow_amd import preset
+    from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
+    from actor_critic_algs_on_tensorflow_amd.ops.optim import frag_order
+    runs = []
+    for on in (True, False):
+        kw = dict(n_steps=5) if preset_name == "pong_a2c" else dict(n_steps=8, ppo_epochs=2, ppo_minibatches=2)
+        tr = ActorCriticTrainer(preset(preset_name, num_envs=envs, device="cuda:0", outdir=None, quiet=True,
+                                       stdout_freq=0, save_every=0, seed=3, engine_opts=dict(frag_weights=on), **kw))
+        eng = tr.engine
+        assert (eng.frag is not None) == on
+        tr.capture(warmup=1)
+        snaps = []
+        for _ in range(3):
+            tr.step()
+            st = tr.storage
+            snaps.append([tr.flat.data.clone(), st.actions[:].clone(), st.values[:].clone(), st.logp[:].clone()])
+        torch.cuda.synchronize()
+        if on:
+            for S, (K, N), F in zip((eng.sW1, eng.sW2, eng.sW3), eng._FRAG_SHAPES, eng.frag):
+                assert torch.equal(F.view(torch.int16), frag_order(S, K, N).view(torch.int16))
+        runs.append(snaps)
+    for k, (a, b) in enumerate(zip(*runs)):
+        for j, (x, y) in enumerate(zip(a, b)):
+            assert torch.equal(x, y), (k, j)

@@ -176,7 +176,8 @@ def test_per_env_trunk_forward_reads_are_conflict_free():
     src = open(CNN).read()
     y1_ld, y2_ld = (int(v) for v in re.search(r"constexpr int Y1_LD = (\d+), Y2_LD = (\d+);", src).groups())
     e1_w, e2_w = (int(v) for v in re.search(r"constexpr int E1_W = (\d+), E2_W = (\d+);", src).groups())
-    body = src[src.index("void trunk_env_convs("):src.index("// conv1 / conv2 weight fragments of this wave")]
+    a = src.index("void trunk_env_convs(")
+    body = src[a:src.index("\n}\n", a)]
     assert "((oh * 2 + i) * E1_W + ow * 2 + j) * Y1_LD + c0" in body and "((oh + i) * E2_W + ow + j) * Y2_LD + c0" in body
     for ks in range(16):
         for mt in range(6):

@@ -1381,6 +1381,11 @@ __global__ void __launch_bounds__(256) pong_fused_env_step_kernel(
 //  * the B operands are weight rows read by ds_read_b64_tr_b16 (8 rows x 16 columns per 32-lane group): W3 rows of
 //    64 and W2 rows of 32 elements unpadded, each row's 16-byte chunks XOR-swizzled (bw_sw3 / bw_sw2), so the 8
 //    rows of a group cover all 64 banks (unswizzled padded rows: 2 cycles per read instead of 1).
+// exact small-range divisions as full-rate multiply-shifts (the compiler's signed division is a quarter-rate
+// mul_hi sequence): n / 9 for 0 <= n < 200, n / 10 for n < 1029, n / 7 for n < 64 (tests/test_lds_layouts_cpu.py)
+__device__ __forceinline__ int div9(int n) { return (int)(((unsigned)n * 57u) >> 9); }
+__device__ __forceinline__ int div10(int n) { return (int)(((unsigned)n * 205u) >> 11); }
+__device__ __forceinline__ int div7(int n) { return (int)(((unsigned)n * 37u) >> 8); }
 constexpr int BW_LDW3 = 64;                 // W3 B rows [576][64], chunks ^ bw_sw3(row)
 constexpr int BW_LDW2 = 32;                 // W2 B rows [1024][32], chunks ^ bw_sw2(row)
 constexpr int BW_PS = 80;                   // image pixel stride (64 channels + 16 unused)
@@ -1390,7 +1395,7 @@ constexpr int BW_RW = 576 * BW_LDW3;        // >= 1024 * BW_LDW2
 constexpr int BW_P3E = BW_P3H * BW_P3W * BW_PS;
 constexpr int BW_M2E = 81 * 64;
 constexpr int BW_P2E = BW_P2H * BW_P2W * BW_PS;
-static_assert(400 * 32 <= BW_P3E + BW_M2E, "dy1 staging aliases the dy3 image + y2 mask");
+static_assert(400 * 32 + 32 <= BW_P3E + BW_M2E, "dy1 staging (+ its discard slots) aliases the dy3 image + y2 mask");
 static_assert(1024 * BW_LDW2 <= BW_RW, "W2 rows fit the W3 region");
 static_assert(BW_P3W % 8 == 9 % 8 && BW_P2W % 8 == 10 % 8 && BW_PS == 80, "conflict-free image geometry");
 __device__ __forceinline__ int bw_sw3(int r) { return (((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2); }
@@ -1524,15 +1529,23 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_kernel(
     floatx4 acc[3];
 #pragma unroll
     for (int mt = 0; mt < 3; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    // per-lane A row offsets once, every k-step's read at a compile-time immediate from them (persist kernel notes)
+    constexpr int P3_LO = 2 * BW_P3W + 2;
+    int pb[3];
+#pragma unroll
+    for (int mt = 0; mt < 3; ++mt) {
+      const int m = min((mh + mt) * 16 + l16, 80);
+      const int a = div9(m), c = m - a * 9;
+      pb[mt] = ((a + 2) * BW_P3W + (c + 2) - P3_LO) * BW_PS + lg * 8;
+    }
 #pragma unroll
     for (int ks = 0; ks < 18; ++ks) {
-      const int kb = ks * 32 + lg * 8, t = kb >> 6, o0 = kb & 63, ti = t / 3, tj = t - ti * 3;
+      const int t = ks >> 1, ti = t / 3, tj = t - ti * 3;
+      const int off = (P3_LO - ti * BW_P3W - tj) * BW_PS + (ks & 1) * 32;
       const bf16x8 bf = tr_frag_sw<3>(s_w + ks * 32 * BW_LDW3, BW_LDW3, n0, lane);
 #pragma unroll
       for (int mt = 0; mt < 3; ++mt) {
-        const int m = min((mh + mt) * 16 + l16, 80);
-        const int a = m / 9, c = m - a * 9;
-        const bf16x8 af = *reinterpret_cast<const bf16x8*>(s_p3 + ((a - ti + 2) * BW_P3W + (c - tj + 2)) * BW_PS + o0);
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(s_p3 + pb[mt] + off);
         acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, acc[mt], 0, 0, 0);
       }
     }
@@ -1542,17 +1555,16 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_kernel(
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = (mh + mt) * 16 + lg * 4 + r;
-        if (m < 81) {
-          const int a = m / 9, c = m - a * 9;
-          const float v = bf2f(s_m2[m * 64 + n]) > 0.f ? acc[mt][r] : 0.f;
-          s_p2[((a + 1) * BW_P2W + (c + 1)) * BW_PS + n] = f2bf(v);
-        }
+        const int a = div9(m), c = m - a * 9;
+        const float v = bf2f(s_m2[min(m, 80) * 64 + n]) > 0.f ? acc[mt][r] : 0.f;
+        const int dst = m < 81 ? ((a + 1) * BW_P2W + (c + 1)) * BW_PS + n : 64 + l16;   // past 81: unread slot
+        s_p2[dst] = f2bf(v);
       }
   }
   // db3 partial from the dy3 image (before it is overwritten): thread -> channel group tid % 8, fixed order
   float part3[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int c = tid; c < 49 * 8; c += BW_T) {
-    const int px = c >> 3, g = c & 7, pa = px / 7, pb = px - pa * 7;
+    const int px = c >> 3, g = c & 7, pa = div7(px), pb = px - pa * 7;
     const uint4 v = *reinterpret_cast<const uint4*>(s_p3 + ((pa + 2) * BW_P3W + (pb + 2)) * BW_PS + g * 8);
 #pragma unroll
     for (int e = 0; e < 8; ++e) part3[e] += bf_lane(v, e);
@@ -1571,7 +1583,7 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_kernel(
 #undef ACA_W2_ST
   float part2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int c = tid; c < 81 * 8; c += BW_T) {
-    const int m = c >> 3, g = c & 7, a = m / 9, cc = m - a * 9;
+    const int m = c >> 3, g = c & 7, a = div9(m), cc = m - a * 9;
     const uint4 v = *reinterpret_cast<const uint4*>(s_p2 + ((a + 1) * BW_P2W + (cc + 1)) * BW_PS + g * 8);
     *reinterpret_cast<uint4*>(dy2g + ((size_t)b * 81 + m) * 64 + g * 8) = v;
 #pragma unroll
@@ -1608,16 +1620,22 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_kernel(
     floatx4 acc[7];
 #pragma unroll
     for (int i = 0; i < 7; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+    constexpr int P2_LO = BW_P2W + 1;
+    int pb1[7];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      const int u = min(i * 16 + l16, 99), yy = div10(u), xx = u - yy * 10;
+      pb1[i] = ((yy + 1) * BW_P2W + (xx + 1) - P2_LO) * BW_PS + lg * 8;
+    }
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) {
       const int d = ks >> 1, di = d >> 1, dj = d & 1, ob = (ks & 1) * 32;
       const int tap = (py + 2 * di) * 4 + (px + 2 * dj);
+      const int off = (P2_LO - di * BW_P2W - dj) * BW_PS + ob;
       const bf16x8 bf = tr_frag_sw<2>(s_w + (tap * 64 + ob) * BW_LDW2, BW_LDW2, nt * 16, lane);
 #pragma unroll
       for (int i = 0; i < 7; ++i) {
-        const int u = min(i * 16 + l16, 99), yy = u / 10, xx = u - yy * 10;
-        const bf16x8 af = *reinterpret_cast<const bf16x8*>(
-            s_p2 + ((yy - di + 1) * BW_P2W + (xx - dj + 1)) * BW_PS + ob + lg * 8);
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(s_p2 + pb1[i] + off);
         acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, acc[i], 0, 0, 0);
       }
     }
@@ -1628,10 +1646,9 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_kernel(
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int u = i * 16 + lg * 4 + r;
-        if (u < 100) {
-          const int yy = u / 10, xx = u - yy * 10;
-          s_d1[((2 * yy + py) * 20 + 2 * xx + px) * 32 + n] = f2bf(acc[i][r]);
-        }
+        const int yy = div10(u), xx = u - yy * 10;
+        const int dst = u < 100 ? ((2 * yy + py) * 20 + 2 * xx + px) * 32 + n : 400 * 32 + n;   // past 100: unread
+        s_d1[dst] = f2bf(acc[i][r]);
       }
   }
   __syncthreads();
@@ -1782,20 +1799,25 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
       for (int mt = 0; mt < 3; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
       // operands of k-step ks + 1 read while ks's MFMAs run (two register buffers): left to the compiler, every
       // MFMA waited out the LDS read issued just before it
-      int pix[3];
+      // A rows: per-lane LDS offsets (pixel, channel chunk lg) computed once per sample, relative to the largest tap
+      // displacement, so every k-step's read is that base + a compile-time immediate (k-step ks = tap ks / 2,
+      // channels (ks & 1) * 32 + lg * 8: lg * 8 < 32 never carries into the tap). Divisions by 9 / 10 below are
+      // exact multiply-shifts over their ranges (tests/test_lds_layouts_cpu.py); no per-read multiply or divide.
+      constexpr int P3_LO = 2 * BW_P3W + 2;
+      int pb[3];
 #pragma unroll
       for (int mt = 0; mt < 3; ++mt) {
         const int m = min((mh + mt) * 16 + l16, 80);
-        const int a = m / 9, c = m - a * 9;
-        pix[mt] = (a + 2) * BW_P3W + (c + 2);
+        const int a = div9(m), c = m - a * 9;
+        pb[mt] = ((a + 2) * BW_P3W + (c + 2) - P3_LO) * BW_PS + lg * 8;
       }
       bf16x8 af[2][3], bwf[2];
       auto ld2 = [&](int ks, int buf) {
-        const int kb = ks * 32 + lg * 8, t = kb >> 6, o0 = kb & 63, ti = t / 3, tj = t - ti * 3;
+        const int t = ks >> 1, ti = t / 3, tj = t - ti * 3;
+        const int off = (P3_LO - ti * BW_P3W - tj) * BW_PS + (ks & 1) * 32;   // >= 0
         bwf[buf] = tr_frag_sw<3>(s_w3z + ks * 32 * BW_LDW3, BW_LDW3, n0, lane);
 #pragma unroll
-        for (int mt = 0; mt < 3; ++mt)
-          af[buf][mt] = *reinterpret_cast<const bf16x8*>(s_p3 + (pix[mt] - ti * BW_P3W - tj) * BW_PS + o0);
+        for (int mt = 0; mt < 3; ++mt) af[buf][mt] = *reinterpret_cast<const bf16x8*>(s_p3 + pb[mt] + off);
       };
       ld2(0, 0);
 #pragma unroll
@@ -1807,21 +1829,22 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
       }
       pst(it, 6);
       const int n = n0 + l16;
+      // rows past the 81 outputs go to an unread slot (channel 64 + l16 of the dy2 image's first border pixel):
+      // select instead of branch
 #pragma unroll
       for (int mt = 0; mt < 3; ++mt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int m = (mh + mt) * 16 + lg * 4 + r;
-          if (m < 81) {
-            const int a = m / 9, c = m - a * 9;
-            const float v = bf2f(s_m2[m * 64 + n]) > 0.f ? acc[mt][r] : 0.f;
-            s_p2[((a + 1) * BW_P2W + (c + 1)) * BW_PS + n] = f2bf(v);
-          }
+          const int a = div9(m), c = m - a * 9;
+          const float v = bf2f(s_m2[min(m, 80) * 64 + n]) > 0.f ? acc[mt][r] : 0.f;
+          const int dst = m < 81 ? ((a + 1) * BW_P2W + (c + 1)) * BW_PS + n : 64 + l16;
+          s_p2[dst] = f2bf(v);
         }
     }
     float part3[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int c = tid; c < 49 * 8; c += BW_T) {
-      const int px = c >> 3, g = c & 7, pa = px / 7, pb = px - pa * 7;
+      const int px = c >> 3, g = c & 7, pa = div7(px), pb = px - pa * 7;
       const uint4 v = *reinterpret_cast<const uint4*>(s_p3 + ((pa + 2) * BW_P3W + (pb + 2)) * BW_PS + g * 8);
 #pragma unroll
       for (int e = 0; e < 8; ++e) part3[e] += bf_lane(v, e);
@@ -1833,7 +1856,7 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
     // ---- dy2 out (16-byte rows) + db2 / db3 channel sums
     float part2[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int c = tid; c < 81 * 8; c += BW_T) {
-      const int m = c >> 3, g = c & 7, a = m / 9, cc = m - a * 9;
+      const int m = c >> 3, g = c & 7, a = div9(m), cc = m - a * 9;
       const uint4 v = *reinterpret_cast<const uint4*>(s_p2 + ((a + 1) * BW_P2W + (cc + 1)) * BW_PS + g * 8);
       *reinterpret_cast<uint4*>(dy2g + ((size_t)b * 81 + m) * 64 + g * 8) = v;
 #pragma unroll
@@ -1859,18 +1882,19 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
       floatx4 acc[7];
 #pragma unroll
       for (int i = 0; i < 7; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
-      int pix1[7];
+      constexpr int P2_LO = BW_P2W + 1;   // largest tap displacement (di = dj = 1)
+      int pb1[7];
 #pragma unroll
       for (int i = 0; i < 7; ++i) {
-        const int u = min(i * 16 + l16, 99), yy = u / 10, xx = u - yy * 10;
-        pix1[i] = (yy + 1) * BW_P2W + (xx + 1);
+        const int u = min(i * 16 + l16, 99), yy = div10(u), xx = u - yy * 10;
+        pb1[i] = ((yy + 1) * BW_P2W + (xx + 1) - P2_LO) * BW_PS + lg * 8;
       }
       bf16x8 a1[2][7];   // k-step ks + 1's A fragments read while ks's MFMAs run
       auto ld1 = [&](int ks, int buf) {
         const int d = ks >> 1, di = d >> 1, dj = d & 1, ob = (ks & 1) * 32;
+        const int off = (P2_LO - di * BW_P2W - dj) * BW_PS + ob;   // >= 0
 #pragma unroll
-        for (int i = 0; i < 7; ++i)
-          a1[buf][i] = *reinterpret_cast<const bf16x8*>(s_p2 + (pix1[i] - di * BW_P2W - dj) * BW_PS + ob + lg * 8);
+        for (int i = 0; i < 7; ++i) a1[buf][i] = *reinterpret_cast<const bf16x8*>(s_p2 + pb1[i] + off);
       };
       ld1(0, 0);
 #pragma unroll
@@ -1889,15 +1913,15 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
         biasp[(size_t)b * 160 + tid] = v;                      // db3 (0..63) | db2 (64..127)
       }
       const int n = nt * 16 + l16;
+      // outputs past the class's 100 go to an unread slot (the dead y2-mask region behind the [400][32] dy1 rows)
 #pragma unroll
       for (int i = 0; i < 7; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int u = i * 16 + lg * 4 + r;
-          if (u < 100) {
-            const int yy = u / 10, xx = u - yy * 10;
-            s_d1[((2 * yy + py) * 20 + 2 * xx + px) * 32 + n] = f2bf(acc[i][r]);
-          }
+          const int yy = div10(u), xx = u - yy * 10;
+          const int dst = u < 100 ? ((2 * yy + py) * 20 + 2 * xx + px) * 32 + n : 400 * 32 + n;
+          s_d1[dst] = f2bf(acc[i][r]);
         }
     }
     __syncthreads();

@@ -224,3 +224,12 @@ def test_w1_lds_image_is_a_permutation_and_fragment_reads_are_conflict_free():
                 assert placed[row * 32 + ks * 4 + lg] == row * 32 + pc
                 addr.append((row * 256 + pc * 8) * 2)
             assert cycles([[addr[l] for l in g] for g in G128], 4, 64) == 4, (nt, ks)
+
+
+def test_fast_divisions_are_exact_over_their_ranges():
+    """cnn_fused.hip div9 / div10 / div7 (multiply-shift) == integer division over the ranges the kernels use."""
+    src = open(CNN).read()
+    for name, d, lim in (("div9", 9, 200), ("div10", 10, 1029), ("div7", 7, 64)):
+        m = re.search(name + r"\(int n\) \{ return \(int\)\(\(\(unsigned\)n \* (\d+)u\) >> (\d+)\); \}", src)
+        mul, sh = int(m.group(1)), int(m.group(2))
+        assert all((n * mul) >> sh == n // d for n in range(lim)), name

@@ -1,6 +1,7 @@
 """Phase stamps of the per-env fused rollout step (cnn_fused.hip pong_fused_env_step_kernel) at the Breakout-shape
 bank (128 envs), split (two workgroups per env) and whole-env forms: event-timed launches plus per-workgroup
-s_memrealtime stamps, medians over workgroups (per half for the split form). GPU only."""
+s_memrealtime stamps, medians over workgroups (per half for the split form); conv2 / conv3 weights fragment-ordered
+(EngineOpts.frag_weights) or row-major. GPU only."""
 import json
 import os
 import sys
@@ -25,15 +26,20 @@ def main():
     b = eng.bufs(N)
     eng.forward(st.obs[0], b, head=False, shift_out=st.obs[1], fc_parts=True)
     out = {}
-    for split in (True, False):
+    _, F2, F3, _ = eng.trunk_w()
+    for split, frag in ((True, True), (True, False), (False, True)):
+        if frag and eng.frag is None:
+            continue
+        W2, W3 = (F2, F3) if frag else (eng.sW2, eng.sW3)
+
         def launch(stamps=None):
             hp, S = eng.last_fc
             ops.pong_fused_env_step(b.h, eng.sWh, eng.bh, b.z, st.actions[0], st.logp[0], st.entropy[0],
                                     st.values[0], KEY_ENV_BITS, tr.policy_seed, env.state, env.t, env.tg,
                                     env.ep_ret, env.ep_stats, env.env_ids, st.obs[1], st.rewards[0], st.dones[0],
                                     st.truncated[0], env.seed, env.max_episode_steps, hp, S, eng.bfc, eng.sW1,
-                                    eng.b1, eng.sW2, eng.b2, eng.sW3, eng.b3, b.y1, b.y2, b.y3, 1.0 / 255.0,
-                                    st.obs[2], list(env.next_state()) if split else None, stamps)
+                                    eng.b1, W2, eng.b2, W3, eng.b3, b.y1, b.y2, b.y3, 1.0 / 255.0,
+                                    st.obs[2], list(env.next_state()) if split else None, stamps, frag)
             if split:
                 env.flip()
         for _ in range(5):
@@ -61,7 +67,7 @@ def main():
             res[name] = ph
         res["start spread us"] = round(float(x[:, 0].max() - x[:, 0].min()), 2)
         res["end spread us (last - first end)"] = round(float(x[:, 7].max() - x[:, 7].min()), 2)
-        out["split" if split else "whole"] = res
+        out[("split" if split else "whole") + ("_frag" if frag else "_rowmajor")] = res
     print(json.dumps(out, indent=1))
 
 

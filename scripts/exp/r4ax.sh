@@ -1,0 +1,7 @@
+#!/bin/bash
+# round-end rehearsal: smoke + the whole GPU suite
+set -o pipefail
+O=gpurun_out/r4ax
+mkdir -p $O
+timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && \
+timeout -k 10 1000 python3 -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1

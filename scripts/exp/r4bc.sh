@@ -1,0 +1,7 @@
+#!/bin/bash
+# A3C CartPole learning test: same code twice (is the single-worker run deterministic?)
+set -o pipefail
+O=gpurun_out/r4bc
+mkdir -p $O
+timeout -k 10 400 python3 -u -m pytest tests/test_a3c_gpu_mode.py -k learns -x -q --timeout 300 --timeout-method thread > $O/run1.log 2>&1 ; \
+timeout -k 10 400 python3 -u -m pytest tests/test_a3c_gpu_mode.py -k learns -x -q --timeout 300 --timeout-method thread > $O/run2.log 2>&1 ; true

@@ -45,6 +45,50 @@ __global__ void __launch_bounds__(256) probe(const uint4* __restrict__ buf, int 
   if constexpr (DMA) { if (tid == 0 && lds[1].x == 0x12345678u) sink[1] = 1.f; }
 }
 
+// Row-scattered pattern of the learner kernels' weight-fragment loads: lane (r = lane & 15, q = lane >> 4) of wave w
+// reads 16 B at row (w * 16 + r) and column chunk q + 4 u of a row-major [rows][ROWB bytes] matrix, U loads in
+// flight per thread -- a wave load covers 16 rows x 64 contiguous bytes (16 cache lines, half of each).
+template <int U, int ROWB>
+__global__ void __launch_bounds__(256) probe_rows(const uint4* __restrict__ buf, int rows, int reps, float* sink,
+                                                  unsigned long long* clk) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, r = lane & 15, q = lane >> 4;
+  unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+  uint4 acc = make_uint4(0, 0, 0, 0);
+  constexpr int CH = ROWB / 16;   // 16-byte chunks per row
+  for (int rep = 0; rep < reps; ++rep) {
+    for (int rb = 0; rb < rows; rb += 64) {
+      for (int c0 = 0; c0 < CH; c0 += 4 * U) {
+        uint4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = buf[(size_t)(rb + wid * 16 + r) * CH + c0 + 4 * u + q];
+#pragma unroll
+        for (int u = 0; u < U; ++u) { acc.x ^= v[u].x; acc.y ^= v[u].y; acc.z ^= v[u].z; acc.w ^= v[u].w; }
+      }
+    }
+  }
+  unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+  if (tid == 0) { clk[blockIdx.x * 2] = t1 - t0; clk[blockIdx.x * 2 + 1] = r1 - r0; }
+  if (acc.x == 0x12345678u && acc.y == 1u) sink[0] = 1.f;
+}
+
+template <int U, int ROWB>
+void run_rows(const uint4* d, int rows, int reps, float* sink, unsigned long long* clk, int grid) {
+  probe_rows<U, ROWB><<<grid, 256>>>(d, rows, 1, sink, clk);
+  hipDeviceSynchronize();
+  probe_rows<U, ROWB><<<grid, 256>>>(d, rows, reps, sink, clk);
+  hipDeviceSynchronize();
+  std::vector<unsigned long long> h(2 * grid);
+  hipMemcpy(h.data(), clk, 16 * grid, hipMemcpyDeviceToHost);
+  double cyc = 0, us = 0;
+  for (int b = 0; b < grid; ++b) { cyc += h[2 * b]; us += h[2 * b + 1] * 0.01; }
+  cyc /= grid; us /= grid;
+  const double bytes = (double)rows * ROWB * reps;
+  printf("rows  U=%2d grid=%3d rowB=%4d (%d KB): %.1f B/clk/CU, %.1f GB/s per CU\n", U, grid, ROWB, rows * ROWB / 1024,
+         bytes / cyc, bytes / us / 1e3);
+}
+
 template <int U, bool DMA>
 void run(const uint4* d, int n16, int reps, float* sink, unsigned long long* clk, int grid) {
   probe<U, DMA><<<grid, 256>>>(d, n16, 1, sink, clk);   // warm L2
@@ -68,6 +112,9 @@ int main() {
   hipMalloc(&d, n16 * 16); hipMalloc(&sink, 64); hipMalloc(&clk, 16 * 256);
   hipMemset(d, 1, n16 * 16);
   for (int grid : {1, 256}) {
+    run_rows<1, 1024>(d, 256, 20, sink, clk, grid);    // one round of loads per 64 B of each of 16 rows
+    run_rows<4, 1024>(d, 256, 20, sink, clk, grid);
+    run_rows<16, 1024>(d, 256, 20, sink, clk, grid);   // the MLP critic layer shape: 16 loads per lane per round
     run<4, false>(d, n16, 20, sink, clk, grid);
     run<8, false>(d, n16, 20, sink, clk, grid);
     run<16, false>(d, n16, 20, sink, clk, grid);

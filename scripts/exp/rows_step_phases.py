@@ -1,5 +1,6 @@
 """Phase stamps of the row-split fused rollout step (cnn_fused.hip pong_fused_step_kernel, 7 workgroups per env) at
-the headline bank (Pong, 32 envs): per-workgroup s_memrealtime stamps, medians over workgroups. GPU only."""
+the headline bank (Pong, 32 envs): per-workgroup s_memrealtime stamps, medians over workgroups; conv2 / conv3 weights
+fragment-ordered (EngineOpts.frag_weights) and row-major. GPU only."""
 import json
 import os
 import sys
@@ -25,17 +26,26 @@ def main():
     N = env.num_envs
     b = eng.bufs(N)
     eng.forward(st.obs[0], b, head=False, shift_out=st.obs[1], fc_parts=True)
+    out = {}
+    _, F2, F3, _ = eng.trunk_w()
+    for frag in (True, False):
+        W2, W3 = (F2, F3) if frag else (eng.sW2, eng.sW3)
+        out["frag" if frag else "rowmajor"] = phases(ops, tr, st, env, eng, N, b, W2, W3, frag)
+    print(json.dumps(out, indent=1))
+
+
+def phases(ops, tr, st, env, eng, N, b, W2, W3, frag):
     sts = torch.zeros(N * 7 * 16, dtype=torch.int64, device="cuda:0")
     res = {}
-    for rep in range(3):
+    for rep in range(6):
         hp, S = eng.last_fc
         sn, tn, tgn, ern = env.next_state()
         ops.pong_fused_step(b.h, eng.sWh, eng.bh, b.z, st.actions[0], st.logp[0], st.entropy[0], st.values[0],
                             KEY_ENV_BITS, tr.policy_seed, env.state, env.t, env.tg, env.ep_ret, sn, tn, tgn, ern,
                             env.ep_stats, env.env_ids, st.obs[0], st.obs[1], st.rewards[0], st.dones[0],
                             st.truncated[0], env.seed, env.max_episode_steps, hp, S, eng.bfc, eng.sW1, eng.b1,
-                            eng.sW2, eng.b2, eng.sW3, eng.b3, b.y1, b.y2, b.y3, 1.0 / 255.0, st.obs[2],
-                            sts if rep == 2 else None)
+                            W2, eng.b2, W3, eng.b3, b.y1, b.y2, b.y3, 1.0 / 255.0, st.obs[2],
+                            sts if rep == 5 else None, frag)
         env.flip()
     torch.cuda.synchronize()
     x = sts.view(N * 7, 16).double().cpu() * 10e-3
@@ -45,7 +55,7 @@ def main():
     res["total (start -> conv3 issued)"] = round(float((x[:, 4] - x[:, 0]).median()), 2)
     res["start spread us"] = round(float(x[:, 0].max() - x[:, 0].min()), 2)
     res["first start -> last end us"] = round(float(x[:, 4].max() - x[:, 0].min()), 2)
-    print(json.dumps(res, indent=1))
+    return res
 
 
 if __name__ == "__main__":

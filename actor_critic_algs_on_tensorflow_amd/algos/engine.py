@@ -285,6 +285,10 @@ class CNNEngine:
                 F1, F2, F3 = self.frag   # mode 5: the bf16-staged kernel on the fragment-ordered weights
                 G.cnn_trunk_fwd(obs, F1, self.b1, F2, self.b2, F3, self.b3, b.y1, b.y2, b.y3, shift_out=shift_out,
                                 mode=5, obs_idx=obs_idx)
+            elif B <= self.trunk_rows_max_b and self.frag is not None:
+                _, F2, F3 = self.frag   # modes 6 / 7: the row-split kernel on fragment-ordered conv2 / conv3 weights
+                G.cnn_trunk_fwd(obs, self.sW1, self.b1, F2, self.b2, F3, self.b3, b.y1, b.y2, b.y3,
+                                shift_out=shift_out, mode=self.trunk_mode + 5, obs_idx=obs_idx)
             else:
                 G.cnn_trunk_fwd(obs, self.sW1, self.b1, self.sW2, self.b2, self.sW3, self.b3, b.y1, b.y2, b.y3,
                                 shift_out=shift_out, mode=self.trunk_mode if B <= self.trunk_rows_max_b else

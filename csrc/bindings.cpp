@@ -128,7 +128,7 @@ hipError_t aca_cnn_trunk_bwd(const uint16_t*, const uint16_t*, const uint16_t*, 
                              uint16_t*, uint16_t*, float*, int, uint64_t*, int, hipStream_t);
 hipError_t aca_cnn_trunk_rows(const uint8_t*, const uint16_t*, const float*, const uint16_t*, const float*,
                               const uint16_t*, const float*, uint16_t*, uint16_t*, uint16_t*, int, float, uint8_t*,
-                              uint8_t*, uint64_t*, int, hipStream_t);
+                              uint8_t*, uint64_t*, int, int, hipStream_t);
 }
 
 namespace {
@@ -1458,18 +1458,20 @@ void cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tenso
   }
   uint8_t* co = nullptr;
   if (copy_out.has_value() && copy_out->defined()) {
-    TORCH_CHECK(mode >= 1, "cnn_trunk_fwd: copy_out needs a row-split mode");
+    TORCH_CHECK(mode == 1 || mode == 2 || mode == 6 || mode == 7, "cnn_trunk_fwd: copy_out needs a row-split mode");
     need(*copy_out, at::kByte, "copy_out");
     TORCH_CHECK(copy_out->numel() == obs.numel() && reinterpret_cast<uintptr_t>(copy_out->data_ptr()) % 16 == 0 &&
                     copy_out->data_ptr() != obs.data_ptr(),
                 "cnn_trunk_fwd: copy_out must be a distinct, aligned [B, 4, 84, 84] uint8 buffer");
     co = ptr<uint8_t>(*copy_out);
   }
-  if (mode == 1 || mode == 2) {   // 2: the row kernel with its conv2/conv3 weight loads issued after conv1
+  if (mode == 1 || mode == 2 || mode == 6 || mode == 7) {
+    // 2: the row kernel with its conv2/conv3 weight loads issued after conv1; 6 / 7: modes 1 / 2 reading
+    // fragment-ordered W2 / W3 copies (W1 row-major)
     check(aca_cnn_trunk_rows(ptr<uint8_t>(obs), ptr<uint16_t>(W1), ptr<float>(b1), ptr<uint16_t>(W2),
                              ptr<float>(b2), ptr<uint16_t>(W3), ptr<float>(b3), ptr<uint16_t>(y1), ptr<uint16_t>(y2),
                              ptr<uint16_t>(y3), (int)B, (float)scale, so, co, stamps_ptr(stamps, B * 7),
-                             mode == 2 ? 1 : 0, cur_stream(obs)),
+                             (mode == 2 || mode == 7) ? 1 : 0, mode >= 6 ? 1 : 0, cur_stream(obs)),
           "cnn_trunk_rows");
     return;
   }
@@ -1483,7 +1485,7 @@ void cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tenso
           "cnn_trunk_fwd_s16");
     return;
   }
-  TORCH_CHECK(mode == 0, "cnn_trunk_fwd: mode must be 0..3 or 5");
+  TORCH_CHECK(mode == 0, "cnn_trunk_fwd: mode must be 0..3 or 5..7");
   check(aca_cnn_trunk_fwd(ptr<uint8_t>(obs), ptr<uint16_t>(W1), ptr<float>(b1), ptr<uint16_t>(W2), ptr<float>(b2),
                           ptr<uint16_t>(W3), ptr<float>(b3), ptr<uint16_t>(y1), ptr<uint16_t>(y2), ptr<uint16_t>(y3),
                           (int)B, (float)scale, so, stamps_ptr(stamps, B), idxp, cur_stream(obs)),

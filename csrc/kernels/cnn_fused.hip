@@ -898,7 +898,7 @@ __device__ __forceinline__ void trunk_rows_compute(const u16* __restrict__ s_in,
 }
 
 
-template <bool LATE_W>
+template <bool LATE_W, bool FRAG>
 __global__ void __launch_bounds__(T_THREADS) cnn_trunk_rows_kernel(
     const uint8_t* __restrict__ obs, const u16* __restrict__ W1, const float* __restrict__ b1,
     const u16* __restrict__ W2, const float* __restrict__ b2, const u16* __restrict__ W3,
@@ -972,8 +972,8 @@ __global__ void __launch_bounds__(T_THREADS) cnn_trunk_rows_kernel(
   }
   stamp(stamps, 1);
   bf16x8 bw2[16], bw3[18];
-  trunk_rows_compute<LATE_W ? 1 : 0>(s_in, s_w1, s_y1, s_y2, e, r, bias1a, bias1b, bias2, bias3, W2, W3, y1g, y2g,
-                                     y3g, scale, stamps, bw2, bw3);
+  trunk_rows_compute<LATE_W ? 1 : 0, FRAG>(s_in, s_w1, s_y1, s_y2, e, r, bias1a, bias1b, bias2, bias3, W2, W3, y1g,
+                                           y2g, y3g, scale, stamps, bw2, bw3);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -2032,14 +2032,18 @@ extern "C" hipError_t aca_cnn_trunk_fwd_s16(const uint8_t* obs, const uint16_t* 
 extern "C" hipError_t aca_cnn_trunk_rows(const uint8_t* obs, const uint16_t* W1, const float* b1, const uint16_t* W2,
                                          const float* b2, const uint16_t* W3, const float* b3, uint16_t* y1,
                                          uint16_t* y2, uint16_t* y3, int B, float scale, uint8_t* shift_out,
-                                         uint8_t* copy_out, uint64_t* stamps, int late_w, hipStream_t stream) {
+                                         uint8_t* copy_out, uint64_t* stamps, int late_w, int frag,
+                                         hipStream_t stream) {
+  // frag: W2 / W3 are the fragment-ordered copies (W1 row-major: the kernel stages it through LDS)
   if (B <= 0) return hipSuccess;
-  if (late_w)
-    aca::cnn_trunk_rows_kernel<true><<<B * aca::TR_ROWS, aca::T_THREADS, 0, stream>>>(
-        obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale, shift_out, copy_out, stamps);
-  else
-    aca::cnn_trunk_rows_kernel<false><<<B * aca::TR_ROWS, aca::T_THREADS, 0, stream>>>(
-        obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale, shift_out, copy_out, stamps);
+#define ACA_ROWS(LW, FR)                                                                                         \
+  aca::cnn_trunk_rows_kernel<LW, FR><<<B * aca::TR_ROWS, aca::T_THREADS, 0, stream>>>(                          \
+      obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale, shift_out, copy_out, stamps);
+  if (late_w && frag) ACA_ROWS(true, true)
+  else if (late_w) ACA_ROWS(true, false)
+  else if (frag) ACA_ROWS(false, true)
+  else ACA_ROWS(false, false)
+#undef ACA_ROWS
   return hipGetLastError();
 }
 

@@ -389,3 +389,31 @@ def test_fragment_ordered_weights_equal_row_major(cuda, preset_name, envs, monke
     for k, (a, b) in enumerate(zip(*runs)):
         for j, (x, y) in enumerate(zip(a, b)):
             assert torch.equal(x, y), (k, j)
+
+
+def test_row_split_trunk_on_fragment_ordered_weights_is_bitwise(cuda):
+    """cnn_trunk_fwd modes 6 / 7 (the row-split trunk reading fragment-ordered conv2 / conv3 weights) == modes 1 / 2
+    bit for bit, shifted frames included."""
+    from actor_critic_algs_on_tensorflow_amd.ops import gemm as G
+    from actor_critic_algs_on_tensorflow_amd.ops.optim import frag_order
+    g = torch.Generator(device="cpu").manual_seed(21)
+    B = 37
+    obs = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, generator=g).to(cuda)
+    W1 = (torch.randn(32, 256, generator=g) * 0.05).to(torch.bfloat16).to(cuda)
+    W2 = (torch.randn(64, 512, generator=g) * 0.05).to(torch.bfloat16).to(cuda)
+    W3 = (torch.randn(64, 576, generator=g) * 0.05).to(torch.bfloat16).to(cuda)
+    b1, b2, b3 = ((torch.rand(n, generator=g) * 0.1 - 0.02).to(cuda) for n in (32, 64, 64))
+    F2, F3 = frag_order(W2, 64, 512), frag_order(W3, 64, 576)
+    for base in (1, 2):
+        outs = []
+        for mode in (base, base + 5):
+            ys = [torch.full((B * r, c), float("nan"), dtype=torch.bfloat16, device=cuda)
+                  for r, c in ((400, 32), (81, 64), (49, 64))]
+            sh = torch.zeros_like(obs)
+            w2, w3 = (F2, F3) if mode > 5 else (W2, W3)
+            G.cnn_trunk_fwd(obs, W1, b1, w2, b2, w3, b3, *ys, shift_out=sh, mode=mode)
+            outs.append(ys + [sh])
+        torch.cuda.synchronize()
+        for a, b in zip(*outs):
+            assert torch.equal(a.view(torch.uint8) if a.dtype == torch.uint8 else a.view(torch.int16),
+                               b.view(torch.uint8) if b.dtype == torch.uint8 else b.view(torch.int16)), base

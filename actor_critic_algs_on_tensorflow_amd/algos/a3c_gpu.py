@@ -34,14 +34,16 @@ actor/critic as a TF bundle ``<checkpoint_dir>/model-<Env>-<global step>`` every
 reference's ``CheckpointSaverHook``; reference variable names, so ``cli/test_model.py`` evaluates it) and every
 worker keeps a reference-format Logger file ``<log_dir>/worker_<task>.log``.
 
-Failure handling: a worker that dies mid-run (``fault_inject="rank:iteration"``) makes the PS's next
-control-plane receive fail -- gloo reports the closed peer, or the group timeout expires -- and the PS returns an
-``"aborted"`` summary instead of waiting forever; the surviving workers' exchange with the departed PS raises, so
-every process of the job ends.
+Failure handling: a worker that dies mid-run (``fault_inject="rank:iteration"`` at the start of an
+iteration; ``"rank:iteration:push"`` after its push header, before the payload; ``"rank:iteration:reply"`` after the
+push, before the PS's reply) makes the PS's next exchange with it fail -- gloo reports the closed peer, or the group
+timeout expires -- and the PS returns an ``"aborted"`` summary instead of waiting forever or raising; the surviving
+workers' exchange with the departed PS raises, so every process of the job ends.
 """
 from __future__ import annotations
 
 import os
+import sys
 import time
 
 import torch
@@ -189,21 +191,35 @@ class DeviceParameterServer:
         return self.n_applies[w] - slowest <= self.max_staleness
 
     def serve(self):
-        """Serves until every worker said DONE. A failed control-plane receive (a worker died: gloo reports the
-        closed peer, or the group timeout expired) ends the PS with ``status == "aborted"`` instead of a hang. Only
-        that receive is treated as a departure: a failure of the apply (optimiser launch) or of the reply
-        propagates, so a kernel error on the PS is never reported as a worker death."""
+        """Serves until every worker said DONE. A failed exchange with a worker -- the control-plane header receive,
+        the payload receive after a push header, or the reply (header + parameters) to a worker -- means the worker
+        died (gloo reports the closed peer, or the group timeout expired) and ends the PS with ``status ==
+        "aborted"`` instead of a hang or an exception. Only peer I/O is treated as a departure: a failure of the
+        apply (optimiser launch) propagates, so a kernel error on the PS is never reported as a worker death."""
         try:
             self._serve()
         except _PeerLost as e:
             self.status = "aborted"
             self.error = repr(e.__cause__)
 
-    def _recv_hdr(self):
+    @staticmethod
+    def _peer_io(fn, *args):
+        """One exchange with a worker; a transport error (gloo: peer closed / timeout -- DistBackendError is a
+        RuntimeError) becomes :class:`_PeerLost`."""
         try:
-            return self.planes.recv_hdr()
-        except RuntimeError as e:   # gloo: peer closed / timeout (DistBackendError is a RuntimeError)
+            return fn(*args)
+        except RuntimeError as e:
             raise _PeerLost() from e
+
+    def _recv_hdr(self):
+        return self._peer_io(self.planes.recv_hdr)
+
+    def _reply(self, w):
+        self._peer_io(self.reply, w)
+
+    def _apply_and_reply(self, w, v):
+        self.apply(w, v)      # not peer I/O: errors propagate
+        self._reply(w)
 
     def _serve(self):
         pending = []   # deferred applies (stale-synchronous bound), served in arrival order once allowed
@@ -213,9 +229,9 @@ class DeviceParameterServer:
                 if cmd == CMD_DONE:
                     self.live.discard(src)
                 elif cmd == CMD_PULL:
-                    self.reply(src)
+                    self._reply(src)
                 else:
-                    self.planes.recv(self._pay[src], src)
+                    self._peer_io(self.planes.recv, self._pay[src], src)
                     pending.append((src, version))
             progressed = True
             while progressed:
@@ -223,14 +239,12 @@ class DeviceParameterServer:
                 for i, (w, v) in enumerate(pending):
                     if self._allowed(w) or not self.live - {w}:
                         pending.pop(i)
-                        self.apply(w, v)
-                        self.reply(w)
+                        self._apply_and_reply(w, v)
                         progressed = True
                         break
             if not self.live and pending:   # every other worker finished: nothing left to wait for
                 for w, v in pending:
-                    self.apply(w, v)
-                    self.reply(w)
+                    self._apply_and_reply(w, v)
                 pending = []
 
 
@@ -258,6 +272,7 @@ class GPUWorker:
             self.tr.logger = Logger(os.path.join(log_dir, f"worker_{task}.log"), quiet=cfg.quiet)
         self.ckpt_base = checkpoint_basename
         self.version = 0
+        self._die_at = None   # mid-exchange fault point armed by run() (fault_inject "rank:iter:push|reply")
         n = [e - s for s, e in ranges]
         self._pay = [torch.zeros(_pay_len(k), device=self.device) for k in n]
         self.saved = []
@@ -271,11 +286,15 @@ class GPUWorker:
         lr = tr.actor_opt.lr
         for sid, ((s, e), r) in enumerate(zip(self.ranges, self.ps_ranks)):
             self.planes.send_hdr([CMD_PULL if pull_only else CMD_APPLY, self.task, self.version, 0], r)
+            if not pull_only and self._die_at == "push":   # fault point: the header is out, the payload never comes
+                self._die()
             if not pull_only:
                 p = self._pay[sid]
                 p[:e - s].copy_(flat.grad[s:e])
                 p[p.numel() - PAY_ALIGN:p.numel() - PAY_ALIGN + 1].copy_(lr.reshape(1))
                 self.planes.send(p, r)
+        if not pull_only and self._die_at == "reply":   # fault point: pushed, dies before the PS's reply
+            self._die()
         version = 0
         for sid, ((s, e), r) in enumerate(zip(self.ranges, self.ps_ranks)):
             _, (cmd, _sid, gstep, _) = self.planes.recv_hdr(r)
@@ -286,12 +305,19 @@ class GPUWorker:
         self.version = version
         return version
 
+    @staticmethod
+    def _die():
+        from .trainer import FAULT_EXIT_CODE
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(FAULT_EXIT_CODE)
+
     def run(self, total_updates, report_every=0):
         """Trains until the PS global step reaches ``total_updates``. Returns the global step after each of this
         worker's updates; with ``report_every`` also (update, global step, mean finished-episode return) rows in
         ``self.returns`` (a host read of the env bank's episode statistics every ``report_every`` updates). Worker
         0 (the chief) checkpoints every ``save_every`` global steps; each worker logs reference-format rows."""
-        from .trainer import FAULT_EXIT_CODE, parse_fault
+        from .trainer import parse_fault
         cfg, tr = self.cfg, self.tr
         fault = parse_fault(cfg.fault_inject)
         self._exchange(pull_only=True)   # initial sync_w_global (reference bug #12 fixed)
@@ -312,8 +338,10 @@ class GPUWorker:
             return (s / n if n else float("nan")), n, (ln / n if n else float("nan"))
 
         while self.version < total_updates:
-            if fault is not None and fault == (self.rank, i):   # SURVEY §5.3 test hook: die without goodbye
-                os._exit(FAULT_EXIT_CODE)
+            if fault is not None and fault[:2] == (self.rank, i):   # SURVEY §5.3 test hook: die without goodbye
+                if len(fault) == 2:
+                    self._die()
+                self._die_at = fault[2]   # inside this iteration's exchange (parse_fault: "push" / "reply")
             tr.step()
             hist.append(self.version)
             rep_due = bool(report_every) and len(hist) % report_every == 0

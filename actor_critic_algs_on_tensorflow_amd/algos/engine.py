@@ -178,6 +178,12 @@ class CNNEngine:
         if o.frag_weights and self.dev.type == "cuda" and implicit:
             self.frag = [torch.empty(n, dtype=torch.bfloat16, device=self.dev) for n in (32 * 256, 64 * 512, 64 * 576)]
             self.sync_frag()
+        # fragment-ordered bf16 copy of Wfc for the rollout fc product (fc_rollout.hip, EngineOpts.fc_frag)
+        self.fc_frag = o.fc_frag if (self.dev.type == "cuda" and o.fc_frag >= 0) else -1
+        self.wfc_frag = None
+        if self.fc_frag >= 0:
+            self.wfc_frag = torch.empty(3136 * 512, dtype=torch.bfloat16, device=self.dev)
+            self.sync_fc_frag()
         self.side = torch.cuda.Stream(device=self.dev) if self.dev.type == "cuda" else None
         self._ev = [torch.cuda.Event() for _ in range(6)] if self.side is not None else None
 
@@ -193,11 +199,26 @@ class CNNEngine:
     def sync_frag(self):
         """Rebuild the fragment-ordered copies from the bf16 shadow (parameters changed outside the optimiser:
         construction, checkpoint load, parameter-server pull)."""
+        self.sync_fc_frag()
         if self.frag is None:
             return
         from ..ops.optim import frag_order
         for S, (K, N), F in zip((self.sW1, self.sW2, self.sW3), self._FRAG_SHAPES, self.frag):
             F.copy_(frag_order(S, K, N))
+
+    @torch.no_grad()
+    def sync_fc_frag(self):
+        """Rebuild the fragment-ordered Wfc copy from the bf16 shadow."""
+        if getattr(self, "wfc_frag", None) is not None:
+            from ..ops.optim import frag_order_kc
+            self.wfc_frag.copy_(frag_order_kc(self.sWfc, 3136, 512))
+
+    def _fc_rollout(self, b, hp):
+        """Split-K planes of the rollout fc product into ``hp``; returns the plane count."""
+        if self.fc_frag >= 0 and b.B <= 32:
+            return int(_native.require().fc_rollout(b.y3.view(b.B, 3136), self.wfc_frag, hp, self.fc_frag))
+        return G.gemm(b.y3, 3136, True, self.sWfc, 512, False, hp, 512, 3, b.B, 512, 3136, workspace=self.ws,
+                      max_planes=self.fc_max_planes)
 
     def trunk_w(self):
         """(W1, W2, W3) operands of the fused trunk kernels and whether they are fragment-ordered."""
@@ -256,8 +277,7 @@ class CNNEngine:
     def fc_planes(self, b: _Bufs):
         """fc product of ``b.y3`` as split-K partial planes (consumed by the fused step / value kernels)."""
         hp = self.hpart(b.B)
-        S = G.gemm(b.y3, 3136, True, self.sWfc, 512, False, hp, 512, 3, b.B, 512, 3136, workspace=self.ws,
-                   max_planes=self.fc_max_planes)
+        S = self._fc_rollout(b, hp)
         self.last_fc = (hp, S)
         return hp, S
 
@@ -321,8 +341,7 @@ class CNNEngine:
             # partial planes only: the consumer (fused policy/env kernel or fc_value) reduces, adds the bias,
             # applies ReLU and writes b.h
             hp = self.hpart(B)
-            S = G.gemm(b.y3, 3136, True, self.sWfc, 512, False, hp, 512, 3, B, 512, 3136, workspace=ws,
-                       max_planes=self.fc_max_planes)
+            S = self._fc_rollout(b, hp)
             self.last_fc = (hp, S)
             return shifted if want_shift else b.z
         if self.big_gemm_ok(B):   # 128 x 128 tiles, 2 splits: 256 workgroups at B = 4096

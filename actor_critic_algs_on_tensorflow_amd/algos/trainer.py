@@ -52,10 +52,17 @@ FAULT_EXIT_CODE = 43   # exit status of a rank killed by ``fault_inject`` (SURVE
 
 
 def parse_fault(spec):
-    """``"rank:iteration"`` -> (rank, iteration) or None."""
+    """``"rank:iteration"`` -> (rank, iteration); ``"rank:iteration:where"`` -> (rank, iteration, where) for the
+    async PS worker's mid-exchange fault points (``where`` = ``"push"``: die after the push header, before the
+    payload; ``"reply"``: die after the push, before the PS's reply); None for no fault."""
     if not spec:
         return None
-    r, it = str(spec).split(":")
+    parts = str(spec).split(":")
+    if len(parts) == 3:
+        if parts[2] not in ("push", "reply"):
+            raise ValueError(f"fault_inject {spec!r}: the fault point must be 'push' or 'reply'")
+        return int(parts[0]), int(parts[1]), parts[2]
+    r, it = parts
     return int(r), int(it)
 
 # layout of the device statistics buffer; slots 0..6 are written directly by the fused loss kernel
@@ -603,6 +610,8 @@ class ActorCriticTrainer:
             if self.engine is not None:
                 opt.zero_grad_after = not stores_all
             opt.step()
+        if self.engine is not None and self.engine.wfc_frag is not None:
+            self.engine.sync_fc_frag()
         if self.mlp is not None:
             self.mlp.sync_shadow()
 
@@ -1146,17 +1155,28 @@ class ActorCriticTrainer:
                     avg_rew=avg_rew, print_tog=print_tog, act_lr=self.actor_opt.get_lr(), avg_ent=s["entropy"],
                     worker_id=self.worker_id, ev_before=s["ev_before"], ev_after=s["ev_after"])
         s.update(avg_rew=avg_rew, episodes=n_ep, ep_len=ep_len)
+        if self._kl_deferred():
+            # DP + global advantage normalisation: this row's kl is rank 0's local post-update KL and act_lr the value
+            # before the KL-adaptive rule, which settles inside the NEXT update's moments all-reduce (_kl_deferred);
+            # the lr sequence used for training is the single-GPU one, the logged columns lag it by one update
+            s["kl_lr_presettle"] = 1
         return s
 
-    def check_health(self):
+    def check_health(self, collective=False):
         """Raises if a native in-launch hand-off timed out (its outputs, and so this update's gradients, would be
         corrupt). One host read; called at log / checkpoint time, after the capture warm-up and at the end of
-        ``train``."""
-        if self.engine is not None:
-            errs = self.engine.health_errors()
-            if errs:
-                raise RuntimeError("native engine hand-off timed out (" + ", ".join(errs) + "): the affected "
-                                   "updates trained on incomplete data")
+        ``train``. ``collective`` (DP, at points every rank reaches: checkpoints, end of train): the flag is
+        max-all-reduced first, so every rank raises together instead of the healthy ones waiting in the next
+        collective until ``dist_timeout_s``."""
+        errs = self.engine.health_errors() if self.engine is not None else []
+        if collective and self.dp is not None:
+            flag = torch.tensor([1.0 if errs else 0.0], device=self.device)
+            torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.MAX, group=self.dp.group)
+            if float(flag) > 0 and not errs:
+                errs = ["a peer rank's native hand-off"]
+        if errs:
+            raise RuntimeError("native engine hand-off timed out (" + ", ".join(errs) + "): the affected "
+                               "updates trained on incomplete data")
 
     def train(self, num_updates=None, callback=None):
         cfg = self.cfg
@@ -1190,13 +1210,16 @@ class ActorCriticTrainer:
                 callback(self, it)
         self.flush_pending()
         self.flush_kl()
-        self.check_health()
+        self.check_health(collective=True)
         return history
 
     # ------------------------------------------------------------------ checkpoints
     def save_checkpoint(self, path=None):
-        self.check_health()
+        # the collective flush first: a rank whose hand-off timed out raises only after its peers left the
+        # all-reduce, so they reach their own check (or the next collective's error) instead of waiting out
+        # dist_timeout_s in a collective this rank never joins
         self.flush_kl()
+        self.check_health(collective=True)
         from ..ckpt import save_trainer
         return save_trainer(self, path)
 

@@ -25,6 +25,8 @@ class EngineOpts:
     frag_weights: bool = True         # conv weights also kept fragment-ordered (written by the optimiser step): the
                                       # MFMA weight loads become one contiguous 1 KB read per wave
     fc_max_planes: int = 32           # split-K partial planes of the rollout fc product (consumer-reduced)
+    fc_frag: int = -1                 # rollout fc product (<= 32 envs) on a fragment-ordered Wfc copy (fc_rollout.hip
+                                      # variant 0..6; -1: the general GEMM on the row-major shadow)
     # -- learner -------------------------------------------------------------------------------------------------
     a2c_head: bool = True             # A2C: V(s_T) + returns + loss + head backward in one launch (loss.hip a2c_head)
     fused_head: bool = True           # A2C: loss + head backward in one launch (round-2 head_bwd) when a2c_head is off
@@ -158,6 +160,8 @@ class TrainConfig:
                              "only the critic would decay; pick one")
         if not isinstance(self.engine_opts, EngineOpts):
             self.engine_opts = EngineOpts(**dict(self.engine_opts or {}))
+        if self.look_ahead is not None and int(self.look_ahead) < 1:
+            raise ValueError(f"TrainConfig.look_ahead={self.look_ahead}: must be >= 1 (None = the whole rollout)")
 
     def replace(self, **kw):
         return dataclasses.replace(self, **kw)

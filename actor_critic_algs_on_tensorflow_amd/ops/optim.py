@@ -315,6 +315,13 @@ def frag_order(W, K, N):
     return W.reshape(K // 16, 16, N // 32, 4, 8).permute(0, 2, 3, 1, 4).reshape(-1).to(torch.bfloat16)
 
 
+def frag_order_kc(W, K, N):
+    """bf16 copy of the row-major [K][N] weight ``W`` in 32x32x16-MFMA B-fragment order (``fc_rollout.hip``): the
+    fragment of (16-deep k block kb, 32-wide column block nb) is 1 KB contiguous, lane ``(k / 8 % 2) * 32 + n % 32``
+    holding the 8 consecutive k at ((kb * N / 32 + nb) * 64 + lane) * 8."""
+    return W.reshape(K // 16, 2, 8, N // 32, 32).permute(0, 3, 1, 4, 2).reshape(-1).to(torch.bfloat16)
+
+
 SUMSQ_PARTS = 256   # optim.hip: partial slots of the global-norm reduction = max finaliser workgroups
 
 

@@ -69,10 +69,13 @@ def nstep_returns_ref(rews, vals, dones, gamma, look_ahead):
     """PyTorch oracle. rews/dones ``[T, N]``, vals ``[T+1, N]`` -> (targets, advs) fp32 ``[T, N]``."""
     _check(rews, vals, dones)
     T, N = rews.shape
+    if int(look_ahead) < 1:
+        # L = 0 would make every target the bootstrap V(s_t) itself (advantage 0); no entry point supports it
+        raise ValueError(f"look_ahead must be >= 1, got {look_ahead}")
     r = rews.double()
     v = vals.double()
     d = dones.to(torch.bool)
-    L = max(1, min(int(look_ahead), T))
+    L = min(int(look_ahead), T)
     # every start t at once, one window offset j per pass (L passes instead of T * L): the same per-t summation
     # order and the same Python-float discount products as a per-t loop, so the values are bitwise those of it
     acc = torch.zeros(T, N, dtype=torch.float64, device=rews.device)
@@ -112,6 +115,8 @@ def gae_ref(rews, vals, dones, gamma, lam):
 def nstep_returns(rews, vals, dones, gamma=0.99, look_ahead=None):
     """L-step truncated returns with bootstrap (``look_ahead=None`` -> whole rollout, classic A2C)."""
     L = rews.shape[0] if look_ahead is None else int(look_ahead)
+    if L < 1:
+        raise ValueError(f"look_ahead must be >= 1 (or None for the whole rollout), got {look_ahead}")
     if _native.use_native(rews):
         tgt = torch.empty_like(rews, dtype=torch.float32)
         adv = torch.empty_like(tgt)

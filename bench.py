@@ -44,6 +44,8 @@ def main():
                          "late")
     ap.add_argument("--bucket-dtype", default="fp32", choices=["fp32", "bf16"],
                     help="dtype of the all-reduced gradient buckets (bf16 halves the xGMI bytes)")
+    ap.add_argument("--engine-opts", default="",
+                    help="JSON dict of EngineOpts overrides (A/B runs; the defaults are the measured fastest)")
     args = ap.parse_args()
 
     from actor_critic_algs_on_tensorflow_amd import preset
@@ -57,7 +59,8 @@ def main():
     dp = DP.DataParallel() if world > 1 else None
     cfg = preset("pong_a2c", num_envs=args.envs, device=f"cuda:{local}", outdir=None, quiet=True,
                  stdout_freq=0, save_every=0, engine=args.engine, cuda_graph=not args.no_graph,
-                 overlap=args.overlap, grad_bucket_dtype=args.bucket_dtype)
+                 overlap=args.overlap, grad_bucket_dtype=args.bucket_dtype,
+                 engine_opts=json.loads(args.engine_opts) if args.engine_opts else None)
     tr = ActorCriticTrainer(cfg, dp=dp)
     if cfg.cuda_graph:
         tr.capture(warmup=2)

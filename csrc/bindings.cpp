@@ -28,6 +28,8 @@ hipError_t aca_mlp_fwd(const aca::MlpArgs*, int, size_t, hipStream_t);
 hipError_t aca_mlp_wgrad(const aca::WgradArgs*, hipStream_t);
 hipError_t aca_ppo_head(const aca::PpoHeadArgs*, int, hipStream_t);
 int aca_ppo_head_planes(int);
+hipError_t aca_fc_rollout(const uint16_t*, int64_t, int, const uint16_t*, int, int, float*, int64_t, int, int, int*,
+                          hipStream_t);
 hipError_t aca_mlp_rollout(const aca::RolloutArgs*, size_t, hipStream_t);
 hipError_t aca_env_step_cartpole(float*, int32_t*, int64_t*, float*, float*, const int64_t*, const int32_t*,
                                  const float*, float*, float*, uint8_t*, uint8_t*, uint32_t, int, int, int, float*,
@@ -436,6 +438,23 @@ void pong_fused_env_step(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, T
                                 ptr<uint16_t>(y3), (float)scale, so, sn, tn, tgn, ern, stamps_ptr(stamps, sn ? 2 * N : N),
                                 frag ? 1 : 0, N, cur_stream(state)),
         "pong_fused_env_step");
+}
+
+// rollout fc product as split-K partial planes on the fragment-ordered Wfc copy (fc_rollout.hip); hpart holds 32
+// equal planes of [M, 512]; returns the number of planes written
+int64_t fc_rollout(Tensor X, Tensor Wf, Tensor hpart, int64_t variant) {
+  need(X, at::kBFloat16, "X");
+  need(Wf, at::kBFloat16, "Wf");
+  need(hpart, at::kFloat, "hpart");
+  TORCH_CHECK(X.dim() == 2 && X.stride(1) == 1 && X.size(1) == 3136 && X.size(0) >= 1 && X.size(0) <= 32,
+              "fc_rollout: X must be [M <= 32, 3136] row-major");
+  TORCH_CHECK(Wf.numel() == 3136 * 512 && Wf.is_contiguous(), "fc_rollout: Wf must be the [3136 x 512] fragment copy");
+  TORCH_CHECK(hpart.numel() % 32 == 0 && hpart.numel() / 32 >= X.size(0) * 512, "fc_rollout: hpart must hold 32 planes");
+  int S = 0;
+  check(aca_fc_rollout(ptr<uint16_t>(X), X.stride(0), (int)X.size(0), ptr<uint16_t>(Wf), 3136, 512, ptr<float>(hpart),
+                       hpart.numel() / 32, (int)variant, 32, &S, cur_stream(X)),
+        "fc_rollout");
+  return S;
 }
 
 // bootstrap value from the fc partial planes (cnn_fused.hip); hpart holds 32 equal planes of [N, 512]
@@ -1836,6 +1855,7 @@ TORCH_LIBRARY(acamd, m) {
         "Tensor pWh, Tensor pbh, Tensor pbfc, Tensor pstats, Tensor ticket, Tensor stats, Tensor? hp=None, "
         "int hp_planes=0, Tensor? hbias=None) -> ()");
   m.def("ppo_head_planes(int B) -> int", &ppo_head_planes);
+  m.def("fc_rollout(Tensor X, Tensor Wf, Tensor hpart, int variant) -> int");
   m.def("head_bwd(Tensor z, Tensor act, Tensor logp_old, Tensor ent_coef, Tensor kl_coef, float vf_coef, Tensor rew, "
         "Tensor val, Tensor dones, int L, int returns_mode, bool norm_adv, float gamma, float lam, Tensor ret_w, "
         "Tensor adv_w, Tensor h, Tensor Wh, Tensor dh, Tensor gWh, Tensor gbh, Tensor gbfc, Tensor stats, "
@@ -1893,6 +1913,7 @@ TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
   m.impl("gemm", &gemm);
   m.impl("cnn_trunk_fwd", &cnn_trunk_fwd);
   m.impl("fc_value", &fc_value);
+  m.impl("fc_rollout", &fc_rollout);
   m.impl("cnn_trunk_bwd", &cnn_trunk_bwd);
   m.impl("grad_finalize", &grad_finalize);
   m.impl("ppo_head", &ppo_head);

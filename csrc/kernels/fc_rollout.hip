@@ -1,0 +1,106 @@
+// Rollout fc product of the Nature-CNN (SURVEY §2.4 K01 at the headline's rollout batch): the fc layer's split-K
+// partial planes  P[s][m][n] = sum_{k in chunk s} X[m][k] * W[k][n]  for the M <= 32 envs of one rollout step
+// (X = y3 [M, 3136] bf16, W = Wfc [3136, 512]), consumed by the fused rollout step / the A2C head, which sum the
+// planes in plane order, add the bias and apply ReLU (cnn_head.h).
+//
+// Why not the general GEMM (gemm_impl.h, 5.0 us per launch at this shape): its 32 x 32 tiles stream W through LDS
+// as 64-byte row pieces (16 rows per wave instruction: ~16 B/clk/CU from L2 against 50-60 for whole-line wave loads,
+// profiles/r4_l2_stream_probe.txt) and walk 4 dependent k-steps of load -> LDS -> barrier -> transposing read ->
+// MFMA. Here W is read from a FRAGMENT-ORDERED bf16 copy kept by the optimiser step (ops/optim.py frag_order_kc):
+// the 32x32x16 MFMA's B fragment of (16-deep k block kb, 32-wide column block nb) is 1 KB contiguous --
+//     u16 index  ((kb * N/32 + nb) * 64 + (k / 8 % 2) * 32 + n % 32) * 8 + k % 8
+// -- so every operand goes global -> VGPRs in ONE round of loads (no LDS staging, no barrier before the MFMAs):
+// each wave issues its KR A fragments (16 bytes of an X row per lane) and KR B fragments (1 KB wave loads) at once,
+// runs KR MFMAs, and the W waves of a workgroup (consecutive k ranges of one 32-column block) sum their
+// accumulators through LDS in wave order into ONE plane: S = (K/16) / (KR * W) planes, fixed summation order
+// (deterministic), no atomics, no in-launch cross-workgroup hand-off.
+// Workgroup order is XCD-grouped: the 16 column blocks of a k chunk run on one XCD, so their shared X lines meet in
+// one L2; the same workgroup reads the same W fragments every launch (they stay in that XCD's L2 across steps).
+#include "common.h"
+
+namespace aca {
+
+typedef float fr_f32x16 __attribute__((ext_vector_type(16)));
+
+struct FcRolloutArgs {
+  const u16* X; int64_t ldx; int M;
+  const u16* Wf; int K, N;
+  float* P; int64_t pstride;
+};
+
+template <int KR, int W>
+__global__ void __launch_bounds__(64 * W) fc_rollout_kernel(FcRolloutArgs a) {
+  __shared__ float red[W > 1 ? W * 16 * 64 : 1];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int NB = a.N >> 5;
+  // XCD-grouped order: workgroups are dealt round-robin over the 8 XCDs; logical index L runs contiguously per XCD
+  const int G = gridDim.x, bid = blockIdx.x;
+  const int L = (G & 7) ? bid : (bid & 7) * (G >> 3) + (bid >> 3);
+  const int s = L / NB, nb = L - s * NB;
+  const int kb0 = (s * W + w) * KR;
+  const int m = min(lane & 31, a.M - 1);   // rows past M read row M - 1 (never stored)
+  const u16* xa = a.X + (int64_t)m * a.ldx + kb0 * 16 + 8 * (lane >> 5);
+  const u16* wb = a.Wf + ((int64_t)kb0 * NB + nb) * 512 + lane * 8;
+  bf16x8 af[KR], bf[KR];
+#pragma unroll
+  for (int q = 0; q < KR; ++q) {
+    af[q] = *reinterpret_cast<const bf16x8*>(xa + q * 16);
+    bf[q] = *reinterpret_cast<const bf16x8*>(wb + (int64_t)q * NB * 512);
+  }
+  fr_f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+  for (int q = 0; q < KR; ++q) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[q], bf[q], acc, 0, 0, 0);
+  float* plane = a.P + (int64_t)s * a.pstride + nb * 32 + (lane & 31);
+  const int mr = 4 * (lane >> 5);
+  if constexpr (W == 1) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = (r & 3) + 8 * (r >> 2) + mr;
+      if (row < a.M) plane[(int64_t)row * a.N] = acc[r];
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[(w * 16 + r) * 64 + lane] = acc[r];
+    __syncthreads();
+    // wave w sums accumulator rows r = w, w + W, ... over the waves in wave order (the same order for every r)
+    for (int r = w; r < 16; r += W) {
+      float v = red[r * 64 + lane];
+#pragma unroll
+      for (int ww = 1; ww < W; ++ww) v += red[(ww * 16 + r) * 64 + lane];
+      const int row = (r & 3) + 8 * (r >> 2) + mr;
+      if (row < a.M) plane[(int64_t)row * a.N] = v;
+    }
+  }
+}
+
+}  // namespace aca
+
+// variant: (KR, W) = 0: (2, 7) -> 14 planes, 1: (4, 7) -> 7 planes, 2: (1, 14) -> 14 planes, 3: (7, 4) -> 7 planes,
+// 4: (7, 2) -> 14 planes, 5: (2, 14) -> 7 planes, 6: (1, 7) -> 28 planes. Returns the plane count through *S_out.
+extern "C" hipError_t aca_fc_rollout(const uint16_t* X, int64_t ldx, int M, const uint16_t* Wf, int K, int N,
+                                     float* P, int64_t pstride, int variant, int max_planes, int* S_out,
+                                     hipStream_t stream) {
+  static const int cfg[7][2] = {{2, 7}, {4, 7}, {1, 14}, {7, 4}, {7, 2}, {2, 14}, {1, 7}};
+  if (variant < 0 || variant > 6 || M < 1 || M > 32 || K % 16 || N % 32 || ldx % 8 ||
+      reinterpret_cast<uintptr_t>(X) % 16 || reinterpret_cast<uintptr_t>(Wf) % 16 || (N >> 5) % 8)
+    return hipErrorInvalidValue;
+  const int kr = cfg[variant][0], w = cfg[variant][1];
+  const int KB = K / 16;
+  if (KB % (kr * w)) return hipErrorInvalidValue;
+  const int S = KB / (kr * w);
+  if (S > max_planes || pstride < (int64_t)M * N) return hipErrorInvalidValue;
+  if (S_out) *S_out = S;
+  aca::FcRolloutArgs a{reinterpret_cast<const aca::u16*>(X), ldx, M, reinterpret_cast<const aca::u16*>(Wf), K, N, P,
+                       pstride};
+  const int grid = S * (N >> 5);
+  switch (variant) {
+#define ACA_FR_CASE(v, KR, W) \
+  case v: aca::fc_rollout_kernel<KR, W><<<grid, 64 * W, 0, stream>>>(a); break;
+    ACA_FR_CASE(0, 2, 7) ACA_FR_CASE(1, 4, 7) ACA_FR_CASE(2, 1, 14) ACA_FR_CASE(3, 7, 4) ACA_FR_CASE(4, 7, 2)
+    ACA_FR_CASE(5, 2, 14) ACA_FR_CASE(6, 1, 7)
+#undef ACA_FR_CASE
+  }
+  return hipGetLastError();
+}

@@ -11,7 +11,7 @@ KL-adaptive lr in [1e-6, 0.1] and the log10 gamma / beta schedules (``process.py
 (eps 1e-8 outside the bias correction). ``--separate-local-init``: the first rollout uses a second random init as
 the reference's unsynced local actor does (``process.py:205-207``).
 
-    python scripts/exp/a3c_oracle.py --updates 300 --desired-kl 2e-3 [--seed 0]
+    python tests/oracles/a3c_oracle.py --updates 300 --desired-kl 2e-3 [--seed 0]
 """
 import argparse
 import json

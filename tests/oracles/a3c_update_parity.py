@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
-"""One reference A3C update, this framework vs the independent oracle (scripts/exp/a3c_oracle.py), from the SAME
+"""One reference A3C update, this framework vs the independent oracle (tests/oracles/a3c_oracle.py), from the SAME
 parameters on the SAME batch: targets, normalised advantages, post-update actor / critic parameters, KL proxy and
 the adaptive lr. Prints the largest differences. CPU.
 
-    python scripts/exp/a3c_update_parity.py [--updates 3]
+    python tests/oracles/a3c_update_parity.py [--updates 3]
 """
 import argparse
 import math

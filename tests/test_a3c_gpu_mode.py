@@ -174,6 +174,35 @@ def test_a3c_gpu_mode_worker_death_aborts_cleanly_cpu(tmp_path):
     assert "error" in w0 or w0["global_step"] >= 40
 
 
+@pytest.mark.parametrize("where", ["push", "reply"])
+def test_a3c_gpu_mode_worker_death_mid_exchange_cpu(tmp_path, where):
+    """a worker that dies INSIDE an exchange -- after its push header but before the payload ("push"),
+    or after the push while the PS is about to reply ("reply") -- ends the PS with status "aborted" (its payload
+    receive / reply send fails), never with an exception escaping serve() and never with a hang. One worker, no
+    staleness bound: the PS's next peer I/O is with the dead worker."""
+    import multiprocessing
+    from actor_critic_algs_on_tensorflow_amd.algos.trainer import FAULT_EXIT_CODE
+    ctx = multiprocessing.get_context("spawn")
+    port = _free_port()
+    args = (2, port, str(tmp_path), "cpu", 40, 1, -1, dict(fault_inject=f"1:2:{where}", dist_timeout_s=30))
+    procs = [ctx.Process(target=_proc, args=(r,) + args) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(150)
+    alive = [p.is_alive() for p in procs]
+    for p in procs:   # the exact child objects, never a pattern
+        if p.is_alive():
+            p.kill()
+    assert not any(alive), "a process of the job hung after a worker died mid-exchange"
+    assert procs[1].exitcode == FAULT_EXIT_CODE
+    assert procs[0].exitcode == 0, "the PS must end cleanly (no escaped exception)"
+    ps = torch.load(tmp_path / "r0.pt", weights_only=False)
+    assert ps["role"] == "ps" and ps["status"] == "aborted", ps.get("status")
+    # iterations 0, 1 applied; "reply": iteration 2's payload arrived and was applied before the reply failed
+    assert ps["n_applies"][1] == (3 if where == "reply" else 2), ps["n_applies"]
+
+
 def _pf_proc(rank, port, d):
     from actor_critic_algs_on_tensorflow_amd.compat import reference as ref
     cluster = {"ps": [f"localhost:{port}"], "worker": [f"localhost:{port + 1}", f"localhost:{port + 2}"]}

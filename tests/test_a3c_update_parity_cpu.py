@@ -1,5 +1,5 @@
 """The reference A3C worker update (A3C/process.py:217-278, A3C/policies.py:34-104) in this framework vs an
-independent plain-PyTorch oracle (scripts/exp/a3c_oracle.py, written from the reference's equations with no code from
+independent plain-PyTorch oracle (tests/oracles/a3c_oracle.py, written from the reference's equations with no code from
 this package), from the same parameters on the same 1200-step Pendulum batch: PathAdv targets, the actor gradient
 (policy gradient + beta KL + gamma entropy, value-clipped), TF-Adam parameters, the KL proxy and the adaptive lr."""
 import os
@@ -7,7 +7,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "scripts", "exp"))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "oracles"))
 
 
 def test_a3c_update_matches_independent_oracle():

@@ -109,6 +109,11 @@ class CNNEngine:
         # narrow workgroups (off: fc_value + the 8-workgroup head_bwd kernel of round 2)
         self.a2c_head = o.a2c_head
         self._a2c_bar = None
+        # A2C head v3 (loss.hip a2c_head_env_kernel): one workgroup per env, no grid-wide hand-off; the head's weight /
+        # bias gradients as per-env planes and the statistics as per-env rows, both reduced by the finaliser
+        self.a2c_head_env = o.a2c_head_env
+        self._ae = {}
+        self._stats_duty = None
         # A2C learner on ONE stream with grouped GEMM launches instead of a side stream joined by events
         self.grouped = o.grouped
         # conv weight gradients as split-K partial planes reduced in plane order by the finaliser (deterministic);
@@ -476,12 +481,40 @@ class CNNEngine:
         return (self.fused_head and 2 <= self.A <= 7 and 1 <= B <= self.HB_MAXB and 1 <= N <= self.HB_MAXN
                 and B % N == 0)
 
-    def head_backward(self, b: _Bufs, actions, logp_old, ent_coef, kl_coef, vf_coef, stats, returns, boot=None):
+    def head_env_ok(self, T, N, norm_adv):
+        """The per-env A2C head (``a2c_head_env``) applies: no advantage normalisation (no batch-wide moments), at
+        most 64 rollout steps."""
+        return (self.a2c_head_env and self.a2c_head and not norm_adv and 1 <= T <= 64 and 2 <= self.A <= 7
+                and self.grouped and self.fused_bwd and self.det_wgrad)   # the grouped backward's finaliser sums them
+
+    def head_backward(self, b: _Bufs, actions, logp_old, ent_coef, kl_coef, vf_coef, stats, returns, boot=None,
+                      planes_ok=False):
         """A2C fast path: ``a2c_head`` (or round 2's ``head_bwd``) -- returns/EV/adv-norm + loss + dz and the head's
         backward (dh, dWh, dbh, dbfc) in one launch; :meth:`backward` then starts at the fc layer (``head_done=True``).
         ``boot`` = (fc partial planes, count) of the bootstrap observation: V(s_T) is computed in the same launch and
         written into ``returns["val"][T]`` (the rollout then skips its ``fc_value`` launch)."""
         r = returns
+        T, N = r["rew"].shape
+        if planes_ok and self.head_env_ok(T, N, r["norm_adv"]):
+            # the head's gradients stay per-env planes until THIS backward's finaliser (planes_ok: the caller runs the
+            # whole backward with its finaliser before anything reads the fc/head gradients)
+            ae = self._ae.get(N)
+            if ae is None:
+                dev, A1 = self.dev, self.A1
+                ae = dict(Wh=torch.zeros(N * 512 * A1, device=dev), bfc=torch.zeros(N * 512, device=dev),
+                          bh=torch.zeros(N * A1, device=dev), st=torch.zeros(N, 10, dtype=torch.float64, device=dev))
+                self._ae[N] = ae
+            hp, S = boot if boot is not None else (None, 0)
+            _native.require().a2c_head_env(b.z, actions, logp_old, ent_coef, kl_coef, float(vf_coef), r["rew"],
+                                           r["val"], r["dones"], int(r["L"]), int(r["mode"]), float(r["gamma"]),
+                                           float(r["lam"]), r["ret_w"], r["adv_w"], b.h, self.sWh, b.dh, hp, int(S),
+                                           self.bfc if hp is not None else None, self.bh if hp is not None else None,
+                                           ae["Wh"], ae["bfc"], ae["bh"], ae["st"])
+            for name in ("Wh", "bh", "bfc"):
+                self._planes["ae_" + name] = ae[name]
+            self._head_planes = {"ae_Wh": N, "ae_bh": N, "ae_bfc": N}
+            self._stats_duty = (ae["st"], T * N, ent_coef, kl_coef, stats)
+            return stats
         if self.a2c_head:
             if self._a2c_bar is None:
                 self._a2c_bar = torch.zeros(4, dtype=torch.int32, device=self.dev)
@@ -662,7 +695,8 @@ class CNNEngine:
                           self.gb1.data_ptr(): (bp + 128 * 4, 160, b.B)}
             for name, S in planes:
                 g = {"W1": self.gW1, "W2": self.gW2, "W3": self.gW3, "Wh": self.gWh, "ph_Wh": self.gWh,
-                     "ph_bh": self.gbh, "ph_bfc": self.gbfc, "Wfc": self.gWfc}[name]
+                     "ph_bh": self.gbh, "ph_bfc": self.gbfc, "Wfc": self.gWfc, "ae_Wh": self.gWh,
+                     "ae_bh": self.gbh, "ae_bfc": self.gbfc}[name]
                 src_of[g.data_ptr()] = (self._planes[name].data_ptr(), g.numel(), S)
             for p, off in zip(flat.params, flat.offsets):
                 g = flat.grad[off:off + p.numel()]
@@ -674,7 +708,12 @@ class CNNEngine:
             from ..ops.optim import finalize_jobs
             words = finalize_jobs(segs, self.dev, return_max=True)
             self._fin_words[key] = words
-        _native.require().grad_finalize(words[0], self.fin_parts)
+        sd, self._stats_duty = self._stats_duty, None
+        if sd is not None:   # the per-env head's statistics rows -> stats[0..7] (one extra finaliser workgroup)
+            spart, B, ent, kl, stats = sd
+            _native.require().grad_finalize(words[0], self.fin_parts, spart, B, ent, kl, stats)
+        else:
+            _native.require().grad_finalize(words[0], self.fin_parts)
 
     @staticmethod
     def dcol3(b):   # only the col2im data-gradient path materialises the column gradients

@@ -819,7 +819,12 @@ class ActorCriticTrainer:
         if head_done:
             # loss + dz + the head's backward (dh, dWh, dbh, dbfc) in one launch
             boot, self._boot = getattr(self, "_boot", None), None
-            eng.head_backward(b, actions, logp_old, self.ent_coef, self.kl_coef, vf, self.stats_buf, rets, boot=boot)
+            # the per-env head's gradient planes are summed by this backward's finaliser (DP: the fc/head bucket must
+            # be final before the conv backward's all-reduce split, and eager / segmented DP schedules stay on one
+            # kernel so they remain bitwise comparable)
+            planes_ok = self._bw_stage == "all" and self.dp is None
+            eng.head_backward(b, actions, logp_old, self.ent_coef, self.kl_coef, vf, self.stats_buf, rets, boot=boot,
+                              planes_ok=planes_ok)
         else:
             eng.loss(b, actions, logp_old, None, None, None, self.ent_coef, self.kl_coef, vf, 0.0, 0.0,
                      stats=self.stats_buf, returns=rets)

@@ -29,6 +29,8 @@ class EngineOpts:
                                       # variant 0..6; -1: the general GEMM on the row-major shadow)
     # -- learner -------------------------------------------------------------------------------------------------
     a2c_head: bool = True             # A2C: V(s_T) + returns + loss + head backward in one launch (loss.hip a2c_head)
+    a2c_head_env: bool = True         # ... as one workgroup per env without a grid-wide hand-off (A2C without
+                                      # advantage normalisation; head gradients as per-env planes the finaliser sums)
     fused_head: bool = True           # A2C: loss + head backward in one launch (round-2 head_bwd) when a2c_head is off
     grouped: bool = True              # independent backward products as ONE grouped GEMM launch (no side stream)
     det_wgrad: bool = True            # weight gradients as split-K planes reduced in fixed order (bitwise determinism)

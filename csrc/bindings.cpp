@@ -29,7 +29,7 @@ hipError_t aca_mlp_wgrad(const aca::WgradArgs*, hipStream_t);
 hipError_t aca_ppo_head(const aca::PpoHeadArgs*, int, hipStream_t);
 int aca_ppo_head_planes(int);
 hipError_t aca_fc_rollout(const uint16_t*, int64_t, int, const uint16_t*, int, int, float*, int64_t, int, int, int*,
-                          hipStream_t);
+                          unsigned long long*, hipStream_t);
 hipError_t aca_mlp_rollout(const aca::RolloutArgs*, size_t, hipStream_t);
 hipError_t aca_env_step_cartpole(float*, int32_t*, int64_t*, float*, float*, const int64_t*, const int32_t*,
                                  const float*, float*, float*, uint8_t*, uint8_t*, uint32_t, int, int, int, float*,
@@ -117,7 +117,12 @@ hipError_t aca_cnn_trunk_fwd(const uint8_t*, const uint16_t*, const float*, cons
 hipError_t aca_cnn_trunk_fwd_s16(const uint8_t*, const uint16_t*, const float*, const uint16_t*, const float*,
                                  const uint16_t*, const float*, uint16_t*, uint16_t*, uint16_t*, int, float, uint8_t*,
                                  const int64_t*, int, hipStream_t);
-hipError_t aca_grad_finalize(const int64_t*, int, float*, hipStream_t);
+hipError_t aca_grad_finalize(const int64_t*, int, float*, const double*, int, int, const float*, const float*, float*,
+                             hipStream_t);
+hipError_t aca_a2c_head_env(const float*, const int32_t*, const float*, const float*, const float*, float,
+                            const float*, float*, const uint8_t*, int, int, int, int, float, float, float*, float*,
+                            const uint16_t*, const uint16_t*, uint16_t*, int, const float*, int, int64_t,
+                            const float*, const float*, float*, float*, float*, double*, hipStream_t);
 hipError_t aca_head_bwd(const float*, const int32_t*, const float*, const float*, const float*, float, const float*,
                         const float*, const uint8_t*, int, int, int, int, int, float, float, float*, float*,
                         const uint16_t*, const uint16_t*, uint16_t*, float*, float*, float*, float*, int,
@@ -442,7 +447,7 @@ void pong_fused_env_step(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, T
 
 // rollout fc product as split-K partial planes on the fragment-ordered Wfc copy (fc_rollout.hip); hpart holds 32
 // equal planes of [M, 512]; returns the number of planes written
-int64_t fc_rollout(Tensor X, Tensor Wf, Tensor hpart, int64_t variant) {
+int64_t fc_rollout(Tensor X, Tensor Wf, Tensor hpart, int64_t variant, c10::optional<Tensor> stamps) {
   need(X, at::kBFloat16, "X");
   need(Wf, at::kBFloat16, "Wf");
   need(hpart, at::kFloat, "hpart");
@@ -452,7 +457,8 @@ int64_t fc_rollout(Tensor X, Tensor Wf, Tensor hpart, int64_t variant) {
   TORCH_CHECK(hpart.numel() % 32 == 0 && hpart.numel() / 32 >= X.size(0) * 512, "fc_rollout: hpart must hold 32 planes");
   int S = 0;
   check(aca_fc_rollout(ptr<uint16_t>(X), X.stride(0), (int)X.size(0), ptr<uint16_t>(Wf), 3136, 512, ptr<float>(hpart),
-                       hpart.numel() / 32, (int)variant, 32, &S, cur_stream(X)),
+                       hpart.numel() / 32, (int)variant, 32, &S,
+                       reinterpret_cast<unsigned long long*>(stamps_ptr(stamps, 1)), cur_stream(X)),
         "fc_rollout");
   return S;
 }
@@ -1535,14 +1541,82 @@ void cnn_trunk_bwd(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tenso
 // Gradient finaliser (optim.hip grad_finalize_kernel): jobs = device int64 [njobs, 8] (dst, src, n, stride, S,
 // vec, 0, 0) built by ops/optim.py finalize_jobs; writes dst = sum of S planes where src != 0 and the
 // SUMSQ_PARTS sum-of-squares partials.
-void grad_finalize(Tensor jobs, Tensor partial) {
+// Optional statistics duty (one extra workgroup): spart [N, 10] fp64 per-env A2C statistics rows (a2c_head_env)
+// combined into stats[0..7] over B = T * N rows.
+void grad_finalize(Tensor jobs, Tensor partial, c10::optional<Tensor> spart, int64_t B, c10::optional<Tensor> ent_coef,
+                   c10::optional<Tensor> kl_coef, c10::optional<Tensor> stats) {
   need(jobs, at::kLong, "jobs");
   TORCH_CHECK(jobs.dim() == 2 && jobs.size(1) == 8 && jobs.is_contiguous(), "grad_finalize: jobs must be [njobs, 8]");
   need(partial, at::kFloat, "partial");
   TORCH_CHECK(partial.numel() >= aca_sumsq_parts() && jobs.size(0) <= aca_sumsq_parts(),
               "grad_finalize: partial too small / too many jobs");
-  check(aca_grad_finalize(jobs.data_ptr<int64_t>(), (int)jobs.size(0), ptr<float>(partial), cur_stream(partial)),
+  const double* sp = nullptr;
+  int sN = 0;
+  if (spart.has_value() && spart->defined()) {
+    need(*spart, at::kDouble, "spart");
+    TORCH_CHECK(spart->dim() == 2 && spart->size(1) == 10 && B >= 1 && ent_coef.has_value() && kl_coef.has_value() &&
+                    stats.has_value() && stats->numel() >= 8,
+                "grad_finalize: statistics duty needs spart [N, 10], B, ent_coef, kl_coef and stats[8]");
+    need(*ent_coef, at::kFloat, "ent_coef");
+    need(*kl_coef, at::kFloat, "kl_coef");
+    need(*stats, at::kFloat, "stats");
+    sp = spart->data_ptr<double>();
+    sN = (int)spart->size(0);
+  }
+  check(aca_grad_finalize(jobs.data_ptr<int64_t>(), (int)jobs.size(0), ptr<float>(partial), sp, sN, (int)B,
+                          optr<float>(ent_coef), optr<float>(kl_coef), optr<float>(stats), cur_stream(partial)),
         "grad_finalize");
+}
+
+// A2C learner head, one workgroup per env (loss.hip a2c_head_env_kernel; A2C without advantage normalisation): the
+// bootstrap value V(s_T) from the rollout's last fc planes (written into val[T]), returns, loss, dz, dh, and per-env
+// partial planes of dWh [N, 512 * A1], dbfc [N, 512], dbh [N, A1] + statistics rows spart [N, 10] (reduced by the
+// gradient finaliser).
+void a2c_head_env(Tensor z, Tensor act, Tensor logp_old, Tensor ent_coef, Tensor kl_coef, double vf_coef, Tensor rew,
+                  Tensor val, Tensor dones, int64_t L, int64_t returns_mode, double gamma, double lam, Tensor ret_w,
+                  Tensor adv_w, Tensor h, Tensor Wh, Tensor dh, c10::optional<Tensor> hpart, int64_t S,
+                  c10::optional<Tensor> bfc, c10::optional<Tensor> bh, Tensor pWh, Tensor pbfc, Tensor pbh,
+                  Tensor spart) {
+  TORCH_CHECK(rew.dim() == 2, "a2c_head_env: rewards must be [T, N]");
+  const int T = rew.size(0), N = rew.size(1), B = T * N;
+  TORCH_CHECK(z.dim() == 2 && z.size(0) >= B, "a2c_head_env: z must be [B, A + 1]");
+  const int A = z.size(1) - 1, A1 = A + 1;
+  need(z, at::kFloat, "z");
+  need(act, at::kInt, "act");
+  need(dones, at::kByte, "dones");
+  for (auto* t : {&logp_old, &ent_coef, &kl_coef, &rew, &val, &ret_w, &adv_w, &pWh, &pbfc, &pbh})
+    need(*t, at::kFloat, "a2c_head_env fp32 operand");
+  need(spart, at::kDouble, "spart");
+  for (auto* t : {&h, &Wh, &dh}) need(*t, at::kBFloat16, "a2c_head_env bf16 operand");
+  TORCH_CHECK(z.is_contiguous() && z.stride(0) == A1, "a2c_head_env: z must be contiguous [B, A + 1]");
+  TORCH_CHECK(act.numel() >= B && logp_old.numel() >= B && val.numel() >= (int64_t)(T + 1) * N &&
+                  dones.numel() >= B && ret_w.numel() >= B && adv_w.numel() >= B && h.numel() >= (int64_t)B * 512 &&
+                  dh.numel() >= (int64_t)B * 512 && Wh.numel() == 512 * A1,
+              "a2c_head_env: shape mismatch");
+  TORCH_CHECK(pWh.numel() >= (int64_t)N * 512 * A1 && pbfc.numel() >= (int64_t)N * 512 && pbh.numel() >= (int64_t)N * A1 &&
+                  spart.numel() >= (int64_t)N * 10,
+              "a2c_head_env: partial planes too small");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(pbfc.data_ptr()) % 8 == 0, "a2c_head_env: pbfc must be 8-byte aligned");
+  const float* hp = nullptr;
+  int64_t pstride = 0;
+  if (hpart.has_value() && hpart->defined()) {
+    need(*hpart, at::kFloat, "hpart");
+    TORCH_CHECK(bfc.has_value() && bh.has_value(), "a2c_head_env: hpart needs bfc and bh");
+    need(*bfc, at::kFloat, "bfc");
+    need(*bh, at::kFloat, "bh");
+    pstride = hpart->numel() / 32;
+    TORCH_CHECK(hpart->numel() % 32 == 0 && pstride >= (int64_t)N * 512 && S >= 1 && S <= 32,
+                "a2c_head_env: hpart must hold 32 planes of [N, 512]");
+    TORCH_CHECK(bfc->numel() == 512 && bh->numel() == A1, "a2c_head_env: bad bootstrap operands");
+    hp = ptr<float>(*hpart);
+  }
+  check(aca_a2c_head_env(ptr<float>(z), ptr<int32_t>(act), ptr<float>(logp_old), ptr<float>(ent_coef),
+                         ptr<float>(kl_coef), (float)vf_coef, ptr<float>(rew), ptr<float>(val), ptr<uint8_t>(dones), T,
+                         N, (int)L, (int)returns_mode, (float)gamma, (float)lam, ptr<float>(ret_w), ptr<float>(adv_w),
+                         ptr<uint16_t>(h), ptr<uint16_t>(Wh), ptr<uint16_t>(dh), A, hp, (int)S, pstride,
+                         optr<float>(bfc), optr<float>(bh), ptr<float>(pWh), ptr<float>(pbfc), ptr<float>(pbh),
+                         spart.data_ptr<double>(), cur_stream(z)),
+        "a2c_head_env");
 }
 
 // A2C learner head in one launch (loss.hip head_bwd_kernel): returns + EV + advantage normalisation + loss + dz,
@@ -1849,13 +1923,18 @@ TORCH_LIBRARY(acamd, m) {
         "Tensor? copy_out=None, Tensor? obs_idx=None) -> ()");
   m.def("cnn_trunk_bwd(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tensor dy2, Tensor dy1, "
         "Tensor biasp, Tensor? stamps=None, int persist=0) -> ()");
-  m.def("grad_finalize(Tensor jobs, Tensor partial) -> ()");
+  m.def("grad_finalize(Tensor jobs, Tensor partial, Tensor? spart=None, int B=0, Tensor? ent_coef=None, "
+        "Tensor? kl_coef=None, Tensor? stats=None) -> ()");
+  m.def("a2c_head_env(Tensor z, Tensor act, Tensor logp_old, Tensor ent_coef, Tensor kl_coef, float vf_coef, "
+        "Tensor rew, Tensor val, Tensor dones, int L, int returns_mode, float gamma, float lam, Tensor ret_w, "
+        "Tensor adv_w, Tensor h, Tensor Wh, Tensor dh, Tensor? hpart, int S, Tensor? bfc, Tensor? bh, Tensor pWh, "
+        "Tensor pbfc, Tensor pbh, Tensor spart) -> ()");
   m.def("ppo_head(Tensor h, Tensor Wh, Tensor bh, Tensor act, Tensor logp_old, Tensor adv, Tensor ret, Tensor? v_old, "
         "Tensor ent_coef, Tensor kl_coef, float vf_coef, float ppo_clip, float v_clip, Tensor dh, Tensor? z_out, "
         "Tensor pWh, Tensor pbh, Tensor pbfc, Tensor pstats, Tensor ticket, Tensor stats, Tensor? hp=None, "
         "int hp_planes=0, Tensor? hbias=None) -> ()");
   m.def("ppo_head_planes(int B) -> int", &ppo_head_planes);
-  m.def("fc_rollout(Tensor X, Tensor Wf, Tensor hpart, int variant) -> int");
+  m.def("fc_rollout(Tensor X, Tensor Wf, Tensor hpart, int variant, Tensor? stamps=None) -> int");
   m.def("head_bwd(Tensor z, Tensor act, Tensor logp_old, Tensor ent_coef, Tensor kl_coef, float vf_coef, Tensor rew, "
         "Tensor val, Tensor dones, int L, int returns_mode, bool norm_adv, float gamma, float lam, Tensor ret_w, "
         "Tensor adv_w, Tensor h, Tensor Wh, Tensor dh, Tensor gWh, Tensor gbh, Tensor gbfc, Tensor stats, "
@@ -1916,6 +1995,7 @@ TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
   m.impl("fc_rollout", &fc_rollout);
   m.impl("cnn_trunk_bwd", &cnn_trunk_bwd);
   m.impl("grad_finalize", &grad_finalize);
+  m.impl("a2c_head_env", &a2c_head_env);
   m.impl("ppo_head", &ppo_head);
   m.impl("gemm_big", &gemm_big);
   m.impl("pong_fused_env_step", &pong_fused_env_step);

@@ -15,6 +15,10 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef unsigned short u16;
 
+// per-env A2C statistics row (loss.hip a2c_head_env_kernel -> optim.hip a2c_stats_duty):
+// [pg, kl, entropy, value loss, R, R^2, V, V^2, R V, unused] as fp64 sums over the env's rows
+constexpr int A2C_STATS = 10;
+
 // ------------------------------------------------------------------------------------------------------------
 // Counter-based RNG. Bit-identical to actor_critic_algs_on_tensorflow_amd/envs/rng.py (lowbias32 finaliser).
 // ------------------------------------------------------------------------------------------------------------

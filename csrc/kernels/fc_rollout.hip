@@ -26,12 +26,15 @@ struct FcRolloutArgs {
   const u16* X; int64_t ldx; int M;
   const u16* Wf; int K, N;
   float* P; int64_t pstride;
+  unsigned long long* stamps;   // diagnostics: per wave [entry, operands landed, MFMAs done, stores drained]
 };
 
 template <int KR, int W>
 __global__ void __launch_bounds__(64 * W) fc_rollout_kernel(FcRolloutArgs a) {
   __shared__ float red[W > 1 ? W * 16 * 64 : 1];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  unsigned long long* st = a.stamps ? a.stamps + ((size_t)blockIdx.x * W + w) * 4 : nullptr;
+  if (st && lane == 0) st[0] = __builtin_amdgcn_s_memrealtime();
   const int NB = a.N >> 5;
   // XCD-grouped order: workgroups are dealt round-robin over the 8 XCDs; logical index L runs contiguously per XCD
   const int G = gridDim.x, bid = blockIdx.x;
@@ -50,8 +53,13 @@ __global__ void __launch_bounds__(64 * W) fc_rollout_kernel(FcRolloutArgs a) {
   fr_f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  if (st) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) st[1] = __builtin_amdgcn_s_memrealtime();
+  }
 #pragma unroll
   for (int q = 0; q < KR; ++q) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[q], bf[q], acc, 0, 0, 0);
+  if (st && lane == 0) st[2] = __builtin_amdgcn_s_memrealtime() + (unsigned long long)(acc[0] != acc[0]);
   float* plane = a.P + (int64_t)s * a.pstride + nb * 32 + (lane & 31);
   const int mr = 4 * (lane >> 5);
   if constexpr (W == 1) {
@@ -73,6 +81,10 @@ __global__ void __launch_bounds__(64 * W) fc_rollout_kernel(FcRolloutArgs a) {
       if (row < a.M) plane[(int64_t)row * a.N] = v;
     }
   }
+  if (st) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) st[3] = __builtin_amdgcn_s_memrealtime();
+  }
 }
 
 }  // namespace aca
@@ -81,7 +93,7 @@ __global__ void __launch_bounds__(64 * W) fc_rollout_kernel(FcRolloutArgs a) {
 // 4: (7, 2) -> 14 planes, 5: (2, 14) -> 7 planes, 6: (1, 7) -> 28 planes. Returns the plane count through *S_out.
 extern "C" hipError_t aca_fc_rollout(const uint16_t* X, int64_t ldx, int M, const uint16_t* Wf, int K, int N,
                                      float* P, int64_t pstride, int variant, int max_planes, int* S_out,
-                                     hipStream_t stream) {
+                                     unsigned long long* stamps, hipStream_t stream) {
   static const int cfg[7][2] = {{2, 7}, {4, 7}, {1, 14}, {7, 4}, {7, 2}, {2, 14}, {1, 7}};
   if (variant < 0 || variant > 6 || M < 1 || M > 32 || K % 16 || N % 32 || ldx % 8 ||
       reinterpret_cast<uintptr_t>(X) % 16 || reinterpret_cast<uintptr_t>(Wf) % 16 || (N >> 5) % 8)
@@ -93,7 +105,7 @@ extern "C" hipError_t aca_fc_rollout(const uint16_t* X, int64_t ldx, int M, cons
   if (S > max_planes || pstride < (int64_t)M * N) return hipErrorInvalidValue;
   if (S_out) *S_out = S;
   aca::FcRolloutArgs a{reinterpret_cast<const aca::u16*>(X), ldx, M, reinterpret_cast<const aca::u16*>(Wf), K, N, P,
-                       pstride};
+                       pstride, stamps};
   const int grid = S * (N >> 5);
   switch (variant) {
 #define ACA_FR_CASE(v, KR, W) \

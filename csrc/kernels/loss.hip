@@ -922,6 +922,209 @@ __global__ void __launch_bounds__(AH_THREADS) a2c_head_kernel(A2cHeadArgs args) 
   }
 }
 
+// ------------------------------------------------------------------------------------------------------------
+// A2C learner head v3, one workgroup PER ENV, no grid-wide hand-off (A2C without advantage normalisation -- the
+// headline pong_a2c config --: every quantity of env e's rows depends only on env e). Workgroup e:
+//   * V(s_T, e) straight from the rollout's last fc partial planes (fc_h2_from_parts: the rollout step's plane order
+//     and bf16 rounding of h), dot with the value column of Wh reduced in a fixed order, stored into val[T][e];
+//   * the returns / advantages of its T rows (n-step or GAE), loss + dz (bf16-rounded like the GEMM path);
+//   * the head backward of its rows: dh = (h > 0) * dz Wh^T (stored), and PER-ENV PARTIAL PLANES of dWh = h^T dz,
+//     dbfc = colsum(dh) and dbh = colsum(dz): plane e of [N, 512 * A1] / [N, 512] / [N, A1], summed in plane order by
+//     the gradient finaliser (engine._head_planes -> finalize jobs), as the large-batch ppo_head's planes are;
+//   * its share of the statistics as one fp64 row [pg, kl, H, vl, R, R^2, V, V^2, R V] of `spart`, combined by the
+//     finaliser's statistics duty (a2c_stats_duty) into stats[0..7].
+// Replaces a2c_head's 32-workgroup grid barrier (the bootstrap values handed over with sc1 stores + a spinning
+// counter: ~4.5 us of its ~15) and its per-column layout (which needed every V(s_T) in every workgroup).
+// thread t: hidden units 2t, 2t + 1.
+// ------------------------------------------------------------------------------------------------------------
+constexpr int AE_THREADS = 256;
+constexpr int AE_MAXT = 64;
+
+struct A2cEnvArgs {
+  HeadBwdArgs h;
+  const float* hpart; int S; int64_t plane_stride;   // last fc product of s_T (split-K planes), or null: val[T] holds V
+  const float* bfc; const float* bh;
+  float* pWh; float* pbfc; float* pbh;               // planes [N][512 * A1], [N][512], [N][A1]
+  double* spart;                                     // [N][A2C_STATS] statistics rows
+};
+
+template <int AC>
+__global__ void __launch_bounds__(AE_THREADS) a2c_head_env_kernel(A2cEnvArgs args) {
+  constexpr int A1 = AC + 1;
+  const HeadBwdArgs& a = args.h;
+  __shared__ float s_dz[AE_MAXT * A1];
+  __shared__ float s_rew[AE_MAXT], s_val[AE_MAXT + 1];
+  __shared__ uint8_t s_dn[AE_MAXT];
+  __shared__ float s_vw[4];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int e = blockIdx.x, N = a.N, T = a.T;
+  // ---- loads: the bootstrap planes first (the longest chain), then everything else of this env
+  FcH2<16> fh;
+  if (args.hpart) fh.issue(args.hpart, args.S, args.plane_stride, args.bfc, e, tid);
+  float w2[2][A1];
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int q = 0; q < A1; ++q) w2[c][q] = bf2f(a.Wh[(2 * tid + c) * A1 + q]);
+  if (tid < T) {
+    const int i = tid * N + e;
+    s_rew[tid] = a.rew[i];
+    s_dn[tid] = a.dn[i];
+    s_val[tid] = a.val[i];
+  }
+  float zr[A1];
+  int ab = 0;
+  float lpo = 0.f;
+  if (tid < T) {
+    const int64_t row = (int64_t)tid * N + e;
+#pragma unroll
+    for (int j = 0; j < A1; ++j) zr[j] = a.z[row * A1 + j];
+    ab = a.act[row];
+    lpo = a.logp_old[row];
+  }
+  // this thread's two hidden units (bf16 pair) of rows 0..7, requested before the bootstrap wait (later rows: in
+  // the backward loop, 8 at a time)
+  constexpr int HR = 8;
+  uint32_t hr[HR];
+#pragma unroll
+  for (int r = 0; r < HR; ++r)
+    hr[r] = r < T ? reinterpret_cast<const uint32_t*>(a.h + ((int64_t)r * N + e) * HB_H)[tid] : 0u;
+  const float c_ent = *a.ent_coef, beta = *a.kl_coef;
+  // ---- bootstrap value V(s_T, e): fixed order (xor tree per wave, waves in order)
+  if (args.hpart) {
+    float hv[2];
+    fh.finish(args.hpart, args.S, args.plane_stride, e, tid, nullptr, hv);
+    const float part = wave_sum(hv[0] * w2[0][AC] + hv[1] * w2[1][AC]);
+    if (lane == 0) s_vw[wv] = part;
+    __syncthreads();
+    const float vT = ((s_vw[0] + s_vw[1]) + (s_vw[2] + s_vw[3])) + args.bh[AC];
+    if (tid == 0) {
+      s_val[T] = vT;
+      const_cast<float*>(a.val)[(int64_t)T * N + e] = vT;
+    }
+  } else if (tid == 0) {
+    s_val[T] = a.val[(int64_t)T * N + e];
+  }
+  __syncthreads();
+  // ---- returns, loss, dz of row t (thread t < T), statistics row
+  double st[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  if (tid < T) {
+    const int t = tid;
+    float R;
+    if (a.returns_mode == 1) {
+      const int hh = min(t + a.L, T);
+      float acc = 0.f, disc = 1.f;
+      bool alive = true;
+      for (int q = t; q < hh; ++q) {
+        acc += disc * s_rew[q];
+        disc *= a.gamma;
+        if (s_dn[q]) { alive = false; break; }
+      }
+      if (alive) acc += disc * s_val[hh];
+      R = acc;
+    } else {
+      float last = 0.f;
+      for (int q = T - 1; q >= t; --q) {
+        const float nd = s_dn[q] ? 0.f : 1.f;
+        const float delta = s_rew[q] + a.gamma * s_val[q + 1] * nd - s_val[q];
+        last = delta + a.gamma * a.lam * nd * last;
+      }
+      R = last + s_val[t];
+    }
+    const float v = s_val[t], adv = R - v;
+    const int64_t row = (int64_t)t * N + e;
+    a.ret_w[row] = R;
+    a.adv_w[row] = adv;
+    const float invB = 1.0f / (float)a.B;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < AC; ++j) mx = fmaxf(mx, zr[j]);
+    float se = 0.f;
+#pragma unroll
+    for (int j = 0; j < AC; ++j) se += expf(zr[j] - mx);
+    const float lse = mx + logf(se);
+    float H = 0.f, lpa = 0.f;
+#pragma unroll
+    for (int j = 0; j < AC; ++j) {
+      const float lz = zr[j] - lse;
+      H -= expf(lz) * lz;
+      lpa = (j == ab) ? lz : lpa;
+    }
+    const float dkl = lpo - lpa;
+    const float g_lpa = -adv * invB - 2.0f * beta * dkl * invB;
+#pragma unroll
+    for (int j = 0; j < AC; ++j) {
+      const float lz = zr[j] - lse, pj = expf(lz);
+      const float g = g_lpa * (((j == ab) ? 1.0f : 0.0f) - pj) + c_ent * invB * pj * (lz + H);
+      s_dz[t * A1 + j] = bf2f(f2bf(g));   // the bf16 rounding of the GEMM path's dz buffer
+    }
+    const float d = zr[AC] - R;
+    s_dz[t * A1 + AC] = bf2f(f2bf(a.vf_coef * 2.0f * d * invB));
+    st[0] = -(double)(adv * lpa);
+    st[1] = (double)(dkl * dkl);
+    st[2] = H;
+    st[3] = (double)(d * d);
+    st[4] = R; st[5] = (double)R * R; st[6] = v; st[7] = (double)v * v; st[8] = (double)R * v;
+  }
+  if (wv == 0 && T <= 64) {   // rows t < T live in wave 0: xor tree in fixed order, lane 0 writes the row
+#pragma unroll
+    for (int k = 0; k < 9; ++k) st[k] = wave_sum_d(st[k]);
+    if (lane == 0) {
+      double* sp = args.spart + (int64_t)e * A2C_STATS;
+#pragma unroll
+      for (int k = 0; k < 9; ++k) sp[k] = st[k];
+    }
+  }
+  __syncthreads();   // s_dz complete
+  // ---- head backward of this env's rows: units 2t, 2t + 1
+  float dwp[2][A1], dbf[2] = {0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int q = 0; q < A1; ++q) dwp[c][q] = 0.f;
+  for (int r0 = 0; r0 < T; r0 += HR) {
+    if (r0 > 0) {
+#pragma unroll
+      for (int u = 0; u < HR; ++u)
+        hr[u] = r0 + u < T ? reinterpret_cast<const uint32_t*>(a.h + ((int64_t)(r0 + u) * N + e) * HB_H)[tid] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < HR; ++u) {
+    const int r = r0 + u;
+    if (r >= T) break;
+    float dzb[A1];
+#pragma unroll
+    for (int q = 0; q < A1; ++q) dzb[q] = s_dz[r * A1 + q];
+    uint32_t packed = 0;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const float hf = __uint_as_float(c ? (hr[u] & 0xFFFF0000u) : (hr[u] << 16));
+      float sacc = 0.f;
+#pragma unroll
+      for (int q = 0; q < A1; ++q) {
+        sacc += dzb[q] * w2[c][q];
+        dwp[c][q] += hf * dzb[q];
+      }
+      const float d = hf > 0.f ? sacc : 0.f;
+      dbf[c] += d;
+      packed |= (uint32_t)f2bf(d) << (16 * c);
+    }
+    reinterpret_cast<uint32_t*>(a.dh + ((int64_t)r * N + e) * HB_H)[tid] = packed;
+    }
+  }
+  float* pw = args.pWh + (int64_t)e * HB_H * A1 + 2 * tid * A1;
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int q = 0; q < A1; ++q) pw[c * A1 + q] = dwp[c][q];
+  reinterpret_cast<float2*>(args.pbfc + (int64_t)e * HB_H)[tid] = make_float2(dbf[0], dbf[1]);
+  if (tid < A1) {   // head-bias gradient of this env: column tid of dz over the rows in order
+    float sb = 0.f;
+    for (int r = 0; r < T; ++r) sb += s_dz[r * A1 + tid];
+    args.pbh[(int64_t)e * A1 + tid] = sb;
+  }
+}
+
 }  // namespace aca
 
 extern "C" hipError_t aca_head_bwd(const float* z, const int32_t* act, const float* logp_old, const float* ent_coef,
@@ -966,6 +1169,34 @@ extern "C" hipError_t aca_a2c_head(const float* z, const int32_t* act, const flo
   case n: aca::a2c_head_kernel<n><<<aca::AH_WG, aca::AH_THREADS, 0, stream>>>(a); break;
     ACA_AH_CASE(2) ACA_AH_CASE(3) ACA_AH_CASE(4) ACA_AH_CASE(5) ACA_AH_CASE(6) ACA_AH_CASE(7)
 #undef ACA_AH_CASE
+  }
+  return hipGetLastError();
+}
+
+extern "C" hipError_t aca_a2c_head_env(const float* z, const int32_t* act, const float* logp_old,
+                                       const float* ent_coef, const float* kl_coef, float vf_coef, const float* rew,
+                                       float* val, const uint8_t* dn, int T, int N, int L, int returns_mode,
+                                       float gamma, float lam, float* ret_w, float* adv_w, const uint16_t* h,
+                                       const uint16_t* Wh, uint16_t* dh, int A, const float* hpart, int S,
+                                       int64_t plane_stride, const float* bfc, const float* bh, float* pWh,
+                                       float* pbfc, float* pbh, double* spart, hipStream_t stream) {
+  const int B = T * N;
+  if (T < 1 || T > aca::AE_MAXT || N < 1 || A < 2 || A > 7 || (returns_mode != 1 && returns_mode != 2) || !pWh ||
+      !pbfc || !pbh || !spart)
+    return hipErrorInvalidValue;
+  if (hpart && (S < 1 || S > aca::FC_MAX_PLANES || !bfc || !bh || reinterpret_cast<uintptr_t>(hpart) % 16 ||
+                reinterpret_cast<uintptr_t>(bfc) % 16 || plane_stride % 4))
+    return hipErrorInvalidValue;
+  aca::A2cEnvArgs a;
+  a.h = aca::HeadBwdArgs{z, act, logp_old, ent_coef, kl_coef, vf_coef, rew, val, dn, T, N, L, returns_mode, 0,
+                         gamma, lam, ret_w, adv_w, h, Wh, dh, nullptr, nullptr, nullptr, nullptr, B, nullptr};
+  a.hpart = hpart; a.S = S; a.plane_stride = plane_stride; a.bfc = bfc; a.bh = bh;
+  a.pWh = pWh; a.pbfc = pbfc; a.pbh = pbh; a.spart = spart;
+  switch (A) {
+#define ACA_AE_CASE(n) \
+  case n: aca::a2c_head_env_kernel<n><<<N, aca::AE_THREADS, 0, stream>>>(a); break;
+    ACA_AE_CASE(2) ACA_AE_CASE(3) ACA_AE_CASE(4) ACA_AE_CASE(5) ACA_AE_CASE(6) ACA_AE_CASE(7)
+#undef ACA_AE_CASE
   }
   return hipGetLastError();
 }

@@ -437,10 +437,48 @@ __device__ __forceinline__ float fin_job(const int64_t* __restrict__ w, float* _
 }
 
 
+// Statistics duty of the finaliser (one extra workgroup past the jobs): the per-env A2C statistics rows written by
+// loss.hip a2c_head_env_kernel ([N][A2C_STATS] fp64 sums) combined in env order into stats[0..7] -- the same slots
+// and formulas as a2c_head_kernel's (pg, kl, entropy, value loss, clip fraction 0, actor loss, ratio 1, EV-before).
+struct StatsDuty {
+  const double* part; int N, B;
+  const float* ent_coef; const float* kl_coef;
+  float* stats;
+};
+
+__device__ __forceinline__ void a2c_stats_duty(const StatsDuty& d) {
+  __shared__ double tot[A2C_STATS];
+  const int tid = threadIdx.x;
+  if (tid < 9) {
+    double v = 0.0;
+    for (int e = 0; e < d.N; ++e) v += d.part[(int64_t)e * A2C_STATS + tid];
+    tot[tid] = v;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const double inv = 1.0 / d.B;
+    const float beta = *d.kl_coef, c_ent = *d.ent_coef;
+    d.stats[0] = (float)(tot[0] * inv);
+    d.stats[1] = (float)(tot[1] * inv);
+    d.stats[2] = (float)(tot[2] * inv);
+    d.stats[3] = (float)(tot[3] * inv);
+    d.stats[4] = 0.f;
+    d.stats[5] = (float)(tot[0] * inv + beta * tot[1] * inv - c_ent * tot[2] * inv);
+    d.stats[6] = 1.f;
+    const double mr = tot[4] * inv, mv = tot[6] * inv;
+    const double vr = fmax(tot[5] * inv - mr * mr, 0.0), vv = fmax(tot[7] * inv - mv * mv, 0.0);
+    d.stats[7] = (float)((tot[8] * inv - mr * mv) / sqrt(vr * vv));
+  }
+}
+
 __global__ void __launch_bounds__(OPT_THREADS) grad_finalize_kernel(const int64_t* __restrict__ jobs, int njobs,
-                                                                    float* __restrict__ partial) {
+                                                                    float* __restrict__ partial, StatsDuty sd) {
   __shared__ float sh[16];
   __shared__ float red[16 * 64];
+  if ((int)blockIdx.x == njobs) {   // past the jobs: the statistics duty (its partial slot is zeroed by workgroup 0)
+    a2c_stats_duty(sd);
+    return;
+  }
   float s = fin_job<false>(jobs + (int64_t)blockIdx.x * FIN_WORDS, nullptr, red);
   if (blockIdx.x == 0)
     for (int b = njobs + threadIdx.x; b < SUMSQ_PARTS; b += OPT_THREADS) partial[b] = 0.f;
@@ -514,9 +552,13 @@ extern "C" hipError_t aca_sumsq_multi(const float* const* xs, const size_t* ns, 
 }
 
 // jobs: device int64 [njobs, FIN_WORDS] (built by the host, ops/optim.py finalize_jobs); partial: SUMSQ_PARTS floats
-extern "C" hipError_t aca_grad_finalize(const int64_t* jobs, int njobs, float* partial, hipStream_t stream) {
+extern "C" hipError_t aca_grad_finalize(const int64_t* jobs, int njobs, float* partial, const double* spart, int sN,
+                                        int sB, const float* ent_coef, const float* kl_coef, float* stats,
+                                        hipStream_t stream) {
   if (njobs < 1 || njobs > SUMSQ_PARTS) return hipErrorInvalidValue;
-  grad_finalize_kernel<<<njobs, OPT_THREADS, 0, stream>>>(jobs, njobs, partial);
+  if (spart && (sN < 1 || sB < 1 || !ent_coef || !kl_coef || !stats)) return hipErrorInvalidValue;
+  const StatsDuty sd{spart, sN, sB, ent_coef, kl_coef, stats};
+  grad_finalize_kernel<<<njobs + (spart ? 1 : 0), OPT_THREADS, 0, stream>>>(jobs, njobs, partial, sd);
   return hipGetLastError();
 }
 

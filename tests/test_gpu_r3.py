@@ -254,7 +254,7 @@ def test_a2c_head_timeout_is_raised_not_trained_on(cuda):
     from actor_critic_algs_on_tensorflow_amd import preset
     from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
     tr = ActorCriticTrainer(preset("pong_a2c", num_envs=32, device="cuda:0", outdir=None, quiet=True, stdout_freq=0,
-                                   save_every=0, cuda_graph=False))
+                                   save_every=0, cuda_graph=False, engine_opts=dict(a2c_head_env=False)))
     tr.step()
     torch.cuda.synchronize()
     assert tr.engine._a2c_bar is not None and not tr.engine.a2c_head_timed_out()

@@ -1,0 +1,129 @@
+"""Round-5 HIP kernels vs fp32 / fp64 PyTorch references of the same op.
+
+* ``a2c_head_env`` (loss.hip): the A2C learner head as one workgroup per env -- V(s_T) from the rollout's last fc
+  partial planes, returns, loss, dz, dh and per-env partial planes of dWh / dbfc / dbh + fp64 statistics rows --
+  against the 32-workgroup ``a2c_head`` (which itself is pinned to fc_value + head_bwd and to autograd in
+  test_gpu_r3 / test_gpu_learning), and the whole headline update through it against the ``a2c_head`` path.
+* ``fc_rollout`` (fc_rollout.hip): the rollout fc product on the fragment-ordered Wfc copy vs an fp64 product of the
+  same bf16 operands, every variant.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("T,N,mode", [(5, 32, 1), (5, 32, 2), (16, 24, 2), (5, 7, 1), (40, 3, 1)])
+def test_a2c_head_env_matches_a2c_head(cuda, T, N, mode):
+    """Per-env head == the grid-barrier head: V(s_T), targets / advantages and dh bit-identical (same plane
+    reduction and dot-product tree, same per-row arithmetic); dWh / dbfc / dbh (per-env planes summed over envs) and
+    the statistics (per-env fp64 rows combined by the finaliser duty) equal up to the summation order over rows."""
+    from actor_critic_algs_on_tensorflow_amd import _native
+    ops = _native.require()
+    A, A1, B, S = 6, 7, T * N, 13
+    g = torch.Generator(device="cpu").manual_seed(T * 100 + N + mode)
+    z = torch.randn(B, A1, generator=g).to(cuda)
+    act = torch.randint(0, A, (B,), dtype=torch.int32, generator=g).to(cuda)
+    lpo = (-torch.rand(B, generator=g) * 2).to(cuda)
+    rew = torch.randn(T, N, generator=g).to(cuda)
+    dones = (torch.rand(T, N, generator=g) < 0.1).to(torch.uint8).to(cuda)
+    h = torch.relu(torch.randn(B, 512, generator=g)).to(torch.bfloat16).to(cuda)
+    Wh = (0.05 * torch.randn(512, A1, generator=g)).to(torch.bfloat16).to(cuda)
+    hpart = (0.1 * torch.randn(32, N, 512, generator=g)).to(cuda)
+    bfc = (0.1 * torch.randn(512, generator=g)).to(cuda)
+    bh = torch.randn(A1, generator=g).to(cuda)
+    ent, kl = torch.tensor([0.01], device=cuda), torch.tensor([0.3], device=cuda)
+    val0 = torch.randn(T + 1, N, generator=g).to(cuda)
+    L = 5
+
+    def outs():
+        return dict(ret=torch.zeros(B, device=cuda), adv=torch.zeros(B, device=cuda),
+                    dh=torch.zeros(B, 512, dtype=torch.bfloat16, device=cuda), gWh=torch.zeros(512 * A1, device=cuda),
+                    gbh=torch.zeros(A1, device=cuda), gbfc=torch.zeros(512, device=cuda),
+                    stats=torch.zeros(8, device=cuda))
+
+    ref, new = outs(), outs()
+    vref = val0.clone()
+    bar = torch.zeros(4, dtype=torch.int32, device=cuda)
+    ops.a2c_head(z, act, lpo, ent, kl, 0.5, rew, vref, dones, L, mode, False, 0.99, 0.95, ref["ret"], ref["adv"], h,
+                 Wh, ref["dh"], ref["gWh"], ref["gbh"], ref["gbfc"], ref["stats"], hpart, S, bfc, bh, bar)
+    vnew = val0.clone()
+    vnew[T] = float("nan")
+    pWh, pbfc, pbh = (torch.full((N * n,), float("nan"), device=cuda) for n in (512 * A1, 512, A1))
+    spart = torch.full((N, 10), float("nan"), dtype=torch.float64, device=cuda)
+    ops.a2c_head_env(z, act, lpo, ent, kl, 0.5, rew, vnew, dones, L, mode, 0.99, 0.95, new["ret"], new["adv"], h, Wh,
+                     new["dh"], hpart, S, bfc, bh, pWh, pbfc, pbh, spart)
+    # the finaliser's statistics duty (no jobs but the duty's extra workgroup: one empty job)
+    jobs = torch.zeros(1, 8, dtype=torch.int64, device=cuda)
+    dummy = torch.zeros(4, device=cuda)
+    jobs[0, 0] = dummy.data_ptr()
+    jobs[0, 2] = 4
+    parts = torch.zeros(256, device=cuda)
+    ops.grad_finalize(jobs, parts, spart, B, ent, kl, new["stats"])
+    torch.cuda.synchronize()
+    assert torch.equal(vnew, vref)
+    for k in ("ret", "adv", "dh"):
+        assert torch.equal(new[k], ref[k]), k
+    torch.testing.assert_close(pWh.view(N, -1).sum(0), ref["gWh"], rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(pbfc.view(N, -1).sum(0), ref["gbfc"], rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(pbh.view(N, -1).sum(0), ref["gbh"], rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(new["stats"], ref["stats"], rtol=1e-4, atol=1e-6)
+    # without planes the kernel reads V(s_T) from val
+    new2 = outs()
+    pWh2 = torch.zeros_like(pWh)
+    ops.a2c_head_env(z, act, lpo, ent, kl, 0.5, rew, vnew, dones, L, mode, 0.99, 0.95, new2["ret"], new2["adv"], h,
+                     Wh, new2["dh"], None, 0, None, None, pWh2, torch.zeros_like(pbfc), torch.zeros_like(pbh),
+                     torch.zeros_like(spart))
+    torch.cuda.synchronize()
+    for k in ("ret", "adv", "dh"):
+        assert torch.equal(new2[k], new[k]), k
+    assert torch.equal(pWh2, pWh)
+
+
+def test_a2c_update_with_per_env_head_matches_a2c_head(cuda):
+    """Native Pong A2C, 3 graph-captured updates: the per-env head (head gradients as per-env planes summed by the
+    finaliser, statistics by its duty workgroup) tracks the a2c_head path: statistics close, parameters equal up to
+    the summation order of dWh / dbfc / dbh; and the update stays bitwise deterministic."""
+    from actor_critic_algs_on_tensorflow_amd import preset
+    from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
+    res = {}
+    for knob in (True, False, True):
+        cfg = preset("pong_a2c", num_envs=32, device="cuda:0", outdir=None, quiet=True, stdout_freq=0, save_every=0,
+                     engine_opts=dict(a2c_head_env=knob))
+        tr = ActorCriticTrainer(cfg)
+        tr.capture(warmup=1)
+        p0 = tr.flat.data.clone()
+        for _ in range(3):
+            tr.step()
+        torch.cuda.synchronize()
+        assert bool(tr.engine._ae) == knob
+        out = (tr.flat.data - p0, tr.stats_buf.clone(), tr.storage.values.clone())
+        if knob in res:
+            assert all(torch.equal(a, b) for a, b in zip(out, res[knob])), "per-env head update not deterministic"
+        res[knob] = out
+    d1, s1, _ = res[True]
+    d0, s0, _ = res[False]
+    assert torch.allclose(s0[:8], s1[:8], rtol=1e-3, atol=1e-5), (s0[:8], s1[:8])
+    assert (d0 - d1).norm() / d0.norm() < 1e-2, float((d0 - d1).norm() / d0.norm())
+
+
+@pytest.mark.parametrize("M", [32, 7, 1])
+def test_fc_rollout_matches_fp64_product(cuda, M):
+    """fc_rollout's planes summed in plane order == X @ W in fp64 (same bf16 operands) for every variant; the
+    fragment-ordered copy is frag_order_kc of the row-major weight."""
+    from actor_critic_algs_on_tensorflow_amd import _native
+    from actor_critic_algs_on_tensorflow_amd.ops.optim import frag_order_kc
+    ops = _native.require()
+    g = torch.Generator(device="cpu").manual_seed(M)
+    X = (torch.randn(M, 3136, generator=g) * 0.5).to(torch.bfloat16).to(cuda)
+    W = (torch.randn(3136, 512, generator=g) * 0.05).to(torch.bfloat16).to(cuda)
+    Wf = frag_order_kc(W.float(), 3136, 512)
+    # the layout itself: element (k, n) at ((k/16 * 16 + n/32) * 64 + (k/8 % 2) * 32 + n % 32) * 8 + k % 8
+    k, n = 1234, 345
+    assert torch.equal(Wf[((k // 16 * 16 + n // 32) * 64 + (k // 8 % 2) * 32 + n % 32) * 8 + k % 8], W[k, n])
+    ref = X.double() @ W.double()
+    for v in range(7):
+        hp = torch.full((32 * M * 512,), float("nan"), device=cuda)
+        S = ops.fc_rollout(X, Wf, hp, v)
+        got = hp.view(32, M, 512)[:S].double().sum(0)
+        assert float((got - ref).abs().max() / ref.abs().max()) < 1e-5, v

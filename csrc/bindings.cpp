@@ -28,6 +28,7 @@ hipError_t aca_mlp_fwd(const aca::MlpArgs*, int, size_t, hipStream_t);
 hipError_t aca_mlp_wgrad(const aca::WgradArgs*, hipStream_t);
 hipError_t aca_ppo_head(const aca::PpoHeadArgs*, int, hipStream_t);
 int aca_ppo_head_planes(int);
+int aca_opt_set_unroll(int);
 hipError_t aca_fc_rollout(const uint16_t*, int64_t, int, const uint16_t*, int, int, float*, int64_t, int, int, int*,
                           unsigned long long*, hipStream_t);
 hipError_t aca_mlp_rollout(const aca::RolloutArgs*, size_t, hipStream_t);
@@ -941,6 +942,8 @@ void ppo_head(Tensor h, Tensor Wh, Tensor bh, Tensor act, Tensor logp_old, Tenso
 }
 
 int64_t ppo_head_planes(int64_t B) { return aca_ppo_head_planes((int)B); }
+// float4 groups per thread of the single-segment optimiser launches (1, 2 or 4; A/B diagnostics); returns the value
+int64_t opt_set_unroll(int64_t u) { return aca_opt_set_unroll((int)u); }
 
 void prp_perm(Tensor out, int64_t seed, Tensor uc, int64_t epoch) {
   need(out, at::kLong, "out");
@@ -1934,6 +1937,7 @@ TORCH_LIBRARY(acamd, m) {
         "Tensor pWh, Tensor pbh, Tensor pbfc, Tensor pstats, Tensor ticket, Tensor stats, Tensor? hp=None, "
         "int hp_planes=0, Tensor? hbias=None) -> ()");
   m.def("ppo_head_planes(int B) -> int", &ppo_head_planes);
+  m.def("opt_set_unroll(int u) -> int", &opt_set_unroll);
   m.def("fc_rollout(Tensor X, Tensor Wf, Tensor hpart, int variant, Tensor? stamps=None) -> int");
   m.def("head_bwd(Tensor z, Tensor act, Tensor logp_old, Tensor ent_coef, Tensor kl_coef, float vf_coef, Tensor rew, "
         "Tensor val, Tensor dones, int L, int returns_mode, bool norm_adv, float gamma, float lam, Tensor ret_w, "

@@ -123,7 +123,37 @@ __device__ __forceinline__ void write_trans(const OptSeg& S, size_t i, float v) 
   }
 }
 
-template <bool ADAM>
+// The four consecutive elements 4 * i4 .. + 3 of a float4 group: for a fragment-ordered copy (ldt < 0, offset and N
+// multiples of 4) they are 4 consecutive u16 of one lane's 8 -> ONE 8-byte store (one 32-bit index computation)
+// instead of four 2-byte stores; other shadows per element.
+__device__ __forceinline__ void write_trans4(const OptSeg& S, size_t i4, float4 p4) {
+  const size_t i = 4 * i4;
+  for (int e = 0; e < S.ntrans; ++e) {
+    const OptTrans& T = S.tr[e];
+    const int64_t o = (int64_t)i - T.off;
+    if (o + 3 >= 0 && o < (int64_t)T.K * T.N) {
+      if (T.ldt < 0 && o >= 0 && o + 3 < (int64_t)T.K * T.N && ((o | T.N) & 3) == 0) {
+        const uint32_t ou = (uint32_t)o, n = (uint32_t)T.N;
+        const uint32_t k = ou / n, c = ou - k * n;
+        const uint32_t f = (((k >> 4) * (n >> 5) + (c >> 5)) * 64u + ((c >> 3) & 3u) * 16u + (k & 15u)) * 8u + (c & 7u);
+        uint2 pk;
+        pk.x = (uint32_t)f2bf(p4.x) | ((uint32_t)f2bf(p4.y) << 16);
+        pk.y = (uint32_t)f2bf(p4.z) | ((uint32_t)f2bf(p4.w) << 16);
+        *reinterpret_cast<uint2*>(reinterpret_cast<u16*>(T.dst) + f) = pk;
+        return;
+      }
+      write_trans(S, i, p4.x);
+      write_trans(S, i + 1, p4.y);
+      write_trans(S, i + 2, p4.z);
+      write_trans(S, i + 3, p4.w);
+      return;
+    }
+  }
+}
+
+// U float4 groups per thread per round; the first round's operands are requested BEFORE the global-norm reduction
+// (its partial loads + block sum would otherwise be a dependent round trip ahead of every element load).
+template <bool ADAM, int U>
 __device__ __forceinline__ void opt_body(const OptSeg& S, float b1, float b2, float eps, int zero_grad, int vblk,
                                          int vgrid, int* flag, float* shr) {
   float* __restrict__ p = S.p;
@@ -133,6 +163,23 @@ __device__ __forceinline__ void opt_body(const OptSeg& S, float b1, float b2, fl
   const size_t n = S.n;
   const float lr = *S.lr;
   const float t = ADAM ? (*S.t + 1.0f + (S.t_off > 0 ? (float)S.t_off : 0.f)) : 0.f;
+  const size_t n4 = n / 4;
+  const size_t stride = (size_t)vgrid * blockDim.x * U;
+  float4 g4[U], v4[U], p4[U], m4[U];
+  auto load = [&](size_t i0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const size_t i = i0 + (size_t)u * blockDim.x;
+      if (i < n4) {
+        g4[u] = reinterpret_cast<const float4*>(g)[i];
+        v4[u] = reinterpret_cast<const float4*>(v)[i];
+        p4[u] = reinterpret_cast<const float4*>(p)[i];
+        m4[u] = ADAM ? reinterpret_cast<const float4*>(m)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+  };
+  size_t i0 = vblk * (size_t)blockDim.x * U + threadIdx.x;
+  if (i0 < n4) load(i0);
   float scale = 1.f;
   if (S.parts) {
     const float gsq = partial_total(S.parts, shr) * S.norm_mul;
@@ -146,43 +193,40 @@ __device__ __forceinline__ void opt_body(const OptSeg& S, float b1, float b2, fl
     gi *= gmul;   // data parallelism: 1/world averaging of the summed gradient, folded in (no extra pass)
     if (clip > 0.f) gi = fminf(fmaxf(gi, -clip), clip);
     gi *= scale;
-    vi = b2 * vi + (1.0f - b2) * gi * gi;
+    // explicit fused multiply-adds: the rounding of the update is fixed by the source, not by how the compiler
+    // contracts it around the surrounding loads (which moved with the load order and changed the last ulp)
+    vi = __builtin_fmaf(1.0f - b2, gi * gi, b2 * vi);
     if (ADAM) {
-      mi = b1 * mi + (1.0f - b1) * gi;
-      pi -= lr_t * mi / (sqrtf(vi) + eps);
+      mi = __builtin_fmaf(1.0f - b1, gi, b1 * mi);
+      pi = __builtin_fmaf(-lr_t, mi / (sqrtf(vi) + eps), pi);
     } else {
-      pi -= lr * gi / sqrtf(vi + eps);
+      pi = __builtin_fmaf(-lr, gi / sqrtf(vi + eps), pi);
     }
   };
   u16* shadow = S.shadow;
-  // float4 body: all operand loads of a thread are issued together (one memory round trip per element group)
-  const size_t n4 = n / 4;
-  const size_t stride = (size_t)vgrid * blockDim.x;
-  for (size_t i = vblk * (size_t)blockDim.x + threadIdx.x; i < n4; i += stride) {
-    float4 g4 = reinterpret_cast<const float4*>(g)[i];
-    float4 v4 = reinterpret_cast<const float4*>(v)[i];
-    float4 p4 = reinterpret_cast<const float4*>(p)[i];
-    float4 m4 = ADAM ? reinterpret_cast<const float4*>(m)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-    if (zero_grad) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    upd(g4.x, v4.x, m4.x, p4.x);
-    upd(g4.y, v4.y, m4.y, p4.y);
-    upd(g4.z, v4.z, m4.z, p4.z);
-    upd(g4.w, v4.w, m4.w, p4.w);
-    reinterpret_cast<float4*>(v)[i] = v4;
-    if (ADAM) reinterpret_cast<float4*>(m)[i] = m4;
-    reinterpret_cast<float4*>(p)[i] = p4;
-    if (shadow) {
-      uint2 sv;
-      sv.x = (uint32_t)f2bf(p4.x) | ((uint32_t)f2bf(p4.y) << 16);
-      sv.y = (uint32_t)f2bf(p4.z) | ((uint32_t)f2bf(p4.w) << 16);
-      reinterpret_cast<uint2*>(shadow)[i] = sv;
+  // float4 body: all operand loads of a round are issued together (one memory round trip per round)
+  for (; i0 < n4; i0 += stride) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const size_t i = i0 + (size_t)u * blockDim.x;
+      if (i >= n4) break;
+      if (zero_grad) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      upd(g4[u].x, v4[u].x, m4[u].x, p4[u].x);
+      upd(g4[u].y, v4[u].y, m4[u].y, p4[u].y);
+      upd(g4[u].z, v4[u].z, m4[u].z, p4[u].z);
+      upd(g4[u].w, v4[u].w, m4[u].w, p4[u].w);
+      reinterpret_cast<float4*>(v)[i] = v4[u];
+      if (ADAM) reinterpret_cast<float4*>(m)[i] = m4[u];
+      reinterpret_cast<float4*>(p)[i] = p4[u];
+      if (shadow) {
+        uint2 sv;
+        sv.x = (uint32_t)f2bf(p4[u].x) | ((uint32_t)f2bf(p4[u].y) << 16);
+        sv.y = (uint32_t)f2bf(p4[u].z) | ((uint32_t)f2bf(p4[u].w) << 16);
+        reinterpret_cast<uint2*>(shadow)[i] = sv;
+      }
+      if (S.ntrans) write_trans4(S, i, p4[u]);
     }
-    if (S.ntrans) {
-      write_trans(S, 4 * i, p4.x);
-      write_trans(S, 4 * i + 1, p4.y);
-      write_trans(S, 4 * i + 2, p4.z);
-      write_trans(S, 4 * i + 3, p4.w);
-    }
+    if (i0 + stride < n4) load(i0 + stride);
   }
   if (vblk == 0) {   // scalar tail
     for (size_t i = n4 * 4 + threadIdx.x; i < n; i += blockDim.x) {
@@ -225,11 +269,11 @@ __device__ __forceinline__ void opt_body(const OptSeg& S, float b1, float b2, fl
   }
 }
 
-template <bool ADAM>
+template <bool ADAM, int U>
 __global__ void __launch_bounds__(OPT_THREADS) opt_kernel(OptSeg S, float b1, float b2, float eps, int zero_grad) {
   __shared__ int flag;
   __shared__ float shr[16];
-  opt_body<ADAM>(S, b1, b2, eps, zero_grad, blockIdx.x, gridDim.x, &flag, shr);
+  opt_body<ADAM, U>(S, b1, b2, eps, zero_grad, blockIdx.x, gridDim.x, &flag, shr);
 }
 
 // Several parameter groups (e.g. the reference's separate actor and critic optimisers) in ONE launch: the grid is
@@ -247,7 +291,7 @@ __global__ void __launch_bounds__(OPT_THREADS) opt_multi_kernel(OptMulti M, floa
   __shared__ float shr[16];
   int b = blockIdx.x, k = 0;
   while (k + 1 < M.nseg && b >= M.seg[k].nblocks) b -= M.seg[k++].nblocks;
-  opt_body<ADAM>(M.seg[k], b1, b2, eps, zero_grad, b, M.seg[k].nblocks, &flag, shr);
+  opt_body<ADAM, 1>(M.seg[k], b1, b2, eps, zero_grad, b, M.seg[k].nblocks, &flag, shr);
 }
 
 // Gradient finaliser: the last step of a backward pass before the optimiser. Gradient segments are either
@@ -509,11 +553,25 @@ __global__ void cast_bf16_kernel(const float* __restrict__ x, u16* __restrict__ 
     y[i] = f2bf(x[i]);
 }
 
-static int opt_grid(size_t n) {   // one float4 per thread (up to 16M parameters per pass)
-  size_t b = (n / 4 + OPT_THREADS - 1) / OPT_THREADS;
+static int opt_grid(size_t n, int unroll = 1) {   // `unroll` float4 groups per thread (up to 16M parameters per pass)
+  size_t b = (n / 4 + (size_t)OPT_THREADS * unroll - 1) / ((size_t)OPT_THREADS * unroll);
   if (b < 1) b = 1;
   if (b > 16384) b = 16384;
   return (int)b;
+}
+
+// float4 groups per thread of the single-segment optimiser launches (a diagnostic knob, aca_opt_set_unroll)
+static int g_opt_unroll = 1;
+
+template <bool ADAM>
+static void launch_opt(OptSeg& S, float b1, float b2, float eps, int zero_grad, hipStream_t stream) {
+  const int U = g_opt_unroll;
+  S.nblocks = opt_grid(S.n, U);
+  switch (U) {
+    case 2: opt_kernel<ADAM, 2><<<S.nblocks, OPT_THREADS, 0, stream>>>(S, b1, b2, eps, zero_grad); break;
+    case 4: opt_kernel<ADAM, 4><<<S.nblocks, OPT_THREADS, 0, stream>>>(S, b1, b2, eps, zero_grad); break;
+    default: opt_kernel<ADAM, 1><<<S.nblocks, OPT_THREADS, 0, stream>>>(S, b1, b2, eps, zero_grad); break;
+  }
 }
 
 }  // namespace aca
@@ -591,7 +649,7 @@ extern "C" hipError_t aca_adam_step(float* p, float* g, float* m, float* v, size
            0, {}};
   if (!ticket || !t) return hipErrorInvalidValue;
   if (!opt_load_trans(S, trans)) return hipErrorInvalidValue;
-  opt_kernel<true><<<S.nblocks, OPT_THREADS, 0, stream>>>(S, b1, b2, eps, zero_grad);
+  launch_opt<true>(S, b1, b2, eps, zero_grad, stream);
   return hipGetLastError();
 }
 
@@ -604,7 +662,7 @@ extern "C" hipError_t aca_rmsprop_step(float* p, float* g, float* v, size_t n, c
   OptSeg S{p, g, nullptr, v, n, lr, nullptr, gnorm_parts, gnorm_out, shadow, clip, max_norm, gmul, norm_mul, nullptr,
            opt_grid(n), 0, {}};
   if (!opt_load_trans(S, trans)) return hipErrorInvalidValue;
-  opt_kernel<false><<<S.nblocks, OPT_THREADS, 0, stream>>>(S, 0.f, alpha, eps, zero_grad);
+  launch_opt<false>(S, 0.f, alpha, eps, zero_grad, stream);
   return hipGetLastError();
 }
 
@@ -647,6 +705,11 @@ extern "C" hipError_t aca_opt_multi(const int64_t* words, const float* fvals, co
   if (adam) opt_multi_kernel<true><<<total, OPT_THREADS, 0, stream>>>(M, b1, b2, eps, zero_grad);
   else opt_multi_kernel<false><<<total, OPT_THREADS, 0, stream>>>(M, 0.f, b2, eps, zero_grad);
   return hipGetLastError();
+}
+
+extern "C" int aca_opt_set_unroll(int u) {
+  if (u == 1 || u == 2 || u == 4) g_opt_unroll = u;
+  return g_opt_unroll;
 }
 
 extern "C" hipError_t aca_grad_move(float* src, float* dst, size_t n, hipStream_t stream) {

@@ -195,10 +195,15 @@ class CNNEngine:
     _FRAG_SHAPES = ((32, 256), (64, 512), (64, 576))
 
     def frag_entries(self):
-        """(fp32 W view, rows, cols, fragment-ordered bf16 copy) of conv1..3 for the optimiser (``set_frag``)."""
-        if self.frag is None:
-            return []
-        return [(W, K, N, F) for W, (K, N), F in zip((self.W1, self.W2, self.W3), self._FRAG_SHAPES, self.frag)]
+        """(fp32 W view, rows, cols, fragment-ordered bf16 copy, layout) of conv1..3 (layout -1) and, with
+        ``fc_frag``, of Wfc (layout -2: the rollout fc product's B-fragment order) for the optimiser
+        (``set_frag``): the update writes them as it goes."""
+        ent = []
+        if self.frag is not None:
+            ent += [(W, K, N, F, -1) for W, (K, N), F in zip((self.W1, self.W2, self.W3), self._FRAG_SHAPES, self.frag)]
+        if self.wfc_frag is not None:
+            ent.append((self.Wfc, 3136, 512, self.wfc_frag, -2))
+        return ent
 
     @torch.no_grad()
     def sync_frag(self):

@@ -166,12 +166,12 @@ class ActorCriticTrainer:
             if dp is not None:
                 opt.grad_mul = dp.grad_mul   # the all-reduce leaves the sum; the update kernel averages on read
             self.opts[g] = opt
-        if self.engine is not None and self.engine.frag is not None:
-            # the group holding the conv weights also rewrites their fragment-ordered copies in its update
+        if self.engine is not None and self.engine.frag_entries():
+            # the group holding the conv (and fc) weights also rewrites their fragment-ordered copies in its update
             ent = self.engine.frag_entries()
             owner = [o for o in self.opts.values()
-                     if all(0 <= W.data_ptr() - o.p.data_ptr() < o.p.numel() * 4 for W, _, _, _ in ent)]
-            assert len(owner) == 1, "the conv weights must live in one optimiser group"
+                     if all(0 <= e[0].data_ptr() - o.p.data_ptr() < o.p.numel() * 4 for e in ent)]
+            assert len(owner) == 1, "the conv / fc weights must live in one optimiser group"
             owner[0].set_frag(ent)
         self.actor_opt = self.opts.get("actor", self.opts.get("shared"))
         if (self.engine is not None and dp is None and len(self.opts) == 1
@@ -610,8 +610,6 @@ class ActorCriticTrainer:
             if self.engine is not None:
                 opt.zero_grad_after = not stores_all
             opt.step()
-        if self.engine is not None and self.engine.wfc_frag is not None:
-            self.engine.sync_fc_frag()
         if self.mlp is not None:
             self.mlp.sync_shadow()
 

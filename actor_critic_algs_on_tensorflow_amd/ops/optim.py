@@ -102,24 +102,29 @@ class FusedAdam:
         self.g = grad_slab[self.start:self.end]
 
     def set_frag(self, entries):
-        """Fragment-ordered bf16 weight copies the update writes as it goes (``optim.hip`` OptTrans with ldt < 0):
-        ``entries`` = [(W fp32 view into this group, K rows, N cols, dst bf16 [K * N])]; the CNN engine's MFMA
-        kernels read them as one contiguous 1 KB load per wave fragment (``cnn_fused.hip`` frag_w1..3)."""
-        self.frag = list(entries)
+        """Fragment-ordered bf16 weight copies the update writes as it goes: ``entries`` = [(W fp32 view into this
+        group, K rows, N cols, dst bf16 [K * N][, layout])]. layout -1 (default, ``optim.hip`` OptTrans): the conv
+        kernels' order (``frag_order``), read as one contiguous 1 KB load per wave fragment (``cnn_fused.hip``
+        frag_w1..3); layout -2 (at most one): the 32x32x16 B-fragment order of the rollout fc product
+        (``frag_order_kc``, ``fc_rollout.hip``), whose region the kernel updates by wave items with a transposed
+        512-byte store per wave."""
+        self.frag = [tuple(e) if len(e) == 5 else tuple(e) + (-1,) for e in entries]
         self._frag_table = None
         if not self.frag:
             return
+        assert len(self.frag) <= 6 and sum(e[4] == -2 for e in self.frag) <= 1
         t = torch.zeros(6, 5, dtype=torch.int64)
-        for e, (W, K, N, dst) in enumerate(self.frag):
+        for e, (W, K, N, dst, lay) in enumerate(self.frag):
             off = (W.data_ptr() - self.p.data_ptr()) // 4
-            assert 0 <= off and off + K * N <= self.p.numel() and W.numel() == K * N
+            assert 0 <= off and off + K * N <= self.p.numel() and W.numel() == K * N and lay in (-1, -2)
             assert K % 16 == 0 and N % 32 == 0 and dst.dtype == torch.bfloat16 and dst.numel() == K * N
-            t[e] = torch.tensor([off, K, N, -1, dst.data_ptr()])
+            assert lay == -1 or (off % 4 == 0 and dst.data_ptr() % 16 == 0)
+            t[e] = torch.tensor([off, K, N, lay, dst.data_ptr()])
         self._frag_table = t
 
     def _torch_frag(self):
-        for W, K, N, dst in getattr(self, "frag", ()):
-            dst.copy_(frag_order(W, K, N))
+        for W, K, N, dst, lay in getattr(self, "frag", ()):
+            dst.copy_(frag_order(W, K, N) if lay == -1 else frag_order_kc(W, K, N))
 
     def set_lr(self, lr):
         self.lr.fill_(float(lr))

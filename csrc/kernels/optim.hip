@@ -102,6 +102,12 @@ struct OptSeg {
   // >= 0: this launch is Adam step *t + t_off + 1 of a captured sequence whose counter the host advances once per
   // update (the launch-time step is known), so no workgroup publishes t + 1 and the ticket is skipped; -1: ticket
   int t_off = -1;
+  // optional k-contiguous FRAGMENT-ORDERED bf16 copy of one row-major [K][N] weight inside the segment (the rollout
+  // fc product's B operand, fc_rollout.hip): element (k, n) at u16 ((k/16 * N/32 + n/32) * 64 + (k/8 % 2) * 32 +
+  // n % 32) * 8 + k % 8. Its region is updated by a separate wave-item loop (see opt_body); kc_K == 0: none.
+  int64_t kc_off = 0;
+  int kc_K = 0, kc_N = 0;
+  u16* kc_dst = nullptr;
 };
 
 __device__ __forceinline__ void write_trans(const OptSeg& S, size_t i, float v) {
@@ -155,7 +161,7 @@ __device__ __forceinline__ void write_trans4(const OptSeg& S, size_t i4, float4 
 // (its partial loads + block sum would otherwise be a dependent round trip ahead of every element load).
 template <bool ADAM, int U>
 __device__ __forceinline__ void opt_body(const OptSeg& S, float b1, float b2, float eps, int zero_grad, int vblk,
-                                         int vgrid, int* flag, float* shr) {
+                                         int vgrid, int* flag, float* shr, u16* kcs) {
   float* __restrict__ p = S.p;
   float* __restrict__ g = S.g;
   float* __restrict__ m = S.m;
@@ -165,12 +171,15 @@ __device__ __forceinline__ void opt_body(const OptSeg& S, float b1, float b2, fl
   const float t = ADAM ? (*S.t + 1.0f + (S.t_off > 0 ? (float)S.t_off : 0.f)) : 0.f;
   const size_t n4 = n / 4;
   const size_t stride = (size_t)vgrid * blockDim.x * U;
+  // the k-contiguous fragment region [kc0, kc1) in float4 groups is left to the wave-item loop below
+  const size_t kc0 = S.kc_K ? (size_t)S.kc_off / 4 : 0, kc1 = S.kc_K ? kc0 + (size_t)S.kc_K * S.kc_N / 4 : 0;
+  auto in_kc = [&](size_t i) { return i >= kc0 && i < kc1; };
   float4 g4[U], v4[U], p4[U], m4[U];
   auto load = [&](size_t i0) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const size_t i = i0 + (size_t)u * blockDim.x;
-      if (i < n4) {
+      if (i < n4 && !in_kc(i)) {
         g4[u] = reinterpret_cast<const float4*>(g)[i];
         v4[u] = reinterpret_cast<const float4*>(v)[i];
         p4[u] = reinterpret_cast<const float4*>(p)[i];
@@ -180,6 +189,25 @@ __device__ __forceinline__ void opt_body(const OptSeg& S, float b1, float b2, fl
   };
   size_t i0 = vblk * (size_t)blockDim.x * U + threadIdx.x;
   if (i0 < n4) load(i0);
+  // wave items of the fragment region: (k octet kq, 32-column block nb); lane -> row kq * 8 + (lane & 7), columns
+  // nb * 32 + 4 (lane >> 3) .. + 3 (a wave load: 8 rows x 128 bytes)
+  const int lane = threadIdx.x & 63, nwv = blockDim.x >> 6;
+  const int kNB = S.kc_N >> 5;
+  const int kItems = S.kc_K ? (S.kc_K >> 3) * kNB : 0;
+  const int gw0 = vblk * nwv + (threadIdx.x >> 6), GW = vgrid * nwv;
+  auto kc_index = [&](int it) {
+    const int kq = it / kNB, nb = it - kq * kNB;
+    return kc0 + ((size_t)(kq * 8 + (lane & 7)) * S.kc_N + nb * 32 + 4 * (lane >> 3)) / 4;
+  };
+  float4 kg, kv, kp, km;
+  auto kc_load = [&](int it) {
+    const size_t i = kc_index(it);
+    kg = reinterpret_cast<const float4*>(g)[i];
+    kv = reinterpret_cast<const float4*>(v)[i];
+    kp = reinterpret_cast<const float4*>(p)[i];
+    km = ADAM ? reinterpret_cast<const float4*>(m)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  if (gw0 < kItems) kc_load(gw0);
   float scale = 1.f;
   if (S.parts) {
     const float gsq = partial_total(S.parts, shr) * S.norm_mul;
@@ -210,6 +238,7 @@ __device__ __forceinline__ void opt_body(const OptSeg& S, float b1, float b2, fl
     for (int u = 0; u < U; ++u) {
       const size_t i = i0 + (size_t)u * blockDim.x;
       if (i >= n4) break;
+      if (in_kc(i)) continue;
       if (zero_grad) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
       upd(g4[u].x, v4[u].x, m4[u].x, p4[u].x);
       upd(g4[u].y, v4[u].y, m4[u].y, p4[u].y);
@@ -227,6 +256,40 @@ __device__ __forceinline__ void opt_body(const OptSeg& S, float b1, float b2, fl
       if (S.ntrans) write_trans4(S, i, p4[u]);
     }
     if (i0 + stride < n4) load(i0 + stride);
+  }
+  // fragment region: the same update per element, then the bf16 copy transposed through a 512-byte per-wave LDS
+  // scratch laid out exactly as the destination run ([32 columns][8 k]) -> one contiguous 512-byte wave store
+  for (int it = gw0; it < kItems; it += GW) {
+    const size_t i = kc_index(it);
+    if (zero_grad) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    upd(kg.x, kv.x, km.x, kp.x);
+    upd(kg.y, kv.y, km.y, kp.y);
+    upd(kg.z, kv.z, km.z, kp.z);
+    upd(kg.w, kv.w, km.w, kp.w);
+    reinterpret_cast<float4*>(v)[i] = kv;
+    if (ADAM) reinterpret_cast<float4*>(m)[i] = km;
+    reinterpret_cast<float4*>(p)[i] = kp;
+    const u16 h0 = f2bf(kp.x), h1 = f2bf(kp.y), h2 = f2bf(kp.z), h3 = f2bf(kp.w);
+    if (shadow) {
+      uint2 sv;
+      sv.x = (uint32_t)h0 | ((uint32_t)h1 << 16);
+      sv.y = (uint32_t)h2 | ((uint32_t)h3 << 16);
+      reinterpret_cast<uint2*>(shadow)[i] = sv;
+    }
+    u16* ws = kcs + (threadIdx.x >> 6) * 256;
+    const int r = lane & 7, c4 = lane >> 3;
+    ws[(4 * c4 + 0) * 8 + r] = h0;
+    ws[(4 * c4 + 1) * 8 + r] = h1;
+    ws[(4 * c4 + 2) * 8 + r] = h2;
+    ws[(4 * c4 + 3) * 8 + r] = h3;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint2 o = reinterpret_cast<const uint2*>(ws)[lane];
+    const int kq = it / kNB, nb = it - kq * kNB;
+    reinterpret_cast<uint2*>(S.kc_dst + ((size_t)(kq >> 1) * kNB + nb) * 512 + (kq & 1) * 256)[lane] = o;
+    __builtin_amdgcn_wave_barrier();   // the scratch is rewritten by the next item
+    if (it + GW < kItems) kc_load(it + GW);
   }
   if (vblk == 0) {   // scalar tail
     for (size_t i = n4 * 4 + threadIdx.x; i < n; i += blockDim.x) {
@@ -273,7 +336,8 @@ template <bool ADAM, int U>
 __global__ void __launch_bounds__(OPT_THREADS) opt_kernel(OptSeg S, float b1, float b2, float eps, int zero_grad) {
   __shared__ int flag;
   __shared__ float shr[16];
-  opt_body<ADAM, U>(S, b1, b2, eps, zero_grad, blockIdx.x, gridDim.x, &flag, shr);
+  __shared__ __attribute__((aligned(16))) u16 kcs[OPT_THREADS / 64 * 256];
+  opt_body<ADAM, U>(S, b1, b2, eps, zero_grad, blockIdx.x, gridDim.x, &flag, shr, kcs);
 }
 
 // Several parameter groups (e.g. the reference's separate actor and critic optimisers) in ONE launch: the grid is
@@ -289,9 +353,10 @@ __global__ void __launch_bounds__(OPT_THREADS) opt_multi_kernel(OptMulti M, floa
                                                                 int zero_grad) {
   __shared__ int flag;
   __shared__ float shr[16];
+  __shared__ __attribute__((aligned(16))) u16 kcs[OPT_THREADS / 64 * 256];
   int b = blockIdx.x, k = 0;
   while (k + 1 < M.nseg && b >= M.seg[k].nblocks) b -= M.seg[k++].nblocks;
-  opt_body<ADAM, 1>(M.seg[k], b1, b2, eps, zero_grad, b, M.seg[k].nblocks, &flag, shr);
+  opt_body<ADAM, 1>(M.seg[k], b1, b2, eps, zero_grad, b, M.seg[k].nblocks, &flag, shr, kcs);
 }
 
 // Gradient finaliser: the last step of a backward pass before the optimiser. Gradient segments are either
@@ -620,16 +685,25 @@ extern "C" hipError_t aca_grad_finalize(const int64_t* jobs, int njobs, float* p
   return hipGetLastError();
 }
 
-// trans: host table [OPT_MAXT][5] = (offset, K, N, ldt, dst) of one segment; K == 0 ends the list
+// trans: host table [OPT_MAXT][5] = (offset, K, N, ldt, dst) of one segment; K == 0 ends the list. ldt -1: the
+// conv kernels' fragment order (write_trans); ldt -2: the k-contiguous fragment region (at most one; opt_body).
 static bool opt_load_trans(OptSeg& S, const int64_t* tw0) {
   S.ntrans = 0;
+  S.kc_K = 0;
   if (!tw0) return true;
   for (int e = 0; e < OPT_MAXT; ++e) {
     const int64_t* tw = tw0 + (int64_t)e * 5;
     if (tw[1] <= 0) break;
     if (tw[3] < 0 && (tw[1] % 16 || tw[2] % 32)) return false;   // fragment order: 16-row tiles, 32-wide k-steps
-    S.tr[e] = OptTrans{tw[0], (int)tw[1], (int)tw[2], (int)tw[3], reinterpret_cast<float*>(tw[4])};
-    S.ntrans = e + 1;
+    if (tw[3] == -2) {
+      if (S.kc_K || tw[0] % 4 || tw[0] < 0 || (size_t)(tw[0] + tw[1] * tw[2]) > S.n || tw[4] % 16) return false;
+      S.kc_off = tw[0];
+      S.kc_K = (int)tw[1];
+      S.kc_N = (int)tw[2];
+      S.kc_dst = reinterpret_cast<u16*>(tw[4]);
+      continue;
+    }
+    S.tr[S.ntrans++] = OptTrans{tw[0], (int)tw[1], (int)tw[2], (int)tw[3], reinterpret_cast<float*>(tw[4])};
   }
   return true;
 }

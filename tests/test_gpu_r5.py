@@ -127,3 +127,44 @@ def test_fc_rollout_matches_fp64_product(cuda, M):
         S = ops.fc_rollout(X, Wf, hp, v)
         got = hp.view(32, M, 512)[:S].double().sum(0)
         assert float((got - ref).abs().max() / ref.abs().max()) < 1e-5, v
+
+
+@pytest.mark.parametrize("cls_name", ["rmsprop", "adam"])
+def test_optimiser_writes_the_kc_fragment_copy(cuda, cls_name):
+    """The native optimiser's k-contiguous fragment region (optim.hip opt_body wave items, layout -2): parameters,
+    moments and the row-major bf16 shadow bit-identical to the same update without the region (the per-element
+    arithmetic is shared), and the copy == frag_order_kc of the updated shadow, over 3 steps; a conv-layout copy in
+    the same segment stays current too."""
+    from actor_critic_algs_on_tensorflow_amd.ops.optim import (FlatParams, FusedAdam, FusedRMSprop, frag_order,
+                                                               frag_order_kc)
+    cls = FusedRMSprop if cls_name == "rmsprop" else FusedAdam
+    runs = []
+    for with_kc in (True, False):
+        g = torch.Generator(device="cpu").manual_seed(11)
+        Wc = torch.nn.Parameter(torch.randn(64, 512, generator=g).to(cuda))
+        Wa = torch.nn.Parameter(torch.randn(37, generator=g).to(cuda))
+        Wk = torch.nn.Parameter(torch.randn(3136, 512, generator=g).to(cuda))
+        flat = FlatParams({"shared": [Wc, Wa, Wk]}, cuda)
+        sh = torch.empty(flat.numel, dtype=torch.bfloat16, device=cuda)
+        sh.copy_(flat.data)
+        opt = cls(flat, "shared", lr=1e-2, max_grad_norm=0.5, bf16_shadow=sh)
+        Fc = torch.empty(64 * 512, dtype=torch.bfloat16, device=cuda)
+        Fk = torch.full((3136 * 512,), float("nan"), dtype=torch.bfloat16, device=cuda)
+        vc = flat.data[flat.offsets[0]:flat.offsets[0] + Wc.numel()]
+        ok, nk = flat.offsets[2], Wk.numel()
+        ent = [(vc, 64, 512, Fc)] + ([(flat.data[ok:ok + nk], 3136, 512, Fk, -2)] if with_kc else [])
+        opt.set_frag(ent)
+        for _ in range(3):
+            flat.grad.copy_(torch.randn(flat.numel, generator=g).to(cuda))
+            from actor_critic_algs_on_tensorflow_amd import _native
+            ops = _native.require()
+            ops.sumsq(flat.grad, opt._partial)
+            opt.ext_parts = opt._partial
+            opt.step()
+        torch.cuda.synchronize()
+        assert torch.equal(Fc, frag_order(sh[flat.offsets[0]:flat.offsets[0] + Wc.numel()].float(), 64, 512))
+        if with_kc:
+            assert torch.equal(Fk, frag_order_kc(sh[ok:ok + nk].float(), 3136, 512))
+        runs.append((flat.data.clone(), opt.v.clone(), sh.clone()))
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)

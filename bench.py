@@ -46,6 +46,10 @@ def main():
                     help="dtype of the all-reduced gradient buckets (bf16 halves the xGMI bytes)")
     ap.add_argument("--engine-opts", default="",
                     help="JSON dict of EngineOpts overrides (A/B runs; the defaults are the measured fastest)")
+    ap.add_argument("--dp-world1", action="store_true",
+                    help="one process: run the data-parallel schedule (--overlap, --bucket-dtype) on a 1-rank RCCL "
+                         "group, so its collectives and buckets are issued exactly as at N >= 2 (the step from N = 1 "
+                         "to N = 2 of a scaling curve, without the second GPU)")
     args = ap.parse_args()
 
     from actor_critic_algs_on_tensorflow_amd import preset
@@ -56,7 +60,11 @@ def main():
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     torch.cuda.set_device(local)
-    dp = DP.DataParallel() if world > 1 else None
+    if args.dp_world1 and world == 1 and not torch.distributed.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
+        torch.distributed.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", local))
+    dp = DP.DataParallel() if (world > 1 or args.dp_world1) else None
     cfg = preset("pong_a2c", num_envs=args.envs, device=f"cuda:{local}", outdir=None, quiet=True,
                  stdout_freq=0, save_every=0, engine=args.engine, cuda_graph=not args.no_graph,
                  overlap=args.overlap, grad_bucket_dtype=args.bucket_dtype,
@@ -104,13 +112,13 @@ def main():
                        "algo": "A2C (RMSprop 7e-4, n-step returns, grad-norm 0.5)",
                        "parallelism": f"dp{world}", "engine": "native" if tr.engine is not None else "torch",
                        "hipgraph": bool(tr.graph), "dp_schedule": tr.graph[0] if tr.graph else "eager",
-                       "grad_bucket_dtype": args.bucket_dtype},
+                       "grad_bucket_dtype": args.bucket_dtype, "dp_world1": bool(args.dp_world1)},
         }
         print(json.dumps(out), flush=True)
         if os.environ.get("ACA_BENCH_SAVE_PLANS"):   # record the GEMM plans this run tuned (scripts/plan_search.sh)
             from actor_critic_algs_on_tensorflow_amd.ops import gemm as G
             G.save_plans(os.environ["ACA_BENCH_SAVE_PLANS"])
-    if dp is not None:
+    if torch.distributed.is_initialized():
         torch.distributed.destroy_process_group()
 
 

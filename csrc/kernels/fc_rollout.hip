@@ -90,12 +90,13 @@ __global__ void __launch_bounds__(64 * W) fc_rollout_kernel(FcRolloutArgs a) {
 }  // namespace aca
 
 // variant: (KR, W) = 0: (2, 7) -> 14 planes, 1: (4, 7) -> 7 planes, 2: (1, 14) -> 14 planes, 3: (7, 4) -> 7 planes,
-// 4: (7, 2) -> 14 planes, 5: (2, 14) -> 7 planes, 6: (1, 7) -> 28 planes. Returns the plane count through *S_out.
+// 4: (7, 2) -> 14 planes, 5: (2, 14) -> 7 planes, 6: (1, 7) -> 28 planes, 7: (7, 7) -> 4 planes, 8: (14, 1) -> 14
+// planes, 9: (7, 14) -> 2 planes. Returns the plane count through *S_out.
 extern "C" hipError_t aca_fc_rollout(const uint16_t* X, int64_t ldx, int M, const uint16_t* Wf, int K, int N,
                                      float* P, int64_t pstride, int variant, int max_planes, int* S_out,
                                      unsigned long long* stamps, hipStream_t stream) {
-  static const int cfg[7][2] = {{2, 7}, {4, 7}, {1, 14}, {7, 4}, {7, 2}, {2, 14}, {1, 7}};
-  if (variant < 0 || variant > 6 || M < 1 || M > 32 || K % 16 || N % 32 || ldx % 8 ||
+  static const int cfg[10][2] = {{2, 7}, {4, 7}, {1, 14}, {7, 4}, {7, 2}, {2, 14}, {1, 7}, {7, 7}, {14, 1}, {7, 14}};
+  if (variant < 0 || variant > 9 || M < 1 || M > 32 || K % 16 || N % 32 || ldx % 8 ||
       reinterpret_cast<uintptr_t>(X) % 16 || reinterpret_cast<uintptr_t>(Wf) % 16 || (N >> 5) % 8)
     return hipErrorInvalidValue;
   const int kr = cfg[variant][0], w = cfg[variant][1];
@@ -111,7 +112,7 @@ extern "C" hipError_t aca_fc_rollout(const uint16_t* X, int64_t ldx, int M, cons
 #define ACA_FR_CASE(v, KR, W) \
   case v: aca::fc_rollout_kernel<KR, W><<<grid, 64 * W, 0, stream>>>(a); break;
     ACA_FR_CASE(0, 2, 7) ACA_FR_CASE(1, 4, 7) ACA_FR_CASE(2, 1, 14) ACA_FR_CASE(3, 7, 4) ACA_FR_CASE(4, 7, 2)
-    ACA_FR_CASE(5, 2, 14) ACA_FR_CASE(6, 1, 7)
+    ACA_FR_CASE(5, 2, 14) ACA_FR_CASE(6, 1, 7) ACA_FR_CASE(7, 7, 7) ACA_FR_CASE(8, 14, 1) ACA_FR_CASE(9, 7, 14)
 #undef ACA_FR_CASE
   }
   return hipGetLastError();

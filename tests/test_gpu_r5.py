@@ -122,7 +122,7 @@ def test_fc_rollout_matches_fp64_product(cuda, M):
     k, n = 1234, 345
     assert torch.equal(Wf[((k // 16 * 16 + n // 32) * 64 + (k // 8 % 2) * 32 + n % 32) * 8 + k % 8], W[k, n])
     ref = X.double() @ W.double()
-    for v in range(7):
+    for v in range(10):
         hp = torch.full((32 * M * 512,), float("nan"), device=cuda)
         S = ops.fc_rollout(X, Wf, hp, v)
         got = hp.view(32, M, 512)[:S].double().sum(0)

@@ -225,6 +225,8 @@ class CNNEngine:
 
     def _fc_rollout(self, b, hp):
         """Split-K planes of the rollout fc product into ``hp``; returns the plane count."""
+        # (rollout banks up to 32 envs: at 128 envs the general GEMM measured faster, 12.33 vs 12.62 ms per Breakout
+        # PPO update, profiles/r5_fc_frag_breakout.txt; the kernel itself takes up to 128 rows)
         if self.fc_frag >= 0 and b.B <= 32:
             return int(_native.require().fc_rollout(b.y3.view(b.B, 3136), self.wfc_frag, hp, self.fc_frag))
         return G.gemm(b.y3, 3136, True, self.sWfc, 512, False, hp, 512, 3, b.B, 512, 3136, workspace=self.ws,
@@ -367,16 +369,17 @@ class CNNEngine:
 
     # ------------------------------------------------------------------------------------------------ backward
     def tail_bucket(self):
-        """(start, end) slab offsets of the parameters whose gradients are final after the ``"tail"`` backward stage
-        (fc + policy/value head: 95% of the bytes). They are contiguous at the end of the slab, so data parallelism
-        can all-reduce them while the conv backward (``"trunk"`` stage) still runs."""
+        """(start, end) slab offsets of the parameters whose gradients are final after the ``"tail"`` backward stage:
+        the fc weight (95% of the bytes), stored by the fc-layer backward. It sits at the end of the slab
+        (``CNNActorCritic.param_groups``), so data parallelism can all-reduce it while the conv backward (``"trunk"``
+        stage) runs and then the rest -- conv, head and fc-bias gradients, the latter two summed from the head
+        launch's partial planes by the trunk stage's finaliser -- as the contiguous range before it."""
         base = self.flat.grad.data_ptr()
         start = (self.gWfc.data_ptr() - base) // 4
-        end = (self.gbh.data_ptr() - base) // 4 + self.gbh.numel()
-        for g in (self.gW1, self.gb1, self.gW2, self.gb2, self.gW3, self.gb3):
-            assert (g.data_ptr() - base) // 4 + g.numel() <= start, "conv gradients must precede the fc/head bucket"
-        for g in (self.gbfc, self.gWh):
-            assert start <= (g.data_ptr() - base) // 4 < end
+        end = start + self.gWfc.numel()
+        assert self.flat.grad.numel() - end < 64, "the fc weight must close the slab (up to alignment padding)"
+        for g in (self.gW1, self.gb1, self.gW2, self.gb2, self.gW3, self.gb3, self.gbfc, self.gWh, self.gbh):
+            assert (g.data_ptr() - base) // 4 + g.numel() <= start, "every other gradient must precede the fc weight"
         return start, end
 
     def _wgrad(self, name, gview, A, lda, B_, ldb, M, N, K, ws, gb, gb_scale=1.0):
@@ -558,8 +561,10 @@ class CNNEngine:
         ws2 = self._side_ws()
         grouped = self.grouped and (head_done or stage == "trunk") and self.fused_bwd and self.det_wgrad
         # every gradient element of this backward is STORED (fused head, dWfc out_mode 0, conv planes and bias rows
-        # through the finaliser): the optimiser may skip zeroing the slab (trainer._run_optimizers)
-        self.last_bwd_stores_all = grouped and head_done and stage == "all"
+        # through the finaliser): the optimiser may skip zeroing the slab (trainer._run_optimizers). A "tail" stage
+        # decides it for the "trunk" stage that completes the same backward.
+        if stage != "trunk":
+            self.last_bwd_stores_all = grouped and head_done and stage in ("all", "tail")
         if stage == "trunk":
             if grouped:
                 return self._backward_grouped(b, stage, ws, ws2)
@@ -683,18 +688,32 @@ class CNNEngine:
     # ------------------------------------------------------------------------------------------------ finaliser
     want_parts = False   # set by the trainer when the optimiser may take the finaliser's sum-of-squares partials
 
-    def finalize(self, b: _Bufs):
+    def finalize(self, b: _Bufs, planes=None, parts=None, bias_rows=True):
         """One launch after the backward (``grad_finalize``): reduces the per-sample conv bias-gradient rows
         (fused backward) into the slab and, with ``want_parts``, writes the global-norm partials of the whole
-        gradient (``fin_parts``) so the optimiser needs no sum-of-squares pass."""
-        planes = tuple(sorted(self._cur_planes.items())) if self.det_wgrad else ()
-        key = (b.B, self.want_parts, self.fused_bwd, planes)
+        gradient (``fin_parts``) so the optimiser needs no sum-of-squares pass. ``planes``: only these plane sets
+        (default: every set of this backward); ``parts`` / ``bias_rows`` False: no norm partials / no bias rows."""
+        words = self._fin_table(b, planes, parts, bias_rows)
+        sd, self._stats_duty = self._stats_duty, None
+        if sd is not None:   # the per-env head's statistics rows -> stats[0..7] (one extra finaliser workgroup)
+            spart, B, ent, kl, stats = sd
+            _native.require().grad_finalize(words[0], self.fin_parts, spart, B, ent, kl, stats)
+        else:
+            _native.require().grad_finalize(words[0], self.fin_parts)
+
+    def _fin_table(self, b: _Bufs, planes=None, parts=None, bias_rows=True):
+        """The finaliser's device job table for these plane sets (built once per key, outside graph capture: the
+        head launches pre-build their tail-stage tables on first use)."""
+        want_parts = self.want_parts if parts is None else parts
+        fused_rows = self.fused_bwd and bias_rows
+        planes = tuple(sorted((self._cur_planes if planes is None else planes).items())) if self.det_wgrad else ()
+        key = (b.B, want_parts, fused_rows, planes)
         words = self._fin_words.get(key)
         if words is None:
             segs = []
             flat = self.flat
             src_of = {}   # gradient slot -> (source, stride, planes)
-            if self.fused_bwd:
+            if fused_rows:
                 bp = b.biasp.data_ptr()
                 src_of = {self.gb3.data_ptr(): (bp, 160, b.B), self.gb2.data_ptr(): (bp + 64 * 4, 160, b.B),
                           self.gb1.data_ptr(): (bp + 128 * 4, 160, b.B)}
@@ -708,17 +727,12 @@ class CNNEngine:
                 src = src_of.get(g.data_ptr())
                 if src is not None:
                     segs.append((g.data_ptr(), src[0], g.numel(), src[1], src[2]))
-                elif self.want_parts:
+                elif want_parts:
                     segs.append((g.data_ptr(), 0, g.numel(), 0, 0))
             from ..ops.optim import finalize_jobs
             words = finalize_jobs(segs, self.dev, return_max=True)
             self._fin_words[key] = words
-        sd, self._stats_duty = self._stats_duty, None
-        if sd is not None:   # the per-env head's statistics rows -> stats[0..7] (one extra finaliser workgroup)
-            spart, B, ent, kl, stats = sd
-            _native.require().grad_finalize(words[0], self.fin_parts, spart, B, ent, kl, stats)
-        else:
-            _native.require().grad_finalize(words[0], self.fin_parts)
+        return words
 
     @staticmethod
     def dcol3(b):   # only the col2im data-gradient path materialises the column gradients

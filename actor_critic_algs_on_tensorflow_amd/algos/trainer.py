@@ -536,7 +536,7 @@ class ActorCriticTrainer:
                 and self._grad_sink is None)
 
     def _inline_dp_overlap(self):
-        """RCCL DP on the CNN engine: the gradient all-reduce is split into the fc/head bucket (all-reduced while
+        """RCCL DP on the CNN engine: the gradient all-reduce is split into the fc-weight bucket (all-reduced while
         the conv backward runs) and the conv bucket. (Also with ``dp_capture="segments"``, where both are host
         cuts, so the two capture modes run the same kernels and stay bitwise equal.)"""
         return (self.engine is not None and self.dp is not None and self.dp.graph_capturable
@@ -544,7 +544,7 @@ class ActorCriticTrainer:
 
     def _backward_allreduce_overlapped(self, b, head_bias_done, head_done=False):
         """Backward + gradient all-reduce + optimiser for RCCL data parallelism, as ONE stream-ordered sequence that
-        a hipGraph records whole (SURVEY §5.8): the head/fc backward makes the tail bucket (95 % of the bytes) final;
+        a hipGraph records whole (SURVEY §5.8): the fc-layer backward makes the tail bucket (the fc weight, 95 % of the bytes) final;
         its all-reduce is issued on RCCL's stream (a forked branch of the graph) while the conv backward runs on the
         compute stream; then the conv bucket is all-reduced and the compute stream joins both before the optimiser.
         Nothing is issued from the host at replay time."""
@@ -604,7 +604,8 @@ class ActorCriticTrainer:
         # the CNN engine's grouped A2C backward STORES every gradient element (head launch, dWfc GEMM, finaliser of the
         # conv planes and bias rows), so the optimiser need not zero the slab behind itself: one 6.75 MB write pass
         # less per update. Every other backward (atomics, accumulating GEMM epilogues, DP buckets) keeps the zeroing.
-        stores_all = (self.engine is not None and self.dp is None and self._grad_sink is None
+        # (DP: the all-reduce / bf16 unpack overwrite the slab in place; lag-1's grad_move zeroes G itself)
+        stores_all = (self.engine is not None and self._grad_sink is None
                       and getattr(self.engine, "last_bwd_stores_all", False))
         for opt in opts:
             if self.engine is not None:
@@ -743,7 +744,7 @@ class ActorCriticTrainer:
             uc = self.update_counter.view(1)
             # the grouped Adam launches of this update know their step (t + j + 1 for minibatch j): no per-launch
             # step ticket, the counters advance once after the loop
-            offsets = self.cfg.engine_opts.adam_step_offsets and self.dp is None
+            offsets = self.cfg.engine_opts.adam_step_offsets
             self._t_offs_used = 0
             for ep in range(cfg.ppo_epochs):
                 for k in range(cfg.ppo_minibatches):
@@ -772,15 +773,18 @@ class ActorCriticTrainer:
         b = eng.bufs(obs.shape[0] if obs_idx is None else obs_idx.numel(), with_grad=True)
         ppo = cfg.algo == "ppo"
         vf = cfg.vf_coef if "shared" in self.flat.groups else 1.0
-        if (forward and self.dp is None and self._grad_sink is None and self._bw_stage == "all"
+        if (forward and self._grad_sink is None and self._bw_stage == "all"
                 and actions.dtype == torch.int32 and eng.ppo_head_ok(b.B)):
-            # ONE head launch (z, loss, dz, dh, head gradient planes); the backward starts at the fc layer
+            # ONE head launch (z, loss, dz, dh, head gradient planes); the backward starts at the fc layer (DP: the
+            # head planes are summed by the finaliser at the end of the bucketed backward, before the 2nd bucket)
             planes = eng.big_gemm_ok(b.B)   # the fc product's split-K planes go straight to the head launch
             eng.forward(obs, b, head=False, obs_idx=obs_idx, fc_parts=planes)
             eng.ppo_head(b, actions, logp_old, adv, ret, v_old, self.ent_coef, self.kl_coef, vf,
                          cfg.ppo_clip if ppo else 0.0, (cfg.ppo_value_clip or 0.0) if ppo else 0.0, self.stats_buf,
                          fc=eng.last_fc if planes else None)
             self._bw_pending = (b, True)
+            if self._inline_dp_overlap():
+                return self._backward_allreduce_overlapped(b, True, head_done=True)
             eng.backward(b, head_bias_done=True, stage="all", head_done=True)
             self._apply_grads()
             return
@@ -817,12 +821,10 @@ class ActorCriticTrainer:
         if head_done:
             # loss + dz + the head's backward (dh, dWh, dbh, dbfc) in one launch
             boot, self._boot = getattr(self, "_boot", None), None
-            # the per-env head's gradient planes are summed by this backward's finaliser (DP: the fc/head bucket must
-            # be final before the conv backward's all-reduce split, and eager / segmented DP schedules stay on one
-            # kernel so they remain bitwise comparable)
-            planes_ok = self._bw_stage == "all" and self.dp is None
+            # the per-env head's gradient planes are summed by this backward's finaliser (under DP at the end of the
+            # "trunk" stage: the head / fc-bias gradients belong to the second bucket, engine.tail_bucket)
             eng.head_backward(b, actions, logp_old, self.ent_coef, self.kl_coef, vf, self.stats_buf, rets, boot=boot,
-                              planes_ok=planes_ok)
+                              planes_ok=self._bw_stage in ("all", "tail"))
         else:
             eng.loss(b, actions, logp_old, None, None, None, self.ent_coef, self.kl_coef, vf, 0.0, 0.0,
                      stats=self.stats_buf, returns=rets)
@@ -908,15 +910,15 @@ class ActorCriticTrainer:
     # ------------------------------------------------------------------ driver
     # Without DP the whole update is ONE captured hipGraph. With RCCL data parallelism it is ONE graph too: every
     # collective is recorded in it (RCCL calls are stream-ordered and capturable); the CNN engine's gradient
-    # all-reduce is split into the fc/head bucket, issued on RCCL's stream (a forked graph branch) while the conv
+    # all-reduce is split into the fc-weight bucket, issued on RCCL's stream (a forked graph branch) while the conv
     # backward runs, and the conv bucket (_backward_allreduce_overlapped). The host issues nothing per replay.
     # Host-side collectives (gloo) cannot be captured, so there the update is split into captured segments around
     # them, issued from the host between replays (async w.r.t. the host: the stream waits, the CPU does not); the
     # same segment schedules serve RCCL lag-1 A2C, whose all-reduce spans two updates:
     #   overlap="strict" (exact synchronous A2C, the default):
     #       pre   = rollout + returns + loss + backward of the head and fc layers        (graph 1)
-    #       AR(fc/head bucket, 95% of the bytes) on the RCCL stream    || mid = conv backward (graph 2)
-    #       AR(conv bucket) ; the main stream waits for both ; post = optimiser + stats    (graph 3)
+    #       AR(fc-weight bucket, 95% of the bytes) on the RCCL stream    || mid = conv backward (graph 2)
+    #       AR(conv + head bucket) ; the main stream waits for both ; post = optimiser + stats    (graph 3)
     #   overlap="lag1" (policy lag 1, BASELINE's "all-reduce overlapped with the next rollout"):
     #       pre   = rollout + returns + loss + full backward into the gradient slab G     (graph 1)
     #               || AR(C) of the PREVIOUS update's gradient, issued at the end of the previous step
@@ -936,14 +938,39 @@ class ActorCriticTrainer:
     def _can_capture(self):
         return self.cfg.cuda_graph and self.device.type == "cuda"
 
-    def _segmented(self):
-        """The A2C strict / lag-1 schedules with host-issued collectives between captured segments (gloo; and lag-1
-        under RCCL, whose all-reduce spans two updates). RCCL strict A2C is one graph (see _capture_set)."""
+    def _a2c_dp_schedule(self):
+        """The strict / lag-1 A2C data-parallel schedules apply (no batch-wide statistic inside the update)."""
         cfg = self.cfg
-        if self._inline_comm() and not self._lag1():
-            return False
         return (self.dp is not None and cfg.algo == "a2c" and self.engine is not None and not cfg.norm_adv
                 and self.lr_ctrl is None and cfg.kl_coef == 0.0)
+
+    def _segmented(self):
+        """The A2C strict / lag-1 schedules with host-issued collectives between captured segments (gloo). Under
+        RCCL both are ONE graph per update (see _capture_set; lag-1: _update_body_lag1)."""
+        if self._inline_comm():
+            return False
+        return self._a2c_dp_schedule()
+
+    def _update_body_lag1(self):
+        """RCCL lag-1 A2C as ONE captured graph per update: the all-reduce of the PREVIOUS update's gradient C is
+        forked onto RCCL's stream at the start, so it runs under this update's rollout, loss and backward (which
+        write G); then C is applied, C <- G, G <- 0, and C is packed for the next replay's all-reduce. The first
+        replay all-reduces and applies C = 0: a no-op for RMSprop (Adam advances its step count once more)."""
+        dp, C = self.dp, self._comm_grad
+        w = dp.allreduce_async(dp.comm_view(C))
+        self._defer_allreduce = True
+        try:
+            self.collect()
+            ret, adv = self.compute_returns()
+            self.learn(ret, adv)
+        finally:
+            self._defer_allreduce = False
+        w.wait()
+        dp.unpack(C)
+        self._post_body()
+        self._grad_move()
+        dp.pack(C)
+        self.storage.roll_over()
 
     def update_body(self):
         with self.timer.phase("rollout"):
@@ -980,6 +1007,14 @@ class ActorCriticTrainer:
         finally:
             self.timer.suspended = False
 
+    def _bind_comm_grad(self):
+        """lag-1: the optimisers read C, the all-reduced copy of the previous update's gradient."""
+        if self._comm_grad is None:   # one buffer shared by both ring-phase graph sets
+            self._comm_grad = torch.zeros_like(self.flat.grad)
+            for opt in self.opts.values():
+                opt.bind_grad(self._comm_grad)
+            self.dp.pack(self._comm_grad)
+
     def _capture(self, warmup):
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
@@ -1008,10 +1043,7 @@ class ActorCriticTrainer:
             self._defer_allreduce = True
             try:
                 if self._lag1():
-                    if self._comm_grad is None:   # one buffer shared by both ring-phase graph sets
-                        self._comm_grad = torch.zeros_like(self.flat.grad)
-                        for opt in self.opts.values():
-                            opt.bind_grad(self._comm_grad)
+                    self._bind_comm_grad()
                     g1 = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g1, capture_error_mode=CAPTURE_MODE):
                         self.update_body()
@@ -1047,10 +1079,18 @@ class ActorCriticTrainer:
                 self._bw_stage = "all"
         elif self._inline_comm():
             # RCCL: every collective of the update (gradient buckets per optimiser step, the advantage moments, the
-            # KL scalar) is recorded in the graph -- one replay per update, zero host-issued collectives
+            # KL scalar; lag-1: the previous gradient's all-reduce) is recorded in the graph -- one replay per
+            # update, zero host-issued collectives
+            lag1 = self._lag1() and self._a2c_dp_schedule()
+            if lag1:
+                self._bind_comm_grad()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
-                self.update_body()
+                if lag1:
+                    self._update_body_lag1()
+                else:
+                    self.update_body()
+            self._lag1_inline = lag1
             graph = ("single", g)
         elif self.dp is not None or self._grad_sink is not None:
             rec = SegmentRecorder()
@@ -1138,6 +1178,15 @@ class ActorCriticTrainer:
 
     def flush_pending(self):
         """lag-1 DP: apply the last all-reduced gradient (end of training / before a checkpoint)."""
+        if self.graph is not None and getattr(self, "_lag1_inline", False):
+            # the one-graph schedule leaves the last update's gradient packed in C (its all-reduce would open the
+            # next replay): all-reduce and apply it now, then C = 0 (the next replay applies nothing twice)
+            self.dp.allreduce_packed(self._comm_grad)
+            self.dp.unpack(self._comm_grad)
+            self._post_body()
+            self._comm_grad.zero_()
+            self.dp.pack(self._comm_grad)
+            return
         if self.graph is not None and self.graph[0] == "lag1" and self._comm_work is not None:
             self._comm_work.wait()
             self.dp.unpack(self._comm_grad)

@@ -107,6 +107,16 @@ class CNNActorCritic(ActorCritic):
     def value(self, obs):
         return self.net(obs)[1]
 
+    def param_groups(self):
+        """One group; the fc weight LAST in the flat slab. Data parallelism all-reduces the gradient in two buckets:
+        the fc weight (95 % of the bytes, final right after the fc-layer backward) overlapped with the conv backward,
+        then everything else -- the conv layers and the small head / fc-bias gradients, which the native head
+        launches leave as partial planes that only the backward's last (finaliser) launch sums -- so both buckets
+        are contiguous ranges and no extra launch is needed before the first all-reduce (algos/engine.py
+        tail_bucket)."""
+        fck = self.net.trunk.fc.kernel
+        return {"shared": [p for p in self.parameters() if p is not fck] + [fck]}
+
 
 def build_model(env, family="auto", variant="basic", seed=0, hidden=512):
     """Builds the model family for an env bank (``family``: auto | mlp | cnn)."""

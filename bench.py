@@ -30,7 +30,17 @@ BASELINE_VALUE = 63.08
 BASELINE_WHAT = "reference-style loop (1 env, batch-1 inference, CPU; this repo's code), 63.08 env-steps/s"
 
 
+def _json_stdout():
+    """stdout carries exactly ONE JSON line: native libraries (RCCL's version banner and warnings) write to fd 1, so
+    fd 1 is pointed at stderr for the whole run and the result goes to the saved original stdout."""
+    sys.stdout.flush()
+    out = os.dup(1)
+    os.dup2(2, 1)
+    return out
+
+
 def main():
+    out_fd = _json_stdout()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -114,7 +124,7 @@ def main():
                        "hipgraph": bool(tr.graph), "dp_schedule": tr.graph[0] if tr.graph else "eager",
                        "grad_bucket_dtype": args.bucket_dtype, "dp_world1": bool(args.dp_world1)},
         }
-        print(json.dumps(out), flush=True)
+        os.write(out_fd, (json.dumps(out) + "\n").encode())
         if os.environ.get("ACA_BENCH_SAVE_PLANS"):   # record the GEMM plans this run tuned (scripts/plan_search.sh)
             from actor_critic_algs_on_tensorflow_amd.ops import gemm as G
             G.save_plans(os.environ["ACA_BENCH_SAVE_PLANS"])

@@ -452,8 +452,8 @@ int64_t fc_rollout(Tensor X, Tensor Wf, Tensor hpart, int64_t variant, c10::opti
   need(X, at::kBFloat16, "X");
   need(Wf, at::kBFloat16, "Wf");
   need(hpart, at::kFloat, "hpart");
-  TORCH_CHECK(X.dim() == 2 && X.stride(1) == 1 && X.size(1) == 3136 && X.size(0) >= 1 && X.size(0) <= 32,
-              "fc_rollout: X must be [M <= 32, 3136] row-major");
+  TORCH_CHECK(X.dim() == 2 && X.stride(1) == 1 && X.size(1) == 3136 && X.size(0) >= 1 && X.size(0) <= 128,
+              "fc_rollout: X must be [M <= 128, 3136] row-major");
   TORCH_CHECK(Wf.numel() == 3136 * 512 && Wf.is_contiguous(), "fc_rollout: Wf must be the [3136 x 512] fragment copy");
   TORCH_CHECK(hpart.numel() % 32 == 0 && hpart.numel() / 32 >= X.size(0) * 512, "fc_rollout: hpart must hold 32 planes");
   int S = 0;

@@ -1,5 +1,5 @@
 // Rollout fc product of the Nature-CNN (SURVEY §2.4 K01 at the headline's rollout batch): the fc layer's split-K
-// partial planes  P[s][m][n] = sum_{k in chunk s} X[m][k] * W[k][n]  for the M <= 32 envs of one rollout step
+// partial planes  P[s][m][n] = sum_{k in chunk s} X[m][k] * W[k][n]  for the M <= 128 envs of one rollout step
 // (X = y3 [M, 3136] bf16, W = Wfc [3136, 512]), consumed by the fused rollout step / the A2C head, which sum the
 // planes in plane order, add the bias and apply ReLU (cnn_head.h).
 //
@@ -29,7 +29,7 @@ struct FcRolloutArgs {
   unsigned long long* stamps;   // diagnostics: per wave [entry, operands landed, MFMAs done, stores drained]
 };
 
-template <int KR, int W>
+template <int KR, int W, int MT>
 __global__ void __launch_bounds__(64 * W) fc_rollout_kernel(FcRolloutArgs a) {
   __shared__ float red[W > 1 ? W * 16 * 64 : 1];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -41,44 +41,56 @@ __global__ void __launch_bounds__(64 * W) fc_rollout_kernel(FcRolloutArgs a) {
   const int L = (G & 7) ? bid : (bid & 7) * (G >> 3) + (bid >> 3);
   const int s = L / NB, nb = L - s * NB;
   const int kb0 = (s * W + w) * KR;
-  const int m = min(lane & 31, a.M - 1);   // rows past M read row M - 1 (never stored)
-  const u16* xa = a.X + (int64_t)m * a.ldx + kb0 * 16 + 8 * (lane >> 5);
+  // MT 32-row blocks of X (rows past M read row M - 1, never stored); the B fragments are shared by all of them
   const u16* wb = a.Wf + ((int64_t)kb0 * NB + nb) * 512 + lane * 8;
-  bf16x8 af[KR], bf[KR];
+  bf16x8 af[MT][KR], bf[KR];
 #pragma unroll
-  for (int q = 0; q < KR; ++q) {
-    af[q] = *reinterpret_cast<const bf16x8*>(xa + q * 16);
-    bf[q] = *reinterpret_cast<const bf16x8*>(wb + (int64_t)q * NB * 512);
+  for (int q = 0; q < KR; ++q) bf[q] = *reinterpret_cast<const bf16x8*>(wb + (int64_t)q * NB * 512);
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    const int m = min(mt * 32 + (lane & 31), a.M - 1);
+    const u16* xa = a.X + (int64_t)m * a.ldx + kb0 * 16 + 8 * (lane >> 5);
+#pragma unroll
+    for (int q = 0; q < KR; ++q) af[mt][q] = *reinterpret_cast<const bf16x8*>(xa + q * 16);
   }
-  fr_f32x16 acc;
+  fr_f32x16 acc[MT];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[mt][r] = 0.f;
   if (st) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) st[1] = __builtin_amdgcn_s_memrealtime();
   }
 #pragma unroll
-  for (int q = 0; q < KR; ++q) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[q], bf[q], acc, 0, 0, 0);
-  if (st && lane == 0) st[2] = __builtin_amdgcn_s_memrealtime() + (unsigned long long)(acc[0] != acc[0]);
+  for (int q = 0; q < KR; ++q)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mt][q], bf[q], acc[mt], 0, 0, 0);
+  if (st && lane == 0) st[2] = __builtin_amdgcn_s_memrealtime() + (unsigned long long)(acc[0][0] != acc[0][0]);
   float* plane = a.P + (int64_t)s * a.pstride + nb * 32 + (lane & 31);
   const int mr = 4 * (lane >> 5);
-  if constexpr (W == 1) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = (r & 3) + 8 * (r >> 2) + mr;
-      if (row < a.M) plane[(int64_t)row * a.N] = acc[r];
-    }
-  } else {
+  for (int mt = 0; mt < MT; ++mt) {
+    if (mt * 32 >= a.M) break;
+    if constexpr (W == 1) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) red[(w * 16 + r) * 64 + lane] = acc[r];
-    __syncthreads();
-    // wave w sums accumulator rows r = w, w + W, ... over the waves in wave order (the same order for every r)
-    for (int r = w; r < 16; r += W) {
-      float v = red[r * 64 + lane];
+      for (int r = 0; r < 16; ++r) {
+        const int row = mt * 32 + (r & 3) + 8 * (r >> 2) + mr;
+        if (row < a.M) plane[(int64_t)row * a.N] = acc[mt][r];
+      }
+    } else {
+      if (mt > 0) __syncthreads();   // the previous block's reduction has read the buffer
 #pragma unroll
-      for (int ww = 1; ww < W; ++ww) v += red[(ww * 16 + r) * 64 + lane];
-      const int row = (r & 3) + 8 * (r >> 2) + mr;
-      if (row < a.M) plane[(int64_t)row * a.N] = v;
+      for (int r = 0; r < 16; ++r) red[(w * 16 + r) * 64 + lane] = acc[mt][r];
+      __syncthreads();
+      // wave w sums accumulator rows r = w, w + W, ... over the waves in wave order (the same order for every r)
+      for (int r = w; r < 16; r += W) {
+        float v = red[r * 64 + lane];
+#pragma unroll
+        for (int ww = 1; ww < W; ++ww) v += red[(ww * 16 + r) * 64 + lane];
+        const int row = mt * 32 + (r & 3) + 8 * (r >> 2) + mr;
+        if (row < a.M) plane[(int64_t)row * a.N] = v;
+      }
     }
   }
   if (st) {
@@ -96,7 +108,7 @@ extern "C" hipError_t aca_fc_rollout(const uint16_t* X, int64_t ldx, int M, cons
                                      float* P, int64_t pstride, int variant, int max_planes, int* S_out,
                                      unsigned long long* stamps, hipStream_t stream) {
   static const int cfg[10][2] = {{2, 7}, {4, 7}, {1, 14}, {7, 4}, {7, 2}, {2, 14}, {1, 7}, {7, 7}, {14, 1}, {7, 14}};
-  if (variant < 0 || variant > 9 || M < 1 || M > 32 || K % 16 || N % 32 || ldx % 8 ||
+  if (variant < 0 || variant > 9 || M < 1 || M > 128 || K % 16 || N % 32 || ldx % 8 ||
       reinterpret_cast<uintptr_t>(X) % 16 || reinterpret_cast<uintptr_t>(Wf) % 16 || (N >> 5) % 8)
     return hipErrorInvalidValue;
   const int kr = cfg[variant][0], w = cfg[variant][1];
@@ -108,9 +120,14 @@ extern "C" hipError_t aca_fc_rollout(const uint16_t* X, int64_t ldx, int M, cons
   aca::FcRolloutArgs a{reinterpret_cast<const aca::u16*>(X), ldx, M, reinterpret_cast<const aca::u16*>(Wf), K, N, P,
                        pstride, stamps};
   const int grid = S * (N >> 5);
-  switch (variant) {
-#define ACA_FR_CASE(v, KR, W) \
-  case v: aca::fc_rollout_kernel<KR, W><<<grid, 64 * W, 0, stream>>>(a); break;
+  const int MT = (M + 31) / 32;   // 32-row blocks of X per wave (the fc's B fragments loaded once for all of them)
+  if (variant == 9 && MT > 2) return hipErrorInvalidValue;   // 14 waves x 7 k-blocks x 3-4 row blocks would spill
+  switch (variant * 4 + (MT - 1)) {
+#define ACA_FR_CASE(v, KR, W)                                                                      \
+  case 4 * v + 0: aca::fc_rollout_kernel<KR, W, 1><<<grid, 64 * W, 0, stream>>>(a); break;         \
+  case 4 * v + 1: aca::fc_rollout_kernel<KR, W, 2><<<grid, 64 * W, 0, stream>>>(a); break;         \
+  case 4 * v + 2: aca::fc_rollout_kernel<KR, W, 3><<<grid, 64 * W, 0, stream>>>(a); break;         \
+  case 4 * v + 3: aca::fc_rollout_kernel<KR, W, 4><<<grid, 64 * W, 0, stream>>>(a); break;
     ACA_FR_CASE(0, 2, 7) ACA_FR_CASE(1, 4, 7) ACA_FR_CASE(2, 1, 14) ACA_FR_CASE(3, 7, 4) ACA_FR_CASE(4, 7, 2)
     ACA_FR_CASE(5, 2, 14) ACA_FR_CASE(6, 1, 7) ACA_FR_CASE(7, 7, 7) ACA_FR_CASE(8, 14, 1) ACA_FR_CASE(9, 7, 14)
 #undef ACA_FR_CASE

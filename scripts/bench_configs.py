@@ -68,6 +68,10 @@ def run(name, updates, warmup, engine, device, dp_world1=False, engine_opts=None
 
 
 def main():
+    # one JSON line per config on stdout: native libraries (RCCL's banner / warnings) write to fd 1 -> stderr
+    sys.stdout.flush()
+    out_fd = os.dup(1)
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="pong_a2c,breakout_ppo,mujoco_ppo_dp8,cartpole_cpu")
     ap.add_argument("--updates", type=int, default=20)
@@ -79,7 +83,8 @@ def main():
     args = ap.parse_args()
     opts = json.loads(args.engine_opts) if args.engine_opts else None
     for name in args.configs.split(","):
-        print(json.dumps(run(name, args.updates, args.warmup, args.engine, args.device, args.dp_world1, opts)), flush=True)
+        res = run(name, args.updates, args.warmup, args.engine, args.device, args.dp_world1, opts)
+        os.write(out_fd, (json.dumps(res) + "\n").encode())
 
 
 if __name__ == "__main__":

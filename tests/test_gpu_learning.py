@@ -106,6 +106,28 @@ def test_mujoco_ppo_mlp_engine_learns_and_does_not_decay(cuda):
     assert sum(last_third) / len(last_third) >= 0.9 * peak, rets
 
 
+def test_breakout_ppo_learns_on_the_large_batch_kernels_and_tracks_torch(cuda):
+    """BASELINE config 3 (Breakout-shape PPO: 128 envs x 128 steps, GAE 0.95, 4 epochs x 4 minibatches of 4096) with
+    the default EngineOpts -- the per-env split fused rollout step, the large-batch head (ppo_head), gemm_big fc
+    products and the persistent trunk backward, all asserted taken -- LEARNS: the fraction of points won rises from
+    random play (~0.10) past 0.45 within 300 updates (4.9M env steps; measured 0.10 -> 0.77 / 0.63 on seeds 1 / 2),
+    and the torch/autograd engine on the same seed follows it within a band at 200 updates (measured native 0.44 /
+    torch 0.45 on seed 1, 0.26 / 0.28 on seed 2; profiles/r5_breakout_learning.txt)."""
+    tr, rows = _curve("breakout_ppo", 300, 25, device="cuda:0", seed=1)
+    eng = tr.engine
+    assert eng is not None and tr.graph is not None
+    mb = tr.cfg.num_envs * tr.cfg.n_steps // tr.cfg.ppo_minibatches
+    assert eng.fused_env_step_ok(tr.cfg.num_envs) and eng.opts.fused_env_split
+    assert eng.ppo_head_ok(mb) and eng.big_gemm_ok(mb) and mb >= eng.trunk_bwd_persist_min_b
+    win = [r["win"] for r in rows]
+    assert win[0] < 0.15 and win[-1] > 0.45 and win[-1] > win[0] + 0.3, win
+    trt, rows_t = _curve("breakout_ppo", 200, 25, device="cuda:0", seed=1, engine="torch")
+    assert trt.engine is None
+    win_t = [r["win"] for r in rows_t]
+    assert win_t[-1] > win_t[0] + 0.15, win_t
+    assert abs(win_t[-1] - win[7]) < 0.15, (win[7], win_t[-1])
+
+
 @pytest.mark.parametrize("B,ppo", [(160, False), (4096, True)])
 def test_cnn_engine_matches_autograd_at_production_batch(cuda, B, ppo):
     """Native forward + fused loss + backward (trunk rows / per-env trunk, fused data-gradient kernel, split-K
@@ -149,9 +171,15 @@ def test_cnn_engine_matches_autograd_at_production_batch(cuda, B, ppo):
     else:
         al, *_ = L.actor_loss(logp, lpo, adv, ent, 0.0, 0.01)
     (al + 0.5 * L.value_loss(v, ret)).backward()
+    errs = {}
     for (name, p), pr in zip(model.named_parameters(), ref.parameters()):
         i = [id(q) for q in flat.params].index(id(p))
         off = flat.offsets[i]
         gn = flat.grad[off:off + p.numel()].view_as(p)
-        err = float((gn - pr.grad).norm() / (pr.grad.norm() + 1e-12))
-        assert err < 0.05, (name, err)
+        errs[name] = float((gn - pr.grad).norm() / (pr.grad.norm() + 1e-12))
+    print("relative gradient errors", B, errs)
+    # bf16 operands, fp32 accumulation: measured max 1.28 % (B = 160, conv1) and 0.17 % (B = 4096) per parameter
+    # (profiles/r5_breakout_learning.txt); the bars keep ~1.5-3x of headroom
+    bar = 0.02 if B <= 256 else 0.005
+    for name, err in errs.items():
+        assert err < bar, (name, err, bar)

@@ -107,7 +107,7 @@ def test_a2c_update_with_per_env_head_matches_a2c_head(cuda):
     assert (d0 - d1).norm() / d0.norm() < 1e-2, float((d0 - d1).norm() / d0.norm())
 
 
-@pytest.mark.parametrize("M", [32, 7, 1])
+@pytest.mark.parametrize("M", [32, 7, 1, 128, 70])
 def test_fc_rollout_matches_fp64_product(cuda, M):
     """fc_rollout's planes summed in plane order == X @ W in fp64 (same bf16 operands) for every variant; the
     fragment-ordered copy is frag_order_kc of the row-major weight."""
@@ -123,6 +123,8 @@ def test_fc_rollout_matches_fp64_product(cuda, M):
     assert torch.equal(Wf[((k // 16 * 16 + n // 32) * 64 + (k // 8 % 2) * 32 + n % 32) * 8 + k % 8], W[k, n])
     ref = X.double() @ W.double()
     for v in range(10):
+        if v == 9 and M > 64:
+            continue   # rejected by the launcher (would spill)
         hp = torch.full((32 * M * 512,), float("nan"), device=cuda)
         S = ops.fc_rollout(X, Wf, hp, v)
         got = hp.view(32, M, 512)[:S].double().sum(0)

@@ -229,6 +229,8 @@ class CNNEngine:
         # PPO update, profiles/r5_fc_frag_breakout.txt; the kernel itself takes up to 128 rows)
         if self.fc_frag >= 0 and b.B <= 32:
             return int(_native.require().fc_rollout(b.y3.view(b.B, 3136), self.wfc_frag, hp, self.fc_frag))
+        if self.fc_frag >= 0 and self.opts.fc_frag_big >= 0 and b.B <= 128:
+            return int(_native.require().fc_rollout(b.y3.view(b.B, 3136), self.wfc_frag, hp, self.opts.fc_frag_big))
         return G.gemm(b.y3, 3136, True, self.sWfc, 512, False, hp, 512, 3, b.B, 512, 3136, workspace=self.ws,
                       max_planes=self.fc_max_planes)
 

@@ -30,7 +30,7 @@ hipError_t aca_ppo_head(const aca::PpoHeadArgs*, int, hipStream_t);
 int aca_ppo_head_planes(int);
 int aca_opt_set_unroll(int);
 hipError_t aca_fc_rollout(const uint16_t*, int64_t, int, const uint16_t*, int, int, float*, int64_t, int, int, int*,
-                          unsigned long long*, hipStream_t);
+                          unsigned long long*, int, hipStream_t);
 hipError_t aca_mlp_rollout(const aca::RolloutArgs*, size_t, hipStream_t);
 hipError_t aca_env_step_cartpole(float*, int32_t*, int64_t*, float*, float*, const int64_t*, const int32_t*,
                                  const float*, float*, float*, uint8_t*, uint8_t*, uint32_t, int, int, int, float*,
@@ -123,7 +123,7 @@ hipError_t aca_grad_finalize(const int64_t*, int, float*, const double*, int, in
 hipError_t aca_a2c_head_env(const float*, const int32_t*, const float*, const float*, const float*, float,
                             const float*, float*, const uint8_t*, int, int, int, int, float, float, float*, float*,
                             const uint16_t*, const uint16_t*, uint16_t*, int, const float*, int, int64_t,
-                            const float*, const float*, float*, float*, float*, double*, hipStream_t);
+                            const float*, const float*, float*, float*, float*, double*, uint64_t*, hipStream_t);
 hipError_t aca_head_bwd(const float*, const int32_t*, const float*, const float*, const float*, float, const float*,
                         const float*, const uint8_t*, int, int, int, int, int, float, float, float*, float*,
                         const uint16_t*, const uint16_t*, uint16_t*, float*, float*, float*, float*, int,
@@ -448,6 +448,7 @@ void pong_fused_env_step(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, T
 
 // rollout fc product as split-K partial planes on the fragment-ordered Wfc copy (fc_rollout.hip); hpart holds 32
 // equal planes of [M, 512]; returns the number of planes written
+// variant >= 16: variant - 16 with the 32-row blocks split over workgroups (gridDim.y) instead of looped per wave
 int64_t fc_rollout(Tensor X, Tensor Wf, Tensor hpart, int64_t variant, c10::optional<Tensor> stamps) {
   need(X, at::kBFloat16, "X");
   need(Wf, at::kBFloat16, "Wf");
@@ -458,8 +459,9 @@ int64_t fc_rollout(Tensor X, Tensor Wf, Tensor hpart, int64_t variant, c10::opti
   TORCH_CHECK(hpart.numel() % 32 == 0 && hpart.numel() / 32 >= X.size(0) * 512, "fc_rollout: hpart must hold 32 planes");
   int S = 0;
   check(aca_fc_rollout(ptr<uint16_t>(X), X.stride(0), (int)X.size(0), ptr<uint16_t>(Wf), 3136, 512, ptr<float>(hpart),
-                       hpart.numel() / 32, (int)variant, 32, &S,
-                       reinterpret_cast<unsigned long long*>(stamps_ptr(stamps, 1)), cur_stream(X)),
+                       hpart.numel() / 32, (int)(variant & 15), 32, &S,
+                       reinterpret_cast<unsigned long long*>(stamps_ptr(stamps, 1)), variant >= 16 ? 1 : 0,
+                       cur_stream(X)),
         "fc_rollout");
   return S;
 }
@@ -1579,7 +1581,7 @@ void a2c_head_env(Tensor z, Tensor act, Tensor logp_old, Tensor ent_coef, Tensor
                   Tensor val, Tensor dones, int64_t L, int64_t returns_mode, double gamma, double lam, Tensor ret_w,
                   Tensor adv_w, Tensor h, Tensor Wh, Tensor dh, c10::optional<Tensor> hpart, int64_t S,
                   c10::optional<Tensor> bfc, c10::optional<Tensor> bh, Tensor pWh, Tensor pbfc, Tensor pbh,
-                  Tensor spart) {
+                  Tensor spart, c10::optional<Tensor> stamps) {
   TORCH_CHECK(rew.dim() == 2, "a2c_head_env: rewards must be [T, N]");
   const int T = rew.size(0), N = rew.size(1), B = T * N;
   TORCH_CHECK(z.dim() == 2 && z.size(0) >= B, "a2c_head_env: z must be [B, A + 1]");
@@ -1618,7 +1620,7 @@ void a2c_head_env(Tensor z, Tensor act, Tensor logp_old, Tensor ent_coef, Tensor
                          N, (int)L, (int)returns_mode, (float)gamma, (float)lam, ptr<float>(ret_w), ptr<float>(adv_w),
                          ptr<uint16_t>(h), ptr<uint16_t>(Wh), ptr<uint16_t>(dh), A, hp, (int)S, pstride,
                          optr<float>(bfc), optr<float>(bh), ptr<float>(pWh), ptr<float>(pbfc), ptr<float>(pbh),
-                         spart.data_ptr<double>(), cur_stream(z)),
+                         spart.data_ptr<double>(), stamps_ptr(stamps, N), cur_stream(z)),
         "a2c_head_env");
 }
 
@@ -1931,7 +1933,7 @@ TORCH_LIBRARY(acamd, m) {
   m.def("a2c_head_env(Tensor z, Tensor act, Tensor logp_old, Tensor ent_coef, Tensor kl_coef, float vf_coef, "
         "Tensor rew, Tensor val, Tensor dones, int L, int returns_mode, float gamma, float lam, Tensor ret_w, "
         "Tensor adv_w, Tensor h, Tensor Wh, Tensor dh, Tensor? hpart, int S, Tensor? bfc, Tensor? bh, Tensor pWh, "
-        "Tensor pbfc, Tensor pbh, Tensor spart) -> ()");
+        "Tensor pbfc, Tensor pbh, Tensor spart, Tensor? stamps=None) -> ()");
   m.def("ppo_head(Tensor h, Tensor Wh, Tensor bh, Tensor act, Tensor logp_old, Tensor adv, Tensor ret, Tensor? v_old, "
         "Tensor ent_coef, Tensor kl_coef, float vf_coef, float ppo_clip, float v_clip, Tensor dh, Tensor? z_out, "
         "Tensor pWh, Tensor pbh, Tensor pbfc, Tensor pstats, Tensor ticket, Tensor stats, Tensor? hp=None, "

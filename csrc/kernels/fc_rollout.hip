@@ -43,12 +43,14 @@ __global__ void __launch_bounds__(64 * W) fc_rollout_kernel(FcRolloutArgs a) {
   const int kb0 = (s * W + w) * KR;
   // MT 32-row blocks of X (rows past M read row M - 1, never stored); the B fragments are shared by all of them
   const u16* wb = a.Wf + ((int64_t)kb0 * NB + nb) * 512 + lane * 8;
+  // gridDim.y > 1: the 32-row blocks are split over workgroups instead (MT == 1; B fragments re-read per block)
+  const int m0 = blockIdx.y * 32;
   bf16x8 af[MT][KR], bf[KR];
 #pragma unroll
   for (int q = 0; q < KR; ++q) bf[q] = *reinterpret_cast<const bf16x8*>(wb + (int64_t)q * NB * 512);
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
-    const int m = min(mt * 32 + (lane & 31), a.M - 1);
+    const int m = min(m0 + mt * 32 + (lane & 31), a.M - 1);
     const u16* xa = a.X + (int64_t)m * a.ldx + kb0 * 16 + 8 * (lane >> 5);
 #pragma unroll
     for (int q = 0; q < KR; ++q) af[mt][q] = *reinterpret_cast<const bf16x8*>(xa + q * 16);
@@ -67,16 +69,16 @@ __global__ void __launch_bounds__(64 * W) fc_rollout_kernel(FcRolloutArgs a) {
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[mt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[mt][q], bf[q], acc[mt], 0, 0, 0);
   if (st && lane == 0) st[2] = __builtin_amdgcn_s_memrealtime() + (unsigned long long)(acc[0][0] != acc[0][0]);
-  float* plane = a.P + (int64_t)s * a.pstride + nb * 32 + (lane & 31);
+  float* plane = a.P + (int64_t)s * a.pstride + (int64_t)m0 * a.N + nb * 32 + (lane & 31);
   const int mr = 4 * (lane >> 5);
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
-    if (mt * 32 >= a.M) break;
+    if (m0 + mt * 32 >= a.M) break;
     if constexpr (W == 1) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = mt * 32 + (r & 3) + 8 * (r >> 2) + mr;
-        if (row < a.M) plane[(int64_t)row * a.N] = acc[mt][r];
+        if (m0 + row < a.M) plane[(int64_t)row * a.N] = acc[mt][r];
       }
     } else {
       if (mt > 0) __syncthreads();   // the previous block's reduction has read the buffer
@@ -89,7 +91,7 @@ __global__ void __launch_bounds__(64 * W) fc_rollout_kernel(FcRolloutArgs a) {
 #pragma unroll
         for (int ww = 1; ww < W; ++ww) v += red[(ww * 16 + r) * 64 + lane];
         const int row = mt * 32 + (r & 3) + 8 * (r >> 2) + mr;
-        if (row < a.M) plane[(int64_t)row * a.N] = v;
+        if (m0 + row < a.M) plane[(int64_t)row * a.N] = v;
       }
     }
   }
@@ -106,7 +108,7 @@ __global__ void __launch_bounds__(64 * W) fc_rollout_kernel(FcRolloutArgs a) {
 // planes, 9: (7, 14) -> 2 planes. Returns the plane count through *S_out.
 extern "C" hipError_t aca_fc_rollout(const uint16_t* X, int64_t ldx, int M, const uint16_t* Wf, int K, int N,
                                      float* P, int64_t pstride, int variant, int max_planes, int* S_out,
-                                     unsigned long long* stamps, hipStream_t stream) {
+                                     unsigned long long* stamps, int msplit, hipStream_t stream) {
   static const int cfg[10][2] = {{2, 7}, {4, 7}, {1, 14}, {7, 4}, {7, 2}, {2, 14}, {1, 7}, {7, 7}, {14, 1}, {7, 14}};
   if (variant < 0 || variant > 9 || M < 1 || M > 128 || K % 16 || N % 32 || ldx % 8 ||
       reinterpret_cast<uintptr_t>(X) % 16 || reinterpret_cast<uintptr_t>(Wf) % 16 || (N >> 5) % 8)
@@ -120,14 +122,18 @@ extern "C" hipError_t aca_fc_rollout(const uint16_t* X, int64_t ldx, int M, cons
   aca::FcRolloutArgs a{reinterpret_cast<const aca::u16*>(X), ldx, M, reinterpret_cast<const aca::u16*>(Wf), K, N, P,
                        pstride, stamps};
   const int grid = S * (N >> 5);
-  const int MT = (M + 31) / 32;   // 32-row blocks of X per wave (the fc's B fragments loaded once for all of them)
+  // 32-row blocks of X per wave (the fc's B fragments loaded once for all of them), or with msplit one block per
+  // workgroup row (gridDim.y)
+  const int MB = (M + 31) / 32;
+  const int MT = msplit ? 1 : MB;
   if (variant == 9 && MT > 2) return hipErrorInvalidValue;   // 14 waves x 7 k-blocks x 3-4 row blocks would spill
+  const dim3 gdim(grid, msplit ? MB : 1);
   switch (variant * 4 + (MT - 1)) {
 #define ACA_FR_CASE(v, KR, W)                                                                      \
-  case 4 * v + 0: aca::fc_rollout_kernel<KR, W, 1><<<grid, 64 * W, 0, stream>>>(a); break;         \
-  case 4 * v + 1: aca::fc_rollout_kernel<KR, W, 2><<<grid, 64 * W, 0, stream>>>(a); break;         \
-  case 4 * v + 2: aca::fc_rollout_kernel<KR, W, 3><<<grid, 64 * W, 0, stream>>>(a); break;         \
-  case 4 * v + 3: aca::fc_rollout_kernel<KR, W, 4><<<grid, 64 * W, 0, stream>>>(a); break;
+  case 4 * v + 0: aca::fc_rollout_kernel<KR, W, 1><<<gdim, 64 * W, 0, stream>>>(a); break;         \
+  case 4 * v + 1: aca::fc_rollout_kernel<KR, W, 2><<<gdim, 64 * W, 0, stream>>>(a); break;         \
+  case 4 * v + 2: aca::fc_rollout_kernel<KR, W, 3><<<gdim, 64 * W, 0, stream>>>(a); break;         \
+  case 4 * v + 3: aca::fc_rollout_kernel<KR, W, 4><<<gdim, 64 * W, 0, stream>>>(a); break;
     ACA_FR_CASE(0, 2, 7) ACA_FR_CASE(1, 4, 7) ACA_FR_CASE(2, 1, 14) ACA_FR_CASE(3, 7, 4) ACA_FR_CASE(4, 7, 2)
     ACA_FR_CASE(5, 2, 14) ACA_FR_CASE(6, 1, 7) ACA_FR_CASE(7, 7, 7) ACA_FR_CASE(8, 14, 1) ACA_FR_CASE(9, 7, 14)
 #undef ACA_FR_CASE

@@ -958,6 +958,7 @@ __global__ void __launch_bounds__(AE_THREADS) a2c_head_env_kernel(A2cEnvArgs arg
   __shared__ float s_vw[4];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int e = blockIdx.x, N = a.N, T = a.T;
+  hb_stamp(a, 0);
   // ---- loads: the bootstrap planes first (the longest chain), then everything else of this env
   FcH2<16> fh;
   if (args.hpart) fh.issue(args.hpart, args.S, args.plane_stride, args.bfc, e, tid);
@@ -1006,6 +1007,7 @@ __global__ void __launch_bounds__(AE_THREADS) a2c_head_env_kernel(A2cEnvArgs arg
     s_val[T] = a.val[(int64_t)T * N + e];
   }
   __syncthreads();
+  hb_stamp(a, 1);
   // ---- returns, loss, dz of row t (thread t < T), statistics row
   double st[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   if (tid < T) {
@@ -1076,6 +1078,7 @@ __global__ void __launch_bounds__(AE_THREADS) a2c_head_env_kernel(A2cEnvArgs arg
     }
   }
   __syncthreads();   // s_dz complete
+  hb_stamp(a, 2);
   // ---- head backward of this env's rows: units 2t, 2t + 1
   float dwp[2][A1], dbf[2] = {0.f, 0.f};
 #pragma unroll
@@ -1112,6 +1115,7 @@ __global__ void __launch_bounds__(AE_THREADS) a2c_head_env_kernel(A2cEnvArgs arg
     reinterpret_cast<uint32_t*>(a.dh + ((int64_t)r * N + e) * HB_H)[tid] = packed;
     }
   }
+  hb_stamp(a, 3);
   float* pw = args.pWh + (int64_t)e * HB_H * A1 + 2 * tid * A1;
 #pragma unroll
   for (int c = 0; c < 2; ++c)
@@ -1122,6 +1126,11 @@ __global__ void __launch_bounds__(AE_THREADS) a2c_head_env_kernel(A2cEnvArgs arg
     float sb = 0.f;
     for (int r = 0; r < T; ++r) sb += s_dz[r * A1 + tid];
     args.pbh[(int64_t)e * A1 + tid] = sb;
+  }
+  if (a.stamps) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    hb_stamp(a, 4);
   }
 }
 
@@ -1179,7 +1188,8 @@ extern "C" hipError_t aca_a2c_head_env(const float* z, const int32_t* act, const
                                        float gamma, float lam, float* ret_w, float* adv_w, const uint16_t* h,
                                        const uint16_t* Wh, uint16_t* dh, int A, const float* hpart, int S,
                                        int64_t plane_stride, const float* bfc, const float* bh, float* pWh,
-                                       float* pbfc, float* pbh, double* spart, hipStream_t stream) {
+                                       float* pbfc, float* pbh, double* spart, uint64_t* stamps,
+                                       hipStream_t stream) {
   const int B = T * N;
   if (T < 1 || T > aca::AE_MAXT || N < 1 || A < 2 || A > 7 || (returns_mode != 1 && returns_mode != 2) || !pWh ||
       !pbfc || !pbh || !spart)
@@ -1189,7 +1199,7 @@ extern "C" hipError_t aca_a2c_head_env(const float* z, const int32_t* act, const
     return hipErrorInvalidValue;
   aca::A2cEnvArgs a;
   a.h = aca::HeadBwdArgs{z, act, logp_old, ent_coef, kl_coef, vf_coef, rew, val, dn, T, N, L, returns_mode, 0,
-                         gamma, lam, ret_w, adv_w, h, Wh, dh, nullptr, nullptr, nullptr, nullptr, B, nullptr};
+                         gamma, lam, ret_w, adv_w, h, Wh, dh, nullptr, nullptr, nullptr, nullptr, B, stamps};
   a.hpart = hpart; a.S = S; a.plane_stride = plane_stride; a.bfc = bfc; a.bh = bh;
   a.pWh = pWh; a.pbfc = pbfc; a.pbh = pbh; a.spart = spart;
   switch (A) {

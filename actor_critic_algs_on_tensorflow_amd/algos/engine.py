@@ -225,8 +225,9 @@ class CNNEngine:
 
     def _fc_rollout(self, b, hp):
         """Split-K planes of the rollout fc product into ``hp``; returns the plane count."""
-        # (rollout banks up to 32 envs: at 128 envs the general GEMM measured faster, 12.33 vs 12.62 ms per Breakout
-        # PPO update, profiles/r5_fc_frag_breakout.txt; the kernel itself takes up to 128 rows)
+        # (up to 32 envs: variant fc_frag, one 32-row block per wave; 33..128 envs: fc_frag_big -- the per-wave
+        # row-block loop measured slower than the general GEMM at 128 envs, the row blocks split over workgroups
+        # slightly faster, profiles/r5_fc_frag_breakout.txt)
         if self.fc_frag >= 0 and b.B <= 32:
             return int(_native.require().fc_rollout(b.y3.view(b.B, 3136), self.wfc_frag, hp, self.fc_frag))
         if self.fc_frag >= 0 and self.opts.fc_frag_big >= 0 and b.B <= 128:

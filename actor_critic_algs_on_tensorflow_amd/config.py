@@ -25,7 +25,7 @@ class EngineOpts:
     frag_weights: bool = True         # conv weights also kept fragment-ordered (written by the optimiser step): the
                                       # MFMA weight loads become one contiguous 1 KB read per wave
     fc_max_planes: int = 32           # split-K partial planes of the rollout fc product (consumer-reduced)
-    fc_frag_big: int = -1             # ... for banks of 33..128 envs (+16: 32-row blocks split over workgroups)
+    fc_frag_big: int = 17             # ... for banks of 33..128 envs (+16: 32-row blocks split over workgroups)
     fc_frag: int = 5                  # rollout fc product (<= 32 envs) on a fragment-ordered Wfc copy (fc_rollout.hip
                                       # variant 0..6; -1: the general GEMM on the row-major shadow)
     # -- learner -------------------------------------------------------------------------------------------------

@@ -956,6 +956,7 @@ __global__ void __launch_bounds__(AE_THREADS) a2c_head_env_kernel(A2cEnvArgs arg
   __shared__ float s_rew[AE_MAXT], s_val[AE_MAXT + 1];
   __shared__ uint8_t s_dn[AE_MAXT];
   __shared__ float s_vw[4];
+  __shared__ double s_st[AE_MAXT * 9];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int e = blockIdx.x, N = a.N, T = a.T;
   hb_stamp(a, 0);
@@ -963,10 +964,17 @@ __global__ void __launch_bounds__(AE_THREADS) a2c_head_env_kernel(A2cEnvArgs arg
   FcH2<16> fh;
   if (args.hpart) fh.issue(args.hpart, args.S, args.plane_stride, args.bfc, e, tid);
   float w2[2][A1];
+  {   // rows 2t, 2t + 1 of Wh = 2 A1 consecutive bf16 at a 4-byte aligned offset: A1 32-bit loads
+    const uint32_t* wp = reinterpret_cast<const uint32_t*>(a.Wh) + tid * A1;
+    uint32_t wu[A1];
 #pragma unroll
-  for (int c = 0; c < 2; ++c)
+    for (int q = 0; q < A1; ++q) wu[q] = wp[q];
 #pragma unroll
-    for (int q = 0; q < A1; ++q) w2[c][q] = bf2f(a.Wh[(2 * tid + c) * A1 + q]);
+    for (int i = 0; i < 2 * A1; ++i) {
+      const float v = __uint_as_float((i & 1) ? (wu[i >> 1] & 0xFFFF0000u) : (wu[i >> 1] << 16));
+      w2[i / A1][i % A1] = v;
+    }
+  }
   if (tid < T) {
     const int i = tid * N + e;
     s_rew[tid] = a.rew[i];
@@ -1068,16 +1076,13 @@ __global__ void __launch_bounds__(AE_THREADS) a2c_head_env_kernel(A2cEnvArgs arg
     st[3] = (double)(d * d);
     st[4] = R; st[5] = (double)R * R; st[6] = v; st[7] = (double)v * v; st[8] = (double)R * v;
   }
-  if (wv == 0 && T <= 64) {   // rows t < T live in wave 0: xor tree in fixed order, lane 0 writes the row
+  // the statistics rows go through LDS and are summed by one thread after the backward (off the critical path:
+  // a 64-lane fp64 xor tree per statistic was ~1.5 us of dependent shuffles before the barrier)
+  if (tid < T) {
 #pragma unroll
-    for (int k = 0; k < 9; ++k) st[k] = wave_sum_d(st[k]);
-    if (lane == 0) {
-      double* sp = args.spart + (int64_t)e * A2C_STATS;
-#pragma unroll
-      for (int k = 0; k < 9; ++k) sp[k] = st[k];
-    }
+    for (int k = 0; k < 9; ++k) s_st[tid * 9 + k] = st[k];
   }
-  __syncthreads();   // s_dz complete
+  __syncthreads();   // s_dz, s_st complete
   hb_stamp(a, 2);
   // ---- head backward of this env's rows: units 2t, 2t + 1
   float dwp[2][A1], dbf[2] = {0.f, 0.f};
@@ -1126,6 +1131,15 @@ __global__ void __launch_bounds__(AE_THREADS) a2c_head_env_kernel(A2cEnvArgs arg
     float sb = 0.f;
     for (int r = 0; r < T; ++r) sb += s_dz[r * A1 + tid];
     args.pbh[(int64_t)e * A1 + tid] = sb;
+  }
+  if (tid == 64) {   // this env's statistics row: the rows summed in order (a thread of the second wave)
+    double tot[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int r = 0; r < T; ++r)
+#pragma unroll
+      for (int k = 0; k < 9; ++k) tot[k] += s_st[r * 9 + k];
+    double* sp = args.spart + (int64_t)e * A2C_STATS;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) sp[k] = tot[k];
   }
   if (a.stamps) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

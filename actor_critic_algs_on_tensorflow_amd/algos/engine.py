@@ -109,6 +109,7 @@ class CNNEngine:
         # narrow workgroups (off: fc_value + the 8-workgroup head_bwd kernel of round 2)
         self.a2c_head = o.a2c_head
         self._a2c_bar = None
+        self._fcf_cnt = None   # fused step fc product: slice counters + timeout word (fused_fc_args)
         # A2C head v3 (loss.hip a2c_head_env_kernel): one workgroup per env, no grid-wide hand-off; the head's weight /
         # bias gradients as per-env planes and the statistics as per-env rows, both reduced by the finaliser
         self.a2c_head_env = o.a2c_head_env
@@ -248,11 +249,30 @@ class CNNEngine:
         return self._bufs[key]
 
     # ------------------------------------------------------------------------------------------------ forward
-    def hpart(self, B):
-        """fp32 [FC_PLANES, B, 512] split-K partial planes of the rollout fc product (GEMM out_mode 3)."""
-        if B not in self._hpart:
-            self._hpart[B] = torch.zeros(FC_PLANES * B * 512, dtype=torch.float32, device=self.dev)
-        return self._hpart[B]
+    def hpart(self, B, slot=0):
+        """fp32 [FC_PLANES, B, 512] split-K partial planes of the rollout fc product (GEMM out_mode 3); slot 1: the
+        second buffer of the fused step's in-launch fc product (it reads one while it writes the other)."""
+        key = (B, slot)
+        if key not in self._hpart:
+            self._hpart[key] = torch.zeros(FC_PLANES * B * 512, dtype=torch.float32, device=self.dev)
+        return self._hpart[key]
+
+    def fused_fc_ok(self, B):
+        """The row-split fused step also computes the next observation's fc product (``EngineOpts.fused_fc``: at
+        most 32 envs, the fragment-ordered Wfc and conv copies)."""
+        return (self.opts.fused_fc and self.wfc_frag is not None and self.frag is not None and 1 <= B <= 32
+                and self.fused_step_ok(B))
+
+    def fused_fc_args(self, B):
+        """(Wfc copy, output planes, slice counters) of the next fused step's fc product: the planes go to the hpart
+        buffer the last fc product did NOT write (the step reads that one); ``last_fc`` then names the new planes."""
+        if self._fcf_cnt is None:   # 7 slices x (arrivals, departures) on own 64-byte lines + the timeout word
+            self._fcf_cnt = torch.zeros(232, dtype=torch.int32, device=self.dev)
+        hp = self.last_fc[0]
+        out = self.hpart(B, 1) if hp.data_ptr() == self.hpart(B, 0).data_ptr() else self.hpart(B, 0)
+        return self.wfc_frag, out, self._fcf_cnt
+
+    FCF_PLANES = 14   # cnn_fused.hip FCF_PLANES: 7 conv3 rows x 2 K halves
 
     def value(self, obs, b: _Bufs, out):
         """Bootstrap value of ``obs`` written straight into ``out`` [B] (trunk + the value column of the head)."""
@@ -276,7 +296,10 @@ class CNNEngine:
 
     def health_errors(self):
         """Names of the in-launch hand-offs that timed out since the engine was built (empty = healthy)."""
-        return ["a2c_head bootstrap-value hand-off"] if self.a2c_head_timed_out() else []
+        err = ["a2c_head bootstrap-value hand-off"] if self.a2c_head_timed_out() else []
+        if self._fcf_cnt is not None and int(self._fcf_cnt[224]) != 0:
+            err.append("fused-step fc product hand-off")
+        return err
 
     def fused_step_ok(self, B):
         """The rollout step can run as ONE launch of policy/env + the next observation's row-split trunk."""

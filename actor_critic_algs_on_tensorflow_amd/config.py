@@ -24,6 +24,9 @@ class EngineOpts:
     adam_step_offsets: bool = True    # MLP PPO: grouped Adam launches take their step from the minibatch index (no ticket)
     frag_weights: bool = True         # conv weights also kept fragment-ordered (written by the optimiser step): the
                                       # MFMA weight loads become one contiguous 1 KB read per wave
+    fused_fc: bool = False            # Pong bank of <= 32 envs: the next observation's fc product inside the fused step
+                                      # (in-launch hand-off of the conv3 rows instead of the fc launch; the hand-off
+                                      # costs as much as the boundary it removes: profiles/r5_fused_fc_ab.txt)
     fc_max_planes: int = 32           # split-K partial planes of the rollout fc product (consumer-reduced)
     fc_frag_big: int = 17             # ... for banks of 33..128 envs (+16: 32-row blocks split over workgroups)
     fc_frag: int = 5                  # rollout fc product (<= 32 envs) on a fragment-ordered Wfc copy (fc_rollout.hip

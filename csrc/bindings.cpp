@@ -56,7 +56,8 @@ hipError_t aca_pong_fused_step(uint16_t*, const float*, int, int64_t, const floa
                                float*, float*, int32_t*, int64_t*, float*, float*, const int64_t*, const uint8_t*,
                                uint8_t*, float*, uint8_t*, uint8_t*, uint32_t, int, const uint16_t*, const float*,
                                const uint16_t*, const float*, const uint16_t*, const float*, uint16_t*, uint16_t*,
-                               uint16_t*, float, uint8_t*, uint64_t*, int, int, hipStream_t);
+                               uint16_t*, float, uint8_t*, uint64_t*, int, int, const uint16_t*, float*, int64_t,
+                               unsigned*, hipStream_t);
 hipError_t aca_pong_fused_env_step(uint16_t*, const float*, int, int64_t, const float*, const uint16_t*, const float*,
                                    int, float*, int32_t*, float*, float*, float*, int, uint32_t, float*, int32_t*,
                                    int64_t*, float*, float*, const int64_t*, uint8_t*, float*, uint8_t*, uint8_t*,
@@ -329,8 +330,11 @@ void pong_fused_step(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, Tenso
                      Tensor prev, Tensor out, Tensor reward, Tensor done, Tensor trunc, int64_t seed,
                      int64_t max_steps, Tensor hpart, int64_t planes, Tensor bfc, Tensor W1, Tensor b1, Tensor W2,
                      Tensor b2, Tensor W3, Tensor b3, Tensor y1, Tensor y2, Tensor y3, double scale,
-                     c10::optional<Tensor> shift_out, c10::optional<Tensor> stamps, bool frag) {
+                     c10::optional<Tensor> shift_out, c10::optional<Tensor> stamps, bool frag,
+                     c10::optional<Tensor> fc_w, c10::optional<Tensor> fc_out, c10::optional<Tensor> fc_cnt) {
   // frag: W2 / W3 are the fragment-ordered copies (ops/optim.py frag_order); W1 row-major
+  // fc_w / fc_out / fc_cnt: the next observation's fc product in the same launch (fragment-ordered Wfc, 14 partial
+  // planes into fc_out, the slice counters + timeout word: int32 [232], zero-initialised)
   check_env(state, t, tg, ep_ret, ep_stats, ids, reward, done, trunc);
   check_env(state_n, t_n, tg_n, ep_ret_n, ep_stats, ids, reward, done, trunc);
   for (auto* x : {&h, &Wh, &W1, &W2, &W3, &y1, &y2, &y3}) need(*x, at::kBFloat16, "pong_fused_step bf16");
@@ -366,6 +370,27 @@ void pong_fused_step(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, Tenso
                     shift_out->data_ptr() != out.data_ptr(), "pong_fused_step: shift_out shape / aliasing");
     so = shift_out->data_ptr<uint8_t>();
   }
+  const uint16_t* fcw = nullptr;
+  float* fco = nullptr;
+  int64_t fcs = 0;
+  unsigned* fcc = nullptr;
+  if (fc_w.has_value() && fc_w->defined()) {
+    TORCH_CHECK(frag && N <= 32, "pong_fused_step: the fused fc product needs the fragment copies and <= 32 envs");
+    TORCH_CHECK(fc_out.has_value() && fc_out->defined() && fc_cnt.has_value() && fc_cnt->defined(),
+                "pong_fused_step: fc_w needs fc_out and fc_cnt");
+    need(*fc_w, at::kBFloat16, "fc_w");
+    need(*fc_out, at::kFloat, "fc_out");
+    need(*fc_cnt, at::kInt, "fc_cnt");
+    TORCH_CHECK(fc_w->numel() == 3136 * 512 && fc_w->is_contiguous(), "pong_fused_step: fc_w = [3136 x 512] copy");
+    TORCH_CHECK(fc_out->numel() % 32 == 0 && fc_out->numel() / 32 >= (int64_t)N * 512 &&
+                    fc_out->data_ptr() != hpart.data_ptr(), "pong_fused_step: fc_out = 32 planes, not hpart");
+    TORCH_CHECK(fc_cnt->numel() >= 232, "pong_fused_step: fc_cnt needs 232 words");
+    TORCH_CHECK(y3.is_contiguous(), "pong_fused_step: y3 contiguous");
+    fcw = ptr<uint16_t>(*fc_w);
+    fco = ptr<float>(*fc_out);
+    fcs = fc_out->numel() / 32;
+    fcc = reinterpret_cast<unsigned*>(fc_cnt->data_ptr<int32_t>());
+  }
   check(aca_pong_fused_step(ptr<uint16_t>(h), ptr<float>(hpart), (int)planes, pstride, ptr<float>(bfc),
                             ptr<uint16_t>(Wh), ptr<float>(bh), A, ptr<float>(z), ptr<int32_t>(act), ptr<float>(logp),
                             ptr<float>(ent), ptr<float>(value), (int)key_shift, (uint32_t)pseed, ptr<float>(state),
@@ -375,7 +400,7 @@ void pong_fused_step(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, Tenso
                             ptr<uint8_t>(done), ptr<uint8_t>(trunc), (uint32_t)seed, (int)max_steps,
                             ptr<uint16_t>(W1), ptr<float>(b1), ptr<uint16_t>(W2), ptr<float>(b2), ptr<uint16_t>(W3),
                             ptr<float>(b3), ptr<uint16_t>(y1), ptr<uint16_t>(y2), ptr<uint16_t>(y3), (float)scale,
-                            so, stamps_ptr(stamps, N * 7), frag ? 1 : 0, N, cur_stream(state)),
+                            so, stamps_ptr(stamps, N * 7), frag ? 1 : 0, N, fcw, fco, fcs, fcc, cur_stream(state)),
         "pong_fused_step");
 }
 
@@ -1854,7 +1879,8 @@ TORCH_LIBRARY(acamd, m) {
         "Tensor t_n, Tensor tg_n, Tensor ep_ret_n, Tensor ep_stats, Tensor env_ids, Tensor prev, Tensor out, "
         "Tensor reward, Tensor done, Tensor truncated, int seed, int max_steps, Tensor hpart, int planes, "
         "Tensor bfc, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, Tensor y1, Tensor y2, "
-        "Tensor y3, float scale, Tensor? shift_out=None, Tensor? stamps=None, bool frag=False) -> ()");
+        "Tensor y3, float scale, Tensor? shift_out=None, Tensor? stamps=None, bool frag=False, Tensor? fc_w=None, "
+        "Tensor? fc_out=None, Tensor? fc_cnt=None) -> ()");
   m.def("pong_fused_env_step(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, Tensor logp, Tensor ent, "
         "Tensor value, int key_shift, int pseed, Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, "
         "Tensor env_ids, Tensor out, Tensor reward, Tensor done, Tensor truncated, int seed, int max_steps, "

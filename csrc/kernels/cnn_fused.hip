@@ -737,7 +737,7 @@ __device__ __forceinline__ void trunk_rows_compute(const u16* __restrict__ s_in,
                                                    const u16* __restrict__ W3, u16* __restrict__ y1g,
                                                    u16* __restrict__ y2g, u16* __restrict__ y3g, float scale,
                                                    uint64_t* __restrict__ stamps, bf16x8 (&bw2)[16],
-                                                   bf16x8 (&bw3)[18]) {
+                                                   bf16x8 (&bw3)[18], u16* __restrict__ s_y3 = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l16 = lane & 15, lg = lane >> 4;
   const int n2 = wid * 16 + l16;
@@ -871,7 +871,10 @@ __device__ __forceinline__ void trunk_rows_compute(const u16* __restrict__ s_in,
     for (int q = 0; q < 4; ++q) {
       const int row = lg * 4 + q;
       const u16 v = f2bf(fmaxf(acc[q] + bias, 0.f));
-      if (row < 7) y3g[((size_t)e * Y3_ROWS + r * 7 + row) * Y3_C + n] = v;
+      if (row < 7) {   // s_y3: the caller publishes the row itself (fused fc product)
+        if (s_y3) s_y3[row * Y3_C + n] = v;
+        else y3g[((size_t)e * Y3_ROWS + r * 7 + row) * Y3_C + n] = v;
+      }
     }
   }
   // ---------------------------------------------------------------- owned y1 / y2 rows: LDS -> global, 16-byte rows
@@ -988,6 +991,106 @@ __global__ void __launch_bounds__(T_THREADS) cnn_trunk_rows_kernel(
 //   kernel boundary less per rollout step than policy/env kernel + trunk kernel, and the new frame never makes a
 //   global round trip before conv1.
 // ------------------------------------------------------------------------------------------------------------
+// ------------------------------------------------------------------------------------------------------------
+// The next observation's fc product inside the fused step (banks of at most 32 envs, one MFMA row block): slice r
+// of the product = conv3 output row r = K range [448 r, 448 r + 448) of h = y3 Wfc. Every (env, r) workgroup
+// publishes its y3 row write-through (16-byte sc1 stores, every storing wave drained, then one relaxed agent-scope
+// add on slice r's arrival counter: cdna_hip_programming.md Guideline 16, valid-forms row 1) and waits for the N
+// arrivals of its slice (one polling lane, bounded: a timeout sets the sticky word and the health check reports
+// it). The slice's 32 units -- 16 column blocks of 32 x 2 K halves of 224 -- go to its N workgroups round-robin
+// (unit u = env, env + N, ...); wave w owns the 16 x 16 quadrant (envs 16 (w >> 1).., columns 16 (w & 1)..) of a
+// unit: 7 MFMA 16x16x32 steps, A = the published rows (sc1 loads only), B = the fragment-ordered Wfc
+// (ops/optim.py frag_order_kc, requested before the wait). Unit (nb, kh) of slice r stores its partial sums into
+// plane 2 r + kh: 14 planes, summed in plane order by the consumer (FcH2), so the product is deterministic. This
+// replaces the separate fc_rollout launch (its kernel boundary and its operand round trip) after every step.
+// ------------------------------------------------------------------------------------------------------------
+struct FcFuse {
+  const u16* Wf;     // fragment-ordered Wfc copy (k-contiguous B fragments)
+  float* out;        // partial planes [14][pstride] (row e of a plane at e * 512)
+  int64_t pstride;
+  unsigned* cnt;     // per slice r: arrivals at [32 r], departures at [32 r + 16] (own 64-byte lines); word 224:
+                     // the sticky timeout flag. Zero at the first launch; the last departure re-arms the slice.
+};
+constexpr int FCF_PLANES = 2 * TR_ROWS;
+constexpr unsigned FCF_SPIN_LIMIT = 1u << 21;
+
+__device__ __forceinline__ void fc_fused_tail(const FcFuse& f, const u16* __restrict__ s_y3, u16* __restrict__ y3g,
+                                              int e, int r, int N, uint64_t* __restrict__ stamps) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, l16 = lane & 15, lg = lane >> 4;
+  constexpr int SC1 = 16;   // buffer instruction cache-policy bits: sc1 (write-through stores, L1-bypassing loads)
+  const int ybytes = N * Y3_ROWS * Y3_C * 2;
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(y3g, 0, ybytes, 0x00020000);
+  __syncthreads();   // the conv3 row is complete in LDS
+  if (tid < 56) {    // y3 row r of env e: 7 x 64 bf16 = 56 x 16 bytes
+    const uint4 v = reinterpret_cast<const uint4*>(s_y3)[tid];
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const int off = ((e * Y3_ROWS + r * 7) * Y3_C + tid * 8) * 2;
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{v.x, v.y, v.z, v.w}, yr, off, 0, SC1);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drained
+  __syncthreads();
+  unsigned* arr = f.cnt + 32 * r;
+  if (tid == 0) __hip_atomic_fetch_add(arr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  stamp(stamps, 11);
+  // this workgroup's first unit: the B fragments do not depend on the hand-off
+  const int mq = wid >> 1, nq = wid & 1;
+  const bool active = 16 * mq < N;
+  bf16x8 bq[7];
+  auto load_b = [&](int u) {
+    const int nb = u >> 1, kh = u & 1;
+#pragma unroll
+    for (int s = 0; s < 7; ++s) {
+      const int kk = 448 * r + 224 * kh + 32 * s + 8 * lg;
+      const int kb = kk >> 4, half = (kk >> 3) & 1;
+      bq[s] = *reinterpret_cast<const bf16x8*>(f.Wf + ((size_t)((kb * 16 + nb) * 64 + half * 32 + nq * 16 + l16)) * 8);
+    }
+  };
+  if (active) load_b(e);
+  if (tid == 0) {
+    unsigned spins = 0;
+    while (__hip_atomic_load(arr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)N) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > FCF_SPIN_LIMIT) {
+        __hip_atomic_store(f.cnt + 32 * TR_ROWS, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    // departure: the last workgroup of the slice past the wait re-arms it for the next launch (stream-ordered)
+    if (__hip_atomic_fetch_add(arr + 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)N - 1u) {
+      __hip_atomic_store(arr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(arr + 16, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);   // no load of the published rows above the wait
+  stamp(stamps, 12);
+  if (!active) return;
+  const int env = min(16 * mq + l16, N - 1);
+  for (int u = e; u < 32; u += N) {
+    if (u != e) load_b(u);
+    const int nb = u >> 1, kh = u & 1;
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    bf16x8 a[7];
+    const int off0 = (env * Y3_ROWS * Y3_C + 448 * r + 224 * kh + 8 * lg) * 2;
+#pragma unroll
+    for (int s = 0; s < 7; ++s) {
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(yr, off0 + 64 * s, 0, SC1);
+      a[s] = __builtin_bit_cast(bf16x8, v);
+    }
+    __builtin_amdgcn_sched_barrier(0);   // all seven loads in flight before the first MFMA waits (one round trip)
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 7; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s], bq[s], acc, 0, 0, 0);
+    float* o = f.out + (int64_t)(2 * r + kh) * f.pstride + nb * 32 + nq * 16 + l16;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = 16 * mq + 4 * lg + q;
+      if (row < N) o[(int64_t)row * FC_UNITS] = acc[q];
+    }
+  }
+  stamp(stamps, 13);
+}
+
 struct PongNext {   // the next parity's env state buffers (written by the committing workgroup)
   float* state;
   int32_t* tsteps;
@@ -1013,9 +1116,9 @@ __device__ __forceinline__ void pong_commit_next(const PongIO& io, const PongNex
   sp[0] = q.bx; sp[1] = q.by; sp[2] = q.vx; sp[3] = q.vy; sp[4] = q.pa; sp[5] = q.po; sp[6] = q.sa; sp[7] = q.so;
 }
 
-template <int A1, bool FRAG>
+template <int A1, bool FRAG, bool FCF>
 __global__ void __launch_bounds__(T_THREADS) pong_fused_step_kernel(
-    PongIO io, PongNext nx, FcParts fc, u16* __restrict__ h, const u16* __restrict__ Wh,
+    PongIO io, PongNext nx, FcParts fc, FcFuse ff, u16* __restrict__ h, const u16* __restrict__ Wh,
     const float* __restrict__ bh, float* __restrict__ z_out, int32_t* __restrict__ act, float* __restrict__ logp,
     float* __restrict__ ent, float* __restrict__ vout, int key_shift, uint32_t pseed, const u16* __restrict__ W1,
     const float* __restrict__ b1, const u16* __restrict__ W2, const float* __restrict__ b2,
@@ -1174,8 +1277,10 @@ __global__ void __launch_bounds__(T_THREADS) pong_fused_step_kernel(
   }
   __syncthreads();
   stamp(stamps, 1);
+  // FCF: s_in (dead after conv1) stages the conv3 row, which the fused fc product publishes
   trunk_rows_compute<3, FRAG>(s_in, s_w1, s_y1, s_y2, e, r, bias1a, bias1b, bias2, bias3, W2, W3, y1g, y2g, y3g,
-                              scale, stamps, bw2, bw3);
+                              scale, stamps, bw2, bw3, FCF ? s_in : nullptr);
+  if constexpr (FCF) fc_fused_tail(ff, s_in, y3g, e, r, (int)gridDim.x / TR_ROWS, stamps);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -2069,9 +2174,17 @@ extern "C" hipError_t aca_pong_fused_step(
     int64_t* tg_n, float* ep_ret_n, float* ep_stats, const int64_t* ids, const uint8_t* prev, uint8_t* out,
     float* reward, uint8_t* done, uint8_t* trunc, uint32_t seed, int max_steps, const uint16_t* W1, const float* b1,
     const uint16_t* W2, const float* b2, const uint16_t* W3, const float* b3, uint16_t* y1, uint16_t* y2,
-    uint16_t* y3, float scale, uint8_t* shift_out, uint64_t* stamps, int frag, int N, hipStream_t stream) {
+    uint16_t* y3, float scale, uint8_t* shift_out, uint64_t* stamps, int frag, int N, const uint16_t* fc_w,
+    float* fc_out, int64_t fc_pstride, unsigned* fc_cnt, hipStream_t stream) {
   // frag: W2 / W3 are the fragment-ordered copies (W1 stays row-major: the kernel stages it through LDS)
+  // fc_w: the fragment-ordered Wfc -> the next observation's fc product in the same launch (FcFuse: 14 planes into
+  // fc_out, N <= 32, frag copies only)
   if (N <= 0) return hipSuccess;
+  const bool fcf = fc_w != nullptr;
+  if (fcf && (!frag || N > 32 || !fc_out || !fc_cnt || fc_pstride < (int64_t)N * 512 || fc_out == hpart ||
+              reinterpret_cast<uintptr_t>(fc_w) % 16 || reinterpret_cast<uintptr_t>(y3) % 16))
+    return hipErrorInvalidValue;
+  const aca::FcFuse ff{fc_w, fc_out, fc_pstride, fc_cnt};
   aca::PongIO io;
   io.state = state; io.tsteps = t; io.tglob = tg; io.ep_ret = ep_ret; io.ep_stats = ep_stats; io.env_ids = ids;
   io.prev = prev; io.out = out; io.reward = reward; io.done_out = done; io.trunc_out = trunc; io.seed = seed;
@@ -2082,14 +2195,18 @@ extern "C" hipError_t aca_pong_fused_step(
   switch (A + 1) {
 #define ACA_FUSED_CASE(A1)                                                                                       \
   case A1:                                                                                                       \
-    if (frag)                                                                                                    \
-      aca::pong_fused_step_kernel<A1, true><<<grid, aca::T_THREADS, 0, stream>>>(                                \
-          io, nx, fc, h, Wh, bh, z, act, logp, ent, value, key_shift, pseed, W1, b1, W2, b2, W3, b3, y1, y2, y3,  \
-          scale, shift_out, stamps);                                                                             \
+    if (fcf)                                                                                                     \
+      aca::pong_fused_step_kernel<A1, true, true><<<grid, aca::T_THREADS, 0, stream>>>(                          \
+          io, nx, fc, ff, h, Wh, bh, z, act, logp, ent, value, key_shift, pseed, W1, b1, W2, b2, W3, b3, y1, y2,  \
+          y3, scale, shift_out, stamps);                                                                         \
+    else if (frag)                                                                                               \
+      aca::pong_fused_step_kernel<A1, true, false><<<grid, aca::T_THREADS, 0, stream>>>(                         \
+          io, nx, fc, ff, h, Wh, bh, z, act, logp, ent, value, key_shift, pseed, W1, b1, W2, b2, W3, b3, y1, y2,  \
+          y3, scale, shift_out, stamps);                                                                         \
     else                                                                                                         \
-      aca::pong_fused_step_kernel<A1, false><<<grid, aca::T_THREADS, 0, stream>>>(                               \
-          io, nx, fc, h, Wh, bh, z, act, logp, ent, value, key_shift, pseed, W1, b1, W2, b2, W3, b3, y1, y2, y3,  \
-          scale, shift_out, stamps);                                                                             \
+      aca::pong_fused_step_kernel<A1, false, false><<<grid, aca::T_THREADS, 0, stream>>>(                        \
+          io, nx, fc, ff, h, Wh, bh, z, act, logp, ent, value, key_shift, pseed, W1, b1, W2, b2, W3, b3, y1, y2,  \
+          y3, scale, shift_out, stamps);                                                                         \
     break;
     ACA_FUSED_CASE(3) ACA_FUSED_CASE(4) ACA_FUSED_CASE(5) ACA_FUSED_CASE(6) ACA_FUSED_CASE(7)
 #undef ACA_FUSED_CASE

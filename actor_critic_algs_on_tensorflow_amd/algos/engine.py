@@ -626,6 +626,11 @@ class CNNEngine:
             return
         return self._backward_trunk(b, main, side, ev, ws, ws2)
 
+    def fc_bwd_ok(self, B):
+        """The learner's fc backward of a ``B``-row batch runs as the dedicated two-product launch (``fc_bwd.hip``,
+        ``EngineOpts.fc_bwd``: at most 256 rows)."""
+        return self.opts.fc_bwd and self.dev.type == "cuda" and 1 <= B <= 256
+
     def big_gemm_ok(self, B):
         """The fc products of a ``B``-row learner batch run on gemm_big.hip (large tiles, LDS-DMA ring)."""
         return self.big_ws is not None and 0 < self.opts.big_gemm_min_b <= B and B % 64 == 0
@@ -649,6 +654,12 @@ class CNNEngine:
             else:
                 G.gemm_big(b.y3, 3136, False, b.dh, 512, False, self.gWfc, 512, 0, 3136, 512, B, splits=2,
                            workspace=self.big_ws)
+            if stage == "tail":
+                return
+        elif stage in ("all", "tail") and self.fc_bwd_ok(B):
+            # both fc products in one launch of two job kinds (fc_bwd.hip): dWfc tiles staged in LDS, dy3 tiles
+            # straight from the k-contiguous rows of dh and Wfc
+            _native.require().fc_bwd(b.dh, self.sWfc, b.y3, b.dy3, self.gWfc)
             if stage == "tail":
                 return
         elif stage in ("all", "tail"):

@@ -41,6 +41,7 @@ class EngineOpts:
     fused_bwd: bool = True            # dy3 -> dy2 -> dy1 in one per-sample kernel (cnn_trunk_bwd)
     mb_index: bool = True             # PPO minibatches read their observations in place through a row index
     ppo_head: bool = True             # large-batch head: z, loss, dz, dh and dWh / dbh / dbfc planes in one launch
+    fc_bwd: bool = True               # learner batches of <= 256 rows: dy3 and dWfc in one dedicated launch (fc_bwd.hip)
     big_gemm_min_b: int = 1024        # learner batches from this size run the fc products on gemm_big.hip (0: never)
     wgrad_gemm: bool = True           # conv2/conv3 weight gradients: batched-position MFMA kernel (else per-sample)
     serial_bwd_min_b: int = 1024      # learner batches from this size run the backward on one stream

@@ -29,6 +29,7 @@ hipError_t aca_mlp_wgrad(const aca::WgradArgs*, hipStream_t);
 hipError_t aca_ppo_head(const aca::PpoHeadArgs*, int, hipStream_t);
 int aca_ppo_head_planes(int);
 int aca_opt_set_unroll(int);
+hipError_t aca_fc_bwd(const uint16_t*, const uint16_t*, const uint16_t*, uint16_t*, float*, int, uint64_t*, hipStream_t);
 hipError_t aca_fc_rollout(const uint16_t*, int64_t, int, const uint16_t*, int, int, float*, int64_t, int, int, int*,
                           unsigned long long*, int, hipStream_t);
 hipError_t aca_mlp_rollout(const aca::RolloutArgs*, size_t, hipStream_t);
@@ -469,6 +470,23 @@ void pong_fused_env_step(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, T
                                 ptr<uint16_t>(y3), (float)scale, so, sn, tn, tgn, ern, stamps_ptr(stamps, sn ? 2 * N : N),
                                 frag ? 1 : 0, N, cur_stream(state)),
         "pong_fused_env_step");
+}
+
+// learner fc backward at B <= 256 rows (fc_bwd.hip): dy3 = (dh Wfc^T) * (y3 > 0) bf16, dW = y3^T dh fp32 (stored)
+void fc_bwd(Tensor dh, Tensor W, Tensor y3, Tensor dy3, Tensor dW, c10::optional<Tensor> stamps) {
+  for (auto* x : {&dh, &W, &y3, &dy3}) need(*x, at::kBFloat16, "fc_bwd bf16");
+  need(dW, at::kFloat, "fc_bwd dW");
+  const int64_t B = dh.numel() / 512;
+  TORCH_CHECK(B >= 1 && B <= 256 && dh.numel() == B * 512 && y3.numel() == B * 3136 && dy3.numel() == B * 3136 &&
+                  W.numel() == 3136 * 512 && dW.numel() == 3136 * 512,
+              "fc_bwd: dh [B <= 256, 512], y3 / dy3 [B, 3136], W / dW [3136, 512]");
+  for (const Tensor* x : {&dh, &W, &y3, &dy3, &dW})
+    TORCH_CHECK(x->is_contiguous() && reinterpret_cast<uintptr_t>(x->data_ptr()) % 16 == 0,
+                "fc_bwd: contiguous 16-byte aligned buffers");
+  const int64_t nwg = 392 + ((B + 31) / 32) * 49;
+  check(aca_fc_bwd(ptr<uint16_t>(dh), ptr<uint16_t>(W), ptr<uint16_t>(y3), ptr<uint16_t>(dy3), ptr<float>(dW), (int)B,
+                   stamps_ptr(stamps, nwg / 4 + 1), cur_stream(dh)),
+        "fc_bwd");
 }
 
 // rollout fc product as split-K partial planes on the fragment-ordered Wfc copy (fc_rollout.hip); hpart holds 32
@@ -1967,6 +1985,7 @@ TORCH_LIBRARY(acamd, m) {
   m.def("ppo_head_planes(int B) -> int", &ppo_head_planes);
   m.def("opt_set_unroll(int u) -> int", &opt_set_unroll);
   m.def("fc_rollout(Tensor X, Tensor Wf, Tensor hpart, int variant, Tensor? stamps=None) -> int");
+  m.def("fc_bwd(Tensor dh, Tensor W, Tensor y3, Tensor dy3, Tensor dW, Tensor? stamps=None) -> ()");
   m.def("head_bwd(Tensor z, Tensor act, Tensor logp_old, Tensor ent_coef, Tensor kl_coef, float vf_coef, Tensor rew, "
         "Tensor val, Tensor dones, int L, int returns_mode, bool norm_adv, float gamma, float lam, Tensor ret_w, "
         "Tensor adv_w, Tensor h, Tensor Wh, Tensor dh, Tensor gWh, Tensor gbh, Tensor gbfc, Tensor stats, "
@@ -2025,6 +2044,7 @@ TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
   m.impl("cnn_trunk_fwd", &cnn_trunk_fwd);
   m.impl("fc_value", &fc_value);
   m.impl("fc_rollout", &fc_rollout);
+  m.impl("fc_bwd", &fc_bwd);
   m.impl("cnn_trunk_bwd", &cnn_trunk_bwd);
   m.impl("grad_finalize", &grad_finalize);
   m.impl("a2c_head_env", &a2c_head_env);

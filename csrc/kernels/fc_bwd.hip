@@ -1,0 +1,181 @@
+// Learner fc-layer backward at rollout-sized batches (A2C: B = T x N <= 256 rows; SURVEY §2.4 K01, backward):
+//   dy3  = (dh Wfc^T) * (y3 > 0)   [B, 3136] bf16   -- the conv trunk backward's input
+//   dWfc = y3^T dh                 [3136, 512] fp32 -- stored final into the gradient slab
+// as ONE launch of two job kinds (replaces the grouped general-GEMM launch, 21.7 us in the headline update trace,
+// profiles/r5_headline.txt, for ~1 GFLOP and ~12 MB).
+//
+// dWfc jobs (64 x 64 output tiles, 49 x 8): both operands have the reduction index b as their ROW index, so the tile's
+// y3 columns [B][64] and dh columns [B][64] are staged whole in LDS (one round of 16-byte loads, 128-byte row pieces)
+// and both MFMA operands are read with the transposing ds_read_b64_tr_b16. LDS rows are 192 bytes: the four rows of
+// a transposed read fall into four disjoint 16-bank windows (conflict-free). Wave w owns the 32 x 32 quadrant
+// (kf rows 32 (w >> 1).., n columns 32 (w & 1)..), K = B in 16-deep steps (rows past B are zero). Every output
+// element is written once: no planes, no atomics.
+// dy3 jobs (32 b x 64 kf tiles): both operands are k-contiguous rows (dh rows, Wfc rows), so every fragment goes
+// global -> VGPRs directly (16 bytes per lane, all of a wave's 16 k-steps in flight at once); wave w takes the 32
+// columns 32 (w & 1).. and the K half (w >> 1), the halves added through LDS in a fixed order, then the ReLU mask of
+// y3 and the bf16 rounding.
+// Workgroup order is XCD-grouped per job kind (contiguous tile ranges per XCD), so the tiles sharing y3 / Wfc
+// column blocks meet in one L2.
+#include "common.h"
+
+namespace aca {
+
+typedef float fb_f32x16 __attribute__((ext_vector_type(16)));
+typedef short fb_s4 __attribute__((ext_vector_type(4)));
+typedef short fb_s8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) fb_s4 fb_lds4;
+
+constexpr int FB_THREADS = 256;
+constexpr int FB_MAXB = 256;
+constexpr int FB_LD = 96;        // LDS row of the dWfc images (bf16): 128 bytes of data + 64 of padding
+constexpr int FB_KF = 3136, FB_N = 512;
+constexpr int FB_DW_TILES = (FB_KF / 64) * (FB_N / 64);   // 392
+
+struct FcBwdArgs {
+  const u16* dh;      // [B][512] bf16
+  const u16* W;       // Wfc [3136][512] bf16 (row-major shadow)
+  const u16* y3;      // [B][3136] bf16 (saved activations, ReLU outputs)
+  u16* dy3;           // [B][3136] bf16
+  float* dW;          // [3136][512] fp32
+  int B;
+  int n_dy;           // dy3 tiles: ceil(B / 32) x 49
+  uint64_t* stamps;   // diagnostics: per workgroup [entry, operands in, MFMAs done, stores issued]
+};
+
+// tile index of workgroup `id` among `T` tiles such that each XCD (id % 8 under round-robin dispatch) runs one
+// contiguous range of tiles
+__device__ __forceinline__ int fb_xcd_tile(int id, int T) {
+  const int x = id & 7, s = id >> 3, q = T >> 3, rem = T & 7;
+  return x * q + min(x, rem) + s;
+}
+
+__device__ __forceinline__ void fb_stamp(uint64_t* st, int slot) {
+  if (st && threadIdx.x == 0) st[(size_t)blockIdx.x * 4 + slot] = __builtin_amdgcn_s_memrealtime();
+}
+
+__device__ __forceinline__ bf16x8 fb_tr8(const u16* lo, const u16* hi) {
+  const fb_s4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((fb_lds4*)(lo));
+  const fb_s4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((fb_lds4*)(hi));
+  const fb_s8 v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__device__ __forceinline__ void fb_dw_job(const FcBwdArgs& a, int t, u16* smem) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int B = a.B, Bp = (B + 15) & ~15, KS = Bp >> 4;
+  const int i = t >> 3, j = t & 7;   // kf block of 64, n block of 64
+  u16* sY = smem;                    // [Bp][FB_LD]: y3[b][64 i ..]
+  u16* sD = smem + Bp * FB_LD;       // [Bp][FB_LD]: dh[b][64 j ..]
+  // ---- staging: Bp rows x 8 chunks of 16 bytes per image, every load of the thread in flight at once
+  const int nch = Bp * 8;            // chunks per image (<= 2048)
+  uint4 vy[8], vd[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {   // branch-free (clamped rows): a guarded load kept the arrays in scratch
+    const int c = tid + u * FB_THREADS;
+    const int b = min(c >> 3, B - 1), q = c & 7;
+    vy[u] = *reinterpret_cast<const uint4*>(a.y3 + (size_t)b * FB_KF + 64 * i + 8 * q);
+    vd[u] = *reinterpret_cast<const uint4*>(a.dh + (size_t)b * FB_N + 64 * j + 8 * q);
+  }
+  fb_stamp(a.stamps, 1);
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int c = tid + u * FB_THREADS;
+    if (c < nch) {   // rows past B: zero (masked word by word; a select of whole uint4s went through scratch)
+      const int b = c >> 3, q = c & 7;
+      const unsigned m = b < B ? 0xFFFFFFFFu : 0u;
+      *reinterpret_cast<uint4*>(sY + b * FB_LD + 8 * q) = make_uint4(vy[u].x & m, vy[u].y & m, vy[u].z & m, vy[u].w & m);
+      *reinterpret_cast<uint4*>(sD + b * FB_LD + 8 * q) = make_uint4(vd[u].x & m, vd[u].y & m, vd[u].z & m, vd[u].w & m);
+    }
+  }
+  __syncthreads();
+  // ---- MFMAs: wave w -> quadrant (kf rows 32 mq.., n columns 32 nq..); transposing reads of both images
+  const int mq = w >> 1, nq = w & 1;
+  const int gl = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3;
+  const int acol = 32 * mq + 16 * (gl & 1) + 4 * p4, bcol = 32 * nq + 16 * (gl & 1) + 4 * p4;
+  const int khalf = 8 * (gl >> 1);
+  fb_f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  for (int ks = 0; ks < KS; ++ks) {
+    const int kb = 16 * ks + khalf;
+    const bf16x8 af = fb_tr8(sY + (kb + q) * FB_LD + acol, sY + (kb + 4 + q) * FB_LD + acol);
+    const bf16x8 bf = fb_tr8(sD + (kb + q) * FB_LD + bcol, sD + (kb + 4 + q) * FB_LD + bcol);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, acc, 0, 0, 0);
+  }
+  fb_stamp(a.stamps, 2);
+  // ---- the quadrant, written once: 32 lanes per row x 4 bytes
+  const int col = lane & 31, rh = 4 * (lane >> 5);
+  float* dst = a.dW + (size_t)(64 * i + 32 * mq) * FB_N + 64 * j + 32 * nq + col;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) dst[(size_t)((r & 3) + 8 * (r >> 2) + rh) * FB_N] = acc[r];
+}
+
+__device__ __forceinline__ void fb_dy_job(const FcBwdArgs& a, int t, float* red) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int B = a.B, nbb = (B + 31) >> 5;
+  const int jb = t / nbb, ib = t - jb * nbb;   // kf block of 64, b block of 32
+  const int ch = w & 1, kh = w >> 1;
+  const int ra = min(32 * ib + (lane & 31), B - 1);
+  const int kf = 64 * jb + 32 * ch + (lane & 31);
+  const int k0 = 256 * kh + 8 * (lane >> 5);
+  const u16* pa = a.dh + (size_t)ra * FB_N + k0;
+  const u16* pb = a.W + (size_t)kf * FB_N + k0;
+  bf16x8 av[16], bv[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    av[s] = *reinterpret_cast<const bf16x8*>(pa + 16 * s);
+    bv[s] = *reinterpret_cast<const bf16x8*>(pb + 16 * s);
+  }
+  __builtin_amdgcn_sched_barrier(0);   // all 32 fragment loads in flight before the first MFMA waits
+  fb_stamp(a.stamps, 1);
+  fb_f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+  for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[s], bv[s], acc, 0, 0, 0);
+  fb_stamp(a.stamps, 2);
+  // K halves: the upper half's accumulators through LDS, added to the lower half's (fixed order)
+  if (kh == 1)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[(ch * 16 + r) * 64 + lane] = acc[r];
+  __syncthreads();
+  if (kh == 1) return;
+  const int col = 64 * jb + 32 * ch + (lane & 31), rh = 4 * (lane >> 5);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int b = 32 * ib + (r & 3) + 8 * (r >> 2) + rh;
+    const float v = acc[r] + red[(ch * 16 + r) * 64 + lane];
+    if (b < B) {
+      const size_t o = (size_t)b * FB_KF + col;
+      a.dy3[o] = bf2f(a.y3[o]) > 0.f ? f2bf(v) : (u16)0;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(FB_THREADS, 2) fc_bwd_kernel(FcBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) u16 fb_smem[];
+  fb_stamp(a.stamps, 0);
+  const int id = blockIdx.x;
+  if (id < FB_DW_TILES) {
+    fb_dw_job(a, fb_xcd_tile(id, FB_DW_TILES), fb_smem);
+  } else {
+    fb_dy_job(a, fb_xcd_tile(id - FB_DW_TILES, a.n_dy), reinterpret_cast<float*>(fb_smem));
+  }
+  fb_stamp(a.stamps, 3);
+}
+
+}  // namespace aca
+
+// dh [B][512], W = Wfc [3136][512], y3 [B][3136] bf16 -> dy3 [B][3136] bf16, dW [3136][512] fp32; 1 <= B <= 256,
+// every pointer 16-byte aligned, the row strides dense.
+extern "C" hipError_t aca_fc_bwd(const uint16_t* dh, const uint16_t* W, const uint16_t* y3, uint16_t* dy3, float* dW,
+                                 int B, uint64_t* stamps, hipStream_t stream) {
+  if (B < 1 || B > aca::FB_MAXB) return hipErrorInvalidValue;
+  for (const void* p : {(const void*)dh, (const void*)W, (const void*)y3, (const void*)dy3, (const void*)dW})
+    if (!p || reinterpret_cast<uintptr_t>(p) % 16) return hipErrorInvalidValue;
+  aca::FcBwdArgs a{dh, W, y3, dy3, dW, B, ((B + 31) / 32) * (aca::FB_KF / 64), stamps};
+  const int Bp = (B + 15) & ~15;
+  const size_t lds = std::max((size_t)2 * Bp * aca::FB_LD * 2, (size_t)2 * 16 * 64 * 4);
+  aca::fc_bwd_kernel<<<aca::FB_DW_TILES + a.n_dy, aca::FB_THREADS, lds, stream>>>(a);
+  return hipGetLastError();
+}

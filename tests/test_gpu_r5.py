@@ -229,3 +229,25 @@ def test_fused_step_fc_update_tracks_separate_fc_launch(cuda):
     d0, s0, a0 = res[False]
     assert float((a1 != a0).float().mean()) < 0.05
     assert (d0 - d1).norm() / d0.norm() < 5e-2, float((d0 - d1).norm() / d0.norm())
+
+
+@pytest.mark.parametrize("B", [160, 7, 256, 33, 1])
+def test_fc_bwd_matches_fp64(cuda, B):
+    """fc_bwd.hip: dWfc = y3^T dh (fp32, every element stored) and dy3 = (dh Wfc^T) * (y3 > 0) (bf16) against fp64
+    products of the same bf16 operands."""
+    from actor_critic_algs_on_tensorflow_amd import _native
+    ops = _native.require()
+    g = torch.Generator(device="cpu").manual_seed(B)
+    dh = (torch.randn(B, 512, generator=g) * 0.1).to(torch.bfloat16).to(cuda)
+    W = (torch.randn(3136, 512, generator=g) * 0.05).to(torch.bfloat16).to(cuda)
+    y3 = torch.relu(torch.randn(B, 3136, generator=g)).to(torch.bfloat16).to(cuda)
+    dy3 = torch.full((B, 3136), float("nan"), dtype=torch.bfloat16, device=cuda)
+    dW = torch.full((3136, 512), float("nan"), device=cuda)
+    ops.fc_bwd(dh, W, y3, dy3, dW)
+    torch.cuda.synchronize()
+    ref_w = y3.double().t() @ dh.double()
+    assert float((dW.double() - ref_w).abs().max() / ref_w.abs().max()) < 1e-5
+    ref_d = (dh.double() @ W.double().t()) * (y3.double() > 0)
+    err = (dy3.double() - ref_d).abs()
+    assert bool((err <= ref_d.abs() * 2.0 ** -8 + 1e-6).all()), float(err.max())
+    assert bool((dy3[y3 == 0] == 0).all())

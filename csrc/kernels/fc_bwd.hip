@@ -10,10 +10,11 @@
 // a transposed read fall into four disjoint 16-bank windows (conflict-free). Wave w owns the 32 x 32 quadrant
 // (kf rows 32 (w >> 1).., n columns 32 (w & 1)..), K = B in 16-deep steps (rows past B are zero). Every output
 // element is written once: no planes, no atomics.
-// dy3 jobs (32 b x 64 kf tiles): both operands are k-contiguous rows (dh rows, Wfc rows), so every fragment goes
-// global -> VGPRs directly (16 bytes per lane, all of a wave's 16 k-steps in flight at once); wave w takes the 32
-// columns 32 (w & 1).. and the K half (w >> 1), the halves added through LDS in a fixed order, then the ReLU mask of
-// y3 and the bf16 rounding.
+// dy3 jobs (32 b x 32 kf tiles): both operands are k-contiguous rows (32 dh rows, 32 Wfc rows of 1 KB), staged in
+// LDS by whole-line loads (fragment-shaped global loads -- 32 rows x 32 bytes per wave instruction -- issued at a
+// fraction of the line rate: 1.4 us of issue for 64 KB) and read back as MFMA fragments by ds_read_b128; wave w takes
+// the K quarter w, the quarters added through LDS in wave order, then the ReLU mask of y3 (requested with the
+// operands) and the bf16 rounding.
 // Workgroup order is XCD-grouped per job kind (contiguous tile ranges per XCD), so the tiles sharing y3 / Wfc
 // column blocks meet in one L2.
 #include "common.h"
@@ -30,6 +31,7 @@ constexpr int FB_MAXB = 256;
 constexpr int FB_LD = 96;        // LDS row of the dWfc images (bf16): 128 bytes of data + 64 of padding
 constexpr int FB_KF = 3136, FB_N = 512;
 constexpr int FB_DW_TILES = (FB_KF / 64) * (FB_N / 64);   // 392
+constexpr int FB_LDK = FB_N + 8;  // LDS row of the dy3 operand blocks (bf16): 1 KB + 16 bytes (conflict-free b128 reads)
 
 struct FcBwdArgs {
   const u16* dh;      // [B][512] bf16
@@ -38,7 +40,7 @@ struct FcBwdArgs {
   u16* dy3;           // [B][3136] bf16
   float* dW;          // [3136][512] fp32
   int B;
-  int n_dy;           // dy3 tiles: ceil(B / 32) x 49
+  int n_dy;           // dy3 tiles: ceil(B / 32) x 98
   uint64_t* stamps;   // diagnostics: per workgroup [entry, operands in, MFMAs done, stores issued]
 };
 
@@ -110,45 +112,59 @@ __device__ __forceinline__ void fb_dw_job(const FcBwdArgs& a, int t, u16* smem) 
   for (int r = 0; r < 16; ++r) dst[(size_t)((r & 3) + 8 * (r >> 2) + rh) * FB_N] = acc[r];
 }
 
-__device__ __forceinline__ void fb_dy_job(const FcBwdArgs& a, int t, float* red) {
+__device__ __forceinline__ void fb_dy_job(const FcBwdArgs& a, int t, u16* smem) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int B = a.B, nbb = (B + 31) >> 5;
-  const int jb = t / nbb, ib = t - jb * nbb;   // kf block of 64, b block of 32
-  const int ch = w & 1, kh = w >> 1;
-  const int ra = min(32 * ib + (lane & 31), B - 1);
-  const int kf = 64 * jb + 32 * ch + (lane & 31);
-  const int k0 = 256 * kh + 8 * (lane >> 5);
-  const u16* pa = a.dh + (size_t)ra * FB_N + k0;
-  const u16* pb = a.W + (size_t)kf * FB_N + k0;
-  bf16x8 av[16], bv[16];
+  const int jb = t / nbb, ib = t - jb * nbb;   // kf block of 32, b block of 32
+  u16* sA = smem;                              // [32][FB_LDK]: dh rows 32 ib ..
+  u16* sB = smem + 32 * FB_LDK;                // [32][FB_LDK]: Wfc rows 32 jb ..
+  // ---- staging: two 32 x 1 KB row blocks, whole 128-byte lines per 8 lanes, every load in flight at once
+  uint4 va[8], vb[8];
 #pragma unroll
-  for (int s = 0; s < 16; ++s) {
-    av[s] = *reinterpret_cast<const bf16x8*>(pa + 16 * s);
-    bv[s] = *reinterpret_cast<const bf16x8*>(pb + 16 * s);
+  for (int u = 0; u < 8; ++u) {
+    const int c = tid + u * FB_THREADS, r = c >> 6, q = c & 63;   // row, 16-byte chunk
+    va[u] = *reinterpret_cast<const uint4*>(a.dh + (size_t)min(32 * ib + r, B - 1) * FB_N + 8 * q);
+    vb[u] = *reinterpret_cast<const uint4*>(a.W + (size_t)(32 * jb + r) * FB_N + 8 * q);
   }
-  __builtin_amdgcn_sched_barrier(0);   // all 32 fragment loads in flight before the first MFMA waits
+  // the ReLU mask of this lane's 16 outputs, requested with the operands (used by wave 0)
+  const int col = 32 * jb + (lane & 31), rh = 4 * (lane >> 5);
+  const u16* ym = a.y3 + col;
+  u16 mk[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) mk[r] = ym[(size_t)min(32 * ib + (r & 3) + 8 * (r >> 2) + rh, B - 1) * FB_KF];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int c = tid + u * FB_THREADS, r = c >> 6, q = c & 63;
+    *reinterpret_cast<uint4*>(sA + r * FB_LDK + 8 * q) = va[u];
+    *reinterpret_cast<uint4*>(sB + r * FB_LDK + 8 * q) = vb[u];
+  }
   fb_stamp(a.stamps, 1);
+  __syncthreads();
+  // ---- wave w: K quarter [128 w, 128 w + 128), 8 steps of 32x32x16 (fragments by ds_read_b128)
   fb_f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  const int ro = (lane & 31) * FB_LDK + 128 * w + 8 * (lane >> 5);
 #pragma unroll
-  for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[s], bv[s], acc, 0, 0, 0);
+  for (int s = 0; s < 8; ++s) {
+    const bf16x8 af = *reinterpret_cast<const bf16x8*>(sA + ro + 16 * s);
+    const bf16x8 bf = *reinterpret_cast<const bf16x8*>(sB + ro + 16 * s);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, acc, 0, 0, 0);
+  }
   fb_stamp(a.stamps, 2);
-  // K halves: the upper half's accumulators through LDS, added to the lower half's (fixed order)
-  if (kh == 1)
+  // ---- K quarters summed through LDS in wave order (deterministic), then the mask and the bf16 rounding
+  __syncthreads();   // every wave is past its operand reads
+  float* red = reinterpret_cast<float*>(smem);
+  if (w > 0)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) red[(ch * 16 + r) * 64 + lane] = acc[r];
+    for (int r = 0; r < 16; ++r) red[((w - 1) * 16 + r) * 64 + lane] = acc[r];
   __syncthreads();
-  if (kh == 1) return;
-  const int col = 64 * jb + 32 * ch + (lane & 31), rh = 4 * (lane >> 5);
+  if (w > 0) return;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int b = 32 * ib + (r & 3) + 8 * (r >> 2) + rh;
-    const float v = acc[r] + red[(ch * 16 + r) * 64 + lane];
-    if (b < B) {
-      const size_t o = (size_t)b * FB_KF + col;
-      a.dy3[o] = bf2f(a.y3[o]) > 0.f ? f2bf(v) : (u16)0;
-    }
+    const float v = ((acc[r] + red[r * 64 + lane]) + red[(16 + r) * 64 + lane]) + red[(32 + r) * 64 + lane];
+    if (b < B) a.dy3[(size_t)b * FB_KF + col] = bf2f(mk[r]) > 0.f ? f2bf(v) : (u16)0;
   }
 }
 
@@ -159,7 +175,7 @@ __global__ void __launch_bounds__(FB_THREADS, 2) fc_bwd_kernel(FcBwdArgs a) {
   if (id < FB_DW_TILES) {
     fb_dw_job(a, fb_xcd_tile(id, FB_DW_TILES), fb_smem);
   } else {
-    fb_dy_job(a, fb_xcd_tile(id - FB_DW_TILES, a.n_dy), reinterpret_cast<float*>(fb_smem));
+    fb_dy_job(a, fb_xcd_tile(id - FB_DW_TILES, a.n_dy), fb_smem);
   }
   fb_stamp(a.stamps, 3);
 }
@@ -173,9 +189,9 @@ extern "C" hipError_t aca_fc_bwd(const uint16_t* dh, const uint16_t* W, const ui
   if (B < 1 || B > aca::FB_MAXB) return hipErrorInvalidValue;
   for (const void* p : {(const void*)dh, (const void*)W, (const void*)y3, (const void*)dy3, (const void*)dW})
     if (!p || reinterpret_cast<uintptr_t>(p) % 16) return hipErrorInvalidValue;
-  aca::FcBwdArgs a{dh, W, y3, dy3, dW, B, ((B + 31) / 32) * (aca::FB_KF / 64), stamps};
+  aca::FcBwdArgs a{dh, W, y3, dy3, dW, B, ((B + 31) / 32) * (aca::FB_KF / 32), stamps};
   const int Bp = (B + 15) & ~15;
-  const size_t lds = std::max((size_t)2 * Bp * aca::FB_LD * 2, (size_t)2 * 16 * 64 * 4);
+  const size_t lds = std::max((size_t)2 * Bp * aca::FB_LD * 2, (size_t)2 * 32 * aca::FB_LDK * 2);
   aca::fc_bwd_kernel<<<aca::FB_DW_TILES + a.n_dy, aca::FB_THREADS, lds, stream>>>(a);
   return hipGetLastError();
 }

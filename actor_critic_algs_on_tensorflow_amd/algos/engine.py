@@ -424,6 +424,10 @@ class CNNEngine:
         self._cur_planes[name] = S
 
     def _trunk_bwd(self, b):
+        if self.opts.trunk_bwd_v2:   # trunk_bwd2.hip: at most trunk_bwd_persist workgroups, walking the samples
+            _native.require().cnn_trunk_bwd2(b.dy3, self.sW3, b.y2, self.sW2, b.y1, b.dy2, b.dy1, b.biasp, None,
+                                             self.trunk_bwd_persist)
+            return
         persist = self.trunk_bwd_persist if b.B >= self.trunk_bwd_persist_min_b else 0
         _native.require().cnn_trunk_bwd(b.dy3, self.sW3, b.y2, self.sW2, b.y1, b.dy2, b.dy1, b.biasp, None, persist)
 

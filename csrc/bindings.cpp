@@ -136,6 +136,8 @@ hipError_t aca_a2c_head(const float*, const int32_t*, const float*, const float*
                         const float*, int, int64_t, const float*, const float*, unsigned int*, uint64_t*, hipStream_t);
 hipError_t aca_cnn_trunk_bwd(const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*,
                              uint16_t*, uint16_t*, float*, int, uint64_t*, int, hipStream_t);
+hipError_t aca_cnn_trunk_bwd2(const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*,
+                              uint16_t*, uint16_t*, float*, int, uint64_t*, int, hipStream_t);
 hipError_t aca_cnn_trunk_rows(const uint8_t*, const uint16_t*, const float*, const uint16_t*, const float*,
                               const uint16_t*, const float*, uint16_t*, uint16_t*, uint16_t*, int, float, uint8_t*,
                               uint8_t*, uint64_t*, int, int, hipStream_t);
@@ -1586,6 +1588,25 @@ void cnn_trunk_bwd(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tenso
         "cnn_trunk_bwd");
 }
 
+// v2 of the fused data-gradient chain (trunk_bwd2.hip: 32x32x16 MFMAs, register blocking, weights staged once per
+// workgroup); max_wg > 0: at most that many workgroups walking the samples, else one per sample
+void cnn_trunk_bwd2(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tensor dy2, Tensor dy1, Tensor biasp,
+                    c10::optional<Tensor> stamps, int64_t max_wg) {
+  for (auto* t : {&dy3, &W3, &y2, &W2, &y1, &dy2, &dy1}) need(*t, at::kBFloat16, "trunk_bwd2 bf16 operand");
+  need(biasp, at::kFloat, "biasp");
+  TORCH_CHECK(dy3.numel() % (49 * 64) == 0, "cnn_trunk_bwd2: dy3 must be [B*49, 64]");
+  const int64_t B = dy3.numel() / (49 * 64);
+  TORCH_CHECK(W3.numel() == 64 * 576 && W2.numel() == 64 * 512, "cnn_trunk_bwd2: weights must be conv3 / conv2");
+  TORCH_CHECK(y2.numel() >= B * 81 * 64 && y1.numel() >= B * 400 * 32 && dy2.numel() >= B * 81 * 64 &&
+                  dy1.numel() >= B * 400 * 32 && biasp.numel() >= B * 160,
+              "cnn_trunk_bwd2: buffers too small");
+  const int64_t grid = max_wg > 0 && max_wg < B ? max_wg : B;
+  check(aca_cnn_trunk_bwd2(ptr<uint16_t>(dy3), ptr<uint16_t>(W3), ptr<uint16_t>(y2), ptr<uint16_t>(W2),
+                           ptr<uint16_t>(y1), ptr<uint16_t>(dy2), ptr<uint16_t>(dy1), ptr<float>(biasp), (int)B,
+                           stamps_ptr(stamps, grid), (int)max_wg, cur_stream(dy3)),
+        "cnn_trunk_bwd2");
+}
+
 // Gradient finaliser (optim.hip grad_finalize_kernel): jobs = device int64 [njobs, 8] (dst, src, n, stride, S,
 // vec, 0, 0) built by ops/optim.py finalize_jobs; writes dst = sum of S planes where src != 0 and the
 // SUMSQ_PARTS sum-of-squares partials.
@@ -1972,6 +1993,8 @@ TORCH_LIBRARY(acamd, m) {
         "Tensor? copy_out=None, Tensor? obs_idx=None) -> ()");
   m.def("cnn_trunk_bwd(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tensor dy2, Tensor dy1, "
         "Tensor biasp, Tensor? stamps=None, int persist=0) -> ()");
+  m.def("cnn_trunk_bwd2(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tensor dy2, Tensor dy1, "
+        "Tensor biasp, Tensor? stamps=None, int max_wg=0) -> ()");
   m.def("grad_finalize(Tensor jobs, Tensor partial, Tensor? spart=None, int B=0, Tensor? ent_coef=None, "
         "Tensor? kl_coef=None, Tensor? stats=None) -> ()");
   m.def("a2c_head_env(Tensor z, Tensor act, Tensor logp_old, Tensor ent_coef, Tensor kl_coef, float vf_coef, "
@@ -2046,6 +2069,7 @@ TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
   m.impl("fc_rollout", &fc_rollout);
   m.impl("fc_bwd", &fc_bwd);
   m.impl("cnn_trunk_bwd", &cnn_trunk_bwd);
+  m.impl("cnn_trunk_bwd2", &cnn_trunk_bwd2);
   m.impl("grad_finalize", &grad_finalize);
   m.impl("a2c_head_env", &a2c_head_env);
   m.impl("ppo_head", &ppo_head);

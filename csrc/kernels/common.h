@@ -310,6 +310,25 @@ __device__ __forceinline__ void grid_records_sum(const double* part, int stride,
   block_sum_multi<N>(v, sh);
 }
 
+// XCD-grouped work order: workgroups are dealt round-robin over the 8 XCDs (block b on XCD b % 8, observed, not
+// guaranteed: a wrong guess costs locality, never correctness), so logical index xcd_remap(b, T) gives every XCD ONE
+// contiguous range of the T work items -- neighbouring items (tiles of one K split, sharing their operand lines) meet
+// in one L2 instead of being fetched by every XCD. A bijection on [0, T).
+__device__ __forceinline__ int xcd_remap(int b, int T) {
+  const int x = b & 7, s = b >> 3, q = T >> 3, rem = T & 7;
+  return x * q + min(x, rem) + s;
+}
+
+// The same in chunks of g items: chunk c of g consecutive items runs on XCD c % 8, so a chunk (the tiles of one K
+// split) shares one L2 while the chunks of every product are spread over all XCDs (balance). The tail past the last
+// full round of 8 chunks keeps the plain order. A bijection on [0, T).
+__device__ __forceinline__ int xcd_chunk_remap(int b, int T, int g) {
+  const int full = (T / (8 * g)) * 8 * g;
+  if (b >= full) return b;
+  const int x = b & 7, s = b >> 3;
+  return (x + 8 * (s / g)) * g + s % g;
+}
+
 // Last-arriver ticket (Guideline 16 counter form): every wave drains its stores, the block releases at agent
 // scope and takes a ticket; returns true in every thread of the block that arrived last. The caller then reads
 // the other blocks' results with plain loads (this function already performed the acquire).

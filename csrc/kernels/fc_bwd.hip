@@ -47,13 +47,6 @@ struct FcBwdArgs {
   uint64_t* stamps;   // diagnostics: per workgroup [entry, operands in, MFMAs done, stores issued]
 };
 
-// tile index of workgroup `id` among `T` tiles such that each XCD (id % 8 under round-robin dispatch) runs one
-// contiguous range of tiles
-__device__ __forceinline__ int fb_xcd_tile(int id, int T) {
-  const int x = id & 7, s = id >> 3, q = T >> 3, rem = T & 7;
-  return x * q + min(x, rem) + s;
-}
-
 __device__ __forceinline__ void fb_stamp(uint64_t* st, int slot) {
   if (st && threadIdx.x == 0) st[(size_t)blockIdx.x * 4 + slot] = __builtin_amdgcn_s_memrealtime();
 }
@@ -191,9 +184,9 @@ __global__ void __launch_bounds__(FB_THREADS, 4) fc_bwd_kernel(FcBwdArgs a) {
   fb_stamp(a.stamps, 0);
   const int id = blockIdx.x;
   if (id < FB_DW_TILES) {
-    fb_dw_job(a, fb_xcd_tile(id, FB_DW_TILES), fb_smem);
+    fb_dw_job(a, xcd_remap(id, FB_DW_TILES), fb_smem);
   } else {
-    fb_dy_job(a, fb_xcd_tile(id - FB_DW_TILES, a.n_dy), fb_smem);
+    fb_dy_job(a, xcd_remap(id - FB_DW_TILES, a.n_dy), fb_smem);
   }
   fb_stamp(a.stamps, 3);
 }

@@ -584,7 +584,9 @@ template <int BM, int BN, int BK, bool A_K, bool B_K, int AG, int BG, bool VEC>
 __global__ void __launch_bounds__(256) gemm_kernel(GemmParams P) {
   __shared__ __attribute__((aligned(16))) u16 smem[GemmSmem<BM, BN, BK, A_K, B_K>::ELEMS];
   __shared__ int sh_flag;
-  gemm_block<BM, BN, BK, A_K, B_K, AG, BG, VEC>(P, blockIdx.x, blockIdx.z, gridDim.x, smem, sh_flag);
+  // XCD-grouped order: the tiles of one K split (which share their operand rows) run on one XCD
+  const int L = xcd_chunk_remap(blockIdx.z * gridDim.x + blockIdx.x, gridDim.x * gridDim.z, gridDim.x);
+  gemm_block<BM, BN, BK, A_K, B_K, AG, BG, VEC>(P, L % gridDim.x, L / gridDim.x, gridDim.x, smem, sh_flag);
 }
 
 // ---------------------------------------------------------------------------------------------- grouped launch
@@ -617,7 +619,11 @@ __global__ void __launch_bounds__(256) gemm_group_kernel(GemmGroupArgs G) {
   int k = 0;
   if (G.n > 1 && b >= G.start[1]) k = 1;
   if (G.n > 2 && b >= G.start[2]) k = 2;
-  const int local = b - G.start[k], tiles = G.tiles[k];
+  // XCD-grouped order per product: the tiles of one K split (sharing their operand rows: the conv weight gradients'
+  // input pixels) run on one XCD, the splits rotate over the XCDs (profiles/r5_pong_pmc.txt: 53 MB fetched for
+  // ~17 MB of operands in plain order)
+  const int tiles = G.tiles[k];
+  const int local = xcd_chunk_remap(b - G.start[k], G.start[k + 1] - G.start[k], tiles);
   if (G.cfg[k] == 0) CA::run(G.p[k], local % tiles, local / tiles, tiles, smem, sh_flag);
   else CB::run(G.p[k], local % tiles, local / tiles, tiles, smem, sh_flag);
 }

@@ -251,3 +251,45 @@ def test_fc_bwd_matches_fp64(cuda, B):
     err = (dy3.double() - ref_d).abs()
     assert bool((err <= ref_d.abs() * 2.0 ** -8 + 1e-6).all()), float(err.max())
     assert bool((dy3[y3 == 0] == 0).all())
+
+
+@pytest.mark.parametrize("B", [1, 5, 160, 700])
+def test_trunk_bwd2_matches_conv_transpose(cuda, B):
+    """trunk_bwd2.hip (32x32x16 MFMAs, weights staged once per workgroup) vs fp32 torch conv_transpose2d on the same
+    bf16 inputs: dy2 = tconv(dy3, W3) * (y2 > 0), dy1 = tconv(dy2_bf16, W2) * (y1 > 0), the per-sample bias-gradient
+    partials; bitwise reproducible and identical for every workgroup count (one per sample, 3, 256 walking)."""
+    import torch.nn.functional as F
+    from actor_critic_algs_on_tensorflow_amd import _native
+    ops = _native.require()
+    g = torch.Generator(device="cpu").manual_seed(B + 7)
+    dy3 = (torch.randn(B, 7, 7, 64, generator=g) * (torch.rand(B, 7, 7, 64, generator=g) > 0.4)).to(torch.bfloat16)
+    W3 = (torch.randn(64, 3, 3, 64, generator=g) * 0.05).to(torch.bfloat16)        # OHWI
+    W2 = (torch.randn(64, 4, 4, 32, generator=g) * 0.05).to(torch.bfloat16)
+    y2 = (torch.rand(B, 9, 9, 64, generator=g) - 0.3).clamp(min=0).to(torch.bfloat16)
+    y1 = (torch.rand(B, 20, 20, 32, generator=g) - 0.3).clamp(min=0).to(torch.bfloat16)
+    dev = [t.to(cuda) for t in (dy3, W3, y2, W2, y1)]
+    args = (dev[0].reshape(B * 49, 64), dev[1].reshape(64, 576), dev[2].reshape(B * 81, 64), dev[3].reshape(64, 512),
+            dev[4].reshape(B * 400, 32))
+    res = []
+    for max_wg in (0, 3, 256, 0):
+        dy2 = torch.full((B * 81, 64), float("nan"), dtype=torch.bfloat16, device=cuda)
+        dy1 = torch.full((B * 400, 32), float("nan"), dtype=torch.bfloat16, device=cuda)
+        bp = torch.full((B, 160), float("nan"), device=cuda)
+        ops.cnn_trunk_bwd2(*args, dy2, dy1, bp, None, max_wg)
+        torch.cuda.synchronize()
+        res.append((dy2.view(torch.int16).clone(), dy1.view(torch.int16).clone(), bp.clone()))
+    for r in res[1:]:
+        assert all(torch.equal(a, b) for a, b in zip(res[0], r))
+    dy2, dy1, bp = res[0][0].view(torch.bfloat16), res[0][1].view(torch.bfloat16), res[0][2]
+    r2 = F.conv_transpose2d(dy3.float().permute(0, 3, 1, 2), W3.float().permute(0, 3, 1, 2), stride=1)
+    r2 = r2.permute(0, 2, 3, 1) * (y2.float() > 0)
+    got2 = dy2.float().cpu().view(B, 9, 9, 64)
+    assert torch.allclose(got2, r2, rtol=2e-2, atol=2e-2), (got2 - r2).abs().max()
+    r1 = F.conv_transpose2d(got2.permute(0, 3, 1, 2), W2.float().permute(0, 3, 1, 2), stride=2)
+    r1 = r1.permute(0, 2, 3, 1) * (y1.float() > 0)
+    got1 = dy1.float().cpu().view(B, 20, 20, 32)
+    assert torch.allclose(got1, r1, rtol=2e-2, atol=2e-2), (got1 - r1).abs().max()
+    bpc = bp.cpu()
+    assert torch.allclose(bpc[:, :64], dy3.float().sum((1, 2)), rtol=1e-4, atol=1e-4)
+    assert torch.allclose(bpc[:, 64:128], got2.sum((1, 2)), rtol=1e-4, atol=1e-3)
+    assert torch.allclose(bpc[:, 128:], got1.sum((1, 2)), rtol=1e-4, atol=1e-3)

@@ -334,7 +334,11 @@ __global__ void __launch_bounds__(512) conv_wgrad_gemm_kernel(const u16* __restr
   constexpr int T = 512;
   constexpr int NPOS = OH * OW, NCOL = KS * KS * C;
   constexpr int GP = SB * NPOS, KST = (GP + 15) / 16, KP = KST * 16;
-  constexpr int LDI = C + 8, LDD = 72, IMG_E = H * W * LDI;
+  // LDS rows: the 4 rows of a transposing read (positions kb + q) land in 4 disjoint 16-bank windows -- dy rows of
+  // 192 bytes, image pixels of 96 bytes at stride 2 / 192 bytes at stride 1 (S x pixel bytes = 64 mod 256 or 192);
+  // the +8 / 144-byte layouts read 2x / 1.9x the ideal cycles (tests/test_lds_layouts_cpu.py models both reads)
+  constexpr int LDI = S == 2 ? C + 16 : C + 32, LDD = 96, IMG_E = H * W * LDI;
+  static_assert((S * LDI * 2) % 256 == 64 || (S * LDI * 2) % 256 == 192, "conflict-free image rows");
   constexpr int NT = NCOL / 32;                         // n tiles of 32
   constexpr int TPW = (NT + 3) / 4;                     // n tiles per wave (wave pairs share an n tile set)
   constexpr int CPP = C / 8;                            // 16-byte chunks per pixel

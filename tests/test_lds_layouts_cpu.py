@@ -276,3 +276,50 @@ def test_trunk_bwd2_reads_are_conflict_free():
                         r, col = row0 + 8 * (gl >> 1) + q + hi, col0 + 16 * (gl & 1) + 4 * p
                         addr.append((r * ld + (((col >> 3) ^ sw(r)) << 3) + (col & 7)) * 2)
                     assert cycles([[addr[x] for x in g] for g in GTR], 2, 64) == 2, (ld, col0, row0, hi)
+
+
+def _wgrad_src():
+    return open(os.path.join(os.path.dirname(__file__), "..", "csrc", "kernels", "conv_wgrad.hip")).read()
+
+
+@pytest.mark.parametrize("geom", [(20, 20, 32, 4, 2, 9, 9, 2), (9, 9, 64, 3, 1, 7, 7, 2)])
+def test_conv_wgrad_gemm_dy_reads_are_conflict_free_and_image_reads_bounded(geom):
+    """conv_wgrad_gemm: the dy A fragments (192-byte rows) at one cycle per 32-lane group; the implicit-im2col B
+    fragments within 1.35x of ideal (only reads whose 4 positions wrap an output row conflict; 1.9x before)."""
+    H, W, C, KS, S, OH, OW, SB = geom
+    src = _wgrad_src()
+    assert "constexpr int LDI = S == 2 ? C + 16 : C + 32, LDD = 96, IMG_E = H * W * LDI;" in src
+    LDI, LDD = (C + 16 if S == 2 else C + 32), 96
+    NPOS, NCOL = OH * OW, KS * KS * C
+    GP = SB * NPOS
+    KST = (GP + 15) // 16
+    IMG_E = H * W * LDI
+
+    def pos_off(pk):
+        if pk >= GP:
+            return SB * IMG_E
+        sm, pp = pk // NPOS, pk % NPOS
+        oy, ox = pp // OW, pp % OW
+        return sm * IMG_E + (S * oy * W + S * ox) * LDI
+    tot = n = 0
+    for ks in range(KST):
+        for mt in range(2):
+            for hi in (0, 4):
+                addr = []
+                for lane in range(64):
+                    gl, q, p4 = lane >> 4, (lane >> 2) & 3, lane & 3
+                    addr.append(((ks * 16 + 8 * (gl >> 1) + hi + q) * LDD + mt * 32 + (gl & 1) * 16 + 4 * p4) * 2)
+                assert cycles([[addr[x] for x in g] for g in GTR], 2, 64) == 2, ("dy", ks, mt, hi)
+        for nt in range(NCOL // 32):
+            for hi in (0, 4):
+                addr = []
+                for lane in range(64):
+                    gl, q, p4 = lane >> 4, (lane >> 2) & 3, lane & 3
+                    n0 = nt * 32 + (gl & 1) * 16 + 4 * p4
+                    kyx, c0 = n0 // C, n0 % C
+                    ky, kx = kyx // KS, kyx % KS
+                    po = pos_off(ks * 16 + 8 * (gl >> 1) + hi + q)
+                    addr.append((po if po == SB * IMG_E else po + (ky * W + kx) * LDI + c0) * 2)
+                tot += cycles([[addr[x] for x in g] for g in GTR], 2, 64)
+                n += 1
+    assert tot / n / 2 < 1.35

@@ -110,6 +110,8 @@ class CNNEngine:
         self.a2c_head = o.a2c_head
         self._a2c_bar = None
         self._fcf_cnt = None   # fused step fc product: slice counters + timeout word (fused_fc_args)
+        self._fcb_sq = None    # fc_bwd's per-tile dWfc sums of squares (the finaliser's presummed norm job)
+        self._cur_presum = False
         # A2C head v3 (loss.hip a2c_head_env_kernel): one workgroup per env, no grid-wide hand-off; the head's weight /
         # bias gradients as per-env planes and the statistics as per-env rows, both reduced by the finaliser
         self.a2c_head_env = o.a2c_head_env
@@ -600,8 +602,9 @@ class CNNEngine:
                 return self._backward_grouped(b, stage, ws, ws2)
             return self._backward_trunk(b, main, side, ev, ws, ws2)
         # weight-gradient plane sets written by THIS backward (reduced by its finaliser), plus the head's planes when
-        # ppo_head ran just before it
+        # ppo_head ran just before it; whether dWfc's norm comes as fc_bwd's presummed partials
         self._cur_planes, self._head_planes = dict(self._head_planes) if head_done else {}, {}
+        self._cur_presum = False
         if grouped:
             return self._backward_grouped(b, stage, ws, ws2)
         head_bias_done = head_bias_done or getattr(b, "bias_done", False)
@@ -662,8 +665,15 @@ class CNNEngine:
                 return
         elif stage in ("all", "tail") and self.fc_bwd_ok(B):
             # both fc products in one launch of two job kinds (fc_bwd.hip): dWfc tiles staged in LDS, dy3 tiles
-            # straight from the k-contiguous rows of dh and Wfc
-            _native.require().fc_bwd(b.dh, self.sWfc, b.y3, b.dy3, self.gWfc)
+            # from whole-line row loads; with the finaliser's norm partials wanted, the dWfc tiles also leave their
+            # sums of squares (the finaliser adds those instead of re-reading the 6.4 MB gradient)
+            sq = None
+            if self.want_parts and stage == "all":
+                if self._fcb_sq is None:
+                    self._fcb_sq = torch.zeros(392 * 4, dtype=torch.float32, device=self.dev)
+                sq = self._fcb_sq
+                self._cur_presum = True
+            _native.require().fc_bwd(b.dh, self.sWfc, b.y3, b.dy3, self.gWfc, None, sq)
             if stage == "tail":
                 return
         elif stage in ("all", "tail"):
@@ -748,7 +758,8 @@ class CNNEngine:
         want_parts = self.want_parts if parts is None else parts
         fused_rows = self.fused_bwd and bias_rows
         planes = tuple(sorted((self._cur_planes if planes is None else planes).items())) if self.det_wgrad else ()
-        key = (b.B, want_parts, fused_rows, planes)
+        presum = want_parts and self._cur_presum and self._fcb_sq is not None
+        key = (b.B, want_parts, fused_rows, planes, presum)
         words = self._fin_words.get(key)
         if words is None:
             segs = []
@@ -768,6 +779,8 @@ class CNNEngine:
                 src = src_of.get(g.data_ptr())
                 if src is not None:
                     segs.append((g.data_ptr(), src[0], g.numel(), src[1], src[2]))
+                elif presum and g.data_ptr() == self.gWfc.data_ptr():
+                    segs.append((self._fcb_sq.data_ptr(), 0, self._fcb_sq.numel(), 0, -1))
                 elif want_parts:
                     segs.append((g.data_ptr(), 0, g.numel(), 0, 0))
             from ..ops.optim import finalize_jobs

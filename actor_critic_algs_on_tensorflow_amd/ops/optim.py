@@ -336,14 +336,17 @@ def finalize_jobs(segments, device, return_max=False):
     (``n * S`` spread over the workgroups: 1024-element jobs for the many-plane conv gradients, long jobs for a
     two-plane fc gradient of 1.6 M elements, which at 1024 elements per job would not fit the job budget), per-sample
     bias rows (n <= 64) take one job each, and the read-only segments share the remaining workgroups in equal
-    multiples of 1024 elements; at most ``SUMSQ_PARTS`` jobs."""
+    multiples of 1024 elements; at most ``SUMSQ_PARTS`` jobs. ``S = -1`` with ``src_ptr`` 0: ``n`` presummed sums of
+    squares at ``dst_ptr`` (fc_bwd's per-tile partials), one job that adds them."""
+    pre = [sg for sg in segments if not sg[1] and sg[4] < 0]   # presummed sums of squares: one job each
+    segments = [sg for sg in segments if sg[1] or sg[4] >= 0]
     small = [sg for sg in segments if sg[1] and sg[2] <= 64]
     big = [sg for sg in segments if sg[1] and sg[2] > 64]
     ro = [sg for sg in segments if not sg[1]]
-    budget = max(1, SUMSQ_PARTS - len(small) - max(1, len(ro)))
+    budget = max(1, SUMSQ_PARTS - len(pre) - len(small) - max(1, len(ro)))
     target = max(1024.0, sum(n * S for _, _, n, _, S in big) / budget)   # plane loads per job
     while True:
-        jobs = [[dst, src, n, stride, S] for dst, src, n, stride, S in small]
+        jobs = [list(sg) for sg in pre] + [[dst, src, n, stride, S] for dst, src, n, stride, S in small]
         for dst, src, n, stride, S in big:
             ch = max(1024, -(-int(target // max(1, S)) // 1024) * 1024)
             for a in range(0, n, ch):

@@ -29,7 +29,8 @@ hipError_t aca_mlp_wgrad(const aca::WgradArgs*, hipStream_t);
 hipError_t aca_ppo_head(const aca::PpoHeadArgs*, int, hipStream_t);
 int aca_ppo_head_planes(int);
 int aca_opt_set_unroll(int);
-hipError_t aca_fc_bwd(const uint16_t*, const uint16_t*, const uint16_t*, uint16_t*, float*, int, uint64_t*, hipStream_t);
+hipError_t aca_fc_bwd(const uint16_t*, const uint16_t*, const uint16_t*, uint16_t*, float*, int, float*, uint64_t*,
+                      hipStream_t);
 hipError_t aca_fc_rollout(const uint16_t*, int64_t, int, const uint16_t*, int, int, float*, int64_t, int, int, int*,
                           unsigned long long*, int, hipStream_t);
 hipError_t aca_mlp_rollout(const aca::RolloutArgs*, size_t, hipStream_t);
@@ -475,7 +476,9 @@ void pong_fused_env_step(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, T
 }
 
 // learner fc backward at B <= 256 rows (fc_bwd.hip): dy3 = (dh Wfc^T) * (y3 > 0) bf16, dW = y3^T dh fp32 (stored)
-void fc_bwd(Tensor dh, Tensor W, Tensor y3, Tensor dy3, Tensor dW, c10::optional<Tensor> stamps) {
+// sq (optional, fp32 >= 1568): per (dWfc tile, wave) sums of squares for the finaliser's norm partials
+void fc_bwd(Tensor dh, Tensor W, Tensor y3, Tensor dy3, Tensor dW, c10::optional<Tensor> stamps,
+            c10::optional<Tensor> sq) {
   for (auto* x : {&dh, &W, &y3, &dy3}) need(*x, at::kBFloat16, "fc_bwd bf16");
   need(dW, at::kFloat, "fc_bwd dW");
   const int64_t B = dh.numel() / 512;
@@ -486,8 +489,14 @@ void fc_bwd(Tensor dh, Tensor W, Tensor y3, Tensor dy3, Tensor dW, c10::optional
     TORCH_CHECK(x->is_contiguous() && reinterpret_cast<uintptr_t>(x->data_ptr()) % 16 == 0,
                 "fc_bwd: contiguous 16-byte aligned buffers");
   const int64_t nwg = 392 + ((B + 31) / 32) * 49;
+  float* sqp = nullptr;
+  if (sq.has_value() && sq->defined()) {
+    need(*sq, at::kFloat, "fc_bwd sq");
+    TORCH_CHECK(sq->numel() >= 392 * 4, "fc_bwd: sq needs 1568 floats");
+    sqp = ptr<float>(*sq);
+  }
   check(aca_fc_bwd(ptr<uint16_t>(dh), ptr<uint16_t>(W), ptr<uint16_t>(y3), ptr<uint16_t>(dy3), ptr<float>(dW), (int)B,
-                   stamps_ptr(stamps, nwg / 4 + 1), cur_stream(dh)),
+                   sqp, stamps_ptr(stamps, nwg / 4 + 1), cur_stream(dh)),
         "fc_bwd");
 }
 
@@ -2008,7 +2017,7 @@ TORCH_LIBRARY(acamd, m) {
   m.def("ppo_head_planes(int B) -> int", &ppo_head_planes);
   m.def("opt_set_unroll(int u) -> int", &opt_set_unroll);
   m.def("fc_rollout(Tensor X, Tensor Wf, Tensor hpart, int variant, Tensor? stamps=None) -> int");
-  m.def("fc_bwd(Tensor dh, Tensor W, Tensor y3, Tensor dy3, Tensor dW, Tensor? stamps=None) -> ()");
+  m.def("fc_bwd(Tensor dh, Tensor W, Tensor y3, Tensor dy3, Tensor dW, Tensor? stamps=None, Tensor? sq=None) -> ()");
   m.def("head_bwd(Tensor z, Tensor act, Tensor logp_old, Tensor ent_coef, Tensor kl_coef, float vf_coef, Tensor rew, "
         "Tensor val, Tensor dones, int L, int returns_mode, bool norm_adv, float gamma, float lam, Tensor ret_w, "
         "Tensor adv_w, Tensor h, Tensor Wh, Tensor dh, Tensor gWh, Tensor gbh, Tensor gbfc, Tensor stats, "

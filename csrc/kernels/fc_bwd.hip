@@ -45,6 +45,8 @@ struct FcBwdArgs {
   int B;
   int n_dy;           // dy3 tiles: ceil(B / 32) x 98
   uint64_t* stamps;   // diagnostics: per workgroup [entry, operands in, MFMAs done, stores issued]
+  float* sq;          // optional: per (dWfc tile, wave) sum of squares [392 x 4] (the finaliser's norm partials
+                      // then need no 6.4 MB re-read of dWfc)
 };
 
 __device__ __forceinline__ void fb_stamp(uint64_t* st, int slot) {
@@ -111,6 +113,14 @@ __device__ __forceinline__ void fb_dw_job(const FcBwdArgs& a, int t, u16* smem) 
   float* dst = a.dW + (size_t)(64 * i + 32 * mq) * FB_N + 64 * j + 32 * nq + col;
 #pragma unroll
   for (int r = 0; r < 16; ++r) dst[(size_t)((r & 3) + 8 * (r >> 2) + rh) * FB_N] = acc[r];
+  if (a.sq) {   // the quadrant's sum of squares: lane terms in register order, then a fixed xor tree
+    float v = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v = fmaf(acc[r], acc[r], v);
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) v += lane_xor(v, o);
+    if (lane == 0) a.sq[t * 4 + w] = v;
+  }
 }
 
 __device__ __forceinline__ void fb_dy_job(const FcBwdArgs& a, int t, u16* smem) {
@@ -196,11 +206,11 @@ __global__ void __launch_bounds__(FB_THREADS, 4) fc_bwd_kernel(FcBwdArgs a) {
 // dh [B][512], W = Wfc [3136][512], y3 [B][3136] bf16 -> dy3 [B][3136] bf16, dW [3136][512] fp32; 1 <= B <= 256,
 // every pointer 16-byte aligned, the row strides dense.
 extern "C" hipError_t aca_fc_bwd(const uint16_t* dh, const uint16_t* W, const uint16_t* y3, uint16_t* dy3, float* dW,
-                                 int B, uint64_t* stamps, hipStream_t stream) {
+                                 int B, float* sq, uint64_t* stamps, hipStream_t stream) {
   if (B < 1 || B > aca::FB_MAXB) return hipErrorInvalidValue;
   for (const void* p : {(const void*)dh, (const void*)W, (const void*)y3, (const void*)dy3, (const void*)dW})
     if (!p || reinterpret_cast<uintptr_t>(p) % 16) return hipErrorInvalidValue;
-  aca::FcBwdArgs a{dh, W, y3, dy3, dW, B, ((B + 31) / 32) * (aca::FB_KF / 32), stamps};
+  aca::FcBwdArgs a{dh, W, y3, dy3, dW, B, ((B + 31) / 32) * (aca::FB_KF / 32), stamps, sq};
   const int Bp = (B + 15) & ~15;
   const size_t lds = std::max((size_t)4 * Bp * 32 * 2, (size_t)2 * 32 * aca::FB_LDH * 2);
   aca::fc_bwd_kernel<<<aca::FB_DW_TILES + a.n_dy, aca::FB_THREADS, lds, stream>>>(a);

@@ -367,7 +367,7 @@ __global__ void __launch_bounds__(OPT_THREADS) opt_multi_kernel(OptMulti M, floa
 // squares of its share of the final gradient into its own partial slot (the unused slots zeroed), which the
 // optimiser reduces in a fixed order: the global-norm clip needs no separate sum-of-squares pass.
 // Job record (8 int64 words): dst, src, n, stride, S, (unused x3). dst / src / stride are float4-aligned when the
-// job's flag word 5 is 1 (host-checked).
+// job's flag word 5 is 1 (host-checked). src = 0, S = -1: dst holds n presummed sums of squares (added, not squared).
 constexpr int FIN_WORDS = 8;
 
 // One finaliser job (record w) by the whole workgroup; returns this thread's share of the sum of squares of the
@@ -381,7 +381,10 @@ __device__ __forceinline__ float fin_job(const int64_t* __restrict__ w, float* _
   const int64_t stride = w[3];
   const int tid = threadIdx.x;
   float s = 0.f;
-  if (!src) {
+  if (!src && S < 0) {
+    // presummed: n sums of squares a producer already formed (fc_bwd's per-tile partials), added as they are
+    for (int i = tid; i < n; i += OPT_THREADS) s += dst[i];
+  } else if (!src) {
     if (vec) {   // read-only, 8 independent 16-byte loads per thread in flight
       const int n4 = n >> 2;
       for (int i0 = tid; i0 < n4; i0 += OPT_THREADS * 8) {

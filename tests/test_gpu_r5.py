@@ -233,8 +233,9 @@ def test_fused_step_fc_update_tracks_separate_fc_launch(cuda):
 
 @pytest.mark.parametrize("B", [160, 7, 256, 33, 1])
 def test_fc_bwd_matches_fp64(cuda, B):
-    """fc_bwd.hip: dWfc = y3^T dh (fp32, every element stored) and dy3 = (dh Wfc^T) * (y3 > 0) (bf16) against fp64
-    products of the same bf16 operands."""
+    """fc_bwd.hip: dWfc = y3^T dh (fp32, every element stored), its per-(tile, wave) sums of squares (the finaliser's
+    presummed norm partials) and dy3 = (dh Wfc^T) * (y3 > 0) (bf16) against fp64 products of the same bf16
+    operands."""
     from actor_critic_algs_on_tensorflow_amd import _native
     ops = _native.require()
     g = torch.Generator(device="cpu").manual_seed(B)
@@ -243,8 +244,14 @@ def test_fc_bwd_matches_fp64(cuda, B):
     y3 = torch.relu(torch.randn(B, 3136, generator=g)).to(torch.bfloat16).to(cuda)
     dy3 = torch.full((B, 3136), float("nan"), dtype=torch.bfloat16, device=cuda)
     dW = torch.full((3136, 512), float("nan"), device=cuda)
-    ops.fc_bwd(dh, W, y3, dy3, dW)
+    sq = torch.full((392 * 4,), float("nan"), device=cuda)
+    ops.fc_bwd(dh, W, y3, dy3, dW, None, sq)
     torch.cuda.synchronize()
+    # per (64 x 64 tile, wave quadrant) sums of squares: tile t = kf block t // 8, n block t % 8 in XCD order is a
+    # permutation, so compare per-tile sets and the total
+    q = dW.double().view(49, 2, 32, 8, 2, 32).pow(2).sum((2, 5))          # [kf blk, mq, n blk, nq]
+    ref_sq = q.permute(0, 2, 1, 3).reshape(392 * 4)                       # tile (i, j) -> wave 2 mq + nq
+    assert float((sq.double() - ref_sq).abs().max() / ref_sq.abs().max()) < 1e-5
     ref_w = y3.double().t() @ dh.double()
     assert float((dW.double() - ref_w).abs().max() / ref_w.abs().max()) < 1e-5
     ref_d = (dh.double() @ W.double().t()) * (y3.double() > 0)

@@ -143,6 +143,7 @@ class CNNEngine:
         self._wsplits = {}
         self._cur_planes = {}
         self._fin_words = {}
+        self._retired = []     # outgrown plane buffers (+ the tables naming them) kept for captured graphs
         # rollout fc product left as split-K partial planes, reduced by its consumer kernel (no in-launch fence)
         self.fc_parts = True
         # split-K planes the fc GEMM may use (more planes: more workgroups stream Wfc, more for the consumer to sum)
@@ -425,13 +426,29 @@ class CNNEngine:
         self._wsplits[name] = S
         self._cur_planes[name] = S
 
-    def _trunk_bwd(self, b):
+    def conv1_fold_ok(self, B):
+        """The per-sample trunk backward also leaves the sample's conv1 weight gradient (``EngineOpts.conv1_fold``):
+        one [32, 256] plane per sample, summed in order by the finaliser, instead of the conv1 product of the grouped
+        weight-gradient launch."""
+        return (self.opts.conv1_fold and self.dev.type == "cuda" and self.det_wgrad and self.implicit
+                and not self.opts.trunk_bwd_v2 and 1 <= B < self.trunk_bwd_persist_min_b)
+
+    def _trunk_bwd(self, b, fold=False):
+        """dy3 -> dy2 -> dy1 (+ the bias-gradient rows); ``fold``: with :meth:`conv1_fold_ok`, the conv1 weight
+        gradient too (returns True when it was folded)."""
         if self.opts.trunk_bwd_v2:   # trunk_bwd2.hip: at most trunk_bwd_persist workgroups, walking the samples
             _native.require().cnn_trunk_bwd2(b.dy3, self.sW3, b.y2, self.sW2, b.y1, b.dy2, b.dy1, b.biasp, None,
                                              self.trunk_bwd_persist)
-            return
+            return False
+        if fold and self.conv1_fold_ok(b.B):
+            buf = self._plane_buf("W1f", b.B * 32 * 256)
+            _native.require().cnn_trunk_bwd(b.dy3, self.sW3, b.y2, self.sW2, b.y1, b.dy2, b.dy1, b.biasp, None, 0,
+                                            b.obs, getattr(b, "obs_idx", None), buf, 1.0 / 255.0)
+            self._cur_planes["W1f"] = b.B
+            return True
         persist = self.trunk_bwd_persist if b.B >= self.trunk_bwd_persist_min_b else 0
         _native.require().cnn_trunk_bwd(b.dy3, self.sW3, b.y2, self.sW2, b.y1, b.dy2, b.dy1, b.biasp, None, persist)
+        return False
 
     def _wgrad_conv23(self, name, b, ws2):
         B = b.B
@@ -446,8 +463,7 @@ class CNNEngine:
         P = max(1, min(self.nhwc_planes if name == "W2" else self.nhwc3_planes, B))
         buf = self._planes.get(name)
         if buf is None or buf.numel() < P * 64 * n:
-            buf = torch.zeros(max(P, self.wgrad_planes) * 64 * n, dtype=torch.float32, device=self.dev)
-            self._planes[name] = buf
+            buf = self._plane_buf(name, max(P, self.wgrad_planes) * 64 * n)
         # batched-position MFMA 32x32x16 kernel (default) or the per-sample kernel (EngineOpts.wgrad_gemm off)
         fn = _native.require().conv_wgrad_gemm if self.wgrad_gemm else _native.require().conv_wgrad_nhwc
         if name == "W2":
@@ -466,8 +482,7 @@ class CNNEngine:
         P = max(1, min(self.conv1_planes, B))
         buf = self._planes.get("W1")
         if buf is None or buf.numel() < P * 32 * 256:
-            buf = torch.zeros(max(P, self.wgrad_planes) * 32 * 256, dtype=torch.float32, device=self.dev)
-            self._planes["W1"] = buf
+            buf = self._plane_buf("W1", max(P, self.wgrad_planes) * 32 * 256)
         _native.require().conv1_wgrad(b.obs, b.dy1, buf, P, 1.0 / 255.0, getattr(b, "obs_idx", None))
         self._wsplits["W1"] = P
         self._cur_planes["W1"] = P
@@ -479,8 +494,17 @@ class CNNEngine:
                 and self.fused_bwd and self.det_wgrad and B >= 1)
 
     def _big_planes(self, name, n):
+        return self._plane_buf(name, n)
+
+    def _plane_buf(self, name, n):
+        """Plane set ``name`` with room for ``n`` floats. A buffer outgrown here is retired, not freed: captured graphs
+        and the cached finaliser tables may still name it (the tables are dropped, to be rebuilt on the new one)."""
         buf = self._planes.get(name)
         if buf is None or buf.numel() < n:
+            if buf is not None:
+                self._retired.append(buf)
+                self._retired.extend(self._fin_words.values())
+                self._fin_words = {}
             buf = torch.zeros(n, dtype=torch.float32, device=self.dev)
             self._planes[name] = buf
         return buf
@@ -683,9 +707,10 @@ class CNNEngine:
                 G.gemm(b.y3, 3136, False, b.dh, 512, False, self.gWfc, 512, 0, 3136, 512, B, workspace=ws2)
             if stage == "tail":
                 return
-        self._trunk_bwd(b)
+        folded = self._trunk_bwd(b, fold=True)
         with G.group():   # the longest product (conv1, K = 400 B) first
-            self._wgrad_conv1(b, ws)
+            if not folded:
+                self._wgrad_conv1(b, ws)
             self._wgrad_conv23("W2", b, ws2)
             self._wgrad_conv23("W3", b, ws2)
         self.finalize(b)
@@ -770,8 +795,8 @@ class CNNEngine:
                 src_of = {self.gb3.data_ptr(): (bp, 160, b.B), self.gb2.data_ptr(): (bp + 64 * 4, 160, b.B),
                           self.gb1.data_ptr(): (bp + 128 * 4, 160, b.B)}
             for name, S in planes:
-                g = {"W1": self.gW1, "W2": self.gW2, "W3": self.gW3, "Wh": self.gWh, "ph_Wh": self.gWh,
-                     "ph_bh": self.gbh, "ph_bfc": self.gbfc, "Wfc": self.gWfc, "ae_Wh": self.gWh,
+                g = {"W1": self.gW1, "W1f": self.gW1, "W2": self.gW2, "W3": self.gW3, "Wh": self.gWh,
+                     "ph_Wh": self.gWh, "ph_bh": self.gbh, "ph_bfc": self.gbfc, "Wfc": self.gWfc, "ae_Wh": self.gWh,
                      "ae_bh": self.gbh, "ae_bfc": self.gbfc}[name]
                 src_of[g.data_ptr()] = (self._planes[name].data_ptr(), g.numel(), S)
             for p, off in zip(flat.params, flat.offsets):

@@ -136,7 +136,8 @@ hipError_t aca_a2c_head(const float*, const int32_t*, const float*, const float*
                         const uint16_t*, const uint16_t*, uint16_t*, float*, float*, float*, float*, int,
                         const float*, int, int64_t, const float*, const float*, unsigned int*, uint64_t*, hipStream_t);
 hipError_t aca_cnn_trunk_bwd(const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*,
-                             uint16_t*, uint16_t*, float*, int, uint64_t*, int, hipStream_t);
+                             uint16_t*, uint16_t*, float*, int, uint64_t*, int, const uint8_t*, const int64_t*, float*,
+                             float, hipStream_t);
 hipError_t aca_cnn_trunk_bwd2(const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*,
                               uint16_t*, uint16_t*, float*, int, uint64_t*, int, hipStream_t);
 hipError_t aca_cnn_trunk_rows(const uint8_t*, const uint16_t*, const float*, const uint16_t*, const float*,
@@ -1581,8 +1582,11 @@ void cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tenso
 // held in registers (cnn_trunk_bwd_persist_kernel, bit-identical): dy3 [B*49, 64] (already masked by y3 > 0), W3 [64, 576] / W2 [64, 512]
 // (OHWI bf16 shadows), masks y2 [B*81, 64] / y1 [B*400, 32]; writes dy2, dy1 (masked) and the per-sample bias
 // gradient partials biasp [B, 160] = (sum dy3 | sum dy2 | sum dy1).
+// w1_obs / w1_planes (per-sample kernel only): the conv1 weight gradient folded in -- one [32][256] fp32 plane per
+// sample (times w1_scale), frames of sample b = w1_obs row w1_obs_idx[b] (or b)
 void cnn_trunk_bwd(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tensor dy2, Tensor dy1, Tensor biasp,
-                   c10::optional<Tensor> stamps, int64_t persist) {
+                   c10::optional<Tensor> stamps, int64_t persist, c10::optional<Tensor> w1_obs,
+                   c10::optional<Tensor> w1_obs_idx, c10::optional<Tensor> w1_planes, double w1_scale) {
   for (auto* t : {&dy3, &W3, &y2, &W2, &y1, &dy2, &dy1}) need(*t, at::kBFloat16, "trunk_bwd bf16 operand");
   need(biasp, at::kFloat, "biasp");
   TORCH_CHECK(dy3.numel() % (49 * 64) == 0, "cnn_trunk_bwd: dy3 must be [B*49, 64]");
@@ -1591,9 +1595,29 @@ void cnn_trunk_bwd(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tenso
   TORCH_CHECK(y2.numel() >= B * 81 * 64 && y1.numel() >= B * 400 * 32 && dy2.numel() >= B * 81 * 64 &&
                   dy1.numel() >= B * 400 * 32 && biasp.numel() >= B * 160,
               "cnn_trunk_bwd: buffers too small");
+  const uint8_t* wo = nullptr;
+  const int64_t* wi = nullptr;
+  float* wp = nullptr;
+  if (w1_obs.has_value() && w1_obs->defined()) {
+    TORCH_CHECK(persist <= 0, "cnn_trunk_bwd: the conv1 fold runs in the per-sample kernel only");
+    need(*w1_obs, at::kByte, "w1_obs");
+    TORCH_CHECK(w1_obs->is_contiguous() && w1_obs->numel() % (4 * 84 * 84) == 0, "cnn_trunk_bwd: w1_obs [*, 4, 84, 84]");
+    TORCH_CHECK(w1_planes.has_value() && w1_planes->defined(), "cnn_trunk_bwd: w1_obs needs w1_planes");
+    need(*w1_planes, at::kFloat, "w1_planes");
+    TORCH_CHECK(w1_planes->numel() >= B * 32 * 256, "cnn_trunk_bwd: w1_planes needs B x 8192 floats");
+    if (w1_obs_idx.has_value() && w1_obs_idx->defined()) {
+      need(*w1_obs_idx, at::kLong, "w1_obs_idx");
+      TORCH_CHECK(w1_obs_idx->numel() >= B, "cnn_trunk_bwd: w1_obs_idx needs B rows");
+      wi = ptr<int64_t>(*w1_obs_idx);
+    } else {
+      TORCH_CHECK(w1_obs->numel() >= B * 4 * 84 * 84, "cnn_trunk_bwd: w1_obs needs B samples");
+    }
+    wo = ptr<uint8_t>(*w1_obs);
+    wp = ptr<float>(*w1_planes);
+  }
   check(aca_cnn_trunk_bwd(ptr<uint16_t>(dy3), ptr<uint16_t>(W3), ptr<uint16_t>(y2), ptr<uint16_t>(W2),
                           ptr<uint16_t>(y1), ptr<uint16_t>(dy2), ptr<uint16_t>(dy1), ptr<float>(biasp), (int)B,
-                          stamps_ptr(stamps, B), (int)persist, cur_stream(dy3)),
+                          stamps_ptr(stamps, B), (int)persist, wo, wi, wp, (float)w1_scale, cur_stream(dy3)),
         "cnn_trunk_bwd");
 }
 
@@ -2001,7 +2025,8 @@ TORCH_LIBRARY(acamd, m) {
         "Tensor y2, Tensor y3, float scale, Tensor? shift_out=None, Tensor? stamps=None, int mode=0, "
         "Tensor? copy_out=None, Tensor? obs_idx=None) -> ()");
   m.def("cnn_trunk_bwd(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tensor dy2, Tensor dy1, "
-        "Tensor biasp, Tensor? stamps=None, int persist=0) -> ()");
+        "Tensor biasp, Tensor? stamps=None, int persist=0, Tensor? w1_obs=None, Tensor? w1_obs_idx=None, "
+        "Tensor? w1_planes=None, float w1_scale=1.0) -> ()");
   m.def("cnn_trunk_bwd2(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tensor dy2, Tensor dy1, "
         "Tensor biasp, Tensor? stamps=None, int max_wg=0) -> ()");
   m.def("grad_finalize(Tensor jobs, Tensor partial, Tensor? spart=None, int B=0, Tensor? ent_coef=None, "

@@ -1558,10 +1558,27 @@ __device__ __forceinline__ bf16x8 tr_frag(const u16* rows, int ld, int col0, int
 
 // 8 waves (2 per SIMD: one wave per SIMD left every LDS read latency exposed); one workgroup per CU by LDS.
 constexpr int BW_T = 512;
+// W1G: the conv1 weight gradient of the sample folded in (W1Fold): dW1[o][c] = scale * sum_p dy1[p][o] *
+// obs[ch][4 oy + ky][4 ox + kx], c = (ch, ky, kx), p = (oy, ox) -- the masked dy1 rows are on chip already, the
+// sample's 4 frames (prefetched into registers at entry) are staged as exact bf16 over the dead W2 rows; 8 waves x
+// (2 x 2 tiles of the 16x16x32 MFMA), 13 k-steps of 32 positions; the sample's [32][256] fp32 plane is written once
+// (the finaliser sums the per-sample planes in order). Replaces the conv1 split-K GEMM of the grouped weight-gradient
+// launch (EngineOpts.conv1_fold).
+struct W1Fold {
+  const uint8_t* obs;        // [*, 4, 84, 84] uint8 frames
+  const int64_t* obs_idx;    // sample b reads obs row obs_idx[b] (null: row b)
+  float* planes;             // [B][32 * 256]
+  float scale;               // 1 / 255
+};
+constexpr int BW_FR = 4 * 84 * 84;   // frame pixels of a sample (bf16 in LDS: 56.4 KB over the dead W2 rows)
+static_assert(BW_FR + 8 <= BW_RW, "the bf16 frames + a zero chunk fit the weight region");
+static_assert(416 * 32 <= BW_P3E + BW_M2E, "dy1 rows + 16 zero padding rows (13 k-steps of 32) fit the staging");
+
+template <bool W1G>
 __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_kernel(
     const u16* __restrict__ dy3g, const u16* __restrict__ W3, const u16* __restrict__ y2g,
     const u16* __restrict__ W2, const u16* __restrict__ y1g, u16* __restrict__ dy2g, u16* __restrict__ dy1g,
-    float* __restrict__ biasp, uint64_t* __restrict__ stamps) {
+    float* __restrict__ biasp, uint64_t* __restrict__ stamps, W1Fold wf) {
   __shared__ __attribute__((aligned(16))) u16 s_w[BW_RW];
   __shared__ __attribute__((aligned(16))) u16 s_p3m2[BW_P3E + BW_M2E];   // dy3 image + y2 mask; later dy1 staging
   __shared__ __attribute__((aligned(16))) u16 s_p2[BW_P2E];
@@ -1624,6 +1641,16 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_kernel(
   for (int u = 0; u < M1_PER; ++u) {
     const int c = min(tid + u * BW_T, M1_CH - 1);
     vm1[u] = *reinterpret_cast<const uint4*>(y1g + (size_t)b * 400 * 32 + c * 8);
+  }
+  // W1G: the sample's frames, 16-pixel chunks (1764 of them: <= 4 per thread), held until the dy1 output pass
+  constexpr int FR_CH = BW_FR / 16;
+  uint4 fr0, fr1, fr2, fr3;
+  if constexpr (W1G) {
+    const uint4* f = reinterpret_cast<const uint4*>(wf.obs + (size_t)(wf.obs_idx ? wf.obs_idx[b] : b) * BW_FR);
+    fr0 = f[tid];
+    fr1 = f[tid + BW_T];
+    fr2 = f[tid + 2 * BW_T];
+    fr3 = f[min(tid + 3 * BW_T, FR_CH - 1)];
   }
   __syncthreads();
   stamp(stamps, 1);
@@ -1772,7 +1799,23 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_kernel(
 #pragma unroll
       for (int e = 0; e < 8; ++e) part1[e] += bf_lane(v, e);
       *reinterpret_cast<uint4*>(dy1g + (size_t)b * 400 * 32 + c * 8) = v;
+      if constexpr (W1G) *reinterpret_cast<uint4*>(s_d1 + c * 8) = v;   // the masked rows: dW1's A operand
     }
+  }
+  if constexpr (W1G) {
+    // the frames as exact bf16 over the dead W2 rows, a zero chunk behind them, zero dy1 rows 400..415
+    u16* const s_fr = s_w;
+    auto put = [&](const uint4& w, int i) {
+      const uint2 a = u8x4_to_bf16(w.x), b2 = u8x4_to_bf16(w.y), c = u8x4_to_bf16(w.z), d = u8x4_to_bf16(w.w);
+      *reinterpret_cast<uint4*>(s_fr + i * 16) = make_uint4(a.x, a.y, b2.x, b2.y);
+      *reinterpret_cast<uint4*>(s_fr + i * 16 + 8) = make_uint4(c.x, c.y, d.x, d.y);
+    };
+    put(fr0, tid);
+    put(fr1, tid + BW_T);
+    put(fr2, tid + 2 * BW_T);
+    if (tid + 3 * BW_T < FR_CH) put(fr3, tid + 3 * BW_T);
+    if (tid == 0) *reinterpret_cast<uint4*>(s_fr + BW_FR) = make_uint4(0u, 0u, 0u, 0u);
+    s_d1[400 * 32 + tid] = 0;   // 16 padding rows x 32 = 512 (the dy1 epilogue's discard slot lives there)
   }
 #pragma unroll
   for (int e = 0; e < 8; ++e)
@@ -1787,6 +1830,45 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_kernel(
 #pragma unroll
     for (int w = 0; w < 8; ++w) v += s_red[1024 + w * 32 + tid];
     biasp[(size_t)b * 160 + 128 + tid] = v;
+  }
+  if constexpr (W1G) {
+    // dW1 of the sample: wave -> (o tiles 0, 1) x (c tiles 2 wid, 2 wid + 1); A = masked dy1 rows [p][o] and B =
+    // the patch matrix straight from the bf16 frames, both by transposing reads; positions past 400 read zeros
+    const u16* const s_fr = s_w;
+    floatx4 acc[2][2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int n = 0; n < 2; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const int q = l16 >> 2, pq = l16 & 3;
+    for (int ks = 0; ks < 13; ++ks) {
+      const bf16x8 a0 = tr_frag(s_d1 + ks * 32 * 32, 32, 0, lane);
+      const bf16x8 a1 = tr_frag(s_d1 + ks * 32 * 32, 32, 16, lane);
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        const int c = (2 * wid + n) * 16 + 4 * pq, ch = c >> 6, ky = (c >> 3) & 7, kx0 = c & 7;
+        const int pa = ks * 32 + lg * 8 + q, pb = pa + 4;
+        const int oya = pa / 20, oyb = pb / 20;
+        const int offa = pa < 400 ? ch * 7056 + (4 * oya + ky) * 84 + 4 * (pa - oya * 20) + kx0 : BW_FR;
+        const int offb = pb < 400 ? ch * 7056 + (4 * oyb + ky) * 84 + 4 * (pb - oyb * 20) + kx0 : BW_FR;
+        typedef short short4x __attribute__((ext_vector_type(4)));
+        typedef __attribute__((address_space(3))) short4x lds4;
+        const short4x lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(s_fr + offa));
+        const short4x hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(s_fr + offb));
+        const short8v bv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const bf16x8 bf = __builtin_bit_cast(bf16x8, bv);
+        acc[0][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf, acc[0][n], 0, 0, 0);
+        acc[1][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bf, acc[1][n], 0, 0, 0);
+      }
+    }
+    float* const pl = wf.planes + (size_t)b * 32 * 256;
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          pl[(size_t)(16 * m + 4 * lg + r) * 256 + (2 * wid + n) * 16 + l16] = acc[m][n][r] * wf.scale;
   }
   if (stamps) {
     stamp(stamps, 5);
@@ -2154,7 +2236,10 @@ extern "C" hipError_t aca_cnn_trunk_rows(const uint8_t* obs, const uint16_t* W1,
 
 extern "C" hipError_t aca_cnn_trunk_bwd(const uint16_t* dy3, const uint16_t* W3, const uint16_t* y2, const uint16_t* W2,
                                         const uint16_t* y1, uint16_t* dy2, uint16_t* dy1, float* biasp, int B,
-                                        uint64_t* stamps, int persist, hipStream_t stream) {
+                                        uint64_t* stamps, int persist, const uint8_t* w1_obs,
+                                        const int64_t* w1_obs_idx, float* w1_planes, float w1_scale,
+                                        hipStream_t stream) {
+  // w1_obs: the conv1 weight gradient folded into the per-sample kernel (one [32][256] plane per sample)
   if (B <= 0) return hipSuccess;
   for (const void* p : {(const void*)dy3, (const void*)W3, (const void*)y2, (const void*)W2, (const void*)y1,
                         (const void*)dy2, (const void*)dy1})
@@ -2162,8 +2247,14 @@ extern "C" hipError_t aca_cnn_trunk_bwd(const uint16_t* dy3, const uint16_t* W3,
   if (persist > 0)
     aca::cnn_trunk_bwd_persist_kernel<<<persist < B ? persist : B, aca::BW_T, 0, stream>>>(dy3, W3, y2, W2, y1, dy2,
                                                                                              dy1, biasp, B, stamps);
-  else
-    aca::cnn_trunk_bwd_kernel<<<B, aca::BW_T, 0, stream>>>(dy3, W3, y2, W2, y1, dy2, dy1, biasp, stamps);
+  else if (w1_obs) {
+    if (!w1_planes || reinterpret_cast<uintptr_t>(w1_obs) % 16) return hipErrorInvalidValue;
+    const aca::W1Fold wf{w1_obs, w1_obs_idx, w1_planes, w1_scale};
+    aca::cnn_trunk_bwd_kernel<true><<<B, aca::BW_T, 0, stream>>>(dy3, W3, y2, W2, y1, dy2, dy1, biasp, stamps, wf);
+  } else {
+    aca::cnn_trunk_bwd_kernel<false><<<B, aca::BW_T, 0, stream>>>(dy3, W3, y2, W2, y1, dy2, dy1, biasp, stamps,
+                                                                  aca::W1Fold{nullptr, nullptr, nullptr, 0.f});
+  }
   return hipGetLastError();
 }
 

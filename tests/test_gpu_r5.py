@@ -300,3 +300,74 @@ def test_trunk_bwd2_matches_conv_transpose(cuda, B):
     assert torch.allclose(bpc[:, :64], dy3.float().sum((1, 2)), rtol=1e-4, atol=1e-4)
     assert torch.allclose(bpc[:, 64:128], got2.sum((1, 2)), rtol=1e-4, atol=1e-3)
     assert torch.allclose(bpc[:, 128:], got1.sum((1, 2)), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("B,idx", [(1, False), (5, True), (37, False), (160, True)])
+def test_trunk_bwd_conv1_fold_matches_fp64(cuda, B, idx):
+    """cnn_trunk_bwd with the conv1 weight gradient folded in (W1Fold): the data-gradient outputs are bit-identical
+    to the plain kernel's, and each sample's [32, 256] plane == scale * dy1_b^T unfold(obs_b) in fp64 (the masked bf16
+    dy1 the kernel wrote, frames of row obs_idx[b] when given)."""
+    import torch.nn.functional as F
+    from actor_critic_algs_on_tensorflow_amd import _native
+    ops = _native.require()
+    g = torch.Generator(device="cpu").manual_seed(B + 11)
+    dy3 = (torch.randn(B, 7, 7, 64, generator=g) * (torch.rand(B, 7, 7, 64, generator=g) > 0.4)).to(torch.bfloat16)
+    W3 = (torch.randn(64, 3, 3, 64, generator=g) * 0.05).to(torch.bfloat16)
+    W2 = (torch.randn(64, 4, 4, 32, generator=g) * 0.05).to(torch.bfloat16)
+    y2 = (torch.rand(B, 9, 9, 64, generator=g) - 0.3).clamp(min=0).to(torch.bfloat16)
+    y1 = (torch.rand(B, 20, 20, 32, generator=g) - 0.3).clamp(min=0).to(torch.bfloat16)
+    R = 2 * B + 3 if idx else B
+    obs = torch.randint(0, 256, (R, 4, 84, 84), dtype=torch.uint8, generator=g)
+    oi = torch.randperm(R, generator=g)[:B] if idx else None
+    dev = [t.to(cuda) for t in (dy3, W3, y2, W2, y1)]
+    args = (dev[0].reshape(B * 49, 64), dev[1].reshape(64, 576), dev[2].reshape(B * 81, 64), dev[3].reshape(64, 512),
+            dev[4].reshape(B * 400, 32))
+    res = []
+    planes = torch.full((B, 32, 256), float("nan"), device=cuda)
+    for fold in (False, True):
+        dy2 = torch.full((B * 81, 64), float("nan"), dtype=torch.bfloat16, device=cuda)
+        dy1 = torch.full((B * 400, 32), float("nan"), dtype=torch.bfloat16, device=cuda)
+        bp = torch.full((B, 160), float("nan"), device=cuda)
+        if fold:
+            ops.cnn_trunk_bwd(*args, dy2, dy1, bp, None, 0, obs.to(cuda), oi.to(cuda) if idx else None, planes,
+                              1.0 / 255.0)
+        else:
+            ops.cnn_trunk_bwd(*args, dy2, dy1, bp)
+        torch.cuda.synchronize()
+        res.append((dy2.view(torch.int16).clone(), dy1.view(torch.int16).clone(), bp.clone()))
+    assert all(torch.equal(a, b) for a, b in zip(res[0], res[1]))
+    d1 = res[1][1].view(torch.bfloat16).cpu().double().view(B, 400, 32)
+    fr = obs[oi] if idx else obs
+    cols = F.unfold(fr.double(), 8, stride=4)                           # [B, 256 = (ch, ky, kx), 400]
+    ref = torch.einsum("bpo,bcp->boc", d1, cols) / 255.0
+    got = planes.cpu().double()
+    assert not torch.isnan(got).any()
+    err = float((got - ref).abs().max() / ref.abs().max())
+    assert err < 1e-5, err
+
+
+@pytest.mark.parametrize("algo,kw", [("pong_a2c", {}), ("breakout_ppo", dict(n_steps=16, ppo_minibatches=2,
+                                                                              ppo_epochs=1))])
+def test_conv1_fold_update_tracks_grouped_wgrad(cuda, algo, kw):
+    """One optimiser step with the conv1 weight gradient folded into the trunk backward (EngineOpts.conv1_fold) vs
+    the conv1 product of the grouped weight-gradient launch: same statistics, same update up to fp32 summation
+    order and the GEMM's bf16 rounding of the scaled frames."""
+    from actor_critic_algs_on_tensorflow_amd import preset
+    from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
+    res = {}
+    for knob in (True, False):
+        cfg = preset(algo, num_envs=8, device="cuda:0", outdir=None, quiet=True, stdout_freq=0, save_every=0,
+                     cuda_graph=False, optimizer="adam", engine_opts=dict(conv1_fold=knob), **kw)
+        tr = ActorCriticTrainer(cfg)
+        p0 = tr.flat.data.clone()
+        tr.step()
+        torch.cuda.synchronize()
+        assert ("W1f" in tr.engine._planes) == knob
+        res[knob] = (tr.flat.data - p0, tr.stats_buf.clone(), tr.engine.gW1.clone())
+    d1, s1, g1 = res[True]
+    d0, s0, g0 = res[False]
+    assert torch.allclose(s0[:8], s1[:8], rtol=1e-4, atol=1e-6), (s0[:8], s1[:8])
+    # the GEMM path stages the frames as bf16(pixel / 255) (relative rounding <= 2^-9); the fold multiplies exact
+    # integer pixels and scales the fp32 sums
+    assert float((g0 - g1).norm() / g0.norm()) < 5e-3
+    assert (d0 - d1).norm() / d0.norm() < 1e-2, float((d0 - d1).norm() / d0.norm())

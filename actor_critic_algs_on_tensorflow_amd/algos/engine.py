@@ -447,8 +447,17 @@ class CNNEngine:
             self._cur_planes["W1f"] = b.B
             return True
         persist = self.trunk_bwd_persist if b.B >= self.trunk_bwd_persist_min_b else 0
-        _native.require().cnn_trunk_bwd(b.dy3, self.sW3, b.y2, self.sW2, b.y1, b.dy2, b.dy1, b.biasp, None, persist)
+        _native.require().cnn_trunk_bwd(b.dy3, self.sW3, b.y2, self.sW2, b.y1, b.dy2, b.dy1, b.biasp, None, persist,
+                                        None, None, None, 1.0, self.bias_rows(b.B) < b.B)
         return False
+
+    def bias_rows(self, B):
+        """Bias-gradient partial rows the trunk backward of a ``B``-row batch leaves for the finaliser: one per
+        sample, or one per workgroup of the persistent kernel (``EngineOpts.bias_rows_acc``)."""
+        if (self.opts.bias_rows_acc and not self.opts.trunk_bwd_v2 and B >= self.trunk_bwd_persist_min_b
+                and self.trunk_bwd_persist < B):
+            return self.trunk_bwd_persist
+        return B
 
     def _wgrad_conv23(self, name, b, ws2):
         B = b.B
@@ -791,9 +800,9 @@ class CNNEngine:
             flat = self.flat
             src_of = {}   # gradient slot -> (source, stride, planes)
             if fused_rows:
-                bp = b.biasp.data_ptr()
-                src_of = {self.gb3.data_ptr(): (bp, 160, b.B), self.gb2.data_ptr(): (bp + 64 * 4, 160, b.B),
-                          self.gb1.data_ptr(): (bp + 128 * 4, 160, b.B)}
+                bp, R = b.biasp.data_ptr(), self.bias_rows(b.B)
+                src_of = {self.gb3.data_ptr(): (bp, 160, R), self.gb2.data_ptr(): (bp + 64 * 4, 160, R),
+                          self.gb1.data_ptr(): (bp + 128 * 4, 160, R)}
             for name, S in planes:
                 g = {"W1": self.gW1, "W1f": self.gW1, "W2": self.gW2, "W3": self.gW3, "Wh": self.gWh,
                      "ph_Wh": self.gWh, "ph_bh": self.gbh, "ph_bfc": self.gbfc, "Wfc": self.gWfc, "ae_Wh": self.gWh,

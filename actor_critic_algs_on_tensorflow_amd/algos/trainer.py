@@ -147,6 +147,7 @@ class ActorCriticTrainer:
         if self._want_native_mlp():
             from ..ops.mlp import MLPEngine
             self.mlp = MLPEngine(self.model, self.flat)
+            self.mlp.prefetch = cfg.engine_opts.mlp_prefetch
         elif self._want_native():
             from .engine import CNNEngine
             self.shadow = torch.empty(self.flat.numel, dtype=torch.bfloat16, device=self.device)

@@ -47,11 +47,13 @@ class EngineOpts:
     serial_bwd_min_b: int = 1024      # learner batches from this size run the backward on one stream
     conv1_wgrad_min_b: int = 1024     # per-sample conv1 weight-gradient kernel from this many rows (else GEMM)
     nhwc_wgrad_min_b: int = 1024      # conv2/conv3 weight-gradient kernels from this many rows (else GEMM)
+    mlp_prefetch: bool = True         # MLP engine train launch: every layer's weights requested at entry (LDS-DMA touch)
     conv1_fold: bool = False          # learner batches below trunk_bwd_persist_min_b: the per-sample trunk backward also
                                       # writes each sample's conv1 weight-gradient plane (no conv1 product in the wgrad launch)
     trunk_bwd_v2: bool = False        # trunk data-gradient chain as trunk_bwd2.hip (transposed 32x32x16 MFMAs, direct epilogues)
     trunk_bwd_persist_min_b: int = 1024   # persistent trunk backward (weights in registers) from this many rows
     trunk_bwd_persist: int = 256      # its workgroups
+    bias_rows_acc: bool = True        # ... each summing its samples' bias-gradient rows into one (finaliser: 256 rows, not B)
     wgrad_planes: int = 64            # split-K planes of the GEMM weight gradients
     conv1_planes: int = 128           # planes of the per-sample conv1 weight gradient
     nhwc_planes: int = 256            # planes of the conv2 / conv3 weight-gradient kernels

@@ -99,6 +99,7 @@ class MLPEngine:
                 kp = _ld(lay.in_features) - 4
                 self.wt[id(lay)] = torch.zeros(lay.out_features, kp, dtype=torch.float32, device=self.dev)
         self.n_weights = sum(l.in_features * l.out_features for tw in self.towers for l in tw)
+        self.prefetch = True   # train launches request every layer's weights at entry (EngineOpts.mlp_prefetch)
         self.sync_shadow()
 
     def transposes(self):
@@ -175,7 +176,8 @@ class MLPEngine:
                     self.log_std, self.ac_scale, tg, env_ids, key_shift, seed, act_out, logp_out, ent_out, v_out,
                     act_in, logp_old, adv, ret, v_old, ent_coef, kl_coef, float(vf_coef), float(ppo_clip),
                     float(v_clip or 0.0), bool(ppo), self.g_log_std if mode == 2 else None,
-                    self.mstats if mode == 2 else None, self._mpart(B) if mode == 2 else None, stamps)
+                    self.mstats if mode == 2 else None, self._mpart(B) if mode == 2 else None, stamps,
+                    self.prefetch)
 
     # ------------------------------------------------------------------------------------------- API
     def policy_step(self, obs, act_out, logp_out, ent_out, v_out, tg, env_ids, key_shift, seed):

@@ -333,8 +333,10 @@ SUMSQ_PARTS = 256   # optim.hip: partial slots of the global-norm reduction = ma
 def finalize_jobs(segments, device, return_max=False):
     """Job table of the gradient finaliser (``grad_finalize``): ``segments`` = [(dst_ptr, src_ptr, n, stride, S)]
     (``src_ptr`` 0: final already, read for the norm). Plane reductions are cut into jobs of about equal load count
-    (``n * S`` spread over the workgroups: 1024-element jobs for the many-plane conv gradients, long jobs for a
-    two-plane fc gradient of 1.6 M elements, which at 1024 elements per job would not fit the job budget), per-sample
+    (``n * S`` spread over the workgroups: 256- / 512-element jobs for the many-plane conv gradients when the budget
+    allows -- more workgroups streaming the planes; the kernel splits such a job's planes over its thread groups --,
+    long jobs for a two-plane fc gradient of 1.6 M elements, which at 1024 elements per job would not fit the job
+    budget), per-sample
     bias rows (n <= 64) take one job each, and the read-only segments share the remaining workgroups in equal
     multiples of 1024 elements; at most ``SUMSQ_PARTS`` jobs. ``S = -1`` with ``src_ptr`` 0: ``n`` presummed sums of
     squares at ``dst_ptr`` (fc_bwd's per-tile partials), one job that adds them."""
@@ -348,7 +350,12 @@ def finalize_jobs(segments, device, return_max=False):
     while True:
         jobs = [list(sg) for sg in pre] + [[dst, src, n, stride, S] for dst, src, n, stride, S in small]
         for dst, src, n, stride, S in big:
-            ch = max(1024, -(-int(target // max(1, S)) // 1024) * 1024)
+            # many-plane segments in 256-element steps (the kernel splits their planes over thread groups), the
+            # rest in multiples of 1024
+            q = 256 if S >= 16 else 1024
+            ch = max(q, -(-int(target // max(1, S)) // q) * q)
+            if q == 256 and ch > 512:
+                ch = -(-ch // 1024) * 1024
             for a in range(0, n, ch):
                 jobs.append([dst + 4 * a, src + 4 * a, min(ch, n - a), stride, S])
         left = SUMSQ_PARTS - len(jobs)

@@ -137,7 +137,7 @@ hipError_t aca_a2c_head(const float*, const int32_t*, const float*, const float*
                         const float*, int, int64_t, const float*, const float*, unsigned int*, uint64_t*, hipStream_t);
 hipError_t aca_cnn_trunk_bwd(const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*,
                              uint16_t*, uint16_t*, float*, int, uint64_t*, int, const uint8_t*, const int64_t*, float*,
-                             float, hipStream_t);
+                             float, int, hipStream_t);
 hipError_t aca_cnn_trunk_bwd2(const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*,
                               uint16_t*, uint16_t*, float*, int, uint64_t*, int, hipStream_t);
 hipError_t aca_cnn_trunk_rows(const uint8_t*, const uint16_t*, const float*, const uint16_t*, const float*,
@@ -1019,7 +1019,8 @@ void mlp_fwd(Tensor desc, int64_t tw_base, int64_t ntw, int64_t mode, int64_t ld
              c10::optional<Tensor> logp_old, c10::optional<Tensor> adv, c10::optional<Tensor> ret,
              c10::optional<Tensor> v_old, c10::optional<Tensor> ent_coef, c10::optional<Tensor> kl_coef,
              double vf_coef, double ppo_clip, double v_clip, bool ppo, c10::optional<Tensor> g_log_std,
-             c10::optional<Tensor> mstats, c10::optional<Tensor> mpart, c10::optional<Tensor> stamps) {
+             c10::optional<Tensor> mstats, c10::optional<Tensor> mpart, c10::optional<Tensor> stamps,
+             bool prefetch) {
   need(desc, at::kLong, "desc");
   TORCH_CHECK(desc.numel() * 8 >= (int64_t)(2 * sizeof(aca::MlpTower)), "mlp_fwd: desc too small");
   TORCH_CHECK(obs.is_cuda() && obs.scalar_type() == at::kFloat && obs.dim() == 2 && obs.stride(1) == 1,
@@ -1078,6 +1079,7 @@ void mlp_fwd(Tensor desc, int64_t tw_base, int64_t ntw, int64_t mode, int64_t ld
                            "mlp_fwd: mpart must hold ceil(B/16) rows of ", aca::MPART_W, " (train mode)");
   a.inv_B = B > 0 ? 1.0f / (float)B : 0.f;
   a.stamps = reinterpret_cast<int64_t*>(stamps_ptr(stamps, 2));   // [2 towers][16 phases]
+  a.prefetch = prefetch && mode == 2 ? 1 : 0;
   const bool policy = tw_base == 0;
   if (policy) {
     TORCH_CHECK(head == 1 || head == 2, "mlp_fwd: policy tower needs head 1 (categorical) or 2 (gaussian)");
@@ -1582,11 +1584,13 @@ void cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tenso
 // held in registers (cnn_trunk_bwd_persist_kernel, bit-identical): dy3 [B*49, 64] (already masked by y3 > 0), W3 [64, 576] / W2 [64, 512]
 // (OHWI bf16 shadows), masks y2 [B*81, 64] / y1 [B*400, 32]; writes dy2, dy1 (masked) and the per-sample bias
 // gradient partials biasp [B, 160] = (sum dy3 | sum dy2 | sum dy1).
+// bias_acc (persistent kernel only): biasp gets min(persist, B) rows, each the sum of its workgroup's samples' rows.
 // w1_obs / w1_planes (per-sample kernel only): the conv1 weight gradient folded in -- one [32][256] fp32 plane per
 // sample (times w1_scale), frames of sample b = w1_obs row w1_obs_idx[b] (or b)
 void cnn_trunk_bwd(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tensor dy2, Tensor dy1, Tensor biasp,
                    c10::optional<Tensor> stamps, int64_t persist, c10::optional<Tensor> w1_obs,
-                   c10::optional<Tensor> w1_obs_idx, c10::optional<Tensor> w1_planes, double w1_scale) {
+                   c10::optional<Tensor> w1_obs_idx, c10::optional<Tensor> w1_planes, double w1_scale,
+                   bool bias_acc) {
   for (auto* t : {&dy3, &W3, &y2, &W2, &y1, &dy2, &dy1}) need(*t, at::kBFloat16, "trunk_bwd bf16 operand");
   need(biasp, at::kFloat, "biasp");
   TORCH_CHECK(dy3.numel() % (49 * 64) == 0, "cnn_trunk_bwd: dy3 must be [B*49, 64]");
@@ -1595,6 +1599,7 @@ void cnn_trunk_bwd(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tenso
   TORCH_CHECK(y2.numel() >= B * 81 * 64 && y1.numel() >= B * 400 * 32 && dy2.numel() >= B * 81 * 64 &&
                   dy1.numel() >= B * 400 * 32 && biasp.numel() >= B * 160,
               "cnn_trunk_bwd: buffers too small");
+  TORCH_CHECK(!bias_acc || persist > 0, "cnn_trunk_bwd: bias_acc needs the persistent kernel");
   const uint8_t* wo = nullptr;
   const int64_t* wi = nullptr;
   float* wp = nullptr;
@@ -1617,7 +1622,8 @@ void cnn_trunk_bwd(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tenso
   }
   check(aca_cnn_trunk_bwd(ptr<uint16_t>(dy3), ptr<uint16_t>(W3), ptr<uint16_t>(y2), ptr<uint16_t>(W2),
                           ptr<uint16_t>(y1), ptr<uint16_t>(dy2), ptr<uint16_t>(dy1), ptr<float>(biasp), (int)B,
-                          stamps_ptr(stamps, B), (int)persist, wo, wi, wp, (float)w1_scale, cur_stream(dy3)),
+                          stamps_ptr(stamps, B), (int)persist, wo, wi, wp, (float)w1_scale, bias_acc ? 1 : 0,
+                          cur_stream(dy3)),
         "cnn_trunk_bwd");
 }
 
@@ -2002,7 +2008,7 @@ TORCH_LIBRARY(acamd, m) {
         "int A, Tensor? log_std, Tensor? ac_scale, Tensor? tg, Tensor? env_ids, int key_shift, int seed, "
         "Tensor? act_out, Tensor? logp_out, Tensor? ent_out, Tensor? v_out, Tensor? act_in, Tensor? logp_old, "
         "Tensor? adv, Tensor? ret, Tensor? v_old, Tensor? ent_coef, Tensor? kl_coef, float vf_coef, float ppo_clip, "
-        "float v_clip, bool ppo, Tensor? g_log_std, Tensor? mstats, Tensor? mpart=None, Tensor? stamps=None) -> ()");
+        "float v_clip, bool ppo, Tensor? g_log_std, Tensor? mstats, Tensor? mpart=None, Tensor? stamps=None, bool prefetch=False) -> ()");
   m.def("mlp_wgrad(Tensor desc, int ntw, int B, int nsplit, int items0, int items1, Tensor? parts0, "
         "Tensor? parts1, float clip0, float clip1, Tensor? g_log_std, int A, Tensor? mstats, Tensor? stats, "
         "Tensor? ent_coef, Tensor? kl_coef, Tensor? mpart=None, int mpart_rows=0, Tensor? bump=None) -> ()");
@@ -2026,7 +2032,7 @@ TORCH_LIBRARY(acamd, m) {
         "Tensor? copy_out=None, Tensor? obs_idx=None) -> ()");
   m.def("cnn_trunk_bwd(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tensor dy2, Tensor dy1, "
         "Tensor biasp, Tensor? stamps=None, int persist=0, Tensor? w1_obs=None, Tensor? w1_obs_idx=None, "
-        "Tensor? w1_planes=None, float w1_scale=1.0) -> ()");
+        "Tensor? w1_planes=None, float w1_scale=1.0, bool bias_acc=False) -> ()");
   m.def("cnn_trunk_bwd2(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tensor dy2, Tensor dy1, "
         "Tensor biasp, Tensor? stamps=None, int max_wg=0) -> ()");
   m.def("grad_finalize(Tensor jobs, Tensor partial, Tensor? spart=None, int B=0, Tensor? ent_coef=None, "

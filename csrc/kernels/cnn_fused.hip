@@ -1888,7 +1888,11 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_kernel(
 __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
     const u16* __restrict__ dy3g, const u16* __restrict__ W3, const u16* __restrict__ y2g,
     const u16* __restrict__ W2, const u16* __restrict__ y1g, u16* __restrict__ dy2g, u16* __restrict__ dy1g,
-    float* __restrict__ biasp, int B, uint64_t* __restrict__ stamps) {
+    float* __restrict__ biasp, int B, uint64_t* __restrict__ stamps, int bias_acc) {
+  // bias_acc: the bias-gradient partials summed over the workgroup's samples (in walk order) into ONE row per
+  // workgroup, biasp[blockIdx.x] -- gridDim.x rows for the finaliser instead of B (its latency-bound walk over the
+  // per-sample rows was the longest job of the Breakout finaliser)
+  float bacc = 0.f, bacc1 = 0.f;
   // diagnostics: phase stamps of the first two samples of every workgroup ([blockIdx][16]: 8 per sample)
   auto pst = [&](int it, int k) {
     if (stamps && it < 2 && threadIdx.x == 0)
@@ -2097,7 +2101,8 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
         float v = 0.f;
 #pragma unroll
         for (int w = 0; w < 8; ++w) v += s_red[w * 128 + tid];
-        biasp[(size_t)b * 160 + tid] = v;                      // db3 (0..63) | db2 (64..127)
+        if (bias_acc) bacc += v;
+        else biasp[(size_t)b * 160 + tid] = v;                 // db3 (0..63) | db2 (64..127)
       }
       const int n = nt * 16 + l16;
       // outputs past the class's 100 go to an unread slot (the dead y2-mask region behind the [400][32] dy1 rows)
@@ -2141,9 +2146,14 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
       float v = 0.f;
 #pragma unroll
       for (int w = 0; w < 8; ++w) v += s_red[1024 + w * 32 + tid];
-      biasp[(size_t)b * 160 + 128 + tid] = v;
+      if (bias_acc) bacc1 += v;
+      else biasp[(size_t)b * 160 + 128 + tid] = v;
     }
     pst(it, 5);
+  }
+  if (bias_acc) {
+    if (tid < 128) biasp[(size_t)blockIdx.x * 160 + tid] = bacc;
+    if (tid < 32) biasp[(size_t)blockIdx.x * 160 + 128 + tid] = bacc1;
   }
 }
 
@@ -2237,8 +2247,9 @@ extern "C" hipError_t aca_cnn_trunk_rows(const uint8_t* obs, const uint16_t* W1,
 extern "C" hipError_t aca_cnn_trunk_bwd(const uint16_t* dy3, const uint16_t* W3, const uint16_t* y2, const uint16_t* W2,
                                         const uint16_t* y1, uint16_t* dy2, uint16_t* dy1, float* biasp, int B,
                                         uint64_t* stamps, int persist, const uint8_t* w1_obs,
-                                        const int64_t* w1_obs_idx, float* w1_planes, float w1_scale,
+                                        const int64_t* w1_obs_idx, float* w1_planes, float w1_scale, int bias_acc,
                                         hipStream_t stream) {
+  // bias_acc (persistent form): one bias-gradient row per workgroup (min(persist, B) rows) instead of one per sample
   // w1_obs: the conv1 weight gradient folded into the per-sample kernel (one [32][256] plane per sample)
   if (B <= 0) return hipSuccess;
   for (const void* p : {(const void*)dy3, (const void*)W3, (const void*)y2, (const void*)W2, (const void*)y1,
@@ -2246,7 +2257,8 @@ extern "C" hipError_t aca_cnn_trunk_bwd(const uint16_t* dy3, const uint16_t* W3,
     if (reinterpret_cast<uintptr_t>(p) % 16) return hipErrorInvalidValue;
   if (persist > 0)
     aca::cnn_trunk_bwd_persist_kernel<<<persist < B ? persist : B, aca::BW_T, 0, stream>>>(dy3, W3, y2, W2, y1, dy2,
-                                                                                             dy1, biasp, B, stamps);
+                                                                                             dy1, biasp, B, stamps,
+                                                                                             bias_acc);
   else if (w1_obs) {
     if (!w1_planes || reinterpret_cast<uintptr_t>(w1_obs) % 16) return hipErrorInvalidValue;
     const aca::W1Fold wf{w1_obs, w1_obs_idx, w1_planes, w1_scale};

@@ -278,6 +278,27 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
     s_grow[threadIdx.x] = g;
   }
   __syncthreads();
+  // ---- train: every layer's weights (forward shadow Wt and, for the data-gradient chain, W) requested at entry, one
+  // dword per 128-byte line by LDS-DMA into a dead slot (no registers, nothing waits on it): the optimiser step just
+  // rewrote them, so each layer's own loads would otherwise start a cold miss only once the previous layer is done.
+  // The tower's workgroups on one XCD (linear id % 8 when the row tiles are a multiple of 8) split the lines.
+  __shared__ float s_pf[64];
+  if (a.mode == 2 && a.prefetch) {
+    const bool split = (gridDim.x & 7) == 0;
+    const int per = split ? (int)gridDim.x >> 3 : 1, me = split ? (int)blockIdx.x >> 3 : 0;
+    const int step = per * MLP_THREADS;
+    for (int l = 0; l < nl; ++l) {
+      const int K = s_in[l], N = s_out[l];
+      for (int rg = (l == 0 ? 0 : -1); rg < 1; ++rg) {   // rg -1: W (row-major, data-gradient), 0: Wt (forward)
+        const float* base = reinterpret_cast<const float*>(rg < 0 ? s_W[l] : s_Wt[l]);
+        const int n = rg < 0 ? K * N : N * 16 * ngp2(K);
+        const int lines = (n + 31) >> 5;
+        for (int i = me + per * (int)threadIdx.x; i < lines; i += step)
+          __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(base + ((size_t)i << 5)),
+                                           (__attribute__((address_space(3))) void*)s_pf, 4, 0, 0);
+      }
+    }
+  }
   stamp(1);
   // ---- input tile (gathered rows; padded rows / columns are zero)
   for (int e = threadIdx.x; e < MLP_BM * ld0; e += MLP_THREADS) {
@@ -539,6 +560,8 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
     nxt = tmp;
   }
   cstamp(13);
+  // the prefetch DMA must land before the workgroup's LDS is handed to another workgroup
+  if (a.prefetch) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // ------------------------------------------------------------------------------------------------ weight grads

@@ -49,6 +49,7 @@ struct MlpArgs {
   float* mpart;               // optional [ceil(B/16)][MPART_W]: per-workgroup partials instead of the atomics above
   float inv_B;
   int64_t* stamps;            // optional diagnostics: [2 towers][16] s_memrealtime at phase ends of workgroup (0, tower)
+  int prefetch;               // train: touch this workgroup's share of the tower's weights at entry (LDS-DMA, no registers)
 };
 
 struct WgradArgs {

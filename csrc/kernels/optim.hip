@@ -369,6 +369,7 @@ __global__ void __launch_bounds__(OPT_THREADS) opt_multi_kernel(OptMulti M, floa
 // Job record (8 int64 words): dst, src, n, stride, S, (unused x3). dst / src / stride are float4-aligned when the
 // job's flag word 5 is 1 (host-checked). src = 0, S = -1: dst holds n presummed sums of squares (added, not squared).
 constexpr int FIN_WORDS = 8;
+constexpr int FIN_RND = 32;   // 16-byte loads per thread in flight in the many-plane reductions (was 16)
 
 // One finaliser job (record w) by the whole workgroup; returns this thread's share of the sum of squares of the
 // final gradient. FUSED (the finaliser + optimiser kernel below): the final values go to `out` (LDS, job-local
@@ -418,20 +419,20 @@ __device__ __forceinline__ float fin_job(const int64_t* __restrict__ w, float* _
     }
   } else if (n <= 64 && vec && (n & 3) == 0) {
     // few elements, many planes (per-sample bias rows, up to one per learner sample): 16 float4 columns x 16 plane
-    // groups, 16 16-byte loads in flight per thread (4x the bytes in flight of the scalar form -- this reduction is
-    // latency-bound: one workgroup walks B planes), groups combined in LDS in group order
+    // groups, FIN_RND 16-byte loads in flight per thread (this reduction is latency-bound: one workgroup walks B
+    // planes in B / (16 FIN_RND) dependent rounds), groups combined in LDS in group order
     const int c4 = tid & 15, pg = tid >> 4, n4 = n >> 2;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     if (c4 < n4) {
-      for (int z0 = pg; z0 < S; z0 += 256) {
-        float4 v[16];
+      for (int z0 = pg; z0 < S; z0 += 16 * FIN_RND) {
+        float4 v[FIN_RND];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) {
+        for (int u = 0; u < FIN_RND; ++u) {
           const int z = z0 + 16 * u;
           v[u] = *reinterpret_cast<const float4*>(src + (int64_t)(z < S ? z : pg) * stride + 4 * c4);
         }
 #pragma unroll
-        for (int u = 0; u < 16; ++u)
+        for (int u = 0; u < FIN_RND; ++u)
           if (z0 + 16 * u < S) { acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w; }
       }
     }
@@ -509,11 +510,46 @@ __device__ __forceinline__ float fin_job(const int64_t* __restrict__ w, float* _
       if constexpr (FUSED) out[i] = v; else dst[i] = v;
       s += v * v;
     }
+  } else if (vec && S >= 16 && n <= 512 && (n & 3) == 0) {
+    // many planes of a short chunk (the conv weight-gradient jobs cut at 256 / 512 elements so that more workgroups
+    // stream the planes): the planes split into G contiguous ranges, one per thread group (G = 4 of 64 float4
+    // columns, or 2 of 128), each walked in plane order with FIN_RND loads in flight, the G partial columns added in
+    // group order through LDS
+    const int n4 = n >> 2, G = n4 <= 64 ? 4 : 2, cols = OPT_THREADS / G;
+    const int c4 = tid % cols, g = tid / cols;
+    const int z_lo = (int)((int64_t)S * g / G), z_hi = (int)((int64_t)S * (g + 1) / G);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c4 < n4) {
+      for (int z0 = z_lo; z0 < z_hi; z0 += FIN_RND) {
+        float4 v[FIN_RND];
+#pragma unroll
+        for (int u = 0; u < FIN_RND; ++u) {
+          const int z = z0 + u < z_hi ? z0 + u : z_lo;
+          v[u] = *reinterpret_cast<const float4*>(src + (int64_t)z * stride + 4 * (int64_t)c4);
+        }
+#pragma unroll
+        for (int u = 0; u < FIN_RND; ++u)
+          if (z0 + u < z_hi) { acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w; }
+      }
+    }
+    float4* red4 = reinterpret_cast<float4*>(red);   // [G][cols] float4 (256 x 16 bytes)
+    __syncthreads();
+    red4[g * cols + c4] = acc;
+    __syncthreads();
+    if (tid < n4) {
+      float4 v = red4[tid];
+      for (int k = 1; k < G; ++k) {
+        const float4 w = red4[k * cols + tid];
+        v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+      }
+      if constexpr (FUSED) reinterpret_cast<float4*>(out)[tid] = v; else reinterpret_cast<float4*>(dst)[tid] = v;
+      s = v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+    }
   } else if (vec) {
-    // planes, float4 elements: 16 planes per round in flight (the rounds are dependent memory round trips: 4 of
-    // them for the headline's 64 weight-gradient planes, not 8), elements striding over the workgroup; the adds run
-    // in plane order whatever the round size
-    constexpr int RND = 16;
+    // planes, float4 elements: FIN_RND planes per round in flight (the rounds are dependent memory round trips: 8 of
+    // them for a 256-plane conv weight gradient), elements striding over the workgroup; the adds run in plane order
+    // whatever the round size
+    constexpr int RND = FIN_RND;
     const int n4 = n >> 2;
     for (int i = tid; i < n4; i += OPT_THREADS) {
       float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -586,7 +622,7 @@ __device__ __forceinline__ void a2c_stats_duty(const StatsDuty& d) {
 __global__ void __launch_bounds__(OPT_THREADS) grad_finalize_kernel(const int64_t* __restrict__ jobs, int njobs,
                                                                     float* __restrict__ partial, StatsDuty sd) {
   __shared__ float sh[16];
-  __shared__ float red[16 * 64];
+  __shared__ __attribute__((aligned(16))) float red[16 * 64];
   if ((int)blockIdx.x == njobs) {   // past the jobs: the statistics duty (its partial slot is zeroed by workgroup 0)
     a2c_stats_duty(sd);
     return;

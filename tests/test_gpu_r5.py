@@ -371,3 +371,37 @@ def test_conv1_fold_update_tracks_grouped_wgrad(cuda, algo, kw):
     # integer pixels and scales the fp32 sums
     assert float((g0 - g1).norm() / g0.norm()) < 5e-3
     assert (d0 - d1).norm() / d0.norm() < 1e-2, float((d0 - d1).norm() / d0.norm())
+
+
+@pytest.mark.parametrize("B,persist", [(1100, 256), (300, 7)])
+def test_trunk_bwd_persist_bias_rows_accumulated_per_workgroup(cuda, B, persist):
+    """cnn_trunk_bwd_persist with bias_acc: dy2 / dy1 bit-identical to the per-sample-row form, and row w of biasp ==
+    the fp32 sum, in walk order (samples w, w + grid, ...), of the per-sample rows the plain form writes."""
+    from actor_critic_algs_on_tensorflow_amd import _native
+    ops = _native.require()
+    g = torch.Generator(device="cpu").manual_seed(B)
+    dy3 = (torch.randn(B, 7, 7, 64, generator=g) * (torch.rand(B, 7, 7, 64, generator=g) > 0.4)).to(torch.bfloat16)
+    W3 = (torch.randn(64, 3, 3, 64, generator=g) * 0.05).to(torch.bfloat16)
+    W2 = (torch.randn(64, 4, 4, 32, generator=g) * 0.05).to(torch.bfloat16)
+    y2 = (torch.rand(B, 9, 9, 64, generator=g) - 0.3).clamp(min=0).to(torch.bfloat16)
+    y1 = (torch.rand(B, 20, 20, 32, generator=g) - 0.3).clamp(min=0).to(torch.bfloat16)
+    dev = [t.to(cuda) for t in (dy3, W3, y2, W2, y1)]
+    args = (dev[0].reshape(B * 49, 64), dev[1].reshape(64, 576), dev[2].reshape(B * 81, 64), dev[3].reshape(64, 512),
+            dev[4].reshape(B * 400, 32))
+    res = []
+    for acc in (False, True):
+        dy2 = torch.full((B * 81, 64), float("nan"), dtype=torch.bfloat16, device=cuda)
+        dy1 = torch.full((B * 400, 32), float("nan"), dtype=torch.bfloat16, device=cuda)
+        bp = torch.full((B, 160), float("nan"), device=cuda)
+        ops.cnn_trunk_bwd(*args, dy2, dy1, bp, None, persist, None, None, None, 1.0, acc)
+        torch.cuda.synchronize()
+        res.append((dy2.view(torch.int16).clone(), dy1.view(torch.int16).clone(), bp.cpu()))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    rows, got = res[0][2], res[1][2]
+    grid = min(persist, B)
+    for w in range(grid):
+        ref = torch.zeros(160)
+        for b in range(w, B, grid):
+            ref = ref + rows[b]
+        assert torch.equal(got[w], ref), w
+    assert torch.isnan(got[grid:]).all(), "rows past the grid are not written"

@@ -99,7 +99,7 @@ class MLPEngine:
                 kp = _ld(lay.in_features) - 4
                 self.wt[id(lay)] = torch.zeros(lay.out_features, kp, dtype=torch.float32, device=self.dev)
         self.n_weights = sum(l.in_features * l.out_features for tw in self.towers for l in tw)
-        self.prefetch = True   # train launches request every layer's weights at entry (EngineOpts.mlp_prefetch)
+        self.prefetch = False  # train launches request every layer's weights at entry (EngineOpts.mlp_prefetch)
         self.sync_shadow()
 
     def transposes(self):

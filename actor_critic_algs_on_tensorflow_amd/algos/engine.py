@@ -488,11 +488,12 @@ class CNNEngine:
             self._wgrad("W1", self.gW1, b.dy1, 32, b.obs, 0, 32, 256, B * 400, ws, [1, B, 4, 84, 84, 8, 8, 4],
                         1.0 / 255.0)
             return
-        P = max(1, min(self.conv1_planes, B))
+        v2 = self.opts.conv1_wgrad_v2
+        P = max(1, min(self.opts.conv1_v2_planes if v2 else self.conv1_planes, B))
         buf = self._planes.get("W1")
         if buf is None or buf.numel() < P * 32 * 256:
             buf = self._plane_buf("W1", max(P, self.wgrad_planes) * 32 * 256)
-        _native.require().conv1_wgrad(b.obs, b.dy1, buf, P, 1.0 / 255.0, getattr(b, "obs_idx", None))
+        _native.require().conv1_wgrad(b.obs, b.dy1, buf, P, 1.0 / 255.0, getattr(b, "obs_idx", None), v2)
         self._wsplits["W1"] = P
         self._cur_planes["W1"] = P
 

@@ -57,6 +57,8 @@ class EngineOpts:
     bias_rows_acc: bool = True        # ... each summing its samples' bias-gradient rows into one (finaliser: 256 rows, not B)
     wgrad_planes: int = 64            # split-K planes of the GEMM weight gradients
     conv1_planes: int = 128           # planes of the per-sample conv1 weight gradient
+    conv1_wgrad_v2: bool = True       # ... as conv1_wgrad2 (all 4 channels per workgroup, 32x32x16 MFMAs)
+    conv1_v2_planes: int = 256        # its planes (one workgroup each)
     nhwc_planes: int = 256            # planes of the conv2 / conv3 weight-gradient kernels
 
     def replace(self, **kw):

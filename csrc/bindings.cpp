@@ -87,6 +87,7 @@ hipError_t aca_mb_gather(const uint8_t*, int64_t, const int*, const float*, cons
                          const double*, float, unsigned int*, int64_t*, hipStream_t);
 hipError_t aca_ev_multi(const float*, const float*, float*, int, double*, unsigned int*, hipStream_t);
 hipError_t aca_conv1_wgrad(const uint8_t*, const uint16_t*, float*, int, int, float, const int64_t*, hipStream_t);
+hipError_t aca_conv1_wgrad2(const uint8_t*, const uint16_t*, float*, int, int, float, const int64_t*, hipStream_t);
 hipError_t aca_conv_wgrad_nhwc(int, const uint16_t*, const uint16_t*, float*, int, int, hipStream_t);
 hipError_t aca_conv_wgrad_gemm(int, const uint16_t*, const uint16_t*, float*, int, int, hipStream_t);
 hipError_t aca_gemm_big(const AcaGemmDesc*, hipStream_t);
@@ -705,7 +706,9 @@ void returns_scan(Tensor r, Tensor v, Tensor d, Tensor ret, Tensor adv, int64_t 
 // conv1 weight gradient as P partial planes [P][32][256] (conv_wgrad.hip): obs uint8 [B, 4, 84, 84], dy1 bf16
 // [B * 400, 32]; plane g holds samples [g B / P, (g + 1) B / P).
 // obs_idx (optional int64 [B]): sample b's frames are row obs_idx[b] of obs (a PPO minibatch gathered by index)
-void conv1_wgrad(Tensor obs, Tensor dy1, Tensor planes, int64_t P, double scale, c10::optional<Tensor> obs_idx) {
+// v2: conv1_wgrad2_kernel (all four channels per workgroup, 32x32x16 MFMAs; grid P instead of 4 P)
+void conv1_wgrad(Tensor obs, Tensor dy1, Tensor planes, int64_t P, double scale, c10::optional<Tensor> obs_idx,
+                 bool v2) {
   TORCH_CHECK(obs.is_cuda() && obs.is_contiguous() && obs.scalar_type() == at::kByte, "conv1_wgrad: obs uint8");
   need(dy1, at::kBFloat16, "conv1_wgrad dy1");
   need(planes, at::kFloat, "conv1_wgrad planes");
@@ -722,8 +725,8 @@ void conv1_wgrad(Tensor obs, Tensor dy1, Tensor planes, int64_t P, double scale,
   TORCH_CHECK(P >= 1 && P <= 1024 && planes.numel() >= P * 32 * 256, "conv1_wgrad: planes too small");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(obs.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(dy1.data_ptr()) % 16 == 0,
               "conv1_wgrad: 16-byte aligned operands");
-  check(aca_conv1_wgrad(obs.data_ptr<uint8_t>(), ptr<uint16_t>(dy1), ptr<float>(planes), (int)B, (int)P, (float)scale,
-                        idx, cur_stream(obs)),
+  check((v2 ? aca_conv1_wgrad2 : aca_conv1_wgrad)(obs.data_ptr<uint8_t>(), ptr<uint16_t>(dy1), ptr<float>(planes),
+                                                  (int)B, (int)P, (float)scale, idx, cur_stream(obs)),
         "conv1_wgrad");
 }
 
@@ -1978,7 +1981,8 @@ TORCH_LIBRARY(acamd, m) {
   m.def("gemm_group_begin() -> ()", &gemm_group_begin);
   m.def("gemm_group_end() -> int", &gemm_group_end);
   m.def("gemm_group_pause(bool paused) -> ()", &gemm_group_pause);
-  m.def("conv1_wgrad(Tensor obs, Tensor dy1, Tensor planes, int P, float scale, Tensor? obs_idx=None) -> ()");
+  m.def("conv1_wgrad(Tensor obs, Tensor dy1, Tensor planes, int P, float scale, Tensor? obs_idx=None, "
+        "bool v2=False) -> ()");
   m.def("conv_wgrad_nhwc(int layer, Tensor img, Tensor dy, Tensor planes, int P) -> ()");
   m.def("conv_wgrad_gemm(int layer, Tensor img, Tensor dy, Tensor planes, int P) -> ()");
   m.def("mb_gather(Tensor obs, Tensor act, Tensor logp, Tensor adv, Tensor ret, Tensor v, Tensor? o_obs, "

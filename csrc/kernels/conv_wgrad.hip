@@ -183,6 +183,139 @@ __global__ void __launch_bounds__(CW_T) conv1_wgrad_kernel(const uint8_t* __rest
 
 
 // ------------------------------------------------------------------------------------------------------------
+// conv1 weight gradient, all four input channels per workgroup on the 32x32x16 MFMA (conv1_wgrad2_kernel):
+//   the kernel above stages a sample's dy1 rows once PER CHANNEL (four workgroups read and stage the same 25.6 KB)
+//   and keeps 16x16 tiles, so it is bound by staging and LDS reads (48 % bank conflicts, ~380 TF/s at B = 4096).
+//   Here workgroup g walks the samples of plane g and stages, per sample, the dy1 rows [416][32] (64-byte rows: the 4
+//   rows of a transposing read land in disjoint bank windows) and all four frames as exact bf16 (56 KB) ONCE; the next
+//   sample is in flight in registers. Wave w = (k quarter w >> 1, column half w & 1) owns a 32 x 128 output slice
+//   (four 32x32 fp32 accumulators) over the k-steps ks = kq, kq + 4, ... of 16 positions: per k-step one A fragment
+//   (dy1 rows, two transposing reads) feeds four MFMAs whose B fragments point each lane's transposing read at the 4
+//   contiguous frame pixels of its (position, ch, ky, kx0..kx0+3) -- no im2col. The k quarters meet in LDS in order
+//   at the end; plane g ([32][256] fp32) is written once, scaled. Deterministic (fixed order, no atomics).
+// ------------------------------------------------------------------------------------------------------------
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+constexpr int C2_T = 512;
+constexpr int C2_FR = 4 * 84 * 84;                 // 28224 frame pixels per sample (bf16 in LDS) + a zero chunk
+constexpr int C2_FR4 = C2_FR / 16;                 // 1764 16-byte chunks of uint8 pixels
+constexpr int C2_DY4 = 400 * 4;                    // 1600 16-byte chunks of dy1
+constexpr int C2_DYOFF = (C2_FR + 8) * 2;          // byte offset of the dy1 rows in LDS
+constexpr int C2_RED = 3 * 2 * 32 * 128 * 4;       // k-quarter partials at the end (96 KB, aliases the staging)
+constexpr int C2_LDS = C2_RED > C2_DYOFF + 416 * 64 ? C2_RED : C2_DYOFF + 416 * 64;
+static_assert(C2_DYOFF % 16 == 0 && C2_FR4 <= 4 * C2_T && C2_DY4 <= 4 * C2_T, "conv1_wgrad2 staging geometry");
+
+__global__ void __launch_bounds__(C2_T) conv1_wgrad2_kernel(const uint8_t* __restrict__ obs,
+                                                            const u16* __restrict__ dy1, float* __restrict__ planes,
+                                                            int B, int P, float scale,
+                                                            const int64_t* __restrict__ obs_idx) {
+  __shared__ __attribute__((aligned(16))) unsigned char s_raw[C2_LDS];
+  u16* const s_fr = reinterpret_cast<u16*>(s_raw);
+  u16* const s_dy = reinterpret_cast<u16*>(s_raw + C2_DYOFF);
+  const int g = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int b0 = (int)((int64_t)g * B / P), b1 = (int)((int64_t)(g + 1) * B / P);
+  const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
+  // padding positions 400..415: zero dy1 rows and the zero frame chunk, written once (never restaged)
+  if (tid < 64) *reinterpret_cast<uint4*>(s_dy + 400 * 32 + tid * 8) = z4;
+  if (tid == 0) *reinterpret_cast<uint4*>(s_fr + C2_FR) = z4;
+
+  uint4 f0, f1, f2, f3, d0, d1, d2, d3;   // the next sample (named registers: arrays of uint4 went to scratch)
+  auto load = [&](int b) {
+    const uint4* f = reinterpret_cast<const uint4*>(obs + (size_t)(obs_idx ? obs_idx[b] : b) * C2_FR);
+    const uint4* d = reinterpret_cast<const uint4*>(dy1 + (size_t)b * 400 * 32);
+    f0 = f[tid];
+    f1 = f[tid + C2_T];
+    f2 = f[tid + 2 * C2_T];
+    f3 = f[min(tid + 3 * C2_T, C2_FR4 - 1)];
+    d0 = d[tid];
+    d1 = d[tid + C2_T];
+    d2 = d[tid + 2 * C2_T];
+    d3 = d[min(tid + 3 * C2_T, C2_DY4 - 1)];
+  };
+  auto put_fr = [&](const uint4& w, int i) {
+    const uint2 a = cw_u8x4(w.x), b_ = cw_u8x4(w.y), c = cw_u8x4(w.z), d = cw_u8x4(w.w);
+    *reinterpret_cast<uint4*>(s_fr + i * 16) = make_uint4(a.x, a.y, b_.x, b_.y);
+    *reinterpret_cast<uint4*>(s_fr + i * 16 + 8) = make_uint4(c.x, c.y, d.x, d.y);
+  };
+  auto store = [&]() {
+    put_fr(f0, tid);
+    put_fr(f1, tid + C2_T);
+    put_fr(f2, tid + 2 * C2_T);
+    if (tid + 3 * C2_T < C2_FR4) put_fr(f3, tid + 3 * C2_T);
+    *reinterpret_cast<uint4*>(s_dy + tid * 8) = d0;
+    *reinterpret_cast<uint4*>(s_dy + (tid + C2_T) * 8) = d1;
+    *reinterpret_cast<uint4*>(s_dy + (tid + 2 * C2_T) * 8) = d2;
+    if (tid + 3 * C2_T < C2_DY4) *reinterpret_cast<uint4*>(s_dy + (tid + 3 * C2_T) * 8) = d3;
+  };
+
+  const int nh = wid & 1, kq = wid >> 1;
+  // lane roles of the transposing reads: 16-lane group gl, lane 4 q + p4 of the group
+  const int gl = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3;
+  const int acol = (gl & 1) * 16 + 4 * p4, khalf = 8 * (gl >> 1);
+  int noff[4];   // (ch, ky, kx0) pixel offset of this lane's 4 B columns, per 32-column tile
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int c = nh * 128 + t * 32 + (gl & 1) * 16 + 4 * p4;
+    noff[t] = (c >> 6) * 7056 + ((c >> 3) & 7) * 84 + (c & 7);
+  }
+  floatx16 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+  typedef short short4x __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) short4x lds4;
+  auto pos = [&](int p) -> int {   // frame offset of position p's (4 oy, 4 ox) pixel; padding -> -1
+    const int oy = (p * 3277) >> 16;   // p / 20 for p < 5000
+    return p < 400 ? (4 * oy) * 84 + 4 * (p - 20 * oy) : -1;
+  };
+  if (b0 < b1) load(b0);
+  for (int b = b0; b < b1; ++b) {
+    store();
+    __syncthreads();
+    if (b + 1 < b1) load(b + 1);
+    for (int ks = kq; ks < 26; ks += 4) {
+      const int kb = ks * 16 + khalf;
+      const short4x a_lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(s_dy + (kb + q) * 32 + acol));
+      const short4x a_hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(s_dy + (kb + 4 + q) * 32 + acol));
+      const cw_short8 av = {a_lo[0], a_lo[1], a_lo[2], a_lo[3], a_hi[0], a_hi[1], a_hi[2], a_hi[3]};
+      const bf16x8 af = __builtin_bit_cast(bf16x8, av);
+      const int pa = pos(kb + q), pb = pos(kb + 4 + q);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const short4x lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(s_fr + (pa < 0 ? C2_FR : pa + noff[t])));
+        const short4x hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(s_fr + (pb < 0 ? C2_FR : pb + noff[t])));
+        const cw_short8 bv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, __builtin_bit_cast(bf16x8, bv), acc[t], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  // k quarters 1..3 -> LDS, quarter 0 adds them in order and writes the plane
+  float* const red = reinterpret_cast<float*>(s_raw);
+  if (kq > 0)
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) red[(((kq - 1) * 2 + nh) * 64 + t * 16 + i) * 64 + lane] = acc[t][i];
+  __syncthreads();
+  if (kq == 0) {
+    float* const dst = planes + (size_t)g * 32 * 256;
+    const int col = lane & 31, rh = 4 * (lane >> 5);
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float v = acc[t][i];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) v += red[((k * 2 + nh) * 64 + t * 16 + i) * 64 + lane];
+        const int o = (i & 3) + 8 * (i >> 2) + rh;
+        dst[o * 256 + nh * 128 + t * 32 + col] = v * scale;
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
 // Per-sample weight gradient of a bf16 NHWC conv layer (conv2: y1 [20][20][32] -> 9x9, 4x4 stride 2; conv3: y2
 // [9][9][64] -> 7x7, 3x3 stride 1; 64 output channels, OHWI weights [64][KS KS C]), same scheme as conv1 above:
 //   dW[o][(ky, kx, c)] = sum_b sum_p dy[b][p][o] * img[b][S oy + ky][S ox + kx][c]
@@ -325,8 +458,6 @@ __global__ void __launch_bounds__(512) conv_wgrad_nhwc_kernel(const u16* __restr
 // (position, ky, kx, c0) pixel, no column matrix. Plane g (samples [g B / P, (g + 1) B / P)) is written once, in
 // full; the gradient finaliser reduces the P planes in plane order (deterministic, no atomics).
 // ---------------------------------------------------------------------------------------------------------------
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-
 template <int H, int W, int C, int KS, int S, int OH, int OW, int SB>
 __global__ void __launch_bounds__(512) conv_wgrad_gemm_kernel(const u16* __restrict__ img,
                                                               const u16* __restrict__ dy,
@@ -482,6 +613,16 @@ extern "C" hipError_t aca_conv1_wgrad(const uint8_t* obs, const uint16_t* dy1, f
   if (B <= 0) return hipSuccess;
   if (P < 1 || P > 1024) return hipErrorInvalidValue;
   aca::conv1_wgrad_kernel<<<4 * P, aca::CW_T, 0, stream>>>(obs, dy1, planes, B, P, scale, obs_idx);
+  return hipGetLastError();
+}
+
+// All four channels per workgroup (conv1_wgrad2_kernel): grid P, plane g of [32][256] per workgroup.
+extern "C" hipError_t aca_conv1_wgrad2(const uint8_t* obs, const uint16_t* dy1, float* planes, int B, int P,
+                                       float scale, const int64_t* obs_idx, hipStream_t stream) {
+  if (B <= 0) return hipSuccess;
+  if (P < 1 || P > 1024 || reinterpret_cast<uintptr_t>(obs) % 16 || reinterpret_cast<uintptr_t>(dy1) % 16)
+    return hipErrorInvalidValue;
+  aca::conv1_wgrad2_kernel<<<P, aca::C2_T, 0, stream>>>(obs, dy1, planes, B, P, scale, obs_idx);
   return hipGetLastError();
 }
 

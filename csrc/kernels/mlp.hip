@@ -282,6 +282,29 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
   // dword per 128-byte line by LDS-DMA into a dead slot (no registers, nothing waits on it): the optimiser step just
   // rewrote them, so each layer's own loads would otherwise start a cold miss only once the previous layer is done.
   // The tower's workgroups on one XCD (linear id % 8 when the row tiles are a multiple of 8) split the lines.
+  // ---- train: the loss head's per-row inputs loaded now, consumed after the forward (issued behind the forward's
+  // first weight loads they were a dependent global round trip in the middle of the chain): gaussian-phase thread
+  // (r, j) the action component, row thread r the old log-prob and advantage (policy) or return and old value
+  // (critic) -- the same threads that read them below
+  const bool policy = (t == 0);
+  float e_act = 0.f, e_lo = 0.f, e_adv = 0.f, e_ret = 0.f, e_vo = 0.f;
+  int e_ai = 0;
+  if (a.mode == 2) {
+    const int r = threadIdx.x / MLP_MAXA, j = threadIdx.x % MLP_MAXA;
+    if (policy && a.head == 2 && threadIdx.x < MLP_BM * MLP_MAXA && j < a.A && r < rows)
+      e_act = a.act_f_in[s_grow[r] * a.A + j];
+    if (threadIdx.x < rows) {
+      const int64_t grow = s_grow[threadIdx.x];
+      if (policy) {
+        e_lo = a.logp_old[grow];
+        e_adv = a.adv[grow];
+        if (a.head != 2) e_ai = a.act_i_in[grow];
+      } else {
+        e_ret = a.ret[grow];
+        if (a.v_old && a.v_clip > 0.f) e_vo = a.v_old[grow];
+      }
+    }
+  }
   __shared__ float s_pf[64];
   if (a.mode == 2 && a.prefetch) {
     const bool split = (gridDim.x & 7) == 0;
@@ -336,7 +359,6 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
   const float* Yo = sm + s_yo[L];
   const int ldo = s_ld[L];
   // ---- heads: one thread per row
-  const bool policy = (t == 0);
   float* dPtop = P0;
   const int ldP = MLP_MAXW + 4;
   if (a.mode == 2) {   // zero the top dP tile (the head writes only valid columns)
@@ -367,7 +389,7 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
           aj = mu + expf(ls) * eps;
           if (live) a.act_f_out[grow * a.A + j] = aj;
         } else {
-          aj = live ? a.act_f_in[grow * a.A + j] : mu;
+          aj = live ? (a.mode == 2 ? e_act : a.act_f_in[grow * a.A + j]) : mu;
         }
         const float zz = (aj - mu) * expf(-ls);
         s_hl[r][j] = -0.5f * zz * zz - ls - HALF_LOG_2PI;
@@ -387,10 +409,10 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
       const float v = Yo[r * ldo];
       if (live && (a.mode == 0 || a.mode == 1) && a.v_out) a.v_out[grow] = v;
       if (live && a.mode == 2) {
-        const float R = a.ret[grow];
+        const float R = e_ret;
         float dv = 2.f * (v - R), l2 = (v - R) * (v - R);
         if (a.v_old && a.v_clip > 0.f) {
-          const float vo = a.v_old[grow];
+          const float vo = e_vo;
           const float d = fminf(fmaxf(v - vo, -a.v_clip), a.v_clip);
           const float vc = vo + d;
           const float l2c = (vc - R) * (vc - R);
@@ -414,7 +436,7 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
       }
       float g = 0.f;
       if (a.mode == 2 && live) {
-        const float lo = a.logp_old[grow], adv = a.adv[grow];
+        const float lo = e_lo, adv = e_adv;
         const float beta = *a.kl_coef;
         float dsurr;
         if (a.ppo) {
@@ -457,7 +479,7 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
         }
         if (live) a.act_i_out[grow] = ai;
       } else {
-        ai = live ? a.act_i_in[grow] : 0;
+        ai = live ? (a.mode == 2 ? e_ai : a.act_i_in[grow]) : 0;
       }
       const float lpa = z[ai] - lse;
       if (live && a.mode != 2) {
@@ -465,7 +487,7 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
         if (a.ent_out) a.ent_out[grow] = H;
       }
       if (a.mode == 2 && live) {
-        const float lo = a.logp_old[grow], adv = a.adv[grow];
+        const float lo = e_lo, adv = e_adv;
         const float beta = *a.kl_coef, ce = *a.ent_coef;
         float dsurr;
         if (a.ppo) {

@@ -345,18 +345,19 @@ def test_fused_rollout_step_equals_separate_policy_and_trunk(cuda, capture, monk
             assert torch.equal(x, y), (k, j)
 
 
-@pytest.mark.parametrize("B,P", [(7, 4), (160, 64), (1024, 64)])
-def test_conv1_wgrad_planes_match_autograd(cuda, B, P):
-    """Per-sample conv1 weight gradient (conv_wgrad.hip): the plane sum == the fp32 autograd conv weight gradient of
-    obs/255 and dy1, every plane holds exactly its sample range, and two runs are bit-identical."""
-    import torch.nn.functional as F
+@pytest.mark.parametrize("v2", [False, True])
+@pytest.mark.parametrize("B,P", [(7, 4), (160, 64), (1024, 64), (1100, 256)])
+def test_conv1_wgrad_planes_match_autograd(cuda, B, P, v2):
+    """Per-sample conv1 weight gradient (conv_wgrad.hip; v2: conv1_wgrad2_kernel, all channels per workgroup): the
+    plane sum == the fp32 autograd conv weight gradient of obs/255 and dy1, every plane holds exactly its sample
+    range, and two runs are bit-identical."""
     from actor_critic_algs_on_tensorflow_amd import _native
     ops = _native.require()
     g = torch.Generator(device="cpu").manual_seed(B)
     obs = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, generator=g).to(cuda)
     dy1 = (torch.randn(B * 400, 32, generator=g) * 0.1).to(torch.bfloat16).to(cuda)
-    planes = torch.full((64 * 32 * 256,), float("nan"), device=cuda)
-    ops.conv1_wgrad(obs, dy1, planes, P, 1.0 / 255.0)
+    planes = torch.full((max(64, P) * 32 * 256,), float("nan"), device=cuda)
+    ops.conv1_wgrad(obs, dy1, planes, P, 1.0 / 255.0, None, v2)
     got = planes[:P * 8192].view(P, 32, 256)
     # fp32 references on the CPU (a MIOpen weight-gradient solver is not a reliable reference, test_gpu_r3.py)
     go = dy1.float().cpu().view(B, 20, 20, 32).permute(0, 3, 1, 2)
@@ -371,8 +372,13 @@ def test_conv1_wgrad_planes_match_autograd(cuda, B, P):
                                          stride=4).reshape(32, 256).to(cuda)
         torch.testing.assert_close(got[0], r0, rtol=1e-4, atol=1e-4)
     again = torch.zeros_like(planes)
-    ops.conv1_wgrad(obs, dy1, again, P, 1.0 / 255.0)
+    ops.conv1_wgrad(obs, dy1, again, P, 1.0 / 255.0, None, v2)
     assert torch.equal(again[:P * 8192], planes[:P * 8192])
+    # frames gathered through an index (PPO minibatch rows of a larger observation buffer)
+    perm = torch.randperm(B, generator=g).to(cuda)
+    by_idx = torch.zeros_like(planes)
+    ops.conv1_wgrad(obs[perm.argsort()].contiguous(), dy1, by_idx, P, 1.0 / 255.0, perm.argsort().argsort(), v2)
+    assert torch.equal(by_idx[:P * 8192], planes[:P * 8192])
 
 
 @pytest.mark.parametrize("layer,B,P", [(2, 5, 3), (2, 300, 64), (3, 9, 4), (3, 300, 64)])

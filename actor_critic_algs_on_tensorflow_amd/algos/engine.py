@@ -447,9 +447,24 @@ class CNNEngine:
             self._cur_planes["W1f"] = b.B
             return True
         persist = self.trunk_bwd_persist if b.B >= self.trunk_bwd_persist_min_b else 0
+        acc = self.bias_rows(b.B) < b.B
+        if fold and persist and self.conv1_fold_persist_ok(b.B):
+            # one conv1 weight-gradient plane per workgroup, dy1 never stored (the fold was its only consumer)
+            R = min(persist, b.B)
+            buf = self._plane_buf("W1f", R * 32 * 256)
+            _native.require().cnn_trunk_bwd(b.dy3, self.sW3, b.y2, self.sW2, b.y1, b.dy2, b.dy1, b.biasp, None,
+                                            persist, b.obs, getattr(b, "obs_idx", None), buf, 1.0 / 255.0, acc, True)
+            self._cur_planes["W1f"] = R
+            return True
         _native.require().cnn_trunk_bwd(b.dy3, self.sW3, b.y2, self.sW2, b.y1, b.dy2, b.dy1, b.biasp, None, persist,
-                                        None, None, None, 1.0, self.bias_rows(b.B) < b.B)
+                                        None, None, None, 1.0, acc)
         return False
+
+    def conv1_fold_persist_ok(self, B):
+        """The persistent trunk backward of a ``B``-row batch also computes the conv1 weight gradient
+        (``EngineOpts.conv1_fold_persist``)."""
+        return (self.opts.conv1_fold_persist and self.dev.type == "cuda" and self.det_wgrad and self.implicit
+                and not self.opts.trunk_bwd_v2 and B >= self.trunk_bwd_persist_min_b and self.trunk_bwd_persist > 0)
 
     def bias_rows(self, B):
         """Bias-gradient partial rows the trunk backward of a ``B``-row batch leaves for the finaliser: one per

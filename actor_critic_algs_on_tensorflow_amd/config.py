@@ -49,6 +49,7 @@ class EngineOpts:
     nhwc_wgrad_min_b: int = 1024      # conv2/conv3 weight-gradient kernels from this many rows (else GEMM)
     mlp_prefetch: bool = False        # MLP engine train launch: every layer's weights requested at entry (LDS-DMA touch;
                                       # measured 13.84 vs 13.71 ms MuJoCo PPO: off)
+    conv1_fold_persist: bool = True   # ... and in the persistent trunk backward (one plane per workgroup; dy1 not stored)
     conv1_fold: bool = False          # learner batches below trunk_bwd_persist_min_b: the per-sample trunk backward also
                                       # writes each sample's conv1 weight-gradient plane (no conv1 product in the wgrad launch)
     trunk_bwd_v2: bool = False        # trunk data-gradient chain as trunk_bwd2.hip (transposed 32x32x16 MFMAs, direct epilogues)

@@ -1588,12 +1588,13 @@ void cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tenso
 // (OHWI bf16 shadows), masks y2 [B*81, 64] / y1 [B*400, 32]; writes dy2, dy1 (masked) and the per-sample bias
 // gradient partials biasp [B, 160] = (sum dy3 | sum dy2 | sum dy1).
 // bias_acc (persistent kernel only): biasp gets min(persist, B) rows, each the sum of its workgroup's samples' rows.
-// w1_obs / w1_planes (per-sample kernel only): the conv1 weight gradient folded in -- one [32][256] fp32 plane per
-// sample (times w1_scale), frames of sample b = w1_obs row w1_obs_idx[b] (or b)
+// w1_obs / w1_planes: the conv1 weight gradient folded in -- one [32][256] fp32 plane per sample (per-sample
+// kernel) or per workgroup (persistent kernel), times w1_scale; frames of sample b = w1_obs row w1_obs_idx[b] (or b).
+// skip_dy1 (persistent fold): dy1 is not stored (its only consumer is the folded weight gradient).
 void cnn_trunk_bwd(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tensor dy2, Tensor dy1, Tensor biasp,
                    c10::optional<Tensor> stamps, int64_t persist, c10::optional<Tensor> w1_obs,
                    c10::optional<Tensor> w1_obs_idx, c10::optional<Tensor> w1_planes, double w1_scale,
-                   bool bias_acc) {
+                   bool bias_acc, bool skip_dy1) {
   for (auto* t : {&dy3, &W3, &y2, &W2, &y1, &dy2, &dy1}) need(*t, at::kBFloat16, "trunk_bwd bf16 operand");
   need(biasp, at::kFloat, "biasp");
   TORCH_CHECK(dy3.numel() % (49 * 64) == 0, "cnn_trunk_bwd: dy3 must be [B*49, 64]");
@@ -1607,12 +1608,12 @@ void cnn_trunk_bwd(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tenso
   const int64_t* wi = nullptr;
   float* wp = nullptr;
   if (w1_obs.has_value() && w1_obs->defined()) {
-    TORCH_CHECK(persist <= 0, "cnn_trunk_bwd: the conv1 fold runs in the per-sample kernel only");
     need(*w1_obs, at::kByte, "w1_obs");
     TORCH_CHECK(w1_obs->is_contiguous() && w1_obs->numel() % (4 * 84 * 84) == 0, "cnn_trunk_bwd: w1_obs [*, 4, 84, 84]");
     TORCH_CHECK(w1_planes.has_value() && w1_planes->defined(), "cnn_trunk_bwd: w1_obs needs w1_planes");
     need(*w1_planes, at::kFloat, "w1_planes");
-    TORCH_CHECK(w1_planes->numel() >= B * 32 * 256, "cnn_trunk_bwd: w1_planes needs B x 8192 floats");
+    const int64_t np = persist > 0 ? std::min<int64_t>(persist, B) : B;   // one plane per workgroup
+    TORCH_CHECK(w1_planes->numel() >= np * 32 * 256, "cnn_trunk_bwd: w1_planes needs a [32][256] plane per workgroup");
     if (w1_obs_idx.has_value() && w1_obs_idx->defined()) {
       need(*w1_obs_idx, at::kLong, "w1_obs_idx");
       TORCH_CHECK(w1_obs_idx->numel() >= B, "cnn_trunk_bwd: w1_obs_idx needs B rows");
@@ -1623,8 +1624,10 @@ void cnn_trunk_bwd(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tenso
     wo = ptr<uint8_t>(*w1_obs);
     wp = ptr<float>(*w1_planes);
   }
+  TORCH_CHECK(!skip_dy1 || (wo && persist > 0), "cnn_trunk_bwd: skip_dy1 needs the persistent conv1 fold");
   check(aca_cnn_trunk_bwd(ptr<uint16_t>(dy3), ptr<uint16_t>(W3), ptr<uint16_t>(y2), ptr<uint16_t>(W2),
-                          ptr<uint16_t>(y1), ptr<uint16_t>(dy2), ptr<uint16_t>(dy1), ptr<float>(biasp), (int)B,
+                          ptr<uint16_t>(y1), ptr<uint16_t>(dy2), skip_dy1 ? nullptr : ptr<uint16_t>(dy1),
+                          ptr<float>(biasp), (int)B,
                           stamps_ptr(stamps, B), (int)persist, wo, wi, wp, (float)w1_scale, bias_acc ? 1 : 0,
                           cur_stream(dy3)),
         "cnn_trunk_bwd");
@@ -2036,7 +2039,7 @@ TORCH_LIBRARY(acamd, m) {
         "Tensor? copy_out=None, Tensor? obs_idx=None) -> ()");
   m.def("cnn_trunk_bwd(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tensor dy2, Tensor dy1, "
         "Tensor biasp, Tensor? stamps=None, int persist=0, Tensor? w1_obs=None, Tensor? w1_obs_idx=None, "
-        "Tensor? w1_planes=None, float w1_scale=1.0, bool bias_acc=False) -> ()");
+        "Tensor? w1_planes=None, float w1_scale=1.0, bool bias_acc=False, bool skip_dy1=False) -> ()");
   m.def("cnn_trunk_bwd2(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tensor dy2, Tensor dy1, "
         "Tensor biasp, Tensor? stamps=None, int max_wg=0) -> ()");
   m.def("grad_finalize(Tensor jobs, Tensor partial, Tensor? spart=None, int B=0, Tensor? ent_coef=None, "

@@ -1885,10 +1885,17 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_kernel(
 // them in registers for all of its samples; the next sample's dy3 image, y2 mask and y1 mask are loaded into
 // registers while the current one is processed. Same MFMA order per sample as the per-sample kernel: bit-identical
 // outputs.
+// W1G: the conv1 weight gradient folded in (W1Fold, as in the per-sample kernel): after a sample's dy1 rows are
+// masked they stay in LDS and its four frames (prefetched with the sample's other operands) are staged as exact bf16
+// over the dead image region (which is extended for it; the dy2 image border is then re-zeroed per sample); 13 k-steps
+// of 16x16x32 MFMAs accumulate the workgroup's [32][256] slice in registers across its samples, written once at the
+// end as plane blockIdx.x (scaled). dy1 itself is then not stored (dy1g null): conv1 is the first layer, so its
+// weight gradient was dy1's only consumer -- the 105 MB dy1 write and re-read of a 4096-row minibatch disappear.
+template <bool W1G>
 __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
     const u16* __restrict__ dy3g, const u16* __restrict__ W3, const u16* __restrict__ y2g,
     const u16* __restrict__ W2, const u16* __restrict__ y1g, u16* __restrict__ dy2g, u16* __restrict__ dy1g,
-    float* __restrict__ biasp, int B, uint64_t* __restrict__ stamps, int bias_acc) {
+    float* __restrict__ biasp, int B, uint64_t* __restrict__ stamps, int bias_acc, W1Fold wf) {
   // bias_acc: the bias-gradient partials summed over the workgroup's samples (in walk order) into ONE row per
   // workgroup, biasp[blockIdx.x] -- gridDim.x rows for the finaliser instead of B (its latency-bound walk over the
   // per-sample rows was the longest job of the Breakout finaliser)
@@ -1900,8 +1907,10 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
   };
   // staging area for the weight fragments (aliases the images: used before the sample loop only)
   constexpr int STAGE = BW_P3E + BW_M2E + BW_P2E;   // 14960 + 5184 + 15840 u16 = 70 KB
+  constexpr int FR_OFF = 416 * 32;                   // W1G: bf16 frames behind the 416 dy1 rows
+  constexpr int IMG_E = W1G && FR_OFF + BW_FR + 8 > STAGE ? FR_OFF + BW_FR + 8 : STAGE;
   __shared__ __attribute__((aligned(16))) u16 s_w3[576 * BW_LDW3];   // 72 KB
-  __shared__ __attribute__((aligned(16))) u16 s_img[STAGE];
+  __shared__ __attribute__((aligned(16))) u16 s_img[IMG_E];
   __shared__ float s_red[8 * 128 + 8 * 32];
   u16* const s_p2i = s_img + BW_P3E + BW_M2E;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -1943,6 +1952,23 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
   constexpr int M1_CH = 400 * 4, M1_PER = (M1_CH + BW_T - 1) / BW_T;             // 1600 -> 4
   static_assert(M2_PER == 2 && M1_PER == 4, "prefetch registers are written out");
   uint4 vp0, vm0, vm1_, m10, m11, m12, m13;   // next sample
+  uint4 fr0, fr1, fr2, fr3;                   // W1G: its frames, 16-pixel chunks (1764: <= 4 per thread)
+  constexpr int FR_CH = BW_FR / 16;
+  floatx4 w1acc[2][2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) w1acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+  // (the frames are fetched right after the previous sample's frames were staged: a phase later than the rest)
+  auto fetch_fr = [&](int b) {
+    if constexpr (W1G) {
+      const uint4* f = reinterpret_cast<const uint4*>(wf.obs + (size_t)(wf.obs_idx ? wf.obs_idx[b] : b) * BW_FR);
+      fr0 = f[tid];
+      fr1 = f[tid + BW_T];
+      fr2 = f[tid + 2 * BW_T];
+      fr3 = f[min(tid + 3 * BW_T, FR_CH - 1)];
+    }
+  };
   auto fetch = [&](int b) {
     // dy3: 49 pixels x 8 chunks = 392 <= BW_T: one 16-byte load per thread
     vp0 = *reinterpret_cast<const uint4*>(dy3g + (size_t)b * 49 * 64 + min(tid, 391) * 8);
@@ -1953,7 +1979,10 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
     m12 = *reinterpret_cast<const uint4*>(y1g + (size_t)b * 400 * 32 + (tid + 2 * BW_T) * 8);
     m13 = *reinterpret_cast<const uint4*>(y1g + (size_t)b * 400 * 32 + min(tid + 3 * BW_T, M1_CH - 1) * 8);
   };
-  if ((int)blockIdx.x < B) fetch(blockIdx.x);
+  if ((int)blockIdx.x < B) {
+    fetch(blockIdx.x);
+    fetch_fr(blockIdx.x);
+  }
   for (int b = blockIdx.x, it = 0; b < B; b += gridDim.x, ++it) {
     pst(it, 0);
     // opaque zero (per iteration): keeps the LDS address arithmetic of the unrolled MFMA loops inside the sample
@@ -1974,6 +2003,7 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
         *reinterpret_cast<uint4*>(s_p3 + ((pa + 2) * BW_P3W + pb + 2) * BW_PS + (tid & 7) * 8) = vp0;
       }
       bw_zero_border<BW_P3H, BW_P3W, 2, 7, BW_T>(s_p3);
+      if constexpr (W1G) bw_zero_border<BW_P2H, BW_P2W, 1, 9, BW_T>(s_p2);   // the frames overwrote it
       *reinterpret_cast<uint4*>(s_m2 + tid * 8) = vm0;
       if (tid + BW_T < M2_CH) *reinterpret_cast<uint4*>(s_m2 + (tid + BW_T) * 8) = vm1_;
     }
@@ -2131,8 +2161,26 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
         v.w = mask_pair(v.w, vm1[u].w);
 #pragma unroll
         for (int e = 0; e < 8; ++e) part1[e] += bf_lane(v, e);
-        *reinterpret_cast<uint4*>(dy1g + (size_t)b * 400 * 32 + c * 8) = v;
+        if (dy1g) *reinterpret_cast<uint4*>(dy1g + (size_t)b * 400 * 32 + c * 8) = v;
+        if constexpr (W1G) *reinterpret_cast<uint4*>(s_d1 + c * 8) = v;   // masked rows: dW1's A operand
       }
+    }
+    if constexpr (W1G) {
+      // frames as exact bf16 behind the dy1 rows (the dy2 image is dead), a zero chunk behind them; zero dy1 rows
+      // 400..415 (the dy1 epilogue's discard slots live there)
+      u16* const s_fr = s_img + FR_OFF + z0;
+      auto put = [&](const uint4& w, int i) {
+        const uint2 a = u8x4_to_bf16(w.x), b2 = u8x4_to_bf16(w.y), c = u8x4_to_bf16(w.z), d = u8x4_to_bf16(w.w);
+        *reinterpret_cast<uint4*>(s_fr + i * 16) = make_uint4(a.x, a.y, b2.x, b2.y);
+        *reinterpret_cast<uint4*>(s_fr + i * 16 + 8) = make_uint4(c.x, c.y, d.x, d.y);
+      };
+      put(fr0, tid);
+      put(fr1, tid + BW_T);
+      put(fr2, tid + 2 * BW_T);
+      if (tid + 3 * BW_T < FR_CH) put(fr3, tid + 3 * BW_T);
+      if (tid == 0) *reinterpret_cast<uint4*>(s_fr + BW_FR) = make_uint4(0u, 0u, 0u, 0u);
+      s_d1[400 * 32 + tid] = 0;
+      if (b + (int)gridDim.x < B) fetch_fr(b + gridDim.x);
     }
 #pragma unroll
     for (int e = 0; e < 8; ++e)
@@ -2149,7 +2197,44 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_persist_kernel(
       if (bias_acc) bacc1 += v;
       else biasp[(size_t)b * 160 + 128 + tid] = v;
     }
+    if constexpr (W1G) {
+      // dW1 += dy1^T patches: wave -> (o tiles 0, 1) x (c tiles 2 wid, 2 wid + 1), 13 k-steps of 32 positions
+      const u16* const s_fr = s_img + FR_OFF + z0;
+      const int q = l16 >> 2, pq = l16 & 3;
+      for (int ks = 0; ks < 13; ++ks) {
+        const bf16x8 a0 = tr_frag(s_d1 + ks * 32 * 32, 32, 0, lane);
+        const bf16x8 a1 = tr_frag(s_d1 + ks * 32 * 32, 32, 16, lane);
+        const int pa = ks * 32 + lg * 8 + q, pb = pa + 4;
+        const int oya = (pa * 3277) >> 16, oyb = (pb * 3277) >> 16;   // / 20
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+          const int c = (2 * wid + n) * 16 + 4 * pq;
+          const int co = (c >> 6) * 7056 + ((c >> 3) & 7) * 84 + (c & 7);
+          const int offa = pa < 400 ? co + 4 * oya * 84 + 4 * (pa - oya * 20) : BW_FR;
+          const int offb = pb < 400 ? co + 4 * oyb * 84 + 4 * (pb - oyb * 20) : BW_FR;
+          typedef short short4x __attribute__((ext_vector_type(4)));
+          typedef __attribute__((address_space(3))) short4x lds4;
+          const short4x lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(s_fr + offa));
+          const short4x hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(s_fr + offb));
+          const short8v bv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          const bf16x8 bf = __builtin_bit_cast(bf16x8, bv);
+          w1acc[0][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf, w1acc[0][n], 0, 0, 0);
+          w1acc[1][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bf, w1acc[1][n], 0, 0, 0);
+        }
+      }
+      __syncthreads();   // the dy1 rows / frames are read before the next sample's images land on them
+    }
     pst(it, 5);
+  }
+  if constexpr (W1G) {
+    float* const pl = wf.planes + (size_t)blockIdx.x * 32 * 256;
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          pl[(size_t)(16 * m + 4 * lg + r) * 256 + (2 * wid + n) * 16 + l16] = w1acc[m][n][r] * wf.scale;
   }
   if (bias_acc) {
     if (tid < 128) biasp[(size_t)blockIdx.x * 160 + tid] = bacc;
@@ -2255,11 +2340,15 @@ extern "C" hipError_t aca_cnn_trunk_bwd(const uint16_t* dy3, const uint16_t* W3,
   for (const void* p : {(const void*)dy3, (const void*)W3, (const void*)y2, (const void*)W2, (const void*)y1,
                         (const void*)dy2, (const void*)dy1})
     if (reinterpret_cast<uintptr_t>(p) % 16) return hipErrorInvalidValue;
-  if (persist > 0)
-    aca::cnn_trunk_bwd_persist_kernel<<<persist < B ? persist : B, aca::BW_T, 0, stream>>>(dy3, W3, y2, W2, y1, dy2,
-                                                                                             dy1, biasp, B, stamps,
-                                                                                             bias_acc);
-  else if (w1_obs) {
+  if (persist > 0 && w1_obs) {
+    if (!w1_planes || reinterpret_cast<uintptr_t>(w1_obs) % 16) return hipErrorInvalidValue;
+    const aca::W1Fold wf{w1_obs, w1_obs_idx, w1_planes, w1_scale};
+    aca::cnn_trunk_bwd_persist_kernel<true><<<persist < B ? persist : B, aca::BW_T, 0, stream>>>(
+        dy3, W3, y2, W2, y1, dy2, dy1, biasp, B, stamps, bias_acc, wf);
+  } else if (persist > 0) {
+    aca::cnn_trunk_bwd_persist_kernel<false><<<persist < B ? persist : B, aca::BW_T, 0, stream>>>(
+        dy3, W3, y2, W2, y1, dy2, dy1, biasp, B, stamps, bias_acc, aca::W1Fold{nullptr, nullptr, nullptr, 0.f});
+  } else if (w1_obs) {
     if (!w1_planes || reinterpret_cast<uintptr_t>(w1_obs) % 16) return hipErrorInvalidValue;
     const aca::W1Fold wf{w1_obs, w1_obs_idx, w1_planes, w1_scale};
     aca::cnn_trunk_bwd_kernel<true><<<B, aca::BW_T, 0, stream>>>(dy3, W3, y2, W2, y1, dy2, dy1, biasp, stamps, wf);

@@ -405,3 +405,49 @@ def test_trunk_bwd_persist_bias_rows_accumulated_per_workgroup(cuda, B, persist)
             ref = ref + rows[b]
         assert torch.equal(got[w], ref), w
     assert torch.isnan(got[grid:]).all(), "rows past the grid are not written"
+
+
+@pytest.mark.parametrize("B,persist,idx", [(1100, 256, True), (300, 7, False)])
+def test_persistent_trunk_bwd_conv1_fold_matches_fp64(cuda, B, persist, idx):
+    """The persistent trunk backward with the conv1 weight gradient folded in: dy2 and the bias rows bit-identical to
+    the plain persistent kernel, dy1 not stored (skip_dy1), and plane w == scale * sum over the workgroup's samples
+    (w, w + grid, ...) of dy1_b^T unfold(obs_b), in fp64, using the dy1 the plain kernel writes."""
+    import torch.nn.functional as F
+    from actor_critic_algs_on_tensorflow_amd import _native
+    ops = _native.require()
+    g = torch.Generator(device="cpu").manual_seed(B + persist)
+    dy3 = (torch.randn(B, 7, 7, 64, generator=g) * (torch.rand(B, 7, 7, 64, generator=g) > 0.4)).to(torch.bfloat16)
+    W3 = (torch.randn(64, 3, 3, 64, generator=g) * 0.05).to(torch.bfloat16)
+    W2 = (torch.randn(64, 4, 4, 32, generator=g) * 0.05).to(torch.bfloat16)
+    y2 = (torch.rand(B, 9, 9, 64, generator=g) - 0.3).clamp(min=0).to(torch.bfloat16)
+    y1 = (torch.rand(B, 20, 20, 32, generator=g) - 0.3).clamp(min=0).to(torch.bfloat16)
+    R = B + 17 if idx else B
+    obs = torch.randint(0, 256, (R, 4, 84, 84), dtype=torch.uint8, generator=g)
+    oi = torch.randperm(R, generator=g)[:B] if idx else None
+    dev = [t.to(cuda) for t in (dy3, W3, y2, W2, y1)]
+    args = (dev[0].reshape(B * 49, 64), dev[1].reshape(64, 576), dev[2].reshape(B * 81, 64), dev[3].reshape(64, 512),
+            dev[4].reshape(B * 400, 32))
+    grid = min(persist, B)
+    planes = torch.full((grid, 32, 256), float("nan"), device=cuda)
+    res = []
+    for fold in (False, True):
+        dy2 = torch.full((B * 81, 64), float("nan"), dtype=torch.bfloat16, device=cuda)
+        dy1 = torch.full((B * 400, 32), float("nan"), dtype=torch.bfloat16, device=cuda)
+        bp = torch.full((B, 160), float("nan"), device=cuda)
+        if fold:
+            ops.cnn_trunk_bwd(*args, dy2, dy1, bp, None, persist, obs.to(cuda), oi.to(cuda) if idx else None, planes,
+                              1.0 / 255.0, True, True)
+        else:
+            ops.cnn_trunk_bwd(*args, dy2, dy1, bp, None, persist, None, None, None, 1.0, True)
+        torch.cuda.synchronize()
+        res.append((dy2.view(torch.int16).clone(), dy1.clone(), bp.clone()))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][2][:grid], res[1][2][:grid])
+    assert torch.isnan(res[1][1].float()).all(), "skip_dy1: dy1 must not be written"
+    d1 = res[0][1].cpu().double().view(B, 400, 32)
+    fr = obs[oi] if idx else obs
+    cols = F.unfold(fr.double(), 8, stride=4)
+    per = torch.einsum("bpo,bcp->boc", d1, cols) / 255.0                # [B, 32, 256]
+    ref = torch.stack([per[w::grid].sum(0) for w in range(grid)])
+    got = planes.cpu().double()
+    err = float((got - ref).abs().max() / ref.abs().max())
+    assert err < 1e-5, err

@@ -16,6 +16,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--B", type=int, default=4096)
     ap.add_argument("--persist", type=int, default=256)
+    ap.add_argument("--fold", action="store_true", help="conv1 weight gradient folded in (dy1 not stored)")
     a = ap.parse_args()
     ops = _native.require()
     dev, B = "cuda:0", a.B
@@ -25,7 +26,13 @@ def main():
     dy2 = torch.empty(B * 81, 64, dtype=torch.bfloat16, device=dev)
     dy1 = torch.empty(B * 400, 32, dtype=torch.bfloat16, device=dev)
     biasp = torch.empty(B * 160, device=dev)
-    run = lambda st=None: ops.cnn_trunk_bwd(dy3, W3, y2, W2, y1, dy2, dy1, biasp, st, a.persist)
+    obs = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, generator=g).to(dev)
+    planes = torch.empty(a.persist * 8192, device=dev)
+    if a.fold:
+        run = lambda st=None: ops.cnn_trunk_bwd(dy3, W3, y2, W2, y1, dy2, dy1, biasp, st, a.persist, obs, None, planes,
+                                                1.0 / 255.0, True, True)
+    else:
+        run = lambda st=None: ops.cnn_trunk_bwd(dy3, W3, y2, W2, y1, dy2, dy1, biasp, st, a.persist)
     for _ in range(3):
         run()
     torch.cuda.synchronize()
@@ -40,8 +47,8 @@ def main():
     run(st)
     torch.cuda.synchronize()
     x = st.view(B, 16)[:a.persist].double().cpu() * 10e-3   # 100 MHz -> us
-    names = ["stage+barrier", "dy2 mfma+epi+barrier", "dy2 out+dy1 mfma", "barrier+d1 write+barrier", "dy1 out+barrier"]
-    out = {"B": B, "persist": a.persist, "launch_us": round(t, 2), "per_sample_us": round(t / (B / a.persist), 3)}
+    names = ["stage+barrier", "dy2 mfma+epi+barrier", "dy2 out+dy1 mfma", "barrier+d1 write+barrier", "dy1 out+barrier (+ conv1 fold)"]
+    out = {"B": B, "persist": a.persist, "fold": a.fold, "launch_us": round(t, 2), "per_sample_us": round(t / (B / a.persist), 3)}
     for it in (0, 1):
         ph = {}
         for k, n in enumerate(names):

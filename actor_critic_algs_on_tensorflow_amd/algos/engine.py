@@ -834,7 +834,7 @@ class CNNEngine:
                 elif want_parts:
                     segs.append((g.data_ptr(), 0, g.numel(), 0, 0))
             from ..ops.optim import finalize_jobs
-            words = finalize_jobs(segs, self.dev, return_max=True)
+            words = finalize_jobs(segs, self.dev, return_max=True, split_planes=self.opts.fin_split)
             self._fin_words[key] = words
         return words
 

@@ -47,6 +47,8 @@ class EngineOpts:
     serial_bwd_min_b: int = 1024      # learner batches from this size run the backward on one stream
     conv1_wgrad_min_b: int = 1024     # per-sample conv1 weight-gradient kernel from this many rows (else GEMM)
     nhwc_wgrad_min_b: int = 1024      # conv2/conv3 weight-gradient kernels from this many rows (else GEMM)
+    dp_self_norm: bool = False        # MLP engine under DP: the global norm inside the Adam launch (no sumsq launch;
+                                      # every workgroup re-reads the whole segment: 16.50 vs 15.12 ms, off)
     mlp_prefetch: bool = False        # MLP engine train launch: every layer's weights requested at entry (LDS-DMA touch;
                                       # measured 13.84 vs 13.71 ms MuJoCo PPO: off)
     conv1_fold_persist: bool = True   # ... and in the persistent trunk backward (one plane per workgroup; dy1 not stored)
@@ -55,6 +57,7 @@ class EngineOpts:
     trunk_bwd_v2: bool = False        # trunk data-gradient chain as trunk_bwd2.hip (transposed 32x32x16 MFMAs, direct epilogues)
     trunk_bwd_persist_min_b: int = 1024   # persistent trunk backward (weights in registers) from this many rows
     trunk_bwd_persist: int = 256      # its workgroups
+    fin_split: bool = True            # finaliser: many-plane segments as 256 / 512-element jobs split over thread groups
     bias_rows_acc: bool = True        # ... each summing its samples' bias-gradient rows into one (finaliser: 256 rows, not B)
     wgrad_planes: int = 64            # split-K planes of the GEMM weight gradients
     conv1_planes: int = 128           # planes of the per-sample conv1 weight gradient

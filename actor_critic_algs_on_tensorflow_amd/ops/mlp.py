@@ -207,6 +207,7 @@ class MLPEngine:
                   v_clip=v_clip, ppo=ppo, stamps=stamps)
         desc, _ = self.desc(B)
         nsplit = max(1, min(16, B // 2048))
+        self.last_stores_all = nsplit == 1   # every gradient element stored (no atomics): no zeroing needed after use
         use_parts = want_parts and nsplit == 1
         st = stats if stats is not None else self._dummy_stats
         ops.mlp_wgrad(desc, 2, B, nsplit, self.items[0], self.items[1], self.parts[0] if use_parts else None,

@@ -89,6 +89,9 @@ class FusedAdam:
         self._ticket = torch.zeros(9 * 32, dtype=torch.int32, device=dev)
         # native engine: the update kernel zeroes each gradient after reading it (saves a memset per step)
         self.zero_grad_after = False
+        # grouped launch (FusedGroupStep), plain global norm, no zero-after-use: every workgroup of the optimiser
+        # launch sums the whole (small) segment itself instead of a sum-of-squares launch before it
+        self.self_norm = False
         # data parallelism: the slab holds the SUM over ranks; the kernel folds the 1/world average into its read
         self.grad_mul = 1.0
         # sumsq partials already produced by the gradient kernel (MLP engine): the norm needs no extra launch
@@ -275,14 +278,19 @@ class FusedGroupStep:
         afterwards (:meth:`advance`) -- the launch skips the step ticket (one agent-scope atomic chain per launch)."""
         ops = _native.require()
         plain = [o for o in self.opts if o.max_grad_norm is not None and o.ext_parts is None and o.clip_value is None]
+        # self-normed groups: the optimiser launch's workgroups each sum the whole gradient segment (parts = g)
+        selfn = [o for o in plain if o.self_norm and not o.zero_grad_after]
+        for o in selfn:
+            o._norm_mul = o.grad_mul * o.grad_mul
+        plain = [o for o in plain if o not in selfn]
         if len(plain) > 1:
             # the groups' plain sums of squares (data parallelism: no engine-written partials) in ONE launch
             ops.sumsq_multi([o.g for o in plain], [o._partial for o in plain])
             for o in plain:
                 o._norm_mul = o.grad_mul * o.grad_mul
-            parts = [o._partial if o in plain else o._native_norm(ops) for o in self.opts]
+            parts = [o.g if o in selfn else o._partial if o in plain else o._native_norm(ops) for o in self.opts]
         else:
-            parts = [o._native_norm(ops) for o in self.opts]
+            parts = [o.g if o in selfn else o._native_norm(ops) for o in self.opts]
         key = tuple((p.data_ptr() if p is not None else 0, o._norm_mul, o.grad_mul, o.g.data_ptr())
                     for p, o in zip(parts, self.opts))
         if key != self._key:
@@ -330,13 +338,13 @@ def frag_order_kc(W, K, N):
 SUMSQ_PARTS = 256   # optim.hip: partial slots of the global-norm reduction = max finaliser workgroups
 
 
-def finalize_jobs(segments, device, return_max=False):
+def finalize_jobs(segments, device, return_max=False, split_planes=True):
     """Job table of the gradient finaliser (``grad_finalize``): ``segments`` = [(dst_ptr, src_ptr, n, stride, S)]
     (``src_ptr`` 0: final already, read for the norm). Plane reductions are cut into jobs of about equal load count
     (``n * S`` spread over the workgroups: 256- / 512-element jobs for the many-plane conv gradients when the budget
     allows -- more workgroups streaming the planes; the kernel splits such a job's planes over its thread groups --,
     long jobs for a two-plane fc gradient of 1.6 M elements, which at 1024 elements per job would not fit the job
-    budget), per-sample
+    budget; ``split_planes`` False: 1024-element jobs throughout), per-sample
     bias rows (n <= 64) take one job each, and the read-only segments share the remaining workgroups in equal
     multiples of 1024 elements; at most ``SUMSQ_PARTS`` jobs. ``S = -1`` with ``src_ptr`` 0: ``n`` presummed sums of
     squares at ``dst_ptr`` (fc_bwd's per-tile partials), one job that adds them."""
@@ -352,7 +360,7 @@ def finalize_jobs(segments, device, return_max=False):
         for dst, src, n, stride, S in big:
             # many-plane segments in 256-element steps (the kernel splits their planes over thread groups), the
             # rest in multiples of 1024
-            q = 256 if S >= 16 else 1024
+            q = 256 if S >= 16 and split_planes else 1024
             ch = max(q, -(-int(target // max(1, S)) // q) * q)
             if q == 256 and ch > 512:
                 ch = -(-ch // 1024) * 1024

@@ -619,13 +619,16 @@ __global__ void __launch_bounds__(256) mlp_wgrad_kernel(WgradArgs a) {
     }
     float g = 0.f;
     if (a.g_log_std && lane < a.A) {
-      g = a.g_log_std[lane];
       if (a.mpart) {
+        // the train kernel left its log-std terms in the partial rows only: the gradient is STORED (like every
+        // other element of this launch), so the slab needs no zeroing between minibatches
         float part = 0.f;   // v[8 + lane] with compile-time indices (a runtime index would put v in scratch)
 #pragma unroll
         for (int j = 0; j < MLP_MAXA; ++j) part = lane == j ? v[8 + j] : part;
-        g += part;
+        g = part;
         a.g_log_std[lane] = g;
+      } else {
+        g = a.g_log_std[lane];   // added atomically by the train kernel
       }
     }
     if (a.g_log_std && a.nsplit == 1 && a.parts[0]) {

@@ -707,6 +707,12 @@ class CNNEngine:
                 buf = self._big_planes("Wfc", 2 * 3136 * 512)
                 G.gemm_big(b.y3, 3136, False, b.dh, 512, False, buf, 512, 3, 3136, 512, B, splits=2)
                 self._cur_planes["Wfc"] = 2
+            elif stage == "tail" and self.det_wgrad and self.opts.dp_tail_planes:
+                # data parallelism: the same two planes, summed into the slab by a finaliser launch of the fc weight
+                # alone (the bucket must be final before its all-reduce): cheaper than the in-launch split reduction
+                buf = self._big_planes("Wfc", 2 * 3136 * 512)
+                G.gemm_big(b.y3, 3136, False, b.dh, 512, False, buf, 512, 3, 3136, 512, B, splits=2)
+                self.finalize(b, planes={"Wfc": 2}, parts=False, bias_rows=False)
             else:
                 G.gemm_big(b.y3, 3136, False, b.dh, 512, False, self.gWfc, 512, 0, 3136, 512, B, splits=2,
                            workspace=self.big_ws)

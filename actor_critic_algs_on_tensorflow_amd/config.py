@@ -42,6 +42,7 @@ class EngineOpts:
     mb_index: bool = True             # PPO minibatches read their observations in place through a row index
     ppo_head: bool = True             # large-batch head: z, loss, dz, dh and dWh / dbh / dbfc planes in one launch
     fc_bwd: bool = True               # learner batches of <= 256 rows: dy3 and dWfc in one dedicated launch (fc_bwd.hip)
+    dp_tail_planes: bool = True       # DP tail stage at those sizes: dWfc as 2 planes + a finaliser launch (not in-launch)
     big_gemm_min_b: int = 1024        # learner batches from this size run the fc products on gemm_big.hip (0: never)
     wgrad_gemm: bool = True           # conv2/conv3 weight gradients: batched-position MFMA kernel (else per-sample)
     serial_bwd_min_b: int = 1024      # learner batches from this size run the backward on one stream

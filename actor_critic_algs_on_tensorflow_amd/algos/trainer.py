@@ -734,12 +734,6 @@ class ActorCriticTrainer:
                          clips=(cfg.clip_value, cfg.critic_clip_value), want_parts=self.dp is None)
         for t, g in enumerate(("actor", "critic")):
             self.opts[g].ext_parts = eng.parts[t] if used else None
-            if self.dp is not None and cfg.engine_opts.dp_self_norm:
-                # data parallelism: the all-reduced gradient's norm summed inside the optimiser launch by each of its
-                # workgroups (no sum-of-squares launch); the slab is fully rewritten by the next weight-gradient
-                # launch, so it needs no zeroing behind the optimiser
-                self.opts[g].self_norm = eng.last_stores_all
-                self.opts[g].zero_grad_after = not eng.last_stores_all
         self._apply_grads()
 
     @torch.no_grad()

@@ -48,8 +48,6 @@ class EngineOpts:
     serial_bwd_min_b: int = 1024      # learner batches from this size run the backward on one stream
     conv1_wgrad_min_b: int = 1024     # per-sample conv1 weight-gradient kernel from this many rows (else GEMM)
     nhwc_wgrad_min_b: int = 1024      # conv2/conv3 weight-gradient kernels from this many rows (else GEMM)
-    dp_self_norm: bool = False        # MLP engine under DP: the global norm inside the Adam launch (no sumsq launch;
-                                      # every workgroup re-reads the whole segment: 16.50 vs 15.12 ms, off)
     mlp_prefetch: bool = False        # MLP engine train launch: every layer's weights requested at entry (LDS-DMA touch;
                                       # measured 13.84 vs 13.71 ms MuJoCo PPO: off)
     conv1_fold_persist: bool = True   # ... and in the persistent trunk backward (one plane per workgroup; dy1 not stored)

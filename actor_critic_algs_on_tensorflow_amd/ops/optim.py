@@ -89,9 +89,6 @@ class FusedAdam:
         self._ticket = torch.zeros(9 * 32, dtype=torch.int32, device=dev)
         # native engine: the update kernel zeroes each gradient after reading it (saves a memset per step)
         self.zero_grad_after = False
-        # grouped launch (FusedGroupStep), plain global norm, no zero-after-use: every workgroup of the optimiser
-        # launch sums the whole (small) segment itself instead of a sum-of-squares launch before it
-        self.self_norm = False
         # data parallelism: the slab holds the SUM over ranks; the kernel folds the 1/world average into its read
         self.grad_mul = 1.0
         # sumsq partials already produced by the gradient kernel (MLP engine): the norm needs no extra launch
@@ -278,19 +275,14 @@ class FusedGroupStep:
         afterwards (:meth:`advance`) -- the launch skips the step ticket (one agent-scope atomic chain per launch)."""
         ops = _native.require()
         plain = [o for o in self.opts if o.max_grad_norm is not None and o.ext_parts is None and o.clip_value is None]
-        # self-normed groups: the optimiser launch's workgroups each sum the whole gradient segment (parts = g)
-        selfn = [o for o in plain if o.self_norm and not o.zero_grad_after]
-        for o in selfn:
-            o._norm_mul = o.grad_mul * o.grad_mul
-        plain = [o for o in plain if o not in selfn]
         if len(plain) > 1:
             # the groups' plain sums of squares (data parallelism: no engine-written partials) in ONE launch
             ops.sumsq_multi([o.g for o in plain], [o._partial for o in plain])
             for o in plain:
                 o._norm_mul = o.grad_mul * o.grad_mul
-            parts = [o.g if o in selfn else o._partial if o in plain else o._native_norm(ops) for o in self.opts]
+            parts = [o._partial if o in plain else o._native_norm(ops) for o in self.opts]
         else:
-            parts = [o.g if o in selfn else o._native_norm(ops) for o in self.opts]
+            parts = [o._native_norm(ops) for o in self.opts]
         key = tuple((p.data_ptr() if p is not None else 0, o._norm_mul, o.grad_mul, o.g.data_ptr())
                     for p, o in zip(parts, self.opts))
         if key != self._key:

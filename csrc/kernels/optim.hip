@@ -77,29 +77,6 @@ __device__ __forceinline__ float partial_total(const float* __restrict__ parts, 
 }
 
 
-// Sum of squares of a whole (small) segment, computed by EVERY workgroup of an optimiser launch in the same fixed
-// order -- bitwise the same value in all of them (the data-parallel MLP update: the norm of the all-reduced gradient
-// without a separate sum-of-squares launch; selected by parts == g, and only without zero-after-use, since the
-// workgroups read every element while others update theirs). 16 float4 loads per thread in flight per round.
-__device__ __forceinline__ float seg_sumsq(const float* __restrict__ x, size_t n, float* sh) {
-  constexpr int R = 16;
-  float s = 0.f;
-  const size_t n4 = n / 4;
-  const float4* x4 = reinterpret_cast<const float4*>(x);
-  for (size_t i0 = threadIdx.x; i0 < n4; i0 += (size_t)blockDim.x * R) {
-    float4 v[R];
-#pragma unroll
-    for (int u = 0; u < R; ++u) {
-      const size_t i = i0 + (size_t)u * blockDim.x;
-      v[u] = i < n4 ? x4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-#pragma unroll
-    for (int u = 0; u < R; ++u) s += v[u].x * v[u].x + v[u].y * v[u].y + v[u].z * v[u].z + v[u].w * v[u].w;
-  }
-  for (size_t i = n4 * 4 + threadIdx.x; i < n; i += blockDim.x) s += x[i] * x[i];
-  return block_sum(s, sh);
-}
-
 // One optimiser segment (a parameter group of the flat slab) with its own lr / step / clip / norm settings.
 // Optional transposed fp32 shadows of [K][N] weight matrices inside the segment (the MLP engine's forward reads
 // Wt[N][ldt]); written by the update itself, so the shadow never needs a pass of its own.
@@ -233,8 +210,7 @@ __device__ __forceinline__ void opt_body(const OptSeg& S, float b1, float b2, fl
   if (gw0 < kItems) kc_load(gw0);
   float scale = 1.f;
   if (S.parts) {
-    const bool self_norm = S.parts == static_cast<const float*>(g);   // every workgroup sums the whole segment
-    const float gsq = (self_norm ? seg_sumsq(g, n, shr) : partial_total(S.parts, shr)) * S.norm_mul;
+    const float gsq = partial_total(S.parts, shr) * S.norm_mul;
     scale = grad_scale(gsq, S.max_norm);
     if (S.gnorm_out && vblk == 0 && threadIdx.x == 0) *S.gnorm_out = gsq;
   }
@@ -834,7 +810,6 @@ extern "C" hipError_t aca_opt_multi(const int64_t* words, const float* fvals, co
     S.t_off = t_off < 0 ? -1 : t_off;
     if (S.n == 0 || !opt_aligned(S.p, S.g, adam ? S.m : S.v, S.v, S.shadow)) return hipErrorInvalidValue;
     if (adam && (!S.m || !S.t || !S.ticket)) return hipErrorInvalidValue;
-    if (S.parts == S.g && zero_grad) return hipErrorInvalidValue;   // self-norm reads g while others zero theirs
     S.nblocks = opt_grid(S.n);
     total += S.nblocks;
     // trans: [nseg][OPT_MAXT][5]

@@ -227,16 +227,12 @@ def test_rccl_dp_update_is_one_graph(cuda, tmp_path, name, kw):
     assert not torch.equal(one["snaps"][0], one["snaps"][-1])
 
 
-@pytest.mark.parametrize("self_norm", [True, False])
-def test_dp_world1_mlp_ppo_tracks_single_process(cuda, tmp_path, self_norm):
-    """MuJoCo-shaped PPO under DP at world 1 (the gradient all-reduce is the identity) follows the non-DP update:
-    with ``EngineOpts.dp_self_norm`` the global norm of the all-reduced gradient is summed inside the Adam launch by
-    each of its workgroups (and the slab is not zeroed behind it -- every element, the log-std gradient included,
-    is stored by the next weight-gradient launch); without it, by a sum-of-squares launch. The norms differ from the
-    engine's per-tile partials only in summation order."""
-    kw = dict(name="mujoco_ppo_dp8", n_steps=16, ppo_epochs=2, ppo_minibatches=4,
-              engine_opts=dict(dp_self_norm=self_norm))
-    one = _spawn(tmp_path, 1, 8, "strict", tag=f"mlp_w1_{self_norm}", **kw)
+def test_dp_world1_mlp_ppo_tracks_single_process(cuda, tmp_path):
+    """MuJoCo-shaped PPO under DP at world 1 (the gradient all-reduce is the identity) follows the non-DP update: the
+    global norm of the all-reduced gradient (a sum-of-squares launch) differs from the engine's per-tile partials
+    only in summation order."""
+    kw = dict(name="mujoco_ppo_dp8", n_steps=16, ppo_epochs=2, ppo_minibatches=4)
+    one = _spawn(tmp_path, 1, 8, "strict", tag="mlp_w1", **kw)
     _, tr, _, snaps = _run(None, 8, "strict", **kw)
     for k, (d_dp, d_sg) in enumerate(zip(_deltas(one[0]["snaps"]), _deltas([s.cpu() for s in snaps]))):
         rel = float((d_dp - d_sg).norm() / d_sg.norm())

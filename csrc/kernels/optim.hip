@@ -369,7 +369,9 @@ __global__ void __launch_bounds__(OPT_THREADS) opt_multi_kernel(OptMulti M, floa
 // Job record (8 int64 words): dst, src, n, stride, S, (unused x3). dst / src / stride are float4-aligned when the
 // job's flag word 5 is 1 (host-checked). src = 0, S = -1: dst holds n presummed sums of squares (added, not squared).
 constexpr int FIN_WORDS = 8;
-constexpr int FIN_RND = 32;   // 16-byte loads per thread in flight in the many-plane reductions (was 16)
+constexpr int FIN_RND = 32;        // 16-byte loads per thread in flight in the many-plane reductions (was 16)
+constexpr int FIN_RND_ROWS = 16;   // ... in the bias-row reduction (256 rows per round: one round for the headline's
+                                   // 160 rows and for the 256 per-workgroup rows of the persistent backward)
 
 // One finaliser job (record w) by the whole workgroup; returns this thread's share of the sum of squares of the
 // final gradient. FUSED (the finaliser + optimiser kernel below): the final values go to `out` (LDS, job-local
@@ -419,20 +421,20 @@ __device__ __forceinline__ float fin_job(const int64_t* __restrict__ w, float* _
     }
   } else if (n <= 64 && vec && (n & 3) == 0) {
     // few elements, many planes (per-sample bias rows, up to one per learner sample): 16 float4 columns x 16 plane
-    // groups, FIN_RND 16-byte loads in flight per thread (this reduction is latency-bound: one workgroup walks B
-    // planes in B / (16 FIN_RND) dependent rounds), groups combined in LDS in group order
+    // groups, FIN_RND_ROWS 16-byte loads in flight per thread (this reduction is latency-bound: one workgroup walks
+    // B planes in B / (16 FIN_RND_ROWS) dependent rounds), groups combined in LDS in group order
     const int c4 = tid & 15, pg = tid >> 4, n4 = n >> 2;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     if (c4 < n4) {
-      for (int z0 = pg; z0 < S; z0 += 16 * FIN_RND) {
-        float4 v[FIN_RND];
+      for (int z0 = pg; z0 < S; z0 += 16 * FIN_RND_ROWS) {
+        float4 v[FIN_RND_ROWS];
 #pragma unroll
-        for (int u = 0; u < FIN_RND; ++u) {
+        for (int u = 0; u < FIN_RND_ROWS; ++u) {
           const int z = z0 + 16 * u;
           v[u] = *reinterpret_cast<const float4*>(src + (int64_t)(z < S ? z : pg) * stride + 4 * c4);
         }
 #pragma unroll
-        for (int u = 0; u < FIN_RND; ++u)
+        for (int u = 0; u < FIN_RND_ROWS; ++u)
           if (z0 + 16 * u < S) { acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w; }
       }
     }

@@ -204,6 +204,28 @@ __device__ __forceinline__ void layer_dgrad(const float* dP, int ldp, int N, gcf
 #undef ACA_DG
 }
 
+// rows [0, rows) x [0, w) of an LDS tile (row stride ld, 16-byte aligned rows) -> global rows of w floats. Widths
+// that are multiples of 4 go as 16-byte copies with the row index by shift when w / 4 is a power of two (these
+// copies sit between two layers of the dependent chain: the scalar form spent ~40 instructions per element on the
+// runtime division alone)
+__device__ __forceinline__ void rows_out(const float* __restrict__ src, int ld, gf32* __restrict__ dst, int w,
+                                         int rows) {
+  if ((w & 3) == 0) {
+    const int w4 = w >> 2, sh = __builtin_ctz(w4);
+    const bool p2 = (w4 & (w4 - 1)) == 0;
+    for (int e = threadIdx.x; e < rows * w4; e += MLP_THREADS) {
+      const int r = p2 ? e >> sh : e / w4, c4 = e - r * w4;
+      const floatx4 v = *reinterpret_cast<const floatx4*>(src + r * ld + 4 * c4);
+      *(__attribute__((address_space(1))) floatx4*)(dst + (size_t)r * w + 4 * c4) = v;
+    }
+  } else {
+    for (int e = threadIdx.x; e < rows * w; e += MLP_THREADS) {
+      const int r = e / w, c = e - r * w;
+      dst[(size_t)r * w + c] = src[r * ld + c];
+    }
+  }
+}
+
 __device__ __forceinline__ int64_t row_key(const MlpArgs& a, int grow) {
   return a.tg[grow] * ((int64_t)1 << a.key_shift) + a.env_ids[grow];
 }
@@ -344,14 +366,8 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
               Yl, ldl);
     __syncthreads();
     stamp(3 + l);
-    if (a.mode == 2 && l + 1 < nl) {   // inputs of layer l+1 for its weight gradient
-      const int w = s_out[l];
-      gf32* xs = P_<float>(s_xs[l + 1]);
-      for (int e = threadIdx.x; e < rows * w; e += MLP_THREADS) {
-        const int r = e / w, c = e - r * w;
-        xs[(size_t)(row0 + r) * w + c] = Yl[r * ldl + c];
-      }
-    }
+    if (a.mode == 2 && l + 1 < nl)   // inputs of layer l+1 for its weight gradient
+      rows_out(Yl, ldl, P_<float>(s_xs[l + 1]) + (size_t)row0 * s_out[l], s_out[l], rows);
     X = Yl;
     ldx = ldl;
   }
@@ -559,14 +575,7 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
   }
   stamp(14);   // head phase C + log-std sums (the data-gradient layers take slots 9 ..)
   // ---- top layer dP: apply the head activation derivative (tanh applied above) and publish
-  {
-    const int w = s_out[L];
-    gf32* dp = P_<float>(s_dp[L]);
-    for (int e = threadIdx.x; e < rows * w; e += MLP_THREADS) {
-      const int r = e / w, c = e - r * w;
-      dp[(size_t)(row0 + r) * w + c] = dPtop[r * ldP + c];
-    }
-  }
+  rows_out(dPtop, ldP, P_<float>(s_dp[L]) + (size_t)row0 * s_out[L], s_out[L], rows);
   // ---- data-gradient chain: dP_l -> dP_{l-1}
   float* cur = P0;
   float* nxt = P1;

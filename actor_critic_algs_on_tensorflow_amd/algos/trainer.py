@@ -147,7 +147,6 @@ class ActorCriticTrainer:
         if self._want_native_mlp():
             from ..ops.mlp import MLPEngine
             self.mlp = MLPEngine(self.model, self.flat)
-            self.mlp.prefetch = cfg.engine_opts.mlp_prefetch
         elif self._want_native():
             from .engine import CNNEngine
             self.shadow = torch.empty(self.flat.numel, dtype=torch.bfloat16, device=self.device)
@@ -960,8 +959,10 @@ class ActorCriticTrainer:
     def _update_body_lag1(self):
         """RCCL lag-1 A2C as ONE captured graph per update: the all-reduce of the PREVIOUS update's gradient C is
         forked onto RCCL's stream at the start, so it runs under this update's rollout, loss and backward (which
-        write G); then C is applied, C <- G, G <- 0, and C is packed for the next replay's all-reduce. The first
-        replay all-reduces and applies C = 0: a no-op for RMSprop (Adam advances its step count once more)."""
+        write G); then C is applied, C <- G, G <- 0, and C is packed for the next replay's all-reduce. The optimiser
+        launches are gated on a device flag that the C <- G move sets (``_lag1_gate``): the first replay after
+        capture and the first after :meth:`flush_pending` hold no gradient in C and apply nothing -- parameters,
+        moments and the Adam step count unchanged, exactly as the segmented schedule's first update."""
         dp, C = self.dp, self._comm_grad
         w = dp.allreduce_async(dp.comm_view(C))
         self._defer_allreduce = True
@@ -996,12 +997,15 @@ class ActorCriticTrainer:
 
     def _grad_move(self):
         """lag-1: C <- G, G <- 0 (one launch) so the next backward accumulates into a clean slab while C is
-        all-reduced and consumed by the next optimiser step."""
+        all-reduced and consumed by the next optimiser step; the one-graph schedule's gate opens in the same launch."""
+        gate = getattr(self, "_lag1_gate", None)
         if _native.use_native(self.flat.grad):
-            _native.require().grad_move(self.flat.grad, self._comm_grad)
+            _native.require().grad_move(self.flat.grad, self._comm_grad, gate)
         else:
             self._comm_grad.copy_(self.flat.grad)
             self.flat.grad.zero_()
+            if gate is not None:
+                gate.fill_(1)
 
     def capture(self, warmup=2):
         """Capture the update as hipGraph(s) (see above). Warm-up updates run first (GEMM autotuning, allocator)."""
@@ -1090,6 +1094,10 @@ class ActorCriticTrainer:
             lag1 = self._lag1() and self._a2c_dp_schedule()
             if lag1:
                 self._bind_comm_grad()
+                if getattr(self, "_lag1_gate", None) is None:   # closed: C holds no gradient yet
+                    self._lag1_gate = torch.zeros(1, dtype=torch.int32, device=self.device)
+                    for opt in self.opts.values():
+                        opt.set_gate(self._lag1_gate)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
                 if lag1:
@@ -1191,6 +1199,7 @@ class ActorCriticTrainer:
             self.dp.unpack(self._comm_grad)
             self._post_body()
             self._comm_grad.zero_()
+            self._lag1_gate.zero_()   # the next replay's optimiser step has nothing to apply
             self.dp.pack(self._comm_grad)
             return
         if self.graph is not None and self.graph[0] == "lag1" and self._comm_work is not None:

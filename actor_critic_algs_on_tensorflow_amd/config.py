@@ -48,8 +48,6 @@ class EngineOpts:
     serial_bwd_min_b: int = 1024      # learner batches from this size run the backward on one stream
     conv1_wgrad_min_b: int = 1024     # per-sample conv1 weight-gradient kernel from this many rows (else GEMM)
     nhwc_wgrad_min_b: int = 1024      # conv2/conv3 weight-gradient kernels from this many rows (else GEMM)
-    mlp_prefetch: bool = False        # MLP engine train launch: every layer's weights requested at entry (LDS-DMA touch;
-                                      # measured 13.84 vs 13.71 ms MuJoCo PPO: off)
     conv1_fold_persist: bool = True   # ... and in the persistent trunk backward (one plane per workgroup; dy1 not stored)
     conv1_fold: bool = False          # learner batches below trunk_bwd_persist_min_b: the per-sample trunk backward also
                                       # writes each sample's conv1 weight-gradient plane (no conv1 product in the wgrad launch)

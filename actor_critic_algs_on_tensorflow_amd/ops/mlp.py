@@ -28,7 +28,7 @@ import torch
 from .. import _native
 
 MAXL = 5
-TOWER_WORDS = 2 + 10 * MAXL    # int64 words of one MlpTower (csrc/kernels/mlp_desc.h)
+TOWER_WORDS = 2 + 11 * MAXL    # int64 words of one MlpTower (csrc/kernels/mlp_desc.h)
 ACT_CODES = {None: 0, "none": 0, "relu": 1, "lrelu": 2, "tanh": 3}
 BM = 16
 MAXW = 256
@@ -37,11 +37,31 @@ MPART_W = 24    # per-workgroup partial row of the train kernel (mlp_desc.h)
 LIN_OBS, LIN_ACT = 17, 6
 
 
+def ngp2(w):
+    """16-wide groups of a width rounded up to a power of two (common.h mlp_ngp2)."""
+    g = (w + 15) // 16
+    return 1 if g <= 1 else 2 if g <= 2 else 4 if g <= 4 else 8 if g <= 8 else 16
+
+
 def _ld(w):
     """LDS row stride of a width (mlp.hip ld_of: 16 * power-of-two k-groups + 4)."""
-    g = (w + 15) // 16
-    g = 1 if g <= 1 else 2 if g <= 2 else 4 if g <= 4 else 8 if g <= 8 else 16
-    return 16 * g + 4
+    return 16 * ngp2(w) + 4
+
+
+def frag_f(W):
+    """Forward fragment copy of a [K][N] weight (common.h mlp_frag_f): [ngp2(N) tiles][ngp2(K) groups][64 lanes][4],
+    zero pad -- the layout the optimiser step and ``mlp_tshadow`` write."""
+    K, N = W.shape
+    gk, tn = ngp2(K), ngp2(N)
+    P = torch.zeros(16 * gk, 16 * tn, dtype=W.dtype, device=W.device)
+    P[:K, :N] = W
+    # (tile, r) = c, (g, q, s) = k: element at ((tile * gk + g) * 64 + q * 16 + r) * 4 + s
+    return P.reshape(gk, 4, 4, tn, 16).permute(3, 0, 1, 4, 2).reshape(-1)
+
+
+def frag_g(W):
+    """Data-gradient fragment copy of a [K][N] weight (common.h mlp_frag_g): [ngp2(K) tiles][ngp2(N) groups][64][4]."""
+    return frag_f(W.t())
 
 
 class MLPEngine:
@@ -90,26 +110,43 @@ class MLPEngine:
         self.items = [sum(((l.in_features + 15) // 16) * ((l.out_features + 15) // 16) for l in tw)
                       for tw in self.towers]
         self._descs = {}
+        self._hdescs = {}
         self._mparts = {}
         self._dummy_stats = torch.zeros(16, dtype=torch.float32, device=self.dev)
-        # transposed weight shadows [out][16 * ngp2(in)] (zero pad) -- the forward's B operand
-        self.wt = {}
+        # fp32 FRAGMENT copies of every weight (common.h mlp_frag_f / mlp_frag_g, zero pad): F, the forward's B
+        # operand, for every layer; G, the data gradient's, for layers >= 1 (layer 0 has no data gradient)
+        self.F, self.G = {}, {}
         for tw in self.towers:
-            for lay in tw:
-                kp = _ld(lay.in_features) - 4
-                self.wt[id(lay)] = torch.zeros(lay.out_features, kp, dtype=torch.float32, device=self.dev)
+            for i, lay in enumerate(tw):
+                n = ngp2(lay.in_features) * ngp2(lay.out_features) * 256
+                self.F[id(lay)] = torch.zeros(n, dtype=torch.float32, device=self.dev)
+                if i:
+                    self.G[id(lay)] = torch.zeros(n, dtype=torch.float32, device=self.dev)
         self.n_weights = sum(l.in_features * l.out_features for tw in self.towers for l in tw)
-        self.prefetch = False  # train launches request every layer's weights at entry (EngineOpts.mlp_prefetch)
+        # reference tower shapes: the train launches take the SPEC path (every weight fragment preloaded, mlp.hip)
+        self.spec = True
         self.sync_shadow()
 
     def transposes(self):
-        """Per tower (= optimiser group actor, critic): (W view, K, N, Wt) for the optimiser-written shadows."""
-        return [[(self._views(l.kernel)[0], l.in_features, l.out_features, self.wt[id(l)]) for l in tw]
-                for tw in self.towers]
+        """Per tower (= optimiser group actor, critic): (W view, K, N, dst, code) of the fragment copies the optimiser
+        step writes as it goes (optim.hip): weights with N % 64 == 0 as 16-row x 64-column block items writing whole
+        1 KB fragments (-5 forward copy F, -6 data-gradient copy G), the others per element (-3 F, -4 G)."""
+        out = []
+        for tw in self.towers:
+            lst = []
+            for lay in tw:
+                W = self._views(lay.kernel)[0]
+                K, N = lay.in_features, lay.out_features
+                blk = N % 64 == 0
+                lst.append((W, K, N, self.F[id(lay)], -5 if blk else -3))
+                if id(lay) in self.G:
+                    lst.append((W, K, N, self.G[id(lay)], -6 if blk else -4))
+            out.append(lst)
+        return out
 
     def sync_shadow(self):
-        """Rewrites the transposed weight shadows from the fp32 slab (after every optimiser step, and whenever the
-        parameters change outside the optimiser: checkpoint load, broadcast, parameter-server pull)."""
+        """Rewrites the weight fragment copies from the fp32 slab (the optimiser step writes them itself; this pass
+        covers engine creation and parameter changes outside it: checkpoint load, broadcast, parameter-server pull)."""
         desc, _ = self.desc(None)
         _native.require().mlp_tshadow(desc, 2, self.n_weights)
 
@@ -131,7 +168,9 @@ class MLPEngine:
                 words[base + 2 + 2 * MAXL + l] = ACT_CODES[lay.activation]
                 for j, tns in enumerate((W, b, gW, gb)):
                     words[base + 2 + (3 + j) * MAXL + l] = tns.data_ptr()
-                words[base + 2 + 9 * MAXL + l] = self.wt[id(lay)].data_ptr()
+                words[base + 2 + 9 * MAXL + l] = self.F[id(lay)].data_ptr()
+                if id(lay) in self.G:
+                    words[base + 2 + 10 * MAXL + l] = self.G[id(lay)].data_ptr()
                 if B is not None:
                     # rows padded to a multiple of 128 and never written: the weight-gradient kernel reads whole
                     # 128-row chunks unguarded
@@ -143,6 +182,7 @@ class MLPEngine:
                     words[base + 2 + 8 * MAXL + l] = dp.data_ptr()
         d = (words.to(self.dev), ws)
         self._descs[B] = d
+        self._hdescs[B] = words   # CPU copy: the SPEC train path takes the tower descriptors as kernel arguments
         return d
 
     def lds_bytes(self, mode, tw_base, ntw):
@@ -177,7 +217,7 @@ class MLPEngine:
                     act_in, logp_old, adv, ret, v_old, ent_coef, kl_coef, float(vf_coef), float(ppo_clip),
                     float(v_clip or 0.0), bool(ppo), self.g_log_std if mode == 2 else None,
                     self.mstats if mode == 2 else None, self._mpart(B) if mode == 2 else None, stamps,
-                    self.prefetch)
+                    self._hdescs[desc_B] if (mode == 2 and self.spec) else None)
 
     # ------------------------------------------------------------------------------------------- API
     def policy_step(self, obs, act_out, logp_out, ent_out, v_out, tg, env_ids, key_shift, seed):

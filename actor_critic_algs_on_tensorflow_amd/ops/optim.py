@@ -96,6 +96,8 @@ class FusedAdam:
         # fragment-ordered bf16 copies of some weights, written by the update (set_frag)
         self.frag = []
         self._frag_table = None
+        # optional device int32 gate: the update is skipped while it is 0 (set_gate)
+        self.gate = None
 
     def bind_grad(self, grad_slab):
         """Read gradients from this group's segment of another slab (lag-1 DP reads the all-reduced copy)."""
@@ -109,18 +111,37 @@ class FusedAdam:
         (``frag_order_kc``, ``fc_rollout.hip``), whose region the kernel updates by wave items with a transposed
         512-byte store per wave."""
         self.frag = [tuple(e) if len(e) == 5 else tuple(e) + (-1,) for e in entries]
-        self._frag_table = None
-        if not self.frag:
-            return
-        assert len(self.frag) <= 6 and sum(e[4] == -2 for e in self.frag) <= 1
-        t = torch.zeros(6, 5, dtype=torch.int64)
-        for e, (W, K, N, dst, lay) in enumerate(self.frag):
+        for W, K, N, dst, lay in self.frag:
             off = (W.data_ptr() - self.p.data_ptr()) // 4
             assert 0 <= off and off + K * N <= self.p.numel() and W.numel() == K * N and lay in (-1, -2)
             assert K % 16 == 0 and N % 32 == 0 and dst.dtype == torch.bfloat16 and dst.numel() == K * N
             assert lay == -1 or (off % 4 == 0 and dst.data_ptr() % 16 == 0)
-            t[e] = torch.tensor([off, K, N, lay, dst.data_ptr()])
-        self._frag_table = t
+        assert sum(e[4] == -2 for e in self.frag) <= 1
+        self._frag_table = self._table()
+
+    def set_gate(self, gate):
+        """Device int32 flag (``optim.hip`` OptSeg::gate): while it is 0 the native update is skipped -- parameters,
+        moments and the Adam step count stay as they are (lag-1 data parallelism before its first all-reduced
+        gradient, ``trainer.py`` _update_body_lag1). ``None`` removes it."""
+        self.gate = gate
+        self._frag_table = self._table()
+
+    def table_rows(self):
+        """Rows (offset, K, N, code, ptr) of this optimiser's copy / gate table (``optim.hip`` opt_load_trans)."""
+        rows = [[(W.data_ptr() - self.p.data_ptr()) // 4, K, N, lay, dst.data_ptr()] for W, K, N, dst, lay in self.frag]
+        if self.gate is not None:
+            assert self.gate.dtype == torch.int32 and self.gate.numel() == 1
+            rows.append([0, 1, 1, -9, self.gate.data_ptr()])
+        return rows
+
+    def _table(self):
+        rows = self.table_rows()
+        if not rows:
+            return None
+        assert len(rows) <= 8
+        t = torch.zeros(8, 5, dtype=torch.int64)
+        t[:len(rows)] = torch.tensor(rows, dtype=torch.int64)
+        return t
 
     def _torch_frag(self):
         for W, K, N, dst, lay in getattr(self, "frag", ()):
@@ -136,7 +157,7 @@ class FusedAdam:
     def step(self):
         if _native.use_native(self.p):
             self._native_step()
-        else:
+        elif self.gate is None or int(self.gate) != 0:
             self._torch_step()
 
     def _native_norm(self, ops):
@@ -233,30 +254,32 @@ class FusedGroupStep:
     Adam, ``Basic_AC/policies.py:79-82,142-143``) with ONE native launch (``opt_multi_kernel``): each group keeps its
     own lr / step / clip / norm; any sum-of-squares launches they need run first."""
 
-    MAXT = 6
+    MAXT = 8
 
     def __init__(self, opts, transposes=None):
-        """``transposes``: optional per-optimiser lists of (W view, K, N, Wt tensor) -- transposed fp32 shadows the
-        update writes as it goes (the MLP engine's forward operand)."""
+        """``transposes``: optional per-optimiser lists of (W view, K, N, dst tensor, code) -- weight copies the update
+        writes as it goes (the MLP engine's fp32 fragment copies, ``optim.hip``: codes -3 / -4 forward operand F /
+        data-gradient operand G per element, -5 / -6 the same by 16 x 16 block items; a -6 row follows the -5 row of
+        its weight)."""
         self.opts = list(opts)
         o0 = self.opts[0]
         self.adam = not isinstance(o0, FusedRMSprop)
         self._key = None
         self._words = self._fvals = None
         self._trans = None
-        frag = [getattr(o, "_frag_table", None) for o in self.opts]
-        if transposes is not None or any(f is not None for f in frag):
+        own = [o.table_rows() for o in self.opts]
+        if transposes is not None or any(own):
             t = torch.zeros(len(self.opts), self.MAXT, 5, dtype=torch.int64)
             for k, o in enumerate(self.opts):
-                lst = transposes[k] if transposes is not None else []
-                nf = len(o.frag) if frag[k] is not None else 0
-                assert len(lst) + nf <= self.MAXT
-                for e, (W, K, N, Wt) in enumerate(lst):
+                rows = []
+                for W, K, N, dst, code in (transposes[k] if transposes is not None else []):
                     off = (W.data_ptr() - o.p.data_ptr()) // 4
-                    assert 0 <= off and off + K * N <= o.p.numel()
-                    t[k, e] = torch.tensor([off, K, N, Wt.shape[1], Wt.data_ptr()])
-                if nf:
-                    t[k, len(lst):len(lst) + nf] = frag[k][:nf]
+                    assert 0 <= off and off + K * N <= o.p.numel() and code in (-3, -4, -5, -6)
+                    rows.append([off, K, N, code, dst.data_ptr()])
+                rows += own[k]
+                assert len(rows) <= self.MAXT
+                if rows:
+                    t[k, :len(rows)] = torch.tensor(rows, dtype=torch.int64)
             self._trans = t
 
     @staticmethod

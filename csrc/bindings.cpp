@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstring>
 #include <vector>
 
 #include "gemm_desc.h"
@@ -24,7 +25,7 @@ hipError_t aca_mlp_tshadow(const aca::MlpTower*, int, int, hipStream_t);
 hipError_t aca_opt_multi(const int64_t*, const float*, const int64_t*, int, int, float, float, float, int, int,
                          hipStream_t);
 hipError_t aca_prp_perm(int64_t*, int, uint32_t, const int64_t*, int, hipStream_t);
-hipError_t aca_mlp_fwd(const aca::MlpArgs*, int, size_t, hipStream_t);
+hipError_t aca_mlp_fwd(const aca::MlpArgs*, int, size_t, int, hipStream_t);
 hipError_t aca_mlp_wgrad(const aca::WgradArgs*, hipStream_t);
 hipError_t aca_ppo_head(const aca::PpoHeadArgs*, int, hipStream_t);
 int aca_ppo_head_planes(int);
@@ -101,7 +102,7 @@ hipError_t aca_adam_step(float*, float*, float*, float*, size_t, const float*, f
 hipError_t aca_rmsprop_step(float*, float*, float*, size_t, const float*, const float*, float*, uint16_t*, float, float,
                             float, float, int, float, float, const int64_t*, hipStream_t);
 hipError_t aca_cast_bf16(const float*, uint16_t*, size_t, hipStream_t);
-hipError_t aca_grad_move(float*, float*, size_t, hipStream_t);
+hipError_t aca_grad_move(float*, float*, size_t, int*, hipStream_t);
 hipError_t aca_gemm_run(const AcaGemmDesc*, hipStream_t);
 int aca_gemm_effective_splits(int, int, int);
 int aca_gemm_tile_dims(int, int*, int*);
@@ -883,7 +884,7 @@ uint16_t* shadow_ptr(const c10::optional<Tensor>& shadow, const Tensor& p, const
 static const int64_t* trans_table(const c10::optional<Tensor>& trans, const char* who) {
   if (!(trans.has_value() && trans->defined())) return nullptr;
   TORCH_CHECK(!trans->is_cuda() && trans->scalar_type() == at::kLong && trans->is_contiguous() &&
-                  trans->numel() == 6 * 5, who, ": trans must be CPU int64 [6, 5]");
+                  trans->numel() == 8 * 5, who, ": trans must be CPU int64 [8, 5]");
   return ptr<int64_t>(*trans);
 }
 
@@ -1023,7 +1024,7 @@ void mlp_fwd(Tensor desc, int64_t tw_base, int64_t ntw, int64_t mode, int64_t ld
              c10::optional<Tensor> v_old, c10::optional<Tensor> ent_coef, c10::optional<Tensor> kl_coef,
              double vf_coef, double ppo_clip, double v_clip, bool ppo, c10::optional<Tensor> g_log_std,
              c10::optional<Tensor> mstats, c10::optional<Tensor> mpart, c10::optional<Tensor> stamps,
-             bool prefetch) {
+             c10::optional<Tensor> hdesc) {
   need(desc, at::kLong, "desc");
   TORCH_CHECK(desc.numel() * 8 >= (int64_t)(2 * sizeof(aca::MlpTower)), "mlp_fwd: desc too small");
   TORCH_CHECK(obs.is_cuda() && obs.scalar_type() == at::kFloat && obs.dim() == 2 && obs.stride(1) == 1,
@@ -1082,7 +1083,27 @@ void mlp_fwd(Tensor desc, int64_t tw_base, int64_t ntw, int64_t mode, int64_t ld
                            "mlp_fwd: mpart must hold ceil(B/16) rows of ", aca::MPART_W, " (train mode)");
   a.inv_B = B > 0 ? 1.0f / (float)B : 0.f;
   a.stamps = reinterpret_cast<int64_t*>(stamps_ptr(stamps, 2));   // [2 towers][16 phases]
-  a.prefetch = prefetch && mode == 2 ? 1 : 0;
+  // SPEC train path (mlp.hip): hdesc = the CPU copy of desc; taken when both towers have the reference shapes
+  int spec = 0;
+  if (hdesc.has_value() && hdesc->defined() && mode == 2 && tw_base == 0 && ntw == 2) {
+    TORCH_CHECK(!hdesc->is_cuda() && hdesc->scalar_type() == at::kLong && hdesc->is_contiguous() &&
+                    hdesc->numel() * 8 >= (int64_t)(2 * sizeof(aca::MlpTower)), "mlp_fwd: hdesc must be the CPU desc");
+    std::memcpy(a.htw, hdesc->data_ptr(), sizeof(a.htw));
+    const aca::MlpTower& P = a.htw[0];
+    const aca::MlpTower& C = a.htw[1];
+    const int D = (int)obs.size(1);
+    const int g0 = D <= 16 ? 1 : D <= 32 ? 2 : D <= 64 ? 4 : 0;
+    const bool ok = g0 && P.nl == 4 && P.in[0] == D && P.out[0] == 128 && P.out[1] == 128 && P.out[2] == 64 &&
+                    P.out[3] >= 1 && P.out[3] <= 16 && P.out[3] == A && C.nl == 3 && C.in[0] == D &&
+                    C.out[0] == 256 && C.out[1] == 128 && C.out[2] == 1;
+    if (ok) {
+      for (int t = 0; t < 2; ++t)
+        for (int l = 0; l < (int)a.htw[t].nl; ++l)
+          TORCH_CHECK(a.htw[t].F[l] && (l == 0 || a.htw[t].G[l]) && a.htw[t].xs[l] && a.htw[t].dp[l],
+                      "mlp_fwd: hdesc lacks fragment copies / workspace");
+      spec = g0;
+    }
+  }
   const bool policy = tw_base == 0;
   if (policy) {
     TORCH_CHECK(head == 1 || head == 2, "mlp_fwd: policy tower needs head 1 (categorical) or 2 (gaussian)");
@@ -1097,7 +1118,7 @@ void mlp_fwd(Tensor desc, int64_t tw_base, int64_t ntw, int64_t mode, int64_t ld
                                 (!gauss || a.g_log_std), "mlp_fwd: train needs actions, logp_old, adv (+ g_log_std)");
     if (ppo && v_clip > 0) TORCH_CHECK(a.v_old, "mlp_fwd: clipped value loss needs v_old");
   }
-  check(aca_mlp_fwd(&a, (int)ntw, (size_t)lds, cur_stream(obs)), "mlp_fwd");
+  check(aca_mlp_fwd(&a, (int)ntw, (size_t)lds, spec, cur_stream(obs)), "mlp_fwd");
 }
 
 void mlp_tshadow(Tensor desc, int64_t ntw, int64_t total) {
@@ -1213,7 +1234,7 @@ void opt_multi(Tensor words, Tensor fvals, c10::optional<Tensor> trans, bool ada
   const int64_t* tp = nullptr;
   if (trans.has_value() && trans->defined()) {
     TORCH_CHECK(!trans->is_cuda() && trans->scalar_type() == at::kLong && trans->is_contiguous() &&
-                    trans->numel() == words.size(0) * 6 * 5, "opt_multi: trans must be CPU int64 [nseg, 6, 5]");
+                    trans->numel() == words.size(0) * 8 * 5, "opt_multi: trans must be CPU int64 [nseg, 8, 5]");
     tp = ptr<int64_t>(*trans);
   }
   check(aca_opt_multi(ptr<int64_t>(words), ptr<float>(fvals), tp, (int)words.size(0), adam ? 1 : 0, (float)b1,
@@ -1221,11 +1242,12 @@ void opt_multi(Tensor words, Tensor fvals, c10::optional<Tensor> trans, bool ada
         "opt_multi");
 }
 
-void grad_move(Tensor src, Tensor dst) {
+void grad_move(Tensor src, Tensor dst, c10::optional<Tensor> gate) {
   need(src, at::kFloat, "src");
   need(dst, at::kFloat, "dst");
   TORCH_CHECK(src.numel() == dst.numel(), "grad_move: size mismatch");
-  check(aca_grad_move(ptr<float>(src), ptr<float>(dst), src.numel(), cur_stream(src)), "grad_move");
+  int* gp = const_cast<int*>(copt<int32_t>(gate, at::kInt, "gate"));
+  check(aca_grad_move(ptr<float>(src), ptr<float>(dst), src.numel(), gp, cur_stream(src)), "grad_move");
 }
 
 void cast_bf16(Tensor x, Tensor y) {
@@ -2005,7 +2027,7 @@ TORCH_LIBRARY(acamd, m) {
         "Tensor? shadow, float alpha, float eps, float clip, float max_norm, bool zero_grad=False, float gmul=1.0, "
         "float norm_mul=1.0, Tensor? trans=None) -> ()");
   m.def("cast_bf16(Tensor x, Tensor y) -> ()");
-  m.def("grad_move(Tensor src, Tensor dst) -> ()");
+  m.def("grad_move(Tensor src, Tensor dst, Tensor? gate=None) -> ()");
   m.def("opt_multi(Tensor words, Tensor fvals, Tensor? trans, bool adam, float b1, float b2, float eps, bool zero_grad, "
         "Tensor stream_ref, int t_off=-1) -> ()");
   m.def("prp_perm(Tensor out, int seed, Tensor uc, int epoch) -> ()");
@@ -2015,7 +2037,7 @@ TORCH_LIBRARY(acamd, m) {
         "int A, Tensor? log_std, Tensor? ac_scale, Tensor? tg, Tensor? env_ids, int key_shift, int seed, "
         "Tensor? act_out, Tensor? logp_out, Tensor? ent_out, Tensor? v_out, Tensor? act_in, Tensor? logp_old, "
         "Tensor? adv, Tensor? ret, Tensor? v_old, Tensor? ent_coef, Tensor? kl_coef, float vf_coef, float ppo_clip, "
-        "float v_clip, bool ppo, Tensor? g_log_std, Tensor? mstats, Tensor? mpart=None, Tensor? stamps=None, bool prefetch=False) -> ()");
+        "float v_clip, bool ppo, Tensor? g_log_std, Tensor? mstats, Tensor? mpart=None, Tensor? stamps=None, Tensor? hdesc=None) -> ()");
   m.def("mlp_wgrad(Tensor desc, int ntw, int B, int nsplit, int items0, int items1, Tensor? parts0, "
         "Tensor? parts1, float clip0, float clip1, Tensor? g_log_std, int A, Tensor? mstats, Tensor? stats, "
         "Tensor? ent_coef, Tensor? kl_coef, Tensor? mpart=None, int mpart_rows=0, Tensor? bump=None) -> ()");

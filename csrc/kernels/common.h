@@ -80,6 +80,29 @@ __host__ __device__ __forceinline__ uint32_t minibatch_key(uint32_t seed, int64_
 }
 
 // ------------------------------------------------------------------------------------------------------------
+// MLP engine weight FRAGMENT copies (mlp.hip, written by the optimiser step, optim.hip OptTrans ldt -3 / -4).
+// The f32 MFMA 16x16x4 B operand of a wave is 64 lanes x 4 floats; with the k index of a 16-deep k-group remapped
+// to k = 16 g + 4 (lane >> 4) + s, lane l's four values of group g are 16 consecutive bytes and the wave's whole
+// fragment is ONE contiguous 1 KB block at ((tile * NG + g) * 64 + l) * 4 -- a whole-line wave load (the row-major
+// or transposed forms read 16 rows x 64 B per wave instruction, which the L2 -> CU path serves at a third of the
+// rate, profiles/r4_l2_stream_probe.txt).
+//   F (forward, Y = X W): column tiles c / 16 (ngp2(N) of them, pad zero), k-groups over K (NG = ngp2(K)):
+//     element (k, c) of W [K][N] at ((c/16 * NG + k/16) * 64 + (k/4 % 4) * 16 + c % 16) * 4 + k % 4
+//   G (data gradient, dX = dP W^T): tiles over K (ngp2(K)), k-groups over N (NG = ngp2(N)):
+//     element (k, c) at ((k/16 * NG + c/16) * 64 + (c/4 % 4) * 16 + k % 16) * 4 + c % 4
+// ------------------------------------------------------------------------------------------------------------
+__host__ __device__ __forceinline__ int mlp_ngp2(int w) {   // 16-wide groups of a width, rounded up to a power of 2
+  const int g = (w + 15) >> 4;
+  return g <= 1 ? 1 : g <= 2 ? 2 : g <= 4 ? 4 : g <= 8 ? 8 : 16;
+}
+__host__ __device__ __forceinline__ uint32_t mlp_frag_f(uint32_t k, uint32_t c, int K) {
+  return (((c >> 4) * (uint32_t)mlp_ngp2(K) + (k >> 4)) * 64u + ((k >> 2) & 3u) * 16u + (c & 15u)) * 4u + (k & 3u);
+}
+__host__ __device__ __forceinline__ uint32_t mlp_frag_g(uint32_t k, uint32_t c, int N) {
+  return (((k >> 4) * (uint32_t)mlp_ngp2(N) + (c >> 4)) * 64u + ((c >> 2) & 3u) * 16u + (k & 15u)) * 4u + (c & 3u);
+}
+
+// ------------------------------------------------------------------------------------------------------------
 // bf16 helpers (round-to-nearest-even through the compiler's cvt; NaN stays NaN)
 // ------------------------------------------------------------------------------------------------------------
 __device__ __forceinline__ float bf2f(u16 x) { return __uint_as_float(((uint32_t)x) << 16); }

@@ -13,7 +13,13 @@
 //                  policy loss with the reference's KL-proxy and entropy terms, Gaussian or categorical head; MSE or
 //                  clipped value loss) and the whole data-gradient chain dP_l -> dX_l = dP_l W_l^T -> * act'(y_{l-1})
 //                  in LDS; layer inputs X_l and pre-activation gradients dP_l are written out for the weight
-//                  gradients, the log-std gradient is reduced per tile and added atomically.
+//                  gradients, the log-std gradient is reduced per tile.
+//                  SPEC > 0 (train launches of the reference towers, actor D -> 128 -> 128 -> 64 -> A and the Basic
+//                  critic D -> 256 -> 128 -> 1, D <= 64): the tower's layer sequence is compile-time, so every wave
+//                  requests ALL of its weight fragments for the whole forward + data-gradient chain at entry (up to
+//                  ~180 registers; 216 / 304 KB per actor / critic workgroup as whole 1 KB wave loads) and the layer
+//                  chain then runs out of registers and LDS with no global round trip between layers; one-tile
+//                  layers (the head and the value layer) split their k-groups over the waves.
 // mlp_wgrad_kernel one wave per 16x16 tile of every dW_l = X_l^T dP_l (+ the bias column sums): the whole batch is
 //                  its K dimension, so every gradient element is written exactly once (no atomics, deterministic),
 //                  and the wave also emits its sum of squares into a fixed slot -- the global-norm clip of the fused
@@ -23,8 +29,12 @@
 // v_mfma_f32_16x16x4_f32 (exact f32 products, f32 accumulate; on gfx950 it runs at the f32 vector rate with 4x the
 // operand reuse of a VALU FMA tile). Fragment maps (cdna_hip_programming.md §3): A[l&15][k=l>>4], B[k=l>>4][l&15],
 // C/D col = l&15, row = 4(l>>4)+i. The k index of a 16-wide k-group is remapped k = 16g + 4(l>>4) + s for the four
-// MFMAs s = 0..3, so each lane's A fragments for a k-group are one 16-byte LDS read and, in the data-gradient
-// products, its B fragments one 16-byte load of a weight row ([in][out] = TF dense layout).
+// MFMAs s = 0..3, so each lane's A fragments for a k-group are one 16-byte LDS read and its B fragments 16 bytes of
+// a FRAGMENT copy of the weight (common.h mlp_frag_f / mlp_frag_g: a wave's k-group is one contiguous 1 KB block),
+// rewritten by the optimiser step itself (optim.hip OptTrans ldt -3 / -4). Weights are [in][out] = TF dense layout
+// in the parameter slab; the fragment copies are the only form the kernels read.
+#include <type_traits>
+
 #include "common.h"
 #include "mlp_desc.h"
 
@@ -32,6 +42,7 @@ namespace aca {
 
 constexpr int MLP_BM = 16;          // rows per workgroup
 constexpr int MLP_THREADS = 512;    // 8 waves
+constexpr int MLP_WAVES = MLP_THREADS / 64;
 constexpr int MLP_MAXW = 256;       // widest layer
 constexpr int MLP_MAXA = 16;        // widest head
 constexpr int MLP_PARTS = 256;      // sumsq partial slots per tower (= optim.hip SUMSQ_PARTS)
@@ -43,6 +54,7 @@ enum { ACT_NONE = 0, ACT_RELU = 1, ACT_LRELU = 2, ACT_TANH = 3 };
 // every LDS fragment read would also wait for all outstanding weight loads.
 typedef const __attribute__((address_space(1))) float gcf32;
 typedef __attribute__((address_space(1))) float gf32;
+typedef const __attribute__((address_space(1))) floatx4 gcfx4;
 template <typename T>
 __device__ __forceinline__ __attribute__((address_space(1))) T* P_(int64_t v) {
   return (__attribute__((address_space(1))) T*)v;
@@ -52,10 +64,7 @@ __device__ __forceinline__ int rup16(int x) { return (x + 15) & ~15; }
 // k-groups of a width, rounded up to a power of two: the layer loops are instantiated for NG in {1, 2, 4, 8, 16} so
 // they are straight-line code (a runtime group count means a branch per group, and the waitcnt pass then drains
 // every group's loads before the next one issues)
-__device__ __forceinline__ int ngp2(int w) {
-  const int g = (w + 15) >> 4;
-  return g <= 1 ? 1 : g <= 2 ? 2 : g <= 4 ? 4 : g <= 8 ? 8 : 16;
-}
+__device__ __forceinline__ int ngp2(int w) { return mlp_ngp2(w); }
 __device__ __forceinline__ int ld_of(int w) { return 16 * ngp2(w) + 4; }   // padded LDS row stride
 
 // Hidden-layer activations as one branch-free form y = v > 0 ? v : slope * v (relu: slope 0, lrelu(0.2) of
@@ -77,25 +86,22 @@ constexpr int MLP_MAXG = MLP_MAXW / 16;   // k-groups of the widest layer
 // Y[16][N] = act(X[16][K] W[K][N] + b). X: LDS, zero-padded to 16*NG columns (NG = ngp2(K)).
 // Y: LDS; every column tile up to ngp2(N) is written, columns >= N as 0 (a valid zero-padded input of the next
 // layer). For the tanh head Y holds z (the head code applies tanh and the scale).
-// B operand from the transposed shadow Wt[N][16*NG] (zero-padded rows, refreshed after every optimiser step by
-// mlp_tshadow_kernel): with the remapped k index a lane's four B values of a k-group are Wt[c][16g+4q .. +3], ONE
-// 16-byte load at a constant offset -- all NG loads of a tile are issued before its first MFMA (one L2 round trip
-// per tile, 4*NG live registers, no per-k address registers).
+// B operand from the forward fragment copy F: a lane's four B values of k-group g are 16 bytes, the wave's group one
+// contiguous 1 KB block -- all NG loads of a tile are issued before its first MFMA (one L2 round trip per tile).
 template <int NG>
-__device__ void layer_fwd_t(const float* __restrict__ X, int ldx, gcf32* __restrict__ Wt, gcf32* __restrict__ bias,
+__device__ void layer_fwd_t(const float* __restrict__ X, int ldx, gcf32* __restrict__ F, gcf32* __restrict__ bias,
                             int N, int act, float* __restrict__ Y, int ldy) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 15, q = lane >> 4;
   const int ntile = ngp2(N);
-  for (int tile = wave; tile < ntile; tile += MLP_THREADS / 64) {
+  for (int tile = wave; tile < ntile; tile += MLP_WAVES) {
     const int c = tile * 16 + r;
     const bool cok = c < N;
-    const int cc = cok ? c : N - 1;   // discarded column: any in-range row
-    const __attribute__((address_space(1))) floatx4* wrow =
-        (const __attribute__((address_space(1))) floatx4*)(Wt + (size_t)cc * (16 * NG) + 4 * q);
+    const int cc = cok ? c : N - 1;   // discarded column: any in-range bias
+    gcfx4* wf = (gcfx4*)(F + ((size_t)tile * NG * 64 + lane) * 4);
     floatx4 bv[NG];
 #pragma unroll
-    for (int g = 0; g < NG; ++g) bv[g] = wrow[4 * g];
+    for (int g = 0; g < NG; ++g) bv[g] = wf[64 * g];
     // keep every load above this point (under register pressure the scheduler would sink each load to its MFMA)
     __builtin_amdgcn_sched_barrier(0);
     floatx4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -121,46 +127,35 @@ __device__ void layer_fwd_t(const float* __restrict__ X, int ldx, gcf32* __restr
   }
 }
 
-__device__ __forceinline__ void layer_fwd(const float* X, int ldx, int K, gcf32* Wt, gcf32* bias, int N, int act,
+__device__ __forceinline__ void layer_fwd(const float* X, int ldx, int K, gcf32* F, gcf32* bias, int N, int act,
                                           float* Y, int ldy) {
   switch (ngp2(K)) {
-    case 1: layer_fwd_t<1>(X, ldx, Wt, bias, N, act, Y, ldy); break;
-    case 2: layer_fwd_t<2>(X, ldx, Wt, bias, N, act, Y, ldy); break;
-    case 4: layer_fwd_t<4>(X, ldx, Wt, bias, N, act, Y, ldy); break;
-    case 8: layer_fwd_t<8>(X, ldx, Wt, bias, N, act, Y, ldy); break;
-    default: layer_fwd_t<16>(X, ldx, Wt, bias, N, act, Y, ldy); break;
+    case 1: layer_fwd_t<1>(X, ldx, F, bias, N, act, Y, ldy); break;
+    case 2: layer_fwd_t<2>(X, ldx, F, bias, N, act, Y, ldy); break;
+    case 4: layer_fwd_t<4>(X, ldx, F, bias, N, act, Y, ldy); break;
+    case 8: layer_fwd_t<8>(X, ldx, F, bias, N, act, Y, ldy); break;
+    default: layer_fwd_t<16>(X, ldx, F, bias, N, act, Y, ldy); break;
   }
 }
 
 // dX[16][K] = dP[16][N] W[K][N]^T, then * act'(Yprev) (Yprev: LDS outputs of the previous layer, act_prev) ->
 // dPprev (LDS; every column tile up to ngp2(K) written, columns >= K as 0) and, when gdst != null, the global rows
-// of the previous layer's dP. dP is zero-padded to 16*NG columns (NG = ngp2(N)).
-// VEC: N % 16 == 0, each k-group's B fragment is one 16-byte load of a weight row; all groups loaded up front.
-template <int NG, bool VEC>
-__device__ void layer_dgrad_t(const float* __restrict__ dP, int ldp, int N, gcf32* __restrict__ W, int K,
+// of the previous layer's dP. dP is zero-padded to 16*NG columns (NG = ngp2(N)); B operand from the data-gradient
+// fragment copy G (zero pad, so no clamped loads).
+template <int NG>
+__device__ void layer_dgrad_t(const float* __restrict__ dP, int ldp, gcf32* __restrict__ G, int K,
                               const float* __restrict__ Yprev, int ldyp, int act_prev, float* __restrict__ dPprev,
                               int lddp, gf32* __restrict__ gdst, int rows) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 15, q = lane >> 4;
   const int ntile = ngp2(K);
-  for (int tile = wave; tile < ntile; tile += MLP_THREADS / 64) {
+  for (int tile = wave; tile < ntile; tile += MLP_WAVES) {
     const int kc = tile * 16 + r;   // output column = input feature of the layer
     const bool kok = kc < K;
-    gcf32* wrow = W + (size_t)(kok ? kc : 0) * N;
-    float4 bv[NG];
+    gcfx4* wg = (gcfx4*)(G + ((size_t)tile * NG * 64 + lane) * 4);
+    floatx4 bv[NG];
 #pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      const int n0 = 16 * g + 4 * q;
-      // (kc >= K rows are discarded, n >= N meets a zero-padded dP column: clamped loads, no selects)
-      if (VEC) {
-        const int nn = N >= 16 * NG ? n0 : min(n0, N - 4);
-        const floatx4 w4 = *(const __attribute__((address_space(1))) floatx4*)(wrow + nn);
-        bv[g] = make_float4(w4[0], w4[1], w4[2], w4[3]);
-      } else {
-        bv[g] = make_float4(wrow[min(n0, N - 1)], wrow[min(n0 + 1, N - 1)], wrow[min(n0 + 2, N - 1)],
-                            wrow[min(n0 + 3, N - 1)]);
-      }
-    }
+    for (int g = 0; g < NG; ++g) bv[g] = wg[64 * g];
     __builtin_amdgcn_sched_barrier(0);
     floatx4 acc = {0.f, 0.f, 0.f, 0.f};
     const int z0 = __builtin_amdgcn_readfirstlane(tile) - tile;
@@ -168,10 +163,10 @@ __device__ void layer_dgrad_t(const float* __restrict__ dP, int ldp, int N, gcf3
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
       const float4 a4 = *reinterpret_cast<const float4*>(&Pr[16 * g]);
-      acc = mfma4(a4.x, bv[g].x, acc);
-      acc = mfma4(a4.y, bv[g].y, acc);
-      acc = mfma4(a4.z, bv[g].z, acc);
-      acc = mfma4(a4.w, bv[g].w, acc);
+      acc = mfma4(a4.x, bv[g][0], acc);
+      acc = mfma4(a4.y, bv[g][1], acc);
+      acc = mfma4(a4.z, bv[g][2], acc);
+      acc = mfma4(a4.w, bv[g][3], acc);
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
     }
@@ -187,21 +182,160 @@ __device__ void layer_dgrad_t(const float* __restrict__ dP, int ldp, int N, gcf3
   }
 }
 
-__device__ __forceinline__ void layer_dgrad(const float* dP, int ldp, int N, gcf32* W, int K, const float* Yprev,
+__device__ __forceinline__ void layer_dgrad(const float* dP, int ldp, int N, gcf32* G, int K, const float* Yprev,
                                             int ldyp, int act_prev, float* dPprev, int lddp, gf32* gdst, int rows) {
-  const bool vec = (N & 15) == 0;
-#define ACA_DG(NG_)                                                                                      \
-  if (vec) layer_dgrad_t<NG_, true>(dP, ldp, N, W, K, Yprev, ldyp, act_prev, dPprev, lddp, gdst, rows);  \
-  else layer_dgrad_t<NG_, false>(dP, ldp, N, W, K, Yprev, ldyp, act_prev, dPprev, lddp, gdst, rows);
-  // (non-multiple-of-16 widths above 32 are rejected by the host: ops/mlp.py)
   switch (ngp2(N)) {
-    case 1: ACA_DG(1) break;
-    case 2: ACA_DG(2) break;
-    case 4: layer_dgrad_t<4, true>(dP, ldp, N, W, K, Yprev, ldyp, act_prev, dPprev, lddp, gdst, rows); break;
-    case 8: layer_dgrad_t<8, true>(dP, ldp, N, W, K, Yprev, ldyp, act_prev, dPprev, lddp, gdst, rows); break;
-    default: layer_dgrad_t<16, true>(dP, ldp, N, W, K, Yprev, ldyp, act_prev, dPprev, lddp, gdst, rows); break;
+    case 1: layer_dgrad_t<1>(dP, ldp, G, K, Yprev, ldyp, act_prev, dPprev, lddp, gdst, rows); break;
+    case 2: layer_dgrad_t<2>(dP, ldp, G, K, Yprev, ldyp, act_prev, dPprev, lddp, gdst, rows); break;
+    case 4: layer_dgrad_t<4>(dP, ldp, G, K, Yprev, ldyp, act_prev, dPprev, lddp, gdst, rows); break;
+    case 8: layer_dgrad_t<8>(dP, ldp, G, K, Yprev, ldyp, act_prev, dPprev, lddp, gdst, rows); break;
+    default: layer_dgrad_t<16>(dP, ldp, G, K, Yprev, ldyp, act_prev, dPprev, lddp, gdst, rows); break;
   }
-#undef ACA_DG
+}
+
+// ---- SPEC path: one wave's register share of a layer (tiles wave, wave + 8, ... < NT; NG k-groups each) and, for
+// forward layers, the bias of the lane's output column per tile. Loaded at kernel entry, consumed by the layer.
+template <int NG, int NT>
+struct WSet {
+  static constexpr int NS = (NT + MLP_WAVES - 1) / MLP_WAVES;
+  floatx4 w[NS][NG];
+  float b[NS];
+};
+
+// Every wave issues the same loads (a wave without a tile of a narrow layer re-reads the last tile): the waitcnt pass
+// merges the two sides of a wave-dependent branch conservatively, so a skipped load on one side would make every
+// later wait of the loaded side count too few outstanding loads.
+template <int NG, int NT, bool BIAS>
+__device__ __forceinline__ void wset_load(WSet<NG, NT>& R, int64_t frag, int64_t bias, int N, int wave, int lane) {
+#pragma unroll
+  for (int s = 0; s < WSet<NG, NT>::NS; ++s) {
+    const int tile = min(wave + MLP_WAVES * s, NT - 1);
+    if (BIAS) {
+      const int c = tile * 16 + (lane & 15);
+      R.b[s] = P_<const float>(bias)[c < N ? c : N - 1];
+    }
+    gcfx4* p = (gcfx4*)(P_<const float>(frag) + ((size_t)tile * NG * 64 + lane) * 4);
+#pragma unroll
+    for (int g = 0; g < NG; ++g) R.w[s][g] = p[64 * g];
+  }
+}
+
+// forward layer from registers: the A fragment of a k-group (X rows) is shared by the wave's tiles
+template <int NG, int NT>
+__device__ __forceinline__ void wset_fwd(const WSet<NG, NT>& R, const float* __restrict__ X, int ldx, int N,
+                                         float slope, float* __restrict__ Y, int ldy, int wave, int lane) {
+  constexpr int NS = WSet<NG, NT>::NS;
+  const int r = lane & 15, q = lane >> 4;
+  if (!(NT % MLP_WAVES == 0 || wave < NT)) return;
+  floatx4 acc[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) acc[s] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const float* Xr = X + r * ldx + 4 * q;
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    const float4 a4 = *reinterpret_cast<const float4*>(&Xr[16 * g]);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      if (NT % MLP_WAVES == 0 || wave + MLP_WAVES * s < NT) {
+        acc[s] = mfma4(a4.x, R.w[s][g][0], acc[s]);
+        acc[s] = mfma4(a4.y, R.w[s][g][1], acc[s]);
+        acc[s] = mfma4(a4.z, R.w[s][g][2], acc[s]);
+        acc[s] = mfma4(a4.w, R.w[s][g][3], acc[s]);
+      }
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    if (NT % MLP_WAVES == 0 || wave + MLP_WAVES * s < NT) {
+      const int c = (wave + MLP_WAVES * s) * 16 + r;
+      const bool cok = c < N;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) Y[(4 * q + i) * ldy + c] = cok ? act_fwd(acc[s][i] + R.b[s], slope) : 0.f;
+    }
+  }
+}
+
+// data-gradient layer from registers (G fragments: tiles over K, k-groups over N)
+template <int NG, int NT>
+__device__ __forceinline__ void wset_dgrad(const WSet<NG, NT>& R, const float* __restrict__ dP, int ldp, int K,
+                                           const float* __restrict__ Yprev, int ldyp, float slope_prev,
+                                           float* __restrict__ dPprev, int lddp, gf32* __restrict__ gdst, int rows,
+                                           int wave, int lane) {
+  constexpr int NS = WSet<NG, NT>::NS;
+  const int r = lane & 15, q = lane >> 4;
+  if (!(NT % MLP_WAVES == 0 || wave < NT)) return;
+  floatx4 acc[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) acc[s] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const float* Pr = dP + r * ldp + 4 * q;
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    const float4 a4 = *reinterpret_cast<const float4*>(&Pr[16 * g]);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      if (NT % MLP_WAVES == 0 || wave + MLP_WAVES * s < NT) {
+        acc[s] = mfma4(a4.x, R.w[s][g][0], acc[s]);
+        acc[s] = mfma4(a4.y, R.w[s][g][1], acc[s]);
+        acc[s] = mfma4(a4.z, R.w[s][g][2], acc[s]);
+        acc[s] = mfma4(a4.w, R.w[s][g][3], acc[s]);
+      }
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    if (NT % MLP_WAVES == 0 || wave + MLP_WAVES * s < NT) {
+      const int kc = (wave + MLP_WAVES * s) * 16 + r;
+      const bool kok = kc < K;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = 4 * q + i;
+        const float v = kok ? acc[s][i] * act_bwd(Yprev[row * ldyp + kc], slope_prev) : 0.f;
+        dPprev[row * lddp + kc] = v;
+        if (kok && row < rows) gdst[(size_t)row * K + kc] = v;
+      }
+    }
+  }
+}
+
+// One-tile forward layer (the policy head 64 -> A, the value layer 128 -> 1) with its NG k-groups split over the
+// first NG waves (4 MFMAs each instead of one wave's 4 * NG dependent MFMAs), the partial tiles summed in a fixed
+// order through `scratch` (NG * 256 floats of LDS). Contains one workgroup barrier.
+template <int NG>
+struct WHead {
+  floatx4 w;
+  float b;
+};
+template <int NG>
+__device__ __forceinline__ void whead_load(WHead<NG>& R, int64_t frag, int64_t bias, int N, int wave, int lane,
+                                           int tid) {
+  R.w = *((gcfx4*)P_<const float>(frag) + min(wave, NG - 1) * 64 + lane);   // (same loads on every wave, above)
+  const int c = tid & 15;
+  R.b = P_<const float>(bias)[c < N ? c : N - 1];
+}
+template <int NG>
+__device__ __forceinline__ void whead_fwd(const WHead<NG>& R, const float* __restrict__ X, int ldx, int N,
+                                          float slope, float* __restrict__ Y, int ldy, float* __restrict__ scratch,
+                                          int wave, int lane, int tid) {
+  static_assert(NG <= MLP_WAVES, "one k-group per wave");
+  if (wave < NG) {
+    const int r = lane & 15, q = lane >> 4;
+    const float4 a4 = *reinterpret_cast<const float4*>(&X[r * ldx + 16 * wave + 4 * q]);
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    acc = mfma4(a4.x, R.w[0], acc);
+    acc = mfma4(a4.y, R.w[1], acc);
+    acc = mfma4(a4.z, R.w[2], acc);
+    acc = mfma4(a4.w, R.w[3], acc);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) scratch[wave * 256 + (4 * q + i) * 16 + r] = acc[i];
+  }
+  __syncthreads();
+  if (tid < 256) {
+    const int row = tid >> 4, c = tid & 15;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < NG; ++w) v += scratch[w * 256 + tid];
+    Y[row * ldy + c] = c < N ? act_fwd(v + R.b, slope) : 0.f;
+  }
 }
 
 // rows [0, rows) x [0, w) of an LDS tile (row stride ld, 16-byte aligned rows) -> global rows of w floats. Widths
@@ -233,22 +367,105 @@ __device__ __forceinline__ int64_t row_key(const MlpArgs& a, int grow) {
 constexpr float HALF_LOG_2PI = 0.91893853320467274178f;
 constexpr float TWO_PI = 6.28318530717958647692f;
 
-__global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];   // 16-byte base: the b128 LDS reads stay aligned
-  __shared__ float s_red[MLP_BM][MLP_MAXA + 8];   // per-row partials: log-std grads + stats
-  const int t = blockIdx.y + a.tw_base;
+// static LDS of the fused kernel
+struct MlpShared {
+  float red[MLP_BM][MLP_MAXA + 8];   // per-row partials: log-std grads
+  int yo[MLP_MAXL], ld[MLP_MAXL];     // per-layer LDS offsets / strides
+  int in[MLP_MAXL], out[MLP_MAXL], act[MLP_MAXL];
+  int64_t F[MLP_MAXL], b[MLP_MAXL], G[MLP_MAXL], xs[MLP_MAXL], dp[MLP_MAXL];
+  int64_t grow[MLP_BM];
+  float hl[MLP_BM][MLP_MAXA], ht[MLP_BM][MLP_MAXA], hd[MLP_BM][MLP_MAXA];
+  float g[MLP_BM];
+  float hls[MLP_MAXA], hsc[MLP_MAXA], hco[2];   // head parameters: raw log-std, action scale, kl / entropy coefs
+  int64_t ts[16];                               // SPEC diagnostics stamps
+};
+
+// SPEC register sets of the reference towers (NG0 = k-groups of the observation width)
+template <int NG0>
+struct ActorRegs {   // D -> 128 -> 128 -> 64 -> A
+  WSet<NG0, 8> f0;
+  WSet<8, 8> f1;
+  WSet<8, 4> f2;
+  WHead<4> f3;
+  WSet<1, 4> g3;     // W3 [64][A]: tiles over 64, one k-group over A
+  WSet<4, 8> g2;     // W2 [128][64]
+  WSet<8, 8> g1;     // W1 [128][128]
+};
+template <int NG0>
+struct CriticRegs {  // D -> 256 -> 128 -> 1
+  WSet<NG0, 16> f0;
+  WSet<16, 8> f1;
+  WHead<8> f2;
+  WSet<1, 8> g2;     // W2 [128][1]
+  WSet<8, 16> g1;    // W1 [256][128]
+};
+
+// (the scheduling barriers pin the issue order to the use order: the waitcnt pass merges the two load sites of
+// mlp_tower conservatively, so they must issue every layer's loads in the same order)
+template <int NG0>
+__device__ __forceinline__ void spec_load(ActorRegs<NG0>& R, const MlpTower& T, int wave, int lane, int tid) {
+  __builtin_amdgcn_sched_barrier(0);
+  wset_load<NG0, 8, true>(R.f0, T.F[0], T.b[0], (int)T.out[0], wave, lane);
+  __builtin_amdgcn_sched_barrier(0);
+  wset_load<8, 8, true>(R.f1, T.F[1], T.b[1], (int)T.out[1], wave, lane);
+  __builtin_amdgcn_sched_barrier(0);
+  wset_load<8, 4, true>(R.f2, T.F[2], T.b[2], (int)T.out[2], wave, lane);
+  __builtin_amdgcn_sched_barrier(0);
+  whead_load<4>(R.f3, T.F[3], T.b[3], (int)T.out[3], wave, lane, tid);
+  __builtin_amdgcn_sched_barrier(0);
+  wset_load<1, 4, false>(R.g3, T.G[3], 0, 0, wave, lane);
+  __builtin_amdgcn_sched_barrier(0);
+  wset_load<4, 8, false>(R.g2, T.G[2], 0, 0, wave, lane);
+  __builtin_amdgcn_sched_barrier(0);
+  wset_load<8, 8, false>(R.g1, T.G[1], 0, 0, wave, lane);
+  __builtin_amdgcn_sched_barrier(0);
+}
+template <int NG0>
+__device__ __forceinline__ void spec_load(CriticRegs<NG0>& R, const MlpTower& T, int wave, int lane, int tid) {
+  __builtin_amdgcn_sched_barrier(0);
+  wset_load<NG0, 16, true>(R.f0, T.F[0], T.b[0], (int)T.out[0], wave, lane);
+  __builtin_amdgcn_sched_barrier(0);
+  wset_load<16, 8, true>(R.f1, T.F[1], T.b[1], (int)T.out[1], wave, lane);
+  __builtin_amdgcn_sched_barrier(0);
+  whead_load<8>(R.f2, T.F[2], T.b[2], (int)T.out[2], wave, lane, tid);
+  __builtin_amdgcn_sched_barrier(0);
+  wset_load<1, 8, false>(R.g2, T.G[2], 0, 0, wave, lane);
+  __builtin_amdgcn_sched_barrier(0);
+  wset_load<8, 16, false>(R.g1, T.G[1], 0, 0, wave, lane);
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// one tower of mlp_fwd_kernel. SPEC 0: any tower (t at run time, layer loops over the device descriptor); SPEC > 0:
+// tower TW of the reference shapes in train mode, weights from registers.
+template <int SPEC, int TW>
+__device__ __forceinline__ void mlp_tower(const MlpArgs& a, const int t, float* sm, MlpShared& S) {
+  constexpr bool SP = SPEC > 0;
+  using Regs = typename std::conditional<TW == 0, ActorRegs<SP ? SPEC : 1>, CriticRegs<SP ? SPEC : 1>>::type;
   const MlpTower& T = a.tw[t];
-  const int nl = (int)T.nl;
+  const int nl = SP ? (TW == 0 ? 4 : 3) : (int)T.nl;
   const int row0 = blockIdx.x * MLP_BM;
   const int rows = min(MLP_BM, a.B - row0);
+  // (the wave index through readfirstlane: the compiler then knows it is uniform, so `wave`-dependent branches are
+  // scalar branches with exclusive sides, not two exec-masked blocks run one after the other -- the waitcnt pass would
+  // otherwise see both sides' weight loads in sequence and drain the stream at the first MFMA)
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   // diagnostics: s_memrealtime (100 MHz) at phase ends, thread 0 of workgroup (0, tower) after the barrier; slots 12
   // and 13 hold s_memtime (shader clock) at the ends of the input tile and of the data-gradient chain
+  // (SPEC: kept in LDS and stored at the end -- a global store between the weight loads and their MFMAs makes the
+  // waitcnt pass drain the weight stream)
   auto stamp = [&](int slot) {
-    if (a.stamps && blockIdx.x == 0 && threadIdx.x == 0) a.stamps[blockIdx.y * 16 + slot] = __builtin_amdgcn_s_memrealtime();
+    if (a.stamps && blockIdx.x == 0 && tid == 0) {
+      if (SP) S.ts[slot] = __builtin_amdgcn_s_memrealtime();
+      else a.stamps[blockIdx.y * 16 + slot] = __builtin_amdgcn_s_memrealtime();
+    }
   };
   auto cstamp = [&](int slot) {
-    if (a.stamps && blockIdx.x == 0 && threadIdx.x == 0) a.stamps[blockIdx.y * 16 + slot] = __builtin_amdgcn_s_memtime();
+    if (a.stamps && blockIdx.x == 0 && tid == 0) {
+      if (SP) S.ts[slot] = __builtin_amdgcn_s_memtime();
+      else a.stamps[blockIdx.y * 16 + slot] = __builtin_amdgcn_s_memtime();
+    }
   };
+  if (SP && a.stamps && blockIdx.x == 0 && tid < 16) S.ts[tid] = 0;
   stamp(0);
   // ---- LDS layout: X0 | Y_0 .. Y_{nl-1} | dP ping-pong (train)
   const int ld0 = ld_of(a.D);
@@ -261,49 +478,61 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
     for (int j = 0; j < l; ++j) off += MLP_BM * ldyf(j);
     return sm + off;
   };
-  float* P0 = Yp(nl);
-  float* P1 = P0 + MLP_BM * (MLP_MAXW + 4);
   // per-layer LDS offsets and strides, computed once (one LDS read per use instead of a chain over the earlier
   // layers' widths read from the descriptor)
-  __shared__ int s_yo[MLP_MAXL], s_ld[MLP_MAXL];
-  if (threadIdx.x == 64) {
+  if (tid == 64) {
     for (int l = 0; l < nl; ++l) {
-      s_yo[l] = (int)(Yp(l) - sm);
-      s_ld[l] = ldyf(l);
+      S.yo[l] = (int)(Yp(l) - sm);
+      S.ld[l] = ldyf(l);
     }
   }
   // the tower descriptor's per-layer words staged in LDS once: indexed by the runtime layer number they are vector
   // memory loads, and on gfx9 a load issued after the layer's workspace stores waits for those stores (vmcnt counts
   // both, in order) -- each layer paid that before it could even address its weights
-  __shared__ int s_in[MLP_MAXL], s_out[MLP_MAXL], s_act[MLP_MAXL];
-  __shared__ int64_t s_Wt[MLP_MAXL], s_bb[MLP_MAXL], s_W[MLP_MAXL], s_xs[MLP_MAXL], s_dp[MLP_MAXL];
-  if (threadIdx.x >= 96 && threadIdx.x < 96 + nl) {
-    const int l = threadIdx.x - 96;
-    s_in[l] = (int)T.in[l];
-    s_out[l] = (int)T.out[l];
-    s_act[l] = (int)T.act[l];
-    s_Wt[l] = T.Wt[l];
-    s_bb[l] = T.b[l];
-    s_W[l] = T.W[l];
-    s_xs[l] = T.xs[l];
-    s_dp[l] = T.dp[l];
+  // head parameters (log-std, action scale, regulariser coefficients) staged in LDS: the head reads them inside
+  // the dependent chain (SPEC: wave 0 loads them below, ahead of its weights)
+  auto head_params = [&](int i) {   // i in [0, 18): 16 components + the two coefficients
+    float v = 0.f;
+    if (i < MLP_MAXA) {
+      if (a.log_std && i < a.A) v = a.log_std[i];
+    } else if (i < 2 * MLP_MAXA) {
+      if (a.ac_scale && i - MLP_MAXA < a.A) v = a.ac_scale[i - MLP_MAXA];
+    } else if (i == 2 * MLP_MAXA) {
+      if (a.kl_coef) v = *a.kl_coef;
+    } else if (i == 2 * MLP_MAXA + 1) {
+      if (a.ent_coef) v = *a.ent_coef;
+    }
+    return v;
+  };
+  auto head_params_store = [&](int i, float v) {
+    if (i < MLP_MAXA) S.hls[i] = v;
+    else if (i < 2 * MLP_MAXA) S.hsc[i - MLP_MAXA] = v;
+    else if (i < 2 * MLP_MAXA + 2) S.hco[i - 2 * MLP_MAXA] = v;
+  };
+  if (!SP && tid >= 128 && tid < 128 + 2 * MLP_MAXA + 2) head_params_store(tid - 128, head_params(tid - 128));
+  if (tid >= 96 && tid < 96 + nl) {
+    const int l = tid - 96;
+    S.in[l] = (int)T.in[l];
+    S.out[l] = (int)T.out[l];
+    S.act[l] = (int)T.act[l];
+    S.F[l] = T.F[l];
+    S.b[l] = T.b[l];
+    S.G[l] = T.G[l];
+    S.xs[l] = T.xs[l];
+    S.dp[l] = T.dp[l];
   }
   // ---- row gather: explicit index list, the keyed minibatch permutation (PPO), or identity
-  __shared__ int64_t s_grow[MLP_BM];
-  if (threadIdx.x < MLP_BM) {
-    const int lrow = min(row0 + (int)threadIdx.x, a.B - 1);
-    int64_t g = lrow;
-    if (a.idx) g = a.idx[lrow];
-    else if (a.perm_uc)
-      g = prp_index((uint32_t)(a.perm_off + lrow), (uint32_t)a.perm_n,
-                    minibatch_key(a.perm_seed, *a.perm_uc, a.perm_ep));
-    s_grow[threadIdx.x] = g;
-  }
-  __syncthreads();
-  // ---- train: every layer's weights (forward shadow Wt and, for the data-gradient chain, W) requested at entry, one
-  // dword per 128-byte line by LDS-DMA into a dead slot (no registers, nothing waits on it): the optimiser step just
-  // rewrote them, so each layer's own loads would otherwise start a cold miss only once the previous layer is done.
-  // The tower's workgroups on one XCD (linear id % 8 when the row tiles are a multiple of 8) split the lines.
+  auto gather_rows = [&]() {
+    if (tid < MLP_BM) {
+      const int lrow = min(row0 + tid, a.B - 1);
+      int64_t g = lrow;
+      if (a.idx) g = a.idx[lrow];
+      else if (a.perm_uc)
+        g = prp_index((uint32_t)(a.perm_off + lrow), (uint32_t)a.perm_n,
+                      minibatch_key(a.perm_seed, *a.perm_uc, a.perm_ep));
+      S.grow[tid] = g;
+    }
+  };
   // ---- train: the loss head's per-row inputs loaded now, consumed after the forward (issued behind the forward's
   // first weight loads they were a dependent global round trip in the middle of the chain): gaussian-phase thread
   // (r, j) the action component, row thread r the old log-prob and advantage (policy) or return and old value
@@ -311,12 +540,10 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
   const bool policy = (t == 0);
   float e_act = 0.f, e_lo = 0.f, e_adv = 0.f, e_ret = 0.f, e_vo = 0.f;
   int e_ai = 0;
-  if (a.mode == 2) {
-    const int r = threadIdx.x / MLP_MAXA, j = threadIdx.x % MLP_MAXA;
-    if (policy && a.head == 2 && threadIdx.x < MLP_BM * MLP_MAXA && j < a.A && r < rows)
-      e_act = a.act_f_in[s_grow[r] * a.A + j];
-    if (threadIdx.x < rows) {
-      const int64_t grow = s_grow[threadIdx.x];
+  // (SPEC: wave 0 loads them all, ahead of its input tile and weights; the action components go through LDS)
+  auto head_rows = [&]() {
+    if (tid < rows) {
+      const int64_t grow = S.grow[tid];
       if (policy) {
         e_lo = a.logp_old[grow];
         e_adv = a.adv[grow];
@@ -326,77 +553,150 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
         if (a.v_old && a.v_clip > 0.f) e_vo = a.v_old[grow];
       }
     }
-  }
-  __shared__ float s_pf[64];
-  if (a.mode == 2 && a.prefetch) {
-    const bool split = (gridDim.x & 7) == 0;
-    const int per = split ? (int)gridDim.x >> 3 : 1, me = split ? (int)blockIdx.x >> 3 : 0;
-    const int step = per * MLP_THREADS;
-    for (int l = 0; l < nl; ++l) {
-      const int K = s_in[l], N = s_out[l];
-      for (int rg = (l == 0 ? 0 : -1); rg < 1; ++rg) {   // rg -1: W (row-major, data-gradient), 0: Wt (forward)
-        const float* base = reinterpret_cast<const float*>(rg < 0 ? s_W[l] : s_Wt[l]);
-        const int n = rg < 0 ? K * N : N * 16 * ngp2(K);
-        const int lines = (n + 31) >> 5;
-        for (int i = me + per * (int)threadIdx.x; i < lines; i += step)
-          __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(base + ((size_t)i << 5)),
-                                           (__attribute__((address_space(3))) void*)s_pf, 4, 0, 0);
+  };
+  auto head_inputs = [&]() {
+    const int r = tid / MLP_MAXA, j = tid % MLP_MAXA;
+    if (policy && a.head == 2 && tid < MLP_BM * MLP_MAXA && j < a.A && r < rows) e_act = a.act_f_in[S.grow[r] * a.A + j];
+    head_rows();
+  };
+  Regs R;
+  if constexpr (SP) {
+    // SPEC: the tower's weight fragments into registers at entry. Wave 0 first gathers the rows and the input tile
+    // (vmcnt retires in issue order: the gather must not queue behind its weight stream), the other waves' weight
+    // loads are in flight meanwhile. (Each load sits on ONE path: a register loaded on both sides of a join would
+    // make the waitcnt pass drain every load before the second one.)
+    if (wave == 0) {
+      gather_rows();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      head_rows();
+      const float hp = head_params(lane);   // (lanes 0 .. 33)
+      float ea[4];   // Gaussian action components, (row, j) = e / A for e = lane + 64 u (A <= 16: 4 per lane)
+      const bool eg = policy && a.head == 2;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = lane + 64 * u;
+        ea[u] = (eg && e < rows * a.A) ? a.act_f_in[S.grow[e / a.A] * a.A + e % a.A] : 0.f;
       }
+      constexpr int LD0 = 16 * (SP ? SPEC : 1) + 4;   // = ld0 (host-checked: ngp2(D) == SPEC)
+      constexpr int PER = (MLP_BM * LD0 + 63) / 64;
+      float xv[PER];
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int e = lane + 64 * u, r = e / LD0, c = e - r * LD0;
+        xv[u] = 0.f;
+        if (e < MLP_BM * LD0 && r < rows && c < a.D) xv[u] = a.obs[S.grow[r] * a.ld_obs + c];
+      }
+      spec_load<SPEC>(R, a.htw[TW], wave, lane, tid);
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int e = lane + 64 * u;
+        if (e < MLP_BM * LD0) X0[e] = xv[u];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = lane + 64 * u;
+        if (eg && e < rows * a.A) S.hd[e / a.A][e % a.A] = ea[u];   // (phase A reads it as e_act)
+      }
+      head_params_store(lane, hp);
+    } else {
+      spec_load<SPEC>(R, a.htw[TW], wave, lane, tid);
     }
-  }
-  stamp(1);
-  // ---- input tile (gathered rows; padded rows / columns are zero)
-  for (int e = threadIdx.x; e < MLP_BM * ld0; e += MLP_THREADS) {
-    const int r = e / ld0, c = e - r * ld0;
-    float v = 0.f;
-    if (r < rows && c < a.D) v = a.obs[s_grow[r] * a.ld_obs + c];
-    X0[e] = v;
-    if (a.mode == 2 && r < rows && c < a.D) P_<float>(s_xs[0])[(size_t)(row0 + r) * a.D + c] = v;
+    __syncthreads();
+    stamp(1);
+    if (a.stamps && blockIdx.x == 0 && tid == 0) {   // diagnostics: slot 15 = wave 0's weight stream landed
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      S.ts[15] = __builtin_amdgcn_s_memrealtime();
+    }
+    if (policy && a.head == 2 && tid < MLP_BM * MLP_MAXA) {
+      const int r = tid / MLP_MAXA, j = tid % MLP_MAXA;
+      if (j < a.A && r < rows) e_act = S.hd[r][j];
+    }
+  } else {
+    gather_rows();
+    __syncthreads();
+    if (a.mode == 2) head_inputs();
+    stamp(1);
+    // ---- input tile (gathered rows; padded rows / columns are zero)
+    for (int e = tid; e < MLP_BM * ld0; e += MLP_THREADS) {
+      const int r = e / ld0, c = e - r * ld0;
+      float v = 0.f;
+      if (r < rows && c < a.D) v = a.obs[S.grow[r] * a.ld_obs + c];
+      X0[e] = v;
+      if (a.mode == 2 && r < rows && c < a.D) P_<float>(S.xs[0])[(size_t)(row0 + r) * a.D + c] = v;
+    }
   }
   __syncthreads();
   stamp(2);
   cstamp(12);
   // ---- forward
-  const float* X = X0;
-  int ldx = ld0;
-  for (int l = 0; l < nl; ++l) {
-    float* Yl = sm + s_yo[l];
-    const int ldl = s_ld[l];
-    layer_fwd(X, ldx, s_in[l], P_<const float>(s_Wt[l]), P_<const float>(s_bb[l]), s_out[l], s_act[l],
-              Yl, ldl);
-    __syncthreads();
-    stamp(3 + l);
-    if (a.mode == 2 && l + 1 < nl)   // inputs of layer l+1 for its weight gradient
-      rows_out(Yl, ldl, P_<float>(s_xs[l + 1]) + (size_t)row0 * s_out[l], s_out[l], rows);
-    X = Yl;
-    ldx = ldl;
+  if constexpr (SP) {
+    // (the layer inputs X_l for the weight gradients stay in LDS and are stored after the data-gradient chain: a
+    // store loop between the weight loads and their MFMAs would make the waitcnt pass drain the whole weight stream)
+    float* P1 = sm + S.yo[nl - 1] + MLP_BM * S.ld[nl - 1] + MLP_BM * (MLP_MAXW + 4);   // head split-K scratch
+    auto next = [&](int l) {
+      __syncthreads();
+      stamp(3 + l);
+    };
+    if constexpr (TW == 0) {
+      wset_fwd(R.f0, X0, ld0, S.out[0], act_slope(S.act[0]), sm + S.yo[0], S.ld[0], wave, lane);
+      next(0);
+      wset_fwd(R.f1, sm + S.yo[0], S.ld[0], S.out[1], act_slope(S.act[1]), sm + S.yo[1], S.ld[1], wave, lane);
+      next(1);
+      wset_fwd(R.f2, sm + S.yo[1], S.ld[1], S.out[2], act_slope(S.act[2]), sm + S.yo[2], S.ld[2], wave, lane);
+      next(2);
+      whead_fwd(R.f3, sm + S.yo[2], S.ld[2], S.out[3], act_slope(S.act[3]), sm + S.yo[3], S.ld[3], P1, wave, lane,
+                tid);
+      next(3);
+    } else {
+      wset_fwd(R.f0, X0, ld0, S.out[0], act_slope(S.act[0]), sm + S.yo[0], S.ld[0], wave, lane);
+      next(0);
+      wset_fwd(R.f1, sm + S.yo[0], S.ld[0], S.out[1], act_slope(S.act[1]), sm + S.yo[1], S.ld[1], wave, lane);
+      next(1);
+      whead_fwd(R.f2, sm + S.yo[1], S.ld[1], S.out[2], act_slope(S.act[2]), sm + S.yo[2], S.ld[2], P1, wave, lane,
+                tid);
+      next(2);
+    }
+  } else {
+    const float* X = X0;
+    int ldx = ld0;
+    for (int l = 0; l < nl; ++l) {
+      float* Yl = sm + S.yo[l];
+      const int ldl = S.ld[l];
+      layer_fwd(X, ldx, S.in[l], P_<const float>(S.F[l]), P_<const float>(S.b[l]), S.out[l], S.act[l], Yl, ldl);
+      __syncthreads();
+      stamp(3 + l);
+      if (a.mode == 2 && l + 1 < nl)   // inputs of layer l+1 for its weight gradient
+        rows_out(Yl, ldl, P_<float>(S.xs[l + 1]) + (size_t)row0 * S.out[l], S.out[l], rows);
+      X = Yl;
+      ldx = ldl;
+    }
   }
   const int L = nl - 1;
-  const float* Yo = sm + s_yo[L];
-  const int ldo = s_ld[L];
+  const float* Yo = sm + S.yo[L];
+  const int ldo = S.ld[L];
   // ---- heads: one thread per row
-  float* dPtop = P0;
+  float* dPtop = sm + S.yo[L] + MLP_BM * S.ld[L];   // P0
+  float* P1 = dPtop + MLP_BM * (MLP_MAXW + 4);
   const int ldP = MLP_MAXW + 4;
   if (a.mode == 2) {   // zero the top dP tile (the head writes only valid columns)
-    for (int e = threadIdx.x; e < MLP_BM * ldP; e += MLP_THREADS) dPtop[e] = 0.f;
+    for (int e = tid; e < MLP_BM * ldP; e += MLP_THREADS) dPtop[e] = 0.f;
     __syncthreads();
   }
-  const int tid = threadIdx.x;
   // Gaussian policy head, phase A: one thread per (row, action component) -- mean, sample (rollout) or given action,
   // the component's log-prob term (a per-row loop of tanh / hash / log / sqrt / cos / exp chains on 16 lanes would
   // idle 7 of 8 waves; the per-row sums below keep the sequential order, so the results do not change)
-  __shared__ float s_hl[MLP_BM][MLP_MAXA], s_ht[MLP_BM][MLP_MAXA], s_hd[MLP_BM][MLP_MAXA];
-  __shared__ float s_g[MLP_BM];
   const bool gauss = policy && a.head == 2;
   if (gauss) {
     if (tid < MLP_BM * MLP_MAXA) {
       const int r = tid / MLP_MAXA, j = tid % MLP_MAXA;
       if (j < a.A) {
         const bool live = r < rows;
-        const int64_t grow = s_grow[r];
-        const float ls = fminf(fmaxf(a.log_std[j], -2.5f), 2.5f);
+        const int64_t grow = S.grow[r];
+        const float ls = fminf(fmaxf(S.hls[j], -2.5f), 2.5f);
         const float th = tanhf(Yo[r * ldo + j]);
-        const float mu = th * a.ac_scale[j];
+        const float mu = th * S.hsc[j];
         float aj;
         if (a.mode == 0) {
           const int64_t key = live ? row_key(a, (int)grow) : 0;
@@ -408,9 +708,9 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
           aj = live ? (a.mode == 2 ? e_act : a.act_f_in[grow * a.A + j]) : mu;
         }
         const float zz = (aj - mu) * expf(-ls);
-        s_hl[r][j] = -0.5f * zz * zz - ls - HALF_LOG_2PI;
-        s_ht[r][j] = th;
-        s_hd[r][j] = aj - mu;
+        S.hl[r][j] = -0.5f * zz * zz - ls - HALF_LOG_2PI;
+        S.ht[r][j] = th;
+        S.hd[r][j] = aj - mu;
       }
     }
     __syncthreads();
@@ -418,23 +718,22 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
   if (tid < MLP_BM) {
     const int r = tid;
     const bool live = r < rows;
-    const int lrow = row0 + r;   // batch-local row (workspace / minibatch order)
-    const int64_t grow = s_grow[r];
+    const int64_t grow = S.grow[r];
     float st[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     if (!policy) {
       const float v = Yo[r * ldo];
       if (live && (a.mode == 0 || a.mode == 1) && a.v_out) a.v_out[grow] = v;
       if (live && a.mode == 2) {
-        const float R = e_ret;
-        float dv = 2.f * (v - R), l2 = (v - R) * (v - R);
+        const float R_ = e_ret;
+        float dv = 2.f * (v - R_), l2 = (v - R_) * (v - R_);
         if (a.v_old && a.v_clip > 0.f) {
           const float vo = e_vo;
           const float d = fminf(fmaxf(v - vo, -a.v_clip), a.v_clip);
           const float vc = vo + d;
-          const float l2c = (vc - R) * (vc - R);
+          const float l2c = (vc - R_) * (vc - R_);
           const bool inr = (v - vo) >= -a.v_clip && (v - vo) <= a.v_clip;
-          if (l2c > l2) { dv = inr ? 2.f * (vc - R) : 0.f; l2 = l2c; }
-          else if (l2c == l2) dv = 0.5f * dv + 0.5f * (inr ? 2.f * (vc - R) : 0.f);
+          if (l2c > l2) { dv = inr ? 2.f * (vc - R_) : 0.f; l2 = l2c; }
+          else if (l2c == l2) dv = 0.5f * dv + 0.5f * (inr ? 2.f * (vc - R_) : 0.f);
         }
         dPtop[r * ldP] = a.vf_coef * a.inv_B * dv;
         st[3] = l2;
@@ -443,8 +742,8 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
       const int A = a.A;
       float lp = 0.f, H = 0.f;
       for (int j = 0; j < A; ++j) {
-        lp += s_hl[r][j];
-        H += 0.5f + HALF_LOG_2PI + fminf(fmaxf(a.log_std[j], -2.5f), 2.5f);
+        lp += S.hl[r][j];
+        H += 0.5f + HALF_LOG_2PI + fminf(fmaxf(S.hls[j], -2.5f), 2.5f);
       }
       if (live && a.mode != 2) {
         if (a.logp_out) a.logp_out[grow] = lp;
@@ -453,7 +752,7 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
       float g = 0.f;
       if (a.mode == 2 && live) {
         const float lo = e_lo, adv = e_adv;
-        const float beta = *a.kl_coef;
+        const float beta = S.hco[0];
         float dsurr;
         if (a.ppo) {
           const float ratio = expf(lp - lo);
@@ -473,7 +772,7 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
         st[2] = H;
         g = a.inv_B * (-dsurr - 2.f * beta * (lo - lp));
       }
-      s_g[r] = g;
+      S.g[r] = g;
     } else {   // categorical logits
       const int A = a.A;
       float z[MLP_MAXA];
@@ -504,7 +803,7 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
       }
       if (a.mode == 2 && live) {
         const float lo = e_lo, adv = e_adv;
-        const float beta = *a.kl_coef, ce = *a.ent_coef;
+        const float beta = S.hco[0], ce = S.hco[1];
         float dsurr;
         if (a.ppo) {
           const float ratio = expf(lpa - lo);
@@ -554,45 +853,100 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
       const int r = tid / MLP_MAXA, j = tid % MLP_MAXA;
       if (j < a.A) {
         const bool live = r < rows;
-        const float raw = a.log_std[j];
+        const float raw = S.hls[j];
         const float ls = fminf(fmaxf(raw, -2.5f), 2.5f);
         const float ivar = expf(-2.f * ls);
-        const float d = s_hd[r][j], th = s_ht[r][j], g = s_g[r];
+        const float d = S.hd[r][j], th = S.ht[r][j], g = S.g[r];
         const float dmu = g * d * ivar;
-        dPtop[r * ldP + j] = live ? dmu * a.ac_scale[j] * (1.f - th * th) : 0.f;
+        dPtop[r * ldP + j] = live ? dmu * S.hsc[j] * (1.f - th * th) : 0.f;
         const bool inr = raw >= -2.5f && raw <= 2.5f;
-        s_red[r][j] = (live && inr) ? g * (d * d * ivar - 1.f) - (*a.ent_coef) * a.inv_B : 0.f;
+        S.red[r][j] = (live && inr) ? g * (d * d * ivar - 1.f) - S.hco[1] * a.inv_B : 0.f;
       }
     }
     __syncthreads();
   }
   // log-std gradient: column sums over the tile's rows, one atomic per column
-  if (policy && a.head == 2 && threadIdx.x < a.A) {
+  if (policy && a.head == 2 && tid < a.A) {
     float s = 0.f;
-    for (int r = 0; r < MLP_BM; ++r) s += s_red[r][threadIdx.x];
-    if (a.mpart) a.mpart[(size_t)blockIdx.x * MPART_W + 8 + threadIdx.x] = s;
-    else atomicAdd(&a.g_log_std[threadIdx.x], s);
+    for (int r = 0; r < MLP_BM; ++r) s += S.red[r][tid];
+    if (a.mpart) a.mpart[(size_t)blockIdx.x * MPART_W + 8 + tid] = s;
+    else atomicAdd(&a.g_log_std[tid], s);
   }
   stamp(14);   // head phase C + log-std sums (the data-gradient layers take slots 9 ..)
   // ---- top layer dP: apply the head activation derivative (tanh applied above) and publish
-  rows_out(dPtop, ldP, P_<float>(s_dp[L]) + (size_t)row0 * s_out[L], s_out[L], rows);
+  if constexpr (SP) {   // (no store loop ahead of the data-gradient MFMAs, see above; N <= 16)
+    const int N = S.out[L];
+    if (tid < MLP_BM * 16) {
+      const int r = tid >> 4, c = tid & 15;
+      if (r < rows && c < N) P_<float>(S.dp[L])[(size_t)(row0 + r) * N + c] = dPtop[r * ldP + c];
+    }
+  } else {
+    rows_out(dPtop, ldP, P_<float>(S.dp[L]) + (size_t)row0 * S.out[L], S.out[L], rows);
+  }
   // ---- data-gradient chain: dP_l -> dP_{l-1}
-  float* cur = P0;
-  float* nxt = P1;
-  for (int l = L; l >= 1; --l) {
-    const int N = s_out[l], K = s_in[l];
-    gf32* gdst = P_<float>(s_dp[l - 1]) + (size_t)row0 * K;
-    gcf32* W = P_<const float>(s_W[l]);
-    layer_dgrad(cur, ldP, N, W, K, sm + s_yo[l - 1], s_ld[l - 1], s_act[l - 1], nxt, ldP, gdst, rows);
-    __syncthreads();
-    stamp(9 + L - l);
-    float* tmp = cur;
-    cur = nxt;
-    nxt = tmp;
+  if constexpr (SP) {
+    auto gd = [&](int l) { return P_<float>(S.dp[l - 1]) + (size_t)row0 * S.in[l]; };
+    if constexpr (TW == 0) {
+      wset_dgrad(R.g3, dPtop, ldP, S.in[3], sm + S.yo[2], S.ld[2], act_slope(S.act[2]), P1, ldP, gd(3), rows,
+                 wave, lane);
+      __syncthreads();
+      stamp(9);
+      wset_dgrad(R.g2, P1, ldP, S.in[2], sm + S.yo[1], S.ld[1], act_slope(S.act[1]), dPtop, ldP, gd(2), rows, wave,
+                 lane);
+      __syncthreads();
+      stamp(10);
+      wset_dgrad(R.g1, dPtop, ldP, S.in[1], sm + S.yo[0], S.ld[0], act_slope(S.act[0]), P1, ldP, gd(1), rows, wave,
+                 lane);
+      stamp(11);
+    } else {
+      wset_dgrad(R.g2, dPtop, ldP, S.in[2], sm + S.yo[1], S.ld[1], act_slope(S.act[1]), P1, ldP, gd(2), rows,
+                 wave, lane);
+      __syncthreads();
+      stamp(9);
+      wset_dgrad(R.g1, P1, ldP, S.in[1], sm + S.yo[0], S.ld[0], act_slope(S.act[0]), dPtop, ldP, gd(1), rows, wave,
+                 lane);
+      stamp(10);
+    }
+    // the layer inputs for the weight gradients (X0 and Y_0 .. Y_{L-1} are still in LDS)
+    rows_out(X0, ld0, P_<float>(S.xs[0]) + (size_t)row0 * a.D, a.D, rows);
+    for (int l = 0; l < L; ++l)
+      rows_out(sm + S.yo[l], S.ld[l], P_<float>(S.xs[l + 1]) + (size_t)row0 * S.out[l], S.out[l], rows);
+    if (a.stamps && blockIdx.x == 0) {
+      cstamp(13);
+      stamp(7);   // end of the data-gradient chain (stores issued)
+      __syncthreads();
+      if (tid < 16) a.stamps[blockIdx.y * 16 + tid] = S.ts[tid];
+    }
+    return;
+  } else {
+    float* cur = dPtop;
+    float* nxt = P1;
+    for (int l = L; l >= 1; --l) {
+      const int K = S.in[l];
+      gf32* gdst = P_<float>(S.dp[l - 1]) + (size_t)row0 * K;
+      layer_dgrad(cur, ldP, S.out[l], P_<const float>(S.G[l]), K, sm + S.yo[l - 1], S.ld[l - 1], S.act[l - 1], nxt,
+                  ldP, gdst, rows);
+      __syncthreads();
+      stamp(9 + L - l);
+      float* tmp = cur;
+      cur = nxt;
+      nxt = tmp;
+    }
   }
   cstamp(13);
-  // the prefetch DMA must land before the workgroup's LDS is handed to another workgroup
-  if (a.prefetch) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int SPEC>
+__global__ void __launch_bounds__(MLP_THREADS) mlp_fwd_kernel(MlpArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];   // 16-byte base: the b128 LDS reads stay aligned
+  __shared__ MlpShared S;
+  const int t = blockIdx.y + a.tw_base;
+  if constexpr (SPEC == 0) {
+    mlp_tower<0, -1>(a, t, sm, S);
+  } else {
+    if (t == 0) mlp_tower<SPEC, 0>(a, 0, sm, S);
+    else mlp_tower<SPEC, 1>(a, 1, sm, S);
+  }
 }
 
 // ------------------------------------------------------------------------------------------------ weight grads
@@ -754,8 +1108,9 @@ __global__ void __launch_bounds__(256) mlp_wgrad_kernel(WgradArgs a) {
   }
 }
 
-// Wt[c][k] = W[k][c] (rows padded to 16 * ngp2(K), pad stays zero) for every layer of the launched towers: the
-// forward's B operand. One thread per weight element; runs after each optimiser step (and at engine creation).
+// The fragment copies F (every layer) and G (layers >= 1) of every W of the launched towers (common.h mlp_frag_f /
+// mlp_frag_g; the pads stay zero). One thread per weight element; the optimiser step writes them as it goes (optim.hip
+// OptTrans ldt -3 / -4), this pass covers engine creation and parameter changes outside the optimiser.
 __global__ void __launch_bounds__(256) mlp_tshadow_kernel(const MlpTower* __restrict__ tw, int ntw, int total) {
   int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= total) return;
@@ -765,7 +1120,9 @@ __global__ void __launch_bounds__(256) mlp_tshadow_kernel(const MlpTower* __rest
       const int K = (int)T.in[l], N = (int)T.out[l];
       if (e < K * N) {
         const int k = e / N, c = e - k * N;
-        P_<float>(T.Wt[l])[(size_t)c * (16 * ngp2(K)) + k] = P_<const float>(T.W[l])[e];
+        const float w = P_<const float>(T.W[l])[e];
+        P_<float>(T.F[l])[mlp_frag_f(k, c, K)] = w;
+        if (T.G[l]) P_<float>(T.G[l])[mlp_frag_g(k, c, N)] = w;
         return;
       }
       e -= K * N;
@@ -887,7 +1244,7 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_rollout_kernel(RolloutArgs a)
     s_in[tid] = (int)T.in[tid];
     s_out[tid] = (int)T.out[tid];
     s_actc[tid] = (int)T.act[tid];
-    s_wt[tid] = T.Wt[tid];
+    s_wt[tid] = T.F[tid];
     s_b[tid] = T.b[tid];
   }
   if (tid < MLP_MAXA) {
@@ -930,15 +1287,15 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_rollout_kernel(RolloutArgs a)
     for (int l = 0; l <= nl; ++l) s_yo[l] = (int)(Yp(l) - sm);
     for (int l = 0; l < nl; ++l) s_wo[l] = (int)(Wl(l) - sm);
   }
-  if (WLDS) {   // W_l [out][16*ngp2(in) + 4] (from the zero-padded transposed shadow), then b_l [16*ngp2(out)]
+  if (WLDS) {   // W_l [out][16*ngp2(in) + 4] (transposed, from the zero-padded forward fragment copy), then b_l
     for (int l = 0; l < nl; ++l) {
-      const int K4 = 4 * ngp2(s_in[l]), N = s_out[l], ldw = 16 * ngp2(s_in[l]) + 4;
+      const int NG = ngp2(s_in[l]), K4 = 4 * NG, N = s_out[l], ldw = 16 * NG + 4;
       float* w = Wl(l);
-      const __attribute__((address_space(1))) floatx4* src =
-          (const __attribute__((address_space(1))) floatx4*)P_<const float>(s_wt[l]);
+      gcfx4* src = (gcfx4*)P_<const float>(s_wt[l]);
       for (int e = tid; e < N * K4; e += MLP_THREADS) {
         const int c = e / K4, k4 = e - c * K4;
-        *reinterpret_cast<floatx4*>(w + c * ldw + 4 * k4) = src[e];
+        // W[4 k4 .. 4 k4 + 3][c] is one float4 of F (common.h mlp_frag_f with k % 4 == 0)
+        *reinterpret_cast<floatx4*>(w + c * ldw + 4 * k4) = src[((c >> 4) * NG + (k4 >> 2)) * 64 + (k4 & 3) * 16 + (c & 15)];
       }
       float* b = w + N * ldw;
       gcf32* bsrc = P_<const float>(s_b[l]);
@@ -1093,19 +1450,32 @@ using namespace aca;
 
 // Host launchers. The descriptor lives in device memory, so shape validation and the LDS size are the caller's
 // (ops/mlp.py validates the tower shapes when it builds the descriptor and passes the LDS bytes it computed).
-extern "C" hipError_t aca_mlp_fwd(const MlpArgs* a, int ntw, size_t lds, hipStream_t stream) {
+// spec: 0 = the generic kernel; 1 / 2 / 4 = the SPEC train path for the reference towers with ngp2(D) == spec (the
+// binding checks the shapes against a->htw)
+extern "C" hipError_t aca_mlp_fwd(const MlpArgs* a, int ntw, size_t lds, int spec, hipStream_t stream) {
   if (a->B <= 0) return hipSuccess;
   if (a->A > MLP_MAXA || a->D > MLP_MAXW || ntw < 1 || a->tw_base + ntw > 2 || !a->tw) return hipErrorInvalidValue;
+  if (spec && (a->mode != 2 || a->tw_base != 0 || ntw != 2 || mlp_ngp2(a->D) != spec)) return hipErrorInvalidValue;
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_fwd_kernel),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 140 * 1024) != hipSuccess)
-      return hipErrorInvalidValue;
+    const void* ks[4] = {reinterpret_cast<const void*>(&mlp_fwd_kernel<0>),
+                         reinterpret_cast<const void*>(&mlp_fwd_kernel<1>),
+                         reinterpret_cast<const void*>(&mlp_fwd_kernel<2>),
+                         reinterpret_cast<const void*>(&mlp_fwd_kernel<4>)};
+    for (const void* k : ks)
+      if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 140 * 1024) != hipSuccess)
+        return hipErrorInvalidValue;
     attr = true;
   }
   if (lds > 140 * 1024) return hipErrorInvalidValue;
   dim3 grid((a->B + MLP_BM - 1) / MLP_BM, ntw);
-  mlp_fwd_kernel<<<grid, MLP_THREADS, lds, stream>>>(*a);
+  switch (spec) {
+    case 0: mlp_fwd_kernel<0><<<grid, MLP_THREADS, lds, stream>>>(*a); break;
+    case 1: mlp_fwd_kernel<1><<<grid, MLP_THREADS, lds, stream>>>(*a); break;
+    case 2: mlp_fwd_kernel<2><<<grid, MLP_THREADS, lds, stream>>>(*a); break;
+    case 4: mlp_fwd_kernel<4><<<grid, MLP_THREADS, lds, stream>>>(*a); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

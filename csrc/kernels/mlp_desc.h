@@ -20,7 +20,8 @@ struct MlpTower {
   int64_t gb[MLP_MAXL];
   int64_t xs[MLP_MAXL];       // train workspace: layer inputs  [B][in]
   int64_t dp[MLP_MAXL];       // train workspace: dL/d(pre-activation) [B][out]
-  int64_t Wt[MLP_MAXL];       // transposed weight shadow [out][16 * ngp2(in)] (forward B operand)
+  int64_t F[MLP_MAXL];        // forward operand: fp32 FRAGMENT copy of W (common.h mlp_frag_f), zero pad
+  int64_t G[MLP_MAXL];        // data-gradient operand: fp32 fragment copy of W (mlp_frag_g; layers >= 1), zero pad
 };
 
 struct MlpArgs {
@@ -49,7 +50,9 @@ struct MlpArgs {
   float* mpart;               // optional [ceil(B/16)][MPART_W]: per-workgroup partials instead of the atomics above
   float inv_B;
   int64_t* stamps;            // optional diagnostics: [2 towers][16] s_memrealtime at phase ends of workgroup (0, tower)
-  int prefetch;               // train: touch this workgroup's share of the tower's weights at entry (LDS-DMA, no registers)
+  // train launches of the reference towers (mlp.hip SPEC path): a by-value copy of both tower descriptors, so the
+  // weight-fragment pointers are kernel-argument (scalar) reads at entry, before any other memory round trip
+  MlpTower htw[2];
 };
 
 struct WgradArgs {

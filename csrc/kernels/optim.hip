@@ -78,16 +78,30 @@ __device__ __forceinline__ float partial_total(const float* __restrict__ parts, 
 
 
 // One optimiser segment (a parameter group of the flat slab) with its own lr / step / clip / norm settings.
-// Optional transposed fp32 shadows of [K][N] weight matrices inside the segment (the MLP engine's forward reads
-// Wt[N][ldt]); written by the update itself, so the shadow never needs a pass of its own.
-constexpr int OPT_MAXT = 6;
-// ldt < 0: a FRAGMENT-ORDERED bf16 copy of the row-major [K][N] weight (the CNN engine's MFMA weight operands,
-// cnn_fused.hip frag_w1..3): element (k, c) goes to u16 ((((k / 16) * (N / 32) + c / 32) * 64 + (c / 8 % 4) * 16 +
-// k % 16) * 8 + c % 8), so a wave's 16-byte-per-lane fragment load is one contiguous 1 KB read.
+// Optional copies of [K][N] weight matrices inside the segment, written by the update itself (no pass of their own):
+//   ldt >= 0: transposed fp32 Wt[N][ldt];
+//   ldt -1:   a FRAGMENT-ORDERED bf16 copy (the CNN engine's MFMA weight operands, cnn_fused.hip frag_w1..3): element
+//             (k, c) goes to u16 ((((k / 16) * (N / 32) + c / 32) * 64 + (c / 8 % 4) * 16 + k % 16) * 8 + c % 8), so a
+//             wave's 16-byte-per-lane fragment load is one contiguous 1 KB read;
+//   ldt -3 / -4: the MLP engine's fp32 fragment copies F (forward operand) / G (data-gradient operand), common.h
+//             mlp_frag_f / mlp_frag_g. One weight has both entries over the same range, so these entries never end
+//             the search (the others do: their ranges are disjoint).
+constexpr int OPT_MAXT = 8;
 struct OptTrans {
   int64_t off;   // element offset of W within the segment
   int K, N, ldt;
   float* dst;
+};
+// An MLP weight [K][N] with N % 64 == 0 updated by 16-row x 64-column wave items (whole 256-byte row runs) that also
+// write its fragment copies F / G (G may be absent: layer 0) as contiguous 1 KB wave stores, transposed through LDS --
+// instead of per-element scattered stores (table codes -5 / -6)
+constexpr int OPT_MAXBLK = 4;
+constexpr int BLK_LD = 68;   // row stride (floats) of the workgroup's 16 x 64 LDS tile
+struct OptBlk {
+  int64_t off;
+  int K, N, items;
+  float* F;
+  float* G;
 };
 
 struct OptSeg {
@@ -108,52 +122,83 @@ struct OptSeg {
   int64_t kc_off = 0;
   int kc_K = 0, kc_N = 0;
   u16* kc_dst = nullptr;
+  // optional device gate: the launch is skipped (no parameter, moment or step-count change) while *gate == 0 (lag-1
+  // data parallelism before its first all-reduced gradient, trainer.py _update_body_lag1)
+  const int* gate = nullptr;
+  int nblk = 0;
+  OptBlk blk[OPT_MAXBLK];
+  int dbg = 0;   // diagnostics (aca_opt_set_unroll(100 + mode)): 1 no G stores, 2 no F stores, 4 no LDS tile
 };
+
+// element o (< K * N) of one copy entry; returns false for the MLP fragment codes (the search goes on)
+__device__ __forceinline__ bool write_one(const OptTrans& T, uint32_t o, float v) {
+  // 32-bit division (a 64-bit one is a ~100-instruction software sequence per element)
+  const uint32_t n = (uint32_t)T.N;
+  const uint32_t k = o / n, c = o - k * n;
+  if (T.ldt == -3) {
+    T.dst[mlp_frag_f(k, c, T.K)] = v;
+    return false;
+  }
+  if (T.ldt == -4) {
+    T.dst[mlp_frag_g(k, c, T.N)] = v;
+    return false;
+  }
+  if (T.ldt < 0) {
+    const uint32_t f = (((k >> 4) * (n >> 5) + (c >> 5)) * 64u + ((c >> 3) & 3u) * 16u + (k & 15u)) * 8u + (c & 7u);
+    reinterpret_cast<u16*>(T.dst)[f] = f2bf(v);
+  } else {
+    T.dst[(size_t)c * T.ldt + k] = v;
+  }
+  return true;
+}
 
 __device__ __forceinline__ void write_trans(const OptSeg& S, size_t i, float v) {
   for (int e = 0; e < S.ntrans; ++e) {
     const OptTrans& T = S.tr[e];
     const int64_t o = (int64_t)i - T.off;
-    if (o >= 0 && o < (int64_t)T.K * T.N) {
-      // 32-bit division (a 64-bit one is a ~100-instruction software sequence per element)
-      const uint32_t ou = (uint32_t)o, n = (uint32_t)T.N;
-      const uint32_t k = ou / n, c = ou - k * n;
-      if (T.ldt < 0) {
-        const uint32_t f = (((k >> 4) * (n >> 5) + (c >> 5)) * 64u + ((c >> 3) & 3u) * 16u + (k & 15u)) * 8u + (c & 7u);
-        reinterpret_cast<u16*>(T.dst)[f] = f2bf(v);
-      } else {
-        T.dst[(size_t)c * T.ldt + k] = v;
-      }
-      return;
-    }
+    if (o >= 0 && o < (int64_t)T.K * T.N && write_one(T, (uint32_t)o, v)) return;
   }
 }
 
-// The four consecutive elements 4 * i4 .. + 3 of a float4 group: for a fragment-ordered copy (ldt < 0, offset and N
-// multiples of 4) they are 4 consecutive u16 of one lane's 8 -> ONE 8-byte store (one 32-bit index computation)
-// instead of four 2-byte stores; other shadows per element.
+// The four consecutive elements 4 * i4 .. + 3 of a float4 group. Whole groups inside one row (offset and N multiples
+// of 4): a bf16 fragment copy (ldt -1) takes them as 4 consecutive u16 of one lane's 8 -> ONE 8-byte store, the MLP
+// G copy as 4 consecutive floats -> ONE 16-byte store (one 32-bit index computation each); others per element.
 __device__ __forceinline__ void write_trans4(const OptSeg& S, size_t i4, float4 p4) {
   const size_t i = 4 * i4;
   for (int e = 0; e < S.ntrans; ++e) {
     const OptTrans& T = S.tr[e];
     const int64_t o = (int64_t)i - T.off;
-    if (o + 3 >= 0 && o < (int64_t)T.K * T.N) {
-      if (T.ldt < 0 && o >= 0 && o + 3 < (int64_t)T.K * T.N && ((o | T.N) & 3) == 0) {
-        const uint32_t ou = (uint32_t)o, n = (uint32_t)T.N;
-        const uint32_t k = ou / n, c = ou - k * n;
-        const uint32_t f = (((k >> 4) * (n >> 5) + (c >> 5)) * 64u + ((c >> 3) & 3u) * 16u + (k & 15u)) * 8u + (c & 7u);
-        uint2 pk;
-        pk.x = (uint32_t)f2bf(p4.x) | ((uint32_t)f2bf(p4.y) << 16);
-        pk.y = (uint32_t)f2bf(p4.z) | ((uint32_t)f2bf(p4.w) << 16);
-        *reinterpret_cast<uint2*>(reinterpret_cast<u16*>(T.dst) + f) = pk;
-        return;
+    const int64_t KN = (int64_t)T.K * T.N;
+    if (o + 3 < 0 || o >= KN) continue;
+    const bool whole = o >= 0 && o + 3 < KN && ((o | T.N) & 3) == 0;
+    if (whole && T.ldt <= -3) {
+      const uint32_t ou = (uint32_t)o, n = (uint32_t)T.N;
+      const uint32_t k = ou / n, c = ou - k * n;
+      if (T.ldt == -4) {
+        *reinterpret_cast<float4*>(T.dst + mlp_frag_g(k, c, T.N)) = p4;
+      } else {
+        const uint32_t f = mlp_frag_f(k, c, T.K);   // c .. c + 3 share the tile (c % 4 == 0): lanes 4 floats apart
+        T.dst[f] = p4.x;
+        T.dst[f + 4] = p4.y;
+        T.dst[f + 8] = p4.z;
+        T.dst[f + 12] = p4.w;
       }
-      write_trans(S, i, p4.x);
-      write_trans(S, i + 1, p4.y);
-      write_trans(S, i + 2, p4.z);
-      write_trans(S, i + 3, p4.w);
+      continue;
+    }
+    if (whole && T.ldt == -1) {
+      const uint32_t ou = (uint32_t)o, n = (uint32_t)T.N;
+      const uint32_t k = ou / n, c = ou - k * n;
+      const uint32_t f = (((k >> 4) * (n >> 5) + (c >> 5)) * 64u + ((c >> 3) & 3u) * 16u + (k & 15u)) * 8u + (c & 7u);
+      uint2 pk;
+      pk.x = (uint32_t)f2bf(p4.x) | ((uint32_t)f2bf(p4.y) << 16);
+      pk.y = (uint32_t)f2bf(p4.z) | ((uint32_t)f2bf(p4.w) << 16);
+      *reinterpret_cast<uint2*>(reinterpret_cast<u16*>(T.dst) + f) = pk;
       return;
     }
+    const float pv[4] = {p4.x, p4.y, p4.z, p4.w};   // (a group straddling two entries: each takes its part)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (o + j >= 0 && o + j < KN) write_one(T, (uint32_t)(o + j), pv[j]);
   }
 }
 
@@ -161,7 +206,8 @@ __device__ __forceinline__ void write_trans4(const OptSeg& S, size_t i4, float4 
 // (its partial loads + block sum would otherwise be a dependent round trip ahead of every element load).
 template <bool ADAM, int U>
 __device__ __forceinline__ void opt_body(const OptSeg& S, float b1, float b2, float eps, int zero_grad, int vblk,
-                                         int vgrid, int* flag, float* shr, u16* kcs) {
+                                         int vgrid, int* flag, float* shr, u16* kcs, float* blks) {
+  if (S.gate && *S.gate == 0) return;   // uniform over the launch
   float* __restrict__ p = S.p;
   float* __restrict__ g = S.g;
   float* __restrict__ m = S.m;
@@ -173,7 +219,15 @@ __device__ __forceinline__ void opt_body(const OptSeg& S, float b1, float b2, fl
   const size_t stride = (size_t)vgrid * blockDim.x * U;
   // the k-contiguous fragment region [kc0, kc1) in float4 groups is left to the wave-item loop below
   const size_t kc0 = S.kc_K ? (size_t)S.kc_off / 4 : 0, kc1 = S.kc_K ? kc0 + (size_t)S.kc_K * S.kc_N / 4 : 0;
-  auto in_kc = [&](size_t i) { return i >= kc0 && i < kc1; };
+  // ... and so are the MLP weight blocks (their 16 x 16 wave items below)
+  auto in_kc = [&](size_t i) {
+    bool r = i >= kc0 && i < kc1;
+    for (int e = 0; e < S.nblk; ++e) {
+      const size_t b0 = (size_t)S.blk[e].off / 4;
+      r |= i >= b0 && i < b0 + (size_t)S.blk[e].K * S.blk[e].N / 4;
+    }
+    return r;
+  };
   float4 g4[U], v4[U], p4[U], m4[U];
   auto load = [&](size_t i0) {
 #pragma unroll
@@ -208,6 +262,37 @@ __device__ __forceinline__ void opt_body(const OptSeg& S, float b1, float b2, fl
     km = ADAM ? reinterpret_cast<const float4*>(m)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
   };
   if (gw0 < kItems) kc_load(gw0);
+  // MLP weight blocks: WORKGROUP items (matrix e, 16-row tile kt, 64-column group cg), taken by workgroup vblk,
+  // vblk + vgrid, ...; wave w, lane -> row kt * 16 + 4 w + (lane >> 4), columns cg * 64 + 4 (lane & 15) .. + 3 (whole
+  // 256-byte row runs, one float4 per thread like the element path)
+  int bItems = 0;
+  for (int e = 0; e < S.nblk; ++e) bItems += S.blk[e].items;
+  auto blk_at = [&](int it, int& e, int& kt, int& cg) {
+    e = 0;
+    while (e + 1 < S.nblk && it >= S.blk[e].items) it -= S.blk[e++].items;
+    const int ncg = S.blk[e].N >> 6;
+    kt = it / ncg;
+    cg = it - kt * ncg;
+  };
+  float4 bg, bv, bp, bm;
+  auto blk_row = [&](const OptBlk& Bk, int kt, int cg, bool& ok) {
+    const int k = kt * 16 + 4 * (threadIdx.x >> 6) + (lane >> 4);
+    ok = k < Bk.K;
+    return ((size_t)Bk.off + (size_t)k * Bk.N + cg * 64 + 4 * (lane & 15)) / 4;
+  };
+  auto blk_load = [&](int it) {
+    int e, kt, cg;
+    blk_at(it, e, kt, cg);
+    bool ok;
+    const size_t i = blk_row(S.blk[e], kt, cg, ok);
+    if (ok) {
+      bg = reinterpret_cast<const float4*>(g)[i];
+      bv = reinterpret_cast<const float4*>(v)[i];
+      bp = reinterpret_cast<const float4*>(p)[i];
+      bm = ADAM ? reinterpret_cast<const float4*>(m)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  if (vblk < bItems) blk_load(vblk);
   float scale = 1.f;
   if (S.parts) {
     const float gsq = partial_total(S.parts, shr) * S.norm_mul;
@@ -291,6 +376,56 @@ __device__ __forceinline__ void opt_body(const OptSeg& S, float b1, float b2, fl
     __builtin_amdgcn_wave_barrier();   // the scratch is rewritten by the next item
     if (it + GW < kItems) kc_load(it + GW);
   }
+  // MLP weight blocks: the update (whole row runs), the new values into the workgroup's LDS tile T[16][64] (row stride
+  // BLK_LD), then wave w writes the G and F fragment blocks of column tile cg * 4 + w as whole 1 KB wave stores
+  // (OPT_THREADS = 4 waves = the 4 column tiles of the item)
+  for (int it = vblk; it < bItems; it += vgrid) {
+    int e, kt, cg;
+    blk_at(it, e, kt, cg);
+    const OptBlk& Bk = S.blk[e];
+    const int w = threadIdx.x >> 6;
+    bool ok;
+    const size_t i = blk_row(Bk, kt, cg, ok);
+    float4 w4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (ok) {
+      if (zero_grad) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      upd(bg.x, bv.x, bm.x, bp.x);
+      upd(bg.y, bv.y, bm.y, bp.y);
+      upd(bg.z, bv.z, bm.z, bp.z);
+      upd(bg.w, bv.w, bm.w, bp.w);
+      reinterpret_cast<float4*>(v)[i] = bv;
+      if (ADAM) reinterpret_cast<float4*>(m)[i] = bm;
+      reinterpret_cast<float4*>(p)[i] = bp;
+      if (shadow) {
+        uint2 sv;
+        sv.x = (uint32_t)f2bf(bp.x) | ((uint32_t)f2bf(bp.y) << 16);
+        sv.y = (uint32_t)f2bf(bp.z) | ((uint32_t)f2bf(bp.w) << 16);
+        reinterpret_cast<uint2*>(shadow)[i] = sv;
+      }
+      w4 = bp;
+    }
+    if (S.dbg & 4) {
+      if (it + vgrid < bItems) blk_load(it + vgrid);
+      continue;
+    }
+    // (rows past K are zero: the fragment pads)
+    *reinterpret_cast<float4*>(blks + (4 * w + (lane >> 4)) * BLK_LD + 4 * (lane & 15)) = w4;
+    __syncthreads();
+    const int r = lane & 15, q = lane >> 4, ct = cg * 4 + w;
+    // G block (kt, ct), lane (q, r): W[kt * 16 + r][ct * 16 + 4 q .. + 3]
+    if (Bk.G && !(S.dbg & 1))
+      *reinterpret_cast<float4*>(Bk.G + ((size_t)(kt * mlp_ngp2(Bk.N) + ct) * 64 + lane) * 4) =
+          *reinterpret_cast<const float4*>(blks + r * BLK_LD + 16 * w + 4 * q);
+    // F block (ct, kt), lane (q, r): W[kt * 16 + 4 q + s][ct * 16 + r], s = 0..3
+    float4 f4;
+    f4.x = blks[(4 * q + 0) * BLK_LD + 16 * w + r];
+    f4.y = blks[(4 * q + 1) * BLK_LD + 16 * w + r];
+    f4.z = blks[(4 * q + 2) * BLK_LD + 16 * w + r];
+    f4.w = blks[(4 * q + 3) * BLK_LD + 16 * w + r];
+    if (!(S.dbg & 2)) *reinterpret_cast<float4*>(Bk.F + ((size_t)(ct * mlp_ngp2(Bk.K) + kt) * 64 + lane) * 4) = f4;
+    __syncthreads();   // the tile is rewritten by the next item
+    if (it + vgrid < bItems) blk_load(it + vgrid);
+  }
   if (vblk == 0) {   // scalar tail
     for (size_t i = n4 * 4 + threadIdx.x; i < n; i += blockDim.x) {
       float gi = g[i], vi = v[i], pi = p[i], mi = ADAM ? m[i] : 0.f;
@@ -337,7 +472,8 @@ __global__ void __launch_bounds__(OPT_THREADS) opt_kernel(OptSeg S, float b1, fl
   __shared__ int flag;
   __shared__ float shr[16];
   __shared__ __attribute__((aligned(16))) u16 kcs[OPT_THREADS / 64 * 256];
-  opt_body<ADAM, U>(S, b1, b2, eps, zero_grad, blockIdx.x, gridDim.x, &flag, shr, kcs);
+  __shared__ __attribute__((aligned(16))) float blks[16 * BLK_LD];
+  opt_body<ADAM, U>(S, b1, b2, eps, zero_grad, blockIdx.x, gridDim.x, &flag, shr, kcs, blks);
 }
 
 // Several parameter groups (e.g. the reference's separate actor and critic optimisers) in ONE launch: the grid is
@@ -354,9 +490,10 @@ __global__ void __launch_bounds__(OPT_THREADS) opt_multi_kernel(OptMulti M, floa
   __shared__ int flag;
   __shared__ float shr[16];
   __shared__ __attribute__((aligned(16))) u16 kcs[OPT_THREADS / 64 * 256];
+  __shared__ __attribute__((aligned(16))) float blks[16 * BLK_LD];
   int b = blockIdx.x, k = 0;
   while (k + 1 < M.nseg && b >= M.seg[k].nblocks) b -= M.seg[k++].nblocks;
-  opt_body<ADAM, 1>(M.seg[k], b1, b2, eps, zero_grad, b, M.seg[k].nblocks, &flag, shr, kcs);
+  opt_body<ADAM, 1>(M.seg[k], b1, b2, eps, zero_grad, b, M.seg[k].nblocks, &flag, shr, kcs, blks);
 }
 
 // Gradient finaliser: the last step of a backward pass before the optimiser. Gradient segments are either
@@ -638,8 +775,11 @@ __global__ void __launch_bounds__(OPT_THREADS) grad_finalize_kernel(const int64_
 
 // lag-1 data parallelism: dst <- src, src <- 0 in one pass (the next backward accumulates into a clean slab while
 // dst is all-reduced and consumed by the next optimiser step)
+// lag-1 data parallelism: C <- G, G <- 0; `gate` (optional) is set to 1 -- C now holds a gradient the next
+// optimiser launch gated on it may apply (OptSeg::gate)
 __global__ void __launch_bounds__(OPT_THREADS) grad_move_kernel(float* __restrict__ src, float* __restrict__ dst,
-                                                                size_t n) {
+                                                                size_t n, int* __restrict__ gate) {
+  if (gate && blockIdx.x == 0 && threadIdx.x == 0) *gate = 1;
   const size_t n4 = n / 4;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += stride) {
@@ -668,11 +808,15 @@ static int opt_grid(size_t n, int unroll = 1) {   // `unroll` float4 groups per 
 
 // float4 groups per thread of the single-segment optimiser launches (a diagnostic knob, aca_opt_set_unroll)
 static int g_opt_unroll = 1;
+static int g_opt_dbg = 0;
 
 template <bool ADAM>
 static void launch_opt(OptSeg& S, float b1, float b2, float eps, int zero_grad, hipStream_t stream) {
   const int U = g_opt_unroll;
   S.nblocks = opt_grid(S.n, U);
+  int bi = 0;   // one workgroup per MLP block item (see aca_opt_multi)
+  for (int e = 0; e < S.nblk; ++e) bi += S.blk[e].items;
+  if (bi > S.nblocks) S.nblocks = bi;
   switch (U) {
     case 2: opt_kernel<ADAM, 2><<<S.nblocks, OPT_THREADS, 0, stream>>>(S, b1, b2, eps, zero_grad); break;
     case 4: opt_kernel<ADAM, 4><<<S.nblocks, OPT_THREADS, 0, stream>>>(S, b1, b2, eps, zero_grad); break;
@@ -727,24 +871,53 @@ extern "C" hipError_t aca_grad_finalize(const int64_t* jobs, int njobs, float* p
 }
 
 // trans: host table [OPT_MAXT][5] = (offset, K, N, ldt, dst) of one segment; K == 0 ends the list. ldt -1: the
-// conv kernels' fragment order (write_trans); ldt -2: the k-contiguous fragment region (at most one; opt_body).
+// conv kernels' fragment order (write_trans); ldt -2: the k-contiguous fragment region (at most one; opt_body);
+// ldt -3 / -4: the MLP engine's F / G fragment copies, per element; ldt -5 (+ an optional -6 row of the same weight):
+// the F (G) copy of an N % 16 == 0 weight by 16 x 16 block items (OptBlk); ldt -9 (K = N = 1, at most one): dst is the
+// launch's gate (const int*, OptSeg::gate).
 static bool opt_load_trans(OptSeg& S, const int64_t* tw0) {
   S.ntrans = 0;
   S.kc_K = 0;
+  S.gate = nullptr;
   if (!tw0) return true;
+  S.nblk = 0;
   for (int e = 0; e < OPT_MAXT; ++e) {
     const int64_t* tw = tw0 + (int64_t)e * 5;
     if (tw[1] <= 0) break;
-    if (tw[3] < 0 && (tw[1] % 16 || tw[2] % 32)) return false;   // fragment order: 16-row tiles, 32-wide k-steps
-    if (tw[3] == -2) {
-      if (S.kc_K || tw[0] % 4 || tw[0] < 0 || (size_t)(tw[0] + tw[1] * tw[2]) > S.n || tw[4] % 16) return false;
+    const int64_t ldt = tw[3];
+    if (ldt == -5) {   // an MLP weight block matrix: F (a -6 row of the same weight may follow with G)
+      if (S.nblk >= OPT_MAXBLK || tw[2] % 64 || tw[0] % 4 || tw[0] < 0 || (size_t)(tw[0] + tw[1] * tw[2]) > S.n ||
+          !tw[4] || tw[4] % 16 || tw[1] > 4096 || tw[2] > 4096)
+        return false;
+      OptBlk& B = S.blk[S.nblk++];
+      B = OptBlk{tw[0], (int)tw[1], (int)tw[2], (int)(((tw[1] + 15) / 16) * (tw[2] / 64)),
+                 reinterpret_cast<float*>(tw[4]), nullptr};
+      continue;
+    }
+    if (ldt == -6) {
+      if (!S.nblk || S.blk[S.nblk - 1].off != tw[0] || S.blk[S.nblk - 1].K != tw[1] || S.blk[S.nblk - 1].N != tw[2] ||
+          S.blk[S.nblk - 1].G || !tw[4] || tw[4] % 16)
+        return false;
+      S.blk[S.nblk - 1].G = reinterpret_cast<float*>(tw[4]);
+      continue;
+    }
+    if (ldt == -9) {
+      if (S.gate || !tw[4] || tw[4] % 4) return false;
+      S.gate = reinterpret_cast<const int*>(tw[4]);
+      continue;
+    }
+    if ((ldt == -1 || ldt == -2) && (tw[1] % 16 || tw[2] % 32)) return false;   // 16-row tiles, 32-wide k-steps
+    if (ldt < -4 || ldt == 0 || tw[0] < 0 || (size_t)(tw[0] + tw[1] * tw[2]) > S.n || tw[2] <= 0) return false;
+    if (ldt <= -3 && (tw[4] % 16 || tw[1] * tw[2] > (int64_t)1 << 31)) return false;
+    if (ldt == -2) {
+      if (S.kc_K || tw[0] % 4 || tw[4] % 16) return false;
       S.kc_off = tw[0];
       S.kc_K = (int)tw[1];
       S.kc_N = (int)tw[2];
       S.kc_dst = reinterpret_cast<u16*>(tw[4]);
       continue;
     }
-    S.tr[S.ntrans++] = OptTrans{tw[0], (int)tw[1], (int)tw[2], (int)tw[3], reinterpret_cast<float*>(tw[4])};
+    S.tr[S.ntrans++] = OptTrans{tw[0], (int)tw[1], (int)tw[2], (int)ldt, reinterpret_cast<float*>(tw[4])};
   }
   return true;
 }
@@ -810,12 +983,16 @@ extern "C" hipError_t aca_opt_multi(const int64_t* words, const float* fvals, co
     S.gmul = f[2];
     S.norm_mul = f[3];
     S.t_off = t_off < 0 ? -1 : t_off;
+    S.dbg = g_opt_dbg;
     if (S.n == 0 || !opt_aligned(S.p, S.g, adam ? S.m : S.v, S.v, S.shadow)) return hipErrorInvalidValue;
     if (adam && (!S.m || !S.t || !S.ticket)) return hipErrorInvalidValue;
-    S.nblocks = opt_grid(S.n);
-    total += S.nblocks;
     // trans: [nseg][OPT_MAXT][5]
     if (!opt_load_trans(S, trans ? trans + (int64_t)k * OPT_MAXT * 5 : nullptr)) return hipErrorInvalidValue;
+    S.nblocks = opt_grid(S.n);
+    int bi = 0;   // one workgroup per MLP block item: a second round would be a dependent memory round trip
+    for (int e = 0; e < S.nblk; ++e) bi += S.blk[e].items;
+    if (bi > S.nblocks) S.nblocks = bi;
+    total += S.nblocks;
   }
   if (adam) opt_multi_kernel<true><<<total, OPT_THREADS, 0, stream>>>(M, b1, b2, eps, zero_grad);
   else opt_multi_kernel<false><<<total, OPT_THREADS, 0, stream>>>(M, 0.f, b2, eps, zero_grad);
@@ -824,13 +1001,14 @@ extern "C" hipError_t aca_opt_multi(const int64_t* words, const float* fvals, co
 
 extern "C" int aca_opt_set_unroll(int u) {
   if (u == 1 || u == 2 || u == 4) g_opt_unroll = u;
+  if (u >= 100 && u < 108) g_opt_dbg = u - 100;
   return g_opt_unroll;
 }
 
-extern "C" hipError_t aca_grad_move(float* src, float* dst, size_t n, hipStream_t stream) {
+extern "C" hipError_t aca_grad_move(float* src, float* dst, size_t n, int* gate, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   if ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) % 16) return hipErrorInvalidValue;
-  grad_move_kernel<<<opt_grid(n), OPT_THREADS, 0, stream>>>(src, dst, n);
+  grad_move_kernel<<<opt_grid(n), OPT_THREADS, 0, stream>>>(src, dst, n, gate);
   return hipGetLastError();
 }
 

@@ -215,9 +215,10 @@ def test_prp_permutation_kernel_matches_oracle(cuda):
         assert torch.equal(torch.sort(out.cpu()).values, torch.arange(n))
 
 
-def test_optimizer_writes_transposed_shadows(cuda):
-    """The multi-group optimiser launch keeps the MLP engine's transposed weight shadows equal to W^T after every
-    step, and checkpoint restore refreshes them."""
+def test_optimizer_writes_fragment_copies(cuda):
+    """The multi-group optimiser launch keeps the MLP engine's fp32 weight fragment copies (forward F, data-gradient
+    G) equal to the fragment order of W after every step, and the refresh pass rewrites them."""
+    from actor_critic_algs_on_tensorflow_amd.ops.mlp import frag_f, frag_g
     from actor_critic_algs_on_tensorflow_amd import preset
     from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
     tr = ActorCriticTrainer(preset("mujoco_ppo_dp8", num_envs=8, n_steps=16, ppo_epochs=1, ppo_minibatches=2,
@@ -230,11 +231,13 @@ def test_optimizer_writes_transposed_shadows(cuda):
 
     def check():
         for tw in tr.mlp.towers:
-            for lay in tw:
-                wt = tr.mlp.wt[id(lay)]
-                K = lay.in_features
-                assert torch.equal(wt[:, :K], lay.kernel.detach().t()), lay
-                assert (wt[:, K:] == 0).all()
+            for i, lay in enumerate(tw):
+                W = lay.kernel.detach()
+                assert torch.equal(tr.mlp.F[id(lay)], frag_f(W)), lay
+                if i:
+                    assert torch.equal(tr.mlp.G[id(lay)], frag_g(W)), lay
+                else:
+                    assert id(lay) not in tr.mlp.G
     check()
     with torch.no_grad():
         tr.flat.data.mul_(0.5)

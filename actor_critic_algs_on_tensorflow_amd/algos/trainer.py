@@ -587,23 +587,23 @@ class ActorCriticTrainer:
 
     def _run_optimizers(self):
         """Optimiser step(s). Several groups (the reference's separate actor / critic Adam) run as ONE launch, which
-        also writes the MLP engine's transposed weight shadows; otherwise one launch per group (+ a shadow pass)."""
+        also writes the MLP engine's weight fragment copies; otherwise one launch per group (+ a copy pass)."""
         opts = list(self.opts.values())
         if len(opts) > 1 and _native.use_native(self.flat.data):
             from ..ops.optim import FusedGroupStep
             if not hasattr(self, "_group_step"):
                 self._group_step = None
                 if FusedGroupStep.compatible(opts):
-                    tr = None
+                    copies = None
                     if self.mlp is not None and list(self.opts) == ["actor", "critic"]:
-                        tr = self.mlp.transposes()
-                    self._group_step = FusedGroupStep(opts, tr)
+                        copies = self.mlp.frag_copies()
+                    self._group_step = FusedGroupStep(opts, copies)
             if self._group_step is not None:
                 t_off = getattr(self, "_t_off", None)
                 self._group_step.step(t_off=t_off)
                 if t_off is not None:
                     self._t_offs_used += 1
-                if self.mlp is not None and self._group_step._trans is None:
+                if self.mlp is not None and self._group_step._items[0] is None:
                     self.mlp.sync_shadow()
                 return
         # the CNN engine's grouped A2C backward STORES every gradient element (head launch, dWfc GEMM, finaliser of the

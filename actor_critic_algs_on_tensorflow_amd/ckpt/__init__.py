@@ -167,6 +167,48 @@ def _gather_env_states(trainer):
     return got if dp.rank == 0 else None
 
 
+_SLAB_STATE = ("m", "v")   # optimiser state laid out like the parameter slab
+
+
+def _param_ranges(trainer, opt):
+    """(parameter name, start, end) of every parameter of ``opt``'s slab segment, relative to the segment."""
+    flat = trainer.flat
+    name_of = {id(p): n for n, p in trainer.model.named_parameters()}
+    out = []
+    for p, off in zip(flat.params, flat.offsets):
+        if opt.start <= off < opt.end:
+            out.append((name_of[id(p)], off - opt.start, off - opt.start + p.numel()))
+    return out
+
+
+def _load_opt_state(trainer, opt, g, t, path):
+    """Optimiser state of group ``g``: m / v scattered by parameter name; a bundle written before the per-name form
+    (whole slab vectors) is accepted only when its size matches this slab."""
+    sd = {}
+    for k, v in t.items():
+        if not k.startswith(f"_acamd/opt/{g}/"):
+            continue
+        rest = k[len(f"_acamd/opt/{g}/"):]
+        if "/" not in rest:
+            sd[rest] = torch.as_tensor(np.array(v))
+    for k in _SLAB_STATE:
+        per_name = {kk[len(f"_acamd/opt/{g}/{k}/"):]: v for kk, v in t.items() if kk.startswith(f"_acamd/opt/{g}/{k}/")}
+        if not per_name:
+            if k in sd and sd[k].numel() != getattr(opt, k).numel():
+                raise ValueError(f"checkpoint {path}: optimiser state {g}/{k} has {sd[k].numel()} elements, this "
+                                 f"slab {getattr(opt, k).numel()} (written with another parameter layout)")
+            continue
+        vec = torch.zeros_like(getattr(opt, k), device="cpu")
+        for name, a, b in _param_ranges(trainer, opt):
+            if name not in per_name:
+                raise KeyError(f"checkpoint {path} lacks optimiser state {g}/{k}/{name}")
+            vec[a:b] = torch.as_tensor(np.array(per_name[name])).reshape(-1)
+        sd[k] = vec
+    if sd:
+        sd = {k: (v.reshape(()) if v.numel() == 1 and k in ("t", "lr") else v) for k, v in sd.items()}
+        opt.load_state_dict(sd)
+
+
 def save_trainer(trainer, path=None):
     """Checkpoint of an :class:`..algos.trainer.ActorCriticTrainer` (model + optimiser + counters + env banks).
 
@@ -184,7 +226,11 @@ def save_trainer(trainer, path=None):
     tensors = dict(model_tensors(trainer.model, cfg.model_variant, trainer.opts))
     for g, opt in trainer.opts.items():
         for k, v in opt.state_dict().items():
-            tensors[f"_acamd/opt/{g}/{k}"] = v.reshape(-1) if v.dim() else v
+            if k in _SLAB_STATE:   # per parameter name: independent of the slab layout (parameter order, padding)
+                for name, a, b in _param_ranges(trainer, opt):
+                    tensors[f"_acamd/opt/{g}/{k}/{name}"] = v[a:b]
+            else:
+                tensors[f"_acamd/opt/{g}/{k}"] = v.reshape(-1) if v.dim() else v
     tensors["_acamd/iteration"] = np.asarray(trainer.iteration, dtype=np.int64)
     tensors["_acamd/env_steps"] = np.asarray(trainer.env_steps, dtype=np.int64)
     for k, v in envs[0].items():
@@ -233,14 +279,10 @@ def load_trainer(trainer, path):
         trainer.shadow.copy_(trainer.flat.data)
         if getattr(trainer, "engine", None) is not None:   # the engine's fragment-ordered conv weight copies
             trainer.engine.sync_frag()
-    if getattr(trainer, "mlp", None) is not None:   # transposed weight shadows of the MLP engine
+    if getattr(trainer, "mlp", None) is not None:   # the MLP engine's weight fragment copies
         trainer.mlp.sync_shadow()
     for g, opt in trainer.opts.items():
-        sd = {k.rsplit("/", 1)[1]: torch.as_tensor(np.array(v)) for k, v in t.items()
-              if k.startswith(f"_acamd/opt/{g}/")}
-        if sd:
-            sd = {k: (v.reshape(()) if v.numel() == 1 and k in ("t", "lr") else v) for k, v in sd.items()}
-            opt.load_state_dict(sd)
+        _load_opt_state(trainer, opt, g, t, path)
     if "_acamd/iteration" in t:
         trainer.iteration = int(t["_acamd/iteration"])
         trainer.env_steps = int(t["_acamd/env_steps"])

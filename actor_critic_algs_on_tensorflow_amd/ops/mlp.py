@@ -127,22 +127,11 @@ class MLPEngine:
         self.spec = True
         self.sync_shadow()
 
-    def transposes(self):
-        """Per tower (= optimiser group actor, critic): (W view, K, N, dst, code) of the fragment copies the optimiser
-        step writes as it goes (optim.hip): weights with N % 64 == 0 as 16-row x 64-column block items writing whole
-        1 KB fragments (-5 forward copy F, -6 data-gradient copy G), the others per element (-3 F, -4 G)."""
-        out = []
-        for tw in self.towers:
-            lst = []
-            for lay in tw:
-                W = self._views(lay.kernel)[0]
-                K, N = lay.in_features, lay.out_features
-                blk = N % 64 == 0
-                lst.append((W, K, N, self.F[id(lay)], -5 if blk else -3))
-                if id(lay) in self.G:
-                    lst.append((W, K, N, self.G[id(lay)], -6 if blk else -4))
-            out.append(lst)
-        return out
+    def frag_copies(self):
+        """Per tower (= optimiser group actor, critic): (W view, K, N, F, G or None) -- the fragment copies the
+        optimiser step writes as it goes (``ops/optim.py`` FusedGroupStep item tables)."""
+        return [[(self._views(l.kernel)[0], l.in_features, l.out_features, self.F[id(l)], self.G.get(id(l)))
+                 for l in tw] for tw in self.towers]
 
     def sync_shadow(self):
         """Rewrites the weight fragment copies from the fp32 slab (the optimiser step writes them itself; this pass

@@ -256,31 +256,63 @@ class FusedGroupStep:
 
     MAXT = 8
 
-    def __init__(self, opts, transposes=None):
-        """``transposes``: optional per-optimiser lists of (W view, K, N, dst tensor, code) -- weight copies the update
-        writes as it goes (the MLP engine's fp32 fragment copies, ``optim.hip``: codes -3 / -4 forward operand F /
-        data-gradient operand G per element, -5 / -6 the same by 16 x 16 block items; a -6 row follows the -5 row of
-        its weight)."""
+    def __init__(self, opts, copies=None):
+        """``copies``: optional per-optimiser lists of (W view, K, N, F, G or None) -- the MLP engine's fp32 weight
+        fragment copies (``ops/mlp.py``), written by the update itself: such a segment runs on the ITEM path of
+        ``optim.hip`` (one workgroup per item of :meth:`item_table`)."""
         self.opts = list(opts)
         o0 = self.opts[0]
         self.adam = not isinstance(o0, FusedRMSprop)
         self._key = None
         self._words = self._fvals = None
         self._trans = None
-        own = [o.table_rows() for o in self.opts]
-        if transposes is not None or any(own):
-            t = torch.zeros(len(self.opts), self.MAXT, 5, dtype=torch.int64)
+        self._items = [None] * len(self.opts)
+        if copies is not None:
             for k, o in enumerate(self.opts):
-                rows = []
-                for W, K, N, dst, code in (transposes[k] if transposes is not None else []):
-                    off = (W.data_ptr() - o.p.data_ptr()) // 4
-                    assert 0 <= off and off + K * N <= o.p.numel() and code in (-3, -4, -5, -6)
-                    rows.append([off, K, N, code, dst.data_ptr()])
-                rows += own[k]
+                if copies[k]:
+                    self._items[k] = self.item_table(o, copies[k])
+        own = [o.table_rows() for o in self.opts]
+        if any(own):
+            t = torch.zeros(len(self.opts), self.MAXT, 5, dtype=torch.int64)
+            for k, rows in enumerate(own):
                 assert len(rows) <= self.MAXT
                 if rows:
                     t[k, :len(rows)] = torch.tensor(rows, dtype=torch.int64)
             self._trans = t
+
+    @staticmethod
+    def item_table(o, copies):
+        """Item records (``optim.hip`` opt_items, 8 int64 each) covering optimiser ``o``'s whole segment: every weight
+        with N % 64 == 0 as 16-row x 64-column blocks (type 1: the update plus whole 1 KB F / G fragment stores),
+        other copied weights whole (type 2, K * N <= 1024), the rest as element ranges of <= 1024 (type 0)."""
+        from .mlp import ngp2
+        n = o.p.numel()
+        recs, covered = [], []
+        for W, K, N, F, G in copies:
+            off = (W.data_ptr() - o.p.data_ptr()) // 4
+            assert 0 <= off and off + K * N <= n and W.numel() == K * N
+            assert F.numel() == ngp2(K) * ngp2(N) * 256 and (G is None or G.numel() == F.numel())
+            if N % 64 == 0:
+                assert off % 4 == 0 and F.data_ptr() % 16 == 0 and (G is None or G.data_ptr() % 16 == 0)
+                gk, gn = ngp2(K), ngp2(N)
+                for kt in range((K + 15) // 16):
+                    for cg in range(N // 64):
+                        fp = F.data_ptr() + 4 * ((4 * cg) * gk + kt) * 256
+                        gp = G.data_ptr() + 4 * (kt * gn + 4 * cg) * 256 if G is not None else 0
+                        recs.append([1, off + kt * 16 * N + cg * 64, min(16, K - kt * 16), N, fp, gp, gk * 256, 0])
+            else:
+                assert K * N <= 1024, "small copied weights are one workgroup item"
+                recs.append([2, off, K, N, F.data_ptr(), G.data_ptr() if G is not None else 0, 0, 0])
+            covered.append((off, off + K * N))
+        pos = 0
+        for a, b in sorted(covered) + [(n, n)]:
+            assert a >= pos or b <= pos, "overlapping copied weights"
+            while pos < a:
+                c = min(1024, a - pos)
+                recs.append([0, pos, c, 0, 0, 0, 0, 0])
+                pos += c
+            pos = max(pos, b)
+        return torch.tensor(recs, dtype=torch.int64, device=o.p.device)
 
     @staticmethod
     def compatible(opts):
@@ -313,10 +345,13 @@ class FusedGroupStep:
             for p, o in zip(parts, self.opts):
                 shadow = o.shadow.data_ptr() if o.shadow is not None else 0
                 adam = self.adam
+                items = self._items[len(words)]
                 words.append([o.p.data_ptr(), o.g.data_ptr(), o.m.data_ptr() if adam else 0, o.v.data_ptr(),
                               o.p.numel(), o.lr.data_ptr(), o.t.data_ptr() if adam else 0,
                               p.data_ptr() if p is not None else 0, o.gnorm.data_ptr(), shadow,
-                              o._ticket.data_ptr() if adam else 0])
+                              o._ticket.data_ptr() if adam else 0,
+                              items.data_ptr() if items is not None else 0,
+                              items.shape[0] if items is not None else 0])
                 fvals.append([float(o.clip_value) if o.clip_value is not None else -1.0,
                               float(o.max_grad_norm) if o.max_grad_norm is not None else -1.0,
                               float(o.grad_mul), float(o._norm_mul)])

@@ -30,6 +30,7 @@ hipError_t aca_mlp_wgrad(const aca::WgradArgs*, hipStream_t);
 hipError_t aca_ppo_head(const aca::PpoHeadArgs*, int, hipStream_t);
 int aca_ppo_head_planes(int);
 int aca_opt_set_unroll(int);
+void aca_opt_set_stamps(int64_t*);
 hipError_t aca_fc_bwd(const uint16_t*, const uint16_t*, const uint16_t*, uint16_t*, float*, int, float*, uint64_t*,
                       hipStream_t);
 hipError_t aca_fc_rollout(const uint16_t*, int64_t, int, const uint16_t*, int, int, float*, int64_t, int, int, int*,
@@ -1005,6 +1006,16 @@ void ppo_head(Tensor h, Tensor Wh, Tensor bh, Tensor act, Tensor logp_old, Tenso
 int64_t ppo_head_planes(int64_t B) { return aca_ppo_head_planes((int)B); }
 // float4 groups per thread of the single-segment optimiser launches (1, 2 or 4; A/B diagnostics); returns the value
 int64_t opt_set_unroll(int64_t u) { return aca_opt_set_unroll((int)u); }
+// diagnostics: optimiser launches write s_memtime phase stamps of every workgroup ([workgroup][8] int64) into buf
+// (None: off); see optim.hip opt_body
+void opt_set_stamps(c10::optional<Tensor> buf) {
+  int64_t* p = nullptr;
+  if (buf.has_value() && buf->defined()) {
+    need(*buf, at::kLong, "buf");
+    p = buf->data_ptr<int64_t>();
+  }
+  aca_opt_set_stamps(p);
+}
 
 void prp_perm(Tensor out, int64_t seed, Tensor uc, int64_t epoch) {
   need(out, at::kLong, "out");
@@ -1224,11 +1235,11 @@ void mlp_rollout(Tensor desc, int64_t lds, Tensor obs, Tensor act, Tensor logp, 
   check(aca_mlp_rollout(&a, (size_t)lds, cur_stream(obs)), "mlp_rollout");
 }
 
-// words: CPU int64 [nseg, 11], fvals: CPU float [nseg, 4] (built once by ops/optim.py FusedGroupStep)
+// words: CPU int64 [nseg, 13], fvals: CPU float [nseg, 4] (built once by ops/optim.py FusedGroupStep)
 void opt_multi(Tensor words, Tensor fvals, c10::optional<Tensor> trans, bool adam, double b1, double b2, double eps,
                bool zero_grad, Tensor stream_ref, int64_t t_off) {
   TORCH_CHECK(!words.is_cuda() && words.scalar_type() == at::kLong && words.is_contiguous() && words.dim() == 2 &&
-                  words.size(1) == 11, "opt_multi: words must be CPU int64 [nseg, 11]");
+                  words.size(1) == 13, "opt_multi: words must be CPU int64 [nseg, 13]");
   TORCH_CHECK(!fvals.is_cuda() && fvals.scalar_type() == at::kFloat && fvals.is_contiguous() &&
                   fvals.numel() == words.size(0) * 4, "opt_multi: fvals must be CPU float [nseg, 4]");
   const int64_t* tp = nullptr;
@@ -2076,6 +2087,7 @@ TORCH_LIBRARY(acamd, m) {
         "int hp_planes=0, Tensor? hbias=None) -> ()");
   m.def("ppo_head_planes(int B) -> int", &ppo_head_planes);
   m.def("opt_set_unroll(int u) -> int", &opt_set_unroll);
+  m.def("opt_set_stamps(Tensor? buf) -> ()", &opt_set_stamps);
   m.def("fc_rollout(Tensor X, Tensor Wf, Tensor hpart, int variant, Tensor? stamps=None) -> int");
   m.def("fc_bwd(Tensor dh, Tensor W, Tensor y3, Tensor dy3, Tensor dW, Tensor? stamps=None, Tensor? sq=None) -> ()");
   m.def("head_bwd(Tensor z, Tensor act, Tensor logp_old, Tensor ent_coef, Tensor kl_coef, float vf_coef, Tensor rew, "

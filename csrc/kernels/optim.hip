@@ -92,17 +92,7 @@ struct OptTrans {
   int K, N, ldt;
   float* dst;
 };
-// An MLP weight [K][N] with N % 64 == 0 updated by 16-row x 64-column wave items (whole 256-byte row runs) that also
-// write its fragment copies F / G (G may be absent: layer 0) as contiguous 1 KB wave stores, transposed through LDS --
-// instead of per-element scattered stores (table codes -5 / -6)
-constexpr int OPT_MAXBLK = 4;
-constexpr int BLK_LD = 68;   // row stride (floats) of the workgroup's 16 x 64 LDS tile
-struct OptBlk {
-  int64_t off;
-  int K, N, items;
-  float* F;
-  float* G;
-};
+constexpr int BLK_LD = 68;   // row stride (floats) of the workgroup's 16 x 64 LDS tile (item path)
 
 struct OptSeg {
   float* p; float* g; float* m; float* v; size_t n;
@@ -125,24 +115,24 @@ struct OptSeg {
   // optional device gate: the launch is skipped (no parameter, moment or step-count change) while *gate == 0 (lag-1
   // data parallelism before its first all-reduced gradient, trainer.py _update_body_lag1)
   const int* gate = nullptr;
-  int nblk = 0;
-  OptBlk blk[OPT_MAXBLK];
-  int dbg = 0;   // diagnostics (aca_opt_set_unroll(100 + mode)): 1 no G stores, 2 no F stores, 4 no LDS tile
+  // optional ITEM TABLE (device, OPT_ITEM_WORDS int64 per item, built by ops/optim.py FusedGroupStep): the segment is
+  // updated by one workgroup per item instead of the float4 sweep -- element ranges, 16-row x 64-column blocks of
+  // MLP weights that also write the weight's fp32 fragment copies F / G (common.h) as whole 1 KB wave stores, and
+  // small MLP weights whose copies are written per element. A workgroup reads its item with ONE scalar load; the
+  // copy tables of the sweep path (write_trans) are searched per element through kernel-argument reads, which cost
+  // more than the update itself at the MLP sizes (~4 us of a 9 us launch, profiles/r6_mlp_opt.txt).
+  const int64_t* items = nullptr;
+  int nitems = 0;
+  int64_t* stamps = nullptr;   // diagnostics: [global workgroup][8] s_memrealtime phase stamps (aca_opt_set_stamps)
+  int wg0 = 0;                 // global index of the segment's first workgroup (stamps row)
 };
+constexpr int OPT_ITEM_WORDS = 8;   // type, e0, n / rows / K, N, F, G, F column-tile stride, unused
 
-// element o (< K * N) of one copy entry; returns false for the MLP fragment codes (the search goes on)
+// element o (< K * N) of one copy entry
 __device__ __forceinline__ bool write_one(const OptTrans& T, uint32_t o, float v) {
   // 32-bit division (a 64-bit one is a ~100-instruction software sequence per element)
   const uint32_t n = (uint32_t)T.N;
   const uint32_t k = o / n, c = o - k * n;
-  if (T.ldt == -3) {
-    T.dst[mlp_frag_f(k, c, T.K)] = v;
-    return false;
-  }
-  if (T.ldt == -4) {
-    T.dst[mlp_frag_g(k, c, T.N)] = v;
-    return false;
-  }
   if (T.ldt < 0) {
     const uint32_t f = (((k >> 4) * (n >> 5) + (c >> 5)) * 64u + ((c >> 3) & 3u) * 16u + (k & 15u)) * 8u + (c & 7u);
     reinterpret_cast<u16*>(T.dst)[f] = f2bf(v);
@@ -152,8 +142,12 @@ __device__ __forceinline__ bool write_one(const OptTrans& T, uint32_t o, float v
   return true;
 }
 
+// (the entry loops below are unrolled over compile-time indices: a loop with the runtime bound S.ntrans reads the
+// kernel-argument table through a chain of dependent scalar loads, ~1.4 us per launch of the MLP optimiser)
 __device__ __forceinline__ void write_trans(const OptSeg& S, size_t i, float v) {
-  for (int e = 0; e < S.ntrans; ++e) {
+#pragma unroll
+  for (int e = 0; e < OPT_MAXT; ++e) {
+    if (e >= S.ntrans) break;
     const OptTrans& T = S.tr[e];
     const int64_t o = (int64_t)i - T.off;
     if (o >= 0 && o < (int64_t)T.K * T.N && write_one(T, (uint32_t)o, v)) return;
@@ -161,30 +155,18 @@ __device__ __forceinline__ void write_trans(const OptSeg& S, size_t i, float v) 
 }
 
 // The four consecutive elements 4 * i4 .. + 3 of a float4 group. Whole groups inside one row (offset and N multiples
-// of 4): a bf16 fragment copy (ldt -1) takes them as 4 consecutive u16 of one lane's 8 -> ONE 8-byte store, the MLP
-// G copy as 4 consecutive floats -> ONE 16-byte store (one 32-bit index computation each); others per element.
+// of 4): a bf16 fragment copy (ldt -1) takes them as 4 consecutive u16 of one lane's 8 -> ONE 8-byte store (one 32-bit
+// index computation); others per element.
 __device__ __forceinline__ void write_trans4(const OptSeg& S, size_t i4, float4 p4) {
   const size_t i = 4 * i4;
-  for (int e = 0; e < S.ntrans; ++e) {
+#pragma unroll
+  for (int e = 0; e < OPT_MAXT; ++e) {
+    if (e >= S.ntrans) break;
     const OptTrans& T = S.tr[e];
     const int64_t o = (int64_t)i - T.off;
     const int64_t KN = (int64_t)T.K * T.N;
     if (o + 3 < 0 || o >= KN) continue;
     const bool whole = o >= 0 && o + 3 < KN && ((o | T.N) & 3) == 0;
-    if (whole && T.ldt <= -3) {
-      const uint32_t ou = (uint32_t)o, n = (uint32_t)T.N;
-      const uint32_t k = ou / n, c = ou - k * n;
-      if (T.ldt == -4) {
-        *reinterpret_cast<float4*>(T.dst + mlp_frag_g(k, c, T.N)) = p4;
-      } else {
-        const uint32_t f = mlp_frag_f(k, c, T.K);   // c .. c + 3 share the tile (c % 4 == 0): lanes 4 floats apart
-        T.dst[f] = p4.x;
-        T.dst[f + 4] = p4.y;
-        T.dst[f + 8] = p4.z;
-        T.dst[f + 12] = p4.w;
-      }
-      continue;
-    }
     if (whole && T.ldt == -1) {
       const uint32_t ou = (uint32_t)o, n = (uint32_t)T.N;
       const uint32_t k = ou / n, c = ou - k * n;
@@ -202,12 +184,195 @@ __device__ __forceinline__ void write_trans4(const OptSeg& S, size_t i4, float4 
   }
 }
 
+// Adam step ticket (t_off < 0):
+__device__ __forceinline__ void opt_ticket(const OptSeg& S, int vblk, int vgrid, float t) {
+    // The last workgroup to finish publishes t + 1. Only a COUNT is needed (no data hand-off), so the ticket is a
+    // relaxed atomic with no release fence: a fenced last-arriver ticket (last_block_arrival) costs every workgroup
+    // an agent-scope release -- an L2 write-back on this multi-XCD part -- which was 60 us of a 70 us step over a
+    // 1.7M-parameter slab. The barrier orders this workgroup's reads of *S.t (every wave, at its start) before its
+    // ticket, so the final write cannot overtake a reader.
+    // The ticket is sharded by workgroup % 8 (each shard counter on its own 128-byte line): one counter took ~12 ns
+    // per arrival serialised in memory -- ~20 us over the 1650 workgroups of a 1.7M-parameter Adam step. A shard's
+    // last arriver (told by the returned count) resets its counter and adds to the top counter; the last shard
+    // publishes t + 1 and resets the top. Words: [x * OPT_TK_LINE] shards, [8 * OPT_TK_LINE] top.
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned int x = (unsigned int)vblk & 7u, G = (unsigned int)vgrid;
+      const unsigned int nsh = G < 8u ? G : 8u, nx = (G - x + 7u) / 8u;
+      const unsigned int prev =
+          __hip_atomic_fetch_add(S.ticket + x * OPT_TK_LINE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (prev == nx - 1u) {
+        __hip_atomic_store(S.ticket + x * OPT_TK_LINE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned int done =
+            __hip_atomic_fetch_add(S.ticket + 8 * OPT_TK_LINE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (done == nsh - 1u) {
+          *S.t = t;
+          __hip_atomic_store(S.ticket + 8 * OPT_TK_LINE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+}
+
+// ---- item path (OptSeg::items): one workgroup per item record of OPT_ITEM_WORDS int64:
+//   type 0: elements [e0, e0 + n) (n <= 4 * OPT_THREADS; thread t: e0 + t + OPT_THREADS j, coalesced)
+//   type 1: rows [0, w2) of the 16-row x 64-column block at element e0 of a [K][N] weight (N = w3, N % 64 == 0): wave
+//           w updates rows 4 w + (lane >> 4), columns 4 (lane & 15) .. + 3 (whole 256-byte row runs), the new values
+//           go through the workgroup's LDS tile, then wave w stores the 1 KB F block of column tile w (at
+//           F = w4 + w * w6 floats) and the 1 KB G block (at G = w5 + 256 w floats, w5 = 0: none)
+//   type 2: a whole small [K][N] weight at e0 (K = w2, N = w3, K * N <= 4 * OPT_THREADS), F / G written per element
+template <bool ADAM>
+__device__ __forceinline__ void opt_items(const OptSeg& S, float b1, float b2, float eps, int zero_grad, int vblk,
+                                          int vgrid, float* shr, float* blks) {
+  auto stamp = [&](int k) {
+    if (S.stamps && threadIdx.x == 0) S.stamps[(size_t)(S.wg0 + vblk) * 8 + k] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
+  float* __restrict__ p = S.p;
+  float* __restrict__ g = S.g;
+  float* __restrict__ m = S.m;
+  float* __restrict__ v = S.v;
+  const int64_t* rec = S.items + (size_t)vblk * OPT_ITEM_WORDS;
+  const int type = (int)rec[0];
+  const int64_t e0 = rec[1];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // ---- operands requested before the global-norm reduction
+  float4 x4[4][4];   // [array g, v, p, m][j]: type 0 / 2 element j (scalars in .x), type 1 the thread's float4 in [0]
+  const int n = (int)rec[2], N = (int)rec[3];
+  int cnt = 0;       // elements (types 0, 2) or float4 (type 1) this thread owns
+  auto elem = [&](int j) -> int64_t { return e0 + tid + (int64_t)OPT_THREADS * j; };
+  if (type == 1) {
+    const int r = 4 * w + (lane >> 4);
+    if (r < n) {
+      cnt = 1;
+      const size_t i = (size_t)(e0 + (int64_t)r * N + 4 * (lane & 15)) / 4;
+      x4[0][0] = reinterpret_cast<const float4*>(g)[i];
+      x4[1][0] = reinterpret_cast<const float4*>(v)[i];
+      x4[2][0] = reinterpret_cast<const float4*>(p)[i];
+      x4[3][0] = ADAM ? reinterpret_cast<const float4*>(m)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  } else {
+    const int tot = type == 0 ? n : n * N;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (tid + OPT_THREADS * j < tot) {
+        cnt = j + 1;
+        const int64_t i = elem(j);
+        x4[0][j].x = g[i];
+        x4[1][j].x = v[i];
+        x4[2][j].x = p[i];
+        x4[3][j].x = ADAM ? m[i] : 0.f;
+      }
+    }
+  }
+  stamp(1);
+  const float lr = *S.lr;
+  const float t = ADAM ? (*S.t + 1.0f + (S.t_off > 0 ? (float)S.t_off : 0.f)) : 0.f;
+  float scale = 1.f;
+  if (S.parts) {
+    const float gsq = partial_total(S.parts, shr) * S.norm_mul;
+    scale = grad_scale(gsq, S.max_norm);
+    if (S.gnorm_out && vblk == 0 && tid == 0) *S.gnorm_out = gsq;
+  }
+  stamp(2);
+  const float clip = S.clip, gmul = S.gmul;
+  float lr_t = lr;
+  if (ADAM) lr_t = lr * sqrtf(1.0f - powf(b2, t)) / (1.0f - powf(b1, t));
+  // (the update arithmetic of opt_body, term for term: the two paths give bit-identical parameters)
+  auto upd = [&](float gi, float& vi, float& mi, float& pi) {
+    gi *= gmul;
+    if (clip > 0.f) gi = fminf(fmaxf(gi, -clip), clip);
+    gi *= scale;
+    vi = __builtin_fmaf(1.0f - b2, gi * gi, b2 * vi);
+    if (ADAM) {
+      mi = __builtin_fmaf(1.0f - b1, gi, b1 * mi);
+      pi = __builtin_fmaf(-lr_t, mi / (sqrtf(vi) + eps), pi);
+    } else {
+      pi = __builtin_fmaf(-lr, gi / sqrtf(vi + eps), pi);
+    }
+  };
+  u16* shadow = S.shadow;
+  if (type == 1) {
+    float4 w4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int r = 4 * w + (lane >> 4);
+    if (cnt) {
+      float4 &g4 = x4[0][0], &v4 = x4[1][0], &p4 = x4[2][0], &m4 = x4[3][0];
+      const size_t i = (size_t)(e0 + (int64_t)r * N + 4 * (lane & 15)) / 4;
+      if (zero_grad) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      upd(g4.x, v4.x, m4.x, p4.x);
+      upd(g4.y, v4.y, m4.y, p4.y);
+      upd(g4.z, v4.z, m4.z, p4.z);
+      upd(g4.w, v4.w, m4.w, p4.w);
+      reinterpret_cast<float4*>(v)[i] = v4;
+      if (ADAM) reinterpret_cast<float4*>(m)[i] = m4;
+      reinterpret_cast<float4*>(p)[i] = p4;
+      if (shadow) {
+        uint2 sv;
+        sv.x = (uint32_t)f2bf(p4.x) | ((uint32_t)f2bf(p4.y) << 16);
+        sv.y = (uint32_t)f2bf(p4.z) | ((uint32_t)f2bf(p4.w) << 16);
+        reinterpret_cast<uint2*>(shadow)[i] = sv;
+      }
+      w4 = p4;
+    }
+    // (rows past K are zero: the fragment pads)
+    *reinterpret_cast<float4*>(blks + r * BLK_LD + 4 * (lane & 15)) = w4;
+    __syncthreads();
+    const int rr = lane & 15, q = lane >> 4;
+    float* G = reinterpret_cast<float*>(rec[5]);
+    // G block of column tile w, lane (q, rr): W[rr][16 w + 4 q .. + 3]
+    if (G)
+      *reinterpret_cast<float4*>(G + 256 * w + 4 * lane) =
+          *reinterpret_cast<const float4*>(blks + rr * BLK_LD + 16 * w + 4 * q);
+    // F block of column tile w, lane (q, rr): W[4 q + s][16 w + rr], s = 0..3
+    float4 f4;
+    f4.x = blks[(4 * q + 0) * BLK_LD + 16 * w + rr];
+    f4.y = blks[(4 * q + 1) * BLK_LD + 16 * w + rr];
+    f4.z = blks[(4 * q + 2) * BLK_LD + 16 * w + rr];
+    f4.w = blks[(4 * q + 3) * BLK_LD + 16 * w + rr];
+    *reinterpret_cast<float4*>(reinterpret_cast<float*>(rec[4]) + rec[6] * w + 4 * lane) = f4;
+  } else {
+    float* F = reinterpret_cast<float*>(rec[4]);
+    float* G = reinterpret_cast<float*>(rec[5]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (j < cnt) {
+        const int64_t i = elem(j);
+        float &gi = x4[0][j].x, &vi = x4[1][j].x, &pi = x4[2][j].x, &mi = x4[3][j].x;
+        if (zero_grad) g[i] = 0.f;
+        upd(gi, vi, mi, pi);
+        v[i] = vi;
+        if (ADAM) m[i] = mi;
+        p[i] = pi;
+        if (shadow) shadow[i] = f2bf(pi);
+        if (type == 2) {
+          const uint32_t o = (uint32_t)(tid + OPT_THREADS * j), k = o / (uint32_t)N, c = o - k * (uint32_t)N;
+          F[mlp_frag_f(k, c, n)] = pi;
+          if (G) G[mlp_frag_g(k, c, N)] = pi;
+        }
+      }
+    }
+  }
+  stamp(4);
+  if (S.stamps) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp(5);
+  }
+  if (ADAM && S.t_off < 0) opt_ticket(S, vblk, vgrid, t);
+}
+
 // U float4 groups per thread per round; the first round's operands are requested BEFORE the global-norm reduction
 // (its partial loads + block sum would otherwise be a dependent round trip ahead of every element load).
 template <bool ADAM, int U>
 __device__ __forceinline__ void opt_body(const OptSeg& S, float b1, float b2, float eps, int zero_grad, int vblk,
                                          int vgrid, int* flag, float* shr, u16* kcs, float* blks) {
   if (S.gate && *S.gate == 0) return;   // uniform over the launch
+  if (S.items) {
+    opt_items<ADAM>(S, b1, b2, eps, zero_grad, vblk, vgrid, shr, blks);
+    return;
+  }
+  auto stamp = [&](int k) {
+    if (S.stamps && threadIdx.x == 0) S.stamps[(size_t)(S.wg0 + vblk) * 8 + k] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
   float* __restrict__ p = S.p;
   float* __restrict__ g = S.g;
   float* __restrict__ m = S.m;
@@ -219,15 +384,7 @@ __device__ __forceinline__ void opt_body(const OptSeg& S, float b1, float b2, fl
   const size_t stride = (size_t)vgrid * blockDim.x * U;
   // the k-contiguous fragment region [kc0, kc1) in float4 groups is left to the wave-item loop below
   const size_t kc0 = S.kc_K ? (size_t)S.kc_off / 4 : 0, kc1 = S.kc_K ? kc0 + (size_t)S.kc_K * S.kc_N / 4 : 0;
-  // ... and so are the MLP weight blocks (their 16 x 16 wave items below)
-  auto in_kc = [&](size_t i) {
-    bool r = i >= kc0 && i < kc1;
-    for (int e = 0; e < S.nblk; ++e) {
-      const size_t b0 = (size_t)S.blk[e].off / 4;
-      r |= i >= b0 && i < b0 + (size_t)S.blk[e].K * S.blk[e].N / 4;
-    }
-    return r;
-  };
+  auto in_kc = [&](size_t i) { return i >= kc0 && i < kc1; };
   float4 g4[U], v4[U], p4[U], m4[U];
   auto load = [&](size_t i0) {
 #pragma unroll
@@ -262,43 +419,14 @@ __device__ __forceinline__ void opt_body(const OptSeg& S, float b1, float b2, fl
     km = ADAM ? reinterpret_cast<const float4*>(m)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
   };
   if (gw0 < kItems) kc_load(gw0);
-  // MLP weight blocks: WORKGROUP items (matrix e, 16-row tile kt, 64-column group cg), taken by workgroup vblk,
-  // vblk + vgrid, ...; wave w, lane -> row kt * 16 + 4 w + (lane >> 4), columns cg * 64 + 4 (lane & 15) .. + 3 (whole
-  // 256-byte row runs, one float4 per thread like the element path)
-  int bItems = 0;
-  for (int e = 0; e < S.nblk; ++e) bItems += S.blk[e].items;
-  auto blk_at = [&](int it, int& e, int& kt, int& cg) {
-    e = 0;
-    while (e + 1 < S.nblk && it >= S.blk[e].items) it -= S.blk[e++].items;
-    const int ncg = S.blk[e].N >> 6;
-    kt = it / ncg;
-    cg = it - kt * ncg;
-  };
-  float4 bg, bv, bp, bm;
-  auto blk_row = [&](const OptBlk& Bk, int kt, int cg, bool& ok) {
-    const int k = kt * 16 + 4 * (threadIdx.x >> 6) + (lane >> 4);
-    ok = k < Bk.K;
-    return ((size_t)Bk.off + (size_t)k * Bk.N + cg * 64 + 4 * (lane & 15)) / 4;
-  };
-  auto blk_load = [&](int it) {
-    int e, kt, cg;
-    blk_at(it, e, kt, cg);
-    bool ok;
-    const size_t i = blk_row(S.blk[e], kt, cg, ok);
-    if (ok) {
-      bg = reinterpret_cast<const float4*>(g)[i];
-      bv = reinterpret_cast<const float4*>(v)[i];
-      bp = reinterpret_cast<const float4*>(p)[i];
-      bm = ADAM ? reinterpret_cast<const float4*>(m)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  };
-  if (vblk < bItems) blk_load(vblk);
+  stamp(1);
   float scale = 1.f;
   if (S.parts) {
     const float gsq = partial_total(S.parts, shr) * S.norm_mul;
     scale = grad_scale(gsq, S.max_norm);
     if (S.gnorm_out && vblk == 0 && threadIdx.x == 0) *S.gnorm_out = gsq;
   }
+  stamp(2);
   const float clip = S.clip, gmul = S.gmul;
   float lr_t = lr;
   if (ADAM) lr_t = lr * sqrtf(1.0f - powf(b2, t)) / (1.0f - powf(b1, t));
@@ -342,6 +470,7 @@ __device__ __forceinline__ void opt_body(const OptSeg& S, float b1, float b2, fl
     }
     if (i0 + stride < n4) load(i0 + stride);
   }
+  stamp(3);
   // fragment region: the same update per element, then the bf16 copy transposed through a 512-byte per-wave LDS
   // scratch laid out exactly as the destination run ([32 columns][8 k]) -> one contiguous 512-byte wave store
   for (int it = gw0; it < kItems; it += GW) {
@@ -376,56 +505,7 @@ __device__ __forceinline__ void opt_body(const OptSeg& S, float b1, float b2, fl
     __builtin_amdgcn_wave_barrier();   // the scratch is rewritten by the next item
     if (it + GW < kItems) kc_load(it + GW);
   }
-  // MLP weight blocks: the update (whole row runs), the new values into the workgroup's LDS tile T[16][64] (row stride
-  // BLK_LD), then wave w writes the G and F fragment blocks of column tile cg * 4 + w as whole 1 KB wave stores
-  // (OPT_THREADS = 4 waves = the 4 column tiles of the item)
-  for (int it = vblk; it < bItems; it += vgrid) {
-    int e, kt, cg;
-    blk_at(it, e, kt, cg);
-    const OptBlk& Bk = S.blk[e];
-    const int w = threadIdx.x >> 6;
-    bool ok;
-    const size_t i = blk_row(Bk, kt, cg, ok);
-    float4 w4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (ok) {
-      if (zero_grad) reinterpret_cast<float4*>(g)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-      upd(bg.x, bv.x, bm.x, bp.x);
-      upd(bg.y, bv.y, bm.y, bp.y);
-      upd(bg.z, bv.z, bm.z, bp.z);
-      upd(bg.w, bv.w, bm.w, bp.w);
-      reinterpret_cast<float4*>(v)[i] = bv;
-      if (ADAM) reinterpret_cast<float4*>(m)[i] = bm;
-      reinterpret_cast<float4*>(p)[i] = bp;
-      if (shadow) {
-        uint2 sv;
-        sv.x = (uint32_t)f2bf(bp.x) | ((uint32_t)f2bf(bp.y) << 16);
-        sv.y = (uint32_t)f2bf(bp.z) | ((uint32_t)f2bf(bp.w) << 16);
-        reinterpret_cast<uint2*>(shadow)[i] = sv;
-      }
-      w4 = bp;
-    }
-    if (S.dbg & 4) {
-      if (it + vgrid < bItems) blk_load(it + vgrid);
-      continue;
-    }
-    // (rows past K are zero: the fragment pads)
-    *reinterpret_cast<float4*>(blks + (4 * w + (lane >> 4)) * BLK_LD + 4 * (lane & 15)) = w4;
-    __syncthreads();
-    const int r = lane & 15, q = lane >> 4, ct = cg * 4 + w;
-    // G block (kt, ct), lane (q, r): W[kt * 16 + r][ct * 16 + 4 q .. + 3]
-    if (Bk.G && !(S.dbg & 1))
-      *reinterpret_cast<float4*>(Bk.G + ((size_t)(kt * mlp_ngp2(Bk.N) + ct) * 64 + lane) * 4) =
-          *reinterpret_cast<const float4*>(blks + r * BLK_LD + 16 * w + 4 * q);
-    // F block (ct, kt), lane (q, r): W[kt * 16 + 4 q + s][ct * 16 + r], s = 0..3
-    float4 f4;
-    f4.x = blks[(4 * q + 0) * BLK_LD + 16 * w + r];
-    f4.y = blks[(4 * q + 1) * BLK_LD + 16 * w + r];
-    f4.z = blks[(4 * q + 2) * BLK_LD + 16 * w + r];
-    f4.w = blks[(4 * q + 3) * BLK_LD + 16 * w + r];
-    if (!(S.dbg & 2)) *reinterpret_cast<float4*>(Bk.F + ((size_t)(ct * mlp_ngp2(Bk.K) + kt) * 64 + lane) * 4) = f4;
-    __syncthreads();   // the tile is rewritten by the next item
-    if (it + vgrid < bItems) blk_load(it + vgrid);
-  }
+  stamp(4);
   if (vblk == 0) {   // scalar tail
     for (size_t i = n4 * 4 + threadIdx.x; i < n; i += blockDim.x) {
       float gi = g[i], vi = v[i], pi = p[i], mi = ADAM ? m[i] : 0.f;
@@ -438,33 +518,11 @@ __device__ __forceinline__ void opt_body(const OptSeg& S, float b1, float b2, fl
       if (S.ntrans) write_trans(S, i, pi);
     }
   }
-  if (ADAM && S.t_off < 0) {
-    // The last workgroup to finish publishes t + 1. Only a COUNT is needed (no data hand-off), so the ticket is a
-    // relaxed atomic with no release fence: a fenced last-arriver ticket (last_block_arrival) costs every workgroup
-    // an agent-scope release -- an L2 write-back on this multi-XCD part -- which was 60 us of a 70 us step over a
-    // 1.7M-parameter slab. The barrier orders this workgroup's reads of *S.t (every wave, at its start) before its
-    // ticket, so the final write cannot overtake a reader.
-    // The ticket is sharded by workgroup % 8 (each shard counter on its own 128-byte line): one counter took ~12 ns
-    // per arrival serialised in memory -- ~20 us over the 1650 workgroups of a 1.7M-parameter Adam step. A shard's
-    // last arriver (told by the returned count) resets its counter and adds to the top counter; the last shard
-    // publishes t + 1 and resets the top. Words: [x * OPT_TK_LINE] shards, [8 * OPT_TK_LINE] top.
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const unsigned int x = (unsigned int)vblk & 7u, G = (unsigned int)vgrid;
-      const unsigned int nsh = G < 8u ? G : 8u, nx = (G - x + 7u) / 8u;
-      const unsigned int prev =
-          __hip_atomic_fetch_add(S.ticket + x * OPT_TK_LINE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (prev == nx - 1u) {
-        __hip_atomic_store(S.ticket + x * OPT_TK_LINE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned int done =
-            __hip_atomic_fetch_add(S.ticket + 8 * OPT_TK_LINE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (done == nsh - 1u) {
-          *S.t = t;
-          __hip_atomic_store(S.ticket + 8 * OPT_TK_LINE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-    }
+  if (S.stamps) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    stamp(5);
   }
+  if (ADAM && S.t_off < 0) opt_ticket(S, vblk, vgrid, t);
 }
 
 template <bool ADAM, int U>
@@ -808,15 +866,12 @@ static int opt_grid(size_t n, int unroll = 1) {   // `unroll` float4 groups per 
 
 // float4 groups per thread of the single-segment optimiser launches (a diagnostic knob, aca_opt_set_unroll)
 static int g_opt_unroll = 1;
-static int g_opt_dbg = 0;
+static int64_t* g_opt_stamps = nullptr;
 
 template <bool ADAM>
 static void launch_opt(OptSeg& S, float b1, float b2, float eps, int zero_grad, hipStream_t stream) {
   const int U = g_opt_unroll;
   S.nblocks = opt_grid(S.n, U);
-  int bi = 0;   // one workgroup per MLP block item (see aca_opt_multi)
-  for (int e = 0; e < S.nblk; ++e) bi += S.blk[e].items;
-  if (bi > S.nblocks) S.nblocks = bi;
   switch (U) {
     case 2: opt_kernel<ADAM, 2><<<S.nblocks, OPT_THREADS, 0, stream>>>(S, b1, b2, eps, zero_grad); break;
     case 4: opt_kernel<ADAM, 4><<<S.nblocks, OPT_THREADS, 0, stream>>>(S, b1, b2, eps, zero_grad); break;
@@ -872,43 +927,24 @@ extern "C" hipError_t aca_grad_finalize(const int64_t* jobs, int njobs, float* p
 
 // trans: host table [OPT_MAXT][5] = (offset, K, N, ldt, dst) of one segment; K == 0 ends the list. ldt -1: the
 // conv kernels' fragment order (write_trans); ldt -2: the k-contiguous fragment region (at most one; opt_body);
-// ldt -3 / -4: the MLP engine's F / G fragment copies, per element; ldt -5 (+ an optional -6 row of the same weight):
-// the F (G) copy of an N % 16 == 0 weight by 16 x 16 block items (OptBlk); ldt -9 (K = N = 1, at most one): dst is the
-// launch's gate (const int*, OptSeg::gate).
+// ldt -9 (K = N = 1, at most one): dst is the launch's gate (const int*, OptSeg::gate). (The MLP engine's fragment
+// copies go through the item table, OptSeg::items.)
 static bool opt_load_trans(OptSeg& S, const int64_t* tw0) {
   S.ntrans = 0;
   S.kc_K = 0;
   S.gate = nullptr;
   if (!tw0) return true;
-  S.nblk = 0;
   for (int e = 0; e < OPT_MAXT; ++e) {
     const int64_t* tw = tw0 + (int64_t)e * 5;
     if (tw[1] <= 0) break;
     const int64_t ldt = tw[3];
-    if (ldt == -5) {   // an MLP weight block matrix: F (a -6 row of the same weight may follow with G)
-      if (S.nblk >= OPT_MAXBLK || tw[2] % 64 || tw[0] % 4 || tw[0] < 0 || (size_t)(tw[0] + tw[1] * tw[2]) > S.n ||
-          !tw[4] || tw[4] % 16 || tw[1] > 4096 || tw[2] > 4096)
-        return false;
-      OptBlk& B = S.blk[S.nblk++];
-      B = OptBlk{tw[0], (int)tw[1], (int)tw[2], (int)(((tw[1] + 15) / 16) * (tw[2] / 64)),
-                 reinterpret_cast<float*>(tw[4]), nullptr};
-      continue;
-    }
-    if (ldt == -6) {
-      if (!S.nblk || S.blk[S.nblk - 1].off != tw[0] || S.blk[S.nblk - 1].K != tw[1] || S.blk[S.nblk - 1].N != tw[2] ||
-          S.blk[S.nblk - 1].G || !tw[4] || tw[4] % 16)
-        return false;
-      S.blk[S.nblk - 1].G = reinterpret_cast<float*>(tw[4]);
-      continue;
-    }
     if (ldt == -9) {
       if (S.gate || !tw[4] || tw[4] % 4) return false;
       S.gate = reinterpret_cast<const int*>(tw[4]);
       continue;
     }
     if ((ldt == -1 || ldt == -2) && (tw[1] % 16 || tw[2] % 32)) return false;   // 16-row tiles, 32-wide k-steps
-    if (ldt < -4 || ldt == 0 || tw[0] < 0 || (size_t)(tw[0] + tw[1] * tw[2]) > S.n || tw[2] <= 0) return false;
-    if (ldt <= -3 && (tw[4] % 16 || tw[1] * tw[2] > (int64_t)1 << 31)) return false;
+    if (ldt < -2 || ldt == 0 || tw[0] < 0 || (size_t)(tw[0] + tw[1] * tw[2]) > S.n || tw[2] <= 0) return false;
     if (ldt == -2) {
       if (S.kc_K || tw[0] % 4 || tw[4] % 16) return false;
       S.kc_off = tw[0];
@@ -954,8 +990,10 @@ extern "C" hipError_t aca_rmsprop_step(float* p, float* g, float* v, size_t n, c
   return hipGetLastError();
 }
 
-// Multi-group step. segs: nseg records of 16 words (see ops/optim.py FusedGroupStep): p, g, m, v, n, lr, t, parts,
-// gnorm_out, shadow, ticket (pointers / sizes as 64-bit words) and clip, max_norm, gmul, norm_mul (floats).
+// Multi-group step. words: nseg records of OPT_MULTI_WORDS (see ops/optim.py FusedGroupStep): p, g, m, v, n, lr, t,
+// parts, gnorm_out, shadow, ticket, items, nitems (pointers / sizes as 64-bit words); fvals: clip, max_norm, gmul,
+// norm_mul (floats). The item tables (OptSeg::items) are the caller's, validated where they are built.
+constexpr int OPT_MULTI_WORDS = 13;
 extern "C" hipError_t aca_opt_multi(const int64_t* words, const float* fvals, const int64_t* trans, int nseg,
                                     int adam, float b1, float b2, float eps, int zero_grad, int t_off,
                                     hipStream_t stream) {
@@ -964,7 +1002,7 @@ extern "C" hipError_t aca_opt_multi(const int64_t* words, const float* fvals, co
   M.nseg = nseg;
   int total = 0;
   for (int k = 0; k < nseg; ++k) {
-    const int64_t* w = words + 11 * k;
+    const int64_t* w = words + OPT_MULTI_WORDS * k;
     const float* f = fvals + 4 * k;
     OptSeg& S = M.seg[k];
     S.p = reinterpret_cast<float*>(w[0]);
@@ -983,15 +1021,16 @@ extern "C" hipError_t aca_opt_multi(const int64_t* words, const float* fvals, co
     S.gmul = f[2];
     S.norm_mul = f[3];
     S.t_off = t_off < 0 ? -1 : t_off;
-    S.dbg = g_opt_dbg;
+    S.stamps = g_opt_stamps;
+    S.items = reinterpret_cast<const int64_t*>(w[11]);
+    S.nitems = (int)w[12];
+    if ((S.items != nullptr) != (S.nitems > 0) || S.nitems > 4096) return hipErrorInvalidValue;
     if (S.n == 0 || !opt_aligned(S.p, S.g, adam ? S.m : S.v, S.v, S.shadow)) return hipErrorInvalidValue;
     if (adam && (!S.m || !S.t || !S.ticket)) return hipErrorInvalidValue;
     // trans: [nseg][OPT_MAXT][5]
     if (!opt_load_trans(S, trans ? trans + (int64_t)k * OPT_MAXT * 5 : nullptr)) return hipErrorInvalidValue;
-    S.nblocks = opt_grid(S.n);
-    int bi = 0;   // one workgroup per MLP block item: a second round would be a dependent memory round trip
-    for (int e = 0; e < S.nblk; ++e) bi += S.blk[e].items;
-    if (bi > S.nblocks) S.nblocks = bi;
+    S.nblocks = S.items ? S.nitems : opt_grid(S.n);   // item path: one workgroup per item
+    S.wg0 = total;
     total += S.nblocks;
   }
   if (adam) opt_multi_kernel<true><<<total, OPT_THREADS, 0, stream>>>(M, b1, b2, eps, zero_grad);
@@ -999,9 +1038,10 @@ extern "C" hipError_t aca_opt_multi(const int64_t* words, const float* fvals, co
   return hipGetLastError();
 }
 
+extern "C" void aca_opt_set_stamps(int64_t* p) { g_opt_stamps = p; }
+
 extern "C" int aca_opt_set_unroll(int u) {
   if (u == 1 || u == 2 || u == 4) g_opt_unroll = u;
-  if (u >= 100 && u < 108) g_opt_dbg = u - 100;
   return g_opt_unroll;
 }
 

@@ -76,15 +76,12 @@ def main():
     out["opt"] = graph_us(opt)
     tr._t_off = 0
     out["step"] = graph_us(step)
-    from actor_critic_algs_on_tensorflow_amd import _native
-    for mode in (1, 2, 3, 4, 7):
-        _native.require().opt_set_unroll(100 + mode)
-        out[f"opt_dbg{mode}"] = graph_us(opt)
-    _native.require().opt_set_unroll(100)
-    trans = gs._trans
-    gs._trans = None
+    items = gs._items
+    gs._items = [None, None]
+    gs._key = None
     out["opt_no_frag_copies"] = graph_us(opt)
-    gs._trans = trans
+    gs._items = items
+    gs._key = None
     parts = [tr.opts[g].ext_parts for g in ("actor", "critic")]
     for g in ("actor", "critic"):
         tr.opts[g].ext_parts = None

@@ -151,3 +151,60 @@ def test_cnn_checkpoint_roundtrip(tmp_path):
     ckpt.load_model(ag2.model, codec.read(p))
     for a, b in zip(ag.model.parameters(), ag2.model.parameters()):
         assert torch.equal(a, b)
+
+
+def test_optimizer_state_saved_per_parameter_name(tmp_path):
+    """Adam m / v are stored per parameter name (whole-slab vectors depend on the slab's parameter order and
+    padding): a trainer whose slab lays the parameters out differently restores every parameter's moments; a legacy
+    whole-vector entry of the wrong size is refused instead of loading permuted state."""
+    from actor_critic_algs_on_tensorflow_amd import preset
+    from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
+    cfg = preset("cartpole_cpu", num_envs=4, outdir=None, quiet=True, stdout_freq=0, save_every=0,
+                 checkpoint_dir=str(tmp_path))
+    tr = ActorCriticTrainer(cfg)
+    for _ in range(3):
+        tr.step()
+    p1 = tr.save_checkpoint()
+    names = list(codec.read(p1).keys())
+    assert any(n.startswith("_acamd/opt/actor/m/") for n in names)
+    assert not any(n in ("_acamd/opt/actor/m", "_acamd/opt/actor/v") for n in names)
+
+    def moments(t):
+        out = {}
+        for g, opt in t.opts.items():
+            for name, a, b in ckpt._param_ranges(t, opt):
+                out[(g, name)] = (opt.m[a:b].clone(), opt.v[a:b].clone())
+        return out
+
+    ref = moments(tr)
+    tr2 = ActorCriticTrainer(cfg)
+    for opt in tr2.opts.values():
+        opt.m.zero_()
+        opt.v.zero_()
+    old_offsets = list(tr2.flat.offsets)
+    try:
+        # another slab layout: two equal-size actor parameters trade places
+        sizes = {}
+        g0 = tr2.opts["actor"]
+        for i, (p, o) in enumerate(zip(tr2.flat.params, old_offsets)):
+            if g0.start <= o < g0.end:
+                sizes.setdefault(p.numel(), []).append(i)
+        i, j = next(v for v in sizes.values() if len(v) >= 2)[:2]
+        offs = list(old_offsets)
+        offs[i], offs[j] = offs[j], offs[i]
+        tr2.flat.offsets = offs
+        tr2.load_checkpoint(p1)
+        for key, (m, v) in moments(tr2).items():
+            assert torch.equal(m, ref[key][0]) and torch.equal(v, ref[key][1]), key
+    finally:
+        tr2.flat.offsets = old_offsets
+    # legacy whole-slab entry of another size: refused
+    t = dict(codec.read(p1))
+    for k in [k for k in t if k.startswith("_acamd/opt/actor/m/") or k.startswith("_acamd/opt/actor/v/")]:
+        del t[k]
+    t["_acamd/opt/actor/m"] = np.zeros(tr.opts["actor"].m.numel() + 8, np.float32)
+    p2 = str(tmp_path / "legacy")
+    codec.write(p2, t)
+    import pytest
+    with pytest.raises(ValueError, match="another parameter layout"):
+        ActorCriticTrainer(cfg).load_checkpoint(p2)

@@ -227,7 +227,7 @@ def test_optimizer_writes_fragment_copies(cuda):
     for _ in range(2):
         tr.step()
     torch.cuda.synchronize()
-    assert tr._group_step is not None and tr._group_step._trans is not None
+    assert tr._group_step is not None and tr._group_step._items[0] is not None
 
     def check():
         for tw in tr.mlp.towers:

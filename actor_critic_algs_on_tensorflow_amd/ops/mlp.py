@@ -48,6 +48,11 @@ def _ld(w):
     return 16 * ngp2(w) + 4
 
 
+def _nct(w):
+    """16-wide column tiles of a width (the training workspace's blocks per row tile)."""
+    return (w + 15) // 16
+
+
 def frag_f(W):
     """Forward fragment copy of a [K][N] weight (common.h mlp_frag_f): [ngp2(N) tiles][ngp2(K) groups][64 lanes][4],
     zero pad -- the layout the optimiser step and ``mlp_tshadow`` write."""
@@ -111,6 +116,7 @@ class MLPEngine:
                       for tw in self.towers]
         self._descs = {}
         self._hdescs = {}
+        self._witems = {}
         self._mparts = {}
         self._dummy_stats = torch.zeros(16, dtype=torch.float32, device=self.dev)
         # fp32 FRAGMENT copies of every weight (common.h mlp_frag_f / mlp_frag_g, zero pad): F, the forward's B
@@ -161,11 +167,10 @@ class MLPEngine:
                 if id(lay) in self.G:
                     words[base + 2 + 10 * MAXL + l] = self.G[id(lay)].data_ptr()
                 if B is not None:
-                    # rows padded to a multiple of 128 and never written: the weight-gradient kernel reads whole
-                    # 128-row chunks unguarded
-                    Bp = (B + 127) // 128 * 128
-                    xs = torch.zeros(Bp, lay.in_features, dtype=torch.float32, device=self.dev)
-                    dp = torch.zeros(Bp, lay.out_features, dtype=torch.float32, device=self.dev)
+                    # 16 x 16 blocks, column-major inside (mlp.hip blk_out), one row of blocks per 16-row tile
+                    nrt = (B + BM - 1) // BM
+                    xs = torch.zeros(nrt * _nct(lay.in_features) * 256, dtype=torch.float32, device=self.dev)
+                    dp = torch.zeros(nrt * _nct(lay.out_features) * 256, dtype=torch.float32, device=self.dev)
                     ws += [xs, dp]
                     words[base + 2 + 7 * MAXL + l] = xs.data_ptr()
                     words[base + 2 + 8 * MAXL + l] = dp.data_ptr()
@@ -234,16 +239,54 @@ class MLPEngine:
         self._fwd(2, obs, B, 0, 2, desc_B=B, idx=idx, perm=perm, act_in=actions, logp_old=logp_old, adv=adv, ret=ret,
                   v_old=v_old, ent_coef=ent_coef, kl_coef=kl_coef, vf_coef=vf_coef, ppo_clip=ppo_clip,
                   v_clip=v_clip, ppo=ppo, stamps=stamps)
-        desc, _ = self.desc(B)
-        nsplit = max(1, min(16, B // 2048))
+        nrt = (B + BM - 1) // BM
+        nsplit = max(1, min(16, nrt // 128))
         self.last_stores_all = nsplit == 1   # every gradient element stored (no atomics): no zeroing needed after use
         use_parts = want_parts and nsplit == 1
         st = stats if stats is not None else self._dummy_stats
-        ops.mlp_wgrad(desc, 2, B, nsplit, self.items[0], self.items[1], self.parts[0] if use_parts else None,
-                      self.parts[1] if use_parts else None, float(clips[0] or -1.0), float(clips[1] or -1.0),
-                      self.g_log_std, self.A, self.mstats, st, ent_coef, kl_coef, self._mpart(B), (B + BM - 1) // BM,
-                      bump)
+        items = self.wgrad_items(B, use_parts, clips)
+        ls_part = self.parts[0][self.items[0]:self.items[0] + 1] if (use_parts and self.g_log_std is not None) else None
+        ops.mlp_wgrad(items, nrt, nsplit, self.g_log_std, self.A, ls_part, float(clips[0] or -1.0), st, ent_coef,
+                      kl_coef, self._mpart(B), nrt, bump)
         return use_parts
+
+    def wgrad_items(self, B, parts=True, clips=(None, None)):
+        """Item table of the weight-gradient launch (``mlp.hip`` mlp_wgrad_kernel, 8 int64 per 16 x 16 tile of every
+        dW_l): operand block bases and strides, the gradient tile, its bias (first row of tiles), its sum-of-squares
+        slot in :attr:`parts` and the clip applied before squaring; item 0 of a tower zeroes the tower's unused
+        slots."""
+        key = (B, bool(parts), clips)
+        if key in self._witems:
+            return self._witems[key]
+        _, ws = self.desc(B)
+        import struct
+        recs = []
+        wi = 0
+        for t, tw in enumerate(self.towers):
+            clip = float(clips[t] or -1.0)
+            cbits = struct.unpack("<i", struct.pack("<f", clip))[0] & 0xFFFFFFFF
+            local = 0
+            first_unused = self.items[t] + (1 if t == 0 and self.g_log_std is not None else 0)
+            for lay in tw:
+                xs, dp = ws[wi], ws[wi + 1]
+                wi += 2
+                K, N = lay.in_features, lay.out_features
+                gW = self._views(lay.kernel)[1]
+                gb = self._views(lay.bias)[1]
+                sx, sp = _nct(K) * 256, _nct(N) * 256
+                for ti in range(_nct(K)):
+                    for tj in range(_nct(N)):
+                        ni, nj = min(16, K - 16 * ti), min(16, N - 16 * tj)
+                        slot = self.parts[t].data_ptr() + 4 * local if parts else 0
+                        zf = first_unused if (parts and local == 0) else 0
+                        recs.append([xs.data_ptr() + 4 * 256 * ti, dp.data_ptr() + 4 * 256 * tj, sx | (sp << 32),
+                                     ni | (nj << 8) | (N << 32), gW.data_ptr() + 4 * (16 * ti * N + 16 * tj),
+                                     gb.data_ptr() + 4 * 16 * tj if ti == 0 else 0, slot, cbits | (zf << 32)])
+                        local += 1
+            assert local == self.items[t] and first_unused <= PARTS
+        out = torch.tensor(recs, dtype=torch.int64).to(self.dev)
+        self._witems[key] = out
+        return out
 
     # ------------------------------------------------------------------------------------------- fused rollout
     def supports_fused_rollout(self, env):

@@ -1139,40 +1139,35 @@ void mlp_tshadow(Tensor desc, int64_t ntw, int64_t total) {
         "mlp_tshadow");
 }
 
-void mlp_wgrad(Tensor desc, int64_t ntw, int64_t B, int64_t nsplit, int64_t items0, int64_t items1,
-               c10::optional<Tensor> parts0, c10::optional<Tensor> parts1, double clip0, double clip1,
-               c10::optional<Tensor> g_log_std, int64_t A, c10::optional<Tensor> mstats, c10::optional<Tensor> stats,
-               c10::optional<Tensor> ent_coef, c10::optional<Tensor> kl_coef, c10::optional<Tensor> mpart,
-               int64_t mpart_rows, c10::optional<Tensor> bump) {
-  need(desc, at::kLong, "desc");
+// items: device int64 [nitems, 8] (ops/mlp.py MLPEngine.wgrad_items); nrt: 16-row tiles of the batch
+void mlp_wgrad(Tensor items, int64_t nrt, int64_t nsplit, c10::optional<Tensor> g_log_std, int64_t A,
+               c10::optional<Tensor> ls_part, double ls_clip, c10::optional<Tensor> stats, Tensor ent_coef,
+               Tensor kl_coef, Tensor mpart, int64_t mpart_rows, c10::optional<Tensor> bump) {
+  need(items, at::kLong, "items");
+  TORCH_CHECK(items.dim() == 2 && items.size(1) == 8 && items.size(0) >= 1, "mlp_wgrad: items must be [n, 8]");
   aca::WgradArgs a{};
   if (bump.has_value() && bump->defined()) {
     need(*bump, at::kLong, "bump");
     a.bump = bump->data_ptr<int64_t>();
   }
-  a.mpart = copt<float>(mpart, at::kFloat, "mpart");
-  a.mpart_rows = (int)mpart_rows;
-  if (a.mpart) TORCH_CHECK(mpart_rows >= 0 && mpart->numel() >= mpart_rows * aca::MPART_W && A <= 16,
-                           "mlp_wgrad: mpart too small");
-  a.tw = reinterpret_cast<const aca::MlpTower*>(desc.data_ptr());
-  a.ntw = (int)ntw;
-  a.B = (int)B;
+  need(mpart, at::kFloat, "mpart");
+  TORCH_CHECK(mpart_rows >= 0 && mpart.numel() >= mpart_rows * aca::MPART_W && A <= 16, "mlp_wgrad: mpart too small");
+  a.items = items.data_ptr<int64_t>();
+  a.nitems = (int)items.size(0);
+  a.nrt = (int)nrt;
   a.nsplit = (int)nsplit;
-  a.items[0] = (int)items0;
-  a.items[1] = (int)items1;
-  a.parts[0] = const_cast<float*>(copt<float>(parts0, at::kFloat, "parts0"));
-  a.parts[1] = const_cast<float*>(copt<float>(parts1, at::kFloat, "parts1"));
-  a.clip[0] = (float)clip0;
-  a.clip[1] = (float)clip1;
   a.g_log_std = const_cast<float*>(copt<float>(g_log_std, at::kFloat, "g_log_std"));
   a.A = (int)A;
-  a.mstats = const_cast<float*>(copt<float>(mstats, at::kFloat, "mstats"));
+  a.ls_part = const_cast<float*>(copt<float>(ls_part, at::kFloat, "ls_part"));
+  a.ls_clip = (float)ls_clip;
   a.stats = const_cast<float*>(copt<float>(stats, at::kFloat, "stats"));
-  a.ent_coef = copt<float>(ent_coef, at::kFloat, "ent_coef");
-  a.kl_coef = copt<float>(kl_coef, at::kFloat, "kl_coef");
-  if (a.stats) TORCH_CHECK(a.mstats && a.ent_coef && a.kl_coef, "mlp_wgrad: stats need mstats and coefficients");
-  if (a.mpart) TORCH_CHECK(a.mstats, "mlp_wgrad: mpart needs mstats");
-  check(aca_mlp_wgrad(&a, cur_stream(desc)), "mlp_wgrad");
+  need(ent_coef, at::kFloat, "ent_coef");
+  need(kl_coef, at::kFloat, "kl_coef");
+  a.ent_coef = ent_coef.data_ptr<float>();
+  a.kl_coef = kl_coef.data_ptr<float>();
+  a.mpart = mpart.data_ptr<float>();
+  a.mpart_rows = (int)mpart_rows;
+  check(aca_mlp_wgrad(&a, cur_stream(items)), "mlp_wgrad");
 }
 
 void mlp_rollout(Tensor desc, int64_t lds, Tensor obs, Tensor act, Tensor logp, Tensor ent, Tensor reward,
@@ -2049,9 +2044,8 @@ TORCH_LIBRARY(acamd, m) {
         "Tensor? act_out, Tensor? logp_out, Tensor? ent_out, Tensor? v_out, Tensor? act_in, Tensor? logp_old, "
         "Tensor? adv, Tensor? ret, Tensor? v_old, Tensor? ent_coef, Tensor? kl_coef, float vf_coef, float ppo_clip, "
         "float v_clip, bool ppo, Tensor? g_log_std, Tensor? mstats, Tensor? mpart=None, Tensor? stamps=None, Tensor? hdesc=None) -> ()");
-  m.def("mlp_wgrad(Tensor desc, int ntw, int B, int nsplit, int items0, int items1, Tensor? parts0, "
-        "Tensor? parts1, float clip0, float clip1, Tensor? g_log_std, int A, Tensor? mstats, Tensor? stats, "
-        "Tensor? ent_coef, Tensor? kl_coef, Tensor? mpart=None, int mpart_rows=0, Tensor? bump=None) -> ()");
+  m.def("mlp_wgrad(Tensor items, int nrt, int nsplit, Tensor? g_log_std, int A, Tensor? ls_part, float ls_clip, "
+        "Tensor? stats, Tensor ent_coef, Tensor kl_coef, Tensor mpart, int mpart_rows, Tensor? bump) -> ()");
   m.def("mlp_rollout(Tensor desc, int lds, Tensor obs, Tensor act, Tensor logp, Tensor ent, Tensor reward, "
         "Tensor done, Tensor truncated, Tensor log_std, Tensor ac_scale, int key_shift, int policy_seed, "
         "Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, Tensor env_ids, Tensor lin_A, "

@@ -139,8 +139,8 @@ __device__ __forceinline__ void layer_fwd(const float* X, int ldx, int K, gcf32*
 }
 
 // dX[16][K] = dP[16][N] W[K][N]^T, then * act'(Yprev) (Yprev: LDS outputs of the previous layer, act_prev) ->
-// dPprev (LDS; every column tile up to ngp2(K) written, columns >= K as 0) and, when gdst != null, the global rows
-// of the previous layer's dP. dP is zero-padded to 16*NG columns (NG = ngp2(N)); B operand from the data-gradient
+// dPprev (LDS; every column tile up to ngp2(K) written, columns >= K as 0) and, when gdst != null, the row tile's
+// blocks of the previous layer's dP in the training workspace (blk_out layout). dP is zero-padded to 16*NG columns (NG = ngp2(N)); B operand from the data-gradient
 // fragment copy G (zero pad, so no clamped loads).
 template <int NG>
 __device__ void layer_dgrad_t(const float* __restrict__ dP, int ldp, gcf32* __restrict__ G, int K,
@@ -170,15 +170,17 @@ __device__ void layer_dgrad_t(const float* __restrict__ dP, int ldp, gcf32* __re
       __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
     }
-    // C layout: col = lane&15 = kc, rows 4q + i
+    // C layout: col = lane&15 = kc, rows 4q + i -- in the workspace's block layout one 16-byte store per lane
+    floatx4 o;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = 4 * q + i;
       float v = 0.f;
       if (kok) v = acc[i] * act_bwd(Yprev[row * ldyp + kc], act_slope(act_prev));
       dPprev[row * lddp + kc] = v;
-      if (gdst && kok && row < rows) gdst[(size_t)row * K + kc] = v;
+      o[i] = v;
     }
+    if (gdst && kok) *(__attribute__((address_space(1))) floatx4*)(gdst + tile * 256 + r * 16 + 4 * q) = o;
   }
 }
 
@@ -286,13 +288,15 @@ __device__ __forceinline__ void wset_dgrad(const WSet<NG, NT>& R, const float* _
     if (NT % MLP_WAVES == 0 || wave + MLP_WAVES * s < NT) {
       const int kc = (wave + MLP_WAVES * s) * 16 + r;
       const bool kok = kc < K;
+      floatx4 o;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int row = 4 * q + i;
         const float v = kok ? acc[s][i] * act_bwd(Yprev[row * ldyp + kc], slope_prev) : 0.f;
         dPprev[row * lddp + kc] = v;
-        if (kok && row < rows) gdst[(size_t)row * K + kc] = v;
+        o[i] = v;
       }
+      if (kok) *(__attribute__((address_space(1))) floatx4*)(gdst + (wave + MLP_WAVES * s) * 256 + r * 16 + 4 * q) = o;
     }
   }
 }
@@ -338,25 +342,25 @@ __device__ __forceinline__ void whead_fwd(const WHead<NG>& R, const float* __res
   }
 }
 
-// rows [0, rows) x [0, w) of an LDS tile (row stride ld, 16-byte aligned rows) -> global rows of w floats. Widths
-// that are multiples of 4 go as 16-byte copies with the row index by shift when w / 4 is a power of two (these
-// copies sit between two layers of the dependent chain: the scalar form spent ~40 instructions per element on the
-// runtime division alone)
-__device__ __forceinline__ void rows_out(const float* __restrict__ src, int ld, gf32* __restrict__ dst, int w,
-                                         int rows) {
-  if ((w & 3) == 0) {
-    const int w4 = w >> 2, sh = __builtin_ctz(w4);
-    const bool p2 = (w4 & (w4 - 1)) == 0;
-    for (int e = threadIdx.x; e < rows * w4; e += MLP_THREADS) {
-      const int r = p2 ? e >> sh : e / w4, c4 = e - r * w4;
-      const floatx4 v = *reinterpret_cast<const floatx4*>(src + r * ld + 4 * c4);
-      *(__attribute__((address_space(1))) floatx4*)(dst + (size_t)r * w + 4 * c4) = v;
+// Training workspace layout (xs: layer inputs X_l, dp: pre-activation gradients dP_l, written by the train kernel):
+// 16 x 16 BLOCKS, column-major inside -- element (row, col) of a [B][w] array at
+//   ((row / 16) * ceil(w / 16) + col / 16) * 256 + (col % 16) * 16 + row % 16
+// so the weight-gradient MFMA's operand for column c and rows 4q .. 4q + 3 of a row tile is one 16-byte load and a
+// wave's 16 x 16 block one contiguous 1 KB read (row-major, each wave load was 4 rows x 64 B and one float per lane).
+
+// LDS tile rows [0, 16) x [0, w) (row stride ld) -> the row tile's blocks at dst (rows past the batch are written
+// too: their dP is zero, so their X -- finite -- adds nothing)
+__device__ __forceinline__ void blk_out(const float* __restrict__ src, int ld, gf32* __restrict__ dst, int w) {
+  const int nct = (w + 15) >> 4;
+  for (int e = threadIdx.x; e < nct * 64; e += MLP_THREADS) {
+    const int ct = e >> 6, c = (e >> 2) & 15, r4 = e & 3;
+    const int col = ct * 16 + c;
+    floatx4 v = {0.f, 0.f, 0.f, 0.f};
+    if (col < w) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) v[s] = src[(4 * r4 + s) * ld + col];
     }
-  } else {
-    for (int e = threadIdx.x; e < rows * w; e += MLP_THREADS) {
-      const int r = e / w, c = e - r * w;
-      dst[(size_t)r * w + c] = src[r * ld + c];
-    }
+    *(__attribute__((address_space(1))) floatx4*)(dst + ct * 256 + c * 16 + 4 * r4) = v;
   }
 }
 
@@ -537,6 +541,8 @@ __device__ __forceinline__ void mlp_tower(const MlpArgs& a, const int t, float* 
   // first weight loads they were a dependent global round trip in the middle of the chain): gaussian-phase thread
   // (r, j) the action component, row thread r the old log-prob and advantage (policy) or return and old value
   // (critic) -- the same threads that read them below
+  // this row tile's blocks of a workspace array of width w (blk_out layout)
+  auto wsp = [&](int64_t base, int w) { return P_<float>(base) + (size_t)blockIdx.x * ((w + 15) >> 4) * 256; };
   const bool policy = (t == 0);
   float e_act = 0.f, e_lo = 0.f, e_adv = 0.f, e_ret = 0.f, e_vo = 0.f;
   int e_ai = 0;
@@ -624,7 +630,6 @@ __device__ __forceinline__ void mlp_tower(const MlpArgs& a, const int t, float* 
       float v = 0.f;
       if (r < rows && c < a.D) v = a.obs[S.grow[r] * a.ld_obs + c];
       X0[e] = v;
-      if (a.mode == 2 && r < rows && c < a.D) P_<float>(S.xs[0])[(size_t)(row0 + r) * a.D + c] = v;
     }
   }
   __syncthreads();
@@ -667,8 +672,8 @@ __device__ __forceinline__ void mlp_tower(const MlpArgs& a, const int t, float* 
       layer_fwd(X, ldx, S.in[l], P_<const float>(S.F[l]), P_<const float>(S.b[l]), S.out[l], S.act[l], Yl, ldl);
       __syncthreads();
       stamp(3 + l);
-      if (a.mode == 2 && l + 1 < nl)   // inputs of layer l+1 for its weight gradient
-        rows_out(Yl, ldl, P_<float>(S.xs[l + 1]) + (size_t)row0 * S.out[l], S.out[l], rows);
+      if (a.mode == 2 && l == 0) blk_out(X0, ld0, wsp(S.xs[0], a.D), a.D);   // inputs of each layer for its
+      if (a.mode == 2 && l + 1 < nl) blk_out(Yl, ldl, wsp(S.xs[l + 1], S.out[l]), S.out[l]);   // weight gradient
       X = Yl;
       ldx = ldl;
     }
@@ -874,18 +879,20 @@ __device__ __forceinline__ void mlp_tower(const MlpArgs& a, const int t, float* 
   }
   stamp(14);   // head phase C + log-std sums (the data-gradient layers take slots 9 ..)
   // ---- top layer dP: apply the head activation derivative (tanh applied above) and publish
-  if constexpr (SP) {   // (no store loop ahead of the data-gradient MFMAs, see above; N <= 16)
-    const int N = S.out[L];
-    if (tid < MLP_BM * 16) {
-      const int r = tid >> 4, c = tid & 15;
-      if (r < rows && c < N) P_<float>(S.dp[L])[(size_t)(row0 + r) * N + c] = dPtop[r * ldP + c];
+  if constexpr (SP) {   // (no store loop ahead of the data-gradient MFMAs, see above; N <= 16: one block)
+    if (tid < 64) {
+      const int c = tid >> 2, r4 = tid & 3;
+      floatx4 v;
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) v[s2] = dPtop[(4 * r4 + s2) * ldP + c];   // (columns >= N are zero)
+      *(__attribute__((address_space(1))) floatx4*)(wsp(S.dp[L], S.out[L]) + c * 16 + 4 * r4) = v;
     }
   } else {
-    rows_out(dPtop, ldP, P_<float>(S.dp[L]) + (size_t)row0 * S.out[L], S.out[L], rows);
+    blk_out(dPtop, ldP, wsp(S.dp[L], S.out[L]), S.out[L]);
   }
   // ---- data-gradient chain: dP_l -> dP_{l-1}
   if constexpr (SP) {
-    auto gd = [&](int l) { return P_<float>(S.dp[l - 1]) + (size_t)row0 * S.in[l]; };
+    auto gd = [&](int l) { return wsp(S.dp[l - 1], S.in[l]); };
     if constexpr (TW == 0) {
       wset_dgrad(R.g3, dPtop, ldP, S.in[3], sm + S.yo[2], S.ld[2], act_slope(S.act[2]), P1, ldP, gd(3), rows,
                  wave, lane);
@@ -908,9 +915,8 @@ __device__ __forceinline__ void mlp_tower(const MlpArgs& a, const int t, float* 
       stamp(10);
     }
     // the layer inputs for the weight gradients (X0 and Y_0 .. Y_{L-1} are still in LDS)
-    rows_out(X0, ld0, P_<float>(S.xs[0]) + (size_t)row0 * a.D, a.D, rows);
-    for (int l = 0; l < L; ++l)
-      rows_out(sm + S.yo[l], S.ld[l], P_<float>(S.xs[l + 1]) + (size_t)row0 * S.out[l], S.out[l], rows);
+    blk_out(X0, ld0, wsp(S.xs[0], a.D), a.D);
+    for (int l = 0; l < L; ++l) blk_out(sm + S.yo[l], S.ld[l], wsp(S.xs[l + 1], S.out[l]), S.out[l]);
     if (a.stamps && blockIdx.x == 0) {
       cstamp(13);
       stamp(7);   // end of the data-gradient chain (stores issued)
@@ -923,7 +929,7 @@ __device__ __forceinline__ void mlp_tower(const MlpArgs& a, const int t, float* 
     float* nxt = P1;
     for (int l = L; l >= 1; --l) {
       const int K = S.in[l];
-      gf32* gdst = P_<float>(S.dp[l - 1]) + (size_t)row0 * K;
+      gf32* gdst = wsp(S.dp[l - 1], K);
       layer_dgrad(cur, ldP, S.out[l], P_<const float>(S.G[l]), K, sm + S.yo[l - 1], S.ld[l - 1], S.act[l - 1], nxt,
                   ldP, gdst, rows);
       __syncthreads();
@@ -956,111 +962,88 @@ __device__ __forceinline__ float clipsq(float v, float c) {
   return v * v;
 }
 
-// One 4-wave workgroup per 16x16 gradient tile: the waves take interleaved 128-row chunks of the batch (all 64
-// operand loads of a chunk in flight before its MFMAs), then the four partial tiles are summed through LDS.
-constexpr int WG_CHUNK = 32;   // loads per operand per lane per chunk (128 rows)
+// One 4-wave workgroup per ITEM (a 16 x 16 tile of one dW_l = X_l^T dP_l, its bias column sums when it is in the first
+// row of tiles, and its sum of squares for the global-norm clip), per batch split. The item record (8 int64, built by
+// ops/mlp.py, read with one scalar load -- the tower / layer / tile search over the device descriptor was a chain of
+// dependent round trips): X block base, dP block base, their row-tile strides (floats, low / high 32 bits),
+// (valid dW rows | valid columns << 8 | N << 32), dW tile pointer, bias pointer (0: none), sum-of-squares slot (0:
+// none), (clip as float bits | first parts slot to zero << 32, item 0 of a tower). The waves take interleaved row
+// tiles, every operand of a wave's row tiles in flight before its MFMAs; the partial tiles are summed through LDS.
+constexpr int WG_RT = 8;   // row tiles per wave per round (16 loads in flight per lane)
 
 __global__ void __launch_bounds__(256) mlp_wgrad_kernel(WgradArgs a) {
   __shared__ float red[4][64][5];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (blockIdx.x == gridDim.x - 1) {
-    // The bookkeeping workgroup (one past the tiles): the train kernel's partial rows summed in a fixed order
-    // (deterministic), the log-std gradient finished and its sum of squares written to its own slot, the loss
-    // statistics published, the update counter advanced. Done by a tile workgroup, this chain of dependent global
-    // round trips made that workgroup -- and so the launch -- finish last.
+    // The bookkeeping workgroup (one past the items): the train kernel's per-workgroup partial rows summed in a fixed
+    // order (deterministic) -- the loss statistics published and the log-std gradient finished with its sum of
+    // squares in its own slot -- and the update counter advanced. Every load is issued up front (one round trip).
     if (wave != 0) return;
+    const float kl = *a.kl_coef, ec = *a.ent_coef;
     float v[MPART_W];
 #pragma unroll
     for (int c = 0; c < MPART_W; ++c) v[c] = 0.f;
-    if (a.mpart) {
-      for (int row = lane; row < a.mpart_rows; row += 64) {
+    for (int row = lane; row < a.mpart_rows; row += 64) {
 #pragma unroll
-        for (int c = 0; c < MPART_W; ++c) v[c] += a.mpart[(size_t)row * MPART_W + c];
-      }
-#pragma unroll
-      for (int c = 0; c < MPART_W; ++c) v[c] = wave_sum(v[c]);
+      for (int c = 0; c < MPART_W; ++c) v[c] += a.mpart[(size_t)row * MPART_W + c];
     }
-    float g = 0.f;
-    if (a.g_log_std && lane < a.A) {
-      if (a.mpart) {
-        // the train kernel left its log-std terms in the partial rows only: the gradient is STORED (like every
-        // other element of this launch), so the slab needs no zeroing between minibatches
-        float part = 0.f;   // v[8 + lane] with compile-time indices (a runtime index would put v in scratch)
 #pragma unroll
-        for (int j = 0; j < MLP_MAXA; ++j) part = lane == j ? v[8 + j] : part;
-        g = part;
-        a.g_log_std[lane] = g;
-      } else {
-        g = a.g_log_std[lane];   // added atomically by the train kernel
+    for (int c = 0; c < MPART_W; ++c) v[c] = wave_sum(v[c]);
+    if (a.g_log_std) {
+      float g = 0.f;   // v[8 + lane] with compile-time indices (a runtime index would put v in scratch)
+#pragma unroll
+      for (int j = 0; j < MLP_MAXA; ++j) g = lane == j ? v[8 + j] : g;
+      // the gradient is STORED (like every other element of this launch): no zeroing between minibatches
+      if (lane < a.A) a.g_log_std[lane] = g;
+      if (a.ls_part) {
+        const float ss = wave_sum(lane < a.A ? clipsq(g, a.ls_clip) : 0.f);
+        if (lane == 0) *a.ls_part = ss;
       }
-    }
-    if (a.g_log_std && a.nsplit == 1 && a.parts[0]) {
-      const float ss = wave_sum(lane < a.A ? clipsq(g, a.clip[0]) : 0.f);
-      if (lane == 0) a.parts[0][a.items[0]] = ss;   // the slot after tower 0's tiles (host-checked < MLP_PARTS)
     }
     if (lane == 0) {
-      if (a.mpart)
-        for (int k = 0; k < 8; ++k) a.mstats[k] += v[k];
-      if (a.stats) {   // publish (and reset) the fused kernel's statistics
+      if (a.stats) {
         float m[8];
-        for (int k = 0; k < 8; ++k) m[k] = a.mstats[k];
-        m[5] = m[0] + (*a.kl_coef) * m[1] - (*a.ent_coef) * m[2];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) m[k] = v[k];
+        m[5] = m[0] + kl * m[1] - ec * m[2];
+#pragma unroll
         for (int k = 0; k < 7; ++k) a.stats[k] = m[k];
-        for (int k = 0; k < 8; ++k) a.mstats[k] = 0.f;
       }
       // the train kernel (the counter's only reader in this minibatch) has finished: stream order
-      if (a.bump) *a.bump += 1;
+      if (a.bump) __hip_atomic_fetch_add(a.bump, (int64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     return;
   }
   const int split = blockIdx.x % a.nsplit;
-  int item = blockIdx.x / a.nsplit;
-  // locate (tower, layer, tile)
-  int t = 0;
-  if (item >= a.items[0]) {
-    item -= a.items[0];
-    t = 1;
-    if (t >= a.ntw || item >= a.items[1]) return;
-  }
-  const int local_item = item;
-  const MlpTower& T = a.tw[t];
-  const int nl = (int)T.nl;
-  int l = 0;
-  for (; l < nl; ++l) {
-    const int n = (((int)T.in[l] + 15) >> 4) * (((int)T.out[l] + 15) >> 4);
-    if (item < n) break;
-    item -= n;
-  }
-  if (l >= nl) return;
-  const int K = (int)T.in[l], N = (int)T.out[l];
-  const int tn = (N + 15) >> 4;
-  const int ti = item / tn, tj = item - ti * tn;
-  const int i0 = ti * 16, j0 = tj * 16;
+  const int64_t* rec = a.items + (size_t)(blockIdx.x / a.nsplit) * 8;
+  gcf32* X = P_<const float>(rec[0]);
+  gcf32* P = P_<const float>(rec[1]);
+  const int sx = (int)(rec[2] & 0xFFFFFFFF), sp = (int)(rec[2] >> 32);
+  const int ni = (int)(rec[3] & 0xFF), nj = (int)((rec[3] >> 8) & 0xFF), N = (int)(rec[3] >> 32);
+  const int per = (a.nrt + a.nsplit - 1) / a.nsplit;
+  const int rb = split * per, re = min(a.nrt, rb + per);
   const int r = lane & 15, q = lane >> 4;
-  gcf32* X = P_<const float>(T.xs[l]);
-  gcf32* P = P_<const float>(T.dp[l]);
-  const int ia = i0 + r, jb = j0 + r;
-  const bool iok = ia < K, jok = jb < N;
-  const int iac = iok ? ia : 0, jbc = jok ? jb : 0;
-  // split ranges are whole 128-row chunks; the workspace is zero-padded to a multiple of 128 rows, so a chunk is
-  // always in bounds and its pad rows contribute zero (no selects on loaded values: all 64 loads stay in flight)
-  const int per = (((a.B + a.nsplit - 1) / a.nsplit) + 127) & ~127;
-  const int rb = split * per, re = min(a.B, rb + per);
   floatx4 acc = {0.f, 0.f, 0.f, 0.f};
   float bsum = 0.f;
-  for (int c0 = rb + wave * 4 * WG_CHUNK; c0 < re; c0 += 16 * WG_CHUNK) {
-    float av[WG_CHUNK], bv[WG_CHUNK];
+  for (int c0 = rb + wave; c0 < re; c0 += 4 * WG_RT) {
+    floatx4 xa[WG_RT], pb[WG_RT];
 #pragma unroll
-    for (int u = 0; u < WG_CHUNK; ++u) {
-      const int row = c0 + 16 * (u >> 2) + 4 * q + (u & 3);
-      av[u] = X[(size_t)row * K + iac];
-      bv[u] = P[(size_t)row * N + jbc];
+    for (int u = 0; u < WG_RT; ++u) {
+      const int rt = min(c0 + 4 * u, re - 1);   // (clamped: a duplicate load, not used)
+      xa[u] = *(gcfx4*)(X + (size_t)rt * sx + r * 16 + 4 * q);
+      pb[u] = *(gcfx4*)(P + (size_t)rt * sp + r * 16 + 4 * q);
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int u = 0; u < WG_CHUNK; ++u) {
-      acc = mfma4(av[u], bv[u], acc);
-      bsum += bv[u];
+    for (int u = 0; u < WG_RT; ++u) {
+      if (c0 + 4 * u < re) {
+        // lane (column r, quad q): rows 4q + s of the row tile, k-slot q of MFMA s (the same row mapping on both sides)
+        acc = mfma4(xa[u][0], pb[u][0], acc);
+        acc = mfma4(xa[u][1], pb[u][1], acc);
+        acc = mfma4(xa[u][2], pb[u][2], acc);
+        acc = mfma4(xa[u][3], pb[u][3], acc);
+        bsum += (pb[u][0] + pb[u][1]) + (pb[u][2] + pb[u][3]);
+      }
     }
   }
 #pragma unroll
@@ -1072,13 +1055,14 @@ __global__ void __launch_bounds__(256) mlp_wgrad_kernel(WgradArgs a) {
   for (int i = 0; i < 4; ++i) acc[i] = red[0][lane][i] + red[1][lane][i] + red[2][lane][i] + red[3][lane][i];
   bsum = red[0][lane][4] + red[1][lane][4] + red[2][lane][4] + red[3][lane][4];
   float ss = 0.f;
-  const float c = a.clip[t];
+  const float c = __int_as_float((int)(rec[7] & 0xFFFFFFFF));
+  gf32* gW = P_<float>(rec[4]);
   // C: col = lane&15 -> j, rows 4q+i -> i
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int ii = i0 + 4 * q + i, jj = j0 + r;
-    if (ii < K && jj < N) {
-      gf32* dst = P_<float>(T.gW[l]) + (size_t)ii * N + jj;
+    const int ii = 4 * q + i;
+    if (ii < ni && r < nj) {
+      gf32* dst = gW + (size_t)ii * N + r;
       if (a.nsplit > 1) atomicAdd((float*)dst, acc[i]);
       else {
         *dst = acc[i];
@@ -1086,25 +1070,26 @@ __global__ void __launch_bounds__(256) mlp_wgrad_kernel(WgradArgs a) {
       }
     }
   }
-  if (ti == 0) {
+  if (rec[5]) {
     // lanes with equal (lane & 15) hold partial column sums over rows = q (mod 4)
     bsum += lane_xor(bsum, 16);
     bsum += lane_xor(bsum, 32);
-    if (q == 0 && jok) {
-      if (a.nsplit > 1) atomicAdd((float*)(P_<float>(T.gb[l]) + jb), bsum);
+    if (q == 0 && r < nj) {
+      gf32* gb = P_<float>(rec[5]) + r;
+      if (a.nsplit > 1) atomicAdd((float*)gb, bsum);
       else {
-        P_<float>(T.gb[l])[jb] = bsum;
+        *gb = bsum;
         ss += clipsq(bsum, c);
       }
     }
   }
-  if (a.nsplit == 1 && a.parts[t]) {
+  if (a.nsplit == 1 && rec[6]) {
     ss = wave_sum(ss);
-    if (lane == 0) a.parts[t][local_item] = ss;
-    if (local_item == 0) {   // unused slots are zero: the optimiser sums all MLP_PARTS in a fixed order
-      const int first = a.items[t] + (t == 0 && a.g_log_std ? 1 : 0);   // (tower 0: the log-std slot is taken)
-      for (int k = first + lane; k < MLP_PARTS; k += 64) a.parts[t][k] = 0.f;
-    }
+    float* slot = reinterpret_cast<float*>(rec[6]);
+    if (lane == 0) *slot = ss;
+    const int zf = (int)(rec[7] >> 32);
+    if (zf)   // item 0 of its tower: the unused slots are zero (the optimiser sums all MLP_PARTS in a fixed order)
+      for (int k = zf + lane; k < MLP_PARTS; k += 64) slot[k] = 0.f;
   }
 }
 
@@ -1480,14 +1465,11 @@ extern "C" hipError_t aca_mlp_fwd(const MlpArgs* a, int ntw, size_t lds, int spe
 }
 
 extern "C" hipError_t aca_mlp_wgrad(const WgradArgs* a, hipStream_t stream) {
-  if (a->B <= 0) return hipSuccess;
-  if (!a->tw || a->nsplit < 1 || a->ntw < 1 || a->ntw > 2) return hipErrorInvalidValue;
-  for (int t = 0; t < a->ntw; ++t)
-    if (a->parts[t] && a->nsplit == 1 && a->items[t] > MLP_PARTS) return hipErrorInvalidValue;
-  if (a->g_log_std && a->parts[0] && a->nsplit == 1 && a->items[0] >= MLP_PARTS) return hipErrorInvalidValue;
-  const int total = a->items[0] + (a->ntw > 1 ? a->items[1] : 0);
+  if (a->nrt <= 0) return hipSuccess;
+  if (!a->items || a->nitems < 1 || a->nsplit < 1 || !a->mpart || !a->kl_coef || !a->ent_coef || a->A > MLP_MAXA)
+    return hipErrorInvalidValue;
   // + the bookkeeping workgroup (statistics, log-std gradient, update counter)
-  mlp_wgrad_kernel<<<total * a->nsplit + 1, 256, 0, stream>>>(*a);
+  mlp_wgrad_kernel<<<a->nitems * a->nsplit + 1, 256, 0, stream>>>(*a);
   return hipGetLastError();
 }
 

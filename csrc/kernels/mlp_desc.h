@@ -18,8 +18,8 @@ struct MlpTower {
   int64_t b[MLP_MAXL];
   int64_t gW[MLP_MAXL];
   int64_t gb[MLP_MAXL];
-  int64_t xs[MLP_MAXL];       // train workspace: layer inputs  [B][in]
-  int64_t dp[MLP_MAXL];       // train workspace: dL/d(pre-activation) [B][out]
+  int64_t xs[MLP_MAXL];       // train workspace: layer inputs [B][in], 16 x 16 blocks (mlp.hip blk_out)
+  int64_t dp[MLP_MAXL];       // train workspace: dL/d(pre-activation) [B][out], 16 x 16 blocks
   int64_t F[MLP_MAXL];        // forward operand: fp32 FRAGMENT copy of W (common.h mlp_frag_f), zero pad
   int64_t G[MLP_MAXL];        // data-gradient operand: fp32 fragment copy of W (mlp_frag_g; layers >= 1), zero pad
 };
@@ -56,15 +56,13 @@ struct MlpArgs {
 };
 
 struct WgradArgs {
-  const MlpTower* tw;
-  int ntw;
-  int B;
-  int nsplit;                 // > 1: the batch is split over waves, results added atomically (no sumsq)
-  float* parts[2];            // sumsq slots per tower (null: none)
-  float clip[2];              // element-wise clip applied before squaring (<= 0: none)
-  float* g_log_std; int A;         // included in tower 0's first slot (the partial rows are added here)
-  float* mstats; float* stats; const float* ent_coef; const float* kl_coef;
-  int items[2];               // 16x16 tiles per tower (host-computed)
+  const int64_t* items;       // device item table (mlp.hip mlp_wgrad_kernel; ops/mlp.py MLPEngine.wgrad_items)
+  int nitems;
+  int nrt;                    // 16-row tiles of the batch
+  int nsplit;                 // > 1: the row tiles are split over workgroups, results added atomically (no sumsq)
+  float* g_log_std; int A;    // the log-std gradient (summed from the train kernel's partial rows)
+  float* ls_part; float ls_clip;   // its sum of squares slot (tower 0's slot after its tiles; null: none)
+  float* stats; const float* ent_coef; const float* kl_coef;
   const float* mpart; int mpart_rows;   // the train kernel's partial rows (reduced here in a fixed order)
   int64_t* bump;              // optional counter advanced once (PPO update counter after the update's last minibatch)
 };

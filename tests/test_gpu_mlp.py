@@ -281,3 +281,64 @@ def test_seg_stats_kernel_matches_reference(cuda):
     x = torch.randn(300000, device=cuda) * 3 + 1
     segs = torch.tensor([[0, 1], [7, 100], [1000, 65536], [70000, 229999], [5, 3]], device=cuda)
     torch.testing.assert_close(seg_stats(x, segs), seg_stats_ref(x, segs), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("case", [(17, 6, False, "basic"), (4, 2, True, "basic"), (40, 3, False, "basic")])
+def test_mlp_spec_train_path_matches_generic(cuda, case):
+    """The train launch's SPEC path (reference towers, every weight fragment preloaded into registers, split-K head
+    layers) == the generic layer loop: same gradients to fp32 summation-order noise, same statistics."""
+    ob, ac, disc, variant = case
+    m, ref, flat, eng = _model(cuda, ob, ac, disc, variant, seed=5)
+    B = 512
+    obs = torch.randn(B, ob, device=cuda)
+    with torch.no_grad():
+        pi, v0 = ref(obs)
+        keys = torch.arange(B, device=cuda, dtype=torch.int64)
+        act, lp0, _ = (D.categorical_sample_ref(pi, keys, 9) if disc else
+                       D.gaussian_sample_ref(pi, ref.actor.log_std, keys, 9))
+    lo = lp0 + 0.2 * torch.randn(B, device=cuda)
+    adv, ret = torch.randn(B, device=cuda), v0 + torch.randn(B, device=cuda)
+    beta, ce = torch.tensor(0.3, device=cuda), torch.tensor(0.02, device=cuda)
+    out = []
+    for spec in (True, False):
+        eng.spec = spec
+        flat.grad.zero_()
+        stats = torch.zeros(16, device=cuda)
+        eng.train(obs, act, lo, adv, ret, ce, beta, B, v_old=v0, ppo=True, ppo_clip=0.2, stats=stats,
+                  want_parts=True)
+        torch.cuda.synchronize()
+        out.append((flat.grad.clone(), stats.clone(), [p.clone() for p in eng.parts]))
+    (g1, s1, p1), (g0, s0, p0) = out
+    scale = g0.abs().max()
+    assert (g1 - g0).abs().max() <= 1e-5 * scale, float((g1 - g0).abs().max() / scale)
+    torch.testing.assert_close(s1, s0, rtol=1e-5, atol=1e-7)
+    for a, b in zip(p1, p0):
+        torch.testing.assert_close(a.sum(), b.sum(), rtol=1e-5, atol=1e-9)
+
+
+@pytest.mark.parametrize("variant", ["basic", "a3c"])
+def test_item_path_optimizer_matches_sweep(cuda, variant):
+    """The optimiser's item path (MLP segments: 16 x 64 weight blocks that also write the fragment copies, small
+    weights, element ranges) updates every parameter, moment and step count exactly as the float4 sweep path."""
+    from actor_critic_algs_on_tensorflow_amd.ops.mlp import frag_f, frag_g
+    from actor_critic_algs_on_tensorflow_amd.ops.optim import FusedGroupStep, make_optimizer
+    runs = []
+    for items in (True, False):
+        m, ref, flat, eng = _model(cuda, 17, 6, False, variant, seed=11)
+        opts = [make_optimizer("adam", flat, g, lr, max_grad_norm=0.5)
+                for g, lr in (("actor", 3e-3), ("critic", 1e-2))]
+        gs = FusedGroupStep(opts, eng.frag_copies() if items else None)
+        assert (gs._items[0] is not None) == items
+        for it in range(3):
+            flat.grad.copy_(torch.randn(flat.numel, generator=torch.Generator().manual_seed(20 + it)).to(cuda))
+            gs.step()
+        torch.cuda.synchronize()
+        runs.append((flat.data.clone(), [(o.m.clone(), o.v.clone(), o.t.clone()) for o in opts], eng, m))
+    (p1, st1, eng1, m1), (p0, st0, _, _) = runs
+    assert torch.equal(p1, p0)
+    for (a, b, c), (x, y, z) in zip(st1, st0):
+        assert torch.equal(a, x) and torch.equal(b, y) and torch.equal(c, z)
+    for i, lay in enumerate(l for tw in eng1.towers for l in tw):
+        assert torch.equal(eng1.F[id(lay)], frag_f(lay.kernel.detach()))
+        if id(lay) in eng1.G:
+            assert torch.equal(eng1.G[id(lay)], frag_g(lay.kernel.detach()))

@@ -735,6 +735,17 @@ class ActorCriticTrainer:
             self.opts[g].ext_parts = eng.parts[t] if used else None
         self._apply_grads()
 
+    def _epoch_buffers(self, obs, actions, B):
+        """Persistent minibatch-order copies of one epoch's PPO inputs (fixed addresses: graph-capturable)."""
+        key = (B, obs.shape[1], tuple(actions.shape[1:]), actions.dtype)
+        if getattr(self, "_epoch_key", None) != key:
+            dev = obs.device
+            self._epoch_bufs = dict(obs=torch.empty(B, obs.shape[1], device=dev),
+                                    act=torch.empty((B,) + tuple(actions.shape[1:]), dtype=actions.dtype, device=dev),
+                                    **{k: torch.empty(B, device=dev) for k in ("logp", "adv", "ret", "v")})
+            self._epoch_key = key
+        return self._epoch_bufs
+
     @torch.no_grad()
     def _learn_mlp(self, ret, adv):
         cfg, st, eng = self.cfg, self.storage, self.mlp
@@ -744,20 +755,25 @@ class ActorCriticTrainer:
         adv, ret = adv.contiguous(), ret.contiguous()
         B = obs.shape[0]
         if cfg.algo == "ppo":
-            # minibatch rows come from the keyed epoch permutation computed inside the fused kernel (no index list)
             mb = B // cfg.ppo_minibatches
             uc = self.update_counter.view(1)
             # the grouped Adam launches of this update know their step (t + j + 1 for minibatch j): no per-launch
             # step ticket, the counters advance once after the loop
             offsets = self.cfg.engine_opts.adam_step_offsets
             self._t_offs_used = 0
+            g = self._epoch_buffers(obs, actions, B)
             for ep in range(cfg.ppo_epochs):
+                # the epoch's rows in minibatch order (the keyed permutation, one gather launch): the train launches
+                # read contiguous rows, with no index or permutation round trip ahead of their input tiles
+                _native.require().mlp_epoch_gather(obs, actions, logp_old, adv, ret, v_old, g["obs"], g["act"],
+                                                   g["logp"], g["adv"], g["ret"], g["v"], uc, ep, self.policy_seed)
                 for k in range(cfg.ppo_minibatches):
                     last = ep == cfg.ppo_epochs - 1 and k == cfg.ppo_minibatches - 1
                     self._t_off = ep * cfg.ppo_minibatches + k if offsets else None
+                    sl = slice(k * mb, (k + 1) * mb)
                     # the last minibatch's weight-gradient launch advances the update counter (no extra launch)
-                    self._mlp_step(eng, mb, None, obs, actions, logp_old, adv, ret, v_old,
-                                   perm=(uc, ep, k * mb, B, self.policy_seed), bump=self.update_counter if last else None)
+                    self._mlp_step(eng, mb, None, g["obs"][sl], g["act"][sl], g["logp"][sl], g["adv"][sl],
+                                   g["ret"][sl], g["v"][sl], bump=self.update_counter if last else None)
             self._t_off = None
             if self._t_offs_used:
                 assert self._t_offs_used == cfg.ppo_epochs * cfg.ppo_minibatches

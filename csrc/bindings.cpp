@@ -27,6 +27,7 @@ hipError_t aca_opt_multi(const int64_t*, const float*, const int64_t*, int, int,
 hipError_t aca_prp_perm(int64_t*, int, uint32_t, const int64_t*, int, hipStream_t);
 hipError_t aca_mlp_fwd(const aca::MlpArgs*, int, size_t, int, hipStream_t);
 hipError_t aca_mlp_wgrad(const aca::WgradArgs*, hipStream_t);
+hipError_t aca_mlp_epoch_gather(const aca::EpochGatherArgs*, hipStream_t);
 hipError_t aca_ppo_head(const aca::PpoHeadArgs*, int, hipStream_t);
 int aca_ppo_head_planes(int);
 int aca_opt_set_unroll(int);
@@ -1170,6 +1171,49 @@ void mlp_wgrad(Tensor items, int64_t nrt, int64_t nsplit, c10::optional<Tensor> 
   check(aca_mlp_wgrad(&a, cur_stream(items)), "mlp_wgrad");
 }
 
+// PPO epoch gather for the MLP engine: out rows i = in rows prp(i) (keyed by the device update counter uc, epoch ep)
+void mlp_epoch_gather(Tensor obs, Tensor act, Tensor logp, Tensor adv, Tensor ret, c10::optional<Tensor> v,
+                      Tensor o_obs, Tensor o_act, Tensor o_logp, Tensor o_adv, Tensor o_ret, c10::optional<Tensor> o_v,
+                      Tensor uc, int64_t ep, int64_t seed) {
+  TORCH_CHECK(obs.is_cuda() && obs.scalar_type() == at::kFloat && obs.dim() == 2 && obs.stride(1) == 1,
+              "mlp_epoch_gather: obs must be fp32 [n, D] with unit column stride");
+  const int64_t n = obs.size(0), D = obs.size(1);
+  TORCH_CHECK(act.is_cuda() && act.is_contiguous() && act.element_size() == 4 && act.size(0) == n,
+              "mlp_epoch_gather: act must be [n] int32 or [n, A] fp32");
+  const int64_t aw = act.numel() / n;
+  for (const Tensor* t : {&logp, &adv, &ret, &o_logp, &o_adv, &o_ret}) {
+    need(*t, at::kFloat, "mlp_epoch_gather row value");
+    TORCH_CHECK(t->numel() == n, "mlp_epoch_gather: per-row values must have n elements");
+  }
+  need(o_obs, at::kFloat, "o_obs");
+  TORCH_CHECK(o_obs.numel() == n * D && o_act.is_contiguous() && o_act.numel() == n * aw &&
+                  o_act.element_size() == 4, "mlp_epoch_gather: output shapes");
+  need(uc, at::kLong, "uc");
+  aca::EpochGatherArgs a{};
+  a.n = (int)n;
+  a.D = (int)D;
+  a.aw = (int)aw;
+  a.obs = ptr<float>(obs);
+  a.ld_obs = obs.stride(0);
+  a.act = reinterpret_cast<const uint32_t*>(act.data_ptr());
+  a.logp = ptr<float>(logp);
+  a.adv = ptr<float>(adv);
+  a.ret = ptr<float>(ret);
+  a.v = copt<float>(v, at::kFloat, "v");
+  a.o_obs = ptr<float>(o_obs);
+  a.o_act = reinterpret_cast<uint32_t*>(o_act.data_ptr());
+  a.o_logp = ptr<float>(o_logp);
+  a.o_adv = ptr<float>(o_adv);
+  a.o_ret = ptr<float>(o_ret);
+  a.o_v = const_cast<float*>(copt<float>(o_v, at::kFloat, "o_v"));
+  TORCH_CHECK((a.v != nullptr) == (a.o_v != nullptr), "mlp_epoch_gather: v and o_v go together");
+  if (a.v) TORCH_CHECK(v->numel() == n && o_v->numel() == n, "mlp_epoch_gather: v shapes");
+  a.uc = uc.data_ptr<int64_t>();
+  a.ep = (int)ep;
+  a.seed = (uint32_t)seed;
+  check(aca_mlp_epoch_gather(&a, cur_stream(obs)), "mlp_epoch_gather");
+}
+
 void mlp_rollout(Tensor desc, int64_t lds, Tensor obs, Tensor act, Tensor logp, Tensor ent, Tensor reward,
                  Tensor done, Tensor trunc, Tensor log_std, Tensor ac_scale, int64_t key_shift, int64_t policy_seed,
                  Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, Tensor env_ids, Tensor lin_A,
@@ -2046,6 +2090,8 @@ TORCH_LIBRARY(acamd, m) {
         "float v_clip, bool ppo, Tensor? g_log_std, Tensor? mstats, Tensor? mpart=None, Tensor? stamps=None, Tensor? hdesc=None) -> ()");
   m.def("mlp_wgrad(Tensor items, int nrt, int nsplit, Tensor? g_log_std, int A, Tensor? ls_part, float ls_clip, "
         "Tensor? stats, Tensor ent_coef, Tensor kl_coef, Tensor mpart, int mpart_rows, Tensor? bump) -> ()");
+  m.def("mlp_epoch_gather(Tensor obs, Tensor act, Tensor logp, Tensor adv, Tensor ret, Tensor? v, Tensor o_obs, "
+        "Tensor o_act, Tensor o_logp, Tensor o_adv, Tensor o_ret, Tensor? o_v, Tensor uc, int ep, int seed) -> ()");
   m.def("mlp_rollout(Tensor desc, int lds, Tensor obs, Tensor act, Tensor logp, Tensor ent, Tensor reward, "
         "Tensor done, Tensor truncated, Tensor log_std, Tensor ac_scale, int key_shift, int policy_seed, "
         "Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, Tensor env_ids, Tensor lin_A, "
@@ -2138,6 +2184,7 @@ TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
   m.impl("mlp_tshadow", &mlp_tshadow);
   m.impl("mlp_wgrad", &mlp_wgrad);
   m.impl("mlp_rollout", &mlp_rollout);
+  m.impl("mlp_epoch_gather", &mlp_epoch_gather);
   m.impl("gemm", &gemm);
   m.impl("cnn_trunk_fwd", &cnn_trunk_fwd);
   m.impl("fc_value", &fc_value);

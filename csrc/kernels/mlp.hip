@@ -364,6 +364,27 @@ __device__ __forceinline__ void blk_out(const float* __restrict__ src, int ld, g
   }
 }
 
+// blk_out with at most NCT column tiles: straight-line (predicated) stores, so the waitcnt pass can count them
+// (a store loop between the SPEC weight loads and their MFMAs makes it drain the whole weight stream)
+template <int NCT>
+__device__ __forceinline__ void blk_out_c(const float* __restrict__ src, int ld, gf32* __restrict__ dst, int w) {
+  const int nct = (w + 15) >> 4;
+#pragma unroll
+  for (int j = 0; j < (NCT * 64 + MLP_THREADS - 1) / MLP_THREADS; ++j) {
+    const int e = threadIdx.x + MLP_THREADS * j;
+    if (e < nct * 64) {
+      const int ct = e >> 6, c = (e >> 2) & 15, r4 = e & 3;
+      const int col = ct * 16 + c;
+      floatx4 v = {0.f, 0.f, 0.f, 0.f};
+      if (col < w) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) v[s] = src[(4 * r4 + s) * ld + col];
+      }
+      *(__attribute__((address_space(1))) floatx4*)(dst + ct * 256 + c * 16 + 4 * r4) = v;
+    }
+  }
+}
+
 __device__ __forceinline__ int64_t row_key(const MlpArgs& a, int grow) {
   return a.tg[grow] * ((int64_t)1 << a.key_shift) + a.env_ids[grow];
 }
@@ -382,6 +403,7 @@ struct MlpShared {
   float g[MLP_BM];
   float hls[MLP_MAXA], hsc[MLP_MAXA], hco[2];   // head parameters: raw log-std, action scale, kl / entropy coefs
   int64_t ts[16];                               // SPEC diagnostics stamps
+  float er[5][MLP_BM];                          // SPEC: the loss head's row inputs (log-prob, adv, ret, v, action)
 };
 
 // SPEC register sets of the reference towers (NG0 = k-groups of the observation width)
@@ -605,6 +627,15 @@ __device__ __forceinline__ void mlp_tower(const MlpArgs& a, const int t, float* 
         const int e = lane + 64 * u;
         if (eg && e < rows * a.A) S.hd[e / a.A][e % a.A] = ea[u];   // (phase A reads it as e_act)
       }
+      // the row inputs through LDS too: read from registers, the head's first use would wait (vmcnt) for every
+      // weight load and workspace store issued after them
+      if (lane < MLP_BM) {
+        S.er[0][lane] = e_lo;
+        S.er[1][lane] = e_adv;
+        S.er[2][lane] = e_ret;
+        S.er[3][lane] = e_vo;
+        S.er[4][lane] = __int_as_float(e_ai);
+      }
       head_params_store(lane, hp);
     } else {
       spec_load<SPEC>(R, a.htw[TW], wave, lane, tid);
@@ -618,6 +649,13 @@ __device__ __forceinline__ void mlp_tower(const MlpArgs& a, const int t, float* 
     if (policy && a.head == 2 && tid < MLP_BM * MLP_MAXA) {
       const int r = tid / MLP_MAXA, j = tid % MLP_MAXA;
       if (j < a.A && r < rows) e_act = S.hd[r][j];
+    }
+    if (tid < MLP_BM) {
+      e_lo = S.er[0][tid];
+      e_adv = S.er[1][tid];
+      e_ret = S.er[2][tid];
+      e_vo = S.er[3][tid];
+      e_ai = __float_as_int(S.er[4][tid]);
     }
   } else {
     gather_rows();
@@ -637,8 +675,8 @@ __device__ __forceinline__ void mlp_tower(const MlpArgs& a, const int t, float* 
   cstamp(12);
   // ---- forward
   if constexpr (SP) {
-    // (the layer inputs X_l for the weight gradients stay in LDS and are stored after the data-gradient chain: a
-    // store loop between the weight loads and their MFMAs would make the waitcnt pass drain the whole weight stream)
+    // (the layer inputs X_l for the weight gradients are stored after the forward: a store loop between the weight
+    // loads and their MFMAs would make the waitcnt pass drain the whole weight stream)
     float* P1 = sm + S.yo[nl - 1] + MLP_BM * S.ld[nl - 1] + MLP_BM * (MLP_MAXW + 4);   // head split-K scratch
     auto next = [&](int l) {
       __syncthreads();
@@ -662,6 +700,16 @@ __device__ __forceinline__ void mlp_tower(const MlpArgs& a, const int t, float* 
       whead_fwd(R.f2, sm + S.yo[1], S.ld[1], S.out[2], act_slope(S.act[2]), sm + S.yo[2], S.ld[2], P1, wave, lane,
                 tid);
       next(2);
+    }
+    // the layer inputs for the weight gradients, issued now: they drain under the head and the data-gradient chain
+    blk_out_c<SP ? SPEC : 1>(X0, ld0, wsp(S.xs[0], a.D), a.D);
+    if constexpr (TW == 0) {
+      blk_out_c<8>(sm + S.yo[0], S.ld[0], wsp(S.xs[1], S.out[0]), S.out[0]);
+      blk_out_c<8>(sm + S.yo[1], S.ld[1], wsp(S.xs[2], S.out[1]), S.out[1]);
+      blk_out_c<4>(sm + S.yo[2], S.ld[2], wsp(S.xs[3], S.out[2]), S.out[2]);
+    } else {
+      blk_out_c<16>(sm + S.yo[0], S.ld[0], wsp(S.xs[1], S.out[0]), S.out[0]);
+      blk_out_c<8>(sm + S.yo[1], S.ld[1], wsp(S.xs[2], S.out[1]), S.out[1]);
     }
   } else {
     const float* X = X0;
@@ -914,9 +962,6 @@ __device__ __forceinline__ void mlp_tower(const MlpArgs& a, const int t, float* 
                  lane);
       stamp(10);
     }
-    // the layer inputs for the weight gradients (X0 and Y_0 .. Y_{L-1} are still in LDS)
-    blk_out(X0, ld0, wsp(S.xs[0], a.D), a.D);
-    for (int l = 0; l < L; ++l) blk_out(sm + S.yo[l], S.ld[l], wsp(S.xs[l + 1], S.out[l]), S.out[l]);
     if (a.stamps && blockIdx.x == 0) {
       cstamp(13);
       stamp(7);   // end of the data-gradient chain (stores issued)
@@ -1091,6 +1136,22 @@ __global__ void __launch_bounds__(256) mlp_wgrad_kernel(WgradArgs a) {
     if (zf)   // item 0 of its tower: the unused slots are zero (the optimiser sums all MLP_PARTS in a fixed order)
       for (int k = zf + lane; k < MLP_PARTS; k += 64) slot[k] = 0.f;
   }
+}
+
+// PPO epoch gather: row i of every minibatch input (observation, action, old log-prob, advantage, return, old value)
+// copied from row prp(i) of the batch -- the keyed epoch permutation (envs/rng.py prp; key from the device update
+// counter) -- so the epoch's train launches read contiguous rows: no index or permutation round trip ahead of
+// their input tiles. Actions are copied as 4-byte words (float components or the int32 index). One thread per row.
+__global__ void __launch_bounds__(256) mlp_epoch_gather_kernel(EpochGatherArgs a) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n) return;
+  const int64_t src = prp_index((uint32_t)i, (uint32_t)a.n, minibatch_key(a.seed, *a.uc, a.ep));
+  for (int c = 0; c < a.D; ++c) a.o_obs[(size_t)i * a.D + c] = a.obs[src * a.ld_obs + c];
+  for (int c = 0; c < a.aw; ++c) a.o_act[(size_t)i * a.aw + c] = a.act[src * a.aw + c];
+  a.o_logp[i] = a.logp[src];
+  a.o_adv[i] = a.adv[src];
+  a.o_ret[i] = a.ret[src];
+  if (a.v) a.o_v[i] = a.v[src];
 }
 
 // The fragment copies F (every layer) and G (layers >= 1) of every W of the launched towers (common.h mlp_frag_f /
@@ -1470,6 +1531,13 @@ extern "C" hipError_t aca_mlp_wgrad(const WgradArgs* a, hipStream_t stream) {
     return hipErrorInvalidValue;
   // + the bookkeeping workgroup (statistics, log-std gradient, update counter)
   mlp_wgrad_kernel<<<a->nitems * a->nsplit + 1, 256, 0, stream>>>(*a);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t aca_mlp_epoch_gather(const EpochGatherArgs* a, hipStream_t stream) {
+  if (a->n <= 0) return hipSuccess;
+  if (!a->uc || a->D < 1 || a->aw < 1) return hipErrorInvalidValue;
+  mlp_epoch_gather_kernel<<<(a->n + 255) / 256, 256, 0, stream>>>(*a);
   return hipGetLastError();
 }
 

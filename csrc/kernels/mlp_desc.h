@@ -67,6 +67,15 @@ struct WgradArgs {
   int64_t* bump;              // optional counter advanced once (PPO update counter after the update's last minibatch)
 };
 
+// PPO epoch gather (mlp_epoch_gather_kernel): row i of the outputs = row prp(i) of the inputs
+struct EpochGatherArgs {
+  int n, D, aw;               // rows, observation width, action words per row (A floats or 1 int32)
+  const float* obs; int64_t ld_obs;
+  const uint32_t* act; const float* logp; const float* adv; const float* ret; const float* v;   // v optional
+  float* o_obs; uint32_t* o_act; float* o_logp; float* o_adv; float* o_ret; float* o_v;
+  const int64_t* uc; int ep; uint32_t seed;
+};
+
 // Fused rollout of the MuJoCo-shaped linear bank (mlp_rollout_kernel): T steps of actor + Gaussian sample + env step.
 struct RolloutArgs {
   const MlpTower* tw;         // tower 0 (actor) of the engine descriptor

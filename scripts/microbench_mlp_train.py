@@ -46,8 +46,9 @@ def main():
     res = {0: [], 1: []}
     for rep in range(20):
         stamps.zero_()
-        eng.train(obs, actions, logp_old, adv, ret, tr.ent_coef, tr.kl_coef, mb, perm=(uc, 0, 0, B, tr.policy_seed),
-                  stamps=stamps, **kw)
+        # contiguous minibatch rows (the trainer's epoch-gathered layout)
+        eng.train(obs[:mb], actions[:mb], logp_old[:mb], adv[:mb], ret[:mb], tr.ent_coef, tr.kl_coef, mb,
+                  stamps=stamps, **dict(kw, v_old=v_old[:mb]))
         torch.cuda.synchronize()
         s = stamps.cpu().tolist()
         for t in (0, 1):

@@ -89,7 +89,7 @@ def _cos(a, b):
     return float(torch.nn.functional.cosine_similarity(a.double().flatten(), b.double().flatten(), dim=0))
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 @pytest.mark.parametrize("overlap", ["strict", "lag1"])
 def test_dp_segments_union_equivalence(cuda, tmp_path, overlap, world):
     two = _spawn(tmp_path, world, 16 // world, overlap)
@@ -123,7 +123,7 @@ def _deltas(snaps):
     return [snaps[k] - snaps[k - 1] for k in range(1, len(snaps))]
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_dp_ppo_captured_as_segments_equals_eager(cuda, tmp_path, world, monkeypatch):
     """Breakout-shaped PPO under DP (minibatch gradient all-reduces, global advantage normalisation via the packed
     fp64 moments, which also carry the KL proxy for the adaptive lr) is captured as a segment chain -- no eager
@@ -144,14 +144,17 @@ def test_dp_ppo_captured_as_segments_equals_eager(cuda, tmp_path, world, monkeyp
         assert torch.equal(a, b), (k, _cos(a, b))
 
 
-def test_dp_mlp_ppo_captured_as_segments(cuda, tmp_path):
-    """MuJoCo-shaped PPO on the MLP engine under DP: captured (segments), ranks identical, replay follows eager."""
+@pytest.mark.parametrize("world", [2, 8])
+def test_dp_mlp_ppo_captured_as_segments(cuda, tmp_path, world):
+    """MuJoCo-shaped PPO on the MLP engine under DP (world 2, and the BASELINE node's 8 ranks): captured (segments),
+    ranks identical, replay follows eager."""
     kw = dict(name="mujoco_ppo_dp8", n_steps=16, ppo_epochs=2, ppo_minibatches=4)
-    cap = _spawn(tmp_path, 2, 8, "strict", tag="mlp_cap", **kw)
-    eag = _spawn(tmp_path, 2, 8, "strict", tag="mlp_eager", capture=False, **kw)
+    cap = _spawn(tmp_path, world, 16 // world, "strict", tag="mlp_cap", **kw)
+    eag = _spawn(tmp_path, world, 16 // world, "strict", tag="mlp_eager", capture=False, **kw)
     assert cap[0]["kind"] == "segments"
-    for a, b in zip(cap[0]["snaps"], cap[1]["snaps"]):
-        assert torch.equal(a, b), "ranks diverged"
+    for r in range(1, world):
+        for a, b in zip(cap[0]["snaps"], cap[r]["snaps"]):
+            assert torch.equal(a, b), "ranks diverged"
     for d_c, d_e in zip(_deltas(cap[0]["snaps"]), _deltas(eag[0]["snaps"])):
         assert _cos(d_c, d_e) > 0.99, _cos(d_c, d_e)
 
@@ -169,7 +172,7 @@ def test_dp_bf16_buckets_track_fp32(cuda, tmp_path, overlap):
 
 
 # ---------------------------------------------------------------------------------------------- RCCL, in-graph
-def _rccl_worker(_idx, port, out_dir, name, kw, modes):
+def _rccl_worker(_idx, port, out_dir, name, kw, modes, overlap="strict"):
     """One process, an RCCL ("nccl") group of world 1 on cuda:0: the same DP update captured with the collectives
     INSIDE one hipGraph (``dp_capture="auto"``) and as the host-cut segment chain (``"segments"``)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ACAMD_GEMM_TUNE="0")
@@ -183,7 +186,7 @@ def _rccl_worker(_idx, port, out_dir, name, kw, modes):
         for mode in modes:
             dp = DataParallel()
             assert dp.backend == "nccl"
-            tr = ActorCriticTrainer(_cfg(kw_envs(name), "strict", name, dp_capture=mode, **kw), dp=dp)
+            tr = ActorCriticTrainer(_cfg(kw_envs(name), overlap, name, dp_capture=mode, **kw), dp=dp)
             tr.capture(warmup=1)
             kind = tr.graph[0]
             n_graphs = (tr.graph[1].n_graphs if kind == "segments" else
@@ -196,7 +199,7 @@ def _rccl_worker(_idx, port, out_dir, name, kw, modes):
                 snaps.append(tr.flat.data.cpu().clone())
             res[mode] = {"kind": kind, "n_graphs": n_graphs, "host_collectives": dp.issued - issued,
                          "snaps": snaps}
-        torch.save(res, os.path.join(out_dir, f"rccl_{name}.pt"))
+        torch.save(res, os.path.join(out_dir, f"rccl_{name}_{overlap}.pt"))
     finally:
         dist.destroy_process_group()
 
@@ -217,11 +220,25 @@ def test_rccl_dp_update_is_one_graph(cuda, tmp_path, name, kw):
     to the segment-chain capture of the same update (host-issued collectives between graphs)."""
     mp.spawn(_rccl_worker, args=(_free_port(), str(tmp_path), name, dict(kw), ["auto", "segments"]), nprocs=1,
              join=True)
-    res = torch.load(tmp_path / f"rccl_{name}.pt", weights_only=True)
+    res = torch.load(tmp_path / f"rccl_{name}_strict.pt", weights_only=True)
     one, seg = res["auto"], res["segments"]
     assert one["kind"] == "single", one["kind"]
     assert one["host_collectives"] == 0, one["host_collectives"]
     assert seg["host_collectives"] > 0 and seg["n_graphs"] > 1
+    for k, (a, b) in enumerate(zip(one["snaps"], seg["snaps"])):
+        assert torch.equal(a, b), (k, _cos(a, b))
+    assert not torch.equal(one["snaps"][0], one["snaps"][-1])
+
+
+def test_rccl_lag1_one_graph_with_adam_equals_segments(cuda, tmp_path):
+    """RCCL lag-1 A2C as one graph per update, with Adam: the first replay holds no gradient in the
+    all-reduced copy C, so the gated optimiser launches apply nothing -- no moment decay, no step count -- exactly as
+    the segmented lag-1 schedule, which skips its first optimiser graph on the host. Bitwise equal, every update."""
+    mp.spawn(_rccl_worker, args=(_free_port(), str(tmp_path), "pong_a2c", dict(optimizer="adam"),
+                                 ["auto", "segments"], "lag1"), nprocs=1, join=True)
+    res = torch.load(tmp_path / "rccl_pong_a2c_lag1.pt", weights_only=True)
+    one, seg = res["auto"], res["segments"]
+    assert one["kind"] == "single" and seg["kind"] == "lag1", (one["kind"], seg["kind"])
     for k, (a, b) in enumerate(zip(one["snaps"], seg["snaps"])):
         assert torch.equal(a, b), (k, _cos(a, b))
     assert not torch.equal(one["snaps"][0], one["snaps"][-1])

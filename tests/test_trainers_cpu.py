@@ -101,7 +101,7 @@ def _dp_worker(rank, world, port, out_dir, n_envs=4, extra=None, updates=3, kl_d
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_dp_gloo_equals_single_process_union_batch(tmp_path, world):
     """Sync DP over W ranks x 8/W envs == one process over the same 8 envs (grad all-reduce + global adv norm via
     the packed moments all-reduce)."""
@@ -157,14 +157,60 @@ def test_dp_gloo_kl_rides_in_moments_allreduce(tmp_path):
     assert torch.equal(out[True][1]["p"], a["p"]) and out[True][1]["kl"] == a["kl"]
 
 
-def _a3c_proc(rank, world, port, d):
+def _dp_union_worker(rank, world, port, out_dir, name, kw):
+    import torch.distributed as dist
+    from actor_critic_algs_on_tensorflow_amd.parallel.dp import DataParallel
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    tr = ActorCriticTrainer(preset(name, **_quiet(device="cpu", cuda_graph=False, **kw)), dp=DataParallel())
+    for _ in range(3):
+        tr.step()
+    torch.save({"p": tr.flat.data.clone(), "env": tr.env.num_envs}, os.path.join(out_dir, f"u{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name,kw,exact", [
+    # MLP PPO (BASELINE config 5 shape, Gaussian head): one minibatch per epoch, so the union-batch step is the same
+    ("mujoco_ppo_dp8", dict(n_steps=8, ppo_epochs=2, ppo_minibatches=1), True),
+    # CNN PPO (BASELINE config 3 shape, Nature CNN on the autograd engine): Adam turns the fp32 summation-order noise
+    # of near-zero gradients (dead ReLU units) into lr-sized steps, so the update is compared by direction and size
+    ("breakout_ppo", dict(n_steps=4, ppo_epochs=2, ppo_minibatches=1), False),
+])
+def test_dp_gloo_world8_ppo_equals_union_batch(tmp_path, name, kw, exact):
+    """World-8 data parallelism (the BASELINE node: 8 ranks, one env bank per rank): PPO with the
+    minibatch gradient all-reduce and the global advantage moments == one process stepping the union batch of 8
+    env banks (every rank's envs are its own: env ids offset by rank * N, so the union is the same 8 envs); ranks
+    bit-identical."""
+    world = 8
+    mp.spawn(_dp_union_worker, args=(world, _free_port(), str(tmp_path), name, dict(kw, num_envs=1, seed=5)),
+             nprocs=world, join=True)
+    ps = [torch.load(tmp_path / f"u{r}.pt", weights_only=True)["p"] for r in range(world)]
+    for p in ps[1:]:
+        assert torch.equal(p, ps[0]), "ranks diverged"
+    torch.set_num_threads(4)
+    single = ActorCriticTrainer(preset(name, **_quiet(device="cpu", cuda_graph=False, **dict(kw, num_envs=world,
+                                                                                              seed=5))))
+    p0 = single.flat.data.clone()
+    for _ in range(3):
+        single.step()
+    d8, d1 = ps[0] - p0, single.flat.data - p0
+    assert d1.abs().max() > 0
+    if exact:
+        assert torch.allclose(ps[0], single.flat.data, rtol=1e-4, atol=1e-6), float((d8 - d1).abs().max())
+    cos = float(torch.nn.functional.cosine_similarity(d8.double(), d1.double(), dim=0))
+    assert cos > 0.999 and abs(float(d8.norm() / d1.norm()) - 1) < 1e-2, (cos, float(d8.norm() / d1.norm()))
+
+
+def _a3c_proc(rank, world, port, d, ps=1, iters=6):
     from actor_critic_algs_on_tensorflow_amd.cli import train
-    ps = 1
+    torch.set_num_threads(1)
     job = "ps" if rank < ps else "worker"
     task = rank if rank < ps else rank - ps
     out = train.main([job, str(task), "--env", "CartPole-v0", "--ps_num", str(ps), "--worker_num", str(world - ps),
                       "--initport", str(port), "--outdir", d + "/logs", "--checkpoint_dir", d + "/ck",
-                      "--max_iters", "6", "--save_every", "3", "--quiet"])
+                      "--max_iters", str(iters), "--save_every", "3", "--quiet"])
     torch.save({"gstep": out["global_step"], "role": out["role"],
                 "steps": [h["gstep"] for h in out.get("history", [])]}, f"{d}/r{rank}.pt")
 
@@ -183,6 +229,27 @@ def test_a3c_async_parameter_server(tmp_path):
     latest = ckpt.latest_checkpoint(f"{d}/ck")
     t = ckpt.load_tensors(latest)
     assert "global_actor/logits/kernel" in t and "global_critic/Variable_1" in t
+
+
+def test_a3c_eight_process_cluster_two_ps_six_workers(tmp_path):
+    """An 8-process A3C cluster (2 parameter-server shards + 6 workers; the reference's default is 2 ps + 4 workers,
+    A3C/train.py:15-16): the shards split the variables (greedy_ps_strategy), every push is applied once under one
+    serialised global step, each worker's steps are increasing, and the chief's checkpoint holds every reference
+    variable."""
+    d = str(tmp_path)
+    mp.spawn(_a3c_proc, args=(8, _free_port(), d, 2, 4), nprocs=8, join=True)
+    roles = [torch.load(f"{d}/r{r}.pt", weights_only=True) for r in range(8)]
+    assert [r["role"] for r in roles] == ["ps", "ps"] + ["worker"] * 6
+    steps = sorted(s for r in roles[2:] for s in r["steps"])
+    assert steps == list(range(1, len(steps) + 1)), "every global step taken exactly once across 6 workers"
+    for r in roles[2:]:
+        assert r["steps"] == sorted(r["steps"]) and len(r["steps"]) >= 1
+    assert all(r["gstep"] >= 4 for r in roles[:2])
+    for w in range(6):
+        assert os.path.exists(f"{d}/logs/worker_{w}.log")
+    from actor_critic_algs_on_tensorflow_amd import ckpt
+    t = ckpt.load_tensors(ckpt.latest_checkpoint(f"{d}/ck"))
+    assert "global_actor/logits/kernel" in t and "global_critic/value/bias" in t
 
 
 def test_pendulum_ppo_solves_on_cpu_and_test_model_scores_checkpoint(tmp_path):

@@ -257,6 +257,40 @@ __device__ __forceinline__ void wset_fwd(const WSet<NG, NT>& R, const float* __r
   }
 }
 
+// wset_fwd with the A operands (rows of the layer input) already in registers: xa[g] = the lane's four k values of
+// group g (lane (r, q): row r, columns 16 g + 4 q .. + 3)
+template <int NG, int NT>
+__device__ __forceinline__ void wset_fwd_rega(const WSet<NG, NT>& R, const float (&xa)[NG][4], int N, float slope,
+                                              float* __restrict__ Y, int ldy, int wave, int lane) {
+  constexpr int NS = WSet<NG, NT>::NS;
+  const int r = lane & 15, q = lane >> 4;
+  if (!(NT % MLP_WAVES == 0 || wave < NT)) return;
+  floatx4 acc[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) acc[s] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      if (NT % MLP_WAVES == 0 || wave + MLP_WAVES * s < NT) {
+        acc[s] = mfma4(xa[g][0], R.w[s][g][0], acc[s]);
+        acc[s] = mfma4(xa[g][1], R.w[s][g][1], acc[s]);
+        acc[s] = mfma4(xa[g][2], R.w[s][g][2], acc[s]);
+        acc[s] = mfma4(xa[g][3], R.w[s][g][3], acc[s]);
+      }
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    if (NT % MLP_WAVES == 0 || wave + MLP_WAVES * s < NT) {
+      const int c = (wave + MLP_WAVES * s) * 16 + r;
+      const bool cok = c < N;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) Y[(4 * q + i) * ldy + c] = cok ? act_fwd(acc[s][i] + R.b[s], slope) : 0.f;
+    }
+  }
+}
+
 // data-gradient layer from registers (G fragments: tiles over K, k-groups over N)
 template <int NG, int NT>
 __device__ __forceinline__ void wset_dgrad(const WSet<NG, NT>& R, const float* __restrict__ dP, int ldp, int K,
@@ -505,8 +539,22 @@ __device__ __forceinline__ void mlp_tower(const MlpArgs& a, const int t, float* 
     return sm + off;
   };
   // per-layer LDS offsets and strides, computed once (one LDS read per use instead of a chain over the earlier
-  // layers' widths read from the descriptor)
-  if (tid == 64) {
+  // layers' widths read from the descriptor); SPEC: compile-time (the reference widths; A <= 16, D <= 16 * SPEC)
+  constexpr int SLD[2][4] = {{132, 132, 68, 20}, {260, 132, 20, 20}};
+  auto LDY = [&](int l) { return SP ? SLD[TW == 0 ? 0 : 1][l] : S.ld[l]; };
+  auto YO = [&](int l) {
+    if (!SP) return S.yo[l];
+    int o = MLP_BM * (16 * (SP ? SPEC : 1) + 4);
+    for (int j = 0; j < l; ++j) o += MLP_BM * SLD[TW == 0 ? 0 : 1][j];
+    return o;
+  };
+  // descriptor words: SPEC from the kernel-argument copy (compile-time layer indices: scalar loads), else LDS-staged
+  auto INW = [&](int l) { return SP ? (int)a.htw[TW == 0 ? 0 : 1].in[l] : S.in[l]; };
+  auto OUTW = [&](int l) { return SP ? (int)a.htw[TW == 0 ? 0 : 1].out[l] : S.out[l]; };
+  auto ACT = [&](int l) { return SP ? (int)a.htw[TW == 0 ? 0 : 1].act[l] : S.act[l]; };
+  auto XS = [&](int l) { return SP ? a.htw[TW == 0 ? 0 : 1].xs[l] : S.xs[l]; };
+  auto DPW = [&](int l) { return SP ? a.htw[TW == 0 ? 0 : 1].dp[l] : S.dp[l]; };
+  if (!SP && tid == 64) {
     for (int l = 0; l < nl; ++l) {
       S.yo[l] = (int)(Yp(l) - sm);
       S.ld[l] = ldyf(l);
@@ -536,7 +584,7 @@ __device__ __forceinline__ void mlp_tower(const MlpArgs& a, const int t, float* 
     else if (i < 2 * MLP_MAXA + 2) S.hco[i - 2 * MLP_MAXA] = v;
   };
   if (!SP && tid >= 128 && tid < 128 + 2 * MLP_MAXA + 2) head_params_store(tid - 128, head_params(tid - 128));
-  if (tid >= 96 && tid < 96 + nl) {
+  if (!SP && tid >= 96 && tid < 96 + nl) {
     const int l = tid - 96;
     S.in[l] = (int)T.in[l];
     S.out[l] = (int)T.out[l];
@@ -588,75 +636,65 @@ __device__ __forceinline__ void mlp_tower(const MlpArgs& a, const int t, float* 
     head_rows();
   };
   Regs R;
+  // SPEC wave 0: Gaussian action components, head parameter, row inputs (raw loads, selected when staged)
+  float ea[4] = {0.f, 0.f, 0.f, 0.f}, hp = 0.f, hx[2] = {0.f, 0.f};
+  int32_t hxi = 0;
+  constexpr int NG0 = SP ? SPEC : 1;
+  float xa[NG0][4];   // SPEC: this lane's layer-0 A operands (row r, columns 16 g + 4 q + s) straight from memory
   if constexpr (SP) {
-    // SPEC: the tower's weight fragments into registers at entry. Wave 0 first gathers the rows and the input tile
-    // (vmcnt retires in issue order: the gather must not queue behind its weight stream), the other waves' weight
-    // loads are in flight meanwhile. (Each load sits on ONE path: a register loaded on both sides of a join would
-    // make the waitcnt pass drain every load before the second one.)
+    // SPEC: every wave requests its layer-0 input operands first, then ALL of its weight fragments for the whole
+    // forward + data-gradient chain (216 / 304 KB per actor / critic workgroup, which the L2 -> CU path delivers at
+    // ~60 B/clk in ~1.5 / 2.1 us), with no barrier in between: the CU's memory pipeline serves requests in order,
+    // so the inputs land first and layer 0 starts while the later layers' weights stream in. (Staging the input
+    // tile through one wave queued it behind the weight stream: the first layer started ~2.6 us into the launch.)
+    const int r = lane & 15, q = lane >> 4;
+    const int lrow = min(row0 + r, a.B - 1);
+    int64_t grow = lrow;
+    if (a.idx) grow = a.idx[lrow];
+    else if (a.perm_uc)
+      grow = prp_index((uint32_t)(a.perm_off + lrow), (uint32_t)a.perm_n,
+                       minibatch_key(a.perm_seed, *a.perm_uc, a.perm_ep));
+#pragma unroll
+    for (int g = 0; g < NG0; ++g)
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) {
+        const int col = 16 * g + 4 * q + s2;
+        xa[g][s2] = (col < a.D && row0 + r < a.B) ? a.obs[grow * a.ld_obs + col] : 0.f;
+      }
+    if (wave == 0 && lane < MLP_BM) S.grow[lane] = grow;
+    spec_load<SPEC>(R, a.htw[TW], wave, lane, tid);
+    // the loss head's inputs behind the weights (consumed after the forward, staged through LDS by then). Every
+    // load unconditional from a valid address, values selected afterwards: a register loaded on one side of a
+    // divergent branch and zeroed on the other makes the waitcnt pass drain the whole weight stream at the join.
     if (wave == 0) {
-      gather_rows();
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      head_rows();
-      const float hp = head_params(lane);   // (lanes 0 .. 33)
-      float ea[4];   // Gaussian action components, (row, j) = e / A for e = lane + 64 u (A <= 16: 4 per lane)
-      const bool eg = policy && a.head == 2;
+      const int64_t gr = S.grow[lane & 15];
+      const bool vclip = a.v_old && a.v_clip > 0.f;
+      const float* p0 = policy ? a.logp_old : a.ret;
+      const float* p1 = policy ? a.adv : (vclip ? a.v_old : a.ret);
+      const int32_t* p2 = (policy && a.head != 2) ? a.act_i_in : reinterpret_cast<const int32_t*>(a.ret);
+      hx[0] = p0[gr];
+      hx[1] = p1[gr];
+      hxi = p2[gr];
+      // head parameters: lane i < 16 log-std, < 32 action scale, 32 / 33 the kl / entropy coefficients
+      const bool gs = a.log_std && a.ac_scale;
+      const float* ph = (lane < MLP_MAXA && gs) ? a.log_std + min(lane, max(a.A - 1, 0))
+                        : (lane < 2 * MLP_MAXA && gs) ? a.ac_scale + min(lane - MLP_MAXA, max(a.A - 1, 0))
+                        : (lane == 2 * MLP_MAXA && a.kl_coef) ? a.kl_coef
+                        : (lane == 2 * MLP_MAXA + 1 && a.ent_coef) ? a.ent_coef : a.ret;
+      hp = *ph;   // (the raw values: selected where they are staged, after the forward -- a use here would wait)
+      if (policy && a.head == 2) {
+        const int n = max(rows * a.A, 1);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int e = lane + 64 * u;
-        ea[u] = (eg && e < rows * a.A) ? a.act_f_in[S.grow[e / a.A] * a.A + e % a.A] : 0.f;
+        for (int u = 0; u < 4; ++u) {
+          const int e = min(lane + 64 * u, n - 1);
+          ea[u] = a.act_f_in[S.grow[e / a.A] * a.A + e % a.A];
+        }
       }
-      constexpr int LD0 = 16 * (SP ? SPEC : 1) + 4;   // = ld0 (host-checked: ngp2(D) == SPEC)
-      constexpr int PER = (MLP_BM * LD0 + 63) / 64;
-      float xv[PER];
-#pragma unroll
-      for (int u = 0; u < PER; ++u) {
-        const int e = lane + 64 * u, r = e / LD0, c = e - r * LD0;
-        xv[u] = 0.f;
-        if (e < MLP_BM * LD0 && r < rows && c < a.D) xv[u] = a.obs[S.grow[r] * a.ld_obs + c];
-      }
-      spec_load<SPEC>(R, a.htw[TW], wave, lane, tid);
-#pragma unroll
-      for (int u = 0; u < PER; ++u) {
-        const int e = lane + 64 * u;
-        if (e < MLP_BM * LD0) X0[e] = xv[u];
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int e = lane + 64 * u;
-        if (eg && e < rows * a.A) S.hd[e / a.A][e % a.A] = ea[u];   // (phase A reads it as e_act)
-      }
-      // the row inputs through LDS too: read from registers, the head's first use would wait (vmcnt) for every
-      // weight load and workspace store issued after them
-      if (lane < MLP_BM) {
-        S.er[0][lane] = e_lo;
-        S.er[1][lane] = e_adv;
-        S.er[2][lane] = e_ret;
-        S.er[3][lane] = e_vo;
-        S.er[4][lane] = __int_as_float(e_ai);
-      }
-      head_params_store(lane, hp);
-    } else {
-      spec_load<SPEC>(R, a.htw[TW], wave, lane, tid);
     }
-    __syncthreads();
     stamp(1);
-    if (a.stamps && blockIdx.x == 0 && tid == 0) {   // diagnostics: slot 15 = wave 0's weight stream landed
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      S.ts[15] = __builtin_amdgcn_s_memrealtime();
-    }
-    if (policy && a.head == 2 && tid < MLP_BM * MLP_MAXA) {
-      const int r = tid / MLP_MAXA, j = tid % MLP_MAXA;
-      if (j < a.A && r < rows) e_act = S.hd[r][j];
-    }
-    if (tid < MLP_BM) {
-      e_lo = S.er[0][tid];
-      e_adv = S.er[1][tid];
-      e_ret = S.er[2][tid];
-      e_vo = S.er[3][tid];
-      e_ai = __float_as_int(S.er[4][tid]);
-    }
   } else {
     gather_rows();
     __syncthreads();
@@ -677,39 +715,76 @@ __device__ __forceinline__ void mlp_tower(const MlpArgs& a, const int t, float* 
   if constexpr (SP) {
     // (the layer inputs X_l for the weight gradients are stored after the forward: a store loop between the weight
     // loads and their MFMAs would make the waitcnt pass drain the whole weight stream)
-    float* P1 = sm + S.yo[nl - 1] + MLP_BM * S.ld[nl - 1] + MLP_BM * (MLP_MAXW + 4);   // head split-K scratch
+    float* P1 = sm + YO(nl - 1) + MLP_BM * LDY(nl - 1) + MLP_BM * (MLP_MAXW + 4);   // head split-K scratch
     auto next = [&](int l) {
       __syncthreads();
       stamp(3 + l);
     };
+    // layer 0 from the A operands in registers; wave 0 then keeps the tile in LDS (workspace store below)
+    wset_fwd_rega(R.f0, xa, OUTW(0), act_slope(ACT(0)), sm + YO(0), LDY(0), wave, lane);
+    if (wave == 0) {
+      const int r = lane & 15, q = lane >> 4;
+#pragma unroll
+      for (int g = 0; g < NG0; ++g)
+        *reinterpret_cast<floatx4*>(X0 + r * ld0 + 16 * g + 4 * q) = floatx4{xa[g][0], xa[g][1], xa[g][2], xa[g][3]};
+    }
+    auto stage_head_inputs = [&]() {   // wave 0, before the last forward barrier (the loads landed long before)
+      if (wave != 0) return;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = lane + 64 * u;
+        if (policy && a.head == 2 && e < rows * a.A) S.hd[e / a.A][e % a.A] = ea[u];   // (read as e_act)
+      }
+      if (lane < MLP_BM) {
+        const bool vclip = a.v_old && a.v_clip > 0.f;
+        S.er[0][lane] = policy ? hx[0] : 0.f;                                    // log-prob
+        S.er[1][lane] = policy ? hx[1] : 0.f;                                    // advantage
+        S.er[2][lane] = policy ? 0.f : hx[0];                                    // return
+        S.er[3][lane] = (!policy && vclip) ? hx[1] : 0.f;                        // old value
+        S.er[4][lane] = __int_as_float((policy && a.head != 2) ? hxi : 0);       // action index
+      }
+      const bool gs = a.log_std && a.ac_scale;
+      const bool hok = (lane < MLP_MAXA && gs && lane < a.A) ||
+                       (lane >= MLP_MAXA && lane < 2 * MLP_MAXA && gs && lane - MLP_MAXA < a.A) ||
+                       (lane == 2 * MLP_MAXA && a.kl_coef) || (lane == 2 * MLP_MAXA + 1 && a.ent_coef);
+      head_params_store(lane, hok ? hp : 0.f);
+    };
+    next(0);
     if constexpr (TW == 0) {
-      wset_fwd(R.f0, X0, ld0, S.out[0], act_slope(S.act[0]), sm + S.yo[0], S.ld[0], wave, lane);
-      next(0);
-      wset_fwd(R.f1, sm + S.yo[0], S.ld[0], S.out[1], act_slope(S.act[1]), sm + S.yo[1], S.ld[1], wave, lane);
+      wset_fwd(R.f1, sm + YO(0), LDY(0), OUTW(1), act_slope(ACT(1)), sm + YO(1), LDY(1), wave, lane);
       next(1);
-      wset_fwd(R.f2, sm + S.yo[1], S.ld[1], S.out[2], act_slope(S.act[2]), sm + S.yo[2], S.ld[2], wave, lane);
+      wset_fwd(R.f2, sm + YO(1), LDY(1), OUTW(2), act_slope(ACT(2)), sm + YO(2), LDY(2), wave, lane);
       next(2);
-      whead_fwd(R.f3, sm + S.yo[2], S.ld[2], S.out[3], act_slope(S.act[3]), sm + S.yo[3], S.ld[3], P1, wave, lane,
-                tid);
+      whead_fwd(R.f3, sm + YO(2), LDY(2), OUTW(3), act_slope(ACT(3)), sm + YO(3), LDY(3), P1, wave, lane, tid);
+      stage_head_inputs();
       next(3);
     } else {
-      wset_fwd(R.f0, X0, ld0, S.out[0], act_slope(S.act[0]), sm + S.yo[0], S.ld[0], wave, lane);
-      next(0);
-      wset_fwd(R.f1, sm + S.yo[0], S.ld[0], S.out[1], act_slope(S.act[1]), sm + S.yo[1], S.ld[1], wave, lane);
+      wset_fwd(R.f1, sm + YO(0), LDY(0), OUTW(1), act_slope(ACT(1)), sm + YO(1), LDY(1), wave, lane);
       next(1);
-      whead_fwd(R.f2, sm + S.yo[1], S.ld[1], S.out[2], act_slope(S.act[2]), sm + S.yo[2], S.ld[2], P1, wave, lane,
-                tid);
+      whead_fwd(R.f2, sm + YO(1), LDY(1), OUTW(2), act_slope(ACT(2)), sm + YO(2), LDY(2), P1, wave, lane, tid);
+      stage_head_inputs();
       next(2);
     }
+    if (policy && a.head == 2 && tid < MLP_BM * MLP_MAXA) {
+      const int r = tid / MLP_MAXA, j = tid % MLP_MAXA;
+      if (j < a.A && r < rows) e_act = S.hd[r][j];
+    }
+    if (tid < MLP_BM) {
+      e_lo = S.er[0][tid];
+      e_adv = S.er[1][tid];
+      e_ret = S.er[2][tid];
+      e_vo = S.er[3][tid];
+      e_ai = __float_as_int(S.er[4][tid]);
+    }
     // the layer inputs for the weight gradients, issued now: they drain under the head and the data-gradient chain
-    blk_out_c<SP ? SPEC : 1>(X0, ld0, wsp(S.xs[0], a.D), a.D);
+    blk_out_c<NG0>(X0, ld0, wsp(XS(0), a.D), a.D);
     if constexpr (TW == 0) {
-      blk_out_c<8>(sm + S.yo[0], S.ld[0], wsp(S.xs[1], S.out[0]), S.out[0]);
-      blk_out_c<8>(sm + S.yo[1], S.ld[1], wsp(S.xs[2], S.out[1]), S.out[1]);
-      blk_out_c<4>(sm + S.yo[2], S.ld[2], wsp(S.xs[3], S.out[2]), S.out[2]);
+      blk_out_c<8>(sm + YO(0), LDY(0), wsp(XS(1), OUTW(0)), OUTW(0));
+      blk_out_c<8>(sm + YO(1), LDY(1), wsp(XS(2), OUTW(1)), OUTW(1));
+      blk_out_c<4>(sm + YO(2), LDY(2), wsp(XS(3), OUTW(2)), OUTW(2));
     } else {
-      blk_out_c<16>(sm + S.yo[0], S.ld[0], wsp(S.xs[1], S.out[0]), S.out[0]);
-      blk_out_c<8>(sm + S.yo[1], S.ld[1], wsp(S.xs[2], S.out[1]), S.out[1]);
+      blk_out_c<16>(sm + YO(0), LDY(0), wsp(XS(1), OUTW(0)), OUTW(0));
+      blk_out_c<8>(sm + YO(1), LDY(1), wsp(XS(2), OUTW(1)), OUTW(1));
     }
   } else {
     const float* X = X0;
@@ -727,10 +802,10 @@ __device__ __forceinline__ void mlp_tower(const MlpArgs& a, const int t, float* 
     }
   }
   const int L = nl - 1;
-  const float* Yo = sm + S.yo[L];
-  const int ldo = S.ld[L];
+  const float* Yo = sm + YO(L);
+  const int ldo = LDY(L);
   // ---- heads: one thread per row
-  float* dPtop = sm + S.yo[L] + MLP_BM * S.ld[L];   // P0
+  float* dPtop = sm + YO(L) + MLP_BM * LDY(L);   // P0
   float* P1 = dPtop + MLP_BM * (MLP_MAXW + 4);
   const int ldP = MLP_MAXW + 4;
   if (a.mode == 2) {   // zero the top dP tile (the head writes only valid columns)
@@ -933,32 +1008,32 @@ __device__ __forceinline__ void mlp_tower(const MlpArgs& a, const int t, float* 
       floatx4 v;
 #pragma unroll
       for (int s2 = 0; s2 < 4; ++s2) v[s2] = dPtop[(4 * r4 + s2) * ldP + c];   // (columns >= N are zero)
-      *(__attribute__((address_space(1))) floatx4*)(wsp(S.dp[L], S.out[L]) + c * 16 + 4 * r4) = v;
+      *(__attribute__((address_space(1))) floatx4*)(wsp(DPW(L), OUTW(L)) + c * 16 + 4 * r4) = v;
     }
   } else {
     blk_out(dPtop, ldP, wsp(S.dp[L], S.out[L]), S.out[L]);
   }
   // ---- data-gradient chain: dP_l -> dP_{l-1}
   if constexpr (SP) {
-    auto gd = [&](int l) { return wsp(S.dp[l - 1], S.in[l]); };
+    auto gd = [&](int l) { return wsp(DPW(l - 1), INW(l)); };
     if constexpr (TW == 0) {
-      wset_dgrad(R.g3, dPtop, ldP, S.in[3], sm + S.yo[2], S.ld[2], act_slope(S.act[2]), P1, ldP, gd(3), rows,
+      wset_dgrad(R.g3, dPtop, ldP, INW(3), sm + YO(2), LDY(2), act_slope(ACT(2)), P1, ldP, gd(3), rows,
                  wave, lane);
       __syncthreads();
       stamp(9);
-      wset_dgrad(R.g2, P1, ldP, S.in[2], sm + S.yo[1], S.ld[1], act_slope(S.act[1]), dPtop, ldP, gd(2), rows, wave,
+      wset_dgrad(R.g2, P1, ldP, INW(2), sm + YO(1), LDY(1), act_slope(ACT(1)), dPtop, ldP, gd(2), rows, wave,
                  lane);
       __syncthreads();
       stamp(10);
-      wset_dgrad(R.g1, dPtop, ldP, S.in[1], sm + S.yo[0], S.ld[0], act_slope(S.act[0]), P1, ldP, gd(1), rows, wave,
+      wset_dgrad(R.g1, dPtop, ldP, INW(1), sm + YO(0), LDY(0), act_slope(ACT(0)), P1, ldP, gd(1), rows, wave,
                  lane);
       stamp(11);
     } else {
-      wset_dgrad(R.g2, dPtop, ldP, S.in[2], sm + S.yo[1], S.ld[1], act_slope(S.act[1]), P1, ldP, gd(2), rows,
+      wset_dgrad(R.g2, dPtop, ldP, INW(2), sm + YO(1), LDY(1), act_slope(ACT(1)), P1, ldP, gd(2), rows,
                  wave, lane);
       __syncthreads();
       stamp(9);
-      wset_dgrad(R.g1, P1, ldP, S.in[1], sm + S.yo[0], S.ld[0], act_slope(S.act[0]), dPtop, ldP, gd(1), rows, wave,
+      wset_dgrad(R.g1, P1, ldP, INW(1), sm + YO(0), LDY(0), act_slope(ACT(0)), dPtop, ldP, gd(1), rows, wave,
                  lane);
       stamp(10);
     }

@@ -96,6 +96,9 @@ def _ref_grads(ref, obs, act, lo, adv, ret, v_old, ppo, beta, ce, clip, vclip):
 def test_mlp_train_gradients_match_autograd(cuda, case, ppo):
     ob, ac, disc, variant = case
     m, ref, flat, eng = _model(cuda, ob, ac, disc, variant, seed=3)
+    # fixed inputs: an unseeded draw occasionally puts a pre-activation within rounding of the leaky-ReLU kink, where
+    # the kernel and autograd legitimately take different sides (one run in ~40 failed the 2e-3 bar on one element)
+    torch.manual_seed(1234)
     Bfull, B = 300, 200
     obs = torch.randn(Bfull, ob, device=cuda)
     with torch.no_grad():

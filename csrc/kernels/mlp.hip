@@ -776,16 +776,6 @@ __device__ __forceinline__ void mlp_tower(const MlpArgs& a, const int t, float* 
       e_vo = S.er[3][tid];
       e_ai = __float_as_int(S.er[4][tid]);
     }
-    // the layer inputs for the weight gradients, issued now: they drain under the head and the data-gradient chain
-    blk_out_c<NG0>(X0, ld0, wsp(XS(0), a.D), a.D);
-    if constexpr (TW == 0) {
-      blk_out_c<8>(sm + YO(0), LDY(0), wsp(XS(1), OUTW(0)), OUTW(0));
-      blk_out_c<8>(sm + YO(1), LDY(1), wsp(XS(2), OUTW(1)), OUTW(1));
-      blk_out_c<4>(sm + YO(2), LDY(2), wsp(XS(3), OUTW(2)), OUTW(2));
-    } else {
-      blk_out_c<16>(sm + YO(0), LDY(0), wsp(XS(1), OUTW(0)), OUTW(0));
-      blk_out_c<8>(sm + YO(1), LDY(1), wsp(XS(2), OUTW(1)), OUTW(1));
-    }
   } else {
     const float* X = X0;
     int ldx = ld0;
@@ -842,6 +832,7 @@ __device__ __forceinline__ void mlp_tower(const MlpArgs& a, const int t, float* 
       }
     }
     __syncthreads();
+    stamp(15);
   }
   if (tid < MLP_BM) {
     const int r = tid;
@@ -1003,6 +994,17 @@ __device__ __forceinline__ void mlp_tower(const MlpArgs& a, const int t, float* 
   stamp(14);   // head phase C + log-std sums (the data-gradient layers take slots 9 ..)
   // ---- top layer dP: apply the head activation derivative (tanh applied above) and publish
   if constexpr (SP) {   // (no store loop ahead of the data-gradient MFMAs, see above; N <= 16: one block)
+    // the layer inputs for the weight gradients, issued after the head (whose branch joins would otherwise wait for
+    // them to land): they drain under the data-gradient chain
+    blk_out_c<NG0>(X0, ld0, wsp(XS(0), a.D), a.D);
+    if constexpr (TW == 0) {
+      blk_out_c<8>(sm + YO(0), LDY(0), wsp(XS(1), OUTW(0)), OUTW(0));
+      blk_out_c<8>(sm + YO(1), LDY(1), wsp(XS(2), OUTW(1)), OUTW(1));
+      blk_out_c<4>(sm + YO(2), LDY(2), wsp(XS(3), OUTW(2)), OUTW(2));
+    } else {
+      blk_out_c<16>(sm + YO(0), LDY(0), wsp(XS(1), OUTW(0)), OUTW(0));
+      blk_out_c<8>(sm + YO(1), LDY(1), wsp(XS(2), OUTW(1)), OUTW(1));
+    }
     if (tid < 64) {
       const int c = tid >> 2, r4 = tid & 3;
       floatx4 v;

@@ -42,7 +42,7 @@ def main():
               clips=(cfg.clip_value, cfg.critic_clip_value))
     out = {"B_minibatch": mb}
     names = {1: "gather", 2: "x0", 3: "fwd0", 4: "fwd1", 5: "fwd2", 6: "fwd3", 8: "head", 14: "headC",
-             9: "dg_top", 10: "dg_2", 11: "dg_3", 7: "end", 15: "w_landed"}
+             9: "dg_top", 10: "dg_2", 11: "dg_3", 7: "end", 15: "headA"}
     res = {0: [], 1: []}
     for rep in range(20):
         stamps.zero_()

@@ -92,11 +92,11 @@ class CNNEngine:
         self.tconv_dgrad = implicit if tconv_dgrad is None else tconv_dgrad
         # one workgroup per env: the fused trunk wins whenever the per-layer GEMMs are launch/latency bound
         self.fused_trunk_max_b = 4096 if fused_trunk_max_b is None else fused_trunk_max_b
-        # rollout batches up to trunk_rows_max_b envs: seven row workgroups per env (224 CUs at 32 envs; late_w
-        # issues the conv2/conv3 weight loads after conv1, leaving conv1 the registers to pipeline its LDS reads).
-        # Larger batches already fill the chip with one workgroup per env (mode 0), where the split's recomputed
-        # receptive fields only cost
-        self.trunk_mode = 2 if o.trunk_late_w else 1
+        # rollout batches up to trunk_rows_max_b envs: seven row workgroups per env (224 CUs at 32 envs; mode 2 issues
+        # the conv2/conv3 weight loads after conv1, leaving conv1 the registers to pipeline its LDS reads). Larger
+        # batches already fill the chip with one workgroup per env (mode 3), where the split's recomputed receptive
+        # fields only cost
+        self.trunk_mode = 2
         self.trunk_rows_max_b = o.trunk_rows_max_b
         # learner data-gradient chain dy3 -> dy2 -> dy1 as ONE per-sample kernel (cnn_trunk_bwd; bias gradients as
         # per-sample partial rows reduced by the gradient finaliser) instead of two transposed-conv GEMMs
@@ -109,7 +109,6 @@ class CNNEngine:
         # narrow workgroups (off: fc_value + the 8-workgroup head_bwd kernel of round 2)
         self.a2c_head = o.a2c_head
         self._a2c_bar = None
-        self._fcf_cnt = None   # fused step fc product: slice counters + timeout word (fused_fc_args)
         self._fcb_sq = None    # fc_bwd's per-tile dWfc sums of squares (the finaliser's presummed norm job)
         self._cur_presum = False
         # A2C head v3 (loss.hip a2c_head_env_kernel): one workgroup per env, no grid-wide hand-off; the head's weight /
@@ -123,21 +122,14 @@ class CNNEngine:
         # off: split-K fp32 atomics into the slab (nondeterministic summation order)
         self.det_wgrad = implicit and o.det_wgrad
         self.wgrad_planes = o.wgrad_planes
-        # conv1 weight gradient by the per-sample kernel (conv_wgrad.hip: frames + dy1 staged once per sample) instead
-        # of the implicit-im2col GEMM, from this many learner rows up
-        self.conv1_wgrad_min_b = o.conv1_wgrad_min_b
-        self.conv1_planes = o.conv1_planes
-        # conv2 / conv3 weight gradients by the batched-position MFMA kernel (wgrad_gemm) or the per-sample NHWC
-        # kernel (conv_wgrad.hip) from this many rows up; one workgroup per plane: 256 planes cover the CUs
-        self.nhwc_wgrad_min_b = o.nhwc_wgrad_min_b
-        self.wgrad_gemm = o.wgrad_gemm
+        # learner batches from large_batch_min_b rows up: the conv1 weight gradient by the per-sample kernel
+        # (conv_wgrad.hip: frames + dy1 staged once per sample) or folded into the persistent trunk backward instead
+        # of the implicit-im2col GEMM; conv2 / conv3 weight gradients by the batched-position MFMA kernel (one
+        # workgroup per plane: 256 planes cover the CUs); the backward on ONE stream (Breakout PPO 18.3 -> 17.0 ms per
+        # update, profiles/r3_breakout_ab.txt); the fused trunk backward as a persistent kernel (weights in registers,
+        # one workgroup per CU walking the samples)
+        self.large_b = o.large_batch_min_b
         self.nhwc_planes = o.nhwc_planes
-        self.nhwc3_planes = o.nhwc_planes
-        # large-batch backward on ONE stream (Breakout PPO 18.3 -> 17.0 ms per update, profiles/r3_breakout_ab.txt)
-        self.serial_bwd_min_b = o.serial_bwd_min_b
-        # fused trunk backward as a persistent kernel (weights in registers, one workgroup per CU walking the samples)
-        # from this many learner rows up
-        self.trunk_bwd_persist_min_b = o.trunk_bwd_persist_min_b
         self.trunk_bwd_persist = o.trunk_bwd_persist
         self._planes = {}
         self._wsplits = {}
@@ -253,29 +245,11 @@ class CNNEngine:
 
     # ------------------------------------------------------------------------------------------------ forward
     def hpart(self, B, slot=0):
-        """fp32 [FC_PLANES, B, 512] split-K partial planes of the rollout fc product (GEMM out_mode 3); slot 1: the
-        second buffer of the fused step's in-launch fc product (it reads one while it writes the other)."""
+        """fp32 [FC_PLANES, B, 512] split-K partial planes of the rollout fc product (GEMM out_mode 3)."""
         key = (B, slot)
         if key not in self._hpart:
             self._hpart[key] = torch.zeros(FC_PLANES * B * 512, dtype=torch.float32, device=self.dev)
         return self._hpart[key]
-
-    def fused_fc_ok(self, B):
-        """The row-split fused step also computes the next observation's fc product (``EngineOpts.fused_fc``: at
-        most 32 envs, the fragment-ordered Wfc and conv copies)."""
-        return (self.opts.fused_fc and self.wfc_frag is not None and self.frag is not None and 1 <= B <= 32
-                and self.fused_step_ok(B))
-
-    def fused_fc_args(self, B):
-        """(Wfc copy, output planes, slice counters) of the next fused step's fc product: the planes go to the hpart
-        buffer the last fc product did NOT write (the step reads that one); ``last_fc`` then names the new planes."""
-        if self._fcf_cnt is None:   # 7 slices x (arrivals, departures) on own 64-byte lines + the timeout word
-            self._fcf_cnt = torch.zeros(232, dtype=torch.int32, device=self.dev)
-        hp = self.last_fc[0]
-        out = self.hpart(B, 1) if hp.data_ptr() == self.hpart(B, 0).data_ptr() else self.hpart(B, 0)
-        return self.wfc_frag, out, self._fcf_cnt
-
-    FCF_PLANES = 14   # cnn_fused.hip FCF_PLANES: 7 conv3 rows x 2 K halves
 
     def value(self, obs, b: _Bufs, out):
         """Bootstrap value of ``obs`` written straight into ``out`` [B] (trunk + the value column of the head)."""
@@ -299,10 +273,7 @@ class CNNEngine:
 
     def health_errors(self):
         """Names of the in-launch hand-offs that timed out since the engine was built (empty = healthy)."""
-        err = ["a2c_head bootstrap-value hand-off"] if self.a2c_head_timed_out() else []
-        if self._fcf_cnt is not None and int(self._fcf_cnt[224]) != 0:
-            err.append("fused-step fc product hand-off")
-        return err
+        return ["a2c_head bootstrap-value hand-off"] if self.a2c_head_timed_out() else []
 
     def fused_step_ok(self, B):
         """The rollout step can run as ONE launch of policy/env + the next observation's row-split trunk."""
@@ -328,7 +299,7 @@ class CNNEngine:
         kernel are the only readers of the frames then (``EngineOpts.mb_index`` off: copy the minibatch's
         observations)."""
         return (self.opts.mb_index and self.implicit and self.det_wgrad and B <= self.fused_trunk_max_b
-                and B > self.trunk_rows_max_b and B >= self.conv1_wgrad_min_b)
+                and B > self.trunk_rows_max_b and B >= self.large_b)
 
     def forward(self, obs, b: _Bufs, head=True, shift_out=None, fc_parts=False, obs_idx=None):
         """obs uint8 [B, 4, 84, 84] -> b.z fp32 [B, A+1] (logits | value); ``head=False`` stops at ``b.h`` (the
@@ -342,7 +313,7 @@ class CNNEngine:
         shifted = False
         want_shift = shift_out is not None
         if self.implicit and B <= self.fused_trunk_max_b:
-            if B > self.trunk_rows_max_b and self.opts.trunk_fwd_staged and self.frag is not None:
+            if B > self.trunk_rows_max_b and self.frag is not None:
                 F1, F2, F3 = self.frag   # mode 5: the bf16-staged kernel on the fragment-ordered weights
                 G.cnn_trunk_fwd(obs, F1, self.b1, F2, self.b2, F3, self.b3, b.y1, b.y2, b.y3, shift_out=shift_out,
                                 mode=5, obs_idx=obs_idx)
@@ -352,8 +323,8 @@ class CNNEngine:
                                 shift_out=shift_out, mode=self.trunk_mode + 5, obs_idx=obs_idx)
             else:
                 G.cnn_trunk_fwd(obs, self.sW1, self.b1, self.sW2, self.b2, self.sW3, self.b3, b.y1, b.y2, b.y3,
-                                shift_out=shift_out, mode=self.trunk_mode if B <= self.trunk_rows_max_b else
-                                (3 if self.opts.trunk_fwd_staged else 0), obs_idx=obs_idx)
+                                shift_out=shift_out, mode=self.trunk_mode if B <= self.trunk_rows_max_b else 3,
+                                obs_idx=obs_idx)
             shifted = shift_out is not None
         elif self.implicit:
             G.gemm(obs, 0, True, self.sW1, 256, True, b.y1, 32, 1, B * 400, 32, 256, bias=self.b1, relu=True,
@@ -426,30 +397,12 @@ class CNNEngine:
         self._wsplits[name] = S
         self._cur_planes[name] = S
 
-    def conv1_fold_ok(self, B):
-        """The per-sample trunk backward also leaves the sample's conv1 weight gradient (``EngineOpts.conv1_fold``):
-        one [32, 256] plane per sample, summed in order by the finaliser, instead of the conv1 product of the grouped
-        weight-gradient launch."""
-        return (self.opts.conv1_fold and self.dev.type == "cuda" and self.det_wgrad and self.implicit
-                and not self.opts.trunk_bwd_v2 and 1 <= B < self.trunk_bwd_persist_min_b)
-
     def _trunk_bwd(self, b, fold=False):
-        """dy3 -> dy2 -> dy1 (+ the bias-gradient rows); ``fold``: with :meth:`conv1_fold_ok`, the conv1 weight
-        gradient too (returns True when it was folded)."""
-        if self.opts.trunk_bwd_v2:   # trunk_bwd2.hip: at most trunk_bwd_persist workgroups, walking the samples
-            _native.require().cnn_trunk_bwd2(b.dy3, self.sW3, b.y2, self.sW2, b.y1, b.dy2, b.dy1, b.biasp, None,
-                                             self.trunk_bwd_persist)
-            return False
-        if fold and self.conv1_fold_ok(b.B):
-            buf = self._plane_buf("W1f", b.B * 32 * 256)
-            _native.require().cnn_trunk_bwd(b.dy3, self.sW3, b.y2, self.sW2, b.y1, b.dy2, b.dy1, b.biasp, None, 0,
-                                            b.obs, getattr(b, "obs_idx", None), buf, 1.0 / 255.0)
-            self._cur_planes["W1f"] = b.B
-            return True
-        persist = self.trunk_bwd_persist if b.B >= self.trunk_bwd_persist_min_b else 0
+        """dy3 -> dy2 -> dy1 (+ the bias-gradient rows); ``fold``: the persistent form of a large batch also computes
+        the conv1 weight gradient (one plane per workgroup, dy1 never stored; returns True when it did)."""
+        persist = self.trunk_bwd_persist if b.B >= self.large_b else 0
         acc = self.bias_rows(b.B) < b.B
-        if fold and persist and self.conv1_fold_persist_ok(b.B):
-            # one conv1 weight-gradient plane per workgroup, dy1 never stored (the fold was its only consumer)
+        if fold and persist and self.conv1_fold_ok(b.B):
             R = min(persist, b.B)
             buf = self._plane_buf("W1f", R * 32 * 256)
             _native.require().cnn_trunk_bwd(b.dy3, self.sW3, b.y2, self.sW2, b.y1, b.dy2, b.dy1, b.biasp, None,
@@ -460,36 +413,33 @@ class CNNEngine:
                                         None, None, None, 1.0, acc)
         return False
 
-    def conv1_fold_persist_ok(self, B):
-        """The persistent trunk backward of a ``B``-row batch also computes the conv1 weight gradient
-        (``EngineOpts.conv1_fold_persist``)."""
-        return (self.opts.conv1_fold_persist and self.dev.type == "cuda" and self.det_wgrad and self.implicit
-                and not self.opts.trunk_bwd_v2 and B >= self.trunk_bwd_persist_min_b and self.trunk_bwd_persist > 0)
+    def conv1_fold_ok(self, B):
+        """The persistent trunk backward of a ``B``-row batch also computes the conv1 weight gradient."""
+        return (self.dev.type == "cuda" and self.det_wgrad and self.implicit and B >= self.large_b
+                and self.trunk_bwd_persist > 0)
 
     def bias_rows(self, B):
         """Bias-gradient partial rows the trunk backward of a ``B``-row batch leaves for the finaliser: one per
-        sample, or one per workgroup of the persistent kernel (``EngineOpts.bias_rows_acc``)."""
-        if (self.opts.bias_rows_acc and not self.opts.trunk_bwd_v2 and B >= self.trunk_bwd_persist_min_b
-                and self.trunk_bwd_persist < B):
+        sample, or one per workgroup of the persistent kernel."""
+        if B >= self.large_b and self.trunk_bwd_persist < B:
             return self.trunk_bwd_persist
         return B
 
     def _wgrad_conv23(self, name, b, ws2):
         B = b.B
-        min_b = self.nhwc_wgrad_min_b
-        if not (self.det_wgrad and self.implicit and B >= min_b):
+        if not (self.det_wgrad and self.implicit and B >= self.large_b):
             if name == "W2":
                 self._wgrad("W2", self.gW2, b.dy2, 64, b.y1, 0, 64, 512, B * 81, ws2, [2, B, 32, 20, 20, 4, 4, 2])
             else:
                 self._wgrad("W3", self.gW3, b.dy3, 64, b.y2, 0, 64, 576, B * 49, ws2, [2, B, 64, 9, 9, 3, 3, 1])
             return
         n = 512 if name == "W2" else 576
-        P = max(1, min(self.nhwc_planes if name == "W2" else self.nhwc3_planes, B))
+        P = max(1, min(self.nhwc_planes, B))
         buf = self._planes.get(name)
         if buf is None or buf.numel() < P * 64 * n:
             buf = self._plane_buf(name, max(P, self.wgrad_planes) * 64 * n)
-        # batched-position MFMA 32x32x16 kernel (default) or the per-sample kernel (EngineOpts.wgrad_gemm off)
-        fn = _native.require().conv_wgrad_gemm if self.wgrad_gemm else _native.require().conv_wgrad_nhwc
+        # batched-position MFMA 32x32x16 kernel
+        fn = _native.require().conv_wgrad_gemm
         if name == "W2":
             fn(2, b.y1, b.dy2, buf, P)
         else:
@@ -499,16 +449,15 @@ class CNNEngine:
 
     def _wgrad_conv1(self, b, ws):
         B = b.B
-        if not (self.det_wgrad and self.implicit and B >= self.conv1_wgrad_min_b):
+        if not (self.det_wgrad and self.implicit and B >= self.large_b):
             self._wgrad("W1", self.gW1, b.dy1, 32, b.obs, 0, 32, 256, B * 400, ws, [1, B, 4, 84, 84, 8, 8, 4],
                         1.0 / 255.0)
             return
-        v2 = self.opts.conv1_wgrad_v2
-        P = max(1, min(self.opts.conv1_v2_planes if v2 else self.conv1_planes, B))
+        P = max(1, min(self.opts.conv1_v2_planes, B))
         buf = self._planes.get("W1")
         if buf is None or buf.numel() < P * 32 * 256:
             buf = self._plane_buf("W1", max(P, self.wgrad_planes) * 32 * 256)
-        _native.require().conv1_wgrad(b.obs, b.dy1, buf, P, 1.0 / 255.0, getattr(b, "obs_idx", None), v2)
+        _native.require().conv1_wgrad(b.obs, b.dy1, buf, P, 1.0 / 255.0, getattr(b, "obs_idx", None))
         self._wsplits["W1"] = P
         self._cur_planes["W1"] = P
 
@@ -637,7 +586,7 @@ class CNNEngine:
         main = torch.cuda.current_stream(self.dev)
         # serial_bwd: the weight-gradient products run on the compute stream too (large batches: the persistent
         # trunk backward holds every CU, and a side-stream product beside it only waits for LDS room)
-        side = main if b.B >= self.serial_bwd_min_b else self.side
+        side = main if b.B >= self.large_b else self.side
         ev = self._ev
         ws2 = self._side_ws()
         grouped = self.grouped and (head_done or stage == "trunk") and self.fused_bwd and self.det_wgrad
@@ -689,7 +638,7 @@ class CNNEngine:
 
     def big_gemm_ok(self, B):
         """The fc products of a ``B``-row learner batch run on gemm_big.hip (large tiles, LDS-DMA ring)."""
-        return self.big_ws is not None and 0 < self.opts.big_gemm_min_b <= B and B % 64 == 0
+        return self.big_ws is not None and 0 < self.large_b <= B and B % 64 == 0
 
     def _backward_grouped(self, b, stage, ws, ws2):
         """One stream, no cross-stream edges: the independent products of each stage run as ONE grouped launch
@@ -707,7 +656,7 @@ class CNNEngine:
                 buf = self._big_planes("Wfc", 2 * 3136 * 512)
                 G.gemm_big(b.y3, 3136, False, b.dh, 512, False, buf, 512, 3, 3136, 512, B, splits=2)
                 self._cur_planes["Wfc"] = 2
-            elif stage == "tail" and self.det_wgrad and self.opts.dp_tail_planes:
+            elif stage == "tail" and self.det_wgrad:
                 # data parallelism: the same two planes, summed into the slab by a finaliser launch of the fc weight
                 # alone (the bucket must be final before its all-reduce): cheaper than the in-launch split reduction
                 buf = self._big_planes("Wfc", 2 * 3136 * 512)
@@ -840,7 +789,7 @@ class CNNEngine:
                 elif want_parts:
                     segs.append((g.data_ptr(), 0, g.numel(), 0, 0))
             from ..ops.optim import finalize_jobs
-            words = finalize_jobs(segs, self.dev, return_max=True, split_planes=self.opts.fin_split)
+            words = finalize_jobs(segs, self.dev, return_max=True, split_planes=True)
             self._fin_words[key] = words
         return words
 

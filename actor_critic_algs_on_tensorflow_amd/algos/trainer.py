@@ -363,25 +363,20 @@ class ActorCriticTrainer:
         rows = (lambda t: lb.rows(t * N, N)) if lb is not None else (lambda t: b)
         _, W2, W3, frag = eng.trunk_w()   # conv2 / conv3 operands (fragment-ordered copies when kept)
         eng.forward(st.obs[0], rows(0), head=False, shift_out=st.obs[1], fc_parts=True)
-        ffc = eng.fused_fc_ok(N)   # the step also leaves the next observation's fc planes (no fc launch)
         for t in range(T):
             hp, S = eng.last_fc
             cur = rows(t)
             nxt = rows(t + 1) if t + 1 < T else b
             sn, tn, tgn, ern = env.next_state()
-            fw, fo, fcnt = eng.fused_fc_args(N) if ffc else (None, None, None)
             ops.pong_fused_step(cur.h, eng.sWh, eng.bh, cur.z, st.actions[t], st.logp[t], st.entropy[t],
                                 st.values[t], KEY_ENV_BITS, self.policy_seed, env.state, env.t, env.tg, env.ep_ret,
                                 sn, tn, tgn, ern, env.ep_stats, env.env_ids, st.obs[t], st.obs[t + 1],
                                 st.rewards[t], st.dones[t], st.truncated[t], env.seed, env.max_episode_steps, hp, S,
                                 eng.bfc, eng.sW1, eng.b1, W2, eng.b2, W3, eng.b3, nxt.y1, nxt.y2, nxt.y3,
-                                1.0 / 255.0, st.obs[t + 2] if t + 2 <= T else None, None, frag, fw, fo, fcnt)
+                                1.0 / 255.0, st.obs[t + 2] if t + 2 <= T else None, None, frag)
             env.flip()
             nxt.obs = st.obs[t + 1]
-            if ffc:
-                eng.last_fc = (fo, eng.FCF_PLANES)
-            else:
-                eng.fc_planes(nxt)
+            eng.fc_planes(nxt)
         hp, S = eng.last_fc
         self._env_flips = T
         if self._boot_in_head():

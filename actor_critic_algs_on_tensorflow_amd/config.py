@@ -12,25 +12,21 @@ from dataclasses import dataclass, field
 
 @dataclass
 class EngineOpts:
-    """Kernel selection of the native CNN engine (``algos/engine.py``). Every switch is a path that is tested and
-    measured (the A/B evidence sits next to each default in ``profiles/``); the defaults are the fastest measured
-    configuration on MI355X. ``TrainConfig.engine_opts`` carries one; plain dicts are accepted and converted."""
+    """Kernel selection of the native CNN engine (``algos/engine.py``). Every switch is a path that is the default of
+    some BASELINE config or the oracle of a test (tests/test_config_cpu.py pins the list); the defaults are the
+    fastest measured configuration on MI355X (A/B evidence in ``profiles/``). ``TrainConfig.engine_opts`` carries one;
+    plain dicts are accepted and converted."""
     # -- rollout -------------------------------------------------------------------------------------------------
-    fused_step: bool = True           # Pong bank: policy/env step t fused with the row-split trunk of obs t+1
+    fused_step: bool = True           # Pong bank: policy/env step t fused with the trunk of obs t+1 (off: oracle)
     trunk_rows_max_b: int = 64        # row-split trunk (7 workgroups per env) up to this many envs, per-env above
-    trunk_late_w: bool = True         # row-split trunk: conv2/conv3 weight fragments requested after conv1's MFMAs
     fused_env_split: bool = True      # per-env fused step (banks above trunk_rows_max_b): two workgroups per env
-    trunk_fwd_staged: bool = True     # per-env trunk forward: bytes converted once into a bf16 LDS image (mode 3)
     adam_step_offsets: bool = True    # MLP PPO: grouped Adam launches take their step from the minibatch index (no ticket)
     frag_weights: bool = True         # conv weights also kept fragment-ordered (written by the optimiser step): the
                                       # MFMA weight loads become one contiguous 1 KB read per wave
-    fused_fc: bool = False            # Pong bank of <= 32 envs: the next observation's fc product inside the fused step
-                                      # (in-launch hand-off of the conv3 rows instead of the fc launch; the hand-off
-                                      # costs as much as the boundary it removes: profiles/r5_fused_fc_ab.txt)
     fc_max_planes: int = 32           # split-K partial planes of the rollout fc product (consumer-reduced)
     fc_frag_big: int = 17             # ... for banks of 33..128 envs (+16: 32-row blocks split over workgroups)
     fc_frag: int = 5                  # rollout fc product (<= 32 envs) on a fragment-ordered Wfc copy (fc_rollout.hip
-                                      # variant 0..6; -1: the general GEMM on the row-major shadow)
+                                      # variant 0..9; -1: the general GEMM on the row-major shadow)
     # -- learner -------------------------------------------------------------------------------------------------
     a2c_head: bool = True             # A2C: V(s_T) + returns + loss + head backward in one launch (loss.hip a2c_head)
     a2c_head_env: bool = True         # ... as one workgroup per env without a grid-wide hand-off (A2C without
@@ -42,24 +38,12 @@ class EngineOpts:
     mb_index: bool = True             # PPO minibatches read their observations in place through a row index
     ppo_head: bool = True             # large-batch head: z, loss, dz, dh and dWh / dbh / dbfc planes in one launch
     fc_bwd: bool = True               # learner batches of <= 256 rows: dy3 and dWfc in one dedicated launch (fc_bwd.hip)
-    dp_tail_planes: bool = True       # DP tail stage at those sizes: dWfc as 2 planes + a finaliser launch (not in-launch)
-    big_gemm_min_b: int = 1024        # learner batches from this size run the fc products on gemm_big.hip (0: never)
-    wgrad_gemm: bool = True           # conv2/conv3 weight gradients: batched-position MFMA kernel (else per-sample)
-    serial_bwd_min_b: int = 1024      # learner batches from this size run the backward on one stream
-    conv1_wgrad_min_b: int = 1024     # per-sample conv1 weight-gradient kernel from this many rows (else GEMM)
-    nhwc_wgrad_min_b: int = 1024      # conv2/conv3 weight-gradient kernels from this many rows (else GEMM)
-    conv1_fold_persist: bool = True   # ... and in the persistent trunk backward (one plane per workgroup; dy1 not stored)
-    conv1_fold: bool = False          # learner batches below trunk_bwd_persist_min_b: the per-sample trunk backward also
-                                      # writes each sample's conv1 weight-gradient plane (no conv1 product in the wgrad launch)
-    trunk_bwd_v2: bool = False        # trunk data-gradient chain as trunk_bwd2.hip (transposed 32x32x16 MFMAs, direct epilogues)
-    trunk_bwd_persist_min_b: int = 1024   # persistent trunk backward (weights in registers) from this many rows
-    trunk_bwd_persist: int = 256      # its workgroups
-    fin_split: bool = True            # finaliser: many-plane segments as 256 / 512-element jobs split over thread groups
-    bias_rows_acc: bool = True        # ... each summing its samples' bias-gradient rows into one (finaliser: 256 rows, not B)
+    large_batch_min_b: int = 1024     # learner batches from this many rows: the persistent trunk backward (with the
+                                      # conv1 weight gradient folded in), the batched-position conv2 / conv3 weight
+                                      # gradients, gemm_big fc products, the backward on one stream
+    trunk_bwd_persist: int = 256      # workgroups of the persistent trunk backward
     wgrad_planes: int = 64            # split-K planes of the GEMM weight gradients
-    conv1_planes: int = 128           # planes of the per-sample conv1 weight gradient
-    conv1_wgrad_v2: bool = True       # ... as conv1_wgrad2 (all 4 channels per workgroup, 32x32x16 MFMAs)
-    conv1_v2_planes: int = 256        # its planes (one workgroup each)
+    conv1_v2_planes: int = 256        # planes of the conv1 weight gradient when it is not folded (one workgroup each)
     nhwc_planes: int = 256            # planes of the conv2 / conv3 weight-gradient kernels
 
     def replace(self, **kw):

@@ -386,10 +386,10 @@ def cnn_trunk_fwd(obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale=1.0 / 255.0, sh
                   copy_out=None, obs_idx=None):
     """Fused Nature-CNN conv1..conv3, activations through LDS (``cnn_fused.hip``). ``mode`` 1: seven workgroups per
     env, one per conv3 output row (its receptive field recomputed), 2: the same with the conv2 / conv3 weight loads
-    after conv1; 0: one workgroup per env, 3: per env with the frame converted to bf16 once; 5: mode 3 reading
-    fragment-ordered W1..W3 (``ops.optim.frag_order``), 6 / 7: modes 1 / 2 reading fragment-ordered W2 / W3.
+    after conv1; 3: one workgroup per env with the frame converted to bf16 once; 5: mode 3 reading fragment-ordered
+    W1..W3 (``ops.optim.frag_order``), 6 / 7: modes 1 / 2 reading fragment-ordered W2 / W3.
     ``shift_out``: also write frames 1..3 of every observation as frames 0..2 of this buffer (frame-stack shift);
-    ``copy_out`` (mode 1): also copy the whole observation there. ``obs_idx`` (int64 [B], mode 0): sample b is row
+    ``copy_out`` (mode 1): also copy the whole observation there. ``obs_idx`` (int64 [B], modes 3 / 5): sample b is row
     ``obs_idx[b]`` of ``obs`` (a PPO minibatch gathered by index)."""
     _native.require().cnn_trunk_fwd(obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, float(scale), shift_out, None,
                                     int(mode), copy_out, obs_idx)

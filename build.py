@@ -30,7 +30,7 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
 KERNELS = ["env_classic", "env_atari", "heads", "returns", "optim", "gemm", "gemm_plain", "gemm_conv", "gemm_group", "gemm_big",
            "conv", "conv_wgrad",
-           "loss", "cnn_fused", "mlp", "ppo_head", "fc_rollout", "fc_bwd", "trunk_bwd2"]
+           "loss", "cnn_fused", "mlp", "ppo_head", "fc_rollout", "fc_bwd"]
 # env kernels must round exactly like the PyTorch oracles: no fma contraction (the Pong physics carries its own
 # `fp contract(off)` pragma, so env_atari.hip compiles like cnn_fused.hip: their shared policy-head maths rounds alike)
 NO_CONTRACT = {"env_classic"}

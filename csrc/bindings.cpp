@@ -61,8 +61,7 @@ hipError_t aca_pong_fused_step(uint16_t*, const float*, int, int64_t, const floa
                                float*, float*, int32_t*, int64_t*, float*, float*, const int64_t*, const uint8_t*,
                                uint8_t*, float*, uint8_t*, uint8_t*, uint32_t, int, const uint16_t*, const float*,
                                const uint16_t*, const float*, const uint16_t*, const float*, uint16_t*, uint16_t*,
-                               uint16_t*, float, uint8_t*, uint64_t*, int, int, const uint16_t*, float*, int64_t,
-                               unsigned*, hipStream_t);
+                               uint16_t*, float, uint8_t*, uint64_t*, int, int, hipStream_t);
 hipError_t aca_pong_fused_env_step(uint16_t*, const float*, int, int64_t, const float*, const uint16_t*, const float*,
                                    int, float*, int32_t*, float*, float*, float*, int, uint32_t, float*, int32_t*,
                                    int64_t*, float*, float*, const int64_t*, uint8_t*, float*, uint8_t*, uint8_t*,
@@ -89,9 +88,7 @@ hipError_t aca_mb_gather(const uint8_t*, int64_t, const int*, const float*, cons
                          uint8_t*, int*, float*, float*, float*, float*, int, int, uint32_t, int64_t*, int, int,
                          const double*, float, unsigned int*, int64_t*, hipStream_t);
 hipError_t aca_ev_multi(const float*, const float*, float*, int, double*, unsigned int*, hipStream_t);
-hipError_t aca_conv1_wgrad(const uint8_t*, const uint16_t*, float*, int, int, float, const int64_t*, hipStream_t);
 hipError_t aca_conv1_wgrad2(const uint8_t*, const uint16_t*, float*, int, int, float, const int64_t*, hipStream_t);
-hipError_t aca_conv_wgrad_nhwc(int, const uint16_t*, const uint16_t*, float*, int, int, hipStream_t);
 hipError_t aca_conv_wgrad_gemm(int, const uint16_t*, const uint16_t*, float*, int, int, hipStream_t);
 hipError_t aca_gemm_big(const AcaGemmDesc*, hipStream_t);
 int64_t aca_gemm_big_ws(int, int, int);
@@ -119,9 +116,6 @@ hipError_t aca_ac_loss(const float*, int64_t, const float*, int64_t, const int32
                        float, uint16_t*, int64_t, uint16_t*, int64_t, float*, float*, int, int, int, int,
                        const float*, const float*, const uint8_t*, int, int, int, float, float, int, float*, float*,
                        float*, int, hipStream_t);
-hipError_t aca_cnn_trunk_fwd(const uint8_t*, const uint16_t*, const float*, const uint16_t*, const float*,
-                             const uint16_t*, const float*, uint16_t*, uint16_t*, uint16_t*, int, float, uint8_t*,
-                             uint64_t*, const int64_t*, hipStream_t);
 hipError_t aca_cnn_trunk_fwd_s16(const uint8_t*, const uint16_t*, const float*, const uint16_t*, const float*,
                                  const uint16_t*, const float*, uint16_t*, uint16_t*, uint16_t*, int, float, uint8_t*,
                                  const int64_t*, int, hipStream_t);
@@ -142,8 +136,6 @@ hipError_t aca_a2c_head(const float*, const int32_t*, const float*, const float*
 hipError_t aca_cnn_trunk_bwd(const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*,
                              uint16_t*, uint16_t*, float*, int, uint64_t*, int, const uint8_t*, const int64_t*, float*,
                              float, int, hipStream_t);
-hipError_t aca_cnn_trunk_bwd2(const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*, const uint16_t*,
-                              uint16_t*, uint16_t*, float*, int, uint64_t*, int, hipStream_t);
 hipError_t aca_cnn_trunk_rows(const uint8_t*, const uint16_t*, const float*, const uint16_t*, const float*,
                               const uint16_t*, const float*, uint16_t*, uint16_t*, uint16_t*, int, float, uint8_t*,
                               uint8_t*, uint64_t*, int, int, hipStream_t);
@@ -339,11 +331,8 @@ void pong_fused_step(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, Tenso
                      Tensor prev, Tensor out, Tensor reward, Tensor done, Tensor trunc, int64_t seed,
                      int64_t max_steps, Tensor hpart, int64_t planes, Tensor bfc, Tensor W1, Tensor b1, Tensor W2,
                      Tensor b2, Tensor W3, Tensor b3, Tensor y1, Tensor y2, Tensor y3, double scale,
-                     c10::optional<Tensor> shift_out, c10::optional<Tensor> stamps, bool frag,
-                     c10::optional<Tensor> fc_w, c10::optional<Tensor> fc_out, c10::optional<Tensor> fc_cnt) {
+                     c10::optional<Tensor> shift_out, c10::optional<Tensor> stamps, bool frag) {
   // frag: W2 / W3 are the fragment-ordered copies (ops/optim.py frag_order); W1 row-major
-  // fc_w / fc_out / fc_cnt: the next observation's fc product in the same launch (fragment-ordered Wfc, 14 partial
-  // planes into fc_out, the slice counters + timeout word: int32 [232], zero-initialised)
   check_env(state, t, tg, ep_ret, ep_stats, ids, reward, done, trunc);
   check_env(state_n, t_n, tg_n, ep_ret_n, ep_stats, ids, reward, done, trunc);
   for (auto* x : {&h, &Wh, &W1, &W2, &W3, &y1, &y2, &y3}) need(*x, at::kBFloat16, "pong_fused_step bf16");
@@ -379,27 +368,6 @@ void pong_fused_step(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, Tenso
                     shift_out->data_ptr() != out.data_ptr(), "pong_fused_step: shift_out shape / aliasing");
     so = shift_out->data_ptr<uint8_t>();
   }
-  const uint16_t* fcw = nullptr;
-  float* fco = nullptr;
-  int64_t fcs = 0;
-  unsigned* fcc = nullptr;
-  if (fc_w.has_value() && fc_w->defined()) {
-    TORCH_CHECK(frag && N <= 32, "pong_fused_step: the fused fc product needs the fragment copies and <= 32 envs");
-    TORCH_CHECK(fc_out.has_value() && fc_out->defined() && fc_cnt.has_value() && fc_cnt->defined(),
-                "pong_fused_step: fc_w needs fc_out and fc_cnt");
-    need(*fc_w, at::kBFloat16, "fc_w");
-    need(*fc_out, at::kFloat, "fc_out");
-    need(*fc_cnt, at::kInt, "fc_cnt");
-    TORCH_CHECK(fc_w->numel() == 3136 * 512 && fc_w->is_contiguous(), "pong_fused_step: fc_w = [3136 x 512] copy");
-    TORCH_CHECK(fc_out->numel() % 32 == 0 && fc_out->numel() / 32 >= (int64_t)N * 512 &&
-                    fc_out->data_ptr() != hpart.data_ptr(), "pong_fused_step: fc_out = 32 planes, not hpart");
-    TORCH_CHECK(fc_cnt->numel() >= 232, "pong_fused_step: fc_cnt needs 232 words");
-    TORCH_CHECK(y3.is_contiguous(), "pong_fused_step: y3 contiguous");
-    fcw = ptr<uint16_t>(*fc_w);
-    fco = ptr<float>(*fc_out);
-    fcs = fc_out->numel() / 32;
-    fcc = reinterpret_cast<unsigned*>(fc_cnt->data_ptr<int32_t>());
-  }
   check(aca_pong_fused_step(ptr<uint16_t>(h), ptr<float>(hpart), (int)planes, pstride, ptr<float>(bfc),
                             ptr<uint16_t>(Wh), ptr<float>(bh), A, ptr<float>(z), ptr<int32_t>(act), ptr<float>(logp),
                             ptr<float>(ent), ptr<float>(value), (int)key_shift, (uint32_t)pseed, ptr<float>(state),
@@ -409,7 +377,7 @@ void pong_fused_step(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, Tenso
                             ptr<uint8_t>(done), ptr<uint8_t>(trunc), (uint32_t)seed, (int)max_steps,
                             ptr<uint16_t>(W1), ptr<float>(b1), ptr<uint16_t>(W2), ptr<float>(b2), ptr<uint16_t>(W3),
                             ptr<float>(b3), ptr<uint16_t>(y1), ptr<uint16_t>(y2), ptr<uint16_t>(y3), (float)scale,
-                            so, stamps_ptr(stamps, N * 7), frag ? 1 : 0, N, fcw, fco, fcs, fcc, cur_stream(state)),
+                            so, stamps_ptr(stamps, N * 7), frag ? 1 : 0, N, cur_stream(state)),
         "pong_fused_step");
 }
 
@@ -709,9 +677,8 @@ void returns_scan(Tensor r, Tensor v, Tensor d, Tensor ret, Tensor adv, int64_t 
 // conv1 weight gradient as P partial planes [P][32][256] (conv_wgrad.hip): obs uint8 [B, 4, 84, 84], dy1 bf16
 // [B * 400, 32]; plane g holds samples [g B / P, (g + 1) B / P).
 // obs_idx (optional int64 [B]): sample b's frames are row obs_idx[b] of obs (a PPO minibatch gathered by index)
-// v2: conv1_wgrad2_kernel (all four channels per workgroup, 32x32x16 MFMAs; grid P instead of 4 P)
-void conv1_wgrad(Tensor obs, Tensor dy1, Tensor planes, int64_t P, double scale, c10::optional<Tensor> obs_idx,
-                 bool v2) {
+// (conv1_wgrad2_kernel: all four channels per workgroup, 32x32x16 MFMAs, grid P)
+void conv1_wgrad(Tensor obs, Tensor dy1, Tensor planes, int64_t P, double scale, c10::optional<Tensor> obs_idx) {
   TORCH_CHECK(obs.is_cuda() && obs.is_contiguous() && obs.scalar_type() == at::kByte, "conv1_wgrad: obs uint8");
   need(dy1, at::kBFloat16, "conv1_wgrad dy1");
   need(planes, at::kFloat, "conv1_wgrad planes");
@@ -728,32 +695,14 @@ void conv1_wgrad(Tensor obs, Tensor dy1, Tensor planes, int64_t P, double scale,
   TORCH_CHECK(P >= 1 && P <= 1024 && planes.numel() >= P * 32 * 256, "conv1_wgrad: planes too small");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(obs.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(dy1.data_ptr()) % 16 == 0,
               "conv1_wgrad: 16-byte aligned operands");
-  check((v2 ? aca_conv1_wgrad2 : aca_conv1_wgrad)(obs.data_ptr<uint8_t>(), ptr<uint16_t>(dy1), ptr<float>(planes),
-                                                  (int)B, (int)P, (float)scale, idx, cur_stream(obs)),
+  check(aca_conv1_wgrad2(obs.data_ptr<uint8_t>(), ptr<uint16_t>(dy1), ptr<float>(planes), (int)B, (int)P,
+                         (float)scale, idx, cur_stream(obs)),
         "conv1_wgrad");
 }
 
-// conv2 / conv3 weight gradient as P partial planes [P][64][KS KS C] (conv_wgrad.hip conv_wgrad_nhwc_kernel):
-// layer 2: img = y1 [B * 400, 32], dy = dy2 [B * 81, 64]; layer 3: img = y2 [B * 81, 64], dy = dy3 [B * 49, 64].
-void conv_wgrad_nhwc(int64_t layer, Tensor img, Tensor dy, Tensor planes, int64_t P) {
-  need(img, at::kBFloat16, "conv_wgrad_nhwc img");
-  need(dy, at::kBFloat16, "conv_wgrad_nhwc dy");
-  need(planes, at::kFloat, "conv_wgrad_nhwc planes");
-  TORCH_CHECK(layer == 2 || layer == 3, "conv_wgrad_nhwc: layer 2 or 3");
-  const int64_t img_per = layer == 2 ? 400 * 32 : 81 * 64, dy_per = layer == 2 ? 81 * 64 : 49 * 64;
-  const int64_t ncol = layer == 2 ? 512 : 576;
-  const int64_t B = dy.numel() / dy_per;
-  TORCH_CHECK(B >= 1 && dy.numel() == B * dy_per && img.numel() == B * img_per, "conv_wgrad_nhwc: shapes");
-  TORCH_CHECK(P >= 1 && P <= 1024 && planes.numel() >= P * 64 * ncol, "conv_wgrad_nhwc: planes too small");
-  TORCH_CHECK(reinterpret_cast<uintptr_t>(img.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(dy.data_ptr()) % 16 == 0,
-              "conv_wgrad_nhwc: 16-byte aligned operands");
-  check(aca_conv_wgrad_nhwc((int)layer, ptr<uint16_t>(img), ptr<uint16_t>(dy), ptr<float>(planes), (int)B, (int)P,
-                            cur_stream(img)),
-        "conv_wgrad_nhwc");
-}
-
-// Same planes from the batched-position MFMA 32x32x16 kernel (conv_wgrad.hip conv_wgrad_gemm_kernel): grid P, every
-// workgroup owns its whole plane.
+// conv2 / conv3 weight gradient as P partial planes [P][64][KS KS C] from the batched-position MFMA 32x32x16 kernel
+// (conv_wgrad.hip conv_wgrad_gemm_kernel): grid P, every workgroup owns its whole plane. layer 2: img = y1
+// [B * 400, 32], dy = dy2 [B * 81, 64]; layer 3: img = y2 [B * 81, 64], dy = dy3 [B * 49, 64].
 void conv_wgrad_gemm(int64_t layer, Tensor img, Tensor dy, Tensor planes, int64_t P) {
   need(img, at::kBFloat16, "conv_wgrad_gemm img");
   need(dy, at::kBFloat16, "conv_wgrad_gemm dy");
@@ -1597,9 +1546,9 @@ void cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tenso
   TORCH_CHECK(obs.numel() % (4 * 84 * 84) == 0, "cnn_trunk_fwd: obs must be [B, 4, 84, 84]");
   int64_t B = obs.numel() / (4 * 84 * 84);
   const int64_t* idxp = nullptr;
-  if (obs_idx.has_value() && obs_idx->defined()) {   // sample b = row obs_idx[b] of obs (per-env mode 0 only)
+  if (obs_idx.has_value() && obs_idx->defined()) {   // sample b = row obs_idx[b] of obs (per-env modes 3 / 5)
     need(*obs_idx, at::kLong, "obs_idx");
-    TORCH_CHECK(mode == 0 || mode == 3 || mode == 5, "cnn_trunk_fwd: obs_idx needs a per-env mode");
+    TORCH_CHECK(mode == 3 || mode == 5, "cnn_trunk_fwd: obs_idx needs a per-env mode");
     B = obs_idx->numel();
     idxp = obs_idx->data_ptr<int64_t>();
   }
@@ -1647,11 +1596,7 @@ void cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tenso
           "cnn_trunk_fwd_s16");
     return;
   }
-  TORCH_CHECK(mode == 0, "cnn_trunk_fwd: mode must be 0..3 or 5..7");
-  check(aca_cnn_trunk_fwd(ptr<uint8_t>(obs), ptr<uint16_t>(W1), ptr<float>(b1), ptr<uint16_t>(W2), ptr<float>(b2),
-                          ptr<uint16_t>(W3), ptr<float>(b3), ptr<uint16_t>(y1), ptr<uint16_t>(y2), ptr<uint16_t>(y3),
-                          (int)B, (float)scale, so, stamps_ptr(stamps, B), idxp, cur_stream(obs)),
-        "cnn_trunk_fwd");
+  TORCH_CHECK(false, "cnn_trunk_fwd: mode must be 1, 2, 3, 5, 6 or 7");
 }
 
 // Fused data-gradient chain dy3 -> dy2 -> dy1 of the Nature-CNN trunk, one workgroup per sample
@@ -1703,25 +1648,6 @@ void cnn_trunk_bwd(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tenso
                           stamps_ptr(stamps, B), (int)persist, wo, wi, wp, (float)w1_scale, bias_acc ? 1 : 0,
                           cur_stream(dy3)),
         "cnn_trunk_bwd");
-}
-
-// v2 of the fused data-gradient chain (trunk_bwd2.hip: 32x32x16 MFMAs, register blocking, weights staged once per
-// workgroup); max_wg > 0: at most that many workgroups walking the samples, else one per sample
-void cnn_trunk_bwd2(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tensor dy2, Tensor dy1, Tensor biasp,
-                    c10::optional<Tensor> stamps, int64_t max_wg) {
-  for (auto* t : {&dy3, &W3, &y2, &W2, &y1, &dy2, &dy1}) need(*t, at::kBFloat16, "trunk_bwd2 bf16 operand");
-  need(biasp, at::kFloat, "biasp");
-  TORCH_CHECK(dy3.numel() % (49 * 64) == 0, "cnn_trunk_bwd2: dy3 must be [B*49, 64]");
-  const int64_t B = dy3.numel() / (49 * 64);
-  TORCH_CHECK(W3.numel() == 64 * 576 && W2.numel() == 64 * 512, "cnn_trunk_bwd2: weights must be conv3 / conv2");
-  TORCH_CHECK(y2.numel() >= B * 81 * 64 && y1.numel() >= B * 400 * 32 && dy2.numel() >= B * 81 * 64 &&
-                  dy1.numel() >= B * 400 * 32 && biasp.numel() >= B * 160,
-              "cnn_trunk_bwd2: buffers too small");
-  const int64_t grid = max_wg > 0 && max_wg < B ? max_wg : B;
-  check(aca_cnn_trunk_bwd2(ptr<uint16_t>(dy3), ptr<uint16_t>(W3), ptr<uint16_t>(y2), ptr<uint16_t>(W2),
-                           ptr<uint16_t>(y1), ptr<uint16_t>(dy2), ptr<uint16_t>(dy1), ptr<float>(biasp), (int)B,
-                           stamps_ptr(stamps, grid), (int)max_wg, cur_stream(dy3)),
-        "cnn_trunk_bwd2");
 }
 
 // Gradient finaliser (optim.hip grad_finalize_kernel): jobs = device int64 [njobs, 8] (dst, src, n, stride, S,
@@ -2035,8 +1961,7 @@ TORCH_LIBRARY(acamd, m) {
         "Tensor t_n, Tensor tg_n, Tensor ep_ret_n, Tensor ep_stats, Tensor env_ids, Tensor prev, Tensor out, "
         "Tensor reward, Tensor done, Tensor truncated, int seed, int max_steps, Tensor hpart, int planes, "
         "Tensor bfc, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, Tensor y1, Tensor y2, "
-        "Tensor y3, float scale, Tensor? shift_out=None, Tensor? stamps=None, bool frag=False, Tensor? fc_w=None, "
-        "Tensor? fc_out=None, Tensor? fc_cnt=None) -> ()");
+        "Tensor y3, float scale, Tensor? shift_out=None, Tensor? stamps=None, bool frag=False) -> ()");
   m.def("pong_fused_env_step(Tensor h, Tensor Wh, Tensor bh, Tensor z, Tensor act, Tensor logp, Tensor ent, "
         "Tensor value, int key_shift, int pseed, Tensor state, Tensor t, Tensor tg, Tensor ep_ret, Tensor ep_stats, "
         "Tensor env_ids, Tensor out, Tensor reward, Tensor done, Tensor truncated, int seed, int max_steps, "
@@ -2056,9 +1981,7 @@ TORCH_LIBRARY(acamd, m) {
   m.def("gemm_group_begin() -> ()", &gemm_group_begin);
   m.def("gemm_group_end() -> int", &gemm_group_end);
   m.def("gemm_group_pause(bool paused) -> ()", &gemm_group_pause);
-  m.def("conv1_wgrad(Tensor obs, Tensor dy1, Tensor planes, int P, float scale, Tensor? obs_idx=None, "
-        "bool v2=False) -> ()");
-  m.def("conv_wgrad_nhwc(int layer, Tensor img, Tensor dy, Tensor planes, int P) -> ()");
+  m.def("conv1_wgrad(Tensor obs, Tensor dy1, Tensor planes, int P, float scale, Tensor? obs_idx=None) -> ()");
   m.def("conv_wgrad_gemm(int layer, Tensor img, Tensor dy, Tensor planes, int P) -> ()");
   m.def("mb_gather(Tensor obs, Tensor act, Tensor logp, Tensor adv, Tensor ret, Tensor v, Tensor? o_obs, "
         "Tensor o_act, Tensor o_logp, Tensor o_adv, Tensor o_ret, Tensor o_v, int seed, Tensor uc, int ep, "
@@ -2108,13 +2031,11 @@ TORCH_LIBRARY(acamd, m) {
   m.def("seg_stats(Tensor x, Tensor segs, Tensor out) -> ()");
   m.def("gemm_effective_splits(int K, int bk, int splits) -> int", &gemm_effective_splits);
   m.def("cnn_trunk_fwd(Tensor obs, Tensor W1, Tensor b1, Tensor W2, Tensor b2, Tensor W3, Tensor b3, Tensor y1, "
-        "Tensor y2, Tensor y3, float scale, Tensor? shift_out=None, Tensor? stamps=None, int mode=0, "
+        "Tensor y2, Tensor y3, float scale, Tensor? shift_out=None, Tensor? stamps=None, int mode=3, "
         "Tensor? copy_out=None, Tensor? obs_idx=None) -> ()");
   m.def("cnn_trunk_bwd(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tensor dy2, Tensor dy1, "
         "Tensor biasp, Tensor? stamps=None, int persist=0, Tensor? w1_obs=None, Tensor? w1_obs_idx=None, "
         "Tensor? w1_planes=None, float w1_scale=1.0, bool bias_acc=False, bool skip_dy1=False) -> ()");
-  m.def("cnn_trunk_bwd2(Tensor dy3, Tensor W3, Tensor y2, Tensor W2, Tensor y1, Tensor dy2, Tensor dy1, "
-        "Tensor biasp, Tensor? stamps=None, int max_wg=0) -> ()");
   m.def("grad_finalize(Tensor jobs, Tensor partial, Tensor? spart=None, int B=0, Tensor? ent_coef=None, "
         "Tensor? kl_coef=None, Tensor? stats=None) -> ()");
   m.def("a2c_head_env(Tensor z, Tensor act, Tensor logp_old, Tensor ent_coef, Tensor kl_coef, float vf_coef, "
@@ -2169,7 +2090,6 @@ TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
   m.impl("normalize_mom", &normalize_mom);
   m.impl("mb_gather", &mb_gather);
   m.impl("conv1_wgrad", &conv1_wgrad);
-  m.impl("conv_wgrad_nhwc", &conv_wgrad_nhwc);
   m.impl("conv_wgrad_gemm", &conv_wgrad_gemm);
   m.impl("moments", &moments);
   m.impl("sumsq", &sumsq);
@@ -2191,7 +2111,6 @@ TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
   m.impl("fc_rollout", &fc_rollout);
   m.impl("fc_bwd", &fc_bwd);
   m.impl("cnn_trunk_bwd", &cnn_trunk_bwd);
-  m.impl("cnn_trunk_bwd2", &cnn_trunk_bwd2);
   m.impl("grad_finalize", &grad_finalize);
   m.impl("a2c_head_env", &a2c_head_env);
   m.impl("ppo_head", &ppo_head);

@@ -51,183 +51,6 @@ __device__ __forceinline__ void stamp(uint64_t* st, int slot) {
   if (st && threadIdx.x == 0) st[(size_t)blockIdx.x * 16 + slot] = __builtin_amdgcn_s_memrealtime();
 }
 
-__global__ void __launch_bounds__(T_THREADS) cnn_trunk_fwd_kernel(
-    const uint8_t* __restrict__ obs, const u16* __restrict__ W1, const float* __restrict__ b1,
-    const u16* __restrict__ W2, const float* __restrict__ b2, const u16* __restrict__ W3,
-    const float* __restrict__ b3, u16* __restrict__ y1g, u16* __restrict__ y2g, u16* __restrict__ y3g,
-    float scale, uint8_t* __restrict__ shift_out, uint64_t* __restrict__ stamps) {
-  __shared__ __attribute__((aligned(16))) u16 s_obs[OBS_BYTES];
-  __shared__ __attribute__((aligned(16))) u16 s_w1[32 * W1_LD];
-  __shared__ __attribute__((aligned(16))) u16 s_y1[Y1_ROWS * Y1_LD];
-  __shared__ __attribute__((aligned(16))) u16 s_y2[Y2_ROWS * Y2_LD];
-
-  const int e = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int l16 = lane & 15, lg = lane >> 4;
-
-  // ---------------------------------------------------------------- stage obs + W1 in LDS (16-byte copies)
-  stamp(stamps, 0);
-  const int n2 = wid * 16 + l16;
-  bf16x8 bw2[16];
-  // every staging load of a thread is issued before its first LDS store (11 x 16 B in flight): one round trip
-  {
-    constexpr int OBS_CH = OBS_BYTES / 16, OBS_PER = (OBS_CH + T_THREADS - 1) / T_THREADS;   // 1764 -> 7
-    constexpr int W1_PER = 32 * 256 / 8 / T_THREADS;                                         // 4
-    const uint4* src = reinterpret_cast<const uint4*>(obs + (size_t)e * OBS_BYTES);
-    uint4 vo[OBS_PER], vw[W1_PER];
-#pragma unroll
-    for (int u = 0; u < OBS_PER; ++u)
-      if (tid + u * T_THREADS < OBS_CH) vo[u] = src[tid + u * T_THREADS];
-#pragma unroll
-    for (int u = 0; u < W1_PER; ++u) vw[u] = reinterpret_cast<const uint4*>(W1)[tid + u * T_THREADS];
-    // W2 B fragments for conv2 (wave w owns output-channel tile w): issued behind the staging loads (returns are
-    // in order, so the staging wait does not cover them), consumed two phases later
-#pragma unroll
-    for (int ks = 0; ks < 16; ++ks) bw2[ks] = *reinterpret_cast<const bf16x8*>(W2 + n2 * 512 + ks * 32 + lg * 8);
-    uint4* dst = reinterpret_cast<uint4*>(s_obs);
-#pragma unroll
-    for (int u = 0; u < OBS_PER; ++u) {
-      const int i = tid + u * T_THREADS;
-      if (i < OBS_CH) {
-        const uint2 a = u8x4_to_bf16(vo[u].x), b = u8x4_to_bf16(vo[u].y);
-        const uint2 c = u8x4_to_bf16(vo[u].z), d = u8x4_to_bf16(vo[u].w);
-        dst[2 * i] = make_uint4(a.x, a.y, b.x, b.y);
-        dst[2 * i + 1] = make_uint4(c.x, c.y, d.x, d.y);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < W1_PER; ++u) {
-      const int i = tid + u * T_THREADS, r = i / 32, c8 = (i % 32) * 8;
-      *reinterpret_cast<uint4*>(s_w1 + r * W1_LD + c8) = vw[u];
-    }
-    __syncthreads();
-    stamp(stamps, 1);
-    if (shift_out) {
-      // rollout: the next observation's frame stack starts with frames 1..3 of this one (the env step then only
-      // renders the newest frame): the bytes are still in registers; the stores drain behind conv1
-      uint4* so = reinterpret_cast<uint4*>(shift_out + (size_t)e * OBS_BYTES);
-#pragma unroll
-      for (int u = 0; u < OBS_PER; ++u) {
-        const int i = tid + u * T_THREADS;
-        if (i >= OBS_CH / 4 && i < OBS_CH) so[i - OBS_CH / 4] = vo[u];
-      }
-    }
-  }
-
-  // ---------------------------------------------------------------- conv1: M 400 (25 tiles), N 32 (2), K 256 (8)
-  {
-    bf16x8 bw[2][8];
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-      for (int ks = 0; ks < 8; ++ks)
-        bw[nt][ks] = *reinterpret_cast<const bf16x8*>(s_w1 + (nt * 16 + l16) * W1_LD + ks * 32 + lg * 8);
-    const float bias0 = b1[l16], bias1 = b1[16 + l16];
-    for (int mt = wid; mt < 25; mt += 4) {
-      floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-      const int m = mt * 16 + l16;
-      const int oh = m / 20, ow = m - oh * 20;
-#pragma unroll
-      for (int ks = 0; ks < 8; ++ks) {
-        const int k = ks * 32 + lg * 8;             // (c, i, j0 = 0): c = k / 64, i = (k / 8) % 8
-        const int c = k >> 6, i = (k >> 3) & 7;
-        const u16* p = s_obs + (c * 84 + oh * 4 + i) * 84 + ow * 4;   // 8-byte aligned
-        const uint2 lo = *reinterpret_cast<const uint2*>(p), hi = *reinterpret_cast<const uint2*>(p + 4);
-        const bf16x8 a = __builtin_bit_cast(bf16x8, make_uint4(lo.x, lo.y, hi.x, hi.y));
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw[0][ks], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw[1][ks], acc1, 0, 0, 0);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = mt * 16 + lg * 4 + r;
-        const u16 v0 = f2bf(fmaxf(acc0[r] * scale + bias0, 0.f));
-        const u16 v1 = f2bf(fmaxf(acc1[r] * scale + bias1, 0.f));
-        s_y1[row * Y1_LD + l16] = v0;
-        s_y1[row * Y1_LD + 16 + l16] = v1;
-        y1g[((size_t)e * Y1_ROWS + row) * Y1_C + l16] = v0;
-        y1g[((size_t)e * Y1_ROWS + row) * Y1_C + 16 + l16] = v1;
-      }
-    }
-  }
-  __syncthreads();
-
-  stamp(stamps, 2);
-  // W3 B fragments, issued before conv2's MFMAs
-  bf16x8 bw3[18];
-#pragma unroll
-  for (int ks = 0; ks < 18; ++ks) bw3[ks] = *reinterpret_cast<const bf16x8*>(W3 + n2 * 576 + ks * 32 + lg * 8);
-  // ---------------------------------------------------------------- conv2: M 81 (6 tiles), N 64 (wave = N tile), K 512
-  {
-    const int n = n2;
-    const float bias = b2[n];
-    floatx4 acc[6];
-#pragma unroll
-    for (int mt = 0; mt < 6; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < 16; ++ks) {
-      const int k = ks * 32 + lg * 8;   // (i, j, c0): i = k / 128, j = (k / 32) % 4, c0 = k % 32
-      const int i = k >> 7, j = (k >> 5) & 3, c0 = k & 31;
-#pragma unroll
-      for (int mt = 0; mt < 6; ++mt) {
-        // rows past the 81 outputs are computed on a clamped (valid) pixel and never stored: no branch, so all
-        // 96 fragment reads of the layer stay in flight together
-        const int m = min(mt * 16 + l16, Y2_ROWS - 1);
-        const int oh = m / 9, ow = m - oh * 9;
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(s_y1 + ((oh * 2 + i) * 20 + ow * 2 + j) * Y1_LD + c0);
-        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw2[ks], acc[mt], 0, 0, 0);
-      }
-    }
-#pragma unroll
-    for (int mt = 0; mt < 6; ++mt) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = mt * 16 + lg * 4 + r;
-        if (row < Y2_ROWS) {
-          const u16 v = f2bf(fmaxf(acc[mt][r] + bias, 0.f));
-          s_y2[row * Y2_LD + n] = v;
-          y2g[((size_t)e * Y2_ROWS + row) * Y2_C + n] = v;
-        }
-      }
-    }
-  }
-  __syncthreads();
-
-  stamp(stamps, 3);
-  // ---------------------------------------------------------------- conv3: M 49 (4 tiles), N 64 (wave = N tile), K 576
-  {
-    const int n = n2;
-    const float bias = b3[n];
-    floatx4 acc[4];
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) acc[mt] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < 18; ++ks) {
-      const int k = ks * 32 + lg * 8;   // (i, j, c0): i = k / 192, j = (k / 64) % 3, c0 = k % 64
-      const int i = k / 192, j = (k >> 6) % 3, c0 = k & 63;
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        const int m = min(mt * 16 + l16, Y3_ROWS - 1);
-        const int oh = m / 7, ow = m - oh * 7;
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(s_y2 + ((oh + i) * 9 + ow + j) * Y2_LD + c0);
-        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw3[ks], acc[mt], 0, 0, 0);
-      }
-    }
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = mt * 16 + lg * 4 + r;
-        if (row < Y3_ROWS) y3g[((size_t)e * Y3_ROWS + row) * Y3_C + n] = f2bf(fmaxf(acc[mt][r] + bias, 0.f));
-      }
-    }
-  }
-  if (stamps) {
-    stamp(stamps, 4);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    stamp(stamps, 5);
-  }
-}
-
 // ------------------------------------------------------------------------------------------------------------
 // One observation copied global -> LDS by the LDS-DMA path (global_load_lds_dwordx4: no registers, tracked by the vm
 // counter), padded to whole 1 KB wave copies.
@@ -508,37 +331,8 @@ __device__ __forceinline__ void w1_frags_from_lds(const u16* __restrict__ s_w, b
     }
 }
 
-__global__ void __launch_bounds__(256) cnn_trunk_fwd_u8_kernel(
-    const uint8_t* __restrict__ obs, const u16* __restrict__ W1, const float* __restrict__ b1,
-    const u16* __restrict__ W2, const float* __restrict__ b2, const u16* __restrict__ W3,
-    const float* __restrict__ b3, u16* __restrict__ y1g, u16* __restrict__ y2g, u16* __restrict__ y3g,
-    float scale, uint8_t* __restrict__ shift_out, const int64_t* __restrict__ obs_idx) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_obs8[TP_OBS_PAD];   // later the y2 image
-  __shared__ __attribute__((aligned(16))) u16 s_y1[E1_ELEMS];
-  u16* const s_y2 = reinterpret_cast<u16*>(s_obs8);
-  const int e = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int l16 = lane & 15;
-  const int n2 = wid * 16 + l16;
-  // loads in the order they are consumed (the vm counter retires in issue order): frames (LDS-DMA), conv1
-  // fragments, conv2 fragments; conv3's after conv1
-  // obs_idx (PPO minibatch in index mode): sample e is row obs_idx[e] of the rollout's observations
-  trunk_obs_dma(obs + (size_t)(obs_idx ? obs_idx[e] : e) * OBS_BYTES, s_obs8);
-  bf16x8 bw[2][8], bw2[16];
-  trunk_env_w12(W1, W2, bw, bw2);
-  const float bias0 = b1[l16], bias1 = b1[16 + l16], bias2 = b2[n2], bias3 = b3[n2];
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (shift_out) {   // rollout: frames 1..3 of this observation become frames 0..2 of the next one
-    uint4* so = reinterpret_cast<uint4*>(shift_out + (size_t)e * OBS_BYTES);
-    const uint4* si = reinterpret_cast<const uint4*>(s_obs8);
-    for (int i = OBS_BYTES / 64 + tid; i < OBS_BYTES / 16; i += 256) so[i - OBS_BYTES / 64] = si[i];
-  }
-  trunk_env_convs<-1>(s_obs8, s_y1, s_y2, e, bw, bw2, W3, bias0, bias1, bias2, bias3, y1g, y2g, y3g, scale);
-}
-
 // ------------------------------------------------------------------------------------------------------------
-// Per-env trunk, bf16-staged form (the learner's minibatch forward): the lean form above converts every observation
+// Per-env trunk, bf16-staged form (the learner's minibatch forward): a lean form (retired) converted every observation
 // byte to bf16 in conv1's inner loop, ~3.6 times per byte (the 8x8 / stride-4 windows overlap) -- conv1 is then
 // vector-issue bound (2.4k VALU vs 0.27k MFMA instructions per wave, profiles/r4_trunk_mix.txt). Here the bytes are
 // converted ONCE into a bf16 image (56 KB: still two workgroups per CU), conv1's outputs wait in registers until
@@ -737,7 +531,7 @@ __device__ __forceinline__ void trunk_rows_compute(const u16* __restrict__ s_in,
                                                    const u16* __restrict__ W3, u16* __restrict__ y1g,
                                                    u16* __restrict__ y2g, u16* __restrict__ y3g, float scale,
                                                    uint64_t* __restrict__ stamps, bf16x8 (&bw2)[16],
-                                                   bf16x8 (&bw3)[18], u16* __restrict__ s_y3 = nullptr) {
+                                                   bf16x8 (&bw3)[18]) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int l16 = lane & 15, lg = lane >> 4;
   const int n2 = wid * 16 + l16;
@@ -871,10 +665,7 @@ __device__ __forceinline__ void trunk_rows_compute(const u16* __restrict__ s_in,
     for (int q = 0; q < 4; ++q) {
       const int row = lg * 4 + q;
       const u16 v = f2bf(fmaxf(acc[q] + bias, 0.f));
-      if (row < 7) {   // s_y3: the caller publishes the row itself (fused fc product)
-        if (s_y3) s_y3[row * Y3_C + n] = v;
-        else y3g[((size_t)e * Y3_ROWS + r * 7 + row) * Y3_C + n] = v;
-      }
+      if (row < 7) y3g[((size_t)e * Y3_ROWS + r * 7 + row) * Y3_C + n] = v;
     }
   }
   // ---------------------------------------------------------------- owned y1 / y2 rows: LDS -> global, 16-byte rows
@@ -991,106 +782,6 @@ __global__ void __launch_bounds__(T_THREADS) cnn_trunk_rows_kernel(
 //   kernel boundary less per rollout step than policy/env kernel + trunk kernel, and the new frame never makes a
 //   global round trip before conv1.
 // ------------------------------------------------------------------------------------------------------------
-// ------------------------------------------------------------------------------------------------------------
-// The next observation's fc product inside the fused step (banks of at most 32 envs, one MFMA row block): slice r
-// of the product = conv3 output row r = K range [448 r, 448 r + 448) of h = y3 Wfc. Every (env, r) workgroup
-// publishes its y3 row write-through (16-byte sc1 stores, every storing wave drained, then one relaxed agent-scope
-// add on slice r's arrival counter: cdna_hip_programming.md Guideline 16, valid-forms row 1) and waits for the N
-// arrivals of its slice (one polling lane, bounded: a timeout sets the sticky word and the health check reports
-// it). The slice's 32 units -- 16 column blocks of 32 x 2 K halves of 224 -- go to its N workgroups round-robin
-// (unit u = env, env + N, ...); wave w owns the 16 x 16 quadrant (envs 16 (w >> 1).., columns 16 (w & 1)..) of a
-// unit: 7 MFMA 16x16x32 steps, A = the published rows (sc1 loads only), B = the fragment-ordered Wfc
-// (ops/optim.py frag_order_kc, requested before the wait). Unit (nb, kh) of slice r stores its partial sums into
-// plane 2 r + kh: 14 planes, summed in plane order by the consumer (FcH2), so the product is deterministic. This
-// replaces the separate fc_rollout launch (its kernel boundary and its operand round trip) after every step.
-// ------------------------------------------------------------------------------------------------------------
-struct FcFuse {
-  const u16* Wf;     // fragment-ordered Wfc copy (k-contiguous B fragments)
-  float* out;        // partial planes [14][pstride] (row e of a plane at e * 512)
-  int64_t pstride;
-  unsigned* cnt;     // per slice r: arrivals at [32 r], departures at [32 r + 16] (own 64-byte lines); word 224:
-                     // the sticky timeout flag. Zero at the first launch; the last departure re-arms the slice.
-};
-constexpr int FCF_PLANES = 2 * TR_ROWS;
-constexpr unsigned FCF_SPIN_LIMIT = 1u << 21;
-
-__device__ __forceinline__ void fc_fused_tail(const FcFuse& f, const u16* __restrict__ s_y3, u16* __restrict__ y3g,
-                                              int e, int r, int N, uint64_t* __restrict__ stamps) {
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, l16 = lane & 15, lg = lane >> 4;
-  constexpr int SC1 = 16;   // buffer instruction cache-policy bits: sc1 (write-through stores, L1-bypassing loads)
-  const int ybytes = N * Y3_ROWS * Y3_C * 2;
-  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(y3g, 0, ybytes, 0x00020000);
-  __syncthreads();   // the conv3 row is complete in LDS
-  if (tid < 56) {    // y3 row r of env e: 7 x 64 bf16 = 56 x 16 bytes
-    const uint4 v = reinterpret_cast<const uint4*>(s_y3)[tid];
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    const int off = ((e * Y3_ROWS + r * 7) * Y3_C + tid * 8) * 2;
-    __builtin_amdgcn_raw_buffer_store_b128(u32x4{v.x, v.y, v.z, v.w}, yr, off, 0, SC1);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drained
-  __syncthreads();
-  unsigned* arr = f.cnt + 32 * r;
-  if (tid == 0) __hip_atomic_fetch_add(arr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  stamp(stamps, 11);
-  // this workgroup's first unit: the B fragments do not depend on the hand-off
-  const int mq = wid >> 1, nq = wid & 1;
-  const bool active = 16 * mq < N;
-  bf16x8 bq[7];
-  auto load_b = [&](int u) {
-    const int nb = u >> 1, kh = u & 1;
-#pragma unroll
-    for (int s = 0; s < 7; ++s) {
-      const int kk = 448 * r + 224 * kh + 32 * s + 8 * lg;
-      const int kb = kk >> 4, half = (kk >> 3) & 1;
-      bq[s] = *reinterpret_cast<const bf16x8*>(f.Wf + ((size_t)((kb * 16 + nb) * 64 + half * 32 + nq * 16 + l16)) * 8);
-    }
-  };
-  if (active) load_b(e);
-  if (tid == 0) {
-    unsigned spins = 0;
-    while (__hip_atomic_load(arr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)N) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > FCF_SPIN_LIMIT) {
-        __hip_atomic_store(f.cnt + 32 * TR_ROWS, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-    // departure: the last workgroup of the slice past the wait re-arms it for the next launch (stream-ordered)
-    if (__hip_atomic_fetch_add(arr + 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)N - 1u) {
-      __hip_atomic_store(arr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(arr + 16, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  __syncthreads();
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);   // no load of the published rows above the wait
-  stamp(stamps, 12);
-  if (!active) return;
-  const int env = min(16 * mq + l16, N - 1);
-  for (int u = e; u < 32; u += N) {
-    if (u != e) load_b(u);
-    const int nb = u >> 1, kh = u & 1;
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    bf16x8 a[7];
-    const int off0 = (env * Y3_ROWS * Y3_C + 448 * r + 224 * kh + 8 * lg) * 2;
-#pragma unroll
-    for (int s = 0; s < 7; ++s) {
-      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(yr, off0 + 64 * s, 0, SC1);
-      a[s] = __builtin_bit_cast(bf16x8, v);
-    }
-    __builtin_amdgcn_sched_barrier(0);   // all seven loads in flight before the first MFMA waits (one round trip)
-    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < 7; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s], bq[s], acc, 0, 0, 0);
-    float* o = f.out + (int64_t)(2 * r + kh) * f.pstride + nb * 32 + nq * 16 + l16;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int row = 16 * mq + 4 * lg + q;
-      if (row < N) o[(int64_t)row * FC_UNITS] = acc[q];
-    }
-  }
-  stamp(stamps, 13);
-}
-
 struct PongNext {   // the next parity's env state buffers (written by the committing workgroup)
   float* state;
   int32_t* tsteps;
@@ -1116,9 +807,9 @@ __device__ __forceinline__ void pong_commit_next(const PongIO& io, const PongNex
   sp[0] = q.bx; sp[1] = q.by; sp[2] = q.vx; sp[3] = q.vy; sp[4] = q.pa; sp[5] = q.po; sp[6] = q.sa; sp[7] = q.so;
 }
 
-template <int A1, bool FRAG, bool FCF>
+template <int A1, bool FRAG>
 __global__ void __launch_bounds__(T_THREADS) pong_fused_step_kernel(
-    PongIO io, PongNext nx, FcParts fc, FcFuse ff, u16* __restrict__ h, const u16* __restrict__ Wh,
+    PongIO io, PongNext nx, FcParts fc, u16* __restrict__ h, const u16* __restrict__ Wh,
     const float* __restrict__ bh, float* __restrict__ z_out, int32_t* __restrict__ act, float* __restrict__ logp,
     float* __restrict__ ent, float* __restrict__ vout, int key_shift, uint32_t pseed, const u16* __restrict__ W1,
     const float* __restrict__ b1, const u16* __restrict__ W2, const float* __restrict__ b2,
@@ -1277,10 +968,8 @@ __global__ void __launch_bounds__(T_THREADS) pong_fused_step_kernel(
   }
   __syncthreads();
   stamp(stamps, 1);
-  // FCF: s_in (dead after conv1) stages the conv3 row, which the fused fc product publishes
   trunk_rows_compute<3, FRAG>(s_in, s_w1, s_y1, s_y2, e, r, bias1a, bias1b, bias2, bias3, W2, W3, y1g, y2g, y3g,
-                              scale, stamps, bw2, bw3, FCF ? s_in : nullptr);
-  if constexpr (FCF) fc_fused_tail(ff, s_in, y3g, e, r, (int)gridDim.x / TR_ROWS, stamps);
+                              scale, stamps, bw2, bw3);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -1558,12 +1247,8 @@ __device__ __forceinline__ bf16x8 tr_frag(const u16* rows, int ld, int col0, int
 
 // 8 waves (2 per SIMD: one wave per SIMD left every LDS read latency exposed); one workgroup per CU by LDS.
 constexpr int BW_T = 512;
-// W1G: the conv1 weight gradient of the sample folded in (W1Fold): dW1[o][c] = scale * sum_p dy1[p][o] *
-// obs[ch][4 oy + ky][4 ox + kx], c = (ch, ky, kx), p = (oy, ox) -- the masked dy1 rows are on chip already, the
-// sample's 4 frames (prefetched into registers at entry) are staged as exact bf16 over the dead W2 rows; 8 waves x
-// (2 x 2 tiles of the 16x16x32 MFMA), 13 k-steps of 32 positions; the sample's [32][256] fp32 plane is written once
-// (the finaliser sums the per-sample planes in order). Replaces the conv1 split-K GEMM of the grouped weight-gradient
-// launch (EngineOpts.conv1_fold).
+// The conv1 weight gradient folded into the persistent data-gradient chain (cnn_trunk_bwd_persist_kernel W1G):
+// dW1[o][c] = scale * sum_p dy1[p][o] * obs[ch][4 oy + ky][4 ox + kx], c = (ch, ky, kx), p = (oy, ox).
 struct W1Fold {
   const uint8_t* obs;        // [*, 4, 84, 84] uint8 frames
   const int64_t* obs_idx;    // sample b reads obs row obs_idx[b] (null: row b)
@@ -1574,11 +1259,10 @@ constexpr int BW_FR = 4 * 84 * 84;   // frame pixels of a sample (bf16 in LDS: 5
 static_assert(BW_FR + 8 <= BW_RW, "the bf16 frames + a zero chunk fit the weight region");
 static_assert(416 * 32 <= BW_P3E + BW_M2E, "dy1 rows + 16 zero padding rows (13 k-steps of 32) fit the staging");
 
-template <bool W1G>
 __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_kernel(
     const u16* __restrict__ dy3g, const u16* __restrict__ W3, const u16* __restrict__ y2g,
     const u16* __restrict__ W2, const u16* __restrict__ y1g, u16* __restrict__ dy2g, u16* __restrict__ dy1g,
-    float* __restrict__ biasp, uint64_t* __restrict__ stamps, W1Fold wf) {
+    float* __restrict__ biasp, uint64_t* __restrict__ stamps) {
   __shared__ __attribute__((aligned(16))) u16 s_w[BW_RW];
   __shared__ __attribute__((aligned(16))) u16 s_p3m2[BW_P3E + BW_M2E];   // dy3 image + y2 mask; later dy1 staging
   __shared__ __attribute__((aligned(16))) u16 s_p2[BW_P2E];
@@ -1641,16 +1325,6 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_kernel(
   for (int u = 0; u < M1_PER; ++u) {
     const int c = min(tid + u * BW_T, M1_CH - 1);
     vm1[u] = *reinterpret_cast<const uint4*>(y1g + (size_t)b * 400 * 32 + c * 8);
-  }
-  // W1G: the sample's frames, 16-pixel chunks (1764 of them: <= 4 per thread), held until the dy1 output pass
-  constexpr int FR_CH = BW_FR / 16;
-  uint4 fr0, fr1, fr2, fr3;
-  if constexpr (W1G) {
-    const uint4* f = reinterpret_cast<const uint4*>(wf.obs + (size_t)(wf.obs_idx ? wf.obs_idx[b] : b) * BW_FR);
-    fr0 = f[tid];
-    fr1 = f[tid + BW_T];
-    fr2 = f[tid + 2 * BW_T];
-    fr3 = f[min(tid + 3 * BW_T, FR_CH - 1)];
   }
   __syncthreads();
   stamp(stamps, 1);
@@ -1799,23 +1473,7 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_kernel(
 #pragma unroll
       for (int e = 0; e < 8; ++e) part1[e] += bf_lane(v, e);
       *reinterpret_cast<uint4*>(dy1g + (size_t)b * 400 * 32 + c * 8) = v;
-      if constexpr (W1G) *reinterpret_cast<uint4*>(s_d1 + c * 8) = v;   // the masked rows: dW1's A operand
     }
-  }
-  if constexpr (W1G) {
-    // the frames as exact bf16 over the dead W2 rows, a zero chunk behind them, zero dy1 rows 400..415
-    u16* const s_fr = s_w;
-    auto put = [&](const uint4& w, int i) {
-      const uint2 a = u8x4_to_bf16(w.x), b2 = u8x4_to_bf16(w.y), c = u8x4_to_bf16(w.z), d = u8x4_to_bf16(w.w);
-      *reinterpret_cast<uint4*>(s_fr + i * 16) = make_uint4(a.x, a.y, b2.x, b2.y);
-      *reinterpret_cast<uint4*>(s_fr + i * 16 + 8) = make_uint4(c.x, c.y, d.x, d.y);
-    };
-    put(fr0, tid);
-    put(fr1, tid + BW_T);
-    put(fr2, tid + 2 * BW_T);
-    if (tid + 3 * BW_T < FR_CH) put(fr3, tid + 3 * BW_T);
-    if (tid == 0) *reinterpret_cast<uint4*>(s_fr + BW_FR) = make_uint4(0u, 0u, 0u, 0u);
-    s_d1[400 * 32 + tid] = 0;   // 16 padding rows x 32 = 512 (the dy1 epilogue's discard slot lives there)
   }
 #pragma unroll
   for (int e = 0; e < 8; ++e)
@@ -1830,45 +1488,6 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_kernel(
 #pragma unroll
     for (int w = 0; w < 8; ++w) v += s_red[1024 + w * 32 + tid];
     biasp[(size_t)b * 160 + 128 + tid] = v;
-  }
-  if constexpr (W1G) {
-    // dW1 of the sample: wave -> (o tiles 0, 1) x (c tiles 2 wid, 2 wid + 1); A = masked dy1 rows [p][o] and B =
-    // the patch matrix straight from the bf16 frames, both by transposing reads; positions past 400 read zeros
-    const u16* const s_fr = s_w;
-    floatx4 acc[2][2];
-#pragma unroll
-    for (int m = 0; m < 2; ++m)
-#pragma unroll
-      for (int n = 0; n < 2; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
-    const int q = l16 >> 2, pq = l16 & 3;
-    for (int ks = 0; ks < 13; ++ks) {
-      const bf16x8 a0 = tr_frag(s_d1 + ks * 32 * 32, 32, 0, lane);
-      const bf16x8 a1 = tr_frag(s_d1 + ks * 32 * 32, 32, 16, lane);
-#pragma unroll
-      for (int n = 0; n < 2; ++n) {
-        const int c = (2 * wid + n) * 16 + 4 * pq, ch = c >> 6, ky = (c >> 3) & 7, kx0 = c & 7;
-        const int pa = ks * 32 + lg * 8 + q, pb = pa + 4;
-        const int oya = pa / 20, oyb = pb / 20;
-        const int offa = pa < 400 ? ch * 7056 + (4 * oya + ky) * 84 + 4 * (pa - oya * 20) + kx0 : BW_FR;
-        const int offb = pb < 400 ? ch * 7056 + (4 * oyb + ky) * 84 + 4 * (pb - oyb * 20) + kx0 : BW_FR;
-        typedef short short4x __attribute__((ext_vector_type(4)));
-        typedef __attribute__((address_space(3))) short4x lds4;
-        const short4x lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(s_fr + offa));
-        const short4x hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(s_fr + offb));
-        const short8v bv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        const bf16x8 bf = __builtin_bit_cast(bf16x8, bv);
-        acc[0][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf, acc[0][n], 0, 0, 0);
-        acc[1][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bf, acc[1][n], 0, 0, 0);
-      }
-    }
-    float* const pl = wf.planes + (size_t)b * 32 * 256;
-#pragma unroll
-    for (int m = 0; m < 2; ++m)
-#pragma unroll
-      for (int n = 0; n < 2; ++n)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          pl[(size_t)(16 * m + 4 * lg + r) * 256 + (2 * wid + n) * 16 + l16] = acc[m][n][r] * wf.scale;
   }
   if (stamps) {
     stamp(stamps, 5);
@@ -1885,7 +1504,7 @@ __global__ void __launch_bounds__(BW_T) cnn_trunk_bwd_kernel(
 // them in registers for all of its samples; the next sample's dy3 image, y2 mask and y1 mask are loaded into
 // registers while the current one is processed. Same MFMA order per sample as the per-sample kernel: bit-identical
 // outputs.
-// W1G: the conv1 weight gradient folded in (W1Fold, as in the per-sample kernel): after a sample's dy1 rows are
+// W1G: the conv1 weight gradient folded in (W1Fold): after a sample's dy1 rows are
 // masked they stay in LDS and its four frames (prefetched with the sample's other operands) are staged as exact bf16
 // over the dead image region (which is extended for it; the dy2 image border is then re-zeroed per sample); 13 k-steps
 // of 16x16x32 MFMAs accumulate the workgroup's [32][256] slice in registers across its samples, written once at the
@@ -2277,25 +1896,6 @@ extern "C" hipError_t aca_fc_value(const float* hpart, int S, int64_t plane_stri
   return hipGetLastError();
 }
 
-extern "C" hipError_t aca_cnn_trunk_fwd(const uint8_t* obs, const uint16_t* W1, const float* b1, const uint16_t* W2,
-                                        const float* b2, const uint16_t* W3, const float* b3, uint16_t* y1,
-                                        uint16_t* y2, uint16_t* y3, int B, float scale, uint8_t* shift_out,
-                                        uint64_t* stamps, const int64_t* obs_idx, hipStream_t stream) {
-  if (B <= 0) return hipSuccess;
-  // the lean-LDS per-env form (two workgroups per CU) unless phase stamps are asked for: those live in the
-  // bf16-staged per-env kernel (diagnostic builds, scripts/microbench_*.py). Only the lean form reads through
-  // an index (obs_idx: gathered minibatch rows).
-  if (!stamps) {
-    aca::cnn_trunk_fwd_u8_kernel<<<B, 256, 0, stream>>>(obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale, shift_out,
-                                                          obs_idx);
-    return hipGetLastError();
-  }
-  if (obs_idx) return hipErrorInvalidValue;
-  aca::cnn_trunk_fwd_kernel<<<B, aca::T_THREADS, 0, stream>>>(obs, W1, b1, W2, b2, W3, b3, y1, y2, y3, scale,
-                                                               shift_out, stamps);
-  return hipGetLastError();
-}
-
 extern "C" hipError_t aca_cnn_trunk_fwd_s16(const uint8_t* obs, const uint16_t* W1, const float* b1,
                                             const uint16_t* W2, const float* b2, const uint16_t* W3, const float* b3,
                                             uint16_t* y1, uint16_t* y2, uint16_t* y3, int B, float scale,
@@ -2335,7 +1935,7 @@ extern "C" hipError_t aca_cnn_trunk_bwd(const uint16_t* dy3, const uint16_t* W3,
                                         const int64_t* w1_obs_idx, float* w1_planes, float w1_scale, int bias_acc,
                                         hipStream_t stream) {
   // bias_acc (persistent form): one bias-gradient row per workgroup (min(persist, B) rows) instead of one per sample
-  // w1_obs: the conv1 weight gradient folded into the per-sample kernel (one [32][256] plane per sample)
+  // w1_obs: the conv1 weight gradient folded into the persistent kernel (one [32][256] plane per workgroup)
   if (B <= 0) return hipSuccess;
   for (const void* p : {(const void*)dy3, (const void*)W3, (const void*)y2, (const void*)W2, (const void*)y1,
                         (const void*)dy2, (const void*)dy1})
@@ -2349,12 +1949,9 @@ extern "C" hipError_t aca_cnn_trunk_bwd(const uint16_t* dy3, const uint16_t* W3,
     aca::cnn_trunk_bwd_persist_kernel<false><<<persist < B ? persist : B, aca::BW_T, 0, stream>>>(
         dy3, W3, y2, W2, y1, dy2, dy1, biasp, B, stamps, bias_acc, aca::W1Fold{nullptr, nullptr, nullptr, 0.f});
   } else if (w1_obs) {
-    if (!w1_planes || reinterpret_cast<uintptr_t>(w1_obs) % 16) return hipErrorInvalidValue;
-    const aca::W1Fold wf{w1_obs, w1_obs_idx, w1_planes, w1_scale};
-    aca::cnn_trunk_bwd_kernel<true><<<B, aca::BW_T, 0, stream>>>(dy3, W3, y2, W2, y1, dy2, dy1, biasp, stamps, wf);
+    return hipErrorInvalidValue;   // the conv1 fold is a persistent-kernel feature
   } else {
-    aca::cnn_trunk_bwd_kernel<false><<<B, aca::BW_T, 0, stream>>>(dy3, W3, y2, W2, y1, dy2, dy1, biasp, stamps,
-                                                                  aca::W1Fold{nullptr, nullptr, nullptr, 0.f});
+    aca::cnn_trunk_bwd_kernel<<<B, aca::BW_T, 0, stream>>>(dy3, W3, y2, W2, y1, dy2, dy1, biasp, stamps);
   }
   return hipGetLastError();
 }
@@ -2366,17 +1963,9 @@ extern "C" hipError_t aca_pong_fused_step(
     int64_t* tg_n, float* ep_ret_n, float* ep_stats, const int64_t* ids, const uint8_t* prev, uint8_t* out,
     float* reward, uint8_t* done, uint8_t* trunc, uint32_t seed, int max_steps, const uint16_t* W1, const float* b1,
     const uint16_t* W2, const float* b2, const uint16_t* W3, const float* b3, uint16_t* y1, uint16_t* y2,
-    uint16_t* y3, float scale, uint8_t* shift_out, uint64_t* stamps, int frag, int N, const uint16_t* fc_w,
-    float* fc_out, int64_t fc_pstride, unsigned* fc_cnt, hipStream_t stream) {
+    uint16_t* y3, float scale, uint8_t* shift_out, uint64_t* stamps, int frag, int N, hipStream_t stream) {
   // frag: W2 / W3 are the fragment-ordered copies (W1 stays row-major: the kernel stages it through LDS)
-  // fc_w: the fragment-ordered Wfc -> the next observation's fc product in the same launch (FcFuse: 14 planes into
-  // fc_out, N <= 32, frag copies only)
   if (N <= 0) return hipSuccess;
-  const bool fcf = fc_w != nullptr;
-  if (fcf && (!frag || N > 32 || !fc_out || !fc_cnt || fc_pstride < (int64_t)N * 512 || fc_out == hpart ||
-              reinterpret_cast<uintptr_t>(fc_w) % 16 || reinterpret_cast<uintptr_t>(y3) % 16))
-    return hipErrorInvalidValue;
-  const aca::FcFuse ff{fc_w, fc_out, fc_pstride, fc_cnt};
   aca::PongIO io;
   io.state = state; io.tsteps = t; io.tglob = tg; io.ep_ret = ep_ret; io.ep_stats = ep_stats; io.env_ids = ids;
   io.prev = prev; io.out = out; io.reward = reward; io.done_out = done; io.trunc_out = trunc; io.seed = seed;
@@ -2387,18 +1976,14 @@ extern "C" hipError_t aca_pong_fused_step(
   switch (A + 1) {
 #define ACA_FUSED_CASE(A1)                                                                                       \
   case A1:                                                                                                       \
-    if (fcf)                                                                                                     \
-      aca::pong_fused_step_kernel<A1, true, true><<<grid, aca::T_THREADS, 0, stream>>>(                          \
-          io, nx, fc, ff, h, Wh, bh, z, act, logp, ent, value, key_shift, pseed, W1, b1, W2, b2, W3, b3, y1, y2,  \
-          y3, scale, shift_out, stamps);                                                                         \
-    else if (frag)                                                                                               \
-      aca::pong_fused_step_kernel<A1, true, false><<<grid, aca::T_THREADS, 0, stream>>>(                         \
-          io, nx, fc, ff, h, Wh, bh, z, act, logp, ent, value, key_shift, pseed, W1, b1, W2, b2, W3, b3, y1, y2,  \
-          y3, scale, shift_out, stamps);                                                                         \
+    if (frag)                                                                                                    \
+      aca::pong_fused_step_kernel<A1, true><<<grid, aca::T_THREADS, 0, stream>>>(                                \
+          io, nx, fc, h, Wh, bh, z, act, logp, ent, value, key_shift, pseed, W1, b1, W2, b2, W3, b3, y1, y2, y3,  \
+          scale, shift_out, stamps);                                                                             \
     else                                                                                                         \
-      aca::pong_fused_step_kernel<A1, false, false><<<grid, aca::T_THREADS, 0, stream>>>(                        \
-          io, nx, fc, ff, h, Wh, bh, z, act, logp, ent, value, key_shift, pseed, W1, b1, W2, b2, W3, b3, y1, y2,  \
-          y3, scale, shift_out, stamps);                                                                         \
+      aca::pong_fused_step_kernel<A1, false><<<grid, aca::T_THREADS, 0, stream>>>(                               \
+          io, nx, fc, h, Wh, bh, z, act, logp, ent, value, key_shift, pseed, W1, b1, W2, b2, W3, b3, y1, y2, y3,  \
+          scale, shift_out, stamps);                                                                             \
     break;
     ACA_FUSED_CASE(3) ACA_FUSED_CASE(4) ACA_FUSED_CASE(5) ACA_FUSED_CASE(6) ACA_FUSED_CASE(7)
 #undef ACA_FUSED_CASE

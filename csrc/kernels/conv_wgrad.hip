@@ -1,48 +1,19 @@
-// Per-sample conv1 weight gradient of the Nature-CNN trunk for large learner batches (PPO minibatches):
+// Weight gradients of the Nature-CNN trunk for large learner batches (PPO minibatches), as deterministic partial
+// planes (each written once, no atomics) that the gradient finaliser reduces in plane order:
 //
-//   dW1[o][c] = scale * sum_b sum_p dy1[b][p][o] * obs[b][ch][4 oy + ky][4 ox + kx],   c = (ch, ky, kx), p = (oy, ox)
+//   conv1:  dW1[o][c] = scale * sum_b sum_p dy1[b][p][o] * obs[b][ch][4 oy + ky][4 ox + kx],  c = (ch, ky, kx)
+//   conv2 / conv3:  dW[o][(ky, kx, c)] = sum_b sum_p dy[b][p][o] * img[b][S oy + ky][S ox + kx][c]
 //
-// As an implicit-im2col GEMM (M 32, N 256, K = 400 B) every K chunk re-gathers its uint8 patches from global
-// memory and every N tile re-reads dy1: at B = 4096 that product fetched 2.4x its operand bytes and ran at ~6 % of
-// the MFMA rate. Here workgroup (g, ch) owns input channel ch of the sample range of partial plane g: per sample it
-// stages the 84x84 frame of that channel (as exact bf16 pixel values) and the sample's dy1 rows in LDS ONCE and runs
-// the K loop (positions) out of LDS, both MFMA operands read by the transposing ds_read_b64_tr_b16: the dy1 rows
-// [position][channel] as A, and the patch matrix as B WITHOUT materialising it -- each lane points its transposing
-// read at the frame bytes of its own (position, ky, kx0..kx0+3), which are contiguous. The eight waves split the
-// 13 k-steps of a sample and each keeps the whole 32x64 output slice in registers; the waves' partial sums meet in
-// LDS once per workgroup, in a fixed order. The next two samples' frames and dy1 rows are in flight in registers
-// while the current one is multiplied. Each partial plane is written exactly once (no atomics) and the gradient
-// finaliser reduces the planes in plane order: deterministic. The 1/255 observation scale multiplies the fp32
-// sums. Workgroups of one plane share an XCD (blockIdx = g + P ch, P a multiple of 8), so the four channel slices
-// of a sample read its dy1 rows through one L2.
+// As implicit-im2col GEMMs (conv1: M 32, N 256, K = 400 B) every K chunk re-gathers its patches from global memory
+// and every N tile re-reads dy: at B = 4096 the conv1 product fetched 2.4x its operand bytes and ran at ~6 % of the
+// MFMA rate. Both kernels here stage the operands in LDS once per sample and read the patch matrix through the
+// transposing ds_read_b64_tr_b16 WITHOUT materialising it (each lane points its read at the contiguous pixels of its
+// own position / kernel tap).
 #include "common.h"
 
 namespace aca {
 
-constexpr int CW_T = 512;                        // 8 waves: 2 per SIMD (LDS allows one workgroup per CU)
-constexpr int CW_POS = 416;                      // 400 positions padded to 13 k-steps of 32
-constexpr int CW_LDY = 40;                       // dy1 LDS row stride (32 channels + 8 pad, bf16)
-constexpr int CW_FR = 84 * 84;                   // frame bytes
-constexpr int CW_FR4 = CW_FR / 16;               // 441 16-byte chunks
-constexpr int CW_DY4 = 400 * 4;                  // 1600 16-byte chunks of dy1 rows
-constexpr int CW_FR_PER = (CW_FR4 + CW_T - 1) / CW_T;   // 2
-constexpr int CW_DY_PER = (CW_DY4 + CW_T - 1) / CW_T;   // 7
-
 typedef short cw_short8 __attribute__((ext_vector_type(8)));
-
-// MFMA fragment (k = 8 (lane >> 4) + 0..7, n = col0 + lane & 15) of k-major rows via two transposing reads: as the
-// B operand it is B[k][n], as the A operand A[m = n][k]
-__device__ __forceinline__ bf16x8 cw_tr_frag(const u16* rows, int ld, int col0, int lane) {
-  const int lr16 = lane & 15, lg = lane >> 4, q = lr16 >> 2, p = lr16 & 3;
-  const u16* p0 = rows + (lg * 8 + q) * ld + col0 + 4 * p;
-  const u16* p1 = rows + (lg * 8 + 4 + q) * ld + col0 + 4 * p;
-  typedef short short4x __attribute__((ext_vector_type(4)));
-  typedef __attribute__((address_space(3))) short4x lds4;
-  const short4x lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(p0));
-  const short4x hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(p1));
-  const cw_short8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8, v);
-}
 
 // 4 uint8 -> 4 bf16 (exact integers)
 __device__ __forceinline__ uint2 cw_u8x4(uint32_t w) {
@@ -52,141 +23,10 @@ __device__ __forceinline__ uint2 cw_u8x4(uint32_t w) {
   return r;
 }
 
-__global__ void __launch_bounds__(CW_T) conv1_wgrad_kernel(const uint8_t* __restrict__ obs,
-                                                          const u16* __restrict__ dy1, float* __restrict__ planes,
-                                                          int B, int P, float scale,
-                                                          const int64_t* __restrict__ obs_idx) {
-  __shared__ __attribute__((aligned(16))) float red[4 * 8 * 4 * 64];      // the waves' partial slices (32 KB)
-  __shared__ __attribute__((aligned(16))) u16 s_dy[CW_POS * CW_LDY];
-  __shared__ __attribute__((aligned(16))) u16 s_fb[CW_FR + 8];            // frame as exact bf16 + a zero chunk
-  const int g = blockIdx.x % P, ch = blockIdx.x / P;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int b0 = (int)((int64_t)g * B / P), b1 = (int)((int64_t)(g + 1) * B / P);
-  const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
-  // padding positions 400..415: zero dy1 rows and zero patch rows, written once
-  for (int c = tid; c < 16 * (CW_LDY / 8); c += CW_T) *reinterpret_cast<uint4*>(s_dy + 400 * CW_LDY + c * 8) = z4;
-  if (tid == 0) *reinterpret_cast<uint4*>(s_fb + CW_FR) = z4;
-
-  // two samples in flight in named registers (a private uint4 array here was promoted to LDS, which made every
-  // prefetch wait for its loads at issue)
-  static_assert(CW_FR_PER == 1 && CW_DY_PER == 4, "register sets are written out for 1 + 4 chunks per thread");
-#define CW_SET(S) uint4 S##f0, S##d0, S##d1, S##d2, S##d3;
-#define CW_LOAD(S, b)                                                                                    \
-  {                                                                                                      \
-    const uint4* f = reinterpret_cast<const uint4*>(obs + ((size_t)(obs_idx ? obs_idx[b] : (b)) * 4 + ch) * CW_FR); \
-    const uint4* d = reinterpret_cast<const uint4*>(dy1 + (size_t)(b) * 400 * 32);                       \
-    S##f0 = f[min(tid, CW_FR4 - 1)];                                                                     \
-    S##d0 = d[tid]; S##d1 = d[tid + CW_T]; S##d2 = d[tid + 2 * CW_T];                                    \
-    S##d3 = d[min(tid + 3 * CW_T, CW_DY4 - 1)];                                                          \
-  }
-#define CW_DST(c, v) *reinterpret_cast<uint4*>(s_dy + ((c) >> 2) * CW_LDY + ((c) & 3) * 8) = (v);
-#define CW_STORE(S)                                                                                      \
-  {                                                                                                      \
-    if (tid < CW_FR4) {                                                                                  \
-      const uint2 a = cw_u8x4(S##f0.x), b_ = cw_u8x4(S##f0.y), c = cw_u8x4(S##f0.z), d = cw_u8x4(S##f0.w); \
-      *reinterpret_cast<uint4*>(s_fb + tid * 16) = make_uint4(a.x, a.y, b_.x, b_.y);                      \
-      *reinterpret_cast<uint4*>(s_fb + tid * 16 + 8) = make_uint4(c.x, c.y, d.x, d.y);                    \
-    }                                                                                                    \
-    CW_DST(tid, S##d0) CW_DST(tid + CW_T, S##d1) CW_DST(tid + 2 * CW_T, S##d2)                           \
-    if (tid + 3 * CW_T < CW_DY4) CW_DST(tid + 3 * CW_T, S##d3)                                           \
-  }
-  CW_SET(ra)
-  CW_SET(rb)
-  floatx4 acc[2][4];
-#pragma unroll
-  for (int m = 0; m < 2; ++m)
-#pragma unroll
-    for (int n = 0; n < 4; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
-  // B fragments straight from the bf16 frame: row k of the patch matrix is position p = (oy, ox), and the 4
-  // consecutive columns a lane reads in a transposing read are kx0 .. kx0 + 3 of one ky -- 8 contiguous bytes of
-  // frame row 4 oy + ky at column 4 ox + kx0 (8-byte aligned). Positions past 400 read the zero chunk.
-  const int lr16 = lane & 15, lg = lane >> 4, q = lr16 >> 2, pq = lr16 & 3;
-  auto bfrag = [&](int kb, int nt) -> bf16x8 {
-    const int n = nt * 16 + 4 * pq, ky = n >> 3, kx0 = n & 7;
-    const int pa = kb + lg * 8 + q, pb = pa + 4;
-    const int oya = pa / 20, oyb = pb / 20;
-    const int offa = pa < 400 ? (4 * oya + ky) * 84 + 4 * (pa - oya * 20) + kx0 : CW_FR;
-    const int offb = pb < 400 ? (4 * oyb + ky) * 84 + 4 * (pb - oyb * 20) + kx0 : CW_FR;
-    typedef short short4x __attribute__((ext_vector_type(4)));
-    typedef __attribute__((address_space(3))) short4x lds4;
-    const short4x lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(s_fb + offa));
-    const short4x hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(s_fb + offb));
-    const cw_short8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    return __builtin_bit_cast(bf16x8, v);
-  };
-  auto sample = [&]() {
-    for (int ks = wid; ks < CW_POS / 32; ks += CW_T / 64) {
-      const bf16x8 a0 = cw_tr_frag(s_dy + ks * 32 * CW_LDY, CW_LDY, 0, lane);
-      const bf16x8 a1 = cw_tr_frag(s_dy + ks * 32 * CW_LDY, CW_LDY, 16, lane);
-#pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        const bf16x8 bf = bfrag(ks * 32, n);
-        acc[0][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf, acc[0][n], 0, 0, 0);
-        acc[1][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bf, acc[1][n], 0, 0, 0);
-      }
-    }
-    __syncthreads();
-  };
-  if (b0 < b1) CW_LOAD(ra, b0)
-  if (b0 + 1 < b1) CW_LOAD(rb, b0 + 1)
-  for (int b = b0; b < b1; b += 2) {
-    CW_STORE(ra)
-    __syncthreads();
-    if (b + 2 < b1) CW_LOAD(ra, b + 2)
-    sample();
-    if (b + 1 >= b1) break;
-    CW_STORE(rb)
-    __syncthreads();
-    if (b + 3 < b1) CW_LOAD(rb, b + 3)
-    sample();
-  }
-#undef CW_SET
-#undef CW_LOAD
-#undef CW_DST
-#undef CW_STORE
-  // the eight waves' partial slices meet in LDS in a fixed order: ((w0 + w4) + (w1 + w5)) + ((w2 + w6) + (w3 + w7));
-  // D: row m = 4 (lane >> 4) + i, column lane & 15
-  if (wid >= 4)
-#pragma unroll
-    for (int m = 0; m < 2; ++m)
-#pragma unroll
-      for (int n = 0; n < 4; ++n)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) red[(((wid - 4) * 8 + m * 4 + n) * 4 + i) * 64 + lane] = acc[m][n][i];
-  __syncthreads();
-  if (wid < 4)
-#pragma unroll
-    for (int m = 0; m < 2; ++m)
-#pragma unroll
-      for (int n = 0; n < 4; ++n)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc[m][n][i] += red[((wid * 8 + m * 4 + n) * 4 + i) * 64 + lane];
-  __syncthreads();
-  if (wid < 4)
-#pragma unroll
-    for (int m = 0; m < 2; ++m)
-#pragma unroll
-      for (int n = 0; n < 4; ++n)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) red[((wid * 8 + m * 4 + n) * 4 + i) * 64 + lane] = acc[m][n][i];
-  __syncthreads();
-  float* dst = planes + (size_t)g * 32 * 256;
-  for (int e = tid; e < 8 * 4 * 64; e += CW_T) {
-    const int t = e >> 8, i = (e >> 6) & 3, l = e & 63;
-    const float v = ((red[((0 * 8 + t) * 4 + i) * 64 + l] + red[((1 * 8 + t) * 4 + i) * 64 + l]) +
-                     (red[((2 * 8 + t) * 4 + i) * 64 + l] + red[((3 * 8 + t) * 4 + i) * 64 + l])) * scale;
-    const int m = t >> 2, n = t & 3;
-    const int o = m * 16 + 4 * (l >> 4) + i, c = ch * 64 + n * 16 + (l & 15);
-    dst[o * 256 + c] = v;
-  }
-}
-
-
 // ------------------------------------------------------------------------------------------------------------
-// conv1 weight gradient, all four input channels per workgroup on the 32x32x16 MFMA (conv1_wgrad2_kernel):
-//   the kernel above stages a sample's dy1 rows once PER CHANNEL (four workgroups read and stage the same 25.6 KB)
-//   and keeps 16x16 tiles, so it is bound by staging and LDS reads (48 % bank conflicts, ~380 TF/s at B = 4096).
-//   Here workgroup g walks the samples of plane g and stages, per sample, the dy1 rows [416][32] (64-byte rows: the 4
+// conv1 weight gradient, all four input channels per workgroup on the 32x32x16 MFMA (conv1_wgrad2_kernel; a
+//   first version staged a sample's dy1 rows once PER CHANNEL in four workgroups on 16x16 tiles and was bound by
+//   staging and LDS reads: 48 % bank conflicts, ~380 TF/s at B = 4096). Workgroup g walks the samples of plane g and stages, per sample, the dy1 rows [416][32] (64-byte rows: the 4
 //   rows of a transposing read land in disjoint bank windows) and all four frames as exact bf16 (56 KB) ONCE; the next
 //   sample is in flight in registers. Wave w = (k quarter w >> 1, column half w & 1) owns a 32 x 128 output slice
 //   (four 32x32 fp32 accumulators) over the k-steps ks = kq, kq + 4, ... of 16 positions: per k-step one A fragment
@@ -315,141 +155,13 @@ __global__ void __launch_bounds__(C2_T) conv1_wgrad2_kernel(const uint8_t* __res
   }
 }
 
-// ------------------------------------------------------------------------------------------------------------
-// Per-sample weight gradient of a bf16 NHWC conv layer (conv2: y1 [20][20][32] -> 9x9, 4x4 stride 2; conv3: y2
-// [9][9][64] -> 7x7, 3x3 stride 1; 64 output channels, OHWI weights [64][KS KS C]), same scheme as conv1 above:
-//   dW[o][(ky, kx, c)] = sum_b sum_p dy[b][p][o] * img[b][S oy + ky][S ox + kx][c]
-// Workgroup (g, ky) owns kernel row ky (KS C columns) of plane g's samples; per sample the image and the dy rows
-// are staged in LDS once, A fragments are the dy rows (transposing reads, positions = K), and each lane points its
-// B-fragment transposing read at the 4 contiguous channels c0..c0+3 of pixel (S oy + ky, S ox + kx) of its
-// position -- no im2col. Wave w owns column tiles w, w + 8, ... and all four 16-channel output tiles, so the
-// waves' outputs are disjoint (no cross-wave reduction). Two samples in flight in registers.
-template <int H, int W, int C, int KS, int S, int OH, int OW>
-__global__ void __launch_bounds__(512) conv_wgrad_nhwc_kernel(const u16* __restrict__ img,
-                                                              const u16* __restrict__ dy,
-                                                              float* __restrict__ planes, int B, int P) {
-  constexpr int T = 512;
-  constexpr int NPOS = OH * OW, KSTEPS = (NPOS + 31) / 32, KPOS = KSTEPS * 32;
-  constexpr int NCOL = KS * KS * C, SLICE = KS * C, NT = SLICE / 16;
-  constexpr int LDI = C + 8, LDD = 72;
-  constexpr int IMG4 = H * W * C / 8, DY4 = NPOS * 8;          // 16-byte chunks per sample
-  constexpr int IPER = (IMG4 + T - 1) / T, DPER = (DY4 + T - 1) / T;
-  constexpr int NTW = (NT + 7) / 8;                            // column tiles per wave (at most)
-  static_assert(SLICE % 16 == 0 && C % 4 == 0, "tile shapes");
-  __shared__ __attribute__((aligned(16))) u16 s_img[H * W * LDI + 8];
-  __shared__ __attribute__((aligned(16))) u16 s_dy[KPOS * LDD];
-  const int g = blockIdx.x % P, ky = blockIdx.x / P;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int b0 = (int)((int64_t)g * B / P), b1 = (int)((int64_t)(g + 1) * B / P);
-  const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
-  for (int c = tid; c < (KPOS - NPOS) * (LDD / 8); c += T)
-    *reinterpret_cast<uint4*>(s_dy + NPOS * LDD + c * 8) = z4;
-  if (tid == 0) *reinterpret_cast<uint4*>(s_img + H * W * LDI) = z4;
-
-  // two register sets of up to 4 image + 2 dy chunks per thread, written out as named variables (private arrays
-  // here stayed in scratch)
-  static_assert(IPER <= 4 && DPER <= 2, "register sets hold 4 image + 2 dy chunks per thread");
-  uint4 ra0, ra1, ra2, ra3, ra4, ra5, rb0, rb1, rb2, rb3, rb4, rb5;
-#define CWN_LD1(R, k, base, lim, u) if ((u) < (lim##PER)) R##k = base[min(tid + (u) * T, lim##4 - 1)];
-#define CWN_LOAD(R, b)                                                                                   \
-  {                                                                                                      \
-    const uint4* ip = reinterpret_cast<const uint4*>(img + (size_t)(b) * H * W * C);                     \
-    const uint4* dp = reinterpret_cast<const uint4*>(dy + (size_t)(b) * NPOS * 64);                      \
-    if (0 < IPER) R##0 = ip[min(tid, IMG4 - 1)];                                                         \
-    if (1 < IPER) R##1 = ip[min(tid + T, IMG4 - 1)];                                                     \
-    if (2 < IPER) R##2 = ip[min(tid + 2 * T, IMG4 - 1)];                                                 \
-    if (3 < IPER) R##3 = ip[min(tid + 3 * T, IMG4 - 1)];                                                 \
-    if (0 < DPER) R##4 = dp[min(tid, DY4 - 1)];                                                          \
-    if (1 < DPER) R##5 = dp[min(tid + T, DY4 - 1)];                                                      \
-  }
-#define CWN_ST_I(v, u)                                                                                   \
-  if ((u) < IPER && tid + (u) * T < IMG4) {                                                              \
-    const int c = tid + (u) * T;                                                                         \
-    *reinterpret_cast<uint4*>(s_img + (c / (C / 8)) * LDI + (c % (C / 8)) * 8) = (v);                    \
-  }
-#define CWN_ST_D(v, u)                                                                                   \
-  if ((u) < DPER && tid + (u) * T < DY4) {                                                               \
-    const int c = tid + (u) * T;                                                                         \
-    *reinterpret_cast<uint4*>(s_dy + (c >> 3) * LDD + (c & 7) * 8) = (v);                                \
-  }
-#define CWN_STORE(R)                                                                                     \
-  {                                                                                                      \
-    CWN_ST_I(R##0, 0) CWN_ST_I(R##1, 1) CWN_ST_I(R##2, 2) CWN_ST_I(R##3, 3)                              \
-    CWN_ST_D(R##4, 0) CWN_ST_D(R##5, 1)                                                                  \
-  }
-  floatx4 acc[NTW][4];
-#pragma unroll
-  for (int j = 0; j < NTW; ++j)
-#pragma unroll
-    for (int m = 0; m < 4; ++m) acc[j][m] = floatx4{0.f, 0.f, 0.f, 0.f};
-  const int lr16 = lane & 15, lg = lane >> 4, q = lr16 >> 2, pq = lr16 & 3;
-#define CWN_SAMPLE()                                                                                     \
-  {                                                                                                      \
-    _Pragma("unroll") for (int ks = 0; ks < KSTEPS; ++ks) {                                              \
-      bf16x8 af[4];                                                                                      \
-      _Pragma("unroll") for (int m = 0; m < 4; ++m) af[m] = cw_tr_frag(s_dy + ks * 32 * LDD, LDD, m * 16, lane); \
-      const int pa = ks * 32 + lg * 8 + q, pb = pa + 4;                                                  \
-      const int oya = pa / OW, oyb = pb / OW;                                                            \
-      const int ba = (S * oya + ky) * W + S * (pa - oya * OW), bb = (S * oyb + ky) * W + S * (pb - oyb * OW); \
-      _Pragma("unroll") for (int j = 0; j < NTW; ++j) {                                                  \
-        const int nt = wid + 8 * j;                                                                      \
-        if (nt < NT) {                                                                                   \
-          const int n = nt * 16 + 4 * pq, kx = n / C, c0 = n - kx * C;                                   \
-          const int offa = pa < NPOS ? (ba + kx) * LDI + c0 : H * W * LDI;                               \
-          const int offb = pb < NPOS ? (bb + kx) * LDI + c0 : H * W * LDI;                               \
-          typedef short short4x __attribute__((ext_vector_type(4)));                                     \
-          typedef __attribute__((address_space(3))) short4x lds4;                                        \
-          const short4x lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(s_img + offa));             \
-          const short4x hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(s_img + offb));             \
-          const cw_short8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};                   \
-          const bf16x8 bf = __builtin_bit_cast(bf16x8, v);                                               \
-          _Pragma("unroll") for (int m = 0; m < 4; ++m)                                                  \
-            acc[j][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bf, acc[j][m], 0, 0, 0);          \
-        }                                                                                                \
-      }                                                                                                  \
-    }                                                                                                    \
-    __syncthreads();                                                                                     \
-  }
-  if (b0 < b1) CWN_LOAD(ra, b0)
-  if (b0 + 1 < b1) CWN_LOAD(rb, b0 + 1)
-  for (int b = b0; b < b1; b += 2) {
-    CWN_STORE(ra)
-    __syncthreads();
-    if (b + 2 < b1) CWN_LOAD(ra, b + 2)
-    CWN_SAMPLE()
-    if (b + 1 >= b1) break;
-    CWN_STORE(rb)
-    __syncthreads();
-    if (b + 3 < b1) CWN_LOAD(rb, b + 3)
-    CWN_SAMPLE()
-  }
-#undef CWN_LD1
-#undef CWN_LOAD
-#undef CWN_ST_I
-#undef CWN_ST_D
-#undef CWN_STORE
-#undef CWN_SAMPLE
-  float* dst = planes + (size_t)g * 64 * NCOL;
-#pragma unroll
-  for (int j = 0; j < NTW; ++j) {
-    const int nt = wid + 8 * j;
-    if (nt < NT)
-#pragma unroll
-      for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          dst[(size_t)(m * 16 + 4 * lg + i) * NCOL + ky * SLICE + nt * 16 + lr16] = acc[j][m][i];
-  }
-}
-
-
 // ---------------------------------------------------------------------------------------------------------------
 // Batched-position weight gradient of a bf16 NHWC conv layer on the 32x32x16 MFMA (large learner batches):
 //   dW[o][n] = sum_P dy[P][o] * col[P][n],   P = (sample, oy, ox) over the workgroup's samples,
 //                                              n = (ky, kx, c),  col[P][n] = img[sample][S oy + ky][S ox + kx][c]
 // i.e. ONE GEMM with M = 64 output channels, N = KS KS C, K = the positions of SB samples at a time (positions of
 // consecutive samples are consecutive K rows -- no per-sample padding of the 49 / 81 positions to a k-step). The
-// per-sample kernel above multiplies 12-16 MFMAs per wave per staged sample and spends its time staging and at
+// per-sample form (one kernel row per workgroup, retired) multiplied 12-16 MFMAs per wave per staged sample and spends its time staging and at
 // barriers; here every workgroup owns ALL 64 x N outputs of its plane (8 waves: wave w holds m-tile w & 1 and the
 // n-tiles (w >> 1) + 4 i, 32x32 fp32 accumulators in registers), stages SB samples per LDS fill (the next fill is in
 // flight in registers meanwhile) and runs KP / 16 k-steps of 4-5 MFMAs per wave between two barriers. Both MFMA
@@ -606,16 +318,6 @@ __global__ void __launch_bounds__(512) conv_wgrad_gemm_kernel(const u16* __restr
 
 }  // namespace aca
 
-// obs uint8 [B][4][84][84], dy1 bf16 [B][400][32] -> planes fp32 [P][32][256] (plane g: samples
-// [g B / P, (g + 1) B / P)); grid 4 P. Shapes and alignment are checked by the binding.
-extern "C" hipError_t aca_conv1_wgrad(const uint8_t* obs, const uint16_t* dy1, float* planes, int B, int P,
-                                      float scale, const int64_t* obs_idx, hipStream_t stream) {
-  if (B <= 0) return hipSuccess;
-  if (P < 1 || P > 1024) return hipErrorInvalidValue;
-  aca::conv1_wgrad_kernel<<<4 * P, aca::CW_T, 0, stream>>>(obs, dy1, planes, B, P, scale, obs_idx);
-  return hipGetLastError();
-}
-
 // All four channels per workgroup (conv1_wgrad2_kernel): grid P, plane g of [32][256] per workgroup.
 extern "C" hipError_t aca_conv1_wgrad2(const uint8_t* obs, const uint16_t* dy1, float* planes, int B, int P,
                                        float scale, const int64_t* obs_idx, hipStream_t stream) {
@@ -635,21 +337,6 @@ extern "C" hipError_t aca_conv_wgrad_gemm(int layer, const uint16_t* img, const 
     aca::conv_wgrad_gemm_kernel<20, 20, 32, 4, 2, 9, 9, 2><<<P, 512, 0, stream>>>(img, dy, planes, B, P);
   else if (layer == 3)
     aca::conv_wgrad_gemm_kernel<9, 9, 64, 3, 1, 7, 7, 2><<<P, 512, 0, stream>>>(img, dy, planes, B, P);
-  else
-    return hipErrorInvalidValue;
-  return hipGetLastError();
-}
-
-// conv2 (layer 2: y1 [B][20][20][32] -> dy2 [B][81][64], W2 [64][512]) / conv3 (layer 3: y2 [B][9][9][64] -> dy3
-// [B][49][64], W3 [64][576]) weight gradient as P partial planes; grid KS P (workgroup (g, ky)).
-extern "C" hipError_t aca_conv_wgrad_nhwc(int layer, const uint16_t* img, const uint16_t* dy, float* planes, int B,
-                                          int P, hipStream_t stream) {
-  if (B <= 0) return hipSuccess;
-  if (P < 1 || P > 1024) return hipErrorInvalidValue;
-  if (layer == 2)
-    aca::conv_wgrad_nhwc_kernel<20, 20, 32, 4, 2, 9, 9><<<4 * P, 512, 0, stream>>>(img, dy, planes, B, P);
-  else if (layer == 3)
-    aca::conv_wgrad_nhwc_kernel<9, 9, 64, 3, 1, 7, 7><<<3 * P, 512, 0, stream>>>(img, dy, planes, B, P);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();

@@ -73,7 +73,12 @@ step() {
       timeout -s KILL 240 rocprofv3 --kernel-trace --output-format csv --pmc FETCH_SIZE GRBM_GUI_ACTIVE \
         -d $O/pmc_${arg}_fetch -o run -- "${p[@]:3}" > $O/pmc_${arg}_fetch.log 2>&1 \
         || { tail -5 $O/pmc_${arg}_fetch.log; return 1; }
-      python3 scripts/pmc_table.py --last 4 $(find $O/pmc_${arg}_sq $O/pmc_${arg}_fetch -name "*counter_collection.csv") \
+      # WRITE_SIZE takes 2 of the 4 TCC counters of a pass, the L2 hit / miss sums the other two
+      timeout -s KILL 240 rocprofv3 --kernel-trace --output-format csv --pmc WRITE_SIZE TCC_HIT_sum TCC_MISS_sum \
+        -d $O/pmc_${arg}_write -o run -- "${p[@]:3}" > $O/pmc_${arg}_write.log 2>&1 \
+        || { tail -5 $O/pmc_${arg}_write.log; return 1; }
+      python3 scripts/pmc_table.py --last 4 $(find $O/pmc_${arg}_sq $O/pmc_${arg}_fetch $O/pmc_${arg}_write \
+        -name "*counter_collection.csv") \
         > $O/${arg}_pmc.txt && head -40 $O/${arg}_pmc.txt
       find $O -name "*.csv" -size +8M -delete ;;
     cmd)

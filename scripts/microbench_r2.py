@@ -61,7 +61,7 @@ def main():
     bt = lb.rows(0, N)
     scratch = st.obs[1].clone()
     cands = {}
-    for mode in (0, 1, 2):
+    for mode in (3, 1, 2):
         cands[f"trunk_mode{mode}"] = (lambda m=mode: ops.cnn_trunk_fwd(
             st.obs[0], eng.sW1, eng.b1, eng.sW2, eng.b2, eng.sW3, eng.b3, bt.y1, bt.y2, bt.y3, 1.0 / 255.0, scratch,
             None, m, None))

@@ -54,9 +54,6 @@ def main():
         for P in (64, 128, 256, 512):
             us = time_fn(lambda: ops.conv_wgrad_gemm(layer, img, dy, planes, P))
             out[f"wgrad{layer}_gemm_P{P}"] = {"us": round(us, 2), "tflops": round(flop / us / 1e6, 1)}
-        for P in (128, 256):
-            us = time_fn(lambda: ops.conv_wgrad_nhwc(layer, img, dy, planes, P))
-            out[f"wgrad{layer}_nhwc_P{P}"] = {"us": round(us, 2), "tflops": round(flop / us / 1e6, 1)}
     # fc GEMMs (PPO minibatch)
     y3 = torch.randn(B * 3136, device=dev).to(torch.bfloat16)
     dh = torch.randn(B * 512, device=dev).to(torch.bfloat16)

@@ -51,3 +51,16 @@ def test_engine_opts_typed_and_round_trips():
     assert TrainConfig(**d) == c
     with pytest.raises(TypeError):
         EngineOpts(no_such_knob=1)
+
+
+def test_engine_opts_field_list_is_pinned():
+    """Every EngineOpts switch is the default path of a BASELINE config or a test oracle; variants that measured
+    slower were deleted with their kernels (fused_fc, per-sample conv1_fold, trunk_bwd_v2, mlp_prefetch, conv1_wgrad
+    v1, conv_wgrad_nhwc, cnn_trunk_fwd_u8). A new knob must be added here on purpose."""
+    import dataclasses
+    names = [f.name for f in dataclasses.fields(EngineOpts)]
+    assert names == ["fused_step", "trunk_rows_max_b", "fused_env_split", "adam_step_offsets", "frag_weights",
+                     "fc_max_planes", "fc_frag_big", "fc_frag", "a2c_head", "a2c_head_env", "fused_head", "grouped",
+                     "det_wgrad", "fused_bwd", "mb_index", "ppo_head", "fc_bwd", "large_batch_min_b",
+                     "trunk_bwd_persist", "wgrad_planes", "conv1_v2_planes", "nhwc_planes"]
+    assert len(names) <= 25

@@ -125,7 +125,7 @@ def test_breakout_ppo_learns_on_the_large_batch_kernels_and_tracks_torch(cuda):
     assert eng is not None and tr.graph is not None
     mb = tr.cfg.num_envs * tr.cfg.n_steps // tr.cfg.ppo_minibatches
     assert eng.fused_env_step_ok(tr.cfg.num_envs) and eng.opts.fused_env_split
-    assert eng.ppo_head_ok(mb) and eng.big_gemm_ok(mb) and mb >= eng.trunk_bwd_persist_min_b
+    assert eng.ppo_head_ok(mb) and eng.big_gemm_ok(mb) and mb >= eng.large_b
     win = [r["win"] for r in rows]
     assert win[0] < 0.15 and win[-1] > 0.45 and win[-1] > win[0] + 0.3, win
     trt, rows_t = _curve("breakout_ppo", 200, 25, device="cuda:0", seed=1, engine="torch")

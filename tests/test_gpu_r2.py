@@ -345,10 +345,9 @@ def test_fused_rollout_step_equals_separate_policy_and_trunk(cuda, capture, monk
             assert torch.equal(x, y), (k, j)
 
 
-@pytest.mark.parametrize("v2", [False, True])
 @pytest.mark.parametrize("B,P", [(7, 4), (160, 64), (1024, 64), (1100, 256)])
-def test_conv1_wgrad_planes_match_autograd(cuda, B, P, v2):
-    """Per-sample conv1 weight gradient (conv_wgrad.hip; v2: conv1_wgrad2_kernel, all channels per workgroup): the
+def test_conv1_wgrad_planes_match_autograd(cuda, B, P):
+    """Per-sample conv1 weight gradient (conv_wgrad.hip conv1_wgrad2_kernel, all channels per workgroup): the
     plane sum == the fp32 autograd conv weight gradient of obs/255 and dy1, every plane holds exactly its sample
     range, and two runs are bit-identical."""
     from actor_critic_algs_on_tensorflow_amd import _native
@@ -357,7 +356,7 @@ def test_conv1_wgrad_planes_match_autograd(cuda, B, P, v2):
     obs = torch.randint(0, 256, (B, 4, 84, 84), dtype=torch.uint8, generator=g).to(cuda)
     dy1 = (torch.randn(B * 400, 32, generator=g) * 0.1).to(torch.bfloat16).to(cuda)
     planes = torch.full((max(64, P) * 32 * 256,), float("nan"), device=cuda)
-    ops.conv1_wgrad(obs, dy1, planes, P, 1.0 / 255.0, None, v2)
+    ops.conv1_wgrad(obs, dy1, planes, P, 1.0 / 255.0, None)
     got = planes[:P * 8192].view(P, 32, 256)
     # fp32 references on the CPU (a MIOpen weight-gradient solver is not a reliable reference, test_gpu_r3.py)
     go = dy1.float().cpu().view(B, 20, 20, 32).permute(0, 3, 1, 2)
@@ -372,33 +371,10 @@ def test_conv1_wgrad_planes_match_autograd(cuda, B, P, v2):
                                          stride=4).reshape(32, 256).to(cuda)
         torch.testing.assert_close(got[0], r0, rtol=1e-4, atol=1e-4)
     again = torch.zeros_like(planes)
-    ops.conv1_wgrad(obs, dy1, again, P, 1.0 / 255.0, None, v2)
+    ops.conv1_wgrad(obs, dy1, again, P, 1.0 / 255.0, None)
     assert torch.equal(again[:P * 8192], planes[:P * 8192])
     # frames gathered through an index (PPO minibatch rows of a larger observation buffer)
     perm = torch.randperm(B, generator=g).to(cuda)
     by_idx = torch.zeros_like(planes)
-    ops.conv1_wgrad(obs[perm.argsort()].contiguous(), dy1, by_idx, P, 1.0 / 255.0, perm.argsort().argsort(), v2)
+    ops.conv1_wgrad(obs[perm.argsort()].contiguous(), dy1, by_idx, P, 1.0 / 255.0, perm.argsort().argsort())
     assert torch.equal(by_idx[:P * 8192], planes[:P * 8192])
-
-
-@pytest.mark.parametrize("layer,B,P", [(2, 5, 3), (2, 300, 64), (3, 9, 4), (3, 300, 64)])
-def test_conv_wgrad_nhwc_planes_match_autograd(cuda, layer, B, P):
-    """Per-sample conv2 / conv3 weight gradient (conv_wgrad.hip, no im2col): the plane sum == the fp32 autograd conv
-    weight gradient (OHWI layout), and two runs are bit-identical."""
-    from actor_critic_algs_on_tensorflow_amd import _native
-    ops = _native.require()
-    H, C, KS, S, OH = (20, 32, 4, 2, 9) if layer == 2 else (9, 64, 3, 1, 7)
-    g = torch.Generator(device="cpu").manual_seed(B + layer)
-    img = torch.rand(B, H, H, C, generator=g).to(torch.bfloat16).to(cuda)
-    dy = (torch.randn(B, OH, OH, 64, generator=g) * 0.1).to(torch.bfloat16).to(cuda)
-    n = KS * KS * C
-    planes = torch.full((P * 64 * n,), float("nan"), device=cuda)
-    ops.conv_wgrad_nhwc(layer, img.view(B * H * H, C), dy.view(B * OH * OH, 64), planes, P)
-    ref = torch.nn.grad.conv2d_weight(img.float().cpu().permute(0, 3, 1, 2), (64, C, KS, KS),
-                                      dy.float().cpu().permute(0, 3, 1, 2), stride=S)
-    ref = ref.permute(0, 2, 3, 1).reshape(64, n).to(cuda)
-    tot = planes.view(P, 64, n).sum(0)
-    assert ((tot - ref).norm() / ref.norm()).item() < 1e-4
-    again = torch.zeros_like(planes)
-    ops.conv_wgrad_nhwc(layer, img.view(B * H * H, C), dy.view(B * OH * OH, 64), again, P)
-    assert torch.equal(again, planes)

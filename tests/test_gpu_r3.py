@@ -84,9 +84,9 @@ def test_native_mlp_time_limit_bootstrap_matches_oracle(cuda):
 
 
 def test_trunk_fwd_per_env_is_batch_invariant(cuda):
-    """The per-env lean-LDS trunk forward (cnn_fused.hip cnn_trunk_fwd_u8_kernel: one workgroup per sample, the
-    observation staged as uint8 by LDS-DMA) gives every sample the same bits whatever batch it is launched in: a
-    1283-sample launch == two launches of 700 and 583 samples."""
+    """The per-env trunk forward (cnn_fused.hip cnn_trunk_fwd_s16_kernel, mode 3: one workgroup per sample, the
+    observation converted once into a bf16 LDS image) gives every sample the same bits whatever batch it is launched
+    in: a 1283-sample launch == two launches of 700 and 583 samples."""
     from actor_critic_algs_on_tensorflow_amd.ops import gemm as G
     torch.manual_seed(4)
     B = 1283
@@ -101,7 +101,7 @@ def test_trunk_fwd_per_env_is_batch_invariant(cuda):
         y1 = torch.full((n * 400, 32), float("nan"), dtype=torch.bfloat16, device=cuda)
         y2 = torch.full((n * 81, 64), float("nan"), dtype=torch.bfloat16, device=cuda)
         y3 = torch.full((n * 49, 64), float("nan"), dtype=torch.bfloat16, device=cuda)
-        G.cnn_trunk_fwd(o, W1, b1, W2, b2, W3, b3, y1, y2, y3, mode=0)
+        G.cnn_trunk_fwd(o, W1, b1, W2, b2, W3, b3, y1, y2, y3, mode=3)
         return y1, y2, y3
 
     big = run(obs)

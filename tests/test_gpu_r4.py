@@ -274,9 +274,8 @@ def test_sumsq_multi_equals_separate_launches(cuda):
 
 def test_trunk_fwd_bf16_staged_by_index_equals_lean_form(cuda):
     """cnn_trunk_fwd mode 3 (cnn_trunk_fwd_s16_kernel: bytes converted once into a bf16 image, y1/y2/y3 out through
-    LDS as 16-byte rows) reading a PPO minibatch through an index == the lean per-env form (mode 0) bit for bit, as
-    does mode 5 (the same kernel on fragment-ordered weight copies), and they match the fp32 torch convolutions of
-    the same bf16 operands."""
+    LDS as 16-byte rows) reading a PPO minibatch through an index == mode 5 (the same kernel on fragment-ordered
+    weight copies) bit for bit, and both match the fp32 torch convolutions of the same bf16 operands."""
     import torch.nn.functional as F
     from actor_critic_algs_on_tensorflow_amd.ops import gemm as G
     g = torch.Generator(device="cpu").manual_seed(11)
@@ -290,7 +289,7 @@ def test_trunk_fwd_bf16_staged_by_index_equals_lean_form(cuda):
     from actor_critic_algs_on_tensorflow_amd.ops.optim import frag_order
     F1, F2, F3 = (frag_order(W, *W.shape) for W in (W1, W2, W3))
     outs = []
-    for mode in (0, 3, 5):   # 5: the staged kernel reading the fragment-ordered weight copies
+    for mode in (3, 5):   # 5: the staged kernel reading the fragment-ordered weight copies
         ys = [torch.full((B * r, c), float("nan"), dtype=torch.bfloat16, device=cuda)
               for r, c in ((400, 32), (81, 64), (49, 64))]
         w = (F1, F2, F3) if mode == 5 else (W1, W2, W3)

@@ -172,65 +172,6 @@ def test_optimiser_writes_the_kc_fragment_copy(cuda, cls_name):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("N", [32, 20, 7, 1])
-def test_fused_step_fc_product_matches_fp64(cuda, N):
-    """The fused step's in-launch fc product (cnn_fused.hip fc_fused_tail, EngineOpts.fused_fc): after a native
-    rollout the bootstrap observation's 14 planes summed in plane order == y3 @ Wfc in fp64 (same bf16 operands), the
-    published y3 rows == the trunk kernel's, the slice counters re-armed to zero and no hand-off timed out."""
-    from actor_critic_algs_on_tensorflow_amd import preset
-    from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
-    cfg = preset("pong_a2c", num_envs=N, device="cuda:0", outdir=None, quiet=True, stdout_freq=0, save_every=0,
-                 engine_opts=dict(fused_fc=True))
-    tr = ActorCriticTrainer(cfg)
-    eng = tr.engine
-    assert eng.fused_fc_ok(N)
-    tr.step()
-    tr.collect()   # a rollout alone: the weights the planes were computed with are still current
-    torch.cuda.synchronize()
-    hp, S = eng.last_fc
-    assert S == eng.FCF_PLANES
-    b = eng.bufs(N)
-    y3 = b.y3.view(N, 3136)
-    ref = y3.double() @ eng.sWfc.view(3136, 512).double()
-    got = hp.view(32, -1)[:S, :N * 512].double().sum(0).view(N, 512)
-    assert float((got - ref).abs().max() / ref.abs().max().clamp_min(1e-30)) < 1e-5
-    # the published rows are the trunk's own: recompute the trunk of the bootstrap observation
-    chk = eng.bufs(N, with_grad=False)
-    y3_pub = y3.clone()
-    eng.forward(tr.storage.obs[tr.storage.T], chk, head=False)
-    torch.cuda.synchronize()
-    assert torch.equal(chk.y3.view(N, 3136), y3_pub)
-    assert int(eng._fcf_cnt.abs().sum()) == 0
-    assert eng.health_errors() == []
-
-
-def test_fused_step_fc_update_tracks_separate_fc_launch(cuda):
-    """Native Pong A2C, 3 graph-captured updates with the fc product inside the fused step vs the separate
-    fc_rollout launch: statistics close, parameter updates equal up to the plane split's fp32 summation order (a
-    rare bf16 rounding flip of h may change a sampled action), and the fused path bitwise deterministic."""
-    from actor_critic_algs_on_tensorflow_amd import preset
-    from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
-    res = {}
-    for knob in (True, False, True):
-        cfg = preset("pong_a2c", device="cuda:0", outdir=None, quiet=True, stdout_freq=0, save_every=0,
-                     engine_opts=dict(fused_fc=knob))
-        tr = ActorCriticTrainer(cfg)
-        tr.capture(warmup=1)
-        p0 = tr.flat.data.clone()
-        for _ in range(3):
-            tr.step()
-        torch.cuda.synchronize()
-        assert tr.engine.health_errors() == []
-        out = (tr.flat.data - p0, tr.stats_buf.clone(), tr.storage.actions.clone())
-        if knob in res:
-            assert all(torch.equal(a, b) for a, b in zip(out, res[knob])), "fused fc update not deterministic"
-        res[knob] = out
-    d1, s1, a1 = res[True]
-    d0, s0, a0 = res[False]
-    assert float((a1 != a0).float().mean()) < 0.05
-    assert (d0 - d1).norm() / d0.norm() < 5e-2, float((d0 - d1).norm() / d0.norm())
-
-
 @pytest.mark.parametrize("B", [160, 7, 256, 33, 1])
 def test_fc_bwd_matches_fp64(cuda, B):
     """fc_bwd.hip: dWfc = y3^T dh (fp32, every element stored), its per-(tile, wave) sums of squares (the finaliser's
@@ -258,119 +199,6 @@ def test_fc_bwd_matches_fp64(cuda, B):
     err = (dy3.double() - ref_d).abs()
     assert bool((err <= ref_d.abs() * 2.0 ** -8 + 1e-6).all()), float(err.max())
     assert bool((dy3[y3 == 0] == 0).all())
-
-
-@pytest.mark.parametrize("B", [1, 5, 160, 700])
-def test_trunk_bwd2_matches_conv_transpose(cuda, B):
-    """trunk_bwd2.hip (32x32x16 MFMAs, weights staged once per workgroup) vs fp32 torch conv_transpose2d on the same
-    bf16 inputs: dy2 = tconv(dy3, W3) * (y2 > 0), dy1 = tconv(dy2_bf16, W2) * (y1 > 0), the per-sample bias-gradient
-    partials; bitwise reproducible and identical for every workgroup count (one per sample, 3, 256 walking)."""
-    import torch.nn.functional as F
-    from actor_critic_algs_on_tensorflow_amd import _native
-    ops = _native.require()
-    g = torch.Generator(device="cpu").manual_seed(B + 7)
-    dy3 = (torch.randn(B, 7, 7, 64, generator=g) * (torch.rand(B, 7, 7, 64, generator=g) > 0.4)).to(torch.bfloat16)
-    W3 = (torch.randn(64, 3, 3, 64, generator=g) * 0.05).to(torch.bfloat16)        # OHWI
-    W2 = (torch.randn(64, 4, 4, 32, generator=g) * 0.05).to(torch.bfloat16)
-    y2 = (torch.rand(B, 9, 9, 64, generator=g) - 0.3).clamp(min=0).to(torch.bfloat16)
-    y1 = (torch.rand(B, 20, 20, 32, generator=g) - 0.3).clamp(min=0).to(torch.bfloat16)
-    dev = [t.to(cuda) for t in (dy3, W3, y2, W2, y1)]
-    args = (dev[0].reshape(B * 49, 64), dev[1].reshape(64, 576), dev[2].reshape(B * 81, 64), dev[3].reshape(64, 512),
-            dev[4].reshape(B * 400, 32))
-    res = []
-    for max_wg in (0, 3, 256, 0):
-        dy2 = torch.full((B * 81, 64), float("nan"), dtype=torch.bfloat16, device=cuda)
-        dy1 = torch.full((B * 400, 32), float("nan"), dtype=torch.bfloat16, device=cuda)
-        bp = torch.full((B, 160), float("nan"), device=cuda)
-        ops.cnn_trunk_bwd2(*args, dy2, dy1, bp, None, max_wg)
-        torch.cuda.synchronize()
-        res.append((dy2.view(torch.int16).clone(), dy1.view(torch.int16).clone(), bp.clone()))
-    for r in res[1:]:
-        assert all(torch.equal(a, b) for a, b in zip(res[0], r))
-    dy2, dy1, bp = res[0][0].view(torch.bfloat16), res[0][1].view(torch.bfloat16), res[0][2]
-    r2 = F.conv_transpose2d(dy3.float().permute(0, 3, 1, 2), W3.float().permute(0, 3, 1, 2), stride=1)
-    r2 = r2.permute(0, 2, 3, 1) * (y2.float() > 0)
-    got2 = dy2.float().cpu().view(B, 9, 9, 64)
-    assert torch.allclose(got2, r2, rtol=2e-2, atol=2e-2), (got2 - r2).abs().max()
-    r1 = F.conv_transpose2d(got2.permute(0, 3, 1, 2), W2.float().permute(0, 3, 1, 2), stride=2)
-    r1 = r1.permute(0, 2, 3, 1) * (y1.float() > 0)
-    got1 = dy1.float().cpu().view(B, 20, 20, 32)
-    assert torch.allclose(got1, r1, rtol=2e-2, atol=2e-2), (got1 - r1).abs().max()
-    bpc = bp.cpu()
-    assert torch.allclose(bpc[:, :64], dy3.float().sum((1, 2)), rtol=1e-4, atol=1e-4)
-    assert torch.allclose(bpc[:, 64:128], got2.sum((1, 2)), rtol=1e-4, atol=1e-3)
-    assert torch.allclose(bpc[:, 128:], got1.sum((1, 2)), rtol=1e-4, atol=1e-3)
-
-
-@pytest.mark.parametrize("B,idx", [(1, False), (5, True), (37, False), (160, True)])
-def test_trunk_bwd_conv1_fold_matches_fp64(cuda, B, idx):
-    """cnn_trunk_bwd with the conv1 weight gradient folded in (W1Fold): the data-gradient outputs are bit-identical
-    to the plain kernel's, and each sample's [32, 256] plane == scale * dy1_b^T unfold(obs_b) in fp64 (the masked bf16
-    dy1 the kernel wrote, frames of row obs_idx[b] when given)."""
-    import torch.nn.functional as F
-    from actor_critic_algs_on_tensorflow_amd import _native
-    ops = _native.require()
-    g = torch.Generator(device="cpu").manual_seed(B + 11)
-    dy3 = (torch.randn(B, 7, 7, 64, generator=g) * (torch.rand(B, 7, 7, 64, generator=g) > 0.4)).to(torch.bfloat16)
-    W3 = (torch.randn(64, 3, 3, 64, generator=g) * 0.05).to(torch.bfloat16)
-    W2 = (torch.randn(64, 4, 4, 32, generator=g) * 0.05).to(torch.bfloat16)
-    y2 = (torch.rand(B, 9, 9, 64, generator=g) - 0.3).clamp(min=0).to(torch.bfloat16)
-    y1 = (torch.rand(B, 20, 20, 32, generator=g) - 0.3).clamp(min=0).to(torch.bfloat16)
-    R = 2 * B + 3 if idx else B
-    obs = torch.randint(0, 256, (R, 4, 84, 84), dtype=torch.uint8, generator=g)
-    oi = torch.randperm(R, generator=g)[:B] if idx else None
-    dev = [t.to(cuda) for t in (dy3, W3, y2, W2, y1)]
-    args = (dev[0].reshape(B * 49, 64), dev[1].reshape(64, 576), dev[2].reshape(B * 81, 64), dev[3].reshape(64, 512),
-            dev[4].reshape(B * 400, 32))
-    res = []
-    planes = torch.full((B, 32, 256), float("nan"), device=cuda)
-    for fold in (False, True):
-        dy2 = torch.full((B * 81, 64), float("nan"), dtype=torch.bfloat16, device=cuda)
-        dy1 = torch.full((B * 400, 32), float("nan"), dtype=torch.bfloat16, device=cuda)
-        bp = torch.full((B, 160), float("nan"), device=cuda)
-        if fold:
-            ops.cnn_trunk_bwd(*args, dy2, dy1, bp, None, 0, obs.to(cuda), oi.to(cuda) if idx else None, planes,
-                              1.0 / 255.0)
-        else:
-            ops.cnn_trunk_bwd(*args, dy2, dy1, bp)
-        torch.cuda.synchronize()
-        res.append((dy2.view(torch.int16).clone(), dy1.view(torch.int16).clone(), bp.clone()))
-    assert all(torch.equal(a, b) for a, b in zip(res[0], res[1]))
-    d1 = res[1][1].view(torch.bfloat16).cpu().double().view(B, 400, 32)
-    fr = obs[oi] if idx else obs
-    cols = F.unfold(fr.double(), 8, stride=4)                           # [B, 256 = (ch, ky, kx), 400]
-    ref = torch.einsum("bpo,bcp->boc", d1, cols) / 255.0
-    got = planes.cpu().double()
-    assert not torch.isnan(got).any()
-    err = float((got - ref).abs().max() / ref.abs().max())
-    assert err < 1e-5, err
-
-
-@pytest.mark.parametrize("algo,kw", [("pong_a2c", {}), ("breakout_ppo", dict(n_steps=16, ppo_minibatches=2,
-                                                                              ppo_epochs=1))])
-def test_conv1_fold_update_tracks_grouped_wgrad(cuda, algo, kw):
-    """One optimiser step with the conv1 weight gradient folded into the trunk backward (EngineOpts.conv1_fold) vs
-    the conv1 product of the grouped weight-gradient launch: same statistics, same update up to fp32 summation
-    order and the GEMM's bf16 rounding of the scaled frames."""
-    from actor_critic_algs_on_tensorflow_amd import preset
-    from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
-    res = {}
-    for knob in (True, False):
-        cfg = preset(algo, num_envs=8, device="cuda:0", outdir=None, quiet=True, stdout_freq=0, save_every=0,
-                     cuda_graph=False, optimizer="adam", engine_opts=dict(conv1_fold=knob), **kw)
-        tr = ActorCriticTrainer(cfg)
-        p0 = tr.flat.data.clone()
-        tr.step()
-        torch.cuda.synchronize()
-        assert ("W1f" in tr.engine._planes) == knob
-        res[knob] = (tr.flat.data - p0, tr.stats_buf.clone(), tr.engine.gW1.clone())
-    d1, s1, g1 = res[True]
-    d0, s0, g0 = res[False]
-    assert torch.allclose(s0[:8], s1[:8], rtol=1e-4, atol=1e-6), (s0[:8], s1[:8])
-    # the GEMM path stages the frames as bf16(pixel / 255) (relative rounding <= 2^-9); the fold multiplies exact
-    # integer pixels and scales the fp32 sums
-    assert float((g0 - g1).norm() / g0.norm()) < 5e-3
-    assert (d0 - d1).norm() / d0.norm() < 1e-2, float((d0 - d1).norm() / d0.norm())
 
 
 @pytest.mark.parametrize("B,persist", [(1100, 256), (300, 7)])

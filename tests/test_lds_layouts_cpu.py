@@ -235,49 +235,6 @@ def test_fast_divisions_are_exact_over_their_ranges():
         assert all((n * mul) >> sh == n // d for n in range(lim)), name
 
 
-def test_trunk_bwd2_reads_are_conflict_free():
-    """trunk_bwd2.hip: the 32x32x16 A fragments of dy2 (dy3 image 25 wide) and dy1 (dy2 image 26 wide; 128-byte
-    pixels, chunk ^ (pixel >> 1) & 7) at one LDS cycle per ds_read_b128 group, the W3 (chunk ^ ((row >> 1) & 1) << 2)
-    and W2 (plain 64-byte rows) transposing B reads at one cycle per 32-lane group."""
-    src = open(os.path.join(os.path.dirname(__file__), "..", "csrc", "kernels", "trunk_bwd2.hip")).read()
-    w3i, w2i = (int(v) for v in re.search(r"constexpr int B2_P3W = (\d+), B2_P2W = (\d+)", src).groups())
-    assert "return pix * 64 + ((ch ^ ((pix >> 1) & 7)) << 3);" in src and "return ((r >> 1) & 1) << 2;" in src
-    assert "p < 81 ? p : 64 + (p & 15)" in src
-    px = lambda pix, ch: pix * 128 + ((ch ^ ((pix >> 1) & 7)) * 16)
-    for mt in range(3):
-        for s in range(36):
-            t, cb0 = s // 4, (s % 4) * 16
-            ti, tj = t // 3, t % 3
-            addr = []
-            for lane in range(64):
-                m = 32 * mt + (lane & 31)
-                mm = m if m < 81 else 64 + (m & 15)
-                a, b = mm // 9, mm % 9
-                addr.append(px((a + 2 - ti) * w3i + (b + 2 - tj), (cb0 + 8 * (lane >> 5)) // 8))
-            assert cycles([[addr[x] for x in g] for g in G128], 4, 64) == 4, ("dy2", mt, s)
-    for mt in range(4):
-        for s in range(16):
-            d = s >> 2
-            di, dj, cb0 = d >> 1, d & 1, (s & 3) * 16
-            addr = []
-            for lane in range(64):
-                u = min(32 * mt + (lane & 31), 99)
-                yy, xx = u // 10, u % 10
-                addr.append(px((yy + 1 - di) * w2i + (xx + 1 - dj), (cb0 + 8 * (lane >> 5)) // 8))
-            assert cycles([[addr[x] for x in g] for g in G128], 4, 64) == 4, ("dy1", mt, s)
-    sw3 = lambda r: ((r >> 1) & 1) << 2
-    for ld, sw, col0s, nrows in ((64, sw3, (0, 32), 576), (32, lambda r: 0, (0,), 1024)):
-        for col0 in col0s:
-            for row0 in range(0, nrows, 16):
-                for hi in (0, 4):
-                    addr = []
-                    for lane in range(64):
-                        gl, q, p = lane >> 4, (lane >> 2) & 3, lane & 3
-                        r, col = row0 + 8 * (gl >> 1) + q + hi, col0 + 16 * (gl & 1) + 4 * p
-                        addr.append((r * ld + (((col >> 3) ^ sw(r)) << 3) + (col & 7)) * 2)
-                    assert cycles([[addr[x] for x in g] for g in GTR], 2, 64) == 2, (ld, col0, row0, hi)
-
-
 def _wgrad_src():
     return open(os.path.join(os.path.dirname(__file__), "..", "csrc", "kernels", "conv_wgrad.hip")).read()
 

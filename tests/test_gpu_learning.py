@@ -190,3 +190,68 @@ def test_cnn_engine_matches_autograd_at_production_batch(cuda, B, ppo):
     bar = 0.02 if B <= 256 else 0.005
     for name, err in errs.items():
         assert err < bar, (name, err, bar)
+
+
+def test_default_headline_update_matches_fp32_torch_update(cuda):
+    """Direct fp32 pin of the DEFAULT headline update (BASELINE config 2, pong_a2c, default EngineOpts, one captured
+    graph replay: fused rollout steps -> per-env A2C head -> fc_bwd -> grouped conv weight gradients -> finaliser ->
+    RMSprop with the 0.5 global-norm clip) against the reference semantics in fp32 (``Basic_AC/policies.py:72-82``:
+    loss, clip, optimiser step) computed by the torch engine: the same rollout (observations, actions, rewards,
+    dones of the replayed update), the same bf16-rounded parameters, the same optimiser state, n-step returns from
+    fp32 values, autograd of the trainer's torch loss, FusedRMSprop's plain-torch step. Every parameter tensor's
+    update must match: relative error ||dp_native - dp_torch|| / ||dp_torch|| below the bar (bf16 operands with
+    fp32 accumulation in the native engine)."""
+    from actor_critic_algs_on_tensorflow_amd import preset
+    from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
+    from actor_critic_algs_on_tensorflow_amd.ops import returns as R
+    kw = dict(device="cuda:0", outdir=None, quiet=True, stdout_freq=0, save_every=0, seed=7)
+    tr = ActorCriticTrainer(preset("pong_a2c", **kw))
+    assert tr.engine is not None and tr.engine.opts == type(tr.engine.opts)()
+    tr.capture(warmup=1)
+    assert tr.graph is not None
+    st = tr.storage
+    T, N = st.T, tr.env.num_envs
+    p0 = tr.flat.data.clone()
+    v0 = {g: o.v.clone() for g, o in tr.opts.items()}
+    phase0 = st.phase
+    tr.step()
+    torch.cuda.synchronize()
+    d_nat = tr.flat.data - p0
+    ph = st.phase
+    st.phase = phase0   # the replayed rollout's observation slots
+    obs = torch.stack([st.obs[t] for t in range(T + 1)]).clone()
+    st.phase = ph
+    act, rew, dn = st.actions.clone(), st.rewards.clone(), st.dones.clone()
+    lpo = st.logp.clone()
+    stats_nat = tr.stats_buf.clone()
+
+    ref = ActorCriticTrainer(preset("pong_a2c", engine="torch", dtype="fp32", cuda_graph=False, **kw))
+    assert ref.engine is None and ref.flat.data.numel() == p0.numel() and list(ref.opts) == list(tr.opts)
+    pb = p0.to(torch.bfloat16).float()
+    with torch.no_grad():
+        ref.flat.data.copy_(pb)
+        for g, o in ref.opts.items():
+            o.v.copy_(v0[g])
+            o.lr.copy_(tr.opts[g].lr)
+        _, v_all = ref.model(obs.view((T + 1) * N, *obs.shape[2:]))
+        ret, adv = R.nstep_returns_ref(rew, v_all.view(T + 1, N).float(), dn, tr.cfg.gamma, T)
+    ref.flat.zero_grad()
+    total, a_loss, c_loss, kl, ent, _ = ref._loss(obs[:T].reshape(T * N, *obs.shape[2:]), act.reshape(-1),
+                                                  lpo.reshape(-1), adv.reshape(-1).float(), ret.reshape(-1).float())
+    total.backward()
+    for o in ref.opts.values():
+        o._torch_step()
+    torch.cuda.synchronize()
+    d_ref = ref.flat.data - pb
+    errs = {}
+    for name, p in ref.model.named_parameters():
+        i = [id(q) for q in ref.flat.params].index(id(p))
+        off, n = ref.flat.offsets[i], p.numel()
+        a, b = d_nat[off:off + n], d_ref[off:off + n]
+        errs[name] = float((a - b).norm() / (b.norm() + 1e-20))
+    print("relative update errors", errs)
+    print("native stats", stats_nat[:8].tolist(), "torch", [float(a_loss), float(c_loss), float(ent)])
+    from actor_critic_algs_on_tensorflow_amd.algos.trainer import STAT_KEYS
+    assert float(stats_nat[STAT_KEYS.index("entropy")]) == pytest.approx(float(ent), rel=2e-2)
+    for name, err in errs.items():
+        assert err < 0.05, (name, err)

@@ -200,7 +200,7 @@ def test_default_headline_update_matches_fp32_torch_update(cuda):
     dones of the replayed update), the same bf16-rounded parameters, the same optimiser state, n-step returns from
     fp32 values, autograd of the trainer's torch loss, FusedRMSprop's plain-torch step. Every parameter tensor's
     update must match: relative error ||dp_native - dp_torch|| / ||dp_torch|| below the bar (bf16 operands with
-    fp32 accumulation in the native engine)."""
+    fp32 accumulation in the native engine; measured 0.1 % (heads) .. 2.7 % (conv1 bias), so 5 % keeps ~1.9x)."""
     from actor_critic_algs_on_tensorflow_amd import preset
     from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
     from actor_critic_algs_on_tensorflow_amd.ops import returns as R

@@ -83,9 +83,7 @@ __device__ __forceinline__ float partial_total(const float* __restrict__ parts, 
 //   ldt -1:   a FRAGMENT-ORDERED bf16 copy (the CNN engine's MFMA weight operands, cnn_fused.hip frag_w1..3): element
 //             (k, c) goes to u16 ((((k / 16) * (N / 32) + c / 32) * 64 + (c / 8 % 4) * 16 + k % 16) * 8 + c % 8), so a
 //             wave's 16-byte-per-lane fragment load is one contiguous 1 KB read;
-//   ldt -3 / -4: the MLP engine's fp32 fragment copies F (forward operand) / G (data-gradient operand), common.h
-//             mlp_frag_f / mlp_frag_g. One weight has both entries over the same range, so these entries never end
-//             the search (the others do: their ranges are disjoint).
+//   (the MLP engine's fp32 fragment copies F / G are written by the item path below, not through this table)
 constexpr int OPT_MAXT = 8;
 struct OptTrans {
   int64_t off;   // element offset of W within the segment
@@ -142,45 +140,44 @@ __device__ __forceinline__ bool write_one(const OptTrans& T, uint32_t o, float v
   return true;
 }
 
-// (the entry loops below are unrolled over compile-time indices: a loop with the runtime bound S.ntrans reads the
-// kernel-argument table through a chain of dependent scalar loads, ~1.4 us per launch of the MLP optimiser)
+// (runtime-bound entry loops: the pong / breakout segments carry 1-4 entries; the MLP segments, whose per-element
+// search through the kernel-argument table cost more than their update, take the item path instead)
 __device__ __forceinline__ void write_trans(const OptSeg& S, size_t i, float v) {
-#pragma unroll
-  for (int e = 0; e < OPT_MAXT; ++e) {
-    if (e >= S.ntrans) break;
+  for (int e = 0; e < S.ntrans; ++e) {
     const OptTrans& T = S.tr[e];
     const int64_t o = (int64_t)i - T.off;
-    if (o >= 0 && o < (int64_t)T.K * T.N && write_one(T, (uint32_t)o, v)) return;
+    if (o >= 0 && o < (int64_t)T.K * T.N) {
+      write_one(T, (uint32_t)o, v);
+      return;
+    }
   }
 }
 
-// The four consecutive elements 4 * i4 .. + 3 of a float4 group. Whole groups inside one row (offset and N multiples
-// of 4): a bf16 fragment copy (ldt -1) takes them as 4 consecutive u16 of one lane's 8 -> ONE 8-byte store (one 32-bit
-// index computation); others per element.
+// The four consecutive elements 4 * i4 .. + 3 of a float4 group: for a fragment-ordered copy (ldt -1, offset and N
+// multiples of 4) they are 4 consecutive u16 of one lane's 8 -> ONE 8-byte store (one 32-bit index computation)
+// instead of four 2-byte stores; other copies per element.
 __device__ __forceinline__ void write_trans4(const OptSeg& S, size_t i4, float4 p4) {
   const size_t i = 4 * i4;
-#pragma unroll
-  for (int e = 0; e < OPT_MAXT; ++e) {
-    if (e >= S.ntrans) break;
+  for (int e = 0; e < S.ntrans; ++e) {
     const OptTrans& T = S.tr[e];
     const int64_t o = (int64_t)i - T.off;
-    const int64_t KN = (int64_t)T.K * T.N;
-    if (o + 3 < 0 || o >= KN) continue;
-    const bool whole = o >= 0 && o + 3 < KN && ((o | T.N) & 3) == 0;
-    if (whole && T.ldt == -1) {
-      const uint32_t ou = (uint32_t)o, n = (uint32_t)T.N;
-      const uint32_t k = ou / n, c = ou - k * n;
-      const uint32_t f = (((k >> 4) * (n >> 5) + (c >> 5)) * 64u + ((c >> 3) & 3u) * 16u + (k & 15u)) * 8u + (c & 7u);
-      uint2 pk;
-      pk.x = (uint32_t)f2bf(p4.x) | ((uint32_t)f2bf(p4.y) << 16);
-      pk.y = (uint32_t)f2bf(p4.z) | ((uint32_t)f2bf(p4.w) << 16);
-      *reinterpret_cast<uint2*>(reinterpret_cast<u16*>(T.dst) + f) = pk;
+    if (o + 3 >= 0 && o < (int64_t)T.K * T.N) {
+      if (T.ldt < 0 && o >= 0 && o + 3 < (int64_t)T.K * T.N && ((o | T.N) & 3) == 0) {
+        const uint32_t ou = (uint32_t)o, n = (uint32_t)T.N;
+        const uint32_t k = ou / n, c = ou - k * n;
+        const uint32_t f = (((k >> 4) * (n >> 5) + (c >> 5)) * 64u + ((c >> 3) & 3u) * 16u + (k & 15u)) * 8u + (c & 7u);
+        uint2 pk;
+        pk.x = (uint32_t)f2bf(p4.x) | ((uint32_t)f2bf(p4.y) << 16);
+        pk.y = (uint32_t)f2bf(p4.z) | ((uint32_t)f2bf(p4.w) << 16);
+        *reinterpret_cast<uint2*>(reinterpret_cast<u16*>(T.dst) + f) = pk;
+        return;
+      }
+      write_trans(S, i, p4.x);
+      write_trans(S, i + 1, p4.y);
+      write_trans(S, i + 2, p4.z);
+      write_trans(S, i + 3, p4.w);
       return;
     }
-    const float pv[4] = {p4.x, p4.y, p4.z, p4.w};   // (a group straddling two entries: each takes its part)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (o + j >= 0 && o + j < KN) write_one(T, (uint32_t)(o + j), pv[j]);
   }
 }
 
@@ -361,13 +358,17 @@ __device__ __forceinline__ void opt_items(const OptSeg& S, float b1, float b2, f
 
 // U float4 groups per thread per round; the first round's operands are requested BEFORE the global-norm reduction
 // (its partial loads + block sum would otherwise be a dependent round trip ahead of every element load).
-template <bool ADAM, int U>
+// ITEMS: the item path is compiled in (the grouped launch of the MLP optimisers); the plain launch leaves it out --
+// its code and LDS tile raised the sweep's registers and cost the headline RMSprop step ~30 % (12.5 -> 16.3 us).
+template <bool ADAM, int U, bool ITEMS>
 __device__ __forceinline__ void opt_body(const OptSeg& S, float b1, float b2, float eps, int zero_grad, int vblk,
                                          int vgrid, int* flag, float* shr, u16* kcs, float* blks) {
   if (S.gate && *S.gate == 0) return;   // uniform over the launch
-  if (S.items) {
-    opt_items<ADAM>(S, b1, b2, eps, zero_grad, vblk, vgrid, shr, blks);
-    return;
+  if constexpr (ITEMS) {
+    if (S.items) {
+      opt_items<ADAM>(S, b1, b2, eps, zero_grad, vblk, vgrid, shr, blks);
+      return;
+    }
   }
   auto stamp = [&](int k) {
     if (S.stamps && threadIdx.x == 0) S.stamps[(size_t)(S.wg0 + vblk) * 8 + k] = __builtin_amdgcn_s_memrealtime();
@@ -530,8 +531,7 @@ __global__ void __launch_bounds__(OPT_THREADS) opt_kernel(OptSeg S, float b1, fl
   __shared__ int flag;
   __shared__ float shr[16];
   __shared__ __attribute__((aligned(16))) u16 kcs[OPT_THREADS / 64 * 256];
-  __shared__ __attribute__((aligned(16))) float blks[16 * BLK_LD];
-  opt_body<ADAM, U>(S, b1, b2, eps, zero_grad, blockIdx.x, gridDim.x, &flag, shr, kcs, blks);
+  opt_body<ADAM, U, false>(S, b1, b2, eps, zero_grad, blockIdx.x, gridDim.x, &flag, shr, kcs, nullptr);
 }
 
 // Several parameter groups (e.g. the reference's separate actor and critic optimisers) in ONE launch: the grid is
@@ -551,7 +551,7 @@ __global__ void __launch_bounds__(OPT_THREADS) opt_multi_kernel(OptMulti M, floa
   __shared__ __attribute__((aligned(16))) float blks[16 * BLK_LD];
   int b = blockIdx.x, k = 0;
   while (k + 1 < M.nseg && b >= M.seg[k].nblocks) b -= M.seg[k++].nblocks;
-  opt_body<ADAM, 1>(M.seg[k], b1, b2, eps, zero_grad, b, M.seg[k].nblocks, &flag, shr, kcs, blks);
+  opt_body<ADAM, 1, true>(M.seg[k], b1, b2, eps, zero_grad, b, M.seg[k].nblocks, &flag, shr, kcs, blks);
 }
 
 // Gradient finaliser: the last step of a backward pass before the optimiser. Gradient segments are either

@@ -65,6 +65,37 @@ class DataParallel:
         # gloo collectives run on the host, so a captured gloo update is a chain of graphs cut at each one.
         self.backend = dist.get_backend(group)
         self.issued = 0   # collectives issued from the host (a replayed one-graph update issues none)
+        # RCCL: the stream-ordered all-reduces go straight to the process group's communicator ON THE CURRENT STREAM
+        # (native rccl_allreduce) instead of through torch's collective, which runs on the group's internal stream
+        # joined to the compute stream by two events -- graph edges that cost more than the all-reduce itself at the
+        # per-minibatch gradient sizes (profiles/r6_dp_world1.txt). The async form (allreduce_async, overlapped with
+        # compute) keeps torch's stream.
+        # (while an async collective is outstanding on the group's stream, the stream-ordered ones go there too: two
+        # collectives of one communicator must never run concurrently on two streams)
+        self._comm = self._direct_comm() if self.backend == "nccl" else 0
+        self._pending = 0
+
+    def _direct_comm(self):
+        from .. import _native
+        if not (torch.cuda.is_available() and _native.available()):
+            return 0
+        dev = torch.device("cuda", torch.cuda.current_device())
+        pg = self.group if self.group is not None else dist.distributed_c10d._get_default_group()
+        try:
+            # the communicator exists from init when the group was created with a device_id (init_from_env does
+            # that); otherwise it is created lazily by torch and this returns 0 (torch's collectives are used)
+            return int(pg._get_backend(dev)._comm_ptr())
+        except (AttributeError, RuntimeError):
+            return 0
+
+    def _allreduce_now(self, t):
+        """Stream-ordered in-place SUM all-reduce of ``t`` (on the current stream when the communicator is ours)."""
+        self.issued += 1
+        if self._comm and not self._pending:
+            from .. import _native
+            _native.require().rccl_allreduce(t, self._comm)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
 
     # -- gradient buckets (optionally bf16) ----------------------------------------------------------------------
     def prepare(self, grad):
@@ -92,8 +123,7 @@ class DataParallel:
     @torch.no_grad()
     def allreduce_packed(self, grad, s=0, e=None):
         """Synchronous (stream-ordered) SUM all-reduce of the packed range."""
-        self.issued += 1
-        dist.all_reduce(self.comm_view(grad, s, e), op=dist.ReduceOp.SUM, group=self.group)
+        self._allreduce_now(self.comm_view(grad, s, e))
 
     # -- parameters ---------------------------------------------------------------------------------------------
     @torch.no_grad()
@@ -126,7 +156,8 @@ class DataParallel:
         work already queued on the current stream, and returns the work handle. ``handle.wait()`` makes the
         *current stream* wait for it (no host block), so the caller keeps queueing compute that overlaps it."""
         self.issued += 1
-        return dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        self._pending += 1
+        return _Work(self, dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
 
     # -- statistics ---------------------------------------------------------------------------------------------
     @torch.no_grad()
@@ -149,8 +180,11 @@ class DataParallel:
     def allreduce_sum_(self, t):
         """In-place SUM all-reduce of a small device tensor (e.g. the packed fp64 return-scan moments): no host
         round trip, capturable."""
-        self.issued += 1
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        if t.dtype in (torch.float32, torch.bfloat16, torch.float64) and t.is_contiguous():
+            self._allreduce_now(t)
+        else:
+            self.issued += 1
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
         return t
 
     @torch.no_grad()
@@ -167,3 +201,17 @@ class DataParallel:
 
     def barrier(self):
         dist.barrier(group=self.group)
+
+
+class _Work:
+    """Handle of an async all-reduce; ``wait()`` joins it to the current stream and lets the stream-ordered
+    collectives take the direct path again."""
+
+    def __init__(self, dp, work):
+        self._dp, self._work, self._open = dp, work, True
+
+    def wait(self):
+        self._work.wait()
+        if self._open:
+            self._open = False
+            self._dp._pending -= 1

@@ -64,7 +64,7 @@ def write_ninja(verbose=False):
     w(f"bflags = -O2 -std=c++17 -fPIC -D__HIP_PLATFORM_AMD__=1 -DUSE_ROCM=1 -D_GLIBCXX_USE_CXX11_ABI={abi} "
       f"-isystem {ROCM}/include {binc} -I{ROOT}/csrc/kernels -Wno-deprecated-declarations")
     w(f"tbflags = -O2 -std=c++17 -fPIC -isystem {py_inc} -isystem {_pybind_include()} -I{ROOT}/csrc/tfbundle")
-    w(f"ldflags = -shared -L{tlib} -Wl,-rpath,{tlib} -lamdhip64 -lc10 -lc10_hip -ltorch -ltorch_cpu -ltorch_hip")
+    w(f"ldflags = -shared -L{tlib} -Wl,-rpath,{tlib} -lamdhip64 -lc10 -lc10_hip -ltorch -ltorch_cpu -ltorch_hip -lrccl")
     w("rule hipcc\n  command = $hipcc $kflags $extra -c $in -o $out\n  description = HIPCC $in")
     w("rule cxx\n  command = $cxx $bflags -c $in -o $out\n  description = CXX $in")
     w("rule tbcxx\n  command = $cxx $tbflags -c $in -o $out\n  description = CXX $in")

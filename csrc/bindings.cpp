@@ -9,6 +9,7 @@
 #include <torch/library.h>
 
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <cstdint>
 #include <cstring>
@@ -1241,6 +1242,24 @@ void opt_multi(Tensor words, Tensor fvals, c10::optional<Tensor> trans, bool ada
         "opt_multi");
 }
 
+// In-place SUM all-reduce of a contiguous fp32 / bf16 / fp64 device tensor through an RCCL communicator (the one torch's
+// ProcessGroupNCCL owns, passed as its address: ProcessGroupNCCL._comm_ptr()) ON THE CALLER'S STREAM. A torch
+// collective runs on the process group's internal stream joined by two events to the compute stream; inside a captured
+// update those cross-stream edges cost more than the all-reduce itself at the MLP engine's gradient sizes
+// (profiles/r6_dp_world1.txt). Issued in program order on every rank, like the process group's own collectives.
+void rccl_allreduce(Tensor buf, int64_t comm) {
+  TORCH_CHECK(buf.is_cuda() && buf.is_contiguous(), "rccl_allreduce: contiguous device tensor");
+  TORCH_CHECK(comm != 0, "rccl_allreduce: no communicator");
+  ncclDataType_t dt;
+  if (buf.scalar_type() == at::kFloat) dt = ncclFloat32;
+  else if (buf.scalar_type() == at::kBFloat16) dt = ncclBfloat16;
+  else if (buf.scalar_type() == at::kDouble) dt = ncclFloat64;
+  else TORCH_CHECK(false, "rccl_allreduce: fp32, bf16 or fp64");
+  const ncclResult_t r = ncclAllReduce(buf.data_ptr(), buf.data_ptr(), (size_t)buf.numel(), dt, ncclSum,
+                                       reinterpret_cast<ncclComm_t>(comm), cur_stream(buf));
+  TORCH_CHECK(r == ncclSuccess, "rccl_allreduce: ", ncclGetErrorString(r));
+}
+
 void grad_move(Tensor src, Tensor dst, c10::optional<Tensor> gate) {
   need(src, at::kFloat, "src");
   need(dst, at::kFloat, "dst");
@@ -2001,6 +2020,7 @@ TORCH_LIBRARY(acamd, m) {
         "float norm_mul=1.0, Tensor? trans=None) -> ()");
   m.def("cast_bf16(Tensor x, Tensor y) -> ()");
   m.def("grad_move(Tensor src, Tensor dst, Tensor? gate=None) -> ()");
+  m.def("rccl_allreduce(Tensor buf, int comm) -> ()");
   m.def("opt_multi(Tensor words, Tensor fvals, Tensor? trans, bool adam, float b1, float b2, float eps, bool zero_grad, "
         "Tensor stream_ref, int t_off=-1) -> ()");
   m.def("prp_perm(Tensor out, int seed, Tensor uc, int epoch) -> ()");
@@ -2098,6 +2118,7 @@ TORCH_LIBRARY_IMPL(acamd, CUDA, m) {
   m.impl("rmsprop_step", &rmsprop_step);
   m.impl("cast_bf16", &cast_bf16);
   m.impl("grad_move", &grad_move);
+  m.impl("rccl_allreduce", &rccl_allreduce);
   m.impl("opt_multi", &opt_multi);
   m.impl("mlp_fwd", &mlp_fwd);
   m.impl("prp_perm", &prp_perm);

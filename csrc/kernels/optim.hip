@@ -21,6 +21,7 @@ constexpr int SUMSQ_PARTS = 256;   // max sumsq workgroups = partial slots the o
 
 // Partial sums of squares of x over `nblk` workgroups (this one: `bid`), one partial slot each; slot `nblk` .. are
 // zeroed by workgroup 0 so the consumer always sums SUMSQ_PARTS entries in a fixed order.
+template <int U = SUMSQ_U>
 __device__ __forceinline__ void sumsq_body(const float* __restrict__ x, size_t n, float* __restrict__ partial,
                                            int nblk, int bid, float* sh) {
   float s = 0.f;
@@ -28,16 +29,16 @@ __device__ __forceinline__ void sumsq_body(const float* __restrict__ x, size_t n
   const float4* x4 = reinterpret_cast<const float4*>(x);
   // SUMSQ_U independent 16-byte loads in flight per thread before any use: the grid is capped at one workgroup
   // per CU, so latency (not bandwidth) bounds a one-load-at-a-time loop
-  const size_t step = (size_t)nblk * blockDim.x * SUMSQ_U;
-  for (size_t i0 = bid * (size_t)blockDim.x * SUMSQ_U + threadIdx.x; i0 < n4; i0 += step) {
-    float4 v[SUMSQ_U];
+  const size_t step = (size_t)nblk * blockDim.x * U;
+  for (size_t i0 = bid * (size_t)blockDim.x * U + threadIdx.x; i0 < n4; i0 += step) {
+    float4 v[U];
 #pragma unroll
-    for (int u = 0; u < SUMSQ_U; ++u) {
+    for (int u = 0; u < U; ++u) {
       const size_t i = i0 + (size_t)u * blockDim.x;
       v[u] = i < n4 ? x4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
-    for (int u = 0; u < SUMSQ_U; ++u) s += v[u].x * v[u].x + v[u].y * v[u].y + v[u].z * v[u].z + v[u].w * v[u].w;
+    for (int u = 0; u < U; ++u) s += v[u].x * v[u].x + v[u].y * v[u].y + v[u].z * v[u].z + v[u].w * v[u].w;
   }
   if (bid == 0) {
     for (size_t i = n4 * 4 + threadIdx.x; i < n; i += blockDim.x) s += x[i] * x[i];
@@ -54,7 +55,9 @@ __global__ void __launch_bounds__(OPT_THREADS) sumsq_kernel(const float* __restr
 }
 
 // Several independent sums of squares in ONE launch (the separate actor / critic norms of a data-parallel MLP
-// update): blockIdx.y = segment, each with the workgroup count a single sumsq launch would use (same partials).
+// update, per minibatch: tens of thousands of elements): blockIdx.y = segment, SUMSQ_MU float4 per thread -- one
+// memory round trip over more workgroups instead of the 8-deep loop over 5 (4.8 -> ~2 us, profiles/r6_dp_world1.txt).
+constexpr int SUMSQ_MU = 2;
 struct SumsqSegs {
   const float* x[4];
   float* partial[4];
@@ -65,7 +68,7 @@ __global__ void __launch_bounds__(OPT_THREADS) sumsq_multi_kernel(SumsqSegs a) {
   __shared__ float sh[16];
   const int g = blockIdx.y;
   if ((int)blockIdx.x >= a.nblk[g]) return;
-  sumsq_body(a.x[g], a.n[g], a.partial[g], a.nblk[g], blockIdx.x, sh);
+  sumsq_body<SUMSQ_MU>(a.x[g], a.n[g], a.partial[g], a.nblk[g], blockIdx.x, sh);
 }
 
 // Global squared norm from the sumsq partials, reduced by every consumer workgroup in the same fixed order
@@ -901,7 +904,7 @@ extern "C" hipError_t aca_sumsq_multi(const float* const* xs, const size_t* ns, 
   int gx = 1;
   for (int g = 0; g < nseg; ++g) {
     if (reinterpret_cast<uintptr_t>(xs[g]) % 16) return hipErrorInvalidValue;
-    int grid = (int)((ns[g] / 4 + OPT_THREADS * SUMSQ_U - 1) / (OPT_THREADS * SUMSQ_U));
+    int grid = (int)((ns[g] / 4 + OPT_THREADS * SUMSQ_MU - 1) / (OPT_THREADS * SUMSQ_MU));
     if (grid < 1) grid = 1;
     if (grid > SUMSQ_PARTS) grid = SUMSQ_PARTS;
     a.x[g] = xs[g];

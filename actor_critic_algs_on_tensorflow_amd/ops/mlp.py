@@ -14,7 +14,7 @@ per 16 rows with its activations in LDS, on f32 MFMA:
 * :meth:`MLPEngine.evaluate` / :meth:`value` -- log-prob / entropy of given actions and values (post-update KL proxy
   and EV of the reference, ``Basic_AC/run_AC.py:257-258``; bootstrap values).
 * :meth:`MLPEngine.rollout_linear` -- the whole T-step rollout of the MuJoCo-shaped bank in ONE persistent launch
-  (actor + sampling + env dynamics + frame stack per 16-env workgroup, ``mlp_rollout_kernel``) followed by ONE
+  (actor on 4x4x1 MFMA tiles + sampling + env dynamics + frame stack per 4-env workgroup, ``mlp_rollout_kernel``) followed by ONE
   batched critic launch over all ``(T+1) N`` observations (the rollout's Session.run-per-step loop of
   ``Basic_AC/run_AC.py:82-107``).
 
@@ -292,14 +292,17 @@ class MLPEngine:
     def supports_fused_rollout(self, env):
         from ..envs.mujoco import MujocoShapeVecEnv
         return (isinstance(env, MujocoShapeVecEnv) and not self.discrete and self.A == LIN_ACT
-                and self.D == LIN_OBS * env.frame_stack)
+                and self.D == LIN_OBS * env.frame_stack and env.frame_stack <= 3 and self.rollout_weights_in_lds()
+                and [l.out_features for l in self.towers[0]] == [128, 128, 64, LIN_ACT])   # mlp_rollout_kernel shapes
 
-    ROLLOUT_MAX_LDS = 152 * 1024
+    ROLLOUT_MAX_LDS = 150 * 1024
+    ROLL_RB = 4   # envs per rollout workgroup (mlp.hip ROLL_RB: 4x4x1 MFMA tiles)
 
     def rollout_lds_bytes(self, wlds):
         """Dynamic LDS of mlp_rollout_kernel (layout in mlp.hip); ``wlds`` adds the staged actor weights + biases."""
-        n = 2 * BM * _ld(self.D) + sum(BM * _ld(l.out_features) for l in self.towers[0])
-        n += LIN_OBS * LIN_OBS + LIN_OBS * LIN_ACT + BM * LIN_OBS + BM * 16
+        RB = self.ROLL_RB
+        n = 2 * RB * _ld(self.D) + sum(RB * _ld(l.out_features) for l in self.towers[0])
+        n += LIN_OBS * LIN_OBS + LIN_OBS * LIN_ACT + RB * LIN_OBS + RB * 16
         if wlds:
             n = (n + 3) // 4 * 4 + sum(l.out_features * _ld(l.in_features) + _ld(l.out_features) - 4
                                        for l in self.towers[0])
@@ -310,7 +313,8 @@ class MLPEngine:
 
     def rollout_linear(self, env, st, key_shift, seed, stamps=None):
         """T steps of policy + env for the whole bank in one launch, then V(s) of all (T+1) N observations in one
-        critic launch. Bit-identical to T x (:meth:`policy_step` + ``env.step``) + :meth:`value`."""
+        critic launch. Equal to T x (:meth:`policy_step` + ``env.step``) + :meth:`value` up to the actor's fp32
+        summation order (4x4x1 tiles with the K range split over waves vs 16x16x4 tiles): same RNG keys and resets."""
         T, N = st.T, env.num_envs
         desc, _ = self.desc(None)
         wlds = self.rollout_weights_in_lds()

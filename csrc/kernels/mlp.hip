@@ -1288,78 +1288,103 @@ __device__ __forceinline__ float lin_reset(float u) {
   return (u - 0.5f) * 0.2f;
 }
 
-// Y = act(X W + b) with the transposed weights W[N][ldw] and the bias in LDS (ldw = 16*NG + 4: consecutive output
-// columns land 4 banks apart, so a 16-byte fragment read is conflict-free). No global memory at all.
-template <int NG>
-__device__ void layer_fwd_lds_t(const float* __restrict__ X, int ldx, const float* __restrict__ W, int ldw,
-                                const float* __restrict__ bias, int N, int act, float* __restrict__ Y, int ldy,
-                                int64_t* dbg) {
+// The rollout's tile is ROLL_RB = 4 envs: its per-step chain is bound by the f32 MFMA work of ONE CU (16 env rows on
+// 16x16x4 tiles: 0.86 MFLOP = 3.4k clocks per step at the CU's 256 FLOP/clk, ~4.5 of 6.3 us measured), so 4-env
+// workgroups on the 4x4x1 MFMA (16 blocks of 4 x 4, k = 1: one instruction = 4 env rows x 64 columns, no padded rows)
+// spread the rollout over 4x the CUs. Lane 4 b + i supplies A[i][k] (env row i), lane 4 b + j B[k][j] (column
+// 4 b + j of the 64-column group), and lane 4 b + j receives D[0..3][j] (scripts/probes/mfma4x4.hip).
+constexpr int ROLL_RB = 4;
+__device__ __forceinline__ floatx4 mfma4x4(float a, float b, floatx4 c) {
+  return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 0, 0, 0);
+}
+
+// One actor layer of the rollout step: Y[4][ldy] = act(X[4][ldx] W + b). The 8 waves split (64-column group cg, K
+// range sp); each wave holds ITS slice of W -- column cg * 64 + lane, rows [sp * kper, (sp + 1) * kper), as kper / 4
+// float4 -- in registers for the whole rollout (loaded once before the step loop: the step reads no weight bytes at
+// all), reads its env rows' X float4s from LDS up front, and runs kper 4x4x1 MFMAs; the partial tiles meet in LDS
+// (`red`) and the epilogue sums them in K order, adds the bias, applies the activation and writes the zero pad columns
+// [N, 16 ngp2(N)) that the next layer's K pad reads.
+template <int K_, int N_>   // K_ padded (16 ngp2(K)), N_ <= 256
+struct RollLayer {
+  static constexpr int CG = (N_ + 63) / 64;                                              // column groups
+  static constexpr int S = MLP_THREADS / 64 / CG < K_ / 4 ? MLP_THREADS / 64 / CG : K_ / 4;   // K splits
+  static constexpr int kper = K_ / S, NU = kper / 4;                                     // K rows / float4 per wave
+};
+
+template <class L>
+__device__ __forceinline__ void roll_layer_load_w(float4 (&w)[L::NU], const float* __restrict__ W, int ldw, int N) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int r = lane & 15, q = lane >> 4;
-  const int ntile = ngp2(N);
-  if (dbg && lane == 0) dbg[wave * 8 + 0] = __builtin_amdgcn_s_memtime();
-  for (int tile = wave; tile < ntile; tile += MLP_THREADS / 64) {
-    const int c = tile * 16 + r;
-    const bool cok = c < N;
-    const int cc = cok ? c : N - 1;
-    const float* wrow = W + cc * ldw + 4 * q;
-    floatx4 bv[NG];
+  const int cg = wave % L::CG, sp = wave / L::CG;
+  const int c = min(cg * 64 + lane, N - 1);
 #pragma unroll
-    for (int g = 0; g < NG; ++g) bv[g] = *reinterpret_cast<const floatx4*>(wrow + 16 * g);
+  for (int u = 0; u < L::NU; ++u) w[u] = *reinterpret_cast<const float4*>(W + c * ldw + sp * L::kper + 4 * u);
+}
+
+template <class L>
+__device__ __forceinline__ void roll_layer_mfma(const float4 (&w)[L::NU], const float* __restrict__ X, int ldx,
+                                                float* __restrict__ red) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (wave < L::CG * L::S) {
+    const int sp = wave / L::CG;
+    const float* xr = X + (lane & 3) * ldx + sp * L::kper;
+    float4 x[L::NU];
+#pragma unroll
+    for (int u = 0; u < L::NU; ++u) x[u] = *reinterpret_cast<const float4*>(xr + 4 * u);
     floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-    const float* Xr = X + r * ldx + 4 * q;
 #pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      const float4 a4 = *reinterpret_cast<const float4*>(&Xr[16 * g]);
-      acc = mfma4(a4.x, bv[g][0], acc);
-      acc = mfma4(a4.y, bv[g][1], acc);
-      acc = mfma4(a4.z, bv[g][2], acc);
-      acc = mfma4(a4.w, bv[g][3], acc);
+    for (int u = 0; u < L::NU; ++u) {
+      acc = mfma4x4(x[u].x, w[u].x, acc);
+      acc = mfma4x4(x[u].y, w[u].y, acc);
+      acc = mfma4x4(x[u].z, w[u].z, acc);
+      acc = mfma4x4(x[u].w, w[u].w, acc);
     }
-    const float bb = bias[cc];
-    const float slope = act_slope(act);
-    if (dbg && lane == 0) dbg[wave * 8 + 1] = __builtin_amdgcn_s_memtime();
 #pragma unroll
-    for (int i = 0; i < 4; ++i) Y[(4 * q + i) * ldy + c] = cok ? act_fwd(acc[i] + bb, slope) : 0.f;
-    if (dbg && lane == 0) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the epilogue's LDS stores (and so the MFMA results) done
-      dbg[wave * 8 + 2] = __builtin_amdgcn_s_memtime();
-    }
+    for (int i = 0; i < 4; ++i) red[(wave * 4 + i) * 64 + lane] = acc[i];
   }
 }
 
-__device__ __forceinline__ void layer_fwd_lds(const float* X, int ldx, int K, const float* W, const float* bias, int N,
-                                              int act, float* Y, int ldy, int64_t* dbg = nullptr) {
-  const int ldw = 16 * ngp2(K) + 4;
-  switch (ngp2(K)) {
-    case 1: layer_fwd_lds_t<1>(X, ldx, W, ldw, bias, N, act, Y, ldy, dbg); break;
-    case 2: layer_fwd_lds_t<2>(X, ldx, W, ldw, bias, N, act, Y, ldy, dbg); break;
-    case 4: layer_fwd_lds_t<4>(X, ldx, W, ldw, bias, N, act, Y, ldy, dbg); break;
-    case 8: layer_fwd_lds_t<8>(X, ldx, W, ldw, bias, N, act, Y, ldy, dbg); break;
-    default: layer_fwd_lds_t<16>(X, ldx, W, ldw, bias, N, act, Y, ldy, dbg); break;
+template <class L>
+__device__ __forceinline__ void roll_layer_epilogue(const float* __restrict__ red, const float* __restrict__ bias,
+                                                    int N, int act, float* __restrict__ Y, int ldy) {
+  const float slope = act_slope(act);
+  const int NP = 16 * ngp2(N);
+  for (int e = threadIdx.x; e < ROLL_RB * NP; e += MLP_THREADS) {
+    const int i = e / NP, c = e - i * NP;
+    float v = 0.f;
+    if (c < N) {
+      const int cg = c >> 6, l = c & 63;
+      float sum = 0.f;
+#pragma unroll
+      for (int sp = 0; sp < L::S; ++sp) sum += red[((sp * L::CG + cg) * 4 + i) * 64 + l];
+      v = act_fwd(sum + bias[c], slope);
+    }
+    Y[i * ldy + c] = v;
   }
 }
 
-// WLDS: the actor's weights and biases are staged in LDS once (the reference actor at D = 17 is ~120 KB, SURVEY
-// §2.4 K01), so the step loop issues no global loads at all. That matters beyond the load latency: on gfx9 global
-// stores count on vmcnt too, so every wait for a load issued after the previous step's stores (observations,
-// actions, rewards) would first drain those stores. The descriptor, head parameters and env ids are staged as well.
-// !WLDS (wider frame stacks): weights stream from the L2-resident transposed shadows.
-template <bool WLDS>
+// The actor's weights and biases are staged in LDS once (the reference actor at D = 17 is ~120 KB, SURVEY §2.4 K01;
+// ops/mlp.py takes this kernel only when they fit), so the step loop issues no global loads at all. That matters
+// beyond the load latency: on gfx9 global stores count on vmcnt too, so every wait for a load issued after the
+// previous step's stores (observations, actions, rewards) would first drain those stores. The descriptor, head
+// parameters and env ids are staged as well.
+// KP0: the padded observation width (32 / 64: frame stacks of 1 / 2-3); the actor is the reference's 128-128-64-A
+// (ops/mlp.py supports_fused_rollout)
+template <int KP0>
 __global__ void __launch_bounds__(MLP_THREADS) mlp_rollout_kernel(RolloutArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm[];   // 16-byte base: the b128 LDS reads stay aligned
-  __shared__ int64_t s_tg[MLP_BM];
-  __shared__ int64_t s_ids[MLP_BM];
-  __shared__ int s_t[MLP_BM];
-  __shared__ float s_er[MLP_BM];
+  __shared__ int64_t s_tg[ROLL_RB];
+  __shared__ int64_t s_ids[ROLL_RB];
+  __shared__ int s_t[ROLL_RB];
+  __shared__ float s_er[ROLL_RB];
   __shared__ float s_ls[MLP_MAXA], s_sc[MLP_MAXA];
-  __shared__ float s_hl[MLP_BM * MLP_MAXA];
+  __shared__ float s_hl[ROLL_RB * MLP_MAXA];
   __shared__ int s_in[MLP_MAXL], s_out[MLP_MAXL], s_actc[MLP_MAXL];
   __shared__ int64_t s_wt[MLP_MAXL], s_b[MLP_MAXL];
+  __shared__ float s_red[MLP_THREADS / 64 * 4 * 64];   // the layers' partial tiles (roll_layer_mfma)
   const MlpTower& T = a.tw[0];
   const int nl = (int)T.nl;
-  const int row0 = blockIdx.x * MLP_BM;
-  const int rows = min(MLP_BM, a.N - row0);
+  const int row0 = blockIdx.x * ROLL_RB;
+  const int rows = min(ROLL_RB, a.N - row0);
   const int tid = threadIdx.x;
   const int A = a.A, D = a.D;
   const int ld0 = ld_of(D);
@@ -1374,7 +1399,7 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_rollout_kernel(RolloutArgs a)
     s_ls[tid] = tid < A ? fminf(fmaxf(a.log_std[tid], -2.5f), 2.5f) : 0.f;
     s_sc[tid] = tid < A ? a.ac_scale[tid] : 0.f;
   }
-  if (tid < MLP_BM) {
+  if (tid < ROLL_RB) {
     const bool live = tid < rows;
     s_tg[tid] = live ? a.tg[row0 + tid] : 0;
     s_ids[tid] = live ? a.env_ids[row0 + tid] : 0;
@@ -1388,16 +1413,16 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_rollout_kernel(RolloutArgs a)
   };
   auto ldyf = [&](int l) { return ld_of(s_out[l]); };
   auto Yp = [&](int l) {
-    int off = 2 * MLP_BM * ld0;
-    for (int j = 0; j < l; ++j) off += MLP_BM * ldyf(j);
+    int off = 2 * ROLL_RB * ld0;
+    for (int j = 0; j < l; ++j) off += ROLL_RB * ldyf(j);
     return sm + off;
   };
-  // LDS: obs tile x2 | Y_0 .. Y_{nl-1} | A | B | env state [16][17] | actions [16][16] | (WLDS) W_l, b_l per layer
+  // LDS: obs tile x2 | Y_0 .. Y_{nl-1} | A | B | env state [4][17] | actions [4][16] | W_l, b_l per layer
   float* sA = Yp(nl);
   float* sB = sA + LIN_OBS * LIN_OBS;
   float* s_state = sB + LIN_OBS * LIN_ACT;
-  float* s_act = s_state + MLP_BM * LIN_OBS;
-  float* s_w0 = sm + (((s_act - sm) + MLP_BM * MLP_MAXA + 3) & ~3);   // 16-byte aligned (b128 reads)
+  float* s_act = s_state + ROLL_RB * LIN_OBS;
+  float* s_w0 = sm + (((s_act - sm) + ROLL_RB * MLP_MAXA + 3) & ~3);   // 16-byte aligned (b128 reads)
   auto Wl = [&](int l) {
     float* p = s_w0;
     for (int j = 0; j < l; ++j) p += s_out[j] * (16 * ngp2(s_in[j]) + 4) + 16 * ngp2(s_out[j]);
@@ -1410,7 +1435,7 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_rollout_kernel(RolloutArgs a)
     for (int l = 0; l <= nl; ++l) s_yo[l] = (int)(Yp(l) - sm);
     for (int l = 0; l < nl; ++l) s_wo[l] = (int)(Wl(l) - sm);
   }
-  if (WLDS) {   // W_l [out][16*ngp2(in) + 4] (transposed, from the zero-padded forward fragment copy), then b_l
+  {   // W_l [out][16*ngp2(in) + 4] (transposed, from the zero-padded forward fragment copy), then b_l
     for (int l = 0; l < nl; ++l) {
       const int NG = ngp2(s_in[l]), K4 = 4 * NG, N = s_out[l], ldw = 16 * NG + 4;
       float* w = Wl(l);
@@ -1425,7 +1450,7 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_rollout_kernel(RolloutArgs a)
       for (int e = tid; e < 16 * ngp2(N); e += MLP_THREADS) b[e] = e < N ? bsrc[e] : 0.f;
     }
   }
-  for (int e = tid; e < 2 * MLP_BM * ld0; e += MLP_THREADS) {   // step-0 tile (+ a zeroed second buffer)
+  for (int e = tid; e < 2 * ROLL_RB * ld0; e += MLP_THREADS) {   // step-0 tile (+ a zeroed second buffer)
     const int r = e / ld0, c = e - r * ld0;
     float v = 0.f;
     if (r < rows && c < D) v = a.obs[(size_t)(row0 + r) * D + c];
@@ -1433,39 +1458,53 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_rollout_kernel(RolloutArgs a)
   }
   for (int j = tid; j < LIN_OBS * LIN_OBS; j += MLP_THREADS) sA[j] = a.lin_A[j];
   for (int j = tid; j < LIN_OBS * LIN_ACT; j += MLP_THREADS) sB[j] = a.lin_B[j];
-  for (int e = tid; e < MLP_BM * LIN_OBS; e += MLP_THREADS)
+  for (int e = tid; e < ROLL_RB * LIN_OBS; e += MLP_THREADS)
     s_state[e] = e / LIN_OBS < rows ? a.state[(size_t)row0 * LIN_OBS + e] : 0.f;
-  for (int e = tid; e < MLP_BM * MLP_MAXA; e += MLP_THREADS) s_act[e] = 0.f;
+  for (int e = tid; e < ROLL_RB * MLP_MAXA; e += MLP_THREADS) s_act[e] = 0.f;
   __syncthreads();
+  // every wave's weight slices of the four layers, in registers for the whole rollout
+  using L0 = RollLayer<KP0, 128>;
+  using L1 = RollLayer<128, 128>;
+  using L2 = RollLayer<128, 64>;
+  using L3 = RollLayer<64, 16>;
+  float4 w0[L0::NU], w1[L1::NU], w2[L2::NU], w3[L3::NU];
+  roll_layer_load_w<L0>(w0, sm + s_wo[0], KP0 + 4, s_out[0]);
+  roll_layer_load_w<L1>(w1, sm + s_wo[1], 132, s_out[1]);
+  roll_layer_load_w<L2>(w2, sm + s_wo[2], 132, s_out[2]);
+  roll_layer_load_w<L3>(w3, sm + s_wo[3], 68, s_out[3]);
+  auto bias_of = [&](int l, int ldw) { return sm + s_wo[l] + s_out[l] * ldw; };
   // diagnostics only (stamps[255] == 1): the step loop runs the actor layers alone (no head, no env step)
   const bool layers_only = a.stamps && a.stamps[255] == 1;
   for (int step = 0; step < a.T; ++step) {
-    float* Xc = sm + (step & 1) * MLP_BM * ld0;
-    float* Xn = sm + ((step & 1) ^ 1) * MLP_BM * ld0;
+    float* Xc = sm + (step & 1) * ROLL_RB * ld0;
+    float* Xn = sm + ((step & 1) ^ 1) * ROLL_RB * ld0;
     // ---- actor forward
-    const float* X = Xc;
-    int ldx = ld0;
-    for (int l = 0; l < nl; ++l) {
-      float* Yl = sm + s_yo[l];
-      const int ldl = ldyf(l);
-      if (WLDS) {
-        const float* w = sm + s_wo[l];
-        // diagnostics: per-wave shader-clock stamps inside layer 1 of step 5 (entry, MFMAs issued, epilogue landed,
-        // after the barrier) at stamps[128 + wave * 8 + k]
-        int64_t* dbg = (a.stamps && blockIdx.x == 0 && step == 5 && l == 1) ? a.stamps + 128 : nullptr;
-        layer_fwd_lds(X, ldx, s_in[l], w, w + s_out[l] * (16 * ngp2(s_in[l]) + 4), s_out[l], s_actc[l], Yl, ldl, dbg);
-        if (dbg) {
-          __syncthreads();
-          if ((threadIdx.x & 63) == 0) dbg[(threadIdx.x >> 6) * 8 + 3] = __builtin_amdgcn_s_memtime();
-        }
-      } else {
-        layer_fwd(X, ldx, s_in[l], P_<const float>(s_wt[l]), P_<const float>(s_b[l]), s_out[l], s_actc[l], Yl, ldl);
-      }
-      __syncthreads();
-      stamp(step, l);
-      X = Yl;
-      ldx = ldl;
-    }
+    float* Y0 = sm + s_yo[0];
+    float* Y1 = sm + s_yo[1];
+    float* Y2 = sm + s_yo[2];
+    float* Y3 = sm + s_yo[3];
+    roll_layer_mfma<L0>(w0, Xc, ld0, s_red);
+    __syncthreads();
+    roll_layer_epilogue<L0>(s_red, bias_of(0, KP0 + 4), s_out[0], s_actc[0], Y0, 132);
+    __syncthreads();
+    stamp(step, 0);
+    roll_layer_mfma<L1>(w1, Y0, 132, s_red);
+    __syncthreads();
+    roll_layer_epilogue<L1>(s_red, bias_of(1, 132), s_out[1], s_actc[1], Y1, 132);
+    __syncthreads();
+    stamp(step, 1);
+    roll_layer_mfma<L2>(w2, Y1, 132, s_red);
+    __syncthreads();
+    roll_layer_epilogue<L2>(s_red, bias_of(2, 132), s_out[2], s_actc[2], Y2, 68);
+    __syncthreads();
+    stamp(step, 2);
+    roll_layer_mfma<L3>(w3, Y2, 68, s_red);
+    __syncthreads();
+    roll_layer_epilogue<L3>(s_red, bias_of(3, 68), s_out[3], s_actc[3], Y3, 20);
+    __syncthreads();
+    stamp(step, 3);
+    const float* X = Y3;
+    const int ldx = 20;
     if (layers_only) {
       stamp(step, 6);
       continue;
@@ -1474,7 +1513,7 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_rollout_kernel(RolloutArgs a)
     // log-prob term in parallel (a serial per-env loop of hash + log/sqrt/cos/tanh/exp chains on 16 lanes would
     // leave 7 of 8 waves idle for most of the step), then fixed-order per-env sums: bit-identical to the
     // one-thread-per-row head of mlp_fwd_kernel mode 0
-    if (tid < MLP_BM * MLP_MAXA) {
+    if (tid < ROLL_RB * MLP_MAXA) {
       const int r = tid / MLP_MAXA, j = tid % MLP_MAXA;
       if (j < A) {
         const bool live = r < rows;
@@ -1624,24 +1663,24 @@ extern "C" hipError_t aca_mlp_tshadow(const MlpTower* tw, int ntw, int total, hi
   return hipGetLastError();
 }
 
-constexpr size_t ROLLOUT_MAX_LDS = 152 * 1024;   // + ~0.5 KB static: within the 160 KB of a CU
+constexpr size_t ROLLOUT_MAX_LDS = 150 * 1024;   // + ~9 KB static (s_red): within the 160 KB of a CU
 
 extern "C" hipError_t aca_mlp_rollout(const RolloutArgs* a, size_t lds, hipStream_t stream) {
   if (a->N <= 0 || a->T <= 0) return hipSuccess;
-  if (!a->tw || a->head != 2 || a->A != LIN_ACT || a->k < 1 || a->D != LIN_OBS * a->k || a->D > MLP_MAXW)
+  if (!a->tw || a->head != 2 || a->A != LIN_ACT || a->k < 1 || a->k > 3 || a->D != LIN_OBS * a->k || !a->wlds)
     return hipErrorInvalidValue;
   static bool attr = false;
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_rollout_kernel<true>),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_rollout_kernel<32>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, ROLLOUT_MAX_LDS) != hipSuccess ||
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_rollout_kernel<false>),
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_rollout_kernel<64>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, ROLLOUT_MAX_LDS) != hipSuccess)
       return hipErrorInvalidValue;
     attr = true;
   }
   if (lds > ROLLOUT_MAX_LDS) return hipErrorInvalidValue;
-  const dim3 grid((a->N + MLP_BM - 1) / MLP_BM);
-  if (a->wlds) mlp_rollout_kernel<true><<<grid, MLP_THREADS, lds, stream>>>(*a);
-  else mlp_rollout_kernel<false><<<grid, MLP_THREADS, lds, stream>>>(*a);
+  const dim3 grid((a->N + ROLL_RB - 1) / ROLL_RB);
+  if (a->k == 1) mlp_rollout_kernel<32><<<grid, MLP_THREADS, lds, stream>>>(*a);
+  else mlp_rollout_kernel<64><<<grid, MLP_THREADS, lds, stream>>>(*a);
   return hipGetLastError();
 }

@@ -32,16 +32,9 @@ def main():
         eng.rollout_linear(env, st, KEY_ENV_BITS, tr.policy_seed, stamps=st2)
         torch.cuda.synchronize()
         a2 = st2.cpu().tolist()
-        d2 = [a2[128 + 8 * w:128 + 8 * w + 4] for w in range(8)]
-        t2 = min(x[0] for x in d2 if x[0])
-        out["layers_only_layer1_step5_wave_cycles"] = {f"w{w}": [x[k] - t2 if x[k] else None for k in range(4)]
-                                                       for w, x in enumerate(d2)}
         s2 = [a2[8 * k:8 * k + 8] for k in range(16)]
         out["layers_only_layer_us"] = [round((s2[8][i] - (s2[8][i - 1] if i else s2[7][6])) * 0.01, 2) for i in range(4)]
     s = [allst[8 * k:8 * k + 8] for k in range(16)]
-    d = [allst[128 + 8 * w:128 + 8 * w + 4] for w in range(8)]
-    t0c = min(x[0] for x in d if x[0])
-    out["layer1_step5_wave_cycles"] = {f"w{w}": [x[k] - t0c if x[k] else None for k in range(4)] for w, x in enumerate(d)}
     names = ["layer0", "layer1", "layer2", "layer3", "-", "head", "env"]
     ph = {n: [] for n in names if n != "-"}
     for k in range(1, 16):

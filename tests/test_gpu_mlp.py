@@ -250,9 +250,11 @@ def test_optimizer_writes_fragment_copies(cuda):
 
 @pytest.mark.parametrize("frames,num_envs", [(1, 20), (3, 37)])
 def test_fused_rollout_matches_per_step_launches(cuda, frames, num_envs):
-    """mlp_rollout_kernel (whole T-step rollout of the MuJoCo-shaped bank in one launch + one batched critic launch)
-    == T x (policy_step launch + env_step_linear launch) + value launch: same actions, log-probs, observations,
-    rewards, resets and env bank state (episode limit 7 so resets happen inside the rollout; partial 16-env tiles)."""
+    """mlp_rollout_kernel (whole T-step rollout of the MuJoCo-shaped bank in one launch, 4-env workgroups on 4x4x1
+    MFMAs + one batched critic launch) == T x (policy_step launch + env_step_linear launch) + value launch: the same
+    resets, done flags and step counters exactly, actions, log-probs, observations, rewards, values and env state up
+    to the actor's fp32 summation order (measured max |diff| ~1e-6; episode limit 7 so resets happen inside the
+    rollout; partial 4-env tiles)."""
     from actor_critic_algs_on_tensorflow_amd import preset
     from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
     kw = dict(num_envs=num_envs, n_steps=24, frames=frames, ppo_epochs=1, ppo_minibatches=2, device="cuda:0",
@@ -266,12 +268,16 @@ def test_fused_rollout_matches_per_step_launches(cuda, frames, num_envs):
             tr.collect()
         torch.cuda.synchronize()
         a, b = (tr.storage for tr in trs)
-        for name in ("obs", "actions", "logp", "entropy", "rewards", "dones", "truncated", "values"):
+        for name in ("dones", "truncated"):
+            assert torch.equal(getattr(a, name), getattr(b, name)), name
+        for name in ("obs", "actions", "logp", "entropy", "rewards", "values"):
             x, y = getattr(a, name), getattr(b, name)
-            assert torch.equal(x, y), (name, (x.float() - y.float()).abs().max().item())
+            torch.testing.assert_close(x, y, rtol=1e-4, atol=1e-4, msg=name)
         ea, eb = (tr.env for tr in trs)
-        for name in ("state", "t", "tg", "ep_ret"):
+        for name in ("t", "tg"):
             assert torch.equal(getattr(ea, name), getattr(eb, name)), name
+        for name in ("state", "ep_ret"):
+            torch.testing.assert_close(getattr(ea, name), getattr(eb, name), rtol=1e-4, atol=1e-4, msg=name)
         torch.testing.assert_close(ea.ep_stats, eb.ep_stats, rtol=1e-5, atol=1e-4)
         assert int(a.dones.sum()) > 0
         for tr in trs:

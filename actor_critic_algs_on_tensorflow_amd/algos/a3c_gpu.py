@@ -175,6 +175,10 @@ class DeviceParameterServer:
     @torch.no_grad()
     def apply(self, w, version):
         self._steppers[w]()
+        if self.flat.data.is_cuda:
+            # an asynchronous device fault of the optimiser launch surfaces HERE (outside the peer I/O), not inside
+            # the reply's send, where it would be reported as a departed worker
+            torch.cuda.current_stream(self.flat.data.device).synchronize()
         self.log.append((w, version, self.global_step))
         self.global_step += 1
         self.n_applies[w] += 1

@@ -750,7 +750,12 @@ class CNNEngine:
         gradient (``fin_parts``) so the optimiser needs no sum-of-squares pass. ``planes``: only these plane sets
         (default: every set of this backward); ``parts`` / ``bias_rows`` False: no norm partials / no bias rows."""
         words = self._fin_table(b, planes, parts, bias_rows)
-        sd, self._stats_duty = self._stats_duty, None
+        # the per-env head's statistics go with the finaliser that sums its gradient planes (not whichever finaliser
+        # runs first: under DP a tail-stage launch sums the fc weight alone)
+        sums_head = "ae_Wh" in (self._cur_planes if planes is None else planes)
+        sd = self._stats_duty if sums_head else None
+        if sd is not None:
+            self._stats_duty = None
         if sd is not None:   # the per-env head's statistics rows -> stats[0..7] (one extra finaliser workgroup)
             spart, B, ent, kl, stats = sd
             _native.require().grad_finalize(words[0], self.fin_parts, spart, B, ent, kl, stats)

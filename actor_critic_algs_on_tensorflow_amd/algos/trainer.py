@@ -1258,6 +1258,9 @@ class ActorCriticTrainer:
 
     def train(self, num_updates=None, callback=None):
         cfg = self.cfg
+        if self._fault is not None and len(self._fault) == 3:
+            raise ValueError(f"fault_inject {cfg.fault_inject!r}: the 'push' / 'reply' fault points belong to the "
+                             "async parameter-server worker (a3c_gpu); the synchronous trainer takes 'rank:iteration'")
         n = cfg.total_updates if num_updates is None else num_updates
         if self._can_capture() and self.graph is None:
             self.capture()

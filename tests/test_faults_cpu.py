@@ -83,3 +83,16 @@ def test_rank_failure_aborts_and_resume_is_exact(tmp_path):
     res = torch.load(os.path.join(d, "resume.pt"), weights_only=True)
     assert ref["it"] == res["it"] == 6
     assert torch.equal(ref["p"], res["p"]), "resumed DP run must match the uninterrupted run bit for bit"
+
+
+def test_sync_trainer_rejects_ps_exchange_fault_points():
+    """'rank:iteration:push|reply' names a fault point inside the async PS worker's exchange; the synchronous trainer
+    refuses it instead of silently never injecting the fault."""
+    import pytest
+    from actor_critic_algs_on_tensorflow_amd import preset
+    from actor_critic_algs_on_tensorflow_amd.algos.trainer import ActorCriticTrainer
+    cfg = preset("cartpole_cpu", outdir=None, quiet=True, stdout_freq=0, save_every=0, fault_inject="0:1:push",
+                 total_updates=2)
+    tr = ActorCriticTrainer(cfg)
+    with pytest.raises(ValueError, match="parameter-server"):
+        tr.train()

@@ -174,6 +174,14 @@ class ActorCriticTrainer:
             assert len(owner) == 1, "the conv / fc weights must live in one optimiser group"
             owner[0].set_frag(ent)
         self.actor_opt = self.opts.get("actor", self.opts.get("shared"))
+        if (dp is not None and dp.compress == "bf16" and self.engine is not None and len(self.opts) == 1
+                and all(o.clip_value is None for o in self.opts.values()) and _native.use_native(self.flat.data)):
+            # bf16 buckets: the optimiser (and its sum of squares) read the all-reduced bf16 comm buffer itself -- no
+            # cast back into the fp32 slab (one launch and ~10 MB of traffic less per update)
+            dp.prepare(self.flat.grad)
+            for o in self.opts.values():
+                o.bind_grad16(dp.comm_view(self.flat.grad))
+            dp.direct_read = True
         if (self.engine is not None and dp is None and len(self.opts) == 1
                 and all(o.clip_value is None for o in self.opts.values())):
             # the engine's gradient finaliser writes the global-norm partials: no separate sum-of-squares pass
@@ -1010,11 +1018,15 @@ class ActorCriticTrainer:
         """lag-1: C <- G, G <- 0 (one launch) so the next backward accumulates into a clean slab while C is
         all-reduced and consumed by the next optimiser step; the one-graph schedule's gate opens in the same launch."""
         gate = getattr(self, "_lag1_gate", None)
+        # G needs no clearing when the next backward stores every gradient element (the CNN engine's grouped
+        # backward: head launch, fc_bwd, finaliser planes)
+        zero = not (self.engine is not None and getattr(self.engine, "last_bwd_stores_all", False))
         if _native.use_native(self.flat.grad):
-            _native.require().grad_move(self.flat.grad, self._comm_grad, gate)
+            _native.require().grad_move(self.flat.grad, self._comm_grad, gate, zero)
         else:
             self._comm_grad.copy_(self.flat.grad)
-            self.flat.grad.zero_()
+            if zero:
+                self.flat.grad.zero_()
             if gate is not None:
                 gate.fill_(1)
 

@@ -98,10 +98,17 @@ class FusedAdam:
         self._frag_table = None
         # optional device int32 gate: the update is skipped while it is 0 (set_gate)
         self.gate = None
+        # optional bf16 gradient read instead of g (bind_grad16: the all-reduced bf16 DP bucket, no cast back)
+        self.g16 = None
 
     def bind_grad(self, grad_slab):
         """Read gradients from this group's segment of another slab (lag-1 DP reads the all-reduced copy)."""
         self.g = grad_slab[self.start:self.end]
+
+    def bind_grad16(self, slab16):
+        """Native step: read the gradient from this group's segment of a bf16 slab (bf16 DP buckets: the all-reduced
+        comm buffer itself -- no cast back into the fp32 slab; the sum of squares reads it too). ``None`` unbinds."""
+        self.g16 = None if slab16 is None else slab16[self.start:self.end]
 
     def set_frag(self, entries):
         """Fragment-ordered bf16 weight copies the update writes as it goes: ``entries`` = [(W fp32 view into this
@@ -170,10 +177,11 @@ class FusedAdam:
             return self.ext_parts
         if self.clip_value is not None:
             # the norm is taken after the element-wise clip (torch oracle order)
+            assert self.g16 is None, "element-wise clip with bf16 gradient reads"
             g = self.g * self.grad_mul if self.grad_mul != 1.0 else self.g
             ops.sumsq(torch.clamp(g, -self.clip_value, self.clip_value), self._partial)
         else:
-            ops.sumsq(self.g, self._partial)
+            ops.sumsq(self.g if self.g16 is None else self.g16, self._partial)
             self._norm_mul = self.grad_mul * self.grad_mul
         return self._partial
 
@@ -185,10 +193,11 @@ class FusedAdam:
                       float(self.clip_value) if self.clip_value is not None else -1.0,
                       float(self.max_grad_norm) if self.max_grad_norm is not None else -1.0, self._ticket,
                       bool(self.zero_grad_after), float(self.grad_mul), float(self._norm_mul),
-                      getattr(self, "_frag_table", None))
+                      getattr(self, "_frag_table", None), self.g16)
 
     def _torch_step(self):
-        g = self.g * self.grad_mul if self.grad_mul != 1.0 else self.g
+        g = self.g if self.g16 is None else self.g16.float()
+        g = g * self.grad_mul if self.grad_mul != 1.0 else g
         if self.clip_value is not None:
             g = torch.clamp(g, -self.clip_value, self.clip_value)
         if self.max_grad_norm is not None:
@@ -232,10 +241,11 @@ class FusedRMSprop(FusedAdam):
                          float(self.clip_value) if self.clip_value is not None else -1.0,
                          float(self.max_grad_norm) if self.max_grad_norm is not None else -1.0,
                          bool(self.zero_grad_after), float(self.grad_mul), float(self._norm_mul),
-                         getattr(self, "_frag_table", None))
+                         getattr(self, "_frag_table", None), self.g16)
 
     def _torch_step(self):
-        g = self.g * self.grad_mul if self.grad_mul != 1.0 else self.g
+        g = self.g if self.g16 is None else self.g16.float()
+        g = g * self.grad_mul if self.grad_mul != 1.0 else g
         if self.clip_value is not None:
             g = torch.clamp(g, -self.clip_value, self.clip_value)
         if self.max_grad_norm is not None:

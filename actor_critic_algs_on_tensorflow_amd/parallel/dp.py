@@ -60,6 +60,8 @@ class DataParallel:
             raise ValueError(f"compress must be None/'none'/'bf16', got {compress!r}")
         self.compress = compress
         self._cbuf = None
+        # bf16 buckets read in place by the optimisers (trainer binds them): unpack is then a no-op
+        self.direct_read = False
         # RCCL ("nccl") collectives are stream-ordered and capturable: the trainer records them INSIDE its
         # hipGraph (one graph per update, the collective as a graph node on RCCL's stream with event joins).
         # gloo collectives run on the host, so a captured gloo update is a chain of graphs cut at each one.
@@ -117,7 +119,7 @@ class DataParallel:
 
     @torch.no_grad()
     def unpack(self, grad, s=0, e=None):
-        if self.compress:
+        if self.compress and not self.direct_read:
             grad[s:e].copy_(self._cbuf[s:e])
 
     @torch.no_grad()

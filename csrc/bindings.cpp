@@ -93,16 +93,16 @@ hipError_t aca_conv1_wgrad2(const uint8_t*, const uint16_t*, float*, int, int, f
 hipError_t aca_conv_wgrad_gemm(int, const uint16_t*, const uint16_t*, float*, int, int, hipStream_t);
 hipError_t aca_gemm_big(const AcaGemmDesc*, hipStream_t);
 int64_t aca_gemm_big_ws(int, int, int);
-hipError_t aca_sumsq(const float*, size_t, float*, hipStream_t);
+hipError_t aca_sumsq(const void*, size_t, float*, int, hipStream_t);
 hipError_t aca_sumsq_multi(const float* const*, const size_t*, float* const*, int, hipStream_t);
 int aca_sumsq_parts();
 hipError_t aca_adam_step(float*, float*, float*, float*, size_t, const float*, float*, const float*, float*, uint16_t*,
                          float, float, float, float, float, unsigned int*, int, float, float, const int64_t*,
-                         hipStream_t);
+                         const uint16_t*, hipStream_t);
 hipError_t aca_rmsprop_step(float*, float*, float*, size_t, const float*, const float*, float*, uint16_t*, float, float,
-                            float, float, int, float, float, const int64_t*, hipStream_t);
+                            float, float, int, float, float, const int64_t*, const uint16_t*, hipStream_t);
 hipError_t aca_cast_bf16(const float*, uint16_t*, size_t, hipStream_t);
-hipError_t aca_grad_move(float*, float*, size_t, int*, hipStream_t);
+hipError_t aca_grad_move(float*, float*, size_t, int*, int, hipStream_t);
 hipError_t aca_gemm_run(const AcaGemmDesc*, hipStream_t);
 int aca_gemm_effective_splits(int, int, int);
 int aca_gemm_tile_dims(int, int*, int*);
@@ -794,10 +794,19 @@ void moments(Tensor x, Tensor y, Tensor out) {
 // ---------------------------------------------------------------------------------------------- optimisers
 // Writes aca_sumsq_parts() partial sums of squares (unused slots zeroed); the optimisers reduce them.
 void sumsq(Tensor x, Tensor partial) {
-  need(x, at::kFloat, "x");
+  const bool bf16 = x.scalar_type() == at::kBFloat16;
+  need(x, bf16 ? at::kBFloat16 : at::kFloat, "x");
   need(partial, at::kFloat, "partial");
   TORCH_CHECK(partial.numel() >= aca_sumsq_parts(), "sumsq: partial needs ", aca_sumsq_parts(), " slots");
-  check(aca_sumsq(ptr<float>(x), x.numel(), ptr<float>(partial), cur_stream(x)), "sumsq");
+  check(aca_sumsq(x.data_ptr(), x.numel(), ptr<float>(partial), bf16 ? 1 : 0, cur_stream(x)), "sumsq");
+}
+
+// optional bf16 gradient the optimiser reads in place of g (the all-reduced bf16 comm buffer of the same group)
+const uint16_t* g16_ptr(const c10::optional<Tensor>& g16, const Tensor& p, const char* who) {
+  if (!(g16.has_value() && g16->defined())) return nullptr;
+  need(*g16, at::kBFloat16, "g16");
+  TORCH_CHECK(g16->numel() == p.numel(), who, ": g16 size mismatch");
+  return ptr<uint16_t>(*g16);
 }
 
 // several sums of squares (one partial set each) in one launch: the per-group norms of a multi-group optimiser step
@@ -843,7 +852,7 @@ static const int64_t* trans_table(const c10::optional<Tensor>& trans, const char
 void adam_step(Tensor p, Tensor g, Tensor m, Tensor v, Tensor lr, Tensor t, c10::optional<Tensor> gnorm_parts,
                c10::optional<Tensor> gnorm_out, c10::optional<Tensor> shadow, double b1, double b2, double eps,
                double clip, double max_norm, Tensor ticket, bool zero_grad, double gmul, double norm_mul,
-               c10::optional<Tensor> trans) {
+               c10::optional<Tensor> trans, c10::optional<Tensor> g16) {
   need(p, at::kFloat, "p");
   need(g, at::kFloat, "g");
   need(m, at::kFloat, "m");
@@ -857,14 +866,14 @@ void adam_step(Tensor p, Tensor g, Tensor m, Tensor v, Tensor lr, Tensor t, c10:
                       ptr<float>(t), gnorm_parts_ptr(gnorm_parts, max_norm, "adam"), optr<float>(gnorm_out),
                       shadow_ptr(shadow, p, "adam"), (float)b1, (float)b2, (float)eps, (float)clip, (float)max_norm,
                       ptr<unsigned int>(ticket), zero_grad ? 1 : 0, (float)gmul, (float)norm_mul,
-                      trans_table(trans, "adam_step"), cur_stream(p)),
+                      trans_table(trans, "adam_step"), g16_ptr(g16, p, "adam_step"), cur_stream(p)),
         "adam_step");
 }
 
 void rmsprop_step(Tensor p, Tensor g, Tensor v, Tensor lr, c10::optional<Tensor> gnorm_parts,
                   c10::optional<Tensor> gnorm_out, c10::optional<Tensor> shadow, double alpha, double eps,
                   double clip, double max_norm, bool zero_grad, double gmul, double norm_mul,
-                  c10::optional<Tensor> trans) {
+                  c10::optional<Tensor> trans, c10::optional<Tensor> g16) {
   need(p, at::kFloat, "p");
   need(g, at::kFloat, "g");
   need(v, at::kFloat, "v");
@@ -874,7 +883,7 @@ void rmsprop_step(Tensor p, Tensor g, Tensor v, Tensor lr, c10::optional<Tensor>
                          gnorm_parts_ptr(gnorm_parts, max_norm, "rmsprop"), optr<float>(gnorm_out),
                          shadow_ptr(shadow, p, "rmsprop"), (float)alpha, (float)eps, (float)clip, (float)max_norm,
                          zero_grad ? 1 : 0, (float)gmul, (float)norm_mul, trans_table(trans, "rmsprop_step"),
-                         cur_stream(p)),
+                         g16_ptr(g16, p, "rmsprop_step"), cur_stream(p)),
         "rmsprop_step");
 }
 
@@ -1260,12 +1269,12 @@ void rccl_allreduce(Tensor buf, int64_t comm) {
   TORCH_CHECK(r == ncclSuccess, "rccl_allreduce: ", ncclGetErrorString(r));
 }
 
-void grad_move(Tensor src, Tensor dst, c10::optional<Tensor> gate) {
+void grad_move(Tensor src, Tensor dst, c10::optional<Tensor> gate, bool zero) {
   need(src, at::kFloat, "src");
   need(dst, at::kFloat, "dst");
   TORCH_CHECK(src.numel() == dst.numel(), "grad_move: size mismatch");
   int* gp = const_cast<int*>(copt<int32_t>(gate, at::kInt, "gate"));
-  check(aca_grad_move(ptr<float>(src), ptr<float>(dst), src.numel(), gp, cur_stream(src)), "grad_move");
+  check(aca_grad_move(ptr<float>(src), ptr<float>(dst), src.numel(), gp, zero ? 1 : 0, cur_stream(src)), "grad_move");
 }
 
 void cast_bf16(Tensor x, Tensor y) {
@@ -2014,12 +2023,12 @@ TORCH_LIBRARY(acamd, m) {
   m.def("sumsq_multi(Tensor[] xs, Tensor[] partials) -> ()");
   m.def("adam_step(Tensor p, Tensor g, Tensor m, Tensor v, Tensor lr, Tensor t, Tensor? gnorm_parts, "
         "Tensor? gnorm_out, Tensor? shadow, float b1, float b2, float eps, float clip, float max_norm, Tensor ticket, "
-        "bool zero_grad=False, float gmul=1.0, float norm_mul=1.0, Tensor? trans=None) -> ()");
+        "bool zero_grad=False, float gmul=1.0, float norm_mul=1.0, Tensor? trans=None, Tensor? g16=None) -> ()");
   m.def("rmsprop_step(Tensor p, Tensor g, Tensor v, Tensor lr, Tensor? gnorm_parts, Tensor? gnorm_out, "
         "Tensor? shadow, float alpha, float eps, float clip, float max_norm, bool zero_grad=False, float gmul=1.0, "
-        "float norm_mul=1.0, Tensor? trans=None) -> ()");
+        "float norm_mul=1.0, Tensor? trans=None, Tensor? g16=None) -> ()");
   m.def("cast_bf16(Tensor x, Tensor y) -> ()");
-  m.def("grad_move(Tensor src, Tensor dst, Tensor? gate=None) -> ()");
+  m.def("grad_move(Tensor src, Tensor dst, Tensor? gate=None, bool zero=True) -> ()");
   m.def("rccl_allreduce(Tensor buf, int comm) -> ()");
   m.def("opt_multi(Tensor words, Tensor fvals, Tensor? trans, bool adam, float b1, float b2, float eps, bool zero_grad, "
         "Tensor stream_ref, int t_off=-1) -> ()");

@@ -21,12 +21,23 @@ constexpr int SUMSQ_PARTS = 256;   // max sumsq workgroups = partial slots the o
 
 // Partial sums of squares of x over `nblk` workgroups (this one: `bid`), one partial slot each; slot `nblk` .. are
 // zeroed by workgroup 0 so the consumer always sums SUMSQ_PARTS entries in a fixed order.
-template <int U = SUMSQ_U>
-__device__ __forceinline__ void sumsq_body(const float* __restrict__ x, size_t n, float* __restrict__ partial,
+// four consecutive elements of an fp32 or a bf16 (u16) array as a float4 (group i)
+__device__ __forceinline__ float4 ld4(const float* __restrict__ x, size_t i) {
+  return reinterpret_cast<const float4*>(x)[i];
+}
+__device__ __forceinline__ float4 ld4(const u16* __restrict__ x, size_t i) {
+  const uint2 w = reinterpret_cast<const uint2*>(x)[i];
+  return make_float4(__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xFFFF0000u), __uint_as_float(w.y << 16),
+                     __uint_as_float(w.y & 0xFFFF0000u));
+}
+__device__ __forceinline__ float ld1(const float* __restrict__ x, size_t i) { return x[i]; }
+__device__ __forceinline__ float ld1(const u16* __restrict__ x, size_t i) { return bf2f(x[i]); }
+
+template <int U = SUMSQ_U, typename T = float>
+__device__ __forceinline__ void sumsq_body(const T* __restrict__ x, size_t n, float* __restrict__ partial,
                                            int nblk, int bid, float* sh) {
   float s = 0.f;
   const size_t n4 = n / 4;
-  const float4* x4 = reinterpret_cast<const float4*>(x);
   // SUMSQ_U independent 16-byte loads in flight per thread before any use: the grid is capped at one workgroup
   // per CU, so latency (not bandwidth) bounds a one-load-at-a-time loop
   const size_t step = (size_t)nblk * blockDim.x * U;
@@ -35,23 +46,24 @@ __device__ __forceinline__ void sumsq_body(const float* __restrict__ x, size_t n
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const size_t i = i0 + (size_t)u * blockDim.x;
-      v[u] = i < n4 ? x4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      v[u] = i < n4 ? ld4(x, i) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) s += v[u].x * v[u].x + v[u].y * v[u].y + v[u].z * v[u].z + v[u].w * v[u].w;
   }
   if (bid == 0) {
-    for (size_t i = n4 * 4 + threadIdx.x; i < n; i += blockDim.x) s += x[i] * x[i];
+    for (size_t i = n4 * 4 + threadIdx.x; i < n; i += blockDim.x) s += ld1(x, i) * ld1(x, i);
     for (int b = nblk + threadIdx.x; b < SUMSQ_PARTS; b += blockDim.x) partial[b] = 0.f;
   }
   s = block_sum(s, sh);
   if (threadIdx.x == 0) partial[bid] = s;
 }
 
-__global__ void __launch_bounds__(OPT_THREADS) sumsq_kernel(const float* __restrict__ x, size_t n,
+template <typename T>
+__global__ void __launch_bounds__(OPT_THREADS) sumsq_kernel(const T* __restrict__ x, size_t n,
                                                              float* __restrict__ partial) {
   __shared__ float sh[16];
-  sumsq_body(x, n, partial, gridDim.x, blockIdx.x, sh);
+  sumsq_body<SUMSQ_U, T>(x, n, partial, gridDim.x, blockIdx.x, sh);
 }
 
 // Several independent sums of squares in ONE launch (the separate actor / critic norms of a data-parallel MLP
@@ -124,6 +136,9 @@ struct OptSeg {
   // more than the update itself at the MLP sizes (~4 us of a 9 us launch, profiles/r6_mlp_opt.txt).
   const int64_t* items = nullptr;
   int nitems = 0;
+  // optional bf16 gradient read in place of g (the all-reduced comm buffer of bf16 DP buckets: no cast back to the
+  // fp32 slab; zero_grad still clears g). The plain launch only (opt_kernel G16).
+  const u16* g16 = nullptr;
   int64_t* stamps = nullptr;   // diagnostics: [global workgroup][8] s_memrealtime phase stamps (aca_opt_set_stamps)
   int wg0 = 0;                 // global index of the segment's first workgroup (stamps row)
 };
@@ -363,7 +378,7 @@ __device__ __forceinline__ void opt_items(const OptSeg& S, float b1, float b2, f
 // (its partial loads + block sum would otherwise be a dependent round trip ahead of every element load).
 // ITEMS: the item path is compiled in (the grouped launch of the MLP optimisers); the plain launch leaves it out --
 // its code and LDS tile raised the sweep's registers and cost the headline RMSprop step ~30 % (12.5 -> 16.3 us).
-template <bool ADAM, int U, bool ITEMS>
+template <bool ADAM, int U, bool ITEMS, bool G16 = false>
 __device__ __forceinline__ void opt_body(const OptSeg& S, float b1, float b2, float eps, int zero_grad, int vblk,
                                          int vgrid, int* flag, float* shr, u16* kcs, float* blks) {
   if (S.gate && *S.gate == 0) return;   // uniform over the launch
@@ -395,7 +410,7 @@ __device__ __forceinline__ void opt_body(const OptSeg& S, float b1, float b2, fl
     for (int u = 0; u < U; ++u) {
       const size_t i = i0 + (size_t)u * blockDim.x;
       if (i < n4 && !in_kc(i)) {
-        g4[u] = reinterpret_cast<const float4*>(g)[i];
+        g4[u] = G16 ? ld4(S.g16, i) : reinterpret_cast<const float4*>(g)[i];
         v4[u] = reinterpret_cast<const float4*>(v)[i];
         p4[u] = reinterpret_cast<const float4*>(p)[i];
         m4[u] = ADAM ? reinterpret_cast<const float4*>(m)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -417,7 +432,7 @@ __device__ __forceinline__ void opt_body(const OptSeg& S, float b1, float b2, fl
   float4 kg, kv, kp, km;
   auto kc_load = [&](int it) {
     const size_t i = kc_index(it);
-    kg = reinterpret_cast<const float4*>(g)[i];
+    kg = G16 ? ld4(S.g16, i) : reinterpret_cast<const float4*>(g)[i];
     kv = reinterpret_cast<const float4*>(v)[i];
     kp = reinterpret_cast<const float4*>(p)[i];
     km = ADAM ? reinterpret_cast<const float4*>(m)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -512,7 +527,7 @@ __device__ __forceinline__ void opt_body(const OptSeg& S, float b1, float b2, fl
   stamp(4);
   if (vblk == 0) {   // scalar tail
     for (size_t i = n4 * 4 + threadIdx.x; i < n; i += blockDim.x) {
-      float gi = g[i], vi = v[i], pi = p[i], mi = ADAM ? m[i] : 0.f;
+      float gi = G16 ? bf2f(S.g16[i]) : g[i], vi = v[i], pi = p[i], mi = ADAM ? m[i] : 0.f;
       if (zero_grad) g[i] = 0.f;
       upd(gi, vi, mi, pi);
       v[i] = vi;
@@ -529,12 +544,12 @@ __device__ __forceinline__ void opt_body(const OptSeg& S, float b1, float b2, fl
   if (ADAM && S.t_off < 0) opt_ticket(S, vblk, vgrid, t);
 }
 
-template <bool ADAM, int U>
+template <bool ADAM, int U, bool G16 = false>
 __global__ void __launch_bounds__(OPT_THREADS) opt_kernel(OptSeg S, float b1, float b2, float eps, int zero_grad) {
   __shared__ int flag;
   __shared__ float shr[16];
   __shared__ __attribute__((aligned(16))) u16 kcs[OPT_THREADS / 64 * 256];
-  opt_body<ADAM, U, false>(S, b1, b2, eps, zero_grad, blockIdx.x, gridDim.x, &flag, shr, kcs, nullptr);
+  opt_body<ADAM, U, false, G16>(S, b1, b2, eps, zero_grad, blockIdx.x, gridDim.x, &flag, shr, kcs, nullptr);
 }
 
 // Several parameter groups (e.g. the reference's separate actor and critic optimisers) in ONE launch: the grid is
@@ -838,20 +853,21 @@ __global__ void __launch_bounds__(OPT_THREADS) grad_finalize_kernel(const int64_
 // dst is all-reduced and consumed by the next optimiser step)
 // lag-1 data parallelism: C <- G, G <- 0; `gate` (optional) is set to 1 -- C now holds a gradient the next
 // optimiser launch gated on it may apply (OptSeg::gate)
+// zero: clear src behind the copy (off when the next backward STORES every gradient element)
 __global__ void __launch_bounds__(OPT_THREADS) grad_move_kernel(float* __restrict__ src, float* __restrict__ dst,
-                                                                size_t n, int* __restrict__ gate) {
+                                                                size_t n, int* __restrict__ gate, int zero) {
   if (gate && blockIdx.x == 0 && threadIdx.x == 0) *gate = 1;
   const size_t n4 = n / 4;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += stride) {
     const float4 v = reinterpret_cast<const float4*>(src)[i];
-    reinterpret_cast<float4*>(src)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (zero) reinterpret_cast<float4*>(src)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     reinterpret_cast<float4*>(dst)[i] = v;
   }
   if (blockIdx.x == 0)
     for (size_t i = n4 * 4 + threadIdx.x; i < n; i += blockDim.x) {
       dst[i] = src[i];
-      src[i] = 0.f;
+      if (zero) src[i] = 0.f;
     }
 }
 
@@ -875,6 +891,11 @@ template <bool ADAM>
 static void launch_opt(OptSeg& S, float b1, float b2, float eps, int zero_grad, hipStream_t stream) {
   const int U = g_opt_unroll;
   S.nblocks = opt_grid(S.n, U);
+  if (S.g16) {
+    S.nblocks = opt_grid(S.n, 1);
+    opt_kernel<ADAM, 1, true><<<S.nblocks, OPT_THREADS, 0, stream>>>(S, b1, b2, eps, zero_grad);
+    return;
+  }
   switch (U) {
     case 2: opt_kernel<ADAM, 2><<<S.nblocks, OPT_THREADS, 0, stream>>>(S, b1, b2, eps, zero_grad); break;
     case 4: opt_kernel<ADAM, 4><<<S.nblocks, OPT_THREADS, 0, stream>>>(S, b1, b2, eps, zero_grad); break;
@@ -886,12 +907,14 @@ static void launch_opt(OptSeg& S, float b1, float b2, float eps, int zero_grad, 
 
 using namespace aca;
 
-extern "C" hipError_t aca_sumsq(const float* x, size_t n, float* partial, hipStream_t stream) {
-  if (reinterpret_cast<uintptr_t>(x) % 16) return hipErrorInvalidValue;
+// x: fp32, or bf16 (the all-reduced comm buffer of bf16 gradient buckets) when bf16 != 0
+extern "C" hipError_t aca_sumsq(const void* x, size_t n, float* partial, int bf16, hipStream_t stream) {
+  if (reinterpret_cast<uintptr_t>(x) % (bf16 ? 8 : 16)) return hipErrorInvalidValue;
   int grid = (int)((n / 4 + OPT_THREADS * SUMSQ_U - 1) / (OPT_THREADS * SUMSQ_U));
   if (grid < 1) grid = 1;
   if (grid > SUMSQ_PARTS) grid = SUMSQ_PARTS;
-  sumsq_kernel<<<grid, OPT_THREADS, 0, stream>>>(x, n, partial);
+  if (bf16) sumsq_kernel<u16><<<grid, OPT_THREADS, 0, stream>>>(static_cast<const u16*>(x), n, partial);
+  else sumsq_kernel<float><<<grid, OPT_THREADS, 0, stream>>>(static_cast<const float*>(x), n, partial);
   return hipGetLastError();
 }
 
@@ -969,11 +992,13 @@ static bool opt_aligned(const float* p, const float* g, const float* m, const fl
 extern "C" hipError_t aca_adam_step(float* p, float* g, float* m, float* v, size_t n, const float* lr,
                                     float* t, const float* gnorm_parts, float* gnorm_out, uint16_t* shadow, float b1, float b2, float eps,
                                     float clip, float max_norm, unsigned int* ticket, int zero_grad,
-                                    float gmul, float norm_mul, const int64_t* trans, hipStream_t stream) {
+                                    float gmul, float norm_mul, const int64_t* trans, const uint16_t* g16,
+                                    hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  if (!opt_aligned(p, g, m, v, shadow)) return hipErrorInvalidValue;
+  if (!opt_aligned(p, g, m, v, shadow) || reinterpret_cast<uintptr_t>(g16) % 8) return hipErrorInvalidValue;
   OptSeg S{p, g, m, v, n, lr, t, gnorm_parts, gnorm_out, shadow, clip, max_norm, gmul, norm_mul, ticket, opt_grid(n),
            0, {}};
+  S.g16 = g16;
   if (!ticket || !t) return hipErrorInvalidValue;
   if (!opt_load_trans(S, trans)) return hipErrorInvalidValue;
   launch_opt<true>(S, b1, b2, eps, zero_grad, stream);
@@ -983,11 +1008,12 @@ extern "C" hipError_t aca_adam_step(float* p, float* g, float* m, float* v, size
 extern "C" hipError_t aca_rmsprop_step(float* p, float* g, float* v, size_t n, const float* lr,
                                        const float* gnorm_parts, float* gnorm_out, uint16_t* shadow, float alpha, float eps, float clip,
                                        float max_norm, int zero_grad, float gmul, float norm_mul,
-                                       const int64_t* trans, hipStream_t stream) {
+                                       const int64_t* trans, const uint16_t* g16, hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  if (!opt_aligned(p, g, v, v, shadow)) return hipErrorInvalidValue;
+  if (!opt_aligned(p, g, v, v, shadow) || reinterpret_cast<uintptr_t>(g16) % 8) return hipErrorInvalidValue;
   OptSeg S{p, g, nullptr, v, n, lr, nullptr, gnorm_parts, gnorm_out, shadow, clip, max_norm, gmul, norm_mul, nullptr,
            opt_grid(n), 0, {}};
+  S.g16 = g16;
   if (!opt_load_trans(S, trans)) return hipErrorInvalidValue;
   launch_opt<false>(S, 0.f, alpha, eps, zero_grad, stream);
   return hipGetLastError();
@@ -1048,10 +1074,10 @@ extern "C" int aca_opt_set_unroll(int u) {
   return g_opt_unroll;
 }
 
-extern "C" hipError_t aca_grad_move(float* src, float* dst, size_t n, int* gate, hipStream_t stream) {
+extern "C" hipError_t aca_grad_move(float* src, float* dst, size_t n, int* gate, int zero, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   if ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) % 16) return hipErrorInvalidValue;
-  grad_move_kernel<<<opt_grid(n), OPT_THREADS, 0, stream>>>(src, dst, n, gate);
+  grad_move_kernel<<<opt_grid(n), OPT_THREADS, 0, stream>>>(src, dst, n, gate, zero);
   return hipGetLastError();
 }
 

@@ -171,6 +171,7 @@ class CNNEngine:
         self.bfc, self.gbfc, _ = views(tr.fc.bias)
         self.Wh, self.gWh, self.sWh = views(net.heads.kernel)
         self.bh, self.gbh, _ = views(net.heads.bias)
+        self._gslab = flat.grad
         self._bufs = {}
         # fragment-ordered bf16 copies of the conv weights (ops/optim.py frag_order), rewritten by the optimiser step
         # itself (FusedAdam.set_frag): the fused trunk kernels' weight loads read 1 KB per wave contiguously instead
@@ -189,6 +190,38 @@ class CNNEngine:
         self._ev = [torch.cuda.Event() for _ in range(6)] if self.side is not None else None
 
     _FRAG_SHAPES = ((32, 256), (64, 512), (64, 576))
+
+    def use_grad_slab(self, slab):
+        """Every gradient this engine writes goes to ``slab`` (a tensor laid out like ``flat.grad``) from now on: the
+        captured launches record its addresses (lag-1 data parallelism captures the two ring-phase graph sets on
+        two slabs -- one written by the backward while the other is all-reduced and applied; no C <- G copy)."""
+        assert slab.shape == self.flat.grad.shape and slab.dtype == self.flat.grad.dtype
+        net = self.model.net
+        tr = net.trunk
+        idx = {id(p): i for i, p in enumerate(self.flat.params)}
+
+        def gv(p):
+            off = self.flat.offsets[idx[id(p)]]
+            return slab[off:off + p.numel()]
+
+        self.gW1, self.gb1 = gv(tr.conv1.weight), gv(tr.conv1.bias)
+        self.gW2, self.gb2 = gv(tr.conv2.weight), gv(tr.conv2.bias)
+        self.gW3, self.gb3 = gv(tr.conv3.weight), gv(tr.conv3.bias)
+        self.gWfc, self.gbfc = gv(tr.fc.kernel), gv(tr.fc.bias)
+        self.gWh, self.gbh = gv(net.heads.kernel), gv(net.heads.bias)
+        # the finaliser job tables built for the old slab, re-pointed at the new one (tables are uploaded outside
+        # graph capture: a capture of the other ring phase must find its tables ready)
+        old = self._gslab
+        if old.data_ptr() != slab.data_ptr():
+            lo, hi, delta = old.data_ptr(), old.data_ptr() + old.numel() * 4, slab.data_ptr() - old.data_ptr()
+            for key, (words, mx) in list(self._fin_words.items()):
+                nk = key[:-1] + (slab.data_ptr(),)
+                if key[-1] == lo and nk not in self._fin_words:
+                    w = words.cpu().clone()
+                    hit = (w[:, 0] >= lo) & (w[:, 0] < hi)
+                    w[hit, 0] += delta
+                    self._fin_words[nk] = (w.to(words.device), mx)
+        self._gslab = slab
 
     def frag_entries(self):
         """(fp32 W view, rows, cols, fragment-ordered bf16 copy, layout) of conv1..3 (layout -1) and, with
@@ -374,10 +407,10 @@ class CNNEngine:
         (``CNNActorCritic.param_groups``), so data parallelism can all-reduce it while the conv backward (``"trunk"``
         stage) runs and then the rest -- conv, head and fc-bias gradients, the latter two summed from the head
         launch's partial planes by the trunk stage's finaliser -- as the contiguous range before it."""
-        base = self.flat.grad.data_ptr()
+        base = self._gslab.data_ptr()
         start = (self.gWfc.data_ptr() - base) // 4
         end = start + self.gWfc.numel()
-        assert self.flat.grad.numel() - end < 64, "the fc weight must close the slab (up to alignment padding)"
+        assert self._gslab.numel() - end < 64, "the fc weight must close the slab (up to alignment padding)"
         for g in (self.gW1, self.gb1, self.gW2, self.gb2, self.gW3, self.gb3, self.gbfc, self.gWh, self.gbh):
             assert (g.data_ptr() - base) // 4 + g.numel() <= start, "every other gradient must precede the fc weight"
         return start, end
@@ -769,7 +802,7 @@ class CNNEngine:
         fused_rows = self.fused_bwd and bias_rows
         planes = tuple(sorted((self._cur_planes if planes is None else planes).items())) if self.det_wgrad else ()
         presum = want_parts and self._cur_presum and self._fcb_sq is not None
-        key = (b.B, want_parts, fused_rows, planes, presum)
+        key = (b.B, want_parts, fused_rows, planes, presum, self._gslab.data_ptr())
         words = self._fin_words.get(key)
         if words is None:
             segs = []
@@ -785,7 +818,7 @@ class CNNEngine:
                      "ae_bh": self.gbh, "ae_bfc": self.gbfc}[name]
                 src_of[g.data_ptr()] = (self._planes[name].data_ptr(), g.numel(), S)
             for p, off in zip(flat.params, flat.offsets):
-                g = flat.grad[off:off + p.numel()]
+                g = self._gslab[off:off + p.numel()]
                 src = src_of.get(g.data_ptr())
                 if src is not None:
                     segs.append((g.data_ptr(), src[0], g.numel(), src[1], src[2]))

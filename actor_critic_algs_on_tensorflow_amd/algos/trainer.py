@@ -976,14 +976,19 @@ class ActorCriticTrainer:
         return self._a2c_dp_schedule()
 
     def _update_body_lag1(self):
-        """RCCL lag-1 A2C as ONE captured graph per update: the all-reduce of the PREVIOUS update's gradient C is
-        forked onto RCCL's stream at the start, so it runs under this update's rollout, loss and backward (which
-        write G); then C is applied, C <- G, G <- 0, and C is packed for the next replay's all-reduce. The optimiser
-        launches are gated on a device flag that the C <- G move sets (``_lag1_gate``): the first replay after
-        capture and the first after :meth:`flush_pending` hold no gradient in C and apply nothing -- parameters,
-        moments and the Adam step count unchanged, exactly as the segmented schedule's first update."""
-        dp, C = self.dp, self._comm_grad
-        w = dp.allreduce_async(dp.comm_view(C))
+        """RCCL lag-1 A2C as ONE captured graph per update, on PING-PONG gradient slabs: the graph set of ring phase p
+        has the engine write G[p] and the optimiser read G[1-p]. The all-reduce of G[1-p] -- the PREVIOUS update's
+        gradient -- is forked onto RCCL's stream at the start, so it runs under this update's rollout, loss and
+        backward (which write G[p]); then G[1-p] is applied and G[p] packed for the next replay's all-reduce. No
+        C <- G copy, and with a backward that stores every element no zeroing either (the optimiser clears the slab
+        it read otherwise: the next backward into it accumulates). The optimiser launches are gated on a device flag
+        (``_lag1_gate``) set at the end of every replay: the first replay after capture and the first after
+        :meth:`flush_pending` hold no gradient in G[1-p] and apply nothing -- parameters, moments and the Adam step
+        count unchanged, exactly as the segmented schedule's first update."""
+        dp, G = self.dp, self._lag1_slabs
+        p = self.storage.phase
+        prev = G[1 - p]
+        w = dp.allreduce_async(dp.comm_view(prev))
         self._defer_allreduce = True
         try:
             self.collect()
@@ -992,11 +997,20 @@ class ActorCriticTrainer:
         finally:
             self._defer_allreduce = False
         w.wait()
-        dp.unpack(C)
+        dp.unpack(prev)
         self._post_body()
-        self._grad_move()
-        dp.pack(C)
+        self._lag1_gate.fill_(1)   # from the next replay on, the slab it reads holds a gradient
+        dp.pack(G[p])
         self.storage.roll_over()
+
+    def _bind_lag1_phase(self, p):
+        """Engine writes G[p], optimisers read G[1-p] (the bf16 comm buffer of G[1-p] with direct reads)."""
+        G = self._lag1_slabs
+        self.engine.use_grad_slab(G[p])
+        for opt in self.opts.values():
+            opt.bind_grad(G[1 - p])
+            if self.dp.direct_read:
+                opt.bind_grad16(self.dp.comm_view(G[1 - p]))
 
     def update_body(self):
         with self.timer.phase("rollout"):
@@ -1046,6 +1060,8 @@ class ActorCriticTrainer:
             self._comm_grad = torch.zeros_like(self.flat.grad)
             for opt in self.opts.values():
                 opt.bind_grad(self._comm_grad)
+                if self.dp.direct_read:   # bf16 buckets read in place: C's own comm buffer
+                    opt.bind_grad16(self.dp.comm_view(self._comm_grad))
             self.dp.pack(self._comm_grad)
 
     def _capture(self, warmup):
@@ -1116,11 +1132,16 @@ class ActorCriticTrainer:
             # update, zero host-issued collectives
             lag1 = self._lag1() and self._a2c_dp_schedule()
             if lag1:
-                self._bind_comm_grad()
-                if getattr(self, "_lag1_gate", None) is None:   # closed: C holds no gradient yet
+                if getattr(self, "_lag1_slabs", None) is None:   # G[0] is the slab the engine was built on
+                    self._lag1_slabs = [self.flat.grad, torch.zeros_like(self.flat.grad)]
+                    for g in self._lag1_slabs:
+                        self.dp.prepare(g)
+                        self.dp.pack(g)
+                if getattr(self, "_lag1_gate", None) is None:   # closed: no slab holds a gradient yet
                     self._lag1_gate = torch.zeros(1, dtype=torch.int32, device=self.device)
                     for opt in self.opts.values():
                         opt.set_gate(self._lag1_gate)
+                self._bind_lag1_phase(self.storage.phase)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
                 if lag1:
@@ -1216,14 +1237,18 @@ class ActorCriticTrainer:
     def flush_pending(self):
         """lag-1 DP: apply the last all-reduced gradient (end of training / before a checkpoint)."""
         if self.graph is not None and getattr(self, "_lag1_inline", False):
-            # the one-graph schedule leaves the last update's gradient packed in C (its all-reduce would open the
-            # next replay): all-reduce and apply it now, then C = 0 (the next replay applies nothing twice)
-            self.dp.allreduce_packed(self._comm_grad)
-            self.dp.unpack(self._comm_grad)
+            # the one-graph schedule leaves the last update's gradient packed in G[q] (its all-reduce would open the
+            # next replay): all-reduce and apply it now (eagerly, the optimisers pointed at G[q]), then G[q] = 0 and
+            # the gate closed (the next replay applies nothing twice)
+            q = 1 - self.storage.phase   # the last replay's phase (its rollover flipped the ring)
+            last = self._lag1_slabs[q]
+            self.dp.allreduce_packed(last)
+            self.dp.unpack(last)
+            self._bind_lag1_phase(1 - q)   # optimisers read G[q]
             self._post_body()
-            self._comm_grad.zero_()
+            last.zero_()
             self._lag1_gate.zero_()   # the next replay's optimiser step has nothing to apply
-            self.dp.pack(self._comm_grad)
+            self.dp.pack(last)
             return
         if self.graph is not None and self.graph[0] == "lag1" and self._comm_work is not None:
             self._comm_work.wait()

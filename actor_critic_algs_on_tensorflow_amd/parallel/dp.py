@@ -59,7 +59,7 @@ class DataParallel:
         if compress not in (None, "bf16"):
             raise ValueError(f"compress must be None/'none'/'bf16', got {compress!r}")
         self.compress = compress
-        self._cbuf = None
+        self._cbufs = {}   # gradient slab address -> its persistent bf16 comm buffer
         # bf16 buckets read in place by the optimisers (trainer binds them): unpack is then a no-op
         self.direct_read = False
         # RCCL ("nccl") collectives are stream-ordered and capturable: the trainer records them INSIDE its
@@ -101,15 +101,17 @@ class DataParallel:
 
     # -- gradient buckets (optionally bf16) ----------------------------------------------------------------------
     def prepare(self, grad):
-        """Allocates the persistent comm buffer (call outside any graph capture)."""
-        if self.compress and (self._cbuf is None or self._cbuf.numel() != grad.numel()):
-            self._cbuf = torch.zeros(grad.numel(), dtype=torch.bfloat16, device=grad.device)
+        """Allocates the persistent comm buffer of gradient slab ``grad`` (call outside any graph capture)."""
+        if self.compress:
+            b = self._cbufs.get(grad.data_ptr())
+            if b is None or b.numel() != grad.numel():
+                self._cbufs[grad.data_ptr()] = torch.zeros(grad.numel(), dtype=torch.bfloat16, device=grad.device)
 
     def comm_view(self, grad, s=0, e=None):
-        """The tensor the collective runs on for slab range [s, e)."""
+        """The tensor the collective runs on for range [s, e) of gradient slab ``grad``."""
         if self.compress:
             self.prepare(grad)
-            return self._cbuf[s:e]
+            return self._cbufs[grad.data_ptr()][s:e]
         return grad[s:e]
 
     @torch.no_grad()
@@ -120,7 +122,7 @@ class DataParallel:
     @torch.no_grad()
     def unpack(self, grad, s=0, e=None):
         if self.compress and not self.direct_read:
-            grad[s:e].copy_(self._cbuf[s:e])
+            grad[s:e].copy_(self.comm_view(grad, s, e))
 
     @torch.no_grad()
     def allreduce_packed(self, grad, s=0, e=None):

@@ -23,8 +23,6 @@ transposes) and gradients are written straight into the gradient slab.
 """
 from __future__ import annotations
 
-import os
-
 import torch
 
 from .. import _native
@@ -133,13 +131,6 @@ class MLPEngine:
         self.n_weights = sum(l.in_features * l.out_features for tw in self.towers for l in tw)
         # reference tower shapes: the train launches take the SPEC path (every weight fragment preloaded, mlp.hip)
         self.spec = True
-        # ... and, with a gaussian head, the 4-row path (mlp_train4_kernel: 4x the workgroups on 4x4x1 MFMAs, weights
-        # read straight from the slab) for contiguous minibatches of a multiple of 4 rows
-        shapes = [[(l.in_features, l.out_features) for l in tw] for tw in self.towers]
-        D = self.D
-        self.rows4 = (os.environ.get("ACA_MLP_ROWS4", "1") != "0" and self.head == 2 and D <= 64
-                      and shapes[0] == [(D, 128), (128, 128), (128, 64), (64, self.A)]
-                      and shapes[1] == [(D, 256), (256, 128), (128, 1)])
         self.sync_shadow()
 
     def frag_copies(self):
@@ -203,14 +194,13 @@ class MLPEngine:
         """Per-workgroup partial rows of the train kernel (loss statistics + log-std gradient), summed by the
         weight-gradient kernel -- no same-address atomics from every workgroup."""
         if B not in self._mparts:
-            # (ceil(B/4) rows: room for the 4-row path's workgroups)
-            self._mparts[B] = torch.zeros((B + 3) // 4 * MPART_W, dtype=torch.float32, device=self.dev)
+            self._mparts[B] = torch.zeros((B + BM - 1) // BM * MPART_W, dtype=torch.float32, device=self.dev)
         return self._mparts[B]
 
     def _fwd(self, mode, obs, B, tw_base=0, ntw=2, desc_B=None, idx=None, perm=None, tg=None, env_ids=None, key_shift=0,
              seed=0, act_out=None, logp_out=None, ent_out=None, v_out=None, act_in=None, logp_old=None, adv=None,
              ret=None, v_old=None, ent_coef=None, kl_coef=None, vf_coef=1.0, ppo_clip=0.0, v_clip=0.0, ppo=False,
-             stamps=None, rows=16):
+             stamps=None):
         ops = _native.require()
         desc, _ = self.desc(desc_B)
         obs2 = obs.reshape(obs.shape[0], -1)
@@ -221,7 +211,7 @@ class MLPEngine:
                     act_in, logp_old, adv, ret, v_old, ent_coef, kl_coef, float(vf_coef), float(ppo_clip),
                     float(v_clip or 0.0), bool(ppo), self.g_log_std if mode == 2 else None,
                     self.mstats if mode == 2 else None, self._mpart(B) if mode == 2 else None, stamps,
-                    self._hdescs[desc_B] if (mode == 2 and self.spec) else None, rows)
+                    self._hdescs[desc_B] if (mode == 2 and self.spec) else None)
 
     # ------------------------------------------------------------------------------------------- API
     def policy_step(self, obs, act_out, logp_out, ent_out, v_out, tg, env_ids, key_shift, seed):
@@ -246,10 +236,9 @@ class MLPEngine:
         :attr:`parts` (when ``want_parts``). ``bump``: an int64 counter the weight-gradient launch advances by one
         (the PPO update counter, after the update's last minibatch -- no separate launch)."""
         ops = _native.require()
-        rows = 4 if (self.rows4 and self.spec and idx is None and perm is None and B % 4 == 0 and stamps is None) else 16
         self._fwd(2, obs, B, 0, 2, desc_B=B, idx=idx, perm=perm, act_in=actions, logp_old=logp_old, adv=adv, ret=ret,
                   v_old=v_old, ent_coef=ent_coef, kl_coef=kl_coef, vf_coef=vf_coef, ppo_clip=ppo_clip,
-                  v_clip=v_clip, ppo=ppo, stamps=stamps, rows=rows)
+                  v_clip=v_clip, ppo=ppo, stamps=stamps)
         nrt = (B + BM - 1) // BM
         nsplit = max(1, min(16, nrt // 128))
         self.last_stores_all = nsplit == 1   # every gradient element stored (no atomics): no zeroing needed after use
@@ -258,7 +247,7 @@ class MLPEngine:
         items = self.wgrad_items(B, use_parts, clips)
         ls_part = self.parts[0][self.items[0]:self.items[0] + 1] if (use_parts and self.g_log_std is not None) else None
         ops.mlp_wgrad(items, nrt, nsplit, self.g_log_std, self.A, ls_part, float(clips[0] or -1.0), st, ent_coef,
-                      kl_coef, self._mpart(B), (B + rows - 1) // rows, bump)
+                      kl_coef, self._mpart(B), nrt, bump)
         return use_parts
 
     def wgrad_items(self, B, parts=True, clips=(None, None)):

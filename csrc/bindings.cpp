@@ -995,9 +995,8 @@ void mlp_fwd(Tensor desc, int64_t tw_base, int64_t ntw, int64_t mode, int64_t ld
              c10::optional<Tensor> v_old, c10::optional<Tensor> ent_coef, c10::optional<Tensor> kl_coef,
              double vf_coef, double ppo_clip, double v_clip, bool ppo, c10::optional<Tensor> g_log_std,
              c10::optional<Tensor> mstats, c10::optional<Tensor> mpart, c10::optional<Tensor> stamps,
-             c10::optional<Tensor> hdesc, int64_t rows) {
+             c10::optional<Tensor> hdesc) {
   need(desc, at::kLong, "desc");
-  TORCH_CHECK(rows == 16 || rows == 4, "mlp_fwd: rows per workgroup must be 16 or 4");
   TORCH_CHECK(desc.numel() * 8 >= (int64_t)(2 * sizeof(aca::MlpTower)), "mlp_fwd: desc too small");
   TORCH_CHECK(obs.is_cuda() && obs.scalar_type() == at::kFloat && obs.dim() == 2 && obs.stride(1) == 1,
               "mlp_fwd: obs must be fp32 [rows, D] with unit column stride");
@@ -1051,8 +1050,8 @@ void mlp_fwd(Tensor desc, int64_t tw_base, int64_t ntw, int64_t mode, int64_t ld
   a.g_log_std = const_cast<float*>(copt<float>(g_log_std, at::kFloat, "g_log_std"));
   a.mstats = const_cast<float*>(copt<float>(mstats, at::kFloat, "mstats"));
   a.mpart = const_cast<float*>(copt<float>(mpart, at::kFloat, "mpart"));
-  if (a.mpart) TORCH_CHECK(mode == 2 && mpart->numel() >= (B + rows - 1) / rows * aca::MPART_W,
-                           "mlp_fwd: mpart must hold ceil(B/rows) rows of ", aca::MPART_W, " (train mode)");
+  if (a.mpart) TORCH_CHECK(mode == 2 && mpart->numel() >= (B + 15) / 16 * aca::MPART_W,
+                           "mlp_fwd: mpart must hold ceil(B/16) rows of ", aca::MPART_W, " (train mode)");
   a.inv_B = B > 0 ? 1.0f / (float)B : 0.f;
   a.stamps = reinterpret_cast<int64_t*>(stamps_ptr(stamps, 2));   // [2 towers][16 phases]
   // SPEC train path (mlp.hip): hdesc = the CPU copy of desc; taken when both towers have the reference shapes
@@ -1075,14 +1074,6 @@ void mlp_fwd(Tensor desc, int64_t tw_base, int64_t ntw, int64_t mode, int64_t ld
                       "mlp_fwd: hdesc lacks fragment copies / workspace");
       spec = g0;
     }
-  }
-  // 4-row train path (mlp.hip mlp_train4_kernel): the reference towers, gaussian head, contiguous rows -- the caller
-  // asks for it (its weight-gradient launch then sums ceil(B/4) partial rows), so an ineligible call is an error
-  if (rows == 4) {
-    TORCH_CHECK(spec > 0 && head == 2 && !a.idx && !a.perm_uc && B % 4 == 0 && a.mpart && a.D <= 64,
-                "mlp_fwd: the 4-row train path needs the reference towers, a gaussian head, contiguous rows, "
-                "B % 4 == 0, D <= 64 and mpart");
-    spec = -1;
   }
   const bool policy = tw_base == 0;
   if (policy) {
@@ -2048,7 +2039,7 @@ TORCH_LIBRARY(acamd, m) {
         "int A, Tensor? log_std, Tensor? ac_scale, Tensor? tg, Tensor? env_ids, int key_shift, int seed, "
         "Tensor? act_out, Tensor? logp_out, Tensor? ent_out, Tensor? v_out, Tensor? act_in, Tensor? logp_old, "
         "Tensor? adv, Tensor? ret, Tensor? v_old, Tensor? ent_coef, Tensor? kl_coef, float vf_coef, float ppo_clip, "
-        "float v_clip, bool ppo, Tensor? g_log_std, Tensor? mstats, Tensor? mpart=None, Tensor? stamps=None, Tensor? hdesc=None, int rows=16) -> ()");
+        "float v_clip, bool ppo, Tensor? g_log_std, Tensor? mstats, Tensor? mpart=None, Tensor? stamps=None, Tensor? hdesc=None) -> ()");
   m.def("mlp_wgrad(Tensor items, int nrt, int nsplit, Tensor? g_log_std, int A, Tensor? ls_part, float ls_clip, "
         "Tensor? stats, Tensor ent_coef, Tensor kl_coef, Tensor mpart, int mpart_rows, Tensor? bump) -> ()");
   m.def("mlp_epoch_gather(Tensor obs, Tensor act, Tensor logp, Tensor adv, Tensor ret, Tensor? v, Tensor o_obs, "

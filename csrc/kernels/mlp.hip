@@ -1606,438 +1606,6 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_rollout_kernel(RolloutArgs a)
   }
 }
 
-// ------------------------------------------------------------------------------------------------ 4-row train
-// mlp_train4_kernel: the learner (mini)batch of the reference towers (actor D -> 128 -> 128 -> 64 -> A, critic
-// D -> 256 -> 128 -> 1) on 4-ROW workgroups and 4x4x1 MFMAs -- the rollout's layout (ROLL_RB, RollLayer) -- instead
-// of 16-row tiles on 16x16x4: 128 workgroups per tower at a 512-row minibatch (256 on the chip, one per CU) where
-// the 16-row path launches 32, each with a quarter of the f32 MFMA work per layer (the 16-row critic tile spends
-// ~0.9 us per 256 x 128 layer at the CU's f32 MFMA rate). Every wave holds its slices of every weight -- forward W
-// columns over a K range, data-gradient W rows over an N range -- in registers for the whole launch, loaded at entry
-// straight from the fp32 master slab (row-major [in][out]: the forward slice with 4-byte loads of 64 consecutive
-// columns, the data-gradient slice with 4-byte loads along a row; no fragment copies needed); clamped addresses
-// (zero activation / gradient pads make the clamped operands harmless) so every load is unconditional.
-// Per layer: the waves' partial tiles meet in LDS (`red`), the epilogue sums them in K order, adds the bias and
-// applies the activation (forward) or multiplies by its derivative (data gradient). The workspace layout, the
-// loss head and the per-workgroup partial rows are those of the 16-row path (mlp_tower): mlp_wgrad_kernel consumes
-// them unchanged (mpart rows = workgroups).
-constexpr int T4_MAXN = 256;
-
-// forward weight slice of a wave: W[k][c], k = sp kper + 4 u + s (clamped to K - 1), c = cg 64 + lane (clamped)
-// Every workgroup of the launch streams the same weights at about the same time: walked in the same order, all of a
-// XCD's CUs would ask the same L2 lines (channel) at once. Each workgroup therefore walks its K range starting at
-// float4 step blockIdx.x mod NU (t4_rot; the MFMA reads the matching X columns), spreading the concurrent requests
-// over the whole matrix. (The sum order over K changes with it: fp32 rounding differences between workgroups only.)
-template <class L>
-__device__ __forceinline__ int t4_rot(int u) {
-  static_assert((L::NU & (L::NU - 1)) == 0, "power-of-two float4 steps");
-  return (u + (int)blockIdx.x) & (L::NU - 1);
-}
-
-// roll_layer_mfma with the X float4 read per step (the 16-float4 slices of the wide layers would otherwise hold 64
-// more registers next to the resident weights)
-template <class L>
-__device__ __forceinline__ void t4_mfma(const float4 (&w)[L::NU], const float* __restrict__ X, int ldx,
-                                        float* __restrict__ red) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (wave < L::CG * L::S) {
-    const int sp = wave / L::CG;
-    const float* xr = X + (lane & 3) * ldx + sp * L::kper;
-    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int u = 0; u < L::NU; ++u) {
-      const float4 x = *reinterpret_cast<const float4*>(xr + 4 * t4_rot<L>(u));
-      acc = mfma4x4(x.x, w[u].x, acc);
-      acc = mfma4x4(x.y, w[u].y, acc);
-      acc = mfma4x4(x.z, w[u].z, acc);
-      acc = mfma4x4(x.w, w[u].w, acc);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) red[(wave * 4 + i) * 64 + lane] = acc[i];
-  }
-}
-
-template <class L>
-__device__ __forceinline__ void t4_load_fw(float4 (&w)[L::NU], gcf32* __restrict__ W, int K, int N) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int cg = wave % L::CG, sp = wave / L::CG;
-  const int c = min(cg * 64 + lane, N - 1);
-#pragma unroll
-  for (int u = 0; u < L::NU; ++u) {
-    float v[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) v[s] = W[(size_t)min(sp * L::kper + 4 * t4_rot<L>(u) + s, K - 1) * N + c];
-    w[u] = make_float4(v[0], v[1], v[2], v[3]);
-  }
-}
-// data-gradient weight slice: the product dX = dP W^T runs over n (its K dim) into columns k: W[k][n], k = cg 64 +
-// lane, n = sp kper + 4 u + s -- VEC (N = the padded K dim, a multiple of 4): one 16-byte load along the row;
-// else (the 6-action / 1-value heads) 4-byte loads, n clamped
-template <class L, bool VEC>
-__device__ __forceinline__ void t4_load_bw(float4 (&w)[L::NU], gcf32* __restrict__ W, int K, int N) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int cg = wave % L::CG, sp = wave / L::CG;
-  const int k = min(cg * 64 + lane, K - 1);
-#pragma unroll
-  for (int u = 0; u < L::NU; ++u) {
-    if constexpr (VEC) {
-      const floatx4 v = *(gcfx4*)(W + (size_t)k * N + sp * L::kper + 4 * t4_rot<L>(u));
-      w[u] = make_float4(v[0], v[1], v[2], v[3]);
-    } else {
-      float v[4];
-#pragma unroll
-      for (int s = 0; s < 4; ++s) v[s] = W[(size_t)k * N + min(sp * L::kper + 4 * t4_rot<L>(u) + s, N - 1)];
-      w[u] = make_float4(v[0], v[1], v[2], v[3]);
-    }
-  }
-}
-
-// forward epilogue: Y[i][c] = act(sum + b[c]) for c < N, 0 on [N, NP)
-template <class L>
-__device__ __forceinline__ void t4_fwd_epi(const float* __restrict__ red, const float* __restrict__ bias, int N,
-                                           float slope, float* __restrict__ Y, int ldy, int NP) {
-  for (int e = threadIdx.x; e < ROLL_RB * NP; e += MLP_THREADS) {
-    const int i = e / NP, c = e - i * NP;
-    float v = 0.f;
-    if (c < N) {
-      const int cg = c >> 6, l = c & 63;
-      float sum = 0.f;
-#pragma unroll
-      for (int sp = 0; sp < L::S; ++sp) sum += red[((sp * L::CG + cg) * 4 + i) * 64 + l];
-      v = act_fwd(sum + bias[c], slope);
-    }
-    Y[i * ldy + c] = v;
-  }
-}
-// data-gradient epilogue: dP[i][k] = sum * act'(Y[i][k]) for k < K, 0 on [K, KP)
-template <class L>
-__device__ __forceinline__ void t4_bwd_epi(const float* __restrict__ red, const float* __restrict__ Yp, int ldyp,
-                                           float slope, int K, float* __restrict__ dP, int ldp, int KP) {
-  for (int e = threadIdx.x; e < ROLL_RB * KP; e += MLP_THREADS) {
-    const int i = e / KP, k = e - i * KP;
-    float v = 0.f;
-    if (k < K) {
-      const int cg = k >> 6, l = k & 63;
-      float sum = 0.f;
-#pragma unroll
-      for (int sp = 0; sp < L::S; ++sp) sum += red[((sp * L::CG + cg) * 4 + i) * 64 + l];
-      v = sum * act_bwd(Yp[i * ldyp + k], slope);
-    }
-    dP[i * ldp + k] = v;
-  }
-}
-// the 4 rows of a tile as one float4 per column into the 16 x 16 blocked workspace (blk_out layout); the pad columns
-// up to the block edge are copied too (zero in LDS)
-__device__ __forceinline__ void t4_ws_store(const float* __restrict__ Y, int ldy, int w, gf32* __restrict__ base,
-                                            int row0) {
-  const int nct = (w + 15) >> 4;
-  gf32* blk = base + (size_t)(row0 >> 4) * nct * 256 + (row0 & 15);
-  for (int c = threadIdx.x; c < 16 * nct; c += MLP_THREADS)
-    *(__attribute__((address_space(1))) floatx4*)(blk + (c >> 4) * 256 + (c & 15) * 16) =
-        floatx4{Y[c], Y[ldy + c], Y[2 * ldy + c], Y[3 * ldy + c]};
-}
-
-template <int TW, int KP0>
-__device__ __forceinline__ void t4_tower(const MlpArgs& a) {
-  constexpr bool POL = TW == 0;
-  // layer geometry: widths (N padded to 16 for the 6-action / 1-value heads), LDS strides
-  constexpr int N0 = POL ? 128 : 256, N1 = 128, N2 = POL ? 64 : 16, N3 = 16;
-  constexpr int NL = POL ? 4 : 3;
-  using F0 = RollLayer<KP0, N0>;
-  using F1 = RollLayer<N0, N1>;
-  using F2 = RollLayer<N1, N2>;
-  using F3 = RollLayer<64, N3>;
-  using B1 = RollLayer<N1, N0>;    // dP0 = dP1 W1^T: K dim N1, columns N0
-  using B2 = RollLayer<N2, N1>;    // dP1 = dP2 W2^T
-  using B3 = RollLayer<N3, 64>;    // (actor) dP2 = dP3 W3^T
-  __shared__ __attribute__((aligned(16))) float X0[ROLL_RB * (KP0 + 4)];
-  __shared__ __attribute__((aligned(16))) float Y0[ROLL_RB * (N0 + 4)], Y1[ROLL_RB * (N1 + 4)],
-      Y2[ROLL_RB * (N2 + 4)], Y3[ROLL_RB * (N3 + 4)];
-  __shared__ __attribute__((aligned(16))) float dPa[ROLL_RB * (T4_MAXN + 4)], dPb[ROLL_RB * (T4_MAXN + 4)];
-  __shared__ __attribute__((aligned(16))) float red[MLP_THREADS / 64 * 4 * 64];
-  __shared__ float sb[4][T4_MAXN];   // biases
-  __shared__ float hl[ROLL_RB][MLP_MAXA], ht[ROLL_RB][MLP_MAXA], hd[ROLL_RB][MLP_MAXA], hg[ROLL_RB];
-  __shared__ float hls[MLP_MAXA], hsc[MLP_MAXA], hco[2];
-  __shared__ float hst[8][ROLL_RB];
-  __shared__ int64_t ts[16];   // diagnostics (a.stamps): s_memrealtime at phase ends, workgroup (0, tower), thread 0
-  const MlpTower& T = a.htw[TW];
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const bool stamping = a.stamps && blockIdx.x == 0;
-  if (stamping && tid < 16) ts[tid] = 0;
-  auto stamp = [&](int slot) {
-    if (stamping && tid == 0) ts[slot] = __builtin_amdgcn_s_memrealtime();
-  };
-  stamp(0);
-  const int row0 = blockIdx.x * ROLL_RB;
-  gcf32* W0 = P_<const float>(T.W[0]);
-  gcf32* W1 = P_<const float>(T.W[1]);
-  gcf32* W2 = P_<const float>(T.W[2]);
-  gcf32* W3 = P_<const float>(T.W[POL ? 3 : 2]);
-  const int D = a.D, NA = (int)T.out[NL - 1];
-  // ---- every load up front: the small operands (input rows, biases, head inputs and parameters) first, into
-  // registers, then the weight slices in use order; the LDS stores of the small operands follow the weight requests
-  // (a store right after its load would wait out the load before the weight stream is even requested)
-  float xv = 0.f;
-  if (tid < ROLL_RB * KP0) {
-    const int i = tid / KP0, c = tid - i * KP0;
-    if (c < D) xv = a.obs[(size_t)(row0 + i) * a.ld_obs + c];
-  }
-  constexpr int NBV = (NL * T4_MAXN + MLP_THREADS - 1) / MLP_THREADS;
-  float bv[NBV];
-#pragma unroll
-  for (int j = 0; j < NBV; ++j) {
-    const int e = tid + MLP_THREADS * j;
-    const int l = e / T4_MAXN, c = e - l * T4_MAXN;
-    bv[j] = 0.f;
-    if (l < NL && c < (int)T.out[l]) bv[j] = P_<const float>(T.b[l])[c];
-  }
-  float e_act = 0.f, e_lo = 0.f, e_adv = 0.f, e_ret = 0.f, e_vo = 0.f, hp = 0.f;
-  if (POL && tid < ROLL_RB * MLP_MAXA) {
-    const int r = tid / MLP_MAXA, j = tid % MLP_MAXA;
-    if (j < a.A) e_act = a.act_f_in[(size_t)(row0 + r) * a.A + j];
-  }
-  if (tid < ROLL_RB) {
-    if (POL) {
-      e_lo = a.logp_old[row0 + tid];
-      e_adv = a.adv[row0 + tid];
-    } else {
-      e_ret = a.ret[row0 + tid];
-      if (a.v_old && a.v_clip > 0.f) e_vo = a.v_old[row0 + tid];
-    }
-  }
-  if (POL && tid >= 64 && tid < 64 + 2 * MLP_MAXA + 2) {   // (wave 1: wave 0 holds the row inputs)
-    const int i = tid - 64;
-    if (i < MLP_MAXA) { if (i < a.A) hp = a.log_std[i]; }
-    else if (i < 2 * MLP_MAXA) { if (i - MLP_MAXA < a.A) hp = a.ac_scale[i - MLP_MAXA]; }
-    else if (i == 2 * MLP_MAXA) hp = *a.kl_coef;
-    else hp = *a.ent_coef;
-  }
-  float4 f0[F0::NU], f1[F1::NU], f2[F2::NU], f3[F3::NU];
-  t4_load_fw<F0>(f0, W0, D, N0);
-  t4_load_fw<F1>(f1, W1, N0, N1);
-  if constexpr (POL) {
-    t4_load_fw<F2>(f2, W2, N1, N2);
-    t4_load_fw<F3>(f3, W3, 64, NA);
-  } else {
-    t4_load_fw<F2>(f2, W3, N1, NA);
-  }
-  // (the critic's W1 data-gradient slice, 64 registers, is requested once layer 1 has consumed its forward slice)
-  float4 b1[B1::NU], b2[B2::NU], b3[B3::NU];
-  if constexpr (POL) {
-    t4_load_bw<B1, true>(b1, W1, N0, N1);
-    t4_load_bw<B2, true>(b2, W2, N1, N2);
-    t4_load_bw<B3, false>(b3, W3, 64, NA);
-  } else {
-    t4_load_bw<B2, false>(b2, W3, N1, NA);
-  }
-  if (tid < ROLL_RB * KP0) {
-    const int i = tid / KP0, c = tid - i * KP0;
-    X0[i * (KP0 + 4) + c] = xv;
-  }
-#pragma unroll
-  for (int j = 0; j < NBV; ++j) {
-    const int e = tid + MLP_THREADS * j;
-    if (e < NL * T4_MAXN) sb[e / T4_MAXN][e % T4_MAXN] = bv[j];
-  }
-  if (POL && tid >= 64 && tid < 64 + 2 * MLP_MAXA + 2) {
-    const int i = tid - 64;
-    if (i < MLP_MAXA) hls[i] = hp;
-    else if (i < 2 * MLP_MAXA) hsc[i - MLP_MAXA] = hp;
-    else hco[i - 2 * MLP_MAXA] = hp;
-  }
-  stamp(1);
-  __syncthreads();
-  stamp(2);
-  // ---- forward
-  const float s0 = act_slope((int)T.act[0]), s1 = act_slope((int)T.act[1]), s2 = act_slope((int)T.act[2]);
-  t4_mfma<F0>(f0, X0, KP0 + 4, red);
-  __syncthreads();
-  t4_fwd_epi<F0>(red, sb[0], N0, s0, Y0, N0 + 4, N0);
-  __syncthreads();
-  stamp(3);
-  t4_mfma<F1>(f1, Y0, N0 + 4, red);
-  if constexpr (!POL) t4_load_bw<B1, true>(b1, W1, N0, N1);
-  __syncthreads();
-  t4_fwd_epi<F1>(red, sb[1], N1, s1, Y1, N1 + 4, N1);
-  __syncthreads();
-  stamp(4);
-  float* Yo;
-  int ldo;
-  if constexpr (POL) {
-    t4_mfma<F2>(f2, Y1, N1 + 4, red);
-    __syncthreads();
-    t4_fwd_epi<F2>(red, sb[2], N2, s2, Y2, N2 + 4, N2);
-    __syncthreads();
-    stamp(5);
-    t4_mfma<F3>(f3, Y2, N2 + 4, red);
-    __syncthreads();
-    t4_fwd_epi<F3>(red, sb[3], NA, act_slope((int)T.act[3]), Y3, N3 + 4, N3);
-    __syncthreads();
-    stamp(6);
-    Yo = Y3;
-    ldo = N3 + 4;
-  } else {
-    t4_mfma<F2>(f2, Y1, N1 + 4, red);
-    __syncthreads();
-    t4_fwd_epi<F2>(red, sb[2], NA, s2, Y2, N2 + 4, N2);
-    __syncthreads();
-    stamp(5);
-    Yo = Y2;
-    ldo = N2 + 4;
-  }
-  // ---- loss head (the 16-row path's arithmetic, mlp_tower): top-layer gradient into dPa, statistics partials
-  float* dP = dPa;
-  constexpr int ldP = T4_MAXN + 4;
-  for (int e = tid; e < ROLL_RB * ldP; e += MLP_THREADS) dP[e] = 0.f;
-  if (POL) {
-    if (tid < ROLL_RB * MLP_MAXA) {
-      const int r = tid / MLP_MAXA, j = tid % MLP_MAXA;
-      if (j < a.A) {
-        const float ls = fminf(fmaxf(hls[j], -2.5f), 2.5f);
-        const float th = tanhf(Yo[r * ldo + j]);
-        const float mu = th * hsc[j];
-        const float aj = e_act;
-        const float zz = (aj - mu) * expf(-ls);
-        hl[r][j] = -0.5f * zz * zz - ls - HALF_LOG_2PI;
-        ht[r][j] = th;
-        hd[r][j] = aj - mu;
-      }
-    }
-  }
-  __syncthreads();
-  if (tid < ROLL_RB) {
-    const int r = tid;
-    float st[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (!POL) {
-      const float v = Yo[r * ldo];
-      const float R_ = e_ret;
-      float dv = 2.f * (v - R_), l2 = (v - R_) * (v - R_);
-      if (a.v_old && a.v_clip > 0.f) {
-        const float vo = e_vo;
-        const float d = fminf(fmaxf(v - vo, -a.v_clip), a.v_clip);
-        const float vc = vo + d;
-        const float l2c = (vc - R_) * (vc - R_);
-        const bool inr = (v - vo) >= -a.v_clip && (v - vo) <= a.v_clip;
-        if (l2c > l2) { dv = inr ? 2.f * (vc - R_) : 0.f; l2 = l2c; }
-        else if (l2c == l2) dv = 0.5f * dv + 0.5f * (inr ? 2.f * (vc - R_) : 0.f);
-      }
-      dP[r * ldP] = a.vf_coef * a.inv_B * dv;
-      st[3] = l2;
-    } else {
-      float lp = 0.f, H = 0.f;
-      for (int j = 0; j < a.A; ++j) {
-        lp += hl[r][j];
-        H += 0.5f + HALF_LOG_2PI + fminf(fmaxf(hls[j], -2.5f), 2.5f);
-      }
-      const float lo = e_lo, adv = e_adv;
-      const float beta = hco[0];
-      float dsurr;
-      if (a.ppo) {
-        const float ratio = expf(lp - lo);
-        const float s1_ = ratio * adv;
-        const float rc = fminf(fmaxf(ratio, 1.f - a.ppo_clip), 1.f + a.ppo_clip);
-        const float s2_ = rc * adv;
-        dsurr = (s1_ <= s2_) ? ratio * adv : 0.f;
-        st[0] = -fminf(s1_, s2_);
-        st[4] = fabsf(ratio - 1.f) > a.ppo_clip ? 1.f : 0.f;
-        st[6] = ratio;
-      } else {
-        dsurr = adv;
-        st[0] = -adv * lp;
-        st[6] = 1.f;
-      }
-      st[1] = (lo - lp) * (lo - lp);
-      st[2] = H;
-      hg[r] = a.inv_B * (-dsurr - 2.f * beta * (lo - lp));
-    }
-#pragma unroll
-    for (int k = 0; k < 8; ++k) hst[k][r] = st[k];
-  }
-  __syncthreads();
-  if (tid < 8 && (POL ? tid != 3 : tid == 3)) {   // this workgroup's partial row (summed by the weight-gradient kernel)
-    const float v = ((hst[tid][0] + hst[tid][1]) + (hst[tid][2] + hst[tid][3]));
-    a.mpart[(size_t)blockIdx.x * MPART_W + tid] = v * a.inv_B;
-  }
-  if (POL) {   // phase C: d(loss)/d(pre-tanh mean) and the log-std gradient terms
-    if (tid < ROLL_RB * MLP_MAXA) {
-      const int r = tid / MLP_MAXA, j = tid % MLP_MAXA;
-      float lsg = 0.f;
-      if (j < a.A) {
-        const float raw = hls[j];
-        const float ls = fminf(fmaxf(raw, -2.5f), 2.5f);
-        const float ivar = expf(-2.f * ls);
-        const float d = hd[r][j], th = ht[r][j], g = hg[r];
-        dP[r * ldP + j] = g * d * ivar * hsc[j] * (1.f - th * th);
-        const bool inr = raw >= -2.5f && raw <= 2.5f;
-        lsg = inr ? g * (d * d * ivar - 1.f) - hco[1] * a.inv_B : 0.f;
-      }
-      hl[r][j] = lsg;
-    }
-    __syncthreads();
-    if (tid < a.A) {
-      float s = 0.f;
-      for (int r = 0; r < ROLL_RB; ++r) s += hl[r][tid];
-      a.mpart[(size_t)blockIdx.x * MPART_W + 8 + tid] = s;
-    }
-  }
-  __syncthreads();
-  stamp(8);
-  // ---- workspace: the layer inputs and the top gradient (weight-gradient operands)
-  t4_ws_store(X0, KP0 + 4, D, P_<float>(T.xs[0]), row0);
-  t4_ws_store(Y0, N0 + 4, N0, P_<float>(T.xs[1]), row0);
-  if constexpr (POL) {
-    t4_ws_store(Y1, N1 + 4, N1, P_<float>(T.xs[2]), row0);
-    t4_ws_store(Y2, N2 + 4, N2, P_<float>(T.xs[3]), row0);
-    t4_ws_store(dP, ldP, NA, P_<float>(T.dp[3]), row0);
-  } else {
-    t4_ws_store(Y1, N1 + 4, N1, P_<float>(T.xs[2]), row0);
-    t4_ws_store(dP, ldP, NA, P_<float>(T.dp[2]), row0);
-  }
-  // ---- data-gradient chain
-  float* dQ = dPb;
-  if constexpr (POL) {
-    t4_mfma<B3>(b3, dP, ldP, red);
-    __syncthreads();
-    t4_bwd_epi<B3>(red, Y2, N2 + 4, s2, N2, dQ, ldP, N2);
-    __syncthreads();
-    t4_ws_store(dQ, ldP, N2, P_<float>(T.dp[2]), row0);
-    stamp(9);
-    t4_mfma<B2>(b2, dQ, ldP, red);
-    __syncthreads();
-    t4_bwd_epi<B2>(red, Y1, N1 + 4, s1, N1, dP, ldP, N1);
-    __syncthreads();
-    t4_ws_store(dP, ldP, N1, P_<float>(T.dp[1]), row0);
-    stamp(10);
-    t4_mfma<B1>(b1, dP, ldP, red);
-    __syncthreads();
-    t4_bwd_epi<B1>(red, Y0, N0 + 4, s0, N0, dQ, ldP, N0);
-    __syncthreads();
-    t4_ws_store(dQ, ldP, N0, P_<float>(T.dp[0]), row0);
-  } else {
-    t4_mfma<B2>(b2, dP, ldP, red);
-    __syncthreads();
-    t4_bwd_epi<B2>(red, Y1, N1 + 4, s1, N1, dQ, ldP, N1);
-    __syncthreads();
-    t4_ws_store(dQ, ldP, N1, P_<float>(T.dp[1]), row0);
-    stamp(9);
-    t4_mfma<B1>(b1, dQ, ldP, red);
-    __syncthreads();
-    t4_bwd_epi<B1>(red, Y0, N0 + 4, s0, N0, dP, ldP, N0);
-    __syncthreads();
-    t4_ws_store(dP, ldP, N0, P_<float>(T.dp[0]), row0);
-  }
-  stamp(7);
-  if (stamping) {
-    __syncthreads();
-    if (tid < 16) a.stamps[blockIdx.y * 16 + tid] = ts[tid];
-  }
-}
-
-template <int KP0>
-__global__ void __launch_bounds__(MLP_THREADS) __attribute__((amdgpu_waves_per_eu(1, 2))) mlp_train4_kernel(MlpArgs a) {
-  if (blockIdx.y == 0) t4_tower<0, KP0>(a);
-  else t4_tower<1, KP0>(a);
-}
-
 }  // namespace aca
 
 using namespace aca;
@@ -2049,15 +1617,6 @@ using namespace aca;
 extern "C" hipError_t aca_mlp_fwd(const MlpArgs* a, int ntw, size_t lds, int spec, hipStream_t stream) {
   if (a->B <= 0) return hipSuccess;
   if (a->A > MLP_MAXA || a->D > MLP_MAXW || ntw < 1 || a->tw_base + ntw > 2 || !a->tw) return hipErrorInvalidValue;
-  if (spec < 0) {   // 4-row train path (mlp_train4_kernel): reference towers, gaussian head, contiguous rows
-    if (a->mode != 2 || a->tw_base != 0 || ntw != 2 || a->head != 2 || a->idx || a->perm_uc || a->B % ROLL_RB ||
-        a->D > 64 || !a->mpart)
-      return hipErrorInvalidValue;
-    const dim3 grid4(a->B / ROLL_RB, 2);
-    if (a->D <= 32) mlp_train4_kernel<32><<<grid4, MLP_THREADS, 0, stream>>>(*a);
-    else mlp_train4_kernel<64><<<grid4, MLP_THREADS, 0, stream>>>(*a);
-    return hipGetLastError();
-  }
   if (spec && (a->mode != 2 || a->tw_base != 0 || ntw != 2 || mlp_ngp2(a->D) != spec)) return hipErrorInvalidValue;
   static bool attr = false;
   if (!attr) {

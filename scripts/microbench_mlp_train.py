@@ -63,29 +63,6 @@ def main():
         last = max(k for k in (9, 10, 11) if res[t][-1][k] > 0)
         ghz = [(r[13] - r[12]) / ((r[last] - r[2]) * 10.0) for r in res[t][2:] if r[last] > r[2]]
         out[f"tower{t}_shader_clock_ghz"] = round(sorted(ghz)[len(ghz) // 2], 3) if ghz else None
-    # the 4-row path (mlp_train4_kernel) on the same minibatch: its phase stamps and launch time
-    names4 = {1: "issued", 2: "x0", 3: "fwd0", 4: "fwd1", 5: "fwd2", 6: "fwd3", 8: "head", 9: "dg_a", 10: "dg_b",
-              7: "end"}
-    res4 = {0: [], 1: []}
-    mbk = dict(desc_B=mb, act_in=actions[:mb], logp_old=logp_old[:mb], adv=adv[:mb], ret=ret[:mb],
-               v_old=v_old[:mb], ent_coef=tr.ent_coef, kl_coef=tr.kl_coef, ppo=True, ppo_clip=cfg.ppo_clip)
-    if eng.rows4:
-        for rep in range(20):
-            stamps.zero_()
-            eng._fwd(2, obs[:mb], mb, 0, 2, stamps=stamps, rows=4, **mbk)
-            torch.cuda.synchronize()
-            s = stamps.cpu().tolist()
-            for t in (0, 1):
-                res4[t].append(s[t])
-        for t in (0, 1):
-            ph = {}
-            for slot, name in names4.items():
-                vals = [(r[slot] - r[0]) * 0.01 for r in res4[t][2:] if r[slot] > 0]
-                if vals:
-                    ph[name] = round(sorted(vals)[len(vals) // 2], 2)
-            out[f"rows4_tower{t}_us_from_start"] = dict(sorted(ph.items(), key=lambda kv: kv[1]))
-        out["rows4_train_launch_us"] = ev_time(lambda: eng._fwd(2, obs[:mb], mb, 0, 2, rows=4, **mbk))
-        out["rows16_contig_train_launch_us"] = ev_time(lambda: eng._fwd(2, obs[:mb], mb, 0, 2, **mbk))
     out["train_launch_us"] = ev_time(lambda: eng._fwd(2, obs, mb, 0, 2, desc_B=mb, perm=(uc, 0, 0, B, tr.policy_seed),
                                                       act_in=actions, logp_old=logp_old, adv=adv, ret=ret,
                                                       v_old=v_old, ent_coef=tr.ent_coef, kl_coef=tr.kl_coef,

@@ -325,47 +325,6 @@ def test_mlp_spec_train_path_matches_generic(cuda, case):
         torch.testing.assert_close(a.sum(), b.sum(), rtol=1e-5, atol=1e-9)
 
 
-@pytest.mark.parametrize("ob", [17, 40])
-@pytest.mark.parametrize("ppo", [False, True])
-def test_mlp_rows4_train_path_matches_autograd_and_spec(cuda, ob, ppo):
-    """The 4-row train launch (mlp_train4_kernel: contiguous minibatch, gaussian head, reference towers; weights read
-    from the slab on 4x4x1 MFMAs) == autograd of the reference losses, and == the 16-row SPEC path to fp32
-    summation-order noise (gradients, statistics, log-std gradient, per-tower sums of squares)."""
-    m, ref, flat, eng = _model(cuda, ob, 6, False, "basic", seed=11)
-    assert eng.rows4
-    torch.manual_seed(4321)
-    B = 204   # 51 four-row workgroups: the last 16-row tile of the workspace is partial
-    obs = torch.randn(B, ob, device=cuda)
-    with torch.no_grad():
-        pi, v0 = ref(obs)
-        act, lp0, _ = D.gaussian_sample_ref(pi, ref.actor.log_std, torch.arange(B, device=cuda), 13)
-    lo = lp0 + 0.3 * torch.randn(B, device=cuda)
-    adv, ret = torch.randn(B, device=cuda), v0 + torch.randn(B, device=cuda)
-    v_old = v0 + 0.1 * torch.randn(B, device=cuda)
-    beta, ce = torch.tensor(0.7, device=cuda), torch.tensor(0.05, device=cuda)
-    out = []
-    for rows4 in (True, False):
-        eng.rows4 = rows4
-        flat.grad.zero_()
-        stats = torch.zeros(16, device=cuda)
-        eng.train(obs, act, lo, adv, ret, ce, beta, B, v_old=v_old, ppo=ppo, ppo_clip=0.2,
-                  v_clip=0.15 if ppo else 0.0, stats=stats, want_parts=True)
-        torch.cuda.synchronize()
-        out.append((flat.grad.clone(), stats.clone(), [p.clone() for p in eng.parts]))
-    (g4, s4, p4), (g16, s16, p16) = out
-    scale = g16.abs().max()
-    assert (g4 - g16).abs().max() <= 1e-5 * scale, float((g4 - g16).abs().max() / scale)
-    torch.testing.assert_close(s4, s16, rtol=1e-5, atol=1e-7)
-    for a, b in zip(p4, p16):
-        torch.testing.assert_close(a.sum(), b.sum(), rtol=1e-5, atol=1e-9)
-    g_ref, s_ref = _ref_grads(ref, obs, act, lo, adv, ret, v_old, ppo, beta, ce, 0.2, 0.15)
-    flat.grad.copy_(g4)
-    for (n, p) in m.named_parameters():
-        torch.testing.assert_close(p.grad, g_ref[n], rtol=2e-3, atol=2e-5, msg=lambda s: f"{n}: {s}")
-    for nm, k in zip(("pg", "kl", "entropy", "crit_loss", "clipfrac"), range(5)):
-        torch.testing.assert_close(s4[k], s_ref[nm].float().to(cuda), rtol=1e-3, atol=1e-5, msg=nm)
-
-
 @pytest.mark.parametrize("variant", ["basic", "a3c"])
 def test_item_path_optimizer_matches_sweep(cuda, variant):
     """The optimiser's item path (MLP segments: 16 x 64 weight blocks that also write the fragment copies, small

@@ -16,8 +16,6 @@ same kernel writes a bf16 shadow copy of the parameters for the MFMA forward/bac
 """
 from __future__ import annotations
 
-import os
-
 import torch
 
 from .. import _native
@@ -279,10 +277,6 @@ class FusedGroupStep:
         self._words = self._fvals = None
         self._trans = None
         self._items = [None] * len(self.opts)
-        # in-launch global norm for groups without engine-written partials (data parallelism): barrier words
-        # [arrivals, departures, timeout flag]; ``ACA_OPT_FUSED_NORM=0`` keeps the separate sum-of-squares launch
-        self.fused_norm = os.environ.get("ACA_OPT_FUSED_NORM", "1") != "0"
-        self._fbar = torch.zeros(3, dtype=torch.int32, device=o0.p.device)
         if copies is not None:
             for k, o in enumerate(self.opts):
                 if copies[k]:
@@ -346,15 +340,7 @@ class FusedGroupStep:
         afterwards (:meth:`advance`) -- the launch skips the step ticket (one agent-scope atomic chain per launch)."""
         ops = _native.require()
         plain = [o for o in self.opts if o.max_grad_norm is not None and o.ext_parts is None and o.clip_value is None]
-        # every group's norm from this launch's own items (optim.hip OptSeg::fbar): no sum-of-squares launch between
-        # the all-reduce and the update (data-parallel MLP steps; the item workgroups must all be co-resident)
-        fused = (self.fused_norm and len(plain) == len(self.opts) and all(it is not None for it in self._items)
-                 and sum(it.shape[0] for it in self._items) <= 256)
-        if fused:
-            for o in plain:
-                o._norm_mul = o.grad_mul * o.grad_mul
-            parts = [o._partial for o in self.opts]
-        elif len(plain) > 1:
+        if len(plain) > 1:
             # the groups' plain sums of squares (data parallelism: no engine-written partials) in ONE launch
             ops.sumsq_multi([o.g for o in plain], [o._partial for o in plain])
             for o in plain:
@@ -362,7 +348,7 @@ class FusedGroupStep:
             parts = [o._partial if o in plain else o._native_norm(ops) for o in self.opts]
         else:
             parts = [o._native_norm(ops) for o in self.opts]
-        key = tuple((p.data_ptr() if p is not None else 0, o._norm_mul, o.grad_mul, o.g.data_ptr(), fused)
+        key = tuple((p.data_ptr() if p is not None else 0, o._norm_mul, o.grad_mul, o.g.data_ptr())
                     for p, o in zip(parts, self.opts))
         if key != self._key:
             words, fvals = [], []
@@ -375,8 +361,7 @@ class FusedGroupStep:
                               p.data_ptr() if p is not None else 0, o.gnorm.data_ptr(), shadow,
                               o._ticket.data_ptr() if adam else 0,
                               items.data_ptr() if items is not None else 0,
-                              items.shape[0] if items is not None else 0,
-                              self._fbar.data_ptr() if fused else 0])
+                              items.shape[0] if items is not None else 0])
                 fvals.append([float(o.clip_value) if o.clip_value is not None else -1.0,
                               float(o.max_grad_norm) if o.max_grad_norm is not None else -1.0,
                               float(o.grad_mul), float(o._norm_mul)])

@@ -16,7 +16,6 @@ namespace aca {
 
 constexpr int OPT_THREADS = 256;
 constexpr unsigned int OPT_TK_LINE = 32;   // Adam step ticket: 9 counters, one per 128-byte line (ops/optim.py)
-constexpr unsigned int OPT_SPIN_LIMIT = 1u << 21;   // fused-norm barrier: bounded wait, then fbar[2]
 constexpr int SUMSQ_U = 8;
 constexpr int SUMSQ_PARTS = 256;   // max sumsq workgroups = partial slots the optimiser reduces
 
@@ -140,13 +139,6 @@ struct OptSeg {
   // optional bf16 gradient read in place of g (the all-reduced comm buffer of bf16 DP buckets: no cast back to the
   // fp32 slab; zero_grad still clears g). The plain launch only (opt_kernel G16).
   const u16* g16 = nullptr;
-  // optional in-launch global norm (item path, data-parallel MLP step): every workgroup of the launch writes the sum
-  // of squares of its item's gradient to parts[item] (S.parts, then written here, not read from a prior launch),
-  // meets the others at a counting barrier (fbar: [0] arrivals, [1] departures, [2] timeout flag; fbar_n = the
-  // launch's workgroups, all co-resident) and sums its segment's nitems slots in item order -- replaces the separate
-  // sum-of-squares launch between the all-reduce and the update
-  unsigned int* fbar = nullptr;
-  int fbar_n = 0;
   int64_t* stamps = nullptr;   // diagnostics: [global workgroup][8] s_memrealtime phase stamps (aca_opt_set_stamps)
   int wg0 = 0;                 // global index of the segment's first workgroup (stamps row)
 };
@@ -291,53 +283,7 @@ __device__ __forceinline__ void opt_items(const OptSeg& S, float b1, float b2, f
   const float lr = *S.lr;
   const float t = ADAM ? (*S.t + 1.0f + (S.t_off > 0 ? (float)S.t_off : 0.f)) : 0.f;
   float scale = 1.f;
-  if (S.fbar) {
-    float sq = 0.f;
-    if (type == 1) {
-      if (cnt) sq = x4[0][0].x * x4[0][0].x + x4[0][0].y * x4[0][0].y + x4[0][0].z * x4[0][0].z + x4[0][0].w * x4[0][0].w;
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (j < cnt) sq += x4[0][j].x * x4[0][j].x;
-    }
-    sq = block_sum(sq, shr);
-    float* slots = const_cast<float*>(S.parts);
-    if (tid == 0) __hip_atomic_store(&slots[vblk], sq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the slot store is acknowledged before the arrival
-    __syncthreads();
-    if (tid == 0) {
-      __hip_atomic_fetch_add(&S.fbar[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      unsigned int spins = 0;
-      while (__hip_atomic_load(&S.fbar[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned int)S.fbar_n) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++spins > OPT_SPIN_LIMIT) {
-          __hip_atomic_store(&S.fbar[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-      }
-    }
-    __syncthreads();
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    // the segment's slots in item order (every workgroup the same order: one value launch-wide)
-    float v = 0.f;
-    if (tid < 64) {
-      for (int i = tid; i < S.nitems; i += 64) v += __hip_atomic_load(&slots[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      v = wave_sum(v);
-    }
-    if (tid == 0) {
-      shr[0] = v;
-      // departure: the last workgroup past the wait resets the barrier for the next launch (stream-ordered)
-      const unsigned int prev = __hip_atomic_fetch_add(&S.fbar[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (prev == (unsigned int)S.fbar_n - 1u) {
-        __hip_atomic_store(&S.fbar[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&S.fbar[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    __syncthreads();
-    const float gsq = shr[0] * S.norm_mul;
-    scale = grad_scale(gsq, S.max_norm);
-    if (S.gnorm_out && vblk == 0 && tid == 0) *S.gnorm_out = gsq;
-  } else if (S.parts) {
+  if (S.parts) {
     const float gsq = partial_total(S.parts, shr) * S.norm_mul;
     scale = grad_scale(gsq, S.max_norm);
     if (S.gnorm_out && vblk == 0 && tid == 0) *S.gnorm_out = gsq;
@@ -1074,10 +1020,9 @@ extern "C" hipError_t aca_rmsprop_step(float* p, float* g, float* v, size_t n, c
 }
 
 // Multi-group step. words: nseg records of OPT_MULTI_WORDS (see ops/optim.py FusedGroupStep): p, g, m, v, n, lr, t,
-// parts, gnorm_out, shadow, ticket, items, nitems, fbar (pointers / sizes as 64-bit words); fvals: clip, max_norm, gmul,
+// parts, gnorm_out, shadow, ticket, items, nitems (pointers / sizes as 64-bit words); fvals: clip, max_norm, gmul,
 // norm_mul (floats). The item tables (OptSeg::items) are the caller's, validated where they are built.
-constexpr int OPT_MULTI_WORDS = 14;   // + fused-norm barrier words (OptSeg::fbar; 0: none)
-constexpr int OPT_FBAR_MAX = 256;      // fused norm: at most one workgroup per CU (co-residency of the barrier)
+constexpr int OPT_MULTI_WORDS = 13;
 extern "C" hipError_t aca_opt_multi(const int64_t* words, const float* fvals, const int64_t* trans, int nseg,
                                     int adam, float b1, float b2, float eps, int zero_grad, int t_off,
                                     hipStream_t stream) {
@@ -1116,14 +1061,6 @@ extern "C" hipError_t aca_opt_multi(const int64_t* words, const float* fvals, co
     S.nblocks = S.items ? S.nitems : opt_grid(S.n);   // item path: one workgroup per item
     S.wg0 = total;
     total += S.nblocks;
-    S.fbar = reinterpret_cast<unsigned int*>(w[13]);
-    if (S.fbar && (!S.items || !S.parts || S.clip > 0.f || S.nitems > SUMSQ_PARTS || S.fbar != M.seg[0].fbar))
-      return hipErrorInvalidValue;
-    if ((S.fbar != nullptr) != (M.seg[0].fbar != nullptr)) return hipErrorInvalidValue;
-  }
-  if (M.seg[0].fbar) {
-    if (total > OPT_FBAR_MAX) return hipErrorInvalidValue;
-    for (int k = 0; k < nseg; ++k) M.seg[k].fbar_n = total;
   }
   if (adam) opt_multi_kernel<true><<<total, OPT_THREADS, 0, stream>>>(M, b1, b2, eps, zero_grad);
   else opt_multi_kernel<false><<<total, OPT_THREADS, 0, stream>>>(M, 0.f, b2, eps, zero_grad);

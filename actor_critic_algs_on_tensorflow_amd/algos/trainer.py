@@ -603,6 +603,13 @@ class ActorCriticTrainer:
                     self._group_step = FusedGroupStep(opts, copies)
             if self._group_step is not None:
                 t_off = getattr(self, "_t_off", None)
+                if (self.mlp is not None and self.dp is not None and self.cfg.overlap != "lag1"
+                        and self._grad_sink is None):
+                    # strict DP on the MLP engine: the weight-gradient launch stores every element and the all-reduce
+                    # runs in place, so nothing accumulates into the slab -- no zeroing pass, which also lets the
+                    # item path read whole segments for the norm (ops/optim.py FusedGroupStep.full_norm)
+                    for o in opts:
+                        o.zero_grad_after = not getattr(self.mlp, "last_stores_all", False)
                 self._group_step.step(t_off=t_off)
                 if t_off is not None:
                     self._t_offs_used += 1

@@ -606,8 +606,7 @@ class ActorCriticTrainer:
                 if (self.mlp is not None and self.dp is not None and self.cfg.overlap != "lag1"
                         and self._grad_sink is None):
                     # strict DP on the MLP engine: the weight-gradient launch stores every element and the all-reduce
-                    # runs in place, so nothing accumulates into the slab -- no zeroing pass, which also lets the
-                    # item path read whole segments for the norm (ops/optim.py FusedGroupStep.full_norm)
+                    # runs in place, so nothing accumulates into the slab -- no zeroing pass behind the update
                     for o in opts:
                         o.zero_grad_after = not getattr(self.mlp, "last_stores_all", False)
                 self._group_step.step(t_off=t_off)

@@ -277,7 +277,6 @@ class FusedGroupStep:
         self._words = self._fvals = None
         self._trans = None
         self._items = [None] * len(self.opts)
-        self.full_norm = True   # (tests switch it off to compare with the sum-of-squares launch)
         if copies is not None:
             for k, o in enumerate(self.opts):
                 if copies[k]:
@@ -341,23 +340,15 @@ class FusedGroupStep:
         afterwards (:meth:`advance`) -- the launch skips the step ticket (one agent-scope atomic chain per launch)."""
         ops = _native.require()
         plain = [o for o in self.opts if o.max_grad_norm is not None and o.ext_parts is None and o.clip_value is None]
-        # item-path groups without engine-written partials (data parallelism): each workgroup reads its whole segment
-        # for the norm (optim.hip OptSeg::full_norm) -- no sum-of-squares launch between the all-reduce and the update
-        # (not with zeroing behind the update: a workgroup would read gradients another one already cleared)
-        full = [o for k, o in enumerate(self.opts)
-                if o in plain and self._items[k] is not None and self.full_norm and not o.zero_grad_after]
-        for o in full:
-            o._norm_mul = o.grad_mul * o.grad_mul
-        plain = [o for o in plain if o not in full]
         if len(plain) > 1:
             # the groups' plain sums of squares (data parallelism: no engine-written partials) in ONE launch
             ops.sumsq_multi([o.g for o in plain], [o._partial for o in plain])
             for o in plain:
                 o._norm_mul = o.grad_mul * o.grad_mul
-            parts = [o._partial if o in plain else None if o in full else o._native_norm(ops) for o in self.opts]
+            parts = [o._partial if o in plain else o._native_norm(ops) for o in self.opts]
         else:
-            parts = [None if o in full else o._native_norm(ops) for o in self.opts]
-        key = tuple((p.data_ptr() if p is not None else 0, o._norm_mul, o.grad_mul, o.g.data_ptr(), o in full)
+            parts = [o._native_norm(ops) for o in self.opts]
+        key = tuple((p.data_ptr() if p is not None else 0, o._norm_mul, o.grad_mul, o.g.data_ptr())
                     for p, o in zip(parts, self.opts))
         if key != self._key:
             words, fvals = [], []
@@ -370,7 +361,7 @@ class FusedGroupStep:
                               p.data_ptr() if p is not None else 0, o.gnorm.data_ptr(), shadow,
                               o._ticket.data_ptr() if adam else 0,
                               items.data_ptr() if items is not None else 0,
-                              items.shape[0] if items is not None else 0, int(o in full)])
+                              items.shape[0] if items is not None else 0])
                 fvals.append([float(o.clip_value) if o.clip_value is not None else -1.0,
                               float(o.max_grad_norm) if o.max_grad_norm is not None else -1.0,
                               float(o.grad_mul), float(o._norm_mul)])

@@ -1237,7 +1237,7 @@ void mlp_rollout(Tensor desc, int64_t lds, Tensor obs, Tensor act, Tensor logp, 
 void opt_multi(Tensor words, Tensor fvals, c10::optional<Tensor> trans, bool adam, double b1, double b2, double eps,
                bool zero_grad, Tensor stream_ref, int64_t t_off) {
   TORCH_CHECK(!words.is_cuda() && words.scalar_type() == at::kLong && words.is_contiguous() && words.dim() == 2 &&
-                  words.size(1) == 14, "opt_multi: words must be CPU int64 [nseg, 14]");
+                  words.size(1) == 13, "opt_multi: words must be CPU int64 [nseg, 13]");
   TORCH_CHECK(!fvals.is_cuda() && fvals.scalar_type() == at::kFloat && fvals.is_contiguous() &&
                   fvals.numel() == words.size(0) * 4, "opt_multi: fvals must be CPU float [nseg, 4]");
   const int64_t* tp = nullptr;

@@ -139,10 +139,6 @@ struct OptSeg {
   // optional bf16 gradient read in place of g (the all-reduced comm buffer of bf16 DP buckets: no cast back to the
   // fp32 slab; zero_grad still clears g). The plain launch only (opt_kernel G16).
   const u16* g16 = nullptr;
-  // optional norm from the segment itself (item path, data-parallel MLP steps: no engine-written partials): every
-  // workgroup reads the WHOLE segment's gradient and sums its squares in the same fixed order (tens of thousands of
-  // elements, L2-resident after the first reader) -- no sum-of-squares launch between the all-reduce and the update
-  int full_norm = 0;
   int64_t* stamps = nullptr;   // diagnostics: [global workgroup][8] s_memrealtime phase stamps (aca_opt_set_stamps)
   int wg0 = 0;                 // global index of the segment's first workgroup (stamps row)
 };
@@ -287,26 +283,7 @@ __device__ __forceinline__ void opt_items(const OptSeg& S, float b1, float b2, f
   const float lr = *S.lr;
   const float t = ADAM ? (*S.t + 1.0f + (S.t_off > 0 ? (float)S.t_off : 0.f)) : 0.f;
   float scale = 1.f;
-  if (S.full_norm) {
-    // thread t: float4 groups t + OPT_THREADS j, FN_U loads in flight per round, then the scalar tail
-    constexpr int FN_U = 8;
-    const size_t n4 = S.n / 4;
-    float sq = 0.f;
-    for (size_t i0 = tid; i0 < n4; i0 += (size_t)OPT_THREADS * FN_U) {
-      float4 q[FN_U];
-#pragma unroll
-      for (int u = 0; u < FN_U; ++u) {
-        const size_t i = i0 + (size_t)OPT_THREADS * u;
-        q[u] = i < n4 ? reinterpret_cast<const float4*>(g)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-#pragma unroll
-      for (int u = 0; u < FN_U; ++u) sq += q[u].x * q[u].x + q[u].y * q[u].y + q[u].z * q[u].z + q[u].w * q[u].w;
-    }
-    for (size_t i = n4 * 4 + tid; i < S.n; i += OPT_THREADS) sq += g[i] * g[i];
-    const float gsq = block_sum(sq, shr) * S.norm_mul;
-    scale = grad_scale(gsq, S.max_norm);
-    if (S.gnorm_out && vblk == 0 && tid == 0) *S.gnorm_out = gsq;
-  } else if (S.parts) {
+  if (S.parts) {
     const float gsq = partial_total(S.parts, shr) * S.norm_mul;
     scale = grad_scale(gsq, S.max_norm);
     if (S.gnorm_out && vblk == 0 && tid == 0) *S.gnorm_out = gsq;
@@ -1043,9 +1020,9 @@ extern "C" hipError_t aca_rmsprop_step(float* p, float* g, float* v, size_t n, c
 }
 
 // Multi-group step. words: nseg records of OPT_MULTI_WORDS (see ops/optim.py FusedGroupStep): p, g, m, v, n, lr, t,
-// parts, gnorm_out, shadow, ticket, items, nitems, full_norm (pointers / sizes / flags as 64-bit words); fvals: clip, max_norm, gmul,
+// parts, gnorm_out, shadow, ticket, items, nitems (pointers / sizes as 64-bit words); fvals: clip, max_norm, gmul,
 // norm_mul (floats). The item tables (OptSeg::items) are the caller's, validated where they are built.
-constexpr int OPT_MULTI_WORDS = 14;   // + full_norm (OptSeg::full_norm)
+constexpr int OPT_MULTI_WORDS = 13;
 extern "C" hipError_t aca_opt_multi(const int64_t* words, const float* fvals, const int64_t* trans, int nseg,
                                     int adam, float b1, float b2, float eps, int zero_grad, int t_off,
                                     hipStream_t stream) {
@@ -1081,14 +1058,10 @@ extern "C" hipError_t aca_opt_multi(const int64_t* words, const float* fvals, co
     if (adam && (!S.m || !S.t || !S.ticket)) return hipErrorInvalidValue;
     // trans: [nseg][OPT_MAXT][5]
     if (!opt_load_trans(S, trans ? trans + (int64_t)k * OPT_MAXT * 5 : nullptr)) return hipErrorInvalidValue;
-    S.full_norm = (int)w[13];
-    if (S.full_norm && (!S.items || S.clip > 0.f || S.max_norm <= 0.f)) return hipErrorInvalidValue;
     S.nblocks = S.items ? S.nitems : opt_grid(S.n);   // item path: one workgroup per item
     S.wg0 = total;
     total += S.nblocks;
   }
-  for (int k = 0; k < nseg; ++k)   // (a workgroup would read gradients another one already cleared)
-    if (M.seg[k].full_norm && zero_grad) return hipErrorInvalidValue;
   if (adam) opt_multi_kernel<true><<<total, OPT_THREADS, 0, stream>>>(M, b1, b2, eps, zero_grad);
   else opt_multi_kernel<false><<<total, OPT_THREADS, 0, stream>>>(M, 0.f, b2, eps, zero_grad);
   return hipGetLastError();

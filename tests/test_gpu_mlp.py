@@ -337,7 +337,6 @@ def test_item_path_optimizer_matches_sweep(cuda, variant):
         opts = [make_optimizer("adam", flat, g, lr, max_grad_norm=0.5)
                 for g, lr in (("actor", 3e-3), ("critic", 1e-2))]
         gs = FusedGroupStep(opts, eng.frag_copies() if items else None)
-        gs.full_norm = False   # (the same sum-of-squares launch on both paths: bit-identical norms)
         assert (gs._items[0] is not None) == items
         for it in range(3):
             flat.grad.copy_(torch.randn(flat.numel, generator=torch.Generator().manual_seed(20 + it)).to(cuda))
@@ -352,32 +351,3 @@ def test_item_path_optimizer_matches_sweep(cuda, variant):
         assert torch.equal(eng1.F[id(lay)], frag_f(lay.kernel.detach()))
         if id(lay) in eng1.G:
             assert torch.equal(eng1.G[id(lay)], frag_g(lay.kernel.detach()))
-
-
-@pytest.mark.parametrize("max_norm", [0.5, 1e6])
-def test_item_path_segment_norm_matches_sumsq_launch(cuda, max_norm):
-    """Data-parallel MLP step: the item path's norm from the whole segment read by every workgroup (no sum-of-squares
-    launch) == the separate sum-of-squares launch, to fp32 summation-order noise of the norm (clip active at 0.5;
-    inactive at 1e6: bit-identical parameters)."""
-    from actor_critic_algs_on_tensorflow_amd.ops.optim import FusedGroupStep, make_optimizer
-    runs = []
-    for full in (True, False):
-        m, ref, flat, eng = _model(cuda, 17, 6, False, "basic", seed=12)
-        opts = [make_optimizer("adam", flat, g, lr, max_grad_norm=max_norm)
-                for g, lr in (("actor", 3e-3), ("critic", 1e-2))]
-        for o in opts:
-            o.grad_mul = 0.5   # (the 1/world averaging factor of a 2-rank job)
-        gs = FusedGroupStep(opts, eng.frag_copies())
-        gs.full_norm = full
-        for it in range(4):
-            flat.grad.copy_(torch.randn(flat.numel, generator=torch.Generator().manual_seed(40 + it)).to(cuda))
-            gs.step()
-        torch.cuda.synchronize()
-        runs.append((flat.data.clone(), [o.gnorm.clone() for o in opts]))
-    (p1, n1), (p0, n0) = runs
-    for a, b in zip(n1, n0):
-        torch.testing.assert_close(a, b, rtol=1e-6, atol=0)
-    if max_norm > 1e3:
-        assert torch.equal(p1, p0)
-    else:
-        torch.testing.assert_close(p1, p0, rtol=1e-6, atol=1e-7)

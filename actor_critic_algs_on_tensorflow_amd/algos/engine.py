@@ -534,13 +534,18 @@ class CNNEngine:
                       bfc=torch.zeros(P * 512, device=dev), st=torch.zeros(P * 6, dtype=torch.float64, device=dev),
                       ticket=torch.zeros(1, dtype=torch.int32, device=dev))
             self._ph[B] = ph
+        # the statistics records go to the finaliser that reduces this launch's planes (no last-arriver ticket in the
+        # head: it cost every head workgroup an agent-scope release); det_wgrad: the planes always reach a finaliser
+        defer = self.det_wgrad
         ops.ppo_head(b.h, self.sWh, self.bh, actions, logp_old, adv, ret, v_old if v_clip else None, ent_coef,
                      kl_coef, float(vf_coef), float(ppo_clip or 0.0), float(v_clip or 0.0), b.dh, z_out, ph["Wh"],
-                     ph["bh"], ph["bfc"], ph["st"], ph["ticket"], stats, fc[0] if fc else None, fc[1] if fc else 0,
-                     self.bfc if fc else None)
+                     ph["bh"], ph["bfc"], ph["st"], None if defer else ph["ticket"], stats,
+                     fc[0] if fc else None, fc[1] if fc else 0, self.bfc if fc else None)
         for name in ("Wh", "bh", "bfc"):
             self._planes["ph_" + name] = ph[name]
         self._head_planes = {"ph_Wh": ph["P"], "ph_bh": ph["P"], "ph_bfc": ph["P"]}
+        if defer:
+            self._stats_duty = (ph["st"].view(ph["P"], 6), B, ent_coef, kl_coef, stats)
         return stats
 
     # limits of loss.hip head_bwd_kernel: B rows staged in LDS (HB_MAXB), the bootstrap row of N values after them
@@ -785,7 +790,8 @@ class CNNEngine:
         words = self._fin_table(b, planes, parts, bias_rows)
         # the per-env head's statistics go with the finaliser that sums its gradient planes (not whichever finaliser
         # runs first: under DP a tail-stage launch sums the fc weight alone)
-        sums_head = "ae_Wh" in (self._cur_planes if planes is None else planes)
+        cur = self._cur_planes if planes is None else planes
+        sums_head = "ae_Wh" in cur or "ph_Wh" in cur
         sd = self._stats_duty if sums_head else None
         if sd is not None:
             self._stats_duty = None

@@ -121,7 +121,7 @@ hipError_t aca_cnn_trunk_fwd_s16(const uint8_t*, const uint16_t*, const float*, 
                                  const uint16_t*, const float*, uint16_t*, uint16_t*, uint16_t*, int, float, uint8_t*,
                                  const int64_t*, int, hipStream_t);
 hipError_t aca_grad_finalize(const int64_t*, int, float*, const double*, int, int, const float*, const float*, float*,
-                             hipStream_t);
+                             int, hipStream_t);
 hipError_t aca_a2c_head_env(const float*, const int32_t*, const float*, const float*, const float*, float,
                             const float*, float*, const uint8_t*, int, int, int, int, float, float, float*, float*,
                             const uint16_t*, const uint16_t*, uint16_t*, int, const float*, int, int64_t,
@@ -859,7 +859,6 @@ void adam_step(Tensor p, Tensor g, Tensor m, Tensor v, Tensor lr, Tensor t, c10:
   need(v, at::kFloat, "v");
   need(lr, at::kFloat, "lr");
   need(t, at::kFloat, "t");
-  need(ticket, at::kInt, "ticket");
   TORCH_CHECK(ticket.numel() >= 9 * 32, "adam_step: the step ticket needs 9 x 32 words (8 shards + top)");
   TORCH_CHECK(g.numel() == p.numel() && m.numel() == p.numel() && v.numel() == p.numel(), "adam: size mismatch");
   check(aca_adam_step(ptr<float>(p), ptr<float>(g), ptr<float>(m), ptr<float>(v), p.numel(), ptr<float>(lr),
@@ -904,7 +903,7 @@ const T* copt(const c10::optional<Tensor>& t, at::ScalarType dt, const char* nam
 void ppo_head(Tensor h, Tensor Wh, Tensor bh, Tensor act, Tensor logp_old, Tensor adv, Tensor ret,
               c10::optional<Tensor> v_old, Tensor ent_coef, Tensor kl_coef, double vf_coef, double ppo_clip,
               double v_clip, Tensor dh, c10::optional<Tensor> z_out, Tensor pWh, Tensor pbh, Tensor pbfc,
-              Tensor pstats, Tensor ticket, Tensor stats, c10::optional<Tensor> hp, int64_t hp_planes,
+              Tensor pstats, c10::optional<Tensor> ticket, Tensor stats, c10::optional<Tensor> hp, int64_t hp_planes,
               c10::optional<Tensor> hbias) {
   need(h, at::kBFloat16, "h");
   need(Wh, at::kBFloat16, "Wh");
@@ -913,7 +912,6 @@ void ppo_head(Tensor h, Tensor Wh, Tensor bh, Tensor act, Tensor logp_old, Tenso
     need(*x, at::kFloat, "ppo_head f32 operand");
   need(act, at::kInt, "act");
   need(pstats, at::kDouble, "pstats");
-  need(ticket, at::kInt, "ticket");
   const int64_t B = act.numel(), A1 = bh.numel();
   TORCH_CHECK(A1 >= 3 && A1 <= 8, "ppo_head: 2..7 actions + value");
   TORCH_CHECK(h.is_contiguous() && h.numel() == B * 512 && dh.is_contiguous() && dh.numel() == B * 512,
@@ -922,7 +920,7 @@ void ppo_head(Tensor h, Tensor Wh, Tensor bh, Tensor act, Tensor logp_old, Tenso
   TORCH_CHECK(logp_old.numel() >= B && adv.numel() >= B && ret.numel() >= B, "ppo_head: row operands too small");
   const int64_t P = aca_ppo_head_planes((int)B);
   TORCH_CHECK(pWh.numel() >= P * 512 * A1 && pbh.numel() >= P * A1 && pbfc.numel() >= P * 512 &&
-                  pstats.numel() >= P * aca::PH_NSTAT && ticket.numel() >= 1 && stats.numel() >= 7,
+                  pstats.numel() >= P * aca::PH_NSTAT && stats.numel() >= 7,
               "ppo_head: plane / scratch buffers too small");
   aca::PpoHeadArgs a{};
   a.h = ptr<uint16_t>(h);
@@ -946,7 +944,8 @@ void ppo_head(Tensor h, Tensor Wh, Tensor bh, Tensor act, Tensor logp_old, Tenso
   a.pbh = ptr<float>(pbh);
   a.pbfc = ptr<float>(pbfc);
   a.pstats = ptr<double>(pstats);
-  a.ticket = reinterpret_cast<unsigned int*>(ptr<int32_t>(ticket));
+  // (no ticket: the statistics records are summed by the gradient finaliser's duty, grad_finalize)
+  a.ticket = reinterpret_cast<unsigned int*>(const_cast<int32_t*>(copt<int32_t>(ticket, at::kInt, "ticket")));
   a.stats = ptr<float>(stats);
   a.B = (int)B;
   if (hp.has_value() && hp->defined()) {
@@ -1691,20 +1690,22 @@ void grad_finalize(Tensor jobs, Tensor partial, c10::optional<Tensor> spart, int
   TORCH_CHECK(partial.numel() >= aca_sumsq_parts() && jobs.size(0) <= aca_sumsq_parts(),
               "grad_finalize: partial too small / too many jobs");
   const double* sp = nullptr;
-  int sN = 0;
+  int sN = 0, sppo = 0;
   if (spart.has_value() && spart->defined()) {
     need(*spart, at::kDouble, "spart");
-    TORCH_CHECK(spart->dim() == 2 && spart->size(1) == 10 && B >= 1 && ent_coef.has_value() && kl_coef.has_value() &&
-                    stats.has_value() && stats->numel() >= 8,
-                "grad_finalize: statistics duty needs spart [N, 10], B, ent_coef, kl_coef and stats[8]");
+    TORCH_CHECK(spart->dim() == 2 && (spart->size(1) == 10 || spart->size(1) == aca::PH_NSTAT) && B >= 1 &&
+                    ent_coef.has_value() && kl_coef.has_value() && stats.has_value() && stats->numel() >= 8,
+                "grad_finalize: statistics duty needs spart [N, 10] (a2c_head_env) or [N, 6] (ppo_head), B, "
+                "ent_coef, kl_coef and stats[8]");
     need(*ent_coef, at::kFloat, "ent_coef");
     need(*kl_coef, at::kFloat, "kl_coef");
     need(*stats, at::kFloat, "stats");
     sp = spart->data_ptr<double>();
     sN = (int)spart->size(0);
+    sppo = spart->size(1) == aca::PH_NSTAT ? 1 : 0;
   }
   check(aca_grad_finalize(jobs.data_ptr<int64_t>(), (int)jobs.size(0), ptr<float>(partial), sp, sN, (int)B,
-                          optr<float>(ent_coef), optr<float>(kl_coef), optr<float>(stats), cur_stream(partial)),
+                          optr<float>(ent_coef), optr<float>(kl_coef), optr<float>(stats), sppo, cur_stream(partial)),
         "grad_finalize");
 }
 
@@ -2073,7 +2074,7 @@ TORCH_LIBRARY(acamd, m) {
         "Tensor pbfc, Tensor pbh, Tensor spart, Tensor? stamps=None) -> ()");
   m.def("ppo_head(Tensor h, Tensor Wh, Tensor bh, Tensor act, Tensor logp_old, Tensor adv, Tensor ret, Tensor? v_old, "
         "Tensor ent_coef, Tensor kl_coef, float vf_coef, float ppo_clip, float v_clip, Tensor dh, Tensor? z_out, "
-        "Tensor pWh, Tensor pbh, Tensor pbfc, Tensor pstats, Tensor ticket, Tensor stats, Tensor? hp=None, "
+        "Tensor pWh, Tensor pbh, Tensor pbfc, Tensor pstats, Tensor? ticket, Tensor stats, Tensor? hp=None, "
         "int hp_planes=0, Tensor? hbias=None) -> ()");
   m.def("ppo_head_planes(int B) -> int", &ppo_head_planes);
   m.def("opt_set_unroll(int u) -> int", &opt_set_unroll);

@@ -807,7 +807,43 @@ struct StatsDuty {
   const double* part; int N, B;
   const float* ent_coef; const float* kl_coef;
   float* stats;
+  int ppo;   // 1: the PPO head's records (ppo_head.hip, PH_NSTAT doubles per workgroup), else a2c_head_env's rows
 };
+
+// The large-batch PPO head's per-workgroup statistics records [N][PH_NSTAT] (pg, kl, entropy, value loss, clip
+// fraction, ratio sums) -> stats[0..6], the head kernel's own formulas; taken here instead of by the head's
+// last-arriving workgroup (whose ticket cost every head workgroup an agent-scope release). 32 lanes per statistic
+// stride over the records, then lane order (fixed: deterministic).
+constexpr int PPO_NSTAT = 6;
+__device__ __forceinline__ void ppo_stats_duty(const StatsDuty& d) {
+  __shared__ double part[PPO_NSTAT * 32];
+  __shared__ double tot[PPO_NSTAT];
+  const int tid = threadIdx.x, q = tid >> 5, l = tid & 31;
+  if (q < PPO_NSTAT) {
+    double v = 0.0;
+    for (int e = l; e < d.N; e += 32) v += d.part[(int64_t)e * PPO_NSTAT + q];
+    part[q * 32 + l] = v;
+  }
+  __syncthreads();
+  if (tid < PPO_NSTAT) {
+    double v = 0.0;
+    for (int j = 0; j < 32; ++j) v += part[tid * 32 + j];
+    tot[tid] = v;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const double inv = 1.0 / d.B;
+    const float beta = *d.kl_coef, c_ent = *d.ent_coef;
+    const double pg = tot[0] * inv, kl = tot[1] * inv, H = tot[2] * inv;
+    d.stats[0] = (float)pg;
+    d.stats[1] = (float)kl;
+    d.stats[2] = (float)H;
+    d.stats[3] = (float)(tot[3] * inv);
+    d.stats[4] = (float)(tot[4] * inv);
+    d.stats[5] = (float)(pg + beta * kl - c_ent * H);
+    d.stats[6] = (float)(tot[5] * inv);
+  }
+}
 
 __device__ __forceinline__ void a2c_stats_duty(const StatsDuty& d) {
   __shared__ double tot[A2C_STATS];
@@ -839,7 +875,8 @@ __global__ void __launch_bounds__(OPT_THREADS) grad_finalize_kernel(const int64_
   __shared__ float sh[16];
   __shared__ __attribute__((aligned(16))) float red[16 * 64];
   if ((int)blockIdx.x == njobs) {   // past the jobs: the statistics duty (its partial slot is zeroed by workgroup 0)
-    a2c_stats_duty(sd);
+    if (sd.ppo) ppo_stats_duty(sd);
+    else a2c_stats_duty(sd);
     return;
   }
   float s = fin_job<false>(jobs + (int64_t)blockIdx.x * FIN_WORDS, nullptr, red);
@@ -942,11 +979,11 @@ extern "C" hipError_t aca_sumsq_multi(const float* const* xs, const size_t* ns, 
 
 // jobs: device int64 [njobs, FIN_WORDS] (built by the host, ops/optim.py finalize_jobs); partial: SUMSQ_PARTS floats
 extern "C" hipError_t aca_grad_finalize(const int64_t* jobs, int njobs, float* partial, const double* spart, int sN,
-                                        int sB, const float* ent_coef, const float* kl_coef, float* stats,
+                                        int sB, const float* ent_coef, const float* kl_coef, float* stats, int sppo,
                                         hipStream_t stream) {
   if (njobs < 1 || njobs > SUMSQ_PARTS) return hipErrorInvalidValue;
   if (spart && (sN < 1 || sB < 1 || !ent_coef || !kl_coef || !stats)) return hipErrorInvalidValue;
-  const StatsDuty sd{spart, sN, sB, ent_coef, kl_coef, stats};
+  const StatsDuty sd{spart, sN, sB, ent_coef, kl_coef, stats, sppo};
   grad_finalize_kernel<<<njobs + (spart ? 1 : 0), OPT_THREADS, 0, stream>>>(jobs, njobs, partial, sd);
   return hipGetLastError();
 }

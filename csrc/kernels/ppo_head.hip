@@ -27,8 +27,11 @@ namespace aca {
 template <int A1>
 __global__ void __launch_bounds__(PH_THREADS) ppo_head_kernel(PpoHeadArgs p) {
   constexpr int A = A1 - 1;
-  __shared__ float s_red[PH_THREADS / 64][PH_H * A1];   // per-wave dWh partials (wave-ordered combine)
-  __shared__ float s_rb[PH_THREADS / 64][PH_H];          // per-wave dbfc partials
+  // per-wave dWh / dbfc partials (wave-ordered combine); lane l's 8 x A1 (8) values at l * (8 A1 + 1) (l * 9): an odd
+  // lane stride keeps the 64 lanes' stores on distinct banks (stride 8 A1 / 8 was an 8-way conflict per store)
+  constexpr int RS = 8 * A1 + 1, BS = 9;
+  __shared__ float s_red[PH_THREADS / 64][64 * RS];
+  __shared__ float s_rb[PH_THREADS / 64][64 * BS];
   __shared__ double s_st[PH_THREADS / 64][PH_NSTAT + A1];
   __shared__ double s_sum[16 * PH_NSTAT];                 // last workgroup: statistics reduction
   __shared__ int sh_flag;
@@ -221,9 +224,9 @@ __global__ void __launch_bounds__(PH_THREADS) ppo_head_kernel(PpoHeadArgs p) {
   // ---- per-workgroup planes: waves combined in wave order through LDS
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    s_rb[wid][k0 + e] = accB[e];
+    s_rb[wid][lane * BS + e] = accB[e];
 #pragma unroll
-    for (int a = 0; a < A1; ++a) s_red[wid][(k0 + e) * A1 + a] = accW[e][a];
+    for (int a = 0; a < A1; ++a) s_red[wid][lane * RS + e * A1 + a] = accW[e][a];
   }
   if (lane == 0) {
 #pragma unroll
@@ -233,16 +236,23 @@ __global__ void __launch_bounds__(PH_THREADS) ppo_head_kernel(PpoHeadArgs p) {
   }
   __syncthreads();
   float* pw = p.pWh + (size_t)wg * PH_H * A1;
-  for (int j = tid; j < PH_H * A1; j += PH_THREADS)
-    pw[j] = ((s_red[0][j] + s_red[1][j]) + s_red[2][j]) + s_red[3][j];
-  for (int j = tid; j < PH_H; j += PH_THREADS)
-    p.pbfc[(size_t)wg * PH_H + j] = ((s_rb[0][j] + s_rb[1][j]) + s_rb[2][j]) + s_rb[3][j];
+  // element j = k A1 + a (k = 8 l + e) sits at l RS + e A1 + a = j + l
+  for (int j = tid; j < PH_H * A1; j += PH_THREADS) {
+    const int o = j + j / (8 * A1);
+    pw[j] = ((s_red[0][o] + s_red[1][o]) + s_red[2][o]) + s_red[3][o];
+  }
+  for (int j = tid; j < PH_H; j += PH_THREADS) {
+    const int o = j + (j >> 3);
+    p.pbfc[(size_t)wg * PH_H + j] = ((s_rb[0][o] + s_rb[1][o]) + s_rb[2][o]) + s_rb[3][o];
+  }
   if (tid < A1)
     p.pbh[(size_t)wg * A1 + tid] = (float)(((s_st[0][PH_NSTAT + tid] + s_st[1][PH_NSTAT + tid]) +
                                             s_st[2][PH_NSTAT + tid]) + s_st[3][PH_NSTAT + tid]);
   if (tid < PH_NSTAT)
     p.pstats[(size_t)wg * PH_NSTAT + tid] = ((s_st[0][tid] + s_st[1][tid]) + s_st[2][tid]) + s_st[3][tid];
-  // ---- statistics: the last workgroup sums the records (fixed order)
+  // ---- statistics: the last workgroup sums the records (fixed order); no ticket: the gradient finaliser that
+  // reduces this launch's planes sums them (optim.hip ppo_stats_duty)
+  if (!p.ticket) return;
   if (!last_block_arrival(p.ticket, gridDim.x, &sh_flag)) return;
   {
     double t[PH_NSTAT];

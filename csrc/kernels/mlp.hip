@@ -728,6 +728,10 @@ __device__ __forceinline__ void mlp_tower(const MlpArgs& a, const int t, float* 
       for (int g = 0; g < NG0; ++g)
         *reinterpret_cast<floatx4*>(X0 + r * ld0 + 16 * g + 4 * q) = floatx4{xa[g][0], xa[g][1], xa[g][2], xa[g][3]};
     }
+    if (TW == 0 && a.head == 2) {   // the fused Gaussian head's top-gradient tile, zeroed off the head's chain
+      float* dz = sm + YO(nl - 1) + MLP_BM * LDY(nl - 1);
+      for (int e = tid; e < MLP_BM * (MLP_MAXW + 4); e += MLP_THREADS) dz[e] = 0.f;
+    }
     auto stage_head_inputs = [&]() {   // wave 0, before the last forward barrier (the loads landed long before)
       if (wave != 0) return;
 #pragma unroll
@@ -798,10 +802,97 @@ __device__ __forceinline__ void mlp_tower(const MlpArgs& a, const int t, float* 
   float* dPtop = sm + YO(L) + MLP_BM * LDY(L);   // P0
   float* P1 = dPtop + MLP_BM * (MLP_MAXW + 4);
   const int ldP = MLP_MAXW + 4;
-  if (a.mode == 2) {   // zero the top dP tile (the head writes only valid columns)
+  // SPEC actor with the Gaussian head: the whole loss head in ONE barrier-free phase (fused_gauss_head below)
+  const bool fgh = SP && TW == 0 && a.head == 2;
+  if (a.mode == 2 && !fgh) {   // zero the top dP tile (the head writes only valid columns)
     for (int e = tid; e < MLP_BM * ldP; e += MLP_THREADS) dPtop[e] = 0.f;
     __syncthreads();
   }
+  if (fgh) {
+    // Thread (r, j) = (tid >> 4, tid & 15) of waves 0-3: component j of row r -- mean, log-prob term, then the row's
+    // log-prob and entropy as 16-lane xor trees (every lane of the row group gets the same bits), the PPO / A2C
+    // surrogate and KL-proxy gradient redundantly per lane, d(loss)/d(pre-tanh mean) and the log-std term straight
+    // from registers; the 4 rows of a wave meet through xor 16 / 32, the 4 waves through S.red in wave order.
+    // (The generic head runs phase A, a 16-thread row section and phase C with a barrier between each.)
+    if (tid < MLP_BM * MLP_MAXA) {
+      const int r = tid >> 4, j = tid & 15;
+      const bool comp = j < a.A, live = r < rows;
+      float hl = 0.f, hc = 0.f, d = 0.f, th = 0.f, ivar = 0.f, lsc = 0.f, sc = 0.f, raw = 0.f;
+      if (comp) {
+        raw = S.hls[j];
+        lsc = fminf(fmaxf(raw, -2.5f), 2.5f);
+        sc = S.hsc[j];
+        th = tanhf(Yo[r * ldo + j]);
+        const float mu = th * sc;
+        const float aj = live ? e_act : mu;
+        const float zz = (aj - mu) * expf(-lsc);
+        hl = -0.5f * zz * zz - lsc - HALF_LOG_2PI;
+        hc = 0.5f + HALF_LOG_2PI + lsc;
+        d = aj - mu;
+        ivar = expf(-2.f * lsc);
+      }
+      float lp = hl, H = hc;
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) {
+        lp += lane_xor(lp, o);
+        H += lane_xor(H, o);
+      }
+      const float lo = S.er[0][r], adv = S.er[1][r];
+      const float beta = S.hco[0];
+      float st[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      float dsurr;
+      if (a.ppo) {
+        const float ratio = expf(lp - lo);
+        const float s1 = ratio * adv;
+        const float rc = fminf(fmaxf(ratio, 1.f - a.ppo_clip), 1.f + a.ppo_clip);
+        const float s2 = rc * adv;
+        dsurr = (s1 <= s2) ? ratio * adv : 0.f;
+        st[0] = -fminf(s1, s2);
+        st[4] = fabsf(ratio - 1.f) > a.ppo_clip ? 1.f : 0.f;
+        st[6] = ratio;
+      } else {
+        dsurr = adv;
+        st[0] = -adv * lp;
+        st[6] = 1.f;
+      }
+      st[1] = (lo - lp) * (lo - lp);
+      st[2] = H;
+      const float g = live ? a.inv_B * (-dsurr - 2.f * beta * (lo - lp)) : 0.f;
+      if (comp) dPtop[r * ldP + j] = live ? g * d * ivar * sc * (1.f - th * th) : 0.f;
+      const bool inr = raw >= -2.5f && raw <= 2.5f;
+      float lsg = (comp && live && inr) ? g * (d * d * ivar - 1.f) - S.hco[1] * a.inv_B : 0.f;
+      // the wave's 4 rows (lanes j, j + 16, j + 32, j + 48)
+      lsg += lane_xor(lsg, 16);
+      lsg += lane_xor(lsg, 32);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float v = live ? st[k] : 0.f;
+        v += lane_xor(v, 16);
+        v += lane_xor(v, 32);
+        st[k] = v;
+      }
+      if (lane < MLP_MAXA) S.red[wave][lane] = lsg;
+      if (lane == 0)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) S.red[wave][MLP_MAXA + k] = st[k];
+    }
+    __syncthreads();
+    stamp(8);
+    if (tid < MLP_MAXA + 8) {   // partial row of this workgroup: 4 waves in order (summed by the weight-gradient kernel)
+      const float v = ((S.red[0][tid] + S.red[1][tid]) + S.red[2][tid]) + S.red[3][tid];
+      const int k = tid - MLP_MAXA;
+      if (tid < MLP_MAXA) {
+        if (tid < a.A) {
+          if (a.mpart) a.mpart[(size_t)blockIdx.x * MPART_W + 8 + tid] = v;
+          else atomicAdd(&a.g_log_std[tid], v);
+        }
+      } else if (k != 3) {
+        if (a.mpart) a.mpart[(size_t)blockIdx.x * MPART_W + k] = v * a.inv_B;
+        else if (k != 5 && v != 0.f) atomicAdd(&a.mstats[k], v * a.inv_B);
+      }
+    }
+    stamp(14);
+  } else {
   // Gaussian policy head, phase A: one thread per (row, action component) -- mean, sample (rollout) or given action,
   // the component's log-prob term (a per-row loop of tanh / hash / log / sqrt / cos / exp chains on 16 lanes would
   // idle 7 of 8 waves; the per-row sums below keep the sequential order, so the results do not change)
@@ -992,6 +1083,7 @@ __device__ __forceinline__ void mlp_tower(const MlpArgs& a, const int t, float* 
     else atomicAdd(&a.g_log_std[tid], s);
   }
   stamp(14);   // head phase C + log-std sums (the data-gradient layers take slots 9 ..)
+  }   // !fgh
   // ---- top layer dP: apply the head activation derivative (tanh applied above) and publish
   if constexpr (SP) {   // (no store loop ahead of the data-gradient MFMAs, see above; N <= 16: one block)
     // the layer inputs for the weight gradients, issued after the head (whose branch joins would otherwise wait for

@@ -728,7 +728,7 @@ __device__ __forceinline__ void mlp_tower(const MlpArgs& a, const int t, float* 
       for (int g = 0; g < NG0; ++g)
         *reinterpret_cast<floatx4*>(X0 + r * ld0 + 16 * g + 4 * q) = floatx4{xa[g][0], xa[g][1], xa[g][2], xa[g][3]};
     }
-    if (TW == 0 && a.head == 2) {   // the fused Gaussian head's top-gradient tile, zeroed off the head's chain
+    if (TW == 1 || a.head == 2) {   // the loss head's top-gradient tile (value / fused Gaussian head), zeroed off the head's chain
       float* dz = sm + YO(nl - 1) + MLP_BM * LDY(nl - 1);
       for (int e = tid; e < MLP_BM * (MLP_MAXW + 4); e += MLP_THREADS) dz[e] = 0.f;
     }
@@ -804,7 +804,7 @@ __device__ __forceinline__ void mlp_tower(const MlpArgs& a, const int t, float* 
   const int ldP = MLP_MAXW + 4;
   // SPEC actor with the Gaussian head: the whole loss head in ONE barrier-free phase (fused_gauss_head below)
   const bool fgh = SP && TW == 0 && a.head == 2;
-  if (a.mode == 2 && !fgh) {   // zero the top dP tile (the head writes only valid columns)
+  if (a.mode == 2 && !(SP && (TW == 1 || fgh))) {   // zero the top dP tile (the head writes only valid columns)
     for (int e = tid; e < MLP_BM * ldP; e += MLP_THREADS) dPtop[e] = 0.f;
     __syncthreads();
   }

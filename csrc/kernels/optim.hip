@@ -846,11 +846,29 @@ __device__ __forceinline__ void ppo_stats_duty(const StatsDuty& d) {
 }
 
 __device__ __forceinline__ void a2c_stats_duty(const StatsDuty& d) {
+  // 9 statistics x 16 lanes (thread 16 q + l: records l, l + 16, ...; all of a lane's loads in flight together), then
+  // the 16 lane partials in lane order (fixed: deterministic)
+  __shared__ double part[9 * 16];
   __shared__ double tot[A2C_STATS];
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, q = tid >> 4, l = tid & 15;
+  if (q < 9) {
+    double v = 0.0;
+    int e = l;
+    for (; e + 48 < d.N; e += 64) {
+      const double a0 = d.part[(int64_t)e * A2C_STATS + q], a1 = d.part[(int64_t)(e + 16) * A2C_STATS + q];
+      const double a2 = d.part[(int64_t)(e + 32) * A2C_STATS + q], a3 = d.part[(int64_t)(e + 48) * A2C_STATS + q];
+      v += a0;
+      v += a1;
+      v += a2;
+      v += a3;
+    }
+    for (; e < d.N; e += 16) v += d.part[(int64_t)e * A2C_STATS + q];
+    part[q * 16 + l] = v;
+  }
+  __syncthreads();
   if (tid < 9) {
     double v = 0.0;
-    for (int e = 0; e < d.N; ++e) v += d.part[(int64_t)e * A2C_STATS + tid];
+    for (int j = 0; j < 16; ++j) v += part[tid * 16 + j];
     tot[tid] = v;
   }
   __syncthreads();

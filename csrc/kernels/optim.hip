@@ -821,7 +821,16 @@ __device__ __forceinline__ void ppo_stats_duty(const StatsDuty& d) {
   const int tid = threadIdx.x, q = tid >> 5, l = tid & 31;
   if (q < PPO_NSTAT) {
     double v = 0.0;
-    for (int e = l; e < d.N; e += 32) v += d.part[(int64_t)e * PPO_NSTAT + q];
+    int e = l;
+    for (; e + 96 < d.N; e += 128) {   // 4 loads in flight per lane
+      const double a0 = d.part[(int64_t)e * PPO_NSTAT + q], a1 = d.part[(int64_t)(e + 32) * PPO_NSTAT + q];
+      const double a2 = d.part[(int64_t)(e + 64) * PPO_NSTAT + q], a3 = d.part[(int64_t)(e + 96) * PPO_NSTAT + q];
+      v += a0;
+      v += a1;
+      v += a2;
+      v += a3;
+    }
+    for (; e < d.N; e += 32) v += d.part[(int64_t)e * PPO_NSTAT + q];
     part[q * 32 + l] = v;
   }
   __syncthreads();

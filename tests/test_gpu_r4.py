@@ -86,6 +86,20 @@ def test_ppo_head_matches_fp32_autograd(cuda, B, A1, clip, v_clip):
         r = ref[k].reshape(-1)
         assert ((v.cpu().double() - r).norm() / r.norm()).item() < 1e-5, k
     torch.testing.assert_close(out["stats"][:7].cpu().double(), ref["stats"], rtol=1e-5, atol=1e-6)
+    # without the ticket (the engine's default): the statistics records are left for the gradient finaliser's duty,
+    # which reduces them along with the head's planes -- the same statistics
+    from actor_critic_algs_on_tensorflow_amd.ops.optim import finalize_jobs
+    st2 = torch.zeros(8, device=cuda)
+    ops.ppo_head(h, Wh, bh, act, lpo, adv, ret, v_old if v_clip else None, ent, kl, 0.5, clip, v_clip,
+                 out["dh"], out["z"], out["pWh"], out["pbh"], out["pbfc"], out["st"], None, st2)
+    dbh = torch.zeros(A1, device=cuda)
+    jobs = finalize_jobs([(dbh.data_ptr(), out["pbh"].data_ptr(), A1, A1, P)], cuda)
+    parts = torch.zeros(256, device=cuda)
+    ops.grad_finalize(jobs, parts, out["st"].view(P, 6), B, ent, kl, st2)
+    torch.cuda.synchronize()
+    assert torch.equal(st2[7], torch.zeros((), device=cuda))
+    torch.testing.assert_close(st2[:7], out["stats"][:7], rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(dbh.cpu().double(), ref["dbh"], rtol=1e-4, atol=1e-6)
 
 
 def test_ppo_update_through_ppo_head_tracks_generic_head(cuda, monkeypatch):

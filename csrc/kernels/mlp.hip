@@ -222,6 +222,13 @@ __device__ __forceinline__ void wset_load(WSet<NG, NT>& R, int64_t frag, int64_t
   }
 }
 
+// one (tile slot s, k-group g) fragment of a WSet (wset_load's addressing, no bias)
+template <int NG, int NT>
+__device__ __forceinline__ void wset_load_one(WSet<NG, NT>& R, int64_t frag, int s, int g, int wave, int lane) {
+  const int tile = min(wave + MLP_WAVES * s, NT - 1);
+  R.w[s][g] = *((gcfx4*)(P_<const float>(frag) + ((size_t)tile * NG * 64 + lane) * 4) + 64 * g);
+}
+
 // forward layer from registers: the A fragment of a k-group (X rows) is shared by the wave's tiles
 template <int NG, int NT>
 __device__ __forceinline__ void wset_fwd(const WSet<NG, NT>& R, const float* __restrict__ X, int ldx, int N,
@@ -255,6 +262,33 @@ __device__ __forceinline__ void wset_fwd(const WSet<NG, NT>& R, const float* __r
       for (int i = 0; i < 4; ++i) Y[(4 * q + i) * ldy + c] = cok ? act_fwd(acc[s][i] + R.b[s], slope) : 0.f;
     }
   }
+}
+
+// wset_fwd (one tile per wave) that also issues one fragment load of a LATER layer after each k-group's MFMAs:
+// side(g). The later layer's weight stream then goes out under this layer's MFMAs instead of ahead of the first
+// layer (in-order issue: a wave cannot reach its first MFMA before every load ahead of it has been issued, and the
+// CU's address path takes a 1 KB wave load per ~16 clocks).
+template <int NG, int NT, class Side>
+__device__ __forceinline__ void wset_fwd_side(const WSet<NG, NT>& R, const float* __restrict__ X, int ldx, int N,
+                                              float slope, float* __restrict__ Y, int ldy, int wave, int lane,
+                                              Side side) {
+  static_assert(WSet<NG, NT>::NS == 1 && NT == MLP_WAVES, "one tile per wave");
+  const int r = lane & 15, q = lane >> 4;
+  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+  const float* Xr = X + r * ldx + 4 * q;
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    const float4 a4 = *reinterpret_cast<const float4*>(&Xr[16 * g]);
+    acc = mfma4(a4.x, R.w[0][g][0], acc);
+    acc = mfma4(a4.y, R.w[0][g][1], acc);
+    acc = mfma4(a4.z, R.w[0][g][2], acc);
+    acc = mfma4(a4.w, R.w[0][g][3], acc);
+    side(g);
+  }
+  const int c = wave * 16 + r;
+  const bool cok = c < N;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) Y[(4 * q + i) * ldy + c] = cok ? act_fwd(acc[i] + R.b[0], slope) : 0.f;
 }
 
 // wset_fwd with the A operands (rows of the layer input) already in registers: xa[g] = the lane's four k values of
@@ -477,8 +511,7 @@ __device__ __forceinline__ void spec_load(ActorRegs<NG0>& R, const MlpTower& T, 
   __builtin_amdgcn_sched_barrier(0);
   wset_load<4, 8, false>(R.g2, T.G[2], 0, 0, wave, lane);
   __builtin_amdgcn_sched_barrier(0);
-  wset_load<8, 8, false>(R.g1, T.G[1], 0, 0, wave, lane);
-  __builtin_amdgcn_sched_barrier(0);
+  // (g1, W1's data-gradient set: issued under layer 1's MFMAs, wset_fwd_side)
 }
 template <int NG0>
 __device__ __forceinline__ void spec_load(CriticRegs<NG0>& R, const MlpTower& T, int wave, int lane, int tid) {
@@ -491,8 +524,7 @@ __device__ __forceinline__ void spec_load(CriticRegs<NG0>& R, const MlpTower& T,
   __builtin_amdgcn_sched_barrier(0);
   wset_load<1, 8, false>(R.g2, T.G[2], 0, 0, wave, lane);
   __builtin_amdgcn_sched_barrier(0);
-  wset_load<8, 16, false>(R.g1, T.G[1], 0, 0, wave, lane);
-  __builtin_amdgcn_sched_barrier(0);
+  // (g1, W1's data-gradient set: issued under layer 1's MFMAs, wset_fwd_side)
 }
 
 // one tower of mlp_fwd_kernel. SPEC 0: any tower (t at run time, layer loops over the device descriptor); SPEC > 0:
@@ -754,8 +786,11 @@ __device__ __forceinline__ void mlp_tower(const MlpArgs& a, const int t, float* 
       head_params_store(lane, hok ? hp : 0.f);
     };
     next(0);
+    const int64_t G1 = a.htw[TW == 0 ? 0 : 1].G[1];
     if constexpr (TW == 0) {
-      wset_fwd(R.f1, sm + YO(0), LDY(0), OUTW(1), act_slope(ACT(1)), sm + YO(1), LDY(1), wave, lane);
+      // W1 [128][128]: g1 = WSet<8, 8> (one slot, 8 groups), one load per k-group of layer 1 (8 groups)
+      wset_fwd_side(R.f1, sm + YO(0), LDY(0), OUTW(1), act_slope(ACT(1)), sm + YO(1), LDY(1), wave, lane,
+                    [&](int g) { wset_load_one(R.g1, G1, 0, g, wave, lane); });
       next(1);
       wset_fwd(R.f2, sm + YO(1), LDY(1), OUTW(2), act_slope(ACT(2)), sm + YO(2), LDY(2), wave, lane);
       next(2);
@@ -763,7 +798,9 @@ __device__ __forceinline__ void mlp_tower(const MlpArgs& a, const int t, float* 
       stage_head_inputs();
       next(3);
     } else {
-      wset_fwd(R.f1, sm + YO(0), LDY(0), OUTW(1), act_slope(ACT(1)), sm + YO(1), LDY(1), wave, lane);
+      // W1 [256][128]: g1 = WSet<8, 16> (two slots x 8 groups), one load per k-group of layer 1 (16 groups)
+      wset_fwd_side(R.f1, sm + YO(0), LDY(0), OUTW(1), act_slope(ACT(1)), sm + YO(1), LDY(1), wave, lane,
+                    [&](int g) { wset_load_one(R.g1, G1, g >> 3, g & 7, wave, lane); });
       next(1);
       whead_fwd(R.f2, sm + YO(1), LDY(1), OUTW(2), act_slope(ACT(2)), sm + YO(2), LDY(2), P1, wave, lane, tid);
       stage_head_inputs();

@@ -935,9 +935,24 @@ __global__ void __launch_bounds__(OPT_THREADS) grad_move_kernel(float* __restric
     }
 }
 
-__global__ void cast_bf16_kernel(const float* __restrict__ x, u16* __restrict__ y, size_t n) {
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-    y[i] = f2bf(x[i]);
+// fp32 -> bf16 (the comm buffer of bf16 DP buckets): one thread per 4 elements (a 16-byte load, an 8-byte store) when
+// both ends are aligned, else one per element -- a single memory round trip per thread (a grid-stride loop of
+// 4-byte loads was one dependent round trip per element)
+__global__ void cast_bf16_kernel(const float* __restrict__ x, u16* __restrict__ y, size_t n, int vec) {
+  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (vec) {
+    const size_t n4 = n / 4;
+    if (t < n4) {
+      const float4 v = reinterpret_cast<const float4*>(x)[t];
+      uint2 o;
+      o.x = (uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16);
+      o.y = (uint32_t)f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16);
+      reinterpret_cast<uint2*>(y)[t] = o;
+    }
+    if (t < n - n4 * 4) y[n4 * 4 + t] = f2bf(x[n4 * 4 + t]);
+  } else if (t < n) {
+    y[t] = f2bf(x[t]);
+  }
 }
 
 static int opt_grid(size_t n, int unroll = 1) {   // `unroll` float4 groups per thread (up to 16M parameters per pass)
@@ -1147,6 +1162,8 @@ extern "C" hipError_t aca_grad_move(float* src, float* dst, size_t n, int* gate,
 
 extern "C" hipError_t aca_cast_bf16(const float* x, uint16_t* y, size_t n, hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  cast_bf16_kernel<<<opt_grid(n), OPT_THREADS, 0, stream>>>(x, y, n);
+  const int vec = (reinterpret_cast<uintptr_t>(x) % 16 == 0 && reinterpret_cast<uintptr_t>(y) % 8 == 0) ? 1 : 0;
+  const size_t threads = vec ? (n / 4 > 0 ? n / 4 : 1) : n;
+  cast_bf16_kernel<<<(unsigned)((threads + OPT_THREADS - 1) / OPT_THREADS), OPT_THREADS, 0, stream>>>(x, y, n, vec);
   return hipGetLastError();
 }

@@ -434,3 +434,18 @@ def test_row_split_trunk_on_fragment_ordered_weights_is_bitwise(cuda):
         for a, b in zip(*outs):
             assert torch.equal(a.view(torch.uint8) if a.dtype == torch.uint8 else a.view(torch.int16),
                                b.view(torch.uint8) if b.dtype == torch.uint8 else b.view(torch.int16)), base
+
+
+@pytest.mark.parametrize("n,off", [(1, 0), (3, 1), (1024, 0), (1000003, 0), (4097, 1), (65536, 2)])
+def test_cast_bf16_matches_torch_rounding(cuda, n, off):
+    """The comm-buffer cast of bf16 DP buckets (vector path when both ends are aligned, scalar path otherwise) rounds
+    exactly as torch's fp32 -> bf16 conversion."""
+    from actor_critic_algs_on_tensorflow_amd import _native
+    ops = _native.require()
+    g = torch.Generator(device="cpu").manual_seed(n + off)
+    x = (torch.randn(n + off + 3, generator=g) * 1e3).to(cuda)
+    x[::7] *= 1e-30
+    y = torch.zeros(n + off, dtype=torch.bfloat16, device=cuda)
+    ops.cast_bf16(x[off:off + n], y[off:])
+    torch.cuda.synchronize()
+    assert torch.equal(y[off:], x[off:off + n].to(torch.bfloat16))

@@ -1265,8 +1265,11 @@ __global__ void __launch_bounds__(256) mlp_wgrad_kernel(WgradArgs a) {
     }
     return;
   }
-  const int split = blockIdx.x % a.nsplit;
-  const int64_t* rec = a.items + (size_t)(blockIdx.x / a.nsplit) * 8;
+  // XCD-grouped item order (common.h xcd_remap): each XCD takes one contiguous range of the item table, whose
+  // neighbouring items (tiles of one layer) share their X / dP column blocks -- they meet in one L2
+  const int bid = xcd_remap((int)blockIdx.x, (int)gridDim.x - 1);
+  const int split = bid % a.nsplit;
+  const int64_t* rec = a.items + (size_t)(bid / a.nsplit) * 8;
   gcf32* X = P_<const float>(rec[0]);
   gcf32* P = P_<const float>(rec[1]);
   const int sx = (int)(rec[2] & 0xFFFFFFFF), sp = (int)(rec[2] >> 32);

@@ -1355,12 +1355,30 @@ __global__ void __launch_bounds__(256) mlp_epoch_gather_kernel(EpochGatherArgs a
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.n) return;
   const int64_t src = prp_index((uint32_t)i, (uint32_t)a.n, minibatch_key(a.seed, *a.uc, a.ep));
-  for (int c = 0; c < a.D; ++c) a.o_obs[(size_t)i * a.D + c] = a.obs[src * a.ld_obs + c];
-  for (int c = 0; c < a.aw; ++c) a.o_act[(size_t)i * a.aw + c] = a.act[src * a.aw + c];
-  a.o_logp[i] = a.logp[src];
-  a.o_adv[i] = a.adv[src];
-  a.o_ret[i] = a.ret[src];
-  if (a.v) a.o_v[i] = a.v[src];
+  // every load of a chunk issued before its stores (a load -> store loop per column waits out one round trip per
+  // column: the row's D + aw + 4 words were ~D + aw dependent round trips)
+  const float lp = a.logp[src], ad = a.adv[src], rt = a.ret[src], vv = a.v ? a.v[src] : 0.f;
+  constexpr int CH = 8;
+  for (int c0 = 0; c0 < a.D; c0 += CH) {
+    float x[CH];
+#pragma unroll
+    for (int u = 0; u < CH; ++u) x[u] = c0 + u < a.D ? a.obs[src * a.ld_obs + c0 + u] : 0.f;
+#pragma unroll
+    for (int u = 0; u < CH; ++u)
+      if (c0 + u < a.D) a.o_obs[(size_t)i * a.D + c0 + u] = x[u];
+  }
+  for (int c0 = 0; c0 < a.aw; c0 += CH) {
+    uint32_t w[CH];
+#pragma unroll
+    for (int u = 0; u < CH; ++u) w[u] = c0 + u < a.aw ? a.act[src * a.aw + c0 + u] : 0u;
+#pragma unroll
+    for (int u = 0; u < CH; ++u)
+      if (c0 + u < a.aw) a.o_act[(size_t)i * a.aw + c0 + u] = w[u];
+  }
+  a.o_logp[i] = lp;
+  a.o_adv[i] = ad;
+  a.o_ret[i] = rt;
+  if (a.v) a.o_v[i] = vv;
 }
 
 // The fragment copies F (every layer) and G (layers >= 1) of every W of the launched towers (common.h mlp_frag_f /

@@ -170,6 +170,7 @@ __device__ __forceinline__ float wave_sum_ref(float v) {
 
 // wave-aggregated episode statistics [sum_ret, count, sum_len] (one atomic per wave and field)
 __device__ __forceinline__ void add_ep_stats(float* ep_stats, bool active, bool done, float ret, float len) {
+  if (__builtin_amdgcn_ballot_w64(active && done) == 0) return;   // no episode ended in this wave (the usual step)
   float a = (active && done) ? ret : 0.f;
   float b = (active && done) ? 1.f : 0.f;
   float c = (active && done) ? len : 0.f;

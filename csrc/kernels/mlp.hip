@@ -1682,14 +1682,16 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_rollout_kernel(RolloutArgs a)
     }
     __syncthreads();
     stamp(step, 5);
-    if (tid < rows) {
+    // (the per-env log-prob / entropy sums run on wave 2, beside the env step of waves 0-1)
+    if (tid >= 128 && tid < 128 + rows) {
+      const int r = tid - 128;
       float lp = 0.f, H = 0.f;
       for (int j = 0; j < A; ++j) {
-        lp += s_hl[tid * MLP_MAXA + j];
+        lp += s_hl[r * MLP_MAXA + j];
         H += 0.5f + HALF_LOG_2PI + s_ls[j];
       }
-      a.logp[(size_t)step * a.N + row0 + tid] = lp;
-      a.ent[(size_t)step * a.N + row0 + tid] = H;
+      a.logp[(size_t)step * a.N + row0 + r] = lp;
+      a.ent[(size_t)step * a.N + row0 + r] = H;
     }
     // ---- env step: 32 lanes per env, lane r < 17 owns state row r (linear_step_kernel)
     {

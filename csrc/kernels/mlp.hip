@@ -1528,6 +1528,9 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_rollout_kernel(RolloutArgs a)
   __shared__ float s_er[ROLL_RB];
   __shared__ float s_ls[MLP_MAXA], s_sc[MLP_MAXA];
   __shared__ float s_hl[ROLL_RB * MLP_MAXA];
+  // the NEXT step's Box-Muller factors sqrt(-2 log u1) and cos(2 pi u2) (computed a step ahead, by two waves)
+  __shared__ float s_epa[ROLL_RB * MLP_MAXA], s_epb[ROLL_RB * MLP_MAXA];
+  __shared__ float s_els[MLP_MAXA], s_eils[MLP_MAXA];   // exp(log_std), exp(-log_std): step-invariant
   __shared__ int s_in[MLP_MAXL], s_out[MLP_MAXL], s_actc[MLP_MAXL];
   __shared__ int64_t s_wt[MLP_MAXL], s_b[MLP_MAXL];
   __shared__ float s_red[MLP_THREADS / 64 * 4 * 64];   // the layers' partial tiles (roll_layer_mfma)
@@ -1546,7 +1549,10 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_rollout_kernel(RolloutArgs a)
     s_b[tid] = T.b[tid];
   }
   if (tid < MLP_MAXA) {
-    s_ls[tid] = tid < A ? fminf(fmaxf(a.log_std[tid], -2.5f), 2.5f) : 0.f;
+    const float ls = tid < A ? fminf(fmaxf(a.log_std[tid], -2.5f), 2.5f) : 0.f;
+    s_ls[tid] = ls;
+    s_els[tid] = expf(ls);
+    s_eils[tid] = expf(-ls);
     s_sc[tid] = tid < A ? a.ac_scale[tid] : 0.f;
   }
   if (tid < ROLL_RB) {
@@ -1623,6 +1629,29 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_rollout_kernel(RolloutArgs a)
   roll_layer_load_w<L2>(w2, sm + s_wo[2], 132, s_out[2]);
   roll_layer_load_w<L3>(w3, sm + s_wo[3], 68, s_out[3]);
   auto bias_of = [&](int l, int ldw) { return sm + s_wo[l] + s_out[l] * ldw; };
+  // The policy noise of step t depends only on (seed, env counter, env id, component): waves 2 and 4 (idle during the
+  // env step) compute step t + 1's two Box-Muller factors while waves 0-1 step the envs -- wave 2 sqrt(-2 log u1),
+  // wave 4 cos(2 pi u2), multiplied in the head as before (bit-identical). The env counter advances by one per step
+  // (the env step's tg + 1), so a register copy of the key follows it.
+  const int nbase = tid < 256 ? 128 : 256;
+  const bool nz_owner = (tid >= 128 && tid < 128 + ROLL_RB * MLP_MAXA) || (tid >= 256 && tid < 256 + ROLL_RB * MLP_MAXA);
+  const bool nz_a = tid < 256;
+  const int nr = (tid - nbase) / MLP_MAXA, nj = (tid - nbase) % MLP_MAXA;
+  const bool nz_live = nz_owner && nr < rows && nj < A;
+  int64_t nkey = nz_live ? s_tg[nr] * ((int64_t)1 << a.key_shift) + s_ids[nr] : 0;
+  auto noise_ahead = [&]() {
+    if (nz_owner) {
+      float f = 0.f;
+      if (nj < A) {
+        if (nz_a) f = sqrtf(-2.0f * logf(uniform_open(a.policy_seed, nkey, 2 * nj)));
+        else f = cosf(TWO_PI * uniform_open(a.policy_seed, nkey, 2 * nj + 1));
+      }
+      (nz_a ? s_epa : s_epb)[nr * MLP_MAXA + nj] = f;
+      if (nz_live) nkey += (int64_t)1 << a.key_shift;
+    }
+  };
+  noise_ahead();
+  __syncthreads();
   // diagnostics only (stamps[255] == 1): the step loop runs the actor layers alone (no head, no env step)
   const bool layers_only = a.stamps && a.stamps[255] == 1;
   for (int step = 0; step < a.T; ++step) {
@@ -1668,13 +1697,11 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_rollout_kernel(RolloutArgs a)
       if (j < A) {
         const bool live = r < rows;
         const float* Yo = X + r * ldx;
-        const int64_t key = live ? s_tg[r] * ((int64_t)1 << a.key_shift) + s_ids[r] : 0;
         const float ls = s_ls[j];
         const float mu = tanhf(Yo[j]) * s_sc[j];
-        const float u1 = uniform_open(a.policy_seed, key, 2 * j), u2 = uniform_open(a.policy_seed, key, 2 * j + 1);
-        const float eps = sqrtf(-2.0f * logf(u1)) * cosf(TWO_PI * u2);
-        const float aj = mu + expf(ls) * eps;
-        const float zz = (aj - mu) * expf(-ls);
+        const float eps = s_epa[r * MLP_MAXA + j] * s_epb[r * MLP_MAXA + j];   // (noise_ahead: the previous step)
+        const float aj = mu + s_els[j] * eps;
+        const float zz = (aj - mu) * s_eils[j];
         s_hl[r * MLP_MAXA + j] = -0.5f * zz * zz - ls - HALF_LOG_2PI;
         s_act[r * MLP_MAXA + j] = aj;
         if (live) a.act[((size_t)step * a.N + row0 + r) * A + j] = aj;
@@ -1682,9 +1709,9 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_rollout_kernel(RolloutArgs a)
     }
     __syncthreads();
     stamp(step, 5);
-    // (the per-env log-prob / entropy sums run on wave 2, beside the env step of waves 0-1)
-    if (tid >= 128 && tid < 128 + rows) {
-      const int r = tid - 128;
+    // (the per-env log-prob / entropy sums run on wave 3, beside the env step of waves 0-1 and wave 2's noise)
+    if (tid >= 192 && tid < 192 + rows) {
+      const int r = tid - 192;
       float lp = 0.f, H = 0.f;
       for (int j = 0; j < A; ++j) {
         lp += s_hl[r * MLP_MAXA + j];
@@ -1693,6 +1720,7 @@ __global__ void __launch_bounds__(MLP_THREADS) mlp_rollout_kernel(RolloutArgs a)
       a.logp[(size_t)step * a.N + row0 + r] = lp;
       a.ent[(size_t)step * a.N + row0 + r] = H;
     }
+    noise_ahead();   // waves 2 and 4: step + 1's policy noise, beside the env step below
     // ---- env step: 32 lanes per env, lane r < 17 owns state row r (linear_step_kernel)
     {
       const int e = tid / LIN_LANES, r = tid % LIN_LANES;
